@@ -1,0 +1,192 @@
+#!/usr/bin/env python3
+"""bench.py -- composed frames/s of the MI355X scroll composer.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload p720]
+
+One process per GPU (torch.distributed.run for N > 1; RANK / LOCAL_RANK /
+WORLD_SIZE from the env).  Streams are independent, so each rank owns a static
+shard (its own streams; weak scaling, no collective in the data path; gloo is
+used only for the timing barrier / max-over-ranks).
+
+A step = one scroll_batch_compose over every stream of the rank:
+  workload p720 (BASELINE config 2): 256 streams x 1024 composed frames of
+  1280x720, offsets = SURVEY 8(d) synthetic scroll (speed 1+(s%8), phase
+  97 s mod 1440), resident in HBM before timing; output arenas in HBM are
+  rewound on device at every step (the bytes of a step are the product).
+Prints ONE JSON line (rank 0).  Also reports the dominant kernel's roofline
+(k_emit, HIP events on its launch stream) and the CPU oracle on host cores.
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(HERE, "h264-scroll-encoder_amd"))
+
+METRIC = "composed frames/sec (1280x720, 360x360 dyn) at 1/2/4/8 GPU; bit-exact vs CPU"
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
+NAL_DESC_BYTES = 32            # NalDesc read per NAL by k_emit
+
+WORKLOADS = {
+    "p720": dict(w=1280, h=720, streams=256, frames=1024,
+                 desc="BASELINE config 2: 256 concurrent 1280x720 streams, P-only "
+                      "(no dynamic rect), composer_write_scroll_frame semantics"),
+}
+
+
+def synthetic_offsets(first, nstreams, nframes, h):
+    import numpy as np
+    s = np.arange(first, first + nstreams, dtype=np.int64)[:, None]
+    i = np.arange(nframes, dtype=np.int64)[None, :]
+    p = (i * (1 + s % 8) + (97 * s) % (2 * h)) % (2 * h)
+    return np.where(p < h, p, 2 * h - p).astype(np.int32)
+
+
+def cpu_baseline(wl, threads):
+    """Oracle (C restatement, bit-exact to the reference) on host cores."""
+    repo_oracle = os.path.join(HERE, "oracle")
+    so = os.path.join(repo_oracle, "_build", "liboracle.so")
+    if not os.path.exists(so):
+        import subprocess
+        subprocess.run(["make", "-s", "-C", repo_oracle], check=True)
+    lib = ctypes.CDLL(so)
+    lib.or_bench_compose.restype = ctypes.c_double
+    nstreams, nframes = 256, 512
+    nbytes = ctypes.c_ulonglong()
+    fps = lib.or_bench_compose(nstreams, nframes, wl["w"], wl["h"], threads, 200,
+                               ctypes.byref(nbytes))
+    fps1 = lib.or_bench_compose(8, 512, wl["w"], wl["h"], 1, 100, ctypes.byref(nbytes))
+    return dict(value=round(fps, 1), unit="frames/s", cores=threads, kind="port",
+                sample=f"{nstreams} streams x {nframes} frames {wl['w']}x{wl['h']} (same "
+                       f"synthetic offsets), {threads} pthreads, oracle/scroll_oracle.c -O2",
+                single_core_fps=round(fps1, 1))
+
+
+def load_traffic(workload):
+    p = os.path.join(HERE, "profiles", f"traffic_{workload}.json")
+    if os.path.exists(p):
+        try:
+            return json.load(open(p))
+        except Exception:
+            return None
+    return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--workload", default="p720", choices=sorted(WORKLOADS))
+    ap.add_argument("--streams", type=int, default=0, help="override streams per GPU")
+    ap.add_argument("--frames", type=int, default=0, help="override frames per step")
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    args = ap.parse_args()
+
+    wl = dict(WORKLOADS[args.workload])
+    if args.streams:
+        wl["streams"] = args.streams
+    if args.frames:
+        wl["frames"] = args.frames
+
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    local = int(os.environ.get("LOCAL_RANK", 0))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("gloo")
+
+    import numpy as np
+    import torch
+    import h264scroll as hs
+
+    torch.cuda.set_device(local)
+    stream = torch.cuda.current_stream()
+    S, F, W, H = wl["streams"], wl["frames"], wl["w"], wl["h"]
+    first = rank * S                               # static contiguous shard
+    per_frame_bound = 2 * (64 + (W // 16) * (H // 16))
+    b = hs.Batch(S, F, F * per_frame_bound + (1 << 16), device=local)
+    for _ in range(S):
+        b.add_stream(hs.make_config(W, H))
+    b.set_offsets(synthetic_offsets(first, S, F, H))
+
+    def barrier():
+        torch.cuda.synchronize()
+        if dist:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        b.compose(F, stream=stream.cuda_stream, rewind=True)
+    barrier()
+    if b.sync() != 0:
+        raise RuntimeError(hs.last_error())
+    b.enable_timing(True)
+    b.kernel_stats(1)                               # reset accumulators
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        b.compose(F, stream=stream.cuda_stream, rewind=True)
+    barrier()
+    t1 = time.perf_counter()
+    if b.sync() != 0:
+        raise RuntimeError(hs.last_error())
+    emit_ms, n_emit = b.kernel_stats(1)
+    plan_ms, n_plan = b.kernel_stats(0)
+    step_bytes = b.last_bytes()                     # per step, all streams of this rank
+    step_nals = b.last_nals()
+    b.enable_timing(False)
+
+    el = t1 - t0
+    if dist:
+        t = torch.tensor([el], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    frames_total = S * F * args.steps * world
+    value = frames_total / el
+    ms_step = 1000.0 * el / args.steps
+
+    if rank == 0:
+        emit_avg_ms = emit_ms / max(n_emit, 1)
+        alg_bytes = step_bytes + NAL_DESC_BYTES * step_nals   # per k_emit launch
+        achieved = alg_bytes / (emit_avg_ms * 1e-3) / 1e9
+        traffic = load_traffic(args.workload)
+        out = {
+            "metric": METRIC,
+            "value": round(value, 1),
+            "unit": "frames/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_step, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic",
+            "config": {"workload": wl["desc"], "resolution": f"{W}x{H}",
+                       "streams_per_gpu": S, "frames_per_step": F,
+                       "parallelism": f"static stream shard x{world}, no RCCL"},
+            "bytes_per_frame": round(step_bytes / (S * F), 1),
+            "roofline": {"bound": "hbm", "kernel": "k_emit",
+                         "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": traffic.get("hbm_bytes_per_launch") if traffic else None,
+                         "alg_bytes_per_launch": alg_bytes,
+                         "emit_ms_avg": round(emit_avg_ms, 4),
+                         "plan_ms_avg": round(plan_ms / max(n_plan, 1), 4)},
+        }
+        if world == 1 and not args.no_cpu:
+            threads = min(16, os.cpu_count() or 1)
+            out["cpu_baseline"] = cpu_baseline(wl, threads)
+        print(json.dumps(out), flush=True)
+    b.close()
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,1045 @@
+/*
+ * scroll_kernels.hip -- MI355X (gfx950) engine of the many-stream scroll
+ * composer: plan kernel (per-stream state machine + exact NAL sizes + output
+ * offsets), emit kernel (random-access bit generation, 16 B per lane) and the
+ * host-side batch engine behind include/composer_batch.h.
+ *
+ * Reference hot path: src/composer.c:255-264 -> src/h264_writer.c:541-782 ->
+ * src/bitwriter.c -> src/nal.c:52-84.  See DESIGN.md for the data layout and
+ * the roofline of each kernel.
+ */
+#include <hip/hip_runtime.h>
+
+#include <stdarg.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <mutex>
+#include <vector>
+
+#include "engine.h"
+#include "scroll_device.h"
+
+using namespace scroll;
+
+static_assert(sizeof(DevStream) == 256, "DevStream must stay 256 B");
+static_assert(sizeof(NalDesc) == 32, "NalDesc must stay 32 B");
+
+namespace {
+
+constexpr int TILE = 32;          /* NAL units per wave tile in k_emit        */
+constexpr int EMIT_WAVES = 4;     /* waves per k_emit workgroup               */
+constexpr int PLAN_THREADS = 256;
+constexpr int PLAN_REWIND = 1 << 8;   /* k_plan flag: arena restarts at 0 */
+
+/* ---------------------------------------------------------------------- */
+/* helpers                                                                 */
+/* ---------------------------------------------------------------------- */
+__device__ inline uint64_t lanemask_lt()
+{
+    uint32_t lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+    return lane == 0 ? 0ull : (~0ull >> (64 - lane));
+}
+
+__device__ inline uint64_t wave_incl_scan(uint64_t v, int lane)
+{
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        uint64_t t = __shfl_up(v, d, 64);
+        if (lane >= d) v += t;
+    }
+    return v;
+}
+
+__device__ inline void wave_lds_sync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ inline NalCtx make_ctx(const int32_t *cfg, const int32_t *wo, const int32_t *wl,
+                                  const int32_t *wv, const NalDesc &d)
+{
+    NalCtx c;
+    c.w = cfg[0];
+    c.h = cfg[1];
+    c.log2_mfn = cfg[2];
+    c.poc_type = cfg[3];
+    c.log2_poc = cfg[4];
+    c.deblock = cfg[5];
+    c.kind = d.kind;
+    c.off = d.off;
+    c.frame_num = d.frame_num;
+    c.nwp = d.nwp;
+    c.wp_off = wo;
+    c.wp_lt = wl;
+    c.wp_valid = wv;
+    return c;
+}
+
+/* ---------------------------------------------------------------------- */
+/* k_plan: one workgroup per stream.                                       */
+/*  phase 1 (wave 0): composer_write_scroll_frame state machine over the   */
+/*          stream's offsets (src/composer.c:255-264, h264_writer.c:666-676,*/
+/*          :772-777) -> one NalDesc per NAL unit, frame_num per NAL.       */
+/*  phase 2 (all waves): exact size of every NAL (run layout, or the serial */
+/*          path when emulation prevention / long codes are possible), and  */
+/*          a block scan -> byte offset of every NAL in the stream arena.   */
+/* ---------------------------------------------------------------------- */
+__global__ __launch_bounds__(PLAN_THREADS) void k_plan(DevStream *__restrict__ st,
+                                                       const int32_t *__restrict__ offs,
+                                                       int ld_off, NalDesc *__restrict__ nal,
+                                                       int ld_nal, int nframes, int mode,
+                                                       int flags)
+{
+    const int s = blockIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    __shared__ int32_t s_cfg[8];
+    __shared__ int32_t s_wo[8], s_wl[8], s_wv[8];
+    __shared__ int32_t s_nnal, s_nwp_end, s_fn_end, s_nalwp;
+    __shared__ uint64_t s_wsum[PLAN_THREADS / 64];
+    __shared__ uint64_t s_carry;
+    __shared__ int32_t s_nslow;
+
+    DevStream *S = st + s;
+    if (tid < 8) {
+        s_wo[tid] = S->wp_off[tid];
+        s_wl[tid] = S->wp_lt[tid];
+        s_wv[tid] = S->wp_valid[tid];
+    }
+    if (tid == 0) {
+        s_cfg[0] = S->w; s_cfg[1] = S->h; s_cfg[2] = S->log2_mfn; s_cfg[3] = S->poc_type;
+        s_cfg[4] = S->log2_poc; s_cfg[5] = S->deblock; s_cfg[6] = S->frame_num; s_cfg[7] = S->nwp;
+        s_carry = 0;
+        s_nslow = 0;
+        if (flags & PLAN_REWIND) S->out_pos = 0;
+    }
+    const int F = nframes >= 0 ? nframes : S->frames;
+    NalDesc *N = nal + (size_t)s * ld_nal;
+    __syncthreads();
+    const uint64_t out0 = S->out_pos;
+
+    if (mode == SCROLL_PLAN_EXPLICIT) {
+        if (tid == 0) {
+            s_nnal = S->nnal;
+            s_nwp_end = s_cfg[7];
+            s_fn_end = s_cfg[6];
+            s_nalwp = 0;
+        }
+    } else if (wave == 0) {
+        /* waypoint table held in registers with static indices (no scratch) */
+        int wo[8], wl[8], wv[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            wo[k] = s_wo[k];
+            wl[k] = s_wl[k];
+            wv[k] = s_wv[k];
+        }
+        int n = s_cfg[7];
+        const int fn0 = s_cfg[6];
+        int nalc = 0, nalwp = 0;
+        const int32_t *O = offs + (size_t)s * ld_off;
+        for (int base = 0; base < F; base += 64) {
+            int i = base + lane;
+            bool valid = i < F;
+            int off = valid ? O[i] : 0;
+            bool cand = valid && off != 0 && (off % MVL) == 0;   /* h264_writer.c:667-668 */
+            uint64_t mask = __ballot(cand);
+            int my_n = n, has_wp = 0, wp_nb = 0;
+            while (mask) {
+                int jl = __ffsll((unsigned long long)mask) - 1;
+                mask &= mask - 1;
+                int offj = __shfl(off, jl, 64);
+                bool need = true;
+#pragma unroll
+                for (int k = 0; k < 8; ++k)                       /* :670-674 */
+                    if (k < n && wv[k] && wo[k] == offj) need = false;
+                if (need) {
+                    if (lane == jl) {
+                        has_wp = 1;
+                        wp_nb = n;
+                    }
+                    if (n < 8) {                                  /* :772-777 */
+#pragma unroll
+                        for (int k = 0; k < 8; ++k)
+                            if (k == n) {
+                                wo[k] = offj;
+                                wl[k] = 2 + n;
+                                wv[k] = 1;
+                            }
+                        n++;
+                    }
+                    if (lane >= jl) my_n = n;
+                }
+            }
+            uint64_t vmask = __ballot(valid), wmask = __ballot(has_wp != 0);
+            uint64_t lt = lanemask_lt();
+            if (mode == SCROLL_PLAN_COMPOSER) {
+                int first = nalc + __popcll(vmask & lt) + __popcll(wmask & lt);
+                if (valid) {
+                    if (has_wp) {
+                        NalDesc d{};
+                        d.kind = 1; d.off = off; d.frame_num = fn0 + first; d.nwp = (uint8_t)wp_nb;
+                        d.frame = (uint32_t)i;
+                        N[first] = d;
+                    }
+                    NalDesc d{};
+                    d.kind = 0; d.off = off; d.frame_num = fn0 + first + has_wp;
+                    d.nwp = (uint8_t)my_n; d.frame = (uint32_t)i;
+                    N[first + has_wp] = d;
+                }
+                nalc += __popcll(vmask) + __popcll(wmask);
+            } else {   /* experiment: waypoint NAL replaces the scroll NAL */
+                int idx = nalc + __popcll(vmask & lt);
+                if (valid) {
+                    NalDesc d{};
+                    d.kind = has_wp ? 1 : 0; d.off = off; d.frame_num = fn0 + idx;
+                    d.nwp = (uint8_t)(has_wp ? wp_nb : my_n); d.frame = (uint32_t)i;
+                    N[idx] = d;
+                }
+                nalc += __popcll(vmask);
+            }
+            nalwp += __popcll(wmask);
+        }
+        if (lane < 8) {
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
+                if (k == lane) {
+                    s_wo[k] = wo[k];
+                    s_wl[k] = wl[k];
+                    s_wv[k] = wv[k];
+                }
+        }
+        if (lane == 0) {
+            s_nnal = nalc;
+            s_nwp_end = n;
+            s_fn_end = fn0 + nalc;
+            s_nalwp = nalwp;
+        }
+    }
+    __syncthreads();
+
+    /* phase 2: sizes + offsets.  Every NAL reads the FINAL table: entries are
+     * only appended, and a NAL only looks at its first nwp entries. */
+    const int nnal = s_nnal;
+    for (int t = 0; t < nnal; t += PLAN_THREADS) {
+        int j = t + tid;
+        uint64_t sz = 0;
+        int slow = 0;
+        if (j < nnal) {
+            NalDesc d = N[j];
+            NalCtx c = make_ctx(s_cfg, s_wo, s_wl, s_wv, d);
+            uint32_t fsz = 0;
+            bool fast = !(flags & SCROLL_DEBUG_FORCE_SERIAL) && build_nal<false>(c, nullptr, &fsz);
+            if (fast) {
+                sz = fsz;
+            } else {
+                sz = serial_size(c);
+                slow = 1;
+            }
+        }
+        uint64_t inc = wave_incl_scan(sz, lane);
+        if (lane == 63) s_wsum[wave] = inc;
+        int ns = __popcll(__ballot(slow != 0));
+        if (lane == 0 && ns) atomicAdd(&s_nslow, ns);
+        __syncthreads();
+        uint64_t before = s_carry;
+        for (int w = 0; w < wave; ++w) before += s_wsum[w];
+        if (j < nnal) {
+            N[j].out_off = out0 + before + inc - sz;
+            N[j].size = (uint32_t)sz;
+            N[j].slow = (uint8_t)slow;
+        }
+        __syncthreads();
+        if (tid == 0) {
+            uint64_t tot = 0;
+            for (int w = 0; w < PLAN_THREADS / 64; ++w) tot += s_wsum[w];
+            s_carry += tot;
+        }
+        __syncthreads();
+    }
+
+    if (tid == 0) {
+        uint64_t total = s_carry;
+        S->n_slow = s_nslow;
+        if (out0 + total > S->out_cap) {
+            S->err |= SCROLL_DEVERR_OVERFLOW;   /* nothing committed, nothing emitted */
+            S->nnal = 0;
+            S->batch_bytes = 0;
+        } else {
+            S->out_pos = out0 + total;
+            S->batch_bytes = total;
+            S->nnal = nnal;
+            S->nal_wp = s_nalwp;
+            S->frame_num = s_fn_end;
+            S->nwp = s_nwp_end;
+            if (mode != SCROLL_PLAN_EXPLICIT) S->frames_written += F;
+        }
+    }
+    if (tid < 8 && mode != SCROLL_PLAN_EXPLICIT && out0 + s_carry <= S->out_cap) {
+        S->wp_off[tid] = s_wo[tid];
+        S->wp_lt[tid] = s_wl[tid];
+        S->wp_valid[tid] = s_wv[tid];
+    }
+}
+
+/* ---------------------------------------------------------------------- */
+/* k_emit: each wave owns TILE consecutive NAL units of one stream.         */
+/*  1. lane i builds the run layout of NAL t0+i in LDS (32 NALs at once).   */
+/*  2. the wave sweeps the tile's byte range in 16-byte aligned chunks;     */
+/*     each lane random-accesses 128 bits through the layouts (crossing NAL */
+/*     boundaries in-register) and issues one 16 B store.                   */
+/*  3. partial chunks at the tile ends use byte stores; NALs on the serial  */
+/*     path are written by their own lane.                                  */
+/* ---------------------------------------------------------------------- */
+__global__ __launch_bounds__(EMIT_WAVES * 64) void k_emit(const DevStream *__restrict__ st,
+                                                          const NalDesc *__restrict__ nal,
+                                                          int ld_nal, uint8_t *__restrict__ arena,
+                                                          uint64_t ld_arena, int flags)
+{
+    __shared__ Lay s_lay[EMIT_WAVES][TILE];
+    __shared__ uint32_t s_noff[EMIT_WAVES][TILE + 1];
+    __shared__ int32_t s_cfg[8], s_wo[8], s_wl[8], s_wv[8];
+    (void)flags;
+
+    const int s = blockIdx.y;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const DevStream *S = st + s;
+    if (tid < 8) {
+        s_wo[tid] = S->wp_off[tid];
+        s_wl[tid] = S->wp_lt[tid];
+        s_wv[tid] = S->wp_valid[tid];
+    }
+    if (tid == 0) {
+        s_cfg[0] = S->w; s_cfg[1] = S->h; s_cfg[2] = S->log2_mfn; s_cfg[3] = S->poc_type;
+        s_cfg[4] = S->log2_poc; s_cfg[5] = S->deblock;
+    }
+    __syncthreads();
+    const int nnal = S->nnal;
+    const int t0 = (blockIdx.x * EMIT_WAVES + wave) * TILE;
+    if (t0 >= nnal) return;
+    const int cnt = min(TILE, nnal - t0);
+    const NalDesc *D = nal + (size_t)s * ld_nal + t0;
+    Lay *L = s_lay[wave];
+    uint32_t *noff = s_noff[wave];
+    uint8_t *A = arena + (size_t)s * ld_arena;
+
+    const uint64_t B0 = D[0].out_off;
+    bool my_slow = false;
+    NalCtx my_ctx;
+    if (lane < cnt) {
+        NalDesc d = D[lane];
+        my_ctx = make_ctx(s_cfg, s_wo, s_wl, s_wv, d);
+        my_slow = d.slow != 0;
+        if (!my_slow) {
+            uint32_t sz;
+            build_nal<true>(my_ctx, &L[lane], &sz);
+        } else {
+            L[lane].nal_bits = d.size * 8u;   /* keeps tile_bits32 well-defined */
+            L[lane].used_bits = 0;
+            L[lane].hdr_bits = 0;
+        }
+        noff[lane] = (uint32_t)(d.out_off - B0);
+        if (lane == cnt - 1) noff[cnt] = (uint32_t)(d.out_off + d.size - B0);
+    }
+    const bool any_slow = __ballot(my_slow) != 0;
+    wave_lds_sync();
+
+    const uint64_t B1 = B0 + noff[cnt];
+    const uint64_t c0 = B0 >> 4, c1 = (B1 + 15) >> 4;
+    int j = 0;
+    for (uint64_t c = c0 + lane; c < c1; c += 64) {
+        const uint64_t p = c << 4;
+        const bool full = p >= B0 && p + 16 <= B1 && !any_slow;
+        if (full) {
+            uint32_t wv[4];
+            chunk_words(L, noff, cnt, j, (uint32_t)(p - B0), wv);
+            uint4 o;
+            o.x = __builtin_bswap32(wv[0]);
+            o.y = __builtin_bswap32(wv[1]);
+            o.z = __builtin_bswap32(wv[2]);
+            o.w = __builtin_bswap32(wv[3]);
+            *reinterpret_cast<uint4 *>(A + p) = o;
+        } else {
+            for (int k = 0; k < 16; ++k) {
+                uint64_t q = p + (uint64_t)k;
+                if (q < B0 || q >= B1) continue;
+                uint32_t rel = (uint32_t)(q - B0);
+                while (j + 1 < cnt && noff[j + 1] <= rel) j++;
+                if (D[j].slow) continue;
+                A[q] = (uint8_t)tile_byte(L, noff, cnt, j, rel);
+            }
+        }
+    }
+    if (my_slow) serial_write(my_ctx, A + D[lane].out_off);
+}
+
+/* ---------------------------------------------------------------------- */
+/* host engine                                                             */
+/* ---------------------------------------------------------------------- */
+thread_local char g_err[512];
+
+void set_err(const char *fmt, ...)
+{
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof(g_err), fmt, ap);
+    va_end(ap);
+}
+
+#define HIPCHK(x)                                                                  \
+    do {                                                                           \
+        hipError_t e_ = (x);                                                       \
+        if (e_ != hipSuccess) {                                                    \
+            set_err("%s failed: %s", #x, hipGetErrorString(e_));                   \
+            return SCROLL_ERR_HIP;                                                 \
+        }                                                                          \
+    } while (0)
+
+int usable_devices(std::vector<int> *ids)
+{
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) {
+        set_err("no HIP device visible (libh264scroll needs an MI355X / gfx950)");
+        return 0;
+    }
+    int ok = 0;
+    for (int i = 0; i < n; ++i) {
+        hipDeviceProp_t p;
+        if (hipGetDeviceProperties(&p, i) != hipSuccess) continue;
+        if (strncmp(p.gcnArchName, "gfx950", 6) == 0) {
+            ok++;
+            if (ids) ids->push_back(i);
+        }
+    }
+    if (!ok) set_err("no gfx950 device among %d HIP devices", n);
+    return ok;
+}
+
+int check_cfg(const ComposerConfig *c)
+{
+    if (c->log2_max_frame_num < 1 || c->log2_max_frame_num > 16 ||
+        (c->pic_order_cnt_type == 0 &&
+         (c->log2_max_pic_order_cnt_lsb < 1 || c->log2_max_pic_order_cnt_lsb > 16)) ||
+        c->num_waypoints < 0 || c->num_waypoints > MAX_WAYPOINTS || c->width < 0 ||
+        c->height < 0) {
+        set_err("unsupported ComposerConfig (log2 fields must be 1..16, num_waypoints 0..8)");
+        return SCROLL_ERR_CONFIG;
+    }
+    return SCROLL_OK;
+}
+
+void cfg_to_dev(const ComposerConfig *c, DevStream *d)
+{
+    d->w = c->width;
+    d->h = c->height;
+    d->log2_mfn = c->log2_max_frame_num;
+    d->poc_type = c->pic_order_cnt_type;
+    d->log2_poc = c->log2_max_pic_order_cnt_lsb;
+    d->deblock = c->deblocking_filter_control_present_flag;
+    d->frame_num = c->frame_num;
+    d->nwp = c->num_waypoints;
+    for (int i = 0; i < 8; ++i) {
+        d->wp_off[i] = c->waypoints[i].offset_px;
+        d->wp_lt[i] = c->waypoints[i].long_term_idx;
+        d->wp_valid[i] = c->waypoints[i].valid;
+    }
+}
+
+void dev_to_cfg(const DevStream *d, ComposerConfig *c)
+{
+    c->frame_num = d->frame_num;
+    c->num_waypoints = d->nwp;
+    for (int i = 0; i < 8; ++i) {
+        c->waypoints[i].offset_px = d->wp_off[i];
+        c->waypoints[i].long_term_idx = d->wp_lt[i];
+        c->waypoints[i].valid = d->wp_valid[i];
+    }
+}
+
+}  // namespace
+
+/* ======================================================================== */
+/* ScrollBatch                                                              */
+/* ======================================================================== */
+struct ScrollBatch {
+    int device = 0;
+    int mode = SCROLL_MODE_COMPOSER;
+    int max_streams = 0, max_frames = 0, nstreams = 0;
+    int debug = 0;
+    size_t arena_bytes = 0, ld_arena = 0;
+    int ld_nal = 0;
+    DevStream *d_st = nullptr;
+    DevStream *h_st = nullptr;
+    int32_t *d_off = nullptr;
+    NalDesc *d_nal = nullptr;
+    uint8_t *d_arena = nullptr;
+    hipStream_t own = nullptr;
+    hipStream_t last = nullptr;
+    hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
+    int timing = 0;
+    int timed_pending = 0;
+    float ms[2] = {0, 0};
+    std::vector<hipEvent_t> ring;      /* 3 events per timed compose, pending */
+    int ring_used = 0;
+    double acc_ms[2] = {0, 0};
+    int acc_n = 0;
+    int host_valid = 1;
+    int last_plan_mode = SCROLL_PLAN_COMPOSER;
+    int last_nframes = 0;
+    std::vector<NalDesc> nal_cache;
+    int nal_cache_valid = 0;
+};
+
+extern "C" {
+
+const char *scroll_last_error(void) { return g_err; }
+
+const char *scroll_version(void) { return "h264scroll-amd 0.1 (gfx950)"; }
+
+int scroll_device_count(void) { return usable_devices(nullptr); }
+
+int scroll_batch_create(ScrollBatch **out, const ScrollBatchDesc *desc)
+{
+    if (!out || !desc || desc->max_streams <= 0 || desc->max_frames <= 0 ||
+        desc->arena_bytes == 0 ||
+        (desc->mode != SCROLL_MODE_COMPOSER && desc->mode != SCROLL_MODE_EXPERIMENT)) {
+        set_err("scroll_batch_create: bad descriptor");
+        return SCROLL_ERR_ARG;
+    }
+    *out = nullptr;
+    std::vector<int> ids;
+    if (!usable_devices(&ids)) return SCROLL_ERR_NO_DEVICE;
+    int n = 0;
+    (void)hipGetDeviceCount(&n);
+    if (desc->device < 0 || desc->device >= n) {
+        set_err("scroll_batch_create: device %d out of range (%d visible)", desc->device, n);
+        return SCROLL_ERR_ARG;
+    }
+    bool ok = false;
+    for (int i : ids) ok |= (i == desc->device);
+    if (!ok) {
+        set_err("scroll_batch_create: device %d is not gfx950", desc->device);
+        return SCROLL_ERR_NO_DEVICE;
+    }
+    HIPCHK(hipSetDevice(desc->device));
+    ScrollBatch *b = new ScrollBatch();
+    b->device = desc->device;
+    b->mode = desc->mode;
+    b->max_streams = desc->max_streams;
+    b->max_frames = desc->max_frames;
+    b->arena_bytes = desc->arena_bytes;
+    b->ld_arena = (desc->arena_bytes + 255) & ~(size_t)255;
+    b->ld_nal = 2 * desc->max_frames;
+    size_t S = (size_t)desc->max_streams;
+    hipError_t e = hipSuccess;
+    if (e == hipSuccess) e = hipMalloc(&b->d_st, S * sizeof(DevStream));
+    if (e == hipSuccess) e = hipHostMalloc(&b->h_st, S * sizeof(DevStream), hipHostMallocDefault);
+    if (e == hipSuccess) e = hipMalloc(&b->d_off, S * (size_t)desc->max_frames * sizeof(int32_t));
+    if (e == hipSuccess) e = hipMalloc(&b->d_nal, S * (size_t)b->ld_nal * sizeof(NalDesc));
+    if (e == hipSuccess) e = hipMalloc(&b->d_arena, S * b->ld_arena);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&b->own, hipStreamNonBlocking);
+    for (int i = 0; i < 3 && e == hipSuccess; ++i) e = hipEventCreate(&b->ev[i]);
+    if (e == hipSuccess) e = hipMemset(b->d_st, 0, S * sizeof(DevStream));
+    if (e == hipSuccess) e = hipMemset(b->d_off, 0, S * (size_t)desc->max_frames * sizeof(int32_t));
+    if (e != hipSuccess) {
+        set_err("scroll_batch_create: %s", hipGetErrorString(e));
+        scroll_batch_destroy(b);
+        return e == hipErrorOutOfMemory ? SCROLL_ERR_OOM : SCROLL_ERR_HIP;
+    }
+    memset(b->h_st, 0, S * sizeof(DevStream));
+    b->last = b->own;
+    *out = b;
+    return SCROLL_OK;
+}
+
+void scroll_batch_destroy(ScrollBatch *b)
+{
+    if (!b) return;
+    (void)hipSetDevice(b->device);
+    if (b->own) (void)hipStreamSynchronize(b->own);
+    for (int i = 0; i < 3; ++i)
+        if (b->ev[i]) (void)hipEventDestroy(b->ev[i]);
+    for (hipEvent_t e : b->ring) (void)hipEventDestroy(e);
+    if (b->own) (void)hipStreamDestroy(b->own);
+    (void)hipFree(b->d_st);
+    (void)hipHostFree(b->h_st);
+    (void)hipFree(b->d_off);
+    (void)hipFree(b->d_nal);
+    (void)hipFree(b->d_arena);
+    delete b;
+}
+
+int scroll_batch_num_streams(const ScrollBatch *b) { return b ? b->nstreams : 0; }
+
+int scroll_batch_set_debug(ScrollBatch *b, int flags)
+{
+    if (!b) return SCROLL_ERR_ARG;
+    b->debug = flags;
+    return SCROLL_OK;
+}
+
+static int batch_host_sync(ScrollBatch *b)
+{
+    if (b->host_valid) return SCROLL_OK;
+    HIPCHK(hipSetDevice(b->device));
+    HIPCHK(hipStreamSynchronize(b->last));
+    HIPCHK(hipMemcpy(b->h_st, b->d_st, (size_t)b->nstreams * sizeof(DevStream),
+                     hipMemcpyDeviceToHost));
+    b->host_valid = 1;
+    return SCROLL_OK;
+}
+
+int scroll_batch_add_stream(ScrollBatch *b, const ComposerConfig *cfg)
+{
+    if (!b || !cfg) return SCROLL_ERR_ARG;
+    if (b->nstreams >= b->max_streams) {
+        set_err("scroll_batch_add_stream: batch full (%d streams)", b->max_streams);
+        return SCROLL_ERR_ARG;
+    }
+    int rc = check_cfg(cfg);
+    if (rc) return rc;
+    rc = batch_host_sync(b);
+    if (rc) return rc;
+    int s = b->nstreams;
+    DevStream *d = &b->h_st[s];
+    memset(d, 0, sizeof(*d));
+    cfg_to_dev(cfg, d);
+    d->out_pos = 0;
+    d->out_cap = b->arena_bytes;
+    HIPCHK(hipSetDevice(b->device));
+    HIPCHK(hipMemcpy(b->d_st + s, d, sizeof(DevStream), hipMemcpyHostToDevice));
+    b->nstreams++;
+    return s;
+}
+
+int scroll_batch_get_config(ScrollBatch *b, int s, ComposerConfig *cfg)
+{
+    if (!b || !cfg || s < 0 || s >= b->nstreams) return SCROLL_ERR_ARG;
+    int rc = batch_host_sync(b);
+    if (rc) return rc;
+    const DevStream *d = &b->h_st[s];
+    composer_config_init(cfg, d->w, d->h);
+    cfg->log2_max_frame_num = d->log2_mfn;
+    cfg->pic_order_cnt_type = d->poc_type;
+    cfg->log2_max_pic_order_cnt_lsb = d->log2_poc;
+    cfg->deblocking_filter_control_present_flag = d->deblock;
+    dev_to_cfg(d, cfg);
+    return SCROLL_OK;
+}
+
+int scroll_batch_set_config(ScrollBatch *b, int s, const ComposerConfig *cfg)
+{
+    if (!b || !cfg || s < 0 || s >= b->nstreams) return SCROLL_ERR_ARG;
+    int rc = check_cfg(cfg);
+    if (rc) return rc;
+    rc = batch_host_sync(b);
+    if (rc) return rc;
+    DevStream *d = &b->h_st[s];
+    cfg_to_dev(cfg, d);
+    HIPCHK(hipSetDevice(b->device));
+    HIPCHK(hipMemcpy(b->d_st + s, d, sizeof(DevStream), hipMemcpyHostToDevice));
+    return SCROLL_OK;
+}
+
+int scroll_batch_set_offsets(ScrollBatch *b, const int32_t *offsets, int nframes)
+{
+    if (!b || !offsets || nframes < 0 || nframes > b->max_frames) return SCROLL_ERR_ARG;
+    if (nframes == 0 || b->nstreams == 0) return SCROLL_OK;
+    HIPCHK(hipSetDevice(b->device));
+    HIPCHK(hipMemcpy2D(b->d_off, (size_t)b->max_frames * sizeof(int32_t), offsets,
+                       (size_t)nframes * sizeof(int32_t), (size_t)nframes * sizeof(int32_t),
+                       (size_t)b->nstreams, hipMemcpyHostToDevice));
+    return SCROLL_OK;
+}
+
+int32_t *scroll_batch_offsets_device(ScrollBatch *b) { return b ? b->d_off : nullptr; }
+
+static int ring_events(ScrollBatch *b, hipEvent_t **evs)
+{
+    if ((size_t)b->ring_used + 3 > b->ring.size()) {
+        if (b->ring.size() >= 3 * 256) {        /* bound: fold pending timings first */
+            HIPCHK(hipStreamSynchronize(b->last));
+            for (int i = 0; i < b->ring_used; i += 3) {
+                float a = 0, c = 0;
+                HIPCHK(hipEventElapsedTime(&a, b->ring[i], b->ring[i + 1]));
+                HIPCHK(hipEventElapsedTime(&c, b->ring[i + 1], b->ring[i + 2]));
+                b->acc_ms[0] += a;
+                b->acc_ms[1] += c;
+                b->acc_n++;
+            }
+            b->ring_used = 0;
+        } else {
+            for (int i = 0; i < 3; ++i) {
+                hipEvent_t e;
+                HIPCHK(hipEventCreate(&e));
+                b->ring.push_back(e);
+            }
+        }
+    }
+    *evs = &b->ring[b->ring_used];
+    b->ring_used += 3;
+    return SCROLL_OK;
+}
+
+static int launch(ScrollBatch *b, int nframes, int plan_mode, int nal_max, hipStream_t hs,
+                  int plan_flags = 0)
+{
+    int S = b->nstreams;
+    if (S == 0) return SCROLL_OK;
+    hipEvent_t *rev = nullptr;
+    if (b->timing) {
+        int rc = ring_events(b, &rev);
+        if (rc) return rc;
+        HIPCHK(hipEventRecord(b->ev[0], hs));
+        HIPCHK(hipEventRecord(rev[0], hs));
+    }
+    hipLaunchKernelGGL(k_plan, dim3(S), dim3(PLAN_THREADS), 0, hs, b->d_st, b->d_off,
+                       b->max_frames, b->d_nal, b->ld_nal, nframes, plan_mode,
+                       b->debug | plan_flags);
+    HIPCHK(hipGetLastError());
+    if (b->timing) {
+        HIPCHK(hipEventRecord(b->ev[1], hs));
+        HIPCHK(hipEventRecord(rev[1], hs));
+    }
+    int per_wg = EMIT_WAVES * TILE;
+    int gx = (nal_max + per_wg - 1) / per_wg;
+    if (gx > 0) {
+        hipLaunchKernelGGL(k_emit, dim3(gx, S), dim3(EMIT_WAVES * 64), 0, hs, b->d_st, b->d_nal,
+                           b->ld_nal, b->d_arena, (uint64_t)b->ld_arena, b->debug);
+        HIPCHK(hipGetLastError());
+    }
+    if (b->timing) {
+        HIPCHK(hipEventRecord(b->ev[2], hs));
+        HIPCHK(hipEventRecord(rev[2], hs));
+        b->timed_pending = 1;
+    }
+    b->host_valid = 0;
+    b->nal_cache_valid = 0;
+    b->last = hs;
+    return SCROLL_OK;
+}
+
+int scroll_batch_compose(ScrollBatch *b, int nframes, void *hip_stream)
+{
+    return scroll_batch_compose_ex(b, nframes, hip_stream, 0);
+}
+
+int scroll_batch_compose_ex(ScrollBatch *b, int nframes, void *hip_stream, int flags)
+{
+    if (!b || nframes < 0 || nframes > b->max_frames) {
+        set_err("scroll_batch_compose: nframes %d out of range", nframes);
+        return SCROLL_ERR_ARG;
+    }
+    HIPCHK(hipSetDevice(b->device));
+    hipStream_t hs = hip_stream ? (hipStream_t)hip_stream : b->own;
+    int plan = b->mode == SCROLL_MODE_EXPERIMENT ? SCROLL_PLAN_EXPERIMENT : SCROLL_PLAN_COMPOSER;
+    int nal_max = plan == SCROLL_PLAN_COMPOSER ? 2 * nframes : nframes;
+    b->last_plan_mode = plan;
+    b->last_nframes = nframes;
+    return launch(b, nframes, plan, nal_max, hs,
+                  (flags & SCROLL_COMPOSE_REWIND) ? PLAN_REWIND : 0);
+}
+
+int scroll_batch_sync(ScrollBatch *b)
+{
+    if (!b) return SCROLL_ERR_ARG;
+    int rc = batch_host_sync(b);
+    if (rc) return rc;
+    if (b->timed_pending) {
+        HIPCHK(hipEventElapsedTime(&b->ms[0], b->ev[0], b->ev[1]));
+        HIPCHK(hipEventElapsedTime(&b->ms[1], b->ev[1], b->ev[2]));
+        b->timed_pending = 0;
+    }
+    for (int s = 0; s < b->nstreams; ++s) {
+        if (b->h_st[s].err & SCROLL_DEVERR_OVERFLOW) {
+            set_err("stream %d: output arena overflow (%llu + batch > %llu bytes)", s,
+                    (unsigned long long)b->h_st[s].out_pos,
+                    (unsigned long long)b->h_st[s].out_cap);
+            b->h_st[s].err = 0;
+            (void)hipMemcpy(&b->d_st[s].err, &b->h_st[s].err, sizeof(int32_t),
+                            hipMemcpyHostToDevice);
+            return SCROLL_ERR_OVERFLOW;
+        }
+    }
+    return SCROLL_OK;
+}
+
+size_t scroll_batch_output_size(ScrollBatch *b, int s)
+{
+    if (!b || s < 0 || s >= b->nstreams || batch_host_sync(b)) return 0;
+    return (size_t)b->h_st[s].out_pos;
+}
+
+int scroll_batch_copy_output(ScrollBatch *b, int s, size_t from, uint8_t *dst, size_t n)
+{
+    if (!b || s < 0 || s >= b->nstreams || (!dst && n)) return SCROLL_ERR_ARG;
+    int rc = batch_host_sync(b);
+    if (rc) return rc;
+    if (from + n > b->h_st[s].out_pos) {
+        set_err("scroll_batch_copy_output: range beyond stream output");
+        return SCROLL_ERR_ARG;
+    }
+    if (n == 0) return SCROLL_OK;
+    HIPCHK(hipSetDevice(b->device));
+    HIPCHK(hipMemcpy(dst, b->d_arena + (size_t)s * b->ld_arena + from, n, hipMemcpyDeviceToHost));
+    return SCROLL_OK;
+}
+
+const uint8_t *scroll_batch_output_device(ScrollBatch *b, int s)
+{
+    if (!b || s < 0 || s >= b->nstreams) return nullptr;
+    return b->d_arena + (size_t)s * b->ld_arena;
+}
+
+int scroll_batch_reset_output(ScrollBatch *b)
+{
+    if (!b) return SCROLL_ERR_ARG;
+    int rc = batch_host_sync(b);
+    if (rc) return rc;
+    for (int s = 0; s < b->nstreams; ++s) b->h_st[s].out_pos = 0;
+    HIPCHK(hipSetDevice(b->device));
+    HIPCHK(hipMemcpy(b->d_st, b->h_st, (size_t)b->nstreams * sizeof(DevStream),
+                     hipMemcpyHostToDevice));
+    return SCROLL_OK;
+}
+
+static int load_nals(ScrollBatch *b)
+{
+    if (b->nal_cache_valid) return SCROLL_OK;
+    int rc = batch_host_sync(b);
+    if (rc) return rc;
+    b->nal_cache.resize((size_t)b->nstreams * b->ld_nal);
+    HIPCHK(hipMemcpy(b->nal_cache.data(), b->d_nal, b->nal_cache.size() * sizeof(NalDesc),
+                     hipMemcpyDeviceToHost));
+    b->nal_cache_valid = 1;
+    return SCROLL_OK;
+}
+
+int scroll_batch_nal_count(ScrollBatch *b, int s)
+{
+    if (!b || s < 0 || s >= b->nstreams) return SCROLL_ERR_ARG;
+    int rc = batch_host_sync(b);
+    if (rc) return rc;
+    return b->h_st[s].nnal;
+}
+
+int scroll_batch_nal_info(ScrollBatch *b, int s, int i, int *kind, int *offset_px,
+                          uint32_t *size, int *slow)
+{
+    if (!b || s < 0 || s >= b->nstreams) return SCROLL_ERR_ARG;
+    int rc = load_nals(b);
+    if (rc) return rc;
+    if (i < 0 || i >= b->h_st[s].nnal) return SCROLL_ERR_ARG;
+    const NalDesc &d = b->nal_cache[(size_t)s * b->ld_nal + i];
+    if (kind) *kind = d.kind;
+    if (offset_px) *offset_px = d.off;
+    if (size) *size = d.size;
+    if (slow) *slow = d.slow;
+    return SCROLL_OK;
+}
+
+int scroll_batch_kernel_stats(ScrollBatch *b, int which, double *total_ms, int *count)
+{
+    if (!b || which < 0 || which > 1) return SCROLL_ERR_ARG;
+    int rc = batch_host_sync(b);
+    if (rc) return rc;
+    HIPCHK(hipStreamSynchronize(b->last));
+    for (int i = 0; i < b->ring_used; i += 3) {
+        float a = 0, c = 0;
+        HIPCHK(hipEventElapsedTime(&a, b->ring[i], b->ring[i + 1]));
+        HIPCHK(hipEventElapsedTime(&c, b->ring[i + 1], b->ring[i + 2]));
+        b->acc_ms[0] += a;
+        b->acc_ms[1] += c;
+        b->acc_n++;
+    }
+    b->ring_used = 0;
+    if (total_ms) *total_ms = b->acc_ms[which];
+    if (count) *count = b->acc_n;
+    b->acc_ms[0] = b->acc_ms[1] = 0;
+    b->acc_n = 0;
+    return SCROLL_OK;
+}
+
+unsigned long long scroll_batch_last_bytes(ScrollBatch *b)
+{
+    if (!b || batch_host_sync(b)) return 0;
+    unsigned long long t = 0;
+    for (int s = 0; s < b->nstreams; ++s) t += b->h_st[s].batch_bytes;
+    return t;
+}
+
+long long scroll_batch_last_nals(ScrollBatch *b)
+{
+    if (!b || batch_host_sync(b)) return -1;
+    long long t = 0;
+    for (int s = 0; s < b->nstreams; ++s) t += b->h_st[s].nnal;
+    return t;
+}
+
+int scroll_batch_enable_timing(ScrollBatch *b, int on)
+{
+    if (!b) return SCROLL_ERR_ARG;
+    b->timing = on;
+    return SCROLL_OK;
+}
+
+float scroll_batch_kernel_ms(ScrollBatch *b, int which)
+{
+    if (!b || which < 0 || which > 1) return -1.0f;
+    if (batch_host_sync(b)) return -1.0f;
+    if (b->timed_pending) {
+        if (hipEventElapsedTime(&b->ms[0], b->ev[0], b->ev[1]) != hipSuccess) return -1.0f;
+        if (hipEventElapsedTime(&b->ms[1], b->ev[1], b->ev[2]) != hipSuccess) return -1.0f;
+        b->timed_pending = 0;
+    }
+    return b->ms[which];
+}
+
+/* ======================================================================== */
+/* synchronous helpers for the drop-in entry points (engine.h)              */
+/* ======================================================================== */
+static std::mutex g_mu;
+
+struct TempBatch {
+    ScrollBatch *b = nullptr;
+    int streams = 0, frames = 0;
+    size_t arena = 0;
+    int mode = -1;
+};
+static TempBatch g_tmp;
+
+static int temp_batch(int streams, int frames, size_t arena, int mode, ScrollBatch **out)
+{
+    TempBatch &t = g_tmp;
+    if (!t.b || t.streams < streams || t.frames < frames || t.arena < arena || t.mode != mode) {
+        if (t.b) scroll_batch_destroy(t.b);
+        t.b = nullptr;
+        ScrollBatchDesc d;
+        d.device = 0;
+        std::vector<int> ids;
+        if (!usable_devices(&ids)) return SCROLL_ERR_NO_DEVICE;
+        d.device = ids[0];
+        d.max_streams = streams > t.streams ? streams : t.streams;
+        d.max_frames = frames > t.frames ? frames : t.frames;
+        d.arena_bytes = arena > t.arena ? arena : t.arena;
+        d.mode = mode;
+        int rc = scroll_batch_create(&t.b, &d);
+        if (rc) return rc;
+        t.streams = d.max_streams;
+        t.frames = d.max_frames;
+        t.arena = d.arena_bytes;
+        t.mode = mode;
+    }
+    t.b->nstreams = 0;
+    t.b->host_valid = 1;
+    *out = t.b;
+    return SCROLL_OK;
+}
+
+static size_t round_arena(size_t n)
+{
+    size_t a = 1u << 20;
+    while (a < n) a <<= 1;
+    return a;
+}
+
+int scroll_engine_write_nals(const ComposerConfig *cfg, const NalDesc *nals, int n,
+                             uint8_t *dst, size_t cap, size_t *written)
+{
+    std::lock_guard<std::mutex> lk(g_mu);
+    *written = 0;
+    int rc = check_cfg(cfg);
+    if (rc) return rc;
+    ScrollBatch *b;
+    rc = temp_batch(1, n, round_arena(cap), SCROLL_MODE_COMPOSER, &b);
+    if (rc) return rc;
+    DevStream *d = &b->h_st[0];
+    memset(d, 0, sizeof(*d));
+    cfg_to_dev(cfg, d);
+    d->out_pos = 0;
+    d->out_cap = cap;
+    d->nnal = n;
+    b->nstreams = 1;
+    HIPCHK(hipSetDevice(b->device));
+    HIPCHK(hipMemcpyAsync(b->d_st, d, sizeof(DevStream), hipMemcpyHostToDevice, b->own));
+    HIPCHK(hipMemcpyAsync(b->d_nal, nals, (size_t)n * sizeof(NalDesc), hipMemcpyHostToDevice,
+                          b->own));
+    rc = launch(b, 0, SCROLL_PLAN_EXPLICIT, n, b->own);
+    if (rc) return rc;
+    rc = scroll_batch_sync(b);
+    if (rc) return rc;
+    size_t tot = (size_t)b->h_st[0].out_pos;
+    HIPCHK(hipMemcpy(dst, b->d_arena, tot, hipMemcpyDeviceToHost));
+    *written = tot;
+    return SCROLL_OK;
+}
+
+int scroll_engine_compose(ComposerConfig *const *cfgs, const int *const *offs, const int *frames,
+                          int nstreams, int mode, uint8_t *const *dsts, const size_t *caps,
+                          size_t *written, int **wp_offsets_out)
+{
+    std::lock_guard<std::mutex> lk(g_mu);
+    int fmax = 0;
+    size_t cmax = 0;
+    for (int i = 0; i < nstreams; ++i) {
+        written[i] = 0;
+        int rc = check_cfg(cfgs[i]);
+        if (rc) return rc;
+        if (frames[i] > fmax) fmax = frames[i];
+        if (caps[i] > cmax) cmax = caps[i];
+    }
+    if (nstreams == 0 || fmax == 0) return SCROLL_OK;
+    ScrollBatch *b;
+    int rc = temp_batch(nstreams, fmax, round_arena(cmax), mode, &b);
+    if (rc) return rc;
+    std::vector<int32_t> off((size_t)nstreams * fmax, 0);
+    for (int i = 0; i < nstreams; ++i) {
+        DevStream *d = &b->h_st[i];
+        memset(d, 0, sizeof(*d));
+        cfg_to_dev(cfgs[i], d);
+        d->out_pos = 0;
+        d->out_cap = caps[i];
+        d->frames = frames[i];
+        memcpy(&off[(size_t)i * fmax], offs[i], (size_t)frames[i] * sizeof(int32_t));
+    }
+    b->nstreams = nstreams;
+    HIPCHK(hipSetDevice(b->device));
+    HIPCHK(hipMemcpyAsync(b->d_st, b->h_st, (size_t)nstreams * sizeof(DevStream),
+                          hipMemcpyHostToDevice, b->own));
+    HIPCHK(hipMemcpy2DAsync(b->d_off, (size_t)b->max_frames * sizeof(int32_t), off.data(),
+                            (size_t)fmax * sizeof(int32_t), (size_t)fmax * sizeof(int32_t),
+                            (size_t)nstreams, hipMemcpyHostToDevice, b->own));
+    int plan = mode == SCROLL_MODE_EXPERIMENT ? SCROLL_PLAN_EXPERIMENT : SCROLL_PLAN_COMPOSER;
+    rc = launch(b, -1, plan, plan == SCROLL_PLAN_COMPOSER ? 2 * fmax : fmax, b->own);
+    if (rc) return rc;
+    rc = scroll_batch_sync(b);
+    if (rc) return rc;
+    if (wp_offsets_out) {
+        rc = load_nals(b);
+        if (rc) return rc;
+    }
+    for (int i = 0; i < nstreams; ++i) {
+        size_t tot = (size_t)b->h_st[i].out_pos;
+        if (tot) {
+            HIPCHK(hipMemcpy(dsts[i], b->d_arena + (size_t)i * b->ld_arena, tot,
+                             hipMemcpyDeviceToHost));
+        }
+        written[i] = tot;
+        dev_to_cfg(&b->h_st[i], cfgs[i]);
+        if (wp_offsets_out && wp_offsets_out[i]) {
+            int k = 0;
+            for (int j = 0; j < b->h_st[i].nnal; ++j) {
+                const NalDesc &nd = b->nal_cache[(size_t)i * b->ld_nal + j];
+                if (nd.kind == 1) wp_offsets_out[i][k++] = nd.off;
+            }
+            wp_offsets_out[i][k] = -1;
+        }
+    }
+    return SCROLL_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,360 @@
+"""ctypes binding of libh264scroll.so (the C ABI in include/*.h).
+
+Python is only the test/bench harness here: the product is the C-ABI
+library.  This module loads lib/libh264scroll.so from this directory and
+raises immediately if it is missing -- there is no Python or CPU fallback.
+
+Mirrors the reference interface names (include/composer.h, h264_writer.h,
+nal.h, bitwriter.h, nal_parser.h) plus the additive batch API of
+include/composer_batch.h.
+"""
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libh264scroll.so")
+
+SCROLL_OK = 0
+SCROLL_ERR_NO_DEVICE = -1
+SCROLL_ERR_ARG = -2
+SCROLL_ERR_OOM = -3
+SCROLL_ERR_OVERFLOW = -4
+SCROLL_ERR_HIP = -5
+SCROLL_ERR_CONFIG = -6
+SCROLL_MODE_COMPOSER = 0
+SCROLL_MODE_EXPERIMENT = 1
+SCROLL_DEBUG_FORCE_SERIAL = 1
+SCROLL_COMPOSE_REWIND = 1
+MAX_WAYPOINTS = 8
+MV_LIMIT_PX = 496
+
+
+class WaypointInfo(ctypes.Structure):
+    _fields_ = [("offset_px", ctypes.c_int), ("long_term_idx", ctypes.c_int),
+                ("valid", ctypes.c_int)]
+
+
+class ComposerConfig(ctypes.Structure):
+    """include/h264_writer.h ComposerConfig (reference :37-59)."""
+    _fields_ = [("width", ctypes.c_int), ("height", ctypes.c_int),
+                ("mb_width", ctypes.c_int), ("mb_height", ctypes.c_int),
+                ("log2_max_frame_num", ctypes.c_int), ("pic_order_cnt_type", ctypes.c_int),
+                ("log2_max_pic_order_cnt_lsb", ctypes.c_int),
+                ("num_ref_idx_l0_default_minus1", ctypes.c_int),
+                ("deblocking_filter_control_present_flag", ctypes.c_int),
+                ("frame_num", ctypes.c_int), ("idr_pic_id", ctypes.c_int),
+                ("waypoints", WaypointInfo * MAX_WAYPOINTS), ("num_waypoints", ctypes.c_int)]
+
+
+class NALWriter(ctypes.Structure):
+    _fields_ = [("output", ctypes.POINTER(ctypes.c_uint8)), ("output_capacity", ctypes.c_size_t),
+                ("output_pos", ctypes.c_size_t), ("rbsp", ctypes.POINTER(ctypes.c_uint8)),
+                ("rbsp_capacity", ctypes.c_size_t)]
+
+
+class BitWriter(ctypes.Structure):
+    _fields_ = [("buffer", ctypes.POINTER(ctypes.c_uint8)), ("capacity", ctypes.c_size_t),
+                ("byte_pos", ctypes.c_size_t), ("bit_pos", ctypes.c_int),
+                ("current_byte", ctypes.c_uint8)]
+
+
+class BitReader(ctypes.Structure):
+    _fields_ = [("buffer", ctypes.POINTER(ctypes.c_uint8)), ("size", ctypes.c_size_t),
+                ("byte_pos", ctypes.c_size_t), ("bit_pos", ctypes.c_int)]
+
+
+class NALUnit(ctypes.Structure):
+    _fields_ = [("nal_ref_idc", ctypes.c_int), ("nal_unit_type", ctypes.c_int),
+                ("data", ctypes.POINTER(ctypes.c_uint8)), ("size", ctypes.c_size_t),
+                ("rbsp_size", ctypes.c_size_t)]
+
+
+class NALParser(ctypes.Structure):
+    _fields_ = [("data", ctypes.POINTER(ctypes.c_uint8)), ("size", ctypes.c_size_t),
+                ("pos", ctypes.c_size_t)]
+
+
+class Composer(ctypes.Structure):
+    """include/composer.h Composer (reference :23-49), caller-allocated."""
+    _fields_ = [("cfg", ComposerConfig), ("parse_cfg", ComposerConfig),
+                ("ref_a_rbsp", ctypes.c_void_p), ("ref_a_size", ctypes.c_size_t),
+                ("ref_b_rbsp", ctypes.c_void_p), ("ref_b_size", ctypes.c_size_t),
+                ("orig_sps", ctypes.c_void_p), ("orig_sps_size", ctypes.c_size_t),
+                ("orig_pps", ctypes.c_void_p), ("orig_pps_size", ctypes.c_size_t),
+                ("nw", NALWriter), ("output_buffer", ctypes.c_void_p),
+                ("output_capacity", ctypes.c_size_t), ("rbsp_temp", ctypes.c_void_p),
+                ("rbsp_capacity", ctypes.c_size_t), ("frames_written", ctypes.c_int)]
+
+
+class ScrollBatchDesc(ctypes.Structure):
+    _fields_ = [("device", ctypes.c_int), ("max_streams", ctypes.c_int),
+                ("max_frames", ctypes.c_int), ("arena_bytes", ctypes.c_size_t),
+                ("mode", ctypes.c_int)]
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"{LIB_PATH} not built: run `make -C h264-scroll-encoder_amd` "
+                          "(there is no fallback implementation)")
+    lib = ctypes.CDLL(LIB_PATH)
+    P = ctypes.POINTER
+    u8p = P(ctypes.c_uint8)
+    sig = {
+        "scroll_last_error": (ctypes.c_char_p, []),
+        "scroll_device_count": (ctypes.c_int, []),
+        "scroll_version": (ctypes.c_char_p, []),
+        "scroll_batch_create": (ctypes.c_int, [P(ctypes.c_void_p), P(ScrollBatchDesc)]),
+        "scroll_batch_destroy": (None, [ctypes.c_void_p]),
+        "scroll_batch_add_stream": (ctypes.c_int, [ctypes.c_void_p, P(ComposerConfig)]),
+        "scroll_batch_num_streams": (ctypes.c_int, [ctypes.c_void_p]),
+        "scroll_batch_set_debug": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+        "scroll_batch_set_offsets": (ctypes.c_int, [ctypes.c_void_p, P(ctypes.c_int32),
+                                                    ctypes.c_int]),
+        "scroll_batch_offsets_device": (ctypes.c_void_p, [ctypes.c_void_p]),
+        "scroll_batch_compose": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]),
+        "scroll_batch_sync": (ctypes.c_int, [ctypes.c_void_p]),
+        "scroll_batch_compose_ex": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
+                                                   ctypes.c_int]),
+        "scroll_batch_kernel_stats": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int,
+                                                     P(ctypes.c_double), P(ctypes.c_int)]),
+        "scroll_batch_last_bytes": (ctypes.c_ulonglong, [ctypes.c_void_p]),
+        "scroll_batch_last_nals": (ctypes.c_longlong, [ctypes.c_void_p]),
+        "scroll_batch_get_config": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int,
+                                                   P(ComposerConfig)]),
+        "scroll_batch_set_config": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int,
+                                                   P(ComposerConfig)]),
+        "scroll_batch_output_size": (ctypes.c_size_t, [ctypes.c_void_p, ctypes.c_int]),
+        "scroll_batch_copy_output": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int,
+                                                    ctypes.c_size_t, u8p, ctypes.c_size_t]),
+        "scroll_batch_output_device": (ctypes.c_void_p, [ctypes.c_void_p, ctypes.c_int]),
+        "scroll_batch_reset_output": (ctypes.c_int, [ctypes.c_void_p]),
+        "scroll_batch_nal_count": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+        "scroll_batch_nal_info": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                                 P(ctypes.c_int), P(ctypes.c_int),
+                                                 P(ctypes.c_uint32), P(ctypes.c_int)]),
+        "scroll_batch_enable_timing": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+        "scroll_batch_kernel_ms": (ctypes.c_float, [ctypes.c_void_p, ctypes.c_int]),
+        "composer_batch_write_scroll_frames": (ctypes.c_int, [P(P(Composer)), P(ctypes.c_int),
+                                                              ctypes.c_int, ctypes.c_int]),
+        "composer_flush": (ctypes.c_int, [P(Composer)]),
+        # reference ABI
+        "composer_init": (ctypes.c_int, [P(Composer), ctypes.c_char_p, ctypes.c_char_p]),
+        "composer_get_width": (ctypes.c_int, [P(Composer)]),
+        "composer_get_height": (ctypes.c_int, [P(Composer)]),
+        "composer_write_header": (None, [P(Composer)]),
+        "composer_write_scroll_frame": (None, [P(Composer), ctypes.c_int]),
+        "composer_get_output_size": (ctypes.c_size_t, [P(Composer)]),
+        "composer_get_output": (u8p, [P(Composer)]),
+        "composer_write_to_file": (ctypes.c_int, [P(Composer), ctypes.c_char_p]),
+        "composer_finish": (None, [P(Composer)]),
+        "composer_config_init": (None, [P(ComposerConfig), ctypes.c_int, ctypes.c_int]),
+        "composer_config_set_sps_params": (None, [P(ComposerConfig), ctypes.c_int, ctypes.c_int,
+                                                  ctypes.c_int]),
+        "composer_config_set_pps_params": (None, [P(ComposerConfig), ctypes.c_int,
+                                                  ctypes.c_int]),
+        "h264_generate_sps": (ctypes.c_size_t, [u8p, ctypes.c_size_t, ctypes.c_int,
+                                                ctypes.c_int]),
+        "h264_generate_pps": (ctypes.c_size_t, [u8p, ctypes.c_size_t]),
+        "h264_rewrite_idr_frame": (ctypes.c_size_t, [P(NALWriter), P(ComposerConfig),
+                                                     P(ComposerConfig), u8p, ctypes.c_size_t]),
+        "h264_rewrite_as_non_idr_i_frame": (ctypes.c_size_t, [P(NALWriter), P(ComposerConfig),
+                                                              P(ComposerConfig), u8p,
+                                                              ctypes.c_size_t, ctypes.c_int]),
+        "h264_write_scroll_p_frame": (ctypes.c_size_t, [P(NALWriter), P(ComposerConfig),
+                                                        ctypes.c_int]),
+        "h264_needs_waypoint": (ctypes.c_int, [P(ComposerConfig), ctypes.c_int]),
+        "h264_write_waypoint_p_frame": (ctypes.c_size_t, [P(NALWriter), P(ComposerConfig),
+                                                          ctypes.c_int]),
+        "nal_writer_init": (None, [P(NALWriter), u8p, ctypes.c_size_t, u8p, ctypes.c_size_t]),
+        "nal_write_unit": (ctypes.c_size_t, [P(NALWriter), ctypes.c_int, ctypes.c_int, u8p,
+                                             ctypes.c_size_t, ctypes.c_int]),
+        "nal_writer_get_size": (ctypes.c_size_t, [P(NALWriter)]),
+        "nal_writer_get_output": (u8p, [P(NALWriter)]),
+        "rbsp_to_ebsp": (ctypes.c_size_t, [u8p, ctypes.c_size_t, u8p, ctypes.c_size_t]),
+        "nal_parser_init": (None, [P(NALParser), u8p, ctypes.c_size_t]),
+        "nal_parser_next": (ctypes.c_int, [P(NALParser), P(NALUnit)]),
+        "ebsp_to_rbsp": (ctypes.c_size_t, [u8p, u8p, ctypes.c_size_t]),
+        "parse_sps": (ctypes.c_int, [u8p, ctypes.c_size_t] + [P(ctypes.c_int)] * 5),
+        "parse_pps": (ctypes.c_int, [u8p, ctypes.c_size_t] + [P(ctypes.c_int)] * 2),
+        "bitwriter_init": (None, [P(BitWriter), u8p, ctypes.c_size_t]),
+        "bitwriter_write_bits": (None, [P(BitWriter), ctypes.c_uint32, ctypes.c_int]),
+        "bitwriter_write_bit": (None, [P(BitWriter), ctypes.c_int]),
+        "bitwriter_write_ue": (None, [P(BitWriter), ctypes.c_uint32]),
+        "bitwriter_write_se": (None, [P(BitWriter), ctypes.c_int32]),
+        "bitwriter_write_trailing_bits": (None, [P(BitWriter)]),
+        "bitwriter_flush": (None, [P(BitWriter)]),
+        "bitwriter_get_size": (ctypes.c_size_t, [P(BitWriter)]),
+        "bitwriter_get_bit_position": (ctypes.c_size_t, [P(BitWriter)]),
+        "bitwriter_is_byte_aligned": (ctypes.c_int, [P(BitWriter)]),
+        "bitreader_init": (None, [P(BitReader), u8p, ctypes.c_size_t]),
+        "bitreader_read_bits": (ctypes.c_uint32, [P(BitReader), ctypes.c_int]),
+        "bitreader_read_bit": (ctypes.c_int, [P(BitReader)]),
+        "bitreader_read_ue": (ctypes.c_uint32, [P(BitReader)]),
+        "bitreader_read_se": (ctypes.c_int32, [P(BitReader)]),
+        "bitreader_get_bit_position": (ctypes.c_size_t, [P(BitReader)]),
+        "bitreader_is_byte_aligned": (ctypes.c_int, [P(BitReader)]),
+        "bitreader_get_remaining_bytes": (ctypes.c_size_t, [P(BitReader)]),
+        "bitreader_get_pointer": (u8p, [P(BitReader)]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(lib, name)
+        f.restype = res
+        f.argtypes = args
+    return lib
+
+
+lib = _load()
+
+
+def last_error():
+    return (lib.scroll_last_error() or b"").decode()
+
+
+def device_count():
+    return lib.scroll_device_count()
+
+
+def u8buf(data_or_size):
+    if isinstance(data_or_size, int):
+        return (ctypes.c_uint8 * data_or_size)()
+    b = (ctypes.c_uint8 * len(data_or_size)).from_buffer_copy(data_or_size)
+    return b
+
+
+def make_config(w, h, frame_num=2, log2_mfn=4, poc_type=2, log2_poc=4, deblock=1,
+                waypoints=()):
+    """ComposerConfig in the state composer_init + composer_write_header leave it
+    (reference src/composer.c:199-203: frame_num 2 after the two I frames)."""
+    c = ComposerConfig()
+    lib.composer_config_init(ctypes.byref(c), w, h)
+    lib.composer_config_set_sps_params(ctypes.byref(c), log2_mfn, poc_type, log2_poc)
+    lib.composer_config_set_pps_params(ctypes.byref(c), 1, deblock)
+    c.frame_num = frame_num
+    for i, (off, lt, valid) in enumerate(waypoints):
+        c.waypoints[i].offset_px, c.waypoints[i].long_term_idx, c.waypoints[i].valid = off, lt, valid
+    c.num_waypoints = len(waypoints)
+    return c
+
+
+class Batch:
+    """Many-stream batch on one GPU (include/composer_batch.h)."""
+
+    def __init__(self, max_streams, max_frames, arena_bytes, device=0,
+                 mode=SCROLL_MODE_COMPOSER):
+        d = ScrollBatchDesc(device, max_streams, max_frames, arena_bytes, mode)
+        h = ctypes.c_void_p()
+        rc = lib.scroll_batch_create(ctypes.byref(h), ctypes.byref(d))
+        if rc != SCROLL_OK:
+            raise RuntimeError(f"scroll_batch_create failed ({rc}): {last_error()}")
+        self.h = h
+        self.max_frames = max_frames
+
+    def close(self):
+        if self.h:
+            lib.scroll_batch_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _chk(self, rc, what):
+        if rc < 0:
+            raise RuntimeError(f"{what} failed ({rc}): {last_error()}")
+        return rc
+
+    def add_stream(self, cfg):
+        return self._chk(lib.scroll_batch_add_stream(self.h, ctypes.byref(cfg)), "add_stream")
+
+    @property
+    def num_streams(self):
+        return lib.scroll_batch_num_streams(self.h)
+
+    def set_debug(self, flags):
+        self._chk(lib.scroll_batch_set_debug(self.h, flags), "set_debug")
+
+    def set_offsets(self, offsets):
+        """offsets: numpy int32 array [num_streams, nframes]"""
+        import numpy as np
+        a = np.ascontiguousarray(offsets, dtype=np.int32)
+        self._chk(lib.scroll_batch_set_offsets(
+            self.h, a.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), a.shape[1]), "set_offsets")
+
+    def offsets_device_ptr(self):
+        return lib.scroll_batch_offsets_device(self.h)
+
+    def compose(self, nframes, stream=None, rewind=False):
+        self._chk(lib.scroll_batch_compose_ex(self.h, nframes, stream,
+                                              SCROLL_COMPOSE_REWIND if rewind else 0), "compose")
+
+    def sync(self):
+        return lib.scroll_batch_sync(self.h)
+
+    def config(self, s):
+        c = ComposerConfig()
+        self._chk(lib.scroll_batch_get_config(self.h, s, ctypes.byref(c)), "get_config")
+        return c
+
+    def set_config(self, s, cfg):
+        self._chk(lib.scroll_batch_set_config(self.h, s, ctypes.byref(cfg)), "set_config")
+
+    def output_size(self, s):
+        return lib.scroll_batch_output_size(self.h, s)
+
+    def output(self, s, start=0, n=None):
+        if n is None:
+            n = self.output_size(s) - start
+        b = u8buf(max(n, 1))
+        self._chk(lib.scroll_batch_copy_output(self.h, s, start, b, n), "copy_output")
+        return bytes(b[:n])
+
+    def reset_output(self):
+        self._chk(lib.scroll_batch_reset_output(self.h), "reset_output")
+
+    def nals(self, s):
+        n = self._chk(lib.scroll_batch_nal_count(self.h, s), "nal_count")
+        out = []
+        k, o, sl = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        sz = ctypes.c_uint32()
+        for i in range(n):
+            self._chk(lib.scroll_batch_nal_info(self.h, s, i, ctypes.byref(k), ctypes.byref(o),
+                                                ctypes.byref(sz), ctypes.byref(sl)), "nal_info")
+            out.append((k.value, o.value, sz.value, sl.value))
+        return out
+
+    def enable_timing(self, on=True):
+        self._chk(lib.scroll_batch_enable_timing(self.h, 1 if on else 0), "enable_timing")
+
+    def kernel_ms(self, which):
+        return lib.scroll_batch_kernel_ms(self.h, which)
+
+    def kernel_stats(self, which):
+        """(summed ms, count) of kernel `which` (0 plan, 1 emit) since last call"""
+        t, n = ctypes.c_double(), ctypes.c_int()
+        self._chk(lib.scroll_batch_kernel_stats(self.h, which, ctypes.byref(t), ctypes.byref(n)),
+                  "kernel_stats")
+        return t.value, n.value
+
+    def last_bytes(self):
+        return lib.scroll_batch_last_bytes(self.h)
+
+    def last_nals(self):
+        return lib.scroll_batch_last_nals(self.h)
+
+
+def header_symbols():
+    """Every function declared in include/*.h (the C-ABI contract)."""
+    import re
+    inc = os.path.join(os.path.dirname(HERE), "include")
+    names = []
+    for fn in sorted(os.listdir(inc)):
+        if not fn.endswith(".h"):
+            continue
+        txt = open(os.path.join(inc, fn)).read()
+        txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+        for m in re.finditer(r"^[A-Za-z_][\w \*]*?\b([a-z_][a-z0-9_]*)\s*\(", txt, flags=re.M):
+            if m.group(1) not in ("if", "while", "for", "sizeof", "return"):
+                names.append(m.group(1))
+    return sorted(set(names))

@@ -1,0 +1,123 @@
+/*
+ * composer_batch.h -- ADDITIVE many-stream API (no reference counterpart).
+ *
+ * The reference API is synchronous, single-stream and single-frame
+ * (include/composer.h:79, include/h264_writer.h:124).  Throughput on an
+ * MI355X needs many (stream, frame) items per launch, so this header adds a
+ * batch object that keeps every stream's ComposerConfig state, its scroll
+ * offsets ("UI hints") and its Annex-B output arena resident in HBM:
+ *
+ *   scroll_batch_create()            one batch per GPU (device ordinal)
+ *   scroll_batch_add_stream(cfg)     a stream = one ComposerConfig
+ *   scroll_batch_set_offsets()       [streams][frames] offsets -> HBM
+ *   scroll_batch_compose(n, stream)  async: GPU state machine (waypoints,
+ *                                    frame_num) + P-slice kernels; appends
+ *                                    n composed frames to every stream arena
+ *   scroll_batch_sync()              wait + surface device error words
+ *   scroll_batch_copy_output()       arena -> host
+ *
+ * Semantics per stream are exactly n calls of composer_write_scroll_frame
+ * (src/composer.c:255-264), or of the experiment's loop body
+ * (experiments/scroll-encoder/src/main.c:418-424) in SCROLL_MODE_EXPERIMENT.
+ * Streams are independent; multi-GPU = one batch per device with a static
+ * contiguous shard of the streams (no collective).
+ *
+ * All functions return SCROLL_OK (0) or a negative SCROLL_ERR_* code;
+ * scroll_last_error() has the message.  No CPU fallback exists: without a
+ * usable gfx950 device every compose call fails with SCROLL_ERR_NO_DEVICE.
+ */
+#ifndef COMPOSER_BATCH_H
+#define COMPOSER_BATCH_H
+
+#include <stddef.h>
+#include <stdint.h>
+#include "composer.h"
+#include "h264_writer.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SCROLL_OK             0
+#define SCROLL_ERR_NO_DEVICE (-1)
+#define SCROLL_ERR_ARG       (-2)
+#define SCROLL_ERR_OOM       (-3)
+#define SCROLL_ERR_OVERFLOW  (-4)   /* output arena full (reference: assert abort) */
+#define SCROLL_ERR_HIP       (-5)
+#define SCROLL_ERR_CONFIG    (-6)   /* config outside the supported syntax range  */
+
+#define SCROLL_MODE_COMPOSER   0    /* waypoint NAL in addition to the scroll NAL */
+#define SCROLL_MODE_EXPERIMENT 1    /* waypoint NAL instead of the scroll NAL     */
+
+/* debug flags (tests) */
+#define SCROLL_DEBUG_FORCE_SERIAL 1 /* every NAL through the serial device path   */
+
+typedef struct ScrollBatch ScrollBatch;
+
+typedef struct {
+    int device;            /* HIP device ordinal                               */
+    int max_streams;
+    int max_frames;        /* max composed frames per scroll_batch_compose    */
+    size_t arena_bytes;    /* device output arena per stream                   */
+    int mode;              /* SCROLL_MODE_*                                    */
+} ScrollBatchDesc;
+
+const char *scroll_last_error(void);
+int scroll_device_count(void);                 /* usable gfx950 devices (0 if none) */
+const char *scroll_version(void);
+
+int scroll_batch_create(ScrollBatch **out, const ScrollBatchDesc *desc);
+void scroll_batch_destroy(ScrollBatch *b);
+int scroll_batch_add_stream(ScrollBatch *b, const ComposerConfig *cfg); /* -> stream id */
+int scroll_batch_num_streams(const ScrollBatch *b);
+int scroll_batch_set_debug(ScrollBatch *b, int flags);
+
+/* offsets: host array [num_streams][nframes] (row stride nframes) */
+int scroll_batch_set_offsets(ScrollBatch *b, const int32_t *offsets, int nframes);
+/* device array [num_streams][max_frames]; fill it from device code to skip H2D */
+int32_t *scroll_batch_offsets_device(ScrollBatch *b);
+
+/* async on hip_stream (hipStream_t; NULL = the batch's own stream) */
+int scroll_batch_compose(ScrollBatch *b, int nframes, void *hip_stream);
+/* flags: SCROLL_COMPOSE_REWIND = start every arena at 0 (the caller has
+ * consumed the previous batch's bytes) -- device-side, no host sync. */
+#define SCROLL_COMPOSE_REWIND 1
+int scroll_batch_compose_ex(ScrollBatch *b, int nframes, void *hip_stream, int flags);
+int scroll_batch_sync(ScrollBatch *b);
+
+/* state after sync: ComposerConfig as the reference would hold it */
+int scroll_batch_get_config(ScrollBatch *b, int s, ComposerConfig *cfg);
+int scroll_batch_set_config(ScrollBatch *b, int s, const ComposerConfig *cfg);
+size_t scroll_batch_output_size(ScrollBatch *b, int s);
+int scroll_batch_copy_output(ScrollBatch *b, int s, size_t from, uint8_t *dst, size_t n);
+const uint8_t *scroll_batch_output_device(ScrollBatch *b, int s);
+int scroll_batch_reset_output(ScrollBatch *b);   /* rewind all arenas, keep state */
+
+/* last compose: planned NAL units of stream s (kind/size/offset per NAL) */
+int scroll_batch_nal_count(ScrollBatch *b, int s);
+int scroll_batch_nal_info(ScrollBatch *b, int s, int i, int *kind, int *offset_px,
+                          uint32_t *size, int *slow);
+
+/* HIP-event timing of the last compose's kernels, on the launch stream:
+ * which 0 = plan kernel, 1 = emit kernel.  Enable before compose. */
+int scroll_batch_enable_timing(ScrollBatch *b, int on);
+float scroll_batch_kernel_ms(ScrollBatch *b, int which);
+/* all composes since the last call: summed kernel ms and count (then reset) */
+int scroll_batch_kernel_stats(ScrollBatch *b, int which, double *total_ms, int *count);
+/* bytes appended to every arena by the last compose (sum over streams) */
+unsigned long long scroll_batch_last_bytes(ScrollBatch *b);
+/* NAL units planned by the last compose (sum over streams) */
+long long scroll_batch_last_nals(ScrollBatch *b);
+
+/* Composer-level batch: offsets[i] composed on cs[i], i < n, in
+ * order; Composers may repeat.  Output lands in each Composer's buffer before
+ * return (equivalent to n composer_write_scroll_frame calls + a flush). */
+int composer_batch_write_scroll_frames(Composer *const *cs, const int *offsets, int n,
+                                       int flags);
+/* Force queued frames of c onto the GPU now (0 or SCROLL_ERR_*). */
+int composer_flush(Composer *c);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* COMPOSER_BATCH_H */

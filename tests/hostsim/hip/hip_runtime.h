@@ -1,0 +1,17 @@
+/*
+ * TEST-ONLY shim: lets g++ compile the product's device header
+ * (h264-scroll-encoder_amd/csrc/scroll_device.h) on the CPU so its run-layout
+ * and bit-extraction logic can be unit-tested without a GPU.  Never linked
+ * into libh264scroll.so; the GPU tests (tests/test_gpu_*.py) are the parity
+ * evidence for the real kernels.
+ */
+#pragma once
+#include <algorithm>
+#include <cstdint>
+#define __device__
+#define __host__
+using std::max;
+using std::min;
+static inline int __clzll(uint64_t x) { return x ? __builtin_clzll(x) : 64; }
+static inline int __clz(int x) { return x ? __builtin_clz((unsigned)x) : 32; }
+static inline float __builtin_amdgcn_rcpf(float x) { return 1.0f / x; }

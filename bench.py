@@ -125,7 +125,7 @@ def main():
     if b.sync() != 0:
         raise RuntimeError(hs.last_error())
     b.enable_timing(True)
-    b.kernel_stats(1)                               # reset accumulators
+    b.kernel_stats()                                # reset accumulators
     barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -134,8 +134,8 @@ def main():
     t1 = time.perf_counter()
     if b.sync() != 0:
         raise RuntimeError(hs.last_error())
-    emit_ms, n_emit = b.kernel_stats(1)
-    plan_ms, n_plan = b.kernel_stats(0)
+    plan_ms, emit_ms, n_emit = b.kernel_stats()
+    n_plan = n_emit
     step_bytes = b.last_bytes()                     # per step, all streams of this rank
     step_nals = b.last_nals()
     b.enable_timing(False)

@@ -28,11 +28,12 @@
 namespace scroll {
 
 constexpr int MVL = 496;          /* MV_LIMIT_PX, include/h264_writer.h:24       */
-constexpr int RUNS_MAX = 12;      /* runs per NAL on the fast path                */
+constexpr int RUNS_MAX = 9;       /* runs per NAL on the fast path (row-class max) */
 constexpr int HDR_WORDS = 12;     /* 384 bits: 40-bit NAL prefix + slice header   */
 constexpr int EP_ZERO_RUN = 22;   /* 00 00 0x (x<=3) needs >= 22 consecutive 0s   */
 
-/* Per-NAL emission layout, built in LDS by one lane. 276 bytes. */
+/* Per-NAL emission layout, built in LDS by one lane.  260 bytes = 65 dwords:
+ * an odd stride keeps lanes that read different NALs on different banks. */
 struct Lay {
     uint32_t nal_bits;            /* 8 * NAL bytes (prefix + RBSP incl. padding)  */
     uint32_t used_bits;           /* prefix + header + runs + stop bit            */
@@ -41,7 +42,9 @@ struct Lay {
     uint32_t hdr[HDR_WORDS];      /* prefix + header bits, MSB first              */
     uint32_t run_end[RUNS_MAX];   /* NAL bit where run r ends                     */
     uint32_t pat[RUNS_MAX][3];    /* run codeword repeated over 96 bits           */
+    uint32_t magic[RUNS_MAX];     /* ceil(2^32 / len): x mod len by mul-high      */
     uint8_t len[RUNS_MAX];        /* codeword length (1..64)                      */
+    uint8_t pad_[7];
 };
 
 /* Everything the syntax of one NAL depends on. */
@@ -95,30 +98,47 @@ __device__ inline void zr_push(ZR &z, uint64_t v, int n, uint32_t rep = 1)
 /* ---------------------------------------------------------------------- */
 __device__ inline uint32_t low_mask(int n) { return n >= 32 ? 0xffffffffu : ((1u << n) - 1u); }
 
-/* header bits -> LDS words (or just counted when w == nullptr) */
+/* header bits -> LDS words (STORE) or just counted.  CHECK tracks zero runs
+ * and the HDR_WORDS bound; the emit kernel builds only NALs the plan kernel
+ * already proved fast, so it skips both.  Words are assembled in a 64-bit
+ * register and written whole (no LDS read-modify-write). */
+template <bool STORE, bool CHECK>
 struct HdrSink {
     uint32_t *w;
     int len;
     bool over;
     bool track;
     ZR zr;
+    uint64_t acc;                  /* pending bits (len & 31), left-aligned */
     __device__ inline void put(uint32_t v, int n)
     {
         if (n <= 0) return;
         v &= low_mask(n);
-        if (track) zr_push(zr, v, n);
-        if (len + n > HDR_WORDS * 32) {
-            over = true;
-            len += n;
-            return;
+        if (CHECK) {
+            if (track) zr_push(zr, v, n);
+            if (len + n > HDR_WORDS * 32) {
+                over = true;
+                len += n;
+                return;
+            }
         }
-        if (w) {
-            int k = len >> 5, sh = len & 31;
-            uint64_t t = (uint64_t)v << (64 - n);
-            w[k] |= (uint32_t)(t >> 32) >> sh;
-            if (sh + n > 32) w[k + 1] |= (uint32_t)((t << (32 - sh)) >> 32);
+        if (STORE) {
+            const int nacc = len & 31;
+            acc |= ((uint64_t)v << (64 - n)) >> nacc;
+            if (nacc + n >= 32) {
+                w[len >> 5] = (uint32_t)(acc >> 32);
+                acc <<= 32;
+            }
         }
         len += n;
+    }
+    /* flush the partial word and zero the rest of the header words */
+    __device__ inline void finish()
+    {
+        if (!STORE || over) return;
+        int k = len >> 5;
+        if (len & 31) w[k++] = (uint32_t)(acc >> 32);
+        for (; k < HDR_WORDS; ++k) w[k] = 0u;
     }
 };
 
@@ -320,6 +340,7 @@ __device__ inline void fill_pattern(uint32_t *p, uint64_t v, int len)
     p[2] = (uint32_t)((r << d) >> 32);
 }
 
+template <bool CHECK>
 struct RunAcc {
     Lay *L;
     int n;
@@ -331,7 +352,8 @@ struct RunAcc {
     __device__ inline void append(uint64_t v, int len, uint64_t rep)
     {
         if (rep == 0) return;
-        zr_push(*zr, v >> (64 - len), len, rep > 0xffffffffull ? 0xffffffffu : (uint32_t)rep);
+        if (CHECK)
+            zr_push(*zr, v >> (64 - len), len, rep > 0xffffffffull ? 0xffffffffu : (uint32_t)rep);
         uint64_t end = pos + (uint64_t)len * rep;
         if (n > 0 && last_len == len && last_v == v) {
             if (L && !over) L->run_end[n - 1] = (uint32_t)end;
@@ -341,6 +363,8 @@ struct RunAcc {
             if (L) {
                 L->len[n] = (uint8_t)len;
                 L->run_end[n] = (uint32_t)end;
+                /* ceil(2^32 / len) = floor((2^32 - 1) / len) + 1 for len >= 2 */
+                L->magic[n] = len == 1 ? 0xffffffffu : 0xffffffffu / (uint32_t)len + 1u;
                 fill_pattern(L->pat[n], v, len);
             }
             n++;
@@ -364,7 +388,8 @@ __device__ inline CodeSink mb_code(int x, int y, int mbw, int ref, int mv4, int 
 }
 
 /* rows [y, y+count) of one class: all have region cur, row above region abv */
-__device__ inline bool emit_group(RunAcc &ra, int mbw, int nrefs, int y, int count,
+template <class RA>
+__device__ inline bool emit_group(RA &ra, int mbw, int nrefs, int y, int count,
                                   int ref, int mv4, int aref, int amv4)
 {
     if (count <= 0) return true;
@@ -390,22 +415,19 @@ __device__ inline bool emit_group(RunAcc &ra, int mbw, int nrefs, int y, int cou
  * fast path applies (no EP possible, codes <= 64 bits, <= RUNS_MAX runs,
  * header <= HDR_WORDS); *size = NAL bytes in that case.  The decision is the
  * same in the plan and emit kernels (it never depends on STORE). */
-template <bool STORE>
+template <bool STORE, bool CHECK = true>
 __device__ bool build_nal(const NalCtx &c, Lay *L, uint32_t *size)
 {
-    HdrSink hs{STORE ? L->hdr : nullptr, 0, false, false, {0, 0}};
-    if (STORE) {
-#pragma unroll
-        for (int k = 0; k < HDR_WORDS; ++k) L->hdr[k] = 0;
-    }
+    HdrSink<STORE, CHECK> hs{STORE ? L->hdr : nullptr, 0, false, false, {0, 0}, 0};
     hs.put(0, 24);                               /* 00 00 00 01 (nal.c:59-64) */
     hs.put(1, 8);
     hs.put(nal_header_byte(c.kind), 8);
     hs.track = true;
     emit_slice_header(hs, c);
+    hs.finish();
     bool ok = !hs.over;
     ZR zr = hs.zr;
-    RunAcc ra{STORE ? L : nullptr, 0, 0, 0, (uint64_t)hs.len, false, &zr};
+    RunAcc<CHECK> ra{STORE ? L : nullptr, 0, 0, 0, (uint64_t)hs.len, false, &zr};
 
     Regions rg = regions(c);
     int mbw = c.w / 16, mbh = c.h / 16;
@@ -425,7 +447,7 @@ __device__ bool build_nal(const NalCtx &c, Lay *L, uint32_t *size)
         }
     }
     ra.append(0x8000000000000000ull, 1, 1);      /* rbsp_stop_one_bit */
-    ok = ok && !ra.over && zr.max < EP_ZERO_RUN;
+    ok = ok && !ra.over && (!CHECK || zr.max < EP_ZERO_RUN);
     uint64_t used = ra.pos;
     uint64_t nal_bits = (used + 7) & ~7ull;
     if (STORE && ok) {
@@ -496,44 +518,164 @@ __device__ inline uint32_t lay_bits32(const Lay *L, uint32_t b)
 }
 
 
-/* ---------------------------------------------------------------------- */
-/* 16 output bytes of a tile (32 NAL layouts in LDS) at tile byte rel,     */
-/* rel 16-B aligned in arena terms; may cross NAL boundaries. j = cursor.  */
-/* ---------------------------------------------------------------------- */
-__device__ inline uint32_t tile_bits32(const Lay *L, int cnt, int j, uint32_t b)
-{
-    uint32_t w = lay_bits32(&L[j], b);
-    uint32_t nb = L[j].nal_bits;
-    if (b + 32 > nb && j + 1 < cnt) {
-        uint32_t rem = nb - b;                 /* 1..31 bits left in NAL j */
-        w |= lay_bits32(&L[j + 1], 0) >> rem;
-    }
-    return w;
-}
-
-__device__ inline void chunk_words(const Lay *L, const uint32_t *noff, int cnt, int &j,
-                                   uint32_t rel, uint32_t w[4])
-{
-    while (j + 1 < cnt && noff[j + 1] <= rel) j++;
-    uint32_t b = (rel - noff[j]) * 8u;
-    int jj = j;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        w[k] = tile_bits32(L, cnt, jj, b);
-        b += 32;
-        if (b >= L[jj].nal_bits && jj + 1 < cnt) {
-            b -= L[jj].nal_bits;
-            jj++;
-        }
-    }
-}
-
 /* one byte of the tile at tile byte rel (fast NALs only) */
 __device__ inline uint32_t tile_byte(const Lay *L, const uint32_t *noff, int cnt, int &j,
                                      uint32_t rel)
 {
     while (j + 1 < cnt && noff[j + 1] <= rel) j++;
     return lay_bits32(&L[j], (rel - noff[j]) * 8u) >> 24;
+}
+
+
+/* ---------------------------------------------------------------------- */
+/* k_emit helpers: a PURE chunk (16 output bytes wholly inside one periodic */
+/* run) is 4 funnel shifts of the run's 192-bit pattern expansion at phase  */
+/* (bit offset into the run) mod len, the modulo by mul-high; a MIXED chunk */
+/* ORs the masked pieces of every segment it meets (mixed_chunk).           */
+/* ---------------------------------------------------------------------- */
+__device__ inline uint32_t uni(uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); }
+
+__device__ inline uint32_t mod_magic(uint32_t d, uint32_t len, uint32_t magic)
+{
+    uint32_t q = __umulhi(d, magic);                 /* floor(d/len) or +1 */
+    int32_t r = (int32_t)(d - q * len);
+    r += r < 0 ? (int32_t)len : 0;
+    r -= r >= (int32_t)len ? (int32_t)len : 0;
+    return (uint32_t)r;
+}
+
+__device__ inline uint32_t pat_window(uint32_t p0, uint32_t p1, uint32_t p2, uint32_t phi)
+{
+    /* bits [phi, phi + 32) of the 96-bit pattern, phi < 64 */
+    uint64_t hi = phi < 32 ? (((uint64_t)p0 << 32) | p1) : (((uint64_t)p1 << 32) | p2);
+    return (uint32_t)(hi >> (32 - (phi & 31)));
+}
+
+/* 192-bit expansion of a run pattern: words 3..5 continue the repetition
+ * (bits [96, 192)), so any 128-bit window at phase phi < 64 is 4 funnel
+ * shifts of 5 consecutive words with ONE shift amount. */
+__device__ inline void pattern192(uint32_t p0, uint32_t p1, uint32_t p2, uint32_t len,
+                                  uint32_t magic, uint32_t q[6])
+{
+    q[0] = p0;
+    q[1] = p1;
+    q[2] = p2;
+    q[3] = pat_window(p0, p1, p2, mod_magic(96u, len, magic));
+    q[4] = pat_window(p0, p1, p2, mod_magic(128u, len, magic));
+    q[5] = pat_window(p0, p1, p2, mod_magic(160u, len, magic));
+}
+
+/* 128 bits of a run's repetition starting at pattern phase phi (< len <= 64);
+ * q = pattern192 of the run. */
+__device__ inline void pure_words_phi(uint32_t phi, const uint32_t q[6], uint32_t w[4])
+{
+    const bool hi = phi >= 32;
+    const uint32_t sh = phi & 31;
+    uint32_t a[5];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) a[k] = hi ? q[k + 1] : q[k];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) w[k] = sh ? __builtin_amdgcn_alignbit(a[k], a[k + 1], 32 - sh) : a[k];
+}
+
+/* 128 bits of a PURE chunk (wholly inside one periodic run) starting d bits
+ * after the run's first bit; q = pattern192 of the run. */
+__device__ inline void pure_words(uint32_t d, uint32_t len, uint32_t magic, const uint32_t q[6],
+                                  uint32_t w[4])
+{
+    pure_words_phi(mod_magic(d, len, magic), q, w);      /* phase < len <= 64 */
+}
+
+/* bits [lo, hi) of a 32-bit word (MSB first), lo / hi clamped to [0, 32] */
+__device__ inline uint32_t range_mask(int32_t lo, int32_t hi)
+{
+    lo = lo < 0 ? 0 : lo;
+    hi = hi > 32 ? 32 : hi;
+    if (hi <= lo) return 0u;
+    const uint32_t b = hi >= 32 ? 0u : (0xffffffffu >> hi);
+    return (0xffffffffu >> lo) & ~b;
+}
+
+__device__ inline int32_t clamp_bits(int64_t x)
+{
+    return x < -64 ? -64 : (x > 192 ? 192 : (int32_t)x);
+}
+
+/* 128 bits of the tile at tile bit x0 (x0 = 8 * (chunk byte - tile start),
+ * negative for the chunk straddling the tile start), j = the NAL holding the
+ * chunk's first bit (0 for that leading chunk).  The chunk is the OR of the
+ * pieces of every segment it meets -- header words, periodic runs, and the
+ * same for the following NALs -- each run taken at its phase at x0 (a
+ * negative offset when the run starts inside the chunk) and masked to its
+ * bit range, so no per-word segment search is needed.  Bits past the last
+ * NAL of the tile read as zero. */
+__device__ inline void mixed_chunk(const Lay *L, const uint32_t *noff, int cnt, int j, int64_t x0,
+                                   uint32_t w[4])
+{
+    w[0] = w[1] = w[2] = w[3] = 0u;
+    for (; j < cnt; ++j) {
+        const int64_t nb = (int64_t)noff[j] * 8;
+        if (nb >= x0 + 128) break;
+        const Lay &Lj = L[j];
+        const int64_t rel0 = x0 - nb;                    /* NAL bits, may be < 0 */
+        if (rel0 >= (int64_t)Lj.nal_bits) continue;
+        const uint32_t hb = Lj.hdr_bits;
+        if (rel0 < (int64_t)hb) {
+            const int32_t r0 = (int32_t)rel0;            /* (-128, 384) */
+            const int32_t i0 = r0 >> 5;                  /* floor */
+            const uint32_t sh = (uint32_t)r0 & 31u;
+            uint32_t hw[5];
+#pragma unroll
+            for (int k = 0; k < 5; ++k) {
+                const int32_t idx = i0 + k;
+                hw[k] = (idx >= 0 && idx < HDR_WORDS) ? Lj.hdr[idx] : 0u;
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                w[k] |= sh ? __builtin_amdgcn_alignbit(hw[k], hw[k + 1], 32 - sh) : hw[k];
+        }
+        const uint32_t nr = Lj.nruns;
+        uint32_t r = 0, s0 = hb;
+        if (rel0 > (int64_t)hb) {           /* first run ending after rel0: independent loads */
+#pragma unroll
+            for (int q = 0; q < RUNS_MAX; ++q) {
+                const uint32_t e = Lj.run_end[q];
+                const bool past = (uint32_t)q < nr && (int64_t)e <= rel0;
+                r += past ? 1u : 0u;
+                s0 = past ? e : s0;
+            }
+        }
+        for (; r < nr && (int64_t)s0 < rel0 + 128; ++r) {
+            const uint32_t s1 = Lj.run_end[r];
+            const uint32_t len = Lj.len[r], mag = Lj.magic[r];
+            const int64_t d = rel0 - (int64_t)s0;
+            uint32_t phi;
+            if (d >= 0) {
+                phi = mod_magic((uint32_t)d, len, mag);
+            } else {
+                const uint32_t m = mod_magic((uint32_t)(-d), len, mag);
+                phi = m ? len - m : 0u;
+            }
+            uint32_t q[6], pw[4];
+            pattern192(Lj.pat[r][0], Lj.pat[r][1], Lj.pat[r][2], len, mag, q);
+            pure_words_phi(phi, q, pw);
+            const int32_t lo = clamp_bits((int64_t)s0 - rel0);
+            const int32_t hi = clamp_bits((int64_t)s1 - rel0);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) w[k] |= pw[k] & range_mask(lo - 32 * k, hi - 32 * k);
+            s0 = s1;
+        }
+    }
+}
+
+/* pure chunk ranges of NAL j: run r covers arena bits [Aj + s0, Aj + s1);
+ * its pure chunks are [ceil((Aj+s0)/128), floor((Aj+s1)/128)). */
+__device__ inline void pure_range(uint64_t Aj, uint32_t s0, uint32_t s1, uint64_t &cp0,
+                                  uint64_t &cp1)
+{
+    cp0 = (Aj + s0 + 127) >> 7;
+    cp1 = (Aj + s1) >> 7;
+    if (cp1 < cp0) cp1 = cp0;
 }
 
 /* ---------------------------------------------------------------------- */

@@ -29,8 +29,14 @@ static_assert(sizeof(NalDesc) == 32, "NalDesc must stay 32 B");
 
 namespace {
 
-constexpr int TILE = 32;          /* NAL units per wave tile in k_emit        */
-constexpr int EMIT_WAVES = 4;     /* waves per k_emit workgroup               */
+#ifndef SCROLL_TILE
+#define SCROLL_TILE 32
+#endif
+#ifndef SCROLL_EMIT_WAVES
+#define SCROLL_EMIT_WAVES 1
+#endif
+constexpr int TILE = SCROLL_TILE;              /* NAL units per wave tile in k_emit */
+constexpr int EMIT_WAVES = SCROLL_EMIT_WAVES;  /* waves per k_emit workgroup        */
 constexpr int PLAN_THREADS = 256;
 constexpr int PLAN_REWIND = 1 << 8;   /* k_plan flag: arena restarts at 0 */
 
@@ -288,25 +294,79 @@ __global__ __launch_bounds__(PLAN_THREADS) void k_plan(DevStream *__restrict__ s
 
 /* ---------------------------------------------------------------------- */
 /* k_emit: each wave owns TILE consecutive NAL units of one stream.         */
-/*  1. lane i builds the run layout of NAL t0+i in LDS (32 NALs at once).   */
-/*  2. the wave sweeps the tile's byte range in 16-byte aligned chunks;     */
-/*     each lane random-accesses 128 bits through the layouts (crossing NAL */
-/*     boundaries in-register) and issues one 16 B store.                   */
-/*  3. partial chunks at the tile ends use byte stores; NALs on the serial  */
-/*     path are written by their own lane.                                  */
+/*  1. lane i builds the run layout of NAL t0+i in LDS.                      */
+/*  2. lane i classifies the 16-byte arena chunks it owns (first byte in    */
+/*     NAL i): PURE chunks lie inside one periodic run, the rest are MIXED. */
+/*     Wave scans turn both into compact per-wave lists in LDS.             */
+/*  3. PURE phase: the wave walks the pure list 64 chunks at a time with    */
+/*     wave-uniform run data (SGPRs): phase by mul-high, 4 words from the   */
+/*     run's 96-bit pattern, one 16-B store per lane.  No divergence.       */
+/*  4. MIXED phase: one lane per mixed chunk, generic bit extraction across */
+/*     header / runs / NAL boundaries; byte stores at the tile's two ends.  */
+/*  Tiles holding a serial-path NAL use the generic path for every byte and */
+/*  the owning lane writes that NAL serially.                               */
 /* ---------------------------------------------------------------------- */
+#ifndef SCROLL_PURE_U
+#define SCROLL_PURE_U 4
+#endif
+constexpr int PURE_U = SCROLL_PURE_U;   /* 64-chunk groups per pure-phase iteration */
+constexpr int MAXPE = 5 * TILE;   /* pure-run entries per wave                */
+constexpr int MAXMX = 16 * TILE;  /* mixed chunks per wave                    */
+constexpr uint32_t PE_VS_MASK = (1u << 22) - 1;   /* tiles < 64 MB: chunks < 2^22 */
+static_assert(TILE <= 64, "owner NAL index is 6 bits");
+
+struct EmitWaveLds {
+    Lay lay[TILE];
+    uint32_t noff[TILE + 1];
+    uint32_t pe_cb[MAXPE];        /* first pure chunk, relative to c0         */
+    uint32_t pe_vj[MAXPE];        /* virtual start | nal << 22 | run << 28     */
+    uint32_t mx[MAXMX];           /* (chunk rel c0 << 6) | owner nal          */
+};
+
+/* 16-B global store to an integer address (address space 1: a
+ * global_store, not flat) */
+__device__ inline void store_raw(uint64_t addr, const uint32_t o[4])
+{
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    typedef __attribute__((address_space(1))) u32x4 gu32x4;
+    u32x4 v;
+    v.x = o[0];
+    v.y = o[1];
+    v.z = o[2];
+    v.w = o[3];
+    *reinterpret_cast<gu32x4 *>(addr) = v;
+}
+
+#ifndef SCROLL_NT_STORE
+#define SCROLL_NT_STORE 0
+#endif
+__device__ inline void store_chunk(uint8_t *A, uint64_t p, const uint32_t w[4])
+{
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    u32x4 o;
+    o.x = __builtin_bswap32(w[0]);
+    o.y = __builtin_bswap32(w[1]);
+    o.z = __builtin_bswap32(w[2]);
+    o.w = __builtin_bswap32(w[3]);
+#if SCROLL_NT_STORE
+    __builtin_nontemporal_store(o, reinterpret_cast<u32x4 *>(A + p));
+#else
+    *reinterpret_cast<u32x4 *>(A + p) = o;
+#endif
+}
+
 __global__ __launch_bounds__(EMIT_WAVES * 64) void k_emit(const DevStream *__restrict__ st,
                                                           const NalDesc *__restrict__ nal,
                                                           int ld_nal, uint8_t *__restrict__ arena,
-                                                          uint64_t ld_arena, int flags)
+                                                          uint64_t ld_arena, int flags,
+                                                          uint64_t *__restrict__ dbg)
 {
-    __shared__ Lay s_lay[EMIT_WAVES][TILE];
-    __shared__ uint32_t s_noff[EMIT_WAVES][TILE + 1];
+    __shared__ EmitWaveLds s_w[EMIT_WAVES];
     __shared__ int32_t s_cfg[8], s_wo[8], s_wl[8], s_wv[8];
-    (void)flags;
 
     const int s = blockIdx.y;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = (int)uni((uint32_t)(tid >> 6));      /* wave-uniform -> SGPR */
     const DevStream *S = st + s;
     if (tid < 8) {
         s_wo[tid] = S->wp_off[tid];
@@ -323,47 +383,273 @@ __global__ __launch_bounds__(EMIT_WAVES * 64) void k_emit(const DevStream *__res
     if (t0 >= nnal) return;
     const int cnt = min(TILE, nnal - t0);
     const NalDesc *D = nal + (size_t)s * ld_nal + t0;
-    Lay *L = s_lay[wave];
-    uint32_t *noff = s_noff[wave];
+    EmitWaveLds &W = s_w[wave];
+    const bool stamps = (flags & SCROLL_DEBUG_EMIT_STAMPS) && dbg;
+    uint64_t *stamp = dbg + ((size_t)(blockIdx.y * gridDim.x + blockIdx.x) * EMIT_WAVES + wave) * 8;
+    auto mark = [&](int k) {
+        if (stamps) {
+            uint64_t t = __builtin_amdgcn_s_memtime();
+            if (lane == 0) stamp[k] = t;
+        }
+    };
+    mark(0);
+    if (stamps && lane == 0) stamp[5] = __builtin_amdgcn_s_memrealtime();
+    Lay *L = W.lay;
+    uint32_t *noff = W.noff;
     uint8_t *A = arena + (size_t)s * ld_arena;
 
+    /* 1. layouts */
     const uint64_t B0 = D[0].out_off;
     bool my_slow = false;
     NalCtx my_ctx;
+    uint32_t my_size = 0;
     if (lane < cnt) {
         NalDesc d = D[lane];
         my_ctx = make_ctx(s_cfg, s_wo, s_wl, s_wv, d);
         my_slow = d.slow != 0;
+        my_size = d.size;
         if (!my_slow) {
             uint32_t sz;
-            build_nal<true>(my_ctx, &L[lane], &sz);
+            build_nal<true, false>(my_ctx, &L[lane], &sz);   /* plan proved it fast */
         } else {
-            L[lane].nal_bits = d.size * 8u;   /* keeps tile_bits32 well-defined */
+            L[lane].nal_bits = d.size * 8u;
             L[lane].used_bits = 0;
             L[lane].hdr_bits = 0;
+            L[lane].nruns = 0;
         }
         noff[lane] = (uint32_t)(d.out_off - B0);
         if (lane == cnt - 1) noff[cnt] = (uint32_t)(d.out_off + d.size - B0);
     }
     const bool any_slow = __ballot(my_slow) != 0;
     wave_lds_sync();
+    mark(1);
+    if (flags & SCROLL_DEBUG_EMIT_BUILD) return;
 
-    const uint64_t B1 = B0 + noff[cnt];
+    const uint64_t B1 = B0 + uni(noff[cnt]);
     const uint64_t c0 = B0 >> 4, c1 = (B1 + 15) >> 4;
-    int j = 0;
-    for (uint64_t c = c0 + lane; c < c1; c += 64) {
-        const uint64_t p = c << 4;
-        const bool full = p >= B0 && p + 16 <= B1 && !any_slow;
-        if (full) {
-            uint32_t wv[4];
-            chunk_words(L, noff, cnt, j, (uint32_t)(p - B0), wv);
-            uint4 o;
-            o.x = __builtin_bswap32(wv[0]);
-            o.y = __builtin_bswap32(wv[1]);
-            o.z = __builtin_bswap32(wv[2]);
-            o.w = __builtin_bswap32(wv[3]);
-            *reinterpret_cast<uint4 *>(A + p) = o;
-        } else {
+
+    /* 2. classify owned chunks */
+    uint32_t npe = 0, nchunks_pure = 0, nmx = 0;
+    uint64_t own0 = 0, own1 = 0, Aj = 0;
+    if (lane < cnt) {
+        Aj = 8 * (B0 + noff[lane]);
+        uint64_t Aj1 = 8 * (B0 + (uint64_t)noff[lane] + my_size);
+        own0 = lane == 0 ? c0 : (Aj + 127) >> 7;
+        own1 = lane == cnt - 1 ? c1 : (Aj1 + 127) >> 7;
+        if (own1 < own0) own1 = own0;
+        if (!my_slow) {
+            uint32_t s0 = L[lane].hdr_bits;
+            for (uint32_t r = 0; r < L[lane].nruns; ++r) {
+                uint32_t s1 = L[lane].run_end[r];
+                uint64_t cp0, cp1;
+                pure_range(Aj, s0, s1, cp0, cp1);
+                if (cp1 > cp0) {
+                    npe++;
+                    nchunks_pure += (uint32_t)(cp1 - cp0);
+                }
+                s0 = s1;
+            }
+        }
+        nmx = (uint32_t)(own1 - own0) - nchunks_pure;
+    }
+    const uint32_t pe_inc = (uint32_t)wave_incl_scan(npe, lane);
+    const uint32_t vs_inc = (uint32_t)wave_incl_scan(nchunks_pure, lane);
+    const uint32_t mx_inc = (uint32_t)wave_incl_scan(nmx, lane);
+    const uint32_t tot_pe = uni((uint32_t)__shfl(pe_inc, 63, 64));
+    const uint32_t tot_pure = uni((uint32_t)__shfl(vs_inc, 63, 64));
+    const uint32_t tot_mx = uni((uint32_t)__shfl(mx_inc, 63, 64));
+    const bool generic = any_slow || (B1 - B0) >= (1ull << 26) || tot_pe > (uint32_t)MAXPE ||
+                         tot_mx > (uint32_t)MAXMX;
+
+    if (!generic) {
+        if (lane < cnt) {
+            uint32_t e = pe_inc - npe, v = vs_inc - nchunks_pure, m = mx_inc - nmx;
+            uint64_t prev = own0;
+            uint32_t s0 = L[lane].hdr_bits;
+            for (uint32_t r = 0; r <= L[lane].nruns; ++r) {
+                uint64_t cp0 = own1, cp1 = own1;              /* r == nruns: tail gap */
+                if (r < L[lane].nruns) {
+                    uint32_t s1 = L[lane].run_end[r];
+                    pure_range(Aj, s0, s1, cp0, cp1);
+                    s0 = s1;
+                    if (cp1 <= cp0) continue;
+                }
+                for (uint64_t c = prev; c < cp0; ++c)          /* mixed gap before it */
+                    W.mx[m++] = ((uint32_t)(c - c0) << 6) | (uint32_t)lane;
+                if (r < L[lane].nruns) {
+                    W.pe_cb[e] = (uint32_t)(cp0 - c0);
+                    W.pe_vj[e] = v | ((uint32_t)lane << 22) | (r << 28);
+                    e++;
+                    v += (uint32_t)(cp1 - cp0);
+                }
+                prev = cp1;
+            }
+        }
+        wave_lds_sync();
+        mark(2);
+
+        /* 3. pure phase.  The wave writes the pure chunks 64 at a time in
+         * virtual order.  Lane k of a window holds pure entry ebase + k (its
+         * first virtual chunk vs and end, K = run bit of virtual chunk 0,
+         * chunk bias C, code len / magic, pattern192).  Each lane finds its
+         * entry from the (usually 0-2) entries that start inside the group
+         * and pulls that entry's data with ds_bpermute: no per-entry select
+         * chains, no LDS round trip for the common case. */
+        uint32_t ebase = 0;
+        uint32_t e_vs = 0xffffffffu, e_end = 0xffffffffu, e_K = 0, e_C = 0, e_len = 1,
+                 e_mag = 0xffffffffu, e_q[6] = {0, 0, 0, 0, 0, 0};
+        auto load_window = [&](uint32_t base) {
+            const uint32_t idx = base + (uint32_t)lane;
+            e_vs = e_end = 0xffffffffu;
+            if (idx < tot_pe) {
+                const uint32_t vj = W.pe_vj[idx], cb = W.pe_cb[idx];
+                const uint32_t vs = vj & PE_VS_MASK;
+                const int j = (int)((vj >> 22) & 63u), r = (int)(vj >> 28);
+                const Lay &Lj = L[j];
+                const uint32_t rs0 = r ? Lj.run_end[r - 1] : Lj.hdr_bits;
+                const uint64_t Arun = 8 * (B0 + (uint64_t)noff[j]) + rs0;
+                e_vs = vs;
+                e_end = idx + 1 < tot_pe ? (W.pe_vj[idx + 1] & PE_VS_MASK) : tot_pure;
+                e_K = (uint32_t)(((c0 + cb - vs) << 7) - Arun);
+                e_C = cb - vs;
+                e_len = Lj.len[r];
+                e_mag = Lj.magic[r];
+                pattern192(Lj.pat[r][0], Lj.pat[r][1], Lj.pat[r][2], e_len, e_mag, e_q);
+            }
+        };
+        const uint32_t pure_end = (flags & SCROLL_DEBUG_EMIT_NOPURE) ? 0u : tot_pure;
+        const bool do_store = !(flags & SCROLL_DEBUG_EMIT_NOSTORE);
+        if (pure_end) load_window(0);
+        uint32_t e0 = 0;                     /* entry holding virtual chunk v0 (uniform) */
+
+        /* one group of 64 virtual chunks at g with its own window upkeep:
+         * the fallback for iterations touching > 64 entries */
+        auto group1 = [&](uint32_t g) {
+            const uint32_t v = g + (uint32_t)lane;
+            const uint32_t vhi = min(g + 63u, pure_end - 1u);
+            uint64_t m = __ballot(e_vs <= vhi);
+            if ((m >> 63) && e0 != ebase && ebase + 64 < tot_pe) {
+                ebase = e0;
+                load_window(ebase);
+                m = __ballot(e_vs <= vhi);
+            }
+            const uint32_t ks = (uint32_t)__popcll(__ballot(e_vs <= g)) - 1u;
+            const uint32_t ke = (uint32_t)__popcll(m) - 1u;
+            uint32_t kk = ks;
+            for (uint32_t jb = ks + 1; jb <= ke; ++jb)
+                kk += v >= (uint32_t)__builtin_amdgcn_readlane((int)e_vs, (int)jb) ? 1u : 0u;
+            e0 = ebase + (uint32_t)__popcll(__ballot(e_vs <= g + 64u)) - 1u;
+            const int src = (int)(kk << 2);
+            const uint32_t K = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)e_K);
+            const uint32_t C = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)e_C);
+            const uint32_t len = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)e_len);
+            const uint32_t mag = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)e_mag);
+            uint32_t q[6], w[4];
+#pragma unroll
+            for (int z = 0; z < 6; ++z) q[z] = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)e_q[z]);
+            pure_words(K + (v << 7), len, mag, q, w);
+            if (v < pure_end && do_store) store_chunk(A, (c0 + (uint64_t)(uint32_t)(v + C)) << 4, w);
+        };
+
+        for (uint32_t v0 = 0; v0 < pure_end; v0 += 64u * PURE_U) {
+            const uint32_t vlast = min(v0 + 64u * PURE_U, pure_end) - 1u;
+            uint64_t m = __ballot(e_vs <= vlast);
+            if ((m >> 63) && e0 != ebase && ebase + 64 < tot_pe) {
+                ebase = e0;                              /* window must reach the groups */
+                load_window(ebase);
+                m = __ballot(e_vs <= vlast);
+            }
+            if ((m >> 63) && ebase + 64 < tot_pe) {      /* > 64 entries: group by group */
+                for (uint32_t g = v0; g <= vlast; g += 64u) group1(g);
+                continue;
+            }
+            /* per group: the entry holding its first chunk (ks) and the entries
+             * starting inside it (ks, ke]; lanes past the end are clamped to
+             * the last pure chunk and store the same bytes again */
+            uint32_t kk[PURE_U], vv[PURE_U];
+#pragma unroll
+            for (int u = 0; u < PURE_U; ++u) {
+                const uint32_t g = min(v0 + 64u * (uint32_t)u, vlast);
+                const uint32_t gh = min(g + 63u, vlast);
+                const uint32_t v = min(g + (uint32_t)lane, vlast);
+                const uint32_t ks = (uint32_t)__popcll(__ballot(e_vs <= g)) - 1u;
+                const uint32_t ke = (uint32_t)__popcll(__ballot(e_vs <= gh)) - 1u;
+                uint32_t k = ks;
+                for (uint32_t jb = ks + 1; jb <= ke; ++jb)
+                    k += v >= (uint32_t)__builtin_amdgcn_readlane((int)e_vs, (int)jb) ? 1u : 0u;
+                kk[u] = k;
+                vv[u] = v;
+            }
+            e0 = ebase + (uint32_t)__popcll(__ballot(e_vs <= v0 + 64u * PURE_U)) - 1u;
+            uint32_t w[PURE_U][4];
+            uint64_t addr[PURE_U];
+#pragma unroll
+            for (int u = 0; u < PURE_U; ++u) {
+                const int src = (int)(kk[u] << 2);
+                const uint32_t K = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)e_K);
+                const uint32_t C = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)e_C);
+                const uint32_t len = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)e_len);
+                const uint32_t mag = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)e_mag);
+                uint32_t q[6];
+#pragma unroll
+                for (int z = 0; z < 6; ++z) q[z] = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)e_q[z]);
+                pure_words(K + (vv[u] << 7), len, mag, q, w[u]);
+                addr[u] = (c0 + (uint64_t)(uint32_t)(vv[u] + C)) << 4;
+            }
+            if (do_store) {
+                /* byte-swap all groups first and keep them live together, so
+                 * the stores read distinct registers (no WAR stall behind a
+                 * queued store) */
+                uint32_t o[PURE_U][4];
+#pragma unroll
+                for (int u = 0; u < PURE_U; ++u)
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) o[u][k] = __builtin_bswap32(w[u][k]);
+                uint64_t ptr[PURE_U];
+#pragma unroll
+                for (int u = 0; u < PURE_U; ++u) {
+                    ptr[u] = (uint64_t)(uintptr_t)A + addr[u];
+                    asm volatile("" : "+v"(o[u][0]), "+v"(o[u][1]), "+v"(o[u][2]), "+v"(o[u][3]),
+                                 "+v"(ptr[u]));
+                }
+#pragma unroll
+                for (int u = 0; u < PURE_U; ++u) store_raw(ptr[u], o[u]);
+                asm volatile("" ::"v"(o[PURE_U - 1][0]), "v"(ptr[0]));
+            } else {
+#pragma unroll
+                for (int u = 0; u < PURE_U; ++u)
+                    asm volatile("" ::"v"(w[u][0]), "v"(w[u][1]), "v"(w[u][2]), "v"(w[u][3]));
+            }
+        }
+
+        mark(3);
+        if (stamps && lane == 0) stamp[6] = ((uint64_t)tot_pure << 32) | tot_mx;
+        /* 4. mixed phase: one lane per mixed chunk (header, run boundaries,
+         * NAL boundaries, the two partial chunks at the tile ends). */
+        const uint32_t mx_end = (flags & SCROLL_DEBUG_EMIT_NOMIXED) ? 0u : tot_mx;
+        for (uint32_t k = (uint32_t)lane; k < mx_end; k += 64) {
+            const uint32_t mm = W.mx[k];
+            const uint64_t c = c0 + (mm >> 6);
+            const uint64_t p = c << 4;
+            uint32_t w[4];
+            mixed_chunk(L, noff, cnt, (int)(mm & 63u), ((int64_t)p - (int64_t)B0) * 8, w);
+            if (p >= B0 && p + 16 <= B1) {
+                if (flags & SCROLL_DEBUG_EMIT_NOSTORE)
+                    asm volatile("" ::"v"(w[0]), "v"(w[1]), "v"(w[2]), "v"(w[3]));
+                else
+                    store_chunk(A, p, w);
+            } else {
+                for (int kk = 0; kk < 16; ++kk) {
+                    const uint64_t x = p + (uint64_t)kk;
+                    if (x < B0 || x >= B1) continue;
+                    A[x] = (uint8_t)(w[kk >> 2] >> (24 - 8 * (kk & 3)));
+                }
+            }
+        }
+    } else {
+        int j = 0;
+        for (uint64_t c = c0 + lane; c < c1; c += 64) {
+            const uint64_t p = c << 4;
             for (int k = 0; k < 16; ++k) {
                 uint64_t q = p + (uint64_t)k;
                 if (q < B0 || q >= B1) continue;
@@ -373,6 +659,13 @@ __global__ __launch_bounds__(EMIT_WAVES * 64) void k_emit(const DevStream *__res
                 A[q] = (uint8_t)tile_byte(L, noff, cnt, j, rel);
             }
         }
+    }
+    mark(4);
+    if (stamps && lane == 0) {
+        uint64_t hw = (uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 4);      /* HW_ID */
+        uint64_t xcc = (uint32_t)__builtin_amdgcn_s_getreg((15 << 11) | 20);    /* XCC_ID */
+        stamp[7] = (__builtin_amdgcn_s_memrealtime() & 0xffffffffull) | (hw << 32);
+        stamp[6] = (stamp[6] & 0x00ffffffffffffffull) | ((xcc & 0xff) << 56);
     }
     if (my_slow) serial_write(my_ctx, A + D[lane].out_off);
 }
@@ -492,6 +785,8 @@ struct ScrollBatch {
     int last_nframes = 0;
     std::vector<NalDesc> nal_cache;
     int nal_cache_valid = 0;
+    uint64_t *d_dbg = nullptr;
+    size_t dbg_slots = 0;
 };
 
 extern "C" {
@@ -570,6 +865,7 @@ void scroll_batch_destroy(ScrollBatch *b)
     (void)hipFree(b->d_off);
     (void)hipFree(b->d_nal);
     (void)hipFree(b->d_arena);
+    if (b->d_dbg) (void)hipFree(b->d_dbg);
     delete b;
 }
 
@@ -707,9 +1003,18 @@ static int launch(ScrollBatch *b, int nframes, int plan_mode, int nal_max, hipSt
     }
     int per_wg = EMIT_WAVES * TILE;
     int gx = (nal_max + per_wg - 1) / per_wg;
+    if (gx > 0 && (b->debug & SCROLL_DEBUG_EMIT_STAMPS)) {
+        size_t slots = (size_t)gx * S * EMIT_WAVES;
+        if (slots > b->dbg_slots) {
+            if (b->d_dbg) (void)hipFree(b->d_dbg);
+            HIPCHK(hipMalloc(&b->d_dbg, slots * 8 * sizeof(uint64_t)));
+            b->dbg_slots = slots;
+        }
+        HIPCHK(hipMemsetAsync(b->d_dbg, 0, slots * 8 * sizeof(uint64_t), hs));
+    }
     if (gx > 0) {
         hipLaunchKernelGGL(k_emit, dim3(gx, S), dim3(EMIT_WAVES * 64), 0, hs, b->d_st, b->d_nal,
-                           b->ld_nal, b->d_arena, (uint64_t)b->ld_arena, b->debug);
+                           b->ld_nal, b->d_arena, (uint64_t)b->ld_arena, b->debug, b->d_dbg);
         HIPCHK(hipGetLastError());
     }
     if (b->timing) {
@@ -747,24 +1052,28 @@ int scroll_batch_compose_ex(ScrollBatch *b, int nframes, void *hip_stream, int f
 int scroll_batch_sync(ScrollBatch *b)
 {
     if (!b) return SCROLL_ERR_ARG;
-    int rc = batch_host_sync(b);
-    if (rc) return rc;
+    {
+        int rc0 = batch_host_sync(b);
+        if (rc0) return rc0;
+    }
     if (b->timed_pending) {
         HIPCHK(hipEventElapsedTime(&b->ms[0], b->ev[0], b->ev[1]));
         HIPCHK(hipEventElapsedTime(&b->ms[1], b->ev[1], b->ev[2]));
         b->timed_pending = 0;
     }
+    int rc = SCROLL_OK;
     for (int s = 0; s < b->nstreams; ++s) {
-        if (b->h_st[s].err & SCROLL_DEVERR_OVERFLOW) {
-            set_err("stream %d: output arena overflow (%llu + batch > %llu bytes)", s,
+        if (!b->h_st[s].err) continue;
+        if (rc == SCROLL_OK)
+            set_err("stream %d: output arena overflow (%llu bytes used, capacity %llu)", s,
                     (unsigned long long)b->h_st[s].out_pos,
                     (unsigned long long)b->h_st[s].out_cap);
-            b->h_st[s].err = 0;
-            (void)hipMemcpy(&b->d_st[s].err, &b->h_st[s].err, sizeof(int32_t),
-                            hipMemcpyHostToDevice);
-            return SCROLL_ERR_OVERFLOW;
-        }
+        rc = SCROLL_ERR_OVERFLOW;
+        b->h_st[s].err = 0;                      /* reported once, then cleared */
+        HIPCHK(hipMemcpy(&b->d_st[s].err, &b->h_st[s].err, sizeof(int32_t),
+                         hipMemcpyHostToDevice));
     }
+    if (rc) return rc;
     return SCROLL_OK;
 }
 
@@ -842,9 +1151,9 @@ int scroll_batch_nal_info(ScrollBatch *b, int s, int i, int *kind, int *offset_p
     return SCROLL_OK;
 }
 
-int scroll_batch_kernel_stats(ScrollBatch *b, int which, double *total_ms, int *count)
+int scroll_batch_kernel_stats(ScrollBatch *b, double *plan_ms, double *emit_ms, int *count)
 {
-    if (!b || which < 0 || which > 1) return SCROLL_ERR_ARG;
+    if (!b) return SCROLL_ERR_ARG;
     int rc = batch_host_sync(b);
     if (rc) return rc;
     HIPCHK(hipStreamSynchronize(b->last));
@@ -857,11 +1166,22 @@ int scroll_batch_kernel_stats(ScrollBatch *b, int which, double *total_ms, int *
         b->acc_n++;
     }
     b->ring_used = 0;
-    if (total_ms) *total_ms = b->acc_ms[which];
+    if (plan_ms) *plan_ms = b->acc_ms[0];
+    if (emit_ms) *emit_ms = b->acc_ms[1];
     if (count) *count = b->acc_n;
     b->acc_ms[0] = b->acc_ms[1] = 0;
     b->acc_n = 0;
     return SCROLL_OK;
+}
+
+long long scroll_batch_debug_stamps(ScrollBatch *b, uint64_t *dst, long long max_slots)
+{
+    if (!b || batch_host_sync(b) || !b->d_dbg) return 0;
+    long long n = (long long)b->dbg_slots < max_slots ? (long long)b->dbg_slots : max_slots;
+    if (hipMemcpy(dst, b->d_dbg, (size_t)n * 8 * sizeof(uint64_t), hipMemcpyDeviceToHost) !=
+        hipSuccess)
+        return 0;
+    return n;
 }
 
 unsigned long long scroll_batch_last_bytes(ScrollBatch *b)

@@ -12,7 +12,7 @@ import ctypes
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "libh264scroll.so")
+LIB_PATH = os.environ.get("H264SCROLL_LIB") or os.path.join(HERE, "lib", "libh264scroll.so")
 
 SCROLL_OK = 0
 SCROLL_ERR_NO_DEVICE = -1
@@ -24,6 +24,12 @@ SCROLL_ERR_CONFIG = -6
 SCROLL_MODE_COMPOSER = 0
 SCROLL_MODE_EXPERIMENT = 1
 SCROLL_DEBUG_FORCE_SERIAL = 1
+SCROLL_DEBUG_EMIT_NOSTORE = 2
+SCROLL_DEBUG_EMIT_ZEROS = 4
+SCROLL_DEBUG_EMIT_BUILD = 8
+SCROLL_DEBUG_EMIT_NOPURE = 16
+SCROLL_DEBUG_EMIT_NOMIXED = 32
+SCROLL_DEBUG_EMIT_STAMPS = 64
 SCROLL_COMPOSE_REWIND = 1
 MAX_WAYPOINTS = 8
 MV_LIMIT_PX = 496
@@ -115,9 +121,11 @@ def _load():
         "scroll_batch_sync": (ctypes.c_int, [ctypes.c_void_p]),
         "scroll_batch_compose_ex": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
                                                    ctypes.c_int]),
-        "scroll_batch_kernel_stats": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int,
+        "scroll_batch_kernel_stats": (ctypes.c_int, [ctypes.c_void_p, P(ctypes.c_double),
                                                      P(ctypes.c_double), P(ctypes.c_int)]),
         "scroll_batch_last_bytes": (ctypes.c_ulonglong, [ctypes.c_void_p]),
+        "scroll_batch_debug_stamps": (ctypes.c_longlong, [ctypes.c_void_p, P(ctypes.c_uint64),
+                                                          ctypes.c_longlong]),
         "scroll_batch_last_nals": (ctypes.c_longlong, [ctypes.c_void_p]),
         "scroll_batch_get_config": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int,
                                                    P(ComposerConfig)]),
@@ -330,12 +338,12 @@ class Batch:
     def kernel_ms(self, which):
         return lib.scroll_batch_kernel_ms(self.h, which)
 
-    def kernel_stats(self, which):
-        """(summed ms, count) of kernel `which` (0 plan, 1 emit) since last call"""
-        t, n = ctypes.c_double(), ctypes.c_int()
-        self._chk(lib.scroll_batch_kernel_stats(self.h, which, ctypes.byref(t), ctypes.byref(n)),
-                  "kernel_stats")
-        return t.value, n.value
+    def kernel_stats(self):
+        """(plan ms, emit ms, composes) summed since the last call"""
+        a, e, n = ctypes.c_double(), ctypes.c_double(), ctypes.c_int()
+        self._chk(lib.scroll_batch_kernel_stats(self.h, ctypes.byref(a), ctypes.byref(e),
+                                                ctypes.byref(n)), "kernel_stats")
+        return a.value, e.value, n.value
 
     def last_bytes(self):
         return lib.scroll_batch_last_bytes(self.h)

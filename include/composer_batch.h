@@ -49,8 +49,14 @@ extern "C" {
 #define SCROLL_MODE_COMPOSER   0    /* waypoint NAL in addition to the scroll NAL */
 #define SCROLL_MODE_EXPERIMENT 1    /* waypoint NAL instead of the scroll NAL     */
 
-/* debug flags (tests) */
+/* debug flags (tests / profiling ablations; outputs are wrong for 2, 4, 8) */
 #define SCROLL_DEBUG_FORCE_SERIAL 1 /* every NAL through the serial device path   */
+#define SCROLL_DEBUG_EMIT_NOSTORE 2 /* k_emit computes every chunk, stores none   */
+#define SCROLL_DEBUG_EMIT_ZEROS   4 /* k_emit stores zero chunks, computes none   */
+#define SCROLL_DEBUG_EMIT_BUILD   8 /* k_emit builds the layouts and stops        */
+#define SCROLL_DEBUG_EMIT_NOPURE 16 /* k_emit skips the pure-chunk phase          */
+#define SCROLL_DEBUG_EMIT_NOMIXED 32 /* k_emit skips the mixed-chunk phase        */
+#define SCROLL_DEBUG_EMIT_STAMPS 64 /* k_emit records s_memtime per phase per wave */
 
 typedef struct ScrollBatch ScrollBatch;
 
@@ -102,8 +108,12 @@ int scroll_batch_nal_info(ScrollBatch *b, int s, int i, int *kind, int *offset_p
  * which 0 = plan kernel, 1 = emit kernel.  Enable before compose. */
 int scroll_batch_enable_timing(ScrollBatch *b, int on);
 float scroll_batch_kernel_ms(ScrollBatch *b, int which);
-/* all composes since the last call: summed kernel ms and count (then reset) */
-int scroll_batch_kernel_stats(ScrollBatch *b, int which, double *total_ms, int *count);
+/* all timed composes since the last call: summed plan / emit kernel ms and
+ * the number of composes; the accumulators are reset afterwards */
+int scroll_batch_kernel_stats(ScrollBatch *b, double *plan_ms, double *emit_ms, int *count);
+/* SCROLL_DEBUG_EMIT_STAMPS: copy the per-wave phase stamps of the last
+ * compose (8 x u64 per wave slot); returns the number of wave slots */
+long long scroll_batch_debug_stamps(ScrollBatch *b, uint64_t *dst, long long max_slots);
 /* bytes appended to every arena by the last compose (sum over streams) */
 unsigned long long scroll_batch_last_bytes(ScrollBatch *b);
 /* NAL units planned by the last compose (sum over streams) */

@@ -45,6 +45,23 @@ def synthetic_offsets(first, nstreams, nframes, h):
     return np.where(p < h, p, 2 * h - p).astype(np.int32)
 
 
+def shard_streams(rank, world, per_gpu):
+    """Static contiguous stream shard of rank (weak scaling): [first, first + per_gpu)."""
+    if not (0 <= rank < world) or per_gpu <= 0:
+        raise ValueError("bad shard")
+    return rank * per_gpu, per_gpu
+
+
+def max_over_ranks(x, dist):
+    """Elapsed time of the slowest rank (gloo all-reduce MAX; identity for one rank)."""
+    if dist is None:
+        return float(x)
+    import torch
+    t = torch.tensor([float(x)], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
 def cpu_baseline(wl, threads):
     """Oracle (C restatement, bit-exact to the reference) on host cores."""
     repo_oracle = os.path.join(HERE, "oracle")
@@ -107,7 +124,7 @@ def main():
     torch.cuda.set_device(local)
     stream = torch.cuda.current_stream()
     S, F, W, H = wl["streams"], wl["frames"], wl["w"], wl["h"]
-    first = rank * S                               # static contiguous shard
+    first, _ = shard_streams(rank, world, S)       # static contiguous shard
     per_frame_bound = 2 * (64 + (W // 16) * (H // 16))
     b = hs.Batch(S, F, F * per_frame_bound + (1 << 16), device=local)
     for _ in range(S):
@@ -140,11 +157,7 @@ def main():
     step_nals = b.last_nals()
     b.enable_timing(False)
 
-    el = t1 - t0
-    if dist:
-        t = torch.tensor([el], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
+    el = max_over_ranks(t1 - t0, dist)
     frames_total = S * F * args.steps * world
     value = frames_total / el
     ms_step = 1000.0 * el / args.steps

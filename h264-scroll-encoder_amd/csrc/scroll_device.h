@@ -29,11 +29,15 @@ namespace scroll {
 
 constexpr int MVL = 496;          /* MV_LIMIT_PX, include/h264_writer.h:24       */
 constexpr int RUNS_MAX = 9;       /* runs per NAL on the fast path (row-class max) */
-constexpr int HDR_WORDS = 12;     /* 384 bits: 40-bit NAL prefix + slice header   */
+constexpr int HDR_WORDS = 8;      /* 256 bits: 40-bit NAL prefix + slice header
+                                     (worst realistic case ~209 bits: 8 waypoints +
+                                     MMCO; longer headers take the serial path)  */
 constexpr int EP_ZERO_RUN = 22;   /* 00 00 0x (x<=3) needs >= 22 consecutive 0s   */
 
-/* Per-NAL emission layout, built in LDS by one lane.  260 bytes = 65 dwords:
- * an odd stride keeps lanes that read different NALs on different banks. */
+/* Per-NAL emission layout, built in LDS by one lane.  172 bytes = 43 dwords:
+ * an odd stride keeps lanes that read different NALs on different banks.
+ * Everything derivable from a run's codeword length (mul-high magic, the
+ * pattern's continuation past 64 bits) lives in the per-wave LenLut. */
 struct Lay {
     uint32_t nal_bits;            /* 8 * NAL bytes (prefix + RBSP incl. padding)  */
     uint32_t used_bits;           /* prefix + header + runs + stop bit            */
@@ -41,11 +45,24 @@ struct Lay {
     uint32_t nruns;
     uint32_t hdr[HDR_WORDS];      /* prefix + header bits, MSB first              */
     uint32_t run_end[RUNS_MAX];   /* NAL bit where run r ends                     */
-    uint32_t pat[RUNS_MAX][3];    /* run codeword repeated over 96 bits           */
-    uint32_t magic[RUNS_MAX];     /* ceil(2^32 / len): x mod len by mul-high      */
+    uint32_t pat[RUNS_MAX][2];    /* run codeword repeated over 64 bits           */
     uint8_t len[RUNS_MAX];        /* codeword length (1..64)                      */
     uint8_t pad_[7];
 };
+static_assert(sizeof(Lay) == 172, "Lay stride must stay an odd number of dwords");
+
+/* Per codeword length len in 1..64 (index len - 1): the mul-high magic
+ * ceil(2^32 / len) and the pattern phases 64 / 96 / 128 / 160 mod len. */
+struct LenLut {
+    uint32_t magic[64];
+    uint32_t mods[64];            /* bytes: 64%len | 96%len << 8 | 128%len << 16 | 160%len << 24 */
+};
+
+__device__ inline void lut_entry(uint32_t len, uint32_t &magic, uint32_t &mods)
+{
+    magic = len == 1 ? 0xffffffffu : 0xffffffffu / len + 1u;   /* ceil(2^32/len), len >= 2 */
+    mods = (64u % len) | ((96u % len) << 8) | ((128u % len) << 16) | ((160u % len) << 24);
+}
 
 /* Everything the syntax of one NAL depends on. */
 struct NalCtx {
@@ -336,8 +353,13 @@ __device__ inline void fill_pattern(uint32_t *p, uint64_t v, int len)
     for (int rl = len; rl < 64; rl <<= 1) r |= r >> rl;
     p[0] = (uint32_t)(r >> 32);
     p[1] = (uint32_t)r;
-    int d = 64 % len;
-    p[2] = (uint32_t)((r << d) >> 32);
+}
+
+/* bits [64, 96) of the repetition: the 64-bit pattern at phase 64 mod len
+ * (< 32 for every len <= 64) */
+__device__ inline uint32_t pattern_word2(uint32_t p0, uint32_t p1, uint32_t m64)
+{
+    return m64 ? __builtin_amdgcn_alignbit(p0, p1, 32 - m64) : p0;
 }
 
 template <bool CHECK>
@@ -363,8 +385,6 @@ struct RunAcc {
             if (L) {
                 L->len[n] = (uint8_t)len;
                 L->run_end[n] = (uint32_t)end;
-                /* ceil(2^32 / len) = floor((2^32 - 1) / len) + 1 for len >= 2 */
-                L->magic[n] = len == 1 ? 0xffffffffu : 0xffffffffu / (uint32_t)len + 1u;
                 fill_pattern(L->pat[n], v, len);
             }
             n++;
@@ -505,7 +525,8 @@ __device__ inline uint32_t lay_bits32(const Lay *L, uint32_t b)
             uint32_t len = L->len[r];
             uint32_t phi = umod_small(pos - start, len);
             const uint32_t *p = L->pat[r];
-            w = phi < 32 ? funnel(p[0], p[1], (int)phi) : funnel(p[1], p[2], (int)(phi - 32));
+            const uint32_t p2 = pattern_word2(p[0], p[1], 64u % len);
+            w = phi < 32 ? funnel(p[0], p[1], (int)phi) : funnel(p[1], p2, (int)(phi - 32));
             seg_end = L->run_end[r];
         }
         uint32_t avail = seg_end - pos;
@@ -519,11 +540,11 @@ __device__ inline uint32_t lay_bits32(const Lay *L, uint32_t b)
 
 
 /* one byte of the tile at tile byte rel (fast NALs only) */
-__device__ inline uint32_t tile_byte(const Lay *L, const uint32_t *noff, int cnt, int &j,
+__device__ inline uint32_t tile_byte(const Lay *L, const int32_t *noff, int cnt, int &j,
                                      uint32_t rel)
 {
-    while (j + 1 < cnt && noff[j + 1] <= rel) j++;
-    return lay_bits32(&L[j], (rel - noff[j]) * 8u) >> 24;
+    while (j + 1 < cnt && (uint32_t)noff[j + 1] <= rel) j++;
+    return lay_bits32(&L[j], (rel - (uint32_t)noff[j]) * 8u) >> 24;
 }
 
 
@@ -554,15 +575,15 @@ __device__ inline uint32_t pat_window(uint32_t p0, uint32_t p1, uint32_t p2, uin
 /* 192-bit expansion of a run pattern: words 3..5 continue the repetition
  * (bits [96, 192)), so any 128-bit window at phase phi < 64 is 4 funnel
  * shifts of 5 consecutive words with ONE shift amount. */
-__device__ inline void pattern192(uint32_t p0, uint32_t p1, uint32_t p2, uint32_t len,
-                                  uint32_t magic, uint32_t q[6])
+__device__ inline void pattern192(uint32_t p0, uint32_t p1, uint32_t mods, uint32_t q[6])
 {
+    const uint32_t p2 = pattern_word2(p0, p1, mods & 255u);
     q[0] = p0;
     q[1] = p1;
     q[2] = p2;
-    q[3] = pat_window(p0, p1, p2, mod_magic(96u, len, magic));
-    q[4] = pat_window(p0, p1, p2, mod_magic(128u, len, magic));
-    q[5] = pat_window(p0, p1, p2, mod_magic(160u, len, magic));
+    q[3] = pat_window(p0, p1, p2, (mods >> 8) & 255u);
+    q[4] = pat_window(p0, p1, p2, (mods >> 16) & 255u);
+    q[5] = pat_window(p0, p1, p2, mods >> 24);
 }
 
 /* 128 bits of a run's repetition starting at pattern phase phi (< len <= 64);
@@ -602,15 +623,16 @@ __device__ inline int32_t clamp_bits(int64_t x)
 }
 
 /* 128 bits of the tile at tile bit x0 (x0 = 8 * (chunk byte - tile start),
- * negative for the chunk straddling the tile start), j = the NAL holding the
- * chunk's first bit (0 for that leading chunk).  The chunk is the OR of the
+ * negative before the tile start), j = the first layout that can hold a bit
+ * of the chunk; noff[j] = layout j's first byte relative to the tile start
+ * (negative for the previous tile's NALs), layouts j .. cnt-1 are read.  The chunk is the OR of the
  * pieces of every segment it meets -- header words, periodic runs, and the
  * same for the following NALs -- each run taken at its phase at x0 (a
  * negative offset when the run starts inside the chunk) and masked to its
  * bit range, so no per-word segment search is needed.  Bits past the last
  * NAL of the tile read as zero. */
-__device__ inline void mixed_chunk(const Lay *L, const uint32_t *noff, int cnt, int j, int64_t x0,
-                                   uint32_t w[4])
+__device__ inline void mixed_chunk(const Lay *L, const int32_t *noff, int cnt, int j, int64_t x0,
+                                   const LenLut &T, uint32_t w[4])
 {
     w[0] = w[1] = w[2] = w[3] = 0u;
     for (; j < cnt; ++j) {
@@ -647,7 +669,7 @@ __device__ inline void mixed_chunk(const Lay *L, const uint32_t *noff, int cnt, 
         }
         for (; r < nr && (int64_t)s0 < rel0 + 128; ++r) {
             const uint32_t s1 = Lj.run_end[r];
-            const uint32_t len = Lj.len[r], mag = Lj.magic[r];
+            const uint32_t len = Lj.len[r], mag = T.magic[len - 1];
             const int64_t d = rel0 - (int64_t)s0;
             uint32_t phi;
             if (d >= 0) {
@@ -657,7 +679,7 @@ __device__ inline void mixed_chunk(const Lay *L, const uint32_t *noff, int cnt, 
                 phi = m ? len - m : 0u;
             }
             uint32_t q[6], pw[4];
-            pattern192(Lj.pat[r][0], Lj.pat[r][1], Lj.pat[r][2], len, mag, q);
+            pattern192(Lj.pat[r][0], Lj.pat[r][1], T.mods[len - 1], q);
             pure_words_phi(phi, q, pw);
             const int32_t lo = clamp_bits((int64_t)s0 - rel0);
             const int32_t hi = clamp_bits((int64_t)s1 - rel0);
@@ -676,6 +698,108 @@ __device__ inline void pure_range(uint64_t Aj, uint32_t s0, uint32_t s1, uint64_
     cp0 = (Aj + s0 + 127) >> 7;
     cp1 = (Aj + s1) >> 7;
     if (cp1 < cp0) cp1 = cp0;
+}
+
+/* ---------------------------------------------------------------------- */
+/* k_emit tile plan (shared with the CPU test harness tests/hostsim).       */
+/* Layout i of a tile is NAL t0 - SEAM_XB + i; the tile's own NALs are      */
+/* layouts SEAM_XB .. SEAM_XB + cnt - 1; noff[i] = layout i's first byte     */
+/* relative to the tile start B0.  Every 128-byte line in [line(B0),        */
+/* line(B1)) is produced whole by the tile, the two seam lines included     */
+/* when their neighbour bytes are available (see k_emit).                    */
+/* ---------------------------------------------------------------------- */
+constexpr int SEAM_XB = 2, SEAM_XA = 2;   /* neighbour layouts before / after */
+
+struct Seams {
+    bool head_full, head_rmw, tail_full;
+    int hj;                 /* first layout feeding the head line          */
+    int t_hi;               /* one past the last layout feeding the tail   */
+    uint64_t cs, ce;        /* chunk range of the tile's single store pass */
+};
+
+/* lo / hi: valid layouts; slow_mask bit i: layout i is a serial-path NAL */
+__device__ inline Seams seam_plan(uint64_t B0, uint64_t B1, int t0, int cnt, int nnal, int lo,
+                                  int hi, const int32_t *noff, uint64_t slow_mask)
+{
+    Seams z;
+    const uint64_t ls = B0 & ~127ull, le = (B1 + 127) & ~127ull;
+    z.head_full = B0 == ls;
+    z.head_rmw = false;
+    z.tail_full = B1 == le;
+    z.hj = SEAM_XB;
+    z.t_hi = SEAM_XB + cnt;
+    if (!z.head_full) {
+        if (t0 == 0) {                          /* previous compose's bytes */
+            z.head_full = z.head_rmw = true;
+        } else {
+            for (int i = SEAM_XB - 1; i >= lo; --i) {
+                if ((slow_mask >> i) & 1ull) break;
+                if ((int64_t)noff[i] <= (int64_t)ls - (int64_t)B0) {
+                    z.head_full = true;
+                    z.hj = i;
+                    break;
+                }
+            }
+        }
+    }
+    if (!z.tail_full) {
+        if (t0 + cnt == nnal) {                 /* past the stream's end: zeros */
+            z.tail_full = true;
+        } else {
+            for (int i = SEAM_XB + cnt; i < hi; ++i) {
+                if ((slow_mask >> i) & 1ull) break;
+                if ((int64_t)noff[i + 1] >= (int64_t)le - (int64_t)B0 ||
+                    t0 - SEAM_XB + i == nnal - 1) {
+                    z.tail_full = true;
+                    z.t_hi = i + 1;
+                    break;
+                }
+            }
+        }
+    }
+    z.cs = z.head_full ? (ls >> 4) : ((B0 + 15) >> 4);
+    z.ce = z.tail_full ? (le >> 4) : (B1 >> 4);
+    if (z.ce < z.cs) z.ce = z.cs;
+    return z;
+}
+
+/* chunks [own0, own1) whose first byte is in own NAL i (the first own NAL
+ * also takes the head chunks, the last one the tail chunks) */
+__device__ inline void owned_chunks(const Seams &z, uint64_t B0, const int32_t *noff, int i, int cnt,
+                                    uint64_t &own0, uint64_t &own1)
+{
+    const uint64_t Aj = 8 * (B0 + (uint64_t)(int64_t)noff[i]);
+    const uint64_t Aj1 = 8 * (B0 + (uint64_t)(int64_t)noff[i + 1]);
+    own0 = i == SEAM_XB ? z.cs : (Aj + 127) >> 7;
+    own1 = i == SEAM_XB + cnt - 1 ? z.ce : (Aj1 + 127) >> 7;
+    if (own1 < own0) own1 = own0;
+}
+
+/* Walk the owned chunks of a fast NAL in order as entries: emit(r, c0, c1)
+ * with r = run index for a PURE entry (chunks inside run r) or -1 for a
+ * MIXED entry (a maximal gap between pure entries). */
+template <class F>
+__device__ inline void entry_walk(const Lay &Lj, uint64_t Aj, uint64_t own0, uint64_t own1, F &&emit)
+{
+    uint64_t prev = own0;
+    uint32_t s0 = Lj.hdr_bits;
+    for (uint32_t r = 0; r < Lj.nruns; ++r) {
+        const uint32_t s1 = Lj.run_end[r];
+        uint64_t cp0, cp1;
+        pure_range(Aj, s0, s1, cp0, cp1);
+        s0 = s1;
+        if (cp1 <= cp0) continue;
+        if (cp0 > prev) emit(-1, prev, cp0);
+        emit((int)r, cp0, cp1);
+        prev = cp1;
+    }
+    if (own1 > prev) emit(-1, prev, own1);
+}
+
+/* first layout holding a bit of chunk c (byte p = 16 c) of own NAL i */
+__device__ inline uint32_t mixed_first(const Seams &z, uint64_t p, uint64_t B0, int i)
+{
+    return p < B0 ? (uint32_t)(z.head_rmw ? SEAM_XB : z.hj) : (uint32_t)i;
 }
 
 /* ---------------------------------------------------------------------- */

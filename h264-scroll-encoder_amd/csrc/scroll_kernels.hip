@@ -293,34 +293,51 @@ __global__ __launch_bounds__(PLAN_THREADS) void k_plan(DevStream *__restrict__ s
 }
 
 /* ---------------------------------------------------------------------- */
-/* k_emit: each wave owns TILE consecutive NAL units of one stream.         */
-/*  1. lane i builds the run layout of NAL t0+i in LDS.                      */
-/*  2. lane i classifies the 16-byte arena chunks it owns (first byte in    */
-/*     NAL i): PURE chunks lie inside one periodic run, the rest are MIXED. */
-/*     Wave scans turn both into compact per-wave lists in LDS.             */
-/*  3. PURE phase: the wave walks the pure list 64 chunks at a time with    */
-/*     wave-uniform run data (SGPRs): phase by mul-high, 4 words from the   */
-/*     run's 96-bit pattern, one 16-B store per lane.  No divergence.       */
-/*  4. MIXED phase: one lane per mixed chunk, generic bit extraction across */
-/*     header / runs / NAL boundaries; byte stores at the tile's two ends.  */
-/*  Tiles holding a serial-path NAL use the generic path for every byte and */
-/*  the owning lane writes that NAL serially.                               */
+/* k_emit: one wave per tile of TILE consecutive NAL units of one stream.   */
+/*                                                                          */
+/* Rule: every 128-byte line of an arena is written whole, by one wave, in  */
+/* one pass.  A line written in pieces at different times (16- to 64-byte   */
+/* holes filled later) costs the memory system up to 2x (DESIGN.md §6,      */
+/* tools/store_floor.hip).  So:                                             */
+/*  1. lanes build the run layouts of the tile's NALs plus up to XB / XA    */
+/*     neighbour NALs, which supply the bytes of the two seam lines the     */
+/*     tile shares with the adjacent tiles;                                 */
+/*  2. the wave's chunk range covers whole lines [line(B0), line(B1)).      */
+/*     Chunks are classified into PURE entries (runs of chunks inside one   */
+/*     periodic run) and MIXED entries (runs of chunks holding NAL headers, */
+/*     run boundaries, NAL boundaries, seam bytes);                         */
+/*  3. mixed chunks are computed, one lane each, into LDS;                  */
+/*  4. one pass streams every chunk of the range in order, 4 groups of 64   */
+/*     chunks per iteration: each lane finds its entry (entry-start flag    */
+/*     map + mbcnt), pulls the entry data by ds_bpermute and either expands */
+/*     the run pattern at its phase or copies its mixed words from LDS.     */
+/* Seam lines: both neighbours compute the identical full line and write    */
+/* it (benign duplicate); a side whose neighbour bytes cannot be computed   */
+/* here (serial-path or too many tiny neighbour NALs) writes only its own   */
+/* bytes of that line.  A stream's first tile in a launch merges the line   */
+/* head from memory (the previous compose's bytes); its last tile zero-     */
+/* fills its line tail (arena slack).  Tiles holding a serial-path NAL use  */
+/* the generic byte path and the owning lane writes that NAL serially.      */
 /* ---------------------------------------------------------------------- */
-#ifndef SCROLL_PURE_U
-#define SCROLL_PURE_U 4
-#endif
-constexpr int PURE_U = SCROLL_PURE_U;   /* 64-chunk groups per pure-phase iteration */
-constexpr int MAXPE = 5 * TILE;   /* pure-run entries per wave                */
-constexpr int MAXMX = 16 * TILE;  /* mixed chunks per wave                    */
-constexpr uint32_t PE_VS_MASK = (1u << 22) - 1;   /* tiles < 64 MB: chunks < 2^22 */
-static_assert(TILE <= 64, "owner NAL index is 6 bits");
+constexpr int PURE_U = 4;         /* 64-chunk groups per stream iteration      */
+constexpr int XB = SEAM_XB, XA = SEAM_XA;   /* neighbour layouts before / after the tile */
+constexpr int NL = XB + TILE + XA;
+constexpr int MAXPE = 8 * TILE;   /* pure + mixed entries per wave             */
+constexpr int MAXMX = 6 * TILE;   /* mixed chunks per wave (~3-4 per NAL)      */
+constexpr uint32_t PE_VS_MASK = (1u << 22) - 1;   /* chunks of a tile < 2^22   */
+constexpr uint32_t PE_MIXED = 15u;                /* run field of a mixed entry */
+static_assert(NL <= 64, "layout index is 6 bits and one lane builds each layout");
+static_assert(PURE_U == 4, "the flag map packs 4 groups per lane dword");
 
 struct EmitWaveLds {
-    Lay lay[TILE];
-    uint32_t noff[TILE + 1];
-    uint32_t pe_cb[MAXPE];        /* first pure chunk, relative to c0         */
-    uint32_t pe_vj[MAXPE];        /* virtual start | nal << 22 | run << 28     */
-    uint32_t mx[MAXMX];           /* (chunk rel c0 << 6) | owner nal          */
+    Lay lay[NL];
+    int32_t noff[NL + 1];         /* layout i's first byte - B0 (signed)       */
+    uint32_t pe_cb[MAXPE];        /* mixed entry: index of its first chunk in mw */
+    uint32_t pe_vj[MAXPE];        /* first chunk (rel cs) | layout << 22 | run << 28 */
+    uint32_t mx[MAXMX];           /* mixed chunk: (chunk rel cs) << 6 | first layout */
+    alignas(16) uint32_t mw[MAXMX][4];   /* mixed chunk words, MSB first (ds_read_b128) */
+    uint32_t flg[64];             /* stream loop: entry-start flags, byte 4 p + u
+                                     = an entry starts at chunk v0 + 64 u + p   */
 };
 
 /* 16-B global store to an integer address (address space 1: a
@@ -337,22 +354,15 @@ __device__ inline void store_raw(uint64_t addr, const uint32_t o[4])
     *reinterpret_cast<gu32x4 *>(addr) = v;
 }
 
-#ifndef SCROLL_NT_STORE
-#define SCROLL_NT_STORE 0
-#endif
-__device__ inline void store_chunk(uint8_t *A, uint64_t p, const uint32_t w[4])
+/* MSB-first words of a chunk whose bytes < first are outside this wave */
+__device__ inline void store_bytes(uint8_t *A, uint64_t p, uint64_t lo, uint64_t hi,
+                                   const uint32_t w[4])
 {
-    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-    u32x4 o;
-    o.x = __builtin_bswap32(w[0]);
-    o.y = __builtin_bswap32(w[1]);
-    o.z = __builtin_bswap32(w[2]);
-    o.w = __builtin_bswap32(w[3]);
-#if SCROLL_NT_STORE
-    __builtin_nontemporal_store(o, reinterpret_cast<u32x4 *>(A + p));
-#else
-    *reinterpret_cast<u32x4 *>(A + p) = o;
-#endif
+    for (int k = 0; k < 16; ++k) {
+        const uint64_t x = p + (uint64_t)k;
+        if (x < lo || x >= hi) continue;
+        A[x] = (uint8_t)(w[k >> 2] >> (24 - 8 * (k & 3)));
+    }
 }
 
 __global__ __launch_bounds__(EMIT_WAVES * 64) void k_emit(const DevStream *__restrict__ st,
@@ -363,11 +373,20 @@ __global__ __launch_bounds__(EMIT_WAVES * 64) void k_emit(const DevStream *__res
 {
     __shared__ EmitWaveLds s_w[EMIT_WAVES];
     __shared__ int32_t s_cfg[8], s_wo[8], s_wl[8], s_wv[8];
+    __shared__ LenLut s_lut;
 
     const int s = blockIdx.y;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = (int)uni((uint32_t)(tid >> 6));      /* wave-uniform -> SGPR */
     const DevStream *S = st + s;
+    const int t0 = (blockIdx.x * EMIT_WAVES + wave) * TILE;
+    /* lane i <-> layout i <-> NAL t0 - XB + i.  Every start-up load in one
+     * memory round trip: the descriptors (bounded by the descriptor
+     * capacity; lanes past nnal are ignored below), the stream config and
+     * its waypoint table. */
+    const int ti = t0 - XB + lane;
+    NalDesc d{};
+    if (lane < NL && ti >= 0 && ti < ld_nal) d = nal[(size_t)s * ld_nal + ti];
     if (tid < 8) {
         s_wo[tid] = S->wp_off[tid];
         s_wl[tid] = S->wp_lt[tid];
@@ -377,12 +396,14 @@ __global__ __launch_bounds__(EMIT_WAVES * 64) void k_emit(const DevStream *__res
         s_cfg[0] = S->w; s_cfg[1] = S->h; s_cfg[2] = S->log2_mfn; s_cfg[3] = S->poc_type;
         s_cfg[4] = S->log2_poc; s_cfg[5] = S->deblock;
     }
-    __syncthreads();
+    if (tid < 64) lut_entry((uint32_t)tid + 1u, s_lut.magic[tid], s_lut.mods[tid]);
     const int nnal = S->nnal;
-    const int t0 = (blockIdx.x * EMIT_WAVES + wave) * TILE;
+    __syncthreads();
     if (t0 >= nnal) return;
     const int cnt = min(TILE, nnal - t0);
-    const NalDesc *D = nal + (size_t)s * ld_nal + t0;
+    const int lo = max(0, XB - t0);                       /* first valid layout   */
+    const int hi = XB + cnt + min(XA, nnal - t0 - cnt);   /* one past the last    */
+    const LenLut &T = s_lut;
     EmitWaveLds &W = s_w[wave];
     const bool stamps = (flags & SCROLL_DEBUG_EMIT_STAMPS) && dbg;
     uint64_t *stamp = dbg + ((size_t)(blockIdx.y * gridDim.x + blockIdx.x) * EMIT_WAVES + wave) * 8;
@@ -395,19 +416,19 @@ __global__ __launch_bounds__(EMIT_WAVES * 64) void k_emit(const DevStream *__res
     mark(0);
     if (stamps && lane == 0) stamp[5] = __builtin_amdgcn_s_memrealtime();
     Lay *L = W.lay;
-    uint32_t *noff = W.noff;
+    int32_t *noff = W.noff;
     uint8_t *A = arena + (size_t)s * ld_arena;
 
-    /* 1. layouts */
-    const uint64_t B0 = D[0].out_off;
+    /* 1. layouts (own NALs + neighbours) */
+    const uint64_t B0 = ((uint64_t)__builtin_amdgcn_readlane((int)(uint32_t)(d.out_off >> 32), XB) << 32) |
+                        (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)d.out_off, XB);
+    const bool valid = lane >= lo && lane < hi;
+    const bool own = lane >= XB && lane < XB + cnt;
     bool my_slow = false;
     NalCtx my_ctx;
-    uint32_t my_size = 0;
-    if (lane < cnt) {
-        NalDesc d = D[lane];
+    if (valid) {
         my_ctx = make_ctx(s_cfg, s_wo, s_wl, s_wv, d);
         my_slow = d.slow != 0;
-        my_size = d.size;
         if (!my_slow) {
             uint32_t sz;
             build_nal<true, false>(my_ctx, &L[lane], &sz);   /* plan proved it fast */
@@ -417,185 +438,133 @@ __global__ __launch_bounds__(EMIT_WAVES * 64) void k_emit(const DevStream *__res
             L[lane].hdr_bits = 0;
             L[lane].nruns = 0;
         }
-        noff[lane] = (uint32_t)(d.out_off - B0);
-        if (lane == cnt - 1) noff[cnt] = (uint32_t)(d.out_off + d.size - B0);
+        noff[lane] = (int32_t)(int64_t)(d.out_off - B0);
+        if (lane == hi - 1) noff[hi] = (int32_t)(int64_t)(d.out_off + d.size - B0);
     }
-    const bool any_slow = __ballot(my_slow) != 0;
+    const uint64_t slow_mask = __ballot(valid && my_slow);
+    const bool any_slow = (slow_mask >> XB) & ((cnt == 64 ? 0ull : (1ull << cnt)) - 1ull) ? true : false;
     wave_lds_sync();
     mark(1);
     if (flags & SCROLL_DEBUG_EMIT_BUILD) return;
 
-    const uint64_t B1 = B0 + uni(noff[cnt]);
-    const uint64_t c0 = B0 >> 4, c1 = (B1 + 15) >> 4;
+    const uint64_t B1 = B0 + (uint64_t)(int64_t)noff[XB + cnt];
 
-    /* 2. classify owned chunks */
-    uint32_t npe = 0, nchunks_pure = 0, nmx = 0;
+    /* seam lines (scroll_device.h seam_plan): head bytes [line(B0), B0)
+     * from memory (a stream's first tile) or from previous layouts; tail
+     * bytes [B1, line end) zero (last tile) or from next layouts */
+    const Seams z = seam_plan(B0, B1, t0, cnt, nnal, lo, hi, noff, slow_mask);
+    const bool head_full = z.head_full, tail_full = z.tail_full;
+    const uint64_t cs = z.cs, ce = z.ce;
+    const uint64_t nch = ce - cs;
+
+    /* 2. classify the owned chunks of every own NAL into entries */
+    uint32_t npe = 0, nmx = 0;
     uint64_t own0 = 0, own1 = 0, Aj = 0;
-    if (lane < cnt) {
-        Aj = 8 * (B0 + noff[lane]);
-        uint64_t Aj1 = 8 * (B0 + (uint64_t)noff[lane] + my_size);
-        own0 = lane == 0 ? c0 : (Aj + 127) >> 7;
-        own1 = lane == cnt - 1 ? c1 : (Aj1 + 127) >> 7;
-        if (own1 < own0) own1 = own0;
-        if (!my_slow) {
-            uint32_t s0 = L[lane].hdr_bits;
-            for (uint32_t r = 0; r < L[lane].nruns; ++r) {
-                uint32_t s1 = L[lane].run_end[r];
-                uint64_t cp0, cp1;
-                pure_range(Aj, s0, s1, cp0, cp1);
-                if (cp1 > cp0) {
-                    npe++;
-                    nchunks_pure += (uint32_t)(cp1 - cp0);
-                }
-                s0 = s1;
-            }
-        }
-        nmx = (uint32_t)(own1 - own0) - nchunks_pure;
+    if (own && !my_slow) {
+        owned_chunks(z, B0, noff, lane, cnt, own0, own1);
+        Aj = 8 * (B0 + (uint64_t)(int64_t)noff[lane]);
+        entry_walk(L[lane], Aj, own0, own1, [&](int r, uint64_t c0e, uint64_t c1e) {
+            npe++;
+            if (r < 0) nmx += (uint32_t)(c1e - c0e);
+        });
     }
     const uint32_t pe_inc = (uint32_t)wave_incl_scan(npe, lane);
-    const uint32_t vs_inc = (uint32_t)wave_incl_scan(nchunks_pure, lane);
     const uint32_t mx_inc = (uint32_t)wave_incl_scan(nmx, lane);
     const uint32_t tot_pe = uni((uint32_t)__shfl(pe_inc, 63, 64));
-    const uint32_t tot_pure = uni((uint32_t)__shfl(vs_inc, 63, 64));
     const uint32_t tot_mx = uni((uint32_t)__shfl(mx_inc, 63, 64));
-    const bool generic = any_slow || (B1 - B0) >= (1ull << 26) || tot_pe > (uint32_t)MAXPE ||
-                         tot_mx > (uint32_t)MAXMX;
+    const bool generic = any_slow || (B1 - B0) >= (1ull << 26) || nch >= (1ull << 22) ||
+                         tot_pe > (uint32_t)MAXPE || tot_mx > (uint32_t)MAXMX;
 
     if (!generic) {
-        if (lane < cnt) {
-            uint32_t e = pe_inc - npe, v = vs_inc - nchunks_pure, m = mx_inc - nmx;
-            uint64_t prev = own0;
-            uint32_t s0 = L[lane].hdr_bits;
-            for (uint32_t r = 0; r <= L[lane].nruns; ++r) {
-                uint64_t cp0 = own1, cp1 = own1;              /* r == nruns: tail gap */
-                if (r < L[lane].nruns) {
-                    uint32_t s1 = L[lane].run_end[r];
-                    pure_range(Aj, s0, s1, cp0, cp1);
-                    s0 = s1;
-                    if (cp1 <= cp0) continue;
-                }
-                for (uint64_t c = prev; c < cp0; ++c)          /* mixed gap before it */
-                    W.mx[m++] = ((uint32_t)(c - c0) << 6) | (uint32_t)lane;
-                if (r < L[lane].nruns) {
-                    W.pe_cb[e] = (uint32_t)(cp0 - c0);
-                    W.pe_vj[e] = v | ((uint32_t)lane << 22) | (r << 28);
-                    e++;
-                    v += (uint32_t)(cp1 - cp0);
-                }
-                prev = cp1;
-            }
+        if (own) {
+            uint32_t e = pe_inc - npe, m = mx_inc - nmx;
+            entry_walk(L[lane], Aj, own0, own1, [&](int r, uint64_t c0e, uint64_t c1e) {
+                W.pe_vj[e] = (uint32_t)(c0e - cs) | ((uint32_t)lane << 22) |
+                             ((r < 0 ? PE_MIXED : (uint32_t)r) << 28);
+                W.pe_cb[e] = m;
+                e++;
+                if (r < 0)
+                    for (uint64_t c = c0e; c < c1e; ++c)
+                        W.mx[m++] = ((uint32_t)(c - cs) << 6) | mixed_first(z, c << 4, B0, lane);
+            });
         }
         wave_lds_sync();
         mark(2);
 
-        /* 3. pure phase.  The wave writes the pure chunks 64 at a time in
-         * virtual order.  Lane k of a window holds pure entry ebase + k (its
-         * first virtual chunk vs and end, K = run bit of virtual chunk 0,
-         * chunk bias C, code len / magic, pattern192).  Each lane finds its
-         * entry from the (usually 0-2) entries that start inside the group
-         * and pulls that entry's data with ds_bpermute: no per-entry select
-         * chains, no LDS round trip for the common case. */
+        /* 3. mixed chunks -> LDS (head chunks merge the bytes before B0 from
+         * memory on the launch's first tile) */
+        const int mix_hi = tail_full ? z.t_hi : XB + cnt;
+        const uint32_t mx_end = (flags & SCROLL_DEBUG_EMIT_NOMIXED) ? 0u : tot_mx;
+        for (uint32_t k = (uint32_t)lane; k < mx_end; k += 64) {
+            const uint32_t mm = W.mx[k];
+            const uint64_t p = (cs + (mm >> 6)) << 4;
+            uint32_t w[4];
+            mixed_chunk(L, noff, mix_hi, (int)(mm & 63u), ((int64_t)p - (int64_t)B0) * 8, T, w);
+            if (z.head_rmw && p < B0) {
+                const uint4 old = *reinterpret_cast<const uint4 *>(A + p);
+                const uint32_t ow[4] = {__builtin_bswap32(old.x), __builtin_bswap32(old.y),
+                                        __builtin_bswap32(old.z), __builtin_bswap32(old.w)};
+                const int32_t nb = (int32_t)(B0 - p);          /* bytes kept, 1..15 */
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    w[q] |= ow[q] & range_mask(0, 8 * nb - 32 * q);
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q) W.mw[k][q] = w[q];
+        }
+        wave_lds_sync();
+        mark(3);
+        if (stamps && lane == 0) stamp[6] = ((uint64_t)nch << 32) | tot_mx;
+
+        /* 4. stream.  Lane k of a window holds entry ebase + k: first chunk
+         * vs (relative to cs), and for a pure entry K = run bit of chunk cs
+         * (mod 2^32; chunk cs + v starts at run bit K + 128 v), code len,
+         * magic, pattern192; for a mixed entry len = 0 and K + v = the mw
+         * index of chunk cs + v. */
         uint32_t ebase = 0;
-        uint32_t e_vs = 0xffffffffu, e_end = 0xffffffffu, e_K = 0, e_C = 0, e_len = 1,
-                 e_mag = 0xffffffffu, e_q[6] = {0, 0, 0, 0, 0, 0};
+        uint32_t e_vs = 0xffffffffu, e_K = 0, e_len = 0, e_mag = 0, e_q[6] = {0, 0, 0, 0, 0, 0};
         auto load_window = [&](uint32_t base) {
             const uint32_t idx = base + (uint32_t)lane;
-            e_vs = e_end = 0xffffffffu;
+            e_vs = 0xffffffffu;
             if (idx < tot_pe) {
-                const uint32_t vj = W.pe_vj[idx], cb = W.pe_cb[idx];
+                const uint32_t vj = W.pe_vj[idx];
                 const uint32_t vs = vj & PE_VS_MASK;
-                const int j = (int)((vj >> 22) & 63u), r = (int)(vj >> 28);
-                const Lay &Lj = L[j];
-                const uint32_t rs0 = r ? Lj.run_end[r - 1] : Lj.hdr_bits;
-                const uint64_t Arun = 8 * (B0 + (uint64_t)noff[j]) + rs0;
+                const int j = (int)((vj >> 22) & 63u);
+                const uint32_t r = vj >> 28;
                 e_vs = vs;
-                e_end = idx + 1 < tot_pe ? (W.pe_vj[idx + 1] & PE_VS_MASK) : tot_pure;
-                e_K = (uint32_t)(((c0 + cb - vs) << 7) - Arun);
-                e_C = cb - vs;
-                e_len = Lj.len[r];
-                e_mag = Lj.magic[r];
-                pattern192(Lj.pat[r][0], Lj.pat[r][1], Lj.pat[r][2], e_len, e_mag, e_q);
+                if (r == PE_MIXED) {
+                    e_len = 0;
+                    e_mag = 0;
+                    e_K = W.pe_cb[idx] - vs;
+#pragma unroll
+                    for (int z = 0; z < 6; ++z) e_q[z] = 0;
+                } else {
+                    const Lay &Lj = L[j];
+                    const uint32_t rs0 = r ? Lj.run_end[r - 1] : Lj.hdr_bits;
+                    const uint64_t Arun = 8 * (B0 + (uint64_t)(int64_t)noff[j]) + rs0;
+                    e_K = (uint32_t)((cs << 7) - Arun);        /* chunk cs + v: bit K + 128 v */
+                    e_len = Lj.len[r];
+                    e_mag = T.magic[e_len - 1];
+                    pattern192(Lj.pat[r][0], Lj.pat[r][1], T.mods[e_len - 1], e_q);
+                }
             }
         };
-        const uint32_t pure_end = (flags & SCROLL_DEBUG_EMIT_NOPURE) ? 0u : tot_pure;
+        /* the 4 words of chunk v from entry data (len 0 = mixed) */
+        auto words = [&](uint32_t v, uint32_t K, uint32_t len, uint32_t mag, const uint32_t q[6],
+                         uint32_t w[4]) {
+            uint32_t pw[4];
+            pure_words(K + (v << 7), len ? len : 1u, mag, q, pw);
+            const uint32_t mi = len ? 0u : min(K + v, (uint32_t)MAXMX - 1u);
+            const uint4 mv = *reinterpret_cast<const uint4 *>(W.mw[mi]);
+            w[0] = len ? pw[0] : mv.x;
+            w[1] = len ? pw[1] : mv.y;
+            w[2] = len ? pw[2] : mv.z;
+            w[3] = len ? pw[3] : mv.w;
+        };
+        const uint32_t nv = (flags & SCROLL_DEBUG_EMIT_NOPURE) ? 0u : (uint32_t)nch;
         const bool do_store = !(flags & SCROLL_DEBUG_EMIT_NOSTORE);
-        if (pure_end) load_window(0);
-        uint32_t e0 = 0;                     /* entry holding virtual chunk v0 (uniform) */
-
-        /* one group of 64 virtual chunks at g with its own window upkeep:
-         * the fallback for iterations touching > 64 entries */
-        auto group1 = [&](uint32_t g) {
-            const uint32_t v = g + (uint32_t)lane;
-            const uint32_t vhi = min(g + 63u, pure_end - 1u);
-            uint64_t m = __ballot(e_vs <= vhi);
-            if ((m >> 63) && e0 != ebase && ebase + 64 < tot_pe) {
-                ebase = e0;
-                load_window(ebase);
-                m = __ballot(e_vs <= vhi);
-            }
-            const uint32_t ks = (uint32_t)__popcll(__ballot(e_vs <= g)) - 1u;
-            const uint32_t ke = (uint32_t)__popcll(m) - 1u;
-            uint32_t kk = ks;
-            for (uint32_t jb = ks + 1; jb <= ke; ++jb)
-                kk += v >= (uint32_t)__builtin_amdgcn_readlane((int)e_vs, (int)jb) ? 1u : 0u;
-            e0 = ebase + (uint32_t)__popcll(__ballot(e_vs <= g + 64u)) - 1u;
-            const int src = (int)(kk << 2);
-            const uint32_t K = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)e_K);
-            const uint32_t C = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)e_C);
-            const uint32_t len = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)e_len);
-            const uint32_t mag = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)e_mag);
-            uint32_t q[6], w[4];
-#pragma unroll
-            for (int z = 0; z < 6; ++z) q[z] = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)e_q[z]);
-            pure_words(K + (v << 7), len, mag, q, w);
-            if (v < pure_end && do_store) store_chunk(A, (c0 + (uint64_t)(uint32_t)(v + C)) << 4, w);
-        };
-
-        for (uint32_t v0 = 0; v0 < pure_end; v0 += 64u * PURE_U) {
-            const uint32_t vlast = min(v0 + 64u * PURE_U, pure_end) - 1u;
-            uint64_t m = __ballot(e_vs <= vlast);
-            if ((m >> 63) && e0 != ebase && ebase + 64 < tot_pe) {
-                ebase = e0;                              /* window must reach the groups */
-                load_window(ebase);
-                m = __ballot(e_vs <= vlast);
-            }
-            if ((m >> 63) && ebase + 64 < tot_pe) {      /* > 64 entries: group by group */
-                for (uint32_t g = v0; g <= vlast; g += 64u) group1(g);
-                continue;
-            }
-            /* per group: the entry holding its first chunk (ks) and the entries
-             * starting inside it (ks, ke]; lanes past the end are clamped to
-             * the last pure chunk and store the same bytes again */
-            uint32_t kk[PURE_U], vv[PURE_U];
-#pragma unroll
-            for (int u = 0; u < PURE_U; ++u) {
-                const uint32_t g = min(v0 + 64u * (uint32_t)u, vlast);
-                const uint32_t gh = min(g + 63u, vlast);
-                const uint32_t v = min(g + (uint32_t)lane, vlast);
-                const uint32_t ks = (uint32_t)__popcll(__ballot(e_vs <= g)) - 1u;
-                const uint32_t ke = (uint32_t)__popcll(__ballot(e_vs <= gh)) - 1u;
-                uint32_t k = ks;
-                for (uint32_t jb = ks + 1; jb <= ke; ++jb)
-                    k += v >= (uint32_t)__builtin_amdgcn_readlane((int)e_vs, (int)jb) ? 1u : 0u;
-                kk[u] = k;
-                vv[u] = v;
-            }
-            e0 = ebase + (uint32_t)__popcll(__ballot(e_vs <= v0 + 64u * PURE_U)) - 1u;
-            uint32_t w[PURE_U][4];
-            uint64_t addr[PURE_U];
-#pragma unroll
-            for (int u = 0; u < PURE_U; ++u) {
-                const int src = (int)(kk[u] << 2);
-                const uint32_t K = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)e_K);
-                const uint32_t C = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)e_C);
-                const uint32_t len = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)e_len);
-                const uint32_t mag = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)e_mag);
-                uint32_t q[6];
-#pragma unroll
-                for (int z = 0; z < 6; ++z) q[z] = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)e_q[z]);
-                pure_words(K + (vv[u] << 7), len, mag, q, w[u]);
-                addr[u] = (c0 + (uint64_t)(uint32_t)(vv[u] + C)) << 4;
-            }
+        if (nv) load_window(0);
+        auto store4 = [&](uint32_t (&w)[PURE_U][4], const uint32_t (&vv)[PURE_U]) {
             if (do_store) {
                 /* byte-swap all groups first and keep them live together, so
                  * the stores read distinct registers (no WAR stall behind a
@@ -608,7 +577,7 @@ __global__ __launch_bounds__(EMIT_WAVES * 64) void k_emit(const DevStream *__res
                 uint64_t ptr[PURE_U];
 #pragma unroll
                 for (int u = 0; u < PURE_U; ++u) {
-                    ptr[u] = (uint64_t)(uintptr_t)A + addr[u];
+                    ptr[u] = (uint64_t)(uintptr_t)A + ((cs + vv[u]) << 4);
                     asm volatile("" : "+v"(o[u][0]), "+v"(o[u][1]), "+v"(o[u][2]), "+v"(o[u][3]),
                                  "+v"(ptr[u]));
                 }
@@ -620,43 +589,131 @@ __global__ __launch_bounds__(EMIT_WAVES * 64) void k_emit(const DevStream *__res
                 for (int u = 0; u < PURE_U; ++u)
                     asm volatile("" ::"v"(w[u][0]), "v"(w[u][1]), "v"(w[u][2]), "v"(w[u][3]));
             }
+        };
+
+        for (uint32_t v0 = 0; v0 < nv; v0 += 64u * PURE_U) {
+            const uint32_t vlast = min(v0 + 64u * PURE_U, nv) - 1u;
+            uint64_t m = __ballot(e_vs <= vlast);
+            if ((m >> 63) && ebase + 64 < tot_pe) {
+                /* the window must hold every entry of the iteration */
+                const uint32_t ks = ebase + (uint32_t)__popcll(__ballot(e_vs <= v0)) - 1u;
+                if (ks != ebase) {
+                    ebase = ks;
+                    load_window(ebase);
+                    m = __ballot(e_vs <= vlast);
+                }
+            }
+            uint32_t w[PURE_U][4], vv[PURE_U];
+            if ((m >> 63) && ebase + 64 < tot_pe) {
+                /* > 64 entries in 256 chunks (tiny NALs): group by group,
+                 * entry by entry, reloading the window as needed */
+#pragma unroll
+                for (int u = 0; u < PURE_U; ++u) {
+                    const uint32_t v = min(v0 + 64u * (uint32_t)u + (uint32_t)lane, vlast);
+                    vv[u] = v;
+                    const uint32_t g = min(v0 + 64u * (uint32_t)u, vlast);
+                    /* move the window to start at the entry holding g, so it
+                     * holds all (<= 64) entries of the group */
+                    for (;;) {
+                        const uint64_t b = __ballot(e_vs <= g);
+                        if (!(b >> 63) || ebase + 64 >= tot_pe) break;
+                        ebase += 63;                      /* every entry starts <= g */
+                        load_window(ebase);
+                    }
+                    const uint32_t ks = ebase + (uint32_t)__popcll(__ballot(e_vs <= g)) - 1u;
+                    if (ks != ebase) {
+                        ebase = ks;
+                        load_window(ebase);
+                    }
+                    const uint32_t k0 = 0u;
+                    const uint32_t k1 = (uint32_t)__popcll(__ballot(e_vs <= min(g + 63u, vlast))) - 1u;
+                    uint32_t kk = k0;
+                    for (uint32_t jb = k0 + 1; jb <= k1; ++jb)
+                        kk += v >= (uint32_t)__builtin_amdgcn_readlane((int)e_vs, (int)jb) ? 1u : 0u;
+                    const int src = (int)(kk << 2);
+                    uint32_t q[6];
+#pragma unroll
+                    for (int z = 0; z < 6; ++z) q[z] = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)e_q[z]);
+                    words(v, (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)e_K),
+                          (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)e_len),
+                          (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)e_mag), q, w[u]);
+                }
+                store4(w, vv);
+                continue;
+            }
+            const uint32_t ks0 = (uint32_t)__popcll(__ballot(e_vs <= v0)) - 1u;  /* window index */
+            const bool starts = e_vs > v0 && e_vs <= vlast;
+            if (__ballot(starts) == 0) {
+                /* one entry covers the whole iteration: SGPR operands */
+                const uint32_t K = (uint32_t)__builtin_amdgcn_readlane((int)e_K, (int)ks0);
+                const uint32_t len = (uint32_t)__builtin_amdgcn_readlane((int)e_len, (int)ks0);
+                const uint32_t mag = (uint32_t)__builtin_amdgcn_readlane((int)e_mag, (int)ks0);
+                uint32_t q[6];
+#pragma unroll
+                for (int z = 0; z < 6; ++z) q[z] = (uint32_t)__builtin_amdgcn_readlane((int)e_q[z], (int)ks0);
+#pragma unroll
+                for (int u = 0; u < PURE_U; ++u) {
+                    vv[u] = min(v0 + 64u * (uint32_t)u + (uint32_t)lane, vlast);
+                    words(vv[u], K, len, mag, q, w[u]);
+                }
+            } else {
+                /* entry-start flags of the 4 groups -> per-lane entry index
+                 * (window lane) by one ballot + mbcnt per group */
+                W.flg[lane] = 0u;
+                if (starts) {
+                    const uint32_t rel = e_vs - v0;
+                    reinterpret_cast<uint8_t *>(W.flg)[(rel & 63u) * 4u + (rel >> 6)] = 1;
+                }
+                wave_lds_sync();
+                const uint32_t f4 = W.flg[lane];
+                uint32_t base = ks0;
+#pragma unroll
+                for (int u = 0; u < PURE_U; ++u) {
+                    const uint32_t fu = (f4 >> (8 * u)) & 255u;
+                    const uint64_t B = __ballot(fu != 0u);
+                    const uint32_t below = __builtin_amdgcn_mbcnt_hi(
+                        (uint32_t)(B >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)B, 0u));
+                    const uint32_t kk = base + below + fu;
+                    base += (uint32_t)__popcll(B);
+                    vv[u] = min(v0 + 64u * (uint32_t)u + (uint32_t)lane, vlast);
+                    const int src = (int)(kk << 2);
+                    uint32_t q[6];
+#pragma unroll
+                    for (int z = 0; z < 6; ++z) q[z] = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)e_q[z]);
+                    words(vv[u], (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)e_K),
+                          (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)e_len),
+                          (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)e_mag), q, w[u]);
+                }
+            }
+            store4(w, vv);
         }
 
-        mark(3);
-        if (stamps && lane == 0) stamp[6] = ((uint64_t)tot_pure << 32) | tot_mx;
-        /* 4. mixed phase: one lane per mixed chunk (header, run boundaries,
-         * NAL boundaries, the two partial chunks at the tile ends). */
-        const uint32_t mx_end = (flags & SCROLL_DEBUG_EMIT_NOMIXED) ? 0u : tot_mx;
-        for (uint32_t k = (uint32_t)lane; k < mx_end; k += 64) {
-            const uint32_t mm = W.mx[k];
-            const uint64_t c = c0 + (mm >> 6);
-            const uint64_t p = c << 4;
-            uint32_t w[4];
-            mixed_chunk(L, noff, cnt, (int)(mm & 63u), ((int64_t)p - (int64_t)B0) * 8, w);
-            if (p >= B0 && p + 16 <= B1) {
-                if (flags & SCROLL_DEBUG_EMIT_NOSTORE)
-                    asm volatile("" ::"v"(w[0]), "v"(w[1]), "v"(w[2]), "v"(w[3]));
-                else
-                    store_chunk(A, p, w);
-            } else {
-                for (int kk = 0; kk < 16; ++kk) {
-                    const uint64_t x = p + (uint64_t)kk;
-                    if (x < B0 || x >= B1) continue;
-                    A[x] = (uint8_t)(w[kk >> 2] >> (24 - 8 * (kk & 3)));
-                }
+        /* partial chunks of a seam line whose neighbour bytes are not
+         * available here: own bytes only */
+        if (!(flags & SCROLL_DEBUG_EMIT_NOBYTES)) {
+            const bool ph = !head_full && (B0 & 15);
+            const bool pt = !tail_full && (B1 & 15) && (B1 >> 4) >= cs;
+            const uint64_t pc = lane == 0 ? (B0 >> 4) : (B1 >> 4);
+            if ((lane == 0 && ph) || (lane == 1 && pt && !(ph && (B1 >> 4) == (B0 >> 4)))) {
+                uint32_t w[4];
+                mixed_chunk(L, noff, XB + cnt, XB, ((int64_t)(pc << 4) - (int64_t)B0) * 8, T, w);
+                store_bytes(A, pc << 4, B0, B1, w);
             }
         }
     } else {
+        const Lay *Lo = L + XB;
+        const int32_t *no = noff + XB;
         int j = 0;
+        const uint64_t c0 = B0 >> 4, c1 = (B1 + 15) >> 4;
         for (uint64_t c = c0 + lane; c < c1; c += 64) {
             const uint64_t p = c << 4;
             for (int k = 0; k < 16; ++k) {
                 uint64_t q = p + (uint64_t)k;
                 if (q < B0 || q >= B1) continue;
                 uint32_t rel = (uint32_t)(q - B0);
-                while (j + 1 < cnt && noff[j + 1] <= rel) j++;
-                if (D[j].slow) continue;
-                A[q] = (uint8_t)tile_byte(L, noff, cnt, j, rel);
+                while (j + 1 < cnt && (uint32_t)no[j + 1] <= rel) j++;
+                if ((slow_mask >> (XB + j)) & 1ull) continue;
+                A[q] = (uint8_t)tile_byte(Lo, no, cnt, j, rel);
             }
         }
     }
@@ -667,7 +724,7 @@ __global__ __launch_bounds__(EMIT_WAVES * 64) void k_emit(const DevStream *__res
         stamp[7] = (__builtin_amdgcn_s_memrealtime() & 0xffffffffull) | (hw << 32);
         stamp[6] = (stamp[6] & 0x00ffffffffffffffull) | ((xcc & 0xff) << 56);
     }
-    if (my_slow) serial_write(my_ctx, A + D[lane].out_off);
+    if (own && my_slow) serial_write(my_ctx, A + d.out_off);
 }
 
 /* ---------------------------------------------------------------------- */
@@ -827,7 +884,9 @@ int scroll_batch_create(ScrollBatch **out, const ScrollBatchDesc *desc)
     b->max_streams = desc->max_streams;
     b->max_frames = desc->max_frames;
     b->arena_bytes = desc->arena_bytes;
-    b->ld_arena = (desc->arena_bytes + 255) & ~(size_t)255;
+    /* >= 128 B slack past out_cap: k_emit writes whole 128-byte lines and
+     * zero-fills the tail of a stream's last line */
+    b->ld_arena = (desc->arena_bytes + 128 + 255) & ~(size_t)255;
     b->ld_nal = 2 * desc->max_frames;
     size_t S = (size_t)desc->max_streams;
     hipError_t e = hipSuccess;

@@ -34,7 +34,8 @@ def main():
     variants = {"full": 0, "nostore": hs.SCROLL_DEBUG_EMIT_NOSTORE,
                 "zeros": hs.SCROLL_DEBUG_EMIT_ZEROS, "build": hs.SCROLL_DEBUG_EMIT_BUILD,
                 "nopure": hs.SCROLL_DEBUG_EMIT_NOPURE, "nomixed": hs.SCROLL_DEBUG_EMIT_NOMIXED,
-                "classify": hs.SCROLL_DEBUG_EMIT_NOPURE | hs.SCROLL_DEBUG_EMIT_NOMIXED}
+                "classify": hs.SCROLL_DEBUG_EMIT_NOPURE | hs.SCROLL_DEBUG_EMIT_NOMIXED,
+                "nobytes": hs.SCROLL_DEBUG_EMIT_NOBYTES}
     if args.variant:
         variants = {args.variant: variants[args.variant]}
     res = {k: [] for k in variants}

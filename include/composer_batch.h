@@ -57,6 +57,7 @@ extern "C" {
 #define SCROLL_DEBUG_EMIT_NOPURE 16 /* k_emit skips the pure-chunk phase          */
 #define SCROLL_DEBUG_EMIT_NOMIXED 32 /* k_emit skips the mixed-chunk phase        */
 #define SCROLL_DEBUG_EMIT_STAMPS 64 /* k_emit records s_memtime per phase per wave */
+#define SCROLL_DEBUG_EMIT_NOBYTES 128 /* k_emit skips the tile-end partial chunks  */
 
 typedef struct ScrollBatch ScrollBatch;
 

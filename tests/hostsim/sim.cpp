@@ -3,13 +3,17 @@
  * (scroll_device.h).  Exposes:
  *   sim_nal():   one NAL via build_nal<true> + lay_bits32 (fast path) or the
  *                serial path, so tests can compare bytes with the oracle;
- *   sim_tile():  a sequence of NALs laid out as one k_emit tile and read back
- *                through pure_words()/mixed_chunk() at 16-byte granularity.
+ *   sim_stream(): a whole stream produced tile by tile through k_emit's
+ *                shared store plan (seam_plan / owned_chunks / entry_walk /
+ *                mixed_chunk / pure_words), checked for coverage and for
+ *                consistent duplicate seam-line writes.
  */
 #include <cstdio>
 #include <cstdlib>
 #include <cstddef>
 #include <cstring>
+#include <algorithm>
+#include <array>
 #include <vector>
 #include "scroll_device.h"
 
@@ -37,7 +41,7 @@ long sim_nal(int w, int h, int l2f, int poct, int l2p, int dbf, int kind, int of
         build_nal<true, false>(c, &L3, &sz3);
         if (sz3 != sz || memcmp(&L3, &L, offsetof(Lay, run_end)) != 0) return -5;
         for (uint32_t r = 0; r < L.nruns; ++r)
-            if (L3.run_end[r] != L.run_end[r] || L3.len[r] != L.len[r] || L3.magic[r] != L.magic[r] ||
+            if (L3.run_end[r] != L.run_end[r] || L3.len[r] != L.len[r] ||
                 memcmp(L3.pat[r], L.pat[r], sizeof(L.pat[r])) != 0)
                 return -5;
     }
@@ -67,84 +71,145 @@ long sim_nal(int w, int h, int l2f, int poct, int l2p, int dbf, int kind, int of
     return (long)n;
 }
 
-/* Lay out n NALs (all fast) back to back starting at arena byte base0 and read
- * them with the k_emit chunk logic; out gets the concatenated bytes. */
-long sim_tile(int w, int h, int l2f, int poct, int l2p, int dbf, int n, const int *kinds,
-              const int *offs, const int *fns, const int *nwps, const int *wo, const int *wl,
-              const int *wv, int base0, uint8_t *out, long cap)
+/* LenLut: mod_magic(d) == d % len for len 1..64 over small, near-2^31 and
+ * random d; pattern phase bytes equal the direct modulo.  0 = ok. */
+int sim_check_lut(void)
 {
-    std::vector<Lay> L(n);
-    std::vector<uint32_t> noff(n + 1);
-    uint32_t pos = 0;
+    LenLut T;
+    for (uint32_t len = 1; len <= 64; ++len) lut_entry(len, T.magic[len - 1], T.mods[len - 1]);
+    uint64_t x = 88172645463325252ull;
+    for (uint32_t len = 1; len <= 64; ++len) {
+        const uint32_t m = T.mods[len - 1];
+        if ((m & 255u) != 64u % len || ((m >> 8) & 255u) != 96u % len ||
+            ((m >> 16) & 255u) != 128u % len || (m >> 24) != 160u % len)
+            return -1;
+        for (uint32_t k = 0; k < 300000; ++k) {
+            x ^= x << 13; x ^= x >> 7; x ^= x << 17;
+            const uint32_t d = k < 100000 ? k : (k < 200000 ? 0x7fffffffu - (k - 100000)
+                                                            : (uint32_t)x);
+            if (mod_magic(d, len, T.magic[len - 1]) != d % len) return -2;
+        }
+    }
+    return 0;
+}
+
+/* k_emit's store plan over a whole stream: n fast NALs laid out from arena
+ * byte base0 (bytes [0, base0) hold a previous compose), tiles of `tile`
+ * NALs, each produced through the shared seam_plan / owned_chunks /
+ * entry_walk / mixed_chunk / pure_words code exactly as one wave does.
+ * out receives arena [0, base0 + total + 128).  Returns total, or
+ *  -1 capacity, -2 a NAL not on the fast path, -4 a byte written twice with
+ *  different values, -6 an output byte never written. */
+long sim_stream(int w, int h, int l2f, int poct, int l2p, int dbf, int n, const int *kinds,
+                const int *offs, const int *fns, const int *nwps, const int *wo, const int *wl,
+                const int *wv, int base0, int tile, uint8_t *out, long cap)
+{
+    std::vector<Lay> La(n);
+    std::vector<uint64_t> at(n + 1);
+    at[0] = (uint64_t)base0;
     for (int i = 0; i < n; ++i) {
         NalCtx c{w, h, l2f, poct, l2p, dbf, kinds[i], offs[i], fns[i], nwps[i], wo, wl, wv};
-        memset(&L[i], 0, sizeof(Lay));
+        memset(&La[i], 0, sizeof(Lay));
         uint32_t sz;
-        if (!build_nal<true>(c, &L[i], &sz)) return -2;
-        noff[i] = pos;
-        pos += sz;
+        if (!build_nal<true, false>(c, &La[i], &sz)) return -2;
+        at[i + 1] = at[i] + sz;
     }
-    noff[n] = pos;
-    if ((long)pos > cap) return -1;
-    /* arena positions: tile starts at base0 (not 16-aligned in general) */
-    uint64_t B0 = (uint64_t)base0, B1 = B0 + pos;
-    std::vector<uint8_t> arena(B1 + 32, 0xEE);
-    /* mirrors k_emit: classify owned chunks into pure / mixed, then both phases */
-    const uint64_t c0 = B0 >> 4, c1 = (B1 + 15) >> 4;
-    struct PE { uint32_t cb, n, j, r; };
-    std::vector<PE> pes;
-    std::vector<std::pair<uint32_t, int>> mxs;
-    for (int lane = 0; lane < n; ++lane) {
-        uint64_t Aj = 8 * (B0 + noff[lane]), Aj1 = 8 * (B0 + noff[lane + 1]);
-        uint64_t own0 = lane == 0 ? c0 : (Aj + 127) >> 7;
-        uint64_t own1 = lane == n - 1 ? c1 : (Aj1 + 127) >> 7;
-        if (own1 < own0) own1 = own0;
-        uint64_t prev = own0;
-        uint32_t s0 = L[lane].hdr_bits;
-        for (uint32_t r = 0; r <= L[lane].nruns; ++r) {
-            uint64_t cp0 = own1, cp1 = own1;
-            if (r < L[lane].nruns) {
-                uint32_t s1 = L[lane].run_end[r];
-                pure_range(Aj, s0, s1, cp0, cp1);
-                s0 = s1;
-                if (cp1 <= cp0) continue;
+    const uint64_t total = at[n] - (uint64_t)base0;
+    const uint64_t span = at[n] + 128;
+    if ((long)span > cap) return -1;
+    std::vector<uint8_t> A(span + 256, 0xEE);
+    for (int i = 0; i < base0; ++i) A[i] = (uint8_t)(i * 37 + 11);
+    std::vector<int> wr(A.size(), -1);
+    bool clash = false;
+    auto put = [&](uint64_t x, uint8_t v) {
+        if (wr[x] >= 0 && wr[x] != v) clash = true;
+        wr[x] = v;
+        A[x] = v;
+    };
+    LenLut T;
+    for (uint32_t len = 1; len <= 64; ++len) lut_entry(len, T.magic[len - 1], T.mods[len - 1]);
+    constexpr int XB = SEAM_XB, XA = SEAM_XA;
+    for (int t0 = 0; t0 < n; t0 += tile) {
+        const int cnt = std::min(tile, n - t0);
+        const int lo = std::max(0, XB - t0), hi = XB + cnt + std::min(XA, n - t0 - cnt);
+        std::vector<Lay> L(XB + tile + XA);
+        std::vector<int32_t> noff(XB + tile + XA + 1, 0);
+        const uint64_t B0 = at[t0], B1 = at[t0 + cnt];
+        for (int i = lo; i < hi; ++i) {
+            L[i] = La[t0 - XB + i];
+            noff[i] = (int32_t)((int64_t)at[t0 - XB + i] - (int64_t)B0);
+        }
+        noff[hi] = (int32_t)((int64_t)at[t0 - XB + hi] - (int64_t)B0);
+        const Seams z = seam_plan(B0, B1, t0, cnt, n, lo, hi, noff.data(), 0);
+        struct E { uint32_t vs; int r, i; uint32_t mbase; };
+        std::vector<E> ent;
+        std::vector<std::pair<uint64_t, uint32_t>> mxl;    /* chunk, first layout */
+        for (int i = XB; i < XB + cnt; ++i) {
+            uint64_t own0, own1;
+            owned_chunks(z, B0, noff.data(), i, cnt, own0, own1);
+            const uint64_t Aj = 8 * (B0 + (uint64_t)(int64_t)noff[i]);
+            entry_walk(L[i], Aj, own0, own1, [&](int r, uint64_t c0e, uint64_t c1e) {
+                ent.push_back({(uint32_t)(c0e - z.cs), r, i, (uint32_t)mxl.size()});
+                if (r < 0)
+                    for (uint64_t c = c0e; c < c1e; ++c) mxl.push_back({c, mixed_first(z, c << 4, B0, i)});
+            });
+        }
+        const int mix_hi = z.tail_full ? z.t_hi : XB + cnt;
+        std::vector<std::array<uint32_t, 4>> mw(mxl.size());
+        for (size_t k = 0; k < mxl.size(); ++k) {
+            const uint64_t p = mxl[k].first << 4;
+            uint32_t ww[4];
+            mixed_chunk(L.data(), noff.data(), mix_hi, (int)mxl[k].second,
+                        ((int64_t)p - (int64_t)B0) * 8, T, ww);
+            if (z.head_rmw && p < B0) {
+                const int32_t nb = (int32_t)(B0 - p);
+                for (int q = 0; q < 4; ++q) {
+                    uint32_t o = 0;
+                    for (int b = 0; b < 4; ++b) o = (o << 8) | A[p + 4 * q + b];
+                    ww[q] |= o & range_mask(0, 8 * nb - 32 * q);
+                }
             }
-            for (uint64_t c = prev; c < cp0; ++c) mxs.push_back({(uint32_t)(c - c0), lane});
-            if (r < L[lane].nruns) pes.push_back({(uint32_t)(cp0 - c0), (uint32_t)(cp1 - cp0), (uint32_t)lane, r});
-            prev = cp1;
+            for (int q = 0; q < 4; ++q) mw[k][q] = ww[q];
         }
-    }
-    std::vector<int> owned(c1 - c0, 0);
-    for (auto &e : pes) {
-        const Lay &Lj = L[e.j];
-        uint32_t rs0 = e.r ? Lj.run_end[e.r - 1] : Lj.hdr_bits;
-        uint32_t len = Lj.len[e.r], magic = Lj.magic[e.r];
-        uint64_t Arun = 8 * (B0 + noff[e.j]) + rs0;
-        uint32_t q6[6];
-        pattern192(Lj.pat[e.r][0], Lj.pat[e.r][1], Lj.pat[e.r][2], len, magic, q6);
-        for (uint32_t k = 0; k < e.n; ++k) {
-            uint64_t c = c0 + e.cb + k;
-            owned[c - c0]++;
-            uint32_t w[4];
-            pure_words((uint32_t)((c << 7) - Arun), len, magic, q6, w);
-            for (int q = 0; q < 16; ++q) arena[(c << 4) + q] = (uint8_t)(w[q >> 2] >> (24 - 8 * (q & 3)));
+        const uint64_t nch = z.ce - z.cs;
+        size_t e = 0;
+        for (uint64_t v = 0; v < nch; ++v) {
+            while (e + 1 < ent.size() && ent[e + 1].vs <= v) e++;
+            uint32_t ww[4];
+            const E &en = ent[e];
+            if (en.r < 0) {
+                for (int q = 0; q < 4; ++q) ww[q] = mw[en.mbase + (v - en.vs)][q];
+            } else {
+                const Lay &Lj = L[en.i];
+                const uint32_t rs0 = en.r ? Lj.run_end[en.r - 1] : Lj.hdr_bits;
+                const uint64_t Arun = 8 * (B0 + (uint64_t)(int64_t)noff[en.i]) + rs0;
+                const uint32_t K = (uint32_t)((z.cs << 7) - Arun);
+                const uint32_t len = Lj.len[en.r];
+                uint32_t q6[6];
+                pattern192(Lj.pat[en.r][0], Lj.pat[en.r][1], T.mods[len - 1], q6);
+                pure_words(K + ((uint32_t)v << 7), len, T.magic[len - 1], q6, ww);
+            }
+            const uint64_t p = (z.cs + v) << 4;
+            for (int b = 0; b < 16; ++b) put(p + b, (uint8_t)(ww[b >> 2] >> (24 - 8 * (b & 3))));
         }
+        auto partial = [&](uint64_t pc) {
+            uint32_t ww[4];
+            mixed_chunk(L.data(), noff.data(), XB + cnt, XB, ((int64_t)(pc << 4) - (int64_t)B0) * 8, T, ww);
+            for (int b = 0; b < 16; ++b) {
+                const uint64_t x = (pc << 4) + b;
+                if (x >= B0 && x < B1) put(x, (uint8_t)(ww[b >> 2] >> (24 - 8 * (b & 3))));
+            }
+        };
+        const bool ph = !z.head_full && (B0 & 15);
+        const bool pt = !z.tail_full && (B1 & 15) && (B1 >> 4) >= z.cs;
+        if (ph) partial(B0 >> 4);
+        if (pt && !(ph && (B1 >> 4) == (B0 >> 4))) partial(B1 >> 4);
     }
-    for (auto &m : mxs) {
-        uint64_t c = c0 + m.first, p = c << 4;
-        owned[c - c0]++;
-        uint32_t w[4];
-        mixed_chunk(L.data(), noff.data(), n, m.second, ((int64_t)p - (int64_t)B0) * 8, w);
-        for (int q = 0; q < 16; ++q) {
-            uint64_t x = p + q;
-            if (x < B0 || x >= B1) continue;
-            arena[x] = (uint8_t)(w[q >> 2] >> (24 - 8 * (q & 3)));
-        }
-    }
-    for (size_t k = 0; k < owned.size(); ++k)
-        if (owned[k] != 1) return -4;                        /* every chunk exactly once */
-    memcpy(out, arena.data() + B0, pos);
-    return pos;
+    if (clash) return -4;
+    for (uint64_t x = (uint64_t)base0; x < at[n]; ++x)
+        if (wr[x] < 0) return -6;
+    memcpy(out, A.data(), span);
+    return (long)total;
 }
 
 }  // extern "C"

@@ -40,14 +40,23 @@ def test_fast_and_serial_paths_vs_golden(hostsim, golden_frames):
     assert nfast > 400 and nslow > 10
 
 
-def test_tile_chunks_cross_nal_boundaries(hostsim):
+def test_len_lut_modulo(hostsim):
+    assert hostsim.sim_check_lut() == 0
+
+
+def test_stream_whole_lines(hostsim):
+    """k_emit's store plan (shared device code) over whole streams: tiles of
+    1..7 NALs, appends after a previous compose (head line merged from
+    memory), tiny NALs (16x16) that exceed the neighbour layouts; bytes must
+    equal the per-NAL reference, the previous bytes survive, the tail of the
+    last line is zero and duplicate seam writes agree."""
     buf = (ctypes.c_uint8 * BUF)()
     out = (ctypes.c_uint8 * BUF)()
-    rng = random.Random(11)
+    rng = random.Random(7)
     wo, wl, wv = I8(*[496 * (k + 1) for k in range(8)]), I8(*[2 + k for k in range(8)]), I8(*[1] * 8)
-    for _ in range(150):
-        w, h = 16 * rng.randint(1, 40), 16 * rng.randint(1, 30)
-        n = rng.randint(1, 32)
+    for it in range(160):
+        w, h = 16 * rng.choice([1, 1, 2, 4, rng.randint(1, 40)]), 16 * rng.choice([1, 3, rng.randint(1, 30)])
+        n = rng.randint(1, 40)
         kinds = [rng.choice([0, 0, 0, 1]) for _ in range(n)]
         offs = [rng.randint(0, h) for _ in range(n)]
         fns = [rng.randint(0, 50) for _ in range(n)]
@@ -61,7 +70,14 @@ def test_tile_chunks_cross_nal_boundaries(hostsim):
             assert fast
             ref += b
         A = lambda v: (ctypes.c_int * n)(*v)
-        base = rng.randint(0, 200)
-        m = hostsim.sim_tile(w, h, 4, 2, 4, 1, n, A(kinds), A(offs), A(fns), A(nwps), wo, wl, wv,
-                             base, out, BUF)
-        assert m == len(ref) and bytes(out[:m]) == ref
+        base = rng.choice([0, rng.randint(0, 300)])
+        tile = rng.randint(1, 7)
+        m = hostsim.sim_stream(w, h, 4, 2, 4, 1, n, A(kinds), A(offs), A(fns), A(nwps), wo, wl, wv,
+                               base, tile, out, BUF)
+        assert m == len(ref), (it, m)
+        got = bytes(out[:base + m + 128])
+        assert got[:base] == bytes((i * 37 + 11) & 255 for i in range(base))
+        assert got[base:base + m] == ref, it
+        end = base + m
+        le = (end + 127) & ~127
+        assert got[end:le] == bytes(le - end)

@@ -552,14 +552,15 @@ __global__ __launch_bounds__(EMIT_WAVES * 64) void k_emit(const DevStream *__res
         /* the 4 words of chunk v from entry data (len 0 = mixed) */
         auto words = [&](uint32_t v, uint32_t K, uint32_t len, uint32_t mag, const uint32_t q[6],
                          uint32_t w[4]) {
-            uint32_t pw[4];
-            pure_words(K + (v << 7), len ? len : 1u, mag, q, pw);
-            const uint32_t mi = len ? 0u : min(K + v, (uint32_t)MAXMX - 1u);
-            const uint4 mv = *reinterpret_cast<const uint4 *>(W.mw[mi]);
-            w[0] = len ? pw[0] : mv.x;
-            w[1] = len ? pw[1] : mv.y;
-            w[2] = len ? pw[2] : mv.z;
-            w[3] = len ? pw[3] : mv.w;
+            pure_words(K + (v << 7), len ? len : 1u, mag, q, w);
+            if (__ballot(len == 0u)) {                  /* some lane in a mixed entry */
+                const uint32_t mi = len ? 0u : min(K + v, (uint32_t)MAXMX - 1u);
+                const uint4 mv = *reinterpret_cast<const uint4 *>(W.mw[mi]);
+                w[0] = len ? w[0] : mv.x;
+                w[1] = len ? w[1] : mv.y;
+                w[2] = len ? w[2] : mv.z;
+                w[3] = len ? w[3] : mv.w;
+            }
         };
         const uint32_t nv = (flags & SCROLL_DEBUG_EMIT_NOPURE) ? 0u : (uint32_t)nch;
         const bool do_store = !(flags & SCROLL_DEBUG_EMIT_NOSTORE);

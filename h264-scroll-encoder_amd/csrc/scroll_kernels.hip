@@ -37,7 +37,10 @@ namespace {
 #endif
 constexpr int TILE = SCROLL_TILE;              /* NAL units per wave tile in k_emit */
 constexpr int EMIT_WAVES = SCROLL_EMIT_WAVES;  /* waves per k_emit workgroup        */
-constexpr int PLAN_THREADS = 256;
+#ifndef SCROLL_PLAN_THREADS
+#define SCROLL_PLAN_THREADS 1024   /* 16 waves: the NAL sizing pass is latency-bound */
+#endif
+constexpr int PLAN_THREADS = SCROLL_PLAN_THREADS;
 constexpr int PLAN_REWIND = 1 << 8;   /* k_plan flag: arena restarts at 0 */
 
 /* ---------------------------------------------------------------------- */

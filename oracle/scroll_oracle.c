@@ -291,6 +291,16 @@ static void or_mb_loop(or_bits *b, const or_cfg *c, int a_end,
     free(cur);
 }
 
+/* slice header of a scroll (non-reference) P frame, :549-553 */
+void or_scroll_header(or_bits *b, const or_cfg *c)
+{
+    int fn = c->frame_num % (1 << c->log2_mfn);
+    if (c->nwp > 0)
+        or_hdr_wp(b, c, fn, 0, -1);
+    else
+        or_hdr_plain(b, c, fn, 0);
+}
+
 /* :541-664 */
 size_t or_scroll_nal(uint8_t *dst, size_t cap, or_cfg *c, int off)
 {

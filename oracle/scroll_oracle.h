@@ -58,6 +58,8 @@ void or_ue(or_bits *b, uint32_t v);              /* bitwriter_write_ue   :50-74 
 void or_se(or_bits *b, int32_t v);               /* bitwriter_write_se   :91-101 */
 void or_trailing(or_bits *b);                    /* :103-111 */
 size_t or_bytes(or_bits *b);                     /* bitwriter_get_size :124-131 */
+/* slice header of a scroll P frame (src/h264_writer.c:549-553) */
+void or_scroll_header(or_bits *b, const or_cfg *c);
 
 /* ---- NAL framing restatement (src/nal.c) ---- */
 size_t or_rbsp_to_ebsp(uint8_t *dst, size_t cap, const uint8_t *src, size_t n); /* :24-50 */

@@ -1,0 +1,416 @@
+"""TEST-ONLY H.264 P-slice parser / reconstructor for the composer's NALs.
+
+Parses the slices this repository emits (CAVLC, P_L0_16x16 MBs, no skips) --
+slice header (7.3.3), mb layer (7.3.5), residual (7.3.5.3, CAVLC 9.2) -- and
+reconstructs the dynamic MBs (dequantisation 8.5.12.1, inverse transform
+8.5.12.2, chroma DC 8.5.11) on top of their inter prediction, so tests can
+check the residual coder end to end against the source pixels.  Written from
+the standard; its CAVLC tables are independent of the encoder's (oracle and
+device code) and of the reference's parser.
+"""
+
+# ---------------------------------------------------------------- bits -------
+
+def ebsp_to_rbsp(b):
+    out, zeros = bytearray(), 0
+    for x in b:
+        if zeros >= 2 and x == 3:
+            zeros = 0
+            continue
+        out.append(x)
+        zeros = zeros + 1 if x == 0 else 0
+    return bytes(out)
+
+
+class Bits:
+    def __init__(self, data, pos=0):
+        self.d, self.p = data, pos
+
+    def u(self, n):
+        v = 0
+        for _ in range(n):
+            v = (v << 1) | ((self.d[self.p >> 3] >> (7 - (self.p & 7))) & 1)
+            self.p += 1
+        return v
+
+    def ue(self):
+        z = 0
+        while self.u(1) == 0:
+            z += 1
+        return (1 << z) - 1 + (self.u(z) if z else 0)
+
+    def se(self):
+        k = self.ue()
+        return (k + 1) // 2 if k & 1 else -(k // 2)
+
+
+# ------------------------------------------------------------ CAVLC ---------
+# Table 9-5: code -> (TotalCoeff, TrailingOnes) per nC class (0: 0<=nC<2, 2: 2<=nC<4,
+# 4: 4<=nC<8, -1: chroma DC); nC >= 8 is a 6-bit FLC.
+CT_TABLES = {}
+
+
+def _init_tables():
+    # explicit (tc, t1) -> code per class (Table 9-5), written out to avoid
+    # ambiguity with fillers
+    rows = {
+        0: [["1"], ["000101", "01"], ["00000111", "000100", "001"],
+            ["000000111", "00000110", "0000101", "00011"],
+            ["0000000111", "000000110", "00000101", "000011"],
+            ["00000000111", "0000000110", "000000101", "0000100"],
+            ["0000000001111", "00000000110", "0000000101", "00000100"],
+            ["0000000001011", "0000000001110", "00000000101", "000000100"],
+            ["0000000001000", "0000000001010", "0000000001101", "0000000100"],
+            ["00000000001111", "00000000001110", "0000000001001", "00000000100"],
+            ["00000000001011", "00000000001010", "00000000001101", "0000000001100"],
+            ["000000000001111", "000000000001110", "00000000001001", "00000000001100"],
+            ["000000000001011", "000000000001010", "000000000001101", "00000000001000"],
+            ["0000000000001111", "000000000000001", "000000000001001", "000000000001100"],
+            ["0000000000001011", "0000000000001110", "0000000000001101", "000000000001000"],
+            ["0000000000000111", "0000000000001010", "0000000000001001", "0000000000001100"],
+            ["0000000000000100", "0000000000000110", "0000000000000101", "0000000000001000"]],
+        2: [["11"], ["001011", "10"], ["000111", "00111", "011"],
+            ["0000111", "001010", "001001", "0101"],
+            ["00000111", "000110", "000101", "0100"],
+            ["00000100", "0000110", "0000101", "00110"],
+            ["000000111", "00000110", "00000101", "001000"],
+            ["00000001111", "000000110", "000000101", "000100"],
+            ["00000001011", "00000001110", "00000001101", "0000100"],
+            ["000000001111", "00000001010", "00000001001", "000000100"],
+            ["000000001011", "000000001110", "000000001101", "00000001100"],
+            ["000000001000", "000000001010", "000000001001", "00000001000"],
+            ["0000000001111", "0000000001110", "0000000001101", "000000001100"],
+            ["0000000001011", "0000000001010", "0000000001001", "0000000001100"],
+            ["0000000000111", "00000000001011", "0000000000110", "0000000001000"],
+            ["00000000001001", "00000000001000", "00000000001010", "0000000000001"],
+            ["00000000000111", "00000000000110", "00000000000101", "00000000000100"]],
+        4: [["1111"], ["001111", "1110"], ["001011", "01111", "1101"],
+            ["001000", "01100", "01110", "1100"],
+            ["0001111", "01010", "01011", "1011"],
+            ["0001011", "01000", "01001", "1010"],
+            ["0001001", "001110", "001101", "1001"],
+            ["0001000", "001010", "001001", "1000"],
+            ["00001111", "0001110", "0001101", "01101"],
+            ["00001011", "00001110", "0001010", "001100"],
+            ["000001111", "00001010", "00001101", "0001100"],
+            ["000001011", "000001110", "00001001", "00001100"],
+            ["000001000", "000001010", "000001101", "00001000"],
+            ["0000001101", "000000111", "000001001", "000001100"],
+            ["0000001001", "0000001100", "0000001011", "0000001010"],
+            ["0000000101", "0000001000", "0000000111", "0000000110"],
+            ["0000000001", "0000000100", "0000000011", "0000000010"]],
+    }
+    for nc, rr in rows.items():
+        d = {}
+        for tc, row in enumerate(rr):
+            for t1, code in enumerate(row):
+                d[code] = (tc, t1)
+        CT_TABLES[nc] = d
+    dc = [["01"], ["000111", "1"], ["000100", "000110", "001"],
+          ["000011", "0000011", "0000010", "000101"],
+          ["000010", "00000011", "00000010", "0000000"]]
+    d = {}
+    for tc, row in enumerate(dc):
+        for t1, code in enumerate(row):
+            d[code] = (tc, t1)
+    CT_TABLES[-1] = d
+
+
+_init_tables()
+
+# total_zeros, Tables 9-7 / 9-8: TZ[tc] = list of codes for total_zeros 0..16-tc
+TZ = {
+    1: "1 011 010 0011 0010 00011 00010 000011 000010 0000011 0000010 00000011 00000010 000000011 000000010 000000001",
+    2: "111 110 101 100 011 0101 0100 0011 0010 00011 00010 000011 000010 000001 000000",
+    3: "0101 111 110 101 0100 0011 100 011 0010 00011 00010 000001 00001 000000",
+    4: "00011 111 0101 0100 110 101 100 0011 011 0010 00010 00001 00000",
+    5: "0101 0100 0011 111 110 101 100 011 0010 00001 0001 00000",
+    6: "000001 00001 111 110 101 100 011 010 0001 001 000000",
+    7: "000001 00001 101 100 011 11 010 0001 001 000000",
+    8: "000001 0001 00001 011 11 10 010 001 000000",
+    9: "000001 000000 0001 11 10 001 01 00001",
+    10: "00001 00000 001 11 10 01 0001",
+    11: "0000 0001 001 010 1 011",
+    12: "0000 0001 01 1 001",
+    13: "000 001 1 01",
+    14: "00 01 1",
+    15: "0 1",
+}
+TZ = {k: {c: i for i, c in enumerate(v.split())} for k, v in TZ.items()}
+TZDC = {1: {"1": 0, "01": 1, "001": 2, "000": 3}, 2: {"1": 0, "01": 1, "00": 2}, 3: {"1": 0, "0": 1}}
+RB = {
+    1: {"1": 0, "0": 1}, 2: {"1": 0, "01": 1, "00": 2}, 3: {"11": 0, "10": 1, "01": 2, "00": 3},
+    4: {"11": 0, "10": 1, "01": 2, "001": 3, "000": 4},
+    5: {"11": 0, "10": 1, "011": 2, "010": 3, "001": 4, "000": 5},
+    6: {"11": 0, "000": 1, "001": 2, "011": 3, "010": 4, "101": 5, "100": 6},
+    7: {"111": 0, "110": 1, "101": 2, "100": 3, "011": 4, "010": 5, "001": 6, "0001": 7,
+        "00001": 8, "000001": 9, "0000001": 10, "00000001": 11, "000000001": 12,
+        "0000000001": 13, "00000000001": 14},
+}
+
+
+def _match(bits, table, maxlen=16):
+    s = ""
+    for _ in range(maxlen):
+        s += str(bits.u(1))
+        if s in table:
+            return table[s]
+    raise ValueError("no VLC match: " + s)
+
+
+def cavlc_block(bits, nC, maxc):
+    """-> (coefficients in scan order [maxc], TotalCoeff)"""
+    if nC == -1:
+        tc, t1 = _match(bits, CT_TABLES[-1])
+    elif nC >= 8:
+        code = bits.u(6)
+        tc, t1 = (0, 0) if code == 3 else ((code >> 2) + 1, code & 3)
+    else:
+        tc, t1 = _match(bits, CT_TABLES[0 if nC < 2 else (2 if nC < 4 else 4)])
+    coef = [0] * maxc
+    if tc == 0:
+        return coef, 0
+    lv = []
+    for _ in range(t1):
+        lv.append(-1 if bits.u(1) else 1)
+    sl = 1 if (tc > 10 and t1 < 3) else 0
+    for i in range(tc - t1):
+        prefix = 0
+        while bits.u(1) == 0:
+            prefix += 1
+        code = (min(15, prefix) << sl)
+        if sl > 0 or prefix >= 14:
+            ssize = sl
+            if prefix == 14 and sl == 0:
+                ssize = 4
+            if prefix >= 15:
+                ssize = prefix - 3
+            if ssize:
+                code += bits.u(ssize)
+        if prefix >= 15 and sl == 0:
+            code += 15
+        if i == 0 and t1 < 3:
+            code += 2
+        level = (code + 2) >> 1 if code % 2 == 0 else -((code + 1) >> 1)
+        lv.append(level)
+        if sl == 0:
+            sl = 1
+        if abs(level) > (3 << (sl - 1)) and sl < 6:
+            sl += 1
+    tz = 0
+    if tc < maxc:
+        tz = _match(bits, TZDC[tc] if maxc == 4 else TZ[tc])
+    runs, zl = [], tz
+    for i in range(tc - 1):
+        r = _match(bits, RB[min(zl, 7)]) if zl > 0 else 0
+        runs.append(r)
+        zl -= r
+    runs.append(zl)
+    pos = tc + tz - 1
+    for i in range(tc):
+        coef[pos] = lv[i]
+        pos -= 1 + runs[i]
+    return coef, tc
+
+
+# ------------------------------------------------------- reconstruction ----
+ZZ = [0, 1, 4, 8, 5, 2, 3, 6, 9, 12, 13, 10, 7, 11, 14, 15]
+V = [[10, 16, 13], [11, 18, 14], [13, 20, 16], [14, 23, 18], [16, 25, 20], [18, 29, 23]]
+GOLOMB_TO_INTER_CBP = [0, 16, 1, 2, 4, 8, 32, 3, 5, 10, 12, 15, 47, 7, 11, 13, 14, 6, 9, 31, 35,
+                       37, 42, 44, 33, 34, 36, 40, 39, 43, 45, 46, 17, 18, 20, 24, 19, 21, 26, 28,
+                       23, 27, 29, 30, 22, 25, 38, 41]
+
+
+def _cls(i, j):
+    return 0 if (i % 2 == 0 and j % 2 == 0) else (1 if (i % 2 and j % 2) else 2)
+
+
+def dequant4x4(scan, qp, dc=None):
+    c = [0] * 16
+    for k in range(16):
+        c[ZZ[k]] = scan[k]
+    d = [0] * 16
+    for p in range(16):
+        i, j = divmod(p, 4)
+        d[p] = (c[p] * V[qp % 6][_cls(i, j)]) << (qp // 6)
+    if dc is not None:
+        d[0] = dc
+    return d
+
+
+def idct4x4(d):
+    t = [0] * 16
+    for i in range(4):
+        r = d[4 * i:4 * i + 4]
+        e0, e1 = r[0] + r[2], r[0] - r[2]
+        e2, e3 = (r[1] >> 1) - r[3], r[1] + (r[3] >> 1)
+        t[4 * i:4 * i + 4] = [e0 + e3, e1 + e2, e1 - e2, e0 - e3]
+    out = [0] * 16
+    for j in range(4):
+        c = [t[j], t[4 + j], t[8 + j], t[12 + j]]
+        e0, e1 = c[0] + c[2], c[0] - c[2]
+        e2, e3 = (c[1] >> 1) - c[3], c[1] + (c[3] >> 1)
+        for i, v in enumerate([e0 + e3, e1 + e2, e1 - e2, e0 - e3]):
+            out[4 * i + j] = (v + 32) >> 6
+    return out
+
+
+def slice_header(nal, log2_mfn=4, poc_type=2, log2_poc=4, deblock=1):
+    """-> (header dict, Bits positioned at the first MB, RBSP bytes)"""
+    assert nal[:4] == b"\x00\x00\x00\x01"
+    ref_idc = nal[4] >> 5
+    b = Bits(ebsp_to_rbsp(nal[5:]))
+    H = {"first_mb": b.ue(), "slice_type": b.ue(), "pps": b.ue(), "frame_num": b.u(log2_mfn)}
+    if poc_type == 0:
+        H["poc"] = b.u(log2_poc)
+    nrefs = 1
+    if b.u(1):
+        nrefs = b.ue() + 1
+    H["nrefs"] = nrefs
+    if b.u(1):
+        while True:
+            idc = b.ue()
+            if idc == 3:
+                break
+            b.ue()
+    if ref_idc:
+        if b.u(1):
+            while True:
+                op = b.ue()
+                if op == 0:
+                    break
+                if op in (1, 3):
+                    b.ue()
+                if op in (2, 3, 6):
+                    b.ue()
+                if op == 4:
+                    b.ue()
+    H["qp_delta"] = b.se()
+    if deblock:
+        if b.ue() != 1:
+            b.se(); b.se()
+    return H, b, b.d
+
+
+def parse_p_slice(nal, w, h, log2_mfn=4, poc_type=2, log2_poc=4, deblock=1, on_mb=None):
+    """Parse one P-slice NAL (Annex-B bytes).  on_mb(x, y, ref, mvd, cbp,
+    luma, cdc, cac) is called per MB with the decoded levels.  Returns the
+    header dict and the MB count."""
+    assert nal[:4] == b"\x00\x00\x00\x01"
+    hdr = nal[4]
+    ref_idc, nut = hdr >> 5, hdr & 31
+    b = Bits(ebsp_to_rbsp(nal[5:]))
+    H = {"first_mb": b.ue(), "slice_type": b.ue(), "pps": b.ue(), "frame_num": b.u(log2_mfn)}
+    if poc_type == 0:
+        H["poc"] = b.u(log2_poc)
+    nrefs = 1
+    if b.u(1):
+        nrefs = b.ue() + 1
+    H["nrefs"] = nrefs
+    if b.u(1):                                   # ref_pic_list_modification
+        while True:
+            idc = b.ue()
+            if idc == 3:
+                break
+            b.ue()
+    if ref_idc:
+        if b.u(1):                               # adaptive ref pic marking
+            while True:
+                op = b.ue()
+                if op == 0:
+                    break
+                if op in (1, 3):
+                    b.ue()
+                if op in (2, 3, 6):
+                    b.ue()
+                if op == 4:
+                    b.ue()
+    H["qp_delta"] = b.se()
+    if deblock:
+        if b.ue() != 1:
+            b.se(); b.se()
+    mbw, mbh = w // 16, h // 16
+    tc_above = [None] * mbw
+    n = 0
+    for y in range(mbh):
+        left = None
+        for x in range(mbw):
+            assert b.ue() == 0, "mb_skip_run"
+            assert b.ue() == 0, "mb_type"
+            if nrefs == 2:
+                ref = 1 - b.u(1)
+            elif nrefs > 2:
+                ref = b.ue()
+            else:
+                ref = 0
+            mvd = (b.se(), b.se())
+            cbp = GOLOMB_TO_INTER_CBP[b.ue()]
+            tcs = [0] * 24
+            luma = [[0] * 16 for _ in range(16)]
+            cdc = [[0] * 4 for _ in range(2)]
+            cac = [[[0] * 15 for _ in range(4)] for _ in range(2)]
+            if cbp:
+                b.se()                           # mb_qp_delta
+                top = tc_above[x]
+                for blk in range(16):
+                    q8, q4 = divmod(blk, 4)
+                    bx, by = (q8 % 2) * 2 + q4 % 2, (q8 // 2) * 2 + q4 // 2
+                    r = 4 * by + bx
+                    if not cbp & (1 << q8):
+                        continue
+                    nA = tcs[r - 1] if bx > 0 else (left[r + 3] if left else -1)
+                    nB = tcs[r - 4] if by > 0 else (top[r + 12] if top else -1)
+                    nc = (nA + nB + 1) >> 1 if nA >= 0 and nB >= 0 else (nA if nA >= 0 else (nB if nB >= 0 else 0))
+                    luma[r], tcs[r] = cavlc_block(b, nc, 16)
+                if cbp >> 4:
+                    for p in range(2):
+                        cdc[p], _ = cavlc_block(b, -1, 4)
+                    if (cbp >> 4) == 2:
+                        for p in range(2):
+                            for k in range(4):
+                                bx, by = k % 2, k // 2
+                                i = 16 + 4 * p + k
+                                nA = tcs[i - 1] if bx > 0 else (left[i + 1] if left else -1)
+                                nB = tcs[i - 2] if by > 0 else (top[i + 2] if top else -1)
+                                nc = (nA + nB + 1) >> 1 if nA >= 0 and nB >= 0 else (nA if nA >= 0 else (nB if nB >= 0 else 0))
+                                cac[p][k], tcs[i] = cavlc_block(b, nc, 15)
+            if on_mb:
+                on_mb(x, y, ref, mvd, cbp, luma, cdc, cac)
+            tc_above[x] = tcs
+            left = tcs
+            n += 1
+    # rbsp_stop_one_bit + alignment
+    assert b.u(1) == 1, "stop bit"
+    while b.p & 7:
+        assert b.u(1) == 0
+    assert b.p == 8 * len(b.d), (b.p, 8 * len(b.d))
+    return H, n
+
+
+def reconstruct_mb(luma, cdc, cac, pred_y, pred_u, pred_v, qp=26, qpc=26):
+    """Residual + prediction of one MB: pred_* are 16x16 / 8x8 lists (rows)."""
+    ry = [[0] * 16 for _ in range(16)]
+    for r in range(16):
+        res = idct4x4(dequant4x4(luma[r], qp))
+        bx, by = 4 * (r % 4), 4 * (r // 4)
+        for i in range(4):
+            for j in range(4):
+                ry[by + i][bx + j] = min(255, max(0, pred_y[by + i][bx + j] + res[4 * i + j]))
+    out_c = []
+    for p, pred in enumerate((pred_u, pred_v)):
+        c = cdc[p]
+        f = [c[0] + c[1] + c[2] + c[3], c[0] - c[1] + c[2] - c[3],
+             c[0] + c[1] - c[2] - c[3], c[0] - c[1] - c[2] + c[3]]
+        # 8.5.11.2: dcC = ((f * LevelScale4x4(qPc % 6, 0, 0)) << (qPc / 6)) >> 5 with
+        # LevelScale4x4 = 16 * V for flat weights
+        dcs = [((v * 16 * V[qpc % 6][0]) << (qpc // 6)) >> 5 for v in f]
+        rc = [[0] * 8 for _ in range(8)]
+        for k in range(4):
+            scan = [0] + cac[p][k]
+            res = idct4x4(dequant4x4(scan, qpc, dc=dcs[k]))
+            bx, by = 4 * (k % 2), 4 * (k // 2)
+            for i in range(4):
+                for j in range(4):
+                    rc[by + i][bx + j] = min(255, max(0, pred[by + i][bx + j] + res[4 * i + j]))
+        out_c.append(rc)
+    return ry, out_c[0], out_c[1]

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """bench.py -- composed frames/s of the MI355X scroll composer.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload p720]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload p720dyn|p720]
 
 One process per GPU (torch.distributed.run for N > 1; RANK / LOCAL_RANK /
 WORLD_SIZE from the env).  Streams are independent, so each rank owns a static
@@ -9,12 +9,20 @@ shard (its own streams; weak scaling, no collective in the data path; gloo is
 used only for the timing barrier / max-over-ranks).
 
 A step = one scroll_batch_compose over every stream of the rank:
-  workload p720 (BASELINE config 2): 256 streams x 1024 composed frames of
-  1280x720, offsets = SURVEY 8(d) synthetic scroll (speed 1+(s%8), phase
-  97 s mod 1440), resident in HBM before timing; output arenas in HBM are
-  rewound on device at every step (the bytes of a step are the product).
-Prints ONE JSON line (rank 0).  Also reports the dominant kernel's roofline
-(k_emit, HIP events on its launch stream) and the CPU oracle on host cores.
+  workload p720dyn (default, BASELINE config 3 -- the metric's "1280x720,
+  360x360 dyn"): 256 streams x 16 composed 1280x720 frames, each scroll NAL
+  with the 360x360 dynamic rect at MB (28, 10) coded by the 4x4 transform +
+  quant + CAVLC path; source pixels = the SURVEY 8(d) synthetic generator
+  (k_dyn_synth), reference pictures A / B = the experiment's striped I_PCM
+  pictures, one copy per stream; all resident in HBM before timing.
+  workload p720 (BASELINE config 2): 256 streams x 1024 composed frames,
+  P-only (no dynamic rect).
+  Offsets = SURVEY 8(d) synthetic scroll (speed 1+(s%8), phase 97 s mod 1440)
+  in HBM; output arenas are rewound on device at every step (the bytes of a
+  step are the product).
+Prints ONE JSON line (rank 0) with the dominant kernel's roofline (k_dyn_stage
+resp. k_emit, HIP events on its launch stream) and the CPU oracle on host
+cores (rank 0, N = 1).
 """
 import argparse
 import ctypes
@@ -31,10 +39,29 @@ HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 NAL_DESC_BYTES = 32            # NalDesc read per NAL by k_emit
 
 WORKLOADS = {
-    "p720": dict(w=1280, h=720, streams=256, frames=1024,
+    "p720dyn": dict(w=1280, h=720, streams=256, frames=16, rect=(28, 10, 25, 25),
+                    desc="BASELINE config 3: 256 concurrent 1280x720 streams + 360x360 "
+                         "synthetic dynamic rect (4x4 int transform + quant + CAVLC), "
+                         "composer_write_scroll_frame semantics"),
+    "p720": dict(w=1280, h=720, streams=256, frames=1024, rect=None,
                  desc="BASELINE config 2: 256 concurrent 1280x720 streams, P-only "
                       "(no dynamic rect), composer_write_scroll_frame semantics"),
 }
+
+
+def striped_i420(w, h, which):
+    """The experiment's striped I_PCM picture (experiments/scroll-encoder/src/
+    main.c:234-243 colours, h264_encoder.c:816-829 bands) as I420 bytes."""
+    import numpy as np
+    cols = ([81, 90, 240, 145, 54, 34, 41, 240, 110], [210, 16, 146, 170, 166, 16, 106, 202, 222])[which]
+    third = (h // 16) // 3
+    band = np.where(np.arange(h // 16) < third, 0, np.where(np.arange(h // 16) < 2 * third, 1, 2))
+    yrow = np.repeat(band, 16)
+    crow = yrow[::2]
+    Y = np.repeat(np.array([cols[3 * b] for b in yrow], np.uint8)[:, None], w, 1)
+    U = np.repeat(np.array([cols[3 * b + 1] for b in crow], np.uint8)[:, None], w // 2, 1)
+    V = np.repeat(np.array([cols[3 * b + 2] for b in crow], np.uint8)[:, None], w // 2, 1)
+    return Y.tobytes() + U.tobytes() + V.tobytes()
 
 
 def synthetic_offsets(first, nstreams, nframes, h):
@@ -71,6 +98,21 @@ def cpu_baseline(wl, threads):
         subprocess.run(["make", "-s", "-C", repo_oracle], check=True)
     lib = ctypes.CDLL(so)
     lib.or_bench_compose.restype = ctypes.c_double
+    lib.or_bench_compose_dyn.restype = ctypes.c_double
+    if wl["rect"]:
+        x0, y0, rw, rh = wl["rect"]
+        nstreams, nframes = 4 * threads, 64
+        nbytes = ctypes.c_ulonglong()
+        fps = lib.or_bench_compose_dyn(nstreams, nframes, wl["w"], wl["h"], x0, y0, rw, rh,
+                                       threads, ctypes.byref(nbytes))
+        fps1 = lib.or_bench_compose_dyn(1, 48, wl["w"], wl["h"], x0, y0, rw, rh, 1,
+                                        ctypes.byref(nbytes))
+        return dict(value=round(fps, 1), unit="frames/s", cores=threads, kind="port",
+                    sample=f"{nstreams} streams x {nframes} frames {wl['w']}x{wl['h']} + "
+                           f"360x360 dynamic rect ({rw}x{rh} MBs; same synthetic offsets, 4 source "
+                           f"frames cycled per stream), {threads} pthreads, "
+                           f"oracle/dyn_oracle.c -O2",
+                    single_core_fps=round(fps1, 1))
     nstreams, nframes = 256, 512
     nbytes = ctypes.c_ulonglong()
     fps = lib.or_bench_compose(nstreams, nframes, wl["w"], wl["h"], threads, 200,
@@ -97,7 +139,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default="p720", choices=sorted(WORKLOADS))
+    ap.add_argument("--workload", default="p720dyn", choices=sorted(WORKLOADS))
     ap.add_argument("--streams", type=int, default=0, help="override streams per GPU")
     ap.add_argument("--frames", type=int, default=0, help="override frames per step")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
@@ -125,11 +167,20 @@ def main():
     stream = torch.cuda.current_stream()
     S, F, W, H = wl["streams"], wl["frames"], wl["w"], wl["h"]
     first, _ = shard_streams(rank, world, S)       # static contiguous shard
+    rect = wl["rect"]
     per_frame_bound = 2 * (64 + (W // 16) * (H // 16))
-    b = hs.Batch(S, F, F * per_frame_bound + (1 << 16), device=local)
+    if rect:
+        per_frame_bound += 192 * rect[2] * rect[3]      # ~75 B per dynamic MB measured
+    b = hs.Batch(S, F, F * per_frame_bound + (1 << 20), device=local)
     for _ in range(S):
         b.add_stream(hs.make_config(W, H))
     b.set_offsets(synthetic_offsets(first, S, F, H))
+    if rect:
+        b.set_dyn_rect(*rect)
+        ra, rb = striped_i420(W, H, 0), striped_i420(W, H, 1)
+        for s in range(S):                               # one copy per stream (own traffic)
+            b.set_dyn_refs(ra, rb, stream=s)
+        b.dyn_source_synth(F, stream_base=first, t0=0)
 
     def barrier():
         torch.cuda.synchronize()
@@ -142,7 +193,7 @@ def main():
     if b.sync() != 0:
         raise RuntimeError(hs.last_error())
     b.enable_timing(True)
-    b.kernel_stats()                                # reset accumulators
+    b.kernel_stats_ex()                             # reset accumulators
     barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -151,10 +202,11 @@ def main():
     t1 = time.perf_counter()
     if b.sync() != 0:
         raise RuntimeError(hs.last_error())
-    plan_ms, emit_ms, n_emit = b.kernel_stats()
-    n_plan = n_emit
+    (plan_ms, emit_ms, stage_ms, demit_ms), n_launch = b.kernel_stats_ex()
     step_bytes = b.last_bytes()                     # per step, all streams of this rank
     step_nals = b.last_nals()
+    if rect:
+        rbsp_tot, ep_tot, dyn_nals = b.dyn_totals()
     b.enable_timing(False)
 
     el = max_over_ranks(t1 - t0, dist)
@@ -163,9 +215,20 @@ def main():
     ms_step = 1000.0 * el / args.steps
 
     if rank == 0:
-        emit_avg_ms = emit_ms / max(n_emit, 1)
-        alg_bytes = step_bytes + NAL_DESC_BYTES * step_nals   # per k_emit launch
-        achieved = alg_bytes / (emit_avg_ms * 1e-3) / 1e9
+        n = max(n_launch, 1)
+        kms = {"plan": plan_ms / n, "emit": emit_ms / n, "dyn_stage": stage_ms / n,
+               "dyn_emit": demit_ms / n}
+        if rect:
+            # k_dyn_stage per launch: source + prediction samples of every
+            # dynamic MB (384 B each) read, the staged RBSP written
+            kern = "k_dyn_stage"
+            alg_bytes = dyn_nals * 2 * 384 * rect[2] * rect[3] + rbsp_tot
+            kern_ms = kms["dyn_stage"]
+        else:
+            kern = "k_emit"
+            alg_bytes = step_bytes + NAL_DESC_BYTES * step_nals   # per k_emit launch
+            kern_ms = kms["emit"]
+        achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
         traffic = load_traffic(args.workload)
         out = {
             "metric": METRIC,
@@ -184,14 +247,17 @@ def main():
                        "streams_per_gpu": S, "frames_per_step": F,
                        "parallelism": f"static stream shard x{world}, no RCCL"},
             "bytes_per_frame": round(step_bytes / (S * F), 1),
-            "roofline": {"bound": "hbm", "kernel": "k_emit",
+            "roofline": {"bound": "hbm", "kernel": kern,
                          "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic.get("hbm_bytes_per_launch") if traffic else None,
                          "alg_bytes_per_launch": alg_bytes,
-                         "emit_ms_avg": round(emit_avg_ms, 4),
-                         "plan_ms_avg": round(plan_ms / max(n_plan, 1), 4)},
+                         "kernel_ms_avg": {k: round(v, 4) for k, v in kms.items()}},
         }
+        if rect:
+            out["config"]["dyn_rect_mb"] = list(rect)
+            out["dyn"] = {"rbsp_bytes_per_frame": round(rbsp_tot / max(dyn_nals, 1), 1),
+                          "ep_bytes_per_frame": round(ep_tot / max(dyn_nals, 1), 2)}
         if world == 1 and not args.no_cpu:
             threads = min(16, os.cpu_count() or 1)
             out["cpu_baseline"] = cpu_baseline(wl, threads)

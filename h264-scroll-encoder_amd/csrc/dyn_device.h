@@ -1,0 +1,440 @@
+/*
+ * dyn_device.h -- device functions of the dynamic-rect residual coder
+ * (BASELINE configs 3-5, SURVEY §8a "dynamic-MB splice"; no reference
+ * implementation exists, the bits are defined by oracle/dyn_oracle.h).
+ *
+ * Pure integer functions, no LDS / wave intrinsics: the kernels in
+ * dyn_kernels.hip use them per lane, and tests/hostsim compiles this header
+ * for the CPU to check each function against the oracle.
+ *
+ *  - prediction: full-pel luma, 1/8-pel bilinear chroma from the reference
+ *    pictures A / B, a waypoint (long-term ref 2+k) resolved through its own
+ *    row-uniform (ref, mv) (src/h264_writer.c:689-729), coordinates clamped;
+ *  - 4x4 forward core transform, flat quantiser at QP 26, chroma DC 2x2
+ *    Hadamard (dyn_oracle.c or_fwd4x4 / or_quant);
+ *  - CAVLC residual blocks (H.264 9.2) into any bit sink;
+ *  - the emulation-prevention rule in closed form (nal.c:33-38).
+ */
+#ifndef SCROLL_DYN_DEVICE_H
+#define SCROLL_DYN_DEVICE_H
+
+#include "scroll_device.h"
+
+namespace scroll {
+namespace dyn {
+
+constexpr int QP = 26;               /* pic_init_qp 26, slice_qp_delta 0 (h264_writer.c:118-120) */
+constexpr int QBITS = 15 + QP / 6;   /* 19 */
+constexpr int QF = (1 << QBITS) / 6; /* rounding offset f = 2^qbits / 6 */
+/* MF for QP % 6 == 2: classes (even, even) / (odd, odd) / mixed */
+constexpr int MF0 = 10082, MF1 = 4194, MF2 = 6554;
+/* provable bound on the bits of one dynamic MB (codeword + residual):
+ * 16 x 640 luma + 8 x 602 chroma AC + 2 x 130 chroma DC + cbp/qp + 64 < 16384 */
+constexpr int MB_BITS_MAX = 16384;
+
+/* coded_block_pattern -> codeNum, inter column of Table 9-4 */
+struct Tabs {
+    uint8_t ct_len[3][68], ct_bits[3][68];
+    uint8_t ctdc_len[20], ctdc_bits[20];
+    uint8_t tz_len[15][16], tz_bits[15][16];
+    uint8_t tzdc_len[3][4], tzdc_bits[3][4];
+    uint8_t rb_len[7][15], rb_bits[7][15];
+    uint8_t cbp_code[48];
+    uint8_t zz[16];
+};
+
+/* Tables 9-5 (coeff_token, 0 <= nC < 8 in three columns), 9-5 nC = -1,
+ * 9-7/9-8 (total_zeros), 9-9a (chroma DC total_zeros), 9-10 (run_before). */
+#define SCROLL_DYN_TABS                                                                        \
+    {{{1, 0, 0, 0, 6, 2, 0, 0, 8, 6, 3, 0, 9, 8, 7, 5, 10, 9, 8, 6, 11, 10, 9, 7, 13, 11, 10, 8, \
+       13, 13, 11, 9, 13, 13, 13, 10, 14, 14, 13, 11, 14, 14, 14, 13, 15, 15, 14, 14, 15, 15,    \
+       15, 14, 16, 15, 15, 15, 16, 16, 16, 15, 16, 16, 16, 16, 16, 16, 16, 16},                  \
+      {2, 0, 0, 0, 6, 2, 0, 0, 6, 5, 3, 0, 7, 6, 6, 4, 8, 6, 6, 4, 8, 7, 7, 5, 9, 8, 8, 6,       \
+       11, 9, 9, 6, 11, 11, 11, 7, 12, 11, 11, 9, 12, 12, 12, 11, 12, 12, 12, 11, 13, 13, 13,    \
+       12, 13, 13, 13, 13, 13, 14, 13, 13, 14, 14, 14, 13, 14, 14, 14, 14},                      \
+      {4, 0, 0, 0, 6, 4, 0, 0, 6, 5, 4, 0, 6, 5, 5, 4, 7, 5, 5, 4, 7, 5, 5, 4, 7, 6, 6, 4,       \
+       7, 6, 6, 4, 8, 7, 7, 5, 8, 8, 7, 6, 9, 8, 8, 7, 9, 9, 8, 8, 9, 9, 9, 8,                   \
+       10, 9, 9, 9, 10, 10, 10, 10, 10, 10, 10, 10, 10, 10, 10, 10}},                            \
+     {{1, 0, 0, 0, 5, 1, 0, 0, 7, 4, 1, 0, 7, 6, 5, 3, 7, 6, 5, 3, 7, 6, 5, 4, 15, 6, 5, 4,      \
+       11, 14, 5, 4, 8, 10, 13, 4, 15, 14, 9, 4, 11, 10, 13, 12, 15, 14, 9, 12, 11, 10, 13, 8,   \
+       15, 1, 9, 12, 11, 14, 13, 8, 7, 10, 9, 12, 4, 6, 5, 8},                                   \
+      {3, 0, 0, 0, 11, 2, 0, 0, 7, 7, 3, 0, 7, 10, 9, 5, 7, 6, 5, 4, 4, 6, 5, 6, 7, 6, 5, 8,     \
+       15, 6, 5, 4, 11, 14, 13, 4, 15, 10, 9, 4, 11, 14, 13, 12, 8, 10, 9, 8, 15, 14, 13, 12,    \
+       11, 10, 9, 12, 7, 11, 6, 8, 9, 8, 10, 1, 7, 6, 5, 4},                                     \
+      {15, 0, 0, 0, 15, 14, 0, 0, 11, 15, 13, 0, 8, 12, 14, 12, 15, 10, 11, 11, 11, 8, 9, 10,    \
+       9, 14, 13, 9, 8, 10, 9, 8, 15, 14, 13, 13, 11, 14, 10, 12, 15, 10, 13, 12, 11, 14, 9,     \
+       12, 8, 10, 13, 8, 13, 7, 9, 12, 9, 12, 11, 10, 5, 8, 7, 6, 1, 4, 3, 2}},                  \
+     {2, 0, 0, 0, 6, 1, 0, 0, 6, 6, 3, 0, 6, 7, 7, 6, 6, 8, 8, 7},                               \
+     {1, 0, 0, 0, 7, 1, 0, 0, 4, 6, 1, 0, 3, 3, 2, 5, 2, 3, 2, 0},                               \
+     {{1, 3, 3, 4, 4, 5, 5, 6, 6, 7, 7, 8, 8, 9, 9, 9}, {3, 3, 3, 3, 3, 4, 4, 4, 4, 5, 5, 6, 6, 6, 6}, \
+      {4, 3, 3, 3, 4, 4, 3, 3, 4, 5, 5, 6, 5, 6}, {5, 3, 4, 4, 3, 3, 3, 4, 3, 4, 5, 5, 5},      \
+      {4, 4, 4, 3, 3, 3, 3, 3, 4, 5, 4, 5}, {6, 5, 3, 3, 3, 3, 3, 3, 4, 3, 6},                   \
+      {6, 5, 3, 3, 3, 2, 3, 4, 3, 6}, {6, 4, 5, 3, 2, 2, 3, 3, 6}, {6, 6, 4, 2, 2, 3, 2, 5},     \
+      {5, 5, 3, 2, 2, 2, 4}, {4, 4, 3, 3, 1, 3}, {4, 4, 2, 1, 3}, {3, 3, 1, 2}, {2, 2, 1},       \
+      {1, 1}},                                                                                   \
+     {{1, 3, 2, 3, 2, 3, 2, 3, 2, 3, 2, 3, 2, 3, 2, 1}, {7, 6, 5, 4, 3, 5, 4, 3, 2, 3, 2, 3, 2, 1, 0}, \
+      {5, 7, 6, 5, 4, 3, 4, 3, 2, 3, 2, 1, 1, 0}, {3, 7, 5, 4, 6, 5, 4, 3, 3, 2, 2, 1, 0},      \
+      {5, 4, 3, 7, 6, 5, 4, 3, 2, 1, 1, 0}, {1, 1, 7, 6, 5, 4, 3, 2, 1, 1, 0},                   \
+      {1, 1, 5, 4, 3, 3, 2, 1, 1, 0}, {1, 1, 1, 3, 3, 2, 2, 1, 0}, {1, 0, 1, 3, 2, 1, 1, 1},     \
+      {1, 0, 1, 3, 2, 1, 1}, {0, 1, 1, 2, 1, 3}, {0, 1, 1, 1, 1}, {0, 1, 1, 1}, {0, 1, 1},       \
+      {0, 1}},                                                                                   \
+     {{1, 2, 3, 3}, {1, 2, 2, 0}, {1, 1, 0, 0}},                                                 \
+     {{1, 1, 1, 0}, {1, 1, 0, 0}, {1, 0, 0, 0}},                                                 \
+     {{1, 1}, {1, 2, 2}, {2, 2, 2, 2}, {2, 2, 2, 3, 3}, {2, 2, 3, 3, 3, 3},                      \
+      {2, 3, 3, 3, 3, 3, 3}, {3, 3, 3, 3, 3, 3, 3, 4, 5, 6, 7, 8, 9, 10, 11}},                   \
+     {{1, 0}, {1, 1, 0}, {3, 2, 1, 0}, {3, 2, 1, 1, 0}, {3, 2, 3, 2, 1, 0},                      \
+      {3, 0, 1, 3, 2, 5, 4}, {7, 6, 5, 4, 3, 2, 1, 1, 1, 1, 1, 1, 1, 1, 1}},                     \
+     {0, 2, 3, 7, 4, 8, 17, 13, 5, 18, 9, 14, 10, 15, 16, 11,                                    \
+      1, 32, 33, 36, 34, 37, 44, 40, 35, 45, 38, 41, 39, 42, 43, 19,                             \
+      6, 24, 25, 20, 26, 21, 46, 28, 27, 47, 22, 29, 23, 30, 31, 12},                            \
+     {0, 1, 4, 8, 5, 2, 3, 6, 9, 12, 13, 10, 7, 11, 14, 15}}
+
+/* ---------------------------------------------------------------------- */
+/* bit sinks                                                               */
+/* ---------------------------------------------------------------------- */
+struct CountSink {
+    uint32_t n;
+    __device__ __host__ inline void put(uint32_t, int k) { n += (uint32_t)k; }
+};
+
+/* ORs bits into a zero-initialised word buffer starting at any bit
+ * position; OR is the caller's atomic (LDS atomicOr) or plain |= on the
+ * CPU.  Words are written once each except the two boundary words. */
+template <class OR>
+struct OrSink {
+    OR orw;
+    uint32_t wi;                  /* word of the pending bits                  */
+    int fill;                     /* bits of word wi already used             */
+    uint64_t acc;                 /* pending bits, left-aligned in 64         */
+    __device__ __host__ inline void start(uint32_t pos)
+    {
+        wi = pos >> 5;
+        fill = (int)(pos & 31);
+        acc = 0;
+    }
+    __device__ __host__ inline void put(uint32_t v, int n)       /* n <= 32 */
+    {
+        if (n <= 0) return;
+        v &= low_mask(n);
+        acc |= ((uint64_t)v << (64 - n)) >> fill;
+        fill += n;
+        if (fill >= 32) {
+            orw(wi, (uint32_t)(acc >> 32));
+            acc <<= 32;
+            fill -= 32;
+            wi++;
+        }
+    }
+    __device__ __host__ inline void finish()
+    {
+        if (fill > 0 && acc) orw(wi, (uint32_t)(acc >> 32));
+    }
+};
+
+/* MB head without the trailing coded_block_pattern: mb_skip_run ue(0),
+ * mb_type ue(0), ref_idx te(v), mvd_x se, mvd_y se (h264_writer.c:434-453) */
+template <class S>
+__device__ __host__ inline void put_mb_head(S &s, int ref, int dx, int dy, int nrefs)
+{
+    s.put(1, 1);
+    s.put(1, 1);
+    if (nrefs == 2) s.put((uint32_t)(1 - (ref & 1)), 1);
+    else if (nrefs > 2) put_ue(s, (uint32_t)ref);
+    put_se(s, dx);
+    put_se(s, dy);
+}
+
+/* ---------------------------------------------------------------------- */
+/* prediction                                                              */
+/* ---------------------------------------------------------------------- */
+/* waypoint table of the frame being coded (entries only ever appended) */
+struct WpTab {
+    const int32_t *wo, *wv;
+    int h;                        /* picture height (luma)                    */
+};
+
+__device__ __host__ inline int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
+
+/* (ref, mv_px) of MB row `row` of waypoint frame k: src/h264_writer.c:689-729
+ * with the table as it stood when k was created (entries < k) */
+__device__ __host__ inline void wp_row(const WpTab &T, int k, int row, int &ref, int &mv)
+{
+    const int wo = T.wo[k];
+    const int a_end = (T.h - wo) / 16;                 /* C truncation (:690) */
+    if (row < a_end) {
+        int wa = -1, woa = 0;
+        if (wo > MVL && k > 0)
+            for (int i = 0; i < k; ++i) {
+                if (!T.wv[i]) continue;
+                const int w2 = T.wo[i];
+                if (w2 <= wo && w2 > woa && wo - w2 <= MVL) {
+                    wa = i;
+                    woa = w2;
+                }
+            }
+        ref = wa >= 0 ? 2 + wa : 0;
+        mv = wa >= 0 ? wo - woa : wo;
+    } else {
+        ref = 1;
+        mv = wo - T.h;
+    }
+}
+
+/* luma: row y of reference ri -> (picture A / B, clamped row).  A waypoint
+ * k only references pictures < k, so the chain ends within 9 steps. */
+__device__ __host__ inline int luma_row(const WpTab &T, int ri, int y, int &yo)
+{
+    y = clampi(y, 0, T.h - 1);
+    while (ri >= 2) {
+        int ref, mv;
+        wp_row(T, ri - 2, y / 16, ref, mv);
+        y = clampi(y + mv, 0, T.h - 1);
+        ri = ref;
+    }
+    yo = y;
+    return ri;
+}
+
+/* chroma: the same chain for a row while every waypoint step is full-pel
+ * (even mv, always so for waypoints created by the composer: offsets are
+ * multiples of 496 and h of 16).  Returns -1 at a half-pel step. */
+__device__ __host__ inline int chroma_row(const WpTab &T, int ri, int y, int &yo)
+{
+    const int hc = T.h / 2;
+    y = clampi(y, 0, hc - 1);
+    while (ri >= 2) {
+        int ref, mv;
+        wp_row(T, ri - 2, (2 * y) / 16, ref, mv);
+        if ((4 * mv) & 7) return -1;
+        y = clampi(y + ((4 * mv) >> 3), 0, hc - 1);
+        ri = ref;
+    }
+    yo = y;
+    return ri;
+}
+
+/* reference pictures of one stream: plane p of picture i */
+struct RefPics {
+    const uint8_t *pl[2][3];
+    int w, h;
+};
+
+/* general chroma sample (or_ref_sample): any depth, bilinear at half-pel
+ * waypoint steps.  D bounds the recursion (9 levels suffice). */
+template <int D>
+__device__ __host__ __attribute__((noinline)) int chroma_px_any(const WpTab &T, const RefPics &R,
+                                                                int ri, int p, int x, int y)
+{
+    const int hc = T.h / 2;
+    y = clampi(y, 0, hc - 1);
+    if (ri < 2) return R.pl[ri][p][(size_t)y * (R.w / 2) + x];
+    if constexpr (D == 0) {
+        return 0;
+    } else {
+        int ref, mv;
+        wp_row(T, ri - 2, (2 * y) / 16, ref, mv);
+        const int q = 4 * mv, o = q >> 3, f = q & 7;
+        const int a = chroma_px_any<D - 1>(T, R, ref, p, x, y + o);
+        if (!f) return a;
+        const int b = chroma_px_any<D - 1>(T, R, ref, p, x, y + o + 1);
+        return ((8 - f) * a + f * b + 4) >> 3;
+    }
+}
+
+/* ---------------------------------------------------------------------- */
+/* transform / quantisation                                                */
+/* ---------------------------------------------------------------------- */
+__device__ __host__ inline void fwd4x4(const int x[16], int W[16])
+{
+    int t[16];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int s0 = x[4 * i] + x[4 * i + 3], s1 = x[4 * i + 1] + x[4 * i + 2];
+        const int d0 = x[4 * i] - x[4 * i + 3], d1 = x[4 * i + 1] - x[4 * i + 2];
+        t[4 * i + 0] = s0 + s1;
+        t[4 * i + 1] = 2 * d0 + d1;
+        t[4 * i + 2] = s0 - s1;
+        t[4 * i + 3] = d0 - 2 * d1;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int s0 = t[j] + t[12 + j], s1 = t[4 + j] + t[8 + j];
+        const int d0 = t[j] - t[12 + j], d1 = t[4 + j] - t[8 + j];
+        W[j] = s0 + s1;
+        W[4 + j] = 2 * d0 + d1;
+        W[8 + j] = s0 - s1;
+        W[12 + j] = d0 - 2 * d1;
+    }
+}
+
+/* raster position pos of a 4x4 block */
+__device__ __host__ inline int quant(int w, int pos)
+{
+    const int i = pos >> 2, j = pos & 3;
+    const int mf = ((i | j) & 1) == 0 ? MF0 : (((i & j) & 1) ? MF1 : MF2);
+    const int a = w < 0 ? -w : w;
+    const int z = (a * mf + QF) >> QBITS;             /* |w| <= 9180: no overflow */
+    return w < 0 ? -z : z;
+}
+
+__device__ __host__ inline int quant_dc(int w)
+{
+    const int a = w < 0 ? -w : w;
+    const int z = (a * MF0 + 2 * QF) >> (QBITS + 1);  /* |w| <= 16320 */
+    return w < 0 ? -z : z;
+}
+
+/* ---------------------------------------------------------------------- */
+/* CAVLC (9.2)                                                             */
+/* ---------------------------------------------------------------------- */
+__device__ __host__ inline int nc_of(int nA, int nB)
+{
+    if (nA >= 0 && nB >= 0) return (nA + nB + 1) >> 1;
+    if (nA >= 0) return nA;
+    if (nB >= 0) return nB;
+    return 0;
+}
+
+template <class S>
+__device__ __host__ inline void put_level(S &s, int code, int sl)
+{
+    int prefix, ssize = sl, suffix = 0;
+    if (sl == 0) {
+        if (code < 14) {
+            prefix = code;
+            ssize = 0;
+        } else if (code < 30) {
+            prefix = 14;
+            ssize = 4;
+            suffix = code - 14;
+        } else {
+            prefix = 15;
+            ssize = 12;
+            suffix = code - 30;
+        }
+    } else if (code < (15 << sl)) {
+        prefix = code >> sl;
+        suffix = code & ((1 << sl) - 1);
+    } else {
+        prefix = 15;
+        ssize = 12;
+        suffix = code - (15 << sl);
+    }
+    s.put(1, prefix + 1);                              /* prefix zeros, then '1' */
+    if (ssize) s.put((uint32_t)suffix, ssize);
+}
+
+/* coef: `max` levels in scan order (16 luma, 15 AC, 4 chroma DC with
+ * nC = -1); returns TotalCoeff.  Works on a non-zero mask and reads the
+ * levels in place (no per-lane arrays: nothing spills to scratch). */
+__device__ __host__ inline int top_bit(uint32_t m) { return 31 - __clz((int)m); }
+
+template <class S, class C>
+__device__ __host__ inline int cavlc_block(S &s, const Tabs &T, const C *coef, int max, int nC)
+{
+    uint32_t nz = 0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+        if (i < max && coef[i]) nz |= 1u << i;
+    const int tc = __builtin_popcount(nz);
+    int t1 = 0;
+    {
+        uint32_t m = nz;
+        while (m && t1 < 3) {
+            const int p = top_bit(m);
+            const int v = coef[p];
+            if (v != 1 && v != -1) break;
+            t1++;
+            m &= ~(1u << p);
+        }
+    }
+    if (nC == -1) {
+        s.put(T.ctdc_bits[4 * tc + t1], T.ctdc_len[4 * tc + t1]);
+    } else if (nC >= 8) {
+        s.put(tc ? (uint32_t)(((tc - 1) << 2) | t1) : 3u, 6);
+    } else {
+        const int tb = nC < 2 ? 0 : (nC < 4 ? 1 : 2);
+        s.put(T.ct_bits[tb][4 * tc + t1], T.ct_len[tb][4 * tc + t1]);
+    }
+    if (tc == 0) return 0;
+    const int hi = top_bit(nz);
+    uint32_t m = nz;
+    for (int k = 0; k < t1; ++k) {
+        const int p = top_bit(m);
+        s.put(coef[p] < 0 ? 1u : 0u, 1);
+        m &= ~(1u << p);
+    }
+    int sl = (tc > 10 && t1 < 3) ? 1 : 0;
+    for (int k = t1; k < tc; ++k) {
+        const int p = top_bit(m);
+        m &= ~(1u << p);
+        const int L = coef[p];
+        int code = L > 0 ? 2 * L - 2 : -2 * L - 1;
+        if (k == t1 && t1 < 3) code -= 2;
+        put_level(s, code, sl);
+        if (sl == 0) sl = 1;
+        if ((L < 0 ? -L : L) > (3 << (sl - 1)) && sl < 6) sl++;
+    }
+    const int tz = hi + 1 - tc;
+    if (tc < max) {
+        if (max == 4) s.put(T.tzdc_bits[tc - 1][tz], T.tzdc_len[tc - 1][tz]);
+        else s.put(T.tz_bits[tc - 1][tz], T.tz_len[tc - 1][tz]);
+    }
+    int zl = tz;
+    m = nz;
+    int p = hi;
+    for (int k = 0; k < tc - 1 && zl > 0; ++k) {
+        m &= ~(1u << p);
+        const int q = top_bit(m);
+        const int run = p - q - 1;
+        const int zi = (zl < 7 ? zl : 7) - 1;
+        s.put(T.rb_bits[zi][run], T.rb_len[zi][run]);
+        zl -= run;
+        p = q;
+    }
+    return tc;
+}
+
+/* ---------------------------------------------------------------------- */
+/* emulation prevention in closed form                                     */
+/* ---------------------------------------------------------------------- */
+/* nal.c:33-38 inserts 0x03 before RBSP byte i iff b_i <= 3 and the automaton
+ * has seen two zero bytes since its last reset.  With k = the number of
+ * zero bytes immediately before i in the ORIGINAL RBSP, that state is
+ * exactly "k >= 2 and k even" (runs of zeros insert at k = 2, 4, 6, ...),
+ * so every byte decides independently once k is known. */
+__device__ __host__ inline bool ep_insert(uint32_t b, int k) { return b <= 3 && k >= 2 && !(k & 1); }
+
+/* raster index of luma4x4BlkIdx blk (6.4.3) */
+__device__ __host__ inline int blk_raster(int blk)
+{
+    const int q8 = blk >> 2, q4 = blk & 3;
+    return 4 * ((q8 >> 1) * 2 + (q4 >> 1)) + (q8 & 1) * 2 + (q4 & 1);
+}
+
+/* ---------------------------------------------------------------------- */
+/* MB order inside a NAL with the rect                                     */
+/* ---------------------------------------------------------------------- */
+struct Rect {
+    int x0, y0, w, h;
+};
+
+/* number of dynamic MBs before MB m (coding order) */
+__device__ __host__ inline int dyn_rank(const Rect &r, int mbw, int m)
+{
+    const int y = m / mbw, x = m - y * mbw;
+    if (y < r.y0) return 0;
+    if (y >= r.y0 + r.h) return r.w * r.h;
+    return (y - r.y0) * r.w + clampi(x - r.x0, 0, r.w);
+}
+
+/* MB index of dynamic MB number q */
+__device__ __host__ inline int dyn_mb(const Rect &r, int mbw, int q)
+{
+    const int ry = q / r.w;
+    return (r.y0 + ry) * mbw + r.x0 + (q - ry * r.w);
+}
+
+}  // namespace dyn
+}  // namespace scroll
+#endif

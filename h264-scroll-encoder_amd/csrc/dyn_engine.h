@@ -1,0 +1,24 @@
+/*
+ * dyn_engine.h -- engine-internal launchers of the dynamic-rect kernels
+ * (dyn_kernels.hip), used by the batch engine (scroll_kernels.hip).
+ */
+#ifndef SCROLL_DYN_ENGINE_H
+#define SCROLL_DYN_ENGINE_H
+
+#include <hip/hip_runtime.h>
+#include "engine.h"
+
+/* all return 0, or -1 when the launch failed */
+int dyn_launch_stage(hipStream_t hs, int nframes, int S, DevStream *st, const NalDesc *nal,
+                     int ld_nal, const PlanPending *pend, DynFrame *dfr, int ld_fr,
+                     const DynGeom *g, const uint8_t *src, const uint8_t *refs, uint8_t *stage);
+int dyn_launch_emit(hipStream_t hs, int nframes, int S, const DevStream *st, const NalDesc *nal,
+                    int ld_nal, const DynFrame *dfr, int ld_fr, const DynGeom *g,
+                    const uint8_t *stage, uint8_t *arena, uint64_t ld_arena);
+int dyn_launch_synth(hipStream_t hs, int nframes, int S, uint8_t *src, const DynGeom *g,
+                     int stream_base, int t0);
+
+/* staging bytes per frame that no dynamic NAL can exceed */
+size_t dyn_slot_bound(int mbw, int mbh, int rw, int rh);
+
+#endif

@@ -1,0 +1,756 @@
+/*
+ * dyn_kernels.hip -- MI355X (gfx950) kernels of the dynamic-rect residual
+ * coder (BASELINE configs 3-5).  A scroll NAL with the rect is no longer a
+ * handful of periodic runs: every dynamic MB carries a CAVLC residual, and
+ * 60 % of such NALs need emulation prevention.  So these NALs take their own
+ * two kernels around the plan's sizing pass:
+ *
+ *   k_plan (state pass)   waypoint state machine, NalDesc per NAL
+ *   k_dyn_stage           one workgroup per dynamic NAL: its whole RBSP into
+ *                         a staging slot + its exact emulation-prevention count
+ *   k_plan (size pass)    NAL sizes (dynamic: 5 + RBSP + EP), arena offsets
+ *   k_emit                every other NAL (dynamic NALs are "external")
+ *   k_dyn_emit            staged RBSP -> arena: start code, NAL header, EP
+ *                         bytes, written in whole 128-byte lines
+ *
+ * The bits are those of oracle/dyn_oracle.c (or_scroll_nal_dyn); parity is
+ * checked bit-exact by tests/test_gpu_dyn.py.  Roofline: HBM (source pixels
+ * + reference pixels in, NAL bytes out), DESIGN.md §5.
+ */
+#include <hip/hip_runtime.h>
+
+#include <stdint.h>
+
+#include "dyn_device.h"
+#include "dyn_engine.h"
+
+using namespace scroll;
+using namespace scroll::dyn;
+
+namespace {
+
+__constant__ Tabs g_tabs = SCROLL_DYN_TABS;
+
+constexpr int DT = 256;                 /* threads per workgroup                */
+constexpr int NW = DT / 64;
+constexpr int WMB = DYN_WINDOW_MBS;     /* dynamic MBs per window: 24 x 10 = 240 block tasks */
+static_assert(24 * WMB <= 256, "one block task per thread");
+constexpr int WIN = DT;                 /* MBs per window (one MB per thread)    */
+constexpr int HEAD_MAX = 160;           /* bits of one MB head (huge mvd: 2 x 63 + ref) */
+constexpr int HDR_MAX = 1024;           /* slice header bits (8 waypoints + MMCO ~ 250) */
+constexpr int BUF_WORDS = (HDR_MAX + 32 + WMB * MB_BITS_MAX + WIN * HEAD_MAX) / 32 + 4;
+constexpr int OBUF = 6400;              /* k_dyn_emit: 127 carry + 5 + 4096 x 1.5 */
+
+__device__ inline int wave_incl_max(int v, int lane)
+{
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const int u = __shfl_up(v, d, 64);
+        if (lane >= d) v = max(v, u);
+    }
+    return v;
+}
+
+__device__ inline uint32_t wave_incl_sum(uint32_t v, int lane)
+{
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t u = __shfl_up(v, d, 64);
+        if (lane >= d) v += u;
+    }
+    return v;
+}
+
+/* exclusive prefix max over the workgroup (identity -1) and the total;
+ * ends with a barrier so `ws` can be reused */
+__device__ inline void block_excl_max(int v, int *ws, int &excl, int &tot)
+{
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int incl = wave_incl_max(v, lane);
+    if (lane == 63) ws[wave] = incl;
+    int e = __shfl_up(incl, 1, 64);
+    if (lane == 0) e = -1;
+    __syncthreads();
+    int pm = -1, t = -1;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+        if (w < wave) pm = max(pm, ws[w]);
+        t = max(t, ws[w]);
+    }
+    excl = max(pm, e);
+    tot = t;
+    __syncthreads();
+}
+
+__device__ inline void block_excl_sum(uint32_t v, uint32_t *ws, uint32_t &excl, uint32_t &tot)
+{
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t incl = wave_incl_sum(v, lane);
+    if (lane == 63) ws[wave] = incl;
+    __syncthreads();
+    uint32_t pm = 0, t = 0;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+        if (w < wave) pm += ws[w];
+        t += ws[w];
+    }
+    excl = pm + incl - v;
+    tot = t;
+    __syncthreads();
+}
+
+struct LdsOr {
+    uint32_t *b;
+    __device__ inline void operator()(uint32_t i, uint32_t v) const { atomicOr(&b[i], v); }
+};
+typedef OrSink<LdsOr> LSink;
+
+__device__ inline uint32_t ld32(const uint8_t *p) { return *reinterpret_cast<const uint32_t *>(p); }
+
+/* number of EP insertions among the 4 bytes of MSB-first word w whose
+ * global indices start at g (only bytes < lim count); prev = index of the
+ * last non-zero byte before them, updated */
+__device__ inline uint32_t ep_word(uint32_t w, uint32_t g, uint32_t lim, int &prev)
+{
+    uint32_t n = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const uint32_t gi = g + (uint32_t)i;
+        if (gi >= lim) break;
+        const uint32_t b = (w >> (24 - 8 * i)) & 255u;
+        n += ep_insert(b, (int)gi - 1 - prev) ? 1u : 0u;
+        if (b) prev = (int)gi;
+    }
+    return n;
+}
+
+/* ---------------------------------------------------------------------- */
+/* k_dyn_stage                                                             */
+/* ---------------------------------------------------------------------- */
+/* Block tasks of a window with nd dynamic MBs: luma first (lanes walk the
+ * MBs' 4-pixel columns so a block row of the window is one contiguous
+ * source read), then Cb, Cr. */
+struct Task {
+    int k, blk, bx, by, p;
+    bool luma;
+};
+
+__device__ inline Task task_of(int t, int nd)
+{
+    Task q;
+    if (t < 16 * nd) {
+        q.luma = true;
+        q.p = 0;
+        q.by = t / (4 * nd);
+        const int c4 = t - q.by * 4 * nd;
+        q.k = c4 >> 2;
+        q.bx = c4 & 3;
+        q.blk = 4 * q.by + q.bx;
+    } else {
+        const int u = t - 16 * nd;
+        q.luma = false;
+        q.p = u / (4 * nd);
+        const int r = u - q.p * 4 * nd;
+        q.by = r / (2 * nd);
+        const int c2 = r - q.by * 2 * nd;
+        q.k = c2 >> 1;
+        q.bx = c2 & 1;
+        q.blk = 16 + 4 * q.p + 2 * q.by + q.bx;
+    }
+    return q;
+}
+
+struct StageLds {
+    uint32_t buf[BUF_WORDS];      /* NAL bits from word `bw` of the slot on       */
+    int16_t lv[WMB][24][16];      /* levels in scan order: luma raster 0..15, AC 16+4p+kk */
+    int32_t dcraw[WMB][2][4];     /* chroma DC coefficients before the Hadamard   */
+    int16_t dclv[WMB][2][4];
+    uint8_t tc[WMB][24];          /* TotalCoeff per 4x4 block                     */
+    int8_t nc[WMB][24];
+    uint8_t cbp[WMB];
+    uint16_t blen[WMB][26];       /* pieces: luma raster 0..15, DC 16+p, AC 18+4p+kk */
+    uint16_t boff[WMB][26];
+    uint32_t mbo[WMB];            /* bit offset of a dynamic MB in the window     */
+    uint8_t ctx[DYN_CTX_MB][8];   /* bottom-row TotalCoeff of rect MBs (row ring) */
+    uint8_t lcarry[8];            /* right-column TotalCoeff of the last dyn MB   */
+    uint32_t wsum[NW];
+    int32_t wmax[NW];
+    int32_t wo[8], wl[8], wv[8];
+    uint32_t F, bw;
+    int32_t general;              /* a half-pel waypoint step was met            */
+    Tabs tabs;
+};
+
+constexpr uint32_t DF_OVER = 1u, DF_GENERAL = 2u;   /* DynFrame.err bits */
+
+/* GENERAL = false: every waypoint step is full-pel (always so for waypoints
+ * the composer creates); a NAL that meets a half-pel step is flagged and
+ * redone by the GENERAL instantiation, which evaluates the bilinear tree. */
+template <bool GENERAL>
+__global__ __launch_bounds__(DT) void k_dyn_stage(DevStream *__restrict__ st,
+                                                  const NalDesc *__restrict__ nal, int ld_nal,
+                                                  const PlanPending *__restrict__ pend,
+                                                  DynFrame *__restrict__ dfr, int ld_fr,
+                                                  DynGeom g, const uint8_t *__restrict__ src,
+                                                  const uint8_t *__restrict__ refs,
+                                                  uint8_t *__restrict__ stage)
+{
+    __shared__ StageLds L;
+    const int f = blockIdx.x, s = blockIdx.y, t = threadIdx.x;
+    DevStream *S = st + s;
+    DynFrame *DF = dfr + (size_t)s * ld_fr + f;
+    const int j = DF->nal;
+    if (j < 0) return;
+    if (GENERAL && !(DF->err & DF_GENERAL)) return;
+
+    const Rect R{g.x0, g.y0, g.w, g.h};
+    if (t == 0) L.general = 0;
+    if (t < 8) {
+        L.wo[t] = pend[s].wo[t];
+        L.wl[t] = pend[s].wl[t];
+        L.wv[t] = pend[s].wv[t];
+    }
+    for (int i = t; i < (int)sizeof(Tabs); i += DT)
+        reinterpret_cast<uint8_t *>(&L.tabs)[i] = reinterpret_cast<const uint8_t *>(&g_tabs)[i];
+    for (int i = t; i < BUF_WORDS; i += DT) L.buf[i] = 0u;
+    const NalDesc d = nal[(size_t)s * ld_nal + j];
+    NalCtx c;
+    c.w = S->w;
+    c.h = S->h;
+    c.log2_mfn = S->log2_mfn;
+    c.poc_type = S->poc_type;
+    c.log2_poc = S->log2_poc;
+    c.deblock = S->deblock;
+    c.kind = d.kind;
+    c.off = d.off;
+    c.frame_num = d.frame_num;
+    c.nwp = d.nwp;
+    c.wp_off = L.wo;
+    c.wp_lt = L.wl;
+    c.wp_valid = L.wv;
+    __syncthreads();
+
+    if (t == 0) {                                  /* slice header (h264_writer.c:549-553) */
+        LSink hs{{L.buf}, 0, 0, 0};
+        hs.start(0);
+        emit_slice_header(hs, c);
+        const uint32_t hb = hs.wi * 32u + (uint32_t)hs.fill;
+        hs.finish();
+        L.F = hb;
+        L.bw = 0;
+    }
+
+    const int w = c.w, h = c.h, mbw = w / 16, mbh = h / 16;
+    const Regions rg = regions(c);
+    const int a_end = (h - c.off) / 16;
+    const int nrefs = 2 + c.nwp;
+    const WpTab T{L.wo, L.wv, h};
+    const uint8_t *rb = refs + (size_t)s * g.ref_ld;
+    const size_t ysz = (size_t)w * h, csz = ysz / 4;
+    RefPics P;
+    P.w = w;
+    P.h = h;
+    for (int i = 0; i < 2; ++i) {
+        P.pl[i][0] = rb + i * (ysz + 2 * csz);
+        P.pl[i][1] = P.pl[i][0] + ysz;
+        P.pl[i][2] = P.pl[i][1] + csz;
+    }
+    const uint8_t *fs = src + (size_t)s * g.src_ld + (size_t)f * g.src_fr;
+    const int lstride = 16 * R.w, cstride = 8 * R.w;
+    const uint8_t *fcb = fs + (size_t)256 * R.w * R.h, *fcr = fcb + (size_t)64 * R.w * R.h;
+    const int ring = g.ring;
+    uint32_t *out = reinterpret_cast<uint32_t *>(stage + ((size_t)s * ld_fr + f) * g.slot_bytes);
+    const uint32_t cap_words = (uint32_t)(g.slot_bytes / 4) - 4u;
+    const Tabs &TB = L.tabs;
+
+    int carry = -1;              /* last non-zero RBSP byte flushed so far        */
+    uint32_t my_ep = 0;
+    bool over = false;
+    const int nmb = mbw * mbh, ndt = R.w * R.h;
+    for (int m0 = 0; m0 < nmb;) {
+        const int q0 = dyn_rank(R, mbw, m0);
+        int m1 = min(m0 + WIN, nmb);
+        if (q0 + WMB < ndt) m1 = min(m1, dyn_mb(R, mbw, q0 + WMB));
+        const int nd = dyn_rank(R, mbw, m1) - q0;
+        const int nm = m1 - m0;
+
+        /* A: residual -> levels, TotalCoeff (one 4x4 block per thread) */
+        if (t < 24 * nd) {
+            const Task q = task_of(t, nd);
+            const int m = dyn_mb(R, mbw, q0 + q.k), row = m / mbw, col = m - row * mbw;
+            const int cx = col - R.x0, ry = row - R.y0;
+            const bool curA = row < a_end;
+            const int ref = curA ? rg.ra : rg.rb, mvp = curA ? rg.mva : rg.mvb;
+            int res[16], W[16];
+            if (q.luma) {
+                const uint8_t *sp = fs + (size_t)(16 * ry + 4 * q.by) * lstride + 16 * cx + 4 * q.bx;
+                const int X = 16 * col + 4 * q.bx, Y = 16 * row + 4 * q.by;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const uint32_t sv = ld32(sp + (size_t)i * lstride);
+                    int yo;
+                    const int b = luma_row(T, ref, Y + i + mvp, yo);
+                    const uint32_t pv = ld32(P.pl[b][0] + (size_t)yo * w + X);
+#pragma unroll
+                    for (int x = 0; x < 4; ++x)
+                        res[4 * i + x] = (int)((sv >> (8 * x)) & 255u) - (int)((pv >> (8 * x)) & 255u);
+                }
+                fwd4x4(res, W);
+                int n = 0;
+#pragma unroll
+                for (int k2 = 0; k2 < 16; ++k2) {
+                    const int zp = TB.zz[k2];
+                    const int v = quant(W[zp], zp);
+                    L.lv[q.k][q.blk][k2] = (int16_t)v;
+                    n += v != 0;
+                }
+                L.tc[q.k][q.blk] = (uint8_t)n;
+                if (q.by == 3) L.ctx[(ry % ring) * R.w + cx][q.bx] = (uint8_t)n;
+            } else {
+                const uint8_t *sp = (q.p ? fcr : fcb) + (size_t)(8 * ry + 4 * q.by) * cstride +
+                                    8 * cx + 4 * q.bx;
+                const int X = 8 * col + 4 * q.bx, Y = 8 * row + 4 * q.by;
+                const int qq = 4 * mvp, o = qq >> 3, fr = qq & 7;
+                const int cw = w / 2;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const uint32_t sv = ld32(sp + (size_t)i * cstride);
+                    const int ya = Y + i + o;
+                    int yoa = 0, yob = 0;
+                    const int ba = chroma_row(T, ref, ya, yoa);
+                    const int bb = fr ? chroma_row(T, ref, ya + 1, yob) : 0;
+                    int pred[4];
+                    if (!GENERAL && (ba < 0 || bb < 0)) {
+                        L.general = 1;
+                        pred[0] = pred[1] = pred[2] = pred[3] = 0;
+                    } else if (ba >= 0 && bb >= 0) {
+                        const uint32_t av = ld32(P.pl[ba][1 + q.p] + (size_t)yoa * cw + X);
+                        const uint32_t bv = fr ? ld32(P.pl[bb][1 + q.p] + (size_t)yob * cw + X) : 0u;
+#pragma unroll
+                        for (int x = 0; x < 4; ++x) {
+                            const int a = (int)((av >> (8 * x)) & 255u), b = (int)((bv >> (8 * x)) & 255u);
+                            pred[x] = ((8 - fr) * a + fr * b + 4) >> 3;
+                        }
+                    } else {                       /* half-pel waypoint step: general path */
+                        if constexpr (GENERAL) {
+                            for (int x = 0; x < 4; ++x) {
+                                const int a = chroma_px_any<9>(T, P, ref, 1 + q.p, X + x, ya);
+                                const int b = fr ? chroma_px_any<9>(T, P, ref, 1 + q.p, X + x, ya + 1) : 0;
+                                pred[x] = ((8 - fr) * a + fr * b + 4) >> 3;
+                            }
+                        }
+                    }
+#pragma unroll
+                    for (int x = 0; x < 4; ++x) res[4 * i + x] = (int)((sv >> (8 * x)) & 255u) - pred[x];
+                }
+                fwd4x4(res, W);
+                L.dcraw[q.k][q.p][2 * q.by + q.bx] = W[0];
+                int n = 0;
+#pragma unroll
+                for (int k2 = 1; k2 < 16; ++k2) {
+                    const int zp = TB.zz[k2];
+                    const int v = quant(W[zp], zp);
+                    L.lv[q.k][q.blk][k2 - 1] = (int16_t)v;
+                    n += v != 0;
+                }
+                L.tc[q.k][q.blk] = (uint8_t)n;
+                if (q.by == 1) L.ctx[(ry % ring) * R.w + cx][4 + 2 * q.p + q.bx] = (uint8_t)n;
+            }
+        }
+        __syncthreads();
+        if (!GENERAL && L.general) {                /* uniform: read after the barrier */
+            if (t == 0) DF->err = DF_GENERAL;
+            return;
+        }
+
+        /* B: nC, coded flags, CAVLC lengths; chroma DC Hadamard + quant */
+        if (t < 24 * nd) {
+            const Task q = task_of(t, nd);
+            const int m = dyn_mb(R, mbw, q0 + q.k), row = m / mbw, col = m - row * mbw;
+            const int cx = col - R.x0, ry = row - R.y0;
+            const bool ldyn = col > R.x0, lav = col > 0, tdyn = row > R.y0, tav = row > 0;
+            const uint8_t *tc = L.tc[q.k];
+            int nA, nB;
+            bool coded;
+            if (q.luma) {
+                const int r = q.blk;
+                nA = q.bx > 0 ? tc[r - 1]
+                              : (ldyn ? (q.k > 0 ? L.tc[q.k - 1][r + 3] : L.lcarry[q.by]) : (lav ? 0 : -1));
+                nB = q.by > 0 ? tc[r - 4]
+                              : (tdyn ? L.ctx[((ry - 1) % ring) * R.w + cx][q.bx] : (tav ? 0 : -1));
+                const int b8 = 4 * (q.by & 2) + (q.bx & 2);
+                coded = (tc[b8] | tc[b8 + 1] | tc[b8 + 4] | tc[b8 + 5]) != 0;
+            } else {
+                const int i = q.blk;
+                nA = q.bx > 0 ? tc[i - 1]
+                              : (ldyn ? (q.k > 0 ? L.tc[q.k - 1][i + 1] : L.lcarry[4 + 2 * q.p + q.by])
+                                      : (lav ? 0 : -1));
+                nB = q.by > 0 ? tc[i - 2]
+                              : (tdyn ? L.ctx[((ry - 1) % ring) * R.w + cx][4 + 2 * q.p + q.bx]
+                                      : (tav ? 0 : -1));
+                uint32_t any = 0;
+#pragma unroll
+                for (int k2 = 16; k2 < 24; ++k2) any |= tc[k2];
+                coded = any != 0;
+            }
+            const int nC = nc_of(nA, nB);
+            L.nc[q.k][q.blk] = (int8_t)nC;
+            uint32_t bl = 0;
+            if (coded) {
+                CountSink cs{0};
+                cavlc_block(cs, TB, L.lv[q.k][q.blk], q.luma ? 16 : 15, nC);
+                bl = cs.n;
+            }
+            L.blen[q.k][q.luma ? q.blk : 18 + (q.blk - 16)] = (uint16_t)bl;
+        }
+        if (t < 2 * nd) {
+            const int k = t >> 1, p = t & 1;
+            const int *dc = L.dcraw[k][p];
+            const int f00 = dc[0] + dc[1] + dc[2] + dc[3], f01 = dc[0] - dc[1] + dc[2] - dc[3];
+            const int f10 = dc[0] + dc[1] - dc[2] - dc[3], f11 = dc[0] - dc[1] - dc[2] + dc[3];
+            int16_t *o = L.dclv[k][p];
+            o[0] = (int16_t)quant_dc(f00);
+            o[1] = (int16_t)quant_dc(f01);
+            o[2] = (int16_t)quant_dc(f10);
+            o[3] = (int16_t)quant_dc(f11);
+            CountSink cs{0};
+            cavlc_block(cs, TB, o, 4, -1);
+            L.blen[k][16 + p] = (uint16_t)cs.n;
+        }
+        __syncthreads();
+
+        /* C: MB lengths, piece offsets, window scan */
+        uint32_t mlen = 0;
+        int kd = -1, ref = 0, mv4 = 0, px = 0, py = 0, code = 0, cbp = 0;
+        if (t < nm) {
+            const int m = m0 + t, row = m / mbw, col = m - row * mbw;
+            const bool curA = row < a_end, abvA = (row - 1) < a_end;
+            ref = curA ? rg.ra : rg.rb;
+            mv4 = 4 * (curA ? rg.mva : rg.mvb);
+            const int aref = abvA ? rg.ra : rg.rb, amv4 = 4 * (abvA ? rg.mva : rg.mvb);
+            predict(col, row, mbw, ref, mv4, aref, amv4, px, py);
+            CountSink cs{0};
+            put_mb_head(cs, ref, 0 - px, mv4 - py, nrefs);
+            const bool isdyn = col >= R.x0 && col < R.x0 + R.w && row >= R.y0 && row < R.y0 + R.h;
+            if (!isdyn) {
+                mlen = cs.n + 1u;                  /* + coded_block_pattern ue(0) */
+            } else {
+                kd = dyn_rank(R, mbw, m) - q0;
+                const uint8_t *tc = L.tc[kd];
+                int cbp_l = 0;
+#pragma unroll
+                for (int b8 = 0; b8 < 4; ++b8) {
+                    const int r0 = 8 * (b8 >> 1) + 2 * (b8 & 1);
+                    if (tc[r0] | tc[r0 + 1] | tc[r0 + 4] | tc[r0 + 5]) cbp_l |= 1 << b8;
+                }
+                uint32_t ac = 0;
+#pragma unroll
+                for (int k2 = 16; k2 < 24; ++k2) ac |= tc[k2];
+                const int16_t *dl = &L.dclv[kd][0][0];
+                int anydc = 0;
+#pragma unroll
+                for (int k2 = 0; k2 < 8; ++k2) anydc |= dl[k2];
+                const int cbp_c = ac ? 2 : (anydc ? 1 : 0);
+                cbp = cbp_l | (cbp_c << 4);
+                code = TB.cbp_code[cbp];
+                L.cbp[kd] = (uint8_t)cbp;
+                const uint32_t uel = 2u * (31u - (uint32_t)__clz(code + 1)) + 1u;
+                uint32_t off = cs.n + uel + (cbp ? 1u : 0u);
+                for (int blk = 0; blk < 16; ++blk) {
+                    const int r = blk_raster(blk);
+                    L.boff[kd][r] = (uint16_t)off;
+                    off += L.blen[kd][r];
+                }
+                if (cbp_c) {
+                    for (int p = 0; p < 2; ++p) {
+                        L.boff[kd][16 + p] = (uint16_t)off;
+                        off += L.blen[kd][16 + p];
+                    }
+                }
+                if (cbp_c == 2) {
+                    for (int k2 = 18; k2 < 26; ++k2) {
+                        L.boff[kd][k2] = (uint16_t)off;
+                        off += L.blen[kd][k2];
+                    }
+                }
+                mlen = off;
+            }
+        }
+        uint32_t mo, wtot;
+        block_excl_sum(mlen, L.wsum, mo, wtot);
+        if (kd >= 0) L.mbo[kd] = mo;
+        __syncthreads();
+
+        /* D: bits -> LDS buffer */
+        const uint32_t F = L.F, bw = L.bw;
+        if (t < nm) {
+            LSink sk{{L.buf}, 0, 0, 0};
+            sk.start(F + mo);
+            if (kd < 0) {
+                put_mb(sk, ref, 0 - px, mv4 - py, nrefs);
+            } else {
+                put_mb_head(sk, ref, 0 - px, mv4 - py, nrefs);
+                put_ue(sk, (uint32_t)code);
+                if (cbp) put_se(sk, 0);            /* mb_qp_delta */
+            }
+            sk.finish();
+        }
+        if (t < 24 * nd) {
+            const Task q = task_of(t, nd);
+            const int pc = q.luma ? q.blk : 18 + (q.blk - 16);
+            if (L.blen[q.k][pc]) {
+                LSink sk{{L.buf}, 0, 0, 0};
+                sk.start(F + L.mbo[q.k] + L.boff[q.k][pc]);
+                cavlc_block(sk, TB, L.lv[q.k][q.blk], q.luma ? 16 : 15, (int)L.nc[q.k][q.blk]);
+                sk.finish();
+            }
+        }
+        if (t < 2 * nd) {
+            const int k = t >> 1, p = t & 1;
+            if (L.cbp[k] >> 4) {
+                LSink sk{{L.buf}, 0, 0, 0};
+                sk.start(F + L.mbo[k] + L.boff[k][16 + p]);
+                cavlc_block(sk, TB, L.dclv[k][p], 4, -1);
+                sk.finish();
+            }
+        }
+        __syncthreads();
+
+        /* E: flush whole words to the staging slot, count EP insertions */
+        const uint32_t Tb = F + wtot, nfull = Tb >> 5;
+        if (bw + nfull + 2u > cap_words) {
+            over = true;
+            break;
+        }
+        for (uint32_t base = 0; base < nfull; base += DT) {
+            const uint32_t jw = base + (uint32_t)t;
+            const bool v = jw < nfull;
+            const uint32_t wv = v ? L.buf[jw] : 0u;
+            const uint32_t gb = 4u * (bw + jw);
+            int lnz = -1;
+            if (v) {
+                out[bw + jw] = __builtin_bswap32(wv);
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    if ((wv >> (24 - 8 * i)) & 255u) lnz = (int)(gb + (uint32_t)i);
+            }
+            int ex, tot;
+            block_excl_max(lnz, L.wmax, ex, tot);
+            if (v) {
+                int prev = max(carry, ex);
+                my_ep += ep_word(wv, gb, 0xffffffffu, prev);
+            }
+            carry = max(carry, tot);
+        }
+        const uint32_t part = L.buf[nfull];
+        __syncthreads();
+        for (uint32_t jw = (uint32_t)t; jw <= nfull; jw += DT) L.buf[jw] = jw == 0 ? part : 0u;
+        if (nd > 0 && t < 8) {
+            const uint8_t *tc = L.tc[nd - 1];
+            L.lcarry[t] = t < 4 ? tc[4 * t + 3] : tc[16 + 4 * ((t - 4) >> 1) + 2 * ((t - 4) & 1) + 1];
+        }
+        if (t == 0) {
+            L.F = Tb & 31u;
+            L.bw = bw + nfull;
+        }
+        __syncthreads();
+        m0 = m1;
+    }
+
+    if (!over) {
+        /* rbsp_stop_one_bit + alignment (bitwriter.c:103-111); F < 32 */
+        if (t == 0) {
+            const uint32_t F = L.F, bw = L.bw;
+            const uint32_t wv = L.buf[0] | (1u << (31 - F));
+            const uint32_t nb = (F + 1u + 7u) >> 3;
+            out[bw] = __builtin_bswap32(wv);
+            int prev = carry;
+            my_ep += ep_word(wv, 4u * bw, 4u * bw + nb, prev);
+            DF->rbsp_bytes = 4u * bw + nb;
+        }
+    }
+    uint32_t ex, tot;
+    block_excl_sum(my_ep, L.wsum, ex, tot);
+    if (t == 0) {
+        DF->ep = tot;
+        DF->err = over ? DF_OVER : 0u;
+        if (over) atomicOr((unsigned int *)&S->err, SCROLL_DEVERR_DYN);
+    }
+}
+
+/* ---------------------------------------------------------------------- */
+/* k_dyn_emit: staged RBSP -> arena with start code, header, EP bytes       */
+/* ---------------------------------------------------------------------- */
+__device__ inline void store16(uint8_t *A, uint64_t p, const uint8_t *src, uint64_t lo, uint64_t hi)
+{
+    if (p >= lo && p + 16 <= hi) {
+        *reinterpret_cast<uint4 *>(A + p) = *reinterpret_cast<const uint4 *>(src);
+        return;
+    }
+    for (int i = 0; i < 16; ++i)
+        if (p + i >= lo && p + i < hi) A[p + i] = src[i];
+}
+
+__global__ __launch_bounds__(DT) void k_dyn_emit(const DevStream *__restrict__ st,
+                                                 const NalDesc *__restrict__ nal, int ld_nal,
+                                                 const DynFrame *__restrict__ dfr, int ld_fr,
+                                                 DynGeom g, const uint8_t *__restrict__ stage,
+                                                 uint8_t *__restrict__ arena, uint64_t ld_arena)
+{
+    __shared__ alignas(16) uint8_t ob[OBUF];
+    __shared__ int32_t wmax[NW];
+    __shared__ uint32_t wsum[NW];
+    const int f = blockIdx.x, s = blockIdx.y, t = threadIdx.x;
+    const DynFrame df = dfr[(size_t)s * ld_fr + f];
+    const int j = df.nal;
+    if (j < 0 || j >= st[s].nnal || df.err) return;          /* nnal = 0: nothing committed */
+    const NalDesc d = nal[(size_t)s * ld_nal + j];
+    if (d.slow != 2) return;
+    uint8_t *A = arena + (size_t)s * ld_arena;
+    const uint64_t o0 = d.out_off, o1 = o0 + d.size;
+    const uint8_t *in = stage + ((size_t)s * ld_fr + f) * g.slot_bytes;
+    const uint32_t nin = df.rbsp_bytes;
+
+    uint64_t lb = o0 & ~127ull;                  /* arena byte of ob[0] (line aligned) */
+    uint32_t fill = (uint32_t)(o0 - lb);
+    if (t < 5) ob[fill + t] = t < 3 ? 0 : (t == 3 ? 1 : nal_header_byte(0));   /* nal.c:59-64 */
+    fill += 5;
+    int carry = -1;
+    for (uint32_t i0 = 0; i0 < nin; i0 += DT * 16) {
+        const uint32_t ib = i0 + 16u * (uint32_t)t;
+        const uint32_t n = ib < nin ? min(16u, nin - ib) : 0u;
+        uint8_t b[16];
+        {
+            const uint4 v = n ? *reinterpret_cast<const uint4 *>(in + ib) : make_uint4(0, 0, 0, 0);
+            const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int i = 0; i < 16; ++i) b[i] = (uint8_t)(wv[i >> 2] >> (8 * (i & 3)));
+        }
+        int lnz = -1;
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+            if ((uint32_t)i < n && b[i]) lnz = (int)(ib + i);
+        int ex, tot;
+        block_excl_max(lnz, wmax, ex, tot);
+        int prev = max(carry, ex);
+        uint32_t ins = 0, cnt = 0;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            if ((uint32_t)i >= n) break;
+            if (ep_insert(b[i], (int)(ib + i) - 1 - prev)) {
+                ins |= 1u << i;
+                cnt++;
+            }
+            if (b[i]) prev = (int)(ib + i);
+        }
+        uint32_t opos, otot;
+        block_excl_sum(n + cnt, wsum, opos, otot);
+        uint32_t p = fill + opos;
+        for (int i = 0; i < 16; ++i) {
+            if ((uint32_t)i >= n) break;
+            if ((ins >> i) & 1u) ob[p++] = 3;
+            ob[p++] = b[i];
+        }
+        __syncthreads();
+        const uint32_t nf = fill + otot, nlines = nf >> 7;
+        for (uint32_t c = (uint32_t)t; c < nlines * 8; c += DT)
+            store16(A, lb + 16u * c, ob + 16u * c, o0, o1);
+        const uint32_t rem = nf - (nlines << 7);
+        const uint8_t keep = (uint32_t)t < rem ? ob[(nlines << 7) + t] : 0;
+        __syncthreads();
+        if ((uint32_t)t < rem) ob[t] = keep;
+        lb += (uint64_t)nlines << 7;
+        fill = rem;
+        carry = max(carry, tot);
+        __syncthreads();
+    }
+    for (uint32_t c = (uint32_t)t; 16u * c < fill; c += DT) store16(A, lb + 16u * c, ob + 16u * c, o0, o1);
+}
+
+/* ---------------------------------------------------------------------- */
+/* k_dyn_synth: the synthetic dynamic-rect source of SURVEY §8d            */
+/* (dyn_oracle.h), one thread per pixel                                    */
+/* ---------------------------------------------------------------------- */
+__device__ inline uint32_t mix32(uint32_t x)
+{
+    x ^= x >> 16;
+    x *= 0x7feb352du;
+    x ^= x >> 15;
+    x *= 0x846ca68bu;
+    x ^= x >> 16;
+    return x;
+}
+
+__global__ __launch_bounds__(256) void k_dyn_synth(uint8_t *__restrict__ src, DynGeom g,
+                                                   int stream_base, int t0)
+{
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    const int f = blockIdx.y, s = blockIdx.z;
+    const uint32_t npx = 384u * (uint32_t)g.w * (uint32_t)g.h;
+    if (i >= npx) return;
+    const uint32_t tt = (uint32_t)(t0 + f);
+    const uint32_t seed = (0x9E3779B9u * (uint32_t)(stream_base + s)) ^ (0x85EBCA6Bu * tt);
+    const uint32_t hv = mix32(seed + i * 0x9E3779B9u);
+    const uint32_t ly = 256u * (uint32_t)g.w * (uint32_t)g.h;
+    int v;
+    if (i < ly) {
+        const int lw = 16 * g.w;
+        const int y = (int)(i / (uint32_t)lw), x = (int)(i - (uint32_t)(y * lw));
+        const int X = 16 * g.x0 + x, Y = 16 * g.y0 + y;
+        v = 128 + ((X + 2 * Y + 3 * (int)tt) & 63) - 32 + (int)(hv >> 28) - 8;
+    } else {
+        const uint32_t r = (i - ly) % (64u * (uint32_t)g.w * (uint32_t)g.h);
+        const int cw = 8 * g.w;
+        const int y = (int)(r / (uint32_t)cw), x = (int)(r - (uint32_t)(y * cw));
+        const int X = 8 * g.x0 + x, Y = 8 * g.y0 + y;
+        v = 128 + ((X + Y + (int)tt) & 15) - 8 + (int)(hv >> 30);
+    }
+    src[(size_t)s * g.src_ld + (size_t)f * g.src_fr + i] = (uint8_t)clampi(v, 0, 255);
+}
+
+}  // namespace
+
+/* ---------------------------------------------------------------------- */
+/* launchers (engine-internal, engine.h)                                   */
+/* ---------------------------------------------------------------------- */
+int dyn_launch_stage(hipStream_t hs, int nframes, int S, DevStream *st, const NalDesc *nal,
+                     int ld_nal, const PlanPending *pend, DynFrame *dfr, int ld_fr,
+                     const DynGeom *g, const uint8_t *src, const uint8_t *refs, uint8_t *stage)
+{
+    if (nframes <= 0 || S <= 0) return 0;
+    hipLaunchKernelGGL(k_dyn_stage<false>, dim3(nframes, S), dim3(DT), 0, hs, st, nal, ld_nal, pend,
+                       dfr, ld_fr, *g, src, refs, stage);
+    if (hipGetLastError() != hipSuccess) return -1;
+    hipLaunchKernelGGL(k_dyn_stage<true>, dim3(nframes, S), dim3(DT), 0, hs, st, nal, ld_nal, pend,
+                       dfr, ld_fr, *g, src, refs, stage);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int dyn_launch_emit(hipStream_t hs, int nframes, int S, const DevStream *st, const NalDesc *nal,
+                    int ld_nal, const DynFrame *dfr, int ld_fr, const DynGeom *g,
+                    const uint8_t *stage, uint8_t *arena, uint64_t ld_arena)
+{
+    if (nframes <= 0 || S <= 0) return 0;
+    hipLaunchKernelGGL(k_dyn_emit, dim3(nframes, S), dim3(DT), 0, hs, st, nal, ld_nal, dfr, ld_fr,
+                       *g, stage, arena, ld_arena);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int dyn_launch_synth(hipStream_t hs, int nframes, int S, uint8_t *src, const DynGeom *g,
+                     int stream_base, int t0)
+{
+    if (nframes <= 0 || S <= 0) return 0;
+    const uint32_t npx = 384u * (uint32_t)g->w * (uint32_t)g->h;
+    hipLaunchKernelGGL(k_dyn_synth, dim3((npx + 255) / 256, nframes, S), dim3(256), 0, hs, src, *g,
+                       stream_base, t0);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+size_t dyn_slot_bound(int mbw, int mbh, int rw, int rh)
+{
+    /* header + every MB head (+ cbp) + every dynamic MB at its provable
+     * maximum + the stop word + k_dyn_stage's 16-byte margin */
+    const size_t bits = (size_t)HDR_MAX + (size_t)mbw * mbh * (HEAD_MAX + 1) +
+                        (size_t)rw * rh * MB_BITS_MAX + 64;
+    return ((bits / 8 + 32) + 255) & ~(size_t)255;
+}

@@ -47,7 +47,7 @@ typedef struct {
     int32_t frame_num;            /* raw cfg->frame_num when written            */
     uint8_t kind;                 /* 0 scroll P, 1 waypoint P                   */
     uint8_t nwp;                  /* cfg->num_waypoints snapshot                */
-    uint8_t slow;                 /* 1: generated by the serial device path     */
+    uint8_t slow;                 /* 1: serial device path, 2: dynamic rect     */
     uint8_t pad0;
     uint32_t frame;               /* composed-frame index within the batch      */
     uint32_t pad1;
@@ -55,6 +55,38 @@ typedef struct {
 
 #define SCROLL_DEVERR_OVERFLOW 1u   /* arena too small (reference: assert)        */
 #define SCROLL_DEVERR_CONFIG   2u   /* unsupported config (e.g. log2 fields)      */
+#define SCROLL_DEVERR_DYN      4u   /* a dynamic NAL outgrew its staging slot     */
+
+/* k_plan state pass -> size pass: the stream's planned totals and the final
+ * waypoint table (committed only by the size pass).  128 bytes. */
+typedef struct {
+    int32_t nnal, nwp_end, fn_end, nalwp;
+    int32_t wo[8], wl[8], wv[8];
+    int32_t pad[4];
+} PlanPending;
+
+/* per composed frame with the dynamic rect: its scroll NAL (-1: none, the
+ * experiment mode replaced it), staged RBSP bytes, emulation-prevention
+ * bytes to insert, staging overflow.  16 bytes. */
+typedef struct {
+    int32_t nal;
+    uint32_t rbsp_bytes;
+    uint32_t ep;
+    uint32_t err;
+} DynFrame;
+
+/* dynamic rect geometry and buffer strides (one per batch) */
+#define DYN_MAX_W 128               /* rect width limit (MBs)                     */
+#define DYN_CTX_MB 400              /* TotalCoeff row-ring entries (LDS)          */
+#define DYN_WINDOW_MBS 10           /* dynamic MBs per k_dyn_stage window         */
+typedef struct {
+    int32_t x0, y0, w, h;           /* rect, MB units                             */
+    int32_t ring;                   /* rows in the TotalCoeff ring                */
+    int32_t pad;
+    uint64_t src_ld, src_fr;        /* source bytes per stream / per frame        */
+    uint64_t ref_ld;                /* reference-pair bytes per stream (0 shared) */
+    uint64_t slot_bytes;            /* staging bytes per frame                    */
+} DynGeom;
 
 enum { SCROLL_PLAN_COMPOSER = 0, SCROLL_PLAN_EXPERIMENT = 1, SCROLL_PLAN_EXPLICIT = 2 };
 

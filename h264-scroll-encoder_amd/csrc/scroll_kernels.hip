@@ -16,9 +16,11 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <mutex>
 #include <vector>
 
+#include "dyn_engine.h"
 #include "engine.h"
 #include "scroll_device.h"
 
@@ -42,6 +44,9 @@ constexpr int EMIT_WAVES = SCROLL_EMIT_WAVES;  /* waves per k_emit workgroup    
 #endif
 constexpr int PLAN_THREADS = SCROLL_PLAN_THREADS;
 constexpr int PLAN_REWIND = 1 << 8;   /* k_plan flag: arena restarts at 0 */
+constexpr int PLAN_STATE = 1 << 9;    /* phase 1 only -> PlanPending (dynamic rect)   */
+constexpr int PLAN_SIZE = 1 << 10;    /* phase 2 only, from PlanPending              */
+constexpr int PLAN_DYN = 1 << 11;     /* scroll NALs carry the dynamic rect          */
 
 /* ---------------------------------------------------------------------- */
 /* helpers                                                                 */
@@ -97,12 +102,17 @@ __device__ inline NalCtx make_ctx(const int32_t *cfg, const int32_t *wo, const i
 /*  phase 2 (all waves): exact size of every NAL (run layout, or the serial */
 /*          path when emulation prevention / long codes are possible), and  */
 /*          a block scan -> byte offset of every NAL in the stream arena.   */
+/* With the dynamic rect the kernel runs twice around k_dyn_stage: a state  */
+/* pass (PLAN_STATE: phase 1, totals + final table to PlanPending, frame -> */
+/* scroll NAL map to DynFrame) and a size pass (PLAN_SIZE: phase 2, sizes   */
+/* of dynamic NALs from DynFrame).                                          */
 /* ---------------------------------------------------------------------- */
 __global__ __launch_bounds__(PLAN_THREADS) void k_plan(DevStream *__restrict__ st,
                                                        const int32_t *__restrict__ offs,
                                                        int ld_off, NalDesc *__restrict__ nal,
                                                        int ld_nal, int nframes, int mode,
-                                                       int flags)
+                                                       int flags, PlanPending *__restrict__ pend,
+                                                       DynFrame *__restrict__ dfr, int ld_fr)
 {
     const int s = blockIdx.x;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -124,14 +134,26 @@ __global__ __launch_bounds__(PLAN_THREADS) void k_plan(DevStream *__restrict__ s
         s_cfg[4] = S->log2_poc; s_cfg[5] = S->deblock; s_cfg[6] = S->frame_num; s_cfg[7] = S->nwp;
         s_carry = 0;
         s_nslow = 0;
-        if (flags & PLAN_REWIND) S->out_pos = 0;
+        if ((flags & PLAN_REWIND) && !(flags & PLAN_STATE)) S->out_pos = 0;
     }
     const int F = nframes >= 0 ? nframes : S->frames;
     NalDesc *N = nal + (size_t)s * ld_nal;
     __syncthreads();
     const uint64_t out0 = S->out_pos;
 
-    if (mode == SCROLL_PLAN_EXPLICIT) {
+    if (flags & PLAN_SIZE) {
+        if (tid < 8) {
+            s_wo[tid] = pend[s].wo[tid];
+            s_wl[tid] = pend[s].wl[tid];
+            s_wv[tid] = pend[s].wv[tid];
+        }
+        if (tid == 0) {
+            s_nnal = pend[s].nnal;
+            s_nwp_end = pend[s].nwp_end;
+            s_fn_end = pend[s].fn_end;
+            s_nalwp = pend[s].nalwp;
+        }
+    } else if (mode == SCROLL_PLAN_EXPLICIT) {
         if (tid == 0) {
             s_nnal = S->nnal;
             s_nwp_end = s_cfg[7];
@@ -199,6 +221,7 @@ __global__ __launch_bounds__(PLAN_THREADS) void k_plan(DevStream *__restrict__ s
                     d.kind = 0; d.off = off; d.frame_num = fn0 + first + has_wp;
                     d.nwp = (uint8_t)my_n; d.frame = (uint32_t)i;
                     N[first + has_wp] = d;
+                    if (flags & PLAN_DYN) dfr[(size_t)s * ld_fr + i].nal = first + has_wp;
                 }
                 nalc += __popcll(vmask) + __popcll(wmask);
             } else {   /* experiment: waypoint NAL replaces the scroll NAL */
@@ -208,6 +231,7 @@ __global__ __launch_bounds__(PLAN_THREADS) void k_plan(DevStream *__restrict__ s
                     d.kind = has_wp ? 1 : 0; d.off = off; d.frame_num = fn0 + idx;
                     d.nwp = (uint8_t)(has_wp ? wp_nb : my_n); d.frame = (uint32_t)i;
                     N[idx] = d;
+                    if (flags & PLAN_DYN) dfr[(size_t)s * ld_fr + i].nal = has_wp ? -1 : idx;
                 }
                 nalc += __popcll(vmask);
             }
@@ -230,6 +254,20 @@ __global__ __launch_bounds__(PLAN_THREADS) void k_plan(DevStream *__restrict__ s
         }
     }
     __syncthreads();
+    if (flags & PLAN_STATE) {
+        if (tid < 8) {
+            pend[s].wo[tid] = s_wo[tid];
+            pend[s].wl[tid] = s_wl[tid];
+            pend[s].wv[tid] = s_wv[tid];
+        }
+        if (tid == 0) {
+            pend[s].nnal = s_nnal;
+            pend[s].nwp_end = s_nwp_end;
+            pend[s].fn_end = s_fn_end;
+            pend[s].nalwp = s_nalwp;
+        }
+        return;
+    }
 
     /* phase 2: sizes + offsets.  Every NAL reads the FINAL table: entries are
      * only appended, and a NAL only looks at its first nwp entries. */
@@ -242,8 +280,13 @@ __global__ __launch_bounds__(PLAN_THREADS) void k_plan(DevStream *__restrict__ s
             NalDesc d = N[j];
             NalCtx c = make_ctx(s_cfg, s_wo, s_wl, s_wv, d);
             uint32_t fsz = 0;
-            bool fast = !(flags & SCROLL_DEBUG_FORCE_SERIAL) && build_nal<false>(c, nullptr, &fsz);
-            if (fast) {
+            const bool dyn = (flags & PLAN_DYN) && d.kind == 0;
+            bool fast = !dyn && !(flags & SCROLL_DEBUG_FORCE_SERIAL) && build_nal<false>(c, nullptr, &fsz);
+            if (dyn) {
+                const DynFrame df = dfr[(size_t)s * ld_fr + d.frame];
+                sz = 5u + (uint64_t)df.rbsp_bytes + df.ep;     /* start code + header + EBSP */
+                slow = 2;
+            } else if (fast) {
                 sz = fsz;
             } else {
                 sz = serial_size(c);
@@ -252,7 +295,7 @@ __global__ __launch_bounds__(PLAN_THREADS) void k_plan(DevStream *__restrict__ s
         }
         uint64_t inc = wave_incl_scan(sz, lane);
         if (lane == 63) s_wsum[wave] = inc;
-        int ns = __popcll(__ballot(slow != 0));
+        int ns = __popcll(__ballot(slow == 1));
         if (lane == 0 && ns) atomicAdd(&s_nslow, ns);
         __syncthreads();
         uint64_t before = s_carry;
@@ -274,8 +317,9 @@ __global__ __launch_bounds__(PLAN_THREADS) void k_plan(DevStream *__restrict__ s
     if (tid == 0) {
         uint64_t total = s_carry;
         S->n_slow = s_nslow;
-        if (out0 + total > S->out_cap) {
-            S->err |= SCROLL_DEVERR_OVERFLOW;   /* nothing committed, nothing emitted */
+        if (out0 + total > S->out_cap || (S->err & SCROLL_DEVERR_DYN)) {
+            if (!(S->err & SCROLL_DEVERR_DYN))
+                S->err |= SCROLL_DEVERR_OVERFLOW;   /* nothing committed, nothing emitted */
             S->nnal = 0;
             S->batch_bytes = 0;
         } else {
@@ -288,7 +332,8 @@ __global__ __launch_bounds__(PLAN_THREADS) void k_plan(DevStream *__restrict__ s
             if (mode != SCROLL_PLAN_EXPLICIT) S->frames_written += F;
         }
     }
-    if (tid < 8 && mode != SCROLL_PLAN_EXPLICIT && out0 + s_carry <= S->out_cap) {
+    if (tid < 8 && mode != SCROLL_PLAN_EXPLICIT && out0 + s_carry <= S->out_cap &&
+        !(S->err & SCROLL_DEVERR_DYN)) {
         S->wp_off[tid] = s_wo[tid];
         S->wp_lt[tid] = s_wl[tid];
         S->wp_valid[tid] = s_wv[tid];
@@ -320,7 +365,8 @@ __global__ __launch_bounds__(PLAN_THREADS) void k_plan(DevStream *__restrict__ s
 /* bytes of that line.  A stream's first tile in a launch merges the line   */
 /* head from memory (the previous compose's bytes); its last tile zero-     */
 /* fills its line tail (arena slack).  Tiles holding a serial-path NAL use  */
-/* the generic byte path and the owning lane writes that NAL serially.      */
+/* the generic byte path and the owning lane writes that NAL serially;     */
+/* dynamic-rect NALs (slow = 2) are written by k_dyn_emit.                  */
 /* ---------------------------------------------------------------------- */
 constexpr int PURE_U = 4;         /* 64-chunk groups per stream iteration      */
 constexpr int XB = SEAM_XB, XA = SEAM_XA;   /* neighbour layouts before / after the tile */
@@ -705,19 +751,17 @@ __global__ __launch_bounds__(EMIT_WAVES * 64) void k_emit(const DevStream *__res
             }
         }
     } else {
+        /* generic byte path: the bytes of every own run-layout NAL, one
+         * byte per lane; serial-path and dynamic-rect NALs are written by
+         * their own writers (below / k_dyn_emit) */
         const Lay *Lo = L + XB;
         const int32_t *no = noff + XB;
-        int j = 0;
-        const uint64_t c0 = B0 >> 4, c1 = (B1 + 15) >> 4;
-        for (uint64_t c = c0 + lane; c < c1; c += 64) {
-            const uint64_t p = c << 4;
-            for (int k = 0; k < 16; ++k) {
-                uint64_t q = p + (uint64_t)k;
-                if (q < B0 || q >= B1) continue;
-                uint32_t rel = (uint32_t)(q - B0);
-                while (j + 1 < cnt && (uint32_t)no[j + 1] <= rel) j++;
-                if ((slow_mask >> (XB + j)) & 1ull) continue;
-                A[q] = (uint8_t)tile_byte(Lo, no, cnt, j, rel);
+        for (int jn = 0; jn < cnt; ++jn) {
+            if ((slow_mask >> (XB + jn)) & 1ull) continue;
+            const uint32_t r0 = (uint32_t)no[jn], r1 = (uint32_t)no[jn + 1];
+            for (uint32_t rel = r0 + (uint32_t)lane; rel < r1; rel += 64) {
+                int jj = jn;
+                A[B0 + rel] = (uint8_t)tile_byte(Lo, no, cnt, jj, rel);
             }
         }
     }
@@ -728,7 +772,7 @@ __global__ __launch_bounds__(EMIT_WAVES * 64) void k_emit(const DevStream *__res
         stamp[7] = (__builtin_amdgcn_s_memrealtime() & 0xffffffffull) | (hw << 32);
         stamp[6] = (stamp[6] & 0x00ffffffffffffffull) | ((xcc & 0xff) << 56);
     }
-    if (own && my_slow) serial_write(my_ctx, A + d.out_off);
+    if (own && d.slow == 1) serial_write(my_ctx, A + d.out_off);
 }
 
 /* ---------------------------------------------------------------------- */
@@ -819,6 +863,7 @@ void dev_to_cfg(const DevStream *d, ComposerConfig *c)
 /* ======================================================================== */
 /* ScrollBatch                                                              */
 /* ======================================================================== */
+constexpr int NEV = 6;
 struct ScrollBatch {
     int device = 0;
     int mode = SCROLL_MODE_COMPOSER;
@@ -833,13 +878,13 @@ struct ScrollBatch {
     uint8_t *d_arena = nullptr;
     hipStream_t own = nullptr;
     hipStream_t last = nullptr;
-    hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
+    hipEvent_t ev[NEV] = {};
     int timing = 0;
     int timed_pending = 0;
-    float ms[2] = {0, 0};
-    std::vector<hipEvent_t> ring;      /* 3 events per timed compose, pending */
+    float ms[4] = {0, 0, 0, 0};        /* plan, emit, dyn stage, dyn emit */
+    std::vector<hipEvent_t> ring;      /* NEV events per timed compose, pending */
     int ring_used = 0;
-    double acc_ms[2] = {0, 0};
+    double acc_ms[4] = {0, 0, 0, 0};
     int acc_n = 0;
     int host_valid = 1;
     int last_plan_mode = SCROLL_PLAN_COMPOSER;
@@ -848,7 +893,28 @@ struct ScrollBatch {
     int nal_cache_valid = 0;
     uint64_t *d_dbg = nullptr;
     size_t dbg_slots = 0;
+    /* dynamic rect (configs 3-5) */
+    PlanPending *d_pend = nullptr;
+    int dyn_on = 0;
+    int dyn_pw = 0, dyn_ph = 0;        /* picture size every stream must have      */
+    int dyn_refs = 0;                  /* 0 unset, 1 shared pair, 2 per stream     */
+    DynGeom geo{};
+    DynFrame *d_dfr = nullptr;
+    uint8_t *d_src = nullptr, *d_refs = nullptr, *d_stage = nullptr;
 };
+
+/* event pairs of one compose: plan = [0,1) + [2,3), dyn stage [1,2),
+ * emit [3,4), dyn emit [4,5) */
+static void event_ms(const hipEvent_t *e, float out[4])
+{
+    float x[NEV - 1] = {};
+    for (int i = 0; i + 1 < NEV; ++i)
+        if (hipEventElapsedTime(&x[i], e[i], e[i + 1]) != hipSuccess) x[i] = 0.0f;
+    out[0] = x[0] + x[2];
+    out[1] = x[3];
+    out[2] = x[1];
+    out[3] = x[4];
+}
 
 extern "C" {
 
@@ -899,8 +965,9 @@ int scroll_batch_create(ScrollBatch **out, const ScrollBatchDesc *desc)
     if (e == hipSuccess) e = hipMalloc(&b->d_off, S * (size_t)desc->max_frames * sizeof(int32_t));
     if (e == hipSuccess) e = hipMalloc(&b->d_nal, S * (size_t)b->ld_nal * sizeof(NalDesc));
     if (e == hipSuccess) e = hipMalloc(&b->d_arena, S * b->ld_arena);
+    if (e == hipSuccess) e = hipMalloc(&b->d_pend, S * sizeof(PlanPending));
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&b->own, hipStreamNonBlocking);
-    for (int i = 0; i < 3 && e == hipSuccess; ++i) e = hipEventCreate(&b->ev[i]);
+    for (int i = 0; i < NEV && e == hipSuccess; ++i) e = hipEventCreate(&b->ev[i]);
     if (e == hipSuccess) e = hipMemset(b->d_st, 0, S * sizeof(DevStream));
     if (e == hipSuccess) e = hipMemset(b->d_off, 0, S * (size_t)desc->max_frames * sizeof(int32_t));
     if (e != hipSuccess) {
@@ -919,7 +986,7 @@ void scroll_batch_destroy(ScrollBatch *b)
     if (!b) return;
     (void)hipSetDevice(b->device);
     if (b->own) (void)hipStreamSynchronize(b->own);
-    for (int i = 0; i < 3; ++i)
+    for (int i = 0; i < NEV; ++i)
         if (b->ev[i]) (void)hipEventDestroy(b->ev[i]);
     for (hipEvent_t e : b->ring) (void)hipEventDestroy(e);
     if (b->own) (void)hipStreamDestroy(b->own);
@@ -928,6 +995,11 @@ void scroll_batch_destroy(ScrollBatch *b)
     (void)hipFree(b->d_off);
     (void)hipFree(b->d_nal);
     (void)hipFree(b->d_arena);
+    (void)hipFree(b->d_pend);
+    (void)hipFree(b->d_dfr);
+    (void)hipFree(b->d_src);
+    (void)hipFree(b->d_refs);
+    (void)hipFree(b->d_stage);
     if (b->d_dbg) (void)hipFree(b->d_dbg);
     delete b;
 }
@@ -961,6 +1033,11 @@ int scroll_batch_add_stream(ScrollBatch *b, const ComposerConfig *cfg)
     }
     int rc = check_cfg(cfg);
     if (rc) return rc;
+    if (b->dyn_on && (cfg->width != b->dyn_pw || cfg->height != b->dyn_ph)) {
+        set_err("scroll_batch_add_stream: the dynamic rect needs %dx%d streams", b->dyn_pw,
+                b->dyn_ph);
+        return SCROLL_ERR_CONFIG;
+    }
     rc = batch_host_sync(b);
     if (rc) return rc;
     int s = b->nstreams;
@@ -1017,22 +1094,25 @@ int scroll_batch_set_offsets(ScrollBatch *b, const int32_t *offsets, int nframes
 
 int32_t *scroll_batch_offsets_device(ScrollBatch *b) { return b ? b->d_off : nullptr; }
 
+static void fold_ring(ScrollBatch *b)
+{
+    for (int i = 0; i + NEV <= b->ring_used; i += NEV) {
+        float m[4];
+        event_ms(&b->ring[i], m);
+        for (int k = 0; k < 4; ++k) b->acc_ms[k] += m[k];
+        b->acc_n++;
+    }
+    b->ring_used = 0;
+}
+
 static int ring_events(ScrollBatch *b, hipEvent_t **evs)
 {
-    if ((size_t)b->ring_used + 3 > b->ring.size()) {
-        if (b->ring.size() >= 3 * 256) {        /* bound: fold pending timings first */
+    if ((size_t)b->ring_used + NEV > b->ring.size()) {
+        if (b->ring.size() >= (size_t)NEV * 256) {   /* bound: fold pending timings first */
             HIPCHK(hipStreamSynchronize(b->last));
-            for (int i = 0; i < b->ring_used; i += 3) {
-                float a = 0, c = 0;
-                HIPCHK(hipEventElapsedTime(&a, b->ring[i], b->ring[i + 1]));
-                HIPCHK(hipEventElapsedTime(&c, b->ring[i + 1], b->ring[i + 2]));
-                b->acc_ms[0] += a;
-                b->acc_ms[1] += c;
-                b->acc_n++;
-            }
-            b->ring_used = 0;
+            fold_ring(b);
         } else {
-            for (int i = 0; i < 3; ++i) {
+            for (int i = 0; i < NEV; ++i) {
                 hipEvent_t e;
                 HIPCHK(hipEventCreate(&e));
                 b->ring.push_back(e);
@@ -1040,7 +1120,7 @@ static int ring_events(ScrollBatch *b, hipEvent_t **evs)
         }
     }
     *evs = &b->ring[b->ring_used];
-    b->ring_used += 3;
+    b->ring_used += NEV;
     return SCROLL_OK;
 }
 
@@ -1053,16 +1133,42 @@ static int launch(ScrollBatch *b, int nframes, int plan_mode, int nal_max, hipSt
     if (b->timing) {
         int rc = ring_events(b, &rev);
         if (rc) return rc;
-        HIPCHK(hipEventRecord(b->ev[0], hs));
-        HIPCHK(hipEventRecord(rev[0], hs));
     }
-    hipLaunchKernelGGL(k_plan, dim3(S), dim3(PLAN_THREADS), 0, hs, b->d_st, b->d_off,
-                       b->max_frames, b->d_nal, b->ld_nal, nframes, plan_mode,
-                       b->debug | plan_flags);
-    HIPCHK(hipGetLastError());
-    if (b->timing) {
-        HIPCHK(hipEventRecord(b->ev[1], hs));
-        HIPCHK(hipEventRecord(rev[1], hs));
+    auto mark = [&](int k) -> int {
+        if (!b->timing) return SCROLL_OK;
+        HIPCHK(hipEventRecord(b->ev[k], hs));
+        HIPCHK(hipEventRecord(rev[k], hs));
+        return SCROLL_OK;
+    };
+    const bool dyn = b->dyn_on && plan_mode != SCROLL_PLAN_EXPLICIT;
+    const int ld_fr = b->max_frames;
+    int rc = mark(0);
+    if (rc) return rc;
+    if (!dyn) {
+        hipLaunchKernelGGL(k_plan, dim3(S), dim3(PLAN_THREADS), 0, hs, b->d_st, b->d_off,
+                           b->max_frames, b->d_nal, b->ld_nal, nframes, plan_mode,
+                           b->debug | plan_flags, b->d_pend, b->d_dfr, ld_fr);
+        HIPCHK(hipGetLastError());
+        if ((rc = mark(1)) || (rc = mark(2)) || (rc = mark(3))) return rc;
+    } else {
+        hipLaunchKernelGGL(k_plan, dim3(S), dim3(PLAN_THREADS), 0, hs, b->d_st, b->d_off,
+                           b->max_frames, b->d_nal, b->ld_nal, nframes, plan_mode,
+                           b->debug | plan_flags | PLAN_STATE | PLAN_DYN, b->d_pend, b->d_dfr,
+                           ld_fr);
+        HIPCHK(hipGetLastError());
+        if ((rc = mark(1))) return rc;
+        if (dyn_launch_stage(hs, nframes, S, b->d_st, b->d_nal, b->ld_nal, b->d_pend, b->d_dfr,
+                             ld_fr, &b->geo, b->d_src, b->d_refs, b->d_stage)) {
+            set_err("k_dyn_stage launch: %s", hipGetErrorString(hipGetLastError()));
+            return SCROLL_ERR_HIP;
+        }
+        if ((rc = mark(2))) return rc;
+        hipLaunchKernelGGL(k_plan, dim3(S), dim3(PLAN_THREADS), 0, hs, b->d_st, b->d_off,
+                           b->max_frames, b->d_nal, b->ld_nal, nframes, plan_mode,
+                           b->debug | plan_flags | PLAN_SIZE | PLAN_DYN, b->d_pend, b->d_dfr,
+                           ld_fr);
+        HIPCHK(hipGetLastError());
+        if ((rc = mark(3))) return rc;
     }
     int per_wg = EMIT_WAVES * TILE;
     int gx = (nal_max + per_wg - 1) / per_wg;
@@ -1080,11 +1186,14 @@ static int launch(ScrollBatch *b, int nframes, int plan_mode, int nal_max, hipSt
                            b->ld_nal, b->d_arena, (uint64_t)b->ld_arena, b->debug, b->d_dbg);
         HIPCHK(hipGetLastError());
     }
-    if (b->timing) {
-        HIPCHK(hipEventRecord(b->ev[2], hs));
-        HIPCHK(hipEventRecord(rev[2], hs));
-        b->timed_pending = 1;
+    if ((rc = mark(4))) return rc;
+    if (dyn && dyn_launch_emit(hs, nframes, S, b->d_st, b->d_nal, b->ld_nal, b->d_dfr, ld_fr,
+                               &b->geo, b->d_stage, b->d_arena, (uint64_t)b->ld_arena)) {
+        set_err("k_dyn_emit launch: %s", hipGetErrorString(hipGetLastError()));
+        return SCROLL_ERR_HIP;
     }
+    if ((rc = mark(5))) return rc;
+    if (b->timing) b->timed_pending = 1;
     b->host_valid = 0;
     b->nal_cache_valid = 0;
     b->last = hs;
@@ -1101,6 +1210,10 @@ int scroll_batch_compose_ex(ScrollBatch *b, int nframes, void *hip_stream, int f
     if (!b || nframes < 0 || nframes > b->max_frames) {
         set_err("scroll_batch_compose: nframes %d out of range", nframes);
         return SCROLL_ERR_ARG;
+    }
+    if (b->dyn_on && !b->dyn_refs) {
+        set_err("scroll_batch_compose: dynamic rect without reference pictures");
+        return SCROLL_ERR_CONFIG;
     }
     HIPCHK(hipSetDevice(b->device));
     hipStream_t hs = hip_stream ? (hipStream_t)hip_stream : b->own;
@@ -1120,14 +1233,16 @@ int scroll_batch_sync(ScrollBatch *b)
         if (rc0) return rc0;
     }
     if (b->timed_pending) {
-        HIPCHK(hipEventElapsedTime(&b->ms[0], b->ev[0], b->ev[1]));
-        HIPCHK(hipEventElapsedTime(&b->ms[1], b->ev[1], b->ev[2]));
+        event_ms(b->ev, b->ms);
         b->timed_pending = 0;
     }
     int rc = SCROLL_OK;
     for (int s = 0; s < b->nstreams; ++s) {
         if (!b->h_st[s].err) continue;
-        if (rc == SCROLL_OK)
+        if (rc == SCROLL_OK && (b->h_st[s].err & SCROLL_DEVERR_DYN))
+            set_err("stream %d: a dynamic-rect NAL outgrew its staging slot (%llu bytes)", s,
+                    (unsigned long long)b->geo.slot_bytes);
+        else if (rc == SCROLL_OK)
             set_err("stream %d: output arena overflow (%llu bytes used, capacity %llu)", s,
                     (unsigned long long)b->h_st[s].out_pos,
                     (unsigned long long)b->h_st[s].out_cap);
@@ -1220,19 +1335,27 @@ int scroll_batch_kernel_stats(ScrollBatch *b, double *plan_ms, double *emit_ms, 
     int rc = batch_host_sync(b);
     if (rc) return rc;
     HIPCHK(hipStreamSynchronize(b->last));
-    for (int i = 0; i < b->ring_used; i += 3) {
-        float a = 0, c = 0;
-        HIPCHK(hipEventElapsedTime(&a, b->ring[i], b->ring[i + 1]));
-        HIPCHK(hipEventElapsedTime(&c, b->ring[i + 1], b->ring[i + 2]));
-        b->acc_ms[0] += a;
-        b->acc_ms[1] += c;
-        b->acc_n++;
-    }
-    b->ring_used = 0;
+    fold_ring(b);
     if (plan_ms) *plan_ms = b->acc_ms[0];
     if (emit_ms) *emit_ms = b->acc_ms[1];
     if (count) *count = b->acc_n;
-    b->acc_ms[0] = b->acc_ms[1] = 0;
+    for (int k = 0; k < 4; ++k) b->acc_ms[k] = 0;
+    b->acc_n = 0;
+    return SCROLL_OK;
+}
+
+int scroll_batch_kernel_stats_ex(ScrollBatch *b, double ms[4], int *count)
+{
+    if (!b || !ms) return SCROLL_ERR_ARG;
+    int rc = batch_host_sync(b);
+    if (rc) return rc;
+    HIPCHK(hipStreamSynchronize(b->last));
+    fold_ring(b);
+    for (int k = 0; k < 4; ++k) {
+        ms[k] = b->acc_ms[k];
+        b->acc_ms[k] = 0;
+    }
+    if (count) *count = b->acc_n;
     b->acc_n = 0;
     return SCROLL_OK;
 }
@@ -1263,6 +1386,176 @@ long long scroll_batch_last_nals(ScrollBatch *b)
     return t;
 }
 
+/* ------------------------------ dynamic rect ----------------------------- */
+static void dyn_release(ScrollBatch *b)
+{
+    (void)hipFree(b->d_dfr);
+    (void)hipFree(b->d_src);
+    (void)hipFree(b->d_refs);
+    (void)hipFree(b->d_stage);
+    b->d_dfr = nullptr;
+    b->d_src = b->d_refs = b->d_stage = nullptr;
+    b->dyn_on = 0;
+    b->dyn_refs = 0;
+}
+
+static size_t round256(size_t n) { return (n + 255) & ~(size_t)255; }
+
+static size_t dyn_pair_bytes(const ScrollBatch *b)
+{
+    return round256((size_t)3 * b->dyn_pw * b->dyn_ph);   /* A and B, I420 each */
+}
+
+int scroll_batch_set_dyn_rect(ScrollBatch *b, int x0, int y0, int w, int h, size_t slot_bytes)
+{
+    if (!b || x0 < 0 || y0 < 0 || w < 0 || h < 0) return SCROLL_ERR_ARG;
+    int rc = batch_host_sync(b);
+    if (rc) return rc;
+    HIPCHK(hipSetDevice(b->device));
+    dyn_release(b);
+    if (w == 0 || h == 0) return SCROLL_OK;
+    if (b->nstreams == 0) {
+        set_err("scroll_batch_set_dyn_rect: add the streams first");
+        return SCROLL_ERR_ARG;
+    }
+    const int pw = b->h_st[0].w, ph = b->h_st[0].h;
+    for (int s = 1; s < b->nstreams; ++s)
+        if (b->h_st[s].w != pw || b->h_st[s].h != ph) {
+            set_err("scroll_batch_set_dyn_rect: streams of one batch must share the picture size");
+            return SCROLL_ERR_CONFIG;
+        }
+    const int mbw = pw / 16, mbh = ph / 16;
+    const int ring = std::min(h, (DYN_WINDOW_MBS + w - 1) / w + 2);
+    if ((pw & 15) || (ph & 15) || x0 + w > mbw || y0 + h > mbh || w > DYN_MAX_W ||
+        ring * w > DYN_CTX_MB) {
+        set_err("scroll_batch_set_dyn_rect: rect (%d,%d %dx%d MBs) not supported in %dx%d", x0, y0,
+                w, h, pw, ph);
+        return SCROLL_ERR_CONFIG;
+    }
+    DynGeom g{};
+    g.x0 = x0;
+    g.y0 = y0;
+    g.w = w;
+    g.h = h;
+    g.ring = ring;
+    g.src_fr = (uint64_t)384 * w * h;
+    g.src_ld = round256((size_t)b->max_frames * g.src_fr);
+    g.ref_ld = 0;
+    g.slot_bytes = slot_bytes ? round256(slot_bytes) : dyn_slot_bound(mbw, mbh, w, h);
+    b->dyn_pw = pw;
+    b->dyn_ph = ph;
+    const size_t S = (size_t)b->max_streams, F = (size_t)b->max_frames;
+    hipError_t e = hipMalloc(&b->d_dfr, S * F * sizeof(DynFrame));
+    if (e == hipSuccess) e = hipMalloc(&b->d_src, S * g.src_ld);
+    if (e == hipSuccess) e = hipMalloc(&b->d_refs, S * dyn_pair_bytes(b));
+    if (e == hipSuccess) e = hipMalloc(&b->d_stage, S * F * g.slot_bytes);
+    if (e == hipSuccess) e = hipMemset(b->d_dfr, 0, S * F * sizeof(DynFrame));
+    if (e == hipSuccess) e = hipMemset(b->d_src, 0, S * g.src_ld);
+    if (e == hipSuccess) e = hipMemset(b->d_refs, 0, S * dyn_pair_bytes(b));
+    if (e != hipSuccess) {
+        set_err("scroll_batch_set_dyn_rect: %s", hipGetErrorString(e));
+        dyn_release(b);
+        return e == hipErrorOutOfMemory ? SCROLL_ERR_OOM : SCROLL_ERR_HIP;
+    }
+    b->geo = g;
+    b->dyn_on = 1;
+    return SCROLL_OK;
+}
+
+int scroll_batch_set_dyn_refs(ScrollBatch *b, int s, const uint8_t *ref_a, const uint8_t *ref_b)
+{
+    if (!b || !b->dyn_on || !ref_a || !ref_b || s < -1 || s >= b->nstreams) return SCROLL_ERR_ARG;
+    int rc = batch_host_sync(b);
+    if (rc) return rc;
+    HIPCHK(hipSetDevice(b->device));
+    const size_t pic = (size_t)3 * b->dyn_pw * b->dyn_ph / 2, pair = dyn_pair_bytes(b);
+    if (s >= 0 && b->dyn_refs == 1)                      /* shared -> per stream */
+        for (int k = 1; k < b->nstreams; ++k)
+            HIPCHK(hipMemcpy(b->d_refs + k * pair, b->d_refs, pair, hipMemcpyDeviceToDevice));
+    uint8_t *dst = b->d_refs + (s < 0 ? 0 : (size_t)s * pair);
+    HIPCHK(hipMemcpy(dst, ref_a, pic, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(dst + pic, ref_b, pic, hipMemcpyHostToDevice));
+    if (s < 0) {
+        b->dyn_refs = 1;
+        b->geo.ref_ld = 0;
+    } else {
+        b->dyn_refs = 2;
+        b->geo.ref_ld = pair;
+    }
+    return SCROLL_OK;
+}
+
+int scroll_batch_set_dyn_source(ScrollBatch *b, const uint8_t *src, int nframes)
+{
+    if (!b || !b->dyn_on || !src || nframes < 0 || nframes > b->max_frames) return SCROLL_ERR_ARG;
+    if (nframes == 0) return SCROLL_OK;
+    HIPCHK(hipSetDevice(b->device));
+    const size_t row = (size_t)nframes * b->geo.src_fr;
+    HIPCHK(hipMemcpy2D(b->d_src, b->geo.src_ld, src, row, row, (size_t)b->nstreams,
+                       hipMemcpyHostToDevice));
+    return SCROLL_OK;
+}
+
+uint8_t *scroll_batch_dyn_source_device(ScrollBatch *b, size_t *stream_stride, size_t *frame_stride)
+{
+    if (!b || !b->dyn_on) return nullptr;
+    if (stream_stride) *stream_stride = b->geo.src_ld;
+    if (frame_stride) *frame_stride = b->geo.src_fr;
+    return b->d_src;
+}
+
+int scroll_batch_dyn_source_synth(ScrollBatch *b, int nframes, int stream_base, int t0)
+{
+    if (!b || !b->dyn_on || nframes < 0 || nframes > b->max_frames) return SCROLL_ERR_ARG;
+    HIPCHK(hipSetDevice(b->device));
+    if (dyn_launch_synth(b->own, nframes, b->nstreams, b->d_src, &b->geo, stream_base, t0)) {
+        set_err("k_dyn_synth launch: %s", hipGetErrorString(hipGetLastError()));
+        return SCROLL_ERR_HIP;
+    }
+    HIPCHK(hipStreamSynchronize(b->own));
+    return SCROLL_OK;
+}
+
+int scroll_batch_dyn_frame_info(ScrollBatch *b, int s, int f, uint32_t *rbsp_bytes,
+                                uint32_t *ep_bytes)
+{
+    if (!b || !b->dyn_on || s < 0 || s >= b->nstreams || f < 0 || f >= b->max_frames)
+        return SCROLL_ERR_ARG;
+    int rc = batch_host_sync(b);
+    if (rc) return rc;
+    DynFrame d;
+    HIPCHK(hipMemcpy(&d, b->d_dfr + (size_t)s * b->max_frames + f, sizeof(d),
+                     hipMemcpyDeviceToHost));
+    if (rbsp_bytes) *rbsp_bytes = d.rbsp_bytes;
+    if (ep_bytes) *ep_bytes = d.ep;
+    return d.nal < 0 ? 1 : SCROLL_OK;
+}
+
+int scroll_batch_dyn_totals(ScrollBatch *b, unsigned long long *rbsp_bytes,
+                            unsigned long long *ep_bytes, long long *dyn_nals)
+{
+    if (!b || !b->dyn_on) return SCROLL_ERR_ARG;
+    int rc = batch_host_sync(b);
+    if (rc) return rc;
+    const size_t S = (size_t)b->nstreams, F = (size_t)b->max_frames;
+    std::vector<DynFrame> v(S * F);
+    HIPCHK(hipMemcpy(v.data(), b->d_dfr, v.size() * sizeof(DynFrame), hipMemcpyDeviceToHost));
+    unsigned long long r = 0, e = 0;
+    long long n = 0;
+    for (size_t s = 0; s < S; ++s)
+        for (int f = 0; f < b->last_nframes; ++f) {
+            const DynFrame &d = v[s * F + (size_t)f];
+            if (d.nal < 0) continue;
+            r += d.rbsp_bytes;
+            e += d.ep;
+            n++;
+        }
+    if (rbsp_bytes) *rbsp_bytes = r;
+    if (ep_bytes) *ep_bytes = e;
+    if (dyn_nals) *dyn_nals = n;
+    return SCROLL_OK;
+}
+
 int scroll_batch_enable_timing(ScrollBatch *b, int on)
 {
     if (!b) return SCROLL_ERR_ARG;
@@ -1272,11 +1565,10 @@ int scroll_batch_enable_timing(ScrollBatch *b, int on)
 
 float scroll_batch_kernel_ms(ScrollBatch *b, int which)
 {
-    if (!b || which < 0 || which > 1) return -1.0f;
+    if (!b || which < 0 || which > 3) return -1.0f;
     if (batch_host_sync(b)) return -1.0f;
     if (b->timed_pending) {
-        if (hipEventElapsedTime(&b->ms[0], b->ev[0], b->ev[1]) != hipSuccess) return -1.0f;
-        if (hipEventElapsedTime(&b->ms[1], b->ev[1], b->ev[2]) != hipSuccess) return -1.0f;
+        event_ms(b->ev, b->ms);
         b->timed_pending = 0;
     }
     return b->ms[which];

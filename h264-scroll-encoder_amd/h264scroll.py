@@ -143,6 +143,20 @@ def _load():
                                                  P(ctypes.c_uint32), P(ctypes.c_int)]),
         "scroll_batch_enable_timing": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
         "scroll_batch_kernel_ms": (ctypes.c_float, [ctypes.c_void_p, ctypes.c_int]),
+        "scroll_batch_set_dyn_rect": (ctypes.c_int, [ctypes.c_void_p] + [ctypes.c_int] * 4 +
+                                      [ctypes.c_size_t]),
+        "scroll_batch_set_dyn_refs": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, u8p, u8p]),
+        "scroll_batch_set_dyn_source": (ctypes.c_int, [ctypes.c_void_p, u8p, ctypes.c_int]),
+        "scroll_batch_dyn_source_device": (ctypes.c_void_p, [ctypes.c_void_p, P(ctypes.c_size_t),
+                                                             P(ctypes.c_size_t)]),
+        "scroll_batch_dyn_source_synth": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int,
+                                                         ctypes.c_int, ctypes.c_int]),
+        "scroll_batch_dyn_frame_info": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                                       P(ctypes.c_uint32), P(ctypes.c_uint32)]),
+        "scroll_batch_dyn_totals": (ctypes.c_int, [ctypes.c_void_p, P(ctypes.c_ulonglong),
+                                                   P(ctypes.c_ulonglong), P(ctypes.c_longlong)]),
+        "scroll_batch_kernel_stats_ex": (ctypes.c_int, [ctypes.c_void_p, P(ctypes.c_double),
+                                                        P(ctypes.c_int)]),
         "composer_batch_write_scroll_frames": (ctypes.c_int, [P(P(Composer)), P(ctypes.c_int),
                                                               ctypes.c_int, ctypes.c_int]),
         "composer_flush": (ctypes.c_int, [P(Composer)]),
@@ -345,6 +359,49 @@ class Batch:
         self._chk(lib.scroll_batch_kernel_stats(self.h, ctypes.byref(a), ctypes.byref(e),
                                                 ctypes.byref(n)), "kernel_stats")
         return a.value, e.value, n.value
+
+    def kernel_stats_ex(self):
+        """(plan, emit, dyn stage, dyn emit) ms summed since the last call, composes"""
+        ms, n = (ctypes.c_double * 4)(), ctypes.c_int()
+        self._chk(lib.scroll_batch_kernel_stats_ex(self.h, ms, ctypes.byref(n)), "kernel_stats_ex")
+        return tuple(ms), n.value
+
+    # ---- dynamic rect (configs 3-5) ----
+    def set_dyn_rect(self, x0, y0, w, h, slot_bytes=0):
+        self._chk(lib.scroll_batch_set_dyn_rect(self.h, x0, y0, w, h, slot_bytes), "set_dyn_rect")
+
+    def set_dyn_refs(self, ref_a, ref_b, stream=-1):
+        """ref_a / ref_b: I420 bytes (w*h*3/2) of reference pictures A and B"""
+        self._chk(lib.scroll_batch_set_dyn_refs(self.h, stream, u8buf(bytes(ref_a)),
+                                                u8buf(bytes(ref_b))), "set_dyn_refs")
+
+    def set_dyn_source(self, src, nframes):
+        """src: bytes of [num_streams][nframes][384*w*h]"""
+        self._chk(lib.scroll_batch_set_dyn_source(self.h, u8buf(bytes(src)), nframes),
+                  "set_dyn_source")
+
+    def dyn_source_device(self):
+        ls, lf = ctypes.c_size_t(), ctypes.c_size_t()
+        p = lib.scroll_batch_dyn_source_device(self.h, ctypes.byref(ls), ctypes.byref(lf))
+        return p, ls.value, lf.value
+
+    def dyn_source_synth(self, nframes, stream_base=0, t0=0):
+        self._chk(lib.scroll_batch_dyn_source_synth(self.h, nframes, stream_base, t0),
+                  "dyn_source_synth")
+
+    def dyn_frame_info(self, s, f):
+        """(rbsp bytes, EP bytes) of frame f's dynamic NAL, None if it has none"""
+        r, e = ctypes.c_uint32(), ctypes.c_uint32()
+        rc = self._chk(lib.scroll_batch_dyn_frame_info(self.h, s, f, ctypes.byref(r),
+                                                       ctypes.byref(e)), "dyn_frame_info")
+        return None if rc == 1 else (r.value, e.value)
+
+    def dyn_totals(self):
+        """last compose: (staged RBSP bytes, EP bytes, dynamic NALs) over all streams"""
+        r, e, n = ctypes.c_ulonglong(), ctypes.c_ulonglong(), ctypes.c_longlong()
+        self._chk(lib.scroll_batch_dyn_totals(self.h, ctypes.byref(r), ctypes.byref(e),
+                                              ctypes.byref(n)), "dyn_totals")
+        return r.value, e.value, n.value
 
     def last_bytes(self):
         return lib.scroll_batch_last_bytes(self.h)

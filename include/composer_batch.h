@@ -106,7 +106,8 @@ int scroll_batch_nal_info(ScrollBatch *b, int s, int i, int *kind, int *offset_p
                           uint32_t *size, int *slow);
 
 /* HIP-event timing of the last compose's kernels, on the launch stream:
- * which 0 = plan kernel, 1 = emit kernel.  Enable before compose. */
+ * which 0 = plan kernel(s), 1 = emit kernel, 2 = dyn stage, 3 = dyn emit.
+ * Enable before compose. */
 int scroll_batch_enable_timing(ScrollBatch *b, int on);
 float scroll_batch_kernel_ms(ScrollBatch *b, int which);
 /* all timed composes since the last call: summed plan / emit kernel ms and
@@ -119,6 +120,40 @@ long long scroll_batch_debug_stamps(ScrollBatch *b, uint64_t *dst, long long max
 unsigned long long scroll_batch_last_bytes(ScrollBatch *b);
 /* NAL units planned by the last compose (sum over streams) */
 long long scroll_batch_last_nals(ScrollBatch *b);
+
+/* ---- dynamic rect (BASELINE configs 3-5; no reference counterpart) ----
+ * Every scroll NAL of the batch carries a rectangle of dynamic MBs: they keep
+ * their row's (ref_idx, mv) and add coded_block_pattern, mb_qp_delta and a
+ * CAVLC residual of (source - prediction) at QP 26 (bit-exact definition:
+ * oracle/dyn_oracle.h).  Waypoint NALs stay residual-free.  All streams of
+ * the batch must share one picture size; call after adding the streams.
+ *
+ *   scroll_batch_set_dyn_rect(b, x0, y0, w, h, slot)   MB units; w or h = 0
+ *       turns the rect off.  slot = staging bytes per frame, 0 = a bound no
+ *       NAL can exceed (larger ones fail with SCROLL_ERR_OVERFLOW).
+ *   scroll_batch_set_dyn_refs(b, s, a, b)   decoded reference pictures A and
+ *       B (I420, w*h*3/2 bytes each) of stream s, or of every stream (s = -1)
+ *   source pixels: [stream][frame] blocks of 384*w*h bytes (the rect's luma
+ *       16w x 16h, then Cb, Cr 8w x 8h), frame f = the f-th composed frame of
+ *       the next compose: scroll_batch_set_dyn_source (host copy),
+ *       scroll_batch_dyn_source_device (fill in place), or
+ *       scroll_batch_dyn_source_synth (the synthetic source of SURVEY §8d for
+ *       global stream ids stream_base + s and frame numbers t0 + f). */
+int scroll_batch_set_dyn_rect(ScrollBatch *b, int x0, int y0, int w, int h, size_t slot_bytes);
+int scroll_batch_set_dyn_refs(ScrollBatch *b, int s, const uint8_t *ref_a, const uint8_t *ref_b);
+int scroll_batch_set_dyn_source(ScrollBatch *b, const uint8_t *src, int nframes);
+uint8_t *scroll_batch_dyn_source_device(ScrollBatch *b, size_t *stream_stride,
+                                        size_t *frame_stride);
+int scroll_batch_dyn_source_synth(ScrollBatch *b, int nframes, int stream_base, int t0);
+/* last compose, frame f of stream s: staged RBSP bytes and EP bytes */
+int scroll_batch_dyn_frame_info(ScrollBatch *b, int s, int f, uint32_t *rbsp_bytes,
+                                uint32_t *ep_bytes);
+/* last compose, all streams: staged RBSP bytes, EP bytes, dynamic NALs */
+int scroll_batch_dyn_totals(ScrollBatch *b, unsigned long long *rbsp_bytes,
+                            unsigned long long *ep_bytes, long long *dyn_nals);
+/* HIP-event ms of the timed composes since the last call: plan (both
+ * passes), emit, dyn stage, dyn emit; accumulators reset afterwards */
+int scroll_batch_kernel_stats_ex(ScrollBatch *b, double ms[4], int *count);
 
 /* Composer-level batch: offsets[i] composed on cs[i], i < n, in
  * order; Composers may repeat.  Output lands in each Composer's buffer before

@@ -479,7 +479,16 @@ size_t or_scroll_nal_dyn(uint8_t *dst, size_t cap, or_cfg *c, int off, const or_
     if (!rc || rc->w <= 0 || rc->h <= 0) return or_scroll_nal(dst, cap, c, off);
     const int mbw = c->w / 16, mbh = c->h / 16;
     size_t rcap = 64 + (size_t)mbw * mbh * 24 + (size_t)rc->w * rc->h * 2048;
-    uint8_t *rbsp = (uint8_t *)malloc(rcap);
+    /* per-thread scratch reused across calls (a fresh 1+ MB malloc per frame
+     * is an mmap/munmap pair that serialises threads on the mm lock) */
+    static __thread uint8_t *tl_rbsp;
+    static __thread size_t tl_cap;
+    if (tl_cap < rcap) {
+        free(tl_rbsp);
+        tl_rbsp = (uint8_t *)malloc(rcap);
+        tl_cap = rcap;
+    }
+    uint8_t *rbsp = tl_rbsp;
     or_bits b;
     or_bits_init(&b, rbsp, rcap);
     or_scroll_header(&b, c);                               /* :549-553 */
@@ -506,7 +515,7 @@ size_t or_scroll_nal_dyn(uint8_t *dst, size_t cap, or_cfg *c, int off, const or_
     or_mvi2 *cur = (or_mvi2 *)calloc((size_t)mbw, sizeof(or_mvi2));
     or_tcctx *tc_above = (or_tcctx *)calloc((size_t)mbw, sizeof(or_tcctx));
     or_tcctx *tc_cur = (or_tcctx *)calloc((size_t)mbw, sizeof(or_tcctx));
-    static int luma[16][16], cdc[2][4], cac[2][4][15];
+    int luma[16][16], cdc[2][4], cac[2][4][15];           /* per call: thread-safe */
     for (int y = 0; y < mbh; ++y) {
         or_mvi2 left;
         memset(&left, 0, sizeof(left));
@@ -547,7 +556,6 @@ size_t or_scroll_nal_dyn(uint8_t *dst, size_t cap, or_cfg *c, int off, const or_
     free(tc_cur);
     or_trailing(&b);
     const size_t n = or_nal(dst, cap, 0, 1, rbsp, or_bytes(&b));
-    free(rbsp);
     c->frame_num++;
     return n;
 }
@@ -569,4 +577,94 @@ size_t or_compose_dyn(uint8_t *dst, size_t cap, or_cfg *c, int off, int mode,
     n += or_scroll_nal_dyn(dst + n, cap - n, c, off, r, src, R);
     if (n_wp_out) *n_wp_out = nwp;
     return n;
+}
+
+/* ------------------------------------------------------------------------ */
+/* CPU baseline driver (bench.py cpu_baseline leg): BASELINE config 3 on     */
+/* nthreads pthreads, streams split evenly; each stream cycles 4 source     */
+/* frames of the synthetic generator (generated inside the timed region).   */
+/* ------------------------------------------------------------------------ */
+#include <pthread.h>
+#include <time.h>
+
+typedef struct {
+    int s0, s1, nframes, w, h;
+    or_dyn_rect r;
+    const or_refs *R;
+    unsigned long long bytes;
+    long long frames;
+} or_dyn_job;
+
+static void *or_dyn_worker(void *arg)
+{
+    or_dyn_job *j = (or_dyn_job *)arg;
+    const size_t sb = (size_t)384 * j->r.w * j->r.h;
+    const size_t cap = (size_t)(j->w / 16) * (j->h / 16) * 24 + (size_t)j->r.w * j->r.h * 2048 + 4096;
+    uint8_t *buf = (uint8_t *)malloc(cap), *src = (uint8_t *)malloc(4 * sb);
+    for (int s = j->s0; s < j->s1; ++s) {
+        or_cfg c;
+        or_cfg_init(&c, j->w, j->h);
+        c.frame_num = 2;
+        for (int t = 0; t < 4; ++t) or_dyn_source(src + t * sb, s, t, &j->r);
+        for (int i = 0; i < j->nframes; ++i) {
+            const size_t n = or_compose_dyn(buf, cap, &c, or_synthetic_offset(s, i, j->h), 0, &j->r,
+                                            src + (i & 3) * sb, j->R, NULL);
+            j->bytes += n;
+            j->frames++;
+        }
+    }
+    free(buf);
+    free(src);
+    return NULL;
+}
+
+double or_bench_compose_dyn(int nstreams, int nframes, int w, int h, int rx0, int ry0, int rw,
+                            int rh, int nthreads, unsigned long long *bytes_out)
+{
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > nstreams) nthreads = nstreams;
+    const size_t ys = (size_t)w * h, cs = ys / 4;
+    uint8_t *pl = (uint8_t *)malloc(2 * (ys + 2 * cs));
+    or_pic P[2];
+    for (int k = 0; k < 2; ++k) {
+        uint8_t *y = pl + k * (ys + 2 * cs);
+        or_striped_planes(y, y + ys, y + ys + cs, w, h, k);
+        P[k].w = w;
+        P[k].h = h;
+        P[k].y = y;
+        P[k].u = y + ys;
+        P[k].v = y + ys + cs;
+    }
+    or_refs R = {{&P[0], &P[1]}};
+    pthread_t *th = (pthread_t *)calloc((size_t)nthreads, sizeof(pthread_t));
+    or_dyn_job *jobs = (or_dyn_job *)calloc((size_t)nthreads, sizeof(or_dyn_job));
+    for (int t = 0; t < nthreads; ++t) {
+        jobs[t].s0 = (int)((long long)nstreams * t / nthreads);
+        jobs[t].s1 = (int)((long long)nstreams * (t + 1) / nthreads);
+        jobs[t].nframes = nframes;
+        jobs[t].w = w;
+        jobs[t].h = h;
+        jobs[t].r.x0 = rx0;
+        jobs[t].r.y0 = ry0;
+        jobs[t].r.w = rw;
+        jobs[t].r.h = rh;
+        jobs[t].R = &R;
+    }
+    struct timespec a, b;
+    clock_gettime(CLOCK_MONOTONIC, &a);
+    for (int t = 0; t < nthreads; ++t) pthread_create(&th[t], NULL, or_dyn_worker, &jobs[t]);
+    for (int t = 0; t < nthreads; ++t) pthread_join(th[t], NULL);
+    clock_gettime(CLOCK_MONOTONIC, &b);
+    const double dt = (double)(b.tv_sec - a.tv_sec) + 1e-9 * (double)(b.tv_nsec - a.tv_nsec);
+    unsigned long long bytes = 0;
+    long long frames = 0;
+    for (int t = 0; t < nthreads; ++t) {
+        bytes += jobs[t].bytes;
+        frames += jobs[t].frames;
+    }
+    if (bytes_out) *bytes_out = bytes;
+    free(th);
+    free(jobs);
+    free(pl);
+    return dt > 0 ? (double)frames / dt : 0.0;
 }

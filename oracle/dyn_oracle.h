@@ -89,6 +89,11 @@ size_t or_scroll_nal_dyn(uint8_t *dst, size_t cap, or_cfg *c, int off, const or_
 size_t or_compose_dyn(uint8_t *dst, size_t cap, or_cfg *c, int off, int mode,
                       const or_dyn_rect *r, const uint8_t *src, const or_refs *R, int *n_wp_out);
 
+/* CPU baseline: frames/s of BASELINE config 3 (synthetic offsets and source,
+ * striped refs) on nthreads pthreads */
+double or_bench_compose_dyn(int nstreams, int nframes, int w, int h, int rx0, int ry0, int rw,
+                            int rh, int nthreads, unsigned long long *bytes_out);
+
 /* test hook: the residual bits of one dynamic MB (cbp + qp_delta + residual,
  * after the MB's mvd fields) for given quantised levels; tc_out receives
  * TotalCoeff of the 16 luma (raster) + 8 chroma AC blocks */

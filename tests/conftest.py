@@ -51,7 +51,8 @@ def hostsim():
     d = os.path.join(REPO, "tests", "hostsim")
     so = os.path.join(d, "libhostsim.so")
     src = [os.path.join(d, "sim.cpp"),
-           os.path.join(PKG, "csrc", "scroll_device.h")]
+           os.path.join(PKG, "csrc", "scroll_device.h"),
+           os.path.join(PKG, "csrc", "dyn_device.h")]
     if not os.path.exists(so) or any(os.path.getmtime(s) > os.path.getmtime(so) for s in src):
         subprocess.run(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-I", d,
                         "-I", os.path.join(PKG, "csrc"), src[0], "-o", so], check=True)

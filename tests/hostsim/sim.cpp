@@ -16,6 +16,7 @@
 #include <array>
 #include <vector>
 #include "scroll_device.h"
+#include "dyn_device.h"
 
 using namespace scroll;
 
@@ -210,6 +211,78 @@ long sim_stream(int w, int h, int l2f, int poct, int l2p, int dbf, int n, const 
         if (wr[x] < 0) return -6;
     memcpy(out, A.data(), span);
     return (long)total;
+}
+
+
+/* ---- dynamic-rect device functions (dyn_device.h) ---------------------- */
+static const dyn::Tabs g_dyn_tabs = SCROLL_DYN_TABS;
+
+struct HostOr {
+    uint32_t *b;
+    void operator()(uint32_t i, uint32_t v) const { b[i] |= v; }
+};
+
+/* one CAVLC block at bit offset `start` of a zeroed MSB-first word buffer;
+ * returns the bit count (must equal the CountSink pass) or -1 on mismatch */
+long sim_cavlc(const int *coef, int max, int nC, int start, uint32_t *words, int *tc_out)
+{
+    dyn::CountSink cs{0};
+    const int tc = dyn::cavlc_block(cs, g_dyn_tabs, coef, max, nC);
+    dyn::OrSink<HostOr> os{{words}, 0, 0, 0};
+    os.start((uint32_t)start);
+    const int tc2 = dyn::cavlc_block(os, g_dyn_tabs, coef, max, nC);
+    const uint32_t end = os.wi * 32u + (uint32_t)os.fill;
+    os.finish();
+    *tc_out = tc;
+    if (tc != tc2 || end - (uint32_t)start != cs.n) return -1;
+    return (long)cs.n;
+}
+
+/* luma: reference sample via luma_row; chroma: chroma_row where it applies
+ * (else the general tree); planes[ri][p] of the two pictures */
+int sim_ref_sample(int w, int h, const int *wo, const int *wv, int ri, int p, int x, int y,
+                   const uint8_t *const *planes, int *fast)
+{
+    dyn::WpTab T{wo, wv, h};
+    dyn::RefPics R;
+    R.w = w;
+    R.h = h;
+    for (int i = 0; i < 2; ++i)
+        for (int k = 0; k < 3; ++k) R.pl[i][k] = planes[3 * i + k];
+    int yo;
+    if (p == 0) {
+        const int b = dyn::luma_row(T, ri, y, yo);
+        *fast = 1;
+        return R.pl[b][0][(size_t)yo * w + x];
+    }
+    const int b = dyn::chroma_row(T, ri, y, yo);
+    if (b >= 0) {
+        *fast = 1;
+        return R.pl[b][p][(size_t)yo * (w / 2) + x];
+    }
+    *fast = 0;
+    return dyn::chroma_px_any<9>(T, R, ri, p, x, y);
+}
+
+/* forward transform + quantisation of one residual block (raster order in,
+ * levels at raster positions out); dc: chroma DC quantiser of one value */
+void sim_fwd_quant(const int *res, int *lv)
+{
+    int W[16];
+    dyn::fwd4x4(res, W);
+    for (int k = 0; k < 16; ++k) lv[k] = dyn::quant(W[k], k);
+}
+
+int sim_quant_dc(int w) { return dyn::quant_dc(w); }
+
+int sim_ep_count(const uint8_t *b, int n)
+{
+    int prev = -1, c = 0;
+    for (int i = 0; i < n; ++i) {
+        c += dyn::ep_insert(b[i], i - 1 - prev);
+        if (b[i]) prev = i;
+    }
+    return c;
 }
 
 }  // extern "C"

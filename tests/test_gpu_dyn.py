@@ -1,0 +1,266 @@
+"""GPU parity of the dynamic-rect residual coder (BASELINE configs 3-5):
+k_plan (state) -> k_dyn_stage -> k_plan (size) -> k_emit -> k_dyn_emit,
+through the C ABI, against the CPU restatement oracle/dyn_oracle.c
+(or_compose_dyn), byte for byte.  The reference has no implementation of
+this path, so these bits are pinned only by the restatement, which
+tests/test_dyn_oracle.py checks with an independent decoder and the
+reference's own CAVLC parser ("parity unpinned").
+Run on an MI355X: -m gpu."""
+import ctypes
+
+import numpy as np
+import pytest
+
+from conftest import synthetic_offsets
+from dynhelp import OrCfg, Pic, Rect, Refs, StripedRefs, rect_source, split_nals
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def gpu(scroll):
+    if scroll.device_count() < 1:
+        pytest.fail("no gfx950 device: " + scroll.last_error())
+    return scroll
+
+
+class ArrayRefs:
+    """Reference pictures A, B from numpy planes (I420 bytes for the GPU,
+    or_refs for the oracle)."""
+
+    def __init__(self, planes):               # planes: [(y, u, v), (y, u, v)] uint8 arrays
+        self.planes = [tuple(np.ascontiguousarray(p, dtype=np.uint8) for p in pic) for pic in planes]
+        h, w = self.planes[0][0].shape
+        self.pics = [Pic(w, h, p[0].ctypes.data, p[1].ctypes.data, p[2].ctypes.data)
+                     for p in self.planes]
+        self.refs = Refs()
+        self.refs.ab[0] = ctypes.pointer(self.pics[0])
+        self.refs.ab[1] = ctypes.pointer(self.pics[1])
+
+    def i420(self, k):
+        return b"".join(p.tobytes() for p in self.planes[k])
+
+
+def striped_refs(oracle, w, h):
+    sr = StripedRefs(oracle, w, h)
+    planes = []
+    for y, u, v in sr.planes:
+        planes.append((np.frombuffer(bytes(y), np.uint8).reshape(h, w),
+                       np.frombuffer(bytes(u), np.uint8).reshape(h // 2, w // 2),
+                       np.frombuffer(bytes(v), np.uint8).reshape(h // 2, w // 2)))
+    return ArrayRefs(planes)
+
+
+def random_refs(w, h, seed):
+    rng = np.random.default_rng(seed)
+    return ArrayRefs([(rng.integers(0, 256, (h, w)), rng.integers(0, 256, (h // 2, w // 2)),
+                       rng.integers(0, 256, (h // 2, w // 2))) for _ in range(2)])
+
+
+def synth_source(oracle, S, F, rect, t0=0):
+    """[S][F][384 w h] of the documented synthetic source (dyn_oracle.h)"""
+    n = 384 * rect.w * rect.h
+    out = np.zeros((S, F, n), np.uint8)
+    for s in range(S):
+        for t in range(F):
+            out[s, t] = np.frombuffer(bytes(rect_source(oracle, s, t0 + t, rect)), np.uint8)
+    return out
+
+
+def oracle_streams(oracle, w, h, offsets, rect, src, R, mode=0, frame_num=2, waypoints=()):
+    S, F = offsets.shape
+    oracle.or_compose_dyn.restype = ctypes.c_size_t
+    buf = (ctypes.c_uint8 * (16 << 20))()
+    nwp = ctypes.c_int()
+    outs = []
+    for s in range(S):
+        cfg = OrCfg()
+        oracle.or_cfg_init(ctypes.byref(cfg), w, h)
+        cfg.frame_num = frame_num
+        for i, (o, lt, v) in enumerate(waypoints):
+            cfg.wp_off[i], cfg.wp_lt[i], cfg.wp_valid[i] = o, lt, v
+        cfg.nwp = len(waypoints)
+        o = bytearray()
+        for t in range(F):
+            sp = np.ascontiguousarray(src[s, t])
+            n = oracle.or_compose_dyn(buf, len(buf), ctypes.byref(cfg), int(offsets[s, t]), mode,
+                                      ctypes.byref(rect), sp.ctypes.data_as(ctypes.c_void_p),
+                                      ctypes.byref(R.refs), ctypes.byref(nwp))
+            assert n > 0
+            o += bytes(buf[:n])
+        outs.append(bytes(o))
+    return outs
+
+
+def gpu_streams(gpu, w, h, offsets, rect, R, src=None, synth=False, mode=0, chunks=None,
+                arena=None, slot=0, waypoints=(), shared_refs=True, per_stream_refs=None):
+    S, F = offsets.shape
+    b = gpu.Batch(S, F, arena or (8 << 20), mode=mode)
+    for _ in range(S):
+        b.add_stream(gpu.make_config(w, h, waypoints=waypoints))
+    b.set_dyn_rect(rect.x0, rect.y0, rect.w, rect.h, slot)
+    if shared_refs:
+        b.set_dyn_refs(R.i420(0), R.i420(1))
+    for s, Rs in (per_stream_refs or {}).items():
+        b.set_dyn_refs(Rs.i420(0), Rs.i420(1), stream=s)
+    pos = 0
+    for n in (chunks or [F]):
+        b.set_offsets(np.ascontiguousarray(offsets[:, pos:pos + n]))
+        if synth:
+            b.dyn_source_synth(n, 0, pos)
+        else:
+            b.set_dyn_source(np.ascontiguousarray(src[:, pos:pos + n]).tobytes(), n)
+        b.compose(n)
+        rc = b.sync()
+        if rc != 0:
+            return b, rc
+        pos += n
+    return b, 0
+
+
+def check_equal(b, want):
+    for s, ws in enumerate(want):
+        got = b.output(s)
+        if got != ws:
+            gn, wn = split_nals(got), split_nals(ws)
+            bad = next((i for i, (x, y) in enumerate(zip(gn, wn)) if x != y), min(len(gn), len(wn)))
+            detail = ""
+            if bad < min(len(gn), len(wn)):
+                x, y = gn[bad], wn[bad]
+                k = next((i for i, (p, q) in enumerate(zip(x, y)) if p != q), min(len(x), len(y)))
+                detail = f"NAL {bad}: sizes {len(x)} vs {len(y)}, first diff at byte {k}"
+            raise AssertionError(f"stream {s}: {len(got)} vs {len(ws)} bytes, "
+                                 f"{len(gn)} vs {len(wn)} NALs; {detail}")
+
+
+def test_dyn_small_with_waypoints(gpu, oracle):
+    w, h = 64, 512
+    rect = Rect(1, 3, 2, 20)
+    offs = synthetic_offsets(3, 40, h)
+    offs[0] = np.arange(480, 520)                     # crosses 496: a waypoint
+    offs[1] = np.arange(1010, 970, -1)                # crosses 992: a second one
+    R = striped_refs(oracle, w, h)
+    src = synth_source(oracle, 3, 40, rect)
+    want = oracle_streams(oracle, w, h, offs, rect, src, R)
+    b, rc = gpu_streams(gpu, w, h, offs, rect, R, src)
+    assert rc == 0, gpu.last_error()
+    check_equal(b, want)
+    for s in (0, 1):
+        nals = b.nals(s)
+        assert any(k == 1 and sl == 0 for k, _, _, sl in nals)   # waypoints: run layout
+        assert sum(sl == 2 for _, _, _, sl in nals) == 40         # every scroll NAL dynamic
+
+
+def test_dyn_full_frame_random_pixels(gpu, oracle):
+    """rect = whole picture (no left/top neighbours at the edges), random
+    reference and source pixels (large residuals, long level codes)"""
+    w, h = 96, 96
+    rect = Rect(0, 0, 6, 6)
+    rng = np.random.default_rng(7)
+    S, F = 2, 12
+    offs = rng.integers(-200, 300, (S, F)).astype(np.int32)
+    R = random_refs(w, h, 1)
+    src = rng.integers(0, 256, (S, F, 384 * 36)).astype(np.uint8)
+    want = oracle_streams(oracle, w, h, offs, rect, src, R)
+    b, rc = gpu_streams(gpu, w, h, offs, rect, R, src)
+    assert rc == 0, gpu.last_error()
+    check_equal(b, want)
+
+
+@pytest.mark.parametrize("rect", [(0, 0, 1, 20), (3, 4, 13, 3), (7, 0, 12, 20), (19, 19, 1, 1)])
+def test_dyn_rect_shapes(gpu, oracle, rect):
+    """window splits across rows, rect width 1 (TotalCoeff row ring), rects
+    touching every picture edge"""
+    w, h = 320, 320
+    rc_ = Rect(*rect)
+    S, F = 2, 6
+    offs = synthetic_offsets(S, F, h, first_stream=5)
+    R = random_refs(w, h, 3)
+    src = synth_source(oracle, S, F, rc_)
+    want = oracle_streams(oracle, w, h, offs, rc_, src, R)
+    b, rc = gpu_streams(gpu, w, h, offs, rc_, R, src)
+    assert rc == 0, gpu.last_error()
+    check_equal(b, want)
+
+
+def test_dyn_720p_config3_device_synth(gpu, oracle):
+    """BASELINE config 3 geometry: 1280x720, 360x360 rect at MB (28, 10);
+    the source generated on the device (k_dyn_synth) must equal the
+    documented generator, and the NALs the oracle's"""
+    w, h = 1280, 720
+    rect = Rect(28, 10, 25, 25)
+    S, F = 2, 6
+    offs = synthetic_offsets(S, F, h)
+    R = striped_refs(oracle, w, h)
+    src = synth_source(oracle, S, F, rect)
+    want = oracle_streams(oracle, w, h, offs, rect, src, R)
+    b, rc = gpu_streams(gpu, w, h, offs, rect, R, synth=True)
+    assert rc == 0, gpu.last_error()
+    check_equal(b, want)
+    eps = []
+    for s in range(S):
+        for t in range(F):
+            rb, ep = b.dyn_frame_info(s, t)
+            assert rb > 20000
+            eps.append(ep)
+    assert any(eps)                                   # emulation prevention exercised
+    sizes = [sz for k, _, sz, sl in b.nals(0) if sl == 2]
+    assert len(sizes) == F
+
+
+def test_dyn_chunked_composes_and_experiment_mode(gpu, oracle):
+    w, h = 64, 512
+    rect = Rect(0, 5, 4, 9)
+    S, F = 3, 30
+    offs = synthetic_offsets(S, F, h, first_stream=1)
+    R = random_refs(w, h, 11)
+    src = synth_source(oracle, S, F, rect)
+    for mode in (0, 1):
+        want = oracle_streams(oracle, w, h, offs, rect, src, R, mode=mode)
+        b, rc = gpu_streams(gpu, w, h, offs, rect, R, synth=True, mode=mode, chunks=[7, 1, 22])
+        assert rc == 0, gpu.last_error()
+        check_equal(b, want)
+        b.close()
+
+
+def test_dyn_half_pel_waypoint_chain(gpu, oracle):
+    """a resumed config with a waypoint at an odd offset: its rows predict at
+    half-pel chroma positions, which only the general k_dyn_stage path does"""
+    w, h = 64, 1024
+    rect = Rect(1, 0, 2, 64)
+    wps = [(501, 2, 1)]
+    S, F = 1, 6
+    offs = np.array([[600, 610, 777, 900, 505, 996]], np.int32)
+    R = random_refs(w, h, 5)
+    src = synth_source(oracle, S, F, rect)
+    want = oracle_streams(oracle, w, h, offs, rect, src, R, waypoints=wps)
+    b, rc = gpu_streams(gpu, w, h, offs, rect, R, src, waypoints=wps)
+    assert rc == 0, gpu.last_error()
+    check_equal(b, want)
+
+
+def test_dyn_per_stream_refs(gpu, oracle):
+    w, h = 96, 64
+    rect = Rect(1, 1, 3, 2)
+    S, F = 3, 5
+    offs = synthetic_offsets(S, F, h)
+    Rs = [random_refs(w, h, 20 + s) for s in range(S)]
+    src = synth_source(oracle, S, F, rect)
+    want = [oracle_streams(oracle, w, h, offs[s:s + 1], rect, src[s:s + 1], Rs[s])[0]
+            for s in range(S)]
+    b, rc = gpu_streams(gpu, w, h, offs, rect, Rs[0], src, shared_refs=True,
+                        per_stream_refs={1: Rs[1], 2: Rs[2]})
+    assert rc == 0, gpu.last_error()
+    check_equal(b, want)
+
+
+def test_dyn_staging_overflow_commits_nothing(gpu, oracle):
+    w, h = 96, 96
+    rect = Rect(0, 0, 6, 6)
+    rng = np.random.default_rng(3)
+    offs = np.zeros((1, 2), np.int32)
+    R = random_refs(w, h, 2)
+    src = rng.integers(0, 256, (1, 2, 384 * 36)).astype(np.uint8)
+    b, rc = gpu_streams(gpu, w, h, offs, rect, R, src, slot=1024)
+    assert rc == gpu.SCROLL_ERR_OVERFLOW
+    assert b.output_size(0) == 0

@@ -97,6 +97,24 @@ struct CountSink {
     __device__ __host__ inline void put(uint32_t, int k) { n += (uint32_t)k; }
 };
 
+/* Captures up to 128 bits in registers (a 128-bit shift register, bits
+ * right-aligned): a block is CAVLC-coded once, measured, and its bits kept
+ * across the barrier until their position is known.  over = longer than
+ * 128 bits (re-encode into the buffer then). */
+struct CapSink {
+    uint64_t hi, lo;
+    uint32_t n;
+    __device__ __host__ inline void put(uint32_t v, int k)      /* k <= 32 */
+    {
+        if (k <= 0) return;
+        v &= low_mask(k);
+        hi = (hi << k) | (lo >> (64 - k));
+        lo = (lo << k) | v;
+        n += (uint32_t)k;
+    }
+    __device__ __host__ inline bool over() const { return n > 128; }
+};
+
 /* ORs bits into a zero-initialised word buffer starting at any bit
  * position; OR is the caller's atomic (LDS atomicOr) or plain |= on the
  * CPU.  Words are written once each except the two boundary words. */
@@ -128,6 +146,20 @@ struct OrSink {
     __device__ __host__ inline void finish()
     {
         if (fill > 0 && acc) orw(wi, (uint32_t)(acc >> 32));
+    }
+    /* the n <= 128 bits captured by c, first chunk n mod 32, then words */
+    __device__ __host__ inline void put_cap(const CapSink &c)
+    {
+        int rem = (int)c.n;
+        while (rem > 0) {
+            const int k = ((rem - 1) & 31) + 1, pos = rem - k;
+            uint64_t x;
+            if (pos >= 64) x = c.hi >> (pos - 64);
+            else if (pos == 0) x = c.lo;
+            else x = (c.lo >> pos) | (c.hi << (64 - pos));
+            put((uint32_t)x, k);
+            rem -= k;
+        }
     }
 };
 
@@ -267,6 +299,9 @@ __device__ __host__ inline void fwd4x4(const int x[16], int W[16])
     }
 }
 
+/* zig-zag scan (Table 8-13, frame): scan index -> raster position */
+constexpr int ZZ[16] = {0, 1, 4, 8, 5, 2, 3, 6, 9, 12, 13, 10, 7, 11, 14, 15};
+
 /* raster position pos of a 4x4 block */
 __device__ __host__ inline int quant(int w, int pos)
 {
@@ -293,6 +328,36 @@ __device__ __host__ inline int nc_of(int nA, int nB)
     if (nA >= 0) return nA;
     if (nB >= 0) return nB;
     return 0;
+}
+
+/* level_prefix / level_suffix as ONE field: prefix zeros, '1', suffix
+ * (<= 16 + 12 bits) */
+__device__ __host__ inline void level_field(int code, int sl, uint32_t &v, int &len)
+{
+    int prefix, ssize = sl, suffix = 0;
+    if (sl == 0) {
+        if (code < 14) {
+            prefix = code;
+            ssize = 0;
+        } else if (code < 30) {
+            prefix = 14;
+            ssize = 4;
+            suffix = code - 14;
+        } else {
+            prefix = 15;
+            ssize = 12;
+            suffix = code - 30;
+        }
+    } else if (code < (15 << sl)) {
+        prefix = code >> sl;
+        suffix = code & ((1 << sl) - 1);
+    } else {
+        prefix = 15;
+        ssize = 12;
+        suffix = code - (15 << sl);
+    }
+    v = (1u << ssize) | (uint32_t)suffix;
+    len = prefix + 1 + ssize;
 }
 
 template <class S>
@@ -393,6 +458,80 @@ __device__ __host__ inline int cavlc_block(S &s, const Tabs &T, const C *coef, i
         p = q;
     }
     return tc;
+}
+
+/* The part of a CAVLC block after coeff_token -- trailing-ones signs,
+ * levels, total_zeros, run_before -- which does not depend on nC.  c[]
+ * holds the levels in scan order in registers; the loop is fully unrolled
+ * (static indices, no divergence).  Returns TotalCoeff, t1 in *t1o. */
+template <int MAX, class S>
+__device__ __host__ inline int cavlc_rest(S &s, const Tabs &T, const int *c, int &t1o)
+{
+    uint32_t nz = 0;
+#pragma unroll
+    for (int i = 0; i < MAX; ++i) nz |= (c[i] != 0 ? 1u : 0u) << i;
+    const int tc = __builtin_popcount(nz);
+    int t1 = 0, sl = 0;
+    bool trailing = true;
+#pragma unroll
+    for (int i = MAX - 1; i >= 0; --i) {
+        const int v = c[i];
+        if (v != 0) {
+            if (trailing && t1 < 3 && (v == 1 || v == -1)) {
+                s.put(v < 0 ? 1u : 0u, 1);
+                t1++;
+            } else {
+                int code = v > 0 ? 2 * v - 2 : -2 * v - 1;
+                if (trailing) {                        /* first level */
+                    sl = (tc > 10 && t1 < 3) ? 1 : 0;
+                    if (t1 < 3) code -= 2;
+                    trailing = false;
+                }
+                uint32_t fv;
+                int fl;
+                level_field(code, sl, fv, fl);
+                s.put(fv, fl);
+                if (sl == 0) sl = 1;
+                if ((v < 0 ? -v : v) > (3 << (sl - 1)) && sl < 6) sl++;
+            }
+        }
+    }
+    t1o = t1;
+    if (tc == 0) return 0;
+    const int hi = top_bit(nz);
+    const int tz = hi + 1 - tc;
+    if (tc < MAX) {
+        if (MAX == 4) s.put(T.tzdc_bits[tc - 1][tz], T.tzdc_len[tc - 1][tz]);
+        else s.put(T.tz_bits[tc - 1][tz], T.tz_len[tc - 1][tz]);
+    }
+    int zl = tz, p = hi;
+    uint32_t m = nz;
+    for (int k = 0; k < tc - 1 && zl > 0; ++k) {
+        m &= ~(1u << p);
+        const int q = top_bit(m);
+        const int run = p - q - 1;
+        const int zi = (zl < 7 ? zl : 7) - 1;
+        s.put(T.rb_bits[zi][run], T.rb_len[zi][run]);
+        zl -= run;
+        p = q;
+    }
+    return tc;
+}
+
+/* coeff_token (9.2.1) of (TotalCoeff, TrailingOnes) for nC: (bits, len) */
+__device__ __host__ inline void coeff_token(const Tabs &T, int tc, int t1, int nC, uint32_t &v, int &len)
+{
+    if (nC == -1) {
+        v = T.ctdc_bits[4 * tc + t1];
+        len = T.ctdc_len[4 * tc + t1];
+    } else if (nC >= 8) {
+        v = tc ? (uint32_t)(((tc - 1) << 2) | t1) : 3u;
+        len = 6;
+    } else {
+        const int tb = nC < 2 ? 0 : (nC < 4 ? 1 : 2);
+        v = T.ct_bits[tb][4 * tc + t1];
+        len = T.ct_len[tb][4 * tc + t1];
+    }
 }
 
 /* ---------------------------------------------------------------------- */

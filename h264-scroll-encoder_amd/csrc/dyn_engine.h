@@ -11,7 +11,8 @@
 /* all return 0, or -1 when the launch failed */
 int dyn_launch_stage(hipStream_t hs, int nframes, int S, DevStream *st, const NalDesc *nal,
                      int ld_nal, const PlanPending *pend, DynFrame *dfr, int ld_fr,
-                     const DynGeom *g, const uint8_t *src, const uint8_t *refs, uint8_t *stage);
+                     const DynGeom *g, const uint8_t *src, const uint8_t *refs, uint8_t *stage,
+                     uint64_t *stamps);
 int dyn_launch_emit(hipStream_t hs, int nframes, int S, const DevStream *st, const NalDesc *nal,
                     int ld_nal, const DynFrame *dfr, int ld_fr, const DynGeom *g,
                     const uint8_t *stage, uint8_t *arena, uint64_t ld_arena);

@@ -38,7 +38,8 @@ static_assert(24 * WMB <= 256, "one block task per thread");
 constexpr int WIN = DT;                 /* MBs per window (one MB per thread)    */
 constexpr int HEAD_MAX = 160;           /* bits of one MB head (huge mvd: 2 x 63 + ref) */
 constexpr int HDR_MAX = 1024;           /* slice header bits (8 waypoints + MMCO ~ 250) */
-constexpr int BUF_WORDS = (HDR_MAX + 32 + WMB * MB_BITS_MAX + WIN * HEAD_MAX) / 32 + 4;
+constexpr int BUF_WORDS = 2048;        /* 64 Kbit LDS bit buffer; larger windows take passes */
+static_assert(BUF_WORDS * 32 > HDR_MAX + 64, "the slice header fits one buffer");
 constexpr int OBUF = 6400;              /* k_dyn_emit: 127 carry + 5 + 4096 x 1.5 */
 
 __device__ inline int wave_incl_max(int v, int lane)
@@ -162,41 +163,78 @@ __device__ inline Task task_of(int t, int nd)
 
 struct StageLds {
     uint32_t buf[BUF_WORDS];      /* NAL bits from word `bw` of the slot on       */
-    int16_t lv[WMB][24][16];      /* levels in scan order: luma raster 0..15, AC 16+4p+kk */
     int32_t dcraw[WMB][2][4];     /* chroma DC coefficients before the Hadamard   */
     int16_t dclv[WMB][2][4];
     uint8_t tc[WMB][24];          /* TotalCoeff per 4x4 block                     */
-    int8_t nc[WMB][24];
     uint8_t cbp[WMB];
     uint16_t blen[WMB][26];       /* pieces: luma raster 0..15, DC 16+p, AC 18+4p+kk */
     uint16_t boff[WMB][26];
-    uint32_t mbo[WMB];            /* bit offset of a dynamic MB in the window     */
+    uint32_t exw[WIN];            /* MB lengths: in-wave exclusive prefix         */
+    uint32_t wsum[NW];
     uint8_t ctx[DYN_CTX_MB][8];   /* bottom-row TotalCoeff of rect MBs (row ring) */
     uint8_t lcarry[8];            /* right-column TotalCoeff of the last dyn MB   */
-    uint32_t wsum[NW];
-    int32_t wmax[NW];
     int32_t wo[8], wl[8], wv[8];
-    uint32_t F, bw;
+    int32_t lnz_r, lnz_w;         /* last non-zero staged byte: before / of a flush */
     int32_t general;              /* a half-pel waypoint step was met            */
     Tabs tabs;
 };
 
 constexpr uint32_t DF_OVER = 1u, DF_GENERAL = 2u;   /* DynFrame.err bits */
 
+/* windowed LDS OR: word i of the window's bit stream -> buf[i - lo] when in
+ * [lo, lo + n) (one pass of a window larger than the buffer) */
+struct LdsOrWin {
+    uint32_t *b;
+    uint32_t lo, n;
+    __device__ inline void operator()(uint32_t i, uint32_t v) const
+    {
+        const uint32_t k = i - lo;
+        if (k < n) atomicOr(&b[k], v);
+    }
+};
+typedef OrSink<LdsOrWin> WSink;
+
+__device__ inline int last_nz_byte(uint32_t w)      /* MSB-first byte index, w != 0 */
+{
+    return 3 - (__builtin_ctz(w) >> 3);
+}
+
 /* GENERAL = false: every waypoint step is full-pel (always so for waypoints
  * the composer creates); a NAL that meets a half-pel step is flagged and
- * redone by the GENERAL instantiation, which evaluates the bilinear tree. */
+ * redone by the GENERAL instantiation, which evaluates the bilinear tree.
+ *
+ * Window pipeline (barriers: 4 per window):
+ *   A(i)  block tasks: residual -> transform -> quant -> CAVLC rest (regs);
+ *         flush of window i-1's whole words (staging + EP count)
+ *   B(i)  nC + coeff_token, chroma DC; buffer rewind after the flush
+ *   C(i)  MB heads (regs), cbp, piece offsets, in-wave scan of MB lengths
+ *   D(i)  every piece ORed into the LDS bit buffer at its offset          */
+#ifndef SCROLL_DYN_WAVES
+#define SCROLL_DYN_WAVES 8          /* waves per SIMD the register budget targets */
+#endif
 template <bool GENERAL>
-__global__ __launch_bounds__(DT) void k_dyn_stage(DevStream *__restrict__ st,
+__global__ __launch_bounds__(DT, SCROLL_DYN_WAVES) void k_dyn_stage(DevStream *__restrict__ st,
                                                   const NalDesc *__restrict__ nal, int ld_nal,
                                                   const PlanPending *__restrict__ pend,
                                                   DynFrame *__restrict__ dfr, int ld_fr,
                                                   DynGeom g, const uint8_t *__restrict__ src,
                                                   const uint8_t *__restrict__ refs,
-                                                  uint8_t *__restrict__ stage)
+                                                  uint8_t *__restrict__ stage,
+                                                  uint64_t *__restrict__ stamps)
 {
     __shared__ StageLds L;
+    /* debug: cycles per phase (A B C D, multi-pass), windows, total -> stamps */
+    uint64_t ph[5] = {0, 0, 0, 0, 0}, t_start = 0, t_last = 0, nwin = 0;
+    auto mark = [&](int k) {
+        if (stamps) {
+            const uint64_t now = __builtin_amdgcn_s_memtime();
+            ph[k] += now - t_last;
+            t_last = now;
+        }
+    };
+    if (stamps) t_start = t_last = __builtin_amdgcn_s_memtime();
     const int f = blockIdx.x, s = blockIdx.y, t = threadIdx.x;
+    const int lane = t & 63, wave = t >> 6;
     DevStream *S = st + s;
     DynFrame *DF = dfr + (size_t)s * ld_fr + f;
     const int j = DF->nal;
@@ -204,7 +242,11 @@ __global__ __launch_bounds__(DT) void k_dyn_stage(DevStream *__restrict__ st,
     if (GENERAL && !(DF->err & DF_GENERAL)) return;
 
     const Rect R{g.x0, g.y0, g.w, g.h};
-    if (t == 0) L.general = 0;
+    if (t == 0) {
+        L.general = 0;
+        L.lnz_r = -1;
+        L.lnz_w = -1;
+    }
     if (t < 8) {
         L.wo[t] = pend[s].wo[t];
         L.wl[t] = pend[s].wl[t];
@@ -230,14 +272,18 @@ __global__ __launch_bounds__(DT) void k_dyn_stage(DevStream *__restrict__ st,
     c.wp_valid = L.wv;
     __syncthreads();
 
-    if (t == 0) {                                  /* slice header (h264_writer.c:549-553) */
-        LSink hs{{L.buf}, 0, 0, 0};
-        hs.start(0);
-        emit_slice_header(hs, c);
-        const uint32_t hb = hs.wi * 32u + (uint32_t)hs.fill;
-        hs.finish();
-        L.F = hb;
-        L.bw = 0;
+    /* slice header (h264_writer.c:549-553): thread 0 writes, all count */
+    uint32_t F;
+    {
+        CountSink hc{0};
+        emit_slice_header(hc, c);
+        F = hc.n;
+        if (t == 0) {
+            LSink hs{{L.buf}, 0, 0, 0};
+            hs.start(0);
+            emit_slice_header(hs, c);
+            hs.finish();
+        }
     }
 
     const int w = c.w, h = c.h, mbw = w / 16, mbh = h / 16;
@@ -246,26 +292,51 @@ __global__ __launch_bounds__(DT) void k_dyn_stage(DevStream *__restrict__ st,
     const int nrefs = 2 + c.nwp;
     const WpTab T{L.wo, L.wv, h};
     const uint8_t *rb = refs + (size_t)s * g.ref_ld;
-    const size_t ysz = (size_t)w * h, csz = ysz / 4;
-    RefPics P;
-    P.w = w;
-    P.h = h;
-    for (int i = 0; i < 2; ++i) {
-        P.pl[i][0] = rb + i * (ysz + 2 * csz);
-        P.pl[i][1] = P.pl[i][0] + ysz;
-        P.pl[i][2] = P.pl[i][1] + csz;
-    }
+    const size_t ysz = (size_t)w * h, csz = ysz / 4, pic = ysz + 2 * csz;
     const uint8_t *fs = src + (size_t)s * g.src_ld + (size_t)f * g.src_fr;
     const int lstride = 16 * R.w, cstride = 8 * R.w;
     const uint8_t *fcb = fs + (size_t)256 * R.w * R.h, *fcr = fcb + (size_t)64 * R.w * R.h;
     const int ring = g.ring;
-    uint32_t *out = reinterpret_cast<uint32_t *>(stage + ((size_t)s * ld_fr + f) * g.slot_bytes);
-    const uint32_t cap_words = (uint32_t)(g.slot_bytes / 4) - 4u;
+    uint8_t *slot = stage + ((size_t)s * ld_fr + f) * g.slot_bytes;
+    uint32_t *out = reinterpret_cast<uint32_t *>(slot);
+    /* levels of blocks whose CAVLC rest outgrows the 128-bit capture */
+    int16_t *ovf = reinterpret_cast<int16_t *>(slot + g.slot_bytes - DYN_OVF_BYTES) + 16 * t;
+    const uint32_t cap_words = (uint32_t)((g.slot_bytes - DYN_OVF_BYTES) / 4) - 4u;
     const Tabs &TB = L.tabs;
 
-    int carry = -1;              /* last non-zero RBSP byte flushed so far        */
+    uint32_t bw = 0;             /* staging word of buf[0]                        */
     uint32_t my_ep = 0;
     bool over = false;
+    uint32_t pend_T = 0;         /* bits in buf awaiting the deferred flush (0: none) */
+
+    /* whole words buf[0, n) -> staging words [gw0, gw0 + n), EP insertions
+     * counted with the zero run looked up backwards in buf (L.lnz_r before
+     * buf[0]); the last non-zero byte goes to L.lnz_w */
+    auto flush_words = [&](uint32_t n, uint32_t gw0) {
+        for (uint32_t jw = (uint32_t)t; jw < n; jw += DT) {
+            const uint32_t wv = L.buf[jw];
+            out[gw0 + jw] = __builtin_bswap32(wv);
+            int prev = L.lnz_r;
+            for (int jj = (int)jw - 1; jj >= 0; --jj) {
+                const uint32_t pv = L.buf[jj];
+                if (pv) {
+                    prev = 4 * (int)(gw0 + jj) + last_nz_byte(pv);
+                    break;
+                }
+            }
+            const uint32_t gb = 4u * (gw0 + jw);
+            my_ep += ep_word(wv, gb, 0xffffffffu, prev);
+            if (wv) atomicMax(&L.lnz_w, (int)gb + last_nz_byte(wv));
+        }
+    };
+    /* after a flush: carry the last non-zero byte forward */
+    auto rewind_lnz = [&]() {
+        if (t == 0) {
+            L.lnz_r = max(L.lnz_r, L.lnz_w);
+            L.lnz_w = -1;
+        }
+    };
+
     const int nmb = mbw * mbh, ndt = R.w * R.h;
     for (int m0 = 0; m0 < nmb;) {
         const int q0 = dyn_rank(R, mbw, m0);
@@ -273,8 +344,19 @@ __global__ __launch_bounds__(DT) void k_dyn_stage(DevStream *__restrict__ st,
         if (q0 + WMB < ndt) m1 = min(m1, dyn_mb(R, mbw, q0 + WMB));
         const int nd = dyn_rank(R, mbw, m1) - q0;
         const int nm = m1 - m0;
+        nwin++;
 
-        /* A: residual -> levels, TotalCoeff (one 4x4 block per thread) */
+        /* A: the previous window's whole words -> staging; then residual ->
+         * transform -> levels (registers) -> the nC-independent part of the
+         * block's CAVLC (cavlc_rest) captured in registers until D */
+        const uint32_t pnf = pend_T >> 5;
+        uint32_t part = 0;
+        if (pend_T) {
+            flush_words(pnf, bw);
+            part = L.buf[pnf];
+        }
+        CapSink bcap{0, 0, 0}, dcap{0, 0, 0};
+        int bt1 = 0;
         if (t < 24 * nd) {
             const Task q = task_of(t, nd);
             const int m = dyn_mb(R, mbw, q0 + q.k), row = m / mbw, col = m - row * mbw;
@@ -290,20 +372,19 @@ __global__ __launch_bounds__(DT) void k_dyn_stage(DevStream *__restrict__ st,
                     const uint32_t sv = ld32(sp + (size_t)i * lstride);
                     int yo;
                     const int b = luma_row(T, ref, Y + i + mvp, yo);
-                    const uint32_t pv = ld32(P.pl[b][0] + (size_t)yo * w + X);
+                    const uint32_t pv = ld32(rb + (size_t)b * pic + (size_t)yo * w + X);
 #pragma unroll
                     for (int x = 0; x < 4; ++x)
                         res[4 * i + x] = (int)((sv >> (8 * x)) & 255u) - (int)((pv >> (8 * x)) & 255u);
                 }
                 fwd4x4(res, W);
-                int n = 0;
+                int cf[16];
 #pragma unroll
-                for (int k2 = 0; k2 < 16; ++k2) {
-                    const int zp = TB.zz[k2];
-                    const int v = quant(W[zp], zp);
-                    L.lv[q.k][q.blk][k2] = (int16_t)v;
-                    n += v != 0;
-                }
+                for (int k2 = 0; k2 < 16; ++k2) cf[k2] = quant(W[ZZ[k2]], ZZ[k2]);
+                const int n = cavlc_rest<16>(bcap, TB, cf, bt1);
+                if (bcap.over())
+#pragma unroll
+                    for (int k2 = 0; k2 < 16; ++k2) ovf[k2] = (int16_t)cf[k2];
                 L.tc[q.k][q.blk] = (uint8_t)n;
                 if (q.by == 3) L.ctx[(ry % ring) * R.w + cx][q.bx] = (uint8_t)n;
             } else {
@@ -324,8 +405,9 @@ __global__ __launch_bounds__(DT) void k_dyn_stage(DevStream *__restrict__ st,
                         L.general = 1;
                         pred[0] = pred[1] = pred[2] = pred[3] = 0;
                     } else if (ba >= 0 && bb >= 0) {
-                        const uint32_t av = ld32(P.pl[ba][1 + q.p] + (size_t)yoa * cw + X);
-                        const uint32_t bv = fr ? ld32(P.pl[bb][1 + q.p] + (size_t)yob * cw + X) : 0u;
+                        const uint8_t *cp = rb + ysz + (size_t)q.p * csz + X;
+                        const uint32_t av = ld32(cp + (size_t)ba * pic + (size_t)yoa * cw);
+                        const uint32_t bv = fr ? ld32(cp + (size_t)bb * pic + (size_t)yob * cw) : 0u;
 #pragma unroll
                         for (int x = 0; x < 4; ++x) {
                             const int a = (int)((av >> (8 * x)) & 255u), b = (int)((bv >> (8 * x)) & 255u);
@@ -333,6 +415,14 @@ __global__ __launch_bounds__(DT) void k_dyn_stage(DevStream *__restrict__ st,
                         }
                     } else {                       /* half-pel waypoint step: general path */
                         if constexpr (GENERAL) {
+                            RefPics P;
+                            P.w = w;
+                            P.h = h;
+                            for (int i2 = 0; i2 < 2; ++i2) {
+                                P.pl[i2][0] = rb + i2 * pic;
+                                P.pl[i2][1] = P.pl[i2][0] + ysz;
+                                P.pl[i2][2] = P.pl[i2][1] + csz;
+                            }
                             for (int x = 0; x < 4; ++x) {
                                 const int a = chroma_px_any<9>(T, P, ref, 1 + q.p, X + x, ya);
                                 const int b = fr ? chroma_px_any<9>(T, P, ref, 1 + q.p, X + x, ya + 1) : 0;
@@ -345,25 +435,35 @@ __global__ __launch_bounds__(DT) void k_dyn_stage(DevStream *__restrict__ st,
                 }
                 fwd4x4(res, W);
                 L.dcraw[q.k][q.p][2 * q.by + q.bx] = W[0];
-                int n = 0;
+                int cf[15];
 #pragma unroll
-                for (int k2 = 1; k2 < 16; ++k2) {
-                    const int zp = TB.zz[k2];
-                    const int v = quant(W[zp], zp);
-                    L.lv[q.k][q.blk][k2 - 1] = (int16_t)v;
-                    n += v != 0;
-                }
+                for (int k2 = 1; k2 < 16; ++k2) cf[k2 - 1] = quant(W[ZZ[k2]], ZZ[k2]);
+                const int n = cavlc_rest<15>(bcap, TB, cf, bt1);
+                if (bcap.over())
+#pragma unroll
+                    for (int k2 = 0; k2 < 15; ++k2) ovf[k2] = (int16_t)cf[k2];
                 L.tc[q.k][q.blk] = (uint8_t)n;
                 if (q.by == 1) L.ctx[(ry % ring) * R.w + cx][4 + 2 * q.p + q.bx] = (uint8_t)n;
             }
         }
         __syncthreads();
+        mark(0);
         if (!GENERAL && L.general) {                /* uniform: read after the barrier */
             if (t == 0) DF->err = DF_GENERAL;
             return;
         }
 
-        /* B: nC, coded flags, CAVLC lengths; chroma DC Hadamard + quant */
+        /* B: buffer rewind after the flush; nC, coded flags, coeff_token;
+         * chroma DC Hadamard + quant + CAVLC */
+        if (pend_T) {
+            for (uint32_t jw = (uint32_t)t; jw <= pnf; jw += DT) L.buf[jw] = jw == 0 ? part : 0u;
+            rewind_lnz();
+            F = pend_T & 31u;
+            bw += pnf;
+            pend_T = 0;
+        }
+        uint32_t tokv = 0;
+        int tokl = 0;
         if (t < 24 * nd) {
             const Task q = task_of(t, nd);
             const int m = dyn_mb(R, mbw, q0 + q.k), row = m / mbw, col = m - row * mbw;
@@ -394,14 +494,9 @@ __global__ __launch_bounds__(DT) void k_dyn_stage(DevStream *__restrict__ st,
                 coded = any != 0;
             }
             const int nC = nc_of(nA, nB);
-            L.nc[q.k][q.blk] = (int8_t)nC;
-            uint32_t bl = 0;
-            if (coded) {
-                CountSink cs{0};
-                cavlc_block(cs, TB, L.lv[q.k][q.blk], q.luma ? 16 : 15, nC);
-                bl = cs.n;
-            }
-            L.blen[q.k][q.luma ? q.blk : 18 + (q.blk - 16)] = (uint16_t)bl;
+            if (coded) coeff_token(TB, tc[q.blk], bt1, nC, tokv, tokl);
+            L.blen[q.k][q.luma ? q.blk : 18 + (q.blk - 16)] =
+                coded ? (uint16_t)(tokl + (int)bcap.n) : (uint16_t)0;
         }
         if (t < 2 * nd) {
             const int k = t >> 1, p = t & 1;
@@ -413,15 +508,16 @@ __global__ __launch_bounds__(DT) void k_dyn_stage(DevStream *__restrict__ st,
             o[1] = (int16_t)quant_dc(f01);
             o[2] = (int16_t)quant_dc(f10);
             o[3] = (int16_t)quant_dc(f11);
-            CountSink cs{0};
-            cavlc_block(cs, TB, o, 4, -1);
-            L.blen[k][16 + p] = (uint16_t)cs.n;
+            cavlc_block(dcap, TB, o, 4, -1);
+            L.blen[k][16 + p] = (uint16_t)dcap.n;
         }
         __syncthreads();
+        mark(1);
 
-        /* C: MB lengths, piece offsets, window scan */
+        /* C: MB heads, cbp, piece offsets; in-wave scan of the MB lengths */
         uint32_t mlen = 0;
         int kd = -1, ref = 0, mv4 = 0, px = 0, py = 0, code = 0, cbp = 0;
+        CapSink mcap{0, 0, 0};
         if (t < nm) {
             const int m = m0 + t, row = m / mbw, col = m - row * mbw;
             const bool curA = row < a_end, abvA = (row - 1) < a_end;
@@ -429,11 +525,11 @@ __global__ __launch_bounds__(DT) void k_dyn_stage(DevStream *__restrict__ st,
             mv4 = 4 * (curA ? rg.mva : rg.mvb);
             const int aref = abvA ? rg.ra : rg.rb, amv4 = 4 * (abvA ? rg.mva : rg.mvb);
             predict(col, row, mbw, ref, mv4, aref, amv4, px, py);
-            CountSink cs{0};
-            put_mb_head(cs, ref, 0 - px, mv4 - py, nrefs);
+            put_mb_head(mcap, ref, 0 - px, mv4 - py, nrefs);
             const bool isdyn = col >= R.x0 && col < R.x0 + R.w && row >= R.y0 && row < R.y0 + R.h;
             if (!isdyn) {
-                mlen = cs.n + 1u;                  /* + coded_block_pattern ue(0) */
+                mcap.put(1, 1);                    /* coded_block_pattern ue(0) */
+                mlen = mcap.n;
             } else {
                 kd = dyn_rank(R, mbw, m) - q0;
                 const uint8_t *tc = L.tc[kd];
@@ -454,8 +550,9 @@ __global__ __launch_bounds__(DT) void k_dyn_stage(DevStream *__restrict__ st,
                 cbp = cbp_l | (cbp_c << 4);
                 code = TB.cbp_code[cbp];
                 L.cbp[kd] = (uint8_t)cbp;
-                const uint32_t uel = 2u * (31u - (uint32_t)__clz(code + 1)) + 1u;
-                uint32_t off = cs.n + uel + (cbp ? 1u : 0u);
+                put_ue(mcap, (uint32_t)code);
+                if (cbp) put_se(mcap, 0);          /* mb_qp_delta */
+                uint32_t off = mcap.n;
                 for (int blk = 0; blk < 16; ++blk) {
                     const int r = blk_raster(blk);
                     L.boff[kd][r] = (uint16_t)off;
@@ -476,101 +573,140 @@ __global__ __launch_bounds__(DT) void k_dyn_stage(DevStream *__restrict__ st,
                 mlen = off;
             }
         }
-        uint32_t mo, wtot;
-        block_excl_sum(mlen, L.wsum, mo, wtot);
-        if (kd >= 0) L.mbo[kd] = mo;
-        __syncthreads();
-
-        /* D: bits -> LDS buffer */
-        const uint32_t F = L.F, bw = L.bw;
-        if (t < nm) {
-            LSink sk{{L.buf}, 0, 0, 0};
-            sk.start(F + mo);
-            if (kd < 0) {
-                put_mb(sk, ref, 0 - px, mv4 - py, nrefs);
-            } else {
-                put_mb_head(sk, ref, 0 - px, mv4 - py, nrefs);
-                put_ue(sk, (uint32_t)code);
-                if (cbp) put_se(sk, 0);            /* mb_qp_delta */
-            }
-            sk.finish();
-        }
-        if (t < 24 * nd) {
-            const Task q = task_of(t, nd);
-            const int pc = q.luma ? q.blk : 18 + (q.blk - 16);
-            if (L.blen[q.k][pc]) {
-                LSink sk{{L.buf}, 0, 0, 0};
-                sk.start(F + L.mbo[q.k] + L.boff[q.k][pc]);
-                cavlc_block(sk, TB, L.lv[q.k][q.blk], q.luma ? 16 : 15, (int)L.nc[q.k][q.blk]);
-                sk.finish();
-            }
-        }
-        if (t < 2 * nd) {
-            const int k = t >> 1, p = t & 1;
-            if (L.cbp[k] >> 4) {
-                LSink sk{{L.buf}, 0, 0, 0};
-                sk.start(F + L.mbo[k] + L.boff[k][16 + p]);
-                cavlc_block(sk, TB, L.dclv[k][p], 4, -1);
-                sk.finish();
-            }
+        {
+            const uint32_t incl = wave_incl_sum(mlen, lane);
+            L.exw[t] = incl - mlen;
+            if (lane == 63) L.wsum[wave] = incl;
         }
         __syncthreads();
-
-        /* E: flush whole words to the staging slot, count EP insertions */
-        const uint32_t Tb = F + wtot, nfull = Tb >> 5;
-        if (bw + nfull + 2u > cap_words) {
+        mark(2);
+        uint32_t wtot = 0, wpre[NW];
+#pragma unroll
+        for (int w2 = 0; w2 < NW; ++w2) {
+            wpre[w2] = wtot;
+            wtot += L.wsum[w2];
+        }
+        /* offset of MB u of the window */
+        auto mbo = [&](int u) -> uint32_t {
+            uint32_t pre = 0;
+#pragma unroll
+            for (int w2 = 0; w2 < NW; ++w2)
+                if (w2 == (u >> 6)) pre = wpre[w2];
+            return pre + L.exw[u];
+        };
+        const uint32_t Tb = F + wtot;
+        if (bw + (Tb >> 5) + 2u > cap_words) {      /* uniform */
             over = true;
             break;
         }
-        for (uint32_t base = 0; base < nfull; base += DT) {
-            const uint32_t jw = base + (uint32_t)t;
-            const bool v = jw < nfull;
-            const uint32_t wv = v ? L.buf[jw] : 0u;
-            const uint32_t gb = 4u * (bw + jw);
-            int lnz = -1;
-            if (v) {
-                out[bw + jw] = __builtin_bswap32(wv);
+
+        /* D: every piece ORed into the buffer; a window larger than the
+         * buffer is written and flushed in passes of BUF_WORDS - 1 words */
+        const uint32_t nw = (Tb + 31) >> 5;
+        const bool single = nw <= (uint32_t)BUF_WORDS;
+        const uint32_t PW = single ? (uint32_t)BUF_WORDS : (uint32_t)BUF_WORDS - 1u;
+        const uint32_t my_mbo = t < nm ? mbo(t) : 0u;
+        for (uint32_t p0 = 0; p0 < nw; p0 += PW) {
+            const LdsOrWin win{L.buf, p0, PW};
+            if (t < nm) {
+                WSink sk{win, 0, 0, 0};
+                sk.start(F + my_mbo);
+                if (!mcap.over()) {
+                    sk.put_cap(mcap);
+                } else if (kd < 0) {               /* > 128-bit head: huge mvd */
+                    put_mb(sk, ref, 0 - px, mv4 - py, nrefs);
+                } else {
+                    put_mb_head(sk, ref, 0 - px, mv4 - py, nrefs);
+                    put_ue(sk, (uint32_t)code);
+                    if (cbp) put_se(sk, 0);
+                }
+                sk.finish();
+            }
+            if (t < 24 * nd && tokl) {
+                const Task q = task_of(t, nd);
+                const int pc = q.luma ? q.blk : 18 + (q.blk - 16);
+                WSink sk{win, 0, 0, 0};
+                sk.start(F + mbo(dyn_mb(R, mbw, q0 + q.k) - m0) + L.boff[q.k][pc]);
+                sk.put(tokv, tokl);
+                if (!bcap.over()) {
+                    sk.put_cap(bcap);
+                } else {                           /* > 128 bits: re-encode */
+                    int cf[16], t1d;
 #pragma unroll
-                for (int i = 0; i < 4; ++i)
-                    if ((wv >> (24 - 8 * i)) & 255u) lnz = (int)(gb + (uint32_t)i);
+                    for (int k2 = 0; k2 < 16; ++k2) cf[k2] = k2 < 15 || q.luma ? (int)ovf[k2] : 0;
+                    if (q.luma) cavlc_rest<16>(sk, TB, cf, t1d);
+                    else cavlc_rest<15>(sk, TB, cf, t1d);
+                }
+                sk.finish();
             }
-            int ex, tot;
-            block_excl_max(lnz, L.wmax, ex, tot);
-            if (v) {
-                int prev = max(carry, ex);
-                my_ep += ep_word(wv, gb, 0xffffffffu, prev);
+            if (t < 2 * nd) {
+                const int k = t >> 1, p = t & 1;
+                if (L.cbp[k] >> 4) {
+                    WSink sk{win, 0, 0, 0};
+                    sk.start(F + mbo(dyn_mb(R, mbw, q0 + k) - m0) + L.boff[k][16 + p]);
+                    if (!dcap.over()) sk.put_cap(dcap);
+                    else cavlc_block(sk, TB, L.dclv[k][p], 4, -1);
+                    sk.finish();
+                }
             }
-            carry = max(carry, tot);
+            if (nd > 0 && t < 8) {                 /* left context of the next window */
+                const uint8_t *tc = L.tc[nd - 1];
+                L.lcarry[t] = t < 4 ? tc[4 * t + 3] : tc[16 + 4 * ((t - 4) >> 1) + 2 * ((t - 4) & 1) + 1];
+            }
+            __syncthreads();
+            if (single) {
+                pend_T = Tb;                       /* flushed during the next A */
+            } else {                               /* rare: flush this pass now */
+                const uint32_t nfull = Tb >> 5;
+                const uint32_t n = p0 < nfull ? min(PW, nfull - p0) : 0u;
+                flush_words(n, bw + p0);
+                const uint32_t lastp = (Tb & 31u) && nfull - p0 < PW ? L.buf[nfull - p0] : 0u;
+                __syncthreads();
+                rewind_lnz();
+                for (uint32_t jw = (uint32_t)t; jw < (uint32_t)BUF_WORDS; jw += DT)
+                    L.buf[jw] = jw == 0 && p0 + PW >= nw ? lastp : 0u;
+                __syncthreads();
+            }
         }
-        const uint32_t part = L.buf[nfull];
-        __syncthreads();
-        for (uint32_t jw = (uint32_t)t; jw <= nfull; jw += DT) L.buf[jw] = jw == 0 ? part : 0u;
-        if (nd > 0 && t < 8) {
-            const uint8_t *tc = L.tc[nd - 1];
-            L.lcarry[t] = t < 4 ? tc[4 * t + 3] : tc[16 + 4 * ((t - 4) >> 1) + 2 * ((t - 4) & 1) + 1];
+        if (!single) {
+            bw += Tb >> 5;
+            F = Tb & 31u;
         }
-        if (t == 0) {
-            L.F = Tb & 31u;
-            L.bw = bw + nfull;
-        }
-        __syncthreads();
+        mark(3);
         m0 = m1;
     }
 
     if (!over) {
+        if (pend_T) {                              /* the last window's whole words */
+            const uint32_t pnf = pend_T >> 5;
+            flush_words(pnf, bw);
+            const uint32_t part = L.buf[pnf];
+            __syncthreads();
+            rewind_lnz();
+            if (t == 0) L.buf[0] = part;
+            F = pend_T & 31u;
+            bw += pnf;
+            __syncthreads();
+        }
         /* rbsp_stop_one_bit + alignment (bitwriter.c:103-111); F < 32 */
         if (t == 0) {
-            const uint32_t F = L.F, bw = L.bw;
             const uint32_t wv = L.buf[0] | (1u << (31 - F));
             const uint32_t nb = (F + 1u + 7u) >> 3;
             out[bw] = __builtin_bswap32(wv);
-            int prev = carry;
+            int prev = L.lnz_r;
             my_ep += ep_word(wv, 4u * bw, 4u * bw + nb, prev);
             DF->rbsp_bytes = 4u * bw + nb;
         }
     }
     uint32_t ex, tot;
     block_excl_sum(my_ep, L.wsum, ex, tot);
+    if (stamps && t == 0) {
+        uint64_t *o = stamps + ((size_t)s * gridDim.x + f) * 8;
+        for (int k = 0; k < 5; ++k) o[k] = ph[k];
+        o[5] = nwin;
+        o[6] = __builtin_amdgcn_s_memtime() - t_start;
+        o[7] = (uint64_t)(uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 4);     /* HW_ID */
+    }
     if (t == 0) {
         DF->ep = tot;
         DF->err = over ? DF_OVER : 0u;
@@ -715,14 +851,15 @@ __global__ __launch_bounds__(256) void k_dyn_synth(uint8_t *__restrict__ src, Dy
 /* ---------------------------------------------------------------------- */
 int dyn_launch_stage(hipStream_t hs, int nframes, int S, DevStream *st, const NalDesc *nal,
                      int ld_nal, const PlanPending *pend, DynFrame *dfr, int ld_fr,
-                     const DynGeom *g, const uint8_t *src, const uint8_t *refs, uint8_t *stage)
+                     const DynGeom *g, const uint8_t *src, const uint8_t *refs, uint8_t *stage,
+                     uint64_t *stamps)
 {
     if (nframes <= 0 || S <= 0) return 0;
     hipLaunchKernelGGL(k_dyn_stage<false>, dim3(nframes, S), dim3(DT), 0, hs, st, nal, ld_nal, pend,
-                       dfr, ld_fr, *g, src, refs, stage);
+                       dfr, ld_fr, *g, src, refs, stage, stamps);
     if (hipGetLastError() != hipSuccess) return -1;
     hipLaunchKernelGGL(k_dyn_stage<true>, dim3(nframes, S), dim3(DT), 0, hs, st, nal, ld_nal, pend,
-                       dfr, ld_fr, *g, src, refs, stage);
+                       dfr, ld_fr, *g, src, refs, stage, (uint64_t *)nullptr);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -752,5 +889,5 @@ size_t dyn_slot_bound(int mbw, int mbh, int rw, int rh)
      * maximum + the stop word + k_dyn_stage's 16-byte margin */
     const size_t bits = (size_t)HDR_MAX + (size_t)mbw * mbh * (HEAD_MAX + 1) +
                         (size_t)rw * rh * MB_BITS_MAX + 64;
-    return ((bits / 8 + 32) + 255) & ~(size_t)255;
+    return ((bits / 8 + 32 + DYN_OVF_BYTES) + 255) & ~(size_t)255;
 }

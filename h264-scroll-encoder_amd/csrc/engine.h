@@ -79,6 +79,7 @@ typedef struct {
 #define DYN_MAX_W 128               /* rect width limit (MBs)                     */
 #define DYN_CTX_MB 400              /* TotalCoeff row-ring entries (LDS)          */
 #define DYN_WINDOW_MBS 10           /* dynamic MBs per k_dyn_stage window         */
+#define DYN_OVF_BYTES 8192          /* staging-slot tail: levels of > 128-bit blocks */
 typedef struct {
     int32_t x0, y0, w, h;           /* rect, MB units                             */
     int32_t ring;                   /* rows in the TotalCoeff ring                */

@@ -1157,8 +1157,19 @@ static int launch(ScrollBatch *b, int nframes, int plan_mode, int nal_max, hipSt
                            ld_fr);
         HIPCHK(hipGetLastError());
         if ((rc = mark(1))) return rc;
+        uint64_t *stamps = nullptr;
+        if (b->debug & SCROLL_DEBUG_DYN_STAMPS) {
+            const size_t slots = (size_t)nframes * S;
+            if (slots > b->dbg_slots) {
+                if (b->d_dbg) (void)hipFree(b->d_dbg);
+                HIPCHK(hipMalloc(&b->d_dbg, slots * 8 * sizeof(uint64_t)));
+                b->dbg_slots = slots;
+            }
+            HIPCHK(hipMemsetAsync(b->d_dbg, 0, slots * 8 * sizeof(uint64_t), hs));
+            stamps = b->d_dbg;
+        }
         if (dyn_launch_stage(hs, nframes, S, b->d_st, b->d_nal, b->ld_nal, b->d_pend, b->d_dfr,
-                             ld_fr, &b->geo, b->d_src, b->d_refs, b->d_stage)) {
+                             ld_fr, &b->geo, b->d_src, b->d_refs, b->d_stage, stamps)) {
             set_err("k_dyn_stage launch: %s", hipGetErrorString(hipGetLastError()));
             return SCROLL_ERR_HIP;
         }
@@ -1441,7 +1452,7 @@ int scroll_batch_set_dyn_rect(ScrollBatch *b, int x0, int y0, int w, int h, size
     g.src_fr = (uint64_t)384 * w * h;
     g.src_ld = round256((size_t)b->max_frames * g.src_fr);
     g.ref_ld = 0;
-    g.slot_bytes = slot_bytes ? round256(slot_bytes) : dyn_slot_bound(mbw, mbh, w, h);
+    g.slot_bytes = slot_bytes ? round256(slot_bytes + DYN_OVF_BYTES) : dyn_slot_bound(mbw, mbh, w, h);
     b->dyn_pw = pw;
     b->dyn_ph = ph;
     const size_t S = (size_t)b->max_streams, F = (size_t)b->max_frames;

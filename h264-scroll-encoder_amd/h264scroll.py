@@ -31,6 +31,7 @@ SCROLL_DEBUG_EMIT_NOPURE = 16
 SCROLL_DEBUG_EMIT_NOMIXED = 32
 SCROLL_DEBUG_EMIT_STAMPS = 64
 SCROLL_DEBUG_EMIT_NOBYTES = 128
+SCROLL_DEBUG_DYN_STAMPS = 256
 SCROLL_COMPOSE_REWIND = 1
 MAX_WAYPOINTS = 8
 MV_LIMIT_PX = 496

@@ -58,6 +58,7 @@ extern "C" {
 #define SCROLL_DEBUG_EMIT_NOMIXED 32 /* k_emit skips the mixed-chunk phase        */
 #define SCROLL_DEBUG_EMIT_STAMPS 64 /* k_emit records s_memtime per phase per wave */
 #define SCROLL_DEBUG_EMIT_NOBYTES 128 /* k_emit skips the tile-end partial chunks  */
+#define SCROLL_DEBUG_DYN_STAMPS 256 /* k_dyn_stage: s_memtime per phase per NAL   */
 
 typedef struct ScrollBatch ScrollBatch;
 

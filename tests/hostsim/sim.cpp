@@ -285,4 +285,35 @@ int sim_ep_count(const uint8_t *b, int n)
     return c;
 }
 
+/* the kernels' split form: coeff_token (phase B) + cavlc_rest (phase A,
+ * register levels); must equal cavlc_block bit for bit */
+long sim_cavlc_split(const int *coef, int max, int nC, int start, uint32_t *words, int *tc_out)
+{
+    dyn::CapSink cap{0, 0, 0};
+    int t1 = 0, tc = 0;
+    int c[16];
+    for (int i = 0; i < 16; ++i) c[i] = i < max ? coef[i] : 0;
+    if (max == 16) tc = dyn::cavlc_rest<16>(cap, g_dyn_tabs, c, t1);
+    else if (max == 15) tc = dyn::cavlc_rest<15>(cap, g_dyn_tabs, c, t1);
+    else tc = dyn::cavlc_rest<4>(cap, g_dyn_tabs, c, t1);
+    uint32_t tv;
+    int tl;
+    dyn::coeff_token(g_dyn_tabs, tc, t1, nC, tv, tl);
+    dyn::OrSink<HostOr> os{{words}, 0, 0, 0};
+    os.start((uint32_t)start);
+    os.put(tv, tl);
+    if (cap.over()) {
+        if (max == 16) dyn::cavlc_rest<16>(os, g_dyn_tabs, c, t1);
+        else if (max == 15) dyn::cavlc_rest<15>(os, g_dyn_tabs, c, t1);
+        else dyn::cavlc_rest<4>(os, g_dyn_tabs, c, t1);
+    } else {
+        os.put_cap(cap);
+    }
+    const uint32_t end = os.wi * 32u + (uint32_t)os.fill;
+    os.finish();
+    *tc_out = tc;
+    if (end - (uint32_t)start != (uint32_t)tl + cap.n) return -1;
+    return (long)(end - (uint32_t)start);
+}
+
 }  // extern "C"

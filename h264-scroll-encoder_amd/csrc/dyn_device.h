@@ -104,11 +104,10 @@ struct CountSink {
 struct CapSink {
     uint64_t hi, lo;
     uint32_t n;
-    __device__ __host__ inline void put(uint32_t v, int k)      /* k <= 32 */
+    __device__ __host__ inline void put(uint32_t v, int k)      /* 0 <= k <= 32, branch-free */
     {
-        if (k <= 0) return;
         v &= low_mask(k);
-        hi = (hi << k) | (lo >> (64 - k));
+        hi = (hi << k) | ((lo >> 1) >> (63 - k));
         lo = (lo << k) | v;
         n += (uint32_t)k;
     }
@@ -307,15 +306,15 @@ __device__ __host__ inline int quant(int w, int pos)
 {
     const int i = pos >> 2, j = pos & 3;
     const int mf = ((i | j) & 1) == 0 ? MF0 : (((i & j) & 1) ? MF1 : MF2);
-    const int a = w < 0 ? -w : w;
-    const int z = (a * mf + QF) >> QBITS;             /* |w| <= 9180: no overflow */
+    const int a = w < 0 ? -w : w;                     /* |w| <= 9180, mf < 2^14: 24-bit multiply */
+    const int z = (int)((__umul24((uint32_t)a, (uint32_t)mf) + (uint32_t)QF) >> QBITS);
     return w < 0 ? -z : z;
 }
 
 __device__ __host__ inline int quant_dc(int w)
 {
-    const int a = w < 0 ? -w : w;
-    const int z = (a * MF0 + 2 * QF) >> (QBITS + 1);  /* |w| <= 16320 */
+    const int a = w < 0 ? -w : w;                     /* |w| <= 16320 */
+    const int z = (int)((__umul24((uint32_t)a, (uint32_t)MF0) + 2u * QF) >> (QBITS + 1));
     return w < 0 ? -z : z;
 }
 
@@ -534,6 +533,205 @@ __device__ __host__ inline void coeff_token(const Tabs &T, int tc, int t1, int n
     }
 }
 
+/* CAVLC tables packed (len << 8 | bits) for one LDS read per field */
+struct PTabs {
+    uint16_t ct[4][68];           /* [0..2]: nC tables, [3]: chroma DC (nC = -1) */
+    uint16_t tz[15][16];
+    uint16_t tzdc[3][4];
+    uint16_t rb[7][16];
+};
+
+__device__ __host__ inline void build_ptabs(const Tabs &T, PTabs &P, int tid, int nthr)
+{
+    for (int i = tid; i < 3 * 68; i += nthr)
+        P.ct[i / 68][i % 68] = (uint16_t)(T.ct_len[i / 68][i % 68] << 8 | T.ct_bits[i / 68][i % 68]);
+    for (int i = tid; i < 68; i += nthr)
+        P.ct[3][i] = i < 20 ? (uint16_t)(T.ctdc_len[i] << 8 | T.ctdc_bits[i]) : (uint16_t)0;
+    for (int i = tid; i < 15 * 16; i += nthr)
+        P.tz[i / 16][i % 16] = (uint16_t)(T.tz_len[i / 16][i % 16] << 8 | T.tz_bits[i / 16][i % 16]);
+    for (int i = tid; i < 12; i += nthr)
+        P.tzdc[i / 4][i % 4] = (uint16_t)(T.tzdc_len[i / 4][i % 4] << 8 | T.tzdc_bits[i / 4][i % 4]);
+    for (int i = tid; i < 7 * 16; i += nthr)
+        P.rb[i / 16][i % 16] = i % 16 < 15 ? (uint16_t)(T.rb_len[i / 16][i % 16] << 8 | T.rb_bits[i / 16][i % 16])
+                                           : (uint16_t)0;
+}
+
+/* level_prefix / level_suffix as one field, branch-free (9.2.2.1) */
+__device__ __host__ inline void level_field_bf(int code, int sl, uint32_t &v, int &len)
+{
+    const bool s0 = sl == 0;
+    const int lim = s0 ? 14 : (15 << sl);
+    int prefix = code >> sl, ssize = sl, suffix = code & ((1 << sl) - 1);
+    const bool mid = s0 && code >= 14 && code < 30;        /* level_prefix 14, 4-bit suffix */
+    const bool esc = s0 ? code >= 30 : code >= lim;        /* level_prefix 15, 12-bit suffix */
+    prefix = mid ? 14 : (esc ? 15 : prefix);
+    ssize = mid ? 4 : (esc ? 12 : ssize);
+    suffix = mid ? code - 14 : (esc ? code - (s0 ? 30 : lim) : suffix);
+    v = (1u << ssize) | (uint32_t)suffix;
+    len = prefix + 1 + ssize;
+}
+
+/* A whole CAVLC residual block (coeff_token .. run_before) of MAX levels
+ * held as packed int8 (scan order, pk[i >> 2] byte i & 3), in one loop
+ * over the NON-ZERO levels only, branch-free inside: the wave iterates
+ * max TotalCoeff of its lanes (callers group blocks by TotalCoeff).  All
+ * bits go to cap (token, signs / levels, total_zeros, runs); run_before
+ * codes gather in a 64-bit side register first.  Returns TotalCoeff;
+ * *ok = false when cap or the run register overflowed (cap.n is still the
+ * exact length). */
+template <int MAX, class CAP>
+__device__ __host__ inline int cavlc_nz(CAP &cap, const PTabs &P, const uint32_t pk[4], int nC, bool &ok)
+{
+    uint32_t nz = 0;
+#pragma unroll
+    for (int i = 0; i < MAX; ++i) nz |= (((pk[i >> 2] >> (8 * (i & 3))) & 255u) != 0 ? 1u : 0u) << i;
+    const int tc = __builtin_popcount(nz);
+    auto lev = [&](int p) -> int {                         /* three selects + bfe */
+        const uint32_t w01 = (p & 4) ? pk[1] : pk[0], w23 = (p & 4) ? pk[3] : pk[2];
+        const uint32_t wv = (p & 8) ? w23 : w01;
+        return (int)(int8_t)(uint8_t)(wv >> (8 * (p & 3)));
+    };
+    /* trailing ones: the top <= 3 non-zero levels while they are +-1 */
+    int t1 = 0;
+    {
+        uint32_t m = nz;
+        bool run = true;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const int p = m ? top_bit(m) : 0;
+            const int v = m ? lev(p) : 0;
+            run = run && m && (v == 1 || v == -1);
+            t1 += run ? 1 : 0;
+            m &= m ? ~(1u << p) : ~0u;
+        }
+    }
+    {
+        const int tb = nC < 0 ? 3 : (nC < 2 ? 0 : (nC < 4 ? 1 : 2));
+        uint32_t tv;
+        int tl;
+        if (nC >= 8) {
+            tv = tc ? (uint32_t)(((tc - 1) << 2) | t1) : 3u;
+            tl = 6;
+        } else {
+            const uint32_t e = P.ct[tb][4 * tc + t1];
+            tv = e & 255u;
+            tl = (int)(e >> 8);
+        }
+        cap.put(tv, tl);
+    }
+    ok = true;
+    if (tc == 0) return 0;
+    const int hi = top_bit(nz);
+    const int tz = hi + 1 - tc;
+    uint64_t runs = 0;
+    int rn = 0, zl = tz, sl = (tc > 10 && t1 < 3) ? 1 : 0, pprev = hi;
+    uint32_t m = nz;
+    for (int k = 0; k < tc; ++k) {
+        const int p = top_bit(m);
+        m &= ~(1u << p);
+        const int v = lev(p);
+        const int a = v < 0 ? -v : v;
+        const bool sgn = k < t1;
+        int code = 2 * a - 2 + (v < 0 ? 1 : 0);
+        code -= (k == t1 && t1 < 3) ? 2 : 0;
+        uint32_t fv;
+        int fl;
+        level_field_bf(code, sl, fv, fl);
+        cap.put(sgn ? (v < 0 ? 1u : 0u) : fv, sgn ? 1 : fl);
+        const int s1 = sl == 0 ? 1 : sl;
+        sl = sgn ? sl : ((a > (3 << (s1 - 1)) && s1 < 6) ? s1 + 1 : s1);
+        /* run_before of the previous non-zero level (7.4.5.3.3), masked */
+        {
+            const bool act = k > 0 && zl > 0;
+            const int run = act ? pprev - p - 1 : 0;
+            const uint32_t e = P.rb[(zl < 7 ? (zl > 0 ? zl : 1) : 7) - 1][run];
+            const int l = act ? (int)(e >> 8) : 0;
+            runs = (runs << l) | (act ? (e & 255u) : 0u);
+            rn += l;
+            zl -= run;
+        }
+        pprev = p;
+    }
+    if (tc < MAX) {
+        const uint32_t e = MAX == 4 ? P.tzdc[tc - 1][tz] : P.tz[tc - 1][tz];
+        cap.put(e & 255u, (int)(e >> 8));
+    }
+    if (rn > 64) {
+        ok = false;
+        cap.n += (uint32_t)rn;
+    } else {
+        if (rn > 32) cap.put((uint32_t)(runs >> 32), rn - 32);
+        cap.put((uint32_t)runs, rn > 32 ? 32 : rn);
+    }
+    ok = ok && cap.n <= 128;
+    return tc;
+}
+
+/* chroma DC (2x2, nC = -1): the whole block from 4 levels in registers,
+ * unrolled, packed LDS tables (P.ct[3], P.tzdc, P.rb) */
+template <class CAP>
+__device__ __host__ inline int cavlc_dc4(CAP &cap, const PTabs &P, const int c[4])
+{
+    const uint32_t nz = (c[0] != 0 ? 1u : 0u) | (c[1] != 0 ? 2u : 0u) | (c[2] != 0 ? 4u : 0u) |
+                        (c[3] != 0 ? 8u : 0u);
+    const int tc = __builtin_popcount(nz);
+    int t1 = 0;
+    bool trail = true;
+#pragma unroll
+    for (int i = 3; i >= 0; --i) {
+        const bool one = c[i] == 1 || c[i] == -1;
+        if (c[i] != 0) {
+            trail = trail && one && t1 < 3;
+            t1 += trail ? 1 : 0;
+        }
+    }
+    {
+        const uint32_t e = P.ct[3][4 * tc + t1];
+        cap.put(e & 255u, (int)(e >> 8));
+    }
+    if (tc == 0) return 0;
+    int k = 0, sl = 0, zl = 0, pprev = -1;
+    uint64_t runs = 0;
+    int rn = 0;
+    const int hi = top_bit(nz);
+    const int tz = hi + 1 - tc;
+    zl = tz;
+#pragma unroll
+    for (int i = 3; i >= 0; --i) {
+        const int v = c[i];
+        if (v != 0) {
+            const int a = v < 0 ? -v : v;
+            if (k < t1) {
+                cap.put(v < 0 ? 1u : 0u, 1);
+            } else {
+                int code = 2 * a - 2 + (v < 0 ? 1 : 0);
+                if (k == t1 && t1 < 3) code -= 2;
+                uint32_t fv;
+                int fl;
+                level_field_bf(code, sl, fv, fl);
+                cap.put(fv, fl);
+                if (sl == 0) sl = 1;
+                if (a > (3 << (sl - 1)) && sl < 6) sl++;
+            }
+            if (k > 0 && zl > 0) {
+                const int run = pprev - i - 1;
+                const uint32_t e = P.rb[(zl < 7 ? zl : 7) - 1][run];
+                runs = (runs << (e >> 8)) | (e & 255u);
+                rn += (int)(e >> 8);
+                zl -= run;
+            }
+            pprev = i;
+            k++;
+        }
+    }
+    if (tc < 4) {
+        const uint32_t e = P.tzdc[tc - 1][tz];
+        cap.put(e & 255u, (int)(e >> 8));
+    }
+    cap.put((uint32_t)runs, rn);                        /* <= 3 runs x 2 bits */
+    return tc;
+}
+
 /* ---------------------------------------------------------------------- */
 /* emulation prevention in closed form                                     */
 /* ---------------------------------------------------------------------- */
@@ -558,6 +756,14 @@ struct Rect {
     int x0, y0, w, h;
 };
 
+/* x / d by multiply: m = magic(d) = ceil(2^32 / d) (0 for d = 1); exact for
+ * x, d < 2^16 */
+__device__ __host__ inline uint32_t magic32(uint32_t d) { return d <= 1 ? 0u : 0xffffffffu / d + 1u; }
+__device__ __host__ inline uint32_t div_m(uint32_t x, uint32_t m) { return m ? __umulhi(x, m) : x; }
+/* x / d for x * d < 2^16 (window task indices): m16 = ceil(2^16 / d) */
+__device__ __host__ inline uint32_t magic16(uint32_t d) { return (65536u + d - 1u) / d; }
+__device__ __host__ inline uint32_t div16(uint32_t x, uint32_t m16) { return __umul24(x, m16) >> 16; }
+
 /* number of dynamic MBs before MB m (coding order) */
 __device__ __host__ inline int dyn_rank(const Rect &r, int mbw, int m)
 {
@@ -565,6 +771,21 @@ __device__ __host__ inline int dyn_rank(const Rect &r, int mbw, int m)
     if (y < r.y0) return 0;
     if (y >= r.y0 + r.h) return r.w * r.h;
     return (y - r.y0) * r.w + clampi(x - r.x0, 0, r.w);
+}
+
+/* dyn_rank / dyn_mb with the divisions by mbw / r.w as multiplies */
+__device__ __host__ inline int dyn_rank_m(const Rect &r, int mbw, uint32_t m_mbw, int m)
+{
+    const int y = (int)div_m((uint32_t)m, m_mbw), x = m - y * mbw;
+    if (y < r.y0) return 0;
+    if (y >= r.y0 + r.h) return r.w * r.h;
+    return (y - r.y0) * r.w + clampi(x - r.x0, 0, r.w);
+}
+
+__device__ __host__ inline int dyn_mb_m(const Rect &r, int mbw, uint32_t m_rw, int q)
+{
+    const int ry = (int)div_m((uint32_t)q, m_rw);
+    return (r.y0 + ry) * mbw + r.x0 + (q - ry * r.w);
 }
 
 /* MB index of dynamic MB number q */

@@ -38,7 +38,7 @@ static_assert(24 * WMB <= 256, "one block task per thread");
 constexpr int WIN = DT;                 /* MBs per window (one MB per thread)    */
 constexpr int HEAD_MAX = 160;           /* bits of one MB head (huge mvd: 2 x 63 + ref) */
 constexpr int HDR_MAX = 1024;           /* slice header bits (8 waypoints + MMCO ~ 250) */
-constexpr int BUF_WORDS = 2048;        /* 64 Kbit LDS bit buffer; larger windows take passes */
+constexpr int BUF_WORDS = 1536;        /* 48 Kbit LDS bit buffer; larger windows take passes */
 static_assert(BUF_WORDS * 32 > HDR_MAX + 64, "the slice header fits one buffer");
 constexpr int OBUF = 6400;              /* k_dyn_emit: 127 carry + 5 + 4096 x 1.5 */
 
@@ -136,13 +136,14 @@ struct Task {
     bool luma;
 };
 
-__device__ inline Task task_of(int t, int nd)
+/* m4 = magic16(4 nd), m2 = magic16(2 nd): t < 240, divisors <= 40 */
+__device__ inline Task task_of(int t, int nd, uint32_t m4, uint32_t m2)
 {
     Task q;
     if (t < 16 * nd) {
         q.luma = true;
         q.p = 0;
-        q.by = t / (4 * nd);
+        q.by = (int)div16((uint32_t)t, m4);
         const int c4 = t - q.by * 4 * nd;
         q.k = c4 >> 2;
         q.bx = c4 & 3;
@@ -150,9 +151,9 @@ __device__ inline Task task_of(int t, int nd)
     } else {
         const int u = t - 16 * nd;
         q.luma = false;
-        q.p = u / (4 * nd);
+        q.p = (int)div16((uint32_t)u, m4);
         const int r = u - q.p * 4 * nd;
-        q.by = r / (2 * nd);
+        q.by = (int)div16((uint32_t)r, m2);
         const int c2 = r - q.by * 2 * nd;
         q.k = c2 >> 1;
         q.bx = c2 & 1;
@@ -163,6 +164,9 @@ __device__ inline Task task_of(int t, int nd)
 
 struct StageLds {
     uint32_t buf[BUF_WORDS];      /* NAL bits from word `bw` of the slot on       */
+    uint32_t lv8[WMB * 24][4];    /* block levels, int8 packed, scan order        */
+    uint8_t order[WMB * 24];      /* encode order: light blocks first, then heavy */
+    uint32_t whc[NW];             /* heavy blocks per wave                        */
     int32_t dcraw[WMB][2][4];     /* chroma DC coefficients before the Hadamard   */
     int16_t dclv[WMB][2][4];
     uint8_t tc[WMB][24];          /* TotalCoeff per 4x4 block                     */
@@ -172,12 +176,16 @@ struct StageLds {
     uint32_t exw[WIN];            /* MB lengths: in-wave exclusive prefix         */
     uint32_t wsum[NW];
     uint8_t ctx[DYN_CTX_MB][8];   /* bottom-row TotalCoeff of rect MBs (row ring) */
+    uint16_t rmap[32 * DYN_MAX_H]; /* prediction rows of the rect, per frame row: picture << 15 | row;
+                                      luma 16 h, chroma top 8 h, chroma bottom 8 h; 0xffff: half-pel */
     uint8_t lcarry[8];            /* right-column TotalCoeff of the last dyn MB   */
     int32_t wo[8], wl[8], wv[8];
     int32_t lnz_r, lnz_w;         /* last non-zero staged byte: before / of a flush */
     int32_t general;              /* a half-pel waypoint step was met            */
-    Tabs tabs;
+    PTabs ptabs;
 };
+
+constexpr int HEAVY_TC = 3;       /* blocks with more non-zero levels encode in the heavy group */
 
 constexpr uint32_t DF_OVER = 1u, DF_GENERAL = 2u;   /* DynFrame.err bits */
 
@@ -252,9 +260,8 @@ __global__ __launch_bounds__(DT, SCROLL_DYN_WAVES) void k_dyn_stage(DevStream *_
         L.wl[t] = pend[s].wl[t];
         L.wv[t] = pend[s].wv[t];
     }
-    for (int i = t; i < (int)sizeof(Tabs); i += DT)
-        reinterpret_cast<uint8_t *>(&L.tabs)[i] = reinterpret_cast<const uint8_t *>(&g_tabs)[i];
     for (int i = t; i < BUF_WORDS; i += DT) L.buf[i] = 0u;
+    build_ptabs(*reinterpret_cast<const Tabs *>(&g_tabs), L.ptabs, t, DT);
     const NalDesc d = nal[(size_t)s * ld_nal + j];
     NalCtx c;
     c.w = S->w;
@@ -296,13 +303,36 @@ __global__ __launch_bounds__(DT, SCROLL_DYN_WAVES) void k_dyn_stage(DevStream *_
     const uint8_t *fs = src + (size_t)s * g.src_ld + (size_t)f * g.src_fr;
     const int lstride = 16 * R.w, cstride = 8 * R.w;
     const uint8_t *fcb = fs + (size_t)256 * R.w * R.h, *fcr = fcb + (size_t)64 * R.w * R.h;
-    const int ring = g.ring;
+    const int rmask = g.ring - 1;       /* TotalCoeff row ring: a power of two */
+    /* the waypoint chain of every prediction row, once per NAL: frame row
+     * -> (picture A / B, row) for luma, and for the two chroma rows of the
+     * 1/8-pel bilinear (src/h264_writer.c:689-729 via dyn_device.h) */
+    for (int i = t; i < 32 * R.h; i += DT) {
+        uint16_t e;
+        if (i < 16 * R.h) {
+            const int Y = 16 * R.y0 + i, row = Y >> 4;
+            const bool cA = row < a_end;
+            int yo;
+            const int b = luma_row(T, cA ? rg.ra : rg.rb, Y + (cA ? rg.mva : rg.mvb), yo);
+            e = (uint16_t)(b << 15 | yo);
+        } else {
+            const int i2 = i - 16 * R.h, bot = i2 >= 8 * R.h;
+            const int Y = 8 * R.y0 + (bot ? i2 - 8 * R.h : i2), row = Y >> 3;
+            const bool cA = row < a_end;
+            const int o = (4 * (cA ? rg.mva : rg.mvb)) >> 3;
+            int yo;
+            const int b = chroma_row(T, cA ? rg.ra : rg.rb, Y + o + bot, yo);
+            e = b < 0 ? (uint16_t)0xffff : (uint16_t)(b << 15 | yo);
+        }
+        L.rmap[i] = e;
+    }
+    __syncthreads();
+    const uint32_t m_mbw = magic32((uint32_t)mbw), m_rw = magic32((uint32_t)R.w);
     uint8_t *slot = stage + ((size_t)s * ld_fr + f) * g.slot_bytes;
     uint32_t *out = reinterpret_cast<uint32_t *>(slot);
-    /* levels of blocks whose CAVLC rest outgrows the 128-bit capture */
-    int16_t *ovf = reinterpret_cast<int16_t *>(slot + g.slot_bytes - DYN_OVF_BYTES) + 16 * t;
     const uint32_t cap_words = (uint32_t)((g.slot_bytes - DYN_OVF_BYTES) / 4) - 4u;
-    const Tabs &TB = L.tabs;
+    const Tabs &TB = g_tabs;            /* chroma DC and the rare > 128-bit blocks */
+    const PTabs &PT = L.ptabs;
 
     uint32_t bw = 0;             /* staging word of buf[0]                        */
     uint32_t my_ep = 0;
@@ -339,54 +369,63 @@ __global__ __launch_bounds__(DT, SCROLL_DYN_WAVES) void k_dyn_stage(DevStream *_
 
     const int nmb = mbw * mbh, ndt = R.w * R.h;
     for (int m0 = 0; m0 < nmb;) {
-        const int q0 = dyn_rank(R, mbw, m0);
+        const int q0 = dyn_rank_m(R, mbw, m_mbw, m0);
         int m1 = min(m0 + WIN, nmb);
-        if (q0 + WMB < ndt) m1 = min(m1, dyn_mb(R, mbw, q0 + WMB));
-        const int nd = dyn_rank(R, mbw, m1) - q0;
+        if (q0 + WMB < ndt) m1 = min(m1, dyn_mb_m(R, mbw, m_rw, q0 + WMB));
+        const int nd = dyn_rank_m(R, mbw, m_mbw, m1) - q0;
         const int nm = m1 - m0;
+        const uint32_t m4 = nd ? magic16(4u * nd) : 0u, m2 = nd ? magic16(2u * nd) : 0u;
+        /* rect coordinates (ry, cx) of dynamic MB k of the window */
+        auto dcoord = [&](int k, int &ry, int &cx) {
+            const int qq = q0 + k;
+            ry = (int)div_m((uint32_t)qq, m_rw);
+            cx = qq - ry * R.w;
+        };
         nwin++;
 
         /* A: the previous window's whole words -> staging; then residual ->
-         * transform -> levels (registers) -> the nC-independent part of the
-         * block's CAVLC (cavlc_rest) captured in registers until D */
+         * transform -> quantised levels (int8 packed) and TotalCoeff to LDS */
         const uint32_t pnf = pend_T >> 5;
         uint32_t part = 0;
         if (pend_T) {
             flush_words(pnf, bw);
             part = L.buf[pnf];
         }
-        CapSink bcap{0, 0, 0}, dcap{0, 0, 0};
-        int bt1 = 0;
+        CapSink bcap{0, 0, 0};
+        bool heavy = false;
         if (t < 24 * nd) {
-            const Task q = task_of(t, nd);
-            const int m = dyn_mb(R, mbw, q0 + q.k), row = m / mbw, col = m - row * mbw;
-            const int cx = col - R.x0, ry = row - R.y0;
+            const Task q = task_of(t, nd, m4, m2);
+            int ry, cx;
+            dcoord(q.k, ry, cx);
+            const int row = R.y0 + ry, col = R.x0 + cx;
             const bool curA = row < a_end;
             const int ref = curA ? rg.ra : rg.rb, mvp = curA ? rg.mva : rg.mvb;
             int res[16], W[16];
             if (q.luma) {
                 const uint8_t *sp = fs + (size_t)(16 * ry + 4 * q.by) * lstride + 16 * cx + 4 * q.bx;
-                const int X = 16 * col + 4 * q.bx, Y = 16 * row + 4 * q.by;
+                const int X = 16 * col + 4 * q.bx;
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
                     const uint32_t sv = ld32(sp + (size_t)i * lstride);
-                    int yo;
-                    const int b = luma_row(T, ref, Y + i + mvp, yo);
-                    const uint32_t pv = ld32(rb + (size_t)b * pic + (size_t)yo * w + X);
+                    const uint32_t e = L.rmap[16 * ry + 4 * q.by + i];
+                    const uint32_t pv = ld32(rb + (e >> 15) * (uint32_t)pic + (e & 0x7fffu) * (uint32_t)w + X);
 #pragma unroll
                     for (int x = 0; x < 4; ++x)
                         res[4 * i + x] = (int)((sv >> (8 * x)) & 255u) - (int)((pv >> (8 * x)) & 255u);
                 }
                 fwd4x4(res, W);
-                int cf[16];
+                uint32_t pk[4] = {0, 0, 0, 0};
+                int n = 0;
 #pragma unroll
-                for (int k2 = 0; k2 < 16; ++k2) cf[k2] = quant(W[ZZ[k2]], ZZ[k2]);
-                const int n = cavlc_rest<16>(bcap, TB, cf, bt1);
-                if (bcap.over())
-#pragma unroll
-                    for (int k2 = 0; k2 < 16; ++k2) ovf[k2] = (int16_t)cf[k2];
+                for (int k2 = 0; k2 < 16; ++k2) {
+                    const int v = quant(W[ZZ[k2]], ZZ[k2]);          /* |v| <= 78: int8 */
+                    pk[k2 >> 2] |= ((uint32_t)v & 255u) << (8 * (k2 & 3));
+                    n += v != 0;
+                }
+                *reinterpret_cast<uint4 *>(L.lv8[24 * q.k + q.blk]) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+                heavy = n > HEAVY_TC;
                 L.tc[q.k][q.blk] = (uint8_t)n;
-                if (q.by == 3) L.ctx[(ry % ring) * R.w + cx][q.bx] = (uint8_t)n;
+                if (q.by == 3) L.ctx[(ry & rmask) * R.w + cx][q.bx] = (uint8_t)n;
             } else {
                 const uint8_t *sp = (q.p ? fcr : fcb) + (size_t)(8 * ry + 4 * q.by) * cstride +
                                     8 * cx + 4 * q.bx;
@@ -397,17 +436,19 @@ __global__ __launch_bounds__(DT, SCROLL_DYN_WAVES) void k_dyn_stage(DevStream *_
                 for (int i = 0; i < 4; ++i) {
                     const uint32_t sv = ld32(sp + (size_t)i * cstride);
                     const int ya = Y + i + o;
-                    int yoa = 0, yob = 0;
-                    const int ba = chroma_row(T, ref, ya, yoa);
-                    const int bb = fr ? chroma_row(T, ref, ya + 1, yob) : 0;
+                    const uint32_t ea = L.rmap[16 * R.h + 8 * ry + 4 * q.by + i];
+                    const uint32_t eb = fr ? L.rmap[24 * R.h + 8 * ry + 4 * q.by + i] : 0u;
+                    const int ba = ea == 0xffffu ? -1 : (int)(ea >> 15), yoa = (int)(ea & 0x7fffu);
+                    const int bb = eb == 0xffffu ? -1 : (int)(eb >> 15), yob = (int)(eb & 0x7fffu);
                     int pred[4];
                     if (!GENERAL && (ba < 0 || bb < 0)) {
                         L.general = 1;
                         pred[0] = pred[1] = pred[2] = pred[3] = 0;
                     } else if (ba >= 0 && bb >= 0) {
                         const uint8_t *cp = rb + ysz + (size_t)q.p * csz + X;
-                        const uint32_t av = ld32(cp + (size_t)ba * pic + (size_t)yoa * cw);
-                        const uint32_t bv = fr ? ld32(cp + (size_t)bb * pic + (size_t)yob * cw) : 0u;
+                        const uint32_t av = ld32(cp + (uint32_t)ba * (uint32_t)pic + (uint32_t)yoa * (uint32_t)cw);
+                        const uint32_t bv =
+                            fr ? ld32(cp + (uint32_t)bb * (uint32_t)pic + (uint32_t)yob * (uint32_t)cw) : 0u;
 #pragma unroll
                         for (int x = 0; x < 4; ++x) {
                             const int a = (int)((av >> (8 * x)) & 255u), b = (int)((bv >> (8 * x)) & 255u);
@@ -435,17 +476,22 @@ __global__ __launch_bounds__(DT, SCROLL_DYN_WAVES) void k_dyn_stage(DevStream *_
                 }
                 fwd4x4(res, W);
                 L.dcraw[q.k][q.p][2 * q.by + q.bx] = W[0];
-                int cf[15];
+                uint32_t pk[4] = {0, 0, 0, 0};
+                int n = 0;
 #pragma unroll
-                for (int k2 = 1; k2 < 16; ++k2) cf[k2 - 1] = quant(W[ZZ[k2]], ZZ[k2]);
-                const int n = cavlc_rest<15>(bcap, TB, cf, bt1);
-                if (bcap.over())
-#pragma unroll
-                    for (int k2 = 0; k2 < 15; ++k2) ovf[k2] = (int16_t)cf[k2];
+                for (int k2 = 1; k2 < 16; ++k2) {
+                    const int v = quant(W[ZZ[k2]], ZZ[k2]);
+                    pk[(k2 - 1) >> 2] |= ((uint32_t)v & 255u) << (8 * ((k2 - 1) & 3));
+                    n += v != 0;
+                }
+                *reinterpret_cast<uint4 *>(L.lv8[24 * q.k + q.blk]) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+                heavy = n > HEAVY_TC;
                 L.tc[q.k][q.blk] = (uint8_t)n;
-                if (q.by == 1) L.ctx[(ry % ring) * R.w + cx][4 + 2 * q.p + q.bx] = (uint8_t)n;
+                if (q.by == 1) L.ctx[(ry & rmask) * R.w + cx][4 + 2 * q.p + q.bx] = (uint8_t)n;
             }
         }
+        const uint64_t hb = __ballot(heavy);
+        if (lane == 0) L.whc[wave] = (uint32_t)__popcll(hb);
         __syncthreads();
         mark(0);
         if (!GENERAL && L.general) {                /* uniform: read after the barrier */
@@ -462,12 +508,53 @@ __global__ __launch_bounds__(DT, SCROLL_DYN_WAVES) void k_dyn_stage(DevStream *_
             bw += pnf;
             pend_T = 0;
         }
-        uint32_t tokv = 0;
-        int tokl = 0;
-        if (t < 24 * nd) {
-            const Task q = task_of(t, nd);
-            const int m = dyn_mb(R, mbw, q0 + q.k), row = m / mbw, col = m - row * mbw;
-            const int cx = col - R.x0, ry = row - R.y0;
+        /* encode order: light blocks (<= HEAVY_TC non-zero levels) first, so
+         * the encode loop of a wave runs few iterations; heavy ones share the
+         * last wave(s) */
+        const int ntask = 24 * nd;
+        if (t < ntask) {
+            uint32_t hpre = 0, htot = 0;
+#pragma unroll
+            for (int w2 = 0; w2 < NW; ++w2) {
+                hpre += w2 < wave ? L.whc[w2] : 0u;
+                htot += L.whc[w2];
+            }
+            const uint32_t hr = hpre + (uint32_t)__builtin_amdgcn_mbcnt_hi(
+                                           (uint32_t)(hb >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)hb, 0u));
+            const uint32_t lr = (uint32_t)t - hr;
+            L.order[heavy ? (uint32_t)ntask - htot + hr : lr] = (uint8_t)t;
+        }
+        if (t < 2 * nd) {
+            const int k = t >> 1, p = t & 1;
+            const int *dc = L.dcraw[k][p];
+            const int f00 = dc[0] + dc[1] + dc[2] + dc[3], f01 = dc[0] - dc[1] + dc[2] - dc[3];
+            const int f10 = dc[0] + dc[1] - dc[2] - dc[3], f11 = dc[0] - dc[1] - dc[2] + dc[3];
+            const int dq[4] = {quant_dc(f00), quant_dc(f01), quant_dc(f10), quant_dc(f11)};
+            int16_t *o = L.dclv[k][p];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) o[i] = (int16_t)dq[i];
+            CountSink dn{0};
+            cavlc_dc4(dn, PT, dq);
+            L.blen[k][16 + p] = (uint16_t)dn.n;
+        }
+        __syncthreads();
+
+        /* B2: CAVLC of the block order[t] (token .. runs) into registers */
+        /* the encoded block, packed to keep registers free across barriers:
+         * bit 31 valid, 30 ok, 24..29 nC + 1, 16..23 MB of the window, 8..15
+         * piece, 0..7 dynamic MB k */
+        uint32_t enc = 0;
+        if (t < ntask) {
+            int enc_nc = 0, e_k = 0, e_pc = 0, e_u = 0, etask;
+            bool enc_ok = true;
+            etask = L.order[t];
+            const Task q = task_of(etask, nd, m4, m2);
+            int ry, cx;
+            dcoord(q.k, ry, cx);
+            const int row = R.y0 + ry, col = R.x0 + cx;
+            e_k = q.k;
+            e_pc = q.luma ? q.blk : 18 + (q.blk - 16);
+            e_u = row * mbw + col - m0;                /* MB of the window */
             const bool ldyn = col > R.x0, lav = col > 0, tdyn = row > R.y0, tav = row > 0;
             const uint8_t *tc = L.tc[q.k];
             int nA, nB;
@@ -477,7 +564,7 @@ __global__ __launch_bounds__(DT, SCROLL_DYN_WAVES) void k_dyn_stage(DevStream *_
                 nA = q.bx > 0 ? tc[r - 1]
                               : (ldyn ? (q.k > 0 ? L.tc[q.k - 1][r + 3] : L.lcarry[q.by]) : (lav ? 0 : -1));
                 nB = q.by > 0 ? tc[r - 4]
-                              : (tdyn ? L.ctx[((ry - 1) % ring) * R.w + cx][q.bx] : (tav ? 0 : -1));
+                              : (tdyn ? L.ctx[((ry - 1) & rmask) * R.w + cx][q.bx] : (tav ? 0 : -1));
                 const int b8 = 4 * (q.by & 2) + (q.bx & 2);
                 coded = (tc[b8] | tc[b8 + 1] | tc[b8 + 4] | tc[b8 + 5]) != 0;
             } else {
@@ -486,30 +573,23 @@ __global__ __launch_bounds__(DT, SCROLL_DYN_WAVES) void k_dyn_stage(DevStream *_
                               : (ldyn ? (q.k > 0 ? L.tc[q.k - 1][i + 1] : L.lcarry[4 + 2 * q.p + q.by])
                                       : (lav ? 0 : -1));
                 nB = q.by > 0 ? tc[i - 2]
-                              : (tdyn ? L.ctx[((ry - 1) % ring) * R.w + cx][4 + 2 * q.p + q.bx]
+                              : (tdyn ? L.ctx[((ry - 1) & rmask) * R.w + cx][4 + 2 * q.p + q.bx]
                                       : (tav ? 0 : -1));
                 uint32_t any = 0;
 #pragma unroll
                 for (int k2 = 16; k2 < 24; ++k2) any |= tc[k2];
                 coded = any != 0;
             }
-            const int nC = nc_of(nA, nB);
-            if (coded) coeff_token(TB, tc[q.blk], bt1, nC, tokv, tokl);
-            L.blen[q.k][q.luma ? q.blk : 18 + (q.blk - 16)] =
-                coded ? (uint16_t)(tokl + (int)bcap.n) : (uint16_t)0;
-        }
-        if (t < 2 * nd) {
-            const int k = t >> 1, p = t & 1;
-            const int *dc = L.dcraw[k][p];
-            const int f00 = dc[0] + dc[1] + dc[2] + dc[3], f01 = dc[0] - dc[1] + dc[2] - dc[3];
-            const int f10 = dc[0] + dc[1] - dc[2] - dc[3], f11 = dc[0] - dc[1] - dc[2] + dc[3];
-            int16_t *o = L.dclv[k][p];
-            o[0] = (int16_t)quant_dc(f00);
-            o[1] = (int16_t)quant_dc(f01);
-            o[2] = (int16_t)quant_dc(f10);
-            o[3] = (int16_t)quant_dc(f11);
-            cavlc_block(dcap, TB, o, 4, -1);
-            L.blen[k][16 + p] = (uint16_t)dcap.n;
+            enc_nc = nc_of(nA, nB);
+            if (coded) {
+                const uint4 v4 = *reinterpret_cast<const uint4 *>(L.lv8[24 * q.k + q.blk]);
+                const uint32_t pk[4] = {v4.x, v4.y, v4.z, v4.w};
+                if (q.luma) cavlc_nz<16>(bcap, PT, pk, enc_nc, enc_ok);
+                else cavlc_nz<15>(bcap, PT, pk, enc_nc, enc_ok);
+            }
+            L.blen[q.k][q.luma ? q.blk : 18 + (q.blk - 16)] = (uint16_t)bcap.n;
+            enc = 0x80000000u | (enc_ok ? 0x40000000u : 0u) | (uint32_t)(enc_nc + 1) << 24 |
+                  (uint32_t)e_u << 16 | (uint32_t)e_pc << 8 | (uint32_t)e_k;
         }
         __syncthreads();
         mark(1);
@@ -517,21 +597,20 @@ __global__ __launch_bounds__(DT, SCROLL_DYN_WAVES) void k_dyn_stage(DevStream *_
         /* C: MB heads, cbp, piece offsets; in-wave scan of the MB lengths */
         uint32_t mlen = 0;
         int kd = -1, ref = 0, mv4 = 0, px = 0, py = 0, code = 0, cbp = 0;
-        CapSink mcap{0, 0, 0};
         if (t < nm) {
-            const int m = m0 + t, row = m / mbw, col = m - row * mbw;
+            const int m = m0 + t, row = (int)div_m((uint32_t)m, m_mbw), col = m - row * mbw;
             const bool curA = row < a_end, abvA = (row - 1) < a_end;
             ref = curA ? rg.ra : rg.rb;
             mv4 = 4 * (curA ? rg.mva : rg.mvb);
             const int aref = abvA ? rg.ra : rg.rb, amv4 = 4 * (abvA ? rg.mva : rg.mvb);
             predict(col, row, mbw, ref, mv4, aref, amv4, px, py);
-            put_mb_head(mcap, ref, 0 - px, mv4 - py, nrefs);
+            CountSink mc{0};
+            put_mb_head(mc, ref, 0 - px, mv4 - py, nrefs);
             const bool isdyn = col >= R.x0 && col < R.x0 + R.w && row >= R.y0 && row < R.y0 + R.h;
             if (!isdyn) {
-                mcap.put(1, 1);                    /* coded_block_pattern ue(0) */
-                mlen = mcap.n;
+                mlen = mc.n + 1u;                  /* + coded_block_pattern ue(0) */
             } else {
-                kd = dyn_rank(R, mbw, m) - q0;
+                kd = (row - R.y0) * R.w + (col - R.x0) - q0;
                 const uint8_t *tc = L.tc[kd];
                 int cbp_l = 0;
 #pragma unroll
@@ -550,9 +629,9 @@ __global__ __launch_bounds__(DT, SCROLL_DYN_WAVES) void k_dyn_stage(DevStream *_
                 cbp = cbp_l | (cbp_c << 4);
                 code = TB.cbp_code[cbp];
                 L.cbp[kd] = (uint8_t)cbp;
-                put_ue(mcap, (uint32_t)code);
-                if (cbp) put_se(mcap, 0);          /* mb_qp_delta */
-                uint32_t off = mcap.n;
+                put_ue(mc, (uint32_t)code);
+                if (cbp) put_se(mc, 0);            /* mb_qp_delta */
+                uint32_t off = mc.n;
                 for (int blk = 0; blk < 16; ++blk) {
                     const int r = blk_raster(blk);
                     L.boff[kd][r] = (uint16_t)off;
@@ -608,44 +687,41 @@ __global__ __launch_bounds__(DT, SCROLL_DYN_WAVES) void k_dyn_stage(DevStream *_
         const uint32_t my_mbo = t < nm ? mbo(t) : 0u;
         for (uint32_t p0 = 0; p0 < nw; p0 += PW) {
             const LdsOrWin win{L.buf, p0, PW};
-            if (t < nm) {
+            if (t < nm) {                          /* MB head (+ cbp, qp_delta) */
                 WSink sk{win, 0, 0, 0};
                 sk.start(F + my_mbo);
-                if (!mcap.over()) {
-                    sk.put_cap(mcap);
-                } else if (kd < 0) {               /* > 128-bit head: huge mvd */
-                    put_mb(sk, ref, 0 - px, mv4 - py, nrefs);
+                if (kd < 0) {
+                    put_mb(sk, ref, 0, mv4 - py, nrefs);
                 } else {
-                    put_mb_head(sk, ref, 0 - px, mv4 - py, nrefs);
+                    put_mb_head(sk, ref, 0, mv4 - py, nrefs);
                     put_ue(sk, (uint32_t)code);
                     if (cbp) put_se(sk, 0);
                 }
                 sk.finish();
             }
-            if (t < 24 * nd && tokl) {
-                const Task q = task_of(t, nd);
-                const int pc = q.luma ? q.blk : 18 + (q.blk - 16);
+            if ((enc >> 31) && bcap.n) {
+                const int e_k = (int)(enc & 255u), e_pc = (int)((enc >> 8) & 255u);
                 WSink sk{win, 0, 0, 0};
-                sk.start(F + mbo(dyn_mb(R, mbw, q0 + q.k) - m0) + L.boff[q.k][pc]);
-                sk.put(tokv, tokl);
-                if (!bcap.over()) {
+                sk.start(F + mbo((int)((enc >> 16) & 255u)) + L.boff[e_k][e_pc]);
+                if ((enc >> 30) & 1u) {
                     sk.put_cap(bcap);
-                } else {                           /* > 128 bits: re-encode */
-                    int cf[16], t1d;
-#pragma unroll
-                    for (int k2 = 0; k2 < 16; ++k2) cf[k2] = k2 < 15 || q.luma ? (int)ovf[k2] : 0;
-                    if (q.luma) cavlc_rest<16>(sk, TB, cf, t1d);
-                    else cavlc_rest<15>(sk, TB, cf, t1d);
+                } else {                           /* > 128 bits: re-encode from LDS */
+                    const int blk = e_pc < 16 ? e_pc : 16 + (e_pc - 18);
+                    const int8_t *lv = reinterpret_cast<const int8_t *>(L.lv8[24 * e_k + blk]);
+                    cavlc_block(sk, TB, lv, e_pc < 16 ? 16 : 15, (int)((enc >> 24) & 63u) - 1);
                 }
                 sk.finish();
             }
-            if (t < 2 * nd) {
+            if (t < 2 * nd) {                      /* chroma DC, re-encoded from LDS */
                 const int k = t >> 1, p = t & 1;
                 if (L.cbp[k] >> 4) {
+                    int ry, cx;
+                    dcoord(k, ry, cx);
                     WSink sk{win, 0, 0, 0};
-                    sk.start(F + mbo(dyn_mb(R, mbw, q0 + k) - m0) + L.boff[k][16 + p]);
-                    if (!dcap.over()) sk.put_cap(dcap);
-                    else cavlc_block(sk, TB, L.dclv[k][p], 4, -1);
+                    sk.start(F + mbo((R.y0 + ry) * mbw + R.x0 + cx - m0) + L.boff[k][16 + p]);
+                    const int16_t *o = L.dclv[k][p];
+                    const int dq[4] = {o[0], o[1], o[2], o[3]};
+                    cavlc_dc4(sk, PT, dq);
                     sk.finish();
                 }
             }

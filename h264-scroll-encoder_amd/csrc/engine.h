@@ -76,8 +76,9 @@ typedef struct {
 } DynFrame;
 
 /* dynamic rect geometry and buffer strides (one per batch) */
-#define DYN_MAX_W 128               /* rect width limit (MBs)                     */
-#define DYN_CTX_MB 400              /* TotalCoeff row-ring entries (LDS)          */
+#define DYN_MAX_W 64                /* rect width limit (MBs)                     */
+#define DYN_MAX_H 48                /* rect height limit (MBs)                    */
+#define DYN_CTX_MB 256              /* TotalCoeff row-ring entries (LDS)          */
 #define DYN_WINDOW_MBS 10           /* dynamic MBs per k_dyn_stage window         */
 #define DYN_OVF_BYTES 8192          /* staging-slot tail: levels of > 128-bit blocks */
 typedef struct {

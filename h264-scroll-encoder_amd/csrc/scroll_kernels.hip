@@ -1436,8 +1436,9 @@ int scroll_batch_set_dyn_rect(ScrollBatch *b, int x0, int y0, int w, int h, size
             return SCROLL_ERR_CONFIG;
         }
     const int mbw = pw / 16, mbh = ph / 16;
-    const int ring = std::min(h, (DYN_WINDOW_MBS + w - 1) / w + 2);
-    if ((pw & 15) || (ph & 15) || x0 + w > mbw || y0 + h > mbh || w > DYN_MAX_W ||
+    int ring = 1;                      /* rows a window spans + 1, as a power of two */
+    while (ring < std::min(h, (DYN_WINDOW_MBS + w - 1) / w + 2)) ring <<= 1;
+    if ((pw & 15) || (ph & 15) || x0 + w > mbw || y0 + h > mbh || w > DYN_MAX_W || h > DYN_MAX_H ||
         ring * w > DYN_CTX_MB) {
         set_err("scroll_batch_set_dyn_rect: rect (%d,%d %dx%d MBs) not supported in %dx%d", x0, y0,
                 w, h, pw, ph);

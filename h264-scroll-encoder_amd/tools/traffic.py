@@ -33,16 +33,21 @@ def main():
     ap.add_argument("out")
     ap.add_argument("--kernel", default="k_emit")
     ap.add_argument("--alg-bytes", type=float, default=0.0)
+    ap.add_argument("--fetch-scale", type=float, default=2.0,
+                    help="gfx950 FETCH_SIZE correction (2 = wide coalesced reads, the guide's "
+                         "calibrated case; other access widths are uncalibrated)")
     a = ap.parse_args()
     fk = per_dispatch(a.fetch_dir, "FETCH_SIZE", a.kernel)
     wk = per_dispatch(a.write_dir, "WRITE_SIZE", a.kernel)
-    fetch = 2.0 * 1024 * sum(fk) / len(fk)          # KB -> bytes, x2 gfx950 correction
+    raw = 1024 * sum(fk) / len(fk)                  # KB -> bytes
+    fetch = a.fetch_scale * raw
     write = 1024 * sum(wk) / len(wk)
     out = {"kernel": a.kernel, "dispatches": [len(fk), len(wk)],
+           "fetch_size_raw_bytes_per_launch": round(raw),
            "fetch_bytes_per_launch": round(fetch), "write_bytes_per_launch": round(write),
            "hbm_bytes_per_launch": round(fetch + write),
            "method": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes); "
-                     "FETCH_SIZE doubled per the gfx950 correction"}
+                     f"FETCH_SIZE x {a.fetch_scale} (gfx950 correction)"}
     if a.alg_bytes:
         out["alg_bytes_per_launch"] = a.alg_bytes
         out["traffic_over_alg"] = round((fetch + write) / a.alg_bytes, 4)

@@ -316,4 +316,22 @@ long sim_cavlc_split(const int *coef, int max, int nC, int start, uint32_t *word
     return (long)(end - (uint32_t)start);
 }
 
+long sim_cavlc_dc4(const int *coef, int start, uint32_t *words, int *tc_out)
+{
+    static dyn::PTabs P;
+    static bool init = false;
+    if (!init) {
+        dyn::build_ptabs(g_dyn_tabs, P, 0, 1);
+        init = true;
+    }
+    dyn::CapSink cap{0, 0, 0};
+    int c[4] = {coef[0], coef[1], coef[2], coef[3]};
+    *tc_out = dyn::cavlc_dc4(cap, P, c);
+    dyn::OrSink<HostOr> os{{words}, 0, 0, 0};
+    os.start((uint32_t)start);
+    os.put_cap(cap);
+    os.finish();
+    return (long)cap.n;
+}
+
 }  // extern "C"

@@ -227,7 +227,7 @@ def test_dyn_half_pel_waypoint_chain(gpu, oracle):
     """a resumed config with a waypoint at an odd offset: its rows predict at
     half-pel chroma positions, which only the general k_dyn_stage path does"""
     w, h = 64, 1024
-    rect = Rect(1, 0, 2, 64)
+    rect = Rect(1, 0, 2, 48)
     wps = [(501, 2, 1)]
     S, F = 1, 6
     offs = np.array([[600, 610, 777, 900, 505, 996]], np.int32)

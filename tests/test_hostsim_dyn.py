@@ -71,6 +71,11 @@ def test_cavlc_blocks_vs_oracle(hostsim, oracle):
         n2 = hostsim.sim_cavlc_split(ca, mx, nC, start, words, ctypes.byref(tc))
         assert n2 == n and tc.value == tco, (it, coef, nC)
         assert _word_bits(words, start, n) == _bits(ob, 0, n), (it, coef, nC)
+        if mx == 4:                                    # the kernels' chroma-DC encoder
+            ctypes.memset(words, 0, ctypes.sizeof(words))
+            n3 = hostsim.sim_cavlc_dc4(ca, start, words, ctypes.byref(tc))
+            assert n3 == n and tc.value == tco, (it, coef)
+            assert _word_bits(words, start, n) == _bits(ob, 0, n), (it, coef)
 
 
 def _planes(rng, w, h):

@@ -169,10 +169,10 @@ struct StageLds {
     uint32_t whc[NW];             /* heavy blocks per wave                        */
     int32_t dcraw[WMB][2][4];     /* chroma DC coefficients before the Hadamard   */
     int16_t dclv[WMB][2][4];
-    uint8_t tc[WMB][24];          /* TotalCoeff per 4x4 block                     */
+    alignas(16) uint8_t tc[WMB][32];   /* TotalCoeff per 4x4 block (24 used)      */
     uint8_t cbp[WMB];
-    uint16_t blen[WMB][26];       /* pieces: luma raster 0..15, DC 16+p, AC 18+4p+kk */
-    uint16_t boff[WMB][26];
+    alignas(16) uint16_t blen[WMB][32];  /* pieces: luma raster 0..15, DC 16+p, AC 18+4p+kk */
+    alignas(16) uint16_t boff[WMB][32];
     uint32_t exw[WIN];            /* MB lengths: in-wave exclusive prefix         */
     uint32_t wsum[NW];
     uint8_t ctx[DYN_CTX_MB][8];   /* bottom-row TotalCoeff of rect MBs (row ring) */
@@ -182,6 +182,9 @@ struct StageLds {
     int32_t wo[8], wl[8], wv[8];
     int32_t lnz_r, lnz_w;         /* last non-zero staged byte: before / of a flush */
     int32_t general;              /* a half-pel waypoint step was met            */
+    uint64_t hhi[12], hlo[12];    /* MB head codewords [row type 0..3][first / middle / last] */
+    uint32_t hlen[12];
+    int32_t head_over;            /* a head longer than 128 bits: compute per MB */
     PTabs ptabs;
 };
 
@@ -217,6 +220,10 @@ __device__ inline int last_nz_byte(uint32_t w)      /* MSB-first byte index, w !
  *   B(i)  nC + coeff_token, chroma DC; buffer rewind after the flush
  *   C(i)  MB heads (regs), cbp, piece offsets, in-wave scan of MB lengths
  *   D(i)  every piece ORed into the LDS bit buffer at its offset          */
+#ifndef SCROLL_DYN_ABLATE
+#define SCROLL_DYN_ABLATE 0         /* 1: honour the SCROLL_DEBUG_DYN_* ablation flags (profiling builds) */
+#endif
+#define ABL(flag) (SCROLL_DYN_ABLATE && (g.debug & (flag)))
 #ifndef SCROLL_DYN_WAVES
 #define SCROLL_DYN_WAVES 8          /* waves per SIMD the register budget targets */
 #endif
@@ -254,6 +261,7 @@ __global__ __launch_bounds__(DT, SCROLL_DYN_WAVES) void k_dyn_stage(DevStream *_
         L.general = 0;
         L.lnz_r = -1;
         L.lnz_w = -1;
+        L.head_over = 0;
     }
     if (t < 8) {
         L.wo[t] = pend[s].wo[t];
@@ -325,6 +333,25 @@ __global__ __launch_bounds__(DT, SCROLL_DYN_WAVES) void k_dyn_stage(DevStream *_
             e = b < 0 ? (uint16_t)0xffff : (uint16_t)(b << 15 | yo);
         }
         L.rmap[i] = e;
+    }
+    /* MB head codewords (mb_skip_run .. mvd, h264_writer.c:434-453): they
+     * depend only on the row type -- row 0, steady A, A->B boundary, steady
+     * B -- and on first / middle / last position */
+    if (t < 12) {
+        const int ty = t / 3, pos = t - 3 * ty;
+        const int x = pos == 0 ? 0 : (pos == 1 ? min(1, mbw - 1) : mbw - 1);
+        const bool cur = ty == 0 ? 0 < a_end : ty == 1;
+        const bool abv = ty == 1 || ty == 2;
+        const int ref = cur ? rg.ra : rg.rb, mv4 = 4 * (cur ? rg.mva : rg.mvb);
+        const int aref = abv ? rg.ra : rg.rb, amv4 = 4 * (abv ? rg.mva : rg.mvb);
+        int px, py;
+        predict(x, ty == 0 ? 0 : 1, mbw, ref, mv4, aref, amv4, px, py);
+        CapSink hc{0, 0, 0};
+        put_mb_head(hc, ref, 0 - px, mv4 - py, nrefs);
+        L.hhi[t] = hc.hi;
+        L.hlo[t] = hc.lo;
+        L.hlen[t] = hc.n;
+        if (hc.over()) L.head_over = 1;
     }
     __syncthreads();
     const uint32_t m_mbw = magic32((uint32_t)mbw), m_rw = magic32((uint32_t)R.w);
@@ -406,9 +433,12 @@ __global__ __launch_bounds__(DT, SCROLL_DYN_WAVES) void k_dyn_stage(DevStream *_
                 const int X = 16 * col + 4 * q.bx;
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
-                    const uint32_t sv = ld32(sp + (size_t)i * lstride);
                     const uint32_t e = L.rmap[16 * ry + 4 * q.by + i];
-                    const uint32_t pv = ld32(rb + (e >> 15) * (uint32_t)pic + (e & 0x7fffu) * (uint32_t)w + X);
+                    uint32_t sv = 0x80604020u + (uint32_t)(t + i), pv = 0x10203040u;
+                    if (!ABL(SCROLL_DEBUG_DYN_NOLOAD)) {
+                        sv = ld32(sp + (size_t)i * lstride);
+                        pv = ld32(rb + (e >> 15) * (uint32_t)pic + (e & 0x7fffu) * (uint32_t)w + X);
+                    }
 #pragma unroll
                     for (int x = 0; x < 4; ++x)
                         res[4 * i + x] = (int)((sv >> (8 * x)) & 255u) - (int)((pv >> (8 * x)) & 255u);
@@ -434,7 +464,8 @@ __global__ __launch_bounds__(DT, SCROLL_DYN_WAVES) void k_dyn_stage(DevStream *_
                 const int cw = w / 2;
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
-                    const uint32_t sv = ld32(sp + (size_t)i * cstride);
+                    const uint32_t sv = ABL(SCROLL_DEBUG_DYN_NOLOAD) ? 0x40506070u + (uint32_t)t
+                                                                          : ld32(sp + (size_t)i * cstride);
                     const int ya = Y + i + o;
                     const uint32_t ea = L.rmap[16 * R.h + 8 * ry + 4 * q.by + i];
                     const uint32_t eb = fr ? L.rmap[24 * R.h + 8 * ry + 4 * q.by + i] : 0u;
@@ -446,9 +477,11 @@ __global__ __launch_bounds__(DT, SCROLL_DYN_WAVES) void k_dyn_stage(DevStream *_
                         pred[0] = pred[1] = pred[2] = pred[3] = 0;
                     } else if (ba >= 0 && bb >= 0) {
                         const uint8_t *cp = rb + ysz + (size_t)q.p * csz + X;
-                        const uint32_t av = ld32(cp + (uint32_t)ba * (uint32_t)pic + (uint32_t)yoa * (uint32_t)cw);
+                        const bool nl = ABL(SCROLL_DEBUG_DYN_NOLOAD);
+                        const uint32_t av =
+                            nl ? 0x11223344u : ld32(cp + (uint32_t)ba * (uint32_t)pic + (uint32_t)yoa * (uint32_t)cw);
                         const uint32_t bv =
-                            fr ? ld32(cp + (uint32_t)bb * (uint32_t)pic + (uint32_t)yob * (uint32_t)cw) : 0u;
+                            fr && !nl ? ld32(cp + (uint32_t)bb * (uint32_t)pic + (uint32_t)yob * (uint32_t)cw) : 0u;
 #pragma unroll
                         for (int x = 0; x < 4; ++x) {
                             const int a = (int)((av >> (8 * x)) & 255u), b = (int)((bv >> (8 * x)) & 255u);
@@ -581,7 +614,9 @@ __global__ __launch_bounds__(DT, SCROLL_DYN_WAVES) void k_dyn_stage(DevStream *_
                 coded = any != 0;
             }
             enc_nc = nc_of(nA, nB);
-            if (coded) {
+            if (coded && ABL(SCROLL_DEBUG_DYN_NOCAVLC)) {
+                bcap.put(1, 1);
+            } else if (coded) {
                 const uint4 v4 = *reinterpret_cast<const uint4 *>(L.lv8[24 * q.k + q.blk]);
                 const uint32_t pk[4] = {v4.x, v4.y, v4.z, v4.w};
                 if (q.luma) cavlc_nz<16>(bcap, PT, pk, enc_nc, enc_ok);
@@ -596,31 +631,39 @@ __global__ __launch_bounds__(DT, SCROLL_DYN_WAVES) void k_dyn_stage(DevStream *_
 
         /* C: MB heads, cbp, piece offsets; in-wave scan of the MB lengths */
         uint32_t mlen = 0;
-        int kd = -1, ref = 0, mv4 = 0, px = 0, py = 0, code = 0, cbp = 0;
-        if (t < nm) {
+        int kd = -1, hsel = 0, code = 0, cbp = 0;
+        const bool head_over = L.head_over;        /* uniform */
+        if (t < nm && ABL(SCROLL_DEBUG_DYN_NOHEAD)) {
+            mlen = 1;
+        } else if (t < nm) {
             const int m = m0 + t, row = (int)div_m((uint32_t)m, m_mbw), col = m - row * mbw;
             const bool curA = row < a_end, abvA = (row - 1) < a_end;
-            ref = curA ? rg.ra : rg.rb;
-            mv4 = 4 * (curA ? rg.mva : rg.mvb);
-            const int aref = abvA ? rg.ra : rg.rb, amv4 = 4 * (abvA ? rg.mva : rg.mvb);
-            predict(col, row, mbw, ref, mv4, aref, amv4, px, py);
-            CountSink mc{0};
-            put_mb_head(mc, ref, 0 - px, mv4 - py, nrefs);
+            hsel = 3 * (row == 0 ? 0 : (curA ? 1 : (abvA ? 2 : 3))) +
+                   (col == 0 ? 0 : (col == mbw - 1 ? 2 : 1));
+            CountSink mc{head_over ? 0u : L.hlen[hsel]};
+            if (head_over) {                       /* > 128-bit heads: per MB */
+                const int ref = curA ? rg.ra : rg.rb, mv4 = 4 * (curA ? rg.mva : rg.mvb);
+                const int aref = abvA ? rg.ra : rg.rb, amv4 = 4 * (abvA ? rg.mva : rg.mvb);
+                int px, py;
+                predict(col, row, mbw, ref, mv4, aref, amv4, px, py);
+                put_mb_head(mc, ref, 0 - px, mv4 - py, nrefs);
+            }
             const bool isdyn = col >= R.x0 && col < R.x0 + R.w && row >= R.y0 && row < R.y0 + R.h;
             if (!isdyn) {
                 mlen = mc.n + 1u;                  /* + coded_block_pattern ue(0) */
             } else {
                 kd = (row - R.y0) * R.w + (col - R.x0) - q0;
-                const uint8_t *tc = L.tc[kd];
+                /* bulk LDS reads (no dependent chains): TotalCoeff, lengths */
+                const uint4 t0 = *reinterpret_cast<const uint4 *>(L.tc[kd]);
+                const uint2 t1 = *reinterpret_cast<const uint2 *>(L.tc[kd] + 16);
+                const uint32_t tw[6] = {t0.x, t0.y, t0.z, t0.w, t1.x, t1.y};
                 int cbp_l = 0;
 #pragma unroll
-                for (int b8 = 0; b8 < 4; ++b8) {
-                    const int r0 = 8 * (b8 >> 1) + 2 * (b8 & 1);
-                    if (tc[r0] | tc[r0 + 1] | tc[r0 + 4] | tc[r0 + 5]) cbp_l |= 1 << b8;
+                for (int b8 = 0; b8 < 4; ++b8) {             /* rows 2(b8>>1), +1; cols 2(b8&1), +1 */
+                    const int r0 = 2 * (b8 >> 1), sh = 16 * (b8 & 1);
+                    if (((tw[r0] >> sh) & 0xffffu) | ((tw[r0 + 1] >> sh) & 0xffffu)) cbp_l |= 1 << b8;
                 }
-                uint32_t ac = 0;
-#pragma unroll
-                for (int k2 = 16; k2 < 24; ++k2) ac |= tc[k2];
+                const uint32_t ac = tw[4] | tw[5];
                 const int16_t *dl = &L.dclv[kd][0][0];
                 int anydc = 0;
 #pragma unroll
@@ -631,24 +674,36 @@ __global__ __launch_bounds__(DT, SCROLL_DYN_WAVES) void k_dyn_stage(DevStream *_
                 L.cbp[kd] = (uint8_t)cbp;
                 put_ue(mc, (uint32_t)code);
                 if (cbp) put_se(mc, 0);            /* mb_qp_delta */
+                uint32_t bl[32], bo[32];
+#pragma unroll
+                for (int v = 0; v < 4; ++v) {
+                    const uint4 x = reinterpret_cast<const uint4 *>(L.blen[kd])[v];
+                    const uint32_t xw[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+                    for (int h = 0; h < 4; ++h) {
+                        bl[8 * v + 2 * h] = xw[h] & 0xffffu;
+                        bl[8 * v + 2 * h + 1] = xw[h] >> 16;
+                    }
+                }
                 uint32_t off = mc.n;
-                for (int blk = 0; blk < 16; ++blk) {
+#pragma unroll
+                for (int blk = 0; blk < 16; ++blk) {       /* luma4x4BlkIdx order */
                     const int r = blk_raster(blk);
-                    L.boff[kd][r] = (uint16_t)off;
-                    off += L.blen[kd][r];
+                    bo[r] = off;
+                    off += bl[r];
                 }
-                if (cbp_c) {
-                    for (int p = 0; p < 2; ++p) {
-                        L.boff[kd][16 + p] = (uint16_t)off;
-                        off += L.blen[kd][16 + p];
-                    }
+#pragma unroll
+                for (int k2 = 16; k2 < 26; ++k2) {         /* Cb DC, Cr DC, Cb AC 0-3, Cr AC 0-3 */
+                    bo[k2] = off;
+                    off += (k2 < 18 ? cbp_c >= 1 : cbp_c == 2) ? bl[k2] : 0u;
                 }
-                if (cbp_c == 2) {
-                    for (int k2 = 18; k2 < 26; ++k2) {
-                        L.boff[kd][k2] = (uint16_t)off;
-                        off += L.blen[kd][k2];
-                    }
-                }
+#pragma unroll
+                for (int k2 = 26; k2 < 32; ++k2) bo[k2] = 0;
+#pragma unroll
+                for (int v = 0; v < 4; ++v)
+                    reinterpret_cast<uint4 *>(L.boff[kd])[v] =
+                        make_uint4(bo[8 * v] | bo[8 * v + 1] << 16, bo[8 * v + 2] | bo[8 * v + 3] << 16,
+                                   bo[8 * v + 4] | bo[8 * v + 5] << 16, bo[8 * v + 6] | bo[8 * v + 7] << 16);
                 mlen = off;
             }
         }
@@ -687,19 +742,29 @@ __global__ __launch_bounds__(DT, SCROLL_DYN_WAVES) void k_dyn_stage(DevStream *_
         const uint32_t my_mbo = t < nm ? mbo(t) : 0u;
         for (uint32_t p0 = 0; p0 < nw; p0 += PW) {
             const LdsOrWin win{L.buf, p0, PW};
-            if (t < nm) {                          /* MB head (+ cbp, qp_delta) */
+            if (t < nm && !ABL(SCROLL_DEBUG_DYN_NOWRITE | SCROLL_DEBUG_DYN_NOHEAD)) {   /* MB head */
                 WSink sk{win, 0, 0, 0};
                 sk.start(F + my_mbo);
-                if (kd < 0) {
-                    put_mb(sk, ref, 0, mv4 - py, nrefs);
+                if (!head_over) {
+                    sk.put_cap(CapSink{L.hhi[hsel], L.hlo[hsel], L.hlen[hsel]});
                 } else {
-                    put_mb_head(sk, ref, 0, mv4 - py, nrefs);
+                    const int m = m0 + t, row = (int)div_m((uint32_t)m, m_mbw), col = m - row * mbw;
+                    const bool curA = row < a_end, abvA = (row - 1) < a_end;
+                    const int ref = curA ? rg.ra : rg.rb, mv4 = 4 * (curA ? rg.mva : rg.mvb);
+                    const int aref = abvA ? rg.ra : rg.rb, amv4 = 4 * (abvA ? rg.mva : rg.mvb);
+                    int px, py;
+                    predict(col, row, mbw, ref, mv4, aref, amv4, px, py);
+                    put_mb_head(sk, ref, 0 - px, mv4 - py, nrefs);
+                }
+                if (kd < 0) {
+                    sk.put(1, 1);                  /* coded_block_pattern ue(0) */
+                } else {
                     put_ue(sk, (uint32_t)code);
                     if (cbp) put_se(sk, 0);
                 }
                 sk.finish();
             }
-            if ((enc >> 31) && bcap.n) {
+            if ((enc >> 31) && bcap.n && !ABL(SCROLL_DEBUG_DYN_NOWRITE)) {
                 const int e_k = (int)(enc & 255u), e_pc = (int)((enc >> 8) & 255u);
                 WSink sk{win, 0, 0, 0};
                 sk.start(F + mbo((int)((enc >> 16) & 255u)) + L.boff[e_k][e_pc]);
@@ -712,7 +777,7 @@ __global__ __launch_bounds__(DT, SCROLL_DYN_WAVES) void k_dyn_stage(DevStream *_
                 }
                 sk.finish();
             }
-            if (t < 2 * nd) {                      /* chroma DC, re-encoded from LDS */
+            if (t < 2 * nd && !ABL(SCROLL_DEBUG_DYN_NOWRITE)) {   /* chroma DC, from LDS */
                 const int k = t >> 1, p = t & 1;
                 if (L.cbp[k] >> 4) {
                     int ry, cx;

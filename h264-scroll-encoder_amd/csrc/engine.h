@@ -84,7 +84,7 @@ typedef struct {
 typedef struct {
     int32_t x0, y0, w, h;           /* rect, MB units                             */
     int32_t ring;                   /* rows in the TotalCoeff ring                */
-    int32_t pad;
+    int32_t debug;                  /* SCROLL_DEBUG_DYN_* ablation bits           */
     uint64_t src_ld, src_fr;        /* source bytes per stream / per frame        */
     uint64_t ref_ld;                /* reference-pair bytes per stream (0 shared) */
     uint64_t slot_bytes;            /* staging bytes per frame                    */

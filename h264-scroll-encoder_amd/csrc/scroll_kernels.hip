@@ -1168,6 +1168,7 @@ static int launch(ScrollBatch *b, int nframes, int plan_mode, int nal_max, hipSt
             HIPCHK(hipMemsetAsync(b->d_dbg, 0, slots * 8 * sizeof(uint64_t), hs));
             stamps = b->d_dbg;
         }
+        b->geo.debug = b->debug;
         if (dyn_launch_stage(hs, nframes, S, b->d_st, b->d_nal, b->ld_nal, b->d_pend, b->d_dfr,
                              ld_fr, &b->geo, b->d_src, b->d_refs, b->d_stage, stamps)) {
             set_err("k_dyn_stage launch: %s", hipGetErrorString(hipGetLastError()));

@@ -32,6 +32,10 @@ SCROLL_DEBUG_EMIT_NOMIXED = 32
 SCROLL_DEBUG_EMIT_STAMPS = 64
 SCROLL_DEBUG_EMIT_NOBYTES = 128
 SCROLL_DEBUG_DYN_STAMPS = 256
+SCROLL_DEBUG_DYN_NOLOAD = 512
+SCROLL_DEBUG_DYN_NOCAVLC = 1024
+SCROLL_DEBUG_DYN_NOHEAD = 2048
+SCROLL_DEBUG_DYN_NOWRITE = 4096
 SCROLL_COMPOSE_REWIND = 1
 MAX_WAYPOINTS = 8
 MV_LIMIT_PX = 496

@@ -59,6 +59,13 @@ extern "C" {
 #define SCROLL_DEBUG_EMIT_STAMPS 64 /* k_emit records s_memtime per phase per wave */
 #define SCROLL_DEBUG_EMIT_NOBYTES 128 /* k_emit skips the tile-end partial chunks  */
 #define SCROLL_DEBUG_DYN_STAMPS 256 /* k_dyn_stage: s_memtime per phase per NAL   */
+/* k_dyn_stage ablations (builds with -DSCROLL_DYN_ABLATE=1 only; timing only, outputs
+ * wrong): skip the pixel loads /
+ * the block CAVLC / the MB-head work / the bit writes */
+#define SCROLL_DEBUG_DYN_NOLOAD  512
+#define SCROLL_DEBUG_DYN_NOCAVLC 1024
+#define SCROLL_DEBUG_DYN_NOHEAD  2048
+#define SCROLL_DEBUG_DYN_NOWRITE 4096
 
 typedef struct ScrollBatch ScrollBatch;
 

@@ -32,7 +32,7 @@ static_assert(sizeof(NalDesc) == 32, "NalDesc must stay 32 B");
 namespace {
 
 #ifndef SCROLL_TILE
-#define SCROLL_TILE 32
+#define SCROLL_TILE 16
 #endif
 #ifndef SCROLL_EMIT_WAVES
 #define SCROLL_EMIT_WAVES 1
@@ -883,6 +883,8 @@ struct ScrollBatch {
     int timed_pending = 0;
     float ms[4] = {0, 0, 0, 0};        /* plan, emit, dyn stage, dyn emit */
     std::vector<hipEvent_t> ring;      /* NEV events per timed compose, pending */
+    std::vector<uint8_t> ring_dyn;     /* per pending compose: the dynamic-rect pipeline ran */
+    int ev_dyn = 0;                    /* the same for b->ev */
     int ring_used = 0;
     double acc_ms[4] = {0, 0, 0, 0};
     int acc_n = 0;
@@ -903,17 +905,32 @@ struct ScrollBatch {
     uint8_t *d_src = nullptr, *d_refs = nullptr, *d_stage = nullptr;
 };
 
-/* event pairs of one compose: plan = [0,1) + [2,3), dyn stage [1,2),
- * emit [3,4), dyn emit [4,5) */
-static void event_ms(const hipEvent_t *e, float out[4])
+/* event pairs of one compose.  Dynamic rect: plan = [0,1) + [2,3), dyn
+ * stage [1,2), emit [3,4), dyn emit [4,5).  Otherwise only events 0, 1, 4
+ * are recorded (fewer markers between the kernels): plan [0,1), emit [1,4). */
+static void event_ms(const hipEvent_t *e, bool dyn, float out[4])
 {
-    float x[NEV - 1] = {};
-    for (int i = 0; i + 1 < NEV; ++i)
-        if (hipEventElapsedTime(&x[i], e[i], e[i + 1]) != hipSuccess) x[i] = 0.0f;
-    out[0] = x[0] + x[2];
-    out[1] = x[3];
-    out[2] = x[1];
-    out[3] = x[4];
+    auto el = [&](int a, int b) {
+        float v = 0.0f;
+        return hipEventElapsedTime(&v, e[a], e[b]) == hipSuccess ? v : 0.0f;
+    };
+    if (dyn) {
+        out[0] = el(0, 1) + el(2, 3);
+        out[1] = el(3, 4);
+        out[2] = el(1, 2);
+        out[3] = el(4, 5);
+    } else {
+        out[0] = el(0, 1);
+        out[1] = el(1, 4);
+        out[2] = out[3] = 0.0f;
+    }
+}
+
+/* timing-only events: no system-scope fence on record (no cache writeback /
+ * invalidate between the kernels being timed) */
+static hipError_t timing_event(hipEvent_t *e)
+{
+    return hipEventCreateWithFlags(e, hipEventDisableSystemFence);
 }
 
 extern "C" {
@@ -967,7 +984,7 @@ int scroll_batch_create(ScrollBatch **out, const ScrollBatchDesc *desc)
     if (e == hipSuccess) e = hipMalloc(&b->d_arena, S * b->ld_arena);
     if (e == hipSuccess) e = hipMalloc(&b->d_pend, S * sizeof(PlanPending));
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&b->own, hipStreamNonBlocking);
-    for (int i = 0; i < NEV && e == hipSuccess; ++i) e = hipEventCreate(&b->ev[i]);
+    for (int i = 0; i < NEV && e == hipSuccess; ++i) e = timing_event(&b->ev[i]);
     if (e == hipSuccess) e = hipMemset(b->d_st, 0, S * sizeof(DevStream));
     if (e == hipSuccess) e = hipMemset(b->d_off, 0, S * (size_t)desc->max_frames * sizeof(int32_t));
     if (e != hipSuccess) {
@@ -1098,7 +1115,7 @@ static void fold_ring(ScrollBatch *b)
 {
     for (int i = 0; i + NEV <= b->ring_used; i += NEV) {
         float m[4];
-        event_ms(&b->ring[i], m);
+        event_ms(&b->ring[i], b->ring_dyn[i / NEV] != 0, m);
         for (int k = 0; k < 4; ++k) b->acc_ms[k] += m[k];
         b->acc_n++;
     }
@@ -1114,9 +1131,10 @@ static int ring_events(ScrollBatch *b, hipEvent_t **evs)
         } else {
             for (int i = 0; i < NEV; ++i) {
                 hipEvent_t e;
-                HIPCHK(hipEventCreate(&e));
+                HIPCHK(timing_event(&e));
                 b->ring.push_back(e);
             }
+            b->ring_dyn.push_back(0);
         }
     }
     *evs = &b->ring[b->ring_used];
@@ -1134,13 +1152,17 @@ static int launch(ScrollBatch *b, int nframes, int plan_mode, int nal_max, hipSt
         int rc = ring_events(b, &rev);
         if (rc) return rc;
     }
+    const bool dyn = b->dyn_on && plan_mode != SCROLL_PLAN_EXPLICIT;
     auto mark = [&](int k) -> int {
-        if (!b->timing) return SCROLL_OK;
+        if (!b->timing || (!dyn && k != 0 && k != 1 && k != 4)) return SCROLL_OK;
         HIPCHK(hipEventRecord(b->ev[k], hs));
         HIPCHK(hipEventRecord(rev[k], hs));
         return SCROLL_OK;
     };
-    const bool dyn = b->dyn_on && plan_mode != SCROLL_PLAN_EXPLICIT;
+    if (b->timing) {
+        b->ring_dyn[(b->ring_used - NEV) / NEV] = dyn ? 1 : 0;
+        b->ev_dyn = dyn ? 1 : 0;
+    }
     const int ld_fr = b->max_frames;
     int rc = mark(0);
     if (rc) return rc;
@@ -1245,7 +1267,7 @@ int scroll_batch_sync(ScrollBatch *b)
         if (rc0) return rc0;
     }
     if (b->timed_pending) {
-        event_ms(b->ev, b->ms);
+        event_ms(b->ev, b->ev_dyn != 0, b->ms);
         b->timed_pending = 0;
     }
     int rc = SCROLL_OK;
@@ -1581,7 +1603,7 @@ float scroll_batch_kernel_ms(ScrollBatch *b, int which)
     if (!b || which < 0 || which > 3) return -1.0f;
     if (batch_host_sync(b)) return -1.0f;
     if (b->timed_pending) {
-        event_ms(b->ev, b->ms);
+        event_ms(b->ev, b->ev_dyn != 0, b->ms);
         b->timed_pending = 0;
     }
     return b->ms[which];

@@ -17,6 +17,9 @@ A step = one scroll_batch_compose over every stream of the rank:
   pictures, one copy per stream; all resident in HBM before timing.
   workload p720 (BASELINE config 2): 256 streams x 1024 composed frames,
   P-only (no dynamic rect).
+  workload p4kdyn (BASELINE config 5 per GPU): 128 streams x 16 composed
+  3840x2160 frames with a 720x720 rect (47x47 MBs); config 4 = p720dyn with
+  --streams 1024 per GPU on 8 GPUs.
   Offsets = SURVEY 8(d) synthetic scroll (speed 1+(s%8), phase 97 s mod 1440)
   in HBM; output arenas are rewound on device at every step (the bytes of a
   step are the product).
@@ -39,10 +42,14 @@ HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 NAL_DESC_BYTES = 32            # NalDesc read per NAL by k_emit
 
 WORKLOADS = {
-    "p720dyn": dict(w=1280, h=720, streams=256, frames=16, rect=(28, 10, 25, 25),
+    "p720dyn": dict(w=1280, h=720, streams=256, frames=16, rect=(28, 10, 25, 25), rect_px=360,
                     desc="BASELINE config 3: 256 concurrent 1280x720 streams + 360x360 "
                          "synthetic dynamic rect (4x4 int transform + quant + CAVLC), "
                          "composer_write_scroll_frame semantics"),
+    "p4kdyn": dict(w=3840, h=2160, streams=128, frames=16, rect=(96, 44, 47, 47), rect_px=720,
+                   desc="BASELINE config 5 per GPU: 128 concurrent 3840x2160 streams (1024 over 8 "
+                        "GPUs) + 720x720 dynamic rect (47x47 MBs, +16 px margin); the scroll passes "
+                        "496/992/1488/1984 -> up to 6 reference pictures"),
     "p720": dict(w=1280, h=720, streams=256, frames=1024, rect=None,
                  desc="BASELINE config 2: 256 concurrent 1280x720 streams, P-only "
                       "(no dynamic rect), composer_write_scroll_frame semantics"),
@@ -101,7 +108,7 @@ def cpu_baseline(wl, threads):
     lib.or_bench_compose_dyn.restype = ctypes.c_double
     if wl["rect"]:
         x0, y0, rw, rh = wl["rect"]
-        nstreams, nframes = 4 * threads, 64
+        nstreams, nframes = 4 * threads, max(8, 64 * 625 // (rw * rh))
         nbytes = ctypes.c_ulonglong()
         fps = lib.or_bench_compose_dyn(nstreams, nframes, wl["w"], wl["h"], x0, y0, rw, rh,
                                        threads, ctypes.byref(nbytes))
@@ -109,7 +116,7 @@ def cpu_baseline(wl, threads):
                                         ctypes.byref(nbytes))
         return dict(value=round(fps, 1), unit="frames/s", cores=threads, kind="port",
                     sample=f"{nstreams} streams x {nframes} frames {wl['w']}x{wl['h']} + "
-                           f"360x360 dynamic rect ({rw}x{rh} MBs; same synthetic offsets, 4 source "
+                           f"{wl['rect_px']}x{wl['rect_px']} dynamic rect ({rw}x{rh} MBs; same synthetic offsets, 4 source "
                            f"frames cycled per stream), {threads} pthreads, "
                            f"oracle/dyn_oracle.c -O2",
                     single_core_fps=round(fps1, 1))
@@ -171,6 +178,7 @@ def main():
     per_frame_bound = 2 * (64 + (W // 16) * (H // 16))
     if rect:
         per_frame_bound += 192 * rect[2] * rect[3]      # ~75 B per dynamic MB measured
+        per_frame_bound += 8 * (W // 16) * (H // 16)     # waypoint-heavy headers at 4K
     b = hs.Batch(S, F, F * per_frame_bound + (1 << 20), device=local)
     for _ in range(S):
         b.add_stream(hs.make_config(W, H))

@@ -208,6 +208,23 @@ def test_dyn_720p_config3_device_synth(gpu, oracle):
     assert len(sizes) == F
 
 
+def test_dyn_4k_config5_many_refs(gpu, oracle):
+    """BASELINE config 5 geometry: 3840x2160 with the 720x720 rect (47x47 MBs);
+    offsets walk past 496 / 992 / 1488 / 1984, so the slice carries up to 6
+    reference pictures (ue(ref_idx)) and region-A rows predict through
+    waypoint chains"""
+    w, h = 3840, 2160
+    rect = Rect(96, 44, 47, 47)
+    offs = np.array([[400, 496, 700, 992, 1300, 1488, 1900, 1984, 2100]], np.int32)
+    R = random_refs(w, h, 8)
+    src = synth_source(oracle, 1, offs.shape[1], rect)
+    want = oracle_streams(oracle, w, h, offs, rect, src, R)
+    b, rc = gpu_streams(gpu, w, h, offs, rect, R, src, arena=64 << 20)
+    assert rc == 0, gpu.last_error()
+    check_equal(b, want)
+    assert sum(k == 1 for k, _, _, _ in b.nals(0)) == 4          # four waypoint NALs
+
+
 def test_dyn_chunked_composes_and_experiment_mode(gpu, oracle):
     w, h = 64, 512
     rect = Rect(0, 5, 4, 9)

@@ -15,7 +15,7 @@ int dyn_launch_stage(hipStream_t hs, int nframes, int S, DevStream *st, const Na
                      uint64_t *stamps);
 int dyn_launch_emit(hipStream_t hs, int nframes, int S, const DevStream *st, const NalDesc *nal,
                     int ld_nal, const DynFrame *dfr, int ld_fr, const DynGeom *g,
-                    const uint8_t *stage, uint8_t *arena, uint64_t ld_arena);
+                    const uint8_t *stage, uint8_t *arena, uint64_t ld_arena, uint64_t *stamps);
 int dyn_launch_synth(hipStream_t hs, int nframes, int S, uint8_t *src, const DynGeom *g,
                      int stream_base, int t0);
 

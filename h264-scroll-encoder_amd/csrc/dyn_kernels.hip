@@ -41,6 +41,7 @@ constexpr int HDR_MAX = 1024;           /* slice header bits (8 waypoints + MMCO
 constexpr int BUF_WORDS = 1536;        /* 48 Kbit LDS bit buffer; larger windows take passes */
 static_assert(BUF_WORDS * 32 > HDR_MAX + 64, "the slice header fits one buffer");
 constexpr int OBUF = 6400;              /* k_dyn_emit: 127 carry + 5 + 4096 x 1.5 */
+constexpr int EPLIST_MAX = DYN_OVF_BYTES / 4;   /* EP positions kept per NAL (slot tail) */
 
 __device__ inline int wave_incl_max(int v, int lane)
 {
@@ -111,7 +112,8 @@ __device__ inline uint32_t ld32(const uint8_t *p) { return *reinterpret_cast<con
 /* number of EP insertions among the 4 bytes of MSB-first word w whose
  * global indices start at g (only bytes < lim count); prev = index of the
  * last non-zero byte before them, updated */
-__device__ inline uint32_t ep_word(uint32_t w, uint32_t g, uint32_t lim, int &prev)
+__device__ inline uint32_t ep_word(uint32_t w, uint32_t g, uint32_t lim, int &prev,
+                                   uint32_t *list = nullptr, uint32_t *cnt = nullptr)
 {
     uint32_t n = 0;
 #pragma unroll
@@ -119,7 +121,13 @@ __device__ inline uint32_t ep_word(uint32_t w, uint32_t g, uint32_t lim, int &pr
         const uint32_t gi = g + (uint32_t)i;
         if (gi >= lim) break;
         const uint32_t b = (w >> (24 - 8 * i)) & 255u;
-        n += ep_insert(b, (int)gi - 1 - prev) ? 1u : 0u;
+        if (ep_insert(b, (int)gi - 1 - prev)) {
+            n++;
+            if (list) {                              /* RBSP index the 03 precedes */
+                const uint32_t k = atomicAdd(cnt, 1u);
+                if (k < (uint32_t)EPLIST_MAX) list[k] = gi;
+            }
+        }
         if (b) prev = (int)gi;
     }
     return n;
@@ -181,6 +189,7 @@ struct StageLds {
     uint8_t lcarry[8];            /* right-column TotalCoeff of the last dyn MB   */
     int32_t wo[8], wl[8], wv[8];
     int32_t lnz_r, lnz_w;         /* last non-zero staged byte: before / of a flush */
+    uint32_t ep_n;                /* EP positions recorded                         */
     int32_t general;              /* a half-pel waypoint step was met            */
     uint64_t hhi[12], hlo[12];    /* MB head codewords [row type 0..3][first / middle / last] */
     uint32_t hlen[12];
@@ -262,6 +271,7 @@ __global__ __launch_bounds__(DT, SCROLL_DYN_WAVES) void k_dyn_stage(DevStream *_
         L.lnz_r = -1;
         L.lnz_w = -1;
         L.head_over = 0;
+        L.ep_n = 0;
     }
     if (t < 8) {
         L.wo[t] = pend[s].wo[t];
@@ -358,6 +368,8 @@ __global__ __launch_bounds__(DT, SCROLL_DYN_WAVES) void k_dyn_stage(DevStream *_
     uint8_t *slot = stage + ((size_t)s * ld_fr + f) * g.slot_bytes;
     uint32_t *out = reinterpret_cast<uint32_t *>(slot);
     const uint32_t cap_words = (uint32_t)((g.slot_bytes - DYN_OVF_BYTES) / 4) - 4u;
+    /* RBSP positions of the EP bytes (unsorted), for k_dyn_emit's gather */
+    uint32_t *eplist = reinterpret_cast<uint32_t *>(slot + g.slot_bytes - DYN_OVF_BYTES);
     const Tabs &TB = g_tabs;            /* chroma DC and the rare > 128-bit blocks */
     const PTabs &PT = L.ptabs;
 
@@ -382,7 +394,7 @@ __global__ __launch_bounds__(DT, SCROLL_DYN_WAVES) void k_dyn_stage(DevStream *_
                 }
             }
             const uint32_t gb = 4u * (gw0 + jw);
-            my_ep += ep_word(wv, gb, 0xffffffffu, prev);
+            my_ep += ep_word(wv, gb, 0xffffffffu, prev, eplist, &L.ep_n);
             if (wv) atomicMax(&L.lnz_w, (int)gb + last_nz_byte(wv));
         }
     };
@@ -835,7 +847,7 @@ __global__ __launch_bounds__(DT, SCROLL_DYN_WAVES) void k_dyn_stage(DevStream *_
             const uint32_t nb = (F + 1u + 7u) >> 3;
             out[bw] = __builtin_bswap32(wv);
             int prev = L.lnz_r;
-            my_ep += ep_word(wv, 4u * bw, 4u * bw + nb, prev);
+            my_ep += ep_word(wv, 4u * bw, 4u * bw + nb, prev, eplist, &L.ep_n);
             DF->rbsp_bytes = 4u * bw + nb;
         }
     }
@@ -881,6 +893,7 @@ __global__ __launch_bounds__(DT) void k_dyn_emit(const DevStream *__restrict__ s
     const DynFrame df = dfr[(size_t)s * ld_fr + f];
     const int j = df.nal;
     if (j < 0 || j >= st[s].nnal || df.err) return;          /* nnal = 0: nothing committed */
+    if (df.ep <= (uint32_t)EPLIST_MAX) return;               /* k_dyn_emit_gather's NAL */
     const NalDesc d = nal[(size_t)s * ld_nal + j];
     if (d.slow != 2) return;
     uint8_t *A = arena + (size_t)s * ld_arena;
@@ -945,6 +958,161 @@ __global__ __launch_bounds__(DT) void k_dyn_emit(const DevStream *__restrict__ s
 }
 
 /* ---------------------------------------------------------------------- */
+/* k_dyn_emit_gather: the same output for NALs with <= EPLIST_MAX EP bytes  */
+/* (all in practice: 82 per config-3 frame).  k_dyn_stage recorded where    */
+/* the 03 bytes go; after sorting those positions once, every thread builds */
+/* whole 16-byte arena chunks independently -- no barriers, no LDS byte     */
+/* buffer: a chunk without an EP byte is a funnel shift of the staged RBSP. */
+/* ---------------------------------------------------------------------- */
+__device__ inline uint32_t pick4(const uint32_t w[8], int i)     /* w[i], i in 0..7, no indexing */
+{
+    const uint32_t a = (i & 1) ? w[1] : w[0], b = (i & 1) ? w[3] : w[2];
+    const uint32_t c = (i & 1) ? w[5] : w[4], e = (i & 1) ? w[7] : w[6];
+    const uint32_t ab = (i & 2) ? b : a, ce = (i & 2) ? e : c;
+    return (i & 4) ? ce : ab;
+}
+
+__global__ __launch_bounds__(DT) void k_dyn_emit_gather(const DevStream *__restrict__ st,
+                                                        const NalDesc *__restrict__ nal, int ld_nal,
+                                                        const DynFrame *__restrict__ dfr, int ld_fr,
+                                                        DynGeom g, const uint8_t *__restrict__ stage,
+                                                        uint8_t *__restrict__ arena, uint64_t ld_arena,
+                                                        uint64_t *__restrict__ stamps)
+{
+    __shared__ uint32_t raw[EPLIST_MAX], sp[EPLIST_MAX];
+    const int f = blockIdx.x, s = blockIdx.y, t = threadIdx.x;
+    /* debug: realtime at entry / after the sort / at exit, EP count, HW_ID */
+    uint64_t *stp = stamps && t == 0 ? stamps + ((size_t)s * gridDim.x + f) * 8 : nullptr;
+    if (stp) stp[0] = __builtin_amdgcn_s_memrealtime();
+    const DynFrame df = dfr[(size_t)s * ld_fr + f];
+    const int j = df.nal;
+    if (j < 0 || j >= st[s].nnal || df.err) return;          /* nnal = 0: nothing committed */
+    const uint32_t n = df.ep;
+    if (n > (uint32_t)EPLIST_MAX) return;                     /* k_dyn_emit's NAL */
+    const NalDesc d = nal[(size_t)s * ld_nal + j];
+    if (d.slow != 2) return;
+    const uint8_t *in = stage + ((size_t)s * ld_fr + f) * g.slot_bytes;
+    const uint32_t *el = reinterpret_cast<const uint32_t *>(in + g.slot_bytes - DYN_OVF_BYTES);
+    for (uint32_t i = t; i < n; i += DT) raw[i] = el[i];
+    __syncthreads();
+    /* sort by rank (positions are distinct): sp[j] = j-th smallest */
+    for (uint32_t i = t; i < n; i += DT) {
+        const uint32_t v = raw[i];
+        uint32_t r = 0;
+        for (uint32_t k = 0; k < n; ++k) r += raw[k] < v ? 1u : 0u;
+        sp[r] = v;
+    }
+    __syncthreads();
+    if (stp) {
+        stp[1] = __builtin_amdgcn_s_memrealtime();
+        stp[3] = n;
+        stp[4] = (uint64_t)(uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 4);    /* HW_ID */
+    }
+
+    uint8_t *A = arena + (size_t)s * ld_arena;
+    const uint64_t o0 = d.out_off, o1 = o0 + d.size;
+    const uint32_t nin = df.rbsp_bytes;
+    const uint8_t hdr[5] = {0, 0, 0, 1, nal_header_byte(0)};           /* nal.c:59-64 */
+    /* U chunks per thread and iteration: all their loads are in flight
+     * before the first is used (the loop is load-latency bound otherwise) */
+    constexpr int U = 4;
+    const uint64_t cend = (o1 + 15) >> 4;
+    uint32_t K = 0;               /* EP bytes before the current chunk (monotone per thread) */
+    for (uint64_t cb = (o0 >> 4) + (uint64_t)t; cb < cend; cb += (uint64_t)U * DT) {
+        uint32_t Ku[U], epm[U], shv[U];
+        bool inner[U];
+        uint4 x[U], y[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t q0 = (cb + (uint64_t)u * DT) << 4;
+            const int64_t u0 = (int64_t)q0 - (int64_t)o0 - 5;        /* EBSP index of byte 0 */
+            /* the j-th EP byte sits at EBSP index sp[j] + j */
+            while (K < n && (int64_t)(sp[K] + K) < u0) K++;
+            Ku[u] = K;
+            inner[u] = u0 >= 0 && q0 + 16 <= o1;
+            epm[u] = 0;
+            shv[u] = 0;
+            x[u] = y[u] = make_uint4(0, 0, 0, 0);
+            if (inner[u]) {
+                /* interior chunk: EP bytes of the chunk as a mask; output byte
+                 * b takes RBSP byte i0 + b - (EP bytes before b), or is 03 */
+                uint32_t em = 0;
+                for (uint32_t m = K; m < n; ++m) {
+                    const int64_t e = (int64_t)(sp[m] + m) - u0;
+                    if (e >= 16) break;
+                    em |= 1u << e;
+                }
+                epm[u] = em;
+                const uint32_t i0 = (uint32_t)u0 - K, a0 = i0 & ~15u;
+                shv[u] = i0 & 15u;
+                x[u] = *reinterpret_cast<const uint4 *>(in + a0);
+                if (a0 + 16 < nin) y[u] = *reinterpret_cast<const uint4 *>(in + a0 + 16);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t c = cb + (uint64_t)u * DT;
+            if (c >= cend) break;
+            const uint64_t q0 = c << 4;
+            if (inner[u]) {
+                const uint32_t w[8] = {x[u].x, x[u].y, x[u].z, x[u].w, y[u].x, y[u].y, y[u].z, y[u].w};
+                const uint32_t sh = shv[u], em = epm[u];
+                uint32_t o[4];
+                if (em == 0) {                               /* funnel shift */
+                    const int wi = (int)(sh >> 2), bs = (int)(sh & 3u);
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        const uint32_t lo = pick4(w, wi + k), hi = pick4(w, wi + k + 1);
+                        o[k] = bs ? __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)bs) : lo;
+                    }
+                } else {               /* a word's bytes span <= 2 RBSP words: v_perm */
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        const uint32_t b0 = 4u * (uint32_t)k;
+                        const uint32_t r0 = sh + b0 - (uint32_t)__builtin_popcount(em & ((1u << b0) - 1u));
+                        const uint32_t base = r0 >> 2;
+                        const uint32_t lo = pick4(w, (int)base), hi = pick4(w, (int)base + 1);
+                        uint32_t sel = 0, three = 0;
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) {
+                            const uint32_t bb = b0 + (uint32_t)i;
+                            uint32_t v;
+                            if ((em >> bb) & 1u) {
+                                v = 0x0cu;                           /* perm: byte 00 */
+                                three |= 3u << (8 * i);
+                            } else {
+                                v = sh + bb - (uint32_t)__builtin_popcount(em & ((1u << bb) - 1u)) - 4u * base;
+                            }
+                            sel |= v << (8 * i);
+                        }
+                        o[k] = __builtin_amdgcn_perm(hi, lo, sel) | three;
+                    }
+                }
+                *reinterpret_cast<uint4 *>(A + q0) = make_uint4(o[0], o[1], o[2], o[3]);
+            } else {                                     /* NAL edges, start code */
+                uint32_t kk = Ku[u];
+                for (int b = 0; b < 16; ++b) {
+                    const uint64_t q = q0 + (uint64_t)b;
+                    if (q < o0 || q >= o1) continue;
+                    const int64_t uu = (int64_t)q - (int64_t)o0 - 5;
+                    uint8_t v;
+                    if (uu < 0) {
+                        v = hdr[q - o0];
+                    } else if (kk < n && (int64_t)(sp[kk] + kk) == uu) {
+                        v = 3;
+                        kk++;
+                    } else {
+                        v = in[(uint32_t)uu - kk];
+                    }
+                    A[q] = v;
+                }
+            }
+        }
+    }
+    if (stp) stp[2] = __builtin_amdgcn_s_memrealtime();
+}
+
+/* ---------------------------------------------------------------------- */
 /* k_dyn_synth: the synthetic dynamic-rect source of SURVEY §8d            */
 /* (dyn_oracle.h), one thread per pixel                                    */
 /* ---------------------------------------------------------------------- */
@@ -1006,9 +1174,12 @@ int dyn_launch_stage(hipStream_t hs, int nframes, int S, DevStream *st, const Na
 
 int dyn_launch_emit(hipStream_t hs, int nframes, int S, const DevStream *st, const NalDesc *nal,
                     int ld_nal, const DynFrame *dfr, int ld_fr, const DynGeom *g,
-                    const uint8_t *stage, uint8_t *arena, uint64_t ld_arena)
+                    const uint8_t *stage, uint8_t *arena, uint64_t ld_arena, uint64_t *stamps)
 {
     if (nframes <= 0 || S <= 0) return 0;
+    hipLaunchKernelGGL(k_dyn_emit_gather, dim3(nframes, S), dim3(DT), 0, hs, st, nal, ld_nal, dfr,
+                       ld_fr, *g, stage, arena, ld_arena, stamps);
+    if (hipGetLastError() != hipSuccess) return -1;
     hipLaunchKernelGGL(k_dyn_emit, dim3(nframes, S), dim3(DT), 0, hs, st, nal, ld_nal, dfr, ld_fr,
                        *g, stage, arena, ld_arena);
     return hipGetLastError() == hipSuccess ? 0 : -1;

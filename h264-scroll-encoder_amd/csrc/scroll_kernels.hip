@@ -1180,8 +1180,8 @@ static int launch(ScrollBatch *b, int nframes, int plan_mode, int nal_max, hipSt
         HIPCHK(hipGetLastError());
         if ((rc = mark(1))) return rc;
         uint64_t *stamps = nullptr;
-        if (b->debug & SCROLL_DEBUG_DYN_STAMPS) {
-            const size_t slots = (size_t)nframes * S;
+        if (b->debug & SCROLL_DEBUG_DYN_STAMPS) {   /* k_dyn_stage's, then k_dyn_emit's */
+            const size_t slots = 2 * (size_t)nframes * S;
             if (slots > b->dbg_slots) {
                 if (b->d_dbg) (void)hipFree(b->d_dbg);
                 HIPCHK(hipMalloc(&b->d_dbg, slots * 8 * sizeof(uint64_t)));
@@ -1222,7 +1222,9 @@ static int launch(ScrollBatch *b, int nframes, int plan_mode, int nal_max, hipSt
     }
     if ((rc = mark(4))) return rc;
     if (dyn && dyn_launch_emit(hs, nframes, S, b->d_st, b->d_nal, b->ld_nal, b->d_dfr, ld_fr,
-                               &b->geo, b->d_stage, b->d_arena, (uint64_t)b->ld_arena)) {
+                               &b->geo, b->d_stage, b->d_arena, (uint64_t)b->ld_arena,
+                               (b->debug & SCROLL_DEBUG_DYN_STAMPS) && b->d_dbg
+                                   ? b->d_dbg + (size_t)nframes * S * 8 : nullptr)) {
         set_err("k_dyn_emit launch: %s", hipGetErrorString(hipGetLastError()));
         return SCROLL_ERR_HIP;
     }

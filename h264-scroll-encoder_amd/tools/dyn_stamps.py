@@ -80,9 +80,10 @@ def main():
     b.set_debug(hs.SCROLL_DEBUG_DYN_STAMPS)
     b.compose(F, rewind=True)
     assert b.sync() == 0, hs.last_error()
-    buf = (ctypes.c_uint64 * (S * F * 8))()
-    got = hs.lib.scroll_batch_debug_stamps(b.h, buf, S * F)
-    a = np.frombuffer(buf, dtype=np.uint64).reshape(-1, 8)[:got].astype(np.float64)
+    buf = (ctypes.c_uint64 * (2 * S * F * 8))()
+    got = hs.lib.scroll_batch_debug_stamps(b.h, buf, 2 * S * F)
+    allst = np.frombuffer(buf, dtype=np.uint64).reshape(-1, 8)[:got]
+    a = allst[:S * F].astype(np.float64)
     names = ["A levels", "B cavlc", "C offsets", "D bits", "E flush"]
     tot = a[:, 6].mean()
     print(f"{got} NALs, windows/NAL {a[:, 5].mean():.1f}, cycles/NAL {tot:.0f} "
@@ -92,6 +93,20 @@ def main():
         print(f"  {nm:10s} {m:10.0f} cycles/NAL  {m / a[:, 5].mean():8.0f} /window  {100 * m / tot:5.1f} %")
     rest = tot - a[:, :5].sum(1).mean()
     print(f"  {'setup+tail':10s} {rest:10.0f} cycles/NAL  {100 * rest / tot:5.1f} %")
+    e = allst[S * F:].astype(np.int64)          # k_dyn_emit_gather: realtime (100 MHz)
+    e = e[e[:, 0] > 0]
+    if len(e):
+        t0 = e[:, 0].min()
+        span = (e[:, 2].max() - t0) / 100.0
+        dur = (e[:, 2] - e[:, 0]) / 100.0
+        srt = (e[:, 1] - e[:, 0]) / 100.0
+        print(f"k_dyn_emit_gather: {len(e)} WGs, span {span:.1f} us, WG duration mean {dur.mean():.1f} "
+              f"p50 {np.percentile(dur, 50):.1f} p99 {np.percentile(dur, 99):.1f} max {dur.max():.1f} us, "
+              f"prologue+sort mean {srt.mean():.1f} us")
+        st0 = (e[:, 0] - t0) / 100.0
+        print("  WG start times (us) p0/25/50/75/100:", np.percentile(st0, [0, 25, 50, 75, 100]).round(1))
+        conc = [(np.sum((e[:, 0] <= x) & (e[:, 2] > x))) for x in np.linspace(t0, e[:, 2].max(), 12)]
+        print("  resident WGs over time:", conc)
     b.close()
 
 

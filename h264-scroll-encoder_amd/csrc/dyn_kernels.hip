@@ -133,6 +133,18 @@ __device__ inline uint32_t ep_word(uint32_t w, uint32_t g, uint32_t lim, int &pr
     return n;
 }
 
+/* Workgroup (x, s) -> frame: rotated by the stream so that consecutive
+ * workgroups -- which the dispatcher deals round-robin to the 8 XCDs --
+ * mix frame indices; the residual cost of a frame depends on t, and without
+ * the rotation frame f of every stream lands on XCD f % 8 (frames >= 8). */
+__device__ inline int dyn_frame_of(int x, int s)
+{
+    const int F = (int)gridDim.x;
+    int r = x + (s & 7);                     /* uniform: no integer division */
+    while (r >= F) r -= F;
+    return __builtin_amdgcn_readfirstlane(r);
+}
+
 /* ---------------------------------------------------------------------- */
 /* k_dyn_stage                                                             */
 /* ---------------------------------------------------------------------- */
@@ -257,7 +269,7 @@ __global__ __launch_bounds__(DT, SCROLL_DYN_WAVES) void k_dyn_stage(DevStream *_
         }
     };
     if (stamps) t_start = t_last = __builtin_amdgcn_s_memtime();
-    const int f = blockIdx.x, s = blockIdx.y, t = threadIdx.x;
+    const int s = blockIdx.y, f = dyn_frame_of(blockIdx.x, s), t = threadIdx.x;
     const int lane = t & 63, wave = t >> 6;
     DevStream *S = st + s;
     DynFrame *DF = dfr + (size_t)s * ld_fr + f;
@@ -980,7 +992,7 @@ __global__ __launch_bounds__(DT) void k_dyn_emit_gather(const DevStream *__restr
                                                         uint64_t *__restrict__ stamps)
 {
     __shared__ uint32_t raw[EPLIST_MAX], sp[EPLIST_MAX];
-    const int f = blockIdx.x, s = blockIdx.y, t = threadIdx.x;
+    const int s = blockIdx.y, f = dyn_frame_of(blockIdx.x, s), t = threadIdx.x;
     /* debug: realtime at entry / after the sort / at exit, EP count, HW_ID */
     uint64_t *stp = stamps && t == 0 ? stamps + ((size_t)s * gridDim.x + f) * 8 : nullptr;
     if (stp) stp[0] = __builtin_amdgcn_s_memrealtime();
@@ -1017,7 +1029,8 @@ __global__ __launch_bounds__(DT) void k_dyn_emit_gather(const DevStream *__restr
      * before the first is used (the loop is load-latency bound otherwise) */
     constexpr int U = 4;
     const uint64_t cend = (o1 + 15) >> 4;
-    uint32_t K = 0;               /* EP bytes before the current chunk (monotone per thread) */
+    int lg = 0;                   /* binary-search steps: 2^lg > n */
+    while ((1u << lg) <= n) lg++;
     for (uint64_t cb = (o0 >> 4) + (uint64_t)t; cb < cend; cb += (uint64_t)U * DT) {
         uint32_t Ku[U], epm[U], shv[U];
         bool inner[U];
@@ -1026,8 +1039,14 @@ __global__ __launch_bounds__(DT) void k_dyn_emit_gather(const DevStream *__restr
         for (int u = 0; u < U; ++u) {
             const uint64_t q0 = (cb + (uint64_t)u * DT) << 4;
             const int64_t u0 = (int64_t)q0 - (int64_t)o0 - 5;        /* EBSP index of byte 0 */
-            /* the j-th EP byte sits at EBSP index sp[j] + j */
-            while (K < n && (int64_t)(sp[K] + K) < u0) K++;
+            /* K = EP bytes before the chunk; the j-th sits at EBSP index
+             * sp[j] + j (strictly increasing): branch-free binary search,
+             * the U searches of an iteration are independent */
+            uint32_t K = 0;
+            for (int b = lg - 1; b >= 0; --b) {
+                const uint32_t k2 = K + (1u << b);
+                K = k2 <= n && (int64_t)(sp[k2 - 1] + (k2 - 1)) < u0 ? k2 : K;
+            }
             Ku[u] = K;
             inner[u] = u0 >= 0 && q0 + 16 <= o1;
             epm[u] = 0;

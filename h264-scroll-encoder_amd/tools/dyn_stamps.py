@@ -86,7 +86,7 @@ def main():
     a = allst[:S * F].astype(np.float64)
     names = ["A levels", "B cavlc", "C offsets", "D bits", "E flush"]
     tot = a[:, 6].mean()
-    print(f"{got} NALs, windows/NAL {a[:, 5].mean():.1f}, cycles/NAL {tot:.0f} "
+    print(f"{S * F} NALs, windows/NAL {a[:, 5].mean():.1f}, cycles/NAL {tot:.0f} "
           f"(min {a[:, 6].min():.0f} max {a[:, 6].max():.0f})")
     for k, nm in enumerate(names):
         m = a[:, k].mean()

@@ -23,16 +23,16 @@
 
 #include "dyn_device.h"
 #include "dyn_engine.h"
+#include "stage_util.h"
 
 using namespace scroll;
 using namespace scroll::dyn;
+using namespace scroll::stage;
 
 namespace {
 
 __constant__ Tabs g_tabs = SCROLL_DYN_TABS;
 
-constexpr int DT = 256;                 /* threads per workgroup                */
-constexpr int NW = DT / 64;
 constexpr int WMB = DYN_WINDOW_MBS;     /* dynamic MBs per window: 24 x 10 = 240 block tasks */
 static_assert(24 * WMB <= 256, "one block task per thread");
 constexpr int WIN = DT;                 /* MBs per window (one MB per thread)    */
@@ -41,109 +41,8 @@ constexpr int HDR_MAX = 1024;           /* slice header bits (8 waypoints + MMCO
 constexpr int BUF_WORDS = 1536;        /* 48 Kbit LDS bit buffer; larger windows take passes */
 static_assert(BUF_WORDS * 32 > HDR_MAX + 64, "the slice header fits one buffer");
 constexpr int OBUF = 6400;              /* k_dyn_emit: 127 carry + 5 + 4096 x 1.5 */
-constexpr int EPLIST_MAX = DYN_OVF_BYTES / 4;   /* EP positions kept per NAL (slot tail) */
-
-__device__ inline int wave_incl_max(int v, int lane)
-{
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const int u = __shfl_up(v, d, 64);
-        if (lane >= d) v = max(v, u);
-    }
-    return v;
-}
-
-__device__ inline uint32_t wave_incl_sum(uint32_t v, int lane)
-{
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t u = __shfl_up(v, d, 64);
-        if (lane >= d) v += u;
-    }
-    return v;
-}
-
-/* exclusive prefix max over the workgroup (identity -1) and the total;
- * ends with a barrier so `ws` can be reused */
-__device__ inline void block_excl_max(int v, int *ws, int &excl, int &tot)
-{
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int incl = wave_incl_max(v, lane);
-    if (lane == 63) ws[wave] = incl;
-    int e = __shfl_up(incl, 1, 64);
-    if (lane == 0) e = -1;
-    __syncthreads();
-    int pm = -1, t = -1;
-#pragma unroll
-    for (int w = 0; w < NW; ++w) {
-        if (w < wave) pm = max(pm, ws[w]);
-        t = max(t, ws[w]);
-    }
-    excl = max(pm, e);
-    tot = t;
-    __syncthreads();
-}
-
-__device__ inline void block_excl_sum(uint32_t v, uint32_t *ws, uint32_t &excl, uint32_t &tot)
-{
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const uint32_t incl = wave_incl_sum(v, lane);
-    if (lane == 63) ws[wave] = incl;
-    __syncthreads();
-    uint32_t pm = 0, t = 0;
-#pragma unroll
-    for (int w = 0; w < NW; ++w) {
-        if (w < wave) pm += ws[w];
-        t += ws[w];
-    }
-    excl = pm + incl - v;
-    tot = t;
-    __syncthreads();
-}
-
-struct LdsOr {
-    uint32_t *b;
-    __device__ inline void operator()(uint32_t i, uint32_t v) const { atomicOr(&b[i], v); }
-};
-typedef OrSink<LdsOr> LSink;
 
 __device__ inline uint32_t ld32(const uint8_t *p) { return *reinterpret_cast<const uint32_t *>(p); }
-
-/* number of EP insertions among the 4 bytes of MSB-first word w whose
- * global indices start at g (only bytes < lim count); prev = index of the
- * last non-zero byte before them, updated */
-__device__ inline uint32_t ep_word(uint32_t w, uint32_t g, uint32_t lim, int &prev,
-                                   uint32_t *list = nullptr, uint32_t *cnt = nullptr)
-{
-    uint32_t n = 0;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const uint32_t gi = g + (uint32_t)i;
-        if (gi >= lim) break;
-        const uint32_t b = (w >> (24 - 8 * i)) & 255u;
-        if (ep_insert(b, (int)gi - 1 - prev)) {
-            n++;
-            if (list) {                              /* RBSP index the 03 precedes */
-                const uint32_t k = atomicAdd(cnt, 1u);
-                if (k < (uint32_t)EPLIST_MAX) list[k] = gi;
-            }
-        }
-        if (b) prev = (int)gi;
-    }
-    return n;
-}
-
-/* Workgroup (x, s) -> frame: rotated by the stream so that consecutive
- * workgroups -- which the dispatcher deals round-robin to the 8 XCDs --
- * mix frame indices; the residual cost of a frame depends on t, and without
- * the rotation frame f of every stream lands on XCD f % 8 (frames >= 8). */
-__device__ inline int dyn_frame_of(int x, int s)
-{
-    const int F = (int)gridDim.x;
-    int r = x + (s & 7);                     /* uniform: no integer division */
-    while (r >= F) r -= F;
-    return __builtin_amdgcn_readfirstlane(r);
-}
 
 /* ---------------------------------------------------------------------- */
 /* k_dyn_stage                                                             */
@@ -226,10 +125,6 @@ struct LdsOrWin {
 };
 typedef OrSink<LdsOrWin> WSink;
 
-__device__ inline int last_nz_byte(uint32_t w)      /* MSB-first byte index, w != 0 */
-{
-    return 3 - (__builtin_ctz(w) >> 3);
-}
 
 /* GENERAL = false: every waypoint step is full-pel (always so for waypoints
  * the composer creates); a NAL that meets a half-pel step is flagged and

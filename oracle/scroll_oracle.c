@@ -195,9 +195,6 @@ static void or_hdr_wp(or_bits *b, const or_cfg *c, int fn, int is_ref, int lt_id
 /* ------------------------------------------------------------------------ */
 /* MV prediction: src/h264_writer.c:356-432                                  */
 /* ------------------------------------------------------------------------ */
-typedef struct {
-    int mx, my, ref, avail;
-} or_mvi;
 
 /* median3 :362-367 -- NOT a true median (returns c when c < min(a,b)) */
 static int or_median3(int a, int b, int c)
@@ -208,8 +205,8 @@ static int or_median3(int a, int b, int c)
     return b > a ? b : a;
 }
 
-static void or_predict(int x, int y, int mbw, const or_mvi *above, const or_mvi *left,
-                       int ref, int *px, int *py)
+void or_predict(int x, int y, int mbw, const or_mvi *above, const or_mvi *left,
+                int ref, int *px, int *py)
 {
     or_mvi n[3];
     int avail[3] = {0, 0, 0}, match[3] = {0, 0, 0};
@@ -314,7 +311,20 @@ size_t or_scroll_nal(uint8_t *dst, size_t cap, or_cfg *c, int off)
     else
         or_hdr_plain(&b, c, fn, 0);
 
-    int a_end = (c->h - off) / 16;
+    int a_end, ra, mva, rb, mvb;
+    or_scroll_regions(c, off, &a_end, &ra, &mva, &rb, &mvb);
+    or_mb_loop(&b, c, a_end, ra, mva, rb, mvb);
+    or_trailing(&b);
+    size_t n = or_nal(dst, cap, 0, 1, rbsp, or_bytes(&b));
+    free(rbsp);
+    c->frame_num++;
+    return n;
+}
+
+/* region split and waypoint choice of a scroll frame, :555-617 */
+void or_scroll_regions(const or_cfg *c, int off, int *a_end_out, int *ra_out, int *mva_out,
+                       int *rb_out, int *mvb_out)
+{
     /* A-region waypoint (:558-571): best valid wo <= off, wo > best, off-wo <= 496 */
     int wa = -1, woa = 0;
     if (off > OR_MV_LIMIT && c->nwp > 0) {
@@ -338,14 +348,11 @@ size_t or_scroll_nal(uint8_t *dst, size_t cap, or_cfg *c, int off)
             }
         }
     }
-    int ra = wa >= 0 ? 2 + wa : 0, mva = wa >= 0 ? off - woa : off;
-    int rb = wb >= 0 ? 2 + wb : 1, mvb = wb >= 0 ? off - wob : off - c->h;
-    or_mb_loop(&b, c, a_end, ra, mva, rb, mvb);
-    or_trailing(&b);
-    size_t n = or_nal(dst, cap, 0, 1, rbsp, or_bytes(&b));
-    free(rbsp);
-    c->frame_num++;
-    return n;
+    *a_end_out = (c->h - off) / 16;
+    *ra_out = wa >= 0 ? 2 + wa : 0;
+    *mva_out = wa >= 0 ? off - woa : off;
+    *rb_out = wb >= 0 ? 2 + wb : 1;
+    *mvb_out = wb >= 0 ? off - wob : off - c->h;
 }
 
 /* :666-676 */

@@ -74,6 +74,19 @@ size_t or_waypoint_nal(uint8_t *dst, size_t cap, or_cfg *c, int off);
 /* h264_needs_waypoint :666-676 */
 int or_needs_waypoint(const or_cfg *c, int off);
 
+/* ---- MB-layer pieces shared with the UI-hint restatement (hint_oracle.c) ---- */
+/* MVInfo (src/h264_writer.c:356-360); mx, my in quarter pels */
+typedef struct {
+    int mx, my, ref, avail;
+} or_mvi;
+/* get_mv_prediction (src/h264_writer.c:369-432) with median3 (:362-367) */
+void or_predict(int x, int y, int mbw, const or_mvi *above, const or_mvi *left,
+                int ref, int *px, int *py);
+/* region split (:555) and waypoint choice for A (:558-571) and B (:573-588)
+ * of a scroll frame at offset off; mv in pixels */
+void or_scroll_regions(const or_cfg *c, int off, int *a_end, int *ra, int *mva, int *rb,
+                       int *mvb);
+
 /* One composed frame.
  * mode 0 = composer_write_scroll_frame (src/composer.c:255-264): optional
  *          waypoint NAL *then* the scroll NAL.

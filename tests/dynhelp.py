@@ -58,3 +58,39 @@ def split_nals(data):
     for k, a in enumerate(starts):
         out.append(data[a:starts[k + 1] if k + 1 < len(starts) else len(data)])
     return out
+
+
+class HintRect(ctypes.Structure):
+    """or_hint_rect / ScrollHintRect (include/composer_batch.h)"""
+    _fields_ = [(n, ctypes.c_int16) for n in ("x0", "y0", "x1", "y1", "ref", "reserved")] + [
+        ("mv_x", ctypes.c_int32), ("mv_y", ctypes.c_int32)]
+
+
+def hint_array(rects):
+    """[(x0, y0, x1, y1, ref, mv_x, mv_y), ...] -> ctypes array (or None)"""
+    if not rects:
+        return None, 0
+    arr = (HintRect * len(rects))()
+    for i, (x0, y0, x1, y1, ref, mx, my) in enumerate(rects):
+        arr[i] = HintRect(x0, y0, x1, y1, ref, 0, mx, my)
+    return arr, len(rects)
+
+
+def random_hints(rng, mbw, mbh, refs, nmax=6):
+    """a UI-like overlay: static chrome (ref 0, mv 0), horizontally scrolling
+    rows, second panes, random rects; refs = the valid reference indices"""
+    out = []
+    for _ in range(rng.randint(0, nmax)):
+        kind = rng.random()
+        if kind < 0.3:                                     # static chrome bar
+            y0 = rng.choice([0, max(0, mbh - 2)])
+            out.append((0, y0, mbw, y0 + rng.randint(1, 2), 0, 0, 0))
+        elif kind < 0.55:                                  # horizontally scrolling row(s)
+            y0 = rng.randint(0, mbh - 1)
+            out.append((0, y0, mbw, y0 + rng.randint(1, 3), rng.choice(refs),
+                        rng.choice([-37, -16, -5, 3, 16, 64]), rng.choice([0, 0, 16, -32])))
+        else:                                              # pane / popup
+            x0, y0 = rng.randint(-2, mbw - 1), rng.randint(-2, mbh - 1)
+            out.append((x0, y0, x0 + rng.randint(1, mbw), y0 + rng.randint(1, mbh),
+                        rng.choice(refs), rng.randint(-80, 80), rng.randint(-300, 300)))
+    return out

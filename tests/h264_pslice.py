@@ -414,3 +414,104 @@ def reconstruct_mb(luma, cdc, cac, pred_y, pred_u, pred_v, qp=26, qpc=26):
                     rc[by + i][bx + j] = min(255, max(0, pred[by + i][bx + j] + res[4 * i + j]))
         out_c.append(rc)
     return ry, out_c[0], out_c[1]
+
+
+# --------------------------------------------------- MV field (UI hints) -----
+# Decodes the motion of a residual-free P slice: mb_skip_run (7.3.4), P_Skip
+# motion (8.4.1.1), P_L0_16x16 with mvd + prediction.  predictor="spec" is
+# the standard's median prediction (8.4.1.3); "ref" is the reference
+# composer's get_mv_prediction (src/h264_writer.c:369-432, median3 :362-367),
+# which its P slices (and the hint EXACT mode) are written with.
+
+def _med(a, b, c):
+    return sorted((a, b, c))[1]
+
+
+def _ref_median3(a, b, c):
+    if a > b:
+        a, b = b, a
+    if b > c:
+        b = c
+    if a > b:
+        a = b
+    return max(a, b)
+
+
+def _neigh(field, x, y, mbw):
+    """A, B, C-or-D as (ref, mx, my) or None"""
+    A = field[y][x - 1] if x > 0 else None
+    B = field[y - 1][x] if y > 0 else None
+    if y > 0 and x + 1 < mbw:
+        C = field[y - 1][x + 1]
+    elif y > 0 and x > 0:
+        C = field[y - 1][x - 1]
+    else:
+        C = None
+    return A, B, C
+
+
+def mvp_spec(A, B, C, ref):
+    if B is None and C is None and A is not None:
+        B = C = A
+    nb = [n for n in (A, B, C)]
+    match = [n is not None and n[0] == ref for n in nb]
+    if sum(match) == 1:
+        n = nb[match.index(True)]
+        return n[1], n[2]
+    v = [(0, 0) if n is None else (n[1], n[2]) for n in nb]
+    return _med(v[0][0], v[1][0], v[2][0]), _med(v[0][1], v[1][1], v[2][1])
+
+
+def mvp_ref(A, B, C, ref):
+    nb = (A, B, C)
+    avail = [n is not None for n in nb]
+    match = [n is not None and n[0] == ref for n in nb]
+    if sum(avail) == 0:
+        return 0, 0
+    if sum(avail) == 1:
+        n = nb[avail.index(True)]
+        return (n[1], n[2]) if n[0] == ref else (0, 0)
+    if sum(match) == 1:
+        n = nb[match.index(True)]
+        return n[1], n[2]
+    v = [(0, 0) if n is None else (n[1], n[2]) for n in nb]
+    return _ref_median3(v[0][0], v[1][0], v[2][0]), _ref_median3(v[0][1], v[1][1], v[2][1])
+
+
+def pskip_mv(A, B, C):
+    if A is None or B is None or (A[0] == 0 and A[1] == 0 and A[2] == 0) or \
+            (B[0] == 0 and B[1] == 0 and B[2] == 0):
+        return 0, 0
+    return mvp_spec(A, B, C, 0)
+
+
+def decode_mv_field(nal, w, h, predictor="spec", **hdr_kw):
+    """-> (header, field[y][x] = (ref, mx, my) in quarter pels, skipped MBs)"""
+    H, b, data = slice_header(nal, **hdr_kw)
+    pred = mvp_spec if predictor == "spec" else mvp_ref
+    mbw, mbh = w // 16, h // 16
+    field = [[None] * mbw for _ in range(mbh)]
+    m, nskip, nrefs = 0, 0, H["nrefs"]
+    while m < mbw * mbh:
+        run = b.ue()
+        for _ in range(run):
+            y, x = divmod(m, mbw)
+            assert y < mbh, "mb_skip_run past the picture"
+            field[y][x] = (0,) + pskip_mv(*_neigh(field, x, y, mbw))
+            m += 1
+            nskip += 1
+        if m >= mbw * mbh:
+            break
+        y, x = divmod(m, mbw)
+        assert b.ue() == 0, "mb_type P_L0_16x16"
+        ref = (1 - b.u(1)) if nrefs == 2 else (b.ue() if nrefs > 2 else 0)
+        dx, dy = b.se(), b.se()
+        assert b.ue() == 0, "coded_block_pattern"
+        px, py = pred(*_neigh(field, x, y, mbw), ref)
+        field[y][x] = (ref, px + dx, py + dy)
+        m += 1
+    assert b.u(1) == 1, "stop bit"
+    while b.p & 7:
+        assert b.u(1) == 0
+    assert b.p == 8 * len(data), (b.p, 8 * len(data))
+    return H, field, nskip

@@ -56,6 +56,8 @@ typedef struct {
 #define SCROLL_DEVERR_OVERFLOW 1u   /* arena too small (reference: assert)        */
 #define SCROLL_DEVERR_CONFIG   2u   /* unsupported config (e.g. log2 fields)      */
 #define SCROLL_DEVERR_DYN      4u   /* a dynamic NAL outgrew its staging slot     */
+#define SCROLL_DEVERR_HINT     8u   /* a hint rect names an invalid reference     */
+#define SCROLL_DEVERR_STAGED   (SCROLL_DEVERR_DYN | SCROLL_DEVERR_HINT)   /* nothing committed */
 
 /* k_plan state pass -> size pass: the stream's planned totals and the final
  * waypoint table (committed only by the size pass).  128 bytes. */
@@ -89,6 +91,14 @@ typedef struct {
     uint64_t ref_ld;                /* reference-pair bytes per stream (0 shared) */
     uint64_t slot_bytes;            /* staging bytes per frame                    */
 } DynGeom;
+
+/* hints of one composed frame: rects [first, first + n) of the batch's rect
+ * pool, SCROLL_HINT_* mode.  8 bytes. */
+typedef struct {
+    int32_t first;
+    int16_t n;
+    int16_t mode;
+} HintFrame;
 
 enum { SCROLL_PLAN_COMPOSER = 0, SCROLL_PLAN_EXPERIMENT = 1, SCROLL_PLAN_EXPLICIT = 2 };
 

@@ -1,0 +1,20 @@
+/*
+ * hint_engine.h -- host-side launcher of the UI-hint stage kernel
+ * (hint_kernels.hip); the batch (scroll_kernels.hip) drives it between the
+ * plan's state and size passes, like k_dyn_stage.
+ */
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#include "engine.h"
+
+/* 0, or -1 when the launch failed */
+int hint_launch_stage(hipStream_t hs, int nframes, int S, DevStream *st, const NalDesc *nal,
+                      int ld_nal, const PlanPending *pend, DynFrame *dfr, int ld_fr,
+                      const HintFrame *hf, const ScrollHintRect *pool, uint8_t *stage,
+                      uint64_t slot_bytes);
+/* staging bytes per frame that no hinted NAL of an mbw x mbh picture exceeds */
+size_t hint_slot_bound(int mbw, int mbh);

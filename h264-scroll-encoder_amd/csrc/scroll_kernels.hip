@@ -21,6 +21,7 @@
 #include <vector>
 
 #include "dyn_engine.h"
+#include "hint_engine.h"
 #include "engine.h"
 #include "scroll_device.h"
 
@@ -317,8 +318,8 @@ __global__ __launch_bounds__(PLAN_THREADS) void k_plan(DevStream *__restrict__ s
     if (tid == 0) {
         uint64_t total = s_carry;
         S->n_slow = s_nslow;
-        if (out0 + total > S->out_cap || (S->err & SCROLL_DEVERR_DYN)) {
-            if (!(S->err & SCROLL_DEVERR_DYN))
+        if (out0 + total > S->out_cap || (S->err & SCROLL_DEVERR_STAGED)) {
+            if (!(S->err & SCROLL_DEVERR_STAGED))
                 S->err |= SCROLL_DEVERR_OVERFLOW;   /* nothing committed, nothing emitted */
             S->nnal = 0;
             S->batch_bytes = 0;
@@ -333,7 +334,7 @@ __global__ __launch_bounds__(PLAN_THREADS) void k_plan(DevStream *__restrict__ s
         }
     }
     if (tid < 8 && mode != SCROLL_PLAN_EXPLICIT && out0 + s_carry <= S->out_cap &&
-        !(S->err & SCROLL_DEVERR_DYN)) {
+        !(S->err & SCROLL_DEVERR_STAGED)) {
         S->wp_off[tid] = s_wo[tid];
         S->wp_lt[tid] = s_wl[tid];
         S->wp_valid[tid] = s_wv[tid];
@@ -903,6 +904,16 @@ struct ScrollBatch {
     DynGeom geo{};
     DynFrame *d_dfr = nullptr;
     uint8_t *d_src = nullptr, *d_refs = nullptr, *d_stage = nullptr;
+    /* UI hints: staged like the dynamic rect (shares
+     * d_dfr, d_stage and geo.slot_bytes; the two are exclusive) */
+    int hint_on = 0;
+    int hint_dirty = 0;
+    int hint_max_mb = 0;               /* MBs per picture the slots are sized for */
+    std::vector<std::vector<ScrollHintRect>> h_hint;   /* [s * max_frames + f] */
+    std::vector<int16_t> h_hint_mode;
+    HintFrame *d_hf = nullptr;
+    ScrollHintRect *d_pool = nullptr;
+    size_t pool_cap = 0;
 };
 
 /* event pairs of one compose.  Dynamic rect: plan = [0,1) + [2,3), dyn
@@ -1017,6 +1028,8 @@ void scroll_batch_destroy(ScrollBatch *b)
     (void)hipFree(b->d_src);
     (void)hipFree(b->d_refs);
     (void)hipFree(b->d_stage);
+    (void)hipFree(b->d_hf);
+    (void)hipFree(b->d_pool);
     if (b->d_dbg) (void)hipFree(b->d_dbg);
     delete b;
 }
@@ -1053,6 +1066,11 @@ int scroll_batch_add_stream(ScrollBatch *b, const ComposerConfig *cfg)
     if (b->dyn_on && (cfg->width != b->dyn_pw || cfg->height != b->dyn_ph)) {
         set_err("scroll_batch_add_stream: the dynamic rect needs %dx%d streams", b->dyn_pw,
                 b->dyn_ph);
+        return SCROLL_ERR_CONFIG;
+    }
+    if (b->hint_on && (cfg->width / 16) * (cfg->height / 16) > b->hint_max_mb) {
+        set_err("scroll_batch_add_stream: hint staging slots hold %d MBs per picture",
+                b->hint_max_mb);
         return SCROLL_ERR_CONFIG;
     }
     rc = batch_host_sync(b);
@@ -1152,7 +1170,8 @@ static int launch(ScrollBatch *b, int nframes, int plan_mode, int nal_max, hipSt
         int rc = ring_events(b, &rev);
         if (rc) return rc;
     }
-    const bool dyn = b->dyn_on && plan_mode != SCROLL_PLAN_EXPLICIT;
+    const bool hint = b->hint_on && plan_mode != SCROLL_PLAN_EXPLICIT;
+    const bool dyn = (b->dyn_on || hint) && plan_mode != SCROLL_PLAN_EXPLICIT;   /* staged NALs */
     auto mark = [&](int k) -> int {
         if (!b->timing || (!dyn && k != 0 && k != 1 && k != 4)) return SCROLL_OK;
         HIPCHK(hipEventRecord(b->ev[k], hs));
@@ -1191,8 +1210,16 @@ static int launch(ScrollBatch *b, int nframes, int plan_mode, int nal_max, hipSt
             stamps = b->d_dbg;
         }
         b->geo.debug = b->debug;
-        if (dyn_launch_stage(hs, nframes, S, b->d_st, b->d_nal, b->ld_nal, b->d_pend, b->d_dfr,
-                             ld_fr, &b->geo, b->d_src, b->d_refs, b->d_stage, stamps)) {
+        if (hint) {
+            if (hint_launch_stage(hs, nframes, S, b->d_st, b->d_nal, b->ld_nal, b->d_pend,
+                                  b->d_dfr, ld_fr, b->d_hf, b->d_pool, b->d_stage,
+                                  b->geo.slot_bytes)) {
+                set_err("k_hint_stage launch: %s", hipGetErrorString(hipGetLastError()));
+                return SCROLL_ERR_HIP;
+            }
+        } else if (dyn_launch_stage(hs, nframes, S, b->d_st, b->d_nal, b->ld_nal, b->d_pend,
+                                    b->d_dfr, ld_fr, &b->geo, b->d_src, b->d_refs, b->d_stage,
+                                    stamps)) {
             set_err("k_dyn_stage launch: %s", hipGetErrorString(hipGetLastError()));
             return SCROLL_ERR_HIP;
         }
@@ -1236,6 +1263,8 @@ static int launch(ScrollBatch *b, int nframes, int plan_mode, int nal_max, hipSt
     return SCROLL_OK;
 }
 
+static int hint_upload(ScrollBatch *b);
+
 int scroll_batch_compose(ScrollBatch *b, int nframes, void *hip_stream)
 {
     return scroll_batch_compose_ex(b, nframes, hip_stream, 0);
@@ -1252,6 +1281,10 @@ int scroll_batch_compose_ex(ScrollBatch *b, int nframes, void *hip_stream, int f
         return SCROLL_ERR_CONFIG;
     }
     HIPCHK(hipSetDevice(b->device));
+    if (b->hint_on && b->hint_dirty) {
+        int rc = hint_upload(b);
+        if (rc) return rc;
+    }
     hipStream_t hs = hip_stream ? (hipStream_t)hip_stream : b->own;
     int plan = b->mode == SCROLL_MODE_EXPERIMENT ? SCROLL_PLAN_EXPERIMENT : SCROLL_PLAN_COMPOSER;
     int nal_max = plan == SCROLL_PLAN_COMPOSER ? 2 * nframes : nframes;
@@ -1275,14 +1308,20 @@ int scroll_batch_sync(ScrollBatch *b)
     int rc = SCROLL_OK;
     for (int s = 0; s < b->nstreams; ++s) {
         if (!b->h_st[s].err) continue;
-        if (rc == SCROLL_OK && (b->h_st[s].err & SCROLL_DEVERR_DYN))
-            set_err("stream %d: a dynamic-rect NAL outgrew its staging slot (%llu bytes)", s,
+        if (rc == SCROLL_OK && (b->h_st[s].err & SCROLL_DEVERR_HINT)) {
+            set_err("stream %d: a hint rect names a reference that is not valid in its frame "
+                    "(ref 2 + i needs waypoint i)", s);
+            rc = SCROLL_ERR_CONFIG;
+        } else if (rc == SCROLL_OK && (b->h_st[s].err & SCROLL_DEVERR_DYN)) {
+            set_err("stream %d: a staged NAL outgrew its staging slot (%llu bytes)", s,
                     (unsigned long long)b->geo.slot_bytes);
-        else if (rc == SCROLL_OK)
+            rc = SCROLL_ERR_OVERFLOW;
+        } else if (rc == SCROLL_OK) {
             set_err("stream %d: output arena overflow (%llu bytes used, capacity %llu)", s,
                     (unsigned long long)b->h_st[s].out_pos,
                     (unsigned long long)b->h_st[s].out_cap);
-        rc = SCROLL_ERR_OVERFLOW;
+            rc = SCROLL_ERR_OVERFLOW;
+        }
         b->h_st[s].err = 0;                      /* reported once, then cleared */
         HIPCHK(hipMemcpy(&b->d_st[s].err, &b->h_st[s].err, sizeof(int32_t),
                          hipMemcpyHostToDevice));
@@ -1445,6 +1484,11 @@ static size_t dyn_pair_bytes(const ScrollBatch *b)
 int scroll_batch_set_dyn_rect(ScrollBatch *b, int x0, int y0, int w, int h, size_t slot_bytes)
 {
     if (!b || x0 < 0 || y0 < 0 || w < 0 || h < 0) return SCROLL_ERR_ARG;
+    if (b->hint_on) {                  /* the staging buffers belong to the hints */
+        if (w == 0 || h == 0) return SCROLL_OK;
+        set_err("scroll_batch_set_dyn_rect: not combinable with UI hints (clear them first)");
+        return SCROLL_ERR_CONFIG;
+    }
     int rc = batch_host_sync(b);
     if (rc) return rc;
     HIPCHK(hipSetDevice(b->device));
@@ -1556,7 +1600,8 @@ int scroll_batch_dyn_source_synth(ScrollBatch *b, int nframes, int stream_base, 
 int scroll_batch_dyn_frame_info(ScrollBatch *b, int s, int f, uint32_t *rbsp_bytes,
                                 uint32_t *ep_bytes)
 {
-    if (!b || !b->dyn_on || s < 0 || s >= b->nstreams || f < 0 || f >= b->max_frames)
+    if (!b || !(b->dyn_on || b->hint_on) || s < 0 || s >= b->nstreams || f < 0 ||
+        f >= b->max_frames)
         return SCROLL_ERR_ARG;
     int rc = batch_host_sync(b);
     if (rc) return rc;
@@ -1571,7 +1616,7 @@ int scroll_batch_dyn_frame_info(ScrollBatch *b, int s, int f, uint32_t *rbsp_byt
 int scroll_batch_dyn_totals(ScrollBatch *b, unsigned long long *rbsp_bytes,
                             unsigned long long *ep_bytes, long long *dyn_nals)
 {
-    if (!b || !b->dyn_on) return SCROLL_ERR_ARG;
+    if (!b || !(b->dyn_on || b->hint_on)) return SCROLL_ERR_ARG;
     int rc = batch_host_sync(b);
     if (rc) return rc;
     const size_t S = (size_t)b->nstreams, F = (size_t)b->max_frames;
@@ -1590,6 +1635,120 @@ int scroll_batch_dyn_totals(ScrollBatch *b, unsigned long long *rbsp_bytes,
     if (rbsp_bytes) *rbsp_bytes = r;
     if (ep_bytes) *ep_bytes = e;
     if (dyn_nals) *dyn_nals = n;
+    return SCROLL_OK;
+}
+
+/* --------------------------------- UI hints -------------------------------- */
+static void hint_release(ScrollBatch *b)
+{
+    (void)hipFree(b->d_dfr);
+    (void)hipFree(b->d_stage);
+    (void)hipFree(b->d_hf);
+    (void)hipFree(b->d_pool);
+    b->d_dfr = nullptr;
+    b->d_stage = nullptr;
+    b->d_hf = nullptr;
+    b->d_pool = nullptr;
+    b->pool_cap = 0;
+    b->hint_on = 0;
+    b->hint_dirty = 0;
+    b->h_hint.clear();
+    b->h_hint_mode.clear();
+}
+
+/* host hint tables -> d_hf (per frame) + d_pool (all rects) */
+static int hint_upload(ScrollBatch *b)
+{
+    const size_t n = b->h_hint.size();
+    std::vector<HintFrame> hf(n);
+    std::vector<ScrollHintRect> pool;
+    for (size_t i = 0; i < n; ++i) {
+        hf[i].first = (int32_t)pool.size();
+        hf[i].n = (int16_t)b->h_hint[i].size();
+        hf[i].mode = b->h_hint_mode[i];
+        pool.insert(pool.end(), b->h_hint[i].begin(), b->h_hint[i].end());
+    }
+    if (pool.size() > b->pool_cap) {
+        (void)hipFree(b->d_pool);
+        b->d_pool = nullptr;
+        b->pool_cap = 0;
+        hipError_t e = hipMalloc(&b->d_pool, pool.size() * sizeof(ScrollHintRect));
+        if (e != hipSuccess) {
+            set_err("scroll_batch_compose: hint rects: %s", hipGetErrorString(e));
+            return e == hipErrorOutOfMemory ? SCROLL_ERR_OOM : SCROLL_ERR_HIP;
+        }
+        b->pool_cap = pool.size();
+    }
+    HIPCHK(hipMemcpy(b->d_hf, hf.data(), n * sizeof(HintFrame), hipMemcpyHostToDevice));
+    if (!pool.empty())
+        HIPCHK(hipMemcpy(b->d_pool, pool.data(), pool.size() * sizeof(ScrollHintRect),
+                         hipMemcpyHostToDevice));
+    b->hint_dirty = 0;
+    return SCROLL_OK;
+}
+
+int scroll_batch_set_hints(ScrollBatch *b, int s, int f, const ScrollHintRect *rects, int n,
+                           int mode)
+{
+    if (!b || s < 0 || s >= b->nstreams || f < 0 || f >= b->max_frames || n < 0 ||
+        n > SCROLL_HINT_MAX_RECTS || (n > 0 && !rects) ||
+        (mode != SCROLL_HINT_EXACT && mode != SCROLL_HINT_PSKIP)) {
+        set_err("scroll_batch_set_hints: bad arguments");
+        return SCROLL_ERR_ARG;
+    }
+    for (int i = 0; i < n; ++i) {
+        const ScrollHintRect &r = rects[i];
+        if (r.ref < 0 || r.ref >= 2 + 8 || r.mv_x < -SCROLL_HINT_MAX_MV ||
+            r.mv_x > SCROLL_HINT_MAX_MV || r.mv_y < -SCROLL_HINT_MAX_MV ||
+            r.mv_y > SCROLL_HINT_MAX_MV) {
+            set_err("scroll_batch_set_hints: rect %d: ref %d / mv (%d, %d) out of range", i,
+                    r.ref, r.mv_x, r.mv_y);
+            return SCROLL_ERR_ARG;
+        }
+    }
+    if (b->dyn_on) {
+        set_err("scroll_batch_set_hints: not combinable with a dynamic rect");
+        return SCROLL_ERR_CONFIG;
+    }
+    int rc = batch_host_sync(b);
+    if (rc) return rc;
+    HIPCHK(hipSetDevice(b->device));
+    if (!b->hint_on) {
+        int mb = 0;
+        for (int k = 0; k < b->nstreams; ++k) mb = std::max(mb, (b->h_st[k].w / 16) * (b->h_st[k].h / 16));
+        const size_t slot = hint_slot_bound(1, mb);     /* slots from the MB count only */
+        const size_t S = (size_t)b->max_streams, F = (size_t)b->max_frames;
+        hipError_t e = hipMalloc(&b->d_dfr, S * F * sizeof(DynFrame));
+        if (e == hipSuccess) e = hipMalloc(&b->d_stage, S * F * slot);
+        if (e == hipSuccess) e = hipMalloc(&b->d_hf, S * F * sizeof(HintFrame));
+        if (e == hipSuccess) e = hipMemset(b->d_dfr, 0, S * F * sizeof(DynFrame));
+        if (e != hipSuccess) {
+            set_err("scroll_batch_set_hints: %s", hipGetErrorString(e));
+            hint_release(b);
+            return e == hipErrorOutOfMemory ? SCROLL_ERR_OOM : SCROLL_ERR_HIP;
+        }
+        b->geo = DynGeom{};
+        b->geo.slot_bytes = slot;
+        b->hint_max_mb = mb;
+        b->h_hint.assign(S * F, {});
+        b->h_hint_mode.assign(S * F, (int16_t)SCROLL_HINT_EXACT);
+        b->hint_on = 1;
+    }
+    const size_t i = (size_t)s * b->max_frames + f;
+    b->h_hint[i].assign(rects, rects + n);
+    b->h_hint_mode[i] = (int16_t)mode;
+    b->hint_dirty = 1;
+    return SCROLL_OK;
+}
+
+int scroll_batch_clear_hints(ScrollBatch *b)
+{
+    if (!b) return SCROLL_ERR_ARG;
+    if (!b->hint_on) return SCROLL_OK;
+    int rc = batch_host_sync(b);
+    if (rc) return rc;
+    HIPCHK(hipSetDevice(b->device));
+    hint_release(b);
     return SCROLL_OK;
 }
 

@@ -104,6 +104,16 @@ class ScrollBatchDesc(ctypes.Structure):
                 ("mode", ctypes.c_int)]
 
 
+class ScrollHintRect(ctypes.Structure):
+    """include/composer_batch.h: MBs [x0, x1) x [y0, y1) take reference
+    `ref` (0 = A, 1 = B, 2 + i = waypoint i) and displacement (mv_x, mv_y) px"""
+    _fields_ = [(n, ctypes.c_int16) for n in ("x0", "y0", "x1", "y1", "ref", "reserved")] + [
+        ("mv_x", ctypes.c_int32), ("mv_y", ctypes.c_int32)]
+
+
+SCROLL_HINT_EXACT, SCROLL_HINT_PSKIP, SCROLL_HINT_MAX_RECTS = 0, 1, 64
+
+
 def _load():
     if not os.path.exists(LIB_PATH):
         raise ImportError(f"{LIB_PATH} not built: run `make -C h264-scroll-encoder_amd` "
@@ -162,6 +172,9 @@ def _load():
                                                    P(ctypes.c_ulonglong), P(ctypes.c_longlong)]),
         "scroll_batch_kernel_stats_ex": (ctypes.c_int, [ctypes.c_void_p, P(ctypes.c_double),
                                                         P(ctypes.c_int)]),
+        "scroll_batch_set_hints": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                                  P(ScrollHintRect), ctypes.c_int, ctypes.c_int]),
+        "scroll_batch_clear_hints": (ctypes.c_int, [ctypes.c_void_p]),
         "composer_batch_write_scroll_frames": (ctypes.c_int, [P(P(Composer)), P(ctypes.c_int),
                                                               ctypes.c_int, ctypes.c_int]),
         "composer_flush": (ctypes.c_int, [P(Composer)]),
@@ -370,6 +383,17 @@ class Batch:
         ms, n = (ctypes.c_double * 4)(), ctypes.c_int()
         self._chk(lib.scroll_batch_kernel_stats_ex(self.h, ms, ctypes.byref(n)), "kernel_stats_ex")
         return tuple(ms), n.value
+
+    # ---- UI hints ----
+    def set_hints(self, s, f, rects, mode=SCROLL_HINT_EXACT):
+        """rects: [(x0, y0, x1, y1, ref, mv_x, mv_y), ...] for frame f of stream s"""
+        arr = (ScrollHintRect * max(1, len(rects)))()
+        for i, (x0, y0, x1, y1, ref, mx, my) in enumerate(rects):
+            arr[i] = ScrollHintRect(x0, y0, x1, y1, ref, 0, mx, my)
+        self._chk(lib.scroll_batch_set_hints(self.h, s, f, arr, len(rects), mode), "set_hints")
+
+    def clear_hints(self):
+        self._chk(lib.scroll_batch_clear_hints(self.h), "clear_hints")
 
     # ---- dynamic rect (configs 3-5) ----
     def set_dyn_rect(self, x0, y0, w, h, slot_bytes=0):

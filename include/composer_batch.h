@@ -163,6 +163,41 @@ int scroll_batch_dyn_totals(ScrollBatch *b, unsigned long long *rbsp_bytes,
  * passes), emit, dyn stage, dyn emit; accumulators reset afterwards */
 int scroll_batch_kernel_stats_ex(ScrollBatch *b, double ms[4], int *count);
 
+/* ---- UI hints (reference design docs/MASTER_DESIGN.md:
+ * 58-64,103-146, no reference implementation) ----
+ * Rectangles of MBs with their own reference and displacement, laid over
+ * the scroll layout of the frame's offset: static chrome, a horizontally
+ * scrolling row, a second pane.  MBs no rect covers keep the scroll frame's
+ * (ref, mv).  Later rects lie on top.  Bit-exact definition:
+ * oracle/hint_oracle.h.  Once hints are set, every scroll NAL of the batch
+ * is coded per MB (waypoint NALs are unchanged); a frame without hints then
+ * equals the reference's scroll frame byte for byte in SCROLL_HINT_EXACT.
+ *
+ *   modes: SCROLL_HINT_EXACT  the reference's MB syntax (mb_skip_run 0,
+ *              get_mv_prediction of h264_writer.c:369-432) for any MV field;
+ *          SCROLL_HINT_PSKIP  standard median prediction (H.264 8.4.1.3) and
+ *              P_Skip runs for ref-0 MBs on their skip motion (8.4.1.1).
+ *   scroll_batch_set_hints(b, s, f, rects, n, mode)   hints of frame f (the
+ *       f-th frame of each following compose) of stream s; n <=
+ *       SCROLL_HINT_MAX_RECTS; n = 0 gives the plain layout in `mode`.  A
+ *       rect whose ref is not a valid reference of its frame (2 + i needs
+ *       waypoint i) fails that stream's compose with SCROLL_ERR_CONFIG.
+ *   scroll_batch_clear_hints(b)   back to plain scroll frames (k_emit path).
+ * Not combinable with a dynamic rect (SCROLL_ERR_CONFIG). */
+#define SCROLL_HINT_EXACT 0
+#define SCROLL_HINT_PSKIP 1
+#define SCROLL_HINT_MAX_RECTS 64
+#define SCROLL_HINT_MAX_MV 8192     /* |mv_x|, |mv_y| in pixels */
+typedef struct ScrollHintRect {
+    int16_t x0, y0, x1, y1;         /* MBs [x0, x1) x [y0, y1), clipped to the picture */
+    int16_t ref;                    /* 0 = A, 1 = B, 2 + i = waypoint i               */
+    int16_t reserved;               /* 0                                              */
+    int32_t mv_x, mv_y;             /* pixels: MB (x, y) predicts from (16x + mv_x, 16y + mv_y) */
+} ScrollHintRect;
+int scroll_batch_set_hints(ScrollBatch *b, int s, int f, const ScrollHintRect *rects, int n,
+                           int mode);
+int scroll_batch_clear_hints(ScrollBatch *b);
+
 /* Composer-level batch: offsets[i] composed on cs[i], i < n, in
  * order; Composers may repeat.  Output lands in each Composer's buffer before
  * return (equivalent to n composer_write_scroll_frame calls + a flush). */

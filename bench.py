@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """bench.py -- composed frames/s of the MI355X scroll composer.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload p720dyn|p720]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload p720dyn|p720|p4kdyn|p720hint]
 
 One process per GPU (torch.distributed.run for N > 1; RANK / LOCAL_RANK /
 WORLD_SIZE from the env).  Streams are independent, so each rank owns a static
@@ -20,6 +20,10 @@ A step = one scroll_batch_compose over every stream of the rank:
   workload p4kdyn (BASELINE config 5 per GPU): 128 streams x 16 composed
   3840x2160 frames with a 720x720 rect (47x47 MBs); config 4 = p720dyn with
   --streams 1024 per GPU on 8 GPUs.
+  workload p720hint (UI hints; no BASELINE number): 256
+  streams x 16 composed 1280x720 frames whose scroll NALs carry a UI overlay
+  (static chrome and side panel, a horizontally scrolling carousel) in the
+  P_Skip mode, coded per MB by k_hint_stage.
   Offsets = SURVEY 8(d) synthetic scroll (speed 1+(s%8), phase 97 s mod 1440)
   in HBM; output arenas are rewound on device at every step (the bytes of a
   step are the product).
@@ -53,7 +57,23 @@ WORKLOADS = {
     "p720": dict(w=1280, h=720, streams=256, frames=1024, rect=None,
                  desc="BASELINE config 2: 256 concurrent 1280x720 streams, P-only "
                       "(no dynamic rect), composer_write_scroll_frame semantics"),
+    "p720hint": dict(w=1280, h=720, streams=256, frames=16, rect=None, hints=True,
+                     desc="UI hints (SURVEY 8f row 1): 256 concurrent 1280x720 streams, scroll "
+                          "frames with a static chrome / side panel / horizontal carousel "
+                          "overlay, P_Skip mode"),
 }
+
+
+def ui_hints(s, f, w, h):
+    """the UI overlay of frame f of stream s (MB rects, include/composer_batch.h):
+    static top / bottom chrome and a side panel (reference A, no motion), a
+    carousel band scrolling horizontally on reference B"""
+    mbw, mbh = w // 16, h // 16
+    side = mbw // 7
+    return [(0, 0, mbw, 2, 0, 0, 0),                                  # top chrome
+            (0, mbh - 2, mbw, mbh, 0, 0, 0),                          # bottom bar
+            (0, 2, side, mbh - 2, 0, 0, 0),                           # side panel
+            (side, mbh // 2 - 3, mbw, mbh // 2 + 3, 1, -((3 * f + s) % 256), 0)]   # carousel
 
 
 def striped_i420(w, h, which):
@@ -131,6 +151,41 @@ def cpu_baseline(wl, threads):
                 single_core_fps=round(fps1, 1))
 
 
+def cpu_baseline_hint(wl, nstreams=128, nframes=256):
+    """Oracle (oracle/hint_oracle.c) on one host core over a bounded sample
+    of the same workload."""
+    import numpy as np
+    repo_oracle = os.path.join(HERE, "oracle")
+    so = os.path.join(repo_oracle, "_build", "liboracle.so")
+    if not os.path.exists(so):
+        import subprocess
+        subprocess.run(["make", "-s", "-C", repo_oracle], check=True)
+    lib = ctypes.CDLL(so)
+    sys.path.insert(0, os.path.join(HERE, "tests"))
+    from dynhelp import OrCfg, hint_array
+    W, H = wl["w"], wl["h"]
+    offs = synthetic_offsets(0, nstreams, nframes, H)
+    buf = (ctypes.c_uint8 * (1 << 20))()
+    err = ctypes.c_int()
+    arrs = {}
+    t0 = time.perf_counter()
+    for s in range(nstreams):
+        c = OrCfg()
+        lib.or_cfg_init(ctypes.byref(c), W, H)
+        c.frame_num = 2
+        for f in range(nframes):
+            key = (s, f % wl["frames"])
+            if key not in arrs:
+                arrs[key] = hint_array(ui_hints(s, key[1], W, H))
+            arr, n = arrs[key]
+            lib.or_compose_hint(buf, len(buf), ctypes.byref(c), int(offs[s, f]), 0, arr, n, 1,
+                                ctypes.byref(err))
+    fps = nstreams * nframes / (time.perf_counter() - t0)
+    return dict(value=round(fps, 1), unit="frames/s", cores=1, kind="port",
+                sample=f"{nstreams} streams x {nframes} frames {W}x{H}, same offsets and UI "
+                       f"overlay, P_Skip mode, 1 thread, oracle/hint_oracle.c -O2")
+
+
 def load_traffic(workload):
     p = os.path.join(HERE, "profiles", f"traffic_{workload}.json")
     if os.path.exists(p):
@@ -175,6 +230,7 @@ def main():
     S, F, W, H = wl["streams"], wl["frames"], wl["w"], wl["h"]
     first, _ = shard_streams(rank, world, S)       # static contiguous shard
     rect = wl["rect"]
+    hints = wl.get("hints", False)
     per_frame_bound = 2 * (64 + (W // 16) * (H // 16))
     if rect:
         per_frame_bound += 192 * rect[2] * rect[3]      # ~75 B per dynamic MB measured
@@ -189,6 +245,10 @@ def main():
         for s in range(S):                               # one copy per stream (own traffic)
             b.set_dyn_refs(ra, rb, stream=s)
         b.dyn_source_synth(F, stream_base=first, t0=0)
+    if hints:
+        for s in range(S):
+            for f in range(F):
+                b.set_hints(s, f, ui_hints(first + s, f, W, H), hs.SCROLL_HINT_PSKIP)
 
     def barrier():
         torch.cuda.synchronize()
@@ -213,7 +273,7 @@ def main():
     (plan_ms, emit_ms, stage_ms, demit_ms), n_launch = b.kernel_stats_ex()
     step_bytes = b.last_bytes()                     # per step, all streams of this rank
     step_nals = b.last_nals()
-    if rect:
+    if rect or hints:
         rbsp_tot, ep_tot, dyn_nals = b.dyn_totals()
     b.enable_timing(False)
 
@@ -231,6 +291,11 @@ def main():
             # dynamic MB (384 B each) read, the staged RBSP written
             kern = "k_dyn_stage"
             alg_bytes = dyn_nals * 2 * 384 * rect[2] * rect[3] + rbsp_tot
+            kern_ms = kms["dyn_stage"]
+        elif hints:
+            # k_hint_stage per launch: the staged RBSP written, the rects read
+            kern = "k_hint_stage"
+            alg_bytes = rbsp_tot + dyn_nals * (8 + 20 * 4)
             kern_ms = kms["dyn_stage"]
         else:
             kern = "k_emit"
@@ -266,9 +331,12 @@ def main():
             out["config"]["dyn_rect_mb"] = list(rect)
             out["dyn"] = {"rbsp_bytes_per_frame": round(rbsp_tot / max(dyn_nals, 1), 1),
                           "ep_bytes_per_frame": round(ep_tot / max(dyn_nals, 1), 2)}
+        if hints:
+            out["hint"] = {"rbsp_bytes_per_frame": round(rbsp_tot / max(dyn_nals, 1), 1),
+                           "ep_bytes_per_frame": round(ep_tot / max(dyn_nals, 1), 2)}
         if world == 1 and not args.no_cpu:
             threads = min(16, os.cpu_count() or 1)
-            out["cpu_baseline"] = cpu_baseline(wl, threads)
+            out["cpu_baseline"] = cpu_baseline_hint(wl) if hints else cpu_baseline(wl, threads)
         print(json.dumps(out), flush=True)
     b.close()
     if dist:

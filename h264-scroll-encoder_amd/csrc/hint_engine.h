@@ -11,6 +11,8 @@
 
 #include "engine.h"
 
+#define HINT_MAX_MBW 240            /* MBs per row k_hint_stage's motion ring holds (3840 px) */
+
 /* 0, or -1 when the launch failed */
 int hint_launch_stage(hipStream_t hs, int nframes, int S, DevStream *st, const NalDesc *nal,
                       int ld_nal, const PlanPending *pend, DynFrame *dfr, int ld_fr,

@@ -41,6 +41,8 @@ constexpr int HDR_BITS = 1024;          /* slice header bound (8 waypoints + MMC
 constexpr int MB_BITS = 128;            /* one MB: run + type + ref + 2 mvd + cbp <= 110 */
 constexpr int HB_WORDS = 1152;          /* LDS bit buffer: header + one window + carry */
 static_assert(HB_WORDS * 32 >= HDR_BITS + DT * MB_BITS + 64, "a window fits the buffer");
+constexpr int RING = 512;               /* MB motion ring: this window + the row above */
+static_assert(RING >= DT + HINT_MAX_MBW + 1, "the row above a window stays in the ring");
 
 /* (ref, mv) of an MB, mv in quarter pels; ref -1 = not available */
 struct Mv {
@@ -49,6 +51,7 @@ struct Mv {
 
 struct HintLds {
     uint32_t buf[HB_WORDS];
+    int32_t fr[RING], fx[RING], fy[RING];   /* motion of MB m at m % RING */
     ScrollHintRect rc[SCROLL_HINT_MAX_RECTS];
     int32_t wo[8], wl[8], wv[8];
     uint32_t wsum[NW];
@@ -221,15 +224,22 @@ __global__ __launch_bounds__(DT) void k_hint_stage(DevStream *__restrict__ st,
         int px = 0, py = 0;
         if (m < nmb) {
             const int y = (int)div_m((uint32_t)m, m_mbw), x = m - y * mbw;
-            bool bad, nb;
+            bool bad;
             me = field(L, nr, x, y, lay, c.nwp, bad);
             my_bad |= bad;
+            L.fr[m & (RING - 1)] = me.ref;
+            L.fx[m & (RING - 1)] = me.mx;
+            L.fy[m & (RING - 1)] = me.my;
+        }
+        __syncthreads();
+        if (m < nmb) {
+            /* neighbours from the ring: this window or the one(s) before */
+            const int y = (int)div_m((uint32_t)m, m_mbw), x = m - y * mbw;
+            auto at = [&](int k) { return Mv{L.fr[k & (RING - 1)], L.fx[k & (RING - 1)], L.fy[k & (RING - 1)]}; };
             const Mv none{-1, 0, 0};
-            const Mv A = x > 0 ? field(L, nr, x - 1, y, lay, c.nwp, nb) : none;
-            const Mv B = y > 0 ? field(L, nr, x, y - 1, lay, c.nwp, nb) : none;
-            const Mv C = y == 0 ? none
-                         : (x + 1 < mbw ? field(L, nr, x + 1, y - 1, lay, c.nwp, nb)
-                                        : (x > 0 ? field(L, nr, x - 1, y - 1, lay, c.nwp, nb) : none));
+            const Mv A = x > 0 ? at(m - 1) : none;
+            const Mv B = y > 0 ? at(m - mbw) : none;
+            const Mv C = y == 0 ? none : (x + 1 < mbw ? at(m - mbw + 1) : (x > 0 ? at(m - mbw - 1) : none));
             if (pskip) {
                 int sx, sy;
                 pskip_mv(x, y, A, B, C, sx, sy);

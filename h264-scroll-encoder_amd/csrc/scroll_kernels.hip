@@ -1068,9 +1068,10 @@ int scroll_batch_add_stream(ScrollBatch *b, const ComposerConfig *cfg)
                 b->dyn_ph);
         return SCROLL_ERR_CONFIG;
     }
-    if (b->hint_on && (cfg->width / 16) * (cfg->height / 16) > b->hint_max_mb) {
-        set_err("scroll_batch_add_stream: hint staging slots hold %d MBs per picture",
-                b->hint_max_mb);
+    if (b->hint_on && ((cfg->width / 16) * (cfg->height / 16) > b->hint_max_mb ||
+                       cfg->width / 16 > HINT_MAX_MBW)) {
+        set_err("scroll_batch_add_stream: hint staging slots hold %d MBs per picture, %d per row",
+                b->hint_max_mb, HINT_MAX_MBW);
         return SCROLL_ERR_CONFIG;
     }
     rc = batch_host_sync(b);
@@ -1715,7 +1716,13 @@ int scroll_batch_set_hints(ScrollBatch *b, int s, int f, const ScrollHintRect *r
     HIPCHK(hipSetDevice(b->device));
     if (!b->hint_on) {
         int mb = 0;
-        for (int k = 0; k < b->nstreams; ++k) mb = std::max(mb, (b->h_st[k].w / 16) * (b->h_st[k].h / 16));
+        for (int k = 0; k < b->nstreams; ++k) {
+            mb = std::max(mb, (b->h_st[k].w / 16) * (b->h_st[k].h / 16));
+            if (b->h_st[k].w / 16 > HINT_MAX_MBW) {
+                set_err("scroll_batch_set_hints: stream %d is wider than %d MBs", k, HINT_MAX_MBW);
+                return SCROLL_ERR_CONFIG;
+            }
+        }
         const size_t slot = hint_slot_bound(1, mb);     /* slots from the MB count only */
         const size_t S = (size_t)b->max_streams, F = (size_t)b->max_frames;
         hipError_t e = hipMalloc(&b->d_dfr, S * F * sizeof(DynFrame));

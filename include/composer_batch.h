@@ -183,6 +183,7 @@ int scroll_batch_kernel_stats_ex(ScrollBatch *b, double ms[4], int *count);
  *       rect whose ref is not a valid reference of its frame (2 + i needs
  *       waypoint i) fails that stream's compose with SCROLL_ERR_CONFIG.
  *   scroll_batch_clear_hints(b)   back to plain scroll frames (k_emit path).
+ * Pictures up to 240 MBs (3840 px) wide.
  * Not combinable with a dynamic rect (SCROLL_ERR_CONFIG). */
 #define SCROLL_HINT_EXACT 0
 #define SCROLL_HINT_PSKIP 1

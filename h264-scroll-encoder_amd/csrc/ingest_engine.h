@@ -1,0 +1,41 @@
+/*
+ * ingest_engine.h -- device-side types and launcher of the stream ingest
+ * (ingest_kernels.hip): batched composer_init + composer_write_header.
+ */
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#define ING_SC_MAX 64               /* 00 00 01 patterns kept per reference file */
+
+enum {
+    ING_OK = 0,
+    ING_ERR_MISSING = 1,            /* no SPS / PPS / IDR (composer.c:116-120)   */
+    ING_ERR_PARSE = 2,              /* parse_sps / parse_pps refused the file    */
+    ING_ERR_DIMS = 3,               /* A and B differ in size (composer.c:177)   */
+    ING_ERR_NALS = 4,               /* more than ING_SC_MAX NAL units in a file  */
+    ING_ERR_OVERFLOW = 5,           /* the header does not fit the arena         */
+};
+
+typedef struct {
+    uint64_t off, size;             /* bytes of the file in the input buffer     */
+} IngestFile;
+
+typedef struct {
+    uint32_t n;                     /* patterns found (may exceed ING_SC_MAX)    */
+    uint32_t pos[ING_SC_MAX];
+} IngestScan;
+
+typedef struct {
+    int32_t err;                    /* ING_*                                     */
+    int32_t w, h, deblock;          /* stream config from reference A            */
+    uint64_t bytes;                 /* header bytes written to the arena         */
+} IngestOut;
+
+/* files[2 k], files[2 k + 1] = reference A, B of new stream first_stream + k;
+ * header bytes at the start of its arena.  0, or -1 when a launch failed. */
+int ingest_launch(hipStream_t hs, const uint8_t *in, const IngestFile *files, int nstreams,
+                  uint64_t max_file, IngestScan *scan, IngestOut *outs, uint8_t *arena,
+                  uint64_t ld_arena, uint64_t cap, int first_stream);

@@ -1,0 +1,651 @@
+/*
+ * ingest_kernels.hip -- MI355X (gfx950) stream ingest (SURVEY.md §8f rows
+ * 3-4): composer_init + composer_write_header for many new streams at once.
+ * Reference path, per stream (src/composer.c:127-253):
+ *   parse_reference_file(A), (B)   nal_parser_next (src/nal_parser.c:28-65),
+ *                                  ebsp_to_rbsp (:67-88), parse_sps / parse_pps
+ *   composer_write_header          SPS + PPS (h264_writer.c:49-127),
+ *                                  h264_rewrite_idr_frame (:242-294) of A,
+ *                                  h264_rewrite_as_non_idr_i_frame (:296-350) of B
+ * whose heavy part is a bit-serial copy of the whole slice body behind a new
+ * header (copy_bits, :228-240) and the NAL framing with emulation prevention.
+ *
+ *   k_ing_scan    grid over every byte of every reference file: the
+ *                 positions of the 00 00 01 patterns (a handful per file)
+ *   k_ing_stream  one workgroup per new stream: lane 0 walks the NAL units
+ *                 (first SPS / PPS / IDR, the reference's stop rules) and
+ *                 parses SPS, PPS and both slice headers through an
+ *                 unescaping bit reader; then the workgroup streams each
+ *                 slice body in 4 KB EBSP windows: removal flags (closed form
+ *                 of ebsp_to_rbsp) -> scan -> RBSP ring in LDS -> output
+ *                 bytes = constant bit shift behind the new header -> EP
+ *                 insertion (closed form of rbsp_to_ebsp from the last
+ *                 non-zero byte, max-scan) -> arena.
+ * Bits: byte-identical to the reference's composer_write_header output
+ * (tests/test_gpu_ingest.py against oracle/scroll_oracle.c, pinned by the
+ * reference's golden header files).  Roofline: HBM (files in, header NALs
+ * out), DESIGN.md §5.
+ */
+#include <hip/hip_runtime.h>
+
+#include <stdint.h>
+
+#include "ingest_engine.h"
+#include "scroll_device.h"
+#include "stage_util.h"
+
+using namespace scroll;
+using namespace scroll::stage;
+
+namespace {
+
+constexpr int WINB = DT * 16;           /* EBSP bytes per window: 16 per lane      */
+constexpr int RING = 4 * WINB;          /* RBSP ring (power of two)                */
+constexpr int OCH = WINB;               /* output bytes per emit chunk: 16 per lane */
+constexpr int OBUF = OCH + OCH / 2 + 64; /* one chunk after EP (<= 1.5x)           */
+
+/* ---------------------------------------------------------------------- */
+/* k_ing_scan                                                              */
+/* ---------------------------------------------------------------------- */
+__global__ __launch_bounds__(DT) void k_ing_scan(const uint8_t *__restrict__ in,
+                                                 const IngestFile *__restrict__ files,
+                                                 IngestScan *__restrict__ scan)
+{
+    const int fi = blockIdx.y;
+    const IngestFile F = files[fi];
+    const uint64_t base = (uint64_t)blockIdx.x * WINB + 16u * threadIdx.x;
+    if (base >= F.size) return;
+    const uint8_t *d = in + F.off;
+    for (uint64_t i = base; i < base + 16 && i + 2 < F.size; ++i) {
+        if (d[i] == 0 && d[i + 1] == 0 && d[i + 2] == 1) {     /* nal_parser.c:16-18 */
+            const uint32_t k = atomicAdd(&scan[fi].n, 1u);
+            if (k < (uint32_t)ING_SC_MAX) scan[fi].pos[k] = i;
+        }
+    }
+}
+
+/* ---------------------------------------------------------------------- */
+/* serial parsing (lane 0)                                                 */
+/* ---------------------------------------------------------------------- */
+/* bit reader over an EBSP payload that removes emulation-prevention bytes
+ * as ebsp_to_rbsp does (src/nal_parser.c:67-88); reads past the end give 0
+ * (the reference's bitreader, :104-113) */
+struct EbspReader {
+    const uint8_t *d;
+    uint64_t n, i;                /* next EBSP byte */
+    int zeros;
+    uint32_t cur;                 /* current RBSP byte                       */
+    int bit;                      /* bits of cur consumed, 8 = need a byte   */
+    bool eof;
+    uint64_t rbsp_pos;            /* RBSP bytes fetched                      */
+    __device__ void init(const uint8_t *p, uint64_t size)
+    {
+        d = p;
+        n = size;
+        i = 0;
+        zeros = 0;
+        bit = 8;
+        eof = false;
+        rbsp_pos = 0;
+        cur = 0;
+    }
+    __device__ bool next_byte(uint32_t &v)
+    {
+        while (i < n) {
+            const uint32_t b = d[i];
+            if (zeros >= 2 && b == 3 && i + 1 < n && d[i + 1] <= 3) {
+                zeros = 0;
+                i++;
+                continue;
+            }
+            zeros = b ? 0 : zeros + 1;
+            i++;
+            v = b;
+            rbsp_pos++;
+            return true;
+        }
+        return false;
+    }
+    __device__ uint32_t u1()
+    {
+        if (bit == 8) {
+            if (eof || !next_byte(cur)) {
+                eof = true;
+                return 0;
+            }
+            bit = 0;
+        }
+        return (cur >> (7 - bit++)) & 1u;
+    }
+    __device__ uint32_t u(int k)
+    {
+        uint32_t v = 0;
+        for (int q = 0; q < k; ++q) v = (v << 1) | u1();
+        return v;
+    }
+    __device__ uint32_t ue()                 /* h264_writer.c:164-174 */
+    {
+        int lz = 0;
+        while (u1() == 0 && lz < 32) lz++;
+        if (lz == 0) return 0;
+        return (1u << lz) - 1u + u(lz);
+    }
+    __device__ int32_t se()
+    {
+        const uint32_t k = ue();
+        return (k & 1) ? (int32_t)((k + 1) / 2) : -(int32_t)(k / 2);
+    }
+    /* RBSP bit position of the next bit to read */
+    __device__ uint64_t pos() const { return 8 * rbsp_pos - (uint64_t)(bit == 8 ? 0 : 8 - bit); }
+};
+
+struct NalRange {
+    uint64_t off, n;              /* payload after the NAL header byte, EBSP bytes */
+    int found;
+};
+
+/* parse_reference_file's NAL walk (src/composer.c:62-108 over
+ * nal_parser_next, src/nal_parser.c:28-65): first SPS / PPS / IDR */
+__device__ int walk_nals(const uint8_t *d, uint64_t n, uint32_t *pos, int np, NalRange &sps,
+                         NalRange &pps, NalRange &idr)
+{
+    for (int a = 1; a < np; ++a) {                         /* sort the pattern positions */
+        const uint32_t v = pos[a];
+        int b = a - 1;
+        while (b >= 0 && pos[b] > v) {
+            pos[b + 1] = pos[b];
+            b--;
+        }
+        pos[b + 1] = v;
+    }
+    sps.found = pps.found = idr.found = 0;
+    for (int k = 0; k < np; ++k) {
+        const uint64_t s = (uint64_t)pos[k] + 3;          /* after 00 00 01 */
+        uint64_t e = k + 1 < np ? (uint64_t)pos[k + 1] : n;
+        while (e > s && d[e - 1] == 0) e--;                /* :46-48 */
+        if (e <= s) break;                                 /* :50-53: the parser stops */
+        const int type = d[s] & 31;
+        NalRange r{s + 1, e - s - 1, 1};
+        if (type == 7 && !sps.found) sps = r;
+        else if (type == 8 && !pps.found) pps = r;
+        else if (type == 5 && !idr.found) idr = r;
+    }
+    return sps.found && pps.found && idr.found ? 0 : -1;
+}
+
+struct SpsInfo {
+    int w, h, l2f, poct, l2p;
+};
+
+__device__ int parse_sps(const uint8_t *p, uint64_t n, SpsInfo &o)   /* nal_parser.c:137-222 */
+{
+    EbspReader r;
+    r.init(p, n);
+    const int prof = (int)r.u(8);
+    r.u(8);
+    r.u(8);
+    r.ue();
+    if (prof == 100 || prof == 110 || prof == 122 || prof == 244 || prof == 44 || prof == 83 ||
+        prof == 86 || prof == 118 || prof == 128 || prof == 138 || prof == 139 || prof == 134) {
+        if (r.ue() == 3) r.u1();
+        r.ue();
+        r.ue();
+        r.u1();
+        if (r.u1()) return -1;                              /* scaling matrices */
+    }
+    o.l2f = (int)r.ue() + 4;
+    o.poct = (int)r.ue();
+    o.l2p = 0;
+    if (o.poct == 0) o.l2p = (int)r.ue() + 4;
+    else if (o.poct == 1) return -1;
+    r.ue();
+    r.u1();
+    const int wm = (int)r.ue() + 1;
+    int hm = (int)r.ue() + 1;
+    if (!r.u1()) {
+        r.u1();
+        hm *= 2;
+    }
+    o.w = wm * 16;
+    o.h = hm * 16;
+    return 0;
+}
+
+__device__ int parse_pps(const uint8_t *p, uint64_t n, int &nref, int &dbf)   /* :224-276 */
+{
+    EbspReader r;
+    r.init(p, n);
+    r.ue();
+    r.ue();
+    r.u1();
+    r.u1();
+    if (r.ue() > 0) return -1;                             /* slice groups */
+    nref = (int)r.ue();
+    r.ue();
+    r.u1();
+    r.u(2);
+    r.ue();
+    r.ue();
+    r.ue();
+    dbf = (int)r.u1();
+    return 0;
+}
+
+struct SliceHdr {
+    uint64_t mb_start;            /* RBSP bit where the MB data begins */
+    int32_t qpd, alpha, beta;
+    uint32_t dbf;
+};
+
+/* parse_idr_slice_header (h264_writer.c:194-226) with the parse config */
+__device__ void parse_idr(const uint8_t *p, uint64_t n, const SpsInfo &pc, int pdbf, SliceHdr &h)
+{
+    EbspReader r;
+    r.init(p, n);
+    r.ue();
+    r.ue();
+    r.ue();
+    r.u(pc.l2f);
+    r.ue();
+    if (pc.poct == 0) r.u(pc.l2p);
+    r.u1();
+    r.u1();
+    h.qpd = r.se();
+    h.dbf = 0;
+    h.alpha = h.beta = 0;
+    if (pdbf) {
+        h.dbf = r.ue();
+        if (h.dbf != 1) {
+            h.alpha = r.se();
+            h.beta = r.se();
+        }
+    }
+    h.mb_start = r.pos();
+}
+
+/* a small MSB-first bit string (headers: <= 256 bits) */
+struct SmallBits {
+    uint32_t w[8];
+    int n;
+    __device__ void clear()
+    {
+        for (int k = 0; k < 8; ++k) w[k] = 0;
+        n = 0;
+    }
+    __device__ void put(uint32_t v, int k)       /* k <= 32 */
+    {
+        for (int q = k - 1; q >= 0; --q) {
+            if ((v >> q) & 1u) w[n >> 5] |= 0x80000000u >> (n & 31);
+            n++;
+        }
+    }
+    __device__ uint32_t byte(int o) const { return (w[o >> 2] >> (24 - 8 * (o & 3))) & 255u; }
+};
+
+/* write-side headers of the composer (log2_max_frame_num 4, poc type 2:
+ * src/composer.c:199-203).  rewrite_idr :262-283, rewrite_non_idr :314-339 */
+__device__ void slice_header(SmallBits &b, bool idr, int dbf, const SliceHdr &h)
+{
+    b.clear();
+    put_ue(b, 0);
+    put_ue(b, 7);                                          /* SLICE_TYPE_I_ALL */
+    put_ue(b, 0);
+    if (idr) {
+        b.put(0, 4);                                       /* frame_num 0 */
+        put_ue(b, 0);                                      /* idr_pic_id */
+        b.put(0, 1);
+        b.put(1, 1);                                       /* long_term_reference_flag */
+    } else {
+        b.put(1, 4);                                       /* frame_num 1 */
+        b.put(1, 1);                                       /* adaptive marking */
+        put_ue(b, 4);
+        put_ue(b, 2);
+        put_ue(b, 6);
+        put_ue(b, 1);
+        put_ue(b, 0);
+    }
+    put_se(b, h.qpd);
+    if (dbf) {
+        put_ue(b, h.dbf);
+        if (h.dbf != 1) {
+            put_se(b, h.alpha);
+            put_se(b, h.beta);
+        }
+    }
+}
+
+/* h264_generate_sps / _pps (h264_writer.c:49-127) */
+__device__ void gen_sps(SmallBits &b, int w, int h)
+{
+    b.clear();
+    b.put(66, 8);
+    b.put(0xc0, 8);
+    b.put(40, 8);
+    put_ue(b, 0);
+    put_ue(b, 0);
+    put_ue(b, 2);
+    put_ue(b, 2 + 8);
+    b.put(0, 1);
+    put_ue(b, (uint32_t)(w / 16 - 1));
+    put_ue(b, (uint32_t)(h / 16 - 1));
+    b.put(1, 1);
+    b.put(1, 1);
+    b.put(0, 1);
+    b.put(0, 1);
+    b.put(1, 1);                                           /* rbsp trailing */
+    b.n = (b.n + 7) & ~7;
+}
+
+__device__ void gen_pps(SmallBits &b)
+{
+    b.clear();
+    put_ue(b, 0);
+    put_ue(b, 0);
+    b.put(0, 1);
+    b.put(0, 1);
+    put_ue(b, 0);
+    put_ue(b, 1);
+    put_ue(b, 0);
+    b.put(0, 1);
+    b.put(0, 2);
+    put_se(b, 0);
+    put_se(b, 0);
+    put_se(b, 0);
+    b.put(1, 1);
+    b.put(0, 1);
+    b.put(0, 1);
+    b.put(1, 1);
+    b.n = (b.n + 7) & ~7;
+}
+
+/* nal_write_unit of a small RBSP (lane 0): start code, header, EP automaton */
+__device__ uint64_t put_small_nal(uint8_t *A, uint64_t at, uint64_t cap, int ref_idc, int type,
+                                  const SmallBits &b, bool &over)
+{
+    const int nb = b.n >> 3;
+    if (at + 5 + 2 * (uint64_t)nb > cap) {
+        over = true;
+        return at;
+    }
+    A[at++] = 0;
+    A[at++] = 0;
+    A[at++] = 0;
+    A[at++] = 1;
+    A[at++] = (uint8_t)(((ref_idc & 3) << 5) | (type & 31));
+    int zeros = 0;
+    for (int k = 0; k < nb; ++k) {                         /* nal.c:24-50 */
+        const uint32_t v = b.byte(k);
+        if (zeros >= 2 && v <= 3) {
+            A[at++] = 3;
+            zeros = 0;
+        }
+        A[at++] = (uint8_t)v;
+        zeros = v ? 0 : zeros + 1;
+    }
+    return at;
+}
+
+/* ---------------------------------------------------------------------- */
+/* k_ing_stream                                                            */
+/* ---------------------------------------------------------------------- */
+struct IngLds {
+    uint8_t ring[RING];           /* RBSP bytes, index k at k % RING          */
+    uint8_t obuf[OBUF];           /* one output chunk after EP insertion       */
+    uint32_t wsum[NW];
+    int32_t wmax[NW];
+    uint32_t pos[2][ING_SC_MAX];
+    SmallBits hdr[2];             /* new slice headers of A and B             */
+    uint8_t pre[2][40];           /* first output bytes (header + body mix)   */
+    NalRange sps[2], pps[2], idr[2];
+    SliceHdr sh[2];
+    SpsInfo si[2];
+    int32_t dbf, err;
+};
+
+/* one slice NAL: new header bits H ++ RBSP bits [mb_start, 8 R) of the EBSP
+ * payload d[0, n), NAL-framed with EP into A[at, ...) */
+__device__ uint64_t stream_slice(IngLds &L, const uint8_t *__restrict__ d, uint64_t n,
+                                 const SmallBits &H, const uint8_t *pre, uint64_t mb_start,
+                                 int ref_idc, int type, uint8_t *__restrict__ A, uint64_t at,
+                                 uint64_t cap, bool &over)
+{
+    const int t = threadIdx.x;
+    const int hlen = H.n;
+    const int npre = (hlen + 7) >> 3;                       /* output bytes holding header bits */
+    if (t == 0 && at + 5 <= cap) {
+        A[at] = 0;
+        A[at + 1] = 0;
+        A[at + 2] = 0;
+        A[at + 3] = 1;
+        A[at + 4] = (uint8_t)(((ref_idc & 3) << 5) | (type & 31));
+    }
+    at += 5;
+    uint64_t R = 0;               /* RBSP bytes produced (uniform) */
+    uint64_t O = 0;               /* output RBSP bytes emitted      */
+    int64_t lnz = -1;             /* output index of the last non-zero byte emitted */
+    const uint32_t s = (uint32_t)((mb_start + 8 * (uint64_t)npre - (uint64_t)hlen) & 7u);
+    /* output byte o >= npre takes RBSP bits [q, q + 8), q = 8 o - hlen + mb_start */
+    for (uint64_t w0 = 0;; w0 += WINB) {
+        const bool last = w0 + WINB >= n;
+        /* 1. this window's RBSP bytes -> ring */
+        int kept = 0;
+        uint8_t v[16];
+        uint32_t keepm = 0;
+        const uint64_t i0 = w0 + 16u * (uint32_t)t;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            const uint64_t i = i0 + (uint64_t)q;
+            v[q] = 0;
+            if (i < n) {
+                const uint32_t b = d[i];
+                v[q] = (uint8_t)b;
+                const bool rm = b == 3 && i >= 2 && d[i - 1] == 0 && d[i - 2] == 0 && i + 1 < n &&
+                                d[i + 1] <= 3;             /* nal_parser.c:72 */
+                if (!rm) {
+                    keepm |= 1u << q;
+                    kept++;
+                }
+            }
+        }
+        uint32_t ex, tot;
+        block_excl_sum((uint32_t)kept, L.wsum, ex, tot);
+        {
+            uint64_t k = R + ex;
+#pragma unroll
+            for (int q = 0; q < 16; ++q)
+                if ((keepm >> q) & 1u) L.ring[(k++) & (RING - 1)] = v[q];
+        }
+        R += tot;
+        __syncthreads();
+        /* 2. output bytes whose source bytes are all in the ring */
+        const uint64_t total_bits = 8 * R >= mb_start ? (uint64_t)hlen + 8 * R - mb_start : (uint64_t)hlen;
+        uint64_t O_end;
+        if (last) {
+            O_end = (total_bits + 7) >> 3;
+        } else {
+            /* byte o needs RBSP byte ((8o - hlen + mb_start) >> 3) + 1 < R */
+            const int64_t lim = (int64_t)(8 * (R - 1)) + (int64_t)hlen - (int64_t)mb_start - 8;
+            O_end = lim < 8 * (int64_t)npre ? (uint64_t)npre : (uint64_t)(lim / 8);
+            O_end = O_end > (uint64_t)npre ? O_end : (uint64_t)npre;
+            if (O_end < O) O_end = O;
+        }
+        while (O < O_end) {
+            const uint64_t oc = O_end - O < (uint64_t)OCH ? O_end - O : (uint64_t)OCH;
+            /* each lane: 16 output bytes */
+            uint8_t ob[16];
+            int64_t my_lnz = -1;
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                const uint64_t o = O + 16u * (uint32_t)t + (uint64_t)q;
+                uint32_t x = 0;
+                if (o < O + oc) {
+                    if (o < (uint64_t)npre) {
+                        x = pre[o];
+                    } else {
+                        const uint64_t qb = 8 * o - (uint64_t)hlen + mb_start;
+                        const uint64_t k = qb >> 3;
+                        const uint32_t a = k < R ? L.ring[k & (RING - 1)] : 0u;
+                        const uint32_t b = k + 1 < R ? L.ring[(k + 1) & (RING - 1)] : 0u;
+                        x = ((a << s) | (b >> (8 - s))) & 255u;
+                        if (8 * o + 8 > total_bits) x &= (0xff00u >> (total_bits - 8 * o)) & 255u;
+                    }
+                    if (x) my_lnz = (int64_t)o;
+                }
+                ob[q] = (uint8_t)x;
+            }
+            /* EP insertion: before byte o iff ob <= 3 and the zero run before o
+             * (o - 1 - last non-zero) is even and >= 2 (nal.c:33-38) */
+            int mx_ex, mx_tot;
+            const int rel = my_lnz < 0 ? -1 : (int)(my_lnz - (int64_t)O);
+            block_excl_max(rel, L.wmax, mx_ex, mx_tot);
+            int64_t prev = mx_ex >= 0 ? (int64_t)O + mx_ex : lnz;
+            uint32_t insm = 0;
+            int nins = 0, nout = 0;
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                const uint64_t o = O + 16u * (uint32_t)t + (uint64_t)q;
+                if (o < O + oc) {
+                    const int64_t run = (int64_t)o - 1 - prev;
+                    if (ob[q] <= 3 && run >= 2 && !(run & 1)) {
+                        insm |= 1u << q;
+                        nins++;
+                    }
+                    if (ob[q]) prev = (int64_t)o;
+                    nout++;
+                }
+            }
+            uint32_t oex, otot;
+            block_excl_sum((uint32_t)(nout + nins), L.wsum, oex, otot);
+            if (at + otot > cap) {
+                over = true;
+                return at;
+            }
+            {
+                uint32_t k = oex;
+#pragma unroll
+                for (int q = 0; q < 16; ++q) {
+                    if (q >= nout) break;
+                    if ((insm >> q) & 1u) L.obuf[k++] = 3;
+                    L.obuf[k++] = ob[q];
+                }
+            }
+            __syncthreads();
+            for (uint32_t k = (uint32_t)t; k < otot; k += DT) A[at + k] = L.obuf[k];
+            at += otot;
+            if (mx_tot >= 0) lnz = (int64_t)O + mx_tot;
+            O += oc;
+            __syncthreads();
+        }
+        if (last) break;
+    }
+    return at;
+}
+
+__global__ __launch_bounds__(DT) void k_ing_stream(const uint8_t *__restrict__ in,
+                                                   const IngestFile *__restrict__ files,
+                                                   const IngestScan *__restrict__ scan,
+                                                   IngestOut *__restrict__ outs,
+                                                   uint8_t *__restrict__ arena, uint64_t ld_arena,
+                                                   uint64_t cap, int first_stream)
+{
+    __shared__ IngLds L;
+    const int k = blockIdx.x, t = threadIdx.x;
+    uint8_t *A = arena + (size_t)(first_stream + k) * ld_arena;
+    const uint8_t *d[2] = {in + files[2 * k].off, in + files[2 * k + 1].off};
+    const uint64_t n[2] = {files[2 * k].size, files[2 * k + 1].size};
+    if (t == 0) {
+        L.err = ING_OK;
+        for (int f = 0; f < 2 && L.err == ING_OK; ++f) {
+            const int np = (int)scan[2 * k + f].n;
+            if (np > ING_SC_MAX) {
+                L.err = ING_ERR_NALS;
+                break;
+            }
+            for (int q = 0; q < np; ++q) L.pos[f][q] = scan[2 * k + f].pos[q];
+            if (walk_nals(d[f], n[f], L.pos[f], np, L.sps[f], L.pps[f], L.idr[f])) {
+                L.err = ING_ERR_MISSING;
+                break;
+            }
+            int nref, dbf;
+            if (parse_sps(d[f] + L.sps[f].off, L.sps[f].n, L.si[f]) ||
+                parse_pps(d[f] + L.pps[f].off, L.pps[f].n, nref, dbf)) {
+                L.err = ING_ERR_PARSE;
+                break;
+            }
+            if (f == 0) L.dbf = dbf;
+        }
+        if (L.err == ING_OK && (L.si[0].w != L.si[1].w || L.si[0].h != L.si[1].h))
+            L.err = ING_ERR_DIMS;                          /* composer.c:177-186 */
+        if (L.err == ING_OK) {
+            for (int f = 0; f < 2; ++f) {                  /* both with A's parse config */
+                parse_idr(d[f] + L.idr[f].off, L.idr[f].n, L.si[0], L.dbf, L.sh[f]);
+                slice_header(L.hdr[f], f == 0, L.dbf, L.sh[f]);
+                /* first output bytes: header bits, then the body's first bits */
+                EbspReader r;
+                r.init(d[f] + L.idr[f].off, L.idr[f].n);
+                for (uint64_t q = 0; q < L.sh[f].mb_start; ++q) r.u1();
+                SmallBits pb = L.hdr[f];
+                const int npre = (pb.n + 7) >> 3;
+                while (pb.n < 8 * npre && !r.eof) {
+                    const uint32_t bit = r.u1();
+                    if (r.eof) break;
+                    pb.put(bit, 1);
+                }
+                for (int q = 0; q < npre; ++q) L.pre[f][q] = (uint8_t)pb.byte(q);
+            }
+        }
+    }
+    __syncthreads();
+    IngestOut &o = outs[k];
+    if (L.err != ING_OK) {
+        if (t == 0) {
+            o.err = L.err;
+            o.bytes = 0;
+        }
+        return;
+    }
+    bool over = false;
+    uint64_t at = 0;
+    if (t == 0) {
+        SmallBits b;
+        gen_sps(b, L.si[0].w, L.si[0].h);
+        at = put_small_nal(A, at, cap, 3, 7, b, over);
+        gen_pps(b);
+        at = put_small_nal(A, at, cap, 3, 8, b, over);
+        L.wsum[0] = (uint32_t)at;
+        L.wmax[0] = over ? 1 : 0;
+    }
+    __syncthreads();
+    at = L.wsum[0];
+    over = L.wmax[0] != 0;
+    __syncthreads();
+    for (int f = 0; f < 2 && !over; ++f)
+        at = stream_slice(L, d[f] + L.idr[f].off, L.idr[f].n, L.hdr[f], L.pre[f], L.sh[f].mb_start,
+                          3, f == 0 ? 5 : 1, A, at, cap, over);
+    if (t == 0) {
+        o.err = over ? ING_ERR_OVERFLOW : ING_OK;
+        o.bytes = over ? 0 : at;
+        o.w = L.si[0].w;
+        o.h = L.si[0].h;
+        o.deblock = L.dbf;
+    }
+}
+
+}  // namespace
+
+int ingest_launch(hipStream_t hs, const uint8_t *in, const IngestFile *files, int nstreams,
+                  uint64_t max_file, IngestScan *scan, IngestOut *outs, uint8_t *arena,
+                  uint64_t ld_arena, uint64_t cap, int first_stream)
+{
+    if (nstreams <= 0) return 0;
+    if (hipMemsetAsync(scan, 0, sizeof(IngestScan) * 2 * (size_t)nstreams, hs) != hipSuccess)
+        return -1;
+    const uint32_t gx = (uint32_t)((max_file + WINB - 1) / WINB);
+    if (gx > 0) {
+        hipLaunchKernelGGL(k_ing_scan, dim3(gx, 2 * nstreams), dim3(DT), 0, hs, in, files, scan);
+        if (hipGetLastError() != hipSuccess) return -1;
+    }
+    hipLaunchKernelGGL(k_ing_stream, dim3(nstreams), dim3(DT), 0, hs, in, files, scan, outs, arena,
+                       ld_arena, cap, first_stream);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}

@@ -22,6 +22,7 @@
 
 #include "dyn_engine.h"
 #include "hint_engine.h"
+#include "ingest_engine.h"
 #include "engine.h"
 #include "scroll_device.h"
 
@@ -914,6 +915,13 @@ struct ScrollBatch {
     HintFrame *d_hf = nullptr;
     ScrollHintRect *d_pool = nullptr;
     size_t pool_cap = 0;
+    /* stream ingest: scratch, grown on demand */
+    uint8_t *d_ing_in = nullptr;
+    size_t ing_in_cap = 0;
+    IngestFile *d_ing_files = nullptr;
+    IngestScan *d_ing_scan = nullptr;
+    IngestOut *d_ing_out = nullptr;
+    int ing_cap = 0;
 };
 
 /* event pairs of one compose.  Dynamic rect: plan = [0,1) + [2,3), dyn
@@ -1030,6 +1038,10 @@ void scroll_batch_destroy(ScrollBatch *b)
     (void)hipFree(b->d_stage);
     (void)hipFree(b->d_hf);
     (void)hipFree(b->d_pool);
+    (void)hipFree(b->d_ing_in);
+    (void)hipFree(b->d_ing_files);
+    (void)hipFree(b->d_ing_scan);
+    (void)hipFree(b->d_ing_out);
     if (b->d_dbg) (void)hipFree(b->d_dbg);
     delete b;
 }
@@ -1757,6 +1769,139 @@ int scroll_batch_clear_hints(ScrollBatch *b)
     HIPCHK(hipSetDevice(b->device));
     hint_release(b);
     return SCROLL_OK;
+}
+
+/* ------------------------------ stream ingest ------------------------------ */
+static const char *ing_msg(int e)
+{
+    switch (e) {
+    case ING_ERR_MISSING: return "reference file missing SPS/PPS/IDR";
+    case ING_ERR_PARSE: return "unsupported SPS/PPS (scaling matrices, POC type 1 or slice groups)";
+    case ING_ERR_DIMS: return "reference frame dimensions don't match";
+    case ING_ERR_NALS: return "too many NAL units in a reference file";
+    case ING_ERR_OVERFLOW: return "header larger than the stream arena";
+    default: return "ingest failed";
+    }
+}
+
+int scroll_batch_ingest_device(ScrollBatch *b, int n, const uint8_t *d_files, const uint64_t *desc,
+                               int *first)
+{
+    if (!b || n < 0 || (n > 0 && (!d_files || !desc))) return SCROLL_ERR_ARG;
+    if (b->nstreams + n > b->max_streams) {
+        set_err("scroll_batch_ingest: %d + %d streams exceed the batch (%d)", b->nstreams, n,
+                b->max_streams);
+        return SCROLL_ERR_ARG;
+    }
+    int rc = batch_host_sync(b);
+    if (rc) return rc;
+    if (first) *first = b->nstreams;
+    if (n == 0) return SCROLL_OK;
+    HIPCHK(hipSetDevice(b->device));
+    if (n > b->ing_cap) {
+        (void)hipFree(b->d_ing_files);
+        (void)hipFree(b->d_ing_scan);
+        (void)hipFree(b->d_ing_out);
+        b->d_ing_files = nullptr;
+        b->d_ing_scan = nullptr;
+        b->d_ing_out = nullptr;
+        b->ing_cap = 0;
+        hipError_t e = hipMalloc(&b->d_ing_files, 2 * (size_t)n * sizeof(IngestFile));
+        if (e == hipSuccess) e = hipMalloc(&b->d_ing_scan, 2 * (size_t)n * sizeof(IngestScan));
+        if (e == hipSuccess) e = hipMalloc(&b->d_ing_out, (size_t)n * sizeof(IngestOut));
+        if (e != hipSuccess) {
+            set_err("scroll_batch_ingest: %s", hipGetErrorString(e));
+            return e == hipErrorOutOfMemory ? SCROLL_ERR_OOM : SCROLL_ERR_HIP;
+        }
+        b->ing_cap = n;
+    }
+    std::vector<IngestFile> files(2 * (size_t)n);
+    uint64_t maxf = 0;
+    for (int k = 0; k < 2 * n; ++k) {
+        files[k].off = desc[2 * k];
+        files[k].size = desc[2 * k + 1];
+        maxf = std::max(maxf, files[k].size);
+    }
+    hipStream_t hs = b->own;
+    HIPCHK(hipMemcpyAsync(b->d_ing_files, files.data(), files.size() * sizeof(IngestFile),
+                          hipMemcpyHostToDevice, hs));
+    if (ingest_launch(hs, d_files, b->d_ing_files, n, maxf, b->d_ing_scan, b->d_ing_out,
+                      b->d_arena, (uint64_t)b->ld_arena, (uint64_t)b->arena_bytes, b->nstreams)) {
+        set_err("ingest launch: %s", hipGetErrorString(hipGetLastError()));
+        return SCROLL_ERR_HIP;
+    }
+    std::vector<IngestOut> outs((size_t)n);
+    HIPCHK(hipMemcpyAsync(outs.data(), b->d_ing_out, outs.size() * sizeof(IngestOut),
+                          hipMemcpyDeviceToHost, hs));
+    HIPCHK(hipStreamSynchronize(hs));
+    for (int k = 0; k < n; ++k) {
+        if (outs[k].err != ING_OK) {
+            set_err("scroll_batch_ingest: new stream %d: %s", k, ing_msg(outs[k].err));
+            return outs[k].err == ING_ERR_OVERFLOW ? SCROLL_ERR_OVERFLOW : SCROLL_ERR_CONFIG;
+        }
+        if ((b->dyn_on && (outs[k].w != b->dyn_pw || outs[k].h != b->dyn_ph)) ||
+            (b->hint_on && ((outs[k].w / 16) * (outs[k].h / 16) > b->hint_max_mb ||
+                            outs[k].w / 16 > HINT_MAX_MBW))) {
+            set_err("scroll_batch_ingest: new stream %d (%dx%d) does not fit the batch's "
+                    "dynamic rect / hint slots", k, outs[k].w, outs[k].h);
+            return SCROLL_ERR_CONFIG;
+        }
+    }
+    /* the config composer_init derives (src/composer.c:193-203), frame_num 2
+     * after composer_write_header */
+    const int s0 = b->nstreams;
+    for (int k = 0; k < n; ++k) {
+        ComposerConfig cfg;
+        composer_config_init(&cfg, outs[k].w, outs[k].h);
+        composer_config_set_sps_params(&cfg, 4, 2, 4);
+        composer_config_set_pps_params(&cfg, 1, outs[k].deblock);
+        cfg.frame_num = 2;
+        if ((rc = check_cfg(&cfg))) return rc;
+        DevStream *d = &b->h_st[s0 + k];
+        memset(d, 0, sizeof(*d));
+        cfg_to_dev(&cfg, d);
+        d->out_pos = outs[k].bytes;
+        d->out_cap = b->arena_bytes;
+    }
+    HIPCHK(hipMemcpy(b->d_st + s0, b->h_st + s0, (size_t)n * sizeof(DevStream),
+                     hipMemcpyHostToDevice));
+    b->nstreams += n;
+    return SCROLL_OK;
+}
+
+int scroll_batch_ingest(ScrollBatch *b, int n, const uint8_t *const *ref_a, const size_t *na,
+                        const uint8_t *const *ref_b, const size_t *nb, int *first)
+{
+    if (!b || n < 0 || (n > 0 && (!ref_a || !na || !ref_b || !nb))) return SCROLL_ERR_ARG;
+    if (n == 0) return scroll_batch_ingest_device(b, 0, nullptr, nullptr, first);
+    std::vector<uint64_t> desc(4 * (size_t)n);
+    size_t tot = 0;
+    for (int k = 0; k < n; ++k) {
+        if ((na[k] && !ref_a[k]) || (nb[k] && !ref_b[k])) return SCROLL_ERR_ARG;
+        desc[4 * k] = tot;
+        desc[4 * k + 1] = na[k];
+        tot += (na[k] + 255) & ~(size_t)255;
+        desc[4 * k + 2] = tot;
+        desc[4 * k + 3] = nb[k];
+        tot += (nb[k] + 255) & ~(size_t)255;
+    }
+    HIPCHK(hipSetDevice(b->device));
+    if (tot > b->ing_in_cap) {
+        (void)hipFree(b->d_ing_in);
+        b->d_ing_in = nullptr;
+        b->ing_in_cap = 0;
+        hipError_t e = hipMalloc(&b->d_ing_in, tot);
+        if (e != hipSuccess) {
+            set_err("scroll_batch_ingest: %s", hipGetErrorString(e));
+            return e == hipErrorOutOfMemory ? SCROLL_ERR_OOM : SCROLL_ERR_HIP;
+        }
+        b->ing_in_cap = tot;
+    }
+    for (int k = 0; k < n; ++k) {
+        if (na[k]) HIPCHK(hipMemcpy(b->d_ing_in + desc[4 * k], ref_a[k], na[k], hipMemcpyHostToDevice));
+        if (nb[k]) HIPCHK(hipMemcpy(b->d_ing_in + desc[4 * k + 2], ref_b[k], nb[k], hipMemcpyHostToDevice));
+    }
+    return scroll_batch_ingest_device(b, n, b->d_ing_in, desc.data(), first);
 }
 
 int scroll_batch_enable_timing(ScrollBatch *b, int on)

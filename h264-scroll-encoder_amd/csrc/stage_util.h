@@ -10,6 +10,7 @@
 #include <stdint.h>
 
 #include "dyn_device.h"
+#include "engine.h"
 
 namespace scroll {
 namespace stage {

@@ -175,6 +175,12 @@ def _load():
         "scroll_batch_set_hints": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
                                                   P(ScrollHintRect), ctypes.c_int, ctypes.c_int]),
         "scroll_batch_clear_hints": (ctypes.c_int, [ctypes.c_void_p]),
+        "scroll_batch_ingest": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, P(u8p),
+                                               P(ctypes.c_size_t), P(u8p), P(ctypes.c_size_t),
+                                               P(ctypes.c_int)]),
+        "scroll_batch_ingest_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int,
+                                                      ctypes.c_void_p, P(ctypes.c_uint64),
+                                                      P(ctypes.c_int)]),
         "composer_batch_write_scroll_frames": (ctypes.c_int, [P(P(Composer)), P(ctypes.c_int),
                                                               ctypes.c_int, ctypes.c_int]),
         "composer_flush": (ctypes.c_int, [P(Composer)]),
@@ -383,6 +389,29 @@ class Batch:
         ms, n = (ctypes.c_double * 4)(), ctypes.c_int()
         self._chk(lib.scroll_batch_kernel_stats_ex(self.h, ms, ctypes.byref(n)), "kernel_stats_ex")
         return tuple(ms), n.value
+
+    # ---- stream ingest ----
+    def ingest(self, refs):
+        """refs: [(ref_a_bytes, ref_b_bytes), ...] -> id of the first new stream
+        (batched composer_init + composer_write_header on the GPU)"""
+        n = len(refs)
+        bufs = [(u8buf(bytes(a) or b"\0"), u8buf(bytes(b) or b"\0")) for a, b in refs]
+        u8p = ctypes.POINTER(ctypes.c_uint8)
+        pa = (u8p * max(n, 1))(*[ctypes.cast(x[0], u8p) for x in bufs])
+        pb = (u8p * max(n, 1))(*[ctypes.cast(x[1], u8p) for x in bufs])
+        na = (ctypes.c_size_t * max(n, 1))(*[len(a) for a, _ in refs])
+        nb = (ctypes.c_size_t * max(n, 1))(*[len(b) for _, b in refs])
+        first = ctypes.c_int()
+        self._chk(lib.scroll_batch_ingest(self.h, n, pa, na, pb, nb, ctypes.byref(first)), "ingest")
+        return first.value
+
+    def ingest_device(self, n, d_files, desc):
+        """files already on the device: desc = 4 n uint64 (offset, size of A, of B)"""
+        arr = (ctypes.c_uint64 * max(1, len(desc)))(*desc)
+        first = ctypes.c_int()
+        self._chk(lib.scroll_batch_ingest_device(self.h, n, ctypes.c_void_p(d_files), arr,
+                                                 ctypes.byref(first)), "ingest_device")
+        return first.value
 
     # ---- UI hints (SURVEY §8f row 1) ----
     def set_hints(self, s, f, rects, mode=SCROLL_HINT_EXACT):

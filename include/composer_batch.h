@@ -199,6 +199,25 @@ int scroll_batch_set_hints(ScrollBatch *b, int s, int f, const ScrollHintRect *r
                            int mode);
 int scroll_batch_clear_hints(ScrollBatch *b);
 
+/* ---- stream ingest on the GPU ----
+ * Batched composer_init + composer_write_header (reference src/composer.c:
+ * 127-253): n new streams from their reference files (Annex-B with SPS, PPS
+ * and an IDR slice: A and B), parsed and rewritten on the GPU.  Each new
+ * stream's arena starts with SPS + PPS + IDR A (long-term 0) + non-IDR I B
+ * (long-term 1), byte-identical to the reference; its config is the one
+ * composer_init derives (log2_max_frame_num 4, POC type 2, A's deblocking
+ * flag; frame_num 2 after the header).  Synchronous.  On an error no stream
+ * is added and the message names the first failing one (missing NAL unit,
+ * unsupported SPS/PPS, A/B size mismatch, header larger than the arena).
+ *   scroll_batch_ingest(b, n, a, na, b_, nb, &first)   host files
+ *   scroll_batch_ingest_device(b, n, d_files, desc, &first)   files already in
+ *       device memory: desc[4k..4k+3] = offset, size of A, offset, size of B
+ * The new streams get ids first .. first + n - 1. */
+int scroll_batch_ingest(ScrollBatch *b, int n, const uint8_t *const *ref_a, const size_t *na,
+                        const uint8_t *const *ref_b, const size_t *nb, int *first);
+int scroll_batch_ingest_device(ScrollBatch *b, int n, const uint8_t *d_files,
+                               const uint64_t *desc, int *first);
+
 /* Composer-level batch: offsets[i] composed on cs[i], i < n, in
  * order; Composers may repeat.  Output lands in each Composer's buffer before
  * return (equivalent to n composer_write_scroll_frame calls + a flush). */

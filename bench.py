@@ -24,6 +24,10 @@ A step = one scroll_batch_compose over every stream of the rank:
   streams x 16 composed 1280x720 frames whose scroll NALs carry a UI overlay
   (static chrome and side panel, a horizontally scrolling carousel) in the
   P_Skip mode, coded per MB by k_hint_stage.
+  workload ingest720 (metric: ingested streams/s): a
+  step = scroll_batch_ingest_device of 256 new streams whose 1280x720 I_PCM
+  reference files (A, B; one copy per stream) are resident in HBM --
+  composer_init + composer_write_header on the GPU.
   Offsets = SURVEY 8(d) synthetic scroll (speed 1+(s%8), phase 97 s mod 1440)
   in HBM; output arenas are rewound on device at every step (the bytes of a
   step are the product).
@@ -57,11 +61,160 @@ WORKLOADS = {
     "p720": dict(w=1280, h=720, streams=256, frames=1024, rect=None,
                  desc="BASELINE config 2: 256 concurrent 1280x720 streams, P-only "
                       "(no dynamic rect), composer_write_scroll_frame semantics"),
+    "ingest720": dict(w=1280, h=720, streams=256, frames=1, rect=None, ingest=True,
+                      desc="stream ingest (SURVEY 8f rows 3-4): 256 new 1280x720 streams per step, "
+                           "composer_init + composer_write_header from I_PCM reference files in HBM"),
     "p720hint": dict(w=1280, h=720, streams=256, frames=16, rect=None, hints=True,
                      desc="UI hints (SURVEY 8f row 1): 256 concurrent 1280x720 streams, scroll "
                           "frames with a static chrome / side panel / horizontal carousel "
                           "overlay, P_Skip mode"),
 }
+
+
+def _bits_to_bytes(bits):
+    import numpy as np
+    bits = np.asarray(bits, np.uint8)
+    return np.packbits(bits).tobytes()
+
+
+def _ue(v):
+    v += 1
+    n = v.bit_length()
+    return [0] * (n - 1) + [(v >> (n - 1 - i)) & 1 for i in range(n)]
+
+
+def _u(v, n):
+    return [(v >> (n - 1 - i)) & 1 for i in range(n)]
+
+
+def _escape(rbsp):
+    """nal.c:24-50 emulation prevention (vectorised check, loop only if needed)"""
+    import numpy as np
+    a = np.frombuffer(rbsp, np.uint8)
+    if len(a) < 3 or not np.any((a[:-2] == 0) & (a[1:-1] == 0) & (a[2:] <= 3)):
+        return rbsp
+    out, z = bytearray(), 0
+    for v in rbsp:
+        if z >= 2 and v <= 3:
+            out.append(3)
+            z = 0
+        out.append(v)
+        z = z + 1 if v == 0 else 0
+    return bytes(out)
+
+
+def ipcm_ref_file(w, h, which):
+    """an Annex-B reference file as a harness would write it (SURVEY Appendix
+    B): SPS + PPS + IDR of striped I_PCM MBs in the experiment's colours"""
+    import numpy as np
+    trail = lambda b: b + [1] + [0] * (-(len(b) + 1) % 8)
+    sps = trail(_u(66, 8) + _u(0xc0, 8) + _u(40, 8) + _ue(0) + _ue(0) + _ue(2) + _ue(10) + [0] +
+                _ue(w // 16 - 1) + _ue(h // 16 - 1) + [1, 1, 0, 0])
+    pps = trail(_ue(0) + _ue(0) + [0, 0] + _ue(0) + _ue(1) + _ue(0) + [0, 0, 0] + _ue(0) * 3 +
+                [1, 0, 0])
+    hdr = _ue(0) + _ue(7) + _ue(0) + _u(0, 4) + _ue(0) + [0, 1] + _ue(0) + _ue(1) + _ue(25)
+    hdr += [0] * (-len(hdr) % 8)
+    cols = ([81, 90, 240, 145, 54, 34, 41, 240, 110], [210, 16, 146, 170, 166, 16, 106, 202, 222])[which]
+    mbw, mbh = w // 16, h // 16
+    third = mbh // 3
+    body = bytearray(_bits_to_bytes(hdr))
+    for y in range(mbh):
+        st = 0 if y < third else (1 if y < 2 * third else 2)
+        mb = bytes([cols[3 * st]] * 256 + [cols[3 * st + 1]] * 64 + [cols[3 * st + 2]] * 64)
+        row = (mb + b"\x0d\x00") * mbw
+        body += row if y < mbh - 1 else row[:-2]
+    body += b"\x80"
+    nal = lambda hb, r: b"\0\0\0\1" + bytes([hb]) + _escape(r)
+    return nal(0x67, _bits_to_bytes(sps)) + nal(0x68, _bits_to_bytes(pps)) + nal(0x65, bytes(body))
+
+
+def cpu_baseline_ingest(files, nstreams=8):
+    """composer_init + composer_write_header restated (oracle/scroll_oracle.c
+    or_composer_run, no frames) on one host core"""
+    repo_oracle = os.path.join(HERE, "oracle")
+    so = os.path.join(repo_oracle, "_build", "liboracle.so")
+    if not os.path.exists(so):
+        import subprocess
+        subprocess.run(["make", "-s", "-C", repo_oracle], check=True)
+    lib = ctypes.CDLL(so)
+    lib.or_composer_run.restype = ctypes.c_size_t
+    a, b = files
+    cap = 2 * (len(a) + len(b)) + 4096
+    buf = (ctypes.c_uint8 * cap)()
+    t0 = time.perf_counter()
+    for _ in range(nstreams):
+        if not lib.or_composer_run(buf, cap, a, len(a), b, len(b), 0, 1):
+            raise RuntimeError("oracle refused the reference files")
+    sps = nstreams / (time.perf_counter() - t0)
+    return dict(value=round(sps, 2), unit="streams/s", cores=1, kind="port",
+                sample=f"{nstreams} streams, the same 1280x720 I_PCM reference pair, 1 thread, "
+                       f"oracle/scroll_oracle.c or_composer_run -O2")
+
+
+def run_ingest(args, wl, rank, world, local, dist):
+    import numpy as np
+    import torch
+    import h264scroll as hs
+    torch.cuda.set_device(local)
+    W, H, S = wl["w"], wl["h"], wl["streams"]
+    fa, fb = ipcm_ref_file(W, H, 0), ipcm_ref_file(W, H, 1)
+    la, lb = (len(fa) + 255) & ~255, (len(fb) + 255) & ~255
+    pair = la + lb
+    host = np.zeros(S * pair, np.uint8)
+    for k in range(S):                        # one copy per stream (own HBM traffic)
+        host[k * pair:k * pair + len(fa)] = np.frombuffer(fa, np.uint8)
+        host[k * pair + la:k * pair + la + len(fb)] = np.frombuffer(fb, np.uint8)
+    dev = torch.from_numpy(host).to(f"cuda:{local}")
+    desc = []
+    for k in range(S):
+        desc += [k * pair, len(fa), k * pair + la, len(fb)]
+    nsteps = args.warmup + args.steps
+    arena = (2 * pair + (1 << 20) + 4095) & ~4095
+    b = hs.Batch(S * nsteps, 1, arena, device=local)
+    torch.cuda.synchronize()
+
+    def barrier():
+        torch.cuda.synchronize()
+        if dist:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        b.ingest_device(S, dev.data_ptr(), desc)
+    b.enable_timing(True)
+    b.ingest_stats()
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        b.ingest_device(S, dev.data_ptr(), desc)
+    barrier()
+    t1 = time.perf_counter()
+    kms, kn = b.ingest_stats()
+    out_bytes = b.output_size(S * nsteps - 1)
+    b.enable_timing(False)
+    el = max_over_ranks(t1 - t0, dist)
+    if rank == 0:
+        k_ms = kms / max(kn, 1)
+        alg = S * (len(fa) + len(fb) + out_bytes)          # files in, header NALs out
+        achieved = alg / (k_ms * 1e-3) / 1e9
+        out = {
+            "metric": "ingested streams/s (composer_init + composer_write_header, 1280x720 "
+                      "I_PCM reference pair per stream); bit-exact vs CPU",
+            "value": round(S * args.steps * world / el, 1),
+            "unit": "streams/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(1000.0 * el / args.steps, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
+            "config": {"workload": wl["desc"], "resolution": f"{W}x{H}", "streams_per_step": S,
+                       "parallelism": f"static stream shard x{world}, no RCCL"},
+            "bytes_per_stream": {"in": len(fa) + len(fb), "out": out_bytes},
+            "roofline": {"bound": "hbm", "kernel": "k_ing_scan + k_ing_stream",
+                         "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                         "alg_bytes_per_launch": alg, "kernel_ms_avg": round(k_ms, 4)},
+        }
+        if world == 1 and not args.no_cpu:
+            out["cpu_baseline"] = cpu_baseline_ingest((fa, fb))
+        print(json.dumps(out), flush=True)
+    b.close()
 
 
 def ui_hints(s, f, w, h):
@@ -220,6 +373,12 @@ def main():
     if world > 1:
         import torch.distributed as dist
         dist.init_process_group("gloo")
+
+    if wl.get("ingest"):
+        run_ingest(args, wl, rank, world, local, dist)
+        if dist:
+            dist.destroy_process_group()
+        return
 
     import numpy as np
     import torch

@@ -922,6 +922,9 @@ struct ScrollBatch {
     IngestScan *d_ing_scan = nullptr;
     IngestOut *d_ing_out = nullptr;
     int ing_cap = 0;
+    hipEvent_t ing_ev[2] = {};         /* timing: around the ingest kernels */
+    double ing_ms = 0.0;
+    int ing_n = 0;
 };
 
 /* event pairs of one compose.  Dynamic rect: plan = [0,1) + [2,3), dyn
@@ -1042,6 +1045,8 @@ void scroll_batch_destroy(ScrollBatch *b)
     (void)hipFree(b->d_ing_files);
     (void)hipFree(b->d_ing_scan);
     (void)hipFree(b->d_ing_out);
+    for (hipEvent_t e : b->ing_ev)
+        if (e) (void)hipEventDestroy(e);
     if (b->d_dbg) (void)hipFree(b->d_dbg);
     delete b;
 }
@@ -1825,15 +1830,28 @@ int scroll_batch_ingest_device(ScrollBatch *b, int n, const uint8_t *d_files, co
     hipStream_t hs = b->own;
     HIPCHK(hipMemcpyAsync(b->d_ing_files, files.data(), files.size() * sizeof(IngestFile),
                           hipMemcpyHostToDevice, hs));
+    if (b->timing) {
+        for (hipEvent_t &e : b->ing_ev)
+            if (!e) HIPCHK(timing_event(&e));
+        HIPCHK(hipEventRecord(b->ing_ev[0], hs));
+    }
     if (ingest_launch(hs, d_files, b->d_ing_files, n, maxf, b->d_ing_scan, b->d_ing_out,
                       b->d_arena, (uint64_t)b->ld_arena, (uint64_t)b->arena_bytes, b->nstreams)) {
         set_err("ingest launch: %s", hipGetErrorString(hipGetLastError()));
         return SCROLL_ERR_HIP;
     }
+    if (b->timing) HIPCHK(hipEventRecord(b->ing_ev[1], hs));
     std::vector<IngestOut> outs((size_t)n);
     HIPCHK(hipMemcpyAsync(outs.data(), b->d_ing_out, outs.size() * sizeof(IngestOut),
                           hipMemcpyDeviceToHost, hs));
     HIPCHK(hipStreamSynchronize(hs));
+    if (b->timing) {
+        float ms = 0.0f;
+        if (hipEventElapsedTime(&ms, b->ing_ev[0], b->ing_ev[1]) == hipSuccess) {
+            b->ing_ms += ms;
+            b->ing_n++;
+        }
+    }
     for (int k = 0; k < n; ++k) {
         if (outs[k].err != ING_OK) {
             set_err("scroll_batch_ingest: new stream %d: %s", k, ing_msg(outs[k].err));
@@ -1866,6 +1884,16 @@ int scroll_batch_ingest_device(ScrollBatch *b, int n, const uint8_t *d_files, co
     HIPCHK(hipMemcpy(b->d_st + s0, b->h_st + s0, (size_t)n * sizeof(DevStream),
                      hipMemcpyHostToDevice));
     b->nstreams += n;
+    return SCROLL_OK;
+}
+
+int scroll_batch_ingest_stats(ScrollBatch *b, double *ms, int *count)
+{
+    if (!b) return SCROLL_ERR_ARG;
+    if (ms) *ms = b->ing_ms;
+    if (count) *count = b->ing_n;
+    b->ing_ms = 0.0;
+    b->ing_n = 0;
     return SCROLL_OK;
 }
 

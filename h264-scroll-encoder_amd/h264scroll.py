@@ -178,6 +178,8 @@ def _load():
         "scroll_batch_ingest": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, P(u8p),
                                                P(ctypes.c_size_t), P(u8p), P(ctypes.c_size_t),
                                                P(ctypes.c_int)]),
+        "scroll_batch_ingest_stats": (ctypes.c_int, [ctypes.c_void_p, P(ctypes.c_double),
+                                                     P(ctypes.c_int)]),
         "scroll_batch_ingest_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int,
                                                       ctypes.c_void_p, P(ctypes.c_uint64),
                                                       P(ctypes.c_int)]),
@@ -412,6 +414,12 @@ class Batch:
         self._chk(lib.scroll_batch_ingest_device(self.h, n, ctypes.c_void_p(d_files), arr,
                                                  ctypes.byref(first)), "ingest_device")
         return first.value
+
+    def ingest_stats(self):
+        ms, n = ctypes.c_double(), ctypes.c_int()
+        self._chk(lib.scroll_batch_ingest_stats(self.h, ctypes.byref(ms), ctypes.byref(n)),
+                  "ingest_stats")
+        return ms.value, n.value
 
     # ---- UI hints ----
     def set_hints(self, s, f, rects, mode=SCROLL_HINT_EXACT):

@@ -217,6 +217,9 @@ int scroll_batch_ingest(ScrollBatch *b, int n, const uint8_t *const *ref_a, cons
                         const uint8_t *const *ref_b, const size_t *nb, int *first);
 int scroll_batch_ingest_device(ScrollBatch *b, int n, const uint8_t *d_files,
                                const uint64_t *desc, int *first);
+/* with timing enabled: summed ms of the ingest kernels (HIP events on the
+ * batch's stream) and the number of ingest calls since the last call */
+int scroll_batch_ingest_stats(ScrollBatch *b, double *ms, int *count);
 
 /* Composer-level batch: offsets[i] composed on cs[i], i < n, in
  * order; Composers may repeat.  Output lands in each Composer's buffer before

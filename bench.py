@@ -429,7 +429,7 @@ def main():
     t1 = time.perf_counter()
     if b.sync() != 0:
         raise RuntimeError(hs.last_error())
-    (plan_ms, emit_ms, stage_ms, demit_ms), n_launch = b.kernel_stats_ex()
+    (plan_ms, emit_ms, stage_ms, demit_ms, code_ms, pack_ms), n_launch = b.kernel_stats_ex()
     step_bytes = b.last_bytes()                     # per step, all streams of this rank
     step_nals = b.last_nals()
     if rect or hints:

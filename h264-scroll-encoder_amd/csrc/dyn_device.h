@@ -667,6 +667,86 @@ __device__ __host__ inline int cavlc_nz(CAP &cap, const PTabs &P, const uint32_t
     return tc;
 }
 
+/* The nC-independent part of a CAVLC block (everything after coeff_token:
+ * trailing-ones signs, levels, total_zeros, run_before) of up to 16 packed
+ * int8 levels, maxc = maxNumCoeff (16 luma, 15 chroma AC; the level bytes
+ * past maxc are zero), in the same branch-free loop over the non-zero
+ * levels as cavlc_nz.  Returns TotalCoeff, TrailingOnes in t1o; ok = false
+ * when cap or the run register overflowed (cap.n is still exact). */
+template <class CAP>
+__device__ __host__ inline int cavlc_body(CAP &cap, const PTabs &P, const uint32_t pk[4], int maxc, int &t1o,
+                                          bool &ok)
+{
+    uint32_t nz = 0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) nz |= (((pk[i >> 2] >> (8 * (i & 3))) & 255u) != 0 ? 1u : 0u) << i;
+    const int tc = __builtin_popcount(nz);
+    auto lev = [&](int p) -> int {
+        const uint32_t w01 = (p & 4) ? pk[1] : pk[0], w23 = (p & 4) ? pk[3] : pk[2];
+        const uint32_t wv = (p & 8) ? w23 : w01;
+        return (int)(int8_t)(uint8_t)(wv >> (8 * (p & 3)));
+    };
+    int t1 = 0;
+    {
+        uint32_t m = nz;
+        bool run = true;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const int p = m ? top_bit(m) : 0;
+            const int v = m ? lev(p) : 0;
+            run = run && m && (v == 1 || v == -1);
+            t1 += run ? 1 : 0;
+            m &= m ? ~(1u << p) : ~0u;
+        }
+    }
+    t1o = t1;
+    ok = true;
+    if (tc == 0) return 0;
+    const int hi = top_bit(nz);
+    const int tz = hi + 1 - tc;
+    uint64_t runs = 0;
+    int rn = 0, zl = tz, sl = (tc > 10 && t1 < 3) ? 1 : 0, pprev = hi;
+    uint32_t m = nz;
+    for (int k = 0; k < tc; ++k) {
+        const int p = top_bit(m);
+        m &= ~(1u << p);
+        const int v = lev(p);
+        const int a = v < 0 ? -v : v;
+        const bool sgn = k < t1;
+        int code = 2 * a - 2 + (v < 0 ? 1 : 0);
+        code -= (k == t1 && t1 < 3) ? 2 : 0;
+        uint32_t fv;
+        int fl;
+        level_field_bf(code, sl, fv, fl);
+        cap.put(sgn ? (v < 0 ? 1u : 0u) : fv, sgn ? 1 : fl);
+        const int s1 = sl == 0 ? 1 : sl;
+        sl = sgn ? sl : ((a > (3 << (s1 - 1)) && s1 < 6) ? s1 + 1 : s1);
+        {
+            const bool act = k > 0 && zl > 0;
+            const int run = act ? pprev - p - 1 : 0;
+            const uint32_t e = P.rb[(zl < 7 ? (zl > 0 ? zl : 1) : 7) - 1][run];
+            const int l = act ? (int)(e >> 8) : 0;
+            runs = (runs << l) | (act ? (e & 255u) : 0u);
+            rn += l;
+            zl -= run;
+        }
+        pprev = p;
+    }
+    if (tc < maxc) {
+        const uint32_t e = P.tz[tc - 1][tz];
+        cap.put(e & 255u, (int)(e >> 8));
+    }
+    if (rn > 64) {
+        ok = false;
+        cap.n += (uint32_t)rn;
+    } else {
+        if (rn > 32) cap.put((uint32_t)(runs >> 32), rn - 32);
+        cap.put((uint32_t)runs, rn > 32 ? 32 : rn);
+    }
+    ok = ok && cap.n <= 128;
+    return tc;
+}
+
 /* chroma DC (2x2, nC = -1): the whole block from 4 levels in registers,
  * unrolled, packed LDS tables (P.ct[3], P.tzdc, P.rb) */
 template <class CAP>

@@ -9,10 +9,23 @@
 #include "engine.h"
 
 /* all return 0, or -1 when the launch failed */
-int dyn_launch_stage(hipStream_t hs, int nframes, int S, DevStream *st, const NalDesc *nal,
-                     int ld_nal, const PlanPending *pend, DynFrame *dfr, int ld_fr,
-                     const DynGeom *g, const uint8_t *src, const uint8_t *refs, uint8_t *stage,
-                     uint64_t *stamps);
+/* per-batch scratch of the dynamic-rect coder: prediction
+ * rows (32 h u32 per NAL), block records (DYN_PIECES per dynamic MB: a u32
+ * meta word and a 16-byte body) */
+typedef struct {
+    uint32_t *rows;
+    uint32_t *meta;
+    uint4 *body;
+} DynScratch;
+
+/* k_dyn_rows + k_dyn_code (both instantiations): block records */
+int dyn_launch_code(hipStream_t hs, int nframes, int S, const DevStream *st, const NalDesc *nal,
+                    int ld_nal, const PlanPending *pend, DynFrame *dfr, int ld_fr,
+                    const DynGeom *g, const uint8_t *src, const uint8_t *refs, const DynScratch *x);
+/* k_dyn_pack: records -> staged RBSP + EP positions */
+int dyn_launch_pack(hipStream_t hs, int nframes, int S, DevStream *st, const NalDesc *nal,
+                    int ld_nal, const PlanPending *pend, DynFrame *dfr, int ld_fr,
+                    const DynGeom *g, const DynScratch *x, uint8_t *stage, uint64_t *stamps);
 int dyn_launch_emit(hipStream_t hs, int nframes, int S, const DevStream *st, const NalDesc *nal,
                     int ld_nal, const DynFrame *dfr, int ld_fr, const DynGeom *g,
                     const uint8_t *stage, uint8_t *arena, uint64_t ld_arena, uint64_t *stamps);

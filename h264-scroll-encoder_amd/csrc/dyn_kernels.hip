@@ -33,87 +33,391 @@ namespace {
 
 __constant__ Tabs g_tabs = SCROLL_DYN_TABS;
 
-constexpr int WMB = DYN_WINDOW_MBS;     /* dynamic MBs per window: 24 x 10 = 240 block tasks */
-static_assert(24 * WMB <= 256, "one block task per thread");
-constexpr int WIN = DT;                 /* MBs per window (one MB per thread)    */
+
 constexpr int HEAD_MAX = 160;           /* bits of one MB head (huge mvd: 2 x 63 + ref) */
 constexpr int HDR_MAX = 1024;           /* slice header bits (8 waypoints + MMCO ~ 250) */
-constexpr int BUF_WORDS = 1536;        /* 48 Kbit LDS bit buffer; larger windows take passes */
-static_assert(BUF_WORDS * 32 > HDR_MAX + 64, "the slice header fits one buffer");
 constexpr int OBUF = 6400;              /* k_dyn_emit: 127 carry + 5 + 4096 x 1.5 */
-
-__device__ inline uint32_t ld32(const uint8_t *p) { return *reinterpret_cast<const uint32_t *>(p); }
-
-/* ---------------------------------------------------------------------- */
-/* k_dyn_stage                                                             */
-/* ---------------------------------------------------------------------- */
-/* Block tasks of a window with nd dynamic MBs: luma first (lanes walk the
- * MBs' 4-pixel columns so a block row of the window is one contiguous
- * source read), then Cb, Cr. */
-struct Task {
-    int k, blk, bx, by, p;
-    bool luma;
-};
-
-/* m4 = magic16(4 nd), m2 = magic16(2 nd): t < 240, divisors <= 40 */
-__device__ inline Task task_of(int t, int nd, uint32_t m4, uint32_t m2)
-{
-    Task q;
-    if (t < 16 * nd) {
-        q.luma = true;
-        q.p = 0;
-        q.by = (int)div16((uint32_t)t, m4);
-        const int c4 = t - q.by * 4 * nd;
-        q.k = c4 >> 2;
-        q.bx = c4 & 3;
-        q.blk = 4 * q.by + q.bx;
-    } else {
-        const int u = t - 16 * nd;
-        q.luma = false;
-        q.p = (int)div16((uint32_t)u, m4);
-        const int r = u - q.p * 4 * nd;
-        q.by = (int)div16((uint32_t)r, m2);
-        const int c2 = r - q.by * 2 * nd;
-        q.k = c2 >> 1;
-        q.bx = c2 & 1;
-        q.blk = 16 + 4 * q.p + 2 * q.by + q.bx;
-    }
-    return q;
-}
-
-struct StageLds {
-    uint32_t buf[BUF_WORDS];      /* NAL bits from word `bw` of the slot on       */
-    uint32_t lv8[WMB * 24][4];    /* block levels, int8 packed, scan order        */
-    uint8_t order[WMB * 24];      /* encode order: light blocks first, then heavy */
-    uint32_t whc[NW];             /* heavy blocks per wave                        */
-    int32_t dcraw[WMB][2][4];     /* chroma DC coefficients before the Hadamard   */
-    int16_t dclv[WMB][2][4];
-    alignas(16) uint8_t tc[WMB][32];   /* TotalCoeff per 4x4 block (24 used)      */
-    uint8_t cbp[WMB];
-    alignas(16) uint16_t blen[WMB][32];  /* pieces: luma raster 0..15, DC 16+p, AC 18+4p+kk */
-    alignas(16) uint16_t boff[WMB][32];
-    uint32_t exw[WIN];            /* MB lengths: in-wave exclusive prefix         */
-    uint32_t wsum[NW];
-    uint8_t ctx[DYN_CTX_MB][8];   /* bottom-row TotalCoeff of rect MBs (row ring) */
-    uint16_t rmap[32 * DYN_MAX_H]; /* prediction rows of the rect, per frame row: picture << 15 | row;
-                                      luma 16 h, chroma top 8 h, chroma bottom 8 h; 0xffff: half-pel */
-    uint8_t lcarry[8];            /* right-column TotalCoeff of the last dyn MB   */
-    int32_t wo[8], wl[8], wv[8];
-    int32_t lnz_r, lnz_w;         /* last non-zero staged byte: before / of a flush */
-    uint32_t ep_n;                /* EP positions recorded                         */
-    int32_t general;              /* a half-pel waypoint step was met            */
-    uint64_t hhi[12], hlo[12];    /* MB head codewords [row type 0..3][first / middle / last] */
-    uint32_t hlen[12];
-    int32_t head_over;            /* a head longer than 128 bits: compute per MB */
-    PTabs ptabs;
-};
-
-constexpr int HEAVY_TC = 3;       /* blocks with more non-zero levels encode in the heavy group */
 
 constexpr uint32_t DF_OVER = 1u, DF_GENERAL = 2u;   /* DynFrame.err bits */
 
-/* windowed LDS OR: word i of the window's bit stream -> buf[i - lo] when in
- * [lo, lo + n) (one pass of a window larger than the buffer) */
+__device__ inline uint32_t ld32(const uint8_t *p) { return *reinterpret_cast<const uint32_t *>(p); }
+
+/* NalCtx of scroll NAL d of stream S with the waypoint table (wo, wl, wv) */
+__device__ inline NalCtx nal_ctx(const DevStream *S, const NalDesc &d, const int32_t *wo, const int32_t *wl,
+                                 const int32_t *wv)
+{
+    NalCtx c;
+    c.w = S->w;
+    c.h = S->h;
+    c.log2_mfn = S->log2_mfn;
+    c.poc_type = S->poc_type;
+    c.log2_poc = S->log2_poc;
+    c.deblock = S->deblock;
+    c.kind = d.kind;
+    c.off = d.off;
+    c.frame_num = d.frame_num;
+    c.nwp = d.nwp;
+    c.wp_off = wo;
+    c.wp_lt = wl;
+    c.wp_valid = wv;
+    return c;
+}
+
+/* ====================================================================== */
+/* The dynamic-rect coder is three kernels:                */
+/*                                                                         */
+/*   k_dyn_rows   per NAL: the waypoint chain of every prediction row of   */
+/*                the rect, resolved once to byte offsets in picture A / B */
+/*   k_dyn_code   per 4x4 block, all blocks of all NALs at once: residual, */
+/*                transform, quant and the nC-independent CAVLC body      */
+/*                (signs, levels, total_zeros, run_before) -> records;     */
+/*                chroma DC whole (nC = -1)                                */
+/*   k_dyn_pack   per NAL: coeff_token from the neighbours' TotalCoeff,    */
+/*                cbp, MB heads, bit placement; whole words -> staging     */
+/*                with the exact emulation-prevention positions            */
+/*                                                                         */
+/* Records of dynamic MB q (rect raster order) of NAL n, piece pc:          */
+/*   0..15 luma 4x4 (raster), 16 / 17 Cb / Cr DC, 18 + 4p + b chroma AC    */
+/*   (plane p, raster b): meta[n][q][pc] = body bits | TotalCoeff << 8 |   */
+/*   TrailingOnes << 13 | ovf << 15, body[n][q][pc] = the body right-      */
+/*   aligned in 128 bits (x = bits 0..31 .. w = bits 96..127); DC pieces   */
+/*   hold the whole block.  ovf: more than 128 bits -- body holds the      */
+/*   levels instead (int8 scan order; DC: int16) and k_dyn_pack re-codes.  */
+/* ====================================================================== */
+constexpr int NPC = DYN_PIECES;         /* pieces per dynamic MB */
+constexpr uint32_t M_OVF = 1u << 15;
+constexpr uint32_t ROW_GEN = 1u << 31, ROW_OFF = 0x0fffffffu;
+
+/* ---------------------------------------------------------------------- */
+/* k_dyn_rows                                                              */
+/* ---------------------------------------------------------------------- */
+/* rows[n][i], i < 32 h (h = rect MB rows):
+ *   i < 16 h        luma row 16 y0 + i: byte offset of its prediction row in
+ *                   the stream's reference pair (picture * pic + row * w)
+ *   16 h .. 24 h    chroma row 8 y0 + i': the upper bilinear row
+ *                   (picture * pic + ysz + row * w / 2), the 1/8-pel
+ *                   fraction in bits 28..30, ROW_GEN if the waypoint chain
+ *                   has a half-pel step (the general path)
+ *   24 h .. 32 h    the lower bilinear row (used when the fraction != 0)
+ * Sets DynFrame.err = DF_GENERAL when some row of the NAL needs the general
+ * path (never for waypoints the composer creates), else 0. */
+__global__ __launch_bounds__(256) void k_dyn_rows(const DevStream *__restrict__ st,
+                                                  const NalDesc *__restrict__ nal, int ld_nal,
+                                                  const PlanPending *__restrict__ pend,
+                                                  DynFrame *__restrict__ dfr, int ld_fr, DynGeom g,
+                                                  uint32_t *__restrict__ rows)
+{
+    __shared__ int32_t wo[8], wl[8], wv[8];
+    __shared__ int32_t gen;
+    const int s = blockIdx.y, f = blockIdx.x, t = threadIdx.x;
+    DynFrame *DF = dfr + (size_t)s * ld_fr + f;
+    const int j = DF->nal;
+    if (j < 0) return;
+    if (t < 8) {
+        wo[t] = pend[s].wo[t];
+        wl[t] = pend[s].wl[t];
+        wv[t] = pend[s].wv[t];
+    }
+    if (t == 0) gen = 0;
+    __syncthreads();
+    const DevStream *S = st + s;
+    const NalDesc d = nal[(size_t)s * ld_nal + j];
+    const NalCtx c = nal_ctx(S, d, wo, wl, wv);
+    const Regions rg = regions(c);
+    const int w = c.w, h = c.h, a_end = (h - c.off) / 16;
+    const uint32_t ysz = (uint32_t)w * (uint32_t)h, pic = ysz + ysz / 2;
+    const WpTab T{wo, wv, h};
+    uint32_t *rw = rows + ((size_t)s * ld_fr + f) * (size_t)(32 * g.h);
+    bool my_gen = false;
+    for (int i = t; i < 32 * g.h; i += 256) {
+        uint32_t e;
+        if (i < 16 * g.h) {
+            const int Y = 16 * g.y0 + i, row = Y >> 4;
+            const bool cA = row < a_end;
+            int yo;
+            const int b = luma_row(T, cA ? rg.ra : rg.rb, Y + (cA ? rg.mva : rg.mvb), yo);
+            e = (uint32_t)b * pic + (uint32_t)yo * (uint32_t)w;
+        } else {
+            const int i2 = i - 16 * g.h, bot = i2 >= 8 * g.h;
+            const int Y = 8 * g.y0 + (bot ? i2 - 8 * g.h : i2), row = Y >> 3;
+            const bool cA = row < a_end;
+            const int q = 4 * (cA ? rg.mva : rg.mvb), o = q >> 3, fr = q & 7;
+            int yo;
+            const int b = chroma_row(T, cA ? rg.ra : rg.rb, Y + o + bot, yo);
+            if (b < 0) {
+                e = ROW_GEN;
+                if (!bot || fr) my_gen = true;
+            } else {
+                e = ((uint32_t)b * pic + ysz + (uint32_t)yo * (uint32_t)(w / 2)) | (uint32_t)fr << 28;
+            }
+        }
+        rw[i] = e;
+    }
+    if (my_gen) gen = 1;
+    __syncthreads();
+    if (t == 0) DF->err = gen ? DF_GENERAL : 0u;
+}
+
+/* ---------------------------------------------------------------------- */
+/* k_dyn_code                                                              */
+/* ---------------------------------------------------------------------- */
+/* grid (ceil(24 nd / 256), frames, streams); task = one 4x4 block of a NAL:
+ * [0, 16 nd) luma, MB-major (16 lanes = one MB: 4 MBs per wave read 64
+ * contiguous source bytes per row), then [16 nd, 24 nd) chroma AC, MB-major,
+ * Cb quad then Cr quad (a quad's lanes exchange their DC coefficients).
+ * Phase 1: residual -> transform -> quant -> levels (LDS); phase 2, after
+ * one barrier: blocks with <= 3 non-zero levels are coded first, so the
+ * CAVLC loop of most waves iterates <= 3 times. */
+constexpr int CODE_T = 256;
+constexpr int HEAVY_TC = 3;
+
+template <bool GENERAL>
+__global__ __launch_bounds__(CODE_T) void k_dyn_code(const DevStream *__restrict__ st,
+                                                     const DynFrame *__restrict__ dfr, int ld_fr,
+                                                     const PlanPending *__restrict__ pend,
+                                                     const NalDesc *__restrict__ nal, int ld_nal,
+                                                     DynGeom g, const uint32_t *__restrict__ rows,
+                                                     const uint8_t *__restrict__ src,
+                                                     const uint8_t *__restrict__ refs,
+                                                     uint32_t *__restrict__ meta, uint4 *__restrict__ body)
+{
+    __shared__ uint4 lv[CODE_T];
+    __shared__ uint32_t whc[CODE_T / 64];
+    __shared__ uint8_t order[CODE_T];
+    __shared__ PTabs ptabs;
+    __shared__ int32_t wo[8], wv[8];
+    const int s = blockIdx.z, f = blockIdx.y, t = threadIdx.x;
+    const int lane = t & 63, wave = t >> 6;
+    const DynFrame df = dfr[(size_t)s * ld_fr + f];
+    if (df.nal < 0) return;
+    if (GENERAL != ((df.err & DF_GENERAL) != 0)) return;
+    build_ptabs(*reinterpret_cast<const Tabs *>(&g_tabs), ptabs, t, CODE_T);
+    if (GENERAL && t < 8) {
+        wo[t] = pend[s].wo[t];
+        wv[t] = pend[s].wv[t];
+    }
+    __syncthreads();
+
+    const int ndt = g.w * g.h, ntask = 24 * ndt;
+    const int task = (int)blockIdx.x * CODE_T + t;
+    const size_t nb = (size_t)s * ld_fr + f;
+    const uint32_t *rw = rows + nb * (size_t)(32 * g.h);
+    const int w = st[s].w, h = st[s].h;
+    const uint32_t ysz = (uint32_t)w * (uint32_t)h, csz = ysz / 4;
+    const uint8_t *rb = refs + (size_t)s * g.ref_ld;
+    const uint8_t *fs = src + (size_t)s * g.src_ld + (size_t)f * g.src_fr;
+    const int lstride = 16 * g.w, cstride = 8 * g.w;
+    const uint8_t *fcb = fs + (size_t)256 * ndt, *fcr = fcb + (size_t)64 * ndt;
+    const uint32_t m_rw = magic32((uint32_t)g.w);
+    uint32_t *M = meta + nb * (size_t)(NPC * ndt);
+    uint4 *B = body + nb * (size_t)(NPC * ndt);
+
+    const bool luma = task < 16 * ndt;
+    const bool act = task < ntask;
+    int k, r, p = 0;                    /* MB, raster block, chroma plane */
+    if (luma) {
+        k = task >> 4;
+        r = task & 15;
+    } else {
+        const int jj = task - 16 * ndt;
+        k = jj >> 3;
+        p = (jj >> 2) & 1;
+        r = jj & 3;
+    }
+    const int ry = (int)div_m((uint32_t)k, m_rw), cx = k - ry * g.w;
+    const int col = g.x0 + cx;
+    uint32_t pk[4] = {0, 0, 0, 0};
+    int n = 0, w0 = 0;
+    if (act && luma) {
+        const int bx = r & 3, by = r >> 2;
+        const uint8_t *sp = fs + (size_t)(16 * ry + 4 * by) * lstride + 16 * cx + 4 * bx;
+        const uint8_t *pp = rb + 16 * col + 4 * bx;
+        const uint32_t *re = rw + 16 * ry + 4 * by;
+        uint32_t sv[4], pv[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            sv[i] = ld32(sp + (size_t)i * lstride);
+            pv[i] = ld32(pp + re[i]);
+        }
+        int res[16], W[16];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int x = 0; x < 4; ++x)
+                res[4 * i + x] = (int)((sv[i] >> (8 * x)) & 255u) - (int)((pv[i] >> (8 * x)) & 255u);
+        fwd4x4(res, W);
+#pragma unroll
+        for (int k2 = 0; k2 < 16; ++k2) {
+            const int v = quant(W[ZZ[k2]], ZZ[k2]);          /* |v| <= 78: int8 */
+            pk[k2 >> 2] |= ((uint32_t)v & 255u) << (8 * (k2 & 3));
+            n += v != 0;
+        }
+    } else if (act) {
+        const int bx = r & 1, by = r >> 1;
+        const uint8_t *sp = (p ? fcr : fcb) + (size_t)(8 * ry + 4 * by) * cstride + 8 * cx + 4 * bx;
+        const int X = 8 * col + 4 * bx;
+        const uint8_t *cp = rb + (size_t)p * csz + X;
+        const uint32_t *re = rw + 16 * g.h + 8 * ry + 4 * by;
+        int res[16], W[16];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const uint32_t sv = ld32(sp + (size_t)i * cstride);
+            const uint32_t ea = re[i];
+            int pred[4];
+            if (!GENERAL || !(ea & ROW_GEN)) {
+                const uint32_t fr = (ea >> 28) & 7u;
+                const uint32_t av = ld32(cp + (ea & ROW_OFF));
+                const uint32_t bv = fr ? ld32(cp + (re[8 * g.h + i] & ROW_OFF)) : 0u;
+#pragma unroll
+                for (int x = 0; x < 4; ++x) {
+                    const int a = (int)((av >> (8 * x)) & 255u), b = (int)((bv >> (8 * x)) & 255u);
+                    pred[x] = ((8 - (int)fr) * a + (int)fr * b + 4) >> 3;
+                }
+            } else {
+                if constexpr (GENERAL) {        /* half-pel waypoint step: any depth */
+                    const NalDesc d = nal[(size_t)s * ld_nal + df.nal];
+                    const int off = d.off, a_end = (h - off) / 16;
+                    const int row = g.y0 + ry;
+                    int32_t wl0[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+                    const NalCtx c = nal_ctx(st + s, d, wo, wl0, wv);
+                    const Regions rg = regions(c);
+                    const bool cA = row < a_end;
+                    const int ref = cA ? rg.ra : rg.rb, q = 4 * (cA ? rg.mva : rg.mvb);
+                    const int o = q >> 3, fr = q & 7;
+                    const WpTab T{wo, wv, h};
+                    RefPics P;
+                    P.w = w;
+                    P.h = h;
+                    const size_t pic = (size_t)ysz + 2 * csz;
+                    for (int i2 = 0; i2 < 2; ++i2) {
+                        P.pl[i2][0] = rb + i2 * pic;
+                        P.pl[i2][1] = P.pl[i2][0] + ysz;
+                        P.pl[i2][2] = P.pl[i2][1] + csz;
+                    }
+                    const int ya = 8 * row + 4 * by + i + o;
+                    for (int x = 0; x < 4; ++x) {
+                        const int a = chroma_px_any<9>(T, P, ref, 1 + p, X + x, ya);
+                        const int b = fr ? chroma_px_any<9>(T, P, ref, 1 + p, X + x, ya + 1) : 0;
+                        pred[x] = ((8 - fr) * a + fr * b + 4) >> 3;
+                    }
+                }
+            }
+#pragma unroll
+            for (int x = 0; x < 4; ++x) res[4 * i + x] = (int)((sv >> (8 * x)) & 255u) - pred[x];
+        }
+        fwd4x4(res, W);
+        w0 = W[0];
+#pragma unroll
+        for (int k2 = 1; k2 < 16; ++k2) {
+            const int v = quant(W[ZZ[k2]], ZZ[k2]);
+            pk[(k2 - 1) >> 2] |= ((uint32_t)v & 255u) << (8 * ((k2 - 1) & 3));
+            n += v != 0;
+        }
+    }
+    /* chroma DC: the quad's four DC coefficients -> 2x2 Hadamard, quant,
+     * whole CAVLC block (nC = -1) by the quad's first lane */
+    {
+        const int qb = lane & ~3;
+        const int d0 = __shfl(w0, qb, 64), d1 = __shfl(w0, qb + 1, 64);
+        const int d2 = __shfl(w0, qb + 2, 64), d3 = __shfl(w0, qb + 3, 64);
+        if (act && !luma && r == 0) {
+            const int dq[4] = {quant_dc(d0 + d1 + d2 + d3), quant_dc(d0 - d1 + d2 - d3),
+                               quant_dc(d0 + d1 - d2 - d3), quant_dc(d0 - d1 - d2 + d3)};
+            CapSink cap{0, 0, 0};
+            const int tc = cavlc_dc4(cap, ptabs, dq);
+            const size_t idx = (size_t)k * NPC + 16 + p;
+            if (cap.n <= 128) {
+                M[idx] = cap.n | (uint32_t)tc << 8;
+                if (cap.n)
+                    B[idx] = make_uint4((uint32_t)cap.lo, (uint32_t)(cap.lo >> 32), (uint32_t)cap.hi,
+                                        (uint32_t)(cap.hi >> 32));
+            } else {
+                M[idx] = (uint32_t)tc << 8 | M_OVF;
+                B[idx] = make_uint4(((uint32_t)dq[0] & 0xffffu) | (uint32_t)dq[1] << 16,
+                                    ((uint32_t)dq[2] & 0xffffu) | (uint32_t)dq[3] << 16, 0u, 0u);
+            }
+        }
+    }
+    /* encode order: light blocks first */
+    const bool heavy = act && n > HEAVY_TC;
+    lv[t] = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+    const uint64_t hb = __ballot(heavy);
+    if (lane == 0) whc[wave] = (uint32_t)__popcll(hb);
+    __syncthreads();
+    {
+        uint32_t hpre = 0, htot = 0;
+#pragma unroll
+        for (int w2 = 0; w2 < CODE_T / 64; ++w2) {
+            hpre += w2 < wave ? whc[w2] : 0u;
+            htot += whc[w2];
+        }
+        const uint32_t hr = hpre + (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(hb >> 32),
+                                                                       __builtin_amdgcn_mbcnt_lo((uint32_t)hb, 0u));
+        const uint32_t lr = (uint32_t)t - hr;
+        order[heavy ? (uint32_t)CODE_T - htot + hr : lr] = (uint8_t)t;
+    }
+    __syncthreads();
+    const int u = order[t];
+    const int tk = (int)blockIdx.x * CODE_T + u;
+    if (tk >= ntask) return;
+    const uint4 v4 = lv[u];
+    const uint32_t q[4] = {v4.x, v4.y, v4.z, v4.w};
+    const bool ul = tk < 16 * ndt;
+    size_t idx;
+    if (ul) {
+        idx = (size_t)(tk >> 4) * NPC + (tk & 15);
+    } else {
+        const int jj = tk - 16 * ndt;
+        idx = (size_t)(jj >> 3) * NPC + 18 + (jj & 7);
+    }
+    CapSink cap{0, 0, 0};
+    int t1;
+    bool ok;
+    const int tc = cavlc_body(cap, ptabs, q, ul ? 16 : 15, t1, ok);
+    if (ok) {
+        M[idx] = cap.n | (uint32_t)tc << 8 | (uint32_t)t1 << 13;
+        if (cap.n)
+            B[idx] = make_uint4((uint32_t)cap.lo, (uint32_t)(cap.lo >> 32), (uint32_t)cap.hi,
+                                (uint32_t)(cap.hi >> 32));
+    } else {
+        M[idx] = (uint32_t)tc << 8 | (uint32_t)t1 << 13 | M_OVF;
+        B[idx] = v4;
+    }
+}
+
+/* ---------------------------------------------------------------------- */
+/* k_dyn_pack                                                              */
+/* ---------------------------------------------------------------------- */
+/* One workgroup of PACK_T threads per dynamic NAL walks its MBs in coding
+ * order in windows [m0, m1) of nm MBs, nd of them dynamic, with
+ * nm + 26 nd <= PACK_T: thread u < nm is the head of MB m0 + u, thread
+ * nm + 26 k + pc is piece pc of the window's dynamic MB k.  Three barriers
+ * per window:
+ *   P1  previous window's whole words -> staging (+ EP positions); pieces:
+ *       nC from the neighbours' TotalCoeff (records), coeff_token, length
+ *   P2  buffer rewind; heads: cbp, piece offsets, MB length; scan
+ *   P3  every head and piece ORed into the LDS bit buffer at its offset */
+constexpr int PACK_T = 1024, PNW = PACK_T / 64;
+constexpr int PK_MB = PACK_T / (NPC + 1);          /* dynamic MBs per window, at most */
+constexpr int PBUF_WORDS = 4096;                   /* 128 Kbit; larger windows take passes */
+static_assert(PBUF_WORDS * 32 > HDR_MAX + 64, "the slice header fits one buffer");
+
+struct PackLds {
+    uint32_t buf[PBUF_WORDS];
+    alignas(16) uint8_t tc[PK_MB][32];
+    alignas(16) uint16_t blen[PK_MB][32];
+    alignas(16) uint16_t boff[PK_MB][32];
+    uint32_t exw[PACK_T];
+    uint32_t wsum[PNW];
+    int32_t wo[8], wl[8], wv[8];
+    int32_t lnz_r, lnz_w;
+    uint32_t ep_n;
+    uint64_t hhi[12], hlo[12];
+    uint32_t hlen[12];
+    int32_t head_over;
+    PTabs ptabs;
+};
+
 struct LdsOrWin {
     uint32_t *b;
     uint32_t lo, n;
@@ -125,36 +429,23 @@ struct LdsOrWin {
 };
 typedef OrSink<LdsOrWin> WSink;
 
-
-/* GENERAL = false: every waypoint step is full-pel (always so for waypoints
- * the composer creates); a NAL that meets a half-pel step is flagged and
- * redone by the GENERAL instantiation, which evaluates the bilinear tree.
- *
- * Window pipeline (barriers: 4 per window):
- *   A(i)  block tasks: residual -> transform -> quant -> CAVLC rest (regs);
- *         flush of window i-1's whole words (staging + EP count)
- *   B(i)  nC + coeff_token, chroma DC; buffer rewind after the flush
- *   C(i)  MB heads (regs), cbp, piece offsets, in-wave scan of MB lengths
- *   D(i)  every piece ORed into the LDS bit buffer at its offset          */
-#ifndef SCROLL_DYN_ABLATE
-#define SCROLL_DYN_ABLATE 0         /* 1: honour the SCROLL_DEBUG_DYN_* ablation flags (profiling builds) */
-#endif
-#define ABL(flag) (SCROLL_DYN_ABLATE && (g.debug & (flag)))
-#ifndef SCROLL_DYN_WAVES
-#define SCROLL_DYN_WAVES 8          /* waves per SIMD the register budget targets */
-#endif
-template <bool GENERAL>
-__global__ __launch_bounds__(DT, SCROLL_DYN_WAVES) void k_dyn_stage(DevStream *__restrict__ st,
-                                                  const NalDesc *__restrict__ nal, int ld_nal,
-                                                  const PlanPending *__restrict__ pend,
-                                                  DynFrame *__restrict__ dfr, int ld_fr,
-                                                  DynGeom g, const uint8_t *__restrict__ src,
-                                                  const uint8_t *__restrict__ refs,
-                                                  uint8_t *__restrict__ stage,
-                                                  uint64_t *__restrict__ stamps)
+__device__ inline uint32_t pack_wave_pre(const uint32_t *ws, int wave)
 {
-    __shared__ StageLds L;
-    /* debug: cycles per phase (A B C D, multi-pass), windows, total -> stamps */
+    uint32_t pre = 0;
+#pragma unroll
+    for (int w2 = 0; w2 < PNW; ++w2) pre += w2 < wave ? ws[w2] : 0u;
+    return pre;
+}
+
+__global__ __launch_bounds__(PACK_T, 8) void k_dyn_pack(DevStream *__restrict__ st,
+                                                     const NalDesc *__restrict__ nal, int ld_nal,
+                                                     const PlanPending *__restrict__ pend,
+                                                     DynFrame *__restrict__ dfr, int ld_fr, DynGeom g,
+                                                     const uint32_t *__restrict__ meta,
+                                                     const uint4 *__restrict__ body,
+                                                     uint8_t *__restrict__ stage, uint64_t *__restrict__ stamps)
+{
+    __shared__ PackLds L;
     uint64_t ph[5] = {0, 0, 0, 0, 0}, t_start = 0, t_last = 0, nwin = 0;
     auto mark = [&](int k) {
         if (stamps) {
@@ -170,11 +461,9 @@ __global__ __launch_bounds__(DT, SCROLL_DYN_WAVES) void k_dyn_stage(DevStream *_
     DynFrame *DF = dfr + (size_t)s * ld_fr + f;
     const int j = DF->nal;
     if (j < 0) return;
-    if (GENERAL && !(DF->err & DF_GENERAL)) return;
 
     const Rect R{g.x0, g.y0, g.w, g.h};
     if (t == 0) {
-        L.general = 0;
         L.lnz_r = -1;
         L.lnz_w = -1;
         L.head_over = 0;
@@ -185,23 +474,10 @@ __global__ __launch_bounds__(DT, SCROLL_DYN_WAVES) void k_dyn_stage(DevStream *_
         L.wl[t] = pend[s].wl[t];
         L.wv[t] = pend[s].wv[t];
     }
-    for (int i = t; i < BUF_WORDS; i += DT) L.buf[i] = 0u;
-    build_ptabs(*reinterpret_cast<const Tabs *>(&g_tabs), L.ptabs, t, DT);
+    for (int i = t; i < PBUF_WORDS; i += PACK_T) L.buf[i] = 0u;
+    build_ptabs(*reinterpret_cast<const Tabs *>(&g_tabs), L.ptabs, t, PACK_T);
     const NalDesc d = nal[(size_t)s * ld_nal + j];
-    NalCtx c;
-    c.w = S->w;
-    c.h = S->h;
-    c.log2_mfn = S->log2_mfn;
-    c.poc_type = S->poc_type;
-    c.log2_poc = S->log2_poc;
-    c.deblock = S->deblock;
-    c.kind = d.kind;
-    c.off = d.off;
-    c.frame_num = d.frame_num;
-    c.nwp = d.nwp;
-    c.wp_off = L.wo;
-    c.wp_lt = L.wl;
-    c.wp_valid = L.wv;
+    const NalCtx c = nal_ctx(S, d, L.wo, L.wl, L.wv);
     __syncthreads();
 
     /* slice header (h264_writer.c:549-553): thread 0 writes, all count */
@@ -217,40 +493,10 @@ __global__ __launch_bounds__(DT, SCROLL_DYN_WAVES) void k_dyn_stage(DevStream *_
             hs.finish();
         }
     }
-
     const int w = c.w, h = c.h, mbw = w / 16, mbh = h / 16;
     const Regions rg = regions(c);
     const int a_end = (h - c.off) / 16;
     const int nrefs = 2 + c.nwp;
-    const WpTab T{L.wo, L.wv, h};
-    const uint8_t *rb = refs + (size_t)s * g.ref_ld;
-    const size_t ysz = (size_t)w * h, csz = ysz / 4, pic = ysz + 2 * csz;
-    const uint8_t *fs = src + (size_t)s * g.src_ld + (size_t)f * g.src_fr;
-    const int lstride = 16 * R.w, cstride = 8 * R.w;
-    const uint8_t *fcb = fs + (size_t)256 * R.w * R.h, *fcr = fcb + (size_t)64 * R.w * R.h;
-    const int rmask = g.ring - 1;       /* TotalCoeff row ring: a power of two */
-    /* the waypoint chain of every prediction row, once per NAL: frame row
-     * -> (picture A / B, row) for luma, and for the two chroma rows of the
-     * 1/8-pel bilinear (src/h264_writer.c:689-729 via dyn_device.h) */
-    for (int i = t; i < 32 * R.h; i += DT) {
-        uint16_t e;
-        if (i < 16 * R.h) {
-            const int Y = 16 * R.y0 + i, row = Y >> 4;
-            const bool cA = row < a_end;
-            int yo;
-            const int b = luma_row(T, cA ? rg.ra : rg.rb, Y + (cA ? rg.mva : rg.mvb), yo);
-            e = (uint16_t)(b << 15 | yo);
-        } else {
-            const int i2 = i - 16 * R.h, bot = i2 >= 8 * R.h;
-            const int Y = 8 * R.y0 + (bot ? i2 - 8 * R.h : i2), row = Y >> 3;
-            const bool cA = row < a_end;
-            const int o = (4 * (cA ? rg.mva : rg.mvb)) >> 3;
-            int yo;
-            const int b = chroma_row(T, cA ? rg.ra : rg.rb, Y + o + bot, yo);
-            e = b < 0 ? (uint16_t)0xffff : (uint16_t)(b << 15 | yo);
-        }
-        L.rmap[i] = e;
-    }
     /* MB head codewords (mb_skip_run .. mvd, h264_writer.c:434-453): they
      * depend only on the row type -- row 0, steady A, A->B boundary, steady
      * B -- and on first / middle / last position */
@@ -271,13 +517,17 @@ __global__ __launch_bounds__(DT, SCROLL_DYN_WAVES) void k_dyn_stage(DevStream *_
         if (hc.over()) L.head_over = 1;
     }
     __syncthreads();
-    const uint32_t m_mbw = magic32((uint32_t)mbw), m_rw = magic32((uint32_t)R.w);
-    uint8_t *slot = stage + ((size_t)s * ld_fr + f) * g.slot_bytes;
+    const bool head_over = L.head_over;           /* uniform */
+    const uint32_t m_mbw = magic32((uint32_t)mbw), m_rw = magic32((uint32_t)R.w), m_pc = magic32(NPC);
+    const size_t nb = (size_t)s * ld_fr + f;
+    const int ndt = R.w * R.h;
+    const uint32_t *M = meta + nb * (size_t)(NPC * ndt);
+    const uint4 *Bd = body + nb * (size_t)(NPC * ndt);
+    uint8_t *slot = stage + nb * g.slot_bytes;
     uint32_t *out = reinterpret_cast<uint32_t *>(slot);
     const uint32_t cap_words = (uint32_t)((g.slot_bytes - DYN_OVF_BYTES) / 4) - 4u;
-    /* RBSP positions of the EP bytes (unsorted), for k_dyn_emit's gather */
     uint32_t *eplist = reinterpret_cast<uint32_t *>(slot + g.slot_bytes - DYN_OVF_BYTES);
-    const Tabs &TB = g_tabs;            /* chroma DC and the rare > 128-bit blocks */
+    const Tabs &TB = g_tabs;
     const PTabs &PT = L.ptabs;
 
     uint32_t bw = 0;             /* staging word of buf[0]                        */
@@ -286,10 +536,10 @@ __global__ __launch_bounds__(DT, SCROLL_DYN_WAVES) void k_dyn_stage(DevStream *_
     uint32_t pend_T = 0;         /* bits in buf awaiting the deferred flush (0: none) */
 
     /* whole words buf[0, n) -> staging words [gw0, gw0 + n), EP insertions
-     * counted with the zero run looked up backwards in buf (L.lnz_r before
-     * buf[0]); the last non-zero byte goes to L.lnz_w */
+     * with the zero run looked up backwards in buf (L.lnz_r before buf[0]);
+     * the last non-zero byte goes to L.lnz_w */
     auto flush_words = [&](uint32_t n, uint32_t gw0) {
-        for (uint32_t jw = (uint32_t)t; jw < n; jw += DT) {
+        for (uint32_t jw = (uint32_t)t; jw < n; jw += PACK_T) {
             const uint32_t wv = L.buf[jw];
             out[gw0 + jw] = __builtin_bswap32(wv);
             int prev = L.lnz_r;
@@ -305,322 +555,183 @@ __global__ __launch_bounds__(DT, SCROLL_DYN_WAVES) void k_dyn_stage(DevStream *_
             if (wv) atomicMax(&L.lnz_w, (int)gb + last_nz_byte(wv));
         }
     };
-    /* after a flush: carry the last non-zero byte forward */
     auto rewind_lnz = [&]() {
         if (t == 0) {
             L.lnz_r = max(L.lnz_r, L.lnz_w);
             L.lnz_w = -1;
         }
     };
+    /* MB m's head codeword class */
+    auto head_sel = [&](int row, int col) {
+        const bool curA = row < a_end, abvA = (row - 1) < a_end;
+        return 3 * (row == 0 ? 0 : (curA ? 1 : (abvA ? 2 : 3))) + (col == 0 ? 0 : (col == mbw - 1 ? 2 : 1));
+    };
+    auto put_head_slow = [&](auto &sk, int row, int col) {       /* > 128-bit heads */
+        const bool curA = row < a_end, abvA = (row - 1) < a_end;
+        const int ref = curA ? rg.ra : rg.rb, mv4 = 4 * (curA ? rg.mva : rg.mvb);
+        const int aref = abvA ? rg.ra : rg.rb, amv4 = 4 * (abvA ? rg.mva : rg.mvb);
+        int px, py;
+        predict(col, row, mbw, ref, mv4, aref, amv4, px, py);
+        put_mb_head(sk, ref, 0 - px, mv4 - py, nrefs);
+    };
 
-    const int nmb = mbw * mbh, ndt = R.w * R.h;
+    const int nmb = mbw * mbh;
     for (int m0 = 0; m0 < nmb;) {
         const int q0 = dyn_rank_m(R, mbw, m_mbw, m0);
-        int m1 = min(m0 + WIN, nmb);
-        if (q0 + WMB < ndt) m1 = min(m1, dyn_mb_m(R, mbw, m_rw, q0 + WMB));
-        const int nd = dyn_rank_m(R, mbw, m_mbw, m1) - q0;
-        const int nm = m1 - m0;
-        const uint32_t m4 = nd ? magic16(4u * nd) : 0u, m2 = nd ? magic16(2u * nd) : 0u;
-        /* rect coordinates (ry, cx) of dynamic MB k of the window */
-        auto dcoord = [&](int k, int &ry, int &cx) {
-            const int qq = q0 + k;
-            ry = (int)div_m((uint32_t)qq, m_rw);
-            cx = qq - ry * R.w;
-        };
+        /* largest m1 with (m1 - m0) + 26 (rank(m1) - q0) <= PACK_T */
+        int lo = m0 + 1, hi = min(nmb, m0 + PACK_T);
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if ((mid - m0) + NPC * (dyn_rank_m(R, mbw, m_mbw, mid) - q0) <= PACK_T) lo = mid;
+            else hi = mid - 1;
+        }
+        const int m1 = lo, nm = m1 - m0, nd = dyn_rank_m(R, mbw, m_mbw, m1) - q0;
         nwin++;
 
-        /* A: the previous window's whole words -> staging; then residual ->
-         * transform -> quantised levels (int8 packed) and TotalCoeff to LDS */
+        /* P1: flush of the previous window; pieces: token and length */
         const uint32_t pnf = pend_T >> 5;
         uint32_t part = 0;
         if (pend_T) {
             flush_words(pnf, bw);
             part = L.buf[pnf];
         }
-        CapSink bcap{0, 0, 0};
-        bool heavy = false;
-        if (t < 24 * nd) {
-            const Task q = task_of(t, nd, m4, m2);
-            int ry, cx;
-            dcoord(q.k, ry, cx);
+        const int pi = t - nm;
+        const bool is_piece = pi >= 0 && pi < NPC * nd;
+        int kd = 0, pc = 0;
+        uint32_t tv = 0, tl = 0, mv = 0;
+        int nC = 0;
+        uint4 bd = make_uint4(0, 0, 0, 0);
+        if (is_piece) {
+            kd = (int)div_m((uint32_t)pi, m_pc);
+            pc = pi - kd * NPC;
+            const int q = q0 + kd;
+            const int ry = (int)div_m((uint32_t)q, m_rw), cx = q - ry * R.w;
             const int row = R.y0 + ry, col = R.x0 + cx;
-            const bool curA = row < a_end;
-            const int ref = curA ? rg.ra : rg.rb, mvp = curA ? rg.mva : rg.mvb;
-            int res[16], W[16];
-            if (q.luma) {
-                const uint8_t *sp = fs + (size_t)(16 * ry + 4 * q.by) * lstride + 16 * cx + 4 * q.bx;
-                const int X = 16 * col + 4 * q.bx;
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const uint32_t e = L.rmap[16 * ry + 4 * q.by + i];
-                    uint32_t sv = 0x80604020u + (uint32_t)(t + i), pv = 0x10203040u;
-                    if (!ABL(SCROLL_DEBUG_DYN_NOLOAD)) {
-                        sv = ld32(sp + (size_t)i * lstride);
-                        pv = ld32(rb + (e >> 15) * (uint32_t)pic + (e & 0x7fffu) * (uint32_t)w + X);
-                    }
-#pragma unroll
-                    for (int x = 0; x < 4; ++x)
-                        res[4 * i + x] = (int)((sv >> (8 * x)) & 255u) - (int)((pv >> (8 * x)) & 255u);
-                }
-                fwd4x4(res, W);
-                uint32_t pk[4] = {0, 0, 0, 0};
-                int n = 0;
-#pragma unroll
-                for (int k2 = 0; k2 < 16; ++k2) {
-                    const int v = quant(W[ZZ[k2]], ZZ[k2]);          /* |v| <= 78: int8 */
-                    pk[k2 >> 2] |= ((uint32_t)v & 255u) << (8 * (k2 & 3));
-                    n += v != 0;
-                }
-                *reinterpret_cast<uint4 *>(L.lv8[24 * q.k + q.blk]) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
-                heavy = n > HEAVY_TC;
-                L.tc[q.k][q.blk] = (uint8_t)n;
-                if (q.by == 3) L.ctx[(ry & rmask) * R.w + cx][q.bx] = (uint8_t)n;
+            const uint32_t *Mq = M + (size_t)q * NPC;
+            mv = Mq[pc];
+            const int tc = (int)((mv >> 8) & 31u), t1 = (int)((mv >> 13) & 3u);
+            uint32_t len;
+            if (pc == 16 || pc == 17) {
+                nC = -1;
+                len = mv & 255u;
             } else {
-                const uint8_t *sp = (q.p ? fcr : fcb) + (size_t)(8 * ry + 4 * q.by) * cstride +
-                                    8 * cx + 4 * q.bx;
-                const int X = 8 * col + 4 * q.bx, Y = 8 * row + 4 * q.by;
-                const int qq = 4 * mvp, o = qq >> 3, fr = qq & 7;
-                const int cw = w / 2;
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const uint32_t sv = ABL(SCROLL_DEBUG_DYN_NOLOAD) ? 0x40506070u + (uint32_t)t
-                                                                          : ld32(sp + (size_t)i * cstride);
-                    const int ya = Y + i + o;
-                    const uint32_t ea = L.rmap[16 * R.h + 8 * ry + 4 * q.by + i];
-                    const uint32_t eb = fr ? L.rmap[24 * R.h + 8 * ry + 4 * q.by + i] : 0u;
-                    const int ba = ea == 0xffffu ? -1 : (int)(ea >> 15), yoa = (int)(ea & 0x7fffu);
-                    const int bb = eb == 0xffffu ? -1 : (int)(eb >> 15), yob = (int)(eb & 0x7fffu);
-                    int pred[4];
-                    if (!GENERAL && (ba < 0 || bb < 0)) {
-                        L.general = 1;
-                        pred[0] = pred[1] = pred[2] = pred[3] = 0;
-                    } else if (ba >= 0 && bb >= 0) {
-                        const uint8_t *cp = rb + ysz + (size_t)q.p * csz + X;
-                        const bool nl = ABL(SCROLL_DEBUG_DYN_NOLOAD);
-                        const uint32_t av =
-                            nl ? 0x11223344u : ld32(cp + (uint32_t)ba * (uint32_t)pic + (uint32_t)yoa * (uint32_t)cw);
-                        const uint32_t bv =
-                            fr && !nl ? ld32(cp + (uint32_t)bb * (uint32_t)pic + (uint32_t)yob * (uint32_t)cw) : 0u;
-#pragma unroll
-                        for (int x = 0; x < 4; ++x) {
-                            const int a = (int)((av >> (8 * x)) & 255u), b = (int)((bv >> (8 * x)) & 255u);
-                            pred[x] = ((8 - fr) * a + fr * b + 4) >> 3;
-                        }
-                    } else {                       /* half-pel waypoint step: general path */
-                        if constexpr (GENERAL) {
-                            RefPics P;
-                            P.w = w;
-                            P.h = h;
-                            for (int i2 = 0; i2 < 2; ++i2) {
-                                P.pl[i2][0] = rb + i2 * pic;
-                                P.pl[i2][1] = P.pl[i2][0] + ysz;
-                                P.pl[i2][2] = P.pl[i2][1] + csz;
-                            }
-                            for (int x = 0; x < 4; ++x) {
-                                const int a = chroma_px_any<9>(T, P, ref, 1 + q.p, X + x, ya);
-                                const int b = fr ? chroma_px_any<9>(T, P, ref, 1 + q.p, X + x, ya + 1) : 0;
-                                pred[x] = ((8 - fr) * a + fr * b + 4) >> 3;
-                            }
-                        }
-                    }
-#pragma unroll
-                    for (int x = 0; x < 4; ++x) res[4 * i + x] = (int)((sv >> (8 * x)) & 255u) - pred[x];
+                int nA, nB;
+                if (pc < 16) {
+                    const int bx = pc & 3, by = pc >> 2;
+                    nA = bx > 0 ? (int)((Mq[pc - 1] >> 8) & 31u)
+                                : (cx > 0 ? (int)((Mq[pc + 3 - NPC] >> 8) & 31u) : (col > 0 ? 0 : -1));
+                    nB = by > 0 ? (int)((Mq[pc - 4] >> 8) & 31u)
+                                : (ry > 0 ? (int)((Mq[pc + 12 - NPC * R.w] >> 8) & 31u)
+                                          : (row > 0 ? 0 : -1));
+                } else {
+                    const int b = (pc - 18) & 3, bx = b & 1, by = b >> 1;
+                    nA = bx > 0 ? (int)((Mq[pc - 1] >> 8) & 31u)
+                                : (cx > 0 ? (int)((Mq[pc + 1 - NPC] >> 8) & 31u) : (col > 0 ? 0 : -1));
+                    nB = by > 0 ? (int)((Mq[pc - 2] >> 8) & 31u)
+                                : (ry > 0 ? (int)((Mq[pc + 2 - NPC * R.w] >> 8) & 31u)
+                                          : (row > 0 ? 0 : -1));
                 }
-                fwd4x4(res, W);
-                L.dcraw[q.k][q.p][2 * q.by + q.bx] = W[0];
-                uint32_t pk[4] = {0, 0, 0, 0};
-                int n = 0;
-#pragma unroll
-                for (int k2 = 1; k2 < 16; ++k2) {
-                    const int v = quant(W[ZZ[k2]], ZZ[k2]);
-                    pk[(k2 - 1) >> 2] |= ((uint32_t)v & 255u) << (8 * ((k2 - 1) & 3));
-                    n += v != 0;
+                nC = nc_of(nA, nB);
+                if (nC >= 8) {
+                    tv = tc ? (uint32_t)(((tc - 1) << 2) | t1) : 3u;
+                    tl = 6;
+                } else {
+                    const uint32_t e = PT.ct[nC < 2 ? 0 : (nC < 4 ? 1 : 2)][4 * tc + t1];
+                    tv = e & 255u;
+                    tl = e >> 8;
                 }
-                *reinterpret_cast<uint4 *>(L.lv8[24 * q.k + q.blk]) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
-                heavy = n > HEAVY_TC;
-                L.tc[q.k][q.blk] = (uint8_t)n;
-                if (q.by == 1) L.ctx[(ry & rmask) * R.w + cx][4 + 2 * q.p + q.bx] = (uint8_t)n;
+                len = tl + (mv & 255u);
             }
+            if (mv & M_OVF) {                          /* rare: re-code from the levels */
+                bd = Bd[(size_t)q * NPC + pc];
+                CountSink cn{0};
+                if (nC == -1) {
+                    const int dq[4] = {(int)(int16_t)(bd.x & 0xffffu), (int)(int16_t)(bd.x >> 16),
+                                       (int)(int16_t)(bd.y & 0xffffu), (int)(int16_t)(bd.y >> 16)};
+                    cavlc_dc4(cn, PT, dq);
+                } else {
+                    const int8_t *lvp = reinterpret_cast<const int8_t *>(&bd);
+                    cavlc_block(cn, TB, lvp, pc < 16 ? 16 : 15, nC);
+                }
+                len = cn.n;
+            } else if (mv & 255u) {
+                bd = Bd[(size_t)q * NPC + pc];
+            }
+            L.tc[kd][pc] = (uint8_t)tc;
+            L.blen[kd][pc] = (uint16_t)len;
         }
-        const uint64_t hb = __ballot(heavy);
-        if (lane == 0) L.whc[wave] = (uint32_t)__popcll(hb);
         __syncthreads();
         mark(0);
-        if (!GENERAL && L.general) {                /* uniform: read after the barrier */
-            if (t == 0) DF->err = DF_GENERAL;
-            return;
-        }
 
-        /* B: buffer rewind after the flush; nC, coded flags, coeff_token;
-         * chroma DC Hadamard + quant + CAVLC */
+        /* P2: buffer rewind; heads: cbp, piece offsets, MB length, scan */
         if (pend_T) {
-            for (uint32_t jw = (uint32_t)t; jw <= pnf; jw += DT) L.buf[jw] = jw == 0 ? part : 0u;
+            for (uint32_t jw = (uint32_t)t; jw <= pnf; jw += PACK_T) L.buf[jw] = jw == 0 ? part : 0u;
             rewind_lnz();
             F = pend_T & 31u;
             bw += pnf;
             pend_T = 0;
         }
-        /* encode order: light blocks (<= HEAVY_TC non-zero levels) first, so
-         * the encode loop of a wave runs few iterations; heavy ones share the
-         * last wave(s) */
-        const int ntask = 24 * nd;
-        if (t < ntask) {
-            uint32_t hpre = 0, htot = 0;
-#pragma unroll
-            for (int w2 = 0; w2 < NW; ++w2) {
-                hpre += w2 < wave ? L.whc[w2] : 0u;
-                htot += L.whc[w2];
-            }
-            const uint32_t hr = hpre + (uint32_t)__builtin_amdgcn_mbcnt_hi(
-                                           (uint32_t)(hb >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)hb, 0u));
-            const uint32_t lr = (uint32_t)t - hr;
-            L.order[heavy ? (uint32_t)ntask - htot + hr : lr] = (uint8_t)t;
-        }
-        if (t < 2 * nd) {
-            const int k = t >> 1, p = t & 1;
-            const int *dc = L.dcraw[k][p];
-            const int f00 = dc[0] + dc[1] + dc[2] + dc[3], f01 = dc[0] - dc[1] + dc[2] - dc[3];
-            const int f10 = dc[0] + dc[1] - dc[2] - dc[3], f11 = dc[0] - dc[1] - dc[2] + dc[3];
-            const int dq[4] = {quant_dc(f00), quant_dc(f01), quant_dc(f10), quant_dc(f11)};
-            int16_t *o = L.dclv[k][p];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) o[i] = (int16_t)dq[i];
-            CountSink dn{0};
-            cavlc_dc4(dn, PT, dq);
-            L.blen[k][16 + p] = (uint16_t)dn.n;
-        }
-        __syncthreads();
-
-        /* B2: CAVLC of the block order[t] (token .. runs) into registers */
-        /* the encoded block, packed to keep registers free across barriers:
-         * bit 31 valid, 30 ok, 24..29 nC + 1, 16..23 MB of the window, 8..15
-         * piece, 0..7 dynamic MB k */
-        uint32_t enc = 0;
-        if (t < ntask) {
-            int enc_nc = 0, e_k = 0, e_pc = 0, e_u = 0, etask;
-            bool enc_ok = true;
-            etask = L.order[t];
-            const Task q = task_of(etask, nd, m4, m2);
-            int ry, cx;
-            dcoord(q.k, ry, cx);
-            const int row = R.y0 + ry, col = R.x0 + cx;
-            e_k = q.k;
-            e_pc = q.luma ? q.blk : 18 + (q.blk - 16);
-            e_u = row * mbw + col - m0;                /* MB of the window */
-            const bool ldyn = col > R.x0, lav = col > 0, tdyn = row > R.y0, tav = row > 0;
-            const uint8_t *tc = L.tc[q.k];
-            int nA, nB;
-            bool coded;
-            if (q.luma) {
-                const int r = q.blk;
-                nA = q.bx > 0 ? tc[r - 1]
-                              : (ldyn ? (q.k > 0 ? L.tc[q.k - 1][r + 3] : L.lcarry[q.by]) : (lav ? 0 : -1));
-                nB = q.by > 0 ? tc[r - 4]
-                              : (tdyn ? L.ctx[((ry - 1) & rmask) * R.w + cx][q.bx] : (tav ? 0 : -1));
-                const int b8 = 4 * (q.by & 2) + (q.bx & 2);
-                coded = (tc[b8] | tc[b8 + 1] | tc[b8 + 4] | tc[b8 + 5]) != 0;
-            } else {
-                const int i = q.blk;
-                nA = q.bx > 0 ? tc[i - 1]
-                              : (ldyn ? (q.k > 0 ? L.tc[q.k - 1][i + 1] : L.lcarry[4 + 2 * q.p + q.by])
-                                      : (lav ? 0 : -1));
-                nB = q.by > 0 ? tc[i - 2]
-                              : (tdyn ? L.ctx[((ry - 1) & rmask) * R.w + cx][4 + 2 * q.p + q.bx]
-                                      : (tav ? 0 : -1));
-                uint32_t any = 0;
-#pragma unroll
-                for (int k2 = 16; k2 < 24; ++k2) any |= tc[k2];
-                coded = any != 0;
-            }
-            enc_nc = nc_of(nA, nB);
-            if (coded && ABL(SCROLL_DEBUG_DYN_NOCAVLC)) {
-                bcap.put(1, 1);
-            } else if (coded) {
-                const uint4 v4 = *reinterpret_cast<const uint4 *>(L.lv8[24 * q.k + q.blk]);
-                const uint32_t pk[4] = {v4.x, v4.y, v4.z, v4.w};
-                if (q.luma) cavlc_nz<16>(bcap, PT, pk, enc_nc, enc_ok);
-                else cavlc_nz<15>(bcap, PT, pk, enc_nc, enc_ok);
-            }
-            L.blen[q.k][q.luma ? q.blk : 18 + (q.blk - 16)] = (uint16_t)bcap.n;
-            enc = 0x80000000u | (enc_ok ? 0x40000000u : 0u) | (uint32_t)(enc_nc + 1) << 24 |
-                  (uint32_t)e_u << 16 | (uint32_t)e_pc << 8 | (uint32_t)e_k;
-        }
-        __syncthreads();
-        mark(1);
-
-        /* C: MB heads, cbp, piece offsets; in-wave scan of the MB lengths */
         uint32_t mlen = 0;
-        int kd = -1, hsel = 0, code = 0, cbp = 0;
-        const bool head_over = L.head_over;        /* uniform */
-        if (t < nm && ABL(SCROLL_DEBUG_DYN_NOHEAD)) {
-            mlen = 1;
-        } else if (t < nm) {
-            const int m = m0 + t, row = (int)div_m((uint32_t)m, m_mbw), col = m - row * mbw;
-            const bool curA = row < a_end, abvA = (row - 1) < a_end;
-            hsel = 3 * (row == 0 ? 0 : (curA ? 1 : (abvA ? 2 : 3))) +
-                   (col == 0 ? 0 : (col == mbw - 1 ? 2 : 1));
+        int hsel = 0, code = 0, cbp = 0, hrow = 0, hcol = 0, hkd = -1;
+        if (t < nm) {
+            const int m = m0 + t;
+            hrow = (int)div_m((uint32_t)m, m_mbw);
+            hcol = m - hrow * mbw;
+            hsel = head_sel(hrow, hcol);
             CountSink mc{head_over ? 0u : L.hlen[hsel]};
-            if (head_over) {                       /* > 128-bit heads: per MB */
-                const int ref = curA ? rg.ra : rg.rb, mv4 = 4 * (curA ? rg.mva : rg.mvb);
-                const int aref = abvA ? rg.ra : rg.rb, amv4 = 4 * (abvA ? rg.mva : rg.mvb);
-                int px, py;
-                predict(col, row, mbw, ref, mv4, aref, amv4, px, py);
-                put_mb_head(mc, ref, 0 - px, mv4 - py, nrefs);
-            }
-            const bool isdyn = col >= R.x0 && col < R.x0 + R.w && row >= R.y0 && row < R.y0 + R.h;
+            if (head_over) put_head_slow(mc, hrow, hcol);
+            const bool isdyn = hcol >= R.x0 && hcol < R.x0 + R.w && hrow >= R.y0 && hrow < R.y0 + R.h;
             if (!isdyn) {
-                mlen = mc.n + 1u;                  /* + coded_block_pattern ue(0) */
+                mlen = mc.n + 1u;                      /* + coded_block_pattern ue(0) */
             } else {
-                kd = (row - R.y0) * R.w + (col - R.x0) - q0;
-                /* bulk LDS reads (no dependent chains): TotalCoeff, lengths */
-                const uint4 t0 = *reinterpret_cast<const uint4 *>(L.tc[kd]);
-                const uint2 t1 = *reinterpret_cast<const uint2 *>(L.tc[kd] + 16);
-                const uint32_t tw[6] = {t0.x, t0.y, t0.z, t0.w, t1.x, t1.y};
+                hkd = (hrow - R.y0) * R.w + (hcol - R.x0) - q0;
+                const uint4 t0 = *reinterpret_cast<const uint4 *>(L.tc[hkd]);
+                const uint4 t1 = *reinterpret_cast<const uint4 *>(L.tc[hkd] + 16);
+                const uint32_t tw[8] = {t0.x, t0.y, t0.z, t0.w, t1.x, t1.y, t1.z, t1.w};
                 int cbp_l = 0;
 #pragma unroll
-                for (int b8 = 0; b8 < 4; ++b8) {             /* rows 2(b8>>1), +1; cols 2(b8&1), +1 */
+                for (int b8 = 0; b8 < 4; ++b8) {      /* raster rows 2(b8>>1), +1; cols 2(b8&1), +1 */
                     const int r0 = 2 * (b8 >> 1), sh = 16 * (b8 & 1);
                     if (((tw[r0] >> sh) & 0xffffu) | ((tw[r0 + 1] >> sh) & 0xffffu)) cbp_l |= 1 << b8;
                 }
-                const uint32_t ac = tw[4] | tw[5];
-                const int16_t *dl = &L.dclv[kd][0][0];
-                int anydc = 0;
-#pragma unroll
-                for (int k2 = 0; k2 < 8; ++k2) anydc |= dl[k2];
+                /* pieces 16, 17 = DC (bytes 0, 1 of tw[4]); 18..25 AC */
+                const bool ac = ((tw[4] >> 16) | tw[5] | (tw[6] & 0xffffu)) != 0u;
+                const bool anydc = (tw[4] & 0xffffu) != 0u;
                 const int cbp_c = ac ? 2 : (anydc ? 1 : 0);
                 cbp = cbp_l | (cbp_c << 4);
                 code = TB.cbp_code[cbp];
-                L.cbp[kd] = (uint8_t)cbp;
                 put_ue(mc, (uint32_t)code);
-                if (cbp) put_se(mc, 0);            /* mb_qp_delta */
+                if (cbp) put_se(mc, 0);                /* mb_qp_delta */
                 uint32_t bl[32], bo[32];
 #pragma unroll
                 for (int v = 0; v < 4; ++v) {
-                    const uint4 x = reinterpret_cast<const uint4 *>(L.blen[kd])[v];
+                    const uint4 x = reinterpret_cast<const uint4 *>(L.blen[hkd])[v];
                     const uint32_t xw[4] = {x.x, x.y, x.z, x.w};
 #pragma unroll
-                    for (int h = 0; h < 4; ++h) {
-                        bl[8 * v + 2 * h] = xw[h] & 0xffffu;
-                        bl[8 * v + 2 * h + 1] = xw[h] >> 16;
+                    for (int hh = 0; hh < 4; ++hh) {
+                        bl[8 * v + 2 * hh] = xw[hh] & 0xffffu;
+                        bl[8 * v + 2 * hh + 1] = xw[hh] >> 16;
                     }
                 }
                 uint32_t off = mc.n;
 #pragma unroll
-                for (int blk = 0; blk < 16; ++blk) {       /* luma4x4BlkIdx order */
+                for (int blk = 0; blk < 16; ++blk) {   /* luma4x4BlkIdx order */
                     const int r = blk_raster(blk);
-                    bo[r] = off;
-                    off += bl[r];
+                    const bool pres = (cbp_l >> (blk >> 2)) & 1;
+                    bo[r] = pres ? off : 0xffffu;
+                    off += pres ? bl[r] : 0u;
                 }
 #pragma unroll
-                for (int k2 = 16; k2 < 26; ++k2) {         /* Cb DC, Cr DC, Cb AC 0-3, Cr AC 0-3 */
-                    bo[k2] = off;
-                    off += (k2 < 18 ? cbp_c >= 1 : cbp_c == 2) ? bl[k2] : 0u;
+                for (int k2 = 16; k2 < NPC; ++k2) {    /* Cb DC, Cr DC, Cb AC 0-3, Cr AC 0-3 */
+                    const bool pres = k2 < 18 ? cbp_c >= 1 : cbp_c == 2;
+                    bo[k2] = pres ? off : 0xffffu;
+                    off += pres ? bl[k2] : 0u;
                 }
 #pragma unroll
-                for (int k2 = 26; k2 < 32; ++k2) bo[k2] = 0;
+                for (int k2 = NPC; k2 < 32; ++k2) bo[k2] = 0xffffu;
 #pragma unroll
                 for (int v = 0; v < 4; ++v)
-                    reinterpret_cast<uint4 *>(L.boff[kd])[v] =
+                    reinterpret_cast<uint4 *>(L.boff[hkd])[v] =
                         make_uint4(bo[8 * v] | bo[8 * v + 1] << 16, bo[8 * v + 2] | bo[8 * v + 3] << 16,
                                    bo[8 * v + 4] | bo[8 * v + 5] << 16, bo[8 * v + 6] | bo[8 * v + 7] << 16);
                 mlen = off;
@@ -632,98 +743,76 @@ __global__ __launch_bounds__(DT, SCROLL_DYN_WAVES) void k_dyn_stage(DevStream *_
             if (lane == 63) L.wsum[wave] = incl;
         }
         __syncthreads();
-        mark(2);
-        uint32_t wtot = 0, wpre[NW];
+        mark(1);
+
+        uint32_t wtot = 0;
 #pragma unroll
-        for (int w2 = 0; w2 < NW; ++w2) {
-            wpre[w2] = wtot;
-            wtot += L.wsum[w2];
-        }
-        /* offset of MB u of the window */
-        auto mbo = [&](int u) -> uint32_t {
-            uint32_t pre = 0;
-#pragma unroll
-            for (int w2 = 0; w2 < NW; ++w2)
-                if (w2 == (u >> 6)) pre = wpre[w2];
-            return pre + L.exw[u];
-        };
+        for (int w2 = 0; w2 < PNW; ++w2) wtot += L.wsum[w2];
+        auto mbo = [&](int u) -> uint32_t { return pack_wave_pre(L.wsum, u >> 6) + L.exw[u]; };
         const uint32_t Tb = F + wtot;
-        if (bw + (Tb >> 5) + 2u > cap_words) {      /* uniform */
+        if (bw + (Tb >> 5) + 2u > cap_words) {         /* uniform */
             over = true;
             break;
         }
 
-        /* D: every piece ORed into the buffer; a window larger than the
-         * buffer is written and flushed in passes of BUF_WORDS - 1 words */
+        /* P3: heads and pieces ORed into the buffer; a window larger than
+         * the buffer is written and flushed in passes of PBUF_WORDS - 1 words */
         const uint32_t nw = (Tb + 31) >> 5;
-        const bool single = nw <= (uint32_t)BUF_WORDS;
-        const uint32_t PW = single ? (uint32_t)BUF_WORDS : (uint32_t)BUF_WORDS - 1u;
-        const uint32_t my_mbo = t < nm ? mbo(t) : 0u;
+        const bool single = nw <= (uint32_t)PBUF_WORDS;
+        const uint32_t PW = single ? (uint32_t)PBUF_WORDS : (uint32_t)PBUF_WORDS - 1u;
+        const uint32_t my_head = t < nm ? F + mbo(t) : 0u;
+        uint32_t my_piece = 0xffffffffu;
+        if (is_piece) {
+            const uint32_t bo = L.boff[kd][pc];
+            if (bo != 0xffffu) {
+                const int q = q0 + kd;
+                const int mq = dyn_mb_m(R, mbw, m_rw, q) - m0;
+                my_piece = F + mbo(mq) + bo;
+            }
+        }
         for (uint32_t p0 = 0; p0 < nw; p0 += PW) {
             const LdsOrWin win{L.buf, p0, PW};
-            if (t < nm && !ABL(SCROLL_DEBUG_DYN_NOWRITE | SCROLL_DEBUG_DYN_NOHEAD)) {   /* MB head */
+            if (t < nm) {
                 WSink sk{win, 0, 0, 0};
-                sk.start(F + my_mbo);
-                if (!head_over) {
-                    sk.put_cap(CapSink{L.hhi[hsel], L.hlo[hsel], L.hlen[hsel]});
-                } else {
-                    const int m = m0 + t, row = (int)div_m((uint32_t)m, m_mbw), col = m - row * mbw;
-                    const bool curA = row < a_end, abvA = (row - 1) < a_end;
-                    const int ref = curA ? rg.ra : rg.rb, mv4 = 4 * (curA ? rg.mva : rg.mvb);
-                    const int aref = abvA ? rg.ra : rg.rb, amv4 = 4 * (abvA ? rg.mva : rg.mvb);
-                    int px, py;
-                    predict(col, row, mbw, ref, mv4, aref, amv4, px, py);
-                    put_mb_head(sk, ref, 0 - px, mv4 - py, nrefs);
-                }
-                if (kd < 0) {
-                    sk.put(1, 1);                  /* coded_block_pattern ue(0) */
+                sk.start(my_head);
+                if (!head_over) sk.put_cap(CapSink{L.hhi[hsel], L.hlo[hsel], L.hlen[hsel]});
+                else put_head_slow(sk, hrow, hcol);
+                if (hkd < 0) {
+                    sk.put(1, 1);                      /* coded_block_pattern ue(0) */
                 } else {
                     put_ue(sk, (uint32_t)code);
                     if (cbp) put_se(sk, 0);
                 }
                 sk.finish();
             }
-            if ((enc >> 31) && bcap.n && !ABL(SCROLL_DEBUG_DYN_NOWRITE)) {
-                const int e_k = (int)(enc & 255u), e_pc = (int)((enc >> 8) & 255u);
+            if (my_piece != 0xffffffffu) {
                 WSink sk{win, 0, 0, 0};
-                sk.start(F + mbo((int)((enc >> 16) & 255u)) + L.boff[e_k][e_pc]);
-                if ((enc >> 30) & 1u) {
-                    sk.put_cap(bcap);
-                } else {                           /* > 128 bits: re-encode from LDS */
-                    const int blk = e_pc < 16 ? e_pc : 16 + (e_pc - 18);
-                    const int8_t *lv = reinterpret_cast<const int8_t *>(L.lv8[24 * e_k + blk]);
-                    cavlc_block(sk, TB, lv, e_pc < 16 ? 16 : 15, (int)((enc >> 24) & 63u) - 1);
+                sk.start(my_piece);
+                if (!(mv & M_OVF)) {
+                    if (nC != -1) sk.put(tv, (int)tl);
+                    sk.put_cap(CapSink{(uint64_t)bd.z | (uint64_t)bd.w << 32,
+                                       (uint64_t)bd.x | (uint64_t)bd.y << 32, mv & 255u});
+                } else if (nC == -1) {
+                    const int dq[4] = {(int)(int16_t)(bd.x & 0xffffu), (int)(int16_t)(bd.x >> 16),
+                                       (int)(int16_t)(bd.y & 0xffffu), (int)(int16_t)(bd.y >> 16)};
+                    cavlc_dc4(sk, PT, dq);
+                } else {
+                    const int8_t *lvp = reinterpret_cast<const int8_t *>(&bd);
+                    cavlc_block(sk, TB, lvp, pc < 16 ? 16 : 15, nC);
                 }
                 sk.finish();
             }
-            if (t < 2 * nd && !ABL(SCROLL_DEBUG_DYN_NOWRITE)) {   /* chroma DC, from LDS */
-                const int k = t >> 1, p = t & 1;
-                if (L.cbp[k] >> 4) {
-                    int ry, cx;
-                    dcoord(k, ry, cx);
-                    WSink sk{win, 0, 0, 0};
-                    sk.start(F + mbo((R.y0 + ry) * mbw + R.x0 + cx - m0) + L.boff[k][16 + p]);
-                    const int16_t *o = L.dclv[k][p];
-                    const int dq[4] = {o[0], o[1], o[2], o[3]};
-                    cavlc_dc4(sk, PT, dq);
-                    sk.finish();
-                }
-            }
-            if (nd > 0 && t < 8) {                 /* left context of the next window */
-                const uint8_t *tc = L.tc[nd - 1];
-                L.lcarry[t] = t < 4 ? tc[4 * t + 3] : tc[16 + 4 * ((t - 4) >> 1) + 2 * ((t - 4) & 1) + 1];
-            }
             __syncthreads();
             if (single) {
-                pend_T = Tb;                       /* flushed during the next A */
-            } else {                               /* rare: flush this pass now */
+                pend_T = Tb;                           /* flushed during the next P1 */
+            } else {                                   /* rare: flush this pass now */
                 const uint32_t nfull = Tb >> 5;
                 const uint32_t n = p0 < nfull ? min(PW, nfull - p0) : 0u;
                 flush_words(n, bw + p0);
                 const uint32_t lastp = (Tb & 31u) && nfull - p0 < PW ? L.buf[nfull - p0] : 0u;
                 __syncthreads();
                 rewind_lnz();
-                for (uint32_t jw = (uint32_t)t; jw < (uint32_t)BUF_WORDS; jw += DT)
+                for (uint32_t jw = (uint32_t)t; jw < (uint32_t)PBUF_WORDS; jw += PACK_T)
                     L.buf[jw] = jw == 0 && p0 + PW >= nw ? lastp : 0u;
                 __syncthreads();
             }
@@ -732,12 +821,12 @@ __global__ __launch_bounds__(DT, SCROLL_DYN_WAVES) void k_dyn_stage(DevStream *_
             bw += Tb >> 5;
             F = Tb & 31u;
         }
-        mark(3);
+        mark(2);
         m0 = m1;
     }
 
     if (!over) {
-        if (pend_T) {                              /* the last window's whole words */
+        if (pend_T) {                                  /* the last window's whole words */
             const uint32_t pnf = pend_T >> 5;
             flush_words(pnf, bw);
             const uint32_t part = L.buf[pnf];
@@ -751,15 +840,20 @@ __global__ __launch_bounds__(DT, SCROLL_DYN_WAVES) void k_dyn_stage(DevStream *_
         /* rbsp_stop_one_bit + alignment (bitwriter.c:103-111); F < 32 */
         if (t == 0) {
             const uint32_t wv = L.buf[0] | (1u << (31 - F));
-            const uint32_t nb = (F + 1u + 7u) >> 3;
+            const uint32_t nb2 = (F + 1u + 7u) >> 3;
             out[bw] = __builtin_bswap32(wv);
             int prev = L.lnz_r;
-            my_ep += ep_word(wv, 4u * bw, 4u * bw + nb, prev, eplist, &L.ep_n);
-            DF->rbsp_bytes = 4u * bw + nb;
+            my_ep += ep_word(wv, 4u * bw, 4u * bw + nb2, prev, eplist, &L.ep_n);
+            DF->rbsp_bytes = 4u * bw + nb2;
         }
     }
-    uint32_t ex, tot;
-    block_excl_sum(my_ep, L.wsum, ex, tot);
+    /* EP total over the workgroup */
+    {
+        const uint32_t incl = wave_incl_sum(my_ep, lane);
+        __syncthreads();
+        if (lane == 63) L.wsum[wave] = incl;
+        __syncthreads();
+    }
     if (stamps && t == 0) {
         uint64_t *o = stamps + ((size_t)s * gridDim.x + f) * 8;
         for (int k = 0; k < 5; ++k) o[k] = ph[k];
@@ -768,11 +862,14 @@ __global__ __launch_bounds__(DT, SCROLL_DYN_WAVES) void k_dyn_stage(DevStream *_
         o[7] = (uint64_t)(uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 4);     /* HW_ID */
     }
     if (t == 0) {
+        uint32_t tot = 0;
+        for (int w2 = 0; w2 < PNW; ++w2) tot += L.wsum[w2];
         DF->ep = tot;
         DF->err = over ? DF_OVER : 0u;
         if (over) atomicOr((unsigned int *)&S->err, SCROLL_DEVERR_DYN);
     }
 }
+
 
 /* ---------------------------------------------------------------------- */
 /* k_dyn_emit: staged RBSP -> arena with start code, header, EP bytes       */
@@ -1072,17 +1169,30 @@ __global__ __launch_bounds__(256) void k_dyn_synth(uint8_t *__restrict__ src, Dy
 /* ---------------------------------------------------------------------- */
 /* launchers (engine-internal, engine.h)                                   */
 /* ---------------------------------------------------------------------- */
-int dyn_launch_stage(hipStream_t hs, int nframes, int S, DevStream *st, const NalDesc *nal,
-                     int ld_nal, const PlanPending *pend, DynFrame *dfr, int ld_fr,
-                     const DynGeom *g, const uint8_t *src, const uint8_t *refs, uint8_t *stage,
-                     uint64_t *stamps)
+int dyn_launch_code(hipStream_t hs, int nframes, int S, const DevStream *st, const NalDesc *nal,
+                    int ld_nal, const PlanPending *pend, DynFrame *dfr, int ld_fr,
+                    const DynGeom *g, const uint8_t *src, const uint8_t *refs, const DynScratch *x)
 {
     if (nframes <= 0 || S <= 0) return 0;
-    hipLaunchKernelGGL(k_dyn_stage<false>, dim3(nframes, S), dim3(DT), 0, hs, st, nal, ld_nal, pend,
-                       dfr, ld_fr, *g, src, refs, stage, stamps);
+    hipLaunchKernelGGL(k_dyn_rows, dim3(nframes, S), dim3(256), 0, hs, st, nal, ld_nal, pend, dfr, ld_fr,
+                       *g, x->rows);
     if (hipGetLastError() != hipSuccess) return -1;
-    hipLaunchKernelGGL(k_dyn_stage<true>, dim3(nframes, S), dim3(DT), 0, hs, st, nal, ld_nal, pend,
-                       dfr, ld_fr, *g, src, refs, stage, (uint64_t *)nullptr);
+    const int nchunk = (24 * g->w * g->h + CODE_T - 1) / CODE_T;
+    hipLaunchKernelGGL(k_dyn_code<false>, dim3(nchunk, nframes, S), dim3(CODE_T), 0, hs, st, dfr, ld_fr,
+                       pend, nal, ld_nal, *g, x->rows, src, refs, x->meta, x->body);
+    if (hipGetLastError() != hipSuccess) return -1;
+    hipLaunchKernelGGL(k_dyn_code<true>, dim3(nchunk, nframes, S), dim3(CODE_T), 0, hs, st, dfr, ld_fr,
+                       pend, nal, ld_nal, *g, x->rows, src, refs, x->meta, x->body);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int dyn_launch_pack(hipStream_t hs, int nframes, int S, DevStream *st, const NalDesc *nal,
+                    int ld_nal, const PlanPending *pend, DynFrame *dfr, int ld_fr,
+                    const DynGeom *g, const DynScratch *x, uint8_t *stage, uint64_t *stamps)
+{
+    if (nframes <= 0 || S <= 0) return 0;
+    hipLaunchKernelGGL(k_dyn_pack, dim3(nframes, S), dim3(PACK_T), 0, hs, st, nal, ld_nal, pend, dfr, ld_fr,
+                       *g, x->meta, x->body, stage, stamps);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -80,12 +80,11 @@ typedef struct {
 /* dynamic rect geometry and buffer strides (one per batch) */
 #define DYN_MAX_W 64                /* rect width limit (MBs)                     */
 #define DYN_MAX_H 48                /* rect height limit (MBs)                    */
-#define DYN_CTX_MB 256              /* TotalCoeff row-ring entries (LDS)          */
-#define DYN_WINDOW_MBS 10           /* dynamic MBs per k_dyn_stage window         */
+#define DYN_PIECES 26               /* coded pieces per dynamic MB: 16 luma, 2 DC, 8 AC */
 #define DYN_OVF_BYTES 8192          /* staging-slot tail: levels of > 128-bit blocks */
 typedef struct {
     int32_t x0, y0, w, h;           /* rect, MB units                             */
-    int32_t ring;                   /* rows in the TotalCoeff ring                */
+    int32_t pad0;
     int32_t debug;                  /* SCROLL_DEBUG_DYN_* ablation bits           */
     uint64_t src_ld, src_fr;        /* source bytes per stream / per frame        */
     uint64_t ref_ld;                /* reference-pair bytes per stream (0 shared) */

@@ -865,7 +865,7 @@ void dev_to_cfg(const DevStream *d, ComposerConfig *c)
 /* ======================================================================== */
 /* ScrollBatch                                                              */
 /* ======================================================================== */
-constexpr int NEV = 6;
+constexpr int NEV = 7;
 struct ScrollBatch {
     int device = 0;
     int mode = SCROLL_MODE_COMPOSER;
@@ -883,12 +883,12 @@ struct ScrollBatch {
     hipEvent_t ev[NEV] = {};
     int timing = 0;
     int timed_pending = 0;
-    float ms[4] = {0, 0, 0, 0};        /* plan, emit, dyn stage, dyn emit */
+    float ms[6] = {0, 0, 0, 0, 0, 0};  /* plan, emit, dyn stage, dyn emit, dyn code, dyn pack */
     std::vector<hipEvent_t> ring;      /* NEV events per timed compose, pending */
     std::vector<uint8_t> ring_dyn;     /* per pending compose: the dynamic-rect pipeline ran */
     int ev_dyn = 0;                    /* the same for b->ev */
     int ring_used = 0;
-    double acc_ms[4] = {0, 0, 0, 0};
+    double acc_ms[6] = {0, 0, 0, 0, 0, 0};
     int acc_n = 0;
     int host_valid = 1;
     int last_plan_mode = SCROLL_PLAN_COMPOSER;
@@ -905,6 +905,7 @@ struct ScrollBatch {
     DynGeom geo{};
     DynFrame *d_dfr = nullptr;
     uint8_t *d_src = nullptr, *d_refs = nullptr, *d_stage = nullptr;
+    DynScratch dx{};                   /* rows + block records of k_dyn_code / k_dyn_pack */
     /* UI hints: staged like the dynamic rect (shares
      * d_dfr, d_stage and geo.slot_bytes; the two are exclusive) */
     int hint_on = 0;
@@ -930,7 +931,7 @@ struct ScrollBatch {
 /* event pairs of one compose.  Dynamic rect: plan = [0,1) + [2,3), dyn
  * stage [1,2), emit [3,4), dyn emit [4,5).  Otherwise only events 0, 1, 4
  * are recorded (fewer markers between the kernels): plan [0,1), emit [1,4). */
-static void event_ms(const hipEvent_t *e, bool dyn, float out[4])
+static void event_ms(const hipEvent_t *e, bool dyn, float out[6])
 {
     auto el = [&](int a, int b) {
         float v = 0.0f;
@@ -941,10 +942,12 @@ static void event_ms(const hipEvent_t *e, bool dyn, float out[4])
         out[1] = el(3, 4);
         out[2] = el(1, 2);
         out[3] = el(4, 5);
+        out[4] = el(1, 6);
+        out[5] = el(6, 2);
     } else {
         out[0] = el(0, 1);
         out[1] = el(1, 4);
-        out[2] = out[3] = 0.0f;
+        out[2] = out[3] = out[4] = out[5] = 0.0f;
     }
 }
 
@@ -1150,9 +1153,9 @@ int32_t *scroll_batch_offsets_device(ScrollBatch *b) { return b ? b->d_off : nul
 static void fold_ring(ScrollBatch *b)
 {
     for (int i = 0; i + NEV <= b->ring_used; i += NEV) {
-        float m[4];
+        float m[6];
         event_ms(&b->ring[i], b->ring_dyn[i / NEV] != 0, m);
-        for (int k = 0; k < 4; ++k) b->acc_ms[k] += m[k];
+        for (int k = 0; k < 6; ++k) b->acc_ms[k] += m[k];
         b->acc_n++;
     }
     b->ring_used = 0;
@@ -1235,11 +1238,19 @@ static int launch(ScrollBatch *b, int nframes, int plan_mode, int nal_max, hipSt
                 set_err("k_hint_stage launch: %s", hipGetErrorString(hipGetLastError()));
                 return SCROLL_ERR_HIP;
             }
-        } else if (dyn_launch_stage(hs, nframes, S, b->d_st, b->d_nal, b->ld_nal, b->d_pend,
-                                    b->d_dfr, ld_fr, &b->geo, b->d_src, b->d_refs, b->d_stage,
-                                    stamps)) {
-            set_err("k_dyn_stage launch: %s", hipGetErrorString(hipGetLastError()));
-            return SCROLL_ERR_HIP;
+            if ((rc = mark(6))) return rc;
+        } else {
+            if (dyn_launch_code(hs, nframes, S, b->d_st, b->d_nal, b->ld_nal, b->d_pend, b->d_dfr,
+                                ld_fr, &b->geo, b->d_src, b->d_refs, &b->dx)) {
+                set_err("k_dyn_code launch: %s", hipGetErrorString(hipGetLastError()));
+                return SCROLL_ERR_HIP;
+            }
+            if ((rc = mark(6))) return rc;
+            if (dyn_launch_pack(hs, nframes, S, b->d_st, b->d_nal, b->ld_nal, b->d_pend, b->d_dfr,
+                                ld_fr, &b->geo, &b->dx, b->d_stage, stamps)) {
+                set_err("k_dyn_pack launch: %s", hipGetErrorString(hipGetLastError()));
+                return SCROLL_ERR_HIP;
+            }
         }
         if ((rc = mark(2))) return rc;
         hipLaunchKernelGGL(k_plan, dim3(S), dim3(PLAN_THREADS), 0, hs, b->d_st, b->d_off,
@@ -1432,19 +1443,19 @@ int scroll_batch_kernel_stats(ScrollBatch *b, double *plan_ms, double *emit_ms, 
     if (plan_ms) *plan_ms = b->acc_ms[0];
     if (emit_ms) *emit_ms = b->acc_ms[1];
     if (count) *count = b->acc_n;
-    for (int k = 0; k < 4; ++k) b->acc_ms[k] = 0;
+    for (int k = 0; k < 6; ++k) b->acc_ms[k] = 0;
     b->acc_n = 0;
     return SCROLL_OK;
 }
 
-int scroll_batch_kernel_stats_ex(ScrollBatch *b, double ms[4], int *count)
+int scroll_batch_kernel_stats_ex(ScrollBatch *b, double ms[6], int *count)
 {
     if (!b || !ms) return SCROLL_ERR_ARG;
     int rc = batch_host_sync(b);
     if (rc) return rc;
     HIPCHK(hipStreamSynchronize(b->last));
     fold_ring(b);
-    for (int k = 0; k < 4; ++k) {
+    for (int k = 0; k < 6; ++k) {
         ms[k] = b->acc_ms[k];
         b->acc_ms[k] = 0;
     }
@@ -1486,8 +1497,12 @@ static void dyn_release(ScrollBatch *b)
     (void)hipFree(b->d_src);
     (void)hipFree(b->d_refs);
     (void)hipFree(b->d_stage);
+    (void)hipFree(b->dx.rows);
+    (void)hipFree(b->dx.meta);
+    (void)hipFree(b->dx.body);
     b->d_dfr = nullptr;
     b->d_src = b->d_refs = b->d_stage = nullptr;
+    b->dx = DynScratch{};
     b->dyn_on = 0;
     b->dyn_refs = 0;
 }
@@ -1523,10 +1538,9 @@ int scroll_batch_set_dyn_rect(ScrollBatch *b, int x0, int y0, int w, int h, size
             return SCROLL_ERR_CONFIG;
         }
     const int mbw = pw / 16, mbh = ph / 16;
-    int ring = 1;                      /* rows a window spans + 1, as a power of two */
-    while (ring < std::min(h, (DYN_WINDOW_MBS + w - 1) / w + 2)) ring <<= 1;
+    /* prediction rows are byte offsets into a reference pair below 2^28 */
     if ((pw & 15) || (ph & 15) || x0 + w > mbw || y0 + h > mbh || w > DYN_MAX_W || h > DYN_MAX_H ||
-        ring * w > DYN_CTX_MB) {
+        (size_t)3 * pw * ph >= ((size_t)1 << 28)) {
         set_err("scroll_batch_set_dyn_rect: rect (%d,%d %dx%d MBs) not supported in %dx%d", x0, y0,
                 w, h, pw, ph);
         return SCROLL_ERR_CONFIG;
@@ -1536,7 +1550,6 @@ int scroll_batch_set_dyn_rect(ScrollBatch *b, int x0, int y0, int w, int h, size
     g.y0 = y0;
     g.w = w;
     g.h = h;
-    g.ring = ring;
     g.src_fr = (uint64_t)384 * w * h;
     g.src_ld = round256((size_t)b->max_frames * g.src_fr);
     g.ref_ld = 0;
@@ -1548,6 +1561,9 @@ int scroll_batch_set_dyn_rect(ScrollBatch *b, int x0, int y0, int w, int h, size
     if (e == hipSuccess) e = hipMalloc(&b->d_src, S * g.src_ld);
     if (e == hipSuccess) e = hipMalloc(&b->d_refs, S * dyn_pair_bytes(b));
     if (e == hipSuccess) e = hipMalloc(&b->d_stage, S * F * g.slot_bytes);
+    if (e == hipSuccess) e = hipMalloc(&b->dx.rows, S * F * 32 * h * sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMalloc(&b->dx.meta, S * F * DYN_PIECES * w * h * sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMalloc(&b->dx.body, S * F * DYN_PIECES * w * h * sizeof(uint4));
     if (e == hipSuccess) e = hipMemset(b->d_dfr, 0, S * F * sizeof(DynFrame));
     if (e == hipSuccess) e = hipMemset(b->d_src, 0, S * g.src_ld);
     if (e == hipSuccess) e = hipMemset(b->d_refs, 0, S * dyn_pair_bytes(b));
@@ -1941,7 +1957,7 @@ int scroll_batch_enable_timing(ScrollBatch *b, int on)
 
 float scroll_batch_kernel_ms(ScrollBatch *b, int which)
 {
-    if (!b || which < 0 || which > 3) return -1.0f;
+    if (!b || which < 0 || which > 5) return -1.0f;
     if (batch_host_sync(b)) return -1.0f;
     if (b->timed_pending) {
         event_ms(b->ev, b->ev_dyn != 0, b->ms);

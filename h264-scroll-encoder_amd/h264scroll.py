@@ -387,8 +387,9 @@ class Batch:
         return a.value, e.value, n.value
 
     def kernel_stats_ex(self):
-        """(plan, emit, dyn stage, dyn emit) ms summed since the last call, composes"""
-        ms, n = (ctypes.c_double * 4)(), ctypes.c_int()
+        """(plan, emit, dyn stage, dyn emit, dyn code, dyn pack) ms summed since
+        the last call, composes"""
+        ms, n = (ctypes.c_double * 6)(), ctypes.c_int()
         self._chk(lib.scroll_batch_kernel_stats_ex(self.h, ms, ctypes.byref(n)), "kernel_stats_ex")
         return tuple(ms), n.value
 

@@ -114,7 +114,8 @@ int scroll_batch_nal_info(ScrollBatch *b, int s, int i, int *kind, int *offset_p
                           uint32_t *size, int *slow);
 
 /* HIP-event timing of the last compose's kernels, on the launch stream:
- * which 0 = plan kernel(s), 1 = emit kernel, 2 = dyn stage, 3 = dyn emit.
+ * which 0 = plan kernel(s), 1 = emit kernel, 2 = dyn stage, 3 = dyn emit,
+ * 4 = dyn code (k_dyn_rows + k_dyn_code), 5 = dyn pack (k_dyn_pack).
  * Enable before compose. */
 int scroll_batch_enable_timing(ScrollBatch *b, int on);
 float scroll_batch_kernel_ms(ScrollBatch *b, int which);
@@ -160,8 +161,10 @@ int scroll_batch_dyn_frame_info(ScrollBatch *b, int s, int f, uint32_t *rbsp_byt
 int scroll_batch_dyn_totals(ScrollBatch *b, unsigned long long *rbsp_bytes,
                             unsigned long long *ep_bytes, long long *dyn_nals);
 /* HIP-event ms of the timed composes since the last call: plan (both
- * passes), emit, dyn stage, dyn emit; accumulators reset afterwards */
-int scroll_batch_kernel_stats_ex(ScrollBatch *b, double ms[4], int *count);
+ * passes), emit, dyn stage (= dyn code + dyn pack), dyn emit, dyn code
+ * (k_dyn_rows + k_dyn_code), dyn pack (k_dyn_pack); accumulators reset
+ * afterwards */
+int scroll_batch_kernel_stats_ex(ScrollBatch *b, double ms[6], int *count);
 
 /* ---- UI hints (reference design docs/MASTER_DESIGN.md:
  * 58-64,103-146, no reference implementation) ----

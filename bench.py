@@ -446,11 +446,20 @@ def main():
         kms = {"plan": plan_ms / n, "emit": emit_ms / n, "dyn_stage": stage_ms / n,
                "dyn_emit": demit_ms / n}
         if rect:
-            # k_dyn_stage per launch: source + prediction samples of every
-            # dynamic MB (384 B each) read, the staged RBSP written
-            kern = "k_dyn_stage"
-            alg_bytes = dyn_nals * 2 * 384 * rect[2] * rect[3] + rbsp_tot
-            kern_ms = kms["dyn_stage"]
+            kms["dyn_code"] = code_ms / n
+            kms["dyn_pack"] = pack_ms / n
+        if rect and kms["dyn_code"] >= kms["dyn_pack"]:
+            # k_dyn_rows + k_dyn_code per launch: the source and prediction
+            # samples of every dynamic MB (384 B each) read; the block
+            # records they write for k_dyn_pack are not algorithmic bytes
+            kern = "k_dyn_rows + k_dyn_code"
+            alg_bytes = dyn_nals * 2 * 384 * rect[2] * rect[3]
+            kern_ms = kms["dyn_code"]
+        elif rect:
+            # k_dyn_pack per launch: the staged RBSP written
+            kern = "k_dyn_pack"
+            alg_bytes = rbsp_tot
+            kern_ms = kms["dyn_pack"]
         elif hints:
             # k_hint_stage per launch: the staged RBSP written, the rects read
             kern = "k_hint_stage"

@@ -702,38 +702,22 @@ __global__ __launch_bounds__(PACK_T, 8) void k_dyn_pack(DevStream *__restrict__ 
                 code = TB.cbp_code[cbp];
                 put_ue(mc, (uint32_t)code);
                 if (cbp) put_se(mc, 0);                /* mb_qp_delta */
-                uint32_t bl[32], bo[32];
-#pragma unroll
-                for (int v = 0; v < 4; ++v) {
-                    const uint4 x = reinterpret_cast<const uint4 *>(L.blen[hkd])[v];
-                    const uint32_t xw[4] = {x.x, x.y, x.z, x.w};
-#pragma unroll
-                    for (int hh = 0; hh < 4; ++hh) {
-                        bl[8 * v + 2 * hh] = xw[hh] & 0xffffu;
-                        bl[8 * v + 2 * hh + 1] = xw[hh] >> 16;
-                    }
-                }
                 uint32_t off = mc.n;
+                uint16_t *bo = L.boff[hkd];
+                const uint16_t *bl = L.blen[hkd];
 #pragma unroll
                 for (int blk = 0; blk < 16; ++blk) {   /* luma4x4BlkIdx order */
                     const int r = blk_raster(blk);
                     const bool pres = (cbp_l >> (blk >> 2)) & 1;
-                    bo[r] = pres ? off : 0xffffu;
+                    bo[r] = pres ? (uint16_t)off : (uint16_t)0xffffu;
                     off += pres ? bl[r] : 0u;
                 }
 #pragma unroll
                 for (int k2 = 16; k2 < NPC; ++k2) {    /* Cb DC, Cr DC, Cb AC 0-3, Cr AC 0-3 */
                     const bool pres = k2 < 18 ? cbp_c >= 1 : cbp_c == 2;
-                    bo[k2] = pres ? off : 0xffffu;
+                    bo[k2] = pres ? (uint16_t)off : (uint16_t)0xffffu;
                     off += pres ? bl[k2] : 0u;
                 }
-#pragma unroll
-                for (int k2 = NPC; k2 < 32; ++k2) bo[k2] = 0xffffu;
-#pragma unroll
-                for (int v = 0; v < 4; ++v)
-                    reinterpret_cast<uint4 *>(L.boff[hkd])[v] =
-                        make_uint4(bo[8 * v] | bo[8 * v + 1] << 16, bo[8 * v + 2] | bo[8 * v + 3] << 16,
-                                   bo[8 * v + 4] | bo[8 * v + 5] << 16, bo[8 * v + 6] | bo[8 * v + 7] << 16);
                 mlen = off;
             }
         }

@@ -1,0 +1,39 @@
+/*
+ * ipcm_engine.h -- reference pictures -> reference files on the GPU
+ * (SURVEY §8f row 3): the experiment's I_PCM IDR writer
+ * (experiments/scroll-encoder/src/h264_encoder.c:730-918, one stripe colour
+ * per MB there) for arbitrary I420 pictures, as the SURVEY Appendix B harness
+ * frames it: SPS + PPS + one IDR slice of I_PCM MBs.
+ *
+ * RBSP of the IDR slice: hdr[0, nh) = slice header (h264_encoder.c:622-662)
+ * + MB 0's mb_type ue(25) + pcm_alignment_zero_bits; MB 0's 384 samples;
+ * then per MB m >= 1 the bytes 0x0D 0x00 (ue(25) at a byte boundary + 7
+ * alignment bits) and its 384 samples; the stop byte 0x80.  With
+ * base = nh - 2, MB m's 386-byte record starts at RBSP byte base + 386 m.
+ */
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#define IPCM_CHUNK 4096              /* RBSP bytes per workgroup              */
+#define IPCM_PRE_MAX 96              /* SPS + PPS NAL units + IDR start code   */
+
+typedef struct {
+    int32_t w, h;
+    uint32_t mbw, nmb;
+    uint32_t m_mbw, m_386;           /* magic multipliers: / mbw, / 386        */
+    uint64_t pic_stride, out_stride;
+    uint32_t nh;                     /* header RBSP bytes (<= 16)              */
+    uint32_t rbsp_len;               /* RBSP bytes including the stop byte     */
+    uint32_t npre;                   /* file prefix bytes                      */
+    uint32_t nchunk;                 /* IPCM_CHUNK chunks per file             */
+    uint8_t hdr[16];
+    uint8_t pre[IPCM_PRE_MAX];
+} IpcmGeom;
+
+/* pass 0: emulation-prevention bytes per chunk -> counts[n][nchunk];
+ * pass 1: files -> out (prefix, EBSP).  0, or -1 when a launch failed. */
+int ipcm_launch(hipStream_t hs, int pass, int n, const IpcmGeom *g, const uint8_t *pics,
+                uint32_t *counts, uint8_t *out);

@@ -23,6 +23,7 @@
 #include "dyn_engine.h"
 #include "hint_engine.h"
 #include "ingest_engine.h"
+#include "ipcm_engine.h"
 #include "engine.h"
 #include "scroll_device.h"
 
@@ -924,6 +925,11 @@ struct ScrollBatch {
     IngestOut *d_ing_out = nullptr;
     int ing_cap = 0;
     hipEvent_t ing_ev[2] = {};         /* timing: around the ingest kernels */
+    /* reference files from pictures: EP count per chunk */
+    uint32_t *d_ipcm_cnt = nullptr;
+    size_t ipcm_cap = 0;
+    double ipcm_ms = 0.0;
+    int ipcm_n = 0;
     double ing_ms = 0.0;
     int ing_n = 0;
 };
@@ -1045,6 +1051,7 @@ void scroll_batch_destroy(ScrollBatch *b)
     (void)hipFree(b->d_hf);
     (void)hipFree(b->d_pool);
     (void)hipFree(b->d_ing_in);
+    (void)hipFree(b->d_ipcm_cnt);
     (void)hipFree(b->d_ing_files);
     (void)hipFree(b->d_ing_scan);
     (void)hipFree(b->d_ing_out);
@@ -1910,6 +1917,132 @@ int scroll_batch_ingest_stats(ScrollBatch *b, double *ms, int *count)
     if (count) *count = b->ing_n;
     b->ing_ms = 0.0;
     b->ing_n = 0;
+    return SCROLL_OK;
+}
+
+/* ------------------- reference files from pictures (I_PCM) ------------------ */
+int scroll_batch_ipcm_files_device(ScrollBatch *b, int n, int w, int h, const uint8_t *d_pics,
+                                   size_t pic_stride, uint8_t *d_out, size_t out_stride,
+                                   uint64_t *sizes)
+{
+    if (!b || n < 0 || (n > 0 && (!d_pics || !d_out || !sizes))) return SCROLL_ERR_ARG;
+    if (n == 0) return SCROLL_OK;
+    const size_t nmb = (size_t)(w / 16) * (size_t)(h / 16);
+    if (w <= 0 || h <= 0 || (w & 15) || (h & 15) || nmb >= 65536 ||
+        pic_stride < (size_t)w * h * 3 / 2) {
+        set_err("scroll_batch_ipcm_files: %dx%d pictures (stride %zu) not supported", w, h, pic_stride);
+        return SCROLL_ERR_ARG;
+    }
+    int rc = batch_host_sync(b);
+    if (rc) return rc;
+    HIPCHK(hipSetDevice(b->device));
+    IpcmGeom g{};
+    g.w = w;
+    g.h = h;
+    g.mbw = (uint32_t)(w / 16);
+    g.nmb = (uint32_t)nmb;
+    g.m_mbw = g.mbw <= 1 ? 0u : 0xffffffffu / g.mbw + 1u;
+    g.m_386 = 0;
+    g.pic_stride = pic_stride;
+    g.out_stride = out_stride;
+    /* prefix: SPS, PPS (h264_generate_sps / _pps, identical in the composer
+     * and the experiment) as NAL units, then the IDR's start code + header */
+    {
+        uint8_t rbsp[64];
+        NALWriter nw;
+        uint8_t tmp[64];
+        nal_writer_init(&nw, g.pre, IPCM_PRE_MAX, tmp, sizeof(tmp));
+        size_t k = h264_generate_sps(rbsp, sizeof(rbsp), w, h);
+        nal_write_unit(&nw, 3, 7, rbsp, k, 1);
+        k = h264_generate_pps(rbsp, sizeof(rbsp));
+        nal_write_unit(&nw, 3, 8, rbsp, k, 1);
+        size_t o = nal_writer_get_size(&nw);
+        const uint8_t idr[5] = {0, 0, 0, 1, (uint8_t)(3 << 5 | 5)};
+        memcpy(g.pre + o, idr, 5);
+        g.npre = (uint32_t)(o + 5);
+    }
+    /* IDR slice header with the experiment's defaults (h264_encoder.c:12-29,
+     * :622-662) + MB 0's mb_type ue(25) and alignment (:730-736) */
+    {
+        BitWriter bw;
+        bitwriter_init(&bw, g.hdr, sizeof(g.hdr));
+        bitwriter_write_ue(&bw, 0);          /* first_mb_in_slice */
+        bitwriter_write_ue(&bw, 7);          /* slice_type I (all) */
+        bitwriter_write_ue(&bw, 0);          /* pic_parameter_set_id */
+        bitwriter_write_bits(&bw, 0, 4);     /* frame_num, log2_max_frame_num 4 */
+        bitwriter_write_ue(&bw, 0);          /* idr_pic_id */
+        bitwriter_write_bit(&bw, 0);         /* no_output_of_prior_pics_flag */
+        bitwriter_write_bit(&bw, 1);         /* long_term_reference_flag */
+        bitwriter_write_se(&bw, 0);          /* slice_qp_delta */
+        bitwriter_write_ue(&bw, 1);          /* disable_deblocking_filter_idc */
+        bitwriter_write_ue(&bw, 25);         /* mb_type I_PCM */
+        while (!bitwriter_is_byte_aligned(&bw)) bitwriter_write_bit(&bw, 0);
+        g.nh = (uint32_t)bitwriter_get_size(&bw);
+    }
+    g.rbsp_len = (uint32_t)(g.nh - 2 + 386 * nmb + 1);
+    g.nchunk = (g.rbsp_len + IPCM_CHUNK - 1) / IPCM_CHUNK;
+    const size_t need = (size_t)n * g.nchunk * sizeof(uint32_t);
+    if (need > b->ipcm_cap) {
+        (void)hipFree(b->d_ipcm_cnt);
+        b->d_ipcm_cnt = nullptr;
+        b->ipcm_cap = 0;
+        hipError_t e = hipMalloc(&b->d_ipcm_cnt, need);
+        if (e != hipSuccess) {
+            set_err("scroll_batch_ipcm_files: %s", hipGetErrorString(e));
+            return e == hipErrorOutOfMemory ? SCROLL_ERR_OOM : SCROLL_ERR_HIP;
+        }
+        b->ipcm_cap = need;
+    }
+    hipStream_t hs = b->own;
+    if (b->timing) HIPCHK(hipEventRecord(b->ing_ev[0], hs));
+    if (ipcm_launch(hs, 0, n, &g, d_pics, b->d_ipcm_cnt, d_out)) {
+        set_err("ipcm launch: %s", hipGetErrorString(hipGetLastError()));
+        return SCROLL_ERR_HIP;
+    }
+    std::vector<uint32_t> cnt((size_t)n * g.nchunk);
+    HIPCHK(hipMemcpyAsync(cnt.data(), b->d_ipcm_cnt, need, hipMemcpyDeviceToHost, hs));
+    HIPCHK(hipStreamSynchronize(hs));
+    float ms0 = 0.0f;
+    if (b->timing) {
+        HIPCHK(hipEventRecord(b->ing_ev[1], hs));
+        HIPCHK(hipEventSynchronize(b->ing_ev[1]));
+        HIPCHK(hipEventElapsedTime(&ms0, b->ing_ev[0], b->ing_ev[1]));
+    }
+    int over = -1;
+    for (int k = 0; k < n; ++k) {
+        uint64_t ep = 0;
+        for (uint32_t c = 0; c < g.nchunk; ++c) ep += cnt[(size_t)k * g.nchunk + c];
+        sizes[k] = g.npre + (uint64_t)g.rbsp_len + ep;
+        if (sizes[k] > out_stride && over < 0) over = k;
+    }
+    if (over >= 0) {
+        set_err("scroll_batch_ipcm_files: file %d needs %llu bytes, out_stride is %zu", over,
+                (unsigned long long)sizes[over], out_stride);
+        return SCROLL_ERR_OVERFLOW;
+    }
+    if (b->timing) HIPCHK(hipEventRecord(b->ing_ev[0], hs));
+    if (ipcm_launch(hs, 1, n, &g, d_pics, b->d_ipcm_cnt, d_out)) {
+        set_err("ipcm launch: %s", hipGetErrorString(hipGetLastError()));
+        return SCROLL_ERR_HIP;
+    }
+    if (b->timing) HIPCHK(hipEventRecord(b->ing_ev[1], hs));
+    HIPCHK(hipStreamSynchronize(hs));
+    if (b->timing) {
+        float ms1 = 0.0f;
+        HIPCHK(hipEventElapsedTime(&ms1, b->ing_ev[0], b->ing_ev[1]));
+        b->ipcm_ms += (double)ms0 + ms1;
+        b->ipcm_n++;
+    }
+    return SCROLL_OK;
+}
+
+int scroll_batch_ipcm_stats(ScrollBatch *b, double *ms, int *count)
+{
+    if (!b) return SCROLL_ERR_ARG;
+    if (ms) *ms = b->ipcm_ms;
+    if (count) *count = b->ipcm_n;
+    b->ipcm_ms = 0.0;
+    b->ipcm_n = 0;
     return SCROLL_OK;
 }
 

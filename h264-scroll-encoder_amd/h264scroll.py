@@ -183,6 +183,12 @@ def _load():
         "scroll_batch_ingest_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int,
                                                       ctypes.c_void_p, P(ctypes.c_uint64),
                                                       P(ctypes.c_int)]),
+        "scroll_batch_ipcm_files_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                                          ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t,
+                                                          ctypes.c_void_p, ctypes.c_size_t,
+                                                          P(ctypes.c_uint64)]),
+        "scroll_batch_ipcm_stats": (ctypes.c_int, [ctypes.c_void_p, P(ctypes.c_double),
+                                                   P(ctypes.c_int)]),
         "composer_batch_write_scroll_frames": (ctypes.c_int, [P(P(Composer)), P(ctypes.c_int),
                                                               ctypes.c_int, ctypes.c_int]),
         "composer_flush": (ctypes.c_int, [P(Composer)]),
@@ -420,6 +426,22 @@ class Batch:
         ms, n = ctypes.c_double(), ctypes.c_int()
         self._chk(lib.scroll_batch_ingest_stats(self.h, ctypes.byref(ms), ctypes.byref(n)),
                   "ingest_stats")
+        return ms.value, n.value
+
+    # ---- reference files from pictures ----
+    def ipcm_files_device(self, n, w, h, d_pics, pic_stride, d_out, out_stride):
+        """n I420 pictures (device) -> n SPS+PPS+I_PCM IDR files (device);
+        returns the file sizes"""
+        sizes = (ctypes.c_uint64 * max(1, n))()
+        self._chk(lib.scroll_batch_ipcm_files_device(self.h, n, w, h, ctypes.c_void_p(d_pics),
+                                                     pic_stride, ctypes.c_void_p(d_out),
+                                                     out_stride, sizes), "ipcm_files_device")
+        return [int(sizes[i]) for i in range(n)]
+
+    def ipcm_stats(self):
+        ms, n = ctypes.c_double(), ctypes.c_int()
+        self._chk(lib.scroll_batch_ipcm_stats(self.h, ctypes.byref(ms), ctypes.byref(n)),
+                  "ipcm_stats")
         return ms.value, n.value
 
     # ---- UI hints (SURVEY §8f row 1) ----

@@ -224,6 +224,25 @@ int scroll_batch_ingest_device(ScrollBatch *b, int n, const uint8_t *d_files,
  * batch's stream) and the number of ingest calls since the last call */
 int scroll_batch_ingest_stats(ScrollBatch *b, double *ms, int *count);
 
+/* ---- reference files from pictures on the GPU ----
+ * The experiment's I_PCM reference writer (experiments/scroll-encoder/src/
+ * h264_encoder.c:730-918: SPS + PPS + an IDR slice of I_PCM MBs, as the
+ * SURVEY Appendix B harness frames it) generalised from one stripe colour per
+ * MB to any I420 picture: n pictures at d_pics + i * pic_stride (Y w*h, then
+ * Cb, Cr w*h/4 each, device memory) become n Annex-B files at d_out + i *
+ * out_stride (device memory); sizes[i] (host) receives each file's bytes.
+ * The files are what scroll_batch_ingest_device reads, so new streams (or a
+ * new long-term reference picture) go from pixels to a composing stream
+ * without leaving the GPU.  Synchronous; SCROLL_ERR_OVERFLOW (the sizes are
+ * filled, nothing written) when a file exceeds out_stride -- at most
+ * 1.5 x (w*h*193/128) + 128 bytes.  w, h multiples of 16, < 65536 MBs. */
+int scroll_batch_ipcm_files_device(ScrollBatch *b, int n, int w, int h, const uint8_t *d_pics,
+                                   size_t pic_stride, uint8_t *d_out, size_t out_stride,
+                                   uint64_t *sizes);
+/* with timing enabled: summed kernel ms of the calls above since the last
+ * call (both passes) and the number of calls */
+int scroll_batch_ipcm_stats(ScrollBatch *b, double *ms, int *count);
+
 /* Composer-level batch: offsets[i] composed on cs[i], i < n, in
  * order; Composers may repeat.  Output lands in each Composer's buffer before
  * return (equivalent to n composer_write_scroll_frame calls + a flush). */

@@ -677,6 +677,45 @@ size_t or_ipcm_ref_file(uint8_t *dst, size_t cap, int w, int h, int which)
     return o;
 }
 
+/* An arbitrary I420 picture as one IDR of I_PCM MBs: the IDR header of
+ * or_ipcm_striped (h264_encoder.c:622-662) and h264_write_ipcm_mb (:730-753)
+ * with the picture's own samples in place of a stripe colour (raster order
+ * inside the MB: 256 luma, 64 Cb, 64 Cr). */
+size_t or_ipcm_picture_file(uint8_t *dst, size_t cap, int w, int h, const uint8_t *pic)
+{
+    or_cfg c;
+    or_cfg_init(&c, w, h);
+    size_t o = or_sps_pps(dst, cap, w, h);
+    const int mbw = w / 16, mbh = h / 16;
+    const uint8_t *Y = pic, *U = pic + (size_t)w * h, *V = U + (size_t)w * h / 4;
+    size_t rc = (size_t)mbw * (size_t)mbh * 400 + 1024;
+    uint8_t *rb = (uint8_t *)malloc(rc);
+    or_bits b;
+    or_bits_init(&b, rb, rc);
+    or_ue(&b, 0);
+    or_ue(&b, 7);
+    or_ue(&b, 0);
+    or_put(&b, 0, c.log2_mfn);
+    or_ue(&b, (uint32_t)c.idr_pic_id);
+    if (c.poc_type == 0) or_put(&b, 0, c.log2_poc);
+    or_put(&b, 0, 1);
+    or_put(&b, 1, 1);
+    or_se(&b, 0);
+    if (c.deblock) or_ue(&b, 1);
+    for (int my = 0; my < mbh; ++my)
+        for (int mx = 0; mx < mbw; ++mx) {
+            or_ue(&b, 25);
+            while (b.nbits & 7) or_put(&b, 0, 1);
+            for (int i = 0; i < 256; ++i) or_put(&b, Y[(size_t)(16 * my + i / 16) * w + 16 * mx + i % 16], 8);
+            for (int i = 0; i < 64; ++i) or_put(&b, U[(size_t)(8 * my + i / 8) * (w / 2) + 8 * mx + i % 8], 8);
+            for (int i = 0; i < 64; ++i) or_put(&b, V[(size_t)(8 * my + i / 8) * (w / 2) + 8 * mx + i % 8], 8);
+        }
+    or_trailing(&b);
+    o += or_nal(dst + o, cap - o, 3, 5, rb, or_bytes(&b));
+    free(rb);
+    return o;
+}
+
 /* ------------------------------------------------------------------------ */
 /* ingest: src/nal_parser.c:14-276                                           */
 /* ------------------------------------------------------------------------ */

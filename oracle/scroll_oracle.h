@@ -111,6 +111,12 @@ size_t or_ipcm_striped(uint8_t *dst, size_t cap, or_cfg *c, int which,
  * (SURVEY Appendix B).  which=0 -> colours of frame A, 1 -> frame B. */
 size_t or_ipcm_ref_file(uint8_t *dst, size_t cap, int w, int h, int which);
 
+/* The same file for an arbitrary I420 picture (Y w*h, Cb, Cr w*h/4 each):
+ * SPS + PPS + IDR whose I_PCM MBs carry the picture's samples
+ * (h264_encoder.c:730-753 generalised from one colour per MB).  For the
+ * striped pictures it equals or_ipcm_ref_file. */
+size_t or_ipcm_picture_file(uint8_t *dst, size_t cap, int w, int h, const uint8_t *pic);
+
 /* ---- ingest (src/nal_parser.c) ---- */
 size_t or_ebsp_to_rbsp(uint8_t *dst, const uint8_t *src, size_t n);   /* :67-88 */
 

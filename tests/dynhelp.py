@@ -94,3 +94,28 @@ def random_hints(rng, mbw, mbh, refs, nmax=6):
             out.append((x0, y0, x0 + rng.randint(1, mbw), y0 + rng.randint(1, mbh),
                         rng.choice(refs), rng.randint(-80, 80), rng.randint(-300, 300)))
     return out
+
+
+def striped_i420(w, h, which):
+    """The experiment's striped I_PCM picture (experiments/scroll-encoder/src/
+    main.c:234-243 colours, h264_encoder.c:816-829 bands) as I420 bytes."""
+    import numpy as np
+    cols = ([81, 90, 240, 145, 54, 34, 41, 240, 110], [210, 16, 146, 170, 166, 16, 106, 202, 222])[which]
+    third = (h // 16) // 3
+    band = np.where(np.arange(h // 16) < third, 0, np.where(np.arange(h // 16) < 2 * third, 1, 2))
+    yrow = np.repeat(band, 16)
+    crow = yrow[::2]
+    Y = np.repeat(np.array([cols[3 * b] for b in yrow], np.uint8)[:, None], w, 1)
+    U = np.repeat(np.array([cols[3 * b + 1] for b in crow], np.uint8)[:, None], w // 2, 1)
+    V = np.repeat(np.array([cols[3 * b + 2] for b in crow], np.uint8)[:, None], w // 2, 1)
+    return Y.tobytes() + U.tobytes() + V.tobytes()
+
+
+def ipcm_file(oracle, w, h, pic):
+    """oracle: SPS + PPS + I_PCM IDR of an I420 picture"""
+    import ctypes
+    cap = w * h * 3 + 4096
+    buf = (ctypes.c_uint8 * cap)()
+    src = (ctypes.c_uint8 * len(pic)).from_buffer_copy(pic)
+    n = oracle.or_ipcm_picture_file(buf, cap, w, h, src)
+    return bytes(buf[:n])

@@ -1,0 +1,158 @@
+"""GPU reference-file writer: scroll_batch_ipcm_files_device
+turns I420 pictures in HBM into SPS + PPS + I_PCM IDR files, byte for byte
+what the CPU restatement or_ipcm_picture_file writes (oracle/scroll_oracle.c;
+pinned to the reference's striped I_PCM files by tests/test_oracle_golden.py).
+Pictures vary what the kernels must handle: the reference's stripes, random
+samples, all-zero pictures (an emulation-prevention byte every third RBSP
+byte of each MB, zero runs longer than a workgroup's look-back), samples
+0..3 only, chunk edges at every size.  The files then feed
+scroll_batch_ingest_device and the composed streams are checked against the
+reference composer's restatement.  Run on an MI355X: -m gpu."""
+import ctypes
+import hashlib
+
+import numpy as np
+import pytest
+
+from dynhelp import ipcm_file, striped_i420
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def gpu(scroll):
+    if scroll.device_count() < 1:
+        pytest.fail("no gfx950 device: " + scroll.last_error())
+    return scroll
+
+
+def pictures(w, h, kinds, seed=7):
+    rng = np.random.default_rng(seed)
+    n = w * h * 3 // 2
+    out = []
+    for k in kinds:
+        if k == "a" or k == "b":
+            out.append(striped_i420(w, h, "ab".index(k)))
+        elif k == "rand":
+            out.append(rng.integers(0, 256, n, dtype=np.uint8).tobytes())
+        elif k == "zero":
+            out.append(bytes(n))
+        elif k == "low":
+            out.append(rng.integers(0, 4, n, dtype=np.uint8).tobytes())
+        elif k == "sparse":              # mostly zero with isolated small values
+            p = np.zeros(n, np.uint8)
+            idx = rng.integers(0, n, n // 50)
+            p[idx] = rng.integers(1, 4, idx.size, dtype=np.uint8)
+            out.append(p.tobytes())
+        else:
+            raise ValueError(k)
+    return out
+
+
+def gpu_files(gpu, torch, w, h, pics, out_stride=None, b=None):
+    n = len(pics)
+    psz = w * h * 3 // 2
+    stride = (psz + 255) // 256 * 256
+    dev = torch.zeros(n * stride, dtype=torch.uint8, device="cuda")
+    for i, p in enumerate(pics):
+        dev[i * stride:i * stride + psz] = torch.frombuffer(bytearray(p), dtype=torch.uint8).cuda()
+    if out_stride is None:
+        out_stride = (psz * 3 // 2 + psz + 4096 + 255) // 256 * 256
+    out = torch.full((n * out_stride,), 0xAB, dtype=torch.uint8, device="cuda")
+    own = b is None
+    if own:
+        b = gpu.Batch(1, 1, 1 << 20, device=0)
+    try:
+        sizes = b.ipcm_files_device(n, w, h, dev.data_ptr(), stride, out.data_ptr(), out_stride)
+        torch.cuda.synchronize()
+        host = out.cpu().numpy()
+        files = [host[i * out_stride:i * out_stride + sizes[i]].tobytes() for i in range(n)]
+        tails = [host[i * out_stride + sizes[i]:(i + 1) * out_stride] for i in range(n)]
+    finally:
+        if own:
+            b.close()
+    return files, tails
+
+
+@pytest.fixture(scope="module")
+def torch():
+    import torch as t
+    if not t.cuda.is_available():
+        pytest.fail("torch sees no GPU")
+    return t
+
+
+@pytest.mark.parametrize("w,h", [(64, 48), (1280, 720)])
+def test_striped_refs_match_reference(gpu, torch, oracle, golden_md5, w, h):
+    files, _ = gpu_files(gpu, torch, w, h, pictures(w, h, ["a", "b"]))
+    for which, f in enumerate(files):
+        g = golden_md5[f"ipcm_{w}x{h}_{'ab'[which]}.h264"]
+        assert len(f) == g["bytes"] and hashlib.md5(f).hexdigest() == g["md5"]
+
+
+@pytest.mark.parametrize("w,h", [(16, 16), (48, 32), (176, 144), (640, 480), (1280, 720)])
+def test_pictures_match_oracle(gpu, torch, oracle, w, h):
+    kinds = ["rand", "zero", "low", "sparse", "a"]
+    pics = pictures(w, h, kinds, seed=w + h)
+    files, tails = gpu_files(gpu, torch, w, h, pics)
+    for k, (p, f, t) in enumerate(zip(pics, files, tails)):
+        want = ipcm_file(oracle, w, h, p)
+        assert f == want, f"{kinds[k]} {w}x{h}: {len(f)} vs {len(want)} bytes"
+        assert (t == 0xAB).all(), "bytes written past the file"
+
+
+def test_4k_pictures(gpu, torch, oracle, golden_md5):
+    w, h = 3840, 2160
+    pics = pictures(w, h, ["a", "zero"])
+    files, _ = gpu_files(gpu, torch, w, h, pics)
+    g = golden_md5["ipcm_3840x2160_a.h264"]
+    assert len(files[0]) == g["bytes"] and hashlib.md5(files[0]).hexdigest() == g["md5"]
+    assert files[1] == ipcm_file(oracle, w, h, pics[1])
+
+
+def test_overflow_reports_sizes(gpu, torch, oracle):
+    w, h = 64, 48
+    pics = pictures(w, h, ["zero"])
+    want = ipcm_file(oracle, w, h, pics[0])
+    b = gpu.Batch(1, 1, 1 << 20, device=0)
+    try:
+        with pytest.raises(RuntimeError):
+            gpu_files(gpu, torch, w, h, pics, out_stride=len(want) - 1, b=b)
+        files, _ = gpu_files(gpu, torch, w, h, pics, out_stride=len(want), b=b)
+        assert files[0] == want
+    finally:
+        b.close()
+
+
+def test_files_feed_ingest_and_compose(gpu, torch, oracle):
+    """pixels -> reference files -> new streams -> scroll frames without
+    leaving the GPU (scroll_batch_ingest_device on the files in place);
+    equal to the reference composer's restatement run on the oracle's files"""
+    w, h, nfr, speed = 176, 144, 30, 4
+    pics = pictures(w, h, ["rand", "sparse", "a", "b"], seed=3)
+    psz = w * h * 3 // 2
+    stride = (psz + 255) // 256 * 256
+    dev = torch.zeros(4 * stride, dtype=torch.uint8, device="cuda")
+    for i, p in enumerate(pics):
+        dev[i * stride:i * stride + psz] = torch.frombuffer(bytearray(p), dtype=torch.uint8).cuda()
+    ostride = 2 * stride + 4096
+    out = torch.zeros(4 * ostride, dtype=torch.uint8, device="cuda")
+    b = gpu.Batch(2, nfr, 4 << 20, device=0)
+    try:
+        sizes = b.ipcm_files_device(4, w, h, dev.data_ptr(), stride, out.data_ptr(), ostride)
+        desc = []
+        for k in range(2):
+            desc += [2 * k * ostride, sizes[2 * k], (2 * k + 1) * ostride, sizes[2 * k + 1]]
+        assert b.ingest_device(2, out.data_ptr(), desc) == 0
+        offs = np.array([[oracle.or_tri(i * speed, h) for i in range(nfr)] for _ in range(2)], np.int32)
+        b.set_offsets(offs)
+        b.compose(nfr)
+        assert b.sync() == 0, gpu.last_error()
+        for k in range(2):
+            a_, b_ = ipcm_file(oracle, w, h, pics[2 * k]), ipcm_file(oracle, w, h, pics[2 * k + 1])
+            cap = 2 * (len(a_) + len(b_)) + 65536
+            buf = (ctypes.c_uint8 * cap)()
+            n = oracle.or_composer_run(buf, cap, a_, len(a_), b_, len(b_), nfr, speed)
+            assert n and b.output(k) == bytes(buf[:n])
+    finally:
+        b.close()

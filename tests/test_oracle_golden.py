@@ -128,3 +128,15 @@ def test_median3_quirk_and_bench_smoke(oracle):
     b = ctypes.c_ulonglong()
     fps = oracle.or_bench_compose(4, 20, 1280, 720, 2, 2, ctypes.byref(b))
     assert fps > 0 and b.value > 4 * 20 * 2000
+
+
+@pytest.mark.parametrize("w,h", [(64, 48), (1280, 720)])
+@pytest.mark.parametrize("which", [0, 1])
+def test_ipcm_picture_file_pinned(oracle, golden_md5, w, h, which):
+    """or_ipcm_picture_file (any I420 picture, the GPU reference-file
+    writer's checker) reproduces the reference's striped I_PCM files when
+    given the striped pictures"""
+    from dynhelp import ipcm_file, striped_i420
+    got = ipcm_file(oracle, w, h, striped_i420(w, h, which))
+    g = golden_md5[f"ipcm_{w}x{h}_{'ab'[which]}.h264"]
+    assert len(got) == g["bytes"] and hashlib.md5(got).hexdigest() == g["md5"]

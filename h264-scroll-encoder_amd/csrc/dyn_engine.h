@@ -16,16 +16,18 @@ typedef struct {
     uint32_t *rows;
     uint32_t *meta;
     uint4 *body;
+    uint32_t *rowst;                /* k_dyn_len -> k_dyn_write: MB-row bit offsets */
+    int ld_row;                     /* picture MB rows + 1 */
 } DynScratch;
 
 /* k_dyn_rows + k_dyn_code (both instantiations): block records */
 int dyn_launch_code(hipStream_t hs, int nframes, int S, const DevStream *st, const NalDesc *nal,
                     int ld_nal, const PlanPending *pend, DynFrame *dfr, int ld_fr,
                     const DynGeom *g, const uint8_t *src, const uint8_t *refs, const DynScratch *x);
-/* k_dyn_pack: records -> staged RBSP + EP positions */
+/* k_dyn_len + k_dyn_write + k_dyn_ep: records -> staged RBSP + EP positions */
 int dyn_launch_pack(hipStream_t hs, int nframes, int S, DevStream *st, const NalDesc *nal,
                     int ld_nal, const PlanPending *pend, DynFrame *dfr, int ld_fr,
-                    const DynGeom *g, const DynScratch *x, uint8_t *stage, uint64_t *stamps);
+                    const DynGeom *g, const DynScratch *x, uint8_t *stage);
 int dyn_launch_emit(hipStream_t hs, int nframes, int S, const DevStream *st, const NalDesc *nal,
                     int ld_nal, const DynFrame *dfr, int ld_fr, const DynGeom *g,
                     const uint8_t *stage, uint8_t *arena, uint64_t ld_arena, uint64_t *stamps);

@@ -385,39 +385,6 @@ __global__ __launch_bounds__(CODE_T) void k_dyn_code(const DevStream *__restrict
     }
 }
 
-/* ---------------------------------------------------------------------- */
-/* k_dyn_pack                                                              */
-/* ---------------------------------------------------------------------- */
-/* One workgroup of PACK_T threads per dynamic NAL walks its MBs in coding
- * order in windows [m0, m1) of nm MBs, nd of them dynamic, with
- * nm + 26 nd <= PACK_T: thread u < nm is the head of MB m0 + u, thread
- * nm + 26 k + pc is piece pc of the window's dynamic MB k.  Three barriers
- * per window:
- *   P1  previous window's whole words -> staging (+ EP positions); pieces:
- *       nC from the neighbours' TotalCoeff (records), coeff_token, length
- *   P2  buffer rewind; heads: cbp, piece offsets, MB length; scan
- *   P3  every head and piece ORed into the LDS bit buffer at its offset */
-constexpr int PACK_T = 1024, PNW = PACK_T / 64;
-constexpr int PK_MB = PACK_T / (NPC + 1);          /* dynamic MBs per window, at most */
-constexpr int PBUF_WORDS = 4096;                   /* 128 Kbit; larger windows take passes */
-static_assert(PBUF_WORDS * 32 > HDR_MAX + 64, "the slice header fits one buffer");
-
-struct PackLds {
-    uint32_t buf[PBUF_WORDS];
-    alignas(16) uint8_t tc[PK_MB][32];
-    alignas(16) uint16_t blen[PK_MB][32];
-    alignas(16) uint16_t boff[PK_MB][32];
-    uint32_t exw[PACK_T];
-    uint32_t wsum[PNW];
-    int32_t wo[8], wl[8], wv[8];
-    int32_t lnz_r, lnz_w;
-    uint32_t ep_n;
-    uint64_t hhi[12], hlo[12];
-    uint32_t hlen[12];
-    int32_t head_over;
-    PTabs ptabs;
-};
-
 struct LdsOrWin {
     uint32_t *b;
     uint32_t lo, n;
@@ -429,79 +396,44 @@ struct LdsOrWin {
 };
 typedef OrSink<LdsOrWin> WSink;
 
-__device__ inline uint32_t pack_wave_pre(const uint32_t *ws, int wave)
-{
-    uint32_t pre = 0;
-#pragma unroll
-    for (int w2 = 0; w2 < PNW; ++w2) pre += w2 < wave ? ws[w2] : 0u;
-    return pre;
-}
+/* ---------------------------------------------------------------------- */
+/* k_dyn_len / k_dyn_write / k_dyn_ep: records -> staged RBSP               */
+/* ---------------------------------------------------------------------- */
+/* A NAL's bits are: slice header, then per MB row the MB heads (one of 12
+ * codeword classes) and, for dynamic MBs, coded_block_pattern,
+ * mb_qp_delta and the present pieces (coeff_token from the neighbours'
+ * TotalCoeff + the body k_dyn_code left in the records), then the stop bit.
+ *   k_dyn_len    per NAL: every MB row's length -> row bit offsets; writes
+ *                the header words, the stop word, and zeroes every staging
+ *                word two rows share
+ *   k_dyn_write  per MB row (all rows of all NALs at once): MB offsets by a
+ *                block scan, heads and pieces ORed into an LDS line of the
+ *                row, whole words stored, the two shared words atomically ORed
+ *   k_dyn_ep     per NAL: emulation-prevention positions + count from the
+ *                staged bytes (closed form of nal.c:33-38, ep_insert) */
+constexpr int WR_T = 256;
+constexpr int WBUF_WORDS = 2048;        /* 64 Kbit per pass; a config-3 row is ~19 Kbit */
+constexpr int MAX_MBW = DYN_MAX_MBW, MAX_MBH = DYN_MAX_MBH;
+constexpr int WR_ROWS = 3;              /* MB rows per k_dyn_write workgroup */
+constexpr int PL_LEN = 0x7ff;           /* piece length bits of a pl entry; nC + 1 above */
+constexpr uint32_t TK_OVF = 1u << 31;
 
-__global__ __launch_bounds__(PACK_T, 8) void k_dyn_pack(DevStream *__restrict__ st,
-                                                     const NalDesc *__restrict__ nal, int ld_nal,
-                                                     const PlanPending *__restrict__ pend,
-                                                     DynFrame *__restrict__ dfr, int ld_fr, DynGeom g,
-                                                     const uint32_t *__restrict__ meta,
-                                                     const uint4 *__restrict__ body,
-                                                     uint8_t *__restrict__ stage, uint64_t *__restrict__ stamps)
-{
-    __shared__ PackLds L;
-    uint64_t ph[5] = {0, 0, 0, 0, 0}, t_start = 0, t_last = 0, nwin = 0;
-    auto mark = [&](int k) {
-        if (stamps) {
-            const uint64_t now = __builtin_amdgcn_s_memtime();
-            ph[k] += now - t_last;
-            t_last = now;
-        }
-    };
-    if (stamps) t_start = t_last = __builtin_amdgcn_s_memtime();
-    const int s = blockIdx.y, f = dyn_frame_of(blockIdx.x, s), t = threadIdx.x;
-    const int lane = t & 63, wave = t >> 6;
-    DevStream *S = st + s;
-    DynFrame *DF = dfr + (size_t)s * ld_fr + f;
-    const int j = DF->nal;
-    if (j < 0) return;
+__device__ inline int tc_of(uint32_t m) { return (int)((m >> 8) & 31u); }
 
-    const Rect R{g.x0, g.y0, g.w, g.h};
-    if (t == 0) {
-        L.lnz_r = -1;
-        L.lnz_w = -1;
-        L.head_over = 0;
-        L.ep_n = 0;
-    }
-    if (t < 8) {
-        L.wo[t] = pend[s].wo[t];
-        L.wl[t] = pend[s].wl[t];
-        L.wv[t] = pend[s].wv[t];
-    }
-    for (int i = t; i < PBUF_WORDS; i += PACK_T) L.buf[i] = 0u;
-    build_ptabs(*reinterpret_cast<const Tabs *>(&g_tabs), L.ptabs, t, PACK_T);
-    const NalDesc d = nal[(size_t)s * ld_nal + j];
-    const NalCtx c = nal_ctx(S, d, L.wo, L.wl, L.wv);
-    __syncthreads();
-
-    /* slice header (h264_writer.c:549-553): thread 0 writes, all count */
-    uint32_t F;
+/* the head codeword classes of a NAL (3 row types x first / middle / last) */
+struct HeadCtx {
+    Regions rg;
+    int a_end, mbw, nrefs;
+    __device__ inline int sel(int row, int col) const
     {
-        CountSink hc{0};
-        emit_slice_header(hc, c);
-        F = hc.n;
-        if (t == 0) {
-            LSink hs{{L.buf}, 0, 0, 0};
-            hs.start(0);
-            emit_slice_header(hs, c);
-            hs.finish();
-        }
+        const bool curA = row < a_end, abvA = (row - 1) < a_end;
+        return 3 * (row == 0 ? 0 : (curA ? 1 : (abvA ? 2 : 3))) + (col == 0 ? 0 : (col == mbw - 1 ? 2 : 1));
     }
-    const int w = c.w, h = c.h, mbw = w / 16, mbh = h / 16;
-    const Regions rg = regions(c);
-    const int a_end = (h - c.off) / 16;
-    const int nrefs = 2 + c.nwp;
-    /* MB head codewords (mb_skip_run .. mvd, h264_writer.c:434-453): they
-     * depend only on the row type -- row 0, steady A, A->B boundary, steady
-     * B -- and on first / middle / last position */
-    if (t < 12) {
-        const int ty = t / 3, pos = t - 3 * ty;
+    /* head of class cls (h264_writer.c:434-453 after the row-uniform predictor) */
+    template <class S>
+    __device__ inline void put_class(S &sk, int cls) const
+    {
+        const int ty = cls / 3, pos = cls - 3 * ty;
         const int x = pos == 0 ? 0 : (pos == 1 ? min(1, mbw - 1) : mbw - 1);
         const bool cur = ty == 0 ? 0 < a_end : ty == 1;
         const bool abv = ty == 1 || ty == 2;
@@ -509,274 +441,427 @@ __global__ __launch_bounds__(PACK_T, 8) void k_dyn_pack(DevStream *__restrict__ 
         const int aref = abv ? rg.ra : rg.rb, amv4 = 4 * (abv ? rg.mva : rg.mvb);
         int px, py;
         predict(x, ty == 0 ? 0 : 1, mbw, ref, mv4, aref, amv4, px, py);
-        CapSink hc{0, 0, 0};
-        put_mb_head(hc, ref, 0 - px, mv4 - py, nrefs);
-        L.hhi[t] = hc.hi;
-        L.hlo[t] = hc.lo;
-        L.hlen[t] = hc.n;
-        if (hc.over()) L.head_over = 1;
+        put_mb_head(sk, ref, 0 - px, mv4 - py, nrefs);
     }
-    __syncthreads();
-    const bool head_over = L.head_over;           /* uniform */
-    const uint32_t m_mbw = magic32((uint32_t)mbw), m_rw = magic32((uint32_t)R.w), m_pc = magic32(NPC);
-    const size_t nb = (size_t)s * ld_fr + f;
-    const int ndt = R.w * R.h;
-    const uint32_t *M = meta + nb * (size_t)(NPC * ndt);
-    const uint4 *Bd = body + nb * (size_t)(NPC * ndt);
-    uint8_t *slot = stage + nb * g.slot_bytes;
-    uint32_t *out = reinterpret_cast<uint32_t *>(slot);
-    const uint32_t cap_words = (uint32_t)((g.slot_bytes - DYN_OVF_BYTES) / 4) - 4u;
-    uint32_t *eplist = reinterpret_cast<uint32_t *>(slot + g.slot_bytes - DYN_OVF_BYTES);
-    const Tabs &TB = g_tabs;
-    const PTabs &PT = L.ptabs;
-
-    uint32_t bw = 0;             /* staging word of buf[0]                        */
-    uint32_t my_ep = 0;
-    bool over = false;
-    uint32_t pend_T = 0;         /* bits in buf awaiting the deferred flush (0: none) */
-
-    /* whole words buf[0, n) -> staging words [gw0, gw0 + n), EP insertions
-     * with the zero run looked up backwards in buf (L.lnz_r before buf[0]);
-     * the last non-zero byte goes to L.lnz_w */
-    auto flush_words = [&](uint32_t n, uint32_t gw0) {
-        for (uint32_t jw = (uint32_t)t; jw < n; jw += PACK_T) {
-            const uint32_t wv = L.buf[jw];
-            out[gw0 + jw] = __builtin_bswap32(wv);
-            int prev = L.lnz_r;
-            for (int jj = (int)jw - 1; jj >= 0; --jj) {
-                const uint32_t pv = L.buf[jj];
-                if (pv) {
-                    prev = 4 * (int)(gw0 + jj) + last_nz_byte(pv);
-                    break;
-                }
-            }
-            const uint32_t gb = 4u * (gw0 + jw);
-            my_ep += ep_word(wv, gb, 0xffffffffu, prev, eplist, &L.ep_n);
-            if (wv) atomicMax(&L.lnz_w, (int)gb + last_nz_byte(wv));
-        }
-    };
-    auto rewind_lnz = [&]() {
-        if (t == 0) {
-            L.lnz_r = max(L.lnz_r, L.lnz_w);
-            L.lnz_w = -1;
-        }
-    };
-    /* MB m's head codeword class */
-    auto head_sel = [&](int row, int col) {
-        const bool curA = row < a_end, abvA = (row - 1) < a_end;
-        return 3 * (row == 0 ? 0 : (curA ? 1 : (abvA ? 2 : 3))) + (col == 0 ? 0 : (col == mbw - 1 ? 2 : 1));
-    };
-    auto put_head_slow = [&](auto &sk, int row, int col) {       /* > 128-bit heads */
+    /* the same for MB (row, col) directly (heads over 128 bits) */
+    template <class S>
+    __device__ inline void put_slow(S &sk, int row, int col) const
+    {
         const bool curA = row < a_end, abvA = (row - 1) < a_end;
         const int ref = curA ? rg.ra : rg.rb, mv4 = 4 * (curA ? rg.mva : rg.mvb);
         const int aref = abvA ? rg.ra : rg.rb, amv4 = 4 * (abvA ? rg.mva : rg.mvb);
         int px, py;
         predict(col, row, mbw, ref, mv4, aref, amv4, px, py);
         put_mb_head(sk, ref, 0 - px, mv4 - py, nrefs);
+    }
+};
+
+__device__ inline HeadCtx head_ctx(const NalCtx &c)
+{
+    HeadCtx H;
+    H.rg = regions(c);
+    H.a_end = (c.h - c.off) / 16;
+    H.mbw = c.w / 16;
+    H.nrefs = 2 + c.nwp;
+    return H;
+}
+
+/* Layout of dynamic MB q at frame MB (row, col): per piece pc the length
+ * with its coeff_token (pl[pc] = len | (nC + 1) << 11) and, when tk, the
+ * token (tk[pc] = bits | len << 16 | nC + 1 << 21 | TK_OVF) and the offset
+ * from the MB start (po[pc], 0xffff: not coded).  hb = head bits.  Returns
+ * the MB's bits; cbp and its me(v) code number out.  pl / tk / po: LDS. */
+template <bool TOK>
+__device__ inline uint32_t dyn_mb_layout(const uint32_t *__restrict__ M, const uint4 *__restrict__ Bd,
+                                         const Rect &R, int q, int row, int col, const PTabs &PT,
+                                         const Tabs &TB, uint16_t *pl, uint32_t *tk, uint16_t *po,
+                                         uint32_t hb, int &cbp_o, int &code_o)
+{
+    const int ry = row - R.y0, cx = col - R.x0;
+    const uint32_t *Mq = M + (size_t)q * NPC;
+    const uint32_t *ML = Mq - NPC, *MT = Mq - (size_t)NPC * R.w;
+    uint32_t m[NPC];
+#pragma unroll
+    for (int i = 0; i < NPC / 2; ++i) {
+        const uint2 v = *reinterpret_cast<const uint2 *>(Mq + 2 * i);
+        m[2 * i] = v.x;
+        m[2 * i + 1] = v.y;
+    }
+    const int nAe = col > 0 ? 0 : -1, nBe = row > 0 ? 0 : -1;     /* a neighbour outside the rect */
+    uint32_t ovf = 0;
+    int cbp_l = 0;
+    bool dc = false, ac = false;
+#pragma unroll
+    for (int pc = 0; pc < NPC; ++pc) {
+        const uint32_t mv = m[pc];
+        const int tc = tc_of(mv);
+        uint32_t tl = 0, tv = 0;
+        int nC = -1;
+        if (pc == 16 || pc == 17) {
+            dc |= tc != 0;
+        } else {
+            int nA, nB;
+            if (pc < 16) {
+                const int bx = pc & 3, by = pc >> 2;
+                nA = bx > 0 ? tc_of(m[pc - 1]) : (cx > 0 ? tc_of(ML[pc + 3]) : nAe);
+                nB = by > 0 ? tc_of(m[pc - 4]) : (ry > 0 ? tc_of(MT[pc + 12]) : nBe);
+                if (tc) cbp_l |= 1 << (2 * (by >> 1) + (bx >> 1));
+            } else {
+                const int b = (pc - 18) & 3, bx = b & 1, by = b >> 1;
+                nA = bx > 0 ? tc_of(m[pc - 1]) : (cx > 0 ? tc_of(ML[pc + 1]) : nAe);
+                nB = by > 0 ? tc_of(m[pc - 2]) : (ry > 0 ? tc_of(MT[pc + 2]) : nBe);
+                ac |= tc != 0;
+            }
+            nC = nc_of(nA, nB);
+            const int t1 = (int)((mv >> 13) & 3u);
+            if (nC >= 8) {
+                tv = tc ? (uint32_t)(((tc - 1) << 2) | t1) : 3u;
+                tl = 6;
+            } else {
+                const uint32_t e = PT.ct[nC < 2 ? 0 : (nC < 4 ? 1 : 2)][4 * tc + t1];
+                tv = e & 255u;
+                tl = e >> 8;
+            }
+        }
+        pl[pc] = (uint16_t)((tl + (mv & 255u)) | (uint32_t)(nC + 1) << 11);
+        if (TOK) tk[pc] = tv | tl << 16 | (uint32_t)(nC + 1) << 21 | (mv & M_OVF ? TK_OVF : 0u);
+        if (mv & M_OVF) ovf |= 1u << pc;
+    }
+    while (ovf) {                       /* rare: > 128-bit block, measure from the levels */
+        const int pc = __builtin_ctz(ovf);
+        ovf &= ovf - 1u;
+        const uint4 bd = Bd[(size_t)q * NPC + pc];
+        CountSink cn{0};
+        const uint32_t e = pl[pc];
+        if (pc == 16 || pc == 17) {
+            const int dq[4] = {(int)(int16_t)(bd.x & 0xffffu), (int)(int16_t)(bd.x >> 16),
+                               (int)(int16_t)(bd.y & 0xffffu), (int)(int16_t)(bd.y >> 16)};
+            cavlc_dc4(cn, PT, dq);
+        } else {
+            const int8_t *lvp = reinterpret_cast<const int8_t *>(&bd);
+            cavlc_block(cn, TB, lvp, pc < 16 ? 16 : 15, (int)(e >> 11) - 1);
+        }
+        pl[pc] = (uint16_t)(cn.n | (e & ~(uint32_t)PL_LEN));
+    }
+    const int cbp_c = ac ? 2 : (dc ? 1 : 0);
+    const int cbp = cbp_l | cbp_c << 4;
+    const int code = TB.cbp_code[cbp];
+    CountSink hs{hb};
+    put_ue(hs, (uint32_t)code);
+    if (cbp) put_se(hs, 0);                                 /* mb_qp_delta */
+    uint32_t off = hs.n;
+#pragma unroll
+    for (int blk = 0; blk < 16; ++blk) {                    /* luma4x4BlkIdx order */
+        const int r = blk_raster(blk);
+        const bool pres = (cbp_l >> (blk >> 2)) & 1;
+        if (TOK) po[r] = pres ? (uint16_t)off : (uint16_t)0xffffu;
+        off += pres ? (uint32_t)(pl[r] & PL_LEN) : 0u;
+    }
+#pragma unroll
+    for (int k2 = 16; k2 < NPC; ++k2) {                     /* Cb DC, Cr DC, Cb AC 0-3, Cr AC 0-3 */
+        const bool pres = k2 < 18 ? cbp_c >= 1 : cbp_c == 2;
+        if (TOK) po[k2] = pres ? (uint16_t)off : (uint16_t)0xffffu;
+        off += pres ? (uint32_t)(pl[k2] & PL_LEN) : 0u;
+    }
+    cbp_o = cbp;
+    code_o = code;
+    return off;
+}
+
+/* bits of the non-dynamic MBs of one row: (head + coded_block_pattern ue(0))
+ * per MB, by class counts (first / middle / last column) */
+__device__ inline uint32_t row_static_bits(const HeadCtx &H, const uint32_t *hlen, int row, const Rect &R)
+{
+    const int mbw = H.mbw;
+    const bool in = row >= R.y0 && row < R.y0 + R.h;
+    auto isdyn = [&](int col) { return in && col >= R.x0 && col < R.x0 + R.w; };
+    const int base = H.sel(row, 0) - 0;                     /* class of column 0 */
+    uint32_t bits = isdyn(0) ? 0u : hlen[base] + 1u;
+    if (mbw >= 2) {
+        if (!isdyn(mbw - 1)) bits += hlen[base + 2] + 1u;
+        int nmid = mbw - 2;
+        if (in) nmid -= max(0, min(R.x0 + R.w, mbw - 1) - max(R.x0, 1));
+        bits += (uint32_t)nmid * (hlen[base + 1] + 1u);
+    }
+    return bits;
+}
+
+struct LenLds {
+    uint16_t pl[WR_T][NPC];
+    uint32_t rowbits[MAX_MBH];
+    uint32_t hdr[HDR_MAX / 32 + 2];
+    uint32_t wsum[NW];
+    uint32_t hlen[12];
+    int32_t head_over;
+    int32_t wo[8], wl[8], wv[8];
+    PTabs ptabs;
+};
+
+/* grid (frames, streams), WR_T threads per NAL */
+__global__ __launch_bounds__(WR_T) void k_dyn_len(DevStream *__restrict__ st, const NalDesc *__restrict__ nal,
+                                                  int ld_nal, const PlanPending *__restrict__ pend,
+                                                  DynFrame *__restrict__ dfr, int ld_fr, DynGeom g,
+                                                  const uint32_t *__restrict__ meta,
+                                                  const uint4 *__restrict__ body, uint32_t *__restrict__ rowst,
+                                                  int ld_row, uint8_t *__restrict__ stage)
+{
+    __shared__ LenLds L;
+    const int s = blockIdx.y, f = blockIdx.x, t = threadIdx.x;
+    DevStream *S = st + s;
+    DynFrame *DF = dfr + (size_t)s * ld_fr + f;
+    const int j = DF->nal;
+    if (j < 0) return;
+    if (t < 8) {
+        L.wo[t] = pend[s].wo[t];
+        L.wl[t] = pend[s].wl[t];
+        L.wv[t] = pend[s].wv[t];
+    }
+    for (int i = t; i < HDR_MAX / 32 + 2; i += WR_T) L.hdr[i] = 0u;
+    if (t == 0) L.head_over = 0;
+    build_ptabs(*reinterpret_cast<const Tabs *>(&g_tabs), L.ptabs, t, WR_T);
+    const NalDesc d = nal[(size_t)s * ld_nal + j];
+    const NalCtx c = nal_ctx(S, d, L.wo, L.wl, L.wv);
+    __syncthreads();
+    uint32_t F;
+    {
+        CountSink hc{0};
+        emit_slice_header(hc, c);
+        F = hc.n;
+        if (t == 0) {
+            LSink hs{{L.hdr}, 0, 0, 0};
+            hs.start(0);
+            emit_slice_header(hs, c);
+            hs.finish();
+        }
+    }
+    const HeadCtx H = head_ctx(c);
+    if (t < 12) {
+        CapSink hc{0, 0, 0};
+        H.put_class(hc, t);
+        L.hlen[t] = hc.n;
+        if (hc.over()) L.head_over = 1;
+    }
+    __syncthreads();
+    const bool head_over = L.head_over;
+    const int mbw = H.mbw, mbh = c.h / 16;
+    const Rect R{g.x0, g.y0, g.w, g.h};
+    for (int r = t; r < mbh; r += WR_T) {
+        uint32_t b;
+        if (!head_over) {
+            b = row_static_bits(H, L.hlen, r, R);
+        } else {
+            b = 0;
+            for (int col = 0; col < mbw; ++col) {
+                if (r >= R.y0 && r < R.y0 + R.h && col >= R.x0 && col < R.x0 + R.w) continue;
+                CountSink cn{1};
+                H.put_slow(cn, r, col);
+                b += cn.n;
+            }
+        }
+        L.rowbits[r] = b;
+    }
+    __syncthreads();
+    const size_t nb = (size_t)s * ld_fr + f;
+    const int ndt = R.w * R.h;
+    const uint32_t *M = meta + nb * (size_t)(NPC * ndt);
+    const uint4 *Bd = body + nb * (size_t)(NPC * ndt);
+    const uint32_t m_rw = magic32((uint32_t)R.w);
+    const Tabs &TB = g_tabs;
+    for (int q = t; q < ndt; q += WR_T) {
+        const int ry = (int)div_m((uint32_t)q, m_rw), cx = q - ry * R.w;
+        const int row = R.y0 + ry, col = R.x0 + cx;
+        uint32_t hb;
+        if (!head_over) {
+            hb = L.hlen[H.sel(row, col)];
+        } else {
+            CountSink cn{0};
+            H.put_slow(cn, row, col);
+            hb = cn.n;
+        }
+        int cbp, code;
+        const uint32_t bits = dyn_mb_layout<false>(M, Bd, R, q, row, col, L.ptabs, TB, L.pl[t], nullptr,
+                                                   nullptr, hb, cbp, code);
+        atomicAdd(&L.rowbits[row], bits);
+    }
+    __syncthreads();
+    uint32_t *RS = rowst + nb * (size_t)ld_row;
+    uint32_t carry = F;
+    for (int r0 = 0; r0 < mbh; r0 += WR_T) {
+        const int r = r0 + t;
+        const uint32_t v = r < mbh ? L.rowbits[r] : 0u;
+        uint32_t ex, tot;
+        block_excl_sum(v, L.wsum, ex, tot);
+        if (r < mbh) {
+            RS[r] = carry + ex;
+            L.rowbits[r] = carry + ex;                      /* own entry: start of row r */
+        }
+        carry += tot;
+    }
+    const uint32_t end = carry;                             /* bit of rbsp_stop_one_bit */
+    uint8_t *slot = stage + nb * g.slot_bytes;
+    uint32_t *out = reinterpret_cast<uint32_t *>(slot);
+    const uint32_t cap_words = (uint32_t)((g.slot_bytes - DYN_OVF_BYTES) / 4) - 4u;
+    const bool over = (end >> 5) + 2u > cap_words;          /* uniform */
+    if (t == 0) {
+        RS[mbh] = end;
+        DF->ep = 0;
+        DF->err = over ? DF_OVER : 0u;
+        DF->rbsp_bytes = over ? 0u : (end + 8u) >> 3;       /* bitwriter.c:103-111 */
+        if (over) atomicOr((unsigned int *)&S->err, SCROLL_DEVERR_DYN);
+    }
+    if (over) return;
+    /* words the writers OR into: header words (with the header), words two
+     * rows share (zero), the stop word (with the stop bit) */
+    const uint32_t hw = (F + 31u) >> 5, ew = end >> 5;
+    auto val = [&](uint32_t w) -> uint32_t {
+        return (w < hw ? L.hdr[w] : 0u) | (w == ew ? 0x80000000u >> (end & 31u) : 0u);
     };
+    for (uint32_t w = (uint32_t)t; w < hw; w += WR_T) out[w] = __builtin_bswap32(val(w));
+    for (int r = t; r < mbh; r += WR_T) {
+        const uint32_t rs = L.rowbits[r];
+        if (r > 0 && (rs & 31u) && (rs >> 5) >= hw) out[rs >> 5] = __builtin_bswap32(val(rs >> 5));
+    }
+    if (t == 0 && ew >= hw) out[ew] = __builtin_bswap32(val(ew));
+}
 
-    const int nmb = mbw * mbh;
-    for (int m0 = 0; m0 < nmb;) {
-        const int q0 = dyn_rank_m(R, mbw, m_mbw, m0);
-        /* largest m1 with (m1 - m0) + 26 (rank(m1) - q0) <= PACK_T */
-        int lo = m0 + 1, hi = min(nmb, m0 + PACK_T);
-        while (lo < hi) {
-            const int mid = (lo + hi + 1) >> 1;
-            if ((mid - m0) + NPC * (dyn_rank_m(R, mbw, m_mbw, mid) - q0) <= PACK_T) lo = mid;
-            else hi = mid - 1;
-        }
-        const int m1 = lo, nm = m1 - m0, nd = dyn_rank_m(R, mbw, m_mbw, m1) - q0;
-        nwin++;
+struct WrLds {
+    uint32_t buf[WBUF_WORDS];
+    uint32_t tk[DYN_MAX_W][NPC];
+    uint16_t pl[DYN_MAX_W][NPC];
+    uint16_t po[DYN_MAX_W][NPC];
+    uint32_t moff[MAX_MBW];
+    uint32_t mbits[DYN_MAX_W];
+    uint8_t cbp[DYN_MAX_W], code[DYN_MAX_W];
+    uint32_t wsum[NW];
+    uint64_t hhi[3], hlo[3];
+    uint32_t hlen[3];
+    int32_t head_over;
+    int32_t wo[8], wl[8], wv[8];
+    PTabs ptabs;
+};
 
-        /* P1: flush of the previous window; pieces: token and length */
-        const uint32_t pnf = pend_T >> 5;
-        uint32_t part = 0;
-        if (pend_T) {
-            flush_words(pnf, bw);
-            part = L.buf[pnf];
-        }
-        const int pi = t - nm;
-        const bool is_piece = pi >= 0 && pi < NPC * nd;
-        int kd = 0, pc = 0;
-        uint32_t tv = 0, tl = 0, mv = 0;
-        int nC = 0;
-        uint4 bd = make_uint4(0, 0, 0, 0);
-        if (is_piece) {
-            kd = (int)div_m((uint32_t)pi, m_pc);
-            pc = pi - kd * NPC;
-            const int q = q0 + kd;
-            const int ry = (int)div_m((uint32_t)q, m_rw), cx = q - ry * R.w;
-            const int row = R.y0 + ry, col = R.x0 + cx;
-            const uint32_t *Mq = M + (size_t)q * NPC;
-            mv = Mq[pc];
-            const int tc = (int)((mv >> 8) & 31u), t1 = (int)((mv >> 13) & 3u);
-            uint32_t len;
-            if (pc == 16 || pc == 17) {
-                nC = -1;
-                len = mv & 255u;
-            } else {
-                int nA, nB;
-                if (pc < 16) {
-                    const int bx = pc & 3, by = pc >> 2;
-                    nA = bx > 0 ? (int)((Mq[pc - 1] >> 8) & 31u)
-                                : (cx > 0 ? (int)((Mq[pc + 3 - NPC] >> 8) & 31u) : (col > 0 ? 0 : -1));
-                    nB = by > 0 ? (int)((Mq[pc - 4] >> 8) & 31u)
-                                : (ry > 0 ? (int)((Mq[pc + 12 - NPC * R.w] >> 8) & 31u)
-                                          : (row > 0 ? 0 : -1));
-                } else {
-                    const int b = (pc - 18) & 3, bx = b & 1, by = b >> 1;
-                    nA = bx > 0 ? (int)((Mq[pc - 1] >> 8) & 31u)
-                                : (cx > 0 ? (int)((Mq[pc + 1 - NPC] >> 8) & 31u) : (col > 0 ? 0 : -1));
-                    nB = by > 0 ? (int)((Mq[pc - 2] >> 8) & 31u)
-                                : (ry > 0 ? (int)((Mq[pc + 2 - NPC * R.w] >> 8) & 31u)
-                                          : (row > 0 ? 0 : -1));
-                }
-                nC = nc_of(nA, nB);
-                if (nC >= 8) {
-                    tv = tc ? (uint32_t)(((tc - 1) << 2) | t1) : 3u;
-                    tl = 6;
-                } else {
-                    const uint32_t e = PT.ct[nC < 2 ? 0 : (nC < 4 ? 1 : 2)][4 * tc + t1];
-                    tv = e & 255u;
-                    tl = e >> 8;
-                }
-                len = tl + (mv & 255u);
-            }
-            if (mv & M_OVF) {                          /* rare: re-code from the levels */
-                bd = Bd[(size_t)q * NPC + pc];
-                CountSink cn{0};
-                if (nC == -1) {
-                    const int dq[4] = {(int)(int16_t)(bd.x & 0xffffu), (int)(int16_t)(bd.x >> 16),
-                                       (int)(int16_t)(bd.y & 0xffffu), (int)(int16_t)(bd.y >> 16)};
-                    cavlc_dc4(cn, PT, dq);
-                } else {
-                    const int8_t *lvp = reinterpret_cast<const int8_t *>(&bd);
-                    cavlc_block(cn, TB, lvp, pc < 16 ? 16 : 15, nC);
-                }
-                len = cn.n;
-            } else if (mv & 255u) {
-                bd = Bd[(size_t)q * NPC + pc];
-            }
-            L.tc[kd][pc] = (uint8_t)tc;
-            L.blen[kd][pc] = (uint16_t)len;
+/* grid (row groups, frames, streams): workgroup x writes MB rows x, x + gx, ... */
+__global__ __launch_bounds__(WR_T) void k_dyn_write(const DevStream *__restrict__ st,
+                                                    const NalDesc *__restrict__ nal, int ld_nal,
+                                                    const PlanPending *__restrict__ pend,
+                                                    const DynFrame *__restrict__ dfr, int ld_fr, DynGeom g,
+                                                    const uint32_t *__restrict__ meta,
+                                                    const uint4 *__restrict__ body,
+                                                    const uint32_t *__restrict__ rowst, int ld_row,
+                                                    uint8_t *__restrict__ stage)
+{
+    __shared__ WrLds L;
+    const int s = blockIdx.z, f = blockIdx.y, t = threadIdx.x;
+    const DynFrame df = dfr[(size_t)s * ld_fr + f];
+    if (df.nal < 0 || df.err) return;
+    if (t < 8) {
+        L.wo[t] = pend[s].wo[t];
+        L.wl[t] = pend[s].wl[t];
+        L.wv[t] = pend[s].wv[t];
+    }
+    build_ptabs(*reinterpret_cast<const Tabs *>(&g_tabs), L.ptabs, t, WR_T);
+    const NalDesc d = nal[(size_t)s * ld_nal + df.nal];
+    const NalCtx c = nal_ctx(st + s, d, L.wo, L.wl, L.wv);
+    const HeadCtx H = head_ctx(c);
+    const int mbw = H.mbw, mbh = c.h / 16;
+    const Rect R{g.x0, g.y0, g.w, g.h};
+    const size_t nb = (size_t)s * ld_fr + f;
+    const int ndt = R.w * R.h;
+    const uint32_t *M = meta + nb * (size_t)(NPC * ndt);
+    const uint4 *Bd = body + nb * (size_t)(NPC * ndt);
+    const uint32_t *RS = rowst + nb * (size_t)ld_row;
+    uint32_t *out = reinterpret_cast<uint32_t *>(stage + nb * g.slot_bytes);
+    const Tabs &TB = g_tabs;
+    const PTabs &PT = L.ptabs;
+
+    for (int row = blockIdx.x; row < mbh; row += gridDim.x) {
+        const uint32_t rs = RS[row], re = RS[row + 1];
+        if (t == 0) L.head_over = 0;
+        __syncthreads();                                    /* previous row done with L */
+        if (t < 3) {
+            CapSink hc{0, 0, 0};
+            H.put_class(hc, H.sel(row, 0) + t);
+            L.hhi[t] = hc.hi;
+            L.hlo[t] = hc.lo;
+            L.hlen[t] = hc.n;
+            if (hc.over()) L.head_over = 1;
         }
         __syncthreads();
-        mark(0);
-
-        /* P2: buffer rewind; heads: cbp, piece offsets, MB length, scan */
-        if (pend_T) {
-            for (uint32_t jw = (uint32_t)t; jw <= pnf; jw += PACK_T) L.buf[jw] = jw == 0 ? part : 0u;
-            rewind_lnz();
-            F = pend_T & 31u;
-            bw += pnf;
-            pend_T = 0;
+        const bool head_over = L.head_over;
+        const bool in = row >= R.y0 && row < R.y0 + R.h;
+        const int nd = in ? R.w : 0;
+        auto head_bits = [&](int col) -> uint32_t {
+            if (!head_over) return L.hlen[col == 0 ? 0 : (col == mbw - 1 ? 2 : 1)];
+            CountSink cn{0};
+            H.put_slow(cn, row, col);
+            return cn.n;
+        };
+        for (int k = t; k < nd; k += WR_T) {
+            const int col = R.x0 + k, q = (row - R.y0) * R.w + k;
+            int cbp, code;
+            L.mbits[k] = dyn_mb_layout<true>(M, Bd, R, q, row, col, PT, TB, L.pl[k], L.tk[k], L.po[k],
+                                             head_bits(col), cbp, code);
+            L.cbp[k] = (uint8_t)cbp;
+            L.code[k] = (uint8_t)code;
         }
-        uint32_t mlen = 0;
-        int hsel = 0, code = 0, cbp = 0, hrow = 0, hcol = 0, hkd = -1;
-        if (t < nm) {
-            const int m = m0 + t;
-            hrow = (int)div_m((uint32_t)m, m_mbw);
-            hcol = m - hrow * mbw;
-            hsel = head_sel(hrow, hcol);
-            CountSink mc{head_over ? 0u : L.hlen[hsel]};
-            if (head_over) put_head_slow(mc, hrow, hcol);
-            const bool isdyn = hcol >= R.x0 && hcol < R.x0 + R.w && hrow >= R.y0 && hrow < R.y0 + R.h;
-            if (!isdyn) {
-                mlen = mc.n + 1u;                      /* + coded_block_pattern ue(0) */
-            } else {
-                hkd = (hrow - R.y0) * R.w + (hcol - R.x0) - q0;
-                const uint4 t0 = *reinterpret_cast<const uint4 *>(L.tc[hkd]);
-                const uint4 t1 = *reinterpret_cast<const uint4 *>(L.tc[hkd] + 16);
-                const uint32_t tw[8] = {t0.x, t0.y, t0.z, t0.w, t1.x, t1.y, t1.z, t1.w};
-                int cbp_l = 0;
-#pragma unroll
-                for (int b8 = 0; b8 < 4; ++b8) {      /* raster rows 2(b8>>1), +1; cols 2(b8&1), +1 */
-                    const int r0 = 2 * (b8 >> 1), sh = 16 * (b8 & 1);
-                    if (((tw[r0] >> sh) & 0xffffu) | ((tw[r0 + 1] >> sh) & 0xffffu)) cbp_l |= 1 << b8;
-                }
-                /* pieces 16, 17 = DC (bytes 0, 1 of tw[4]); 18..25 AC */
-                const bool ac = ((tw[4] >> 16) | tw[5] | (tw[6] & 0xffffu)) != 0u;
-                const bool anydc = (tw[4] & 0xffffu) != 0u;
-                const int cbp_c = ac ? 2 : (anydc ? 1 : 0);
-                cbp = cbp_l | (cbp_c << 4);
-                code = TB.cbp_code[cbp];
-                put_ue(mc, (uint32_t)code);
-                if (cbp) put_se(mc, 0);                /* mb_qp_delta */
-                uint32_t off = mc.n;
-                uint16_t *bo = L.boff[hkd];
-                const uint16_t *bl = L.blen[hkd];
-#pragma unroll
-                for (int blk = 0; blk < 16; ++blk) {   /* luma4x4BlkIdx order */
-                    const int r = blk_raster(blk);
-                    const bool pres = (cbp_l >> (blk >> 2)) & 1;
-                    bo[r] = pres ? (uint16_t)off : (uint16_t)0xffffu;
-                    off += pres ? bl[r] : 0u;
-                }
-#pragma unroll
-                for (int k2 = 16; k2 < NPC; ++k2) {    /* Cb DC, Cr DC, Cb AC 0-3, Cr AC 0-3 */
-                    const bool pres = k2 < 18 ? cbp_c >= 1 : cbp_c == 2;
-                    bo[k2] = pres ? (uint16_t)off : (uint16_t)0xffffu;
-                    off += pres ? bl[k2] : 0u;
-                }
-                mlen = off;
-            }
-        }
+        __syncthreads();
         {
-            const uint32_t incl = wave_incl_sum(mlen, lane);
-            L.exw[t] = incl - mlen;
-            if (lane == 63) L.wsum[wave] = incl;
-        }
-        __syncthreads();
-        mark(1);
-
-        uint32_t wtot = 0;
-#pragma unroll
-        for (int w2 = 0; w2 < PNW; ++w2) wtot += L.wsum[w2];
-        auto mbo = [&](int u) -> uint32_t { return pack_wave_pre(L.wsum, u >> 6) + L.exw[u]; };
-        const uint32_t Tb = F + wtot;
-        if (bw + (Tb >> 5) + 2u > cap_words) {         /* uniform */
-            over = true;
-            break;
-        }
-
-        /* P3: heads and pieces ORed into the buffer; a window larger than
-         * the buffer is written and flushed in passes of PBUF_WORDS - 1 words */
-        const uint32_t nw = (Tb + 31) >> 5;
-        const bool single = nw <= (uint32_t)PBUF_WORDS;
-        const uint32_t PW = single ? (uint32_t)PBUF_WORDS : (uint32_t)PBUF_WORDS - 1u;
-        const uint32_t my_head = t < nm ? F + mbo(t) : 0u;
-        uint32_t my_piece = 0xffffffffu;
-        if (is_piece) {
-            const uint32_t bo = L.boff[kd][pc];
-            if (bo != 0xffffu) {
-                const int q = q0 + kd;
-                const int mq = dyn_mb_m(R, mbw, m_rw, q) - m0;
-                my_piece = F + mbo(mq) + bo;
+            uint32_t carry = 0;
+            for (int c0 = 0; c0 < mbw; c0 += WR_T) {
+                const int col = c0 + t;
+                uint32_t len = 0;
+                if (col < mbw) {
+                    const int k = col - R.x0;
+                    len = (in && k >= 0 && k < R.w) ? L.mbits[k] : head_bits(col) + 1u;
+                }
+                uint32_t ex, tot;
+                block_excl_sum(len, L.wsum, ex, tot);
+                if (col < mbw) L.moff[col] = carry + ex;
+                carry += tot;
             }
         }
-        for (uint32_t p0 = 0; p0 < nw; p0 += PW) {
-            const LdsOrWin win{L.buf, p0, PW};
-            if (t < nm) {
+        const uint32_t rel0 = rs & 31u, w0 = rs >> 5;
+        const uint32_t nw = (rel0 + (re - rs) + 31u) >> 5;
+        for (uint32_t p0 = 0; p0 < nw; p0 += WBUF_WORDS) {
+            const uint32_t n = min((uint32_t)WBUF_WORDS, nw - p0);
+            for (uint32_t i = (uint32_t)t; i < n; i += WR_T) L.buf[i] = 0u;
+            __syncthreads();
+            const LdsOrWin win{L.buf, p0, n};
+            for (int col = t; col < mbw; col += WR_T) {
                 WSink sk{win, 0, 0, 0};
-                sk.start(my_head);
-                if (!head_over) sk.put_cap(CapSink{L.hhi[hsel], L.hlo[hsel], L.hlen[hsel]});
-                else put_head_slow(sk, hrow, hcol);
-                if (hkd < 0) {
-                    sk.put(1, 1);                      /* coded_block_pattern ue(0) */
+                sk.start(rel0 + L.moff[col]);
+                if (!head_over) {
+                    const int pos = col == 0 ? 0 : (col == mbw - 1 ? 2 : 1);
+                    sk.put_cap(CapSink{L.hhi[pos], L.hlo[pos], L.hlen[pos]});
                 } else {
-                    put_ue(sk, (uint32_t)code);
-                    if (cbp) put_se(sk, 0);
+                    H.put_slow(sk, row, col);
+                }
+                const int k = col - R.x0;
+                if (!(in && k >= 0 && k < R.w)) {
+                    sk.put(1, 1);                           /* coded_block_pattern ue(0) */
+                } else {
+                    put_ue(sk, (uint32_t)L.code[k]);
+                    if (L.cbp[k]) put_se(sk, 0);
                 }
                 sk.finish();
             }
-            if (my_piece != 0xffffffffu) {
+            for (int i = t; i < NPC * nd; i += WR_T) {
+                const int k = i / NPC, pc = i - k * NPC;
+                const uint32_t o = L.po[k][pc];
+                if (o == 0xffffu) continue;
+                const uint32_t tkv = L.tk[k][pc], len = L.pl[k][pc] & PL_LEN;
+                const int tl = (int)((tkv >> 16) & 31u), nC = (int)((tkv >> 21) & 31u) - 1;
+                const uint32_t bl = len - (uint32_t)tl;
+                uint4 bd = make_uint4(0, 0, 0, 0);
+                const size_t bi = (size_t)((row - R.y0) * R.w + k) * NPC + pc;
+                if (bl || (tkv & TK_OVF)) bd = Bd[bi];
                 WSink sk{win, 0, 0, 0};
-                sk.start(my_piece);
-                if (!(mv & M_OVF)) {
-                    if (nC != -1) sk.put(tv, (int)tl);
+                sk.start(rel0 + L.moff[R.x0 + k] + o);
+                if (!(tkv & TK_OVF)) {
+                    if (pc != 16 && pc != 17) sk.put(tkv & 0xffffu, tl);
                     sk.put_cap(CapSink{(uint64_t)bd.z | (uint64_t)bd.w << 32,
-                                       (uint64_t)bd.x | (uint64_t)bd.y << 32, mv & 255u});
-                } else if (nC == -1) {
+                                       (uint64_t)bd.x | (uint64_t)bd.y << 32, bl});
+                } else if (pc == 16 || pc == 17) {
                     const int dq[4] = {(int)(int16_t)(bd.x & 0xffffu), (int)(int16_t)(bd.x >> 16),
                                        (int)(int16_t)(bd.y & 0xffffu), (int)(int16_t)(bd.y >> 16)};
                     cavlc_dc4(sk, PT, dq);
@@ -787,70 +872,67 @@ __global__ __launch_bounds__(PACK_T, 8) void k_dyn_pack(DevStream *__restrict__ 
                 sk.finish();
             }
             __syncthreads();
-            if (single) {
-                pend_T = Tb;                           /* flushed during the next P1 */
-            } else {                                   /* rare: flush this pass now */
-                const uint32_t nfull = Tb >> 5;
-                const uint32_t n = p0 < nfull ? min(PW, nfull - p0) : 0u;
-                flush_words(n, bw + p0);
-                const uint32_t lastp = (Tb & 31u) && nfull - p0 < PW ? L.buf[nfull - p0] : 0u;
-                __syncthreads();
-                rewind_lnz();
-                for (uint32_t jw = (uint32_t)t; jw < (uint32_t)PBUF_WORDS; jw += PACK_T)
-                    L.buf[jw] = jw == 0 && p0 + PW >= nw ? lastp : 0u;
-                __syncthreads();
+            for (uint32_t i = (uint32_t)t; i < n; i += WR_T) {
+                const uint32_t gw = w0 + p0 + i, v = L.buf[i];
+                if ((gw == w0 && rel0) || gw == (re >> 5)) {
+                    if (v) atomicOr(&out[gw], __builtin_bswap32(v));
+                } else {
+                    out[gw] = __builtin_bswap32(v);
+                }
             }
         }
-        if (!single) {
-            bw += Tb >> 5;
-            F = Tb & 31u;
-        }
-        mark(2);
-        m0 = m1;
     }
+}
 
-    if (!over) {
-        if (pend_T) {                                  /* the last window's whole words */
-            const uint32_t pnf = pend_T >> 5;
-            flush_words(pnf, bw);
-            const uint32_t part = L.buf[pnf];
-            __syncthreads();
-            rewind_lnz();
-            if (t == 0) L.buf[0] = part;
-            F = pend_T & 31u;
-            bw += pnf;
-            __syncthreads();
+/* grid (frames, streams): EP positions (slot tail, unsorted) and count */
+__global__ __launch_bounds__(WR_T) void k_dyn_ep(DynFrame *__restrict__ dfr, int ld_fr, DynGeom g,
+                                                 const uint8_t *__restrict__ stage)
+{
+    __shared__ int32_t wmax[NW];
+    const int s = blockIdx.y, f = blockIdx.x, t = threadIdx.x, lane = t & 63;
+    DynFrame *DF = dfr + (size_t)s * ld_fr + f;
+    const DynFrame df = *DF;
+    if (df.nal < 0 || df.err) return;
+    const size_t nb = (size_t)s * ld_fr + f;
+    const uint8_t *in = stage + nb * g.slot_bytes;
+    uint32_t *eplist = reinterpret_cast<uint32_t *>(const_cast<uint8_t *>(in) + g.slot_bytes - DYN_OVF_BYTES);
+    const uint32_t nin = df.rbsp_bytes;
+    int carry = -1;
+    for (uint32_t i0 = 0; i0 < nin; i0 += WR_T * 16) {
+        const uint32_t ib = i0 + 16u * (uint32_t)t;
+        const uint32_t n = ib < nin ? min(16u, nin - ib) : 0u;
+        const uint4 v = n ? *reinterpret_cast<const uint4 *>(in + ib) : make_uint4(0, 0, 0, 0);
+        const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
+        int lnz = -1;
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+            if ((uint32_t)i < n && ((wv[i >> 2] >> (8 * (i & 3))) & 255u)) lnz = (int)(ib + i);
+        int ex, tot;
+        block_excl_max(lnz, wmax, ex, tot);
+        int prev = max(carry, ex);
+        uint32_t ins = 0;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const uint32_t b = (wv[i >> 2] >> (8 * (i & 3))) & 255u;
+            if ((uint32_t)i < n && ep_insert(b, (int)(ib + i) - 1 - prev)) ins |= 1u << i;
+            if ((uint32_t)i < n && b) prev = (int)(ib + i);
         }
-        /* rbsp_stop_one_bit + alignment (bitwriter.c:103-111); F < 32 */
-        if (t == 0) {
-            const uint32_t wv = L.buf[0] | (1u << (31 - F));
-            const uint32_t nb2 = (F + 1u + 7u) >> 3;
-            out[bw] = __builtin_bswap32(wv);
-            int prev = L.lnz_r;
-            my_ep += ep_word(wv, 4u * bw, 4u * bw + nb2, prev, eplist, &L.ep_n);
-            DF->rbsp_bytes = 4u * bw + nb2;
+        const uint32_t cnt = (uint32_t)__builtin_popcount(ins);
+        const uint32_t incl = wave_incl_sum(cnt, lane);
+        const uint32_t wtot = __shfl(incl, 63, 64);
+        uint32_t base = 0;
+        if (wtot) {
+            if (lane == 0) base = atomicAdd(&DF->ep, wtot);
+            base = __shfl(base, 0, 64);
         }
-    }
-    /* EP total over the workgroup */
-    {
-        const uint32_t incl = wave_incl_sum(my_ep, lane);
-        __syncthreads();
-        if (lane == 63) L.wsum[wave] = incl;
-        __syncthreads();
-    }
-    if (stamps && t == 0) {
-        uint64_t *o = stamps + ((size_t)s * gridDim.x + f) * 8;
-        for (int k = 0; k < 5; ++k) o[k] = ph[k];
-        o[5] = nwin;
-        o[6] = __builtin_amdgcn_s_memtime() - t_start;
-        o[7] = (uint64_t)(uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 4);     /* HW_ID */
-    }
-    if (t == 0) {
-        uint32_t tot = 0;
-        for (int w2 = 0; w2 < PNW; ++w2) tot += L.wsum[w2];
-        DF->ep = tot;
-        DF->err = over ? DF_OVER : 0u;
-        if (over) atomicOr((unsigned int *)&S->err, SCROLL_DEVERR_DYN);
+        uint32_t k = base + incl - cnt;
+        while (ins) {
+            const int i = __builtin_ctz(ins);
+            ins &= ins - 1u;
+            if (k < (uint32_t)EPLIST_MAX) eplist[k] = ib + (uint32_t)i;   /* RBSP index the 03 precedes */
+            k++;
+        }
+        carry = max(carry, tot);
     }
 }
 
@@ -1172,11 +1254,18 @@ int dyn_launch_code(hipStream_t hs, int nframes, int S, const DevStream *st, con
 
 int dyn_launch_pack(hipStream_t hs, int nframes, int S, DevStream *st, const NalDesc *nal,
                     int ld_nal, const PlanPending *pend, DynFrame *dfr, int ld_fr,
-                    const DynGeom *g, const DynScratch *x, uint8_t *stage, uint64_t *stamps)
+                    const DynGeom *g, const DynScratch *x, uint8_t *stage)
 {
     if (nframes <= 0 || S <= 0) return 0;
-    hipLaunchKernelGGL(k_dyn_pack, dim3(nframes, S), dim3(PACK_T), 0, hs, st, nal, ld_nal, pend, dfr, ld_fr,
-                       *g, x->meta, x->body, stage, stamps);
+    const int mbh = x->ld_row - 1;
+    hipLaunchKernelGGL(k_dyn_len, dim3(nframes, S), dim3(WR_T), 0, hs, st, nal, ld_nal, pend, dfr, ld_fr,
+                       *g, x->meta, x->body, x->rowst, x->ld_row, stage);
+    if (hipGetLastError() != hipSuccess) return -1;
+    const int gx = (mbh + WR_ROWS - 1) / WR_ROWS;
+    hipLaunchKernelGGL(k_dyn_write, dim3(gx, nframes, S), dim3(WR_T), 0, hs, st, nal, ld_nal, pend, dfr,
+                       ld_fr, *g, x->meta, x->body, x->rowst, x->ld_row, stage);
+    if (hipGetLastError() != hipSuccess) return -1;
+    hipLaunchKernelGGL(k_dyn_ep, dim3(nframes, S), dim3(WR_T), 0, hs, dfr, ld_fr, *g, stage);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

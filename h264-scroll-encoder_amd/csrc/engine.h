@@ -80,6 +80,8 @@ typedef struct {
 /* dynamic rect geometry and buffer strides (one per batch) */
 #define DYN_MAX_W 64                /* rect width limit (MBs)                     */
 #define DYN_MAX_H 48                /* rect height limit (MBs)                    */
+#define DYN_MAX_MBW 512             /* picture width limit with the rect (MBs)   */
+#define DYN_MAX_MBH 512             /* picture height limit with the rect (MBs)  */
 #define DYN_PIECES 26               /* coded pieces per dynamic MB: 16 luma, 2 DC, 8 AC */
 #define DYN_OVF_BYTES 8192          /* staging-slot tail: levels of > 128-bit blocks */
 typedef struct {

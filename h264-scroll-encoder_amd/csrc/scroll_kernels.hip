@@ -1235,9 +1235,10 @@ static int launch(ScrollBatch *b, int nframes, int plan_mode, int nal_max, hipSt
                 b->dbg_slots = slots;
             }
             HIPCHK(hipMemsetAsync(b->d_dbg, 0, slots * 8 * sizeof(uint64_t), hs));
-            stamps = b->d_dbg;
+            stamps = b->d_dbg;      /* k_dyn_emit_gather writes past the first half */
         }
         b->geo.debug = b->debug;
+        (void)stamps;
         if (hint) {
             if (hint_launch_stage(hs, nframes, S, b->d_st, b->d_nal, b->ld_nal, b->d_pend,
                                   b->d_dfr, ld_fr, b->d_hf, b->d_pool, b->d_stage,
@@ -1254,7 +1255,7 @@ static int launch(ScrollBatch *b, int nframes, int plan_mode, int nal_max, hipSt
             }
             if ((rc = mark(6))) return rc;
             if (dyn_launch_pack(hs, nframes, S, b->d_st, b->d_nal, b->ld_nal, b->d_pend, b->d_dfr,
-                                ld_fr, &b->geo, &b->dx, b->d_stage, stamps)) {
+                                ld_fr, &b->geo, &b->dx, b->d_stage)) {
                 set_err("k_dyn_pack launch: %s", hipGetErrorString(hipGetLastError()));
                 return SCROLL_ERR_HIP;
             }
@@ -1507,6 +1508,7 @@ static void dyn_release(ScrollBatch *b)
     (void)hipFree(b->dx.rows);
     (void)hipFree(b->dx.meta);
     (void)hipFree(b->dx.body);
+    (void)hipFree(b->dx.rowst);
     b->d_dfr = nullptr;
     b->d_src = b->d_refs = b->d_stage = nullptr;
     b->dx = DynScratch{};
@@ -1547,6 +1549,7 @@ int scroll_batch_set_dyn_rect(ScrollBatch *b, int x0, int y0, int w, int h, size
     const int mbw = pw / 16, mbh = ph / 16;
     /* prediction rows are byte offsets into a reference pair below 2^28 */
     if ((pw & 15) || (ph & 15) || x0 + w > mbw || y0 + h > mbh || w > DYN_MAX_W || h > DYN_MAX_H ||
+        mbw > DYN_MAX_MBW || mbh > DYN_MAX_MBH ||
         (size_t)3 * pw * ph >= ((size_t)1 << 28)) {
         set_err("scroll_batch_set_dyn_rect: rect (%d,%d %dx%d MBs) not supported in %dx%d", x0, y0,
                 w, h, pw, ph);
@@ -1571,6 +1574,8 @@ int scroll_batch_set_dyn_rect(ScrollBatch *b, int x0, int y0, int w, int h, size
     if (e == hipSuccess) e = hipMalloc(&b->dx.rows, S * F * 32 * h * sizeof(uint32_t));
     if (e == hipSuccess) e = hipMalloc(&b->dx.meta, S * F * DYN_PIECES * w * h * sizeof(uint32_t));
     if (e == hipSuccess) e = hipMalloc(&b->dx.body, S * F * DYN_PIECES * w * h * sizeof(uint4));
+    if (e == hipSuccess) e = hipMalloc(&b->dx.rowst, S * F * (mbh + 1) * sizeof(uint32_t));
+    b->dx.ld_row = mbh + 1;
     if (e == hipSuccess) e = hipMemset(b->d_dfr, 0, S * F * sizeof(DynFrame));
     if (e == hipSuccess) e = hipMemset(b->d_src, 0, S * g.src_ld);
     if (e == hipSuccess) e = hipMemset(b->d_refs, 0, S * dyn_pair_bytes(b));

@@ -16,18 +16,20 @@ typedef struct {
     uint32_t *rows;
     uint32_t *meta;
     uint4 *body;
-    uint32_t *rowst;                /* k_dyn_len -> k_dyn_write: MB-row bit offsets */
-    int ld_row;                     /* picture MB rows + 1 */
+    unsigned long long *status;     /* k_dyn_group look-back: per (frame, row group) */
+    uint2 *side;                    /* k_dyn_group -> k_dyn_ep: shared boundary words */
+    uint32_t epoch;                 /* look-back epoch of the last compose (24 bits, never 0) */
 } DynScratch;
 
 /* k_dyn_rows + k_dyn_code (both instantiations): block records */
 int dyn_launch_code(hipStream_t hs, int nframes, int S, const DevStream *st, const NalDesc *nal,
                     int ld_nal, const PlanPending *pend, DynFrame *dfr, int ld_fr,
                     const DynGeom *g, const uint8_t *src, const uint8_t *refs, const DynScratch *x);
-/* k_dyn_len + k_dyn_write + k_dyn_ep: records -> staged RBSP + EP positions */
+/* k_dyn_group + k_dyn_ep: records -> staged RBSP + EP positions */
 int dyn_launch_pack(hipStream_t hs, int nframes, int S, DevStream *st, const NalDesc *nal,
                     int ld_nal, const PlanPending *pend, DynFrame *dfr, int ld_fr,
-                    const DynGeom *g, const DynScratch *x, uint8_t *stage);
+                    const DynGeom *g, const DynScratch *x, uint8_t *stage, uint32_t epoch,
+                    uint64_t *stamps, int mbw, int mbh);
 int dyn_launch_emit(hipStream_t hs, int nframes, int S, const DevStream *st, const NalDesc *nal,
                     int ld_nal, const DynFrame *dfr, int ld_fr, const DynGeom *g,
                     const uint8_t *stage, uint8_t *arena, uint64_t ld_arena, uint64_t *stamps);

@@ -64,7 +64,7 @@ __device__ inline NalCtx nal_ctx(const DevStream *S, const NalDesc &d, const int
 }
 
 /* ====================================================================== */
-/* The dynamic-rect coder is three kernels:                */
+/* The dynamic-rect coder is four kernels:                 */
 /*                                                                         */
 /*   k_dyn_rows   per NAL: the waypoint chain of every prediction row of   */
 /*                the rect, resolved once to byte offsets in picture A / B */
@@ -72,9 +72,12 @@ __device__ inline NalCtx nal_ctx(const DevStream *S, const NalDesc &d, const int
 /*                transform, quant and the nC-independent CAVLC body      */
 /*                (signs, levels, total_zeros, run_before) -> records;     */
 /*                chroma DC whole (nC = -1)                                */
-/*   k_dyn_pack   per NAL: coeff_token from the neighbours' TotalCoeff,    */
-/*                cbp, MB heads, bit placement; whole words -> staging     */
-/*                with the exact emulation-prevention positions            */
+/*   k_dyn_group  per MB-row group of a NAL: coeff_token from the          */
+/*                neighbours' TotalCoeff, cbp, MB heads, offsets; start    */
+/*                bit by a look-back over the groups before; bits -> LDS   */
+/*                -> staging words                                         */
+/*   k_dyn_ep     per NAL: shared boundary words merged, emulation-        */
+/*                prevention positions and count                           */
 /*                                                                         */
 /* Records of dynamic MB q (rect raster order) of NAL n, piece pc:          */
 /*   0..15 luma 4x4 (raster), 16 / 17 Cb / Cr DC, 18 + 4p + b chroma AC    */
@@ -82,7 +85,7 @@ __device__ inline NalCtx nal_ctx(const DevStream *S, const NalDesc &d, const int
 /*   TrailingOnes << 13 | ovf << 15, body[n][q][pc] = the body right-      */
 /*   aligned in 128 bits (x = bits 0..31 .. w = bits 96..127); DC pieces   */
 /*   hold the whole block.  ovf: more than 128 bits -- body holds the      */
-/*   levels instead (int8 scan order; DC: int16) and k_dyn_pack re-codes.  */
+/*   levels instead (int8 scan order; DC: int16) and k_dyn_group re-codes. */
 /* ====================================================================== */
 constexpr int NPC = DYN_PIECES;         /* pieces per dynamic MB */
 constexpr uint32_t M_OVF = 1u << 15;
@@ -172,21 +175,22 @@ constexpr int CODE_T = 256;
 constexpr int HEAVY_TC = 3;
 
 template <bool GENERAL>
-__global__ __launch_bounds__(CODE_T) void k_dyn_code(const DevStream *__restrict__ st,
+__device__ inline void code_frame(const DevStream *__restrict__ st,
                                                      const DynFrame *__restrict__ dfr, int ld_fr,
                                                      const PlanPending *__restrict__ pend,
                                                      const NalDesc *__restrict__ nal, int ld_nal,
                                                      DynGeom g, const uint32_t *__restrict__ rows,
                                                      const uint8_t *__restrict__ src,
                                                      const uint8_t *__restrict__ refs,
-                                                     uint32_t *__restrict__ meta, uint4 *__restrict__ body)
+                                                     uint32_t *__restrict__ meta, uint4 *__restrict__ body,
+                                                     int s, int f, int bx)
 {
     __shared__ uint4 lv[CODE_T];
     __shared__ uint32_t whc[CODE_T / 64];
     __shared__ uint8_t order[CODE_T];
     __shared__ PTabs ptabs;
     __shared__ int32_t wo[8], wv[8];
-    const int s = blockIdx.z, f = blockIdx.y, t = threadIdx.x;
+    const int t = threadIdx.x;
     const int lane = t & 63, wave = t >> 6;
     const DynFrame df = dfr[(size_t)s * ld_fr + f];
     if (df.nal < 0) return;
@@ -199,7 +203,7 @@ __global__ __launch_bounds__(CODE_T) void k_dyn_code(const DevStream *__restrict
     __syncthreads();
 
     const int ndt = g.w * g.h, ntask = 24 * ndt;
-    const int task = (int)blockIdx.x * CODE_T + t;
+    const int task = bx * CODE_T + t;
     const size_t nb = (size_t)s * ld_fr + f;
     const uint32_t *rw = rows + nb * (size_t)(32 * g.h);
     const int w = st[s].w, h = st[s].h;
@@ -358,7 +362,7 @@ __global__ __launch_bounds__(CODE_T) void k_dyn_code(const DevStream *__restrict
     }
     __syncthreads();
     const int u = order[t];
-    const int tk = (int)blockIdx.x * CODE_T + u;
+    const int tk = bx * CODE_T + u;
     if (tk >= ntask) return;
     const uint4 v4 = lv[u];
     const uint32_t q[4] = {v4.x, v4.y, v4.z, v4.w};
@@ -385,6 +389,53 @@ __global__ __launch_bounds__(CODE_T) void k_dyn_code(const DevStream *__restrict
     }
 }
 
+
+/* the frames without a half-pel waypoint chain: grid (chunks, frames, streams) */
+__global__ __launch_bounds__(CODE_T) void k_dyn_code(const DevStream *__restrict__ st,
+                                                     const DynFrame *__restrict__ dfr, int ld_fr,
+                                                     const PlanPending *__restrict__ pend,
+                                                     const NalDesc *__restrict__ nal, int ld_nal,
+                                                     DynGeom g, const uint32_t *__restrict__ rows,
+                                                     const uint8_t *__restrict__ src,
+                                                     const uint8_t *__restrict__ refs,
+                                                     uint32_t *__restrict__ meta, uint4 *__restrict__ body)
+{
+    code_frame<false>(st, dfr, ld_fr, pend, nal, ld_nal, g, rows, src, refs, meta, body, blockIdx.z,
+                      blockIdx.y, blockIdx.x);
+}
+
+/* the others (general chroma path, never for the composer's own waypoints):
+ * grid (chunks, 1, streams), each workgroup finds its stream's flagged
+ * frames 64 at a time -- a launch over every frame would cost more in empty
+ * workgroups than the frames it serves */
+__global__ __launch_bounds__(CODE_T) void k_dyn_code_general(const DevStream *__restrict__ st,
+                                                             const DynFrame *__restrict__ dfr, int ld_fr,
+                                                             const PlanPending *__restrict__ pend,
+                                                             const NalDesc *__restrict__ nal, int ld_nal,
+                                                             DynGeom g, const uint32_t *__restrict__ rows,
+                                                             const uint8_t *__restrict__ src,
+                                                             const uint8_t *__restrict__ refs,
+                                                             uint32_t *__restrict__ meta,
+                                                             uint4 *__restrict__ body, int nframes)
+{
+    const int s = blockIdx.z, lane = threadIdx.x & 63;
+    for (int f0 = 0; f0 < nframes; f0 += 64) {
+        bool gen = false;
+        if (f0 + lane < nframes) {
+            const DynFrame df = dfr[(size_t)s * ld_fr + f0 + lane];
+            gen = df.nal >= 0 && (df.err & DF_GENERAL);
+        }
+        uint64_t m = __ballot(gen);                     /* the same in every wave */
+        while (m) {
+            const int f = f0 + __builtin_ctzll(m);
+            m &= m - 1;
+            code_frame<true>(st, dfr, ld_fr, pend, nal, ld_nal, g, rows, src, refs, meta, body, s, f,
+                             blockIdx.x);
+            __syncthreads();
+        }
+    }
+}
+
 struct LdsOrWin {
     uint32_t *b;
     uint32_t lo, n;
@@ -397,26 +448,13 @@ struct LdsOrWin {
 typedef OrSink<LdsOrWin> WSink;
 
 /* ---------------------------------------------------------------------- */
-/* k_dyn_len / k_dyn_write / k_dyn_ep: records -> staged RBSP               */
+/* k_dyn_group / k_dyn_ep: records -> staged RBSP                         */
 /* ---------------------------------------------------------------------- */
 /* A NAL's bits are: slice header, then per MB row the MB heads (one of 12
  * codeword classes) and, for dynamic MBs, coded_block_pattern,
  * mb_qp_delta and the present pieces (coeff_token from the neighbours'
- * TotalCoeff + the body k_dyn_code left in the records), then the stop bit.
- *   k_dyn_len    per NAL: every MB row's length -> row bit offsets; writes
- *                the header words, the stop word, and zeroes every staging
- *                word two rows share
- *   k_dyn_write  per MB row (all rows of all NALs at once): MB offsets by a
- *                block scan, heads and pieces ORed into an LDS line of the
- *                row, whole words stored, the two shared words atomically ORed
- *   k_dyn_ep     per NAL: emulation-prevention positions + count from the
- *                staged bytes (closed form of nal.c:33-38, ep_insert) */
-constexpr int WR_T = 256;
-constexpr int WBUF_WORDS = 2048;        /* 64 Kbit per pass; a config-3 row is ~19 Kbit */
-constexpr int MAX_MBW = DYN_MAX_MBW, MAX_MBH = DYN_MAX_MBH;
-constexpr int WR_ROWS = 3;              /* MB rows per k_dyn_write workgroup */
-constexpr int PL_LEN = 0x7ff;           /* piece length bits of a pl entry; nC + 1 above */
-constexpr uint32_t TK_OVF = 1u << 31;
+ * TotalCoeff + the body k_dyn_code left in the records), then the stop bit. */
+constexpr int WR_T = 512, WR_NW = WR_T / 64;
 
 __device__ inline int tc_of(uint32_t m) { return (int)((m >> 8) & 31u); }
 
@@ -466,108 +504,6 @@ __device__ inline HeadCtx head_ctx(const NalCtx &c)
     return H;
 }
 
-/* Layout of dynamic MB q at frame MB (row, col): per piece pc the length
- * with its coeff_token (pl[pc] = len | (nC + 1) << 11) and, when tk, the
- * token (tk[pc] = bits | len << 16 | nC + 1 << 21 | TK_OVF) and the offset
- * from the MB start (po[pc], 0xffff: not coded).  hb = head bits.  Returns
- * the MB's bits; cbp and its me(v) code number out.  pl / tk / po: LDS. */
-template <bool TOK>
-__device__ inline uint32_t dyn_mb_layout(const uint32_t *__restrict__ M, const uint4 *__restrict__ Bd,
-                                         const Rect &R, int q, int row, int col, const PTabs &PT,
-                                         const Tabs &TB, uint16_t *pl, uint32_t *tk, uint16_t *po,
-                                         uint32_t hb, int &cbp_o, int &code_o)
-{
-    const int ry = row - R.y0, cx = col - R.x0;
-    const uint32_t *Mq = M + (size_t)q * NPC;
-    const uint32_t *ML = Mq - NPC, *MT = Mq - (size_t)NPC * R.w;
-    uint32_t m[NPC];
-#pragma unroll
-    for (int i = 0; i < NPC / 2; ++i) {
-        const uint2 v = *reinterpret_cast<const uint2 *>(Mq + 2 * i);
-        m[2 * i] = v.x;
-        m[2 * i + 1] = v.y;
-    }
-    const int nAe = col > 0 ? 0 : -1, nBe = row > 0 ? 0 : -1;     /* a neighbour outside the rect */
-    uint32_t ovf = 0;
-    int cbp_l = 0;
-    bool dc = false, ac = false;
-#pragma unroll
-    for (int pc = 0; pc < NPC; ++pc) {
-        const uint32_t mv = m[pc];
-        const int tc = tc_of(mv);
-        uint32_t tl = 0, tv = 0;
-        int nC = -1;
-        if (pc == 16 || pc == 17) {
-            dc |= tc != 0;
-        } else {
-            int nA, nB;
-            if (pc < 16) {
-                const int bx = pc & 3, by = pc >> 2;
-                nA = bx > 0 ? tc_of(m[pc - 1]) : (cx > 0 ? tc_of(ML[pc + 3]) : nAe);
-                nB = by > 0 ? tc_of(m[pc - 4]) : (ry > 0 ? tc_of(MT[pc + 12]) : nBe);
-                if (tc) cbp_l |= 1 << (2 * (by >> 1) + (bx >> 1));
-            } else {
-                const int b = (pc - 18) & 3, bx = b & 1, by = b >> 1;
-                nA = bx > 0 ? tc_of(m[pc - 1]) : (cx > 0 ? tc_of(ML[pc + 1]) : nAe);
-                nB = by > 0 ? tc_of(m[pc - 2]) : (ry > 0 ? tc_of(MT[pc + 2]) : nBe);
-                ac |= tc != 0;
-            }
-            nC = nc_of(nA, nB);
-            const int t1 = (int)((mv >> 13) & 3u);
-            if (nC >= 8) {
-                tv = tc ? (uint32_t)(((tc - 1) << 2) | t1) : 3u;
-                tl = 6;
-            } else {
-                const uint32_t e = PT.ct[nC < 2 ? 0 : (nC < 4 ? 1 : 2)][4 * tc + t1];
-                tv = e & 255u;
-                tl = e >> 8;
-            }
-        }
-        pl[pc] = (uint16_t)((tl + (mv & 255u)) | (uint32_t)(nC + 1) << 11);
-        if (TOK) tk[pc] = tv | tl << 16 | (uint32_t)(nC + 1) << 21 | (mv & M_OVF ? TK_OVF : 0u);
-        if (mv & M_OVF) ovf |= 1u << pc;
-    }
-    while (ovf) {                       /* rare: > 128-bit block, measure from the levels */
-        const int pc = __builtin_ctz(ovf);
-        ovf &= ovf - 1u;
-        const uint4 bd = Bd[(size_t)q * NPC + pc];
-        CountSink cn{0};
-        const uint32_t e = pl[pc];
-        if (pc == 16 || pc == 17) {
-            const int dq[4] = {(int)(int16_t)(bd.x & 0xffffu), (int)(int16_t)(bd.x >> 16),
-                               (int)(int16_t)(bd.y & 0xffffu), (int)(int16_t)(bd.y >> 16)};
-            cavlc_dc4(cn, PT, dq);
-        } else {
-            const int8_t *lvp = reinterpret_cast<const int8_t *>(&bd);
-            cavlc_block(cn, TB, lvp, pc < 16 ? 16 : 15, (int)(e >> 11) - 1);
-        }
-        pl[pc] = (uint16_t)(cn.n | (e & ~(uint32_t)PL_LEN));
-    }
-    const int cbp_c = ac ? 2 : (dc ? 1 : 0);
-    const int cbp = cbp_l | cbp_c << 4;
-    const int code = TB.cbp_code[cbp];
-    CountSink hs{hb};
-    put_ue(hs, (uint32_t)code);
-    if (cbp) put_se(hs, 0);                                 /* mb_qp_delta */
-    uint32_t off = hs.n;
-#pragma unroll
-    for (int blk = 0; blk < 16; ++blk) {                    /* luma4x4BlkIdx order */
-        const int r = blk_raster(blk);
-        const bool pres = (cbp_l >> (blk >> 2)) & 1;
-        if (TOK) po[r] = pres ? (uint16_t)off : (uint16_t)0xffffu;
-        off += pres ? (uint32_t)(pl[r] & PL_LEN) : 0u;
-    }
-#pragma unroll
-    for (int k2 = 16; k2 < NPC; ++k2) {                     /* Cb DC, Cr DC, Cb AC 0-3, Cr AC 0-3 */
-        const bool pres = k2 < 18 ? cbp_c >= 1 : cbp_c == 2;
-        if (TOK) po[k2] = pres ? (uint16_t)off : (uint16_t)0xffffu;
-        off += pres ? (uint32_t)(pl[k2] & PL_LEN) : 0u;
-    }
-    cbp_o = cbp;
-    code_o = code;
-    return off;
-}
-
 /* bits of the non-dynamic MBs of one row: (head + coded_block_pattern ue(0))
  * per MB, by class counts (first / middle / last column) */
 __device__ inline uint32_t row_static_bits(const HeadCtx &H, const uint32_t *hlen, int row, const Rect &R)
@@ -586,29 +522,189 @@ __device__ inline uint32_t row_static_bits(const HeadCtx &H, const uint32_t *hle
     return bits;
 }
 
-struct LenLds {
-    uint16_t pl[WR_T][NPC];
-    uint32_t rowbits[MAX_MBH];
-    uint32_t hdr[HDR_MAX / 32 + 2];
-    uint32_t wsum[NW];
+/* Row groups of a NAL: g = 0 the rows above the rect (with the slice
+ * header), g = 1 .. h the rect rows, g = h + 1 the rows below (with the stop
+ * bit).  One workgroup per group measures its bits, takes its start bit from
+ * the groups before it by a decoupled look-back over per-group status words,
+ * and writes every staging word it owns alone; its first / last word, when
+ * shared with a neighbour group, goes to a side entry that k_dyn_ep merges. */
+constexpr uint32_t SIDE_NONE = 0xffffffffu;
+
+/* status word: epoch (24) | flag (2: 1 aggregate, 2 inclusive prefix) | bits (38) */
+__device__ inline uint64_t lb_pack(uint32_t epoch, uint32_t flag, uint64_t v)
+{
+    return (uint64_t)(epoch & 0xffffffu) << 40 | (uint64_t)flag << 38 | v;
+}
+
+__device__ inline void lb_store(unsigned long long *p, uint64_t v)
+{
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+/* exclusive prefix of group g, by the 64 lanes of one wave: publishes the
+ * aggregate, then reads the status of the 64 groups before at once, sums
+ * back to the nearest inclusive prefix (retrying while a group in that span
+ * has not published), publishes its own inclusive prefix */
+__device__ inline uint64_t lb_lookback(unsigned long long *sa, int g, uint32_t epoch, uint64_t bits, int lane)
+{
+    if (g == 0) {
+        if (lane == 0) lb_store(sa, lb_pack(epoch, 2, bits));
+        return 0;
+    }
+    if (lane == 0) lb_store(sa + g, lb_pack(epoch, 1, bits));
+    uint64_t pre = 0;
+    for (int j = g - 1;;) {
+        const int jj = j - lane;
+        uint64_t v = 0;
+        uint32_t fl = 2;                                    /* before group 0: empty, inclusive */
+        if (jj >= 0) {
+            v = __hip_atomic_load(sa + jj, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            fl = (uint32_t)(v >> 40) == (epoch & 0xffffffu) ? (uint32_t)(v >> 38) & 3u : 0u;
+            v &= (1ull << 38) - 1;
+        }
+        const uint64_t incl = __ballot(fl == 2), none = __ballot(fl == 0);
+        const int fi = incl ? __builtin_ctzll(incl) : 63;   /* nearest inclusive in the window */
+        const uint64_t span = fi == 63 ? ~0ull : (2ull << fi) - 1;
+        if (none & span) {
+            __builtin_amdgcn_s_sleep(1);
+            continue;
+        }
+        const uint64_t c = lane <= fi ? v : 0;
+        uint32_t lo = (uint32_t)(c & 0xffffffu), hi = (uint32_t)(c >> 24);
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) {
+            lo += __shfl_xor(lo, d, 64);
+            hi += __shfl_xor(hi, d, 64);
+        }
+        pre += ((uint64_t)hi << 24) + lo;
+        if (incl) break;
+        j -= 64;
+    }
+    if (lane == 0) lb_store(sa + g, lb_pack(epoch, 2, pre + bits));
+    return pre;
+}
+
+/* a > 128-bit block from its levels (rare): measure / write */
+__device__ __attribute__((noinline)) uint32_t ovf_bits(const PTabs &PT, const Tabs &TB, uint4 bd, int pc, int nC)
+{
+    CountSink cn{0};
+    if (nC == -1) {
+        const int dq[4] = {(int)(int16_t)(bd.x & 0xffffu), (int)(int16_t)(bd.x >> 16),
+                           (int)(int16_t)(bd.y & 0xffffu), (int)(int16_t)(bd.y >> 16)};
+        cavlc_dc4(cn, PT, dq);
+    } else {
+        const int8_t *lvp = reinterpret_cast<const int8_t *>(&bd);
+        cavlc_block(cn, TB, lvp, pc < 16 ? 16 : 15, nC);
+    }
+    return cn.n;
+}
+
+/* the sink lives in the callee: a sink passed by reference would be kept in
+ * scratch memory by the caller on its every put */
+__device__ __attribute__((noinline)) void ovf_put(uint32_t *buf, uint32_t lo, uint32_t n, uint32_t pos,
+                                                  const PTabs &PT, const Tabs &TB, uint4 bd, int pc, int nC)
+{
+    WSink sk{LdsOrWin{buf, lo, n}, 0, 0, 0};
+    sk.start(pos);
+    if (nC == -1) {
+        const int dq[4] = {(int)(int16_t)(bd.x & 0xffffu), (int)(int16_t)(bd.x >> 16),
+                           (int)(int16_t)(bd.y & 0xffffu), (int)(int16_t)(bd.y >> 16)};
+        cavlc_dc4(sk, PT, dq);
+    } else {
+        const int8_t *lvp = reinterpret_cast<const int8_t *>(&bd);
+        cavlc_block(sk, TB, lvp, pc < 16 ? 16 : 15, nC);
+    }
+    sk.finish();
+}
+
+/* k_dyn_group is ONE wave per row group: the group's work is a chain of
+ * short dependent phases (records -> tokens -> MB layout -> scans ->
+ * look-back -> bits -> words), so throughput comes from many groups in
+ * flight per CU rather than from wide workgroups; LDS is sized to the rect
+ * (dynamic shared memory, group_lds_bytes) */
+constexpr int GW = 64;
+constexpr int GBUF_WORDS = 1024;         /* 32 Kbit per pass; a config-3 row is ~18 Kbit */
+
+struct GroupFixed {
+    uint32_t buf[GBUF_WORDS];
+    uint64_t hhi[12], hlo[12];
     uint32_t hlen[12];
     int32_t head_over;
     int32_t wo[8], wl[8], wv[8];
     PTabs ptabs;
 };
 
-/* grid (frames, streams), WR_T threads per NAL */
-__global__ __launch_bounds__(WR_T) void k_dyn_len(DevStream *__restrict__ st, const NalDesc *__restrict__ nal,
-                                                  int ld_nal, const PlanPending *__restrict__ pend,
+/* dynamic LDS: mt, lo [NPC w] u32, ma [8 w] u32, moff [lines] u32,
+ * mbits [w] u32, off16 [NPC w] u16, cbp / code [w] u8 */
+__host__ __device__ inline size_t group_lds_bytes(int w, int lines)
+{
+    return (size_t)4 * (2 * NPC * w + 8 * w + lines + w) + (size_t)2 * NPC * w + (size_t)2 * w + 16;
+}
+
+/* lo[i]: piece length (11) | coeff_token bits (8) << 11 | its length (5) << 19 | nC + 1 (5) << 24 */
+constexpr uint32_t LO_LEN = 0x7ffu;
+
+/* grid (R.h + 2, frames, streams), GW threads */
+__global__ __launch_bounds__(GW) void k_dyn_group(DevStream *__restrict__ st,
+                                                  const NalDesc *__restrict__ nal, int ld_nal,
+                                                  const PlanPending *__restrict__ pend,
                                                   DynFrame *__restrict__ dfr, int ld_fr, DynGeom g,
                                                   const uint32_t *__restrict__ meta,
-                                                  const uint4 *__restrict__ body, uint32_t *__restrict__ rowst,
-                                                  int ld_row, uint8_t *__restrict__ stage)
+                                                  const uint4 *__restrict__ body,
+                                                  unsigned long long *__restrict__ status,
+                                                  uint2 *__restrict__ side, uint32_t epoch, int lines,
+                                                  uint8_t *__restrict__ stage, uint64_t *__restrict__ stamps)
 {
-    __shared__ LenLds L;
-    const int s = blockIdx.y, f = blockIdx.x, t = threadIdx.x;
-    DevStream *S = st + s;
+    __shared__ GroupFixed L;
+    extern __shared__ uint32_t gdyn[];
+    uint64_t stv[6] = {0, 0, 0, 0, 0, 0};
+    if (stamps) stv[0] = __builtin_amdgcn_s_memrealtime();
+    const int gi = blockIdx.x, ng = (int)gridDim.x, f = blockIdx.y, s = blockIdx.z, t = threadIdx.x;
     DynFrame *DF = dfr + (size_t)s * ld_fr + f;
+    const Rect R{g.x0, g.y0, g.w, g.h};
+    const size_t nb = (size_t)s * ld_fr + f;
+    const int ndt = R.w * R.h;
+    const uint32_t *M = meta + nb * (size_t)(NPC * ndt);
+    const uint4 *Bd = body + nb * (size_t)(NPC * ndt);
+    const bool first = gi == 0, last = gi == ng - 1, rect = !first && !last;
+    const int row = rect ? R.y0 + gi - 1 : 0;
+    const int nd = rect ? R.w : 0, npc = NPC * nd;
+    const int q0 = rect ? (row - R.y0) * R.w : 0;
+    uint32_t *mt = gdyn, *lo = mt + NPC * R.w, *ma = lo + NPC * R.w, *moff = ma + 8 * R.w;
+    uint32_t *mbits = moff + lines;
+    uint16_t *off16 = reinterpret_cast<uint16_t *>(mbits + R.w);
+    uint8_t *cbpa = reinterpret_cast<uint8_t *>(off16 + NPC * R.w), *codea = cbpa + R.w;
+    const uint32_t *Mq = M + (size_t)q0 * NPC;
+    const uint4 *Bq = Bd + (size_t)q0 * NPC;
+
+    /* rect row: the records first */
+    for (int i0 = 0; i0 < npc; i0 += 4 * GW) {
+        uint32_t v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int i = i0 + t + GW * u;
+            v[u] = i < npc ? Mq[i] : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int i = i0 + t + GW * u;
+            if (i < npc) mt[i] = v[u];
+        }
+    }
+    for (int i0 = 0; i0 < 8 * nd; i0 += 4 * GW) {
+        uint32_t v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int i = i0 + t + GW * u, k = i >> 3, e = i & 7;
+            const int pcA = e < 4 ? 12 + e : (e < 6 ? 16 + e : 18 + e);
+            v[u] = i < 8 * nd && row > R.y0 ? M[(size_t)(q0 + k - R.w) * NPC + pcA] : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int i = i0 + t + GW * u;
+            if (i < 8 * nd) ma[i] = v[u];
+        }
+    }
     const int j = DF->nal;
     if (j < 0) return;
     if (t < 8) {
@@ -616,286 +712,313 @@ __global__ __launch_bounds__(WR_T) void k_dyn_len(DevStream *__restrict__ st, co
         L.wl[t] = pend[s].wl[t];
         L.wv[t] = pend[s].wv[t];
     }
-    for (int i = t; i < HDR_MAX / 32 + 2; i += WR_T) L.hdr[i] = 0u;
     if (t == 0) L.head_over = 0;
-    build_ptabs(*reinterpret_cast<const Tabs *>(&g_tabs), L.ptabs, t, WR_T);
+    build_ptabs(*reinterpret_cast<const Tabs *>(&g_tabs), L.ptabs, t, GW);
+    DevStream *S = st + s;
     const NalDesc d = nal[(size_t)s * ld_nal + j];
+    __syncthreads();                                        /* waypoint table, ptabs, records */
     const NalCtx c = nal_ctx(S, d, L.wo, L.wl, L.wv);
-    __syncthreads();
-    uint32_t F;
-    {
+    const HeadCtx H = head_ctx(c);
+    const int mbw = H.mbw, mbh = c.h / 16;
+    const Tabs &TB = g_tabs;
+    const PTabs &PT = L.ptabs;
+    const int ra = first ? 0 : (rect ? row : R.y0 + R.h), rb = first ? R.y0 : (rect ? row + 1 : mbh);
+    uint32_t F = 0;
+    if (first) {
         CountSink hc{0};
         emit_slice_header(hc, c);
         F = hc.n;
-        if (t == 0) {
-            LSink hs{{L.hdr}, 0, 0, 0};
-            hs.start(0);
-            emit_slice_header(hs, c);
-            hs.finish();
-        }
     }
-    const HeadCtx H = head_ctx(c);
     if (t < 12) {
         CapSink hc{0, 0, 0};
         H.put_class(hc, t);
+        L.hhi[t] = hc.hi;
+        L.hlo[t] = hc.lo;
         L.hlen[t] = hc.n;
         if (hc.over()) L.head_over = 1;
     }
     __syncthreads();
     const bool head_over = L.head_over;
-    const int mbw = H.mbw, mbh = c.h / 16;
-    const Rect R{g.x0, g.y0, g.w, g.h};
-    for (int r = t; r < mbh; r += WR_T) {
-        uint32_t b;
-        if (!head_over) {
-            b = row_static_bits(H, L.hlen, r, R);
-        } else {
-            b = 0;
-            for (int col = 0; col < mbw; ++col) {
-                if (r >= R.y0 && r < R.y0 + R.h && col >= R.x0 && col < R.x0 + R.w) continue;
-                CountSink cn{1};
-                H.put_slow(cn, r, col);
-                b += cn.n;
+    auto head_bits = [&](int r, int col) -> uint32_t {
+        if (!head_over) return L.hlen[H.sel(r, col)];
+        CountSink cn{0};
+        H.put_slow(cn, r, col);
+        return cn.n;
+    };
+
+    uint64_t bits = 0;                   /* the group's bits */
+    if (rect) {
+        /* pieces: coeff_token from the neighbours' TotalCoeff, length */
+        const uint32_t m26 = magic32(NPC);
+        for (int i = t; i < npc; i += GW) {
+            const int k = (int)div_m((uint32_t)i, m26), pc = i - k * NPC;
+            const int col = R.x0 + k;
+            const uint32_t mv = mt[i];
+            const int tc = tc_of(mv);
+            const uint32_t *mk = mt + k * NPC;
+            uint32_t tv = 0, tl = 0;
+            int nC = -1;
+            if (pc != 16 && pc != 17) {
+                const int nAe = col > 0 ? 0 : -1, nBe = row > 0 ? 0 : -1;
+                int nA, nB;
+                if (pc < 16) {
+                    const int bx = pc & 3, by = pc >> 2;
+                    nA = bx > 0 ? tc_of(mk[pc - 1]) : (k > 0 ? tc_of(mk[pc + 3 - NPC]) : nAe);
+                    nB = by > 0 ? tc_of(mk[pc - 4]) : (row > R.y0 ? tc_of(ma[8 * k + pc]) : nBe);
+                } else {
+                    const int b = (pc - 18) & 3, bx = b & 1, by = b >> 1;
+                    nA = bx > 0 ? tc_of(mk[pc - 1]) : (k > 0 ? tc_of(mk[pc + 1 - NPC]) : nAe);
+                    nB = by > 0 ? tc_of(mk[pc - 2])
+                                : (row > R.y0 ? tc_of(ma[8 * k + (pc < 22 ? pc - 14 : pc - 16)]) : nBe);
+                }
+                nC = nc_of(nA, nB);
+                const int t1 = (int)((mv >> 13) & 3u);
+                if (nC >= 8) {
+                    tv = tc ? (uint32_t)(((tc - 1) << 2) | t1) : 3u;
+                    tl = 6;
+                } else {
+                    const uint32_t e = PT.ct[nC < 2 ? 0 : (nC < 4 ? 1 : 2)][4 * tc + t1];
+                    tv = e & 255u;
+                    tl = e >> 8;
+                }
             }
+            uint32_t len = tl + (mv & 255u);
+            if (mv & M_OVF) len = ovf_bits(PT, TB, Bq[i], pc, nC);     /* rare: > 128-bit block */
+            lo[i] = len | tv << 11 | tl << 19 | (uint32_t)(nC + 1) << 24;
         }
-        L.rowbits[r] = b;
-    }
-    __syncthreads();
-    const size_t nb = (size_t)s * ld_fr + f;
-    const int ndt = R.w * R.h;
-    const uint32_t *M = meta + nb * (size_t)(NPC * ndt);
-    const uint4 *Bd = body + nb * (size_t)(NPC * ndt);
-    const uint32_t m_rw = magic32((uint32_t)R.w);
-    const Tabs &TB = g_tabs;
-    for (int q = t; q < ndt; q += WR_T) {
-        const int ry = (int)div_m((uint32_t)q, m_rw), cx = q - ry * R.w;
-        const int row = R.y0 + ry, col = R.x0 + cx;
-        uint32_t hb;
-        if (!head_over) {
-            hb = L.hlen[H.sel(row, col)];
-        } else {
-            CountSink cn{0};
-            H.put_slow(cn, row, col);
-            hb = cn.n;
+        __syncthreads();
+        if (stamps) stv[1] = __builtin_amdgcn_s_memrealtime();
+        /* per dynamic MB: cbp, its code, piece offsets, bits */
+        for (int k = t; k < nd; k += GW) {
+            const uint32_t *mk = mt + k * NPC;
+            int cbp_l = 0;
+#pragma unroll
+            for (int pc = 0; pc < 16; ++pc)
+                if (tc_of(mk[pc])) cbp_l |= 1 << (2 * (pc >> 3) + ((pc & 3) >> 1));
+            bool ac = false;
+#pragma unroll
+            for (int pc = 18; pc < NPC; ++pc) ac |= tc_of(mk[pc]) != 0;
+            const bool dc = (tc_of(mk[16]) | tc_of(mk[17])) != 0;
+            const int cbp_c = ac ? 2 : (dc ? 1 : 0);
+            const int cbp = cbp_l | cbp_c << 4;
+            const int code = TB.cbp_code[cbp];
+            CountSink hs{head_bits(row, R.x0 + k)};
+            put_ue(hs, (uint32_t)code);
+            if (cbp) put_se(hs, 0);                         /* mb_qp_delta */
+            uint32_t off = hs.n;
+            const uint32_t *lk = lo + k * NPC;
+            uint16_t *ok = off16 + k * NPC;
+#pragma unroll
+            for (int blk = 0; blk < 16; ++blk) {            /* luma4x4BlkIdx order */
+                const int r = blk_raster(blk);
+                const bool pres = (cbp_l >> (blk >> 2)) & 1;
+                ok[r] = pres ? (uint16_t)off : (uint16_t)0xffffu;
+                off += pres ? (lk[r] & LO_LEN) : 0u;
+            }
+#pragma unroll
+            for (int k2 = 16; k2 < NPC; ++k2) {             /* Cb DC, Cr DC, Cb AC 0-3, Cr AC 0-3 */
+                const bool pres = k2 < 18 ? cbp_c >= 1 : cbp_c == 2;
+                ok[k2] = pres ? (uint16_t)off : (uint16_t)0xffffu;
+                off += pres ? (lk[k2] & LO_LEN) : 0u;
+            }
+            mbits[k] = off;
+            cbpa[k] = (uint8_t)cbp;
+            codea[k] = (uint8_t)code;
         }
-        int cbp, code;
-        const uint32_t bits = dyn_mb_layout<false>(M, Bd, R, q, row, col, L.ptabs, TB, L.pl[t], nullptr,
-                                                   nullptr, hb, cbp, code);
-        atomicAdd(&L.rowbits[row], bits);
-    }
-    __syncthreads();
-    uint32_t *RS = rowst + nb * (size_t)ld_row;
-    uint32_t carry = F;
-    for (int r0 = 0; r0 < mbh; r0 += WR_T) {
-        const int r = r0 + t;
-        const uint32_t v = r < mbh ? L.rowbits[r] : 0u;
-        uint32_t ex, tot;
-        block_excl_sum(v, L.wsum, ex, tot);
-        if (r < mbh) {
-            RS[r] = carry + ex;
-            L.rowbits[r] = carry + ex;                      /* own entry: start of row r */
+        __syncthreads();
+        if (stamps) stv[2] = __builtin_amdgcn_s_memrealtime();
+        uint32_t carry = 0;
+        for (int c0 = 0; c0 < mbw; c0 += GW) {
+            const int col = c0 + t;
+            uint32_t len = 0;
+            if (col < mbw) {
+                const int k = col - R.x0;
+                len = (k >= 0 && k < R.w) ? mbits[k] : head_bits(row, col) + 1u;
+            }
+            const uint32_t incl = wave_incl_sum(len, t);
+            if (col < mbw) moff[col] = carry + incl - len;
+            carry += __shfl(incl, GW - 1, GW);
         }
-        carry += tot;
+        bits = carry;
+    } else {
+        /* rows without dynamic MBs: row offsets */
+        uint32_t carry = F;
+        for (int r0 = ra; r0 < rb; r0 += GW) {
+            const int r = r0 + t;
+            uint32_t len = 0;
+            if (r < rb) {
+                if (!head_over) {
+                    len = row_static_bits(H, L.hlen, r, R);
+                } else {
+                    for (int col = 0; col < mbw; ++col) len += head_bits(r, col) + 1u;
+                }
+            }
+            const uint32_t incl = wave_incl_sum(len, t);
+            if (r < rb) moff[r - ra] = carry + incl - len;
+            carry += __shfl(incl, GW - 1, GW);
+        }
+        bits = carry + (last ? 1u : 0u);
     }
-    const uint32_t end = carry;                             /* bit of rbsp_stop_one_bit */
-    uint8_t *slot = stage + nb * g.slot_bytes;
-    uint32_t *out = reinterpret_cast<uint32_t *>(slot);
-    const uint32_t cap_words = (uint32_t)((g.slot_bytes - DYN_OVF_BYTES) / 4) - 4u;
-    const bool over = (end >> 5) + 2u > cap_words;          /* uniform */
-    if (t == 0) {
-        RS[mbh] = end;
+
+    /* start bit from the groups before */
+    if (stamps) stv[3] = __builtin_amdgcn_s_memrealtime();
+    const uint64_t start = lb_lookback(status + nb * (size_t)ng, gi, epoch, bits, t);
+    if (stamps) stv[4] = __builtin_amdgcn_s_memrealtime();
+    const uint64_t end = start + bits;
+    uint32_t *out = reinterpret_cast<uint32_t *>(stage + nb * g.slot_bytes);
+    const uint64_t cap_words = (g.slot_bytes - DYN_OVF_BYTES) / 4 - 4;
+    const bool over = bits && ((end - 1) >> 5) + 2 > cap_words;
+    uint2 *sd = side + nb * (size_t)(2 * ng) + 2 * gi;
+    if (last && t == 0) {
         DF->ep = 0;
         DF->err = over ? DF_OVER : 0u;
-        DF->rbsp_bytes = over ? 0u : (end + 8u) >> 3;       /* bitwriter.c:103-111 */
+        DF->rbsp_bytes = over ? 0u : (uint32_t)((end + 7) >> 3);   /* bitwriter.c:103-111 */
         if (over) atomicOr((unsigned int *)&S->err, SCROLL_DEVERR_DYN);
     }
-    if (over) return;
-    /* words the writers OR into: header words (with the header), words two
-     * rows share (zero), the stop word (with the stop bit) */
-    const uint32_t hw = (F + 31u) >> 5, ew = end >> 5;
-    auto val = [&](uint32_t w) -> uint32_t {
-        return (w < hw ? L.hdr[w] : 0u) | (w == ew ? 0x80000000u >> (end & 31u) : 0u);
-    };
-    for (uint32_t w = (uint32_t)t; w < hw; w += WR_T) out[w] = __builtin_bswap32(val(w));
-    for (int r = t; r < mbh; r += WR_T) {
-        const uint32_t rs = L.rowbits[r];
-        if (r > 0 && (rs & 31u) && (rs >> 5) >= hw) out[rs >> 5] = __builtin_bswap32(val(rs >> 5));
+    const uint32_t rel0 = (uint32_t)(start & 31u);
+    const uint64_t w0 = start >> 5, wl = bits ? (end - 1) >> 5 : 0;
+    const uint32_t nw = (over || !bits) ? 0u : (uint32_t)(wl - w0 + 1);
+    const bool first_sh = nw && rel0, last_sh = nw && (end & 31u) && !(nw == 1 && rel0);
+    if (t == 0) {
+        if (!first_sh) sd[0] = make_uint2(SIDE_NONE, 0u);
+        if (!last_sh) sd[1] = make_uint2(SIDE_NONE, 0u);
     }
-    if (t == 0 && ew >= hw) out[ew] = __builtin_bswap32(val(ew));
-}
-
-struct WrLds {
-    uint32_t buf[WBUF_WORDS];
-    uint32_t tk[DYN_MAX_W][NPC];
-    uint16_t pl[DYN_MAX_W][NPC];
-    uint16_t po[DYN_MAX_W][NPC];
-    uint32_t moff[MAX_MBW];
-    uint32_t mbits[DYN_MAX_W];
-    uint8_t cbp[DYN_MAX_W], code[DYN_MAX_W];
-    uint32_t wsum[NW];
-    uint64_t hhi[3], hlo[3];
-    uint32_t hlen[3];
-    int32_t head_over;
-    int32_t wo[8], wl[8], wv[8];
-    PTabs ptabs;
-};
-
-/* grid (row groups, frames, streams): workgroup x writes MB rows x, x + gx, ... */
-__global__ __launch_bounds__(WR_T) void k_dyn_write(const DevStream *__restrict__ st,
-                                                    const NalDesc *__restrict__ nal, int ld_nal,
-                                                    const PlanPending *__restrict__ pend,
-                                                    const DynFrame *__restrict__ dfr, int ld_fr, DynGeom g,
-                                                    const uint32_t *__restrict__ meta,
-                                                    const uint4 *__restrict__ body,
-                                                    const uint32_t *__restrict__ rowst, int ld_row,
-                                                    uint8_t *__restrict__ stage)
-{
-    __shared__ WrLds L;
-    const int s = blockIdx.z, f = blockIdx.y, t = threadIdx.x;
-    const DynFrame df = dfr[(size_t)s * ld_fr + f];
-    if (df.nal < 0 || df.err) return;
-    if (t < 8) {
-        L.wo[t] = pend[s].wo[t];
-        L.wl[t] = pend[s].wl[t];
-        L.wv[t] = pend[s].wv[t];
-    }
-    build_ptabs(*reinterpret_cast<const Tabs *>(&g_tabs), L.ptabs, t, WR_T);
-    const NalDesc d = nal[(size_t)s * ld_nal + df.nal];
-    const NalCtx c = nal_ctx(st + s, d, L.wo, L.wl, L.wv);
-    const HeadCtx H = head_ctx(c);
-    const int mbw = H.mbw, mbh = c.h / 16;
-    const Rect R{g.x0, g.y0, g.w, g.h};
-    const size_t nb = (size_t)s * ld_fr + f;
-    const int ndt = R.w * R.h;
-    const uint32_t *M = meta + nb * (size_t)(NPC * ndt);
-    const uint4 *Bd = body + nb * (size_t)(NPC * ndt);
-    const uint32_t *RS = rowst + nb * (size_t)ld_row;
-    uint32_t *out = reinterpret_cast<uint32_t *>(stage + nb * g.slot_bytes);
-    const Tabs &TB = g_tabs;
-    const PTabs &PT = L.ptabs;
-
-    for (int row = blockIdx.x; row < mbh; row += gridDim.x) {
-        const uint32_t rs = RS[row], re = RS[row + 1];
-        if (t == 0) L.head_over = 0;
-        __syncthreads();                                    /* previous row done with L */
-        if (t < 3) {
-            CapSink hc{0, 0, 0};
-            H.put_class(hc, H.sel(row, 0) + t);
-            L.hhi[t] = hc.hi;
-            L.hlo[t] = hc.lo;
-            L.hlen[t] = hc.n;
-            if (hc.over()) L.head_over = 1;
-        }
+    for (uint32_t p0 = 0; p0 < nw; p0 += GBUF_WORDS) {
+        const uint32_t n = min((uint32_t)GBUF_WORDS, nw - p0);
+        for (uint32_t i = (uint32_t)t; i < n; i += GW) L.buf[i] = 0u;
         __syncthreads();
-        const bool head_over = L.head_over;
-        const bool in = row >= R.y0 && row < R.y0 + R.h;
-        const int nd = in ? R.w : 0;
-        auto head_bits = [&](int col) -> uint32_t {
-            if (!head_over) return L.hlen[col == 0 ? 0 : (col == mbw - 1 ? 2 : 1)];
-            CountSink cn{0};
-            H.put_slow(cn, row, col);
-            return cn.n;
-        };
-        for (int k = t; k < nd; k += WR_T) {
-            const int col = R.x0 + k, q = (row - R.y0) * R.w + k;
-            int cbp, code;
-            L.mbits[k] = dyn_mb_layout<true>(M, Bd, R, q, row, col, PT, TB, L.pl[k], L.tk[k], L.po[k],
-                                             head_bits(col), cbp, code);
-            L.cbp[k] = (uint8_t)cbp;
-            L.code[k] = (uint8_t)code;
-        }
-        __syncthreads();
-        {
-            uint32_t carry = 0;
-            for (int c0 = 0; c0 < mbw; c0 += WR_T) {
-                const int col = c0 + t;
-                uint32_t len = 0;
-                if (col < mbw) {
-                    const int k = col - R.x0;
-                    len = (in && k >= 0 && k < R.w) ? L.mbits[k] : head_bits(col) + 1u;
-                }
-                uint32_t ex, tot;
-                block_excl_sum(len, L.wsum, ex, tot);
-                if (col < mbw) L.moff[col] = carry + ex;
-                carry += tot;
-            }
-        }
-        const uint32_t rel0 = rs & 31u, w0 = rs >> 5;
-        const uint32_t nw = (rel0 + (re - rs) + 31u) >> 5;
-        for (uint32_t p0 = 0; p0 < nw; p0 += WBUF_WORDS) {
-            const uint32_t n = min((uint32_t)WBUF_WORDS, nw - p0);
-            for (uint32_t i = (uint32_t)t; i < n; i += WR_T) L.buf[i] = 0u;
-            __syncthreads();
-            const LdsOrWin win{L.buf, p0, n};
-            for (int col = t; col < mbw; col += WR_T) {
+        const LdsOrWin win{L.buf, p0, n};
+        if (rect) {
+            for (int col = t; col < mbw; col += GW) {
                 WSink sk{win, 0, 0, 0};
-                sk.start(rel0 + L.moff[col]);
+                sk.start(rel0 + moff[col]);
                 if (!head_over) {
-                    const int pos = col == 0 ? 0 : (col == mbw - 1 ? 2 : 1);
-                    sk.put_cap(CapSink{L.hhi[pos], L.hlo[pos], L.hlen[pos]});
+                    const int cls = H.sel(row, col);
+                    sk.put_cap(CapSink{L.hhi[cls], L.hlo[cls], L.hlen[cls]});
                 } else {
                     H.put_slow(sk, row, col);
                 }
                 const int k = col - R.x0;
-                if (!(in && k >= 0 && k < R.w)) {
+                if (!(k >= 0 && k < R.w)) {
                     sk.put(1, 1);                           /* coded_block_pattern ue(0) */
                 } else {
-                    put_ue(sk, (uint32_t)L.code[k]);
-                    if (L.cbp[k]) put_se(sk, 0);
+                    put_ue(sk, (uint32_t)codea[k]);
+                    if (cbpa[k]) put_se(sk, 0);
                 }
                 sk.finish();
             }
-            for (int i = t; i < NPC * nd; i += WR_T) {
-                const int k = i / NPC, pc = i - k * NPC;
-                const uint32_t o = L.po[k][pc];
-                if (o == 0xffffu) continue;
-                const uint32_t tkv = L.tk[k][pc], len = L.pl[k][pc] & PL_LEN;
-                const int tl = (int)((tkv >> 16) & 31u), nC = (int)((tkv >> 21) & 31u) - 1;
-                const uint32_t bl = len - (uint32_t)tl;
-                uint4 bd = make_uint4(0, 0, 0, 0);
-                const size_t bi = (size_t)((row - R.y0) * R.w + k) * NPC + pc;
-                if (bl || (tkv & TK_OVF)) bd = Bd[bi];
+            const uint32_t m26 = magic32(NPC);
+            for (int i0 = 0; i0 < npc; i0 += 4 * GW) {
+                uint4 bd[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {               /* four body loads in flight */
+                    const int i = i0 + t + GW * u;
+                    bd[u] = make_uint4(0, 0, 0, 0);
+                    if (i < npc && off16[i] != 0xffffu && (mt[i] & (255u | M_OVF))) bd[u] = Bq[i];
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int i = i0 + t + GW * u;
+                    if (i >= npc) continue;
+                    const uint32_t o = off16[i];
+                    if (o == 0xffffu) continue;
+                    const int k = (int)div_m((uint32_t)i, m26), pc = i - k * NPC;
+                    const uint32_t e = lo[i], mv = mt[i];
+                    const int tl = (int)((e >> 19) & 31u), nC = (int)((e >> 24) & 31u) - 1;
+                    const uint32_t pos = rel0 + moff[R.x0 + k] + o;
+                    if (!(mv & M_OVF)) {
+                        WSink sk{win, 0, 0, 0};
+                        sk.start(pos);
+                        if (nC != -1) sk.put((e >> 11) & 255u, tl);
+                        sk.put_cap(CapSink{(uint64_t)bd[u].z | (uint64_t)bd[u].w << 32,
+                                           (uint64_t)bd[u].x | (uint64_t)bd[u].y << 32, mv & 255u});
+                        sk.finish();
+                    } else {
+                        ovf_put(L.buf, p0, n, pos, PT, TB, bd[u], pc, nC);
+                    }
+                }
+            }
+        } else {
+            if (first && t == 0) {                          /* slice header, h264_writer.c:549-553 */
+                WSink hs{win, 0, 0, 0};
+                hs.start(0);
+                emit_slice_header(hs, c);
+                hs.finish();
+            }
+            const int nm = (rb - ra) * mbw;
+            const uint32_t m_mbw = magic32((uint32_t)mbw);
+            for (int m = t; m < nm; m += GW) {
+                const int rr = (int)div_m((uint32_t)m, m_mbw), col = m - rr * mbw, r = ra + rr;
+                uint32_t off = moff[rr];
                 WSink sk{win, 0, 0, 0};
-                sk.start(rel0 + L.moff[R.x0 + k] + o);
-                if (!(tkv & TK_OVF)) {
-                    if (pc != 16 && pc != 17) sk.put(tkv & 0xffffu, tl);
-                    sk.put_cap(CapSink{(uint64_t)bd.z | (uint64_t)bd.w << 32,
-                                       (uint64_t)bd.x | (uint64_t)bd.y << 32, bl});
-                } else if (pc == 16 || pc == 17) {
-                    const int dq[4] = {(int)(int16_t)(bd.x & 0xffffu), (int)(int16_t)(bd.x >> 16),
-                                       (int)(int16_t)(bd.y & 0xffffu), (int)(int16_t)(bd.y >> 16)};
-                    cavlc_dc4(sk, PT, dq);
+                if (!head_over) {
+                    const int b3 = H.sel(r, 0);
+                    off += col == 0 ? 0u : L.hlen[b3] + 1u + (uint32_t)(col - 1) * (L.hlen[b3 + 1] + 1u);
+                    const int cls = b3 + (col == 0 ? 0 : (col == mbw - 1 ? 2 : 1));
+                    sk.start(rel0 + off);
+                    sk.put_cap(CapSink{L.hhi[cls], L.hlo[cls], L.hlen[cls]});
                 } else {
-                    const int8_t *lvp = reinterpret_cast<const int8_t *>(&bd);
-                    cavlc_block(sk, TB, lvp, pc < 16 ? 16 : 15, nC);
+                    for (int c2 = 0; c2 < col; ++c2) off += head_bits(r, c2) + 1u;
+                    sk.start(rel0 + off);
+                    H.put_slow(sk, r, col);
                 }
+                sk.put(1, 1);                               /* coded_block_pattern ue(0) */
                 sk.finish();
             }
-            __syncthreads();
-            for (uint32_t i = (uint32_t)t; i < n; i += WR_T) {
-                const uint32_t gw = w0 + p0 + i, v = L.buf[i];
-                if ((gw == w0 && rel0) || gw == (re >> 5)) {
-                    if (v) atomicOr(&out[gw], __builtin_bswap32(v));
-                } else {
-                    out[gw] = __builtin_bswap32(v);
-                }
+            if (last && t == 0) {                           /* rbsp_stop_one_bit */
+                WSink sk{win, 0, 0, 0};
+                sk.start(rel0 + (uint32_t)bits - 1u);
+                sk.put(1, 1);
+                sk.finish();
             }
         }
+        __syncthreads();
+        for (uint32_t i = (uint32_t)t; i < n; i += GW) {
+            const uint32_t q = p0 + i, v = L.buf[i];
+            const uint64_t gw = w0 + q;
+            if (q == 0 && first_sh) sd[0] = make_uint2((uint32_t)gw, v);
+            else if (q == nw - 1 && last_sh) sd[1] = make_uint2((uint32_t)gw, v);
+            else out[gw] = __builtin_bswap32(v);
+        }
+        __syncthreads();
+    }
+    if (stamps && t == 0) {
+        stv[5] = __builtin_amdgcn_s_memrealtime();
+        uint64_t *o = stamps + (((size_t)s * gridDim.y + f) * ng + gi) * 8;
+        for (int k2 = 0; k2 < 6; ++k2) o[k2] = stv[k2];
+        o[6] = bits;
+        o[7] = (uint64_t)(uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 4);     /* HW_ID */
     }
 }
 
-/* grid (frames, streams): EP positions (slot tail, unsorted) and count */
+/* grid (frames, streams): merges the side entries of k_dyn_group into the
+ * staged words, then EP positions (slot tail, unsorted) and count */
 __global__ __launch_bounds__(WR_T) void k_dyn_ep(DynFrame *__restrict__ dfr, int ld_fr, DynGeom g,
-                                                 const uint8_t *__restrict__ stage)
+                                                 const uint2 *__restrict__ side, int nside,
+                                                 uint8_t *__restrict__ stage)
 {
-    __shared__ int32_t wmax[NW];
+    __shared__ int32_t wmax[WR_NW];
+    __shared__ uint2 se[2 * (DYN_MAX_H + 2)];
     const int s = blockIdx.y, f = blockIdx.x, t = threadIdx.x, lane = t & 63;
     DynFrame *DF = dfr + (size_t)s * ld_fr + f;
     const DynFrame df = *DF;
     if (df.nal < 0 || df.err) return;
     const size_t nb = (size_t)s * ld_fr + f;
-    const uint8_t *in = stage + nb * g.slot_bytes;
-    uint32_t *eplist = reinterpret_cast<uint32_t *>(const_cast<uint8_t *>(in) + g.slot_bytes - DYN_OVF_BYTES);
+    uint8_t *in = stage + nb * g.slot_bytes;
+    uint32_t *iw = reinterpret_cast<uint32_t *>(in);
+    if (t < nside) se[t] = side[nb * (size_t)nside + t];
+    __syncthreads();
+    if (t < nside && se[t].x != SIDE_NONE) {
+        bool lead = true;
+        for (int e = 0; e < t; ++e) lead = lead && se[e].x != se[t].x;
+        if (lead) {
+            uint32_t v = 0;
+            for (int e = t; e < nside; ++e) v |= se[e].x == se[t].x ? se[e].y : 0u;
+            iw[se[t].x] = __builtin_bswap32(v);
+        }
+    }
+    __syncthreads();                    /* stores reach L2 before the barrier; no L1 line is stale */
+    uint32_t *eplist = reinterpret_cast<uint32_t *>(in + g.slot_bytes - DYN_OVF_BYTES);
     const uint32_t nin = df.rbsp_bytes;
     int carry = -1;
     for (uint32_t i0 = 0; i0 < nin; i0 += WR_T * 16) {
@@ -908,7 +1031,7 @@ __global__ __launch_bounds__(WR_T) void k_dyn_ep(DynFrame *__restrict__ dfr, int
         for (int i = 0; i < 16; ++i)
             if ((uint32_t)i < n && ((wv[i >> 2] >> (8 * (i & 3))) & 255u)) lnz = (int)(ib + i);
         int ex, tot;
-        block_excl_max(lnz, wmax, ex, tot);
+        block_excl_max<WR_NW>(lnz, wmax, ex, tot);
         int prev = max(carry, ex);
         uint32_t ins = 0;
 #pragma unroll
@@ -1244,28 +1367,27 @@ int dyn_launch_code(hipStream_t hs, int nframes, int S, const DevStream *st, con
                        *g, x->rows);
     if (hipGetLastError() != hipSuccess) return -1;
     const int nchunk = (24 * g->w * g->h + CODE_T - 1) / CODE_T;
-    hipLaunchKernelGGL(k_dyn_code<false>, dim3(nchunk, nframes, S), dim3(CODE_T), 0, hs, st, dfr, ld_fr,
+    hipLaunchKernelGGL(k_dyn_code, dim3(nchunk, nframes, S), dim3(CODE_T), 0, hs, st, dfr, ld_fr,
                        pend, nal, ld_nal, *g, x->rows, src, refs, x->meta, x->body);
     if (hipGetLastError() != hipSuccess) return -1;
-    hipLaunchKernelGGL(k_dyn_code<true>, dim3(nchunk, nframes, S), dim3(CODE_T), 0, hs, st, dfr, ld_fr,
-                       pend, nal, ld_nal, *g, x->rows, src, refs, x->meta, x->body);
+    hipLaunchKernelGGL(k_dyn_code_general, dim3(nchunk, 1, S), dim3(CODE_T), 0, hs, st, dfr, ld_fr,
+                       pend, nal, ld_nal, *g, x->rows, src, refs, x->meta, x->body, nframes);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 int dyn_launch_pack(hipStream_t hs, int nframes, int S, DevStream *st, const NalDesc *nal,
                     int ld_nal, const PlanPending *pend, DynFrame *dfr, int ld_fr,
-                    const DynGeom *g, const DynScratch *x, uint8_t *stage)
+                    const DynGeom *g, const DynScratch *x, uint8_t *stage, uint32_t epoch,
+                    uint64_t *stamps, int mbw, int mbh)
 {
     if (nframes <= 0 || S <= 0) return 0;
-    const int mbh = x->ld_row - 1;
-    hipLaunchKernelGGL(k_dyn_len, dim3(nframes, S), dim3(WR_T), 0, hs, st, nal, ld_nal, pend, dfr, ld_fr,
-                       *g, x->meta, x->body, x->rowst, x->ld_row, stage);
+    const int ng = g->h + 2;
+    const int lines = mbw > mbh ? mbw : mbh;
+    hipLaunchKernelGGL(k_dyn_group, dim3(ng, nframes, S), dim3(GW), group_lds_bytes(g->w, lines), hs, st, nal,
+                       ld_nal, pend, dfr, ld_fr, *g, x->meta, x->body, x->status, x->side, epoch, lines,
+                       stage, stamps);
     if (hipGetLastError() != hipSuccess) return -1;
-    const int gx = (mbh + WR_ROWS - 1) / WR_ROWS;
-    hipLaunchKernelGGL(k_dyn_write, dim3(gx, nframes, S), dim3(WR_T), 0, hs, st, nal, ld_nal, pend, dfr,
-                       ld_fr, *g, x->meta, x->body, x->rowst, x->ld_row, stage);
-    if (hipGetLastError() != hipSuccess) return -1;
-    hipLaunchKernelGGL(k_dyn_ep, dim3(nframes, S), dim3(WR_T), 0, hs, dfr, ld_fr, *g, stage);
+    hipLaunchKernelGGL(k_dyn_ep, dim3(nframes, S), dim3(WR_T), 0, hs, dfr, ld_fr, *g, x->side, 2 * ng, stage);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -1227,18 +1227,17 @@ static int launch(ScrollBatch *b, int nframes, int plan_mode, int nal_max, hipSt
         HIPCHK(hipGetLastError());
         if ((rc = mark(1))) return rc;
         uint64_t *stamps = nullptr;
-        if (b->debug & SCROLL_DEBUG_DYN_STAMPS) {   /* k_dyn_stage's, then k_dyn_emit's */
-            const size_t slots = 2 * (size_t)nframes * S;
+        if (b->debug & SCROLL_DEBUG_DYN_STAMPS) {   /* k_dyn_emit_gather's, then k_dyn_group's */
+            const size_t slots = (2 + (size_t)b->geo.h + 2) * (size_t)nframes * S;
             if (slots > b->dbg_slots) {
                 if (b->d_dbg) (void)hipFree(b->d_dbg);
                 HIPCHK(hipMalloc(&b->d_dbg, slots * 8 * sizeof(uint64_t)));
                 b->dbg_slots = slots;
             }
             HIPCHK(hipMemsetAsync(b->d_dbg, 0, slots * 8 * sizeof(uint64_t), hs));
-            stamps = b->d_dbg;      /* k_dyn_emit_gather writes past the first half */
+            stamps = b->d_dbg + 2 * (size_t)nframes * S * 8;
         }
         b->geo.debug = b->debug;
-        (void)stamps;
         if (hint) {
             if (hint_launch_stage(hs, nframes, S, b->d_st, b->d_nal, b->ld_nal, b->d_pend,
                                   b->d_dfr, ld_fr, b->d_hf, b->d_pool, b->d_stage,
@@ -1254,8 +1253,10 @@ static int launch(ScrollBatch *b, int nframes, int plan_mode, int nal_max, hipSt
                 return SCROLL_ERR_HIP;
             }
             if ((rc = mark(6))) return rc;
+            b->dx.epoch = b->dx.epoch % 0xffffffu + 1u;    /* look-back epoch, never 0 */
             if (dyn_launch_pack(hs, nframes, S, b->d_st, b->d_nal, b->ld_nal, b->d_pend, b->d_dfr,
-                                ld_fr, &b->geo, &b->dx, b->d_stage)) {
+                                ld_fr, &b->geo, &b->dx, b->d_stage, b->dx.epoch, stamps,
+                                b->dyn_pw / 16, b->dyn_ph / 16)) {
                 set_err("k_dyn_pack launch: %s", hipGetErrorString(hipGetLastError()));
                 return SCROLL_ERR_HIP;
             }
@@ -1508,7 +1509,8 @@ static void dyn_release(ScrollBatch *b)
     (void)hipFree(b->dx.rows);
     (void)hipFree(b->dx.meta);
     (void)hipFree(b->dx.body);
-    (void)hipFree(b->dx.rowst);
+    (void)hipFree(b->dx.status);
+    (void)hipFree(b->dx.side);
     b->d_dfr = nullptr;
     b->d_src = b->d_refs = b->d_stage = nullptr;
     b->dx = DynScratch{};
@@ -1574,8 +1576,10 @@ int scroll_batch_set_dyn_rect(ScrollBatch *b, int x0, int y0, int w, int h, size
     if (e == hipSuccess) e = hipMalloc(&b->dx.rows, S * F * 32 * h * sizeof(uint32_t));
     if (e == hipSuccess) e = hipMalloc(&b->dx.meta, S * F * DYN_PIECES * w * h * sizeof(uint32_t));
     if (e == hipSuccess) e = hipMalloc(&b->dx.body, S * F * DYN_PIECES * w * h * sizeof(uint4));
-    if (e == hipSuccess) e = hipMalloc(&b->dx.rowst, S * F * (mbh + 1) * sizeof(uint32_t));
-    b->dx.ld_row = mbh + 1;
+    if (e == hipSuccess) e = hipMalloc(&b->dx.status, S * F * (h + 2) * sizeof(unsigned long long));
+    if (e == hipSuccess) e = hipMalloc(&b->dx.side, S * F * 2 * (h + 2) * sizeof(uint2));
+    if (e == hipSuccess) e = hipMemset(b->dx.status, 0, S * F * (h + 2) * sizeof(unsigned long long));
+    b->dx.epoch = 0;
     if (e == hipSuccess) e = hipMemset(b->d_dfr, 0, S * F * sizeof(DynFrame));
     if (e == hipSuccess) e = hipMemset(b->d_src, 0, S * g.src_ld);
     if (e == hipSuccess) e = hipMemset(b->d_refs, 0, S * dyn_pair_bytes(b));

@@ -44,6 +44,7 @@ __device__ inline uint32_t wave_incl_sum(uint32_t v, int lane)
 
 /* exclusive prefix max over the workgroup (identity -1) and the total;
  * ends with a barrier so `ws` can be reused */
+template <int NWV = NW>
 __device__ inline void block_excl_max(int v, int *ws, int &excl, int &tot)
 {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -54,7 +55,7 @@ __device__ inline void block_excl_max(int v, int *ws, int &excl, int &tot)
     __syncthreads();
     int pm = -1, t = -1;
 #pragma unroll
-    for (int w = 0; w < NW; ++w) {
+    for (int w = 0; w < NWV; ++w) {
         if (w < wave) pm = max(pm, ws[w]);
         t = max(t, ws[w]);
     }
@@ -63,6 +64,7 @@ __device__ inline void block_excl_max(int v, int *ws, int &excl, int &tot)
     __syncthreads();
 }
 
+template <int NWV = NW>
 __device__ inline void block_excl_sum(uint32_t v, uint32_t *ws, uint32_t &excl, uint32_t &tot)
 {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -71,7 +73,7 @@ __device__ inline void block_excl_sum(uint32_t v, uint32_t *ws, uint32_t &excl, 
     __syncthreads();
     uint32_t pm = 0, t = 0;
 #pragma unroll
-    for (int w = 0; w < NW; ++w) {
+    for (int w = 0; w < NWV; ++w) {
         if (w < wave) pm += ws[w];
         t += ws[w];
     }

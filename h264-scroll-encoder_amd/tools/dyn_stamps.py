@@ -1,16 +1,17 @@
 #!/usr/bin/env python3
-"""dyn_stamps.py -- profiling aid: where k_dyn_stage's time goes.
+"""dyn_stamps.py -- profiling aid: where k_dyn_group's time goes.
 
 Runs the bench's config-3 workload (bench.py p720dyn) once with
-SCROLL_DEBUG_DYN_STAMPS and prints, per dynamic NAL (one workgroup), the
-s_memtime cycles spent in each window phase:
-  A  residual -> transform -> quant -> levels / TotalCoeff
-  B  nC + CAVLC encode into registers, chroma DC
-  C  MB heads, piece offsets, window scan
-  D  bits -> LDS buffer
-  E  flush to the staging slot + EP count
-plus the number of windows and the workgroup's total.  Then times the
-workload without stamps (HIP events).
+SCROLL_DEBUG_DYN_STAMPS and prints, per row-group workgroup of k_dyn_group
+(rect rows and the two static groups separately), the s_memrealtime span
+(100 MHz, microseconds) of each phase:
+  load+tok   records loaded, coeff_token / lengths of the pieces
+  mb         cbp, piece offsets per dynamic MB
+  scan       MB offsets of the row (static groups: row offsets)
+  lookback   waiting for the groups before (decoupled look-back)
+  write      bits -> LDS -> staging words
+plus the k_dyn_emit_gather workgroup spans.  Then times the workload
+without stamps (HIP events).
 
     python h264-scroll-encoder_amd/tools/dyn_stamps.py [--streams 256 --frames 16]
 """
@@ -57,7 +58,7 @@ def main():
         b.compose(F, rewind=True)
     assert b.sync() == 0, hs.last_error()
     ms, n = b.kernel_stats_ex()
-    print("kernel ms per compose: plan %.4f  emit %.4f  dyn_stage %.4f  dyn_emit %.4f"
+    print("kernel ms per compose: plan %.4f  emit %.4f  dyn_stage %.4f  dyn_emit %.4f  dyn_code %.4f  dyn_pack %.4f"
           % tuple(x / n for x in ms))
     b.enable_timing(False)
 
@@ -80,20 +81,34 @@ def main():
     b.set_debug(hs.SCROLL_DEBUG_DYN_STAMPS)
     b.compose(F, rewind=True)
     assert b.sync() == 0, hs.last_error()
-    buf = (ctypes.c_uint64 * (2 * S * F * 8))()
-    got = hs.lib.scroll_batch_debug_stamps(b.h, buf, 2 * S * F)
+    ng = rect[3] + 2
+    nslot = (2 + ng) * S * F
+    buf = (ctypes.c_uint64 * (nslot * 8))()
+    got = hs.lib.scroll_batch_debug_stamps(b.h, buf, nslot)
     allst = np.frombuffer(buf, dtype=np.uint64).reshape(-1, 8)[:got]
-    a = allst[:S * F].astype(np.float64)
-    names = ["A levels", "B cavlc", "C offsets", "D bits", "E flush"]
-    tot = a[:, 6].mean()
-    print(f"{S * F} NALs, windows/NAL {a[:, 5].mean():.1f}, cycles/NAL {tot:.0f} "
-          f"(min {a[:, 6].min():.0f} max {a[:, 6].max():.0f})")
-    for k, nm in enumerate(names):
-        m = a[:, k].mean()
-        print(f"  {nm:10s} {m:10.0f} cycles/NAL  {m / a[:, 5].mean():8.0f} /window  {100 * m / tot:5.1f} %")
-    rest = tot - a[:, :5].sum(1).mean()
-    print(f"  {'setup+tail':10s} {rest:10.0f} cycles/NAL  {100 * rest / tot:5.1f} %")
-    e = allst[S * F:].astype(np.int64)          # k_dyn_emit_gather: realtime (100 MHz)
+    grp = allst[2 * S * F:].astype(np.int64).reshape(S * F, ng, 8)
+    names = ["load+tok", "mb", "scan", "lookback", "write"]
+    for label, sel in (("rect rows", slice(1, ng - 1)), ("group 0", slice(0, 1)), ("last group", slice(ng - 1, ng))):
+        gsel = grp[:, sel].reshape(-1, 8)
+        gsel = gsel[gsel[:, 5] > 0]
+        st = gsel[:, :6].astype(np.float64)
+        tot = (st[:, 5] - st[:, 0]) / 100.0
+        print(f"{label}: {len(gsel)} WGs, duration mean {tot.mean():.2f} us p50 {np.percentile(tot, 50):.2f} "
+              f"p99 {np.percentile(tot, 99):.2f}, bits mean {gsel[:, 6].mean():.0f}")
+        prev = st[:, 0]
+        for k, nm in enumerate(names):
+            cur = st[:, k + 1]
+            cur = np.where(cur > 0, cur, prev)
+            d = (cur - prev) / 100.0
+            print(f"  {nm:9s} mean {d.mean():7.2f} us  p99 {np.percentile(d, 99):7.2f}")
+            prev = cur
+    g0 = grp[:, :, 0][grp[:, :, 5] > 0]
+    t0, t1 = g0.min(), grp[:, :, 5].max()
+    print(f"k_dyn_group span {(t1 - t0) / 100.0:.1f} us")
+    ends = grp[:, :, 5][grp[:, :, 5] > 0]
+    conc = [int(np.sum((g0 <= x) & (ends > x))) for x in np.linspace(t0, t1, 12)]
+    print("  resident WGs over time:", conc)
+    e = allst[S * F:2 * S * F].astype(np.int64)  # k_dyn_emit_gather: realtime (100 MHz)
     e = e[e[:, 0] > 0]
     if len(e):
         t0 = e[:, 0].min()

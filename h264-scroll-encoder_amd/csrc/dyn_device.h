@@ -534,7 +534,7 @@ __device__ __host__ inline void coeff_token(const Tabs &T, int tc, int t1, int n
 }
 
 /* CAVLC tables packed (len << 8 | bits) for one LDS read per field */
-struct PTabs {
+struct alignas(16) PTabs {
     uint16_t ct[4][68];           /* [0..2]: nC tables, [3]: chroma DC (nC = -1) */
     uint16_t tz[15][16];
     uint16_t tzdc[3][4];
@@ -554,6 +554,24 @@ __device__ __host__ inline void build_ptabs(const Tabs &T, PTabs &P, int tid, in
     for (int i = tid; i < 7 * 16; i += nthr)
         P.rb[i / 16][i % 16] = i % 16 < 15 ? (uint16_t)(T.rb_len[i / 16][i % 16] << 8 | T.rb_bits[i / 16][i % 16])
                                            : (uint16_t)0;
+}
+
+/* the same at compile time (kernels copy it into LDS with 16-byte loads) */
+constexpr PTabs make_ptabs(const Tabs &T)
+{
+    PTabs P{};
+    for (int i = 0; i < 3 * 68; ++i)
+        P.ct[i / 68][i % 68] = (uint16_t)(T.ct_len[i / 68][i % 68] << 8 | T.ct_bits[i / 68][i % 68]);
+    for (int i = 0; i < 68; ++i)
+        P.ct[3][i] = i < 20 ? (uint16_t)(T.ctdc_len[i] << 8 | T.ctdc_bits[i]) : (uint16_t)0;
+    for (int i = 0; i < 15 * 16; ++i)
+        P.tz[i / 16][i % 16] = (uint16_t)(T.tz_len[i / 16][i % 16] << 8 | T.tz_bits[i / 16][i % 16]);
+    for (int i = 0; i < 12; ++i)
+        P.tzdc[i / 4][i % 4] = (uint16_t)(T.tzdc_len[i / 4][i % 4] << 8 | T.tzdc_bits[i / 4][i % 4]);
+    for (int i = 0; i < 7 * 16; ++i)
+        P.rb[i / 16][i % 16] = i % 16 < 15 ? (uint16_t)(T.rb_len[i / 16][i % 16] << 8 | T.rb_bits[i / 16][i % 16])
+                                           : (uint16_t)0;
+    return P;
 }
 
 /* level_prefix / level_suffix as one field, branch-free (9.2.2.1) */

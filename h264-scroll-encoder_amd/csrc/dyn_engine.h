@@ -11,10 +11,10 @@
 /* all return 0, or -1 when the launch failed */
 /* per-batch scratch of the dynamic-rect coder: prediction
  * rows (32 h u32 per NAL), block records (DYN_PIECES per dynamic MB: a u32
- * meta word and a 16-byte body) */
+ * meta half-word and a 16-byte body) */
 typedef struct {
     uint32_t *rows;
-    uint32_t *meta;
+    uint16_t *meta;
     uint4 *body;
     unsigned long long *status;     /* k_dyn_group look-back: per (frame, row group) */
     uint2 *side;                    /* k_dyn_group -> k_dyn_ep: shared boundary words */

@@ -32,6 +32,16 @@ using namespace scroll::stage;
 namespace {
 
 __constant__ Tabs g_tabs = SCROLL_DYN_TABS;
+constexpr Tabs k_tabs = SCROLL_DYN_TABS;
+__constant__ PTabs g_ptabs = make_ptabs(k_tabs);
+
+/* packed CAVLC tables -> LDS, one 16-byte load per thread */
+__device__ inline void load_ptabs(PTabs &dst, int t, int nthr)
+{
+    constexpr int N = (int)(sizeof(PTabs) / 16);
+    static_assert(sizeof(PTabs) % 16 == 0, "PTabs copies as uint4");
+    for (int i = t; i < N; i += nthr) reinterpret_cast<uint4 *>(&dst)[i] = reinterpret_cast<const uint4 *>(&g_ptabs)[i];
+}
 
 
 constexpr int HEAD_MAX = 160;           /* bits of one MB head (huge mvd: 2 x 63 + ref) */
@@ -81,7 +91,7 @@ __device__ inline NalCtx nal_ctx(const DevStream *S, const NalDesc &d, const int
 /*                                                                         */
 /* Records of dynamic MB q (rect raster order) of NAL n, piece pc:          */
 /*   0..15 luma 4x4 (raster), 16 / 17 Cb / Cr DC, 18 + 4p + b chroma AC    */
-/*   (plane p, raster b): meta[n][q][pc] = body bits | TotalCoeff << 8 |   */
+/*   (plane p, raster b): meta[n][q][pc] (u16) = body bits | TotalCoeff << 8 | */
 /*   TrailingOnes << 13 | ovf << 15, body[n][q][pc] = the body right-      */
 /*   aligned in 128 bits (x = bits 0..31 .. w = bits 96..127); DC pieces   */
 /*   hold the whole block.  ovf: more than 128 bits -- body holds the      */
@@ -182,7 +192,7 @@ __device__ inline void code_frame(const DevStream *__restrict__ st,
                                                      DynGeom g, const uint32_t *__restrict__ rows,
                                                      const uint8_t *__restrict__ src,
                                                      const uint8_t *__restrict__ refs,
-                                                     uint32_t *__restrict__ meta, uint4 *__restrict__ body,
+                                                     uint16_t *__restrict__ meta, uint4 *__restrict__ body,
                                                      int s, int f, int bx)
 {
     __shared__ uint4 lv[CODE_T];
@@ -195,7 +205,7 @@ __device__ inline void code_frame(const DevStream *__restrict__ st,
     const DynFrame df = dfr[(size_t)s * ld_fr + f];
     if (df.nal < 0) return;
     if (GENERAL != ((df.err & DF_GENERAL) != 0)) return;
-    build_ptabs(*reinterpret_cast<const Tabs *>(&g_tabs), ptabs, t, CODE_T);
+    load_ptabs(ptabs, t, CODE_T);
     if (GENERAL && t < 8) {
         wo[t] = pend[s].wo[t];
         wv[t] = pend[s].wv[t];
@@ -213,7 +223,7 @@ __device__ inline void code_frame(const DevStream *__restrict__ st,
     const int lstride = 16 * g.w, cstride = 8 * g.w;
     const uint8_t *fcb = fs + (size_t)256 * ndt, *fcr = fcb + (size_t)64 * ndt;
     const uint32_t m_rw = magic32((uint32_t)g.w);
-    uint32_t *M = meta + nb * (size_t)(NPC * ndt);
+    uint16_t *M = meta + nb * (size_t)(NPC * ndt);
     uint4 *B = body + nb * (size_t)(NPC * ndt);
 
     const bool luma = task < 16 * ndt;
@@ -331,12 +341,12 @@ __device__ inline void code_frame(const DevStream *__restrict__ st,
             const int tc = cavlc_dc4(cap, ptabs, dq);
             const size_t idx = (size_t)k * NPC + 16 + p;
             if (cap.n <= 128) {
-                M[idx] = cap.n | (uint32_t)tc << 8;
+                M[idx] = (uint16_t)(cap.n | (uint32_t)tc << 8);
                 if (cap.n)
                     B[idx] = make_uint4((uint32_t)cap.lo, (uint32_t)(cap.lo >> 32), (uint32_t)cap.hi,
                                         (uint32_t)(cap.hi >> 32));
             } else {
-                M[idx] = (uint32_t)tc << 8 | M_OVF;
+                M[idx] = (uint16_t)((uint32_t)tc << 8 | M_OVF);
                 B[idx] = make_uint4(((uint32_t)dq[0] & 0xffffu) | (uint32_t)dq[1] << 16,
                                     ((uint32_t)dq[2] & 0xffffu) | (uint32_t)dq[3] << 16, 0u, 0u);
             }
@@ -379,12 +389,12 @@ __device__ inline void code_frame(const DevStream *__restrict__ st,
     bool ok;
     const int tc = cavlc_body(cap, ptabs, q, ul ? 16 : 15, t1, ok);
     if (ok) {
-        M[idx] = cap.n | (uint32_t)tc << 8 | (uint32_t)t1 << 13;
+        M[idx] = (uint16_t)(cap.n | (uint32_t)tc << 8 | (uint32_t)t1 << 13);
         if (cap.n)
             B[idx] = make_uint4((uint32_t)cap.lo, (uint32_t)(cap.lo >> 32), (uint32_t)cap.hi,
                                 (uint32_t)(cap.hi >> 32));
     } else {
-        M[idx] = (uint32_t)tc << 8 | (uint32_t)t1 << 13 | M_OVF;
+        M[idx] = (uint16_t)((uint32_t)tc << 8 | (uint32_t)t1 << 13 | M_OVF);
         B[idx] = v4;
     }
 }
@@ -398,7 +408,7 @@ __global__ __launch_bounds__(CODE_T) void k_dyn_code(const DevStream *__restrict
                                                      DynGeom g, const uint32_t *__restrict__ rows,
                                                      const uint8_t *__restrict__ src,
                                                      const uint8_t *__restrict__ refs,
-                                                     uint32_t *__restrict__ meta, uint4 *__restrict__ body)
+                                                     uint16_t *__restrict__ meta, uint4 *__restrict__ body)
 {
     code_frame<false>(st, dfr, ld_fr, pend, nal, ld_nal, g, rows, src, refs, meta, body, blockIdx.z,
                       blockIdx.y, blockIdx.x);
@@ -415,7 +425,7 @@ __global__ __launch_bounds__(CODE_T) void k_dyn_code_general(const DevStream *__
                                                              DynGeom g, const uint32_t *__restrict__ rows,
                                                              const uint8_t *__restrict__ src,
                                                              const uint8_t *__restrict__ refs,
-                                                             uint32_t *__restrict__ meta,
+                                                             uint16_t *__restrict__ meta,
                                                              uint4 *__restrict__ body, int nframes)
 {
     const int s = blockIdx.z, lane = threadIdx.x & 63;
@@ -634,22 +644,36 @@ struct GroupFixed {
     PTabs ptabs;
 };
 
-/* dynamic LDS: mt, lo [NPC w] u32, ma [8 w] u32, moff [lines] u32,
- * mbits [w] u32, off16 [NPC w] u16, cbp / code [w] u8 */
+/* dynamic LDS: moff [lines] u32, mbits [w] u32, mt, lo, off16 [NPC w] u16,
+ * ma [8 w] u16, cbp / code [w] u8 */
 __host__ __device__ inline size_t group_lds_bytes(int w, int lines)
 {
-    return (size_t)4 * (2 * NPC * w + 8 * w + lines + w) + (size_t)2 * NPC * w + (size_t)2 * w + 16;
+    return (size_t)4 * (lines + w) + (size_t)2 * (3 * NPC * w + 8 * w) + (size_t)2 * w + 16;
 }
 
-/* lo[i]: piece length (11) | coeff_token bits (8) << 11 | its length (5) << 19 | nC + 1 (5) << 24 */
+/* lo[i]: piece length (11) | nC + 1 (5) << 11 */
 constexpr uint32_t LO_LEN = 0x7ffu;
+
+/* coeff_token of a piece with meta mv at context nC >= 0 (Table 9-5) */
+__device__ inline void piece_token(const PTabs &PT, uint32_t mv, int nC, uint32_t &tv, uint32_t &tl)
+{
+    const int tc = tc_of(mv), t1 = (int)((mv >> 13) & 3u);
+    if (nC >= 8) {
+        tv = tc ? (uint32_t)(((tc - 1) << 2) | t1) : 3u;
+        tl = 6;
+    } else {
+        const uint32_t e = PT.ct[nC < 2 ? 0 : (nC < 4 ? 1 : 2)][4 * tc + t1];
+        tv = e & 255u;
+        tl = e >> 8;
+    }
+}
 
 /* grid (R.h + 2, frames, streams), GW threads */
 __global__ __launch_bounds__(GW) void k_dyn_group(DevStream *__restrict__ st,
                                                   const NalDesc *__restrict__ nal, int ld_nal,
                                                   const PlanPending *__restrict__ pend,
                                                   DynFrame *__restrict__ dfr, int ld_fr, DynGeom g,
-                                                  const uint32_t *__restrict__ meta,
+                                                  const uint16_t *__restrict__ meta,
                                                   const uint4 *__restrict__ body,
                                                   unsigned long long *__restrict__ status,
                                                   uint2 *__restrict__ side, uint32_t epoch, int lines,
@@ -664,26 +688,26 @@ __global__ __launch_bounds__(GW) void k_dyn_group(DevStream *__restrict__ st,
     const Rect R{g.x0, g.y0, g.w, g.h};
     const size_t nb = (size_t)s * ld_fr + f;
     const int ndt = R.w * R.h;
-    const uint32_t *M = meta + nb * (size_t)(NPC * ndt);
+    const uint16_t *M = meta + nb * (size_t)(NPC * ndt);
     const uint4 *Bd = body + nb * (size_t)(NPC * ndt);
     const bool first = gi == 0, last = gi == ng - 1, rect = !first && !last;
     const int row = rect ? R.y0 + gi - 1 : 0;
     const int nd = rect ? R.w : 0, npc = NPC * nd;
     const int q0 = rect ? (row - R.y0) * R.w : 0;
-    uint32_t *mt = gdyn, *lo = mt + NPC * R.w, *ma = lo + NPC * R.w, *moff = ma + 8 * R.w;
-    uint32_t *mbits = moff + lines;
-    uint16_t *off16 = reinterpret_cast<uint16_t *>(mbits + R.w);
-    uint8_t *cbpa = reinterpret_cast<uint8_t *>(off16 + NPC * R.w), *codea = cbpa + R.w;
-    const uint32_t *Mq = M + (size_t)q0 * NPC;
+    uint32_t *moff = gdyn, *mbits = moff + lines;
+    uint16_t *mt = reinterpret_cast<uint16_t *>(mbits + R.w), *lo = mt + NPC * R.w, *off16 = lo + NPC * R.w;
+    uint16_t *ma = off16 + NPC * R.w;
+    uint8_t *cbpa = reinterpret_cast<uint8_t *>(ma + 8 * R.w), *codea = cbpa + R.w;
+    const uint16_t *Mq = M + (size_t)q0 * NPC;
     const uint4 *Bq = Bd + (size_t)q0 * NPC;
 
     /* rect row: the records first */
     for (int i0 = 0; i0 < npc; i0 += 4 * GW) {
-        uint32_t v[4];
+        uint16_t v[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             const int i = i0 + t + GW * u;
-            v[u] = i < npc ? Mq[i] : 0u;
+            v[u] = i < npc ? Mq[i] : (uint16_t)0;
         }
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
@@ -692,12 +716,12 @@ __global__ __launch_bounds__(GW) void k_dyn_group(DevStream *__restrict__ st,
         }
     }
     for (int i0 = 0; i0 < 8 * nd; i0 += 4 * GW) {
-        uint32_t v[4];
+        uint16_t v[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             const int i = i0 + t + GW * u, k = i >> 3, e = i & 7;
             const int pcA = e < 4 ? 12 + e : (e < 6 ? 16 + e : 18 + e);
-            v[u] = i < 8 * nd && row > R.y0 ? M[(size_t)(q0 + k - R.w) * NPC + pcA] : 0u;
+            v[u] = i < 8 * nd && row > R.y0 ? M[(size_t)(q0 + k - R.w) * NPC + pcA] : (uint16_t)0;
         }
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
@@ -713,7 +737,7 @@ __global__ __launch_bounds__(GW) void k_dyn_group(DevStream *__restrict__ st,
         L.wv[t] = pend[s].wv[t];
     }
     if (t == 0) L.head_over = 0;
-    build_ptabs(*reinterpret_cast<const Tabs *>(&g_tabs), L.ptabs, t, GW);
+    load_ptabs(L.ptabs, t, GW);
     DevStream *S = st + s;
     const NalDesc d = nal[(size_t)s * ld_nal + j];
     __syncthreads();                                        /* waypoint table, ptabs, records */
@@ -754,8 +778,7 @@ __global__ __launch_bounds__(GW) void k_dyn_group(DevStream *__restrict__ st,
             const int k = (int)div_m((uint32_t)i, m26), pc = i - k * NPC;
             const int col = R.x0 + k;
             const uint32_t mv = mt[i];
-            const int tc = tc_of(mv);
-            const uint32_t *mk = mt + k * NPC;
+            const uint16_t *mk = mt + k * NPC;
             uint32_t tv = 0, tl = 0;
             int nC = -1;
             if (pc != 16 && pc != 17) {
@@ -772,25 +795,17 @@ __global__ __launch_bounds__(GW) void k_dyn_group(DevStream *__restrict__ st,
                                 : (row > R.y0 ? tc_of(ma[8 * k + (pc < 22 ? pc - 14 : pc - 16)]) : nBe);
                 }
                 nC = nc_of(nA, nB);
-                const int t1 = (int)((mv >> 13) & 3u);
-                if (nC >= 8) {
-                    tv = tc ? (uint32_t)(((tc - 1) << 2) | t1) : 3u;
-                    tl = 6;
-                } else {
-                    const uint32_t e = PT.ct[nC < 2 ? 0 : (nC < 4 ? 1 : 2)][4 * tc + t1];
-                    tv = e & 255u;
-                    tl = e >> 8;
-                }
+                piece_token(PT, mv, nC, tv, tl);
             }
             uint32_t len = tl + (mv & 255u);
             if (mv & M_OVF) len = ovf_bits(PT, TB, Bq[i], pc, nC);     /* rare: > 128-bit block */
-            lo[i] = len | tv << 11 | tl << 19 | (uint32_t)(nC + 1) << 24;
+            lo[i] = (uint16_t)(len | (uint32_t)(nC + 1) << 11);
         }
         __syncthreads();
         if (stamps) stv[1] = __builtin_amdgcn_s_memrealtime();
         /* per dynamic MB: cbp, its code, piece offsets, bits */
         for (int k = t; k < nd; k += GW) {
-            const uint32_t *mk = mt + k * NPC;
+            const uint16_t *mk = mt + k * NPC;
             int cbp_l = 0;
 #pragma unroll
             for (int pc = 0; pc < 16; ++pc)
@@ -806,7 +821,7 @@ __global__ __launch_bounds__(GW) void k_dyn_group(DevStream *__restrict__ st,
             put_ue(hs, (uint32_t)code);
             if (cbp) put_se(hs, 0);                         /* mb_qp_delta */
             uint32_t off = hs.n;
-            const uint32_t *lk = lo + k * NPC;
+            const uint16_t *lk = lo + k * NPC;
             uint16_t *ok = off16 + k * NPC;
 #pragma unroll
             for (int blk = 0; blk < 16; ++blk) {            /* luma4x4BlkIdx order */
@@ -924,12 +939,16 @@ __global__ __launch_bounds__(GW) void k_dyn_group(DevStream *__restrict__ st,
                     if (o == 0xffffu) continue;
                     const int k = (int)div_m((uint32_t)i, m26), pc = i - k * NPC;
                     const uint32_t e = lo[i], mv = mt[i];
-                    const int tl = (int)((e >> 19) & 31u), nC = (int)((e >> 24) & 31u) - 1;
+                    const int nC = (int)(e >> 11) - 1;
                     const uint32_t pos = rel0 + moff[R.x0 + k] + o;
                     if (!(mv & M_OVF)) {
                         WSink sk{win, 0, 0, 0};
                         sk.start(pos);
-                        if (nC != -1) sk.put((e >> 11) & 255u, tl);
+                        if (nC != -1) {
+                            uint32_t tv, tl;
+                            piece_token(PT, mv, nC, tv, tl);
+                            sk.put(tv, (int)tl);
+                        }
                         sk.put_cap(CapSink{(uint64_t)bd[u].z | (uint64_t)bd[u].w << 32,
                                            (uint64_t)bd[u].x | (uint64_t)bd[u].y << 32, mv & 255u});
                         sk.finish();

@@ -1574,7 +1574,7 @@ int scroll_batch_set_dyn_rect(ScrollBatch *b, int x0, int y0, int w, int h, size
     if (e == hipSuccess) e = hipMalloc(&b->d_refs, S * dyn_pair_bytes(b));
     if (e == hipSuccess) e = hipMalloc(&b->d_stage, S * F * g.slot_bytes);
     if (e == hipSuccess) e = hipMalloc(&b->dx.rows, S * F * 32 * h * sizeof(uint32_t));
-    if (e == hipSuccess) e = hipMalloc(&b->dx.meta, S * F * DYN_PIECES * w * h * sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMalloc(&b->dx.meta, S * F * DYN_PIECES * w * h * sizeof(uint16_t));
     if (e == hipSuccess) e = hipMalloc(&b->dx.body, S * F * DYN_PIECES * w * h * sizeof(uint4));
     if (e == hipSuccess) e = hipMalloc(&b->dx.status, S * F * (h + 2) * sizeof(unsigned long long));
     if (e == hipSuccess) e = hipMalloc(&b->dx.side, S * F * 2 * (h + 2) * sizeof(uint2));

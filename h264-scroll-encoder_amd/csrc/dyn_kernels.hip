@@ -89,7 +89,9 @@ __device__ inline NalCtx nal_ctx(const DevStream *S, const NalDesc &d, const int
 /*   k_dyn_ep     per NAL: shared boundary words merged, emulation-        */
 /*                prevention positions and count                           */
 /*                                                                         */
-/* Records of dynamic MB q (rect raster order) of NAL n, piece pc:          */
+/* Records of dynamic MB q (rect raster order) of NAL n, piece pc, at       */
+/*   rec_of(q, pc): k_dyn_code's task order -- luma 16 q + pc, chroma AC    */
+/*   16 nd + 8 q + pc - 18, chroma DC 24 nd + 2 q + pc - 16 (nd = w h):     */
 /*   0..15 luma 4x4 (raster), 16 / 17 Cb / Cr DC, 18 + 4p + b chroma AC    */
 /*   (plane p, raster b): meta[n][q][pc] (u16) = body bits | TotalCoeff << 8 | */
 /*   TrailingOnes << 13 | ovf << 15, body[n][q][pc] = the body right-      */
@@ -98,6 +100,11 @@ __device__ inline NalCtx nal_ctx(const DevStream *S, const NalDesc &d, const int
 /*   levels instead (int8 scan order; DC: int16) and k_dyn_group re-codes. */
 /* ====================================================================== */
 constexpr int NPC = DYN_PIECES;         /* pieces per dynamic MB */
+
+__device__ inline int rec_of(int q, int pc, int ndt)
+{
+    return pc < 16 ? 16 * q + pc : (pc < 18 ? 24 * ndt + 2 * q + (pc - 16) : 16 * ndt + 8 * q + (pc - 18));
+}
 constexpr uint32_t M_OVF = 1u << 15;
 constexpr uint32_t ROW_GEN = 1u << 31, ROW_OFF = 0x0fffffffu;
 
@@ -181,8 +188,10 @@ __global__ __launch_bounds__(256) void k_dyn_rows(const DevStream *__restrict__ 
  * Phase 1: residual -> transform -> quant -> levels (LDS); phase 2, after
  * one barrier: blocks with <= 3 non-zero levels are coded first, so the
  * CAVLC loop of most waves iterates <= 3 times. */
-constexpr int CODE_T = 256;
-constexpr int HEAVY_TC = 3;
+#ifndef SCROLL_CODE_T
+#define SCROLL_CODE_T 256
+#endif
+constexpr int CODE_T = SCROLL_CODE_T, CODE_NW = CODE_T / 64;
 
 template <bool GENERAL>
 __device__ inline void code_frame(const DevStream *__restrict__ st,
@@ -196,8 +205,9 @@ __device__ inline void code_frame(const DevStream *__restrict__ st,
                                                      int s, int f, int bx)
 {
     __shared__ uint4 lv[CODE_T];
-    __shared__ uint32_t whc[CODE_T / 64];
-    __shared__ uint8_t order[CODE_T];
+    __shared__ uint16_t wc[CODE_NW][17];           /* per wave: blocks per TotalCoeff */
+    __shared__ uint16_t order[CODE_T];
+    __shared__ uint16_t mrec[CODE_T];
     __shared__ PTabs ptabs;
     __shared__ int32_t wo[8], wv[8];
     const int t = threadIdx.x;
@@ -250,8 +260,13 @@ __device__ inline void code_frame(const DevStream *__restrict__ st,
         uint32_t sv[4], pv[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
+#ifdef SCROLL_ABL_NOLOAD
+            sv[i] = 0x80808080u + (uint32_t)(task * 7 + i * 3) * 0x01010101u;
+            pv[i] = 0x80808080u;
+#else
             sv[i] = ld32(sp + (size_t)i * lstride);
             pv[i] = ld32(pp + re[i]);
+#endif
         }
         int res[16], W[16];
 #pragma unroll
@@ -275,13 +290,22 @@ __device__ inline void code_frame(const DevStream *__restrict__ st,
         int res[16], W[16];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
+#ifdef SCROLL_ABL_NOLOAD
+            const uint32_t sv = 0x80808080u + (uint32_t)(task * 5 + i) * 0x01010101u;
+            const uint32_t ea = 0;
+#else
             const uint32_t sv = ld32(sp + (size_t)i * cstride);
             const uint32_t ea = re[i];
+#endif
             int pred[4];
             if (!GENERAL || !(ea & ROW_GEN)) {
                 const uint32_t fr = (ea >> 28) & 7u;
+#ifdef SCROLL_ABL_NOLOAD
+                const uint32_t av = 0x80808080u, bv = 0u;
+#else
                 const uint32_t av = ld32(cp + (ea & ROW_OFF));
                 const uint32_t bv = fr ? ld32(cp + (re[8 * g.h + i] & ROW_OFF)) : 0u;
+#endif
 #pragma unroll
                 for (int x = 0; x < 4; ++x) {
                     const int a = (int)((av >> (8 * x)) & 255u), b = (int)((bv >> (8 * x)) & 255u);
@@ -339,7 +363,7 @@ __device__ inline void code_frame(const DevStream *__restrict__ st,
                                quant_dc(d0 + d1 - d2 - d3), quant_dc(d0 - d1 - d2 + d3)};
             CapSink cap{0, 0, 0};
             const int tc = cavlc_dc4(cap, ptabs, dq);
-            const size_t idx = (size_t)k * NPC + 16 + p;
+            const size_t idx = (size_t)24 * ndt + 2 * k + p;    /* rec_of(k, 16 + p) */
             if (cap.n <= 128) {
                 M[idx] = (uint16_t)(cap.n | (uint32_t)tc << 8);
                 if (cap.n)
@@ -352,53 +376,79 @@ __device__ inline void code_frame(const DevStream *__restrict__ st,
             }
         }
     }
-    /* encode order: light blocks first */
-    const bool heavy = act && n > HEAVY_TC;
+    /* encode order: by TotalCoeff, largest first (a counting sort over the
+     * workgroup), so each wave's CAVLC loop runs about its own blocks' count */
     lv[t] = make_uint4(pk[0], pk[1], pk[2], pk[3]);
-    const uint64_t hb = __ballot(heavy);
-    if (lane == 0) whc[wave] = (uint32_t)__popcll(hb);
-    __syncthreads();
     {
-        uint32_t hpre = 0, htot = 0;
+        const int key = 16 - n;                         /* inactive tasks: n = 0 */
+        uint32_t below = 0;
 #pragma unroll
-        for (int w2 = 0; w2 < CODE_T / 64; ++w2) {
-            hpre += w2 < wave ? whc[w2] : 0u;
-            htot += whc[w2];
+        for (int k = 0; k < 17; ++k) {
+            const uint64_t m = __ballot(key == k);
+            if (lane == 0) wc[wave][k] = (uint16_t)__popcll(m);
+            if (key == k)
+                below = (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
         }
-        const uint32_t hr = hpre + (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(hb >> 32),
-                                                                       __builtin_amdgcn_mbcnt_lo((uint32_t)hb, 0u));
-        const uint32_t lr = (uint32_t)t - hr;
-        order[heavy ? (uint32_t)CODE_T - htot + hr : lr] = (uint8_t)t;
+        __syncthreads();
+        if (t < 17) {                                   /* key k = t: wave prefixes, key offsets */
+            uint32_t tot = 0;
+#pragma unroll
+            for (int w2 = 0; w2 < CODE_NW; ++w2) tot += wc[w2][t];
+            uint32_t kb = tot;
+#pragma unroll
+            for (int d = 1; d < 32; d <<= 1) {
+                const uint32_t o = __shfl_up(kb, d, 64);
+                if (lane >= d) kb += o;
+            }
+            uint32_t run = kb - tot;
+#pragma unroll
+            for (int w2 = 0; w2 < CODE_NW; ++w2) {
+                const uint32_t c = wc[w2][t];
+                wc[w2][t] = (uint16_t)run;
+                run += c;
+            }
+        }
+        __syncthreads();
+        order[wc[wave][key] + below] = (uint16_t)t;
     }
     __syncthreads();
     const int u = order[t];
     const int tk = bx * CODE_T + u;
-    if (tk >= ntask) return;
     const uint4 v4 = lv[u];
     const uint32_t q[4] = {v4.x, v4.y, v4.z, v4.w};
     const bool ul = tk < 16 * ndt;
-    size_t idx;
-    if (ul) {
-        idx = (size_t)(tk >> 4) * NPC + (tk & 15);
-    } else {
-        const int jj = tk - 16 * ndt;
-        idx = (size_t)(jj >> 3) * NPC + 18 + (jj & 7);
-    }
     CapSink cap{0, 0, 0};
-    int t1;
-    bool ok;
-    const int tc = cavlc_body(cap, ptabs, q, ul ? 16 : 15, t1, ok);
+    int t1 = 0;
+    bool ok = true;
+    int tc = 0;
+    if (tk < ntask) {
+#ifdef SCROLL_ABL_NOCAVLC
+        tc = __builtin_popcount(q[0] | q[1] | q[2] | q[3]) & 15;
+#else
+        tc = cavlc_body(cap, ptabs, q, ul ? 16 : 15, t1, ok);
+#endif
+    }
+    /* back to task order through LDS: the records of a workgroup's tasks are
+     * contiguous (rec_of), so the stores coalesce */
+    __syncthreads();
     if (ok) {
-        M[idx] = (uint16_t)(cap.n | (uint32_t)tc << 8 | (uint32_t)t1 << 13);
-        if (cap.n)
-            B[idx] = make_uint4((uint32_t)cap.lo, (uint32_t)(cap.lo >> 32), (uint32_t)cap.hi,
-                                (uint32_t)(cap.hi >> 32));
+        mrec[u] = (uint16_t)(cap.n | (uint32_t)tc << 8 | (uint32_t)t1 << 13);
+        lv[u] = make_uint4((uint32_t)cap.lo, (uint32_t)(cap.lo >> 32), (uint32_t)cap.hi, (uint32_t)(cap.hi >> 32));
     } else {
-        M[idx] = (uint16_t)((uint32_t)tc << 8 | (uint32_t)t1 << 13 | M_OVF);
-        B[idx] = v4;
+        mrec[u] = (uint16_t)((uint32_t)tc << 8 | (uint32_t)t1 << 13 | M_OVF);       /* lv[u] keeps the levels */
+    }
+    __syncthreads();
+    const int tt = bx * CODE_T + t;
+#ifdef SCROLL_ABL_NOSTORE
+    if (tc == 99)
+#endif
+    if (tt < ntask) {
+        const uint16_t mm = mrec[t];
+        M[tt] = mm;
+        if ((mm & 255u) || (mm & M_OVF)) B[tt] = lv[t];
     }
 }
-
 
 /* the frames without a half-pel waypoint chain: grid (chunks, frames, streams) */
 __global__ __launch_bounds__(CODE_T) void k_dyn_code(const DevStream *__restrict__ st,
@@ -633,7 +683,8 @@ __device__ __attribute__((noinline)) void ovf_put(uint32_t *buf, uint32_t lo, ui
  * flight per CU rather than from wide workgroups; LDS is sized to the rect
  * (dynamic shared memory, group_lds_bytes) */
 constexpr int GW = 64;
-constexpr int GBUF_WORDS = 1024;         /* 32 Kbit per pass; a config-3 row is ~18 Kbit */
+constexpr int GBUF_WORDS = 256;          /* 8 Kbit per pass (a config-3 row: ~18 Kbit in 3 passes);
+                                           each pass walks only the MBs / rows it covers */
 
 struct GroupFixed {
     uint32_t buf[GBUF_WORDS];
@@ -644,11 +695,11 @@ struct GroupFixed {
     PTabs ptabs;
 };
 
-/* dynamic LDS: moff [lines] u32, mbits [w] u32, mt, lo, off16 [NPC w] u16,
- * ma [8 w] u16, cbp / code [w] u8 */
+/* dynamic LDS: moff [lines + 1] u32, mbits [w] u32, mt, lo, off16 [NPC w]
+ * u16, ma [8 w] u16, cbp / code [w] u8 */
 __host__ __device__ inline size_t group_lds_bytes(int w, int lines)
 {
-    return (size_t)4 * (lines + w) + (size_t)2 * (3 * NPC * w + 8 * w) + (size_t)2 * w + 16;
+    return (size_t)4 * (lines + 1 + w) + (size_t)2 * (3 * NPC * w + 8 * w) + (size_t)2 * w + 16;
 }
 
 /* lo[i]: piece length (11) | nC + 1 (5) << 11 */
@@ -694,26 +745,40 @@ __global__ __launch_bounds__(GW) void k_dyn_group(DevStream *__restrict__ st,
     const int row = rect ? R.y0 + gi - 1 : 0;
     const int nd = rect ? R.w : 0, npc = NPC * nd;
     const int q0 = rect ? (row - R.y0) * R.w : 0;
-    uint32_t *moff = gdyn, *mbits = moff + lines;
+    uint32_t *moff = gdyn, *mbits = moff + lines + 1;
     uint16_t *mt = reinterpret_cast<uint16_t *>(mbits + R.w), *lo = mt + NPC * R.w, *off16 = lo + NPC * R.w;
     uint16_t *ma = off16 + NPC * R.w;
     uint8_t *cbpa = reinterpret_cast<uint8_t *>(ma + 8 * R.w), *codea = cbpa + R.w;
-    const uint16_t *Mq = M + (size_t)q0 * NPC;
-    const uint4 *Bq = Bd + (size_t)q0 * NPC;
+    /* piece j of the row in record order (three contiguous runs: luma, chroma
+     * AC, chroma DC) -> its record and its slot k NPC + pc in mt / lo / off16 */
+    auto rec_run = [&](int jr, int &slot) -> int {
+        if (jr < 16 * nd) {
+            slot = (jr >> 4) * NPC + (jr & 15);
+            return 16 * q0 + jr;
+        }
+        if (jr < 24 * nd) {
+            const int a = jr - 16 * nd;
+            slot = (a >> 3) * NPC + 18 + (a & 7);
+            return 16 * ndt + 8 * q0 + a;
+        }
+        const int a = jr - 24 * nd;
+        slot = (a >> 1) * NPC + 16 + (a & 1);
+        return 24 * ndt + 2 * q0 + a;
+    };
 
     /* rect row: the records first */
     for (int i0 = 0; i0 < npc; i0 += 4 * GW) {
         uint16_t v[4];
+        int sl[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-            const int i = i0 + t + GW * u;
-            v[u] = i < npc ? Mq[i] : (uint16_t)0;
+            const int jr = i0 + t + GW * u;
+            sl[u] = -1;
+            v[u] = jr < npc ? M[rec_run(jr, sl[u])] : (uint16_t)0;
         }
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const int i = i0 + t + GW * u;
-            if (i < npc) mt[i] = v[u];
-        }
+        for (int u = 0; u < 4; ++u)
+            if (sl[u] >= 0) mt[sl[u]] = v[u];
     }
     for (int i0 = 0; i0 < 8 * nd; i0 += 4 * GW) {
         uint16_t v[4];
@@ -721,7 +786,7 @@ __global__ __launch_bounds__(GW) void k_dyn_group(DevStream *__restrict__ st,
         for (int u = 0; u < 4; ++u) {
             const int i = i0 + t + GW * u, k = i >> 3, e = i & 7;
             const int pcA = e < 4 ? 12 + e : (e < 6 ? 16 + e : 18 + e);
-            v[u] = i < 8 * nd && row > R.y0 ? M[(size_t)(q0 + k - R.w) * NPC + pcA] : (uint16_t)0;
+            v[u] = i < 8 * nd && row > R.y0 ? M[rec_of(q0 + k - R.w, pcA, ndt)] : (uint16_t)0;
         }
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
@@ -798,7 +863,7 @@ __global__ __launch_bounds__(GW) void k_dyn_group(DevStream *__restrict__ st,
                 piece_token(PT, mv, nC, tv, tl);
             }
             uint32_t len = tl + (mv & 255u);
-            if (mv & M_OVF) len = ovf_bits(PT, TB, Bq[i], pc, nC);     /* rare: > 128-bit block */
+            if (mv & M_OVF) len = ovf_bits(PT, TB, Bd[rec_of(q0 + k, pc, ndt)], pc, nC);   /* rare: > 128 bits */
             lo[i] = (uint16_t)(len | (uint32_t)(nC + 1) << 11);
         }
         __syncthreads();
@@ -854,6 +919,7 @@ __global__ __launch_bounds__(GW) void k_dyn_group(DevStream *__restrict__ st,
             if (col < mbw) moff[col] = carry + incl - len;
             carry += __shfl(incl, GW - 1, GW);
         }
+        if (t == 0) moff[mbw] = carry;
         bits = carry;
     } else {
         /* rows without dynamic MBs: row offsets */
@@ -872,6 +938,7 @@ __global__ __launch_bounds__(GW) void k_dyn_group(DevStream *__restrict__ st,
             if (r < rb) moff[r - ra] = carry + incl - len;
             carry += __shfl(incl, GW - 1, GW);
         }
+        if (t == 0) moff[rb - ra] = carry;
         bits = carry + (last ? 1u : 0u);
     }
 
@@ -903,8 +970,21 @@ __global__ __launch_bounds__(GW) void k_dyn_group(DevStream *__restrict__ st,
         for (uint32_t i = (uint32_t)t; i < n; i += GW) L.buf[i] = 0u;
         __syncthreads();
         const LdsOrWin win{L.buf, p0, n};
+        /* the entries (rect: MB columns, static: rows) whose bits meet the
+         * window [32 p0, 32 (p0 + n)): [ea, eb), by binary search on moff */
+        const int ne = rect ? mbw : rb - ra;
+        auto cnt_le = [&](uint32_t x) -> int {          /* # e in [0, ne] with rel0 + moff[e] <= x */
+            int lo = 0, hi = ne + 1;
+            while (lo < hi) {
+                const int mid = (lo + hi) >> 1;
+                if (rel0 + moff[mid] <= x) lo = mid + 1;
+                else hi = mid;
+            }
+            return lo;
+        };
+        const int ea = max(cnt_le(32u * p0) - 1, 0), eb = min(cnt_le(32u * (p0 + n) - 1u), ne);
         if (rect) {
-            for (int col = t; col < mbw; col += GW) {
+            for (int col = ea + t; col < eb; col += GW) {
                 WSink sk{win, 0, 0, 0};
                 sk.start(rel0 + moff[col]);
                 if (!head_over) {
@@ -923,18 +1003,22 @@ __global__ __launch_bounds__(GW) void k_dyn_group(DevStream *__restrict__ st,
                 sk.finish();
             }
             const uint32_t m26 = magic32(NPC);
-            for (int i0 = 0; i0 < npc; i0 += 4 * GW) {
+            const int pa = NPC * max(ea - R.x0, 0), pb = NPC * min(eb - R.x0, nd);
+            for (int i0 = pa; i0 < pb; i0 += 4 * GW) {
                 uint4 bd[4];
 #pragma unroll
                 for (int u = 0; u < 4; ++u) {               /* four body loads in flight */
                     const int i = i0 + t + GW * u;
                     bd[u] = make_uint4(0, 0, 0, 0);
-                    if (i < npc && off16[i] != 0xffffu && (mt[i] & (255u | M_OVF))) bd[u] = Bq[i];
+                    if (i < pb && off16[i] != 0xffffu && (mt[i] & (255u | M_OVF))) {
+                        const int k = (int)div_m((uint32_t)i, m26);
+                        bd[u] = Bd[rec_of(q0 + k, i - k * NPC, ndt)];
+                    }
                 }
 #pragma unroll
                 for (int u = 0; u < 4; ++u) {
                     const int i = i0 + t + GW * u;
-                    if (i >= npc) continue;
+                    if (i >= pb) continue;
                     const uint32_t o = off16[i];
                     if (o == 0xffffu) continue;
                     const int k = (int)div_m((uint32_t)i, m26), pc = i - k * NPC;
@@ -958,15 +1042,15 @@ __global__ __launch_bounds__(GW) void k_dyn_group(DevStream *__restrict__ st,
                 }
             }
         } else {
-            if (first && t == 0) {                          /* slice header, h264_writer.c:549-553 */
+            if (first && t == 0 && p0 * 32u < F) {          /* slice header, h264_writer.c:549-553 */
                 WSink hs{win, 0, 0, 0};
                 hs.start(0);
                 emit_slice_header(hs, c);
                 hs.finish();
             }
-            const int nm = (rb - ra) * mbw;
+            const int nm = eb * mbw;
             const uint32_t m_mbw = magic32((uint32_t)mbw);
-            for (int m = t; m < nm; m += GW) {
+            for (int m = ea * mbw + t; m < nm; m += GW) {
                 const int rr = (int)div_m((uint32_t)m, m_mbw), col = m - rr * mbw, r = ra + rr;
                 uint32_t off = moff[rr];
                 WSink sk{win, 0, 0, 0};

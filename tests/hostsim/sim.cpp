@@ -316,6 +316,20 @@ long sim_cavlc_split(const int *coef, int max, int nC, int start, uint32_t *word
     return (long)(end - (uint32_t)start);
 }
 
+/* the compile-time packed tables the kernels copy (make_ptabs) equal the
+ * runtime packing (build_ptabs): 1 if identical */
+int sim_ptabs_match(void)
+{
+    dyn::PTabs a, b;
+    std::memset(&a, 0xa5, sizeof a);
+    dyn::build_ptabs(g_dyn_tabs, a, 0, 1);
+    constexpr dyn::Tabs kt = SCROLL_DYN_TABS;
+    constexpr dyn::PTabs kp = dyn::make_ptabs(kt);
+    b = kp;
+    return std::memcmp(a.ct, b.ct, sizeof a.ct) == 0 && std::memcmp(a.tz, b.tz, sizeof a.tz) == 0 &&
+           std::memcmp(a.tzdc, b.tzdc, sizeof a.tzdc) == 0 && std::memcmp(a.rb, b.rb, sizeof a.rb) == 0;
+}
+
 long sim_cavlc_dc4(const int *coef, int start, uint32_t *words, int *tc_out)
 {
     static dyn::PTabs P;

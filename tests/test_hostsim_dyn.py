@@ -165,3 +165,10 @@ def test_ep_closed_form_vs_automaton(hostsim):
         b = np.where(rng.random(n) < p0, 0, rng.integers(0, 6, n)).astype(np.uint8)
         buf = (ctypes.c_uint8 * n).from_buffer_copy(b.tobytes())
         assert hostsim.sim_ep_count(buf, n) == _ep_automaton(b.tolist()), b.tolist()
+
+
+def test_compile_time_tables_match(hostsim):
+    """the kernels copy CAVLC tables packed at compile time (make_ptabs);
+    they must equal the runtime packing the host simulation checks against
+    the oracle"""
+    assert hostsim.sim_ptabs_match() == 1

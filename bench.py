@@ -31,9 +31,9 @@ A step = one scroll_batch_compose over every stream of the rank:
   Offsets = SURVEY 8(d) synthetic scroll (speed 1+(s%8), phase 97 s mod 1440)
   in HBM; output arenas are rewound on device at every step (the bytes of a
   step are the product).
-Prints ONE JSON line (rank 0) with the dominant kernel's roofline (k_dyn_stage
-resp. k_emit, HIP events on its launch stream) and the CPU oracle on host
-cores (rank 0, N = 1).
+Prints ONE JSON line (rank 0) with the dominant kernel's roofline (k_dyn_code
+or k_dyn_group for the dynamic rect, k_hint_stage, k_emit; HIP events on its
+launch stream) and the CPU oracle on host cores (rank 0, N = 1).
 """
 import argparse
 import ctypes
@@ -452,12 +452,12 @@ def main():
             # k_dyn_rows + k_dyn_code per launch: the source and prediction
             # samples of every dynamic MB (384 B each) read; the block
             # records they write for k_dyn_pack are not algorithmic bytes
-            kern = "k_dyn_rows + k_dyn_code"
+            kern = "k_dyn_code"
             alg_bytes = dyn_nals * 2 * 384 * rect[2] * rect[3]
             kern_ms = kms["dyn_code"]
         elif rect:
-            # k_dyn_pack per launch: the staged RBSP written
-            kern = "k_dyn_pack"
+            # k_dyn_group + k_dyn_ep per launch: the staged RBSP written
+            kern = "k_dyn_group"
             alg_bytes = rbsp_tot
             kern_ms = kms["dyn_pack"]
         elif hints:
@@ -471,6 +471,8 @@ def main():
             kern_ms = kms["emit"]
         achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
         traffic = load_traffic(args.workload)
+        if traffic and traffic.get("kernel") != kern:     # measured on another kernel: not this line's
+            traffic = None
         out = {
             "metric": METRIC,
             "value": round(value, 1),

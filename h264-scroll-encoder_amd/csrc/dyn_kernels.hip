@@ -1123,27 +1123,43 @@ __global__ __launch_bounds__(WR_T) void k_dyn_ep(DynFrame *__restrict__ dfr, int
     __syncthreads();                    /* stores reach L2 before the barrier; no L1 line is stale */
     uint32_t *eplist = reinterpret_cast<uint32_t *>(in + g.slot_bytes - DYN_OVF_BYTES);
     const uint32_t nin = df.rbsp_bytes;
+    /* each thread: EP_U x 16 contiguous bytes, all loads in flight; one block
+     * max-scan of the last non-zero byte per pass (a config-3 NAL: one pass) */
+    constexpr int EP_U = 4;
     int carry = -1;
-    for (uint32_t i0 = 0; i0 < nin; i0 += WR_T * 16) {
-        const uint32_t ib = i0 + 16u * (uint32_t)t;
-        const uint32_t n = ib < nin ? min(16u, nin - ib) : 0u;
-        const uint4 v = n ? *reinterpret_cast<const uint4 *>(in + ib) : make_uint4(0, 0, 0, 0);
-        const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
+    for (uint32_t i0 = 0; i0 < nin; i0 += WR_T * 16 * EP_U) {
+        const uint32_t ib = i0 + 16u * EP_U * (uint32_t)t;
+        uint32_t wv[4 * EP_U];
+#pragma unroll
+        for (int u = 0; u < EP_U; ++u) {
+            const uint32_t o = ib + 16u * u;
+            const uint4 v = o < nin ? *reinterpret_cast<const uint4 *>(in + o) : make_uint4(0, 0, 0, 0);
+            wv[4 * u] = v.x;
+            wv[4 * u + 1] = v.y;
+            wv[4 * u + 2] = v.z;
+            wv[4 * u + 3] = v.w;
+        }
+        /* bytes >= nin: not scanned (read as 0 here, as 256 below) */
         int lnz = -1;
 #pragma unroll
-        for (int i = 0; i < 16; ++i)
-            if ((uint32_t)i < n && ((wv[i >> 2] >> (8 * (i & 3))) & 255u)) lnz = (int)(ib + i);
+        for (int w = 0; w < 4 * EP_U; ++w) {
+            const uint32_t m = ib + 4u * w < nin ? wv[w] : 0u;
+            if (m) lnz = (int)(ib + 4u * w) + 3 - (__builtin_clz(m) >> 3);
+        }
         int ex, tot;
         block_excl_max<WR_NW>(lnz, wmax, ex, tot);
         int prev = max(carry, ex);
-        uint32_t ins = 0;
+        uint32_t ins[EP_U / 2] = {};
+        uint32_t cnt = 0;
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            const uint32_t b = (wv[i >> 2] >> (8 * (i & 3))) & 255u;
-            if ((uint32_t)i < n && ep_insert(b, (int)(ib + i) - 1 - prev)) ins |= 1u << i;
-            if ((uint32_t)i < n && b) prev = (int)(ib + i);
+        for (int i = 0; i < 16 * EP_U; ++i) {
+            const uint32_t gi = ib + (uint32_t)i;
+            const uint32_t b = gi < nin ? (wv[i >> 2] >> (8 * (i & 3))) & 255u : 256u;   /* past the end: never inserts */
+            const bool e = ep_insert(b, (int)gi - 1 - prev);
+            ins[i >> 5] |= (e ? 1u : 0u) << (i & 31);
+            cnt += e ? 1u : 0u;
+            prev = b ? (int)gi : prev;
         }
-        const uint32_t cnt = (uint32_t)__builtin_popcount(ins);
         const uint32_t incl = wave_incl_sum(cnt, lane);
         const uint32_t wtot = __shfl(incl, 63, 64);
         uint32_t base = 0;
@@ -1152,11 +1168,15 @@ __global__ __launch_bounds__(WR_T) void k_dyn_ep(DynFrame *__restrict__ dfr, int
             base = __shfl(base, 0, 64);
         }
         uint32_t k = base + incl - cnt;
-        while (ins) {
-            const int i = __builtin_ctz(ins);
-            ins &= ins - 1u;
-            if (k < (uint32_t)EPLIST_MAX) eplist[k] = ib + (uint32_t)i;   /* RBSP index the 03 precedes */
-            k++;
+#pragma unroll
+        for (int w = 0; w < EP_U / 2; ++w) {
+            uint32_t m = ins[w];
+            while (m) {
+                const int i = __builtin_ctz(m);
+                m &= m - 1u;
+                if (k < (uint32_t)EPLIST_MAX) eplist[k] = ib + 32u * w + (uint32_t)i;   /* RBSP index the 03 precedes */
+                k++;
+            }
         }
         carry = max(carry, tot);
     }

@@ -17,7 +17,7 @@ typedef struct {
     uint16_t *meta;
     uint4 *body;
     unsigned long long *status;     /* k_dyn_group look-back: per (frame, row group) */
-    uint2 *side;                    /* k_dyn_group -> k_dyn_ep: shared boundary words */
+    unsigned long long *tails;      /* k_dyn_group: per (frame, row group) pending end word */
     uint32_t epoch;                 /* look-back epoch of the last compose (24 bits, never 0) */
 } DynScratch;
 

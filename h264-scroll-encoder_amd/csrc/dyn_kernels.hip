@@ -465,9 +465,10 @@ __global__ __launch_bounds__(CODE_T) void k_dyn_code(const DevStream *__restrict
 }
 
 /* the others (general chroma path, never for the composer's own waypoints):
- * grid (chunks, 1, streams), each workgroup finds its stream's flagged
- * frames 64 at a time -- a launch over every frame would cost more in empty
+ * grid (chunks, CODE_GEN_Y), each workgroup finds flagged (stream, frame)
+ * pairs 64 at a time -- a launch over every frame would cost more in empty
  * workgroups than the frames it serves */
+constexpr int CODE_GEN_Y = 8;
 __global__ __launch_bounds__(CODE_T) void k_dyn_code_general(const DevStream *__restrict__ st,
                                                              const DynFrame *__restrict__ dfr, int ld_fr,
                                                              const PlanPending *__restrict__ pend,
@@ -476,19 +477,23 @@ __global__ __launch_bounds__(CODE_T) void k_dyn_code_general(const DevStream *__
                                                              const uint8_t *__restrict__ src,
                                                              const uint8_t *__restrict__ refs,
                                                              uint16_t *__restrict__ meta,
-                                                             uint4 *__restrict__ body, int nframes)
+                                                             uint4 *__restrict__ body, int nframes,
+                                                             int nstreams)
 {
-    const int s = blockIdx.z, lane = threadIdx.x & 63;
-    for (int f0 = 0; f0 < nframes; f0 += 64) {
+    const int lane = threadIdx.x & 63, np = nstreams * nframes;
+    for (int p0 = (int)blockIdx.y * 64; p0 < np; p0 += (int)gridDim.y * 64) {
         bool gen = false;
-        if (f0 + lane < nframes) {
-            const DynFrame df = dfr[(size_t)s * ld_fr + f0 + lane];
+        const int p = p0 + lane;
+        if (p < np) {
+            const int s = p / nframes, f = p - s * nframes;
+            const DynFrame df = dfr[(size_t)s * ld_fr + f];
             gen = df.nal >= 0 && (df.err & DF_GENERAL);
         }
         uint64_t m = __ballot(gen);                     /* the same in every wave */
         while (m) {
-            const int f = f0 + __builtin_ctzll(m);
+            const int q = p0 + __builtin_ctzll(m);
             m &= m - 1;
+            const int s = q / nframes, f = q - s * nframes;
             code_frame<true>(st, dfr, ld_fr, pend, nal, ld_nal, g, rows, src, refs, meta, body, s, f,
                              blockIdx.x);
             __syncthreads();
@@ -514,7 +519,6 @@ typedef OrSink<LdsOrWin> WSink;
  * codeword classes) and, for dynamic MBs, coded_block_pattern,
  * mb_qp_delta and the present pieces (coeff_token from the neighbours'
  * TotalCoeff + the body k_dyn_code left in the records), then the stop bit. */
-constexpr int WR_T = 512, WR_NW = WR_T / 64;
 
 __device__ inline int tc_of(uint32_t m) { return (int)((m >> 8) & 31u); }
 
@@ -586,9 +590,8 @@ __device__ inline uint32_t row_static_bits(const HeadCtx &H, const uint32_t *hle
  * header), g = 1 .. h the rect rows, g = h + 1 the rows below (with the stop
  * bit).  One workgroup per group measures its bits, takes its start bit from
  * the groups before it by a decoupled look-back over per-group status words,
- * and writes every staging word it owns alone; its first / last word, when
- * shared with a neighbour group, goes to a side entry that k_dyn_ep merges. */
-constexpr uint32_t SIDE_NONE = 0xffffffffu;
+ * and writes the staging words of its bits; a word shared with the group
+ * before / after is completed through the tail hand-off below. */
 
 /* status word: epoch (24) | flag (2: 1 aggregate, 2 inclusive prefix) | bits (38) */
 __device__ inline uint64_t lb_pack(uint32_t epoch, uint32_t flag, uint64_t v)
@@ -727,7 +730,7 @@ __global__ __launch_bounds__(GW) void k_dyn_group(DevStream *__restrict__ st,
                                                   const uint16_t *__restrict__ meta,
                                                   const uint4 *__restrict__ body,
                                                   unsigned long long *__restrict__ status,
-                                                  uint2 *__restrict__ side, uint32_t epoch, int lines,
+                                                  unsigned long long *__restrict__ tails, uint32_t epoch, int lines,
                                                   uint8_t *__restrict__ stage, uint64_t *__restrict__ stamps)
 {
     __shared__ GroupFixed L;
@@ -950,7 +953,6 @@ __global__ __launch_bounds__(GW) void k_dyn_group(DevStream *__restrict__ st,
     uint32_t *out = reinterpret_cast<uint32_t *>(stage + nb * g.slot_bytes);
     const uint64_t cap_words = (g.slot_bytes - DYN_OVF_BYTES) / 4 - 4;
     const bool over = bits && ((end - 1) >> 5) + 2 > cap_words;
-    uint2 *sd = side + nb * (size_t)(2 * ng) + 2 * gi;
     if (last && t == 0) {
         DF->ep = 0;
         DF->err = over ? DF_OVER : 0u;
@@ -960,12 +962,30 @@ __global__ __launch_bounds__(GW) void k_dyn_group(DevStream *__restrict__ st,
     const uint32_t rel0 = (uint32_t)(start & 31u);
     const uint64_t w0 = start >> 5, wl = bits ? (end - 1) >> 5 : 0;
     const uint32_t nw = (over || !bits) ? 0u : (uint32_t)(wl - w0 + 1);
-    const bool first_sh = nw && rel0, last_sh = nw && (end & 31u) && !(nw == 1 && rel0);
+    /* The word at the start (when rel0 != 0) also holds the groups before;
+     * the word at the end (when end is not word-aligned) the groups after.
+     * Each group publishes its TAIL -- the pending end word, OR of every
+     * group's bits in it so far -- in an epoch-tagged word, and ORs its
+     * predecessor's tail into its own first word.  The last window is
+     * written first, so the tail is out early and successors hardly wait. */
+    unsigned long long *ts = tails + nb * (size_t)ng;
+    const uint32_t ep24 = epoch & 0xffffffu;
+    const bool in_sh = rel0 != 0, out_sh = (end & 31u) != 0 && !last;   /* the last group writes its end word */
+    auto tail_pub = [&](uint32_t v) { lb_store(ts + gi, (uint64_t)ep24 << 40 | 1ull << 32 | v); };
+    auto tail_wait = [&]() -> uint32_t {
+        for (;;) {
+            const uint64_t v = __hip_atomic_load(ts + gi - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if ((uint32_t)(v >> 40) == ep24 && ((v >> 32) & 1u)) return (uint32_t)v;
+            __builtin_amdgcn_s_sleep(1);
+        }
+    };
     if (t == 0) {
-        if (!first_sh) sd[0] = make_uint2(SIDE_NONE, 0u);
-        if (!last_sh) sd[1] = make_uint2(SIDE_NONE, 0u);
+        if (nw == 0) tail_pub(over || !in_sh ? 0u : tail_wait());  /* empty group: passes the tail on */
+        else if (!out_sh) tail_pub(0u);
     }
-    for (uint32_t p0 = 0; p0 < nw; p0 += GBUF_WORDS) {
+    const int npass = (int)((nw + GBUF_WORDS - 1) / GBUF_WORDS);
+    for (int pi = npass - 1; pi >= 0; --pi) {
+        const uint32_t p0 = (uint32_t)pi * GBUF_WORDS;
         const uint32_t n = min((uint32_t)GBUF_WORDS, nw - p0);
         for (uint32_t i = (uint32_t)t; i < n; i += GW) L.buf[i] = 0u;
         __syncthreads();
@@ -1079,9 +1099,15 @@ __global__ __launch_bounds__(GW) void k_dyn_group(DevStream *__restrict__ st,
         for (uint32_t i = (uint32_t)t; i < n; i += GW) {
             const uint32_t q = p0 + i, v = L.buf[i];
             const uint64_t gw = w0 + q;
-            if (q == 0 && first_sh) sd[0] = make_uint2((uint32_t)gw, v);
-            else if (q == nw - 1 && last_sh) sd[1] = make_uint2((uint32_t)gw, v);
-            else out[gw] = __builtin_bswap32(v);
+            if (q == 0 && in_sh) {
+                const uint32_t v2 = v | tail_wait();
+                if (nw == 1 && out_sh) tail_pub(v2);
+                else out[gw] = __builtin_bswap32(v2);
+            } else if (q == nw - 1 && out_sh) {
+                tail_pub(v);
+            } else {
+                out[gw] = __builtin_bswap32(v);
+            }
         }
         __syncthreads();
     }
@@ -1094,44 +1120,47 @@ __global__ __launch_bounds__(GW) void k_dyn_group(DevStream *__restrict__ st,
     }
 }
 
-/* grid (frames, streams): merges the side entries of k_dyn_group into the
- * staged words, then EP positions (slot tail, unsorted) and count */
-__global__ __launch_bounds__(WR_T) void k_dyn_ep(DynFrame *__restrict__ dfr, int ld_fr, DynGeom g,
-                                                 const uint2 *__restrict__ side, int nside,
-                                                 uint8_t *__restrict__ stage)
+/* grid (EP_G, frames, streams): workgroup x scans chunks x, x + EP_G, .. of
+ * EP_CHUNK bytes of its NAL's staged RBSP; a chunk's carry-in (the last
+ * non-zero byte before it) is looked up backwards in the staged bytes, so
+ * chunks are independent.  EP positions (slot tail, unsorted) and count. */
+constexpr int EP_G = 8, EP_T = 256, EP_NW = EP_T / 64, EP_CHUNK = EP_T * 32;
+
+__global__ __launch_bounds__(EP_T) void k_dyn_ep(DynFrame *__restrict__ dfr, int ld_fr, DynGeom g,
+                                                 const uint8_t *__restrict__ stage)
 {
-    __shared__ int32_t wmax[WR_NW];
-    __shared__ uint2 se[2 * (DYN_MAX_H + 2)];
-    const int s = blockIdx.y, f = blockIdx.x, t = threadIdx.x, lane = t & 63;
+    __shared__ int32_t wmax[EP_NW];
+    __shared__ int32_t back;
+    const int s = blockIdx.z, f = blockIdx.y, t = threadIdx.x, lane = t & 63;
     DynFrame *DF = dfr + (size_t)s * ld_fr + f;
     const DynFrame df = *DF;
     if (df.nal < 0 || df.err) return;
     const size_t nb = (size_t)s * ld_fr + f;
-    uint8_t *in = stage + nb * g.slot_bytes;
-    uint32_t *iw = reinterpret_cast<uint32_t *>(in);
-    if (t < nside) se[t] = side[nb * (size_t)nside + t];
-    __syncthreads();
-    if (t < nside && se[t].x != SIDE_NONE) {
-        bool lead = true;
-        for (int e = 0; e < t; ++e) lead = lead && se[e].x != se[t].x;
-        if (lead) {
-            uint32_t v = 0;
-            for (int e = t; e < nside; ++e) v |= se[e].x == se[t].x ? se[e].y : 0u;
-            iw[se[t].x] = __builtin_bswap32(v);
-        }
-    }
-    __syncthreads();                    /* stores reach L2 before the barrier; no L1 line is stale */
-    uint32_t *eplist = reinterpret_cast<uint32_t *>(in + g.slot_bytes - DYN_OVF_BYTES);
+    const uint8_t *in = stage + nb * g.slot_bytes;
+    uint32_t *eplist = reinterpret_cast<uint32_t *>(const_cast<uint8_t *>(in) + g.slot_bytes - DYN_OVF_BYTES);
     const uint32_t nin = df.rbsp_bytes;
-    /* each thread: EP_U x 16 contiguous bytes, all loads in flight; one block
-     * max-scan of the last non-zero byte per pass (a config-3 NAL: one pass) */
-    constexpr int EP_U = 4;
-    int carry = -1;
-    for (uint32_t i0 = 0; i0 < nin; i0 += WR_T * 16 * EP_U) {
-        const uint32_t ib = i0 + 16u * EP_U * (uint32_t)t;
-        uint32_t wv[4 * EP_U];
+    for (uint32_t c0 = (uint32_t)blockIdx.x * EP_CHUNK; c0 < nin; c0 += EP_G * EP_CHUNK) {
+        /* carry-in: wave 0 reads the 256 bytes before the chunk, further back
+         * only while they are all zero */
+        if (t < 64) {
+            int pv = -1;
+            for (int64_t b0 = (int64_t)c0 - 256; b0 > -256; b0 -= 256) {
+                const int64_t o = b0 + 4 * lane;
+                const uint32_t m = o >= 0 ? *reinterpret_cast<const uint32_t *>(in + o) : 0u;
+                const uint64_t nz = __ballot(m != 0);
+                if (nz) {
+                    const int hl = 63 - __builtin_clzll(nz);
+                    const uint32_t mh = __shfl(m, hl, 64);
+                    pv = (int)(b0 + 4 * hl) + 3 - (__builtin_clz(mh) >> 3);
+                    break;
+                }
+            }
+            if (t == 0) back = pv;
+        }
+        const uint32_t ib = c0 + 32u * (uint32_t)t;
+        uint32_t wv[8];
 #pragma unroll
-        for (int u = 0; u < EP_U; ++u) {
+        for (int u = 0; u < 2; ++u) {
             const uint32_t o = ib + 16u * u;
             const uint4 v = o < nin ? *reinterpret_cast<const uint4 *>(in + o) : make_uint4(0, 0, 0, 0);
             wv[4 * u] = v.x;
@@ -1139,27 +1168,24 @@ __global__ __launch_bounds__(WR_T) void k_dyn_ep(DynFrame *__restrict__ dfr, int
             wv[4 * u + 2] = v.z;
             wv[4 * u + 3] = v.w;
         }
-        /* bytes >= nin: not scanned (read as 0 here, as 256 below) */
-        int lnz = -1;
+        int lnz = -1;                                   /* bytes >= nin: not scanned */
 #pragma unroll
-        for (int w = 0; w < 4 * EP_U; ++w) {
+        for (int w = 0; w < 8; ++w) {
             const uint32_t m = ib + 4u * w < nin ? wv[w] : 0u;
             if (m) lnz = (int)(ib + 4u * w) + 3 - (__builtin_clz(m) >> 3);
         }
         int ex, tot;
-        block_excl_max<WR_NW>(lnz, wmax, ex, tot);
-        int prev = max(carry, ex);
-        uint32_t ins[EP_U / 2] = {};
-        uint32_t cnt = 0;
+        block_excl_max<EP_NW>(lnz, wmax, ex, tot);     /* its barriers also publish `back` */
+        int prev = max(back, ex);
+        uint32_t ins = 0;
 #pragma unroll
-        for (int i = 0; i < 16 * EP_U; ++i) {
+        for (int i = 0; i < 32; ++i) {
             const uint32_t gi = ib + (uint32_t)i;
             const uint32_t b = gi < nin ? (wv[i >> 2] >> (8 * (i & 3))) & 255u : 256u;   /* past the end: never inserts */
-            const bool e = ep_insert(b, (int)gi - 1 - prev);
-            ins[i >> 5] |= (e ? 1u : 0u) << (i & 31);
-            cnt += e ? 1u : 0u;
+            ins |= (ep_insert(b, (int)gi - 1 - prev) ? 1u : 0u) << i;
             prev = b ? (int)gi : prev;
         }
+        const uint32_t cnt = (uint32_t)__builtin_popcount(ins);
         const uint32_t incl = wave_incl_sum(cnt, lane);
         const uint32_t wtot = __shfl(incl, 63, 64);
         uint32_t base = 0;
@@ -1168,17 +1194,13 @@ __global__ __launch_bounds__(WR_T) void k_dyn_ep(DynFrame *__restrict__ dfr, int
             base = __shfl(base, 0, 64);
         }
         uint32_t k = base + incl - cnt;
-#pragma unroll
-        for (int w = 0; w < EP_U / 2; ++w) {
-            uint32_t m = ins[w];
-            while (m) {
-                const int i = __builtin_ctz(m);
-                m &= m - 1u;
-                if (k < (uint32_t)EPLIST_MAX) eplist[k] = ib + 32u * w + (uint32_t)i;   /* RBSP index the 03 precedes */
-                k++;
-            }
+        while (ins) {
+            const int i = __builtin_ctz(ins);
+            ins &= ins - 1u;
+            if (k < (uint32_t)EPLIST_MAX) eplist[k] = ib + (uint32_t)i;   /* RBSP index the 03 precedes */
+            k++;
         }
-        carry = max(carry, tot);
+        __syncthreads();                                /* `back` is rewritten by the next chunk */
     }
 }
 
@@ -1493,8 +1515,8 @@ int dyn_launch_code(hipStream_t hs, int nframes, int S, const DevStream *st, con
     hipLaunchKernelGGL(k_dyn_code, dim3(nchunk, nframes, S), dim3(CODE_T), 0, hs, st, dfr, ld_fr,
                        pend, nal, ld_nal, *g, x->rows, src, refs, x->meta, x->body);
     if (hipGetLastError() != hipSuccess) return -1;
-    hipLaunchKernelGGL(k_dyn_code_general, dim3(nchunk, 1, S), dim3(CODE_T), 0, hs, st, dfr, ld_fr,
-                       pend, nal, ld_nal, *g, x->rows, src, refs, x->meta, x->body, nframes);
+    hipLaunchKernelGGL(k_dyn_code_general, dim3(nchunk, CODE_GEN_Y), dim3(CODE_T), 0, hs, st, dfr, ld_fr,
+                       pend, nal, ld_nal, *g, x->rows, src, refs, x->meta, x->body, nframes, S);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -1507,10 +1529,10 @@ int dyn_launch_pack(hipStream_t hs, int nframes, int S, DevStream *st, const Nal
     const int ng = g->h + 2;
     const int lines = mbw > mbh ? mbw : mbh;
     hipLaunchKernelGGL(k_dyn_group, dim3(ng, nframes, S), dim3(GW), group_lds_bytes(g->w, lines), hs, st, nal,
-                       ld_nal, pend, dfr, ld_fr, *g, x->meta, x->body, x->status, x->side, epoch, lines,
+                       ld_nal, pend, dfr, ld_fr, *g, x->meta, x->body, x->status, x->tails, epoch, lines,
                        stage, stamps);
     if (hipGetLastError() != hipSuccess) return -1;
-    hipLaunchKernelGGL(k_dyn_ep, dim3(nframes, S), dim3(WR_T), 0, hs, dfr, ld_fr, *g, x->side, 2 * ng, stage);
+    hipLaunchKernelGGL(k_dyn_ep, dim3(EP_G, nframes, S), dim3(EP_T), 0, hs, dfr, ld_fr, *g, stage);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

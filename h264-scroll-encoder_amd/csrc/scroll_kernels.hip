@@ -1510,7 +1510,7 @@ static void dyn_release(ScrollBatch *b)
     (void)hipFree(b->dx.meta);
     (void)hipFree(b->dx.body);
     (void)hipFree(b->dx.status);
-    (void)hipFree(b->dx.side);
+    (void)hipFree(b->dx.tails);
     b->d_dfr = nullptr;
     b->d_src = b->d_refs = b->d_stage = nullptr;
     b->dx = DynScratch{};
@@ -1577,7 +1577,8 @@ int scroll_batch_set_dyn_rect(ScrollBatch *b, int x0, int y0, int w, int h, size
     if (e == hipSuccess) e = hipMalloc(&b->dx.meta, S * F * DYN_PIECES * w * h * sizeof(uint16_t));
     if (e == hipSuccess) e = hipMalloc(&b->dx.body, S * F * DYN_PIECES * w * h * sizeof(uint4));
     if (e == hipSuccess) e = hipMalloc(&b->dx.status, S * F * (h + 2) * sizeof(unsigned long long));
-    if (e == hipSuccess) e = hipMalloc(&b->dx.side, S * F * 2 * (h + 2) * sizeof(uint2));
+    if (e == hipSuccess) e = hipMalloc(&b->dx.tails, S * F * (h + 2) * sizeof(unsigned long long));
+    if (e == hipSuccess) e = hipMemset(b->dx.tails, 0, S * F * (h + 2) * sizeof(unsigned long long));
     if (e == hipSuccess) e = hipMemset(b->dx.status, 0, S * F * (h + 2) * sizeof(unsigned long long));
     b->dx.epoch = 0;
     if (e == hipSuccess) e = hipMemset(b->d_dfr, 0, S * F * sizeof(DynFrame));

@@ -15,7 +15,7 @@
 typedef struct {
     uint32_t *rows;
     uint16_t *meta;
-    uint4 *body;
+    uint2 *body_lo, *body_hi;       /* record bodies: bits 0..63, bits 64..127 */
     unsigned long long *status;     /* k_dyn_group look-back: per (frame, row group) */
     unsigned long long *tails;      /* k_dyn_group: per (frame, row group) pending end word */
     uint32_t epoch;                 /* look-back epoch of the last compose (24 bits, never 0) */

@@ -101,6 +101,20 @@ __device__ inline NalCtx nal_ctx(const DevStream *S, const NalDesc &d, const int
 /* ====================================================================== */
 constexpr int NPC = DYN_PIECES;         /* pieces per dynamic MB */
 
+/* a record body is two planes of 8 bytes: bits 0..63 (always) and 64..127
+ * (only for bodies over 64 bits and for level records) */
+__device__ inline void put_body(uint2 *BL, uint2 *BH, size_t i, uint4 v, bool hi)
+{
+    BL[i] = make_uint2(v.x, v.y);
+    if (hi) BH[i] = make_uint2(v.z, v.w);
+}
+
+__device__ inline uint4 get_body(const uint2 *BL, const uint2 *BH, size_t i, bool hi)
+{
+    const uint2 a = BL[i], b = hi ? BH[i] : make_uint2(0u, 0u);
+    return make_uint4(a.x, a.y, b.x, b.y);
+}
+
 __device__ inline int rec_of(int q, int pc, int ndt)
 {
     return pc < 16 ? 16 * q + pc : (pc < 18 ? 24 * ndt + 2 * q + (pc - 16) : 16 * ndt + 8 * q + (pc - 18));
@@ -201,8 +215,8 @@ __device__ inline void code_frame(const DevStream *__restrict__ st,
                                                      DynGeom g, const uint32_t *__restrict__ rows,
                                                      const uint8_t *__restrict__ src,
                                                      const uint8_t *__restrict__ refs,
-                                                     uint16_t *__restrict__ meta, uint4 *__restrict__ body,
-                                                     int s, int f, int bx)
+                                                     uint16_t *__restrict__ meta, uint2 *__restrict__ blo,
+                                                     uint2 *__restrict__ bhi, int s, int f, int bx)
 {
     __shared__ uint4 lv[CODE_T];
     __shared__ uint16_t wc[CODE_NW][17];           /* per wave: blocks per TotalCoeff */
@@ -234,7 +248,7 @@ __device__ inline void code_frame(const DevStream *__restrict__ st,
     const uint8_t *fcb = fs + (size_t)256 * ndt, *fcr = fcb + (size_t)64 * ndt;
     const uint32_t m_rw = magic32((uint32_t)g.w);
     uint16_t *M = meta + nb * (size_t)(NPC * ndt);
-    uint4 *B = body + nb * (size_t)(NPC * ndt);
+    uint2 *BL = blo + nb * (size_t)(NPC * ndt), *BH = bhi + nb * (size_t)(NPC * ndt);
 
     const bool luma = task < 16 * ndt;
     const bool act = task < ntask;
@@ -367,12 +381,12 @@ __device__ inline void code_frame(const DevStream *__restrict__ st,
             if (cap.n <= 128) {
                 M[idx] = (uint16_t)(cap.n | (uint32_t)tc << 8);
                 if (cap.n)
-                    B[idx] = make_uint4((uint32_t)cap.lo, (uint32_t)(cap.lo >> 32), (uint32_t)cap.hi,
-                                        (uint32_t)(cap.hi >> 32));
+                    put_body(BL, BH, idx, make_uint4((uint32_t)cap.lo, (uint32_t)(cap.lo >> 32), (uint32_t)cap.hi,
+                                                     (uint32_t)(cap.hi >> 32)), cap.n > 64);
             } else {
                 M[idx] = (uint16_t)((uint32_t)tc << 8 | M_OVF);
-                B[idx] = make_uint4(((uint32_t)dq[0] & 0xffffu) | (uint32_t)dq[1] << 16,
-                                    ((uint32_t)dq[2] & 0xffffu) | (uint32_t)dq[3] << 16, 0u, 0u);
+                put_body(BL, BH, idx, make_uint4(((uint32_t)dq[0] & 0xffffu) | (uint32_t)dq[1] << 16,
+                                                 ((uint32_t)dq[2] & 0xffffu) | (uint32_t)dq[3] << 16, 0u, 0u), false);
             }
         }
     }
@@ -446,7 +460,7 @@ __device__ inline void code_frame(const DevStream *__restrict__ st,
     if (tt < ntask) {
         const uint16_t mm = mrec[t];
         M[tt] = mm;
-        if ((mm & 255u) || (mm & M_OVF)) B[tt] = lv[t];
+        if ((mm & 255u) || (mm & M_OVF)) put_body(BL, BH, tt, lv[t], (mm & 255u) > 64u || (mm & M_OVF));
     }
 }
 
@@ -458,9 +472,10 @@ __global__ __launch_bounds__(CODE_T) void k_dyn_code(const DevStream *__restrict
                                                      DynGeom g, const uint32_t *__restrict__ rows,
                                                      const uint8_t *__restrict__ src,
                                                      const uint8_t *__restrict__ refs,
-                                                     uint16_t *__restrict__ meta, uint4 *__restrict__ body)
+                                                     uint16_t *__restrict__ meta, uint2 *__restrict__ blo,
+                                                     uint2 *__restrict__ bhi)
 {
-    code_frame<false>(st, dfr, ld_fr, pend, nal, ld_nal, g, rows, src, refs, meta, body, blockIdx.z,
+    code_frame<false>(st, dfr, ld_fr, pend, nal, ld_nal, g, rows, src, refs, meta, blo, bhi, blockIdx.z,
                       blockIdx.y, blockIdx.x);
 }
 
@@ -468,7 +483,7 @@ __global__ __launch_bounds__(CODE_T) void k_dyn_code(const DevStream *__restrict
  * grid (chunks, CODE_GEN_Y), each workgroup finds flagged (stream, frame)
  * pairs 64 at a time -- a launch over every frame would cost more in empty
  * workgroups than the frames it serves */
-constexpr int CODE_GEN_Y = 8;
+constexpr int CODE_GEN_Y = 64;
 __global__ __launch_bounds__(CODE_T) void k_dyn_code_general(const DevStream *__restrict__ st,
                                                              const DynFrame *__restrict__ dfr, int ld_fr,
                                                              const PlanPending *__restrict__ pend,
@@ -477,7 +492,7 @@ __global__ __launch_bounds__(CODE_T) void k_dyn_code_general(const DevStream *__
                                                              const uint8_t *__restrict__ src,
                                                              const uint8_t *__restrict__ refs,
                                                              uint16_t *__restrict__ meta,
-                                                             uint4 *__restrict__ body, int nframes,
+                                                             uint2 *__restrict__ blo, uint2 *__restrict__ bhi, int nframes,
                                                              int nstreams)
 {
     const int lane = threadIdx.x & 63, np = nstreams * nframes;
@@ -494,7 +509,7 @@ __global__ __launch_bounds__(CODE_T) void k_dyn_code_general(const DevStream *__
             const int q = p0 + __builtin_ctzll(m);
             m &= m - 1;
             const int s = q / nframes, f = q - s * nframes;
-            code_frame<true>(st, dfr, ld_fr, pend, nal, ld_nal, g, rows, src, refs, meta, body, s, f,
+            code_frame<true>(st, dfr, ld_fr, pend, nal, ld_nal, g, rows, src, refs, meta, blo, bhi, s, f,
                              blockIdx.x);
             __syncthreads();
         }
@@ -686,7 +701,10 @@ __device__ __attribute__((noinline)) void ovf_put(uint32_t *buf, uint32_t lo, ui
  * flight per CU rather than from wide workgroups; LDS is sized to the rect
  * (dynamic shared memory, group_lds_bytes) */
 constexpr int GW = 64;
-constexpr int GBUF_WORDS = 256;          /* 8 Kbit per pass (a config-3 row: ~18 Kbit in 3 passes);
+#ifndef SCROLL_GBUF_WORDS
+#define SCROLL_GBUF_WORDS 256
+#endif
+constexpr int GBUF_WORDS = SCROLL_GBUF_WORDS;          /* 8 Kbit per pass (a config-3 row: ~18 Kbit in 3 passes);
                                            each pass walks only the MBs / rows it covers */
 
 struct GroupFixed {
@@ -728,7 +746,7 @@ __global__ __launch_bounds__(GW) void k_dyn_group(DevStream *__restrict__ st,
                                                   const PlanPending *__restrict__ pend,
                                                   DynFrame *__restrict__ dfr, int ld_fr, DynGeom g,
                                                   const uint16_t *__restrict__ meta,
-                                                  const uint4 *__restrict__ body,
+                                                  const uint2 *__restrict__ blo, const uint2 *__restrict__ bhi,
                                                   unsigned long long *__restrict__ status,
                                                   unsigned long long *__restrict__ tails, uint32_t epoch, int lines,
                                                   uint8_t *__restrict__ stage, uint64_t *__restrict__ stamps)
@@ -743,7 +761,7 @@ __global__ __launch_bounds__(GW) void k_dyn_group(DevStream *__restrict__ st,
     const size_t nb = (size_t)s * ld_fr + f;
     const int ndt = R.w * R.h;
     const uint16_t *M = meta + nb * (size_t)(NPC * ndt);
-    const uint4 *Bd = body + nb * (size_t)(NPC * ndt);
+    const uint2 *BL = blo + nb * (size_t)(NPC * ndt), *BH = bhi + nb * (size_t)(NPC * ndt);
     const bool first = gi == 0, last = gi == ng - 1, rect = !first && !last;
     const int row = rect ? R.y0 + gi - 1 : 0;
     const int nd = rect ? R.w : 0, npc = NPC * nd;
@@ -866,7 +884,7 @@ __global__ __launch_bounds__(GW) void k_dyn_group(DevStream *__restrict__ st,
                 piece_token(PT, mv, nC, tv, tl);
             }
             uint32_t len = tl + (mv & 255u);
-            if (mv & M_OVF) len = ovf_bits(PT, TB, Bd[rec_of(q0 + k, pc, ndt)], pc, nC);   /* rare: > 128 bits */
+            if (mv & M_OVF) len = ovf_bits(PT, TB, get_body(BL, BH, rec_of(q0 + k, pc, ndt), true), pc, nC);   /* rare */
             lo[i] = (uint16_t)(len | (uint32_t)(nC + 1) << 11);
         }
         __syncthreads();
@@ -1032,7 +1050,7 @@ __global__ __launch_bounds__(GW) void k_dyn_group(DevStream *__restrict__ st,
                     bd[u] = make_uint4(0, 0, 0, 0);
                     if (i < pb && off16[i] != 0xffffu && (mt[i] & (255u | M_OVF))) {
                         const int k = (int)div_m((uint32_t)i, m26);
-                        bd[u] = Bd[rec_of(q0 + k, i - k * NPC, ndt)];
+                        bd[u] = get_body(BL, BH, rec_of(q0 + k, i - k * NPC, ndt), (mt[i] & 255u) > 64u || (mt[i] & M_OVF));
                     }
                 }
 #pragma unroll
@@ -1513,10 +1531,10 @@ int dyn_launch_code(hipStream_t hs, int nframes, int S, const DevStream *st, con
     if (hipGetLastError() != hipSuccess) return -1;
     const int nchunk = (24 * g->w * g->h + CODE_T - 1) / CODE_T;
     hipLaunchKernelGGL(k_dyn_code, dim3(nchunk, nframes, S), dim3(CODE_T), 0, hs, st, dfr, ld_fr,
-                       pend, nal, ld_nal, *g, x->rows, src, refs, x->meta, x->body);
+                       pend, nal, ld_nal, *g, x->rows, src, refs, x->meta, x->body_lo, x->body_hi);
     if (hipGetLastError() != hipSuccess) return -1;
     hipLaunchKernelGGL(k_dyn_code_general, dim3(nchunk, CODE_GEN_Y), dim3(CODE_T), 0, hs, st, dfr, ld_fr,
-                       pend, nal, ld_nal, *g, x->rows, src, refs, x->meta, x->body, nframes, S);
+                       pend, nal, ld_nal, *g, x->rows, src, refs, x->meta, x->body_lo, x->body_hi, nframes, S);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -1529,7 +1547,7 @@ int dyn_launch_pack(hipStream_t hs, int nframes, int S, DevStream *st, const Nal
     const int ng = g->h + 2;
     const int lines = mbw > mbh ? mbw : mbh;
     hipLaunchKernelGGL(k_dyn_group, dim3(ng, nframes, S), dim3(GW), group_lds_bytes(g->w, lines), hs, st, nal,
-                       ld_nal, pend, dfr, ld_fr, *g, x->meta, x->body, x->status, x->tails, epoch, lines,
+                       ld_nal, pend, dfr, ld_fr, *g, x->meta, x->body_lo, x->body_hi, x->status, x->tails, epoch, lines,
                        stage, stamps);
     if (hipGetLastError() != hipSuccess) return -1;
     hipLaunchKernelGGL(k_dyn_ep, dim3(EP_G, nframes, S), dim3(EP_T), 0, hs, dfr, ld_fr, *g, stage);

@@ -1508,7 +1508,8 @@ static void dyn_release(ScrollBatch *b)
     (void)hipFree(b->d_stage);
     (void)hipFree(b->dx.rows);
     (void)hipFree(b->dx.meta);
-    (void)hipFree(b->dx.body);
+    (void)hipFree(b->dx.body_lo);
+    (void)hipFree(b->dx.body_hi);
     (void)hipFree(b->dx.status);
     (void)hipFree(b->dx.tails);
     b->d_dfr = nullptr;
@@ -1575,7 +1576,8 @@ int scroll_batch_set_dyn_rect(ScrollBatch *b, int x0, int y0, int w, int h, size
     if (e == hipSuccess) e = hipMalloc(&b->d_stage, S * F * g.slot_bytes);
     if (e == hipSuccess) e = hipMalloc(&b->dx.rows, S * F * 32 * h * sizeof(uint32_t));
     if (e == hipSuccess) e = hipMalloc(&b->dx.meta, S * F * DYN_PIECES * w * h * sizeof(uint16_t));
-    if (e == hipSuccess) e = hipMalloc(&b->dx.body, S * F * DYN_PIECES * w * h * sizeof(uint4));
+    if (e == hipSuccess) e = hipMalloc(&b->dx.body_lo, S * F * DYN_PIECES * w * h * sizeof(uint2));
+    if (e == hipSuccess) e = hipMalloc(&b->dx.body_hi, S * F * DYN_PIECES * w * h * sizeof(uint2));
     if (e == hipSuccess) e = hipMalloc(&b->dx.status, S * F * (h + 2) * sizeof(unsigned long long));
     if (e == hipSuccess) e = hipMalloc(&b->dx.tails, S * F * (h + 2) * sizeof(unsigned long long));
     if (e == hipSuccess) e = hipMemset(b->dx.tails, 0, S * F * (h + 2) * sizeof(unsigned long long));

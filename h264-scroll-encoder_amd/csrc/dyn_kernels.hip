@@ -1328,6 +1328,8 @@ __device__ inline uint32_t pick4(const uint32_t w[8], int i)     /* w[i], i in 0
     return (i & 4) ? ce : ab;
 }
 
+constexpr int GATHER_Z = 1;             /* workgroups per NAL (2 and 4 measured slower) */
+
 __global__ __launch_bounds__(DT) void k_dyn_emit_gather(const DevStream *__restrict__ st,
                                                         const NalDesc *__restrict__ nal, int ld_nal,
                                                         const DynFrame *__restrict__ dfr, int ld_fr,
@@ -1338,7 +1340,7 @@ __global__ __launch_bounds__(DT) void k_dyn_emit_gather(const DevStream *__restr
     __shared__ uint32_t raw[EPLIST_MAX], sp[EPLIST_MAX];
     const int s = blockIdx.y, f = dyn_frame_of(blockIdx.x, s), t = threadIdx.x;
     /* debug: realtime at entry / after the sort / at exit, EP count, HW_ID */
-    uint64_t *stp = stamps && t == 0 ? stamps + ((size_t)s * gridDim.x + f) * 8 : nullptr;
+    uint64_t *stp = stamps && t == 0 && blockIdx.z == 0 ? stamps + ((size_t)s * gridDim.x + f) * 8 : nullptr;
     if (stp) stp[0] = __builtin_amdgcn_s_memrealtime();
     const DynFrame df = dfr[(size_t)s * ld_fr + f];
     const int j = df.nal;
@@ -1372,10 +1374,13 @@ __global__ __launch_bounds__(DT) void k_dyn_emit_gather(const DevStream *__restr
     /* U chunks per thread and iteration: all their loads are in flight
      * before the first is used (the loop is load-latency bound otherwise) */
     constexpr int U = 4;
-    const uint64_t cend = (o1 + 15) >> 4;
+    /* the NAL's 16-byte chunks are split over gridDim.z workgroups */
+    const uint64_t cfirst = o0 >> 4, cnal = ((o1 + 15) >> 4) - cfirst;
+    const uint64_t per = (cnal + gridDim.z - 1) / gridDim.z;
+    const uint64_t cbeg = cfirst + per * blockIdx.z, cend = min(cfirst + cnal, cbeg + per);
     int lg = 0;                   /* binary-search steps: 2^lg > n */
     while ((1u << lg) <= n) lg++;
-    for (uint64_t cb = (o0 >> 4) + (uint64_t)t; cb < cend; cb += (uint64_t)U * DT) {
+    for (uint64_t cb = cbeg + (uint64_t)t; cb < cend; cb += (uint64_t)U * DT) {
         uint32_t Ku[U], epm[U], shv[U];
         bool inner[U];
         uint4 x[U], y[U];
@@ -1559,7 +1564,7 @@ int dyn_launch_emit(hipStream_t hs, int nframes, int S, const DevStream *st, con
                     const uint8_t *stage, uint8_t *arena, uint64_t ld_arena, uint64_t *stamps)
 {
     if (nframes <= 0 || S <= 0) return 0;
-    hipLaunchKernelGGL(k_dyn_emit_gather, dim3(nframes, S), dim3(DT), 0, hs, st, nal, ld_nal, dfr,
+    hipLaunchKernelGGL(k_dyn_emit_gather, dim3(nframes, S, GATHER_Z), dim3(DT), 0, hs, st, nal, ld_nal, dfr,
                        ld_fr, *g, stage, arena, ld_arena, stamps);
     if (hipGetLastError() != hipSuccess) return -1;
     hipLaunchKernelGGL(k_dyn_emit, dim3(nframes, S), dim3(DT), 0, hs, st, nal, ld_nal, dfr, ld_fr,

@@ -740,7 +740,7 @@ __device__ inline void piece_token(const PTabs &PT, uint32_t mv, int nC, uint32_
     }
 }
 
-/* grid (R.h + 2, frames, streams), GW threads */
+/* grid (g.ngroups, frames, streams), GW threads */
 __global__ __launch_bounds__(GW) void k_dyn_group(DevStream *__restrict__ st,
                                                   const NalDesc *__restrict__ nal, int ld_nal,
                                                   const PlanPending *__restrict__ pend,
@@ -762,8 +762,14 @@ __global__ __launch_bounds__(GW) void k_dyn_group(DevStream *__restrict__ st,
     const int ndt = R.w * R.h;
     const uint16_t *M = meta + nb * (size_t)(NPC * ndt);
     const uint2 *BL = blo + nb * (size_t)(NPC * ndt), *BH = bhi + nb * (size_t)(NPC * ndt);
-    const bool first = gi == 0, last = gi == ng - 1, rect = !first && !last;
-    const int row = rect ? R.y0 + gi - 1 : 0;
+    /* groups: nA static groups above the rect (the first one holds the slice
+     * header, and exists even with no rows), one per rect row, the static
+     * groups below (the last one holds the stop bit); DYN_STATIC_ROWS rows
+     * per static group */
+    constexpr int SR = DYN_STATIC_ROWS;
+    const int nA = max(1, (R.y0 + SR - 1) / SR);
+    const bool first = gi == 0, last = gi == ng - 1, rect = gi >= nA && gi < nA + R.h;
+    const int row = rect ? R.y0 + gi - nA : 0;
     const int nd = rect ? R.w : 0, npc = NPC * nd;
     const int q0 = rect ? (row - R.y0) * R.w : 0;
     uint32_t *moff = gdyn, *mbits = moff + lines + 1;
@@ -832,7 +838,17 @@ __global__ __launch_bounds__(GW) void k_dyn_group(DevStream *__restrict__ st,
     const int mbw = H.mbw, mbh = c.h / 16;
     const Tabs &TB = g_tabs;
     const PTabs &PT = L.ptabs;
-    const int ra = first ? 0 : (rect ? row : R.y0 + R.h), rb = first ? R.y0 : (rect ? row + 1 : mbh);
+    int ra, rb;
+    if (gi < nA) {
+        ra = gi * SR;
+        rb = min(ra + SR, R.y0);
+    } else if (rect) {
+        ra = row;
+        rb = row + 1;
+    } else {
+        ra = R.y0 + R.h + (gi - nA - R.h) * SR;
+        rb = min(ra + SR, mbh);
+    }
     uint32_t F = 0;
     if (first) {
         CountSink hc{0};
@@ -1549,7 +1565,7 @@ int dyn_launch_pack(hipStream_t hs, int nframes, int S, DevStream *st, const Nal
                     uint64_t *stamps, int mbw, int mbh)
 {
     if (nframes <= 0 || S <= 0) return 0;
-    const int ng = g->h + 2;
+    const int ng = g->ngroups;
     const int lines = mbw > mbh ? mbw : mbh;
     hipLaunchKernelGGL(k_dyn_group, dim3(ng, nframes, S), dim3(GW), group_lds_bytes(g->w, lines), hs, st, nal,
                        ld_nal, pend, dfr, ld_fr, *g, x->meta, x->body_lo, x->body_hi, x->status, x->tails, epoch, lines,

@@ -82,11 +82,12 @@ typedef struct {
 #define DYN_MAX_H 48                /* rect height limit (MBs)                    */
 #define DYN_MAX_MBW 512             /* picture width limit with the rect (MBs)   */
 #define DYN_MAX_MBH 512             /* picture height limit with the rect (MBs)  */
+#define DYN_STATIC_ROWS 64          /* MB rows per static k_dyn_group row group (4 measured slower) */
 #define DYN_PIECES 26               /* coded pieces per dynamic MB: 16 luma, 2 DC, 8 AC */
 #define DYN_OVF_BYTES 8192          /* staging-slot tail: levels of > 128-bit blocks */
 typedef struct {
     int32_t x0, y0, w, h;           /* rect, MB units                             */
-    int32_t pad0;
+    int32_t ngroups;                /* k_dyn_group row groups per NAL (dyn_groups) */
     int32_t debug;                  /* SCROLL_DEBUG_DYN_* ablation bits           */
     uint64_t src_ld, src_fr;        /* source bytes per stream / per frame        */
     uint64_t ref_ld;                /* reference-pair bytes per stream (0 shared) */

@@ -1228,7 +1228,7 @@ static int launch(ScrollBatch *b, int nframes, int plan_mode, int nal_max, hipSt
         if ((rc = mark(1))) return rc;
         uint64_t *stamps = nullptr;
         if (b->debug & SCROLL_DEBUG_DYN_STAMPS) {   /* k_dyn_emit_gather's, then k_dyn_group's */
-            const size_t slots = (2 + (size_t)b->geo.h + 2) * (size_t)nframes * S;
+            const size_t slots = (2 + (size_t)b->geo.ngroups) * (size_t)nframes * S;
             if (slots > b->dbg_slots) {
                 if (b->d_dbg) (void)hipFree(b->d_dbg);
                 HIPCHK(hipMalloc(&b->d_dbg, slots * 8 * sizeof(uint64_t)));
@@ -1563,6 +1563,11 @@ int scroll_batch_set_dyn_rect(ScrollBatch *b, int x0, int y0, int w, int h, size
     g.y0 = y0;
     g.w = w;
     g.h = h;
+    {
+        const int sr = DYN_STATIC_ROWS;
+        const int na = (y0 + sr - 1) / sr, nbl = (mbh - y0 - h + sr - 1) / sr;
+        g.ngroups = (na > 1 ? na : 1) + h + (nbl > 1 ? nbl : 1);
+    }
     g.src_fr = (uint64_t)384 * w * h;
     g.src_ld = round256((size_t)b->max_frames * g.src_fr);
     g.ref_ld = 0;
@@ -1578,10 +1583,11 @@ int scroll_batch_set_dyn_rect(ScrollBatch *b, int x0, int y0, int w, int h, size
     if (e == hipSuccess) e = hipMalloc(&b->dx.meta, S * F * DYN_PIECES * w * h * sizeof(uint16_t));
     if (e == hipSuccess) e = hipMalloc(&b->dx.body_lo, S * F * DYN_PIECES * w * h * sizeof(uint2));
     if (e == hipSuccess) e = hipMalloc(&b->dx.body_hi, S * F * DYN_PIECES * w * h * sizeof(uint2));
-    if (e == hipSuccess) e = hipMalloc(&b->dx.status, S * F * (h + 2) * sizeof(unsigned long long));
-    if (e == hipSuccess) e = hipMalloc(&b->dx.tails, S * F * (h + 2) * sizeof(unsigned long long));
-    if (e == hipSuccess) e = hipMemset(b->dx.tails, 0, S * F * (h + 2) * sizeof(unsigned long long));
-    if (e == hipSuccess) e = hipMemset(b->dx.status, 0, S * F * (h + 2) * sizeof(unsigned long long));
+    const size_t ng = (size_t)g.ngroups;
+    if (e == hipSuccess) e = hipMalloc(&b->dx.status, S * F * ng * sizeof(unsigned long long));
+    if (e == hipSuccess) e = hipMalloc(&b->dx.tails, S * F * ng * sizeof(unsigned long long));
+    if (e == hipSuccess) e = hipMemset(b->dx.tails, 0, S * F * ng * sizeof(unsigned long long));
+    if (e == hipSuccess) e = hipMemset(b->dx.status, 0, S * F * ng * sizeof(unsigned long long));
     b->dx.epoch = 0;
     if (e == hipSuccess) e = hipMemset(b->d_dfr, 0, S * F * sizeof(DynFrame));
     if (e == hipSuccess) e = hipMemset(b->d_src, 0, S * g.src_ld);

@@ -81,14 +81,17 @@ def main():
     b.set_debug(hs.SCROLL_DEBUG_DYN_STAMPS)
     b.compose(F, rewind=True)
     assert b.sync() == 0, hs.last_error()
-    ng = rect[3] + 2
+    mbh = H // 16
+    na = max(1, -(-rect[1] // 64))                 # DYN_STATIC_ROWS = 64
+    ng = na + rect[3] + max(1, -(-(mbh - rect[1] - rect[3]) // 64))
     nslot = (2 + ng) * S * F
     buf = (ctypes.c_uint64 * (nslot * 8))()
     got = hs.lib.scroll_batch_debug_stamps(b.h, buf, nslot)
     allst = np.frombuffer(buf, dtype=np.uint64).reshape(-1, 8)[:got]
     grp = allst[2 * S * F:].astype(np.int64).reshape(S * F, ng, 8)
     names = ["load+tok", "mb", "scan", "lookback", "write"]
-    for label, sel in (("rect rows", slice(1, ng - 1)), ("group 0", slice(0, 1)), ("last group", slice(ng - 1, ng))):
+    for label, sel in (("rect rows", slice(na, na + rect[3])), ("static above", slice(0, na)),
+                       ("static below", slice(na + rect[3], ng))):
         gsel = grp[:, sel].reshape(-1, 8)
         gsel = gsel[gsel[:, 5] > 0]
         st = gsel[:, :6].astype(np.float64)

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """bench.py -- composed frames/s of the MI355X scroll composer.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload p720dyn|p720|p4kdyn|p720hint]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload p720dyn|p720|p4kdyn|p720hint|ingest720|ipcm720]
 
 One process per GPU (torch.distributed.run for N > 1; RANK / LOCAL_RANK /
 WORLD_SIZE from the env).  Streams are independent, so each rank owns a static
@@ -24,6 +24,9 @@ A step = one scroll_batch_compose over every stream of the rank:
   streams x 16 composed 1280x720 frames whose scroll NALs carry a UI overlay
   (static chrome and side panel, a horizontally scrolling carousel) in the
   P_Skip mode, coded per MB by k_hint_stage.
+  workload ipcm720 (metric: reference files/s): a step =
+  scroll_batch_ipcm_files_device of 256 random 1280x720 I420 pictures in HBM
+  -> 256 SPS+PPS+I_PCM IDR files in HBM (the files ingest720 reads).
   workload ingest720 (metric: ingested streams/s): a
   step = scroll_batch_ingest_device of 256 new streams whose 1280x720 I_PCM
   reference files (A, B; one copy per stream) are resident in HBM --
@@ -64,6 +67,9 @@ WORKLOADS = {
     "ingest720": dict(w=1280, h=720, streams=256, frames=1, rect=None, ingest=True,
                       desc="stream ingest (SURVEY 8f rows 3-4): 256 new 1280x720 streams per step, "
                            "composer_init + composer_write_header from I_PCM reference files in HBM"),
+    "ipcm720": dict(w=1280, h=720, streams=256, frames=1, rect=None, ipcm=True,
+                    desc="reference files from pictures (SURVEY 8f row 3): 256 1280x720 I420 "
+                         "pictures in HBM -> 256 SPS+PPS+I_PCM IDR Annex-B files in HBM per step"),
     "p720hint": dict(w=1280, h=720, streams=256, frames=16, rect=None, hints=True,
                      desc="UI hints (SURVEY 8f row 1): 256 concurrent 1280x720 streams, scroll "
                           "frames with a static chrome / side panel / horizontal carousel "
@@ -214,6 +220,86 @@ def run_ingest(args, wl, rank, world, local, dist):
         if world == 1 and not args.no_cpu:
             out["cpu_baseline"] = cpu_baseline_ingest((fa, fb))
         print(json.dumps(out), flush=True)
+    b.close()
+
+
+def cpu_baseline_ipcm(pics, w, h):
+    """or_ipcm_picture_file (oracle/scroll_oracle.c) on one host core over the
+    given pictures"""
+    repo_oracle = os.path.join(HERE, "oracle")
+    so = os.path.join(repo_oracle, "_build", "liboracle.so")
+    if not os.path.exists(so):
+        import subprocess
+        subprocess.run(["make", "-s", "-C", repo_oracle], check=True)
+    lib = ctypes.CDLL(so)
+    lib.or_ipcm_picture_file.restype = ctypes.c_size_t
+    cap = 2 * w * h + (1 << 16)
+    buf = (ctypes.c_uint8 * cap)()
+    t0 = time.perf_counter()
+    for p in pics:
+        if not lib.or_ipcm_picture_file(buf, cap, w, h, p.ctypes.data_as(ctypes.c_void_p)):
+            raise RuntimeError("oracle I_PCM writer failed")
+    fps = len(pics) / (time.perf_counter() - t0)
+    return dict(value=round(fps, 2), unit="files/s", cores=1, kind="port",
+                sample=f"{len(pics)} random {w}x{h} I420 pictures, 1 thread, "
+                       f"oracle/scroll_oracle.c or_ipcm_picture_file -O2")
+
+
+def run_ipcm(args, wl, rank, world, local, dist):
+    import numpy as np
+    import torch
+    import h264scroll as hs
+    torch.cuda.set_device(local)
+    W, H, S = wl["w"], wl["h"], wl["streams"]
+    pic = W * H * 3 // 2
+    g = torch.Generator(device=f"cuda:{local}").manual_seed(1234 + rank)
+    pics = torch.randint(0, 256, (S, pic), dtype=torch.uint8, device=f"cuda:{local}", generator=g)
+    ostride = ((3 * (W * H * 193 // 128)) // 2 + 128 + 255) & ~255
+    out = torch.empty(S * ostride, dtype=torch.uint8, device=f"cuda:{local}")
+    b = hs.Batch(1, 1, 1 << 16, device=local)
+    torch.cuda.synchronize()
+
+    def barrier():
+        torch.cuda.synchronize()
+        if dist:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        sizes = b.ipcm_files_device(S, W, H, pics.data_ptr(), pic, out.data_ptr(), ostride)
+    b.enable_timing(True)
+    b.ipcm_stats()
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        sizes = b.ipcm_files_device(S, W, H, pics.data_ptr(), pic, out.data_ptr(), ostride)
+    barrier()
+    t1 = time.perf_counter()
+    kms, kn = b.ipcm_stats()
+    b.enable_timing(False)
+    el = max_over_ranks(t1 - t0, dist)
+    if rank == 0:
+        k_ms = kms / max(kn, 1)
+        alg = S * pic + sum(sizes)                       # pictures in, files out
+        achieved = alg / (k_ms * 1e-3) / 1e9
+        res = {
+            "metric": "reference files/s (1280x720 I420 picture -> SPS+PPS+I_PCM IDR Annex-B file); "
+                      "bit-exact vs CPU",
+            "value": round(S * args.steps * world / el, 1),
+            "unit": "files/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(1000.0 * el / args.steps, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
+            "config": {"workload": wl["desc"], "resolution": f"{W}x{H}", "files_per_step": S,
+                       "parallelism": f"static shard x{world}, no RCCL"},
+            "bytes_per_file": {"in": pic, "out": round(sum(sizes) / S, 1)},
+            "roofline": {"bound": "hbm", "kernel": "k_ipcm (count + write passes)",
+                         "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                         "alg_bytes_per_launch": alg, "kernel_ms_avg": round(k_ms, 4)},
+        }
+        if world == 1 and not args.no_cpu:
+            host = pics[:8].cpu().numpy()
+            res["cpu_baseline"] = cpu_baseline_ipcm([np.ascontiguousarray(p) for p in host], W, H)
+        print(json.dumps(res), flush=True)
     b.close()
 
 
@@ -374,8 +460,8 @@ def main():
         import torch.distributed as dist
         dist.init_process_group("gloo")
 
-    if wl.get("ingest"):
-        run_ingest(args, wl, rank, world, local, dist)
+    if wl.get("ingest") or wl.get("ipcm"):
+        (run_ingest if wl.get("ingest") else run_ipcm)(args, wl, rank, world, local, dist)
         if dist:
             dist.destroy_process_group()
         return

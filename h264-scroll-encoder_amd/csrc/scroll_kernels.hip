@@ -2012,7 +2012,11 @@ int scroll_batch_ipcm_files_device(ScrollBatch *b, int n, int w, int h, const ui
         b->ipcm_cap = need;
     }
     hipStream_t hs = b->own;
-    if (b->timing) HIPCHK(hipEventRecord(b->ing_ev[0], hs));
+    if (b->timing) {
+        for (hipEvent_t &e : b->ing_ev)                  /* created lazily, shared with ingest */
+            if (!e) HIPCHK(timing_event(&e));
+        HIPCHK(hipEventRecord(b->ing_ev[0], hs));
+    }
     if (ipcm_launch(hs, 0, n, &g, d_pics, b->d_ipcm_cnt, d_out)) {
         set_err("ipcm launch: %s", hipGetErrorString(hipGetLastError()));
         return SCROLL_ERR_HIP;

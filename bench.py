@@ -537,7 +537,7 @@ def main():
         if rect and kms["dyn_code"] >= kms["dyn_pack"]:
             # k_dyn_rows + k_dyn_code per launch: the source and prediction
             # samples of every dynamic MB (384 B each) read; the block
-            # records they write for k_dyn_pack are not algorithmic bytes
+            # records they write for k_dyn_group are not algorithmic bytes
             kern = "k_dyn_code"
             alg_bytes = dyn_nals * 2 * 384 * rect[2] * rect[3]
             kern_ms = kms["dyn_code"]

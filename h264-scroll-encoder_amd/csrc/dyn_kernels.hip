@@ -3,15 +3,18 @@
  * coder (BASELINE configs 3-5).  A scroll NAL with the rect is no longer a
  * handful of periodic runs: every dynamic MB carries a CAVLC residual, and
  * 60 % of such NALs need emulation prevention.  So these NALs take their own
- * two kernels around the plan's sizing pass:
+ * kernels around the plan's sizing pass:
  *
  *   k_plan (state pass)   waypoint state machine, NalDesc per NAL
- *   k_dyn_stage           one workgroup per dynamic NAL: its whole RBSP into
- *                         a staging slot + its exact emulation-prevention count
+ *   k_dyn_rows            per NAL: prediction row offsets (waypoint chains)
+ *   k_dyn_code[_general]  per 4x4 block: transform, quant, CAVLC body -> records
+ *   k_dyn_group           one wave per MB-row group: tokens, cbp, offsets,
+ *                         start bit by look-back, bits -> staging slot
+ *   k_dyn_ep              emulation-prevention positions + count
  *   k_plan (size pass)    NAL sizes (dynamic: 5 + RBSP + EP), arena offsets
  *   k_emit                every other NAL (dynamic NALs are "external")
- *   k_dyn_emit            staged RBSP -> arena: start code, NAL header, EP
- *                         bytes, written in whole 128-byte lines
+ *   k_dyn_emit_gather     staged RBSP -> arena: start code, NAL header, EP
+ *                         bytes, 16-byte chunks (k_dyn_emit: > 2048 EP bytes)
  *
  * The bits are those of oracle/dyn_oracle.c (or_scroll_nal_dyn); parity is
  * checked bit-exact by tests/test_gpu_dyn.py.  Roofline: HBM (source pixels
@@ -1331,7 +1334,7 @@ __global__ __launch_bounds__(DT) void k_dyn_emit(const DevStream *__restrict__ s
 
 /* ---------------------------------------------------------------------- */
 /* k_dyn_emit_gather: the same output for NALs with <= EPLIST_MAX EP bytes  */
-/* (all in practice: 82 per config-3 frame).  k_dyn_stage recorded where    */
+/* (all in practice: 82 per config-3 frame).  k_dyn_ep recorded where       */
 /* the 03 bytes go; after sorting those positions once, every thread builds */
 /* whole 16-byte arena chunks independently -- no barriers, no LDS byte     */
 /* buffer: a chunk without an EP byte is a funnel shift of the staged RBSP. */
@@ -1601,7 +1604,7 @@ int dyn_launch_synth(hipStream_t hs, int nframes, int S, uint8_t *src, const Dyn
 size_t dyn_slot_bound(int mbw, int mbh, int rw, int rh)
 {
     /* header + every MB head (+ cbp) + every dynamic MB at its provable
-     * maximum + the stop word + k_dyn_stage's 16-byte margin */
+     * maximum + the stop word + a 16-byte read margin (k_dyn_ep) */
     const size_t bits = (size_t)HDR_MAX + (size_t)mbw * mbh * (HEAD_MAX + 1) +
                         (size_t)rw * rh * MB_BITS_MAX + 64;
     return ((bits / 8 + 32 + DYN_OVF_BYTES) + 255) & ~(size_t)255;

@@ -1,7 +1,7 @@
 /*
  * hint_engine.h -- host-side launcher of the UI-hint stage kernel
  * (hint_kernels.hip); the batch (scroll_kernels.hip) drives it between the
- * plan's state and size passes, like k_dyn_stage.
+ * plan's state and size passes, like the dynamic-rect coder.
  */
 #pragma once
 

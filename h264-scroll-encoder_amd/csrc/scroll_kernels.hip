@@ -105,7 +105,7 @@ __device__ inline NalCtx make_ctx(const int32_t *cfg, const int32_t *wo, const i
 /*  phase 2 (all waves): exact size of every NAL (run layout, or the serial */
 /*          path when emulation prevention / long codes are possible), and  */
 /*          a block scan -> byte offset of every NAL in the stream arena.   */
-/* With the dynamic rect the kernel runs twice around k_dyn_stage: a state  */
+/* With the dynamic rect the kernel runs twice around the dynamic coder: a  */
 /* pass (PLAN_STATE: phase 1, totals + final table to PlanPending, frame -> */
 /* scroll NAL map to DynFrame) and a size pass (PLAN_SIZE: phase 2, sizes   */
 /* of dynamic NALs from DynFrame).                                          */
@@ -906,7 +906,7 @@ struct ScrollBatch {
     DynGeom geo{};
     DynFrame *d_dfr = nullptr;
     uint8_t *d_src = nullptr, *d_refs = nullptr, *d_stage = nullptr;
-    DynScratch dx{};                   /* rows + block records of k_dyn_code / k_dyn_pack */
+    DynScratch dx{};                   /* rows, block records, look-back words of the dynamic coder */
     /* UI hints: staged like the dynamic rect (shares
      * d_dfr, d_stage and geo.slot_bytes; the two are exclusive) */
     int hint_on = 0;
@@ -1257,7 +1257,7 @@ static int launch(ScrollBatch *b, int nframes, int plan_mode, int nal_max, hipSt
             if (dyn_launch_pack(hs, nframes, S, b->d_st, b->d_nal, b->ld_nal, b->d_pend, b->d_dfr,
                                 ld_fr, &b->geo, &b->dx, b->d_stage, b->dx.epoch, stamps,
                                 b->dyn_pw / 16, b->dyn_ph / 16)) {
-                set_err("k_dyn_pack launch: %s", hipGetErrorString(hipGetLastError()));
+                set_err("k_dyn_group launch: %s", hipGetErrorString(hipGetLastError()));
                 return SCROLL_ERR_HIP;
             }
         }

@@ -1,6 +1,6 @@
 /*
  * stage_util.h -- device helpers shared by the kernels that stage a whole
- * NAL's RBSP in a slot (k_dyn_stage, k_hint_stage) and by k_dyn_emit_gather:
+ * NAL's RBSP in a slot (k_dyn_group / k_dyn_ep, k_hint_stage) and by k_dyn_emit_gather:
  * workgroup scans, the LDS OR bit sink, the emulation-prevention recorder
  * and the XCD-mixing frame rotation.  Workgroups are NW waves of 64.
  */

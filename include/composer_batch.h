@@ -58,8 +58,8 @@ extern "C" {
 #define SCROLL_DEBUG_EMIT_NOMIXED 32 /* k_emit skips the mixed-chunk phase        */
 #define SCROLL_DEBUG_EMIT_STAMPS 64 /* k_emit records s_memtime per phase per wave */
 #define SCROLL_DEBUG_EMIT_NOBYTES 128 /* k_emit skips the tile-end partial chunks  */
-#define SCROLL_DEBUG_DYN_STAMPS 256 /* k_dyn_stage: s_memtime per phase per NAL   */
-/* k_dyn_stage ablations (builds with -DSCROLL_DYN_ABLATE=1 only; timing only, outputs
+#define SCROLL_DEBUG_DYN_STAMPS 256 /* k_dyn_group / gather: realtime per phase  */
+/* dynamic-coder ablations (builds with -DSCROLL_DYN_ABLATE=1 only; timing only, outputs
  * wrong): skip the pixel loads /
  * the block CAVLC / the MB-head work / the bit writes */
 #define SCROLL_DEBUG_DYN_NOLOAD  512
@@ -115,7 +115,7 @@ int scroll_batch_nal_info(ScrollBatch *b, int s, int i, int *kind, int *offset_p
 
 /* HIP-event timing of the last compose's kernels, on the launch stream:
  * which 0 = plan kernel(s), 1 = emit kernel, 2 = dyn stage, 3 = dyn emit,
- * 4 = dyn code (k_dyn_rows + k_dyn_code), 5 = dyn pack (k_dyn_pack).
+ * 4 = dyn code (k_dyn_rows + k_dyn_code), 5 = dyn pack (k_dyn_group + k_dyn_ep).
  * Enable before compose. */
 int scroll_batch_enable_timing(ScrollBatch *b, int on);
 float scroll_batch_kernel_ms(ScrollBatch *b, int which);
@@ -162,7 +162,7 @@ int scroll_batch_dyn_totals(ScrollBatch *b, unsigned long long *rbsp_bytes,
                             unsigned long long *ep_bytes, long long *dyn_nals);
 /* HIP-event ms of the timed composes since the last call: plan (both
  * passes), emit, dyn stage (= dyn code + dyn pack), dyn emit, dyn code
- * (k_dyn_rows + k_dyn_code), dyn pack (k_dyn_pack); accumulators reset
+ * (k_dyn_rows + k_dyn_code), dyn pack (k_dyn_group + k_dyn_ep); accumulators reset
  * afterwards */
 int scroll_batch_kernel_stats_ex(ScrollBatch *b, double ms[6], int *count);
 

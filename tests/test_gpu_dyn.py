@@ -1,5 +1,6 @@
 """GPU parity of the dynamic-rect residual coder (BASELINE configs 3-5):
-k_plan (state) -> k_dyn_stage -> k_plan (size) -> k_emit -> k_dyn_emit,
+k_plan (state) -> k_dyn_rows -> k_dyn_code -> k_dyn_group -> k_dyn_ep -> k_plan (size) -> k_emit
+-> k_dyn_emit_gather / k_dyn_emit,
 through the C ABI, against the CPU restatement oracle/dyn_oracle.c
 (or_compose_dyn), byte for byte.  The reference has no implementation of
 this path, so these bits are pinned only by the restatement, which
@@ -242,7 +243,7 @@ def test_dyn_chunked_composes_and_experiment_mode(gpu, oracle):
 
 def test_dyn_half_pel_waypoint_chain(gpu, oracle):
     """a resumed config with a waypoint at an odd offset: its rows predict at
-    half-pel chroma positions, which only the general k_dyn_stage path does"""
+    half-pel chroma positions, which only the general k_dyn_code path does"""
     w, h = 64, 1024
     rect = Rect(1, 0, 2, 48)
     wps = [(501, 2, 1)]

@@ -743,6 +743,16 @@ __device__ inline void piece_token(const PTabs &PT, uint32_t mv, int nC, uint32_
     }
 }
 
+/* k_dyn_group's workgroup is ONE wave: its LDS handoffs need ordering, not a
+ * workgroup barrier (whose release fence would also wait for every global
+ * store of the wave to complete) */
+__device__ inline void wave_sync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 /* grid (g.ngroups, frames, streams), GW threads */
 __global__ __launch_bounds__(GW) void k_dyn_group(DevStream *__restrict__ st,
                                                   const NalDesc *__restrict__ nal, int ld_nal,
@@ -835,7 +845,7 @@ __global__ __launch_bounds__(GW) void k_dyn_group(DevStream *__restrict__ st,
     load_ptabs(L.ptabs, t, GW);
     DevStream *S = st + s;
     const NalDesc d = nal[(size_t)s * ld_nal + j];
-    __syncthreads();                                        /* waypoint table, ptabs, records */
+    wave_sync();                                        /* waypoint table, ptabs, records */
     const NalCtx c = nal_ctx(S, d, L.wo, L.wl, L.wv);
     const HeadCtx H = head_ctx(c);
     const int mbw = H.mbw, mbh = c.h / 16;
@@ -866,7 +876,7 @@ __global__ __launch_bounds__(GW) void k_dyn_group(DevStream *__restrict__ st,
         L.hlen[t] = hc.n;
         if (hc.over()) L.head_over = 1;
     }
-    __syncthreads();
+    wave_sync();
     const bool head_over = L.head_over;
     auto head_bits = [&](int r, int col) -> uint32_t {
         if (!head_over) return L.hlen[H.sel(r, col)];
@@ -906,7 +916,7 @@ __global__ __launch_bounds__(GW) void k_dyn_group(DevStream *__restrict__ st,
             if (mv & M_OVF) len = ovf_bits(PT, TB, get_body(BL, BH, rec_of(q0 + k, pc, ndt), true), pc, nC);   /* rare */
             lo[i] = (uint16_t)(len | (uint32_t)(nC + 1) << 11);
         }
-        __syncthreads();
+        wave_sync();
         if (stamps) stv[1] = __builtin_amdgcn_s_memrealtime();
         /* per dynamic MB: cbp, its code, piece offsets, bits */
         for (int k = t; k < nd; k += GW) {
@@ -945,7 +955,7 @@ __global__ __launch_bounds__(GW) void k_dyn_group(DevStream *__restrict__ st,
             cbpa[k] = (uint8_t)cbp;
             codea[k] = (uint8_t)code;
         }
-        __syncthreads();
+        wave_sync();
         if (stamps) stv[2] = __builtin_amdgcn_s_memrealtime();
         uint32_t carry = 0;
         for (int c0 = 0; c0 < mbw; c0 += GW) {
@@ -1025,7 +1035,7 @@ __global__ __launch_bounds__(GW) void k_dyn_group(DevStream *__restrict__ st,
         const uint32_t p0 = (uint32_t)pi * GBUF_WORDS;
         const uint32_t n = min((uint32_t)GBUF_WORDS, nw - p0);
         for (uint32_t i = (uint32_t)t; i < n; i += GW) L.buf[i] = 0u;
-        __syncthreads();
+        wave_sync();
         const LdsOrWin win{L.buf, p0, n};
         /* the entries (rect: MB columns, static: rows) whose bits meet the
          * window [32 p0, 32 (p0 + n)): [ea, eb), by binary search on moff */
@@ -1132,7 +1142,7 @@ __global__ __launch_bounds__(GW) void k_dyn_group(DevStream *__restrict__ st,
                 sk.finish();
             }
         }
-        __syncthreads();
+        wave_sync();
         for (uint32_t i = (uint32_t)t; i < n; i += GW) {
             const uint32_t q = p0 + i, v = L.buf[i];
             const uint64_t gw = w0 + q;
@@ -1146,7 +1156,7 @@ __global__ __launch_bounds__(GW) void k_dyn_group(DevStream *__restrict__ st,
                 out[gw] = __builtin_bswap32(v);
             }
         }
-        __syncthreads();
+        wave_sync();
     }
     if (stamps && t == 0) {
         stv[5] = __builtin_amdgcn_s_memrealtime();

@@ -224,7 +224,6 @@ __device__ inline void code_frame(const DevStream *__restrict__ st,
     __shared__ uint4 lv[CODE_T];
     __shared__ uint16_t wc[CODE_NW][17];           /* per wave: blocks per TotalCoeff */
     __shared__ uint16_t order[CODE_T];
-    __shared__ uint16_t mrec[CODE_T];
     __shared__ PTabs ptabs;
     __shared__ int32_t wo[8], wv[8];
     const int t = threadIdx.x;
@@ -446,24 +445,19 @@ __device__ inline void code_frame(const DevStream *__restrict__ st,
         tc = cavlc_body(cap, ptabs, q, ul ? 16 : 15, t1, ok);
 #endif
     }
-    /* back to task order through LDS: the records of a workgroup's tasks are
-     * contiguous (rec_of), so the stores coalesce */
-    __syncthreads();
-    if (ok) {
-        mrec[u] = (uint16_t)(cap.n | (uint32_t)tc << 8 | (uint32_t)t1 << 13);
-        lv[u] = make_uint4((uint32_t)cap.lo, (uint32_t)(cap.lo >> 32), (uint32_t)cap.hi, (uint32_t)(cap.hi >> 32));
-    } else {
-        mrec[u] = (uint16_t)((uint32_t)tc << 8 | (uint32_t)t1 << 13 | M_OVF);       /* lv[u] keeps the levels */
-    }
-    __syncthreads();
-    const int tt = bx * CODE_T + t;
-#ifdef SCROLL_ABL_NOSTORE
-    if (tc == 99)
-#endif
-    if (tt < ntask) {
-        const uint16_t mm = mrec[t];
-        M[tt] = mm;
-        if ((mm & 255u) || (mm & M_OVF)) put_body(BL, BH, tt, lv[t], (mm & 255u) > 64u || (mm & M_OVF));
+    /* each lane stores its own block's record (task order, so a workgroup's
+     * records are one contiguous range; un-sorting through LDS first was
+     * measured 3 % slower: light waves waited at its barrier for the heavy one) */
+    if (tk < ntask) {
+        const uint16_t mm = ok ? (uint16_t)(cap.n | (uint32_t)tc << 8 | (uint32_t)t1 << 13)
+                               : (uint16_t)((uint32_t)tc << 8 | (uint32_t)t1 << 13 | M_OVF);
+        M[tk] = mm;
+        if ((mm & 255u) || (mm & M_OVF))
+            put_body(BL, BH, tk,
+                     ok ? make_uint4((uint32_t)cap.lo, (uint32_t)(cap.lo >> 32), (uint32_t)cap.hi,
+                                     (uint32_t)(cap.hi >> 32))
+                        : v4,
+                     (mm & 255u) > 64u || (mm & M_OVF));
     }
 }
 

@@ -710,7 +710,7 @@ struct GroupFixed {
     uint32_t hlen[12];
     int32_t head_over;
     int32_t wo[8], wl[8], wv[8];
-    PTabs ptabs;
+    uint16_t ct[3][68];                 /* coeff_token tables (nC 0-1, 2-3, 4-7), PTabs layout */
 };
 
 /* dynamic LDS: moff [lines + 1] u32, mbits [w] u32, mt, lo, off16 [NPC w]
@@ -724,14 +724,14 @@ __host__ __device__ inline size_t group_lds_bytes(int w, int lines)
 constexpr uint32_t LO_LEN = 0x7ffu;
 
 /* coeff_token of a piece with meta mv at context nC >= 0 (Table 9-5) */
-__device__ inline void piece_token(const PTabs &PT, uint32_t mv, int nC, uint32_t &tv, uint32_t &tl)
+__device__ inline void piece_token(const uint16_t (*ct)[68], uint32_t mv, int nC, uint32_t &tv, uint32_t &tl)
 {
     const int tc = tc_of(mv), t1 = (int)((mv >> 13) & 3u);
     if (nC >= 8) {
         tv = tc ? (uint32_t)(((tc - 1) << 2) | t1) : 3u;
         tl = 6;
     } else {
-        const uint32_t e = PT.ct[nC < 2 ? 0 : (nC < 4 ? 1 : 2)][4 * tc + t1];
+        const uint32_t e = ct[nC < 2 ? 0 : (nC < 4 ? 1 : 2)][4 * tc + t1];
         tv = e & 255u;
         tl = e >> 8;
     }
@@ -836,7 +836,9 @@ __global__ __launch_bounds__(GW) void k_dyn_group(DevStream *__restrict__ st,
         L.wv[t] = pend[s].wv[t];
     }
     if (t == 0) L.head_over = 0;
-    load_ptabs(L.ptabs, t, GW);
+    static_assert(sizeof(L.ct) % 8 == 0, "ct copies as uint2");
+    for (int i = t; i < (int)(sizeof(L.ct) / 8); i += GW)      /* only coeff_token lives in LDS here */
+        reinterpret_cast<uint2 *>(&L.ct[0][0])[i] = reinterpret_cast<const uint2 *>(&g_ptabs.ct[0][0])[i];
     DevStream *S = st + s;
     const NalDesc d = nal[(size_t)s * ld_nal + j];
     wave_sync();                                        /* waypoint table, ptabs, records */
@@ -844,7 +846,7 @@ __global__ __launch_bounds__(GW) void k_dyn_group(DevStream *__restrict__ st,
     const HeadCtx H = head_ctx(c);
     const int mbw = H.mbw, mbh = c.h / 16;
     const Tabs &TB = g_tabs;
-    const PTabs &PT = L.ptabs;
+    const PTabs &PT = *reinterpret_cast<const PTabs *>(&g_ptabs);   /* the rare overflow paths */
     int ra, rb;
     if (gi < nA) {
         ra = gi * SR;
@@ -904,7 +906,7 @@ __global__ __launch_bounds__(GW) void k_dyn_group(DevStream *__restrict__ st,
                                 : (row > R.y0 ? tc_of(ma[8 * k + (pc < 22 ? pc - 14 : pc - 16)]) : nBe);
                 }
                 nC = nc_of(nA, nB);
-                piece_token(PT, mv, nC, tv, tl);
+                piece_token(L.ct, mv, nC, tv, tl);
             }
             uint32_t len = tl + (mv & 255u);
             if (mv & M_OVF) len = ovf_bits(PT, TB, get_body(BL, BH, rec_of(q0 + k, pc, ndt), true), pc, nC);   /* rare */
@@ -1091,7 +1093,7 @@ __global__ __launch_bounds__(GW) void k_dyn_group(DevStream *__restrict__ st,
                         sk.start(pos);
                         if (nC != -1) {
                             uint32_t tv, tl;
-                            piece_token(PT, mv, nC, tv, tl);
+                            piece_token(L.ct, mv, nC, tv, tl);
                             sk.put(tv, (int)tl);
                         }
                         sk.put_cap(CapSink{(uint64_t)bd[u].z | (uint64_t)bd[u].w << 32,

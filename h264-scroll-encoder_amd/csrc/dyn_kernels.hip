@@ -1403,8 +1403,24 @@ __global__ __launch_bounds__(DT) void k_dyn_emit_gather(const DevStream *__restr
     const uint64_t cfirst = o0 >> 4, cnal = ((o1 + 15) >> 4) - cfirst;
     const uint64_t per = (cnal + gridDim.z - 1) / gridDim.z;
     const uint64_t cbeg = cfirst + per * blockIdx.z, cend = min(cfirst + cnal, cbeg + per);
+    /* coarse index (in raw, free after the sort): raw[b] = EP bytes before
+     * EBSP index b << cs, by one binary search per block; a chunk then
+     * starts from its block's count and steps over the few EP bytes between */
     int lg = 0;                   /* binary-search steps: 2^lg > n */
     while ((1u << lg) <= n) lg++;
+    int cs = 10;
+    while ((d.size >> cs) >= 1024) cs++;
+    const int nblk = (int)(d.size >> cs) + 1;
+    for (int bi = t; bi < nblk; bi += DT) {
+        const int64_t e0 = (int64_t)bi << cs;
+        uint32_t K = 0;
+        for (int b = lg - 1; b >= 0; --b) {
+            const uint32_t k2 = K + (1u << b);
+            K = k2 <= n && (int64_t)(sp[k2 - 1] + (k2 - 1)) < e0 ? k2 : K;
+        }
+        raw[bi] = K;
+    }
+    __syncthreads();
     for (uint64_t cb = cbeg + (uint64_t)t; cb < cend; cb += (uint64_t)U * DT) {
         uint32_t Ku[U], epm[U], shv[U];
         bool inner[U];
@@ -1414,13 +1430,9 @@ __global__ __launch_bounds__(DT) void k_dyn_emit_gather(const DevStream *__restr
             const uint64_t q0 = (cb + (uint64_t)u * DT) << 4;
             const int64_t u0 = (int64_t)q0 - (int64_t)o0 - 5;        /* EBSP index of byte 0 */
             /* K = EP bytes before the chunk; the j-th sits at EBSP index
-             * sp[j] + j (strictly increasing): branch-free binary search,
-             * the U searches of an iteration are independent */
-            uint32_t K = 0;
-            for (int b = lg - 1; b >= 0; --b) {
-                const uint32_t k2 = K + (1u << b);
-                K = k2 <= n && (int64_t)(sp[k2 - 1] + (k2 - 1)) < u0 ? k2 : K;
-            }
+             * sp[j] + j (strictly increasing) */
+            uint32_t K = u0 > 0 ? raw[min((int)(u0 >> cs), nblk - 1)] : 0u;
+            while (K < n && (int64_t)(sp[K] + K) < u0) K++;
             Ku[u] = K;
             inner[u] = u0 >= 0 && q0 + 16 <= o1;
             epm[u] = 0;

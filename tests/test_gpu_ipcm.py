@@ -26,6 +26,51 @@ def gpu(scroll):
     return scroll
 
 
+class Hip:
+    """Device buffers through the HIP runtime libh264scroll itself links (so
+    the process holds one runtime, not torch's bundled one beside it)."""
+
+    def __init__(self):
+        self.lib = ctypes.CDLL("libamdhip64.so.7")
+        L = self.lib
+        L.hipMalloc.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t]
+        L.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+        L.hipMemset.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t]
+        L.hipFree.argtypes = [ctypes.c_void_p]
+        for f in (L.hipMalloc, L.hipMemcpy, L.hipMemset, L.hipFree, L.hipDeviceSynchronize):
+            f.restype = ctypes.c_int
+
+    def buf(self, n, fill=0):
+        return DevBuf(self, n, fill)
+
+
+class DevBuf:
+    def __init__(self, hip, n, fill):
+        self.hip, self.n, p = hip, n, ctypes.c_void_p()
+        assert hip.lib.hipMalloc(ctypes.byref(p), n) == 0
+        self.p = p.value
+        assert hip.lib.hipMemset(self.p, fill, n) == 0
+
+    def write(self, off, data):
+        data = bytes(data)
+        assert self.hip.lib.hipMemcpy(self.p + off, data, len(data), 1) == 0      # host -> device
+
+    def read(self):
+        host = np.empty(self.n, np.uint8)
+        assert self.hip.lib.hipMemcpy(host.ctypes.data, self.p, self.n, 2) == 0  # device -> host
+        return host
+
+    def free(self):
+        if self.p:
+            self.hip.lib.hipFree(self.p)
+            self.p = None
+
+
+@pytest.fixture(scope="module")
+def hip(gpu):
+    return Hip()
+
+
 def pictures(w, h, kinds, seed=7):
     rng = np.random.default_rng(seed)
     n = w * h * 3 // 2
@@ -49,82 +94,76 @@ def pictures(w, h, kinds, seed=7):
     return out
 
 
-def gpu_files(gpu, torch, w, h, pics, out_stride=None, b=None):
+def gpu_files(gpu, hip, w, h, pics, out_stride=None, b=None):
     n = len(pics)
     psz = w * h * 3 // 2
     stride = (psz + 255) // 256 * 256
-    dev = torch.zeros(n * stride, dtype=torch.uint8, device="cuda")
-    for i, p in enumerate(pics):
-        dev[i * stride:i * stride + psz] = torch.frombuffer(bytearray(p), dtype=torch.uint8).cuda()
+    dev = hip.buf(n * stride)
     if out_stride is None:
         out_stride = (psz * 3 // 2 + psz + 4096 + 255) // 256 * 256
-    out = torch.full((n * out_stride,), 0xAB, dtype=torch.uint8, device="cuda")
+    out = hip.buf(n * out_stride, 0xAB)
     own = b is None
     if own:
         b = gpu.Batch(1, 1, 1 << 20, device=0)
     try:
-        sizes = b.ipcm_files_device(n, w, h, dev.data_ptr(), stride, out.data_ptr(), out_stride)
-        torch.cuda.synchronize()
-        host = out.cpu().numpy()
+        for i, p in enumerate(pics):
+            dev.write(i * stride, p)
+        sizes = b.ipcm_files_device(n, w, h, dev.p, stride, out.p, out_stride)
+        assert hip.lib.hipDeviceSynchronize() == 0
+        host = out.read()
         files = [host[i * out_stride:i * out_stride + sizes[i]].tobytes() for i in range(n)]
         tails = [host[i * out_stride + sizes[i]:(i + 1) * out_stride] for i in range(n)]
     finally:
         if own:
             b.close()
+        dev.free()
+        out.free()
     return files, tails
 
 
-@pytest.fixture(scope="module")
-def torch():
-    import torch as t
-    if not t.cuda.is_available():
-        pytest.fail("torch sees no GPU")
-    return t
-
-
 @pytest.mark.parametrize("w,h", [(64, 48), (1280, 720)])
-def test_striped_refs_match_reference(gpu, torch, oracle, golden_md5, w, h):
-    files, _ = gpu_files(gpu, torch, w, h, pictures(w, h, ["a", "b"]))
+def test_striped_refs_match_reference(gpu, hip, oracle, golden_md5, w, h):
+    files, _ = gpu_files(gpu, hip, w, h, pictures(w, h, ["a", "b"]))
     for which, f in enumerate(files):
         g = golden_md5[f"ipcm_{w}x{h}_{'ab'[which]}.h264"]
         assert len(f) == g["bytes"] and hashlib.md5(f).hexdigest() == g["md5"]
 
 
 @pytest.mark.parametrize("w,h", [(16, 16), (48, 32), (176, 144), (640, 480), (1280, 720)])
-def test_pictures_match_oracle(gpu, torch, oracle, w, h):
+def test_pictures_match_oracle(gpu, hip, oracle, w, h):
     kinds = ["rand", "zero", "low", "sparse", "a"]
     pics = pictures(w, h, kinds, seed=w + h)
-    files, tails = gpu_files(gpu, torch, w, h, pics)
+    files, tails = gpu_files(gpu, hip, w, h, pics)
     for k, (p, f, t) in enumerate(zip(pics, files, tails)):
         want = ipcm_file(oracle, w, h, p)
         assert f == want, f"{kinds[k]} {w}x{h}: {len(f)} vs {len(want)} bytes"
         assert (t == 0xAB).all(), "bytes written past the file"
 
 
-def test_4k_pictures(gpu, torch, oracle, golden_md5):
+def test_4k_pictures(gpu, hip, oracle, golden_md5):
     w, h = 3840, 2160
     pics = pictures(w, h, ["a", "zero"])
-    files, _ = gpu_files(gpu, torch, w, h, pics)
+    files, _ = gpu_files(gpu, hip, w, h, pics)
     g = golden_md5["ipcm_3840x2160_a.h264"]
     assert len(files[0]) == g["bytes"] and hashlib.md5(files[0]).hexdigest() == g["md5"]
     assert files[1] == ipcm_file(oracle, w, h, pics[1])
 
 
-def test_overflow_reports_sizes(gpu, torch, oracle):
+def test_overflow_reports_sizes(gpu, hip, oracle):
     w, h = 64, 48
     pics = pictures(w, h, ["zero"])
     want = ipcm_file(oracle, w, h, pics[0])
     b = gpu.Batch(1, 1, 1 << 20, device=0)
     try:
         with pytest.raises(RuntimeError):
-            gpu_files(gpu, torch, w, h, pics, out_stride=len(want) - 1, b=b)
-        files, _ = gpu_files(gpu, torch, w, h, pics, out_stride=len(want), b=b)
+            gpu_files(gpu, hip, w, h, pics, out_stride=len(want) - 1, b=b)
+        files, _ = gpu_files(gpu, hip, w, h, pics, out_stride=len(want), b=b)
         assert files[0] == want
     finally:
         b.close()
 
 
-def test_files_feed_ingest_and_compose(gpu, torch, oracle):
+def test_files_feed_ingest_and_compose(gpu, hip, oracle):
     """pixels -> reference files -> new streams -> scroll frames without
     leaving the GPU (scroll_batch_ingest_device on the files in place);
     equal to the reference composer's restatement run on the oracle's files"""
@@ -132,18 +171,18 @@ def test_files_feed_ingest_and_compose(gpu, torch, oracle):
     pics = pictures(w, h, ["rand", "sparse", "a", "b"], seed=3)
     psz = w * h * 3 // 2
     stride = (psz + 255) // 256 * 256
-    dev = torch.zeros(4 * stride, dtype=torch.uint8, device="cuda")
+    dev = hip.buf(4 * stride)
     for i, p in enumerate(pics):
-        dev[i * stride:i * stride + psz] = torch.frombuffer(bytearray(p), dtype=torch.uint8).cuda()
+        dev.write(i * stride, p)
     ostride = 2 * stride + 4096
-    out = torch.zeros(4 * ostride, dtype=torch.uint8, device="cuda")
+    out = hip.buf(4 * ostride)
     b = gpu.Batch(2, nfr, 4 << 20, device=0)
     try:
-        sizes = b.ipcm_files_device(4, w, h, dev.data_ptr(), stride, out.data_ptr(), ostride)
+        sizes = b.ipcm_files_device(4, w, h, dev.p, stride, out.p, ostride)
         desc = []
         for k in range(2):
             desc += [2 * k * ostride, sizes[2 * k], (2 * k + 1) * ostride, sizes[2 * k + 1]]
-        assert b.ingest_device(2, out.data_ptr(), desc) == 0
+        assert b.ingest_device(2, out.p, desc) == 0
         offs = np.array([[oracle.or_tri(i * speed, h) for i in range(nfr)] for _ in range(2)], np.int32)
         b.set_offsets(offs)
         b.compose(nfr)
@@ -156,3 +195,5 @@ def test_files_feed_ingest_and_compose(gpu, torch, oracle):
             assert n and b.output(k) == bytes(buf[:n])
     finally:
         b.close()
+        dev.free()
+        out.free()

@@ -31,7 +31,6 @@ def main():
     ap.add_argument("--streams", type=int, default=256)
     ap.add_argument("--frames", type=int, default=16)
     ap.add_argument("--reps", type=int, default=5)
-    ap.add_argument("--ablate", action="store_true", help="also time the SCROLL_DEBUG_DYN_* ablations")
     args = ap.parse_args()
     import numpy as np
     import h264scroll as hs
@@ -62,22 +61,6 @@ def main():
           % tuple(x / n for x in ms))
     b.enable_timing(False)
 
-    if args.ablate:
-        for name, fl in (("no pixel loads", hs.SCROLL_DEBUG_DYN_NOLOAD),
-                         ("no block CAVLC", hs.SCROLL_DEBUG_DYN_NOCAVLC),
-                         ("no MB heads", hs.SCROLL_DEBUG_DYN_NOHEAD),
-                         ("no bit writes", hs.SCROLL_DEBUG_DYN_NOWRITE),
-                         ("none of these", hs.SCROLL_DEBUG_DYN_NOLOAD | hs.SCROLL_DEBUG_DYN_NOCAVLC |
-                          hs.SCROLL_DEBUG_DYN_NOHEAD | hs.SCROLL_DEBUG_DYN_NOWRITE)):
-            b.set_debug(fl)
-            b.enable_timing(True)
-            b.kernel_stats_ex()
-            for _ in range(args.reps):
-                b.compose(F, rewind=True)
-            b.sync()
-            ms, n = b.kernel_stats_ex()
-            b.enable_timing(False)
-            print("ablation %-16s dyn_stage %.4f ms" % (name, ms[2] / n))
     b.set_debug(hs.SCROLL_DEBUG_DYN_STAMPS)
     b.compose(F, rewind=True)
     assert b.sync() == 0, hs.last_error()

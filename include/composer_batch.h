@@ -59,9 +59,10 @@ extern "C" {
 #define SCROLL_DEBUG_EMIT_STAMPS 64 /* k_emit records s_memtime per phase per wave */
 #define SCROLL_DEBUG_EMIT_NOBYTES 128 /* k_emit skips the tile-end partial chunks  */
 #define SCROLL_DEBUG_DYN_STAMPS 256 /* k_dyn_group / gather: realtime per phase  */
-/* dynamic-coder ablations (builds with -DSCROLL_DYN_ABLATE=1 only; timing only, outputs
- * wrong): skip the pixel loads /
- * the block CAVLC / the MB-head work / the bit writes */
+/* retired: runtime ablations of the earlier one-kernel dynamic coder (no
+ * kernel reads them now; k_dyn_code's ablations are the compile-time
+ * variants -DSCROLL_ABL_NOLOAD / -DSCROLL_ABL_NOCAVLC).  Values kept so the
+ * flag numbering stays stable. */
 #define SCROLL_DEBUG_DYN_NOLOAD  512
 #define SCROLL_DEBUG_DYN_NOCAVLC 1024
 #define SCROLL_DEBUG_DYN_NOHEAD  2048

@@ -925,6 +925,8 @@ struct ScrollBatch {
     IngestOut *d_ing_out = nullptr;
     int ing_cap = 0;
     hipEvent_t ing_ev[2] = {};         /* timing: around the ingest kernels */
+    hipStream_t pipe = nullptr;        /* dynamic coder: k_dyn_group chunks beside the code chain */
+    hipEvent_t pipe_ev[DYN_PIPE_CHUNKS + 1] = {};
     /* reference files from pictures: EP count per chunk */
     uint32_t *d_ipcm_cnt = nullptr;
     size_t ipcm_cap = 0;
@@ -1038,6 +1040,10 @@ void scroll_batch_destroy(ScrollBatch *b)
         if (b->ev[i]) (void)hipEventDestroy(b->ev[i]);
     for (hipEvent_t e : b->ring) (void)hipEventDestroy(e);
     if (b->own) (void)hipStreamDestroy(b->own);
+    if (b->pipe) (void)hipStreamSynchronize(b->pipe);
+    for (hipEvent_t e : b->pipe_ev)
+        if (e) (void)hipEventDestroy(e);
+    if (b->pipe) (void)hipStreamDestroy(b->pipe);
     (void)hipFree(b->d_st);
     (void)hipHostFree(b->h_st);
     (void)hipFree(b->d_off);
@@ -1247,18 +1253,59 @@ static int launch(ScrollBatch *b, int nframes, int plan_mode, int nal_max, hipSt
             }
             if ((rc = mark(6))) return rc;
         } else {
-            if (dyn_launch_code(hs, nframes, S, b->d_st, b->d_nal, b->ld_nal, b->d_pend, b->d_dfr,
-                                ld_fr, &b->geo, b->d_src, b->d_refs, &b->dx)) {
-                set_err("k_dyn_code launch: %s", hipGetErrorString(hipGetLastError()));
-                return SCROLL_ERR_HIP;
-            }
-            if ((rc = mark(6))) return rc;
             b->dx.epoch = b->dx.epoch % 0xffffffu + 1u;    /* look-back epoch, never 0 */
-            if (dyn_launch_pack(hs, nframes, S, b->d_st, b->d_nal, b->ld_nal, b->d_pend, b->d_dfr,
-                                ld_fr, &b->geo, &b->dx, b->d_stage, b->dx.epoch, stamps,
-                                b->dyn_pw / 16, b->dyn_ph / 16)) {
-                set_err("k_dyn_group launch: %s", hipGetErrorString(hipGetLastError()));
-                return SCROLL_ERR_HIP;
+            /* Pipeline over stream chunks: the block coder (issue-bound) runs
+             * chunk after chunk on hs while k_dyn_group + k_dyn_ep (latency-
+             * bound) of the chunks already coded run beside it on b->pipe.
+             * A chunk is the same kernels on a contiguous stream range,
+             * given pointers offset to its first stream. */
+            const int nch = stamps ? 1 : (S < DYN_PIPE_CHUNKS ? S : DYN_PIPE_CHUNKS);
+            if (nch > 1 && !b->pipe) {
+                HIPCHK(hipStreamCreateWithFlags(&b->pipe, hipStreamNonBlocking));
+                for (hipEvent_t &e : b->pipe_ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+            }
+            const DynGeom &G = b->geo;
+            const size_t nalw = (size_t)G.w * G.h, ng = (size_t)G.ngroups;
+            for (int c = 0; c < nch; ++c) {
+                const int s0 = (int)((int64_t)S * c / nch), s1 = (int)((int64_t)S * (c + 1) / nch);
+                const size_t nb0 = (size_t)s0 * ld_fr;
+                DynScratch xc = b->dx;
+                xc.rows = b->dx.rows + nb0 * 32 * G.h;
+                xc.meta = b->dx.meta + nb0 * DYN_PIECES * nalw;
+                xc.body_lo = b->dx.body_lo + nb0 * DYN_PIECES * nalw;
+                xc.body_hi = b->dx.body_hi + nb0 * DYN_PIECES * nalw;
+                xc.status = b->dx.status + nb0 * ng;
+                xc.tails = b->dx.tails + nb0 * ng;
+                DevStream *st0 = b->d_st + s0;
+                NalDesc *nal0 = b->d_nal + (size_t)s0 * b->ld_nal;
+                PlanPending *pend0 = b->d_pend + s0;
+                DynFrame *dfr0 = b->d_dfr + nb0;
+                const uint8_t *src0 = b->d_src + (size_t)s0 * G.src_ld;
+                const uint8_t *refs0 = b->d_refs + (size_t)s0 * G.ref_ld;
+                uint8_t *stage0 = b->d_stage + nb0 * G.slot_bytes;
+                if (dyn_launch_code(hs, nframes, s1 - s0, st0, nal0, b->ld_nal, pend0, dfr0, ld_fr, &G, src0,
+                                    refs0, &xc)) {
+                    set_err("k_dyn_code launch: %s", hipGetErrorString(hipGetLastError()));
+                    return SCROLL_ERR_HIP;
+                }
+                hipStream_t hp = hs;
+                if (nch > 1) {
+                    HIPCHK(hipEventRecord(b->pipe_ev[c], hs));
+                    HIPCHK(hipStreamWaitEvent(b->pipe, b->pipe_ev[c], 0));
+                    hp = b->pipe;
+                } else if ((rc = mark(6))) {
+                    return rc;
+                }
+                if (dyn_launch_pack(hp, nframes, s1 - s0, st0, nal0, b->ld_nal, pend0, dfr0, ld_fr, &G, &xc,
+                                    stage0, b->dx.epoch, stamps, b->dyn_pw / 16, b->dyn_ph / 16)) {
+                    set_err("k_dyn_group launch: %s", hipGetErrorString(hipGetLastError()));
+                    return SCROLL_ERR_HIP;
+                }
+            }
+            if (nch > 1) {                 /* timing: code chain, then the pipe's tail */
+                if ((rc = mark(6))) return rc;
+                HIPCHK(hipEventRecord(b->pipe_ev[DYN_PIPE_CHUNKS], b->pipe));
+                HIPCHK(hipStreamWaitEvent(hs, b->pipe_ev[DYN_PIPE_CHUNKS], 0));
             }
         }
         if ((rc = mark(2))) return rc;

@@ -236,7 +236,10 @@ __device__ inline void code_frame(const DevStream *__restrict__ st,
         wo[t] = pend[s].wo[t];
         wv[t] = pend[s].wv[t];
     }
-    __syncthreads();
+    /* the general chroma path reads wo / wv before the sort; otherwise the
+     * sort's first barrier publishes ptabs, and the pixel loads need not
+     * wait for the table copy */
+    if (GENERAL) __syncthreads();
 
     const int ndt = g.w * g.h, ntask = 24 * ndt;
     const int task = bx * CODE_T + t;

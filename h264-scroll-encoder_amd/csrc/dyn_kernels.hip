@@ -209,6 +209,13 @@ __global__ __launch_bounds__(256) void k_dyn_rows(const DevStream *__restrict__ 
 #define SCROLL_CODE_T 256
 #endif
 constexpr int CODE_T = SCROLL_CODE_T, CODE_NW = CODE_T / 64;
+/* sort classes: TotalCoeff 0 .. SORT_KEYS - 2 each, the rest together (the
+ * tail is rare; fewer classes, fewer ballots) */
+#ifndef SCROLL_SORT_KEYS
+#define SCROLL_SORT_KEYS 9
+#endif
+constexpr int SORT_KEYS = SCROLL_SORT_KEYS;
+static_assert(SORT_KEYS >= 2 && SORT_KEYS <= 17, "TotalCoeff classes");
 
 template <bool GENERAL>
 __device__ inline void code_frame(const DevStream *__restrict__ st,
@@ -222,7 +229,7 @@ __device__ inline void code_frame(const DevStream *__restrict__ st,
                                                      uint2 *__restrict__ bhi, int s, int f, int bx)
 {
     __shared__ uint4 lv[CODE_T];
-    __shared__ uint16_t wc[CODE_NW][17];           /* per wave: blocks per TotalCoeff */
+    __shared__ uint16_t wc[CODE_NW][SORT_KEYS];    /* per wave: blocks per TotalCoeff class */
     __shared__ uint16_t order[CODE_T];
     __shared__ PTabs ptabs;
     __shared__ int32_t wo[8], wv[8];
@@ -399,10 +406,10 @@ __device__ inline void code_frame(const DevStream *__restrict__ st,
      * workgroup), so each wave's CAVLC loop runs about its own blocks' count */
     lv[t] = make_uint4(pk[0], pk[1], pk[2], pk[3]);
     {
-        const int key = 16 - n;                         /* inactive tasks: n = 0 */
+        const int key = SORT_KEYS - 1 - min(n, SORT_KEYS - 1);   /* inactive tasks: n = 0 */
         uint32_t below = 0;
 #pragma unroll
-        for (int k = 0; k < 17; ++k) {
+        for (int k = 0; k < SORT_KEYS; ++k) {
             const uint64_t m = __ballot(key == k);
             if (lane == 0) wc[wave][k] = (uint16_t)__popcll(m);
             if (key == k)
@@ -410,7 +417,7 @@ __device__ inline void code_frame(const DevStream *__restrict__ st,
                                                             __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
         }
         __syncthreads();
-        if (t < 17) {                                   /* key k = t: wave prefixes, key offsets */
+        if (t < SORT_KEYS) {                            /* key k = t: wave prefixes, key offsets */
             uint32_t tot = 0;
 #pragma unroll
             for (int w2 = 0; w2 < CODE_NW; ++w2) tot += wc[w2][t];

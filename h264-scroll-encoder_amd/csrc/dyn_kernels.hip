@@ -757,8 +757,14 @@ __device__ inline void wave_sync()
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-/* grid (g.ngroups, frames, streams), GW threads */
-__global__ __launch_bounds__(GW) void k_dyn_group(DevStream *__restrict__ st,
+/* grid (g.ngroups, frames, streams), GW threads.  The kernel is latency-bound
+ * (one wave per group, look-back waits): SCROLL_GROUP_WAVES caps the VGPRs so
+ * that many waves fit per SIMD */
+#ifndef SCROLL_GROUP_WAVES
+#define SCROLL_GROUP_WAVES 6
+#endif
+__global__ __launch_bounds__(GW) __attribute__((amdgpu_waves_per_eu(SCROLL_GROUP_WAVES)))
+void k_dyn_group(DevStream *__restrict__ st,
                                                   const NalDesc *__restrict__ nal, int ld_nal,
                                                   const PlanPending *__restrict__ pend,
                                                   DynFrame *__restrict__ dfr, int ld_fr, DynGeom g,

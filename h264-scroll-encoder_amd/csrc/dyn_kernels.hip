@@ -378,28 +378,20 @@ __device__ inline void code_frame(const DevStream *__restrict__ st,
             n += v != 0;
         }
     }
-    /* chroma DC: the quad's four DC coefficients -> 2x2 Hadamard, quant,
-     * whole CAVLC block (nC = -1) by the quad's first lane */
+    /* chroma DC: the quad's four DC coefficients -> 2x2 Hadamard, quant; the
+     * whole CAVLC block (nC = -1) is coded by the quad's first lane after the
+     * sort's first barrier, which publishes the LDS tables (ptabs) */
+    int dq[4] = {0, 0, 0, 0};
+    const bool dc_lane = act && !luma && r == 0;
     {
         const int qb = lane & ~3;
         const int d0 = __shfl(w0, qb, 64), d1 = __shfl(w0, qb + 1, 64);
         const int d2 = __shfl(w0, qb + 2, 64), d3 = __shfl(w0, qb + 3, 64);
-        if (act && !luma && r == 0) {
-            const int dq[4] = {quant_dc(d0 + d1 + d2 + d3), quant_dc(d0 - d1 + d2 - d3),
-                               quant_dc(d0 + d1 - d2 - d3), quant_dc(d0 - d1 - d2 + d3)};
-            CapSink cap{0, 0, 0};
-            const int tc = cavlc_dc4(cap, ptabs, dq);
-            const size_t idx = (size_t)24 * ndt + 2 * k + p;    /* rec_of(k, 16 + p) */
-            if (cap.n <= 128) {
-                M[idx] = (uint16_t)(cap.n | (uint32_t)tc << 8);
-                if (cap.n)
-                    put_body(BL, BH, idx, make_uint4((uint32_t)cap.lo, (uint32_t)(cap.lo >> 32), (uint32_t)cap.hi,
-                                                     (uint32_t)(cap.hi >> 32)), cap.n > 64);
-            } else {
-                M[idx] = (uint16_t)((uint32_t)tc << 8 | M_OVF);
-                put_body(BL, BH, idx, make_uint4(((uint32_t)dq[0] & 0xffffu) | (uint32_t)dq[1] << 16,
-                                                 ((uint32_t)dq[2] & 0xffffu) | (uint32_t)dq[3] << 16, 0u, 0u), false);
-            }
+        if (dc_lane) {
+            dq[0] = quant_dc(d0 + d1 + d2 + d3);
+            dq[1] = quant_dc(d0 - d1 + d2 - d3);
+            dq[2] = quant_dc(d0 + d1 - d2 - d3);
+            dq[3] = quant_dc(d0 - d1 - d2 + d3);
         }
     }
     /* encode order: by TotalCoeff, largest first (a counting sort over the
@@ -416,7 +408,22 @@ __device__ inline void code_frame(const DevStream *__restrict__ st,
                 below = (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
                                                             __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
         }
-        __syncthreads();
+        __syncthreads();                                /* also publishes ptabs */
+        if (dc_lane) {
+            CapSink cap{0, 0, 0};
+            const int tc = cavlc_dc4(cap, ptabs, dq);
+            const size_t idx = (size_t)24 * ndt + 2 * k + p;    /* rec_of(k, 16 + p) */
+            if (cap.n <= 128) {
+                M[idx] = (uint16_t)(cap.n | (uint32_t)tc << 8);
+                if (cap.n)
+                    put_body(BL, BH, idx, make_uint4((uint32_t)cap.lo, (uint32_t)(cap.lo >> 32), (uint32_t)cap.hi,
+                                                     (uint32_t)(cap.hi >> 32)), cap.n > 64);
+            } else {
+                M[idx] = (uint16_t)((uint32_t)tc << 8 | M_OVF);
+                put_body(BL, BH, idx, make_uint4(((uint32_t)dq[0] & 0xffffu) | (uint32_t)dq[1] << 16,
+                                                 ((uint32_t)dq[2] & 0xffffu) | (uint32_t)dq[3] << 16, 0u, 0u), false);
+            }
+        }
         if (t < SORT_KEYS) {                            /* key k = t: wave prefixes, key offsets */
             uint32_t tot = 0;
 #pragma unroll
@@ -1155,18 +1162,19 @@ void k_dyn_group(DevStream *__restrict__ st,
             }
         }
         wave_sync();
+        /* every word but a shared first one first -- the out-shared tail is
+         * published before this wave waits for its predecessor's, so small
+         * one-pass groups do not chain their successors behind that wait */
         for (uint32_t i = (uint32_t)t; i < n; i += GW) {
             const uint32_t q = p0 + i, v = L.buf[i];
-            const uint64_t gw = w0 + q;
-            if (q == 0 && in_sh) {
-                const uint32_t v2 = v | tail_wait();
-                if (nw == 1 && out_sh) tail_pub(v2);
-                else out[gw] = __builtin_bswap32(v2);
-            } else if (q == nw - 1 && out_sh) {
-                tail_pub(v);
-            } else {
-                out[gw] = __builtin_bswap32(v);
-            }
+            if (q == 0 && in_sh) continue;
+            if (q == nw - 1 && out_sh) tail_pub(v);
+            else out[w0 + q] = __builtin_bswap32(v);
+        }
+        if (p0 == 0 && in_sh && t == 0) {
+            const uint32_t v2 = L.buf[0] | tail_wait();
+            if (nw == 1 && out_sh) tail_pub(v2);
+            else out[w0] = __builtin_bswap32(v2);
         }
         wave_sync();
     }
@@ -1290,7 +1298,7 @@ __global__ __launch_bounds__(DT) void k_dyn_emit(const DevStream *__restrict__ s
     const DynFrame df = dfr[(size_t)s * ld_fr + f];
     const int j = df.nal;
     if (j < 0 || j >= st[s].nnal || df.err) return;          /* nnal = 0: nothing committed */
-    if (df.ep <= (uint32_t)EPLIST_MAX) return;               /* k_dyn_emit_gather's NAL */
+    if (df.ep <= ep_cap(g)) return;                          /* k_dyn_emit_gather's NAL */
     const NalDesc d = nal[(size_t)s * ld_nal + j];
     if (d.slow != 2) return;
     uint8_t *A = arena + (size_t)s * ld_arena;
@@ -1387,7 +1395,7 @@ __global__ __launch_bounds__(DT) void k_dyn_emit_gather(const DevStream *__restr
     const int j = df.nal;
     if (j < 0 || j >= st[s].nnal || df.err) return;          /* nnal = 0: nothing committed */
     const uint32_t n = df.ep;
-    if (n > (uint32_t)EPLIST_MAX) return;                     /* k_dyn_emit's NAL */
+    if (n > ep_cap(g)) return;                               /* k_dyn_emit's NAL */
     const NalDesc d = nal[(size_t)s * ld_nal + j];
     if (d.slow != 2) return;
     const uint8_t *in = stage + ((size_t)s * ld_fr + f) * g.slot_bytes;

@@ -67,6 +67,10 @@ extern "C" {
 #define SCROLL_DEBUG_DYN_NOCAVLC 1024
 #define SCROLL_DEBUG_DYN_NOHEAD  2048
 #define SCROLL_DEBUG_DYN_NOWRITE 4096
+/* tests: the dynamic emit keeps at most 4 EP positions per NAL, so every NAL
+ * with more emulation-prevention bytes takes the large-NAL path (k_dyn_emit,
+ * otherwise only reached past 2,048 EP bytes); output unchanged */
+#define SCROLL_DEBUG_DYN_EPCAP4 8192
 
 typedef struct ScrollBatch ScrollBatch;
 

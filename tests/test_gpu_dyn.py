@@ -94,9 +94,11 @@ def oracle_streams(oracle, w, h, offsets, rect, src, R, mode=0, frame_num=2, way
 
 
 def gpu_streams(gpu, w, h, offsets, rect, R, src=None, synth=False, mode=0, chunks=None,
-                arena=None, slot=0, waypoints=(), shared_refs=True, per_stream_refs=None):
+                arena=None, slot=0, waypoints=(), shared_refs=True, per_stream_refs=None, debug=0):
     S, F = offsets.shape
     b = gpu.Batch(S, F, arena or (8 << 20), mode=mode)
+    if debug:
+        b.set_debug(debug)
     for _ in range(S):
         b.add_stream(gpu.make_config(w, h, waypoints=waypoints))
     b.set_dyn_rect(rect.x0, rect.y0, rect.w, rect.h, slot)
@@ -282,3 +284,36 @@ def test_dyn_staging_overflow_commits_nothing(gpu, oracle):
     b, rc = gpu_streams(gpu, w, h, offs, rect, R, src, slot=1024)
     assert rc == gpu.SCROLL_ERR_OVERFLOW
     assert b.output_size(0) == 0
+
+
+def test_dyn_large_nal_emit_path(gpu, oracle):
+    """k_dyn_emit, the path for NALs with more EP bytes than the gather's
+    list holds (2,048; no bench NAL reaches it): SCROLL_DEBUG_DYN_EPCAP4
+    caps the list at 4, so every NAL with more EP bytes -- most config-3
+    NALs, and the random-pixel ones -- goes through k_dyn_emit's LDS line
+    buffer and scans, and the bytes must not change"""
+    w, h = 1280, 720
+    rect = Rect(28, 10, 25, 25)
+    S, F = 2, 6
+    offs = synthetic_offsets(S, F, h)
+    R = striped_refs(oracle, w, h)
+    src = synth_source(oracle, S, F, rect)
+    want = oracle_streams(oracle, w, h, offs, rect, src, R)
+    b, rc = gpu_streams(gpu, w, h, offs, rect, R, synth=True, debug=gpu.SCROLL_DEBUG_DYN_EPCAP4)
+    assert rc == 0, gpu.last_error()
+    check_equal(b, want)
+    eps = [b.dyn_frame_info(s, t)[1] for s in range(S) for t in range(F)]
+    assert sum(e > 4 for e in eps) >= 2, eps          # the large-NAL path ran
+
+    w, h = 96, 96
+    rect = Rect(0, 0, 6, 6)
+    rng = np.random.default_rng(17)
+    S, F = 2, 10
+    offs = rng.integers(-200, 300, (S, F)).astype(np.int32)
+    R = random_refs(w, h, 4)
+    src = rng.integers(0, 256, (S, F, 384 * 36)).astype(np.uint8)
+    src[:, ::3] = 0                                   # zero pictures: long zero-bit runs
+    want = oracle_streams(oracle, w, h, offs, rect, src, R)
+    b, rc = gpu_streams(gpu, w, h, offs, rect, R, src, debug=gpu.SCROLL_DEBUG_DYN_EPCAP4)
+    assert rc == 0, gpu.last_error()
+    check_equal(b, want)

@@ -34,7 +34,7 @@ A step = one scroll_batch_compose over every stream of the rank:
   Offsets = SURVEY 8(d) synthetic scroll (speed 1+(s%8), phase 97 s mod 1440)
   in HBM; output arenas are rewound on device at every step (the bytes of a
   step are the product).
-Prints ONE JSON line (rank 0) with the dominant kernel's roofline (k_dyn_code
+Prints ONE JSON line (rank 0) with the dominant kernel's roofline (k_dyn_row
 or k_dyn_group for the dynamic rect, k_hint_stage, k_emit; HIP events on its
 launch stream) and the CPU oracle on host cores (rank 0, N = 1).
 """
@@ -535,14 +535,16 @@ def main():
             kms["dyn_code"] = code_ms / n
             kms["dyn_pack"] = pack_ms / n
         if rect and kms["dyn_code"] >= kms["dyn_pack"]:
-            # k_dyn_rows + k_dyn_code per launch: the source and prediction
-            # samples of every dynamic MB (384 B each) read; the block
-            # records they write for k_dyn_group are not algorithmic bytes
-            kern = "k_dyn_code"
+            # k_dyn_rows + k_dyn_row per launch (k_dyn_code_general: no
+            # frame here): the source and prediction samples of every
+            # dynamic MB (384 B each) read.  The staged RBSP the rect rows
+            # write is not counted (a lower bound: k_dyn_group writes the
+            # static rows' share of it)
+            kern = "k_dyn_row"
             alg_bytes = dyn_nals * 2 * 384 * rect[2] * rect[3]
             kern_ms = kms["dyn_code"]
         elif rect:
-            # k_dyn_group + k_dyn_ep per launch: the staged RBSP written
+            # k_dyn_group (static row groups) + k_dyn_ep per launch
             kern = "k_dyn_group"
             alg_bytes = rbsp_tot
             kern_ms = kms["dyn_pack"]

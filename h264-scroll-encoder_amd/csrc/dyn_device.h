@@ -301,21 +301,23 @@ __device__ __host__ inline void fwd4x4(const int x[16], int W[16])
 /* zig-zag scan (Table 8-13, frame): scan index -> raster position */
 constexpr int ZZ[16] = {0, 1, 4, 8, 5, 2, 3, 6, 9, 12, 13, 10, 7, 11, 14, 15};
 
-/* raster position pos of a 4x4 block */
+/* raster position pos of a 4x4 block.  sign(w) ((|w| mf + f) >> qbits) as
+ * one signed 24-bit multiply-add and an arithmetic shift: for w < 0 the
+ * bias 2^qbits - 1 - f turns the floor into -((|w| mf + f) >> qbits)
+ * (|w| <= 9180, mf < 2^14: the product fits 31 bits) */
 __device__ __host__ inline int quant(int w, int pos)
 {
     const int i = pos >> 2, j = pos & 3;
     const int mf = ((i | j) & 1) == 0 ? MF0 : (((i & j) & 1) ? MF1 : MF2);
-    const int a = w < 0 ? -w : w;                     /* |w| <= 9180, mf < 2^14: 24-bit multiply */
-    const int z = (int)((__umul24((uint32_t)a, (uint32_t)mf) + (uint32_t)QF) >> QBITS);
-    return w < 0 ? -z : z;
+    const int bias = QF + ((w >> 31) & ((1 << QBITS) - 1 - 2 * QF));
+    return (__mul24(w, mf) + bias) >> QBITS;
 }
 
+/* chroma DC (2x2): qbits + 1, f doubled (|w| <= 16320) */
 __device__ __host__ inline int quant_dc(int w)
 {
-    const int a = w < 0 ? -w : w;                     /* |w| <= 16320 */
-    const int z = (int)((__umul24((uint32_t)a, (uint32_t)MF0) + 2u * QF) >> (QBITS + 1));
-    return w < 0 ? -z : z;
+    const int bias = 2 * QF + ((w >> 31) & ((1 << (QBITS + 1)) - 1 - 4 * QF));
+    return (__mul24(w, MF0) + bias) >> (QBITS + 1);
 }
 
 /* ---------------------------------------------------------------------- */
@@ -459,64 +461,6 @@ __device__ __host__ inline int cavlc_block(S &s, const Tabs &T, const C *coef, i
     return tc;
 }
 
-/* The part of a CAVLC block after coeff_token -- trailing-ones signs,
- * levels, total_zeros, run_before -- which does not depend on nC.  c[]
- * holds the levels in scan order in registers; the loop is fully unrolled
- * (static indices, no divergence).  Returns TotalCoeff, t1 in *t1o. */
-template <int MAX, class S>
-__device__ __host__ inline int cavlc_rest(S &s, const Tabs &T, const int *c, int &t1o)
-{
-    uint32_t nz = 0;
-#pragma unroll
-    for (int i = 0; i < MAX; ++i) nz |= (c[i] != 0 ? 1u : 0u) << i;
-    const int tc = __builtin_popcount(nz);
-    int t1 = 0, sl = 0;
-    bool trailing = true;
-#pragma unroll
-    for (int i = MAX - 1; i >= 0; --i) {
-        const int v = c[i];
-        if (v != 0) {
-            if (trailing && t1 < 3 && (v == 1 || v == -1)) {
-                s.put(v < 0 ? 1u : 0u, 1);
-                t1++;
-            } else {
-                int code = v > 0 ? 2 * v - 2 : -2 * v - 1;
-                if (trailing) {                        /* first level */
-                    sl = (tc > 10 && t1 < 3) ? 1 : 0;
-                    if (t1 < 3) code -= 2;
-                    trailing = false;
-                }
-                uint32_t fv;
-                int fl;
-                level_field(code, sl, fv, fl);
-                s.put(fv, fl);
-                if (sl == 0) sl = 1;
-                if ((v < 0 ? -v : v) > (3 << (sl - 1)) && sl < 6) sl++;
-            }
-        }
-    }
-    t1o = t1;
-    if (tc == 0) return 0;
-    const int hi = top_bit(nz);
-    const int tz = hi + 1 - tc;
-    if (tc < MAX) {
-        if (MAX == 4) s.put(T.tzdc_bits[tc - 1][tz], T.tzdc_len[tc - 1][tz]);
-        else s.put(T.tz_bits[tc - 1][tz], T.tz_len[tc - 1][tz]);
-    }
-    int zl = tz, p = hi;
-    uint32_t m = nz;
-    for (int k = 0; k < tc - 1 && zl > 0; ++k) {
-        m &= ~(1u << p);
-        const int q = top_bit(m);
-        const int run = p - q - 1;
-        const int zi = (zl < 7 ? zl : 7) - 1;
-        s.put(T.rb_bits[zi][run], T.rb_len[zi][run]);
-        zl -= run;
-        p = q;
-    }
-    return tc;
-}
-
 /* coeff_token (9.2.1) of (TotalCoeff, TrailingOnes) for nC: (bits, len) */
 __device__ __host__ inline void coeff_token(const Tabs &T, int tc, int t1, int nC, uint32_t &v, int &len)
 {
@@ -589,120 +533,28 @@ __device__ __host__ inline void level_field_bf(int code, int sl, uint32_t &v, in
     len = prefix + 1 + ssize;
 }
 
-/* A whole CAVLC residual block (coeff_token .. run_before) of MAX levels
- * held as packed int8 (scan order, pk[i >> 2] byte i & 3), in one loop
- * over the NON-ZERO levels only, branch-free inside: the wave iterates
- * max TotalCoeff of its lanes (callers group blocks by TotalCoeff).  All
- * bits go to cap (token, signs / levels, total_zeros, runs); run_before
- * codes gather in a 64-bit side register first.  Returns TotalCoeff;
- * *ok = false when cap or the run register overflowed (cap.n is still the
- * exact length). */
-template <int MAX, class CAP>
-__device__ __host__ inline int cavlc_nz(CAP &cap, const PTabs &P, const uint32_t pk[4], int nC, bool &ok)
-{
-    uint32_t nz = 0;
-#pragma unroll
-    for (int i = 0; i < MAX; ++i) nz |= (((pk[i >> 2] >> (8 * (i & 3))) & 255u) != 0 ? 1u : 0u) << i;
-    const int tc = __builtin_popcount(nz);
-    auto lev = [&](int p) -> int {                         /* three selects + bfe */
-        const uint32_t w01 = (p & 4) ? pk[1] : pk[0], w23 = (p & 4) ? pk[3] : pk[2];
-        const uint32_t wv = (p & 8) ? w23 : w01;
-        return (int)(int8_t)(uint8_t)(wv >> (8 * (p & 3)));
-    };
-    /* trailing ones: the top <= 3 non-zero levels while they are +-1 */
-    int t1 = 0;
-    {
-        uint32_t m = nz;
-        bool run = true;
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {
-            const int p = m ? top_bit(m) : 0;
-            const int v = m ? lev(p) : 0;
-            run = run && m && (v == 1 || v == -1);
-            t1 += run ? 1 : 0;
-            m &= m ? ~(1u << p) : ~0u;
-        }
-    }
-    {
-        const int tb = nC < 0 ? 3 : (nC < 2 ? 0 : (nC < 4 ? 1 : 2));
-        uint32_t tv;
-        int tl;
-        if (nC >= 8) {
-            tv = tc ? (uint32_t)(((tc - 1) << 2) | t1) : 3u;
-            tl = 6;
-        } else {
-            const uint32_t e = P.ct[tb][4 * tc + t1];
-            tv = e & 255u;
-            tl = (int)(e >> 8);
-        }
-        cap.put(tv, tl);
-    }
-    ok = true;
-    if (tc == 0) return 0;
-    const int hi = top_bit(nz);
-    const int tz = hi + 1 - tc;
-    uint64_t runs = 0;
-    int rn = 0, zl = tz, sl = (tc > 10 && t1 < 3) ? 1 : 0, pprev = hi;
-    uint32_t m = nz;
-    for (int k = 0; k < tc; ++k) {
-        const int p = top_bit(m);
-        m &= ~(1u << p);
-        const int v = lev(p);
-        const int a = v < 0 ? -v : v;
-        const bool sgn = k < t1;
-        int code = 2 * a - 2 + (v < 0 ? 1 : 0);
-        code -= (k == t1 && t1 < 3) ? 2 : 0;
-        uint32_t fv;
-        int fl;
-        level_field_bf(code, sl, fv, fl);
-        cap.put(sgn ? (v < 0 ? 1u : 0u) : fv, sgn ? 1 : fl);
-        const int s1 = sl == 0 ? 1 : sl;
-        sl = sgn ? sl : ((a > (3 << (s1 - 1)) && s1 < 6) ? s1 + 1 : s1);
-        /* run_before of the previous non-zero level (7.4.5.3.3), masked */
-        {
-            const bool act = k > 0 && zl > 0;
-            const int run = act ? pprev - p - 1 : 0;
-            const uint32_t e = P.rb[(zl < 7 ? (zl > 0 ? zl : 1) : 7) - 1][run];
-            const int l = act ? (int)(e >> 8) : 0;
-            runs = (runs << l) | (act ? (e & 255u) : 0u);
-            rn += l;
-            zl -= run;
-        }
-        pprev = p;
-    }
-    if (tc < MAX) {
-        const uint32_t e = MAX == 4 ? P.tzdc[tc - 1][tz] : P.tz[tc - 1][tz];
-        cap.put(e & 255u, (int)(e >> 8));
-    }
-    if (rn > 64) {
-        ok = false;
-        cap.n += (uint32_t)rn;
-    } else {
-        if (rn > 32) cap.put((uint32_t)(runs >> 32), rn - 32);
-        cap.put((uint32_t)runs, rn > 32 ? 32 : rn);
-    }
-    ok = ok && cap.n <= 128;
-    return tc;
-}
-
 /* The nC-independent part of a CAVLC block (everything after coeff_token:
  * trailing-ones signs, levels, total_zeros, run_before) of up to 16 packed
- * int8 levels, maxc = maxNumCoeff (16 luma, 15 chroma AC; the level bytes
- * past maxc are zero), in the same branch-free loop over the non-zero
- * levels as cavlc_nz.  Returns TotalCoeff, TrailingOnes in t1o; ok = false
+ * int8 levels (scan order, level i in byte i & 3 of word i >> 2), maxc =
+ * maxNumCoeff (16 luma, 15 chroma AC; the level bytes past maxc are zero),
+ * in one loop over the NON-ZERO levels only, branch-free inside: the wave
+ * iterates the max TotalCoeff of its lanes (callers group blocks by
+ * TotalCoeff).  run_before codes gather in a 64-bit side register first.
+ * The levels come by value: an array indexed by a variable would be kept
+ * in scratch memory.  Returns TotalCoeff, TrailingOnes in t1o; ok = false
  * when cap or the run register overflowed (cap.n is still exact). */
 template <class CAP>
-__device__ __host__ inline int cavlc_body(CAP &cap, const PTabs &P, const uint32_t pk[4], int maxc, int &t1o,
-                                          bool &ok)
+__device__ __host__ inline int cavlc_body(CAP &cap, const PTabs &P, uint4 pk, int maxc, int &t1o, bool &ok)
 {
+    const uint32_t pw[4] = {pk.x, pk.y, pk.z, pk.w};
     uint32_t nz = 0;
 #pragma unroll
-    for (int i = 0; i < 16; ++i) nz |= (((pk[i >> 2] >> (8 * (i & 3))) & 255u) != 0 ? 1u : 0u) << i;
+    for (int i = 0; i < 16; ++i) nz |= (((pw[i >> 2] >> (8 * (i & 3))) & 255u) != 0 ? 1u : 0u) << i;
     const int tc = __builtin_popcount(nz);
-    auto lev = [&](int p) -> int {
-        const uint32_t w01 = (p & 4) ? pk[1] : pk[0], w23 = (p & 4) ? pk[3] : pk[2];
-        const uint32_t wv = (p & 8) ? w23 : w01;
-        return (int)(int8_t)(uint8_t)(wv >> (8 * (p & 3)));
+    const uint64_t lo64 = (uint64_t)pk.x | (uint64_t)pk.y << 32, hi64 = (uint64_t)pk.z | (uint64_t)pk.w << 32;
+    auto lev = [](uint64_t lo, uint64_t hi, int p) -> int {   /* captures nothing: no lambda object */
+        const uint64_t v = (p & 8) ? hi : lo;
+        return (int)(int8_t)(uint8_t)(v >> (8 * (p & 7)));
     };
     int t1 = 0;
     {
@@ -711,7 +563,7 @@ __device__ __host__ inline int cavlc_body(CAP &cap, const PTabs &P, const uint32
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
             const int p = m ? top_bit(m) : 0;
-            const int v = m ? lev(p) : 0;
+            const int v = m ? lev(lo64, hi64, p) : 0;
             run = run && m && (v == 1 || v == -1);
             t1 += run ? 1 : 0;
             m &= m ? ~(1u << p) : ~0u;
@@ -728,7 +580,7 @@ __device__ __host__ inline int cavlc_body(CAP &cap, const PTabs &P, const uint32
     for (int k = 0; k < tc; ++k) {
         const int p = top_bit(m);
         m &= ~(1u << p);
-        const int v = lev(p);
+        const int v = lev(lo64, hi64, p);
         const int a = v < 0 ? -v : v;
         const bool sgn = k < t1;
         int code = 2 * a - 2 + (v < 0 ? 1 : 0);

@@ -16,26 +16,30 @@ typedef struct {
     uint32_t *rows;
     uint16_t *meta;
     uint2 *body_lo, *body_hi;       /* record bodies: bits 0..63, bits 64..127 */
-    unsigned long long *status;     /* k_dyn_group look-back: per (frame, row group) */
-    unsigned long long *tails;      /* k_dyn_group: per (frame, row group) pending end word */
+    unsigned long long *tcx;        /* k_dyn_row: per (frame, rect row, MB) bottom TotalCoeffs */
+    uint32_t *rowstage;             /* per (frame, row group): its bits from bit 0 (rs_frame_words) */
+    uint32_t *gbits;                /* per (frame, row group): its bit count */
     uint32_t epoch;                 /* look-back epoch of the last compose (24 bits, never 0) */
 } DynScratch;
 
-/* k_dyn_rows + k_dyn_code (both instantiations): block records */
-int dyn_launch_code(hipStream_t hs, int nframes, int S, const DevStream *st, const NalDesc *nal,
+/* k_dyn_rows + k_dyn_code_general (records of the general-path NALs) +
+ * k_dyn_row (every rect row: block coding + packing -> its row-stage bits) */
+int dyn_launch_code(hipStream_t hs, int nframes, int S, DevStream *st, const NalDesc *nal,
                     int ld_nal, const PlanPending *pend, DynFrame *dfr, int ld_fr,
-                    const DynGeom *g, const uint8_t *src, const uint8_t *refs, const DynScratch *x);
-/* k_dyn_group + k_dyn_ep: records -> staged RBSP + EP positions */
+                    const DynGeom *g, const uint8_t *src, const uint8_t *refs, const DynScratch *x,
+                    uint32_t epoch, int mbw, uint64_t *stamps);
+/* k_dyn_static (static row groups) + k_dyn_stitch: staged RBSP + EP positions */
 int dyn_launch_pack(hipStream_t hs, int nframes, int S, DevStream *st, const NalDesc *nal,
                     int ld_nal, const PlanPending *pend, DynFrame *dfr, int ld_fr,
-                    const DynGeom *g, const DynScratch *x, uint8_t *stage, uint32_t epoch,
-                    uint64_t *stamps, int mbw, int mbh);
+                    const DynGeom *g, const DynScratch *x, uint8_t *stage);
 int dyn_launch_emit(hipStream_t hs, int nframes, int S, const DevStream *st, const NalDesc *nal,
                     int ld_nal, const DynFrame *dfr, int ld_fr, const DynGeom *g,
                     const uint8_t *stage, uint8_t *arena, uint64_t ld_arena, uint64_t *stamps);
 int dyn_launch_synth(hipStream_t hs, int nframes, int S, uint8_t *src, const DynGeom *g,
                      int stream_base, int t0);
 
+/* row-stage geometry (rs_* fields) of a rect in an mbw x mbh picture */
+void dyn_rowstage_geom(DynGeom *g, int mbw, int mbh);
 /* staging bytes per frame that no dynamic NAL can exceed */
 size_t dyn_slot_bound(int mbw, int mbh, int rw, int rh);
 

@@ -7,10 +7,14 @@
  *
  *   k_plan (state pass)   waypoint state machine, NalDesc per NAL
  *   k_dyn_rows            per NAL: prediction row offsets (waypoint chains)
- *   k_dyn_code[_general]  per 4x4 block: transform, quant, CAVLC body -> records
- *   k_dyn_group           one wave per MB-row group: tokens, cbp, offsets,
- *                         start bit by look-back, bits -> staging slot
- *   k_dyn_ep              emulation-prevention positions + count
+ *   k_dyn_code_general    the rare half-pel-chroma NALs: block records
+ *   k_dyn_row             one workgroup per rect MB row: transform, quant,
+ *                         CAVLC, coeff_token, cbp, MB offsets, bits -> the
+ *                         row's own row-stage words (records stay in LDS)
+ *   k_dyn_static          one wave per static row group (slice header, rows
+ *                         above / below the rect, stop bit) -> row-stage words
+ *   k_dyn_stitch          per NAL: row-group offsets, funnel-shift assembly of
+ *                         the staged RBSP, emulation-prevention positions
  *   k_plan (size pass)    NAL sizes (dynamic: 5 + RBSP + EP), arena offsets
  *   k_emit                every other NAL (dynamic NALs are "external")
  *   k_dyn_emit_gather     staged RBSP -> arena: start code, NAL header, EP
@@ -77,30 +81,16 @@ __device__ inline NalCtx nal_ctx(const DevStream *S, const NalDesc &d, const int
 }
 
 /* ====================================================================== */
-/* The dynamic-rect coder is four kernels:                 */
-/*                                                                         */
-/*   k_dyn_rows   per NAL: the waypoint chain of every prediction row of   */
-/*                the rect, resolved once to byte offsets in picture A / B */
-/*   k_dyn_code   per 4x4 block, all blocks of all NALs at once: residual, */
-/*                transform, quant and the nC-independent CAVLC body      */
-/*                (signs, levels, total_zeros, run_before) -> records;     */
-/*                chroma DC whole (nC = -1)                                */
-/*   k_dyn_group  per MB-row group of a NAL: coeff_token from the          */
-/*                neighbours' TotalCoeff, cbp, MB heads, offsets; start    */
-/*                bit by a look-back over the groups before; bits -> LDS   */
-/*                -> staging words                                         */
-/*   k_dyn_ep     per NAL: shared boundary words merged, emulation-        */
-/*                prevention positions and count                           */
-/*                                                                         */
-/* Records of dynamic MB q (rect raster order) of NAL n, piece pc, at       */
-/*   rec_of(q, pc): k_dyn_code's task order -- luma 16 q + pc, chroma AC    */
-/*   16 nd + 8 q + pc - 18, chroma DC 24 nd + 2 q + pc - 16 (nd = w h):     */
-/*   0..15 luma 4x4 (raster), 16 / 17 Cb / Cr DC, 18 + 4p + b chroma AC    */
-/*   (plane p, raster b): meta[n][q][pc] (u16) = body bits | TotalCoeff << 8 | */
-/*   TrailingOnes << 13 | ovf << 15, body[n][q][pc] = the body right-      */
-/*   aligned in 128 bits (x = bits 0..31 .. w = bits 96..127); DC pieces   */
-/*   hold the whole block.  ovf: more than 128 bits -- body holds the      */
-/*   levels instead (int8 scan order; DC: int16) and k_dyn_group re-codes. */
+/* Pieces of dynamic MB q (rect raster order): pc 0..15 luma 4x4 (raster),  */
+/* 16 / 17 Cb / Cr DC, 18 + 4p + b chroma AC (plane p, raster b).  A piece's */
+/* meta (u16) = body bits | TotalCoeff << 8 | TrailingOnes << 13 | ovf << 15;*/
+/* its body = the CAVLC bits after coeff_token right-aligned in 128 bits    */
+/* (x = bits 0..31 .. w = bits 96..127; DC pieces hold the whole block).    */
+/* ovf: more than 128 bits -- the body holds the levels instead (int8 scan  */
+/* order; DC: int16) and the packer re-codes them.  k_dyn_row keeps them in */
+/* LDS by slot q NPC + pc of its row; k_dyn_code_general's records live in  */
+/* global memory at rec_of(q, pc) -- its task order: luma 16 q + pc, chroma */
+/* AC 16 nd + 8 q + pc - 18, chroma DC 24 nd + 2 q + pc - 16 (nd = w h).    */
 /* ====================================================================== */
 constexpr int NPC = DYN_PIECES;         /* pieces per dynamic MB */
 
@@ -196,15 +186,16 @@ __global__ __launch_bounds__(256) void k_dyn_rows(const DevStream *__restrict__ 
 }
 
 /* ---------------------------------------------------------------------- */
-/* k_dyn_code                                                              */
+/* k_dyn_code_general: block records of the general-path NALs              */
 /* ---------------------------------------------------------------------- */
-/* grid (ceil(24 nd / 256), frames, streams); task = one 4x4 block of a NAL:
- * [0, 16 nd) luma, MB-major (16 lanes = one MB: 4 MBs per wave read 64
- * contiguous source bytes per row), then [16 nd, 24 nd) chroma AC, MB-major,
- * Cb quad then Cr quad (a quad's lanes exchange their DC coefficients).
- * Phase 1: residual -> transform -> quant -> levels (LDS); phase 2, after
- * one barrier: blocks with <= 3 non-zero levels are coded first, so the
- * CAVLC loop of most waves iterates <= 3 times. */
+/* NALs whose waypoint chain has a half-pel chroma step (k_dyn_rows flags
+ * them; never for the waypoints the composer creates) predict chroma
+ * through chroma_px_any, a bilinear tree too register-hungry for k_dyn_row.
+ * Their blocks are coded here into records in global memory, which
+ * k_dyn_row then packs.  Workgroup = 256 block tasks of one NAL: [0, 16 nd)
+ * luma MB-major, [16 nd, 24 nd) chroma AC (MB, plane, raster 2x2; a quad's
+ * lanes exchange their DC coefficients); levels, a counting sort on
+ * TotalCoeff, then the CAVLC bodies largest first. */
 #ifndef SCROLL_CODE_T
 #define SCROLL_CODE_T 256
 #endif
@@ -217,7 +208,6 @@ constexpr int CODE_T = SCROLL_CODE_T, CODE_NW = CODE_T / 64;
 constexpr int SORT_KEYS = SCROLL_SORT_KEYS;
 static_assert(SORT_KEYS >= 2 && SORT_KEYS <= 17, "TotalCoeff classes");
 
-template <bool GENERAL>
 __device__ inline void code_frame(const DevStream *__restrict__ st,
                                                      const DynFrame *__restrict__ dfr, int ld_fr,
                                                      const PlanPending *__restrict__ pend,
@@ -236,17 +226,13 @@ __device__ inline void code_frame(const DevStream *__restrict__ st,
     const int t = threadIdx.x;
     const int lane = t & 63, wave = t >> 6;
     const DynFrame df = dfr[(size_t)s * ld_fr + f];
-    if (df.nal < 0) return;
-    if (GENERAL != ((df.err & DF_GENERAL) != 0)) return;
+    if (df.nal < 0 || !(df.err & DF_GENERAL)) return;
     load_ptabs(ptabs, t, CODE_T);
-    if (GENERAL && t < 8) {
+    if (t < 8) {
         wo[t] = pend[s].wo[t];
         wv[t] = pend[s].wv[t];
     }
-    /* the general chroma path reads wo / wv before the sort; otherwise the
-     * sort's first barrier publishes ptabs, and the pixel loads need not
-     * wait for the table copy */
-    if (GENERAL) __syncthreads();
+    __syncthreads();
 
     const int ndt = g.w * g.h, ntask = 24 * ndt;
     const int task = bx * CODE_T + t;
@@ -286,13 +272,8 @@ __device__ inline void code_frame(const DevStream *__restrict__ st,
         uint32_t sv[4], pv[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-#ifdef SCROLL_ABL_NOLOAD
-            sv[i] = 0x80808080u + (uint32_t)(task * 7 + i * 3) * 0x01010101u;
-            pv[i] = 0x80808080u;
-#else
             sv[i] = ld32(sp + (size_t)i * lstride);
             pv[i] = ld32(pp + re[i]);
-#endif
         }
         int res[16], W[16];
 #pragma unroll
@@ -316,29 +297,20 @@ __device__ inline void code_frame(const DevStream *__restrict__ st,
         int res[16], W[16];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-#ifdef SCROLL_ABL_NOLOAD
-            const uint32_t sv = 0x80808080u + (uint32_t)(task * 5 + i) * 0x01010101u;
-            const uint32_t ea = 0;
-#else
             const uint32_t sv = ld32(sp + (size_t)i * cstride);
             const uint32_t ea = re[i];
-#endif
             int pred[4];
-            if (!GENERAL || !(ea & ROW_GEN)) {
+            if (!(ea & ROW_GEN)) {
                 const uint32_t fr = (ea >> 28) & 7u;
-#ifdef SCROLL_ABL_NOLOAD
-                const uint32_t av = 0x80808080u, bv = 0u;
-#else
                 const uint32_t av = ld32(cp + (ea & ROW_OFF));
                 const uint32_t bv = fr ? ld32(cp + (re[8 * g.h + i] & ROW_OFF)) : 0u;
-#endif
 #pragma unroll
                 for (int x = 0; x < 4; ++x) {
                     const int a = (int)((av >> (8 * x)) & 255u), b = (int)((bv >> (8 * x)) & 255u);
                     pred[x] = ((8 - (int)fr) * a + (int)fr * b + 4) >> 3;
                 }
             } else {
-                if constexpr (GENERAL) {        /* half-pel waypoint step: any depth */
+                {                               /* half-pel waypoint step: any depth */
                     const NalDesc d = nal[(size_t)s * ld_nal + df.nal];
                     const int off = d.off, a_end = (h - off) / 16;
                     const int row = g.y0 + ry;
@@ -449,18 +421,13 @@ __device__ inline void code_frame(const DevStream *__restrict__ st,
     const int u = order[t];
     const int tk = bx * CODE_T + u;
     const uint4 v4 = lv[u];
-    const uint32_t q[4] = {v4.x, v4.y, v4.z, v4.w};
     const bool ul = tk < 16 * ndt;
     CapSink cap{0, 0, 0};
     int t1 = 0;
     bool ok = true;
     int tc = 0;
     if (tk < ntask) {
-#ifdef SCROLL_ABL_NOCAVLC
-        tc = __builtin_popcount(q[0] | q[1] | q[2] | q[3]) & 15;
-#else
-        tc = cavlc_body(cap, ptabs, q, ul ? 16 : 15, t1, ok);
-#endif
+        tc = cavlc_body(cap, ptabs, v4, ul ? 16 : 15, t1, ok);
     }
     /* each lane stores its own block's record (task order, so a workgroup's
      * records are one contiguous range; un-sorting through LDS first was
@@ -478,25 +445,9 @@ __device__ inline void code_frame(const DevStream *__restrict__ st,
     }
 }
 
-/* the frames without a half-pel waypoint chain: grid (chunks, frames, streams) */
-__global__ __launch_bounds__(CODE_T) void k_dyn_code(const DevStream *__restrict__ st,
-                                                     const DynFrame *__restrict__ dfr, int ld_fr,
-                                                     const PlanPending *__restrict__ pend,
-                                                     const NalDesc *__restrict__ nal, int ld_nal,
-                                                     DynGeom g, const uint32_t *__restrict__ rows,
-                                                     const uint8_t *__restrict__ src,
-                                                     const uint8_t *__restrict__ refs,
-                                                     uint16_t *__restrict__ meta, uint2 *__restrict__ blo,
-                                                     uint2 *__restrict__ bhi)
-{
-    code_frame<false>(st, dfr, ld_fr, pend, nal, ld_nal, g, rows, src, refs, meta, blo, bhi, blockIdx.z,
-                      blockIdx.y, blockIdx.x);
-}
-
-/* the others (general chroma path, never for the composer's own waypoints):
- * grid (chunks, CODE_GEN_Y), each workgroup finds flagged (stream, frame)
- * pairs 64 at a time -- a launch over every frame would cost more in empty
- * workgroups than the frames it serves */
+/* grid (chunks, CODE_GEN_Y): each workgroup finds the flagged (stream,
+ * frame) pairs 64 at a time -- a launch over every frame would cost more in
+ * empty workgroups than the frames it serves */
 constexpr int CODE_GEN_Y = 64;
 __global__ __launch_bounds__(CODE_T) void k_dyn_code_general(const DevStream *__restrict__ st,
                                                              const DynFrame *__restrict__ dfr, int ld_fr,
@@ -523,7 +474,7 @@ __global__ __launch_bounds__(CODE_T) void k_dyn_code_general(const DevStream *__
             const int q = p0 + __builtin_ctzll(m);
             m &= m - 1;
             const int s = q / nframes, f = q - s * nframes;
-            code_frame<true>(st, dfr, ld_fr, pend, nal, ld_nal, g, rows, src, refs, meta, blo, bhi, s, f,
+            code_frame(st, dfr, ld_fr, pend, nal, ld_nal, g, rows, src, refs, meta, blo, bhi, s, f,
                              blockIdx.x);
             __syncthreads();
         }
@@ -615,65 +566,47 @@ __device__ inline uint32_t row_static_bits(const HeadCtx &H, const uint32_t *hle
     return bits;
 }
 
-/* Row groups of a NAL: g = 0 the rows above the rect (with the slice
- * header), g = 1 .. h the rect rows, g = h + 1 the rows below (with the stop
- * bit).  One workgroup per group measures its bits, takes its start bit from
- * the groups before it by a decoupled look-back over per-group status words,
- * and writes the staging words of its bits; a word shared with the group
- * before / after is completed through the tail hand-off below. */
-
-/* status word: epoch (24) | flag (2: 1 aggregate, 2 inclusive prefix) | bits (38) */
-__device__ inline uint64_t lb_pack(uint32_t epoch, uint32_t flag, uint64_t v)
-{
-    return (uint64_t)(epoch & 0xffffffu) << 40 | (uint64_t)flag << 38 | v;
-}
-
+/* a tagged 8-byte granule, written through to the fabric (k_dyn_row's
+ * TotalCoeff hand-off: epoch in the top 24 bits, read with sc1 polls) */
 __device__ inline void lb_store(unsigned long long *p, uint64_t v)
 {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-/* exclusive prefix of group g, by the 64 lanes of one wave: publishes the
- * aggregate, then reads the status of the 64 groups before at once, sums
- * back to the nearest inclusive prefix (retrying while a group in that span
- * has not published), publishes its own inclusive prefix */
-__device__ inline uint64_t lb_lookback(unsigned long long *sa, int g, uint32_t epoch, uint64_t bits, int lane)
+/* first row-stage word of row group gi in its frame's region: the static
+ * groups above (rs_static_words each), the rect rows (rs_row_words), the
+ * static groups below */
+__host__ __device__ inline uint64_t rs_group_words(const DynGeom &g, int nA, int gi)
 {
-    if (g == 0) {
-        if (lane == 0) lb_store(sa, lb_pack(epoch, 2, bits));
-        return 0;
+    if (gi < nA) return (uint64_t)gi * g.rs_static_words;
+    if (gi < nA + g.h) return (uint64_t)nA * g.rs_static_words + (uint64_t)(gi - nA) * g.rs_row_words;
+    return (uint64_t)(gi - g.h) * g.rs_static_words + (uint64_t)g.h * g.rs_row_words;
+}
+
+/* lo[i]: piece length (11) | nC + 1 (5) << 11 */
+constexpr uint32_t LO_LEN = 0x7ffu;
+
+/* coeff_token of a piece with meta mv at context nC >= 0 (Table 9-5) */
+__device__ inline void piece_token(const uint16_t (*ct)[68], uint32_t mv, int nC, uint32_t &tv, uint32_t &tl)
+{
+    const int tc = tc_of(mv), t1 = (int)((mv >> 13) & 3u);
+    if (nC >= 8) {
+        tv = tc ? (uint32_t)(((tc - 1) << 2) | t1) : 3u;
+        tl = 6;
+    } else {
+        const uint32_t e = ct[nC < 2 ? 0 : (nC < 4 ? 1 : 2)][4 * tc + t1];
+        tv = e & 255u;
+        tl = e >> 8;
     }
-    if (lane == 0) lb_store(sa + g, lb_pack(epoch, 1, bits));
-    uint64_t pre = 0;
-    for (int j = g - 1;;) {
-        const int jj = j - lane;
-        uint64_t v = 0;
-        uint32_t fl = 2;                                    /* before group 0: empty, inclusive */
-        if (jj >= 0) {
-            v = __hip_atomic_load(sa + jj, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            fl = (uint32_t)(v >> 40) == (epoch & 0xffffffu) ? (uint32_t)(v >> 38) & 3u : 0u;
-            v &= (1ull << 38) - 1;
-        }
-        const uint64_t incl = __ballot(fl == 2), none = __ballot(fl == 0);
-        const int fi = incl ? __builtin_ctzll(incl) : 63;   /* nearest inclusive in the window */
-        const uint64_t span = fi == 63 ? ~0ull : (2ull << fi) - 1;
-        if (none & span) {
-            __builtin_amdgcn_s_sleep(1);
-            continue;
-        }
-        const uint64_t c = lane <= fi ? v : 0;
-        uint32_t lo = (uint32_t)(c & 0xffffffu), hi = (uint32_t)(c >> 24);
-#pragma unroll
-        for (int d = 32; d >= 1; d >>= 1) {
-            lo += __shfl_xor(lo, d, 64);
-            hi += __shfl_xor(hi, d, 64);
-        }
-        pre += ((uint64_t)hi << 24) + lo;
-        if (incl) break;
-        j -= 64;
-    }
-    if (lane == 0) lb_store(sa + g, lb_pack(epoch, 2, pre + bits));
-    return pre;
+}
+
+/* one-wave workgroups: LDS hand-offs need ordering, not a workgroup barrier
+ * (whose release fence would also wait for every global store of the wave) */
+__device__ inline void wave_sync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
 /* a > 128-bit block from its levels (rare): measure / write */
@@ -709,174 +642,65 @@ __device__ __attribute__((noinline)) void ovf_put(uint32_t *buf, uint32_t lo, ui
     sk.finish();
 }
 
-/* k_dyn_group is ONE wave per row group: the group's work is a chain of
- * short dependent phases (records -> tokens -> MB layout -> scans ->
- * look-back -> bits -> words), so throughput comes from many groups in
- * flight per CU rather than from wide workgroups; LDS is sized to the rect
- * (dynamic shared memory, group_lds_bytes) */
+/* ---------------------------------------------------------------------- */
+/* k_dyn_static: the static row groups of a dynamic NAL                    */
+/* ---------------------------------------------------------------------- */
+/* A NAL's bits are: slice header, then per MB row the MB heads (one of 12
+ * codeword classes) and, for dynamic MBs, coded_block_pattern,
+ * mb_qp_delta and the present pieces, then the stop bit.  Its MB rows are
+ * row groups: g < nA the rows above the rect, DYN_STATIC_ROWS per group (the
+ * first one holds the slice header and exists even with no rows), then one
+ * per rect row (k_dyn_row), then the static groups below (the last one
+ * holds rbsp_stop_one_bit).  Every group writes its own bits from bit 0 of
+ * its row-stage slot and its bit count; k_dyn_stitch places them. */
 constexpr int GW = 64;
 #ifndef SCROLL_GBUF_WORDS
 #define SCROLL_GBUF_WORDS 256
 #endif
-constexpr int GBUF_WORDS = SCROLL_GBUF_WORDS;          /* 8 Kbit per pass (a config-3 row: ~18 Kbit in 3 passes);
-                                           each pass walks only the MBs / rows it covers */
+constexpr int GBUF_WORDS = SCROLL_GBUF_WORDS;   /* 8 Kbit per pass */
 
-struct GroupFixed {
+struct StaticFixed {
     uint32_t buf[GBUF_WORDS];
     uint64_t hhi[12], hlo[12];
     uint32_t hlen[12];
     int32_t head_over;
     int32_t wo[8], wl[8], wv[8];
-    uint16_t ct[3][68];                 /* coeff_token tables (nC 0-1, 2-3, 4-7), PTabs layout */
+    uint32_t moff[DYN_STATIC_ROWS + 1];
 };
 
-/* dynamic LDS: moff [lines + 1] u32, mbits [w] u32, mt, lo, off16 [NPC w]
- * u16, ma [8 w] u16, cbp / code [w] u8 */
-__host__ __device__ inline size_t group_lds_bytes(int w, int lines)
+/* grid (nA + nB, frames, streams), one wave each */
+__global__ __launch_bounds__(GW) void k_dyn_static(const DevStream *__restrict__ st,
+                                                   const NalDesc *__restrict__ nal, int ld_nal,
+                                                   const PlanPending *__restrict__ pend,
+                                                   const DynFrame *__restrict__ dfr, int ld_fr, DynGeom g,
+                                                   uint32_t *__restrict__ rowstage, uint32_t *__restrict__ gbits)
 {
-    return (size_t)4 * (lines + 1 + w) + (size_t)2 * (3 * NPC * w + 8 * w) + (size_t)2 * w + 16;
-}
-
-/* lo[i]: piece length (11) | nC + 1 (5) << 11 */
-constexpr uint32_t LO_LEN = 0x7ffu;
-
-/* coeff_token of a piece with meta mv at context nC >= 0 (Table 9-5) */
-__device__ inline void piece_token(const uint16_t (*ct)[68], uint32_t mv, int nC, uint32_t &tv, uint32_t &tl)
-{
-    const int tc = tc_of(mv), t1 = (int)((mv >> 13) & 3u);
-    if (nC >= 8) {
-        tv = tc ? (uint32_t)(((tc - 1) << 2) | t1) : 3u;
-        tl = 6;
-    } else {
-        const uint32_t e = ct[nC < 2 ? 0 : (nC < 4 ? 1 : 2)][4 * tc + t1];
-        tv = e & 255u;
-        tl = e >> 8;
-    }
-}
-
-/* k_dyn_group's workgroup is ONE wave: its LDS handoffs need ordering, not a
- * workgroup barrier (whose release fence would also wait for every global
- * store of the wave to complete) */
-__device__ inline void wave_sync()
-{
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-/* grid (g.ngroups, frames, streams), GW threads.  The kernel is latency-bound
- * (one wave per group, look-back waits): SCROLL_GROUP_WAVES caps the VGPRs so
- * that many waves fit per SIMD */
-#ifndef SCROLL_GROUP_WAVES
-#define SCROLL_GROUP_WAVES 6
-#endif
-__global__ __launch_bounds__(GW) __attribute__((amdgpu_waves_per_eu(SCROLL_GROUP_WAVES)))
-void k_dyn_group(DevStream *__restrict__ st,
-                                                  const NalDesc *__restrict__ nal, int ld_nal,
-                                                  const PlanPending *__restrict__ pend,
-                                                  DynFrame *__restrict__ dfr, int ld_fr, DynGeom g,
-                                                  const uint16_t *__restrict__ meta,
-                                                  const uint2 *__restrict__ blo, const uint2 *__restrict__ bhi,
-                                                  unsigned long long *__restrict__ status,
-                                                  unsigned long long *__restrict__ tails, uint32_t epoch, int lines,
-                                                  uint8_t *__restrict__ stage, uint64_t *__restrict__ stamps)
-{
-    __shared__ GroupFixed L;
-    extern __shared__ uint32_t gdyn[];
-    uint64_t stv[6] = {0, 0, 0, 0, 0, 0};
-    if (stamps) stv[0] = __builtin_amdgcn_s_memrealtime();
-    const int gi = blockIdx.x, ng = (int)gridDim.x, f = blockIdx.y, s = blockIdx.z, t = threadIdx.x;
-    DynFrame *DF = dfr + (size_t)s * ld_fr + f;
-    const Rect R{g.x0, g.y0, g.w, g.h};
-    const size_t nb = (size_t)s * ld_fr + f;
-    const int ndt = R.w * R.h;
-    const uint16_t *M = meta + nb * (size_t)(NPC * ndt);
-    const uint2 *BL = blo + nb * (size_t)(NPC * ndt), *BH = bhi + nb * (size_t)(NPC * ndt);
-    /* groups: nA static groups above the rect (the first one holds the slice
-     * header, and exists even with no rows), one per rect row, the static
-     * groups below (the last one holds the stop bit); DYN_STATIC_ROWS rows
-     * per static group */
+    __shared__ StaticFixed L;
     constexpr int SR = DYN_STATIC_ROWS;
+    const Rect R{g.x0, g.y0, g.w, g.h};
     const int nA = max(1, (R.y0 + SR - 1) / SR);
-    const bool first = gi == 0, last = gi == ng - 1, rect = gi >= nA && gi < nA + R.h;
-    const int row = rect ? R.y0 + gi - nA : 0;
-    const int nd = rect ? R.w : 0, npc = NPC * nd;
-    const int q0 = rect ? (row - R.y0) * R.w : 0;
-    uint32_t *moff = gdyn, *mbits = moff + lines + 1;
-    uint16_t *mt = reinterpret_cast<uint16_t *>(mbits + R.w), *lo = mt + NPC * R.w, *off16 = lo + NPC * R.w;
-    uint16_t *ma = off16 + NPC * R.w;
-    uint8_t *cbpa = reinterpret_cast<uint8_t *>(ma + 8 * R.w), *codea = cbpa + R.w;
-    /* piece j of the row in record order (three contiguous runs: luma, chroma
-     * AC, chroma DC) -> its record and its slot k NPC + pc in mt / lo / off16 */
-    auto rec_run = [&](int jr, int &slot) -> int {
-        if (jr < 16 * nd) {
-            slot = (jr >> 4) * NPC + (jr & 15);
-            return 16 * q0 + jr;
-        }
-        if (jr < 24 * nd) {
-            const int a = jr - 16 * nd;
-            slot = (a >> 3) * NPC + 18 + (a & 7);
-            return 16 * ndt + 8 * q0 + a;
-        }
-        const int a = jr - 24 * nd;
-        slot = (a >> 1) * NPC + 16 + (a & 1);
-        return 24 * ndt + 2 * q0 + a;
-    };
-
-    /* rect row: the records first */
-    for (int i0 = 0; i0 < npc; i0 += 4 * GW) {
-        uint16_t v[4];
-        int sl[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const int jr = i0 + t + GW * u;
-            sl[u] = -1;
-            v[u] = jr < npc ? M[rec_run(jr, sl[u])] : (uint16_t)0;
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-            if (sl[u] >= 0) mt[sl[u]] = v[u];
-    }
-    for (int i0 = 0; i0 < 8 * nd; i0 += 4 * GW) {
-        uint16_t v[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const int i = i0 + t + GW * u, k = i >> 3, e = i & 7;
-            const int pcA = e < 4 ? 12 + e : (e < 6 ? 16 + e : 18 + e);
-            v[u] = i < 8 * nd && row > R.y0 ? M[rec_of(q0 + k - R.w, pcA, ndt)] : (uint16_t)0;
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const int i = i0 + t + GW * u;
-            if (i < 8 * nd) ma[i] = v[u];
-        }
-    }
-    const int j = DF->nal;
+    const int gi = (int)blockIdx.x >= nA ? (int)blockIdx.x + R.h : (int)blockIdx.x;
+    const int ng = g.ngroups, f = blockIdx.y, s = blockIdx.z, t = threadIdx.x;
+    const size_t nb = (size_t)s * ld_fr + f;
+    const int j = dfr[nb].nal;
     if (j < 0) return;
+    const bool first = gi == 0, last = gi == ng - 1;
     if (t < 8) {
         L.wo[t] = pend[s].wo[t];
         L.wl[t] = pend[s].wl[t];
         L.wv[t] = pend[s].wv[t];
     }
     if (t == 0) L.head_over = 0;
-    static_assert(sizeof(L.ct) % 8 == 0, "ct copies as uint2");
-    for (int i = t; i < (int)(sizeof(L.ct) / 8); i += GW)      /* only coeff_token lives in LDS here */
-        reinterpret_cast<uint2 *>(&L.ct[0][0])[i] = reinterpret_cast<const uint2 *>(&g_ptabs.ct[0][0])[i];
-    DevStream *S = st + s;
+    const DevStream *S = st + s;
     const NalDesc d = nal[(size_t)s * ld_nal + j];
-    wave_sync();                                        /* waypoint table, ptabs, records */
+    wave_sync();
     const NalCtx c = nal_ctx(S, d, L.wo, L.wl, L.wv);
     const HeadCtx H = head_ctx(c);
     const int mbw = H.mbw, mbh = c.h / 16;
-    const Tabs &TB = g_tabs;
-    const PTabs &PT = *reinterpret_cast<const PTabs *>(&g_ptabs);   /* the rare overflow paths */
     int ra, rb;
     if (gi < nA) {
         ra = gi * SR;
         rb = min(ra + SR, R.y0);
-    } else if (rect) {
-        ra = row;
-        rb = row + 1;
     } else {
         ra = R.y0 + R.h + (gi - nA - R.h) * SR;
         rb = min(ra + SR, mbh);
@@ -903,280 +727,623 @@ void k_dyn_group(DevStream *__restrict__ st,
         H.put_slow(cn, r, col);
         return cn.n;
     };
-
-    uint64_t bits = 0;                   /* the group's bits */
-    if (rect) {
-        /* pieces: coeff_token from the neighbours' TotalCoeff, length */
-        const uint32_t m26 = magic32(NPC);
-        for (int i = t; i < npc; i += GW) {
-            const int k = (int)div_m((uint32_t)i, m26), pc = i - k * NPC;
-            const int col = R.x0 + k;
-            const uint32_t mv = mt[i];
-            const uint16_t *mk = mt + k * NPC;
-            uint32_t tv = 0, tl = 0;
-            int nC = -1;
-            if (pc != 16 && pc != 17) {
-                const int nAe = col > 0 ? 0 : -1, nBe = row > 0 ? 0 : -1;
-                int nA, nB;
-                if (pc < 16) {
-                    const int bx = pc & 3, by = pc >> 2;
-                    nA = bx > 0 ? tc_of(mk[pc - 1]) : (k > 0 ? tc_of(mk[pc + 3 - NPC]) : nAe);
-                    nB = by > 0 ? tc_of(mk[pc - 4]) : (row > R.y0 ? tc_of(ma[8 * k + pc]) : nBe);
-                } else {
-                    const int b = (pc - 18) & 3, bx = b & 1, by = b >> 1;
-                    nA = bx > 0 ? tc_of(mk[pc - 1]) : (k > 0 ? tc_of(mk[pc + 1 - NPC]) : nAe);
-                    nB = by > 0 ? tc_of(mk[pc - 2])
-                                : (row > R.y0 ? tc_of(ma[8 * k + (pc < 22 ? pc - 14 : pc - 16)]) : nBe);
-                }
-                nC = nc_of(nA, nB);
-                piece_token(L.ct, mv, nC, tv, tl);
-            }
-            uint32_t len = tl + (mv & 255u);
-            if (mv & M_OVF) len = ovf_bits(PT, TB, get_body(BL, BH, rec_of(q0 + k, pc, ndt), true), pc, nC);   /* rare */
-            lo[i] = (uint16_t)(len | (uint32_t)(nC + 1) << 11);
+    /* row offsets (rows <= SR: one wave scan) */
+    uint32_t len = 0;
+    const int r = ra + t;
+    if (r < rb) {
+        if (!head_over) {
+            len = row_static_bits(H, L.hlen, r, R);
+        } else {
+            for (int col = 0; col < mbw; ++col) len += head_bits(r, col) + 1u;
         }
-        wave_sync();
-        if (stamps) stv[1] = __builtin_amdgcn_s_memrealtime();
-        /* per dynamic MB: cbp, its code, piece offsets, bits */
-        for (int k = t; k < nd; k += GW) {
-            const uint16_t *mk = mt + k * NPC;
-            int cbp_l = 0;
-#pragma unroll
-            for (int pc = 0; pc < 16; ++pc)
-                if (tc_of(mk[pc])) cbp_l |= 1 << (2 * (pc >> 3) + ((pc & 3) >> 1));
-            bool ac = false;
-#pragma unroll
-            for (int pc = 18; pc < NPC; ++pc) ac |= tc_of(mk[pc]) != 0;
-            const bool dc = (tc_of(mk[16]) | tc_of(mk[17])) != 0;
-            const int cbp_c = ac ? 2 : (dc ? 1 : 0);
-            const int cbp = cbp_l | cbp_c << 4;
-            const int code = TB.cbp_code[cbp];
-            CountSink hs{head_bits(row, R.x0 + k)};
-            put_ue(hs, (uint32_t)code);
-            if (cbp) put_se(hs, 0);                         /* mb_qp_delta */
-            uint32_t off = hs.n;
-            const uint16_t *lk = lo + k * NPC;
-            uint16_t *ok = off16 + k * NPC;
-#pragma unroll
-            for (int blk = 0; blk < 16; ++blk) {            /* luma4x4BlkIdx order */
-                const int r = blk_raster(blk);
-                const bool pres = (cbp_l >> (blk >> 2)) & 1;
-                ok[r] = pres ? (uint16_t)off : (uint16_t)0xffffu;
-                off += pres ? (lk[r] & LO_LEN) : 0u;
-            }
-#pragma unroll
-            for (int k2 = 16; k2 < NPC; ++k2) {             /* Cb DC, Cr DC, Cb AC 0-3, Cr AC 0-3 */
-                const bool pres = k2 < 18 ? cbp_c >= 1 : cbp_c == 2;
-                ok[k2] = pres ? (uint16_t)off : (uint16_t)0xffffu;
-                off += pres ? (lk[k2] & LO_LEN) : 0u;
-            }
-            mbits[k] = off;
-            cbpa[k] = (uint8_t)cbp;
-            codea[k] = (uint8_t)code;
-        }
-        wave_sync();
-        if (stamps) stv[2] = __builtin_amdgcn_s_memrealtime();
-        uint32_t carry = 0;
-        for (int c0 = 0; c0 < mbw; c0 += GW) {
-            const int col = c0 + t;
-            uint32_t len = 0;
-            if (col < mbw) {
-                const int k = col - R.x0;
-                len = (k >= 0 && k < R.w) ? mbits[k] : head_bits(row, col) + 1u;
-            }
-            const uint32_t incl = wave_incl_sum(len, t);
-            if (col < mbw) moff[col] = carry + incl - len;
-            carry += __shfl(incl, GW - 1, GW);
-        }
-        if (t == 0) moff[mbw] = carry;
-        bits = carry;
-    } else {
-        /* rows without dynamic MBs: row offsets */
-        uint32_t carry = F;
-        for (int r0 = ra; r0 < rb; r0 += GW) {
-            const int r = r0 + t;
-            uint32_t len = 0;
-            if (r < rb) {
-                if (!head_over) {
-                    len = row_static_bits(H, L.hlen, r, R);
-                } else {
-                    for (int col = 0; col < mbw; ++col) len += head_bits(r, col) + 1u;
-                }
-            }
-            const uint32_t incl = wave_incl_sum(len, t);
-            if (r < rb) moff[r - ra] = carry + incl - len;
-            carry += __shfl(incl, GW - 1, GW);
-        }
-        if (t == 0) moff[rb - ra] = carry;
-        bits = carry + (last ? 1u : 0u);
     }
+    const uint32_t incl = wave_incl_sum(len, t);
+    if (r < rb) L.moff[r - ra] = F + incl - len;
+    const uint32_t rows_end = F + __shfl(incl, GW - 1, GW);
+    if (t == 0) L.moff[rb - ra] = rows_end;
+    const uint32_t bits = rows_end + (last ? 1u : 0u);
+    if (t == 0) gbits[nb * (size_t)ng + gi] = bits;
+    wave_sync();
 
-    /* start bit from the groups before */
-    if (stamps) stv[3] = __builtin_amdgcn_s_memrealtime();
-    const uint64_t start = lb_lookback(status + nb * (size_t)ng, gi, epoch, bits, t);
-    if (stamps) stv[4] = __builtin_amdgcn_s_memrealtime();
-    const uint64_t end = start + bits;
-    uint32_t *out = reinterpret_cast<uint32_t *>(stage + nb * g.slot_bytes);
-    const uint64_t cap_words = (g.slot_bytes - DYN_OVF_BYTES) / 4 - 4;
-    const bool over = bits && ((end - 1) >> 5) + 2 > cap_words;
-    if (last && t == 0) {
-        DF->ep = 0;
-        DF->err = over ? DF_OVER : 0u;
-        DF->rbsp_bytes = over ? 0u : (uint32_t)((end + 7) >> 3);   /* bitwriter.c:103-111 */
-        if (over) atomicOr((unsigned int *)&S->err, SCROLL_DEVERR_DYN);
-    }
-    const uint32_t rel0 = (uint32_t)(start & 31u);
-    const uint64_t w0 = start >> 5, wl = bits ? (end - 1) >> 5 : 0;
-    const uint32_t nw = (over || !bits) ? 0u : (uint32_t)(wl - w0 + 1);
-    /* The word at the start (when rel0 != 0) also holds the groups before;
-     * the word at the end (when end is not word-aligned) the groups after.
-     * Each group publishes its TAIL -- the pending end word, OR of every
-     * group's bits in it so far -- in an epoch-tagged word, and ORs its
-     * predecessor's tail into its own first word.  The last window is
-     * written first, so the tail is out early and successors hardly wait. */
-    unsigned long long *ts = tails + nb * (size_t)ng;
-    const uint32_t ep24 = epoch & 0xffffffu;
-    const bool in_sh = rel0 != 0, out_sh = (end & 31u) != 0 && !last;   /* the last group writes its end word */
-    auto tail_pub = [&](uint32_t v) { lb_store(ts + gi, (uint64_t)ep24 << 40 | 1ull << 32 | v); };
-    auto tail_wait = [&]() -> uint32_t {
-        for (;;) {
-            const uint64_t v = __hip_atomic_load(ts + gi - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if ((uint32_t)(v >> 40) == ep24 && ((v >> 32) & 1u)) return (uint32_t)v;
-            __builtin_amdgcn_s_sleep(1);
+    uint32_t *out = rowstage + nb * g.rs_frame_words + rs_group_words(g, nA, gi);
+    const uint32_t nw = min((bits + 31u) >> 5, g.rs_static_words);   /* provable bound: never clipped */
+    const int ne = rb - ra;
+    auto cnt_le = [&](uint32_t x) -> int {              /* # e in [0, ne] with moff[e] <= x */
+        int lo = 0, hi = ne + 1;
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (L.moff[mid] <= x) lo = mid + 1;
+            else hi = mid;
         }
+        return lo;
     };
-    if (t == 0) {
-        if (nw == 0) tail_pub(over || !in_sh ? 0u : tail_wait());  /* empty group: passes the tail on */
-        else if (!out_sh) tail_pub(0u);
-    }
-    const int npass = (int)((nw + GBUF_WORDS - 1) / GBUF_WORDS);
-    for (int pi = npass - 1; pi >= 0; --pi) {
-        const uint32_t p0 = (uint32_t)pi * GBUF_WORDS;
+    const uint32_t m_mbw = magic32((uint32_t)mbw);
+    for (uint32_t p0 = 0; p0 < nw; p0 += GBUF_WORDS) {
         const uint32_t n = min((uint32_t)GBUF_WORDS, nw - p0);
         for (uint32_t i = (uint32_t)t; i < n; i += GW) L.buf[i] = 0u;
         wave_sync();
         const LdsOrWin win{L.buf, p0, n};
-        /* the entries (rect: MB columns, static: rows) whose bits meet the
-         * window [32 p0, 32 (p0 + n)): [ea, eb), by binary search on moff */
-        const int ne = rect ? mbw : rb - ra;
-        auto cnt_le = [&](uint32_t x) -> int {          /* # e in [0, ne] with rel0 + moff[e] <= x */
-            int lo = 0, hi = ne + 1;
-            while (lo < hi) {
-                const int mid = (lo + hi) >> 1;
-                if (rel0 + moff[mid] <= x) lo = mid + 1;
-                else hi = mid;
-            }
-            return lo;
-        };
+        if (first && t == 0 && p0 * 32u < F) {          /* slice header, h264_writer.c:549-553 */
+            WSink hs{win, 0, 0, 0};
+            hs.start(0);
+            emit_slice_header(hs, c);
+            hs.finish();
+        }
+        /* the rows whose bits meet the window: [ea, eb) */
         const int ea = max(cnt_le(32u * p0) - 1, 0), eb = min(cnt_le(32u * (p0 + n) - 1u), ne);
-        if (rect) {
-            for (int col = ea + t; col < eb; col += GW) {
-                WSink sk{win, 0, 0, 0};
-                sk.start(rel0 + moff[col]);
-                if (!head_over) {
-                    const int cls = H.sel(row, col);
-                    sk.put_cap(CapSink{L.hhi[cls], L.hlo[cls], L.hlen[cls]});
-                } else {
-                    H.put_slow(sk, row, col);
+        const int nm = eb * mbw;
+        for (int m = ea * mbw + t; m < nm; m += GW) {
+            const int rr = (int)div_m((uint32_t)m, m_mbw), col = m - rr * mbw, rw = ra + rr;
+            uint32_t off = L.moff[rr];
+            WSink sk{win, 0, 0, 0};
+            if (!head_over) {
+                const int b3 = H.sel(rw, 0);
+                off += col == 0 ? 0u : L.hlen[b3] + 1u + (uint32_t)(col - 1) * (L.hlen[b3 + 1] + 1u);
+                if (off >= 32u * (p0 + n)) continue;
+                const int cls = b3 + (col == 0 ? 0 : (col == mbw - 1 ? 2 : 1));
+                if (off + L.hlen[cls] + 1u <= 32u * p0) continue;
+                sk.start(off);
+                sk.put_cap(CapSink{L.hhi[cls], L.hlo[cls], L.hlen[cls]});
+            } else {
+                for (int c2 = 0; c2 < col; ++c2) off += head_bits(rw, c2) + 1u;
+                sk.start(off);
+                H.put_slow(sk, rw, col);
+            }
+            sk.put(1, 1);                               /* coded_block_pattern ue(0) */
+            sk.finish();
+        }
+        if (last && t == 0) {                           /* rbsp_stop_one_bit */
+            WSink sk{win, 0, 0, 0};
+            sk.start(bits - 1u);
+            sk.put(1, 1);
+            sk.finish();
+        }
+        wave_sync();
+        for (uint32_t i = (uint32_t)t; i < n; i += GW) out[p0 + i] = L.buf[i];   /* MSB-first words */
+        wave_sync();
+    }
+}
+
+/* ---------------------------------------------------------------------- */
+/* k_dyn_row: one workgroup per rect MB row of a NAL                       */
+/* ---------------------------------------------------------------------- */
+/* Block coding and row packing in one workgroup: the row's 24 w block
+ * tasks are one thread each (two for rects over 42 MBs wide), their
+ * records never leave LDS.
+ *   1. residual -> transform -> quant -> levels (LDS), chroma DC 2x2;
+ *      the row's bottom TotalCoeffs go out as one tagged 8-byte granule
+ *      per MB (the row below waits for them: its top neighbours, the only
+ *      hand-off between workgroups);
+ *   2. counting sort on TotalCoeff, CAVLC bodies in that order (each
+ *      wave's loop runs about its own blocks' count);
+ *   3. coeff_token per piece from the left / top TotalCoeffs (nC);
+ *   4. per MB cbp, its code and the piece offsets; the row's MB offsets;
+ *   5. the row's bits -> LDS window -> its own row-stage words, from bit 0
+ *      (no position known yet: k_dyn_stitch places every row group).
+ * The static row groups (slice header, rows above / below the rect, stop
+ * bit) are k_dyn_static's.  NALs whose chroma prediction needs the general
+ * path (k_dyn_rows flags them) take their records from k_dyn_code_general
+ * in global memory instead of steps 1-2. */
+constexpr int ROW_MAXT = 1024;
+/* waves per SIMD the register allocation targets (7: <= 72 VGPRs and few
+ * enough SGPRs that two or three row workgroups share a CU) */
+#ifndef SCROLL_ROW_WAVES
+#define SCROLL_ROW_WAVES 7
+#endif
+/* block tasks per thread (about: threads = 24 w / NP rounded up to waves) */
+#ifndef SCROLL_ROW_NP
+#define SCROLL_ROW_NP 3
+#endif
+constexpr int ROW_NPMAX = 8;                    /* tasks per thread at most (1536 tasks / 192) */
+constexpr int ROW_GB = 1024;                    /* bit window: 32 Kbit (a config-3 row ~18 Kbit, one pass) */
+
+struct RowFixed {
+    PTabs ptabs;
+    uint32_t buf[ROW_GB];
+    uint64_t hhi[12], hlo[12];
+    uint32_t hlen[12];
+    int32_t wo[8], wl[8], wv[8];
+    int32_t head_over;
+    uint32_t rt[32];                             /* the row's prediction-row table (k_dyn_rows) */
+    uint16_t wc[48][SORT_KEYS];                  /* blocks per (virtual wave, TotalCoeff class): 24 w / 64 */
+};
+
+/* dynamic LDS of k_dyn_row: lv [NPC w] uint4 (levels, then bodies), mbits
+ * [w] u32, moff [mbw + 1] u32, mt / lo / off16 [NPC w] u16, order [24 w]
+ * u16, ta [8 w] u8 (top TotalCoeffs), cbp / code [w] u8 */
+__host__ __device__ inline size_t row_lds_bytes(int w, int mbw)
+{
+    return (size_t)16 * NPC * w + (size_t)4 * (w + mbw + 1) + (size_t)2 * (3 * NPC * w + 24 * w) +
+           (size_t)10 * w + 16;
+}
+
+/* threads of a k_dyn_row workgroup: one block task each (two past 1024) */
+__host__ __device__ inline int row_threads(int w)
+{
+    const int nt = 24 * w;
+    const int a = (((nt + SCROLL_ROW_NP - 1) / SCROLL_ROW_NP) + 63) & ~63;
+    const int b = (((nt + ROW_NPMAX - 1) / ROW_NPMAX) + 63) & ~63;      /* np <= ROW_NPMAX */
+    const int t = a > b ? a : b;
+    return t < ROW_MAXT ? t : ROW_MAXT;
+}
+
+/* The pixels of block task `task` of rect row ry: luma [0, 16 w)
+ * MB-major, chroma AC [16 w, 24 w) (MB, plane, raster 2x2).  a = source
+ * rows, b = prediction rows (chroma: the upper bilinear rows), c = the lower
+ * bilinear rows, fr = the four rows' 1/8-pel fractions (3 bits each).  The
+ * prediction rows' offsets come from the row's table in LDS (rt). */
+struct BlkPix {
+    uint32_t a[4], b[4], c[4];
+    uint32_t fr;
+};
+
+__device__ inline void row_fetch(int task, int w, int ry, const DynGeom &g, const uint8_t *fs, const uint8_t *rb,
+                                 const uint32_t *rt, uint32_t csz, BlkPix &px)
+{
+    const int lstride = 16 * g.w, cstride = 8 * g.w, ndt = g.w * g.h;
+    px.fr = 0;
+    if (task < 16 * w) {
+        const int k = task >> 4, r = task & 15, bx = r & 3, by = r >> 2;
+        const uint8_t *sp = fs + (size_t)(16 * ry + 4 * by) * lstride + 16 * k + 4 * bx;
+        const uint8_t *pp = rb + 16 * (g.x0 + k) + 4 * bx;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            px.a[i] = ld32(sp + (size_t)i * lstride);
+            px.b[i] = ld32(pp + rt[4 * by + i]);
+            px.c[i] = 0;
+        }
+    } else {
+        const int jj = task - 16 * w, k = jj >> 3, p = (jj >> 2) & 1, r = jj & 3;
+        const int bx = r & 1, by = r >> 1;
+        const uint8_t *fc = fs + (size_t)256 * ndt + (size_t)(p ? 64 * ndt : 0);
+        const uint8_t *sp = fc + (size_t)(8 * ry + 4 * by) * cstride + 8 * k + 4 * bx;
+        const uint8_t *cp = rb + (size_t)p * csz + 8 * (g.x0 + k) + 4 * bx;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const uint32_t ea = rt[16 + 4 * by + i];
+            const uint32_t f = (ea >> 28) & 7u;
+            px.a[i] = ld32(sp + (size_t)i * cstride);
+            px.b[i] = ld32(cp + (ea & ROW_OFF));
+            px.c[i] = f ? ld32(cp + (rt[24 + 4 * by + i] & ROW_OFF)) : 0u;
+            px.fr |= f << (3 * i);
+        }
+    }
+}
+
+/* residual -> transform -> quant: pk = 16 int8 levels in scan order (AC: 15,
+ * from scan index 1), n = TotalCoeff, w0 = chroma DC coefficient
+ * (unquantised) */
+__device__ inline void row_levels(bool luma, const BlkPix &px, uint32_t pk[4], int &n, int &w0)
+{
+    pk[0] = pk[1] = pk[2] = pk[3] = 0;
+    n = 0;
+    w0 = 0;
+    int res[16], W[16];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int f = luma ? 0 : (int)((px.fr >> (3 * i)) & 7u);
+#pragma unroll
+        for (int x = 0; x < 4; ++x) {
+            const int a = (int)((px.b[i] >> (8 * x)) & 255u), c = (int)((px.c[i] >> (8 * x)) & 255u);
+            const int pred = luma ? a : (((8 - f) * a + f * c + 4) >> 3);
+            res[4 * i + x] = (int)((px.a[i] >> (8 * x)) & 255u) - pred;
+        }
+    }
+    fwd4x4(res, W);
+    if (luma) {
+#pragma unroll
+        for (int k2 = 0; k2 < 16; ++k2) {
+            const int v = quant(W[ZZ[k2]], ZZ[k2]);          /* |v| <= 78: int8 */
+            pk[k2 >> 2] |= ((uint32_t)v & 255u) << (8 * (k2 & 3));
+            n += v != 0;
+        }
+    } else {
+        w0 = W[0];
+#pragma unroll
+        for (int k2 = 1; k2 < 16; ++k2) {
+            const int v = quant(W[ZZ[k2]], ZZ[k2]);
+            pk[(k2 - 1) >> 2] |= ((uint32_t)v & 255u) << (8 * ((k2 - 1) & 3));
+            n += v != 0;
+        }
+    }
+}
+
+__device__ inline int row_slot(int task, int w)
+{
+    if (task < 16 * w) return (task >> 4) * NPC + (task & 15);
+    const int jj = task - 16 * w;
+    return (jj >> 3) * NPC + 18 + (jj & 7);
+}
+
+/* grid (h, frames, streams), row_threads(w) threads, row_lds_bytes dynamic LDS */
+__global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL_ROW_WAVES))) void k_dyn_row(DevStream *__restrict__ st,
+                                                     const NalDesc *__restrict__ nal, int ld_nal,
+                                                     const PlanPending *__restrict__ pend,
+                                                     const DynFrame *__restrict__ dfr, int ld_fr, DynGeom g,
+                                                     const uint32_t *__restrict__ rows,
+                                                     const uint8_t *__restrict__ src,
+                                                     const uint8_t *__restrict__ refs,
+                                                     const uint16_t *__restrict__ meta,
+                                                     const uint2 *__restrict__ blo, const uint2 *__restrict__ bhi,
+                                                     unsigned long long *__restrict__ tcx, uint32_t epoch,
+                                                     uint32_t *__restrict__ rowstage, uint32_t *__restrict__ gbits,
+                                                     uint64_t *__restrict__ stamps)
+{
+    __shared__ RowFixed L;
+    extern __shared__ uint4 rdyn[];
+    /* debug: realtime at entry and after each phase (k_dyn_group's slots) */
+    uint64_t stv[6] = {0, 0, 0, 0, 0, 0};
+    if (stamps) stv[0] = __builtin_amdgcn_s_memrealtime();
+    const int r = blockIdx.x, f = blockIdx.y, s = blockIdx.z;
+    const int t = threadIdx.x, T = blockDim.x, lane = t & 63, wave = t >> 6, nwv = T >> 6;
+    const size_t nb = (size_t)s * ld_fr + f;
+    const DynFrame df = dfr[nb];
+    if (df.nal < 0) return;
+    const bool general = (df.err & DF_GENERAL) != 0;
+    const Rect R{g.x0, g.y0, g.w, g.h};
+    const int w = R.w, ndt = R.w * R.h, row = R.y0 + r, npc = NPC * w, ntask = 24 * w;
+    const int ng = g.ngroups;
+    constexpr int SR = DYN_STATIC_ROWS;
+    const int nA = max(1, (R.y0 + SR - 1) / SR);
+    const DevStream *S = st + s;
+    const int mbw = S->w / 16;
+
+    uint4 *lv = rdyn;
+    uint32_t *mbits = reinterpret_cast<uint32_t *>(lv + npc), *moff = mbits + w;
+    uint16_t *mt = reinterpret_cast<uint16_t *>(moff + mbw + 1), *lo = mt + npc, *off16 = lo + npc;
+    uint16_t *order = off16 + npc;
+    uint8_t *ta = reinterpret_cast<uint8_t *>(order + ntask), *cbpa = ta + 8 * w, *codea = cbpa + w;
+
+    if (t < 8) {
+        L.wo[t] = pend[s].wo[t];
+        L.wl[t] = pend[s].wl[t];
+        L.wv[t] = pend[s].wv[t];
+    }
+    if (t == 0) L.head_over = 0;
+    load_ptabs(L.ptabs, t, T);
+    if (!general && t < 32) L.rt[t] = rows[nb * (size_t)(32 * g.h) + (t < 16 ? 16 * r + t : 16 * g.h + (t < 24 ? 8 * r + t - 16 : 8 * g.h + 8 * r + t - 24))];
+    const NalDesc d = nal[(size_t)s * ld_nal + df.nal];
+    const uint32_t ysz = (uint32_t)S->w * (uint32_t)S->h, csz = ysz / 4;
+
+    /* ---- 1-2: records (levels -> CAVLC bodies) into LDS ---------------- */
+    const int np = (ntask + T - 1) / T;                 /* tasks per thread, <= ROW_NPMAX */
+    __syncthreads();                                    /* the row table (rt) */
+    if (!general) {
+        const uint8_t *fs = src + (size_t)s * g.src_ld + (size_t)f * g.src_fr;
+        const uint8_t *rb = refs + (size_t)s * g.ref_ld;
+        int keys[ROW_NPMAX];
+#pragma unroll
+        for (int pa = 0; pa < ROW_NPMAX; ++pa) keys[pa] = SORT_KEYS - 1;
+        BlkPix nx;                                      /* the next task's pixels, in flight */
+        if (t < ntask) row_fetch(t, w, r, g, fs, rb, L.rt, csz, nx);
+        for (int pa = 0; pa < np; ++pa) {
+            const int task = pa * T + t;
+            const BlkPix cur = nx;
+            if (task + T < ntask) row_fetch(task + T, w, r, g, fs, rb, L.rt, csz, nx);
+            uint32_t pk[4];
+            int n = 0, w0 = 0;
+            if (task < ntask) {
+                row_levels(task < 16 * w, cur, pk, n, w0);
+                const int slot = row_slot(task, w);
+                lv[slot] = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+                mt[slot] = (uint16_t)((uint32_t)min(n, 16) << 8);
+            }
+            const int key = SORT_KEYS - 1 - min(n, SORT_KEYS - 1);   /* inactive tasks: n = 0 */
+#pragma unroll
+            for (int q = 0; q < ROW_NPMAX; ++q)
+                if (q == pa) keys[q] = key;
+            /* chroma DC: the quad's four DC coefficients -> 2x2 Hadamard,
+             * quant -> levels as int16 in the DC slot (coded after the
+             * barrier that publishes the CAVLC tables) */
+            const int qb = lane & ~3;
+            const int d0 = __shfl(w0, qb, 64), d1 = __shfl(w0, qb + 1, 64);
+            const int d2 = __shfl(w0, qb + 2, 64), d3 = __shfl(w0, qb + 3, 64);
+            if (task >= 16 * w && task < ntask && (task & 3) == 0) {
+                const int jj = task - 16 * w, k = jj >> 3, p = (jj >> 2) & 1;
+                const int q0 = quant_dc(d0 + d1 + d2 + d3), q1 = quant_dc(d0 - d1 + d2 - d3);
+                const int q2 = quant_dc(d0 + d1 - d2 - d3), q3 = quant_dc(d0 - d1 - d2 + d3);
+                lv[k * NPC + 16 + p] = make_uint4(((uint32_t)q0 & 0xffffu) | (uint32_t)q1 << 16,
+                                                  ((uint32_t)q2 & 0xffffu) | (uint32_t)q3 << 16, 0u, 0u);
+                mt[k * NPC + 16 + p] = (uint16_t)((uint32_t)((q0 != 0) + (q1 != 0) + (q2 != 0) + (q3 != 0)) << 8);
+            }
+        }
+        /* sort classes: per (virtual wave, key) counts */
+        uint32_t belows[ROW_NPMAX];
+#pragma unroll
+        for (int pa = 0; pa < ROW_NPMAX; ++pa) {
+            belows[pa] = 0;
+            if (pa >= np) continue;
+            const int key = keys[pa];
+            uint32_t bl = 0;
+#pragma unroll
+            for (int k = 0; k < SORT_KEYS; ++k) {
+                const uint64_t m = __ballot(key == k);
+                if (lane == 0) L.wc[pa * nwv + wave][k] = (uint16_t)__popcll(m);
+                if (key == k)
+                    bl = (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                             __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+            }
+            belows[pa] = bl;
+        }
+        __syncthreads();                                /* levels, TotalCoeffs, ptabs, counts */
+        if (stamps) stv[1] = __builtin_amdgcn_s_memrealtime();
+        /* the row's bottom TotalCoeffs (luma 12-15, chroma AC raster 2, 3 of
+         * each plane) for the row below: one granule per MB */
+        if (t < w && r + 1 < R.h) {
+            const uint16_t *mk = mt + t * NPC;
+            uint64_t v = 0;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const int pcA = e < 4 ? 12 + e : (e < 6 ? 16 + e : 18 + e);
+                v |= (uint64_t)(tc_of(mk[pcA]) & 31) << (5 * e);
+            }
+            lb_store(tcx + (nb * R.h + r) * (size_t)w + t, (uint64_t)(epoch & 0xffffffu) << 40 | v);
+        }
+        /* chroma DC blocks, whole (nC = -1) */
+        if (t >= T - 2 * w) {
+            const int i = t - (T - 2 * w), k = i >> 1, p = i & 1, sl = k * NPC + 16 + p;
+            const uint4 q = lv[sl];
+            const int dq[4] = {(int)(int16_t)(q.x & 0xffffu), (int)(int16_t)(q.x >> 16),
+                               (int)(int16_t)(q.y & 0xffffu), (int)(int16_t)(q.y >> 16)};
+            CapSink cap{0, 0, 0};
+            const int tc = cavlc_dc4(cap, L.ptabs, dq);
+            if (cap.n <= 128) {
+                mt[sl] = (uint16_t)(cap.n | (uint32_t)tc << 8);
+                lv[sl] = make_uint4((uint32_t)cap.lo, (uint32_t)(cap.lo >> 32), (uint32_t)cap.hi,
+                                    (uint32_t)(cap.hi >> 32));
+            } else {
+                mt[sl] = (uint16_t)((uint32_t)tc << 8 | M_OVF);       /* levels stay in lv */
+            }
+        }
+        const int nvw = np * nwv;
+        if (t < SORT_KEYS) {                            /* key k = t: virtual-wave prefixes, key offsets */
+            uint32_t tot = 0;
+            for (int v2 = 0; v2 < nvw; ++v2) tot += L.wc[v2][t];
+            uint32_t kb = tot;
+#pragma unroll
+            for (int dd = 1; dd < 32; dd <<= 1) {
+                const uint32_t o = __shfl_up(kb, dd, 64);
+                if (lane >= dd) kb += o;
+            }
+            uint32_t run = kb - tot;
+            for (int v2 = 0; v2 < nvw; ++v2) {
+                const uint32_t c2 = L.wc[v2][t];
+                L.wc[v2][t] = (uint16_t)run;
+                run += c2;
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int pa = 0; pa < ROW_NPMAX; ++pa) {        /* inactive tasks sort last, past ntask */
+            if (pa >= np) continue;
+            const int pos = L.wc[pa * nwv + wave][keys[pa]] + (int)belows[pa];
+            if (pos < ntask) order[pos] = (uint16_t)(pa * T + t);
+        }
+        __syncthreads();
+        /* CAVLC bodies, largest TotalCoeff first */
+        for (int pa = 0; pa < np; ++pa) {
+            const int pos = pa * T + t;
+            if (pos >= ntask) continue;
+            const int task = order[pos];
+            const int slot = row_slot(task, w);
+            const uint4 v4 = lv[slot];
+            CapSink cap{0, 0, 0};
+            int t1 = 0;
+            bool ok = true;
+            const int tc = cavlc_body(cap, L.ptabs, v4, task < 16 * w ? 16 : 15, t1, ok);
+            mt[slot] = ok ? (uint16_t)(cap.n | (uint32_t)tc << 8 | (uint32_t)t1 << 13)
+                          : (uint16_t)((uint32_t)tc << 8 | (uint32_t)t1 << 13 | M_OVF);
+            if (ok)
+                lv[slot] = make_uint4((uint32_t)cap.lo, (uint32_t)(cap.lo >> 32), (uint32_t)cap.hi,
+                                      (uint32_t)(cap.hi >> 32));
+        }
+    } else {
+        /* general path: records of k_dyn_code_general */
+        const int q0 = r * w;
+        const uint16_t *M = meta + nb * (size_t)(NPC * ndt);
+        const uint2 *BL = blo + nb * (size_t)(NPC * ndt), *BH = bhi + nb * (size_t)(NPC * ndt);
+        for (int i = t; i < npc; i += T) {
+            const int k = i / NPC, pc = i - k * NPC;
+            const int rec = rec_of(q0 + k, pc, ndt);
+            const uint16_t mv = M[rec];
+            mt[i] = mv;
+            if ((mv & 255u) || (mv & M_OVF)) lv[i] = get_body(BL, BH, rec, (mv & 255u) > 64u || (mv & M_OVF));
+        }
+        for (int i = t; i < 8 * w; i += T) {
+            const int k = i >> 3, e = i & 7;
+            const int pcA = e < 4 ? 12 + e : (e < 6 ? 16 + e : 18 + e);
+            ta[i] = r > 0 ? (uint8_t)tc_of(M[rec_of(q0 + k - w, pcA, ndt)]) : (uint8_t)0;
+        }
+    }
+    /* top TotalCoeffs of the row above (normal path): its granules; the last
+     * wave polls (the sort gives it the lightest blocks) */
+    if (!general && wave == nwv - 1) {
+        for (int k = lane; k < w; k += 64) {
+            uint64_t v = 0;
+            if (r > 0) {
+                const unsigned long long *p = tcx + (nb * R.h + r - 1) * (size_t)w + k;
+                for (;;) {
+                    v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if ((uint32_t)(v >> 40) == (epoch & 0xffffffu)) break;
+                    __builtin_amdgcn_s_sleep(1);
                 }
+            }
+#pragma unroll
+            for (int e = 0; e < 8; ++e) ta[8 * k + e] = (uint8_t)((v >> (5 * e)) & 31u);
+        }
+    }
+    __syncthreads();                                    /* records, top TotalCoeffs, waypoint table */
+    if (stamps) stv[2] = __builtin_amdgcn_s_memrealtime();
+
+    /* ---- 3: coeff_token, piece lengths ----------------------------------- */
+    const NalCtx c = nal_ctx(S, d, L.wo, L.wl, L.wv);
+    const HeadCtx H = head_ctx(c);
+    if (t < 12) {
+        CapSink hc{0, 0, 0};
+        H.put_class(hc, t);
+        L.hhi[t] = hc.hi;
+        L.hlo[t] = hc.lo;
+        L.hlen[t] = hc.n;
+        if (hc.over()) L.head_over = 1;
+    }
+    const Tabs &TB = g_tabs;
+    const PTabs &PT = *reinterpret_cast<const PTabs *>(&g_ptabs);       /* the rare overflow paths */
+    const uint16_t(*ctab)[68] = L.ptabs.ct;
+    for (int i = t; i < npc; i += T) {
+        const int k = i / NPC, pc = i - k * NPC, col = R.x0 + k;
+        const uint32_t mv = mt[i];
+        const uint16_t *mk = mt + k * NPC;
+        uint32_t tv = 0, tl = 0;
+        int nC = -1;
+        if (pc != 16 && pc != 17) {
+            const int nAe = col > 0 ? 0 : -1, nBe = row > 0 ? 0 : -1;
+            int nA2, nB2;
+            if (pc < 16) {
+                const int bx = pc & 3, by = pc >> 2;
+                nA2 = bx > 0 ? tc_of(mk[pc - 1]) : (k > 0 ? tc_of(mk[pc + 3 - NPC]) : nAe);
+                nB2 = by > 0 ? tc_of(mk[pc - 4]) : (r > 0 ? (int)ta[8 * k + pc] : nBe);
+            } else {
+                const int b = (pc - 18) & 3, bx = b & 1, by = b >> 1;
+                nA2 = bx > 0 ? tc_of(mk[pc - 1]) : (k > 0 ? tc_of(mk[pc + 1 - NPC]) : nAe);
+                nB2 = by > 0 ? tc_of(mk[pc - 2]) : (r > 0 ? (int)ta[8 * k + (pc < 22 ? pc - 14 : pc - 16)] : nBe);
+            }
+            nC = nc_of(nA2, nB2);
+            piece_token(ctab, mv, nC, tv, tl);
+        }
+        uint32_t len = tl + (mv & 255u);
+        if (mv & M_OVF) len = ovf_bits(PT, TB, lv[i], pc, nC);            /* rare */
+        lo[i] = (uint16_t)(len | (uint32_t)(nC + 1) << 11);
+    }
+    __syncthreads();
+    if (stamps) stv[3] = __builtin_amdgcn_s_memrealtime();
+    const bool head_over = L.head_over;
+    auto head_bits = [&](int rr, int col) -> uint32_t {
+        if (!head_over) return L.hlen[H.sel(rr, col)];
+        CountSink cn{0};
+        H.put_slow(cn, rr, col);
+        return cn.n;
+    };
+
+    /* ---- 4: per MB cbp, code, piece offsets; the row's MB offsets ------- */
+    for (int k = t; k < w; k += T) {
+        const uint16_t *mk = mt + k * NPC;
+        int cbp_l = 0;
+#pragma unroll
+        for (int pc = 0; pc < 16; ++pc)
+            if (tc_of(mk[pc])) cbp_l |= 1 << (2 * (pc >> 3) + ((pc & 3) >> 1));
+        bool ac = false;
+#pragma unroll
+        for (int pc = 18; pc < NPC; ++pc) ac |= tc_of(mk[pc]) != 0;
+        const bool dc = (tc_of(mk[16]) | tc_of(mk[17])) != 0;
+        const int cbp_c = ac ? 2 : (dc ? 1 : 0);
+        const int cbp = cbp_l | cbp_c << 4;
+        const int code = TB.cbp_code[cbp];
+        CountSink hs{head_bits(row, R.x0 + k)};
+        put_ue(hs, (uint32_t)code);
+        if (cbp) put_se(hs, 0);                         /* mb_qp_delta */
+        uint32_t off = hs.n;
+        const uint16_t *lk = lo + k * NPC;
+        uint16_t *ok = off16 + k * NPC;
+#pragma unroll
+        for (int blk = 0; blk < 16; ++blk) {            /* luma4x4BlkIdx order */
+            const int rr = blk_raster(blk);
+            const bool pres = (cbp_l >> (blk >> 2)) & 1;
+            ok[rr] = pres ? (uint16_t)off : (uint16_t)0xffffu;
+            off += pres ? (lk[rr] & LO_LEN) : 0u;
+        }
+#pragma unroll
+        for (int k2 = 16; k2 < NPC; ++k2) {             /* Cb DC, Cr DC, Cb AC 0-3, Cr AC 0-3 */
+            const bool pres = k2 < 18 ? cbp_c >= 1 : cbp_c == 2;
+            ok[k2] = pres ? (uint16_t)off : (uint16_t)0xffffu;
+            off += pres ? (lk[k2] & LO_LEN) : 0u;
+        }
+        mbits[k] = off;
+        cbpa[k] = (uint8_t)cbp;
+        codea[k] = (uint8_t)code;
+    }
+    __syncthreads();
+    const int gi = nA + r;
+    if (wave == 0) {
+        uint32_t carry = 0;
+        for (int c0 = 0; c0 < mbw; c0 += 64) {
+            const int col = c0 + lane;
+            uint32_t len = 0;
+            if (col < mbw) {
                 const int k = col - R.x0;
-                if (!(k >= 0 && k < R.w)) {
-                    sk.put(1, 1);                           /* coded_block_pattern ue(0) */
-                } else {
-                    put_ue(sk, (uint32_t)codea[k]);
-                    if (cbpa[k]) put_se(sk, 0);
-                }
-                sk.finish();
+                len = (k >= 0 && k < w) ? mbits[k] : head_bits(row, col) + 1u;
             }
-            const uint32_t m26 = magic32(NPC);
-            const int pa = NPC * max(ea - R.x0, 0), pb = NPC * min(eb - R.x0, nd);
-            for (int i0 = pa; i0 < pb; i0 += 4 * GW) {
-                uint4 bd[4];
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {               /* four body loads in flight */
-                    const int i = i0 + t + GW * u;
-                    bd[u] = make_uint4(0, 0, 0, 0);
-                    if (i < pb && off16[i] != 0xffffu && (mt[i] & (255u | M_OVF))) {
-                        const int k = (int)div_m((uint32_t)i, m26);
-                        bd[u] = get_body(BL, BH, rec_of(q0 + k, i - k * NPC, ndt), (mt[i] & 255u) > 64u || (mt[i] & M_OVF));
-                    }
-                }
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    const int i = i0 + t + GW * u;
-                    if (i >= pb) continue;
-                    const uint32_t o = off16[i];
-                    if (o == 0xffffu) continue;
-                    const int k = (int)div_m((uint32_t)i, m26), pc = i - k * NPC;
-                    const uint32_t e = lo[i], mv = mt[i];
-                    const int nC = (int)(e >> 11) - 1;
-                    const uint32_t pos = rel0 + moff[R.x0 + k] + o;
-                    if (!(mv & M_OVF)) {
-                        WSink sk{win, 0, 0, 0};
-                        sk.start(pos);
-                        if (nC != -1) {
-                            uint32_t tv, tl;
-                            piece_token(L.ct, mv, nC, tv, tl);
-                            sk.put(tv, (int)tl);
-                        }
-                        sk.put_cap(CapSink{(uint64_t)bd[u].z | (uint64_t)bd[u].w << 32,
-                                           (uint64_t)bd[u].x | (uint64_t)bd[u].y << 32, mv & 255u});
-                        sk.finish();
-                    } else {
-                        ovf_put(L.buf, p0, n, pos, PT, TB, bd[u], pc, nC);
-                    }
-                }
+            const uint32_t incl = wave_incl_sum(len, lane);
+            if (col < mbw) moff[col] = carry + incl - len;
+            carry += __shfl(incl, 63, 64);
+        }
+        if (lane == 0) {
+            moff[mbw] = carry;
+            gbits[nb * (size_t)ng + gi] = carry;
+        }
+    }
+    __syncthreads();
+    if (stamps) stv[4] = __builtin_amdgcn_s_memrealtime();
+    const uint32_t bits = moff[mbw];
+
+    /* ---- 5: bits -> the row's own row-stage words ------------------------ */
+    uint32_t *out = rowstage + nb * g.rs_frame_words + rs_group_words(g, nA, gi);
+    const uint32_t nw = min((bits + 31u) >> 5, g.rs_row_words);   /* provable bound: never clipped */
+    const int npass = (int)((nw + ROW_GB - 1) / ROW_GB);
+    for (int pi = 0; pi < npass; ++pi) {
+        const uint32_t p0 = (uint32_t)pi * ROW_GB;
+        const uint32_t n = min((uint32_t)ROW_GB, nw - p0);
+        for (uint32_t i = (uint32_t)t; i < n; i += (uint32_t)T) L.buf[i] = 0u;
+        __syncthreads();
+        const LdsOrWin win{L.buf, p0, n};
+        /* MB heads (+ coded_block_pattern / mb_qp_delta) of every column */
+        for (int col = t; col < mbw; col += T) {
+            const uint32_t pos = moff[col];
+            if (pos >= 32u * (p0 + n) || moff[col + 1] <= 32u * p0) continue;
+            WSink sk{win, 0, 0, 0};
+            sk.start(pos);
+            if (!head_over) {
+                const int cls = H.sel(row, col);
+                sk.put_cap(CapSink{L.hhi[cls], L.hlo[cls], L.hlen[cls]});
+            } else {
+                H.put_slow(sk, row, col);
             }
-        } else {
-            if (first && t == 0 && p0 * 32u < F) {          /* slice header, h264_writer.c:549-553 */
-                WSink hs{win, 0, 0, 0};
-                hs.start(0);
-                emit_slice_header(hs, c);
-                hs.finish();
+            const int k = col - R.x0;
+            if (!(k >= 0 && k < w)) {
+                sk.put(1, 1);                           /* coded_block_pattern ue(0) */
+            } else {
+                put_ue(sk, (uint32_t)codea[k]);
+                if (cbpa[k]) put_se(sk, 0);
             }
-            const int nm = eb * mbw;
-            const uint32_t m_mbw = magic32((uint32_t)mbw);
-            for (int m = ea * mbw + t; m < nm; m += GW) {
-                const int rr = (int)div_m((uint32_t)m, m_mbw), col = m - rr * mbw, r = ra + rr;
-                uint32_t off = moff[rr];
+            sk.finish();
+        }
+        /* pieces */
+        for (int i = t; i < npc; i += T) {
+            const uint32_t o = off16[i];
+            if (o == 0xffffu) continue;
+            const int k = i / NPC, pc = i - k * NPC;
+            const uint32_t e = lo[i], mv = mt[i];
+            const uint32_t pos = moff[R.x0 + k] + o;
+            if (pos >= 32u * (p0 + n) || pos + (e & LO_LEN) <= 32u * p0) continue;
+            const int nC = (int)(e >> 11) - 1;
+            const uint4 bd = lv[i];
+            if (!(mv & M_OVF)) {
                 WSink sk{win, 0, 0, 0};
-                if (!head_over) {
-                    const int b3 = H.sel(r, 0);
-                    off += col == 0 ? 0u : L.hlen[b3] + 1u + (uint32_t)(col - 1) * (L.hlen[b3 + 1] + 1u);
-                    const int cls = b3 + (col == 0 ? 0 : (col == mbw - 1 ? 2 : 1));
-                    sk.start(rel0 + off);
-                    sk.put_cap(CapSink{L.hhi[cls], L.hlo[cls], L.hlen[cls]});
-                } else {
-                    for (int c2 = 0; c2 < col; ++c2) off += head_bits(r, c2) + 1u;
-                    sk.start(rel0 + off);
-                    H.put_slow(sk, r, col);
+                sk.start(pos);
+                if (nC != -1) {
+                    uint32_t tv, tl;
+                    piece_token(ctab, mv, nC, tv, tl);
+                    sk.put(tv, (int)tl);
                 }
-                sk.put(1, 1);                               /* coded_block_pattern ue(0) */
+                sk.put_cap(CapSink{(uint64_t)bd.z | (uint64_t)bd.w << 32, (uint64_t)bd.x | (uint64_t)bd.y << 32,
+                                   mv & 255u});
                 sk.finish();
-            }
-            if (last && t == 0) {                           /* rbsp_stop_one_bit */
-                WSink sk{win, 0, 0, 0};
-                sk.start(rel0 + (uint32_t)bits - 1u);
-                sk.put(1, 1);
-                sk.finish();
+            } else {
+                ovf_put(L.buf, p0, n, pos, PT, TB, bd, pc, nC);
             }
         }
-        wave_sync();
-        /* every word but a shared first one first -- the out-shared tail is
-         * published before this wave waits for its predecessor's, so small
-         * one-pass groups do not chain their successors behind that wait */
-        for (uint32_t i = (uint32_t)t; i < n; i += GW) {
-            const uint32_t q = p0 + i, v = L.buf[i];
-            if (q == 0 && in_sh) continue;
-            if (q == nw - 1 && out_sh) tail_pub(v);
-            else out[w0 + q] = __builtin_bswap32(v);
-        }
-        if (p0 == 0 && in_sh && t == 0) {
-            const uint32_t v2 = L.buf[0] | tail_wait();
-            if (nw == 1 && out_sh) tail_pub(v2);
-            else out[w0] = __builtin_bswap32(v2);
-        }
-        wave_sync();
+        __syncthreads();
+        for (uint32_t i = (uint32_t)t; i < n; i += (uint32_t)T) out[p0 + i] = L.buf[i];   /* MSB-first words */
+        __syncthreads();
     }
     if (stamps && t == 0) {
         stv[5] = __builtin_amdgcn_s_memrealtime();
@@ -1187,87 +1354,142 @@ void k_dyn_group(DevStream *__restrict__ st,
     }
 }
 
-/* grid (EP_G, frames, streams): workgroup x scans chunks x, x + EP_G, .. of
- * EP_CHUNK bytes of its NAL's staged RBSP; a chunk's carry-in (the last
- * non-zero byte before it) is looked up backwards in the staged bytes, so
- * chunks are independent.  EP positions (slot tail, unsorted) and count. */
-constexpr int EP_G = 8, EP_T = 256, EP_NW = EP_T / 64, EP_CHUNK = EP_T * 32;
+/* ---------------------------------------------------------------------- */
+/* k_dyn_stitch: row groups -> the NAL's staged RBSP + EP positions         */
+/* ---------------------------------------------------------------------- */
+/* One workgroup per dynamic NAL: the row groups' bit counts -> their
+ * offsets (one wave scan; ngroups <= 64), then every staged word is
+ * assembled from the (one, at group seams two or more) row-stage words it
+ * spans -- a funnel shift -- and stored, 32 bytes per thread and step; the
+ * same step scans those bytes for emulation prevention (closed-form rule,
+ * the zero run carried from the step before by a block max-scan) and
+ * records the EP positions in the slot tail.  Sets rbsp_bytes / ep / err. */
+constexpr int ST_T = 256, ST_NW = ST_T / 64, ST_CHUNK = ST_T * 32;
+static_assert(DYN_MAX_H + 2 * ((DYN_MAX_MBH + DYN_STATIC_ROWS - 1) / DYN_STATIC_ROWS) <= 64,
+              "k_dyn_stitch scans the row groups with one wave");
 
-__global__ __launch_bounds__(EP_T) void k_dyn_ep(DynFrame *__restrict__ dfr, int ld_fr, DynGeom g,
-                                                 const uint8_t *__restrict__ stage)
+__global__ __launch_bounds__(ST_T) void k_dyn_stitch(DevStream *__restrict__ st, DynFrame *__restrict__ dfr,
+                                                     int ld_fr, DynGeom g, const uint32_t *__restrict__ rowstage,
+                                                     const uint32_t *__restrict__ gbits,
+                                                     uint8_t *__restrict__ stage)
 {
-    __shared__ int32_t wmax[EP_NW];
-    __shared__ int32_t back;
-    const int s = blockIdx.z, f = blockIdx.y, t = threadIdx.x, lane = t & 63;
-    DynFrame *DF = dfr + (size_t)s * ld_fr + f;
-    const DynFrame df = *DF;
-    if (df.nal < 0 || df.err) return;
+    __shared__ uint32_t goff[65], gb[64], gw[64];
+    __shared__ int32_t wmax[ST_NW];
+    __shared__ uint32_t ep_n;
+    const int s = blockIdx.y, f = blockIdx.x, t = threadIdx.x, lane = t & 63;
     const size_t nb = (size_t)s * ld_fr + f;
-    const uint8_t *in = stage + nb * g.slot_bytes;
-    uint32_t *eplist = reinterpret_cast<uint32_t *>(const_cast<uint8_t *>(in) + g.slot_bytes - DYN_OVF_BYTES);
-    const uint32_t nin = df.rbsp_bytes;
-    for (uint32_t c0 = (uint32_t)blockIdx.x * EP_CHUNK; c0 < nin; c0 += EP_G * EP_CHUNK) {
-        /* carry-in: wave 0 reads the 256 bytes before the chunk, further back
-         * only while they are all zero */
-        if (t < 64) {
-            int pv = -1;
-            for (int64_t b0 = (int64_t)c0 - 256; b0 > -256; b0 -= 256) {
-                const int64_t o = b0 + 4 * lane;
-                const uint32_t m = o >= 0 ? *reinterpret_cast<const uint32_t *>(in + o) : 0u;
-                const uint64_t nz = __ballot(m != 0);
-                if (nz) {
-                    const int hl = 63 - __builtin_clzll(nz);
-                    const uint32_t mh = __shfl(m, hl, 64);
-                    pv = (int)(b0 + 4 * hl) + 3 - (__builtin_clz(mh) >> 3);
-                    break;
-                }
-            }
-            if (t == 0) back = pv;
+    DynFrame *DF = dfr + nb;
+    if (DF->nal < 0) return;
+    const int ng = g.ngroups;
+    constexpr int SR = DYN_STATIC_ROWS;
+    const int nA = max(1, (g.y0 + SR - 1) / SR);
+    if (t < 64) {
+        const uint32_t b = t < ng ? gbits[nb * (size_t)ng + t] : 0u;
+        const uint32_t incl = wave_incl_sum(b, lane);
+        if (t < ng) {
+            gb[t] = b;
+            goff[t] = incl - b;
+            gw[t] = (uint32_t)rs_group_words(g, nA, t);
         }
-        const uint32_t ib = c0 + 32u * (uint32_t)t;
+        if (t == 63) goff[ng] = incl;
+    }
+    if (t == 0) ep_n = 0;
+    __syncthreads();
+    const uint32_t T = goff[ng];                        /* NAL RBSP bits incl. the stop bit */
+    const uint32_t nin = (T + 7) >> 3;                  /* bitwriter.c:103-111 */
+    /* whole 32-byte steps must fit before the slot tail (EP positions, levels) */
+    const bool over = ((nin + 31u) & ~31u) > g.slot_bytes - DYN_OVF_BYTES;
+    if (over) {
+        if (t == 0) {
+            DF->err = DF_OVER;
+            DF->rbsp_bytes = 0;
+            DF->ep = 0;
+            atomicOr((unsigned int *)&st[s].err, SCROLL_DEVERR_DYN);
+        }
+        return;
+    }
+    uint8_t *out = stage + nb * g.slot_bytes;
+    uint32_t *eplist = reinterpret_cast<uint32_t *>(out + g.slot_bytes - DYN_OVF_BYTES);
+    const uint32_t *fr = rowstage + nb * g.rs_frame_words;
+    int carry = -1;                                     /* last non-zero RBSP byte before the step */
+    for (uint32_t c0 = 0; c0 < nin; c0 += ST_CHUNK) {
+        const uint32_t ib = c0 + 32u * (uint32_t)t;    /* this thread's first byte */
         uint32_t wv[8];
+        {
+            uint32_t P = ib * 8u;                       /* bit position of its first word */
+            int gg = 0;                                 /* the group holding bit P: binary search */
+            {
+                int lo = 0, hi = ng;                    /* last gg with goff[gg] <= P */
+                while (hi - lo > 1) {
+                    const int mid = (lo + hi) >> 1;
+                    if (goff[mid] <= P) lo = mid;
+                    else hi = mid;
+                }
+                gg = lo;
+            }
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            const uint32_t o = ib + 16u * u;
-            const uint4 v = o < nin ? *reinterpret_cast<const uint4 *>(in + o) : make_uint4(0, 0, 0, 0);
-            wv[4 * u] = v.x;
-            wv[4 * u + 1] = v.y;
-            wv[4 * u + 2] = v.z;
-            wv[4 * u + 3] = v.w;
+            for (int k = 0; k < 8; ++k, P += 32u) {
+                uint32_t acc = 0;
+                uint32_t filled = 0;
+                while (filled < 32u && gg < ng && P < T) {
+                    const uint32_t lp = P + filled - goff[gg];
+                    if (lp >= gb[gg]) {                 /* group done (or empty) */
+                        ++gg;
+                        continue;
+                    }
+                    const uint32_t take = min(32u - filled, gb[gg] - lp);
+                    const uint32_t *src = fr + gw[gg];
+                    const uint32_t i = lp >> 5, sh = lp & 31u;
+                    uint32_t x = src[i];
+                    if (sh) {
+                        x <<= sh;
+                        if (32u - sh < take) x |= src[i + 1] >> (32u - sh);
+                    }
+                    x &= take >= 32u ? 0xffffffffu : ~(0xffffffffu >> take);
+                    acc |= x >> filled;
+                    filled += take;
+                }
+                wv[k] = __builtin_bswap32(acc);         /* RBSP bytes in memory order */
+            }
         }
-        int lnz = -1;                                   /* bytes >= nin: not scanned */
+        if (ib < nin) {
+            *reinterpret_cast<uint4 *>(out + ib) = make_uint4(wv[0], wv[1], wv[2], wv[3]);
+            *reinterpret_cast<uint4 *>(out + ib + 16) = make_uint4(wv[4], wv[5], wv[6], wv[7]);
+        }
+        /* emulation prevention of these bytes (nal.c:33-38, closed form) */
+        int lnz = -1;
 #pragma unroll
         for (int w = 0; w < 8; ++w) {
             const uint32_t m = ib + 4u * w < nin ? wv[w] : 0u;
             if (m) lnz = (int)(ib + 4u * w) + 3 - (__builtin_clz(m) >> 3);
         }
         int ex, tot;
-        block_excl_max<EP_NW>(lnz, wmax, ex, tot);     /* its barriers also publish `back` */
-        int prev = max(back, ex);
+        block_excl_max<ST_NW>(lnz, wmax, ex, tot);
+        int prev = max(carry, ex);
+        carry = max(carry, tot);
         uint32_t ins = 0;
 #pragma unroll
         for (int i = 0; i < 32; ++i) {
-            const uint32_t gi = ib + (uint32_t)i;
-            const uint32_t b = gi < nin ? (wv[i >> 2] >> (8 * (i & 3))) & 255u : 256u;   /* past the end: never inserts */
-            ins |= (ep_insert(b, (int)gi - 1 - prev) ? 1u : 0u) << i;
-            prev = b ? (int)gi : prev;
+            const uint32_t gi2 = ib + (uint32_t)i;
+            const uint32_t b = gi2 < nin ? (wv[i >> 2] >> (8 * (i & 3))) & 255u : 256u;   /* past the end: never */
+            ins |= (ep_insert(b, (int)gi2 - 1 - prev) ? 1u : 0u) << i;
+            prev = b ? (int)gi2 : prev;
         }
-        const uint32_t cnt = (uint32_t)__builtin_popcount(ins);
-        const uint32_t incl = wave_incl_sum(cnt, lane);
-        const uint32_t wtot = __shfl(incl, 63, 64);
-        uint32_t base = 0;
-        if (wtot) {
-            if (lane == 0) base = atomicAdd(&DF->ep, wtot);
-            base = __shfl(base, 0, 64);
+        if (ins) {
+            uint32_t k = atomicAdd(&ep_n, (uint32_t)__builtin_popcount(ins));
+            while (ins) {
+                const int i = __builtin_ctz(ins);
+                ins &= ins - 1u;
+                if (k < (uint32_t)EPLIST_MAX) eplist[k] = ib + (uint32_t)i;   /* RBSP index the 03 precedes */
+                k++;
+            }
         }
-        uint32_t k = base + incl - cnt;
-        while (ins) {
-            const int i = __builtin_ctz(ins);
-            ins &= ins - 1u;
-            if (k < (uint32_t)EPLIST_MAX) eplist[k] = ib + (uint32_t)i;   /* RBSP index the 03 precedes */
-            k++;
-        }
-        __syncthreads();                                /* `back` is rewritten by the next chunk */
+    }
+    __syncthreads();
+    if (t == 0) {
+        DF->err = 0;                                    /* clears DF_GENERAL */
+        DF->rbsp_bytes = nin;
+        DF->ep = ep_n;
     }
 }
 
@@ -1587,36 +1809,35 @@ __global__ __launch_bounds__(256) void k_dyn_synth(uint8_t *__restrict__ src, Dy
 /* ---------------------------------------------------------------------- */
 /* launchers (engine-internal, engine.h)                                   */
 /* ---------------------------------------------------------------------- */
-int dyn_launch_code(hipStream_t hs, int nframes, int S, const DevStream *st, const NalDesc *nal,
+int dyn_launch_code(hipStream_t hs, int nframes, int S, DevStream *st, const NalDesc *nal,
                     int ld_nal, const PlanPending *pend, DynFrame *dfr, int ld_fr,
-                    const DynGeom *g, const uint8_t *src, const uint8_t *refs, const DynScratch *x)
+                    const DynGeom *g, const uint8_t *src, const uint8_t *refs, const DynScratch *x,
+                    uint32_t epoch, int mbw, uint64_t *stamps)
 {
     if (nframes <= 0 || S <= 0) return 0;
     hipLaunchKernelGGL(k_dyn_rows, dim3(nframes, S), dim3(256), 0, hs, st, nal, ld_nal, pend, dfr, ld_fr,
                        *g, x->rows);
     if (hipGetLastError() != hipSuccess) return -1;
     const int nchunk = (24 * g->w * g->h + CODE_T - 1) / CODE_T;
-    hipLaunchKernelGGL(k_dyn_code, dim3(nchunk, nframes, S), dim3(CODE_T), 0, hs, st, dfr, ld_fr,
-                       pend, nal, ld_nal, *g, x->rows, src, refs, x->meta, x->body_lo, x->body_hi);
-    if (hipGetLastError() != hipSuccess) return -1;
     hipLaunchKernelGGL(k_dyn_code_general, dim3(nchunk, CODE_GEN_Y), dim3(CODE_T), 0, hs, st, dfr, ld_fr,
                        pend, nal, ld_nal, *g, x->rows, src, refs, x->meta, x->body_lo, x->body_hi, nframes, S);
+    if (hipGetLastError() != hipSuccess) return -1;
+    hipLaunchKernelGGL(k_dyn_row, dim3(g->h, nframes, S), dim3(row_threads(g->w)), row_lds_bytes(g->w, mbw), hs,
+                       st, nal, ld_nal, pend, dfr, ld_fr, *g, x->rows, src, refs, x->meta, x->body_lo,
+                       x->body_hi, x->tcx, epoch, x->rowstage, x->gbits, stamps);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 int dyn_launch_pack(hipStream_t hs, int nframes, int S, DevStream *st, const NalDesc *nal,
                     int ld_nal, const PlanPending *pend, DynFrame *dfr, int ld_fr,
-                    const DynGeom *g, const DynScratch *x, uint8_t *stage, uint32_t epoch,
-                    uint64_t *stamps, int mbw, int mbh)
+                    const DynGeom *g, const DynScratch *x, uint8_t *stage)
 {
     if (nframes <= 0 || S <= 0) return 0;
-    const int ng = g->ngroups;
-    const int lines = mbw > mbh ? mbw : mbh;
-    hipLaunchKernelGGL(k_dyn_group, dim3(ng, nframes, S), dim3(GW), group_lds_bytes(g->w, lines), hs, st, nal,
-                       ld_nal, pend, dfr, ld_fr, *g, x->meta, x->body_lo, x->body_hi, x->status, x->tails, epoch, lines,
-                       stage, stamps);
+    hipLaunchKernelGGL(k_dyn_static, dim3(g->ngroups - g->h, nframes, S), dim3(GW), 0, hs, st, nal, ld_nal,
+                       pend, dfr, ld_fr, *g, x->rowstage, x->gbits);
     if (hipGetLastError() != hipSuccess) return -1;
-    hipLaunchKernelGGL(k_dyn_ep, dim3(EP_G, nframes, S), dim3(EP_T), 0, hs, dfr, ld_fr, *g, stage);
+    hipLaunchKernelGGL(k_dyn_stitch, dim3(nframes, S), dim3(ST_T), 0, hs, st, dfr, ld_fr, *g, x->rowstage,
+                       x->gbits, stage);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -1643,10 +1864,22 @@ int dyn_launch_synth(hipStream_t hs, int nframes, int S, uint8_t *src, const Dyn
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
+void dyn_rowstage_geom(DynGeom *g, int mbw, int mbh)
+{
+    const int SR = DYN_STATIC_ROWS;
+    const int above = g->y0 < SR ? g->y0 : SR, below0 = mbh - g->y0 - g->h;
+    const int below = below0 < SR ? below0 : SR;
+    const int maxrows = above > below ? above : below;
+    auto words = [](uint64_t bits) { return (uint32_t)((((bits + 31) / 32) + 63) & ~(uint64_t)63); };
+    g->rs_static_words = words((uint64_t)HDR_MAX + (uint64_t)maxrows * mbw * (HEAD_MAX + 1) + 64);
+    g->rs_row_words = words((uint64_t)mbw * (HEAD_MAX + 1) + (uint64_t)g->w * MB_BITS_MAX + 64);
+    g->rs_frame_words = (uint64_t)(g->ngroups - g->h) * g->rs_static_words + (uint64_t)g->h * g->rs_row_words;
+}
+
 size_t dyn_slot_bound(int mbw, int mbh, int rw, int rh)
 {
     /* header + every MB head (+ cbp) + every dynamic MB at its provable
-     * maximum + the stop word + a 16-byte read margin (k_dyn_ep) */
+     * maximum + the stop word + k_dyn_stitch's 32-byte steps */
     const size_t bits = (size_t)HDR_MAX + (size_t)mbw * mbh * (HEAD_MAX + 1) +
                         (size_t)rw * rh * MB_BITS_MAX + 64;
     return ((bits / 8 + 32 + DYN_OVF_BYTES) + 255) & ~(size_t)255;

@@ -95,6 +95,9 @@ typedef struct {
     uint64_t src_ld, src_fr;        /* source bytes per stream / per frame        */
     uint64_t ref_ld;                /* reference-pair bytes per stream (0 shared) */
     uint64_t slot_bytes;            /* staging bytes per frame                    */
+    uint32_t rs_static_words;       /* row-stage words per static row group       */
+    uint32_t rs_row_words;          /* row-stage words per rect row               */
+    uint64_t rs_frame_words;        /* row-stage words per frame (all row groups) */
 } DynGeom;
 
 /* hints of one composed frame: rects [first, first + n) of the batch's rect

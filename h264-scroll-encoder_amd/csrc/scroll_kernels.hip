@@ -1274,8 +1274,9 @@ static int launch(ScrollBatch *b, int nframes, int plan_mode, int nal_max, hipSt
                 xc.meta = b->dx.meta + nb0 * DYN_PIECES * nalw;
                 xc.body_lo = b->dx.body_lo + nb0 * DYN_PIECES * nalw;
                 xc.body_hi = b->dx.body_hi + nb0 * DYN_PIECES * nalw;
-                xc.status = b->dx.status + nb0 * ng;
-                xc.tails = b->dx.tails + nb0 * ng;
+                xc.tcx = b->dx.tcx + nb0 * nalw;
+                xc.rowstage = b->dx.rowstage + nb0 * G.rs_frame_words;
+                xc.gbits = b->dx.gbits + nb0 * ng;
                 DevStream *st0 = b->d_st + s0;
                 NalDesc *nal0 = b->d_nal + (size_t)s0 * b->ld_nal;
                 PlanPending *pend0 = b->d_pend + s0;
@@ -1284,7 +1285,7 @@ static int launch(ScrollBatch *b, int nframes, int plan_mode, int nal_max, hipSt
                 const uint8_t *refs0 = b->d_refs + (size_t)s0 * G.ref_ld;
                 uint8_t *stage0 = b->d_stage + nb0 * G.slot_bytes;
                 if (dyn_launch_code(hs, nframes, s1 - s0, st0, nal0, b->ld_nal, pend0, dfr0, ld_fr, &G, src0,
-                                    refs0, &xc)) {
+                                    refs0, &xc, b->dx.epoch, b->dyn_pw / 16, stamps)) {
                     set_err("k_dyn_code launch: %s", hipGetErrorString(hipGetLastError()));
                     return SCROLL_ERR_HIP;
                 }
@@ -1297,8 +1298,8 @@ static int launch(ScrollBatch *b, int nframes, int plan_mode, int nal_max, hipSt
                     return rc;
                 }
                 if (dyn_launch_pack(hp, nframes, s1 - s0, st0, nal0, b->ld_nal, pend0, dfr0, ld_fr, &G, &xc,
-                                    stage0, b->dx.epoch, stamps, b->dyn_pw / 16, b->dyn_ph / 16)) {
-                    set_err("k_dyn_group launch: %s", hipGetErrorString(hipGetLastError()));
+                                    stage0)) {
+                    set_err("k_dyn_static / k_dyn_stitch launch: %s", hipGetErrorString(hipGetLastError()));
                     return SCROLL_ERR_HIP;
                 }
             }
@@ -1557,8 +1558,9 @@ static void dyn_release(ScrollBatch *b)
     (void)hipFree(b->dx.meta);
     (void)hipFree(b->dx.body_lo);
     (void)hipFree(b->dx.body_hi);
-    (void)hipFree(b->dx.status);
-    (void)hipFree(b->dx.tails);
+    (void)hipFree(b->dx.tcx);
+    (void)hipFree(b->dx.rowstage);
+    (void)hipFree(b->dx.gbits);
     b->d_dfr = nullptr;
     b->d_src = b->d_refs = b->d_stage = nullptr;
     b->dx = DynScratch{};
@@ -1619,6 +1621,7 @@ int scroll_batch_set_dyn_rect(ScrollBatch *b, int x0, int y0, int w, int h, size
     g.src_ld = round256((size_t)b->max_frames * g.src_fr);
     g.ref_ld = 0;
     g.slot_bytes = slot_bytes ? round256(slot_bytes + DYN_OVF_BYTES) : dyn_slot_bound(mbw, mbh, w, h);
+    dyn_rowstage_geom(&g, mbw, mbh);
     b->dyn_pw = pw;
     b->dyn_ph = ph;
     const size_t S = (size_t)b->max_streams, F = (size_t)b->max_frames;
@@ -1631,10 +1634,10 @@ int scroll_batch_set_dyn_rect(ScrollBatch *b, int x0, int y0, int w, int h, size
     if (e == hipSuccess) e = hipMalloc(&b->dx.body_lo, S * F * DYN_PIECES * w * h * sizeof(uint2));
     if (e == hipSuccess) e = hipMalloc(&b->dx.body_hi, S * F * DYN_PIECES * w * h * sizeof(uint2));
     const size_t ng = (size_t)g.ngroups;
-    if (e == hipSuccess) e = hipMalloc(&b->dx.status, S * F * ng * sizeof(unsigned long long));
-    if (e == hipSuccess) e = hipMalloc(&b->dx.tails, S * F * ng * sizeof(unsigned long long));
-    if (e == hipSuccess) e = hipMemset(b->dx.tails, 0, S * F * ng * sizeof(unsigned long long));
-    if (e == hipSuccess) e = hipMemset(b->dx.status, 0, S * F * ng * sizeof(unsigned long long));
+    if (e == hipSuccess) e = hipMalloc(&b->dx.tcx, S * F * w * h * sizeof(unsigned long long));
+    if (e == hipSuccess) e = hipMemset(b->dx.tcx, 0, S * F * w * h * sizeof(unsigned long long));
+    if (e == hipSuccess) e = hipMalloc(&b->dx.rowstage, S * F * g.rs_frame_words * sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMalloc(&b->dx.gbits, S * F * ng * sizeof(uint32_t));
     b->dx.epoch = 0;
     if (e == hipSuccess) e = hipMemset(b->d_dfr, 0, S * F * sizeof(DynFrame));
     if (e == hipSuccess) e = hipMemset(b->d_src, 0, S * g.src_ld);

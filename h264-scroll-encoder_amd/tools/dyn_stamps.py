@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""dyn_stamps.py -- profiling aid: where k_dyn_group's time goes.
+"""dyn_stamps.py -- profiling aid: where k_dyn_row's / k_dyn_group's time goes.
 
 Runs the bench's config-3 workload (bench.py p720dyn) once with
 SCROLL_DEBUG_DYN_STAMPS and prints, per row-group workgroup of k_dyn_group
@@ -72,11 +72,15 @@ def main():
     got = hs.lib.scroll_batch_debug_stamps(b.h, buf, nslot)
     allst = np.frombuffer(buf, dtype=np.uint64).reshape(-1, 8)[:got]
     grp = allst[2 * S * F:].astype(np.int64).reshape(S * F, ng, 8)
-    names = ["load+tok", "mb", "scan", "lookback", "write"]
-    for label, sel in (("rect rows", slice(na, na + rect[3])), ("static above", slice(0, na)),
+    gnames = ["load+tok", "mb", "scan", "lookback", "write"]
+    rnames = ["levels", "cavlc+poll", "tokens", "mb+scan+lb", "write"]     # k_dyn_row
+    for label, sel in (("rect rows (k_dyn_row)", slice(na, na + rect[3])), ("static above", slice(0, na)),
                        ("static below", slice(na + rect[3], ng))):
+        names = rnames if label.startswith("rect") else gnames
         gsel = grp[:, sel].reshape(-1, 8)
         gsel = gsel[gsel[:, 5] > 0]
+        if not len(gsel):                          # k_dyn_static records no stamps
+            continue
         st = gsel[:, :6].astype(np.float64)
         tot = (st[:, 5] - st[:, 0]) / 100.0
         print(f"{label}: {len(gsel)} WGs, duration mean {tot.mean():.2f} us p50 {np.percentile(tot, 50):.2f} "
@@ -88,12 +92,14 @@ def main():
             d = (cur - prev) / 100.0
             print(f"  {nm:9s} mean {d.mean():7.2f} us  p99 {np.percentile(d, 99):7.2f}")
             prev = cur
-    g0 = grp[:, :, 0][grp[:, :, 5] > 0]
-    t0, t1 = g0.min(), grp[:, :, 5].max()
-    print(f"k_dyn_group span {(t1 - t0) / 100.0:.1f} us")
-    ends = grp[:, :, 5][grp[:, :, 5] > 0]
-    conc = [int(np.sum((g0 <= x) & (ends > x))) for x in np.linspace(t0, t1, 12)]
-    print("  resident WGs over time:", conc)
+    for label, sel in (("k_dyn_row", slice(na, na + rect[3])),):
+        gg = grp[:, sel]
+        g0 = gg[:, :, 0][gg[:, :, 5] > 0]
+        t0, t1 = g0.min(), gg[:, :, 5].max()
+        print(f"{label} span {(t1 - t0) / 100.0:.1f} us")
+        ends = gg[:, :, 5][gg[:, :, 5] > 0]
+        conc = [int(np.sum((g0 <= x) & (ends > x))) for x in np.linspace(t0, t1, 12)]
+        print("  resident WGs over time:", conc)
     e = allst[S * F:2 * S * F].astype(np.int64)  # k_dyn_emit_gather: realtime (100 MHz)
     e = e[e[:, 0] > 0]
     if len(e):

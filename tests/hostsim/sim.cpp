@@ -285,35 +285,53 @@ int sim_ep_count(const uint8_t *b, int n)
     return c;
 }
 
-/* the kernels' split form: coeff_token (phase B) + cavlc_rest (phase A,
- * register levels); must equal cavlc_block bit for bit */
+/* the kernels' split form: cavlc_body (k_dyn_row's block phase: packed
+ * int8 levels -> the nC-independent bits) + coeff_token (its token phase),
+ * or cavlc_dc4 for chroma DC; must equal cavlc_block bit for bit.  Blocks
+ * with levels outside int8 (the kernels' levels stay within +-78) or over
+ * 128 body bits take cavlc_block, as the kernels' overflow path does. */
 long sim_cavlc_split(const int *coef, int max, int nC, int start, uint32_t *words, int *tc_out)
 {
+    static dyn::PTabs P;
+    static bool init = false;
+    if (!init) {
+        dyn::build_ptabs(g_dyn_tabs, P, 0, 1);
+        init = true;
+    }
+    dyn::OrSink<HostOr> os{{words}, 0, 0, 0};
+    os.start((uint32_t)start);
+    if (max == 4) {
+        dyn::CapSink cap{0, 0, 0};
+        const int c[4] = {coef[0], coef[1], coef[2], coef[3]};
+        *tc_out = dyn::cavlc_dc4(cap, P, c);
+        os.put_cap(cap);
+        os.finish();
+        return (long)cap.n;
+    }
+    bool fits = true;
+    uint32_t pw[4] = {0, 0, 0, 0};
+    for (int i = 0; i < max; ++i) {
+        fits = fits && coef[i] >= -128 && coef[i] <= 127;
+        pw[i >> 2] |= ((uint32_t)coef[i] & 255u) << (8 * (i & 3));
+    }
     dyn::CapSink cap{0, 0, 0};
     int t1 = 0, tc = 0;
-    int c[16];
-    for (int i = 0; i < 16; ++i) c[i] = i < max ? coef[i] : 0;
-    if (max == 16) tc = dyn::cavlc_rest<16>(cap, g_dyn_tabs, c, t1);
-    else if (max == 15) tc = dyn::cavlc_rest<15>(cap, g_dyn_tabs, c, t1);
-    else tc = dyn::cavlc_rest<4>(cap, g_dyn_tabs, c, t1);
+    bool ok = false;
+    if (fits) tc = dyn::cavlc_body(cap, P, make_uint4(pw[0], pw[1], pw[2], pw[3]), max, t1, ok);
+    if (!ok) {                                        /* the overflow path: from the levels */
+        *tc_out = dyn::cavlc_block(os, g_dyn_tabs, coef, max, nC);
+        const uint32_t end = os.wi * 32u + (uint32_t)os.fill;
+        os.finish();
+        return (long)(end - (uint32_t)start);
+    }
     uint32_t tv;
     int tl;
     dyn::coeff_token(g_dyn_tabs, tc, t1, nC, tv, tl);
-    dyn::OrSink<HostOr> os{{words}, 0, 0, 0};
-    os.start((uint32_t)start);
     os.put(tv, tl);
-    if (cap.over()) {
-        if (max == 16) dyn::cavlc_rest<16>(os, g_dyn_tabs, c, t1);
-        else if (max == 15) dyn::cavlc_rest<15>(os, g_dyn_tabs, c, t1);
-        else dyn::cavlc_rest<4>(os, g_dyn_tabs, c, t1);
-    } else {
-        os.put_cap(cap);
-    }
-    const uint32_t end = os.wi * 32u + (uint32_t)os.fill;
+    os.put_cap(cap);
     os.finish();
     *tc_out = tc;
-    if (end - (uint32_t)start != (uint32_t)tl + cap.n) return -1;
-    return (long)(end - (uint32_t)start);
+    return (long)tl + (long)cap.n;
 }
 
 /* the compile-time packed tables the kernels copy (make_ptabs) equal the

@@ -191,8 +191,9 @@ def test_composer_dropin_end_to_end(gpu, tmp_path):
         lib.composer_write_scroll_frame(ctypes.byref(c), p if p < 48 else 96 - p)
     out = tmp_path / "o.h264"
     assert lib.composer_write_to_file(ctypes.byref(c), str(out).encode()) == 0
-    assert out.read_bytes() == golden_file("composer_64x48_n40_s1.h264")
-    assert c.frames_written == 40
+    got, want = out.read_bytes(), golden_file("composer_64x48_n40_s1.h264")
+    assert c.frames_written == 40, (c.frames_written, len(got), len(want), gpu.last_error())
+    assert got == want, (len(got), len(want), gpu.last_error())
     lib.composer_finish(ctypes.byref(c))
 
 

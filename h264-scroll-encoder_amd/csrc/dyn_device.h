@@ -301,6 +301,19 @@ __device__ __host__ inline void fwd4x4(const int x[16], int W[16])
 /* zig-zag scan (Table 8-13, frame): scan index -> raster position */
 constexpr int ZZ[16] = {0, 1, 4, 8, 5, 2, 3, 6, 9, 12, 13, 10, 7, 11, 14, 15};
 
+/* a * b + c with a, b taken as signed 24-bit: one v_mad_i32_i24 (left to
+ * itself the compiler picks a quarter-rate v_mad_u64_u32 here) */
+__device__ __host__ inline int mad_i24(int a, int b, int c)
+{
+#ifdef __HIP_DEVICE_COMPILE__
+    int r;
+    asm("v_mad_i32_i24 %0, %1, %2, %3" : "=v"(r) : "v"(a), "s"(b), "v"(c));
+    return r;
+#else
+    return __mul24(a, b) + c;
+#endif
+}
+
 /* raster position pos of a 4x4 block.  sign(w) ((|w| mf + f) >> qbits) as
  * one signed 24-bit multiply-add and an arithmetic shift: for w < 0 the
  * bias 2^qbits - 1 - f turns the floor into -((|w| mf + f) >> qbits)
@@ -309,15 +322,15 @@ __device__ __host__ inline int quant(int w, int pos)
 {
     const int i = pos >> 2, j = pos & 3;
     const int mf = ((i | j) & 1) == 0 ? MF0 : (((i & j) & 1) ? MF1 : MF2);
-    const int bias = QF + ((w >> 31) & ((1 << QBITS) - 1 - 2 * QF));
-    return (__mul24(w, mf) + bias) >> QBITS;
+    const int bias = w < 0 ? (1 << QBITS) - 1 - QF : QF;
+    return mad_i24(w, mf, bias) >> QBITS;
 }
 
 /* chroma DC (2x2): qbits + 1, f doubled (|w| <= 16320) */
 __device__ __host__ inline int quant_dc(int w)
 {
-    const int bias = 2 * QF + ((w >> 31) & ((1 << (QBITS + 1)) - 1 - 4 * QF));
-    return (__mul24(w, MF0) + bias) >> (QBITS + 1);
+    const int bias = w < 0 ? (1 << (QBITS + 1)) - 1 - 2 * QF : 2 * QF;
+    return mad_i24(w, MF0, bias) >> (QBITS + 1);
 }
 
 /* ---------------------------------------------------------------------- */

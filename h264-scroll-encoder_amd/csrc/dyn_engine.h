@@ -31,7 +31,7 @@ int dyn_launch_code(hipStream_t hs, int nframes, int S, DevStream *st, const Nal
 /* k_dyn_static (static row groups) + k_dyn_stitch: staged RBSP + EP positions */
 int dyn_launch_pack(hipStream_t hs, int nframes, int S, DevStream *st, const NalDesc *nal,
                     int ld_nal, const PlanPending *pend, DynFrame *dfr, int ld_fr,
-                    const DynGeom *g, const DynScratch *x, uint8_t *stage);
+                    const DynGeom *g, const DynScratch *x, uint8_t *stage, uint64_t *stamps);
 int dyn_launch_emit(hipStream_t hs, int nframes, int S, const DevStream *st, const NalDesc *nal,
                     int ld_nal, const DynFrame *dfr, int ld_fr, const DynGeom *g,
                     const uint8_t *stage, uint8_t *arena, uint64_t ld_arena, uint64_t *stamps);

@@ -877,34 +877,51 @@ struct BlkPix {
     uint32_t fr;
 };
 
-__device__ inline void row_fetch(int task, int w, int ry, const DynGeom &g, const uint8_t *fs, const uint8_t *rb,
-                                 const uint32_t *rt, uint32_t csz, BlkPix &px)
+/* raw buffer descriptor over n bytes at p (gfx9 dword3: 32-bit data format) */
+__device__ inline __amdgpu_buffer_rsrc_t buf_rsrc(const void *p, uint32_t n)
+{
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), (short)0, (int)n, 0x00020000);
+}
+
+/* fs: the frame's source bytes, rb: the stream's reference pair, both as
+ * buffer descriptors -- 32-bit lane offsets, the row step in the uniform
+ * soffset, so a pixel row costs one load and at most one add */
+__device__ inline void row_fetch(int task, int w, int ry, const DynGeom &g, __amdgpu_buffer_rsrc_t fs,
+                                 __amdgpu_buffer_rsrc_t rb, const uint32_t *rt, uint32_t csz, BlkPix &px)
 {
     const int lstride = 16 * g.w, cstride = 8 * g.w, ndt = g.w * g.h;
     px.fr = 0;
+#ifdef SCROLL_ABL_NOFETCH
+    for (int i = 0; i < 4; ++i) {
+        px.a[i] = 0x80808080u + (uint32_t)(task * 7 + i * 3) * 0x01010101u;
+        px.b[i] = 0x80808080u + rt[i];
+        px.c[i] = rt[i + 4];
+    }
+    px.fr = task & 7;
+    return;
+#endif
     if (task < 16 * w) {
         const int k = task >> 4, r = task & 15, bx = r & 3, by = r >> 2;
-        const uint8_t *sp = fs + (size_t)(16 * ry + 4 * by) * lstride + 16 * k + 4 * bx;
-        const uint8_t *pp = rb + 16 * (g.x0 + k) + 4 * bx;
+        const uint32_t so = (uint32_t)((16 * ry + 4 * by) * lstride + 16 * k + 4 * bx);
+        const uint32_t po = (uint32_t)(16 * (g.x0 + k) + 4 * bx);
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            px.a[i] = ld32(sp + (size_t)i * lstride);
-            px.b[i] = ld32(pp + rt[4 * by + i]);
+            px.a[i] = __builtin_amdgcn_raw_buffer_load_b32(fs, so, i * lstride, 0);
+            px.b[i] = __builtin_amdgcn_raw_buffer_load_b32(rb, po + rt[4 * by + i], 0, 0);
             px.c[i] = 0;
         }
     } else {
         const int jj = task - 16 * w, k = jj >> 3, p = (jj >> 2) & 1, r = jj & 3;
         const int bx = r & 1, by = r >> 1;
-        const uint8_t *fc = fs + (size_t)256 * ndt + (size_t)(p ? 64 * ndt : 0);
-        const uint8_t *sp = fc + (size_t)(8 * ry + 4 * by) * cstride + 8 * k + 4 * bx;
-        const uint8_t *cp = rb + (size_t)p * csz + 8 * (g.x0 + k) + 4 * bx;
+        const uint32_t so = (uint32_t)(256 * ndt + (p ? 64 * ndt : 0) + (8 * ry + 4 * by) * cstride + 8 * k + 4 * bx);
+        const uint32_t co = (uint32_t)p * csz + (uint32_t)(8 * (g.x0 + k) + 4 * bx);
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const uint32_t ea = rt[16 + 4 * by + i];
             const uint32_t f = (ea >> 28) & 7u;
-            px.a[i] = ld32(sp + (size_t)i * cstride);
-            px.b[i] = ld32(cp + (ea & ROW_OFF));
-            px.c[i] = f ? ld32(cp + (rt[24 + 4 * by + i] & ROW_OFF)) : 0u;
+            px.a[i] = __builtin_amdgcn_raw_buffer_load_b32(fs, so, i * cstride, 0);
+            px.b[i] = __builtin_amdgcn_raw_buffer_load_b32(rb, co + (ea & ROW_OFF), 0, 0);
+            px.c[i] = f ? __builtin_amdgcn_raw_buffer_load_b32(rb, co + (rt[24 + 4 * by + i] & ROW_OFF), 0, 0) : 0u;
             px.fr |= f << (3 * i);
         }
     }
@@ -1009,8 +1026,9 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
     const int np = (ntask + T - 1) / T;                 /* tasks per thread, <= ROW_NPMAX */
     __syncthreads();                                    /* the row table (rt) */
     if (!general) {
-        const uint8_t *fs = src + (size_t)s * g.src_ld + (size_t)f * g.src_fr;
-        const uint8_t *rb = refs + (size_t)s * g.ref_ld;
+        const __amdgpu_buffer_rsrc_t fs = buf_rsrc(src + (size_t)s * g.src_ld + (size_t)f * g.src_fr,
+                                                   (uint32_t)g.src_fr);
+        const __amdgpu_buffer_rsrc_t rb = buf_rsrc(refs + (size_t)s * g.ref_ld, 3u * ysz);
         int keys[ROW_NPMAX];
 #pragma unroll
         for (int pa = 0; pa < ROW_NPMAX; ++pa) keys[pa] = SORT_KEYS - 1;
@@ -1358,25 +1376,100 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
 /* k_dyn_stitch: row groups -> the NAL's staged RBSP + EP positions         */
 /* ---------------------------------------------------------------------- */
 /* One workgroup per dynamic NAL: the row groups' bit counts -> their
- * offsets (one wave scan; ngroups <= 64), then every staged word is
- * assembled from the (one, at group seams two or more) row-stage words it
- * spans -- a funnel shift -- and stored, 32 bytes per thread and step; the
- * same step scans those bytes for emulation prevention (closed-form rule,
- * the zero run carried from the step before by a block max-scan) and
- * records the EP positions in the slot tail.  Sets rbsp_bytes / ep / err. */
-constexpr int ST_T = 256, ST_NW = ST_T / 64, ST_CHUNK = ST_T * 32;
+ * offsets (one wave scan; ngroups <= 64), then per chunk of ST_CHUNK bytes
+ * every staged word is assembled from the (one, at group seams two or more)
+ * row-stage words it spans -- a funnel shift -- and stored; the chunk's
+ * bytes are scanned for emulation prevention (closed-form rule, the zero
+ * run carried from chunk to chunk).  Word w of a chunk is thread w % 256's,
+ * so neighbouring lanes read neighbouring row-stage words, and the loads of
+ * the next chunk are in flight while this one is scanned.  EP positions go
+ * to the slot tail; sets rbsp_bytes / ep / err. */
+constexpr int ST_T = 256, ST_NW = ST_T / 64, ST_CHUNK = ST_T * 32, ST_KW = ST_CHUNK / 4 / ST_T;
 static_assert(DYN_MAX_H + 2 * ((DYN_MAX_MBH + DYN_STATIC_ROWS - 1) / DYN_STATIC_ROWS) <= 64,
               "k_dyn_stitch scans the row groups with one wave");
 
+/* the RBSP word (MSB first) at bit P (a multiple of 32) of a NAL whose row
+ * groups have offsets goff, bit counts gb and row-stage words at fr + gw;
+ * gg: the group holding P or before it, advanced */
+__device__ inline uint32_t stitch_word(uint32_t P, int &gg, int ng, uint32_t T, const uint32_t *goff,
+                                       const uint32_t *gb, const uint32_t *gw, const uint32_t *fr)
+{
+    uint32_t acc = 0, filled = 0;
+    while (filled < 32u && gg < ng && P + filled < T) {
+        const uint32_t lp = P + filled - goff[gg];
+        if (lp >= gb[gg]) {                             /* group done (or empty) */
+            ++gg;
+            continue;
+        }
+        const uint32_t take = min(32u - filled, gb[gg] - lp);
+        const uint32_t *src = fr + gw[gg];
+        const uint32_t i = lp >> 5, sh = lp & 31u;
+        uint32_t x = src[i];
+        if (sh) {
+            x <<= sh;
+            if (32u - sh < take) x |= src[i + 1] >> (32u - sh);
+        }
+        x &= take >= 32u ? 0xffffffffu : ~(0xffffffffu >> take);
+        acc |= x >> filled;
+        filled += take;
+    }
+    return acc;
+}
+
+/* last group with goff[g] <= P */
+__device__ inline int stitch_group(uint32_t P, int ng, const uint32_t *goff)
+{
+    int lo = 0, hi = ng;
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (goff[mid] <= P) lo = mid;
+        else hi = mid;
+    }
+    return lo;
+}
+
+/* the first source words of the ST_KW words thread t assembles for the
+ * chunk at byte c0 (x1: the next word, where the shift needs it) */
+struct StitchLoads {
+    uint32_t x0[ST_KW], x1[ST_KW], y[ST_KW];           /* y: the next group's first word (seam words) */
+    int g[ST_KW];
+};
+
+__device__ inline void stitch_load(StitchLoads &L, uint32_t c0, int t, int ng, uint32_t T, const uint32_t *goff,
+                                   const uint32_t *gb, const uint32_t *gw, const uint32_t *fr)
+{
+    const uint32_t P0 = c0 * 8u + 32u * (uint32_t)t;
+    int gg = stitch_group(P0, ng, goff);
+#pragma unroll
+    for (int k = 0; k < ST_KW; ++k) {
+        const uint32_t P = P0 + 32u * ST_T * (uint32_t)k;
+        while (gg + 1 < ng && goff[gg + 1] <= P) ++gg;
+        L.g[k] = gg;
+        const uint32_t lp = P - goff[gg], i = lp >> 5;
+        const uint32_t *src = fr + gw[gg];
+        L.x0[k] = P < T && lp < gb[gg] ? src[i] : 0u;
+        L.x1[k] = P < T && (lp & 31u) && 32u * (i + 1) < gb[gg] ? src[i + 1] : 0u;
+        const bool seam = P < T && gb[gg] - lp < 32u && gg + 1 < ng;
+        L.y[k] = seam ? fr[gw[gg + 1]] : 0u;
+    }
+}
+
+/* grid (frames, streams) */
 __global__ __launch_bounds__(ST_T) void k_dyn_stitch(DevStream *__restrict__ st, DynFrame *__restrict__ dfr,
                                                      int ld_fr, DynGeom g, const uint32_t *__restrict__ rowstage,
                                                      const uint32_t *__restrict__ gbits,
-                                                     uint8_t *__restrict__ stage)
+                                                     uint8_t *__restrict__ stage, uint64_t *__restrict__ stamps)
 {
     __shared__ uint32_t goff[65], gb[64], gw[64];
     __shared__ int32_t wmax[ST_NW];
     __shared__ uint32_t ep_n;
-    const int s = blockIdx.y, f = blockIdx.x, t = threadIdx.x, lane = t & 63;
+    /* debug: realtime at entry, after the group scan, after the first
+     * chunk's assembly and EP scan, at exit; chunks; HW_ID */
+    uint64_t *stp = stamps && threadIdx.x == 0 ? stamps + ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * 8 : nullptr;
+    if (stp) stp[0] = __builtin_amdgcn_s_memrealtime();
+    __shared__ uint4 cbuf4[ST_CHUNK / 16];              /* the chunk's bytes */
+    uint32_t *cbuf = reinterpret_cast<uint32_t *>(cbuf4);
+    const int f = blockIdx.x, s = blockIdx.y, t = threadIdx.x, lane = t & 63;
     const size_t nb = (size_t)s * ld_fr + f;
     DynFrame *DF = dfr + nb;
     if (DF->nal < 0) return;
@@ -1397,6 +1490,7 @@ __global__ __launch_bounds__(ST_T) void k_dyn_stitch(DevStream *__restrict__ st,
     __syncthreads();
     const uint32_t T = goff[ng];                        /* NAL RBSP bits incl. the stop bit */
     const uint32_t nin = (T + 7) >> 3;                  /* bitwriter.c:103-111 */
+    if (stp) stp[1] = __builtin_amdgcn_s_memrealtime();
     /* whole 32-byte steps must fit before the slot tail (EP positions, levels) */
     const bool over = ((nin + 31u) & ~31u) > g.slot_bytes - DYN_OVF_BYTES;
     if (over) {
@@ -1411,52 +1505,53 @@ __global__ __launch_bounds__(ST_T) void k_dyn_stitch(DevStream *__restrict__ st,
     uint8_t *out = stage + nb * g.slot_bytes;
     uint32_t *eplist = reinterpret_cast<uint32_t *>(out + g.slot_bytes - DYN_OVF_BYTES);
     const uint32_t *fr = rowstage + nb * g.rs_frame_words;
-    int carry = -1;                                     /* last non-zero RBSP byte before the step */
+    const uint32_t Pend = 8u * ((nin + 31u) & ~31u);
+    int carry = -1;                                     /* last non-zero RBSP byte before the chunk */
+    StitchLoads ld;
+    stitch_load(ld, 0, t, ng, T, goff, gb, gw, fr);
     for (uint32_t c0 = 0; c0 < nin; c0 += ST_CHUNK) {
-        const uint32_t ib = c0 + 32u * (uint32_t)t;    /* this thread's first byte */
+        /* assemble this chunk's words (loaded), stage them, then start the
+         * next chunk's loads */
+        {
+            const uint32_t P0 = c0 * 8u + 32u * (uint32_t)t;
+            uint32_t *o32 = reinterpret_cast<uint32_t *>(out + c0);
+#pragma unroll
+            for (int k = 0; k < ST_KW; ++k) {
+                const uint32_t P = P0 + 32u * ST_T * (uint32_t)k;
+                const int g0 = ld.g[k];
+                const uint32_t lp = P - goff[g0], sh = lp & 31u;
+                uint32_t v = 0;
+                if (P < T) {
+                    const uint32_t avail = gb[g0] - lp;
+                    v = sh ? (ld.x0[k] << sh) | (ld.x1[k] >> (32u - sh)) : ld.x0[k];
+                    if (avail < 32u) {
+                        v &= ~(0xffffffffu >> avail);
+                        if (goff[g0] + gb[g0] < T) {          /* the word crosses a group seam */
+                            if (g0 + 1 < ng && gb[g0 + 1] >= 32u - avail) {
+                                v |= ld.y[k] >> avail;      /* the next group's first bits */
+                            } else {                        /* groups under 32 bits: rare */
+                                int g2 = g0;
+                                v = stitch_word(P, g2, ng, T, goff, gb, gw, fr);
+                            }
+                        }
+                    }
+                }
+                v = __builtin_bswap32(v);                  /* memory order */
+                if (P < Pend) o32[t + ST_T * k] = v;
+                cbuf[t + ST_T * k] = v;
+            }
+        }
+        if (c0 + ST_CHUNK < nin) stitch_load(ld, c0 + ST_CHUNK, t, ng, T, goff, gb, gw, fr);
+        lds_barrier();                                  /* the next chunk's loads stay in flight */
+        if (stp && c0 == 0) stp[2] = __builtin_amdgcn_s_memrealtime();
+        /* emulation prevention of this thread's 32 contiguous bytes */
+        const uint32_t ib = c0 + 32u * (uint32_t)t;
         uint32_t wv[8];
         {
-            uint32_t P = ib * 8u;                       /* bit position of its first word */
-            int gg = 0;                                 /* the group holding bit P: binary search */
-            {
-                int lo = 0, hi = ng;                    /* last gg with goff[gg] <= P */
-                while (hi - lo > 1) {
-                    const int mid = (lo + hi) >> 1;
-                    if (goff[mid] <= P) lo = mid;
-                    else hi = mid;
-                }
-                gg = lo;
-            }
-#pragma unroll
-            for (int k = 0; k < 8; ++k, P += 32u) {
-                uint32_t acc = 0;
-                uint32_t filled = 0;
-                while (filled < 32u && gg < ng && P < T) {
-                    const uint32_t lp = P + filled - goff[gg];
-                    if (lp >= gb[gg]) {                 /* group done (or empty) */
-                        ++gg;
-                        continue;
-                    }
-                    const uint32_t take = min(32u - filled, gb[gg] - lp);
-                    const uint32_t *src = fr + gw[gg];
-                    const uint32_t i = lp >> 5, sh = lp & 31u;
-                    uint32_t x = src[i];
-                    if (sh) {
-                        x <<= sh;
-                        if (32u - sh < take) x |= src[i + 1] >> (32u - sh);
-                    }
-                    x &= take >= 32u ? 0xffffffffu : ~(0xffffffffu >> take);
-                    acc |= x >> filled;
-                    filled += take;
-                }
-                wv[k] = __builtin_bswap32(acc);         /* RBSP bytes in memory order */
-            }
+            const uint4 a = cbuf4[2 * t], b2 = cbuf4[2 * t + 1];
+            wv[0] = a.x; wv[1] = a.y; wv[2] = a.z; wv[3] = a.w;
+            wv[4] = b2.x; wv[5] = b2.y; wv[6] = b2.z; wv[7] = b2.w;
         }
-        if (ib < nin) {
-            *reinterpret_cast<uint4 *>(out + ib) = make_uint4(wv[0], wv[1], wv[2], wv[3]);
-            *reinterpret_cast<uint4 *>(out + ib + 16) = make_uint4(wv[4], wv[5], wv[6], wv[7]);
-        }
-        /* emulation prevention of these bytes (nal.c:33-38, closed form) */
         int lnz = -1;
 #pragma unroll
         for (int w = 0; w < 8; ++w) {
@@ -1464,7 +1559,7 @@ __global__ __launch_bounds__(ST_T) void k_dyn_stitch(DevStream *__restrict__ st,
             if (m) lnz = (int)(ib + 4u * w) + 3 - (__builtin_clz(m) >> 3);
         }
         int ex, tot;
-        block_excl_max<ST_NW>(lnz, wmax, ex, tot);
+        block_excl_max<ST_NW, true>(lnz, wmax, ex, tot);   /* its barriers also free cbuf */
         int prev = max(carry, ex);
         carry = max(carry, tot);
         uint32_t ins = 0;
@@ -1484,6 +1579,7 @@ __global__ __launch_bounds__(ST_T) void k_dyn_stitch(DevStream *__restrict__ st,
                 k++;
             }
         }
+        if (stp && c0 == 0) stp[3] = __builtin_amdgcn_s_memrealtime();
     }
     __syncthreads();
     if (t == 0) {
@@ -1491,8 +1587,12 @@ __global__ __launch_bounds__(ST_T) void k_dyn_stitch(DevStream *__restrict__ st,
         DF->rbsp_bytes = nin;
         DF->ep = ep_n;
     }
+    if (stp) {
+        stp[4] = __builtin_amdgcn_s_memrealtime();
+        stp[5] = (nin + ST_CHUNK - 1) / ST_CHUNK;
+        stp[7] = (uint64_t)(uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 4);     /* HW_ID */
+    }
 }
-
 
 /* ---------------------------------------------------------------------- */
 /* k_dyn_emit: staged RBSP -> arena with start code, header, EP bytes       */
@@ -1830,14 +1930,14 @@ int dyn_launch_code(hipStream_t hs, int nframes, int S, DevStream *st, const Nal
 
 int dyn_launch_pack(hipStream_t hs, int nframes, int S, DevStream *st, const NalDesc *nal,
                     int ld_nal, const PlanPending *pend, DynFrame *dfr, int ld_fr,
-                    const DynGeom *g, const DynScratch *x, uint8_t *stage)
+                    const DynGeom *g, const DynScratch *x, uint8_t *stage, uint64_t *stamps)
 {
     if (nframes <= 0 || S <= 0) return 0;
     hipLaunchKernelGGL(k_dyn_static, dim3(g->ngroups - g->h, nframes, S), dim3(GW), 0, hs, st, nal, ld_nal,
                        pend, dfr, ld_fr, *g, x->rowstage, x->gbits);
     if (hipGetLastError() != hipSuccess) return -1;
     hipLaunchKernelGGL(k_dyn_stitch, dim3(nframes, S), dim3(ST_T), 0, hs, st, dfr, ld_fr, *g, x->rowstage,
-                       x->gbits, stage);
+                       x->gbits, stage, stamps);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -1873,6 +1973,10 @@ void dyn_rowstage_geom(DynGeom *g, int mbw, int mbh)
     auto words = [](uint64_t bits) { return (uint32_t)((((bits + 31) / 32) + 63) & ~(uint64_t)63); };
     g->rs_static_words = words((uint64_t)HDR_MAX + (uint64_t)maxrows * mbw * (HEAD_MAX + 1) + 64);
     g->rs_row_words = words((uint64_t)mbw * (HEAD_MAX + 1) + (uint64_t)g->w * MB_BITS_MAX + 64);
+#ifdef SCROLL_RS_SMALL
+    g->rs_static_words = g->rs_static_words < 4096 ? g->rs_static_words : 4096;   /* timing experiment only */
+    g->rs_row_words = g->rs_row_words < 4096 ? g->rs_row_words : 4096;
+#endif
     g->rs_frame_words = (uint64_t)(g->ngroups - g->h) * g->rs_static_words + (uint64_t)g->h * g->rs_row_words;
 }
 

@@ -1298,7 +1298,7 @@ static int launch(ScrollBatch *b, int nframes, int plan_mode, int nal_max, hipSt
                     return rc;
                 }
                 if (dyn_launch_pack(hp, nframes, s1 - s0, st0, nal0, b->ld_nal, pend0, dfr0, ld_fr, &G, &xc,
-                                    stage0)) {
+                                    stage0, stamps ? b->d_dbg : nullptr)) {
                     set_err("k_dyn_static / k_dyn_stitch launch: %s", hipGetErrorString(hipGetLastError()));
                     return SCROLL_ERR_HIP;
                 }

@@ -48,9 +48,20 @@ __device__ inline uint32_t wave_incl_sum(uint32_t v, int lane)
     return v;
 }
 
+/* workgroup barrier for LDS hand-offs only: waits for this wave's LDS
+ * operations, not for its global loads and stores (__syncthreads' release
+ * fence waits for every outstanding vector-memory operation, which would
+ * also drain prefetched loads and fire-and-forget stores).  The "memory"
+ * clobber keeps the compiler from moving memory accesses across it. */
+__device__ inline void lds_barrier()
+{
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
 /* exclusive prefix max over the workgroup (identity -1) and the total;
- * ends with a barrier so `ws` can be reused */
-template <int NWV = NW>
+ * ends with a barrier so `ws` can be reused.  LDS: the barriers are
+ * lds_barrier (global operations stay in flight) */
+template <int NWV = NW, bool LDS = false>
 __device__ inline void block_excl_max(int v, int *ws, int &excl, int &tot)
 {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -58,7 +69,8 @@ __device__ inline void block_excl_max(int v, int *ws, int &excl, int &tot)
     if (lane == 63) ws[wave] = incl;
     int e = __shfl_up(incl, 1, 64);
     if (lane == 0) e = -1;
-    __syncthreads();
+    if (LDS) lds_barrier();
+    else __syncthreads();
     int pm = -1, t = -1;
 #pragma unroll
     for (int w = 0; w < NWV; ++w) {
@@ -67,7 +79,8 @@ __device__ inline void block_excl_max(int v, int *ws, int &excl, int &tot)
     }
     excl = max(pm, e);
     tot = t;
-    __syncthreads();
+    if (LDS) lds_barrier();
+    else __syncthreads();
 }
 
 template <int NWV = NW>

@@ -100,6 +100,17 @@ def main():
         ends = gg[:, :, 5][gg[:, :, 5] > 0]
         conc = [int(np.sum((g0 <= x) & (ends > x))) for x in np.linspace(t0, t1, 12)]
         print("  resident WGs over time:", conc)
+    z = allst[:S * F].astype(np.int64)           # k_dyn_stitch: realtime (100 MHz)
+    z = z[z[:, 0] > 0]
+    if len(z):
+        dur = (z[:, 4] - z[:, 0]) / 100.0
+        print(f"k_dyn_stitch: {len(z)} WGs, span {(z[:, 4].max() - z[:, 0].min()) / 100.0:.1f} us, "
+              f"WG duration mean {dur.mean():.1f} p99 {np.percentile(dur, 99):.1f} us, chunks {z[:, 5].mean():.1f}; "
+              f"scan {((z[:, 1] - z[:, 0]) / 100.0).mean():.2f}  first assembly {((z[:, 2] - z[:, 1]) / 100.0).mean():.2f}  "
+              f"first EP {((z[:, 3] - z[:, 2]) / 100.0).mean():.2f}  rest {((z[:, 4] - z[:, 3]) / 100.0).mean():.2f} us")
+        t0 = z[:, 0].min()
+        conc = [int(np.sum((z[:, 0] <= x) & (z[:, 4] > x))) for x in np.linspace(t0, z[:, 4].max(), 12)]
+        print("  resident WGs over time:", conc)
     e = allst[S * F:2 * S * F].astype(np.int64)  # k_dyn_emit_gather: realtime (100 MHz)
     e = e[e[:, 0] > 0]
     if len(e):

@@ -1148,7 +1148,12 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
             CapSink cap{0, 0, 0};
             int t1 = 0;
             bool ok = true;
+#ifdef SCROLL_ABL_NOCAVLC
+            const int tc = __builtin_popcount(v4.x | v4.y | v4.z | v4.w) & 15;
+            cap.n = tc * 3;
+#else
             const int tc = cavlc_body(cap, L.ptabs, v4, task < 16 * w ? 16 : 15, t1, ok);
+#endif
             mt[slot] = ok ? (uint16_t)(cap.n | (uint32_t)tc << 8 | (uint32_t)t1 << 13)
                           : (uint16_t)((uint32_t)tc << 8 | (uint32_t)t1 << 13 | M_OVF);
             if (ok)
@@ -1335,6 +1340,9 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
             sk.finish();
         }
         /* pieces */
+#ifdef SCROLL_ABL_NOPIECES
+        if (false)
+#endif
         for (int i = t; i < npc; i += T) {
             const uint32_t o = off16[i];
             if (o == 0xffffu) continue;

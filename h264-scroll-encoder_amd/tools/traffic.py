@@ -21,7 +21,7 @@ def per_dispatch(path, counter, kernel):
     vals = collections.defaultdict(float)
     with open(os.path.join(path, "run_counter_collection.csv")) as f:
         for r in csv.DictReader(f):
-            if kernel in r["Kernel_Name"] and r["Counter_Name"] == counter:
+            if kernel + "(" in r["Kernel_Name"] and r["Counter_Name"] == counter:
                 vals[r["Dispatch_Id"]] += float(r["Counter_Value"])
     return list(vals.values())
 

@@ -57,7 +57,8 @@ typedef struct {
 #define SCROLL_DEVERR_CONFIG   2u   /* unsupported config (e.g. log2 fields)      */
 #define SCROLL_DEVERR_DYN      4u   /* a dynamic NAL outgrew its staging slot     */
 #define SCROLL_DEVERR_HINT     8u   /* a hint rect names an invalid reference     */
-#define SCROLL_DEVERR_STAGED   (SCROLL_DEVERR_DYN | SCROLL_DEVERR_HINT)   /* nothing committed */
+#define SCROLL_DEVERR_SPLICE  16u   /* a spliced slice failed (parse / reference) */
+#define SCROLL_DEVERR_STAGED   (SCROLL_DEVERR_DYN | SCROLL_DEVERR_HINT | SCROLL_DEVERR_SPLICE)   /* nothing committed */
 
 /* k_plan state pass -> size pass: the stream's planned totals and the final
  * waypoint table (committed only by the size pass).  128 bytes. */

@@ -28,12 +28,15 @@
 #include <stdint.h>
 
 #include "dyn_device.h"
+#include "hint_device.h"
 #include "hint_engine.h"
+#include "splice_engine.h"
 #include "stage_util.h"
 
 using namespace scroll;
 using namespace scroll::dyn;
 using namespace scroll::stage;
+using namespace scroll::hint;
 
 namespace {
 
@@ -43,11 +46,6 @@ constexpr int HB_WORDS = 1152;          /* LDS bit buffer: header + one window +
 static_assert(HB_WORDS * 32 >= HDR_BITS + DT * MB_BITS + 64, "a window fits the buffer");
 constexpr int RING = 512;               /* MB motion ring: this window + the row above */
 static_assert(RING >= DT + HINT_MAX_MBW + 1, "the row above a window stays in the ring");
-
-/* (ref, mv) of an MB, mv in quarter pels; ref -1 = not available */
-struct Mv {
-    int ref, mx, my;
-};
 
 struct HintLds {
     uint32_t buf[HB_WORDS];
@@ -60,86 +58,6 @@ struct HintLds {
     uint32_t ep_n;                /* EP positions recorded                         */
     int32_t bad;                  /* an MB took a rect with an invalid reference   */
 };
-
-/* scroll layout of the frame (h264_writer.c:555-620) */
-struct Layout {
-    int a_end, ra, mva4, rb, mvb4;
-};
-
-/* the MB's own motion: the topmost rect holding it, else its scroll row;
- * bad = the rect names no valid reference of the frame */
-__device__ inline Mv field(const HintLds &L, int nr, int x, int y, const Layout &lay, int nwp,
-                           bool &bad)
-{
-    for (int i = nr - 1; i >= 0; --i) {
-        const ScrollHintRect r = L.rc[i];
-        if (x >= r.x0 && x < r.x1 && y >= r.y0 && y < r.y1) {
-            const int k = r.ref - 2;
-            bad = !(r.ref == 0 || r.ref == 1 || (k >= 0 && k < nwp && L.wv[k]));
-            return Mv{r.ref, 4 * r.mv_x, 4 * r.mv_y};
-        }
-    }
-    bad = false;
-    return y < lay.a_end ? Mv{lay.ra, 0, lay.mva4} : Mv{lay.rb, 0, lay.mvb4};
-}
-
-/* get_mv_prediction (h264_writer.c:369-432): C is above-right, else
- * above-left; 0 available -> 0; 1 available -> its mv if its ref matches;
- * exactly one ref match -> that mv; else median3 (:362-367) */
-__device__ inline void predict_ref(const Mv &A, const Mv &B, const Mv &C, int ref, int &px,
-                                   int &py)
-{
-    const bool aA = A.ref >= 0, aB = B.ref >= 0, aC = C.ref >= 0;
-    const bool mA = aA && A.ref == ref, mB = aB && B.ref == ref, mC = aC && C.ref == ref;
-    const int na = (int)aA + (int)aB + (int)aC, nm = (int)mA + (int)mB + (int)mC;
-    if (na == 0) {
-        px = py = 0;
-    } else if (na == 1) {
-        const Mv &k = aA ? A : (aB ? B : C);
-        const bool m = k.ref == ref;
-        px = m ? k.mx : 0;
-        py = m ? k.my : 0;
-    } else if (nm == 1) {
-        const Mv &k = mA ? A : (mB ? B : C);
-        px = k.mx;
-        py = k.my;
-    } else {
-        px = median3(aA ? A.mx : 0, aB ? B.mx : 0, aC ? C.mx : 0);
-        py = median3(aA ? A.my : 0, aB ? B.my : 0, aC ? C.my : 0);
-    }
-}
-
-__device__ inline int med3(int a, int b, int c) { return max(min(a, b), min(max(a, b), c)); }
-
-/* H.264 8.4.1.3 for a 16x16 partition (unavailable: ref -1, mv 0) */
-__device__ inline void predict_spec(Mv A, Mv B, Mv C, int ref, int &px, int &py)
-{
-    if (B.ref < 0 && C.ref < 0 && A.ref >= 0) {          /* 8.4.1.3.1 */
-        B = A;
-        C = A;
-    }
-    const bool mA = A.ref == ref, mB = B.ref == ref, mC = C.ref == ref;
-    if ((int)mA + (int)mB + (int)mC == 1) {
-        const Mv &k = mA ? A : (mB ? B : C);
-        px = k.mx;
-        py = k.my;
-    } else {
-        px = med3(A.mx, B.mx, C.mx);
-        py = med3(A.my, B.my, C.my);
-    }
-}
-
-/* H.264 8.4.1.1: motion of a P_Skip MB at (x, y) */
-__device__ inline void pskip_mv(int x, int y, const Mv &A, const Mv &B, const Mv &C, int &px,
-                                int &py)
-{
-    if (x == 0 || y == 0 || (A.ref == 0 && A.mx == 0 && A.my == 0) ||
-        (B.ref == 0 && B.mx == 0 && B.my == 0)) {
-        px = py = 0;
-        return;
-    }
-    predict_spec(A, B, C, 0, px, py);
-}
 
 __global__ __launch_bounds__(DT) void k_hint_stage(DevStream *__restrict__ st,
                                                    const NalDesc *__restrict__ nal, int ld_nal,
@@ -156,8 +74,9 @@ __global__ __launch_bounds__(DT) void k_hint_stage(DevStream *__restrict__ st,
     const int j = DF->nal;
     if (j < 0) return;                                     /* experiment mode: no scroll NAL */
     const HintFrame H = hf[(size_t)s * ld_fr + f];
+    if (H.mode & HINT_MODE_SPLICED) return;                /* k_splice_stage's frame */
     const int nr = min((int)H.n, SCROLL_HINT_MAX_RECTS);
-    const bool pskip = H.mode == SCROLL_HINT_PSKIP;
+    const bool pskip = (H.mode & 0xff) == SCROLL_HINT_PSKIP;
     if (t == 0) {
         L.lnz_r = -1;
         L.lnz_w = -1;
@@ -225,7 +144,7 @@ __global__ __launch_bounds__(DT) void k_hint_stage(DevStream *__restrict__ st,
         if (m < nmb) {
             const int y = (int)div_m((uint32_t)m, m_mbw), x = m - y * mbw;
             bool bad;
-            me = field(L, nr, x, y, lay, c.nwp, bad);
+            me = field(L.rc, L.wv, nr, x, y, lay, c.nwp, bad);
             my_bad |= bad;
             L.fr[m & (RING - 1)] = me.ref;
             L.fx[m & (RING - 1)] = me.mx;

@@ -22,6 +22,7 @@
 
 #include "dyn_engine.h"
 #include "hint_engine.h"
+#include "splice_engine.h"
 #include "ingest_engine.h"
 #include "ipcm_engine.h"
 #include "engine.h"
@@ -917,6 +918,22 @@ struct ScrollBatch {
     HintFrame *d_hf = nullptr;
     ScrollHintRect *d_pool = nullptr;
     size_t pool_cap = 0;
+    /* pre-encoded MB splice: frames of the hint path
+     * whose rect comes from an external slice */
+    struct SpliceHost {
+        int x0 = 0, y0 = 0, w = 0, h = 0;
+        std::vector<uint8_t> nal;
+    };
+    std::vector<SpliceHost> h_sp;      /* [s * max_frames + f]; w = 0: none */
+    int sp_n = 0;                      /* spliced frames                           */
+    int sp_dirty = 0;                  /* upload + parse before the next compose   */
+    int sp_parse = 0;                  /* k_splice_parse pending                   */
+    SpliceFrame *d_spf = nullptr;      /* [max_streams * max_frames]               */
+    uint8_t *d_sp_nal = nullptr;
+    uint32_t *d_sp_rbsp = nullptr;
+    SpliceMbRec *d_sp_rec = nullptr;
+    int32_t *d_sp_list = nullptr;
+    size_t sp_nal_cap = 0, sp_rbsp_cap = 0, sp_rec_cap = 0, sp_list_cap = 0;
     /* stream ingest: scratch, grown on demand */
     uint8_t *d_ing_in = nullptr;
     size_t ing_in_cap = 0;
@@ -1056,6 +1073,11 @@ void scroll_batch_destroy(ScrollBatch *b)
     (void)hipFree(b->d_stage);
     (void)hipFree(b->d_hf);
     (void)hipFree(b->d_pool);
+    (void)hipFree(b->d_spf);
+    (void)hipFree(b->d_sp_nal);
+    (void)hipFree(b->d_sp_rbsp);
+    (void)hipFree(b->d_sp_rec);
+    (void)hipFree(b->d_sp_list);
     (void)hipFree(b->d_ing_in);
     (void)hipFree(b->d_ipcm_cnt);
     (void)hipFree(b->d_ing_files);
@@ -1245,10 +1267,25 @@ static int launch(ScrollBatch *b, int nframes, int plan_mode, int nal_max, hipSt
         }
         b->geo.debug = b->debug;
         if (hint) {
+            if (b->sp_parse) {
+                if (splice_launch_parse(hs, b->sp_n, b->d_sp_list, b->d_spf, b->d_st, ld_fr,
+                                        b->d_sp_nal, b->d_sp_rbsp, b->d_sp_rec)) {
+                    set_err("k_splice_parse launch: %s", hipGetErrorString(hipGetLastError()));
+                    return SCROLL_ERR_HIP;
+                }
+                b->sp_parse = 0;
+            }
             if (hint_launch_stage(hs, nframes, S, b->d_st, b->d_nal, b->ld_nal, b->d_pend,
                                   b->d_dfr, ld_fr, b->d_hf, b->d_pool, b->d_stage,
                                   b->geo.slot_bytes)) {
                 set_err("k_hint_stage launch: %s", hipGetErrorString(hipGetLastError()));
+                return SCROLL_ERR_HIP;
+            }
+            if (b->sp_n > 0 &&
+                splice_launch_stage(hs, nframes, S, b->d_st, b->d_nal, b->ld_nal, b->d_pend,
+                                    b->d_dfr, ld_fr, b->d_hf, b->d_pool, b->d_spf, b->d_sp_rec,
+                                    b->d_sp_rbsp, b->d_stage, b->geo.slot_bytes)) {
+                set_err("k_splice_stage launch: %s", hipGetErrorString(hipGetLastError()));
                 return SCROLL_ERR_HIP;
             }
             if ((rc = mark(6))) return rc;
@@ -1350,6 +1387,9 @@ static int launch(ScrollBatch *b, int nframes, int plan_mode, int nal_max, hipSt
 }
 
 static int hint_upload(ScrollBatch *b);
+static int splice_upload(ScrollBatch *b);
+static int splice_frame_status(ScrollBatch *b, size_t i, int *status);
+static const char *splice_msg(int e);
 
 int scroll_batch_compose(ScrollBatch *b, int nframes, void *hip_stream)
 {
@@ -1367,6 +1407,10 @@ int scroll_batch_compose_ex(ScrollBatch *b, int nframes, void *hip_stream, int f
         return SCROLL_ERR_CONFIG;
     }
     HIPCHK(hipSetDevice(b->device));
+    if (b->hint_on && b->sp_dirty) {
+        int rc = splice_upload(b);
+        if (rc) return rc;
+    }
     if (b->hint_on && b->hint_dirty) {
         int rc = hint_upload(b);
         if (rc) return rc;
@@ -1394,7 +1438,13 @@ int scroll_batch_sync(ScrollBatch *b)
     int rc = SCROLL_OK;
     for (int s = 0; s < b->nstreams; ++s) {
         if (!b->h_st[s].err) continue;
-        if (rc == SCROLL_OK && (b->h_st[s].err & SCROLL_DEVERR_HINT)) {
+        if (rc == SCROLL_OK && (b->h_st[s].err & SCROLL_DEVERR_SPLICE)) {
+            int st = 0, ff = 0;
+            for (; ff < b->max_frames && !st; ++ff)
+                if (splice_frame_status(b, (size_t)s * b->max_frames + ff, &st)) break;
+            set_err("stream %d frame %d: spliced slice: %s", s, ff - 1, splice_msg(st));
+            rc = SCROLL_ERR_CONFIG;
+        } else if (rc == SCROLL_OK && (b->h_st[s].err & SCROLL_DEVERR_HINT)) {
             set_err("stream %d: a hint rect names a reference that is not valid in its frame "
                     "(ref 2 + i needs waypoint i)", s);
             rc = SCROLL_ERR_CONFIG;
@@ -1763,6 +1813,21 @@ static void hint_release(ScrollBatch *b)
     b->hint_dirty = 0;
     b->h_hint.clear();
     b->h_hint_mode.clear();
+    (void)hipFree(b->d_spf);
+    (void)hipFree(b->d_sp_nal);
+    (void)hipFree(b->d_sp_rbsp);
+    (void)hipFree(b->d_sp_rec);
+    (void)hipFree(b->d_sp_list);
+    b->d_spf = nullptr;
+    b->d_sp_nal = nullptr;
+    b->d_sp_rbsp = nullptr;
+    b->d_sp_rec = nullptr;
+    b->d_sp_list = nullptr;
+    b->sp_nal_cap = b->sp_rbsp_cap = b->sp_rec_cap = b->sp_list_cap = 0;
+    b->h_sp.clear();
+    b->sp_n = 0;
+    b->sp_dirty = 0;
+    b->sp_parse = 0;
 }
 
 /* host hint tables -> d_hf (per frame) + d_pool (all rects) */
@@ -1775,6 +1840,7 @@ static int hint_upload(ScrollBatch *b)
         hf[i].first = (int32_t)pool.size();
         hf[i].n = (int16_t)b->h_hint[i].size();
         hf[i].mode = b->h_hint_mode[i];
+        if (i < b->h_sp.size() && b->h_sp[i].w > 0) hf[i].mode |= HINT_MODE_SPLICED;
         pool.insert(pool.end(), b->h_hint[i].begin(), b->h_hint[i].end());
     }
     if (pool.size() > b->pool_cap) {
@@ -1865,6 +1931,174 @@ int scroll_batch_clear_hints(ScrollBatch *b)
     HIPCHK(hipSetDevice(b->device));
     hint_release(b);
     return SCROLL_OK;
+}
+
+/* ------------------------- pre-encoded MB splice --------------------------- */
+/* grow a device buffer to n elements of `size` bytes (contents dropped) */
+static int sp_grow(void **p, size_t *cap, size_t n, size_t size)
+{
+    if (n <= *cap) return SCROLL_OK;
+    (void)hipFree(*p);
+    *p = nullptr;
+    *cap = 0;
+    hipError_t e = hipMalloc(p, std::max<size_t>(n, 1) * size);
+    if (e != hipSuccess) {
+        set_err("splice: %s", hipGetErrorString(e));
+        return e == hipErrorOutOfMemory ? SCROLL_ERR_OOM : SCROLL_ERR_HIP;
+    }
+    *cap = n;
+    return SCROLL_OK;
+}
+
+/* host splices -> device (table, NAL pool, pools sized for the parse) and
+ * staging slots grown to the largest spliced NAL's bound; k_splice_parse
+ * runs on the next compose's stream */
+static int splice_upload(ScrollBatch *b)
+{
+    const size_t S = (size_t)b->max_streams, F = (size_t)b->max_frames;
+    std::vector<SpliceFrame> spf(S * F);
+    std::vector<int32_t> list;
+    std::vector<uint8_t> pool;
+    size_t words = 0, recs = 0, slot = b->geo.slot_bytes;
+    for (size_t i = 0; i < b->h_sp.size(); ++i) {
+        const ScrollBatch::SpliceHost &h = b->h_sp[i];
+        SpliceFrame &o = spf[i];
+        o = SpliceFrame{};
+        if (h.w <= 0) continue;
+        o.x0 = h.x0;
+        o.y0 = h.y0;
+        o.w = h.w;
+        o.h = h.h;
+        o.nal_off = pool.size();
+        o.nal_len = (uint32_t)h.nal.size();
+        o.rbsp_word = words;
+        o.rec_first = (uint32_t)recs;
+        pool.insert(pool.end(), h.nal.begin(), h.nal.end());
+        pool.resize((pool.size() + 3) & ~(size_t)3);
+        words += h.nal.size() / 4 + 2;
+        recs += (size_t)h.w * h.h;
+        list.push_back((int32_t)i);
+        const DevStream &d = b->h_st[i / F];
+        slot = std::max(slot, splice_slot_bound(d.w / 16, d.h / 16, h.w, h.h, h.nal.size()));
+    }
+    int rc;
+    if (!b->d_spf) {
+        HIPCHK(hipMalloc(&b->d_spf, S * F * sizeof(SpliceFrame)));
+    }
+    if ((rc = sp_grow((void **)&b->d_sp_nal, &b->sp_nal_cap, pool.size(), 1)) ||
+        (rc = sp_grow((void **)&b->d_sp_rbsp, &b->sp_rbsp_cap, words, sizeof(uint32_t))) ||
+        (rc = sp_grow((void **)&b->d_sp_rec, &b->sp_rec_cap, recs, sizeof(SpliceMbRec))) ||
+        (rc = sp_grow((void **)&b->d_sp_list, &b->sp_list_cap, list.size(), sizeof(int32_t))))
+        return rc;
+    if (slot > b->geo.slot_bytes) {
+        (void)hipFree(b->d_stage);
+        b->d_stage = nullptr;
+        hipError_t e = hipMalloc(&b->d_stage, S * F * slot);
+        if (e != hipSuccess) {
+            set_err("scroll_batch_compose: splice staging (%zu bytes per frame): %s", slot,
+                    hipGetErrorString(e));
+            hint_release(b);
+            return e == hipErrorOutOfMemory ? SCROLL_ERR_OOM : SCROLL_ERR_HIP;
+        }
+        b->geo.slot_bytes = slot;
+    }
+    HIPCHK(hipMemcpy(b->d_spf, spf.data(), S * F * sizeof(SpliceFrame), hipMemcpyHostToDevice));
+    if (!pool.empty())
+        HIPCHK(hipMemcpy(b->d_sp_nal, pool.data(), pool.size(), hipMemcpyHostToDevice));
+    if (!list.empty())
+        HIPCHK(hipMemcpy(b->d_sp_list, list.data(), list.size() * sizeof(int32_t),
+                         hipMemcpyHostToDevice));
+    b->sp_n = (int)list.size();
+    b->sp_parse = b->sp_n > 0;
+    b->sp_dirty = 0;
+    return SCROLL_OK;
+}
+
+int scroll_batch_set_splice(ScrollBatch *b, int s, int f, int x0, int y0, int w, int h,
+                            const uint8_t *nal, size_t n)
+{
+    if (!b || s < 0 || s >= b->nstreams || f < 0 || f >= b->max_frames ||
+        (n > 0 && (!nal || w <= 0 || h <= 0 || x0 < 0 || y0 < 0 || n > ((size_t)1 << 30)))) {
+        set_err("scroll_batch_set_splice: bad arguments");
+        return SCROLL_ERR_ARG;
+    }
+    if (n > 0 && (x0 + w > b->h_st[s].w / 16 || y0 + h > b->h_st[s].h / 16)) {
+        set_err("scroll_batch_set_splice: rect (%d, %d) %dx%d MBs outside the %dx%d picture", x0,
+                y0, w, h, b->h_st[s].w, b->h_st[s].h);
+        return SCROLL_ERR_ARG;
+    }
+    if (b->dyn_on) {
+        set_err("scroll_batch_set_splice: not combinable with a dynamic rect");
+        return SCROLL_ERR_CONFIG;
+    }
+    if (n == 0 && !b->hint_on) return SCROLL_OK;
+    if (!b->hint_on) {                 /* the splice rides on the hint path */
+        int rc = scroll_batch_set_hints(b, s, f, nullptr, 0, SCROLL_HINT_EXACT);
+        if (rc) return rc;
+    } else {
+        int rc = batch_host_sync(b);
+        if (rc) return rc;
+    }
+    const size_t i = (size_t)s * b->max_frames + f;
+    if (b->h_sp.size() < (size_t)b->max_streams * b->max_frames)
+        b->h_sp.resize((size_t)b->max_streams * b->max_frames);
+    ScrollBatch::SpliceHost &sp = b->h_sp[i];
+    if (n == 0) {
+        sp = ScrollBatch::SpliceHost{};
+    } else {
+        sp.x0 = x0;
+        sp.y0 = y0;
+        sp.w = w;
+        sp.h = h;
+        sp.nal.assign(nal, nal + n);
+    }
+    b->sp_dirty = 1;
+    b->hint_dirty = 1;
+    return SCROLL_OK;
+}
+
+int scroll_batch_clear_splices(ScrollBatch *b)
+{
+    if (!b) return SCROLL_ERR_ARG;
+    if (b->h_sp.empty()) return SCROLL_OK;
+    int rc = batch_host_sync(b);
+    if (rc) return rc;
+    b->h_sp.clear();
+    b->sp_dirty = 1;
+    b->hint_dirty = 1;
+    return SCROLL_OK;
+}
+
+static int splice_frame_status(ScrollBatch *b, size_t i, int *status)
+{
+    *status = SCROLL_SPLICE_OK;
+    if (!b->d_spf || i >= b->h_sp.size() || b->h_sp[i].w <= 0) return SCROLL_OK;
+    SpliceFrame sf;
+    HIPCHK(hipMemcpy(&sf, b->d_spf + i, sizeof(sf), hipMemcpyDeviceToHost));
+    *status = sf.status ? sf.status : sf.stage_status;
+    return SCROLL_OK;
+}
+
+int scroll_batch_splice_status(ScrollBatch *b, int s, int f, int *status)
+{
+    if (!b || !status || s < 0 || s >= b->nstreams || f < 0 || f >= b->max_frames)
+        return SCROLL_ERR_ARG;
+    int rc = batch_host_sync(b);
+    if (rc) return rc;
+    HIPCHK(hipSetDevice(b->device));
+    return splice_frame_status(b, (size_t)s * b->max_frames + f, status);
+}
+
+static const char *splice_msg(int e)
+{
+    switch (e) {
+    case SCROLL_SPLICE_ERR_NAL: return "not a coded slice of a non-IDR picture";
+    case SCROLL_SPLICE_ERR_HEADER: return "slice header outside the supported syntax";
+    case SCROLL_SPLICE_ERR_MBTYPE: return "an MB other than P_L0_16x16 / P_Skip";
+    case SCROLL_SPLICE_ERR_SYNTAX: return "malformed or truncated slice data, or an MB count other than the rect's";
+    case SCROLL_SPLICE_ERR_REF: return "a ref_idx that is not a valid reference of the frame";
+    default: return "unknown";
+    }
 }
 
 /* ------------------------------ stream ingest ------------------------------ */

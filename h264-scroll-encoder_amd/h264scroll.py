@@ -113,6 +113,8 @@ class ScrollHintRect(ctypes.Structure):
 
 
 SCROLL_HINT_EXACT, SCROLL_HINT_PSKIP, SCROLL_HINT_MAX_RECTS = 0, 1, 64
+(SCROLL_SPLICE_OK, SCROLL_SPLICE_ERR_NAL, SCROLL_SPLICE_ERR_HEADER, SCROLL_SPLICE_ERR_MBTYPE,
+ SCROLL_SPLICE_ERR_SYNTAX, SCROLL_SPLICE_ERR_REF) = range(6)
 
 
 def _load():
@@ -176,6 +178,12 @@ def _load():
         "scroll_batch_set_hints": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
                                                   P(ScrollHintRect), ctypes.c_int, ctypes.c_int]),
         "scroll_batch_clear_hints": (ctypes.c_int, [ctypes.c_void_p]),
+        "scroll_batch_set_splice": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                                   ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                                   ctypes.c_int, ctypes.c_char_p, ctypes.c_size_t]),
+        "scroll_batch_clear_splices": (ctypes.c_int, [ctypes.c_void_p]),
+        "scroll_batch_splice_status": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                                      P(ctypes.c_int)]),
         "scroll_batch_ingest": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, P(u8p),
                                                P(ctypes.c_size_t), P(u8p), P(ctypes.c_size_t),
                                                P(ctypes.c_int)]),
@@ -455,6 +463,22 @@ class Batch:
 
     def clear_hints(self):
         self._chk(lib.scroll_batch_clear_hints(self.h), "clear_hints")
+
+    # ---- pre-encoded MB splice ----
+    def set_splice(self, s, f, x0, y0, w, h, nal):
+        """the external P slice `nal` (bytes) into MB rect (x0, y0, w, h) of
+        frame f of stream s; nal = b"" removes it"""
+        nal = bytes(nal)
+        self._chk(lib.scroll_batch_set_splice(self.h, s, f, x0, y0, w, h, nal, len(nal)),
+                  "set_splice")
+
+    def clear_splices(self):
+        self._chk(lib.scroll_batch_clear_splices(self.h), "clear_splices")
+
+    def splice_status(self, s, f):
+        st = ctypes.c_int()
+        self._chk(lib.scroll_batch_splice_status(self.h, s, f, ctypes.byref(st)), "splice_status")
+        return st.value
 
     # ---- dynamic rect (configs 3-5) ----
     def set_dyn_rect(self, x0, y0, w, h, slot_bytes=0):

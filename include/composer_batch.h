@@ -207,6 +207,53 @@ int scroll_batch_set_hints(ScrollBatch *b, int s, int f, const ScrollHintRect *r
                            int mode);
 int scroll_batch_clear_hints(ScrollBatch *b);
 
+/* ---- pre-encoded MB splice (reference design
+ * docs/MASTER_DESIGN.md:39-40,87-90,142-146,166-171, no reference
+ * implementation) ----
+ * The MBs of an external P slice -- a conventional encoder's output for the
+ * dynamic rect, coded as its own w x h MB picture -- are transplanted into
+ * the rect [x0, x0 + w) x [y0, y0 + h) of frame f's scroll NAL: P_Skip MBs
+ * become P_L0_16x16 with their skip motion, mb_skip_run / ref_idx / mvd are
+ * re-coded for the composed picture, mb_qp_delta rebased to the composed
+ * slice QP, each residual block keeps its bits after coeff_token and gets
+ * the coeff_token of its composed nC.  MBs outside the rect follow the frame's
+ * UI hints (a splice turns the hint path on; frames without a splice and
+ * without hints equal the reference's scroll frames in SCROLL_HINT_EXACT;
+ * set_hints(.., NULL, 0, SCROLL_HINT_PSKIP) picks the standard's predictor).
+ * Bit-exact definition: oracle/splice_oracle.h.
+ *
+ * The external slice: one NAL (Annex-B start code optional), nal_unit_type
+ * 1, CAVLC, first_mb_in_slice 0 and all w*h MBs, parsed with the composed
+ * stream's SPS/PPS (log2_max_frame_num, POC type, 2 default references,
+ * disable_deblocking_filter_idc 1 when the stream signals deblocking
+ * control); no ref_pic_list_modification; MBs P_L0_16x16 or P_Skip;
+ * ref_idx 0 = A, 1 = B, 2 + i = waypoint i of the composed stream; motion
+ * vectors are displacements in the composed picture, |mv| <= 16383 quarter
+ * pels; CAVLC level_prefix <= 15 (Baseline / Main).
+ *
+ *   scroll_batch_set_splice(b, s, f, x0, y0, w, h, nal, n)   frame f of
+ *       stream s, for every following compose; n = 0 removes it.  The slice
+ *       is parsed on the GPU by the next compose; a slice outside the
+ *       supported syntax, or a reference the frame does not have, fails that
+ *       stream's compose with SCROLL_ERR_CONFIG (nothing of the batch is
+ *       written for the stream) and scroll_batch_splice_status gives the
+ *       reason (SCROLL_SPLICE_ERR_*).
+ *   scroll_batch_clear_splices(b)   remove every splice (hints stay).
+ * The staging slots grow to the largest spliced NAL's bound (about the
+ * external slice plus 16 bytes per picture MB) for every (stream, frame). */
+#define SCROLL_SPLICE_OK          0
+#define SCROLL_SPLICE_ERR_NAL     1   /* not a coded slice of a non-IDR picture     */
+#define SCROLL_SPLICE_ERR_HEADER  2   /* slice header outside the supported syntax  */
+#define SCROLL_SPLICE_ERR_MBTYPE  3   /* an MB other than P_L0_16x16 / P_Skip       */
+#define SCROLL_SPLICE_ERR_SYNTAX  4   /* malformed, truncated or MB count mismatch   */
+#define SCROLL_SPLICE_ERR_REF     5   /* ref_idx not a valid reference of the frame  */
+int scroll_batch_set_splice(ScrollBatch *b, int s, int f, int x0, int y0, int w, int h,
+                            const uint8_t *nal, size_t n);
+int scroll_batch_clear_splices(ScrollBatch *b);
+/* after sync: SCROLL_SPLICE_* of frame f of stream s in the last compose
+ * (SCROLL_SPLICE_OK also when the frame has no splice) */
+int scroll_batch_splice_status(ScrollBatch *b, int s, int f, int *status);
+
 /* ---- stream ingest on the GPU ----
  * Batched composer_init + composer_write_header (reference src/composer.c:
  * 127-253): n new streams from their reference files (Annex-B with SPS, PPS

@@ -289,8 +289,44 @@ int or_cavlc_block(or_bits *b, const int *coef, int max, int nC)
     return tc;
 }
 
+/* code tables for decoders (splice_oracle.c): (bits, length), length 0 =
+ * no such code */
+int or_ct_code(int tc, int t1, int nC, uint32_t *bits)
+{
+    if (tc < 0 || tc > 16 || t1 < 0 || t1 > 3 || t1 > tc) return 0;
+    if (nC == -1) {
+        if (tc > 4) return 0;
+        *bits = OR_CTDC_BITS[4 * tc + t1];
+        return OR_CTDC_LEN[4 * tc + t1];
+    }
+    if (nC >= 8) {
+        *bits = tc ? (uint32_t)(((tc - 1) << 2) | t1) : 3u;
+        return 6;
+    }
+    const int tb = nC < 2 ? 0 : (nC < 4 ? 1 : 2);
+    *bits = OR_CT_BITS[tb][4 * tc + t1];
+    return OR_CT_LEN[tb][4 * tc + t1];
+}
+int or_tz_code(int tc, int tz, int maxc, uint32_t *bits)
+{
+    if (tc < 1 || tc >= maxc || tz < 0 || tz > maxc - tc) return 0;
+    if (maxc == 4) {
+        *bits = OR_TZDC_BITS[tc - 1][tz];
+        return OR_TZDC_LEN[tc - 1][tz];
+    }
+    *bits = OR_TZ_BITS[tc - 1][tz];
+    return OR_TZ_LEN[tc - 1][tz];
+}
+int or_rb_code(int zl, int run, uint32_t *bits)
+{
+    if (zl < 1 || run < 0 || run > zl || run > 14) return 0;
+    const int zi = (zl < 7 ? zl : 7) - 1;
+    *bits = OR_RB_BITS[zi][run];
+    return OR_RB_LEN[zi][run];
+}
+
 /* coded_block_pattern me(v), Inter column of Table 9-4: cbp -> codeNum */
-static int or_cbp_code(int cbp)
+int or_cbp_code(int cbp)
 {
     static const uint8_t golomb_to_inter[48] = {
         0,  16, 1,  2,  4,  8,  32, 3,  5,  10, 12, 15, 47, 7,  11, 13,

@@ -77,6 +77,13 @@ int or_ref_sample(const or_cfg *c, const or_refs *R, int ri, int plane, int x, i
 /* CAVLC residual block (9.2): coefficients in scan order, max = 16 / 15 /
  * 4 (chroma DC, nC = -1); returns TotalCoeff */
 int or_cavlc_block(or_bits *b, const int *coef, int max, int nC);
+/* code tables for decoders: coeff_token (Table 9-5), total_zeros (9-7,
+ * 9-8, 9-9a), run_before (9-10): returns the length (0 = no such code) and
+ * the bits; or_cbp_code: coded_block_pattern -> codeNum (Table 9-4 Inter) */
+int or_ct_code(int tc, int t1, int nC, uint32_t *bits);
+int or_tz_code(int tc, int tz, int maxc, uint32_t *bits);
+int or_rb_code(int zl, int run, uint32_t *bits);
+int or_cbp_code(int cbp);
 /* forward 4x4 core transform + quantisation of a residual block (raster) */
 void or_fwd4x4(const int res[16], int W[16]);
 int or_quant(int w, int qp, int pos, int dc_chroma);

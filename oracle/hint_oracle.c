@@ -108,6 +108,28 @@ static void pskip_mv(int x, int y, const or_mvi *A, const or_mvi *B, const or_mv
     spec_mvp(A, B, C, 0, px, py);
 }
 
+/* exported for the splice restatement (splice_oracle.c) */
+int or_hint_motion(const or_hint_rect *r, int n, int x, int y, int a_end, int ra, int mva,
+                   int rb, int mvb, int *ref, int *mx, int *my)
+{
+    return field_at(r, n, x, y, a_end, ra, mva, rb, mvb, ref, mx, my);
+}
+int or_ref_valid(const or_cfg *c, int ref) { return ref_valid(c, ref); }
+void or_neighbours(int x, int y, int mbw, const or_mvi *above, const or_mvi *left, or_mvi *A,
+                   or_mvi *B, or_mvi *C)
+{
+    neighbours(x, y, mbw, above, left, A, B, C);
+}
+void or_spec_predict(const or_mvi *A, const or_mvi *B, const or_mvi *C, int ref, int *px, int *py)
+{
+    spec_mvp(A, B, C, ref, px, py);
+}
+void or_pskip_motion(int x, int y, const or_mvi *A, const or_mvi *B, const or_mvi *C, int *px,
+                     int *py)
+{
+    pskip_mv(x, y, A, B, C, px, py);
+}
+
 size_t or_hint_scroll_nal(uint8_t *dst, size_t cap, or_cfg *c, int off,
                           const or_hint_rect *r, int n, int mode, int *err)
 {

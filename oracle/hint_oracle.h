@@ -71,6 +71,21 @@ size_t or_compose_hint(uint8_t *dst, size_t cap, or_cfg *c, int off, int compose
  * row-major, out[3 * mbw * mbh]; returns 0, or -1 on an invalid ref */
 int or_hint_field(const or_cfg *c, int off, const or_hint_rect *r, int n, int32_t *out);
 
+/* motion helpers shared with the splice restatement (splice_oracle.c):
+ * the topmost rect holding MB (x, y) (returns 1; else 0 and the scroll row's
+ * motion, mv in pixels); reference validity; neighbours A, B, C-or-D of
+ * 8.4.1.3.2 (unavailable: avail 0); median prediction 8.4.1.3 and P_Skip
+ * motion 8.4.1.1 (quarter pels) */
+int or_hint_motion(const or_hint_rect *r, int n, int x, int y, int a_end, int ra, int mva,
+                   int rb, int mvb, int *ref, int *mx, int *my);
+int or_ref_valid(const or_cfg *c, int ref);
+void or_neighbours(int x, int y, int mbw, const or_mvi *above, const or_mvi *left, or_mvi *A,
+                   or_mvi *B, or_mvi *C);
+void or_spec_predict(const or_mvi *A, const or_mvi *B, const or_mvi *C, int ref, int *px,
+                     int *py);
+void or_pskip_motion(int x, int y, const or_mvi *A, const or_mvi *B, const or_mvi *C, int *px,
+                     int *py);
+
 #ifdef __cplusplus
 }
 #endif

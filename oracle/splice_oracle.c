@@ -1,0 +1,647 @@
+/*
+ * splice_oracle.c -- CPU ORACLE (test infrastructure only): the pre-encoded
+ * MB splice.  See splice_oracle.h for the semantics and what pins the bits.
+ * The slice parse follows ITU-T H.264 7.3.3 (slice header), 7.3.4 (slice
+ * data), 7.3.5 (macroblock layer), 7.3.5.3 / 9.2 (CAVLC residual) and
+ * 8.4.1.1 / 8.4.1.3 (P_Skip motion, median prediction); the composed MB
+ * loop follows the UI-hint restatement (hint_oracle.c), itself the
+ * reference's scroll frame (src/h264_writer.c:595-646) generalised.
+ */
+#include "splice_oracle.h"
+
+#include <stdlib.h>
+#include <string.h>
+
+#include "dyn_oracle.h"
+
+/* ------------------------------------------------------------------------ */
+/* RBSP bit reader                                                           */
+/* ------------------------------------------------------------------------ */
+typedef struct {
+    const uint8_t *d;
+    size_t nbits, p;
+    int bad;                     /* read past the end */
+} rd_t;
+
+static uint32_t rd_peek(const rd_t *r, int n)
+{
+    uint32_t v = 0;
+    for (int i = 0; i < n; ++i) {
+        const size_t q = r->p + (size_t)i;
+        const uint32_t bit = q < r->nbits ? (uint32_t)(r->d[q >> 3] >> (7 - (q & 7))) & 1u : 0u;
+        v = (v << 1) | bit;
+    }
+    return v;
+}
+
+static uint32_t rd_u(rd_t *r, int n)
+{
+    const uint32_t v = rd_peek(r, n);
+    r->p += (size_t)n;
+    if (r->p > r->nbits) r->bad = 1;
+    return v;
+}
+
+static uint32_t rd_ue(rd_t *r)
+{
+    int z = 0;
+    while (!r->bad && rd_u(r, 1) == 0)
+        if (++z > 31) {
+            r->bad = 1;
+            return 0;
+        }
+    if (r->bad || z == 0) return 0;
+    return ((1u << z) - 1u) + rd_u(r, z);
+}
+
+static int32_t rd_se(rd_t *r)
+{
+    const uint32_t k = rd_ue(r);
+    return (k & 1u) ? (int32_t)((k + 1u) >> 1) : -(int32_t)(k >> 1);
+}
+
+/* consume (bits, len) if the stream continues with it */
+static int rd_match(rd_t *r, uint32_t bits, int len)
+{
+    if (len <= 0 || rd_peek(r, len) != bits) return 0;
+    r->p += (size_t)len;
+    if (r->p > r->nbits) r->bad = 1;
+    return 1;
+}
+
+/* emulation prevention removal (7.4.1: 0x000003 -> 0x0000) */
+static size_t sp_unescape(uint8_t *dst, const uint8_t *src, size_t n)
+{
+    size_t o = 0;
+    int zeros = 0;
+    for (size_t i = 0; i < n; ++i) {
+        if (zeros >= 2 && src[i] == 3) {
+            zeros = 0;
+            continue;
+        }
+        dst[o++] = src[i];
+        zeros = src[i] ? 0 : zeros + 1;
+    }
+    return o;
+}
+
+/* ------------------------------------------------------------------------ */
+/* CAVLC block: coeff_token, then the nC-independent body (9.2)              */
+/* ------------------------------------------------------------------------ */
+static int sp_block(rd_t *r, int nC, int maxc, uint8_t *tc_o, uint8_t *t1_o, uint32_t *boff,
+                    uint32_t *blen)
+{
+    int tc = -1, t1 = 0;
+    const int tcmax = nC == -1 ? 4 : 16;
+    for (int c = 0; c <= tcmax && tc < 0; ++c)
+        for (int o = 0; o <= 3 && o <= c; ++o) {
+            uint32_t b;
+            const int len = or_ct_code(c, o, nC, &b);
+            if (rd_match(r, b, len)) {
+                tc = c;
+                t1 = o;
+                break;
+            }
+        }
+    if (tc < 0 || tc > maxc || r->bad) return -1;
+    *boff = (uint32_t)r->p;
+    if (tc > 0) {
+        for (int k = 0; k < t1; ++k) rd_u(r, 1);                 /* trailing_ones_sign_flag */
+        int sl = (tc > 10 && t1 < 3) ? 1 : 0;
+        for (int k = t1; k < tc; ++k) {
+            int prefix = 0;                                       /* level_prefix (9.2.2.1) */
+            while (!r->bad && rd_u(r, 1) == 0)
+                if (++prefix > 15) return -1;                     /* > 15: High profiles only */
+            if (r->bad) return -1;
+            int ssize = sl;
+            if (prefix == 14 && sl == 0) ssize = 4;
+            if (prefix >= 15) ssize = prefix - 3;
+            int code = (prefix < 15 ? prefix : 15) << sl;
+            if (ssize) code += (int)rd_u(r, ssize);
+            if (prefix >= 15 && sl == 0) code += 15;
+            if (k == t1 && t1 < 3) code += 2;
+            const int L = (code & 1) ? -((code + 1) >> 1) : (code + 2) >> 1;
+            if (sl == 0) sl = 1;
+            if ((L < 0 ? -L : L) > (3 << (sl - 1)) && sl < 6) sl++;
+        }
+        int tz = 0;
+        if (tc < maxc) {                                          /* total_zeros */
+            tz = -1;
+            for (int z = 0; z <= maxc - tc; ++z) {
+                uint32_t b;
+                if (rd_match(r, b, or_tz_code(tc, z, maxc, &b))) {
+                    tz = z;
+                    break;
+                }
+            }
+            if (tz < 0) return -1;
+        }
+        int zl = tz;
+        for (int k = 0; k < tc - 1 && zl > 0; ++k) {              /* run_before */
+            int run = -1;
+            for (int q = 0; q <= zl && q <= 14; ++q) {
+                uint32_t b;
+                if (rd_match(r, b, or_rb_code(zl, q, &b))) {
+                    run = q;
+                    break;
+                }
+            }
+            if (run < 0) return -1;
+            zl -= run;
+        }
+    }
+    *blen = (uint32_t)(r->p - *boff);
+    *tc_o = (uint8_t)tc;
+    *t1_o = (uint8_t)t1;
+    return r->bad ? -1 : 0;
+}
+
+static int sp_nc(int nA, int nB)
+{
+    if (nA >= 0 && nB >= 0) return (nA + nB + 1) >> 1;
+    if (nA >= 0) return nA;
+    if (nB >= 0) return nB;
+    return 0;
+}
+
+/* nC of piece i (luma raster 0..15, chroma AC 18..25) of an MB with
+ * TotalCoeffs cur; left / top = the neighbour MBs' or NULL (unavailable) */
+static int sp_piece_nc(int i, const uint8_t *cur, const uint8_t *left, const uint8_t *top)
+{
+    if (i < 16) {
+        const int bx = i & 3, by = i >> 2;
+        const int nA = bx ? cur[i - 1] : (left ? left[i + 3] : -1);
+        const int nB = by ? cur[i - 4] : (top ? top[i + 12] : -1);
+        return sp_nc(nA, nB);
+    }
+    if (i < 18) return -1;
+    const int k = (i - 18) & 3, bx = k & 1, by = k >> 1;
+    const int nA = bx ? cur[i - 1] : (left ? left[i + 1] : -1);
+    const int nB = by ? cur[i - 2] : (top ? top[i + 2] : -1);
+    return sp_nc(nA, nB);
+}
+
+/* luma4x4BlkIdx -> raster index */
+static int sp_blk_raster(int blk)
+{
+    const int q8 = blk >> 2, q4 = blk & 3;
+    return 4 * ((q8 >> 1) * 2 + (q4 >> 1)) + (q8 & 1) * 2 + (q4 & 1);
+}
+
+/* the residual of one MB (7.3.5.3) in piece order; 0 or -1 */
+static int sp_residual(rd_t *r, int cbp, or_splice_mb *mb, const uint8_t *left, const uint8_t *top)
+{
+    for (int blk = 0; blk < 16; ++blk) {
+        if (!(cbp & (1 << (blk >> 2)))) continue;
+        const int i = sp_blk_raster(blk);
+        if (sp_block(r, sp_piece_nc(i, mb->tc, left, top), 16, &mb->tc[i], &mb->t1[i],
+                     &mb->boff[i], &mb->blen[i]))
+            return -1;
+    }
+    if (cbp >> 4) {
+        for (int i = 16; i < 18; ++i)
+            if (sp_block(r, -1, 4, &mb->tc[i], &mb->t1[i], &mb->boff[i], &mb->blen[i])) return -1;
+        if ((cbp >> 4) == 2)
+            for (int i = 18; i < 26; ++i)
+                if (sp_block(r, sp_piece_nc(i, mb->tc, left, top), 15, &mb->tc[i], &mb->t1[i],
+                             &mb->boff[i], &mb->blen[i]))
+                    return -1;
+    }
+    return 0;
+}
+
+static int sp_cbp_of_code(uint32_t code)
+{
+    for (int cbp = 0; cbp < 48; ++cbp)
+        if ((uint32_t)or_cbp_code(cbp) == code) return cbp;
+    return -1;
+}
+
+int or_splice_parse(const or_cfg *c, const or_splice *sp, or_splice_mb *mbs, uint8_t *rbsp,
+                    size_t *rbsp_n)
+{
+    const uint8_t *p = sp->nal;
+    size_t n = sp->n;
+    *rbsp_n = 0;
+    if (n >= 4 && !p[0] && !p[1] && !p[2] && p[3] == 1) {
+        p += 4;
+        n -= 4;
+    } else if (n >= 3 && !p[0] && !p[1] && p[2] == 1) {
+        p += 3;
+        n -= 3;
+    }
+    if (n < 2 || (p[0] & 0x80) || (p[0] & 31) != 1) return OR_SPLICE_ERR_NAL;
+    const int ref_idc = (p[0] >> 5) & 3;
+    const size_t rn = sp_unescape(rbsp, p + 1, n - 1);
+    *rbsp_n = rn;
+    rd_t r = {rbsp, rn * 8, 0, 0};
+
+    /* slice header (7.3.3) with the composed stream's SPS / PPS fields */
+    if (rd_ue(&r) != 0) return OR_SPLICE_ERR_HEADER;             /* first_mb_in_slice */
+    const uint32_t st = rd_ue(&r);
+    if (st != 0 && st != 5) return OR_SPLICE_ERR_HEADER;          /* P */
+    if (rd_ue(&r) != 0) return OR_SPLICE_ERR_HEADER;             /* pic_parameter_set_id */
+    rd_u(&r, c->log2_mfn);                                        /* frame_num */
+    if (c->poc_type == 0) rd_u(&r, c->log2_poc);                  /* pic_order_cnt_lsb */
+    int nrefs = c->num_ref_default_m1 + 1;
+    if (rd_u(&r, 1)) {                                            /* num_ref_idx_active_override */
+        const uint32_t k = rd_ue(&r);
+        if (k > 31) return OR_SPLICE_ERR_HEADER;
+        nrefs = (int)k + 1;
+    }
+    if (rd_u(&r, 1)) return OR_SPLICE_ERR_HEADER;                /* ref_pic_list_modification */
+    if (ref_idc && rd_u(&r, 1)) {                                 /* adaptive_ref_pic_marking */
+        for (int k = 0;; ++k) {
+            const uint32_t op = rd_ue(&r);
+            if (r.bad || k > 64 || op > 6) return OR_SPLICE_ERR_SYNTAX;
+            if (op == 0) break;
+            if (op == 1 || op == 3) rd_ue(&r);
+            if (op == 2) rd_ue(&r);
+            if (op == 3 || op == 6) rd_ue(&r);
+            if (op == 4) rd_ue(&r);
+        }
+    }
+    int qp = 26 + rd_se(&r);                                      /* pic_init_qp 26 + slice_qp_delta */
+    if (qp < 0 || qp > 51) return OR_SPLICE_ERR_HEADER;
+    if (c->deblock && rd_ue(&r) != 1) return OR_SPLICE_ERR_HEADER;
+    if (r.bad) return OR_SPLICE_ERR_SYNTAX;
+
+    /* slice data (7.3.4) */
+    const int W = sp->w, H = sp->h, nmb = W * H;
+    memset(mbs, 0, sizeof(*mbs) * (size_t)nmb);
+    or_mvi *fld = (or_mvi *)calloc((size_t)nmb, sizeof(or_mvi));
+    or_mvi dummy[1] = {{0, 0, -1, 0}};
+    int m = 0, qp_c = 26, err = OR_SPLICE_OK;
+    while (m < nmb && !err) {
+        const uint32_t run = rd_ue(&r);
+        if (r.bad || run > (uint32_t)(nmb - m)) {
+            err = OR_SPLICE_ERR_SYNTAX;
+            break;
+        }
+        for (uint32_t k = 0; k < run; ++k, ++m) {                 /* P_Skip (8.4.1.1) */
+            const int x = m % W, y = m / W;
+            or_mvi A, B, C;
+            or_neighbours(x, y, W, y ? fld + (size_t)(y - 1) * W : dummy, x ? &fld[m - 1] : dummy,
+                          &A, &B, &C);
+            int px, py;
+            or_pskip_motion(x, y, &A, &B, &C, &px, &py);
+            or_splice_mb *mb = &mbs[m];
+            mb->ref = 0;
+            mb->mx = px;
+            mb->my = py;
+            mb->qp = qp;
+            mb->skip = 1;
+            fld[m] = (or_mvi){px, py, 0, 1};
+        }
+        if (m == nmb) break;
+        const int x = m % W, y = m / W;
+        or_splice_mb *mb = &mbs[m];
+        if (rd_ue(&r) != 0) {                                     /* mb_type P_L0_16x16 */
+            err = r.bad ? OR_SPLICE_ERR_SYNTAX : OR_SPLICE_ERR_MBTYPE;
+            break;
+        }
+        int ref = 0;
+        if (nrefs == 2) ref = 1 - (int)rd_u(&r, 1);               /* te() */
+        else if (nrefs > 2) ref = (int)rd_ue(&r);
+        const int dx = rd_se(&r), dy = rd_se(&r);
+        or_mvi A, B, C;
+        or_neighbours(x, y, W, y ? fld + (size_t)(y - 1) * W : dummy, x ? &fld[m - 1] : dummy, &A,
+                      &B, &C);
+        int px, py;
+        or_spec_predict(&A, &B, &C, ref, &px, &py);
+        const long long mx = (long long)px + dx, my = (long long)py + dy;
+        const int cbp = sp_cbp_of_code(rd_ue(&r));
+        if (r.bad || ref >= nrefs || cbp < 0 || mx < -OR_SPLICE_MAX_MV || mx > OR_SPLICE_MAX_MV ||
+            my < -OR_SPLICE_MAX_MV || my > OR_SPLICE_MAX_MV) {
+            err = OR_SPLICE_ERR_SYNTAX;
+            break;
+        }
+        mb->ref = ref;
+        mb->mx = (int)mx;
+        mb->my = (int)my;
+        mb->cbp = cbp;
+        fld[m] = (or_mvi){(int)mx, (int)my, ref, 1};
+        if (cbp) {
+            const int dq = rd_se(&r);                             /* mb_qp_delta */
+            if (dq < -26 || dq > 25) {
+                err = OR_SPLICE_ERR_SYNTAX;
+                break;
+            }
+            qp = (qp + dq + 52) % 52;
+            int d = qp - qp_c;                                    /* composed chain from 26 */
+            if (d < -26) d += 52;
+            if (d > 25) d -= 52;
+            mb->qpd = d;
+            qp_c = qp;
+            if (sp_residual(&r, cbp, mb, x ? mbs[m - 1].tc : NULL, y ? mbs[m - W].tc : NULL)) {
+                err = OR_SPLICE_ERR_SYNTAX;
+                break;
+            }
+        }
+        mb->qp = qp;
+        ++m;
+    }
+    free(fld);
+    if (err) return err;
+    /* rbsp_slice_trailing_bits: stop bit, alignment zeros (zero bytes after
+     * it are tolerated: trailing_zero_8bits of a byte stream) */
+    if (rd_u(&r, 1) != 1) return OR_SPLICE_ERR_SYNTAX;
+    while (r.p & 7)
+        if (rd_u(&r, 1)) return OR_SPLICE_ERR_SYNTAX;
+    while (r.p < r.nbits)
+        if (rd_u(&r, 8)) return OR_SPLICE_ERR_SYNTAX;
+    return r.bad ? OR_SPLICE_ERR_SYNTAX : OR_SPLICE_OK;
+}
+
+/* ------------------------------------------------------------------------ */
+/* composed scroll NAL                                                        */
+/* ------------------------------------------------------------------------ */
+static void sp_copy_bits(or_bits *b, const uint8_t *src, uint32_t off, uint32_t len)
+{
+    rd_t r = {src, (size_t)off + len, off, 0};
+    while (len) {
+        const int k = len > 16 ? 16 : (int)len;
+        or_put(b, rd_u(&r, k), k);
+        len -= (uint32_t)k;
+    }
+}
+
+static void sp_piece(or_bits *b, const or_splice_mb *mb, int i, int nC, const uint8_t *rbsp)
+{
+    uint32_t bits;
+    const int len = or_ct_code(mb->tc[i], mb->t1[i], nC, &bits);
+    or_put(b, bits, len);
+    sp_copy_bits(b, rbsp, mb->boff[i], mb->blen[i]);
+}
+
+size_t or_splice_scroll_nal(uint8_t *dst, size_t cap, or_cfg *c, int off, const or_hint_rect *r,
+                            int n, int mode, const or_splice *sp, int *err)
+{
+    *err = 0;
+    const int mbw = c->w / 16, mbh = c->h / 16, nrefs = 2 + c->nwp;
+    const int has = sp && sp->w > 0 && sp->h > 0;
+    or_splice_mb *mbs = NULL;
+    uint8_t *erb = NULL;
+    if (has) {
+        if (sp->x0 < 0 || sp->y0 < 0 || sp->x0 + sp->w > mbw || sp->y0 + sp->h > mbh) {
+            *err = OR_SPLICE_ERR_HEADER;
+            return 0;
+        }
+        mbs = (or_splice_mb *)malloc(sizeof(*mbs) * (size_t)sp->w * (size_t)sp->h);
+        erb = (uint8_t *)malloc(sp->n + 8);
+        size_t rn;
+        const int e = or_splice_parse(c, sp, mbs, erb, &rn);
+        if (e) {
+            *err = e;
+            free(mbs);
+            free(erb);
+            return 0;
+        }
+    }
+    int a_end, ra, mva, rb, mvb;
+    or_scroll_regions(c, off, &a_end, &ra, &mva, &rb, &mvb);
+    size_t rcap = 64 + (size_t)mbw * mbh * 24 + (has ? sp->n * 2 + (size_t)sp->w * sp->h * 64 : 0);
+    uint8_t *rbsp = (uint8_t *)malloc(rcap);
+    or_mvi *above = (or_mvi *)calloc((size_t)mbw, sizeof(or_mvi));
+    or_mvi *cur = (or_mvi *)calloc((size_t)mbw, sizeof(or_mvi));
+    uint8_t(*tabove)[OR_SPLICE_PIECES] = calloc((size_t)mbw, OR_SPLICE_PIECES);
+    uint8_t(*tcur)[OR_SPLICE_PIECES] = calloc((size_t)mbw, OR_SPLICE_PIECES);
+    or_bits b;
+    or_bits_init(&b, rbsp, rcap);
+    or_scroll_header(&b, c);
+    int run = 0, bad_hint = 0, bad_ref = 0;
+    for (int y = 0; y < mbh; ++y) {
+        or_mvi left = {0, 0, -1, 0};
+        for (int x = 0; x < mbw; ++x) {
+            const or_splice_mb *mb = NULL;
+            if (has && x >= sp->x0 && x < sp->x0 + sp->w && y >= sp->y0 && y < sp->y0 + sp->h)
+                mb = &mbs[(size_t)(y - sp->y0) * sp->w + (x - sp->x0)];
+            int ref, mx, my, cbp = 0;
+            if (mb) {
+                ref = mb->ref;
+                mx = mb->mx;
+                my = mb->my;
+                cbp = mb->cbp;
+                if (!or_ref_valid(c, ref)) bad_ref = 1;
+            } else {
+                if (or_hint_motion(r, n, x, y, a_end, ra, mva, rb, mvb, &ref, &mx, &my) &&
+                    !or_ref_valid(c, ref))
+                    bad_hint = 1;
+                mx *= 4;
+                my *= 4;
+            }
+            int px, py, coded = 1;
+            if (mode == OR_HINT_PSKIP) {
+                or_mvi A, B, C;
+                or_neighbours(x, y, mbw, above, &left, &A, &B, &C);
+                int sx, sy;
+                or_pskip_motion(x, y, &A, &B, &C, &sx, &sy);
+                coded = !(ref == 0 && mx == sx && my == sy && cbp == 0);
+                or_spec_predict(&A, &B, &C, ref, &px, &py);
+            } else {
+                or_predict(x, y, mbw, above, &left, ref, &px, &py);
+            }
+            memset(tcur[x], 0, OR_SPLICE_PIECES);
+            if (coded) {
+                or_ue(&b, (uint32_t)run);                         /* mb_skip_run */
+                run = 0;
+                or_ue(&b, 0);                                     /* P_L0_16x16 */
+                if (nrefs == 2) or_put(&b, (uint32_t)(1 - (ref & 1)), 1);
+                else if (nrefs > 2) or_ue(&b, (uint32_t)ref);
+                or_se(&b, mx - px);
+                or_se(&b, my - py);
+                or_ue(&b, (uint32_t)or_cbp_code(cbp));
+                if (cbp) {
+                    or_se(&b, mb->qpd);
+                    memcpy(tcur[x], mb->tc, OR_SPLICE_PIECES);
+                    const uint8_t *L = x ? tcur[x - 1] : NULL, *T = y ? tabove[x] : NULL;
+                    for (int blk = 0; blk < 16; ++blk)
+                        if (cbp & (1 << (blk >> 2))) {
+                            const int i = sp_blk_raster(blk);
+                            sp_piece(&b, mb, i, sp_piece_nc(i, tcur[x], L, T), erb);
+                        }
+                    if (cbp >> 4) {
+                        sp_piece(&b, mb, 16, -1, erb);
+                        sp_piece(&b, mb, 17, -1, erb);
+                        if ((cbp >> 4) == 2)
+                            for (int i = 18; i < 26; ++i)
+                                sp_piece(&b, mb, i, sp_piece_nc(i, tcur[x], L, T), erb);
+                    }
+                }
+            } else {
+                run++;                                            /* P_Skip */
+            }
+            cur[x] = (or_mvi){mx, my, ref, 1};
+            left = cur[x];
+        }
+        or_mvi *t = above;
+        above = cur;
+        cur = t;
+        uint8_t(*tt)[OR_SPLICE_PIECES] = tabove;
+        tabove = tcur;
+        tcur = tt;
+    }
+    if (run > 0) or_ue(&b, (uint32_t)run);
+    or_trailing(&b);
+    size_t nb = 0;
+    if (bad_ref) {
+        *err = OR_SPLICE_ERR_REF;
+    } else if (bad_hint) {
+        *err = 0x101;
+    } else {
+        nb = or_nal(dst, cap, 0, 1, rbsp, or_bytes(&b));
+        c->frame_num++;
+    }
+    free(rbsp);
+    free(above);
+    free(cur);
+    free(tabove);
+    free(tcur);
+    free(mbs);
+    free(erb);
+    return nb;
+}
+
+size_t or_compose_splice(uint8_t *dst, size_t cap, or_cfg *c, int off, int compose_mode,
+                         const or_hint_rect *r, int n, int mode, const or_splice *sp, int *err)
+{
+    *err = 0;
+    size_t nb = 0;
+    if (or_needs_waypoint(c, off)) {                              /* src/composer.c:255-264 */
+        nb += or_waypoint_nal(dst, cap, c, off);
+        if (compose_mode == 1) return nb;
+    }
+    const size_t k = or_splice_scroll_nal(dst + nb, cap - nb, c, off, r, n, mode, sp, err);
+    return k ? nb + k : 0;
+}
+
+/* ------------------------------------------------------------------------ */
+/* test-input generator                                                       */
+/* ------------------------------------------------------------------------ */
+static uint32_t sp_rng(uint32_t *s)
+{
+    uint32_t x = *s;
+    x ^= x << 13;
+    x ^= x >> 17;
+    x ^= x << 5;
+    return *s = x;
+}
+
+static int sp_level(uint32_t *s, const or_ext_params *p)
+{
+    const int sign = (sp_rng(s) & 1) ? -1 : 1;
+    if ((int)(sp_rng(s) % 1000) < p->big_pm) return sign * (16 + (int)(sp_rng(s) % 2000));
+    if (sp_rng(s) % 3 == 0) return sign * (2 + (int)(sp_rng(s) % 6));
+    return sign;
+}
+
+static void sp_rand_block(uint32_t *s, const or_ext_params *p, int *coef, int maxc)
+{
+    memset(coef, 0, sizeof(int) * (size_t)maxc);
+    const int k = (sp_rng(s) & 3) ? (int)(sp_rng(s) % 4) : (int)(sp_rng(s) % (unsigned)(maxc + 1));
+    for (int i = 0; i < k; ++i) coef[sp_rng(s) % (unsigned)maxc] = sp_level(s, p);
+}
+
+size_t or_ext_slice(uint8_t *dst, size_t cap, const or_cfg *c, int W, int H, uint32_t seed,
+                    const or_ext_params *p)
+{
+    uint32_t s = seed * 2654435761u + 0x9E3779B9u;
+    if (!s) s = 1;
+    const int nmb = W * H, nrefs_def = c->num_ref_default_m1 + 1;
+    const int nrefs = p->nrefs ? p->nrefs : nrefs_def;
+    const size_t rcap = 64 + (size_t)nmb * 8192;
+    uint8_t *rbsp = (uint8_t *)malloc(rcap);
+    or_bits b;
+    or_bits_init(&b, rbsp, rcap);
+    or_ue(&b, 0);                                                 /* first_mb_in_slice */
+    or_ue(&b, 0);                                                 /* P */
+    or_ue(&b, 0);                                                 /* pps id */
+    or_put(&b, 0, c->log2_mfn);
+    if (c->poc_type == 0) or_put(&b, 0, c->log2_poc);
+    if (nrefs != nrefs_def) {
+        or_put(&b, 1, 1);
+        or_ue(&b, (uint32_t)(nrefs - 1));
+    } else {
+        or_put(&b, 0, 1);
+    }
+    or_put(&b, 0, 1);                                             /* no list modification */
+    if (p->ref_idc) or_put(&b, 0, 1);                             /* sliding window */
+    or_se(&b, p->slice_qp_delta);
+    if (c->deblock) or_ue(&b, 1);
+    int qp = 26 + p->slice_qp_delta;
+    or_mvi *fld = (or_mvi *)calloc((size_t)nmb, sizeof(or_mvi));
+    uint8_t(*tcs)[OR_SPLICE_PIECES] = calloc((size_t)nmb, OR_SPLICE_PIECES);
+    or_mvi dummy[1] = {{0, 0, -1, 0}};
+    int run = 0;
+    for (int m = 0; m < nmb; ++m) {
+        const int x = m % W, y = m / W;
+        or_mvi A, B, C;
+        or_neighbours(x, y, W, y ? fld + (size_t)(y - 1) * W : dummy, x ? &fld[m - 1] : dummy, &A,
+                      &B, &C);
+        if (m == p->bad_mb) {
+            or_ue(&b, (uint32_t)run);
+            or_ue(&b, (uint32_t)p->bad_type);
+            or_put(&b, sp_rng(&s), 32);
+            run = 0;
+            break;
+        }
+        if ((int)(sp_rng(&s) % 1000) < p->skip_pm) {
+            int px, py;
+            or_pskip_motion(x, y, &A, &B, &C, &px, &py);
+            fld[m] = (or_mvi){px, py, 0, 1};
+            run++;
+            continue;
+        }
+        int ref = (int)(sp_rng(&s) % (uint32_t)(p->max_ref + 1));
+        if (ref >= nrefs) ref = nrefs - 1;
+        const int rg = p->mv_range;
+        const int mx = rg ? (int)(sp_rng(&s) % (uint32_t)(2 * rg + 1)) - rg : 0;
+        const int my = rg ? (int)(sp_rng(&s) % (uint32_t)(2 * rg + 1)) - rg : 0;
+        int px, py;
+        or_spec_predict(&A, &B, &C, ref, &px, &py);
+        const int cbp = (int)(sp_rng(&s) % 1000) < p->cbp_pm ? 1 + (int)(sp_rng(&s) % 47) : 0;
+        or_ue(&b, (uint32_t)run);
+        run = 0;
+        or_ue(&b, 0);
+        if (nrefs == 2) or_put(&b, (uint32_t)(1 - ref), 1);
+        else if (nrefs > 2) or_ue(&b, (uint32_t)ref);
+        or_se(&b, mx - px);
+        or_se(&b, my - py);
+        or_ue(&b, (uint32_t)or_cbp_code(cbp));
+        if (cbp) {
+            const int j = p->qp_jitter;
+            int nq = qp + (j ? (int)(sp_rng(&s) % (uint32_t)(2 * j + 1)) - j : 0);
+            nq = nq < 0 ? 0 : (nq > 51 ? 51 : nq);
+            or_se(&b, nq - qp);
+            qp = nq;
+            uint8_t *t = tcs[m];
+            const uint8_t *L = x ? tcs[m - 1] : NULL, *T = y ? tcs[m - W] : NULL;
+            int coef[16];
+            for (int blk = 0; blk < 16; ++blk) {
+                if (!(cbp & (1 << (blk >> 2)))) continue;
+                const int i = sp_blk_raster(blk);
+                sp_rand_block(&s, p, coef, 16);
+                t[i] = (uint8_t)or_cavlc_block(&b, coef, 16, sp_piece_nc(i, t, L, T));
+            }
+            if (cbp >> 4) {
+                for (int i = 16; i < 18; ++i) {
+                    sp_rand_block(&s, p, coef, 4);
+                    or_cavlc_block(&b, coef, 4, -1);
+                }
+                if ((cbp >> 4) == 2)
+                    for (int i = 18; i < 26; ++i) {
+                        sp_rand_block(&s, p, coef, 15);
+                        t[i] = (uint8_t)or_cavlc_block(&b, coef, 15, sp_piece_nc(i, t, L, T));
+                    }
+            }
+        }
+        fld[m] = (or_mvi){mx, my, ref, 1};
+    }
+    if (run > 0) or_ue(&b, (uint32_t)run);
+    or_trailing(&b);
+    const size_t nb = or_nal(dst, cap, p->ref_idc, 1, rbsp, or_bytes(&b));
+    free(rbsp);
+    free(fld);
+    free(tcs);
+    return nb;
+}

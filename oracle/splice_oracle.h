@@ -1,0 +1,118 @@
+/*
+ * splice_oracle.h -- CPU ORACLE (test infrastructure only): the pre-encoded
+ * MB splice.  Used only by tests/ as the checker of
+ * k_splice_parse / k_splice_stage; the product library never links it.
+ *
+ * The reference designs this step but never implements it
+ * (docs/MASTER_DESIGN.md:39-40 "splice the resulting encoded macroblocks into
+ * the final frame", :142-146 "take the corresponding encoded macroblock
+ * payload from the dynamic encoder output", :171 "encode in its own
+ * coordinate system and transplant macroblock payloads while rewriting
+ * addresses").  This file DEFINES that transplant ("parity unpinned",
+ * DESIGN.md §10); tests/h264_pslice.py decodes both the external slice and
+ * the composed NAL from the standard and checks that every spliced MB
+ * decodes to the same (ref, mv, cbp, QP, coefficient levels).
+ *
+ * Input: one external P slice NAL (nal_unit_type 1, CAVLC) coded for a
+ * picture of w x h MBs with the composed stream's SPS/PPS fields
+ * (log2_max_frame_num, POC type, num_ref_idx default, deblocking flag); the
+ * rect [x0, x0 + w) x [y0, y0 + h) of the composed picture receives its MBs.
+ * Supported: first_mb_in_slice 0, no ref_pic_list_modification, no
+ * deblocking when the PPS allows switching it off (disable_deblocking_filter
+ * _idc 1, like the composer's own slices), MBs P_L0_16x16 or P_Skip, any
+ * coded_block_pattern, mb_qp_delta and CAVLC residual (level_prefix <= 15).
+ * Its ref_idx values index the composed stream's list (0 = A, 1 = B, 2 + i =
+ * waypoint i) and its motion vectors are displacements in composed-picture
+ * coordinates.
+ *
+ * Transplant, per spliced MB (composed slice QP 26):
+ *   - P_Skip becomes P_L0_16x16 with ref 0 and its P_Skip motion (8.4.1.1,
+ *     evaluated in the external picture), cbp 0;
+ *   - mb_skip_run, ref_idx te() (composed num_ref_idx = 2 + waypoints) and
+ *     mvd (prediction in the composed picture: the reference's
+ *     get_mv_prediction in EXACT mode, 8.4.1.3 in PSKIP mode) are re-coded;
+ *   - mb_qp_delta is rebased so each MB keeps its external QP;
+ *   - every residual block keeps its bits after coeff_token verbatim (they do
+ *     not depend on nC); coeff_token is re-coded for the nC of the composed
+ *     picture (rect-edge neighbours are available MBs with TotalCoeff 0).
+ * MBs outside the rect follow the UI-hint composition (hint_oracle.h) of
+ * the frame, whose neighbour predictions now see the spliced motion.
+ */
+#ifndef SPLICE_ORACLE_H
+#define SPLICE_ORACLE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "hint_oracle.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* error codes (same values as SCROLL_SPLICE_ERR_* in include/composer_batch.h) */
+#define OR_SPLICE_OK 0
+#define OR_SPLICE_ERR_NAL 1      /* not a coded slice of a non-IDR picture        */
+#define OR_SPLICE_ERR_HEADER 2   /* slice header outside the supported syntax     */
+#define OR_SPLICE_ERR_MBTYPE 3   /* an MB other than P_L0_16x16 / P_Skip          */
+#define OR_SPLICE_ERR_SYNTAX 4   /* malformed / truncated slice data              */
+#define OR_SPLICE_ERR_REF 5      /* ref_idx not a valid reference of the frame    */
+
+#define OR_SPLICE_PIECES 26      /* 16 luma (raster), Cb DC, Cr DC, 4 Cb AC, 4 Cr AC */
+#define OR_SPLICE_MAX_MV 16383   /* |mv| in quarter pels */
+
+typedef struct {
+    int x0, y0, w, h;            /* MB units in the composed picture */
+    const uint8_t *nal;          /* the external NAL (leading Annex-B start code optional) */
+    size_t n;
+} or_splice;
+
+/* one external MB after parsing */
+typedef struct {
+    int ref, mx, my;             /* quarter pels                             */
+    int cbp, qp, qpd;            /* its QP and the composed mb_qp_delta      */
+    int skip;                    /* P_Skip in the external slice             */
+    uint8_t tc[OR_SPLICE_PIECES], t1[OR_SPLICE_PIECES];
+    uint32_t boff[OR_SPLICE_PIECES], blen[OR_SPLICE_PIECES];  /* body bits in the RBSP */
+} or_splice_mb;
+
+/* Parse the external slice: mbs[w * h] (raster), its RBSP into rbsp (cap
+ * >= n bytes), *rbsp_n = its bytes.  Returns OR_SPLICE_OK or an error. */
+int or_splice_parse(const or_cfg *c, const or_splice *sp, or_splice_mb *mbs, uint8_t *rbsp,
+                    size_t *rbsp_n);
+
+/* The scroll NAL of a frame at offset `off` with hint rects r[0..n) in
+ * `mode` (OR_HINT_EXACT / OR_HINT_PSKIP) and the splice sp (NULL = none);
+ * frame_num++.  Returns the Annex-B bytes, or 0 with *err = OR_SPLICE_ERR_*
+ * (or 1 + 0x100 for an invalid hint-rect reference); the state is then left
+ * unchanged. */
+size_t or_splice_scroll_nal(uint8_t *dst, size_t cap, or_cfg *c, int off, const or_hint_rect *r,
+                            int n, int mode, const or_splice *sp, int *err);
+
+/* composer_write_scroll_frame (src/composer.c:255-264) with that scroll NAL */
+size_t or_compose_splice(uint8_t *dst, size_t cap, or_cfg *c, int off, int compose_mode,
+                         const or_hint_rect *r, int n, int mode, const or_splice *sp, int *err);
+
+/* ---- test-input generator: a stand-in "dynamic encoder" (MASTER_DESIGN
+ * §4.2) writing standard CAVLC P slices of a w x h MB picture with random
+ * MBs, so the tests have external slices to splice ---- */
+typedef struct {
+    int nrefs;                   /* num_ref_idx_l0_active; 0 = the PPS default   */
+    int max_ref;                 /* MB refs drawn from [0, max_ref]             */
+    int skip_pm;                 /* per mille: MB coded as P_Skip              */
+    int cbp_pm;                  /* per mille: MB with a residual              */
+    int big_pm;                  /* per mille: level drawn large (escape codes) */
+    int mv_range;                /* |mv| <= mv_range quarter pels               */
+    int slice_qp_delta;
+    int qp_jitter;               /* |mb_qp_delta| <= qp_jitter                  */
+    int ref_idc;                 /* nal_ref_idc (adds dec_ref_pic_marking)      */
+    int bad_mb;                  /* -1, or the MB coded with mb_type bad_type   */
+    int bad_type;
+} or_ext_params;
+size_t or_ext_slice(uint8_t *dst, size_t cap, const or_cfg *c, int w, int h, uint32_t seed,
+                    const or_ext_params *p);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

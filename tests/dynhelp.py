@@ -119,3 +119,36 @@ def ipcm_file(oracle, w, h, pic):
     src = (ctypes.c_uint8 * len(pic)).from_buffer_copy(pic)
     n = oracle.or_ipcm_picture_file(buf, cap, w, h, src)
     return bytes(buf[:n])
+
+
+# ---------------------------------------------------- splice (splice_oracle.h)
+class Splice(ctypes.Structure):
+    _fields_ = [("x0", ctypes.c_int), ("y0", ctypes.c_int), ("w", ctypes.c_int),
+                ("h", ctypes.c_int), ("nal", ctypes.c_void_p), ("n", ctypes.c_size_t)]
+
+
+class ExtParams(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int) for n in
+                ("nrefs", "max_ref", "skip_pm", "cbp_pm", "big_pm", "mv_range",
+                 "slice_qp_delta", "qp_jitter", "ref_idc", "bad_mb", "bad_type")]
+
+
+EXT_DEFAULT = dict(nrefs=0, max_ref=1, skip_pm=250, cbp_pm=600, big_pm=20, mv_range=64,
+                   slice_qp_delta=0, qp_jitter=3, ref_idc=0, bad_mb=-1, bad_type=0)
+
+
+def ext_slice(oracle, cfg, w, h, seed, **kw):
+    """a standard P slice of a w x h MB picture from the oracle's stand-in
+    dynamic encoder (or_ext_slice), as Annex-B bytes"""
+    p = ExtParams(**{**EXT_DEFAULT, **kw})
+    cap = 4096 + w * h * 4096
+    buf = (ctypes.c_uint8 * cap)()
+    n = oracle.or_ext_slice(buf, cap, ctypes.byref(cfg), w, h, seed, ctypes.byref(p))
+    return bytes(buf[:n])
+
+
+def splice_of(x0, y0, w, h, nal):
+    buf = ctypes.create_string_buffer(bytes(nal), max(1, len(nal)))
+    sp = Splice(x0, y0, w, h, ctypes.cast(buf, ctypes.c_void_p), len(nal))
+    sp._buf, sp.data = buf, bytes(nal)       # keep the bytes alive with the struct
+    return sp

@@ -515,3 +515,126 @@ def decode_mv_field(nal, w, h, predictor="spec", **hdr_kw):
         assert b.u(1) == 0
     assert b.p == 8 * len(data), (b.p, 8 * len(data))
     return H, field, nskip
+
+
+# ------------------------------------------- general P slice (splice) --------
+# Any CAVLC P slice of P_L0_16x16 / P_Skip MBs: mb_skip_run, motion with the
+# chosen predictor, coded_block_pattern, mb_qp_delta (QP chain from the slice
+# QP) and the residual levels.  Used to check that a spliced MB of a composed
+# NAL decodes to the same syntax elements as in its external slice.
+
+def _nc(nA, nB):
+    if nA >= 0 and nB >= 0:
+        return (nA + nB + 1) >> 1
+    return nA if nA >= 0 else (nB if nB >= 0 else 0)
+
+
+def decode_p_slice(nal, w, h, predictor="spec", log2_mfn=4, poc_type=2, log2_poc=4, deblock=1,
+                   nrefs_default=2):
+    """-> (header, mbs[y][x] = dict(ref, mx, my, skip, cbp, qp, luma, cdc, cac))
+
+    nal: Annex-B NAL (start code optional).  Unavailable neighbours are the
+    picture edges only (one slice per picture)."""
+    if nal[:4] == b"\x00\x00\x00\x01":
+        nal = nal[4:]
+    elif nal[:3] == b"\x00\x00\x01":
+        nal = nal[3:]
+    ref_idc, nut = nal[0] >> 5, nal[0] & 31
+    assert nut == 1, "coded slice of a non-IDR picture"
+    b = Bits(ebsp_to_rbsp(nal[1:]))
+    H = {"first_mb": b.ue(), "slice_type": b.ue(), "pps": b.ue(), "frame_num": b.u(log2_mfn)}
+    if poc_type == 0:
+        H["poc"] = b.u(log2_poc)
+    nrefs = nrefs_default
+    if b.u(1):
+        nrefs = b.ue() + 1
+    H["nrefs"] = nrefs
+    H["list_mod"] = b.u(1)
+    if H["list_mod"]:                            # ref_pic_list_modification (waypoints)
+        while True:
+            idc = b.ue()
+            if idc == 3:
+                break
+            b.ue()
+    if ref_idc and b.u(1):
+        while True:
+            op = b.ue()
+            if op == 0:
+                break
+            if op in (1, 3):
+                b.ue()
+            if op in (2, 3, 6):
+                b.ue()
+            if op == 4:
+                b.ue()
+    qp = 26 + b.se()
+    H["qp"] = qp
+    if deblock:
+        H["deblock_idc"] = b.ue()
+        if H["deblock_idc"] != 1:
+            b.se(); b.se()
+    pred = mvp_spec if predictor == "spec" else mvp_ref
+    mbw, mbh = w // 16, h // 16
+    field = [[None] * mbw for _ in range(mbh)]
+    mbs = [[None] * mbw for _ in range(mbh)]
+    tcs = [[None] * mbw for _ in range(mbh)]
+    m, nmb = 0, mbw * mbh
+    while m < nmb:
+        run = b.ue()
+        for _ in range(run):
+            y, x = divmod(m, mbw)
+            assert y < mbh, "mb_skip_run past the picture"
+            mv = pskip_mv(*_neigh(field, x, y, mbw))
+            field[y][x] = (0,) + mv
+            tcs[y][x] = [0] * 24
+            mbs[y][x] = dict(ref=0, mx=mv[0], my=mv[1], skip=True, cbp=0, qp=qp,
+                             luma=[[0] * 16 for _ in range(16)], cdc=[[0] * 4] * 2,
+                             cac=[[[0] * 15 for _ in range(4)] for _ in range(2)])
+            m += 1
+        if m >= nmb:
+            break
+        y, x = divmod(m, mbw)
+        assert b.ue() == 0, "mb_type P_L0_16x16"
+        ref = (1 - b.u(1)) if nrefs == 2 else (b.ue() if nrefs > 2 else 0)
+        dx, dy = b.se(), b.se()
+        px, py = pred(*_neigh(field, x, y, mbw), ref)
+        field[y][x] = (ref, px + dx, py + dy)
+        cbp = GOLOMB_TO_INTER_CBP[b.ue()]
+        t = [0] * 24
+        luma = [[0] * 16 for _ in range(16)]
+        cdc = [[0] * 4 for _ in range(2)]
+        cac = [[[0] * 15 for _ in range(4)] for _ in range(2)]
+        left = tcs[y][x - 1] if x > 0 else None
+        top = tcs[y - 1][x] if y > 0 else None
+        if cbp:
+            qp = (qp + b.se() + 52) % 52
+            for blk in range(16):
+                q8, q4 = divmod(blk, 4)
+                bx, by = (q8 % 2) * 2 + q4 % 2, (q8 // 2) * 2 + q4 // 2
+                r = 4 * by + bx
+                if not cbp & (1 << q8):
+                    continue
+                nA = t[r - 1] if bx > 0 else (left[r + 3] if left else -1)
+                nB = t[r - 4] if by > 0 else (top[r + 12] if top else -1)
+                luma[r], t[r] = cavlc_block(b, _nc(nA, nB), 16)
+            if cbp >> 4:
+                for p in range(2):
+                    cdc[p], _ = cavlc_block(b, -1, 4)
+                if (cbp >> 4) == 2:
+                    for p in range(2):
+                        for k in range(4):
+                            bx, by = k % 2, k // 2
+                            i = 16 + 4 * p + k
+                            nA = t[i - 1] if bx > 0 else (left[i + 1] if left else -1)
+                            nB = t[i - 2] if by > 0 else (top[i + 2] if top else -1)
+                            cac[p][k], t[i] = cavlc_block(b, _nc(nA, nB), 15)
+        tcs[y][x] = t
+        mbs[y][x] = dict(ref=ref, mx=px + dx, my=py + dy, skip=False, cbp=cbp, qp=qp, luma=luma,
+                         cdc=cdc, cac=cac)
+        m += 1
+    assert b.u(1) == 1, "stop bit"
+    while b.p & 7:
+        assert b.u(1) == 0
+    while b.p < 8 * len(b.d):
+        assert b.u(8) == 0, "trailing bytes"
+    return H, mbs

@@ -1,0 +1,243 @@
+"""GPU parity of the pre-encoded MB splice:
+k_plan (state) -> k_splice_parse -> k_hint_stage / k_splice_stage ->
+k_plan (size) -> k_emit -> k_dyn_emit_gather / k_dyn_emit, through the C ABI,
+against the CPU restatement oracle/splice_oracle.c (or_compose_splice) byte
+for byte.  tests/test_splice_oracle.py pins the restatement by decoding the
+composed NALs from the standard.  External slices come from the oracle's
+stand-in encoder (or_ext_slice).  Run on an MI355X: -m gpu."""
+import ctypes
+import random
+
+import numpy as np
+import pytest
+
+from conftest import synthetic_offsets
+from dynhelp import OrCfg, hint_array, random_hints, split_nals, ext_slice, splice_of
+
+pytestmark = pytest.mark.gpu
+
+EXACT, PSKIP = 0, 1
+
+
+@pytest.fixture(scope="module")
+def gpu(scroll):
+    if scroll.device_count() < 1:
+        pytest.fail("no gfx950 device: " + scroll.last_error())
+    return scroll
+
+
+def _cfg(oracle, w, h):
+    c = OrCfg()
+    oracle.or_cfg_init(ctypes.byref(c), w, h)
+    c.frame_num = 2
+    return c
+
+
+def plan(oracle, w, h, offsets, seed, p_splice=0.7, p_hint=0.3, modes=(EXACT, PSKIP),
+         max_rect=(10, 8), compose_mode=0, ext_kw=None):
+    """random splices (+ hints) per (stream, frame) whose refs are valid in
+    that frame; -> (frames dict, oracle bytes per stream)"""
+    rng = random.Random(seed)
+    S, F = offsets.shape
+    mbw, mbh = w // 16, h // 16
+    buf = (ctypes.c_uint8 * (16 << 20))()
+    err = ctypes.c_int()
+    frames, outs = {}, []
+    for s in range(S):
+        c = _cfg(oracle, w, h)
+        o = bytearray()
+        for t in range(F):
+            refs = [0, 1] + [2 + i for i in range(c.nwp) if c.wp_valid[i]]
+            rects = random_hints(rng, mbw, mbh, refs, 3) if rng.random() < p_hint else []
+            mode = rng.choice(modes)
+            sp = None
+            if rng.random() < p_splice:
+                sw, sh = rng.randint(1, min(max_rect[0], mbw)), rng.randint(1, min(max_rect[1], mbh))
+                x0, y0 = rng.randint(0, mbw - sw), rng.randint(0, mbh - sh)
+                kw = dict(nrefs=len(refs), max_ref=len(refs) - 1,
+                          skip_pm=rng.choice([0, 200, 600]), cbp_pm=rng.choice([300, 800, 1000]),
+                          big_pm=rng.choice([0, 30]), mv_range=rng.choice([8, 200]),
+                          slice_qp_delta=rng.randint(-4, 4), qp_jitter=rng.choice([0, 3]),
+                          ref_idc=rng.choice([0, 1]))
+                kw.update(ext_kw or {})
+                sp = (x0, y0, sw, sh, ext_slice(oracle, c, sw, sh, seed * 100003 + s * 1009 + t, **kw))
+            frames[(s, t)] = (rects, mode, sp)
+            arr, n = hint_array(rects)
+            spc = splice_of(*sp) if sp else None
+            k = oracle.or_compose_splice(buf, len(buf), ctypes.byref(c), int(offsets[s, t]),
+                                         compose_mode, arr, n, mode,
+                                         ctypes.byref(spc) if spc else None, ctypes.byref(err))
+            assert err.value == 0 and k > 0, (s, t, err.value)
+            o += bytes(buf[:k])
+        outs.append(bytes(o))
+    return frames, outs
+
+
+def gpu_streams(gpu, w, h, offsets, frames, compose_mode=0, arena=16 << 20, debug=0):
+    S, F = offsets.shape
+    b = gpu.Batch(S, F, arena, mode=compose_mode)
+    for _ in range(S):
+        b.add_stream(gpu.make_config(w, h))
+    if debug:
+        b.set_debug(debug)
+    for (s, f), (rects, mode, sp) in frames.items():
+        if rects or mode != EXACT:
+            b.set_hints(s, f, rects, mode)
+        if sp:
+            b.set_splice(s, f, *sp)
+    b.set_offsets(offsets)
+    b.compose(F)
+    return b, b.sync()
+
+
+def check_equal(b, want, streams=None):
+    for s in (streams if streams is not None else range(len(want))):
+        got, ws = b.output(s), want[s]
+        if got != ws:
+            gn, wn = split_nals(got), split_nals(ws)
+            bad = next((i for i, (x, y) in enumerate(zip(gn, wn)) if x != y), min(len(gn), len(wn)))
+            raise AssertionError(f"stream {s}: {len(got)} vs {len(ws)} bytes, {len(gn)} vs "
+                                 f"{len(wn)} NALs, first differing NAL {bad}")
+
+
+@pytest.mark.parametrize("w,h,seed", [(320, 256, 1), (640, 480, 2), (1280, 720, 3)])
+def test_random_splices(gpu, oracle, w, h, seed):
+    offs = synthetic_offsets(5, 16, h, first_stream=seed)
+    offs[1] = np.clip(np.arange(484, 500), 0, h)       # waypoints: refs 2 + i appear
+    frames, want = plan(oracle, w, h, offs, seed)
+    b, rc = gpu_streams(gpu, w, h, offs, frames)
+    assert rc == 0, gpu.last_error()
+    check_equal(b, want)
+    for (s, f), (_, _, sp) in frames.items():
+        assert b.splice_status(s, f) == 0
+    b.close()
+
+
+def test_large_rect_4k_and_ep_path(gpu, oracle, scroll):
+    """3840x2160, up to 25x25 MB splices with large levels; again with the
+    dynamic emit's EP list capped at 4 (every NAL through k_dyn_emit)"""
+    w, h = 3840, 2160
+    offs = np.array([[490, 496, 500, 992], [1984, 1990, 2000, 700]], np.int32)
+    frames, want = plan(oracle, w, h, offs, 11, p_splice=1.0, max_rect=(25, 25),
+                        ext_kw=dict(cbp_pm=1000, big_pm=100, mv_range=2000))
+    for debug in (0, scroll.SCROLL_DEBUG_DYN_EPCAP4):
+        b, rc = gpu_streams(gpu, w, h, offs, frames, arena=64 << 20, debug=debug)
+        assert rc == 0, gpu.last_error()
+        check_equal(b, want)
+        b.close()
+
+
+def test_whole_picture_and_corner_splices(gpu, oracle):
+    w, h = 192, 128
+    mbw, mbh = w // 16, h // 16
+    offs = np.array([[40, 41, 42, 43, 44, 45]], np.int32)
+    c = _cfg(oracle, w, h)
+    rects = [(0, 0, mbw, mbh), (mbw - 3, 0, 3, 3), (0, mbh - 2, 4, 2), (mbw - 2, mbh - 2, 2, 2),
+             (5, 3, 1, 1), (0, 0, 1, mbh)]
+    frames = {}
+    buf = (ctypes.c_uint8 * (4 << 20))()
+    err = ctypes.c_int()
+    o = bytearray()
+    for t, (x0, y0, sw, sh) in enumerate(rects):
+        mode = PSKIP if t % 2 else EXACT
+        sp = (x0, y0, sw, sh, ext_slice(oracle, c, sw, sh, 500 + t, cbp_pm=900, skip_pm=300))
+        frames[(0, t)] = ([], mode, sp)
+        k = oracle.or_compose_splice(buf, len(buf), ctypes.byref(c), int(offs[0, t]), 0, None, 0,
+                                     mode, ctypes.byref(splice_of(*sp)), ctypes.byref(err))
+        assert err.value == 0
+        o += bytes(buf[:k])
+    b, rc = gpu_streams(gpu, w, h, offs, frames)
+    assert rc == 0, gpu.last_error()
+    check_equal(b, [bytes(o)])
+    b.close()
+
+
+def test_experiment_mode(gpu, oracle):
+    w, h = 640, 480
+    offs = synthetic_offsets(3, 20, h, first_stream=4)
+    offs[2] = np.arange(480, 500)
+    frames, want = plan(oracle, w, h, offs, 21, compose_mode=1)
+    b, rc = gpu_streams(gpu, w, h, offs, frames, compose_mode=1)
+    assert rc == 0, gpu.last_error()
+    check_equal(b, want)
+    b.close()
+
+
+def test_errors_fail_only_their_stream(gpu, oracle, scroll):
+    w, h = 256, 256
+    offs = synthetic_offsets(5, 6, h)
+    c = _cfg(oracle, w, h)
+    good = ext_slice(oracle, c, 4, 3, 1)
+    cases = {
+        0: (scroll.SCROLL_SPLICE_ERR_MBTYPE, ext_slice(oracle, c, 4, 3, 1, bad_mb=5, bad_type=3)),
+        1: (scroll.SCROLL_SPLICE_ERR_NAL, good[:4] + bytes([0x65]) + good[5:]),
+        2: (scroll.SCROLL_SPLICE_ERR_SYNTAX, good[:len(good) // 2]),
+        3: (scroll.SCROLL_SPLICE_ERR_REF, ext_slice(oracle, c, 4, 3, 2, nrefs=4, max_ref=3,
+                                                    skip_pm=0)),
+    }
+    b = gpu.Batch(5, 6, 8 << 20)
+    for _ in range(5):
+        b.add_stream(gpu.make_config(w, h))
+    for s, (_, nal) in cases.items():
+        b.set_splice(s, 2, 2, 2, 4, 3, nal)
+    b.set_splice(4, 1, 2, 2, 4, 3, good)
+    b.set_offsets(offs)
+    b.compose(6)
+    assert b.sync() == scroll.SCROLL_ERR_CONFIG
+    assert "splice" in gpu.last_error()
+    for s, (code, _) in cases.items():
+        assert b.splice_status(s, 2) == code, s
+        assert b.output_size(s) == 0, s                     # nothing committed
+    buf = (ctypes.c_uint8 * (1 << 20))()
+    err = ctypes.c_int()
+    c4 = _cfg(oracle, w, h)
+    o = bytearray()
+    for t in range(6):
+        sp = splice_of(2, 2, 4, 3, good) if t == 1 else None
+        k = oracle.or_compose_splice(buf, len(buf), ctypes.byref(c4), int(offs[4, t]), 0, None, 0,
+                                     EXACT, ctypes.byref(sp) if sp else None, ctypes.byref(err))
+        o += bytes(buf[:k])
+    assert b.output(4) == bytes(o)
+    b.close()
+
+
+def test_persist_remove_and_clear(gpu, oracle):
+    """splices persist across composes; removing one / clearing all returns
+    those frames to plain scroll frames"""
+    w, h = 512, 512
+    offs = synthetic_offsets(2, 30, h, first_stream=7)
+    F1 = 10
+    c = _cfg(oracle, w, h)
+    sps = {f: (f % 5, f % 7, 3 + f % 4, 2 + f % 3, ext_slice(oracle, c, 3 + f % 4, 2 + f % 3, 900 + f))
+           for f in range(F1)}
+    b = gpu.Batch(2, F1, 8 << 20)
+    for _ in range(2):
+        b.add_stream(gpu.make_config(w, h))
+    for s in range(2):
+        for f in range(F1):
+            b.set_splice(s, f, *sps[f])
+    b.set_splice(1, 3, 0, 0, 0, 0, b"")                  # removed again
+    buf = (ctypes.c_uint8 * (4 << 20))()
+    err = ctypes.c_int()
+    want = []
+    for s in range(2):
+        cs = _cfg(oracle, w, h)
+        o = bytearray()
+        for t in range(30):
+            f = t % F1
+            sp = splice_of(*sps[f]) if t < 20 and not (s == 1 and f == 3) else None
+            k = oracle.or_compose_splice(buf, len(buf), ctypes.byref(cs), int(offs[s, t]), 0, None,
+                                         0, EXACT, ctypes.byref(sp) if sp else None,
+                                         ctypes.byref(err))
+            assert err.value == 0
+            o += bytes(buf[:k])
+        want.append(bytes(o))
+    for c0 in (0, 10, 20):
+        if c0 == 20:
+            b.clear_splices()
+        b.set_offsets(np.ascontiguousarray(offs[:, c0:c0 + F1]))
+        b.compose(F1)
+        assert b.sync() == 0, gpu.last_error()
+    for s in range(2):
+        assert b.output(s) == want[s], s
+    b.close()

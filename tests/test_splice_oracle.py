@@ -1,0 +1,208 @@
+"""The pre-encoded MB splice restatement (oracle/splice_oracle.c), CPU only.
+
+The reference designs the splice (docs/MASTER_DESIGN.md:39-40,142-146,171)
+but has no implementation, so the oracle DEFINES the bits ("parity
+unpinned").  What pins it:
+  (1) the external slices the stand-in encoder writes decode with the
+      test-only standard decoder (tests/h264_pslice.py, written from the
+      standard and independent of the oracle's tables) to the same motion,
+      cbp and QP the oracle's parse reports;
+  (2) a composed NAL decodes (the reference's predictor for EXACT, the
+      standard's for PSKIP) so that every spliced MB has the external MB's
+      ref, mv, cbp, QP and coefficient levels, and every other MB the
+      UI-hint field of its frame;
+  (3) without a splice the composed NAL equals the UI-hint NAL (itself equal
+      to the reference's scroll frame without hints);
+  (4) unsupported or malformed slices and invalid references are errors.
+"""
+import ctypes
+import random
+
+from dynhelp import OrCfg, hint_array, random_hints, ext_slice, splice_of, Splice
+import h264_pslice as P
+
+EXACT, PSKIP = 0, 1
+ERR_NAL, ERR_HEADER, ERR_MBTYPE, ERR_SYNTAX, ERR_REF = 1, 2, 3, 4, 5
+
+
+class SpliceMb(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int) for n in ("ref", "mx", "my", "cbp", "qp", "qpd", "skip")] + [
+        ("tc", ctypes.c_uint8 * 26), ("t1", ctypes.c_uint8 * 26),
+        ("boff", ctypes.c_uint32 * 26), ("blen", ctypes.c_uint32 * 26)]
+
+
+def _cfg(oracle, w, h):
+    c = OrCfg()
+    oracle.or_cfg_init(ctypes.byref(c), w, h)
+    return c
+
+
+def _refs(c):
+    return [0, 1] + [2 + i for i in range(c.nwp) if c.wp_valid[i]]
+
+
+def _parse(oracle, c, sp):
+    mbs = (SpliceMb * (sp.w * sp.h))()
+    rb = (ctypes.c_uint8 * (sp.n + 8))()
+    rn = ctypes.c_size_t()
+    e = oracle.or_splice_parse(ctypes.byref(c), ctypes.byref(sp), mbs, rb, ctypes.byref(rn))
+    return e, mbs
+
+
+def _field(oracle, c, off, rects):
+    mbw, mbh = c.w // 16, c.h // 16
+    arr, n = hint_array(rects)
+    out = (ctypes.c_int32 * (3 * mbw * mbh))()
+    assert oracle.or_hint_field(ctypes.byref(c), off, arr, n, out) == 0
+    return [[(out[3 * (y * mbw + x)], 4 * out[3 * (y * mbw + x) + 1], 4 * out[3 * (y * mbw + x) + 2])
+             for x in range(mbw)] for y in range(mbh)]
+
+
+def test_ext_slices_parse_like_the_standard_decoder(oracle):
+    c = _cfg(oracle, 640, 368)
+    for seed, kw in enumerate([{}, dict(nrefs=1, max_ref=0), dict(nrefs=5, max_ref=4),
+                               dict(skip_pm=900), dict(cbp_pm=1000, big_pm=300),
+                               dict(slice_qp_delta=-7, qp_jitter=12), dict(ref_idc=2),
+                               dict(mv_range=4000)]):
+        w, h = 5 + seed % 3, 4 + seed % 4
+        nal = ext_slice(oracle, c, w, h, 100 + seed, **kw)
+        e, mbs = _parse(oracle, c, splice_of(0, 0, w, h, nal))
+        assert e == 0, (seed, kw)
+        H, dec = P.decode_p_slice(nal, 16 * w, 16 * h, "spec")
+        for y in range(h):
+            for x in range(w):
+                d, m = dec[y][x], mbs[y * w + x]
+                assert (m.ref, m.mx, m.my, m.cbp, bool(m.skip)) == \
+                    (d["ref"], d["mx"], d["my"], d["cbp"], d["skip"]), (seed, x, y)
+                if m.cbp:
+                    assert m.qp == d["qp"]
+
+
+def _check_frame(oracle, c, off, rects, mode, sp, buf):
+    """compose, decode, compare; returns the NAL"""
+    err = ctypes.c_int()
+    c2 = OrCfg.from_buffer_copy(c)
+    arr, n = hint_array(rects)
+    k = oracle.or_splice_scroll_nal(buf, len(buf), ctypes.byref(c2), off, arr, n, mode,
+                                    ctypes.byref(sp), ctypes.byref(err))
+    assert err.value == 0 and k > 0
+    nal = bytes(buf[:k])
+    field = _field(oracle, c, off, rects)
+    ext_nal = sp.data
+    _, ext = P.decode_p_slice(ext_nal, 16 * sp.w, 16 * sp.h, "spec")
+    H, got = P.decode_p_slice(nal, c.w, c.h, "ref" if mode == EXACT else "spec")
+    assert H["nrefs"] == 2 + c.nwp and H["qp"] == 26
+    for y in range(c.h // 16):
+        for x in range(c.w // 16):
+            g = got[y][x]
+            if sp.x0 <= x < sp.x0 + sp.w and sp.y0 <= y < sp.y0 + sp.h:
+                e = ext[y - sp.y0][x - sp.x0]
+                assert (g["ref"], g["mx"], g["my"], g["cbp"]) == (e["ref"], e["mx"], e["my"], e["cbp"]), \
+                    (off, mode, x, y)
+                if e["cbp"]:
+                    assert g["qp"] == e["qp"]
+                    assert (g["luma"], g["cdc"], g["cac"]) == (e["luma"], e["cdc"], e["cac"])
+            else:
+                assert (g["ref"], g["mx"], g["my"]) == field[y][x] and g["cbp"] == 0, (off, mode, x, y)
+    return nal
+
+
+def test_spliced_mbs_decode_to_the_external_mbs(oracle):
+    rng = random.Random(5)
+    buf = (ctypes.c_uint8 * (1 << 20))()
+    err = ctypes.c_int()
+    w, h = 320, 256
+    c = _cfg(oracle, w, h)
+    for i in range(24):
+        off = oracle.or_synthetic_offset(3, i, h)
+        if oracle.or_needs_waypoint(ctypes.byref(c), off):
+            oracle.or_waypoint_nal(buf, len(buf), ctypes.byref(c), off)
+        refs = _refs(c)
+        sw, sh = rng.randint(1, 8), rng.randint(1, 6)
+        x0, y0 = rng.randint(0, w // 16 - sw), rng.randint(0, h // 16 - sh)
+        kw = dict(nrefs=len(refs), max_ref=len(refs) - 1, skip_pm=rng.choice([0, 200, 700]),
+                  cbp_pm=rng.choice([0, 500, 1000]), big_pm=rng.choice([0, 50]),
+                  mv_range=rng.choice([8, 300]), slice_qp_delta=rng.randint(-5, 5),
+                  qp_jitter=rng.choice([0, 4]), ref_idc=rng.choice([0, 1]))
+        nal = ext_slice(oracle, c, sw, sh, 1000 + i, **kw)
+        sp = splice_of(x0, y0, sw, sh, nal)
+        rects = random_hints(rng, w // 16, h // 16, refs, nmax=3) if i % 3 == 0 else []
+        for mode in (EXACT, PSKIP):
+            _check_frame(oracle, c, off, rects, mode, sp, buf)
+        k = oracle.or_splice_scroll_nal(buf, len(buf), ctypes.byref(c), off, None, 0, EXACT,
+                                        ctypes.byref(sp), ctypes.byref(err))
+        assert k > 0
+
+
+def test_splice_at_picture_corners_and_whole_picture(oracle):
+    buf = (ctypes.c_uint8 * (1 << 20))()
+    w, h = 192, 128
+    c = _cfg(oracle, w, h)
+    mbw, mbh = w // 16, h // 16
+    for j, (x0, y0, sw, sh) in enumerate([(0, 0, 3, 2), (mbw - 3, 0, 3, 3), (0, mbh - 2, 4, 2),
+                                          (mbw - 2, mbh - 2, 2, 2), (0, 0, mbw, mbh),
+                                          (5, 3, 1, 1)]):
+        nal = ext_slice(oracle, c, sw, sh, 77 + j, cbp_pm=900, skip_pm=300)
+        for mode in (EXACT, PSKIP):
+            _check_frame(oracle, c, 40, [], mode, splice_of(x0, y0, sw, sh, nal), buf)
+
+
+def test_no_splice_equals_hint_nal(oracle):
+    rng = random.Random(9)
+    w, h = 256, 256
+    a = (ctypes.c_uint8 * (1 << 18))()
+    b = (ctypes.c_uint8 * (1 << 18))()
+    err = ctypes.c_int()
+    for mode in (EXACT, PSKIP):
+        c1, c2 = _cfg(oracle, w, h), _cfg(oracle, w, h)
+        for i in range(30):
+            off = oracle.or_synthetic_offset(1, i, h)
+            rects = random_hints(rng, w // 16, h // 16, _refs(c1), nmax=3)
+            arr, n = hint_array(rects)
+            ka = oracle.or_compose_hint(a, len(a), ctypes.byref(c1), off, 0, arr, n, mode,
+                                        ctypes.byref(err))
+            assert err.value == 0
+            kb = oracle.or_compose_splice(b, len(b), ctypes.byref(c2), off, 0, arr, n, mode, None,
+                                          ctypes.byref(err))
+            assert err.value == 0 and bytes(a[:ka]) == bytes(b[:kb])
+            empty = Splice(0, 0, 0, 0, None, 0)
+            c3 = OrCfg.from_buffer_copy(c1)
+            c3.frame_num -= 1
+            kc = oracle.or_splice_scroll_nal(b, len(b), ctypes.byref(c3), off, arr, n, mode,
+                                             ctypes.byref(empty), ctypes.byref(err))
+            assert err.value == 0 and bytes(b[:kc]) == bytes(a[ka - kc:ka])
+
+
+def test_errors(oracle):
+    buf = (ctypes.c_uint8 * (1 << 18))()
+    err = ctypes.c_int()
+    w, h = 256, 256
+    c = _cfg(oracle, w, h)
+
+    def compose(sp):
+        c2 = OrCfg.from_buffer_copy(c)
+        k = oracle.or_splice_scroll_nal(buf, len(buf), ctypes.byref(c2), 40, None, 0, EXACT,
+                                        ctypes.byref(sp), ctypes.byref(err))
+        assert (k == 0) == (err.value != 0) and c2.frame_num == c.frame_num + (k > 0)
+        return err.value
+
+    good = ext_slice(oracle, c, 4, 3, 1)
+    assert compose(splice_of(2, 2, 4, 3, good)) == 0
+    # unsupported MB types: P_L0_L0_16x8 (1), P_8x8 (3), intra (5 = I_NxN in P, 30 = I_PCM)
+    for t in (1, 2, 3, 4, 5, 12, 30):
+        bad = ext_slice(oracle, c, 4, 3, 1, bad_mb=5, bad_type=t)
+        assert compose(splice_of(2, 2, 4, 3, bad)) == ERR_MBTYPE, t
+    # not a non-IDR slice: an IDR NAL header, an SPS
+    assert compose(splice_of(2, 2, 4, 3, good[:4] + bytes([0x65]) + good[5:])) == ERR_NAL
+    assert compose(splice_of(2, 2, 4, 3, good[:4] + bytes([0x67]) + good[5:])) == ERR_NAL
+    # a rect whose MB count differs from the slice's: too many MBs / too few
+    assert compose(splice_of(2, 2, 4, 2, good)) == ERR_SYNTAX
+    assert compose(splice_of(2, 2, 4, 4, good)) == ERR_SYNTAX
+    # truncated
+    assert compose(splice_of(2, 2, 4, 3, good[:len(good) // 2])) in (ERR_SYNTAX,)
+    # a reference the frame does not have (waypoint 0 before any waypoint)
+    assert c.nwp == 0
+    bad = ext_slice(oracle, c, 4, 3, 2, nrefs=4, max_ref=3, skip_pm=0)
+    assert compose(splice_of(2, 2, 4, 3, bad)) == ERR_REF
+    # rect outside the picture
+    assert compose(splice_of(14, 2, 4, 3, good)) == ERR_HEADER

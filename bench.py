@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """bench.py -- composed frames/s of the MI355X scroll composer.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload p720dyn|p720|p4kdyn|p720hint|ingest720|ipcm720]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload p720dyn|p720|p4kdyn|p720hint|p720splice|ingest720|ipcm720]
 
 One process per GPU (torch.distributed.run for N > 1; RANK / LOCAL_RANK /
 WORLD_SIZE from the env).  Streams are independent, so each rank owns a static
@@ -24,6 +24,11 @@ A step = one scroll_batch_compose over every stream of the rank:
   streams x 16 composed 1280x720 frames whose scroll NALs carry a UI overlay
   (static chrome and side panel, a horizontally scrolling carousel) in the
   P_Skip mode, coded per MB by k_hint_stage.
+  workload p720splice (pre-encoded MB splice; no BASELINE
+  number): 256 streams x 16 composed 1280x720 frames, each scroll NAL with a
+  25x25-MB external P slice spliced in; the slices are produced on the GPU by
+  the dynamic rect coder for 400x400 pictures (the "dynamic encoder"), stay
+  in HBM and are handed over by device pointer and parsed again every step.
   workload ipcm720 (metric: reference files/s): a step =
   scroll_batch_ipcm_files_device of 256 random 1280x720 I420 pictures in HBM
   -> 256 SPS+PPS+I_PCM IDR files in HBM (the files ingest720 reads).
@@ -70,6 +75,12 @@ WORKLOADS = {
     "ipcm720": dict(w=1280, h=720, streams=256, frames=1, rect=None, ipcm=True,
                     desc="reference files from pictures (SURVEY 8f row 3): 256 1280x720 I420 "
                          "pictures in HBM -> 256 SPS+PPS+I_PCM IDR Annex-B files in HBM per step"),
+    "p720splice": dict(w=1280, h=720, streams=256, frames=16, rect=None, splice=(28, 10, 25, 25),
+                       desc="pre-encoded MB splice (SURVEY 8f row 2): 256 concurrent 1280x720 "
+                            "streams, every scroll NAL carries a 25x25-MB external P slice "
+                            "(400x400 px: a 360x360 preview + margin) spliced at MB (28, 10); "
+                            "the slices are the dynamic rect coder's output for 400x400 "
+                            "pictures, resident in HBM, parsed again every step"),
     "p720hint": dict(w=1280, h=720, streams=256, frames=16, rect=None, hints=True,
                      desc="UI hints (SURVEY 8f row 1): 256 concurrent 1280x720 streams, scroll "
                           "frames with a static chrome / side panel / horizontal carousel "
@@ -425,6 +436,156 @@ def cpu_baseline_hint(wl, nstreams=128, nframes=256):
                        f"overlay, P_Skip mode, 1 thread, oracle/hint_oracle.c -O2")
 
 
+def external_slices(hs, S, F, sw, sh, first, device):
+    """the "dynamic encoder" of MASTER_DESIGN 4.2 on the GPU: a batch of
+    sw*16 x sh*16 pictures whose dynamic rect covers the whole picture, so
+    each scroll NAL is a P slice of sw x sh residual MBs.  Returns the batch
+    (its arenas hold the NALs) and per (s, f) the NAL's device pointer and
+    size."""
+    import numpy as np
+    ew, eh = 16 * sw, 16 * sh
+    e = hs.Batch(S, F, F * (2048 + 1024 * sw * sh) + (1 << 20), device=device)
+    for _ in range(S):
+        e.add_stream(hs.make_config(ew, eh))
+    offs = synthetic_offsets(first, S, F, eh)              # < 496: no waypoints
+    e.set_offsets(offs)
+    e.set_dyn_rect(0, 0, sw, sh)
+    e.set_dyn_refs(striped_i420(ew, eh, 0), striped_i420(ew, eh, 1))
+    e.dyn_source_synth(F, stream_base=first, t0=0)
+    e.compose(F, rewind=True)
+    if e.sync() != 0:
+        raise RuntimeError(hs.last_error())
+    ptrs = {}
+    for s in range(S):
+        base, pos = e.output_device_ptr(s), 0
+        nals = e.nals(s)
+        assert len(nals) == F, "one scroll NAL per frame (no waypoints)"
+        for f, (kind, _, size, _) in enumerate(nals):
+            ptrs[(s, f)] = (base + pos, size)
+            pos += size
+    return e, ptrs
+
+
+def cpu_baseline_splice(wl, slices, nstreams=16, nframes=64):
+    """oracle/splice_oracle.c on one host core over a bounded sample: the
+    same external slices (copied to the host) into nstreams x nframes frames"""
+    import numpy as np
+    repo_oracle = os.path.join(HERE, "oracle")
+    sys.path.insert(0, os.path.join(HERE, "tests"))
+    import subprocess
+    subprocess.run(["make", "-s", "-C", repo_oracle], check=True, stdout=subprocess.DEVNULL)
+    lib = ctypes.CDLL(os.path.join(repo_oracle, "_build", "liboracle.so"))
+    from dynhelp import OrCfg, splice_of
+    W, H = wl["w"], wl["h"]
+    x0, y0, sw, sh = wl["splice"]
+    offs = synthetic_offsets(0, nstreams, nframes, H)
+    buf = (ctypes.c_uint8 * (4 << 20))()
+    err = ctypes.c_int()
+    sps = [splice_of(x0, y0, sw, sh, slices[k % len(slices)]) for k in range(nstreams * nframes)]
+    t0 = time.perf_counter()
+    for s in range(nstreams):
+        c = OrCfg()
+        lib.or_cfg_init(ctypes.byref(c), W, H)
+        c.frame_num = 2
+        for f in range(nframes):
+            lib.or_compose_splice(buf, len(buf), ctypes.byref(c), int(offs[s, f]), 0, None, 0, 0,
+                                  ctypes.byref(sps[s * nframes + f]), ctypes.byref(err))
+    el = time.perf_counter() - t0
+    return {"value": round(nstreams * nframes / el, 1), "unit": "frames/s", "cores": 1,
+            "kind": "port", "sample": f"{nstreams} streams x {nframes} frames, {W}x{H} with a "
+                                      f"{sw}x{sh}-MB spliced slice, 1 thread, "
+                                      f"oracle/splice_oracle.c -O2 (parse + compose)"}
+
+
+def run_splice(args, wl, rank, world, local, dist):
+    import numpy as np
+    import torch
+    import h264scroll as hs
+
+    torch.cuda.set_device(local)
+    stream = torch.cuda.current_stream()
+    S, F, W, H = wl["streams"], wl["frames"], wl["w"], wl["h"]
+    x0, y0, sw, sh = wl["splice"]
+    first, _ = shard_streams(rank, world, S)
+    e, ptrs = external_slices(hs, S, F, sw, sh, first, local)
+    ext_bytes = sum(n for _, n in ptrs.values())
+    entries = [(s, f, x0, y0, sw, sh, p, n) for (s, f), (p, n) in ptrs.items()]
+    per_frame = 2 * (64 + (W // 16) * (H // 16)) + 2 * ext_bytes // (S * F) + 4096
+    b = hs.Batch(S, F, F * per_frame + (1 << 20), device=local)
+    for _ in range(S):
+        b.add_stream(hs.make_config(W, H))
+    b.set_offsets(synthetic_offsets(first, S, F, H))
+
+    def barrier():
+        torch.cuda.synchronize()
+        if dist:
+            dist.barrier()
+
+    def step():
+        b.set_splices_device(entries)            # new content in place: parsed again
+        b.compose(F, stream=stream.cuda_stream, rewind=True)
+
+    for _ in range(args.warmup):
+        step()
+    barrier()
+    if b.sync() != 0:
+        raise RuntimeError(hs.last_error())
+    b.enable_timing(True)
+    b.kernel_stats_ex()
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    barrier()
+    t1 = time.perf_counter()
+    if b.sync() != 0:
+        raise RuntimeError(hs.last_error())
+    (plan_ms, emit_ms, stage_ms, demit_ms, _, _), n_launch = b.kernel_stats_ex()
+    step_bytes = b.last_bytes()
+    rbsp_tot, ep_tot, dyn_nals = b.dyn_totals()
+    b.enable_timing(False)
+    el = max_over_ranks(t1 - t0, dist)
+    value = S * F * args.steps * world / el
+    if rank == 0:
+        n = max(n_launch, 1)
+        kms = {"plan": plan_ms / n, "emit": emit_ms / n, "splice_stage": stage_ms / n,
+               "dyn_emit": demit_ms / n}
+        # k_splice_parse + k_splice_stage per launch: the external slices read
+        # (twice: the parse and the body copy), the staged RBSP written
+        alg_bytes = 2 * ext_bytes + rbsp_tot
+        achieved = alg_bytes / (kms["splice_stage"] * 1e-3) / 1e9
+        out = {
+            "metric": "spliced composed frames/sec (1280x720 + 25x25-MB external slice)",
+            "value": round(value, 1), "unit": "frames/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(1000.0 * el / args.steps, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
+            "config": {"workload": wl["desc"], "resolution": f"{W}x{H}",
+                       "streams_per_gpu": S, "frames_per_step": F, "splice_rect_mb": [x0, y0, sw, sh],
+                       "parallelism": f"static stream shard x{world}, no RCCL"},
+            "bytes_per_frame": round(step_bytes / (S * F), 1),
+            "external_slice_bytes_per_frame": round(ext_bytes / (S * F), 1),
+            "roofline": {"bound": "hbm", "kernel": "k_splice_parse+k_splice_stage",
+                         "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                         "alg_bytes_per_launch": alg_bytes,
+                         "kernel_ms_avg": {k: round(v, 4) for k, v in kms.items()}},
+        }
+        if world == 1 and not args.no_cpu:
+            host = [e.output(s)[:] for s in range(min(S, 4))]
+            slices = []
+            for s in range(min(S, 4)):
+                pos = 0
+                for f in range(F):
+                    n = ptrs[(s, f)][1]
+                    slices.append(host[s][pos:pos + n])
+                    pos += n
+            out["cpu_baseline"] = cpu_baseline_splice(wl, slices)
+        print(json.dumps(out), flush=True)
+    b.close()
+    e.close()
+
+
 def load_traffic(workload):
     p = os.path.join(HERE, "profiles", f"traffic_{workload}.json")
     if os.path.exists(p):
@@ -460,6 +621,11 @@ def main():
         import torch.distributed as dist
         dist.init_process_group("gloo")
 
+    if wl.get("splice"):
+        run_splice(args, wl, rank, world, local, dist)
+        if dist:
+            dist.destroy_process_group()
+        return
     if wl.get("ingest") or wl.get("ipcm"):
         (run_ingest if wl.get("ingest") else run_ipcm)(args, wl, rank, world, local, dist)
         if dist:

@@ -922,7 +922,9 @@ struct ScrollBatch {
      * whose rect comes from an external slice */
     struct SpliceHost {
         int x0 = 0, y0 = 0, w = 0, h = 0;
-        std::vector<uint8_t> nal;
+        std::vector<uint8_t> nal;      /* host bytes (scroll_batch_set_splice)          */
+        const uint8_t *dnal = nullptr; /* or device bytes (scroll_batch_set_splices_device) */
+        size_t n = 0;
     };
     std::vector<SpliceHost> h_sp;      /* [s * max_frames + f]; w = 0: none */
     int sp_n = 0;                      /* spliced frames                           */
@@ -1269,7 +1271,7 @@ static int launch(ScrollBatch *b, int nframes, int plan_mode, int nal_max, hipSt
         if (hint) {
             if (b->sp_parse) {
                 if (splice_launch_parse(hs, b->sp_n, b->d_sp_list, b->d_spf, b->d_st, ld_fr,
-                                        b->d_sp_nal, b->d_sp_rbsp, b->d_sp_rec)) {
+                                        b->d_sp_rbsp, b->d_sp_rec)) {
                     set_err("k_splice_parse launch: %s", hipGetErrorString(hipGetLastError()));
                     return SCROLL_ERR_HIP;
                 }
@@ -1960,6 +1962,7 @@ static int splice_upload(ScrollBatch *b)
     std::vector<int32_t> list;
     std::vector<uint8_t> pool;
     size_t words = 0, recs = 0, slot = b->geo.slot_bytes;
+    std::vector<size_t> pool_off(b->h_sp.size(), 0);
     for (size_t i = 0; i < b->h_sp.size(); ++i) {
         const ScrollBatch::SpliceHost &h = b->h_sp[i];
         SpliceFrame &o = spf[i];
@@ -1969,17 +1972,19 @@ static int splice_upload(ScrollBatch *b)
         o.y0 = h.y0;
         o.w = h.w;
         o.h = h.h;
-        o.nal_off = pool.size();
-        o.nal_len = (uint32_t)h.nal.size();
+        o.nal_len = (uint32_t)h.n;
         o.rbsp_word = words;
         o.rec_first = (uint32_t)recs;
-        pool.insert(pool.end(), h.nal.begin(), h.nal.end());
-        pool.resize((pool.size() + 3) & ~(size_t)3);
-        words += h.nal.size() / 4 + 2;
+        if (!h.dnal) {                 /* host bytes -> the NAL pool */
+            pool_off[i] = pool.size();
+            pool.insert(pool.end(), h.nal.begin(), h.nal.end());
+            pool.resize((pool.size() + 3) & ~(size_t)3);
+        }
+        words += h.n / 4 + 2;
         recs += (size_t)h.w * h.h;
         list.push_back((int32_t)i);
         const DevStream &d = b->h_st[i / F];
-        slot = std::max(slot, splice_slot_bound(d.w / 16, d.h / 16, h.w, h.h, h.nal.size()));
+        slot = std::max(slot, splice_slot_bound(d.w / 16, d.h / 16, h.w, h.h, h.n));
     }
     int rc;
     if (!b->d_spf) {
@@ -2002,6 +2007,8 @@ static int splice_upload(ScrollBatch *b)
         }
         b->geo.slot_bytes = slot;
     }
+    for (size_t i = 0; i < b->h_sp.size(); ++i)
+        if (b->h_sp[i].w > 0) spf[i].nal = b->h_sp[i].dnal ? b->h_sp[i].dnal : b->d_sp_nal + pool_off[i];
     HIPCHK(hipMemcpy(b->d_spf, spf.data(), S * F * sizeof(SpliceFrame), hipMemcpyHostToDevice));
     if (!pool.empty())
         HIPCHK(hipMemcpy(b->d_sp_nal, pool.data(), pool.size(), hipMemcpyHostToDevice));
@@ -2051,6 +2058,56 @@ int scroll_batch_set_splice(ScrollBatch *b, int s, int f, int x0, int y0, int w,
         sp.w = w;
         sp.h = h;
         sp.nal.assign(nal, nal + n);
+        sp.dnal = nullptr;
+        sp.n = n;
+    }
+    b->sp_dirty = 1;
+    b->hint_dirty = 1;
+    return SCROLL_OK;
+}
+
+int scroll_batch_set_splices_device(ScrollBatch *b, int n, const ScrollSpliceDesc *d)
+{
+    if (!b || n < 0 || (n > 0 && !d)) {
+        set_err("scroll_batch_set_splices_device: bad arguments");
+        return SCROLL_ERR_ARG;
+    }
+    for (int k = 0; k < n; ++k) {
+        const ScrollSpliceDesc &e = d[k];
+        const bool on = e.n > 0;
+        if (e.s < 0 || e.s >= b->nstreams || e.f < 0 || e.f >= b->max_frames ||
+            (on && (!e.nal || e.w <= 0 || e.h <= 0 || e.x0 < 0 || e.y0 < 0 ||
+                    e.n > ((uint64_t)1 << 30) || e.x0 + e.w > b->h_st[e.s].w / 16 ||
+                    e.y0 + e.h > b->h_st[e.s].h / 16))) {
+            set_err("scroll_batch_set_splices_device: entry %d: bad stream / frame / rect / size", k);
+            return SCROLL_ERR_ARG;
+        }
+    }
+    if (n == 0) return SCROLL_OK;
+    if (b->dyn_on) {
+        set_err("scroll_batch_set_splices_device: not combinable with a dynamic rect");
+        return SCROLL_ERR_CONFIG;
+    }
+    if (!b->hint_on) {
+        int rc = scroll_batch_set_hints(b, d[0].s, d[0].f, nullptr, 0, SCROLL_HINT_EXACT);
+        if (rc) return rc;
+    } else {
+        int rc = batch_host_sync(b);
+        if (rc) return rc;
+    }
+    if (b->h_sp.size() < (size_t)b->max_streams * b->max_frames)
+        b->h_sp.resize((size_t)b->max_streams * b->max_frames);
+    for (int k = 0; k < n; ++k) {
+        const ScrollSpliceDesc &e = d[k];
+        ScrollBatch::SpliceHost &sp = b->h_sp[(size_t)e.s * b->max_frames + e.f];
+        sp = ScrollBatch::SpliceHost{};
+        if (e.n == 0) continue;
+        sp.x0 = e.x0;
+        sp.y0 = e.y0;
+        sp.w = e.w;
+        sp.h = e.h;
+        sp.dnal = e.nal;
+        sp.n = (size_t)e.n;
     }
     b->sp_dirty = 1;
     b->hint_dirty = 1;

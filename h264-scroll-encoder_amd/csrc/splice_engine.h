@@ -16,12 +16,12 @@
 #define SPLICE_MAX_MV 16383         /* |mv| of a spliced MB, quarter pels          */
 #define HINT_MODE_SPLICED 0x100     /* HintFrame.mode bit: k_splice_stage stages it */
 
-/* one spliced frame: rect, its external NAL in the NAL pool, its RBSP in
+/* one spliced frame: rect, its external NAL (device memory), its RBSP in
  * the word pool (MSB-first words), its MB records, the parse status and the
  * last stage's (reference validity), SCROLL_SPLICE_*.  48 bytes. */
 typedef struct {
     int32_t x0, y0, w, h;
-    uint64_t nal_off;               /* bytes into the NAL pool                    */
+    const uint8_t *nal;             /* device bytes: the NAL pool or the caller's */
     uint64_t rbsp_word;             /* words into the RBSP pool                   */
     uint32_t nal_len;
     uint32_t rec_first;             /* first MB record                            */
@@ -45,8 +45,7 @@ typedef struct {
 
 /* 0, or -1 when the launch failed */
 int splice_launch_parse(hipStream_t hs, int n, const int32_t *list, SpliceFrame *spf,
-                        const DevStream *st, int ld_fr, const uint8_t *nal, uint32_t *rbsp,
-                        SpliceMbRec *rec);
+                        const DevStream *st, int ld_fr, uint32_t *rbsp, SpliceMbRec *rec);
 int splice_launch_stage(hipStream_t hs, int nframes, int S, DevStream *st, const NalDesc *nal,
                         int ld_nal, const PlanPending *pend, DynFrame *dfr, int ld_fr,
                         const HintFrame *hf, const ScrollHintRect *pool, SpliceFrame *spf,

@@ -7,8 +7,9 @@
  * in the rect of a composed scroll frame.  Bits: oracle/splice_oracle.c;
  * tests/test_gpu_splice.py checks them bit-exact.
  *
- *   k_splice_parse   one lane per spliced frame, serial over its slice (a
- *                    CAVLC slice is a sequential bit string): emulation
+ *   k_splice_parse   one wave per spliced frame (a CAVLC slice is a
+ *                    sequential bit string, so the parse is wave-uniform with
+ *                    lane-parallel VLC table matching): emulation
  *                    prevention removed into the RBSP word pool, slice
  *                    header checked against the stream's SPS/PPS, then per
  *                    MB its motion (P_Skip 8.4.1.1 / median 8.4.1.3 in the
@@ -51,132 +52,6 @@ static_assert(RING >= DT + 240 + 1, "the row above a window stays in the ring");
 /* ------------------------------------------------------------------------ */
 /* k_splice_parse                                                            */
 /* ------------------------------------------------------------------------ */
-/* RBSP reader over MSB-first words; words at and past nw read as zero */
-struct Rd {
-    const uint32_t *w;
-    uint32_t nw, nbits, p;
-    bool bad;
-    __device__ inline uint32_t word(uint32_t k) const { return k < nw ? w[k] : 0u; }
-    __device__ inline uint32_t peek32() const
-    {
-        const uint32_t k = p >> 5, o = p & 31u;
-        const uint32_t a = word(k);
-        return o ? (a << o) | (word(k + 1) >> (32u - o)) : a;
-    }
-    __device__ inline uint32_t peek(int n) const { return n ? peek32() >> (32 - n) : 0u; }
-    __device__ inline void skip(int n)
-    {
-        p += (uint32_t)n;
-        bad |= p > nbits;
-    }
-    __device__ inline uint32_t u(int n)
-    {
-        const uint32_t v = peek(n);
-        skip(n);
-        return v;
-    }
-    __device__ inline uint32_t ue()
-    {
-        const uint32_t x = peek32();
-        if (!x) {
-            bad = true;
-            return 0;
-        }
-        const int z = __clz((int)x);
-        skip(z);
-        return u(z + 1) - 1u;
-    }
-    __device__ inline int32_t se()
-    {
-        const uint32_t k = ue();
-        return (k & 1u) ? (int32_t)((k + 1u) >> 1) : -(int32_t)(k >> 1);
-    }
-};
-
-/* coeff_token (9.2.1) by matching Table 9-5 */
-__device__ inline bool rd_token(Rd &r, int nC, int &tc, int &t1)
-{
-    if (nC >= 8) {
-        const uint32_t c = r.u(6);
-        if (c == 3u) {
-            tc = t1 = 0;
-            return true;
-        }
-        tc = (int)(c >> 2) + 1;
-        t1 = (int)(c & 3u);
-        return t1 <= tc;
-    }
-    const uint32_t x = r.peek(16);
-    const int tmax = nC == -1 ? 4 : 16, tb = nC < 2 ? 0 : (nC < 4 ? 1 : 2);
-    for (int c = 0; c <= tmax; ++c)
-        for (int o = 0; o <= 3 && o <= c; ++o) {
-            const int len = nC == -1 ? SPT.ctdc_len[4 * c + o] : SPT.ct_len[tb][4 * c + o];
-            const uint32_t bits = nC == -1 ? SPT.ctdc_bits[4 * c + o] : SPT.ct_bits[tb][4 * c + o];
-            if (len && (x >> (16 - len)) == bits) {
-                r.skip(len);
-                tc = c;
-                t1 = o;
-                return true;
-            }
-        }
-    return false;
-}
-
-/* the body of a block (9.2.2-9.2.4): trailing-ones signs, levels,
- * total_zeros, run_before; consumed, not kept */
-__device__ inline bool rd_body(Rd &r, int tc, int t1, int maxc)
-{
-    if (tc == 0) return true;
-    r.skip(t1);
-    int sl = (tc > 10 && t1 < 3) ? 1 : 0;
-    for (int k = t1; k < tc; ++k) {
-        const uint32_t x = r.peek32();
-        const int prefix = x ? __clz((int)x) : 32;
-        if (prefix > 15) return false;                       /* High profiles only */
-        r.skip(prefix + 1);
-        int ssize = sl;
-        if (prefix == 14 && sl == 0) ssize = 4;
-        if (prefix >= 15) ssize = prefix - 3;
-        int code = min(prefix, 15) << sl;
-        if (ssize) code += (int)r.u(ssize);
-        if (prefix >= 15 && sl == 0) code += 15;
-        if (k == t1 && t1 < 3) code += 2;
-        const int a = (code + 2) >> 1;                       /* |level| */
-        if (sl == 0) sl = 1;
-        if (a > (3 << (sl - 1)) && sl < 6) sl++;
-    }
-    int zl = 0;
-    if (tc < maxc) {
-        const uint32_t x = r.peek(16);
-        int tz = -1;
-        for (int z = 0; z <= maxc - tc && tz < 0; ++z) {
-            const int len = maxc == 4 ? SPT.tzdc_len[tc - 1][z] : SPT.tz_len[tc - 1][z];
-            const uint32_t bits = maxc == 4 ? SPT.tzdc_bits[tc - 1][z] : SPT.tz_bits[tc - 1][z];
-            if (len && (x >> (16 - len)) == bits) {
-                r.skip(len);
-                tz = z;
-            }
-        }
-        if (tz < 0) return false;
-        zl = tz;
-    }
-    for (int k = 0; k < tc - 1 && zl > 0; ++k) {
-        const uint32_t x = r.peek(16);
-        const int zi = min(zl, 7) - 1;
-        int run = -1;
-        for (int q = 0; q <= zl && q <= 14 && run < 0; ++q) {
-            const int len = SPT.rb_len[zi][q];
-            if (len && (x >> (16 - len)) == SPT.rb_bits[zi][q]) {
-                r.skip(len);
-                run = q;
-            }
-        }
-        if (run < 0) return false;
-        zl -= run;
-    }
-    return !r.bad;
-}
-
 __device__ inline int nc2(int nA, int nB)
 {
     return nA >= 0 && nB >= 0 ? (nA + nB + 1) >> 1 : (nA >= 0 ? nA : (nB >= 0 ? nB : 0));
@@ -203,35 +78,305 @@ __device__ inline int blk_raster16(int blk)       /* luma4x4BlkIdx -> raster */
     return 4 * ((q8 >> 1) * 2 + (q4 >> 1)) + (q8 & 1) * 2 + (q4 & 1);
 }
 
-__device__ inline bool rd_piece(Rd &r, SpliceMbRec &mb, int i, int nC, int maxc)
+/* One wave parses one slice.  The slice is a sequential bit string, so the
+ * parse itself is wave-uniform (scalar values, no divergence): the bit window
+ * is 64 RBSP words held one per lane (readlane at the uniform bit position),
+ * every VLC is matched by all lanes at once (lane e tests table entry e,
+ * ballot), lane j keeps piece j's record fields, and the neighbour context
+ * (motion of the two rows above, TotalCoeffs of the row above) sits in LDS. */
+constexpr int PARSE_MAXW = 240;          /* external picture width limit (MBs) */
+
+struct WRd {
+    const uint32_t *w;
+    uint32_t nw, nbits, p, base;
+    uint32_t win;                        /* word base + lane */
+    bool bad;                            /* ue() without a 1 bit; p > nbits is checked per MB */
+    __device__ inline void fill(uint32_t k0)
+    {
+        base = k0;
+        const uint32_t k = k0 + (uint32_t)(threadIdx.x & 63);
+        win = k < nw ? w[k] : 0u;
+    }
+    /* the 32 bits at p: words k, k + 1 of the window by readlane (scalar),
+     * joined by a 64-bit scalar shift */
+    __device__ inline uint32_t peek32()
+    {
+        uint32_t k = (p >> 5) - base;
+        if (k >= 63u) {
+            fill(p >> 5);
+            k = 0;
+        }
+        const uint32_t a = (uint32_t)__builtin_amdgcn_readlane(win, k);
+        const uint32_t b = (uint32_t)__builtin_amdgcn_readlane(win, k + 1);
+        const uint64_t ab = (uint64_t)a << 32 | b;
+        return (uint32_t)((ab << (p & 31u)) >> 32);
+    }
+    __device__ inline uint32_t peek(int n) { return n ? peek32() >> (32 - n) : 0u; }
+    __device__ inline void skip(int n) { p += (uint32_t)n; }
+    __device__ inline bool over() const { return p > nbits; }
+    __device__ inline uint32_t u(int n)
+    {
+        const uint32_t v = peek(n);
+        skip(n);
+        return v;
+    }
+    __device__ inline uint32_t ue()
+    {
+        const uint32_t x = peek32();
+        if (!x) {
+            bad = true;
+            return 0;
+        }
+        const int z = __clz((int)x);
+        if (z < 16) {                    /* the whole code in x */
+            skip(2 * z + 1);
+            return (x >> (31 - 2 * z)) - 1u;
+        }
+        skip(z);
+        return u(z + 1) - 1u;
+    }
+    __device__ inline int32_t se()
+    {
+        const uint32_t k = ue();
+        return (k & 1u) ? (int32_t)((k + 1u) >> 1) : -(int32_t)(k >> 1);
+    }
+};
+
+/* first lane of a ballot, -1 if none */
+__device__ inline int first_lane(uint64_t m) { return m ? __builtin_ctzll(m) : -1; }
+
+/* The CAVLC tables in registers, lane e holding entry e of each (packed
+ * len << 8 | bits, two 16-bit entries per register): a VLC match is then a
+ * few VALU operations and a ballot, no memory access */
+struct LaneTabs {
+    uint32_t ct01, ct2d;          /* coeff_token nC 0-1 | 2-3 ; nC 4-7 | chroma DC, entry e */
+    uint32_t cx01, cx2;           /* entries 64 + e (lanes 0..3)                             */
+    /* total_zeros rows 2k | 2k+1, entry (total_zeros) e -- separate
+     * registers: an array indexed by the row would live in scratch */
+    uint32_t tz0, tz1, tz2, tz3, tz4, tz5, tz6, tz7;
+    uint32_t tzd01, tzd2;         /* chroma DC total_zeros rows 0 | 1, 2                      */
+    uint32_t rb0, rb1, rb2, rb3;  /* run_before rows 2k | 2k+1, entry (run) e                 */
+    uint32_t cbp;                 /* coded_block_pattern -> codeNum, entry e < 48            */
+};
+
+__device__ inline uint32_t pk(int len, int bits) { return len ? (uint32_t)(len << 8 | bits) : 0u; }
+
+__device__ inline LaneTabs lane_tabs()
 {
-    int tc, t1;
-    if (!rd_token(r, nC, tc, t1) || tc > maxc) return false;
-    const uint32_t p0 = r.p;
-    if (!rd_body(r, tc, t1, maxc)) return false;
-    mb.tc[i] = (uint8_t)tc;
-    mb.t1[i] = (uint8_t)t1;
-    mb.boff[i] = p0;
-    mb.blen[i] = (uint16_t)(r.p - p0);
+    const int e = threadIdx.x & 63;
+    LaneTabs T;
+    T.ct01 = pk(SPT.ct_len[0][e], SPT.ct_bits[0][e]) | pk(SPT.ct_len[1][e], SPT.ct_bits[1][e]) << 16;
+    T.ct2d = pk(SPT.ct_len[2][e], SPT.ct_bits[2][e]) |
+             (e < 20 ? pk(SPT.ctdc_len[e], SPT.ctdc_bits[e]) << 16 : 0u);
+    const int x = 64 + (e & 3);
+    T.cx01 = e < 4 ? pk(SPT.ct_len[0][x], SPT.ct_bits[0][x]) | pk(SPT.ct_len[1][x], SPT.ct_bits[1][x]) << 16 : 0u;
+    T.cx2 = e < 4 ? pk(SPT.ct_len[2][x], SPT.ct_bits[2][x]) : 0u;
+    auto tzp = [e](int k) {
+        const int r0 = 2 * k, r1 = 2 * k + 1;
+        const uint32_t lo = e < 16 ? pk(SPT.tz_len[r0][e & 15], SPT.tz_bits[r0][e & 15]) : 0u;
+        const uint32_t hi = e < 16 && r1 < 15 ? pk(SPT.tz_len[r1][e & 15], SPT.tz_bits[r1][e & 15]) : 0u;
+        return lo | hi << 16;
+    };
+    T.tz0 = tzp(0);
+    T.tz1 = tzp(1);
+    T.tz2 = tzp(2);
+    T.tz3 = tzp(3);
+    T.tz4 = tzp(4);
+    T.tz5 = tzp(5);
+    T.tz6 = tzp(6);
+    T.tz7 = tzp(7);
+    T.tzd01 = e < 4 ? pk(SPT.tzdc_len[0][e & 3], SPT.tzdc_bits[0][e & 3]) |
+                          pk(SPT.tzdc_len[1][e & 3], SPT.tzdc_bits[1][e & 3]) << 16 : 0u;
+    T.tzd2 = e < 4 ? pk(SPT.tzdc_len[2][e & 3], SPT.tzdc_bits[2][e & 3]) : 0u;
+    auto rbp = [e](int k) {
+        const int r0 = 2 * k, r1 = 2 * k + 1;
+        const uint32_t lo = e < 15 ? pk(SPT.rb_len[r0][e % 15], SPT.rb_bits[r0][e % 15]) : 0u;
+        const uint32_t hi = e < 15 && r1 < 7 ? pk(SPT.rb_len[r1][e % 15], SPT.rb_bits[r1][e % 15]) : 0u;
+        return lo | hi << 16;
+    };
+    T.rb0 = rbp(0);
+    T.rb1 = rbp(1);
+    T.rb2 = rbp(2);
+    T.rb3 = rbp(3);
+    T.cbp = e < 48 ? SPT.cbp_code[e] : 0xffffu;
+    return T;
+}
+
+/* does the 16-bit lookahead x start with the packed code v? */
+__device__ inline bool code_hit(uint32_t v, uint32_t x)
+{
+    const uint32_t len = (v >> 8) & 255u;
+    return len && (x >> (16u - len)) == (v & 255u);
+}
+
+/* the ballot's entry, its packed code from the lane that holds it */
+__device__ inline int match(uint32_t v, uint32_t x, uint32_t &len)
+{
+    const int e = first_lane(__ballot(code_hit(v, x)));
+    if (e >= 0) len = (__builtin_amdgcn_readlane(v, e) >> 8) & 255u;
+    return e;
+}
+
+/* 16-bit half h (uniform) of a packed register */
+__device__ inline uint32_t half(uint32_t v, int h) { return h ? v >> 16 : v & 0xffffu; }
+
+/* coeff_token (9.2.1): lane e tests entry e (4 * TotalCoeff + TrailingOnes) */
+__device__ __attribute__((always_inline)) inline bool wrd_token(WRd &r, const LaneTabs &T, int nC, int &tc, int &t1)
+{
+    if (nC >= 8) {
+        const uint32_t c = r.u(6);
+        if (c == 3u) {
+            tc = t1 = 0;
+            return true;
+        }
+        tc = (int)(c >> 2) + 1;
+        t1 = (int)(c & 3u);
+        return t1 <= tc;
+    }
+    const uint32_t x = r.peek(16);
+    const int tb = nC == -1 ? 3 : (nC < 2 ? 0 : (nC < 4 ? 1 : 2));
+    const uint32_t v = half(tb < 2 ? T.ct01 : T.ct2d, tb & 1);
+    uint32_t len = 0;
+    int e = match(v, x, len);
+    if (e < 0 && tb != 3) {
+        const uint32_t vx = half(tb < 2 ? T.cx01 : T.cx2, tb & 1);
+        const int e2 = match(vx, x, len);
+        e = e2 < 0 ? -1 : 64 + e2;
+    }
+    if (e < 0) return false;
+    r.skip((int)len);
+    tc = e >> 2;
+    t1 = e & 3;
     return true;
 }
 
-/* P_Skip / median prediction in the external picture from the records */
-__device__ inline Mv rec_mv(const SpliceMbRec *rec, int m) { return Mv{rec[m].ref, rec[m].mx, rec[m].my}; }
+/* the body of a block (9.2.2-9.2.4), consumed, not kept */
+__device__ __attribute__((always_inline)) inline bool wrd_body(WRd &r, const LaneTabs &T, int tc, int t1, int maxc)
+{
+    const int lane = threadIdx.x & 63;
+    if (tc == 0) return true;
+    r.skip(t1);
+    int sl = (tc > 10 && t1 < 3) ? 1 : 0;
+    for (int k = t1; k < tc; ++k) {
+        const uint32_t x = r.peek32();
+        const int prefix = x ? __clz((int)x) : 32;
+        if (prefix > 15) return false;                       /* High profiles only */
+        r.skip(prefix + 1);
+        int ssize = sl;
+        if (prefix == 14 && sl == 0) ssize = 4;
+        if (prefix >= 15) ssize = prefix - 3;
+        int code = min(prefix, 15) << sl;
+        if (ssize) code += (int)r.u(ssize);
+        if (prefix >= 15 && sl == 0) code += 15;
+        if (k == t1 && t1 < 3) code += 2;
+        const int a = (code + 2) >> 1;                       /* |level| */
+        if (sl == 0) sl = 1;
+        if (a > (3 << (sl - 1)) && sl < 6) sl++;
+    }
+    int zl = 0;
+    if (tc < maxc) {
+        const uint32_t x = r.peek(16);
+        const int row = tc - 1;
+        uint32_t v;
+        if (maxc == 4) {
+            v = half(row < 2 ? T.tzd01 : T.tzd2, row & 1);
+        } else {
+            const int q = row >> 1;       /* uniform: a select tree, no indexing */
+            const uint32_t w01 = q & 1 ? T.tz1 : T.tz0, w23 = q & 1 ? T.tz3 : T.tz2;
+            const uint32_t w45 = q & 1 ? T.tz5 : T.tz4, w67 = q & 1 ? T.tz7 : T.tz6;
+            const uint32_t w03 = q & 2 ? w23 : w01, w47 = q & 2 ? w67 : w45;
+            v = half(q & 4 ? w47 : w03, row & 1);
+        }
+        if (lane > maxc - tc) v = 0;
+        uint32_t len = 0;
+        const int tz = match(v, x, len);
+        if (tz < 0) return false;
+        r.skip((int)len);
+        zl = tz;
+    }
+    for (int k = 0; k < tc - 1 && zl > 0; ++k) {
+        const uint32_t x = r.peek(16);
+        const int zi = min(zl, 7) - 1;
+        const int q = zi >> 1;
+        const uint32_t w01 = q & 1 ? T.rb1 : T.rb0, w23 = q & 1 ? T.rb3 : T.rb2;
+        uint32_t v = half(q & 2 ? w23 : w01, zi & 1);
+        if (lane > zl) v = 0;
+        uint32_t len = 0;
+        const int run = match(v, x, len);
+        if (run < 0) return false;
+        r.skip((int)len);
+        zl -= run;
+    }
+    return true;
+}
+
+/* lane j: piece j of the MB being parsed */
+struct PieceOut {
+    uint32_t tc, t1, off, len;
+};
+
+/* one residual block: coeff_token, then the body; lane pi keeps the fields */
+__device__ __attribute__((always_inline)) inline bool wrd_piece(WRd &r, const LaneTabs &T, int pi,
+                                                                int nC, int maxc, PieceOut &po)
+{
+    int tc, t1;
+    if (!wrd_token(r, T, nC, tc, t1) || tc > maxc) return false;
+    const uint32_t p0 = r.p;
+    if (!wrd_body(r, T, tc, t1, maxc)) return false;
+    if ((int)(threadIdx.x & 63) == pi) {
+        po.tc = (uint32_t)tc;
+        po.t1 = (uint32_t)t1;
+        po.off = p0;
+        po.len = r.p - p0;
+    }
+    return true;
+}
+
+/* nC of piece pi from the TotalCoeffs of this MB (lanes' cur), the MB to the
+ * left and the MB above (-1: unavailable at the picture edge) */
+__device__ __attribute__((always_inline)) inline int nc_at(int pi, uint32_t cur, uint32_t left,
+                                                           uint32_t top, int x, int y)
+{
+    int nA, nB;
+    if (pi < 16) {
+        const int bx = pi & 3, by = pi >> 2;
+        nA = bx ? (int)__builtin_amdgcn_readlane(cur, pi - 1)
+                : (x ? (int)__builtin_amdgcn_readlane(left, pi + 3) : -1);
+        nB = by ? (int)__builtin_amdgcn_readlane(cur, pi - 4)
+                : (y ? (int)__builtin_amdgcn_readlane(top, pi + 12) : -1);
+    } else {
+        const int k = (pi - 18) & 3, bx = k & 1, by = k >> 1;
+        nA = bx ? (int)__builtin_amdgcn_readlane(cur, pi - 1)
+                : (x ? (int)__builtin_amdgcn_readlane(left, pi + 1) : -1);
+        nB = by ? (int)__builtin_amdgcn_readlane(cur, pi - 2)
+                : (y ? (int)__builtin_amdgcn_readlane(top, pi + 2) : -1);
+    }
+    return nc2(nA, nB);
+}
+
+/* wave-uniform (ref, mv) */
+struct UMv {
+    int ref, mx, my;
+};
+
+struct ParseLds {
+    int32_t mref[2][PARSE_MAXW], mmx[2][PARSE_MAXW], mmy[2][PARSE_MAXW];  /* rows y-1, y by parity */
+    uint8_t tcrow[PARSE_MAXW][SPLICE_PIECES];                              /* TotalCoeffs, row above */
+};
 
 __global__ __launch_bounds__(64) void k_splice_parse(int n, const int32_t *__restrict__ list,
                                                      SpliceFrame *__restrict__ spf,
                                                      const DevStream *__restrict__ st, int ld_fr,
-                                                     const uint8_t *__restrict__ nal,
                                                      uint32_t *__restrict__ rbsp,
                                                      SpliceMbRec *__restrict__ recs)
 {
-    const int i = blockIdx.x * 64 + threadIdx.x;
+    __shared__ ParseLds L;
+    const int i = blockIdx.x, lane = threadIdx.x;
     if (i >= n) return;
     const int idx = list[i];
     SpliceFrame *F = spf + idx;
     const DevStream S = st[idx / ld_fr];
-    const uint8_t *p = nal + F->nal_off;
+    const uint8_t *p = F->nal;
     uint32_t len = F->nal_len;
     int status = SCROLL_SPLICE_ERR_NAL;
     if (len >= 4 && !p[0] && !p[1] && !p[2] && p[3] == 1) {
@@ -243,30 +388,48 @@ __global__ __launch_bounds__(64) void k_splice_parse(int n, const int32_t *__res
     }
     SpliceMbRec *rec = recs + F->rec_first;
     const int W = F->w, H = F->h, nmb = W * H;
-    if (len < 2 || (p[0] & 0x80) || (p[0] & 31) != 1) {
-        F->status = status;
+    if (len < 2 || (p[0] & 0x80) || (p[0] & 31) != 1 || W > PARSE_MAXW) {
+        if (lane == 0) F->status = len >= 2 && W > PARSE_MAXW ? SCROLL_SPLICE_ERR_HEADER : status;
         return;
     }
     const int ref_idc = (p[0] >> 5) & 3;
-    /* emulation prevention bytes out (7.4.1), MSB-first words */
+    /* emulation prevention bytes out (7.4.1): byte i of the payload goes
+     * unless it is 03 after two zero bytes; 4 bytes per lane per pass, the
+     * output index by a wave prefix count; bytes land MSB-first in words
+     * (byte k at byte address k ^ 3) */
     uint32_t *o = rbsp + F->rbsp_word;
-    uint32_t acc = 0, nb = 0;
-    int zeros = 0;
-    for (uint32_t k = 1; k < len; ++k) {
-        const uint32_t c = p[k];
-        if (zeros >= 2 && c == 3u) {
-            zeros = 0;
-            continue;
+    const uint32_t nwmax = (len + 3u) / 4u + 2u;
+    for (uint32_t k = (uint32_t)lane; k < nwmax; k += 64) o[k] = 0u;
+    __syncthreads();
+    uint8_t *ob = reinterpret_cast<uint8_t *>(o);
+    uint32_t nb = 0;
+    for (uint32_t c0 = 1; c0 < len; c0 += 256) {
+        uint32_t keep = 0, cnt = 0;
+        uint8_t by[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint32_t k = c0 + 4u * (uint32_t)lane + (uint32_t)q;
+            by[q] = k < len ? p[k] : 0;
+            const bool ep = k < len && k >= 3 && by[q] == 3 && p[k - 1] == 0 && p[k - 2] == 0;
+            const bool kp = k < len && !ep;
+            keep |= kp ? 1u << q : 0u;
+            cnt += kp ? 1u : 0u;
         }
-        acc = (acc << 8) | c;
-        if ((++nb & 3u) == 0) {
-            o[(nb >> 2) - 1] = acc;
-            acc = 0;
-        }
-        zeros = c ? 0 : zeros + 1;
+        const uint32_t incl = wave_incl_sum(cnt, lane);
+        uint32_t at = nb + incl - cnt;
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            if (keep & (1u << q)) {
+                ob[at ^ 3u] = by[q];
+                at++;
+            }
+        nb += __builtin_amdgcn_readlane(incl, 63);
     }
-    if (nb & 3u) o[nb >> 2] = acc << (8u * (4u - (nb & 3u)));
-    Rd r{o, (nb + 3u) >> 2, 8u * nb, 0, false};
+    __syncthreads();
+    nb = __builtin_amdgcn_readfirstlane(nb);
+    WRd r{o, (nb + 3u) >> 2, 8u * nb, 0, 0, 0, false};
+    r.fill(0);
+    const LaneTabs T = lane_tabs();
 
     status = SCROLL_SPLICE_ERR_HEADER;
     int nrefs = 2;                         /* the composer's PPS (h264_writer.c:114) */
@@ -284,11 +447,21 @@ __global__ __launch_bounds__(64) void k_splice_parse(int n, const int32_t *__res
         if (k > 31) goto done;
         nrefs = (int)k + 1;
     }
-    if (r.u(1)) goto done;                                         /* list modification */
+    if (r.u(1)) {                          /* list modification: the composed list only */
+        for (int k = 0;; ++k) {
+            const uint32_t idc = r.ue();
+            if (r.bad || r.over() || k > 32) {
+                status = SCROLL_SPLICE_ERR_SYNTAX;
+                goto done;
+            }
+            if (idc == 3) break;
+            if (idc != 2 || r.ue() != (uint32_t)k) goto done;
+        }
+    }
     if (ref_idc && r.u(1)) {                                       /* MMCO */
         for (int k = 0;; ++k) {
             const uint32_t op = r.ue();
-            if (r.bad || k > 64 || op > 6) {
+            if (r.bad || r.over() || k > 64 || op > 6) {
                 status = SCROLL_SPLICE_ERR_SYNTAX;
                 goto done;
             }
@@ -303,55 +476,80 @@ __global__ __launch_bounds__(64) void k_splice_parse(int n, const int32_t *__res
     if (qp < 0 || qp > 51) goto done;
     if (S.deblock && r.ue() != 1) goto done;
     status = SCROLL_SPLICE_ERR_SYNTAX;
-    if (r.bad) goto done;
+    if (r.bad || r.over()) goto done;
     {
         int m = 0, qp_c = 26;
         const Mv none{-1, 0, 0};
+        uint32_t tc_left = 0;              /* lane j: TotalCoeff of piece j, MB to the left */
+        Mv left{-1, 0, 0};
+        /* motion of MB (x, y) from the LDS rows */
+        auto ctx = [&](int x, int y, Mv &A, Mv &B, Mv &C) {
+            const int py = (y - 1) & 1;
+            A = x ? left : none;
+            auto at = [&](int xx) { return Mv{L.mref[py][xx], L.mmx[py][xx], L.mmy[py][xx]}; };
+            B = y ? at(x) : none;
+            C = y ? (x + 1 < W ? at(x + 1) : (x ? at(x - 1) : none)) : none;
+        };
+        auto finish = [&](int x, int y, const Mv &me) {    /* context for the MBs to come */
+            if (lane == 0) {
+                L.mref[y & 1][x] = me.ref;
+                L.mmx[y & 1][x] = me.mx;
+                L.mmy[y & 1][x] = me.my;
+            }
+            left = me;
+        };
         while (m < nmb) {
             const uint32_t run = r.ue();
-            if (r.bad || run > (uint32_t)(nmb - m)) goto done;
+            if (r.bad || r.over() || run > (uint32_t)(nmb - m)) goto done;
             for (uint32_t k = 0; k < run; ++k, ++m) {             /* P_Skip */
                 const int x = m % W, y = m / W;
-                const Mv A = x ? rec_mv(rec, m - 1) : none;
-                const Mv B = y ? rec_mv(rec, m - W) : none;
-                const Mv C = y ? (x + 1 < W ? rec_mv(rec, m - W + 1) : (x ? rec_mv(rec, m - W - 1) : none)) : none;
+                Mv A, B, C;
+                ctx(x, y, A, B, C);
                 int px, py;
                 pskip_mv(x, y, A, B, C, px, py);
-                SpliceMbRec z{};
-                z.ref = 0;
-                z.mx = px;
-                z.my = py;
-                z.skip = 1;
-                rec[m] = z;
+                SpliceMbRec *R = rec + m;
+                if (lane == 0) {
+                    R->ref = 0;
+                    R->cbp = 0;
+                    R->qpd = 0;
+                    R->mx = px;
+                    R->my = py;
+                    R->skip = 1;
+                }
+                if (lane < SPLICE_PIECES) {
+                    R->tc[lane] = 0;
+                    R->t1[lane] = 0;
+                    R->blen[lane] = 0;
+                    R->boff[lane] = 0;
+                    L.tcrow[x][lane] = 0;
+                }
+                tc_left = 0;
+                finish(x, y, Mv{0, px, py});
             }
             if (m == nmb) break;
             const int x = m % W, y = m / W;
             if (r.ue() != 0) {                                     /* mb_type */
-                status = r.bad ? SCROLL_SPLICE_ERR_SYNTAX : SCROLL_SPLICE_ERR_MBTYPE;
+                status = r.bad || r.over() ? SCROLL_SPLICE_ERR_SYNTAX : SCROLL_SPLICE_ERR_MBTYPE;
                 goto done;
             }
             int ref = 0;
             if (nrefs == 2) ref = 1 - (int)r.u(1);
             else if (nrefs > 2) ref = (int)r.ue();
             const int dx = r.se(), dy = r.se();
-            const Mv A = x ? rec_mv(rec, m - 1) : none;
-            const Mv B = y ? rec_mv(rec, m - W) : none;
-            const Mv C = y ? (x + 1 < W ? rec_mv(rec, m - W + 1) : (x ? rec_mv(rec, m - W - 1) : none)) : none;
+            Mv A, B, C;
+            ctx(x, y, A, B, C);
             int px, py;
             predict_spec(A, B, C, ref, px, py);
             const long long mx = (long long)px + dx, my = (long long)py + dy;
             const uint32_t code = r.ue();
-            int cbp = -1;
-            for (int c = 0; c < 48; ++c)
-                if (SPT.cbp_code[c] == code) cbp = c;
-            if (r.bad || ref >= nrefs || cbp < 0 || mx < -SPLICE_MAX_MV || mx > SPLICE_MAX_MV ||
+            const uint64_t cm = __ballot(T.cbp == code);
+            const int cbp = first_lane(cm);
+            if (r.bad || r.over() || ref >= nrefs || cbp < 0 || mx < -SPLICE_MAX_MV || mx > SPLICE_MAX_MV ||
                 my < -SPLICE_MAX_MV || my > SPLICE_MAX_MV)
                 goto done;
-            SpliceMbRec mb{};
-            mb.ref = (int16_t)ref;
-            mb.mx = (int32_t)mx;
-            mb.my = (int32_t)my;
-            mb.cbp = (uint8_t)cbp;
+            int qpd = 0;
+            /* lane j: piece j of this MB */
+            uint32_t my_tc = 0, my_t1 = 0, my_off = 0, my_len = 0;
             if (cbp) {
                 const int dq = r.se();
                 if (dq < -26 || dq > 25) goto done;
@@ -359,22 +557,45 @@ __global__ __launch_bounds__(64) void k_splice_parse(int n, const int32_t *__res
                 int d = qp - qp_c;                                 /* composed chain from 26 */
                 if (d < -26) d += 52;
                 if (d > 25) d -= 52;
-                mb.qpd = (int8_t)d;
+                qpd = d;
                 qp_c = qp;
-                const uint8_t *L = x ? rec[m - 1].tc : nullptr, *T = y ? rec[m - W].tc : nullptr;
+                const uint32_t tc_top = y && lane < SPLICE_PIECES ? L.tcrow[x][lane] : 0u;
+                PieceOut po{0, 0, 0, 0};
                 for (int blk = 0; blk < 16; ++blk) {
                     if (!(cbp & (1 << (blk >> 2)))) continue;
                     const int pi = blk_raster16(blk);
-                    if (!rd_piece(r, mb, pi, piece_nc(pi, mb.tc, L, T), 16)) goto done;
+                    if (!wrd_piece(r, T, pi, nc_at(pi, po.tc, tc_left, tc_top, x, y), 16, po)) goto done;
                 }
                 if (cbp >> 4) {
-                    if (!rd_piece(r, mb, 16, -1, 4) || !rd_piece(r, mb, 17, -1, 4)) goto done;
+                    if (!wrd_piece(r, T, 16, -1, 4, po) || !wrd_piece(r, T, 17, -1, 4, po)) goto done;
                     if ((cbp >> 4) == 2)
                         for (int pi = 18; pi < 26; ++pi)
-                            if (!rd_piece(r, mb, pi, piece_nc(pi, mb.tc, L, T), 15)) goto done;
+                            if (!wrd_piece(r, T, pi, nc_at(pi, po.tc, tc_left, tc_top, x, y), 15, po))
+                                goto done;
                 }
+                my_tc = po.tc;
+                my_t1 = po.t1;
+                my_off = po.off;
+                my_len = po.len;
             }
-            rec[m] = mb;
+            SpliceMbRec *R = rec + m;
+            if (lane == 0) {
+                R->ref = (int16_t)ref;
+                R->cbp = (uint8_t)cbp;
+                R->qpd = (int8_t)qpd;
+                R->mx = (int32_t)mx;
+                R->my = (int32_t)my;
+                R->skip = 0;
+            }
+            if (lane < SPLICE_PIECES) {
+                R->tc[lane] = (uint8_t)my_tc;
+                R->t1[lane] = (uint8_t)my_t1;
+                R->blen[lane] = (uint16_t)my_len;
+                R->boff[lane] = my_off;
+                L.tcrow[x][lane] = (uint8_t)my_tc;
+            }
+            tc_left = my_tc;
+            finish(x, y, Mv{ref, (int)mx, (int)my});
             ++m;
         }
         /* rbsp_slice_trailing_bits (+ zero bytes of a byte stream) */
@@ -385,10 +606,10 @@ __global__ __launch_bounds__(64) void k_splice_parse(int n, const int32_t *__res
         }
         while (r.p < r.nbits)
             if (r.u(8)) goto done;
-        if (!r.bad) status = SCROLL_SPLICE_OK;
+        if (!r.bad && !r.over()) status = SCROLL_SPLICE_OK;
     }
 done:
-    F->status = status;
+    if (lane == 0) F->status = status;
 }
 
 /* ------------------------------------------------------------------------ */
@@ -703,12 +924,11 @@ __global__ __launch_bounds__(DT) void k_splice_stage(DevStream *__restrict__ st,
 }  // namespace
 
 int splice_launch_parse(hipStream_t hs, int n, const int32_t *list, SpliceFrame *spf,
-                        const DevStream *st, int ld_fr, const uint8_t *nal, uint32_t *rbsp,
-                        SpliceMbRec *rec)
+                        const DevStream *st, int ld_fr, uint32_t *rbsp, SpliceMbRec *rec)
 {
     if (n <= 0) return 0;
-    hipLaunchKernelGGL(k_splice_parse, dim3((n + 63) / 64), dim3(64), 0, hs, n, list, spf, st,
-                       ld_fr, nal, rbsp, rec);
+    hipLaunchKernelGGL(k_splice_parse, dim3(n), dim3(64), 0, hs, n, list, spf, st, ld_fr, rbsp,
+                       rec);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -105,6 +105,11 @@ class ScrollBatchDesc(ctypes.Structure):
                 ("mode", ctypes.c_int)]
 
 
+class ScrollSpliceDesc(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int32) for n in ("s", "f", "x0", "y0", "w", "h")] + [
+        ("nal", ctypes.c_void_p), ("n", ctypes.c_uint64)]
+
+
 class ScrollHintRect(ctypes.Structure):
     """include/composer_batch.h: MBs [x0, x1) x [y0, y1) take reference
     `ref` (0 = A, 1 = B, 2 + i = waypoint i) and displacement (mv_x, mv_y) px"""
@@ -182,6 +187,8 @@ def _load():
                                                    ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                                    ctypes.c_int, ctypes.c_char_p, ctypes.c_size_t]),
         "scroll_batch_clear_splices": (ctypes.c_int, [ctypes.c_void_p]),
+        "scroll_batch_set_splices_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int,
+                                                           P(ScrollSpliceDesc)]),
         "scroll_batch_splice_status": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
                                                       P(ctypes.c_int)]),
         "scroll_batch_ingest": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, P(u8p),
@@ -374,6 +381,10 @@ class Batch:
         self._chk(lib.scroll_batch_copy_output(self.h, s, start, b, n), "copy_output")
         return bytes(b[:n])
 
+    def output_device_ptr(self, s):
+        """device address of stream s's arena (scroll_batch_output_device)"""
+        return lib.scroll_batch_output_device(self.h, s)
+
     def reset_output(self):
         self._chk(lib.scroll_batch_reset_output(self.h), "reset_output")
 
@@ -471,6 +482,14 @@ class Batch:
         nal = bytes(nal)
         self._chk(lib.scroll_batch_set_splice(self.h, s, f, x0, y0, w, h, nal, len(nal)),
                   "set_splice")
+
+    def set_splices_device(self, entries):
+        """entries: [(s, f, x0, y0, w, h, device_ptr, nbytes), ...]"""
+        arr = (ScrollSpliceDesc * max(1, len(entries)))()
+        for i, e in enumerate(entries):
+            arr[i] = ScrollSpliceDesc(*e)
+        self._chk(lib.scroll_batch_set_splices_device(self.h, len(entries), arr),
+                  "set_splices_device")
 
     def clear_splices(self):
         self._chk(lib.scroll_batch_clear_splices(self.h), "clear_splices")

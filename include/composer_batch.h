@@ -226,7 +226,9 @@ int scroll_batch_clear_hints(ScrollBatch *b);
  * 1, CAVLC, first_mb_in_slice 0 and all w*h MBs, parsed with the composed
  * stream's SPS/PPS (log2_max_frame_num, POC type, 2 default references,
  * disable_deblocking_filter_idc 1 when the stream signals deblocking
- * control); no ref_pic_list_modification; MBs P_L0_16x16 or P_Skip;
+ * control); no ref_pic_list_modification, or one that restates the composed
+ * list (op k: long_term_pic_num k, as the composer's own slices write it);
+ * MBs P_L0_16x16 or P_Skip;
  * ref_idx 0 = A, 1 = B, 2 + i = waypoint i of the composed stream; motion
  * vectors are displacements in the composed picture, |mv| <= 16383 quarter
  * pels; CAVLC level_prefix <= 15 (Baseline / Main).
@@ -249,6 +251,19 @@ int scroll_batch_clear_hints(ScrollBatch *b);
 #define SCROLL_SPLICE_ERR_REF     5   /* ref_idx not a valid reference of the frame  */
 int scroll_batch_set_splice(ScrollBatch *b, int s, int f, int x0, int y0, int w, int h,
                             const uint8_t *nal, size_t n);
+/* the same for many frames at once, the NALs already in device memory (e.g.
+ * a dynamic encoder's output arena on the same GPU): nal = device pointer,
+ * read by the next compose (keep it valid and unchanged until that compose
+ * has been synced); n = 0 removes the entry's splice.  Each call marks the
+ * slices changed, so the next compose parses them again (new content in
+ * place needs only another call). */
+typedef struct ScrollSpliceDesc {
+    int32_t s, f;                   /* stream, frame                              */
+    int32_t x0, y0, w, h;           /* MB rect                                    */
+    const uint8_t *nal;             /* device pointer to the external NAL         */
+    uint64_t n;                     /* its bytes                                  */
+} ScrollSpliceDesc;
+int scroll_batch_set_splices_device(ScrollBatch *b, int n, const ScrollSpliceDesc *d);
 int scroll_batch_clear_splices(ScrollBatch *b);
 /* after sync: SCROLL_SPLICE_* of frame f of stream s in the last compose
  * (SCROLL_SPLICE_OK also when the frame has no splice) */

@@ -249,7 +249,16 @@ int or_splice_parse(const or_cfg *c, const or_splice *sp, or_splice_mb *mbs, uin
         if (k > 31) return OR_SPLICE_ERR_HEADER;
         nrefs = (int)k + 1;
     }
-    if (rd_u(&r, 1)) return OR_SPLICE_ERR_HEADER;                /* ref_pic_list_modification */
+    if (rd_u(&r, 1)) {                                            /* ref_pic_list_modification */
+        /* only the composer's own list (h264_writer.c:455-539): op k puts
+         * long_term_pic_num k at index k -- the composed list itself */
+        for (int k = 0;; ++k) {
+            const uint32_t idc = rd_ue(&r);
+            if (r.bad || k > 32) return OR_SPLICE_ERR_SYNTAX;
+            if (idc == 3) break;
+            if (idc != 2 || rd_ue(&r) != (uint32_t)k) return OR_SPLICE_ERR_HEADER;
+        }
+    }
     if (ref_idc && rd_u(&r, 1)) {                                 /* adaptive_ref_pic_marking */
         for (int k = 0;; ++k) {
             const uint32_t op = rd_ue(&r);
@@ -564,7 +573,16 @@ size_t or_ext_slice(uint8_t *dst, size_t cap, const or_cfg *c, int W, int H, uin
     } else {
         or_put(&b, 0, 1);
     }
-    or_put(&b, 0, 1);                                             /* no list modification */
+    if (p->list_mod) {                                            /* ref_pic_list_modification */
+        or_put(&b, 1, 1);
+        for (int k = 0; k < nrefs; ++k) {
+            or_ue(&b, 2);                                         /* long_term_pic_num */
+            or_ue(&b, (uint32_t)(p->list_mod == 2 ? nrefs - 1 - k : k));
+        }
+        or_ue(&b, 3);
+    } else {
+        or_put(&b, 0, 1);
+    }
     if (p->ref_idc) or_put(&b, 0, 1);                             /* sliding window */
     or_se(&b, p->slice_qp_delta);
     if (c->deblock) or_ue(&b, 1);

@@ -17,7 +17,9 @@
  * picture of w x h MBs with the composed stream's SPS/PPS fields
  * (log2_max_frame_num, POC type, num_ref_idx default, deblocking flag); the
  * rect [x0, x0 + w) x [y0, y0 + h) of the composed picture receives its MBs.
- * Supported: first_mb_in_slice 0, no ref_pic_list_modification, no
+ * Supported: first_mb_in_slice 0, no ref_pic_list_modification or one that
+ * restates the composed list (op k: long_term_pic_num k, as the composer's
+ * own slices write it, h264_writer.c:455-539), no
  * deblocking when the PPS allows switching it off (disable_deblocking_filter
  * _idc 1, like the composer's own slices), MBs P_L0_16x16 or P_Skip, any
  * coded_block_pattern, mb_qp_delta and CAVLC residual (level_prefix <= 15).
@@ -108,6 +110,8 @@ typedef struct {
     int ref_idc;                 /* nal_ref_idc (adds dec_ref_pic_marking)      */
     int bad_mb;                  /* -1, or the MB coded with mb_type bad_type   */
     int bad_type;
+    int list_mod;                /* 0 none, 1 the composed list restated (long-term
+                                  * k at index k), 2 reversed (unsupported)      */
 } or_ext_params;
 size_t or_ext_slice(uint8_t *dst, size_t cap, const or_cfg *c, int w, int h, uint32_t seed,
                     const or_ext_params *p);

@@ -241,3 +241,40 @@ def test_persist_remove_and_clear(gpu, oracle):
     for s in range(2):
         assert b.output(s) == want[s], s
     b.close()
+
+
+def test_dynamic_coder_output_spliced_from_device(gpu, oracle):
+    """MASTER_DESIGN 4.2 on one GPU: the dynamic rect coder encodes 400x400
+    pictures (rect = the whole picture); its scroll NALs, left in its device
+    arena, are spliced by device pointer into 1280x720 scroll frames"""
+    import sys, os
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    S, F, W, H = 3, 6, 1280, 720
+    e, ptrs = bench.external_slices(gpu, S, F, 25, 25, 0, 0)
+    offs = synthetic_offsets(S, F, H, first_stream=2)
+    offs[1] = np.arange(492, 498)                         # a waypoint on the way
+    b = gpu.Batch(S, F, 16 << 20)
+    for _ in range(S):
+        b.add_stream(gpu.make_config(W, H))
+    b.set_splices_device([(s, f, 28, 10, 25, 25, p, n) for (s, f), (p, n) in ptrs.items()])
+    b.set_offsets(offs)
+    b.compose(F)
+    assert b.sync() == 0, gpu.last_error()
+    buf = (ctypes.c_uint8 * (16 << 20))()
+    err = ctypes.c_int()
+    for s in range(S):
+        host, pos = e.output(s), 0
+        c = _cfg(oracle, W, H)
+        o = bytearray()
+        for f in range(F):
+            n = ptrs[(s, f)][1]
+            sp = splice_of(28, 10, 25, 25, host[pos:pos + n])
+            pos += n
+            k = oracle.or_compose_splice(buf, len(buf), ctypes.byref(c), int(offs[s, f]), 0, None,
+                                         0, EXACT, ctypes.byref(sp), ctypes.byref(err))
+            assert err.value == 0
+            o += bytes(buf[:k])
+        assert b.output(s) == bytes(o), s
+    b.close()
+    e.close()

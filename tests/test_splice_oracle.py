@@ -63,7 +63,7 @@ def test_ext_slices_parse_like_the_standard_decoder(oracle):
     for seed, kw in enumerate([{}, dict(nrefs=1, max_ref=0), dict(nrefs=5, max_ref=4),
                                dict(skip_pm=900), dict(cbp_pm=1000, big_pm=300),
                                dict(slice_qp_delta=-7, qp_jitter=12), dict(ref_idc=2),
-                               dict(mv_range=4000)]):
+                               dict(mv_range=4000), dict(list_mod=1, nrefs=2, max_ref=1)]):
         w, h = 5 + seed % 3, 4 + seed % 4
         nal = ext_slice(oracle, c, w, h, 100 + seed, **kw)
         e, mbs = _parse(oracle, c, splice_of(0, 0, w, h, nal))
@@ -79,7 +79,7 @@ def test_ext_slices_parse_like_the_standard_decoder(oracle):
 
 
 def _check_frame(oracle, c, off, rects, mode, sp, buf):
-    """compose, decode, compare; returns the NAL"""
+    """compose, decode, compare; returns the decoded composed and external MBs"""
     err = ctypes.c_int()
     c2 = OrCfg.from_buffer_copy(c)
     arr, n = hint_array(rects)
@@ -104,17 +104,20 @@ def _check_frame(oracle, c, off, rects, mode, sp, buf):
                     assert (g["luma"], g["cdc"], g["cac"]) == (e["luma"], e["cdc"], e["cac"])
             else:
                 assert (g["ref"], g["mx"], g["my"]) == field[y][x] and g["cbp"] == 0, (off, mode, x, y)
-    return nal
+    return got, ext
 
 
 def test_spliced_mbs_decode_to_the_external_mbs(oracle):
+    """random rects, external slices and hints over a scroll that crosses the
+    496-px waypoint, so spliced MBs use waypoint references too"""
     rng = random.Random(5)
     buf = (ctypes.c_uint8 * (1 << 20))()
     err = ctypes.c_int()
-    w, h = 320, 256
+    w, h = 256, 720
     c = _cfg(oracle, w, h)
-    for i in range(24):
-        off = oracle.or_synthetic_offset(3, i, h)
+    cov = dict(ref2=0, ext_skip=0, skipped=0)
+    for i in range(20):
+        off = 488 + i                              # 496: a waypoint
         if oracle.or_needs_waypoint(ctypes.byref(c), off):
             oracle.or_waypoint_nal(buf, len(buf), ctypes.byref(c), off)
         refs = _refs(c)
@@ -128,10 +131,17 @@ def test_spliced_mbs_decode_to_the_external_mbs(oracle):
         sp = splice_of(x0, y0, sw, sh, nal)
         rects = random_hints(rng, w // 16, h // 16, refs, nmax=3) if i % 3 == 0 else []
         for mode in (EXACT, PSKIP):
-            _check_frame(oracle, c, off, rects, mode, sp, buf)
+            got, ext = _check_frame(oracle, c, off, rects, mode, sp, buf)
+            cov["ref2"] += sum(m["ref"] >= 2 for row in ext for m in row) * (mode == EXACT)
+            cov["ext_skip"] += sum(m["skip"] for row in ext for m in row) * (mode == EXACT)
+            if mode == PSKIP:
+                cov["skipped"] += sum(got[y][x]["skip"] for y in range(y0, y0 + sh)
+                                      for x in range(x0, x0 + sw))
         k = oracle.or_splice_scroll_nal(buf, len(buf), ctypes.byref(c), off, None, 0, EXACT,
                                         ctypes.byref(sp), ctypes.byref(err))
         assert k > 0
+    # waypoint references, external P_Skip MBs, spliced MBs skipped again
+    assert all(v > 0 for v in cov.values()), cov
 
 
 def test_splice_at_picture_corners_and_whole_picture(oracle):
@@ -204,5 +214,10 @@ def test_errors(oracle):
     assert c.nwp == 0
     bad = ext_slice(oracle, c, 4, 3, 2, nrefs=4, max_ref=3, skip_pm=0)
     assert compose(splice_of(2, 2, 4, 3, bad)) == ERR_REF
+    # reference list: restating the composed list is fine, reordering is not
+    ok = ext_slice(oracle, c, 4, 3, 3, list_mod=1)
+    assert compose(splice_of(2, 2, 4, 3, ok)) == 0
+    bad = ext_slice(oracle, c, 4, 3, 3, list_mod=2)
+    assert compose(splice_of(2, 2, 4, 3, bad)) == ERR_HEADER
     # rect outside the picture
     assert compose(splice_of(14, 2, 4, 3, good)) == ERR_HEADER

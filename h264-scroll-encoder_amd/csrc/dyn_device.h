@@ -322,8 +322,16 @@ __device__ __host__ inline int quant(int w, int pos)
 {
     const int i = pos >> 2, j = pos & 3;
     const int mf = ((i | j) & 1) == 0 ? MF0 : (((i & j) & 1) ? MF1 : MF2);
-    const int bias = w < 0 ? (1 << QBITS) - 1 - QF : QF;
+    /* bias by the sign mask as a bit select (v_bfi): no compare, no VCC */
+    const uint32_t m = (uint32_t)(w >> 31);
+    const int bias = (int)((m & (uint32_t)((1 << QBITS) - 1 - QF)) | (~m & (uint32_t)QF));
     return mad_i24(w, mf, bias) >> QBITS;
+}
+
+/* non-zero bytes of a word (levels packed as int8) */
+__device__ __host__ inline int nz_bytes(uint32_t x)
+{
+    return __builtin_popcount((((x & 0x7f7f7f7fu) + 0x7f7f7f7fu) | x) & 0x80808080u);
 }
 
 /* chroma DC (2x2): qbits + 1, f doubled (|w| <= 16320) */
@@ -549,10 +557,11 @@ __device__ __host__ inline void level_field_bf(int code, int sl, uint32_t &v, in
 /* The nC-independent part of a CAVLC block (everything after coeff_token:
  * trailing-ones signs, levels, total_zeros, run_before) of up to 16 packed
  * int8 levels (scan order, level i in byte i & 3 of word i >> 2), maxc =
- * maxNumCoeff (16 luma, 15 chroma AC; the level bytes past maxc are zero),
- * in one loop over the NON-ZERO levels only, branch-free inside: the wave
- * iterates the max TotalCoeff of its lanes (callers group blocks by
- * TotalCoeff).  run_before codes gather in a 64-bit side register first.
+ * maxNumCoeff (16 luma, 15 chroma AC; the level bytes past maxc are zero):
+ * the trailing-one signs as one field, a loop over the other NON-ZERO
+ * levels (branch-free inside: the wave iterates the max over its lanes;
+ * callers group blocks by TotalCoeff), then a light loop for run_before
+ * while zeros are left, its codes gathered in a 64-bit side register.
  * The levels come by value: an array indexed by a variable would be kept
  * in scratch memory.  Returns TotalCoeff, TrailingOnes in t1o; ok = false
  * when cap or the run register overflowed (cap.n is still exact). */
@@ -569,9 +578,11 @@ __device__ __host__ inline int cavlc_body(CAP &cap, const PTabs &P, uint4 pk, in
         const uint64_t v = (p & 8) ? hi : lo;
         return (int)(int8_t)(uint8_t)(v >> (8 * (p & 7)));
     };
+    /* trailing ones (at most 3 +-1 levels from the top): their signs go out
+     * as one field; the level loop starts below them */
     int t1 = 0;
+    uint32_t sg = 0, m = nz;
     {
-        uint32_t m = nz;
         bool run = true;
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
@@ -579,45 +590,49 @@ __device__ __host__ inline int cavlc_body(CAP &cap, const PTabs &P, uint4 pk, in
             const int v = m ? lev(lo64, hi64, p) : 0;
             run = run && m && (v == 1 || v == -1);
             t1 += run ? 1 : 0;
-            m &= m ? ~(1u << p) : ~0u;
+            sg = run ? (sg << 1) | (v < 0 ? 1u : 0u) : sg;
+            m &= run ? ~(1u << p) : ~0u;
         }
     }
     t1o = t1;
     ok = true;
     if (tc == 0) return 0;
+    cap.put(sg, t1);
     const int hi = top_bit(nz);
     const int tz = hi + 1 - tc;
-    uint64_t runs = 0;
-    int rn = 0, zl = tz, sl = (tc > 10 && t1 < 3) ? 1 : 0, pprev = hi;
-    uint32_t m = nz;
-    for (int k = 0; k < tc; ++k) {
+    int sl = (tc > 10 && t1 < 3) ? 1 : 0;
+    for (int k = t1; k < tc; ++k) {                        /* levels below the trailing ones */
         const int p = top_bit(m);
         m &= ~(1u << p);
         const int v = lev(lo64, hi64, p);
         const int a = v < 0 ? -v : v;
-        const bool sgn = k < t1;
         int code = 2 * a - 2 + (v < 0 ? 1 : 0);
         code -= (k == t1 && t1 < 3) ? 2 : 0;
         uint32_t fv;
         int fl;
         level_field_bf(code, sl, fv, fl);
-        cap.put(sgn ? (v < 0 ? 1u : 0u) : fv, sgn ? 1 : fl);
+        cap.put(fv, fl);
         const int s1 = sl == 0 ? 1 : sl;
-        sl = sgn ? sl : ((a > (3 << (s1 - 1)) && s1 < 6) ? s1 + 1 : s1);
-        {
-            const bool act = k > 0 && zl > 0;
-            const int run = act ? pprev - p - 1 : 0;
-            const uint32_t e = P.rb[(zl < 7 ? (zl > 0 ? zl : 1) : 7) - 1][run];
-            const int l = act ? (int)(e >> 8) : 0;
-            runs = (runs << l) | (act ? (e & 255u) : 0u);
-            rn += l;
-            zl -= run;
-        }
-        pprev = p;
+        sl = (a > (3 << (s1 - 1)) && s1 < 6) ? s1 + 1 : s1;
     }
     if (tc < maxc) {
         const uint32_t e = P.tz[tc - 1][tz];
         cap.put(e & 255u, (int)(e >> 8));
+    }
+    /* run_before: between consecutive non-zero levels from the top, while
+     * zeros are left; the codes gather in a 64-bit register first */
+    uint64_t runs = 0;
+    int rn = 0, zl = tz, pprev = hi;
+    uint32_t mm = nz & ~(1u << hi);
+    for (int k = 1; k < tc && zl > 0; ++k) {
+        const int p = top_bit(mm);
+        mm &= ~(1u << p);
+        const int run = pprev - p - 1;
+        const uint32_t e = P.rb[(zl < 7 ? zl : 7) - 1][run];
+        runs = (runs << (e >> 8)) | (e & 255u);
+        rn += (int)(e >> 8);
+        zl -= run;
+        pprev = p;
     }
     if (rn > 64) {
         ok = false;

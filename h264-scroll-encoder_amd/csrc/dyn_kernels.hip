@@ -952,7 +952,6 @@ __device__ inline void row_levels(bool luma, const BlkPix &px, uint32_t pk[4], i
         for (int k2 = 0; k2 < 16; ++k2) {
             const int v = quant(W[ZZ[k2]], ZZ[k2]);          /* |v| <= 78: int8 */
             pk[k2 >> 2] |= ((uint32_t)v & 255u) << (8 * (k2 & 3));
-            n += v != 0;
         }
     } else {
         w0 = W[0];
@@ -960,9 +959,9 @@ __device__ inline void row_levels(bool luma, const BlkPix &px, uint32_t pk[4], i
         for (int k2 = 1; k2 < 16; ++k2) {
             const int v = quant(W[ZZ[k2]], ZZ[k2]);
             pk[(k2 - 1) >> 2] |= ((uint32_t)v & 255u) << (8 * ((k2 - 1) & 3));
-            n += v != 0;
         }
     }
+    n = nz_bytes(pk[0]) + nz_bytes(pk[1]) + nz_bytes(pk[2]) + nz_bytes(pk[3]);
 }
 
 __device__ inline int row_slot(int task, int w)

@@ -255,15 +255,17 @@ def idct4x4(d):
     return out
 
 
-def slice_header(nal, log2_mfn=4, poc_type=2, log2_poc=4, deblock=1):
-    """-> (header dict, Bits positioned at the first MB, RBSP bytes)"""
+def slice_header(nal, log2_mfn=4, poc_type=2, log2_poc=4, deblock=1, nrefs_default=1):
+    """-> (header dict, Bits positioned at the first MB, RBSP bytes);
+    nrefs_default: num_ref_idx_l0_active without an override (the composer's
+    PPS: 2)"""
     assert nal[:4] == b"\x00\x00\x00\x01"
     ref_idc = nal[4] >> 5
     b = Bits(ebsp_to_rbsp(nal[5:]))
     H = {"first_mb": b.ue(), "slice_type": b.ue(), "pps": b.ue(), "frame_num": b.u(log2_mfn)}
     if poc_type == 0:
         H["poc"] = b.u(log2_poc)
-    nrefs = 1
+    nrefs = nrefs_default
     if b.u(1):
         nrefs = b.ue() + 1
     H["nrefs"] = nrefs

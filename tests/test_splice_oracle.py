@@ -221,3 +221,33 @@ def test_errors(oracle):
     assert compose(splice_of(2, 2, 4, 3, bad)) == ERR_HEADER
     # rect outside the picture
     assert compose(splice_of(14, 2, 4, 3, good)) == ERR_HEADER
+
+
+def test_reference_parser_accepts_spliced_nals(oracle):
+    """tests/golden/splice_ref.json: the reference's CAVLC P-slice parser
+    (trans_resizer process_p_slice, built from /root/reference by
+    oracle/Makefile `ref`) consumed the MB layer of every fixture NAL --
+    external slices of the stand-in encoder and composed 320x320 NALs with a
+    spliced rect, both modes, 2 and 3 references -- exactly up to its
+    rbsp_stop_one_bit.  The oracle must still produce those NALs bit for bit;
+    where the reference build exists the parse is repeated live."""
+    import json
+    import os
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, os.path.join(here, "golden"))
+    import make_golden_splice as mg
+    fx = json.load(open(os.path.join(here, "golden", "splice_ref.json")))
+    assert all(c["ref_status"] == 0 and c["ref_end_bit"] == c["stop_bit"] for c in fx)
+    assert {c["kind"] for c in fx} == {"external", "composed"}
+    refso = os.path.join(os.path.dirname(here), "oracle", "_ref", "libref_cavlc.so")
+    ref = ctypes.CDLL(refso) if os.path.exists(refso) else None
+    got = list(mg.cases(oracle))
+    assert len(got) == len(fx)
+    for (c, nal, rbsp), f in zip(got, fx):
+        assert c["sha256"] == f["sha256"] and c["mb_start_bit"] == f["mb_start_bit"]
+        if ref is not None:
+            end = ctypes.c_size_t()
+            assert ref.ref_cavlc_parse(rbsp, len(rbsp), c["mb_start_bit"], c["nrefs"],
+                                       ctypes.byref(end)) == 0
+            assert end.value == c["stop_bit"]

@@ -539,19 +539,23 @@ constexpr PTabs make_ptabs(const Tabs &T)
     return P;
 }
 
-/* level_prefix / level_suffix as one field, branch-free (9.2.2.1) */
+/* level_prefix / level_suffix as one field, branch-free (9.2.2.1): the
+ * common case (level_prefix = code >> sl, sl suffix bits) and the two
+ * escapes (sl = 0: prefix 14 with a 4-bit suffix for codes 14..29; prefix 15
+ * with a 12-bit suffix past the range) merged by bit masks -- written with
+ * selects, the compiler made exec-mask branches of them */
 __device__ __host__ inline void level_field_bf(int code, int sl, uint32_t &v, int &len)
 {
-    const bool s0 = sl == 0;
-    const int lim = s0 ? 14 : (15 << sl);
-    int prefix = code >> sl, ssize = sl, suffix = code & ((1 << sl) - 1);
-    const bool mid = s0 && code >= 14 && code < 30;        /* level_prefix 14, 4-bit suffix */
-    const bool esc = s0 ? code >= 30 : code >= lim;        /* level_prefix 15, 12-bit suffix */
-    prefix = mid ? 14 : (esc ? 15 : prefix);
-    ssize = mid ? 4 : (esc ? 12 : ssize);
-    suffix = mid ? code - 14 : (esc ? code - (s0 ? 30 : lim) : suffix);
-    v = (1u << ssize) | (uint32_t)suffix;
-    len = prefix + 1 + ssize;
+    const int lim = sl ? (15 << sl) : 30;                  /* first escaped code */
+    const uint32_t me = 0u - (uint32_t)(code >= lim);      /* prefix 15, 12-bit suffix */
+    const uint32_t mm = 0u - (uint32_t)(sl == 0 && code >= 14 && code < 30);   /* prefix 14, 4-bit */
+    const uint32_t mc = ~(me | mm);
+    const uint32_t prefix = ((uint32_t)(code >> sl) & mc) | (14u & mm) | (15u & me);
+    const uint32_t ssize = ((uint32_t)sl & mc) | (4u & mm) | (12u & me);
+    const uint32_t suffix = ((uint32_t)(code & ((1 << sl) - 1)) & mc) | ((uint32_t)(code - 14) & mm) |
+                            ((uint32_t)(code - lim) & me);
+    v = (1u << ssize) | suffix;
+    len = (int)(prefix + 1u + ssize);
 }
 
 /* The nC-independent part of a CAVLC block (everything after coeff_token:

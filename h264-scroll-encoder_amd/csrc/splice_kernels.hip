@@ -91,11 +91,16 @@ struct WRd {
     uint32_t nw, nbits, p, base;
     uint32_t win;                        /* word base + lane */
     bool bad;                            /* ue() without a 1 bit; p > nbits is checked per MB */
+    /* the wait sits in the (rare) refill branch: otherwise the compiler
+     * waits for vmcnt(0) before every readlane of the window -- and on gfx9
+     * vmcnt also counts the record stores, so every read would wait for
+     * the last MB's stores to drain */
     __device__ inline void fill(uint32_t k0)
     {
         base = k0;
         const uint32_t k = k0 + (uint32_t)(threadIdx.x & 63);
         win = k < nw ? w[k] : 0u;
+        asm volatile("s_waitcnt vmcnt(0)" : "+v"(win)::"memory");
     }
     /* the 32 bits at p: words k, k + 1 of the window by readlane (scalar),
      * joined by a 64-bit scalar shift */

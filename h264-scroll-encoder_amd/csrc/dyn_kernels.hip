@@ -927,6 +927,19 @@ __device__ inline void row_fetch(int task, int w, int ry, const DynGeom &g, __am
     }
 }
 
+/* ((8 - f) b + f c + 4) >> 3 for the four bytes of b, c: even and odd bytes
+ * as two 16-bit halves each (at most 2,044: no carry between halves), two
+ * 24-bit multiply-adds per half pair */
+__device__ inline uint32_t bilin4(uint32_t b, uint32_t c, uint32_t f)
+{
+    const uint32_t g = 8u - f;
+    const uint32_t be = b & 0x00ff00ffu, bo = (b >> 8) & 0x00ff00ffu;
+    const uint32_t ce = c & 0x00ff00ffu, co = (c >> 8) & 0x00ff00ffu;
+    const uint32_t ve = __umul24(g, be) + __umul24(f, ce) + 0x00040004u;
+    const uint32_t vo = __umul24(g, bo) + __umul24(f, co) + 0x00040004u;
+    return ((ve >> 3) & 0x00ff00ffu) | (((vo >> 3) & 0x00ff00ffu) << 8);
+}
+
 /* residual -> transform -> quant: pk = 16 int8 levels in scan order (AC: 15,
  * from scan index 1), n = TotalCoeff, w0 = chroma DC coefficient
  * (unquantised) */
@@ -936,15 +949,21 @@ __device__ inline void row_levels(bool luma, const BlkPix &px, uint32_t pk[4], i
     n = 0;
     w0 = 0;
     int res[16], W[16];
+    /* prediction rows as packed bytes: luma as fetched, chroma bilinear (one
+     * branch for the block, not one per pixel) */
+    uint32_t pr[4];
+    if (luma) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) pr[i] = px.b[i];
+    } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) pr[i] = bilin4(px.b[i], px.c[i], (px.fr >> (3 * i)) & 7u);
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-        const int f = luma ? 0 : (int)((px.fr >> (3 * i)) & 7u);
 #pragma unroll
-        for (int x = 0; x < 4; ++x) {
-            const int a = (int)((px.b[i] >> (8 * x)) & 255u), c = (int)((px.c[i] >> (8 * x)) & 255u);
-            const int pred = luma ? a : (((8 - f) * a + f * c + 4) >> 3);
-            res[4 * i + x] = (int)((px.a[i] >> (8 * x)) & 255u) - pred;
-        }
+        for (int x = 0; x < 4; ++x)
+            res[4 * i + x] = (int)((px.a[i] >> (8 * x)) & 255u) - (int)((pr[i] >> (8 * x)) & 255u);
     }
     fwd4x4(res, W);
     if (luma) {

@@ -835,25 +835,30 @@ constexpr int ROW_MAXT = 1024;
 #define SCROLL_ROW_NP 3
 #endif
 constexpr int ROW_NPMAX = 8;                    /* tasks per thread at most (1536 tasks / 192) */
-constexpr int ROW_GB = 1024;                    /* bit window: 32 Kbit (a config-3 row ~18 Kbit, one pass) */
+#ifndef SCROLL_ROW_GB
+#define SCROLL_ROW_GB 896
+#endif
+constexpr int ROW_GB = SCROLL_ROW_GB;           /* bit window: 28 Kbit (a config-3 row ~18 Kbit, one pass) */
 
 struct RowFixed {
     PTabs ptabs;
-    uint32_t buf[ROW_GB];
+    union {                                      /* the sort's counts are dead before the bit window */
+        uint32_t buf[ROW_GB];
+        uint16_t wc[48][SORT_KEYS];              /* blocks per (virtual wave, TotalCoeff class): 24 w / 64 */
+    };
     uint64_t hhi[12], hlo[12];
     uint32_t hlen[12];
     int32_t wo[8], wl[8], wv[8];
     int32_t head_over;
     uint32_t rt[32];                             /* the row's prediction-row table (k_dyn_rows) */
-    uint16_t wc[48][SORT_KEYS];                  /* blocks per (virtual wave, TotalCoeff class): 24 w / 64 */
 };
 
 /* dynamic LDS of k_dyn_row: lv [NPC w] uint4 (levels, then bodies), mbits
- * [w] u32, moff [mbw + 1] u32, mt / lo / off16 [NPC w] u16, order [24 w]
- * u16, ta [8 w] u8 (top TotalCoeffs), cbp / code [w] u8 */
+ * [w] u32, moff [mbw + 1] u32, mt / lo / off16 [NPC w] u16 (the sort's
+ * order [24 w] u16 lives in off16 until phase 4), ta [8 w] u8 (top TotalCoeffs), cbp / code [w] u8 */
 __host__ __device__ inline size_t row_lds_bytes(int w, int mbw)
 {
-    return (size_t)16 * NPC * w + (size_t)4 * (w + mbw + 1) + (size_t)2 * (3 * NPC * w + 24 * w) +
+    return (size_t)16 * NPC * w + (size_t)4 * (w + mbw + 1) + (size_t)2 * (3 * NPC * w) +
            (size_t)10 * w + 16;
 }
 
@@ -1026,8 +1031,8 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
     uint4 *lv = rdyn;
     uint32_t *mbits = reinterpret_cast<uint32_t *>(lv + npc), *moff = mbits + w;
     uint16_t *mt = reinterpret_cast<uint16_t *>(moff + mbw + 1), *lo = mt + npc, *off16 = lo + npc;
-    uint16_t *order = off16 + npc;
-    uint8_t *ta = reinterpret_cast<uint8_t *>(order + ntask), *cbpa = ta + 8 * w, *codea = cbpa + w;
+    uint16_t *order = off16;                          /* CAVLC phase only; off16 is phase 4's */
+    uint8_t *ta = reinterpret_cast<uint8_t *>(off16 + npc), *cbpa = ta + 8 * w, *codea = cbpa + w;
 
     if (t < 8) {
         L.wo[t] = pend[s].wo[t];

@@ -1415,7 +1415,12 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
  * so neighbouring lanes read neighbouring row-stage words, and the loads of
  * the next chunk are in flight while this one is scanned.  EP positions go
  * to the slot tail; sets rbsp_bytes / ep / err. */
-constexpr int ST_T = 256, ST_NW = ST_T / 64, ST_CHUNK = ST_T * 32, ST_KW = ST_CHUNK / 4 / ST_T;
+#ifndef SCROLL_ST_KW
+#define SCROLL_ST_KW 4
+#endif
+/* ST_KW words per thread and chunk (4 or 8) */
+constexpr int ST_T = 256, ST_NW = ST_T / 64, ST_KW = SCROLL_ST_KW, ST_CHUNK = ST_T * 4 * ST_KW;
+static_assert(ST_KW % 4 == 0, "the EP scan reads 16-byte LDS vectors");
 static_assert(DYN_MAX_H + 2 * ((DYN_MAX_MBH + DYN_STATIC_ROWS - 1) / DYN_STATIC_ROWS) <= 64,
               "k_dyn_stitch scans the row groups with one wave");
 
@@ -1575,17 +1580,17 @@ __global__ __launch_bounds__(ST_T) void k_dyn_stitch(DevStream *__restrict__ st,
         if (c0 + ST_CHUNK < nin) stitch_load(ld, c0 + ST_CHUNK, t, ng, T, goff, gb, gw, fr);
         lds_barrier();                                  /* the next chunk's loads stay in flight */
         if (stp && c0 == 0) stp[2] = __builtin_amdgcn_s_memrealtime();
-        /* emulation prevention of this thread's 32 contiguous bytes */
-        const uint32_t ib = c0 + 32u * (uint32_t)t;
-        uint32_t wv[8];
-        {
-            const uint4 a = cbuf4[2 * t], b2 = cbuf4[2 * t + 1];
-            wv[0] = a.x; wv[1] = a.y; wv[2] = a.z; wv[3] = a.w;
-            wv[4] = b2.x; wv[5] = b2.y; wv[6] = b2.z; wv[7] = b2.w;
+        /* emulation prevention of this thread's 4 ST_KW contiguous bytes */
+        const uint32_t ib = c0 + 4u * ST_KW * (uint32_t)t;
+        uint32_t wv[ST_KW];
+#pragma unroll
+        for (int j = 0; j < ST_KW / 4; ++j) {
+            const uint4 a = cbuf4[(ST_KW / 4) * t + j];
+            wv[4 * j] = a.x; wv[4 * j + 1] = a.y; wv[4 * j + 2] = a.z; wv[4 * j + 3] = a.w;
         }
         int lnz = -1;
 #pragma unroll
-        for (int w = 0; w < 8; ++w) {
+        for (int w = 0; w < ST_KW; ++w) {
             const uint32_t m = ib + 4u * w < nin ? wv[w] : 0u;
             if (m) lnz = (int)(ib + 4u * w) + 3 - (__builtin_clz(m) >> 3);
         }
@@ -1595,7 +1600,7 @@ __global__ __launch_bounds__(ST_T) void k_dyn_stitch(DevStream *__restrict__ st,
         carry = max(carry, tot);
         uint32_t ins = 0;
 #pragma unroll
-        for (int i = 0; i < 32; ++i) {
+        for (int i = 0; i < 4 * ST_KW; ++i) {
             const uint32_t gi2 = ib + (uint32_t)i;
             const uint32_t b = gi2 < nin ? (wv[i >> 2] >> (8 * (i & 3))) & 255u : 256u;   /* past the end: never */
             ins |= (ep_insert(b, (int)gi2 - 1 - prev) ? 1u : 0u) << i;

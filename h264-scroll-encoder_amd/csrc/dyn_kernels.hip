@@ -844,7 +844,7 @@ struct RowFixed {
     PTabs ptabs;
     union {                                      /* the sort's counts are dead before the bit window */
         uint32_t buf[ROW_GB];
-        uint16_t wc[48][SORT_KEYS];              /* blocks per (virtual wave, TotalCoeff class): 24 w / 64 */
+        uint32_t kc[2][SORT_KEYS];               /* the sort: blocks per TotalCoeff class, then its base */
     };
     uint64_t hhi[12], hlo[12];
     uint32_t hlen[12];
@@ -1040,6 +1040,7 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
         L.wv[t] = pend[s].wv[t];
     }
     if (t == 0) L.head_over = 0;
+    if (t < SORT_KEYS) L.kc[0][t] = 0u;
     load_ptabs(L.ptabs, t, T);
     if (!general && t < 32) L.rt[t] = rows[nb * (size_t)(32 * g.h) + (t < 16 ? 16 * r + t : 16 * g.h + (t < 24 ? 8 * r + t - 16 : 8 * g.h + 8 * r + t - 24))];
     const NalDesc d = nal[(size_t)s * ld_nal + df.nal];
@@ -1052,9 +1053,15 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
         const __amdgpu_buffer_rsrc_t fs = buf_rsrc(src + (size_t)s * g.src_ld + (size_t)f * g.src_fr,
                                                    (uint32_t)g.src_fr);
         const __amdgpu_buffer_rsrc_t rb = buf_rsrc(refs + (size_t)s * g.ref_ld, 3u * ysz);
+        /* counting sort on TotalCoeff class: a task's rank in its class from
+         * an LDS atomic (the order inside a class does not matter) */
         int keys[ROW_NPMAX];
+        uint32_t ranks[ROW_NPMAX];
 #pragma unroll
-        for (int pa = 0; pa < ROW_NPMAX; ++pa) keys[pa] = SORT_KEYS - 1;
+        for (int pa = 0; pa < ROW_NPMAX; ++pa) {
+            keys[pa] = 0;
+            ranks[pa] = 0;
+        }
         BlkPix nx;                                      /* the next task's pixels, in flight */
         if (t < ntask) row_fetch(t, w, r, g, fs, rb, L.rt, csz, nx);
         for (int pa = 0; pa < np; ++pa) {
@@ -1069,10 +1076,14 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
                 lv[slot] = make_uint4(pk[0], pk[1], pk[2], pk[3]);
                 mt[slot] = (uint16_t)((uint32_t)min(n, 16) << 8);
             }
-            const int key = SORT_KEYS - 1 - min(n, SORT_KEYS - 1);   /* inactive tasks: n = 0 */
+            const int key = SORT_KEYS - 1 - min(n, SORT_KEYS - 1);
+            const uint32_t rk = task < ntask ? atomicAdd(&L.kc[0][key], 1u) : 0u;   /* inactive tasks: none */
 #pragma unroll
             for (int q = 0; q < ROW_NPMAX; ++q)
-                if (q == pa) keys[q] = key;
+                if (q == pa) {
+                    keys[q] = key;
+                    ranks[q] = rk;
+                }
             /* chroma DC: the quad's four DC coefficients -> 2x2 Hadamard,
              * quant -> levels as int16 in the DC slot (coded after the
              * barrier that publishes the CAVLC tables) */
@@ -1087,24 +1098,6 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
                                                   ((uint32_t)q2 & 0xffffu) | (uint32_t)q3 << 16, 0u, 0u);
                 mt[k * NPC + 16 + p] = (uint16_t)((uint32_t)((q0 != 0) + (q1 != 0) + (q2 != 0) + (q3 != 0)) << 8);
             }
-        }
-        /* sort classes: per (virtual wave, key) counts */
-        uint32_t belows[ROW_NPMAX];
-#pragma unroll
-        for (int pa = 0; pa < ROW_NPMAX; ++pa) {
-            belows[pa] = 0;
-            if (pa >= np) continue;
-            const int key = keys[pa];
-            uint32_t bl = 0;
-#pragma unroll
-            for (int k = 0; k < SORT_KEYS; ++k) {
-                const uint64_t m = __ballot(key == k);
-                if (lane == 0) L.wc[pa * nwv + wave][k] = (uint16_t)__popcll(m);
-                if (key == k)
-                    bl = (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
-                                                             __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-            }
-            belows[pa] = bl;
         }
         __syncthreads();                                /* levels, TotalCoeffs, ptabs, counts */
         if (stamps) stv[1] = __builtin_amdgcn_s_memrealtime();
@@ -1136,29 +1129,21 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
                 mt[sl] = (uint16_t)((uint32_t)tc << 8 | M_OVF);       /* levels stay in lv */
             }
         }
-        const int nvw = np * nwv;
-        if (t < SORT_KEYS) {                            /* key k = t: virtual-wave prefixes, key offsets */
-            uint32_t tot = 0;
-            for (int v2 = 0; v2 < nvw; ++v2) tot += L.wc[v2][t];
+        if (t < SORT_KEYS) {                            /* class k = t: its base */
+            const uint32_t tot = L.kc[0][t];
             uint32_t kb = tot;
 #pragma unroll
             for (int dd = 1; dd < 32; dd <<= 1) {
                 const uint32_t o = __shfl_up(kb, dd, 64);
                 if (lane >= dd) kb += o;
             }
-            uint32_t run = kb - tot;
-            for (int v2 = 0; v2 < nvw; ++v2) {
-                const uint32_t c2 = L.wc[v2][t];
-                L.wc[v2][t] = (uint16_t)run;
-                run += c2;
-            }
+            L.kc[1][t] = kb - tot;
         }
         __syncthreads();
 #pragma unroll
-        for (int pa = 0; pa < ROW_NPMAX; ++pa) {        /* inactive tasks sort last, past ntask */
-            if (pa >= np) continue;
-            const int pos = L.wc[pa * nwv + wave][keys[pa]] + (int)belows[pa];
-            if (pos < ntask) order[pos] = (uint16_t)(pa * T + t);
+        for (int pa = 0; pa < ROW_NPMAX; ++pa) {
+            if (pa >= np || pa * T + t >= ntask) continue;
+            order[L.kc[1][keys[pa]] + ranks[pa]] = (uint16_t)(pa * T + t);
         }
         __syncthreads();
         /* CAVLC bodies, largest TotalCoeff first */

@@ -1054,14 +1054,8 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
                                                    (uint32_t)g.src_fr);
         const __amdgpu_buffer_rsrc_t rb = buf_rsrc(refs + (size_t)s * g.ref_ld, 3u * ysz);
         /* counting sort on TotalCoeff class: a task's rank in its class from
-         * an LDS atomic (the order inside a class does not matter) */
-        int keys[ROW_NPMAX];
-        uint32_t ranks[ROW_NPMAX];
-#pragma unroll
-        for (int pa = 0; pa < ROW_NPMAX; ++pa) {
-            keys[pa] = 0;
-            ranks[pa] = 0;
-        }
+         * an LDS atomic (the order inside a class does not matter), kept in
+         * lo[] (phase 3's) until the class bases are known */
         BlkPix nx;                                      /* the next task's pixels, in flight */
         if (t < ntask) row_fetch(t, w, r, g, fs, rb, L.rt, csz, nx);
         for (int pa = 0; pa < np; ++pa) {
@@ -1076,14 +1070,8 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
                 lv[slot] = make_uint4(pk[0], pk[1], pk[2], pk[3]);
                 mt[slot] = (uint16_t)((uint32_t)min(n, 16) << 8);
             }
-            const int key = SORT_KEYS - 1 - min(n, SORT_KEYS - 1);
-            const uint32_t rk = task < ntask ? atomicAdd(&L.kc[0][key], 1u) : 0u;   /* inactive tasks: none */
-#pragma unroll
-            for (int q = 0; q < ROW_NPMAX; ++q)
-                if (q == pa) {
-                    keys[q] = key;
-                    ranks[q] = rk;
-                }
+            if (task < ntask)
+                lo[row_slot(task, w)] = (uint16_t)atomicAdd(&L.kc[0][SORT_KEYS - 1 - min(n, SORT_KEYS - 1)], 1u);
             /* chroma DC: the quad's four DC coefficients -> 2x2 Hadamard,
              * quant -> levels as int16 in the DC slot (coded after the
              * barrier that publishes the CAVLC tables) */
@@ -1140,10 +1128,9 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
             L.kc[1][t] = kb - tot;
         }
         __syncthreads();
-#pragma unroll
-        for (int pa = 0; pa < ROW_NPMAX; ++pa) {
-            if (pa >= np || pa * T + t >= ntask) continue;
-            order[L.kc[1][keys[pa]] + ranks[pa]] = (uint16_t)(pa * T + t);
+        for (int task = t; task < ntask; task += T) {
+            const int slot = row_slot(task, w);
+            order[L.kc[1][SORT_KEYS - 1 - min(tc_of(mt[slot]), SORT_KEYS - 1)] + lo[slot]] = (uint16_t)task;
         }
         __syncthreads();
         /* CAVLC bodies, largest TotalCoeff first */

@@ -804,6 +804,44 @@ __global__ __launch_bounds__(GW) void k_dyn_static(const DevStream *__restrict__
     }
 }
 
+/* a block body of n <= 128 bits held right-aligned in hi:lo -> four words,
+ * MSB first, left-aligned (k_dyn_row's LDS form: the piece writer then
+ * needs only funnel shifts by the token length and the bit position) */
+__device__ inline uint4 body_msb(uint64_t hi, uint64_t lo, uint32_t n)
+{
+    const uint32_t k = 128u - n;
+    uint64_t H, Lw;
+    if (k >= 64u) {
+        H = k >= 128u ? 0ull : lo << (k - 64u);
+        Lw = 0ull;
+    } else {
+        H = k ? (hi << k) | (lo >> (64u - k)) : hi;
+        Lw = lo << k;
+    }
+    return make_uint4((uint32_t)(H >> 32), (uint32_t)H, (uint32_t)(Lw >> 32), (uint32_t)Lw);
+}
+
+/* token (tl <= 16 bits) + MSB-first body b (bl <= 128 bits) ORed into the
+ * LDS window buf = words [p0, p0 + n) at bit pos: the <= 144 bits as five
+ * words shifted by tl, then six words shifted by pos mod 32 (v_alignbit);
+ * words outside the window are dropped (the next pass writes them) */
+__device__ inline void put_piece(uint32_t *buf, uint32_t p0, uint32_t n, uint32_t pos, uint32_t tv, uint32_t tl,
+                                 uint4 b, uint32_t bl)
+{
+    const uint32_t tw = tv & low_mask((int)tl);
+    const uint32_t c0 = __builtin_amdgcn_alignbit(tw, b.x, tl), c1 = __builtin_amdgcn_alignbit(b.x, b.y, tl);
+    const uint32_t c2 = __builtin_amdgcn_alignbit(b.y, b.z, tl), c3 = __builtin_amdgcn_alignbit(b.z, b.w, tl);
+    const uint32_t c4 = __builtin_amdgcn_alignbit(b.w, 0u, tl);
+    const uint32_t sh = pos & 31u;
+    const uint32_t o[6] = {c0 >> sh, __builtin_amdgcn_alignbit(c0, c1, sh), __builtin_amdgcn_alignbit(c1, c2, sh),
+                           __builtin_amdgcn_alignbit(c2, c3, sh), __builtin_amdgcn_alignbit(c3, c4, sh),
+                           __builtin_amdgcn_alignbit(c4, 0u, sh)};
+    const uint32_t nw = (sh + tl + bl + 31u) >> 5, w0 = (pos >> 5) - p0;
+#pragma unroll
+    for (uint32_t j = 0; j < 6; ++j)
+        if (j < nw && w0 + j < n && o[j]) atomicOr(&buf[w0 + j], o[j]);
+}
+
 /* ---------------------------------------------------------------------- */
 /* k_dyn_row: one workgroup per rect MB row of a NAL                       */
 /* ---------------------------------------------------------------------- */
@@ -1111,8 +1149,7 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
             const int tc = cavlc_dc4(cap, L.ptabs, dq);
             if (cap.n <= 128) {
                 mt[sl] = (uint16_t)(cap.n | (uint32_t)tc << 8);
-                lv[sl] = make_uint4((uint32_t)cap.lo, (uint32_t)(cap.lo >> 32), (uint32_t)cap.hi,
-                                    (uint32_t)(cap.hi >> 32));
+                lv[sl] = body_msb(cap.hi, cap.lo, cap.n);
             } else {
                 mt[sl] = (uint16_t)((uint32_t)tc << 8 | M_OVF);       /* levels stay in lv */
             }
@@ -1151,9 +1188,7 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
 #endif
             mt[slot] = ok ? (uint16_t)(cap.n | (uint32_t)tc << 8 | (uint32_t)t1 << 13)
                           : (uint16_t)((uint32_t)tc << 8 | (uint32_t)t1 << 13 | M_OVF);
-            if (ok)
-                lv[slot] = make_uint4((uint32_t)cap.lo, (uint32_t)(cap.lo >> 32), (uint32_t)cap.hi,
-                                      (uint32_t)(cap.hi >> 32));
+            if (ok) lv[slot] = body_msb(cap.hi, cap.lo, cap.n);
         }
     } else {
         /* general path: records of k_dyn_code_general */
@@ -1165,7 +1200,12 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
             const int rec = rec_of(q0 + k, pc, ndt);
             const uint16_t mv = M[rec];
             mt[i] = mv;
-            if ((mv & 255u) || (mv & M_OVF)) lv[i] = get_body(BL, BH, rec, (mv & 255u) > 64u || (mv & M_OVF));
+            if ((mv & 255u) || (mv & M_OVF)) {
+                const uint4 bd = get_body(BL, BH, rec, (mv & 255u) > 64u || (mv & M_OVF));
+                lv[i] = (mv & M_OVF) ? bd
+                                     : body_msb((uint64_t)bd.z | (uint64_t)bd.w << 32,
+                                                (uint64_t)bd.x | (uint64_t)bd.y << 32, mv & 255u);
+            }
         }
         for (int i = t; i < 8 * w; i += T) {
             const int k = i >> 3, e = i & 7;
@@ -1348,16 +1388,9 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
             const int nC = (int)(e >> 11) - 1;
             const uint4 bd = lv[i];
             if (!(mv & M_OVF)) {
-                WSink sk{win, 0, 0, 0};
-                sk.start(pos);
-                if (nC != -1) {
-                    uint32_t tv, tl;
-                    piece_token(ctab, mv, nC, tv, tl);
-                    sk.put(tv, (int)tl);
-                }
-                sk.put_cap(CapSink{(uint64_t)bd.z | (uint64_t)bd.w << 32, (uint64_t)bd.x | (uint64_t)bd.y << 32,
-                                   mv & 255u});
-                sk.finish();
+                uint32_t tv = 0, tl = 0;
+                if (nC != -1) piece_token(ctab, mv, nC, tv, tl);
+                put_piece(L.buf, p0, n, pos, tv, tl, bd, mv & 255u);
             } else {
                 ovf_put(L.buf, p0, n, pos, PT, TB, bd, pc, nC);
             }

@@ -601,51 +601,65 @@ __device__ __host__ inline int cavlc_body(CAP &cap, const PTabs &P, uint4 pk, in
     t1o = t1;
     ok = true;
     if (tc == 0) return 0;
-    cap.put(sg, t1);
+    /* the fields gather in a 64-bit register (right-aligned, an bits) and
+     * go to cap only when it would overflow and at the end */
+    uint64_t acc = sg;
+    uint32_t an = (uint32_t)t1;
+    auto push = [](uint64_t &ac, uint32_t &n, uint32_t v, uint32_t len, CAP &c) {
+        if (n + len > 64u) {                               /* rare: spill */
+            if (n > 32u) c.put((uint32_t)(ac >> 32), (int)(n - 32u));
+            c.put((uint32_t)ac, n > 32u ? 32 : (int)n);
+            ac = 0;
+            n = 0;
+        }
+        ac = (ac << len) | v;
+        n += len;
+    };
     const int hi = top_bit(nz);
     const int tz = hi + 1 - tc;
     int sl = (tc > 10 && t1 < 3) ? 1 : 0;
+    int adj = t1 < 3 ? 2 : 0;                              /* the first level after < 3 trailing ones */
     for (int k = t1; k < tc; ++k) {                        /* levels below the trailing ones */
         const int p = top_bit(m);
         m &= ~(1u << p);
         const int v = lev(lo64, hi64, p);
         const int a = v < 0 ? -v : v;
-        int code = 2 * a - 2 + (v < 0 ? 1 : 0);
-        code -= (k == t1 && t1 < 3) ? 2 : 0;
-        uint32_t fv;
-        int fl;
-        level_field_bf(code, sl, fv, fl);
-        cap.put(fv, fl);
+        const int code = 2 * a - 2 + (v < 0 ? 1 : 0) - adj;
+        adj = 0;
+        /* level_prefix / level_suffix (9.2.2.1): code >> sl zeros and sl
+         * suffix bits; escapes: prefix 14 + 4-bit suffix (sl 0, codes
+         * 14..29), prefix 15 + 12-bit suffix past the range */
+        const int lim = sl ? (15 << sl) : 30;
+        const uint32_t mk = (1u << sl) - 1u;
+        uint32_t fv = ((uint32_t)code & mk) | (mk + 1u);
+        uint32_t fl = (uint32_t)((code >> sl) + 1 + sl);
+        const bool e15 = code >= lim, e14 = sl == 0 && code >= 14;
+        fv = e15 ? (uint32_t)(4096 + code - lim) : (e14 ? (uint32_t)(code + 2) : fv);
+        fl = e15 ? 28u : (e14 ? 19u : fl);
+        push(acc, an, fv, fl, cap);
         const int s1 = sl == 0 ? 1 : sl;
-        sl = (a > (3 << (s1 - 1)) && s1 < 6) ? s1 + 1 : s1;
+        sl = s1 + ((a > (3 << (s1 - 1)) && s1 < 6) ? 1 : 0);
     }
     if (tc < maxc) {
         const uint32_t e = P.tz[tc - 1][tz];
-        cap.put(e & 255u, (int)(e >> 8));
+        push(acc, an, e & 255u, e >> 8, cap);
     }
     /* run_before: between consecutive non-zero levels from the top, while
-     * zeros are left; the codes gather in a 64-bit register first */
-    uint64_t runs = 0;
-    int rn = 0, zl = tz, pprev = hi;
+     * zeros are left */
+    int zl = tz, pprev = hi;
     uint32_t mm = nz & ~(1u << hi);
     for (int k = 1; k < tc && zl > 0; ++k) {
         const int p = top_bit(mm);
         mm &= ~(1u << p);
         const int run = pprev - p - 1;
         const uint32_t e = P.rb[(zl < 7 ? zl : 7) - 1][run];
-        runs = (runs << (e >> 8)) | (e & 255u);
-        rn += (int)(e >> 8);
+        push(acc, an, e & 255u, e >> 8, cap);
         zl -= run;
         pprev = p;
     }
-    if (rn > 64) {
-        ok = false;
-        cap.n += (uint32_t)rn;
-    } else {
-        if (rn > 32) cap.put((uint32_t)(runs >> 32), rn - 32);
-        cap.put((uint32_t)runs, rn > 32 ? 32 : rn);
-    }
-    ok = ok && cap.n <= 128;
+    if (an > 32u) cap.put((uint32_t)(acc >> 32), (int)(an - 32u));
+    cap.put((uint32_t)acc, an > 32u ? 32 : (int)an);
+    ok = cap.n <= 128;
     return tc;
 }
 

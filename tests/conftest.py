@@ -54,8 +54,10 @@ def hostsim():
            os.path.join(PKG, "csrc", "scroll_device.h"),
            os.path.join(PKG, "csrc", "dyn_device.h")]
     if not os.path.exists(so) or any(os.path.getmtime(s) > os.path.getmtime(so) for s in src):
+        tmp = f"{so}.{os.getpid()}"           # build aside, then rename: safe under pytest -n
         subprocess.run(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-I", d,
-                        "-I", os.path.join(PKG, "csrc"), src[0], "-o", so], check=True)
+                        "-I", os.path.join(PKG, "csrc"), src[0], "-o", tmp], check=True)
+        os.replace(tmp, so)
     return ctypes.CDLL(so)
 
 

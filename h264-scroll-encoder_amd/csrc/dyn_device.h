@@ -334,6 +334,19 @@ __device__ __host__ inline int nz_bytes(uint32_t x)
     return __builtin_popcount((((x & 0x7f7f7f7fu) + 0x7f7f7f7fu) | x) & 0x80808080u);
 }
 
+/* bit i = level i != 0 for 16 packed int8 levels (byte i & 3 of word
+ * i >> 2): per word the bytes' "non-zero" flags at bits 7/15/23/31, gathered
+ * to a nibble by one multiply (the partial products do not overlap) */
+__device__ __host__ inline uint32_t nz_nibble(uint32_t x)
+{
+    const uint32_t hb = (((x & 0x7f7f7f7fu) + 0x7f7f7f7fu) | x) & 0x80808080u;
+    return (hb * 0x00204081u) >> 28;
+}
+__device__ __host__ inline uint32_t nz_mask16(uint4 pk)
+{
+    return nz_nibble(pk.x) | nz_nibble(pk.y) << 4 | nz_nibble(pk.z) << 8 | nz_nibble(pk.w) << 12;
+}
+
 /* chroma DC (2x2): qbits + 1, f doubled (|w| <= 16320) */
 __device__ __host__ inline int quant_dc(int w)
 {
@@ -572,10 +585,7 @@ __device__ __host__ inline void level_field_bf(int code, int sl, uint32_t &v, in
 template <class CAP>
 __device__ __host__ inline int cavlc_body(CAP &cap, const PTabs &P, uint4 pk, int maxc, int &t1o, bool &ok)
 {
-    const uint32_t pw[4] = {pk.x, pk.y, pk.z, pk.w};
-    uint32_t nz = 0;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) nz |= (((pw[i >> 2] >> (8 * (i & 3))) & 255u) != 0 ? 1u : 0u) << i;
+    const uint32_t nz = nz_mask16(pk);
     const int tc = __builtin_popcount(nz);
     const uint64_t lo64 = (uint64_t)pk.x | (uint64_t)pk.y << 32, hi64 = (uint64_t)pk.z | (uint64_t)pk.w << 32;
     auto lev = [](uint64_t lo, uint64_t hi, int p) -> int {   /* captures nothing: no lambda object */

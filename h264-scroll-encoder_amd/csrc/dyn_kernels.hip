@@ -1176,6 +1176,7 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
             if (pos >= ntask) continue;
             const int task = order[pos];
             const int slot = row_slot(task, w);
+            if (tc_of(mt[slot]) == 0) continue;     /* no levels: no body (the class sorts them last) */
             const uint4 v4 = lv[slot];
             CapSink cap{0, 0, 0};
             int t1 = 0;

@@ -1026,11 +1026,18 @@ __device__ inline void row_levels(bool luma, const BlkPix &px, uint32_t pk[4], i
     n = nz_bytes(pk[0]) + nz_bytes(pk[1]) + nz_bytes(pk[2]) + nz_bytes(pk[3]);
 }
 
+/* i / NPC for a piece index of a rect row (i < NPC DYN_MAX_W): a 24-bit
+ * multiply by the rounded-up reciprocal instead of the compiler's
+ * quarter-rate high multiply */
+static_assert(NPC == 26 && NPC * DYN_MAX_W < 6577, "div_npc's reciprocal (2521 / 2^16) is exact below 6577");
+__device__ inline int div_npc(int i) { return (int)(__umul24((uint32_t)i, 2521u) >> 16); }
+
 __device__ inline int row_slot(int task, int w)
 {
-    if (task < 16 * w) return (task >> 4) * NPC + (task & 15);
-    const int jj = task - 16 * w;
-    return (jj >> 3) * NPC + 18 + (jj & 7);
+    const int jj = task - 16 * w;                      /* < 0: luma */
+    const bool l = jj < 0;
+    const int k = l ? task >> 4 : jj >> 3, pc = l ? task & 15 : 18 + (jj & 7);
+    return (int)__umul24((uint32_t)k, (uint32_t)NPC) + pc;   /* no quarter-rate multiply */
 }
 
 /* grid (h, frames, streams), row_threads(w) threads, row_lds_bytes dynamic LDS */
@@ -1107,9 +1114,8 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
                 const int slot = row_slot(task, w);
                 lv[slot] = make_uint4(pk[0], pk[1], pk[2], pk[3]);
                 mt[slot] = (uint16_t)((uint32_t)min(n, 16) << 8);
+                lo[slot] = (uint16_t)atomicAdd(&L.kc[0][SORT_KEYS - 1 - min(n, SORT_KEYS - 1)], 1u);
             }
-            if (task < ntask)
-                lo[row_slot(task, w)] = (uint16_t)atomicAdd(&L.kc[0][SORT_KEYS - 1 - min(n, SORT_KEYS - 1)], 1u);
             /* chroma DC: the quad's four DC coefficients -> 2x2 Hadamard,
              * quant -> levels as int16 in the DC slot (coded after the
              * barrier that publishes the CAVLC tables) */
@@ -1197,7 +1203,7 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
         const uint16_t *M = meta + nb * (size_t)(NPC * ndt);
         const uint2 *BL = blo + nb * (size_t)(NPC * ndt), *BH = bhi + nb * (size_t)(NPC * ndt);
         for (int i = t; i < npc; i += T) {
-            const int k = i / NPC, pc = i - k * NPC;
+            const int k = div_npc(i), pc = i - k * NPC;
             const int rec = rec_of(q0 + k, pc, ndt);
             const uint16_t mv = M[rec];
             mt[i] = mv;
@@ -1249,7 +1255,7 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
     const PTabs &PT = *reinterpret_cast<const PTabs *>(&g_ptabs);       /* the rare overflow paths */
     const uint16_t(*ctab)[68] = L.ptabs.ct;
     for (int i = t; i < npc; i += T) {
-        const int k = i / NPC, pc = i - k * NPC, col = R.x0 + k;
+        const int k = div_npc(i), pc = i - k * NPC, col = R.x0 + k;
         const uint32_t mv = mt[i];
         const uint16_t *mk = mt + k * NPC;
         uint32_t tv = 0, tl = 0;
@@ -1382,7 +1388,7 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
         for (int i = t; i < npc; i += T) {
             const uint32_t o = off16[i];
             if (o == 0xffffu) continue;
-            const int k = i / NPC, pc = i - k * NPC;
+            const int k = div_npc(i), pc = i - k * NPC;
             const uint32_t e = lo[i], mv = mt[i];
             const uint32_t pos = moff[R.x0 + k] + o;
             if (pos >= 32u * (p0 + n) || pos + (e & LO_LEN) <= 32u * p0) continue;

@@ -1176,6 +1176,9 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
             order[L.kc[1][SORT_KEYS - 1 - min(tc_of(mt[slot]), SORT_KEYS - 1)] + lo[slot]] = (uint16_t)task;
         }
         __syncthreads();
+#if defined(SCROLL_ABL_STOP) && SCROLL_ABL_STOP == 1
+        return;
+#endif
         /* CAVLC bodies, largest TotalCoeff first */
         for (int pa = 0; pa < np; ++pa) {
             const int pos = pa * T + t;
@@ -1239,6 +1242,9 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
     }
     __syncthreads();                                    /* records, top TotalCoeffs, waypoint table */
     if (stamps) stv[2] = __builtin_amdgcn_s_memrealtime();
+#if defined(SCROLL_ABL_STOP) && SCROLL_ABL_STOP == 2
+    return;
+#endif
 
     /* ---- 3: coeff_token, piece lengths ----------------------------------- */
     const NalCtx c = nal_ctx(S, d, L.wo, L.wl, L.wv);
@@ -1281,6 +1287,9 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
     }
     __syncthreads();
     if (stamps) stv[3] = __builtin_amdgcn_s_memrealtime();
+#if defined(SCROLL_ABL_STOP) && SCROLL_ABL_STOP == 3
+    return;
+#endif
     const bool head_over = L.head_over;
     auto head_bits = [&](int rr, int col) -> uint32_t {
         if (!head_over) return L.hlen[H.sel(rr, col)];
@@ -1348,6 +1357,9 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
     }
     __syncthreads();
     if (stamps) stv[4] = __builtin_amdgcn_s_memrealtime();
+#if defined(SCROLL_ABL_STOP) && SCROLL_ABL_STOP == 4
+    return;
+#endif
     const uint32_t bits = moff[mbw];
 
     /* ---- 5: bits -> the row's own row-stage words ------------------------ */

@@ -1759,11 +1759,9 @@ __device__ inline uint32_t pick4(const uint32_t w[8], int i)     /* w[i], i in 0
     return (i & 4) ? ce : ab;
 }
 
-#ifndef SCROLL_GATHER_U
-#define SCROLL_GATHER_U 1
-#endif
 constexpr int GATHER_Z = 1;             /* workgroups per NAL (2 and 4 measured slower) */
 
+template <int U>
 __global__ __launch_bounds__(DT) void k_dyn_emit_gather(const DevStream *__restrict__ st,
                                                         const NalDesc *__restrict__ nal, int ld_nal,
                                                         const DynFrame *__restrict__ dfr, int ld_fr,
@@ -1805,10 +1803,6 @@ __global__ __launch_bounds__(DT) void k_dyn_emit_gather(const DevStream *__restr
     const uint64_t o0 = d.out_off, o1 = o0 + d.size;
     const uint32_t nin = df.rbsp_bytes;
     const uint8_t hdr[5] = {0, 0, 0, 1, nal_header_byte(0)};           /* nal.c:59-64 */
-    /* U chunks per thread and iteration, their loads in flight together;
-     * U = 1 (fewer registers, more resident workgroups) measured fastest:
-     * 0.186 / 0.173 / 0.168 ms at U = 4 / 2 / 1 (config 3) */
-    constexpr int U = SCROLL_GATHER_U;
     /* the NAL's 16-byte chunks are split over gridDim.z workgroups */
     const uint64_t cfirst = o0 >> 4, cnal = ((o1 + 15) >> 4) - cfirst;
     const uint64_t per = (cnal + gridDim.z - 1) / gridDim.z;
@@ -2010,8 +2004,16 @@ int dyn_launch_emit(hipStream_t hs, int nframes, int S, const DevStream *st, con
                     const uint8_t *stage, uint8_t *arena, uint64_t ld_arena, uint64_t *stamps)
 {
     if (nframes <= 0 || S <= 0) return 0;
-    hipLaunchKernelGGL(k_dyn_emit_gather, dim3(nframes, S, GATHER_Z), dim3(DT), 0, hs, st, nal, ld_nal, dfr,
-                       ld_fr, *g, stage, arena, ld_arena, stamps);
+    /* U chunks per thread and iteration, their loads in flight together:
+     * one (fewer registers, more resident workgroups) for NALs up to ~64 KB
+     * (config 3: 0.186 / 0.173 / 0.168 ms at U = 4 / 2 / 1), four for the
+     * large rects (config 5: 0.45 ms at U = 4, 0.56 at U = 1) */
+    if ((int64_t)g->w * g->h > 1024)
+        hipLaunchKernelGGL(k_dyn_emit_gather<4>, dim3(nframes, S, GATHER_Z), dim3(DT), 0, hs, st, nal, ld_nal,
+                           dfr, ld_fr, *g, stage, arena, ld_arena, stamps);
+    else
+        hipLaunchKernelGGL(k_dyn_emit_gather<1>, dim3(nframes, S, GATHER_Z), dim3(DT), 0, hs, st, nal, ld_nal,
+                           dfr, ld_fr, *g, stage, arena, ld_arena, stamps);
     if (hipGetLastError() != hipSuccess) return -1;
     hipLaunchKernelGGL(k_dyn_emit, dim3(nframes, S), dim3(DT), 0, hs, st, nal, ld_nal, dfr, ld_fr,
                        *g, stage, arena, ld_arena);

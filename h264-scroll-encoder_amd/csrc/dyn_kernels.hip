@@ -1119,10 +1119,12 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
             /* chroma DC: the quad's four DC coefficients -> 2x2 Hadamard,
              * quant -> levels as int16 in the DC slot (coded after the
              * barrier that publishes the CAVLC tables) */
+            const bool cdc = task >= 16 * w && task < ntask;
+            if (__builtin_amdgcn_ballot_w64(cdc) == 0) continue;   /* luma-only wave: no chroma DC */
             const int qb = lane & ~3;
             const int d0 = __shfl(w0, qb, 64), d1 = __shfl(w0, qb + 1, 64);
             const int d2 = __shfl(w0, qb + 2, 64), d3 = __shfl(w0, qb + 3, 64);
-            if (task >= 16 * w && task < ntask && (task & 3) == 0) {
+            if (cdc && (task & 3) == 0) {
                 const int jj = task - 16 * w, k = jj >> 3, p = (jj >> 2) & 1;
                 const int q0 = quant_dc(d0 + d1 + d2 + d3), q1 = quant_dc(d0 - d1 + d2 - d3);
                 const int q2 = quant_dc(d0 + d1 - d2 - d3), q3 = quant_dc(d0 - d1 - d2 + d3);
@@ -1443,7 +1445,10 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
 #define SCROLL_ST_KW 4
 #endif
 /* ST_KW words per thread and chunk (4 or 8) */
-constexpr int ST_T = 256, ST_NW = ST_T / 64, ST_KW = SCROLL_ST_KW, ST_CHUNK = ST_T * 4 * ST_KW;
+#ifndef SCROLL_ST_T
+#define SCROLL_ST_T 256
+#endif
+constexpr int ST_T = SCROLL_ST_T, ST_NW = ST_T / 64, ST_KW = SCROLL_ST_KW, ST_CHUNK = ST_T * 4 * ST_KW;
 static_assert(ST_KW % 4 == 0, "the EP scan reads 16-byte LDS vectors");
 static_assert(DYN_MAX_H + 2 * ((DYN_MAX_MBH + DYN_STATIC_ROWS - 1) / DYN_STATIC_ROWS) <= 64,
               "k_dyn_stitch scans the row groups with one wave");

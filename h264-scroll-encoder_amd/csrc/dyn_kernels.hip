@@ -863,10 +863,13 @@ __device__ inline void put_piece(uint32_t *buf, uint32_t p0, uint32_t n, uint32_
  * path (k_dyn_rows flags them) take their records from k_dyn_code_general
  * in global memory instead of steps 1-2. */
 constexpr int ROW_MAXT = 1024;
-/* waves per SIMD the register allocation targets (7: <= 72 VGPRs and few
- * enough SGPRs that two or three row workgroups share a CU) */
+/* waves per SIMD the register allocation targets: 8 (eight row workgroups
+ * per CU; the SGPR budget then spills some uniform values to VGPR lanes).
+ * With the general path in its own instantiation the normal one needs 53
+ * VGPRs and 8 beat 7 (1.43 against 1.50 ms); with both paths in one kernel
+ * (63 VGPRs) the spills ate the gain */
 #ifndef SCROLL_ROW_WAVES
-#define SCROLL_ROW_WAVES 7
+#define SCROLL_ROW_WAVES 8
 #endif
 /* block tasks per thread (about: threads = 24 w / NP rounded up to waves) */
 #ifndef SCROLL_ROW_NP
@@ -1040,7 +1043,12 @@ __device__ inline int row_slot(int task, int w)
     return (int)__umul24((uint32_t)k, (uint32_t)NPC) + pc;   /* no quarter-rate multiply */
 }
 
-/* grid (h, frames, streams), row_threads(w) threads, row_lds_bytes dynamic LDS */
+/* grid (h, frames, streams), row_threads(w) threads, row_lds_bytes dynamic LDS.
+ * GEN: the instantiation for the NALs k_dyn_rows flagged for the general
+ * path (records from k_dyn_code_general); the other one codes the rest --
+ * each returns at once for the other's NALs, and neither carries the
+ * other's code (registers) */
+template <bool GEN>
 __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL_ROW_WAVES))) void k_dyn_row(DevStream *__restrict__ st,
                                                      const NalDesc *__restrict__ nal, int ld_nal,
                                                      const PlanPending *__restrict__ pend,
@@ -1063,8 +1071,8 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
     const int t = threadIdx.x, T = blockDim.x, lane = t & 63, wave = t >> 6, nwv = T >> 6;
     const size_t nb = (size_t)s * ld_fr + f;
     const DynFrame df = dfr[nb];
-    if (df.nal < 0) return;
-    const bool general = (df.err & DF_GENERAL) != 0;
+    if (df.nal < 0 || ((df.err & DF_GENERAL) != 0) != GEN) return;
+    constexpr bool general = GEN;
     const Rect R{g.x0, g.y0, g.w, g.h};
     const int w = R.w, ndt = R.w * R.h, row = R.y0 + r, npc = NPC * w, ntask = 24 * w;
     const int ng = g.ngroups;
@@ -1985,9 +1993,13 @@ int dyn_launch_code(hipStream_t hs, int nframes, int S, DevStream *st, const Nal
     hipLaunchKernelGGL(k_dyn_code_general, dim3(nchunk, CODE_GEN_Y), dim3(CODE_T), 0, hs, st, dfr, ld_fr,
                        pend, nal, ld_nal, *g, x->rows, src, refs, x->meta, x->body_lo, x->body_hi, nframes, S);
     if (hipGetLastError() != hipSuccess) return -1;
-    hipLaunchKernelGGL(k_dyn_row, dim3(g->h, nframes, S), dim3(row_threads(g->w)), row_lds_bytes(g->w, mbw), hs,
-                       st, nal, ld_nal, pend, dfr, ld_fr, *g, x->rows, src, refs, x->meta, x->body_lo,
-                       x->body_hi, x->tcx, epoch, x->rowstage, x->gbits, stamps);
+    hipLaunchKernelGGL(k_dyn_row<false>, dim3(g->h, nframes, S), dim3(row_threads(g->w)),
+                       row_lds_bytes(g->w, mbw), hs, st, nal, ld_nal, pend, dfr, ld_fr, *g, x->rows, src, refs,
+                       x->meta, x->body_lo, x->body_hi, x->tcx, epoch, x->rowstage, x->gbits, stamps);
+    if (hipGetLastError() != hipSuccess) return -1;
+    hipLaunchKernelGGL(k_dyn_row<true>, dim3(g->h, nframes, S), dim3(row_threads(g->w)),
+                       row_lds_bytes(g->w, mbw), hs, st, nal, ld_nal, pend, dfr, ld_fr, *g, x->rows, src, refs,
+                       x->meta, x->body_lo, x->body_hi, x->tcx, epoch, x->rowstage, x->gbits, stamps);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

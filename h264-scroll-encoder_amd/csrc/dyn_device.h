@@ -582,12 +582,12 @@ __device__ __host__ inline void level_field_bf(int code, int sl, uint32_t &v, in
  * The levels come by value: an array indexed by a variable would be kept
  * in scratch memory.  Returns TotalCoeff, TrailingOnes in t1o; ok = false
  * when cap or the run register overflowed (cap.n is still exact). */
-template <class CAP>
+template <class CAP, bool LB = false>
 __device__ __host__ inline int cavlc_body(CAP &cap, const PTabs &P, uint4 pk, int maxc, int &t1o, bool &ok,
                                           const int8_t *lb = nullptr)
 {
-    /* lb: the same 16 levels as bytes in LDS (k_dyn_row): one byte read per
-     * level instead of a half select + 64-bit shift + sign extension */
+    /* LB: lb holds the same 16 levels as bytes in LDS (k_dyn_row): one byte
+     * read per level instead of a half select + 64-bit shift + sign extension */
     const uint32_t nz = nz_mask16(pk);
     const int tc = __builtin_popcount(nz);
     const uint64_t lo64 = (uint64_t)pk.x | (uint64_t)pk.y << 32, hi64 = (uint64_t)pk.z | (uint64_t)pk.w << 32;
@@ -604,7 +604,7 @@ __device__ __host__ inline int cavlc_body(CAP &cap, const PTabs &P, uint4 pk, in
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
             const int p = m ? top_bit(m) : 0;
-            const int v = m ? (lb ? (int)lb[p] : lev(lo64, hi64, p)) : 0;
+            const int v = m ? (LB ? (int)lb[p] : lev(lo64, hi64, p)) : 0;
             run = run && m && (v == 1 || v == -1);
             t1 += run ? 1 : 0;
             sg = run ? (sg << 1) | (v < 0 ? 1u : 0u) : sg;
@@ -635,7 +635,7 @@ __device__ __host__ inline int cavlc_body(CAP &cap, const PTabs &P, uint4 pk, in
     for (int k = t1; k < tc; ++k) {                        /* levels below the trailing ones */
         const int p = top_bit(m);
         m &= ~(1u << p);
-        const int v = lb ? (int)lb[p] : lev(lo64, hi64, p);
+        const int v = LB ? (int)lb[p] : lev(lo64, hi64, p);
         const int a = v < 0 ? -v : v;
         const int code = 2 * a - 2 + (v < 0 ? 1 : 0) - adj;
         adj = 0;

@@ -1204,8 +1204,8 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
             const int tc = __builtin_popcount(v4.x | v4.y | v4.z | v4.w) & 15;
             cap.n = tc * 3;
 #else
-            const int tc = cavlc_body(cap, L.ptabs, v4, task < 16 * w ? 16 : 15, t1, ok,
-                                      reinterpret_cast<const int8_t *>(lv + slot));
+            const int tc = cavlc_body<CapSink, true>(cap, L.ptabs, v4, task < 16 * w ? 16 : 15, t1, ok,
+                                                     reinterpret_cast<const int8_t *>(lv + slot));
 #endif
             mt[slot] = ok ? (uint16_t)(cap.n | (uint32_t)tc << 8 | (uint32_t)t1 << 13)
                           : (uint16_t)((uint32_t)tc << 8 | (uint32_t)t1 << 13 | M_OVF);

@@ -670,6 +670,14 @@ __device__ __host__ inline int cavlc_body(CAP &cap, const PTabs &P, uint4 pk, in
         zl -= run;
         pprev = p;
     }
+    if constexpr (LB) {                                    /* CapSink: nothing spilled -> acc is the body */
+        if (cap.n == 0) {
+            cap.lo = acc;
+            cap.n = an;
+            ok = true;
+            return tc;
+        }
+    }
     if (an > 32u) cap.put((uint32_t)(acc >> 32), (int)(an - 32u));
     cap.put((uint32_t)acc, an > 32u ? 32 : (int)an);
     ok = cap.n <= 128;

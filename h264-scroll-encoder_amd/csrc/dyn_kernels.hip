@@ -1181,21 +1181,23 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
             L.kc[1][t] = kb - tot;
         }
         __syncthreads();
-        for (int task = t; task < ntask; task += T) {
+        for (int task = t; task < ntask; task += T) {       /* the slot, chroma flagged in bit 15 */
             const int slot = row_slot(task, w);
-            order[L.kc[1][SORT_KEYS - 1 - min(tc_of(mt[slot]), SORT_KEYS - 1)] + lo[slot]] = (uint16_t)task;
+            order[L.kc[1][SORT_KEYS - 1 - min(tc_of(mt[slot]), SORT_KEYS - 1)] + lo[slot]] =
+                (uint16_t)(slot | (task < 16 * w ? 0 : 0x8000));
         }
         __syncthreads();
 #if defined(SCROLL_ABL_STOP) && SCROLL_ABL_STOP == 1
         return;
 #endif
         /* CAVLC bodies, largest TotalCoeff first */
+        const int zbase = (int)L.kc[1][SORT_KEYS - 1];      /* blocks without levels sort last: no body */
         for (int pa = 0; pa < np; ++pa) {
             const int pos = pa * T + t;
-            if (pos >= ntask) continue;
-            const int task = order[pos];
-            const int slot = row_slot(task, w);
-            if (tc_of(mt[slot]) == 0) continue;     /* no levels: no body (the class sorts them last) */
+            if (pos >= zbase) continue;
+            const uint32_t oe = order[pos];
+            const int slot = (int)(oe & 0x7fffu);
+            const bool luma = !(oe & 0x8000u);
             const uint4 v4 = lv[slot];
             CapSink cap{0, 0, 0};
             int t1 = 0;
@@ -1204,7 +1206,7 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
             const int tc = __builtin_popcount(v4.x | v4.y | v4.z | v4.w) & 15;
             cap.n = tc * 3;
 #else
-            const int tc = cavlc_body<CapSink, true>(cap, L.ptabs, v4, task < 16 * w ? 16 : 15, t1, ok,
+            const int tc = cavlc_body<CapSink, true>(cap, L.ptabs, v4, luma ? 16 : 15, t1, ok,
                                                      reinterpret_cast<const int8_t *>(lv + slot));
 #endif
             mt[slot] = ok ? (uint16_t)(cap.n | (uint32_t)tc << 8 | (uint32_t)t1 << 13)

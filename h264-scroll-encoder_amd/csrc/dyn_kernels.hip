@@ -1775,7 +1775,10 @@ __device__ inline uint32_t pick4(const uint32_t w[8], int i)     /* w[i], i in 0
     return (i & 4) ? ce : ab;
 }
 
-constexpr int GATHER_Z = 1;             /* workgroups per NAL (2 and 4 measured slower) */
+#ifndef SCROLL_GATHER_Z
+#define SCROLL_GATHER_Z 1
+#endif
+constexpr int GATHER_Z = SCROLL_GATHER_Z;             /* workgroups per NAL (2 and 4 measured slower) */
 
 template <int U>
 __global__ __launch_bounds__(DT) void k_dyn_emit_gather(const DevStream *__restrict__ st,

@@ -616,6 +616,10 @@ def main():
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
     local = int(os.environ.get("LOCAL_RANK", 0))
+    import torch
+    ndev = torch.cuda.device_count()            # counts without initialising the GPU
+    if ndev and local >= ndev:                  # more ranks than GPUs (a rehearsal): share them
+        local %= ndev
     dist = None
     if world > 1:
         import torch.distributed as dist

@@ -1512,10 +1512,13 @@ struct StitchLoads {
 };
 
 __device__ inline void stitch_load(StitchLoads &L, uint32_t c0, int t, int ng, uint32_t T, const uint32_t *goff,
-                                   const uint32_t *gb, const uint32_t *gw, const uint32_t *fr)
+                                   const uint32_t *gb, const uint32_t *gw, const uint32_t *fr, int &gcarry)
 {
+    /* a thread's words only move forward: its group search starts from
+     * where the previous chunk's ended (no binary search per chunk) */
     const uint32_t P0 = c0 * 8u + 32u * (uint32_t)t;
-    int gg = stitch_group(P0, ng, goff);
+    int gg = gcarry;
+    while (gg + 1 < ng && goff[gg + 1] <= P0) ++gg;
 #pragma unroll
     for (int k = 0; k < ST_KW; ++k) {
         const uint32_t P = P0 + 32u * ST_T * (uint32_t)k;
@@ -1528,6 +1531,7 @@ __device__ inline void stitch_load(StitchLoads &L, uint32_t c0, int t, int ng, u
         const bool seam = P < T && gb[gg] - lp < 32u && gg + 1 < ng;
         L.y[k] = seam ? fr[gw[gg + 1]] : 0u;
     }
+    gcarry = gg;
 }
 
 /* grid (frames, streams) */
@@ -1584,7 +1588,8 @@ __global__ __launch_bounds__(ST_T) void k_dyn_stitch(DevStream *__restrict__ st,
     const uint32_t Pend = 8u * ((nin + 31u) & ~31u);
     int carry = -1;                                     /* last non-zero RBSP byte before the chunk */
     StitchLoads ld;
-    stitch_load(ld, 0, t, ng, T, goff, gb, gw, fr);
+    int gcarry = stitch_group(32u * (uint32_t)t, ng, goff);
+    stitch_load(ld, 0, t, ng, T, goff, gb, gw, fr, gcarry);
     for (uint32_t c0 = 0; c0 < nin; c0 += ST_CHUNK) {
         /* assemble this chunk's words (loaded), stage them, then start the
          * next chunk's loads */
@@ -1617,7 +1622,7 @@ __global__ __launch_bounds__(ST_T) void k_dyn_stitch(DevStream *__restrict__ st,
                 cbuf[t + ST_T * k] = v;
             }
         }
-        if (c0 + ST_CHUNK < nin) stitch_load(ld, c0 + ST_CHUNK, t, ng, T, goff, gb, gw, fr);
+        if (c0 + ST_CHUNK < nin) stitch_load(ld, c0 + ST_CHUNK, t, ng, T, goff, gb, gw, fr, gcarry);
         lds_barrier();                                  /* the next chunk's loads stay in flight */
         if (stp && c0 == 0) stp[2] = __builtin_amdgcn_s_memrealtime();
         /* emulation prevention of this thread's 4 ST_KW contiguous bytes */

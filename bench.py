@@ -40,8 +40,10 @@ A step = one scroll_batch_compose over every stream of the rank:
   in HBM; output arenas are rewound on device at every step (the bytes of a
   step are the product).
 Prints ONE JSON line (rank 0) with the dominant kernel's roofline (k_dyn_row
-or k_dyn_group for the dynamic rect, k_hint_stage, k_emit; HIP events on its
-launch stream) and the CPU oracle on host cores (rank 0, N = 1).
+for the dynamic rect, k_hint_stage, k_emit; HIP events on its launch stream),
+the CPU oracle on host cores (rank 0, N = 1) and, after the timed region, the
+check of the last step's bytes against the oracle ("verified"; a mismatch
+exits with status 3).  --gpus N without a launcher starts N ranks itself.
 """
 import argparse
 import ctypes
@@ -488,8 +490,8 @@ def cpu_baseline_splice(wl, slices, nstreams=16, nframes=64):
         lib.or_cfg_init(ctypes.byref(c), W, H)
         c.frame_num = 2
         for f in range(nframes):
-            lib.or_compose_splice(buf, len(buf), ctypes.byref(c), int(offs[s, f]), 0, None, 0, 0,
-                                  ctypes.byref(sps[s * nframes + f]), ctypes.byref(err))
+            lib.or_compose_splice(buf, len(buf), ctypes.byref(c), int(offs[s, f]), 0, None, 0,
+                                  2, ctypes.byref(sps[s * nframes + f]), ctypes.byref(err))
     el = time.perf_counter() - t0
     return {"value": round(nstreams * nframes / el, 1), "unit": "frames/s", "cores": 1,
             "kind": "port", "sample": f"{nstreams} streams x {nframes} frames, {W}x{H} with a "
@@ -546,6 +548,8 @@ def run_splice(args, wl, rank, world, local, dist):
     b.enable_timing(False)
     el = max_over_ranks(t1 - t0, dist)
     value = S * F * args.steps * world / el
+    verified, vdetail = (None, None) if args.no_verify else \
+        verify_splice_step(b, e, ptrs, wl, first, args.warmup + args.steps)
     if rank == 0:
         n = max(n_launch, 1)
         kms = {"plan": plan_ms / n, "emit": emit_ms / n, "splice_stage": stage_ms / n,
@@ -570,6 +574,7 @@ def run_splice(args, wl, rank, world, local, dist):
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
                          "alg_bytes_per_launch": alg_bytes,
                          "kernel_ms_avg": {k: round(v, 4) for k, v in kms.items()}},
+            "verified": verified, "verify": vdetail, "revision": revision(),
         }
         if world == 1 and not args.no_cpu:
             host = [e.output(s)[:] for s in range(min(S, 4))]
@@ -584,16 +589,108 @@ def run_splice(args, wl, rank, world, local, dist):
         print(json.dumps(out), flush=True)
     b.close()
     e.close()
+    if verified is False:
+        sys.exit(3)
 
 
-def load_traffic(workload):
+def verify_splice_step(b, e, ptrs, wl, first, passes, nstreams=8):
+    """CHECKER (after timing): the last step's bytes of the first nstreams
+    streams against oracle/splice_oracle.c (the external slices copied back
+    from the encoder's arena; the splice path's default SCROLL_HINT_SPEC)"""
+    sys.path.insert(0, os.path.join(HERE, "tests"))
+    import stepcheck
+    from dynhelp import OrCfg, splice_of
+    t0 = time.perf_counter()
+    oracle = stepcheck.load_oracle()
+    S, F, W, H = wl["streams"], wl["frames"], wl["w"], wl["h"]
+    x0, y0, sw, sh = wl["splice"]
+    ns = min(S, nstreams)
+    offs = synthetic_offsets(first, ns, F, H)
+    buf = (ctypes.c_uint8 * (8 << 20))()
+    err = ctypes.c_int()
+    want = []
+    for s in range(ns):
+        host, pos = e.output(s), 0
+        c = OrCfg()
+        oracle.or_cfg_init(ctypes.byref(c), W, H)
+        c.frame_num = 2
+        for _ in range(passes - 1):
+            for f in range(F):
+                oracle.or_compose_state(ctypes.byref(c), int(offs[s, f]), 0)
+        o = bytearray()
+        for f in range(F):
+            n = ptrs[(s, f)][1]
+            sp = splice_of(x0, y0, sw, sh, host[pos:pos + n])
+            pos += n
+            k = oracle.or_compose_splice(buf, len(buf), ctypes.byref(c), int(offs[s, f]), 0, None, 0,
+                                         2, ctypes.byref(sp), ctypes.byref(err))
+            if err.value or not k:
+                return False, {"error": f"oracle refused stream {s} frame {f}"}
+            o += bytes(buf[:k])
+        want.append(bytes(o))
+    ok, d = stepcheck.compare_streams(b, want)
+    d.update(sample=f"first {ns} of {S} streams", passes=passes,
+             seconds=round(time.perf_counter() - t0, 2), checker="oracle/splice_oracle.c")
+    return ok, d
+
+
+def load_traffic(workload, kernel, alg_bytes):
+    """PMC traffic of the dominant kernel (profiles/traffic_<workload>.json,
+    rocprofv3 FETCH_SIZE / WRITE_SIZE passes, tools/traffic.py) -- only when
+    it was measured on this very launch: same kernel and the same algorithmic
+    bytes per launch (i.e. the same streams x frames x rect).  Otherwise None:
+    PMC counters need their own rocprofv3 runs, they cannot be read inside
+    this process."""
     p = os.path.join(HERE, "profiles", f"traffic_{workload}.json")
+    try:
+        t = json.load(open(p))
+    except (OSError, ValueError):
+        return None
+    if t.get("kernel") != kernel or abs(float(t.get("alg_bytes_per_launch", -1)) - alg_bytes) > 0.5:
+        return None
+    return t
+
+
+def usable_cores():
+    """host cores this process may use: the CPU affinity set, capped by the
+    cgroup CPU quota (the GPU box grants a 16-CPU quota on a many-core host,
+    where os.cpu_count() shows every core of the machine)"""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, int(-(-int(quota) // int(period)))))
+    except (OSError, ValueError):
+        pass
+    return max(1, n)
+
+
+def revision():
+    """the source revision of this tree (.revision written before a GPU run,
+    else git)"""
+    p = os.path.join(HERE, ".revision")
     if os.path.exists(p):
-        try:
-            return json.load(open(p))
-        except Exception:
-            return None
-    return None
+        return open(p).read().split()[0]
+    try:
+        import subprocess
+        return subprocess.run(["git", "-C", HERE, "rev-parse", "HEAD"], capture_output=True,
+                              text=True, timeout=10).stdout.strip() or None
+    except Exception:
+        return None
+
+
+def launch_ranks(n):
+    """--gpus N without a launcher: start N ranks (torch.distributed.run, one
+    process per GPU, rendezvous on 127.0.0.1) as children and exit with their
+    status.  Runs before anything touches the GPU in this process."""
+    import socket
+    import subprocess
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.run(cmd).returncode
 
 
 def main():
@@ -605,6 +702,8 @@ def main():
     ap.add_argument("--streams", type=int, default=0, help="override streams per GPU")
     ap.add_argument("--frames", type=int, default=0, help="override frames per step")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--no-verify", action="store_true",
+                    help="skip the post-timing oracle check of the last step")
     args = ap.parse_args()
 
     wl = dict(WORKLOADS[args.workload])
@@ -613,9 +712,13 @@ def main():
     if args.frames:
         wl["frames"] = args.frames
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
     local = int(os.environ.get("LOCAL_RANK", 0))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE {world}")
     import torch
     ndev = torch.cuda.device_count()            # counts without initialising the GPU
     if ndev and local >= ndev:                  # more ranks than GPUs (a rehearsal): share them
@@ -636,7 +739,6 @@ def main():
             dist.destroy_process_group()
         return
 
-    import numpy as np
     import torch
     import h264scroll as hs
 
@@ -646,24 +748,7 @@ def main():
     first, _ = shard_streams(rank, world, S)       # static contiguous shard
     rect = wl["rect"]
     hints = wl.get("hints", False)
-    per_frame_bound = 2 * (64 + (W // 16) * (H // 16))
-    if rect:
-        per_frame_bound += 192 * rect[2] * rect[3]      # ~75 B per dynamic MB measured
-        per_frame_bound += 8 * (W // 16) * (H // 16)     # waypoint-heavy headers at 4K
-    b = hs.Batch(S, F, F * per_frame_bound + (1 << 20), device=local)
-    for _ in range(S):
-        b.add_stream(hs.make_config(W, H))
-    b.set_offsets(synthetic_offsets(first, S, F, H))
-    if rect:
-        b.set_dyn_rect(*rect)
-        ra, rb = striped_i420(W, H, 0), striped_i420(W, H, 1)
-        for s in range(S):                               # one copy per stream (own traffic)
-            b.set_dyn_refs(ra, rb, stream=s)
-        b.dyn_source_synth(F, stream_base=first, t0=0)
-    if hints:
-        for s in range(S):
-            for f in range(F):
-                b.set_hints(s, f, ui_hints(first + s, f, W, H), hs.SCROLL_HINT_PSKIP)
+    b = build_compose_batch(hs, wl, first, local)
 
     def barrier():
         torch.cuda.synchronize()
@@ -697,6 +782,17 @@ def main():
     value = frames_total / el
     ms_step = 1000.0 * el / args.steps
 
+    # after the timed region: the last step's bytes of this rank's streams
+    # against the CPU oracle (the checker), every rank its own shard
+    verified, vdetail = (None, None) if args.no_verify else \
+        verify_last_step(b, wl, first, args.warmup + args.steps)
+    all_ok = verified is not False
+    if dist:
+        import torch as _t
+        flag = _t.tensor([0.0 if verified is False else 1.0], dtype=_t.float64)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        all_ok = flag.item() > 0.5
+
     if rank == 0:
         n = max(n_launch, 1)
         kms = {"plan": plan_ms / n, "emit": emit_ms / n, "dyn_stage": stage_ms / n,
@@ -704,20 +800,14 @@ def main():
         if rect:
             kms["dyn_code"] = code_ms / n
             kms["dyn_pack"] = pack_ms / n
-        if rect and kms["dyn_code"] >= kms["dyn_pack"]:
+        if rect:
             # k_dyn_rows + k_dyn_row per launch (k_dyn_code_general: no
             # frame here): the source and prediction samples of every
-            # dynamic MB (384 B each) read.  The staged RBSP the rect rows
-            # write is not counted (a lower bound: k_dyn_group writes the
-            # static rows' share of it)
+            # dynamic MB (384 B each) read.  The row-stage bits the rect rows
+            # write are intermediate and not counted (a lower bound)
             kern = "k_dyn_row"
             alg_bytes = dyn_nals * 2 * 384 * rect[2] * rect[3]
             kern_ms = kms["dyn_code"]
-        elif rect:
-            # k_dyn_group (static row groups) + k_dyn_ep per launch
-            kern = "k_dyn_group"
-            alg_bytes = rbsp_tot
-            kern_ms = kms["dyn_pack"]
         elif hints:
             # k_hint_stage per launch: the staged RBSP written, the rects read
             kern = "k_hint_stage"
@@ -728,9 +818,7 @@ def main():
             alg_bytes = step_bytes + NAL_DESC_BYTES * step_nals   # per k_emit launch
             kern_ms = kms["emit"]
         achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
-        traffic = load_traffic(args.workload)
-        if traffic and traffic.get("kernel") != kern:     # measured on another kernel: not this line's
-            traffic = None
+        traffic = load_traffic(args.workload, kern, alg_bytes)
         out = {
             "metric": METRIC,
             "value": round(value, 1),
@@ -752,8 +840,14 @@ def main():
                          "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic.get("hbm_bytes_per_launch") if traffic else None,
+                         "traffic_source": (f"profiles/traffic_{args.workload}.json (rocprofv3 "
+                                            f"FETCH_SIZE/WRITE_SIZE passes of this launch)")
+                         if traffic else "not measured for this launch",
                          "alg_bytes_per_launch": alg_bytes,
                          "kernel_ms_avg": {k: round(v, 4) for k, v in kms.items()}},
+            "verified": None if verified is None else bool(all_ok),
+            "verify": vdetail,
+            "revision": revision(),
         }
         if rect:
             out["config"]["dyn_rect_mb"] = list(rect)
@@ -763,12 +857,72 @@ def main():
             out["hint"] = {"rbsp_bytes_per_frame": round(rbsp_tot / max(dyn_nals, 1), 1),
                            "ep_bytes_per_frame": round(ep_tot / max(dyn_nals, 1), 2)}
         if world == 1 and not args.no_cpu:
-            threads = min(16, os.cpu_count() or 1)
-            out["cpu_baseline"] = cpu_baseline_hint(wl) if hints else cpu_baseline(wl, threads)
+            cores = usable_cores()
+            out["cpu_baseline"] = cpu_baseline_hint(wl) if hints else cpu_baseline(wl, cores)
+            out["cpu_baseline"]["host"] = {"os_cpu_count": os.cpu_count(), "usable_cores": cores}
         print(json.dumps(out), flush=True)
     b.close()
     if dist:
         dist.destroy_process_group()
+    if not all_ok:
+        sys.exit(3)
+
+
+def build_compose_batch(hs, wl, first, device):
+    """the benched batch of a compose workload (p720dyn / p4kdyn / p720 /
+    p720hint): streams first .. first + S - 1, SURVEY 8(d) offsets, the rect
+    with one copy of the striped reference pictures per stream and the
+    synthetic source on device, or the UI overlay"""
+    S, F, W, H = wl["streams"], wl["frames"], wl["w"], wl["h"]
+    rect = wl["rect"]
+    per_frame_bound = 2 * (64 + (W // 16) * (H // 16))
+    if rect:
+        per_frame_bound += 192 * rect[2] * rect[3]      # ~75 B per dynamic MB measured
+        per_frame_bound += 8 * (W // 16) * (H // 16)     # waypoint-heavy headers at 4K
+    b = hs.Batch(S, F, F * per_frame_bound + (1 << 20), device=device)
+    for _ in range(S):
+        b.add_stream(hs.make_config(W, H))
+    b.set_offsets(synthetic_offsets(first, S, F, H))
+    if rect:
+        b.set_dyn_rect(*rect)
+        ra, rb = striped_i420(W, H, 0), striped_i420(W, H, 1)
+        for s in range(S):                               # one copy per stream (own traffic)
+            b.set_dyn_refs(ra, rb, stream=s)
+        b.dyn_source_synth(F, stream_base=first, t0=0)
+    if wl.get("hints"):
+        for s in range(S):
+            for f in range(F):
+                b.set_hints(s, f, ui_hints(first + s, f, W, H), hs.SCROLL_HINT_PSKIP)
+    return b
+
+
+def verify_last_step(b, wl, first, passes, hint_streams=32):
+    """CHECKER (runs after timing): the bytes of the last composed step
+    against the CPU oracle (tests/stepcheck.py -> oracle/verify_oracle.c on
+    all usable host cores).  Every stream for the rect and P-only workloads,
+    the first `hint_streams` streams for the UI overlay (single-threaded
+    oracle).  -> (ok, detail)"""
+    sys.path.insert(0, os.path.join(HERE, "tests"))
+    import stepcheck
+    t0 = time.perf_counter()
+    S, F, W, H = wl["streams"], wl["frames"], wl["w"], wl["h"]
+    offs = synthetic_offsets(first, S, F, H)
+    oracle = stepcheck.load_oracle()
+    if wl.get("hints"):
+        want, ns = stepcheck.oracle_hint_step(oracle, W, H, offs[:hint_streams], passes,
+                                              lambda s, f: ui_hints(first + s, f, W, H), 1)
+        ok, d = stepcheck.compare_streams(b, want)
+        d["sample"] = f"first {ns} of {S} streams"
+    else:
+        want = stepcheck.oracle_step(oracle, W, H, offs, passes, rect=wl["rect"],
+                                     stream_base=first, t0=0, nthreads=usable_cores())
+        ok, d = stepcheck.compare_streams(b, want)
+        d["sample"] = f"all {S} streams of the rank"
+    d["passes"] = passes
+    d["seconds"] = round(time.perf_counter() - t0, 2)
+    d["checker"] = "oracle/verify_oracle.c" if not wl.get("hints") else "oracle/hint_oracle.c"
+    return ok, d
+
 
 
 if __name__ == "__main__":

@@ -76,7 +76,9 @@ __global__ __launch_bounds__(DT) void k_hint_stage(DevStream *__restrict__ st,
     const HintFrame H = hf[(size_t)s * ld_fr + f];
     if (H.mode & HINT_MODE_SPLICED) return;                /* k_splice_stage's frame */
     const int nr = min((int)H.n, SCROLL_HINT_MAX_RECTS);
-    const bool pskip = (H.mode & 0xff) == SCROLL_HINT_PSKIP;
+    const int hmode = H.mode & 0xff;
+    const bool pskip = hmode == SCROLL_HINT_PSKIP;
+    const bool spec = hmode != SCROLL_HINT_EXACT;
     if (t == 0) {
         L.lnz_r = -1;
         L.lnz_w = -1;
@@ -159,10 +161,10 @@ __global__ __launch_bounds__(DT) void k_hint_stage(DevStream *__restrict__ st,
             const Mv A = x > 0 ? at(m - 1) : none;
             const Mv B = y > 0 ? at(m - mbw) : none;
             const Mv C = y == 0 ? none : (x + 1 < mbw ? at(m - mbw + 1) : (x > 0 ? at(m - mbw - 1) : none));
-            if (pskip) {
+            if (spec) {
                 int sx, sy;
                 pskip_mv(x, y, A, B, C, sx, sy);
-                coded = !(me.ref == 0 && me.mx == sx && me.my == sy);
+                coded = !pskip || !(me.ref == 0 && me.mx == sx && me.my == sy);
                 predict_spec(A, B, C, me.ref, px, py);
             } else {
                 coded = true;

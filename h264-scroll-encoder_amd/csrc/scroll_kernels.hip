@@ -1869,7 +1869,7 @@ int scroll_batch_set_hints(ScrollBatch *b, int s, int f, const ScrollHintRect *r
 {
     if (!b || s < 0 || s >= b->nstreams || f < 0 || f >= b->max_frames || n < 0 ||
         n > SCROLL_HINT_MAX_RECTS || (n > 0 && !rects) ||
-        (mode != SCROLL_HINT_EXACT && mode != SCROLL_HINT_PSKIP)) {
+        (mode != SCROLL_HINT_EXACT && mode != SCROLL_HINT_PSKIP && mode != SCROLL_HINT_SPEC)) {
         set_err("scroll_batch_set_hints: bad arguments");
         return SCROLL_ERR_ARG;
     }
@@ -1980,7 +1980,7 @@ static int splice_upload(ScrollBatch *b)
             pool.insert(pool.end(), h.nal.begin(), h.nal.end());
             pool.resize((pool.size() + 3) & ~(size_t)3);
         }
-        words += h.n / 4 + 2;
+        words += (h.n + 3) / 4 + 2;    /* k_splice_parse zeroes (len + 3) / 4 + 2 words */
         recs += (size_t)h.w * h.h;
         list.push_back((int32_t)i);
         const DevStream &d = b->h_st[i / F];
@@ -1996,15 +1996,19 @@ static int splice_upload(ScrollBatch *b)
         (rc = sp_grow((void **)&b->d_sp_list, &b->sp_list_cap, list.size(), sizeof(int32_t))))
         return rc;
     if (slot > b->geo.slot_bytes) {
-        (void)hipFree(b->d_stage);
-        b->d_stage = nullptr;
-        hipError_t e = hipMalloc(&b->d_stage, S * F * slot);
+        /* the new slots first: on failure the old ones, the hints and the
+         * splices stay as they were (sp_dirty stays set: the next compose
+         * tries again, or the caller clears / shrinks the splices) */
+        void *ns = nullptr;
+        hipError_t e = hipMalloc(&ns, S * F * slot);
         if (e != hipSuccess) {
+            (void)hipGetLastError();
             set_err("scroll_batch_compose: splice staging (%zu bytes per frame): %s", slot,
                     hipGetErrorString(e));
-            hint_release(b);
             return e == hipErrorOutOfMemory ? SCROLL_ERR_OOM : SCROLL_ERR_HIP;
         }
+        (void)hipFree(b->d_stage);
+        b->d_stage = (uint8_t *)ns;
         b->geo.slot_bytes = slot;
     }
     for (size_t i = 0; i < b->h_sp.size(); ++i)
@@ -2025,7 +2029,7 @@ int scroll_batch_set_splice(ScrollBatch *b, int s, int f, int x0, int y0, int w,
                             const uint8_t *nal, size_t n)
 {
     if (!b || s < 0 || s >= b->nstreams || f < 0 || f >= b->max_frames ||
-        (n > 0 && (!nal || w <= 0 || h <= 0 || x0 < 0 || y0 < 0 || n > ((size_t)1 << 30)))) {
+        (n > 0 && (!nal || w <= 0 || h <= 0 || x0 < 0 || y0 < 0 || n >= SCROLL_SPLICE_MAX_BYTES))) {
         set_err("scroll_batch_set_splice: bad arguments");
         return SCROLL_ERR_ARG;
     }
@@ -2039,9 +2043,10 @@ int scroll_batch_set_splice(ScrollBatch *b, int s, int f, int x0, int y0, int w,
         return SCROLL_ERR_CONFIG;
     }
     if (n == 0 && !b->hint_on) return SCROLL_OK;
-    if (!b->hint_on) {                 /* the splice rides on the hint path */
-        int rc = scroll_batch_set_hints(b, s, f, nullptr, 0, SCROLL_HINT_EXACT);
+    if (!b->hint_on) {                 /* the splice rides on the hint path, SPEC by default */
+        int rc = scroll_batch_set_hints(b, s, f, nullptr, 0, SCROLL_HINT_SPEC);
         if (rc) return rc;
+        std::fill(b->h_hint_mode.begin(), b->h_hint_mode.end(), (int16_t)SCROLL_HINT_SPEC);
     } else {
         int rc = batch_host_sync(b);
         if (rc) return rc;
@@ -2077,7 +2082,7 @@ int scroll_batch_set_splices_device(ScrollBatch *b, int n, const ScrollSpliceDes
         const bool on = e.n > 0;
         if (e.s < 0 || e.s >= b->nstreams || e.f < 0 || e.f >= b->max_frames ||
             (on && (!e.nal || e.w <= 0 || e.h <= 0 || e.x0 < 0 || e.y0 < 0 ||
-                    e.n > ((uint64_t)1 << 30) || e.x0 + e.w > b->h_st[e.s].w / 16 ||
+                    e.n >= SCROLL_SPLICE_MAX_BYTES || e.x0 + e.w > b->h_st[e.s].w / 16 ||
                     e.y0 + e.h > b->h_st[e.s].h / 16))) {
             set_err("scroll_batch_set_splices_device: entry %d: bad stream / frame / rect / size", k);
             return SCROLL_ERR_ARG;
@@ -2089,8 +2094,9 @@ int scroll_batch_set_splices_device(ScrollBatch *b, int n, const ScrollSpliceDes
         return SCROLL_ERR_CONFIG;
     }
     if (!b->hint_on) {
-        int rc = scroll_batch_set_hints(b, d[0].s, d[0].f, nullptr, 0, SCROLL_HINT_EXACT);
+        int rc = scroll_batch_set_hints(b, d[0].s, d[0].f, nullptr, 0, SCROLL_HINT_SPEC);
         if (rc) return rc;
+        std::fill(b->h_hint_mode.begin(), b->h_hint_mode.end(), (int16_t)SCROLL_HINT_SPEC);
     } else {
         int rc = batch_host_sync(b);
         if (rc) return rc;

@@ -403,7 +403,7 @@ __global__ __launch_bounds__(64) void k_splice_parse(int n, const int32_t *__res
      * output index by a wave prefix count; bytes land MSB-first in words
      * (byte k at byte address k ^ 3) */
     uint32_t *o = rbsp + F->rbsp_word;
-    const uint32_t nwmax = (len + 3u) / 4u + 2u;
+    const uint32_t nwmax = (len + 3u) / 4u + 2u;   /* = the host's region (splice_upload) */
     for (uint32_t k = (uint32_t)lane; k < nwmax; k += 64) o[k] = 0u;
     __syncthreads();
     uint8_t *ob = reinterpret_cast<uint8_t *>(o);
@@ -720,7 +720,9 @@ __global__ __launch_bounds__(DT) void k_splice_stage(DevStream *__restrict__ st,
     const SpliceMbRec *rec = recs + SF.rec_first;
     const uint32_t *rb = rbsp + SF.rbsp_word;
     const int nr = min((int)H.n, SCROLL_HINT_MAX_RECTS);
-    const bool pskip = (H.mode & 0xff) == SCROLL_HINT_PSKIP;
+    const int hmode = H.mode & 0xff;
+    const bool pskip = hmode == SCROLL_HINT_PSKIP;
+    const bool spec = hmode != SCROLL_HINT_EXACT;
     if (t == 0) {
         L.ep_n = 0;
         L.bad = 0;
@@ -808,10 +810,11 @@ __global__ __launch_bounds__(DT) void k_splice_stage(DevStream *__restrict__ st,
                 const Mv A = x > 0 ? at(m - 1) : none;
                 const Mv B = y > 0 ? at(m - mbw) : none;
                 const Mv C = y == 0 ? none : (x + 1 < mbw ? at(m - mbw + 1) : (x > 0 ? at(m - mbw - 1) : none));
-                if (pskip) {
+                if (spec) {
                     int sx, sy;
                     pskip_mv(x, y, A, B, C, sx, sy);
-                    coded = !(me.ref == 0 && me.mx == sx && me.my == sy && (k < 0 || rec[k].cbp == 0));
+                    coded = !pskip ||
+                            !(me.ref == 0 && me.mx == sx && me.my == sy && (k < 0 || rec[k].cbp == 0));
                     predict_spec(A, B, C, me.ref, px, py);
                 } else {
                     coded = true;

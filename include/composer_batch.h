@@ -184,7 +184,13 @@ int scroll_batch_kernel_stats_ex(ScrollBatch *b, double ms[6], int *count);
  *   modes: SCROLL_HINT_EXACT  the reference's MB syntax (mb_skip_run 0,
  *              get_mv_prediction of h264_writer.c:369-432) for any MV field;
  *          SCROLL_HINT_PSKIP  standard median prediction (H.264 8.4.1.3) and
- *              P_Skip runs for ref-0 MBs on their skip motion (8.4.1.1).
+ *              P_Skip runs for ref-0 MBs on their skip motion (8.4.1.1);
+ *          SCROLL_HINT_SPEC   the reference's MB syntax (no skipped MBs) with
+ *              the standard's median prediction: a standard decoder gets the
+ *              intended motion for any MV field, and the plain scroll layout
+ *              is still the reference's frame byte for byte (a row-uniform
+ *              field never reaches the cases where get_mv_prediction departs
+ *              from 8.4.1.3).
  *   scroll_batch_set_hints(b, s, f, rects, n, mode)   hints of frame f (the
  *       f-th frame of each following compose) of stream s; n <=
  *       SCROLL_HINT_MAX_RECTS; n = 0 gives the plain layout in `mode`.  A
@@ -195,6 +201,7 @@ int scroll_batch_kernel_stats_ex(ScrollBatch *b, double ms[6], int *count);
  * Not combinable with a dynamic rect (SCROLL_ERR_CONFIG). */
 #define SCROLL_HINT_EXACT 0
 #define SCROLL_HINT_PSKIP 1
+#define SCROLL_HINT_SPEC 2
 #define SCROLL_HINT_MAX_RECTS 64
 #define SCROLL_HINT_MAX_MV 8192     /* |mv_x|, |mv_y| in pixels */
 typedef struct ScrollHintRect {
@@ -217,9 +224,11 @@ int scroll_batch_clear_hints(ScrollBatch *b);
  * re-coded for the composed picture, mb_qp_delta rebased to the composed
  * slice QP, each residual block keeps its bits after coeff_token and gets
  * the coeff_token of its composed nC.  MBs outside the rect follow the frame's
- * UI hints (a splice turns the hint path on; frames without a splice and
- * without hints equal the reference's scroll frames in SCROLL_HINT_EXACT;
- * set_hints(.., NULL, 0, SCROLL_HINT_PSKIP) picks the standard's predictor).
+ * UI hints (a splice turns the hint path on in SCROLL_HINT_SPEC, so a standard
+ * decoder gets the spliced motion, and frames without a splice and without
+ * hints still equal the reference's scroll frames; set_hints(.., NULL, 0,
+ * SCROLL_HINT_PSKIP) adds P_Skip runs, SCROLL_HINT_EXACT the reference's own
+ * predictor).
  * Bit-exact definition: oracle/splice_oracle.h.
  *
  * The external slice: one NAL (Annex-B start code optional), nal_unit_type
@@ -243,6 +252,7 @@ int scroll_batch_clear_hints(ScrollBatch *b);
  *   scroll_batch_clear_splices(b)   remove every splice (hints stay).
  * The staging slots grow to the largest spliced NAL's bound (about the
  * external slice plus 16 bytes per picture MB) for every (stream, frame). */
+#define SCROLL_SPLICE_MAX_BYTES   ((uint64_t)1 << 29)   /* n < 512 MiB: 32-bit bit offsets */
 #define SCROLL_SPLICE_OK          0
 #define SCROLL_SPLICE_ERR_NAL     1   /* not a coded slice of a non-IDR picture     */
 #define SCROLL_SPLICE_ERR_HEADER  2   /* slice header outside the supported syntax  */

@@ -155,12 +155,12 @@ size_t or_hint_scroll_nal(uint8_t *dst, size_t cap, or_cfg *c, int off,
             mx *= 4;                                    /* quarter pels */
             my *= 4;
             int px, py;
-            if (mode == OR_HINT_PSKIP) {
+            if (mode != OR_HINT_EXACT) {
                 or_mvi A, B, C;
                 neighbours(x, y, mbw, above, &left, &A, &B, &C);
                 int sx, sy;
                 pskip_mv(x, y, &A, &B, &C, &sx, &sy);
-                if (ref == 0 && mx == sx && my == sy) {
+                if (mode == OR_HINT_PSKIP && ref == 0 && mx == sx && my == sy) {
                     run++;                              /* P_Skip */
                 } else {
                     spec_mvp(&A, &B, &C, ref, &px, &py);

@@ -32,6 +32,13 @@
  *   OR_HINT_PSKIP  standard MV prediction (8.4.1.3) and P_Skip: an MB with
  *                  ref 0 whose mv equals the P_Skip motion (8.4.1.1) is
  *                  skipped; runs of skipped MBs are coded with mb_skip_run.
+ *   OR_HINT_SPEC   the reference's MB syntax (every MB P_L0_16x16 after
+ *                  mb_skip_run 0) with the standard's MV prediction
+ *                  (8.4.1.3): decodable by a standard decoder for any MV
+ *                  field, and byte-identical to the reference's scroll frame
+ *                  for the plain scroll layout (a row-uniform field never
+ *                  reaches the cases where get_mv_prediction departs from
+ *                  the standard).
  */
 #ifndef HINT_ORACLE_H
 #define HINT_ORACLE_H
@@ -47,6 +54,7 @@ extern "C" {
 
 #define OR_HINT_EXACT 0
 #define OR_HINT_PSKIP 1
+#define OR_HINT_SPEC 2
 
 /* layout-identical to ScrollHintRect (include/composer_batch.h) */
 typedef struct {

@@ -440,12 +440,12 @@ size_t or_splice_scroll_nal(uint8_t *dst, size_t cap, or_cfg *c, int off, const 
                 my *= 4;
             }
             int px, py, coded = 1;
-            if (mode == OR_HINT_PSKIP) {
+            if (mode != OR_HINT_EXACT) {
                 or_mvi A, B, C;
                 or_neighbours(x, y, mbw, above, &left, &A, &B, &C);
                 int sx, sy;
                 or_pskip_motion(x, y, &A, &B, &C, &sx, &sy);
-                coded = !(ref == 0 && mx == sx && my == sy && cbp == 0);
+                coded = mode == OR_HINT_SPEC || !(ref == 0 && mx == sx && my == sy && cbp == 0);
                 or_spec_predict(&A, &B, &C, ref, &px, &py);
             } else {
                 or_predict(x, y, mbw, above, &left, ref, &px, &py);

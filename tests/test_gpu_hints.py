@@ -17,7 +17,7 @@ from dynhelp import OrCfg, hint_array, random_hints, split_nals
 
 pytestmark = pytest.mark.gpu
 
-EXACT, PSKIP = 0, 1
+EXACT, PSKIP, SPEC = 0, 1, 2
 
 
 @pytest.fixture(scope="module")
@@ -37,7 +37,7 @@ def _cfg(oracle, w, h, waypoints=()):
     return c
 
 
-def plan_hints(oracle, w, h, offsets, seed, modes=(EXACT, PSKIP), p=0.8, waypoints=(),
+def plan_hints(oracle, w, h, offsets, seed, modes=(EXACT, PSKIP, SPEC), p=0.8, waypoints=(),
                compose_mode=0, nmax=6):
     """random hints per (stream, frame) whose refs are valid in that frame,
     and the oracle's streams for them: -> (hints dict, [bytes per stream])"""

@@ -16,7 +16,7 @@ from dynhelp import OrCfg, hint_array, random_hints, split_nals, ext_slice, spli
 
 pytestmark = pytest.mark.gpu
 
-EXACT, PSKIP = 0, 1
+EXACT, PSKIP, SPEC = 0, 1, 2
 
 
 @pytest.fixture(scope="module")
@@ -33,7 +33,7 @@ def _cfg(oracle, w, h):
     return c
 
 
-def plan(oracle, w, h, offsets, seed, p_splice=0.7, p_hint=0.3, modes=(EXACT, PSKIP),
+def plan(oracle, w, h, offsets, seed, p_splice=0.7, p_hint=0.3, modes=(EXACT, PSKIP, SPEC),
          max_rect=(10, 8), compose_mode=0, ext_kw=None):
     """random splices (+ hints) per (stream, frame) whose refs are valid in
     that frame; -> (frames dict, oracle bytes per stream)"""
@@ -81,7 +81,7 @@ def gpu_streams(gpu, w, h, offsets, frames, compose_mode=0, arena=16 << 20, debu
     if debug:
         b.set_debug(debug)
     for (s, f), (rects, mode, sp) in frames.items():
-        if rects or mode != EXACT:
+        if rects or sp or mode != EXACT:          # a splice alone would default to SPEC
             b.set_hints(s, f, rects, mode)
         if sp:
             b.set_splice(s, f, *sp)
@@ -139,7 +139,7 @@ def test_whole_picture_and_corner_splices(gpu, oracle):
     err = ctypes.c_int()
     o = bytearray()
     for t, (x0, y0, sw, sh) in enumerate(rects):
-        mode = PSKIP if t % 2 else EXACT
+        mode = (EXACT, PSKIP, SPEC)[t % 3]
         sp = (x0, y0, sw, sh, ext_slice(oracle, c, sw, sh, 500 + t, cbp_pm=900, skip_pm=300))
         frames[(0, t)] = ([], mode, sp)
         k = oracle.or_compose_splice(buf, len(buf), ctypes.byref(c), int(offs[0, t]), 0, None, 0,
@@ -195,7 +195,7 @@ def test_errors_fail_only_their_stream(gpu, oracle, scroll):
     for t in range(6):
         sp = splice_of(2, 2, 4, 3, good) if t == 1 else None
         k = oracle.or_compose_splice(buf, len(buf), ctypes.byref(c4), int(offs[4, t]), 0, None, 0,
-                                     EXACT, ctypes.byref(sp) if sp else None, ctypes.byref(err))
+                                     SPEC, ctypes.byref(sp) if sp else None, ctypes.byref(err))
         o += bytes(buf[:k])
     assert b.output(4) == bytes(o)
     b.close()
@@ -227,7 +227,7 @@ def test_persist_remove_and_clear(gpu, oracle):
             f = t % F1
             sp = splice_of(*sps[f]) if t < 20 and not (s == 1 and f == 3) else None
             k = oracle.or_compose_splice(buf, len(buf), ctypes.byref(cs), int(offs[s, t]), 0, None,
-                                         0, EXACT, ctypes.byref(sp) if sp else None,
+                                         0, SPEC, ctypes.byref(sp) if sp else None,
                                          ctypes.byref(err))
             assert err.value == 0
             o += bytes(buf[:k])
@@ -272,9 +272,60 @@ def test_dynamic_coder_output_spliced_from_device(gpu, oracle):
             sp = splice_of(28, 10, 25, 25, host[pos:pos + n])
             pos += n
             k = oracle.or_compose_splice(buf, len(buf), ctypes.byref(c), int(offs[s, f]), 0, None,
-                                         0, EXACT, ctypes.byref(sp), ctypes.byref(err))
+                                         0, SPEC, ctypes.byref(sp), ctypes.byref(err))
             assert err.value == 0
             o += bytes(buf[:k])
         assert b.output(s) == bytes(o), s
     b.close()
     e.close()
+
+
+def test_startcode_less_odd_length_adjacent_frames(gpu, oracle):
+    """NALs handed over without an Annex-B start code (optional in the API)
+    whose lengths are not multiples of 4, in adjacent frames of a stream: the
+    RBSP pool regions of neighbouring frames must not overlap (the parse
+    zeroes (len + 3) / 4 + 2 words of its frame's region)"""
+    w, h = 320, 256
+    S, F = 2, 8
+    offs = synthetic_offsets(S, F, h, first_stream=3)
+    c = _cfg(oracle, w, h)
+    frames = {}
+    lens = set()
+    for s in range(S):
+        for t in range(F):
+            seed = 3000 + 17 * s + t
+            while True:
+                nal = ext_slice(oracle, c, 5, 4, seed, cbp_pm=800, skip_pm=100)[4:]   # no start code
+                if len(nal) % 4:
+                    break
+                seed += 1000
+            lens.add(len(nal) % 4)
+            frames[(s, t)] = ([], SPEC, (3, 2, 5, 4, nal))
+    _, want = plan_from(oracle, w, h, offs, frames)
+    b, rc = gpu_streams(gpu, w, h, offs, frames)
+    assert rc == 0, gpu.last_error()
+    check_equal(b, want)
+    assert lens <= {1, 2, 3}
+    b.close()
+
+
+def plan_from(oracle, w, h, offsets, frames, compose_mode=0):
+    """oracle bytes per stream for a given frames dict (as plan() returns)"""
+    S, F = offsets.shape
+    buf = (ctypes.c_uint8 * (16 << 20))()
+    err = ctypes.c_int()
+    outs = []
+    for s in range(S):
+        c = _cfg(oracle, w, h)
+        o = bytearray()
+        for t in range(F):
+            rects, mode, sp = frames.get((s, t), ([], SPEC, None))
+            arr, n = hint_array(rects)
+            spc = splice_of(*sp) if sp else None
+            k = oracle.or_compose_splice(buf, len(buf), ctypes.byref(c), int(offsets[s, t]),
+                                         compose_mode, arr, n, mode,
+                                         ctypes.byref(spc) if spc else None, ctypes.byref(err))
+            assert err.value == 0 and k > 0, (s, t, err.value)
+            o += bytes(buf[:k])
+        outs.append(bytes(o))
+    return frames, outs

@@ -21,7 +21,7 @@ import random
 from dynhelp import OrCfg, hint_array, random_hints, ext_slice, splice_of, Splice
 import h264_pslice as P
 
-EXACT, PSKIP = 0, 1
+EXACT, PSKIP, SPEC = 0, 1, 2
 ERR_NAL, ERR_HEADER, ERR_MBTYPE, ERR_SYNTAX, ERR_REF = 1, 2, 3, 4, 5
 
 
@@ -130,7 +130,7 @@ def test_spliced_mbs_decode_to_the_external_mbs(oracle):
         nal = ext_slice(oracle, c, sw, sh, 1000 + i, **kw)
         sp = splice_of(x0, y0, sw, sh, nal)
         rects = random_hints(rng, w // 16, h // 16, refs, nmax=3) if i % 3 == 0 else []
-        for mode in (EXACT, PSKIP):
+        for mode in (EXACT, PSKIP, SPEC):
             got, ext = _check_frame(oracle, c, off, rects, mode, sp, buf)
             cov["ref2"] += sum(m["ref"] >= 2 for row in ext for m in row) * (mode == EXACT)
             cov["ext_skip"] += sum(m["skip"] for row in ext for m in row) * (mode == EXACT)
@@ -153,7 +153,7 @@ def test_splice_at_picture_corners_and_whole_picture(oracle):
                                           (mbw - 2, mbh - 2, 2, 2), (0, 0, mbw, mbh),
                                           (5, 3, 1, 1)]):
         nal = ext_slice(oracle, c, sw, sh, 77 + j, cbp_pm=900, skip_pm=300)
-        for mode in (EXACT, PSKIP):
+        for mode in (EXACT, PSKIP, SPEC):
             _check_frame(oracle, c, 40, [], mode, splice_of(x0, y0, sw, sh, nal), buf)
 
 
@@ -163,7 +163,7 @@ def test_no_splice_equals_hint_nal(oracle):
     a = (ctypes.c_uint8 * (1 << 18))()
     b = (ctypes.c_uint8 * (1 << 18))()
     err = ctypes.c_int()
-    for mode in (EXACT, PSKIP):
+    for mode in (EXACT, PSKIP, SPEC):
         c1, c2 = _cfg(oracle, w, h), _cfg(oracle, w, h)
         for i in range(30):
             off = oracle.or_synthetic_offset(1, i, h)

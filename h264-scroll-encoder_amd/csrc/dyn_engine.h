@@ -28,13 +28,19 @@ int dyn_launch_code(hipStream_t hs, int nframes, int S, DevStream *st, const Nal
                     int ld_nal, const PlanPending *pend, DynFrame *dfr, int ld_fr,
                     const DynGeom *g, const uint8_t *src, const uint8_t *refs, const DynScratch *x,
                     uint32_t epoch, int mbw, uint64_t *stamps);
-/* k_dyn_static (static row groups) + k_dyn_stitch: staged RBSP + EP positions */
+/* k_dyn_static (static row groups) + k_dyn_epfix (+ k_dyn_epscan for the
+ * NALs it flags): RBSP sizes and EP positions (eps: DYN_OVF_BYTES per frame)
+ * straight from the row groups */
 int dyn_launch_pack(hipStream_t hs, int nframes, int S, DevStream *st, const NalDesc *nal,
                     int ld_nal, const PlanPending *pend, DynFrame *dfr, int ld_fr,
-                    const DynGeom *g, const DynScratch *x, uint8_t *stage, uint64_t *stamps);
+                    const DynGeom *g, const DynScratch *x, uint8_t *eps, uint64_t *stamps);
+/* k_dyn_emit_gather + k_dyn_emit: x != NULL -- the dynamic rect (RBSP from
+ * the row groups, EP lists in stage = eps); x == NULL -- the staged RBSP of
+ * the hint / splice path (slot_bytes per frame, EP list in the slot tail) */
 int dyn_launch_emit(hipStream_t hs, int nframes, int S, const DevStream *st, const NalDesc *nal,
                     int ld_nal, const DynFrame *dfr, int ld_fr, const DynGeom *g,
-                    const uint8_t *stage, uint8_t *arena, uint64_t ld_arena, uint64_t *stamps);
+                    const uint8_t *stage, const DynScratch *x, uint8_t *arena, uint64_t ld_arena,
+                    uint64_t *stamps);
 int dyn_launch_synth(hipStream_t hs, int nframes, int S, uint8_t *src, const DynGeom *g,
                      int stream_base, int t0);
 

@@ -56,6 +56,95 @@ constexpr int HDR_MAX = 1024;           /* slice header bits (8 waypoints + MMCO
 constexpr int OBUF = 6400;              /* k_dyn_emit: 127 carry + 5 + 4096 x 1.5 */
 
 constexpr uint32_t DF_OVER = 1u, DF_GENERAL = 2u;   /* DynFrame.err bits */
+/* k_dyn_epfix could not settle the NAL's EP positions from the candidates
+ * (too many): k_dyn_epscan scans it whole; not an error for the emit */
+constexpr uint32_t DF_EPSLOW = 0x100u;
+
+/* ---------------------------------------------------------------------- */
+/* emulation-prevention runs                                                */
+/* ---------------------------------------------------------------------- */
+/* A 03 goes before RBSP byte i only if b_i <= 3 after two zero bytes: 22
+ * consecutive zero bits.  Every row group records, while it flushes its
+ * bits, the words in which such a run may start (ep_quick: a cheap
+ * superset); k_dyn_epfix finds the exact runs there (start a after a one
+ * bit, end e = the first one bit after it; group-local, bits past the
+ * group's count taken as ones) and, once the group's NAL bit offset O is
+ * known, the run's EP bytes by arithmetic: with A = O + a rounded up to a
+ * byte, the bytes starting at A + 8m for m = 2, 4, 6, ... while A + 8m + 6
+ * <= O + e (each is <= 3 after m zero bytes; the byte holding bit a - 1 is
+ * non-zero).  Runs starting at the group's first bit, and the bytes reaching
+ * past the group's end, are the group seam's (k_dyn_epfix reads those
+ * bytes).  At most EPC_ROW - 1 / EPC_STATIC - 1 words per group (more: the
+ * NAL takes the whole scan, k_dyn_epscan). */
+/* record words per group (count, then word indices): rect rows, static
+ * groups (64 MB rows of scroll heads: large-mv codewords can repeat a run
+ * in every MB) */
+constexpr int EPC_ROW = 256, EPC_STATIC = 4096;
+
+/* word gi of a group with `bits` data bits, data bits past the end as ones */
+__device__ inline uint32_t ep_data(uint32_t w, uint32_t gi, uint32_t bits)
+{
+    const uint32_t b0 = 32u * gi;
+    if (__builtin_expect(b0 + 32u <= bits, 1)) return w;
+    return w | (bits > b0 ? 0xffffffffu >> (bits - b0) : 0xffffffffu);
+}
+
+/* positions (bit 31 - j = position j from the top) in word w (group word
+ * gi) where a run of >= 22 zero data bits starts after a one; pw, nx: the
+ * words before / after (pw = 0 for the group's first word: a run there is
+ * the seam's) */
+__device__ inline uint32_t ep_run_starts(uint32_t pw, uint32_t w, uint32_t nx, uint32_t gi, uint32_t bits)
+{
+    uint64_t X = (uint64_t)ep_data(w, gi, bits) << 32 | ep_data(nx, gi + 1u, bits);
+    X |= X << 1;
+    X |= X << 2;
+    X |= X << 4;
+    X |= X << 8;                                 /* bit j (from the top): OR of bits j .. j + 15 */
+    X |= X << 6;                                 /* .. j + 21 */
+    const uint32_t z22 = ~(uint32_t)(X >> 32);
+    return z22 & ((ep_data(w, gi, bits) >> 1) | (pw << 31));   /* bit j - 1 is a one */
+}
+
+/* a superset of the words where a run of >= 22 zero bits starts: 22 zero
+ * bits inside w, or w's trailing + nx's leading zeros (padding past the
+ * data counts as zeros here: a few extra words, settled by k_dyn_epfix) */
+__device__ inline bool ep_quick(uint32_t w, uint32_t nx)
+{
+    uint32_t y = w | w << 1;
+    y |= y << 2;
+    y |= y << 4;
+    y |= y << 8;
+    y |= y << 6;                                 /* bit 31 - j: OR of bits j .. j + 21 (j <= 10) */
+    const uint32_t tz = w ? (uint32_t)__builtin_ctz(w) : 32u, lz = nx ? (uint32_t)__builtin_clz(nx) : 32u;
+    return (~y & 0xffe00000u) != 0u || tz + lz >= 22u;
+}
+
+/* the flush of an LDS window buf[0, n) = group words [p0, p0 + n) by a
+ * block of nthr threads (a multiple of 64): the words to the group's
+ * row-stage slot, and the words passing ep_quick to the group's record cg
+ * (count in *ncand, LDS) -- one LDS atomic per wave that has any */
+__device__ inline void flush_window(const uint32_t *buf, uint32_t n, uint32_t p0, bool last, uint32_t *out,
+                                    uint32_t *ncand, uint32_t *cg, uint32_t cmax, int t, int nthr)
+{
+    const int lane = t & 63;
+    for (uint32_t i0 = 0; i0 < n; i0 += (uint32_t)nthr) {
+        const uint32_t i = i0 + (uint32_t)t;
+        bool q = false;
+        if (i < n) {
+            const uint32_t w = buf[i];
+            out[p0 + i] = w;                            /* MSB-first words */
+            q = ep_quick(w, i + 1 < n ? buf[i + 1] : (last ? 0xffffffffu : 0u));
+        }
+        const uint64_t m = __builtin_amdgcn_ballot_w64(q);
+        if (m) {
+            uint32_t base = 0;
+            if (lane == (int)__builtin_ctzll(m)) base = atomicAdd(ncand, (uint32_t)__builtin_popcountll(m));
+            base = (uint32_t)__shfl((int)base, (int)__builtin_ctzll(m), 64);
+            const uint32_t k = base + (uint32_t)__builtin_popcountll(m & ((1ull << lane) - 1ull));
+            if (q && k < cmax) cg[1 + k] = p0 + i;
+        }
+    }
+}
 
 __device__ inline uint32_t ld32(const uint8_t *p) { return *reinterpret_cast<const uint32_t *>(p); }
 
@@ -182,7 +271,10 @@ __global__ __launch_bounds__(256) void k_dyn_rows(const DevStream *__restrict__ 
     }
     if (my_gen) gen = 1;
     __syncthreads();
-    if (t == 0) DF->err = gen ? DF_GENERAL : 0u;
+    if (t == 0) {
+        DF->err = gen ? DF_GENERAL : 0u;
+        DF->ep = 0u;                                    /* k_dyn_epscan adds to it */
+    }
 }
 
 /* ---------------------------------------------------------------------- */
@@ -583,6 +675,14 @@ __host__ __device__ inline uint64_t rs_group_words(const DynGeom &g, int nA, int
     return (uint64_t)(gi - g.h) * g.rs_static_words + (uint64_t)g.h * g.rs_row_words;
 }
 
+/* the EP-candidate record of row group gi (EPC_ROW / EPC_STATIC words at the end of its
+ * row-stage slot, after the group's provable bits) */
+__host__ __device__ inline uint64_t rs_runs_words(const DynGeom &g, int nA, int gi)
+{
+    const bool row = gi >= nA && gi < nA + g.h;
+    return rs_group_words(g, nA, gi) + (row ? g.rs_row_words - EPC_ROW : g.rs_static_words - EPC_STATIC);
+}
+
 /* lo[i]: piece length (11) | nC + 1 (5) << 11 */
 constexpr uint32_t LO_LEN = 0x7ffu;
 
@@ -660,6 +760,7 @@ constexpr int GW = 64;
 constexpr int GBUF_WORDS = SCROLL_GBUF_WORDS;   /* 8 Kbit per pass */
 
 struct StaticFixed {
+    uint32_t ncand;
     uint32_t buf[GBUF_WORDS];
     uint64_t hhi[12], hlo[12];
     uint32_t hlen[12];
@@ -690,7 +791,10 @@ __global__ __launch_bounds__(GW) void k_dyn_static(const DevStream *__restrict__
         L.wl[t] = pend[s].wl[t];
         L.wv[t] = pend[s].wv[t];
     }
-    if (t == 0) L.head_over = 0;
+    if (t == 0) {
+        L.head_over = 0;
+        L.ncand = 0;
+    }
     const DevStream *S = st + s;
     const NalDesc d = nal[(size_t)s * ld_nal + j];
     wave_sync();
@@ -746,7 +850,7 @@ __global__ __launch_bounds__(GW) void k_dyn_static(const DevStream *__restrict__
     wave_sync();
 
     uint32_t *out = rowstage + nb * g.rs_frame_words + rs_group_words(g, nA, gi);
-    const uint32_t nw = min((bits + 31u) >> 5, g.rs_static_words);   /* provable bound: never clipped */
+    const uint32_t nw = min((bits + 31u) >> 5, g.rs_static_words - EPC_STATIC);   /* provable bound: never clipped */
     const int ne = rb - ra;
     auto cnt_le = [&](uint32_t x) -> int {              /* # e in [0, ne] with moff[e] <= x */
         int lo = 0, hi = ne + 1;
@@ -799,9 +903,11 @@ __global__ __launch_bounds__(GW) void k_dyn_static(const DevStream *__restrict__
             sk.finish();
         }
         wave_sync();
-        for (uint32_t i = (uint32_t)t; i < n; i += GW) out[p0 + i] = L.buf[i];   /* MSB-first words */
+        flush_window(L.buf, n, p0, p0 + n >= nw, out, &L.ncand,
+                     rowstage + nb * g.rs_frame_words + rs_runs_words(g, nA, gi), EPC_STATIC - 1, t, GW);
         wave_sync();
     }
+    if (t == 0) rowstage[nb * g.rs_frame_words + rs_runs_words(g, nA, gi)] = L.ncand;
 }
 
 /* a block body of n <= 128 bits held right-aligned in hi:lo -> four words,
@@ -892,6 +998,7 @@ struct RowFixed {
     int32_t wo[8], wl[8], wv[8];
     int32_t head_over;
     uint32_t rt[32];                             /* the row's prediction-row table (k_dyn_rows) */
+    uint32_t ncand;                              /* EP candidate words of the row */
 };
 
 /* dynamic LDS of k_dyn_row: lv [NPC w] uint4 (levels, then bodies), mbits
@@ -1092,7 +1199,10 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
         L.wl[t] = pend[s].wl[t];
         L.wv[t] = pend[s].wv[t];
     }
-    if (t == 0) L.head_over = 0;
+    if (t == 0) {
+        L.head_over = 0;
+        L.ncand = 0;
+    }
     if (t < SORT_KEYS) L.kc[0][t] = 0u;
     load_ptabs(L.ptabs, t, T);
     if (!general && t < 32) L.rt[t] = rows[nb * (size_t)(32 * g.h) + (t < 16 ? 16 * r + t : 16 * g.h + (t < 24 ? 8 * r + t - 16 : 8 * g.h + 8 * r + t - 24))];
@@ -1102,6 +1212,9 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
     /* ---- 1-2: records (levels -> CAVLC bodies) into LDS ---------------- */
     const int np = (ntask + T - 1) / T;                 /* tasks per thread, <= ROW_NPMAX */
     __syncthreads();                                    /* the row table (rt) */
+#if defined(SCROLL_ABL_STOP) && SCROLL_ABL_STOP == 0
+    return;
+#endif
     if (!general) {
         const __amdgpu_buffer_rsrc_t fs = buf_rsrc(src + (size_t)s * g.src_ld + (size_t)f * g.src_fr,
                                                    (uint32_t)g.src_fr);
@@ -1241,7 +1354,11 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
     if (!general && wave == nwv - 1) {
         for (int k = lane; k < w; k += 64) {
             uint64_t v = 0;
+#ifdef SCROLL_ABL_NOPOLL
+            if (false) {
+#else
             if (r > 0) {
+#endif
                 const unsigned long long *p = tcx + (nb * R.h + r - 1) * (size_t)w + k;
                 for (;;) {
                     v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1377,7 +1494,7 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
 
     /* ---- 5: bits -> the row's own row-stage words ------------------------ */
     uint32_t *out = rowstage + nb * g.rs_frame_words + rs_group_words(g, nA, gi);
-    const uint32_t nw = min((bits + 31u) >> 5, g.rs_row_words);   /* provable bound: never clipped */
+    const uint32_t nw = min((bits + 31u) >> 5, g.rs_row_words - EPC_ROW);   /* provable bound: never clipped */
     const int npass = (int)((nw + ROW_GB - 1) / ROW_GB);
     for (int pi = 0; pi < npass; ++pi) {
         const uint32_t p0 = (uint32_t)pi * ROW_GB;
@@ -1428,9 +1545,11 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
             }
         }
         __syncthreads();
-        for (uint32_t i = (uint32_t)t; i < n; i += (uint32_t)T) out[p0 + i] = L.buf[i];   /* MSB-first words */
+        flush_window(L.buf, n, p0, p0 + n >= nw, out, &L.ncand, out + (g.rs_row_words - EPC_ROW), EPC_ROW - 1,
+                     t, T);
         __syncthreads();
     }
+    if (t == 0) out[g.rs_row_words - EPC_ROW] = L.ncand;
     if (stamps && t == 0) {
         stv[5] = __builtin_amdgcn_s_memrealtime();
         uint64_t *o = stamps + (((size_t)s * gridDim.y + f) * ng + gi) * 8;
@@ -1534,31 +1653,18 @@ __device__ inline void stitch_load(StitchLoads &L, uint32_t c0, int t, int ng, u
     gcarry = gg;
 }
 
-/* grid (frames, streams) */
-__global__ __launch_bounds__(ST_T) void k_dyn_stitch(DevStream *__restrict__ st, DynFrame *__restrict__ dfr,
-                                                     int ld_fr, DynGeom g, const uint32_t *__restrict__ rowstage,
-                                                     const uint32_t *__restrict__ gbits,
-                                                     uint8_t *__restrict__ stage, uint64_t *__restrict__ stamps)
+/* the row-group table of NAL nb in LDS (wave 0): goff = bit offsets (goff[ng]
+ * = RBSP bits incl. the stop bit), gb = bit counts, gw = first row-stage
+ * words in the frame's region */
+__device__ inline void rs_table(const uint32_t *gbits, size_t nb, const DynGeom &g, uint32_t *goff,
+                                uint32_t *gb, uint32_t *gw, int t)
 {
-    __shared__ uint32_t goff[65], gb[64], gw[64];
-    __shared__ int32_t wmax[ST_NW];
-    __shared__ uint32_t ep_n;
-    /* debug: realtime at entry, after the group scan, after the first
-     * chunk's assembly and EP scan, at exit; chunks; HW_ID */
-    uint64_t *stp = stamps && threadIdx.x == 0 ? stamps + ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * 8 : nullptr;
-    if (stp) stp[0] = __builtin_amdgcn_s_memrealtime();
-    __shared__ uint4 cbuf4[ST_CHUNK / 16];              /* the chunk's bytes */
-    uint32_t *cbuf = reinterpret_cast<uint32_t *>(cbuf4);
-    const int f = blockIdx.x, s = blockIdx.y, t = threadIdx.x, lane = t & 63;
-    const size_t nb = (size_t)s * ld_fr + f;
-    DynFrame *DF = dfr + nb;
-    if (DF->nal < 0) return;
     const int ng = g.ngroups;
     constexpr int SR = DYN_STATIC_ROWS;
     const int nA = max(1, (g.y0 + SR - 1) / SR);
     if (t < 64) {
         const uint32_t b = t < ng ? gbits[nb * (size_t)ng + t] : 0u;
-        const uint32_t incl = wave_incl_sum(b, lane);
+        const uint32_t incl = wave_incl_sum(b, t);
         if (t < ng) {
             gb[t] = b;
             goff[t] = incl - b;
@@ -1566,36 +1672,154 @@ __global__ __launch_bounds__(ST_T) void k_dyn_stitch(DevStream *__restrict__ st,
         }
         if (t == 63) goff[ng] = incl;
     }
+}
+
+/* the RBSP word (MSB first) at bit P, a multiple of 32 (0 past the end) */
+__device__ inline uint32_t rs_word(uint32_t P, int ng, uint32_t T, const uint32_t *goff, const uint32_t *gb,
+                                   const uint32_t *gw, const uint32_t *fr)
+{
+    if (P >= T) return 0u;
+    int gg = stitch_group(P, ng, goff);
+    return stitch_word(P, gg, ng, T, goff, gb, gw, fr);
+}
+
+/* RBSP byte i */
+__device__ inline uint32_t rs_byte(uint32_t i, int ng, uint32_t T, const uint32_t *goff, const uint32_t *gb,
+                                   const uint32_t *gw, const uint32_t *fr)
+{
+    return (rs_word(8u * (i & ~3u), ng, T, goff, gb, gw, fr) >> (8u * (3u - (i & 3u)))) & 255u;
+}
+
+/* w[i] for i in 0..8 without indexing (three levels of selects) */
+__device__ inline uint32_t pick9(const uint32_t w[9], uint32_t i)
+{
+    const uint32_t a = (i & 1u) ? w[1] : w[0], b = (i & 1u) ? w[3] : w[2];
+    const uint32_t c = (i & 1u) ? w[5] : w[4], e = (i & 1u) ? w[7] : w[6];
+    const uint32_t ab = (i & 2u) ? b : a, ce = (i & 2u) ? e : c;
+    const uint32_t r = (i & 4u) ? ce : ab;
+    return (i & 8u) ? w[8] : r;
+}
+
+/* nine row-stage words from byte offset wo of the frame's region */
+__device__ inline void rs_load9(__amdgpu_buffer_rsrc_t rr, uint32_t wo, uint32_t x[9])
+{
+    const auto a = __builtin_amdgcn_raw_buffer_load_b128(rr, wo, 0, 0);
+    const auto b = __builtin_amdgcn_raw_buffer_load_b128(rr, wo + 16u, 0, 0);
+    x[0] = (uint32_t)a[0]; x[1] = (uint32_t)a[1]; x[2] = (uint32_t)a[2]; x[3] = (uint32_t)a[3];
+    x[4] = (uint32_t)b[0]; x[5] = (uint32_t)b[1]; x[6] = (uint32_t)b[2]; x[7] = (uint32_t)b[3];
+    x[8] = __builtin_amdgcn_raw_buffer_load_b32(rr, wo + 32u, 0, 0);
+}
+
+/* the 32 RBSP bytes from bit P (a multiple of 128) as eight words in memory
+ * order.  Inside one row group: nine row-stage words funnel-shifted by the
+ * group's bit phase (gg: the thread's group, carried forward).  Across one
+ * group seam (a few windows per NAL): the first group's words up to the seam
+ * and the next group's words from its bit 0, shifted into place.  Three or
+ * more groups (groups under 256 bits: rare) word by word.  Bits past the
+ * NAL's end are unspecified (never used). */
+__device__ inline void rs_load8(uint32_t P, int &gg, int ng, uint32_t T, const uint32_t *goff, const uint32_t *gb,
+                                const uint32_t *gw, const uint32_t *fr, __amdgpu_buffer_rsrc_t rr, uint32_t w[8])
+{
+    if (goff[gg] > P) gg = stitch_group(P, ng, goff);     /* never for increasing P */
+    while (gg + 1 < ng && goff[gg + 1] <= P) ++gg;
+    const uint32_t lp = P - goff[gg];
+    const uint32_t end = goff[gg] + gb[gg];              /* the group's end (bits) */
+    const bool two = P + 256u > end && gg + 1 < ng && (gg + 2 >= ng || P + 256u <= goff[gg + 2]) &&
+                     gb[gg + 1] >= 256u;
+    if (P + 256u <= end || gg + 1 >= ng || two) {
+        uint32_t x[9];
+        rs_load9(rr, 4u * (gw[gg] + (lp >> 5)), x);
+        const uint32_t sh = lp & 31u;
+        uint32_t a[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) a[k] = sh ? __builtin_amdgcn_alignbit(x[k], x[k + 1], 32u - sh) : x[k];
+        if (two) {
+            /* m bits from this group, then the next group from its bit 0 */
+            const uint32_t m = end - P, dw = (m + 31u) >> 5, r = m & 31u;
+            uint32_t y[9];
+            rs_load9(rr, 4u * gw[gg + 1], y);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const uint32_t kk = (uint32_t)k;
+                uint32_t v;
+                if (32u * kk + 32u <= m) {
+                    v = a[k];
+                } else if (32u * kk >= m) {                 /* next-group bits 32 k - m .. */
+                    const uint32_t i0 = kk - dw;
+                    const uint32_t lo = pick9(y, i0), hi = pick9(y, i0 + 1u);
+                    v = r ? __builtin_amdgcn_alignbit(lo, hi, r) : lo;
+                } else {                                    /* the seam word */
+                    const uint32_t keep = m - 32u * kk;     /* 1..31 bits of this group */
+                    v = (a[k] & ~(0xffffffffu >> keep)) | (y[0] >> keep);
+                }
+                a[k] = v;
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) w[k] = __builtin_bswap32(a[k]);
+    } else {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const uint32_t Pk = P + 32u * (uint32_t)k;
+            int g2 = gg;
+            w[k] = Pk < T ? __builtin_bswap32(stitch_word(Pk, g2, ng, T, goff, gb, gw, fr)) : 0u;
+        }
+    }
+}
+
+/* ---------------------------------------------------------------------- */
+/* k_dyn_epscan: a NAL's RBSP size and emulation-prevention positions, read  */
+/* straight from its row groups -- no staged copy of the RBSP               */
+/* ---------------------------------------------------------------------- */
+/* Only for the NALs k_dyn_epfix flagged DF_EPSLOW (more candidates or EP
+ * bytes than it keeps; never in the benches).
+ * EPS_Z workgroups per NAL; workgroup z takes the 4 KB chunks z, z + EPS_Z,
+ * ... (the RBSP is never written anywhere: k_dyn_emit_gather assembles the
+ * arena bytes from the row groups again).  Per chunk: every staged word from
+ * the row-stage word(s) it spans (a funnel shift), the chunk's bytes in LDS,
+ * then the closed-form EP rule per byte.  The zero run before the chunk comes
+ * from a look-back over the RBSP before it, and only when the chunk's first
+ * byte is <= 3 (otherwise no byte of the chunk can depend on it).  EP
+ * positions gather in LDS and go to the frame's EP list (k_dyn_emit_gather
+ * sorts them) at a base reserved by one global atomic per workgroup; DF->ep
+ * ends as the NAL's total (k_dyn_epfix zeroed it and set rbsp_bytes). */
+#ifndef SCROLL_EPS_Z
+#define SCROLL_EPS_Z 4
+#endif
+constexpr int EPS_Z = SCROLL_EPS_Z;
+
+/* grid (EPS_Z, frames, streams) */
+__global__ __launch_bounds__(ST_T) void k_dyn_epscan(DevStream *__restrict__ st, DynFrame *__restrict__ dfr,
+                                                     int ld_fr, DynGeom g, const uint32_t *__restrict__ rowstage,
+                                                     const uint32_t *__restrict__ gbits, uint8_t *__restrict__ eps)
+{
+    __shared__ uint32_t goff[65], gb[64], gw[64];
+    __shared__ int32_t wmax[ST_NW];
+    __shared__ uint32_t ep_n, ep_base;
+    __shared__ uint4 cbuf4[ST_CHUNK / 16];              /* the chunk's bytes */
+    __shared__ uint32_t epl[EPLIST_MAX];                /* this workgroup's EP positions */
+    uint32_t *cbuf = reinterpret_cast<uint32_t *>(cbuf4);
+    const int z = blockIdx.x, f = blockIdx.y, s = blockIdx.z, t = threadIdx.x;
+    const size_t nb = (size_t)s * ld_fr + f;
+    DynFrame *DF = dfr + nb;
+    if (DF->nal < 0 || !(DF->err & DF_EPSLOW)) return;  /* k_dyn_epfix settled it */
+    const int ng = g.ngroups;
+    rs_table(gbits, nb, g, goff, gb, gw, t);
     if (t == 0) ep_n = 0;
     __syncthreads();
     const uint32_t T = goff[ng];                        /* NAL RBSP bits incl. the stop bit */
     const uint32_t nin = (T + 7) >> 3;                  /* bitwriter.c:103-111 */
-    if (stp) stp[1] = __builtin_amdgcn_s_memrealtime();
-    /* whole 32-byte steps must fit before the slot tail (EP positions, levels) */
-    const bool over = ((nin + 31u) & ~31u) > g.slot_bytes - DYN_OVF_BYTES;
-    if (over) {
-        if (t == 0) {
-            DF->err = DF_OVER;
-            DF->rbsp_bytes = 0;
-            DF->ep = 0;
-            atomicOr((unsigned int *)&st[s].err, SCROLL_DEVERR_DYN);
-        }
-        return;
-    }
-    uint8_t *out = stage + nb * g.slot_bytes;
-    uint32_t *eplist = reinterpret_cast<uint32_t *>(out + g.slot_bytes - DYN_OVF_BYTES);
     const uint32_t *fr = rowstage + nb * g.rs_frame_words;
-    const uint32_t Pend = 8u * ((nin + 31u) & ~31u);
-    int carry = -1;                                     /* last non-zero RBSP byte before the chunk */
     StitchLoads ld;
-    int gcarry = stitch_group(32u * (uint32_t)t, ng, goff);
-    stitch_load(ld, 0, t, ng, T, goff, gb, gw, fr, gcarry);
-    for (uint32_t c0 = 0; c0 < nin; c0 += ST_CHUNK) {
-        /* assemble this chunk's words (loaded), stage them, then start the
-         * next chunk's loads */
+    uint32_t c0 = (uint32_t)z * ST_CHUNK;
+    int gcarry = 0;
+    if (c0 < nin) {
+        gcarry = stitch_group(c0 * 8u + 32u * (uint32_t)t, ng, goff);
+        stitch_load(ld, c0, t, ng, T, goff, gb, gw, fr, gcarry);
+    }
+    for (; c0 < nin; c0 += EPS_Z * ST_CHUNK) {
         {
             const uint32_t P0 = c0 * 8u + 32u * (uint32_t)t;
-            uint32_t *o32 = reinterpret_cast<uint32_t *>(out + c0);
 #pragma unroll
             for (int k = 0; k < ST_KW; ++k) {
                 const uint32_t P = P0 + 32u * ST_T * (uint32_t)k;
@@ -1617,14 +1841,25 @@ __global__ __launch_bounds__(ST_T) void k_dyn_stitch(DevStream *__restrict__ st,
                         }
                     }
                 }
-                v = __builtin_bswap32(v);                  /* memory order */
-                if (P < Pend) o32[t + ST_T * k] = v;
-                cbuf[t + ST_T * k] = v;
+                cbuf[t + ST_T * k] = __builtin_bswap32(v);   /* memory order */
             }
         }
-        if (c0 + ST_CHUNK < nin) stitch_load(ld, c0 + ST_CHUNK, t, ng, T, goff, gb, gw, fr, gcarry);
+        const uint32_t cn = c0 + EPS_Z * ST_CHUNK;
+        if (cn < nin) stitch_load(ld, cn, t, ng, T, goff, gb, gw, fr, gcarry);
         lds_barrier();                                  /* the next chunk's loads stay in flight */
-        if (stp && c0 == 0) stp[2] = __builtin_amdgcn_s_memrealtime();
+        /* the last non-zero RBSP byte before the chunk: needed only when its
+         * first byte is <= 3 (else that byte is non-zero and no EP decision
+         * of the chunk reaches behind it) */
+        int lz = -1;
+        if (t == 0 && c0 > 0 && (cbuf[0] & 255u) <= 3u) {
+            for (int64_t P = 8ll * c0 - 32; P >= 0; P -= 32) {
+                const uint32_t w = rs_word((uint32_t)P, ng, T, goff, gb, gw, fr);
+                if (w) {
+                    lz = (int)(P >> 3) + 3 - (__builtin_ctz(w) >> 3);
+                    break;
+                }
+            }
+        }
         /* emulation prevention of this thread's 4 ST_KW contiguous bytes */
         const uint32_t ib = c0 + 4u * ST_KW * (uint32_t)t;
         uint32_t wv[ST_KW];
@@ -1639,10 +1874,10 @@ __global__ __launch_bounds__(ST_T) void k_dyn_stitch(DevStream *__restrict__ st,
             const uint32_t m = ib + 4u * w < nin ? wv[w] : 0u;
             if (m) lnz = (int)(ib + 4u * w) + 3 - (__builtin_clz(m) >> 3);
         }
+        if (t == 0 && lnz < 0) lnz = lz;                /* the run reaching back past the chunk */
         int ex, tot;
         block_excl_max<ST_NW, true>(lnz, wmax, ex, tot);   /* its barriers also free cbuf */
-        int prev = max(carry, ex);
-        carry = max(carry, tot);
+        int prev = t == 0 ? lz : ex;
         uint32_t ins = 0;
 #pragma unroll
         for (int i = 0; i < 4 * ST_KW; ++i) {
@@ -1656,22 +1891,181 @@ __global__ __launch_bounds__(ST_T) void k_dyn_stitch(DevStream *__restrict__ st,
             while (ins) {
                 const int i = __builtin_ctz(ins);
                 ins &= ins - 1u;
-                if (k < (uint32_t)EPLIST_MAX) eplist[k] = ib + (uint32_t)i;   /* RBSP index the 03 precedes */
+                if (k < (uint32_t)EPLIST_MAX) epl[k] = ib + (uint32_t)i;   /* RBSP index the 03 precedes */
                 k++;
             }
         }
-        if (stp && c0 == 0) stp[3] = __builtin_amdgcn_s_memrealtime();
+    }
+    __syncthreads();
+    const uint32_t n = ep_n;
+    if (n == 0) return;
+    if (t == 0) ep_base = atomicAdd(&DF->ep, n);
+    __syncthreads();
+    uint32_t *eplist = reinterpret_cast<uint32_t *>(eps + nb * DYN_OVF_BYTES);
+    const uint32_t base = ep_base;
+    for (uint32_t i = (uint32_t)t; i < n && i < (uint32_t)EPLIST_MAX; i += ST_T)
+        if (base + i < (uint32_t)EPLIST_MAX) eplist[base + i] = epl[i];
+}
+
+/* ---------------------------------------------------------------------- */
+/* k_dyn_epfix: a NAL's RBSP size and EP positions from the candidates      */
+/* ---------------------------------------------------------------------- */
+/* One workgroup per dynamic NAL.  The row groups' bit counts place the
+ * groups, which fixes every byte's phase; then
+ *   - each candidate word (ep_quick) is read back from its group's
+ *     row-stage words: its exact runs, each run's EP bytes by arithmetic;
+ *   - each group seam (NAL start included) is decided from the RBSP itself
+ *     (read from the row groups a word at a time): from the byte holding
+ *     the seam, with the zero run before it looked up backwards, up to the
+ *     first non-zero byte at or after the first byte wholly inside the group
+ *     (closed form of nal.c:33-38, ep_insert).
+ * Every other byte is preceded by a non-zero byte within fewer than 22 zero
+ * bits.  A byte can be decided twice (a run's last byte at a seam): kept
+ * once.  More candidates in a group than its record holds, or more than EPF_LIST
+ * positions: DF_EPSLOW (k_dyn_epscan scans the NAL). */
+constexpr int EPF_T = 256;
+constexpr int EPF_LIST = 4096;
+
+/* the RBSP bytes from byte B on, with the zero run before it: EP positions
+ * -> lst (count nlst) until the first non-zero byte at or after byte Bend */
+__device__ inline void ep_eval_bytes(uint32_t B, uint32_t Bend, uint32_t nin, int ng, uint32_t T,
+                                     const uint32_t *goff, const uint32_t *gb, const uint32_t *gw,
+                                     const uint32_t *fr, uint32_t *lst, uint32_t *nlst)
+{
+    uint32_t cw = 0, ci = 0xffffffffu;                  /* one RBSP word cached */
+    auto byte_at = [&](uint32_t i) -> uint32_t {
+        if ((i >> 2) != ci) {
+            ci = i >> 2;
+            cw = rs_word(32u * ci, ng, T, goff, gb, gw, fr);
+        }
+        return (cw >> (8u * (3u - (i & 3u)))) & 255u;
+    };
+    int k = 0;                                          /* zero bytes right before B */
+    for (int64_t i = (int64_t)B - 1; i >= 0; --i) {
+        if (byte_at((uint32_t)i)) break;
+        ++k;
+    }
+    for (uint32_t i = B; i < nin; ++i) {
+        const uint32_t b = byte_at(i);
+        if (ep_insert(b, k)) {
+            const uint32_t q = atomicAdd(nlst, 1u);
+            if (q < (uint32_t)EPF_LIST) lst[q] = i;
+        }
+        if (b == 0) {
+            ++k;
+        } else {
+            if (i >= Bend) break;
+            k = 0;
+        }
+    }
+}
+
+/* grid (frames, streams) */
+__global__ __launch_bounds__(EPF_T) void k_dyn_epfix(DevStream *__restrict__ st, DynFrame *__restrict__ dfr,
+                                                     int ld_fr, DynGeom g, const uint32_t *__restrict__ rowstage,
+                                                     const uint32_t *__restrict__ gbits, uint8_t *__restrict__ eps)
+{
+    __shared__ uint32_t goff[65], gb[64], gw[64];
+    __shared__ uint32_t cbase[65];                      /* runs before group g */
+    __shared__ uint32_t lst[EPF_LIST];
+    __shared__ uint32_t nlst, nu, slow;
+    const int f = blockIdx.x, s = blockIdx.y, t = threadIdx.x;
+    const size_t nb = (size_t)s * ld_fr + f;
+    DynFrame *DF = dfr + nb;
+    if (DF->nal < 0) return;
+    const int ng = g.ngroups;
+    constexpr int SR = DYN_STATIC_ROWS;
+    const int nA = max(1, (g.y0 + SR - 1) / SR);
+    const uint32_t *fr = rowstage + nb * g.rs_frame_words;
+    rs_table(gbits, nb, g, goff, gb, gw, t);
+    if (t < 64) {
+        const uint32_t c = t < ng ? fr[rs_runs_words(g, nA, t)] : 0u;
+        const uint32_t cmax = (t >= nA && t < nA + g.h) ? EPC_ROW - 1u : EPC_STATIC - 1u;
+        const uint32_t cc = min(c, cmax);
+        const uint32_t incl = wave_incl_sum(cc, t);
+        if (t < ng) cbase[t] = incl - cc;
+        if (t == 63) cbase[ng] = incl;
+        const bool ov = __builtin_amdgcn_ballot_w64(c > cmax) != 0;
+        if (t == 0) {
+            slow = ov ? 1u : 0u;
+            nlst = 0;
+            nu = 0;
+        }
+    }
+    __syncthreads();
+    const uint32_t T = goff[ng];                        /* NAL RBSP bits incl. the stop bit */
+    const uint32_t nin = (T + 7) >> 3;                  /* bitwriter.c:103-111 */
+    if (((nin + 31u) & ~31u) > g.slot_bytes - DYN_OVF_BYTES) {   /* the cap the API sets */
+        if (t == 0) {
+            DF->err = DF_OVER;
+            DF->rbsp_bytes = 0;
+            DF->ep = 0;
+            atomicOr((unsigned int *)&st[s].err, SCROLL_DEVERR_DYN);
+        }
+        return;
+    }
+    const uint32_t nseam = (uint32_t)ng, nwork = slow ? 0u : nseam + cbase[ng];
+    for (uint32_t wk = (uint32_t)t; wk < nwork; wk += EPF_T) {
+        if (wk < nseam) {                               /* the seam before group wk (0: NAL start) */
+            const uint32_t S = goff[wk];
+            if (S < T) ep_eval_bytes(S >> 3, (S + 7) >> 3, nin, ng, T, goff, gb, gw, fr, lst, &nlst);
+            continue;
+        }
+        const uint32_t ci = wk - nseam;
+        int gg = 0;
+        while (gg + 1 < ng && cbase[gg + 1] <= ci) ++gg;
+        const uint32_t *src = fr + gw[gg];
+        const uint32_t wi = fr[rs_runs_words(g, nA, gg) + 1 + (ci - cbase[gg])];
+        const uint32_t bits = gb[gg], nwd = (bits + 31u) >> 5, O = goff[gg];
+        if (wi >= nwd) continue;
+        const uint32_t w = ep_data(src[wi], wi, bits);
+        const uint32_t nx = wi + 1 < nwd ? ep_data(src[wi + 1], wi + 1, bits) : 0xffffffffu;
+        uint32_t m = ep_run_starts(wi ? src[wi - 1] : 0u, w, nx, wi, bits);
+        while (m) {                                     /* usually one run */
+            const uint32_t a = (uint32_t)__builtin_clz(m);
+            m &= ~(0x80000000u >> a);
+            const uint64_t Y = ((uint64_t)w << 32 | nx) << a;
+            uint32_t e = bits;
+            if (Y) {
+                e = 32u * wi + a + (uint32_t)__builtin_clzll(Y);
+            } else {
+                for (uint32_t q = wi + 2; q < nwd; ++q) {
+                    const uint32_t v = ep_data(src[q], q, bits);
+                    if (v) {
+                        e = 32u * q + (uint32_t)__builtin_clz(v);
+                        break;
+                    }
+                }
+            }
+            const uint32_t A = (O + 32u * wi + a + 7u) & ~7u, E = O + e;
+            for (uint32_t j = A + 16u; j + 6u <= E; j += 16u) {
+                const uint32_t q = atomicAdd(&nlst, 1u);
+                if (q < (uint32_t)EPF_LIST) lst[q] = j >> 3;
+            }
+        }
+    }
+    __syncthreads();
+    const uint32_t n = nlst;
+    if (slow || n > (uint32_t)EPF_LIST) {
+        if (t == 0) {
+            DF->err = DF_EPSLOW;                        /* k_dyn_epscan finds them */
+            DF->rbsp_bytes = nin;
+            DF->ep = 0;
+        }
+        return;
+    }
+    uint32_t *eplist = reinterpret_cast<uint32_t *>(eps + nb * DYN_OVF_BYTES);
+    for (uint32_t i = (uint32_t)t; i < n; i += EPF_T) {  /* each position once */
+        const uint32_t v = lst[i];
+        bool dup = false;
+        for (uint32_t j = 0; j < i; ++j) dup |= lst[j] == v;
+        if (!dup) eplist[atomicAdd(&nu, 1u)] = v;
     }
     __syncthreads();
     if (t == 0) {
         DF->err = 0;                                    /* clears DF_GENERAL */
         DF->rbsp_bytes = nin;
-        DF->ep = ep_n;
-    }
-    if (stp) {
-        stp[4] = __builtin_amdgcn_s_memrealtime();
-        stp[5] = (nin + ST_CHUNK - 1) / ST_CHUNK;
-        stp[7] = (uint64_t)(uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 4);     /* HW_ID */
+        DF->ep = nu;
     }
 }
 
@@ -1688,25 +2082,37 @@ __device__ inline void store16(uint8_t *A, uint64_t p, const uint8_t *src, uint6
         if (p + i >= lo && p + i < hi) A[p + i] = src[i];
 }
 
+/* rowstage != nullptr: the dynamic rect's NALs, whose RBSP lives only in
+ * their row groups (gbits); else the staged RBSP of the hint / splice path */
 __global__ __launch_bounds__(DT) void k_dyn_emit(const DevStream *__restrict__ st,
                                                  const NalDesc *__restrict__ nal, int ld_nal,
                                                  const DynFrame *__restrict__ dfr, int ld_fr,
                                                  DynGeom g, const uint8_t *__restrict__ stage,
+                                                 const uint32_t *__restrict__ rowstage,
+                                                 const uint32_t *__restrict__ gbits,
                                                  uint8_t *__restrict__ arena, uint64_t ld_arena)
 {
     __shared__ alignas(16) uint8_t ob[OBUF];
     __shared__ int32_t wmax[NW];
     __shared__ uint32_t wsum[NW];
+    __shared__ uint32_t goff[65], gb[64], gw[64];
     const int f = blockIdx.x, s = blockIdx.y, t = threadIdx.x;
-    const DynFrame df = dfr[(size_t)s * ld_fr + f];
+    const size_t nb = (size_t)s * ld_fr + f;
+    const DynFrame df = dfr[nb];
     const int j = df.nal;
-    if (j < 0 || j >= st[s].nnal || df.err) return;          /* nnal = 0: nothing committed */
+    if (j < 0 || j >= st[s].nnal || (df.err & ~DF_EPSLOW)) return;   /* nnal = 0: nothing committed */
     if (df.ep <= ep_cap(g)) return;                          /* k_dyn_emit_gather's NAL */
     const NalDesc d = nal[(size_t)s * ld_nal + j];
     if (d.slow != 2) return;
     uint8_t *A = arena + (size_t)s * ld_arena;
     const uint64_t o0 = d.out_off, o1 = o0 + d.size;
-    const uint8_t *in = stage + ((size_t)s * ld_fr + f) * g.slot_bytes;
+    const bool RS = rowstage != nullptr;
+    const uint8_t *in = RS ? nullptr : stage + nb * g.slot_bytes;
+    const uint32_t *fr = RS ? rowstage + nb * g.rs_frame_words : nullptr;
+    if (RS) rs_table(gbits, nb, g, goff, gb, gw, t);
+    __syncthreads();
+    const int ng = g.ngroups;
+    const uint32_t T = RS ? goff[ng] : 0u;
     const uint32_t nin = df.rbsp_bytes;
 
     uint64_t lb = o0 & ~127ull;                  /* arena byte of ob[0] (line aligned) */
@@ -1719,7 +2125,16 @@ __global__ __launch_bounds__(DT) void k_dyn_emit(const DevStream *__restrict__ s
         const uint32_t n = ib < nin ? min(16u, nin - ib) : 0u;
         uint8_t b[16];
         {
-            const uint4 v = n ? *reinterpret_cast<const uint4 *>(in + ib) : make_uint4(0, 0, 0, 0);
+            uint4 v = make_uint4(0, 0, 0, 0);
+            if (n && RS) {
+                const uint32_t P = 8u * ib;
+                v = make_uint4(__builtin_bswap32(rs_word(P, ng, T, goff, gb, gw, fr)),
+                               __builtin_bswap32(rs_word(P + 32u, ng, T, goff, gb, gw, fr)),
+                               __builtin_bswap32(rs_word(P + 64u, ng, T, goff, gb, gw, fr)),
+                               __builtin_bswap32(rs_word(P + 96u, ng, T, goff, gb, gw, fr)));
+            } else if (n) {
+                v = *reinterpret_cast<const uint4 *>(in + ib);
+            }
             const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
             for (int i = 0; i < 16; ++i) b[i] = (uint8_t)(wv[i >> 2] >> (8 * (i & 3)));
@@ -1785,30 +2200,44 @@ __device__ inline uint32_t pick4(const uint32_t w[8], int i)     /* w[i], i in 0
 #endif
 constexpr int GATHER_Z = SCROLL_GATHER_Z;             /* workgroups per NAL (2 and 4 measured slower) */
 
-template <int U>
+/* RS: the dynamic rect's NALs -- RBSP bytes assembled from the row groups
+ * (rs_load8), EP lists at stage + DYN_OVF_BYTES per frame (k_dyn_epscan);
+ * else the staged RBSP + slot-tail EP list of the hint / splice path */
+template <int U, bool RS>
 __global__ __launch_bounds__(DT) void k_dyn_emit_gather(const DevStream *__restrict__ st,
                                                         const NalDesc *__restrict__ nal, int ld_nal,
                                                         const DynFrame *__restrict__ dfr, int ld_fr,
                                                         DynGeom g, const uint8_t *__restrict__ stage,
+                                                        const uint32_t *__restrict__ rowstage,
+                                                        const uint32_t *__restrict__ gbits,
                                                         uint8_t *__restrict__ arena, uint64_t ld_arena,
                                                         uint64_t *__restrict__ stamps)
 {
     __shared__ uint32_t raw[EPLIST_MAX], sp[EPLIST_MAX];
+    __shared__ uint32_t goff[RS ? 65 : 1], gb[RS ? 64 : 1], gw[RS ? 64 : 1];
     const int s = blockIdx.y, f = dyn_frame_of(blockIdx.x, s), t = threadIdx.x;
     /* debug: realtime at entry / after the sort / at exit, EP count, HW_ID */
     uint64_t *stp = stamps && t == 0 && blockIdx.z == 0 ? stamps + ((size_t)s * gridDim.x + f) * 8 : nullptr;
     if (stp) stp[0] = __builtin_amdgcn_s_memrealtime();
     const DynFrame df = dfr[(size_t)s * ld_fr + f];
     const int j = df.nal;
-    if (j < 0 || j >= st[s].nnal || df.err) return;          /* nnal = 0: nothing committed */
+    if (j < 0 || j >= st[s].nnal || (df.err & ~DF_EPSLOW)) return;   /* nnal = 0: nothing committed */
     const uint32_t n = df.ep;
     if (n > ep_cap(g)) return;                               /* k_dyn_emit's NAL */
     const NalDesc d = nal[(size_t)s * ld_nal + j];
     if (d.slow != 2) return;
-    const uint8_t *in = stage + ((size_t)s * ld_fr + f) * g.slot_bytes;
-    const uint32_t *el = reinterpret_cast<const uint32_t *>(in + g.slot_bytes - DYN_OVF_BYTES);
+    const size_t nb = (size_t)s * ld_fr + f;
+    const uint8_t *in = RS ? nullptr : stage + nb * g.slot_bytes;
+    const uint32_t *el = reinterpret_cast<const uint32_t *>(RS ? stage + nb * DYN_OVF_BYTES
+                                                               : in + g.slot_bytes - DYN_OVF_BYTES);
+    const uint32_t *fr = RS ? rowstage + nb * g.rs_frame_words : nullptr;
+    if (RS) rs_table(gbits, nb, g, goff, gb, gw, t);
     for (uint32_t i = t; i < n; i += DT) raw[i] = el[i];
     __syncthreads();
+    const int ng = RS ? g.ngroups : 0;
+    const uint32_t T = RS ? goff[ng] : 0u;
+    const __amdgpu_buffer_rsrc_t rr = buf_rsrc(fr, RS ? (uint32_t)(4 * g.rs_frame_words) : 0u);
+    int gcar = 0;                                            /* RS: the thread's row group */
     /* sort by rank (positions are distinct): sp[j] = j-th smallest */
     for (uint32_t i = t; i < n; i += DT) {
         const uint32_t v = raw[i];
@@ -1878,8 +2307,15 @@ __global__ __launch_bounds__(DT) void k_dyn_emit_gather(const DevStream *__restr
                 epm[u] = em;
                 const uint32_t i0 = (uint32_t)u0 - K, a0 = i0 & ~15u;
                 shv[u] = i0 & 15u;
-                x[u] = *reinterpret_cast<const uint4 *>(in + a0);
-                if (a0 + 16 < nin) y[u] = *reinterpret_cast<const uint4 *>(in + a0 + 16);
+                if constexpr (RS) {
+                    uint32_t w8[8];
+                    rs_load8(8u * a0, gcar, ng, T, goff, gb, gw, fr, rr, w8);
+                    x[u] = make_uint4(w8[0], w8[1], w8[2], w8[3]);
+                    y[u] = make_uint4(w8[4], w8[5], w8[6], w8[7]);
+                } else {
+                    x[u] = *reinterpret_cast<const uint4 *>(in + a0);
+                    if (a0 + 16 < nin) y[u] = *reinterpret_cast<const uint4 *>(in + a0 + 16);
+                }
             }
         }
 #pragma unroll
@@ -1924,6 +2360,14 @@ __global__ __launch_bounds__(DT) void k_dyn_emit_gather(const DevStream *__restr
                 *reinterpret_cast<uint4 *>(A + q0) = make_uint4(o[0], o[1], o[2], o[3]);
             } else {                                     /* NAL edges, start code */
                 uint32_t kk = Ku[u];
+                /* RS: the <= 16 RBSP bytes of this chunk lie in the 32 from a0 */
+                uint32_t w8[8] = {0, 0, 0, 0, 0, 0, 0, 0}, a0 = 0;
+                if constexpr (RS) {
+                    const int64_t ue = (int64_t)q0 - (int64_t)o0 - 5;
+                    a0 = (uint32_t)(ue > 0 ? ue : 0) - kk;
+                    a0 &= ~15u;
+                    if (a0 < nin) rs_load8(8u * a0, gcar, ng, T, goff, gb, gw, fr, rr, w8);
+                }
                 for (int b = 0; b < 16; ++b) {
                     const uint64_t q = q0 + (uint64_t)b;
                     if (q < o0 || q >= o1) continue;
@@ -1934,6 +2378,10 @@ __global__ __launch_bounds__(DT) void k_dyn_emit_gather(const DevStream *__restr
                     } else if (kk < n && (int64_t)(sp[kk] + kk) == uu) {
                         v = 3;
                         kk++;
+                    } else if constexpr (RS) {
+                        const uint32_t r = (uint32_t)uu - kk - a0;           /* < 32 */
+                        const uint32_t wd = pick4(w8, (int)(r >> 2));
+                        v = (uint8_t)(wd >> (8u * (r & 3u)));
                     } else {
                         v = in[(uint32_t)uu - kk];
                     }
@@ -2016,35 +2464,49 @@ int dyn_launch_code(hipStream_t hs, int nframes, int S, DevStream *st, const Nal
 
 int dyn_launch_pack(hipStream_t hs, int nframes, int S, DevStream *st, const NalDesc *nal,
                     int ld_nal, const PlanPending *pend, DynFrame *dfr, int ld_fr,
-                    const DynGeom *g, const DynScratch *x, uint8_t *stage, uint64_t *stamps)
+                    const DynGeom *g, const DynScratch *x, uint8_t *eps, uint64_t *stamps)
 {
+    (void)stamps;
     if (nframes <= 0 || S <= 0) return 0;
     hipLaunchKernelGGL(k_dyn_static, dim3(g->ngroups - g->h, nframes, S), dim3(GW), 0, hs, st, nal, ld_nal,
                        pend, dfr, ld_fr, *g, x->rowstage, x->gbits);
     if (hipGetLastError() != hipSuccess) return -1;
-    hipLaunchKernelGGL(k_dyn_stitch, dim3(nframes, S), dim3(ST_T), 0, hs, st, dfr, ld_fr, *g, x->rowstage,
-                       x->gbits, stage, stamps);
+    hipLaunchKernelGGL(k_dyn_epfix, dim3(nframes, S), dim3(EPF_T), 0, hs, st, dfr, ld_fr, *g, x->rowstage,
+                       x->gbits, eps);
+    if (hipGetLastError() != hipSuccess) return -1;
+    hipLaunchKernelGGL(k_dyn_epscan, dim3(EPS_Z, nframes, S), dim3(ST_T), 0, hs, st, dfr, ld_fr, *g,
+                       x->rowstage, x->gbits, eps);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 int dyn_launch_emit(hipStream_t hs, int nframes, int S, const DevStream *st, const NalDesc *nal,
                     int ld_nal, const DynFrame *dfr, int ld_fr, const DynGeom *g,
-                    const uint8_t *stage, uint8_t *arena, uint64_t ld_arena, uint64_t *stamps)
+                    const uint8_t *stage, const DynScratch *x, uint8_t *arena, uint64_t ld_arena,
+                    uint64_t *stamps)
 {
     if (nframes <= 0 || S <= 0) return 0;
     /* U chunks per thread and iteration, their loads in flight together:
      * one (fewer registers, more resident workgroups) for NALs up to ~64 KB
      * (config 3: 0.186 / 0.173 / 0.168 ms at U = 4 / 2 / 1), four for the
      * large rects (config 5: 0.45 ms at U = 4, 0.56 at U = 1) */
-    if ((int64_t)g->w * g->h > 1024)
-        hipLaunchKernelGGL(k_dyn_emit_gather<4>, dim3(nframes, S, GATHER_Z), dim3(DT), 0, hs, st, nal, ld_nal,
-                           dfr, ld_fr, *g, stage, arena, ld_arena, stamps);
+    const bool big = (int64_t)g->w * g->h > 1024;
+    const uint32_t *rs = x ? x->rowstage : nullptr, *gbits = x ? x->gbits : nullptr;
+    const dim3 grid(nframes, S, GATHER_Z);
+    if (x && big)
+        hipLaunchKernelGGL((k_dyn_emit_gather<4, true>), grid, dim3(DT), 0, hs, st, nal, ld_nal, dfr, ld_fr, *g,
+                           stage, rs, gbits, arena, ld_arena, stamps);
+    else if (x)
+        hipLaunchKernelGGL((k_dyn_emit_gather<1, true>), grid, dim3(DT), 0, hs, st, nal, ld_nal, dfr, ld_fr, *g,
+                           stage, rs, gbits, arena, ld_arena, stamps);
+    else if (big)
+        hipLaunchKernelGGL((k_dyn_emit_gather<4, false>), grid, dim3(DT), 0, hs, st, nal, ld_nal, dfr, ld_fr,
+                           *g, stage, rs, gbits, arena, ld_arena, stamps);
     else
-        hipLaunchKernelGGL(k_dyn_emit_gather<1>, dim3(nframes, S, GATHER_Z), dim3(DT), 0, hs, st, nal, ld_nal,
-                           dfr, ld_fr, *g, stage, arena, ld_arena, stamps);
+        hipLaunchKernelGGL((k_dyn_emit_gather<1, false>), grid, dim3(DT), 0, hs, st, nal, ld_nal, dfr, ld_fr,
+                           *g, stage, rs, gbits, arena, ld_arena, stamps);
     if (hipGetLastError() != hipSuccess) return -1;
     hipLaunchKernelGGL(k_dyn_emit, dim3(nframes, S), dim3(DT), 0, hs, st, nal, ld_nal, dfr, ld_fr,
-                       *g, stage, arena, ld_arena);
+                       *g, stage, rs, gbits, arena, ld_arena);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -2065,8 +2527,9 @@ void dyn_rowstage_geom(DynGeom *g, int mbw, int mbh)
     const int below = below0 < SR ? below0 : SR;
     const int maxrows = above > below ? above : below;
     auto words = [](uint64_t bits) { return (uint32_t)((((bits + 31) / 32) + 63) & ~(uint64_t)63); };
-    g->rs_static_words = words((uint64_t)HDR_MAX + (uint64_t)maxrows * mbw * (HEAD_MAX + 1) + 64);
-    g->rs_row_words = words((uint64_t)mbw * (HEAD_MAX + 1) + (uint64_t)g->w * MB_BITS_MAX + 64);
+    /* + the group's EP-candidate record (EPC_ROW / EPC_STATIC words) at the slot end */
+    g->rs_static_words = words((uint64_t)HDR_MAX + (uint64_t)maxrows * mbw * (HEAD_MAX + 1) + 64) + EPC_STATIC;
+    g->rs_row_words = words((uint64_t)mbw * (HEAD_MAX + 1) + (uint64_t)g->w * MB_BITS_MAX + 64) + EPC_ROW;
 #ifdef SCROLL_RS_SMALL
     g->rs_static_words = g->rs_static_words < 4096 ? g->rs_static_words : 4096;   /* timing experiment only */
     g->rs_row_words = g->rs_row_words < 4096 ? g->rs_row_words : 4096;

@@ -1322,7 +1322,7 @@ static int launch(ScrollBatch *b, int nframes, int plan_mode, int nal_max, hipSt
                 DynFrame *dfr0 = b->d_dfr + nb0;
                 const uint8_t *src0 = b->d_src + (size_t)s0 * G.src_ld;
                 const uint8_t *refs0 = b->d_refs + (size_t)s0 * G.ref_ld;
-                uint8_t *stage0 = b->d_stage + nb0 * G.slot_bytes;
+                uint8_t *stage0 = b->d_stage + nb0 * DYN_OVF_BYTES;   /* EP lists only */
                 if (dyn_launch_code(hs, nframes, s1 - s0, st0, nal0, b->ld_nal, pend0, dfr0, ld_fr, &G, src0,
                                     refs0, &xc, b->dx.epoch, b->dyn_pw / 16, stamps)) {
                     set_err("k_dyn_code launch: %s", hipGetErrorString(hipGetLastError()));
@@ -1338,7 +1338,7 @@ static int launch(ScrollBatch *b, int nframes, int plan_mode, int nal_max, hipSt
                 }
                 if (dyn_launch_pack(hp, nframes, s1 - s0, st0, nal0, b->ld_nal, pend0, dfr0, ld_fr, &G, &xc,
                                     stage0, stamps ? b->d_dbg : nullptr)) {
-                    set_err("k_dyn_static / k_dyn_stitch launch: %s", hipGetErrorString(hipGetLastError()));
+                    set_err("k_dyn_static / k_dyn_epscan launch: %s", hipGetErrorString(hipGetLastError()));
                     return SCROLL_ERR_HIP;
                 }
             }
@@ -1374,7 +1374,8 @@ static int launch(ScrollBatch *b, int nframes, int plan_mode, int nal_max, hipSt
     }
     if ((rc = mark(4))) return rc;
     if (dyn && dyn_launch_emit(hs, nframes, S, b->d_st, b->d_nal, b->ld_nal, b->d_dfr, ld_fr,
-                               &b->geo, b->d_stage, b->d_arena, (uint64_t)b->ld_arena,
+                               &b->geo, b->d_stage, hint ? nullptr : &b->dx, b->d_arena,
+                               (uint64_t)b->ld_arena,
                                (b->debug & SCROLL_DEBUG_DYN_STAMPS) && b->d_dbg
                                    ? b->d_dbg + (size_t)nframes * S * 8 : nullptr)) {
         set_err("k_dyn_emit launch: %s", hipGetErrorString(hipGetLastError()));
@@ -1680,7 +1681,9 @@ int scroll_batch_set_dyn_rect(ScrollBatch *b, int x0, int y0, int w, int h, size
     hipError_t e = hipMalloc(&b->d_dfr, S * F * sizeof(DynFrame));
     if (e == hipSuccess) e = hipMalloc(&b->d_src, S * g.src_ld);
     if (e == hipSuccess) e = hipMalloc(&b->d_refs, S * dyn_pair_bytes(b));
-    if (e == hipSuccess) e = hipMalloc(&b->d_stage, S * F * g.slot_bytes);
+    /* the RBSP is never staged (k_dyn_epscan / k_dyn_emit_gather read the
+     * row groups): per frame only its EP list; slot_bytes stays the cap */
+    if (e == hipSuccess) e = hipMalloc(&b->d_stage, S * F * DYN_OVF_BYTES);
     if (e == hipSuccess) e = hipMalloc(&b->dx.rows, S * F * 32 * h * sizeof(uint32_t));
     if (e == hipSuccess) e = hipMalloc(&b->dx.meta, S * F * DYN_PIECES * w * h * sizeof(uint16_t));
     if (e == hipSuccess) e = hipMalloc(&b->dx.body_lo, S * F * DYN_PIECES * w * h * sizeof(uint2));

@@ -117,7 +117,7 @@ class ScrollHintRect(ctypes.Structure):
         ("mv_x", ctypes.c_int32), ("mv_y", ctypes.c_int32)]
 
 
-SCROLL_HINT_EXACT, SCROLL_HINT_PSKIP, SCROLL_HINT_MAX_RECTS = 0, 1, 64
+SCROLL_HINT_EXACT, SCROLL_HINT_PSKIP, SCROLL_HINT_SPEC, SCROLL_HINT_MAX_RECTS = 0, 1, 2, 64
 (SCROLL_SPLICE_OK, SCROLL_SPLICE_ERR_NAL, SCROLL_SPLICE_ERR_HEADER, SCROLL_SPLICE_ERR_MBTYPE,
  SCROLL_SPLICE_ERR_SYNTAX, SCROLL_SPLICE_ERR_REF) = range(6)
 

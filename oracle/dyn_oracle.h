@@ -49,7 +49,7 @@
 extern "C" {
 #endif
 
-typedef struct {
+typedef struct or_dyn_rect_s {
     int x0, y0, w, h;             /* MB units */
 } or_dyn_rect;
 
@@ -59,7 +59,7 @@ typedef struct {
 } or_pic;
 
 /* decoded pictures of reference A (idx 0) and B (idx 1) */
-typedef struct {
+typedef struct or_refs_s {
     const or_pic *ab[2];
 } or_refs;
 

@@ -383,33 +383,20 @@ static void sp_piece(or_bits *b, const or_splice_mb *mb, int i, int nC, const ui
     sp_copy_bits(b, rbsp, mb->boff[i], mb->blen[i]);
 }
 
-size_t or_splice_scroll_nal(uint8_t *dst, size_t cap, or_cfg *c, int off, const or_hint_rect *r,
-                            int n, int mode, const or_splice *sp, int *err)
+/* the scroll NAL with the MBs of rect [x0, x0 + w) x [y0, y0 + h) taken
+ * from mbs[] (their piece bodies in erb, erb_n bytes); shared by the splice
+ * and the hinted dynamic rect (or_hint_dyn_scroll_nal) */
+static size_t sp_compose(uint8_t *dst, size_t cap, or_cfg *c, int off, const or_hint_rect *r, int n,
+                         int mode, int x0, int y0, int w, int h, const or_splice_mb *mbs,
+                         const uint8_t *erb, size_t erb_n, int *err)
 {
     *err = 0;
     const int mbw = c->w / 16, mbh = c->h / 16, nrefs = 2 + c->nwp;
-    const int has = sp && sp->w > 0 && sp->h > 0;
-    or_splice_mb *mbs = NULL;
-    uint8_t *erb = NULL;
-    if (has) {
-        if (sp->x0 < 0 || sp->y0 < 0 || sp->x0 + sp->w > mbw || sp->y0 + sp->h > mbh) {
-            *err = OR_SPLICE_ERR_HEADER;
-            return 0;
-        }
-        mbs = (or_splice_mb *)malloc(sizeof(*mbs) * (size_t)sp->w * (size_t)sp->h);
-        erb = (uint8_t *)malloc(sp->n + 8);
-        size_t rn;
-        const int e = or_splice_parse(c, sp, mbs, erb, &rn);
-        if (e) {
-            *err = e;
-            free(mbs);
-            free(erb);
-            return 0;
-        }
-    }
+    const int has = w > 0 && h > 0;
+    const struct { int x0, y0, w, h; } rect = {x0, y0, w, h}, *sp = &rect;
     int a_end, ra, mva, rb, mvb;
     or_scroll_regions(c, off, &a_end, &ra, &mva, &rb, &mvb);
-    size_t rcap = 64 + (size_t)mbw * mbh * 24 + (has ? sp->n * 2 + (size_t)sp->w * sp->h * 64 : 0);
+    size_t rcap = 64 + (size_t)mbw * mbh * 24 + (has ? erb_n * 2 + (size_t)w * h * 64 : 0);
     uint8_t *rbsp = (uint8_t *)malloc(rcap);
     or_mvi *above = (or_mvi *)calloc((size_t)mbw, sizeof(or_mvi));
     or_mvi *cur = (or_mvi *)calloc((size_t)mbw, sizeof(or_mvi));
@@ -506,6 +493,29 @@ size_t or_splice_scroll_nal(uint8_t *dst, size_t cap, or_cfg *c, int off, const 
     free(cur);
     free(tabove);
     free(tcur);
+    return nb;
+}
+
+size_t or_splice_scroll_nal(uint8_t *dst, size_t cap, or_cfg *c, int off, const or_hint_rect *r,
+                            int n, int mode, const or_splice *sp, int *err)
+{
+    *err = 0;
+    const int mbw = c->w / 16, mbh = c->h / 16;
+    const int has = sp && sp->w > 0 && sp->h > 0;
+    if (!has) return sp_compose(dst, cap, c, off, r, n, mode, 0, 0, 0, 0, NULL, NULL, 0, err);
+    if (sp->x0 < 0 || sp->y0 < 0 || sp->x0 + sp->w > mbw || sp->y0 + sp->h > mbh) {
+        *err = OR_SPLICE_ERR_HEADER;
+        return 0;
+    }
+    or_splice_mb *mbs = (or_splice_mb *)malloc(sizeof(*mbs) * (size_t)sp->w * (size_t)sp->h);
+    uint8_t *erb = (uint8_t *)malloc(sp->n + 8);
+    size_t rn;
+    const int e = or_splice_parse(c, sp, mbs, erb, &rn);
+    size_t nb = 0;
+    if (e)
+        *err = e;
+    else
+        nb = sp_compose(dst, cap, c, off, r, n, mode, sp->x0, sp->y0, sp->w, sp->h, mbs, erb, sp->n, err);
     free(mbs);
     free(erb);
     return nb;
@@ -521,6 +531,175 @@ size_t or_compose_splice(uint8_t *dst, size_t cap, or_cfg *c, int off, int compo
         if (compose_mode == 1) return nb;
     }
     const size_t k = or_splice_scroll_nal(dst + nb, cap - nb, c, off, r, n, mode, sp, err);
+    return k ? nb + k : 0;
+}
+
+/* ------------------------------------------------------------------------ */
+/* the dynamic rect under UI hints (or_hint_dyn_scroll_nal)                   */
+/* ------------------------------------------------------------------------ */
+static const int HD_ZZ[16] = {0, 1, 4, 8, 5, 2, 3, 6, 9, 12, 13, 10, 7, 11, 14, 15};
+
+/* TrailingOnes of a block in scan order (9.2.1: up to 3 +-1 levels from the
+ * last non-zero one down) */
+static int hd_t1(const int *coef, int max)
+{
+    int t1 = 0;
+    for (int i = max - 1; i >= 0 && t1 < 3; --i) {
+        if (!coef[i]) continue;
+        if (coef[i] != 1 && coef[i] != -1) break;
+        t1++;
+    }
+    return t1;
+}
+
+/* a block's piece: TotalCoeff, TrailingOnes and its bits after coeff_token
+ * appended to erb (nC does not change them: coded here at nC 0 / -1) */
+static void hd_piece(or_bits *erb, or_splice_mb *mb, int i, const int *coef, int max)
+{
+    uint8_t tmp[128];
+    or_bits tb;
+    or_bits_init(&tb, tmp, sizeof(tmp));
+    const int nC = max == 4 ? -1 : 0;
+    const int tc = or_cavlc_block(&tb, coef, max, nC);
+    const int t1 = hd_t1(coef, max);
+    uint32_t tv;
+    const int tl = or_ct_code(tc, t1, nC, &tv);
+    mb->tc[i] = (uint8_t)tc;
+    mb->t1[i] = (uint8_t)t1;
+    mb->boff[i] = (uint32_t)erb->nbits;
+    mb->blen[i] = (uint32_t)(tb.nbits - (size_t)tl);
+    for (size_t p = (size_t)tl; p < tb.nbits;) {              /* copy the body bits */
+        const int k = tb.nbits - p > 16 ? 16 : (int)(tb.nbits - p);
+        uint32_t v = 0;
+        for (int j = 0; j < k; ++j) v = v << 1 | ((tmp[(p + j) >> 3] >> (7 - ((p + j) & 7))) & 1u);
+        or_put(erb, v, k);
+        p += (size_t)k;
+    }
+}
+
+/* the prediction sample of reference ref at (x, y) of plane 0 (luma,
+ * full-pel displacement in pixels) or 1 / 2 (chroma, 1/8-pel 2-D bilinear,
+ * 8.4.2.2.2), displacement (mvx, mvy) in luma pixels */
+static int hd_pred(const or_cfg *c, const or_refs *R, int ref, int plane, int x, int y, int mvx, int mvy)
+{
+    if (plane == 0) return or_ref_sample(c, R, ref, 0, x + mvx, y + mvy);
+    const int qx = 4 * mvx, qy = 4 * mvy, fx = qx & 7, fy = qy & 7;
+    const int xi = x + (qx >> 3), yi = y + (qy >> 3);
+    const int A = or_ref_sample(c, R, ref, plane, xi, yi), B = or_ref_sample(c, R, ref, plane, xi + 1, yi);
+    const int C = or_ref_sample(c, R, ref, plane, xi, yi + 1), D = or_ref_sample(c, R, ref, plane, xi + 1, yi + 1);
+    return ((8 - fx) * (8 - fy) * A + fx * (8 - fy) * B + (8 - fx) * fy * C + fx * fy * D + 32) >> 6;
+}
+
+/* the record of dynamic MB (x, y) at motion (ref, mvx, mvy) px */
+static void hd_mb(const or_cfg *c, const or_refs *R, const or_dyn_rect *rc, const uint8_t *src, int x,
+                  int y, int ref, int mvx, int mvy, or_splice_mb *mb, or_bits *erb)
+{
+    const int lw = 16 * rc->w, cw = 8 * rc->w;
+    const uint8_t *sy = src, *su = src + (size_t)lw * 16 * rc->h, *sv = su + (size_t)cw * 8 * rc->h;
+    const int lx0 = 16 * (x - rc->x0), ly0 = 16 * (y - rc->y0);
+    int luma[16][16], cdc[2][4], cac[2][4][15];
+    for (int r = 0; r < 16; ++r) {
+        const int bx = 4 * (r % 4), by = 4 * (r / 4);
+        int res[16], W[16];
+        for (int i = 0; i < 4; ++i)
+            for (int j = 0; j < 4; ++j)
+                res[4 * i + j] = sy[(size_t)(ly0 + by + i) * lw + lx0 + bx + j] -
+                                 hd_pred(c, R, ref, 0, 16 * x + bx + j, 16 * y + by + i, mvx, mvy);
+        or_fwd4x4(res, W);
+        for (int k = 0; k < 16; ++k) luma[r][k] = or_quant(W[HD_ZZ[k]], 26, HD_ZZ[k], 0);
+    }
+    const int cx0 = 8 * (x - rc->x0), cy0 = 8 * (y - rc->y0);
+    for (int p = 0; p < 2; ++p) {
+        const uint8_t *spl = p ? sv : su;
+        int dc[4];
+        for (int k = 0; k < 4; ++k) {
+            const int bx = 4 * (k % 2), by = 4 * (k / 2);
+            int res[16], W[16];
+            for (int i = 0; i < 4; ++i)
+                for (int j = 0; j < 4; ++j)
+                    res[4 * i + j] = spl[(size_t)(cy0 + by + i) * cw + cx0 + bx + j] -
+                                     hd_pred(c, R, ref, 1 + p, 8 * x + bx + j, 8 * y + by + i, mvx, mvy);
+            or_fwd4x4(res, W);
+            dc[k] = W[0];
+            for (int i = 1; i < 16; ++i) cac[p][k][i - 1] = or_quant(W[HD_ZZ[i]], 26, HD_ZZ[i], 0);
+        }
+        cdc[p][0] = or_quant(dc[0] + dc[1] + dc[2] + dc[3], 26, 0, 1);
+        cdc[p][1] = or_quant(dc[0] - dc[1] + dc[2] - dc[3], 26, 0, 1);
+        cdc[p][2] = or_quant(dc[0] + dc[1] - dc[2] - dc[3], 26, 0, 1);
+        cdc[p][3] = or_quant(dc[0] - dc[1] - dc[2] + dc[3], 26, 0, 1);
+    }
+    memset(mb, 0, sizeof(*mb));
+    mb->ref = ref;
+    mb->mx = 4 * mvx;
+    mb->my = 4 * mvy;
+    mb->qp = 26;
+    int cbp_l = 0, dcn = 0, acn = 0;
+    for (int r = 0; r < 16; ++r) {
+        hd_piece(erb, mb, r, luma[r], 16);
+        if (mb->tc[r]) cbp_l |= 1 << (2 * (r / 8) + (r % 4) / 2);
+    }
+    for (int p = 0; p < 2; ++p) {
+        hd_piece(erb, mb, 16 + p, cdc[p], 4);
+        dcn += mb->tc[16 + p];
+        for (int k = 0; k < 4; ++k) {
+            hd_piece(erb, mb, 18 + 4 * p + k, cac[p][k], 15);
+            acn += mb->tc[18 + 4 * p + k];
+        }
+    }
+    mb->cbp = cbp_l | (acn ? 2 : (dcn ? 1 : 0)) << 4;
+}
+
+size_t or_hint_dyn_scroll_nal(uint8_t *dst, size_t cap, or_cfg *c, int off, const or_hint_rect *r,
+                              int n, int mode, const or_dyn_rect *rc, const uint8_t *src, const or_refs *R,
+                              int *err)
+{
+    *err = 0;
+    const int mbw = c->w / 16, mbh = c->h / 16;
+    if (!rc || rc->w <= 0 || rc->h <= 0)
+        return sp_compose(dst, cap, c, off, r, n, mode, 0, 0, 0, 0, NULL, NULL, 0, err);
+    if (rc->x0 < 0 || rc->y0 < 0 || rc->x0 + rc->w > mbw || rc->y0 + rc->h > mbh) {
+        *err = OR_SPLICE_ERR_HEADER;
+        return 0;
+    }
+    int a_end, ra, mva, rb, mvb;
+    or_scroll_regions(c, off, &a_end, &ra, &mva, &rb, &mvb);
+    const size_t nmb = (size_t)rc->w * rc->h, ecap = nmb * OR_SPLICE_PIECES * 64 + 64;
+    or_splice_mb *mbs = (or_splice_mb *)malloc(sizeof(*mbs) * nmb);
+    uint8_t *erb = (uint8_t *)calloc(ecap, 1);
+    or_bits eb;
+    or_bits_init(&eb, erb, ecap);
+    for (int y = rc->y0; y < rc->y0 + rc->h; ++y)
+        for (int x = rc->x0; x < rc->x0 + rc->w; ++x) {
+            int ref, mvx, mvy;
+            or_hint_motion(r, n, x, y, a_end, ra, mva, rb, mvb, &ref, &mvx, &mvy);
+            or_splice_mb *mb = &mbs[(size_t)(y - rc->y0) * rc->w + (x - rc->x0)];
+            if (!or_ref_valid(c, ref)) {            /* an invalid hint reference: no residual */
+                memset(mb, 0, sizeof(*mb));
+                mb->ref = ref;
+                mb->mx = 4 * mvx;
+                mb->my = 4 * mvy;
+                continue;
+            }
+            hd_mb(c, R, rc, src, x, y, ref, mvx, mvy, mb, &eb);
+        }
+    const size_t nb = sp_compose(dst, cap, c, off, r, n, mode, rc->x0, rc->y0, rc->w, rc->h, mbs, erb,
+                                 or_bytes(&eb), err);
+    free(mbs);
+    free(erb);
+    return nb;
+}
+
+size_t or_compose_hint_dyn(uint8_t *dst, size_t cap, or_cfg *c, int off, int compose_mode,
+                           const or_hint_rect *r, int n, int mode, const or_dyn_rect *rc,
+                           const uint8_t *src, const or_refs *R, int *err)
+{
+    *err = 0;
+    size_t nb = 0;
+    if (or_needs_waypoint(c, off)) {                              /* src/composer.c:255-264 */
+        nb += or_waypoint_nal(dst, cap, c, off);
+        if (compose_mode == 1) return nb;
+    }
+    const size_t k = or_hint_dyn_scroll_nal(dst + nb, cap - nb, c, off, r, n, mode, rc, src, R, err);
     return k ? nb + k : 0;
 }
 

@@ -47,6 +47,7 @@
 #include <stdint.h>
 
 #include "hint_oracle.h"
+#include "dyn_oracle.h"
 
 #ifdef __cplusplus
 extern "C" {
@@ -94,6 +95,29 @@ size_t or_splice_scroll_nal(uint8_t *dst, size_t cap, or_cfg *c, int off, const 
 /* composer_write_scroll_frame (src/composer.c:255-264) with that scroll NAL */
 size_t or_compose_splice(uint8_t *dst, size_t cap, or_cfg *c, int off, int compose_mode,
                          const or_hint_rect *r, int n, int mode, const or_splice *sp, int *err);
+
+/* ---- the dynamic rect under UI hints (docs/MASTER_DESIGN.md:58-64,
+ * 109-113, 121-146: one per-frame hint record holds the motion regions AND
+ * the dynamic rect; no reference implementation, this DEFINES the bits) ----
+ * The frame's MV field is the UI-hint field (hint_oracle.h); the MBs of the
+ * dynamic rect rc (its position may change from frame to frame and stream to
+ * stream) keep their (ref, mv) from that field and carry the residual of the
+ * rect source src (dyn_oracle.h layout for rc) minus the prediction at that
+ * motion: full-pel luma, 1/8-pel 2-D bilinear chroma (8.4.2.2.2), samples
+ * clamped to the picture, waypoints resolved through their own rows
+ * (or_ref_sample); 4x4 transform + quant at QP 26 and CAVLC as in
+ * dyn_oracle.h.  The MBs are then composed exactly like spliced MBs
+ * (or_splice_scroll_nal): mb_skip_run / ref_idx / mvd for the frame's hint
+ * mode (an MB without residual can be a P_Skip in OR_HINT_PSKIP), cbp,
+ * mb_qp_delta 0, coeff_token for the composed nC.  rc NULL or empty: the
+ * hint NAL.  Returns the Annex-B bytes, or 0 with *err (OR_SPLICE_ERR_REF:
+ * a rect MB's hint reference is not valid in the frame). */
+size_t or_hint_dyn_scroll_nal(uint8_t *dst, size_t cap, or_cfg *c, int off, const or_hint_rect *r,
+                              int n, int mode, const or_dyn_rect *rc, const uint8_t *src,
+                              const or_refs *R, int *err);
+size_t or_compose_hint_dyn(uint8_t *dst, size_t cap, or_cfg *c, int off, int compose_mode,
+                           const or_hint_rect *r, int n, int mode, const or_dyn_rect *rc,
+                           const uint8_t *src, const or_refs *R, int *err);
 
 /* ---- test-input generator: a stand-in "dynamic encoder" (MASTER_DESIGN
  * §4.2) writing standard CAVLC P slices of a w x h MB picture with random

@@ -1683,13 +1683,6 @@ __device__ inline uint32_t rs_word(uint32_t P, int ng, uint32_t T, const uint32_
     return stitch_word(P, gg, ng, T, goff, gb, gw, fr);
 }
 
-/* RBSP byte i */
-__device__ inline uint32_t rs_byte(uint32_t i, int ng, uint32_t T, const uint32_t *goff, const uint32_t *gb,
-                                   const uint32_t *gw, const uint32_t *fr)
-{
-    return (rs_word(8u * (i & ~3u), ng, T, goff, gb, gw, fr) >> (8u * (3u - (i & 3u)))) & 255u;
-}
-
 /* w[i] for i in 0..8 without indexing (three levels of selects) */
 __device__ inline uint32_t pick9(const uint32_t w[9], uint32_t i)
 {

@@ -23,6 +23,7 @@
 #include "dyn_engine.h"
 #include "hint_engine.h"
 #include "splice_engine.h"
+#include "hdyn_engine.h"
 #include "ingest_engine.h"
 #include "ipcm_engine.h"
 #include "engine.h"
@@ -927,6 +928,14 @@ struct ScrollBatch {
         size_t n = 0;
     };
     std::vector<SpliceHost> h_sp;      /* [s * max_frames + f]; w = 0: none */
+    /* the dynamic rect under UI hints (hdyn_kernels.hip): with both on,
+     * every frame's rect MBs are coded by k_hdyn_code into splice records
+     * (d_sp_rec, word pool d_sp_rbsp) and composed by k_splice_stage */
+    std::vector<int32_t> h_dyn_pos;    /* [2 (s * max_frames + f)]: rect origin, x0 < 0: none */
+    int dyn_pos_custom = 0;            /* some frame's origin differs from the batch rect */
+    int hd_dirty = 0;                  /* d_spf / HintFrame of the combined frames out of date */
+    uint32_t hd_mb_words = 0;          /* pool words per rect MB */
+    size_t dyn_cap = 0;                /* the dynamic rect's own staging cap (geo.slot_bytes without hints) */
     int sp_n = 0;                      /* spliced frames                           */
     int sp_dirty = 0;                  /* upload + parse before the next compose   */
     int sp_parse = 0;                  /* k_splice_parse pending                   */
@@ -1283,7 +1292,15 @@ static int launch(ScrollBatch *b, int nframes, int plan_mode, int nal_max, hipSt
                 set_err("k_hint_stage launch: %s", hipGetErrorString(hipGetLastError()));
                 return SCROLL_ERR_HIP;
             }
-            if (b->sp_n > 0 &&
+            const bool combined = b->dyn_on;
+            if (combined &&
+                hdyn_launch_code(hs, nframes, S, b->d_st, b->d_nal, b->ld_nal, b->d_pend, b->d_dfr, ld_fr,
+                                 b->d_hf, b->d_pool, b->d_spf, &b->geo, b->d_src, b->d_refs,
+                                 b->d_sp_rec, b->d_sp_rbsp, b->hd_mb_words)) {
+                set_err("k_hdyn_code launch: %s", hipGetErrorString(hipGetLastError()));
+                return SCROLL_ERR_HIP;
+            }
+            if ((b->sp_n > 0 || combined) &&
                 splice_launch_stage(hs, nframes, S, b->d_st, b->d_nal, b->ld_nal, b->d_pend,
                                     b->d_dfr, ld_fr, b->d_hf, b->d_pool, b->d_spf, b->d_sp_rec,
                                     b->d_sp_rbsp, b->d_stage, b->geo.slot_bytes)) {
@@ -1391,6 +1408,7 @@ static int launch(ScrollBatch *b, int nframes, int plan_mode, int nal_max, hipSt
 
 static int hint_upload(ScrollBatch *b);
 static int splice_upload(ScrollBatch *b);
+static int hd_upload(ScrollBatch *b);
 static int splice_frame_status(ScrollBatch *b, size_t i, int *status);
 static const char *splice_msg(int e);
 
@@ -1410,8 +1428,19 @@ int scroll_batch_compose_ex(ScrollBatch *b, int nframes, void *hip_stream, int f
         return SCROLL_ERR_CONFIG;
     }
     HIPCHK(hipSetDevice(b->device));
+    const bool combined = b->hint_on && b->dyn_on;
+    if (b->dyn_pos_custom && !b->hint_on) {
+        set_err("scroll_batch_compose: per-frame dynamic rect positions need UI hints "
+                "(scroll_batch_set_hints)");
+        return SCROLL_ERR_CONFIG;
+    }
     if (b->hint_on && b->sp_dirty) {
         int rc = splice_upload(b);
+        if (rc) return rc;
+        if (combined) b->hd_dirty = 1;
+    }
+    if (combined && b->hd_dirty) {
+        int rc = hd_upload(b);
         if (rc) return rc;
     }
     if (b->hint_on && b->hint_dirty) {
@@ -1445,8 +1474,16 @@ int scroll_batch_sync(ScrollBatch *b)
             int st = 0, ff = 0;
             for (; ff < b->max_frames && !st; ++ff)
                 if (splice_frame_status(b, (size_t)s * b->max_frames + ff, &st)) break;
-            set_err("stream %d frame %d: spliced slice: %s", s, ff - 1, splice_msg(st));
-            rc = SCROLL_ERR_CONFIG;
+            if (st == HDYN_STATUS_OVERFLOW) {
+                set_err("stream %d frame %d: a dynamic-rect MB under hints outgrew its %u-byte "
+                        "region (raise slot_bytes of scroll_batch_set_dyn_rect)", s, ff - 1,
+                        4u * b->hd_mb_words);
+                rc = SCROLL_ERR_OVERFLOW;
+            } else {
+                set_err("stream %d frame %d: %s: %s", s, ff - 1,
+                        b->dyn_on ? "dynamic rect under hints" : "spliced slice", splice_msg(st));
+                rc = SCROLL_ERR_CONFIG;
+            }
         } else if (rc == SCROLL_OK && (b->h_st[s].err & SCROLL_DEVERR_HINT)) {
             set_err("stream %d: a hint rect names a reference that is not valid in its frame "
                     "(ref 2 + i needs waypoint i)", s);
@@ -1603,10 +1640,14 @@ long long scroll_batch_last_nals(ScrollBatch *b)
 /* ------------------------------ dynamic rect ----------------------------- */
 static void dyn_release(ScrollBatch *b)
 {
-    (void)hipFree(b->d_dfr);
+    if (!b->hint_on) {                 /* else they are the hint path's */
+        (void)hipFree(b->d_dfr);
+        (void)hipFree(b->d_stage);
+        b->d_dfr = nullptr;
+        b->d_stage = nullptr;
+    }
     (void)hipFree(b->d_src);
     (void)hipFree(b->d_refs);
-    (void)hipFree(b->d_stage);
     (void)hipFree(b->dx.rows);
     (void)hipFree(b->dx.meta);
     (void)hipFree(b->dx.body_lo);
@@ -1614,12 +1655,21 @@ static void dyn_release(ScrollBatch *b)
     (void)hipFree(b->dx.tcx);
     (void)hipFree(b->dx.rowstage);
     (void)hipFree(b->dx.gbits);
-    b->d_dfr = nullptr;
-    b->d_src = b->d_refs = b->d_stage = nullptr;
+    b->d_src = b->d_refs = nullptr;
     b->dx = DynScratch{};
     b->dyn_on = 0;
     b->dyn_refs = 0;
+    b->h_dyn_pos.clear();
+    b->dyn_pos_custom = 0;
+    if (b->hint_on) {                  /* the combined frames become plain hint frames */
+        b->geo.x0 = b->geo.y0 = b->geo.w = b->geo.h = 0;
+        b->sp_dirty = 1;                   /* d_spf back to the (no) splices */
+        b->hint_dirty = 1;
+    }
 }
+
+static int hd_setup(ScrollBatch *b);
+static int sp_grow(void **p, size_t *cap, size_t n, size_t size);
 
 static size_t round256(size_t n) { return (n + 255) & ~(size_t)255; }
 
@@ -1631,9 +1681,8 @@ static size_t dyn_pair_bytes(const ScrollBatch *b)
 int scroll_batch_set_dyn_rect(ScrollBatch *b, int x0, int y0, int w, int h, size_t slot_bytes)
 {
     if (!b || x0 < 0 || y0 < 0 || w < 0 || h < 0) return SCROLL_ERR_ARG;
-    if (b->hint_on) {                  /* the staging buffers belong to the hints */
-        if (w == 0 || h == 0) return SCROLL_OK;
-        set_err("scroll_batch_set_dyn_rect: not combinable with UI hints (clear them first)");
+    if (b->hint_on && b->sp_n > 0 && w > 0 && h > 0) {
+        set_err("scroll_batch_set_dyn_rect: not combinable with spliced slices (clear them first)");
         return SCROLL_ERR_CONFIG;
     }
     int rc = batch_host_sync(b);
@@ -1678,12 +1727,16 @@ int scroll_batch_set_dyn_rect(ScrollBatch *b, int x0, int y0, int w, int h, size
     b->dyn_pw = pw;
     b->dyn_ph = ph;
     const size_t S = (size_t)b->max_streams, F = (size_t)b->max_frames;
-    hipError_t e = hipMalloc(&b->d_dfr, S * F * sizeof(DynFrame));
+    hipError_t e = hipSuccess;
+    if (!b->hint_on) {                 /* with hints: the hint path's DynFrames and slots */
+        e = hipMalloc(&b->d_dfr, S * F * sizeof(DynFrame));
+        /* the RBSP is never staged (k_dyn_epfix / k_dyn_emit_gather read the
+         * row groups): per frame only its EP list; slot_bytes stays the cap */
+        if (e == hipSuccess) e = hipMalloc(&b->d_stage, S * F * DYN_OVF_BYTES);
+        if (e == hipSuccess) e = hipMemset(b->d_dfr, 0, S * F * sizeof(DynFrame));
+    }
     if (e == hipSuccess) e = hipMalloc(&b->d_src, S * g.src_ld);
     if (e == hipSuccess) e = hipMalloc(&b->d_refs, S * dyn_pair_bytes(b));
-    /* the RBSP is never staged (k_dyn_epscan / k_dyn_emit_gather read the
-     * row groups): per frame only its EP list; slot_bytes stays the cap */
-    if (e == hipSuccess) e = hipMalloc(&b->d_stage, S * F * DYN_OVF_BYTES);
     if (e == hipSuccess) e = hipMalloc(&b->dx.rows, S * F * 32 * h * sizeof(uint32_t));
     if (e == hipSuccess) e = hipMalloc(&b->dx.meta, S * F * DYN_PIECES * w * h * sizeof(uint16_t));
     if (e == hipSuccess) e = hipMalloc(&b->dx.body_lo, S * F * DYN_PIECES * w * h * sizeof(uint2));
@@ -1694,7 +1747,6 @@ int scroll_batch_set_dyn_rect(ScrollBatch *b, int x0, int y0, int w, int h, size
     if (e == hipSuccess) e = hipMalloc(&b->dx.rowstage, S * F * g.rs_frame_words * sizeof(uint32_t));
     if (e == hipSuccess) e = hipMalloc(&b->dx.gbits, S * F * ng * sizeof(uint32_t));
     b->dx.epoch = 0;
-    if (e == hipSuccess) e = hipMemset(b->d_dfr, 0, S * F * sizeof(DynFrame));
     if (e == hipSuccess) e = hipMemset(b->d_src, 0, S * g.src_ld);
     if (e == hipSuccess) e = hipMemset(b->d_refs, 0, S * dyn_pair_bytes(b));
     if (e != hipSuccess) {
@@ -1702,8 +1754,43 @@ int scroll_batch_set_dyn_rect(ScrollBatch *b, int x0, int y0, int w, int h, size
         dyn_release(b);
         return e == hipErrorOutOfMemory ? SCROLL_ERR_OOM : SCROLL_ERR_HIP;
     }
+    b->dyn_cap = g.slot_bytes;
+    if (b->hint_on) g.slot_bytes = b->geo.slot_bytes;   /* the hint path's slots (grown by hd_setup) */
     b->geo = g;
     b->dyn_on = 1;
+    b->h_dyn_pos.assign(2 * S * F, 0);
+    for (size_t i = 0; i < S * F; ++i) {
+        b->h_dyn_pos[2 * i] = x0;
+        b->h_dyn_pos[2 * i + 1] = y0;
+    }
+    b->dyn_pos_custom = 0;
+    b->hd_mb_words = slot_bytes == 0 ? HDYN_MB_WORDS_DEFAULT
+                                     : (uint32_t)std::min<size_t>(HDYN_MB_WORDS_MAX,
+                                                                  std::max<size_t>(HDYN_MB_WORDS_MIN,
+                                                                                   slot_bytes / (4 * (size_t)w * h)));
+    if (b->hint_on) return hd_setup(b);
+    return SCROLL_OK;
+}
+
+int scroll_batch_set_dyn_rect_at(ScrollBatch *b, int s, int f, int x0, int y0)
+{
+    if (!b || !b->dyn_on || s < 0 || s >= b->nstreams || f < 0 || f >= b->max_frames) {
+        set_err("scroll_batch_set_dyn_rect_at: no dynamic rect, or stream / frame out of range");
+        return SCROLL_ERR_ARG;
+    }
+    const int mbw = b->dyn_pw / 16, mbh = b->dyn_ph / 16;
+    if (x0 >= 0 && (y0 < 0 || x0 + b->geo.w > mbw || y0 + b->geo.h > mbh)) {
+        set_err("scroll_batch_set_dyn_rect_at: rect at (%d, %d) leaves the picture", x0, y0);
+        return SCROLL_ERR_ARG;
+    }
+    int rc = batch_host_sync(b);
+    if (rc) return rc;
+    const size_t i = (size_t)s * b->max_frames + f;
+    b->h_dyn_pos[2 * i] = x0 < 0 ? -1 : x0;
+    b->h_dyn_pos[2 * i + 1] = x0 < 0 ? -1 : y0;
+    if (x0 != b->geo.x0 || (x0 >= 0 && y0 != b->geo.y0)) b->dyn_pos_custom = 1;
+    b->hd_dirty = 1;
+    b->hint_dirty = 1;
     return SCROLL_OK;
 }
 
@@ -1846,6 +1933,8 @@ static int hint_upload(ScrollBatch *b)
         hf[i].n = (int16_t)b->h_hint[i].size();
         hf[i].mode = b->h_hint_mode[i];
         if (i < b->h_sp.size() && b->h_sp[i].w > 0) hf[i].mode |= HINT_MODE_SPLICED;
+        if (b->dyn_on && 2 * i < b->h_dyn_pos.size() && b->h_dyn_pos[2 * i] >= 0)
+            hf[i].mode |= HINT_MODE_SPLICED;   /* the rect's MBs: k_hdyn_code's records */
         pool.insert(pool.end(), b->h_hint[i].begin(), b->h_hint[i].end());
     }
     if (pool.size() > b->pool_cap) {
@@ -1864,6 +1953,63 @@ static int hint_upload(ScrollBatch *b)
         HIPCHK(hipMemcpy(b->d_pool, pool.data(), pool.size() * sizeof(ScrollHintRect),
                          hipMemcpyHostToDevice));
     b->hint_dirty = 0;
+    return SCROLL_OK;
+}
+
+/* the dynamic rect under hints: record / word pools for every frame's rect
+ * MBs, staging slots grown to the largest NAL such a frame composes */
+static int hd_setup(ScrollBatch *b)
+{
+    const size_t S = (size_t)b->max_streams, F = (size_t)b->max_frames;
+    const size_t nmb = (size_t)b->geo.w * b->geo.h;
+    const size_t words = S * F * nmb * b->hd_mb_words + 2;   /* + bits_at's look-ahead */
+    int rc;
+    if (!b->d_spf) {
+        HIPCHK(hipMalloc(&b->d_spf, S * F * sizeof(SpliceFrame)));
+        HIPCHK(hipMemset(b->d_spf, 0, S * F * sizeof(SpliceFrame)));
+    }
+    if ((rc = sp_grow((void **)&b->d_sp_rbsp, &b->sp_rbsp_cap, words, sizeof(uint32_t))) ||
+        (rc = sp_grow((void **)&b->d_sp_rec, &b->sp_rec_cap, S * F * nmb, sizeof(SpliceMbRec))))
+        return rc;
+    const size_t slot = splice_slot_bound(b->dyn_pw / 16, b->dyn_ph / 16, b->geo.w, b->geo.h,
+                                          nmb * 4 * b->hd_mb_words);
+    if (slot > b->geo.slot_bytes) {
+        void *ns = nullptr;
+        hipError_t e = hipMalloc(&ns, S * F * slot);
+        if (e != hipSuccess) {
+            (void)hipGetLastError();
+            set_err("dynamic rect under hints: staging (%zu bytes per frame): %s", slot,
+                    hipGetErrorString(e));
+            return e == hipErrorOutOfMemory ? SCROLL_ERR_OOM : SCROLL_ERR_HIP;
+        }
+        (void)hipFree(b->d_stage);
+        b->d_stage = (uint8_t *)ns;
+        b->geo.slot_bytes = slot;
+    }
+    b->hd_dirty = 1;
+    b->hint_dirty = 1;
+    return SCROLL_OK;
+}
+
+/* every frame's rect position -> d_spf (records and words at fixed places) */
+static int hd_upload(ScrollBatch *b)
+{
+    const size_t S = (size_t)b->max_streams, F = (size_t)b->max_frames;
+    const size_t nmb = (size_t)b->geo.w * b->geo.h;
+    std::vector<SpliceFrame> spf(S * F);
+    for (size_t i = 0; i < S * F; ++i) {
+        SpliceFrame &o = spf[i];
+        o = SpliceFrame{};
+        if (b->h_dyn_pos[2 * i] < 0) continue;
+        o.x0 = b->h_dyn_pos[2 * i];
+        o.y0 = b->h_dyn_pos[2 * i + 1];
+        o.w = b->geo.w;
+        o.h = b->geo.h;
+        o.rbsp_word = i * nmb * b->hd_mb_words;
+        o.rec_first = (uint32_t)(i * nmb);
+    }
+    HIPCHK(hipMemcpy(b->d_spf, spf.data(), S * F * sizeof(SpliceFrame), hipMemcpyHostToDevice));
+    b->hd_dirty = 0;
     return SCROLL_OK;
 }
 
@@ -1886,10 +2032,6 @@ int scroll_batch_set_hints(ScrollBatch *b, int s, int f, const ScrollHintRect *r
             return SCROLL_ERR_ARG;
         }
     }
-    if (b->dyn_on) {
-        set_err("scroll_batch_set_hints: not combinable with a dynamic rect");
-        return SCROLL_ERR_CONFIG;
-    }
     int rc = batch_host_sync(b);
     if (rc) return rc;
     HIPCHK(hipSetDevice(b->device));
@@ -1904,21 +2046,41 @@ int scroll_batch_set_hints(ScrollBatch *b, int s, int f, const ScrollHintRect *r
         }
         const size_t slot = hint_slot_bound(1, mb);     /* slots from the MB count only */
         const size_t S = (size_t)b->max_streams, F = (size_t)b->max_frames;
-        hipError_t e = hipMalloc(&b->d_dfr, S * F * sizeof(DynFrame));
-        if (e == hipSuccess) e = hipMalloc(&b->d_stage, S * F * slot);
-        if (e == hipSuccess) e = hipMalloc(&b->d_hf, S * F * sizeof(HintFrame));
-        if (e == hipSuccess) e = hipMemset(b->d_dfr, 0, S * F * sizeof(DynFrame));
-        if (e != hipSuccess) {
-            set_err("scroll_batch_set_hints: %s", hipGetErrorString(e));
-            hint_release(b);
-            return e == hipErrorOutOfMemory ? SCROLL_ERR_OOM : SCROLL_ERR_HIP;
+        hipError_t e = hipSuccess;
+        if (b->dyn_on) {
+            /* the dynamic rect's DynFrames stay; its EP-list buffer becomes
+             * the hint path's staging slots (hd_setup grows them for the rect) */
+            void *ns = nullptr;
+            e = hipMalloc(&ns, S * F * slot);
+            if (e == hipSuccess) e = hipMalloc(&b->d_hf, S * F * sizeof(HintFrame));
+            if (e != hipSuccess) {
+                (void)hipFree(ns);
+                (void)hipFree(b->d_hf);
+                b->d_hf = nullptr;
+                (void)hipGetLastError();
+                set_err("scroll_batch_set_hints: %s", hipGetErrorString(e));
+                return e == hipErrorOutOfMemory ? SCROLL_ERR_OOM : SCROLL_ERR_HIP;
+            }
+            (void)hipFree(b->d_stage);
+            b->d_stage = (uint8_t *)ns;
+        } else {
+            e = hipMalloc(&b->d_dfr, S * F * sizeof(DynFrame));
+            if (e == hipSuccess) e = hipMalloc(&b->d_stage, S * F * slot);
+            if (e == hipSuccess) e = hipMalloc(&b->d_hf, S * F * sizeof(HintFrame));
+            if (e == hipSuccess) e = hipMemset(b->d_dfr, 0, S * F * sizeof(DynFrame));
+            if (e != hipSuccess) {
+                set_err("scroll_batch_set_hints: %s", hipGetErrorString(e));
+                hint_release(b);
+                return e == hipErrorOutOfMemory ? SCROLL_ERR_OOM : SCROLL_ERR_HIP;
+            }
+            b->geo = DynGeom{};
         }
-        b->geo = DynGeom{};
         b->geo.slot_bytes = slot;
         b->hint_max_mb = mb;
         b->h_hint.assign(S * F, {});
         b->h_hint_mode.assign(S * F, (int16_t)SCROLL_HINT_EXACT);
         b->hint_on = 1;
+        if (b->dyn_on && (rc = hd_setup(b))) return rc;
     }
     const size_t i = (size_t)s * b->max_frames + f;
     b->h_hint[i].assign(rects, rects + n);
@@ -1935,6 +2097,25 @@ int scroll_batch_clear_hints(ScrollBatch *b)
     if (rc) return rc;
     HIPCHK(hipSetDevice(b->device));
     hint_release(b);
+    if (b->dyn_on) {                   /* the dynamic rect alone again: its DynFrames + EP lists */
+        const size_t S = (size_t)b->max_streams, F = (size_t)b->max_frames;
+        hipError_t e = hipMalloc(&b->d_dfr, S * F * sizeof(DynFrame));
+        if (e == hipSuccess) e = hipMalloc(&b->d_stage, S * F * DYN_OVF_BYTES);
+        if (e == hipSuccess) e = hipMemset(b->d_dfr, 0, S * F * sizeof(DynFrame));
+        if (e != hipSuccess) {
+            set_err("scroll_batch_clear_hints: %s", hipGetErrorString(e));
+            dyn_release(b);
+            return e == hipErrorOutOfMemory ? SCROLL_ERR_OOM : SCROLL_ERR_HIP;
+        }
+        b->geo.slot_bytes = b->dyn_cap;
+        if (b->dyn_pos_custom) {
+            for (size_t i = 0; i < S * F; ++i) {
+                b->h_dyn_pos[2 * i] = b->geo.x0;
+                b->h_dyn_pos[2 * i + 1] = b->geo.y0;
+            }
+            b->dyn_pos_custom = 0;
+        }
+    }
     return SCROLL_OK;
 }
 
@@ -2042,7 +2223,7 @@ int scroll_batch_set_splice(ScrollBatch *b, int s, int f, int x0, int y0, int w,
         return SCROLL_ERR_ARG;
     }
     if (b->dyn_on) {
-        set_err("scroll_batch_set_splice: not combinable with a dynamic rect");
+        set_err("scroll_batch_set_splice: not combinable with a dynamic rect (one spliced rect per frame)");
         return SCROLL_ERR_CONFIG;
     }
     if (n == 0 && !b->hint_on) return SCROLL_OK;
@@ -2093,7 +2274,7 @@ int scroll_batch_set_splices_device(ScrollBatch *b, int n, const ScrollSpliceDes
     }
     if (n == 0) return SCROLL_OK;
     if (b->dyn_on) {
-        set_err("scroll_batch_set_splices_device: not combinable with a dynamic rect");
+        set_err("scroll_batch_set_splices_device: not combinable with a dynamic rect (one spliced rect per frame)");
         return SCROLL_ERR_CONFIG;
     }
     if (!b->hint_on) {
@@ -2138,7 +2319,9 @@ int scroll_batch_clear_splices(ScrollBatch *b)
 static int splice_frame_status(ScrollBatch *b, size_t i, int *status)
 {
     *status = SCROLL_SPLICE_OK;
-    if (!b->d_spf || i >= b->h_sp.size() || b->h_sp[i].w <= 0) return SCROLL_OK;
+    const bool on = (i < b->h_sp.size() && b->h_sp[i].w > 0) ||
+                    (b->hint_on && b->dyn_on && 2 * i < b->h_dyn_pos.size() && b->h_dyn_pos[2 * i] >= 0);
+    if (!b->d_spf || !on) return SCROLL_OK;
     SpliceFrame sf;
     HIPCHK(hipMemcpy(&sf, b->d_spf + i, sizeof(sf), hipMemcpyDeviceToHost));
     *status = sf.status ? sf.status : sf.stage_status;

@@ -170,6 +170,7 @@ def _load():
                                       [ctypes.c_size_t]),
         "scroll_batch_set_dyn_refs": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, u8p, u8p]),
         "scroll_batch_set_dyn_source": (ctypes.c_int, [ctypes.c_void_p, u8p, ctypes.c_int]),
+        "scroll_batch_set_dyn_rect_at": (ctypes.c_int, [ctypes.c_void_p] + [ctypes.c_int] * 4),
         "scroll_batch_dyn_source_device": (ctypes.c_void_p, [ctypes.c_void_p, P(ctypes.c_size_t),
                                                              P(ctypes.c_size_t)]),
         "scroll_batch_dyn_source_synth": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int,
@@ -507,6 +508,12 @@ class Batch:
         """ref_a / ref_b: I420 bytes (w*h*3/2) of reference pictures A and B"""
         self._chk(lib.scroll_batch_set_dyn_refs(self.h, stream, u8buf(bytes(ref_a)),
                                                 u8buf(bytes(ref_b))), "set_dyn_refs")
+
+    def set_dyn_rect_at(self, s, f, x0, y0):
+        """Frame f of stream s puts the dynamic rect at MB (x0, y0); x0 = -1:
+        no rect in that frame.  Positions other than set_dyn_rect's need UI
+        hints (set_hints) at compose time."""
+        self._chk(lib.scroll_batch_set_dyn_rect_at(self.h, s, f, x0, y0), "set_dyn_rect_at")
 
     def set_dyn_source(self, src, nframes):
         """src: bytes of [num_streams][nframes][384*w*h]"""

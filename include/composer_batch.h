@@ -156,6 +156,19 @@ long long scroll_batch_last_nals(ScrollBatch *b);
 int scroll_batch_set_dyn_rect(ScrollBatch *b, int x0, int y0, int w, int h, size_t slot_bytes);
 int scroll_batch_set_dyn_refs(ScrollBatch *b, int s, const uint8_t *ref_a, const uint8_t *ref_b);
 int scroll_batch_set_dyn_source(ScrollBatch *b, const uint8_t *src, int nframes);
+/* Under UI hints (scroll_batch_set_hints) the rect's MBs keep the hint
+ * field's (ref, mv) -- full-pel luma, 2-D 1/8-pel chroma prediction at that
+ * motion -- and the rect may sit anywhere in each frame:
+ *   scroll_batch_set_dyn_rect_at(b, s, f, x0, y0)   frame f of stream s puts
+ *       the rect's w x h MBs at (x0, y0); x0 = -1: no rect in that frame.
+ *       Positions other than set_dyn_rect's need hints at compose time
+ *       (SCROLL_ERR_CONFIG otherwise); clear_hints resets them.
+ * Each rect MB's residual bits get a region of slot_bytes / (w h) bytes
+ * (64 to 2048; slot_bytes 0: 512, which saturated +-255 residuals stay well
+ * inside); an MB that outgrows it fails the compose with SCROLL_ERR_OVERFLOW.
+ * Bit-exact definition: oracle/splice_oracle.h or_hint_dyn_scroll_nal.
+ * Not combinable with spliced slices (one rect per frame). */
+int scroll_batch_set_dyn_rect_at(ScrollBatch *b, int s, int f, int x0, int y0);
 uint8_t *scroll_batch_dyn_source_device(ScrollBatch *b, size_t *stream_stride,
                                         size_t *frame_stride);
 int scroll_batch_dyn_source_synth(ScrollBatch *b, int nframes, int stream_base, int t0);
@@ -198,7 +211,7 @@ int scroll_batch_kernel_stats_ex(ScrollBatch *b, double ms[6], int *count);
  *       waypoint i) fails that stream's compose with SCROLL_ERR_CONFIG.
  *   scroll_batch_clear_hints(b)   back to plain scroll frames (k_emit path).
  * Pictures up to 240 MBs (3840 px) wide.
- * Not combinable with a dynamic rect (SCROLL_ERR_CONFIG). */
+ * With a dynamic rect: see scroll_batch_set_dyn_rect_at. */
 #define SCROLL_HINT_EXACT 0
 #define SCROLL_HINT_PSKIP 1
 #define SCROLL_HINT_SPEC 2

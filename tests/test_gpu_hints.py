@@ -196,7 +196,7 @@ def test_invalid_reference_fails_only_its_stream(gpu, oracle, scroll):
 
 def test_chunks_clear_and_exclusivity(gpu, oracle, scroll):
     """hints persist across composes (frame f of each compose); clearing them
-    returns to the k_emit path; a dynamic rect is refused while hints are set"""
+    returns to the k_emit path"""
     w, h = 512, 512
     offs = synthetic_offsets(3, 30, h, first_stream=2)
     F1 = 10
@@ -210,8 +210,6 @@ def test_chunks_clear_and_exclusivity(gpu, oracle, scroll):
     for s in range(3):
         for f in range(F1):
             b.set_hints(s, f, *per_f[f])
-    with pytest.raises(RuntimeError):
-        b.set_dyn_rect(1, 1, 2, 2)
     for c0 in (0, 10):
         b.set_offsets(np.ascontiguousarray(offs[:, c0:c0 + F1]))
         b.compose(F1)

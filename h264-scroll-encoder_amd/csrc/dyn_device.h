@@ -328,6 +328,274 @@ __device__ __host__ inline int quant(int w, int pos)
     return mad_i24(w, mf, bias) >> QBITS;
 }
 
+/* ---------------------------------------------------------------------- */
+/* residual -> transform -> quant on packed 16-bit pairs (k_dyn_row)        */
+/* ---------------------------------------------------------------------- */
+/* The same levels as fwd4x4 + quant, in about half the vector instructions:
+ *   - residuals as 16-bit pairs straight from the pixel bytes (SDWA byte
+ *     selects, one asm block for the 16): row i -> P = (r0, r1), Q = (r3, r2);
+ *   - the horizontal butterflies on pairs: S = P + Q = (s03, s12), D = P - Q
+ *     = (d03, d12); (t0, t2) = one v_pk_mad_i16 of S's halves, (t1, t3) two;
+ *   - the vertical butterflies elementwise on the pairs (cols 0/2, cols 1/3);
+ *     every value stays within int16 (|W| <= 9180);
+ *   - quant per coefficient: the bias from the half's sign (v_bfi), one
+ *     v_mad_i32_i16 reading the half (op_sel), the arithmetic shift written
+ *     straight into its byte of the packed levels (SDWA dst_sel) -- in asm
+ *     blocks of two words (8 coefficients interleaved, so no instruction
+ *     reads the one before it).
+ * The transform is plain vector code, so the compiler schedules it around
+ * the packed-math forwarding wait state.  Both halves of a pair share their
+ * MF class (cols 0/2 or 1/3 of one row).  On the host the same dataflow is
+ * emulated (tests/hostsim checks it against fwd4x4 + quant). */
+namespace pk {
+__device__ __host__ inline uint32_t pack2(int lo, int hi) { return (uint32_t)(uint16_t)lo | (uint32_t)(uint16_t)hi << 16; }
+__device__ __host__ inline int half(uint32_t x, int h) { return (int)(int16_t)(uint16_t)(x >> (16 * h)); }
+}  // namespace pk
+
+/* the quant blocks (generated: scan index k2 -> raster ZZ[k2] = 4 r + c ->
+ * Ye[r] / Yo[r] (c even / odd), half c >> 1, MF by (r, c) parity; luma byte
+ * k2, chroma AC byte k2 - 1) */
+#define SCROLL_QLUMA0 \
+    "v_bfe_i32 %[t0], %[ye0], 15, 1\n\t" \
+    "v_bfe_i32 %[t1], %[yo0], 15, 1\n\t" \
+    "v_bfe_i32 %[t2], %[ye1], 15, 1\n\t" \
+    "v_bfe_i32 %[t3], %[ye2], 15, 1\n\t" \
+    "v_bfe_i32 %[t4], %[yo1], 15, 1\n\t" \
+    "v_ashrrev_i32 %[t5], 31, %[ye0]\n\t" \
+    "v_ashrrev_i32 %[t6], 31, %[yo0]\n\t" \
+    "v_ashrrev_i32 %[t7], 31, %[ye1]\n\t" \
+    "v_bfi_b32 %[t0], %[t0], %[k1], %[k0]\n\t" \
+    "v_bfi_b32 %[t1], %[t1], %[k1], %[k0]\n\t" \
+    "v_bfi_b32 %[t2], %[t2], %[k1], %[k0]\n\t" \
+    "v_bfi_b32 %[t3], %[t3], %[k1], %[k0]\n\t" \
+    "v_bfi_b32 %[t4], %[t4], %[k1], %[k0]\n\t" \
+    "v_bfi_b32 %[t5], %[t5], %[k1], %[k0]\n\t" \
+    "v_bfi_b32 %[t6], %[t6], %[k1], %[k0]\n\t" \
+    "v_bfi_b32 %[t7], %[t7], %[k1], %[k0]\n\t" \
+    "v_mad_i32_i16 %[t0], %[ye0], %[mf0], %[t0]\n\t" \
+    "v_mad_i32_i16 %[t1], %[yo0], %[mf2], %[t1]\n\t" \
+    "v_mad_i32_i16 %[t2], %[ye1], %[mf2], %[t2]\n\t" \
+    "v_mad_i32_i16 %[t3], %[ye2], %[mf0], %[t3]\n\t" \
+    "v_mad_i32_i16 %[t4], %[yo1], %[mf1], %[t4]\n\t" \
+    "v_mad_i32_i16 %[t5], %[ye0], %[mf0], %[t5] op_sel:[1,0,0,0]\n\t" \
+    "v_mad_i32_i16 %[t6], %[yo0], %[mf2], %[t6] op_sel:[1,0,0,0]\n\t" \
+    "v_mad_i32_i16 %[t7], %[ye1], %[mf2], %[t7] op_sel:[1,0,0,0]\n\t" \
+    "v_ashrrev_i32_sdwa %[d0], %[sh], %[t0] dst_sel:BYTE_0 dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:DWORD\n\t" \
+    "v_ashrrev_i32_sdwa %[d1], %[sh], %[t4] dst_sel:BYTE_0 dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:DWORD\n\t" \
+    "v_ashrrev_i32_sdwa %[d0], %[sh], %[t1] dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD\n\t" \
+    "v_ashrrev_i32_sdwa %[d1], %[sh], %[t5] dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD\n\t" \
+    "v_ashrrev_i32_sdwa %[d0], %[sh], %[t2] dst_sel:BYTE_2 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD\n\t" \
+    "v_ashrrev_i32_sdwa %[d1], %[sh], %[t6] dst_sel:BYTE_2 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD\n\t" \
+    "v_ashrrev_i32_sdwa %[d0], %[sh], %[t3] dst_sel:BYTE_3 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD\n\t" \
+    "v_ashrrev_i32_sdwa %[d1], %[sh], %[t7] dst_sel:BYTE_3 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD\n\t"
+/* 8 coefficients */
+#define SCROLL_QLUMA1 \
+    "v_bfe_i32 %[t0], %[yo2], 15, 1\n\t" \
+    "v_bfe_i32 %[t1], %[ye3], 15, 1\n\t" \
+    "v_bfe_i32 %[t2], %[yo3], 15, 1\n\t" \
+    "v_ashrrev_i32 %[t3], 31, %[ye2]\n\t" \
+    "v_ashrrev_i32 %[t4], 31, %[yo1]\n\t" \
+    "v_ashrrev_i32 %[t5], 31, %[yo2]\n\t" \
+    "v_ashrrev_i32 %[t6], 31, %[ye3]\n\t" \
+    "v_ashrrev_i32 %[t7], 31, %[yo3]\n\t" \
+    "v_bfi_b32 %[t0], %[t0], %[k1], %[k0]\n\t" \
+    "v_bfi_b32 %[t1], %[t1], %[k1], %[k0]\n\t" \
+    "v_bfi_b32 %[t2], %[t2], %[k1], %[k0]\n\t" \
+    "v_bfi_b32 %[t3], %[t3], %[k1], %[k0]\n\t" \
+    "v_bfi_b32 %[t4], %[t4], %[k1], %[k0]\n\t" \
+    "v_bfi_b32 %[t5], %[t5], %[k1], %[k0]\n\t" \
+    "v_bfi_b32 %[t6], %[t6], %[k1], %[k0]\n\t" \
+    "v_bfi_b32 %[t7], %[t7], %[k1], %[k0]\n\t" \
+    "v_mad_i32_i16 %[t0], %[yo2], %[mf2], %[t0]\n\t" \
+    "v_mad_i32_i16 %[t1], %[ye3], %[mf2], %[t1]\n\t" \
+    "v_mad_i32_i16 %[t2], %[yo3], %[mf1], %[t2]\n\t" \
+    "v_mad_i32_i16 %[t3], %[ye2], %[mf0], %[t3] op_sel:[1,0,0,0]\n\t" \
+    "v_mad_i32_i16 %[t4], %[yo1], %[mf1], %[t4] op_sel:[1,0,0,0]\n\t" \
+    "v_mad_i32_i16 %[t5], %[yo2], %[mf2], %[t5] op_sel:[1,0,0,0]\n\t" \
+    "v_mad_i32_i16 %[t6], %[ye3], %[mf2], %[t6] op_sel:[1,0,0,0]\n\t" \
+    "v_mad_i32_i16 %[t7], %[yo3], %[mf1], %[t7] op_sel:[1,0,0,0]\n\t" \
+    "v_ashrrev_i32_sdwa %[d0], %[sh], %[t0] dst_sel:BYTE_0 dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:DWORD\n\t" \
+    "v_ashrrev_i32_sdwa %[d1], %[sh], %[t4] dst_sel:BYTE_0 dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:DWORD\n\t" \
+    "v_ashrrev_i32_sdwa %[d0], %[sh], %[t1] dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD\n\t" \
+    "v_ashrrev_i32_sdwa %[d1], %[sh], %[t5] dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD\n\t" \
+    "v_ashrrev_i32_sdwa %[d0], %[sh], %[t2] dst_sel:BYTE_2 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD\n\t" \
+    "v_ashrrev_i32_sdwa %[d1], %[sh], %[t6] dst_sel:BYTE_2 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD\n\t" \
+    "v_ashrrev_i32_sdwa %[d0], %[sh], %[t3] dst_sel:BYTE_3 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD\n\t" \
+    "v_ashrrev_i32_sdwa %[d1], %[sh], %[t7] dst_sel:BYTE_3 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD\n\t"
+/* 8 coefficients */
+#define SCROLL_QCHROMA0 \
+    "v_bfe_i32 %[t0], %[yo0], 15, 1\n\t" \
+    "v_bfe_i32 %[t1], %[ye1], 15, 1\n\t" \
+    "v_bfe_i32 %[t2], %[ye2], 15, 1\n\t" \
+    "v_bfe_i32 %[t3], %[yo1], 15, 1\n\t" \
+    "v_ashrrev_i32 %[t4], 31, %[ye0]\n\t" \
+    "v_ashrrev_i32 %[t5], 31, %[yo0]\n\t" \
+    "v_ashrrev_i32 %[t6], 31, %[ye1]\n\t" \
+    "v_bfe_i32 %[t7], %[yo2], 15, 1\n\t" \
+    "v_bfi_b32 %[t0], %[t0], %[k1], %[k0]\n\t" \
+    "v_bfi_b32 %[t1], %[t1], %[k1], %[k0]\n\t" \
+    "v_bfi_b32 %[t2], %[t2], %[k1], %[k0]\n\t" \
+    "v_bfi_b32 %[t3], %[t3], %[k1], %[k0]\n\t" \
+    "v_bfi_b32 %[t4], %[t4], %[k1], %[k0]\n\t" \
+    "v_bfi_b32 %[t5], %[t5], %[k1], %[k0]\n\t" \
+    "v_bfi_b32 %[t6], %[t6], %[k1], %[k0]\n\t" \
+    "v_bfi_b32 %[t7], %[t7], %[k1], %[k0]\n\t" \
+    "v_mad_i32_i16 %[t0], %[yo0], %[mf2], %[t0]\n\t" \
+    "v_mad_i32_i16 %[t1], %[ye1], %[mf2], %[t1]\n\t" \
+    "v_mad_i32_i16 %[t2], %[ye2], %[mf0], %[t2]\n\t" \
+    "v_mad_i32_i16 %[t3], %[yo1], %[mf1], %[t3]\n\t" \
+    "v_mad_i32_i16 %[t4], %[ye0], %[mf0], %[t4] op_sel:[1,0,0,0]\n\t" \
+    "v_mad_i32_i16 %[t5], %[yo0], %[mf2], %[t5] op_sel:[1,0,0,0]\n\t" \
+    "v_mad_i32_i16 %[t6], %[ye1], %[mf2], %[t6] op_sel:[1,0,0,0]\n\t" \
+    "v_mad_i32_i16 %[t7], %[yo2], %[mf2], %[t7]\n\t" \
+    "v_ashrrev_i32_sdwa %[d0], %[sh], %[t0] dst_sel:BYTE_0 dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:DWORD\n\t" \
+    "v_ashrrev_i32_sdwa %[d1], %[sh], %[t4] dst_sel:BYTE_0 dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:DWORD\n\t" \
+    "v_ashrrev_i32_sdwa %[d0], %[sh], %[t1] dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD\n\t" \
+    "v_ashrrev_i32_sdwa %[d1], %[sh], %[t5] dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD\n\t" \
+    "v_ashrrev_i32_sdwa %[d0], %[sh], %[t2] dst_sel:BYTE_2 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD\n\t" \
+    "v_ashrrev_i32_sdwa %[d1], %[sh], %[t6] dst_sel:BYTE_2 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD\n\t" \
+    "v_ashrrev_i32_sdwa %[d0], %[sh], %[t3] dst_sel:BYTE_3 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD\n\t" \
+    "v_ashrrev_i32_sdwa %[d1], %[sh], %[t7] dst_sel:BYTE_3 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD\n\t"
+/* 8 coefficients */
+#define SCROLL_QCHROMA1 \
+    "v_bfe_i32 %[t0], %[ye3], 15, 1\n\t" \
+    "v_bfe_i32 %[t1], %[yo3], 15, 1\n\t" \
+    "v_ashrrev_i32 %[t2], 31, %[ye2]\n\t" \
+    "v_ashrrev_i32 %[t3], 31, %[yo1]\n\t" \
+    "v_ashrrev_i32 %[t4], 31, %[yo2]\n\t" \
+    "v_ashrrev_i32 %[t5], 31, %[ye3]\n\t" \
+    "v_ashrrev_i32 %[t6], 31, %[yo3]\n\t" \
+    "v_bfi_b32 %[t0], %[t0], %[k1], %[k0]\n\t" \
+    "v_bfi_b32 %[t1], %[t1], %[k1], %[k0]\n\t" \
+    "v_bfi_b32 %[t2], %[t2], %[k1], %[k0]\n\t" \
+    "v_bfi_b32 %[t3], %[t3], %[k1], %[k0]\n\t" \
+    "v_bfi_b32 %[t4], %[t4], %[k1], %[k0]\n\t" \
+    "v_bfi_b32 %[t5], %[t5], %[k1], %[k0]\n\t" \
+    "v_bfi_b32 %[t6], %[t6], %[k1], %[k0]\n\t" \
+    "v_mad_i32_i16 %[t0], %[ye3], %[mf2], %[t0]\n\t" \
+    "v_mad_i32_i16 %[t1], %[yo3], %[mf1], %[t1]\n\t" \
+    "v_mad_i32_i16 %[t2], %[ye2], %[mf0], %[t2] op_sel:[1,0,0,0]\n\t" \
+    "v_mad_i32_i16 %[t3], %[yo1], %[mf1], %[t3] op_sel:[1,0,0,0]\n\t" \
+    "v_mad_i32_i16 %[t4], %[yo2], %[mf2], %[t4] op_sel:[1,0,0,0]\n\t" \
+    "v_mad_i32_i16 %[t5], %[ye3], %[mf2], %[t5] op_sel:[1,0,0,0]\n\t" \
+    "v_mad_i32_i16 %[t6], %[yo3], %[mf1], %[t6] op_sel:[1,0,0,0]\n\t" \
+    "v_ashrrev_i32_sdwa %[d0], %[sh], %[t0] dst_sel:BYTE_0 dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:DWORD\n\t" \
+    "v_ashrrev_i32_sdwa %[d1], %[sh], %[t4] dst_sel:BYTE_0 dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:DWORD\n\t" \
+    "v_ashrrev_i32_sdwa %[d0], %[sh], %[t1] dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD\n\t" \
+    "v_ashrrev_i32_sdwa %[d1], %[sh], %[t5] dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD\n\t" \
+    "v_ashrrev_i32_sdwa %[d0], %[sh], %[t2] dst_sel:BYTE_2 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD\n\t" \
+    "v_ashrrev_i32_sdwa %[d1], %[sh], %[t6] dst_sel:BYTE_2 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD\n\t" \
+    "v_ashrrev_i32_sdwa %[d0], %[sh], %[t3] dst_sel:BYTE_3 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD\n\t"
+/* 7 coefficients */
+
+/* a = source rows, pr = prediction rows (packed bytes): pk = 16 int8 levels
+ * in scan order (chroma AC: the 15 from scan index 1, byte 15 zero), w0 =
+ * W[0] (chroma DC, unquantised); the same values as fwd4x4 + quant of a - pr */
+template <bool LUMA>
+__device__ __host__ inline void levels_pk(const uint32_t a[4], const uint32_t pr[4], uint32_t pk4[4], int &w0)
+{
+#ifdef __HIP_DEVICE_COMPILE__
+    typedef short s2 __attribute__((ext_vector_type(2)));
+    uint32_t P[4], Q[4];
+    asm("v_sub_u16_sdwa %[p0], %[a0], %[b0] dst_sel:WORD_0 dst_unused:UNUSED_PAD src0_sel:BYTE_0 src1_sel:BYTE_0\n\t"
+        "v_sub_u16_sdwa %[p1], %[a1], %[b1] dst_sel:WORD_0 dst_unused:UNUSED_PAD src0_sel:BYTE_0 src1_sel:BYTE_0\n\t"
+        "v_sub_u16_sdwa %[p2], %[a2], %[b2] dst_sel:WORD_0 dst_unused:UNUSED_PAD src0_sel:BYTE_0 src1_sel:BYTE_0\n\t"
+        "v_sub_u16_sdwa %[p3], %[a3], %[b3] dst_sel:WORD_0 dst_unused:UNUSED_PAD src0_sel:BYTE_0 src1_sel:BYTE_0\n\t"
+        "v_sub_u16_sdwa %[q0], %[a0], %[b0] dst_sel:WORD_0 dst_unused:UNUSED_PAD src0_sel:BYTE_3 src1_sel:BYTE_3\n\t"
+        "v_sub_u16_sdwa %[q1], %[a1], %[b1] dst_sel:WORD_0 dst_unused:UNUSED_PAD src0_sel:BYTE_3 src1_sel:BYTE_3\n\t"
+        "v_sub_u16_sdwa %[q2], %[a2], %[b2] dst_sel:WORD_0 dst_unused:UNUSED_PAD src0_sel:BYTE_3 src1_sel:BYTE_3\n\t"
+        "v_sub_u16_sdwa %[q3], %[a3], %[b3] dst_sel:WORD_0 dst_unused:UNUSED_PAD src0_sel:BYTE_3 src1_sel:BYTE_3\n\t"
+        "v_sub_u16_sdwa %[p0], %[a0], %[b0] dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:BYTE_1 src1_sel:BYTE_1\n\t"
+        "v_sub_u16_sdwa %[p1], %[a1], %[b1] dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:BYTE_1 src1_sel:BYTE_1\n\t"
+        "v_sub_u16_sdwa %[p2], %[a2], %[b2] dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:BYTE_1 src1_sel:BYTE_1\n\t"
+        "v_sub_u16_sdwa %[p3], %[a3], %[b3] dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:BYTE_1 src1_sel:BYTE_1\n\t"
+        "v_sub_u16_sdwa %[q0], %[a0], %[b0] dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:BYTE_2 src1_sel:BYTE_2\n\t"
+        "v_sub_u16_sdwa %[q1], %[a1], %[b1] dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:BYTE_2 src1_sel:BYTE_2\n\t"
+        "v_sub_u16_sdwa %[q2], %[a2], %[b2] dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:BYTE_2 src1_sel:BYTE_2\n\t"
+        "v_sub_u16_sdwa %[q3], %[a3], %[b3] dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:BYTE_2 src1_sel:BYTE_2"
+        : [p0] "=&v"(P[0]), [p1] "=&v"(P[1]), [p2] "=&v"(P[2]), [p3] "=&v"(P[3]), [q0] "=&v"(Q[0]),
+          [q1] "=&v"(Q[1]), [q2] "=&v"(Q[2]), [q3] "=&v"(Q[3])
+        : [a0] "v"(a[0]), [a1] "v"(a[1]), [a2] "v"(a[2]), [a3] "v"(a[3]), [b0] "v"(pr[0]), [b1] "v"(pr[1]),
+          [b2] "v"(pr[2]), [b3] "v"(pr[3]));
+    s2 E[4], O[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const s2 p = __builtin_bit_cast(s2, P[i]), q = __builtin_bit_cast(s2, Q[i]);
+        const s2 S = p + q, D = p - q;
+        E[i] = S.yy * (s2){1, -1} + S.xx;                   /* (t0, t2) */
+        O[i] = D.yy * (s2){1, -2} + D.xx * (s2){2, 1};      /* (t1, t3) */
+    }
+    uint32_t ye[4], yo[4];                                  /* row k: (W[4k], W[4k+2]), (W[4k+1], W[4k+3]) */
+    {
+        const s2 s0 = E[0] + E[3], s1 = E[1] + E[2], d0 = E[0] - E[3], d1 = E[1] - E[2];
+        ye[0] = __builtin_bit_cast(uint32_t, s0 + s1);
+        ye[2] = __builtin_bit_cast(uint32_t, s0 - s1);
+        ye[1] = __builtin_bit_cast(uint32_t, d0 * (s2){2, 2} + d1);
+        ye[3] = __builtin_bit_cast(uint32_t, d0 - d1 * (s2){2, 2});
+    }
+    {
+        const s2 s0 = O[0] + O[3], s1 = O[1] + O[2], d0 = O[0] - O[3], d1 = O[1] - O[2];
+        yo[0] = __builtin_bit_cast(uint32_t, s0 + s1);
+        yo[2] = __builtin_bit_cast(uint32_t, s0 - s1);
+        yo[1] = __builtin_bit_cast(uint32_t, d0 * (s2){2, 2} + d1);
+        yo[3] = __builtin_bit_cast(uint32_t, d0 - d1 * (s2){2, 2});
+    }
+    w0 = (int)(int16_t)(uint16_t)ye[0];
+    uint32_t t0, t1, t2, t3, t4, t5, t6, t7;
+#define SCROLL_QOPS(D0, D1)                                                                            \
+    : [d0] "=&v"(D0), [d1] "=&v"(D1), [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2), [t3] "=&v"(t3),   \
+      [t4] "=&v"(t4), [t5] "=&v"(t5), [t6] "=&v"(t6), [t7] "=&v"(t7)                                     \
+    : [ye0] "v"(ye[0]), [ye1] "v"(ye[1]), [ye2] "v"(ye[2]), [ye3] "v"(ye[3]), [yo0] "v"(yo[0]),          \
+      [yo1] "v"(yo[1]), [yo2] "v"(yo[2]), [yo3] "v"(yo[3]),                                              \
+      [k1] "s"((uint32_t)((1 << QBITS) - 1 - QF)), [k0] "v"((uint32_t)QF), [sh] "v"(QBITS), [mf0] "s"(MF0), \
+      [mf1] "s"(MF1), [mf2] "s"(MF2)
+    if constexpr (LUMA) {
+        asm(SCROLL_QLUMA0 SCROLL_QOPS(pk4[0], pk4[1]));
+        asm(SCROLL_QLUMA1 SCROLL_QOPS(pk4[2], pk4[3]));
+    } else {
+        asm(SCROLL_QCHROMA0 SCROLL_QOPS(pk4[0], pk4[1]));
+        asm(SCROLL_QCHROMA1 SCROLL_QOPS(pk4[2], pk4[3]));
+    }
+#undef SCROLL_QOPS
+#else
+    using pk::half;
+    using pk::pack2;
+    uint32_t E[4], O[4];
+    for (int i = 0; i < 4; ++i) {
+        int r[4];
+        for (int c = 0; c < 4; ++c) r[c] = (int)((a[i] >> (8 * c)) & 255u) - (int)((pr[i] >> (8 * c)) & 255u);
+        const uint32_t P = pack2(r[0], r[1]), Q = pack2(r[3], r[2]);
+        const uint32_t S = pack2(half(P, 0) + half(Q, 0), half(P, 1) + half(Q, 1));
+        const uint32_t D = pack2(half(P, 0) - half(Q, 0), half(P, 1) - half(Q, 1));
+        E[i] = pack2(half(S, 0) + half(S, 1), half(S, 0) - half(S, 1));
+        O[i] = pack2(2 * half(D, 0) + half(D, 1), half(D, 0) - 2 * half(D, 1));
+    }
+    uint32_t ye[4], yo[4];
+    for (int g = 0; g < 2; ++g) {
+        const uint32_t *X = g ? O : E;
+        uint32_t *Y = g ? yo : ye;
+        for (int h = 0; h < 2; ++h) {
+            const int s0 = half(X[0], h) + half(X[3], h), s1 = half(X[1], h) + half(X[2], h);
+            const int d0 = half(X[0], h) - half(X[3], h), d1 = half(X[1], h) - half(X[2], h);
+            const int v[4] = {s0 + s1, 2 * d0 + d1, s0 - s1, d0 - 2 * d1};
+            for (int k = 0; k < 4; ++k) Y[k] = (h ? Y[k] & 0xffffu : 0u) | (uint32_t)(uint16_t)v[k] << (16 * h);
+        }
+    }
+    w0 = half(ye[0], 0);
+    pk4[0] = pk4[1] = pk4[2] = pk4[3] = 0;
+    for (int k2 = LUMA ? 0 : 1; k2 < 16; ++k2) {
+        const int p = ZZ[k2], r = p >> 2, c = p & 3, o = LUMA ? k2 : k2 - 1;
+        const int mf = ((r | c) & 1) == 0 ? MF0 : (((r & c) & 1) ? MF1 : MF2);
+        const uint32_t y = (c & 1) ? yo[r] : ye[r];
+        const int w = half(y, c >> 1);
+        const uint32_t sg = (uint32_t)(w >> 31);
+        const uint32_t bias = (sg & (uint32_t)((1 << QBITS) - 1 - QF)) | (~sg & (uint32_t)QF);
+        const int v = w * mf + (int)bias;
+        pk4[o >> 2] |= ((uint32_t)(v >> QBITS) & 255u) << (8 * (o & 3));
+    }
+#endif
+}
+
 /* non-zero bytes of a word (levels packed as int8) */
 __device__ __host__ inline int nz_bytes(uint32_t x)
 {
@@ -677,6 +945,117 @@ __device__ __host__ inline int cavlc_body(CAP &cap, const PTabs &P, uint4 pk, in
             ok = true;
             return tc;
         }
+    }
+    if (an > 32u) cap.put((uint32_t)(acc >> 32), (int)(an - 32u));
+    cap.put((uint32_t)acc, an > 32u ? 32 : (int)an);
+    ok = cap.n <= 128;
+    return tc;
+}
+
+/* total_zeros + run_before of a block depend only on its non-zero mask
+ * (9.2.3, 9.2.4): k_dyn_row looks them up as ONE table entry instead of a
+ * loop per block.  Entry = the bits MSB-first and left-aligned, then a '1'
+ * sentinel, so len = 31 - ctz(entry) (at most 30 bits for 16 coefficients,
+ * 25 for 15).  Table: [0, 65536) luma masks, [65536, 98304) chroma AC
+ * (15 coefficients, bit i = scan index i + 1). */
+constexpr int TZRB_N = 65536 + 32768;
+__device__ __host__ inline uint32_t tzrb_entry(const Tabs &T, uint32_t nz, int maxc)
+{
+    const int tc = __builtin_popcount(nz);
+    if (tc == 0) return 1u << 31;
+    uint32_t acc = 0;
+    int n = 0;
+    const int hi = 31 - __builtin_clz(nz), tz = hi + 1 - tc;
+    if (tc < maxc) {
+        acc = T.tz_bits[tc - 1][tz];
+        n = T.tz_len[tc - 1][tz];
+    }
+    int zl = tz, p = hi;
+    uint32_t m = nz & ~(1u << hi);
+    for (int k = 1; k < tc && zl > 0; ++k) {
+        const int q = 31 - __builtin_clz(m);
+        m &= ~(1u << q);
+        const int run = p - q - 1, zi = (zl < 7 ? zl : 7) - 1;
+        acc = (acc << T.rb_len[zi][run]) | T.rb_bits[zi][run];
+        n += T.rb_len[zi][run];
+        zl -= run;
+        p = q;
+    }
+    return (n ? acc << (32 - n) : 0u) | (1u << (31 - n));
+}
+
+/* cavlc_body for k_dyn_row (levels as LDS bytes lb, bit i = level i non-zero
+ * in nz, tzrb = the block's tzrb_entry, loaded by the caller before the call
+ * so its latency hides behind the level loop):
+ *   - the top three non-zero levels read at once (positions from nz with a
+ *     guard bit, so no zero test per find), TrailingOnes and their signs
+ *     from them;
+ *   - the level loop as in cavlc_body;
+ *   - total_zeros + run_before as one field from the entry.
+ * Same bits, TotalCoeff, TrailingOnes and ok as cavlc_body<CAP, true>. */
+template <class CAP>
+__device__ __host__ inline int cavlc_body_t(CAP &cap, const int8_t *lb, uint32_t nz, uint32_t tzrb, int &t1o,
+                                            bool &ok)
+{
+    const int tc = __builtin_popcount(nz);
+    /* g: the mask shifted up one with a guard bit 0 -- clz(g) <= 31, and
+     * g's position q + 1 is level q; the guard reads lb[-1] (ignored) */
+    const uint32_t g0 = (nz << 1) | 1u;
+    const int c0 = __builtin_clz(g0);
+    const uint32_t g1 = g0 & ~((0x80000000u >> c0) & ~1u);
+    const int c1 = __builtin_clz(g1);
+    const uint32_t g2 = g1 & ~((0x80000000u >> c1) & ~1u);
+    const int c2 = __builtin_clz(g2);
+    const uint32_t g3 = g2 & ~((0x80000000u >> c2) & ~1u);
+    const int v0 = lb[30 - c0], v1 = lb[30 - c1], v2 = lb[30 - c2];
+    /* a level is a trailing one iff it exists (not the guard) and is +-1 */
+    const bool o0 = c0 < 31 && v0 * v0 == 1, o1 = o0 && c1 < 31 && v1 * v1 == 1;
+    const bool o2 = o1 && c2 < 31 && v2 * v2 == 1;
+    const int t1 = (int)o0 + (int)o1 + (int)o2;
+    t1o = t1;
+    ok = true;
+    if (tc == 0) return 0;
+    const uint32_t s3 = ((uint32_t)v0 >> 31) << 2 | ((uint32_t)v1 >> 31) << 1 | ((uint32_t)v2 >> 31);
+    uint64_t acc = s3 >> (3 - t1);                         /* the trailing-one signs, first one first */
+    uint32_t an = (uint32_t)t1;
+    uint32_t m = (t1 == 0 ? g0 : (t1 == 1 ? g1 : (t1 == 2 ? g2 : g3))) >> 1;
+    auto push = [](uint64_t &ac, uint32_t &n, uint32_t v, uint32_t len, CAP &c) {
+        if (n + len > 64u) {                               /* rare: spill */
+            if (n > 32u) c.put((uint32_t)(ac >> 32), (int)(n - 32u));
+            c.put((uint32_t)ac, n > 32u ? 32 : (int)n);
+            ac = 0;
+            n = 0;
+        }
+        ac = (ac << len) | v;
+        n += len;
+    };
+    int sl = (tc > 10 && t1 < 3) ? 1 : 0;
+    int adj = t1 < 3 ? 2 : 0;                              /* the first level after < 3 trailing ones */
+    for (int k = t1; k < tc; ++k) {                        /* levels below the trailing ones */
+        const int p = top_bit(m);
+        m &= ~(1u << p);
+        const int v = (int)lb[p];
+        const int a = v < 0 ? -v : v;
+        const int code = 2 * a - 2 + (v < 0 ? 1 : 0) - adj;
+        adj = 0;
+        const int lim = sl ? (15 << sl) : 30;
+        const uint32_t mk = (1u << sl) - 1u;
+        uint32_t fv = ((uint32_t)code & mk) | (mk + 1u);
+        uint32_t fl = (uint32_t)((code >> sl) + 1 + sl);
+        const bool e15 = code >= lim, e14 = sl == 0 && code >= 14;
+        fv = e15 ? (uint32_t)(4096 + code - lim) : (e14 ? (uint32_t)(code + 2) : fv);
+        fl = e15 ? 28u : (e14 ? 19u : fl);
+        push(acc, an, fv, fl, cap);
+        const int s1 = sl == 0 ? 1 : sl;
+        sl = s1 + ((a > (3 << (s1 - 1)) && s1 < 6) ? 1 : 0);
+    }
+    /* total_zeros + run_before: the entry's code, len = 31 - ctz */
+    const uint32_t tzl = 31u - (uint32_t)__builtin_ctz(tzrb);
+    push(acc, an, (tzrb >> 1) >> (31u - tzl), tzl, cap);
+    if (cap.n == 0) {                                      /* nothing spilled: acc is the body */
+        cap.lo = acc;
+        cap.n = an;
+        return tc;
     }
     if (an > 32u) cap.put((uint32_t)(acc >> 32), (int)(an - 32u));
     cap.put((uint32_t)acc, an > 32u ? 32 : (int)an);

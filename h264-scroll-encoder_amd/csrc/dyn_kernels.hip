@@ -27,6 +27,7 @@
 #include <hip/hip_runtime.h>
 
 #include <stdint.h>
+#include <mutex>
 
 #include "dyn_device.h"
 #include "dyn_engine.h"
@@ -41,6 +42,16 @@ namespace {
 __constant__ Tabs g_tabs = SCROLL_DYN_TABS;
 constexpr Tabs k_tabs = SCROLL_DYN_TABS;
 __constant__ PTabs g_ptabs = make_ptabs(k_tabs);
+/* total_zeros + run_before per non-zero mask (tzrb_entry), k_dyn_row's
+ * table: 384 KB, filled once per device by k_tzrb_init; mostly L2-resident
+ * (the masks of real blocks are few) */
+__device__ uint32_t g_tzrb[TZRB_N];
+
+__global__ __launch_bounds__(256) void k_tzrb_init()
+{
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i < TZRB_N) g_tzrb[i] = i < 65536 ? tzrb_entry(g_tabs, (uint32_t)i, 16) : tzrb_entry(g_tabs, (uint32_t)(i - 65536), 15);
+}
 
 /* packed CAVLC tables -> LDS, one 16-byte load per thread */
 __device__ inline void load_ptabs(PTabs &dst, int t, int nthr)
@@ -1112,6 +1123,13 @@ __device__ inline void row_levels(bool luma, const BlkPix &px, uint32_t pk[4], i
 #pragma unroll
         for (int i = 0; i < 4; ++i) pr[i] = bilin4(px.b[i], px.c[i], (px.fr >> (3 * i)) & 7u);
     }
+#ifndef SCROLL_SCALAR_LEVELS
+    /* packed 16-bit pairs (dyn_device.h levels_pk) */
+    if (luma) levels_pk<true>(px.a, pr, pk, w0);
+    else levels_pk<false>(px.a, pr, pk, w0);
+    n = nz_bytes(pk[0]) + nz_bytes(pk[1]) + nz_bytes(pk[2]) + nz_bytes(pk[3]);
+    return;
+#endif
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
 #pragma unroll
@@ -1318,9 +1336,15 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
 #ifdef SCROLL_ABL_NOCAVLC
             const int tc = __builtin_popcount(v4.x | v4.y | v4.z | v4.w) & 15;
             cap.n = tc * 3;
-#else
+#elif defined(SCROLL_CAVLC_LOOP)
             const int tc = cavlc_body<CapSink, true>(cap, L.ptabs, v4, luma ? 16 : 15, t1, ok,
                                                      reinterpret_cast<const int8_t *>(lv + slot));
+#else
+            /* total_zeros + run_before from the table: the load is in flight
+             * during the trailing ones and the level loop */
+            const uint32_t nz = nz_mask16(v4);
+            const uint32_t tzrb = g_tzrb[luma ? nz : 65536u + nz];
+            const int tc = cavlc_body_t(cap, reinterpret_cast<const int8_t *>(lv + slot), nz, tzrb, t1, ok);
 #endif
             mt[slot] = ok ? (uint16_t)(cap.n | (uint32_t)tc << 8 | (uint32_t)t1 << 13)
                           : (uint16_t)((uint32_t)tc << 8 | (uint32_t)t1 << 13 | M_OVF);
@@ -2438,6 +2462,18 @@ int dyn_launch_code(hipStream_t hs, int nframes, int S, DevStream *st, const Nal
                     uint32_t epoch, int mbw, uint64_t *stamps)
 {
     if (nframes <= 0 || S <= 0) return 0;
+    {                                   /* the tzrb table, once per device (and process) */
+        static std::mutex mu;
+        static uint64_t ready = 0;
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess || dev >= 64) return -1;
+        std::lock_guard<std::mutex> lk(mu);
+        if (!(ready >> dev & 1u)) {
+            hipLaunchKernelGGL(k_tzrb_init, dim3((TZRB_N + 255) / 256), dim3(256), 0, hs);
+            if (hipGetLastError() != hipSuccess || hipStreamSynchronize(hs) != hipSuccess) return -1;
+            ready |= 1ull << dev;
+        }
+    }
     hipLaunchKernelGGL(k_dyn_rows, dim3(nframes, S), dim3(256), 0, hs, st, nal, ld_nal, pend, dfr, ld_fr,
                        *g, x->rows);
     if (hipGetLastError() != hipSuccess) return -1;

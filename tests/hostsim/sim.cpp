@@ -334,6 +334,95 @@ long sim_cavlc_split(const int *coef, int max, int nC, int start, uint32_t *word
     return (long)tl + (long)cap.n;
 }
 
+/* k_dyn_row's form: cavlc_body_t (levels as bytes with one guard byte
+ * before them, total_zeros + run_before from tzrb_entry) + coeff_token; must
+ * equal cavlc_block bit for bit (same overflow rule as sim_cavlc_split) */
+long sim_cavlc_split_t(const int *coef, int max, int nC, int start, uint32_t *words, int *tc_out)
+{
+    dyn::OrSink<HostOr> os{{words}, 0, 0, 0};
+    os.start((uint32_t)start);
+    bool fits = max != 4;
+    int8_t lb[17] = {0};
+    lb[0] = 1;                                        /* the guard byte: any value */
+    uint32_t nz = 0;
+    for (int i = 0; i < max && fits; ++i) {
+        fits = coef[i] >= -128 && coef[i] <= 127;
+        lb[1 + i] = (int8_t)coef[i];
+        if (coef[i]) nz |= 1u << i;
+    }
+    dyn::CapSink cap{0, 0, 0};
+    int t1 = 0, tc = 0;
+    bool ok = false;
+    if (fits) {
+        const uint32_t e = dyn::tzrb_entry(g_dyn_tabs, nz, max);
+        tc = dyn::cavlc_body_t(cap, lb + 1, nz, e, t1, ok);
+    }
+    if (!ok) {
+        *tc_out = dyn::cavlc_block(os, g_dyn_tabs, coef, max, nC);
+        const uint32_t end = os.wi * 32u + (uint32_t)os.fill;
+        os.finish();
+        return (long)(end - (uint32_t)start);
+    }
+    uint32_t tv;
+    int tl;
+    dyn::coeff_token(g_dyn_tabs, tc, t1, nC, tv, tl);
+    os.put(tv, tl);
+    os.put_cap(cap);
+    os.finish();
+    *tc_out = tc;
+    return (long)tl + (long)cap.n;
+}
+
+/* k_dyn_row's packed-pair levels (levels_pk) against fwd4x4 + quant of the
+ * same residual, n random 4x4 blocks (the extremes included): 0 = all equal,
+ * else 1 + the failing block */
+long sim_levels_pk(long n, unsigned seed)
+{
+    uint64_t x = seed * 0x9e3779b97f4a7c15ull + 1;
+    auto rnd = [&]() { x ^= x << 13; x ^= x >> 7; x ^= x << 17; return (uint32_t)x; };
+    for (long it = 0; it < n; ++it) {
+        uint32_t a[4], p[4];
+        const int kind = (int)(it % 5);
+        for (int i = 0; i < 4; ++i) {
+            a[i] = rnd();
+            p[i] = rnd();
+            if (kind == 1) { a[i] = 0xffffffffu; p[i] = 0; }          /* max residual */
+            if (kind == 2) { a[i] = 0; p[i] = 0xffffffffu; }          /* min residual */
+            if (kind == 3) p[i] = a[i] ^ (rnd() & 0x07070707u);      /* small residuals */
+            if (kind == 4) { a[i] = (i & 1) ? 0xff00ff00u : 0x00ff00ffu; p[i] = ~a[i]; }  /* checker */
+        }
+        for (int luma = 0; luma < 2; ++luma) {
+            int res[16], W[16];
+            for (int i = 0; i < 4; ++i)
+                for (int c = 0; c < 4; ++c)
+                    res[4 * i + c] = (int)((a[i] >> (8 * c)) & 255u) - (int)((p[i] >> (8 * c)) & 255u);
+            dyn::fwd4x4(res, W);
+            uint32_t want[4] = {0, 0, 0, 0};
+            for (int k2 = luma ? 0 : 1; k2 < 16; ++k2) {
+                const int v = dyn::quant(W[dyn::ZZ[k2]], dyn::ZZ[k2]), o = luma ? k2 : k2 - 1;
+                want[o >> 2] |= ((uint32_t)v & 255u) << (8 * (o & 3));
+            }
+            uint32_t got[4] = {0x5a5a5a5au, 0x5a5a5a5au, 0x5a5a5a5au, 0x5a5a5a5au};
+            int w0 = 0;
+            if (luma) dyn::levels_pk<true>(a, p, got, w0);
+            else dyn::levels_pk<false>(a, p, got, w0);
+            if (std::memcmp(want, got, sizeof want) != 0 || w0 != W[0]) return 1 + it;
+        }
+    }
+    return 0;
+}
+
+/* tzrb_entry's longest code over every mask (luma 16, chroma AC 15) */
+int sim_tzrb_maxlen(int max)
+{
+    int mx = 0;
+    for (uint32_t nz = 0; nz < (1u << max); ++nz) {
+        const uint32_t e = dyn::tzrb_entry(g_dyn_tabs, nz, max);
+        mx = std::max(mx, 31 - __builtin_ctz(e));
+    }
+    return mx;
+}
+
 /* the compile-time packed tables the kernels copy (make_ptabs) equal the
  * runtime packing (build_ptabs): 1 if identical */
 int sim_ptabs_match(void)

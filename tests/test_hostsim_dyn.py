@@ -71,11 +71,32 @@ def test_cavlc_blocks_vs_oracle(hostsim, oracle):
         n2 = hostsim.sim_cavlc_split(ca, mx, nC, start, words, ctypes.byref(tc))
         assert n2 == n and tc.value == tco, (it, coef, nC)
         assert _word_bits(words, start, n) == _bits(ob, 0, n), (it, coef, nC)
+        if mx != 4:                                    # k_dyn_row's form (tzrb table)
+            ctypes.memset(words, 0, ctypes.sizeof(words))
+            n4 = hostsim.sim_cavlc_split_t(ca, mx, nC, start, words, ctypes.byref(tc))
+            assert n4 == n and tc.value == tco, (it, coef, nC)
+            assert _word_bits(words, start, n) == _bits(ob, 0, n), (it, coef, nC)
         if mx == 4:                                    # the kernels' chroma-DC encoder
             ctypes.memset(words, 0, ctypes.sizeof(words))
             n3 = hostsim.sim_cavlc_dc4(ca, start, words, ctypes.byref(tc))
             assert n3 == n and tc.value == tco, (it, coef)
             assert _word_bits(words, start, n) == _bits(ob, 0, n), (it, coef)
+
+
+def test_tzrb_table_lengths(hostsim):
+    """k_dyn_row's total_zeros + run_before entries fit their 32-bit form
+    (code + sentinel): at most 30 bits for 16 coefficients, 25 for 15"""
+    assert hostsim.sim_tzrb_maxlen(16) == 30
+    assert hostsim.sim_tzrb_maxlen(15) == 25
+
+
+def test_packed_levels_vs_scalar(hostsim):
+    """k_dyn_row's transform + quant on packed 16-bit pairs (levels_pk, host
+    emulation of its dataflow) equals fwd4x4 + quant on random and extreme
+    residual blocks, luma and chroma AC (the GPU parity tests check the
+    instructions themselves)"""
+    hostsim.sim_levels_pk.restype = ctypes.c_long
+    assert hostsim.sim_levels_pk(ctypes.c_long(200000), 7) == 0
 
 
 def _planes(rng, w, h):

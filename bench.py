@@ -704,6 +704,8 @@ def main():
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--no-verify", action="store_true",
                     help="skip the post-timing oracle check of the last step")
+    ap.add_argument("--no-host", action="store_true",
+                    help="skip the host-delivery (PCIe-inclusive) and single-frame latency legs")
     args = ap.parse_args()
 
     wl = dict(WORKLOADS[args.workload])
@@ -793,6 +795,12 @@ def main():
         dist.all_reduce(flag, op=dist.ReduceOp.MIN)
         all_ok = flag.item() > 0.5
 
+    # after the timed region and the check: the same workload delivered to
+    # pinned host memory (never `value`), and the single-frame API latency
+    host_leg = None
+    if world == 1 and not args.no_host:
+        host_leg = host_delivery(hs, wl, first, local, min(args.steps, 10), b)
+
     if rank == 0:
         n = max(n_launch, 1)
         kms = {"plan": plan_ms / n, "emit": emit_ms / n, "dyn_stage": stage_ms / n,
@@ -856,6 +864,8 @@ def main():
         if hints:
             out["hint"] = {"rbsp_bytes_per_frame": round(rbsp_tot / max(dyn_nals, 1), 1),
                            "ep_bytes_per_frame": round(ep_tot / max(dyn_nals, 1), 2)}
+        if host_leg:
+            out["host_delivery"] = host_leg
         if world == 1 and not args.no_cpu:
             cores = usable_cores()
             out["cpu_baseline"] = cpu_baseline_hint(wl) if hints else cpu_baseline(wl, cores)
@@ -866,6 +876,65 @@ def main():
         dist.destroy_process_group()
     if not all_ok:
         sys.exit(3)
+
+
+def host_delivery(hs, wl, first, device, steps, b0):
+    """PCIe-inclusive throughput (the reference hands its bytes over in host
+    memory, composer.c:255-291): every step's bytes of every stream packed by
+    the device into pinned host memory (scroll_batch_output_to_host_async).
+    Two batches alternate on two HIP streams, so one's compose overlaps the
+    other's copy.  Also the single-frame drop-in latency: h264_write_scroll_p_frame
+    (one 1280x720 P NAL per call, host bytes back) against the reference's
+    86-90 us per frame on one CPU core."""
+    import ctypes
+    import torch
+    S, F = wl["streams"], wl["frames"]
+    per_step = b0.last_bytes()
+    cap = int(per_step * 1.25 + 16 * S + (1 << 20))
+    b1 = build_compose_batch(hs, wl, first, device)
+    bats = [b0, b1]
+    hbs = [hs.HostBuffer(cap, S), hs.HostBuffer(cap, S)]
+    sts = [torch.cuda.Stream(device=device), torch.cuda.Stream(device=device)]
+    for i in range(2):                              # warm both
+        bats[i].compose(F, stream=sts[i].cuda_stream, rewind=True)
+        bats[i].output_to_host_async(hbs[i], stream=ctypes.c_void_p(sts[i].cuda_stream))
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(steps):
+        i = k & 1
+        bats[i].compose(F, stream=sts[i].cuda_stream, rewind=True)
+        bats[i].output_to_host_async(hbs[i], stream=ctypes.c_void_p(sts[i].cuda_stream))
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    ok = all(h.total() is not None for h in hbs)
+    # the delivered bytes of the last step equal the arena bytes (checked above against the oracle)
+    i = (steps - 1) & 1
+    bats[i].sync()
+    same = all(hbs[i].stream(s) == bats[i].output(s) for s in range(0, S, max(1, S // 8)))
+    delivered = sum(hbs[i].table[2 + 2 * s] for s in range(S))
+    for h in hbs:
+        h.close()
+    b1.close()
+    # single-frame latency through the reference ABI (one P NAL per call)
+    lib = hs.lib
+    cfg = hs.make_config(1280, 720)
+    buf = (ctypes.c_uint8 * (1 << 20))()
+    rb = (ctypes.c_uint8 * (1 << 20))()
+    nw = hs.NALWriter()
+    lat = []
+    for k in range(60):
+        lib.nal_writer_init(ctypes.byref(nw), buf, len(buf), rb, len(rb))
+        ta = time.perf_counter()
+        lib.h264_write_scroll_p_frame(ctypes.byref(nw), ctypes.byref(cfg), 4 * (k % 100))
+        lat.append(time.perf_counter() - ta)
+    lat = sorted(lat[10:])
+    return {"value": round(S * F * steps / el, 1), "unit": "frames/s (PCIe-inclusive, pinned host memory)",
+            "gb_per_s": round(delivered * steps / el / 1e9, 2), "bytes_per_step": int(delivered),
+            "steps": steps, "ok": bool(ok and same),
+            "how": "scroll_batch_output_to_host_async after each compose; two batches on two HIP streams",
+            "single_frame_us": {"p50": round(1e6 * lat[len(lat) // 2], 1), "min": round(1e6 * lat[0], 1),
+                                "api": "h264_write_scroll_p_frame 1280x720 (GPU round trip per call)",
+                                "reference_cpu_us": "86-90 (BASELINE.md section 2, one core)"}}
 
 
 def build_compose_batch(hs, wl, first, device):

@@ -10,8 +10,9 @@
 
 /* all return 0, or -1 when the launch failed */
 /* per-batch scratch of the dynamic-rect coder: prediction
- * rows (32 h u32 per NAL), block records (DYN_PIECES per dynamic MB: a u32
- * meta half-word and a 16-byte body) */
+ * rows (32 h u32 per NAL), block records of the general-path NALs
+ * (DYN_PIECES per dynamic MB: a u16 meta and a 16-byte body; gen_cap NAL
+ * slots taken per compose), row stage (+ spill slots) */
 typedef struct {
     uint32_t *rows;
     uint16_t *meta;
@@ -19,6 +20,8 @@ typedef struct {
     unsigned long long *tcx;        /* k_dyn_row: per (frame, rect row, MB) bottom TotalCoeffs */
     uint32_t *rowstage;             /* per (frame, row group): its bits from bit 0 (rs_frame_words) */
     uint32_t *gbits;                /* per (frame, row group): its bit count */
+    uint32_t *spill;                /* rs_spill_cap spill slots (rect rows over their slot) */
+    uint32_t *ctr;                  /* per compose: [0] spill slots taken, [1] general records taken */
     uint32_t epoch;                 /* look-back epoch of the last compose (24 bits, never 0) */
 } DynScratch;
 

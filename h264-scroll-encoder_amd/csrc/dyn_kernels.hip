@@ -232,7 +232,7 @@ __global__ __launch_bounds__(256) void k_dyn_rows(const DevStream *__restrict__ 
                                                   const NalDesc *__restrict__ nal, int ld_nal,
                                                   const PlanPending *__restrict__ pend,
                                                   DynFrame *__restrict__ dfr, int ld_fr, DynGeom g,
-                                                  uint32_t *__restrict__ rows)
+                                                  uint32_t *__restrict__ rows, uint32_t *__restrict__ ctr)
 {
     __shared__ int32_t wo[8], wl[8], wv[8];
     __shared__ int32_t gen;
@@ -283,7 +283,20 @@ __global__ __launch_bounds__(256) void k_dyn_rows(const DevStream *__restrict__ 
     if (my_gen) gen = 1;
     __syncthreads();
     if (t == 0) {
-        DF->err = gen ? DF_GENERAL : 0u;
+        /* a general-path NAL takes a record slot (index in rbsp_bytes until
+         * k_dyn_epfix); none left: the frame fails (DF_OVER, the batch
+         * grows the pool for the next compose) */
+        uint32_t e = 0u;
+        if (gen) {
+            const uint32_t k = atomicAdd(&ctr[1], 1u);
+            if (k < g.gen_cap) {
+                DF->rbsp_bytes = k;
+                e = DF_GENERAL;
+            } else {
+                e = DF_OVER;
+            }
+        }
+        DF->err = e;
         DF->ep = 0u;                                    /* k_dyn_epscan adds to it */
     }
 }
@@ -348,8 +361,9 @@ __device__ inline void code_frame(const DevStream *__restrict__ st,
     const int lstride = 16 * g.w, cstride = 8 * g.w;
     const uint8_t *fcb = fs + (size_t)256 * ndt, *fcr = fcb + (size_t)64 * ndt;
     const uint32_t m_rw = magic32((uint32_t)g.w);
-    uint16_t *M = meta + nb * (size_t)(NPC * ndt);
-    uint2 *BL = blo + nb * (size_t)(NPC * ndt), *BH = bhi + nb * (size_t)(NPC * ndt);
+    const size_t gs = df.rbsp_bytes;                    /* its record slot (k_dyn_rows) */
+    uint16_t *M = meta + gs * (size_t)(NPC * ndt);
+    uint2 *BL = blo + gs * (size_t)(NPC * ndt), *BH = bhi + gs * (size_t)(NPC * ndt);
 
     const bool luma = task < 16 * ndt;
     const bool act = task < ntask;
@@ -1010,6 +1024,7 @@ struct RowFixed {
     int32_t head_over;
     uint32_t rt[32];                             /* the row's prediction-row table (k_dyn_rows) */
     uint32_t ncand;                              /* EP candidate words of the row */
+    uint32_t spill;                              /* its spill slot (a row over its slot) */
 };
 
 /* dynamic LDS of k_dyn_row: lv [NPC w] uint4 (levels, then bodies), mbits
@@ -1177,7 +1192,7 @@ template <bool GEN>
 __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL_ROW_WAVES))) void k_dyn_row(DevStream *__restrict__ st,
                                                      const NalDesc *__restrict__ nal, int ld_nal,
                                                      const PlanPending *__restrict__ pend,
-                                                     const DynFrame *__restrict__ dfr, int ld_fr, DynGeom g,
+                                                     DynFrame *__restrict__ dfr, int ld_fr, DynGeom g,
                                                      const uint32_t *__restrict__ rows,
                                                      const uint8_t *__restrict__ src,
                                                      const uint8_t *__restrict__ refs,
@@ -1185,6 +1200,7 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
                                                      const uint2 *__restrict__ blo, const uint2 *__restrict__ bhi,
                                                      unsigned long long *__restrict__ tcx, uint32_t epoch,
                                                      uint32_t *__restrict__ rowstage, uint32_t *__restrict__ gbits,
+                                                     uint32_t *__restrict__ spill, uint32_t *__restrict__ ctr,
                                                      uint64_t *__restrict__ stamps)
 {
     __shared__ RowFixed L;
@@ -1353,8 +1369,9 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
     } else {
         /* general path: records of k_dyn_code_general */
         const int q0 = r * w;
-        const uint16_t *M = meta + nb * (size_t)(NPC * ndt);
-        const uint2 *BL = blo + nb * (size_t)(NPC * ndt), *BH = bhi + nb * (size_t)(NPC * ndt);
+        const size_t gs = df.rbsp_bytes;                /* its record slot (k_dyn_rows) */
+        const uint16_t *M = meta + gs * (size_t)(NPC * ndt);
+        const uint2 *BL = blo + gs * (size_t)(NPC * ndt), *BH = bhi + gs * (size_t)(NPC * ndt);
         for (int i = t; i < npc; i += T) {
             const int k = div_npc(i), pc = i - k * NPC;
             const int rec = rec_of(q0 + k, pc, ndt);
@@ -1394,15 +1411,102 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
             for (int e = 0; e < 8; ++e) ta[8 * k + e] = (uint8_t)((v >> (5 * e)) & 31u);
         }
     }
+    const NalCtx c = nal_ctx(S, d, L.wo, L.wl, L.wv);
+    const HeadCtx H = head_ctx(c);
+#ifdef SCROLL_MERGED_P34
+    /* the 12 MB-head classes, on the polling wave (phase 3+4 reads them) */
+    if (wave == nwv - 1 && lane < 12) {
+        CapSink hc{0, 0, 0};
+        H.put_class(hc, lane);
+        L.hhi[lane] = hc.hi;
+        L.hlo[lane] = hc.lo;
+        L.hlen[lane] = hc.n;
+        if (hc.over()) L.head_over = 1;
+    }
+#endif
     __syncthreads();                                    /* records, top TotalCoeffs, waypoint table */
     if (stamps) stv[2] = __builtin_amdgcn_s_memrealtime();
 #if defined(SCROLL_ABL_STOP) && SCROLL_ABL_STOP == 2
     return;
 #endif
 
+#ifdef SCROLL_MERGED_P34
+    /* ---- 3+4: per piece its coeff_token and length, per MB its cbp, code
+     * and piece offsets -- one pass: an MB's 26 pieces in coding order on
+     * lanes 0-25 of a 32-lane half (two MBs per wave), cbp from one ballot,
+     * the offsets from a wave scan of the present pieces' lengths ---------- */
+    const Tabs &TB = g_tabs;
+    const PTabs &PT = *reinterpret_cast<const PTabs *>(&g_ptabs);       /* the rare overflow paths */
+    const uint16_t(*ctab)[68] = L.ptabs.ct;
+    const bool head_over = L.head_over;
+    auto head_bits = [&](int rr, int col) -> uint32_t {
+        if (!head_over) return L.hlen[H.sel(rr, col)];
+        CountSink cn{0};
+        H.put_slow(cn, rr, col);
+        return cn.n;
+    };
+    {
+        const int hf = lane >> 5, j = lane & 31;
+        const int pc = j < 16 ? blk_raster(j) : j;          /* coding order -> piece slot */
+        for (int pr = wave; 2 * pr < w; pr += nwv) {
+            const int k = 2 * pr + hf, col = R.x0 + k;
+            const bool act = j < NPC && k < w;
+            uint32_t len = 0;
+            bool nzp = false;
+            if (act) {
+                const int i = k * NPC + pc;
+                const uint32_t mv = mt[i];
+                const uint16_t *mk = mt + k * NPC;
+                uint32_t tv = 0, tl = 0;
+                int nC = -1;
+                if (pc != 16 && pc != 17) {
+                    const int nAe = col > 0 ? 0 : -1, nBe = row > 0 ? 0 : -1;
+                    int nA2, nB2;
+                    if (pc < 16) {
+                        const int bx = pc & 3, by = pc >> 2;
+                        nA2 = bx > 0 ? tc_of(mk[pc - 1]) : (k > 0 ? tc_of(mk[pc + 3 - NPC]) : nAe);
+                        nB2 = by > 0 ? tc_of(mk[pc - 4]) : (r > 0 ? (int)ta[8 * k + pc] : nBe);
+                    } else {
+                        const int bq = (pc - 18) & 3, bx = bq & 1, by = bq >> 1;
+                        nA2 = bx > 0 ? tc_of(mk[pc - 1]) : (k > 0 ? tc_of(mk[pc + 1 - NPC]) : nAe);
+                        nB2 = by > 0 ? tc_of(mk[pc - 2]) : (r > 0 ? (int)ta[8 * k + (pc < 22 ? pc - 14 : pc - 16)] : nBe);
+                    }
+                    nC = nc_of(nA2, nB2);
+                    piece_token(ctab, mv, nC, tv, tl);
+                }
+                len = tl + (mv & 255u);
+                if (mv & M_OVF) len = ovf_bits(PT, TB, lv[i], pc, nC);            /* rare */
+                lo[i] = (uint16_t)(len | (uint32_t)(nC + 1) << 11);
+                nzp = tc_of(mv) != 0;
+            }
+            const uint32_t hm = (uint32_t)(__builtin_amdgcn_ballot_w64(nzp) >> (32 * hf));
+            const int cbp_l = ((hm & 0xfu) != 0) | ((hm & 0xf0u) != 0) << 1 | ((hm & 0xf00u) != 0) << 2 |
+                              ((hm & 0xf000u) != 0) << 3;
+            const int cbp_c = (hm >> 18) & 0xffu ? 2 : ((hm >> 16) & 3u ? 1 : 0);
+            const int cbp = cbp_l | cbp_c << 4;
+            const bool pres = act && (j < 16 ? ((cbp_l >> (j >> 2)) & 1) != 0 : (j < 18 ? cbp_c >= 1 : cbp_c == 2));
+            const uint32_t lp = pres ? (len & LO_LEN) : 0u;
+            const uint32_t incl = wave_incl_sum(lp, lane);
+            const uint32_t base = hf ? (uint32_t)__shfl((int)incl, 31, 64) : 0u;
+            const uint32_t tot = (uint32_t)__shfl((int)incl, 32 * hf + 31, 64) - base;
+            if (k < w) {
+                const int code = TB.cbp_code[cbp];
+                CountSink hs{head_bits(row, col)};
+                put_ue(hs, (uint32_t)code);
+                if (cbp) put_se(hs, 0);                     /* mb_qp_delta */
+                if (act) off16[k * NPC + pc] = pres ? (uint16_t)(hs.n + incl - lp - base) : (uint16_t)0xffffu;
+                if (j == 0) {
+                    mbits[k] = hs.n + tot;
+                    cbpa[k] = (uint8_t)cbp;
+                    codea[k] = (uint8_t)code;
+                }
+            }
+        }
+    }
+    __syncthreads();
+    if (stamps) stv[3] = __builtin_amdgcn_s_memrealtime();
+#else
     /* ---- 3: coeff_token, piece lengths ----------------------------------- */
-    const NalCtx c = nal_ctx(S, d, L.wo, L.wl, L.wv);
-    const HeadCtx H = head_ctx(c);
     if (t < 12) {
         CapSink hc{0, 0, 0};
         H.put_class(hc, t);
@@ -1490,6 +1594,7 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
         codea[k] = (uint8_t)code;
     }
     __syncthreads();
+#endif
     const int gi = nA + r;
     if (wave == 0) {
         uint32_t carry = 0;
@@ -1518,7 +1623,26 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
 
     /* ---- 5: bits -> the row's own row-stage words ------------------------ */
     uint32_t *out = rowstage + nb * g.rs_frame_words + rs_group_words(g, nA, gi);
-    const uint32_t nw = min((bits + 31u) >> 5, g.rs_row_words - EPC_ROW);   /* provable bound: never clipped */
+    uint32_t epc = g.rs_row_words - EPC_ROW;            /* the EP-candidate record in the slot */
+    if (((bits + 31u) >> 5) > epc) {
+        /* the row outgrew its slot (sized for typical rows):
+         * its bits go to a spill slot at the provable bound; the slot's
+         * record word names it (k_dyn_epfix / the readers' rs_table follow) */
+        if (t == 0) L.spill = atomicAdd(&ctr[0], 1u);
+        __syncthreads();
+        const uint32_t k = L.spill;
+        uint32_t *fr = rowstage + nb * g.rs_frame_words;
+        uint32_t *sp = spill + (size_t)k * g.rs_spill_words;
+        /* none left, or out of the readers' reach (32-bit byte offsets from fr) */
+        if (k >= g.rs_spill_cap || (uint64_t)(sp - fr) + g.rs_spill_words > 0x3fffffffull) {
+            if (t == 0) atomicOr(&dfr[nb].err, DF_OVER);
+            return;
+        }
+        if (t == 0) out[epc] = 0x80000000u | (uint32_t)(sp - fr);
+        out = sp;
+        epc = g.rs_spill_words - EPC_ROW;
+    }
+    const uint32_t nw = min((bits + 31u) >> 5, epc);     /* provable bound: never clipped */
     const int npass = (int)((nw + ROW_GB - 1) / ROW_GB);
     for (int pi = 0; pi < npass; ++pi) {
         const uint32_t p0 = (uint32_t)pi * ROW_GB;
@@ -1569,11 +1693,10 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
             }
         }
         __syncthreads();
-        flush_window(L.buf, n, p0, p0 + n >= nw, out, &L.ncand, out + (g.rs_row_words - EPC_ROW), EPC_ROW - 1,
-                     t, T);
+        flush_window(L.buf, n, p0, p0 + n >= nw, out, &L.ncand, out + epc, EPC_ROW - 1, t, T);
         __syncthreads();
     }
-    if (t == 0) out[g.rs_row_words - EPC_ROW] = L.ncand;
+    if (t == 0) out[epc] = L.ncand;
     if (stamps && t == 0) {
         stv[5] = __builtin_amdgcn_s_memrealtime();
         uint64_t *o = stamps + (((size_t)s * gridDim.y + f) * ng + gi) * 8;
@@ -1680,8 +1803,8 @@ __device__ inline void stitch_load(StitchLoads &L, uint32_t c0, int t, int ng, u
 /* the row-group table of NAL nb in LDS (wave 0): goff = bit offsets (goff[ng]
  * = RBSP bits incl. the stop bit), gb = bit counts, gw = first row-stage
  * words in the frame's region */
-__device__ inline void rs_table(const uint32_t *gbits, size_t nb, const DynGeom &g, uint32_t *goff,
-                                uint32_t *gb, uint32_t *gw, int t)
+__device__ inline void rs_table(const uint32_t *gbits, size_t nb, const DynGeom &g, const uint32_t *fr,
+                                uint32_t *goff, uint32_t *gb, uint32_t *gw, uint32_t *cw, int t)
 {
     const int ng = g.ngroups;
     constexpr int SR = DYN_STATIC_ROWS;
@@ -1692,7 +1815,18 @@ __device__ inline void rs_table(const uint32_t *gbits, size_t nb, const DynGeom 
         if (t < ng) {
             gb[t] = b;
             goff[t] = incl - b;
-            gw[t] = (uint32_t)rs_group_words(g, nA, t);
+            /* a rect row that outgrew its slot: its record word names the
+             * spill slot (relative to fr) holding its bits and record */
+            uint32_t w = (uint32_t)rs_group_words(g, nA, t), c = (uint32_t)rs_runs_words(g, nA, t);
+            if (t >= nA && t < nA + g.h) {
+                const uint32_t m = fr[c];
+                if (m & 0x80000000u) {
+                    w = m & 0x7fffffffu;
+                    c = w + g.rs_spill_words - EPC_ROW;
+                }
+            }
+            gw[t] = w;
+            if (cw) cw[t] = c;
         }
         if (t == 63) goff[ng] = incl;
     }
@@ -1821,12 +1955,12 @@ __global__ __launch_bounds__(ST_T) void k_dyn_epscan(DevStream *__restrict__ st,
     DynFrame *DF = dfr + nb;
     if (DF->nal < 0 || !(DF->err & DF_EPSLOW)) return;  /* k_dyn_epfix settled it */
     const int ng = g.ngroups;
-    rs_table(gbits, nb, g, goff, gb, gw, t);
+    const uint32_t *fr = rowstage + nb * g.rs_frame_words;
+    rs_table(gbits, nb, g, fr, goff, gb, gw, nullptr, t);
     if (t == 0) ep_n = 0;
     __syncthreads();
     const uint32_t T = goff[ng];                        /* NAL RBSP bits incl. the stop bit */
     const uint32_t nin = (T + 7) >> 3;                  /* bitwriter.c:103-111 */
-    const uint32_t *fr = rowstage + nb * g.rs_frame_words;
     StitchLoads ld;
     uint32_t c0 = (uint32_t)z * ST_CHUNK;
     int gcarry = 0;
@@ -1982,7 +2116,7 @@ __global__ __launch_bounds__(EPF_T) void k_dyn_epfix(DevStream *__restrict__ st,
                                                      int ld_fr, DynGeom g, const uint32_t *__restrict__ rowstage,
                                                      const uint32_t *__restrict__ gbits, uint8_t *__restrict__ eps)
 {
-    __shared__ uint32_t goff[65], gb[64], gw[64];
+    __shared__ uint32_t goff[65], gb[64], gw[64], cw[64];
     __shared__ uint32_t cbase[65];                      /* runs before group g */
     __shared__ uint32_t lst[EPF_LIST];
     __shared__ uint32_t nlst, nu, slow;
@@ -1990,13 +2124,22 @@ __global__ __launch_bounds__(EPF_T) void k_dyn_epfix(DevStream *__restrict__ st,
     const size_t nb = (size_t)s * ld_fr + f;
     DynFrame *DF = dfr + nb;
     if (DF->nal < 0) return;
+    if (DF->err & DF_OVER) {                            /* k_dyn_rows / k_dyn_row: pools exhausted */
+        if (t == 0) {
+            DF->rbsp_bytes = 0;
+            DF->ep = 0;
+            atomicOr((unsigned int *)&st[s].err, SCROLL_DEVERR_DYN);
+        }
+        return;
+    }
     const int ng = g.ngroups;
     constexpr int SR = DYN_STATIC_ROWS;
     const int nA = max(1, (g.y0 + SR - 1) / SR);
     const uint32_t *fr = rowstage + nb * g.rs_frame_words;
-    rs_table(gbits, nb, g, goff, gb, gw, t);
+    rs_table(gbits, nb, g, fr, goff, gb, gw, cw, t);
+    __syncthreads();
     if (t < 64) {
-        const uint32_t c = t < ng ? fr[rs_runs_words(g, nA, t)] : 0u;
+        const uint32_t c = t < ng ? fr[cw[t]] : 0u;
         const uint32_t cmax = (t >= nA && t < nA + g.h) ? EPC_ROW - 1u : EPC_STATIC - 1u;
         const uint32_t cc = min(c, cmax);
         const uint32_t incl = wave_incl_sum(cc, t);
@@ -2032,7 +2175,7 @@ __global__ __launch_bounds__(EPF_T) void k_dyn_epfix(DevStream *__restrict__ st,
         int gg = 0;
         while (gg + 1 < ng && cbase[gg + 1] <= ci) ++gg;
         const uint32_t *src = fr + gw[gg];
-        const uint32_t wi = fr[rs_runs_words(g, nA, gg) + 1 + (ci - cbase[gg])];
+        const uint32_t wi = fr[cw[gg] + 1 + (ci - cbase[gg])];
         const uint32_t bits = gb[gg], nwd = (bits + 31u) >> 5, O = goff[gg];
         if (wi >= nwd) continue;
         const uint32_t w = ep_data(src[wi], wi, bits);
@@ -2126,7 +2269,7 @@ __global__ __launch_bounds__(DT) void k_dyn_emit(const DevStream *__restrict__ s
     const bool RS = rowstage != nullptr;
     const uint8_t *in = RS ? nullptr : stage + nb * g.slot_bytes;
     const uint32_t *fr = RS ? rowstage + nb * g.rs_frame_words : nullptr;
-    if (RS) rs_table(gbits, nb, g, goff, gb, gw, t);
+    if (RS) rs_table(gbits, nb, g, fr, goff, gb, gw, nullptr, t);
     __syncthreads();
     const int ng = g.ngroups;
     const uint32_t T = RS ? goff[ng] : 0u;
@@ -2248,12 +2391,13 @@ __global__ __launch_bounds__(DT) void k_dyn_emit_gather(const DevStream *__restr
     const uint32_t *el = reinterpret_cast<const uint32_t *>(RS ? stage + nb * DYN_OVF_BYTES
                                                                : in + g.slot_bytes - DYN_OVF_BYTES);
     const uint32_t *fr = RS ? rowstage + nb * g.rs_frame_words : nullptr;
-    if (RS) rs_table(gbits, nb, g, goff, gb, gw, t);
+    if (RS) rs_table(gbits, nb, g, fr, goff, gb, gw, nullptr, t);
     for (uint32_t i = t; i < n; i += DT) raw[i] = el[i];
     __syncthreads();
     const int ng = RS ? g.ngroups : 0;
     const uint32_t T = RS ? goff[ng] : 0u;
-    const __amdgpu_buffer_rsrc_t rr = buf_rsrc(fr, RS ? (uint32_t)(4 * g.rs_frame_words) : 0u);
+    /* the frame's row groups, and spill slots up to 4 GB past them (k_dyn_row's bound) */
+    const __amdgpu_buffer_rsrc_t rr = buf_rsrc(fr, RS ? 0xfffffffcu : 0u);
     int gcar = 0;                                            /* RS: the thread's row group */
     /* sort by rank (positions are distinct): sp[j] = j-th smallest */
     for (uint32_t i = t; i < n; i += DT) {
@@ -2475,7 +2619,7 @@ int dyn_launch_code(hipStream_t hs, int nframes, int S, DevStream *st, const Nal
         }
     }
     hipLaunchKernelGGL(k_dyn_rows, dim3(nframes, S), dim3(256), 0, hs, st, nal, ld_nal, pend, dfr, ld_fr,
-                       *g, x->rows);
+                       *g, x->rows, x->ctr);
     if (hipGetLastError() != hipSuccess) return -1;
     const int nchunk = (24 * g->w * g->h + CODE_T - 1) / CODE_T;
     hipLaunchKernelGGL(k_dyn_code_general, dim3(nchunk, CODE_GEN_Y), dim3(CODE_T), 0, hs, st, dfr, ld_fr,
@@ -2483,11 +2627,13 @@ int dyn_launch_code(hipStream_t hs, int nframes, int S, DevStream *st, const Nal
     if (hipGetLastError() != hipSuccess) return -1;
     hipLaunchKernelGGL(k_dyn_row<false>, dim3(g->h, nframes, S), dim3(row_threads(g->w)),
                        row_lds_bytes(g->w, mbw), hs, st, nal, ld_nal, pend, dfr, ld_fr, *g, x->rows, src, refs,
-                       x->meta, x->body_lo, x->body_hi, x->tcx, epoch, x->rowstage, x->gbits, stamps);
+                       x->meta, x->body_lo, x->body_hi, x->tcx, epoch, x->rowstage, x->gbits, x->spill, x->ctr,
+                       stamps);
     if (hipGetLastError() != hipSuccess) return -1;
     hipLaunchKernelGGL(k_dyn_row<true>, dim3(g->h, nframes, S), dim3(row_threads(g->w)),
                        row_lds_bytes(g->w, mbw), hs, st, nal, ld_nal, pend, dfr, ld_fr, *g, x->rows, src, refs,
-                       x->meta, x->body_lo, x->body_hi, x->tcx, epoch, x->rowstage, x->gbits, stamps);
+                       x->meta, x->body_lo, x->body_hi, x->tcx, epoch, x->rowstage, x->gbits, x->spill, x->ctr,
+                       stamps);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -2558,11 +2704,12 @@ void dyn_rowstage_geom(DynGeom *g, int mbw, int mbh)
     auto words = [](uint64_t bits) { return (uint32_t)((((bits + 31) / 32) + 63) & ~(uint64_t)63); };
     /* + the group's EP-candidate record (EPC_ROW / EPC_STATIC words) at the slot end */
     g->rs_static_words = words((uint64_t)HDR_MAX + (uint64_t)maxrows * mbw * (HEAD_MAX + 1) + 64) + EPC_STATIC;
-    g->rs_row_words = words((uint64_t)mbw * (HEAD_MAX + 1) + (uint64_t)g->w * MB_BITS_MAX + 64) + EPC_ROW;
-#ifdef SCROLL_RS_SMALL
-    g->rs_static_words = g->rs_static_words < 4096 ? g->rs_static_words : 4096;   /* timing experiment only */
-    g->rs_row_words = g->rs_row_words < 4096 ? g->rs_row_words : 4096;
-#endif
+    /* a rect row's slot holds a typical row (SCROLL_DYN_ROW_KBITS per MB, ~2.5x
+     * the synthetic source's mean); rows past it take a spill slot at the
+     * provable bound (k_dyn_row) */
+    g->rs_spill_words = words((uint64_t)mbw * (HEAD_MAX + 1) + (uint64_t)g->w * MB_BITS_MAX + 64) + EPC_ROW;
+    g->rs_row_words = words((uint64_t)mbw * (HEAD_MAX + 1) + (uint64_t)g->w * SCROLL_DYN_ROW_KBITS + 64) + EPC_ROW;
+    if (g->rs_row_words > g->rs_spill_words) g->rs_row_words = g->rs_spill_words;
     g->rs_frame_words = (uint64_t)(g->ngroups - g->h) * g->rs_static_words + (uint64_t)g->h * g->rs_row_words;
 }
 

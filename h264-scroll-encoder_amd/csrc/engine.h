@@ -36,7 +36,8 @@ typedef struct {
     int32_t frames_written;       /* Composer::frames_written analogue          */
     int32_t n_slow;               /* NALs routed to the serial device path      */
     uint64_t batch_bytes;         /* bytes appended by this batch               */
-    uint32_t pad[20];
+    uint64_t undelivered;         /* arena bytes not yet packed to the host (output_to_host) */
+    uint32_t pad[18];
 } DevStream;
 
 /* One planned NAL unit (32 bytes). */
@@ -89,6 +90,9 @@ typedef struct {
 #define DYN_STATIC_ROWS 64          /* MB rows per static k_dyn_group row group (4 measured slower) */
 #define DYN_PIECES 26               /* coded pieces per dynamic MB: 16 luma, 2 DC, 8 AC */
 #define DYN_OVF_BYTES 8192          /* staging-slot tail: levels of > 128-bit blocks */
+#ifndef SCROLL_DYN_ROW_KBITS
+#define SCROLL_DYN_ROW_KBITS 1280   /* rect-row slot bits per MB (typical; more: a spill slot) */
+#endif
 typedef struct {
     int32_t x0, y0, w, h;           /* rect, MB units                             */
     int32_t ngroups;                /* k_dyn_group row groups per NAL (dyn_groups) */
@@ -99,6 +103,10 @@ typedef struct {
     uint32_t rs_static_words;       /* row-stage words per static row group       */
     uint32_t rs_row_words;          /* row-stage words per rect row               */
     uint64_t rs_frame_words;        /* row-stage words per frame (all row groups) */
+    uint32_t rs_spill_words;        /* a spill slot: one rect row at its provable bound */
+    uint32_t rs_spill_cap;          /* spill slots after the frames' regions       */
+    uint32_t gen_cap;               /* general-path record slots (NALs)           */
+    uint32_t pad_g;
 } DynGeom;
 
 /* hints of one composed frame: rects [first, first + n) of the batch's rect

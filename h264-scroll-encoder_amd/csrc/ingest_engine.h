@@ -8,6 +8,8 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include "engine.h"
+
 #define ING_SC_MAX 64               /* 00 00 01 patterns kept per reference file */
 
 enum {
@@ -39,3 +41,10 @@ typedef struct {
 int ingest_launch(hipStream_t hs, const uint8_t *in, const IngestFile *files, int nstreams,
                   uint64_t max_file, IngestScan *scan, IngestOut *outs, uint8_t *arena,
                   uint64_t ld_arena, uint64_t cap, int first_stream);
+
+/* mid-stream long-term reference updates (k_ing_update): files[k] -> a
+ * non-IDR I frame of stream ups[2 k] marked long-term ups[2 k + 1],
+ * appended at its cursor (streams distinct).  0, or -1 when a launch failed. */
+int update_launch(hipStream_t hs, const uint8_t *in, const IngestFile *files, int n, uint64_t max_file,
+                  IngestScan *scan, const int32_t *ups, IngestOut *outs, DevStream *st, uint8_t *arena,
+                  uint64_t ld_arena);

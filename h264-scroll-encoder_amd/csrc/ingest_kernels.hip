@@ -30,6 +30,7 @@
 
 #include <stdint.h>
 
+#include "engine.h"
 #include "ingest_engine.h"
 #include "scroll_device.h"
 #include "stage_util.h"
@@ -631,7 +632,136 @@ __global__ __launch_bounds__(DT) void k_ing_stream(const uint8_t *__restrict__ i
     }
 }
 
+/* ---------------------------------------------------------------------- */
+/* k_ing_update: mid-stream long-term reference ("atlas") updates          */
+/* ---------------------------------------------------------------------- */
+/* One workgroup per update of a live stream: the file's first SPS / PPS /
+ * IDR (parse_reference_file's rules), the IDR slice parsed with the file's
+ * own SPS / PPS (composer_init, composer.c:127-196), rewritten as a non-IDR I
+ * frame with the STREAM's write config -- h264_rewrite_as_non_idr_i_frame
+ * (h264_writer.c:296-350) with long_term_frame_idx `which` at the stream's
+ * frame_num (mod 2^log2_max_frame_num, POC lsb 2 frame_num as the waypoint
+ * frames, :683-687) -- appended at the stream's cursor.  Its MMCO 4
+ * (max_long_term_frame_idx_plus1 2) drops the waypoints: the stream's
+ * waypoint table empties and frame_num advances (:779-781).  Bits:
+ * oracle/scroll_oracle.c or_update_ref. */
+__device__ void update_header(SmallBits &b, const DevStream &S, int fn, int which, const SliceHdr &h)
+{
+    b.clear();
+    put_ue(b, 0);
+    put_ue(b, 7);                                          /* SLICE_TYPE_I_ALL */
+    put_ue(b, 0);
+    b.put((uint32_t)fn, S.log2_mfn);
+    if (S.poc_type == 0) b.put((uint32_t)(2 * fn), S.log2_poc);
+    b.put(1, 1);                                           /* adaptive_ref_pic_marking_mode_flag */
+    put_ue(b, 4);
+    put_ue(b, 2);
+    put_ue(b, 6);
+    put_ue(b, (uint32_t)which);
+    put_ue(b, 0);
+    put_se(b, h.qpd);
+    if (S.deblock) {
+        put_ue(b, h.dbf);
+        if (h.dbf != 1) {
+            put_se(b, h.alpha);
+            put_se(b, h.beta);
+        }
+    }
+}
+
+__global__ __launch_bounds__(DT) void k_ing_update(const uint8_t *__restrict__ in,
+                                                   const IngestFile *__restrict__ files,
+                                                   const IngestScan *__restrict__ scan,
+                                                   const int32_t *__restrict__ ups,
+                                                   IngestOut *__restrict__ outs,
+                                                   DevStream *__restrict__ st,
+                                                   uint8_t *__restrict__ arena, uint64_t ld_arena)
+{
+    __shared__ IngLds L;
+    __shared__ uint64_t s_at;
+    const int k = blockIdx.x, t = threadIdx.x;
+    const int s = ups[2 * k], which = ups[2 * k + 1];
+    DevStream *S = st + s;
+    uint8_t *A = arena + (size_t)s * ld_arena;
+    const uint8_t *d = in + files[k].off;
+    const uint64_t n = files[k].size;
+    if (t == 0) {
+        L.err = ING_OK;
+        const int np = (int)scan[k].n;
+        if (np > ING_SC_MAX) {
+            L.err = ING_ERR_NALS;
+        } else {
+            for (int q = 0; q < np; ++q) L.pos[0][q] = scan[k].pos[q];
+            int nref, dbf;
+            if (walk_nals(d, n, L.pos[0], np, L.sps[0], L.pps[0], L.idr[0])) L.err = ING_ERR_MISSING;
+            else if (parse_sps(d + L.sps[0].off, L.sps[0].n, L.si[0]) ||
+                     parse_pps(d + L.pps[0].off, L.pps[0].n, nref, dbf))
+                L.err = ING_ERR_PARSE;
+            else if (L.si[0].w != S->w || L.si[0].h != S->h)
+                L.err = ING_ERR_DIMS;
+            else {
+                parse_idr(d + L.idr[0].off, L.idr[0].n, L.si[0], dbf, L.sh[0]);
+                const int fn = S->frame_num & ((1 << S->log2_mfn) - 1);
+                update_header(L.hdr[0], *S, fn, which, L.sh[0]);
+                EbspReader r;
+                r.init(d + L.idr[0].off, L.idr[0].n);
+                for (uint64_t q = 0; q < L.sh[0].mb_start; ++q) r.u1();
+                SmallBits pb = L.hdr[0];
+                const int npre = (pb.n + 7) >> 3;
+                while (pb.n < 8 * npre && !r.eof) {
+                    const uint32_t bit = r.u1();
+                    if (r.eof) break;
+                    pb.put(bit, 1);
+                }
+                for (int q = 0; q < npre; ++q) L.pre[0][q] = (uint8_t)pb.byte(q);
+            }
+        }
+        s_at = S->out_pos;
+    }
+    __syncthreads();
+    IngestOut &o = outs[k];
+    if (L.err != ING_OK) {
+        if (t == 0) {
+            o.err = L.err;
+            o.bytes = 0;
+        }
+        return;
+    }
+    const uint64_t at0 = s_at;
+    bool over = false;
+    const uint64_t at = stream_slice(L, d + L.idr[0].off, L.idr[0].n, L.hdr[0], L.pre[0], L.sh[0].mb_start, 3, 1,
+                                     A, at0, S->out_cap, over);
+    if (t == 0) {
+        o.err = over ? ING_ERR_OVERFLOW : ING_OK;
+        o.bytes = over ? 0 : at - at0;
+        o.w = L.si[0].w;
+        o.h = L.si[0].h;
+        if (!over) {                                       /* commit */
+            S->out_pos = at;
+            S->undelivered += at - at0;
+            S->frame_num += 1;
+            S->nwp = 0;
+            for (int q = 0; q < 8; ++q) S->wp_valid[q] = 0;
+        }
+    }
+}
+
 }  // namespace
+
+int update_launch(hipStream_t hs, const uint8_t *in, const IngestFile *files, int n, uint64_t max_file,
+                  IngestScan *scan, const int32_t *ups, IngestOut *outs, DevStream *st, uint8_t *arena,
+                  uint64_t ld_arena)
+{
+    if (n <= 0) return 0;
+    if (hipMemsetAsync(scan, 0, sizeof(IngestScan) * (size_t)n, hs) != hipSuccess) return -1;
+    const uint32_t gx = (uint32_t)((max_file + WINB - 1) / WINB);
+    if (gx > 0) {
+        hipLaunchKernelGGL(k_ing_scan, dim3(gx, n), dim3(DT), 0, hs, in, files, scan);
+        if (hipGetLastError() != hipSuccess) return -1;
+    }
+    hipLaunchKernelGGL(k_ing_update, dim3(n), dim3(DT), 0, hs, in, files, scan, ups, outs, st, arena, ld_arena);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
 
 int ingest_launch(hipStream_t hs, const uint8_t *in, const IngestFile *files, int nstreams,
                   uint64_t max_file, IngestScan *scan, IngestOut *outs, uint8_t *arena,

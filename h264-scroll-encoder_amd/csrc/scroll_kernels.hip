@@ -117,7 +117,9 @@ __global__ __launch_bounds__(PLAN_THREADS) void k_plan(DevStream *__restrict__ s
                                                        int ld_off, NalDesc *__restrict__ nal,
                                                        int ld_nal, int nframes, int mode,
                                                        int flags, PlanPending *__restrict__ pend,
-                                                       DynFrame *__restrict__ dfr, int ld_fr)
+                                                       DynFrame *__restrict__ dfr, int ld_fr,
+                                                       const uint32_t *__restrict__ pool_ctr = nullptr,
+                                                       uint32_t spill_cap = 0, uint32_t gen_cap = 0)
 {
     const int s = blockIdx.x;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -139,7 +141,15 @@ __global__ __launch_bounds__(PLAN_THREADS) void k_plan(DevStream *__restrict__ s
         s_cfg[4] = S->log2_poc; s_cfg[5] = S->deblock; s_cfg[6] = S->frame_num; s_cfg[7] = S->nwp;
         s_carry = 0;
         s_nslow = 0;
-        if ((flags & PLAN_REWIND) && !(flags & PLAN_STATE)) S->out_pos = 0;
+        if ((flags & PLAN_REWIND) && !(flags & PLAN_STATE)) {
+            S->out_pos = 0;
+            S->undelivered = 0;
+        }
+        /* the dynamic rect ran out of a scratch pool somewhere in this
+         * compose: no stream commits, so the same compose can be retried
+         * once the batch has grown its pools */
+        if ((flags & PLAN_SIZE) && pool_ctr && (pool_ctr[0] > spill_cap || pool_ctr[1] > gen_cap))
+            S->err |= SCROLL_DEVERR_DYN;
     }
     const int F = nframes >= 0 ? nframes : S->frames;
     NalDesc *N = nal + (size_t)s * ld_nal;
@@ -330,6 +340,7 @@ __global__ __launch_bounds__(PLAN_THREADS) void k_plan(DevStream *__restrict__ s
         } else {
             S->out_pos = out0 + total;
             S->batch_bytes = total;
+            S->undelivered += total;
             S->nnal = nnal;
             S->nal_wp = s_nalwp;
             S->frame_num = s_fn_end;
@@ -962,6 +973,13 @@ struct ScrollBatch {
     int ipcm_n = 0;
     double ing_ms = 0.0;
     int ing_n = 0;
+    /* host delivery: per-stream (offset, bytes) table of the last packing */
+    int dyn_grow = 0;                  /* the dynamic rect's pools at their bounds (after running out) */
+    int32_t *d_upd = nullptr;          /* reference updates: (stream, which) per entry */
+    size_t upd_cap = 0;
+    uint64_t *d_out_tab = nullptr;
+    size_t out_tab_cap = 0;
+    hipEvent_t out_ev = nullptr;
 };
 
 /* event pairs of one compose.  Dynamic rect: plan = [0,1) + [2,3), dyn
@@ -1077,6 +1095,9 @@ void scroll_batch_destroy(ScrollBatch *b)
     (void)hipFree(b->d_off);
     (void)hipFree(b->d_nal);
     (void)hipFree(b->d_arena);
+    (void)hipFree(b->d_out_tab);
+    (void)hipFree(b->d_upd);
+    if (b->out_ev) (void)hipEventDestroy(b->out_ev);
     (void)hipFree(b->d_pend);
     (void)hipFree(b->d_dfr);
     (void)hipFree(b->d_src);
@@ -1108,6 +1129,8 @@ int scroll_batch_set_debug(ScrollBatch *b, int flags)
     b->debug = flags;
     return SCROLL_OK;
 }
+
+static int dyn_grow_pools(ScrollBatch *b);
 
 static int batch_host_sync(ScrollBatch *b)
 {
@@ -1322,14 +1345,12 @@ static int launch(ScrollBatch *b, int nframes, int plan_mode, int nal_max, hipSt
             }
             const DynGeom &G = b->geo;
             const size_t nalw = (size_t)G.w * G.h, ng = (size_t)G.ngroups;
+            HIPCHK(hipMemsetAsync(b->dx.ctr, 0, 2 * sizeof(uint32_t), hs));   /* spill / record slots */
             for (int c = 0; c < nch; ++c) {
                 const int s0 = (int)((int64_t)S * c / nch), s1 = (int)((int64_t)S * (c + 1) / nch);
                 const size_t nb0 = (size_t)s0 * ld_fr;
                 DynScratch xc = b->dx;
                 xc.rows = b->dx.rows + nb0 * 32 * G.h;
-                xc.meta = b->dx.meta + nb0 * DYN_PIECES * nalw;
-                xc.body_lo = b->dx.body_lo + nb0 * DYN_PIECES * nalw;
-                xc.body_hi = b->dx.body_hi + nb0 * DYN_PIECES * nalw;
                 xc.tcx = b->dx.tcx + nb0 * nalw;
                 xc.rowstage = b->dx.rowstage + nb0 * G.rs_frame_words;
                 xc.gbits = b->dx.gbits + nb0 * ng;
@@ -1369,7 +1390,8 @@ static int launch(ScrollBatch *b, int nframes, int plan_mode, int nal_max, hipSt
         hipLaunchKernelGGL(k_plan, dim3(S), dim3(PLAN_THREADS), 0, hs, b->d_st, b->d_off,
                            b->max_frames, b->d_nal, b->ld_nal, nframes, plan_mode,
                            b->debug | plan_flags | PLAN_SIZE | PLAN_DYN, b->d_pend, b->d_dfr,
-                           ld_fr);
+                           ld_fr, (b->dyn_on && !b->hint_on) ? (const uint32_t *)b->dx.ctr : nullptr,
+                           b->geo.rs_spill_cap, b->geo.gen_cap);
         HIPCHK(hipGetLastError());
         if ((rc = mark(3))) return rc;
     }
@@ -1489,8 +1511,23 @@ int scroll_batch_sync(ScrollBatch *b)
                     "(ref 2 + i needs waypoint i)", s);
             rc = SCROLL_ERR_CONFIG;
         } else if (rc == SCROLL_OK && (b->h_st[s].err & SCROLL_DEVERR_DYN)) {
-            set_err("stream %d: a staged NAL outgrew its staging slot (%llu bytes)", s,
-                    (unsigned long long)b->geo.slot_bytes);
+            uint32_t used[2] = {0, 0};
+            if (b->dyn_on && !b->hint_on && b->dx.ctr)
+                HIPCHK(hipMemcpy(used, b->dx.ctr, sizeof(used), hipMemcpyDeviceToHost));
+            if (used[0] > b->geo.rs_spill_cap || used[1] > b->geo.gen_cap) {
+                /* content past the typical-size pools: grow them to their
+                 * bound for the next compose (this one committed nothing for
+                 * the stream) */
+                const int grc = dyn_grow_pools(b);
+                set_err("stream %d: the dynamic rect's %s pool ran out (%u of %u); %s", s,
+                        used[0] > b->geo.rs_spill_cap ? "row-stage spill" : "general-path record",
+                        used[0] > b->geo.rs_spill_cap ? used[0] : used[1],
+                        used[0] > b->geo.rs_spill_cap ? b->geo.rs_spill_cap : b->geo.gen_cap,
+                        grc ? "growing it failed" : "grown: compose again");
+            } else {
+                set_err("stream %d: a staged NAL outgrew its staging slot (%llu bytes)", s,
+                        (unsigned long long)b->geo.slot_bytes);
+            }
             rc = SCROLL_ERR_OVERFLOW;
         } else if (rc == SCROLL_OK) {
             set_err("stream %d: output arena overflow (%llu bytes used, capacity %llu)", s,
@@ -1527,6 +1564,139 @@ int scroll_batch_copy_output(ScrollBatch *b, int s, size_t from, uint8_t *dst, s
     return SCROLL_OK;
 }
 
+/* ------------------------ host delivery (PCIe) ----------------------------- */
+/* The reference hands its bytes over in host memory (composer.c:255-291).
+ * scroll_batch_output_to_host_async packs the bytes appended to every stream
+ * since its previous delivery (DevStream.undelivered) into pinned host memory, device-side and asynchronously: one
+ * workgroup scans the streams' byte counts (16-byte aligned offsets) into the
+ * host table, then every stream's bytes are read from its arena and stored
+ * straight into the pinned buffer by (8, S) workgroups of 16-byte chunks --
+ * no host sync between the compose and the copy, and the host never needs
+ * the sizes before the bytes land. */
+namespace {
+constexpr int OUT_Z = 8;
+__global__ __launch_bounds__(1024) void k_out_table(DevStream *__restrict__ st, int S, uint64_t cap,
+                                                    uint64_t *__restrict__ dtab, uint64_t *__restrict__ htab)
+{
+    __shared__ uint64_t s_w[16], s_carry;
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    if (t == 0) s_carry = 0;
+    __syncthreads();
+    for (int s0 = 0; s0 < S; s0 += 1024) {
+        const int s = s0 + t;
+        const uint64_t n = s < S ? st[s].undelivered : 0, a = (n + 15) & ~(uint64_t)15;
+        const uint64_t inc = wave_incl_scan(a, lane);
+        if (lane == 63) s_w[wave] = inc;
+        __syncthreads();
+        uint64_t before = s_carry;
+        for (int w = 0; w < wave; ++w) before += s_w[w];
+        if (s < S) {
+            dtab[1 + 2 * (size_t)s] = htab[1 + 2 * (size_t)s] = before + inc - a;
+            dtab[2 + 2 * (size_t)s] = htab[2 + 2 * (size_t)s] = n;
+        }
+        __syncthreads();
+        if (t == 0)
+            for (int w = 0; w < 16; ++w) s_carry += s_w[w];
+        __syncthreads();
+    }
+    if (t == 0) {
+        /* total: its aligned size, or ~0 when it does not fit (nothing copied,
+         * the bytes stay undelivered) */
+        const uint64_t tot = s_carry <= cap ? s_carry : ~(uint64_t)0;
+        dtab[0] = htab[0] = tot;
+    }
+    if (s_carry <= cap)
+        for (int s = t; s < S; s += 1024) st[s].undelivered = 0;
+}
+
+/* grid (OUT_Z, S): stream s's last-compose bytes -> dst + its offset, one
+ * 16-byte chunk per thread and iteration: two aligned arena loads and a
+ * byte funnel shift (bytes past n are don't-care: the table has n) */
+__global__ __launch_bounds__(256) void k_out_copy(const DevStream *__restrict__ st, const uint8_t *__restrict__ arena,
+                                                  uint64_t ld_arena, uint64_t arena_end,
+                                                  const uint64_t *__restrict__ dtab, uint8_t *__restrict__ dst)
+{
+    const int s = blockIdx.y;
+    if (dtab[0] == ~(uint64_t)0) return;
+    const uint64_t n = dtab[2 + 2 * (size_t)s], o = dtab[1 + 2 * (size_t)s];
+    const uint64_t from = (uint64_t)s * ld_arena + st[s].out_pos - n;   /* arena byte of the first new byte */
+    uint4 *d = reinterpret_cast<uint4 *>(dst + o);
+    const uint32_t q = (uint32_t)(from & 15u) >> 2, rb = (uint32_t)from & 3u;
+    const uint64_t base = from & ~(uint64_t)15;
+    const uint4 *a = reinterpret_cast<const uint4 *>(arena + base);
+    const uint64_t nch = (n + 15) / 16;
+    for (uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x; j < nch; j += (uint64_t)OUT_Z * 256) {
+        const uint4 x = a[j];
+        const uint4 y = (q | rb) && base + 16 * (j + 2) <= arena_end ? a[j + 1] : x;
+        const uint32_t w0 = x.x, w1 = x.y, w2 = x.z, w3 = x.w, w4 = y.x, w5 = y.y, w6 = y.z, w7 = y.w;
+        /* word k of the output = bytes 4 (q + k) + rb .. of w[] */
+        auto pick = [&](uint32_t i) -> uint32_t {        /* w[i], i <= 7, by selects */
+            const uint32_t lo = i & 1u ? (i & 2u ? w3 : w1) : (i & 2u ? w2 : w0);
+            const uint32_t hi = i & 1u ? (i & 2u ? w7 : w5) : (i & 2u ? w6 : w4);
+            return i & 4u ? hi : lo;
+        };
+        uint32_t o4[4];
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k) {
+            const uint32_t lo = pick(q + k), hi = pick(q + k + 1u);
+            o4[k] = rb ? __builtin_amdgcn_alignbyte(hi, lo, rb) : lo;
+        }
+        d[j] = make_uint4(o4[0], o4[1], o4[2], o4[3]);
+    }
+}
+}  // namespace
+
+int scroll_host_alloc(void **p, size_t n)
+{
+    if (!p) return SCROLL_ERR_ARG;
+    *p = nullptr;
+    hipError_t e = hipHostMalloc(p, n ? n : 1, hipHostMallocDefault);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        set_err("scroll_host_alloc(%zu): %s", n, hipGetErrorString(e));
+        return e == hipErrorOutOfMemory ? SCROLL_ERR_OOM : SCROLL_ERR_HIP;
+    }
+    return SCROLL_OK;
+}
+
+void scroll_host_free(void *p)
+{
+    if (p) (void)hipHostFree(p);
+}
+
+int scroll_batch_output_to_host_async(ScrollBatch *b, uint8_t *dst, size_t cap, uint64_t *table, void *hip_stream)
+{
+    if (!b || !dst || !table || (cap & 15) || (reinterpret_cast<uintptr_t>(dst) & 15)) {
+        set_err("scroll_batch_output_to_host_async: bad arguments (dst / cap must be 16-byte aligned)");
+        return SCROLL_ERR_ARG;
+    }
+    HIPCHK(hipSetDevice(b->device));
+    hipStream_t hs = hip_stream ? (hipStream_t)hip_stream : (b->last ? b->last : b->own);
+    if (b->last && hs != b->last) {                 /* after the last compose */
+        if (!b->out_ev) HIPCHK(hipEventCreateWithFlags(&b->out_ev, hipEventDisableTiming));
+        HIPCHK(hipEventRecord(b->out_ev, b->last));
+        HIPCHK(hipStreamWaitEvent(hs, b->out_ev, 0));
+    }
+    const size_t S = (size_t)b->nstreams;
+    if (b->out_tab_cap < 1 + 2 * S) {
+        (void)hipFree(b->d_out_tab);
+        b->d_out_tab = nullptr;
+        b->out_tab_cap = 0;
+        HIPCHK(hipMalloc(&b->d_out_tab, (1 + 2 * S) * sizeof(uint64_t)));
+        b->out_tab_cap = 1 + 2 * S;
+    }
+    hipLaunchKernelGGL(k_out_table, dim3(1), dim3(1024), 0, hs, b->d_st, (int)S, (uint64_t)cap, b->d_out_tab,
+                       table);
+    HIPCHK(hipGetLastError());
+    if (S) {
+        hipLaunchKernelGGL(k_out_copy, dim3(OUT_Z, (unsigned)S), dim3(256), 0, hs, b->d_st, b->d_arena,
+                           (uint64_t)b->ld_arena, (uint64_t)b->max_streams * b->ld_arena, b->d_out_tab, dst);
+        HIPCHK(hipGetLastError());
+    }
+    b->last = hs;
+    return SCROLL_OK;
+}
+
 const uint8_t *scroll_batch_output_device(ScrollBatch *b, int s)
 {
     if (!b || s < 0 || s >= b->nstreams) return nullptr;
@@ -1538,7 +1708,7 @@ int scroll_batch_reset_output(ScrollBatch *b)
     if (!b) return SCROLL_ERR_ARG;
     int rc = batch_host_sync(b);
     if (rc) return rc;
-    for (int s = 0; s < b->nstreams; ++s) b->h_st[s].out_pos = 0;
+    for (int s = 0; s < b->nstreams; ++s) b->h_st[s].out_pos = b->h_st[s].undelivered = 0;
     HIPCHK(hipSetDevice(b->device));
     HIPCHK(hipMemcpy(b->d_st, b->h_st, (size_t)b->nstreams * sizeof(DevStream),
                      hipMemcpyHostToDevice));
@@ -1654,6 +1824,7 @@ static void dyn_release(ScrollBatch *b)
     (void)hipFree(b->dx.body_hi);
     (void)hipFree(b->dx.tcx);
     (void)hipFree(b->dx.rowstage);
+    (void)hipFree(b->dx.ctr);
     (void)hipFree(b->dx.gbits);
     b->d_src = b->d_refs = nullptr;
     b->dx = DynScratch{};
@@ -1738,13 +1909,30 @@ int scroll_batch_set_dyn_rect(ScrollBatch *b, int x0, int y0, int w, int h, size
     if (e == hipSuccess) e = hipMalloc(&b->d_src, S * g.src_ld);
     if (e == hipSuccess) e = hipMalloc(&b->d_refs, S * dyn_pair_bytes(b));
     if (e == hipSuccess) e = hipMalloc(&b->dx.rows, S * F * 32 * h * sizeof(uint32_t));
-    if (e == hipSuccess) e = hipMalloc(&b->dx.meta, S * F * DYN_PIECES * w * h * sizeof(uint16_t));
-    if (e == hipSuccess) e = hipMalloc(&b->dx.body_lo, S * F * DYN_PIECES * w * h * sizeof(uint2));
-    if (e == hipSuccess) e = hipMalloc(&b->dx.body_hi, S * F * DYN_PIECES * w * h * sizeof(uint2));
+    /* scratch sized for typical content: general-path record
+     * slots for 1/64 of the frames (those NALs need half-pel chroma steps the
+     * composer's own waypoints never make), spill slots for 1/32 of the rect
+     * rows; a compose that runs out fails the frames concerned with
+     * SCROLL_ERR_OVERFLOW and the next compose has pools at their bound */
+    g.gen_cap = (uint32_t)std::min(S * F, std::max<size_t>(32, S * F / 64));
+    g.rs_spill_cap = g.rs_row_words < g.rs_spill_words
+                         ? (uint32_t)std::min(S * F * (size_t)h, std::max<size_t>(2048, S * F * (size_t)h / 32))
+                         : 0u;
+    if (b->dyn_grow) {                 /* pools at their bounds (ran out before) */
+        g.gen_cap = (uint32_t)(S * F);
+        if (g.rs_spill_cap) g.rs_spill_cap = (uint32_t)(S * F * (size_t)h);
+    }
+    const size_t nrec = (size_t)g.gen_cap * DYN_PIECES * w * h;
+    if (e == hipSuccess) e = hipMalloc(&b->dx.meta, nrec * sizeof(uint16_t));
+    if (e == hipSuccess) e = hipMalloc(&b->dx.body_lo, nrec * sizeof(uint2));
+    if (e == hipSuccess) e = hipMalloc(&b->dx.body_hi, nrec * sizeof(uint2));
     const size_t ng = (size_t)g.ngroups;
     if (e == hipSuccess) e = hipMalloc(&b->dx.tcx, S * F * w * h * sizeof(unsigned long long));
     if (e == hipSuccess) e = hipMemset(b->dx.tcx, 0, S * F * w * h * sizeof(unsigned long long));
-    if (e == hipSuccess) e = hipMalloc(&b->dx.rowstage, S * F * g.rs_frame_words * sizeof(uint32_t));
+    const size_t rs_words = S * F * g.rs_frame_words + (size_t)g.rs_spill_cap * g.rs_spill_words;
+    if (e == hipSuccess) e = hipMalloc(&b->dx.rowstage, rs_words * sizeof(uint32_t));
+    if (e == hipSuccess) b->dx.spill = b->dx.rowstage + S * F * g.rs_frame_words;
+    if (e == hipSuccess) e = hipMalloc(&b->dx.ctr, 2 * sizeof(uint32_t));
     if (e == hipSuccess) e = hipMalloc(&b->dx.gbits, S * F * ng * sizeof(uint32_t));
     b->dx.epoch = 0;
     if (e == hipSuccess) e = hipMemset(b->d_src, 0, S * g.src_ld);
@@ -1791,6 +1979,48 @@ int scroll_batch_set_dyn_rect_at(ScrollBatch *b, int s, int f, int x0, int y0)
     if (x0 != b->geo.x0 || (x0 >= 0 && y0 != b->geo.y0)) b->dyn_pos_custom = 1;
     b->hd_dirty = 1;
     b->hint_dirty = 1;
+    return SCROLL_OK;
+}
+
+/* the general-path record pool and the row-stage spill pool at their
+ * bounds (a slot for every NAL / rect row), keeping source and references */
+static int dyn_grow_pools(ScrollBatch *b)
+{
+    if (!b->dyn_on || b->dyn_grow) return SCROLL_OK;
+    HIPCHK(hipSetDevice(b->device));
+    DynGeom g = b->geo;
+    const size_t S = (size_t)b->max_streams, F = (size_t)b->max_frames, nmb = (size_t)g.w * g.h;
+    g.gen_cap = (uint32_t)(S * F);
+    if (g.rs_spill_cap) g.rs_spill_cap = (uint32_t)(S * F * (size_t)g.h);
+    const size_t nrec = (size_t)g.gen_cap * DYN_PIECES * nmb;
+    const size_t rs_words = S * F * g.rs_frame_words + (size_t)g.rs_spill_cap * g.rs_spill_words;
+    uint16_t *meta = nullptr;
+    uint2 *lo = nullptr, *hi = nullptr;
+    uint32_t *rs = nullptr;
+    hipError_t e = hipMalloc(&meta, nrec * sizeof(uint16_t));
+    if (e == hipSuccess) e = hipMalloc(&lo, nrec * sizeof(uint2));
+    if (e == hipSuccess) e = hipMalloc(&hi, nrec * sizeof(uint2));
+    if (e == hipSuccess) e = hipMalloc(&rs, rs_words * sizeof(uint32_t));
+    if (e != hipSuccess) {
+        (void)hipFree(meta);
+        (void)hipFree(lo);
+        (void)hipFree(hi);
+        (void)hipFree(rs);
+        (void)hipGetLastError();
+        return e == hipErrorOutOfMemory ? SCROLL_ERR_OOM : SCROLL_ERR_HIP;
+    }
+    (void)hipFree(b->dx.meta);
+    (void)hipFree(b->dx.body_lo);
+    (void)hipFree(b->dx.body_hi);
+    (void)hipFree(b->dx.rowstage);
+    b->dx.meta = meta;
+    b->dx.body_lo = lo;
+    b->dx.body_hi = hi;
+    b->dx.rowstage = rs;
+    b->dx.spill = rs + S * F * g.rs_frame_words;
+    b->geo.gen_cap = g.gen_cap;
+    b->geo.rs_spill_cap = g.rs_spill_cap;
+    b->dyn_grow = 1;
     return SCROLL_OK;
 }
 
@@ -2634,6 +2864,113 @@ int scroll_batch_ingest(ScrollBatch *b, int n, const uint8_t *const *ref_a, cons
         if (nb[k]) HIPCHK(hipMemcpy(b->d_ing_in + desc[4 * k + 2], ref_b[k], nb[k], hipMemcpyHostToDevice));
     }
     return scroll_batch_ingest_device(b, n, b->d_ing_in, desc.data(), first);
+}
+
+/* mid-stream long-term reference updates (k_ing_update, ingest_kernels.hip) */
+int scroll_batch_update_refs_device(ScrollBatch *b, int n, const int *streams, const int *which,
+                                    const uint8_t *d_files, const uint64_t *desc, int *status)
+{
+    if (!b || n < 0 || (n > 0 && (!streams || !which || !d_files || !desc))) return SCROLL_ERR_ARG;
+    std::vector<uint8_t> seen((size_t)b->nstreams, 0);
+    for (int k = 0; k < n; ++k) {
+        if (streams[k] < 0 || streams[k] >= b->nstreams || which[k] < 0 || which[k] > 1 || seen[streams[k]]) {
+            set_err("scroll_batch_update_refs: entry %d: bad or repeated stream / which", k);
+            return SCROLL_ERR_ARG;
+        }
+        seen[streams[k]] = 1;
+    }
+    if (n == 0) return SCROLL_OK;
+    HIPCHK(hipSetDevice(b->device));
+    if (n > b->ing_cap) {
+        (void)hipFree(b->d_ing_files);
+        (void)hipFree(b->d_ing_scan);
+        (void)hipFree(b->d_ing_out);
+        b->d_ing_files = nullptr;
+        b->d_ing_scan = nullptr;
+        b->d_ing_out = nullptr;
+        b->ing_cap = 0;
+        hipError_t e = hipMalloc(&b->d_ing_files, 2 * (size_t)n * sizeof(IngestFile));
+        if (e == hipSuccess) e = hipMalloc(&b->d_ing_scan, 2 * (size_t)n * sizeof(IngestScan));
+        if (e == hipSuccess) e = hipMalloc(&b->d_ing_out, (size_t)n * sizeof(IngestOut));
+        if (e != hipSuccess) {
+            set_err("scroll_batch_update_refs: %s", hipGetErrorString(e));
+            return e == hipErrorOutOfMemory ? SCROLL_ERR_OOM : SCROLL_ERR_HIP;
+        }
+        b->ing_cap = n;
+    }
+    if ((size_t)n > b->upd_cap) {
+        (void)hipFree(b->d_upd);
+        b->d_upd = nullptr;
+        b->upd_cap = 0;
+        HIPCHK(hipMalloc(&b->d_upd, 2 * (size_t)n * sizeof(int32_t)));
+        b->upd_cap = (size_t)n;
+    }
+    std::vector<IngestFile> files((size_t)n);
+    std::vector<int32_t> ups(2 * (size_t)n);
+    uint64_t maxf = 0;
+    for (int k = 0; k < n; ++k) {
+        files[k].off = desc[2 * k];
+        files[k].size = desc[2 * k + 1];
+        maxf = std::max(maxf, files[k].size);
+        ups[2 * k] = streams[k];
+        ups[2 * k + 1] = which[k];
+    }
+    hipStream_t hs = b->last ? b->last : b->own;   /* after the pending composes */
+    HIPCHK(hipMemcpyAsync(b->d_ing_files, files.data(), files.size() * sizeof(IngestFile),
+                          hipMemcpyHostToDevice, hs));
+    HIPCHK(hipMemcpyAsync(b->d_upd, ups.data(), ups.size() * sizeof(int32_t), hipMemcpyHostToDevice, hs));
+    if (update_launch(hs, d_files, b->d_ing_files, n, maxf, b->d_ing_scan, b->d_upd, b->d_ing_out, b->d_st,
+                      b->d_arena, (uint64_t)b->ld_arena)) {
+        set_err("reference update launch: %s", hipGetErrorString(hipGetLastError()));
+        return SCROLL_ERR_HIP;
+    }
+    std::vector<IngestOut> outs((size_t)n);
+    HIPCHK(hipMemcpyAsync(outs.data(), b->d_ing_out, outs.size() * sizeof(IngestOut), hipMemcpyDeviceToHost, hs));
+    HIPCHK(hipStreamSynchronize(hs));
+    b->host_valid = 0;
+    b->nal_cache_valid = 0;
+    int rc = SCROLL_OK;
+    for (int k = 0; k < n; ++k) {
+        if (status) status[k] = outs[k].err;
+        if (outs[k].err != ING_OK && rc == SCROLL_OK) {
+            set_err("scroll_batch_update_refs: stream %d: %s", streams[k],
+                    outs[k].err == ING_ERR_DIMS ? "picture size differs from the stream's" : ing_msg(outs[k].err));
+            rc = outs[k].err == ING_ERR_OVERFLOW ? SCROLL_ERR_OVERFLOW : SCROLL_ERR_CONFIG;
+        }
+    }
+    return rc;
+}
+
+int scroll_batch_update_refs(ScrollBatch *b, int n, const int *streams, const int *which,
+                             const uint8_t *const *files, const size_t *sizes, int *status)
+{
+    if (!b || n < 0 || (n > 0 && (!files || !sizes))) return SCROLL_ERR_ARG;
+    std::vector<uint64_t> desc(2 * (size_t)n);
+    size_t tot = 0;
+    for (int k = 0; k < n; ++k) {
+        if (sizes[k] && !files[k]) return SCROLL_ERR_ARG;
+        desc[2 * k] = tot;
+        desc[2 * k + 1] = sizes[k];
+        tot += (sizes[k] + 255) & ~(size_t)255;
+    }
+    if (n == 0) return SCROLL_OK;
+    int rc = batch_host_sync(b);                  /* the input buffer may be in use */
+    if (rc) return rc;
+    HIPCHK(hipSetDevice(b->device));
+    if (tot > b->ing_in_cap) {
+        (void)hipFree(b->d_ing_in);
+        b->d_ing_in = nullptr;
+        b->ing_in_cap = 0;
+        hipError_t e = hipMalloc(&b->d_ing_in, tot);
+        if (e != hipSuccess) {
+            set_err("scroll_batch_update_refs: %s", hipGetErrorString(e));
+            return e == hipErrorOutOfMemory ? SCROLL_ERR_OOM : SCROLL_ERR_HIP;
+        }
+        b->ing_in_cap = tot;
+    }
+    for (int k = 0; k < n; ++k)
+        if (sizes[k]) HIPCHK(hipMemcpy(b->d_ing_in + desc[2 * k], files[k], sizes[k], hipMemcpyHostToDevice));
+    return scroll_batch_update_refs_device(b, n, streams, which, b->d_ing_in, desc.data(), status);
 }
 
 int scroll_batch_enable_timing(ScrollBatch *b, int on)

@@ -159,6 +159,11 @@ def _load():
         "scroll_batch_copy_output": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int,
                                                     ctypes.c_size_t, u8p, ctypes.c_size_t]),
         "scroll_batch_output_device": (ctypes.c_void_p, [ctypes.c_void_p, ctypes.c_int]),
+        "scroll_host_alloc": (ctypes.c_int, [P(ctypes.c_void_p), ctypes.c_size_t]),
+        "scroll_host_free": (None, [ctypes.c_void_p]),
+        "scroll_batch_output_to_host_async": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p,
+                                                             ctypes.c_size_t, ctypes.c_void_p,
+                                                             ctypes.c_void_p]),
         "scroll_batch_reset_output": (ctypes.c_int, [ctypes.c_void_p]),
         "scroll_batch_nal_count": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
         "scroll_batch_nal_info": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
@@ -195,6 +200,12 @@ def _load():
         "scroll_batch_ingest": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, P(u8p),
                                                P(ctypes.c_size_t), P(u8p), P(ctypes.c_size_t),
                                                P(ctypes.c_int)]),
+        "scroll_batch_update_refs": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, P(ctypes.c_int),
+                                                    P(ctypes.c_int), P(u8p), P(ctypes.c_size_t),
+                                                    P(ctypes.c_int)]),
+        "scroll_batch_update_refs_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, P(ctypes.c_int),
+                                                           P(ctypes.c_int), ctypes.c_void_p,
+                                                           P(ctypes.c_uint64), P(ctypes.c_int)]),
         "scroll_batch_ingest_stats": (ctypes.c_int, [ctypes.c_void_p, P(ctypes.c_double),
                                                      P(ctypes.c_int)]),
         "scroll_batch_ingest_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int,
@@ -293,6 +304,43 @@ def u8buf(data_or_size):
     return b
 
 
+class HostBuffer:
+    """Pinned host memory the device writes into (scroll_host_alloc): the
+    packed bytes of Batch.output_to_host_async and its (offset, size) table."""
+
+    def __init__(self, nbytes, nstreams):
+        self.cap = (nbytes + 15) & ~15
+        self.ns = nstreams
+        self.p = ctypes.c_void_p()
+        self.t = ctypes.c_void_p()
+        if lib.scroll_host_alloc(ctypes.byref(self.p), self.cap) or \
+                lib.scroll_host_alloc(ctypes.byref(self.t), 8 * (1 + 2 * nstreams)):
+            raise RuntimeError("scroll_host_alloc: " + last_error())
+        self.table = (ctypes.c_uint64 * (1 + 2 * nstreams)).from_address(self.t.value)
+        self.data = (ctypes.c_uint8 * self.cap).from_address(self.p.value)
+
+    def total(self):
+        """packed bytes of the last delivery (None: it did not fit)"""
+        v = self.table[0]
+        return None if v == (1 << 64) - 1 else v
+
+    def stream(self, s):
+        o, n = self.table[1 + 2 * s], self.table[2 + 2 * s]
+        return ctypes.string_at(self.p.value + o, n)
+
+    def close(self):
+        if self.p:
+            lib.scroll_host_free(self.p)
+            lib.scroll_host_free(self.t)
+            self.p = self.t = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 def make_config(w, h, frame_num=2, log2_mfn=4, poc_type=2, log2_poc=4, deblock=1,
                 waypoints=()):
     """ComposerConfig in the state composer_init + composer_write_header leave it
@@ -382,6 +430,12 @@ class Batch:
         self._chk(lib.scroll_batch_copy_output(self.h, s, start, b, n), "copy_output")
         return bytes(b[:n])
 
+    def output_to_host_async(self, hb, stream=None):
+        """the bytes the last compose appended to every stream -> HostBuffer
+        hb (packed, device-written, asynchronous: valid after sync())"""
+        self._chk(lib.scroll_batch_output_to_host_async(self.h, hb.p, hb.cap, hb.t, stream),
+                  "output_to_host_async")
+
     def output_device_ptr(self, s):
         """device address of stream s's arena (scroll_batch_output_device)"""
         return lib.scroll_batch_output_device(self.h, s)
@@ -442,6 +496,22 @@ class Batch:
         self._chk(lib.scroll_batch_ingest_device(self.h, n, ctypes.c_void_p(d_files), arr,
                                                  ctypes.byref(first)), "ingest_device")
         return first.value
+
+    def update_refs(self, streams, which, files, check=True):
+        """mid-stream long-term reference updates: files[k] (Annex-B bytes with
+        an IDR) -> a non-IDR I frame of stream streams[k] marked which[k]
+        (0 = A, 1 = B); -> (rc, statuses)"""
+        n = len(streams)
+        st = (ctypes.c_int * n)(*streams)
+        wh = (ctypes.c_int * n)(*which)
+        bufs = [u8buf(f) for f in files]
+        fp = (ctypes.POINTER(ctypes.c_uint8) * n)(*[ctypes.cast(x, ctypes.POINTER(ctypes.c_uint8)) for x in bufs])
+        sz = (ctypes.c_size_t * n)(*[len(f) for f in files])
+        stat = (ctypes.c_int * n)()
+        rc = lib.scroll_batch_update_refs(self.h, n, st, wh, fp, sz, stat)
+        if check:
+            self._chk(rc, "update_refs")
+        return rc, list(stat)
 
     def ingest_stats(self):
         ms, n = ctypes.c_double(), ctypes.c_int()

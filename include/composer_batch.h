@@ -111,6 +111,20 @@ int scroll_batch_set_config(ScrollBatch *b, int s, const ComposerConfig *cfg);
 size_t scroll_batch_output_size(ScrollBatch *b, int s);
 int scroll_batch_copy_output(ScrollBatch *b, int s, size_t from, uint8_t *dst, size_t n);
 const uint8_t *scroll_batch_output_device(ScrollBatch *b, int s);
+/* Host delivery (the reference returns its bytes in host memory,
+ * composer.c:255-291): pinned host buffers the device writes into, and the
+ * bytes appended to every stream since its previous delivery (composes,
+ * reference updates; a rewound arena starts over) packed into dst back to
+ * back in stream order, asynchronously on hip_stream (NULL = the stream of
+ * the last compose; another stream waits for it).  table (pinned, 1 + 2 S
+ * u64) gets [0] = the packed size (~0: larger than cap, nothing written),
+ * then per stream its offset in dst (16-byte aligned) and its byte count.
+ * dst and cap 16-byte aligned.  Valid after scroll_batch_sync / a stream
+ * sync; the arenas must not be rewritten before the copy has run. */
+int scroll_host_alloc(void **p, size_t n);
+void scroll_host_free(void *p);
+int scroll_batch_output_to_host_async(ScrollBatch *b, uint8_t *dst, size_t cap, uint64_t *table,
+                                      void *hip_stream);
 int scroll_batch_reset_output(ScrollBatch *b);   /* rewind all arenas, keep state */
 
 /* last compose: planned NAL units of stream s (kind/size/offset per NAL) */
@@ -310,6 +324,28 @@ int scroll_batch_ingest(ScrollBatch *b, int n, const uint8_t *const *ref_a, cons
                         const uint8_t *const *ref_b, const size_t *nb, int *first);
 int scroll_batch_ingest_device(ScrollBatch *b, int n, const uint8_t *d_files,
                                const uint64_t *desc, int *first);
+
+/* Mid-stream long-term reference ("atlas") update -- SURVEY 8f row 3; the
+ * reference only installs A / B at composer_write_header.  Entry k: the IDR
+ * picture of Annex-B file k (parse_reference_file's rules, parsed with the
+ * file's own SPS / PPS) becomes a non-IDR I frame of stream streams[k]
+ * marked long_term_frame_idx which[k] (0 = A, 1 = B): the reference's
+ * h264_rewrite_as_non_idr_i_frame (h264_writer.c:296-350) with the index as
+ * a parameter, at the stream's frame_num, written with the stream's config,
+ * appended after everything composed so far.  Its MMCO 4
+ * (max_long_term_frame_idx_plus1 = 2) drops the stream's waypoints, so the
+ * stream continues with an empty waypoint table and frame_num + 1; later
+ * scroll frames predict from the new picture.  Streams distinct per call;
+ * the picture must have the stream's size.  Synchronous; status[k] (may be
+ * NULL) = 0 or the ingest error class (1 missing NAL, 2 refused SPS / PPS,
+ * 3 size, 4 too many NALs, 5 arena full: nothing appended).  For a batch
+ * with a dynamic rect also give the stream its new pictures
+ * (scroll_batch_set_dyn_refs): prediction reads those. */
+int scroll_batch_update_refs(ScrollBatch *b, int n, const int *streams, const int *which,
+                             const uint8_t *const *files, const size_t *sizes, int *status);
+/* the same from files already on the device (desc: offset, size per entry) */
+int scroll_batch_update_refs_device(ScrollBatch *b, int n, const int *streams, const int *which,
+                                    const uint8_t *d_files, const uint64_t *desc, int *status);
 /* with timing enabled: summed ms of the ingest kernels (HIP events on the
  * batch's stream) and the number of ingest calls since the last call */
 int scroll_batch_ingest_stats(ScrollBatch *b, double *ms, int *count);

@@ -574,8 +574,19 @@ size_t or_rewrite_idr(uint8_t *dst, size_t cap, or_cfg *wr, const or_cfg *pc,
     return r;
 }
 
+static size_t or_rewrite_non_idr_lt(uint8_t *dst, size_t cap, or_cfg *wr, const or_cfg *pc,
+                                    const uint8_t *rbsp, size_t n, int frame_num, int lt_idx);
+
 size_t or_rewrite_non_idr(uint8_t *dst, size_t cap, or_cfg *wr, const or_cfg *pc,
                           const uint8_t *rbsp, size_t n, int frame_num)
+{
+    return or_rewrite_non_idr_lt(dst, cap, wr, pc, rbsp, n, frame_num, 1);
+}
+
+/* the same with long_term_frame_idx lt_idx in the MMCO 6 (the reference
+ * writes 1, :328) */
+static size_t or_rewrite_non_idr_lt(uint8_t *dst, size_t cap, or_cfg *wr, const or_cfg *pc,
+                                    const uint8_t *rbsp, size_t n, int frame_num, int lt_idx)
 {
     or_slice_hdr h;
     or_parse_idr(rbsp, n, pc, &h);
@@ -590,7 +601,7 @@ size_t or_rewrite_non_idr(uint8_t *dst, size_t cap, or_cfg *wr, const or_cfg *pc
     if (wr->poc_type == 0) or_put(&b, (uint32_t)(frame_num * 2), wr->log2_poc);
     or_bit(&b, 1);
     or_ue(&b, 4); or_ue(&b, 2);
-    or_ue(&b, 6); or_ue(&b, 1);
+    or_ue(&b, 6); or_ue(&b, (uint32_t)lt_idx);
     or_ue(&b, 0);
     or_tail_fields(&b, wr, &h);
     or_copy_bits(&b, rbsp, n, h.mb_start);
@@ -903,6 +914,37 @@ size_t or_composer_run(uint8_t *dst, size_t cap,
     free(a.idr);
     free(b.idr);
     return o;
+}
+
+/* Mid-stream long-term reference ("atlas") update -- no reference function:
+ * the file's IDR picture (parse_reference_file's rules, parsed with its own
+ * SPS / PPS like composer_init, src/composer.c:127-196) written as a non-IDR
+ * I frame of stream c, h264_rewrite_as_non_idr_i_frame (h264_writer.c:296-350)
+ * with long_term_frame_idx `which` (0 = A, 1 = B) at the stream's frame_num
+ * (mod 2^log2_max_frame_num, POC lsb 2 frame_num, as the waypoint frames,
+ * :683-687); its MMCO 4 (max_long_term_frame_idx_plus1 2) drops every
+ * waypoint, so c loses its waypoints and frame_num advances (:779-781).  0
+ * (c unchanged) if the file is refused or its picture size differs. */
+size_t or_update_ref(uint8_t *dst, size_t cap, or_cfg *c, const uint8_t *file, size_t n, int which)
+{
+    or_refinfo ri;
+    if (which < 0 || which > 1 || or_parse_ref(file, n, &ri) < 0) return 0;
+    if (ri.w != c->w || ri.h != c->h) {
+        free(ri.idr);
+        return 0;
+    }
+    or_cfg pc;
+    or_cfg_init(&pc, ri.w, ri.h);
+    pc.log2_mfn = ri.l2f; pc.poc_type = ri.poct; pc.log2_poc = ri.l2p;
+    pc.num_ref_default_m1 = ri.nref; pc.deblock = ri.dbf;
+    const int fn = c->frame_num % (1 << c->log2_mfn);
+    const int fn_next = c->frame_num + 1;
+    size_t r = or_rewrite_non_idr_lt(dst, cap, c, &pc, ri.idr, ri.nidr, fn, which);
+    free(ri.idr);
+    c->frame_num = fn_next;
+    c->nwp = 0;
+    for (int k = 0; k < OR_MAX_WP; ++k) c->wp_valid[k] = 0;
+    return r;
 }
 
 size_t or_experiment_run(uint8_t *dst, size_t cap, int w, int h, int nframes, int speed)

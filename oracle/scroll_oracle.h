@@ -103,6 +103,9 @@ size_t or_rewrite_idr(uint8_t *dst, size_t cap, or_cfg *wr, const or_cfg *pc,
                       const uint8_t *rbsp, size_t n);
 size_t or_rewrite_non_idr(uint8_t *dst, size_t cap, or_cfg *wr, const or_cfg *pc,
                           const uint8_t *rbsp, size_t n, int frame_num);
+/* mid-stream long-term reference update (scroll_oracle.c): the file's IDR
+ * as a non-IDR I frame marked long-term `which`, waypoints dropped */
+size_t or_update_ref(uint8_t *dst, size_t cap, or_cfg *c, const uint8_t *file, size_t n, int which);
 /* I_PCM striped reference (experiments/scroll-encoder/src/h264_encoder.c:730-918).
  * which = 0: IDR with stripes (y1..cr3), which = 1: non-IDR I frame. */
 size_t or_ipcm_striped(uint8_t *dst, size_t cap, or_cfg *c, int which,

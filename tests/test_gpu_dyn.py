@@ -317,3 +317,36 @@ def test_dyn_large_nal_emit_path(gpu, oracle):
     b, rc = gpu_streams(gpu, w, h, offs, rect, R, src, debug=gpu.SCROLL_DEBUG_DYN_EPCAP4)
     assert rc == 0, gpu.last_error()
     check_equal(b, want)
+
+
+def test_dyn_spill_pool_runs_out_and_grows(gpu, oracle):
+    """the row stage is sized for typical rows (SCROLL_DYN_ROW_KBITS per MB);
+    a row past its slot takes a spill slot (k_dyn_row), and the pool holds
+    1/32 of the rect rows.  Random reference pictures make EVERY row spill:
+    a 16 x 40-frame config-3 batch runs the pool out -- the compose fails
+    with SCROLL_ERR_OVERFLOW and no stream commits anything (also those whose
+    own rows all got slots), the batch grows its pools, and the same compose
+    again is bit-exact (every row through a spill slot)"""
+    w, h = 1280, 720
+    rect = Rect(28, 10, 25, 25)
+    S, F = 16, 40
+    offs = synthetic_offsets(S, F, h)
+    R = random_refs(w, h, 12)
+    b = gpu.Batch(S, F, 16 << 20)
+    for _ in range(S):
+        b.add_stream(gpu.make_config(w, h))
+    b.set_dyn_rect(rect.x0, rect.y0, rect.w, rect.h)
+    b.set_dyn_refs(R.i420(0), R.i420(1))
+    b.set_offsets(offs)
+    b.dyn_source_synth(F, 0, 0)
+    b.compose(F)
+    rc = b.sync()
+    assert rc == -4, gpu.last_error()                               # SCROLL_ERR_OVERFLOW
+    assert "grown" in gpu.last_error()
+    assert all(b.output_size(s) == 0 for s in range(S))             # nothing committed
+    b.compose(F)
+    assert b.sync() == 0, gpu.last_error()
+    src = synth_source(oracle, S, F, rect)
+    want = oracle_streams(oracle, w, h, offs, rect, src, R)
+    check_equal(b, want)
+    b.close()

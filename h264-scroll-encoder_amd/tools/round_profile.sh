@@ -6,7 +6,7 @@
 #   counter pass over the dynamic-rect kernels.  Every GPU step has its own time
 #   limit; the first failing step ends the script.
 set -e -o pipefail
-TAG=${1:-r02}
+TAG=${1:-r03}
 O=gpurun_out/prof_$TAG
 mkdir -p "$O"
 export TMPDIR=/tmp
@@ -17,10 +17,10 @@ for w in p720 p4kdyn p720hint p720splice; do
 done
 $T 200 python3 bench.py --steps 10 --warmup 2 --streams 1024 --no-cpu > "$O/bench_p720dyn_1024streams.json" 2> /dev/null
 for w in p720dyn p4kdyn; do
-    $T 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/stats_$w" -o run -- python3 bench.py --steps 5 --warmup 2 --no-cpu --workload $w > "$O/stats_$w.log" 2>&1
+    $T 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/stats_$w" -o run -- python3 bench.py --steps 5 --warmup 2 --no-cpu --no-host --workload $w > "$O/stats_$w.log" 2>&1
 done
-$T 120 rocprofv3 --output-format csv --pmc FETCH_SIZE -d "$O/pmc_fetch" -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu > "$O/pmc_fetch.log" 2>&1
-$T 120 rocprofv3 --output-format csv --pmc WRITE_SIZE -d "$O/pmc_write" -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu > "$O/pmc_write.log" 2>&1
-$T 120 rocprofv3 --output-format csv --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS GRBM_GUI_ACTIVE -d "$O/pmc_sq" -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu > "$O/pmc_sq.log" 2>&1
+$T 120 rocprofv3 --output-format csv --pmc FETCH_SIZE -d "$O/pmc_fetch" -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu --no-host > "$O/pmc_fetch.log" 2>&1
+$T 120 rocprofv3 --output-format csv --pmc WRITE_SIZE -d "$O/pmc_write" -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu --no-host > "$O/pmc_write.log" 2>&1
+$T 120 rocprofv3 --output-format csv --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS GRBM_GUI_ACTIVE -d "$O/pmc_sq" -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu --no-host > "$O/pmc_sq.log" 2>&1
 $T 120 python3 h264-scroll-encoder_amd/tools/dyn_stamps.py > "$O/dyn_stamps.txt" 2>&1
 echo done > "$O/DONE"

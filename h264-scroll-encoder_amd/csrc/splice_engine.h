@@ -31,16 +31,21 @@ typedef struct {
 
 /* one external MB after parsing: motion (quarter pels), cbp, the composed
  * mb_qp_delta, and per piece its TotalCoeff, TrailingOnes and the bits after
- * coeff_token (offset and length in the RBSP).  224 bytes. */
+ * coeff_token (offset and length in the RBSP).  A partitioned MB (part 1
+ * 16x8, 2 8x16, 3 P_8x8 / P_8x8ref0 with sub_mb_type i in bits 2i..2i+1 of
+ * sub) also carries the motion of each 4x4 block (raster; mv packed x | y
+ * << 16); ref / mx / my are then block 0's.  304 bytes. */
 typedef struct {
     int16_t ref;
     uint8_t cbp;
     int8_t qpd;
     int32_t mx, my;
-    uint32_t skip;
+    uint8_t skip, part, sub, pad;
     uint8_t tc[SPLICE_PIECES], t1[SPLICE_PIECES];
     uint16_t blen[SPLICE_PIECES];
     uint32_t boff[SPLICE_PIECES];
+    int8_t bref[16];
+    uint32_t bmv[16];
 } SpliceMbRec;
 
 /* 0, or -1 when the launch failed */

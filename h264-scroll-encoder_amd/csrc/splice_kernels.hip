@@ -78,6 +78,70 @@ __device__ inline int blk_raster16(int blk)       /* luma4x4BlkIdx -> raster */
     return 4 * ((q8 >> 1) * 2 + (q4 >> 1)) + (q8 & 1) * 2 + (q4 & 1);
 }
 
+/* the (sub-)partitions of an MB partitioned `part` (1 16x8, 2 8x16, 3
+ * P_8x8 with sub_mb_types `sub`) in decoding order: f(bx, by, bw, bh,
+ * mbPartIdx), 4x4-block units (Tables 7-13, 7-17) */
+template <class Fn>
+__device__ __attribute__((always_inline)) inline void for_parts(int part, uint32_t sub, Fn &&f)
+{
+    if (part == 1) {
+        f(0, 0, 4, 2, 0);
+        f(0, 2, 4, 2, 1);
+    } else if (part == 2) {
+        f(0, 0, 2, 4, 0);
+        f(2, 0, 2, 4, 1);
+    } else {
+        for (int i = 0; i < 4; ++i) {
+            const int sx = (i & 1) * 2, sy = (i >> 1) * 2, st = (int)((sub >> (2 * i)) & 3u);
+            if (st == 0) {
+                f(sx, sy, 2, 2, i);
+            } else if (st == 1) {
+                f(sx, sy, 2, 1, i);
+                f(sx, sy + 1, 2, 1, i);
+            } else if (st == 2) {
+                f(sx, sy, 1, 2, i);
+                f(sx + 1, sy, 1, 2, i);
+            } else {
+                for (int k = 0; k < 4; ++k) f(sx + (k & 1), sy + (k >> 1), 1, 1, i);
+            }
+        }
+    }
+}
+
+/* 4x4 blocks of a (sub-)partition as a mask (bit 4 y + x) */
+__device__ inline uint32_t part_mask(int bx, int by, int bw, int bh)
+{
+    const uint32_t row = ((1u << bw) - 1u) << bx;
+    uint32_t m = 0;
+    for (int j = 0; j < bh; ++j) m |= row << (4 * (by + j));
+    return m;
+}
+
+/* 8.4.1.3 for (sub-)partition mbPartIdx mp of an MB partitioned `part`,
+ * neighbours nb(cx, cy) relative to the MB (6.4.11.7: C, else D) */
+template <class NB>
+__device__ __attribute__((always_inline)) inline void predict_part(int part, int mp, int bx, int by, int bw,
+                                                                   int ref, NB &&nb, int &px, int &py)
+{
+    const Mv A = nb(bx - 1, by), B = nb(bx, by - 1);
+    Mv C = nb(bx + bw, by - 1);
+    if (C.ref < 0) C = nb(bx - 1, by - 1);
+    const Mv d = part == 1 ? (mp ? A : B) : (mp ? C : A);
+    if (part != 3 && d.ref == ref) {
+        px = d.mx;
+        py = d.my;
+        return;
+    }
+    predict_spec(A, B, C, ref, px, py);
+}
+
+/* motion of a 4x4 block packed as mv x | y << 16 (quarter pels, |mv| <= 2^14) */
+__device__ inline uint32_t pk_mv(int mx, int my) { return (uint32_t)(mx & 0xffff) | (uint32_t)my << 16; }
+__device__ inline Mv unpk_mv(int ref, uint32_t v)
+{
+    return Mv{ref, (int)(int16_t)(v & 0xffffu), (int)(int16_t)(v >> 16)};
+}
+
 /* One wave parses one slice.  The slice is a sequential bit string, so the
  * parse itself is wave-uniform (scalar values, no divergence): the bit window
  * is 64 RBSP words held one per lane (readlane at the uniform bit position),
@@ -86,10 +150,16 @@ __device__ inline int blk_raster16(int blk)       /* luma4x4BlkIdx -> raster */
  * (motion of the two rows above, TotalCoeffs of the row above) sits in LDS. */
 constexpr int PARSE_MAXW = 240;          /* external picture width limit (MBs) */
 
-struct WRd {
+/* The bit reader keeps the next 33..64 bits of the slice in a 64-bit scalar
+ * register pair (MSB-aligned): a peek is a shift, a read of up to 32 bits
+ * one 64-bit shift, and a word enters from the window -- 64 RBSP words held
+ * one per lane, read by one v_readlane -- once per 32 bits consumed. */
+struct SRd {
     const uint32_t *w;
-    uint32_t nw, nbits, p, base;
-    uint32_t win;                        /* word base + lane */
+    uint32_t nw, nbits, p;               /* words, bits, bits consumed                */
+    uint64_t buf;                        /* the next nv bits at the top               */
+    uint32_t nv, wk;                     /* valid bits (>= 33 between reads); next word */
+    uint32_t base, win;                  /* window: word base + lane                  */
     bool bad;                            /* ue() without a 1 bit; p > nbits is checked per MB */
     /* the wait sits in the (rare) refill branch: otherwise the compiler
      * waits for vmcnt(0) before every readlane of the window -- and on gfx9
@@ -102,27 +172,39 @@ struct WRd {
         win = k < nw ? w[k] : 0u;
         asm volatile("s_waitcnt vmcnt(0)" : "+v"(win)::"memory");
     }
-    /* the 32 bits at p: words k, k + 1 of the window by readlane (scalar),
-     * joined by a 64-bit scalar shift */
-    __device__ inline uint32_t peek32()
+    __device__ inline uint32_t word(uint32_t k)
     {
-        uint32_t k = (p >> 5) - base;
-        if (k >= 63u) {
-            fill(p >> 5);
-            k = 0;
-        }
-        const uint32_t a = (uint32_t)__builtin_amdgcn_readlane(win, k);
-        const uint32_t b = (uint32_t)__builtin_amdgcn_readlane(win, k + 1);
-        const uint64_t ab = (uint64_t)a << 32 | b;
-        return (uint32_t)((ab << (p & 31u)) >> 32);
+        if (k - base >= 64u) fill(k);
+        return (uint32_t)__builtin_amdgcn_readlane(win, k - base);
     }
-    __device__ inline uint32_t peek(int n) { return n ? peek32() >> (32 - n) : 0u; }
-    __device__ inline void skip(int n) { p += (uint32_t)n; }
-    __device__ inline bool over() const { return p > nbits; }
-    __device__ inline uint32_t u(int n)
+    __device__ inline void init(const uint32_t *words, uint32_t nwords, uint32_t bits)
     {
-        const uint32_t v = peek(n);
-        skip(n);
+        w = words;
+        nw = nwords;
+        nbits = bits;
+        p = 0;
+        bad = false;
+        fill(0);
+        buf = (uint64_t)word(0) << 32 | word(1);
+        nv = 64;
+        wk = 2;
+    }
+    __device__ inline uint32_t peek32() const { return (uint32_t)(buf >> 32); }
+    __device__ inline void skip(uint32_t n)                  /* n <= 32 */
+    {
+        buf <<= n;
+        nv -= n;
+        p += n;
+        if (nv <= 32u) {
+            buf |= (uint64_t)word(wk++) << (32u - nv);
+            nv += 32u;
+        }
+    }
+    __device__ inline bool over() const { return p > nbits; }
+    __device__ inline uint32_t u(int n)                      /* 1 <= n <= 32 */
+    {
+        const uint32_t v = (uint32_t)(buf >> (64 - n));
+        skip((uint32_t)n);
         return v;
     }
     __device__ inline uint32_t ue()
@@ -134,10 +216,10 @@ struct WRd {
         }
         const int z = __clz((int)x);
         if (z < 16) {                    /* the whole code in x */
-            skip(2 * z + 1);
+            skip((uint32_t)(2 * z + 1));
             return (x >> (31 - 2 * z)) - 1u;
         }
-        skip(z);
+        skip((uint32_t)z);
         return u(z + 1) - 1u;
     }
     __device__ inline int32_t se()
@@ -147,86 +229,122 @@ struct WRd {
     }
 };
 
-/* first lane of a ballot, -1 if none */
-__device__ inline int first_lane(uint64_t m) { return m ? __builtin_ctzll(m) : -1; }
-
-/* The CAVLC tables in registers, lane e holding entry e of each (packed
- * len << 8 | bits, two 16-bit entries per register): a VLC match is then a
- * few VALU operations and a ballot, no memory access */
+/* The CAVLC tables as v_readlane lookups indexed by the code's leading
+ * zeros and the bits after its first 1 (Tables 9-5, 9-7/9-8, 9-9a, 9-10
+ * have at most 3 / 2 such bits per leading-zero count), built per lane at
+ * the kernel start from the coder's tables:
+ *   ct[c]      coeff_token, class c (nC 0-1, 2-3, 4-7, -1): index lz * 8 +
+ *              3 bits, 16-bit entries (lane i: i | i + 64), len << 8 | tc << 2 | t1
+ *   tz0..2     total_zeros: (tc - 1) * 40 + min(lz, 9) * 4 + 2 bits, bytes
+ *              (lane i byte j: index 256 v + 64 j + i), len << 4 | total_zeros
+ *   tzd        chroma DC total_zeros: (tc - 1) * 16 + min(lz, 3) * 4 + 2 bits
+ *   rb0, rb1   run_before: (min(zerosLeft, 7) - 1) * 48 + min(lz, 11) * 4 + 2 bits
+ *   cbp        coded_block_pattern of codeNum lane (inter, Table 9-4)
+ * (0: no code) */
 struct LaneTabs {
-    uint32_t ct01, ct2d;          /* coeff_token nC 0-1 | 2-3 ; nC 4-7 | chroma DC, entry e */
-    uint32_t cx01, cx2;           /* entries 64 + e (lanes 0..3)                             */
-    /* total_zeros rows 2k | 2k+1, entry (total_zeros) e -- separate
-     * registers: an array indexed by the row would live in scratch */
-    uint32_t tz0, tz1, tz2, tz3, tz4, tz5, tz6, tz7;
-    uint32_t tzd01, tzd2;         /* chroma DC total_zeros rows 0 | 1, 2                      */
-    uint32_t rb0, rb1, rb2, rb3;  /* run_before rows 2k | 2k+1, entry (run) e                 */
-    uint32_t cbp;                 /* coded_block_pattern -> codeNum, entry e < 48            */
+    uint32_t ct0, ct1, ct2, ct3;
+    uint32_t tz0, tz1, tz2, tzd, rb0, rb1;
+    uint32_t cbp;
 };
 
-__device__ inline uint32_t pk(int len, int bits) { return len ? (uint32_t)(len << 8 | bits) : 0u; }
-
-__device__ inline LaneTabs lane_tabs()
+/* the 16-bit pattern `lz` zeros, a 1, then the top `nb` bits of n */
+__device__ inline uint32_t vlc_pattern(int lz, uint32_t n, int nb)
 {
-    const int e = threadIdx.x & 63;
-    LaneTabs T;
-    T.ct01 = pk(SPT.ct_len[0][e], SPT.ct_bits[0][e]) | pk(SPT.ct_len[1][e], SPT.ct_bits[1][e]) << 16;
-    T.ct2d = pk(SPT.ct_len[2][e], SPT.ct_bits[2][e]) |
-             (e < 20 ? pk(SPT.ctdc_len[e], SPT.ctdc_bits[e]) << 16 : 0u);
-    const int x = 64 + (e & 3);
-    T.cx01 = e < 4 ? pk(SPT.ct_len[0][x], SPT.ct_bits[0][x]) | pk(SPT.ct_len[1][x], SPT.ct_bits[1][x]) << 16 : 0u;
-    T.cx2 = e < 4 ? pk(SPT.ct_len[2][x], SPT.ct_bits[2][x]) : 0u;
-    auto tzp = [e](int k) {
-        const int r0 = 2 * k, r1 = 2 * k + 1;
-        const uint32_t lo = e < 16 ? pk(SPT.tz_len[r0][e & 15], SPT.tz_bits[r0][e & 15]) : 0u;
-        const uint32_t hi = e < 16 && r1 < 15 ? pk(SPT.tz_len[r1][e & 15], SPT.tz_bits[r1][e & 15]) : 0u;
-        return lo | hi << 16;
-    };
-    T.tz0 = tzp(0);
-    T.tz1 = tzp(1);
-    T.tz2 = tzp(2);
-    T.tz3 = tzp(3);
-    T.tz4 = tzp(4);
-    T.tz5 = tzp(5);
-    T.tz6 = tzp(6);
-    T.tz7 = tzp(7);
-    T.tzd01 = e < 4 ? pk(SPT.tzdc_len[0][e & 3], SPT.tzdc_bits[0][e & 3]) |
-                          pk(SPT.tzdc_len[1][e & 3], SPT.tzdc_bits[1][e & 3]) << 16 : 0u;
-    T.tzd2 = e < 4 ? pk(SPT.tzdc_len[2][e & 3], SPT.tzdc_bits[2][e & 3]) : 0u;
-    auto rbp = [e](int k) {
-        const int r0 = 2 * k, r1 = 2 * k + 1;
-        const uint32_t lo = e < 15 ? pk(SPT.rb_len[r0][e % 15], SPT.rb_bits[r0][e % 15]) : 0u;
-        const uint32_t hi = e < 15 && r1 < 7 ? pk(SPT.rb_len[r1][e % 15], SPT.rb_bits[r1][e % 15]) : 0u;
-        return lo | hi << 16;
-    };
-    T.rb0 = rbp(0);
-    T.rb1 = rbp(1);
-    T.rb2 = rbp(2);
-    T.rb3 = rbp(3);
-    T.cbp = e < 48 ? SPT.cbp_code[e] : 0xffffu;
-    return T;
+    const int sh = 15 - lz - nb;
+    return (1u << (15 - lz)) | (sh >= 0 ? n << sh : n >> -sh);
 }
 
-/* does the 16-bit lookahead x start with the packed code v? */
-__device__ inline bool code_hit(uint32_t v, uint32_t x)
+/* the entry (index) of the code among `cnt` (len, bits) that starts pattern x */
+__device__ inline int vlc_find(uint32_t x, const uint8_t *len, const uint8_t *bits, int cnt)
 {
-    const uint32_t len = (v >> 8) & 255u;
-    return len && (x >> (16u - len)) == (v & 255u);
-}
-
-/* the ballot's entry, its packed code from the lane that holds it */
-__device__ inline int match(uint32_t v, uint32_t x, uint32_t &len)
-{
-    const int e = first_lane(__ballot(code_hit(v, x)));
-    if (e >= 0) len = (__builtin_amdgcn_readlane(v, e) >> 8) & 255u;
+    int e = -1;
+    for (int i = 0; i < cnt; ++i) {
+        const int l = len[i];
+        if (l && e < 0 && (x >> (16 - l)) == bits[i]) e = i;
+    }
     return e;
 }
 
-/* 16-bit half h (uniform) of a packed register */
-__device__ inline uint32_t half(uint32_t v, int h) { return h ? v >> 16 : v & 0xffffu; }
+__device__ inline LaneTabs lane_tabs()
+{
+    const int lane = threadIdx.x & 63;
+    LaneTabs T;
+    auto ct = [&](int c) {
+        uint32_t v = 0;
+        for (int h = 0; h < 2; ++h) {
+            const int idx = lane + 64 * h, lz = idx >> 3;
+            if (lz > 15) continue;
+            const uint32_t x = vlc_pattern(lz, (uint32_t)(idx & 7), 3);
+            const int e = c < 3 ? vlc_find(x, SPT.ct_len[c], SPT.ct_bits[c], 68)
+                                : vlc_find(x, SPT.ctdc_len, SPT.ctdc_bits, 20);
+            if (e >= 0) {
+                const int l = c < 3 ? SPT.ct_len[c][e] : SPT.ctdc_len[e];
+                v |= (uint32_t)(l << 8 | (e >> 2) << 2 | (e & 3)) << (16 * h);
+            }
+        }
+        return v;
+    };
+    T.ct0 = ct(0);
+    T.ct1 = ct(1);
+    T.ct2 = ct(2);
+    T.ct3 = ct(3);
+    auto bytes = [&](int v, auto entry) {         /* the 4 byte entries of lane, register v */
+        uint32_t r = 0;
+        for (int j = 0; j < 4; ++j) r |= (uint32_t)entry(256 * v + 64 * j + lane) << (8 * j);
+        return r;
+    };
+    auto tz = [&](int idx) -> uint32_t {
+        const int tc = idx / 40 + 1, q = idx % 40, lz = q >> 2;
+        if (tc > 15) return 0u;
+        const int e = vlc_find(vlc_pattern(lz, (uint32_t)(q & 3), 2), SPT.tz_len[tc - 1], SPT.tz_bits[tc - 1],
+                               17 - tc < 16 ? 17 - tc : 16);
+        return e < 0 ? 0u : (uint32_t)(SPT.tz_len[tc - 1][e] << 4 | e);
+    };
+    T.tz0 = bytes(0, tz);
+    T.tz1 = bytes(1, tz);
+    T.tz2 = bytes(2, tz);
+    auto tzd = [&](int idx) -> uint32_t {
+        const int tc = idx / 16 + 1, q = idx % 16, lz = q >> 2;
+        if (tc > 3) return 0u;
+        const int e = vlc_find(vlc_pattern(lz, (uint32_t)(q & 3), 2), SPT.tzdc_len[tc - 1], SPT.tzdc_bits[tc - 1],
+                               5 - tc);
+        return e < 0 ? 0u : (uint32_t)(SPT.tzdc_len[tc - 1][e] << 4 | e);
+    };
+    T.tzd = bytes(0, tzd);
+    auto rb = [&](int idx) -> uint32_t {
+        const int zl = idx / 48 + 1, q = idx % 48, lz = q >> 2;
+        if (zl > 7) return 0u;
+        const int e = vlc_find(vlc_pattern(lz, (uint32_t)(q & 3), 2), SPT.rb_len[zl - 1], SPT.rb_bits[zl - 1],
+                               zl < 7 ? zl + 1 : 15);
+        return e < 0 ? 0u : (uint32_t)(SPT.rb_len[zl - 1][e] << 4 | e);
+    };
+    T.rb0 = bytes(0, rb);
+    T.rb1 = bytes(1, rb);
+    uint32_t cb = 0xffu;
+    for (int k = 0; k < 48; ++k)
+        if (SPT.cbp_code[k] == (uint8_t)lane) cb = (uint32_t)k;
+    T.cbp = cb;
+    return T;
+}
 
-/* coeff_token (9.2.1): lane e tests entry e (4 * TotalCoeff + TrailingOnes) */
-__device__ __attribute__((always_inline)) inline bool wrd_token(WRd &r, const LaneTabs &T, int nC, int &tc, int &t1)
+/* byte entry `idx` of a byte table spread over registers v0, v1, v2 */
+__device__ inline uint32_t tab_byte(uint32_t v0, uint32_t v1, uint32_t v2, uint32_t idx)
+{
+    const uint32_t v = idx < 256u ? v0 : (idx < 512u ? v1 : v2);
+    return ((uint32_t)__builtin_amdgcn_readlane(v, idx & 63u) >> (8u * ((idx >> 6) & 3u))) & 255u;
+}
+
+/* leading zeros of the 32-bit peek, and the `nb` bits after its first 1
+ * with the count clamped to lzmax (the bits then belong to no code) */
+__device__ inline uint32_t lz_index(uint32_t x, int lzmax, int nb)
+{
+    const int lz = x ? __clz((int)x) : 32;
+    const int l = lz < lzmax ? lz : lzmax;
+    return (uint32_t)l << nb | ((x << (l + 1)) >> (32 - nb));
+}
+
+/* coeff_token (9.2.1) */
+__device__ __attribute__((always_inline)) inline bool wrd_token(SRd &r, const LaneTabs &T, int nC, int &tc, int &t1)
 {
     if (nC >= 8) {
         const uint32_t c = r.u(6);
@@ -238,41 +356,40 @@ __device__ __attribute__((always_inline)) inline bool wrd_token(WRd &r, const La
         t1 = (int)(c & 3u);
         return t1 <= tc;
     }
-    const uint32_t x = r.peek(16);
-    const int tb = nC == -1 ? 3 : (nC < 2 ? 0 : (nC < 4 ? 1 : 2));
-    const uint32_t v = half(tb < 2 ? T.ct01 : T.ct2d, tb & 1);
-    uint32_t len = 0;
-    int e = match(v, x, len);
-    if (e < 0 && tb != 3) {
-        const uint32_t vx = half(tb < 2 ? T.cx01 : T.cx2, tb & 1);
-        const int e2 = match(vx, x, len);
-        e = e2 < 0 ? -1 : 64 + e2;
+    const uint32_t x = r.peek32();
+    int lz = x ? __clz((int)x) : 32;
+    if (lz > 15) {                       /* only chroma DC has an all-zero code ("0000000") */
+        if (nC != -1) return false;
+        lz = 15;
     }
-    if (e < 0) return false;
-    r.skip((int)len);
-    tc = e >> 2;
-    t1 = e & 3;
+    const uint32_t idx = (uint32_t)lz << 3 | ((x << (lz + 1)) >> 29);
+    const uint32_t v = nC == -1 ? T.ct3 : (nC < 2 ? T.ct0 : (nC < 4 ? T.ct1 : T.ct2));
+    const uint32_t e = ((uint32_t)__builtin_amdgcn_readlane(v, idx & 63u) >> (idx & 64u ? 16 : 0)) & 0xffffu;
+    if (!e) return false;
+    r.skip(e >> 8);
+    tc = (int)((e >> 2) & 31u);
+    t1 = (int)(e & 3u);
     return true;
 }
 
 /* the body of a block (9.2.2-9.2.4), consumed, not kept */
-__device__ __attribute__((always_inline)) inline bool wrd_body(WRd &r, const LaneTabs &T, int tc, int t1, int maxc)
+__device__ __attribute__((always_inline)) inline bool wrd_body(SRd &r, const LaneTabs &T, int tc, int t1, int maxc)
 {
-    const int lane = threadIdx.x & 63;
     if (tc == 0) return true;
-    r.skip(t1);
+    r.skip((uint32_t)t1);
     int sl = (tc > 10 && t1 < 3) ? 1 : 0;
     for (int k = t1; k < tc; ++k) {
         const uint32_t x = r.peek32();
         const int prefix = x ? __clz((int)x) : 32;
         if (prefix > 15) return false;                       /* High profiles only */
-        r.skip(prefix + 1);
         int ssize = sl;
         if (prefix == 14 && sl == 0) ssize = 4;
-        if (prefix >= 15) ssize = prefix - 3;
-        int code = min(prefix, 15) << sl;
-        if (ssize) code += (int)r.u(ssize);
-        if (prefix >= 15 && sl == 0) code += 15;
+        if (prefix == 15) ssize = 12;
+        /* level_suffix: the ssize bits after the prefix's 1 (<= 28 bits in all) */
+        const uint32_t suf = (uint32_t)(((uint64_t)(x << (prefix + 1))) >> (32 - ssize));
+        r.skip((uint32_t)(prefix + 1 + ssize));
+        int code = (prefix << sl) + (int)suf;
+        if (prefix == 15 && sl == 0) code += 15;
         if (k == t1 && t1 < 3) code += 2;
         const int a = (code + 2) >> 1;                       /* |level| */
         if (sl == 0) sl = 1;
@@ -280,37 +397,24 @@ __device__ __attribute__((always_inline)) inline bool wrd_body(WRd &r, const Lan
     }
     int zl = 0;
     if (tc < maxc) {
-        const uint32_t x = r.peek(16);
-        const int row = tc - 1;
-        uint32_t v;
+        const uint32_t x = r.peek32();
+        uint32_t e;
         if (maxc == 4) {
-            v = half(row < 2 ? T.tzd01 : T.tzd2, row & 1);
+            e = tab_byte(T.tzd, T.tzd, T.tzd, (uint32_t)(tc - 1) * 16u + lz_index(x, 3, 2));
         } else {
-            const int q = row >> 1;       /* uniform: a select tree, no indexing */
-            const uint32_t w01 = q & 1 ? T.tz1 : T.tz0, w23 = q & 1 ? T.tz3 : T.tz2;
-            const uint32_t w45 = q & 1 ? T.tz5 : T.tz4, w67 = q & 1 ? T.tz7 : T.tz6;
-            const uint32_t w03 = q & 2 ? w23 : w01, w47 = q & 2 ? w67 : w45;
-            v = half(q & 4 ? w47 : w03, row & 1);
+            e = tab_byte(T.tz0, T.tz1, T.tz2, (uint32_t)(tc - 1) * 40u + lz_index(x, 9, 2));
         }
-        if (lane > maxc - tc) v = 0;
-        uint32_t len = 0;
-        const int tz = match(v, x, len);
-        if (tz < 0) return false;
-        r.skip((int)len);
-        zl = tz;
+        if (!e) return false;
+        r.skip(e >> 4);
+        zl = (int)(e & 15u);
     }
     for (int k = 0; k < tc - 1 && zl > 0; ++k) {
-        const uint32_t x = r.peek(16);
-        const int zi = min(zl, 7) - 1;
-        const int q = zi >> 1;
-        const uint32_t w01 = q & 1 ? T.rb1 : T.rb0, w23 = q & 1 ? T.rb3 : T.rb2;
-        uint32_t v = half(q & 2 ? w23 : w01, zi & 1);
-        if (lane > zl) v = 0;
-        uint32_t len = 0;
-        const int run = match(v, x, len);
-        if (run < 0) return false;
-        r.skip((int)len);
-        zl -= run;
+        const uint32_t x = r.peek32();
+        const uint32_t e = tab_byte(T.rb0, T.rb1, T.rb1,
+                                    (uint32_t)(min(zl, 7) - 1) * 48u + lz_index(x, 11, 2));
+        if (!e || (int)(e & 15u) > zl) return false;
+        r.skip(e >> 4);
+        zl -= (int)(e & 15u);
     }
     return true;
 }
@@ -321,7 +425,7 @@ struct PieceOut {
 };
 
 /* one residual block: coeff_token, then the body; lane pi keeps the fields */
-__device__ __attribute__((always_inline)) inline bool wrd_piece(WRd &r, const LaneTabs &T, int pi,
+__device__ __attribute__((always_inline)) inline bool wrd_piece(SRd &r, const LaneTabs &T, int pi,
                                                                 int nC, int maxc, PieceOut &po)
 {
     int tc, t1;
@@ -364,9 +468,21 @@ struct UMv {
     int ref, mx, my;
 };
 
+/* the pieces whose TotalCoeff an MB below reads (luma 12..15, chroma AC
+ * 20, 21, 24, 25) -> slot 0..7; -1 for the others */
+__device__ inline int tc_slot(int j)
+{
+    return j >= 12 && j < 16 ? j - 12 : ((j == 20 || j == 21) ? j - 16 : ((j == 24 || j == 25) ? j - 18 : -1));
+}
+
+/* 6.7 KB: 16 parse workgroups fit a CU, so every slice of a 4,096-slice
+ * launch is resident at once */
 struct ParseLds {
-    int32_t mref[2][PARSE_MAXW], mmx[2][PARSE_MAXW], mmy[2][PARSE_MAXW];  /* rows y-1, y by parity */
-    uint8_t tcrow[PARSE_MAXW][SPLICE_PIECES];                              /* TotalCoeffs, row above */
+    uint32_t rmv[PARSE_MAXW][4];         /* bottom 4x4 blocks of the MBs above (row y-1 ahead  */
+    int8_t rrf[PARSE_MAXW][4];           /* of x, row y behind it): mv, ref                     */
+    uint8_t tcrow[PARSE_MAXW][8];        /* their bottom pieces' TotalCoeffs (tc_slot)          */
+    uint32_t cmv[16], lmv[4];            /* this MB's blocks as they decode; the left MB's right */
+    int8_t crf[16], lrf[4];              /* column                                               */
 };
 
 __global__ __launch_bounds__(64) void k_splice_parse(int n, const int32_t *__restrict__ list,
@@ -432,8 +548,8 @@ __global__ __launch_bounds__(64) void k_splice_parse(int n, const int32_t *__res
     }
     __syncthreads();
     nb = __builtin_amdgcn_readfirstlane(nb);
-    WRd r{o, (nb + 3u) >> 2, 8u * nb, 0, 0, 0, false};
-    r.fill(0);
+    SRd r;
+    r.init(o, (nb + 3u) >> 2, 8u * nb);
     const LaneTabs T = lane_tabs();
 
     status = SCROLL_SPLICE_ERR_HEADER;
@@ -486,23 +602,44 @@ __global__ __launch_bounds__(64) void k_splice_parse(int n, const int32_t *__res
         int m = 0, qp_c = 26;
         const Mv none{-1, 0, 0};
         uint32_t tc_left = 0;              /* lane j: TotalCoeff of piece j, MB to the left */
-        Mv left{-1, 0, 0};
-        /* motion of MB (x, y) from the LDS rows */
+        Mv ul = none;                      /* block (3, 3) of the MB above-left */
+        /* whole-MB neighbours of MB (x, y): A = the left MB's block (3, 0),
+         * B = the above MB's (0, 3), C = the above-right MB's (0, 3), else
+         * D = the above-left MB's (3, 3) */
         auto ctx = [&](int x, int y, Mv &A, Mv &B, Mv &C) {
-            const int py = (y - 1) & 1;
-            A = x ? left : none;
-            auto at = [&](int xx) { return Mv{L.mref[py][xx], L.mmx[py][xx], L.mmy[py][xx]}; };
-            B = y ? at(x) : none;
-            C = y ? (x + 1 < W ? at(x + 1) : (x ? at(x - 1) : none)) : none;
+            A = x ? unpk_mv(L.lrf[0], L.lmv[0]) : none;
+            B = y ? unpk_mv(L.rrf[x][0], L.rmv[x][0]) : none;
+            C = y ? (x + 1 < W ? unpk_mv(L.rrf[x + 1][0], L.rmv[x + 1][0]) : (x ? ul : none)) : none;
         };
-        auto finish = [&](int x, int y, const Mv &me) {    /* context for the MBs to come */
-            if (lane == 0) {
-                L.mref[y & 1][x] = me.ref;
-                L.mmx[y & 1][x] = me.mx;
-                L.mmy[y & 1][x] = me.my;
+        /* block (cx, cy) relative to MB (x, y) for a (sub-)partition (6.4.11.7):
+         * inside the MB once decoded (done), right of it never */
+        auto nb = [&](int x, int y, int cx, int cy, uint32_t done) -> Mv {
+            if (cy >= 0) {
+                if (cx >= 4) return none;
+                if (cx >= 0) {
+                    const int q = 4 * cy + cx;
+                    return (done >> q) & 1u ? unpk_mv(L.crf[q], L.cmv[q]) : none;
+                }
+                return x ? unpk_mv(L.lrf[cy], L.lmv[cy]) : none;
             }
-            left = me;
+            if (!y) return none;
+            if (cx < 0) return x ? ul : none;
+            if (cx < 4) return unpk_mv(L.rrf[x][cx], L.rmv[x][cx]);
+            return x + 1 < W ? unpk_mv(L.rrf[x + 1][0], L.rmv[x + 1][0]) : none;
         };
+        /* context for the MBs to come: the bottom row and right column of MB
+         * (x, y) -- from one motion, or from the decoded blocks */
+        auto finish = [&](int x, int y, bool parted, const Mv &me) {
+            ul = y ? unpk_mv(L.rrf[x][3], L.rmv[x][3]) : none;    /* read before it is replaced */
+            if (lane < 4) {
+                const uint32_t v = pk_mv(me.mx, me.my);
+                L.rmv[x][lane] = parted ? L.cmv[12 + lane] : v;
+                L.rrf[x][lane] = parted ? L.crf[12 + lane] : (int8_t)me.ref;
+                L.lmv[lane] = parted ? L.cmv[4 * lane + 3] : v;
+                L.lrf[lane] = parted ? L.crf[4 * lane + 3] : (int8_t)me.ref;
+            }
+        };
+        const int ts = tc_slot(lane);
         while (m < nmb) {
             const uint32_t run = r.ue();
             if (r.bad || r.over() || run > (uint32_t)(nmb - m)) goto done;
@@ -520,38 +657,85 @@ __global__ __launch_bounds__(64) void k_splice_parse(int n, const int32_t *__res
                     R->mx = px;
                     R->my = py;
                     R->skip = 1;
+                    R->part = 0;
                 }
                 if (lane < SPLICE_PIECES) {
                     R->tc[lane] = 0;
                     R->t1[lane] = 0;
                     R->blen[lane] = 0;
                     R->boff[lane] = 0;
-                    L.tcrow[x][lane] = 0;
                 }
+                if (ts >= 0) L.tcrow[x][ts] = 0;
                 tc_left = 0;
-                finish(x, y, Mv{0, px, py});
+                finish(x, y, false, Mv{0, px, py});
             }
             if (m == nmb) break;
             const int x = m % W, y = m / W;
-            if (r.ue() != 0) {                                     /* mb_type */
+            const uint32_t mbt = r.ue();                               /* mb_type (Table 7-13) */
+            if (r.bad || r.over() || mbt > 4) {
                 status = r.bad || r.over() ? SCROLL_SPLICE_ERR_SYNTAX : SCROLL_SPLICE_ERR_MBTYPE;
                 goto done;
             }
-            int ref = 0;
-            if (nrefs == 2) ref = 1 - (int)r.u(1);
-            else if (nrefs > 2) ref = (int)r.ue();
-            const int dx = r.se(), dy = r.se();
-            Mv A, B, C;
-            ctx(x, y, A, B, C);
-            int px, py;
-            predict_spec(A, B, C, ref, px, py);
-            const long long mx = (long long)px + dx, my = (long long)py + dy;
+            Mv me{0, 0, 0};
+            const int part = mbt == 4 ? 3 : (int)mbt;
+            uint32_t sub = 0;
+            if (mbt == 0) {
+                int ref = 0;
+                if (nrefs == 2) ref = 1 - (int)r.u(1);
+                else if (nrefs > 2) ref = (int)r.ue();
+                const int dx = r.se(), dy = r.se();
+                Mv A, B, C;
+                ctx(x, y, A, B, C);
+                int px, py;
+                predict_spec(A, B, C, ref, px, py);
+                const long long mx = (long long)px + dx, my = (long long)py + dy;
+                if (ref >= nrefs || mx < -SPLICE_MAX_MV || mx > SPLICE_MAX_MV || my < -SPLICE_MAX_MV ||
+                    my > SPLICE_MAX_MV)
+                    goto done;
+                me = Mv{ref, (int)mx, (int)my};
+            } else {
+                /* sub_mb_pred / mb_pred (7.3.5.1-2): sub_mb_types, ref_idx per
+                 * mbPartIdx (P_8x8ref0: all 0), mvd per (sub-)partition */
+                if (part == 3)
+                    for (int i = 0; i < 4; ++i) {
+                        const uint32_t st = r.ue();
+                        if (st > 3u) goto done;
+                        sub |= st << (2 * i);
+                    }
+                const int nref = part == 3 ? 4 : 2;
+                uint32_t refw = 0;                                     /* ref of mbPartIdx i: byte i */
+                if (mbt != 4)
+                    for (int i = 0; i < nref; ++i) {
+                        int rf = 0;
+                        if (nrefs == 2) rf = 1 - (int)r.u(1);
+                        else if (nrefs > 2) rf = (int)r.ue();
+                        if (rf >= nrefs) goto done;
+                        refw |= (uint32_t)rf << (8 * i);
+                    }
+                uint32_t dn = 0;
+                bool ok = true;
+                for_parts(part, sub, [&](int bx, int by, int bw, int bh, int mp) {
+                    const int rf = (int)((refw >> (8 * mp)) & 255u);
+                    const int dx = r.se(), dy = r.se();
+                    int px, py;
+                    predict_part(part, mp, bx, by, bw, rf, [&](int cx, int cy) { return nb(x, y, cx, cy, dn); },
+                                 px, py);
+                    const long long mx = (long long)px + dx, my = (long long)py + dy;
+                    ok = ok && mx >= -SPLICE_MAX_MV && mx <= SPLICE_MAX_MV && my >= -SPLICE_MAX_MV &&
+                         my <= SPLICE_MAX_MV;
+                    const uint32_t pm = part_mask(bx, by, bw, bh);
+                    if (lane < 16 && ((pm >> lane) & 1u)) {
+                        L.cmv[lane] = pk_mv((int)mx, (int)my);
+                        L.crf[lane] = (int8_t)rf;
+                    }
+                    dn |= pm;
+                });
+                if (!ok || r.bad || r.over()) goto done;
+                me = unpk_mv(L.crf[0], L.cmv[0]);
+            }
             const uint32_t code = r.ue();
-            const uint64_t cm = __ballot(T.cbp == code);
-            const int cbp = first_lane(cm);
-            if (r.bad || r.over() || ref >= nrefs || cbp < 0 || mx < -SPLICE_MAX_MV || mx > SPLICE_MAX_MV ||
-                my < -SPLICE_MAX_MV || my > SPLICE_MAX_MV)
-                goto done;
+            const int cbp = code < 48u ? (int)__builtin_amdgcn_readlane(T.cbp, code) : -1;
+            if (r.bad || r.over() || cbp < 0) goto done;
             int qpd = 0;
             /* lane j: piece j of this MB */
             uint32_t my_tc = 0, my_t1 = 0, my_off = 0, my_len = 0;
@@ -564,7 +748,9 @@ __global__ __launch_bounds__(64) void k_splice_parse(int n, const int32_t *__res
                 if (d > 25) d -= 52;
                 qpd = d;
                 qp_c = qp;
-                const uint32_t tc_top = y && lane < SPLICE_PIECES ? L.tcrow[x][lane] : 0u;
+                /* lane j (12..15, 20, 21, 24, 25): piece j of the MB above, where
+                 * nc_at reads it */
+                const uint32_t tc_top = y && ts >= 0 ? L.tcrow[x][ts] : 0u;
                 PieceOut po{0, 0, 0, 0};
                 for (int blk = 0; blk < 16; ++blk) {
                     if (!(cbp & (1 << (blk >> 2)))) continue;
@@ -585,22 +771,28 @@ __global__ __launch_bounds__(64) void k_splice_parse(int n, const int32_t *__res
             }
             SpliceMbRec *R = rec + m;
             if (lane == 0) {
-                R->ref = (int16_t)ref;
+                R->ref = (int16_t)me.ref;
                 R->cbp = (uint8_t)cbp;
                 R->qpd = (int8_t)qpd;
-                R->mx = (int32_t)mx;
-                R->my = (int32_t)my;
+                R->mx = me.mx;
+                R->my = me.my;
                 R->skip = 0;
+                R->part = (uint8_t)part;
+                R->sub = (uint8_t)sub;
+            }
+            if (part && lane < 16) {
+                R->bref[lane] = L.crf[lane];
+                R->bmv[lane] = L.cmv[lane];
             }
             if (lane < SPLICE_PIECES) {
                 R->tc[lane] = (uint8_t)my_tc;
                 R->t1[lane] = (uint8_t)my_t1;
                 R->blen[lane] = (uint16_t)my_len;
                 R->boff[lane] = my_off;
-                L.tcrow[x][lane] = (uint8_t)my_tc;
             }
+            if (ts >= 0) L.tcrow[x][ts] = (uint8_t)my_tc;
             tc_left = my_tc;
-            finish(x, y, Mv{ref, (int)mx, (int)my});
+            finish(x, y, part != 0, me);
             ++m;
         }
         /* rbsp_slice_trailing_bits (+ zero bytes of a byte stream) */
@@ -622,6 +814,7 @@ done:
 /* ------------------------------------------------------------------------ */
 struct SpliceLds {
     int32_t fr[RING], fx[RING], fy[RING];   /* motion of MB m at m % RING */
+    int32_t fk[RING];                       /* its record if a partitioned spliced MB, else -1 */
     ScrollHintRect rc[SCROLL_HINT_MAX_RECTS];
     int32_t wo[8], wl[8], wv[8];
     uint32_t wsum[NW];
@@ -780,9 +973,13 @@ __global__ __launch_bounds__(DT) void k_splice_stage(DevStream *__restrict__ st,
             hs.finish();
         }
         for (int m0 = 0; m0 < nmb; m0 += DT) {
+            /* the previous window's writing sweep still reads the ring (the
+             * neighbour blocks of its partitioned MBs): wait before refilling */
+            lds_barrier();
             const int m = m0 + t;
             int x = 0, y = 0, k = -1;
             Mv me{0, 0, 0};
+            bool parted = false;
             if (m < nmb) {
                 y = (int)div_m((uint32_t)m, m_mbw);
                 x = m - y * mbw;
@@ -790,8 +987,14 @@ __global__ __launch_bounds__(DT) void k_splice_stage(DevStream *__restrict__ st,
                     k = (y - SF.y0) * SF.w + (x - SF.x0);
                     const SpliceMbRec &mb = rec[k];
                     me = Mv{mb.ref, mb.mx, mb.my};
-                    const int wk = mb.ref - 2;
-                    my_ref_bad |= !(mb.ref == 0 || mb.ref == 1 || (wk >= 0 && wk < c.nwp && L.wv[wk]));
+                    parted = mb.part != 0;
+                    auto valid = [&](int rf) {
+                        const int wk = rf - 2;
+                        return rf == 0 || rf == 1 || (wk >= 0 && wk < c.nwp && L.wv[wk]);
+                    };
+                    my_ref_bad |= !valid(mb.ref);
+                    if (parted)
+                        for (int q = 1; q < 16; ++q) my_ref_bad |= !valid(mb.bref[q]);
                 } else {
                     bool bad;
                     me = field(L.rc, L.wv, nr, x, y, lay, c.nwp, bad);
@@ -800,16 +1003,23 @@ __global__ __launch_bounds__(DT) void k_splice_stage(DevStream *__restrict__ st,
                 L.fr[m & (RING - 1)] = me.ref;
                 L.fx[m & (RING - 1)] = me.mx;
                 L.fy[m & (RING - 1)] = me.my;
+                L.fk[m & (RING - 1)] = parted ? k : -1;
             }
             __syncthreads();
             bool coded = false;
             int px = 0, py = 0;
-            if (m < nmb) {
-                auto at = [&](int q) { return Mv{L.fr[q & (RING - 1)], L.fx[q & (RING - 1)], L.fy[q & (RING - 1)]}; };
-                const Mv none{-1, 0, 0};
-                const Mv A = x > 0 ? at(m - 1) : none;
-                const Mv B = y > 0 ? at(m - mbw) : none;
-                const Mv C = y == 0 ? none : (x + 1 < mbw ? at(m - mbw + 1) : (x > 0 ? at(m - mbw - 1) : none));
+            const Mv none{-1, 0, 0};
+            /* 4x4 block (bx, by) of MB q (partitioned spliced MBs from their record) */
+            auto blk = [&](int q, int bx, int by) {
+                const int kk = L.fk[q & (RING - 1)];
+                if (kk >= 0) return unpk_mv(rec[kk].bref[4 * by + bx], rec[kk].bmv[4 * by + bx]);
+                return Mv{L.fr[q & (RING - 1)], L.fx[q & (RING - 1)], L.fy[q & (RING - 1)]};
+            };
+            if (m < nmb && !parted) {
+                const Mv A = x > 0 ? blk(m - 1, 3, 0) : none;
+                const Mv B = y > 0 ? blk(m - mbw, 0, 3) : none;
+                const Mv C = y == 0 ? none
+                                    : (x + 1 < mbw ? blk(m - mbw + 1, 0, 3) : (x > 0 ? blk(m - mbw - 1, 3, 3) : none));
                 if (spec) {
                     int sx, sy;
                     pskip_mv(x, y, A, B, C, sx, sy);
@@ -821,6 +1031,7 @@ __global__ __launch_bounds__(DT) void k_splice_stage(DevStream *__restrict__ st,
                     predict_ref(A, B, C, me.ref, px, py);
                 }
             }
+            coded |= m < nmb && parted;                            /* predicted per partition */
             int excl, cmax;
             block_excl_max(coded ? m : -1, L.wmax, excl, cmax);
             /* the MB's bits: head, then (spliced) cbp / qp / pieces */
@@ -829,13 +1040,53 @@ __global__ __launch_bounds__(DT) void k_splice_stage(DevStream *__restrict__ st,
                 Lt = x == 0 ? nullptr : (x > SF.x0 ? rec[k - 1].tc : ZERO_TC);
                 Tt = y == 0 ? nullptr : (y > SF.y0 ? rec[k - SF.w].tc : ZERO_TC);
             }
+            /* a partitioned spliced MB's neighbour block (cx, cy) (6.4.11.7) */
+            auto pnb = [&](int cx, int cy, uint32_t dn) {
+                if (cy >= 0) {
+                    if (cx >= 4) return none;
+                    if (cx >= 0)
+                        return (dn >> (4 * cy + cx)) & 1u ? unpk_mv(rec[k].bref[4 * cy + cx], rec[k].bmv[4 * cy + cx])
+                                                          : none;
+                    return x > 0 ? blk(m - 1, 3, cy) : none;
+                }
+                if (y == 0) return none;
+                if (cx < 0) return x > 0 ? blk(m - mbw - 1, 3, 3) : none;
+                if (cx < 4) return blk(m - mbw, cx, 3);
+                return x + 1 < mbw ? blk(m - mbw + 1, 0, 3) : none;
+            };
             auto code_mb = [&](auto &sk) {
                 put_ue(sk, (uint32_t)(m - max(excl, last) - 1));  /* mb_skip_run */
-                sk.put(1, 1);                                      /* P_L0_16x16 */
-                if (nrefs == 2) sk.put((uint32_t)(1 - (me.ref & 1)), 1);
-                else if (nrefs > 2) put_ue(sk, (uint32_t)me.ref);
-                put_se(sk, me.mx - px);
-                put_se(sk, me.my - py);
+                if (parted) {
+                    const SpliceMbRec &mb = rec[k];
+                    const int part = mb.part;
+                    const uint32_t sub = mb.sub;
+                    put_ue(sk, (uint32_t)part);                    /* P_L0_L0_16x8 / 8x16, P_8x8 */
+                    if (part == 3)
+                        for (int i = 0; i < 4; ++i) put_ue(sk, (sub >> (2 * i)) & 3u);
+                    for (int i = 0; i < (part == 3 ? 4 : 2); ++i) {  /* ref_idx per mbPartIdx */
+                        const int q = part == 1 ? 8 * i : (part == 2 ? 2 * i : 2 * (i & 1) + 8 * (i >> 1));
+                        const int rf = mb.bref[q];
+                        if (nrefs == 2) sk.put((uint32_t)(1 - (rf & 1)), 1);
+                        else put_ue(sk, (uint32_t)rf);
+                    }
+                    uint32_t dn = 0;
+                    for_parts(part, sub, [&](int bx, int by, int bw, int bh, int mp) {
+                        const int q = 4 * by + bx;
+                        const Mv v = unpk_mv(mb.bref[q], mb.bmv[q]);
+                        int qx, qy;
+                        predict_part(part, mp, bx, by, bw, v.ref, [&](int cx, int cy) { return pnb(cx, cy, dn); },
+                                     qx, qy);
+                        put_se(sk, v.mx - qx);
+                        put_se(sk, v.my - qy);
+                        dn |= part_mask(bx, by, bw, bh);
+                    });
+                } else {
+                    sk.put(1, 1);                                  /* P_L0_16x16 */
+                    if (nrefs == 2) sk.put((uint32_t)(1 - (me.ref & 1)), 1);
+                    else if (nrefs > 2) put_ue(sk, (uint32_t)me.ref);
+                    put_se(sk, me.mx - px);
+                    put_se(sk, me.my - py);
+                }
                 if (k >= 0) splice_tail(sk, rec[k], Lt, Tt, rb);
                 else sk.put(1, 1);                                 /* coded_block_pattern 0 */
             };
@@ -956,8 +1207,9 @@ size_t splice_slot_bound(int mbw, int mbh, int w, int h, size_t nal_bytes)
 {
     /* header <= 1024 bits; every MB head <= 128 bits; a spliced MB adds its
      * body bits (<= the slice's) + 26 coeff_tokens (<= 16 bits each) +
-     * cbp / mb_qp_delta (<= 24 bits) */
+     * cbp / mb_qp_delta (<= 24 bits) + a partitioned head (mb_type, 4
+     * sub_mb_types, 4 ref_idx <= 64 bits; 16 mvd pairs <= 2 x 33 bits each) */
     const size_t bits = 1024 + (size_t)mbw * mbh * 128 + 8 * nal_bytes +
-                        (size_t)w * h * (26 * 16 + 24) + 64;
+                        (size_t)w * h * (26 * 16 + 24 + 64 + 16 * 66) + 64;
     return ((bits / 8 + 64 + DYN_OVF_BYTES) + 255) & ~(size_t)255;
 }

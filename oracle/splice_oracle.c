@@ -217,6 +217,110 @@ static int sp_cbp_of_code(uint32_t code)
     return -1;
 }
 
+/* ------------------------------------------------------------------------ */
+/* partitions and 4x4-block motion (7.3.5.1-2, Tables 7-13 / 7-17, 6.4.11.7, */
+/* 8.4.1.3)                                                                   */
+/* ------------------------------------------------------------------------ */
+typedef struct {
+    int bx, by, bw, bh;          /* 4x4-block units inside the MB */
+    int mb_part;                 /* mbPartIdx (8x8 index for P_8x8) */
+} sp_part;
+
+/* the (sub-)partitions of an MB in decoding order */
+static int sp_partitions(int part, int sub, sp_part *o)
+{
+    int n = 0;
+    if (part == 0) {
+        o[n++] = (sp_part){0, 0, 4, 4, 0};
+    } else if (part == 1) {                                       /* 16x8 */
+        o[n++] = (sp_part){0, 0, 4, 2, 0};
+        o[n++] = (sp_part){0, 2, 4, 2, 1};
+    } else if (part == 2) {                                       /* 8x16 */
+        o[n++] = (sp_part){0, 0, 2, 4, 0};
+        o[n++] = (sp_part){2, 0, 2, 4, 1};
+    } else {
+        for (int i = 0; i < 4; ++i) {
+            const int sx = (i & 1) * 2, sy = (i >> 1) * 2, st = (sub >> (2 * i)) & 3;
+            if (st == 0) {
+                o[n++] = (sp_part){sx, sy, 2, 2, i};
+            } else if (st == 1) {                                 /* 8x4 */
+                o[n++] = (sp_part){sx, sy, 2, 1, i};
+                o[n++] = (sp_part){sx, sy + 1, 2, 1, i};
+            } else if (st == 2) {                                 /* 4x8 */
+                o[n++] = (sp_part){sx, sy, 1, 2, i};
+                o[n++] = (sp_part){sx + 1, sy, 1, 2, i};
+            } else {
+                for (int k = 0; k < 4; ++k) o[n++] = (sp_part){sx + (k & 1), sy + (k >> 1), 1, 1, i};
+            }
+        }
+    }
+    return n;
+}
+
+/* motion per 4x4 block of a picture of W MBs across (one slice: every
+ * in-picture MB before the current one is available) */
+typedef struct {
+    int W;
+    or_mvi *f;
+} sp_field;
+
+static or_mvi *sp_at(const sp_field *F, int x, int y, int bx, int by)
+{
+    return &F->f[(size_t)(4 * y + by) * 4 * (size_t)F->W + 4 * (size_t)x + (size_t)bx];
+}
+
+/* the block at (cx, cy) relative to MB (x, y) (cx, cy in -1..4): outside
+ * the MB the neighbour MB's block, inside it only once decoded (bit
+ * 4 cy + cx of done); unavailable: ref -1, mv 0 */
+static or_mvi sp_nb(const sp_field *F, int x, int y, int cx, int cy, unsigned done)
+{
+    const or_mvi none = {0, 0, -1, 0};
+    if (cy >= 0 && cx >= 4) return none;                          /* right: later in order */
+    if (cy >= 0 && cx >= 0) return (done >> (4 * cy + cx)) & 1u ? *sp_at(F, x, y, cx, cy) : none;
+    const int nx = x + (cx < 0 ? -1 : (cx >= 4 ? 1 : 0)), ny = y + (cy < 0 ? -1 : 0);
+    if (nx < 0 || ny < 0 || nx >= F->W) return none;
+    return *sp_at(F, nx, ny, (cx + 4) & 3, (cy + 4) & 3);
+}
+
+/* neighbours of a whole-MB partition: A, B, C (D when C is unavailable) */
+static void sp_nb16(const sp_field *F, int x, int y, or_mvi *A, or_mvi *B, or_mvi *C, or_mvi *Cr,
+                    or_mvi *D)
+{
+    *A = sp_nb(F, x, y, -1, 0, 0);
+    *B = sp_nb(F, x, y, 0, -1, 0);
+    *Cr = sp_nb(F, x, y, 4, -1, 0);
+    *D = sp_nb(F, x, y, -1, -1, 0);
+    *C = Cr->avail ? *Cr : *D;
+}
+
+/* 8.4.1.3 for (sub-)partition p of an MB partitioned `part` */
+static void sp_mvp(const sp_field *F, int x, int y, unsigned done, int part, const sp_part *p, int ref,
+                   int *px, int *py)
+{
+    const or_mvi A = sp_nb(F, x, y, p->bx - 1, p->by, done);
+    const or_mvi B = sp_nb(F, x, y, p->bx, p->by - 1, done);
+    or_mvi C = sp_nb(F, x, y, p->bx + p->bw, p->by - 1, done);
+    if (!C.avail) C = sp_nb(F, x, y, p->bx - 1, p->by - 1, done);
+    const or_mvi *d = NULL;
+    if (part == 1) d = p->mb_part == 0 ? &B : &A;                  /* 16x8 */
+    if (part == 2) d = p->mb_part == 0 ? &A : &C;                  /* 8x16 */
+    if (d && d->avail && d->ref == ref) {
+        *px = d->mx;
+        *py = d->my;
+        return;
+    }
+    or_spec_predict(&A, &B, &C, ref, px, py);
+}
+
+static void sp_fill(const sp_field *F, int x, int y, const sp_part *p, or_mvi v, unsigned *done)
+{
+    for (int j = 0; j < p->bh; ++j)
+        for (int i = 0; i < p->bw; ++i) {
+            *sp_at(F, x, y, p->bx + i, p->by + j) = v;
+            *done |= 1u << (4 * (p->by + j) + p->bx + i);
+        }
+}
+
 int or_splice_parse(const or_cfg *c, const or_splice *sp, or_splice_mb *mbs, uint8_t *rbsp,
                     size_t *rbsp_n)
 {
@@ -278,8 +382,7 @@ int or_splice_parse(const or_cfg *c, const or_splice *sp, or_splice_mb *mbs, uin
     /* slice data (7.3.4) */
     const int W = sp->w, H = sp->h, nmb = W * H;
     memset(mbs, 0, sizeof(*mbs) * (size_t)nmb);
-    or_mvi *fld = (or_mvi *)calloc((size_t)nmb, sizeof(or_mvi));
-    or_mvi dummy[1] = {{0, 0, -1, 0}};
+    sp_field F = {W, (or_mvi *)calloc((size_t)nmb * 16, sizeof(or_mvi))};
     int m = 0, qp_c = 26, err = OR_SPLICE_OK;
     while (m < nmb && !err) {
         const uint32_t run = rd_ue(&r);
@@ -289,9 +392,8 @@ int or_splice_parse(const or_cfg *c, const or_splice *sp, or_splice_mb *mbs, uin
         }
         for (uint32_t k = 0; k < run; ++k, ++m) {                 /* P_Skip (8.4.1.1) */
             const int x = m % W, y = m / W;
-            or_mvi A, B, C;
-            or_neighbours(x, y, W, y ? fld + (size_t)(y - 1) * W : dummy, x ? &fld[m - 1] : dummy,
-                          &A, &B, &C);
+            or_mvi A, B, C, Cr, D;
+            sp_nb16(&F, x, y, &A, &B, &C, &Cr, &D);
             int px, py;
             or_pskip_motion(x, y, &A, &B, &C, &px, &py);
             or_splice_mb *mb = &mbs[m];
@@ -300,36 +402,69 @@ int or_splice_parse(const or_cfg *c, const or_splice *sp, or_splice_mb *mbs, uin
             mb->my = py;
             mb->qp = qp;
             mb->skip = 1;
-            fld[m] = (or_mvi){px, py, 0, 1};
+            for (int b = 0; b < 16; ++b) {
+                mb->bmx[b] = px;
+                mb->bmy[b] = py;
+                *sp_at(&F, x, y, b & 3, b >> 2) = (or_mvi){px, py, 0, 1};
+            }
         }
         if (m == nmb) break;
         const int x = m % W, y = m / W;
         or_splice_mb *mb = &mbs[m];
-        if (rd_ue(&r) != 0) {                                     /* mb_type P_L0_16x16 */
+        const uint32_t mbt = rd_ue(&r);                           /* mb_type (Table 7-13) */
+        if (r.bad || mbt > 4) {
             err = r.bad ? OR_SPLICE_ERR_SYNTAX : OR_SPLICE_ERR_MBTYPE;
             break;
         }
-        int ref = 0;
-        if (nrefs == 2) ref = 1 - (int)rd_u(&r, 1);               /* te() */
-        else if (nrefs > 2) ref = (int)rd_ue(&r);
-        const int dx = rd_se(&r), dy = rd_se(&r);
-        or_mvi A, B, C;
-        or_neighbours(x, y, W, y ? fld + (size_t)(y - 1) * W : dummy, x ? &fld[m - 1] : dummy, &A,
-                      &B, &C);
-        int px, py;
-        or_spec_predict(&A, &B, &C, ref, &px, &py);
-        const long long mx = (long long)px + dx, my = (long long)py + dy;
+        const int part = mbt == 4 ? 3 : (int)mbt;
+        int sub = 0;
+        if (part == 3)                                            /* sub_mb_pred (7.3.5.2) */
+            for (int i = 0; i < 4; ++i) {
+                const uint32_t st = rd_ue(&r);
+                if (st > 3) err = OR_SPLICE_ERR_SYNTAX;
+                sub |= (int)(st & 3u) << (2 * i);
+            }
+        const int nref = part == 0 ? 1 : (part == 3 ? 4 : 2);
+        int refs[4] = {0, 0, 0, 0};
+        if (mbt != 4)
+            for (int i = 0; i < nref; ++i) {                      /* ref_idx_l0: te() */
+                if (nrefs == 2) refs[i] = 1 - (int)rd_u(&r, 1);
+                else if (nrefs > 2) refs[i] = (int)rd_ue(&r);
+                if (refs[i] >= nrefs) err = OR_SPLICE_ERR_SYNTAX;
+            }
+        sp_part ps[16];
+        const int np = sp_partitions(part, sub, ps);
+        unsigned done = 0;
+        for (int k = 0; k < np && !err; ++k) {                   /* mvd_l0 per (sub-)partition */
+            const int ref = refs[ps[k].mb_part];
+            const int dx = rd_se(&r), dy = rd_se(&r);
+            int px, py;
+            sp_mvp(&F, x, y, done, part, &ps[k], ref, &px, &py);
+            const long long mx = (long long)px + dx, my = (long long)py + dy;
+            if (r.bad || mx < -OR_SPLICE_MAX_MV || mx > OR_SPLICE_MAX_MV || my < -OR_SPLICE_MAX_MV ||
+                my > OR_SPLICE_MAX_MV) {
+                err = OR_SPLICE_ERR_SYNTAX;
+                break;
+            }
+            sp_fill(&F, x, y, &ps[k], (or_mvi){(int)mx, (int)my, ref, 1}, &done);
+        }
         const int cbp = sp_cbp_of_code(rd_ue(&r));
-        if (r.bad || ref >= nrefs || cbp < 0 || mx < -OR_SPLICE_MAX_MV || mx > OR_SPLICE_MAX_MV ||
-            my < -OR_SPLICE_MAX_MV || my > OR_SPLICE_MAX_MV) {
+        if (err || r.bad || cbp < 0) {
             err = OR_SPLICE_ERR_SYNTAX;
             break;
         }
-        mb->ref = ref;
-        mb->mx = (int)mx;
-        mb->my = (int)my;
+        for (int b = 0; b < 16; ++b) {
+            const or_mvi v = *sp_at(&F, x, y, b & 3, b >> 2);
+            mb->bref[b] = v.ref;
+            mb->bmx[b] = v.mx;
+            mb->bmy[b] = v.my;
+        }
+        mb->part = part;
+        mb->sub = sub;
+        mb->ref = mb->bref[0];
+        mb->mx = mb->bmx[0];
+        mb->my = mb->bmy[0];
         mb->cbp = cbp;
-        fld[m] = (or_mvi){(int)mx, (int)my, ref, 1};
         if (cbp) {
             const int dq = rd_se(&r);                             /* mb_qp_delta */
             if (dq < -26 || dq > 25) {
@@ -350,7 +485,7 @@ int or_splice_parse(const or_cfg *c, const or_splice *sp, or_splice_mb *mbs, uin
         mb->qp = qp;
         ++m;
     }
-    free(fld);
+    free(F.f);
     if (err) return err;
     /* rbsp_slice_trailing_bits: stop bit, alignment zeros (zero bytes after
      * it are tolerated: trailing_zero_8bits of a byte stream) */
@@ -398,8 +533,7 @@ static size_t sp_compose(uint8_t *dst, size_t cap, or_cfg *c, int off, const or_
     or_scroll_regions(c, off, &a_end, &ra, &mva, &rb, &mvb);
     size_t rcap = 64 + (size_t)mbw * mbh * 24 + (has ? erb_n * 2 + (size_t)w * h * 64 : 0);
     uint8_t *rbsp = (uint8_t *)malloc(rcap);
-    or_mvi *above = (or_mvi *)calloc((size_t)mbw, sizeof(or_mvi));
-    or_mvi *cur = (or_mvi *)calloc((size_t)mbw, sizeof(or_mvi));
+    sp_field F = {mbw, (or_mvi *)calloc((size_t)mbw * mbh * 16, sizeof(or_mvi))};
     uint8_t(*tabove)[OR_SPLICE_PIECES] = calloc((size_t)mbw, OR_SPLICE_PIECES);
     uint8_t(*tcur)[OR_SPLICE_PIECES] = calloc((size_t)mbw, OR_SPLICE_PIECES);
     or_bits b;
@@ -407,18 +541,19 @@ static size_t sp_compose(uint8_t *dst, size_t cap, or_cfg *c, int off, const or_
     or_scroll_header(&b, c);
     int run = 0, bad_hint = 0, bad_ref = 0;
     for (int y = 0; y < mbh; ++y) {
-        or_mvi left = {0, 0, -1, 0};
         for (int x = 0; x < mbw; ++x) {
             const or_splice_mb *mb = NULL;
             if (has && x >= sp->x0 && x < sp->x0 + sp->w && y >= sp->y0 && y < sp->y0 + sp->h)
                 mb = &mbs[(size_t)(y - sp->y0) * sp->w + (x - sp->x0)];
             int ref, mx, my, cbp = 0;
+            const int part = mb ? mb->part : 0;
             if (mb) {
                 ref = mb->ref;
                 mx = mb->mx;
                 my = mb->my;
                 cbp = mb->cbp;
-                if (!or_ref_valid(c, ref)) bad_ref = 1;
+                for (int k = 0; k < (part ? 16 : 1); ++k)
+                    if (!or_ref_valid(c, part ? mb->bref[k] : ref)) bad_ref = 1;
             } else {
                 if (or_hint_motion(r, n, x, y, a_end, ra, mva, rb, mvb, &ref, &mx, &my) &&
                     !or_ref_valid(c, ref))
@@ -426,26 +561,56 @@ static size_t sp_compose(uint8_t *dst, size_t cap, or_cfg *c, int off, const or_
                 mx *= 4;
                 my *= 4;
             }
-            int px, py, coded = 1;
-            if (mode != OR_HINT_EXACT) {
-                or_mvi A, B, C;
-                or_neighbours(x, y, mbw, above, &left, &A, &B, &C);
+            int px = 0, py = 0, coded = 1;
+            or_mvi A, B, C, Cr, D;
+            sp_nb16(&F, x, y, &A, &B, &C, &Cr, &D);
+            if (part) {
+                coded = 1;                                        /* predicted per partition */
+            } else if (mode != OR_HINT_EXACT) {
                 int sx, sy;
                 or_pskip_motion(x, y, &A, &B, &C, &sx, &sy);
                 coded = mode == OR_HINT_SPEC || !(ref == 0 && mx == sx && my == sy && cbp == 0);
                 or_spec_predict(&A, &B, &C, ref, &px, &py);
             } else {
-                or_predict(x, y, mbw, above, &left, ref, &px, &py);
+                /* the reference's get_mv_prediction over the neighbour blocks:
+                 * above[x - 1 .. x + 1] = D, B, C at a stand-in x = 1 of 3 */
+                const or_mvi ab[3] = {D, B, Cr};
+                or_predict(1, y, 3, ab, &A, ref, &px, &py);
             }
             memset(tcur[x], 0, OR_SPLICE_PIECES);
             if (coded) {
                 or_ue(&b, (uint32_t)run);                         /* mb_skip_run */
                 run = 0;
-                or_ue(&b, 0);                                     /* P_L0_16x16 */
-                if (nrefs == 2) or_put(&b, (uint32_t)(1 - (ref & 1)), 1);
-                else if (nrefs > 2) or_ue(&b, (uint32_t)ref);
-                or_se(&b, mx - px);
-                or_se(&b, my - py);
+                if (part) {
+                    sp_part ps[16];
+                    const int np = sp_partitions(part, mb->sub, ps), nref = part == 3 ? 4 : 2;
+                    or_ue(&b, (uint32_t)part);                    /* P_L0_L0_16x8 / 8x16, P_8x8 */
+                    if (part == 3)
+                        for (int i = 0; i < 4; ++i) or_ue(&b, (uint32_t)((mb->sub >> (2 * i)) & 3));
+                    for (int i = 0; i < nref; ++i) {              /* ref_idx_l0 per mbPartIdx */
+                        int k = 0;
+                        while (ps[k].mb_part != i) ++k;
+                        const int rf = mb->bref[4 * ps[k].by + ps[k].bx];
+                        if (nrefs == 2) or_put(&b, (uint32_t)(1 - (rf & 1)), 1);
+                        else or_ue(&b, (uint32_t)rf);
+                    }
+                    unsigned done = 0;
+                    for (int k = 0; k < np; ++k) {                /* mvd per (sub-)partition */
+                        const int q = 4 * ps[k].by + ps[k].bx;
+                        const or_mvi v = {mb->bmx[q], mb->bmy[q], mb->bref[q], 1};
+                        int qx, qy;
+                        sp_mvp(&F, x, y, done, part, &ps[k], v.ref, &qx, &qy);
+                        or_se(&b, v.mx - qx);
+                        or_se(&b, v.my - qy);
+                        sp_fill(&F, x, y, &ps[k], v, &done);
+                    }
+                } else {
+                    or_ue(&b, 0);                                 /* P_L0_16x16 */
+                    if (nrefs == 2) or_put(&b, (uint32_t)(1 - (ref & 1)), 1);
+                    else if (nrefs > 2) or_ue(&b, (uint32_t)ref);
+                    or_se(&b, mx - px);
+                    or_se(&b, my - py);
+                }
                 or_ue(&b, (uint32_t)or_cbp_code(cbp));
                 if (cbp) {
                     or_se(&b, mb->qpd);
@@ -467,12 +632,9 @@ static size_t sp_compose(uint8_t *dst, size_t cap, or_cfg *c, int off, const or_
             } else {
                 run++;                                            /* P_Skip */
             }
-            cur[x] = (or_mvi){mx, my, ref, 1};
-            left = cur[x];
+            if (!part)
+                for (int k = 0; k < 16; ++k) *sp_at(&F, x, y, k & 3, k >> 2) = (or_mvi){mx, my, ref, 1};
         }
-        or_mvi *t = above;
-        above = cur;
-        cur = t;
         uint8_t(*tt)[OR_SPLICE_PIECES] = tabove;
         tabove = tcur;
         tcur = tt;
@@ -489,8 +651,7 @@ static size_t sp_compose(uint8_t *dst, size_t cap, or_cfg *c, int off, const or_
         c->frame_num++;
     }
     free(rbsp);
-    free(above);
-    free(cur);
+    free(F.f);
     free(tabove);
     free(tcur);
     return nb;
@@ -766,15 +927,14 @@ size_t or_ext_slice(uint8_t *dst, size_t cap, const or_cfg *c, int W, int H, uin
     or_se(&b, p->slice_qp_delta);
     if (c->deblock) or_ue(&b, 1);
     int qp = 26 + p->slice_qp_delta;
-    or_mvi *fld = (or_mvi *)calloc((size_t)nmb, sizeof(or_mvi));
+    sp_field F = {W, (or_mvi *)calloc((size_t)nmb * 16, sizeof(or_mvi))};
     uint8_t(*tcs)[OR_SPLICE_PIECES] = calloc((size_t)nmb, OR_SPLICE_PIECES);
-    or_mvi dummy[1] = {{0, 0, -1, 0}};
     int run = 0;
+    const int rg = p->mv_range;
     for (int m = 0; m < nmb; ++m) {
         const int x = m % W, y = m / W;
-        or_mvi A, B, C;
-        or_neighbours(x, y, W, y ? fld + (size_t)(y - 1) * W : dummy, x ? &fld[m - 1] : dummy, &A,
-                      &B, &C);
+        or_mvi A, B, C, Cr, D;
+        sp_nb16(&F, x, y, &A, &B, &C, &Cr, &D);
         if (m == p->bad_mb) {
             or_ue(&b, (uint32_t)run);
             or_ue(&b, (uint32_t)p->bad_type);
@@ -785,25 +945,62 @@ size_t or_ext_slice(uint8_t *dst, size_t cap, const or_cfg *c, int W, int H, uin
         if ((int)(sp_rng(&s) % 1000) < p->skip_pm) {
             int px, py;
             or_pskip_motion(x, y, &A, &B, &C, &px, &py);
-            fld[m] = (or_mvi){px, py, 0, 1};
+            for (int k = 0; k < 16; ++k) *sp_at(&F, x, y, k & 3, k >> 2) = (or_mvi){px, py, 0, 1};
             run++;
             continue;
         }
         int ref = (int)(sp_rng(&s) % (uint32_t)(p->max_ref + 1));
         if (ref >= nrefs) ref = nrefs - 1;
-        const int rg = p->mv_range;
         const int mx = rg ? (int)(sp_rng(&s) % (uint32_t)(2 * rg + 1)) - rg : 0;
         const int my = rg ? (int)(sp_rng(&s) % (uint32_t)(2 * rg + 1)) - rg : 0;
-        int px, py;
-        or_spec_predict(&A, &B, &C, ref, &px, &py);
+        /* a partitioned MB (drawn only when part_pm > 0: the other
+         * parameters keep their slices bit for bit) */
+        int mbt = 0;
+        if (p->part_pm > 0 && (int)(sp_rng(&s) % 1000) < p->part_pm) mbt = 1 + (int)(sp_rng(&s) % 4);
         const int cbp = (int)(sp_rng(&s) % 1000) < p->cbp_pm ? 1 + (int)(sp_rng(&s) % 47) : 0;
         or_ue(&b, (uint32_t)run);
         run = 0;
-        or_ue(&b, 0);
-        if (nrefs == 2) or_put(&b, (uint32_t)(1 - ref), 1);
-        else if (nrefs > 2) or_ue(&b, (uint32_t)ref);
-        or_se(&b, mx - px);
-        or_se(&b, my - py);
+        or_ue(&b, (uint32_t)mbt);
+        if (mbt == 0) {
+            int px, py;
+            or_spec_predict(&A, &B, &C, ref, &px, &py);
+            if (nrefs == 2) or_put(&b, (uint32_t)(1 - ref), 1);
+            else if (nrefs > 2) or_ue(&b, (uint32_t)ref);
+            or_se(&b, mx - px);
+            or_se(&b, my - py);
+            for (int k = 0; k < 16; ++k) *sp_at(&F, x, y, k & 3, k >> 2) = (or_mvi){mx, my, ref, 1};
+        } else {
+            const int part = mbt == 4 ? 3 : mbt;
+            int sub = 0, refs[4] = {ref, ref, ref, ref};
+            if (part == 3)
+                for (int i = 0; i < 4; ++i) {
+                    const int st = (int)(sp_rng(&s) % 4);
+                    sub |= st << (2 * i);
+                    or_ue(&b, (uint32_t)st);
+                }
+            const int nref = part == 3 ? 4 : 2;
+            for (int i = 0; i < nref; ++i) {
+                refs[i] = mbt == 4 ? 0 : (int)(sp_rng(&s) % (uint32_t)(p->max_ref + 1));
+                if (refs[i] >= nrefs) refs[i] = nrefs - 1;
+                if (mbt == 4) continue;
+                if (nrefs == 2) or_put(&b, (uint32_t)(1 - refs[i]), 1);
+                else if (nrefs > 2) or_ue(&b, (uint32_t)refs[i]);
+            }
+            sp_part ps[16];
+            const int np = sp_partitions(part, sub, ps);
+            unsigned done = 0;
+            for (int k = 0; k < np; ++k) {
+                /* motion near the MB's own draw, so predictions and mvds vary */
+                const int vx = mx + (rg ? (int)(sp_rng(&s) % 17) - 8 : 0);
+                const int vy = my + (rg ? (int)(sp_rng(&s) % 17) - 8 : 0);
+                const int rf = refs[ps[k].mb_part];
+                int px, py;
+                sp_mvp(&F, x, y, done, part, &ps[k], rf, &px, &py);
+                or_se(&b, vx - px);
+                or_se(&b, vy - py);
+                sp_fill(&F, x, y, &ps[k], (or_mvi){vx, vy, rf, 1}, &done);
+            }
+        }
         or_ue(&b, (uint32_t)or_cbp_code(cbp));
         if (cbp) {
             const int j = p->qp_jitter;
@@ -832,13 +1029,12 @@ size_t or_ext_slice(uint8_t *dst, size_t cap, const or_cfg *c, int W, int H, uin
                     }
             }
         }
-        fld[m] = (or_mvi){mx, my, ref, 1};
     }
     if (run > 0) or_ue(&b, (uint32_t)run);
     or_trailing(&b);
     const size_t nb = or_nal(dst, cap, p->ref_idc, 1, rbsp, or_bytes(&b));
     free(rbsp);
-    free(fld);
+    free(F.f);
     free(tcs);
     return nb;
 }

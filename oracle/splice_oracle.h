@@ -21,8 +21,11 @@
  * restates the composed list (op k: long_term_pic_num k, as the composer's
  * own slices write it, h264_writer.c:455-539), no
  * deblocking when the PPS allows switching it off (disable_deblocking_filter
- * _idc 1, like the composer's own slices), MBs P_L0_16x16 or P_Skip, any
- * coded_block_pattern, mb_qp_delta and CAVLC residual (level_prefix <= 15).
+ * _idc 1, like the composer's own slices), inter MBs of every P type
+ * (P_L0_16x16, P_L0_L0_16x8, P_L0_L0_8x16, P_8x8 with any sub_mb_types,
+ * P_8x8ref0) and P_Skip, any coded_block_pattern, mb_qp_delta and CAVLC
+ * residual (level_prefix <= 15); intra MBs are not spliced (their sample
+ * prediction would read composed-picture neighbours across the rect edge).
  * Its ref_idx values index the composed stream's list (0 = A, 1 = B, 2 + i =
  * waypoint i) and its motion vectors are displacements in composed-picture
  * coordinates.
@@ -33,6 +36,13 @@
  *   - mb_skip_run, ref_idx te() (composed num_ref_idx = 2 + waypoints) and
  *     mvd (prediction in the composed picture: the reference's
  *     get_mv_prediction in EXACT mode, 8.4.1.3 in PSKIP mode) are re-coded;
+ *   - a partitioned MB keeps its partitioning (P_8x8ref0 becomes P_8x8 with
+ *     ref_idx 0 written) and codes every (sub-)partition's mvd against the
+ *     8.4.1.3 prediction (directional 16x8 / 8x16 rules, 4x4-block
+ *     neighbours, C -> D substitution, not-yet-decoded partitions
+ *     unavailable) in the composed picture, in every mode; neighbours of
+ *     any MB are the 4x4 blocks the standard names (A: left of the top-left
+ *     block, B: above it, C: above-right of the top-right, D: above-left);
  *   - mb_qp_delta is rebased so each MB keeps its external QP;
  *   - every residual block keeps its bits after coeff_token verbatim (they do
  *     not depend on nC); coeff_token is re-coded for the nC of the composed
@@ -57,7 +67,7 @@ extern "C" {
 #define OR_SPLICE_OK 0
 #define OR_SPLICE_ERR_NAL 1      /* not a coded slice of a non-IDR picture        */
 #define OR_SPLICE_ERR_HEADER 2   /* slice header outside the supported syntax     */
-#define OR_SPLICE_ERR_MBTYPE 3   /* an MB other than P_L0_16x16 / P_Skip          */
+#define OR_SPLICE_ERR_MBTYPE 3   /* an intra MB (mb_type > 4 in a P slice)        */
 #define OR_SPLICE_ERR_SYNTAX 4   /* malformed / truncated slice data              */
 #define OR_SPLICE_ERR_REF 5      /* ref_idx not a valid reference of the frame    */
 
@@ -72,11 +82,14 @@ typedef struct {
 
 /* one external MB after parsing */
 typedef struct {
-    int ref, mx, my;             /* quarter pels                             */
+    int ref, mx, my;             /* quarter pels (partitioned: 4x4 block 0's) */
     int cbp, qp, qpd;            /* its QP and the composed mb_qp_delta      */
     int skip;                    /* P_Skip in the external slice             */
     uint8_t tc[OR_SPLICE_PIECES], t1[OR_SPLICE_PIECES];
     uint32_t boff[OR_SPLICE_PIECES], blen[OR_SPLICE_PIECES];  /* body bits in the RBSP */
+    int part;                    /* 0 P_L0_16x16 / P_Skip, 1 16x8, 2 8x16, 3 P_8x8 (and P_8x8ref0) */
+    int sub;                     /* P_8x8: sub_mb_type of 8x8 i in bits 2i..2i+1 (0 8x8, 1 8x4, 2 4x8, 3 4x4) */
+    int bref[16], bmx[16], bmy[16];  /* motion per 4x4 block, raster order  */
 } or_splice_mb;
 
 /* Parse the external slice: mbs[w * h] (raster), its RBSP into rbsp (cap
@@ -136,6 +149,8 @@ typedef struct {
     int bad_type;
     int list_mod;                /* 0 none, 1 the composed list restated (long-term
                                   * k at index k), 2 reversed (unsupported)      */
+    int part_pm;                 /* per mille of coded MBs: P_L0_L0_16x8 / 8x16,
+                                  * P_8x8 (random sub_mb_types) or P_8x8ref0     */
 } or_ext_params;
 size_t or_ext_slice(uint8_t *dst, size_t cap, const or_cfg *c, int w, int h, uint32_t seed,
                     const or_ext_params *p);

@@ -38,11 +38,18 @@ EXT = [  # stand-in encoder parameters for 20x20-MB external slices
     dict(nrefs=4, max_ref=3, mv_range=600, qp_jitter=10, slice_qp_delta=-6),
     dict(ref_idc=1, skip_pm=0, cbp_pm=1000),
     dict(list_mod=1, skip_pm=400),
+    # partitioned MBs: P_L0_L0_16x8 / 8x16, P_8x8 (every sub_mb_type), P_8x8ref0
+    dict(part_pm=600),
+    dict(part_pm=1000, nrefs=3, max_ref=2, skip_pm=0, cbp_pm=800, mv_range=900),
+    dict(part_pm=700, nrefs=1, max_ref=0, skip_pm=300),
 ]
 # composed frames: (offset, mode, rect) on a 320x320 stream scrolling 490..500
 SPLICED = [(490 + i, i % 2, rect) for i, rect in enumerate(
     [(3, 4, 8, 6), (0, 0, 20, 20), (19, 19, 1, 1), (5, 0, 10, 3), (0, 12, 7, 8), (12, 5, 8, 9),
      (2, 2, 16, 16), (9, 9, 2, 2), (0, 0, 1, 20), (1, 18, 19, 2), (4, 4, 12, 12)])]
+# the same with partitioned external MBs (scrolling on past the waypoint)
+SPLICED_PART = [(501 + i, i % 2, rect) for i, rect in enumerate(
+    [(3, 4, 8, 6), (0, 0, 20, 20), (19, 0, 1, 20), (6, 6, 9, 9)])]
 
 
 def _stop_bit(rbsp):
@@ -64,12 +71,13 @@ def cases(oracle):
                    nal_bytes=len(nal), mb_start_bit=b.p, stop_bit=_stop_bit(rbsp)), nal, rbsp
     buf = (ctypes.c_uint8 * (1 << 21))()
     err = ctypes.c_int()
-    for k, (off, mode, rect) in enumerate(SPLICED):
+    for k, (off, mode, rect) in enumerate(SPLICED + SPLICED_PART):
         if oracle.or_needs_waypoint(ctypes.byref(c), off):
             oracle.or_waypoint_nal(buf, len(buf), ctypes.byref(c), off)
         nrefs = 2 + c.nwp
+        part = dict(part_pm=600) if k >= len(SPLICED) else {}
         ext = ext_slice(oracle, c, rect[2], rect[3], 8000 + k, nrefs=nrefs, max_ref=nrefs - 1,
-                        skip_pm=300, cbp_pm=700, big_pm=30, qp_jitter=4)
+                        skip_pm=300, cbp_pm=700, big_pm=30, qp_jitter=4, **part)
         sp = splice_of(*rect, ext)
         n = oracle.or_splice_scroll_nal(buf, len(buf), ctypes.byref(c), off, None, 0, mode,
                                         ctypes.byref(sp), ctypes.byref(err))

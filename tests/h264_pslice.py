@@ -520,10 +520,13 @@ def decode_mv_field(nal, w, h, predictor="spec", **hdr_kw):
 
 
 # ------------------------------------------- general P slice (splice) --------
-# Any CAVLC P slice of P_L0_16x16 / P_Skip MBs: mb_skip_run, motion with the
-# chosen predictor, coded_block_pattern, mb_qp_delta (QP chain from the slice
-# QP) and the residual levels.  Used to check that a spliced MB of a composed
-# NAL decodes to the same syntax elements as in its external slice.
+# Any CAVLC P slice of inter MBs (P_L0_16x16, P_L0_L0_16x8 / 8x16, P_8x8 with
+# sub_mb_types, P_8x8ref0) and P_Skip: mb_skip_run, motion per 4x4 block with
+# the chosen predictor (partitions always with the standard's: 8.4.1.3 with the
+# directional 16x8 / 8x16 rules and the 6.4.11.7 neighbour blocks),
+# coded_block_pattern, mb_qp_delta (QP chain from the slice QP) and the
+# residual levels.  Used to check that a spliced MB of a composed NAL decodes
+# to the same syntax elements as in its external slice.
 
 def _nc(nA, nB):
     if nA >= 0 and nB >= 0:
@@ -531,12 +534,86 @@ def _nc(nA, nB):
     return nA if nA >= 0 else (nB if nB >= 0 else 0)
 
 
+def _parts(mbt, sub):
+    """(sub-)partitions in decoding order: (bx, by, bw, bh, mbPartIdx) in 4x4 units"""
+    if mbt == 0:
+        return [(0, 0, 4, 4, 0)]
+    if mbt == 1:
+        return [(0, 0, 4, 2, 0), (0, 2, 4, 2, 1)]
+    if mbt == 2:
+        return [(0, 0, 2, 4, 0), (2, 0, 2, 4, 1)]
+    out = []
+    for i in range(4):
+        sx, sy = (i % 2) * 2, (i // 2) * 2
+        st = sub[i]
+        if st == 0:
+            out.append((sx, sy, 2, 2, i))
+        elif st == 1:
+            out += [(sx, sy, 2, 1, i), (sx, sy + 1, 2, 1, i)]
+        elif st == 2:
+            out += [(sx, sy, 1, 2, i), (sx + 1, sy, 1, 2, i)]
+        else:
+            out += [(sx + k % 2, sy + k // 2, 1, 1, i) for k in range(4)]
+    return out
+
+
+class _BlockField:
+    """motion (ref, mx, my) per 4x4 block of a picture of mbw x mbh MBs"""
+
+    def __init__(self, mbw, mbh):
+        self.mbw = mbw
+        self.f = [[None] * (4 * mbw) for _ in range(4 * mbh)]
+
+    def nb(self, x, y, cx, cy, done):
+        """block (cx, cy) relative to MB (x, y); inside the MB only once decoded"""
+        if cy >= 0 and cx >= 4:
+            return None
+        if cy >= 0 and cx >= 0:
+            return self.f[4 * y + cy][4 * x + cx] if (4 * cy + cx) in done else None
+        nx, ny = x + (-1 if cx < 0 else (1 if cx >= 4 else 0)), y + (-1 if cy < 0 else 0)
+        if nx < 0 or ny < 0 or nx >= self.mbw:
+            return None
+        return self.f[4 * ny + (cy % 4)][4 * nx + (cx % 4)]
+
+    def set(self, x, y, bx, by, bw, bh, v, done):
+        for j in range(bh):
+            for i in range(bw):
+                self.f[4 * y + by + j][4 * x + bx + i] = v
+                done.add(4 * (by + j) + bx + i)
+
+    def mb16(self, x, y):
+        A, B = self.nb(x, y, -1, 0, ()), self.nb(x, y, 0, -1, ())
+        C = self.nb(x, y, 4, -1, ())
+        if C is None:
+            C = self.nb(x, y, -1, -1, ())
+        return A, B, C
+
+
+def mvp_part(F, x, y, done, mbt, p, ref):
+    bx, by, bw, _, mp = p
+    A, B = F.nb(x, y, bx - 1, by, done), F.nb(x, y, bx, by - 1, done)
+    C = F.nb(x, y, bx + bw, by - 1, done)
+    if C is None:
+        C = F.nb(x, y, bx - 1, by - 1, done)
+    d = None
+    if mbt == 1:
+        d = B if mp == 0 else A
+    elif mbt == 2:
+        d = A if mp == 0 else C
+    if d is not None and d[0] == ref:
+        return d[1], d[2]
+    return mvp_spec(A, B, C, ref)
+
+
 def decode_p_slice(nal, w, h, predictor="spec", log2_mfn=4, poc_type=2, log2_poc=4, deblock=1,
-                   nrefs_default=2):
-    """-> (header, mbs[y][x] = dict(ref, mx, my, skip, cbp, qp, luma, cdc, cac))
+                   nrefs_default=2, trace=None):
+    """-> (header, mbs[y][x] = dict(ref, mx, my, skip, cbp, qp, luma, cdc, cac,
+    mbt, sub, blocks))
 
     nal: Annex-B NAL (start code optional).  Unavailable neighbours are the
-    picture edges only (one slice per picture)."""
+    picture edges only (one slice per picture).  mbt: the mb_type (0..4),
+    blocks: (ref, mx, my) per 4x4 block in raster order; ref / mx / my are
+    block 0's."""
     if nal[:4] == b"\x00\x00\x00\x01":
         nal = nal[4:]
     elif nal[:3] == b"\x00\x00\x01":
@@ -577,30 +654,50 @@ def decode_p_slice(nal, w, h, predictor="spec", log2_mfn=4, poc_type=2, log2_poc
             b.se(); b.se()
     pred = mvp_spec if predictor == "spec" else mvp_ref
     mbw, mbh = w // 16, h // 16
-    field = [[None] * mbw for _ in range(mbh)]
+    F = _BlockField(mbw, mbh)
     mbs = [[None] * mbw for _ in range(mbh)]
     tcs = [[None] * mbw for _ in range(mbh)]
     m, nmb = 0, mbw * mbh
+
+    def te():
+        return (1 - b.u(1)) if nrefs == 2 else (b.ue() if nrefs > 2 else 0)
+
     while m < nmb:
         run = b.ue()
         for _ in range(run):
             y, x = divmod(m, mbw)
             assert y < mbh, "mb_skip_run past the picture"
-            mv = pskip_mv(*_neigh(field, x, y, mbw))
-            field[y][x] = (0,) + mv
+            mv = pskip_mv(*F.mb16(x, y))
+            F.set(x, y, 0, 0, 4, 4, (0,) + mv, set())
             tcs[y][x] = [0] * 24
-            mbs[y][x] = dict(ref=0, mx=mv[0], my=mv[1], skip=True, cbp=0, qp=qp,
+            mbs[y][x] = dict(ref=0, mx=mv[0], my=mv[1], skip=True, cbp=0, qp=qp, mbt=0, sub=None,
+                             blocks=[(0,) + mv] * 16,
                              luma=[[0] * 16 for _ in range(16)], cdc=[[0] * 4] * 2,
                              cac=[[[0] * 15 for _ in range(4)] for _ in range(2)])
             m += 1
         if m >= nmb:
             break
         y, x = divmod(m, mbw)
-        assert b.ue() == 0, "mb_type P_L0_16x16"
-        ref = (1 - b.u(1)) if nrefs == 2 else (b.ue() if nrefs > 2 else 0)
-        dx, dy = b.se(), b.se()
-        px, py = pred(*_neigh(field, x, y, mbw), ref)
-        field[y][x] = (ref, px + dx, py + dy)
+        if trace is not None:
+            trace.append((m, b.p))
+        mbt = b.ue()
+        assert mbt <= 4, "an inter mb_type"
+        sub = [b.ue() for _ in range(4)] if mbt >= 3 else None
+        assert sub is None or max(sub) <= 3
+        nref = 1 if mbt == 0 else (4 if mbt >= 3 else 2)
+        refs = [0] * 4 if mbt == 4 else [te() for _ in range(nref)]
+        done = set()
+        if mbt == 0:
+            dx, dy = b.se(), b.se()
+            px, py = pred(*F.mb16(x, y), refs[0])
+            F.set(x, y, 0, 0, 4, 4, (refs[0], px + dx, py + dy), done)
+        else:
+            for p in _parts(mbt, sub):
+                dx, dy = b.se(), b.se()
+                rf = refs[p[4]]
+                px, py = mvp_part(F, x, y, done, mbt, p, rf)
+                F.set(x, y, p[0], p[1], p[2], p[3], (rf, px + dx, py + dy), done)
+        blocks = [F.f[4 * y + k // 4][4 * x + k % 4] for k in range(16)]
         cbp = GOLOMB_TO_INTER_CBP[b.ue()]
         t = [0] * 24
         luma = [[0] * 16 for _ in range(16)]
@@ -631,8 +728,8 @@ def decode_p_slice(nal, w, h, predictor="spec", log2_mfn=4, poc_type=2, log2_poc
                             nB = t[i - 2] if by > 0 else (top[i + 2] if top else -1)
                             cac[p][k], t[i] = cavlc_block(b, _nc(nA, nB), 15)
         tcs[y][x] = t
-        mbs[y][x] = dict(ref=ref, mx=px + dx, my=py + dy, skip=False, cbp=cbp, qp=qp, luma=luma,
-                         cdc=cdc, cac=cac)
+        mbs[y][x] = dict(ref=blocks[0][0], mx=blocks[0][1], my=blocks[0][2], skip=False, cbp=cbp, qp=qp,
+                         mbt=mbt, sub=sub, blocks=blocks, luma=luma, cdc=cdc, cac=cac)
         m += 1
     assert b.u(1) == 1, "stop bit"
     while b.p & 7:

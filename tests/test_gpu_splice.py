@@ -58,7 +58,7 @@ def plan(oracle, w, h, offsets, seed, p_splice=0.7, p_hint=0.3, modes=(EXACT, PS
                           skip_pm=rng.choice([0, 200, 600]), cbp_pm=rng.choice([300, 800, 1000]),
                           big_pm=rng.choice([0, 30]), mv_range=rng.choice([8, 200]),
                           slice_qp_delta=rng.randint(-4, 4), qp_jitter=rng.choice([0, 3]),
-                          ref_idc=rng.choice([0, 1]))
+                          ref_idc=rng.choice([0, 1]), part_pm=rng.choice([0, 300, 1000]))
                 kw.update(ext_kw or {})
                 sp = (x0, y0, sw, sh, ext_slice(oracle, c, sw, sh, seed * 100003 + s * 1009 + t, **kw))
             frames[(s, t)] = (rects, mode, sp)
@@ -113,13 +113,29 @@ def test_random_splices(gpu, oracle, w, h, seed):
     b.close()
 
 
+def test_partitioned_splices(gpu, oracle):
+    """every external MB partitioned (P_L0_L0_16x8 / 8x16, P_8x8 with random
+    sub_mb_types, P_8x8ref0) or skipped, waypoint references, hints, all
+    three modes: the composed 16x16 MBs around them predict from their 4x4
+    blocks"""
+    w, h = 640, 480
+    offs = synthetic_offsets(4, 16, h, first_stream=9)
+    offs[2] = np.arange(486, 502)
+    frames, want = plan(oracle, w, h, offs, 31, p_splice=0.9, p_hint=0.4, max_rect=(12, 9),
+                        ext_kw=dict(part_pm=1000, skip_pm=150, mv_range=300))
+    b, rc = gpu_streams(gpu, w, h, offs, frames)
+    assert rc == 0, gpu.last_error()
+    check_equal(b, want)
+    b.close()
+
+
 def test_large_rect_4k_and_ep_path(gpu, oracle, scroll):
     """3840x2160, up to 25x25 MB splices with large levels; again with the
     dynamic emit's EP list capped at 4 (every NAL through k_dyn_emit)"""
     w, h = 3840, 2160
     offs = np.array([[490, 496, 500, 992], [1984, 1990, 2000, 700]], np.int32)
     frames, want = plan(oracle, w, h, offs, 11, p_splice=1.0, max_rect=(25, 25),
-                        ext_kw=dict(cbp_pm=1000, big_pm=100, mv_range=2000))
+                        ext_kw=dict(cbp_pm=1000, big_pm=100, mv_range=2000, part_pm=500))
     for debug in (0, scroll.SCROLL_DEBUG_DYN_EPCAP4):
         b, rc = gpu_streams(gpu, w, h, offs, frames, arena=64 << 20, debug=debug)
         assert rc == 0, gpu.last_error()
@@ -169,7 +185,7 @@ def test_errors_fail_only_their_stream(gpu, oracle, scroll):
     c = _cfg(oracle, w, h)
     good = ext_slice(oracle, c, 4, 3, 1)
     cases = {
-        0: (scroll.SCROLL_SPLICE_ERR_MBTYPE, ext_slice(oracle, c, 4, 3, 1, bad_mb=5, bad_type=3)),
+        0: (scroll.SCROLL_SPLICE_ERR_MBTYPE, ext_slice(oracle, c, 4, 3, 1, bad_mb=5, bad_type=12)),
         1: (scroll.SCROLL_SPLICE_ERR_NAL, good[:4] + bytes([0x65]) + good[5:]),
         2: (scroll.SCROLL_SPLICE_ERR_SYNTAX, good[:len(good) // 2]),
         3: (scroll.SCROLL_SPLICE_ERR_REF, ext_slice(oracle, c, 4, 3, 2, nrefs=4, max_ref=3,

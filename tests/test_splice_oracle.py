@@ -28,7 +28,9 @@ ERR_NAL, ERR_HEADER, ERR_MBTYPE, ERR_SYNTAX, ERR_REF = 1, 2, 3, 4, 5
 class SpliceMb(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int) for n in ("ref", "mx", "my", "cbp", "qp", "qpd", "skip")] + [
         ("tc", ctypes.c_uint8 * 26), ("t1", ctypes.c_uint8 * 26),
-        ("boff", ctypes.c_uint32 * 26), ("blen", ctypes.c_uint32 * 26)]
+        ("boff", ctypes.c_uint32 * 26), ("blen", ctypes.c_uint32 * 26),
+        ("part", ctypes.c_int), ("sub", ctypes.c_int), ("bref", ctypes.c_int * 16),
+        ("bmx", ctypes.c_int * 16), ("bmy", ctypes.c_int * 16)]
 
 
 def _cfg(oracle, w, h):
@@ -60,10 +62,14 @@ def _field(oracle, c, off, rects):
 
 def test_ext_slices_parse_like_the_standard_decoder(oracle):
     c = _cfg(oracle, 640, 368)
+    cov = [0] * 5
     for seed, kw in enumerate([{}, dict(nrefs=1, max_ref=0), dict(nrefs=5, max_ref=4),
                                dict(skip_pm=900), dict(cbp_pm=1000, big_pm=300),
                                dict(slice_qp_delta=-7, qp_jitter=12), dict(ref_idc=2),
-                               dict(mv_range=4000), dict(list_mod=1, nrefs=2, max_ref=1)]):
+                               dict(mv_range=4000), dict(list_mod=1, nrefs=2, max_ref=1),
+                               dict(part_pm=500), dict(part_pm=1000, nrefs=5, max_ref=4, skip_pm=100),
+                               dict(part_pm=800, nrefs=1, max_ref=0, mv_range=3000),
+                               dict(part_pm=600, skip_pm=600, cbp_pm=900)]):
         w, h = 5 + seed % 3, 4 + seed % 4
         nal = ext_slice(oracle, c, w, h, 100 + seed, **kw)
         e, mbs = _parse(oracle, c, splice_of(0, 0, w, h, nal))
@@ -74,8 +80,15 @@ def test_ext_slices_parse_like_the_standard_decoder(oracle):
                 d, m = dec[y][x], mbs[y * w + x]
                 assert (m.ref, m.mx, m.my, m.cbp, bool(m.skip)) == \
                     (d["ref"], d["mx"], d["my"], d["cbp"], d["skip"]), (seed, x, y)
+                assert m.part == min(d["mbt"], 3), (seed, x, y)
+                if m.part == 3:
+                    assert [(m.sub >> (2 * i)) & 3 for i in range(4)] == d["sub"]
+                assert [(m.bref[k], m.bmx[k], m.bmy[k]) for k in range(16)] == d["blocks"]
+                cov[min(d["mbt"], 3)] += 1
+                cov[4] += d["mbt"] == 4
                 if m.cbp:
                     assert m.qp == d["qp"]
+    assert all(cov), cov                       # every MB partitioning, P_8x8ref0 too
 
 
 def _check_frame(oracle, c, off, rects, mode, sp, buf):
@@ -99,6 +112,10 @@ def _check_frame(oracle, c, off, rects, mode, sp, buf):
                 e = ext[y - sp.y0][x - sp.x0]
                 assert (g["ref"], g["mx"], g["my"], g["cbp"]) == (e["ref"], e["mx"], e["my"], e["cbp"]), \
                     (off, mode, x, y)
+                # partitionings kept (P_8x8ref0 -> P_8x8), every 4x4 block's motion
+                assert (g["mbt"], g["sub"]) == (min(e["mbt"], 3), e["sub"]) or \
+                    (e["skip"] and g["mbt"] == 0), (off, mode, x, y)
+                assert g["blocks"] == e["blocks"], (off, mode, x, y)
                 if e["cbp"]:
                     assert g["qp"] == e["qp"]
                     assert (g["luma"], g["cdc"], g["cac"]) == (e["luma"], e["cdc"], e["cac"])
@@ -115,7 +132,7 @@ def test_spliced_mbs_decode_to_the_external_mbs(oracle):
     err = ctypes.c_int()
     w, h = 256, 720
     c = _cfg(oracle, w, h)
-    cov = dict(ref2=0, ext_skip=0, skipped=0)
+    cov = dict(ref2=0, ext_skip=0, skipped=0, part=0)
     for i in range(20):
         off = 488 + i                              # 496: a waypoint
         if oracle.or_needs_waypoint(ctypes.byref(c), off):
@@ -126,7 +143,8 @@ def test_spliced_mbs_decode_to_the_external_mbs(oracle):
         kw = dict(nrefs=len(refs), max_ref=len(refs) - 1, skip_pm=rng.choice([0, 200, 700]),
                   cbp_pm=rng.choice([0, 500, 1000]), big_pm=rng.choice([0, 50]),
                   mv_range=rng.choice([8, 300]), slice_qp_delta=rng.randint(-5, 5),
-                  qp_jitter=rng.choice([0, 4]), ref_idc=rng.choice([0, 1]))
+                  qp_jitter=rng.choice([0, 4]), ref_idc=rng.choice([0, 1]),
+                  part_pm=rng.choice([0, 300, 900]))
         nal = ext_slice(oracle, c, sw, sh, 1000 + i, **kw)
         sp = splice_of(x0, y0, sw, sh, nal)
         rects = random_hints(rng, w // 16, h // 16, refs, nmax=3) if i % 3 == 0 else []
@@ -134,6 +152,7 @@ def test_spliced_mbs_decode_to_the_external_mbs(oracle):
             got, ext = _check_frame(oracle, c, off, rects, mode, sp, buf)
             cov["ref2"] += sum(m["ref"] >= 2 for row in ext for m in row) * (mode == EXACT)
             cov["ext_skip"] += sum(m["skip"] for row in ext for m in row) * (mode == EXACT)
+            cov["part"] += sum(m["mbt"] > 0 for row in ext for m in row) * (mode == EXACT)
             if mode == PSKIP:
                 cov["skipped"] += sum(got[y][x]["skip"] for y in range(y0, y0 + sh)
                                       for x in range(x0, x0 + sw))
@@ -152,7 +171,7 @@ def test_splice_at_picture_corners_and_whole_picture(oracle):
     for j, (x0, y0, sw, sh) in enumerate([(0, 0, 3, 2), (mbw - 3, 0, 3, 3), (0, mbh - 2, 4, 2),
                                           (mbw - 2, mbh - 2, 2, 2), (0, 0, mbw, mbh),
                                           (5, 3, 1, 1)]):
-        nal = ext_slice(oracle, c, sw, sh, 77 + j, cbp_pm=900, skip_pm=300)
+        nal = ext_slice(oracle, c, sw, sh, 77 + j, cbp_pm=900, skip_pm=300, part_pm=400 * (j % 2))
         for mode in (EXACT, PSKIP, SPEC):
             _check_frame(oracle, c, 40, [], mode, splice_of(x0, y0, sw, sh, nal), buf)
 
@@ -198,8 +217,8 @@ def test_errors(oracle):
 
     good = ext_slice(oracle, c, 4, 3, 1)
     assert compose(splice_of(2, 2, 4, 3, good)) == 0
-    # unsupported MB types: P_L0_L0_16x8 (1), P_8x8 (3), intra (5 = I_NxN in P, 30 = I_PCM)
-    for t in (1, 2, 3, 4, 5, 12, 30):
+    # unsupported MB types: intra (5 = I_NxN in P, 12 = I_16x16, 30 = I_PCM)
+    for t in (5, 12, 30):
         bad = ext_slice(oracle, c, 4, 3, 1, bad_mb=5, bad_type=t)
         assert compose(splice_of(2, 2, 4, 3, bad)) == ERR_MBTYPE, t
     # not a non-IDR slice: an IDR NAL header, an SPS

@@ -84,26 +84,28 @@ __device__ inline int blk_raster16(int blk)       /* luma4x4BlkIdx -> raster */
 template <class Fn>
 __device__ __attribute__((always_inline)) inline void for_parts(int part, uint32_t sub, Fn &&f)
 {
-    if (part == 1) {
-        f(0, 0, 4, 2, 0);
-        f(0, 2, 4, 2, 1);
-    } else if (part == 2) {
-        f(0, 0, 2, 4, 0);
-        f(2, 0, 2, 4, 1);
-    } else {
-        for (int i = 0; i < 4; ++i) {
-            const int sx = (i & 1) * 2, sy = (i >> 1) * 2, st = (int)((sub >> (2 * i)) & 3u);
-            if (st == 0) {
-                f(sx, sy, 2, 2, i);
-            } else if (st == 1) {
-                f(sx, sy, 2, 1, i);
-                f(sx, sy + 1, 2, 1, i);
-            } else if (st == 2) {
-                f(sx, sy, 1, 2, i);
-                f(sx + 1, sy, 1, 2, i);
+    /* one call site of f: the geometry is computed per step (an unrolled
+     * switch would inline f dozens of times) */
+    const int n8 = part == 3 ? 4 : 2;
+#pragma unroll 1
+    for (int i = 0; i < n8; ++i) {
+        const int st = part == 3 ? (int)((sub >> (2 * i)) & 3u) : 0;
+        const int ns = st == 0 ? 1 : (st == 3 ? 4 : 2);
+#pragma unroll 1
+        for (int k = 0; k < ns; ++k) {
+            int bx, by, bw, bh;
+            if (part == 1) {
+                bx = 0, by = 2 * i, bw = 4, bh = 2;
+            } else if (part == 2) {
+                bx = 2 * i, by = 0, bw = 2, bh = 4;
             } else {
-                for (int k = 0; k < 4; ++k) f(sx + (k & 1), sy + (k >> 1), 1, 1, i);
+                const int sx = (i & 1) * 2, sy = (i >> 1) * 2;
+                bw = st == 0 || st == 1 ? 2 : 1;
+                bh = st == 0 || st == 2 ? 2 : 1;
+                bx = sx + (st == 2 ? k : (st == 3 ? (k & 1) : 0));
+                by = sy + (st == 1 ? k : (st == 3 ? (k >> 1) : 0));
             }
+            f(bx, by, bw, bh, i);
         }
     }
 }
@@ -150,16 +152,29 @@ __device__ inline Mv unpk_mv(int ref, uint32_t v)
  * (motion of the two rows above, TotalCoeffs of the row above) sits in LDS. */
 constexpr int PARSE_MAXW = 240;          /* external picture width limit (MBs) */
 
-/* The bit reader keeps the next 33..64 bits of the slice in a 64-bit scalar
- * register pair (MSB-aligned): a peek is a shift, a read of up to 32 bits
- * one 64-bit shift, and a word enters from the window -- 64 RBSP words held
- * one per lane, read by one v_readlane -- once per 32 bits consumed. */
+/* wave-uniform value to a scalar register */
+__device__ inline uint32_t U(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane(v); }
+/* keep a (wave-uniform) value in a vector register: its arithmetic then runs
+ * on the SIMD's VALU, of which a CU has four, instead of the CU's one SALU
+ * that 16 parsing waves would otherwise queue on (and whose registers they
+ * would run out of) */
+template <class T>
+__device__ inline void vpin(T &v)
+{
+    asm("" : "+v"(v));
+}
+
+/* The bit reader keeps the next 33..64 bits of the slice in a 64-bit vector
+ * register pair (MSB-aligned; every lane holds the same value): a peek is a
+ * shift, a read of up to 32 bits one 64-bit shift, and a word enters from the
+ * window -- 64 RBSP words held one per lane, read by one v_readlane -- once
+ * per 32 bits consumed.  Branches test readfirstlane'd values (uniform). */
 struct SRd {
     const uint32_t *w;
-    uint32_t nw, nbits, p;               /* words, bits, bits consumed                */
-    uint64_t buf;                        /* the next nv bits at the top               */
-    uint32_t nv, wk;                     /* valid bits (>= 33 between reads); next word */
-    uint32_t base, win;                  /* window: word base + lane                  */
+    uint32_t nw, nbits;                  /* words, bits                               */
+    uint64_t buf;                        /* the next nv bits at the top (VGPR)        */
+    uint32_t nv, p;                      /* valid bits (>= 33 between reads), bits consumed (VGPR) */
+    uint32_t wk, base, win;              /* next word; window: word base + lane       */
     bool bad;                            /* ue() without a 1 bit; p > nbits is checked per MB */
     /* the wait sits in the (rare) refill branch: otherwise the compiler
      * waits for vmcnt(0) before every readlane of the window -- and on gfx9
@@ -182,42 +197,47 @@ struct SRd {
         w = words;
         nw = nwords;
         nbits = bits;
-        p = 0;
         bad = false;
         fill(0);
         buf = (uint64_t)word(0) << 32 | word(1);
         nv = 64;
+        p = 0;
         wk = 2;
+        vpin(buf);
+        vpin(nv);
+        vpin(p);
     }
     __device__ inline uint32_t peek32() const { return (uint32_t)(buf >> 32); }
+    __device__ inline uint32_t pos() const { return U(p); }
     __device__ inline void skip(uint32_t n)                  /* n <= 32 */
     {
         buf <<= n;
         nv -= n;
         p += n;
-        if (nv <= 32u) {
+        if (U(nv) <= 32u) {
             buf |= (uint64_t)word(wk++) << (32u - nv);
             nv += 32u;
         }
     }
-    __device__ inline bool over() const { return p > nbits; }
-    __device__ inline uint32_t u(int n)                      /* 1 <= n <= 32 */
+    __device__ inline bool over() const { return pos() > nbits; }
+    __device__ inline uint32_t u(int n)                      /* 1 <= n <= 32; uniform */
     {
-        const uint32_t v = (uint32_t)(buf >> (64 - n));
+        const uint32_t v = U((uint32_t)(buf >> (64 - n)));
         skip((uint32_t)n);
         return v;
     }
-    __device__ inline uint32_t ue()
+    __device__ inline uint32_t ue()                          /* uniform */
     {
         const uint32_t x = peek32();
-        if (!x) {
+        const int z = (int)U((uint32_t)__clz((int)x));       /* 32 for x == 0 */
+        if (z >= 32) {
             bad = true;
             return 0;
         }
-        const int z = __clz((int)x);
         if (z < 16) {                    /* the whole code in x */
+            const uint32_t v = U((x >> (31 - 2 * z)) - 1u);
             skip((uint32_t)(2 * z + 1));
-            return (x >> (31 - 2 * z)) - 1u;
+            return v;
         }
         skip((uint32_t)z);
         return u(z + 1) - 1u;
@@ -356,13 +376,14 @@ __device__ __attribute__((always_inline)) inline bool wrd_token(SRd &r, const La
         t1 = (int)(c & 3u);
         return t1 <= tc;
     }
+    /* leading zeros and the 3 bits after the first 1, one readfirstlane */
     const uint32_t x = r.peek32();
-    int lz = x ? __clz((int)x) : 32;
-    if (lz > 15) {                       /* only chroma DC has an all-zero code ("0000000") */
+    const uint32_t lzv = (uint32_t)__clz((int)x);            /* 32 for x == 0 */
+    uint32_t idx = U(min(lzv, 16u) << 3 | ((x << (min(lzv, 15u) + 1u)) >> 29));
+    if (idx >= 128u) {                   /* only chroma DC has an all-zero code ("0000000") */
         if (nC != -1) return false;
-        lz = 15;
+        idx = 120u;
     }
-    const uint32_t idx = (uint32_t)lz << 3 | ((x << (lz + 1)) >> 29);
     const uint32_t v = nC == -1 ? T.ct3 : (nC < 2 ? T.ct0 : (nC < 4 ? T.ct1 : T.ct2));
     const uint32_t e = ((uint32_t)__builtin_amdgcn_readlane(v, idx & 63u) >> (idx & 64u ? 16 : 0)) & 0xffffu;
     if (!e) return false;
@@ -372,49 +393,47 @@ __device__ __attribute__((always_inline)) inline bool wrd_token(SRd &r, const La
     return true;
 }
 
-/* the body of a block (9.2.2-9.2.4), consumed, not kept */
+/* the body of a block (9.2.2-9.2.4), consumed, not kept: the levels are
+ * vector arithmetic on the buffer, total_zeros / run_before table lookups */
 __device__ __attribute__((always_inline)) inline bool wrd_body(SRd &r, const LaneTabs &T, int tc, int t1, int maxc)
 {
     if (tc == 0) return true;
     r.skip((uint32_t)t1);
-    int sl = (tc > 10 && t1 < 3) ? 1 : 0;
+    uint32_t sl = (tc > 10 && t1 < 3) ? 1u : 0u, err = 0;
+    vpin(sl);
     for (int k = t1; k < tc; ++k) {
         const uint32_t x = r.peek32();
-        const int prefix = x ? __clz((int)x) : 32;
-        if (prefix > 15) return false;                       /* High profiles only */
-        int ssize = sl;
-        if (prefix == 14 && sl == 0) ssize = 4;
-        if (prefix == 15) ssize = 12;
+        const uint32_t prefix = min((uint32_t)__clz((int)x), 16u);
+        err |= prefix > 15u;
+        uint32_t ssize = sl;
+        ssize = prefix == 14u && sl == 0u ? 4u : ssize;
+        ssize = prefix >= 15u ? 12u : ssize;
         /* level_suffix: the ssize bits after the prefix's 1 (<= 28 bits in all) */
-        const uint32_t suf = (uint32_t)(((uint64_t)(x << (prefix + 1))) >> (32 - ssize));
-        r.skip((uint32_t)(prefix + 1 + ssize));
-        int code = (prefix << sl) + (int)suf;
-        if (prefix == 15 && sl == 0) code += 15;
-        if (k == t1 && t1 < 3) code += 2;
-        const int a = (code + 2) >> 1;                       /* |level| */
-        if (sl == 0) sl = 1;
-        if (a > (3 << (sl - 1)) && sl < 6) sl++;
+        const uint32_t suf = (uint32_t)(((uint64_t)(x << min(prefix + 1u, 31u))) >> (32u - ssize));
+        r.skip(min(prefix + 1u + ssize, 32u));
+        uint32_t code = (min(prefix, 15u) << sl) + suf;
+        code += prefix >= 15u && sl == 0u ? 15u : 0u;
+        code += k == t1 && t1 < 3 ? 2u : 0u;
+        const uint32_t a = (code + 2u) >> 1;                 /* |level| */
+        sl = sl == 0u ? 1u : sl;
+        sl += a > (3u << (sl - 1u)) && sl < 6u ? 1u : 0u;
     }
-    int zl = 0;
+    if (U(err)) return false;                                /* level_prefix > 15: High profiles */
+    uint32_t zl = 0;
     if (tc < maxc) {
         const uint32_t x = r.peek32();
-        uint32_t e;
-        if (maxc == 4) {
-            e = tab_byte(T.tzd, T.tzd, T.tzd, (uint32_t)(tc - 1) * 16u + lz_index(x, 3, 2));
-        } else {
-            e = tab_byte(T.tz0, T.tz1, T.tz2, (uint32_t)(tc - 1) * 40u + lz_index(x, 9, 2));
-        }
+        const uint32_t e = maxc == 4 ? tab_byte(T.tzd, T.tzd, T.tzd, U((uint32_t)(tc - 1) * 16u + lz_index(x, 3, 2)))
+                                     : tab_byte(T.tz0, T.tz1, T.tz2, U((uint32_t)(tc - 1) * 40u + lz_index(x, 9, 2)));
         if (!e) return false;
         r.skip(e >> 4);
-        zl = (int)(e & 15u);
+        zl = e & 15u;
     }
-    for (int k = 0; k < tc - 1 && zl > 0; ++k) {
+    for (int k = 0; k < tc - 1 && zl > 0u; ++k) {
         const uint32_t x = r.peek32();
-        const uint32_t e = tab_byte(T.rb0, T.rb1, T.rb1,
-                                    (uint32_t)(min(zl, 7) - 1) * 48u + lz_index(x, 11, 2));
-        if (!e || (int)(e & 15u) > zl) return false;
+        const uint32_t e = tab_byte(T.rb0, T.rb1, T.rb1, U((min(zl, 7u) - 1u) * 48u + lz_index(x, 11, 2)));
+        if (!e || (e & 15u) > zl) return false;
         r.skip(e >> 4);
-        zl -= (int)(e & 15u);
+        zl -= e & 15u;
     }
     return true;
 }
@@ -483,6 +502,8 @@ struct ParseLds {
     uint8_t tcrow[PARSE_MAXW][8];        /* their bottom pieces' TotalCoeffs (tc_slot)          */
     uint32_t cmv[16], lmv[4];            /* this MB's blocks as they decode; the left MB's right */
     int8_t crf[16], lrf[4];              /* column                                               */
+    uint32_t ulmv;                       /* block (3, 3) of the MB above-left (kept here, not in */
+    int32_t ulrf;                        /* scalar registers: the parse is short of them)        */
 };
 
 __global__ __launch_bounds__(64) void k_splice_parse(int n, const int32_t *__restrict__ list,
@@ -497,23 +518,26 @@ __global__ __launch_bounds__(64) void k_splice_parse(int n, const int32_t *__res
     const int idx = list[i];
     SpliceFrame *F = spf + idx;
     const DevStream S = st[idx / ld_fr];
+    /* the NAL pointer is a generic one, so the compiler takes its bytes for
+     * per-lane values: the header bytes go through readfirstlane, or every
+     * branch on them -- and the whole bit reader after it -- turns divergent */
     const uint8_t *p = F->nal;
     uint32_t len = F->nal_len;
+    auto byte = [&](uint32_t k) { return (uint32_t)__builtin_amdgcn_readfirstlane(k < len ? p[k] : 0u); };
     int status = SCROLL_SPLICE_ERR_NAL;
-    if (len >= 4 && !p[0] && !p[1] && !p[2] && p[3] == 1) {
-        p += 4;
-        len -= 4;
-    } else if (len >= 3 && !p[0] && !p[1] && p[2] == 1) {
-        p += 3;
-        len -= 3;
-    }
+    uint32_t sc = 0;
+    if (len >= 4 && !byte(0) && !byte(1) && !byte(2) && byte(3) == 1u) sc = 4;
+    else if (len >= 3 && !byte(0) && !byte(1) && byte(2) == 1u) sc = 3;
+    p += sc;
+    len -= sc;
     SpliceMbRec *rec = recs + F->rec_first;
     const int W = F->w, H = F->h, nmb = W * H;
-    if (len < 2 || (p[0] & 0x80) || (p[0] & 31) != 1 || W > PARSE_MAXW) {
+    const uint32_t h0 = byte(0);
+    if (len < 2 || (h0 & 0x80) || (h0 & 31) != 1 || W > PARSE_MAXW) {
         if (lane == 0) F->status = len >= 2 && W > PARSE_MAXW ? SCROLL_SPLICE_ERR_HEADER : status;
         return;
     }
-    const int ref_idc = (p[0] >> 5) & 3;
+    const int ref_idc = (int)(h0 >> 5) & 3;
     /* emulation prevention bytes out (7.4.1): byte i of the payload goes
      * unless it is 03 after two zero bytes; 4 bytes per lane per pass, the
      * output index by a wave prefix count; bytes land MSB-first in words
@@ -602,14 +626,14 @@ __global__ __launch_bounds__(64) void k_splice_parse(int n, const int32_t *__res
         int m = 0, qp_c = 26;
         const Mv none{-1, 0, 0};
         uint32_t tc_left = 0;              /* lane j: TotalCoeff of piece j, MB to the left */
-        Mv ul = none;                      /* block (3, 3) of the MB above-left */
+        auto ul = [&]() { return unpk_mv(L.ulrf, L.ulmv); };     /* block (3, 3) of the MB above-left */
         /* whole-MB neighbours of MB (x, y): A = the left MB's block (3, 0),
          * B = the above MB's (0, 3), C = the above-right MB's (0, 3), else
          * D = the above-left MB's (3, 3) */
         auto ctx = [&](int x, int y, Mv &A, Mv &B, Mv &C) {
             A = x ? unpk_mv(L.lrf[0], L.lmv[0]) : none;
             B = y ? unpk_mv(L.rrf[x][0], L.rmv[x][0]) : none;
-            C = y ? (x + 1 < W ? unpk_mv(L.rrf[x + 1][0], L.rmv[x + 1][0]) : (x ? ul : none)) : none;
+            C = y ? (x + 1 < W ? unpk_mv(L.rrf[x + 1][0], L.rmv[x + 1][0]) : (x ? ul() : none)) : none;
         };
         /* block (cx, cy) relative to MB (x, y) for a (sub-)partition (6.4.11.7):
          * inside the MB once decoded (done), right of it never */
@@ -623,14 +647,17 @@ __global__ __launch_bounds__(64) void k_splice_parse(int n, const int32_t *__res
                 return x ? unpk_mv(L.lrf[cy], L.lmv[cy]) : none;
             }
             if (!y) return none;
-            if (cx < 0) return x ? ul : none;
+            if (cx < 0) return x ? ul() : none;
             if (cx < 4) return unpk_mv(L.rrf[x][cx], L.rmv[x][cx]);
             return x + 1 < W ? unpk_mv(L.rrf[x + 1][0], L.rmv[x + 1][0]) : none;
         };
         /* context for the MBs to come: the bottom row and right column of MB
          * (x, y) -- from one motion, or from the decoded blocks */
         auto finish = [&](int x, int y, bool parted, const Mv &me) {
-            ul = y ? unpk_mv(L.rrf[x][3], L.rmv[x][3]) : none;    /* read before it is replaced */
+            if (lane == 0) {                                  /* read before it is replaced */
+                L.ulmv = L.rmv[x][3];
+                L.ulrf = y ? L.rrf[x][3] : -1;
+            }
             if (lane < 4) {
                 const uint32_t v = pk_mv(me.mx, me.my);
                 L.rmv[x][lane] = parted ? L.cmv[12 + lane] : v;
@@ -733,6 +760,22 @@ __global__ __launch_bounds__(64) void k_splice_parse(int n, const int32_t *__res
                 if (!ok || r.bad || r.over()) goto done;
                 me = unpk_mv(L.crf[0], L.cmv[0]);
             }
+            /* the motion is final: record it and hand the context on now, so
+             * none of it stays live through the residual */
+            SpliceMbRec *R = rec + m;
+            if (lane == 0) {
+                R->ref = (int16_t)me.ref;
+                R->mx = me.mx;
+                R->my = me.my;
+                R->skip = 0;
+                R->part = (uint8_t)part;
+                R->sub = (uint8_t)sub;
+            }
+            if (part && lane < 16) {
+                R->bref[lane] = L.crf[lane];
+                R->bmv[lane] = L.cmv[lane];
+            }
+            finish(x, y, part != 0, me);
             const uint32_t code = r.ue();
             const int cbp = code < 48u ? (int)__builtin_amdgcn_readlane(T.cbp, code) : -1;
             if (r.bad || r.over() || cbp < 0) goto done;
@@ -752,6 +795,9 @@ __global__ __launch_bounds__(64) void k_splice_parse(int n, const int32_t *__res
                  * nc_at reads it */
                 const uint32_t tc_top = y && ts >= 0 ? L.tcrow[x][ts] : 0u;
                 PieceOut po{0, 0, 0, 0};
+                /* the pieces in syntax order (7.3.5.3): luma 4x4 blocks of the
+                 * coded 8x8s, chroma DC, chroma AC -- one loop, one copy of the
+                 * block decoder (an unrolled one overflows the instruction cache) */
                 for (int blk = 0; blk < 16; ++blk) {
                     if (!(cbp & (1 << (blk >> 2)))) continue;
                     const int pi = blk_raster16(blk);
@@ -769,20 +815,9 @@ __global__ __launch_bounds__(64) void k_splice_parse(int n, const int32_t *__res
                 my_off = po.off;
                 my_len = po.len;
             }
-            SpliceMbRec *R = rec + m;
             if (lane == 0) {
-                R->ref = (int16_t)me.ref;
                 R->cbp = (uint8_t)cbp;
                 R->qpd = (int8_t)qpd;
-                R->mx = me.mx;
-                R->my = me.my;
-                R->skip = 0;
-                R->part = (uint8_t)part;
-                R->sub = (uint8_t)sub;
-            }
-            if (part && lane < 16) {
-                R->bref[lane] = L.crf[lane];
-                R->bmv[lane] = L.cmv[lane];
             }
             if (lane < SPLICE_PIECES) {
                 R->tc[lane] = (uint8_t)my_tc;
@@ -792,16 +827,15 @@ __global__ __launch_bounds__(64) void k_splice_parse(int n, const int32_t *__res
             }
             if (ts >= 0) L.tcrow[x][ts] = (uint8_t)my_tc;
             tc_left = my_tc;
-            finish(x, y, part != 0, me);
             ++m;
         }
         /* rbsp_slice_trailing_bits (+ zero bytes of a byte stream) */
         if (r.u(1) != 1u) goto done;
-        if (r.p & 7u) {
-            const int k = 8 - (int)(r.p & 7u);
+        if (r.pos() & 7u) {
+            const int k = 8 - (int)(r.pos() & 7u);
             if (r.u(k)) goto done;
         }
-        while (r.p < r.nbits)
+        while (r.pos() < r.nbits)
             if (r.u(8)) goto done;
         if (!r.bad && !r.over()) status = SCROLL_SPLICE_OK;
     }

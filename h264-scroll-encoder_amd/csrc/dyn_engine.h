@@ -21,7 +21,8 @@ typedef struct {
     uint32_t *rowstage;             /* per (frame, row group): its bits from bit 0 (rs_frame_words) */
     uint32_t *gbits;                /* per (frame, row group): its bit count */
     uint32_t *spill;                /* rs_spill_cap spill slots (rect rows over their slot) */
-    uint32_t *ctr;                  /* per compose: [0] spill slots taken, [1] general records taken */
+    uint32_t *ctr;                  /* per compose: [0] spill slots taken, [1] general records taken,
+                                     * [2 + k] the frame (s ld_fr + f) holding general record k */
     uint32_t epoch;                 /* look-back epoch of the last compose (24 bits, never 0) */
 } DynScratch;
 

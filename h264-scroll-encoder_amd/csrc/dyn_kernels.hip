@@ -291,6 +291,7 @@ __global__ __launch_bounds__(256) void k_dyn_rows(const DevStream *__restrict__ 
             const uint32_t k = atomicAdd(&ctr[1], 1u);
             if (k < g.gen_cap) {
                 DF->rbsp_bytes = k;
+                ctr[2 + k] = (uint32_t)((size_t)s * ld_fr + f);     /* k_dyn_row<true>'s list */
                 e = DF_GENERAL;
             } else {
                 e = DF_OVER;
@@ -1208,8 +1209,15 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
     /* debug: realtime at entry and after each phase (k_dyn_group's slots) */
     uint64_t stv[6] = {0, 0, 0, 0, 0, 0};
     if (stamps) stv[0] = __builtin_amdgcn_s_memrealtime();
-    const int r = blockIdx.x, f = blockIdx.y, s = blockIdx.z;
-    const int t = threadIdx.x, T = blockDim.x, lane = t & 63, wave = t >> 6, nwv = T >> 6;
+    const int r = blockIdx.x, t = threadIdx.x, T = blockDim.x, lane = t & 63, wave = t >> 6, nwv = T >> 6;
+    int f = blockIdx.y, s = blockIdx.z;
+    if (GEN) {                          /* grid (h, record slots): the frames k_dyn_rows listed */
+        const uint32_t j = blockIdx.y, n = min(__builtin_amdgcn_readfirstlane(ctr[1]), g.gen_cap);
+        if (j >= n) return;
+        const uint32_t q = __builtin_amdgcn_readfirstlane(ctr[2 + j]);
+        s = (int)(q / (uint32_t)ld_fr);
+        f = (int)(q - (uint32_t)s * (uint32_t)ld_fr);
+    }
     const size_t nb = (size_t)s * ld_fr + f;
     const DynFrame df = dfr[nb];
     if (df.nal < 0 || ((df.err & DF_GENERAL) != 0) != GEN) return;
@@ -2630,7 +2638,9 @@ int dyn_launch_code(hipStream_t hs, int nframes, int S, DevStream *st, const Nal
                        x->meta, x->body_lo, x->body_hi, x->tcx, epoch, x->rowstage, x->gbits, x->spill, x->ctr,
                        stamps);
     if (hipGetLastError() != hipSuccess) return -1;
-    hipLaunchKernelGGL(k_dyn_row<true>, dim3(g->h, nframes, S), dim3(row_threads(g->w)),
+    /* the general path: one row workgroup per record slot that may be taken */
+    hipLaunchKernelGGL(k_dyn_row<true>, dim3(g->h, std::min<uint32_t>(g->gen_cap, (uint32_t)(nframes * S)), 1),
+                       dim3(row_threads(g->w)),
                        row_lds_bytes(g->w, mbw), hs, st, nal, ld_nal, pend, dfr, ld_fr, *g, x->rows, src, refs,
                        x->meta, x->body_lo, x->body_hi, x->tcx, epoch, x->rowstage, x->gbits, x->spill, x->ctr,
                        stamps);

@@ -1932,7 +1932,8 @@ int scroll_batch_set_dyn_rect(ScrollBatch *b, int x0, int y0, int w, int h, size
     const size_t rs_words = S * F * g.rs_frame_words + (size_t)g.rs_spill_cap * g.rs_spill_words;
     if (e == hipSuccess) e = hipMalloc(&b->dx.rowstage, rs_words * sizeof(uint32_t));
     if (e == hipSuccess) b->dx.spill = b->dx.rowstage + S * F * g.rs_frame_words;
-    if (e == hipSuccess) e = hipMalloc(&b->dx.ctr, 2 * sizeof(uint32_t));
+    /* [0], [1]: slots taken; [2 + k]: the frame (s ld_fr + f) of general record k */
+    if (e == hipSuccess) e = hipMalloc(&b->dx.ctr, (2 + S * F) * sizeof(uint32_t));
     if (e == hipSuccess) e = hipMalloc(&b->dx.gbits, S * F * ng * sizeof(uint32_t));
     b->dx.epoch = 0;
     if (e == hipSuccess) e = hipMemset(b->d_src, 0, S * g.src_ld);

@@ -34,7 +34,7 @@ typedef struct {
  * coeff_token (offset and length in the RBSP).  A partitioned MB (part 1
  * 16x8, 2 8x16, 3 P_8x8 / P_8x8ref0 with sub_mb_type i in bits 2i..2i+1 of
  * sub) also carries the motion of each 4x4 block (raster; mv packed x | y
- * << 16); ref / mx / my are then block 0's.  304 bytes. */
+ * << 16); ref / mx / my are then block 0's.  312 bytes. */
 typedef struct {
     int16_t ref;
     uint8_t cbp;
@@ -46,6 +46,7 @@ typedef struct {
     uint32_t boff[SPLICE_PIECES];
     int8_t bref[16];
     uint32_t bmv[16];
+    uint32_t res_off, res_len;      /* the external residual's bits (0: not parsed / none) */
 } SpliceMbRec;
 
 /* 0, or -1 when the launch failed */

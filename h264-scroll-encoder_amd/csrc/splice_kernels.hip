@@ -685,6 +685,7 @@ __global__ __launch_bounds__(64) void k_splice_parse(int n, const int32_t *__res
                     R->my = py;
                     R->skip = 1;
                     R->part = 0;
+                    R->res_len = 0;
                 }
                 if (lane < SPLICE_PIECES) {
                     R->tc[lane] = 0;
@@ -780,6 +781,7 @@ __global__ __launch_bounds__(64) void k_splice_parse(int n, const int32_t *__res
             const int cbp = code < 48u ? (int)__builtin_amdgcn_readlane(T.cbp, code) : -1;
             if (r.bad || r.over() || cbp < 0) goto done;
             int qpd = 0;
+            uint32_t rs0 = 0, rsn = 0;                         /* the residual's bits */
             /* lane j: piece j of this MB */
             uint32_t my_tc = 0, my_t1 = 0, my_off = 0, my_len = 0;
             if (cbp) {
@@ -795,9 +797,10 @@ __global__ __launch_bounds__(64) void k_splice_parse(int n, const int32_t *__res
                  * nc_at reads it */
                 const uint32_t tc_top = y && ts >= 0 ? L.tcrow[x][ts] : 0u;
                 PieceOut po{0, 0, 0, 0};
+                rs0 = r.pos();
                 /* the pieces in syntax order (7.3.5.3): luma 4x4 blocks of the
-                 * coded 8x8s, chroma DC, chroma AC -- one loop, one copy of the
-                 * block decoder (an unrolled one overflows the instruction cache) */
+                 * coded 8x8s, chroma DC, chroma AC (unrolled: measured faster
+                 * than one loop over the pieces) */
                 for (int blk = 0; blk < 16; ++blk) {
                     if (!(cbp & (1 << (blk >> 2)))) continue;
                     const int pi = blk_raster16(blk);
@@ -814,10 +817,13 @@ __global__ __launch_bounds__(64) void k_splice_parse(int n, const int32_t *__res
                 my_t1 = po.t1;
                 my_off = po.off;
                 my_len = po.len;
+                rsn = r.pos() - rs0;
             }
             if (lane == 0) {
                 R->cbp = (uint8_t)cbp;
                 R->qpd = (int8_t)qpd;
+                R->res_off = rs0;
+                R->res_len = rsn;
             }
             if (lane < SPLICE_PIECES) {
                 R->tc[lane] = (uint8_t)my_tc;
@@ -874,30 +880,42 @@ __device__ inline uint32_t bits_at(const uint32_t *w, uint32_t q)
     return o ? (w[k] << o) | (w[k + 1] >> (32u - o)) : w[k];
 }
 
-/* bits of one spliced MB after its head: cbp, mb_qp_delta, pieces */
+/* n bits at bit q of the RBSP words, put */
+template <class SK>
+__device__ inline void put_rbsp(SK &sk, const uint32_t *rb, uint32_t q0, uint32_t n)
+{
+    if constexpr (__is_same(SK, CountSink)) {
+        sk.n += n;
+    } else {
+        for (uint32_t k = 0; k < n; k += 32) {
+            const int c = (int)min(32u, n - k);
+            sk.put(bits_at(rb, q0 + k) >> (32 - c), c);
+        }
+    }
+}
+
+/* bits of one spliced MB after its head: cbp, mb_qp_delta, pieces.  An MB
+ * whose left and top neighbours are spliced too (verbatim) sees the nC of
+ * its external picture in every block: its residual is the external one
+ * bit for bit and goes over as one run (parsed records only: res_len) */
 template <class SK>
 __device__ inline void splice_tail(SK &sk, const SpliceMbRec &mb, const uint8_t *L, const uint8_t *T,
-                                   const uint32_t *rb)
+                                   const uint32_t *rb, bool verbatim)
 {
     const int cbp = mb.cbp;
     put_ue(sk, SPT.cbp_code[cbp]);
     if (!cbp) return;
     put_se(sk, mb.qpd);
+    if (verbatim && mb.res_len) {
+        put_rbsp(sk, rb, mb.res_off, mb.res_len);
+        return;
+    }
     auto piece = [&](int i, int nC) {
         uint32_t v;
         int len;
         coeff_token(SPT, mb.tc[i], mb.t1[i], nC, v, len);
         sk.put(v, len);
-        const uint32_t q0 = mb.boff[i];
-        const int bl = mb.blen[i];
-        if constexpr (__is_same(SK, CountSink)) {
-            sk.n += (uint32_t)bl;
-        } else {
-            for (int k = 0; k < bl; k += 32) {
-                const int c = min(32, bl - k);
-                sk.put(bits_at(rb, q0 + (uint32_t)k) >> (32 - c), c);
-            }
-        }
+        put_rbsp(sk, rb, mb.boff[i], mb.blen[i]);
     };
     for (int blk = 0; blk < 16; ++blk)
         if (cbp & (1 << (blk >> 2))) {
@@ -1121,7 +1139,7 @@ __global__ __launch_bounds__(DT) void k_splice_stage(DevStream *__restrict__ st,
                     put_se(sk, me.mx - px);
                     put_se(sk, me.my - py);
                 }
-                if (k >= 0) splice_tail(sk, rec[k], Lt, Tt, rb);
+                if (k >= 0) splice_tail(sk, rec[k], Lt, Tt, rb, x > SF.x0 && y > SF.y0);
                 else sk.put(1, 1);                                 /* coded_block_pattern 0 */
             };
             CountSink cs{0};

@@ -247,8 +247,10 @@ int scroll_batch_clear_hints(ScrollBatch *b);
  * The MBs of an external P slice -- a conventional encoder's output for the
  * dynamic rect, coded as its own w x h MB picture -- are transplanted into
  * the rect [x0, x0 + w) x [y0, y0 + h) of frame f's scroll NAL: P_Skip MBs
- * become P_L0_16x16 with their skip motion, mb_skip_run / ref_idx / mvd are
- * re-coded for the composed picture, mb_qp_delta rebased to the composed
+ * become P_L0_16x16 with their skip motion, partitioned MBs keep their
+ * partitioning (P_8x8ref0 written as P_8x8 with ref_idx 0), mb_skip_run /
+ * ref_idx / every (sub-)partition's mvd are re-coded for the composed
+ * picture (4x4-block neighbours, 8.4.1.3), mb_qp_delta rebased to the composed
  * slice QP, each residual block keeps its bits after coeff_token and gets
  * the coeff_token of its composed nC.  MBs outside the rect follow the frame's
  * UI hints (a splice turns the hint path on in SCROLL_HINT_SPEC, so a standard
@@ -264,7 +266,8 @@ int scroll_batch_clear_hints(ScrollBatch *b);
  * disable_deblocking_filter_idc 1 when the stream signals deblocking
  * control); no ref_pic_list_modification, or one that restates the composed
  * list (op k: long_term_pic_num k, as the composer's own slices write it);
- * MBs P_L0_16x16 or P_Skip;
+ * MBs of any inter type (P_L0_16x16, P_L0_L0_16x8 / 8x16, P_8x8 with any
+ * sub_mb_types, P_8x8ref0) or P_Skip -- no intra MBs;
  * ref_idx 0 = A, 1 = B, 2 + i = waypoint i of the composed stream; motion
  * vectors are displacements in the composed picture, |mv| <= 16383 quarter
  * pels; CAVLC level_prefix <= 15 (Baseline / Main).
@@ -283,7 +286,7 @@ int scroll_batch_clear_hints(ScrollBatch *b);
 #define SCROLL_SPLICE_OK          0
 #define SCROLL_SPLICE_ERR_NAL     1   /* not a coded slice of a non-IDR picture     */
 #define SCROLL_SPLICE_ERR_HEADER  2   /* slice header outside the supported syntax  */
-#define SCROLL_SPLICE_ERR_MBTYPE  3   /* an MB other than P_L0_16x16 / P_Skip       */
+#define SCROLL_SPLICE_ERR_MBTYPE  3   /* an intra MB (mb_type > 4 in the P slice)    */
 #define SCROLL_SPLICE_ERR_SYNTAX  4   /* malformed, truncated or MB count mismatch   */
 #define SCROLL_SPLICE_ERR_REF     5   /* ref_idx not a valid reference of the frame  */
 int scroll_batch_set_splice(ScrollBatch *b, int s, int f, int x0, int y0, int w, int h,

@@ -13,12 +13,14 @@
  *                         row's own row-stage words (records stay in LDS)
  *   k_dyn_static          one wave per static row group (slice header, rows
  *                         above / below the rect, stop bit) -> row-stage words
- *   k_dyn_stitch          per NAL: row-group offsets, funnel-shift assembly of
- *                         the staged RBSP, emulation-prevention positions
+ *   k_dyn_epfix           per NAL: row-group offsets, emulation-prevention
+ *                         positions from the groups' EP-candidate words
+ *                         (k_dyn_epscan rescans the NALs it flags)
  *   k_plan (size pass)    NAL sizes (dynamic: 5 + RBSP + EP), arena offsets
  *   k_emit                every other NAL (dynamic NALs are "external")
- *   k_dyn_emit_gather     staged RBSP -> arena: start code, NAL header, EP
- *                         bytes, 16-byte chunks (k_dyn_emit: > 2048 EP bytes)
+ *   k_dyn_emit_gather     row-stage groups -> arena: start code, NAL header,
+ *                         EP bytes, 16-byte chunks (k_dyn_emit: > 2048 EP
+ *                         bytes); the RBSP is never staged
  *
  * The bits are those of oracle/dyn_oracle.c (or_scroll_nal_dyn); parity is
  * checked bit-exact by tests/test_gpu_dyn.py.  Roofline: HBM (source pixels
@@ -989,7 +991,8 @@ __device__ inline void put_piece(uint32_t *buf, uint32_t p0, uint32_t n, uint32_
  *   3. coeff_token per piece from the left / top TotalCoeffs (nC);
  *   4. per MB cbp, its code and the piece offsets; the row's MB offsets;
  *   5. the row's bits -> LDS window -> its own row-stage words, from bit 0
- *      (no position known yet: k_dyn_stitch places every row group).
+ *      (no position known yet: k_dyn_epfix places every row group), with
+ *      the words that may hold an EP site recorded for k_dyn_epfix.
  * The static row groups (slice header, rows above / below the rect, stop
  * bit) are k_dyn_static's.  NALs whose chroma prediction needs the general
  * path (k_dyn_rows flags them) take their records from k_dyn_code_general

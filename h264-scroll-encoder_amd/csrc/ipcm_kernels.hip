@@ -6,7 +6,8 @@
  * one stripe colour per MB to the picture's own samples.  HBM-bound byte
  * work: every workgroup owns IPCM_CHUNK bytes of one file's RBSP.
  *
- *   pass 0  each chunk's RBSP bytes (generated from the picture into LDS)
+ *   pass 0  each chunk's RBSP bytes (staged from the picture into LDS: one
+ *           16- / 8-byte load per source row segment of an MB record)
  *           -> its emulation-prevention count (closed form of nal.c:33-38,
  *           dyn::ep_insert, with the zero run looked up across the chunk)
  *   pass 1  the same bytes + the EP bytes at the chunk's output offset
@@ -52,19 +53,6 @@ __device__ inline Cur cur_at(const IpcmGeom &G, uint32_t j)     /* j = i - (nh -
     return c;
 }
 
-__device__ inline void cur_add(const IpcmGeom &G, Cur &c, uint32_t d)   /* d < 386 */
-{
-    c.r += d;
-    if (c.r >= 386u) {
-        c.r -= 386u;
-        c.m++;
-        if (++c.mx == G.mbw) {
-            c.mx = 0;
-            c.my++;
-        }
-    }
-}
-
 /* byte i of the RBSP with cursor c at i (when i >= nh) */
 __device__ inline uint32_t rbsp_at(const IpcmGeom &G, const uint8_t *pic, uint32_t i, const Cur &c)
 {
@@ -98,27 +86,81 @@ __global__ __launch_bounds__(IT) void k_ipcm(IpcmGeom G, const uint8_t *__restri
     const uint8_t *pic = pics + (size_t)n * G.pic_stride;
     const uint32_t c0 = c * CH, c1 = min(c0 + CH, G.rbsp_len);
 
-    /* RBSP bytes [c0 - LB, c1) -> LDS, thread t takes k = t + IT q (coalesced
-     * sample loads); before byte 0 a non-zero sentinel (the automaton starts
-     * with no zeros seen) */
+    /* RBSP bytes [c0 - LB, c1) -> LDS.  The samples go by source row
+     * segment (an MB record's 16 luma rows of 16 bytes, 8 + 8 chroma rows of
+     * 8): one 16- or 8-byte load per segment, its bytes into LDS at their
+     * RBSP offsets; every other byte -- before the RBSP (a non-zero sentinel:
+     * the automaton starts with no zeros seen), the slice header, the
+     * records' 0x0D 0x00, the stop byte -- by the thread of its index.  Each
+     * byte has exactly one writer. */
     {
+        const int64_t lo = (int64_t)c0 - LB;
         const uint32_t base = G.nh - 2u;
-        Cur cu{0, 0, 0, 0};
-        bool have = false;
         for (uint32_t k = (uint32_t)t; k < (uint32_t)LB + CH; k += IT) {
-            const int64_t i = (int64_t)c0 - LB + (int64_t)k;
-            uint32_t v = 0;
+            const int64_t i = lo + (int64_t)k;
+            int v = -1;                                       /* -1: a sample byte */
             if (i < 0) {
-                v = 0xffu;
-            } else if (i < (int64_t)c1) {
-                if (!have && (uint32_t)i >= G.nh) {
-                    cu = cur_at(G, (uint32_t)i - base);
-                    have = true;
-                }
-                v = rbsp_at(G, pic, (uint32_t)i, cu);
+                v = 0xff;
+            } else if (i >= (int64_t)c1) {
+                v = 0;
+            } else if ((uint32_t)i < G.nh) {
+                v = G.hdr[i];
+            } else if ((uint32_t)i + 1u == G.rbsp_len) {
+                v = 0x80;                                     /* rbsp_stop_one_bit + alignment */
+            } else {
+                const uint32_t j = (uint32_t)i - base;
+                const uint32_t r = j - 386u * (uint32_t)(((uint64_t)j * M386) >> 41);
+                if (r < 2u) v = r == 0u ? 0x0D : 0x00;        /* ue(25) + pcm_alignment_zero_bits */
             }
-            rb[k] = (uint8_t)v;
-            if (have) cur_add(G, cu, IT);
+            if (v >= 0) rb[k] = (uint8_t)v;
+        }
+        /* the records that overlap [max(lo, nh), c1): 32 segments each */
+        const int64_t s0 = lo > (int64_t)G.nh ? lo : (int64_t)G.nh;
+        if (s0 < (int64_t)c1) {
+            const uint32_t m0 = (uint32_t)((((uint64_t)s0 - base) * M386) >> 41);
+            const uint32_t m1 = min((uint32_t)((((uint64_t)c1 - 1u - base) * M386) >> 41), G.nmb - 1u);
+            const uint32_t w = (uint32_t)G.w, cw = w / 2u;
+            const size_t ysz = (size_t)w * (uint32_t)G.h;
+            const bool vec = (reinterpret_cast<uintptr_t>(pic) & 15u) == 0u;
+            const uint32_t nseg = 32u * (m1 - m0 + 1u);
+            for (uint32_t q = (uint32_t)t; q < nseg; q += IT) {
+                const uint32_t m = m0 + (q >> 5), sg = q & 31u;
+                uint32_t my = __umulhi(m, G.m_mbw);
+                if (G.mbw == 1) my = m;
+                const uint32_t mx = m - my * G.mbw;
+                uint32_t off, len;
+                size_t a;
+                if (sg < 16u) {
+                    off = 2u + 16u * sg;
+                    len = 16u;
+                    a = (size_t)(16u * my + sg) * w + 16u * mx;
+                } else {
+                    const uint32_t cr = sg & 7u;
+                    off = (sg < 24u ? 258u : 322u) + 8u * cr;
+                    len = 8u;
+                    a = ysz + (sg < 24u ? 0u : ysz / 4) + (size_t)(8u * my + cr) * cw + 8u * mx;
+                }
+                const int64_t r0 = (int64_t)base + 386 * (int64_t)m + off;      /* its RBSP index */
+                if (r0 + len <= lo || r0 >= (int64_t)c1) continue;
+                uint32_t x[4] = {0, 0, 0, 0};
+                if (vec) {
+                    if (len == 16u) {
+                        const uint4 u = *reinterpret_cast<const uint4 *>(pic + a);
+                        x[0] = u.x, x[1] = u.y, x[2] = u.z, x[3] = u.w;
+                    } else {
+                        const uint2 u = *reinterpret_cast<const uint2 *>(pic + a);
+                        x[0] = u.x, x[1] = u.y;
+                    }
+                } else {
+                    for (uint32_t b = 0; b < len; ++b) x[b >> 2] |= (uint32_t)pic[a + b] << (8u * (b & 3u));
+                }
+#pragma unroll
+                for (uint32_t b = 0; b < 16u; ++b) {
+                    const int64_t i = r0 + b;
+                    if (b < len && i >= lo && i < (int64_t)c1)
+                        rb[(uint32_t)(i - lo)] = (uint8_t)(x[b >> 2] >> (8u * (b & 3u)));
+                }
+            }
         }
     }
     if (t == 0) deep = -2;

@@ -633,6 +633,410 @@ __global__ __launch_bounds__(DT) void k_ing_stream(const uint8_t *__restrict__ i
 }
 
 /* ---------------------------------------------------------------------- */
+/* segmented ingest: every slice body over many workgroups                 */
+/* ---------------------------------------------------------------------- */
+/* k_ing_stream streams a whole slice with one workgroup (one per stream: at
+ * 256 new streams a quarter of the chip, 340 dependent windows each).  The
+ * segmented path cuts each slice's EBSP into SEG-byte segments:
+ *   k_ing_head        per stream: the parse and the SPS / PPS NAL units of
+ *                     k_ing_stream, and a plan per slice (input range,
+ *                     header bits, first output bytes)
+ *   k_ing_count       per segment: its RBSP bytes (closed-form removal)
+ *   k_ing_seg<false>  per segment: its output bytes -- the RBSP bytes it
+ *                     holds, shifted behind the new header -- summarised for
+ *                     emulation prevention: first / last non-zero byte and
+ *                     the insertions after the first, which do not depend on
+ *                     what came before
+ *   k_ing_fix         per stream, serial over its segments: each one's
+ *                     insertions before its first non-zero byte (closed form
+ *                     in the last non-zero byte before it), hence its arena
+ *                     offset; the byte counts and the arena bound
+ *   k_ing_seg<true>   per segment: the bytes again, with their 03s, to the
+ *                     arena.
+ * Bytes: identical to k_ing_stream's (tests/test_gpu_ingest.py checks both
+ * against the oracle). */
+constexpr uint32_t SEG = 16384;          /* EBSP bytes per segment                  */
+constexpr uint32_t SEG_LA = 64;          /* EBSP bytes decoded past it (its successor's first RBSP byte) */
+
+struct IngPlan {                         /* one slice of a new stream               */
+    uint64_t in, n;                      /* EBSP payload in the input, bytes        */
+    uint64_t mb_start;                   /* RBSP bit of the first MB                */
+    uint64_t at;                         /* arena offset of the NAL (k_ing_fix)     */
+    uint64_t R;                          /* RBSP bytes of the payload (k_ing_fix)   */
+    uint32_t hlen, npre, nseg, ok;
+    int32_t ref_idc, type;
+    uint8_t pre[40];
+};
+
+struct IngSeg {
+    uint32_t kept;                       /* RBSP bytes (k_ing_count)                */
+    uint32_t nout;                       /* output bytes it owns (k_ing_seg<false>) */
+    int32_t f, vf, last;                 /* first non-zero output byte (relative, -1: none), its
+                                          * value, the last non-zero one                      */
+    uint32_t cafter;                     /* EP insertions after the first non-zero byte */
+    uint64_t o_lo;                       /* its first output byte                   */
+    int64_t lnz;                         /* last non-zero output byte before it (k_ing_fix) */
+    uint64_t at;                         /* arena offset of its first output byte (k_ing_fix) */
+};
+
+__global__ __launch_bounds__(DT) void k_ing_head(const uint8_t *__restrict__ in,
+                                                 const IngestFile *__restrict__ files,
+                                                 const IngestScan *__restrict__ scan,
+                                                 IngestOut *__restrict__ outs, IngPlan *__restrict__ plans,
+                                                 uint32_t maxseg, uint8_t *__restrict__ arena,
+                                                 uint64_t ld_arena, uint64_t cap, int first_stream)
+{
+    __shared__ IngLds L;
+    const int k = blockIdx.x, t = threadIdx.x;
+    uint8_t *A = arena + (size_t)(first_stream + k) * ld_arena;
+    const uint8_t *d[2] = {in + files[2 * k].off, in + files[2 * k + 1].off};
+    const uint64_t n[2] = {files[2 * k].size, files[2 * k + 1].size};
+    if (t != 0) return;
+    int err = ING_OK;
+    for (int f = 0; f < 2 && err == ING_OK; ++f) {
+        const int np = (int)scan[2 * k + f].n;
+        if (np > ING_SC_MAX) {
+            err = ING_ERR_NALS;
+            break;
+        }
+        for (int q = 0; q < np; ++q) L.pos[f][q] = scan[2 * k + f].pos[q];
+        if (walk_nals(d[f], n[f], L.pos[f], np, L.sps[f], L.pps[f], L.idr[f])) {
+            err = ING_ERR_MISSING;
+            break;
+        }
+        int nref, dbf;
+        if (parse_sps(d[f] + L.sps[f].off, L.sps[f].n, L.si[f]) ||
+            parse_pps(d[f] + L.pps[f].off, L.pps[f].n, nref, dbf)) {
+            err = ING_ERR_PARSE;
+            break;
+        }
+        if (f == 0) L.dbf = dbf;
+    }
+    if (err == ING_OK && (L.si[0].w != L.si[1].w || L.si[0].h != L.si[1].h)) err = ING_ERR_DIMS;
+    IngestOut &o = outs[k];
+    if (err == ING_OK) {
+        for (int f = 0; f < 2 && err == ING_OK; ++f) {          /* both with A's parse config */
+            parse_idr(d[f] + L.idr[f].off, L.idr[f].n, L.si[0], L.dbf, L.sh[f]);
+            slice_header(L.hdr[f], f == 0, L.dbf, L.sh[f]);
+            EbspReader r;
+            r.init(d[f] + L.idr[f].off, L.idr[f].n);
+            for (uint64_t q = 0; q < L.sh[f].mb_start; ++q) r.u1();
+            SmallBits pb = L.hdr[f];
+            const int npre = (pb.n + 7) >> 3;
+            while (pb.n < 8 * npre && !r.eof) {
+                const uint32_t bit = r.u1();
+                if (r.eof) break;
+                pb.put(bit, 1);
+            }
+            IngPlan &P = plans[2 * k + f];
+            P.in = files[2 * k + f].off + L.idr[f].off;
+            P.n = L.idr[f].n;
+            P.mb_start = L.sh[f].mb_start;
+            P.hlen = (uint32_t)L.hdr[f].n;
+            P.npre = (uint32_t)npre;
+            P.nseg = (uint32_t)((P.n + SEG - 1) / SEG);
+            if (P.nseg == 0) P.nseg = 1;
+            if (P.nseg > maxseg) err = ING_ERR_NALS;       /* the host sized maxseg by the files */
+            P.ref_idc = 3;
+            P.type = f == 0 ? 5 : 1;
+            for (int q = 0; q < npre && q < 40; ++q) P.pre[q] = (uint8_t)pb.byte(q);
+        }
+    }
+    bool over = false;
+    uint64_t at = 0;
+    if (err == ING_OK) {
+        SmallBits b;
+        gen_sps(b, L.si[0].w, L.si[0].h);
+        at = put_small_nal(A, at, cap, 3, 7, b, over);
+        gen_pps(b);
+        at = put_small_nal(A, at, cap, 3, 8, b, over);
+        if (over) err = ING_ERR_OVERFLOW;
+    }
+    plans[2 * k].at = at;                                  /* A's NAL; k_ing_fix places B */
+    plans[2 * k].ok = plans[2 * k + 1].ok = err == ING_OK;
+    o.err = err;
+    o.bytes = 0;
+    o.w = L.si[0].w;
+    o.h = L.si[0].h;
+    o.deblock = L.dbf;
+}
+
+/* EBSP byte i of d[0, n) is an emulation-prevention byte (nal_parser.c:72) */
+__device__ inline bool ebsp_removed(const uint8_t *d, uint64_t n, uint64_t i)
+{
+    return i >= 2 && i + 1 < n && d[i] == 3 && d[i - 1] == 0 && d[i - 2] == 0 && d[i + 1] <= 3;
+}
+
+__global__ __launch_bounds__(DT) void k_ing_count(const uint8_t *__restrict__ in,
+                                                  const IngPlan *__restrict__ plans,
+                                                  IngSeg *__restrict__ segs, uint32_t maxseg)
+{
+    __shared__ uint32_t wsum[NW];
+    const uint32_t c = blockIdx.x, p = blockIdx.y;
+    const IngPlan &P = plans[p];
+    if (!P.ok || c >= P.nseg) return;
+    const uint8_t *d = in + P.in;
+    const uint64_t e0 = (uint64_t)c * SEG, e1 = min(P.n, e0 + SEG);
+    uint32_t kept = 0;
+    for (uint64_t i = e0 + threadIdx.x; i < e1; i += DT) kept += ebsp_removed(d, P.n, i) ? 0u : 1u;
+    uint32_t ex, tot;
+    block_excl_sum(kept, wsum, ex, tot);
+    if (threadIdx.x == 0) segs[(size_t)p * maxseg + c].kept = tot;
+}
+
+struct SegLds {
+    uint8_t rb[SEG + SEG_LA + 16];       /* the segment's RBSP bytes (+ look-ahead)   */
+    uint8_t obuf[OBUF];
+    uint32_t wsum[NW];
+    int32_t wmax[NW];
+    int32_t wmin[NW];
+    uint32_t R0;
+};
+
+/* even numbers >= 2 in [a, b] */
+__device__ inline int64_t evens_ge2(int64_t a, int64_t b)
+{
+    if (a < 2) a = 2;
+    const int64_t f = a + (a & 1);
+    return b < f ? 0 : (b - f) / 2 + 1;
+}
+
+template <bool WRITE>
+__global__ __launch_bounds__(DT) void k_ing_seg(const uint8_t *__restrict__ in,
+                                                const IngPlan *__restrict__ plans,
+                                                IngSeg *__restrict__ segs, uint32_t maxseg,
+                                                uint8_t *__restrict__ arena, uint64_t ld_arena,
+                                                int first_stream)
+{
+    __shared__ SegLds L;
+    const uint32_t c = blockIdx.x, p = blockIdx.y;
+    const int t = threadIdx.x, lane = t & 63;
+    const IngPlan &P = plans[p];
+    if (!P.ok || c >= P.nseg) return;
+    IngSeg *SG = segs + (size_t)p * maxseg;
+    const uint8_t *d = in + P.in;
+    const uint64_t n = P.n;
+    /* RBSP bytes before this segment, and in the whole payload */
+    uint32_t pre = 0, all = 0;
+    for (uint32_t q = (uint32_t)t; q < P.nseg; q += DT) {
+        const uint32_t v = SG[q].kept;
+        all += v;
+        if (q < c) pre += v;
+    }
+    uint32_t ex, R0, Rtot;
+    block_excl_sum(pre, L.wsum, ex, R0);
+    block_excl_sum(all, L.wsum, ex, Rtot);
+    const uint32_t kept = SG[c].kept, R1 = R0 + kept;
+    const bool lastseg = c + 1 == P.nseg;
+    /* this segment's RBSP bytes (and the next segment's first ones) -> LDS */
+    const uint64_t e0 = (uint64_t)c * SEG, e1 = min(n, e0 + SEG + SEG_LA);
+    uint32_t R = 0;
+    for (uint64_t w0 = e0; w0 < e1; w0 += 16u * DT) {
+        uint32_t keepm = 0, kn = 0;
+        uint8_t v[16];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            const uint64_t i = w0 + 16u * (uint32_t)t + (uint64_t)q;
+            v[q] = 0;
+            if (i < e1) {
+                v[q] = d[i];
+                if (!ebsp_removed(d, n, i)) {
+                    keepm |= 1u << q;
+                    kn++;
+                }
+            }
+        }
+        uint32_t kx, kt;
+        block_excl_sum(kn, L.wsum, kx, kt);
+        uint32_t at = R + kx;
+#pragma unroll
+        for (int q = 0; q < 16; ++q)
+            if ((keepm >> q) & 1u) {
+                if (at < SEG + SEG_LA + 16) L.rb[at] = v[q];
+                at++;
+            }
+        R += kt;
+    }
+    __syncthreads();
+    const uint32_t have = min(R, (uint32_t)(SEG + SEG_LA + 16));   /* RBSP bytes R0 .. R0 + have in LDS */
+    const int64_t hlen = P.hlen, npre = P.npre, mbs = (int64_t)P.mb_start;
+    const uint64_t total_bits = 8 * (uint64_t)Rtot >= (uint64_t)mbs ? (uint64_t)hlen + 8 * (uint64_t)Rtot - mbs
+                                                                    : (uint64_t)hlen;
+    auto first_o = [&](int64_t Rb) -> int64_t {                      /* first o >= npre with k(o) >= Rb */
+        const int64_t num = 8 * Rb + hlen - mbs;
+        const int64_t o = num <= 0 ? 0 : (num + 7) / 8;
+        return o > npre ? o : npre;
+    };
+    const int64_t o_lo = c == 0 ? 0 : first_o(R0);
+    int64_t o_hi = lastseg ? (int64_t)((total_bits + 7) >> 3) : first_o(R1);
+    if (o_hi < o_lo) o_hi = o_lo;
+    const uint32_t s = (uint32_t)((P.mb_start + 8 * (uint64_t)P.npre - (uint64_t)P.hlen) & 7u);
+    /* WRITE: the arena position and the last non-zero byte before, from
+     * k_ing_fix; else a sentinel far before the segment */
+    const int64_t SENT = -((int64_t)1 << 40);
+    int64_t lnz = WRITE ? SG[c].lnz : SENT;
+    uint8_t *A = arena + (size_t)(first_stream + (int)(p >> 1)) * ld_arena;
+    uint64_t at = WRITE ? SG[c].at : 0;
+    if (WRITE && c == 0 && t == 0) {
+        const uint64_t a0 = P.at;
+        A[a0] = 0;
+        A[a0 + 1] = 0;
+        A[a0 + 2] = 0;
+        A[a0 + 3] = 1;
+        A[a0 + 4] = (uint8_t)(((P.ref_idc & 3) << 5) | (P.type & 31));
+    }
+    int64_t fmin = -1, lastnz = -1;
+    uint32_t cafter = 0;
+    for (int64_t O = o_lo; O < o_hi; O += OCH) {
+        const int64_t oc = o_hi - O < (int64_t)OCH ? o_hi - O : (int64_t)OCH;
+        uint8_t ob[16];
+        int my_lnz = -1, my_f = 0x7fffffff;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            const int64_t o = O + 16 * t + q;
+            uint32_t x = 0;
+            if (o < O + oc) {
+                if (o < npre) {
+                    x = P.pre[o];
+                } else {
+                    const uint64_t qb = 8 * (uint64_t)o - (uint64_t)hlen + (uint64_t)mbs;
+                    const uint64_t kk = qb >> 3;
+                    const uint32_t li = (uint32_t)(kk - R0);
+                    const uint32_t a = kk < Rtot && li < have ? L.rb[li] : 0u;
+                    const uint32_t b = kk + 1 < Rtot && li + 1 < have ? L.rb[li + 1] : 0u;
+                    x = ((a << s) | (b >> (8 - s))) & 255u;
+                    if (8 * (uint64_t)o + 8 > total_bits) x &= (0xff00u >> (total_bits - 8 * (uint64_t)o)) & 255u;
+                }
+                if (x) {
+                    my_lnz = (int)(o - O);
+                    my_f = min(my_f, (int)(o - O));
+                }
+            }
+            ob[q] = (uint8_t)x;
+        }
+        int mx_ex, mx_tot;
+        block_excl_max(my_lnz, L.wmax, mx_ex, mx_tot);
+        int mn_ex, mn_tot;
+        block_excl_max(my_f == 0x7fffffff ? -1 : 0x7fffffff - my_f, L.wmin, mn_ex, mn_tot);
+        if (fmin < 0 && mn_tot >= 0) fmin = O + (0x7fffffff - mn_tot) - o_lo;
+        int64_t prev = mx_ex >= 0 ? O + mx_ex : lnz;
+        uint32_t insm = 0;
+        int nins = 0, nout = 0, naft = 0;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            const int64_t o = O + 16 * t + q;
+            if (o < O + oc) {
+                const int64_t run = o - 1 - prev;
+                if (ob[q] <= 3 && run >= 2 && !(run & 1)) {
+                    insm |= 1u << q;
+                    nins++;
+                    if (prev >= o_lo) naft++;
+                }
+                if (ob[q]) prev = o;
+                nout++;
+            }
+        }
+        if (WRITE) {
+            uint32_t oex, otot;
+            block_excl_sum((uint32_t)(nout + nins), L.wsum, oex, otot);
+            {
+                uint32_t kq = oex;
+#pragma unroll
+                for (int q = 0; q < 16; ++q) {
+                    if (q >= nout) break;
+                    if ((insm >> q) & 1u) L.obuf[kq++] = 3;
+                    L.obuf[kq++] = ob[q];
+                }
+            }
+            __syncthreads();
+            for (uint32_t kq = (uint32_t)t; kq < otot; kq += DT) A[at + kq] = L.obuf[kq];
+            at += otot;
+            __syncthreads();
+        } else {
+            uint32_t aex, atot;
+            block_excl_sum((uint32_t)naft, L.wsum, aex, atot);
+            cafter += atot;
+        }
+        if (mx_tot >= 0) {
+            lnz = O + mx_tot;
+            lastnz = lnz - o_lo;
+        }
+    }
+    (void)lane;
+    if (!WRITE && t == 0) {
+        IngSeg &G = SG[c];
+        G.nout = (uint32_t)(o_hi - o_lo);
+        G.o_lo = (uint64_t)o_lo;
+        G.f = (int32_t)fmin;
+        G.vf = 0;
+        G.last = (int32_t)lastnz;
+        G.cafter = cafter;
+    }
+    if (!WRITE && fmin >= 0) {                          /* the first non-zero byte's value */
+        const int64_t o = o_lo + fmin;
+        if (t == 0) {
+            uint32_t x;
+            if (o < npre) {
+                x = P.pre[o];
+            } else {
+                const uint64_t qb = 8 * (uint64_t)o - (uint64_t)hlen + (uint64_t)mbs, kk = qb >> 3;
+                const uint32_t li = (uint32_t)(kk - R0);
+                const uint32_t a = kk < Rtot && li < have ? L.rb[li] : 0u;
+                const uint32_t b = kk + 1 < Rtot && li + 1 < have ? L.rb[li + 1] : 0u;
+                x = ((a << s) | (b >> (8 - s))) & 255u;
+                if (8 * (uint64_t)o + 8 > total_bits) x &= (0xff00u >> (total_bits - 8 * (uint64_t)o)) & 255u;
+            }
+            SG[c].vf = (int32_t)x;
+        }
+    }
+}
+
+/* per stream, serial over the segments of A then B: arena offsets */
+__global__ __launch_bounds__(64) void k_ing_fix(IngPlan *__restrict__ plans, IngSeg *__restrict__ segs,
+                                                uint32_t maxseg, IngestOut *__restrict__ outs, int nstreams,
+                                                uint64_t cap)
+{
+    const int k = blockIdx.x * 64 + threadIdx.x;
+    if (k >= nstreams) return;
+    IngPlan &PA = plans[2 * k], &PB = plans[2 * k + 1];
+    if (!PA.ok) return;
+    uint64_t at = PA.at;
+    bool over = false;
+    for (int f = 0; f < 2; ++f) {
+        IngPlan &P = f ? PB : PA;
+        IngSeg *SG = segs + (size_t)(2 * k + f) * maxseg;
+        P.at = at;
+        uint64_t pos = at + 5;
+        int64_t lnz = -1;
+        for (uint32_t c = 0; c < P.nseg; ++c) {
+            IngSeg &G = SG[c];
+            G.at = pos;
+            G.lnz = lnz;
+            const int64_t o0 = (int64_t)G.o_lo;
+            const int64_t of = G.f >= 0 ? o0 + G.f : o0 + (int64_t)G.nout;   /* first non-zero (or the end) */
+            /* zero bytes o0 .. of - 1: run o - 1 - lnz */
+            int64_t ins = G.nout ? evens_ge2(o0 - 1 - lnz, of - 2 - lnz) : 0;
+            if (G.f >= 0) {
+                const int64_t run = of - 1 - lnz;
+                if (G.vf <= 3 && run >= 2 && !(run & 1)) ins++;
+                ins += G.cafter;
+                lnz = o0 + G.last;
+            }
+            pos += G.nout + (uint64_t)ins;
+        }
+        if (pos > cap) over = true;
+        at = pos;
+    }
+    if (over) {
+        PA.ok = PB.ok = 0;
+        outs[k].err = ING_ERR_OVERFLOW;
+        outs[k].bytes = 0;
+    } else {
+        outs[k].bytes = at;
+    }
+}
+
+/* ---------------------------------------------------------------------- */
 /* k_ing_update: mid-stream long-term reference ("atlas") updates          */
 /* ---------------------------------------------------------------------- */
 /* One workgroup per update of a live stream: the file's first SPS / PPS /
@@ -765,7 +1169,7 @@ int update_launch(hipStream_t hs, const uint8_t *in, const IngestFile *files, in
 
 int ingest_launch(hipStream_t hs, const uint8_t *in, const IngestFile *files, int nstreams,
                   uint64_t max_file, IngestScan *scan, IngestOut *outs, uint8_t *arena,
-                  uint64_t ld_arena, uint64_t cap, int first_stream)
+                  uint64_t ld_arena, uint64_t cap, int first_stream, void *work)
 {
     if (nstreams <= 0) return 0;
     if (hipMemsetAsync(scan, 0, sizeof(IngestScan) * 2 * (size_t)nstreams, hs) != hipSuccess)
@@ -775,7 +1179,28 @@ int ingest_launch(hipStream_t hs, const uint8_t *in, const IngestFile *files, in
         hipLaunchKernelGGL(k_ing_scan, dim3(gx, 2 * nstreams), dim3(DT), 0, hs, in, files, scan);
         if (hipGetLastError() != hipSuccess) return -1;
     }
-    hipLaunchKernelGGL(k_ing_stream, dim3(nstreams), dim3(DT), 0, hs, in, files, scan, outs, arena,
+    if (!work) {                        /* one workgroup per stream (SCROLL_INGEST_SERIAL) */
+        hipLaunchKernelGGL(k_ing_stream, dim3(nstreams), dim3(DT), 0, hs, in, files, scan, outs, arena,
+                           ld_arena, cap, first_stream);
+        return hipGetLastError() == hipSuccess ? 0 : -1;
+    }
+    const uint32_t maxseg = (uint32_t)((max_file + SEG - 1) / SEG) + 1u;
+    IngPlan *plans = reinterpret_cast<IngPlan *>(work);
+    IngSeg *segs = reinterpret_cast<IngSeg *>(plans + 2 * (size_t)nstreams);
+    hipLaunchKernelGGL(k_ing_head, dim3(nstreams), dim3(DT), 0, hs, in, files, scan, outs, plans, maxseg, arena,
                        ld_arena, cap, first_stream);
+    hipLaunchKernelGGL(k_ing_count, dim3(maxseg, 2 * nstreams), dim3(DT), 0, hs, in, plans, segs, maxseg);
+    hipLaunchKernelGGL(k_ing_seg<false>, dim3(maxseg, 2 * nstreams), dim3(DT), 0, hs, in, plans, segs, maxseg,
+                       arena, ld_arena, first_stream);
+    hipLaunchKernelGGL(k_ing_fix, dim3((nstreams + 63) / 64), dim3(64), 0, hs, plans, segs, maxseg, outs,
+                       nstreams, cap);
+    hipLaunchKernelGGL(k_ing_seg<true>, dim3(maxseg, 2 * nstreams), dim3(DT), 0, hs, in, plans, segs, maxseg,
+                       arena, ld_arena, first_stream);
     return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+size_t ingest_work_bytes(int nstreams, uint64_t max_file)
+{
+    const size_t maxseg = (size_t)((max_file + SEG - 1) / SEG) + 1u;
+    return 2 * (size_t)nstreams * (sizeof(IngPlan) + maxseg * sizeof(IngSeg));
 }

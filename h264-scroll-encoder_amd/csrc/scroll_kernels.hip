@@ -963,6 +963,8 @@ struct ScrollBatch {
     IngestScan *d_ing_scan = nullptr;
     IngestOut *d_ing_out = nullptr;
     int ing_cap = 0;
+    void *d_ing_work = nullptr;                 /* segmented ingest scratch */
+    size_t ing_work_bytes = 0;
     hipEvent_t ing_ev[2] = {};         /* timing: around the ingest kernels */
     hipStream_t pipe = nullptr;        /* dynamic coder: k_dyn_group chunks beside the code chain */
     hipEvent_t pipe_ev[DYN_PIPE_CHUNKS + 1] = {};
@@ -1115,6 +1117,7 @@ void scroll_batch_destroy(ScrollBatch *b)
     (void)hipFree(b->d_ing_files);
     (void)hipFree(b->d_ing_scan);
     (void)hipFree(b->d_ing_out);
+    (void)hipFree(b->d_ing_work);
     for (hipEvent_t e : b->ing_ev)
         if (e) (void)hipEventDestroy(e);
     if (b->d_dbg) (void)hipFree(b->d_dbg);
@@ -2632,6 +2635,19 @@ int scroll_batch_ingest_device(ScrollBatch *b, int n, const uint8_t *d_files, co
         files[k].size = desc[2 * k + 1];
         maxf = std::max(maxf, files[k].size);
     }
+    const bool serial = getenv("SCROLL_INGEST_SERIAL") != nullptr;
+    const size_t wb = serial ? 0 : ingest_work_bytes(n, maxf);
+    if (wb > b->ing_work_bytes) {
+        (void)hipFree(b->d_ing_work);
+        b->d_ing_work = nullptr;
+        b->ing_work_bytes = 0;
+        hipError_t e = hipMalloc(&b->d_ing_work, wb);
+        if (e != hipSuccess) {
+            set_err("scroll_batch_ingest: %s", hipGetErrorString(e));
+            return e == hipErrorOutOfMemory ? SCROLL_ERR_OOM : SCROLL_ERR_HIP;
+        }
+        b->ing_work_bytes = wb;
+    }
     hipStream_t hs = b->own;
     HIPCHK(hipMemcpyAsync(b->d_ing_files, files.data(), files.size() * sizeof(IngestFile),
                           hipMemcpyHostToDevice, hs));
@@ -2641,7 +2657,8 @@ int scroll_batch_ingest_device(ScrollBatch *b, int n, const uint8_t *d_files, co
         HIPCHK(hipEventRecord(b->ing_ev[0], hs));
     }
     if (ingest_launch(hs, d_files, b->d_ing_files, n, maxf, b->d_ing_scan, b->d_ing_out,
-                      b->d_arena, (uint64_t)b->ld_arena, (uint64_t)b->arena_bytes, b->nstreams)) {
+                      b->d_arena, (uint64_t)b->ld_arena, (uint64_t)b->arena_bytes, b->nstreams,
+                      serial ? nullptr : b->d_ing_work)) {
         set_err("ingest launch: %s", hipGetErrorString(hipGetLastError()));
         return SCROLL_ERR_HIP;
     }

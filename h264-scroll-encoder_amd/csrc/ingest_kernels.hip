@@ -48,19 +48,76 @@ constexpr int OBUF = OCH + OCH / 2 + 64; /* one chunk after EP (<= 1.5x)        
 /* ---------------------------------------------------------------------- */
 /* k_ing_scan                                                              */
 /* ---------------------------------------------------------------------- */
+/* The 16 bytes of the aligned 16-byte chunk at absolute address a, with the
+ * dword before it and the dword after, for the byte-pattern rules (start
+ * codes, emulation-prevention removal).  Lanes of a wave hold consecutive
+ * chunks, so the neighbours come over lanes; the wave's end lanes load them.
+ * Only chunks / dwords holding a byte of the file [lo, hi) are read: no load
+ * leaves the pages of the file's bytes.  Every lane of the wave calls it. */
+struct Chunk16 {
+    uint32_t w[4];
+    uint32_t prev, next;
+    __device__ inline uint32_t b(int q) const                /* byte q, -4 <= q < 20 */
+    {
+        const uint32_t x = q < 0 ? prev : q >= 16 ? next : w[q >> 2];
+        return (x >> (8 * ((q + 4) & 3))) & 255u;
+    }
+};
+
+__device__ inline Chunk16 load_chunk16(const uint8_t *a, const uint8_t *lo, const uint8_t *hi)
+{
+    Chunk16 c;
+    uint4 v = make_uint4(0u, 0u, 0u, 0u);
+    if (a < hi && a + 16 > lo) v = *reinterpret_cast<const uint4 *>(a);
+    c.w[0] = v.x;
+    c.w[1] = v.y;
+    c.w[2] = v.z;
+    c.w[3] = v.w;
+    const int lane = threadIdx.x & 63;
+    c.prev = __shfl_up(v.w, 1, 64);
+    c.next = __shfl_down(v.x, 1, 64);
+    if (lane == 0) c.prev = (a - 1 >= lo && a - 1 < hi) ? *reinterpret_cast<const uint32_t *>(a - 4) : 0u;
+    if (lane == 63) c.next = (a + 16 >= lo && a + 16 < hi) ? *reinterpret_cast<const uint32_t *>(a + 16) : 0u;
+    return c;
+}
+
+__device__ inline const uint8_t *align16_down(const uint8_t *p)
+{
+    return reinterpret_cast<const uint8_t *>(reinterpret_cast<uintptr_t>(p) & ~(uintptr_t)15);
+}
+
+/* bit q: byte q of the chunk (file index i0 + q) is an emulation-prevention
+ * byte (nal_parser.c:72: 03 after 00 00, before a byte <= 3) */
+__device__ inline uint32_t ep_removed16(const Chunk16 &c, int64_t i0, int64_t n)
+{
+    uint32_t m = 0;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+        const int64_t i = i0 + q;
+        const bool rm = c.b(q) == 3 && c.b(q - 1) == 0 && c.b(q - 2) == 0 && c.b(q + 1) <= 3 && i >= 2 &&
+                        i + 1 < n;
+        m |= rm ? 1u << q : 0u;
+    }
+    return m;
+}
+
 __global__ __launch_bounds__(DT) void k_ing_scan(const uint8_t *__restrict__ in,
                                                  const IngestFile *__restrict__ files,
                                                  IngestScan *__restrict__ scan)
 {
     const int fi = blockIdx.y;
     const IngestFile F = files[fi];
-    const uint64_t base = (uint64_t)blockIdx.x * WINB + 16u * threadIdx.x;
-    if (base >= F.size) return;
-    const uint8_t *d = in + F.off;
-    for (uint64_t i = base; i < base + 16 && i + 2 < F.size; ++i) {
-        if (d[i] == 0 && d[i + 1] == 0 && d[i + 2] == 1) {     /* nal_parser.c:16-18 */
-            const uint32_t k = atomicAdd(&scan[fi].n, 1u);
-            if (k < (uint32_t)ING_SC_MAX) scan[fi].pos[k] = i;
+    const uint8_t *d = in + F.off, *hi = d + F.size;
+    const uint8_t *a = align16_down(d) + (size_t)blockIdx.x * WINB + 16u * threadIdx.x;
+    if (align16_down(d) + (size_t)blockIdx.x * WINB >= hi) return;     /* uniform over the block */
+    const Chunk16 c = load_chunk16(a, d, hi);
+    const int64_t i0 = a - d;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+        const int64_t i = i0 + q;
+        if (i >= 0 && i + 2 < (int64_t)F.size && c.b(q) == 0 && c.b(q + 1) == 0 && c.b(q + 2) == 1) {
+            const uint32_t k = atomicAdd(&scan[fi].n, 1u);            /* nal_parser.c:16-18 */
+            if (k < (uint32_t)ING_SC_MAX) scan[fi].pos[k] = (uint32_t)i;
         }
     }
 }
@@ -641,12 +698,11 @@ __global__ __launch_bounds__(DT) void k_ing_stream(const uint8_t *__restrict__ i
  *   k_ing_head        per stream: the parse and the SPS / PPS NAL units of
  *                     k_ing_stream, and a plan per slice (input range,
  *                     header bits, first output bytes)
- *   k_ing_count       per segment: its RBSP bytes (closed-form removal)
- *   k_ing_seg<false>  per segment: its output bytes -- the RBSP bytes it
- *                     holds, shifted behind the new header -- summarised for
- *                     emulation prevention: first / last non-zero byte and
- *                     the insertions after the first, which do not depend on
- *                     what came before
+ *   k_ing_seg<false>  per segment: its RBSP bytes (closed-form removal) and
+ *                     its output bytes -- those RBSP bytes shifted behind the
+ *                     new header -- summarised for emulation prevention:
+ *                     first / last non-zero byte and the insertions after the
+ *                     first, which do not depend on what came before
  *   k_ing_fix         per stream, serial over its segments: each one's
  *                     insertions before its first non-zero byte (closed form
  *                     in the last non-zero byte before it), hence its arena
@@ -669,13 +725,12 @@ struct IngPlan {                         /* one slice of a new stream           
 };
 
 struct IngSeg {
-    uint32_t kept;                       /* RBSP bytes (k_ing_count)                */
-    uint32_t nout;                       /* output bytes it owns (k_ing_seg<false>) */
-    int32_t f, vf, last;                 /* first non-zero output byte (relative, -1: none), its
-                                          * value, the last non-zero one                      */
+    uint32_t kept;                       /* RBSP bytes (k_ing_seg<false>)           */
+    uint32_t nout;                       /* output bytes it owns                    */
+    int32_t f, vf, last;                 /* first non-zero output byte (relative to its first,
+                                          * -1: none), its value, the last non-zero one */
     uint32_t cafter;                     /* EP insertions after the first non-zero byte */
-    uint64_t o_lo;                       /* its first output byte                   */
-    int64_t lnz;                         /* last non-zero output byte before it (k_ing_fix) */
+    int64_t lnz;                         /* last non-zero output byte before it, relative (k_ing_fix) */
     uint64_t at;                         /* arena offset of its first output byte (k_ing_fix) */
 };
 
@@ -761,46 +816,82 @@ __global__ __launch_bounds__(DT) void k_ing_head(const uint8_t *__restrict__ in,
     o.deblock = L.dbf;
 }
 
-/* EBSP byte i of d[0, n) is an emulation-prevention byte (nal_parser.c:72) */
-__device__ inline bool ebsp_removed(const uint8_t *d, uint64_t n, uint64_t i)
+/* ---- workgroup scans of NV values at once (2 barriers for all) ---- */
+template <int NV>
+__device__ inline void block_excl_sum_v(const uint32_t (&v)[NV], uint32_t (*ws)[NW], uint32_t (&excl)[NV],
+                                        uint32_t (&tot)[NV])
 {
-    return i >= 2 && i + 1 < n && d[i] == 3 && d[i - 1] == 0 && d[i - 2] == 0 && d[i + 1] <= 3;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint32_t incl[NV];
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+        incl[j] = wave_incl_sum(v[j], lane);
+        if (lane == 63) ws[j][wave] = incl[j];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+        uint32_t pm = 0, tt = 0;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) {
+            const uint32_t x = ws[j][w];
+            pm += w < wave ? x : 0u;
+            tt += x;
+        }
+        excl[j] = pm + incl[j] - v[j];
+        tot[j] = tt;
+    }
+    __syncthreads();
 }
 
-__global__ __launch_bounds__(DT) void k_ing_count(const uint8_t *__restrict__ in,
-                                                  const IngPlan *__restrict__ plans,
-                                                  IngSeg *__restrict__ segs, uint32_t maxseg)
+template <int NV>
+__device__ inline void block_excl_max_v(const int (&v)[NV], int (*ws)[NW], int (&excl)[NV], int (&tot)[NV])
 {
-    __shared__ uint32_t wsum[NW];
-    const uint32_t c = blockIdx.x, p = blockIdx.y;
-    const IngPlan &P = plans[p];
-    if (!P.ok || c >= P.nseg) return;
-    const uint8_t *d = in + P.in;
-    const uint64_t e0 = (uint64_t)c * SEG, e1 = min(P.n, e0 + SEG);
-    uint32_t kept = 0;
-    for (uint64_t i = e0 + threadIdx.x; i < e1; i += DT) kept += ebsp_removed(d, P.n, i) ? 0u : 1u;
-    uint32_t ex, tot;
-    block_excl_sum(kept, wsum, ex, tot);
-    if (threadIdx.x == 0) segs[(size_t)p * maxseg + c].kept = tot;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    int incl[NV];
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+        incl[j] = wave_incl_max(v[j], lane);
+        if (lane == 63) ws[j][wave] = incl[j];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+        int e = __shfl_up(incl[j], 1, 64);
+        if (lane == 0) e = -1;
+        int pm = -1, tt = -1;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) {
+            const int x = ws[j][w];
+            pm = w < wave ? max(pm, x) : pm;
+            tt = max(tt, x);
+        }
+        excl[j] = max(pm, e);
+        tot[j] = tt;
+    }
+    __syncthreads();
 }
+
+constexpr int NJ = (int)((SEG + SEG_LA + 15 + 16 * DT - 1) / (16 * DT));   /* 16-byte-per-lane windows */
+constexpr uint32_t RBCAP = SEG + SEG_LA + 16;                            /* RBSP bytes kept in LDS   */
 
 struct SegLds {
-    uint8_t rb[SEG + SEG_LA + 16];       /* the segment's RBSP bytes (+ look-ahead)   */
-    uint8_t obuf[OBUF];
-    uint32_t wsum[NW];
-    int32_t wmax[NW];
-    int32_t wmin[NW];
-    uint32_t R0;
+    alignas(16) uint8_t rb[RBCAP + 48];  /* the segment's RBSP bytes (+ look-ahead), zeros after */
+    alignas(16) uint8_t obuf[OBUF + 16]; /* one window of output bytes after EP, at the arena's phase */
+    uint32_t wsum[NJ + 1][NW];
+    int32_t wmax[NJ][NW];
+    int32_t wmin[1][NW];
 };
 
-/* even numbers >= 2 in [a, b] */
-__device__ inline int64_t evens_ge2(int64_t a, int64_t b)
-{
-    if (a < 2) a = 2;
-    const int64_t f = a + (a & 1);
-    return b < f ? 0 : (b - f) / 2 + 1;
-}
-
+/* One segment of a slice body: EBSP bytes [c SEG, (c + 1) SEG) of the
+ * payload.  Its output bytes do not depend on the segments before: output
+ * byte u (relative) is RBSP byte u and the next one (the look-ahead byte at
+ * the end) shifted by the slice's constant s -- for segment 0 after the
+ * npre header bytes -- so k_ing_seg<false> summarises a segment without
+ * knowing where it lands, and k_ing_seg<true> writes it where k_ing_fix
+ * puts it.  Emulation prevention needs the last non-zero byte before each
+ * byte: inside the segment a max-scan, from the segments before k_ing_fix's
+ * lnz.  All windows of a phase share one workgroup scan. */
 template <bool WRITE>
 __global__ __launch_bounds__(DT) void k_ing_seg(const uint8_t *__restrict__ in,
                                                 const IngPlan *__restrict__ plans,
@@ -810,188 +901,244 @@ __global__ __launch_bounds__(DT) void k_ing_seg(const uint8_t *__restrict__ in,
 {
     __shared__ SegLds L;
     const uint32_t c = blockIdx.x, p = blockIdx.y;
-    const int t = threadIdx.x, lane = t & 63;
+    const int t = threadIdx.x;
     const IngPlan &P = plans[p];
     if (!P.ok || c >= P.nseg) return;
-    IngSeg *SG = segs + (size_t)p * maxseg;
+    IngSeg &G = segs[(size_t)p * maxseg + c];
     const uint8_t *d = in + P.in;
-    const uint64_t n = P.n;
-    /* RBSP bytes before this segment, and in the whole payload */
-    uint32_t pre = 0, all = 0;
-    for (uint32_t q = (uint32_t)t; q < P.nseg; q += DT) {
-        const uint32_t v = SG[q].kept;
-        all += v;
-        if (q < c) pre += v;
-    }
-    uint32_t ex, R0, Rtot;
-    block_excl_sum(pre, L.wsum, ex, R0);
-    block_excl_sum(all, L.wsum, ex, Rtot);
-    const uint32_t kept = SG[c].kept, R1 = R0 + kept;
+    const int64_t n = (int64_t)P.n;
     const bool lastseg = c + 1 == P.nseg;
-    /* this segment's RBSP bytes (and the next segment's first ones) -> LDS */
-    const uint64_t e0 = (uint64_t)c * SEG, e1 = min(n, e0 + SEG + SEG_LA);
-    uint32_t R = 0;
-    for (uint64_t w0 = e0; w0 < e1; w0 += 16u * DT) {
-        uint32_t keepm = 0, kn = 0;
-        uint8_t v[16];
+    /* 1. RBSP bytes of [e0, e1) -> LDS; kept: those of [e0, es) */
+    const int64_t e0 = (int64_t)c * SEG, es = min(n, e0 + (int64_t)SEG), e1 = min(n, e0 + (int64_t)(SEG + SEG_LA));
+    const uint8_t *a0 = align16_down(d + e0), *hi = d + min(n, e1 + 1);
+    uint32_t have, kept;
+    {
+        uint32_t km[NJ], cnt[NJ + 1];
+        cnt[NJ] = 0;
+        Chunk16 ch[NJ];
 #pragma unroll
-        for (int q = 0; q < 16; ++q) {
-            const uint64_t i = w0 + 16u * (uint32_t)t + (uint64_t)q;
-            v[q] = 0;
-            if (i < e1) {
-                v[q] = d[i];
-                if (!ebsp_removed(d, n, i)) {
-                    keepm |= 1u << q;
-                    kn++;
-                }
+        for (int j = 0; j < NJ; ++j) ch[j] = load_chunk16(a0 + 16 * (t + DT * j), d, hi);
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            const int64_t i0 = a0 + 16 * (t + DT * j) - d;
+            km[j] = 0;
+            uint32_t sm = 0;
+            if (i0 + 16 > e0 && i0 < e1) {
+                const uint32_t rm = ep_removed16(ch[j], i0, n);
+                const int64_t lo = max(e0 - i0, (int64_t)0), h1 = min(e1 - i0, (int64_t)16),
+                              h2 = min(es - i0, (int64_t)16);
+                const uint64_t lom = (1ull << lo) - 1;
+                km[j] = (uint32_t)(((1ull << h1) - 1) & ~lom) & ~rm;
+                sm = h2 > lo ? (uint32_t)(((1ull << h2) - 1) & ~lom) & ~rm : 0u;
             }
+            cnt[j] = (uint32_t)__popc(km[j]);
+            cnt[NJ] += (uint32_t)__popc(sm);
         }
-        uint32_t kx, kt;
-        block_excl_sum(kn, L.wsum, kx, kt);
-        uint32_t at = R + kx;
+        uint32_t ex[NJ + 1], tot[NJ + 1];
+        block_excl_sum_v<NJ + 1>(cnt, L.wsum, ex, tot);
+        uint32_t base = 0;
 #pragma unroll
-        for (int q = 0; q < 16; ++q)
-            if ((keepm >> q) & 1u) {
-                if (at < SEG + SEG_LA + 16) L.rb[at] = v[q];
-                at++;
-            }
-        R += kt;
+        for (int j = 0; j < NJ; ++j) {
+            uint32_t at = base + ex[j];
+#pragma unroll
+            for (int q = 0; q < 16; ++q)
+                if ((km[j] >> q) & 1u) {
+                    if (at < RBCAP) L.rb[at] = (uint8_t)ch[j].b(q);
+                    at++;
+                }
+            base += tot[j];
+        }
+        have = min(base, RBCAP);
+        kept = tot[NJ];
     }
+    if (t < 48) L.rb[have + t] = 0;                         /* bytes past the end read as 0 */
     __syncthreads();
-    const uint32_t have = min(R, (uint32_t)(SEG + SEG_LA + 16));   /* RBSP bytes R0 .. R0 + have in LDS */
-    const int64_t hlen = P.hlen, npre = P.npre, mbs = (int64_t)P.mb_start;
-    const uint64_t total_bits = 8 * (uint64_t)Rtot >= (uint64_t)mbs ? (uint64_t)hlen + 8 * (uint64_t)Rtot - mbs
-                                                                    : (uint64_t)hlen;
-    auto first_o = [&](int64_t Rb) -> int64_t {                      /* first o >= npre with k(o) >= Rb */
-        const int64_t num = 8 * Rb + hlen - mbs;
-        const int64_t o = num <= 0 ? 0 : (num + 7) / 8;
-        return o > npre ? o : npre;
-    };
-    const int64_t o_lo = c == 0 ? 0 : first_o(R0);
-    int64_t o_hi = lastseg ? (int64_t)((total_bits + 7) >> 3) : first_o(R1);
-    if (o_hi < o_lo) o_hi = o_lo;
-    const uint32_t s = (uint32_t)((P.mb_start + 8 * (uint64_t)P.npre - (uint64_t)P.hlen) & 7u);
-    /* WRITE: the arena position and the last non-zero byte before, from
-     * k_ing_fix; else a sentinel far before the segment */
-    const int64_t SENT = -((int64_t)1 << 40);
-    int64_t lnz = WRITE ? SG[c].lnz : SENT;
-    uint8_t *A = arena + (size_t)(first_stream + (int)(p >> 1)) * ld_arena;
-    uint64_t at = WRITE ? SG[c].at : 0;
-    if (WRITE && c == 0 && t == 0) {
-        const uint64_t a0 = P.at;
-        A[a0] = 0;
-        A[a0 + 1] = 0;
-        A[a0 + 2] = 0;
-        A[a0 + 3] = 1;
-        A[a0 + 4] = (uint8_t)(((P.ref_idc & 3) << 5) | (P.type & 31));
-    }
-    int64_t fmin = -1, lastnz = -1;
-    uint32_t cafter = 0;
-    for (int64_t O = o_lo; O < o_hi; O += OCH) {
-        const int64_t oc = o_hi - O < (int64_t)OCH ? o_hi - O : (int64_t)OCH;
-        uint8_t ob[16];
-        int my_lnz = -1, my_f = 0x7fffffff;
-#pragma unroll
-        for (int q = 0; q < 16; ++q) {
-            const int64_t o = O + 16 * t + q;
-            uint32_t x = 0;
-            if (o < O + oc) {
-                if (o < npre) {
-                    x = P.pre[o];
-                } else {
-                    const uint64_t qb = 8 * (uint64_t)o - (uint64_t)hlen + (uint64_t)mbs;
-                    const uint64_t kk = qb >> 3;
-                    const uint32_t li = (uint32_t)(kk - R0);
-                    const uint32_t a = kk < Rtot && li < have ? L.rb[li] : 0u;
-                    const uint32_t b = kk + 1 < Rtot && li + 1 < have ? L.rb[li + 1] : 0u;
-                    x = ((a << s) | (b >> (8 - s))) & 255u;
-                    if (8 * (uint64_t)o + 8 > total_bits) x &= (0xff00u >> (total_bits - 8 * (uint64_t)o)) & 255u;
-                }
-                if (x) {
-                    my_lnz = (int)(o - O);
-                    my_f = min(my_f, (int)(o - O));
-                }
-            }
-            ob[q] = (uint8_t)x;
-        }
-        int mx_ex, mx_tot;
-        block_excl_max(my_lnz, L.wmax, mx_ex, mx_tot);
-        int mn_ex, mn_tot;
-        block_excl_max(my_f == 0x7fffffff ? -1 : 0x7fffffff - my_f, L.wmin, mn_ex, mn_tot);
-        if (fmin < 0 && mn_tot >= 0) fmin = O + (0x7fffffff - mn_tot) - o_lo;
-        int64_t prev = mx_ex >= 0 ? O + mx_ex : lnz;
-        uint32_t insm = 0;
-        int nins = 0, nout = 0, naft = 0;
-#pragma unroll
-        for (int q = 0; q < 16; ++q) {
-            const int64_t o = O + 16 * t + q;
-            if (o < O + oc) {
-                const int64_t run = o - 1 - prev;
-                if (ob[q] <= 3 && run >= 2 && !(run & 1)) {
-                    insm |= 1u << q;
-                    nins++;
-                    if (prev >= o_lo) naft++;
-                }
-                if (ob[q]) prev = o;
-                nout++;
-            }
-        }
-        if (WRITE) {
-            uint32_t oex, otot;
-            block_excl_sum((uint32_t)(nout + nins), L.wsum, oex, otot);
-            {
-                uint32_t kq = oex;
-#pragma unroll
-                for (int q = 0; q < 16; ++q) {
-                    if (q >= nout) break;
-                    if ((insm >> q) & 1u) L.obuf[kq++] = 3;
-                    L.obuf[kq++] = ob[q];
-                }
-            }
-            __syncthreads();
-            for (uint32_t kq = (uint32_t)t; kq < otot; kq += DT) A[at + kq] = L.obuf[kq];
-            at += otot;
-            __syncthreads();
+    /* 2. the segment's output bytes u = 0 .. nout - 1 */
+    const int64_t hlen = P.hlen, npre = P.npre, mbs = (int64_t)P.mb_start, D = hlen - mbs;
+    const int64_t cd = (D + 7) >> 3;                        /* ceil(D / 8) */
+    const uint32_t s = (uint32_t)((-D) & 7);
+    int64_t nout, off = 0, ufast = 0, umask = INT64_MAX, total_bits = 0;
+    if (c == 0) {
+        off = -cd;                                          /* RBSP byte of output u: u - cd */
+        ufast = npre;
+        if (lastseg) {
+            total_bits = 8 * (int64_t)kept >= mbs ? D + 8 * (int64_t)kept : hlen;
+            nout = (total_bits + 7) >> 3;
+            umask = total_bits >> 3;
         } else {
-            uint32_t aex, atot;
-            block_excl_sum((uint32_t)naft, L.wsum, aex, atot);
-            cafter += atot;
+            nout = max((int64_t)kept + cd, npre);
         }
-        if (mx_tot >= 0) {
-            lnz = O + mx_tot;
-            lastnz = lnz - o_lo;
-        }
+    } else {
+        nout = kept;
     }
-    (void)lane;
-    if (!WRITE && t == 0) {
-        IngSeg &G = SG[c];
-        G.nout = (uint32_t)(o_hi - o_lo);
-        G.o_lo = (uint64_t)o_lo;
-        G.f = (int32_t)fmin;
-        G.vf = 0;
-        G.last = (int32_t)lastnz;
-        G.cafter = cafter;
-    }
-    if (!WRITE && fmin >= 0) {                          /* the first non-zero byte's value */
-        const int64_t o = o_lo + fmin;
-        if (t == 0) {
-            uint32_t x;
-            if (o < npre) {
-                x = P.pre[o];
-            } else {
-                const uint64_t qb = 8 * (uint64_t)o - (uint64_t)hlen + (uint64_t)mbs, kk = qb >> 3;
-                const uint32_t li = (uint32_t)(kk - R0);
-                const uint32_t a = kk < Rtot && li < have ? L.rb[li] : 0u;
-                const uint32_t b = kk + 1 < Rtot && li + 1 < have ? L.rb[li + 1] : 0u;
-                x = ((a << s) | (b >> (8 - s))) & 255u;
-                if (8 * (uint64_t)o + 8 > total_bits) x &= (0xff00u >> (total_bits - 8 * (uint64_t)o)) & 255u;
+    uint32_t ow[NJ][4];
+    int my_l[NJ], my_f = INT32_MAX;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+        const int64_t u0 = (int64_t)OCH * j + 16 * t;
+        ow[j][0] = ow[j][1] = ow[j][2] = ow[j][3] = 0;
+        my_l[j] = -1;
+        if (u0 >= nout) continue;
+        if (u0 >= ufast && u0 + 16 <= umask) {
+            /* RBSP bytes li0 .. li0 + 16 from five LDS dwords, then the bit
+             * shift s of every byte with SWAR masks */
+            const uint32_t li0 = (uint32_t)(u0 + off), m = li0 & 3u;
+            const uint32_t *rw = reinterpret_cast<const uint32_t *>(L.rb) + (li0 >> 2);
+            const uint32_t D0 = rw[0], D1 = rw[1], D2 = rw[2], D3 = rw[3], D4 = rw[4];
+            const uint32_t E[5] = {__builtin_amdgcn_alignbyte(D1, D0, m), __builtin_amdgcn_alignbyte(D2, D1, m),
+                                   __builtin_amdgcn_alignbyte(D3, D2, m), __builtin_amdgcn_alignbyte(D4, D3, m),
+                                   D4 >> (8 * m)};
+            const uint32_t mH = ((0xffu << s) & 0xffu) * 0x01010101u, mL = (0xffu >> (8 - s)) * 0x01010101u;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint32_t Y = __builtin_amdgcn_alignbyte(E[k + 1], E[k], 1u);
+                ow[j][k] = ((E[k] << s) & mH) | (s ? (Y >> (8 - s)) & mL : 0u);
             }
-            SG[c].vf = (int32_t)x;
+        } else {
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                const int64_t u = u0 + q;
+                uint32_t x;
+                if (c == 0 && u < npre) {
+                    x = P.pre[u];
+                } else {
+                    const int64_t k = u + off;
+                    const uint32_t a = k >= 0 && k < (int64_t)have ? L.rb[k] : 0u;
+                    const uint32_t b = k + 1 >= 0 && k + 1 < (int64_t)have ? L.rb[k + 1] : 0u;
+                    x = ((a << s) | (b >> (8 - s))) & 255u;
+                    if (u >= umask) x &= (0xff00u >> (total_bits - 8 * u)) & 255u;
+                }
+                ow[j][q >> 2] |= x << (8 * (q & 3));
+            }
         }
+        if (u0 + 16 > nout) {                               /* bytes past the segment's end */
+            const int64_t keep = nout - u0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int64_t kb = keep - 4 * k;
+                ow[j][k] &= kb >= 4 ? 0xffffffffu : kb <= 0 ? 0u : (1u << (8 * kb)) - 1;
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (ow[j][k]) {
+                my_l[j] = 16 * t + 4 * k + 3 - (__builtin_clz(ow[j][k]) >> 3);
+                if (my_f == INT32_MAX) my_f = OCH * j + 16 * t + 4 * k + (__builtin_ctz(ow[j][k]) >> 3);
+            }
+    }
+    /* 3. emulation prevention (nal.c:33-38): before byte u iff it is <= 3 and
+     * the zero run since the last non-zero byte is even and >= 2 */
+    int lx[NJ], lt[NJ];
+    block_excl_max_v<NJ>(my_l, L.wmax, lx, lt);
+    const int64_t SENT = -((int64_t)1 << 40);
+    int64_t before = WRITE ? G.lnz : SENT;                  /* relative; < 0: before the segment */
+    uint32_t nb[NJ + 1], insm[NJ];
+    uint32_t naft = 0;
+    nb[NJ] = 0;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+        const int64_t u0 = (int64_t)OCH * j + 16 * t;
+        int64_t prev = lx[j] >= 0 ? (int64_t)OCH * j + lx[j] : before;
+        insm[j] = 0;
+        nb[j] = 0;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            const int64_t u = u0 + q;
+            if (u < nout) {
+                const uint32_t x = (ow[j][q >> 2] >> (8 * (q & 3))) & 255u;
+                const int64_t run = u - 1 - prev;
+                if (x <= 3 && run >= 2 && !(run & 1)) {
+                    insm[j] |= 1u << q;
+                    nb[j]++;
+                    naft += prev >= 0 ? 1u : 0u;
+                }
+                if (x) prev = u;
+                nb[j]++;
+            }
+        }
+        if (lt[j] >= 0) before = (int64_t)OCH * j + lt[j];
+    }
+    if (!WRITE) {
+        uint32_t v1[1] = {naft}, e1v[1], t1v[1];
+        int fv[1] = {my_f == INT32_MAX ? -1 : INT32_MAX - my_f}, fe[1], ft[1];
+        block_excl_max_v<1>(fv, L.wmin, fe, ft);
+        block_excl_sum_v<1>(v1, L.wsum, e1v, t1v);
+        const int32_t first = ft[0] >= 0 ? INT32_MAX - ft[0] : -1;
+        if (t == 0) {
+            G.kept = kept;
+            G.nout = (uint32_t)nout;
+            G.f = first;
+            G.last = (int32_t)(before >= 0 ? before : -1);
+            G.cafter = t1v[0];
+            if (first < 0) G.vf = 0;
+        }
+        if (first >= 0 && my_f == first) {                  /* the lane holding the first non-zero byte */
+            const int j = first / OCH, q = first % OCH - 16 * t;
+            uint32_t x = 0;
+#pragma unroll
+            for (int jj = 0; jj < NJ; ++jj)
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    if (jj == j && k == (q >> 2)) x = (ow[jj][k] >> (8 * (q & 3))) & 255u;
+            G.vf = (int32_t)x;
+        }
+        return;
+    }
+    /* 4. write, window by window, staged at the arena address's phase in
+     * 16-byte lines: whole lines go out as one 16-byte store, the two end
+     * lines (shared with the neighbouring segments) byte by byte */
+    uint32_t ex[NJ + 1], tot[NJ + 1];
+    block_excl_sum_v<NJ + 1>(nb, L.wsum, ex, tot);
+    uint8_t *A = arena + (size_t)(first_stream + (int)(p >> 1)) * ld_arena;
+    uint64_t at = G.at;
+    if (c == 0 && t == 0) {
+        const uint64_t a5 = P.at;
+        A[a5] = 0;
+        A[a5 + 1] = 0;
+        A[a5 + 2] = 0;
+        A[a5 + 3] = 1;
+        A[a5 + 4] = (uint8_t)(((P.ref_idc & 3) << 5) | (P.type & 31));
+    }
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+        if ((int64_t)OCH * j >= nout) break;                /* uniform */
+        const uint32_t ph = (uint32_t)(reinterpret_cast<uintptr_t>(A + at) & 15u);
+        {
+            uint32_t kq = ph + ex[j];
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                if ((int64_t)OCH * j + 16 * t + q >= nout) break;
+                if ((insm[j] >> q) & 1u) L.obuf[kq++] = 3;
+                L.obuf[kq++] = (uint8_t)(ow[j][q >> 2] >> (8 * (q & 3)));
+            }
+        }
+        __syncthreads();
+        uint8_t *line0 = A + at - ph;
+        const uint32_t end = ph + tot[j], nl = (end + 15) >> 4;
+        for (uint32_t l = (uint32_t)t; l < nl; l += DT) {
+            const uint32_t b0 = 16 * l;
+            if (b0 >= ph && b0 + 16 <= end) {
+                *reinterpret_cast<uint4 *>(line0 + b0) = *reinterpret_cast<const uint4 *>(L.obuf + b0);
+            } else {
+                for (uint32_t q = max(b0, ph); q < min(b0 + 16, end); ++q) line0[q] = L.obuf[q];
+            }
+        }
+        at += tot[j];
+        __syncthreads();
     }
 }
 
-/* per stream, serial over the segments of A then B: arena offsets */
+/* even numbers >= 2 in [a, b] */
+__device__ inline int64_t evens_ge2(int64_t a, int64_t b)
+{
+    if (a < 2) a = 2;
+    const int64_t f = a + (a & 1);
+    return b < f ? 0 : (b - f) / 2 + 1;
+}
+
+/* per stream, serial over the segments of A then B: RBSP prefix, output
+ * offsets, the insertions before each segment's first non-zero byte (closed
+ * form in the last non-zero byte before it), arena offsets, the bound */
 __global__ __launch_bounds__(64) void k_ing_fix(IngPlan *__restrict__ plans, IngSeg *__restrict__ segs,
                                                 uint32_t maxseg, IngestOut *__restrict__ outs, int nstreams,
                                                 uint64_t cap)
@@ -1001,18 +1148,20 @@ __global__ __launch_bounds__(64) void k_ing_fix(IngPlan *__restrict__ plans, Ing
     IngPlan &PA = plans[2 * k], &PB = plans[2 * k + 1];
     if (!PA.ok) return;
     uint64_t at = PA.at;
-    bool over = false;
+    bool over = false, bad = false;
     for (int f = 0; f < 2; ++f) {
         IngPlan &P = f ? PB : PA;
         IngSeg *SG = segs + (size_t)(2 * k + f) * maxseg;
+        const int64_t D = (int64_t)P.hlen - (int64_t)P.mb_start, cd = (D + 7) >> 3;
         P.at = at;
-        uint64_t pos = at + 5;
-        int64_t lnz = -1;
+        uint64_t pos = at + 5, R0 = 0;
+        int64_t lnz = -1;                                   /* output index in the slice */
         for (uint32_t c = 0; c < P.nseg; ++c) {
             IngSeg &G = SG[c];
+            const int64_t o0 = c == 0 ? 0 : (int64_t)R0 + cd;
+            if (c > 0 && o0 < (int64_t)P.npre) bad = true;   /* a header longer than a segment's body */
             G.at = pos;
-            G.lnz = lnz;
-            const int64_t o0 = (int64_t)G.o_lo;
+            G.lnz = lnz - o0;
             const int64_t of = G.f >= 0 ? o0 + G.f : o0 + (int64_t)G.nout;   /* first non-zero (or the end) */
             /* zero bytes o0 .. of - 1: run o - 1 - lnz */
             int64_t ins = G.nout ? evens_ge2(o0 - 1 - lnz, of - 2 - lnz) : 0;
@@ -1023,13 +1172,15 @@ __global__ __launch_bounds__(64) void k_ing_fix(IngPlan *__restrict__ plans, Ing
                 lnz = o0 + G.last;
             }
             pos += G.nout + (uint64_t)ins;
+            R0 += G.kept;
         }
+        P.R = R0;
         if (pos > cap) over = true;
         at = pos;
     }
-    if (over) {
+    if (over || bad) {
         PA.ok = PB.ok = 0;
-        outs[k].err = ING_ERR_OVERFLOW;
+        outs[k].err = bad ? ING_ERR_PARSE : ING_ERR_OVERFLOW;
         outs[k].bytes = 0;
     } else {
         outs[k].bytes = at;
@@ -1158,7 +1309,7 @@ int update_launch(hipStream_t hs, const uint8_t *in, const IngestFile *files, in
 {
     if (n <= 0) return 0;
     if (hipMemsetAsync(scan, 0, sizeof(IngestScan) * (size_t)n, hs) != hipSuccess) return -1;
-    const uint32_t gx = (uint32_t)((max_file + WINB - 1) / WINB);
+    const uint32_t gx = (uint32_t)((max_file + 15 + WINB - 1) / WINB);
     if (gx > 0) {
         hipLaunchKernelGGL(k_ing_scan, dim3(gx, n), dim3(DT), 0, hs, in, files, scan);
         if (hipGetLastError() != hipSuccess) return -1;
@@ -1174,7 +1325,7 @@ int ingest_launch(hipStream_t hs, const uint8_t *in, const IngestFile *files, in
     if (nstreams <= 0) return 0;
     if (hipMemsetAsync(scan, 0, sizeof(IngestScan) * 2 * (size_t)nstreams, hs) != hipSuccess)
         return -1;
-    const uint32_t gx = (uint32_t)((max_file + WINB - 1) / WINB);
+    const uint32_t gx = (uint32_t)((max_file + 15 + WINB - 1) / WINB);
     if (gx > 0) {
         hipLaunchKernelGGL(k_ing_scan, dim3(gx, 2 * nstreams), dim3(DT), 0, hs, in, files, scan);
         if (hipGetLastError() != hipSuccess) return -1;
@@ -1189,7 +1340,6 @@ int ingest_launch(hipStream_t hs, const uint8_t *in, const IngestFile *files, in
     IngSeg *segs = reinterpret_cast<IngSeg *>(plans + 2 * (size_t)nstreams);
     hipLaunchKernelGGL(k_ing_head, dim3(nstreams), dim3(DT), 0, hs, in, files, scan, outs, plans, maxseg, arena,
                        ld_arena, cap, first_stream);
-    hipLaunchKernelGGL(k_ing_count, dim3(maxseg, 2 * nstreams), dim3(DT), 0, hs, in, plans, segs, maxseg);
     hipLaunchKernelGGL(k_ing_seg<false>, dim3(maxseg, 2 * nstreams), dim3(DT), 0, hs, in, plans, segs, maxseg,
                        arena, ld_arena, first_stream);
     hipLaunchKernelGGL(k_ing_fix, dim3((nstreams + 63) / 64), dim3(64), 0, hs, plans, segs, maxseg, outs,

@@ -86,19 +86,45 @@ __device__ inline const uint8_t *align16_down(const uint8_t *p)
     return reinterpret_cast<const uint8_t *>(reinterpret_cast<uintptr_t>(p) & ~(uintptr_t)15);
 }
 
+/* SWAR byte tests in "high bit" form: bit 8k + 7 set iff byte k passes */
+__device__ inline uint32_t zero_hi(uint32_t x)
+{
+    return ~(((x & 0x7f7f7f7fu) + 0x7f7f7f7fu) | x) & 0x80808080u;
+}
+
+__device__ inline uint32_t hi_to_bits4(uint32_t h)          /* bit k: byte k */
+{
+    return (h >> 7 | h >> 14 | h >> 21 | h >> 28) & 0xfu;
+}
+
+/* bits [lo, hi) of 16 */
+__device__ inline uint32_t range16(int64_t lo, int64_t hi)
+{
+    const uint32_t l = (uint32_t)min(max(lo, (int64_t)0), (int64_t)16), h = (uint32_t)min(max(hi, (int64_t)0), (int64_t)16);
+    return h > l ? ((1u << h) - 1u) & ~((1u << l) - 1u) : 0u;
+}
+
 /* bit q: byte q of the chunk (file index i0 + q) is an emulation-prevention
- * byte (nal_parser.c:72: 03 after 00 00, before a byte <= 3) */
+ * byte (nal_parser.c:72: 03 after 00 00, before a byte <= 3).  Per dword:
+ * its own test, the zero tests of the bytes one and two before and the <= 3
+ * test of the byte after, lined up with alignbyte */
 __device__ inline uint32_t ep_removed16(const Chunk16 &c, int64_t i0, int64_t n)
 {
-    uint32_t m = 0;
+    const uint32_t W[6] = {c.prev, c.w[0], c.w[1], c.w[2], c.w[3], c.next};
+    uint32_t Z[5], L3[6];
 #pragma unroll
-    for (int q = 0; q < 16; ++q) {
-        const int64_t i = i0 + q;
-        const bool rm = c.b(q) == 3 && c.b(q - 1) == 0 && c.b(q - 2) == 0 && c.b(q + 1) <= 3 && i >= 2 &&
-                        i + 1 < n;
-        m |= rm ? 1u << q : 0u;
+    for (int k = 0; k < 5; ++k) Z[k] = zero_hi(W[k]);
+#pragma unroll
+    for (int k = 1; k < 6; ++k) L3[k] = zero_hi(W[k] & 0xfcfcfcfcu);
+    uint32_t rm = 0;
+#pragma unroll
+    for (int k = 1; k < 5; ++k) {
+        const uint32_t r = zero_hi(W[k] ^ 0x03030303u) & __builtin_amdgcn_alignbyte(Z[k], Z[k - 1], 3u) &
+                           __builtin_amdgcn_alignbyte(Z[k], Z[k - 1], 2u) &
+                           __builtin_amdgcn_alignbyte(L3[k + 1], L3[k], 1u);
+        rm |= hi_to_bits4(r) << (4 * (k - 1));
     }
-    return m;
+    return rm & range16(2 - i0, n - 1 - i0);
 }
 
 __global__ __launch_bounds__(DT) void k_ing_scan(const uint8_t *__restrict__ in,
@@ -112,13 +138,26 @@ __global__ __launch_bounds__(DT) void k_ing_scan(const uint8_t *__restrict__ in,
     if (align16_down(d) + (size_t)blockIdx.x * WINB >= hi) return;     /* uniform over the block */
     const Chunk16 c = load_chunk16(a, d, hi);
     const int64_t i0 = a - d;
+    const uint32_t W[5] = {c.w[0], c.w[1], c.w[2], c.w[3], c.next};
+    uint32_t Z[5], E1[5];
 #pragma unroll
-    for (int q = 0; q < 16; ++q) {
-        const int64_t i = i0 + q;
-        if (i >= 0 && i + 2 < (int64_t)F.size && c.b(q) == 0 && c.b(q + 1) == 0 && c.b(q + 2) == 1) {
-            const uint32_t k = atomicAdd(&scan[fi].n, 1u);            /* nal_parser.c:16-18 */
-            if (k < (uint32_t)ING_SC_MAX) scan[fi].pos[k] = (uint32_t)i;
-        }
+    for (int k = 0; k < 5; ++k) {
+        Z[k] = zero_hi(W[k]);
+        E1[k] = zero_hi(W[k] ^ 0x01010101u);
+    }
+    uint32_t sc = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t r = Z[k] & __builtin_amdgcn_alignbyte(Z[k + 1], Z[k], 1u) &
+                           __builtin_amdgcn_alignbyte(E1[k + 1], E1[k], 2u);
+        sc |= hi_to_bits4(r) << (4 * k);
+    }
+    sc &= range16(-i0, (int64_t)F.size - 2 - i0);
+    while (sc) {                                                      /* nal_parser.c:16-18 */
+        const int q = __builtin_ctz(sc);
+        sc &= sc - 1;
+        const uint32_t k = atomicAdd(&scan[fi].n, 1u);
+        if (k < (uint32_t)ING_SC_MAX) scan[fi].pos[k] = (uint32_t)(i0 + q);
     }
 }
 
@@ -925,11 +964,8 @@ __global__ __launch_bounds__(DT) void k_ing_seg(const uint8_t *__restrict__ in,
             uint32_t sm = 0;
             if (i0 + 16 > e0 && i0 < e1) {
                 const uint32_t rm = ep_removed16(ch[j], i0, n);
-                const int64_t lo = max(e0 - i0, (int64_t)0), h1 = min(e1 - i0, (int64_t)16),
-                              h2 = min(es - i0, (int64_t)16);
-                const uint64_t lom = (1ull << lo) - 1;
-                km[j] = (uint32_t)(((1ull << h1) - 1) & ~lom) & ~rm;
-                sm = h2 > lo ? (uint32_t)(((1ull << h2) - 1) & ~lom) & ~rm : 0u;
+                km[j] = range16(e0 - i0, e1 - i0) & ~rm;
+                sm = range16(e0 - i0, es - i0) & ~rm;
             }
             cnt[j] = (uint32_t)__popc(km[j]);
             cnt[NJ] += (uint32_t)__popc(sm);
@@ -1030,33 +1066,51 @@ __global__ __launch_bounds__(DT) void k_ing_seg(const uint8_t *__restrict__ in,
      * the zero run since the last non-zero byte is even and >= 2 */
     int lx[NJ], lt[NJ];
     block_excl_max_v<NJ>(my_l, L.wmax, lx, lt);
-    const int64_t SENT = -((int64_t)1 << 40);
-    int64_t before = WRITE ? G.lnz : SENT;                  /* relative; < 0: before the segment */
+    /* positions relative to the segment, int32; a last non-zero byte
+     * further back than 4 bytes only matters through its parity */
+    int32_t before;
+    {
+        const int64_t b = WRITE ? G.lnz : -((int64_t)1 << 40);
+        before = b >= -4 ? (int32_t)b : -4 - (int32_t)(b & 1);
+    }
+    const int32_t nout32 = (int32_t)nout;
     uint32_t nb[NJ + 1], insm[NJ];
     uint32_t naft = 0;
     nb[NJ] = 0;
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
-        const int64_t u0 = (int64_t)OCH * j + 16 * t;
-        int64_t prev = lx[j] >= 0 ? (int64_t)OCH * j + lx[j] : before;
+        const int32_t u0 = OCH * j + 16 * t;
+        int32_t prev = lx[j] >= 0 ? OCH * j + lx[j] : before;
         insm[j] = 0;
-        nb[j] = 0;
+        const uint32_t valid = u0 >= nout32 ? 0u : u0 + 16 <= nout32 ? 0xffffu : (1u << (nout32 - u0)) - 1u;
+        nb[j] = (uint32_t)__popc(valid);
+        /* candidates: bytes <= 3 after two zero bytes (the bytes past nout
+         * may pass too: the exact loop below skips them) */
+        uint32_t cand = 0, zl = (prev < u0 - 1 ? 0x80000000u : 0u) | (prev < u0 - 2 ? 0x00800000u : 0u);
 #pragma unroll
-        for (int q = 0; q < 16; ++q) {
-            const int64_t u = u0 + q;
-            if (u < nout) {
-                const uint32_t x = (ow[j][q >> 2] >> (8 * (q & 3))) & 255u;
-                const int64_t run = u - 1 - prev;
-                if (x <= 3 && run >= 2 && !(run & 1)) {
-                    insm[j] |= 1u << q;
-                    nb[j]++;
-                    naft += prev >= 0 ? 1u : 0u;
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t zk = zero_hi(ow[j][k]);
+            cand |= zero_hi(ow[j][k] & 0xfcfcfcfcu) & __builtin_amdgcn_alignbyte(zk, zl, 3u) &
+                    __builtin_amdgcn_alignbyte(zk, zl, 2u);
+            zl = zk;
+        }
+        if (cand) {
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                const int32_t u = u0 + q;
+                if (u < nout32) {
+                    const uint32_t x = (ow[j][q >> 2] >> (8 * (q & 3))) & 255u;
+                    const int32_t run = u - 1 - prev;
+                    if (x <= 3 && run >= 2 && !(run & 1)) {
+                        insm[j] |= 1u << q;
+                        nb[j]++;
+                        naft += prev >= 0 ? 1u : 0u;
+                    }
+                    if (x) prev = u;
                 }
-                if (x) prev = u;
-                nb[j]++;
             }
         }
-        if (lt[j] >= 0) before = (int64_t)OCH * j + lt[j];
+        if (lt[j] >= 0) before = OCH * j + lt[j];
     }
     if (!WRITE) {
         uint32_t v1[1] = {naft}, e1v[1], t1v[1];
@@ -1068,7 +1122,7 @@ __global__ __launch_bounds__(DT) void k_ing_seg(const uint8_t *__restrict__ in,
             G.kept = kept;
             G.nout = (uint32_t)nout;
             G.f = first;
-            G.last = (int32_t)(before >= 0 ? before : -1);
+            G.last = before >= 0 ? before : -1;
             G.cafter = t1v[0];
             if (first < 0) G.vf = 0;
         }

@@ -104,11 +104,39 @@ __device__ inline uint32_t range16(int64_t lo, int64_t hi)
     return h > l ? ((1u << h) - 1u) & ~((1u << l) - 1u) : 0u;
 }
 
+__device__ inline uint32_t range16_32(int32_t lo, int32_t hi)
+{
+    const uint32_t l = (uint32_t)min(max(lo, 0), 16), h = (uint32_t)min(max(hi, 0), 16);
+    return h > l ? ((1u << h) - 1u) & ~((1u << l) - 1u) : 0u;
+}
+
+/* the 16 bytes w (little-endian) to buf[at, at + 16), any alignment: the
+ * three whole dwords inside as dword writes, the bytes of the two end dwords
+ * (shared with the neighbouring lanes) one by one */
+__device__ inline void lds_put16(uint8_t *buf, uint32_t at, const uint32_t (&w)[4])
+{
+    const uint32_t m = at & 3u;
+    uint32_t *dw = reinterpret_cast<uint32_t *>(buf + (at - m));
+    if (m == 0) {
+        dw[0] = w[0];
+        dw[1] = w[1];
+        dw[2] = w[2];
+        dw[3] = w[3];
+        return;
+    }
+    uint8_t *b = buf + (at - m);
+    for (uint32_t k = m; k < 4; ++k) b[k] = (uint8_t)(w[0] >> (8 * (k - m)));
+    dw[1] = __builtin_amdgcn_alignbyte(w[1], w[0], 4u - m);
+    dw[2] = __builtin_amdgcn_alignbyte(w[2], w[1], 4u - m);
+    dw[3] = __builtin_amdgcn_alignbyte(w[3], w[2], 4u - m);
+    for (uint32_t k = 0; k < m; ++k) b[16 + k] = (uint8_t)(w[3] >> (8 * (4 - m + k)));
+}
+
 /* bit q: byte q of the chunk (file index i0 + q) is an emulation-prevention
  * byte (nal_parser.c:72: 03 after 00 00, before a byte <= 3).  Per dword:
  * its own test, the zero tests of the bytes one and two before and the <= 3
  * test of the byte after, lined up with alignbyte */
-__device__ inline uint32_t ep_removed16(const Chunk16 &c, int64_t i0, int64_t n)
+__device__ inline uint32_t ep_removed16(const Chunk16 &c)
 {
     const uint32_t W[6] = {c.prev, c.w[0], c.w[1], c.w[2], c.w[3], c.next};
     uint32_t Z[5], L3[6];
@@ -124,7 +152,7 @@ __device__ inline uint32_t ep_removed16(const Chunk16 &c, int64_t i0, int64_t n)
                            __builtin_amdgcn_alignbyte(L3[k + 1], L3[k], 1u);
         rm |= hi_to_bits4(r) << (4 * (k - 1));
     }
-    return rm & range16(2 - i0, n - 1 - i0);
+    return rm;                          /* the caller masks file indices [2, n - 1) */
 }
 
 __global__ __launch_bounds__(DT) void k_ing_scan(const uint8_t *__restrict__ in,
@@ -914,9 +942,13 @@ __device__ inline void block_excl_max_v(const int (&v)[NV], int (*ws)[NW], int (
 constexpr int NJ = (int)((SEG + SEG_LA + 15 + 16 * DT - 1) / (16 * DT));   /* 16-byte-per-lane windows */
 constexpr uint32_t RBCAP = SEG + SEG_LA + 16;                            /* RBSP bytes kept in LDS   */
 
+constexpr uint32_t SEG_LDS_BYTES = RBCAP + 48 + OBUF + 16;
 struct SegLds {
-    alignas(16) uint8_t rb[RBCAP + 48];  /* the segment's RBSP bytes (+ look-ahead), zeros after */
-    alignas(16) uint8_t obuf[OBUF + 16]; /* one window of output bytes after EP, at the arena's phase */
+    /* the segment's RBSP bytes (+ look-ahead), zeros after; once the output
+     * bytes are in registers, the output bytes after EP at the arena's
+     * phase (all windows, or one at a time past RBCAP + 48 when they do not
+     * fit) */
+    alignas(16) uint8_t rb[SEG_LDS_BYTES];
     uint32_t wsum[NJ + 1][NW];
     int32_t wmax[NJ][NW];
     int32_t wmin[1][NW];
@@ -957,15 +989,19 @@ __global__ __launch_bounds__(DT) void k_ing_seg(const uint8_t *__restrict__ in,
         Chunk16 ch[NJ];
 #pragma unroll
         for (int j = 0; j < NJ; ++j) ch[j] = load_chunk16(a0 + 16 * (t + DT * j), d, hi);
+        /* indices relative to e0, int32 */
+        const int32_t e1r = (int32_t)(e1 - e0), esr = (int32_t)(es - e0);
+        const int32_t rlo = (int32_t)max((int64_t)2 - e0, (int64_t)-64), rhi = (int32_t)min(n - 1 - e0, (int64_t)(1 << 20));
+        const int32_t ia = (int32_t)(a0 - (d + e0)) + 16 * t;
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
-            const int64_t i0 = a0 + 16 * (t + DT * j) - d;
+            const int32_t i0 = ia + 16 * DT * j;
             km[j] = 0;
             uint32_t sm = 0;
-            if (i0 + 16 > e0 && i0 < e1) {
-                const uint32_t rm = ep_removed16(ch[j], i0, n);
-                km[j] = range16(e0 - i0, e1 - i0) & ~rm;
-                sm = range16(e0 - i0, es - i0) & ~rm;
+            if (i0 + 16 > 0 && i0 < e1r) {
+                const uint32_t rm = ep_removed16(ch[j]) & range16_32(rlo - i0, rhi - i0);
+                km[j] = range16_32(-i0, e1r - i0) & ~rm;
+                sm = range16_32(-i0, esr - i0) & ~rm;
             }
             cnt[j] = (uint32_t)__popc(km[j]);
             cnt[NJ] += (uint32_t)__popc(sm);
@@ -976,12 +1012,16 @@ __global__ __launch_bounds__(DT) void k_ing_seg(const uint8_t *__restrict__ in,
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
             uint32_t at = base + ex[j];
+            if (km[j] == 0xffffu && at + 16 <= RBCAP) {
+                lds_put16(L.rb, at, ch[j].w);
+            } else {
 #pragma unroll
-            for (int q = 0; q < 16; ++q)
-                if ((km[j] >> q) & 1u) {
-                    if (at < RBCAP) L.rb[at] = (uint8_t)ch[j].b(q);
-                    at++;
-                }
+                for (int q = 0; q < 16; ++q)
+                    if ((km[j] >> q) & 1u) {
+                        if (at < RBCAP) L.rb[at] = (uint8_t)ch[j].b(q);
+                        at++;
+                    }
+            }
             base += tot[j];
         }
         have = min(base, RBCAP);
@@ -1153,30 +1193,51 @@ __global__ __launch_bounds__(DT) void k_ing_seg(const uint8_t *__restrict__ in,
         A[a5 + 3] = 1;
         A[a5 + 4] = (uint8_t)(((P.ref_idc & 3) << 5) | (P.type & 31));
     }
+    auto put_lines = [&](const uint8_t *buf, uint32_t ph, uint32_t end, uint8_t *line0) {
+        for (uint32_t l = (uint32_t)t; l < (end + 15) >> 4; l += DT) {
+            const uint32_t b0 = 16 * l;
+            if (b0 >= ph && b0 + 16 <= end) {
+                *reinterpret_cast<uint4 *>(line0 + b0) = *reinterpret_cast<const uint4 *>(buf + b0);
+            } else {
+                for (uint32_t q = max(b0, ph); q < min(b0 + 16, end); ++q) line0[q] = buf[q];
+            }
+        }
+    };
+    auto stage = [&](uint8_t *buf, int j, uint32_t kq) {
+        if (insm[j] == 0 && (int64_t)OCH * j + 16 * t + 16 <= nout) {
+            lds_put16(buf, kq, ow[j]);
+            return;
+        }
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            if ((int64_t)OCH * j + 16 * t + q >= nout) break;
+            if ((insm[j] >> q) & 1u) buf[kq++] = 3;
+            buf[kq++] = (uint8_t)(ow[j][q >> 2] >> (8 * (q & 3)));
+        }
+    };
+    uint32_t total = 0;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) total += tot[j];
+    const uint32_t ph0 = (uint32_t)(reinterpret_cast<uintptr_t>(A + at) & 15u);
+    if (ph0 + total + 16 <= SEG_LDS_BYTES) {                /* all windows at once */
+        uint32_t base = ph0;
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            stage(L.rb, j, base + ex[j]);
+            base += tot[j];
+        }
+        __syncthreads();
+        put_lines(L.rb, ph0, ph0 + total, A + at - ph0);
+        return;
+    }
+    uint8_t *obuf = L.rb + RBCAP + 48;
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
         if ((int64_t)OCH * j >= nout) break;                /* uniform */
         const uint32_t ph = (uint32_t)(reinterpret_cast<uintptr_t>(A + at) & 15u);
-        {
-            uint32_t kq = ph + ex[j];
-#pragma unroll
-            for (int q = 0; q < 16; ++q) {
-                if ((int64_t)OCH * j + 16 * t + q >= nout) break;
-                if ((insm[j] >> q) & 1u) L.obuf[kq++] = 3;
-                L.obuf[kq++] = (uint8_t)(ow[j][q >> 2] >> (8 * (q & 3)));
-            }
-        }
+        stage(obuf, j, ph + ex[j]);
         __syncthreads();
-        uint8_t *line0 = A + at - ph;
-        const uint32_t end = ph + tot[j], nl = (end + 15) >> 4;
-        for (uint32_t l = (uint32_t)t; l < nl; l += DT) {
-            const uint32_t b0 = 16 * l;
-            if (b0 >= ph && b0 + 16 <= end) {
-                *reinterpret_cast<uint4 *>(line0 + b0) = *reinterpret_cast<const uint4 *>(L.obuf + b0);
-            } else {
-                for (uint32_t q = max(b0, ph); q < min(b0 + 16, end); ++q) line0[q] = L.obuf[q];
-            }
-        }
+        put_lines(obuf, ph, ph + tot[j], A + at - ph);
         at += tot[j];
         __syncthreads();
     }
@@ -1193,51 +1254,85 @@ __device__ inline int64_t evens_ge2(int64_t a, int64_t b)
 /* per stream, serial over the segments of A then B: RBSP prefix, output
  * offsets, the insertions before each segment's first non-zero byte (closed
  * form in the last non-zero byte before it), arena offsets, the bound */
+constexpr int FIX_MAXSEG = 1024;             /* segments per slice staged in LDS (16 MB slices; larger files take k_ing_stream) */
+
+struct FixSeg {
+    uint32_t kept, nout, cafter;
+    int32_t f, vf, last;
+};
+
 __global__ __launch_bounds__(64) void k_ing_fix(IngPlan *__restrict__ plans, IngSeg *__restrict__ segs,
-                                                uint32_t maxseg, IngestOut *__restrict__ outs, int nstreams,
-                                                uint64_t cap)
+                                                uint32_t maxseg, IngestOut *__restrict__ outs, uint64_t cap)
 {
-    const int k = blockIdx.x * 64 + threadIdx.x;
-    if (k >= nstreams) return;
+    __shared__ FixSeg S[FIX_MAXSEG];
+    __shared__ uint64_t Sat[FIX_MAXSEG];
+    __shared__ int64_t Slnz[FIX_MAXSEG];
+    __shared__ uint64_t sh_at;
+    __shared__ int sh_bad;
+    const int k = blockIdx.x, t = threadIdx.x;
     IngPlan &PA = plans[2 * k], &PB = plans[2 * k + 1];
     if (!PA.ok) return;
-    uint64_t at = PA.at;
-    bool over = false, bad = false;
+    if (t == 0) {
+        sh_at = PA.at;
+        sh_bad = 0;
+    }
+    __syncthreads();
     for (int f = 0; f < 2; ++f) {
         IngPlan &P = f ? PB : PA;
         IngSeg *SG = segs + (size_t)(2 * k + f) * maxseg;
-        const int64_t D = (int64_t)P.hlen - (int64_t)P.mb_start, cd = (D + 7) >> 3;
-        P.at = at;
-        uint64_t pos = at + 5, R0 = 0;
-        int64_t lnz = -1;                                   /* output index in the slice */
-        for (uint32_t c = 0; c < P.nseg; ++c) {
-            IngSeg &G = SG[c];
-            const int64_t o0 = c == 0 ? 0 : (int64_t)R0 + cd;
-            if (c > 0 && o0 < (int64_t)P.npre) bad = true;   /* a header longer than a segment's body */
-            G.at = pos;
-            G.lnz = lnz - o0;
-            const int64_t of = G.f >= 0 ? o0 + G.f : o0 + (int64_t)G.nout;   /* first non-zero (or the end) */
-            /* zero bytes o0 .. of - 1: run o - 1 - lnz */
-            int64_t ins = G.nout ? evens_ge2(o0 - 1 - lnz, of - 2 - lnz) : 0;
-            if (G.f >= 0) {
-                const int64_t run = of - 1 - lnz;
-                if (G.vf <= 3 && run >= 2 && !(run & 1)) ins++;
-                ins += G.cafter;
-                lnz = o0 + G.last;
-            }
-            pos += G.nout + (uint64_t)ins;
-            R0 += G.kept;
+        const uint32_t ns = P.nseg;
+        if (ns > (uint32_t)FIX_MAXSEG) {                    /* host keeps maxseg below; uniform */
+            if (t == 0) sh_bad = 2;
+            break;
         }
-        P.R = R0;
-        if (pos > cap) over = true;
-        at = pos;
+        for (uint32_t c = (uint32_t)t; c < ns; c += 64) {
+            const IngSeg &G = SG[c];
+            S[c] = FixSeg{G.kept, G.nout, G.cafter, G.f, G.vf, G.last};
+        }
+        __syncthreads();
+        if (t == 0) {
+            const int64_t D = (int64_t)P.hlen - (int64_t)P.mb_start, cd = (D + 7) >> 3;
+            const uint64_t at = sh_at;
+            P.at = at;
+            uint64_t pos = at + 5, R0 = 0;
+            int64_t lnz = -1;                               /* output index in the slice */
+            for (uint32_t c = 0; c < ns; ++c) {
+                const FixSeg G = S[c];
+                const int64_t o0 = c == 0 ? 0 : (int64_t)R0 + cd;
+                if (c > 0 && o0 < (int64_t)P.npre) sh_bad = 1;   /* a header longer than a segment's body */
+                Sat[c] = pos;
+                Slnz[c] = lnz - o0;
+                const int64_t of = G.f >= 0 ? o0 + G.f : o0 + (int64_t)G.nout;   /* first non-zero (or the end) */
+                /* zero bytes o0 .. of - 1: run o - 1 - lnz */
+                int64_t ins = G.nout ? evens_ge2(o0 - 1 - lnz, of - 2 - lnz) : 0;
+                if (G.f >= 0) {
+                    const int64_t run = of - 1 - lnz;
+                    if (G.vf <= 3 && run >= 2 && !(run & 1)) ins++;
+                    ins += G.cafter;
+                    lnz = o0 + G.last;
+                }
+                pos += G.nout + (uint64_t)ins;
+                R0 += G.kept;
+            }
+            P.R = R0;
+            sh_at = pos;
+        }
+        __syncthreads();
+        for (uint32_t c = (uint32_t)t; c < ns; c += 64) {
+            SG[c].at = Sat[c];
+            SG[c].lnz = Slnz[c];
+        }
+        __syncthreads();
     }
-    if (over || bad) {
-        PA.ok = PB.ok = 0;
-        outs[k].err = bad ? ING_ERR_PARSE : ING_ERR_OVERFLOW;
-        outs[k].bytes = 0;
-    } else {
-        outs[k].bytes = at;
+    if (t == 0) {
+        const bool over = sh_at > cap, bad = sh_bad != 0;
+        if (over || bad) {
+            PA.ok = PB.ok = 0;
+            outs[k].err = bad ? ING_ERR_PARSE : ING_ERR_OVERFLOW;
+            outs[k].bytes = 0;
+        } else {
+            outs[k].bytes = sh_at;
+        }
     }
 }
 
@@ -1384,20 +1479,19 @@ int ingest_launch(hipStream_t hs, const uint8_t *in, const IngestFile *files, in
         hipLaunchKernelGGL(k_ing_scan, dim3(gx, 2 * nstreams), dim3(DT), 0, hs, in, files, scan);
         if (hipGetLastError() != hipSuccess) return -1;
     }
-    if (!work) {                        /* one workgroup per stream (SCROLL_INGEST_SERIAL) */
+    const uint32_t maxseg = (uint32_t)((max_file + SEG - 1) / SEG) + 1u;
+    if (!work || maxseg > (uint32_t)FIX_MAXSEG) {   /* one workgroup per stream (SCROLL_INGEST_SERIAL, > 16 MB files) */
         hipLaunchKernelGGL(k_ing_stream, dim3(nstreams), dim3(DT), 0, hs, in, files, scan, outs, arena,
                            ld_arena, cap, first_stream);
         return hipGetLastError() == hipSuccess ? 0 : -1;
     }
-    const uint32_t maxseg = (uint32_t)((max_file + SEG - 1) / SEG) + 1u;
     IngPlan *plans = reinterpret_cast<IngPlan *>(work);
     IngSeg *segs = reinterpret_cast<IngSeg *>(plans + 2 * (size_t)nstreams);
     hipLaunchKernelGGL(k_ing_head, dim3(nstreams), dim3(DT), 0, hs, in, files, scan, outs, plans, maxseg, arena,
                        ld_arena, cap, first_stream);
     hipLaunchKernelGGL(k_ing_seg<false>, dim3(maxseg, 2 * nstreams), dim3(DT), 0, hs, in, plans, segs, maxseg,
                        arena, ld_arena, first_stream);
-    hipLaunchKernelGGL(k_ing_fix, dim3((nstreams + 63) / 64), dim3(64), 0, hs, plans, segs, maxseg, outs,
-                       nstreams, cap);
+    hipLaunchKernelGGL(k_ing_fix, dim3(nstreams), dim3(64), 0, hs, plans, segs, maxseg, outs, cap);
     hipLaunchKernelGGL(k_ing_seg<true>, dim3(maxseg, 2 * nstreams), dim3(DT), 0, hs, in, plans, segs, maxseg,
                        arena, ld_arena, first_stream);
     return hipGetLastError() == hipSuccess ? 0 : -1;

@@ -40,9 +40,11 @@ typedef struct {
  * header bytes at the start of its arena.  0, or -1 when a launch failed. */
 int ingest_launch(hipStream_t hs, const uint8_t *in, const IngestFile *files, int nstreams,
                   uint64_t max_file, IngestScan *scan, IngestOut *outs, uint8_t *arena,
-                  uint64_t ld_arena, uint64_t cap, int first_stream, void *work);
-/* device scratch of the segmented path (work; nullptr: one workgroup per stream) */
-size_t ingest_work_bytes(int nstreams, uint64_t max_file);
+                  uint64_t ld_arena, uint64_t cap, int first_stream, void *work, size_t work_bytes);
+/* device scratch of the segmented path (work; nullptr: one workgroup per
+ * stream); staged: room for the summary pass's output bytes, which the write
+ * pass then reads instead of decoding the segment again */
+size_t ingest_work_bytes(int nstreams, uint64_t max_file, bool staged);
 
 /* mid-stream long-term reference updates (k_ing_update): files[k] -> a
  * non-IDR I frame of stream ups[2 k] marked long-term ups[2 k + 1],

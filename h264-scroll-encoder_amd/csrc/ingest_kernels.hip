@@ -963,13 +963,16 @@ struct SegLds {
  * puts it.  Emulation prevention needs the last non-zero byte before each
  * byte: inside the segment a max-scan, from the segments before k_ing_fix's
  * lnz.  All windows of a phase share one workgroup scan. */
-template <bool WRITE>
+enum { SEG_SUMMARY = 0, SEG_WRITE = 1, SEG_WRITE_STAGED = 2 };
+
+template <int MODE>
 __global__ __launch_bounds__(DT) void k_ing_seg(const uint8_t *__restrict__ in,
                                                 const IngPlan *__restrict__ plans,
                                                 IngSeg *__restrict__ segs, uint32_t maxseg,
                                                 uint8_t *__restrict__ arena, uint64_t ld_arena,
-                                                int first_stream)
+                                                int first_stream, uint8_t *__restrict__ stg)
 {
+    constexpr bool WRITE = MODE != SEG_SUMMARY;
     __shared__ SegLds L;
     const uint32_t c = blockIdx.x, p = blockIdx.y;
     const int t = threadIdx.x;
@@ -982,7 +985,13 @@ __global__ __launch_bounds__(DT) void k_ing_seg(const uint8_t *__restrict__ in,
     /* 1. RBSP bytes of [e0, e1) -> LDS; kept: those of [e0, es) */
     const int64_t e0 = (int64_t)c * SEG, es = min(n, e0 + (int64_t)SEG), e1 = min(n, e0 + (int64_t)(SEG + SEG_LA));
     const uint8_t *a0 = align16_down(d + e0), *hi = d + min(n, e1 + 1);
-    uint32_t have, kept;
+    /* the segment's output bytes (16 per lane and window, little-endian) */
+    uint32_t ow[NJ][4];
+    int64_t nout;
+    uint32_t kept = 0;
+    uint4 *sp = stg ? reinterpret_cast<uint4 *>(stg + ((size_t)p * maxseg + c) * (size_t)(NJ * OCH)) : nullptr;
+    if (MODE != SEG_WRITE_STAGED) {
+    uint32_t have;
     {
         uint32_t km[NJ], cnt[NJ + 1];
         cnt[NJ] = 0;
@@ -1033,7 +1042,7 @@ __global__ __launch_bounds__(DT) void k_ing_seg(const uint8_t *__restrict__ in,
     const int64_t hlen = P.hlen, npre = P.npre, mbs = (int64_t)P.mb_start, D = hlen - mbs;
     const int64_t cd = (D + 7) >> 3;                        /* ceil(D / 8) */
     const uint32_t s = (uint32_t)((-D) & 7);
-    int64_t nout, off = 0, ufast = 0, umask = INT64_MAX, total_bits = 0;
+    int64_t off = 0, ufast = 0, umask = INT64_MAX, total_bits = 0;
     if (c == 0) {
         off = -cd;                                          /* RBSP byte of output u: u - cd */
         ufast = npre;
@@ -1047,13 +1056,10 @@ __global__ __launch_bounds__(DT) void k_ing_seg(const uint8_t *__restrict__ in,
     } else {
         nout = kept;
     }
-    uint32_t ow[NJ][4];
-    int my_l[NJ], my_f = INT32_MAX;
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
         const int64_t u0 = (int64_t)OCH * j + 16 * t;
         ow[j][0] = ow[j][1] = ow[j][2] = ow[j][3] = 0;
-        my_l[j] = -1;
         if (u0 >= nout) continue;
         if (u0 >= ufast && u0 + 16 <= umask) {
             /* RBSP bytes li0 .. li0 + 16 from five LDS dwords, then the bit
@@ -1087,7 +1093,25 @@ __global__ __launch_bounds__(DT) void k_ing_seg(const uint8_t *__restrict__ in,
                 ow[j][q >> 2] |= x << (8 * (q & 3));
             }
         }
-        if (u0 + 16 > nout) {                               /* bytes past the segment's end */
+    }
+    } else {                                                /* the summary pass left them in stg */
+        nout = G.nout;
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            const uint4 v = (int64_t)OCH * j + 16 * t < nout ? sp[(OCH / 16) * j + t] : make_uint4(0u, 0u, 0u, 0u);
+            ow[j][0] = v.x;
+            ow[j][1] = v.y;
+            ow[j][2] = v.z;
+            ow[j][3] = v.w;
+        }
+    }
+    int my_l[NJ], my_f = INT32_MAX;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+        const int64_t u0 = (int64_t)OCH * j + 16 * t;
+        my_l[j] = -1;
+        if (u0 >= nout) continue;
+        if (MODE != SEG_WRITE_STAGED && u0 + 16 > nout) {  /* bytes past the segment's end */
             const int64_t keep = nout - u0;
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
@@ -1095,6 +1119,7 @@ __global__ __launch_bounds__(DT) void k_ing_seg(const uint8_t *__restrict__ in,
                 ow[j][k] &= kb >= 4 ? 0xffffffffu : kb <= 0 ? 0u : (1u << (8 * kb)) - 1;
             }
         }
+        if (MODE == SEG_SUMMARY && sp) sp[(OCH / 16) * j + t] = make_uint4(ow[j][0], ow[j][1], ow[j][2], ow[j][3]);
 #pragma unroll
         for (int k = 0; k < 4; ++k)
             if (ow[j][k]) {
@@ -1469,7 +1494,7 @@ int update_launch(hipStream_t hs, const uint8_t *in, const IngestFile *files, in
 
 int ingest_launch(hipStream_t hs, const uint8_t *in, const IngestFile *files, int nstreams,
                   uint64_t max_file, IngestScan *scan, IngestOut *outs, uint8_t *arena,
-                  uint64_t ld_arena, uint64_t cap, int first_stream, void *work)
+                  uint64_t ld_arena, uint64_t cap, int first_stream, void *work, size_t work_bytes)
 {
     if (nstreams <= 0) return 0;
     if (hipMemsetAsync(scan, 0, sizeof(IngestScan) * 2 * (size_t)nstreams, hs) != hipSuccess)
@@ -1489,16 +1514,25 @@ int ingest_launch(hipStream_t hs, const uint8_t *in, const IngestFile *files, in
     IngSeg *segs = reinterpret_cast<IngSeg *>(plans + 2 * (size_t)nstreams);
     hipLaunchKernelGGL(k_ing_head, dim3(nstreams), dim3(DT), 0, hs, in, files, scan, outs, plans, maxseg, arena,
                        ld_arena, cap, first_stream);
-    hipLaunchKernelGGL(k_ing_seg<false>, dim3(maxseg, 2 * nstreams), dim3(DT), 0, hs, in, plans, segs, maxseg,
-                       arena, ld_arena, first_stream);
+    uint8_t *stg = nullptr;                 /* the summary pass's output bytes, when the scratch holds them */
+    const size_t base = 2 * (size_t)nstreams * (sizeof(IngPlan) + maxseg * sizeof(IngSeg));
+    if (work_bytes >= base + 2 * (size_t)nstreams * maxseg * (size_t)(NJ * OCH) + 16)
+        stg = reinterpret_cast<uint8_t *>(((uintptr_t)work + base + 15) & ~(uintptr_t)15);
+    hipLaunchKernelGGL(k_ing_seg<SEG_SUMMARY>, dim3(maxseg, 2 * nstreams), dim3(DT), 0, hs, in, plans, segs,
+                       maxseg, arena, ld_arena, first_stream, stg);
     hipLaunchKernelGGL(k_ing_fix, dim3(nstreams), dim3(64), 0, hs, plans, segs, maxseg, outs, cap);
-    hipLaunchKernelGGL(k_ing_seg<true>, dim3(maxseg, 2 * nstreams), dim3(DT), 0, hs, in, plans, segs, maxseg,
-                       arena, ld_arena, first_stream);
+    if (stg)
+        hipLaunchKernelGGL(k_ing_seg<SEG_WRITE_STAGED>, dim3(maxseg, 2 * nstreams), dim3(DT), 0, hs, in, plans,
+                           segs, maxseg, arena, ld_arena, first_stream, stg);
+    else
+        hipLaunchKernelGGL(k_ing_seg<SEG_WRITE>, dim3(maxseg, 2 * nstreams), dim3(DT), 0, hs, in, plans, segs,
+                           maxseg, arena, ld_arena, first_stream, stg);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-size_t ingest_work_bytes(int nstreams, uint64_t max_file)
+size_t ingest_work_bytes(int nstreams, uint64_t max_file, bool staged)
 {
     const size_t maxseg = (size_t)((max_file + SEG - 1) / SEG) + 1u;
-    return 2 * (size_t)nstreams * (sizeof(IngPlan) + maxseg * sizeof(IngSeg));
+    const size_t base = 2 * (size_t)nstreams * (sizeof(IngPlan) + maxseg * sizeof(IngSeg));
+    return staged ? base + 2 * (size_t)nstreams * maxseg * (size_t)(NJ * OCH) + 16 : base;
 }

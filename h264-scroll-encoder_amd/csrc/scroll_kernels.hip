@@ -2636,7 +2636,11 @@ int scroll_batch_ingest_device(ScrollBatch *b, int n, const uint8_t *d_files, co
         maxf = std::max(maxf, files[k].size);
     }
     const bool serial = getenv("SCROLL_INGEST_SERIAL") != nullptr;
-    const size_t wb = serial ? 0 : ingest_work_bytes(n, maxf);
+    /* the staged write pass while its scratch stays under 8 GB (the input's
+     * size, rounded up per segment), else the recomputing one */
+    const bool staged = getenv("SCROLL_INGEST_RECOMPUTE") == nullptr &&
+                        ingest_work_bytes(n, maxf, true) <= ((size_t)8 << 30);
+    const size_t wb = serial ? 0 : ingest_work_bytes(n, maxf, staged);
     if (wb > b->ing_work_bytes) {
         (void)hipFree(b->d_ing_work);
         b->d_ing_work = nullptr;
@@ -2658,7 +2662,7 @@ int scroll_batch_ingest_device(ScrollBatch *b, int n, const uint8_t *d_files, co
     }
     if (ingest_launch(hs, d_files, b->d_ing_files, n, maxf, b->d_ing_scan, b->d_ing_out,
                       b->d_arena, (uint64_t)b->ld_arena, (uint64_t)b->arena_bytes, b->nstreams,
-                      serial ? nullptr : b->d_ing_work)) {
+                      serial ? nullptr : b->d_ing_work, wb)) {
         set_err("ingest launch: %s", hipGetErrorString(hipGetLastError()));
         return SCROLL_ERR_HIP;
     }

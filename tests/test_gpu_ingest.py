@@ -214,16 +214,18 @@ def test_ingest_errors_add_no_stream(gpu, oracle, scroll):
 
 def test_ingest_segmented_matches_one_workgroup_path(gpu, oracle, monkeypatch):
     """the segmented path (default: slices cut into 16 KB EBSP segments over
-    many workgroups) and the one-workgroup-per-stream path
-    (SCROLL_INGEST_SERIAL) write the same bytes; EP-heavy 1280x720 files put
-    zero runs of both parities across segment boundaries"""
+    many workgroups, the write pass reading the summary pass's bytes), its
+    recomputing write pass (SCROLL_INGEST_RECOMPUTE) and the
+    one-workgroup-per-stream path (SCROLL_INGEST_SERIAL) write the same bytes;
+    EP-heavy 1280x720 files put zero runs of both parities across segment
+    boundaries"""
     w, h = 1280, 720
     pairs = [variant_files(oracle, w, h, k) for k in (1, 2, 3, 6, 7)]
     outs = []
-    for serial in (False, True):
-        if serial:
-            monkeypatch.setenv("SCROLL_INGEST_SERIAL", "1")
+    for env in (None, "SCROLL_INGEST_RECOMPUTE", "SCROLL_INGEST_SERIAL"):
+        if env:
+            monkeypatch.setenv(env, "1")
         b = check_ingest(gpu, oracle, pairs, nframes=0, arena=8 << 20)
         outs.append([b.output(s) for s in range(len(pairs))])
         b.close()
-    assert outs[0] == outs[1]
+    assert outs[0] == outs[1] == outs[2]

@@ -138,6 +138,9 @@ __device__ inline void lds_put16(uint8_t *buf, uint32_t at, const uint32_t (&w)[
  * test of the byte after, lined up with alignbyte */
 __device__ inline uint32_t ep_removed16(const Chunk16 &c)
 {
+    const uint32_t E3[4] = {zero_hi(c.w[0] ^ 0x03030303u), zero_hi(c.w[1] ^ 0x03030303u),
+                            zero_hi(c.w[2] ^ 0x03030303u), zero_hi(c.w[3] ^ 0x03030303u)};
+    if ((E3[0] | E3[1] | E3[2] | E3[3]) == 0) return 0;   /* no 03 byte: the common case */
     const uint32_t W[6] = {c.prev, c.w[0], c.w[1], c.w[2], c.w[3], c.next};
     uint32_t Z[5], L3[6];
 #pragma unroll
@@ -147,7 +150,7 @@ __device__ inline uint32_t ep_removed16(const Chunk16 &c)
     uint32_t rm = 0;
 #pragma unroll
     for (int k = 1; k < 5; ++k) {
-        const uint32_t r = zero_hi(W[k] ^ 0x03030303u) & __builtin_amdgcn_alignbyte(Z[k], Z[k - 1], 3u) &
+        const uint32_t r = E3[k - 1] & __builtin_amdgcn_alignbyte(Z[k], Z[k - 1], 3u) &
                            __builtin_amdgcn_alignbyte(Z[k], Z[k - 1], 2u) &
                            __builtin_amdgcn_alignbyte(L3[k + 1], L3[k], 1u);
         rm |= hi_to_bits4(r) << (4 * (k - 1));

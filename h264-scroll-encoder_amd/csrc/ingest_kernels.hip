@@ -86,12 +86,6 @@ __device__ inline const uint8_t *align16_down(const uint8_t *p)
     return reinterpret_cast<const uint8_t *>(reinterpret_cast<uintptr_t>(p) & ~(uintptr_t)15);
 }
 
-/* SWAR byte tests in "high bit" form: bit 8k + 7 set iff byte k passes */
-__device__ inline uint32_t zero_hi(uint32_t x)
-{
-    return ~(((x & 0x7f7f7f7fu) + 0x7f7f7f7fu) | x) & 0x80808080u;
-}
-
 __device__ inline uint32_t hi_to_bits4(uint32_t h)          /* bit k: byte k */
 {
     return (h >> 7 | h >> 14 | h >> 21 | h >> 28) & 0xfu;
@@ -108,28 +102,6 @@ __device__ inline uint32_t range16_32(int32_t lo, int32_t hi)
 {
     const uint32_t l = (uint32_t)min(max(lo, 0), 16), h = (uint32_t)min(max(hi, 0), 16);
     return h > l ? ((1u << h) - 1u) & ~((1u << l) - 1u) : 0u;
-}
-
-/* the 16 bytes w (little-endian) to buf[at, at + 16), any alignment: the
- * three whole dwords inside as dword writes, the bytes of the two end dwords
- * (shared with the neighbouring lanes) one by one */
-__device__ inline void lds_put16(uint8_t *buf, uint32_t at, const uint32_t (&w)[4])
-{
-    const uint32_t m = at & 3u;
-    uint32_t *dw = reinterpret_cast<uint32_t *>(buf + (at - m));
-    if (m == 0) {
-        dw[0] = w[0];
-        dw[1] = w[1];
-        dw[2] = w[2];
-        dw[3] = w[3];
-        return;
-    }
-    uint8_t *b = buf + (at - m);
-    for (uint32_t k = m; k < 4; ++k) b[k] = (uint8_t)(w[0] >> (8 * (k - m)));
-    dw[1] = __builtin_amdgcn_alignbyte(w[1], w[0], 4u - m);
-    dw[2] = __builtin_amdgcn_alignbyte(w[2], w[1], 4u - m);
-    dw[3] = __builtin_amdgcn_alignbyte(w[3], w[2], 4u - m);
-    for (uint32_t k = 0; k < m; ++k) b[16 + k] = (uint8_t)(w[3] >> (8 * (4 - m + k)));
 }
 
 /* bit q: byte q of the chunk (file index i0 + q) is an emulation-prevention

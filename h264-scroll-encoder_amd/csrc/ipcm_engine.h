@@ -33,7 +33,9 @@ typedef struct {
     uint8_t pre[IPCM_PRE_MAX];
 } IpcmGeom;
 
-/* pass 0: emulation-prevention bytes per chunk -> counts[n][nchunk];
- * pass 1: files -> out (prefix, EBSP).  0, or -1 when a launch failed. */
+/* pass 0: emulation-prevention bytes per chunk -> counts[n][nchunk] (and,
+ * with stg, each file's RBSP -> stg + n * stg_stride, stg_stride >=
+ * nchunk * IPCM_CHUNK, a multiple of 16); pass 1: files -> out (prefix,
+ * EBSP), from stg when given.  0, or -1 when a launch failed. */
 int ipcm_launch(hipStream_t hs, int pass, int n, const IpcmGeom *g, const uint8_t *pics,
-                uint32_t *counts, uint8_t *out);
+                uint32_t *counts, uint8_t *out, uint8_t *stg, uint64_t stg_stride);

@@ -72,10 +72,14 @@ __device__ inline uint32_t rbsp_at(const IpcmGeom &G, const uint8_t *pic, uint32
     return pic[a];
 }
 
-template <bool WRITE>
+enum { IP_COUNT = 0, IP_WRITE = 1, IP_WRITE_STAGED = 2 };
+
+template <int MODE>
 __global__ __launch_bounds__(IT) void k_ipcm(IpcmGeom G, const uint8_t *__restrict__ pics,
-                                             uint32_t *__restrict__ counts, uint8_t *__restrict__ out)
+                                             uint32_t *__restrict__ counts, uint8_t *__restrict__ out,
+                                             uint8_t *__restrict__ stg, uint64_t stg_stride)
 {
+    constexpr bool WRITE = MODE != IP_COUNT;
     __shared__ alignas(16) uint8_t rb[LB + CH];
     __shared__ alignas(16) uint8_t ob[16 + CH + CH / 2 + 16];
     __shared__ int32_t wsm[IT / 64];
@@ -85,36 +89,38 @@ __global__ __launch_bounds__(IT) void k_ipcm(IpcmGeom G, const uint8_t *__restri
     const uint32_t c = blockIdx.x, n = blockIdx.y;
     const uint8_t *pic = pics + (size_t)n * G.pic_stride;
     const uint32_t c0 = c * CH, c1 = min(c0 + CH, G.rbsp_len);
-
-    /* RBSP bytes [c0 - LB, c1) -> LDS.  The samples go by source row
-     * segment (an MB record's 16 luma rows of 16 bytes, 8 + 8 chroma rows of
-     * 8): one 16- or 8-byte load per segment, its bytes into LDS at their
-     * RBSP offsets; every other byte -- before the RBSP (a non-zero sentinel:
-     * the automaton starts with no zeros seen), the slice header, the
-     * records' 0x0D 0x00, the stop byte -- by the thread of its index.  Each
-     * byte has exactly one writer. */
-    {
+    uint8_t *S = stg ? stg + (size_t)n * stg_stride : nullptr;       /* the file's RBSP (count pass) */
+    const uint32_t g0 = c0 + 16u * (uint32_t)t;
+    const uint32_t nb = g0 < c1 ? min(16u, c1 - g0) : 0u;
+    uint32_t qw[4];
+    if (MODE != IP_WRITE_STAGED) {
+        /* RBSP bytes [c0 - LB, c1) -> LDS.  The samples go by source row
+         * segment (an MB record's 16 luma rows of 16 bytes, 8 + 8 chroma
+         * rows of 8): one 16- or 8-byte load per segment, its bytes into LDS
+         * at their RBSP offsets; a 33rd segment per record is its 0x0D 0x00.
+         * The bytes of the first and the last chunk's ends -- before the RBSP
+         * (a non-zero sentinel: the automaton starts with no zeros seen), the
+         * slice header, the stop byte, past the end -- by the thread of their
+         * index.  Each byte has one value. */
         const int64_t lo = (int64_t)c0 - LB;
         const uint32_t base = G.nh - 2u;
-        for (uint32_t k = (uint32_t)t; k < (uint32_t)LB + CH; k += IT) {
-            const int64_t i = lo + (int64_t)k;
-            int v = -1;                                       /* -1: a sample byte */
-            if (i < 0) {
-                v = 0xff;
-            } else if (i >= (int64_t)c1) {
-                v = 0;
-            } else if ((uint32_t)i < G.nh) {
-                v = G.hdr[i];
-            } else if ((uint32_t)i + 1u == G.rbsp_len) {
-                v = 0x80;                                     /* rbsp_stop_one_bit + alignment */
-            } else {
-                const uint32_t j = (uint32_t)i - base;
-                const uint32_t r = j - 386u * (uint32_t)(((uint64_t)j * M386) >> 41);
-                if (r < 2u) v = r == 0u ? 0x0D : 0x00;        /* ue(25) + pcm_alignment_zero_bits */
+        if (c == 0 || c + 1 == G.nchunk) {
+            for (uint32_t k = (uint32_t)t; k < (uint32_t)LB + CH; k += IT) {
+                const int64_t i = lo + (int64_t)k;
+                int v = -1;                                   /* -1: a record byte */
+                if (i < 0) {
+                    v = 0xff;
+                } else if (i >= (int64_t)c1) {
+                    v = 0;
+                } else if ((uint32_t)i < G.nh) {
+                    v = G.hdr[i];
+                } else if ((uint32_t)i + 1u == G.rbsp_len) {
+                    v = 0x80;                                 /* rbsp_stop_one_bit + alignment */
+                }
+                if (v >= 0) rb[k] = (uint8_t)v;
             }
-            if (v >= 0) rb[k] = (uint8_t)v;
         }
-        /* the records that overlap [max(lo, nh), c1): 32 segments each */
+        /* the records that overlap [max(lo, nh), c1): 33 segments each */
         const int64_t s0 = lo > (int64_t)G.nh ? lo : (int64_t)G.nh;
         if (s0 < (int64_t)c1) {
             const uint32_t m0 = (uint32_t)((((uint64_t)s0 - base) * M386) >> 41);
@@ -122,65 +128,116 @@ __global__ __launch_bounds__(IT) void k_ipcm(IpcmGeom G, const uint8_t *__restri
             const uint32_t w = (uint32_t)G.w, cw = w / 2u;
             const size_t ysz = (size_t)w * (uint32_t)G.h;
             const bool vec = (reinterpret_cast<uintptr_t>(pic) & 15u) == 0u;
-            const uint32_t nseg = 32u * (m1 - m0 + 1u);
+            const uint32_t nseg = 33u * (m1 - m0 + 1u);
             for (uint32_t q = (uint32_t)t; q < nseg; q += IT) {
-                const uint32_t m = m0 + (q >> 5), sg = q & 31u;
-                uint32_t my = __umulhi(m, G.m_mbw);
-                if (G.mbw == 1) my = m;
-                const uint32_t mx = m - my * G.mbw;
+                const uint32_t mq = __umulhi(q, 130150525u);  /* q / 33 (q < 2^26) */
+                const uint32_t m = m0 + mq, sg = q - 33u * mq;
                 uint32_t off, len;
-                size_t a;
-                if (sg < 16u) {
-                    off = 2u + 16u * sg;
-                    len = 16u;
-                    a = (size_t)(16u * my + sg) * w + 16u * mx;
+                uint32_t x[4] = {0, 0, 0, 0};
+                if (sg == 32u) {                              /* ue(25) + pcm_alignment_zero_bits */
+                    if (m == 0u) continue;                    /* MB 0's: in hdr */
+                    off = 0u;
+                    len = 2u;
+                    x[0] = 0x0Du;
                 } else {
-                    const uint32_t cr = sg & 7u;
-                    off = (sg < 24u ? 258u : 322u) + 8u * cr;
-                    len = 8u;
-                    a = ysz + (sg < 24u ? 0u : ysz / 4) + (size_t)(8u * my + cr) * cw + 8u * mx;
+                    uint32_t my = __umulhi(m, G.m_mbw);
+                    if (G.mbw == 1) my = m;
+                    const uint32_t mx = m - my * G.mbw;
+                    size_t a;
+                    if (sg < 16u) {
+                        off = 2u + 16u * sg;
+                        len = 16u;
+                        a = (size_t)(16u * my + sg) * w + 16u * mx;
+                    } else {
+                        const uint32_t cr = sg & 7u;
+                        off = (sg < 24u ? 258u : 322u) + 8u * cr;
+                        len = 8u;
+                        a = ysz + (sg < 24u ? 0u : ysz / 4) + (size_t)(8u * my + cr) * cw + 8u * mx;
+                    }
+                    const int64_t r0 = (int64_t)base + 386 * (int64_t)m + off;
+                    if (r0 + len <= lo || r0 >= (int64_t)c1) continue;
+                    if (vec) {
+                        if (len == 16u) {
+                            const uint4 u = *reinterpret_cast<const uint4 *>(pic + a);
+                            x[0] = u.x, x[1] = u.y, x[2] = u.z, x[3] = u.w;
+                        } else {
+                            const uint2 u = *reinterpret_cast<const uint2 *>(pic + a);
+                            x[0] = u.x, x[1] = u.y;
+                        }
+                    } else {
+                        for (uint32_t b = 0; b < len; ++b) x[b >> 2] |= (uint32_t)pic[a + b] << (8u * (b & 3u));
+                    }
                 }
                 const int64_t r0 = (int64_t)base + 386 * (int64_t)m + off;      /* its RBSP index */
                 if (r0 + len <= lo || r0 >= (int64_t)c1) continue;
-                uint32_t x[4] = {0, 0, 0, 0};
-                if (vec) {
-                    if (len == 16u) {
-                        const uint4 u = *reinterpret_cast<const uint4 *>(pic + a);
-                        x[0] = u.x, x[1] = u.y, x[2] = u.z, x[3] = u.w;
-                    } else {
-                        const uint2 u = *reinterpret_cast<const uint2 *>(pic + a);
-                        x[0] = u.x, x[1] = u.y;
-                    }
+                if (r0 >= lo && r0 + 16 <= (int64_t)c1 && len == 16u) {
+                    lds_put16(rb, (uint32_t)(r0 - lo), x);
                 } else {
-                    for (uint32_t b = 0; b < len; ++b) x[b >> 2] |= (uint32_t)pic[a + b] << (8u * (b & 3u));
-                }
 #pragma unroll
-                for (uint32_t b = 0; b < 16u; ++b) {
-                    const int64_t i = r0 + b;
-                    if (b < len && i >= lo && i < (int64_t)c1)
-                        rb[(uint32_t)(i - lo)] = (uint8_t)(x[b >> 2] >> (8u * (b & 3u)));
+                    for (uint32_t b = 0; b < 16u; ++b) {
+                        const int64_t i = r0 + b;
+                        if (b < len && i >= lo && i < (int64_t)c1)
+                            rb[(uint32_t)(i - lo)] = (uint8_t)(x[b >> 2] >> (8u * (b & 3u)));
+                    }
                 }
             }
         }
+        __syncthreads();
+        const uint4 q4 = *reinterpret_cast<const uint4 *>(&rb[LB + 16 * t]);
+        qw[0] = q4.x, qw[1] = q4.y, qw[2] = q4.z, qw[3] = q4.w;
+        if (MODE == IP_COUNT && S && nb) *reinterpret_cast<uint4 *>(S + g0) = q4;
+    } else {
+        /* the count pass's RBSP bytes; the look-back bytes the same way */
+        uint4 q4 = nb ? *reinterpret_cast<const uint4 *>(S + g0) : make_uint4(0u, 0u, 0u, 0u);
+        qw[0] = q4.x, qw[1] = q4.y, qw[2] = q4.z, qw[3] = q4.w;
+        if (t < LB / 16)
+            *reinterpret_cast<uint4 *>(&rb[16 * t]) =
+                c0 > 0 ? *reinterpret_cast<const uint4 *>(S + c0 - LB + 16 * t) : make_uint4(~0u, ~0u, ~0u, ~0u);
     }
+    if (nb < 16) {                                        /* bytes past the RBSP */
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int kb = (int)nb - 4 * k;
+            qw[k] &= kb >= 4 ? 0xffffffffu : kb <= 0 ? 0u : (1u << (8 * kb)) - 1;
+        }
+    }
+    /* look-back: the last non-zero byte before c0 (-1: the RBSP start), from
+     * the LB staged bytes by the first LB / 16 lanes */
     if (t == 0) deep = -2;
     __syncthreads();
-    /* look-back: last non-zero byte before c0 (-1: the RBSP start) */
+    if (t < LB / 16 && c0 > 0) {
+        const uint4 v = *reinterpret_cast<const uint4 *>(&rb[16 * t]);
+        const uint32_t vw[4] = {v.x, v.y, v.z, v.w};
+        int l = -2;
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (vw[k]) l = (int)c0 - LB + 16 * t + 4 * k + 3 - (__builtin_clz(vw[k]) >> 3);
+        atomicMax(&deep, l);
+    }
+    int mylast = -1;
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        if (qw[k]) mylast = (int)g0 + 4 * k + 3 - (__builtin_clz(qw[k]) >> 3);
+    int pm, tmax;
+    block_excl_max(mylast, wsm, pm, tmax);                /* its barriers publish deep */
     int carry = -1;
     if (c0 > 0) {
-        int lnz = -2;
-#pragma unroll
-        for (int k = 0; k < LB; ++k)
-            if (rb[k]) lnz = (int)c0 - LB + k;
-        if (lnz == -2) {                             /* LB zero bytes: rare (black pictures) */
+        carry = deep;
+        if (carry == -2) {                                /* LB zero bytes: rare (black pictures) */
+            __syncthreads();
             if (t == 0) {
-                int64_t i = (int64_t)c0 - LB - 1;
-                const uint32_t base = G.nh - 2u;
                 int f = -1;
-                for (; i >= 0; --i) {
+                for (int64_t i = (int64_t)c0 - LB - 1; i >= 0; --i) {
                     const uint32_t ii = (uint32_t)i;
-                    const Cur cu = cur_at(G, ii >= G.nh ? ii - base : 2u);
-                    if (rbsp_at(G, pic, ii, cu)) {
+                    uint32_t v;
+                    if (MODE == IP_WRITE_STAGED) {
+                        v = S[ii];
+                    } else {
+                        const uint32_t base = G.nh - 2u;
+                        const Cur cu = cur_at(G, ii >= G.nh ? ii - base : 2u);
+                        v = rbsp_at(G, pic, ii, cu);
+                    }
+                    if (v) {
                         f = (int)ii;
                         break;
                     }
@@ -188,33 +245,35 @@ __global__ __launch_bounds__(IT) void k_ipcm(IpcmGeom G, const uint8_t *__restri
                 deep = f;
             }
             __syncthreads();
-            lnz = deep;
+            carry = deep;
         }
-        carry = lnz;
     }
-    /* this thread's 16 bytes: last non-zero before them (block max-scan) */
-    const uint32_t g0 = c0 + 16u * (uint32_t)t;
-    const uint4 q4 = *reinterpret_cast<const uint4 *>(&rb[LB + 16 * t]);
-    const uint32_t qw[4] = {q4.x, q4.y, q4.z, q4.w};
-    const uint32_t nb = g0 < c1 ? min(16u, c1 - g0) : 0u;
-    int mylast = -1;
-#pragma unroll
-    for (int k = 0; k < 16; ++k)
-        if ((uint32_t)k < nb && ((qw[k >> 2] >> (8 * (k & 3))) & 255u)) mylast = (int)(g0 + k);
-    int pm, tmax;
-    block_excl_max(mylast, wsm, pm, tmax);
+    /* emulation prevention (nal.c:33-38): the exact loop only for lanes with
+     * a byte <= 3 after two zero bytes */
     int prev = max(pm, carry);
     uint32_t epm = 0, cnt = 0;
+    {
+        uint32_t cand = 0, zl = (prev < (int)g0 - 1 ? 0x80000000u : 0u) | (prev < (int)g0 - 2 ? 0x00800000u : 0u);
 #pragma unroll
-    for (int k = 0; k < 16; ++k) {
-        if ((uint32_t)k >= nb) break;
-        const uint32_t b = (qw[k >> 2] >> (8 * (k & 3))) & 255u;
-        const int i = (int)(g0 + k);
-        if (scroll::dyn::ep_insert(b, i - 1 - prev)) {
-            epm |= 1u << k;
-            cnt++;
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t zk = zero_hi(qw[k]);
+            cand |= zero_hi(qw[k] & 0xfcfcfcfcu) & __builtin_amdgcn_alignbyte(zk, zl, 3u) &
+                    __builtin_amdgcn_alignbyte(zk, zl, 2u);
+            zl = zk;
         }
-        if (b) prev = i;
+        if (cand) {
+#pragma unroll
+            for (int k = 0; k < 16; ++k) {
+                if ((uint32_t)k >= nb) break;
+                const uint32_t b = (qw[k >> 2] >> (8 * (k & 3))) & 255u;
+                const int i = (int)(g0 + k);
+                if (scroll::dyn::ep_insert(b, i - 1 - prev)) {
+                    epm |= 1u << k;
+                    cnt++;
+                }
+                if (b) prev = i;
+            }
+        }
     }
     uint32_t ex, tot;
     block_excl_sum(cnt, wss, ex, tot);
@@ -229,16 +288,20 @@ __global__ __launch_bounds__(IT) void k_ipcm(IpcmGeom G, const uint8_t *__restri
     block_excl_sum(pre, wss, pex, ptot);
     uint8_t *F = out + (size_t)n * G.out_stride;
     const uint64_t O = (uint64_t)G.npre + c0 + ptot;            /* file offset of RBSP byte c0 */
-    const uint32_t sh = (uint32_t)(O & 15u);
+    const uint32_t sh = (uint32_t)(reinterpret_cast<uintptr_t>(F + O) & 15u);
     if (c == 0)
         for (uint32_t k = (uint32_t)t; k < G.npre; k += IT) F[k] = G.pre[k];
     {
         uint32_t x = sh + 16u * (uint32_t)t + ex;
+        if (epm == 0 && nb == 16u) {
+            lds_put16(ob, x, qw);
+        } else {
 #pragma unroll
-        for (int k = 0; k < 16; ++k) {
-            if ((uint32_t)k >= nb) break;
-            if ((epm >> k) & 1u) ob[x++] = 0x03;
-            ob[x++] = (uint8_t)((qw[k >> 2] >> (8 * (k & 3))) & 255u);
+            for (int k = 0; k < 16; ++k) {
+                if ((uint32_t)k >= nb) break;
+                if ((epm >> k) & 1u) ob[x++] = 0x03;
+                ob[x++] = (uint8_t)((qw[k >> 2] >> (8 * (k & 3))) & 255u);
+            }
         }
     }
     __syncthreads();
@@ -257,12 +320,17 @@ __global__ __launch_bounds__(IT) void k_ipcm(IpcmGeom G, const uint8_t *__restri
 }  // namespace
 
 int ipcm_launch(hipStream_t hs, int pass, int n, const IpcmGeom *g, const uint8_t *pics,
-                uint32_t *counts, uint8_t *out)
+                uint32_t *counts, uint8_t *out, uint8_t *stg, uint64_t stg_stride)
 {
     if (n <= 0) return 0;
     if (pass == 0)
-        hipLaunchKernelGGL(k_ipcm<false>, dim3(g->nchunk, n), dim3(IT), 0, hs, *g, pics, counts, out);
+        hipLaunchKernelGGL(k_ipcm<IP_COUNT>, dim3(g->nchunk, n), dim3(IT), 0, hs, *g, pics, counts, out, stg,
+                           stg_stride);
+    else if (stg)
+        hipLaunchKernelGGL(k_ipcm<IP_WRITE_STAGED>, dim3(g->nchunk, n), dim3(IT), 0, hs, *g, pics, counts, out,
+                           stg, stg_stride);
     else
-        hipLaunchKernelGGL(k_ipcm<true>, dim3(g->nchunk, n), dim3(IT), 0, hs, *g, pics, counts, out);
+        hipLaunchKernelGGL(k_ipcm<IP_WRITE>, dim3(g->nchunk, n), dim3(IT), 0, hs, *g, pics, counts, out, stg,
+                           stg_stride);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

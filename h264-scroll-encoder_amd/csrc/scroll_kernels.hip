@@ -971,6 +971,8 @@ struct ScrollBatch {
     /* reference files from pictures: EP count per chunk */
     uint32_t *d_ipcm_cnt = nullptr;
     size_t ipcm_cap = 0;
+    uint8_t *d_ipcm_stg = nullptr;              /* count pass RBSP for the write pass */
+    size_t ipcm_stg_cap = 0;
     double ipcm_ms = 0.0;
     int ipcm_n = 0;
     double ing_ms = 0.0;
@@ -1114,6 +1116,7 @@ void scroll_batch_destroy(ScrollBatch *b)
     (void)hipFree(b->d_sp_list);
     (void)hipFree(b->d_ing_in);
     (void)hipFree(b->d_ipcm_cnt);
+    (void)hipFree(b->d_ipcm_stg);
     (void)hipFree(b->d_ing_files);
     (void)hipFree(b->d_ing_scan);
     (void)hipFree(b->d_ing_out);
@@ -2796,13 +2799,28 @@ int scroll_batch_ipcm_files_device(ScrollBatch *b, int n, int w, int h, const ui
         }
         b->ipcm_cap = need;
     }
+    /* the write pass reads the count pass's RBSP while that scratch stays
+     * under 4 GB, else it generates the bytes again */
+    const uint64_t stg_stride = (uint64_t)g.nchunk * IPCM_CHUNK;
+    const size_t stg_need = (size_t)n * stg_stride;
+    uint8_t *stg = nullptr;
+    if (getenv("SCROLL_IPCM_RECOMPUTE") == nullptr && stg_need <= ((size_t)4 << 30)) {
+        if (stg_need > b->ipcm_stg_cap) {
+            (void)hipFree(b->d_ipcm_stg);
+            b->d_ipcm_stg = nullptr;
+            b->ipcm_stg_cap = 0;
+            if (hipMalloc(&b->d_ipcm_stg, stg_need) == hipSuccess) b->ipcm_stg_cap = stg_need;
+            else (void)hipGetLastError();               /* no scratch: the generating write pass */
+        }
+        if (b->d_ipcm_stg) stg = b->d_ipcm_stg;
+    }
     hipStream_t hs = b->own;
     if (b->timing) {
         for (hipEvent_t &e : b->ing_ev)                  /* created lazily, shared with ingest */
             if (!e) HIPCHK(timing_event(&e));
         HIPCHK(hipEventRecord(b->ing_ev[0], hs));
     }
-    if (ipcm_launch(hs, 0, n, &g, d_pics, b->d_ipcm_cnt, d_out)) {
+    if (ipcm_launch(hs, 0, n, &g, d_pics, b->d_ipcm_cnt, d_out, stg, stg_stride)) {
         set_err("ipcm launch: %s", hipGetErrorString(hipGetLastError()));
         return SCROLL_ERR_HIP;
     }
@@ -2828,7 +2846,7 @@ int scroll_batch_ipcm_files_device(ScrollBatch *b, int n, int w, int h, const ui
         return SCROLL_ERR_OVERFLOW;
     }
     if (b->timing) HIPCHK(hipEventRecord(b->ing_ev[0], hs));
-    if (ipcm_launch(hs, 1, n, &g, d_pics, b->d_ipcm_cnt, d_out)) {
+    if (ipcm_launch(hs, 1, n, &g, d_pics, b->d_ipcm_cnt, d_out, stg, stg_stride)) {
         set_err("ipcm launch: %s", hipGetErrorString(hipGetLastError()));
         return SCROLL_ERR_HIP;
     }

@@ -140,6 +140,19 @@ def test_pictures_match_oracle(gpu, hip, oracle, w, h):
         assert (t == 0xAB).all(), "bytes written past the file"
 
 
+@pytest.mark.parametrize("w,h", [(48, 32), (640, 480)])
+def test_generating_write_pass_matches(gpu, hip, oracle, monkeypatch, w, h):
+    """SCROLL_IPCM_RECOMPUTE: the write pass generates the RBSP again instead
+    of reading the count pass's bytes; same files"""
+    kinds = ["rand", "zero", "low", "sparse", "a"]
+    pics = pictures(w, h, kinds, seed=3 * w + h)
+    monkeypatch.setenv("SCROLL_IPCM_RECOMPUTE", "1")
+    files, tails = gpu_files(gpu, hip, w, h, pics)
+    for k, (p, f, t) in enumerate(zip(pics, files, tails)):
+        assert f == ipcm_file(oracle, w, h, p), f"{kinds[k]} {w}x{h}"
+        assert (t == 0xAB).all(), "bytes written past the file"
+
+
 def test_4k_pictures(gpu, hip, oracle, golden_md5):
     w, h = 3840, 2160
     pics = pictures(w, h, ["a", "zero"])

@@ -225,7 +225,7 @@ def run_ingest(args, wl, rank, world, local, dist):
             "config": {"workload": wl["desc"], "resolution": f"{W}x{H}", "streams_per_step": S,
                        "parallelism": f"static stream shard x{world}, no RCCL"},
             "bytes_per_stream": {"in": len(fa) + len(fb), "out": out_bytes},
-            "roofline": {"bound": "hbm", "kernel": "ingest launch: k_ing_scan, k_ing_head, k_ing_seg<false>, k_ing_fix, k_ing_seg<true>",
+            "roofline": {"bound": "hbm", "kernel": "ingest launch: k_ing_scan, k_ing_head, k_ing_seg<SUMMARY>, k_ing_fix, k_ing_seg<WRITE_STAGED>",
                          "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
                          "alg_bytes_per_launch": alg, "kernel_ms_avg": round(k_ms, 4)},

@@ -740,7 +740,7 @@ __global__ __launch_bounds__(DT) void k_ing_stream(const uint8_t *__restrict__ i
  *   k_ing_head        per stream: the parse and the SPS / PPS NAL units of
  *                     k_ing_stream, and a plan per slice (input range,
  *                     header bits, first output bytes)
- *   k_ing_seg<false>  per segment: its RBSP bytes (closed-form removal) and
+ *   k_ing_seg<SUMMARY> per segment: its RBSP bytes (closed-form removal) and
  *                     its output bytes -- those RBSP bytes shifted behind the
  *                     new header -- summarised for emulation prevention:
  *                     first / last non-zero byte and the insertions after the
@@ -749,7 +749,8 @@ __global__ __launch_bounds__(DT) void k_ing_stream(const uint8_t *__restrict__ i
  *                     insertions before its first non-zero byte (closed form
  *                     in the last non-zero byte before it), hence its arena
  *                     offset; the byte counts and the arena bound
- *   k_ing_seg<true>   per segment: the bytes again, with their 03s, to the
+ *   k_ing_seg<WRITE_STAGED> per segment: the summary pass's bytes from
+ *                     scratch (k_ing_seg<WRITE>: decoded again), with their 03s, to the
  *                     arena.
  * Bytes: identical to k_ing_stream's (tests/test_gpu_ingest.py checks both
  * against the oracle). */
@@ -767,7 +768,7 @@ struct IngPlan {                         /* one slice of a new stream           
 };
 
 struct IngSeg {
-    uint32_t kept;                       /* RBSP bytes (k_ing_seg<false>)           */
+    uint32_t kept;                       /* RBSP bytes (the summary pass)           */
     uint32_t nout;                       /* output bytes it owns                    */
     int32_t f, vf, last;                 /* first non-zero output byte (relative to its first,
                                           * -1: none), its value, the last non-zero one */
@@ -933,8 +934,8 @@ struct SegLds {
  * payload.  Its output bytes do not depend on the segments before: output
  * byte u (relative) is RBSP byte u and the next one (the look-ahead byte at
  * the end) shifted by the slice's constant s -- for segment 0 after the
- * npre header bytes -- so k_ing_seg<false> summarises a segment without
- * knowing where it lands, and k_ing_seg<true> writes it where k_ing_fix
+ * npre header bytes -- so the summary pass summarises a segment without
+ * knowing where it lands, and a write pass writes it where k_ing_fix
  * puts it.  Emulation prevention needs the last non-zero byte before each
  * byte: inside the segment a max-scan, from the segments before k_ing_fix's
  * lnz.  All windows of a phase share one workgroup scan. */

@@ -20,7 +20,12 @@
  *                 of ebsp_to_rbsp) -> scan -> RBSP ring in LDS -> output
  *                 bytes = constant bit shift behind the new header -> EP
  *                 insertion (closed form of rbsp_to_ebsp from the last
- *                 non-zero byte, max-scan) -> arena.
+ *                 non-zero byte, max-scan) -> arena.  Kept for slices over
+ *                 16 MB and SCROLL_INGEST_SERIAL.
+ *   segmented     (the default, below k_ing_stream) the same parse in
+ *                 k_ing_head, each slice body cut into 16 KB segments
+ *                 over many workgroups: k_ing_seg<SUMMARY>, k_ing_fix,
+ *                 k_ing_seg<WRITE_STAGED>.
  * Bits: byte-identical to the reference's composer_write_header output
  * (tests/test_gpu_ingest.py against oracle/scroll_oracle.c, pinned by the
  * reference's golden header files).  Roofline: HBM (files in, header NALs

@@ -225,9 +225,9 @@ def run_ingest(args, wl, rank, world, local, dist):
             "config": {"workload": wl["desc"], "resolution": f"{W}x{H}", "streams_per_step": S,
                        "parallelism": f"static stream shard x{world}, no RCCL"},
             "bytes_per_stream": {"in": len(fa) + len(fb), "out": out_bytes},
-            "roofline": {"bound": "hbm", "kernel": "ingest launch: k_ing_scan, k_ing_head, k_ing_seg<SUMMARY>, k_ing_fix, k_ing_seg<WRITE_STAGED>",
+            "roofline": {"bound": "hbm", "kernel": ING_KERNEL,
                          "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic_of(args.workload, ING_KERNEL, alg),
                          "alg_bytes_per_launch": alg, "kernel_ms_avg": round(k_ms, 4)},
         }
         if world == 1 and not args.no_cpu:
@@ -304,9 +304,9 @@ def run_ipcm(args, wl, rank, world, local, dist):
             "config": {"workload": wl["desc"], "resolution": f"{W}x{H}", "files_per_step": S,
                        "parallelism": f"static shard x{world}, no RCCL"},
             "bytes_per_file": {"in": pic, "out": round(sum(sizes) / S, 1)},
-            "roofline": {"bound": "hbm", "kernel": "k_ipcm (count + write passes)",
+            "roofline": {"bound": "hbm", "kernel": IPCM_KERNEL,
                          "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic_of(args.workload, IPCM_KERNEL, alg),
                          "alg_bytes_per_launch": alg, "kernel_ms_avg": round(k_ms, 4)},
         }
         if world == 1 and not args.no_cpu:
@@ -632,6 +632,17 @@ def verify_splice_step(b, e, ptrs, wl, first, passes, nstreams=8):
     d.update(sample=f"first {ns} of {S} streams", passes=passes,
              seconds=round(time.perf_counter() - t0, 2), checker="oracle/splice_oracle.c")
     return ok, d
+
+
+ING_KERNEL = "ingest call: k_ing_scan, k_ing_head, k_ing_seg<SUMMARY>, k_ing_fix, k_ing_seg<WRITE_STAGED>"
+IPCM_KERNEL = "k_ipcm (count + write passes)"
+
+
+def traffic_of(workload, kernel, alg_bytes):
+    """HBM bytes per call from profiles/traffic_<workload>.json when it was
+    measured on this very configuration (load_traffic), else None"""
+    t = load_traffic(workload, kernel, alg_bytes)
+    return t.get("hbm_bytes_per_launch") if t else None
 
 
 def load_traffic(workload, kernel, alg_bytes):

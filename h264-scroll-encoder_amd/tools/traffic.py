@@ -1,7 +1,10 @@
 #!/usr/bin/env python3
 """HBM traffic of k_emit per launch from two rocprofv3 --pmc passes.
 
-    traffic.py FETCH_DIR WRITE_DIR OUT.json [--alg-bytes N]
+    traffic.py FETCH_DIR WRITE_DIR OUT.json [--alg-bytes N] [--kernel K1,K2,..] [--label L]
+
+With several kernels (a call made of several launches, e.g. ingest) the
+figure is the sum of their per-dispatch means, and --label names the whole.
 
 FETCH_DIR / WRITE_DIR hold run_counter_collection.csv of a `--pmc FETCH_SIZE`
 and a `--pmc WRITE_SIZE` pass over the same command (separate passes: the two
@@ -33,16 +36,21 @@ def main():
     ap.add_argument("out")
     ap.add_argument("--kernel", default="k_emit")
     ap.add_argument("--alg-bytes", type=float, default=0.0)
+    ap.add_argument("--label", default="")
     ap.add_argument("--fetch-scale", type=float, default=2.0,
                     help="gfx950 FETCH_SIZE correction (2 = wide coalesced reads, the guide's "
                          "calibrated case; other access widths are uncalibrated)")
     a = ap.parse_args()
-    fk = per_dispatch(a.fetch_dir, "FETCH_SIZE", a.kernel)
-    wk = per_dispatch(a.write_dir, "WRITE_SIZE", a.kernel)
-    raw = 1024 * sum(fk) / len(fk)                  # KB -> bytes
+    raw = write = 0.0
+    nd = []
+    for k in a.kernel.split(","):
+        fk = per_dispatch(a.fetch_dir, "FETCH_SIZE", k)
+        wk = per_dispatch(a.write_dir, "WRITE_SIZE", k)
+        raw += 1024 * sum(fk) / len(fk)             # KB -> bytes
+        write += 1024 * sum(wk) / len(wk)
+        nd.append([k, len(fk), len(wk)])
     fetch = a.fetch_scale * raw
-    write = 1024 * sum(wk) / len(wk)
-    out = {"kernel": a.kernel, "dispatches": [len(fk), len(wk)],
+    out = {"kernel": a.label or a.kernel, "dispatches": nd if len(nd) > 1 else nd[0][1:],
            "fetch_size_raw_bytes_per_launch": round(raw),
            "fetch_bytes_per_launch": round(fetch), "write_bytes_per_launch": round(write),
            "hbm_bytes_per_launch": round(fetch + write),

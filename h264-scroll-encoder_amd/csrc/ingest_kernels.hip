@@ -49,6 +49,7 @@ constexpr int WINB = DT * 16;           /* EBSP bytes per window: 16 per lane   
 constexpr int RING = 4 * WINB;          /* RBSP ring (power of two)                */
 constexpr int OCH = WINB;               /* output bytes per emit chunk: 16 per lane */
 constexpr int OBUF = OCH + OCH / 2 + 64; /* one chunk after EP (<= 1.5x)           */
+constexpr int SCAN_W = 4;               /* k_ing_scan: windows per workgroup        */
 
 /* ---------------------------------------------------------------------- */
 /* k_ing_scan                                                              */
@@ -142,30 +143,35 @@ __global__ __launch_bounds__(DT) void k_ing_scan(const uint8_t *__restrict__ in,
     const int fi = blockIdx.y;
     const IngestFile F = files[fi];
     const uint8_t *d = in + F.off, *hi = d + F.size;
-    const uint8_t *a = align16_down(d) + (size_t)blockIdx.x * WINB + 16u * threadIdx.x;
-    if (align16_down(d) + (size_t)blockIdx.x * WINB >= hi) return;     /* uniform over the block */
-    const Chunk16 c = load_chunk16(a, d, hi);
-    const int64_t i0 = a - d;
-    const uint32_t W[5] = {c.w[0], c.w[1], c.w[2], c.w[3], c.next};
-    uint32_t Z[5], E1[5];
+    const uint8_t *w0 = align16_down(d) + (size_t)blockIdx.x * (SCAN_W * WINB);
+    if (w0 >= hi) return;                                             /* uniform over the block */
+    Chunk16 c[SCAN_W];                                                /* all loads in flight first */
 #pragma unroll
-    for (int k = 0; k < 5; ++k) {
-        Z[k] = zero_hi(W[k]);
-        E1[k] = zero_hi(W[k] ^ 0x01010101u);
-    }
-    uint32_t sc = 0;
+    for (int j = 0; j < SCAN_W; ++j) c[j] = load_chunk16(w0 + j * WINB + 16u * threadIdx.x, d, hi);
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const uint32_t r = Z[k] & __builtin_amdgcn_alignbyte(Z[k + 1], Z[k], 1u) &
-                           __builtin_amdgcn_alignbyte(E1[k + 1], E1[k], 2u);
-        sc |= hi_to_bits4(r) << (4 * k);
-    }
-    sc &= range16(-i0, (int64_t)F.size - 2 - i0);
-    while (sc) {                                                      /* nal_parser.c:16-18 */
-        const int q = __builtin_ctz(sc);
-        sc &= sc - 1;
-        const uint32_t k = atomicAdd(&scan[fi].n, 1u);
-        if (k < (uint32_t)ING_SC_MAX) scan[fi].pos[k] = (uint32_t)(i0 + q);
+    for (int j = 0; j < SCAN_W; ++j) {
+        const int64_t i0 = w0 + j * WINB + 16u * threadIdx.x - d;
+        const uint32_t W[5] = {c[j].w[0], c[j].w[1], c[j].w[2], c[j].w[3], c[j].next};
+        uint32_t Z[5], E1[5];
+#pragma unroll
+        for (int k = 0; k < 5; ++k) {
+            Z[k] = zero_hi(W[k]);
+            E1[k] = zero_hi(W[k] ^ 0x01010101u);
+        }
+        uint32_t sc = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t r = Z[k] & __builtin_amdgcn_alignbyte(Z[k + 1], Z[k], 1u) &
+                               __builtin_amdgcn_alignbyte(E1[k + 1], E1[k], 2u);
+            sc |= hi_to_bits4(r) << (4 * k);
+        }
+        sc &= range16(-i0, (int64_t)F.size - 2 - i0);
+        while (sc) {                                                  /* nal_parser.c:16-18 */
+            const int q = __builtin_ctz(sc);
+            sc &= sc - 1;
+            const uint32_t k = atomicAdd(&scan[fi].n, 1u);
+            if (k < (uint32_t)ING_SC_MAX) scan[fi].pos[k] = (uint32_t)(i0 + q);
+        }
     }
 }
 
@@ -1464,7 +1470,7 @@ int update_launch(hipStream_t hs, const uint8_t *in, const IngestFile *files, in
 {
     if (n <= 0) return 0;
     if (hipMemsetAsync(scan, 0, sizeof(IngestScan) * (size_t)n, hs) != hipSuccess) return -1;
-    const uint32_t gx = (uint32_t)((max_file + 15 + WINB - 1) / WINB);
+    const uint32_t gx = (uint32_t)((max_file + 15 + SCAN_W * WINB - 1) / (SCAN_W * WINB));
     if (gx > 0) {
         hipLaunchKernelGGL(k_ing_scan, dim3(gx, n), dim3(DT), 0, hs, in, files, scan);
         if (hipGetLastError() != hipSuccess) return -1;
@@ -1480,7 +1486,7 @@ int ingest_launch(hipStream_t hs, const uint8_t *in, const IngestFile *files, in
     if (nstreams <= 0) return 0;
     if (hipMemsetAsync(scan, 0, sizeof(IngestScan) * 2 * (size_t)nstreams, hs) != hipSuccess)
         return -1;
-    const uint32_t gx = (uint32_t)((max_file + 15 + WINB - 1) / WINB);
+    const uint32_t gx = (uint32_t)((max_file + 15 + SCAN_W * WINB - 1) / (SCAN_W * WINB));
     if (gx > 0) {
         hipLaunchKernelGGL(k_ing_scan, dim3(gx, 2 * nstreams), dim3(DT), 0, hs, in, files, scan);
         if (hipGetLastError() != hipSuccess) return -1;

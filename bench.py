@@ -147,6 +147,50 @@ def ipcm_ref_file(w, h, which):
     return nal(0x67, _bits_to_bytes(sps)) + nal(0x68, _bits_to_bytes(pps)) + nal(0x65, bytes(body))
 
 
+def oracle_lib():
+    """CHECKER / CPU baseline only: oracle/_build/liboracle.so (built on demand)"""
+    repo_oracle = os.path.join(HERE, "oracle")
+    so = os.path.join(repo_oracle, "_build", "liboracle.so")
+    if not os.path.exists(so):
+        import subprocess
+        subprocess.run(["make", "-s", "-C", repo_oracle], check=True)
+    lib = ctypes.CDLL(so)
+    lib.or_composer_run.restype = ctypes.c_size_t
+    lib.or_ipcm_picture_file.restype = ctypes.c_size_t
+    return lib
+
+
+def verify_ingest_step(b, files, first, S):
+    """CHECKER (after timing): the first and the last stream ingested by the
+    last timed step against or_composer_run (oracle/scroll_oracle.c)"""
+    lib = oracle_lib()
+    a, bb = files
+    cap = 2 * (len(a) + len(bb)) + 4096
+    buf = (ctypes.c_uint8 * cap)()
+    n = lib.or_composer_run(buf, cap, a, len(a), bb, len(bb), 0, 1)
+    want = bytes(buf[:n])
+    bad = [k for k in (first, first + S - 1) if b.output(k) != want]
+    return (not bad), {"streams_checked": 2, "mismatch": bad}
+
+
+def verify_ipcm_step(pics, out, sizes, ostride, W, H):
+    """CHECKER (after timing): the first and the last file of the last timed
+    step against or_ipcm_picture_file (oracle/scroll_oracle.c)"""
+    import numpy as np
+    lib = oracle_lib()
+    cap = 2 * W * H + (1 << 16)
+    buf = (ctypes.c_uint8 * cap)()
+    S = len(sizes)
+    bad = []
+    for k in (0, S - 1):
+        p = np.ascontiguousarray(pics[k].cpu().numpy())
+        n = lib.or_ipcm_picture_file(buf, cap, W, H, p.ctypes.data_as(ctypes.c_void_p))
+        got = out[k * ostride:k * ostride + sizes[k]].cpu().numpy().tobytes()
+        if got != bytes(buf[:n]):
+            bad.append(k)
+    return (not bad), {"files_checked": 2, "mismatch": bad}
+
+
 def cpu_baseline_ingest(files, nstreams=8):
     """composer_init + composer_write_header restated (oracle/scroll_oracle.c
     or_composer_run, no frames) on one host core"""
@@ -211,6 +255,7 @@ def run_ingest(args, wl, rank, world, local, dist):
     out_bytes = b.output_size(S * nsteps - 1)
     b.enable_timing(False)
     el = max_over_ranks(t1 - t0, dist)
+    verified, vdetail = (None, None) if args.no_verify else verify_ingest_step(b, (fa, fb), S * (nsteps - 1), S)
     if rank == 0:
         k_ms = kms / max(kn, 1)
         alg = S * (len(fa) + len(fb) + out_bytes)          # files in, header NALs out
@@ -225,6 +270,7 @@ def run_ingest(args, wl, rank, world, local, dist):
             "config": {"workload": wl["desc"], "resolution": f"{W}x{H}", "streams_per_step": S,
                        "parallelism": f"static stream shard x{world}, no RCCL"},
             "bytes_per_stream": {"in": len(fa) + len(fb), "out": out_bytes},
+            "verified": verified, "verify": vdetail,
             "roofline": {"bound": "hbm", "kernel": ING_KERNEL,
                          "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic_of(args.workload, ING_KERNEL, alg),
@@ -234,6 +280,8 @@ def run_ingest(args, wl, rank, world, local, dist):
             out["cpu_baseline"] = cpu_baseline_ingest((fa, fb))
         print(json.dumps(out), flush=True)
     b.close()
+    if verified is False:
+        sys.exit(3)
 
 
 def cpu_baseline_ipcm(pics, w, h):
@@ -290,6 +338,7 @@ def run_ipcm(args, wl, rank, world, local, dist):
     kms, kn = b.ipcm_stats()
     b.enable_timing(False)
     el = max_over_ranks(t1 - t0, dist)
+    verified, vdetail = (None, None) if args.no_verify else verify_ipcm_step(pics, out, sizes, ostride, W, H)
     if rank == 0:
         k_ms = kms / max(kn, 1)
         alg = S * pic + sum(sizes)                       # pictures in, files out
@@ -304,6 +353,7 @@ def run_ipcm(args, wl, rank, world, local, dist):
             "config": {"workload": wl["desc"], "resolution": f"{W}x{H}", "files_per_step": S,
                        "parallelism": f"static shard x{world}, no RCCL"},
             "bytes_per_file": {"in": pic, "out": round(sum(sizes) / S, 1)},
+            "verified": verified, "verify": vdetail,
             "roofline": {"bound": "hbm", "kernel": IPCM_KERNEL,
                          "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic_of(args.workload, IPCM_KERNEL, alg),
@@ -314,6 +364,8 @@ def run_ipcm(args, wl, rank, world, local, dist):
             res["cpu_baseline"] = cpu_baseline_ipcm([np.ascontiguousarray(p) for p in host], W, H)
         print(json.dumps(res), flush=True)
     b.close()
+    if verified is False:
+        sys.exit(3)
 
 
 def ui_hints(s, f, w, h):

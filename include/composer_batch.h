@@ -322,7 +322,12 @@ int scroll_batch_splice_status(ScrollBatch *b, int s, int f, int *status);
  *   scroll_batch_ingest(b, n, a, na, b_, nb, &first)   host files
  *   scroll_batch_ingest_device(b, n, d_files, desc, &first)   files already in
  *       device memory: desc[4k..4k+3] = offset, size of A, offset, size of B
- * The new streams get ids first .. first + n - 1. */
+ * The new streams get ids first .. first + n - 1.
+ * Device scratch, kept by the batch for later calls: about 1.25 x the input
+ * files' bytes (each slice body's 16 KB segments keep their output bytes
+ * between the summary and the write pass) while that stays under 8 GB, else
+ * a few hundred bytes per segment (the write pass decodes again).  Slices
+ * over 16 MB go one workgroup per stream. */
 int scroll_batch_ingest(ScrollBatch *b, int n, const uint8_t *const *ref_a, const size_t *na,
                         const uint8_t *const *ref_b, const size_t *nb, int *first);
 int scroll_batch_ingest_device(ScrollBatch *b, int n, const uint8_t *d_files,
@@ -364,7 +369,10 @@ int scroll_batch_ingest_stats(ScrollBatch *b, double *ms, int *count);
  * new long-term reference picture) go from pixels to a composing stream
  * without leaving the GPU.  Synchronous; SCROLL_ERR_OVERFLOW (the sizes are
  * filled, nothing written) when a file exceeds out_stride -- at most
- * 1.5 x (w*h*193/128) + 128 bytes.  w, h multiples of 16, < 65536 MBs. */
+ * 1.5 x (w*h*193/128) + 128 bytes.  w, h multiples of 16, < 65536 MBs.
+ * Device scratch, kept by the batch: the files' RBSP bytes (n x about 1.5 x
+ * w*h, 4 KB aligned) while under 4 GB, which the write pass reads instead of
+ * generating them again. */
 int scroll_batch_ipcm_files_device(ScrollBatch *b, int n, int w, int h, const uint8_t *d_pics,
                                    size_t pic_stride, uint8_t *d_out, size_t out_stride,
                                    uint64_t *sizes);

@@ -68,7 +68,14 @@ constexpr int HEAD_MAX = 160;           /* bits of one MB head (huge mvd: 2 x 63
 constexpr int HDR_MAX = 1024;           /* slice header bits (8 waypoints + MMCO ~ 250) */
 constexpr int OBUF = 6400;              /* k_dyn_emit: 127 carry + 5 + 4096 x 1.5 */
 
-constexpr uint32_t DF_OVER = 1u, DF_GENERAL = 2u;   /* DynFrame.err bits */
+/* DynFrame.err bits: a pool ran out (the batch grows it, the compose is
+ * repeated); the general chroma path; k_dyn_row's wait for the row above
+ * expired (the stream fails, SCROLL_ERR_DEVICE) */
+constexpr uint32_t DF_OVER = 1u, DF_GENERAL = 2u, DF_HANDOFF = 4u;
+/* the bound on that wait: 50 ms of s_memrealtime (100 MHz).  A row above is
+ * dispatched first and publishes within microseconds; the bound only turns a
+ * broken hand-off into a failed stream instead of a GPU hang */
+constexpr uint64_t HANDOFF_TICKS = 5000000ull;
 /* k_dyn_epfix could not settle the NAL's EP positions from the candidates
  * (too many): k_dyn_epscan scans it whole; not an error for the emit */
 constexpr uint32_t DF_EPSLOW = 0x100u;
@@ -613,12 +620,12 @@ struct LdsOrWin {
 typedef OrSink<LdsOrWin> WSink;
 
 /* ---------------------------------------------------------------------- */
-/* k_dyn_group / k_dyn_ep: records -> staged RBSP                         */
+/* MB heads and coeff_tokens of the dynamic NAL's row groups              */
 /* ---------------------------------------------------------------------- */
 /* A NAL's bits are: slice header, then per MB row the MB heads (one of 12
  * codeword classes) and, for dynamic MBs, coded_block_pattern,
  * mb_qp_delta and the present pieces (coeff_token from the neighbours'
- * TotalCoeff + the body k_dyn_code left in the records), then the stop bit. */
+ * TotalCoeff + the body k_dyn_row coded), then the stop bit. */
 
 __device__ inline int tc_of(uint32_t m) { return (int)((m >> 8) & 31u); }
 
@@ -780,7 +787,7 @@ __device__ __attribute__((noinline)) void ovf_put(uint32_t *buf, uint32_t lo, ui
  * first one holds the slice header and exists even with no rows), then one
  * per rect row (k_dyn_row), then the static groups below (the last one
  * holds rbsp_stop_one_bit).  Every group writes its own bits from bit 0 of
- * its row-stage slot and its bit count; k_dyn_stitch places them. */
+ * its row-stage slot and its bit count; k_dyn_epfix places them. */
 constexpr int GW = 64;
 #ifndef SCROLL_GBUF_WORDS
 #define SCROLL_GBUF_WORDS 256
@@ -1074,15 +1081,6 @@ __device__ inline void row_fetch(int task, int w, int ry, const DynGeom &g, __am
 {
     const int lstride = 16 * g.w, cstride = 8 * g.w, ndt = g.w * g.h;
     px.fr = 0;
-#ifdef SCROLL_ABL_NOFETCH
-    for (int i = 0; i < 4; ++i) {
-        px.a[i] = 0x80808080u + (uint32_t)(task * 7 + i * 3) * 0x01010101u;
-        px.b[i] = 0x80808080u + rt[i];
-        px.c[i] = rt[i + 4];
-    }
-    px.fr = task & 7;
-    return;
-#endif
     if (task < 16 * w) {
         const int k = task >> 4, r = task & 15, bx = r & 3, by = r >> 2;
         const uint32_t so = (uint32_t)((16 * ry + 4 * by) * lstride + 16 * k + 4 * bx);
@@ -1131,7 +1129,6 @@ __device__ inline void row_levels(bool luma, const BlkPix &px, uint32_t pk[4], i
     pk[0] = pk[1] = pk[2] = pk[3] = 0;
     n = 0;
     w0 = 0;
-    int res[16], W[16];
     /* prediction rows as packed bytes: luma as fetched, chroma bilinear (one
      * branch for the block, not one per pixel) */
     uint32_t pr[4];
@@ -1142,34 +1139,9 @@ __device__ inline void row_levels(bool luma, const BlkPix &px, uint32_t pk[4], i
 #pragma unroll
         for (int i = 0; i < 4; ++i) pr[i] = bilin4(px.b[i], px.c[i], (px.fr >> (3 * i)) & 7u);
     }
-#ifndef SCROLL_SCALAR_LEVELS
     /* packed 16-bit pairs (dyn_device.h levels_pk) */
     if (luma) levels_pk<true>(px.a, pr, pk, w0);
     else levels_pk<false>(px.a, pr, pk, w0);
-    n = nz_bytes(pk[0]) + nz_bytes(pk[1]) + nz_bytes(pk[2]) + nz_bytes(pk[3]);
-    return;
-#endif
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-#pragma unroll
-        for (int x = 0; x < 4; ++x)
-            res[4 * i + x] = (int)((px.a[i] >> (8 * x)) & 255u) - (int)((pr[i] >> (8 * x)) & 255u);
-    }
-    fwd4x4(res, W);
-    if (luma) {
-#pragma unroll
-        for (int k2 = 0; k2 < 16; ++k2) {
-            const int v = quant(W[ZZ[k2]], ZZ[k2]);          /* |v| <= 78: int8 */
-            pk[k2 >> 2] |= ((uint32_t)v & 255u) << (8 * (k2 & 3));
-        }
-    } else {
-        w0 = W[0];
-#pragma unroll
-        for (int k2 = 1; k2 < 16; ++k2) {
-            const int v = quant(W[ZZ[k2]], ZZ[k2]);
-            pk[(k2 - 1) >> 2] |= ((uint32_t)v & 255u) << (8 * ((k2 - 1) & 3));
-        }
-    }
     n = nz_bytes(pk[0]) + nz_bytes(pk[1]) + nz_bytes(pk[2]) + nz_bytes(pk[3]);
 }
 
@@ -1186,6 +1158,15 @@ __device__ inline int row_slot(int task, int w)
     const int k = l ? task >> 4 : jj >> 3, pc = l ? task & 15 : 18 + (jj & 7);
     return (int)__umul24((uint32_t)k, (uint32_t)NPC) + pc;   /* no quarter-rate multiply */
 }
+
+/* profiling variants only (tools/build_variant.sh, -DSCROLL_ABL_STOP=n):
+ * the workgroup stops after phase n, for per-phase time and VALU counts */
+#ifdef SCROLL_ABL_STOP
+#define ROW_CUT(n) \
+    if ((n) == SCROLL_ABL_STOP) return
+#else
+#define ROW_CUT(n) (void)0
+#endif
 
 /* grid (h, frames, streams), row_threads(w) threads, row_lds_bytes dynamic LDS.
  * GEN: the instantiation for the NALs k_dyn_rows flagged for the general
@@ -1209,7 +1190,7 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
 {
     __shared__ RowFixed L;
     extern __shared__ uint4 rdyn[];
-    /* debug: realtime at entry and after each phase (k_dyn_group's slots) */
+    /* debug: realtime at entry and after each phase (tools/dyn_stamps.py) */
     uint64_t stv[6] = {0, 0, 0, 0, 0, 0};
     if (stamps) stv[0] = __builtin_amdgcn_s_memrealtime();
     const int r = blockIdx.x, t = threadIdx.x, T = blockDim.x, lane = t & 63, wave = t >> 6, nwv = T >> 6;
@@ -1257,9 +1238,7 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
     /* ---- 1-2: records (levels -> CAVLC bodies) into LDS ---------------- */
     const int np = (ntask + T - 1) / T;                 /* tasks per thread, <= ROW_NPMAX */
     __syncthreads();                                    /* the row table (rt) */
-#if defined(SCROLL_ABL_STOP) && SCROLL_ABL_STOP == 0
-    return;
-#endif
+    ROW_CUT(0);
     if (!general) {
         const __amdgpu_buffer_rsrc_t fs = buf_rsrc(src + (size_t)s * g.src_ld + (size_t)f * g.src_fr,
                                                    (uint32_t)g.src_fr);
@@ -1303,7 +1282,8 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
         if (stamps) stv[1] = __builtin_amdgcn_s_memrealtime();
         /* the row's bottom TotalCoeffs (luma 12-15, chroma AC raster 2, 3 of
          * each plane) for the row below: one granule per MB */
-        if (t < w && r + 1 < R.h) {
+        const bool nopub = (g.debug & SCROLL_DEBUG_DYN_NOPUBLISH) && s == 0 && f == 0 && r == 0;   /* tests */
+        if (t < w && r + 1 < R.h && !nopub) {
             const uint16_t *mk = mt + t * NPC;
             uint64_t v = 0;
 #pragma unroll
@@ -1345,9 +1325,7 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
                 (uint16_t)(slot | (task < 16 * w ? 0 : 0x8000));
         }
         __syncthreads();
-#if defined(SCROLL_ABL_STOP) && SCROLL_ABL_STOP == 1
-        return;
-#endif
+    ROW_CUT(1);
         /* CAVLC bodies, largest TotalCoeff first */
         const int zbase = (int)L.kc[1][SORT_KEYS - 1];      /* blocks without levels sort last: no body */
         for (int pa = 0; pa < np; ++pa) {
@@ -1360,19 +1338,11 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
             CapSink cap{0, 0, 0};
             int t1 = 0;
             bool ok = true;
-#ifdef SCROLL_ABL_NOCAVLC
-            const int tc = __builtin_popcount(v4.x | v4.y | v4.z | v4.w) & 15;
-            cap.n = tc * 3;
-#elif defined(SCROLL_CAVLC_LOOP)
-            const int tc = cavlc_body<CapSink, true>(cap, L.ptabs, v4, luma ? 16 : 15, t1, ok,
-                                                     reinterpret_cast<const int8_t *>(lv + slot));
-#else
             /* total_zeros + run_before from the table: the load is in flight
              * during the trailing ones and the level loop */
             const uint32_t nz = nz_mask16(v4);
             const uint32_t tzrb = g_tzrb[luma ? nz : 65536u + nz];
             const int tc = cavlc_body_t(cap, reinterpret_cast<const int8_t *>(lv + slot), nz, tzrb, t1, ok);
-#endif
             mt[slot] = ok ? (uint16_t)(cap.n | (uint32_t)tc << 8 | (uint32_t)t1 << 13)
                           : (uint16_t)((uint32_t)tc << 8 | (uint32_t)t1 << 13 | M_OVF);
             if (ok) lv[slot] = body_msb(cap.hi, cap.lo, cap.n);
@@ -1402,121 +1372,38 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
         }
     }
     /* top TotalCoeffs of the row above (normal path): its granules; the last
-     * wave polls (the sort gives it the lightest blocks) */
+     * wave polls (the sort gives it the lightest blocks).  The wait is
+     * bounded: past HANDOFF_TICKS the frame fails (DF_HANDOFF) and the row
+     * finishes on zeros, so a missing granule costs one stream, not the GPU */
     if (!general && wave == nwv - 1) {
+        const uint64_t t0 = r > 0 ? __builtin_amdgcn_s_memrealtime() : 0ull;
+        bool late = false;
         for (int k = lane; k < w; k += 64) {
             uint64_t v = 0;
-#ifdef SCROLL_ABL_NOPOLL
-            if (false) {
-#else
             if (r > 0) {
-#endif
                 const unsigned long long *p = tcx + (nb * R.h + r - 1) * (size_t)w + k;
                 for (;;) {
                     v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     if ((uint32_t)(v >> 40) == (epoch & 0xffffffu)) break;
+                    if (__builtin_amdgcn_s_memrealtime() - t0 > HANDOFF_TICKS) {
+                        v = 0;
+                        late = true;
+                        break;
+                    }
                     __builtin_amdgcn_s_sleep(1);
                 }
             }
 #pragma unroll
             for (int e = 0; e < 8; ++e) ta[8 * k + e] = (uint8_t)((v >> (5 * e)) & 31u);
         }
+        if (__builtin_amdgcn_ballot_w64(late) != 0 && lane == 0) atomicOr(&dfr[nb].err, DF_HANDOFF);
     }
     const NalCtx c = nal_ctx(S, d, L.wo, L.wl, L.wv);
     const HeadCtx H = head_ctx(c);
-#ifdef SCROLL_MERGED_P34
-    /* the 12 MB-head classes, on the polling wave (phase 3+4 reads them) */
-    if (wave == nwv - 1 && lane < 12) {
-        CapSink hc{0, 0, 0};
-        H.put_class(hc, lane);
-        L.hhi[lane] = hc.hi;
-        L.hlo[lane] = hc.lo;
-        L.hlen[lane] = hc.n;
-        if (hc.over()) L.head_over = 1;
-    }
-#endif
     __syncthreads();                                    /* records, top TotalCoeffs, waypoint table */
     if (stamps) stv[2] = __builtin_amdgcn_s_memrealtime();
-#if defined(SCROLL_ABL_STOP) && SCROLL_ABL_STOP == 2
-    return;
-#endif
+    ROW_CUT(2);
 
-#ifdef SCROLL_MERGED_P34
-    /* ---- 3+4: per piece its coeff_token and length, per MB its cbp, code
-     * and piece offsets -- one pass: an MB's 26 pieces in coding order on
-     * lanes 0-25 of a 32-lane half (two MBs per wave), cbp from one ballot,
-     * the offsets from a wave scan of the present pieces' lengths ---------- */
-    const Tabs &TB = g_tabs;
-    const PTabs &PT = *reinterpret_cast<const PTabs *>(&g_ptabs);       /* the rare overflow paths */
-    const uint16_t(*ctab)[68] = L.ptabs.ct;
-    const bool head_over = L.head_over;
-    auto head_bits = [&](int rr, int col) -> uint32_t {
-        if (!head_over) return L.hlen[H.sel(rr, col)];
-        CountSink cn{0};
-        H.put_slow(cn, rr, col);
-        return cn.n;
-    };
-    {
-        const int hf = lane >> 5, j = lane & 31;
-        const int pc = j < 16 ? blk_raster(j) : j;          /* coding order -> piece slot */
-        for (int pr = wave; 2 * pr < w; pr += nwv) {
-            const int k = 2 * pr + hf, col = R.x0 + k;
-            const bool act = j < NPC && k < w;
-            uint32_t len = 0;
-            bool nzp = false;
-            if (act) {
-                const int i = k * NPC + pc;
-                const uint32_t mv = mt[i];
-                const uint16_t *mk = mt + k * NPC;
-                uint32_t tv = 0, tl = 0;
-                int nC = -1;
-                if (pc != 16 && pc != 17) {
-                    const int nAe = col > 0 ? 0 : -1, nBe = row > 0 ? 0 : -1;
-                    int nA2, nB2;
-                    if (pc < 16) {
-                        const int bx = pc & 3, by = pc >> 2;
-                        nA2 = bx > 0 ? tc_of(mk[pc - 1]) : (k > 0 ? tc_of(mk[pc + 3 - NPC]) : nAe);
-                        nB2 = by > 0 ? tc_of(mk[pc - 4]) : (r > 0 ? (int)ta[8 * k + pc] : nBe);
-                    } else {
-                        const int bq = (pc - 18) & 3, bx = bq & 1, by = bq >> 1;
-                        nA2 = bx > 0 ? tc_of(mk[pc - 1]) : (k > 0 ? tc_of(mk[pc + 1 - NPC]) : nAe);
-                        nB2 = by > 0 ? tc_of(mk[pc - 2]) : (r > 0 ? (int)ta[8 * k + (pc < 22 ? pc - 14 : pc - 16)] : nBe);
-                    }
-                    nC = nc_of(nA2, nB2);
-                    piece_token(ctab, mv, nC, tv, tl);
-                }
-                len = tl + (mv & 255u);
-                if (mv & M_OVF) len = ovf_bits(PT, TB, lv[i], pc, nC);            /* rare */
-                lo[i] = (uint16_t)(len | (uint32_t)(nC + 1) << 11);
-                nzp = tc_of(mv) != 0;
-            }
-            const uint32_t hm = (uint32_t)(__builtin_amdgcn_ballot_w64(nzp) >> (32 * hf));
-            const int cbp_l = ((hm & 0xfu) != 0) | ((hm & 0xf0u) != 0) << 1 | ((hm & 0xf00u) != 0) << 2 |
-                              ((hm & 0xf000u) != 0) << 3;
-            const int cbp_c = (hm >> 18) & 0xffu ? 2 : ((hm >> 16) & 3u ? 1 : 0);
-            const int cbp = cbp_l | cbp_c << 4;
-            const bool pres = act && (j < 16 ? ((cbp_l >> (j >> 2)) & 1) != 0 : (j < 18 ? cbp_c >= 1 : cbp_c == 2));
-            const uint32_t lp = pres ? (len & LO_LEN) : 0u;
-            const uint32_t incl = wave_incl_sum(lp, lane);
-            const uint32_t base = hf ? (uint32_t)__shfl((int)incl, 31, 64) : 0u;
-            const uint32_t tot = (uint32_t)__shfl((int)incl, 32 * hf + 31, 64) - base;
-            if (k < w) {
-                const int code = TB.cbp_code[cbp];
-                CountSink hs{head_bits(row, col)};
-                put_ue(hs, (uint32_t)code);
-                if (cbp) put_se(hs, 0);                     /* mb_qp_delta */
-                if (act) off16[k * NPC + pc] = pres ? (uint16_t)(hs.n + incl - lp - base) : (uint16_t)0xffffu;
-                if (j == 0) {
-                    mbits[k] = hs.n + tot;
-                    cbpa[k] = (uint8_t)cbp;
-                    codea[k] = (uint8_t)code;
-                }
-            }
-        }
-    }
-    __syncthreads();
-    if (stamps) stv[3] = __builtin_amdgcn_s_memrealtime();
-#else
     /* ---- 3: coeff_token, piece lengths ----------------------------------- */
     if (t < 12) {
         CapSink hc{0, 0, 0};
@@ -1556,9 +1443,7 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
     }
     __syncthreads();
     if (stamps) stv[3] = __builtin_amdgcn_s_memrealtime();
-#if defined(SCROLL_ABL_STOP) && SCROLL_ABL_STOP == 3
-    return;
-#endif
+    ROW_CUT(3);
     const bool head_over = L.head_over;
     auto head_bits = [&](int rr, int col) -> uint32_t {
         if (!head_over) return L.hlen[H.sel(rr, col)];
@@ -1605,7 +1490,6 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
         codea[k] = (uint8_t)code;
     }
     __syncthreads();
-#endif
     const int gi = nA + r;
     if (wave == 0) {
         uint32_t carry = 0;
@@ -1627,9 +1511,7 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
     }
     __syncthreads();
     if (stamps) stv[4] = __builtin_amdgcn_s_memrealtime();
-#if defined(SCROLL_ABL_STOP) && SCROLL_ABL_STOP == 4
-    return;
-#endif
+    ROW_CUT(4);
     const uint32_t bits = moff[mbw];
 
     /* ---- 5: bits -> the row's own row-stage words ------------------------ */
@@ -1683,9 +1565,6 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
             sk.finish();
         }
         /* pieces */
-#ifdef SCROLL_ABL_NOPIECES
-        if (false)
-#endif
         for (int i = t; i < npc; i += T) {
             const uint32_t o = off16[i];
             if (o == 0xffffu) continue;
@@ -1718,33 +1597,32 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
 }
 
 /* ---------------------------------------------------------------------- */
-/* k_dyn_stitch: row groups -> the NAL's staged RBSP + EP positions         */
+/* reading a NAL's RBSP straight from its row groups                      */
 /* ---------------------------------------------------------------------- */
-/* One workgroup per dynamic NAL: the row groups' bit counts -> their
- * offsets (one wave scan; ngroups <= 64), then per chunk of ST_CHUNK bytes
- * every staged word is assembled from the (one, at group seams two or more)
- * row-stage words it spans -- a funnel shift -- and stored; the chunk's
- * bytes are scanned for emulation prevention (closed-form rule, the zero
- * run carried from chunk to chunk).  Word w of a chunk is thread w % 256's,
- * so neighbouring lanes read neighbouring row-stage words, and the loads of
- * the next chunk are in flight while this one is scanned.  EP positions go
- * to the slot tail; sets rbsp_bytes / ep / err. */
-#ifndef SCROLL_ST_KW
-#define SCROLL_ST_KW 4
+/* A dynamic NAL's RBSP exists only as its row groups' words (each group
+ * from bit 0 of its row-stage slot); the row groups' bit counts give their
+ * offsets (one wave scan; ngroups <= 64).  An RBSP word is assembled from
+ * the (one, at group seams two or more) row-stage words it spans -- a
+ * funnel shift.  k_dyn_epscan reads EPS_CHUNK bytes at a time, EPS_KW words
+ * per thread, word w of a chunk thread w % EPS_T's (neighbouring lanes read
+ * neighbouring row-stage words, the next chunk's loads in flight while this
+ * one is scanned). */
+#ifndef SCROLL_EPS_KW
+#define SCROLL_EPS_KW 4
 #endif
-/* ST_KW words per thread and chunk (4 or 8) */
-#ifndef SCROLL_ST_T
-#define SCROLL_ST_T 256
+/* EPS_KW words per thread and chunk (4 or 8) */
+#ifndef SCROLL_EPS_T
+#define SCROLL_EPS_T 256
 #endif
-constexpr int ST_T = SCROLL_ST_T, ST_NW = ST_T / 64, ST_KW = SCROLL_ST_KW, ST_CHUNK = ST_T * 4 * ST_KW;
-static_assert(ST_KW % 4 == 0, "the EP scan reads 16-byte LDS vectors");
+constexpr int EPS_T = SCROLL_EPS_T, EPS_NW = EPS_T / 64, EPS_KW = SCROLL_EPS_KW, EPS_CHUNK = EPS_T * 4 * EPS_KW;
+static_assert(EPS_KW % 4 == 0, "the EP scan reads 16-byte LDS vectors");
 static_assert(DYN_MAX_H + 2 * ((DYN_MAX_MBH + DYN_STATIC_ROWS - 1) / DYN_STATIC_ROWS) <= 64,
-              "k_dyn_stitch scans the row groups with one wave");
+              "rs_table scans the row groups with one wave");
 
 /* the RBSP word (MSB first) at bit P (a multiple of 32) of a NAL whose row
  * groups have offsets goff, bit counts gb and row-stage words at fr + gw;
  * gg: the group holding P or before it, advanced */
-__device__ inline uint32_t stitch_word(uint32_t P, int &gg, int ng, uint32_t T, const uint32_t *goff,
+__device__ inline uint32_t rs_word_span(uint32_t P, int &gg, int ng, uint32_t T, const uint32_t *goff,
                                        const uint32_t *gb, const uint32_t *gw, const uint32_t *fr)
 {
     uint32_t acc = 0, filled = 0;
@@ -1770,7 +1648,7 @@ __device__ inline uint32_t stitch_word(uint32_t P, int &gg, int ng, uint32_t T, 
 }
 
 /* last group with goff[g] <= P */
-__device__ inline int stitch_group(uint32_t P, int ng, const uint32_t *goff)
+__device__ inline int rs_group_at(uint32_t P, int ng, const uint32_t *goff)
 {
     int lo = 0, hi = ng;
     while (hi - lo > 1) {
@@ -1781,14 +1659,14 @@ __device__ inline int stitch_group(uint32_t P, int ng, const uint32_t *goff)
     return lo;
 }
 
-/* the first source words of the ST_KW words thread t assembles for the
+/* the first source words of the EPS_KW words thread t assembles for the
  * chunk at byte c0 (x1: the next word, where the shift needs it) */
-struct StitchLoads {
-    uint32_t x0[ST_KW], x1[ST_KW], y[ST_KW];           /* y: the next group's first word (seam words) */
-    int g[ST_KW];
+struct ScanLoads {
+    uint32_t x0[EPS_KW], x1[EPS_KW], y[EPS_KW];           /* y: the next group's first word (seam words) */
+    int g[EPS_KW];
 };
 
-__device__ inline void stitch_load(StitchLoads &L, uint32_t c0, int t, int ng, uint32_t T, const uint32_t *goff,
+__device__ inline void scan_load(ScanLoads &L, uint32_t c0, int t, int ng, uint32_t T, const uint32_t *goff,
                                    const uint32_t *gb, const uint32_t *gw, const uint32_t *fr, int &gcarry)
 {
     /* a thread's words only move forward: its group search starts from
@@ -1797,8 +1675,8 @@ __device__ inline void stitch_load(StitchLoads &L, uint32_t c0, int t, int ng, u
     int gg = gcarry;
     while (gg + 1 < ng && goff[gg + 1] <= P0) ++gg;
 #pragma unroll
-    for (int k = 0; k < ST_KW; ++k) {
-        const uint32_t P = P0 + 32u * ST_T * (uint32_t)k;
+    for (int k = 0; k < EPS_KW; ++k) {
+        const uint32_t P = P0 + 32u * EPS_T * (uint32_t)k;
         while (gg + 1 < ng && goff[gg + 1] <= P) ++gg;
         L.g[k] = gg;
         const uint32_t lp = P - goff[gg], i = lp >> 5;
@@ -1815,7 +1693,8 @@ __device__ inline void stitch_load(StitchLoads &L, uint32_t c0, int t, int ng, u
  * = RBSP bits incl. the stop bit), gb = bit counts, gw = first row-stage
  * words in the frame's region */
 __device__ inline void rs_table(const uint32_t *gbits, size_t nb, const DynGeom &g, const uint32_t *fr,
-                                uint32_t *goff, uint32_t *gb, uint32_t *gw, uint32_t *cw, int t)
+                                uint32_t *goff, uint32_t *gb, uint32_t *gw, uint32_t *cw, int t,
+                                uint32_t *bad = nullptr)
 {
     const int ng = g.ngroups;
     constexpr int SR = DYN_STATIC_ROWS;
@@ -1832,8 +1711,20 @@ __device__ inline void rs_table(const uint32_t *gbits, size_t nb, const DynGeom 
             if (t >= nA && t < nA + g.h) {
                 const uint32_t m = fr[c];
                 if (m & 0x80000000u) {
-                    w = m & 0x7fffffffu;
-                    c = w + g.rs_spill_words - EPC_ROW;
+                    /* bounds check of the spill slot the record names: slot k
+                     * of the pool after the rs_frames frame regions, k <
+                     * rs_spill_cap (k_dyn_row's claim is bounded the same
+                     * way).  A record outside the pool is never followed: the
+                     * group reads its own slot and the frame is flagged bad */
+                    const uint64_t base = ((uint64_t)g.rs_frames - nb) * g.rs_frame_words;
+                    const uint64_t rel = (uint64_t)(m & 0x7fffffffu) - base;
+                    if ((m & 0x7fffffffu) >= base && rel % g.rs_spill_words == 0 &&
+                        rel / g.rs_spill_words < g.rs_spill_cap) {
+                        w = m & 0x7fffffffu;
+                        c = w + g.rs_spill_words - EPC_ROW;
+                    } else if (bad) {
+                        *bad = 1u;
+                    }
                 }
             }
             gw[t] = w;
@@ -1848,8 +1739,8 @@ __device__ inline uint32_t rs_word(uint32_t P, int ng, uint32_t T, const uint32_
                                    const uint32_t *gw, const uint32_t *fr)
 {
     if (P >= T) return 0u;
-    int gg = stitch_group(P, ng, goff);
-    return stitch_word(P, gg, ng, T, goff, gb, gw, fr);
+    int gg = rs_group_at(P, ng, goff);
+    return rs_word_span(P, gg, ng, T, goff, gb, gw, fr);
 }
 
 /* w[i] for i in 0..8 without indexing (three levels of selects) */
@@ -1882,7 +1773,7 @@ __device__ inline void rs_load9(__amdgpu_buffer_rsrc_t rr, uint32_t wo, uint32_t
 __device__ inline void rs_load8(uint32_t P, int &gg, int ng, uint32_t T, const uint32_t *goff, const uint32_t *gb,
                                 const uint32_t *gw, const uint32_t *fr, __amdgpu_buffer_rsrc_t rr, uint32_t w[8])
 {
-    if (goff[gg] > P) gg = stitch_group(P, ng, goff);     /* never for increasing P */
+    if (goff[gg] > P) gg = rs_group_at(P, ng, goff);     /* never for increasing P */
     while (gg + 1 < ng && goff[gg + 1] <= P) ++gg;
     const uint32_t lp = P - goff[gg];
     const uint32_t end = goff[gg] + gb[gg];              /* the group's end (bits) */
@@ -1924,7 +1815,7 @@ __device__ inline void rs_load8(uint32_t P, int &gg, int ng, uint32_t T, const u
         for (int k = 0; k < 8; ++k) {
             const uint32_t Pk = P + 32u * (uint32_t)k;
             int g2 = gg;
-            w[k] = Pk < T ? __builtin_bswap32(stitch_word(Pk, g2, ng, T, goff, gb, gw, fr)) : 0u;
+            w[k] = Pk < T ? __builtin_bswap32(rs_word_span(Pk, g2, ng, T, goff, gb, gw, fr)) : 0u;
         }
     }
 }
@@ -1951,14 +1842,14 @@ __device__ inline void rs_load8(uint32_t P, int &gg, int ng, uint32_t T, const u
 constexpr int EPS_Z = SCROLL_EPS_Z;
 
 /* grid (EPS_Z, frames, streams) */
-__global__ __launch_bounds__(ST_T) void k_dyn_epscan(DevStream *__restrict__ st, DynFrame *__restrict__ dfr,
+__global__ __launch_bounds__(EPS_T) void k_dyn_epscan(DevStream *__restrict__ st, DynFrame *__restrict__ dfr,
                                                      int ld_fr, DynGeom g, const uint32_t *__restrict__ rowstage,
                                                      const uint32_t *__restrict__ gbits, uint8_t *__restrict__ eps)
 {
     __shared__ uint32_t goff[65], gb[64], gw[64];
-    __shared__ int32_t wmax[ST_NW];
+    __shared__ int32_t wmax[EPS_NW];
     __shared__ uint32_t ep_n, ep_base;
-    __shared__ uint4 cbuf4[ST_CHUNK / 16];              /* the chunk's bytes */
+    __shared__ uint4 cbuf4[EPS_CHUNK / 16];              /* the chunk's bytes */
     __shared__ uint32_t epl[EPLIST_MAX];                /* this workgroup's EP positions */
     uint32_t *cbuf = reinterpret_cast<uint32_t *>(cbuf4);
     const int z = blockIdx.x, f = blockIdx.y, s = blockIdx.z, t = threadIdx.x;
@@ -1972,19 +1863,19 @@ __global__ __launch_bounds__(ST_T) void k_dyn_epscan(DevStream *__restrict__ st,
     __syncthreads();
     const uint32_t T = goff[ng];                        /* NAL RBSP bits incl. the stop bit */
     const uint32_t nin = (T + 7) >> 3;                  /* bitwriter.c:103-111 */
-    StitchLoads ld;
-    uint32_t c0 = (uint32_t)z * ST_CHUNK;
+    ScanLoads ld;
+    uint32_t c0 = (uint32_t)z * EPS_CHUNK;
     int gcarry = 0;
     if (c0 < nin) {
-        gcarry = stitch_group(c0 * 8u + 32u * (uint32_t)t, ng, goff);
-        stitch_load(ld, c0, t, ng, T, goff, gb, gw, fr, gcarry);
+        gcarry = rs_group_at(c0 * 8u + 32u * (uint32_t)t, ng, goff);
+        scan_load(ld, c0, t, ng, T, goff, gb, gw, fr, gcarry);
     }
-    for (; c0 < nin; c0 += EPS_Z * ST_CHUNK) {
+    for (; c0 < nin; c0 += EPS_Z * EPS_CHUNK) {
         {
             const uint32_t P0 = c0 * 8u + 32u * (uint32_t)t;
 #pragma unroll
-            for (int k = 0; k < ST_KW; ++k) {
-                const uint32_t P = P0 + 32u * ST_T * (uint32_t)k;
+            for (int k = 0; k < EPS_KW; ++k) {
+                const uint32_t P = P0 + 32u * EPS_T * (uint32_t)k;
                 const int g0 = ld.g[k];
                 const uint32_t lp = P - goff[g0], sh = lp & 31u;
                 uint32_t v = 0;
@@ -1998,16 +1889,16 @@ __global__ __launch_bounds__(ST_T) void k_dyn_epscan(DevStream *__restrict__ st,
                                 v |= ld.y[k] >> avail;      /* the next group's first bits */
                             } else {                        /* groups under 32 bits: rare */
                                 int g2 = g0;
-                                v = stitch_word(P, g2, ng, T, goff, gb, gw, fr);
+                                v = rs_word_span(P, g2, ng, T, goff, gb, gw, fr);
                             }
                         }
                     }
                 }
-                cbuf[t + ST_T * k] = __builtin_bswap32(v);   /* memory order */
+                cbuf[t + EPS_T * k] = __builtin_bswap32(v);   /* memory order */
             }
         }
-        const uint32_t cn = c0 + EPS_Z * ST_CHUNK;
-        if (cn < nin) stitch_load(ld, cn, t, ng, T, goff, gb, gw, fr, gcarry);
+        const uint32_t cn = c0 + EPS_Z * EPS_CHUNK;
+        if (cn < nin) scan_load(ld, cn, t, ng, T, goff, gb, gw, fr, gcarry);
         lds_barrier();                                  /* the next chunk's loads stay in flight */
         /* the last non-zero RBSP byte before the chunk: needed only when its
          * first byte is <= 3 (else that byte is non-zero and no EP decision
@@ -2022,27 +1913,27 @@ __global__ __launch_bounds__(ST_T) void k_dyn_epscan(DevStream *__restrict__ st,
                 }
             }
         }
-        /* emulation prevention of this thread's 4 ST_KW contiguous bytes */
-        const uint32_t ib = c0 + 4u * ST_KW * (uint32_t)t;
-        uint32_t wv[ST_KW];
+        /* emulation prevention of this thread's 4 EPS_KW contiguous bytes */
+        const uint32_t ib = c0 + 4u * EPS_KW * (uint32_t)t;
+        uint32_t wv[EPS_KW];
 #pragma unroll
-        for (int j = 0; j < ST_KW / 4; ++j) {
-            const uint4 a = cbuf4[(ST_KW / 4) * t + j];
+        for (int j = 0; j < EPS_KW / 4; ++j) {
+            const uint4 a = cbuf4[(EPS_KW / 4) * t + j];
             wv[4 * j] = a.x; wv[4 * j + 1] = a.y; wv[4 * j + 2] = a.z; wv[4 * j + 3] = a.w;
         }
         int lnz = -1;
 #pragma unroll
-        for (int w = 0; w < ST_KW; ++w) {
+        for (int w = 0; w < EPS_KW; ++w) {
             const uint32_t m = ib + 4u * w < nin ? wv[w] : 0u;
             if (m) lnz = (int)(ib + 4u * w) + 3 - (__builtin_clz(m) >> 3);
         }
         if (t == 0 && lnz < 0) lnz = lz;                /* the run reaching back past the chunk */
         int ex, tot;
-        block_excl_max<ST_NW, true>(lnz, wmax, ex, tot);   /* its barriers also free cbuf */
+        block_excl_max<EPS_NW, true>(lnz, wmax, ex, tot);   /* its barriers also free cbuf */
         int prev = t == 0 ? lz : ex;
         uint32_t ins = 0;
 #pragma unroll
-        for (int i = 0; i < 4 * ST_KW; ++i) {
+        for (int i = 0; i < 4 * EPS_KW; ++i) {
             const uint32_t gi2 = ib + (uint32_t)i;
             const uint32_t b = gi2 < nin ? (wv[i >> 2] >> (8 * (i & 3))) & 255u : 256u;   /* past the end: never */
             ins |= (ep_insert(b, (int)gi2 - 1 - prev) ? 1u : 0u) << i;
@@ -2065,7 +1956,7 @@ __global__ __launch_bounds__(ST_T) void k_dyn_epscan(DevStream *__restrict__ st,
     __syncthreads();
     uint32_t *eplist = reinterpret_cast<uint32_t *>(eps + nb * DYN_OVF_BYTES);
     const uint32_t base = ep_base;
-    for (uint32_t i = (uint32_t)t; i < n && i < (uint32_t)EPLIST_MAX; i += ST_T)
+    for (uint32_t i = (uint32_t)t; i < n && i < (uint32_t)EPLIST_MAX; i += EPS_T)
         if (base + i < (uint32_t)EPLIST_MAX) eplist[base + i] = epl[i];
 }
 
@@ -2130,16 +2021,20 @@ __global__ __launch_bounds__(EPF_T) void k_dyn_epfix(DevStream *__restrict__ st,
     __shared__ uint32_t goff[65], gb[64], gw[64], cw[64];
     __shared__ uint32_t cbase[65];                      /* runs before group g */
     __shared__ uint32_t lst[EPF_LIST];
-    __shared__ uint32_t nlst, nu, slow;
+    __shared__ uint32_t nlst, nu, slow, bad;
     const int f = blockIdx.x, s = blockIdx.y, t = threadIdx.x;
     const size_t nb = (size_t)s * ld_fr + f;
     DynFrame *DF = dfr + nb;
     if (DF->nal < 0) return;
-    if (DF->err & DF_OVER) {                            /* k_dyn_rows / k_dyn_row: pools exhausted */
+    if (t == 0) bad = 0u;
+    __syncthreads();
+    if (DF->err & (DF_OVER | DF_HANDOFF)) {             /* k_dyn_rows / k_dyn_row: pools exhausted,
+                                                           or a row's wait expired */
         if (t == 0) {
             DF->rbsp_bytes = 0;
             DF->ep = 0;
-            atomicOr((unsigned int *)&st[s].err, SCROLL_DEVERR_DYN);
+            atomicOr((unsigned int *)&st[s].err,
+                     (DF->err & DF_HANDOFF) ? SCROLL_DEVERR_HANDOFF : SCROLL_DEVERR_DYN);
         }
         return;
     }
@@ -2147,8 +2042,17 @@ __global__ __launch_bounds__(EPF_T) void k_dyn_epfix(DevStream *__restrict__ st,
     constexpr int SR = DYN_STATIC_ROWS;
     const int nA = max(1, (g.y0 + SR - 1) / SR);
     const uint32_t *fr = rowstage + nb * g.rs_frame_words;
-    rs_table(gbits, nb, g, fr, goff, gb, gw, cw, t);
+    rs_table(gbits, nb, g, fr, goff, gb, gw, cw, t, &bad);
     __syncthreads();
+    if (bad) {                                          /* a spill record outside the pool (never) */
+        if (t == 0) {
+            DF->err = DF_OVER;
+            DF->rbsp_bytes = 0;
+            DF->ep = 0;
+            atomicOr((unsigned int *)&st[s].err, SCROLL_DEVERR_DYN);
+        }
+        return;
+    }
     if (t < 64) {
         const uint32_t c = t < ng ? fr[cw[t]] : 0u;
         const uint32_t cmax = (t >= nA && t < nA + g.h) ? EPC_ROW - 1u : EPC_STATIC - 1u;
@@ -2353,10 +2257,10 @@ __global__ __launch_bounds__(DT) void k_dyn_emit(const DevStream *__restrict__ s
 
 /* ---------------------------------------------------------------------- */
 /* k_dyn_emit_gather: the same output for NALs with <= EPLIST_MAX EP bytes  */
-/* (all in practice: 82 per config-3 frame).  k_dyn_ep recorded where       */
+/* (all in practice: 82 per config-3 frame).  k_dyn_epfix recorded where    */
 /* the 03 bytes go; after sorting those positions once, every thread builds */
 /* whole 16-byte arena chunks independently -- no barriers, no LDS byte     */
-/* buffer: a chunk without an EP byte is a funnel shift of the staged RBSP. */
+/* buffer: a chunk without an EP byte is a funnel shift of the row groups.  */
 /* ---------------------------------------------------------------------- */
 __device__ inline uint32_t pick4(const uint32_t w[8], int i)     /* w[i], i in 0..7, no indexing */
 {
@@ -2662,7 +2566,7 @@ int dyn_launch_pack(hipStream_t hs, int nframes, int S, DevStream *st, const Nal
     hipLaunchKernelGGL(k_dyn_epfix, dim3(nframes, S), dim3(EPF_T), 0, hs, st, dfr, ld_fr, *g, x->rowstage,
                        x->gbits, eps);
     if (hipGetLastError() != hipSuccess) return -1;
-    hipLaunchKernelGGL(k_dyn_epscan, dim3(EPS_Z, nframes, S), dim3(ST_T), 0, hs, st, dfr, ld_fr, *g,
+    hipLaunchKernelGGL(k_dyn_epscan, dim3(EPS_Z, nframes, S), dim3(EPS_T), 0, hs, st, dfr, ld_fr, *g,
                        x->rowstage, x->gbits, eps);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
@@ -2729,7 +2633,7 @@ void dyn_rowstage_geom(DynGeom *g, int mbw, int mbh)
 size_t dyn_slot_bound(int mbw, int mbh, int rw, int rh)
 {
     /* header + every MB head (+ cbp) + every dynamic MB at its provable
-     * maximum + the stop word + k_dyn_stitch's 32-byte steps */
+     * maximum + the stop word + 32 bytes of read-ahead */
     const size_t bits = (size_t)HDR_MAX + (size_t)mbw * mbh * (HEAD_MAX + 1) +
                         (size_t)rw * rh * MB_BITS_MAX + 64;
     return ((bits / 8 + 32 + DYN_OVF_BYTES) + 255) & ~(size_t)255;

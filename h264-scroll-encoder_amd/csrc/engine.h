@@ -59,7 +59,9 @@ typedef struct {
 #define SCROLL_DEVERR_DYN      4u   /* a dynamic NAL outgrew its staging slot     */
 #define SCROLL_DEVERR_HINT     8u   /* a hint rect names an invalid reference     */
 #define SCROLL_DEVERR_SPLICE  16u   /* a spliced slice failed (parse / reference) */
-#define SCROLL_DEVERR_STAGED   (SCROLL_DEVERR_DYN | SCROLL_DEVERR_HINT | SCROLL_DEVERR_SPLICE)   /* nothing committed */
+#define SCROLL_DEVERR_HANDOFF 32u   /* k_dyn_row's wait for the row above timed out */
+#define SCROLL_DEVERR_STAGED   (SCROLL_DEVERR_DYN | SCROLL_DEVERR_HINT | SCROLL_DEVERR_SPLICE | \
+                                SCROLL_DEVERR_HANDOFF)   /* nothing committed */
 
 /* k_plan state pass -> size pass: the stream's planned totals and the final
  * waypoint table (committed only by the size pass).  128 bytes. */
@@ -106,7 +108,7 @@ typedef struct {
     uint32_t rs_spill_words;        /* a spill slot: one rect row at its provable bound */
     uint32_t rs_spill_cap;          /* spill slots after the frames' regions       */
     uint32_t gen_cap;               /* general-path record slots (NALs)           */
-    uint32_t pad_g;
+    uint32_t rs_frames;             /* frame regions before the spill slots (S F)  */
 } DynGeom;
 
 /* hints of one composed frame: rects [first, first + n) of the batch's rect

@@ -1517,9 +1517,12 @@ int ingest_launch(hipStream_t hs, const uint8_t *in, const IngestFile *files, in
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
+/* scratch of the segmented path; 0 when ingest_launch takes the one-workgroup
+ * path anyway (a slice over FIX_MAXSEG segments), which needs none */
 size_t ingest_work_bytes(int nstreams, uint64_t max_file, bool staged)
 {
     const size_t maxseg = (size_t)((max_file + SEG - 1) / SEG) + 1u;
+    if (maxseg > (size_t)FIX_MAXSEG) return 0;
     const size_t base = 2 * (size_t)nstreams * (sizeof(IngPlan) + maxseg * sizeof(IngSeg));
     return staged ? base + 2 * (size_t)nstreams * maxseg * (size_t)(NJ * OCH) + 16 : base;
 }

@@ -1498,7 +1498,11 @@ int scroll_batch_sync(ScrollBatch *b)
     int rc = SCROLL_OK;
     for (int s = 0; s < b->nstreams; ++s) {
         if (!b->h_st[s].err) continue;
-        if (rc == SCROLL_OK && (b->h_st[s].err & SCROLL_DEVERR_SPLICE)) {
+        if (rc == SCROLL_OK && (b->h_st[s].err & SCROLL_DEVERR_HANDOFF)) {
+            set_err("stream %d: a dynamic-rect row waited past its bound for the row above's "
+                    "TotalCoeffs (k_dyn_row hand-off); the stream committed nothing", s);
+            rc = SCROLL_ERR_DEVICE;
+        } else if (rc == SCROLL_OK && (b->h_st[s].err & SCROLL_DEVERR_SPLICE)) {
             int st = 0, ff = 0;
             for (; ff < b->max_frames && !st; ++ff)
                 if (splice_frame_status(b, (size_t)s * b->max_frames + ff, &st)) break;
@@ -1700,6 +1704,8 @@ int scroll_batch_output_to_host_async(ScrollBatch *b, uint8_t *dst, size_t cap, 
         HIPCHK(hipGetLastError());
     }
     b->last = hs;
+    b->host_valid = 0;      /* k_out_table zeroes DevStream.undelivered: the next sync waits for
+                               the copy and refreshes the host mirror before anything uploads it */
     return SCROLL_OK;
 }
 
@@ -1924,6 +1930,7 @@ int scroll_batch_set_dyn_rect(ScrollBatch *b, int x0, int y0, int w, int h, size
     g.rs_spill_cap = g.rs_row_words < g.rs_spill_words
                          ? (uint32_t)std::min(S * F * (size_t)h, std::max<size_t>(2048, S * F * (size_t)h / 32))
                          : 0u;
+    g.rs_frames = (uint32_t)(S * F);
     if (b->dyn_grow) {                 /* pools at their bounds (ran out before) */
         g.gen_cap = (uint32_t)(S * F);
         if (g.rs_spill_cap) g.rs_spill_cap = (uint32_t)(S * F * (size_t)h);
@@ -2632,17 +2639,21 @@ int scroll_batch_ingest_device(ScrollBatch *b, int n, const uint8_t *d_files, co
         b->ing_cap = n;
     }
     std::vector<IngestFile> files(2 * (size_t)n);
-    uint64_t maxf = 0;
+    uint64_t maxf = 0, totf = 0;
     for (int k = 0; k < 2 * n; ++k) {
         files[k].off = desc[2 * k];
         files[k].size = desc[2 * k + 1];
         maxf = std::max(maxf, files[k].size);
+        totf += files[k].size;
     }
     const bool serial = getenv("SCROLL_INGEST_SERIAL") != nullptr;
-    /* the staged write pass while its scratch stays under 8 GB (the input's
-     * size, rounded up per segment), else the recomputing one */
-    const bool staged = getenv("SCROLL_INGEST_RECOMPUTE") == nullptr &&
-                        ingest_work_bytes(n, maxf, true) <= ((size_t)8 << 30);
+    /* the staged write pass while its scratch (every file sized like the
+     * largest, ~1.25x per segment) stays within 4x the input plus 256 MB and
+     * under 8 GB -- a batch of small files with one huge one takes the
+     * recomputing pass instead of a scratch sized by the huge one */
+    const size_t stg_bytes = ingest_work_bytes(n, maxf, true);
+    const bool staged = getenv("SCROLL_INGEST_RECOMPUTE") == nullptr && stg_bytes <= ((size_t)8 << 30) &&
+                        stg_bytes <= 4 * (size_t)totf + ((size_t)256 << 20);
     const size_t wb = serial ? 0 : ingest_work_bytes(n, maxf, staged);
     if (wb > b->ing_work_bytes) {
         (void)hipFree(b->d_ing_work);
@@ -2708,6 +2719,7 @@ int scroll_batch_ingest_device(ScrollBatch *b, int n, const uint8_t *d_files, co
         memset(d, 0, sizeof(*d));
         cfg_to_dev(&cfg, d);
         d->out_pos = outs[k].bytes;
+        d->undelivered = outs[k].bytes;     /* SPS + PPS + A + B go out with the first delivery */
         d->out_cap = b->arena_bytes;
     }
     HIPCHK(hipMemcpy(b->d_st + s0, b->h_st + s0, (size_t)n * sizeof(DevStream),

@@ -21,6 +21,7 @@ SCROLL_ERR_OOM = -3
 SCROLL_ERR_OVERFLOW = -4
 SCROLL_ERR_HIP = -5
 SCROLL_ERR_CONFIG = -6
+SCROLL_ERR_DEVICE = -7
 SCROLL_MODE_COMPOSER = 0
 SCROLL_MODE_EXPERIMENT = 1
 SCROLL_DEBUG_FORCE_SERIAL = 1
@@ -37,6 +38,7 @@ SCROLL_DEBUG_DYN_NOCAVLC = 1024
 SCROLL_DEBUG_DYN_NOHEAD = 2048
 SCROLL_DEBUG_DYN_NOWRITE = 4096
 SCROLL_DEBUG_DYN_EPCAP4 = 8192
+SCROLL_DEBUG_DYN_NOPUBLISH = 16384
 SCROLL_COMPOSE_REWIND = 1
 MAX_WAYPOINTS = 8
 MV_LIMIT_PX = 496
@@ -325,6 +327,10 @@ class HostBuffer:
         return None if v == (1 << 64) - 1 else v
 
     def stream(self, s):
+        """stream s's bytes of the last delivery; raises when that delivery did
+        not fit (nothing was written, the table rows are stale)"""
+        if self.total() is None:
+            raise RuntimeError("the last delivery did not fit the host buffer: nothing was written")
         o, n = self.table[1 + 2 * s], self.table[2 + 2 * s]
         return ctypes.string_at(self.p.value + o, n)
 

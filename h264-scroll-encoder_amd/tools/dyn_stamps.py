@@ -1,15 +1,14 @@
 #!/usr/bin/env python3
-"""dyn_stamps.py -- profiling aid: where k_dyn_row's / k_dyn_group's time goes.
+"""dyn_stamps.py -- profiling aid: where k_dyn_row's time goes.
 
 Runs the bench's config-3 workload (bench.py p720dyn) once with
-SCROLL_DEBUG_DYN_STAMPS and prints, per row-group workgroup of k_dyn_group
-(rect rows and the two static groups separately), the s_memrealtime span
-(100 MHz, microseconds) of each phase:
-  load+tok   records loaded, coeff_token / lengths of the pieces
-  mb         cbp, piece offsets per dynamic MB
-  scan       MB offsets of the row (static groups: row offsets)
-  lookback   waiting for the groups before (decoupled look-back)
-  write      bits -> LDS -> staging words
+SCROLL_DEBUG_DYN_STAMPS and prints, per k_dyn_row workgroup (one rect row),
+the s_memrealtime span (100 MHz, microseconds) of each phase:
+  levels       pixels -> residual -> transform -> quant, TotalCoeff ranks
+  cavlc+poll   CAVLC bodies; the last wave polls the row above's TotalCoeffs
+  tokens       coeff_token and length of every piece
+  mb+scan      cbp, piece offsets per MB; the row's MB offsets
+  write        bits -> LDS window -> the row's row-stage words
 plus the k_dyn_emit_gather workgroup spans.  Then times the workload
 without stamps (HIP events).
 
@@ -72,11 +71,9 @@ def main():
     got = hs.lib.scroll_batch_debug_stamps(b.h, buf, nslot)
     allst = np.frombuffer(buf, dtype=np.uint64).reshape(-1, 8)[:got]
     grp = allst[2 * S * F:].astype(np.int64).reshape(S * F, ng, 8)
-    gnames = ["load+tok", "mb", "scan", "lookback", "write"]
     rnames = ["levels", "cavlc+poll", "tokens", "mb+scan+lb", "write"]     # k_dyn_row
-    for label, sel in (("rect rows (k_dyn_row)", slice(na, na + rect[3])), ("static above", slice(0, na)),
-                       ("static below", slice(na + rect[3], ng))):
-        names = rnames if label.startswith("rect") else gnames
+    for label, sel in (("rect rows (k_dyn_row)", slice(na, na + rect[3])),):
+        names = rnames
         gsel = grp[:, sel].reshape(-1, 8)
         gsel = gsel[gsel[:, 5] > 0]
         if not len(gsel):                          # k_dyn_static records no stamps
@@ -99,17 +96,6 @@ def main():
         print(f"{label} span {(t1 - t0) / 100.0:.1f} us")
         ends = gg[:, :, 5][gg[:, :, 5] > 0]
         conc = [int(np.sum((g0 <= x) & (ends > x))) for x in np.linspace(t0, t1, 12)]
-        print("  resident WGs over time:", conc)
-    z = allst[:S * F].astype(np.int64)           # k_dyn_stitch: realtime (100 MHz)
-    z = z[z[:, 0] > 0]
-    if len(z):
-        dur = (z[:, 4] - z[:, 0]) / 100.0
-        print(f"k_dyn_stitch: {len(z)} WGs, span {(z[:, 4].max() - z[:, 0].min()) / 100.0:.1f} us, "
-              f"WG duration mean {dur.mean():.1f} p99 {np.percentile(dur, 99):.1f} us, chunks {z[:, 5].mean():.1f}; "
-              f"scan {((z[:, 1] - z[:, 0]) / 100.0).mean():.2f}  first assembly {((z[:, 2] - z[:, 1]) / 100.0).mean():.2f}  "
-              f"first EP {((z[:, 3] - z[:, 2]) / 100.0).mean():.2f}  rest {((z[:, 4] - z[:, 3]) / 100.0).mean():.2f} us")
-        t0 = z[:, 0].min()
-        conc = [int(np.sum((z[:, 0] <= x) & (z[:, 4] > x))) for x in np.linspace(t0, z[:, 4].max(), 12)]
         print("  resident WGs over time:", conc)
     e = allst[S * F:2 * S * F].astype(np.int64)  # k_dyn_emit_gather: realtime (100 MHz)
     e = e[e[:, 0] > 0]

@@ -45,6 +45,8 @@ extern "C" {
 #define SCROLL_ERR_OVERFLOW  (-4)   /* output arena full (reference: assert abort) */
 #define SCROLL_ERR_HIP       (-5)
 #define SCROLL_ERR_CONFIG    (-6)   /* config outside the supported syntax range  */
+#define SCROLL_ERR_DEVICE    (-7)   /* a device-side wait timed out (the dynamic rect's
+                                       row hand-off): that stream committed nothing */
 
 #define SCROLL_MODE_COMPOSER   0    /* waypoint NAL in addition to the scroll NAL */
 #define SCROLL_MODE_EXPERIMENT 1    /* waypoint NAL instead of the scroll NAL     */
@@ -58,11 +60,11 @@ extern "C" {
 #define SCROLL_DEBUG_EMIT_NOMIXED 32 /* k_emit skips the mixed-chunk phase        */
 #define SCROLL_DEBUG_EMIT_STAMPS 64 /* k_emit records s_memtime per phase per wave */
 #define SCROLL_DEBUG_EMIT_NOBYTES 128 /* k_emit skips the tile-end partial chunks  */
-#define SCROLL_DEBUG_DYN_STAMPS 256 /* k_dyn_group / gather: realtime per phase  */
+#define SCROLL_DEBUG_DYN_STAMPS 256 /* k_dyn_row / gather: realtime per phase    */
 /* retired: runtime ablations of the earlier one-kernel dynamic coder (no
- * kernel reads them now; k_dyn_code's ablations are the compile-time
- * variants -DSCROLL_ABL_NOLOAD / -DSCROLL_ABL_NOCAVLC).  Values kept so the
- * flag numbering stays stable. */
+ * kernel reads them now; k_dyn_row's per-phase ablation is the compile-time
+ * variant -DSCROLL_ABL_STOP=n).  Values kept so the flag numbering stays
+ * stable. */
 #define SCROLL_DEBUG_DYN_NOLOAD  512
 #define SCROLL_DEBUG_DYN_NOCAVLC 1024
 #define SCROLL_DEBUG_DYN_NOHEAD  2048
@@ -71,6 +73,10 @@ extern "C" {
  * with more emulation-prevention bytes takes the large-NAL path (k_dyn_emit,
  * otherwise only reached past 2,048 EP bytes); output unchanged */
 #define SCROLL_DEBUG_DYN_EPCAP4 8192
+/* tests: k_dyn_row of stream 0, frame 0, rect row 0 does not publish its
+ * bottom TotalCoeffs, so row 1's bounded wait expires: stream 0 fails with
+ * SCROLL_ERR_DEVICE, every other stream composes normally */
+#define SCROLL_DEBUG_DYN_NOPUBLISH 16384
 
 typedef struct ScrollBatch ScrollBatch;
 
@@ -323,11 +329,12 @@ int scroll_batch_splice_status(ScrollBatch *b, int s, int f, int *status);
  *   scroll_batch_ingest_device(b, n, d_files, desc, &first)   files already in
  *       device memory: desc[4k..4k+3] = offset, size of A, offset, size of B
  * The new streams get ids first .. first + n - 1.
- * Device scratch, kept by the batch for later calls: about 1.25 x the input
- * files' bytes (each slice body's 16 KB segments keep their output bytes
- * between the summary and the write pass) while that stays under 8 GB, else
- * a few hundred bytes per segment (the write pass decodes again).  Slices
- * over 16 MB go one workgroup per stream. */
+ * Device scratch, kept by the batch for later calls: 2 n x 1.25 x the LARGEST
+ * file's bytes (each slice body's 16 KB segments keep their output bytes
+ * between the summary and the write pass, every file sized like the largest)
+ * while that stays under 8 GB and under 4 x the input's bytes + 256 MB, else a
+ * few hundred bytes per segment of the largest file (the write pass decodes
+ * again).  Slices over 16 MB go one workgroup per stream, without scratch. */
 int scroll_batch_ingest(ScrollBatch *b, int n, const uint8_t *const *ref_a, const size_t *na,
                         const uint8_t *const *ref_b, const size_t *nb, int *first);
 int scroll_batch_ingest_device(ScrollBatch *b, int n, const uint8_t *d_files,

@@ -1,6 +1,6 @@
 """GPU parity of the dynamic-rect residual coder (BASELINE configs 3-5):
-k_plan (state) -> k_dyn_rows -> k_dyn_code -> k_dyn_group -> k_dyn_ep -> k_plan (size) -> k_emit
--> k_dyn_emit_gather / k_dyn_emit,
+k_plan (state) -> k_dyn_rows -> k_dyn_code_general -> k_dyn_row -> k_dyn_static -> k_dyn_epfix /
+k_dyn_epscan -> k_plan (size) -> k_emit -> k_dyn_emit_gather / k_dyn_emit,
 through the C ABI, against the CPU restatement oracle/dyn_oracle.c
 (or_compose_dyn), byte for byte.  The reference has no implementation of
 this path, so these bits are pinned only by the restatement, which
@@ -245,7 +245,8 @@ def test_dyn_chunked_composes_and_experiment_mode(gpu, oracle):
 
 def test_dyn_half_pel_waypoint_chain(gpu, oracle):
     """a resumed config with a waypoint at an odd offset: its rows predict at
-    half-pel chroma positions, which only the general k_dyn_code path does"""
+    half-pel chroma positions, which only the general path (k_dyn_code_general
+    -> k_dyn_row<true>) does"""
     w, h = 64, 1024
     rect = Rect(1, 0, 2, 48)
     wps = [(501, 2, 1)]
@@ -349,4 +350,32 @@ def test_dyn_spill_pool_runs_out_and_grows(gpu, oracle):
     src = synth_source(oracle, S, F, rect)
     want = oracle_streams(oracle, w, h, offs, rect, src, R)
     check_equal(b, want)
+    b.close()
+
+
+def test_dyn_row_handoff_wait_is_bounded(gpu, oracle):
+    """k_dyn_row's wait for the row above's TotalCoeffs is bounded: with
+    SCROLL_DEBUG_DYN_NOPUBLISH rect row 0 of stream 0, frame 0 never
+    publishes, row 1's wait expires (50 ms), stream 0 fails with
+    SCROLL_ERR_DEVICE and commits nothing, and the other streams stay
+    bit-exact; the next compose without the flag succeeds"""
+    w, h = 1280, 720
+    rect = Rect(28, 10, 25, 25)
+    S, F = 3, 4
+    offs = synthetic_offsets(S, F, h)
+    R = striped_refs(oracle, w, h)
+    src = synth_source(oracle, S, F, rect)
+    want = oracle_streams(oracle, w, h, offs, rect, src, R)
+    b, rc = gpu_streams(gpu, w, h, offs, rect, R, synth=True, debug=gpu.SCROLL_DEBUG_DYN_NOPUBLISH)
+    assert rc == gpu.SCROLL_ERR_DEVICE, (rc, gpu.last_error())
+    assert "stream 0" in gpu.last_error()
+    assert b.output_size(0) == 0
+    for s in (1, 2):
+        assert b.output(s) == want[s], s
+    b.set_debug(0)                                    # recovers: stream 0 composes again
+    b.set_offsets(np.ascontiguousarray(offs[:, :1]))
+    b.dyn_source_synth(1, 0, 0)
+    b.compose(1)
+    assert b.sync() == 0, gpu.last_error()
+    assert len(b.output(0)) > 20000
     b.close()

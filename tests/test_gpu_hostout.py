@@ -74,6 +74,66 @@ def test_host_delivery_dyn(gpu):
     b.close()
 
 
+def test_host_delivery_after_sync_waits_for_the_copy(gpu):
+    """compose -> sync -> deliver -> sync: the second sync must wait for the
+    copy (and refresh the host mirror of undelivered); then deliver ->
+    set_config -> compose -> deliver must not send the old bytes again"""
+    hs = gpu
+    S, F = 6, 24
+    b = hs.Batch(S, F, 1 << 20, device=0)
+    for _ in range(S):
+        b.add_stream(hs.make_config(1280, 720))
+    hb = hs.HostBuffer(S * F * 4096, S)
+    prev = [0] * S
+    offs = np.tile(np.arange(F, dtype=np.int32) * 11, (S, 1))
+    b.set_offsets(offs)
+    b.compose(F)
+    assert b.sync() == 0
+    for i in range(hb.cap):
+        hb.data[i] = 0
+    b.output_to_host_async(hb)
+    _check(hs, b, hb, prev)
+    # a config upload after the delivery: the host mirror must already hold
+    # undelivered = 0, or the next delivery resends the bytes above
+    for s in range(S):
+        b.set_config(s, b.config(s))
+    b.set_offsets(offs + 3)
+    b.compose(F)
+    b.output_to_host_async(hb)
+    _check(hs, b, hb, prev)
+    hb.close()
+    b.close()
+
+
+def test_host_delivery_of_ingested_streams(gpu, oracle):
+    """an ingested stream's first delivery carries its header (SPS, PPS, A,
+    B) and then the composed frames, like b.output(s)"""
+    import ctypes
+    hs = gpu
+    S, F = 3, 10
+    files = []
+    for _ in range(S):
+        pair = []
+        for which in (0, 1):
+            buf = (ctypes.c_uint8 * (320 * 240 * 3 + 4096))()
+            n = oracle.or_ipcm_ref_file(buf, len(buf), 320, 240, which)
+            pair.append(bytes(buf[:n]))
+        files.append(tuple(pair))
+    b = hs.Batch(S, F, 1 << 20, device=0)
+    assert b.ingest(files) == 0
+    hb = hs.HostBuffer(S * (1 << 19), S)
+    prev = [0] * S
+    b.output_to_host_async(hb)
+    _check(hs, b, hb, prev)
+    assert all(p > 200000 for p in prev)          # the I_PCM header went out
+    b.set_offsets(np.tile(np.arange(F, dtype=np.int32) * 8, (S, 1)))
+    b.compose(F)
+    b.output_to_host_async(hb)
+    _check(hs, b, hb, prev)
+    hb.close()
+    b.close()
+
+
 def test_host_delivery_too_small_writes_nothing(gpu):
     hs = gpu
     S, F = 4, 20

@@ -4,8 +4,8 @@ the bench does, and EVERY byte of the last step of every stream compared
 with the CPU oracle (tests/stepcheck.py -> oracle/verify_oracle.c on the
 host's cores).  These launches run the full grids the bench runs -- config
 3's 102,400 k_dyn_row workgroups with the epoch-tagged TotalCoeff hand-off
-between rect rows at full residency, the XCD frame rotation, the stitch and
-gather -- which the small tests of test_gpu_dyn.py do not reach.
+between rect rows at full residency, the XCD frame rotation, the EP fix-up
+and the gather -- which the small tests of test_gpu_dyn.py do not reach.
 Dynamic-rect bits: oracle/dyn_oracle.c (parity unpinned, DESIGN.md §4b);
 P-only bits: pinned to the reference.  Run on an MI355X:
 -m gpu."""

@@ -509,6 +509,11 @@ static void or_predict2(int x, int y, int mbw, const or_mvi2 *above, const or_mv
     }
 }
 
+/* test hook (tests/test_dyn_oracle.py): each dynamic MB's residual start
+ * bit in the RBSP, its levels and its neighbours' TotalCoeffs, as coded */
+static or_dyn_trace_fn or_trace_cb;
+void or_dyn_set_trace(or_dyn_trace_fn fn) { or_trace_cb = fn; }
+
 size_t or_scroll_nal_dyn(uint8_t *dst, size_t cap, or_cfg *c, int off, const or_dyn_rect *rc,
                          const uint8_t *src, const or_refs *R)
 {
@@ -573,6 +578,9 @@ size_t or_scroll_nal_dyn(uint8_t *dst, size_t cap, or_cfg *c, int off, const or_
                 memset(&tc_cur[x], 0, sizeof(or_tcctx));
             } else {
                 or_mb_levels(c, R, rc, src, x, y, ref, mvp, luma, cdc, cac);
+                if (or_trace_cb)
+                    or_trace_cb(x, y, (long long)b.nbits, &luma[0][0], &cdc[0][0], &cac[0][0][0],
+                                x > 0 ? tc_cur[x - 1].tc : NULL, y > 0 ? tc_above[x].tc : NULL);
                 or_mb_residual(&b, (const int(*)[16])luma, (const int(*)[4])cdc,
                                (const int(*)[4][15])cac, x > 0 ? &tc_cur[x - 1] : NULL,
                                y > 0 ? &tc_above[x] : NULL, &tc_cur[x]);

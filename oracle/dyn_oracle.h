@@ -109,6 +109,16 @@ size_t or_dyn_mb_levels_bits(uint8_t *dst, size_t cap, const int luma[16][16],
                              const int nc_left[16 + 8], const int nc_top[16 + 8], int avail_l,
                              int avail_t, int *cbp_out, int tc_out[24], size_t *nbits);
 
+/* test hook: called by or_scroll_nal_dyn for every dynamic MB before its
+ * residual (cbp onwards) is written: MB (x, y), the residual's first bit in
+ * the RBSP (slice header included, NAL header byte not), the levels
+ * (luma[16][16] raster block / scan order, cdc[2][4], cac[2][4][15]) and the
+ * left / top neighbours' TotalCoeffs (24 each, NULL = unavailable).  NULL
+ * turns it off.  Not thread-safe: tests only. */
+typedef void (*or_dyn_trace_fn)(int x, int y, long long bit, const int *luma, const int *cdc, const int *cac,
+                                const int *tc_left, const int *tc_top);
+void or_dyn_set_trace(or_dyn_trace_fn fn);
+
 #ifdef __cplusplus
 }
 #endif

@@ -184,3 +184,38 @@ def test_reference_cavlc_parser_accepts(oracle):
             assert ref.ref_cavlc_parse(rbsp, len(rbsp), c["mb_start_bit"], c["nrefs"],
                                        ctypes.byref(end)) == 0
             assert end.value == c["stop_bit"]
+
+
+def test_cavlc_values_pinned_by_reference_decoder(oracle):
+    """Value-level pin (tests/golden/make_golden_cavlc_values.py): every coded
+    block of every dynamic MB of the cavlc_ref.json NALs (real levels and
+    neighbour contexts) plus 600 synthetic MBs with escape-range levels is
+    decoded by the REFERENCE's CAVLC functions (trans_resizer.c: cbp_inter_table
+    + read_ue/se, compute_luma_nC / compute_chroma_nC, read_coeff_token,
+    copy_cavlc_block's level parser, decode_total_zeros, decode_run_before);
+    the coefficient vector rebuilt from those fields must equal the oracle's
+    quantised coefficients, and nC, token and block lengths must agree.  The
+    committed SHA-256 of those records pins the oracle where the reference
+    build is absent.  Transform and quantiser: no reference (unpinned)."""
+    import json
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden"))
+    import make_golden_cavlc_values as mv
+    fx = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden",
+                                     "cavlc_values.json")))
+    refso = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle",
+                         "_ref", "libref_cavlc.so")
+    ref = ctypes.CDLL(refso) if os.path.exists(refso) else None
+    mine, live, esc = [], [], [0, 0, 0]
+    for case in mv.all_mbs(oracle):
+        lv = case[7]
+        _, exp = mv.expected(oracle, lv, case[3], case[4], case[5], case[6])
+        mine += mv.oracle_records(lv, exp)
+        esc = [a + b for a, b in zip(esc, mv.escapes(lv))]
+        if ref is not None:
+            live += mv.check_mb(oracle, ref, case)
+    assert len(mine) == fx["blocks"]
+    assert mv.digest(mine) == fx["sha256"]
+    if ref is not None:
+        assert live == mine
+    # level_prefix 14 at suffixLength 0, prefix 15 at 0 and at > 0 all occur
+    assert min(esc) > 1000, esc

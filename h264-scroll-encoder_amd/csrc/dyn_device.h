@@ -984,6 +984,46 @@ __device__ __host__ inline uint32_t tzrb_entry(const Tabs &T, uint32_t nz, int m
     return (n ? acc << (32 - n) : 0u) | (1u << (31 - n));
 }
 
+/* Level codewords of k_dyn_row's CAVLC body as ONE table entry per level
+ * (9.2.2.1): class c = suffixLength 0..6, or 7 + suffixLength (0 / 1) for
+ * the first level after fewer than three trailing ones (levelCode - 2), x
+ * level v in [-LVT_V, LVT_V] at index v + LVT_V + 1.  Entry = codeword value
+ * (the bits after level_prefix's zeros: at most 13) | its length << 13 | the
+ * next level's class (suffixLength after this level) << 18.  Levels past
+ * LVT_V take the arithmetic form. */
+constexpr int LVT_V = 47, LVT_W = 96, LVT_C = 9, LVT_N = LVT_C * LVT_W;
+__device__ __host__ constexpr uint32_t lvt_entry(int c, int v)
+{
+    if (v == 0 || v > LVT_V || v < -LVT_V) return 0u;
+    const int sl = c >= 7 ? c - 7 : c, adj = c >= 7 ? 2 : 0;
+    const int a = v < 0 ? -v : v;
+    const int code = 2 * a - 2 + (v < 0 ? 1 : 0) - adj;
+    if (code < 0) return 0u;                               /* |v| = 1 after < 3 trailing ones: never */
+    const int lim = sl ? (15 << sl) : 30;
+    const uint32_t mk = (1u << sl) - 1u;
+    uint32_t fv = ((uint32_t)code & mk) | (mk + 1u), fl = (uint32_t)((code >> sl) + 1 + sl);
+    if (code >= lim) {
+        fv = (uint32_t)(4096 + code - lim);
+        fl = 28u;
+    } else if (sl == 0 && code >= 14) {
+        fv = (uint32_t)(code + 2);
+        fl = 19u;
+    }
+    const int s1 = sl == 0 ? 1 : sl;
+    const int nx = s1 + ((a > (3 << (s1 - 1)) && s1 < 6) ? 1 : 0);
+    return fv | fl << 13 | (uint32_t)nx << 18;
+}
+struct LvTab {
+    uint32_t e[LVT_N];
+};
+constexpr LvTab make_lvt()
+{
+    LvTab T{};
+    for (int c = 0; c < LVT_C; ++c)
+        for (int i = 0; i < LVT_W; ++i) T.e[c * LVT_W + i] = lvt_entry(c, i - LVT_V - 1);
+    return T;
+}
+
 /* cavlc_body for k_dyn_row (levels as LDS bytes lb, bit i = level i non-zero
  * in nz, tzrb = the block's tzrb_entry, loaded by the caller before the call
  * so its latency hides behind the level loop):
@@ -995,7 +1035,7 @@ __device__ __host__ inline uint32_t tzrb_entry(const Tabs &T, uint32_t nz, int m
  * Same bits, TotalCoeff, TrailingOnes and ok as cavlc_body<CAP, true>. */
 template <class CAP>
 __device__ __host__ inline int cavlc_body_t(CAP &cap, const int8_t *lb, uint32_t nz, uint32_t tzrb, int &t1o,
-                                            bool &ok)
+                                            bool &ok, const uint32_t *lvt)
 {
     const int tc = __builtin_popcount(nz);
     /* g: the mask shifted up one with a guard bit 0 -- clz(g) <= 31, and
@@ -1029,25 +1069,32 @@ __device__ __host__ inline int cavlc_body_t(CAP &cap, const int8_t *lb, uint32_t
         ac = (ac << len) | v;
         n += len;
     };
-    int sl = (tc > 10 && t1 < 3) ? 1 : 0;
-    int adj = t1 < 3 ? 2 : 0;                              /* the first level after < 3 trailing ones */
+    /* the level class (lvt_entry): suffixLength, +7 for the first level
+     * after fewer than three trailing ones */
+    int cls = ((tc > 10 && t1 < 3) ? 1 : 0) + (t1 < 3 ? 7 : 0);
     for (int k = t1; k < tc; ++k) {                        /* levels below the trailing ones */
         const int p = top_bit(m);
         m &= ~(1u << p);
         const int v = (int)lb[p];
-        const int a = v < 0 ? -v : v;
-        const int code = 2 * a - 2 + (v < 0 ? 1 : 0) - adj;
-        adj = 0;
-        const int lim = sl ? (15 << sl) : 30;
-        const uint32_t mk = (1u << sl) - 1u;
-        uint32_t fv = ((uint32_t)code & mk) | (mk + 1u);
-        uint32_t fl = (uint32_t)((code >> sl) + 1 + sl);
-        const bool e15 = code >= lim, e14 = sl == 0 && code >= 14;
-        fv = e15 ? (uint32_t)(4096 + code - lim) : (e14 ? (uint32_t)(code + 2) : fv);
-        fl = e15 ? 28u : (e14 ? 19u : fl);
-        push(acc, an, fv, fl, cap);
-        const int s1 = sl == 0 ? 1 : sl;
-        sl = s1 + ((a > (3 << (s1 - 1)) && s1 < 6) ? 1 : 0);
+        uint32_t e;
+        if (v >= -LVT_V && v <= LVT_V) {
+            e = lvt[cls * LVT_W + v + LVT_V + 1];
+        } else {                                           /* rare: the arithmetic form */
+            const int sl = cls >= 7 ? cls - 7 : cls, adj = cls >= 7 ? 2 : 0;
+            const int a = v < 0 ? -v : v;
+            const int code = 2 * a - 2 + (v < 0 ? 1 : 0) - adj;
+            const int lim = sl ? (15 << sl) : 30;
+            const uint32_t mk = (1u << sl) - 1u;
+            uint32_t fv = ((uint32_t)code & mk) | (mk + 1u);
+            uint32_t fl = (uint32_t)((code >> sl) + 1 + sl);
+            const bool e15 = code >= lim, e14 = sl == 0 && code >= 14;
+            fv = e15 ? (uint32_t)(4096 + code - lim) : (e14 ? (uint32_t)(code + 2) : fv);
+            fl = e15 ? 28u : (e14 ? 19u : fl);
+            const int s1 = sl == 0 ? 1 : sl;
+            e = fv | fl << 13 | (uint32_t)(s1 + ((a > (3 << (s1 - 1)) && s1 < 6) ? 1 : 0)) << 18;
+        }
+        push(acc, an, e & 0x1fffu, (e >> 13) & 31u, cap);
+        cls = (int)(e >> 18);
     }
     /* total_zeros + run_before: the entry's code, len = 31 - ctz */
     const uint32_t tzl = 31u - (uint32_t)__builtin_ctz(tzrb);

@@ -48,6 +48,9 @@ __constant__ PTabs g_ptabs = make_ptabs(k_tabs);
  * table: 384 KB, filled once per device by k_tzrb_init; mostly L2-resident
  * (the masks of real blocks are few) */
 __device__ uint32_t g_tzrb[TZRB_N];
+/* level codewords (lvt_entry), copied into k_dyn_row's bit window for its
+ * CAVLC phase */
+__constant__ LvTab g_lvt = make_lvt();
 
 __global__ __launch_bounds__(256) void k_tzrb_init()
 {
@@ -1025,9 +1028,13 @@ constexpr int ROW_GB = SCROLL_ROW_GB;           /* bit window: 28 Kbit (a config
 
 struct RowFixed {
     PTabs ptabs;
-    union {                                      /* the sort's counts are dead before the bit window */
+    union {                                      /* the sort's counts and the level table are dead before the bit window */
         uint32_t buf[ROW_GB];
-        uint32_t kc[2][SORT_KEYS];               /* the sort: blocks per TotalCoeff class, then its base */
+        struct {
+            uint32_t kc[2][SORT_KEYS];           /* the sort: blocks per TotalCoeff class, then its base */
+            uint32_t kc_pad[32 - 2 * SORT_KEYS];
+            uint32_t lvt[LVT_N];                 /* level codewords (CAVLC phase) */
+        };
     };
     uint64_t hhi[12], hlo[12];
     uint32_t hlen[12];
@@ -1037,6 +1044,9 @@ struct RowFixed {
     uint32_t ncand;                              /* EP candidate words of the row */
     uint32_t spill;                              /* its spill slot (a row over its slot) */
 };
+
+static_assert(2 * SORT_KEYS <= 32 && 32 + LVT_N <= ROW_GB, "the sort counts and the level table share the bit window");
+static_assert(offsetof(RowFixed, lvt) % 8 == 0, "the level table is copied in 8-byte words");
 
 /* dynamic LDS of k_dyn_row: lv [NPC w] uint4 (levels, then bodies), mbits
  * [w] u32, moff [mbw + 1] u32, mt / lo / off16 [NPC w] u16 (the sort's
@@ -1231,6 +1241,8 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
     }
     if (t < SORT_KEYS) L.kc[0][t] = 0u;
     load_ptabs(L.ptabs, t, T);
+    for (int i = t; i < LVT_N / 2; i += T)      /* 8-byte aligned in LDS */
+        reinterpret_cast<uint2 *>(L.lvt)[i] = reinterpret_cast<const uint2 *>(&g_lvt)[i];
     if (!general && t < 32) L.rt[t] = rows[nb * (size_t)(32 * g.h) + (t < 16 ? 16 * r + t : 16 * g.h + (t < 24 ? 8 * r + t - 16 : 8 * g.h + 8 * r + t - 24))];
     const NalDesc d = nal[(size_t)s * ld_nal + df.nal];
     const uint32_t ysz = (uint32_t)S->w * (uint32_t)S->h, csz = ysz / 4;
@@ -1342,7 +1354,7 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
              * during the trailing ones and the level loop */
             const uint32_t nz = nz_mask16(v4);
             const uint32_t tzrb = g_tzrb[luma ? nz : 65536u + nz];
-            const int tc = cavlc_body_t(cap, reinterpret_cast<const int8_t *>(lv + slot), nz, tzrb, t1, ok);
+            const int tc = cavlc_body_t(cap, reinterpret_cast<const int8_t *>(lv + slot), nz, tzrb, t1, ok, L.lvt);
             mt[slot] = ok ? (uint16_t)(cap.n | (uint32_t)tc << 8 | (uint32_t)t1 << 13)
                           : (uint16_t)((uint32_t)tc << 8 | (uint32_t)t1 << 13 | M_OVF);
             if (ok) lv[slot] = body_msb(cap.hi, cap.lo, cap.n);

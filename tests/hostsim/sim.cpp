@@ -355,7 +355,8 @@ long sim_cavlc_split_t(const int *coef, int max, int nC, int start, uint32_t *wo
     bool ok = false;
     if (fits) {
         const uint32_t e = dyn::tzrb_entry(g_dyn_tabs, nz, max);
-        tc = dyn::cavlc_body_t(cap, lb + 1, nz, e, t1, ok);
+        static constexpr dyn::LvTab lvt = dyn::make_lvt();
+        tc = dyn::cavlc_body_t(cap, lb + 1, nz, e, t1, ok, lvt.e);
     }
     if (!ok) {
         *tc_out = dyn::cavlc_block(os, g_dyn_tabs, coef, max, nC);

@@ -1043,6 +1043,7 @@ struct RowFixed {
     uint32_t rt[32];                             /* the row's prediction-row table (k_dyn_rows) */
     uint32_t ncand;                              /* EP candidate words of the row */
     uint32_t spill;                              /* its spill slot (a row over its slot) */
+    uint32_t pcd[NPC];                           /* per piece class: its nC neighbours (pc_desc) */
 };
 
 static_assert(2 * SORT_KEYS <= 32 && 32 + LVT_N <= ROW_GB, "the sort counts and the level table share the bit window");
@@ -1055,6 +1056,37 @@ __host__ __device__ inline size_t row_lds_bytes(int w, int mbw)
 {
     return (size_t)16 * NPC * w + (size_t)4 * (w + mbw + 1) + (size_t)2 * (3 * NPC * w) +
            (size_t)10 * w + 16;
+}
+
+/* The nC neighbours of piece class pc (0-15 luma raster, 16 / 17 chroma DC,
+ * 18 + 4 p + b chroma AC), relative to the piece's slot i = k NPC + pc:
+ * bits 0-5 the left neighbour's slot - i + 32 (same MB, or the left MB's
+ * right column), bit 6 it is in the left MB, bits 7-12 the top neighbour's
+ * slot - i + 32 (same MB), bit 13 it is in the row above (then bits 14-16
+ * its index in the row's top TotalCoeffs ta[8 k + e]), bit 17 chroma DC
+ * (nC = -1). */
+__host__ __device__ constexpr uint32_t pc_desc(int pc)
+{
+    if (pc == 16 || pc == 17) return 1u << 17;
+    int da, db, e = 0;
+    bool al, bt;
+    if (pc < 16) {
+        const int bx = pc & 3, by = pc >> 2;
+        al = bx == 0;
+        da = al ? 3 - NPC : -1;
+        bt = by == 0;
+        db = bt ? 0 : -4;
+        e = bt ? pc : 0;
+    } else {
+        const int b = (pc - 18) & 3, bx = b & 1, by = b >> 1;
+        al = bx == 0;
+        da = al ? 1 - NPC : -1;
+        bt = by == 0;
+        db = bt ? 0 : -2;
+        e = bt ? (pc < 22 ? pc - 14 : pc - 16) : 0;
+    }
+    return (uint32_t)(da + 32) | (al ? 1u : 0u) << 6 | (uint32_t)(db + 32) << 7 | (bt ? 1u : 0u) << 13 |
+           (uint32_t)e << 14;
 }
 
 /* threads of a k_dyn_row workgroup: one block task each (two past 1024) */
@@ -1240,6 +1272,7 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
         L.ncand = 0;
     }
     if (t < SORT_KEYS) L.kc[0][t] = 0u;
+    if (t < NPC) L.pcd[t] = pc_desc(t);
     load_ptabs(L.ptabs, t, T);
     for (int i = t; i < LVT_N / 2; i += T)      /* 8-byte aligned in LDS */
         reinterpret_cast<uint2 *>(L.lvt)[i] = reinterpret_cast<const uint2 *>(&g_lvt)[i];
@@ -1248,7 +1281,13 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
     const uint32_t ysz = (uint32_t)S->w * (uint32_t)S->h, csz = ysz / 4;
 
     /* ---- 1-2: records (levels -> CAVLC bodies) into LDS ---------------- */
-    const int np = (ntask + T - 1) / T;                 /* tasks per thread, <= ROW_NPMAX */
+    /* phase 1 walks a slot space: luma tasks at [0, 16 w), chroma tasks from
+     * the next wave boundary cb on, so no wave runs both the luma and the
+     * chroma path (when that costs no extra pass; else cb = 16 w) */
+    const int nl = 16 * w, cba = (nl + 63) & ~63;
+    const int cb = (cba + 8 * w + T - 1) / T == (ntask + T - 1) / T ? cba : nl;
+    const int np = (cb + 8 * w + T - 1) / T;            /* tasks per thread, <= ROW_NPMAX */
+    auto task_of = [&](int v) -> int { return v < nl ? v : (v >= cb && v < cb + 8 * w ? v - cb + nl : -1); };
     __syncthreads();                                    /* the row table (rt) */
     ROW_CUT(0);
     if (!general) {
@@ -1259,14 +1298,17 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
          * an LDS atomic (the order inside a class does not matter), kept in
          * lo[] (phase 3's) until the class bases are known */
         BlkPix nx;                                      /* the next task's pixels, in flight */
-        if (t < ntask) row_fetch(t, w, r, g, fs, rb, L.rt, csz, nx);
+        {
+            const int t0 = task_of(t);
+            if (t0 >= 0) row_fetch(t0, w, r, g, fs, rb, L.rt, csz, nx);
+        }
         for (int pa = 0; pa < np; ++pa) {
-            const int task = pa * T + t;
+            const int task = task_of(pa * T + t), tn = task_of((pa + 1) * T + t);
             const BlkPix cur = nx;
-            if (task + T < ntask) row_fetch(task + T, w, r, g, fs, rb, L.rt, csz, nx);
+            if (tn >= 0) row_fetch(tn, w, r, g, fs, rb, L.rt, csz, nx);
             uint32_t pk[4];
             int n = 0, w0 = 0;
-            if (task < ntask) {
+            if (task >= 0) {
                 row_levels(task < 16 * w, cur, pk, n, w0);
                 const int slot = row_slot(task, w);
                 lv[slot] = make_uint4(pk[0], pk[1], pk[2], pk[3]);
@@ -1276,7 +1318,7 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
             /* chroma DC: the quad's four DC coefficients -> 2x2 Hadamard,
              * quant -> levels as int16 in the DC slot (coded after the
              * barrier that publishes the CAVLC tables) */
-            const bool cdc = task >= 16 * w && task < ntask;
+            const bool cdc = task >= 16 * w;
             if (__builtin_amdgcn_ballot_w64(cdc) == 0) continue;   /* luma-only wave: no chroma DC */
             const int qb = lane & ~3;
             const int d0 = __shfl(w0, qb, 64), d1 = __shfl(w0, qb + 1, 64);
@@ -1428,27 +1470,22 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
     const Tabs &TB = g_tabs;
     const PTabs &PT = *reinterpret_cast<const PTabs *>(&g_ptabs);       /* the rare overflow paths */
     const uint16_t(*ctab)[68] = L.ptabs.ct;
+    /* one straight path for every piece class: its neighbours from pc_desc
+     * (the per-class branches had made every wave run all of them) */
+    const int nAe = R.x0 > 0 ? 0 : -1, nBe = row > 0 ? 0 : -1;
     for (int i = t; i < npc; i += T) {
-        const int k = div_npc(i), pc = i - k * NPC, col = R.x0 + k;
-        const uint32_t mv = mt[i];
-        const uint16_t *mk = mt + k * NPC;
-        uint32_t tv = 0, tl = 0;
-        int nC = -1;
-        if (pc != 16 && pc != 17) {
-            const int nAe = col > 0 ? 0 : -1, nBe = row > 0 ? 0 : -1;
-            int nA2, nB2;
-            if (pc < 16) {
-                const int bx = pc & 3, by = pc >> 2;
-                nA2 = bx > 0 ? tc_of(mk[pc - 1]) : (k > 0 ? tc_of(mk[pc + 3 - NPC]) : nAe);
-                nB2 = by > 0 ? tc_of(mk[pc - 4]) : (r > 0 ? (int)ta[8 * k + pc] : nBe);
-            } else {
-                const int b = (pc - 18) & 3, bx = b & 1, by = b >> 1;
-                nA2 = bx > 0 ? tc_of(mk[pc - 1]) : (k > 0 ? tc_of(mk[pc + 1 - NPC]) : nAe);
-                nB2 = by > 0 ? tc_of(mk[pc - 2]) : (r > 0 ? (int)ta[8 * k + (pc < 22 ? pc - 14 : pc - 16)] : nBe);
-            }
-            nC = nc_of(nA2, nB2);
-            piece_token(ctab, mv, nC, tv, tl);
-        }
+        const int k = div_npc(i), pc = i - k * NPC;
+        const uint32_t mv = mt[i], D = L.pcd[pc];
+        const int ia = max(i + (int)(D & 63u) - 32, 0), ib = max(i + (int)((D >> 7) & 63u) - 32, 0);
+        const int tA = tc_of(mt[ia]), tB = tc_of(mt[ib]), tT = (int)ta[8 * k + (int)((D >> 14) & 7u)];
+        const int nA = ((D & 64u) && k == 0) ? nAe : tA;
+        const int nB = (D & 8192u) ? (r > 0 ? tT : nBe) : tB;
+        const int nC0 = (nA >= 0 && nB >= 0) ? (nA + nB + 1) >> 1 : max(max(nA, nB), 0);
+        const int nC = (D >> 17) ? -1 : nC0;
+        const int tc = tc_of(mv), t1 = (int)((mv >> 13) & 3u);
+        const uint32_t ce = ctab[nC < 0 ? 3 : (nC < 2 ? 0 : (nC < 4 ? 1 : 2))][4 * tc + t1];
+        /* chroma DC: its body holds the whole block, token included */
+        const uint32_t tl = nC < 0 ? 0u : (nC >= 8 ? 6u : ce >> 8);
         uint32_t len = tl + (mv & 255u);
         if (mv & M_OVF) len = ovf_bits(PT, TB, lv[i], pc, nC);            /* rare */
         lo[i] = (uint16_t)(len | (uint32_t)(nC + 1) << 11);

@@ -82,6 +82,9 @@ constexpr uint64_t HANDOFF_TICKS = 5000000ull;
 /* k_dyn_epfix could not settle the NAL's EP positions from the candidates
  * (too many): k_dyn_epscan scans it whole; not an error for the emit */
 constexpr uint32_t DF_EPSLOW = 0x100u;
+/* the NAL's size and EP list are final (ep_fix ran; the list is sorted
+ * unless DF_EPSLOW) */
+constexpr uint32_t DF_FIXED = 0x200u;
 
 /* ---------------------------------------------------------------------- */
 /* emulation-prevention runs                                                */
@@ -1068,8 +1071,8 @@ __host__ __device__ inline size_t row_lds_bytes(int w, int mbw)
 __host__ __device__ constexpr uint32_t pc_desc(int pc)
 {
     if (pc == 16 || pc == 17) return 1u << 17;
-    int da, db, e = 0;
-    bool al, bt;
+    int da = 0, db = 0, e = 0;
+    bool al = false, bt = false;
     if (pc < 16) {
         const int bx = pc & 3, by = pc >> 2;
         al = bx == 0;
@@ -1088,6 +1091,16 @@ __host__ __device__ constexpr uint32_t pc_desc(int pc)
     return (uint32_t)(da + 32) | (al ? 1u : 0u) << 6 | (uint32_t)(db + 32) << 7 | (bt ? 1u : 0u) << 13 |
            (uint32_t)e << 14;
 }
+
+/* LDS of ep_fix: the row-group table, candidate bases, the position list
+ * (capacity lcap) and four counters */
+struct EpfLds {
+    uint32_t *goff, *gb, *gw, *cw, *cbase, *lst, *cnt;    /* goff / cbase 65, gb / gw / cw 64, cnt 4 */
+    uint32_t lcap;
+};
+__device__ inline void ep_fix(DevStream *st, DynFrame *DF, size_t nb, int s, const DynGeom &g,
+                              const uint32_t *rowstage, const uint32_t *gbits, uint8_t *eps, const EpfLds &E,
+                              int t, int NT);
 
 /* threads of a k_dyn_row workgroup: one block task each (two past 1024) */
 __host__ __device__ inline int row_threads(int w)
@@ -1228,7 +1241,7 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
                                                      unsigned long long *__restrict__ tcx, uint32_t epoch,
                                                      uint32_t *__restrict__ rowstage, uint32_t *__restrict__ gbits,
                                                      uint32_t *__restrict__ spill, uint32_t *__restrict__ ctr,
-                                                     uint64_t *__restrict__ stamps)
+                                                     uint8_t *__restrict__ eps, uint64_t *__restrict__ stamps)
 {
     __shared__ RowFixed L;
     extern __shared__ uint4 rdyn[];
@@ -1281,13 +1294,10 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
     const uint32_t ysz = (uint32_t)S->w * (uint32_t)S->h, csz = ysz / 4;
 
     /* ---- 1-2: records (levels -> CAVLC bodies) into LDS ---------------- */
-    /* phase 1 walks a slot space: luma tasks at [0, 16 w), chroma tasks from
-     * the next wave boundary cb on, so no wave runs both the luma and the
-     * chroma path (when that costs no extra pass; else cb = 16 w) */
-    const int nl = 16 * w, cba = (nl + 63) & ~63;
-    const int cb = (cba + 8 * w + T - 1) / T == (ntask + T - 1) / T ? cba : nl;
-    const int np = (cb + 8 * w + T - 1) / T;            /* tasks per thread, <= ROW_NPMAX */
-    auto task_of = [&](int v) -> int { return v < nl ? v : (v >= cb && v < cb + 8 * w ? v - cb + nl : -1); };
+    const int np = (ntask + T - 1) / T;                 /* tasks per thread, <= ROW_NPMAX */
+    /* (measured: chroma tasks from the next wave boundary, so no wave runs
+     * both paths, was no faster -- the same number of wave passes) */
+    auto task_of = [&](int v) -> int { return v < ntask ? v : -1; };
     __syncthreads();                                    /* the row table (rt) */
     ROW_CUT(0);
     if (!general) {
@@ -1566,6 +1576,7 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
     /* ---- 5: bits -> the row's own row-stage words ------------------------ */
     uint32_t *out = rowstage + nb * g.rs_frame_words + rs_group_words(g, nA, gi);
     uint32_t epc = g.rs_row_words - EPC_ROW;            /* the EP-candidate record in the slot */
+    bool lost = false;                                  /* no spill slot: the frame fails (DF_OVER) */
     if (((bits + 31u) >> 5) > epc) {
         /* the row outgrew its slot (sized for typical rows):
          * its bits go to a spill slot at the provable bound; the slot's
@@ -1578,13 +1589,14 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
         /* none left, or out of the readers' reach (32-bit byte offsets from fr) */
         if (k >= g.rs_spill_cap || (uint64_t)(sp - fr) + g.rs_spill_words > 0x3fffffffull) {
             if (t == 0) atomicOr(&dfr[nb].err, DF_OVER);
-            return;
+            lost = true;
+        } else {
+            if (t == 0) out[epc] = 0x80000000u | (uint32_t)(sp - fr);
+            out = sp;
+            epc = g.rs_spill_words - EPC_ROW;
         }
-        if (t == 0) out[epc] = 0x80000000u | (uint32_t)(sp - fr);
-        out = sp;
-        epc = g.rs_spill_words - EPC_ROW;
     }
-    const uint32_t nw = min((bits + 31u) >> 5, epc);     /* provable bound: never clipped */
+    const uint32_t nw = lost ? 0u : min((bits + 31u) >> 5, epc);     /* provable bound: never clipped */
     const int npass = (int)((nw + ROW_GB - 1) / ROW_GB);
     for (int pi = 0; pi < npass; ++pi) {
         const uint32_t p0 = (uint32_t)pi * ROW_GB;
@@ -1635,7 +1647,23 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
         flush_window(L.buf, n, p0, p0 + n >= nw, out, &L.ncand, out + epc, EPC_ROW - 1, t, T);
         __syncthreads();
     }
-    if (t == 0) out[epc] = L.ncand;
+    if (t == 0 && !lost) out[epc] = L.ncand;
+    /* the NAL's last row to finish (DF.ep counts them; k_dyn_rows zeroed it)
+     * fixes its size and EP positions (ep_fix), in this workgroup's now dead
+     * LDS: the static groups came before (k_dyn_static), every row's words
+     * and bit count are released before its count */
+    __syncthreads();
+    if (t == 0) {
+        __threadfence();
+        L.spill = atomicAdd(&dfr[nb].ep, 1u) == (uint32_t)(R.h - 1) ? 1u : 0u;
+    }
+    __syncthreads();
+    if (L.spill) {
+        __threadfence();
+        const EpfLds E{L.buf, L.buf + 65, L.buf + 129, L.buf + 193, L.buf + 257, reinterpret_cast<uint32_t *>(rdyn),
+                       L.buf + 322, (uint32_t)(row_lds_bytes(w, mbw) / 4)};
+        ep_fix(st, dfr + nb, nb, s, g, rowstage, gbits, eps, E, t, T);
+    }
     if (stamps && t == 0) {
         stv[5] = __builtin_amdgcn_s_memrealtime();
         uint64_t *o = stamps + (((size_t)s * gridDim.y + f) * ng + gi) * 8;
@@ -2029,10 +2057,11 @@ constexpr int EPF_T = 256;
 constexpr int EPF_LIST = 4096;
 
 /* the RBSP bytes from byte B on, with the zero run before it: EP positions
- * -> lst (count nlst) until the first non-zero byte at or after byte Bend */
+ * -> lst (count nlst, capacity lcap) until the first non-zero byte at or
+ * after byte Bend */
 __device__ inline void ep_eval_bytes(uint32_t B, uint32_t Bend, uint32_t nin, int ng, uint32_t T,
                                      const uint32_t *goff, const uint32_t *gb, const uint32_t *gw,
-                                     const uint32_t *fr, uint32_t *lst, uint32_t *nlst)
+                                     const uint32_t *fr, uint32_t *lst, uint32_t *nlst, uint32_t lcap)
 {
     uint32_t cw = 0, ci = 0xffffffffu;                  /* one RBSP word cached */
     auto byte_at = [&](uint32_t i) -> uint32_t {
@@ -2051,7 +2080,7 @@ __device__ inline void ep_eval_bytes(uint32_t B, uint32_t Bend, uint32_t nin, in
         const uint32_t b = byte_at(i);
         if (ep_insert(b, k)) {
             const uint32_t q = atomicAdd(nlst, 1u);
-            if (q < (uint32_t)EPF_LIST) lst[q] = i;
+            if (q < lcap) lst[q] = i;
         }
         if (b == 0) {
             ++k;
@@ -2062,28 +2091,29 @@ __device__ inline void ep_eval_bytes(uint32_t B, uint32_t Bend, uint32_t nin, in
     }
 }
 
-/* grid (frames, streams) */
-__global__ __launch_bounds__(EPF_T) void k_dyn_epfix(DevStream *__restrict__ st, DynFrame *__restrict__ dfr,
-                                                     int ld_fr, DynGeom g, const uint32_t *__restrict__ rowstage,
-                                                     const uint32_t *__restrict__ gbits, uint8_t *__restrict__ eps)
+
+/* k_dyn_epfix's work for NAL nb (stream s), every thread of the workgroup
+ * (NT of them) calling: size, EP positions sorted and each once into the
+ * frame's EP list (EPLIST_MAX kept), DF_FIXED set.  Run by the last row
+ * workgroup of the NAL to finish (k_dyn_row), or by k_dyn_epfix for the
+ * frames no row workgroup finished. */
+__device__ inline void ep_fix(DevStream *st, DynFrame *DF, size_t nb, int s, const DynGeom &g,
+                              const uint32_t *rowstage, const uint32_t *gbits, uint8_t *eps, const EpfLds &E,
+                              int t, int NT)
 {
-    __shared__ uint32_t goff[65], gb[64], gw[64], cw[64];
-    __shared__ uint32_t cbase[65];                      /* runs before group g */
-    __shared__ uint32_t lst[EPF_LIST];
-    __shared__ uint32_t nlst, nu, slow, bad;
-    const int f = blockIdx.x, s = blockIdx.y, t = threadIdx.x;
-    const size_t nb = (size_t)s * ld_fr + f;
-    DynFrame *DF = dfr + nb;
-    if (DF->nal < 0) return;
+    uint32_t *goff = E.goff, *gb = E.gb, *gw = E.gw, *cw = E.cw, *cbase = E.cbase, *lst = E.lst;
+    uint32_t &nlst = E.cnt[0], &nu = E.cnt[1], &slow = E.cnt[2], &bad = E.cnt[3];
     if (t == 0) bad = 0u;
     __syncthreads();
-    if (DF->err & (DF_OVER | DF_HANDOFF)) {             /* k_dyn_rows / k_dyn_row: pools exhausted,
+    const uint32_t err0 = DF->err;
+    if (err0 & (DF_OVER | DF_HANDOFF)) {                /* k_dyn_rows / k_dyn_row: pools exhausted,
                                                            or a row's wait expired */
         if (t == 0) {
             DF->rbsp_bytes = 0;
             DF->ep = 0;
+            DF->err = err0 | DF_FIXED;
             atomicOr((unsigned int *)&st[s].err,
-                     (DF->err & DF_HANDOFF) ? SCROLL_DEVERR_HANDOFF : SCROLL_DEVERR_DYN);
+                     (err0 & DF_HANDOFF) ? SCROLL_DEVERR_HANDOFF : SCROLL_DEVERR_DYN);
         }
         return;
     }
@@ -2095,7 +2125,7 @@ __global__ __launch_bounds__(EPF_T) void k_dyn_epfix(DevStream *__restrict__ st,
     __syncthreads();
     if (bad) {                                          /* a spill record outside the pool (never) */
         if (t == 0) {
-            DF->err = DF_OVER;
+            DF->err = DF_OVER | DF_FIXED;
             DF->rbsp_bytes = 0;
             DF->ep = 0;
             atomicOr((unsigned int *)&st[s].err, SCROLL_DEVERR_DYN);
@@ -2121,18 +2151,19 @@ __global__ __launch_bounds__(EPF_T) void k_dyn_epfix(DevStream *__restrict__ st,
     const uint32_t nin = (T + 7) >> 3;                  /* bitwriter.c:103-111 */
     if (((nin + 31u) & ~31u) > g.slot_bytes - DYN_OVF_BYTES) {   /* the cap the API sets */
         if (t == 0) {
-            DF->err = DF_OVER;
+            DF->err = DF_OVER | DF_FIXED;
             DF->rbsp_bytes = 0;
             DF->ep = 0;
             atomicOr((unsigned int *)&st[s].err, SCROLL_DEVERR_DYN);
         }
         return;
     }
+    const uint32_t lcap = E.lcap;
     const uint32_t nseam = (uint32_t)ng, nwork = slow ? 0u : nseam + cbase[ng];
-    for (uint32_t wk = (uint32_t)t; wk < nwork; wk += EPF_T) {
+    for (uint32_t wk = (uint32_t)t; wk < nwork; wk += (uint32_t)NT) {
         if (wk < nseam) {                               /* the seam before group wk (0: NAL start) */
             const uint32_t S = goff[wk];
-            if (S < T) ep_eval_bytes(S >> 3, (S + 7) >> 3, nin, ng, T, goff, gb, gw, fr, lst, &nlst);
+            if (S < T) ep_eval_bytes(S >> 3, (S + 7) >> 3, nin, ng, T, goff, gb, gw, fr, lst, &nlst, lcap);
             continue;
         }
         const uint32_t ci = wk - nseam;
@@ -2161,36 +2192,66 @@ __global__ __launch_bounds__(EPF_T) void k_dyn_epfix(DevStream *__restrict__ st,
                     }
                 }
             }
-            const uint32_t A = (O + 32u * wi + a + 7u) & ~7u, E = O + e;
-            for (uint32_t j = A + 16u; j + 6u <= E; j += 16u) {
+            const uint32_t A = (O + 32u * wi + a + 7u) & ~7u, E2 = O + e;
+            for (uint32_t j = A + 16u; j + 6u <= E2; j += 16u) {
                 const uint32_t q = atomicAdd(&nlst, 1u);
-                if (q < (uint32_t)EPF_LIST) lst[q] = j >> 3;
+                if (q < lcap) lst[q] = j >> 3;
             }
         }
     }
     __syncthreads();
     const uint32_t n = nlst;
-    if (slow || n > (uint32_t)EPF_LIST) {
+    if (slow || n > lcap) {
         if (t == 0) {
-            DF->err = DF_EPSLOW;                        /* k_dyn_epscan finds them */
+            DF->err = DF_EPSLOW | DF_FIXED;             /* k_dyn_epscan finds them */
             DF->rbsp_bytes = nin;
             DF->ep = 0;
         }
         return;
     }
-    uint32_t *eplist = reinterpret_cast<uint32_t *>(eps + nb * DYN_OVF_BYTES);
-    for (uint32_t i = (uint32_t)t; i < n; i += EPF_T) {  /* each position once */
-        const uint32_t v = lst[i];
+    /* each position once, in increasing order (k_dyn_emit_gather needs no
+     * sort): a repeat is flagged in bit 31, then each first occurrence
+     * goes to its rank among the first occurrences */
+    for (uint32_t i = (uint32_t)t; i < n; i += (uint32_t)NT) {
+        const uint32_t v = lst[i] & 0x7fffffffu;
         bool dup = false;
-        for (uint32_t j = 0; j < i; ++j) dup |= lst[j] == v;
-        if (!dup) eplist[atomicAdd(&nu, 1u)] = v;
+        for (uint32_t j = 0; j < i; ++j) dup |= (lst[j] & 0x7fffffffu) == v;
+        if (dup) atomicOr(&lst[i], 0x80000000u);
+    }
+    __syncthreads();
+    uint32_t *eplist = reinterpret_cast<uint32_t *>(eps + nb * DYN_OVF_BYTES);
+    for (uint32_t i = (uint32_t)t; i < n; i += (uint32_t)NT) {
+        const uint32_t v = lst[i];
+        if (v & 0x80000000u) continue;
+        uint32_t r = 0;
+        for (uint32_t j = 0; j < n; ++j) r += lst[j] < v ? 1u : 0u;     /* repeats (bit 31) never count */
+        if (r < (uint32_t)EPLIST_MAX) eplist[r] = v;
+        atomicAdd(&nu, 1u);
     }
     __syncthreads();
     if (t == 0) {
-        DF->err = 0;                                    /* clears DF_GENERAL */
+        DF->err = DF_FIXED;                             /* clears DF_GENERAL */
         DF->rbsp_bytes = nin;
         DF->ep = nu;
     }
+}
+
+/* grid (frames, streams): the frames k_dyn_row did not finish (DF_FIXED
+ * clear: every row returned early) */
+__global__ __launch_bounds__(EPF_T) void k_dyn_epfix(DevStream *__restrict__ st, DynFrame *__restrict__ dfr,
+                                                     int ld_fr, DynGeom g, const uint32_t *__restrict__ rowstage,
+                                                     const uint32_t *__restrict__ gbits, uint8_t *__restrict__ eps)
+{
+    __shared__ uint32_t goff[65], gb[64], gw[64], cw[64];
+    __shared__ uint32_t cbase[65];                      /* runs before group g */
+    __shared__ uint32_t lst[EPF_LIST];
+    __shared__ uint32_t cnt[4];
+    const int f = blockIdx.x, s = blockIdx.y, t = threadIdx.x;
+    const size_t nb = (size_t)s * ld_fr + f;
+    DynFrame *DF = dfr + nb;
+    if (DF->nal < 0 || (DF->err & DF_FIXED)) return;
+    const EpfLds E{goff, gb, gw, cw, cbase, lst, cnt, (uint32_t)EPF_LIST};
+    ep_fix(st, DF, nb, s, g, rowstage, gbits, eps, E, t, EPF_T);
 }
 
 /* ---------------------------------------------------------------------- */
@@ -2224,7 +2285,7 @@ __global__ __launch_bounds__(DT) void k_dyn_emit(const DevStream *__restrict__ s
     const size_t nb = (size_t)s * ld_fr + f;
     const DynFrame df = dfr[nb];
     const int j = df.nal;
-    if (j < 0 || j >= st[s].nnal || (df.err & ~DF_EPSLOW)) return;   /* nnal = 0: nothing committed */
+    if (j < 0 || j >= st[s].nnal || (df.err & ~(DF_EPSLOW | DF_FIXED))) return;   /* nnal = 0: nothing committed */
     if (df.ep <= ep_cap(g)) return;                          /* k_dyn_emit_gather's NAL */
     const NalDesc d = nal[(size_t)s * ld_nal + j];
     if (d.slow != 2) return;
@@ -2345,7 +2406,7 @@ __global__ __launch_bounds__(DT) void k_dyn_emit_gather(const DevStream *__restr
     if (stp) stp[0] = __builtin_amdgcn_s_memrealtime();
     const DynFrame df = dfr[(size_t)s * ld_fr + f];
     const int j = df.nal;
-    if (j < 0 || j >= st[s].nnal || (df.err & ~DF_EPSLOW)) return;   /* nnal = 0: nothing committed */
+    if (j < 0 || j >= st[s].nnal || (df.err & ~(DF_EPSLOW | DF_FIXED))) return;   /* nnal = 0: nothing committed */
     const uint32_t n = df.ep;
     if (n > ep_cap(g)) return;                               /* k_dyn_emit's NAL */
     const NalDesc d = nal[(size_t)s * ld_nal + j];
@@ -2356,7 +2417,9 @@ __global__ __launch_bounds__(DT) void k_dyn_emit_gather(const DevStream *__restr
                                                                : in + g.slot_bytes - DYN_OVF_BYTES);
     const uint32_t *fr = RS ? rowstage + nb * g.rs_frame_words : nullptr;
     if (RS) rs_table(gbits, nb, g, fr, goff, gb, gw, nullptr, t);
-    for (uint32_t i = t; i < n; i += DT) raw[i] = el[i];
+    /* ep_fix leaves the list sorted (not k_dyn_epscan, nor the hint / splice path) */
+    const bool sorted = RS && !(df.err & DF_EPSLOW);
+    for (uint32_t i = t; i < n; i += DT) (sorted ? sp : raw)[i] = el[i];
     __syncthreads();
     const int ng = RS ? g.ngroups : 0;
     const uint32_t T = RS ? goff[ng] : 0u;
@@ -2364,7 +2427,7 @@ __global__ __launch_bounds__(DT) void k_dyn_emit_gather(const DevStream *__restr
     const __amdgpu_buffer_rsrc_t rr = buf_rsrc(fr, RS ? 0xfffffffcu : 0u);
     int gcar = 0;                                            /* RS: the thread's row group */
     /* sort by rank (positions are distinct): sp[j] = j-th smallest */
-    for (uint32_t i = t; i < n; i += DT) {
+    for (uint32_t i = t; i < (sorted ? 0u : n); i += DT) {
         const uint32_t v = raw[i];
         uint32_t r = 0;
         for (uint32_t k = 0; k < n; ++k) r += raw[k] < v ? 1u : 0u;
@@ -2567,7 +2630,7 @@ __global__ __launch_bounds__(256) void k_dyn_synth(uint8_t *__restrict__ src, Dy
 int dyn_launch_code(hipStream_t hs, int nframes, int S, DevStream *st, const NalDesc *nal,
                     int ld_nal, const PlanPending *pend, DynFrame *dfr, int ld_fr,
                     const DynGeom *g, const uint8_t *src, const uint8_t *refs, const DynScratch *x,
-                    uint32_t epoch, int mbw, uint64_t *stamps)
+                    uint8_t *eps, uint32_t epoch, int mbw, uint64_t *stamps)
 {
     if (nframes <= 0 || S <= 0) return 0;
     {                                   /* the tzrb table, once per device (and process) */
@@ -2589,17 +2652,21 @@ int dyn_launch_code(hipStream_t hs, int nframes, int S, DevStream *st, const Nal
     hipLaunchKernelGGL(k_dyn_code_general, dim3(nchunk, CODE_GEN_Y), dim3(CODE_T), 0, hs, st, dfr, ld_fr,
                        pend, nal, ld_nal, *g, x->rows, src, refs, x->meta, x->body_lo, x->body_hi, nframes, S);
     if (hipGetLastError() != hipSuccess) return -1;
+    /* the static row groups first: the last row of each NAL places them (ep_fix) */
+    hipLaunchKernelGGL(k_dyn_static, dim3(g->ngroups - g->h, nframes, S), dim3(GW), 0, hs, st, nal, ld_nal,
+                       pend, dfr, ld_fr, *g, x->rowstage, x->gbits);
+    if (hipGetLastError() != hipSuccess) return -1;
     hipLaunchKernelGGL(k_dyn_row<false>, dim3(g->h, nframes, S), dim3(row_threads(g->w)),
                        row_lds_bytes(g->w, mbw), hs, st, nal, ld_nal, pend, dfr, ld_fr, *g, x->rows, src, refs,
                        x->meta, x->body_lo, x->body_hi, x->tcx, epoch, x->rowstage, x->gbits, x->spill, x->ctr,
-                       stamps);
+                       eps, stamps);
     if (hipGetLastError() != hipSuccess) return -1;
     /* the general path: one row workgroup per record slot that may be taken */
     hipLaunchKernelGGL(k_dyn_row<true>, dim3(g->h, std::min<uint32_t>(g->gen_cap, (uint32_t)(nframes * S)), 1),
                        dim3(row_threads(g->w)),
                        row_lds_bytes(g->w, mbw), hs, st, nal, ld_nal, pend, dfr, ld_fr, *g, x->rows, src, refs,
                        x->meta, x->body_lo, x->body_hi, x->tcx, epoch, x->rowstage, x->gbits, x->spill, x->ctr,
-                       stamps);
+                       eps, stamps);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -2609,9 +2676,9 @@ int dyn_launch_pack(hipStream_t hs, int nframes, int S, DevStream *st, const Nal
 {
     (void)stamps;
     if (nframes <= 0 || S <= 0) return 0;
-    hipLaunchKernelGGL(k_dyn_static, dim3(g->ngroups - g->h, nframes, S), dim3(GW), 0, hs, st, nal, ld_nal,
-                       pend, dfr, ld_fr, *g, x->rowstage, x->gbits);
-    if (hipGetLastError() != hipSuccess) return -1;
+    (void)nal;
+    (void)ld_nal;
+    (void)pend;
     hipLaunchKernelGGL(k_dyn_epfix, dim3(nframes, S), dim3(EPF_T), 0, hs, st, dfr, ld_fr, *g, x->rowstage,
                        x->gbits, eps);
     if (hipGetLastError() != hipSuccess) return -1;

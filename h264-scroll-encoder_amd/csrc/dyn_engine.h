@@ -27,15 +27,13 @@ typedef struct {
 } DynScratch;
 
 /* k_dyn_rows + k_dyn_code_general (records of the general-path NALs) +
- * k_dyn_static (the static row groups) + k_dyn_row (every rect row: block
- * coding + packing -> its row-stage bits; the NAL's last row to finish fixes
- * its size and EP list, eps = the frames' EP lists) */
+ * k_dyn_row (every rect row: block coding + packing -> its row-stage bits) */
 int dyn_launch_code(hipStream_t hs, int nframes, int S, DevStream *st, const NalDesc *nal,
                     int ld_nal, const PlanPending *pend, DynFrame *dfr, int ld_fr,
                     const DynGeom *g, const uint8_t *src, const uint8_t *refs, const DynScratch *x,
-                    uint8_t *eps, uint32_t epoch, int mbw, uint64_t *stamps);
-/* k_dyn_epfix (the frames no row workgroup fixed: ep_fix) + k_dyn_epscan (the
- * NALs ep_fix flags): RBSP sizes and EP positions (eps: DYN_OVF_BYTES per
+                    uint32_t epoch, int mbw, uint64_t *stamps);
+/* k_dyn_static (static row groups) + k_dyn_epfix (+ k_dyn_epscan for the
+ * NALs it flags): RBSP sizes and sorted EP positions (eps: DYN_OVF_BYTES per
  * frame) straight from the row groups */
 int dyn_launch_pack(hipStream_t hs, int nframes, int S, DevStream *st, const NalDesc *nal,
                     int ld_nal, const PlanPending *pend, DynFrame *dfr, int ld_fr,

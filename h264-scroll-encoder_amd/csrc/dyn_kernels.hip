@@ -1098,10 +1098,6 @@ struct EpfLds {
     uint32_t *goff, *gb, *gw, *cw, *cbase, *lst, *cnt;    /* goff / cbase 65, gb / gw / cw 64, cnt 4 */
     uint32_t lcap;
 };
-__device__ inline void ep_fix(DevStream *st, DynFrame *DF, size_t nb, int s, const DynGeom &g,
-                              const uint32_t *rowstage, const uint32_t *gbits, uint8_t *eps, const EpfLds &E,
-                              int t, int NT);
-
 /* threads of a k_dyn_row workgroup: one block task each (two past 1024) */
 __host__ __device__ inline int row_threads(int w)
 {
@@ -1241,7 +1237,7 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
                                                      unsigned long long *__restrict__ tcx, uint32_t epoch,
                                                      uint32_t *__restrict__ rowstage, uint32_t *__restrict__ gbits,
                                                      uint32_t *__restrict__ spill, uint32_t *__restrict__ ctr,
-                                                     uint8_t *__restrict__ eps, uint64_t *__restrict__ stamps)
+                                                     uint64_t *__restrict__ stamps)
 {
     __shared__ RowFixed L;
     extern __shared__ uint4 rdyn[];
@@ -1648,22 +1644,6 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
         __syncthreads();
     }
     if (t == 0 && !lost) out[epc] = L.ncand;
-    /* the NAL's last row to finish (DF.ep counts them; k_dyn_rows zeroed it)
-     * fixes its size and EP positions (ep_fix), in this workgroup's now dead
-     * LDS: the static groups came before (k_dyn_static), every row's words
-     * and bit count are released before its count */
-    __syncthreads();
-    if (t == 0) {
-        __threadfence();
-        L.spill = atomicAdd(&dfr[nb].ep, 1u) == (uint32_t)(R.h - 1) ? 1u : 0u;
-    }
-    __syncthreads();
-    if (L.spill) {
-        __threadfence();
-        const EpfLds E{L.buf, L.buf + 65, L.buf + 129, L.buf + 193, L.buf + 257, reinterpret_cast<uint32_t *>(rdyn),
-                       L.buf + 322, (uint32_t)(row_lds_bytes(w, mbw) / 4)};
-        ep_fix(st, dfr + nb, nb, s, g, rowstage, gbits, eps, E, t, T);
-    }
     if (stamps && t == 0) {
         stv[5] = __builtin_amdgcn_s_memrealtime();
         uint64_t *o = stamps + (((size_t)s * gridDim.y + f) * ng + gi) * 8;
@@ -2094,9 +2074,10 @@ __device__ inline void ep_eval_bytes(uint32_t B, uint32_t Bend, uint32_t nin, in
 
 /* k_dyn_epfix's work for NAL nb (stream s), every thread of the workgroup
  * (NT of them) calling: size, EP positions sorted and each once into the
- * frame's EP list (EPLIST_MAX kept), DF_FIXED set.  Run by the last row
- * workgroup of the NAL to finish (k_dyn_row), or by k_dyn_epfix for the
- * frames no row workgroup finished. */
+ * frame's EP list (EPLIST_MAX kept), DF_FIXED set.  (Measured in round 4:
+ * run by each NAL's last row workgroup inside k_dyn_row instead, the
+ * agent-scope release fence every row workgroup then needs -- L2 write-back
+ * across the XCDs -- made k_dyn_row 9.6 ms.) */
 __device__ inline void ep_fix(DevStream *st, DynFrame *DF, size_t nb, int s, const DynGeom &g,
                               const uint32_t *rowstage, const uint32_t *gbits, uint8_t *eps, const EpfLds &E,
                               int t, int NT)
@@ -2236,8 +2217,7 @@ __device__ inline void ep_fix(DevStream *st, DynFrame *DF, size_t nb, int s, con
     }
 }
 
-/* grid (frames, streams): the frames k_dyn_row did not finish (DF_FIXED
- * clear: every row returned early) */
+/* grid (frames, streams) */
 __global__ __launch_bounds__(EPF_T) void k_dyn_epfix(DevStream *__restrict__ st, DynFrame *__restrict__ dfr,
                                                      int ld_fr, DynGeom g, const uint32_t *__restrict__ rowstage,
                                                      const uint32_t *__restrict__ gbits, uint8_t *__restrict__ eps)
@@ -2582,6 +2562,197 @@ __global__ __launch_bounds__(DT) void k_dyn_emit_gather(const DevStream *__restr
 }
 
 /* ---------------------------------------------------------------------- */
+/* k_dyn_gather: the dynamic rect's NALs -> arena, one chunk per thread on  */
+/* one straight path                                                        */
+/* ---------------------------------------------------------------------- */
+/* Round 4's replacement of k_dyn_emit_gather<., true> (≈440 VALU
+ * instructions per 16-byte chunk there, in 64-bit index arithmetic, pick
+ * trees and per-case branches).  Per 16-byte arena chunk inside the NAL:
+ *   K  = EP bytes before it (coarse index per 2^cs EBSP bytes + a short
+ *        step over the sorted positions); its first RBSP byte i0 = u0 - K;
+ *   R  = the 128 RBSP bits from byte i0: five row-stage words of the group
+ *        holding them funnel-shifted by the bit phase, merged at a group
+ *        seam with the next group's first four words (a 128-bit shift and
+ *        mask, computed by every lane: no branch);
+ *   each EP byte inside the chunk (sorted list, usually none): the tail
+ *   shifts right one byte and 03 goes in;
+ *   R byte-swapped -> one 16-byte store.
+ * Chunks at the NAL's ends (start code, header, the last partial chunk) and
+ * chunks meeting three groups (groups under 128 bits: tiny rects) take a
+ * byte loop.  Grid (frames, streams, Z): workgroup z owns 1/Z of the NAL's
+ * chunks. */
+#ifndef SCROLL_GATHER2_Z
+#define SCROLL_GATHER2_Z 1
+#endif
+
+/* 128-bit helpers on four words, word 0 most significant */
+struct W4 {
+    uint32_t w[4];
+};
+/* x >> s (logical), 0 <= s < 128 */
+__device__ inline W4 shr128(const W4 &x, uint32_t s)
+{
+    const uint32_t q = s >> 5, r = s & 31u;
+    uint32_t a[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        /* word k of the result: words k - q (hi part) and k - q - 1 */
+        const int i = k - (int)q;
+        const uint32_t hi = i >= 0 ? (i == 0 ? x.w[0] : (i == 1 ? x.w[1] : (i == 2 ? x.w[2] : x.w[3]))) : 0u;
+        const int j = i - 1;
+        const uint32_t lo = j >= 0 ? (j == 0 ? x.w[0] : (j == 1 ? x.w[1] : x.w[2])) : 0u;
+        a[k] = r ? __builtin_amdgcn_alignbit(lo, hi, r) : hi;
+    }
+    return W4{{a[0], a[1], a[2], a[3]}};
+}
+
+__global__ __launch_bounds__(DT) void k_dyn_gather(const DevStream *__restrict__ st,
+                                                  const NalDesc *__restrict__ nal, int ld_nal,
+                                                  const DynFrame *__restrict__ dfr, int ld_fr, DynGeom g,
+                                                  const uint8_t *__restrict__ eps,
+                                                  const uint32_t *__restrict__ rowstage,
+                                                  const uint32_t *__restrict__ gbits,
+                                                  uint8_t *__restrict__ arena, uint64_t ld_arena)
+{
+    __shared__ uint32_t raw[EPLIST_MAX], sp[EPLIST_MAX + 1];
+    __shared__ uint32_t goff[65], gb[64], gw[64];
+    const int s = blockIdx.y, f = dyn_frame_of(blockIdx.x, s), t = threadIdx.x;
+    const DynFrame df = dfr[(size_t)s * ld_fr + f];
+    const int j = df.nal;
+    if (j < 0 || j >= st[s].nnal || (df.err & ~(DF_EPSLOW | DF_FIXED))) return;   /* nnal = 0: nothing committed */
+    const uint32_t n = df.ep;
+    if (n > ep_cap(g)) return;                               /* k_dyn_emit's NAL */
+    const NalDesc d = nal[(size_t)s * ld_nal + j];
+    if (d.slow != 2) return;
+    const size_t nb = (size_t)s * ld_fr + f;
+    const uint32_t *el = reinterpret_cast<const uint32_t *>(eps + nb * DYN_OVF_BYTES);
+    const uint32_t *fr = rowstage + nb * g.rs_frame_words;
+    rs_table(gbits, nb, g, fr, goff, gb, gw, nullptr, t);
+    const bool sorted = !(df.err & DF_EPSLOW);
+    for (uint32_t i = t; i < n; i += DT) (sorted ? sp : raw)[i] = el[i];
+    if (t == 0) sp[n] = 0x7fffffffu;                         /* sentinel: never before a chunk */
+    __syncthreads();
+    for (uint32_t i = t; i < (sorted ? 0u : n); i += DT) {   /* k_dyn_epscan's lists: by rank */
+        const uint32_t v = raw[i];
+        uint32_t r = 0;
+        for (uint32_t k = 0; k < n; ++k) r += raw[k] < v ? 1u : 0u;
+        sp[r] = v;
+    }
+    __syncthreads();
+    const int ng = g.ngroups;
+    const uint32_t T = goff[ng];
+    const __amdgpu_buffer_rsrc_t rr = buf_rsrc(fr, 0xfffffffcu);   /* the frame's groups + spill slots */
+    uint8_t *A = arena + (size_t)s * ld_arena;
+    const uint64_t o0 = d.out_off, o1 = o0 + d.size;
+    /* coarse index: raw[b] = EP bytes before EBSP index b << cs (the j-th EP
+     * byte sits at EBSP index sp[j] + j, strictly increasing) */
+    int lg = 0;
+    while ((1u << lg) <= n) lg++;
+    int cs = 8;
+    while ((d.size >> cs) >= (uint32_t)EPLIST_MAX) cs++;
+    const int nblk = (int)(d.size >> cs) + 1;
+    for (int bi = t; bi < nblk; bi += DT) {
+        const uint32_t e0 = (uint32_t)bi << cs;
+        uint32_t K = 0;
+        for (int b = lg - 1; b >= 0; --b) {
+            const uint32_t k2 = K + (1u << b);
+            K = k2 <= n && sp[k2 - 1] + (k2 - 1) < e0 ? k2 : K;
+        }
+        raw[bi] = K;
+    }
+    __syncthreads();
+    const uint8_t hdr[5] = {0, 0, 0, 1, nal_header_byte(0)};           /* nal.c:59-64 */
+    const uint64_t cfirst = o0 >> 4;
+    const uint32_t cnal = (uint32_t)(((o1 + 15) >> 4) - cfirst);
+    const uint32_t per = (cnal + gridDim.z - 1) / gridDim.z;
+    const uint32_t cbeg = per * blockIdx.z, cend = min(cnal, cbeg + per);
+    /* EBSP index of chunk c's byte 0: 16 c - d0 (d0 = o0 - 16 cfirst + 5) */
+    const int32_t d0 = (int32_t)(o0 - (cfirst << 4)) + 5;
+    const int32_t nebsp = (int32_t)(d.size - 5);
+    int gg = 0;                                              /* the thread's group, carried */
+    for (uint32_t c = cbeg + (uint32_t)t; c < cend; c += DT) {
+        const int32_t u0 = 16 * (int32_t)c - d0;
+        uint8_t *q = A + ((cfirst + c) << 4);
+        uint32_t K = raw[u0 > 0 ? min(u0 >> cs, nblk - 1) : 0];
+        if (u0 >= 0 && u0 + 16 <= nebsp) {
+            while ((int32_t)(sp[K] + K) < u0) K++;               /* sentinel stops it */
+            const uint32_t i0 = (uint32_t)u0 - K, P = 8u * i0;
+            while (gg + 1 < ng && goff[gg + 1] <= P) ++gg;
+            while (gg > 0 && goff[gg] > P) --gg;                 /* never for increasing P */
+            const uint32_t lp = P - goff[gg], rem = gb[gg] - lp;  /* bits left in the group */
+            const bool two = rem < 128u;
+            if (!two || gg + 1 >= ng || gb[gg + 1] >= 128u - rem) {
+                /* 160 bits of the group from word lp >> 5 */
+                const uint32_t wo = 4u * (gw[gg] + (lp >> 5));
+                const auto xa = __builtin_amdgcn_raw_buffer_load_b128(rr, wo, 0, 0);
+                const uint32_t x4 = __builtin_amdgcn_raw_buffer_load_b32(rr, wo + 16u, 0, 0);
+                uint32_t yb[4] = {0u, 0u, 0u, 0u};
+                if (two && gg + 1 < ng) {
+                    const auto y = __builtin_amdgcn_raw_buffer_load_b128(rr, 4u * gw[gg + 1], 0, 0);
+                    yb[0] = (uint32_t)y[0]; yb[1] = (uint32_t)y[1]; yb[2] = (uint32_t)y[2]; yb[3] = (uint32_t)y[3];
+                }
+                const uint32_t x[5] = {(uint32_t)xa[0], (uint32_t)xa[1], (uint32_t)xa[2], (uint32_t)xa[3], x4};
+                const uint32_t sh = lp & 31u;
+                W4 R;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) R.w[k] = sh ? __builtin_amdgcn_alignbit(x[k], x[k + 1], 32u - sh) : x[k];
+                if (two) {                                       /* rem bits of this group, then the next */
+                    const W4 B = shr128(W4{{yb[0], yb[1], yb[2], yb[3]}}, rem);
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        const uint32_t kb = 32u * (uint32_t)k;  /* bits of word k kept from this group */
+                        const uint32_t keep = rem <= kb ? 0u : (rem >= kb + 32u ? 32u : rem - kb);
+                        const uint32_t m = keep == 0u ? 0u : (keep == 32u ? 0xffffffffu : ~(0xffffffffu >> keep));
+                        R.w[k] = (R.w[k] & m) | B.w[k];
+                    }
+                }
+                /* the EP bytes inside the chunk: byte e becomes 03, the
+                 * bytes from e on move one byte later */
+                for (uint32_t m = K;; ++m) {
+                    const int32_t e = (int32_t)(sp[m] + m) - u0;
+                    if (e >= 16) break;
+                    const W4 S = shr128(R, 8u);
+                    const uint32_t eb = 8u * (uint32_t)e;
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        const uint32_t kb = 32u * (uint32_t)k;
+                        const uint32_t keep = eb <= kb ? 0u : (eb >= kb + 32u ? 32u : eb - kb);
+                        const uint32_t mk = keep == 0u ? 0u : (keep == 32u ? 0xffffffffu : ~(0xffffffffu >> keep));
+                        /* the 03 byte: bits [eb, eb + 8) */
+                        const uint32_t three = (eb >= kb && eb < kb + 32u) ? (3u << (24u - (eb - kb))) : 0u;
+                        const uint32_t mk2 = (eb >= kb && eb < kb + 32u) ? (0xff000000u >> (eb - kb)) : 0u;
+                        R.w[k] = (R.w[k] & mk) | (S.w[k] & ~mk & ~mk2) | three;
+                    }
+                }
+                *reinterpret_cast<uint4 *>(q) = make_uint4(__builtin_bswap32(R.w[0]), __builtin_bswap32(R.w[1]),
+                                                           __builtin_bswap32(R.w[2]), __builtin_bswap32(R.w[3]));
+                continue;
+            }
+        }
+        /* NAL edges and three-group chunks: byte by byte */
+        for (int b = 0; b < 16; ++b) {
+            const uint64_t qa = ((cfirst + c) << 4) + (uint64_t)b;
+            if (qa < o0 || qa >= o1) continue;
+            const int32_t uu = (int32_t)(qa - o0) - 5;
+            uint8_t v;
+            if (uu < 0) {
+                v = hdr[qa - o0];
+            } else {
+                while ((int32_t)(sp[K] + K) < uu) K++;
+                if ((int32_t)(sp[K] + K) == uu) {
+                    v = 3;
+                } else {
+                    const uint32_t ri = (uint32_t)uu - K;
+                    const uint32_t wd = rs_word(32u * (ri >> 2), ng, T, goff, gb, gw, fr);
+                    v = (uint8_t)(wd >> (8u * (3u - (ri & 3u))));
+                }
+            }
+            q[b] = v;
+        }
+    }
+}
+
+/* ---------------------------------------------------------------------- */
 /* k_dyn_synth: the synthetic dynamic-rect source of SURVEY §8d            */
 /* (dyn_oracle.h), one thread per pixel                                    */
 /* ---------------------------------------------------------------------- */
@@ -2630,7 +2801,7 @@ __global__ __launch_bounds__(256) void k_dyn_synth(uint8_t *__restrict__ src, Dy
 int dyn_launch_code(hipStream_t hs, int nframes, int S, DevStream *st, const NalDesc *nal,
                     int ld_nal, const PlanPending *pend, DynFrame *dfr, int ld_fr,
                     const DynGeom *g, const uint8_t *src, const uint8_t *refs, const DynScratch *x,
-                    uint8_t *eps, uint32_t epoch, int mbw, uint64_t *stamps)
+                    uint32_t epoch, int mbw, uint64_t *stamps)
 {
     if (nframes <= 0 || S <= 0) return 0;
     {                                   /* the tzrb table, once per device (and process) */
@@ -2652,21 +2823,17 @@ int dyn_launch_code(hipStream_t hs, int nframes, int S, DevStream *st, const Nal
     hipLaunchKernelGGL(k_dyn_code_general, dim3(nchunk, CODE_GEN_Y), dim3(CODE_T), 0, hs, st, dfr, ld_fr,
                        pend, nal, ld_nal, *g, x->rows, src, refs, x->meta, x->body_lo, x->body_hi, nframes, S);
     if (hipGetLastError() != hipSuccess) return -1;
-    /* the static row groups first: the last row of each NAL places them (ep_fix) */
-    hipLaunchKernelGGL(k_dyn_static, dim3(g->ngroups - g->h, nframes, S), dim3(GW), 0, hs, st, nal, ld_nal,
-                       pend, dfr, ld_fr, *g, x->rowstage, x->gbits);
-    if (hipGetLastError() != hipSuccess) return -1;
     hipLaunchKernelGGL(k_dyn_row<false>, dim3(g->h, nframes, S), dim3(row_threads(g->w)),
                        row_lds_bytes(g->w, mbw), hs, st, nal, ld_nal, pend, dfr, ld_fr, *g, x->rows, src, refs,
                        x->meta, x->body_lo, x->body_hi, x->tcx, epoch, x->rowstage, x->gbits, x->spill, x->ctr,
-                       eps, stamps);
+                       stamps);
     if (hipGetLastError() != hipSuccess) return -1;
     /* the general path: one row workgroup per record slot that may be taken */
     hipLaunchKernelGGL(k_dyn_row<true>, dim3(g->h, std::min<uint32_t>(g->gen_cap, (uint32_t)(nframes * S)), 1),
                        dim3(row_threads(g->w)),
                        row_lds_bytes(g->w, mbw), hs, st, nal, ld_nal, pend, dfr, ld_fr, *g, x->rows, src, refs,
                        x->meta, x->body_lo, x->body_hi, x->tcx, epoch, x->rowstage, x->gbits, x->spill, x->ctr,
-                       eps, stamps);
+                       stamps);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -2676,9 +2843,9 @@ int dyn_launch_pack(hipStream_t hs, int nframes, int S, DevStream *st, const Nal
 {
     (void)stamps;
     if (nframes <= 0 || S <= 0) return 0;
-    (void)nal;
-    (void)ld_nal;
-    (void)pend;
+    hipLaunchKernelGGL(k_dyn_static, dim3(g->ngroups - g->h, nframes, S), dim3(GW), 0, hs, st, nal, ld_nal,
+                       pend, dfr, ld_fr, *g, x->rowstage, x->gbits);
+    if (hipGetLastError() != hipSuccess) return -1;
     hipLaunchKernelGGL(k_dyn_epfix, dim3(nframes, S), dim3(EPF_T), 0, hs, st, dfr, ld_fr, *g, x->rowstage,
                        x->gbits, eps);
     if (hipGetLastError() != hipSuccess) return -1;
@@ -2700,7 +2867,10 @@ int dyn_launch_emit(hipStream_t hs, int nframes, int S, const DevStream *st, con
     const bool big = (int64_t)g->w * g->h > 1024;
     const uint32_t *rs = x ? x->rowstage : nullptr, *gbits = x ? x->gbits : nullptr;
     const dim3 grid(nframes, S, GATHER_Z);
-    if (x && big)
+    if (x && !(g->debug & SCROLL_DEBUG_DYN_GATHER1))
+        hipLaunchKernelGGL(k_dyn_gather, dim3(nframes, S, SCROLL_GATHER2_Z), dim3(DT), 0, hs, st, nal, ld_nal, dfr,
+                           ld_fr, *g, stage, rs, gbits, arena, ld_arena);
+    else if (x && big)
         hipLaunchKernelGGL((k_dyn_emit_gather<4, true>), grid, dim3(DT), 0, hs, st, nal, ld_nal, dfr, ld_fr, *g,
                            stage, rs, gbits, arena, ld_arena, stamps);
     else if (x)

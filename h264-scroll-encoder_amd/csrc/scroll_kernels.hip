@@ -1368,7 +1368,7 @@ static int launch(ScrollBatch *b, int nframes, int plan_mode, int nal_max, hipSt
                 const uint8_t *refs0 = b->d_refs + (size_t)s0 * G.ref_ld;
                 uint8_t *stage0 = b->d_stage + nb0 * DYN_OVF_BYTES;   /* EP lists only */
                 if (dyn_launch_code(hs, nframes, s1 - s0, st0, nal0, b->ld_nal, pend0, dfr0, ld_fr, &G, src0,
-                                    refs0, &xc, stage0, b->dx.epoch, b->dyn_pw / 16, stamps)) {
+                                    refs0, &xc, b->dx.epoch, b->dyn_pw / 16, stamps)) {
                     set_err("k_dyn_code launch: %s", hipGetErrorString(hipGetLastError()));
                     return SCROLL_ERR_HIP;
                 }

@@ -77,6 +77,9 @@ extern "C" {
  * bottom TotalCoeffs, so row 1's bounded wait expires: stream 0 fails with
  * SCROLL_ERR_DEVICE, every other stream composes normally */
 #define SCROLL_DEBUG_DYN_NOPUBLISH 16384
+/* tests: the dynamic rect's NALs go to the arena through the round-3 gather
+ * (k_dyn_emit_gather) instead of k_dyn_gather; output unchanged */
+#define SCROLL_DEBUG_DYN_GATHER1 32768
 
 typedef struct ScrollBatch ScrollBatch;
 

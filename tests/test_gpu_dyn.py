@@ -379,3 +379,25 @@ def test_dyn_row_handoff_wait_is_bounded(gpu, oracle):
     assert b.sync() == 0, gpu.last_error()
     assert len(b.output(0)) > 20000
     b.close()
+
+
+@pytest.mark.parametrize("geom", [((1280, 720), (28, 10, 25, 25)), ((320, 320), (0, 0, 1, 20)),
+                                  ((96, 96), (0, 0, 6, 6))])
+def test_dyn_round3_gather_still_exact(gpu, oracle, geom):
+    """SCROLL_DEBUG_DYN_GATHER1: the round-3 gather (k_dyn_emit_gather) in
+    place of k_dyn_gather gives the same bytes (config-3 geometry, a width-1
+    rect with tiny row groups, EP-dense random pixels)"""
+    (w, h), r = geom
+    rect = Rect(*r)
+    S, F = 2, 5
+    offs = synthetic_offsets(S, F, h)
+    if w == 96:
+        R = random_refs(w, h, 1)
+        src = np.random.default_rng(5).integers(0, 256, (S, F, 384 * rect.w * rect.h)).astype(np.uint8)
+    else:
+        R = striped_refs(oracle, w, h)
+        src = synth_source(oracle, S, F, rect)
+    want = oracle_streams(oracle, w, h, offs, rect, src, R)
+    b, rc = gpu_streams(gpu, w, h, offs, rect, R, src, debug=gpu.SCROLL_DEBUG_DYN_GATHER1)
+    assert rc == 0, gpu.last_error()
+    check_equal(b, want)

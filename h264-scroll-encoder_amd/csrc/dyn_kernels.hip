@@ -2031,10 +2031,9 @@ __global__ __launch_bounds__(EPS_T) void k_dyn_epscan(DevStream *__restrict__ st
  *     (closed form of nal.c:33-38, ep_insert).
  * Every other byte is preceded by a non-zero byte within fewer than 22 zero
  * bits.  A byte can be decided twice (a run's last byte at a seam): kept
- * once.  More candidates in a group than its record holds, or more than EPF_LIST
+ * once.  More candidates in a group than its record holds, or more than EPF_LIST_W
  * positions: DF_EPSLOW (k_dyn_epscan scans the NAL). */
 constexpr int EPF_T = 256;
-constexpr int EPF_LIST = 4096;
 
 /* the RBSP bytes from byte B on, with the zero run before it: EP positions
  * -> lst (count nlst, capacity lcap) until the first non-zero byte at or
@@ -2078,14 +2077,20 @@ __device__ inline void ep_eval_bytes(uint32_t B, uint32_t Bend, uint32_t nin, in
  * run by each NAL's last row workgroup inside k_dyn_row instead, the
  * agent-scope release fence every row workgroup then needs -- L2 write-back
  * across the XCDs -- made k_dyn_row 9.6 ms.) */
+template <int NT>
 __device__ inline void ep_fix(DevStream *st, DynFrame *DF, size_t nb, int s, const DynGeom &g,
                               const uint32_t *rowstage, const uint32_t *gbits, uint8_t *eps, const EpfLds &E,
-                              int t, int NT)
+                              int t)
 {
+    /* NT = 64: one wave per NAL (wave-level hand-offs), else the workgroup */
+    auto sync = [] {
+        if constexpr (NT == 64) wave_sync();
+        else __syncthreads();
+    };
     uint32_t *goff = E.goff, *gb = E.gb, *gw = E.gw, *cw = E.cw, *cbase = E.cbase, *lst = E.lst;
     uint32_t &nlst = E.cnt[0], &nu = E.cnt[1], &slow = E.cnt[2], &bad = E.cnt[3];
     if (t == 0) bad = 0u;
-    __syncthreads();
+    sync();
     const uint32_t err0 = DF->err;
     if (err0 & (DF_OVER | DF_HANDOFF)) {                /* k_dyn_rows / k_dyn_row: pools exhausted,
                                                            or a row's wait expired */
@@ -2103,7 +2108,7 @@ __device__ inline void ep_fix(DevStream *st, DynFrame *DF, size_t nb, int s, con
     const int nA = max(1, (g.y0 + SR - 1) / SR);
     const uint32_t *fr = rowstage + nb * g.rs_frame_words;
     rs_table(gbits, nb, g, fr, goff, gb, gw, cw, t, &bad);
-    __syncthreads();
+    sync();
     if (bad) {                                          /* a spill record outside the pool (never) */
         if (t == 0) {
             DF->err = DF_OVER | DF_FIXED;
@@ -2127,7 +2132,7 @@ __device__ inline void ep_fix(DevStream *st, DynFrame *DF, size_t nb, int s, con
             nu = 0;
         }
     }
-    __syncthreads();
+    sync();
     const uint32_t T = goff[ng];                        /* NAL RBSP bits incl. the stop bit */
     const uint32_t nin = (T + 7) >> 3;                  /* bitwriter.c:103-111 */
     if (((nin + 31u) & ~31u) > g.slot_bytes - DYN_OVF_BYTES) {   /* the cap the API sets */
@@ -2180,7 +2185,7 @@ __device__ inline void ep_fix(DevStream *st, DynFrame *DF, size_t nb, int s, con
             }
         }
     }
-    __syncthreads();
+    sync();
     const uint32_t n = nlst;
     if (slow || n > lcap) {
         if (t == 0) {
@@ -2199,7 +2204,7 @@ __device__ inline void ep_fix(DevStream *st, DynFrame *DF, size_t nb, int s, con
         for (uint32_t j = 0; j < i; ++j) dup |= (lst[j] & 0x7fffffffu) == v;
         if (dup) atomicOr(&lst[i], 0x80000000u);
     }
-    __syncthreads();
+    sync();
     uint32_t *eplist = reinterpret_cast<uint32_t *>(eps + nb * DYN_OVF_BYTES);
     for (uint32_t i = (uint32_t)t; i < n; i += (uint32_t)NT) {
         const uint32_t v = lst[i];
@@ -2209,7 +2214,7 @@ __device__ inline void ep_fix(DevStream *st, DynFrame *DF, size_t nb, int s, con
         if (r < (uint32_t)EPLIST_MAX) eplist[r] = v;
         atomicAdd(&nu, 1u);
     }
-    __syncthreads();
+    sync();
     if (t == 0) {
         DF->err = DF_FIXED;                             /* clears DF_GENERAL */
         DF->rbsp_bytes = nin;
@@ -2217,21 +2222,28 @@ __device__ inline void ep_fix(DevStream *st, DynFrame *DF, size_t nb, int s, con
     }
 }
 
-/* grid (frames, streams) */
+/* grid (frames / EPF_NAL, streams): one wave per NAL (its position list
+ * EPF_LIST_W long; more: DF_EPSLOW), EPF_NAL NALs per workgroup -- the work
+ * is a short latency-bound chain per NAL, so many resident NALs per CU
+ * (round 3: one 256-thread workgroup per NAL, 0.088 ms at config 3) */
+constexpr int EPF_NAL = EPF_T / 64, EPF_LIST_W = 1024;
 __global__ __launch_bounds__(EPF_T) void k_dyn_epfix(DevStream *__restrict__ st, DynFrame *__restrict__ dfr,
-                                                     int ld_fr, DynGeom g, const uint32_t *__restrict__ rowstage,
+                                                     int ld_fr, int nframes, DynGeom g,
+                                                     const uint32_t *__restrict__ rowstage,
                                                      const uint32_t *__restrict__ gbits, uint8_t *__restrict__ eps)
 {
-    __shared__ uint32_t goff[65], gb[64], gw[64], cw[64];
-    __shared__ uint32_t cbase[65];                      /* runs before group g */
-    __shared__ uint32_t lst[EPF_LIST];
-    __shared__ uint32_t cnt[4];
-    const int f = blockIdx.x, s = blockIdx.y, t = threadIdx.x;
+    __shared__ uint32_t goff[EPF_NAL][65], gb[EPF_NAL][64], gw[EPF_NAL][64], cw[EPF_NAL][64];
+    __shared__ uint32_t cbase[EPF_NAL][65];             /* runs before group g */
+    __shared__ uint32_t lst[EPF_NAL][EPF_LIST_W];
+    __shared__ uint32_t cnt[EPF_NAL][4];
+    const int wv = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6), t = threadIdx.x & 63;
+    const int f = (int)blockIdx.x * EPF_NAL + wv, s = blockIdx.y;
+    if (f >= nframes) return;
     const size_t nb = (size_t)s * ld_fr + f;
     DynFrame *DF = dfr + nb;
-    if (DF->nal < 0 || (DF->err & DF_FIXED)) return;
-    const EpfLds E{goff, gb, gw, cw, cbase, lst, cnt, (uint32_t)EPF_LIST};
-    ep_fix(st, DF, nb, s, g, rowstage, gbits, eps, E, t, EPF_T);
+    if (DF->nal < 0) return;
+    const EpfLds E{goff[wv], gb[wv], gw[wv], cw[wv], cbase[wv], lst[wv], cnt[wv], (uint32_t)EPF_LIST_W};
+    ep_fix<64>(st, DF, nb, s, g, rowstage, gbits, eps, E, t);
 }
 
 /* ---------------------------------------------------------------------- */
@@ -2846,8 +2858,8 @@ int dyn_launch_pack(hipStream_t hs, int nframes, int S, DevStream *st, const Nal
     hipLaunchKernelGGL(k_dyn_static, dim3(g->ngroups - g->h, nframes, S), dim3(GW), 0, hs, st, nal, ld_nal,
                        pend, dfr, ld_fr, *g, x->rowstage, x->gbits);
     if (hipGetLastError() != hipSuccess) return -1;
-    hipLaunchKernelGGL(k_dyn_epfix, dim3(nframes, S), dim3(EPF_T), 0, hs, st, dfr, ld_fr, *g, x->rowstage,
-                       x->gbits, eps);
+    hipLaunchKernelGGL(k_dyn_epfix, dim3((nframes + EPF_NAL - 1) / EPF_NAL, S), dim3(EPF_T), 0, hs, st, dfr, ld_fr,
+                       nframes, *g, x->rowstage, x->gbits, eps);
     if (hipGetLastError() != hipSuccess) return -1;
     hipLaunchKernelGGL(k_dyn_epscan, dim3(EPS_Z, nframes, S), dim3(EPS_T), 0, hs, st, dfr, ld_fr, *g,
                        x->rowstage, x->gbits, eps);

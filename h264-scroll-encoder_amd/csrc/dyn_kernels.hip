@@ -2642,7 +2642,7 @@ __global__ __launch_bounds__(DT) void k_dyn_gather(const DevStream *__restrict__
     rs_table(gbits, nb, g, fr, goff, gb, gw, nullptr, t);
     const bool sorted = !(df.err & DF_EPSLOW);
     for (uint32_t i = t; i < n; i += DT) (sorted ? sp : raw)[i] = el[i];
-    if (t == 0) sp[n] = 0x7fffffffu;                         /* sentinel: never before a chunk */
+    if (t == 0) sp[n] = 0x3fffffffu;                         /* sentinel: sp[n] + n never before a chunk */
     __syncthreads();
     for (uint32_t i = t; i < (sorted ? 0u : n); i += DT) {   /* k_dyn_epscan's lists: by rank */
         const uint32_t v = raw[i];

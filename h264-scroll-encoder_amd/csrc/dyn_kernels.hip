@@ -2031,7 +2031,7 @@ __global__ __launch_bounds__(EPS_T) void k_dyn_epscan(DevStream *__restrict__ st
  *     (closed form of nal.c:33-38, ep_insert).
  * Every other byte is preceded by a non-zero byte within fewer than 22 zero
  * bits.  A byte can be decided twice (a run's last byte at a seam): kept
- * once.  More candidates in a group than its record holds, or more than EPF_LIST_W
+ * once.  More candidates in a group than its record holds, or more than EPF_LIST
  * positions: DF_EPSLOW (k_dyn_epscan scans the NAL). */
 constexpr int EPF_T = 256;
 
@@ -2222,28 +2222,26 @@ __device__ inline void ep_fix(DevStream *st, DynFrame *DF, size_t nb, int s, con
     }
 }
 
-/* grid (frames / EPF_NAL, streams): one wave per NAL (its position list
- * EPF_LIST_W long; more: DF_EPSLOW), EPF_NAL NALs per workgroup -- the work
- * is a short latency-bound chain per NAL, so many resident NALs per CU
- * (round 3: one 256-thread workgroup per NAL, 0.088 ms at config 3) */
-constexpr int EPF_NAL = EPF_T / 64, EPF_LIST_W = 1024;
+/* grid (frames, streams): one workgroup per NAL.  (Measured: one wave per
+ * NAL, four NALs per workgroup, 0.138 against 0.086 ms -- each NAL's
+ * candidate and seam loops then take several passes of 64 lanes.) */
+constexpr int EPF_LIST = 4096;
 __global__ __launch_bounds__(EPF_T) void k_dyn_epfix(DevStream *__restrict__ st, DynFrame *__restrict__ dfr,
                                                      int ld_fr, int nframes, DynGeom g,
                                                      const uint32_t *__restrict__ rowstage,
                                                      const uint32_t *__restrict__ gbits, uint8_t *__restrict__ eps)
 {
-    __shared__ uint32_t goff[EPF_NAL][65], gb[EPF_NAL][64], gw[EPF_NAL][64], cw[EPF_NAL][64];
-    __shared__ uint32_t cbase[EPF_NAL][65];             /* runs before group g */
-    __shared__ uint32_t lst[EPF_NAL][EPF_LIST_W];
-    __shared__ uint32_t cnt[EPF_NAL][4];
-    const int wv = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6), t = threadIdx.x & 63;
-    const int f = (int)blockIdx.x * EPF_NAL + wv, s = blockIdx.y;
+    __shared__ uint32_t goff[65], gb[64], gw[64], cw[64];
+    __shared__ uint32_t cbase[65];                      /* runs before group g */
+    __shared__ uint32_t lst[EPF_LIST];
+    __shared__ uint32_t cnt[4];
+    const int f = blockIdx.x, s = blockIdx.y, t = threadIdx.x;
     if (f >= nframes) return;
     const size_t nb = (size_t)s * ld_fr + f;
     DynFrame *DF = dfr + nb;
     if (DF->nal < 0) return;
-    const EpfLds E{goff[wv], gb[wv], gw[wv], cw[wv], cbase[wv], lst[wv], cnt[wv], (uint32_t)EPF_LIST_W};
-    ep_fix<64>(st, DF, nb, s, g, rowstage, gbits, eps, E, t);
+    const EpfLds E{goff, gb, gw, cw, cbase, lst, cnt, (uint32_t)EPF_LIST};
+    ep_fix<EPF_T>(st, DF, nb, s, g, rowstage, gbits, eps, E, t);
 }
 
 /* ---------------------------------------------------------------------- */
@@ -2858,8 +2856,8 @@ int dyn_launch_pack(hipStream_t hs, int nframes, int S, DevStream *st, const Nal
     hipLaunchKernelGGL(k_dyn_static, dim3(g->ngroups - g->h, nframes, S), dim3(GW), 0, hs, st, nal, ld_nal,
                        pend, dfr, ld_fr, *g, x->rowstage, x->gbits);
     if (hipGetLastError() != hipSuccess) return -1;
-    hipLaunchKernelGGL(k_dyn_epfix, dim3((nframes + EPF_NAL - 1) / EPF_NAL, S), dim3(EPF_T), 0, hs, st, dfr, ld_fr,
-                       nframes, *g, x->rowstage, x->gbits, eps);
+    hipLaunchKernelGGL(k_dyn_epfix, dim3(nframes, S), dim3(EPF_T), 0, hs, st, dfr, ld_fr, nframes, *g,
+                       x->rowstage, x->gbits, eps);
     if (hipGetLastError() != hipSuccess) return -1;
     hipLaunchKernelGGL(k_dyn_epscan, dim3(EPS_Z, nframes, S), dim3(EPS_T), 0, hs, st, dfr, ld_fr, *g,
                        x->rowstage, x->gbits, eps);

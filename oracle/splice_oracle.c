@@ -257,11 +257,14 @@ static int sp_partitions(int part, int sub, sp_part *o)
     return n;
 }
 
-/* motion per 4x4 block of a picture of W MBs across (one slice: every
- * in-picture MB before the current one is available) */
+/* motion per 4x4 block of a picture of W MBs across; sid (NULL: one slice)
+ * the slice of each MB, cur the current one -- an MB of another slice is
+ * unavailable (6.4.x) */
 typedef struct {
     int W;
     or_mvi *f;
+    const int *sid;
+    int cur;
 } sp_field;
 
 static or_mvi *sp_at(const sp_field *F, int x, int y, int bx, int by)
@@ -279,6 +282,7 @@ static or_mvi sp_nb(const sp_field *F, int x, int y, int cx, int cy, unsigned do
     if (cy >= 0 && cx >= 0) return (done >> (4 * cy + cx)) & 1u ? *sp_at(F, x, y, cx, cy) : none;
     const int nx = x + (cx < 0 ? -1 : (cx >= 4 ? 1 : 0)), ny = y + (cy < 0 ? -1 : 0);
     if (nx < 0 || ny < 0 || nx >= F->W) return none;
+    if (F->sid && F->sid[(size_t)ny * F->W + nx] != F->cur) return none;
     return *sp_at(F, nx, ny, (cx + 4) & 3, (cy + 4) & 3);
 }
 
@@ -321,180 +325,449 @@ static void sp_fill(const sp_field *F, int x, int y, const sp_part *p, or_mvi v,
         }
 }
 
+/* coded_block_pattern of an Intra_4x4 MB (Table 9-4, ChromaArrayType 1) */
+static const uint8_t SP_CBP_INTRA[48] = {47, 31, 15, 0,  23, 27, 29, 30, 7,  11, 13, 14, 39, 43, 45, 46,
+                                         16, 3,  5,  10, 12, 19, 21, 26, 28, 35, 37, 42, 44, 1,  2,  4,
+                                         8,  17, 18, 20, 24, 6,  9,  22, 25, 32, 33, 34, 36, 40, 38, 41};
+
+/* the NAL units of a splice buffer: Annex-B units (00 00 01 / 00 00 00 01
+ * start codes), or the whole buffer as one NAL when it starts with none;
+ * trailing zero bytes of a unit belong to no unit (7.4.1.2) */
+static int sp_units(const uint8_t *p, size_t n, size_t *ub, size_t *ue, int cap)
+{
+    if (!(n >= 3 && !p[0] && !p[1] && (p[2] == 1 || (n >= 4 && !p[2] && p[3] == 1)))) {
+        ub[0] = 0;
+        ue[0] = n;
+        return 1;
+    }
+    int k = 0;
+    size_t i = 0;
+    while (i + 3 <= n) {
+        if (!p[i] && !p[i + 1] && p[i + 2] == 1) {
+            if (k > 0) {
+                size_t e = i;
+                while (e > ub[k - 1] && !p[e - 1]) --e;
+                ue[k - 1] = e;
+            }
+            if (k == cap) return -1;
+            ub[k++] = i + 3;
+            i += 3;
+        } else {
+            ++i;
+        }
+    }
+    if (k > 0) {
+        size_t e = n;
+        while (e > ub[k - 1] && !p[e - 1]) --e;
+        ue[k - 1] = e;
+    }
+    return k;
+}
+
+/* index of the last 1 bit of an RBSP (its rbsp_stop_one_bit), or -1 */
+static long sp_stop_bit(const uint8_t *d, size_t nb)
+{
+    for (size_t i = nb; i-- > 0;)
+        if (d[i]) return (long)(8 * i + 7 - (size_t)__builtin_ctz(d[i]));
+    return -1;
+}
+
+/* availability of neighbour MB (x + dx, y + dy) of rect MB (x, y): in the
+ * external picture (inside the rect and the same slice) and in the composed
+ * one (inside the composed picture); 1 when they agree */
+static int sp_same_avail(const or_cfg *c, const or_splice *sp, const int *sid, int x, int y, int dx, int dy)
+{
+    const int nx = x + dx, ny = y + dy;
+    const int ext = nx >= 0 && ny >= 0 && nx < sp->w && sid[(size_t)ny * sp->w + nx] == sid[(size_t)y * sp->w + x];
+    const int X = sp->x0 + nx, Y = sp->y0 + ny;
+    const int comp = X >= 0 && Y >= 0 && X < c->w / 16;
+    return ext == comp;
+}
+
+/* an intra MB's prediction reads the same neighbours in both pictures
+ * (splice_oracle.h): modes = its Intra4x4PredModes (raster; I_4x4), or the
+ * I_16x16 luma mode in modes[0]; cm = intra_chroma_pred_mode */
+static int sp_intra_ok(const or_cfg *c, const or_splice *sp, const int *sid, int x, int y, int type,
+                       const int *modes, int cm)
+{
+    int a = 0, b = 0, d = 0, cc = 0;
+    if (cm == 0) a = b = 1;                                       /* chroma DC, horizontal, vertical, plane */
+    else if (cm == 1) a = 1;
+    else if (cm == 2) b = 1;
+    else a = b = d = 1;
+    if (type == 1) {
+        a = b = 1;                                                /* mode prediction (8.3.1.1) */
+        if (modes[0] == 4 || modes[0] == 5 || modes[0] == 6) d = 1;
+        if (modes[3] == 3 || modes[3] == 7) cc = 1;
+    } else {
+        const int lm = modes[0];                                  /* 8.3.3: vertical, horizontal, DC, plane */
+        if (lm == 0) b = 1;
+        else if (lm == 1) a = 1;
+        else if (lm == 2) a = b = 1;
+        else a = b = d = 1;
+    }
+    return (!a || sp_same_avail(c, sp, sid, x, y, -1, 0)) && (!b || sp_same_avail(c, sp, sid, x, y, 0, -1)) &&
+           (!d || sp_same_avail(c, sp, sid, x, y, -1, -1)) && (!cc || sp_same_avail(c, sp, sid, x, y, 1, -1));
+}
+
+/* P_Skip motion (8.4.1.1) from the availability of A and B (slices) */
+static void sp_pskip(const or_mvi *A, const or_mvi *B, const or_mvi *C, int *px, int *py)
+{
+    if (!A->avail || !B->avail || (A->ref == 0 && A->mx == 0 && A->my == 0) ||
+        (B->ref == 0 && B->mx == 0 && B->my == 0)) {
+        *px = 0;
+        *py = 0;
+        return;
+    }
+    or_spec_predict(A, B, C, 0, px, py);
+}
+
 int or_splice_parse(const or_cfg *c, const or_splice *sp, or_splice_mb *mbs, uint8_t *rbsp,
                     size_t *rbsp_n)
 {
-    const uint8_t *p = sp->nal;
-    size_t n = sp->n;
+    enum { MAXU = 1024 };
+    size_t ub[MAXU], ue[MAXU];
     *rbsp_n = 0;
-    if (n >= 4 && !p[0] && !p[1] && !p[2] && p[3] == 1) {
-        p += 4;
-        n -= 4;
-    } else if (n >= 3 && !p[0] && !p[1] && p[2] == 1) {
-        p += 3;
-        n -= 3;
-    }
-    if (n < 2 || (p[0] & 0x80) || (p[0] & 31) != 1) return OR_SPLICE_ERR_NAL;
-    const int ref_idc = (p[0] >> 5) & 3;
-    const size_t rn = sp_unescape(rbsp, p + 1, n - 1);
-    *rbsp_n = rn;
-    rd_t r = {rbsp, rn * 8, 0, 0};
-
-    /* slice header (7.3.3) with the composed stream's SPS / PPS fields */
-    if (rd_ue(&r) != 0) return OR_SPLICE_ERR_HEADER;             /* first_mb_in_slice */
-    const uint32_t st = rd_ue(&r);
-    if (st != 0 && st != 5) return OR_SPLICE_ERR_HEADER;          /* P */
-    if (rd_ue(&r) != 0) return OR_SPLICE_ERR_HEADER;             /* pic_parameter_set_id */
-    rd_u(&r, c->log2_mfn);                                        /* frame_num */
-    if (c->poc_type == 0) rd_u(&r, c->log2_poc);                  /* pic_order_cnt_lsb */
-    int nrefs = c->num_ref_default_m1 + 1;
-    if (rd_u(&r, 1)) {                                            /* num_ref_idx_active_override */
-        const uint32_t k = rd_ue(&r);
-        if (k > 31) return OR_SPLICE_ERR_HEADER;
-        nrefs = (int)k + 1;
-    }
-    if (rd_u(&r, 1)) {                                            /* ref_pic_list_modification */
-        /* only the composer's own list (h264_writer.c:455-539): op k puts
-         * long_term_pic_num k at index k -- the composed list itself */
-        for (int k = 0;; ++k) {
-            const uint32_t idc = rd_ue(&r);
-            if (r.bad || k > 32) return OR_SPLICE_ERR_SYNTAX;
-            if (idc == 3) break;
-            if (idc != 2 || rd_ue(&r) != (uint32_t)k) return OR_SPLICE_ERR_HEADER;
-        }
-    }
-    if (ref_idc && rd_u(&r, 1)) {                                 /* adaptive_ref_pic_marking */
-        for (int k = 0;; ++k) {
-            const uint32_t op = rd_ue(&r);
-            if (r.bad || k > 64 || op > 6) return OR_SPLICE_ERR_SYNTAX;
-            if (op == 0) break;
-            if (op == 1 || op == 3) rd_ue(&r);
-            if (op == 2) rd_ue(&r);
-            if (op == 3 || op == 6) rd_ue(&r);
-            if (op == 4) rd_ue(&r);
-        }
-    }
-    int qp = 26 + rd_se(&r);                                      /* pic_init_qp 26 + slice_qp_delta */
-    if (qp < 0 || qp > 51) return OR_SPLICE_ERR_HEADER;
-    if (c->deblock && rd_ue(&r) != 1) return OR_SPLICE_ERR_HEADER;
-    if (r.bad) return OR_SPLICE_ERR_SYNTAX;
-
-    /* slice data (7.3.4) */
+    const int nu = sp_units(sp->nal, sp->n, ub, ue, MAXU);
+    if (nu <= 0) return OR_SPLICE_ERR_NAL;
     const int W = sp->w, H = sp->h, nmb = W * H;
     memset(mbs, 0, sizeof(*mbs) * (size_t)nmb);
-    sp_field F = {W, (or_mvi *)calloc((size_t)nmb * 16, sizeof(or_mvi))};
-    int m = 0, qp_c = 26, err = OR_SPLICE_OK;
-    while (m < nmb && !err) {
-        const uint32_t run = rd_ue(&r);
-        if (r.bad || run > (uint32_t)(nmb - m)) {
+    int *sid = (int *)malloc(sizeof(int) * (size_t)nmb);
+    int8_t(*im)[16] = malloc((size_t)nmb * 16);                   /* Intra4x4PredMode, -1: not I_4x4 */
+    for (int k = 0; k < nmb; ++k) sid[k] = -1;
+    sp_field F = {W, (or_mvi *)calloc((size_t)nmb * 16, sizeof(or_mvi)), sid, 0};
+    int err = OR_SPLICE_OK, m = 0, qp_c = 26;
+    size_t rb0 = 0;                                               /* this slice's RBSP in rbsp[] */
+    for (int u = 0; u < nu && !err; ++u) {
+        const uint8_t *p = sp->nal + ub[u];
+        const size_t n = ue[u] - ub[u];
+        if (n < 2 || (p[0] & 0x80) || (p[0] & 31) != 1) {
+            err = OR_SPLICE_ERR_NAL;
+            break;
+        }
+        const int ref_idc = (p[0] >> 5) & 3;
+        const size_t rn = sp_unescape(rbsp + rb0, p + 1, n - 1);
+        /* bit positions are kept relative to the whole rbsp[] (all slices) */
+        rd_t r = {rbsp, (rb0 + rn) * 8, rb0 * 8, 0};
+        const long stop = sp_stop_bit(rbsp + rb0, rn);
+        const size_t end = stop < 0 ? 0 : rb0 * 8 + (size_t)stop;
+        rb0 += rn;
+        *rbsp_n = rb0;
+        /* slice header (7.3.3) with the composed stream's SPS / PPS fields */
+        const uint32_t first = rd_ue(&r);
+        if (first != (uint32_t)m) {                               /* slices in order, no gap */
+            err = OR_SPLICE_ERR_HEADER;
+            break;
+        }
+        const uint32_t st = rd_ue(&r);
+        if ((st != 0 && st != 5) || rd_ue(&r) != 0) {             /* P, pic_parameter_set_id 0 */
+            err = OR_SPLICE_ERR_HEADER;
+            break;
+        }
+        rd_u(&r, c->log2_mfn);                                    /* frame_num */
+        if (c->poc_type == 0) rd_u(&r, c->log2_poc);              /* pic_order_cnt_lsb */
+        int nrefs = c->num_ref_default_m1 + 1;
+        if (rd_u(&r, 1)) {                                        /* num_ref_idx_active_override */
+            const uint32_t k = rd_ue(&r);
+            if (k > 31) {
+                err = OR_SPLICE_ERR_HEADER;
+                break;
+            }
+            nrefs = (int)k + 1;
+        }
+        if (rd_u(&r, 1)) {                                        /* ref_pic_list_modification */
+            /* only the composer's own list (h264_writer.c:455-539): op k puts
+             * long_term_pic_num k at index k -- the composed list itself */
+            for (int k = 0;; ++k) {
+                const uint32_t idc = rd_ue(&r);
+                if (r.bad || k > 32) {
+                    err = OR_SPLICE_ERR_SYNTAX;
+                    break;
+                }
+                if (idc == 3) break;
+                if (idc != 2 || rd_ue(&r) != (uint32_t)k) {
+                    err = OR_SPLICE_ERR_HEADER;
+                    break;
+                }
+            }
+            if (err) break;
+        }
+        if (ref_idc && rd_u(&r, 1)) {                             /* adaptive_ref_pic_marking */
+            for (int k = 0;; ++k) {
+                const uint32_t op = rd_ue(&r);
+                if (r.bad || k > 64 || op > 6) {
+                    err = OR_SPLICE_ERR_SYNTAX;
+                    break;
+                }
+                if (op == 0) break;
+                if (op == 1 || op == 3) rd_ue(&r);
+                if (op == 2) rd_ue(&r);
+                if (op == 3 || op == 6) rd_ue(&r);
+                if (op == 4) rd_ue(&r);
+            }
+            if (err) break;
+        }
+        int qp = 26 + rd_se(&r);                                  /* pic_init_qp 26 + slice_qp_delta */
+        if (qp < 0 || qp > 51) {
+            err = OR_SPLICE_ERR_HEADER;
+            break;
+        }
+        if (c->deblock && rd_ue(&r) != 1) {
+            err = OR_SPLICE_ERR_HEADER;
+            break;
+        }
+        if (r.bad) {
             err = OR_SPLICE_ERR_SYNTAX;
             break;
         }
-        for (uint32_t k = 0; k < run; ++k, ++m) {                 /* P_Skip (8.4.1.1) */
+        F.cur = u;
+        /* slice data (7.3.4): MBs until the stop bit (more_rbsp_data) */
+        int first_mb = 1;
+        while (!err) {
+            if (r.p >= end && !first_mb) break;
+            first_mb = 0;
+            const uint32_t run = rd_ue(&r);
+            if (r.bad || run > (uint32_t)(nmb - m)) {
+                err = OR_SPLICE_ERR_SYNTAX;
+                break;
+            }
+            for (uint32_t k = 0; k < run; ++k, ++m) {             /* P_Skip (8.4.1.1) */
+                const int x = m % W, y = m / W;
+                sid[m] = u;
+                or_mvi A, B, C, Cr, D;
+                sp_nb16(&F, x, y, &A, &B, &C, &Cr, &D);
+                int px, py;
+                sp_pskip(&A, &B, &C, &px, &py);
+                or_splice_mb *mb = &mbs[m];
+                mb->ref = 0;
+                mb->mx = px;
+                mb->my = py;
+                mb->qp = qp;
+                mb->skip = 1;
+                memset(im[m], -1, 16);
+                for (int b = 0; b < 16; ++b) {
+                    mb->bmx[b] = px;
+                    mb->bmy[b] = py;
+                    *sp_at(&F, x, y, b & 3, b >> 2) = (or_mvi){px, py, 0, 1};
+                }
+            }
+            if (r.p >= end) break;                                /* skipped MBs end the slice */
+            if (m == nmb) {
+                err = OR_SPLICE_ERR_SYNTAX;
+                break;
+            }
             const int x = m % W, y = m / W;
-            or_mvi A, B, C, Cr, D;
-            sp_nb16(&F, x, y, &A, &B, &C, &Cr, &D);
-            int px, py;
-            or_pskip_motion(x, y, &A, &B, &C, &px, &py);
+            sid[m] = u;
             or_splice_mb *mb = &mbs[m];
-            mb->ref = 0;
-            mb->mx = px;
-            mb->my = py;
-            mb->qp = qp;
-            mb->skip = 1;
-            for (int b = 0; b < 16; ++b) {
-                mb->bmx[b] = px;
-                mb->bmy[b] = py;
-                *sp_at(&F, x, y, b & 3, b >> 2) = (or_mvi){px, py, 0, 1};
-            }
-        }
-        if (m == nmb) break;
-        const int x = m % W, y = m / W;
-        or_splice_mb *mb = &mbs[m];
-        const uint32_t mbt = rd_ue(&r);                           /* mb_type (Table 7-13) */
-        if (r.bad || mbt > 4) {
-            err = r.bad ? OR_SPLICE_ERR_SYNTAX : OR_SPLICE_ERR_MBTYPE;
-            break;
-        }
-        const int part = mbt == 4 ? 3 : (int)mbt;
-        int sub = 0;
-        if (part == 3)                                            /* sub_mb_pred (7.3.5.2) */
-            for (int i = 0; i < 4; ++i) {
-                const uint32_t st = rd_ue(&r);
-                if (st > 3) err = OR_SPLICE_ERR_SYNTAX;
-                sub |= (int)(st & 3u) << (2 * i);
-            }
-        const int nref = part == 0 ? 1 : (part == 3 ? 4 : 2);
-        int refs[4] = {0, 0, 0, 0};
-        if (mbt != 4)
-            for (int i = 0; i < nref; ++i) {                      /* ref_idx_l0: te() */
-                if (nrefs == 2) refs[i] = 1 - (int)rd_u(&r, 1);
-                else if (nrefs > 2) refs[i] = (int)rd_ue(&r);
-                if (refs[i] >= nrefs) err = OR_SPLICE_ERR_SYNTAX;
-            }
-        sp_part ps[16];
-        const int np = sp_partitions(part, sub, ps);
-        unsigned done = 0;
-        for (int k = 0; k < np && !err; ++k) {                   /* mvd_l0 per (sub-)partition */
-            const int ref = refs[ps[k].mb_part];
-            const int dx = rd_se(&r), dy = rd_se(&r);
-            int px, py;
-            sp_mvp(&F, x, y, done, part, &ps[k], ref, &px, &py);
-            const long long mx = (long long)px + dx, my = (long long)py + dy;
-            if (r.bad || mx < -OR_SPLICE_MAX_MV || mx > OR_SPLICE_MAX_MV || my < -OR_SPLICE_MAX_MV ||
-                my > OR_SPLICE_MAX_MV) {
+            const uint8_t *L = x && sid[m - 1] == u ? mbs[m - 1].tc : NULL;
+            const uint8_t *T = y && sid[m - W] == u ? mbs[m - W].tc : NULL;
+            const uint32_t mbt = rd_ue(&r);                       /* mb_type (Table 7-13, 7-11) */
+            if (r.bad || mbt > 30) {
                 err = OR_SPLICE_ERR_SYNTAX;
                 break;
             }
-            sp_fill(&F, x, y, &ps[k], (or_mvi){(int)mx, (int)my, ref, 1}, &done);
+            memset(im[m], -1, 16);
+            if (mbt >= 5) {
+                /* intra in a P slice (7.3.5.1): I_4x4, I_16x16, I_PCM */
+                const int it = (int)mbt - 5;
+                mb->intra = it == 0 ? 1 : (it == 25 ? 3 : 2);
+                mb->mbt = (int)mbt;
+                mb->ref = -1;
+                for (int b = 0; b < 16; ++b) {
+                    mb->bref[b] = -1;
+                    *sp_at(&F, x, y, b & 3, b >> 2) = (or_mvi){0, 0, -1, 1};
+                }
+                if (mb->intra == 3) {                             /* I_PCM (7.3.5) */
+                    while (r.p & 7)
+                        if (rd_u(&r, 1)) err = OR_SPLICE_ERR_SYNTAX;  /* pcm_alignment_zero_bit */
+                    mb->pcm = (uint32_t)(r.p >> 3);
+                    r.p += 384 * 8;
+                    if (r.p > r.nbits) r.bad = 1;
+                    for (int i = 0; i < OR_SPLICE_PIECES; ++i) mb->tc[i] = 16;   /* nC: 16 (9.2.1) */
+                    mb->qp = qp;
+                    if (r.bad) err = OR_SPLICE_ERR_SYNTAX;
+                    ++m;
+                    continue;
+                }
+                int modes[16], cm;
+                mb->poff = (uint32_t)r.p;
+                if (mb->intra == 1) {
+                    /* Intra4x4PredMode per block (8.3.1.1), luma4x4BlkIdx order */
+                    for (int blk = 0; blk < 16; ++blk) {
+                        const int ri = sp_blk_raster(blk), bx = ri & 3, by = ri >> 2;
+                        int mA = -2, mB = -2;                     /* -2 unavailable, -1 not I_4x4 */
+                        if (bx) mA = im[m][ri - 1];
+                        else if (x && sid[m - 1] == u) mA = im[m - 1][ri + 3];
+                        if (by) mB = im[m][ri - 4];
+                        else if (y && sid[m - W] == u) mB = im[m - W][ri + 12];
+                        const int pm = (mA == -2 || mB == -2) ? 2 : ((mA < 0 ? 2 : mA) < (mB < 0 ? 2 : mB)
+                                                                         ? (mA < 0 ? 2 : mA) : (mB < 0 ? 2 : mB));
+                        int md = pm;
+                        if (!rd_u(&r, 1)) {
+                            const int rem = (int)rd_u(&r, 3);
+                            md = rem < pm ? rem : rem + 1;
+                        }
+                        im[m][ri] = (int8_t)md;
+                    }
+                    for (int k = 0; k < 16; ++k) modes[k] = im[m][k];
+                } else {
+                    modes[0] = (it - 1) & 3;
+                }
+                cm = (int)rd_ue(&r);                              /* intra_chroma_pred_mode */
+                mb->plen = (uint32_t)r.p - mb->poff;
+                if (r.bad || cm > 3) {
+                    err = OR_SPLICE_ERR_SYNTAX;
+                    break;
+                }
+                if (!sp_intra_ok(c, sp, sid, x, y, mb->intra, modes, cm)) {
+                    err = OR_SPLICE_ERR_MBTYPE;
+                    break;
+                }
+                int cbp;
+                if (mb->intra == 1) {
+                    const uint32_t code = rd_ue(&r);
+                    if (r.bad || code > 47) {
+                        err = OR_SPLICE_ERR_SYNTAX;
+                        break;
+                    }
+                    mb->cbp_code = (int)code;
+                    cbp = SP_CBP_INTRA[code];
+                } else {
+                    cbp = ((it - 1) >= 12 ? 15 : 0) | (((it - 1) >> 2) % 3) << 4;
+                }
+                mb->cbp = cbp;
+                if (cbp || mb->intra == 2) {
+                    const int dq = rd_se(&r);                     /* mb_qp_delta */
+                    if (dq < -26 || dq > 25) {
+                        err = OR_SPLICE_ERR_SYNTAX;
+                        break;
+                    }
+                    qp = (qp + dq + 52) % 52;
+                    int d = qp - qp_c;
+                    if (d < -26) d += 52;
+                    if (d > 25) d -= 52;
+                    mb->qpd = d;
+                    mb->hasqpd = 1;
+                    qp_c = qp;
+                    int e = 0;
+                    if (mb->intra == 2) {                         /* Intra16x16DCLevel: nC of block 0 */
+                        e = sp_block(&r, sp_piece_nc(0, mb->tc, L, T), 16, &mb->tc[26], &mb->t1[26], &mb->boff[26],
+                                     &mb->blen[26]);
+                        if (!e && (cbp & 15))                     /* Intra16x16ACLevel */
+                            for (int blk = 0; blk < 16 && !e; ++blk) {
+                                const int ri = sp_blk_raster(blk);
+                                e = sp_block(&r, sp_piece_nc(ri, mb->tc, L, T), 15, &mb->tc[ri], &mb->t1[ri],
+                                             &mb->boff[ri], &mb->blen[ri]);
+                            }
+                        if (!e && (cbp >> 4)) {
+                            for (int i = 16; i < 18 && !e; ++i)
+                                e = sp_block(&r, -1, 4, &mb->tc[i], &mb->t1[i], &mb->boff[i], &mb->blen[i]);
+                            if (!e && (cbp >> 4) == 2)
+                                for (int i = 18; i < 26 && !e; ++i)
+                                    e = sp_block(&r, sp_piece_nc(i, mb->tc, L, T), 15, &mb->tc[i], &mb->t1[i],
+                                                 &mb->boff[i], &mb->blen[i]);
+                        }
+                    } else {
+                        e = sp_residual(&r, cbp, mb, L, T);
+                    }
+                    if (e) {
+                        err = OR_SPLICE_ERR_SYNTAX;
+                        break;
+                    }
+                }
+                mb->qp = qp;
+                if (r.bad) err = OR_SPLICE_ERR_SYNTAX;
+                ++m;
+                continue;
+            }
+            const int part = mbt == 4 ? 3 : (int)mbt;
+            int sub = 0;
+            if (part == 3)                                        /* sub_mb_pred (7.3.5.2) */
+                for (int i = 0; i < 4; ++i) {
+                    const uint32_t st2 = rd_ue(&r);
+                    if (st2 > 3) err = OR_SPLICE_ERR_SYNTAX;
+                    sub |= (int)(st2 & 3u) << (2 * i);
+                }
+            const int nref = part == 0 ? 1 : (part == 3 ? 4 : 2);
+            int refs[4] = {0, 0, 0, 0};
+            if (mbt != 4)
+                for (int i = 0; i < nref; ++i) {                  /* ref_idx_l0: te() */
+                    if (nrefs == 2) refs[i] = 1 - (int)rd_u(&r, 1);
+                    else if (nrefs > 2) refs[i] = (int)rd_ue(&r);
+                    if (refs[i] >= nrefs) err = OR_SPLICE_ERR_SYNTAX;
+                }
+            sp_part ps[16];
+            const int np = sp_partitions(part, sub, ps);
+            unsigned done = 0;
+            for (int k = 0; k < np && !err; ++k) {               /* mvd_l0 per (sub-)partition */
+                const int ref = refs[ps[k].mb_part];
+                const int dx = rd_se(&r), dy = rd_se(&r);
+                int px, py;
+                sp_mvp(&F, x, y, done, part, &ps[k], ref, &px, &py);
+                const long long mx = (long long)px + dx, my = (long long)py + dy;
+                if (r.bad || mx < -OR_SPLICE_MAX_MV || mx > OR_SPLICE_MAX_MV || my < -OR_SPLICE_MAX_MV ||
+                    my > OR_SPLICE_MAX_MV) {
+                    err = OR_SPLICE_ERR_SYNTAX;
+                    break;
+                }
+                sp_fill(&F, x, y, &ps[k], (or_mvi){(int)mx, (int)my, ref, 1}, &done);
+            }
+            const int cbp = sp_cbp_of_code(rd_ue(&r));
+            if (err || r.bad || cbp < 0) {
+                err = OR_SPLICE_ERR_SYNTAX;
+                break;
+            }
+            for (int b = 0; b < 16; ++b) {
+                const or_mvi v = *sp_at(&F, x, y, b & 3, b >> 2);
+                mb->bref[b] = v.ref;
+                mb->bmx[b] = v.mx;
+                mb->bmy[b] = v.my;
+            }
+            mb->part = part;
+            mb->sub = sub;
+            mb->ref = mb->bref[0];
+            mb->mx = mb->bmx[0];
+            mb->my = mb->bmy[0];
+            mb->cbp = cbp;
+            if (cbp) {
+                const int dq = rd_se(&r);                         /* mb_qp_delta */
+                if (dq < -26 || dq > 25) {
+                    err = OR_SPLICE_ERR_SYNTAX;
+                    break;
+                }
+                qp = (qp + dq + 52) % 52;
+                int d = qp - qp_c;                                /* composed chain from 26 */
+                if (d < -26) d += 52;
+                if (d > 25) d -= 52;
+                mb->qpd = d;
+                mb->hasqpd = 1;
+                qp_c = qp;
+                if (sp_residual(&r, cbp, mb, L, T)) {
+                    err = OR_SPLICE_ERR_SYNTAX;
+                    break;
+                }
+            }
+            mb->qp = qp;
+            ++m;
         }
-        const int cbp = sp_cbp_of_code(rd_ue(&r));
-        if (err || r.bad || cbp < 0) {
+        if (err) break;
+        /* rbsp_slice_trailing_bits: the stop bit, alignment zeros (zero bytes
+         * after it are tolerated: trailing_zero_8bits of a byte stream) */
+        if (r.p != end || rd_u(&r, 1) != 1) {
             err = OR_SPLICE_ERR_SYNTAX;
             break;
         }
-        for (int b = 0; b < 16; ++b) {
-            const or_mvi v = *sp_at(&F, x, y, b & 3, b >> 2);
-            mb->bref[b] = v.ref;
-            mb->bmx[b] = v.mx;
-            mb->bmy[b] = v.my;
-        }
-        mb->part = part;
-        mb->sub = sub;
-        mb->ref = mb->bref[0];
-        mb->mx = mb->bmx[0];
-        mb->my = mb->bmy[0];
-        mb->cbp = cbp;
-        if (cbp) {
-            const int dq = rd_se(&r);                             /* mb_qp_delta */
-            if (dq < -26 || dq > 25) {
-                err = OR_SPLICE_ERR_SYNTAX;
-                break;
-            }
-            qp = (qp + dq + 52) % 52;
-            int d = qp - qp_c;                                    /* composed chain from 26 */
-            if (d < -26) d += 52;
-            if (d > 25) d -= 52;
-            mb->qpd = d;
-            qp_c = qp;
-            if (sp_residual(&r, cbp, mb, x ? mbs[m - 1].tc : NULL, y ? mbs[m - W].tc : NULL)) {
-                err = OR_SPLICE_ERR_SYNTAX;
-                break;
-            }
-        }
-        mb->qp = qp;
-        ++m;
+        while (r.p & 7)
+            if (rd_u(&r, 1)) err = OR_SPLICE_ERR_SYNTAX;
+        while (!err && r.p < r.nbits)
+            if (rd_u(&r, 8)) err = OR_SPLICE_ERR_SYNTAX;
+        if (r.bad) err = OR_SPLICE_ERR_SYNTAX;
     }
+    if (!err && m != nmb) err = OR_SPLICE_ERR_SYNTAX;             /* the slices cover the picture */
     free(F.f);
-    if (err) return err;
-    /* rbsp_slice_trailing_bits: stop bit, alignment zeros (zero bytes after
-     * it are tolerated: trailing_zero_8bits of a byte stream) */
-    if (rd_u(&r, 1) != 1) return OR_SPLICE_ERR_SYNTAX;
-    while (r.p & 7)
-        if (rd_u(&r, 1)) return OR_SPLICE_ERR_SYNTAX;
-    while (r.p < r.nbits)
-        if (rd_u(&r, 8)) return OR_SPLICE_ERR_SYNTAX;
-    return r.bad ? OR_SPLICE_ERR_SYNTAX : OR_SPLICE_OK;
+    free(sid);
+    free(im);
+    return err;
 }
 
 /* ------------------------------------------------------------------------ */
@@ -533,7 +806,7 @@ static size_t sp_compose(uint8_t *dst, size_t cap, or_cfg *c, int off, const or_
     or_scroll_regions(c, off, &a_end, &ra, &mva, &rb, &mvb);
     size_t rcap = 64 + (size_t)mbw * mbh * 24 + (has ? erb_n * 2 + (size_t)w * h * 64 : 0);
     uint8_t *rbsp = (uint8_t *)malloc(rcap);
-    sp_field F = {mbw, (or_mvi *)calloc((size_t)mbw * mbh * 16, sizeof(or_mvi))};
+    sp_field F = {mbw, (or_mvi *)calloc((size_t)mbw * mbh * 16, sizeof(or_mvi)), NULL, 0};
     uint8_t(*tabove)[OR_SPLICE_PIECES] = calloc((size_t)mbw, OR_SPLICE_PIECES);
     uint8_t(*tcur)[OR_SPLICE_PIECES] = calloc((size_t)mbw, OR_SPLICE_PIECES);
     or_bits b;
@@ -545,6 +818,44 @@ static size_t sp_compose(uint8_t *dst, size_t cap, or_cfg *c, int off, const or_
             const or_splice_mb *mb = NULL;
             if (has && x >= sp->x0 && x < sp->x0 + sp->w && y >= sp->y0 && y < sp->y0 + sp->h)
                 mb = &mbs[(size_t)(y - sp->y0) * sp->w + (x - sp->x0)];
+            if (mb && mb->intra) {
+                /* an intra MB: mb_type, its prediction syntax (and I_4x4's cbp
+                 * codeNum) verbatim, the residual re-contexted; I_PCM
+                 * realigned.  Available with refIdx -1, mv 0 for the motion
+                 * prediction of the MBs after it (8.4.1.3.1) */
+                or_ue(&b, (uint32_t)run);                         /* mb_skip_run */
+                run = 0;
+                or_ue(&b, (uint32_t)mb->mbt);
+                memset(tcur[x], 0, OR_SPLICE_PIECES);
+                if (mb->intra == 3) {
+                    while (b.nbits & 7) or_put(&b, 0, 1);         /* pcm_alignment_zero_bit */
+                    sp_copy_bits(&b, erb, 8u * mb->pcm, 384u * 8u);
+                    memset(tcur[x], 16, OR_SPLICE_PIECES);
+                } else {
+                    sp_copy_bits(&b, erb, mb->poff, mb->plen);
+                    if (mb->intra == 1) or_ue(&b, (uint32_t)mb->cbp_code);
+                    memcpy(tcur[x], mb->tc, OR_SPLICE_PIECES);
+                    const uint8_t *L = x ? tcur[x - 1] : NULL, *T = y ? tabove[x] : NULL;
+                    const int cbp = mb->cbp;
+                    if (mb->hasqpd) {
+                        or_se(&b, mb->qpd);
+                        if (mb->intra == 2) sp_piece(&b, mb, 26, sp_piece_nc(0, tcur[x], L, T), erb);
+                        for (int blk = 0; blk < 16; ++blk)
+                            if (cbp & (1 << (blk >> 2))) {
+                                const int i = sp_blk_raster(blk);
+                                sp_piece(&b, mb, i, sp_piece_nc(i, tcur[x], L, T), erb);
+                            }
+                        if (cbp >> 4) {
+                            sp_piece(&b, mb, 16, -1, erb);
+                            sp_piece(&b, mb, 17, -1, erb);
+                            if ((cbp >> 4) == 2)
+                                for (int i = 18; i < 26; ++i) sp_piece(&b, mb, i, sp_piece_nc(i, tcur[x], L, T), erb);
+                        }
+                    }
+                }
+                for (int k = 0; k < 16; ++k) *sp_at(&F, x, y, k & 3, k >> 2) = (or_mvi){0, 0, -1, 1};
+                continue;
+            }
             int ref, mx, my, cbp = 0;
             const int part = mb ? mb->part : 0;
             if (mb) {
@@ -891,6 +1202,135 @@ static void sp_rand_block(uint32_t *s, const or_ext_params *p, int *coef, int ma
     for (int i = 0; i < k; ++i) coef[sp_rng(s) % (unsigned)maxc] = sp_level(s, p);
 }
 
+/* the slice header of the stand-in encoder's slices */
+static void ext_header(or_bits *b, const or_cfg *c, const or_ext_params *p, int first, int nrefs, int nrefs_def)
+{
+    or_ue(b, (uint32_t)first);                                    /* first_mb_in_slice */
+    or_ue(b, 0);                                                  /* P */
+    or_ue(b, 0);                                                  /* pps id */
+    or_put(b, 0, c->log2_mfn);
+    if (c->poc_type == 0) or_put(b, 0, c->log2_poc);
+    if (nrefs != nrefs_def) {
+        or_put(b, 1, 1);
+        or_ue(b, (uint32_t)(nrefs - 1));
+    } else {
+        or_put(b, 0, 1);
+    }
+    if (p->list_mod) {                                            /* ref_pic_list_modification */
+        or_put(b, 1, 1);
+        for (int k = 0; k < nrefs; ++k) {
+            or_ue(b, 2);                                          /* long_term_pic_num */
+            or_ue(b, (uint32_t)(p->list_mod == 2 ? nrefs - 1 - k : k));
+        }
+        or_ue(b, 3);
+    } else {
+        or_put(b, 0, 1);
+    }
+    if (p->ref_idc) or_put(b, 0, 1);                              /* sliding window */
+    or_se(b, p->slice_qp_delta);
+    if (c->deblock) or_ue(b, 1);
+}
+
+/* an intra MB of the stand-in encoder (type 1 I_4x4, 2 I_16x16, 3 I_PCM, or
+ * mbt_force 5..30), its modes predicted as the parse does (8.3.1.1) */
+static void ext_intra(or_bits *b, uint32_t *s, const or_ext_params *p, int type, int mbt_force, int x, int y,
+                      int W, const int *sid, int8_t (*im)[16], uint8_t (*tcs)[OR_SPLICE_PIECES], int *qp)
+{
+    const int m = y * W + x, u = sid[m];
+    const uint8_t *L = x && sid[m - 1] == u ? tcs[m - 1] : NULL, *T = y && sid[m - W] == u ? tcs[m - W] : NULL;
+    uint8_t *t = tcs[m];
+    memset(t, 0, OR_SPLICE_PIECES);
+    memset(im[m], -1, 16);
+    if (mbt_force) type = mbt_force == 5 ? 1 : (mbt_force == 30 ? 3 : 2);
+    if (type == 3) {
+        or_ue(b, 30);
+        while (b->nbits & 7) or_put(b, 0, 1);
+        for (int k = 0; k < 384; ++k) or_put(b, p->pcm_zero ? 0u : (sp_rng(s) & 255u), 8);
+        memset(t, 16, OR_SPLICE_PIECES);
+        return;
+    }
+    int coef[16];
+    if (type == 1) {
+        or_ue(b, 5);
+        for (int blk = 0; blk < 16; ++blk) {
+            const int ri = sp_blk_raster(blk), bx = ri & 3, by = ri >> 2;
+            int mA = -2, mB = -2;
+            if (bx) mA = im[m][ri - 1];
+            else if (x && sid[m - 1] == u) mA = im[m - 1][ri + 3];
+            if (by) mB = im[m][ri - 4];
+            else if (y && sid[m - W] == u) mB = im[m - W][ri + 12];
+            const int a = mA < 0 ? 2 : mA, bb = mB < 0 ? 2 : mB;
+            const int pm = (mA == -2 || mB == -2) ? 2 : (a < bb ? a : bb);
+            const int md = (sp_rng(s) % 3 == 0) ? pm : (int)(sp_rng(s) % 9);
+            if (md == pm) {
+                or_put(b, 1, 1);
+            } else {
+                or_put(b, 0, 1);
+                or_put(b, (uint32_t)(md < pm ? md : md - 1), 3);
+            }
+            im[m][ri] = (int8_t)md;
+        }
+        or_ue(b, sp_rng(s) % 4);                                  /* intra_chroma_pred_mode */
+        const int cbp = (int)(sp_rng(s) % 48);
+        int code = 0;
+        while (SP_CBP_INTRA[code] != cbp) ++code;
+        or_ue(b, (uint32_t)code);
+        if (!cbp) return;
+        const int j = p->qp_jitter;
+        int nq = *qp + (j ? (int)(sp_rng(s) % (uint32_t)(2 * j + 1)) - j : 0);
+        nq = nq < 0 ? 0 : (nq > 51 ? 51 : nq);
+        or_se(b, nq - *qp);
+        *qp = nq;
+        for (int blk = 0; blk < 16; ++blk) {
+            if (!(cbp & (1 << (blk >> 2)))) continue;
+            const int i = sp_blk_raster(blk);
+            sp_rand_block(s, p, coef, 16);
+            t[i] = (uint8_t)or_cavlc_block(b, coef, 16, sp_piece_nc(i, t, L, T));
+        }
+        if (cbp >> 4) {
+            for (int i = 16; i < 18; ++i) {
+                sp_rand_block(s, p, coef, 4);
+                or_cavlc_block(b, coef, 4, -1);
+            }
+            if ((cbp >> 4) == 2)
+                for (int i = 18; i < 26; ++i) {
+                    sp_rand_block(s, p, coef, 15);
+                    t[i] = (uint8_t)or_cavlc_block(b, coef, 15, sp_piece_nc(i, t, L, T));
+                }
+        }
+        return;
+    }
+    /* I_16x16: prediction mode, chroma cbp, luma cbp in the mb_type */
+    const int it = mbt_force ? mbt_force - 6 : (int)(sp_rng(s) % 24);
+    const int cbl = it >= 12 ? 15 : 0, cbc = (it >> 2) % 3;
+    or_ue(b, (uint32_t)(6 + it));
+    or_ue(b, sp_rng(s) % 4);                                      /* intra_chroma_pred_mode */
+    const int j = p->qp_jitter;
+    int nq = *qp + (j ? (int)(sp_rng(s) % (uint32_t)(2 * j + 1)) - j : 0);
+    nq = nq < 0 ? 0 : (nq > 51 ? 51 : nq);
+    or_se(b, nq - *qp);                                           /* mb_qp_delta: always */
+    *qp = nq;
+    sp_rand_block(s, p, coef, 16);                                /* Intra16x16DCLevel */
+    or_cavlc_block(b, coef, 16, sp_piece_nc(0, t, L, T));
+    if (cbl)
+        for (int blk = 0; blk < 16; ++blk) {                      /* Intra16x16ACLevel */
+            const int i = sp_blk_raster(blk);
+            sp_rand_block(s, p, coef, 15);
+            t[i] = (uint8_t)or_cavlc_block(b, coef, 15, sp_piece_nc(i, t, L, T));
+        }
+    if (cbc) {
+        for (int i = 16; i < 18; ++i) {
+            sp_rand_block(s, p, coef, 4);
+            or_cavlc_block(b, coef, 4, -1);
+        }
+        if (cbc == 2)
+            for (int i = 18; i < 26; ++i) {
+                sp_rand_block(s, p, coef, 15);
+                t[i] = (uint8_t)or_cavlc_block(b, coef, 15, sp_piece_nc(i, t, L, T));
+            }
+    }
+}
+
 size_t or_ext_slice(uint8_t *dst, size_t cap, const or_cfg *c, int W, int H, uint32_t seed,
                     const or_ext_params *p)
 {
@@ -900,53 +1340,60 @@ size_t or_ext_slice(uint8_t *dst, size_t cap, const or_cfg *c, int W, int H, uin
     const int nrefs = p->nrefs ? p->nrefs : nrefs_def;
     const size_t rcap = 64 + (size_t)nmb * 8192;
     uint8_t *rbsp = (uint8_t *)malloc(rcap);
+    int *sid = (int *)malloc(sizeof(int) * (size_t)nmb);
+    int8_t(*im)[16] = malloc((size_t)nmb * 16);
     or_bits b;
     or_bits_init(&b, rbsp, rcap);
-    or_ue(&b, 0);                                                 /* first_mb_in_slice */
-    or_ue(&b, 0);                                                 /* P */
-    or_ue(&b, 0);                                                 /* pps id */
-    or_put(&b, 0, c->log2_mfn);
-    if (c->poc_type == 0) or_put(&b, 0, c->log2_poc);
-    if (nrefs != nrefs_def) {
-        or_put(&b, 1, 1);
-        or_ue(&b, (uint32_t)(nrefs - 1));
-    } else {
-        or_put(&b, 0, 1);
-    }
-    if (p->list_mod) {                                            /* ref_pic_list_modification */
-        or_put(&b, 1, 1);
-        for (int k = 0; k < nrefs; ++k) {
-            or_ue(&b, 2);                                         /* long_term_pic_num */
-            or_ue(&b, (uint32_t)(p->list_mod == 2 ? nrefs - 1 - k : k));
-        }
-        or_ue(&b, 3);
-    } else {
-        or_put(&b, 0, 1);
-    }
-    if (p->ref_idc) or_put(&b, 0, 1);                             /* sliding window */
-    or_se(&b, p->slice_qp_delta);
-    if (c->deblock) or_ue(&b, 1);
-    int qp = 26 + p->slice_qp_delta;
-    sp_field F = {W, (or_mvi *)calloc((size_t)nmb * 16, sizeof(or_mvi))};
+    int qp = 26 + p->slice_qp_delta, slice = 0, top = 0;          /* top: the slice's first MB row */
+    ext_header(&b, c, p, 0, nrefs, nrefs_def);
+    sp_field F = {W, (or_mvi *)calloc((size_t)nmb * 16, sizeof(or_mvi)), sid, 0};
     uint8_t(*tcs)[OR_SPLICE_PIECES] = calloc((size_t)nmb, OR_SPLICE_PIECES);
+    size_t nb = 0;
     int run = 0;
     const int rg = p->mv_range;
     for (int m = 0; m < nmb; ++m) {
         const int x = m % W, y = m / W;
+        if (p->slice_rows > 0 && x == 0 && y > 0 && y % p->slice_rows == 0) {
+            /* the next slice: this one ends (pending skips, trailing bits) */
+            if (run > 0) or_ue(&b, (uint32_t)run);
+            run = 0;
+            or_trailing(&b);
+            nb += or_nal(dst + nb, cap - nb, p->ref_idc, 1, rbsp, or_bytes(&b));
+            or_bits_init(&b, rbsp, rcap);
+            ext_header(&b, c, p, m, nrefs, nrefs_def);
+            qp = 26 + p->slice_qp_delta;
+            F.cur = ++slice;
+            top = y;
+        }
+        sid[m] = slice;
+        memset(im[m], -1, 16);
         or_mvi A, B, C, Cr, D;
         sp_nb16(&F, x, y, &A, &B, &C, &Cr, &D);
-        if (m == p->bad_mb) {
+        if (m == p->bad_mb && (p->bad_type < 5 || p->bad_type > 30)) {
             or_ue(&b, (uint32_t)run);
             or_ue(&b, (uint32_t)p->bad_type);
             or_put(&b, sp_rng(&s), 32);
             run = 0;
             break;
         }
-        if ((int)(sp_rng(&s) % 1000) < p->skip_pm) {
+        const int forced = m == p->bad_mb ? p->bad_type : 0;     /* a valid intra MB of that type here */
+        if (!forced && (int)(sp_rng(&s) % 1000) < p->skip_pm) {
             int px, py;
-            or_pskip_motion(x, y, &A, &B, &C, &px, &py);
+            sp_pskip(&A, &B, &C, &px, &py);
             for (int k = 0; k < 16; ++k) *sp_at(&F, x, y, k & 3, k >> 2) = (or_mvi){px, py, 0, 1};
+            memset(tcs[m], 0, OR_SPLICE_PIECES);
             run++;
+            continue;
+        }
+        /* intra where any rect placement splices it (splice_oracle.h) */
+        if (forced || (p->intra_pm > 0 && (int)(sp_rng(&s) % 1000) < p->intra_pm)) {
+            const int interior = x > 0 && x < W - 1 && y > top;
+            const int k = (int)(sp_rng(&s) % 5);
+            const int type = !interior ? 3 : (k < 2 ? 1 : (k < 4 ? 2 : 3));
+            or_ue(&b, (uint32_t)run);
+            run = 0;
+            ext_intra(&b, &s, p, type, forced, x, y, W, sid, im, tcs, &qp);
+            for (int q = 0; q < 16; ++q) *sp_at(&F, x, y, q & 3, q >> 2) = (or_mvi){0, 0, -1, 1};
             continue;
         }
         int ref = (int)(sp_rng(&s) % (uint32_t)(p->max_ref + 1));
@@ -1002,14 +1449,16 @@ size_t or_ext_slice(uint8_t *dst, size_t cap, const or_cfg *c, int W, int H, uin
             }
         }
         or_ue(&b, (uint32_t)or_cbp_code(cbp));
+        uint8_t *t = tcs[m];
+        memset(t, 0, OR_SPLICE_PIECES);
         if (cbp) {
             const int j = p->qp_jitter;
             int nq = qp + (j ? (int)(sp_rng(&s) % (uint32_t)(2 * j + 1)) - j : 0);
             nq = nq < 0 ? 0 : (nq > 51 ? 51 : nq);
             or_se(&b, nq - qp);
             qp = nq;
-            uint8_t *t = tcs[m];
-            const uint8_t *L = x ? tcs[m - 1] : NULL, *T = y ? tcs[m - W] : NULL;
+            const uint8_t *L = x && sid[m - 1] == slice ? tcs[m - 1] : NULL;
+            const uint8_t *T = y && sid[m - W] == slice ? tcs[m - W] : NULL;
             int coef[16];
             for (int blk = 0; blk < 16; ++blk) {
                 if (!(cbp & (1 << (blk >> 2)))) continue;
@@ -1032,9 +1481,11 @@ size_t or_ext_slice(uint8_t *dst, size_t cap, const or_cfg *c, int W, int H, uin
     }
     if (run > 0) or_ue(&b, (uint32_t)run);
     or_trailing(&b);
-    const size_t nb = or_nal(dst, cap, p->ref_idc, 1, rbsp, or_bytes(&b));
+    nb += or_nal(dst + nb, cap - nb, p->ref_idc, 1, rbsp, or_bytes(&b));
     free(rbsp);
     free(F.f);
     free(tcs);
+    free(sid);
+    free(im);
     return nb;
 }

@@ -17,15 +17,34 @@
  * picture of w x h MBs with the composed stream's SPS/PPS fields
  * (log2_max_frame_num, POC type, num_ref_idx default, deblocking flag); the
  * rect [x0, x0 + w) x [y0, y0 + h) of the composed picture receives its MBs.
- * Supported: first_mb_in_slice 0, no ref_pic_list_modification or one that
- * restates the composed list (op k: long_term_pic_num k, as the composer's
- * own slices write it, h264_writer.c:455-539), no
- * deblocking when the PPS allows switching it off (disable_deblocking_filter
- * _idc 1, like the composer's own slices), inter MBs of every P type
- * (P_L0_16x16, P_L0_L0_16x8, P_L0_L0_8x16, P_8x8 with any sub_mb_types,
- * P_8x8ref0) and P_Skip, any coded_block_pattern, mb_qp_delta and CAVLC
- * residual (level_prefix <= 15); intra MBs are not spliced (their sample
- * prediction would read composed-picture neighbours across the rect edge).
+ * The picture may come as several slices (Annex-B NAL units one after
+ * the other, in MB order, together covering the w x h MBs once: first slice
+ * at MB 0, each next one at the MB after the previous one's last; any MB
+ * boundary, e.g. one slice per MB row, MASTER_DESIGN.md:170,217).  Per
+ * slice: no ref_pic_list_modification or one that restates the composed list
+ * (op k: long_term_pic_num k, as the composer's own slices write it,
+ * h264_writer.c:455-539), no deblocking when the PPS allows switching it off
+ * (disable_deblocking_filter_idc 1, like the composer's own slices); MBs of
+ * every P type (P_L0_16x16, P_L0_L0_16x8, P_L0_L0_8x16, P_8x8 with any
+ * sub_mb_types, P_8x8ref0), P_Skip, and the intra types a P slice carries
+ * (mb_type 5 I_4x4, 6..29 I_16x16, 30 I_PCM; the reference's own P-slice
+ * walker takes all three, trans_resizer.c:1668-1748), any
+ * coded_block_pattern, mb_qp_delta and CAVLC residual (level_prefix <= 15).
+ * Neighbours in another slice are unavailable in the external picture
+ * (6.4.x): motion prediction, P_Skip motion, nC and intra prediction see
+ * them so.
+ * Intra MBs: their sample prediction reads neighbour MBs, so an I_4x4 /
+ * I_16x16 MB is spliced only where each neighbour MB its prediction uses
+ * has the same availability in the external and the composed picture (a
+ * neighbour inside the rect and the same slice: the same MB in both; outside
+ * the rect it is available in the composed picture unless past its edge):
+ * I_16x16 luma / chroma modes their A / B / D per mode (8.3.3, 8.3.4),
+ * I_4x4 always A and B (intra mode prediction, 8.3.1.1), D when raster block
+ * 0 uses a mode reading p[-1, -1] (4, 5, 6), C when raster block 3 uses one
+ * reading above-right samples (3, 7).  So interior MBs of a one-slice picture
+ * always qualify, the rect's left / top edge only at the composed picture's
+ * edge, its right edge without above-right modes.  I_PCM anywhere.  Else
+ * OR_SPLICE_ERR_MBTYPE.
  * Its ref_idx values index the composed stream's list (0 = A, 1 = B, 2 + i =
  * waypoint i) and its motion vectors are displacements in composed-picture
  * coordinates.
@@ -46,7 +65,14 @@
  *   - mb_qp_delta is rebased so each MB keeps its external QP;
  *   - every residual block keeps its bits after coeff_token verbatim (they do
  *     not depend on nC); coeff_token is re-coded for the nC of the composed
- *     picture (rect-edge neighbours are available MBs with TotalCoeff 0).
+ *     picture (rect-edge neighbours are available MBs with TotalCoeff 0);
+ *   - an intra MB keeps mb_type and its prediction syntax (I_4x4: the 16
+ *     prev_intra4x4_pred_mode / rem fields, and intra_chroma_pred_mode) and
+ *     I_4x4's coded_block_pattern codeNum verbatim; I_16x16's DC block is one
+ *     more re-contexted piece; I_PCM is realigned (pcm_alignment_zero_bits
+ *     for its composed position) and its 384 samples copied.  In the
+ *     composed motion field an intra MB is available with refIdx -1, mv 0
+ *     (8.4.1.3.1); it is never skipped.
  * MBs outside the rect follow the UI-hint composition (hint_oracle.h) of
  * the frame, whose neighbour predictions now see the spliced motion.
  */
@@ -67,11 +93,12 @@ extern "C" {
 #define OR_SPLICE_OK 0
 #define OR_SPLICE_ERR_NAL 1      /* not a coded slice of a non-IDR picture        */
 #define OR_SPLICE_ERR_HEADER 2   /* slice header outside the supported syntax     */
-#define OR_SPLICE_ERR_MBTYPE 3   /* an intra MB (mb_type > 4 in a P slice)        */
+#define OR_SPLICE_ERR_MBTYPE 3   /* an intra MB whose prediction would change     */
 #define OR_SPLICE_ERR_SYNTAX 4   /* malformed / truncated slice data              */
 #define OR_SPLICE_ERR_REF 5      /* ref_idx not a valid reference of the frame    */
 
-#define OR_SPLICE_PIECES 26      /* 16 luma (raster), Cb DC, Cr DC, 4 Cb AC, 4 Cr AC */
+#define OR_SPLICE_PIECES 27      /* 16 luma (raster; I_16x16: AC), Cb DC, Cr DC, 4 Cb AC, 4 Cr AC,
+                                  * I_16x16 luma DC */
 #define OR_SPLICE_MAX_MV 16383   /* |mv| in quarter pels */
 
 typedef struct {
@@ -90,6 +117,12 @@ typedef struct {
     int part;                    /* 0 P_L0_16x16 / P_Skip, 1 16x8, 2 8x16, 3 P_8x8 (and P_8x8ref0) */
     int sub;                     /* P_8x8: sub_mb_type of 8x8 i in bits 2i..2i+1 (0 8x8, 1 8x4, 2 4x8, 3 4x4) */
     int bref[16], bmx[16], bmy[16];  /* motion per 4x4 block, raster order  */
+    int intra;                   /* 0 inter / P_Skip, 1 I_4x4, 2 I_16x16, 3 I_PCM */
+    int mbt;                     /* intra: its mb_type (5..30)                */
+    uint32_t poff, plen;         /* intra: prediction syntax bits in the RBSP */
+    int cbp_code;                /* I_4x4: coded_block_pattern codeNum        */
+    uint32_t pcm;                /* I_PCM: byte offset of its samples in the RBSP */
+    int hasqpd;                  /* carries mb_qp_delta                       */
 } or_splice_mb;
 
 /* Parse the external slice: mbs[w * h] (raster), its RBSP into rbsp (cap
@@ -151,6 +184,12 @@ typedef struct {
                                   * k at index k), 2 reversed (unsupported)      */
     int part_pm;                 /* per mille of coded MBs: P_L0_L0_16x8 / 8x16,
                                   * P_8x8 (random sub_mb_types) or P_8x8ref0     */
+    int intra_pm;                /* per mille of coded MBs: I_4x4 / I_16x16 / I_PCM,
+                                  * only where any rect placement splices them
+                                  * (not on the picture's edges, the top MB row of
+                                  * a slice, an I_4x4 not on the right column)   */
+    int slice_rows;              /* 0: one slice; k: a slice per k MB rows       */
+    int pcm_zero;                /* I_PCM samples all 0 (emulation prevention)   */
 } or_ext_params;
 size_t or_ext_slice(uint8_t *dst, size_t cap, const or_cfg *c, int w, int h, uint32_t seed,
                     const or_ext_params *p);

@@ -27,10 +27,12 @@ ERR_NAL, ERR_HEADER, ERR_MBTYPE, ERR_SYNTAX, ERR_REF = 1, 2, 3, 4, 5
 
 class SpliceMb(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int) for n in ("ref", "mx", "my", "cbp", "qp", "qpd", "skip")] + [
-        ("tc", ctypes.c_uint8 * 26), ("t1", ctypes.c_uint8 * 26),
-        ("boff", ctypes.c_uint32 * 26), ("blen", ctypes.c_uint32 * 26),
+        ("tc", ctypes.c_uint8 * 27), ("t1", ctypes.c_uint8 * 27),
+        ("boff", ctypes.c_uint32 * 27), ("blen", ctypes.c_uint32 * 27),
         ("part", ctypes.c_int), ("sub", ctypes.c_int), ("bref", ctypes.c_int * 16),
-        ("bmx", ctypes.c_int * 16), ("bmy", ctypes.c_int * 16)]
+        ("bmx", ctypes.c_int * 16), ("bmy", ctypes.c_int * 16),
+        ("intra", ctypes.c_int), ("mbt", ctypes.c_int), ("poff", ctypes.c_uint32), ("plen", ctypes.c_uint32),
+        ("cbp_code", ctypes.c_int), ("pcm", ctypes.c_uint32), ("hasqpd", ctypes.c_int)]
 
 
 def _cfg(oracle, w, h):
@@ -217,10 +219,27 @@ def test_errors(oracle):
 
     good = ext_slice(oracle, c, 4, 3, 1)
     assert compose(splice_of(2, 2, 4, 3, good)) == 0
-    # unsupported MB types: intra (5 = I_NxN in P, 12 = I_16x16, 30 = I_PCM)
+    # intra MBs (5 = I_NxN in P, 12 = I_16x16 DC, 30 = I_PCM): spliced inside the rect
     for t in (5, 12, 30):
-        bad = ext_slice(oracle, c, 4, 3, 1, bad_mb=5, bad_type=t)
-        assert compose(splice_of(2, 2, 4, 3, bad)) == ERR_MBTYPE, t
+        ok = ext_slice(oracle, c, 4, 3, 1, bad_mb=5, bad_type=t)
+        assert compose(splice_of(2, 2, 4, 3, ok)) == 0, t
+    # on the rect's top / left edge an I_4x4 / I_16x16 DC would predict from
+    # other samples in the composed picture (refused); I_PCM anywhere; with the
+    # rect in the picture's corner those edges are the picture's (accepted)
+    for mb in (0, 1, 4):
+        for t in (5, 12):
+            bad = ext_slice(oracle, c, 4, 3, 1, bad_mb=mb, bad_type=t)
+            assert compose(splice_of(2, 2, 4, 3, bad)) == ERR_MBTYPE, (mb, t)
+            assert compose(splice_of(0, 0, 4, 3, bad)) == 0, (mb, t)
+        ok = ext_slice(oracle, c, 4, 3, 1, bad_mb=mb, bad_type=30)
+        assert compose(splice_of(2, 2, 4, 3, ok)) == 0, mb
+    # I_16x16 vertical prediction (mb_type 6) on the left edge reads no left samples
+    ok = ext_slice(oracle, c, 4, 3, 1, bad_mb=4, bad_type=6)
+    e, mbs = _parse(oracle, c, splice_of(2, 2, 4, 3, ok))
+    assert e == 0 or e == ERR_MBTYPE                # the chroma mode decides (random)
+    # mb_type past the P-slice range
+    bad = ext_slice(oracle, c, 4, 3, 1, bad_mb=5, bad_type=31)
+    assert compose(splice_of(2, 2, 4, 3, bad)) == ERR_SYNTAX
     # not a non-IDR slice: an IDR NAL header, an SPS
     assert compose(splice_of(2, 2, 4, 3, good[:4] + bytes([0x65]) + good[5:])) == ERR_NAL
     assert compose(splice_of(2, 2, 4, 3, good[:4] + bytes([0x67]) + good[5:])) == ERR_NAL

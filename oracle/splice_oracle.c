@@ -1389,13 +1389,19 @@ size_t or_ext_slice(uint8_t *dst, size_t cap, const or_cfg *c, int W, int H, uin
         if (forced || (p->intra_pm > 0 && (int)(sp_rng(&s) % 1000) < p->intra_pm)) {
             const int interior = x > 0 && x < W - 1 && y > top;
             const int k = (int)(sp_rng(&s) % 5);
-            const int type = !interior ? 3 : (k < 2 ? 1 : (k < 4 ? 2 : 3));
+            int type = !interior ? 3 : (k < 2 ? 1 : (k < 4 ? 2 : 3));
+            const int ty = p->intra_types ? p->intra_types : 7;
+            if (!(ty >> (type - 1) & 1)) type = (ty & 2) && interior ? 2 : ((ty & 1) && interior ? 1 : ((ty & 4) ? 3 : 0));
+            if (!forced && type == 0) {                           /* no allowed type here: inter */
+                goto inter;
+            }
             or_ue(&b, (uint32_t)run);
             run = 0;
             ext_intra(&b, &s, p, type, forced, x, y, W, sid, im, tcs, &qp);
             for (int q = 0; q < 16; ++q) *sp_at(&F, x, y, q & 3, q >> 2) = (or_mvi){0, 0, -1, 1};
             continue;
         }
+    inter:;
         int ref = (int)(sp_rng(&s) % (uint32_t)(p->max_ref + 1));
         if (ref >= nrefs) ref = nrefs - 1;
         const int mx = rg ? (int)(sp_rng(&s) % (uint32_t)(2 * rg + 1)) - rg : 0;

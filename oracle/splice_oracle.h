@@ -190,6 +190,7 @@ typedef struct {
                                   * a slice, an I_4x4 not on the right column)   */
     int slice_rows;              /* 0: one slice; k: a slice per k MB rows       */
     int pcm_zero;                /* I_PCM samples all 0 (emulation prevention)   */
+    int intra_types;             /* 0: all; else bit 0 I_4x4, 1 I_16x16, 2 I_PCM  */
 } or_ext_params;
 size_t or_ext_slice(uint8_t *dst, size_t cap, const or_cfg *c, int w, int h, uint32_t seed,
                     const or_ext_params *p);

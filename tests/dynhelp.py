@@ -131,12 +131,12 @@ class ExtParams(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int) for n in
                 ("nrefs", "max_ref", "skip_pm", "cbp_pm", "big_pm", "mv_range",
                  "slice_qp_delta", "qp_jitter", "ref_idc", "bad_mb", "bad_type", "list_mod",
-                 "part_pm", "intra_pm", "slice_rows", "pcm_zero")]
+                 "part_pm", "intra_pm", "slice_rows", "pcm_zero", "intra_types")]
 
 
 EXT_DEFAULT = dict(nrefs=0, max_ref=1, skip_pm=250, cbp_pm=600, big_pm=20, mv_range=64,
                    slice_qp_delta=0, qp_jitter=3, ref_idc=0, bad_mb=-1, bad_type=0,
-                   list_mod=0, part_pm=0, intra_pm=0, slice_rows=0, pcm_zero=0)
+                   list_mod=0, part_pm=0, intra_pm=0, slice_rows=0, pcm_zero=0, intra_types=0)
 
 
 def ext_slice(oracle, cfg, w, h, seed, **kw):

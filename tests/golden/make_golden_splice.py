@@ -42,6 +42,11 @@ EXT = [  # stand-in encoder parameters for 20x20-MB external slices
     dict(part_pm=600),
     dict(part_pm=1000, nrefs=3, max_ref=2, skip_pm=0, cbp_pm=800, mv_range=900),
     dict(part_pm=700, nrefs=1, max_ref=0, skip_pm=300),
+    # intra MBs in P slices (the walker's I_4x4 / I_16x16 paths, :1668-1735;
+    # no I_PCM: the walker resets an I_PCM MB's TotalCoeffs to 0, :1745,
+    # where 9.2.1 counts 16, so it would misread the nC of its neighbours)
+    dict(intra_pm=400, intra_types=3, cbp_pm=800),
+    dict(intra_pm=250, intra_types=3, skip_pm=300, part_pm=300, qp_jitter=6),
 ]
 # composed frames: (offset, mode, rect) on a 320x320 stream scrolling 490..500
 SPLICED = [(490 + i, i % 2, rect) for i, rect in enumerate(
@@ -50,6 +55,12 @@ SPLICED = [(490 + i, i % 2, rect) for i, rect in enumerate(
 # the same with partitioned external MBs (scrolling on past the waypoint)
 SPLICED_PART = [(501 + i, i % 2, rect) for i, rect in enumerate(
     [(3, 4, 8, 6), (0, 0, 20, 20), (19, 0, 1, 20), (6, 6, 9, 9)])]
+
+
+# composed frames with intra MBs spliced from one-slice and multi-slice
+# external pictures (scrolling on)
+SPLICED_INTRA = [(505 + i, i % 2, rect, rows) for i, (rect, rows) in enumerate(
+    [((3, 4, 8, 6), 0), ((0, 0, 20, 20), 2), ((5, 5, 10, 10), 1), ((2, 12, 16, 8), 3)])]
 
 
 def _stop_bit(rbsp):
@@ -87,6 +98,23 @@ def cases(oracle):
         yield dict(kind="composed", case=k, off=off, mode=mode, rect=list(rect), nrefs=H["nrefs"],
                    ext_sha256=hashlib.sha256(ext).hexdigest(), sha256=hashlib.sha256(nal).hexdigest(),
                    nal_bytes=len(nal), mb_start_bit=b.p, stop_bit=_stop_bit(rbsp)), nal, rbsp
+    for k, (off, mode, rect, rows) in enumerate(SPLICED_INTRA):
+        if oracle.or_needs_waypoint(ctypes.byref(c), off):
+            oracle.or_waypoint_nal(buf, len(buf), ctypes.byref(c), off)
+        nrefs = 2 + c.nwp
+        ext = ext_slice(oracle, c, rect[2], rect[3], 9000 + k, nrefs=nrefs, max_ref=nrefs - 1,
+                        skip_pm=300, cbp_pm=700, big_pm=30, qp_jitter=4, intra_pm=350, intra_types=3,
+                        slice_rows=rows)
+        sp = splice_of(*rect, ext)
+        n = oracle.or_splice_scroll_nal(buf, len(buf), ctypes.byref(c), off, None, 0, mode,
+                                        ctypes.byref(sp), ctypes.byref(err))
+        assert err.value == 0 and n > 0
+        nal = bytes(buf[:n])
+        H, b, rbsp = hp.slice_header(nal)
+        yield dict(kind="composed-intra", case=k, off=off, mode=mode, rect=list(rect), slice_rows=rows,
+                   nrefs=H["nrefs"], ext_sha256=hashlib.sha256(ext).hexdigest(),
+                   sha256=hashlib.sha256(nal).hexdigest(), nal_bytes=len(nal), mb_start_bit=b.p,
+                   stop_bit=_stop_bit(rbsp)), nal, rbsp
 
 
 def main():

@@ -557,12 +557,24 @@ def _parts(mbt, sub):
     return out
 
 
+GOLOMB_TO_INTRA_CBP = [47, 31, 15, 0, 23, 27, 29, 30, 7, 11, 13, 14, 39, 43, 45, 46, 16, 3, 5, 10, 12, 19,
+                       21, 26, 28, 35, 37, 42, 44, 1, 2, 4, 8, 17, 18, 20, 24, 6, 9, 22, 25, 32, 33, 34,
+                       36, 40, 38, 41]
+
+
 class _BlockField:
-    """motion (ref, mx, my) per 4x4 block of a picture of mbw x mbh MBs"""
+    """motion (ref, mx, my) per 4x4 block of a picture of mbw x mbh MBs;
+    sid[m]: the slice of MB m (another slice's MB is unavailable); an intra
+    MB's blocks are (-1, 0, 0)"""
 
     def __init__(self, mbw, mbh):
         self.mbw = mbw
         self.f = [[None] * (4 * mbw) for _ in range(4 * mbh)]
+        self.sid = [None] * (mbw * mbh)
+        self.cur = 0
+
+    def avail(self, nx, ny):
+        return 0 <= nx < self.mbw and ny >= 0 and self.sid[ny * self.mbw + nx] == self.cur
 
     def nb(self, x, y, cx, cy, done):
         """block (cx, cy) relative to MB (x, y); inside the MB only once decoded"""
@@ -571,7 +583,7 @@ class _BlockField:
         if cy >= 0 and cx >= 0:
             return self.f[4 * y + cy][4 * x + cx] if (4 * cy + cx) in done else None
         nx, ny = x + (-1 if cx < 0 else (1 if cx >= 4 else 0)), y + (-1 if cy < 0 else 0)
-        if nx < 0 or ny < 0 or nx >= self.mbw:
+        if not self.avail(nx, ny):
             return None
         return self.f[4 * ny + (cy % 4)][4 * nx + (cx % 4)]
 
@@ -605,135 +617,252 @@ def mvp_part(F, x, y, done, mbt, p, ref):
     return mvp_spec(A, B, C, ref)
 
 
+def nal_units(data):
+    """the NAL units of an Annex-B buffer (start codes dropped, trailing zero
+    bytes trimmed); a buffer without a start code is one NAL"""
+    if not (data[:3] == b"\x00\x00\x01" or data[:4] == b"\x00\x00\x00\x01"):
+        return [bytes(data)]
+    out, i, starts = [], 0, []
+    while True:
+        j = data.find(b"\x00\x00\x01", i)
+        if j < 0:
+            break
+        starts.append(j + 3)
+        i = j + 3
+    for k, a in enumerate(starts):
+        e = starts[k + 1] - 3 if k + 1 < len(starts) else len(data)
+        u = data[a:e]
+        out.append(u.rstrip(b"\x00") if k + 1 < len(starts) else u)
+    return out
+
+
+def _rbsp_stop(d):
+    for i in range(len(d) - 1, -1, -1):
+        if d[i]:
+            return 8 * i + 7 - ((d[i] & -d[i]).bit_length() - 1)
+    return -1
+
+
 def decode_p_slice(nal, w, h, predictor="spec", log2_mfn=4, poc_type=2, log2_poc=4, deblock=1,
                    nrefs_default=2, trace=None):
     """-> (header, mbs[y][x] = dict(ref, mx, my, skip, cbp, qp, luma, cdc, cac,
-    mbt, sub, blocks))
+    mbt, sub, blocks, intra, modes, cmode, dc16, pcm))
 
-    nal: Annex-B NAL (start code optional).  Unavailable neighbours are the
-    picture edges only (one slice per picture).  mbt: the mb_type (0..4),
-    blocks: (ref, mx, my) per 4x4 block in raster order; ref / mx / my are
-    block 0's."""
-    if nal[:4] == b"\x00\x00\x00\x01":
-        nal = nal[4:]
-    elif nal[:3] == b"\x00\x00\x01":
-        nal = nal[3:]
-    ref_idc, nut = nal[0] >> 5, nal[0] & 31
-    assert nut == 1, "coded slice of a non-IDR picture"
-    b = Bits(ebsp_to_rbsp(nal[1:]))
-    H = {"first_mb": b.ue(), "slice_type": b.ue(), "pps": b.ue(), "frame_num": b.u(log2_mfn)}
-    if poc_type == 0:
-        H["poc"] = b.u(log2_poc)
-    nrefs = nrefs_default
-    if b.u(1):
-        nrefs = b.ue() + 1
-    H["nrefs"] = nrefs
-    H["list_mod"] = b.u(1)
-    if H["list_mod"]:                            # ref_pic_list_modification (waypoints)
-        while True:
-            idc = b.ue()
-            if idc == 3:
-                break
-            b.ue()
-    if ref_idc and b.u(1):
-        while True:
-            op = b.ue()
-            if op == 0:
-                break
-            if op in (1, 3):
-                b.ue()
-            if op in (2, 3, 6):
-                b.ue()
-            if op == 4:
-                b.ue()
-    qp = 26 + b.se()
-    H["qp"] = qp
-    if deblock:
-        H["deblock_idc"] = b.ue()
-        if H["deblock_idc"] != 1:
-            b.se(); b.se()
-    pred = mvp_spec if predictor == "spec" else mvp_ref
+    nal: the picture's slices as Annex-B bytes (several NAL units one after
+    the other; a single NAL may come without a start code).  An MB of another
+    slice, or past the picture's edge, is unavailable.  mbt: the mb_type
+    (0..4 inter, 5..30 intra), blocks: (ref, mx, my) per 4x4 block in raster
+    order (intra: (-1, 0, 0)); ref / mx / my are block 0's.  intra: 0, 1
+    I_4x4 (modes: Intra4x4PredMode per raster block), 2 I_16x16 (modes[0]:
+    its luma mode, dc16: the DC levels; luma holds the AC levels from scan
+    index 1), 3 I_PCM (pcm: its 384 sample bytes); cmode:
+    intra_chroma_pred_mode."""
     mbw, mbh = w // 16, h // 16
     F = _BlockField(mbw, mbh)
     mbs = [[None] * mbw for _ in range(mbh)]
     tcs = [[None] * mbw for _ in range(mbh)]
-    m, nmb = 0, mbw * mbh
+    im = [[None] * mbw for _ in range(mbh)]          # Intra4x4PredModes (raster) of I_4x4 MBs
+    pred = mvp_spec if predictor == "spec" else mvp_ref
+    m, nmb, H0 = 0, mbw * mbh, None
+    for si, unit in enumerate(nal_units(nal)):
+        ref_idc, nut = unit[0] >> 5, unit[0] & 31
+        assert nut == 1, "coded slice of a non-IDR picture"
+        rb = ebsp_to_rbsp(unit[1:])
+        stop = _rbsp_stop(rb)
+        b = Bits(rb)
+        H = {"first_mb": b.ue(), "slice_type": b.ue(), "pps": b.ue(), "frame_num": b.u(log2_mfn)}
+        assert H["first_mb"] == m, "slices in MB order"
+        if poc_type == 0:
+            H["poc"] = b.u(log2_poc)
+        nrefs = nrefs_default
+        if b.u(1):
+            nrefs = b.ue() + 1
+        H["nrefs"] = nrefs
+        H["list_mod"] = b.u(1)
+        if H["list_mod"]:                        # ref_pic_list_modification (waypoints)
+            while True:
+                idc = b.ue()
+                if idc == 3:
+                    break
+                b.ue()
+        if ref_idc and b.u(1):
+            while True:
+                op = b.ue()
+                if op == 0:
+                    break
+                if op in (1, 3):
+                    b.ue()
+                if op in (2, 3, 6):
+                    b.ue()
+                if op == 4:
+                    b.ue()
+        qp = 26 + b.se()
+        H["qp"] = qp
+        if deblock:
+            H["deblock_idc"] = b.ue()
+            if H["deblock_idc"] != 1:
+                b.se(); b.se()
+        if H0 is None:
+            H0 = H
+        F.cur = si
 
-    def te():
-        return (1 - b.u(1)) if nrefs == 2 else (b.ue() if nrefs > 2 else 0)
+        def te():
+            return (1 - b.u(1)) if nrefs == 2 else (b.ue() if nrefs > 2 else 0)
 
-    while m < nmb:
-        run = b.ue()
-        for _ in range(run):
+        first = True
+        while first or b.p < stop:
+            first = False
+            run = b.ue()
+            for _ in range(run):
+                y, x = divmod(m, mbw)
+                assert y < mbh, "mb_skip_run past the picture"
+                F.sid[m] = si
+                A, B_, C = F.mb16(x, y)
+                if A is None or B_ is None or (A[0] == 0 and A[1:] == (0, 0)) or (B_[0] == 0 and B_[1:] == (0, 0)):
+                    mv = (0, 0)
+                else:
+                    mv = mvp_spec(A, B_, C, 0)
+                F.set(x, y, 0, 0, 4, 4, (0,) + mv, set())
+                tcs[y][x] = [0] * 24
+                mbs[y][x] = dict(ref=0, mx=mv[0], my=mv[1], skip=True, cbp=0, qp=qp, mbt=0, sub=None,
+                                 blocks=[(0,) + mv] * 16, intra=0,
+                                 luma=[[0] * 16 for _ in range(16)], cdc=[[0] * 4] * 2,
+                                 cac=[[[0] * 15 for _ in range(4)] for _ in range(2)])
+                m += 1
+            if b.p >= stop:
+                break
             y, x = divmod(m, mbw)
-            assert y < mbh, "mb_skip_run past the picture"
-            mv = pskip_mv(*F.mb16(x, y))
-            F.set(x, y, 0, 0, 4, 4, (0,) + mv, set())
-            tcs[y][x] = [0] * 24
-            mbs[y][x] = dict(ref=0, mx=mv[0], my=mv[1], skip=True, cbp=0, qp=qp, mbt=0, sub=None,
-                             blocks=[(0,) + mv] * 16,
-                             luma=[[0] * 16 for _ in range(16)], cdc=[[0] * 4] * 2,
-                             cac=[[[0] * 15 for _ in range(4)] for _ in range(2)])
-            m += 1
-        if m >= nmb:
-            break
-        y, x = divmod(m, mbw)
-        if trace is not None:
-            trace.append((m, b.p))
-        mbt = b.ue()
-        assert mbt <= 4, "an inter mb_type"
-        sub = [b.ue() for _ in range(4)] if mbt >= 3 else None
-        assert sub is None or max(sub) <= 3
-        nref = 1 if mbt == 0 else (4 if mbt >= 3 else 2)
-        refs = [0] * 4 if mbt == 4 else [te() for _ in range(nref)]
-        done = set()
-        if mbt == 0:
-            dx, dy = b.se(), b.se()
-            px, py = pred(*F.mb16(x, y), refs[0])
-            F.set(x, y, 0, 0, 4, 4, (refs[0], px + dx, py + dy), done)
-        else:
-            for p in _parts(mbt, sub):
-                dx, dy = b.se(), b.se()
-                rf = refs[p[4]]
-                px, py = mvp_part(F, x, y, done, mbt, p, rf)
-                F.set(x, y, p[0], p[1], p[2], p[3], (rf, px + dx, py + dy), done)
-        blocks = [F.f[4 * y + k // 4][4 * x + k % 4] for k in range(16)]
-        cbp = GOLOMB_TO_INTER_CBP[b.ue()]
-        t = [0] * 24
-        luma = [[0] * 16 for _ in range(16)]
-        cdc = [[0] * 4 for _ in range(2)]
-        cac = [[[0] * 15 for _ in range(4)] for _ in range(2)]
-        left = tcs[y][x - 1] if x > 0 else None
-        top = tcs[y - 1][x] if y > 0 else None
-        if cbp:
-            qp = (qp + b.se() + 52) % 52
-            for blk in range(16):
-                q8, q4 = divmod(blk, 4)
-                bx, by = (q8 % 2) * 2 + q4 % 2, (q8 // 2) * 2 + q4 // 2
-                r = 4 * by + bx
-                if not cbp & (1 << q8):
-                    continue
+            F.sid[m] = si
+            if trace is not None:
+                trace.append((m, b.p))
+            left = tcs[y][x - 1] if F.avail(x - 1, y) else None
+            top = tcs[y - 1][x] if F.avail(x, y - 1) else None
+            mbt = b.ue()
+            assert mbt <= 30, "a P-slice mb_type"
+            t = [0] * 24
+            luma = [[0] * 16 for _ in range(16)]
+            cdc = [[0] * 4 for _ in range(2)]
+            cac = [[[0] * 15 for _ in range(4)] for _ in range(2)]
+
+            def luma_nc(r):
+                bx, by = r % 4, r // 4
                 nA = t[r - 1] if bx > 0 else (left[r + 3] if left else -1)
                 nB = t[r - 4] if by > 0 else (top[r + 12] if top else -1)
-                luma[r], t[r] = cavlc_block(b, _nc(nA, nB), 16)
-            if cbp >> 4:
-                for p in range(2):
-                    cdc[p], _ = cavlc_block(b, -1, 4)
-                if (cbp >> 4) == 2:
+                return _nc(nA, nB)
+
+            def chroma(cbpc):
+                if cbpc:
                     for p in range(2):
-                        for k in range(4):
-                            bx, by = k % 2, k // 2
-                            i = 16 + 4 * p + k
-                            nA = t[i - 1] if bx > 0 else (left[i + 1] if left else -1)
-                            nB = t[i - 2] if by > 0 else (top[i + 2] if top else -1)
-                            cac[p][k], t[i] = cavlc_block(b, _nc(nA, nB), 15)
-        tcs[y][x] = t
-        mbs[y][x] = dict(ref=blocks[0][0], mx=blocks[0][1], my=blocks[0][2], skip=False, cbp=cbp, qp=qp,
-                         mbt=mbt, sub=sub, blocks=blocks, luma=luma, cdc=cdc, cac=cac)
-        m += 1
-    assert b.u(1) == 1, "stop bit"
-    while b.p & 7:
-        assert b.u(1) == 0
-    while b.p < 8 * len(b.d):
-        assert b.u(8) == 0, "trailing bytes"
-    return H, mbs
+                        cdc[p], _ = cavlc_block(b, -1, 4)
+                    if cbpc == 2:
+                        for p in range(2):
+                            for k in range(4):
+                                bx, by = k % 2, k // 2
+                                i = 16 + 4 * p + k
+                                nA = t[i - 1] if bx > 0 else (left[i + 1] if left else -1)
+                                nB = t[i - 2] if by > 0 else (top[i + 2] if top else -1)
+                                cac[p][k], t[i] = cavlc_block(b, _nc(nA, nB), 15)
+
+            if mbt >= 5:                         # intra in a P slice (7.3.5)
+                it = mbt - 5
+                d = dict(ref=-1, mx=0, my=0, skip=False, mbt=mbt, sub=None, blocks=[(-1, 0, 0)] * 16,
+                         intra=1 if it == 0 else (3 if it == 25 else 2), modes=None, cmode=None, dc16=None,
+                         pcm=None, cbp=0)
+                F.set(x, y, 0, 0, 4, 4, (-1, 0, 0), set())
+                if it == 25:
+                    while b.p & 7:
+                        assert b.u(1) == 0, "pcm_alignment_zero_bit"
+                    d["pcm"] = bytes(b.u(8) for _ in range(384))
+                    t = [16] * 24
+                    d.update(qp=qp, luma=luma, cdc=cdc, cac=cac)
+                else:
+                    if it == 0:
+                        modes = [None] * 16
+                        for blk in range(16):
+                            q8, q4 = divmod(blk, 4)
+                            bx, by = (q8 % 2) * 2 + q4 % 2, (q8 // 2) * 2 + q4 // 2
+                            r = 4 * by + bx
+
+                            def nmode(nx, ny, rr):
+                                if not F.avail(nx, ny):
+                                    return None
+                                mm = im[ny][nx]
+                                return 2 if mm is None else mm[rr]
+                            mA = modes[r - 1] if bx else nmode(x - 1, y, r + 3)
+                            mB = modes[r - 4] if by else nmode(x, y - 1, r + 12)
+                            pm = 2 if mA is None or mB is None else min(mA, mB)
+                            if b.u(1):
+                                modes[r] = pm
+                            else:
+                                rem = b.u(3)
+                                modes[r] = rem if rem < pm else rem + 1
+                        im[y][x] = modes
+                        d["modes"] = modes
+                    else:
+                        d["modes"] = [(it - 1) % 4]
+                    d["cmode"] = b.ue()
+                    if it == 0:
+                        cbp = GOLOMB_TO_INTRA_CBP[b.ue()]
+                    else:
+                        cbp = (15 if it - 1 >= 12 else 0) | (((it - 1) // 4) % 3) << 4
+                    d["cbp"] = cbp
+                    if cbp or it != 0:
+                        qp = (qp + b.se() + 52) % 52
+                        if it != 0:
+                            d["dc16"], _ = cavlc_block(b, luma_nc(0), 16)
+                        for blk in range(16):
+                            q8, q4 = divmod(blk, 4)
+                            bx, by = (q8 % 2) * 2 + q4 % 2, (q8 // 2) * 2 + q4 // 2
+                            r = 4 * by + bx
+                            if not cbp & (1 << q8):
+                                continue
+                            if it == 0:
+                                luma[r], t[r] = cavlc_block(b, luma_nc(r), 16)
+                            else:
+                                ac, t[r] = cavlc_block(b, luma_nc(r), 15)
+                                luma[r] = [0] + ac
+                        chroma(cbp >> 4)
+                    d.update(qp=qp, luma=luma, cdc=cdc, cac=cac)
+                tcs[y][x] = t
+                mbs[y][x] = d
+                m += 1
+                continue
+            sub = [b.ue() for _ in range(4)] if mbt >= 3 else None
+            assert sub is None or max(sub) <= 3
+            nref = 1 if mbt == 0 else (4 if mbt >= 3 else 2)
+            refs = [0] * 4 if mbt == 4 else [te() for _ in range(nref)]
+            done = set()
+            if mbt == 0:
+                dx, dy = b.se(), b.se()
+                px, py = pred(*F.mb16(x, y), refs[0])
+                F.set(x, y, 0, 0, 4, 4, (refs[0], px + dx, py + dy), done)
+            else:
+                for p in _parts(mbt, sub):
+                    dx, dy = b.se(), b.se()
+                    rf = refs[p[4]]
+                    px, py = mvp_part(F, x, y, done, mbt, p, rf)
+                    F.set(x, y, p[0], p[1], p[2], p[3], (rf, px + dx, py + dy), done)
+            blocks = [F.f[4 * y + k // 4][4 * x + k % 4] for k in range(16)]
+            cbp = GOLOMB_TO_INTER_CBP[b.ue()]
+            if cbp:
+                qp = (qp + b.se() + 52) % 52
+                for blk in range(16):
+                    q8, q4 = divmod(blk, 4)
+                    bx, by = (q8 % 2) * 2 + q4 % 2, (q8 // 2) * 2 + q4 // 2
+                    r = 4 * by + bx
+                    if not cbp & (1 << q8):
+                        continue
+                    luma[r], t[r] = cavlc_block(b, luma_nc(r), 16)
+                chroma(cbp >> 4)
+            tcs[y][x] = t
+            mbs[y][x] = dict(ref=blocks[0][0], mx=blocks[0][1], my=blocks[0][2], skip=False, cbp=cbp, qp=qp,
+                             mbt=mbt, sub=sub, blocks=blocks, luma=luma, cdc=cdc, cac=cac, intra=0)
+            m += 1
+        assert b.p == stop, "slice data up to the stop bit"
+        assert b.u(1) == 1, "stop bit"
+        while b.p & 7:
+            assert b.u(1) == 0
+        while b.p < 8 * len(b.d):
+            assert b.u(8) == 0, "trailing bytes"
+    assert m == nmb, "the slices cover the picture"
+    return H0, mbs

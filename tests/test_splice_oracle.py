@@ -71,7 +71,9 @@ def test_ext_slices_parse_like_the_standard_decoder(oracle):
                                dict(mv_range=4000), dict(list_mod=1, nrefs=2, max_ref=1),
                                dict(part_pm=500), dict(part_pm=1000, nrefs=5, max_ref=4, skip_pm=100),
                                dict(part_pm=800, nrefs=1, max_ref=0, mv_range=3000),
-                               dict(part_pm=600, skip_pm=600, cbp_pm=900)]):
+                               dict(part_pm=600, skip_pm=600, cbp_pm=900),
+                               dict(intra_pm=400, cbp_pm=900), dict(intra_pm=300, slice_rows=1, skip_pm=300),
+                               dict(intra_pm=500, slice_rows=2, part_pm=300, qp_jitter=6)]):
         w, h = 5 + seed % 3, 4 + seed % 4
         nal = ext_slice(oracle, c, w, h, 100 + seed, **kw)
         e, mbs = _parse(oracle, c, splice_of(0, 0, w, h, nal))
@@ -82,6 +84,12 @@ def test_ext_slices_parse_like_the_standard_decoder(oracle):
                 d, m = dec[y][x], mbs[y * w + x]
                 assert (m.ref, m.mx, m.my, m.cbp, bool(m.skip)) == \
                     (d["ref"], d["mx"], d["my"], d["cbp"], d["skip"]), (seed, x, y)
+                assert m.intra == d["intra"], (seed, x, y)
+                if m.intra:
+                    assert m.mbt == d["mbt"]
+                    if m.hasqpd:
+                        assert m.qp == d["qp"]
+                    continue
                 assert m.part == min(d["mbt"], 3), (seed, x, y)
                 if m.part == 3:
                     assert [(m.sub >> (2 * i)) & 3 for i in range(4)] == d["sub"]
@@ -114,6 +122,14 @@ def _check_frame(oracle, c, off, rects, mode, sp, buf):
                 e = ext[y - sp.y0][x - sp.x0]
                 assert (g["ref"], g["mx"], g["my"], g["cbp"]) == (e["ref"], e["mx"], e["my"], e["cbp"]), \
                     (off, mode, x, y)
+                if e["intra"]:
+                    # the same intra MB: type, every prediction mode, residual or samples
+                    assert (g["intra"], g["mbt"], g["modes"], g["cmode"], g["dc16"], g["pcm"]) == \
+                        (e["intra"], e["mbt"], e["modes"], e["cmode"], e["dc16"], e["pcm"]), (off, mode, x, y)
+                    if e["intra"] == 2 or e["cbp"]:
+                        assert g["qp"] == e["qp"]
+                    assert (g["luma"], g["cdc"], g["cac"]) == (e["luma"], e["cdc"], e["cac"])
+                    continue
                 # partitionings kept (P_8x8ref0 -> P_8x8), every 4x4 block's motion
                 assert (g["mbt"], g["sub"]) == (min(e["mbt"], 3), e["sub"]) or \
                     (e["skip"] and g["mbt"] == 0), (off, mode, x, y)
@@ -163,6 +179,70 @@ def test_spliced_mbs_decode_to_the_external_mbs(oracle):
         assert k > 0
     # waypoint references, external P_Skip MBs, spliced MBs skipped again
     assert all(v > 0 for v in cov.values()), cov
+
+
+def test_intra_and_multislice_splices(oracle):
+    """external pictures with I_4x4 / I_16x16 / I_PCM MBs, in one slice or a
+    slice per one or two MB rows (neighbours in another slice unavailable:
+    motion, P_Skip, nC, intra mode prediction), spliced in all three modes;
+    every spliced MB decodes to its external MB, every other MB to the hint
+    field; over the 496 waypoint"""
+    rng = random.Random(11)
+    buf = (ctypes.c_uint8 * (1 << 21))()
+    err = ctypes.c_int()
+    w, h = 320, 720
+    c = _cfg(oracle, w, h)
+    cov = dict(i4=0, i16=0, pcm=0, slices=0)
+    for i in range(16):
+        off = 488 + i
+        if oracle.or_needs_waypoint(ctypes.byref(c), off):
+            oracle.or_waypoint_nal(buf, len(buf), ctypes.byref(c), off)
+        refs = _refs(c)
+        sw, sh = rng.randint(3, 9), rng.randint(3, 7)
+        x0, y0 = rng.randint(0, w // 16 - sw), rng.randint(0, h // 16 - sh)
+        rows = rng.choice([0, 1, 2])
+        kw = dict(nrefs=len(refs), max_ref=len(refs) - 1, skip_pm=rng.choice([0, 200, 500]),
+                  cbp_pm=rng.choice([500, 1000]), big_pm=rng.choice([0, 50]), mv_range=rng.choice([8, 300]),
+                  slice_qp_delta=rng.randint(-5, 5), qp_jitter=rng.choice([0, 4]),
+                  part_pm=rng.choice([0, 300]), intra_pm=rng.choice([300, 700]), slice_rows=rows,
+                  pcm_zero=i % 4 == 3)
+        nal = ext_slice(oracle, c, sw, sh, 2000 + i, **kw)
+        sp = splice_of(x0, y0, sw, sh, nal)
+        e, _ = _parse(oracle, c, sp)
+        assert e == 0, (i, e)
+        rects = random_hints(rng, w // 16, h // 16, refs, nmax=3) if i % 3 == 0 else []
+        for mode in (EXACT, PSKIP, SPEC):
+            got, ext = _check_frame(oracle, c, off, rects, mode, sp, buf)
+        cov["i4"] += sum(m["intra"] == 1 for row in ext for m in row)
+        cov["i16"] += sum(m["intra"] == 2 for row in ext for m in row)
+        cov["pcm"] += sum(m["intra"] == 3 for row in ext for m in row)
+        cov["slices"] += rows > 0 and sh > rows
+        k = oracle.or_splice_scroll_nal(buf, len(buf), ctypes.byref(c), off, None, 0, EXACT,
+                                        ctypes.byref(sp), ctypes.byref(err))
+        assert k > 0
+    assert all(v > 0 for v in cov.values()), cov
+
+
+def test_multislice_rules(oracle):
+    """slices must start where the previous one ended and cover the picture"""
+    buf = (ctypes.c_uint8 * (1 << 18))()
+    err = ctypes.c_int()
+    c = _cfg(oracle, 256, 256)
+    nal = ext_slice(oracle, c, 4, 4, 5, slice_rows=1)
+    units = P.nal_units(nal)
+    assert len(units) == 4
+
+    def compose(data):
+        c2 = OrCfg.from_buffer_copy(c)
+        oracle.or_splice_scroll_nal(buf, len(buf), ctypes.byref(c2), 40, None, 0, EXACT,
+                                    ctypes.byref(splice_of(2, 2, 4, 4, data)), ctypes.byref(err))
+        return err.value
+
+    sc = b"\x00\x00\x00\x01"
+    assert compose(nal) == 0
+    assert compose(b"".join(sc + u for u in units[:3])) == ERR_SYNTAX            # a row missing
+    assert compose(b"".join(sc + u for u in (units[0], units[2], units[1], units[3]))) == ERR_HEADER
+    assert compose(b"".join(sc + u + b"\x00\x00" for u in units)) == 0       # trailing zero bytes
 
 
 def test_splice_at_picture_corners_and_whole_picture(oracle):
@@ -277,7 +357,7 @@ def test_reference_parser_accepts_spliced_nals(oracle):
     import make_golden_splice as mg
     fx = json.load(open(os.path.join(here, "golden", "splice_ref.json")))
     assert all(c["ref_status"] == 0 and c["ref_end_bit"] == c["stop_bit"] for c in fx)
-    assert {c["kind"] for c in fx} == {"external", "composed"}
+    assert {c["kind"] for c in fx} == {"external", "composed", "composed-intra"}
     refso = os.path.join(os.path.dirname(here), "oracle", "_ref", "libref_cavlc.so")
     ref = ctypes.CDLL(refso) if os.path.exists(refso) else None
     got = list(mg.cases(oracle))

@@ -83,6 +83,11 @@ WORKLOADS = {
                             "(400x400 px: a 360x360 preview + margin) spliced at MB (28, 10); "
                             "the slices are the dynamic rect coder's output for 400x400 "
                             "pictures, resident in HBM, parsed again every step"),
+    "p720splicerows": dict(w=1280, h=720, streams=256, frames=16, rect=None, splice=(28, 10, 25, 25),
+                           slice_rows=True,
+                           desc="pre-encoded MB splice, one slice per MB row (SURVEY 8f row 2): as "
+                                "p720splice, the 25x25-MB external picture as 25 Annex-B slices "
+                                "(first_mb_in_slice 25 r), one parse wave per slice"),
     "p720hint": dict(w=1280, h=720, streams=256, frames=16, rect=None, hints=True,
                      desc="UI hints (SURVEY 8f row 1): 256 concurrent 1280x720 streams, scroll "
                           "frames with a static chrome / side panel / horizontal carousel "
@@ -520,6 +525,61 @@ def external_slices(hs, S, F, sw, sh, first, device):
     return e, ptrs
 
 
+def _set_first_mb(nal, k):
+    """an Annex-B slice NAL whose first_mb_in_slice is 0 with it set to k:
+    the RBSP's bits after that ue(0) shifted behind ue(k), re-aligned and
+    re-escaped (input preparation, outside the timed region)"""
+    import re
+    if k == 0:
+        return nal
+    i = nal.index(b"\x00\x00\x01") + 3
+    rbsp = nal[i + 1:].replace(b"\x00\x00\x03", b"\x00\x00")
+    v = int.from_bytes(rbsp, "big")
+    tz = (v & -v).bit_length() - 1
+    v >>= tz
+    nb = 8 * len(rbsp) - tz                          # through rbsp_stop_one_bit
+    assert (v >> (nb - 1)) & 1, "first_mb_in_slice must be 0"
+    x = k + 1
+    L = 2 * x.bit_length() - 1
+    v = (x << (nb - 1)) | (v & ((1 << (nb - 1)) - 1))
+    nb += L - 1
+    pad = (-nb) % 8
+    out = (v << pad).to_bytes((nb + pad) // 8, "big")
+    out = re.sub(rb"\x00\x00(?=[\x00-\x03])", b"\x00\x00\x03", out)
+    return b"\x00\x00\x00\x01" + nal[i:i + 1] + out
+
+
+def external_row_slices(hs, torch, S, F, sw, sh, first, device):
+    """external pictures of sw x sh MBs coded as one slice per MB row: row r
+    of frame (s, f) is the dynamic rect coder's NAL for an sw x 1-MB picture
+    (stream s * sh + r) -- a slice predicts nothing across its boundary, so a
+    one-row picture's slice data is that row's slice -- with its
+    first_mb_in_slice set to r * sw.  The pictures sit in one device buffer.
+    Returns (keep-alive objects, per (s, f) device pointer and size, per (s,
+    f) host bytes)."""
+    import numpy as np
+    e, ptrs = external_slices(hs, S * sh, F, sw, 1, first * sh, device)
+    rows = {}
+    for ss in range(S * sh):
+        out, pos = e.output(ss), 0
+        for f in range(F):
+            n = ptrs[(ss, f)][1]
+            rows[(ss, f)] = bytes(out[pos:pos + n])
+            pos += n
+    e.close()
+    host, pool, offs = {}, bytearray(), {}
+    for s in range(S):
+        for f in range(F):
+            pic = b"".join(_set_first_mb(rows[(s * sh + r, f)], r * sw) for r in range(sh))
+            host[(s, f)] = pic
+            offs[(s, f)] = len(pool)
+            pool += pic
+            pool += bytes((-len(pool)) % 16)
+    dev = torch.from_numpy(np.frombuffer(bytes(pool), np.uint8).copy()).to(f"cuda:{device}")
+    base = dev.data_ptr()
+    return dev, {k: (base + offs[k], len(host[k])) for k in host}, host
+
+
 def cpu_baseline_splice(wl, slices, nstreams=16, nframes=64):
     """oracle/splice_oracle.c on one host core over a bounded sample: the
     same external slices (copied to the host) into nstreams x nframes frames"""
@@ -561,7 +621,17 @@ def run_splice(args, wl, rank, world, local, dist):
     S, F, W, H = wl["streams"], wl["frames"], wl["w"], wl["h"]
     x0, y0, sw, sh = wl["splice"]
     first, _ = shard_streams(rank, world, S)
-    e, ptrs = external_slices(hs, S, F, sw, sh, first, local)
+    if wl.get("slice_rows"):
+        e, ptrs, ext_host = external_row_slices(hs, torch, S, F, sw, sh, first, local)
+    else:
+        e, ptrs = external_slices(hs, S, F, sw, sh, first, local)
+        ext_host = {}
+        for s in range(S):
+            out, pos = e.output(s), 0
+            for f in range(F):
+                n = ptrs[(s, f)][1]
+                ext_host[(s, f)] = bytes(out[pos:pos + n])
+                pos += n
     ext_bytes = sum(n for _, n in ptrs.values())
     entries = [(s, f, x0, y0, sw, sh, p, n) for (s, f), (p, n) in ptrs.items()]
     per_frame = 2 * (64 + (W // 16) * (H // 16)) + 2 * ext_bytes // (S * F) + 4096
@@ -601,7 +671,7 @@ def run_splice(args, wl, rank, world, local, dist):
     el = max_over_ranks(t1 - t0, dist)
     value = S * F * args.steps * world / el
     verified, vdetail = (None, None) if args.no_verify else \
-        verify_splice_step(b, e, ptrs, wl, first, args.warmup + args.steps)
+        verify_splice_step(b, ext_host, wl, first, args.warmup + args.steps)
     if rank == 0:
         n = max(n_launch, 1)
         kms = {"plan": plan_ms / n, "emit": emit_ms / n, "splice_stage": stage_ms / n,
@@ -611,7 +681,8 @@ def run_splice(args, wl, rank, world, local, dist):
         alg_bytes = 2 * ext_bytes + rbsp_tot
         achieved = alg_bytes / (kms["splice_stage"] * 1e-3) / 1e9
         out = {
-            "metric": "spliced composed frames/sec (1280x720 + 25x25-MB external slice)",
+            "metric": "spliced composed frames/sec (1280x720 + 25x25-MB external " +
+                      ("picture, one slice per MB row)" if wl.get("slice_rows") else "slice)"),
             "value": round(value, 1), "unit": "frames/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(1000.0 * el / args.steps, 4), "higher_is_better": True,
@@ -629,26 +700,21 @@ def run_splice(args, wl, rank, world, local, dist):
             "verified": verified, "verify": vdetail, "revision": revision(),
         }
         if world == 1 and not args.no_cpu:
-            host = [e.output(s)[:] for s in range(min(S, 4))]
-            slices = []
-            for s in range(min(S, 4)):
-                pos = 0
-                for f in range(F):
-                    n = ptrs[(s, f)][1]
-                    slices.append(host[s][pos:pos + n])
-                    pos += n
+            slices = [ext_host[(s, f)] for s in range(min(S, 4)) for f in range(F)]
             out["cpu_baseline"] = cpu_baseline_splice(wl, slices)
         print(json.dumps(out), flush=True)
     b.close()
-    e.close()
+    if not wl.get("slice_rows"):
+        e.close()
     if verified is False:
         sys.exit(3)
 
 
-def verify_splice_step(b, e, ptrs, wl, first, passes, nstreams=8):
-    """CHECKER (after timing): the last step's bytes of the first nstreams
-    streams against oracle/splice_oracle.c (the external slices copied back
-    from the encoder's arena; the splice path's default SCROLL_HINT_SPEC)"""
+def verify_splice_step(b, ext_host, wl, first, passes, nstreams=None):
+    """CHECKER (after timing): the last step's bytes of every stream (or the
+    first nstreams) against oracle/splice_oracle.c (the external slices
+    copied back from the encoder's arena; the splice path's default
+    SCROLL_HINT_SPEC)"""
     sys.path.insert(0, os.path.join(HERE, "tests"))
     import stepcheck
     from dynhelp import OrCfg, splice_of
@@ -656,13 +722,12 @@ def verify_splice_step(b, e, ptrs, wl, first, passes, nstreams=8):
     oracle = stepcheck.load_oracle()
     S, F, W, H = wl["streams"], wl["frames"], wl["w"], wl["h"]
     x0, y0, sw, sh = wl["splice"]
-    ns = min(S, nstreams)
+    ns = S if nstreams is None else min(S, nstreams)
     offs = synthetic_offsets(first, ns, F, H)
     buf = (ctypes.c_uint8 * (8 << 20))()
     err = ctypes.c_int()
     want = []
     for s in range(ns):
-        host, pos = e.output(s), 0
         c = OrCfg()
         oracle.or_cfg_init(ctypes.byref(c), W, H)
         c.frame_num = 2
@@ -671,9 +736,7 @@ def verify_splice_step(b, e, ptrs, wl, first, passes, nstreams=8):
                 oracle.or_compose_state(ctypes.byref(c), int(offs[s, f]), 0)
         o = bytearray()
         for f in range(F):
-            n = ptrs[(s, f)][1]
-            sp = splice_of(x0, y0, sw, sh, host[pos:pos + n])
-            pos += n
+            sp = splice_of(x0, y0, sw, sh, ext_host[(s, f)])
             k = oracle.or_compose_splice(buf, len(buf), ctypes.byref(c), int(offs[s, f]), 0, None, 0,
                                          2, ctypes.byref(sp), ctypes.byref(err))
             if err.value or not k:
@@ -1028,12 +1091,12 @@ def build_compose_batch(hs, wl, first, device):
     return b
 
 
-def verify_last_step(b, wl, first, passes, hint_streams=32):
+def verify_last_step(b, wl, first, passes, hint_streams=None):
     """CHECKER (runs after timing): the bytes of the last composed step
     against the CPU oracle (tests/stepcheck.py -> oracle/verify_oracle.c on
-    all usable host cores).  Every stream for the rect and P-only workloads,
-    the first `hint_streams` streams for the UI overlay (single-threaded
-    oracle).  -> (ok, detail)"""
+    all usable host cores).  Every stream (the UI overlay: every stream, or
+    the first `hint_streams`, through the single-threaded hint oracle).
+    -> (ok, detail)"""
     sys.path.insert(0, os.path.join(HERE, "tests"))
     import stepcheck
     t0 = time.perf_counter()
@@ -1041,7 +1104,7 @@ def verify_last_step(b, wl, first, passes, hint_streams=32):
     offs = synthetic_offsets(first, S, F, H)
     oracle = stepcheck.load_oracle()
     if wl.get("hints"):
-        want, ns = stepcheck.oracle_hint_step(oracle, W, H, offs[:hint_streams], passes,
+        want, ns = stepcheck.oracle_hint_step(oracle, W, H, offs[:hint_streams or S], passes,
                                               lambda s, f: ui_hints(first + s, f, W, H), 1)
         ok, d = stepcheck.compare_streams(b, want)
         d["sample"] = f"first {ns} of {S} streams"

@@ -16,7 +16,8 @@
 namespace scroll {
 namespace hint {
 
-/* (ref, mv) of an MB, mv in quarter pels; ref -1 = not available */
+/* (ref, mv) of an MB, mv in quarter pels; ref -1 = not available, -2 = an
+ * intra MB (available with refIdx -1, mv 0: it matches no reference) */
 struct Mv {
     int ref, mx, my;
 };
@@ -49,7 +50,7 @@ __device__ inline Mv field(const ScrollHintRect *rc, const int32_t *wv, int nr, 
 __device__ inline void predict_ref(const Mv &A, const Mv &B, const Mv &C, int ref, int &px,
                                    int &py)
 {
-    const bool aA = A.ref >= 0, aB = B.ref >= 0, aC = C.ref >= 0;
+    const bool aA = A.ref != -1, aB = B.ref != -1, aC = C.ref != -1;
     const bool mA = aA && A.ref == ref, mB = aB && B.ref == ref, mC = aC && C.ref == ref;
     const int na = (int)aA + (int)aB + (int)aC, nm = (int)mA + (int)mB + (int)mC;
     if (na == 0) {
@@ -74,7 +75,7 @@ __device__ inline int med3(int a, int b, int c) { return max(min(a, b), min(max(
 /* H.264 8.4.1.3 for a 16x16 partition (unavailable: ref -1, mv 0) */
 __device__ inline void predict_spec(Mv A, Mv B, Mv C, int ref, int &px, int &py)
 {
-    if (B.ref < 0 && C.ref < 0 && A.ref >= 0) {          /* 8.4.1.3.1 */
+    if (B.ref == -1 && C.ref == -1 && A.ref != -1) {     /* 8.4.1.3.1 */
         B = A;
         C = A;
     }
@@ -89,11 +90,13 @@ __device__ inline void predict_spec(Mv A, Mv B, Mv C, int ref, int &px, int &py)
     }
 }
 
-/* H.264 8.4.1.1: motion of a P_Skip MB at (x, y) */
-__device__ inline void pskip_mv(int x, int y, const Mv &A, const Mv &B, const Mv &C, int &px,
+/* H.264 8.4.1.1: motion of a P_Skip MB whose left / top neighbour MBs are
+ * available (aA, aB: inside the picture and, in a multi-slice picture, the
+ * same slice) */
+__device__ inline void pskip_mv(bool aA, bool aB, const Mv &A, const Mv &B, const Mv &C, int &px,
                                 int &py)
 {
-    if (x == 0 || y == 0 || (A.ref == 0 && A.mx == 0 && A.my == 0) ||
+    if (!aA || !aB || (A.ref == 0 && A.mx == 0 && A.my == 0) ||
         (B.ref == 0 && B.mx == 0 && B.my == 0)) {
         px = py = 0;
         return;

@@ -163,7 +163,7 @@ __global__ __launch_bounds__(DT) void k_hint_stage(DevStream *__restrict__ st,
             const Mv C = y == 0 ? none : (x + 1 < mbw ? at(m - mbw + 1) : (x > 0 ? at(m - mbw - 1) : none));
             if (spec) {
                 int sx, sy;
-                pskip_mv(x, y, A, B, C, sx, sy);
+                pskip_mv(x > 0, y > 0, A, B, C, sx, sy);
                 coded = !pskip || !(me.ref == 0 && me.mx == sx && me.my == sy);
                 predict_spec(A, B, C, me.ref, px, py);
             } else {

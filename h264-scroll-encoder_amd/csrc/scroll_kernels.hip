@@ -955,7 +955,9 @@ struct ScrollBatch {
     uint32_t *d_sp_rbsp = nullptr;
     SpliceMbRec *d_sp_rec = nullptr;
     int32_t *d_sp_list = nullptr;
-    size_t sp_nal_cap = 0, sp_rbsp_cap = 0, sp_rec_cap = 0, sp_list_cap = 0;
+    SpliceUnit *d_sp_units = nullptr;  /* NAL unit slots (splice_unit_cap per frame) */
+    int sp_ymax = 1;                   /* most unit slots of a frame (parse grid y)  */
+    size_t sp_nal_cap = 0, sp_rbsp_cap = 0, sp_rec_cap = 0, sp_list_cap = 0, sp_units_cap = 0;
     /* stream ingest: scratch, grown on demand */
     uint8_t *d_ing_in = nullptr;
     size_t ing_in_cap = 0;
@@ -1114,6 +1116,7 @@ void scroll_batch_destroy(ScrollBatch *b)
     (void)hipFree(b->d_sp_rbsp);
     (void)hipFree(b->d_sp_rec);
     (void)hipFree(b->d_sp_list);
+    (void)hipFree(b->d_sp_units);
     (void)hipFree(b->d_ing_in);
     (void)hipFree(b->d_ipcm_cnt);
     (void)hipFree(b->d_ipcm_stg);
@@ -1308,8 +1311,8 @@ static int launch(ScrollBatch *b, int nframes, int plan_mode, int nal_max, hipSt
         b->geo.debug = b->debug;
         if (hint) {
             if (b->sp_parse) {
-                if (splice_launch_parse(hs, b->sp_n, b->d_sp_list, b->d_spf, b->d_st, ld_fr,
-                                        b->d_sp_rbsp, b->d_sp_rec)) {
+                if (splice_launch_parse(hs, b->sp_n, b->sp_ymax, b->d_sp_list, b->d_spf, b->d_sp_units,
+                                        b->d_st, ld_fr, b->d_sp_rbsp, b->d_sp_rec)) {
                     set_err("k_splice_parse launch: %s", hipGetErrorString(hipGetLastError()));
                     return SCROLL_ERR_HIP;
                 }
@@ -2154,12 +2157,14 @@ static void hint_release(ScrollBatch *b)
     (void)hipFree(b->d_sp_rbsp);
     (void)hipFree(b->d_sp_rec);
     (void)hipFree(b->d_sp_list);
+    (void)hipFree(b->d_sp_units);
     b->d_spf = nullptr;
     b->d_sp_nal = nullptr;
     b->d_sp_rbsp = nullptr;
     b->d_sp_rec = nullptr;
     b->d_sp_list = nullptr;
-    b->sp_nal_cap = b->sp_rbsp_cap = b->sp_rec_cap = b->sp_list_cap = 0;
+    b->d_sp_units = nullptr;
+    b->sp_nal_cap = b->sp_rbsp_cap = b->sp_rec_cap = b->sp_list_cap = b->sp_units_cap = 0;
     b->h_sp.clear();
     b->sp_n = 0;
     b->sp_dirty = 0;
@@ -2389,7 +2394,8 @@ static int splice_upload(ScrollBatch *b)
     std::vector<SpliceFrame> spf(S * F);
     std::vector<int32_t> list;
     std::vector<uint8_t> pool;
-    size_t words = 0, recs = 0, slot = b->geo.slot_bytes;
+    size_t words = 0, recs = 0, nunits = 0, slot = b->geo.slot_bytes;
+    int ymax = 1;
     std::vector<size_t> pool_off(b->h_sp.size(), 0);
     for (size_t i = 0; i < b->h_sp.size(); ++i) {
         const ScrollBatch::SpliceHost &h = b->h_sp[i];
@@ -2408,8 +2414,11 @@ static int splice_upload(ScrollBatch *b)
             pool.insert(pool.end(), h.nal.begin(), h.nal.end());
             pool.resize((pool.size() + 3) & ~(size_t)3);
         }
-        words += (h.n + 3) / 4 + 2;    /* k_splice_parse zeroes (len + 3) / 4 + 2 words */
+        words += (h.n + 3) / 4 + 2;    /* k_splice_parse's units stay below (len + 2) / 4 + 1 words */
         recs += (size_t)h.w * h.h;
+        o.unit_first = (uint32_t)nunits;
+        nunits += splice_unit_cap(h.w * h.h);
+        ymax = std::max(ymax, (int)splice_unit_cap(h.w * h.h));
         list.push_back((int32_t)i);
         const DevStream &d = b->h_st[i / F];
         slot = std::max(slot, splice_slot_bound(d.w / 16, d.h / 16, h.w, h.h, h.n));
@@ -2421,7 +2430,8 @@ static int splice_upload(ScrollBatch *b)
     if ((rc = sp_grow((void **)&b->d_sp_nal, &b->sp_nal_cap, pool.size(), 1)) ||
         (rc = sp_grow((void **)&b->d_sp_rbsp, &b->sp_rbsp_cap, words, sizeof(uint32_t))) ||
         (rc = sp_grow((void **)&b->d_sp_rec, &b->sp_rec_cap, recs, sizeof(SpliceMbRec))) ||
-        (rc = sp_grow((void **)&b->d_sp_list, &b->sp_list_cap, list.size(), sizeof(int32_t))))
+        (rc = sp_grow((void **)&b->d_sp_list, &b->sp_list_cap, list.size(), sizeof(int32_t))) ||
+        (rc = sp_grow((void **)&b->d_sp_units, &b->sp_units_cap, nunits, sizeof(SpliceUnit))))
         return rc;
     if (slot > b->geo.slot_bytes) {
         /* the new slots first: on failure the old ones, the hints and the
@@ -2448,6 +2458,7 @@ static int splice_upload(ScrollBatch *b)
         HIPCHK(hipMemcpy(b->d_sp_list, list.data(), list.size() * sizeof(int32_t),
                          hipMemcpyHostToDevice));
     b->sp_n = (int)list.size();
+    b->sp_ymax = ymax;
     b->sp_parse = b->sp_n > 0;
     b->sp_dirty = 0;
     return SCROLL_OK;
@@ -2585,10 +2596,10 @@ int scroll_batch_splice_status(ScrollBatch *b, int s, int f, int *status)
 static const char *splice_msg(int e)
 {
     switch (e) {
-    case SCROLL_SPLICE_ERR_NAL: return "not a coded slice of a non-IDR picture";
-    case SCROLL_SPLICE_ERR_HEADER: return "slice header outside the supported syntax";
-    case SCROLL_SPLICE_ERR_MBTYPE: return "an MB other than P_L0_16x16 / P_Skip";
-    case SCROLL_SPLICE_ERR_SYNTAX: return "malformed or truncated slice data, or an MB count other than the rect's";
+    case SCROLL_SPLICE_ERR_NAL: return "not a coded slice of a non-IDR picture (or more than 1,024 slices)";
+    case SCROLL_SPLICE_ERR_HEADER: return "slice header outside the supported syntax, or slices out of order";
+    case SCROLL_SPLICE_ERR_MBTYPE: return "an intra MB whose prediction reads other samples in the composed picture";
+    case SCROLL_SPLICE_ERR_SYNTAX: return "malformed or truncated slice data, or slices not covering the rect's MBs";
     case SCROLL_SPLICE_ERR_REF: return "a ref_idx that is not a valid reference of the frame";
     default: return "unknown";
     }

@@ -12,46 +12,82 @@
 
 #include "engine.h"
 
-#define SPLICE_PIECES 26            /* 16 luma (raster), Cb DC, Cr DC, 4 Cb AC, 4 Cr AC */
+#define SPLICE_PIECES 27            /* 16 luma (raster; I_16x16: AC), Cb DC, Cr DC, 4 Cb AC, 4 Cr AC,
+                                     * I_16x16 luma DC */
 #define SPLICE_MAX_MV 16383         /* |mv| of a spliced MB, quarter pels          */
+#define SPLICE_MAXU 1024            /* NAL units (slices) of one spliced picture   */
+#define SPLICE_REF_INTRA (-2)       /* ref of an intra MB in the motion field:
+                                     * available, never matching (8.4.1.3.1)      */
 #define HINT_MODE_SPLICED 0x100     /* HintFrame.mode bit: k_splice_stage stages it */
 
-/* one spliced frame: rect, its external NAL (device memory), its RBSP in
- * the word pool (MSB-first words), its MB records, the parse status and the
- * last stage's (reference validity), SCROLL_SPLICE_*.  48 bytes. */
+/* unit slots of a spliced picture of nmb MBs: every slice holds an MB, so
+ * slice nmb (if any) is the first one that cannot fit and fails the frame */
+__host__ __device__ static inline uint32_t splice_unit_cap(int nmb)
+{
+    return (uint32_t)(nmb + 1 < SPLICE_MAXU ? nmb + 1 : SPLICE_MAXU);
+}
+
+/* one spliced frame: rect, its external NAL units (device memory), their
+ * RBSPs in the word pool (MSB-first words; unit u's at word ceil(b_u / 4) of
+ * the frame's region), its MB records and unit slots, the parse status and
+ * the last stage's (reference validity), SCROLL_SPLICE_*.  56 bytes. */
 typedef struct {
     int32_t x0, y0, w, h;
     const uint8_t *nal;             /* device bytes: the NAL pool or the caller's */
     uint64_t rbsp_word;             /* words into the RBSP pool                   */
     uint32_t nal_len;
     uint32_t rec_first;             /* first MB record                            */
-    int32_t status;                 /* k_splice_parse                             */
+    int32_t status;                 /* k_splice_fix                               */
     int32_t stage_status;           /* k_splice_stage of the last compose         */
+    uint32_t unit_first;            /* first unit slot                            */
+    int32_t nunits;                 /* NAL units found (k_splice_units; may exceed the slots) */
 } SpliceFrame;
 
-/* one external MB after parsing: motion (quarter pels), cbp, the composed
- * mb_qp_delta, and per piece its TotalCoeff, TrailingOnes and the bits after
- * coeff_token (offset and length in the RBSP).  A partitioned MB (part 1
- * 16x8, 2 8x16, 3 P_8x8 / P_8x8ref0 with sub_mb_type i in bits 2i..2i+1 of
- * sub) also carries the motion of each 4x4 block (raster; mv packed x | y
- * << 16); ref / mx / my are then block 0's.  312 bytes. */
+/* one NAL unit (slice) of a spliced picture: its bytes [b, e) of the
+ * frame's buffer (after the start code, trailing zero bytes trimmed), then
+ * from its parse: first_mb_in_slice, its MB count, status, and for the QP
+ * chain its first MB with mb_qp_delta (-1: none), that MB's QP and the QP of
+ * its last MB with mb_qp_delta.  32 bytes. */
+typedef struct {
+    uint32_t b, e;
+    int32_t first, nmb, status;
+    int32_t fq_mb, fq_qp, last_qp;
+} SpliceUnit;
+
+/* one external MB after parsing: motion (quarter pels; intra: ref
+ * SPLICE_REF_INTRA), cbp, the composed mb_qp_delta, and per piece its
+ * TotalCoeff, TrailingOnes and the bits after coeff_token (bit offset into
+ * the frame's RBSP region, length).  A partitioned MB (part 1 16x8, 2 8x16,
+ * 3 P_8x8 / P_8x8ref0 with sub_mb_type i in bits 2i..2i+1 of sub) also
+ * carries the motion of each 4x4 block (raster; mv packed x | y << 16); ref
+ * / mx / my are then block 0's.  An intra MB (intra 1 I_4x4, 2 I_16x16, 3
+ * I_PCM) keeps its mb_type, its prediction syntax's bits (poff, plen; I_PCM:
+ * poff = its samples), I_4x4's cbp codeNum.  nbsame: bit 0 / 1 the left /
+ * top MB is in the rect and the same slice.  332 bytes. */
 typedef struct {
     int16_t ref;
     uint8_t cbp;
     int8_t qpd;
     int32_t mx, my;
-    uint8_t skip, part, sub, pad;
+    uint8_t skip, part, sub, intra;
     uint8_t tc[SPLICE_PIECES], t1[SPLICE_PIECES];
     uint16_t blen[SPLICE_PIECES];
     uint32_t boff[SPLICE_PIECES];
     int8_t bref[16];
     uint32_t bmv[16];
-    uint32_t res_off, res_len;      /* the external residual's bits (0: not parsed / none) */
+    uint32_t res_off, res_len;      /* the residual after mb_qp_delta (0: none / not parsed) */
+    uint32_t poff;
+    uint16_t plen;
+    uint8_t mbt, cbp_code;
+    uint8_t nbsame, hasqpd, pad[2];
 } SpliceMbRec;
 
 /* 0, or -1 when the launch failed */
-int splice_launch_parse(hipStream_t hs, int n, const int32_t *list, SpliceFrame *spf,
-                        const DevStream *st, int ld_fr, uint32_t *rbsp, SpliceMbRec *rec);
+/* k_splice_units -> k_splice_parse -> k_splice_fix over the n listed
+ * frames; ymax = the most unit slots of a frame */
+int splice_launch_parse(hipStream_t hs, int n, int ymax, const int32_t *list, SpliceFrame *spf,
+                        SpliceUnit *units, const DevStream *st, int ld_fr, uint32_t *rbsp,
+                        SpliceMbRec *rec);
 int splice_launch_stage(hipStream_t hs, int nframes, int S, DevStream *st, const NalDesc *nal,
                         int ld_nal, const PlanPending *pend, DynFrame *dfr, int ld_fr,
                         const HintFrame *hf, const ScrollHintRect *pool, SpliceFrame *spf,

@@ -32,6 +32,8 @@
 
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "dyn_device.h"
 #include "hint_device.h"
 #include "splice_engine.h"
@@ -461,31 +463,27 @@ __device__ __attribute__((always_inline)) inline bool wrd_piece(SRd &r, const La
 }
 
 /* nC of piece pi from the TotalCoeffs of this MB (lanes' cur), the MB to the
- * left and the MB above (-1: unavailable at the picture edge) */
+ * left and the MB above (aA / aB: available -- inside the picture and the
+ * slice) */
 __device__ __attribute__((always_inline)) inline int nc_at(int pi, uint32_t cur, uint32_t left,
-                                                           uint32_t top, int x, int y)
+                                                           uint32_t top, bool aA, bool aB)
 {
     int nA, nB;
     if (pi < 16) {
         const int bx = pi & 3, by = pi >> 2;
         nA = bx ? (int)__builtin_amdgcn_readlane(cur, pi - 1)
-                : (x ? (int)__builtin_amdgcn_readlane(left, pi + 3) : -1);
+                : (aA ? (int)__builtin_amdgcn_readlane(left, pi + 3) : -1);
         nB = by ? (int)__builtin_amdgcn_readlane(cur, pi - 4)
-                : (y ? (int)__builtin_amdgcn_readlane(top, pi + 12) : -1);
+                : (aB ? (int)__builtin_amdgcn_readlane(top, pi + 12) : -1);
     } else {
         const int k = (pi - 18) & 3, bx = k & 1, by = k >> 1;
         nA = bx ? (int)__builtin_amdgcn_readlane(cur, pi - 1)
-                : (x ? (int)__builtin_amdgcn_readlane(left, pi + 1) : -1);
+                : (aA ? (int)__builtin_amdgcn_readlane(left, pi + 1) : -1);
         nB = by ? (int)__builtin_amdgcn_readlane(cur, pi - 2)
-                : (y ? (int)__builtin_amdgcn_readlane(top, pi + 2) : -1);
+                : (aB ? (int)__builtin_amdgcn_readlane(top, pi + 2) : -1);
     }
     return nc2(nA, nB);
 }
-
-/* wave-uniform (ref, mv) */
-struct UMv {
-    int ref, mx, my;
-};
 
 /* the pieces whose TotalCoeff an MB below reads (luma 12..15, chroma AC
  * 20, 21, 24, 25) -> slot 0..7; -1 for the others */
@@ -494,20 +492,97 @@ __device__ inline int tc_slot(int j)
     return j >= 12 && j < 16 ? j - 12 : ((j == 20 || j == 21) ? j - 16 : ((j == 24 || j == 25) ? j - 18 : -1));
 }
 
-/* 6.7 KB: 16 parse workgroups fit a CU, so every slice of a 4,096-slice
- * launch is resident at once */
+/* coded_block_pattern of an Intra_4x4 MB by codeNum (Table 9-4, ChromaArrayType 1) */
+__constant__ uint8_t CBP_INTRA[48] = {47, 31, 15, 0,  23, 27, 29, 30, 7,  11, 13, 14, 39, 43, 45, 46,
+                                      16, 3,  5,  10, 12, 19, 21, 26, 28, 35, 37, 42, 44, 1,  2,  4,
+                                      8,  17, 18, 20, 24, 6,  9,  22, 25, 32, 33, 34, 36, 40, 38, 41};
+
+/* 7 KB: 16 parse workgroups fit a CU */
 struct ParseLds {
     uint32_t rmv[PARSE_MAXW][4];         /* bottom 4x4 blocks of the MBs above (row y-1 ahead  */
     int8_t rrf[PARSE_MAXW][4];           /* of x, row y behind it): mv, ref                     */
     uint8_t tcrow[PARSE_MAXW][8];        /* their bottom pieces' TotalCoeffs (tc_slot)          */
+    int8_t imrow[PARSE_MAXW][4];         /* their bottom Intra4x4PredModes (-1: not I_4x4)      */
     uint32_t cmv[16], lmv[4];            /* this MB's blocks as they decode; the left MB's right */
     int8_t crf[16], lrf[4];              /* column                                               */
+    int8_t iml[4];                       /* the left MB's right-column Intra4x4PredModes         */
     uint32_t ulmv;                       /* block (3, 3) of the MB above-left (kept here, not in */
     int32_t ulrf;                        /* scalar registers: the parse is short of them)        */
 };
 
+/* k_splice_units: the NAL units of each listed frame's buffer -- Annex-B
+ * units (00 00 01 / 00 00 00 01 start codes), or the whole buffer as one NAL
+ * when it starts with none; trailing zero bytes of a unit belong to no unit
+ * (7.4.1.2).  One workgroup per frame; the start codes are found 1,024
+ * positions per pass and numbered in order by a workgroup scan. */
+__global__ __launch_bounds__(DT) void k_splice_units(int n, const int32_t *__restrict__ list,
+                                                     SpliceFrame *__restrict__ spf,
+                                                     SpliceUnit *__restrict__ units)
+{
+    __shared__ uint32_t ws[NW];
+    const int i = blockIdx.x, t = threadIdx.x;
+    if (i >= n) return;
+    SpliceFrame *F = spf + list[i];
+    const uint8_t *p = F->nal;
+    const uint32_t len = F->nal_len;
+    const int w = F->w, h = F->h;
+    const uint32_t cap = splice_unit_cap(w * h);
+    SpliceUnit *U = units + F->unit_first;
+    const bool sc = len >= 3 && !p[0] && !p[1] && (p[2] == 1 || (len >= 4 && !p[2] && p[3] == 1));
+    if (!sc) {
+        if (t == 0) {
+            U[0].b = 0;
+            U[0].e = len;
+            F->nunits = 1;
+        }
+        return;
+    }
+    uint32_t k = 0;                                   /* units so far (uniform) */
+    for (uint32_t c0 = 0; c0 + 3 <= len; c0 += 4 * DT) {
+        uint32_t hit = 0, cnt = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint32_t pos = c0 + 4u * (uint32_t)t + (uint32_t)q;
+            if (pos + 3 <= len && !p[pos] && !p[pos + 1] && p[pos + 2] == 1) {
+                hit |= 1u << q;
+                cnt++;
+            }
+        }
+        uint32_t ex, tot;
+        block_excl_sum(cnt, ws, ex, tot);
+        for (int q = 0; q < 4; ++q)
+            if (hit & (1u << q)) {
+                const uint32_t pos = c0 + 4u * (uint32_t)t + (uint32_t)q, u = k + ex++;
+                if (u < cap) U[u].b = pos + 3u;
+                if (u >= 1 && u - 1 < cap) U[u - 1].e = pos;
+            }
+        k += tot;
+    }
+    if (t == 0 && k >= 1 && k - 1 < cap) U[k - 1].e = len;
+    __threadfence_block();
+    __syncthreads();
+    for (uint32_t u = (uint32_t)t; u < min(k, cap); u += DT) {
+        const uint32_t b = U[u].b;
+        uint32_t e = U[u].e;
+        while (e > b && !p[e - 1]) --e;
+        U[u].e = e;
+    }
+    if (t == 0) F->nunits = (int32_t)k;
+}
+
+/* k_splice_parse: one wave parses one slice (NAL unit; a frame's units are
+ * dealt over the grid's y waves).  The slice is a sequential bit string, so
+ * the parse itself is wave-uniform (scalar values, no divergence): the bit
+ * window is 64 RBSP words held one per lane (readlane at the uniform bit
+ * position), every VLC is matched by all lanes at once, lane j keeps piece
+ * j's record fields, and the neighbour context (motion of the two rows above,
+ * TotalCoeffs and Intra4x4PredModes of the row above) sits in LDS.  A
+ * neighbour MB is available when it is inside the picture and not before the
+ * slice's first MB (6.4.x); the slice's first_mb_in_slice, MB count and QP
+ * ends go to its unit for k_splice_fix. */
 __global__ __launch_bounds__(64) void k_splice_parse(int n, const int32_t *__restrict__ list,
                                                      SpliceFrame *__restrict__ spf,
+                                                     SpliceUnit *__restrict__ units,
                                                      const DevStream *__restrict__ st, int ld_fr,
                                                      uint32_t *__restrict__ rbsp,
                                                      SpliceMbRec *__restrict__ recs)
@@ -517,33 +592,41 @@ __global__ __launch_bounds__(64) void k_splice_parse(int n, const int32_t *__res
     if (i >= n) return;
     const int idx = list[i];
     SpliceFrame *F = spf + idx;
+    const int W = F->w, H = F->h, nmb = W * H;
+    const int nu = min(F->nunits, (int)splice_unit_cap(nmb));
+    if ((int)blockIdx.y >= nu) return;
     const DevStream S = st[idx / ld_fr];
+    const int mbw_c = S.w / 16, x0c = F->x0, y0c = F->y0;
+    SpliceMbRec *rec = recs + F->rec_first;
+    const LaneTabs T = lane_tabs();
+    for (int u = (int)blockIdx.y; u < nu; u += (int)gridDim.y) {
+    SpliceUnit *UN = units + F->unit_first + u;
     /* the NAL pointer is a generic one, so the compiler takes its bytes for
      * per-lane values: the header bytes go through readfirstlane, or every
      * branch on them -- and the whole bit reader after it -- turns divergent */
-    const uint8_t *p = F->nal;
-    uint32_t len = F->nal_len;
+    const uint32_t ub = U(UN->b);
+    const uint8_t *p = F->nal + ub;
+    const uint32_t len = U(UN->e) - ub;
     auto byte = [&](uint32_t k) { return (uint32_t)__builtin_amdgcn_readfirstlane(k < len ? p[k] : 0u); };
-    int status = SCROLL_SPLICE_ERR_NAL;
-    uint32_t sc = 0;
-    if (len >= 4 && !byte(0) && !byte(1) && !byte(2) && byte(3) == 1u) sc = 4;
-    else if (len >= 3 && !byte(0) && !byte(1) && byte(2) == 1u) sc = 3;
-    p += sc;
-    len -= sc;
-    SpliceMbRec *rec = recs + F->rec_first;
-    const int W = F->w, H = F->h, nmb = W * H;
+    int status = SCROLL_SPLICE_ERR_NAL, first = -1, m = 0;
+    int fq_mb = -1, fq_qp = 0, last_qp = 0;
     const uint32_t h0 = byte(0);
-    if (len < 2 || (h0 & 0x80) || (h0 & 31) != 1 || W > PARSE_MAXW) {
-        if (lane == 0) F->status = len >= 2 && W > PARSE_MAXW ? SCROLL_SPLICE_ERR_HEADER : status;
-        return;
-    }
+    SRd r;
+    uint32_t end = 0, base = 0;
+    if (len < 2 || (h0 & 0x80) || (h0 & 31) != 1) goto done;
+    status = SCROLL_SPLICE_ERR_HEADER;
+    if (W > PARSE_MAXW) goto done;
+    {
     const int ref_idc = (int)(h0 >> 5) & 3;
     /* emulation prevention bytes out (7.4.1): byte i of the payload goes
      * unless it is 03 after two zero bytes; 4 bytes per lane per pass, the
      * output index by a wave prefix count; bytes land MSB-first in words
-     * (byte k at byte address k ^ 3) */
-    uint32_t *o = rbsp + F->rbsp_word;
-    const uint32_t nwmax = (len + 3u) / 4u + 2u;   /* = the host's region (splice_upload) */
+     * (byte k at byte address k ^ 3) from word ceil(b / 4) of the frame's
+     * region on -- (len + 2) / 4 words, which never reach the next unit's */
+    const uint32_t w0 = (ub + 3u) >> 2;
+    base = 32u * w0;
+    uint32_t *o = rbsp + F->rbsp_word + w0;
+    const uint32_t nwmax = (len + 2u) / 4u;
     for (uint32_t k = (uint32_t)lane; k < nwmax; k += 64) o[k] = 0u;
     __syncthreads();
     uint8_t *ob = reinterpret_cast<uint8_t *>(o);
@@ -572,14 +655,23 @@ __global__ __launch_bounds__(64) void k_splice_parse(int n, const int32_t *__res
     }
     __syncthreads();
     nb = __builtin_amdgcn_readfirstlane(nb);
-    SRd r;
-    r.init(o, (nb + 3u) >> 2, 8u * nb);
-    const LaneTabs T = lane_tabs();
+    const uint32_t nw = (nb + 3u) >> 2;
+    /* rbsp_stop_one_bit: the last 1 bit (none: end 0, the parse fails) */
+    for (int c = (int)nw - 1; c >= 0; c -= 64) {
+        const int k = c - lane;
+        const uint32_t v = k >= 0 ? o[k] : 0u;
+        const uint64_t bl = __ballot(v != 0u);
+        if (bl) {
+            const int l = __builtin_ctzll(bl);
+            const uint32_t vv = U((uint32_t)__builtin_amdgcn_readlane(v, l));
+            end = 32u * (uint32_t)(c - l) + 31u - (uint32_t)__builtin_ctz(vv);
+            break;
+        }
+    }
+    r.init(o, nw, 8u * nb);
 
-    status = SCROLL_SPLICE_ERR_HEADER;
     int nrefs = 2;                         /* the composer's PPS (h264_writer.c:114) */
-    int qp = 0;
-    if (r.ue() != 0) goto done;                                    /* first_mb_in_slice */
+    first = (int)r.ue();                                           /* first_mb_in_slice */
     {
         const uint32_t stype = r.ue();
         if (stype != 0 && stype != 5) goto done;
@@ -617,46 +709,57 @@ __global__ __launch_bounds__(64) void k_splice_parse(int n, const int32_t *__res
             if (op == 4) r.ue();
         }
     }
-    qp = 26 + r.se();
+    int qp = 26 + r.se();
     if (qp < 0 || qp > 51) goto done;
     if (S.deblock && r.ue() != 1) goto done;
     status = SCROLL_SPLICE_ERR_SYNTAX;
-    if (r.bad || r.over()) goto done;
+    if (r.bad || r.over() || first < 0 || first >= nmb) goto done;   /* k_splice_fix: HEADER if out of order */
     {
-        int m = 0, qp_c = 26;
+        const int m0 = first;
+        m = m0;
+        int x = m0 % W, y = m0 / W;
+        int qp_c = 26;                     /* composed chain from 26 (k_splice_fix rebases the first) */
         const Mv none{-1, 0, 0};
         uint32_t tc_left = 0;              /* lane j: TotalCoeff of piece j, MB to the left */
+        bool aA = false, aB = false, aC = false, aD = false;
+        auto avail = [&]() {
+            aA = x > 0 && m - 1 >= m0;
+            aB = y > 0 && m - W >= m0;
+            aC = y > 0 && x + 1 < W && m - W + 1 >= m0;
+            aD = x > 0 && y > 0 && m - W - 1 >= m0;
+        };
         auto ul = [&]() { return unpk_mv(L.ulrf, L.ulmv); };     /* block (3, 3) of the MB above-left */
         /* whole-MB neighbours of MB (x, y): A = the left MB's block (3, 0),
          * B = the above MB's (0, 3), C = the above-right MB's (0, 3), else
          * D = the above-left MB's (3, 3) */
-        auto ctx = [&](int x, int y, Mv &A, Mv &B, Mv &C) {
-            A = x ? unpk_mv(L.lrf[0], L.lmv[0]) : none;
-            B = y ? unpk_mv(L.rrf[x][0], L.rmv[x][0]) : none;
-            C = y ? (x + 1 < W ? unpk_mv(L.rrf[x + 1][0], L.rmv[x + 1][0]) : (x ? ul() : none)) : none;
+        auto ctx = [&](Mv &A, Mv &B, Mv &C) {
+            A = aA ? unpk_mv(L.lrf[0], L.lmv[0]) : none;
+            B = aB ? unpk_mv(L.rrf[x][0], L.rmv[x][0]) : none;
+            C = aC ? unpk_mv(L.rrf[x + 1][0], L.rmv[x + 1][0]) : (aD ? ul() : none);
         };
         /* block (cx, cy) relative to MB (x, y) for a (sub-)partition (6.4.11.7):
          * inside the MB once decoded (done), right of it never */
-        auto nb = [&](int x, int y, int cx, int cy, uint32_t done) -> Mv {
+        auto nb = [&](int cx, int cy, uint32_t done) -> Mv {
             if (cy >= 0) {
                 if (cx >= 4) return none;
                 if (cx >= 0) {
                     const int q = 4 * cy + cx;
                     return (done >> q) & 1u ? unpk_mv(L.crf[q], L.cmv[q]) : none;
                 }
-                return x ? unpk_mv(L.lrf[cy], L.lmv[cy]) : none;
+                return aA ? unpk_mv(L.lrf[cy], L.lmv[cy]) : none;
             }
-            if (!y) return none;
-            if (cx < 0) return x ? ul() : none;
-            if (cx < 4) return unpk_mv(L.rrf[x][cx], L.rmv[x][cx]);
-            return x + 1 < W ? unpk_mv(L.rrf[x + 1][0], L.rmv[x + 1][0]) : none;
+            if (cx < 0) return aD ? ul() : none;
+            if (cx < 4) return aB ? unpk_mv(L.rrf[x][cx], L.rmv[x][cx]) : none;
+            return aC ? unpk_mv(L.rrf[x + 1][0], L.rmv[x + 1][0]) : none;
         };
         /* context for the MBs to come: the bottom row and right column of MB
-         * (x, y) -- from one motion, or from the decoded blocks */
-        auto finish = [&](int x, int y, bool parted, const Mv &me) {
+         * (x, y) -- from one motion, or from the decoded blocks -- and its
+         * Intra4x4PredModes (lane j: raster block j's; -1 not I_4x4) */
+        auto finish = [&](bool parted, const Mv &me, int imode) {
+            const int im3 = __shfl(imode, 4 * (lane & 3) + 3, 64), im12 = __shfl(imode, 12 + (lane & 3), 64);
             if (lane == 0) {                                  /* read before it is replaced */
                 L.ulmv = L.rmv[x][3];
-                L.ulrf = y ? L.rrf[x][3] : -1;
+                L.ulrf = L.rrf[x][3];
             }
             if (lane < 4) {
                 const uint32_t v = pk_mv(me.mx, me.my);
@@ -664,18 +767,28 @@ __global__ __launch_bounds__(64) void k_splice_parse(int n, const int32_t *__res
                 L.rrf[x][lane] = parted ? L.crf[12 + lane] : (int8_t)me.ref;
                 L.lmv[lane] = parted ? L.cmv[4 * lane + 3] : v;
                 L.lrf[lane] = parted ? L.crf[4 * lane + 3] : (int8_t)me.ref;
+                L.iml[lane] = (int8_t)im3;
+                L.imrow[x][lane] = (int8_t)im12;
+            }
+        };
+        auto next = [&]() {
+            ++m;
+            if (++x == W) {
+                x = 0;
+                ++y;
             }
         };
         const int ts = tc_slot(lane);
-        while (m < nmb) {
+        for (bool first_mb = true;; first_mb = false) {
+            if (r.pos() >= end && !first_mb) break;
             const uint32_t run = r.ue();
             if (r.bad || r.over() || run > (uint32_t)(nmb - m)) goto done;
-            for (uint32_t k = 0; k < run; ++k, ++m) {             /* P_Skip */
-                const int x = m % W, y = m / W;
+            for (uint32_t k = 0; k < run; ++k, next()) {          /* P_Skip */
+                avail();
                 Mv A, B, C;
-                ctx(x, y, A, B, C);
+                ctx(A, B, C);
                 int px, py;
-                pskip_mv(x, y, A, B, C, px, py);
+                pskip_mv(aA, aB, A, B, C, px, py);
                 SpliceMbRec *R = rec + m;
                 if (lane == 0) {
                     R->ref = 0;
@@ -685,6 +798,9 @@ __global__ __launch_bounds__(64) void k_splice_parse(int n, const int32_t *__res
                     R->my = py;
                     R->skip = 1;
                     R->part = 0;
+                    R->intra = 0;
+                    R->hasqpd = 0;
+                    R->nbsame = (uint8_t)((aA ? 1 : 0) | (aB ? 2 : 0));
                     R->res_len = 0;
                 }
                 if (lane < SPLICE_PIECES) {
@@ -695,148 +811,240 @@ __global__ __launch_bounds__(64) void k_splice_parse(int n, const int32_t *__res
                 }
                 if (ts >= 0) L.tcrow[x][ts] = 0;
                 tc_left = 0;
-                finish(x, y, false, Mv{0, px, py});
+                finish(false, Mv{0, px, py}, -1);
             }
-            if (m == nmb) break;
-            const int x = m % W, y = m / W;
-            const uint32_t mbt = r.ue();                               /* mb_type (Table 7-13) */
-            if (r.bad || r.over() || mbt > 4) {
-                status = r.bad || r.over() ? SCROLL_SPLICE_ERR_SYNTAX : SCROLL_SPLICE_ERR_MBTYPE;
-                goto done;
+            if (r.pos() >= end) {                 /* skipped MBs end the slice (a run of 0 cannot) */
+                if (run == 0) goto done;
+                break;
             }
-            Mv me{0, 0, 0};
-            const int part = mbt == 4 ? 3 : (int)mbt;
-            uint32_t sub = 0;
-            if (mbt == 0) {
-                int ref = 0;
-                if (nrefs == 2) ref = 1 - (int)r.u(1);
-                else if (nrefs > 2) ref = (int)r.ue();
-                const int dx = r.se(), dy = r.se();
-                Mv A, B, C;
-                ctx(x, y, A, B, C);
-                int px, py;
-                predict_spec(A, B, C, ref, px, py);
-                const long long mx = (long long)px + dx, my = (long long)py + dy;
-                if (ref >= nrefs || mx < -SPLICE_MAX_MV || mx > SPLICE_MAX_MV || my < -SPLICE_MAX_MV ||
-                    my > SPLICE_MAX_MV)
-                    goto done;
-                me = Mv{ref, (int)mx, (int)my};
-            } else {
-                /* sub_mb_pred / mb_pred (7.3.5.1-2): sub_mb_types, ref_idx per
-                 * mbPartIdx (P_8x8ref0: all 0), mvd per (sub-)partition */
-                if (part == 3)
-                    for (int i = 0; i < 4; ++i) {
-                        const uint32_t st = r.ue();
-                        if (st > 3u) goto done;
-                        sub |= st << (2 * i);
-                    }
-                const int nref = part == 3 ? 4 : 2;
-                uint32_t refw = 0;                                     /* ref of mbPartIdx i: byte i */
-                if (mbt != 4)
-                    for (int i = 0; i < nref; ++i) {
-                        int rf = 0;
-                        if (nrefs == 2) rf = 1 - (int)r.u(1);
-                        else if (nrefs > 2) rf = (int)r.ue();
-                        if (rf >= nrefs) goto done;
-                        refw |= (uint32_t)rf << (8 * i);
-                    }
-                uint32_t dn = 0;
-                bool ok = true;
-                for_parts(part, sub, [&](int bx, int by, int bw, int bh, int mp) {
-                    const int rf = (int)((refw >> (8 * mp)) & 255u);
-                    const int dx = r.se(), dy = r.se();
-                    int px, py;
-                    predict_part(part, mp, bx, by, bw, rf, [&](int cx, int cy) { return nb(x, y, cx, cy, dn); },
-                                 px, py);
-                    const long long mx = (long long)px + dx, my = (long long)py + dy;
-                    ok = ok && mx >= -SPLICE_MAX_MV && mx <= SPLICE_MAX_MV && my >= -SPLICE_MAX_MV &&
-                         my <= SPLICE_MAX_MV;
-                    const uint32_t pm = part_mask(bx, by, bw, bh);
-                    if (lane < 16 && ((pm >> lane) & 1u)) {
-                        L.cmv[lane] = pk_mv((int)mx, (int)my);
-                        L.crf[lane] = (int8_t)rf;
-                    }
-                    dn |= pm;
-                });
-                if (!ok || r.bad || r.over()) goto done;
-                me = unpk_mv(L.crf[0], L.cmv[0]);
-            }
-            /* the motion is final: record it and hand the context on now, so
-             * none of it stays live through the residual */
+            if (m == nmb) goto done;
+            avail();
+            const uint32_t mbt = r.ue();                               /* mb_type (Tables 7-13, 7-11) */
+            if (r.bad || r.over() || mbt > 30) goto done;
             SpliceMbRec *R = rec + m;
-            if (lane == 0) {
-                R->ref = (int16_t)me.ref;
-                R->mx = me.mx;
-                R->my = me.my;
-                R->skip = 0;
-                R->part = (uint8_t)part;
-                R->sub = (uint8_t)sub;
+            const uint8_t nbsame = (uint8_t)((aA ? 1 : 0) | (aB ? 2 : 0));
+            /* lane j (12..15, 20, 21, 24, 25): piece j of the MB above, where
+             * nc_at reads it */
+            const uint32_t tc_top = aB && ts >= 0 ? L.tcrow[x][ts] : 0u;
+            PieceOut po{0, 0, 0, 0};
+            int cbp = 0, hasqpd = 0, qpd = 0, intra = 0, cbp_code = 0;
+            uint32_t rs0 = 0, rsn = 0, poff = 0, plen = 0;
+            if (mbt >= 5) {
+                /* intra in a P slice (7.3.5.1): I_4x4, I_16x16, I_PCM */
+                const int it = (int)mbt - 5;
+                intra = it == 0 ? 1 : (it == 25 ? 3 : 2);
+                int imode = -1;                                        /* lane j: raster block j's mode */
+                if (intra == 3) {                                      /* I_PCM (7.3.5) */
+                    bool bad = false;
+                    if (r.pos() & 7u) bad = r.u(8 - (int)(r.pos() & 7u)) != 0u;   /* pcm_alignment_zero_bits */
+                    poff = r.pos();
+                    for (int k = 0; k < 96; ++k) r.skip(32);           /* 384 samples */
+                    if (bad || r.over()) goto done;
+                    po.tc = lane < SPLICE_PIECES ? 16u : 0u;           /* nC: 16 (9.2.1) */
+                } else {
+                    int m0d = -1, m3 = -1;                             /* modes of raster blocks 0, 3 */
+                    poff = r.pos();
+                    if (intra == 1) {
+                        /* Intra4x4PredMode per block (8.3.1.1), luma4x4BlkIdx order;
+                         * -2 unavailable, -1 not I_4x4 */
+                        for (int blk = 0; blk < 16; ++blk) {
+                            const int ri = blk_raster16(blk), bx = ri & 3, by = ri >> 2;
+                            const int mA = bx ? __builtin_amdgcn_readlane(imode, ri - 1) : (aA ? (int)L.iml[by] : -2);
+                            const int mB = by ? __builtin_amdgcn_readlane(imode, ri - 4)
+                                              : (aB ? (int)L.imrow[x][bx] : -2);
+                            const int pm = (mA == -2 || mB == -2) ? 2 : min(mA < 0 ? 2 : mA, mB < 0 ? 2 : mB);
+                            int md = pm;
+                            if (!r.u(1)) {
+                                const int rem = (int)r.u(3);
+                                md = rem < pm ? rem : rem + 1;
+                            }
+                            if (lane == ri) imode = md;
+                        }
+                        m0d = __builtin_amdgcn_readlane(imode, 0);
+                        m3 = __builtin_amdgcn_readlane(imode, 3);
+                    } else {
+                        m0d = (it - 1) & 3;
+                    }
+                    const uint32_t cm = r.ue();                        /* intra_chroma_pred_mode */
+                    plen = r.pos() - poff;
+                    if (r.bad || r.over() || cm > 3u) goto done;
+                    /* the neighbours its prediction reads have the same
+                     * availability in the external and the composed picture */
+                    bool na = cm == 0 || cm == 1 || cm == 3, nbb = cm == 0 || cm == 2 || cm == 3, nd = cm == 3,
+                         nc = false;
+                    if (intra == 1) {
+                        na = nbb = true;
+                        nd = nd || m0d == 4 || m0d == 5 || m0d == 6;
+                        nc = m3 == 3 || m3 == 7;
+                    } else {
+                        na = na || m0d != 0;
+                        nbb = nbb || m0d != 1;
+                        nd = nd || m0d == 3;
+                    }
+                    auto same = [&](int dx, int dy, bool ext) {
+                        const int X = x0c + x + dx, Y = y0c + y + dy;
+                        return ext == (X >= 0 && Y >= 0 && X < mbw_c);
+                    };
+                    if ((na && !same(-1, 0, aA)) || (nbb && !same(0, -1, aB)) || (nd && !same(-1, -1, aD)) ||
+                        (nc && !same(1, -1, aC))) {
+                        status = SCROLL_SPLICE_ERR_MBTYPE;
+                        goto done;
+                    }
+                    if (intra == 1) {
+                        const uint32_t code = r.ue();
+                        if (r.bad || r.over() || code > 47u) goto done;
+                        cbp_code = (int)code;
+                        cbp = CBP_INTRA[code];
+                    } else {
+                        cbp = ((it - 1) >= 12 ? 15 : 0) | (((it - 1) >> 2) % 3) << 4;
+                    }
+                    hasqpd = cbp || intra == 2;
+                }
+                if (lane == 0) {
+                    R->ref = SPLICE_REF_INTRA;
+                    R->mx = 0;
+                    R->my = 0;
+                    R->skip = 0;
+                    R->part = 0;
+                    R->sub = 0;
+                }
+                finish(false, Mv{SPLICE_REF_INTRA, 0, 0}, imode);
+            } else {
+                Mv me{0, 0, 0};
+                const int part = mbt == 4 ? 3 : (int)mbt;
+                uint32_t sub = 0;
+                if (mbt == 0) {
+                    int ref = 0;
+                    if (nrefs == 2) ref = 1 - (int)r.u(1);
+                    else if (nrefs > 2) ref = (int)r.ue();
+                    const int dx = r.se(), dy = r.se();
+                    Mv A, B, C;
+                    ctx(A, B, C);
+                    int px, py;
+                    predict_spec(A, B, C, ref, px, py);
+                    const long long mx = (long long)px + dx, my = (long long)py + dy;
+                    if (ref >= nrefs || mx < -SPLICE_MAX_MV || mx > SPLICE_MAX_MV || my < -SPLICE_MAX_MV ||
+                        my > SPLICE_MAX_MV)
+                        goto done;
+                    me = Mv{ref, (int)mx, (int)my};
+                } else {
+                    /* sub_mb_pred / mb_pred (7.3.5.1-2): sub_mb_types, ref_idx per
+                     * mbPartIdx (P_8x8ref0: all 0), mvd per (sub-)partition */
+                    if (part == 3)
+                        for (int k = 0; k < 4; ++k) {
+                            const uint32_t stp = r.ue();
+                            if (stp > 3u) goto done;
+                            sub |= stp << (2 * k);
+                        }
+                    const int nref = part == 3 ? 4 : 2;
+                    uint32_t refw = 0;                                 /* ref of mbPartIdx k: byte k */
+                    if (mbt != 4)
+                        for (int k = 0; k < nref; ++k) {
+                            int rf = 0;
+                            if (nrefs == 2) rf = 1 - (int)r.u(1);
+                            else if (nrefs > 2) rf = (int)r.ue();
+                            if (rf >= nrefs) goto done;
+                            refw |= (uint32_t)rf << (8 * k);
+                        }
+                    uint32_t dn = 0;
+                    bool ok = true;
+                    for_parts(part, sub, [&](int bx, int by, int bw, int bh, int mp) {
+                        const int rf = (int)((refw >> (8 * mp)) & 255u);
+                        const int dx = r.se(), dy = r.se();
+                        int px, py;
+                        predict_part(part, mp, bx, by, bw, rf, [&](int cx, int cy) { return nb(cx, cy, dn); },
+                                     px, py);
+                        const long long mx = (long long)px + dx, my = (long long)py + dy;
+                        ok = ok && mx >= -SPLICE_MAX_MV && mx <= SPLICE_MAX_MV && my >= -SPLICE_MAX_MV &&
+                             my <= SPLICE_MAX_MV;
+                        const uint32_t pm = part_mask(bx, by, bw, bh);
+                        if (lane < 16 && ((pm >> lane) & 1u)) {
+                            L.cmv[lane] = pk_mv((int)mx, (int)my);
+                            L.crf[lane] = (int8_t)rf;
+                        }
+                        dn |= pm;
+                    });
+                    if (!ok || r.bad || r.over()) goto done;
+                    me = unpk_mv(L.crf[0], L.cmv[0]);
+                }
+                /* the motion is final: record it and hand the context on now, so
+                 * none of it stays live through the residual */
+                if (lane == 0) {
+                    R->ref = (int16_t)me.ref;
+                    R->mx = me.mx;
+                    R->my = me.my;
+                    R->skip = 0;
+                    R->part = (uint8_t)part;
+                    R->sub = (uint8_t)sub;
+                }
+                if (part && lane < 16) {
+                    R->bref[lane] = L.crf[lane];
+                    R->bmv[lane] = L.cmv[lane];
+                }
+                finish(part != 0, me, -1);
+                const uint32_t code = r.ue();
+                cbp = code < 48u ? (int)__builtin_amdgcn_readlane(T.cbp, code) : -1;
+                if (r.bad || r.over() || cbp < 0) goto done;
+                hasqpd = cbp != 0;
             }
-            if (part && lane < 16) {
-                R->bref[lane] = L.crf[lane];
-                R->bmv[lane] = L.cmv[lane];
-            }
-            finish(x, y, part != 0, me);
-            const uint32_t code = r.ue();
-            const int cbp = code < 48u ? (int)__builtin_amdgcn_readlane(T.cbp, code) : -1;
-            if (r.bad || r.over() || cbp < 0) goto done;
-            int qpd = 0;
-            uint32_t rs0 = 0, rsn = 0;                         /* the residual's bits */
-            /* lane j: piece j of this MB */
-            uint32_t my_tc = 0, my_t1 = 0, my_off = 0, my_len = 0;
-            if (cbp) {
+            if (hasqpd) {
                 const int dq = r.se();
                 if (dq < -26 || dq > 25) goto done;
                 qp = (qp + dq + 52) % 52;
-                int d = qp - qp_c;                                 /* composed chain from 26 */
+                int d = qp - qp_c;
                 if (d < -26) d += 52;
                 if (d > 25) d -= 52;
                 qpd = d;
                 qp_c = qp;
-                /* lane j (12..15, 20, 21, 24, 25): piece j of the MB above, where
-                 * nc_at reads it */
-                const uint32_t tc_top = y && ts >= 0 ? L.tcrow[x][ts] : 0u;
-                PieceOut po{0, 0, 0, 0};
+                if (fq_mb < 0) {
+                    fq_mb = m;
+                    fq_qp = qp;
+                }
+                last_qp = qp;
                 rs0 = r.pos();
-                /* the pieces in syntax order (7.3.5.3): luma 4x4 blocks of the
-                 * coded 8x8s, chroma DC, chroma AC (unrolled: measured faster
-                 * than one loop over the pieces) */
+                /* the pieces in syntax order (7.3.5.3): (I_16x16 DC,) luma 4x4
+                 * blocks of the coded 8x8s, chroma DC, chroma AC */
+                const int lmax = intra == 2 ? 15 : 16;
+                if (intra == 2 && !wrd_piece(r, T, 26, nc_at(0, po.tc, tc_left, tc_top, aA, aB), 16, po)) goto done;
                 for (int blk = 0; blk < 16; ++blk) {
                     if (!(cbp & (1 << (blk >> 2)))) continue;
                     const int pi = blk_raster16(blk);
-                    if (!wrd_piece(r, T, pi, nc_at(pi, po.tc, tc_left, tc_top, x, y), 16, po)) goto done;
+                    if (!wrd_piece(r, T, pi, nc_at(pi, po.tc, tc_left, tc_top, aA, aB), lmax, po)) goto done;
                 }
                 if (cbp >> 4) {
                     if (!wrd_piece(r, T, 16, -1, 4, po) || !wrd_piece(r, T, 17, -1, 4, po)) goto done;
                     if ((cbp >> 4) == 2)
                         for (int pi = 18; pi < 26; ++pi)
-                            if (!wrd_piece(r, T, pi, nc_at(pi, po.tc, tc_left, tc_top, x, y), 15, po))
+                            if (!wrd_piece(r, T, pi, nc_at(pi, po.tc, tc_left, tc_top, aA, aB), 15, po))
                                 goto done;
                 }
-                my_tc = po.tc;
-                my_t1 = po.t1;
-                my_off = po.off;
-                my_len = po.len;
                 rsn = r.pos() - rs0;
             }
             if (lane == 0) {
                 R->cbp = (uint8_t)cbp;
                 R->qpd = (int8_t)qpd;
-                R->res_off = rs0;
+                R->hasqpd = (uint8_t)hasqpd;
+                R->intra = (uint8_t)intra;
+                R->mbt = (uint8_t)mbt;
+                R->cbp_code = (uint8_t)cbp_code;
+                R->poff = base + poff;
+                R->plen = (uint16_t)plen;
+                R->nbsame = nbsame;
+                R->res_off = base + rs0;
                 R->res_len = rsn;
             }
             if (lane < SPLICE_PIECES) {
-                R->tc[lane] = (uint8_t)my_tc;
-                R->t1[lane] = (uint8_t)my_t1;
-                R->blen[lane] = (uint16_t)my_len;
-                R->boff[lane] = my_off;
+                R->tc[lane] = (uint8_t)po.tc;
+                R->t1[lane] = (uint8_t)po.t1;
+                R->blen[lane] = (uint16_t)po.len;
+                R->boff[lane] = base + po.off;
             }
-            if (ts >= 0) L.tcrow[x][ts] = (uint8_t)my_tc;
-            tc_left = my_tc;
-            ++m;
+            if (ts >= 0) L.tcrow[x][ts] = (uint8_t)po.tc;
+            tc_left = po.tc;
+            next();
         }
         /* rbsp_slice_trailing_bits (+ zero bytes of a byte stream) */
-        if (r.u(1) != 1u) goto done;
+        if (r.pos() != end || r.u(1) != 1u) goto done;
         if (r.pos() & 7u) {
             const int k = 8 - (int)(r.pos() & 7u);
             if (r.u(k)) goto done;
@@ -845,8 +1053,67 @@ __global__ __launch_bounds__(64) void k_splice_parse(int n, const int32_t *__res
             if (r.u(8)) goto done;
         if (!r.bad && !r.over()) status = SCROLL_SPLICE_OK;
     }
+    }
 done:
-    if (lane == 0) F->status = status;
+    if (lane == 0) {
+        UN->first = first;
+        UN->nmb = m - (first < 0 ? 0 : first);
+        UN->status = status;
+        UN->fq_mb = fq_mb;
+        UN->fq_qp = fq_qp;
+        UN->last_qp = last_qp;
+    }
+    }
+}
+
+/* k_splice_fix: one wave per frame walks its units in order -- each must
+ * start at the MB after the previous one's last (else HEADER), the first
+ * failing unit's status is the frame's, together they cover the picture --
+ * and rebases the first mb_qp_delta of every slice on the QP chain of the
+ * slices before it (composed slice QP 26). */
+__global__ __launch_bounds__(64) void k_splice_fix(int n, const int32_t *__restrict__ list,
+                                                   SpliceFrame *__restrict__ spf,
+                                                   const SpliceUnit *__restrict__ units,
+                                                   SpliceMbRec *__restrict__ recs)
+{
+    const int i = blockIdx.x;
+    if (i >= n || threadIdx.x != 0) return;
+    SpliceFrame *F = spf + list[i];
+    const int nmb = F->w * F->h, nall = F->nunits;
+    const int nu = min(nall, (int)splice_unit_cap(nmb));
+    const SpliceUnit *UN = units + F->unit_first;
+    SpliceMbRec *rec = recs + F->rec_first;
+    int status = SCROLL_SPLICE_OK;
+    if (nall > SPLICE_MAXU || nall < 1) {
+        status = SCROLL_SPLICE_ERR_NAL;
+    } else {
+        int expect = 0, qp_c = 26;
+        for (int u = 0; u < nu; ++u) {
+            const SpliceUnit un = UN[u];
+            if (un.status == SCROLL_SPLICE_ERR_NAL) {
+                status = un.status;
+                break;
+            }
+            if (un.first != expect) {
+                status = SCROLL_SPLICE_ERR_HEADER;
+                break;
+            }
+            if (un.status != SCROLL_SPLICE_OK) {
+                status = un.status;
+                break;
+            }
+            if (un.fq_mb >= 0) {
+                int d = un.fq_qp - qp_c;
+                if (d < -26) d += 52;
+                if (d > 25) d -= 52;
+                rec[un.fq_mb].qpd = (int8_t)d;
+                qp_c = un.last_qp;
+            }
+            expect += un.nmb;
+        }
+        if (status == SCROLL_SPLICE_OK && (nall > nu || expect != nmb)) status = SCROLL_SPLICE_ERR_SYNTAX;
+    }
+    F->status = status;
 }
 
 /* ------------------------------------------------------------------------ */
@@ -859,6 +1126,8 @@ struct SpliceLds {
     int32_t wo[8], wl[8], wv[8];
     uint32_t wsum[NW];
     int32_t wmax[NW];
+    uint64_t pcm_mask[NW];                  /* I_PCM MBs of the window (alignment) */
+    uint8_t pcm_key[DT];
     uint32_t ep_n;
     int32_t bad;
 };
@@ -894,19 +1163,33 @@ __device__ inline void put_rbsp(SK &sk, const uint32_t *rb, uint32_t q0, uint32_
     }
 }
 
-/* bits of one spliced MB after its head: cbp, mb_qp_delta, pieces.  An MB
- * whose left and top neighbours are spliced too (verbatim) sees the nC of
- * its external picture in every block: its residual is the external one
- * bit for bit and goes over as one run (parsed records only: res_len) */
+/* bits of one spliced MB after its head (inter: after the motion; intra:
+ * after mb_type): an intra MB's prediction syntax (I_4x4: + its cbp codeNum)
+ * or I_PCM's alignment (pad zero bits) and samples; an inter MB's cbp; then
+ * mb_qp_delta and the pieces (I_16x16: its DC first).  An MB whose left and
+ * top neighbours are spliced from the same slice (nbsame 3) sees the nC of
+ * its external picture in every block: its residual is the external one bit
+ * for bit and goes over as one run (parsed records only: res_len) */
 template <class SK>
 __device__ inline void splice_tail(SK &sk, const SpliceMbRec &mb, const uint8_t *L, const uint8_t *T,
-                                   const uint32_t *rb, bool verbatim)
+                                   const uint32_t *rb, uint32_t pad)
 {
     const int cbp = mb.cbp;
-    put_ue(sk, SPT.cbp_code[cbp]);
-    if (!cbp) return;
+    if (mb.intra == 3) {
+        sk.put(0u, (int)pad);                                  /* pcm_alignment_zero_bits */
+        put_rbsp(sk, rb, mb.poff, 384u * 8u);
+        return;
+    }
+    if (mb.intra) {
+        put_rbsp(sk, rb, mb.poff, mb.plen);
+        if (mb.intra == 1) put_ue(sk, mb.cbp_code);
+        if (!mb.hasqpd) return;
+    } else {
+        put_ue(sk, SPT.cbp_code[cbp]);
+        if (!cbp) return;
+    }
     put_se(sk, mb.qpd);
-    if (verbatim && mb.res_len) {
+    if ((mb.nbsame & 3) == 3 && mb.res_len) {
         put_rbsp(sk, rb, mb.res_off, mb.res_len);
         return;
     }
@@ -917,6 +1200,7 @@ __device__ inline void splice_tail(SK &sk, const SpliceMbRec &mb, const uint8_t 
         sk.put(v, len);
         put_rbsp(sk, rb, mb.boff[i], mb.blen[i]);
     };
+    if (mb.intra == 2) piece(26, piece_nc(0, mb.tc, L, T));
     for (int blk = 0; blk < 16; ++blk)
         if (cbp & (1 << (blk >> 2))) {
             const int i = blk_raster16(blk);
@@ -1044,7 +1328,7 @@ __global__ __launch_bounds__(DT) void k_splice_stage(DevStream *__restrict__ st,
                         const int wk = rf - 2;
                         return rf == 0 || rf == 1 || (wk >= 0 && wk < c.nwp && L.wv[wk]);
                     };
-                    my_ref_bad |= !valid(mb.ref);
+                    my_ref_bad |= !mb.intra && !valid(mb.ref);
                     if (parted)
                         for (int q = 1; q < 16; ++q) my_ref_bad |= !valid(mb.bref[q]);
                 } else {
@@ -1074,7 +1358,7 @@ __global__ __launch_bounds__(DT) void k_splice_stage(DevStream *__restrict__ st,
                                     : (x + 1 < mbw ? blk(m - mbw + 1, 0, 3) : (x > 0 ? blk(m - mbw - 1, 3, 3) : none));
                 if (spec) {
                     int sx, sy;
-                    pskip_mv(x, y, A, B, C, sx, sy);
+                    pskip_mv(x > 0, y > 0, A, B, C, sx, sy);
                     coded = !pskip ||
                             !(me.ref == 0 && me.mx == sx && me.my == sy && (k < 0 || rec[k].cbp == 0));
                     predict_spec(A, B, C, me.ref, px, py);
@@ -1106,8 +1390,15 @@ __global__ __launch_bounds__(DT) void k_splice_stage(DevStream *__restrict__ st,
                 if (cx < 4) return blk(m - mbw, cx, 3);
                 return x + 1 < mbw ? blk(m - mbw + 1, 0, 3) : none;
             };
+            const bool intra = k >= 0 && rec[k].intra;
+            uint32_t pcm_pad = 0;
             auto code_mb = [&](auto &sk) {
                 put_ue(sk, (uint32_t)(m - max(excl, last) - 1));  /* mb_skip_run */
+                if (intra) {
+                    put_ue(sk, rec[k].mbt);                        /* verbatim, like its prediction syntax */
+                    splice_tail(sk, rec[k], Lt, Tt, rb, pcm_pad);
+                    return;
+                }
                 if (parted) {
                     const SpliceMbRec &mb = rec[k];
                     const int part = mb.part;
@@ -1139,11 +1430,43 @@ __global__ __launch_bounds__(DT) void k_splice_stage(DevStream *__restrict__ st,
                     put_se(sk, me.mx - px);
                     put_se(sk, me.my - py);
                 }
-                if (k >= 0) splice_tail(sk, rec[k], Lt, Tt, rb, x > SF.x0 && y > SF.y0);
+                if (k >= 0) splice_tail(sk, rec[k], Lt, Tt, rb, 0u);
                 else sk.put(1, 1);                                 /* coded_block_pattern 0 */
             };
             CountSink cs{0};
             if (coded) code_mb(cs);
+            /* I_PCM: pcm_alignment_zero_bits for its composed position.  Sizes
+             * without them, scanned: the n-th I_PCM of the window starts its
+             * samples at key_n + (pads before it) mod 8 with key_n = its
+             * unpadded position mod 8, so pad_n = key_(n-1) - key_n mod 8
+             * (key_0 = 0) */
+            const bool pcm = coded && intra && rec[k].intra == 3;
+            if (__syncthreads_or(pcm)) {
+                uint32_t o0, t0;
+                block_excl_sum(cs.n, L.wsum, o0, t0);
+                CountSink hc{0};
+                put_ue(hc, (uint32_t)(m - max(excl, last) - 1));
+                put_ue(hc, 30u);
+                const int lane = t & 63, wv = t >> 6;
+                const uint64_t bl = __ballot(pcm);
+                if (lane == 0) L.pcm_mask[wv] = bl;
+                L.pcm_key[t] = (uint8_t)((pos + o0 + hc.n) & 7u);
+                __syncthreads();
+                if (pcm) {
+                    int prev = -1;
+                    const uint64_t below = bl & ((1ull << lane) - 1ull);
+                    if (below) {
+                        prev = 64 * wv + 63 - __builtin_clzll(below);
+                    } else {
+                        for (int w2 = wv - 1; w2 >= 0 && prev < 0; --w2)
+                            if (L.pcm_mask[w2]) prev = 64 * w2 + 63 - __builtin_clzll(L.pcm_mask[w2]);
+                    }
+                    const uint32_t kp = prev >= 0 ? L.pcm_key[prev] : 0u;
+                    pcm_pad = (kp - L.pcm_key[t]) & 7u;
+                    cs.n += pcm_pad;
+                }
+                __syncthreads();
+            }
             uint32_t off, T;
             block_excl_sum(cs.n, L.wsum, off, T);
             if (sweep == 1 && coded) {
@@ -1234,12 +1557,15 @@ __global__ __launch_bounds__(DT) void k_splice_stage(DevStream *__restrict__ st,
 
 }  // namespace
 
-int splice_launch_parse(hipStream_t hs, int n, const int32_t *list, SpliceFrame *spf,
-                        const DevStream *st, int ld_fr, uint32_t *rbsp, SpliceMbRec *rec)
+int splice_launch_parse(hipStream_t hs, int n, int ymax, const int32_t *list, SpliceFrame *spf,
+                        SpliceUnit *units, const DevStream *st, int ld_fr, uint32_t *rbsp,
+                        SpliceMbRec *rec)
 {
     if (n <= 0) return 0;
-    hipLaunchKernelGGL(k_splice_parse, dim3(n), dim3(64), 0, hs, n, list, spf, st, ld_fr, rbsp,
-                       rec);
+    hipLaunchKernelGGL(k_splice_units, dim3(n), dim3(DT), 0, hs, n, list, spf, units);
+    hipLaunchKernelGGL(k_splice_parse, dim3(n, (unsigned)std::max(1, std::min(ymax, 64))), dim3(64), 0, hs, n,
+                       list, spf, units, st, ld_fr, rbsp, rec);
+    hipLaunchKernelGGL(k_splice_fix, dim3(n), dim3(64), 0, hs, n, list, spf, units, rec);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -269,14 +269,21 @@ int scroll_batch_clear_hints(ScrollBatch *b);
  * predictor).
  * Bit-exact definition: oracle/splice_oracle.h.
  *
- * The external slice: one NAL (Annex-B start code optional), nal_unit_type
- * 1, CAVLC, first_mb_in_slice 0 and all w*h MBs, parsed with the composed
- * stream's SPS/PPS (log2_max_frame_num, POC type, 2 default references,
- * disable_deblocking_filter_idc 1 when the stream signals deblocking
- * control); no ref_pic_list_modification, or one that restates the composed
- * list (op k: long_term_pic_num k, as the composer's own slices write it);
- * MBs of any inter type (P_L0_16x16, P_L0_L0_16x8 / 8x16, P_8x8 with any
- * sub_mb_types, P_8x8ref0) or P_Skip -- no intra MBs;
+ * The external picture: one NAL (Annex-B start code optional), or several
+ * Annex-B NAL units -- its slices, in MB order, each starting at the MB after
+ * the previous one's last (first_mb_in_slice), together covering the w*h MBs
+ * (at most 1,024 slices; each is parsed by its own wave); nal_unit_type 1,
+ * CAVLC, parsed with the composed stream's SPS/PPS (log2_max_frame_num, POC
+ * type, 2 default references, disable_deblocking_filter_idc 1 when the
+ * stream signals deblocking control); no ref_pic_list_modification, or one
+ * that restates the composed list (op k: long_term_pic_num k, as the
+ * composer's own slices write it); MBs of any inter type (P_L0_16x16,
+ * P_L0_L0_16x8 / 8x16, P_8x8 with any sub_mb_types, P_8x8ref0), P_Skip, and
+ * the intra types of a P slice (I_4x4, I_16x16, I_PCM) where the neighbour
+ * MBs their sample prediction reads have the same availability in the
+ * external and the composed picture (so not on the rect's left / top edge
+ * unless that is the picture's, no above-right I_4x4 modes on its right
+ * edge; I_PCM anywhere; splice_oracle.h has the rule);
  * ref_idx 0 = A, 1 = B, 2 + i = waypoint i of the composed stream; motion
  * vectors are displacements in the composed picture, |mv| <= 16383 quarter
  * pels; CAVLC level_prefix <= 15 (Baseline / Main).
@@ -293,9 +300,10 @@ int scroll_batch_clear_hints(ScrollBatch *b);
  * external slice plus 16 bytes per picture MB) for every (stream, frame). */
 #define SCROLL_SPLICE_MAX_BYTES   ((uint64_t)1 << 29)   /* n < 512 MiB: 32-bit bit offsets */
 #define SCROLL_SPLICE_OK          0
-#define SCROLL_SPLICE_ERR_NAL     1   /* not a coded slice of a non-IDR picture     */
+#define SCROLL_SPLICE_ERR_NAL     1   /* not a coded slice of a non-IDR picture, or
+                                       * more than 1,024 slices                      */
 #define SCROLL_SPLICE_ERR_HEADER  2   /* slice header outside the supported syntax  */
-#define SCROLL_SPLICE_ERR_MBTYPE  3   /* an intra MB (mb_type > 4 in the P slice)    */
+#define SCROLL_SPLICE_ERR_MBTYPE  3   /* an intra MB whose prediction would change   */
 #define SCROLL_SPLICE_ERR_SYNTAX  4   /* malformed, truncated or MB count mismatch   */
 #define SCROLL_SPLICE_ERR_REF     5   /* ref_idx not a valid reference of the frame  */
 int scroll_batch_set_splice(ScrollBatch *b, int s, int f, int x0, int y0, int w, int h,

@@ -551,7 +551,10 @@ int or_splice_parse(const or_cfg *c, const or_splice *sp, or_splice_mb *mbs, uin
                     *sp_at(&F, x, y, b & 3, b >> 2) = (or_mvi){px, py, 0, 1};
                 }
             }
-            if (r.p >= end) break;                                /* skipped MBs end the slice */
+            if (r.p >= end) {                                     /* skipped MBs end the slice; */
+                if (!run) err = OR_SPLICE_ERR_SYNTAX;             /* a run of 0 precedes an MB  */
+                break;
+            }
             if (m == nmb) {
                 err = OR_SPLICE_ERR_SYNTAX;
                 break;

@@ -185,7 +185,7 @@ def test_errors_fail_only_their_stream(gpu, oracle, scroll):
     c = _cfg(oracle, w, h)
     good = ext_slice(oracle, c, 4, 3, 1)
     cases = {
-        0: (scroll.SCROLL_SPLICE_ERR_MBTYPE, ext_slice(oracle, c, 4, 3, 1, bad_mb=5, bad_type=12)),
+        0: (scroll.SCROLL_SPLICE_ERR_MBTYPE, ext_slice(oracle, c, 4, 3, 1, bad_mb=0, bad_type=5)),
         1: (scroll.SCROLL_SPLICE_ERR_NAL, good[:4] + bytes([0x65]) + good[5:]),
         2: (scroll.SCROLL_SPLICE_ERR_SYNTAX, good[:len(good) // 2]),
         3: (scroll.SCROLL_SPLICE_ERR_REF, ext_slice(oracle, c, 4, 3, 2, nrefs=4, max_ref=3,
@@ -345,3 +345,94 @@ def plan_from(oracle, w, h, offsets, frames, compose_mode=0):
             o += bytes(buf[:k])
         outs.append(bytes(o))
     return frames, outs
+
+
+def test_intra_and_multislice_splices(gpu, oracle):
+    """external pictures with I_4x4 / I_16x16 / I_PCM MBs (samples all zero
+    in some: emulation prevention inside I_PCM), in one slice or a slice per
+    one / two / three MB rows, spliced in all three modes over waypoints:
+    k_splice_units finds the slices, one wave parses each, k_splice_fix
+    chains them; I_PCM realigned at its composed position"""
+    w, h = 640, 480
+    offs = synthetic_offsets(4, 12, h, first_stream=5)
+    offs[1] = np.arange(488, 500)
+    for seed, rows in ((41, 0), (42, 1), (43, 2), (44, 3)):
+        frames, want = plan(oracle, w, h, offs, seed, p_splice=0.9, p_hint=0.3, max_rect=(12, 9),
+                            ext_kw=dict(intra_pm=500, slice_rows=rows, pcm_zero=seed % 2,
+                                        part_pm=200, qp_jitter=5))
+        b, rc = gpu_streams(gpu, w, h, offs, frames)
+        assert rc == 0, gpu.last_error()
+        check_equal(b, want)
+        for (s, f), (_, _, sp) in frames.items():
+            assert b.splice_status(s, f) == 0
+        b.close()
+
+
+def test_pcm_only_and_intra_types(gpu, oracle):
+    """every coded MB intra of one type (I_PCM only: many alignments in one
+    staging window; I_4x4 only; I_16x16 only), 4K rects"""
+    w, h = 1920, 1088
+    offs = synthetic_offsets(3, 6, h, first_stream=1)
+    for types in (4, 1, 2):
+        frames, want = plan(oracle, w, h, offs, 50 + types, p_splice=1.0, p_hint=0.2, max_rect=(30, 20),
+                            ext_kw=dict(intra_pm=1000, intra_types=types, skip_pm=100,
+                                        slice_rows=types - 1))
+        b, rc = gpu_streams(gpu, w, h, offs, frames, arena=64 << 20)
+        assert rc == 0, gpu.last_error()
+        check_equal(b, want)
+        b.close()
+
+
+def test_intra_on_rect_edges(gpu, oracle, scroll):
+    """I_4x4 / I_16x16 on the rect's top / left edge: refused inside the
+    picture (SCROLL_SPLICE_ERR_MBTYPE, the stream fails alone), accepted with
+    the rect in the picture's corner; I_PCM anywhere"""
+    w, h = 256, 256
+    offs = synthetic_offsets(4, 4, h, first_stream=2)
+    c = _cfg(oracle, w, h)
+    frames = {}
+    for i, (mb, t) in enumerate(((0, 5), (1, 12), (4, 30), (0, 30))):
+        nal = ext_slice(oracle, c, 4, 3, 1, bad_mb=mb, bad_type=t)
+        frames[(i, 0)] = ([], SPEC, (0, 0, 4, 3, nal))                 # corner: accepted
+        frames[(i, 2)] = ([], SPEC, (2, 2, 4, 3, nal))
+    b, rc = gpu_streams(gpu, w, h, offs, frames)
+    assert rc == scroll.SCROLL_ERR_CONFIG
+    for i, (mb, t) in enumerate(((0, 5), (1, 12), (4, 30), (0, 30))):
+        want = 0 if t == 30 else scroll.SCROLL_SPLICE_ERR_MBTYPE
+        assert b.splice_status(i, 2) == want, (i, b.splice_status(i, 2))
+        if want == 0:
+            assert b.splice_status(i, 0) == 0
+    good = {k: v for k, v in frames.items() if k[0] >= 2}
+    _, want = plan_from(oracle, w, h, offs[2:], {(s - 2, f): v for (s, f), v in good.items()})
+    check_equal(b, [None, None] + want, streams=[2, 3])
+    b.close()
+
+
+def test_multislice_rules(gpu, oracle, scroll):
+    """slices out of order (HEADER), a row missing (SYNTAX), trailing zero
+    bytes after each slice (accepted), more than 1,024 slices (NAL)"""
+    import h264_pslice as P
+    w, h = 256, 256
+    offs = synthetic_offsets(5, 3, h, first_stream=6)
+    c = _cfg(oracle, w, h)
+    nal = ext_slice(oracle, c, 4, 4, 5, slice_rows=1, intra_pm=300)
+    units = P.nal_units(nal)
+    assert len(units) == 4
+    sc = b"\x00\x00\x00\x01"
+    cases = [
+        (scroll.SCROLL_SPLICE_ERR_SYNTAX, b"".join(sc + u for u in units[:3])),
+        (scroll.SCROLL_SPLICE_ERR_HEADER, b"".join(sc + u for u in (units[0], units[2], units[1], units[3]))),
+        (0, b"".join(sc + u + b"\x00\x00" for u in units)),
+        (scroll.SCROLL_SPLICE_ERR_NAL, b"".join(sc + units[0] for _ in range(1025))),
+        (0, nal),
+    ]
+    frames = {(s, 1): ([], SPEC, (2, 2, 4, 4, d)) for s, (_, d) in enumerate(cases)}
+    b, rc = gpu_streams(gpu, w, h, offs, frames)
+    assert rc == scroll.SCROLL_ERR_CONFIG
+    for s, (code, _) in enumerate(cases):
+        assert b.splice_status(s, 1) == code, (s, b.splice_status(s, 1))
+    ok = [s for s, (code, _) in enumerate(cases) if code == 0]
+    _, want = plan_from(oracle, w, h, offs[ok], {(i, f): frames[(s, f)] for i, s in enumerate(ok) for f in (1,)})
+    for i, s in enumerate(ok):
+        assert b.output(s) == want[i], s
+    b.close()

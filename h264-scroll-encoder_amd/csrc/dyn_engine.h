@@ -22,9 +22,14 @@ typedef struct {
     uint32_t *gbits;                /* per (frame, row group): its bit count */
     uint32_t *spill;                /* rs_spill_cap spill slots (rect rows over their slot) */
     uint32_t *ctr;                  /* per compose: [0] spill slots taken, [1] general records taken,
-                                     * [2 + k] the frame (s ld_fr + f) holding general record k */
+                                     * [2] NALs k_dyn_epfix left to k_dyn_epscan, [DYN_CTR_LIST + k]
+                                     * the frame (s ld_fr + f) holding general record k,
+                                     * [DYN_CTR_LIST + ctr_frames + q] the q-th NAL for k_dyn_epscan */
+    uint32_t ctr_frames;            /* frames the lists hold (S ld_fr) */
     uint32_t epoch;                 /* look-back epoch of the last compose (24 bits, never 0) */
 } DynScratch;
+#define DYN_CTR_SLOW 2               /* ctr[]: the k_dyn_epscan count           */
+#define DYN_CTR_LIST 4               /* ctr[]: the lists (the counters zeroed per compose: 4 words) */
 
 /* k_dyn_rows + k_dyn_code_general (records of the general-path NALs) +
  * k_dyn_row (every rect row: block coding + packing -> its row-stage bits) */

@@ -306,7 +306,7 @@ __global__ __launch_bounds__(256) void k_dyn_rows(const DevStream *__restrict__ 
             const uint32_t k = atomicAdd(&ctr[1], 1u);
             if (k < g.gen_cap) {
                 DF->rbsp_bytes = k;
-                ctr[2 + k] = (uint32_t)((size_t)s * ld_fr + f);     /* k_dyn_row<true>'s list */
+                ctr[DYN_CTR_LIST + k] = (uint32_t)((size_t)s * ld_fr + f);   /* k_dyn_row<true>'s list */
                 e = DF_GENERAL;
             } else {
                 e = DF_OVER;
@@ -1249,7 +1249,7 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
     if (GEN) {                          /* grid (h, record slots): the frames k_dyn_rows listed */
         const uint32_t j = blockIdx.y, n = min(__builtin_amdgcn_readfirstlane(ctr[1]), g.gen_cap);
         if (j >= n) return;
-        const uint32_t q = __builtin_amdgcn_readfirstlane(ctr[2 + j]);
+        const uint32_t q = __builtin_amdgcn_readfirstlane(ctr[DYN_CTR_LIST + j]);
         s = (int)(q / (uint32_t)ld_fr);
         f = (int)(q - (uint32_t)s * (uint32_t)ld_fr);
     }
@@ -1898,10 +1898,16 @@ __device__ inline void rs_load8(uint32_t P, int &gg, int ng, uint32_t T, const u
 #endif
 constexpr int EPS_Z = SCROLL_EPS_Z;
 
-/* grid (EPS_Z, frames, streams) */
+/* grid (EPS_Z, EPS_SLOTS): workgroup (z, j) takes the NALs j, j +
+ * EPS_SLOTS, ... of the list k_dyn_epfix filled (*slow_n of them, slow[q] =
+ * s ld_fr + f): an empty list costs EPS_Z EPS_SLOTS workgroups that read one
+ * word, not one per frame */
+constexpr int EPS_SLOTS = 64;
 __global__ __launch_bounds__(EPS_T) void k_dyn_epscan(DevStream *__restrict__ st, DynFrame *__restrict__ dfr,
                                                      int ld_fr, DynGeom g, const uint32_t *__restrict__ rowstage,
-                                                     const uint32_t *__restrict__ gbits, uint8_t *__restrict__ eps)
+                                                     const uint32_t *__restrict__ gbits, uint8_t *__restrict__ eps,
+                                                     const uint32_t *__restrict__ slow_n,
+                                                     const uint32_t *__restrict__ slow)
 {
     __shared__ uint32_t goff[65], gb[64], gw[64];
     __shared__ int32_t wmax[EPS_NW];
@@ -1909,10 +1915,13 @@ __global__ __launch_bounds__(EPS_T) void k_dyn_epscan(DevStream *__restrict__ st
     __shared__ uint4 cbuf4[EPS_CHUNK / 16];              /* the chunk's bytes */
     __shared__ uint32_t epl[EPLIST_MAX];                /* this workgroup's EP positions */
     uint32_t *cbuf = reinterpret_cast<uint32_t *>(cbuf4);
-    const int z = blockIdx.x, f = blockIdx.y, s = blockIdx.z, t = threadIdx.x;
-    const size_t nb = (size_t)s * ld_fr + f;
+    (void)st;
+    const int z = blockIdx.x, t = threadIdx.x;
+    const uint32_t nslow = __builtin_amdgcn_readfirstlane(*slow_n);
+    for (uint32_t q = blockIdx.y; q < nslow; q += EPS_SLOTS) {
+    const size_t nb = __builtin_amdgcn_readfirstlane(slow[q]);
     DynFrame *DF = dfr + nb;
-    if (DF->nal < 0 || !(DF->err & DF_EPSLOW)) return;  /* k_dyn_epfix settled it */
+    __syncthreads();                                    /* the previous NAL's LDS reads are done */
     const int ng = g.ngroups;
     const uint32_t *fr = rowstage + nb * g.rs_frame_words;
     rs_table(gbits, nb, g, fr, goff, gb, gw, nullptr, t);
@@ -2008,13 +2017,14 @@ __global__ __launch_bounds__(EPS_T) void k_dyn_epscan(DevStream *__restrict__ st
     }
     __syncthreads();
     const uint32_t n = ep_n;
-    if (n == 0) return;
+    if (n == 0) continue;
     if (t == 0) ep_base = atomicAdd(&DF->ep, n);
     __syncthreads();
     uint32_t *eplist = reinterpret_cast<uint32_t *>(eps + nb * DYN_OVF_BYTES);
     const uint32_t base = ep_base;
     for (uint32_t i = (uint32_t)t; i < n && i < (uint32_t)EPLIST_MAX; i += EPS_T)
         if (base + i < (uint32_t)EPLIST_MAX) eplist[base + i] = epl[i];
+    }
 }
 
 /* ---------------------------------------------------------------------- */
@@ -2033,7 +2043,13 @@ __global__ __launch_bounds__(EPS_T) void k_dyn_epscan(DevStream *__restrict__ st
  * bits.  A byte can be decided twice (a run's last byte at a seam): kept
  * once.  More candidates in a group than its record holds, or more than EPF_LIST
  * positions: DF_EPSLOW (k_dyn_epscan scans the NAL). */
-constexpr int EPF_T = 256;
+#ifndef SCROLL_EPF_T
+#define SCROLL_EPF_T 256
+#endif
+#ifndef SCROLL_EPF_LIST
+#define SCROLL_EPF_LIST 4096
+#endif
+constexpr int EPF_T = SCROLL_EPF_T;
 
 /* the RBSP bytes from byte B on, with the zero run before it: EP positions
  * -> lst (count nlst, capacity lcap) until the first non-zero byte at or
@@ -2080,7 +2096,7 @@ __device__ inline void ep_eval_bytes(uint32_t B, uint32_t Bend, uint32_t nin, in
 template <int NT>
 __device__ inline void ep_fix(DevStream *st, DynFrame *DF, size_t nb, int s, const DynGeom &g,
                               const uint32_t *rowstage, const uint32_t *gbits, uint8_t *eps, const EpfLds &E,
-                              int t)
+                              int t, uint32_t *slow_n, uint32_t *slow_list)
 {
     /* NT = 64: one wave per NAL (wave-level hand-offs), else the workgroup */
     auto sync = [] {
@@ -2192,6 +2208,7 @@ __device__ inline void ep_fix(DevStream *st, DynFrame *DF, size_t nb, int s, con
             DF->err = DF_EPSLOW | DF_FIXED;             /* k_dyn_epscan finds them */
             DF->rbsp_bytes = nin;
             DF->ep = 0;
+            slow_list[atomicAdd(slow_n, 1u)] = (uint32_t)nb;   /* at most once per frame */
         }
         return;
     }
@@ -2225,11 +2242,12 @@ __device__ inline void ep_fix(DevStream *st, DynFrame *DF, size_t nb, int s, con
 /* grid (frames, streams): one workgroup per NAL.  (Measured: one wave per
  * NAL, four NALs per workgroup, 0.138 against 0.086 ms -- each NAL's
  * candidate and seam loops then take several passes of 64 lanes.) */
-constexpr int EPF_LIST = 4096;
+constexpr int EPF_LIST = SCROLL_EPF_LIST;
 __global__ __launch_bounds__(EPF_T) void k_dyn_epfix(DevStream *__restrict__ st, DynFrame *__restrict__ dfr,
                                                      int ld_fr, int nframes, DynGeom g,
                                                      const uint32_t *__restrict__ rowstage,
-                                                     const uint32_t *__restrict__ gbits, uint8_t *__restrict__ eps)
+                                                     const uint32_t *__restrict__ gbits, uint8_t *__restrict__ eps,
+                                                     uint32_t *__restrict__ slow_n, uint32_t *__restrict__ slow)
 {
     __shared__ uint32_t goff[65], gb[64], gw[64], cw[64];
     __shared__ uint32_t cbase[65];                      /* runs before group g */
@@ -2241,7 +2259,7 @@ __global__ __launch_bounds__(EPF_T) void k_dyn_epfix(DevStream *__restrict__ st,
     DynFrame *DF = dfr + nb;
     if (DF->nal < 0) return;
     const EpfLds E{goff, gb, gw, cw, cbase, lst, cnt, (uint32_t)EPF_LIST};
-    ep_fix<EPF_T>(st, DF, nb, s, g, rowstage, gbits, eps, E, t);
+    ep_fix<EPF_T>(st, DF, nb, s, g, rowstage, gbits, eps, E, t, slow_n, slow);
 }
 
 /* ---------------------------------------------------------------------- */
@@ -2856,11 +2874,12 @@ int dyn_launch_pack(hipStream_t hs, int nframes, int S, DevStream *st, const Nal
     hipLaunchKernelGGL(k_dyn_static, dim3(g->ngroups - g->h, nframes, S), dim3(GW), 0, hs, st, nal, ld_nal,
                        pend, dfr, ld_fr, *g, x->rowstage, x->gbits);
     if (hipGetLastError() != hipSuccess) return -1;
+    uint32_t *slow_n = x->ctr + DYN_CTR_SLOW, *slow = x->ctr + DYN_CTR_LIST + x->ctr_frames;
     hipLaunchKernelGGL(k_dyn_epfix, dim3(nframes, S), dim3(EPF_T), 0, hs, st, dfr, ld_fr, nframes, *g,
-                       x->rowstage, x->gbits, eps);
+                       x->rowstage, x->gbits, eps, slow_n, slow);
     if (hipGetLastError() != hipSuccess) return -1;
-    hipLaunchKernelGGL(k_dyn_epscan, dim3(EPS_Z, nframes, S), dim3(EPS_T), 0, hs, st, dfr, ld_fr, *g,
-                       x->rowstage, x->gbits, eps);
+    hipLaunchKernelGGL(k_dyn_epscan, dim3(EPS_Z, EPS_SLOTS), dim3(EPS_T), 0, hs, st, dfr, ld_fr, *g,
+                       x->rowstage, x->gbits, eps, slow_n, slow);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

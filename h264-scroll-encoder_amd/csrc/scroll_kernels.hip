@@ -1354,7 +1354,7 @@ static int launch(ScrollBatch *b, int nframes, int plan_mode, int nal_max, hipSt
             }
             const DynGeom &G = b->geo;
             const size_t nalw = (size_t)G.w * G.h, ng = (size_t)G.ngroups;
-            HIPCHK(hipMemsetAsync(b->dx.ctr, 0, 2 * sizeof(uint32_t), hs));   /* spill / record slots */
+            HIPCHK(hipMemsetAsync(b->dx.ctr, 0, DYN_CTR_LIST * sizeof(uint32_t), hs));   /* spill / record slots, epscan list */
             for (int c = 0; c < nch; ++c) {
                 const int s0 = (int)((int64_t)S * c / nch), s1 = (int)((int64_t)S * (c + 1) / nch);
                 const size_t nb0 = (size_t)s0 * ld_fr;
@@ -1948,8 +1948,9 @@ int scroll_batch_set_dyn_rect(ScrollBatch *b, int x0, int y0, int w, int h, size
     const size_t rs_words = S * F * g.rs_frame_words + (size_t)g.rs_spill_cap * g.rs_spill_words;
     if (e == hipSuccess) e = hipMalloc(&b->dx.rowstage, rs_words * sizeof(uint32_t));
     if (e == hipSuccess) b->dx.spill = b->dx.rowstage + S * F * g.rs_frame_words;
-    /* [0], [1]: slots taken; [2 + k]: the frame (s ld_fr + f) of general record k */
-    if (e == hipSuccess) e = hipMalloc(&b->dx.ctr, (2 + S * F) * sizeof(uint32_t));
+    /* counters, the general-record list and the k_dyn_epscan list (dyn_engine.h) */
+    if (e == hipSuccess) e = hipMalloc(&b->dx.ctr, (DYN_CTR_LIST + 2 * S * F) * sizeof(uint32_t));
+    b->dx.ctr_frames = (uint32_t)(S * F);
     if (e == hipSuccess) e = hipMalloc(&b->dx.gbits, S * F * ng * sizeof(uint32_t));
     b->dx.epoch = 0;
     if (e == hipSuccess) e = hipMemset(b->d_src, 0, S * g.src_ld);

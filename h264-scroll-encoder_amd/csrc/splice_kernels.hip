@@ -129,7 +129,7 @@ __device__ __attribute__((always_inline)) inline void predict_part(int part, int
 {
     const Mv A = nb(bx - 1, by), B = nb(bx, by - 1);
     Mv C = nb(bx + bw, by - 1);
-    if (C.ref < 0) C = nb(bx - 1, by - 1);
+    if (C.ref == -1) C = nb(bx - 1, by - 1);            /* unavailable (an intra C is available) */
     const Mv d = part == 1 ? (mp ? A : B) : (mp ? C : A);
     if (part != 3 && d.ref == ref) {
         px = d.mx;

@@ -956,6 +956,8 @@ struct ScrollBatch {
     SpliceMbRec *d_sp_rec = nullptr;
     int32_t *d_sp_list = nullptr;
     SpliceUnit *d_sp_units = nullptr;  /* NAL unit slots (splice_unit_cap per frame) */
+    int32_t *d_sp_lanes = nullptr;     /* lane list: count (zero between parses), (list index, unit) pairs */
+    size_t sp_lanes_cap = 0, sp_nslots = 0;
     int sp_ymax = 1;                   /* most unit slots of a frame (parse grid y)  */
     size_t sp_nal_cap = 0, sp_rbsp_cap = 0, sp_rec_cap = 0, sp_list_cap = 0, sp_units_cap = 0;
     /* stream ingest: scratch, grown on demand */
@@ -1117,6 +1119,7 @@ void scroll_batch_destroy(ScrollBatch *b)
     (void)hipFree(b->d_sp_rec);
     (void)hipFree(b->d_sp_list);
     (void)hipFree(b->d_sp_units);
+    (void)hipFree(b->d_sp_lanes);
     (void)hipFree(b->d_ing_in);
     (void)hipFree(b->d_ipcm_cnt);
     (void)hipFree(b->d_ipcm_stg);
@@ -1312,7 +1315,7 @@ static int launch(ScrollBatch *b, int nframes, int plan_mode, int nal_max, hipSt
         if (hint) {
             if (b->sp_parse) {
                 if (splice_launch_parse(hs, b->sp_n, b->sp_ymax, b->d_sp_list, b->d_spf, b->d_sp_units,
-                                        b->d_st, ld_fr, b->d_sp_rbsp, b->d_sp_rec)) {
+                                        b->d_sp_lanes, b->sp_nslots, b->d_st, ld_fr, b->d_sp_rbsp, b->d_sp_rec)) {
                     set_err("k_splice_parse launch: %s", hipGetErrorString(hipGetLastError()));
                     return SCROLL_ERR_HIP;
                 }
@@ -2159,13 +2162,16 @@ static void hint_release(ScrollBatch *b)
     (void)hipFree(b->d_sp_rec);
     (void)hipFree(b->d_sp_list);
     (void)hipFree(b->d_sp_units);
+    (void)hipFree(b->d_sp_lanes);
     b->d_spf = nullptr;
     b->d_sp_nal = nullptr;
     b->d_sp_rbsp = nullptr;
     b->d_sp_rec = nullptr;
     b->d_sp_list = nullptr;
     b->d_sp_units = nullptr;
-    b->sp_nal_cap = b->sp_rbsp_cap = b->sp_rec_cap = b->sp_list_cap = b->sp_units_cap = 0;
+    b->d_sp_lanes = nullptr;
+    b->sp_nal_cap = b->sp_rbsp_cap = b->sp_rec_cap = b->sp_list_cap = b->sp_units_cap = b->sp_lanes_cap = 0;
+    b->sp_nslots = 0;
     b->h_sp.clear();
     b->sp_n = 0;
     b->sp_dirty = 0;
@@ -2434,6 +2440,11 @@ static int splice_upload(ScrollBatch *b)
         (rc = sp_grow((void **)&b->d_sp_list, &b->sp_list_cap, list.size(), sizeof(int32_t))) ||
         (rc = sp_grow((void **)&b->d_sp_units, &b->sp_units_cap, nunits, sizeof(SpliceUnit))))
         return rc;
+    if (1 + 2 * nunits > b->sp_lanes_cap) {
+        if ((rc = sp_grow((void **)&b->d_sp_lanes, &b->sp_lanes_cap, 1 + 2 * nunits, sizeof(int32_t)))) return rc;
+        HIPCHK(hipMemset(b->d_sp_lanes, 0, sizeof(int32_t)));     /* k_splice_fix keeps it zero after */
+    }
+    b->sp_nslots = nunits;
     if (slot > b->geo.slot_bytes) {
         /* the new slots first: on failure the old ones, the hints and the
          * splices stay as they were (sp_dirty stays set: the next compose

@@ -44,15 +44,24 @@ typedef struct {
 } SpliceFrame;
 
 /* one NAL unit (slice) of a spliced picture: its bytes [b, e) of the
- * frame's buffer (after the start code, trailing zero bytes trimmed), then
- * from its parse: first_mb_in_slice, its MB count, status, and for the QP
- * chain its first MB with mb_qp_delta (-1: none), that MB's QP and the QP of
- * its last MB with mb_qp_delta.  32 bytes. */
+ * frame's buffer (after the start code, trailing zero bytes trimmed); from
+ * k_splice_unesc its RBSP (words from w0 of the frame's region, nbytes
+ * bytes) and the bit of its rbsp_stop_one_bit (end; 0: none); from its
+ * parse: first_mb_in_slice, its MB count, status, and for the QP chain its
+ * first MB with mb_qp_delta (-1: none), that MB's QP and the QP of its last
+ * MB with mb_qp_delta.  48 bytes. */
 typedef struct {
     uint32_t b, e;
+    uint32_t w0, nbytes, end;
     int32_t first, nmb, status;
     int32_t fq_mb, fq_qp, last_qp;
+    int32_t pad;
 } SpliceUnit;
+
+/* frames of at least this many slices are parsed one slice per lane
+ * (k_splice_lanes); the others, and slices the lanes hand back, one slice
+ * per wave (k_splice_parse) */
+#define SPLICE_LANE_MIN 4
 
 /* one external MB after parsing: motion (quarter pels; intra: ref
  * SPLICE_REF_INTRA), cbp, the composed mb_qp_delta, and per piece its
@@ -83,11 +92,13 @@ typedef struct {
 } SpliceMbRec;
 
 /* 0, or -1 when the launch failed */
-/* k_splice_units -> k_splice_parse -> k_splice_fix over the n listed
- * frames; ymax = the most unit slots of a frame */
+/* k_splice_units -> k_splice_unesc -> k_splice_lanes -> k_splice_parse ->
+ * k_splice_fix over the n listed frames; ymax = the most unit slots of a
+ * frame; lanes = the lane list (count word, zero between parses, then (list
+ * index, unit) pairs; room for nslots) */
 int splice_launch_parse(hipStream_t hs, int n, int ymax, const int32_t *list, SpliceFrame *spf,
-                        SpliceUnit *units, const DevStream *st, int ld_fr, uint32_t *rbsp,
-                        SpliceMbRec *rec);
+                        SpliceUnit *units, int32_t *lanes, size_t nslots, const DevStream *st, int ld_fr,
+                        uint32_t *rbsp, SpliceMbRec *rec);
 int splice_launch_stage(hipStream_t hs, int nframes, int S, DevStream *st, const NalDesc *nal,
                         int ld_nal, const PlanPending *pend, DynFrame *dfr, int ld_fr,
                         const HintFrame *hf, const ScrollHintRect *pool, SpliceFrame *spf,

@@ -514,12 +514,15 @@ struct ParseLds {
  * units (00 00 01 / 00 00 00 01 start codes), or the whole buffer as one NAL
  * when it starts with none; trailing zero bytes of a unit belong to no unit
  * (7.4.1.2).  One workgroup per frame; the start codes are found 1,024
- * positions per pass and numbered in order by a workgroup scan. */
+ * positions per pass and numbered in order by a workgroup scan.  A frame of
+ * SPLICE_LANE_MIN slices or more puts its slices on the lane list. */
 __global__ __launch_bounds__(DT) void k_splice_units(int n, const int32_t *__restrict__ list,
                                                      SpliceFrame *__restrict__ spf,
-                                                     SpliceUnit *__restrict__ units)
+                                                     SpliceUnit *__restrict__ units,
+                                                     int32_t *__restrict__ lanes)
 {
     __shared__ uint32_t ws[NW];
+    __shared__ uint32_t lbase;
     const int i = blockIdx.x, t = threadIdx.x;
     if (i >= n) return;
     SpliceFrame *F = spf + list[i];
@@ -527,12 +530,12 @@ __global__ __launch_bounds__(DT) void k_splice_units(int n, const int32_t *__res
     const uint32_t len = F->nal_len;
     const int w = F->w, h = F->h;
     const uint32_t cap = splice_unit_cap(w * h);
-    SpliceUnit *U = units + F->unit_first;
+    SpliceUnit *UN = units + F->unit_first;
     const bool sc = len >= 3 && !p[0] && !p[1] && (p[2] == 1 || (len >= 4 && !p[2] && p[3] == 1));
     if (!sc) {
         if (t == 0) {
-            U[0].b = 0;
-            U[0].e = len;
+            UN[0].b = 0;
+            UN[0].e = len;
             F->nunits = 1;
         }
         return;
@@ -553,21 +556,802 @@ __global__ __launch_bounds__(DT) void k_splice_units(int n, const int32_t *__res
         for (int q = 0; q < 4; ++q)
             if (hit & (1u << q)) {
                 const uint32_t pos = c0 + 4u * (uint32_t)t + (uint32_t)q, u = k + ex++;
-                if (u < cap) U[u].b = pos + 3u;
-                if (u >= 1 && u - 1 < cap) U[u - 1].e = pos;
+                if (u < cap) UN[u].b = pos + 3u;
+                if (u >= 1 && u - 1 < cap) UN[u - 1].e = pos;
             }
         k += tot;
     }
-    if (t == 0 && k >= 1 && k - 1 < cap) U[k - 1].e = len;
+    if (t == 0 && k >= 1 && k - 1 < cap) UN[k - 1].e = len;
     __threadfence_block();
     __syncthreads();
-    for (uint32_t u = (uint32_t)t; u < min(k, cap); u += DT) {
-        const uint32_t b = U[u].b;
-        uint32_t e = U[u].e;
+    const uint32_t nu = min(k, cap);
+    for (uint32_t u = (uint32_t)t; u < nu; u += DT) {
+        const uint32_t b = UN[u].b;
+        uint32_t e = UN[u].e;
         while (e > b && !p[e - 1]) --e;
-        U[u].e = e;
+        UN[u].e = e;
     }
-    if (t == 0) F->nunits = (int32_t)k;
+    if (t == 0) {
+        F->nunits = (int32_t)k;
+        if (k >= SPLICE_LANE_MIN && k <= SPLICE_MAXU) lbase = (uint32_t)atomicAdd(&lanes[0], (int32_t)nu);
+    }
+    __syncthreads();
+    if (k >= SPLICE_LANE_MIN && k <= SPLICE_MAXU)
+        for (uint32_t u = (uint32_t)t; u < nu; u += DT) {
+            lanes[1 + 2 * (lbase + u)] = i;
+            lanes[2 + 2 * (lbase + u)] = (int32_t)u;
+        }
+}
+
+/* k_splice_unesc: one wave per slice (a frame's slices dealt over the grid's
+ * y waves): the NAL header checked, emulation prevention bytes out (7.4.1:
+ * byte i of the payload goes unless it is 03 after two zero bytes; 4 bytes
+ * per lane per pass, the output index by a wave prefix count; bytes land
+ * MSB-first in words -- byte k at byte address k ^ 3 -- from word ceil(b / 4)
+ * of the frame's region on: (len + 2) / 4 words, which never reach the next
+ * unit's), and its rbsp_stop_one_bit found by a ballot over the words from
+ * the end.  status: SCROLL_SPLICE_ERR_NAL (a bad header), else 0 until the
+ * parse. */
+__global__ __launch_bounds__(64) void k_splice_unesc(int n, const int32_t *__restrict__ list,
+                                                     const SpliceFrame *__restrict__ spf,
+                                                     SpliceUnit *__restrict__ units,
+                                                     uint32_t *__restrict__ rbsp)
+{
+    const int i = blockIdx.x, lane = threadIdx.x;
+    if (i >= n) return;
+    const SpliceFrame *F = spf + list[i];
+    const int nu = min(F->nunits, (int)splice_unit_cap(F->w * F->h));
+    for (int u = (int)blockIdx.y; u < nu; u += (int)gridDim.y) {
+        SpliceUnit *UN = units + F->unit_first + u;
+        const uint32_t ub = U(UN->b);
+        const uint8_t *p = F->nal + ub;
+        const uint32_t len = U(UN->e) - ub;
+        const uint32_t h0 = len ? U(p[0]) : 0u;
+        const uint32_t w0 = (ub + 3u) >> 2;
+        uint32_t nb = 0, end = 0;
+        const bool ok = len >= 2 && !(h0 & 0x80) && (h0 & 31) == 1;
+        if (ok) {
+            uint32_t *o = rbsp + F->rbsp_word + w0;
+            const uint32_t nwmax = (len + 2u) / 4u;
+            for (uint32_t k = (uint32_t)lane; k < nwmax; k += 64) o[k] = 0u;
+            __syncthreads();
+            uint8_t *ob = reinterpret_cast<uint8_t *>(o);
+            for (uint32_t c0 = 1; c0 < len; c0 += 256) {
+                uint32_t keep = 0, cnt = 0;
+                uint8_t by[4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const uint32_t k = c0 + 4u * (uint32_t)lane + (uint32_t)q;
+                    by[q] = k < len ? p[k] : 0;
+                    const bool ep = k < len && k >= 3 && by[q] == 3 && p[k - 1] == 0 && p[k - 2] == 0;
+                    const bool kp = k < len && !ep;
+                    keep |= kp ? 1u << q : 0u;
+                    cnt += kp ? 1u : 0u;
+                }
+                const uint32_t incl = wave_incl_sum(cnt, lane);
+                uint32_t at = nb + incl - cnt;
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    if (keep & (1u << q)) {
+                        ob[at ^ 3u] = by[q];
+                        at++;
+                    }
+                nb += __builtin_amdgcn_readlane(incl, 63);
+            }
+            __syncthreads();
+            nb = U(nb);
+            const uint32_t nw = (nb + 3u) >> 2;
+            for (int c = (int)nw - 1; c >= 0; c -= 64) {
+                const int k = c - lane;
+                const uint32_t v = k >= 0 ? o[k] : 0u;
+                const uint64_t bl = __ballot(v != 0u);
+                if (bl) {
+                    const int l = __builtin_ctzll(bl);
+                    const uint32_t vv = U((uint32_t)__builtin_amdgcn_readlane(v, l));
+                    end = 32u * (uint32_t)(c - l) + 31u - (uint32_t)__builtin_ctz(vv);
+                    break;
+                }
+            }
+        }
+        if (lane == 0) {
+            UN->w0 = w0;
+            UN->nbytes = nb;
+            UN->end = end;
+            UN->status = ok ? SCROLL_SPLICE_OK : SCROLL_SPLICE_ERR_NAL;
+            UN->first = -1;
+            UN->nmb = 0;
+        }
+    }
+}
+
+/* ------------------------------------------------------------------------ */
+/* k_splice_lanes: one slice per lane                                         */
+/* ------------------------------------------------------------------------ */
+/* Frames of many slices (one per MB row: the low-latency encoder mode) give
+ * enough slices to parse one per LANE, each lane its own bit reader, VLC
+ * lookups from LDS tables, its MB state in registers and lane-private LDS --
+ * the wave then decodes 64 slices with the instructions the wave-uniform
+ * parse spends on one.  A slice parsed here sees no MB above it in its own
+ * slice (slices of at most w MBs: one per row, or shorter); the above-right
+ * MB of its last MB can be its first MB, whose block (0, 3) it keeps.  A
+ * slice that goes on past that (its MB m with m - w >= first) is handed back
+ * (SPLICE_REDO) to the wave-uniform parse.  Bits and records: the same as
+ * k_splice_parse's. */
+constexpr int SPLICE_REDO = 99;
+constexpr int LANE_WAVES = 1;
+
+struct LaneLds {
+    uint16_t ct[4][128];                 /* coeff_token: lz 8 + 3 bits -> len << 8 | tc << 2 | t1 */
+    uint8_t tz[15 * 40];                 /* total_zeros: (tc - 1) 40 + min(lz, 9) 4 + 2 bits -> len << 4 | tz */
+    uint8_t tzd[3 * 16];                 /* chroma DC total_zeros */
+    uint8_t rb[7 * 48];                  /* run_before: (min(zl, 7) - 1) 48 + min(lz, 11) 4 + 2 bits */
+    uint8_t cbpi[48];                    /* inter codeNum -> coded_block_pattern */
+    uint8_t tcc[SPLICE_PIECES][64];      /* per lane: the current MB's TotalCoeffs */
+    uint32_t cmv[16][64];                /* per lane: the current MB's blocks as they decode */
+    int8_t crf[16][64];
+    int8_t im[16][64];                   /* per lane: the current MB's Intra4x4PredModes */
+};
+
+/* a lane's own bit reader: the next 33..64 bits in a 64-bit register, a
+ * word loaded per 32 bits consumed (the next one already in flight) */
+struct LRd {
+    const uint32_t *w;
+    uint32_t nw, nbits;
+    uint64_t buf;
+    uint32_t nv, p, wk, nxt;
+    bool bad;
+    __device__ inline uint32_t word(uint32_t k) const { return k < nw ? w[k] : 0u; }
+    __device__ inline void init(const uint32_t *words, uint32_t nwords, uint32_t bits)
+    {
+        w = words;
+        nw = nwords;
+        nbits = bits;
+        bad = false;
+        buf = (uint64_t)word(0) << 32 | word(1);
+        nxt = word(2);
+        nv = 64;
+        p = 0;
+        wk = 3;
+    }
+    __device__ inline uint32_t peek32() const { return (uint32_t)(buf >> 32); }
+    __device__ inline void skip(uint32_t n)            /* n <= 32 */
+    {
+        buf <<= n;
+        nv -= n;
+        p += n;
+        if (nv <= 32u) {
+            buf |= (uint64_t)nxt << (32u - nv);
+            nv += 32u;
+            nxt = word(wk++);
+        }
+    }
+    __device__ inline bool over() const { return p > nbits; }
+    __device__ inline uint32_t u(int n)                /* 1 <= n <= 32 */
+    {
+        const uint32_t v = (uint32_t)(buf >> (64 - n));
+        skip((uint32_t)n);
+        return v;
+    }
+    __device__ inline uint32_t ue()
+    {
+        const uint32_t x = peek32();
+        const int z = x ? __clz((int)x) : 32;
+        if (z >= 32) {
+            bad = true;
+            return 0;
+        }
+        if (z < 16) {
+            const uint32_t v = (x >> (31 - 2 * z)) - 1u;
+            skip((uint32_t)(2 * z + 1));
+            return v;
+        }
+        skip((uint32_t)z);
+        return u(z + 1) - 1u;
+    }
+    __device__ inline int32_t se()
+    {
+        const uint32_t k = ue();
+        return (k & 1u) ? (int32_t)((k + 1u) >> 1) : -(int32_t)(k >> 1);
+    }
+};
+
+__device__ inline void lane_tables(LaneLds &L, int t, int nt)
+{
+    for (int q = t; q < 4 * 128; q += nt) {
+        const int c = q >> 7, idx = q & 127, lz = idx >> 3;
+        uint16_t v = 0;
+        if (lz <= 15) {
+            const uint32_t x = vlc_pattern(lz, (uint32_t)(idx & 7), 3);
+            const int e = c < 3 ? vlc_find(x, SPT.ct_len[c], SPT.ct_bits[c], 68) : vlc_find(x, SPT.ctdc_len, SPT.ctdc_bits, 20);
+            if (e >= 0) {
+                const int l = c < 3 ? SPT.ct_len[c][e] : SPT.ctdc_len[e];
+                v = (uint16_t)(l << 8 | (e >> 2) << 2 | (e & 3));
+            }
+        }
+        L.ct[c][idx] = v;
+    }
+    for (int q = t; q < 15 * 40; q += nt) {
+        const int tc = q / 40 + 1, r = q % 40, lz = r >> 2;
+        const int e = vlc_find(vlc_pattern(lz, (uint32_t)(r & 3), 2), SPT.tz_len[tc - 1], SPT.tz_bits[tc - 1],
+                               17 - tc < 16 ? 17 - tc : 16);
+        L.tz[q] = e < 0 ? 0 : (uint8_t)(SPT.tz_len[tc - 1][e] << 4 | e);
+    }
+    for (int q = t; q < 3 * 16; q += nt) {
+        const int tc = q / 16 + 1, r = q % 16, lz = r >> 2;
+        const int e = vlc_find(vlc_pattern(lz, (uint32_t)(r & 3), 2), SPT.tzdc_len[tc - 1], SPT.tzdc_bits[tc - 1], 5 - tc);
+        L.tzd[q] = e < 0 ? 0 : (uint8_t)(SPT.tzdc_len[tc - 1][e] << 4 | e);
+    }
+    for (int q = t; q < 7 * 48; q += nt) {
+        const int zl = q / 48 + 1, r = q % 48, lz = r >> 2;
+        const int e = vlc_find(vlc_pattern(lz, (uint32_t)(r & 3), 2), SPT.rb_len[zl - 1], SPT.rb_bits[zl - 1],
+                               zl < 7 ? zl + 1 : 15);
+        L.rb[q] = e < 0 ? 0 : (uint8_t)(SPT.rb_len[zl - 1][e] << 4 | e);
+    }
+    for (int q = t; q < 48; q += nt) L.cbpi[SPT.cbp_code[q]] = (uint8_t)q;
+}
+
+/* one residual block of the lane's slice: coeff_token for nC, the body
+ * (9.2.2-9.2.4) consumed; -> false on a decode failure */
+__device__ inline bool lane_block(LRd &r, const LaneLds &L, int nC, int maxc, int &tc, int &t1, uint32_t &boff,
+                                  uint32_t &blen)
+{
+    if (nC >= 8) {
+        const uint32_t c = r.u(6);
+        if (c == 3u) {
+            tc = t1 = 0;
+        } else {
+            tc = (int)(c >> 2) + 1;
+            t1 = (int)(c & 3u);
+            if (t1 > tc) return false;
+        }
+    } else {
+        const uint32_t x = r.peek32();
+        const uint32_t lzv = x ? (uint32_t)__clz((int)x) : 32u;
+        uint32_t idx = min(lzv, 16u) << 3 | ((x << (min(lzv, 15u) + 1u)) >> 29);
+        if (idx >= 128u) {
+            if (nC != -1) return false;
+            idx = 120u;
+        }
+        const int c = nC == -1 ? 3 : (nC < 2 ? 0 : (nC < 4 ? 1 : 2));
+        const uint32_t e = L.ct[c][idx];
+        if (!e) return false;
+        r.skip(e >> 8);
+        tc = (int)((e >> 2) & 31u);
+        t1 = (int)(e & 3u);
+    }
+    if (tc > maxc) return false;
+    boff = r.p;
+    blen = 0;
+    if (tc == 0) return true;
+    r.skip((uint32_t)t1);
+    uint32_t sl = (tc > 10 && t1 < 3) ? 1u : 0u;
+    for (int k = t1; k < tc; ++k) {
+        const uint32_t x = r.peek32();
+        const uint32_t prefix = min(x ? (uint32_t)__clz((int)x) : 32u, 16u);
+        if (prefix > 15u) return false;
+        uint32_t ssize = sl;
+        ssize = prefix == 14u && sl == 0u ? 4u : ssize;
+        ssize = prefix >= 15u ? 12u : ssize;
+        const uint32_t suf = ssize ? (x << (prefix + 1u)) >> (32u - ssize) : 0u;
+        r.skip(prefix + 1u + ssize);
+        uint32_t code = (min(prefix, 15u) << sl) + suf;
+        code += prefix >= 15u && sl == 0u ? 15u : 0u;
+        code += k == t1 && t1 < 3 ? 2u : 0u;
+        const uint32_t a = (code + 2u) >> 1;
+        sl = sl == 0u ? 1u : sl;
+        sl += a > (3u << (sl - 1u)) && sl < 6u ? 1u : 0u;
+    }
+    uint32_t zl = 0;
+    if (tc < maxc) {
+        const uint32_t x = r.peek32();
+        const uint32_t e = maxc == 4 ? L.tzd[(tc - 1) * 16 + lz_index(x, 3, 2)] : L.tz[(tc - 1) * 40 + lz_index(x, 9, 2)];
+        if (!e) return false;
+        r.skip(e >> 4);
+        zl = e & 15u;
+    }
+    for (int k = 0; k < tc - 1 && zl > 0u; ++k) {
+        const uint32_t x = r.peek32();
+        const uint32_t e = L.rb[(min(zl, 7u) - 1u) * 48 + lz_index(x, 11, 2)];
+        if (!e || (e & 15u) > zl) return false;
+        r.skip(e >> 4);
+        zl -= e & 15u;
+    }
+    blen = r.p - boff;
+    return true;
+}
+
+__global__ __launch_bounds__(64 * LANE_WAVES) void k_splice_lanes(const int32_t *__restrict__ list,
+                                                                  const SpliceFrame *__restrict__ spf,
+                                                                  SpliceUnit *__restrict__ units,
+                                                                  const int32_t *__restrict__ lanes,
+                                                                  const DevStream *__restrict__ st, int ld_fr,
+                                                                  const uint32_t *__restrict__ rbsp,
+                                                                  SpliceMbRec *__restrict__ recs)
+{
+    __shared__ LaneLds L;
+    const int t = threadIdx.x, lane = t & 63;
+    const int nl = lanes[0];
+    const int stride = (int)gridDim.x * (int)blockDim.x;
+    if ((int)blockIdx.x * (int)blockDim.x >= nl) return;
+    lane_tables(L, t, (int)blockDim.x);
+    __syncthreads();
+    for (int q = (int)blockIdx.x * (int)blockDim.x + t; q < nl; q += stride) {
+        const int idx = list[lanes[1 + 2 * q]], u = lanes[2 + 2 * q];
+        const SpliceFrame *F = spf + idx;
+        SpliceUnit *UN = units + F->unit_first + u;
+        if (UN->status != SCROLL_SPLICE_OK) continue;            /* k_splice_unesc: not a slice NAL */
+        const DevStream &S = st[idx / ld_fr];
+        const int W = F->w, H = F->h, nmb = W * H;
+        const int mbw_c = S.w / 16, x0c = F->x0, y0c = F->y0;
+        SpliceMbRec *rec = recs + F->rec_first;
+        const uint32_t w0 = UN->w0, nbytes = UN->nbytes, end = UN->end, base = 32u * w0;
+        const int ref_idc = (int)(F->nal[UN->b] >> 5) & 3;
+        LRd r;
+        r.init(rbsp + F->rbsp_word + w0, (nbytes + 3u) >> 2, 8u * nbytes);
+        int status = SCROLL_SPLICE_ERR_HEADER, first = -1, m = 0;
+        int fq_mb = -1, fq_qp = 0, last_qp = 0;
+        int nrefs = 2;
+        int qp = 0;
+        bool go = true;
+        first = (int)r.ue();
+        {
+            const uint32_t stype = r.ue();
+            if (stype != 0 && stype != 5) go = false;
+        }
+        if (go && r.ue() != 0) go = false;
+        if (go) {
+            r.skip(S.log2_mfn);
+            if (S.poc_type == 0) r.skip(S.log2_poc);
+            if (r.u(1)) {
+                const uint32_t k = r.ue();
+                if (k > 31) go = false;
+                nrefs = (int)k + 1;
+            }
+        }
+        if (go && r.u(1)) {
+            for (int k = 0;; ++k) {
+                const uint32_t idc = r.ue();
+                if (r.bad || r.over() || k > 32) {
+                    status = SCROLL_SPLICE_ERR_SYNTAX;
+                    go = false;
+                    break;
+                }
+                if (idc == 3) break;
+                if (idc != 2 || r.ue() != (uint32_t)k) {
+                    go = false;
+                    break;
+                }
+            }
+        }
+        if (go && ref_idc && r.u(1)) {
+            for (int k = 0;; ++k) {
+                const uint32_t op = r.ue();
+                if (r.bad || r.over() || k > 64 || op > 6) {
+                    status = SCROLL_SPLICE_ERR_SYNTAX;
+                    go = false;
+                    break;
+                }
+                if (op == 0) break;
+                if (op == 1 || op == 3) r.ue();
+                if (op == 2) r.ue();
+                if (op == 3 || op == 6) r.ue();
+                if (op == 4) r.ue();
+            }
+        }
+        if (go) {
+            qp = 26 + r.se();
+            if (qp < 0 || qp > 51) go = false;
+        }
+        if (go && S.deblock && r.ue() != 1) go = false;
+        if (go) {
+            status = SCROLL_SPLICE_ERR_SYNTAX;
+            if (r.bad || r.over() || first < 0 || first >= nmb) go = false;
+        }
+        if (go) {
+            const int m0 = first;
+            m = m0;
+            int x = m0 % W, y = m0 / W;
+            int qp_c = 26;
+            /* the left MB (available when aA): its right-column blocks,
+             * right-column pieces' TotalCoeffs (3, 7, 11, 15, 19, 21, 23,
+             * 25) and Intra4x4PredModes; the slice's first MB's block (0, 3)
+             * (the above-right MB of an MB w - 1 later) */
+            uint32_t lmv0 = 0, lmv1 = 0, lmv2 = 0, lmv3 = 0;
+            int lrf0 = -1, lrf1 = -1, lrf2 = -1, lrf3 = -1;
+            uint32_t ltc = 0, ltc2 = 0;                         /* bytes: 3 7 11 15 | 19 21 23 25 */
+            uint32_t lim = 0xffffffffu;                         /* bytes: modes 3 7 11 15 (0xff: -1) */
+            uint32_t fmv = 0;
+            int frf = -1;
+            const Mv none{-1, 0, 0};
+            auto lmvq = [&](int q) { return q == 0 ? lmv0 : (q == 1 ? lmv1 : (q == 2 ? lmv2 : lmv3)); };
+            auto lrfq = [&](int q) { return q == 0 ? lrf0 : (q == 1 ? lrf1 : (q == 2 ? lrf2 : lrf3)); };
+            auto ltcq = [&](int pi) -> int {          /* the left MB's piece pi + 3 (luma) / pi + 1 (chroma) */
+                if (pi < 16) return (int)((ltc >> (8 * (pi >> 2))) & 255u);
+                const int k = (pi - 18) >> 1;          /* 18 -> 19, 20 -> 21, 22 -> 23, 24 -> 25 */
+                return (int)((ltc2 >> (8 * k)) & 255u);
+            };
+            auto tcg = [&](int pi) -> int { return L.tcc[pi][lane]; };
+            auto ncx = [&](int pi, bool aA) -> int {   /* no MB above in the slice: nB from this MB only */
+                int nA, nB;
+                if (pi < 16) {
+                    const int bx = pi & 3, by = pi >> 2;
+                    nA = bx ? tcg(pi - 1) : (aA ? ltcq(pi) : -1);
+                    nB = by ? tcg(pi - 4) : -1;
+                } else {
+                    const int k = (pi - 18) & 3, bx = k & 1, by = k >> 1;
+                    nA = bx ? tcg(pi - 1) : (aA ? ltcq(pi) : -1);
+                    nB = by ? tcg(pi - 2) : -1;
+                }
+                return nc2(nA, nB);
+            };
+            auto next = [&]() {
+                ++m;
+                if (++x == W) {
+                    x = 0;
+                    ++y;
+                }
+            };
+            bool fail = false;
+            for (bool first_mb = true; !fail; first_mb = false) {
+                if (r.p >= end && !first_mb) break;
+                const uint32_t run = r.ue();
+                if (r.bad || r.over() || run > (uint32_t)(nmb - m)) {
+                    fail = true;
+                    break;
+                }
+                for (uint32_t k = 0; k < run; ++k, next()) {           /* P_Skip */
+                    if (m - W >= m0 && y > 0) {                        /* the MB above is in the slice */
+                        status = SPLICE_REDO;
+                        fail = true;
+                        break;
+                    }
+                    const bool aA = x > 0 && m - 1 >= m0;
+                    const int px = 0, py = 0;                          /* 8.4.1.1: the MB above unavailable */
+                    SpliceMbRec *R = rec + m;
+                    R->ref = 0;
+                    R->cbp = 0;
+                    R->qpd = 0;
+                    R->mx = px;
+                    R->my = py;
+                    R->skip = 1;
+                    R->part = 0;
+                    R->intra = 0;
+                    R->hasqpd = 0;
+                    R->nbsame = (uint8_t)(aA ? 1 : 0);
+                    R->res_len = 0;
+                    for (int j = 0; j < SPLICE_PIECES; ++j) {
+                        R->tc[j] = 0;
+                        R->t1[j] = 0;
+                        R->blen[j] = 0;
+                    }
+                    const uint32_t v = pk_mv(px, py);
+                    if (m == m0) {
+                        fmv = v;
+                        frf = 0;
+                    }
+                    lmv0 = lmv1 = lmv2 = lmv3 = v;
+                    lrf0 = lrf1 = lrf2 = lrf3 = 0;
+                    ltc = ltc2 = 0;
+                    lim = 0xffffffffu;
+                }
+                if (fail) break;
+                if (r.p >= end) {
+                    if (run == 0) fail = true;
+                    break;
+                }
+                if (m == nmb) {
+                    fail = true;
+                    break;
+                }
+                if (m - W >= m0 && y > 0) {
+                    status = SPLICE_REDO;
+                    fail = true;
+                    break;
+                }
+                const bool aA = x > 0 && m - 1 >= m0, aC = y > 0 && x + 1 < W && m - W + 1 >= m0;
+                const uint32_t mbt = r.ue();
+                if (r.bad || r.over() || mbt > 30u) {
+                    fail = true;
+                    break;
+                }
+                SpliceMbRec *R = rec + m;
+                for (int j = 0; j < SPLICE_PIECES; ++j) L.tcc[j][lane] = 0;
+                int cbp = 0, hasqpd = 0, qpd = 0, intra = 0, cbp_code = 0;
+                uint32_t coded = 0;                                     /* pieces parsed */
+                uint32_t rs0 = 0, rsn = 0, poff = 0, plen = 0;
+                uint32_t nim = 0xffffffffu;                             /* this MB's modes 3 7 11 15 */
+                Mv me{0, 0, 0};
+                int part = 0;
+                bool pcm = false;
+                if (mbt >= 5u) {
+                    const int it = (int)mbt - 5;
+                    intra = it == 0 ? 1 : (it == 25 ? 3 : 2);
+                    me = Mv{SPLICE_REF_INTRA, 0, 0};
+                    if (intra == 3) {
+                        pcm = true;
+                        bool bad = false;
+                        if (r.p & 7u) bad = r.u(8 - (int)(r.p & 7u)) != 0u;
+                        poff = r.p;
+                        for (int k = 0; k < 96; ++k) r.skip(32);
+                        if (bad || r.over()) {
+                            fail = true;
+                            break;
+                        }
+                        for (int j = 0; j < SPLICE_PIECES; ++j) L.tcc[j][lane] = 16;
+                    } else {
+                        int m0d = -1, m3 = -1;
+                        poff = r.p;
+                        if (intra == 1) {
+                            for (int blk = 0; blk < 16; ++blk) {
+                                const int ri = blk_raster16(blk), bx = ri & 3, by = ri >> 2;
+                                const int mA = bx ? (int)L.im[ri - 1][lane]
+                                                  : (aA ? (int)(int8_t)((lim >> (8 * by)) & 255u) : -2);
+                                const int mB = by ? (int)L.im[ri - 4][lane] : -2;
+                                const int pm = (mA == -2 || mB == -2) ? 2 : min(mA < 0 ? 2 : mA, mB < 0 ? 2 : mB);
+                                int md = pm;
+                                if (!r.u(1)) {
+                                    const int rem = (int)r.u(3);
+                                    md = rem < pm ? rem : rem + 1;
+                                }
+                                L.im[ri][lane] = (int8_t)md;
+                            }
+                            m0d = L.im[0][lane];
+                            m3 = L.im[3][lane];
+                            nim = (uint32_t)(uint8_t)L.im[3][lane] | (uint32_t)(uint8_t)L.im[7][lane] << 8 |
+                                  (uint32_t)(uint8_t)L.im[11][lane] << 16 | (uint32_t)(uint8_t)L.im[15][lane] << 24;
+                        } else {
+                            m0d = (it - 1) & 3;
+                        }
+                        const uint32_t cm = r.ue();
+                        plen = r.p - poff;
+                        if (r.bad || r.over() || cm > 3u) {
+                            fail = true;
+                            break;
+                        }
+                        bool na = cm == 0 || cm == 1 || cm == 3, nbb = cm == 0 || cm == 2 || cm == 3, nd = cm == 3,
+                             nc = false;
+                        if (intra == 1) {
+                            na = nbb = true;
+                            nd = nd || m0d == 4 || m0d == 5 || m0d == 6;
+                            nc = m3 == 3 || m3 == 7;
+                        } else {
+                            na = na || m0d != 0;
+                            nbb = nbb || m0d != 1;
+                            nd = nd || m0d == 3;
+                        }
+                        auto same = [&](int dx, int dy, bool ext) {
+                            const int X = x0c + x + dx, Y = y0c + y + dy;
+                            return ext == (X >= 0 && Y >= 0 && X < mbw_c);
+                        };
+                        /* B and D are never in this slice here */
+                        if ((na && !same(-1, 0, aA)) || (nbb && !same(0, -1, false)) || (nd && !same(-1, -1, false)) ||
+                            (nc && !same(1, -1, aC))) {
+                            status = SCROLL_SPLICE_ERR_MBTYPE;
+                            fail = true;
+                            break;
+                        }
+                        if (intra == 1) {
+                            const uint32_t code = r.ue();
+                            if (r.bad || r.over() || code > 47u) {
+                                fail = true;
+                                break;
+                            }
+                            cbp_code = (int)code;
+                            cbp = CBP_INTRA[code];
+                        } else {
+                            cbp = ((it - 1) >= 12 ? 15 : 0) | (((it - 1) >> 2) % 3) << 4;
+                        }
+                        hasqpd = cbp || intra == 2;
+                    }
+                } else {
+                    part = mbt == 4u ? 3 : (int)mbt;
+                    uint32_t sub = 0;
+                    const Mv A = aA ? unpk_mv(lrf0, lmv0) : none;
+                    const Mv C = aC ? unpk_mv(frf, fmv) : none;
+                    if (mbt == 0u) {
+                        int ref = 0;
+                        if (nrefs == 2) ref = 1 - (int)r.u(1);
+                        else if (nrefs > 2) ref = (int)r.ue();
+                        const int dx = r.se(), dy = r.se();
+                        int px, py;
+                        predict_spec(A, none, C, ref, px, py);
+                        const long long mx = (long long)px + dx, my = (long long)py + dy;
+                        if (ref >= nrefs || mx < -SPLICE_MAX_MV || mx > SPLICE_MAX_MV || my < -SPLICE_MAX_MV ||
+                            my > SPLICE_MAX_MV) {
+                            fail = true;
+                            break;
+                        }
+                        me = Mv{ref, (int)mx, (int)my};
+                    } else {
+                        bool okp = true;
+                        if (part == 3)
+                            for (int k = 0; k < 4; ++k) {
+                                const uint32_t stp = r.ue();
+                                if (stp > 3u) okp = false;
+                                sub |= (stp & 3u) << (2 * k);
+                            }
+                        const int nref = part == 3 ? 4 : 2;
+                        uint32_t refw = 0;
+                        if (mbt != 4u)
+                            for (int k = 0; k < nref; ++k) {
+                                int rf = 0;
+                                if (nrefs == 2) rf = 1 - (int)r.u(1);
+                                else if (nrefs > 2) rf = (int)r.ue();
+                                if (rf >= nrefs) okp = false;
+                                refw |= (uint32_t)(rf & 255) << (8 * k);
+                            }
+                        if (!okp) {
+                            fail = true;
+                            break;
+                        }
+                        uint32_t dn = 0;
+                        /* block (cx, cy) relative to the MB: inside once decoded,
+                         * the left MB's right column, the slice's first MB's
+                         * block (0, 3) above-right; nothing else above */
+                        auto nb = [&](int cx, int cy) -> Mv {
+                            if (cy >= 0) {
+                                if (cx >= 4) return none;
+                                if (cx >= 0) {
+                                    const int q2 = 4 * cy + cx;
+                                    return (dn >> q2) & 1u ? unpk_mv(L.crf[q2][lane], L.cmv[q2][lane]) : none;
+                                }
+                                return aA ? unpk_mv(lrfq(cy), lmvq(cy)) : none;
+                            }
+                            if (cx >= 4) return aC ? unpk_mv(frf, fmv) : none;
+                            return none;
+                        };
+                        for_parts(part, sub, [&](int bx, int by, int bw, int bh, int mp) {
+                            const int rf = (int)((refw >> (8 * mp)) & 255u);
+                            const int dx = r.se(), dy = r.se();
+                            int px, py;
+                            predict_part(part, mp, bx, by, bw, rf, nb, px, py);
+                            const long long mx = (long long)px + dx, my = (long long)py + dy;
+                            okp = okp && mx >= -SPLICE_MAX_MV && mx <= SPLICE_MAX_MV && my >= -SPLICE_MAX_MV &&
+                                  my <= SPLICE_MAX_MV;
+                            const uint32_t pm = part_mask(bx, by, bw, bh);
+                            for (int q2 = 0; q2 < 16; ++q2)
+                                if ((pm >> q2) & 1u) {
+                                    L.cmv[q2][lane] = pk_mv((int)mx, (int)my);
+                                    L.crf[q2][lane] = (int8_t)rf;
+                                }
+                            dn |= pm;
+                        });
+                        if (!okp || r.bad || r.over()) {
+                            fail = true;
+                            break;
+                        }
+                        me = unpk_mv(L.crf[0][lane], L.cmv[0][lane]);
+                        for (int q2 = 0; q2 < 16; ++q2) {
+                            R->bref[q2] = L.crf[q2][lane];
+                            R->bmv[q2] = L.cmv[q2][lane];
+                        }
+                    }
+                    R->sub = (uint8_t)sub;
+                    const uint32_t code = r.ue();
+                    cbp = code < 48u ? (int)L.cbpi[code] : -1;
+                    if (r.bad || r.over() || cbp < 0) {
+                        fail = true;
+                        break;
+                    }
+                    hasqpd = cbp != 0;
+                }
+                R->ref = (int16_t)me.ref;
+                R->mx = me.mx;
+                R->my = me.my;
+                R->skip = 0;
+                R->part = (uint8_t)part;
+                if (intra) R->sub = 0;
+                if (hasqpd) {
+                    const int dq = r.se();
+                    if (dq < -26 || dq > 25) {
+                        fail = true;
+                        break;
+                    }
+                    qp = (qp + dq + 52) % 52;
+                    int d = qp - qp_c;
+                    if (d < -26) d += 52;
+                    if (d > 25) d -= 52;
+                    qpd = d;
+                    qp_c = qp;
+                    if (fq_mb < 0) {
+                        fq_mb = m;
+                        fq_qp = qp;
+                    }
+                    last_qp = qp;
+                    rs0 = r.p;
+                    const int lmax = intra == 2 ? 15 : 16;
+                    bool okr = true;
+                    /* one piece in syntax order: TotalCoeff, TrailingOnes and
+                     * where its body sits in the frame's RBSP */
+                    auto lane_piece = [&](int pi, int nC, int maxc) {
+                        if (!okr) return;
+                        int tc, t1;
+                        uint32_t bo, bl;
+                        if (!lane_block(r, L, nC, maxc, tc, t1, bo, bl)) {
+                            okr = false;
+                            return;
+                        }
+                        L.tcc[pi][lane] = (uint8_t)tc;
+                        R->t1[pi] = (uint8_t)t1;
+                        R->boff[pi] = base + bo;
+                        R->blen[pi] = (uint16_t)bl;
+                        coded |= 1u << pi;
+                    };
+                    if (intra == 2) lane_piece(26, ncx(0, aA), 16);
+                    for (int blk = 0; blk < 16; ++blk)
+                        if (cbp & (1 << (blk >> 2))) {
+                            const int pi = blk_raster16(blk);
+                            lane_piece(pi, ncx(pi, aA), lmax);
+                        }
+                    if (cbp >> 4) {
+                        lane_piece(16, -1, 4);
+                        lane_piece(17, -1, 4);
+                        if ((cbp >> 4) == 2)
+                            for (int pi = 18; pi < 26; ++pi) lane_piece(pi, ncx(pi, aA), 15);
+                    }
+                    if (!okr) {
+                        fail = true;
+                        break;
+                    }
+                    rsn = r.p - rs0;
+                }
+                R->cbp = (uint8_t)cbp;
+                R->qpd = (int8_t)qpd;
+                R->hasqpd = (uint8_t)hasqpd;
+                R->intra = (uint8_t)intra;
+                R->mbt = (uint8_t)mbt;
+                R->cbp_code = (uint8_t)cbp_code;
+                R->poff = base + poff;
+                R->plen = (uint16_t)plen;
+                R->nbsame = (uint8_t)(aA ? 1 : 0);
+                R->res_off = base + rs0;
+                R->res_len = rsn;
+                for (int j = 0; j < SPLICE_PIECES; ++j) {
+                    R->tc[j] = L.tcc[j][lane];
+                    if (!((coded >> j) & 1u)) {
+                        R->t1[j] = 0;
+                        R->blen[j] = 0;
+                    }
+                }
+                /* hand the context on */
+                const bool parted = part != 0;
+                if (m == m0) {
+                    fmv = parted ? L.cmv[12][lane] : pk_mv(me.mx, me.my);
+                    frf = parted ? L.crf[12][lane] : me.ref;
+                }
+                lmv0 = parted ? L.cmv[3][lane] : pk_mv(me.mx, me.my);
+                lmv1 = parted ? L.cmv[7][lane] : lmv0;
+                lmv2 = parted ? L.cmv[11][lane] : lmv0;
+                lmv3 = parted ? L.cmv[15][lane] : lmv0;
+                lrf0 = parted ? L.crf[3][lane] : me.ref;
+                lrf1 = parted ? L.crf[7][lane] : lrf0;
+                lrf2 = parted ? L.crf[11][lane] : lrf0;
+                lrf3 = parted ? L.crf[15][lane] : lrf0;
+                ltc = (uint32_t)L.tcc[3][lane] | (uint32_t)L.tcc[7][lane] << 8 | (uint32_t)L.tcc[11][lane] << 16 |
+                      (uint32_t)L.tcc[15][lane] << 24;
+                ltc2 = (uint32_t)L.tcc[19][lane] | (uint32_t)L.tcc[21][lane] << 8 | (uint32_t)L.tcc[23][lane] << 16 |
+                       (uint32_t)L.tcc[25][lane] << 24;
+                lim = nim;
+                next();
+            }
+            if (!fail) {
+                if (r.p != end || r.u(1) != 1u) fail = true;
+                if (!fail && (r.p & 7u)) {
+                    const int k = 8 - (int)(r.p & 7u);
+                    if (r.u(k)) fail = true;
+                }
+                while (!fail && r.p < r.nbits)
+                    if (r.u(8)) fail = true;
+                if (!fail && !r.bad && !r.over()) status = SCROLL_SPLICE_OK;
+            }
+        }
+        UN->first = first;
+        UN->nmb = m - (first < 0 ? 0 : first);
+        UN->status = status;
+        UN->fq_mb = fq_mb;
+        UN->fq_qp = fq_qp;
+        UN->last_qp = last_qp;
+    }
 }
 
 /* k_splice_parse: one wave parses one slice (NAL unit; a frame's units are
@@ -601,74 +1385,22 @@ __global__ __launch_bounds__(64) void k_splice_parse(int n, const int32_t *__res
     const LaneTabs T = lane_tabs();
     for (int u = (int)blockIdx.y; u < nu; u += (int)gridDim.y) {
     SpliceUnit *UN = units + F->unit_first + u;
+    /* k_splice_unesc's bad NAL header; the lanes' slices unless handed back */
+    const int st0 = U(UN->status);
+    if (st0 == SCROLL_SPLICE_ERR_NAL || (F->nunits >= SPLICE_LANE_MIN && F->nunits <= SPLICE_MAXU && st0 != SPLICE_REDO))
+        continue;
     /* the NAL pointer is a generic one, so the compiler takes its bytes for
-     * per-lane values: the header bytes go through readfirstlane, or every
-     * branch on them -- and the whole bit reader after it -- turns divergent */
-    const uint32_t ub = U(UN->b);
-    const uint8_t *p = F->nal + ub;
-    const uint32_t len = U(UN->e) - ub;
-    auto byte = [&](uint32_t k) { return (uint32_t)__builtin_amdgcn_readfirstlane(k < len ? p[k] : 0u); };
-    int status = SCROLL_SPLICE_ERR_NAL, first = -1, m = 0;
+     * per-lane values: the header byte goes through readfirstlane, or every
+     * branch on it -- and the whole bit reader after it -- turns divergent */
+    const uint32_t h0 = U(F->nal[U(UN->b)]);
+    int status = SCROLL_SPLICE_ERR_HEADER, first = -1, m = 0;
     int fq_mb = -1, fq_qp = 0, last_qp = 0;
-    const uint32_t h0 = byte(0);
     SRd r;
-    uint32_t end = 0, base = 0;
-    if (len < 2 || (h0 & 0x80) || (h0 & 31) != 1) goto done;
-    status = SCROLL_SPLICE_ERR_HEADER;
+    const uint32_t w0 = U(UN->w0), nb = U(UN->nbytes), end = U(UN->end), base = 32u * w0;
     if (W > PARSE_MAXW) goto done;
     {
     const int ref_idc = (int)(h0 >> 5) & 3;
-    /* emulation prevention bytes out (7.4.1): byte i of the payload goes
-     * unless it is 03 after two zero bytes; 4 bytes per lane per pass, the
-     * output index by a wave prefix count; bytes land MSB-first in words
-     * (byte k at byte address k ^ 3) from word ceil(b / 4) of the frame's
-     * region on -- (len + 2) / 4 words, which never reach the next unit's */
-    const uint32_t w0 = (ub + 3u) >> 2;
-    base = 32u * w0;
-    uint32_t *o = rbsp + F->rbsp_word + w0;
-    const uint32_t nwmax = (len + 2u) / 4u;
-    for (uint32_t k = (uint32_t)lane; k < nwmax; k += 64) o[k] = 0u;
-    __syncthreads();
-    uint8_t *ob = reinterpret_cast<uint8_t *>(o);
-    uint32_t nb = 0;
-    for (uint32_t c0 = 1; c0 < len; c0 += 256) {
-        uint32_t keep = 0, cnt = 0;
-        uint8_t by[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const uint32_t k = c0 + 4u * (uint32_t)lane + (uint32_t)q;
-            by[q] = k < len ? p[k] : 0;
-            const bool ep = k < len && k >= 3 && by[q] == 3 && p[k - 1] == 0 && p[k - 2] == 0;
-            const bool kp = k < len && !ep;
-            keep |= kp ? 1u << q : 0u;
-            cnt += kp ? 1u : 0u;
-        }
-        const uint32_t incl = wave_incl_sum(cnt, lane);
-        uint32_t at = nb + incl - cnt;
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-            if (keep & (1u << q)) {
-                ob[at ^ 3u] = by[q];
-                at++;
-            }
-        nb += __builtin_amdgcn_readlane(incl, 63);
-    }
-    __syncthreads();
-    nb = __builtin_amdgcn_readfirstlane(nb);
-    const uint32_t nw = (nb + 3u) >> 2;
-    /* rbsp_stop_one_bit: the last 1 bit (none: end 0, the parse fails) */
-    for (int c = (int)nw - 1; c >= 0; c -= 64) {
-        const int k = c - lane;
-        const uint32_t v = k >= 0 ? o[k] : 0u;
-        const uint64_t bl = __ballot(v != 0u);
-        if (bl) {
-            const int l = __builtin_ctzll(bl);
-            const uint32_t vv = U((uint32_t)__builtin_amdgcn_readlane(v, l));
-            end = 32u * (uint32_t)(c - l) + 31u - (uint32_t)__builtin_ctz(vv);
-            break;
-        }
-    }
-    r.init(o, nw, 8u * nb);
+    r.init(rbsp + F->rbsp_word + w0, (nb + 3u) >> 2, 8u * nb);
 
     int nrefs = 2;                         /* the composer's PPS (h264_writer.c:114) */
     first = (int)r.ue();                                           /* first_mb_in_slice */
@@ -1074,10 +1806,11 @@ done:
 __global__ __launch_bounds__(64) void k_splice_fix(int n, const int32_t *__restrict__ list,
                                                    SpliceFrame *__restrict__ spf,
                                                    const SpliceUnit *__restrict__ units,
-                                                   SpliceMbRec *__restrict__ recs)
+                                                   SpliceMbRec *__restrict__ recs, int32_t *__restrict__ lanes)
 {
     const int i = blockIdx.x;
     if (i >= n || threadIdx.x != 0) return;
+    if (i == 0) lanes[0] = 0;                           /* the lane list, empty for the next parse */
     SpliceFrame *F = spf + list[i];
     const int nmb = F->w * F->h, nall = F->nunits;
     const int nu = min(nall, (int)splice_unit_cap(nmb));
@@ -1558,14 +2291,18 @@ __global__ __launch_bounds__(DT) void k_splice_stage(DevStream *__restrict__ st,
 }  // namespace
 
 int splice_launch_parse(hipStream_t hs, int n, int ymax, const int32_t *list, SpliceFrame *spf,
-                        SpliceUnit *units, const DevStream *st, int ld_fr, uint32_t *rbsp,
-                        SpliceMbRec *rec)
+                        SpliceUnit *units, int32_t *lanes, size_t nslots, const DevStream *st, int ld_fr,
+                        uint32_t *rbsp, SpliceMbRec *rec)
 {
     if (n <= 0) return 0;
-    hipLaunchKernelGGL(k_splice_units, dim3(n), dim3(DT), 0, hs, n, list, spf, units);
-    hipLaunchKernelGGL(k_splice_parse, dim3(n, (unsigned)std::max(1, std::min(ymax, 64))), dim3(64), 0, hs, n,
-                       list, spf, units, st, ld_fr, rbsp, rec);
-    hipLaunchKernelGGL(k_splice_fix, dim3(n), dim3(64), 0, hs, n, list, spf, units, rec);
+    const dim3 gy(n, (unsigned)std::max(1, std::min(ymax, 64)));
+    hipLaunchKernelGGL(k_splice_units, dim3(n), dim3(DT), 0, hs, n, list, spf, units, lanes);
+    hipLaunchKernelGGL(k_splice_unesc, gy, dim3(64), 0, hs, n, list, spf, units, rbsp);
+    const unsigned lw = (unsigned)std::min<size_t>((nslots + 64 * LANE_WAVES - 1) / (64 * LANE_WAVES), 4096);
+    hipLaunchKernelGGL(k_splice_lanes, dim3(std::max(lw, 1u)), dim3(64 * LANE_WAVES), 0, hs, list, spf, units, lanes, st,
+                       ld_fr, rbsp, rec);
+    hipLaunchKernelGGL(k_splice_parse, gy, dim3(64), 0, hs, n, list, spf, units, st, ld_fr, rbsp, rec);
+    hipLaunchKernelGGL(k_splice_fix, dim3(n), dim3(64), 0, hs, n, list, spf, units, rec, lanes);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

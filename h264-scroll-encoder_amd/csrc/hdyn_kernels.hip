@@ -294,12 +294,15 @@ __global__ __launch_bounds__(HD_T) void k_hdyn_code(const DevStream *__restrict_
         dcn = L.tc[16] + L.tc[17];
         for (int k = 18; k < 26; ++k) acn += L.tc[k];
         r.cbp = (uint8_t)(cbp_l | (acn ? 2 : (dcn ? 1 : 0)) << 4);
+        uint32_t body = 0;
         for (int k = 0; k < 26; ++k) {
             r.tc[k] = L.tc[k];
             r.t1[k] = L.t1[k];
             r.blen[k] = (uint16_t)L.len[k];
             r.boff[k] = 32u * (uint32_t)q * mb_words + L.off[k];
+            body += L.len[k];
         }
+        r.body = (uint16_t)body;
         *R = r;
     }
 }

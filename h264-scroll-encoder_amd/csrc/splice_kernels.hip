@@ -1019,6 +1019,7 @@ __global__ __launch_bounds__(64 * LANE_WAVES) void k_splice_lanes(const int32_t 
                     R->hasqpd = 0;
                     R->nbsame = (uint8_t)(aA ? 1 : 0);
                     R->res_len = 0;
+                    R->body = 0;
                     for (int j = 0; j < SPLICE_PIECES; ++j) {
                         R->tc[j] = 0;
                         R->t1[j] = 0;
@@ -1057,7 +1058,7 @@ __global__ __launch_bounds__(64 * LANE_WAVES) void k_splice_lanes(const int32_t 
                 SpliceMbRec *R = rec + m;
                 for (int j = 0; j < SPLICE_PIECES; ++j) L.tcc[j][lane] = 0;
                 int cbp = 0, hasqpd = 0, qpd = 0, intra = 0, cbp_code = 0;
-                uint32_t coded = 0;                                     /* pieces parsed */
+                uint32_t coded = 0, body = 0;                           /* pieces parsed, their body bits */
                 uint32_t rs0 = 0, rsn = 0, poff = 0, plen = 0;
                 uint32_t nim = 0xffffffffu;                             /* this MB's modes 3 7 11 15 */
                 Mv me{0, 0, 0};
@@ -1276,6 +1277,7 @@ __global__ __launch_bounds__(64 * LANE_WAVES) void k_splice_lanes(const int32_t 
                         R->boff[pi] = base + bo;
                         R->blen[pi] = (uint16_t)bl;
                         coded |= 1u << pi;
+                        body += bl;
                     };
                     if (intra == 2) lane_piece(26, ncx(0, aA), 16);
                     for (int blk = 0; blk < 16; ++blk)
@@ -1304,6 +1306,7 @@ __global__ __launch_bounds__(64 * LANE_WAVES) void k_splice_lanes(const int32_t 
                 R->poff = base + poff;
                 R->plen = (uint16_t)plen;
                 R->nbsame = (uint8_t)(aA ? 1 : 0);
+                R->body = (uint16_t)body;
                 R->res_off = base + rs0;
                 R->res_len = rsn;
                 for (int j = 0; j < SPLICE_PIECES; ++j) {
@@ -1534,6 +1537,7 @@ __global__ __launch_bounds__(64) void k_splice_parse(int n, const int32_t *__res
                     R->hasqpd = 0;
                     R->nbsame = (uint8_t)((aA ? 1 : 0) | (aB ? 2 : 0));
                     R->res_len = 0;
+                    R->body = 0;
                 }
                 if (lane < SPLICE_PIECES) {
                     R->tc[lane] = 0;
@@ -1752,10 +1756,13 @@ __global__ __launch_bounds__(64) void k_splice_parse(int n, const int32_t *__res
                 }
                 rsn = r.pos() - rs0;
             }
+            const uint32_t body = (uint32_t)__builtin_amdgcn_readlane(
+                wave_incl_sum(lane < SPLICE_PIECES ? po.len : 0u, lane), 63);
             if (lane == 0) {
                 R->cbp = (uint8_t)cbp;
                 R->qpd = (int8_t)qpd;
                 R->hasqpd = (uint8_t)hasqpd;
+                R->body = (uint16_t)body;
                 R->intra = (uint8_t)intra;
                 R->mbt = (uint8_t)mbt;
                 R->cbp_code = (uint8_t)cbp_code;
@@ -1861,9 +1868,42 @@ struct SpliceLds {
     int32_t wmax[NW];
     uint64_t pcm_mask[NW];                  /* I_PCM MBs of the window (alignment) */
     uint8_t pcm_key[DT];
+    uint4 etc[RING];                        /* MB m's edge TotalCoeffs at m % RING (EdgeTc; 0: not spliced) */
+    PTabs pt;                               /* coeff_token (len << 8 | bits) */
+    uint8_t cbpc[48];                       /* inter coded_block_pattern -> codeNum */
     uint32_t ep_n;
     int32_t bad;
 };
+static_assert(offsetof(SpliceMbRec, blen) == SPLICE_REC_HEAD && sizeof(SpliceMbRec) == 352,
+              "the stage copies a record's first SPLICE_REC_HEAD bytes in 16-byte loads");
+
+/* an MB's TotalCoeffs its right / lower neighbour reads for nC: x = pieces 3
+ * 7 11 15, y = 19 21 23 25 (right column), z = 12 13 14 15, w = 20 21 24 25
+ * (bottom row), a byte each */
+__device__ inline uint4 edge_tc(const SpliceMbRec &h)
+{
+    auto b4 = [&](int a, int b, int c, int d) {
+        return (uint32_t)h.tc[a] | (uint32_t)h.tc[b] << 8 | (uint32_t)h.tc[c] << 16 | (uint32_t)h.tc[d] << 24;
+    };
+    return make_uint4(b4(3, 7, 11, 15), b4(19, 21, 23, 25), b4(12, 13, 14, 15), b4(20, 21, 24, 25));
+}
+
+/* nC of piece i (luma raster 0..15, chroma AC 18..25) of MB h whose left /
+ * top neighbours' edge TotalCoeffs are l / t (al / at: available) */
+__device__ inline int nc_edge(int i, const SpliceMbRec &h, const uint4 &l, const uint4 &t, bool al, bool at)
+{
+    int nA, nB;
+    if (i < 16) {
+        const int bx = i & 3, by = i >> 2;
+        nA = bx ? (int)h.tc[i - 1] : (al ? (int)((l.x >> (8 * by)) & 255u) : -1);
+        nB = by ? (int)h.tc[i - 4] : (at ? (int)((t.z >> (8 * bx)) & 255u) : -1);
+    } else {
+        const int k = (i - 18) & 3, pl = (i - 18) >> 2, bx = k & 1, by = k >> 1;
+        nA = bx ? (int)h.tc[i - 1] : (al ? (int)((l.y >> (8 * (2 * pl + by))) & 255u) : -1);
+        nB = by ? (int)h.tc[i - 2] : (at ? (int)((t.w >> (8 * (2 * pl + bx))) & 255u) : -1);
+    }
+    return nc2(nA, nB);
+}
 
 /* ORs MSB-first words into the byte-order staging slot */
 struct GlobOr {
@@ -1902,52 +1942,65 @@ __device__ inline void put_rbsp(SK &sk, const uint32_t *rb, uint32_t q0, uint32_
  * mb_qp_delta and the pieces (I_16x16: its DC first).  An MB whose left and
  * top neighbours are spliced from the same slice (nbsame 3) sees the nC of
  * its external picture in every block: its residual is the external one bit
- * for bit and goes over as one run (parsed records only: res_len) */
+ * for bit and goes over as one run (parsed records only: res_len).  h: the
+ * record's head in registers; the counting sweep takes the bodies' length
+ * from h.body, the writing sweep each body's bits from the record (R) */
 template <class SK>
-__device__ inline void splice_tail(SK &sk, const SpliceMbRec &mb, const uint8_t *L, const uint8_t *T,
-                                   const uint32_t *rb, uint32_t pad)
+__device__ inline void splice_tail(SK &sk, const SpliceMbRec &h, const SpliceMbRec *R, const uint4 &l,
+                                   const uint4 &t, bool al, bool at, const SpliceLds &LS, const uint32_t *rb,
+                                   uint32_t pad)
 {
-    const int cbp = mb.cbp;
-    if (mb.intra == 3) {
+    constexpr bool count = __is_same(SK, CountSink);
+    const int cbp = h.cbp;
+    if (h.intra == 3) {
         sk.put(0u, (int)pad);                                  /* pcm_alignment_zero_bits */
-        put_rbsp(sk, rb, mb.poff, 384u * 8u);
+        put_rbsp(sk, rb, h.poff, 384u * 8u);
         return;
     }
-    if (mb.intra) {
-        put_rbsp(sk, rb, mb.poff, mb.plen);
-        if (mb.intra == 1) put_ue(sk, mb.cbp_code);
-        if (!mb.hasqpd) return;
+    if (h.intra) {
+        put_rbsp(sk, rb, h.poff, h.plen);
+        if (h.intra == 1) put_ue(sk, h.cbp_code);
+        if (!h.hasqpd) return;
     } else {
-        put_ue(sk, SPT.cbp_code[cbp]);
+        put_ue(sk, LS.cbpc[cbp]);
         if (!cbp) return;
     }
-    put_se(sk, mb.qpd);
-    if ((mb.nbsame & 3) == 3 && mb.res_len) {
-        put_rbsp(sk, rb, mb.res_off, mb.res_len);
+    put_se(sk, h.qpd);
+    if ((h.nbsame & 3) == 3 && h.res_len) {
+        put_rbsp(sk, rb, h.res_off, h.res_len);
         return;
     }
+    if constexpr (count) sk.n += h.body;
     auto piece = [&](int i, int nC) {
-        uint32_t v;
-        int len;
-        coeff_token(SPT, mb.tc[i], mb.t1[i], nC, v, len);
-        sk.put(v, len);
-        put_rbsp(sk, rb, mb.boff[i], mb.blen[i]);
+        const int tc = h.tc[i], t1 = h.t1[i];
+        uint32_t v, len;
+        if (nC >= 8) {
+            v = tc ? (uint32_t)(((tc - 1) << 2) | t1) : 3u;
+            len = 6;
+        } else {
+            const uint32_t e = LS.pt.ct[nC == -1 ? 3 : (nC < 2 ? 0 : (nC < 4 ? 1 : 2))][4 * tc + t1];
+            v = e & 255u;
+            len = e >> 8;
+        }
+        sk.put(v, (int)len);
+        if constexpr (!count) put_rbsp(sk, rb, R->boff[i], R->blen[i]);
     };
-    if (mb.intra == 2) piece(26, piece_nc(0, mb.tc, L, T));
+    if (h.intra == 2) piece(26, nc_edge(0, h, l, t, al, at));
+#pragma unroll
     for (int blk = 0; blk < 16; ++blk)
         if (cbp & (1 << (blk >> 2))) {
             const int i = blk_raster16(blk);
-            piece(i, piece_nc(i, mb.tc, L, T));
+            piece(i, nc_edge(i, h, l, t, al, at));
         }
     if (cbp >> 4) {
         piece(16, -1);
         piece(17, -1);
-        if ((cbp >> 4) == 2)
-            for (int i = 18; i < 26; ++i) piece(i, piece_nc(i, mb.tc, L, T));
+        if ((cbp >> 4) == 2) {
+#pragma unroll
+            for (int i = 18; i < 26; ++i) piece(i, nc_edge(i, h, l, t, al, at));
+        }
     }
 }
-
-__constant__ uint8_t ZERO_TC[SPLICE_PIECES] = {};
 
 __global__ __launch_bounds__(DT) void k_splice_stage(DevStream *__restrict__ st,
                                                      const NalDesc *__restrict__ nal, int ld_nal,
@@ -1995,6 +2048,8 @@ __global__ __launch_bounds__(DT) void k_splice_stage(DevStream *__restrict__ st,
         L.wv[t] = pend[s].wv[t];
     }
     if (t < nr) L.rc[t] = pool[H.first + t];
+    build_ptabs(SPT, L.pt, t, DT);
+    if (t < 48) L.cbpc[t] = SPT.cbp_code[t];
     const NalDesc d = nal[(size_t)s * ld_nal + j];
     NalCtx c;
     c.w = S->w;
@@ -2049,12 +2104,20 @@ __global__ __launch_bounds__(DT) void k_splice_stage(DevStream *__restrict__ st,
             int x = 0, y = 0, k = -1;
             Mv me{0, 0, 0};
             bool parted = false;
+            SpliceMbRec hd;                                        /* a spliced MB's record head */
+            uint4 et = make_uint4(0u, 0u, 0u, 0u);
             if (m < nmb) {
                 y = (int)div_m((uint32_t)m, m_mbw);
                 x = m - y * mbw;
                 if (x >= SF.x0 && x < SF.x0 + SF.w && y >= SF.y0 && y < SF.y0 + SF.h) {
                     k = (y - SF.y0) * SF.w + (x - SF.x0);
-                    const SpliceMbRec &mb = rec[k];
+                    const uint4 *hp = reinterpret_cast<const uint4 *>(rec + k);
+                    uint4 hv[SPLICE_REC_HEAD / 16];
+#pragma unroll
+                    for (int q = 0; q < SPLICE_REC_HEAD / 16; ++q) hv[q] = hp[q];
+                    __builtin_memcpy(&hd, hv, SPLICE_REC_HEAD);
+                    et = edge_tc(hd);
+                    const SpliceMbRec &mb = hd;
                     me = Mv{mb.ref, mb.mx, mb.my};
                     parted = mb.part != 0;
                     auto valid = [&](int rf) {
@@ -2063,7 +2126,7 @@ __global__ __launch_bounds__(DT) void k_splice_stage(DevStream *__restrict__ st,
                     };
                     my_ref_bad |= !mb.intra && !valid(mb.ref);
                     if (parted)
-                        for (int q = 1; q < 16; ++q) my_ref_bad |= !valid(mb.bref[q]);
+                        for (int q = 1; q < 16; ++q) my_ref_bad |= !valid(rec[k].bref[q]);   /* past the head */
                 } else {
                     bool bad;
                     me = field(L.rc, L.wv, nr, x, y, lay, c.nwp, bad);
@@ -2073,6 +2136,7 @@ __global__ __launch_bounds__(DT) void k_splice_stage(DevStream *__restrict__ st,
                 L.fx[m & (RING - 1)] = me.mx;
                 L.fy[m & (RING - 1)] = me.my;
                 L.fk[m & (RING - 1)] = parted ? k : -1;
+                L.etc[m & (RING - 1)] = et;
             }
             __syncthreads();
             bool coded = false;
@@ -2093,7 +2157,7 @@ __global__ __launch_bounds__(DT) void k_splice_stage(DevStream *__restrict__ st,
                     int sx, sy;
                     pskip_mv(x > 0, y > 0, A, B, C, sx, sy);
                     coded = !pskip ||
-                            !(me.ref == 0 && me.mx == sx && me.my == sy && (k < 0 || rec[k].cbp == 0));
+                            !(me.ref == 0 && me.mx == sx && me.my == sy && (k < 0 || hd.cbp == 0));
                     predict_spec(A, B, C, me.ref, px, py);
                 } else {
                     coded = true;
@@ -2104,11 +2168,9 @@ __global__ __launch_bounds__(DT) void k_splice_stage(DevStream *__restrict__ st,
             int excl, cmax;
             block_excl_max(coded ? m : -1, L.wmax, excl, cmax);
             /* the MB's bits: head, then (spliced) cbp / qp / pieces */
-            const uint8_t *Lt = nullptr, *Tt = nullptr;
-            if (k >= 0) {
-                Lt = x == 0 ? nullptr : (x > SF.x0 ? rec[k - 1].tc : ZERO_TC);
-                Tt = y == 0 ? nullptr : (y > SF.y0 ? rec[k - SF.w].tc : ZERO_TC);
-            }
+            /* the left / top MBs' edge TotalCoeffs (0 outside the rect) */
+            const uint4 el = x > 0 ? L.etc[(m - 1) & (RING - 1)] : make_uint4(0u, 0u, 0u, 0u);
+            const uint4 eu = y > 0 ? L.etc[(m - mbw) & (RING - 1)] : make_uint4(0u, 0u, 0u, 0u);
             /* a partitioned spliced MB's neighbour block (cx, cy) (6.4.11.7) */
             auto pnb = [&](int cx, int cy, uint32_t dn) {
                 if (cy >= 0) {
@@ -2123,13 +2185,13 @@ __global__ __launch_bounds__(DT) void k_splice_stage(DevStream *__restrict__ st,
                 if (cx < 4) return blk(m - mbw, cx, 3);
                 return x + 1 < mbw ? blk(m - mbw + 1, 0, 3) : none;
             };
-            const bool intra = k >= 0 && rec[k].intra;
+            const bool intra = k >= 0 && hd.intra;
             uint32_t pcm_pad = 0;
             auto code_mb = [&](auto &sk) {
                 put_ue(sk, (uint32_t)(m - max(excl, last) - 1));  /* mb_skip_run */
                 if (intra) {
-                    put_ue(sk, rec[k].mbt);                        /* verbatim, like its prediction syntax */
-                    splice_tail(sk, rec[k], Lt, Tt, rb, pcm_pad);
+                    put_ue(sk, hd.mbt);                            /* verbatim, like its prediction syntax */
+                    splice_tail(sk, hd, rec + k, el, eu, x > 0, y > 0, L, rb, pcm_pad);
                     return;
                 }
                 if (parted) {
@@ -2163,7 +2225,7 @@ __global__ __launch_bounds__(DT) void k_splice_stage(DevStream *__restrict__ st,
                     put_se(sk, me.mx - px);
                     put_se(sk, me.my - py);
                 }
-                if (k >= 0) splice_tail(sk, rec[k], Lt, Tt, rb, 0u);
+                if (k >= 0) splice_tail(sk, hd, rec + k, el, eu, x > 0, y > 0, L, rb, 0u);
                 else sk.put(1, 1);                                 /* coded_block_pattern 0 */
             };
             CountSink cs{0};
@@ -2173,7 +2235,7 @@ __global__ __launch_bounds__(DT) void k_splice_stage(DevStream *__restrict__ st,
              * samples at key_n + (pads before it) mod 8 with key_n = its
              * unpadded position mod 8, so pad_n = key_(n-1) - key_n mod 8
              * (key_0 = 0) */
-            const bool pcm = coded && intra && rec[k].intra == 3;
+            const bool pcm = coded && intra && hd.intra == 3;
             if (__syncthreads_or(pcm)) {
                 uint32_t o0, t0;
                 block_excl_sum(cs.n, L.wsum, o0, t0);

@@ -698,7 +698,7 @@ struct LRd {
     const uint32_t *w;
     uint32_t nw, nbits;
     uint64_t buf;
-    uint32_t nv, p, wk, nxt;
+    uint32_t nv, p, wk, nxt, nxt2;
     bool bad;
     __device__ inline uint32_t word(uint32_t k) const { return k < nw ? w[k] : 0u; }
     __device__ inline void init(const uint32_t *words, uint32_t nwords, uint32_t bits)
@@ -709,9 +709,10 @@ struct LRd {
         bad = false;
         buf = (uint64_t)word(0) << 32 | word(1);
         nxt = word(2);
+        nxt2 = word(3);
         nv = 64;
         p = 0;
-        wk = 3;
+        wk = 4;
     }
     __device__ inline uint32_t peek32() const { return (uint32_t)(buf >> 32); }
     __device__ inline void skip(uint32_t n)            /* n <= 32 */
@@ -722,7 +723,8 @@ struct LRd {
         if (nv <= 32u) {
             buf |= (uint64_t)nxt << (32u - nv);
             nv += 32u;
-            nxt = word(wk++);
+            nxt = nxt2;
+            nxt2 = word(wk++);
         }
     }
     __device__ inline bool over() const { return p > nbits; }
@@ -1385,13 +1387,22 @@ __global__ __launch_bounds__(64) void k_splice_parse(int n, const int32_t *__res
     const DevStream S = st[idx / ld_fr];
     const int mbw_c = S.w / 16, x0c = F->x0, y0c = F->y0;
     SpliceMbRec *rec = recs + F->rec_first;
+    /* k_splice_unesc's bad NAL headers and the lanes' slices (unless handed
+     * back) are done: no tables for a wave without a slice left */
+    const bool lanef = F->nunits >= SPLICE_LANE_MIN && F->nunits <= SPLICE_MAXU;
+    auto todo = [&](int u) {
+        const int st0 = U(units[F->unit_first + u].status);
+        return !(st0 == SCROLL_SPLICE_ERR_NAL || (lanef && st0 != SPLICE_REDO));
+    };
+    {
+        bool any = false;
+        for (int u = (int)blockIdx.y; u < nu && !any; u += (int)gridDim.y) any = todo(u);
+        if (!any) return;
+    }
     const LaneTabs T = lane_tabs();
     for (int u = (int)blockIdx.y; u < nu; u += (int)gridDim.y) {
     SpliceUnit *UN = units + F->unit_first + u;
-    /* k_splice_unesc's bad NAL header; the lanes' slices unless handed back */
-    const int st0 = U(UN->status);
-    if (st0 == SCROLL_SPLICE_ERR_NAL || (F->nunits >= SPLICE_LANE_MIN && F->nunits <= SPLICE_MAXU && st0 != SPLICE_REDO))
-        continue;
+    if (!todo(u)) continue;
     /* the NAL pointer is a generic one, so the compiler takes its bytes for
      * per-lane values: the header byte goes through readfirstlane, or every
      * branch on it -- and the whole bit reader after it -- turns divergent */

@@ -1870,6 +1870,19 @@ __global__ __launch_bounds__(64) void k_splice_fix(int n, const int32_t *__restr
 /* ------------------------------------------------------------------------ */
 /* k_splice_stage                                                            */
 /* ------------------------------------------------------------------------ */
+constexpr int SPL_WB = 2048;                 /* writing sweep: LDS words per pass (64 Kbit) */
+
+/* ORs MSB-first words into LDS words [lo, lo + n) (others dropped: another pass) */
+struct LdsWin {
+    uint32_t *b;
+    uint32_t lo, n;
+    __device__ inline void operator()(uint32_t i, uint32_t v) const
+    {
+        const uint32_t k = i - lo;
+        if (k < n && v) atomicOr(&b[k], v);
+    }
+};
+
 struct SpliceLds {
     int32_t fr[RING], fx[RING], fy[RING];   /* motion of MB m at m % RING */
     int32_t fk[RING];                       /* its record if a partitioned spliced MB, else -1 */
@@ -1879,7 +1892,8 @@ struct SpliceLds {
     int32_t wmax[NW];
     uint64_t pcm_mask[NW];                  /* I_PCM MBs of the window (alignment) */
     uint8_t pcm_key[DT];
-    uint4 etc[RING];                        /* MB m's edge TotalCoeffs at m % RING (EdgeTc; 0: not spliced) */
+    uint4 etc[RING];                        /* MB m's edge TotalCoeffs at m % RING (0: not spliced) */
+    uint32_t wbuf[SPL_WB];                  /* the writing sweep's word window */
     PTabs pt;                               /* coeff_token (len << 8 | bits) */
     uint8_t cbpc[48];                       /* inter coded_block_pattern -> codeNum */
     uint32_t ep_n;
@@ -2275,11 +2289,35 @@ __global__ __launch_bounds__(DT) void k_splice_stage(DevStream *__restrict__ st,
             }
             uint32_t off, T;
             block_excl_sum(cs.n, L.wsum, off, T);
-            if (sweep == 1 && coded) {
-                GSink sk{{out}, 0, 0, 0};
-                sk.start(pos + off);
-                code_mb(sk);
-                sk.finish();
+            if (sweep == 1) {
+                /* the window's bits through an LDS word window (passes of
+                 * SPL_WB words), then out with plain stores -- global
+                 * atomics per word would each hold the lane's next loads
+                 * (one in-order vector-memory counter); only the window's
+                 * first and last words, shared with its neighbours, are ORed */
+                const uint32_t wlo = pos >> 5, whi = (pos + T + 31u) >> 5;
+                for (uint32_t b0 = wlo; b0 < whi; b0 += SPL_WB) {
+                    const uint32_t n = min((uint32_t)SPL_WB, whi - b0);
+                    for (uint32_t i = (uint32_t)t; i < n; i += DT) L.wbuf[i] = 0u;
+                    __syncthreads();
+                    const uint32_t a0 = pos + off;
+                    if (coded && a0 < 32u * (b0 + n) && a0 + cs.n > 32u * b0) {
+                        OrSink<LdsWin> sk{LdsWin{L.wbuf, b0, n}, 0, 0, 0};
+                        sk.start(a0);
+                        code_mb(sk);
+                        sk.finish();
+                    }
+                    __syncthreads();
+                    for (uint32_t i = (uint32_t)t; i < n; i += DT) {
+                        const uint32_t v = L.wbuf[i], gi = b0 + i;
+                        if (gi == wlo || gi + 1 == whi) {
+                            if (v) atomicOr(&out[gi], __builtin_bswap32(v));
+                        } else {
+                            out[gi] = __builtin_bswap32(v);
+                        }
+                    }
+                    __syncthreads();
+                }
             }
             pos += T;
             last = max(last, cmax);

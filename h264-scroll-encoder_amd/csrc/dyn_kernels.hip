@@ -2698,86 +2698,66 @@ __global__ __launch_bounds__(DT) void k_dyn_gather(const DevStream *__restrict__
     const int32_t d0 = (int32_t)(o0 - (cfirst << 4)) + 5;
     const int32_t nebsp = (int32_t)(d.size - 5);
     int gg = 0;                                              /* the thread's group, carried */
-    /* one 16-byte chunk: where its 128 RBSP bits sit (fast: at most two
-     * groups), its loads, then the assembly + EP bytes + store; the loop runs
-     * them as a two-stage pipeline (the next chunk's loads in flight while
-     * this one is assembled) */
-    struct Ck {
-        int32_t u0;
-        uint32_t K, lp, rem, wo, wy;
-        bool fast, two, y;
-    };
-    struct Cd {
-        uint32_t x[5], yb[4];
-    };
-    auto prep = [&](uint32_t c, Ck &k) {
-        k.u0 = 16 * (int32_t)c - d0;
-        k.K = raw[k.u0 > 0 ? min(k.u0 >> cs, nblk - 1) : 0];
-        k.fast = false;
-        if (k.u0 >= 0 && k.u0 + 16 <= nebsp) {
-            while ((int32_t)(sp[k.K] + k.K) < k.u0) k.K++;       /* sentinel stops it */
-            const uint32_t i0 = (uint32_t)k.u0 - k.K, P = 8u * i0;
+    for (uint32_t c = cbeg + (uint32_t)t; c < cend; c += DT) {
+        const int32_t u0 = 16 * (int32_t)c - d0;
+        uint8_t *q = A + ((cfirst + c) << 4);
+        uint32_t K = raw[u0 > 0 ? min(u0 >> cs, nblk - 1) : 0];
+        if (u0 >= 0 && u0 + 16 <= nebsp) {
+            while ((int32_t)(sp[K] + K) < u0) K++;               /* sentinel stops it */
+            const uint32_t i0 = (uint32_t)u0 - K, P = 8u * i0;
             while (gg + 1 < ng && goff[gg + 1] <= P) ++gg;
             while (gg > 0 && goff[gg] > P) --gg;                 /* never for increasing P */
-            k.lp = P - goff[gg];
-            k.rem = gb[gg] - k.lp;                               /* bits left in the group */
-            k.two = k.rem < 128u;
-            k.fast = !k.two || gg + 1 >= ng || gb[gg + 1] >= 128u - k.rem;
-            k.wo = 4u * (gw[gg] + (k.lp >> 5));                  /* 160 bits of the group from word lp >> 5 */
-            k.y = k.two && gg + 1 < ng;
-            k.wy = k.y ? 4u * gw[gg + 1] : 0u;
-        }
-    };
-    auto fetch = [&](const Ck &k, Cd &d) {
-        const auto xa = __builtin_amdgcn_raw_buffer_load_b128(rr, k.wo, 0, 0);
-        d.x[4] = __builtin_amdgcn_raw_buffer_load_b32(rr, k.wo + 16u, 0, 0);
-        d.x[0] = (uint32_t)xa[0]; d.x[1] = (uint32_t)xa[1]; d.x[2] = (uint32_t)xa[2]; d.x[3] = (uint32_t)xa[3];
-        d.yb[0] = d.yb[1] = d.yb[2] = d.yb[3] = 0u;
-        if (k.y) {
-            const auto y = __builtin_amdgcn_raw_buffer_load_b128(rr, k.wy, 0, 0);
-            d.yb[0] = (uint32_t)y[0]; d.yb[1] = (uint32_t)y[1]; d.yb[2] = (uint32_t)y[2]; d.yb[3] = (uint32_t)y[3];
-        }
-    };
-    auto assemble = [&](uint32_t c, const Ck &k, const Cd &d) {
-        uint8_t *q = A + ((cfirst + c) << 4);
-        const uint32_t sh = k.lp & 31u;
-        W4 R;
+            const uint32_t lp = P - goff[gg], rem = gb[gg] - lp;  /* bits left in the group */
+            const bool two = rem < 128u;
+            if (!two || gg + 1 >= ng || gb[gg + 1] >= 128u - rem) {
+                /* 160 bits of the group from word lp >> 5 */
+                const uint32_t wo = 4u * (gw[gg] + (lp >> 5));
+                const auto xa = __builtin_amdgcn_raw_buffer_load_b128(rr, wo, 0, 0);
+                const uint32_t x4 = __builtin_amdgcn_raw_buffer_load_b32(rr, wo + 16u, 0, 0);
+                uint32_t yb[4] = {0u, 0u, 0u, 0u};
+                if (two && gg + 1 < ng) {
+                    const auto y = __builtin_amdgcn_raw_buffer_load_b128(rr, 4u * gw[gg + 1], 0, 0);
+                    yb[0] = (uint32_t)y[0]; yb[1] = (uint32_t)y[1]; yb[2] = (uint32_t)y[2]; yb[3] = (uint32_t)y[3];
+                }
+                const uint32_t x[5] = {(uint32_t)xa[0], (uint32_t)xa[1], (uint32_t)xa[2], (uint32_t)xa[3], x4};
+                const uint32_t sh = lp & 31u;
+                W4 R;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) R.w[j] = sh ? __builtin_amdgcn_alignbit(d.x[j], d.x[j + 1], 32u - sh) : d.x[j];
-        if (k.two) {                                             /* rem bits of this group, then the next */
-            const W4 B = shr128(W4{{d.yb[0], d.yb[1], d.yb[2], d.yb[3]}}, k.rem);
+                for (int k = 0; k < 4; ++k) R.w[k] = sh ? __builtin_amdgcn_alignbit(x[k], x[k + 1], 32u - sh) : x[k];
+                if (two) {                                       /* rem bits of this group, then the next */
+                    const W4 B = shr128(W4{{yb[0], yb[1], yb[2], yb[3]}}, rem);
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const uint32_t kb = 32u * (uint32_t)j;           /* bits of word j kept from this group */
-                const uint32_t keep = k.rem <= kb ? 0u : (k.rem >= kb + 32u ? 32u : k.rem - kb);
-                const uint32_t m = keep == 0u ? 0u : (keep == 32u ? 0xffffffffu : ~(0xffffffffu >> keep));
-                R.w[j] = (R.w[j] & m) | B.w[j];
+                    for (int k = 0; k < 4; ++k) {
+                        const uint32_t kb = 32u * (uint32_t)k;  /* bits of word k kept from this group */
+                        const uint32_t keep = rem <= kb ? 0u : (rem >= kb + 32u ? 32u : rem - kb);
+                        const uint32_t m = keep == 0u ? 0u : (keep == 32u ? 0xffffffffu : ~(0xffffffffu >> keep));
+                        R.w[k] = (R.w[k] & m) | B.w[k];
+                    }
+                }
+                /* the EP bytes inside the chunk: byte e becomes 03, the
+                 * bytes from e on move one byte later */
+                for (uint32_t m = K;; ++m) {
+                    const int32_t e = (int32_t)(sp[m] + m) - u0;
+                    if (e >= 16) break;
+                    const W4 S = shr128(R, 8u);
+                    const uint32_t eb = 8u * (uint32_t)e;
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        const uint32_t kb = 32u * (uint32_t)k;
+                        const uint32_t keep = eb <= kb ? 0u : (eb >= kb + 32u ? 32u : eb - kb);
+                        const uint32_t mk = keep == 0u ? 0u : (keep == 32u ? 0xffffffffu : ~(0xffffffffu >> keep));
+                        /* the 03 byte: bits [eb, eb + 8) */
+                        const uint32_t three = (eb >= kb && eb < kb + 32u) ? (3u << (24u - (eb - kb))) : 0u;
+                        const uint32_t mk2 = (eb >= kb && eb < kb + 32u) ? (0xff000000u >> (eb - kb)) : 0u;
+                        R.w[k] = (R.w[k] & mk) | (S.w[k] & ~mk & ~mk2) | three;
+                    }
+                }
+                *reinterpret_cast<uint4 *>(q) = make_uint4(__builtin_bswap32(R.w[0]), __builtin_bswap32(R.w[1]),
+                                                           __builtin_bswap32(R.w[2]), __builtin_bswap32(R.w[3]));
+                continue;
             }
         }
-        /* the EP bytes inside the chunk: byte e becomes 03, the bytes from e
-         * on move one byte later */
-        for (uint32_t m = k.K;; ++m) {
-            const int32_t e = (int32_t)(sp[m] + m) - k.u0;
-            if (e >= 16) break;
-            const W4 S = shr128(R, 8u);
-            const uint32_t eb = 8u * (uint32_t)e;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const uint32_t kb = 32u * (uint32_t)j;
-                const uint32_t keep = eb <= kb ? 0u : (eb >= kb + 32u ? 32u : eb - kb);
-                const uint32_t mk = keep == 0u ? 0u : (keep == 32u ? 0xffffffffu : ~(0xffffffffu >> keep));
-                /* the 03 byte: bits [eb, eb + 8) */
-                const uint32_t three = (eb >= kb && eb < kb + 32u) ? (3u << (24u - (eb - kb))) : 0u;
-                const uint32_t mk2 = (eb >= kb && eb < kb + 32u) ? (0xff000000u >> (eb - kb)) : 0u;
-                R.w[j] = (R.w[j] & mk) | (S.w[j] & ~mk & ~mk2) | three;
-            }
-        }
-        *reinterpret_cast<uint4 *>(q) = make_uint4(__builtin_bswap32(R.w[0]), __builtin_bswap32(R.w[1]),
-                                                   __builtin_bswap32(R.w[2]), __builtin_bswap32(R.w[3]));
-    };
-    /* NAL edges and three-group chunks: byte by byte */
-    auto bytewise = [&](uint32_t c, uint32_t K) {
-        uint8_t *q = A + ((cfirst + c) << 4);
+        /* NAL edges and three-group chunks: byte by byte */
         for (int b = 0; b < 16; ++b) {
             const uint64_t qa = ((cfirst + c) << 4) + (uint64_t)b;
             if (qa < o0 || qa >= o1) continue;
@@ -2797,27 +2777,6 @@ __global__ __launch_bounds__(DT) void k_dyn_gather(const DevStream *__restrict__
             }
             q[b] = v;
         }
-    };
-    uint32_t c = cbeg + (uint32_t)t;
-    Ck ck{};
-    Cd cd{};
-    if (c < cend) {
-        prep(c, ck);
-        if (ck.fast) fetch(ck, cd);
-    }
-    while (c < cend) {
-        const uint32_t cn = c + DT;
-        Ck nk{};
-        Cd nd{};
-        if (cn < cend) {
-            prep(cn, nk);
-            if (nk.fast) fetch(nk, nd);
-        }
-        if (ck.fast) assemble(c, ck, cd);
-        else bytewise(c, ck.K);
-        c = cn;
-        ck = nk;
-        cd = nd;
     }
 }
 

@@ -2027,7 +2027,10 @@ __device__ inline void splice_tail(SK &sk, const SpliceMbRec &h, const SpliceMbR
     }
 }
 
-__global__ __launch_bounds__(DT) void k_splice_stage(DevStream *__restrict__ st,
+#ifndef SCROLL_STAGE_WAVES
+#define SCROLL_STAGE_WAVES 1
+#endif
+__global__ __launch_bounds__(DT) __attribute__((amdgpu_waves_per_eu(SCROLL_STAGE_WAVES))) void k_splice_stage(DevStream *__restrict__ st,
                                                      const NalDesc *__restrict__ nal, int ld_nal,
                                                      const PlanPending *__restrict__ pend,
                                                      DynFrame *__restrict__ dfr, int ld_fr,

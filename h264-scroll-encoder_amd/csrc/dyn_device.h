@@ -10,7 +10,8 @@
  *  - prediction: full-pel luma, 1/8-pel bilinear chroma from the reference
  *    pictures A / B, a waypoint (long-term ref 2+k) resolved through its own
  *    row-uniform (ref, mv) (src/h264_writer.c:689-729), coordinates clamped;
- *  - 4x4 forward core transform, flat quantiser at QP 26, chroma DC 2x2
+ *  - 4x4 forward core transform, flat quantiser at the rect's QP (26 by
+ *    default; chroma at QPc), chroma DC 2x2
  *    Hadamard (dyn_oracle.c or_fwd4x4 / or_quant);
  *  - CAVLC residual blocks (H.264 9.2) into any bit sink;
  *  - the emulation-prevention rule in closed form (nal.c:33-38).
@@ -18,16 +19,34 @@
 #ifndef SCROLL_DYN_DEVICE_H
 #define SCROLL_DYN_DEVICE_H
 
+#include "qparams.h"
 #include "scroll_device.h"
 
 namespace scroll {
 namespace dyn {
 
-constexpr int QP = 26;               /* pic_init_qp 26, slice_qp_delta 0 (h264_writer.c:118-120) */
-constexpr int QBITS = 15 + QP / 6;   /* 19 */
-constexpr int QF = (1 << QBITS) / 6; /* rounding offset f = 2^qbits / 6 */
-/* MF for QP % 6 == 2: classes (even, even) / (odd, odd) / mixed */
-constexpr int MF0 = 10082, MF1 = 4194, MF2 = 6554;
+/* the rect's QP: 26 by default (pic_init_qp 26, slice_qp_delta 0,
+ * h264_writer.c:118-120); scroll_batch_set_dyn_qp picks another, written as
+ * the dynamic NAL's slice_qp_delta.  QP_MIN: the lowest whose levels fit the
+ * packed int8 form (|W| <= 9180: max level 127 at QP 22, 145 at 21) */
+constexpr int QP_DEFAULT = 26, QP_MIN = 22, QP_MAX = 51;
+/* MF by QP % 6 and position class (Table 8-x inverse, the forward scale) */
+__host__ __device__ constexpr int mf_of(int r, int cls)
+{
+    constexpr int T[6][3] = {{13107, 5243, 8066}, {11916, 4660, 7490}, {10082, 4194, 6554},
+                             {9362, 3647, 5825},  {8192, 3355, 5243},  {7282, 2893, 4559}};
+    return T[r][cls];
+}
+__host__ __device__ constexpr QParams qparams(int qp)
+{
+    return QParams{mf_of(qp % 6, 0), mf_of(qp % 6, 1), mf_of(qp % 6, 2), 15 + qp / 6, (1 << (15 + qp / 6)) / 6};
+}
+/* QPc of QP (Table 8-15, chroma_qp_index_offset 0 as the composer's PPS) */
+__host__ __device__ constexpr int qp_chroma(int qp)
+{
+    constexpr int T[22] = {29, 30, 31, 32, 32, 33, 34, 34, 35, 35, 36, 36, 37, 37, 37, 38, 38, 38, 39, 39, 39, 39};
+    return qp < 30 ? qp : T[qp - 30];
+}
 /* provable bound on the bits of one dynamic MB (codeword + residual):
  * 16 x 640 luma + 8 x 602 chroma AC + 2 x 130 chroma DC + cbp/qp + 64 < 16384 */
 constexpr int MB_BITS_MAX = 16384;
@@ -318,14 +337,14 @@ __device__ __host__ inline int mad_i24(int a, int b, int c)
  * one signed 24-bit multiply-add and an arithmetic shift: for w < 0 the
  * bias 2^qbits - 1 - f turns the floor into -((|w| mf + f) >> qbits)
  * (|w| <= 9180, mf < 2^14: the product fits 31 bits) */
-__device__ __host__ inline int quant(int w, int pos)
+__device__ __host__ inline int quant(int w, int pos, const QParams &q)
 {
     const int i = pos >> 2, j = pos & 3;
-    const int mf = ((i | j) & 1) == 0 ? MF0 : (((i & j) & 1) ? MF1 : MF2);
+    const int mf = ((i | j) & 1) == 0 ? q.mf0 : (((i & j) & 1) ? q.mf1 : q.mf2);
     /* bias by the sign mask as a bit select (v_bfi): no compare, no VCC */
     const uint32_t m = (uint32_t)(w >> 31);
-    const int bias = (int)((m & (uint32_t)((1 << QBITS) - 1 - QF)) | (~m & (uint32_t)QF));
-    return mad_i24(w, mf, bias) >> QBITS;
+    const int bias = (int)((m & (uint32_t)((1 << q.qbits) - 1 - q.qf)) | (~m & (uint32_t)q.qf));
+    return mad_i24(w, mf, bias) >> q.qbits;
 }
 
 /* ---------------------------------------------------------------------- */
@@ -492,7 +511,8 @@ __device__ __host__ inline int half(uint32_t x, int h) { return (int)(int16_t)(u
  * in scan order (chroma AC: the 15 from scan index 1, byte 15 zero), w0 =
  * W[0] (chroma DC, unquantised); the same values as fwd4x4 + quant of a - pr */
 template <bool LUMA>
-__device__ __host__ inline void levels_pk(const uint32_t a[4], const uint32_t pr[4], uint32_t pk4[4], int &w0)
+__device__ __host__ inline void levels_pk(const uint32_t a[4], const uint32_t pr[4], uint32_t pk4[4], int &w0,
+                                          const QParams &q)
 {
 #ifdef __HIP_DEVICE_COMPILE__
     typedef short s2 __attribute__((ext_vector_type(2)));
@@ -547,8 +567,8 @@ __device__ __host__ inline void levels_pk(const uint32_t a[4], const uint32_t pr
       [t4] "=&v"(t4), [t5] "=&v"(t5), [t6] "=&v"(t6), [t7] "=&v"(t7)                                     \
     : [ye0] "v"(ye[0]), [ye1] "v"(ye[1]), [ye2] "v"(ye[2]), [ye3] "v"(ye[3]), [yo0] "v"(yo[0]),          \
       [yo1] "v"(yo[1]), [yo2] "v"(yo[2]), [yo3] "v"(yo[3]),                                              \
-      [k1] "s"((uint32_t)((1 << QBITS) - 1 - QF)), [k0] "v"((uint32_t)QF), [sh] "v"(QBITS), [mf0] "s"(MF0), \
-      [mf1] "s"(MF1), [mf2] "s"(MF2)
+      [k1] "s"((uint32_t)((1 << q.qbits) - 1 - q.qf)), [k0] "v"((uint32_t)q.qf), [sh] "v"(q.qbits), [mf0] "s"(q.mf0), \
+      [mf1] "s"(q.mf1), [mf2] "s"(q.mf2)
     if constexpr (LUMA) {
         asm(SCROLL_QLUMA0 SCROLL_QOPS(pk4[0], pk4[1]));
         asm(SCROLL_QLUMA1 SCROLL_QOPS(pk4[2], pk4[3]));
@@ -585,13 +605,13 @@ __device__ __host__ inline void levels_pk(const uint32_t a[4], const uint32_t pr
     pk4[0] = pk4[1] = pk4[2] = pk4[3] = 0;
     for (int k2 = LUMA ? 0 : 1; k2 < 16; ++k2) {
         const int p = ZZ[k2], r = p >> 2, c = p & 3, o = LUMA ? k2 : k2 - 1;
-        const int mf = ((r | c) & 1) == 0 ? MF0 : (((r & c) & 1) ? MF1 : MF2);
+        const int mf = ((r | c) & 1) == 0 ? q.mf0 : (((r & c) & 1) ? q.mf1 : q.mf2);
         const uint32_t y = (c & 1) ? yo[r] : ye[r];
         const int w = half(y, c >> 1);
         const uint32_t sg = (uint32_t)(w >> 31);
-        const uint32_t bias = (sg & (uint32_t)((1 << QBITS) - 1 - QF)) | (~sg & (uint32_t)QF);
+        const uint32_t bias = (sg & (uint32_t)((1 << q.qbits) - 1 - q.qf)) | (~sg & (uint32_t)q.qf);
         const int v = w * mf + (int)bias;
-        pk4[o >> 2] |= ((uint32_t)(v >> QBITS) & 255u) << (8 * (o & 3));
+        pk4[o >> 2] |= ((uint32_t)(v >> q.qbits) & 255u) << (8 * (o & 3));
     }
 #endif
 }
@@ -615,11 +635,11 @@ __device__ __host__ inline uint32_t nz_mask16(uint4 pk)
     return nz_nibble(pk.x) | nz_nibble(pk.y) << 4 | nz_nibble(pk.z) << 8 | nz_nibble(pk.w) << 12;
 }
 
-/* chroma DC (2x2): qbits + 1, f doubled (|w| <= 16320) */
-__device__ __host__ inline int quant_dc(int w)
+/* chroma DC (2x2): qbits + 1, f doubled (|w| <= 16320; q: the chroma QP's) */
+__device__ __host__ inline int quant_dc(int w, const QParams &q)
 {
-    const int bias = w < 0 ? (1 << (QBITS + 1)) - 1 - 2 * QF : 2 * QF;
-    return mad_i24(w, MF0, bias) >> (QBITS + 1);
+    const int bias = w < 0 ? (1 << (q.qbits + 1)) - 1 - 2 * q.qf : 2 * q.qf;
+    return mad_i24(w, q.mf0, bias) >> (q.qbits + 1);
 }
 
 /* ---------------------------------------------------------------------- */

@@ -417,7 +417,7 @@ __device__ inline void code_frame(const DevStream *__restrict__ st,
         fwd4x4(res, W);
 #pragma unroll
         for (int k2 = 0; k2 < 16; ++k2) {
-            const int v = quant(W[ZZ[k2]], ZZ[k2]);          /* |v| <= 78: int8 */
+            const int v = quant(W[ZZ[k2]], ZZ[k2], g.ql);    /* |v| <= 127 (QP >= 22): int8 */
             pk[k2 >> 2] |= ((uint32_t)v & 255u) << (8 * (k2 & 3));
             n += v != 0;
         }
@@ -478,7 +478,7 @@ __device__ inline void code_frame(const DevStream *__restrict__ st,
         w0 = W[0];
 #pragma unroll
         for (int k2 = 1; k2 < 16; ++k2) {
-            const int v = quant(W[ZZ[k2]], ZZ[k2]);
+            const int v = quant(W[ZZ[k2]], ZZ[k2], g.qc);
             pk[(k2 - 1) >> 2] |= ((uint32_t)v & 255u) << (8 * ((k2 - 1) & 3));
             n += v != 0;
         }
@@ -493,10 +493,10 @@ __device__ inline void code_frame(const DevStream *__restrict__ st,
         const int d0 = __shfl(w0, qb, 64), d1 = __shfl(w0, qb + 1, 64);
         const int d2 = __shfl(w0, qb + 2, 64), d3 = __shfl(w0, qb + 3, 64);
         if (dc_lane) {
-            dq[0] = quant_dc(d0 + d1 + d2 + d3);
-            dq[1] = quant_dc(d0 - d1 + d2 - d3);
-            dq[2] = quant_dc(d0 + d1 - d2 - d3);
-            dq[3] = quant_dc(d0 - d1 - d2 + d3);
+            dq[0] = quant_dc(d0 + d1 + d2 + d3, g.qc);
+            dq[1] = quant_dc(d0 - d1 + d2 - d3, g.qc);
+            dq[2] = quant_dc(d0 + d1 - d2 - d3, g.qc);
+            dq[3] = quant_dc(d0 - d1 - d2 + d3, g.qc);
         }
     }
     /* encode order: by TotalCoeff, largest first (a counting sort over the
@@ -839,7 +839,8 @@ __global__ __launch_bounds__(GW) void k_dyn_static(const DevStream *__restrict__
     const DevStream *S = st + s;
     const NalDesc d = nal[(size_t)s * ld_nal + j];
     wave_sync();
-    const NalCtx c = nal_ctx(S, d, L.wo, L.wl, L.wv);
+    NalCtx c = nal_ctx(S, d, L.wo, L.wl, L.wv);
+    c.qpd = g.qp - QP_DEFAULT;                          /* the rect's QP: slice_qp_delta */
     const HeadCtx H = head_ctx(c);
     const int mbw = H.mbw, mbh = c.h / 16;
     int ra, rb;
@@ -1175,7 +1176,7 @@ __device__ inline uint32_t bilin4(uint32_t b, uint32_t c, uint32_t f)
 /* residual -> transform -> quant: pk = 16 int8 levels in scan order (AC: 15,
  * from scan index 1), n = TotalCoeff, w0 = chroma DC coefficient
  * (unquantised) */
-__device__ inline void row_levels(bool luma, const BlkPix &px, uint32_t pk[4], int &n, int &w0)
+__device__ inline void row_levels(bool luma, const BlkPix &px, uint32_t pk[4], int &n, int &w0, const DynGeom &g)
 {
     pk[0] = pk[1] = pk[2] = pk[3] = 0;
     n = 0;
@@ -1191,8 +1192,8 @@ __device__ inline void row_levels(bool luma, const BlkPix &px, uint32_t pk[4], i
         for (int i = 0; i < 4; ++i) pr[i] = bilin4(px.b[i], px.c[i], (px.fr >> (3 * i)) & 7u);
     }
     /* packed 16-bit pairs (dyn_device.h levels_pk) */
-    if (luma) levels_pk<true>(px.a, pr, pk, w0);
-    else levels_pk<false>(px.a, pr, pk, w0);
+    if (luma) levels_pk<true>(px.a, pr, pk, w0, g.ql);
+    else levels_pk<false>(px.a, pr, pk, w0, g.qc);
     n = nz_bytes(pk[0]) + nz_bytes(pk[1]) + nz_bytes(pk[2]) + nz_bytes(pk[3]);
 }
 
@@ -1315,7 +1316,7 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
             uint32_t pk[4];
             int n = 0, w0 = 0;
             if (task >= 0) {
-                row_levels(task < 16 * w, cur, pk, n, w0);
+                row_levels(task < 16 * w, cur, pk, n, w0, g);
                 const int slot = row_slot(task, w);
                 lv[slot] = make_uint4(pk[0], pk[1], pk[2], pk[3]);
                 mt[slot] = (uint16_t)((uint32_t)min(n, 16) << 8);
@@ -1331,8 +1332,8 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
             const int d2 = __shfl(w0, qb + 2, 64), d3 = __shfl(w0, qb + 3, 64);
             if (cdc && (task & 3) == 0) {
                 const int jj = task - 16 * w, k = jj >> 3, p = (jj >> 2) & 1;
-                const int q0 = quant_dc(d0 + d1 + d2 + d3), q1 = quant_dc(d0 - d1 + d2 - d3);
-                const int q2 = quant_dc(d0 + d1 - d2 - d3), q3 = quant_dc(d0 - d1 - d2 + d3);
+                const int q0 = quant_dc(d0 + d1 + d2 + d3, g.qc), q1 = quant_dc(d0 - d1 + d2 - d3, g.qc);
+                const int q2 = quant_dc(d0 + d1 - d2 - d3, g.qc), q3 = quant_dc(d0 - d1 - d2 + d3, g.qc);
                 lv[k * NPC + 16 + p] = make_uint4(((uint32_t)q0 & 0xffffu) | (uint32_t)q1 << 16,
                                                   ((uint32_t)q2 & 0xffffu) | (uint32_t)q3 << 16, 0u, 0u);
                 mt[k * NPC + 16 + p] = (uint16_t)((uint32_t)((q0 != 0) + (q1 != 0) + (q2 != 0) + (q3 != 0)) << 8);

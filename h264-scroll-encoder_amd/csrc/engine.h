@@ -9,6 +9,7 @@
 #include <stddef.h>
 #include <stdint.h>
 #include "composer_batch.h"
+#include "qparams.h"
 
 #ifdef __cplusplus
 extern "C" {
@@ -98,6 +99,8 @@ typedef struct {
 typedef struct {
     int32_t x0, y0, w, h;           /* rect, MB units                             */
     int32_t ngroups;                /* k_dyn_group row groups per NAL (dyn_groups) */
+    int32_t qp;                     /* the rect's QP (slice_qp_delta qp - 26)     */
+    QParams ql, qc;                 /* its luma / chroma (QPc) quantisers          */
     int32_t debug;                  /* SCROLL_DEBUG_DYN_* ablation bits           */
     uint64_t src_ld, src_fr;        /* source bytes per stream / per frame        */
     uint64_t ref_ld;                /* reference-pair bytes per stream (0 shared) */

@@ -42,6 +42,8 @@ using namespace scroll::hint;
 
 namespace {
 
+constexpr QParams HQ = qparams(QP_DEFAULT);   /* the rect under hints codes at QP 26 */
+
 __constant__ Tabs h_tabs = SCROLL_DYN_TABS;
 
 constexpr int HD_T = 64;                /* one wave per MB */
@@ -216,11 +218,11 @@ __global__ __launch_bounds__(HD_T) void k_hdyn_code(const DevStream *__restrict_
         }
         fwd4x4(res, Wc);
         if (t < 16) {
-            for (int k2 = 0; k2 < 16; ++k2) L.lev[t][k2] = quant(Wc[ZZ[k2]], ZZ[k2]);
+            for (int k2 = 0; k2 < 16; ++k2) L.lev[t][k2] = quant(Wc[ZZ[k2]], ZZ[k2], HQ);
         } else {
             const int p = (t - 16) >> 2, k = (t - 16) & 3, pc = 18 + 4 * p + k;
             L.wdc[p][k] = Wc[0];
-            for (int k2 = 1; k2 < 16; ++k2) L.lev[pc][k2 - 1] = quant(Wc[ZZ[k2]], ZZ[k2]);
+            for (int k2 = 1; k2 < 16; ++k2) L.lev[pc][k2 - 1] = quant(Wc[ZZ[k2]], ZZ[k2], HQ);
             L.lev[pc][15] = 0;
         }
     }
@@ -228,10 +230,10 @@ __global__ __launch_bounds__(HD_T) void k_hdyn_code(const DevStream *__restrict_
     if (t == 24 || t == 25) {                               /* chroma DC 2x2 Hadamard */
         const int p = t - 24;
         const int d0 = L.wdc[p][0], d1 = L.wdc[p][1], d2 = L.wdc[p][2], d3 = L.wdc[p][3];
-        L.lev[16 + p][0] = quant_dc(d0 + d1 + d2 + d3);
-        L.lev[16 + p][1] = quant_dc(d0 - d1 + d2 - d3);
-        L.lev[16 + p][2] = quant_dc(d0 + d1 - d2 - d3);
-        L.lev[16 + p][3] = quant_dc(d0 - d1 - d2 + d3);
+        L.lev[16 + p][0] = quant_dc(d0 + d1 + d2 + d3, HQ);
+        L.lev[16 + p][1] = quant_dc(d0 - d1 + d2 - d3, HQ);
+        L.lev[16 + p][2] = quant_dc(d0 + d1 - d2 - d3, HQ);
+        L.lev[16 + p][3] = quant_dc(d0 - d1 - d2 + d3, HQ);
     }
     lds_wave_sync();
 

@@ -72,6 +72,7 @@ struct NalCtx {
     int frame_num;                /* raw cfg->frame_num                           */
     int nwp;                      /* cfg->num_waypoints snapshot                  */
     const int32_t *wp_off, *wp_lt, *wp_valid;
+    int qpd = 0;                  /* slice_qp_delta (the dynamic rect's QP - 26)  */
 };
 
 /* ---------------------------------------------------------------------- */
@@ -244,7 +245,7 @@ __device__ inline void emit_slice_header(S &s, const NalCtx &c)
             put_ue(s, 0);
         }
     }
-    put_se(s, 0);                                    /* slice_qp_delta */
+    put_se(s, c.qpd);                                /* slice_qp_delta (0: h264_writer.c:486) */
     if (c.deblock) put_ue(s, 1);                     /* disable deblocking */
 }
 

@@ -28,6 +28,7 @@
 #include "ipcm_engine.h"
 #include "engine.h"
 #include "scroll_device.h"
+#include "dyn_device.h"
 
 using namespace scroll;
 
@@ -944,6 +945,7 @@ struct ScrollBatch {
      * (d_sp_rec, word pool d_sp_rbsp) and composed by k_splice_stage */
     std::vector<int32_t> h_dyn_pos;    /* [2 (s * max_frames + f)]: rect origin, x0 < 0: none */
     int dyn_pos_custom = 0;            /* some frame's origin differs from the batch rect */
+    int dyn_qp = 26;                   /* the rect's QP (scroll_batch_set_dyn_qp)          */
     int hd_dirty = 0;                  /* d_spf / HintFrame of the combined frames out of date */
     uint32_t hd_mb_words = 0;          /* pool words per rect MB */
     size_t dyn_cap = 0;                /* the dynamic rect's own staging cap (geo.slot_bytes without hints) */
@@ -1903,6 +1905,9 @@ int scroll_batch_set_dyn_rect(ScrollBatch *b, int x0, int y0, int w, int h, size
     g.y0 = y0;
     g.w = w;
     g.h = h;
+    g.qp = b->dyn_qp;
+    g.ql = scroll::dyn::qparams(g.qp);
+    g.qc = scroll::dyn::qparams(scroll::dyn::qp_chroma(g.qp));
     {
         const int sr = DYN_STATIC_ROWS;
         const int na = (y0 + sr - 1) / sr, nbl = (mbh - y0 - h + sr - 1) / sr;
@@ -2269,6 +2274,25 @@ static int hd_upload(ScrollBatch *b)
     return SCROLL_OK;
 }
 
+int scroll_batch_set_dyn_qp(ScrollBatch *b, int qp)
+{
+    if (!b || qp < SCROLL_DYN_QP_MIN || qp > SCROLL_DYN_QP_MAX) {
+        set_err("scroll_batch_set_dyn_qp: QP %d outside %d..%d", qp, SCROLL_DYN_QP_MIN, SCROLL_DYN_QP_MAX);
+        return SCROLL_ERR_ARG;
+    }
+    if (b->hint_on && qp != 26) {
+        set_err("scroll_batch_set_dyn_qp: the rect under UI hints codes at QP 26");
+        return SCROLL_ERR_CONFIG;
+    }
+    int rc = batch_host_sync(b);
+    if (rc) return rc;
+    b->dyn_qp = qp;
+    b->geo.qp = qp;                    /* kernels take the geometry by value at launch */
+    b->geo.ql = scroll::dyn::qparams(qp);
+    b->geo.qc = scroll::dyn::qparams(scroll::dyn::qp_chroma(qp));
+    return SCROLL_OK;
+}
+
 int scroll_batch_set_hints(ScrollBatch *b, int s, int f, const ScrollHintRect *rects, int n,
                            int mode)
 {
@@ -2287,6 +2311,10 @@ int scroll_batch_set_hints(ScrollBatch *b, int s, int f, const ScrollHintRect *r
                     r.ref, r.mv_x, r.mv_y);
             return SCROLL_ERR_ARG;
         }
+    }
+    if (!b->hint_on && b->dyn_qp != 26) {
+        set_err("scroll_batch_set_hints: the dynamic rect's QP is %d; under UI hints it codes at 26", b->dyn_qp);
+        return SCROLL_ERR_CONFIG;
     }
     int rc = batch_host_sync(b);
     if (rc) return rc;

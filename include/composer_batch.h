@@ -161,7 +161,8 @@ long long scroll_batch_last_nals(ScrollBatch *b);
 /* ---- dynamic rect (BASELINE configs 3-5; no reference counterpart) ----
  * Every scroll NAL of the batch carries a rectangle of dynamic MBs: they keep
  * their row's (ref_idx, mv) and add coded_block_pattern, mb_qp_delta and a
- * CAVLC residual of (source - prediction) at QP 26 (bit-exact definition:
+ * CAVLC residual of (source - prediction) at QP 26 or the rect's QP
+ * (scroll_batch_set_dyn_qp; bit-exact definition:
  * oracle/dyn_oracle.h).  Waypoint NALs stay residual-free.  All streams of
  * the batch must share one picture size; call after adding the streams.
  *
@@ -178,6 +179,16 @@ long long scroll_batch_last_nals(ScrollBatch *b);
  *       global stream ids stream_base + s and frame numbers t0 + f). */
 int scroll_batch_set_dyn_rect(ScrollBatch *b, int x0, int y0, int w, int h, size_t slot_bytes);
 int scroll_batch_set_dyn_refs(ScrollBatch *b, int s, const uint8_t *ref_a, const uint8_t *ref_b);
+/*   scroll_batch_set_dyn_qp(b, qp)   the rect's QP, 22..51 (default 26), for
+ *       the following composes: the dynamic scroll NALs then carry
+ *       slice_qp_delta = qp - 26 (chroma at QPc, Table 8-15) and their MBs
+ *       mb_qp_delta 0; waypoint NALs and the P-only path are unchanged.  Not
+ *       combinable with UI hints (their rect codes at 26): SCROLL_ERR_CONFIG.
+ *       Below 22 a level of a +-255 residual would not fit the coder's packed
+ *       8-bit levels (SCROLL_ERR_ARG). */
+#define SCROLL_DYN_QP_MIN 22
+#define SCROLL_DYN_QP_MAX 51
+int scroll_batch_set_dyn_qp(ScrollBatch *b, int qp);
 int scroll_batch_set_dyn_source(ScrollBatch *b, const uint8_t *src, int nframes);
 /* Under UI hints (scroll_batch_set_hints) the rect's MBs keep the hint
  * field's (ref, mv) -- full-pel luma, 2-D 1/8-pel chroma prediction at that

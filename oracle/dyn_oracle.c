@@ -143,6 +143,12 @@ void or_fwd4x4(const int x[16], int W[16])
     }
 }
 
+int or_qp_chroma(int qp)
+{
+    static const int T[22] = {29, 30, 31, 32, 32, 33, 34, 34, 35, 35, 36, 36, 37, 37, 37, 38, 38, 38, 39, 39, 39, 39};
+    return qp < 30 ? qp : T[qp - 30];
+}
+
 /* pos = raster position in the 4x4 block; dc_chroma: 2x2 chroma DC */
 int or_quant(int w, int qp, int pos, int dc_chroma)
 {
@@ -421,6 +427,7 @@ static void or_mb_levels(const or_cfg *c, const or_refs *R, const or_dyn_rect *r
     const int lw = 16 * rc->w, cw = 8 * rc->w;
     const uint8_t *sy = src, *su = src + (size_t)lw * 16 * rc->h, *sv = su + (size_t)cw * 8 * rc->h;
     const int lx0 = 16 * (mbx - rc->x0), ly0 = 16 * (mby - rc->y0);
+    const int qp = rc->qp ? rc->qp : OR_QP, qpc = or_qp_chroma(qp);
     for (int r = 0; r < 16; ++r) {
         const int bx = 4 * (r % 4), by = 4 * (r / 4);
         int res[16], W[16];
@@ -431,7 +438,7 @@ static void or_mb_levels(const or_cfg *c, const or_refs *R, const or_dyn_rect *r
                 res[4 * i + j] = sy[(size_t)(ly0 + by + i) * lw + lx0 + bx + j] - pred;
             }
         or_fwd4x4(res, W);
-        for (int k = 0; k < 16; ++k) luma[r][k] = or_quant(W[OR_ZZ[k]], OR_QP, OR_ZZ[k], 0);
+        for (int k = 0; k < 16; ++k) luma[r][k] = or_quant(W[OR_ZZ[k]], qp, OR_ZZ[k], 0);
     }
     const int cx0 = 8 * (mbx - rc->x0), cy0 = 8 * (mby - rc->y0);
     for (int p = 0; p < 2; ++p) {
@@ -451,14 +458,14 @@ static void or_mb_levels(const or_cfg *c, const or_refs *R, const or_dyn_rect *r
                 }
             or_fwd4x4(res, W);
             dc[k] = W[0];
-            for (int i = 1; i < 16; ++i) cac[p][k][i - 1] = or_quant(W[OR_ZZ[i]], OR_QP, OR_ZZ[i], 0);
+            for (int i = 1; i < 16; ++i) cac[p][k][i - 1] = or_quant(W[OR_ZZ[i]], qpc, OR_ZZ[i], 0);
         }
         const int f00 = dc[0] + dc[1] + dc[2] + dc[3], f01 = dc[0] - dc[1] + dc[2] - dc[3];
         const int f10 = dc[0] + dc[1] - dc[2] - dc[3], f11 = dc[0] - dc[1] - dc[2] + dc[3];
-        cdc[p][0] = or_quant(f00, OR_QP, 0, 1);
-        cdc[p][1] = or_quant(f01, OR_QP, 0, 1);
-        cdc[p][2] = or_quant(f10, OR_QP, 0, 1);
-        cdc[p][3] = or_quant(f11, OR_QP, 0, 1);
+        cdc[p][0] = or_quant(f00, qpc, 0, 1);
+        cdc[p][1] = or_quant(f01, qpc, 0, 1);
+        cdc[p][2] = or_quant(f10, qpc, 0, 1);
+        cdc[p][3] = or_quant(f11, qpc, 0, 1);
     }
 }
 
@@ -532,7 +539,7 @@ size_t or_scroll_nal_dyn(uint8_t *dst, size_t cap, or_cfg *c, int off, const or_
     uint8_t *rbsp = tl_rbsp;
     or_bits b;
     or_bits_init(&b, rbsp, rcap);
-    or_scroll_header(&b, c);                               /* :549-553 */
+    or_scroll_header_qpd(&b, c, rc->qp ? rc->qp - OR_QP : 0);   /* :549-553; the rect's QP */
 
     /* regions (:555-588) */
     int a_end = (c->h - off) / 16, wa = -1, woa = 0, wb = -1, wob = 0;

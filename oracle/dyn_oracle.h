@@ -51,6 +51,8 @@ extern "C" {
 
 typedef struct or_dyn_rect_s {
     int x0, y0, w, h;             /* MB units */
+    int qp;                       /* the rect's QP, 0 = 26 (slice_qp_delta qp - 26;
+                                   * chroma at QPc, Table 8-15); or_scroll_nal_dyn only */
 } or_dyn_rect;
 
 typedef struct {
@@ -87,6 +89,7 @@ int or_cbp_code(int cbp);
 /* forward 4x4 core transform + quantisation of a residual block (raster) */
 void or_fwd4x4(const int res[16], int W[16]);
 int or_quant(int w, int qp, int pos, int dc_chroma);
+int or_qp_chroma(int qp);                 /* QPc (Table 8-15, chroma_qp_index_offset 0) */
 
 /* scroll P NAL with the dynamic rect (src per or_dyn_source); r == NULL or
  * an empty rect gives exactly or_scroll_nal */

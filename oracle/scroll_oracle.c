@@ -140,7 +140,7 @@ static void or_frame_poc(or_bits *b, const or_cfg *c, int fn)
 }
 
 /* :455-488 -- two long-term refs, no waypoints */
-static void or_hdr_plain(or_bits *b, const or_cfg *c, int fn, int is_ref)
+static void or_hdr_plain(or_bits *b, const or_cfg *c, int fn, int is_ref, int qpd)
 {
     or_ue(b, 0);
     or_ue(b, 0);           /* SLICE_TYPE_P */
@@ -154,13 +154,13 @@ static void or_hdr_plain(or_bits *b, const or_cfg *c, int fn, int is_ref)
     or_ue(b, 3);
     if (is_ref)
         or_bit(b, 0);
-    or_se(b, 0);
+    or_se(b, qpd);         /* slice_qp_delta (0; the dynamic rect's QP - 26) */
     if (c->deblock)
         or_ue(b, 1);
 }
 
 /* :490-539 -- waypoint-aware list, optional MMCO marking */
-static void or_hdr_wp(or_bits *b, const or_cfg *c, int fn, int is_ref, int lt_idx)
+static void or_hdr_wp(or_bits *b, const or_cfg *c, int fn, int is_ref, int lt_idx, int qpd)
 {
     or_ue(b, 0);
     or_ue(b, 0);
@@ -187,7 +187,7 @@ static void or_hdr_wp(or_bits *b, const or_cfg *c, int fn, int is_ref, int lt_id
             or_bit(b, 0);
         }
     }
-    or_se(b, 0);
+    or_se(b, qpd);         /* slice_qp_delta (0; the dynamic rect's QP - 26) */
     if (c->deblock)
         or_ue(b, 1);
 }
@@ -288,15 +288,18 @@ static void or_mb_loop(or_bits *b, const or_cfg *c, int a_end,
     free(cur);
 }
 
-/* slice header of a scroll (non-reference) P frame, :549-553 */
-void or_scroll_header(or_bits *b, const or_cfg *c)
+/* slice header of a scroll (non-reference) P frame, :549-553 (slice_qp_delta
+ * qpd: 0 as the reference writes it; a dynamic rect's QP - 26) */
+void or_scroll_header_qpd(or_bits *b, const or_cfg *c, int qpd)
 {
     int fn = c->frame_num % (1 << c->log2_mfn);
     if (c->nwp > 0)
-        or_hdr_wp(b, c, fn, 0, -1);
+        or_hdr_wp(b, c, fn, 0, -1, qpd);
     else
-        or_hdr_plain(b, c, fn, 0);
+        or_hdr_plain(b, c, fn, 0, qpd);
 }
+
+void or_scroll_header(or_bits *b, const or_cfg *c) { or_scroll_header_qpd(b, c, 0); }
 
 /* :541-664 */
 size_t or_scroll_nal(uint8_t *dst, size_t cap, or_cfg *c, int off)
@@ -307,9 +310,9 @@ size_t or_scroll_nal(uint8_t *dst, size_t cap, or_cfg *c, int off)
     or_bits_init(&b, rbsp, rcap);
     int fn = c->frame_num % (1 << c->log2_mfn);
     if (c->nwp > 0)
-        or_hdr_wp(&b, c, fn, 0, -1);
+        or_hdr_wp(&b, c, fn, 0, -1, 0);
     else
-        or_hdr_plain(&b, c, fn, 0);
+        or_hdr_plain(&b, c, fn, 0, 0);
 
     int a_end, ra, mva, rb, mvb;
     or_scroll_regions(c, off, &a_end, &ra, &mva, &rb, &mvb);
@@ -375,7 +378,7 @@ size_t or_waypoint_nal(uint8_t *dst, size_t cap, or_cfg *c, int off)
     or_bits_init(&b, rbsp, rcap);
     int fn = c->frame_num % (1 << c->log2_mfn);
     int lt = 2 + c->nwp;
-    or_hdr_wp(&b, c, fn, 1, lt);
+    or_hdr_wp(&b, c, fn, 1, lt, 0);
     int a_end = (c->h - off) / 16;
     int wa = -1, woa = 0;
     if (off > OR_MV_LIMIT) {

@@ -60,6 +60,7 @@ void or_trailing(or_bits *b);                    /* :103-111 */
 size_t or_bytes(or_bits *b);                     /* bitwriter_get_size :124-131 */
 /* slice header of a scroll P frame (src/h264_writer.c:549-553) */
 void or_scroll_header(or_bits *b, const or_cfg *c);
+void or_scroll_header_qpd(or_bits *b, const or_cfg *c, int qpd);   /* slice_qp_delta qpd */
 
 /* ---- NAL framing restatement (src/nal.c) ---- */
 size_t or_rbsp_to_ebsp(uint8_t *dst, size_t cap, const uint8_t *src, size_t n); /* :24-50 */

@@ -10,7 +10,7 @@ class OrCfg(ctypes.Structure):
 
 
 class Rect(ctypes.Structure):
-    _fields_ = [(n, ctypes.c_int) for n in ("x0", "y0", "w", "h")]
+    _fields_ = [(n, ctypes.c_int) for n in ("x0", "y0", "w", "h", "qp")]   # qp 0 = 26
 
 
 class Pic(ctypes.Structure):

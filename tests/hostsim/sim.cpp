@@ -216,6 +216,7 @@ long sim_stream(int w, int h, int l2f, int poct, int l2p, int dbf, int n, const 
 
 /* ---- dynamic-rect device functions (dyn_device.h) ---------------------- */
 static const dyn::Tabs g_dyn_tabs = SCROLL_DYN_TABS;
+static constexpr QParams Q26 = dyn::qparams(dyn::QP_DEFAULT);   /* the oracle checks run at QP 26 */
 
 struct HostOr {
     uint32_t *b;
@@ -270,10 +271,10 @@ void sim_fwd_quant(const int *res, int *lv)
 {
     int W[16];
     dyn::fwd4x4(res, W);
-    for (int k = 0; k < 16; ++k) lv[k] = dyn::quant(W[k], k);
+    for (int k = 0; k < 16; ++k) lv[k] = dyn::quant(W[k], k, Q26);
 }
 
-int sim_quant_dc(int w) { return dyn::quant_dc(w); }
+int sim_quant_dc(int w) { return dyn::quant_dc(w, Q26); }
 
 int sim_ep_count(const uint8_t *b, int n)
 {
@@ -400,13 +401,13 @@ long sim_levels_pk(long n, unsigned seed)
             dyn::fwd4x4(res, W);
             uint32_t want[4] = {0, 0, 0, 0};
             for (int k2 = luma ? 0 : 1; k2 < 16; ++k2) {
-                const int v = dyn::quant(W[dyn::ZZ[k2]], dyn::ZZ[k2]), o = luma ? k2 : k2 - 1;
+                const int v = dyn::quant(W[dyn::ZZ[k2]], dyn::ZZ[k2], Q26), o = luma ? k2 : k2 - 1;
                 want[o >> 2] |= ((uint32_t)v & 255u) << (8 * (o & 3));
             }
             uint32_t got[4] = {0x5a5a5a5au, 0x5a5a5a5au, 0x5a5a5a5au, 0x5a5a5a5au};
             int w0 = 0;
-            if (luma) dyn::levels_pk<true>(a, p, got, w0);
-            else dyn::levels_pk<false>(a, p, got, w0);
+            if (luma) dyn::levels_pk<true>(a, p, got, w0, Q26);
+            else dyn::levels_pk<false>(a, p, got, w0, Q26);
             if (std::memcmp(want, got, sizeof want) != 0 || w0 != W[0]) return 1 + it;
         }
     }

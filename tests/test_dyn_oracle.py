@@ -219,3 +219,74 @@ def test_cavlc_values_pinned_by_reference_decoder(oracle):
         assert live == mine
     # level_prefix 14 at suffixLength 0, prefix 15 at 0 and at > 0 all occur
     assert min(esc) > 1000, esc
+
+
+# Table 8-15 (chroma_qp_index_offset 0): QPc for QP 30..51
+_QPC = [29, 30, 31, 32, 32, 33, 34, 34, 35, 35, 36, 36, 37, 37, 37, 38, 38, 38, 39, 39, 39, 39]
+
+
+def test_dyn_rect_qp_decodes(oracle):
+    """scroll_batch_set_dyn_qp's bits (or_dyn_rect.qp): the dynamic NAL's
+    slice_qp_delta is qp - 26 and its MBs decode -- luma at qp, chroma at QPc
+    -- to the source within what the quantiser step allows (PSNR falls as
+    QP rises); waypoint NALs and the rect-free path are unchanged"""
+    lib = oracle
+    w, h = 96, 96
+    R = StripedRefs(lib, w, h)
+    buf = (ctypes.c_uint8 * (1 << 21))()
+    psnrs = []
+    for qp in (22, 26, 30, 39, 51):
+        rc = Rect(1, 1, 4, 4, qp)
+        cfg = OrCfg()
+        lib.or_cfg_init(ctypes.byref(cfg), w, h)
+        cfg.frame_num = 2
+        rec, org = [], []
+        for t, off in enumerate([0, 5, 40, 96]):
+            src = rect_source(lib, 3, t, rc)
+            state = OrCfg.from_buffer_copy(cfg)
+            n = lib.or_compose_dyn(buf, len(buf), ctypes.byref(cfg), off, 0, ctypes.byref(rc), src,
+                                   ctypes.byref(R.refs), None)
+            scroll = split_nals(bytes(buf[:n]))[-1]
+            a_end, ra, mva, rb, mvb = _regions(state, off)
+            got = {}
+
+            def on_mb(x, y, ref, mvd, cbp, luma, cdc, cac):
+                if rc.x0 <= x < rc.x0 + rc.w and rc.y0 <= y < rc.y0 + rc.h:
+                    got[(x, y)] = (luma, cdc, cac)
+
+            H, nmb = hp.parse_p_slice(scroll, w, h, on_mb=on_mb)
+            assert H["qp_delta"] == qp - 26 and nmb == (w // 16) * (h // 16)
+            qpc = qp if qp < 30 else _QPC[qp - 30]
+            lw, cw = 16 * rc.w, 8 * rc.w
+            for (x, y), (luma, cdc, cac) in got.items():
+                mv = mva if y < a_end else mvb
+                ref = ra if y < a_end else rb
+                py, pu, pv = _pred(lib, state, R, ref, mv, x, y)
+                ry, ru, rv = hp.reconstruct_mb(luma, cdc, cac, py, pu, pv, qp=qp, qpc=qpc)
+                lx, ly = 16 * (x - rc.x0), 16 * (y - rc.y0)
+                for i in range(16):
+                    for j in range(16):
+                        rec.append(ry[i][j])
+                        org.append(src[(ly + i) * lw + lx + j])
+                cbase = lw * 16 * rc.h
+                for p, rr in enumerate((ru, rv)):
+                    base = cbase + p * cw * 8 * rc.h
+                    for i in range(8):
+                        for j in range(8):
+                            rec.append(rr[i][j])
+                            org.append(src[base + (8 * (y - rc.y0) + i) * cw + 8 * (x - rc.x0) + j])
+            assert len(got) == rc.w * rc.h
+        psnrs.append(_psnr(rec, org))
+    assert psnrs[0] > 38.0 and psnrs[1] > 34.0, psnrs
+    assert all(a > b for a, b in zip(psnrs, psnrs[1:])), psnrs
+    # qp 26 written out is the default's bytes
+    c1, c2 = OrCfg(), OrCfg()
+    lib.or_cfg_init(ctypes.byref(c1), w, h)
+    lib.or_cfg_init(ctypes.byref(c2), w, h)
+    b2 = (ctypes.c_uint8 * (1 << 20))()
+    src = rect_source(lib, 3, 0, Rect(1, 1, 4, 4))
+    n1 = lib.or_compose_dyn(buf, len(buf), ctypes.byref(c1), 40, 0, ctypes.byref(Rect(1, 1, 4, 4)), src,
+                            ctypes.byref(R.refs), None)
+    n2 = lib.or_compose_dyn(b2, len(b2), ctypes.byref(c2), 40, 0, ctypes.byref(Rect(1, 1, 4, 4, 26)), src,
+                            ctypes.byref(R.refs), None)
+    assert bytes(buf[:n1]) == bytes(b2[:n2])

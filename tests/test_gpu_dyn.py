@@ -102,6 +102,8 @@ def gpu_streams(gpu, w, h, offsets, rect, R, src=None, synth=False, mode=0, chun
     for _ in range(S):
         b.add_stream(gpu.make_config(w, h, waypoints=waypoints))
     b.set_dyn_rect(rect.x0, rect.y0, rect.w, rect.h, slot)
+    if rect.qp:
+        b.set_dyn_qp(rect.qp)
     if shared_refs:
         b.set_dyn_refs(R.i420(0), R.i420(1))
     for s, Rs in (per_stream_refs or {}).items():
@@ -401,3 +403,39 @@ def test_dyn_round3_gather_still_exact(gpu, oracle, geom):
     b, rc = gpu_streams(gpu, w, h, offs, rect, R, src, debug=gpu.SCROLL_DEBUG_DYN_GATHER1)
     assert rc == 0, gpu.last_error()
     check_equal(b, want)
+
+
+@pytest.mark.parametrize("qp", [22, 30, 37, 51])
+def test_dyn_rect_qp(gpu, oracle, scroll, qp):
+    """scroll_batch_set_dyn_qp: luma at qp, chroma at QPc, slice_qp_delta qp -
+    26 in the dynamic NALs (waypoints on the way stay the reference's), at
+    the config-3 geometry with random references (the largest levels) and
+    through the general path's half-pel chroma waypoints"""
+    w, h = 1280, 720
+    rect = Rect(28, 10, 25, 25, qp)
+    S, F = 2, 8
+    offs = synthetic_offsets(S, F, h, first_stream=3)
+    offs[1] = np.arange(490, 498)
+    R = random_refs(w, h, 7 + qp)
+    src = synth_source(oracle, S, F, rect)
+    want = oracle_streams(oracle, w, h, offs, rect, src, R)
+    b, rc = gpu_streams(gpu, w, h, offs, rect, R, src)
+    assert rc == 0, gpu.last_error()
+    check_equal(b, want)
+    with pytest.raises(Exception):
+        b.set_dyn_qp(21)
+    b.close()
+
+
+def test_dyn_qp_not_with_hints(gpu, scroll):
+    b = gpu.Batch(1, 2, 1 << 20)
+    b.add_stream(gpu.make_config(320, 320))
+    b.set_dyn_rect(1, 1, 2, 2)
+    b.set_dyn_qp(30)
+    with pytest.raises(Exception):
+        b.set_hints(0, 0, [], 1)
+    b.set_dyn_qp(26)
+    b.set_hints(0, 0, [], 1)
+    with pytest.raises(Exception):
+        b.set_dyn_qp(30)
+    b.close()

@@ -2213,6 +2213,14 @@ __device__ inline void ep_fix(DevStream *st, DynFrame *DF, size_t nb, int s, con
         }
         return;
     }
+#ifdef SCROLL_EPF_NOSORT_TIMING                              /* timing variant only: wrong bytes */
+    if (t == 0) {
+        DF->err = DF_FIXED;
+        DF->rbsp_bytes = nin;
+        DF->ep = 0;
+    }
+    return;
+#endif
     /* each position once, in increasing order (k_dyn_emit_gather needs no
      * sort): a repeat is flagged in bit 31, then each first occurrence
      * goes to its rank among the first occurrences */

@@ -40,9 +40,13 @@ int dyn_launch_code(hipStream_t hs, int nframes, int S, DevStream *st, const Nal
 /* k_dyn_static (static row groups) + k_dyn_epfix (+ k_dyn_epscan for the
  * NALs it flags): RBSP sizes and sorted EP positions (eps: DYN_OVF_BYTES per
  * frame) straight from the row groups */
+/* k_dyn_static alone (the static row groups: header, rows above / below the
+ * rect): it needs only the state pass, so it can run beside dyn_launch_code */
+int dyn_launch_static(hipStream_t hs, int nframes, int S, DevStream *st, const NalDesc *nal, int ld_nal,
+                      const PlanPending *pend, DynFrame *dfr, int ld_fr, const DynGeom *g, const DynScratch *x);
 int dyn_launch_pack(hipStream_t hs, int nframes, int S, DevStream *st, const NalDesc *nal,
                     int ld_nal, const PlanPending *pend, DynFrame *dfr, int ld_fr,
-                    const DynGeom *g, const DynScratch *x, uint8_t *eps, uint64_t *stamps);
+                    const DynGeom *g, const DynScratch *x, uint8_t *eps, uint64_t *stamps, bool with_static = true);
 /* k_dyn_emit_gather + k_dyn_emit: x != NULL -- the dynamic rect (RBSP from
  * the row groups, EP lists in stage = eps); x == NULL -- the staged RBSP of
  * the hint / splice path (slot_bytes per frame, EP list in the slot tail) */

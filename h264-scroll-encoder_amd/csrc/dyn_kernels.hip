@@ -2874,15 +2874,22 @@ int dyn_launch_code(hipStream_t hs, int nframes, int S, DevStream *st, const Nal
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-int dyn_launch_pack(hipStream_t hs, int nframes, int S, DevStream *st, const NalDesc *nal,
-                    int ld_nal, const PlanPending *pend, DynFrame *dfr, int ld_fr,
-                    const DynGeom *g, const DynScratch *x, uint8_t *eps, uint64_t *stamps)
+int dyn_launch_static(hipStream_t hs, int nframes, int S, DevStream *st, const NalDesc *nal, int ld_nal,
+                      const PlanPending *pend, DynFrame *dfr, int ld_fr, const DynGeom *g, const DynScratch *x)
 {
-    (void)stamps;
     if (nframes <= 0 || S <= 0) return 0;
     hipLaunchKernelGGL(k_dyn_static, dim3(g->ngroups - g->h, nframes, S), dim3(GW), 0, hs, st, nal, ld_nal,
                        pend, dfr, ld_fr, *g, x->rowstage, x->gbits);
-    if (hipGetLastError() != hipSuccess) return -1;
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int dyn_launch_pack(hipStream_t hs, int nframes, int S, DevStream *st, const NalDesc *nal,
+                    int ld_nal, const PlanPending *pend, DynFrame *dfr, int ld_fr,
+                    const DynGeom *g, const DynScratch *x, uint8_t *eps, uint64_t *stamps, bool with_static)
+{
+    (void)stamps;
+    if (nframes <= 0 || S <= 0) return 0;
+    if (with_static && dyn_launch_static(hs, nframes, S, st, nal, ld_nal, pend, dfr, ld_fr, g, x)) return -1;
     uint32_t *slow_n = x->ctr + DYN_CTR_SLOW, *slow = x->ctr + DYN_CTR_LIST + x->ctr_frames;
     hipLaunchKernelGGL(k_dyn_epfix, dim3(nframes, S), dim3(EPF_T), 0, hs, st, dfr, ld_fr, nframes, *g,
                        x->rowstage, x->gbits, eps, slow_n, slow);

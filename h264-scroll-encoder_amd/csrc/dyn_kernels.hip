@@ -1098,6 +1098,7 @@ __host__ __device__ constexpr uint32_t pc_desc(int pc)
 struct EpfLds {
     uint32_t *goff, *gb, *gw, *cw, *cbase, *lst, *cnt;    /* goff / cbase 65, gb / gw / cw 64, cnt 4 */
     uint32_t lcap;
+    uint32_t *ws;                                          /* per wave: the unique-position scan */
 };
 /* threads of a k_dyn_row workgroup: one block task each (two past 1024) */
 __host__ __device__ inline int row_threads(int w)
@@ -2213,33 +2214,48 @@ __device__ inline void ep_fix(DevStream *st, DynFrame *DF, size_t nb, int s, con
         }
         return;
     }
-#ifdef SCROLL_EPF_NOSORT_TIMING                              /* timing variant only: wrong bytes */
-    if (t == 0) {
-        DF->err = DF_FIXED;
-        DF->rbsp_bytes = nin;
-        DF->ep = 0;
-    }
-    return;
-#endif
     /* each position once, in increasing order (k_dyn_emit_gather needs no
-     * sort): a repeat is flagged in bit 31, then each first occurrence
-     * goes to its rank among the first occurrences */
-    for (uint32_t i = (uint32_t)t; i < n; i += (uint32_t)NT) {
-        const uint32_t v = lst[i] & 0x7fffffffu;
-        bool dup = false;
-        for (uint32_t j = 0; j < i; ++j) dup |= (lst[j] & 0x7fffffffu) == v;
-        if (dup) atomicOr(&lst[i], 0x80000000u);
-    }
+     * sort): a bitonic sort of the list padded to a power of two (log^2
+     * steps, one compare-exchange per thread and step -- the rank-by-count
+     * form it replaces was n^2 / NT and cost 0.07 ms per launch), then the
+     * first of each run of equal positions goes to its rank: a scan of the
+     * threads' contiguous chunks */
+    const uint32_t P = n <= 1u ? 1u : 1u << (32 - __builtin_clz(n - 1u));   /* <= lcap (n <= lcap) */
+    for (uint32_t i = (uint32_t)t + n; i < P; i += (uint32_t)NT) lst[i] = 0xffffffffu;
     sync();
-    uint32_t *eplist = reinterpret_cast<uint32_t *>(eps + nb * DYN_OVF_BYTES);
-    for (uint32_t i = (uint32_t)t; i < n; i += (uint32_t)NT) {
-        const uint32_t v = lst[i];
-        if (v & 0x80000000u) continue;
-        uint32_t r = 0;
-        for (uint32_t j = 0; j < n; ++j) r += lst[j] < v ? 1u : 0u;     /* repeats (bit 31) never count */
-        if (r < (uint32_t)EPLIST_MAX) eplist[r] = v;
-        atomicAdd(&nu, 1u);
+    for (uint32_t k = 2; k <= P; k <<= 1)
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            for (uint32_t i = (uint32_t)t; i < P; i += (uint32_t)NT) {
+                const uint32_t l = i ^ j;
+                if (l > i) {
+                    const uint32_t a = lst[i], b = lst[l];
+                    if ((a > b) == ((i & k) == 0u)) {
+                        lst[i] = b;
+                        lst[l] = a;
+                    }
+                }
+            }
+            sync();
+        }
+    const uint32_t C = (n + (uint32_t)NT - 1u) / (uint32_t)NT, c0 = (uint32_t)t * C, c1 = min(c0 + C, n);
+    uint32_t mine = 0;
+    for (uint32_t i = c0; i < c1; ++i) mine += (i == 0u || lst[i] != lst[i - 1u]) ? 1u : 0u;
+    uint32_t ex = 0;
+    {
+        const int lane = t & 63, wv = t >> 6;
+        const uint32_t incl = wave_incl_sum(mine, lane);
+        if (lane == 63) E.ws[wv] = incl;
+        sync();
+        for (int q = 0; q < wv; ++q) ex += E.ws[q];
+        ex += incl - mine;
+        if (t == NT - 1) nu = ex + mine;
     }
+    uint32_t *eplist = reinterpret_cast<uint32_t *>(eps + nb * DYN_OVF_BYTES);
+    for (uint32_t i = c0; i < c1; ++i)
+        if (i == 0u || lst[i] != lst[i - 1u]) {
+            if (ex < (uint32_t)EPLIST_MAX) eplist[ex] = lst[i];
+            ++ex;
+        }
     sync();
     if (t == 0) {
         DF->err = DF_FIXED;                             /* clears DF_GENERAL */
@@ -2261,13 +2277,13 @@ __global__ __launch_bounds__(EPF_T) void k_dyn_epfix(DevStream *__restrict__ st,
     __shared__ uint32_t goff[65], gb[64], gw[64], cw[64];
     __shared__ uint32_t cbase[65];                      /* runs before group g */
     __shared__ uint32_t lst[EPF_LIST];
-    __shared__ uint32_t cnt[4];
+    __shared__ uint32_t cnt[4], ws[EPF_T / 64];
     const int f = blockIdx.x, s = blockIdx.y, t = threadIdx.x;
     if (f >= nframes) return;
     const size_t nb = (size_t)s * ld_fr + f;
     DynFrame *DF = dfr + nb;
     if (DF->nal < 0) return;
-    const EpfLds E{goff, gb, gw, cw, cbase, lst, cnt, (uint32_t)EPF_LIST};
+    const EpfLds E{goff, gb, gw, cw, cbase, lst, cnt, (uint32_t)EPF_LIST, ws};
     ep_fix<EPF_T>(st, DF, nb, s, g, rowstage, gbits, eps, E, t, slow_n, slow);
 }
 

@@ -41,12 +41,13 @@ int dyn_launch_code(hipStream_t hs, int nframes, int S, DevStream *st, const Nal
  * NALs it flags): RBSP sizes and sorted EP positions (eps: DYN_OVF_BYTES per
  * frame) straight from the row groups */
 /* k_dyn_static alone (the static row groups: header, rows above / below the
- * rect): it needs only the state pass, so it can run beside dyn_launch_code */
+ * rect).  (Measured in round 4: on a second HIP stream beside the block
+ * coder, 1.69 against 1.67 ms per step -- no gain) */
 int dyn_launch_static(hipStream_t hs, int nframes, int S, DevStream *st, const NalDesc *nal, int ld_nal,
                       const PlanPending *pend, DynFrame *dfr, int ld_fr, const DynGeom *g, const DynScratch *x);
 int dyn_launch_pack(hipStream_t hs, int nframes, int S, DevStream *st, const NalDesc *nal,
                     int ld_nal, const PlanPending *pend, DynFrame *dfr, int ld_fr,
-                    const DynGeom *g, const DynScratch *x, uint8_t *eps, uint64_t *stamps, bool with_static = true);
+                    const DynGeom *g, const DynScratch *x, uint8_t *eps, uint64_t *stamps);
 /* k_dyn_emit_gather + k_dyn_emit: x != NULL -- the dynamic rect (RBSP from
  * the row groups, EP lists in stage = eps); x == NULL -- the staged RBSP of
  * the hint / splice path (slot_bytes per frame, EP list in the slot tail) */

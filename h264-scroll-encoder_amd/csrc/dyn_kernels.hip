@@ -1093,11 +1093,10 @@ __host__ __device__ constexpr uint32_t pc_desc(int pc)
            (uint32_t)e << 14;
 }
 
-/* LDS of ep_fix: the row-group table, candidate bases, the position list
- * (capacity lcap) and four counters */
+/* LDS of ep_fix: the row-group table, candidate bases, the position
+ * bitmap / list (ep_fix's LCAP words) and four counters */
 struct EpfLds {
     uint32_t *goff, *gb, *gw, *cw, *cbase, *lst, *cnt;    /* goff / cbase 65, gb / gw / cw 64, cnt 4 */
-    uint32_t lcap;
     uint32_t *ws;                                          /* per wave: the unique-position scan */
 };
 /* threads of a k_dyn_row workgroup: one block task each (two past 1024) */
@@ -1750,45 +1749,50 @@ __device__ inline void scan_load(ScanLoads &L, uint32_t c0, int t, int ng, uint3
 
 /* the row-group table of NAL nb in LDS (wave 0): goff = bit offsets (goff[ng]
  * = RBSP bits incl. the stop bit), gb = bit counts, gw = first row-stage
- * words in the frame's region */
+ * words in the frame's region, cw = the groups' EP-candidate records.
+ * count (k_dyn_epfix): lane t's group's candidate count, read with the
+ * table (the record word is the count unless it names a spill slot) */
 __device__ inline void rs_table(const uint32_t *gbits, size_t nb, const DynGeom &g, const uint32_t *fr,
                                 uint32_t *goff, uint32_t *gb, uint32_t *gw, uint32_t *cw, int t,
-                                uint32_t *bad = nullptr)
+                                uint32_t *bad = nullptr, uint32_t *count = nullptr)
 {
     const int ng = g.ngroups;
     constexpr int SR = DYN_STATIC_ROWS;
     const int nA = max(1, (g.y0 + SR - 1) / SR);
     if (t < 64) {
+        const bool row = t >= nA && t < nA + g.h;
+        uint32_t w = (uint32_t)rs_group_words(g, nA, t), c = (uint32_t)rs_runs_words(g, nA, t);
+        /* both loads in flight together */
         const uint32_t b = t < ng ? gbits[nb * (size_t)ng + t] : 0u;
+        uint32_t m = t < ng && (row || count) ? fr[c] : 0u;
         const uint32_t incl = wave_incl_sum(b, t);
         if (t < ng) {
             gb[t] = b;
             goff[t] = incl - b;
             /* a rect row that outgrew its slot: its record word names the
              * spill slot (relative to fr) holding its bits and record */
-            uint32_t w = (uint32_t)rs_group_words(g, nA, t), c = (uint32_t)rs_runs_words(g, nA, t);
-            if (t >= nA && t < nA + g.h) {
-                const uint32_t m = fr[c];
-                if (m & 0x80000000u) {
-                    /* bounds check of the spill slot the record names: slot k
-                     * of the pool after the rs_frames frame regions, k <
-                     * rs_spill_cap (k_dyn_row's claim is bounded the same
-                     * way).  A record outside the pool is never followed: the
-                     * group reads its own slot and the frame is flagged bad */
-                    const uint64_t base = ((uint64_t)g.rs_frames - nb) * g.rs_frame_words;
-                    const uint64_t rel = (uint64_t)(m & 0x7fffffffu) - base;
-                    if ((m & 0x7fffffffu) >= base && rel % g.rs_spill_words == 0 &&
-                        rel / g.rs_spill_words < g.rs_spill_cap) {
-                        w = m & 0x7fffffffu;
-                        c = w + g.rs_spill_words - EPC_ROW;
-                    } else if (bad) {
-                        *bad = 1u;
-                    }
+            if (row && (m & 0x80000000u)) {
+                /* bounds check of the spill slot the record names: slot k
+                 * of the pool after the rs_frames frame regions, k <
+                 * rs_spill_cap (k_dyn_row's claim is bounded the same
+                 * way).  A record outside the pool is never followed: the
+                 * group reads its own slot and the frame is flagged bad */
+                const uint64_t base = ((uint64_t)g.rs_frames - nb) * g.rs_frame_words;
+                const uint64_t rel = (uint64_t)(m & 0x7fffffffu) - base;
+                if ((m & 0x7fffffffu) >= base && rel % g.rs_spill_words == 0 &&
+                    rel / g.rs_spill_words < g.rs_spill_cap) {
+                    w = m & 0x7fffffffu;
+                    c = w + g.rs_spill_words - EPC_ROW;
+                    if (count) m = fr[c];
+                } else {
+                    if (bad) *bad = 1u;
+                    m = 0u;
                 }
             }
             gw[t] = w;
             if (cw) cw[t] = c;
         }
+        if (count) *count = t < ng ? m : 0u;
         if (t == 63) goff[ng] = incl;
     }
 }
@@ -2046,19 +2050,38 @@ __global__ __launch_bounds__(EPS_T) void k_dyn_epscan(DevStream *__restrict__ st
  * once.  More candidates in a group than its record holds, or more than EPF_LIST
  * positions: DF_EPSLOW (k_dyn_epscan scans the NAL). */
 #ifndef SCROLL_EPF_T
-#define SCROLL_EPF_T 256
+#define SCROLL_EPF_T 128
 #endif
 #ifndef SCROLL_EPF_LIST
-#define SCROLL_EPF_LIST 4096
+#define SCROLL_EPF_LIST 2048
+#endif
+#ifndef SCROLL_EPF_WINDOW
+#define SCROLL_EPF_WINDOW 1                 /* seams from a register window (0: byte path only) */
+#endif
+#ifndef SCROLL_EPF_CB
+#define SCROLL_EPF_CB 0                     /* candidates per thread and pass (0: by thread count) */
 #endif
 constexpr int EPF_T = SCROLL_EPF_T;
 
+/* an EP position (RBSP byte index j) into k_dyn_epfix's set: a bitmap over
+ * the NAL's bytes (bm: duplicates merge, the order comes with the
+ * compaction) or, for NALs past the bitmap's reach, a list (count *nlst,
+ * capacity lcap) */
+__device__ inline void ep_put(uint32_t j, bool bm, uint32_t *lst, uint32_t *nlst, uint32_t lcap)
+{
+    if (bm) {
+        atomicOr(&lst[j >> 5], 1u << (j & 31u));
+    } else {
+        const uint32_t q = atomicAdd(nlst, 1u);
+        if (q < lcap) lst[q] = j;
+    }
+}
+
 /* the RBSP bytes from byte B on, with the zero run before it: EP positions
- * -> lst (count nlst, capacity lcap) until the first non-zero byte at or
- * after byte Bend */
+ * -> the set (ep_put) until the first non-zero byte at or after byte Bend */
 __device__ inline void ep_eval_bytes(uint32_t B, uint32_t Bend, uint32_t nin, int ng, uint32_t T,
                                      const uint32_t *goff, const uint32_t *gb, const uint32_t *gw,
-                                     const uint32_t *fr, uint32_t *lst, uint32_t *nlst, uint32_t lcap)
+                                     const uint32_t *fr, bool bm, uint32_t *lst, uint32_t *nlst, uint32_t lcap)
 {
     uint32_t cw = 0, ci = 0xffffffffu;                  /* one RBSP word cached */
     auto byte_at = [&](uint32_t i) -> uint32_t {
@@ -2075,10 +2098,7 @@ __device__ inline void ep_eval_bytes(uint32_t B, uint32_t Bend, uint32_t nin, in
     }
     for (uint32_t i = B; i < nin; ++i) {
         const uint32_t b = byte_at(i);
-        if (ep_insert(b, k)) {
-            const uint32_t q = atomicAdd(nlst, 1u);
-            if (q < lcap) lst[q] = i;
-        }
+        if (ep_insert(b, k)) ep_put(i, bm, lst, nlst, lcap);
         if (b == 0) {
             ++k;
         } else {
@@ -2088,27 +2108,97 @@ __device__ inline void ep_eval_bytes(uint32_t B, uint32_t Bend, uint32_t nin, in
     }
 }
 
+/* the seam at bit S = goff[k] (k > 0) from a 64-bit window of the RBSP,
+ * bytes B - 4 .. B + 3 (B = S >> 3): group k - 1's bits before S and group
+ * k's first 64, one round of five independent loads (ep_eval_bytes reads
+ * word after word).  True: decided (its EP positions are in the set).
+ * False: the window cannot decide it (short groups, the zero run before B
+ * reaching its left edge, no non-zero byte at or after the seam's last byte
+ * in its right half) and the byte path redoes the seam (positions the
+ * window put are found again: the set merges them) */
+__device__ inline bool seam_window(int k, uint32_t S, uint32_t nin, const uint32_t *goff, const uint32_t *gb,
+                                   const uint32_t *gw, const uint32_t *fr, bool bm, uint32_t *lst,
+                                   uint32_t *nlst, uint32_t lcap)
+{
+    const uint32_t B = S >> 3, Bend = (S + 7) >> 3;
+    if (B < 4u) return false;
+    const uint32_t L0 = 8u * (B - 4u), G0 = goff[k - 1];
+    if (L0 < G0 || gb[k] < 8u * (B + 4u) - S) return false;
+    const uint32_t lp = L0 - G0, sh = lp & 31u, nL = S - L0;      /* 32 <= nL < 40 */
+    /* group k - 1's words run at most two past its last data word: inside
+     * its slot (the candidate record follows the data) */
+    const uint32_t *a = fr + gw[k - 1] + (lp >> 5), *b = fr + gw[k];
+    const uint32_t a0 = a[0], a1 = a[1], a2 = a[2], b0 = b[0], b1 = b[1];
+    const uint32_t hi = sh ? __builtin_amdgcn_alignbit(a0, a1, 32u - sh) : a0;
+    const uint32_t lo = sh ? __builtin_amdgcn_alignbit(a1, a2, 32u - sh) : a1;
+    const uint64_t Lw = (uint64_t)hi << 32 | lo, Rw = (uint64_t)b0 << 32 | b1;
+    const uint64_t W = (Lw & ~(~0ull >> nL)) | (Rw >> nL);
+    auto byte = [&](int i) -> uint32_t { return (uint32_t)(W >> (56 - 8 * i)) & 255u; };
+    int z = 0;                                          /* zero bytes right before B */
+    int i = 3;
+    for (; i >= 0; --i) {
+        if (byte(i)) break;
+        ++z;
+    }
+    if (i < 0) return false;                            /* the run may go on to the left */
+    for (int j = 4; j < 8; ++j) {
+        const uint32_t pos = B - 4u + (uint32_t)j;
+        if (pos >= nin) return true;
+        const uint32_t v = byte(j);
+        if (ep_insert(v, z)) ep_put(pos, bm, lst, nlst, lcap);
+        if (v == 0) {
+            ++z;
+        } else {
+            if (pos >= Bend) return true;
+            z = 0;
+        }
+    }
+    return false;
+}
+
+/* the group holding candidate i: the last g < ng with cbase[g] <= i (empty
+ * groups have empty ranges) */
+__device__ inline int cand_group(uint32_t i, int ng, const uint32_t *cbase)
+{
+    int lo = 0, hi = ng;
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (cbase[mid] <= i) lo = mid;
+        else hi = mid;
+    }
+    return lo;
+}
 
 /* k_dyn_epfix's work for NAL nb (stream s), every thread of the workgroup
- * (NT of them) calling: size, EP positions sorted and each once into the
- * frame's EP list (EPLIST_MAX kept), DF_FIXED set.  (Measured in round 4:
- * run by each NAL's last row workgroup inside k_dyn_row instead, the
- * agent-scope release fence every row workgroup then needs -- L2 write-back
- * across the XCDs -- made k_dyn_row 9.6 ms.) */
-template <int NT>
+ * (NT of them, at least two waves) calling: size, EP positions sorted and
+ * each once into the frame's EP list (EPLIST_MAX kept), DF_FIXED set.  The
+ * step is a chain of dependent loads per NAL (the measured round-4 split:
+ * table 2.3 us, counts 1.2, seams + candidates 14.6, sort 4.7 per
+ * workgroup), so the work is laid out for few round trips: the candidate
+ * counts come with the table (same wave, one sync), the seams take the last
+ * wave while the others take the candidates two at a time with their loads
+ * in flight together, and the positions go into a bitmap over the NAL's
+ * bytes (no sort: the compaction scan emits them in order, duplicates
+ * merged).  (Measured in round 4: run by each NAL's last row workgroup
+ * inside k_dyn_row instead, the agent-scope release fence every row
+ * workgroup then needs -- L2 write-back across the XCDs -- made k_dyn_row
+ * 9.6 ms.) */
+template <int NT, int LCAP>
 __device__ inline void ep_fix(DevStream *st, DynFrame *DF, size_t nb, int s, const DynGeom &g,
                               const uint32_t *rowstage, const uint32_t *gbits, uint8_t *eps, const EpfLds &E,
-                              int t, uint32_t *slow_n, uint32_t *slow_list)
+                              int t, uint32_t *slow_n, uint32_t *slow_list, uint64_t *stp)
 {
-    /* NT = 64: one wave per NAL (wave-level hand-offs), else the workgroup */
-    auto sync = [] {
-        if constexpr (NT == 64) wave_sync();
-        else __syncthreads();
+    static_assert(NT >= 128 && NT % 64 == 0, "ep_fix: one seam wave and at least one candidate wave");
+    static_assert(LCAP % (4 * NT) == 0, "ep_fix: the bitmap in whole 16-byte chunks per thread");
+    /* stp (debug, SCROLL_DEBUG_DYN_STAMPS): realtime at entry and after each
+     * step (tools/dyn_stamps.py) */
+    auto stamp = [&](int k) {
+        if (stp && t == 0) stp[k] = __builtin_amdgcn_s_memrealtime();
     };
+    stamp(0);
     uint32_t *goff = E.goff, *gb = E.gb, *gw = E.gw, *cw = E.cw, *cbase = E.cbase, *lst = E.lst;
     uint32_t &nlst = E.cnt[0], &nu = E.cnt[1], &slow = E.cnt[2], &bad = E.cnt[3];
-    if (t == 0) bad = 0u;
-    sync();
+    const uint32_t lcap = LCAP;
     const uint32_t err0 = DF->err;
     if (err0 & (DF_OVER | DF_HANDOFF)) {                /* k_dyn_rows / k_dyn_row: pools exhausted,
                                                            or a row's wait expired */
@@ -2125,19 +2215,13 @@ __device__ inline void ep_fix(DevStream *st, DynFrame *DF, size_t nb, int s, con
     constexpr int SR = DYN_STATIC_ROWS;
     const int nA = max(1, (g.y0 + SR - 1) / SR);
     const uint32_t *fr = rowstage + nb * g.rs_frame_words;
-    rs_table(gbits, nb, g, fr, goff, gb, gw, cw, t, &bad);
-    sync();
-    if (bad) {                                          /* a spill record outside the pool (never) */
-        if (t == 0) {
-            DF->err = DF_OVER | DF_FIXED;
-            DF->rbsp_bytes = 0;
-            DF->ep = 0;
-            atomicOr((unsigned int *)&st[s].err, SCROLL_DEVERR_DYN);
-        }
-        return;
-    }
+    /* the bitmap starts empty (list mode overwrites what it uses) */
+    for (uint32_t i = (uint32_t)t; i < lcap / 4u; i += (uint32_t)NT)
+        reinterpret_cast<uint4 *>(lst)[i] = make_uint4(0u, 0u, 0u, 0u);
     if (t < 64) {
-        const uint32_t c = t < ng ? fr[cw[t]] : 0u;
+        if (t == 0) bad = 0u;
+        uint32_t c;                                     /* the group's candidate count */
+        rs_table(gbits, nb, g, fr, goff, gb, gw, cw, t, &bad, &c);
         const uint32_t cmax = (t >= nA && t < nA + g.h) ? EPC_ROW - 1u : EPC_STATIC - 1u;
         const uint32_t cc = min(c, cmax);
         const uint32_t incl = wave_incl_sum(cc, t);
@@ -2147,10 +2231,19 @@ __device__ inline void ep_fix(DevStream *st, DynFrame *DF, size_t nb, int s, con
         if (t == 0) {
             slow = ov ? 1u : 0u;
             nlst = 0;
-            nu = 0;
         }
     }
-    sync();
+    __syncthreads();
+    stamp(1);
+    if (bad) {                                          /* a spill record outside the pool (never) */
+        if (t == 0) {
+            DF->err = DF_OVER | DF_FIXED;
+            DF->rbsp_bytes = 0;
+            DF->ep = 0;
+            atomicOr((unsigned int *)&st[s].err, SCROLL_DEVERR_DYN);
+        }
+        return;
+    }
     const uint32_t T = goff[ng];                        /* NAL RBSP bits incl. the stop bit */
     const uint32_t nin = (T + 7) >> 3;                  /* bitwriter.c:103-111 */
     if (((nin + 31u) & ~31u) > g.slot_bytes - DYN_OVF_BYTES) {   /* the cap the API sets */
@@ -2162,50 +2255,84 @@ __device__ inline void ep_fix(DevStream *st, DynFrame *DF, size_t nb, int s, con
         }
         return;
     }
-    const uint32_t lcap = E.lcap;
-    const uint32_t nseam = (uint32_t)ng, nwork = slow ? 0u : nseam + cbase[ng];
-    for (uint32_t wk = (uint32_t)t; wk < nwork; wk += (uint32_t)NT) {
-        if (wk < nseam) {                               /* the seam before group wk (0: NAL start) */
-            const uint32_t S = goff[wk];
-            if (S < T) ep_eval_bytes(S >> 3, (S + 7) >> 3, nin, ng, T, goff, gb, gw, fr, lst, &nlst, lcap);
-            continue;
-        }
-        const uint32_t ci = wk - nseam;
-        int gg = 0;
-        while (gg + 1 < ng && cbase[gg + 1] <= ci) ++gg;
-        const uint32_t *src = fr + gw[gg];
-        const uint32_t wi = fr[cw[gg] + 1 + (ci - cbase[gg])];
-        const uint32_t bits = gb[gg], nwd = (bits + 31u) >> 5, O = goff[gg];
-        if (wi >= nwd) continue;
-        const uint32_t w = ep_data(src[wi], wi, bits);
-        const uint32_t nx = wi + 1 < nwd ? ep_data(src[wi + 1], wi + 1, bits) : 0xffffffffu;
-        uint32_t m = ep_run_starts(wi ? src[wi - 1] : 0u, w, nx, wi, bits);
-        while (m) {                                     /* usually one run */
-            const uint32_t a = (uint32_t)__builtin_clz(m);
-            m &= ~(0x80000000u >> a);
-            const uint64_t Y = ((uint64_t)w << 32 | nx) << a;
-            uint32_t e = bits;
-            if (Y) {
-                e = 32u * wi + a + (uint32_t)__builtin_clzll(Y);
-            } else {
-                for (uint32_t q = wi + 2; q < nwd; ++q) {
-                    const uint32_t v = ep_data(src[q], q, bits);
-                    if (v) {
-                        e = 32u * q + (uint32_t)__builtin_clz(v);
-                        break;
-                    }
-                }
+    const uint32_t nbw = (nin + 31u) >> 5;              /* bitmap words */
+    const bool bm = nbw <= lcap;
+    const int wave = t >> 6, lane = t & 63;
+    constexpr int NC = NT;                              /* candidate threads: all */
+    const uint32_t nc = cbase[ng];
+    if (!slow) {
+        if (wave == NT / 64 - 1) {
+            /* the seam before group k (0: NAL start): its bytes from a
+             * window of the RBSP, or byte by byte where the window cannot
+             * decide */
+            uint32_t nslow = 0;                         /* seams the window left to the byte path */
+            for (int k = lane; k < ng; k += 64) {
+                const uint32_t S = goff[k];
+                if (S >= T) continue;
+                if (SCROLL_EPF_WINDOW && k > 0 && seam_window(k, S, nin, goff, gb, gw, fr, bm, lst, &nlst, lcap)) continue;
+                ep_eval_bytes(S >> 3, (S + 7) >> 3, nin, ng, T, goff, gb, gw, fr, bm, lst, &nlst, lcap);
+                ++nslow;
             }
-            const uint32_t A = (O + 32u * wi + a + 7u) & ~7u, E2 = O + e;
-            for (uint32_t j = A + 16u; j + 6u <= E2; j += 16u) {
-                const uint32_t q = atomicAdd(&nlst, 1u);
-                if (q < lcap) lst[q] = j >> 3;
+            if (stp) {
+                const uint32_t tot = wave_incl_sum(nslow, lane);
+                if (lane == 63) stp[7] = tot;
+            }
+        }
+        /* candidate words, CB per thread and pass: the index loads, then
+         * the three data words of each, then the runs */
+        constexpr int CB = SCROLL_EPF_CB ? SCROLL_EPF_CB : (NC >= 192 ? 2 : 4);
+        for (uint32_t i0 = 0; i0 < nc; i0 += (uint32_t)(CB * NC)) {
+            uint32_t wi[CB], gg[CB];
+#pragma unroll
+            for (int q = 0; q < CB; ++q) {
+                const uint32_t ci = i0 + (uint32_t)(q * NC + t);
+                gg[q] = ci < nc ? (uint32_t)cand_group(ci, ng, cbase) : 0u;
+                wi[q] = ci < nc ? fr[cw[gg[q]] + 1u + (ci - cbase[gg[q]])] : 0xffffffffu;
+            }
+            uint32_t pw[CB], w[CB], nx[CB], nwd[CB];
+#pragma unroll
+            for (int q = 0; q < CB; ++q) {
+                const uint32_t *src = fr + gw[gg[q]];
+                nwd[q] = (gb[gg[q]] + 31u) >> 5;
+                const bool ok = wi[q] < nwd[q];
+                pw[q] = ok && wi[q] ? src[wi[q] - 1u] : 0u;
+                w[q] = ok ? src[wi[q]] : 0u;
+                nx[q] = ok && wi[q] + 1u < nwd[q] ? src[wi[q] + 1u] : 0u;
+            }
+#pragma unroll
+            for (int q = 0; q < CB; ++q) {
+                if (wi[q] >= nwd[q]) continue;
+                const uint32_t bits = gb[gg[q]], O = goff[gg[q]], x = wi[q];
+                const uint32_t *src = fr + gw[gg[q]];
+                const uint32_t wd = ep_data(w[q], x, bits);
+                const uint32_t nd = x + 1u < nwd[q] ? ep_data(nx[q], x + 1u, bits) : 0xffffffffu;
+                uint32_t m = ep_run_starts(pw[q], wd, nd, x, bits);
+                while (m) {                             /* usually one run */
+                    const uint32_t a = (uint32_t)__builtin_clz(m);
+                    m &= ~(0x80000000u >> a);
+                    const uint64_t Y = ((uint64_t)wd << 32 | nd) << a;
+                    uint32_t e = bits;
+                    if (Y) {
+                        e = 32u * x + a + (uint32_t)__builtin_clzll(Y);
+                    } else {
+                        for (uint32_t r = x + 2u; r < nwd[q]; ++r) {
+                            const uint32_t v = ep_data(src[r], r, bits);
+                            if (v) {
+                                e = 32u * r + (uint32_t)__builtin_clz(v);
+                                break;
+                            }
+                        }
+                    }
+                    const uint32_t A = (O + 32u * x + a + 7u) & ~7u, E2 = O + e;
+                    for (uint32_t j = A + 16u; j + 6u <= E2; j += 16u) ep_put(j >> 3, bm, lst, &nlst, lcap);
+                }
             }
         }
     }
-    sync();
+    __syncthreads();
+    stamp(2);
     const uint32_t n = nlst;
-    if (slow || n > lcap) {
+    if (slow || (!bm && n > lcap)) {
         if (t == 0) {
             DF->err = DF_EPSLOW | DF_FIXED;             /* k_dyn_epscan finds them */
             DF->rbsp_bytes = nin;
@@ -2214,54 +2341,87 @@ __device__ inline void ep_fix(DevStream *st, DynFrame *DF, size_t nb, int s, con
         }
         return;
     }
-    /* each position once, in increasing order (k_dyn_emit_gather needs no
-     * sort): a bitonic sort of the list padded to a power of two (log^2
-     * steps, one compare-exchange per thread and step -- the rank-by-count
-     * form it replaces was n^2 / NT and cost 0.07 ms per launch), then the
-     * first of each run of equal positions goes to its rank: a scan of the
-     * threads' contiguous chunks */
-    const uint32_t P = n <= 1u ? 1u : 1u << (32 - __builtin_clz(n - 1u));   /* <= lcap (n <= lcap) */
-    for (uint32_t i = (uint32_t)t + n; i < P; i += (uint32_t)NT) lst[i] = 0xffffffffu;
-    sync();
-    for (uint32_t k = 2; k <= P; k <<= 1)
-        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-            for (uint32_t i = (uint32_t)t; i < P; i += (uint32_t)NT) {
-                const uint32_t l = i ^ j;
-                if (l > i) {
-                    const uint32_t a = lst[i], b = lst[l];
-                    if ((a > b) == ((i & k) == 0u)) {
-                        lst[i] = b;
-                        lst[l] = a;
+    if (!bm) {
+        /* list mode (NALs over 32 lcap bytes): a bitonic sort of the list
+         * padded to a power of two (log^2 steps, one compare-exchange per
+         * thread and step) */
+        const uint32_t P = n <= 1u ? 1u : 1u << (32 - __builtin_clz(n - 1u));   /* <= lcap (n <= lcap) */
+        for (uint32_t i = (uint32_t)t + n; i < P; i += (uint32_t)NT) lst[i] = 0xffffffffu;
+        __syncthreads();
+        for (uint32_t k = 2; k <= P; k <<= 1)
+            for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+                for (uint32_t i = (uint32_t)t; i < P; i += (uint32_t)NT) {
+                    const uint32_t l = i ^ j;
+                    if (l > i) {
+                        const uint32_t a = lst[i], b = lst[l];
+                        if ((a > b) == ((i & k) == 0u)) {
+                            lst[i] = b;
+                            lst[l] = a;
+                        }
                     }
                 }
+                __syncthreads();
             }
-            sync();
-        }
-    const uint32_t C = (n + (uint32_t)NT - 1u) / (uint32_t)NT, c0 = (uint32_t)t * C, c1 = min(c0 + C, n);
+    }
+    stamp(3);
+    /* compaction: the threads' contiguous chunks (bitmap words -- CW each,
+     * held in registers -- or sorted list entries whose value differs from
+     * the one before), a scan, then each chunk's positions in order from its
+     * rank */
+    constexpr int CW = LCAP / NT;
+    uint4 bw[CW / 4];
+    const uint32_t C = bm ? 0u : (n + (uint32_t)NT - 1u) / (uint32_t)NT, c0 = (uint32_t)t * C, c1 = min(c0 + C, n);
     uint32_t mine = 0;
-    for (uint32_t i = c0; i < c1; ++i) mine += (i == 0u || lst[i] != lst[i - 1u]) ? 1u : 0u;
+    if (bm) {
+#pragma unroll
+        for (int k = 0; k < CW / 4; ++k) {
+            bw[k] = reinterpret_cast<const uint4 *>(lst)[t * (CW / 4) + k];
+            mine += (uint32_t)(__builtin_popcount(bw[k].x) + __builtin_popcount(bw[k].y) +
+                               __builtin_popcount(bw[k].z) + __builtin_popcount(bw[k].w));
+        }
+    } else {
+        for (uint32_t i = c0; i < c1; ++i) mine += (i == 0u || lst[i] != lst[i - 1u]) ? 1u : 0u;
+    }
     uint32_t ex = 0;
     {
-        const int lane = t & 63, wv = t >> 6;
         const uint32_t incl = wave_incl_sum(mine, lane);
-        if (lane == 63) E.ws[wv] = incl;
-        sync();
-        for (int q = 0; q < wv; ++q) ex += E.ws[q];
+        if (lane == 63) E.ws[wave] = incl;
+        __syncthreads();
+        for (int q = 0; q < wave; ++q) ex += E.ws[q];
         ex += incl - mine;
         if (t == NT - 1) nu = ex + mine;
     }
     uint32_t *eplist = reinterpret_cast<uint32_t *>(eps + nb * DYN_OVF_BYTES);
-    for (uint32_t i = c0; i < c1; ++i)
-        if (i == 0u || lst[i] != lst[i - 1u]) {
-            if (ex < (uint32_t)EPLIST_MAX) eplist[ex] = lst[i];
-            ++ex;
+    if (bm) {
+        if (mine) {
+#pragma unroll
+            for (int k = 0; k < CW / 4; ++k) {
+                const uint32_t wv4[4] = {bw[k].x, bw[k].y, bw[k].z, bw[k].w};
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    for (uint32_t m = wv4[e]; m; m &= m - 1u) {
+                        if (ex < (uint32_t)EPLIST_MAX)
+                            eplist[ex] = 32u * (uint32_t)(t * CW + 4 * k + e) + (uint32_t)__builtin_ctz(m);
+                        ++ex;
+                    }
+            }
         }
-    sync();
+    } else {
+        for (uint32_t i = c0; i < c1; ++i)
+            if (i == 0u || lst[i] != lst[i - 1u]) {
+                if (ex < (uint32_t)EPLIST_MAX) eplist[ex] = lst[i];
+                ++ex;
+            }
+    }
+    __syncthreads();
     if (t == 0) {
         DF->err = DF_FIXED;                             /* clears DF_GENERAL */
         DF->rbsp_bytes = nin;
         DF->ep = nu;
+        if (stp) stp[6] = (uint64_t)nc | (uint64_t)nu << 32;
     }
+    stamp(4);
+    stamp(5);
 }
 
 /* grid (frames, streams): one workgroup per NAL.  (Measured: one wave per
@@ -2272,19 +2432,20 @@ __global__ __launch_bounds__(EPF_T) void k_dyn_epfix(DevStream *__restrict__ st,
                                                      int ld_fr, int nframes, DynGeom g,
                                                      const uint32_t *__restrict__ rowstage,
                                                      const uint32_t *__restrict__ gbits, uint8_t *__restrict__ eps,
-                                                     uint32_t *__restrict__ slow_n, uint32_t *__restrict__ slow)
+                                                     uint32_t *__restrict__ slow_n, uint32_t *__restrict__ slow,
+                                                     uint64_t *__restrict__ stamps)
 {
     __shared__ uint32_t goff[65], gb[64], gw[64], cw[64];
     __shared__ uint32_t cbase[65];                      /* runs before group g */
-    __shared__ uint32_t lst[EPF_LIST];
+    __shared__ __attribute__((aligned(16))) uint32_t lst[EPF_LIST];   /* the position bitmap / list */
     __shared__ uint32_t cnt[4], ws[EPF_T / 64];
     const int f = blockIdx.x, s = blockIdx.y, t = threadIdx.x;
     if (f >= nframes) return;
     const size_t nb = (size_t)s * ld_fr + f;
     DynFrame *DF = dfr + nb;
     if (DF->nal < 0) return;
-    const EpfLds E{goff, gb, gw, cw, cbase, lst, cnt, (uint32_t)EPF_LIST, ws};
-    ep_fix<EPF_T>(st, DF, nb, s, g, rowstage, gbits, eps, E, t, slow_n, slow);
+    const EpfLds E{goff, gb, gw, cw, cbase, lst, cnt, ws};
+    ep_fix<EPF_T, EPF_LIST>(st, DF, nb, s, g, rowstage, gbits, eps, E, t, slow_n, slow, stamps ? stamps + ((size_t)s * nframes + f) * 8 : nullptr);
 }
 
 /* ---------------------------------------------------------------------- */
@@ -2665,7 +2826,8 @@ __global__ __launch_bounds__(DT) void k_dyn_gather(const DevStream *__restrict__
                                                   const uint8_t *__restrict__ eps,
                                                   const uint32_t *__restrict__ rowstage,
                                                   const uint32_t *__restrict__ gbits,
-                                                  uint8_t *__restrict__ arena, uint64_t ld_arena)
+                                                  uint8_t *__restrict__ arena, uint64_t ld_arena,
+                                                  uint64_t *__restrict__ stamps)
 {
     __shared__ uint32_t raw[EPLIST_MAX], sp[EPLIST_MAX + 1];
     __shared__ uint32_t goff[65], gb[64], gw[64];
@@ -2677,6 +2839,9 @@ __global__ __launch_bounds__(DT) void k_dyn_gather(const DevStream *__restrict__
     if (n > ep_cap(g)) return;                               /* k_dyn_emit's NAL */
     const NalDesc d = nal[(size_t)s * ld_nal + j];
     if (d.slow != 2) return;
+    /* debug (SCROLL_DEBUG_DYN_STAMPS): realtime at entry, after the prologue, at the end */
+    uint64_t *stp = stamps && blockIdx.z == 0 && t == 0 ? stamps + ((size_t)s * gridDim.x + blockIdx.x) * 8 : nullptr;
+    if (stp) stp[0] = __builtin_amdgcn_s_memrealtime();
     const size_t nb = (size_t)s * ld_fr + f;
     const uint32_t *el = reinterpret_cast<const uint32_t *>(eps + nb * DYN_OVF_BYTES);
     const uint32_t *fr = rowstage + nb * g.rs_frame_words;
@@ -2714,6 +2879,7 @@ __global__ __launch_bounds__(DT) void k_dyn_gather(const DevStream *__restrict__
         raw[bi] = K;
     }
     __syncthreads();
+    if (stp) stp[1] = __builtin_amdgcn_s_memrealtime();
     const uint8_t hdr[5] = {0, 0, 0, 1, nal_header_byte(0)};           /* nal.c:59-64 */
     const uint64_t cfirst = o0 >> 4;
     const uint32_t cnal = (uint32_t)(((o1 + 15) >> 4) - cfirst);
@@ -2802,6 +2968,10 @@ __global__ __launch_bounds__(DT) void k_dyn_gather(const DevStream *__restrict__
             }
             q[b] = v;
         }
+    }
+    if (stamps) {                                            /* uniform */
+        __syncthreads();
+        if (stp) stp[2] = __builtin_amdgcn_s_memrealtime();
     }
 }
 
@@ -2901,14 +3071,13 @@ int dyn_launch_static(hipStream_t hs, int nframes, int S, DevStream *st, const N
 
 int dyn_launch_pack(hipStream_t hs, int nframes, int S, DevStream *st, const NalDesc *nal,
                     int ld_nal, const PlanPending *pend, DynFrame *dfr, int ld_fr,
-                    const DynGeom *g, const DynScratch *x, uint8_t *eps, uint64_t *stamps, bool with_static)
+                    const DynGeom *g, const DynScratch *x, uint8_t *eps, uint64_t *stamps)
 {
-    (void)stamps;
     if (nframes <= 0 || S <= 0) return 0;
-    if (with_static && dyn_launch_static(hs, nframes, S, st, nal, ld_nal, pend, dfr, ld_fr, g, x)) return -1;
+    if (dyn_launch_static(hs, nframes, S, st, nal, ld_nal, pend, dfr, ld_fr, g, x)) return -1;
     uint32_t *slow_n = x->ctr + DYN_CTR_SLOW, *slow = x->ctr + DYN_CTR_LIST + x->ctr_frames;
     hipLaunchKernelGGL(k_dyn_epfix, dim3(nframes, S), dim3(EPF_T), 0, hs, st, dfr, ld_fr, nframes, *g,
-                       x->rowstage, x->gbits, eps, slow_n, slow);
+                       x->rowstage, x->gbits, eps, slow_n, slow, stamps);
     if (hipGetLastError() != hipSuccess) return -1;
     hipLaunchKernelGGL(k_dyn_epscan, dim3(EPS_Z, EPS_SLOTS), dim3(EPS_T), 0, hs, st, dfr, ld_fr, *g,
                        x->rowstage, x->gbits, eps, slow_n, slow);
@@ -2930,7 +3099,7 @@ int dyn_launch_emit(hipStream_t hs, int nframes, int S, const DevStream *st, con
     const dim3 grid(nframes, S, GATHER_Z);
     if (x && !(g->debug & SCROLL_DEBUG_DYN_GATHER1))
         hipLaunchKernelGGL(k_dyn_gather, dim3(nframes, S, SCROLL_GATHER2_Z), dim3(DT), 0, hs, st, nal, ld_nal, dfr,
-                           ld_fr, *g, stage, rs, gbits, arena, ld_arena);
+                           ld_fr, *g, stage, rs, gbits, arena, ld_arena, stamps);
     else if (x && big)
         hipLaunchKernelGGL((k_dyn_emit_gather<4, true>), grid, dim3(DT), 0, hs, st, nal, ld_nal, dfr, ld_fr, *g,
                            stage, rs, gbits, arena, ld_arena, stamps);

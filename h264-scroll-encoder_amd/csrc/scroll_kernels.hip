@@ -29,9 +29,6 @@
 #include "engine.h"
 #include "scroll_device.h"
 
-#ifndef SCROLL_DYN_STATIC_OVERLAP
-#define SCROLL_DYN_STATIC_OVERLAP 1     /* k_dyn_static beside the block coder (b->pipe) */
-#endif
 #include "dyn_device.h"
 
 using namespace scroll;
@@ -1364,23 +1361,6 @@ static int launch(ScrollBatch *b, int nframes, int plan_mode, int nal_max, hipSt
             const DynGeom &G = b->geo;
             const size_t nalw = (size_t)G.w * G.h, ng = (size_t)G.ngroups;
             HIPCHK(hipMemsetAsync(b->dx.ctr, 0, DYN_CTR_LIST * sizeof(uint32_t), hs));   /* spill / record slots, epscan list */
-            /* k_dyn_static (latency-bound, 0.03 ms) needs only the state pass:
-             * it runs on b->pipe beside the issue-bound block coder */
-            const bool ovl = nch == 1 && SCROLL_DYN_STATIC_OVERLAP;
-            if (ovl) {
-                if (!b->pipe) {
-                    HIPCHK(hipStreamCreateWithFlags(&b->pipe, hipStreamNonBlocking));
-                    for (hipEvent_t &e : b->pipe_ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-                }
-                HIPCHK(hipEventRecord(b->pipe_ev[0], hs));
-                HIPCHK(hipStreamWaitEvent(b->pipe, b->pipe_ev[0], 0));
-                if (dyn_launch_static(b->pipe, nframes, S, b->d_st, b->d_nal, b->ld_nal, b->d_pend, b->d_dfr, ld_fr,
-                                      &G, &b->dx)) {
-                    set_err("k_dyn_static launch: %s", hipGetErrorString(hipGetLastError()));
-                    return SCROLL_ERR_HIP;
-                }
-                HIPCHK(hipEventRecord(b->pipe_ev[1], b->pipe));
-            }
             for (int c = 0; c < nch; ++c) {
                 const int s0 = (int)((int64_t)S * c / nch), s1 = (int)((int64_t)S * (c + 1) / nch);
                 const size_t nb0 = (size_t)s0 * ld_fr;
@@ -1409,9 +1389,8 @@ static int launch(ScrollBatch *b, int nframes, int plan_mode, int nal_max, hipSt
                 } else if ((rc = mark(6))) {
                     return rc;
                 }
-                if (ovl) HIPCHK(hipStreamWaitEvent(hs, b->pipe_ev[1], 0));
                 if (dyn_launch_pack(hp, nframes, s1 - s0, st0, nal0, b->ld_nal, pend0, dfr0, ld_fr, &G, &xc,
-                                    stage0, stamps ? b->d_dbg : nullptr, !ovl)) {
+                                    stage0, stamps ? b->d_dbg : nullptr)) {
                     set_err("k_dyn_static / k_dyn_epscan launch: %s", hipGetErrorString(hipGetLastError()));
                     return SCROLL_ERR_HIP;
                 }

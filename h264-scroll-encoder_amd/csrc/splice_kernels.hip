@@ -1065,13 +1065,11 @@ __global__ __launch_bounds__(64 * LANE_WAVES) void k_splice_lanes(const int32_t 
                 uint32_t nim = 0xffffffffu;                             /* this MB's modes 3 7 11 15 */
                 Mv me{0, 0, 0};
                 int part = 0;
-                bool pcm = false;
                 if (mbt >= 5u) {
                     const int it = (int)mbt - 5;
                     intra = it == 0 ? 1 : (it == 25 ? 3 : 2);
                     me = Mv{SPLICE_REF_INTRA, 0, 0};
                     if (intra == 3) {
-                        pcm = true;
                         bool bad = false;
                         if (r.p & 7u) bad = r.u(8 - (int)(r.p & 7u)) != 0u;
                         poff = r.p;

@@ -9,7 +9,7 @@ the s_memrealtime span (100 MHz, microseconds) of each phase:
   tokens       coeff_token and length of every piece
   mb+scan      cbp, piece offsets per MB; the row's MB offsets
   write        bits -> LDS window -> the row's row-stage words
-plus the k_dyn_emit_gather workgroup spans.  Then times the workload
+plus the k_dyn_epfix steps and the k_dyn_gather workgroup spans.  Then times the workload
 without stamps (HIP events).
 
     python h264-scroll-encoder_amd/tools/dyn_stamps.py [--streams 256 --frames 16]
@@ -97,14 +97,28 @@ def main():
         ends = gg[:, :, 5][gg[:, :, 5] > 0]
         conc = [int(np.sum((g0 <= x) & (ends > x))) for x in np.linspace(t0, t1, 12)]
         print("  resident WGs over time:", conc)
-    e = allst[S * F:2 * S * F].astype(np.int64)  # k_dyn_emit_gather: realtime (100 MHz)
+    x = allst[:S * F].astype(np.int64)           # k_dyn_epfix: entry, table+counts, work, sort, end
+    x = x[x[:, 5] > 0]
+    if len(x):
+        t0 = x[:, 0].min()
+        print(f"k_dyn_epfix: {len(x)} WGs, span {(x[:, 5].max() - t0) / 100.0:.1f} us, WG duration mean "
+              f"{((x[:, 5] - x[:, 0]) / 100.0).mean():.1f} us, candidate words mean {(x[:, 6] & 0xffffffff).mean():.1f}, "
+              f"EP positions mean {(x[:, 6] >> 32).mean():.1f}, seams on the byte path mean {x[:, 7].mean():.2f}")
+        prev = x[:, 0]
+        for k, nm in enumerate(["table+counts", "seams+cands", "sort", "compact+out"]):
+            d = (x[:, k + 1] - prev) / 100.0
+            print(f"  {nm:12s} mean {d.mean():7.2f} us  p99 {np.percentile(d, 99):7.2f}")
+            prev = x[:, k + 1]
+        conc = [int(np.sum((x[:, 0] <= v) & (x[:, 5] > v))) for v in np.linspace(t0, x[:, 5].max(), 12)]
+        print("  resident WGs over time:", conc)
+    e = allst[S * F:2 * S * F].astype(np.int64)  # k_dyn_gather: realtime (100 MHz)
     e = e[e[:, 0] > 0]
     if len(e):
         t0 = e[:, 0].min()
         span = (e[:, 2].max() - t0) / 100.0
         dur = (e[:, 2] - e[:, 0]) / 100.0
         srt = (e[:, 1] - e[:, 0]) / 100.0
-        print(f"k_dyn_emit_gather: {len(e)} WGs, span {span:.1f} us, WG duration mean {dur.mean():.1f} "
+        print(f"k_dyn_gather: {len(e)} WGs, span {span:.1f} us, WG duration mean {dur.mean():.1f} "
               f"p50 {np.percentile(dur, 50):.1f} p99 {np.percentile(dur, 99):.1f} max {dur.max():.1f} us, "
               f"prologue+sort mean {srt.mean():.1f} us")
         st0 = (e[:, 0] - t0) / 100.0

@@ -2055,12 +2055,6 @@ __global__ __launch_bounds__(EPS_T) void k_dyn_epscan(DevStream *__restrict__ st
 #ifndef SCROLL_EPF_LIST
 #define SCROLL_EPF_LIST 2048
 #endif
-#ifndef SCROLL_EPF_WINDOW
-#define SCROLL_EPF_WINDOW 1                 /* seams from a register window (0: byte path only) */
-#endif
-#ifndef SCROLL_EPF_CB
-#define SCROLL_EPF_CB 0                     /* candidates per thread and pass (0: by thread count) */
-#endif
 constexpr int EPF_T = SCROLL_EPF_T;
 
 /* an EP position (RBSP byte index j) into k_dyn_epfix's set: a bitmap over
@@ -2106,54 +2100,6 @@ __device__ inline void ep_eval_bytes(uint32_t B, uint32_t Bend, uint32_t nin, in
             k = 0;
         }
     }
-}
-
-/* the seam at bit S = goff[k] (k > 0) from a 64-bit window of the RBSP,
- * bytes B - 4 .. B + 3 (B = S >> 3): group k - 1's bits before S and group
- * k's first 64, one round of five independent loads (ep_eval_bytes reads
- * word after word).  True: decided (its EP positions are in the set).
- * False: the window cannot decide it (short groups, the zero run before B
- * reaching its left edge, no non-zero byte at or after the seam's last byte
- * in its right half) and the byte path redoes the seam (positions the
- * window put are found again: the set merges them) */
-__device__ inline bool seam_window(int k, uint32_t S, uint32_t nin, const uint32_t *goff, const uint32_t *gb,
-                                   const uint32_t *gw, const uint32_t *fr, bool bm, uint32_t *lst,
-                                   uint32_t *nlst, uint32_t lcap)
-{
-    const uint32_t B = S >> 3, Bend = (S + 7) >> 3;
-    if (B < 4u) return false;
-    const uint32_t L0 = 8u * (B - 4u), G0 = goff[k - 1];
-    if (L0 < G0 || gb[k] < 8u * (B + 4u) - S) return false;
-    const uint32_t lp = L0 - G0, sh = lp & 31u, nL = S - L0;      /* 32 <= nL < 40 */
-    /* group k - 1's words run at most two past its last data word: inside
-     * its slot (the candidate record follows the data) */
-    const uint32_t *a = fr + gw[k - 1] + (lp >> 5), *b = fr + gw[k];
-    const uint32_t a0 = a[0], a1 = a[1], a2 = a[2], b0 = b[0], b1 = b[1];
-    const uint32_t hi = sh ? __builtin_amdgcn_alignbit(a0, a1, 32u - sh) : a0;
-    const uint32_t lo = sh ? __builtin_amdgcn_alignbit(a1, a2, 32u - sh) : a1;
-    const uint64_t Lw = (uint64_t)hi << 32 | lo, Rw = (uint64_t)b0 << 32 | b1;
-    const uint64_t W = (Lw & ~(~0ull >> nL)) | (Rw >> nL);
-    auto byte = [&](int i) -> uint32_t { return (uint32_t)(W >> (56 - 8 * i)) & 255u; };
-    int z = 0;                                          /* zero bytes right before B */
-    int i = 3;
-    for (; i >= 0; --i) {
-        if (byte(i)) break;
-        ++z;
-    }
-    if (i < 0) return false;                            /* the run may go on to the left */
-    for (int j = 4; j < 8; ++j) {
-        const uint32_t pos = B - 4u + (uint32_t)j;
-        if (pos >= nin) return true;
-        const uint32_t v = byte(j);
-        if (ep_insert(v, z)) ep_put(pos, bm, lst, nlst, lcap);
-        if (v == 0) {
-            ++z;
-        } else {
-            if (pos >= Bend) return true;
-            z = 0;
-        }
-    }
-    return false;
 }
 
 /* the group holding candidate i: the last g < ng with cbase[g] <= i (empty
@@ -2262,25 +2208,19 @@ __device__ inline void ep_fix(DevStream *st, DynFrame *DF, size_t nb, int s, con
     const uint32_t nc = cbase[ng];
     if (!slow) {
         if (wave == NT / 64 - 1) {
-            /* the seam before group k (0: NAL start): its bytes from a
-             * window of the RBSP, or byte by byte where the window cannot
-             * decide */
-            uint32_t nslow = 0;                         /* seams the window left to the byte path */
+            /* the seam before group k (0: NAL start): its bytes from the
+             * RBSP.  (Measured in round 4: from a 64-bit register window of
+             * the two groups, one round of loads -- the byte path remained
+             * only for the NAL start -- 0.060 against 0.055 ms per launch:
+             * shorter workgroups, but fewer of them resident) */
             for (int k = lane; k < ng; k += 64) {
                 const uint32_t S = goff[k];
-                if (S >= T) continue;
-                if (SCROLL_EPF_WINDOW && k > 0 && seam_window(k, S, nin, goff, gb, gw, fr, bm, lst, &nlst, lcap)) continue;
-                ep_eval_bytes(S >> 3, (S + 7) >> 3, nin, ng, T, goff, gb, gw, fr, bm, lst, &nlst, lcap);
-                ++nslow;
-            }
-            if (stp) {
-                const uint32_t tot = wave_incl_sum(nslow, lane);
-                if (lane == 63) stp[7] = tot;
+                if (S < T) ep_eval_bytes(S >> 3, (S + 7) >> 3, nin, ng, T, goff, gb, gw, fr, bm, lst, &nlst, lcap);
             }
         }
         /* candidate words, CB per thread and pass: the index loads, then
          * the three data words of each, then the runs */
-        constexpr int CB = SCROLL_EPF_CB ? SCROLL_EPF_CB : (NC >= 192 ? 2 : 4);
+        constexpr int CB = NC >= 192 ? 2 : 4;
         for (uint32_t i0 = 0; i0 < nc; i0 += (uint32_t)(CB * NC)) {
             uint32_t wi[CB], gg[CB];
 #pragma unroll

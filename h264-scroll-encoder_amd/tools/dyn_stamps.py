@@ -103,7 +103,7 @@ def main():
         t0 = x[:, 0].min()
         print(f"k_dyn_epfix: {len(x)} WGs, span {(x[:, 5].max() - t0) / 100.0:.1f} us, WG duration mean "
               f"{((x[:, 5] - x[:, 0]) / 100.0).mean():.1f} us, candidate words mean {(x[:, 6] & 0xffffffff).mean():.1f}, "
-              f"EP positions mean {(x[:, 6] >> 32).mean():.1f}, seams on the byte path mean {x[:, 7].mean():.2f}")
+              f"EP positions mean {(x[:, 6] >> 32).mean():.1f}")
         prev = x[:, 0]
         for k, nm in enumerate(["table+counts", "seams+cands", "sort", "compact+out"]):
             d = (x[:, k + 1] - prev) / 100.0

@@ -2,22 +2,22 @@
 # round_profile.sh TAG -- the measurement set committed under profiles/ each round
 # (run on the GPU box from the repo root, e.g. through gpurun):
 #   bench lines of every workload, rocprofv3 kernel stats of p720dyn / p4kdyn /
-#   ingest720 / ipcm720,
+#   p720splicerows / ingest720 / ipcm720,
 #   FETCH_SIZE and WRITE_SIZE passes (separate runs) over k_dyn_row, and one SQ
 #   counter pass over the dynamic-rect kernels.  Every GPU step has its own time
 #   limit; the first failing step ends the script.
 set -e -o pipefail
-TAG=${1:-r03}
+TAG=${1:-r04}
 O=gpurun_out/prof_$TAG
 mkdir -p "$O"
 export TMPDIR=/tmp
 T="timeout -k 10"
 $T 300 python3 bench.py --steps 20 --warmup 3 > "$O/bench_p720dyn.json" 2> "$O/bench_p720dyn.err"
-for w in p720 p4kdyn p720hint p720splice ingest720 ipcm720; do
+for w in p720 p4kdyn p720hint p720splice p720splicerows ingest720 ipcm720; do
     $T 200 python3 bench.py --steps 10 --warmup 2 --workload $w > "$O/bench_$w.json" 2> "$O/bench_$w.err"
 done
 $T 200 python3 bench.py --steps 10 --warmup 2 --streams 1024 --no-cpu > "$O/bench_p720dyn_1024streams.json" 2> /dev/null
-for w in p720dyn p4kdyn ingest720 ipcm720; do
+for w in p720dyn p4kdyn p720splicerows ingest720 ipcm720; do
     $T 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/stats_$w" -o run -- python3 bench.py --steps 5 --warmup 2 --no-cpu --no-host --workload $w > "$O/stats_$w.log" 2>&1
 done
 $T 120 rocprofv3 --output-format csv --pmc FETCH_SIZE -d "$O/pmc_fetch" -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu --no-host > "$O/pmc_fetch.log" 2>&1

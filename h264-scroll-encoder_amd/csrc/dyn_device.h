@@ -806,6 +806,16 @@ struct alignas(16) PTabs {
     uint16_t tzdc[3][4];
     uint16_t rb[7][16];
 };
+/* the subset k_dyn_row keeps in LDS: its bodies take total_zeros / run_before
+ * from one global table entry per block, so only coeff_token and the chroma
+ * DC block's fields stay (480 bytes less per workgroup; config 5's 47-MB rows
+ * still need 33.5 KB, four resident workgroups per CU -- five would need
+ * 32 KB) */
+struct alignas(16) RowTabs {
+    uint16_t ct[4][68];
+    uint16_t tzdc[3][4];
+    uint16_t rb[7][16];
+};
 
 __device__ __host__ inline void build_ptabs(const Tabs &T, PTabs &P, int tid, int nthr)
 {
@@ -1132,8 +1142,8 @@ __device__ __host__ inline int cavlc_body_t(CAP &cap, const int8_t *lb, uint32_t
 
 /* chroma DC (2x2, nC = -1): the whole block from 4 levels in registers,
  * unrolled, packed LDS tables (P.ct[3], P.tzdc, P.rb) */
-template <class CAP>
-__device__ __host__ inline int cavlc_dc4(CAP &cap, const PTabs &P, const int c[4])
+template <class CAP, class PT>
+__device__ __host__ inline int cavlc_dc4(CAP &cap, const PT &P, const int c[4])
 {
     const uint32_t nz = (c[0] != 0 ? 1u : 0u) | (c[1] != 0 ? 2u : 0u) | (c[2] != 0 ? 4u : 0u) |
                         (c[3] != 0 ? 8u : 0u);

@@ -66,6 +66,23 @@ __device__ inline void load_ptabs(PTabs &dst, int t, int nthr)
     for (int i = t; i < N; i += nthr) reinterpret_cast<uint4 *>(&dst)[i] = reinterpret_cast<const uint4 *>(&g_ptabs)[i];
 }
 
+/* RowTabs from g_ptabs, one 32-bit word per thread and step */
+__device__ inline void load_rowtabs(RowTabs &dst, int t, int nthr)
+{
+    constexpr int NC = (int)(sizeof(dst.ct) / 4), NZ = (int)(sizeof(dst.tzdc) / 4), NR = (int)(sizeof(dst.rb) / 4);
+    static_assert(sizeof(dst.ct) % 4 == 0 && sizeof(dst.tzdc) % 4 == 0 && sizeof(dst.rb) % 4 == 0, "word copies");
+    const uint32_t *ct = reinterpret_cast<const uint32_t *>(g_ptabs.ct);
+    const uint32_t *tz = reinterpret_cast<const uint32_t *>(g_ptabs.tzdc);
+    const uint32_t *rb = reinterpret_cast<const uint32_t *>(g_ptabs.rb);
+    uint32_t *dc = reinterpret_cast<uint32_t *>(dst.ct), *dz = reinterpret_cast<uint32_t *>(dst.tzdc);
+    uint32_t *dr = reinterpret_cast<uint32_t *>(dst.rb);
+    for (int i = t; i < NC + NZ + NR; i += nthr) {
+        if (i < NC) dc[i] = ct[i];
+        else if (i < NC + NZ) dz[i - NC] = tz[i - NC];
+        else dr[i - NC - NZ] = rb[i - NC - NZ];
+    }
+}
+
 
 constexpr int HEAD_MAX = 160;           /* bits of one MB head (huge mvd: 2 x 63 + ref) */
 constexpr int HDR_MAX = 1024;           /* slice header bits (8 waypoints + MMCO ~ 250) */
@@ -578,9 +595,9 @@ __device__ inline void code_frame(const DevStream *__restrict__ st,
     }
 }
 
-/* grid (chunks, CODE_GEN_Y): each workgroup finds the flagged (stream,
- * frame) pairs 64 at a time -- a launch over every frame would cost more in
- * empty workgroups than the frames it serves */
+/* grid (chunks, CODE_GEN_Y): workgroup (c, y) codes chunk c of the flagged
+ * NALs y, y + CODE_GEN_Y, ... of k_dyn_rows' list (ctr[1] of them, as
+ * k_dyn_row<true> reads it): with none flagged a launch reads one word */
 constexpr int CODE_GEN_Y = 64;
 __global__ __launch_bounds__(CODE_T) void k_dyn_code_general(const DevStream *__restrict__ st,
                                                              const DynFrame *__restrict__ dfr, int ld_fr,
@@ -590,27 +607,15 @@ __global__ __launch_bounds__(CODE_T) void k_dyn_code_general(const DevStream *__
                                                              const uint8_t *__restrict__ src,
                                                              const uint8_t *__restrict__ refs,
                                                              uint16_t *__restrict__ meta,
-                                                             uint2 *__restrict__ blo, uint2 *__restrict__ bhi, int nframes,
-                                                             int nstreams)
+                                                             uint2 *__restrict__ blo, uint2 *__restrict__ bhi,
+                                                             const uint32_t *__restrict__ ctr)
 {
-    const int lane = threadIdx.x & 63, np = nstreams * nframes;
-    for (int p0 = (int)blockIdx.y * 64; p0 < np; p0 += (int)gridDim.y * 64) {
-        bool gen = false;
-        const int p = p0 + lane;
-        if (p < np) {
-            const int s = p / nframes, f = p - s * nframes;
-            const DynFrame df = dfr[(size_t)s * ld_fr + f];
-            gen = df.nal >= 0 && (df.err & DF_GENERAL);
-        }
-        uint64_t m = __ballot(gen);                     /* the same in every wave */
-        while (m) {
-            const int q = p0 + __builtin_ctzll(m);
-            m &= m - 1;
-            const int s = q / nframes, f = q - s * nframes;
-            code_frame(st, dfr, ld_fr, pend, nal, ld_nal, g, rows, src, refs, meta, blo, bhi, s, f,
-                             blockIdx.x);
-            __syncthreads();
-        }
+    const uint32_t n = min(__builtin_amdgcn_readfirstlane(ctr[1]), g.gen_cap);
+    for (uint32_t j = blockIdx.y; j < n; j += gridDim.y) {
+        const uint32_t q = __builtin_amdgcn_readfirstlane(ctr[DYN_CTR_LIST + j]);
+        const int s = (int)(q / (uint32_t)ld_fr), f = (int)(q - (uint32_t)s * (uint32_t)ld_fr);
+        code_frame(st, dfr, ld_fr, pend, nal, ld_nal, g, rows, src, refs, meta, blo, bhi, s, f, blockIdx.x);
+        __syncthreads();
     }
 }
 
@@ -969,6 +974,17 @@ __device__ inline uint4 body_msb(uint64_t hi, uint64_t lo, uint32_t n)
     return make_uint4((uint32_t)(H >> 32), (uint32_t)H, (uint32_t)(Lw >> 32), (uint32_t)Lw);
 }
 
+/* body_msb's inverse for the MB-head classes k_dyn_row keeps MSB first
+ * (a = words 0-1, b = words 2-3): the n bits right-aligned (CapSink) */
+__device__ inline CapSink cap_of_msb(uint64_t a, uint64_t b, uint32_t n)
+{
+    if (n == 0u) return CapSink{0, 0, 0};
+    const uint32_t sh = 128u - n;
+    if (sh >= 64u) return CapSink{0, a >> (sh - 64u), n};
+    if (sh == 0u) return CapSink{a, b, n};
+    return CapSink{a >> sh, (b >> sh) | (a << (64u - sh)), n};
+}
+
 /* token (tl <= 16 bits) + MSB-first body b (bl <= 128 bits) ORed into the
  * LDS window buf = words [p0, p0 + n) at bit pos: the <= 144 bits as five
  * words shifted by tl, then six words shifted by pos mod 32 (v_alignbit);
@@ -988,6 +1004,32 @@ __device__ inline void put_piece(uint32_t *buf, uint32_t p0, uint32_t n, uint32_
 #pragma unroll
     for (uint32_t j = 0; j < 6; ++j)
         if (j < nw && w0 + j < n && o[j]) atomicOr(&buf[w0 + j], o[j]);
+}
+
+/* put_piece for a row written in one pass (the window is the row's words
+ * from 0, with ROW_PAD spare words after it): the first three words ORed
+ * whatever the piece's length (zero words past its end change nothing), the
+ * rest only for pieces that reach them -- no window tests, no per-word
+ * branches for the common pieces of <= 3 words */
+constexpr uint32_t ROW_PAD = 4;
+__device__ inline void put_piece1(uint32_t *buf, uint32_t pos, uint32_t tv, uint32_t tl, uint4 b, uint32_t bl)
+{
+    const uint32_t tw = tv & low_mask((int)tl);
+    const uint32_t c0 = __builtin_amdgcn_alignbit(tw, b.x, tl), c1 = __builtin_amdgcn_alignbit(b.x, b.y, tl);
+    const uint32_t c2 = __builtin_amdgcn_alignbit(b.y, b.z, tl), c3 = __builtin_amdgcn_alignbit(b.z, b.w, tl);
+    const uint32_t c4 = __builtin_amdgcn_alignbit(b.w, 0u, tl);
+    const uint32_t sh = pos & 31u, nw = (sh + tl + bl + 31u) >> 5;
+    uint32_t *d = buf + (pos >> 5);
+    atomicOr(d, c0 >> sh);
+    atomicOr(d + 1, __builtin_amdgcn_alignbit(c0, c1, sh));
+    atomicOr(d + 2, __builtin_amdgcn_alignbit(c1, c2, sh));
+    if (nw > 3u) {
+        atomicOr(d + 3, __builtin_amdgcn_alignbit(c2, c3, sh));
+        if (nw > 4u) {
+            atomicOr(d + 4, __builtin_amdgcn_alignbit(c3, c4, sh));
+            if (nw > 5u) atomicOr(d + 5, __builtin_amdgcn_alignbit(c4, 0u, sh));
+        }
+    }
 }
 
 /* ---------------------------------------------------------------------- */
@@ -1031,9 +1073,9 @@ constexpr int ROW_NPMAX = 8;                    /* tasks per thread at most (153
 constexpr int ROW_GB = SCROLL_ROW_GB;           /* bit window: 28 Kbit (a config-3 row ~18 Kbit, one pass) */
 
 struct RowFixed {
-    PTabs ptabs;
+    RowTabs ptabs;
     union {                                      /* the sort's counts and the level table are dead before the bit window */
-        uint32_t buf[ROW_GB];
+        uint32_t buf[ROW_GB + 4];                /* + ROW_PAD: put_piece1's spare words */
         struct {
             uint32_t kc[2][SORT_KEYS];           /* the sort: blocks per TotalCoeff class, then its base */
             uint32_t kc_pad[32 - 2 * SORT_KEYS];
@@ -1051,6 +1093,7 @@ struct RowFixed {
 };
 
 static_assert(2 * SORT_KEYS <= 32 && 32 + LVT_N <= ROW_GB, "the sort counts and the level table share the bit window");
+static_assert(ROW_PAD == 4, "RowFixed::buf holds ROW_PAD spare words");
 static_assert(offsetof(RowFixed, lvt) % 8 == 0, "the level table is copied in 8-byte words");
 
 /* dynamic LDS of k_dyn_row: lv [NPC w] uint4 (levels, then bodies), mbits
@@ -1125,36 +1168,62 @@ __device__ inline __amdgpu_buffer_rsrc_t buf_rsrc(const void *p, uint32_t n)
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), (short)0, (int)n, 0x00020000);
 }
 
-/* fs: the frame's source bytes, rb: the stream's reference pair, both as
- * buffer descriptors -- 32-bit lane offsets, the row step in the uniform
- * soffset, so a pixel row costs one load and at most one add */
-__device__ inline void row_fetch(int task, int w, int ry, const DynGeom &g, __amdgpu_buffer_rsrc_t fs,
-                                 __amdgpu_buffer_rsrc_t rb, const uint32_t *rt, uint32_t csz, BlkPix &px)
+/* A thread's block task in pass pa is pa T + t.  With T a multiple of 16
+ * (row_threads) its 4x4 position inside the MB (luma) or the chroma quad
+ * (chroma) is the same in every pass and its byte offsets advance by T per
+ * pass, luma and chroma alike (16 k and 8 k both grow by T): FetchPre holds
+ * pass 0's offsets and the row-table slots, row_fetch adds pa T */
+struct FetchPre {
+    uint32_t so_l, po_l, so_c, co_c;    /* luma source / prediction, chroma source / reference */
+    int rl, rc;                         /* rt[] rows: luma 4 by, chroma 16 + 4 by */
+};
+
+__device__ inline FetchPre fetch_pre(int t, int w, int ry, const DynGeom &g, uint32_t csz)
 {
     const int lstride = 16 * g.w, cstride = 8 * g.w, ndt = g.w * g.h;
+    FetchPre f;
+    {
+        const int r = t & 15, bx = r & 3, by = r >> 2;
+        f.so_l = (uint32_t)((16 * ry + 4 * by) * lstride + 16 * (t >> 4) + 4 * bx);
+        f.po_l = (uint32_t)(16 * (g.x0 + (t >> 4)) + 4 * bx);
+        f.rl = 4 * by;
+    }
+    {
+        const int e = t - 16 * w, k = e >> 3, p = (e >> 2) & 1, r = e & 3;   /* arithmetic shifts: e < 0 fine */
+        const int bx = r & 1, by = r >> 1;
+        f.so_c = (uint32_t)(256 * ndt + (p ? 64 * ndt : 0) + (8 * ry + 4 * by) * cstride + 8 * k + 4 * bx);
+        f.co_c = (uint32_t)p * csz + (uint32_t)(8 * (g.x0 + k) + 4 * bx);
+        f.rc = 16 + 4 * by;
+    }
+    return f;
+}
+
+/* fs: the frame's source bytes, rb: the stream's reference pair, both as
+ * buffer descriptors -- 32-bit lane offsets, the row step in the uniform
+ * soffset, so a pixel row costs one load and at most one add.  The task of
+ * pass pa (luma: task < 16 w); adv = pa T */
+__device__ inline void row_fetch(bool luma, uint32_t adv, const DynGeom &g, __amdgpu_buffer_rsrc_t fs,
+                                 __amdgpu_buffer_rsrc_t rb, const uint32_t *rt, const FetchPre &F, BlkPix &px)
+{
+    const int lstride = 16 * g.w, cstride = 8 * g.w;
     px.fr = 0;
-    if (task < 16 * w) {
-        const int k = task >> 4, r = task & 15, bx = r & 3, by = r >> 2;
-        const uint32_t so = (uint32_t)((16 * ry + 4 * by) * lstride + 16 * k + 4 * bx);
-        const uint32_t po = (uint32_t)(16 * (g.x0 + k) + 4 * bx);
+    if (luma) {
+        const uint32_t so = F.so_l + adv, po = F.po_l + adv;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             px.a[i] = __builtin_amdgcn_raw_buffer_load_b32(fs, so, i * lstride, 0);
-            px.b[i] = __builtin_amdgcn_raw_buffer_load_b32(rb, po + rt[4 * by + i], 0, 0);
+            px.b[i] = __builtin_amdgcn_raw_buffer_load_b32(rb, po + rt[F.rl + i], 0, 0);
             px.c[i] = 0;
         }
     } else {
-        const int jj = task - 16 * w, k = jj >> 3, p = (jj >> 2) & 1, r = jj & 3;
-        const int bx = r & 1, by = r >> 1;
-        const uint32_t so = (uint32_t)(256 * ndt + (p ? 64 * ndt : 0) + (8 * ry + 4 * by) * cstride + 8 * k + 4 * bx);
-        const uint32_t co = (uint32_t)p * csz + (uint32_t)(8 * (g.x0 + k) + 4 * bx);
+        const uint32_t so = F.so_c + adv, co = F.co_c + adv;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            const uint32_t ea = rt[16 + 4 * by + i];
+            const uint32_t ea = rt[F.rc + i];
             const uint32_t f = (ea >> 28) & 7u;
             px.a[i] = __builtin_amdgcn_raw_buffer_load_b32(fs, so, i * cstride, 0);
             px.b[i] = __builtin_amdgcn_raw_buffer_load_b32(rb, co + (ea & ROW_OFF), 0, 0);
-            px.c[i] = f ? __builtin_amdgcn_raw_buffer_load_b32(rb, co + (rt[24 + 4 * by + i] & ROW_OFF), 0, 0) : 0u;
+            px.c[i] = f ? __builtin_amdgcn_raw_buffer_load_b32(rb, co + (rt[F.rc + 8 + i] & ROW_OFF), 0, 0) : 0u;
             px.fr |= f << (3 * i);
         }
     }
@@ -1283,7 +1352,7 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
     }
     if (t < SORT_KEYS) L.kc[0][t] = 0u;
     if (t < NPC) L.pcd[t] = pc_desc(t);
-    load_ptabs(L.ptabs, t, T);
+    load_rowtabs(L.ptabs, t, T);
     for (int i = t; i < LVT_N / 2; i += T)      /* 8-byte aligned in LDS */
         reinterpret_cast<uint2 *>(L.lvt)[i] = reinterpret_cast<const uint2 *>(&g_lvt)[i];
     if (!general && t < 32) L.rt[t] = rows[nb * (size_t)(32 * g.h) + (t < 16 ? 16 * r + t : 16 * g.h + (t < 24 ? 8 * r + t - 16 : 8 * g.h + 8 * r + t - 24))];
@@ -1304,15 +1373,17 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
         /* counting sort on TotalCoeff class: a task's rank in its class from
          * an LDS atomic (the order inside a class does not matter), kept in
          * lo[] (phase 3's) until the class bases are known */
+        static_assert(ROW_MAXT % 16 == 0, "row_threads gives whole waves: FetchPre's per-pass step");
+        const FetchPre FP = fetch_pre(t, w, r, g, csz);
         BlkPix nx;                                      /* the next task's pixels, in flight */
         {
             const int t0 = task_of(t);
-            if (t0 >= 0) row_fetch(t0, w, r, g, fs, rb, L.rt, csz, nx);
+            if (t0 >= 0) row_fetch(t0 < 16 * w, 0u, g, fs, rb, L.rt, FP, nx);
         }
         for (int pa = 0; pa < np; ++pa) {
             const int task = task_of(pa * T + t), tn = task_of((pa + 1) * T + t);
             const BlkPix cur = nx;
-            if (tn >= 0) row_fetch(tn, w, r, g, fs, rb, L.rt, csz, nx);
+            if (tn >= 0) row_fetch(tn < 16 * w, (uint32_t)((pa + 1) * T), g, fs, rb, L.rt, FP, nx);
             uint32_t pk[4];
             int n = 0, w0 = 0;
             if (task >= 0) {
@@ -1466,11 +1537,12 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
     ROW_CUT(2);
 
     /* ---- 3: coeff_token, piece lengths ----------------------------------- */
-    if (t < 12) {
+    if (t < 12) {                                       /* the MB-head classes, MSB first (put_piece1's form) */
         CapSink hc{0, 0, 0};
         H.put_class(hc, t);
-        L.hhi[t] = hc.hi;
-        L.hlo[t] = hc.lo;
+        const uint4 m = body_msb(hc.hi, hc.lo, min(hc.n, 128u));
+        L.hhi[t] = (uint64_t)m.x << 32 | m.y;
+        L.hlo[t] = (uint64_t)m.z << 32 | m.w;
         L.hlen[t] = hc.n;
         if (hc.over()) L.head_over = 1;
     }
@@ -1601,20 +1673,48 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
         for (uint32_t i = (uint32_t)t; i < n; i += (uint32_t)T) L.buf[i] = 0u;
         __syncthreads();
         const LdsOrWin win{L.buf, p0, n};
-        /* MB heads (+ coded_block_pattern / mb_qp_delta) of every column */
+        /* MB heads (+ coded_block_pattern / mb_qp_delta) of every column:
+         * in a one-pass row the class's MSB-first bits with the tail ORed
+         * in, written as one piece */
+        const bool one = npass == 1;
         for (int col = t; col < mbw; col += T) {
             const uint32_t pos = moff[col];
-            if (pos >= 32u * (p0 + n) || moff[col + 1] <= 32u * p0) continue;
+            if (!one && (pos >= 32u * (p0 + n) || moff[col + 1] <= 32u * p0)) continue;
+            const int k = col - R.x0;
+            const bool in = k >= 0 && k < w;
+            if (one && !head_over) {
+                const int cls = H.sel(row, col);
+                const uint32_t hl = L.hlen[cls];
+                uint32_t tv = 1u, tn = 1u;                      /* coded_block_pattern ue(0) */
+                if (in) {
+                    const uint32_t x = (uint32_t)codea[k] + 1u, lz = 31u - (uint32_t)__builtin_clz(x);
+                    tv = x;
+                    tn = 2u * lz + 1u;                          /* ue(code) */
+                    if (cbpa[k]) {
+                        tv = tv << 1 | 1u;                      /* mb_qp_delta se(0) */
+                        ++tn;
+                    }
+                }
+                if (hl + tn <= 128u) {
+                    const uint64_t ha = L.hhi[cls], hb = L.hlo[cls];
+                    const uint32_t t32 = tv << (32u - tn), q = hl >> 5, r = hl & 31u;
+                    uint32_t wv[4] = {(uint32_t)(ha >> 32), (uint32_t)ha, (uint32_t)(hb >> 32), (uint32_t)hb};
+#pragma unroll
+                    for (uint32_t j = 0; j < 4; ++j)
+                        wv[j] |= (j == q ? t32 >> r : 0u) | (j == q + 1u && r ? t32 << (32u - r) : 0u);
+                    put_piece1(L.buf, pos, 0u, 0u, make_uint4(wv[0], wv[1], wv[2], wv[3]), hl + tn);
+                    continue;
+                }
+            }
             WSink sk{win, 0, 0, 0};
             sk.start(pos);
             if (!head_over) {
                 const int cls = H.sel(row, col);
-                sk.put_cap(CapSink{L.hhi[cls], L.hlo[cls], L.hlen[cls]});
+                sk.put_cap(cap_of_msb(L.hhi[cls], L.hlo[cls], L.hlen[cls]));
             } else {
                 H.put_slow(sk, row, col);
             }
-            const int k = col - R.x0;
-            if (!(k >= 0 && k < w)) {
+            if (!in) {
                 sk.put(1, 1);                           /* coded_block_pattern ue(0) */
             } else {
                 put_ue(sk, (uint32_t)codea[k]);
@@ -1622,20 +1722,22 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
             }
             sk.finish();
         }
-        /* pieces */
+        /* pieces (a row in one pass -- all of config 3's -- skips the
+         * window tests) */
         for (int i = t; i < npc; i += T) {
             const uint32_t o = off16[i];
             if (o == 0xffffu) continue;
             const int k = div_npc(i), pc = i - k * NPC;
             const uint32_t e = lo[i], mv = mt[i];
             const uint32_t pos = moff[R.x0 + k] + o;
-            if (pos >= 32u * (p0 + n) || pos + (e & LO_LEN) <= 32u * p0) continue;
+            if (!one && (pos >= 32u * (p0 + n) || pos + (e & LO_LEN) <= 32u * p0)) continue;
             const int nC = (int)(e >> 11) - 1;
             const uint4 bd = lv[i];
             if (!(mv & M_OVF)) {
                 uint32_t tv = 0, tl = 0;
                 if (nC != -1) piece_token(ctab, mv, nC, tv, tl);
-                put_piece(L.buf, p0, n, pos, tv, tl, bd, mv & 255u);
+                if (one) put_piece1(L.buf, pos, tv, tl, bd, mv & 255u);
+                else put_piece(L.buf, p0, n, pos, tv, tl, bd, mv & 255u);
             } else {
                 ovf_put(L.buf, p0, n, pos, PT, TB, bd, pc, nC);
             }
@@ -2984,7 +3086,7 @@ int dyn_launch_code(hipStream_t hs, int nframes, int S, DevStream *st, const Nal
     if (hipGetLastError() != hipSuccess) return -1;
     const int nchunk = (24 * g->w * g->h + CODE_T - 1) / CODE_T;
     hipLaunchKernelGGL(k_dyn_code_general, dim3(nchunk, CODE_GEN_Y), dim3(CODE_T), 0, hs, st, dfr, ld_fr,
-                       pend, nal, ld_nal, *g, x->rows, src, refs, x->meta, x->body_lo, x->body_hi, nframes, S);
+                       pend, nal, ld_nal, *g, x->rows, src, refs, x->meta, x->body_lo, x->body_hi, x->ctr);
     if (hipGetLastError() != hipSuccess) return -1;
     hipLaunchKernelGGL(k_dyn_row<false>, dim3(g->h, nframes, S), dim3(row_threads(g->w)),
                        row_lds_bytes(g->w, mbw), hs, st, nal, ld_nal, pend, dfr, ld_fr, *g, x->rows, src, refs,

@@ -901,7 +901,7 @@ struct ScrollBatch {
     int timed_pending = 0;
     float ms[6] = {0, 0, 0, 0, 0, 0};  /* plan, emit, dyn stage, dyn emit, dyn code, dyn pack */
     std::vector<hipEvent_t> ring;      /* NEV events per timed compose, pending */
-    std::vector<uint8_t> ring_dyn;     /* per pending compose: the dynamic-rect pipeline ran */
+    std::vector<uint8_t> ring_dyn;     /* per pending compose: 1 the dynamic-rect pipeline ran, 2 lite timing */
     int ev_dyn = 0;                    /* the same for b->ev */
     int ring_used = 0;
     double acc_ms[6] = {0, 0, 0, 0, 0, 0};
@@ -995,13 +995,23 @@ struct ScrollBatch {
 
 /* event pairs of one compose.  Dynamic rect: plan = [0,1) + [2,3), dyn
  * stage [1,2), emit [3,4), dyn emit [4,5).  Otherwise only events 0, 1, 4
- * are recorded (fewer markers between the kernels): plan [0,1), emit [1,4). */
-static void event_ms(const hipEvent_t *e, bool dyn, float out[6])
+ * are recorded (fewer markers between the kernels): plan [0,1), emit [1,4).
+ * lite (scroll_batch_enable_timing(b, 2)): only the dominant kernel's pair,
+ * dyn code [1,6) (reported as dyn stage too) or emit [1,4) -- each event
+ * record is a marker packet that holds the queue for microseconds, so the
+ * full set costs a timed step ~ 40 us of gaps between its kernels */
+static void event_ms(const hipEvent_t *e, bool dyn, bool lite, float out[6])
 {
     auto el = [&](int a, int b) {
         float v = 0.0f;
         return hipEventElapsedTime(&v, e[a], e[b]) == hipSuccess ? v : 0.0f;
     };
+    if (lite) {
+        for (int k = 0; k < 6; ++k) out[k] = 0.0f;
+        if (dyn) out[2] = out[4] = el(1, 6);
+        else out[1] = el(1, 4);
+        return;
+    }
     if (dyn) {
         out[0] = el(0, 1) + el(2, 3);
         out[1] = el(3, 4);
@@ -1238,7 +1248,7 @@ static void fold_ring(ScrollBatch *b)
 {
     for (int i = 0; i + NEV <= b->ring_used; i += NEV) {
         float m[6];
-        event_ms(&b->ring[i], b->ring_dyn[i / NEV] != 0, m);
+        event_ms(&b->ring[i], (b->ring_dyn[i / NEV] & 1) != 0, (b->ring_dyn[i / NEV] & 2) != 0, m);
         for (int k = 0; k < 6; ++k) b->acc_ms[k] += m[k];
         b->acc_n++;
     }
@@ -1277,15 +1287,20 @@ static int launch(ScrollBatch *b, int nframes, int plan_mode, int nal_max, hipSt
     }
     const bool hint = b->hint_on && plan_mode != SCROLL_PLAN_EXPLICIT;
     const bool dyn = (b->dyn_on || hint) && plan_mode != SCROLL_PLAN_EXPLICIT;   /* staged NALs */
+    const bool lite = b->timing == 2;
     auto mark = [&](int k) -> int {
         if (!b->timing || (!dyn && k != 0 && k != 1 && k != 4)) return SCROLL_OK;
+        if (lite) {                     /* the dominant kernel's pair, ring only */
+            if (k == 1 || k == (dyn ? 6 : 4)) HIPCHK(hipEventRecord(rev[k], hs));
+            return SCROLL_OK;
+        }
         HIPCHK(hipEventRecord(b->ev[k], hs));
         HIPCHK(hipEventRecord(rev[k], hs));
         return SCROLL_OK;
     };
     if (b->timing) {
-        b->ring_dyn[(b->ring_used - NEV) / NEV] = dyn ? 1 : 0;
-        b->ev_dyn = dyn ? 1 : 0;
+        b->ring_dyn[(b->ring_used - NEV) / NEV] = (uint8_t)((dyn ? 1 : 0) | (lite ? 2 : 0));
+        if (!lite) b->ev_dyn = dyn ? 1 : 0;
     }
     const int ld_fr = b->max_frames;
     int rc = mark(0);
@@ -1436,7 +1451,7 @@ static int launch(ScrollBatch *b, int nframes, int plan_mode, int nal_max, hipSt
         return SCROLL_ERR_HIP;
     }
     if ((rc = mark(5))) return rc;
-    if (b->timing) b->timed_pending = 1;
+    if (b->timing == 1) b->timed_pending = 1;
     b->host_valid = 0;
     b->nal_cache_valid = 0;
     b->last = hs;
@@ -1501,7 +1516,7 @@ int scroll_batch_sync(ScrollBatch *b)
         if (rc0) return rc0;
     }
     if (b->timed_pending) {
-        event_ms(b->ev, b->ev_dyn != 0, b->ms);
+        event_ms(b->ev, b->ev_dyn != 0, false, b->ms);
         b->timed_pending = 0;
     }
     int rc = SCROLL_OK;
@@ -3089,7 +3104,7 @@ float scroll_batch_kernel_ms(ScrollBatch *b, int which)
     if (!b || which < 0 || which > 5) return -1.0f;
     if (batch_host_sync(b)) return -1.0f;
     if (b->timed_pending) {
-        event_ms(b->ev, b->ev_dyn != 0, b->ms);
+        event_ms(b->ev, b->ev_dyn != 0, false, b->ms);
         b->timed_pending = 0;
     }
     return b->ms[which];

@@ -462,8 +462,11 @@ class Batch:
             out.append((k.value, o.value, sz.value, sl.value))
         return out
 
-    def enable_timing(self, on=True):
-        self._chk(lib.scroll_batch_enable_timing(self.h, 1 if on else 0), "enable_timing")
+    def enable_timing(self, on=True, lite=False):
+        """HIP-event timing of the composes that follow: every kernel pair, or
+        (lite) only the dominant kernel's -- dyn code or emit -- with fewer
+        event markers between the kernels (scroll_batch_enable_timing)."""
+        self._chk(lib.scroll_batch_enable_timing(self.h, (2 if lite else 1) if on else 0), "enable_timing")
 
     def kernel_ms(self, which):
         return lib.scroll_batch_kernel_ms(self.h, which)

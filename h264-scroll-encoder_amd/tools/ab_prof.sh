@@ -8,10 +8,12 @@ O=$1; shift
 mkdir -p "$O"
 export TMPDIR=/tmp
 W=${AB_WORKLOAD:-p720dyn}
+V=--no-verify
+[ "${AB_VERIFY:-0}" = 1 ] && V=""                  # the bench's post-timing check of every stream
 for rep in 1 2; do
     for v in "$@" cur; do
         if [ "$v" = cur ]; then L=""; else L=variants/$v/libh264scroll.so; fi
-        H264SCROLL_LIB=$L timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/${v}_$rep" -o run -- python3 bench.py --steps 20 --warmup 3 --no-cpu --no-host --no-verify --workload $W > "$O/bench_${v}_$rep.json" 2> "$O/bench_${v}_$rep.err"
+        H264SCROLL_LIB=$L timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/${v}_$rep" -o run -- python3 bench.py --steps 20 --warmup 3 --no-cpu --no-host $V --workload $W > "$O/bench_${v}_$rep.json" 2> "$O/bench_${v}_$rep.err"
     done
 done
 echo done > "$O/DONE"

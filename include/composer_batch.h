@@ -144,7 +144,11 @@ int scroll_batch_nal_info(ScrollBatch *b, int s, int i, int *kind, int *offset_p
 /* HIP-event timing of the last compose's kernels, on the launch stream:
  * which 0 = plan kernel(s), 1 = emit kernel, 2 = dyn stage, 3 = dyn emit,
  * 4 = dyn code (k_dyn_rows + k_dyn_code), 5 = dyn pack (k_dyn_group + k_dyn_ep).
- * Enable before compose. */
+ * Enable before compose: on = 1 every pair (kernel_ms and kernel_stats_ex
+ * complete); on = 2 ("lite") only the dominant kernel's pair -- dyn code
+ * (also reported as dyn stage) or emit -- into kernel_stats_ex, the others
+ * 0: each event record is a marker packet that holds the queue between the
+ * kernels, so a timed step with every pair runs ~ 40 us longer; 0 off. */
 int scroll_batch_enable_timing(ScrollBatch *b, int on);
 float scroll_batch_kernel_ms(ScrollBatch *b, int which);
 /* all timed composes since the last call: summed plan / emit kernel ms and

@@ -439,3 +439,40 @@ def test_dyn_qp_not_with_hints(gpu, scroll):
     with pytest.raises(Exception):
         b.set_dyn_qp(30)
     b.close()
+
+
+def test_dyn_lite_timing_bytes_and_pairs(gpu, oracle):
+    """scroll_batch_enable_timing(b, 2): only the dominant kernel's event
+    pair (dyn code, also reported as dyn stage) is recorded; the composed
+    bytes are the same as with full timing and with none"""
+    w, h = 128, 256
+    rect = Rect(2, 3, 4, 6)
+    S, F = 4, 6
+    offs = synthetic_offsets(S, F, h)
+    R = striped_refs(oracle, w, h)
+    src = synth_source(oracle, S, F, rect)
+    want = oracle_streams(oracle, w, h, offs, rect, src, R)
+    for mode in (0, 1, 2):
+        b = gpu.Batch(S, F, 8 << 20)
+        for _ in range(S):
+            b.add_stream(gpu.make_config(w, h))
+        b.set_dyn_rect(rect.x0, rect.y0, rect.w, rect.h, 0)
+        b.set_dyn_refs(R.i420(0), R.i420(1))
+        b.set_offsets(np.ascontiguousarray(offs))
+        b.set_dyn_source(np.ascontiguousarray(src).tobytes(), F)
+        if mode:
+            b.enable_timing(True, lite=mode == 2)
+            b.kernel_stats_ex()
+        b.compose(F)
+        assert b.sync() == 0, gpu.last_error()
+        check_equal(b, want)
+        if mode:
+            ms, n = b.kernel_stats_ex()
+            assert n == 1
+            plan, emit, stage, demit, code, pack = ms
+            assert code > 0 and stage > 0
+            if mode == 2:
+                assert plan == 0 and emit == 0 and demit == 0 and pack == 0 and stage == code
+            else:
+                assert plan > 0 and demit > 0
+        b.close()

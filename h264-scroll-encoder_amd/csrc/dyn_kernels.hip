@@ -1567,7 +1567,21 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
         const uint32_t tl = nC < 0 ? 0u : (nC >= 8 ? 6u : ce >> 8);
         uint32_t len = tl + (mv & 255u);
         if (mv & M_OVF) len = ovf_bits(PT, TB, lv[i], pc, nC);            /* rare */
-        lo[i] = (uint16_t)(len | (uint32_t)(nC + 1) << 11);
+        uint32_t nc1 = (uint32_t)(nC + 1);
+        if (!(mv & M_OVF) && nC >= 0 && len <= 128u) {
+            /* the token goes in front of the body here, where its code is
+             * at hand: the piece is then a bare MSB-first body of len bits
+             * (nC field 0, as a chroma DC piece), and phase 5 writes it
+             * without looking the token up again */
+            const uint32_t tv = nC >= 8 ? (tc ? (uint32_t)(((tc - 1) << 2) | t1) : 3u) : (ce & 255u);
+            const uint32_t tw = tv & low_mask((int)tl);
+            const uint4 b = lv[i];
+            lv[i] = make_uint4(__builtin_amdgcn_alignbit(tw, b.x, tl), __builtin_amdgcn_alignbit(b.x, b.y, tl),
+                               __builtin_amdgcn_alignbit(b.y, b.z, tl), __builtin_amdgcn_alignbit(b.z, b.w, tl));
+            mt[i] = (uint16_t)((mv & ~255u) | len);                 /* tc / t1 bits unchanged */
+            nc1 = 0u;
+        }
+        lo[i] = (uint16_t)(len | nc1 << 11);
     }
     __syncthreads();
     if (stamps) stv[3] = __builtin_amdgcn_s_memrealtime();
@@ -1734,10 +1748,15 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
             const int nC = (int)(e >> 11) - 1;
             const uint4 bd = lv[i];
             if (!(mv & M_OVF)) {
-                uint32_t tv = 0, tl = 0;
-                if (nC != -1) piece_token(ctab, mv, nC, tv, tl);
-                if (one) put_piece1(L.buf, pos, tv, tl, bd, mv & 255u);
-                else put_piece(L.buf, p0, n, pos, tv, tl, bd, mv & 255u);
+                if (nC == -1) {                         /* a bare body (token in front since phase 3) */
+                    if (one) put_piece1(L.buf, pos, 0u, 0u, bd, mv & 255u);
+                    else put_piece(L.buf, p0, n, pos, 0u, 0u, bd, mv & 255u);
+                } else {                                /* bodies over 128 - tl bits */
+                    uint32_t tv = 0, tl = 0;
+                    piece_token(ctab, mv, nC, tv, tl);
+                    if (one) put_piece1(L.buf, pos, tv, tl, bd, mv & 255u);
+                    else put_piece(L.buf, p0, n, pos, tv, tl, bd, mv & 255u);
+                }
             } else {
                 ovf_put(L.buf, p0, n, pos, PT, TB, bd, pc, nC);
             }

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """dyn_stamps.py -- profiling aid: where k_dyn_row's time goes.
 
-Runs the bench's config-3 workload (bench.py p720dyn) once with
+Runs a dynamic-rect workload of the bench (default p720dyn = config 3) once with
 SCROLL_DEBUG_DYN_STAMPS and prints, per k_dyn_row workgroup (one rect row),
 the s_memrealtime span (100 MHz, microseconds) of each phase:
   levels       pixels -> residual -> transform -> quant, TotalCoeff ranks
@@ -12,7 +12,7 @@ the s_memrealtime span (100 MHz, microseconds) of each phase:
 plus the k_dyn_epfix steps and the k_dyn_gather workgroup spans.  Then times the workload
 without stamps (HIP events).
 
-    python h264-scroll-encoder_amd/tools/dyn_stamps.py [--streams 256 --frames 16]
+    python h264-scroll-encoder_amd/tools/dyn_stamps.py [--workload p4kdyn]
 """
 import argparse
 import ctypes
@@ -27,26 +27,17 @@ sys.path.insert(0, ROOT)
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--streams", type=int, default=256)
-    ap.add_argument("--frames", type=int, default=16)
+    ap.add_argument("--workload", default="p720dyn", help="a dynamic-rect workload of bench.py")
     ap.add_argument("--reps", type=int, default=5)
     args = ap.parse_args()
     import numpy as np
     import h264scroll as hs
     import bench
 
-    wl = bench.WORKLOADS["p720dyn"]
+    wl = bench.WORKLOADS[args.workload]
     W, H, rect = wl["w"], wl["h"], wl["rect"]
-    S, F = args.streams, args.frames
-    b = hs.Batch(S, F, F * (2 * (64 + 3600) + 192 * 625) + (1 << 20))
-    for _ in range(S):
-        b.add_stream(hs.make_config(W, H))
-    b.set_offsets(bench.synthetic_offsets(0, S, F, H))
-    b.set_dyn_rect(*rect)
-    ra, rb = bench.striped_i420(W, H, 0), bench.striped_i420(W, H, 1)
-    for s in range(S):
-        b.set_dyn_refs(ra, rb, stream=s)
-    b.dyn_source_synth(F)
+    S, F = wl["streams"], wl["frames"]
+    b = bench.build_compose_batch(hs, wl, 0, 0)         # the benched batch
     b.compose(F, rewind=True)
     assert b.sync() == 0, hs.last_error()
 

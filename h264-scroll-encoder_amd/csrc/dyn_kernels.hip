@@ -788,6 +788,23 @@ __device__ __attribute__((noinline)) void ovf_put(uint32_t *buf, uint32_t lo, ui
     sk.finish();
 }
 
+/* a block body of n <= 128 bits held right-aligned in hi:lo -> four words,
+ * MSB first, left-aligned (k_dyn_row's LDS form: the piece writer then
+ * needs only funnel shifts by the token length and the bit position) */
+__device__ inline uint4 body_msb(uint64_t hi, uint64_t lo, uint32_t n)
+{
+    const uint32_t k = 128u - n;
+    uint64_t H, Lw;
+    if (k >= 64u) {
+        H = k >= 128u ? 0ull : lo << (k - 64u);
+        Lw = 0ull;
+    } else {
+        H = k ? (hi << k) | (lo >> (64u - k)) : hi;
+        Lw = lo << k;
+    }
+    return make_uint4((uint32_t)(H >> 32), (uint32_t)H, (uint32_t)(Lw >> 32), (uint32_t)Lw);
+}
+
 /* ---------------------------------------------------------------------- */
 /* k_dyn_static: the static row groups of a dynamic NAL                    */
 /* ---------------------------------------------------------------------- */
@@ -805,10 +822,15 @@ constexpr int GW = 64;
 #endif
 constexpr int GBUF_WORDS = SCROLL_GBUF_WORDS;   /* 8 Kbit per pass */
 
+#ifndef SCROLL_STATIC_WORDS
+#define SCROLL_STATIC_WORDS 1       /* static rows word by word from the head patterns (0: MB by MB) */
+#endif
+
 struct StaticFixed {
     uint32_t ncand;
     uint32_t buf[GBUF_WORDS];
     uint64_t hhi[12], hlo[12];
+    uint4 pat[12];                  /* head class + coded_block_pattern '1', MSB first (hlen + 1 <= 128) */
     uint32_t hlen[12];
     int32_t head_over;
     int32_t wo[8], wl[8], wv[8];
@@ -869,6 +891,12 @@ __global__ __launch_bounds__(GW) void k_dyn_static(const DevStream *__restrict__
         L.hlo[t] = hc.lo;
         L.hlen[t] = hc.n;
         if (hc.over()) L.head_over = 1;
+        if (hc.n < 128u) {                              /* the class's bits and the cbp '1' */
+            const uint64_t hi = (hc.hi << 1) | (hc.lo >> 63), lo = (hc.lo << 1) | 1u;
+            L.pat[t] = body_msb(hi, lo, hc.n + 1u);
+        } else {
+            L.head_over = 1;                            /* (the word path needs patterns of <= 128 bits) */
+        }
     }
     wave_sync();
     const bool head_over = L.head_over;
@@ -914,11 +942,79 @@ __global__ __launch_bounds__(GW) void k_dyn_static(const DevStream *__restrict__
         for (uint32_t i = (uint32_t)t; i < n; i += GW) L.buf[i] = 0u;
         wave_sync();
         const LdsOrWin win{L.buf, p0, n};
-        if (first && t == 0 && p0 * 32u < F) {          /* slice header, h264_writer.c:549-553 */
+        if (!(SCROLL_STATIC_WORDS && !head_over) && first && t == 0 && p0 * 32u < F) {   /* slice header, h264_writer.c:549-553 */
             WSink hs{win, 0, 0, 0};
             hs.start(0);
             emit_slice_header(hs, c);
             hs.finish();
+        }
+        if (SCROLL_STATIC_WORDS && !head_over) {
+            /* word by word: a static row is its first column's head, mbw - 2
+             * copies of the middle class's, the last column's (each with the
+             * cbp '1': the patterns); a lane builds whole words of the window
+             * from the patterns the word's bits fall in (plain stores; the
+             * slice header and the stop bit are ORed in after) */
+            const uint32_t rbeg = L.moff[0], rend = L.moff[ne];
+            for (uint32_t i = (uint32_t)t; i < n; i += GW) {
+                const uint32_t W0 = 32u * (p0 + i), W1 = W0 + 32u;
+                uint32_t acc = 0, b = max(W0, rbeg), R0 = 0, R1 = 0, L0 = 0, Lm = 1;
+                int b3 = 0;
+                float inv = 1.0f;
+                while (b < W1 && b < rend) {
+                    if (b >= R1 || b < R0) {                    /* the row holding bit b */
+                        const int e = cnt_le(b) - 1;
+                        R0 = L.moff[e];
+                        R1 = L.moff[e + 1];
+                        b3 = H.sel(ra + e, 0);
+                        L0 = L.hlen[b3] + 1u;
+                        Lm = L.hlen[b3 + 1] + 1u;
+                        inv = 1.0f / (float)Lm;
+                    }
+                    const uint32_t o = b - R0;
+                    uint32_t cl = (uint32_t)b3, off = o;
+                    if (o >= L0) {
+                        const uint32_t o2 = o - L0;
+                        uint32_t q = (uint32_t)((float)o2 * inv);   /* o2 < 2^24: off by at most one */
+                        if (q * Lm > o2) --q;
+                        else if ((q + 1u) * Lm <= o2) ++q;
+                        if (q < (uint32_t)(mbw - 2)) {
+                            cl = (uint32_t)b3 + 1u;
+                            off = o2 - q * Lm;
+                        } else {
+                            cl = (uint32_t)b3 + 2u;
+                            off = o2 - (uint32_t)(mbw - 2) * Lm;
+                        }
+                    }
+                    const uint32_t k = min(L.hlen[cl] + 1u - off, W1 - b);
+                    const uint4 P = L.pat[cl];
+                    const uint32_t wi = off >> 5, sh = off & 31u;
+                    const uint32_t w0 = wi == 0 ? P.x : (wi == 1 ? P.y : (wi == 2 ? P.z : P.w));
+                    const uint32_t w1 = wi == 0 ? P.y : (wi == 1 ? P.z : (wi == 2 ? P.w : 0u));
+                    uint32_t v = sh ? __builtin_amdgcn_alignbit(w0, w1, 32u - sh) : w0;
+                    v &= k >= 32u ? 0xffffffffu : ~(0xffffffffu >> k);
+                    acc |= v >> (b - W0);
+                    b += k;
+                }
+                L.buf[i] = acc;
+            }
+            wave_sync();
+            if (first && t == 0 && p0 * 32u < F) {      /* slice header, h264_writer.c:549-553 */
+                WSink hs{win, 0, 0, 0};
+                hs.start(0);
+                emit_slice_header(hs, c);
+                hs.finish();
+            }
+            if (last && t == 0) {                       /* rbsp_stop_one_bit */
+                WSink sk{win, 0, 0, 0};
+                sk.start(bits - 1u);
+                sk.put(1, 1);
+                sk.finish();
+            }
+            wave_sync();
+            flush_window(L.buf, n, p0, p0 + n >= nw, out, &L.ncand,
+                         rowstage + nb * g.rs_frame_words + rs_runs_words(g, nA, gi), EPC_STATIC - 1, t, GW);
+            wave_sync();
+            continue;
         }
         /* the rows whose bits meet the window: [ea, eb) */
         const int ea = max(cnt_le(32u * p0) - 1, 0), eb = min(cnt_le(32u * (p0 + n) - 1u), ne);
@@ -957,22 +1053,6 @@ __global__ __launch_bounds__(GW) void k_dyn_static(const DevStream *__restrict__
     if (t == 0) rowstage[nb * g.rs_frame_words + rs_runs_words(g, nA, gi)] = L.ncand;
 }
 
-/* a block body of n <= 128 bits held right-aligned in hi:lo -> four words,
- * MSB first, left-aligned (k_dyn_row's LDS form: the piece writer then
- * needs only funnel shifts by the token length and the bit position) */
-__device__ inline uint4 body_msb(uint64_t hi, uint64_t lo, uint32_t n)
-{
-    const uint32_t k = 128u - n;
-    uint64_t H, Lw;
-    if (k >= 64u) {
-        H = k >= 128u ? 0ull : lo << (k - 64u);
-        Lw = 0ull;
-    } else {
-        H = k ? (hi << k) | (lo >> (64u - k)) : hi;
-        Lw = lo << k;
-    }
-    return make_uint4((uint32_t)(H >> 32), (uint32_t)H, (uint32_t)(Lw >> 32), (uint32_t)Lw);
-}
 
 /* body_msb's inverse for the MB-head classes k_dyn_row keeps MSB first
  * (a = words 0-1, b = words 2-3): the n bits right-aligned (CapSink) */

@@ -2316,6 +2316,64 @@ __device__ inline int cand_group(uint32_t i, int ng, const uint32_t *cbase)
     return lo;
 }
 
+/* ep_fix's list mode (NALs over 32 LCAP bytes) for lists of n <= LCAP -
+ * 4 NT entries: the NAL's bytes in windows of the LDS after the list (HW
+ * words from the first multiple of 4 NT past n); per window every thread
+ * sets the bits of the listed positions lst[0, n) that fall in it, then the
+ * window's compaction emits them in order into eplist (duplicates merged)
+ * -- no sort.  (Measured in round 4: a bitonic sort of the list took 22 us
+ * per config-5 NAL on average, 119 at p99.)  Returns the positions emitted */
+template <int NT, int LCAP>
+__device__ __attribute__((always_inline)) inline uint32_t ep_list_windows(uint32_t *lst, uint32_t n, uint32_t nin,
+                                                                          uint32_t *eplist, uint32_t *ws, int t,
+                                                                          int lane, int wave)
+{
+    const uint32_t ws0 = (n + 4u * NT - 1u) / (4u * NT) * (4u * NT);
+    const uint32_t HW = (uint32_t)LCAP - ws0, CH = HW / (uint32_t)NT;   /* multiples of 4 NT / 4 */
+    uint32_t *win = lst + ws0;
+    const uint4 *wv = reinterpret_cast<const uint4 *>(win) + (uint32_t)t * (CH / 4u);
+    uint32_t base = 0;
+    for (uint32_t w0 = 0; w0 < nin; w0 += 32u * HW) {
+        for (uint32_t i = (uint32_t)t; i < HW / 4u; i += (uint32_t)NT)
+            reinterpret_cast<uint4 *>(win)[i] = make_uint4(0u, 0u, 0u, 0u);
+        __syncthreads();
+        for (uint32_t i = (uint32_t)t; i < n; i += (uint32_t)NT) {
+            const uint32_t v = lst[i] - w0;
+            if (v < 32u * HW) atomicOr(&win[v >> 5], 1u << (v & 31u));
+        }
+        __syncthreads();
+        uint32_t mine = 0;
+        for (uint32_t k = 0; k < CH / 4u; ++k) {
+            const uint4 q = wv[k];
+            mine += (uint32_t)(__builtin_popcount(q.x) + __builtin_popcount(q.y) + __builtin_popcount(q.z) +
+                               __builtin_popcount(q.w));
+        }
+        const uint32_t incl = wave_incl_sum(mine, lane);
+        if (lane == 63) ws[wave] = incl;
+        __syncthreads();
+        uint32_t ex = base, tot = 0;
+        for (int q = 0; q < NT / 64; ++q) {
+            if (q < wave) ex += ws[q];
+            tot += ws[q];
+        }
+        ex += incl - mine;
+        for (uint32_t k = 0; mine && k < CH / 4u; ++k) {
+            const uint4 q = wv[k];
+            const uint32_t wv4[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+                for (uint32_t m = wv4[e]; m; m &= m - 1u) {
+                    if (ex < (uint32_t)EPLIST_MAX)
+                        eplist[ex] = w0 + 32u * ((uint32_t)t * CH + 4u * k + (uint32_t)e) + (uint32_t)__builtin_ctz(m);
+                    ++ex;
+                }
+        }
+        base += tot;
+        __syncthreads();                                /* the window and ws are reused */
+    }
+    return base;
+}
+
 /* k_dyn_epfix's work for NAL nb (stream s), every thread of the workgroup
  * (NT of them, at least two waves) calling: size, EP positions sorted and
  * each once into the frame's EP list (EPLIST_MAX kept), DF_FIXED set.  The
@@ -2336,7 +2394,7 @@ __device__ inline void ep_fix(DevStream *st, DynFrame *DF, size_t nb, int s, con
                               int t, uint32_t *slow_n, uint32_t *slow_list, uint64_t *stp)
 {
     static_assert(NT >= 128 && NT % 64 == 0, "ep_fix: one seam wave and at least one candidate wave");
-    static_assert(LCAP % (4 * NT) == 0, "ep_fix: the bitmap in whole 16-byte chunks per thread");
+    static_assert(LCAP % (4 * NT) == 0 && LCAP >= 8 * NT, "ep_fix: the bitmap in whole 16-byte chunks per thread");
     /* stp (debug, SCROLL_DEBUG_DYN_STAMPS): realtime at entry and after each
      * step (tools/dyn_stamps.py) */
     auto stamp = [&](int k) {
@@ -2482,11 +2540,18 @@ __device__ inline void ep_fix(DevStream *st, DynFrame *DF, size_t nb, int s, con
         }
         return;
     }
-    if (!bm) {
-        /* list mode (NALs over 32 lcap bytes): a bitonic sort of the list
+    uint32_t *eplist = reinterpret_cast<uint32_t *>(eps + nb * DYN_OVF_BYTES);
+    constexpr int CW = LCAP / NT;                       /* bitmap words per thread (whole bitmap) */
+    if (!bm && n <= lcap - 4u * NT) {
+        const uint32_t base = ep_list_windows<NT, LCAP>(lst, n, nin, eplist, E.ws, t, lane, wave);
+        stamp(3);
+        if (t == 0) nu = base;
+    } else if (!bm) {
+        /* a list too long to leave a window: a bitonic sort of the list
          * padded to a power of two (log^2 steps, one compare-exchange per
-         * thread and step) */
-        const uint32_t P = n <= 1u ? 1u : 1u << (32 - __builtin_clz(n - 1u));   /* <= lcap (n <= lcap) */
+         * thread and step), then the first of each run of equal positions
+         * goes to its rank */
+        const uint32_t P = n <= 1u ? 1u : 1u << (32 - __builtin_clz(n - 1u));   /* <= lcap */
         for (uint32_t i = (uint32_t)t + n; i < P; i += (uint32_t)NT) lst[i] = 0xffffffffu;
         __syncthreads();
         for (uint32_t k = 2; k <= P; k <<= 1)
@@ -2503,37 +2568,43 @@ __device__ inline void ep_fix(DevStream *st, DynFrame *DF, size_t nb, int s, con
                 }
                 __syncthreads();
             }
-    }
-    stamp(3);
-    /* compaction: the threads' contiguous chunks (bitmap words -- CW each,
-     * held in registers -- or sorted list entries whose value differs from
-     * the one before), a scan, then each chunk's positions in order from its
-     * rank */
-    constexpr int CW = LCAP / NT;
-    uint4 bw[CW / 4];
-    const uint32_t C = bm ? 0u : (n + (uint32_t)NT - 1u) / (uint32_t)NT, c0 = (uint32_t)t * C, c1 = min(c0 + C, n);
-    uint32_t mine = 0;
-    if (bm) {
-#pragma unroll
-        for (int k = 0; k < CW / 4; ++k) {
-            bw[k] = reinterpret_cast<const uint4 *>(lst)[t * (CW / 4) + k];
-            mine += (uint32_t)(__builtin_popcount(bw[k].x) + __builtin_popcount(bw[k].y) +
-                               __builtin_popcount(bw[k].z) + __builtin_popcount(bw[k].w));
-        }
-    } else {
+        stamp(3);
+        const uint32_t C = (n + (uint32_t)NT - 1u) / (uint32_t)NT, c0 = (uint32_t)t * C, c1 = min(c0 + C, n);
+        uint32_t mine = 0;
         for (uint32_t i = c0; i < c1; ++i) mine += (i == 0u || lst[i] != lst[i - 1u]) ? 1u : 0u;
-    }
-    uint32_t ex = 0;
-    {
+        uint32_t ex = 0;
         const uint32_t incl = wave_incl_sum(mine, lane);
         if (lane == 63) E.ws[wave] = incl;
         __syncthreads();
         for (int q = 0; q < wave; ++q) ex += E.ws[q];
         ex += incl - mine;
         if (t == NT - 1) nu = ex + mine;
-    }
-    uint32_t *eplist = reinterpret_cast<uint32_t *>(eps + nb * DYN_OVF_BYTES);
-    if (bm) {
+        for (uint32_t i = c0; i < c1; ++i)
+            if (i == 0u || lst[i] != lst[i - 1u]) {
+                if (ex < (uint32_t)EPLIST_MAX) eplist[ex] = lst[i];
+                ++ex;
+            }
+    } else {
+        stamp(3);
+        /* bitmap mode: the threads' CW words held in registers, a scan,
+         * then each chunk's positions in order from its rank */
+        uint4 bw[CW / 4];
+        uint32_t mine = 0;
+#pragma unroll
+        for (int k = 0; k < CW / 4; ++k) {
+            bw[k] = reinterpret_cast<const uint4 *>(lst)[t * (CW / 4) + k];
+            mine += (uint32_t)(__builtin_popcount(bw[k].x) + __builtin_popcount(bw[k].y) +
+                               __builtin_popcount(bw[k].z) + __builtin_popcount(bw[k].w));
+        }
+        uint32_t ex = 0;
+        {
+            const uint32_t incl = wave_incl_sum(mine, lane);
+            if (lane == 63) E.ws[wave] = incl;
+            __syncthreads();
+            for (int q = 0; q < wave; ++q) ex += E.ws[q];
+            ex += incl - mine;
+            if (t == NT - 1) nu = ex + mine;
+        }
         if (mine) {
 #pragma unroll
             for (int k = 0; k < CW / 4; ++k) {
@@ -2547,12 +2618,6 @@ __device__ inline void ep_fix(DevStream *st, DynFrame *DF, size_t nb, int s, con
                     }
             }
         }
-    } else {
-        for (uint32_t i = c0; i < c1; ++i)
-            if (i == 0u || lst[i] != lst[i - 1u]) {
-                if (ex < (uint32_t)EPLIST_MAX) eplist[ex] = lst[i];
-                ++ex;
-            }
     }
     __syncthreads();
     if (t == 0) {

@@ -96,6 +96,7 @@ constexpr uint32_t DF_OVER = 1u, DF_GENERAL = 2u, DF_HANDOFF = 4u;
  * dispatched first and publishes within microseconds; the bound only turns a
  * broken hand-off into a failed stream instead of a GPU hang */
 constexpr uint64_t HANDOFF_TICKS = 5000000ull;
+constexpr uint64_t HANDOFF_GAP = 100000ull;     /* 1 ms: a longer gap between two polls is a preemption */
 /* k_dyn_epfix could not settle the NAL's EP positions from the candidates
  * (too many): k_dyn_epscan scans it whole; not an error for the emit */
 constexpr uint32_t DF_EPSLOW = 0x100u;
@@ -1588,7 +1589,11 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
      * bounded: past HANDOFF_TICKS the frame fails (DF_HANDOFF) and the row
      * finishes on zeros, so a missing granule costs one stream, not the GPU */
     if (!general && wave == nwv - 1) {
-        const uint64_t t0 = r > 0 ? __builtin_amdgcn_s_memrealtime() : 0ull;
+        /* waited time = the sum of the gaps between consecutive polls, a gap
+         * over HANDOFF_GAP (the queue preempted or time-sliced: the row above
+         * was paused too) not counted -- a slow-but-alive row above never
+         * fails the stream on a shared GPU */
+        uint64_t prev = r > 0 ? __builtin_amdgcn_s_memrealtime() : 0ull, waited = 0;
         bool late = false;
         for (int k = lane; k < w; k += 64) {
             uint64_t v = 0;
@@ -1597,7 +1602,10 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
                 for (;;) {
                     v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     if ((uint32_t)(v >> 40) == (epoch & 0xffffffu)) break;
-                    if (__builtin_amdgcn_s_memrealtime() - t0 > HANDOFF_TICKS) {
+                    const uint64_t now = __builtin_amdgcn_s_memrealtime(), gap = now - prev;
+                    prev = now;
+                    if (gap < HANDOFF_GAP) waited += gap;
+                    if (waited > HANDOFF_TICKS) {
                         v = 0;
                         late = true;
                         break;

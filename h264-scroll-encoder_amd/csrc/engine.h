@@ -87,9 +87,6 @@ typedef struct {
 #define DYN_MAX_H 48                /* rect height limit (MBs)                    */
 #define DYN_MAX_MBW 512             /* picture width limit with the rect (MBs)   */
 #define DYN_MAX_MBH 512             /* picture height limit with the rect (MBs)  */
-#ifndef DYN_PIPE_CHUNKS
-#define DYN_PIPE_CHUNKS 1           /* stream chunks of the code / group pipeline (2, 4, 8 measured slower) */
-#endif
 #define DYN_STATIC_ROWS 64          /* MB rows per static k_dyn_group row group (4 measured slower) */
 #define DYN_PIECES 26               /* coded pieces per dynamic MB: 16 luma, 2 DC, 8 AC */
 #define DYN_OVF_BYTES 8192          /* staging-slot tail: levels of > 128-bit blocks */

@@ -973,8 +973,6 @@ struct ScrollBatch {
     void *d_ing_work = nullptr;                 /* segmented ingest scratch */
     size_t ing_work_bytes = 0;
     hipEvent_t ing_ev[2] = {};         /* timing: around the ingest kernels */
-    hipStream_t pipe = nullptr;        /* dynamic coder: k_dyn_group chunks beside the code chain */
-    hipEvent_t pipe_ev[DYN_PIPE_CHUNKS + 1] = {};
     /* reference files from pictures: EP count per chunk */
     uint32_t *d_ipcm_cnt = nullptr;
     size_t ipcm_cap = 0;
@@ -1107,10 +1105,6 @@ void scroll_batch_destroy(ScrollBatch *b)
         if (b->ev[i]) (void)hipEventDestroy(b->ev[i]);
     for (hipEvent_t e : b->ring) (void)hipEventDestroy(e);
     if (b->own) (void)hipStreamDestroy(b->own);
-    if (b->pipe) (void)hipStreamSynchronize(b->pipe);
-    for (hipEvent_t e : b->pipe_ev)
-        if (e) (void)hipEventDestroy(e);
-    if (b->pipe) (void)hipStreamDestroy(b->pipe);
     (void)hipFree(b->d_st);
     (void)hipHostFree(b->h_st);
     (void)hipFree(b->d_off);
@@ -1363,57 +1357,22 @@ static int launch(ScrollBatch *b, int nframes, int plan_mode, int nal_max, hipSt
             if ((rc = mark(6))) return rc;
         } else {
             b->dx.epoch = b->dx.epoch % 0xffffffu + 1u;    /* look-back epoch, never 0 */
-            /* Pipeline over stream chunks: the block coder (issue-bound) runs
-             * chunk after chunk on hs while k_dyn_group + k_dyn_ep (latency-
-             * bound) of the chunks already coded run beside it on b->pipe.
-             * A chunk is the same kernels on a contiguous stream range,
-             * given pointers offset to its first stream. */
-            const int nch = stamps ? 1 : (S < DYN_PIPE_CHUNKS ? S : DYN_PIPE_CHUNKS);
-            if (nch > 1 && !b->pipe) {
-                HIPCHK(hipStreamCreateWithFlags(&b->pipe, hipStreamNonBlocking));
-                for (hipEvent_t &e : b->pipe_ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-            }
+            /* (a pipeline over stream chunks, the coder of one chunk beside the
+             * packing of the one before on a second HIP stream, measured slower
+             * at 2 / 4 / 8 chunks: DESIGN.md §6; the device-side frame lists
+             * are batch-wide, so the launches below cover the whole batch) */
             const DynGeom &G = b->geo;
-            const size_t nalw = (size_t)G.w * G.h, ng = (size_t)G.ngroups;
             HIPCHK(hipMemsetAsync(b->dx.ctr, 0, DYN_CTR_LIST * sizeof(uint32_t), hs));   /* spill / record slots, epscan list */
-            for (int c = 0; c < nch; ++c) {
-                const int s0 = (int)((int64_t)S * c / nch), s1 = (int)((int64_t)S * (c + 1) / nch);
-                const size_t nb0 = (size_t)s0 * ld_fr;
-                DynScratch xc = b->dx;
-                xc.rows = b->dx.rows + nb0 * 32 * G.h;
-                xc.tcx = b->dx.tcx + nb0 * nalw;
-                xc.rowstage = b->dx.rowstage + nb0 * G.rs_frame_words;
-                xc.gbits = b->dx.gbits + nb0 * ng;
-                DevStream *st0 = b->d_st + s0;
-                NalDesc *nal0 = b->d_nal + (size_t)s0 * b->ld_nal;
-                PlanPending *pend0 = b->d_pend + s0;
-                DynFrame *dfr0 = b->d_dfr + nb0;
-                const uint8_t *src0 = b->d_src + (size_t)s0 * G.src_ld;
-                const uint8_t *refs0 = b->d_refs + (size_t)s0 * G.ref_ld;
-                uint8_t *stage0 = b->d_stage + nb0 * DYN_OVF_BYTES;   /* EP lists only */
-                if (dyn_launch_code(hs, nframes, s1 - s0, st0, nal0, b->ld_nal, pend0, dfr0, ld_fr, &G, src0,
-                                    refs0, &xc, b->dx.epoch, b->dyn_pw / 16, stamps)) {
-                    set_err("k_dyn_code launch: %s", hipGetErrorString(hipGetLastError()));
-                    return SCROLL_ERR_HIP;
-                }
-                hipStream_t hp = hs;
-                if (nch > 1) {
-                    HIPCHK(hipEventRecord(b->pipe_ev[c], hs));
-                    HIPCHK(hipStreamWaitEvent(b->pipe, b->pipe_ev[c], 0));
-                    hp = b->pipe;
-                } else if ((rc = mark(6))) {
-                    return rc;
-                }
-                if (dyn_launch_pack(hp, nframes, s1 - s0, st0, nal0, b->ld_nal, pend0, dfr0, ld_fr, &G, &xc,
-                                    stage0, stamps ? b->d_dbg : nullptr)) {
-                    set_err("k_dyn_static / k_dyn_epscan launch: %s", hipGetErrorString(hipGetLastError()));
-                    return SCROLL_ERR_HIP;
-                }
+            if (dyn_launch_code(hs, nframes, S, b->d_st, b->d_nal, b->ld_nal, b->d_pend, b->d_dfr, ld_fr, &G,
+                                b->d_src, b->d_refs, &b->dx, b->dx.epoch, b->dyn_pw / 16, stamps)) {
+                set_err("k_dyn_code launch: %s", hipGetErrorString(hipGetLastError()));
+                return SCROLL_ERR_HIP;
             }
-            if (nch > 1) {                 /* timing: code chain, then the pipe's tail */
-                if ((rc = mark(6))) return rc;
-                HIPCHK(hipEventRecord(b->pipe_ev[DYN_PIPE_CHUNKS], b->pipe));
-                HIPCHK(hipStreamWaitEvent(hs, b->pipe_ev[DYN_PIPE_CHUNKS], 0));
+            if ((rc = mark(6))) return rc;
+            if (dyn_launch_pack(hs, nframes, S, b->d_st, b->d_nal, b->ld_nal, b->d_pend, b->d_dfr, ld_fr, &G,
+                                &b->dx, b->d_stage, stamps ? b->d_dbg : nullptr)) {
+                set_err("k_dyn_static / k_dyn_epscan launch: %s", hipGetErrorString(hipGetLastError()));
+                return SCROLL_ERR_HIP;
             }
         }
         if ((rc = mark(2))) return rc;
@@ -3102,6 +3061,7 @@ int scroll_batch_enable_timing(ScrollBatch *b, int on)
 float scroll_batch_kernel_ms(ScrollBatch *b, int which)
 {
     if (!b || which < 0 || which > 5) return -1.0f;
+    if (b->timing == 2) return -1.0f;           /* lite: no per-kernel pairs (kernel_stats_ex has the dominant one) */
     if (batch_host_sync(b)) return -1.0f;
     if (b->timed_pending) {
         event_ms(b->ev, b->ev_dyn != 0, false, b->ms);

@@ -148,7 +148,8 @@ int scroll_batch_nal_info(ScrollBatch *b, int s, int i, int *kind, int *offset_p
  * complete); on = 2 ("lite") only the dominant kernel's pair -- dyn code
  * (also reported as dyn stage) or emit -- into kernel_stats_ex, the others
  * 0: each event record is a marker packet that holds the queue between the
- * kernels, so a timed step with every pair runs ~ 40 us longer; 0 off. */
+ * kernels, so a timed step with every pair runs ~ 40 us longer; 0 off.
+ * kernel_ms returns -1 while lite timing is on (no per-kernel pairs exist). */
 int scroll_batch_enable_timing(ScrollBatch *b, int on);
 float scroll_batch_kernel_ms(ScrollBatch *b, int which);
 /* all timed composes since the last call: summed plan / emit kernel ms and

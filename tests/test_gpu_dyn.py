@@ -473,6 +473,7 @@ def test_dyn_lite_timing_bytes_and_pairs(gpu, oracle):
             assert code > 0 and stage > 0
             if mode == 2:
                 assert plan == 0 and emit == 0 and demit == 0 and pack == 0 and stage == code
+                assert b.kernel_ms(4) == -1.0           # lite: no per-kernel pairs
             else:
                 assert plan > 0 and demit > 0
         b.close()

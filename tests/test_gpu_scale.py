@@ -73,5 +73,5 @@ def test_config2_full_step(gpu):
 
 
 def test_hint_workload_step(gpu):
-    """the UI-hint bench workload (P_Skip mode), first 32 streams checked"""
+    """the UI-hint bench workload (P_Skip mode), every stream checked"""
     _run(gpu, "p720hint", 3)

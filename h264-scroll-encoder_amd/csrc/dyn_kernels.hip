@@ -1223,24 +1223,28 @@ struct EpfLds {
     uint32_t *goff, *gb, *gw, *cw, *cbase, *lst, *cnt;    /* goff / cbase 65, gb / gw / cw 64, cnt 4 */
     uint32_t *ws;                                          /* per wave: the unique-position scan */
 };
-/* threads of a k_dyn_row workgroup: one block task each (two past 1024) */
+/* k_dyn_row's block tasks: luma [0, 16 w), chroma AC from the next wave
+ * boundary row_chroma0(w) on, so that every wave-pass is all luma or all
+ * chroma (uniform branches and per-wave fetch offsets, no exec-mask split) */
+__host__ __device__ inline int row_chroma0(int w) { return (16 * w + 63) & ~63; }
+__host__ __device__ inline int row_vtasks(int w) { return row_chroma0(w) + 8 * w; }
+
+/* threads of a k_dyn_row workgroup: about SCROLL_ROW_NP block tasks each */
 __host__ __device__ inline int row_threads(int w)
 {
-    const int nt = 24 * w;
+    const int nt = row_vtasks(w);
     const int a = (((nt + SCROLL_ROW_NP - 1) / SCROLL_ROW_NP) + 63) & ~63;
     const int b = (((nt + ROW_NPMAX - 1) / ROW_NPMAX) + 63) & ~63;      /* np <= ROW_NPMAX */
     const int t = a > b ? a : b;
     return t < ROW_MAXT ? t : ROW_MAXT;
 }
 
-/* The pixels of block task `task` of rect row ry: luma [0, 16 w)
- * MB-major, chroma AC [16 w, 24 w) (MB, plane, raster 2x2).  a = source
- * rows, b = prediction rows (chroma: the upper bilinear rows), c = the lower
- * bilinear rows, fr = the four rows' 1/8-pel fractions (3 bits each).  The
- * prediction rows' offsets come from the row's table in LDS (rt). */
+/* The pixels of a block task: a = source rows, b = prediction rows (chroma:
+ * the upper bilinear rows), c = the lower bilinear row of b[3] (chroma with
+ * a fraction only; the lower row of b[i < 3] is b[i + 1]: both are the
+ * chroma row after it through the same waypoint chain, k_dyn_rows) */
 struct BlkPix {
-    uint32_t a[4], b[4], c[4];
-    uint32_t fr;
+    uint32_t a[4], b[4], c;
 };
 
 /* raw buffer descriptor over n bytes at p (gfx9 dword3: 32-bit data format) */
@@ -1249,70 +1253,65 @@ __device__ inline __amdgpu_buffer_rsrc_t buf_rsrc(const void *p, uint32_t n)
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), (short)0, (int)n, 0x00020000);
 }
 
-/* A thread's block task in pass pa is pa T + t.  With T a multiple of 16
- * (row_threads) its 4x4 position inside the MB (luma) or the chroma quad
- * (chroma) is the same in every pass and its byte offsets advance by T per
- * pass, luma and chroma alike (16 k and 8 k both grow by T): FetchPre holds
- * pass 0's offsets and the row-table slots, row_fetch adds pa T */
-struct FetchPre {
-    uint32_t so_l, po_l, so_c, co_c;    /* luma source / prediction, chroma source / reference */
-    int rl, rc;                         /* rt[] rows: luma 4 by, chroma 16 + 4 by */
+/* A wave's fetch offsets (lane offsets into the frame's source / the
+ * stream's reference pair) for the tasks of pass pb; pass q's tasks are T q
+ * further on, and with T a multiple of 64 a task's position in its MB
+ * (luma) or chroma quad (chroma) is the same in every pass and both its
+ * byte offsets advance by exactly T q (16 k and 8 k both grow by T).  So the
+ * per-pass advance and the row strides go in the uniform soffset: a pass's
+ * eight (twelve) loads cost no vector instruction.  One set of registers,
+ * reloaded when the wave's tasks turn from luma to chroma (once). */
+struct FetchOff {
+    uint32_t s, b[4], c;        /* source row 0; prediction rows; the lower bilinear row of b[3] */
+    int pb;                     /* the pass they are for (uniform) */
 };
 
-__device__ inline FetchPre fetch_pre(int t, int w, int ry, const DynGeom &g, uint32_t csz)
+/* luma task v (MB k = v / 16, raster block v % 16) of rect row ry; rt = the
+ * row's 16 luma prediction rows (LDS, or k_dyn_rows' table in global memory) */
+__device__ inline void fetch_luma(FetchOff &o, int v, int ry, const DynGeom &g, const uint32_t *rt)
 {
-    const int lstride = 16 * g.w, cstride = 8 * g.w, ndt = g.w * g.h;
-    FetchPre f;
-    {
-        const int r = t & 15, bx = r & 3, by = r >> 2;
-        f.so_l = (uint32_t)((16 * ry + 4 * by) * lstride + 16 * (t >> 4) + 4 * bx);
-        f.po_l = (uint32_t)(16 * (g.x0 + (t >> 4)) + 4 * bx);
-        f.rl = 4 * by;
-    }
-    {
-        const int e = t - 16 * w, k = e >> 3, p = (e >> 2) & 1, r = e & 3;   /* arithmetic shifts: e < 0 fine */
-        const int bx = r & 1, by = r >> 1;
-        f.so_c = (uint32_t)(256 * ndt + (p ? 64 * ndt : 0) + (8 * ry + 4 * by) * cstride + 8 * k + 4 * bx);
-        f.co_c = (uint32_t)p * csz + (uint32_t)(8 * (g.x0 + k) + 4 * bx);
-        f.rc = 16 + 4 * by;
-    }
-    return f;
+    const int k = v >> 4, r = v & 15, bx = r & 3, by = r >> 2;
+    o.s = (uint32_t)((16 * ry + 4 * by) * (16 * g.w) + 16 * k + 4 * bx);
+    const uint32_t po = (uint32_t)(16 * (g.x0 + k) + 4 * bx);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) o.b[i] = po + rt[4 * by + i];
+    o.c = o.b[3];
 }
 
-/* fs: the frame's source bytes, rb: the stream's reference pair, both as
- * buffer descriptors -- 32-bit lane offsets, the row step in the uniform
- * soffset, so a pixel row costs one load and at most one add.  The task of
- * pass pa (luma: task < 16 w); adv = pa T */
-__device__ inline void row_fetch(bool luma, uint32_t adv, const DynGeom &g, __amdgpu_buffer_rsrc_t fs,
-                                 __amdgpu_buffer_rsrc_t rb, const uint32_t *rt, const FetchPre &F, BlkPix &px)
+/* chroma AC task e (MB e / 8, plane (e / 4) % 2, raster block e % 4); ru /
+ * rd = the row's 8 upper / lower bilinear rows */
+__device__ inline void fetch_chroma(FetchOff &o, int e, int ry, const DynGeom &g, uint32_t csz, const uint32_t *ru,
+                                    const uint32_t *rd)
 {
-    const int lstride = 16 * g.w, cstride = 8 * g.w;
-    px.fr = 0;
-    if (luma) {
-        const uint32_t so = F.so_l + adv, po = F.po_l + adv;
+    const int ndt = g.w * g.h, k = e >> 3, p = (e >> 2) & 1, r = e & 3, bx = r & 1, by = r >> 1;
+    o.s = (uint32_t)(256 * ndt + (p ? 64 * ndt : 0) + (8 * ry + 4 * by) * (8 * g.w) + 8 * k + 4 * bx);
+    const uint32_t co = (uint32_t)p * csz + (uint32_t)(8 * (g.x0 + k) + 4 * bx);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            px.a[i] = __builtin_amdgcn_raw_buffer_load_b32(fs, so, i * lstride, 0);
-            px.b[i] = __builtin_amdgcn_raw_buffer_load_b32(rb, po + rt[F.rl + i], 0, 0);
-            px.c[i] = 0;
-        }
-    } else {
-        const uint32_t so = F.so_c + adv, co = F.co_c + adv;
+    for (int i = 0; i < 4; ++i) o.b[i] = co + (ru[4 * by + i] & ROW_OFF);
+    o.c = co + (rd[4 * by + 3] & ROW_OFF);
+}
+
+/* the loads of pass q (soffset = T (q - pb) + the row stride term).  Lanes
+ * past the row's tasks load too: their offsets stay inside the frame's
+ * source / the reference pair or read 0 past the descriptor (raw buffer
+ * range check), and their results are never stored.  Chroma always loads
+ * its lower row (used only with a fraction): no wait for the fraction */
+__device__ inline void fetch_pass(const FetchOff &o, bool luma, uint32_t adv, uint32_t stride,
+                                  __amdgpu_buffer_rsrc_t fs, __amdgpu_buffer_rsrc_t rb, BlkPix &px)
+{
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const uint32_t ea = rt[F.rc + i];
-            const uint32_t f = (ea >> 28) & 7u;
-            px.a[i] = __builtin_amdgcn_raw_buffer_load_b32(fs, so, i * cstride, 0);
-            px.b[i] = __builtin_amdgcn_raw_buffer_load_b32(rb, co + (ea & ROW_OFF), 0, 0);
-            px.c[i] = f ? __builtin_amdgcn_raw_buffer_load_b32(rb, co + (rt[F.rc + 8 + i] & ROW_OFF), 0, 0) : 0u;
-            px.fr |= f << (3 * i);
-        }
+    for (int i = 0; i < 4; ++i) {
+        px.a[i] = __builtin_amdgcn_raw_buffer_load_b32(fs, o.s, adv + (uint32_t)i * stride, 0);
+        px.b[i] = __builtin_amdgcn_raw_buffer_load_b32(rb, o.b[i], adv, 0);
     }
+    px.c = luma ? 0u : __builtin_amdgcn_raw_buffer_load_b32(rb, o.c, adv, 0);
 }
 
 /* ((8 - f) b + f c + 4) >> 3 for the four bytes of b, c: even and odd bytes
  * as two 16-bit halves each (at most 2,044: no carry between halves), two
- * 24-bit multiply-adds per half pair */
+ * 24-bit multiply-adds per half pair.  k_dyn_row's NALs only ever have f = 0
+ * or 4 (full-pel luma motion: the chroma fraction is (4 mv) mod 8), where it
+ * is b or the rounding byte average v_lerp_u8; this form is the guard */
 __device__ inline uint32_t bilin4(uint32_t b, uint32_t c, uint32_t f)
 {
     const uint32_t g = 8u - f;
@@ -1321,30 +1320,6 @@ __device__ inline uint32_t bilin4(uint32_t b, uint32_t c, uint32_t f)
     const uint32_t ve = __umul24(g, be) + __umul24(f, ce) + 0x00040004u;
     const uint32_t vo = __umul24(g, bo) + __umul24(f, co) + 0x00040004u;
     return ((ve >> 3) & 0x00ff00ffu) | (((vo >> 3) & 0x00ff00ffu) << 8);
-}
-
-/* residual -> transform -> quant: pk = 16 int8 levels in scan order (AC: 15,
- * from scan index 1), n = TotalCoeff, w0 = chroma DC coefficient
- * (unquantised) */
-__device__ inline void row_levels(bool luma, const BlkPix &px, uint32_t pk[4], int &n, int &w0, const DynGeom &g)
-{
-    pk[0] = pk[1] = pk[2] = pk[3] = 0;
-    n = 0;
-    w0 = 0;
-    /* prediction rows as packed bytes: luma as fetched, chroma bilinear (one
-     * branch for the block, not one per pixel) */
-    uint32_t pr[4];
-    if (luma) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) pr[i] = px.b[i];
-    } else {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) pr[i] = bilin4(px.b[i], px.c[i], (px.fr >> (3 * i)) & 7u);
-    }
-    /* packed 16-bit pairs (dyn_device.h levels_pk) */
-    if (luma) levels_pk<true>(px.a, pr, pk, w0, g.ql);
-    else levels_pk<false>(px.a, pr, pk, w0, g.qc);
-    n = nz_bytes(pk[0]) + nz_bytes(pk[1]) + nz_bytes(pk[2]) + nz_bytes(pk[3]);
 }
 
 /* i / NPC for a piece index of a rect row (i < NPC DYN_MAX_W): a 24-bit
@@ -1405,8 +1380,6 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
         f = (int)(q - (uint32_t)s * (uint32_t)ld_fr);
     }
     const size_t nb = (size_t)s * ld_fr + f;
-    const DynFrame df = dfr[nb];
-    if (df.nal < 0 || ((df.err & DF_GENERAL) != 0) != GEN) return;
     constexpr bool general = GEN;
     const Rect R{g.x0, g.y0, g.w, g.h};
     const int w = R.w, ndt = R.w * R.h, row = R.y0 + r, npc = NPC * w, ntask = 24 * w;
@@ -1414,7 +1387,43 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
     constexpr int SR = DYN_STATIC_ROWS;
     const int nA = max(1, (R.y0 + SR - 1) / SR);
     const DevStream *S = st + s;
-    const int mbw = S->w / 16;
+    const int mbw = g.pw / 16;
+    const uint32_t ysz = (uint32_t)g.pw * (uint32_t)g.ph, csz = ysz / 4;
+    const int L0 = row_chroma0(w), nl = 16 * w, ntv = L0 + 8 * w;
+    const int np = (ntv + T - 1) / T;                   /* passes over the (wave-aligned) tasks */
+    const int wv0 = 64 * __builtin_amdgcn_readfirstlane(wave);
+    /* the wave's kind in pass q: 0 luma, 1 chroma, 2 none (uniform) */
+    auto kind_of = [&](int q) -> int {
+        const int v0 = q * T + wv0;
+        return v0 < nl ? 0 : (v0 < ntv ? 1 : 2);
+    };
+    const __amdgpu_buffer_rsrc_t fs = buf_rsrc(src + (size_t)s * g.src_ld + (size_t)f * g.src_fr, (uint32_t)g.src_fr);
+    const __amdgpu_buffer_rsrc_t rb = buf_rsrc(refs + (size_t)s * g.ref_ld, 3u * ysz);
+    /* pass 0's pixel loads go out first, their offsets from k_dyn_rows' row
+     * table in global memory: they need neither the frame's DynFrame nor the
+     * LDS copy of the table (a frame this instantiation does not code reads
+     * a table k_dyn_rows did not write: offsets into the descriptors' ranges
+     * or past them, which read 0; nothing is stored) */
+    FetchOff fo;
+    fo.pb = -1;
+    bool fo_chroma = false;
+    BlkPix nx;
+    if (!general) {
+        const uint32_t *rtg = rows + nb * (size_t)(32 * g.h);
+        const int k0 = kind_of(0);
+        if (k0 == 0) {
+            fetch_luma(fo, t, r, g, rtg + 16 * r);
+            fo.pb = 0;
+            fetch_pass(fo, true, 0u, (uint32_t)(16 * w), fs, rb, nx);
+        } else if (k0 == 1) {
+            fetch_chroma(fo, t - L0, r, g, csz, rtg + 16 * g.h + 8 * r, rtg + 24 * g.h + 8 * r);
+            fo.pb = 0;
+            fo_chroma = true;
+            fetch_pass(fo, false, 0u, (uint32_t)(8 * w), fs, rb, nx);
+        }
+    }
+    const DynFrame df = dfr[nb];
+    if (df.nal < 0 || ((df.err & DF_GENERAL) != 0) != GEN) return;
 
     uint4 *lv = rdyn;
     uint32_t *mbits = reinterpret_cast<uint32_t *>(lv + npc), *moff = mbits + w;
@@ -1438,58 +1447,89 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
         reinterpret_cast<uint2 *>(L.lvt)[i] = reinterpret_cast<const uint2 *>(&g_lvt)[i];
     if (!general && t < 32) L.rt[t] = rows[nb * (size_t)(32 * g.h) + (t < 16 ? 16 * r + t : 16 * g.h + (t < 24 ? 8 * r + t - 16 : 8 * g.h + 8 * r + t - 24))];
     const NalDesc d = nal[(size_t)s * ld_nal + df.nal];
-    const uint32_t ysz = (uint32_t)S->w * (uint32_t)S->h, csz = ysz / 4;
 
     /* ---- 1-2: records (levels -> CAVLC bodies) into LDS ---------------- */
-    const int np = (ntask + T - 1) / T;                 /* tasks per thread, <= ROW_NPMAX */
-    /* (measured: chroma tasks from the next wave boundary, so no wave runs
-     * both paths, was no faster -- the same number of wave passes) */
-    auto task_of = [&](int v) -> int { return v < ntask ? v : -1; };
     __syncthreads();                                    /* the row table (rt) */
     ROW_CUT(0);
     if (!general) {
-        const __amdgpu_buffer_rsrc_t fs = buf_rsrc(src + (size_t)s * g.src_ld + (size_t)f * g.src_fr,
-                                                   (uint32_t)g.src_fr);
-        const __amdgpu_buffer_rsrc_t rb = buf_rsrc(refs + (size_t)s * g.ref_ld, 3u * ysz);
+        static_assert(ROW_MAXT % 64 == 0, "row_threads gives whole waves: the per-pass step T is a multiple of 64");
+        /* the row's chroma fraction, the same for all its rows (one region,
+         * one mv): 0 or 4 here (k_dyn_rows sends half-pel chains to the
+         * general path) */
+        const uint32_t frc = __builtin_amdgcn_readfirstlane((L.rt[16] >> 28) & 7u);
+        auto issue = [&](int q, BlkPix &px) {
+            const int kd = kind_of(q);
+            if (kd == 2) return;
+            if (kd == 0 && fo.pb < 0) {
+                fetch_luma(fo, q * T + t, r, g, L.rt);
+                fo.pb = q;
+            } else if (kd == 1 && !fo_chroma) {
+                fetch_chroma(fo, q * T + t - L0, r, g, csz, L.rt + 16, L.rt + 24);
+                fo.pb = q;
+                fo_chroma = true;
+            }
+            fetch_pass(fo, kd == 0, (uint32_t)((q - fo.pb) * T), (uint32_t)(kd == 0 ? 16 * w : 8 * w), fs, rb, px);
+        };
         /* counting sort on TotalCoeff class: a task's rank in its class from
          * an LDS atomic (the order inside a class does not matter), kept in
          * lo[] (phase 3's) until the class bases are known */
-        static_assert(ROW_MAXT % 16 == 0, "row_threads gives whole waves: FetchPre's per-pass step");
-        const FetchPre FP = fetch_pre(t, w, r, g, csz);
-        BlkPix nx;                                      /* the next task's pixels, in flight */
-        {
-            const int t0 = task_of(t);
-            if (t0 >= 0) row_fetch(t0 < 16 * w, 0u, g, fs, rb, L.rt, FP, nx);
-        }
-        for (int pa = 0; pa < np; ++pa) {
-            const int task = task_of(pa * T + t), tn = task_of((pa + 1) * T + t);
-            const BlkPix cur = nx;
-            if (tn >= 0) row_fetch(tn < 16 * w, (uint32_t)((pa + 1) * T), g, fs, rb, L.rt, FP, nx);
+        auto compute = [&](int q, const BlkPix &px) {
+            const int kd = kind_of(q);
+            if (kd == 2) return;
+            const int v = q * T + t;
             uint32_t pk[4];
-            int n = 0, w0 = 0;
-            if (task >= 0) {
-                row_levels(task < 16 * w, cur, pk, n, w0, g);
-                const int slot = row_slot(task, w);
+            int w0 = 0;
+            if (kd == 0) {
+                levels_pk<true>(px.a, px.b, pk, w0, g.ql);
+            } else {
+                uint32_t pr[4];
+                if (frc == 4u) {
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) pr[i] = __builtin_amdgcn_lerp(px.b[i], i < 3 ? px.b[i + 1] : px.c, 0x01010101u);
+                } else if (frc == 0u) {
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) pr[i] = px.b[i];
+                } else {
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) pr[i] = bilin4(px.b[i], i < 3 ? px.b[i + 1] : px.c, frc);
+                }
+                levels_pk<false>(px.a, pr, pk, w0, g.qc);
+            }
+            const int e = v - L0;                           /* chroma task index */
+            const bool ok = kd == 0 ? v < nl : e < 8 * w;
+            if (ok) {
+                const int n = nz_bytes(pk[0]) + nz_bytes(pk[1]) + nz_bytes(pk[2]) + nz_bytes(pk[3]);
+                const int slot = kd == 0 ? (int)__umul24((uint32_t)(v >> 4), (uint32_t)NPC) + (v & 15)
+                                         : (int)__umul24((uint32_t)(e >> 3), (uint32_t)NPC) + 18 + (e & 7);
                 lv[slot] = make_uint4(pk[0], pk[1], pk[2], pk[3]);
                 mt[slot] = (uint16_t)((uint32_t)min(n, 16) << 8);
                 lo[slot] = (uint16_t)atomicAdd(&L.kc[0][SORT_KEYS - 1 - min(n, SORT_KEYS - 1)], 1u);
             }
             /* chroma DC: the quad's four DC coefficients -> 2x2 Hadamard,
              * quant -> levels as int16 in the DC slot (coded after the
-             * barrier that publishes the CAVLC tables) */
-            const bool cdc = task >= 16 * w;
-            if (__builtin_amdgcn_ballot_w64(cdc) == 0) continue;   /* luma-only wave: no chroma DC */
-            const int qb = lane & ~3;
-            const int d0 = __shfl(w0, qb, 64), d1 = __shfl(w0, qb + 1, 64);
-            const int d2 = __shfl(w0, qb + 2, 64), d3 = __shfl(w0, qb + 3, 64);
-            if (cdc && (task & 3) == 0) {
-                const int jj = task - 16 * w, k = jj >> 3, p = (jj >> 2) & 1;
-                const int q0 = quant_dc(d0 + d1 + d2 + d3, g.qc), q1 = quant_dc(d0 - d1 + d2 - d3, g.qc);
-                const int q2 = quant_dc(d0 + d1 - d2 - d3, g.qc), q3 = quant_dc(d0 - d1 - d2 + d3, g.qc);
-                lv[k * NPC + 16 + p] = make_uint4(((uint32_t)q0 & 0xffffu) | (uint32_t)q1 << 16,
-                                                  ((uint32_t)q2 & 0xffffu) | (uint32_t)q3 << 16, 0u, 0u);
-                mt[k * NPC + 16 + p] = (uint16_t)((uint32_t)((q0 != 0) + (q1 != 0) + (q2 != 0) + (q3 != 0)) << 8);
+             * barrier that publishes the CAVLC tables); quads are lane-aligned
+             * (L0 and T are multiples of 64) */
+            if (kd == 1) {
+                const int qb = lane & ~3;
+                const int d0 = __shfl(w0, qb, 64), d1 = __shfl(w0, qb + 1, 64);
+                const int d2 = __shfl(w0, qb + 2, 64), d3 = __shfl(w0, qb + 3, 64);
+                if (ok && (e & 3) == 0) {
+                    const int k = e >> 3, p = (e >> 2) & 1;
+                    const int q0 = quant_dc(d0 + d1 + d2 + d3, g.qc), q1 = quant_dc(d0 - d1 + d2 - d3, g.qc);
+                    const int q2 = quant_dc(d0 + d1 - d2 - d3, g.qc), q3 = quant_dc(d0 - d1 - d2 + d3, g.qc);
+                    lv[k * NPC + 16 + p] = make_uint4(((uint32_t)q0 & 0xffffu) | (uint32_t)q1 << 16,
+                                                      ((uint32_t)q2 & 0xffffu) | (uint32_t)q3 << 16, 0u, 0u);
+                    mt[k * NPC + 16 + p] =
+                        (uint16_t)((uint32_t)((q0 != 0) + (q1 != 0) + (q2 != 0) + (q3 != 0)) << 8);
+                }
             }
+        };
+        /* two pixel sets in turn: the next pass's loads are in flight while
+         * this one is coded, with no register copies between passes */
+        for (int pa = 0; pa < np; ++pa) {                  /* pass 0's loads are in flight already */
+            const BlkPix cur = nx;
+            if (pa + 1 < np) issue(pa + 1, nx);
+            compute(pa, cur);
         }
         __syncthreads();                                /* levels, TotalCoeffs, ptabs, counts */
         if (stamps) stv[1] = __builtin_amdgcn_s_memrealtime();

@@ -95,6 +95,7 @@ typedef struct {
 #endif
 typedef struct {
     int32_t x0, y0, w, h;           /* rect, MB units                             */
+    int32_t pw, ph;                 /* the streams' picture size (pixels)         */
     int32_t ngroups;                /* k_dyn_group row groups per NAL (dyn_groups) */
     int32_t qp;                     /* the rect's QP (slice_qp_delta qp - 26)     */
     QParams ql, qc;                 /* its luma / chroma (QPc) quantisers          */

@@ -1878,6 +1878,8 @@ int scroll_batch_set_dyn_rect(ScrollBatch *b, int x0, int y0, int w, int h, size
     DynGeom g{};
     g.x0 = x0;
     g.y0 = y0;
+    g.pw = pw;
+    g.ph = ph;
     g.w = w;
     g.h = h;
     g.qp = b->dyn_qp;

@@ -26,10 +26,14 @@ namespace scroll {
 namespace dyn {
 
 /* the rect's QP: 26 by default (pic_init_qp 26, slice_qp_delta 0,
- * h264_writer.c:118-120); scroll_batch_set_dyn_qp picks another, written as
- * the dynamic NAL's slice_qp_delta.  QP_MIN: the lowest whose levels fit the
- * packed int8 form (|W| <= 9180: max level 127 at QP 22, 145 at 21) */
-constexpr int QP_DEFAULT = 26, QP_MIN = 22, QP_MAX = 51;
+ * h264_writer.c:118-120); scroll_batch_set_dyn_qp[_stream / _at] picks
+ * another, 0..51, written as the dynamic NAL's slice_qp_delta (under hints:
+ * the rect MBs' mb_qp_delta chain).  QP_MIN: the lowest whose levels fit the
+ * packed int8 form of k_dyn_row (|W| <= 9180: max level 127 at QP 22, 145 at
+ * 21); below it a NAL takes the general path with 16-bit levels.
+ * LEVEL_MAX: levels are clamped to the largest |level| every CAVLC context
+ * codes with level_prefix <= 15 (only chroma DC below QPc 6 reaches it) */
+constexpr int QP_DEFAULT = 26, QP_MIN = 22, QP_MAX = 51, LEVEL_MAX = 2063;
 /* MF by QP % 6 and position class (Table 8-x inverse, the forward scale) */
 __host__ __device__ constexpr int mf_of(int r, int cls)
 {
@@ -40,6 +44,16 @@ __host__ __device__ constexpr int mf_of(int r, int cls)
 __host__ __device__ constexpr QParams qparams(int qp)
 {
     return QParams{mf_of(qp % 6, 0), mf_of(qp % 6, 1), mf_of(qp % 6, 2), 15 + qp / 6, (1 << (15 + qp / 6)) / 6};
+}
+/* qparams for a QP known only at run time (wave-uniform: the selects stay
+ * scalar; no table in private memory) */
+__device__ __host__ inline QParams qparams_rt(int qp)
+{
+    const int r = qp % 6, b = 15 + qp / 6;
+    const int m0 = r == 0 ? 13107 : r == 1 ? 11916 : r == 2 ? 10082 : r == 3 ? 9362 : r == 4 ? 8192 : 7282;
+    const int m1 = r == 0 ? 5243 : r == 1 ? 4660 : r == 2 ? 4194 : r == 3 ? 3647 : r == 4 ? 3355 : 2893;
+    const int m2 = r == 0 ? 8066 : r == 1 ? 7490 : r == 2 ? 6554 : r == 3 ? 5825 : r == 4 ? 5243 : 4559;
+    return QParams{m0, m1, m2, b, (1 << b) / 6};
 }
 /* QPc of QP (Table 8-15, chroma_qp_index_offset 0 as the composer's PPS) */
 __host__ __device__ constexpr int qp_chroma(int qp)
@@ -344,7 +358,7 @@ __device__ __host__ inline int quant(int w, int pos, const QParams &q)
     /* bias by the sign mask as a bit select (v_bfi): no compare, no VCC */
     const uint32_t m = (uint32_t)(w >> 31);
     const int bias = (int)((m & (uint32_t)((1 << q.qbits) - 1 - q.qf)) | (~m & (uint32_t)q.qf));
-    return mad_i24(w, mf, bias) >> q.qbits;
+    return clampi(mad_i24(w, mf, bias) >> q.qbits, -LEVEL_MAX, LEVEL_MAX);
 }
 
 /* ---------------------------------------------------------------------- */
@@ -639,7 +653,7 @@ __device__ __host__ inline uint32_t nz_mask16(uint4 pk)
 __device__ __host__ inline int quant_dc(int w, const QParams &q)
 {
     const int bias = w < 0 ? (1 << (q.qbits + 1)) - 1 - 2 * q.qf : 2 * q.qf;
-    return mad_i24(w, q.mf0, bias) >> (q.qbits + 1);
+    return clampi(mad_i24(w, q.mf0, bias) >> (q.qbits + 1), -LEVEL_MAX, LEVEL_MAX);
 }
 
 /* ---------------------------------------------------------------------- */
@@ -779,6 +793,45 @@ __device__ __host__ inline int cavlc_block(S &s, const Tabs &T, const C *coef, i
         s.put(T.rb_bits[zi][run], T.rb_len[zi][run]);
         zl -= run;
         p = q;
+    }
+    return tc;
+}
+
+/* drops the first `skip` bits (a coeff_token) of what is put: a block's
+ * CAVLC body from cavlc_block */
+template <class S>
+struct SkipSink {
+    S &in;
+    uint32_t skip;
+    __device__ __host__ inline void put(uint32_t v, int n)
+    {
+        if (n <= 0) return;
+        if (skip >= (uint32_t)n) {
+            skip -= (uint32_t)n;
+            return;
+        }
+        if (skip) {
+            n -= (int)skip;
+            v &= low_mask(n);
+            skip = 0;
+        }
+        in.put(v, n);
+    }
+};
+
+/* TotalCoeff and TrailingOnes (9.2.1) of a block in scan order */
+template <class C>
+__device__ __host__ inline int tc_t1_of(const C *c, int max, int &t1)
+{
+    int tc = 0;
+    t1 = 0;
+    bool stop = false;
+    for (int i = max - 1; i >= 0; --i) {
+        if (!c[i]) continue;
+        ++tc;
+        if (stop || t1 >= 3) continue;
+        if (c[i] == 1 || c[i] == -1) t1++;
+        else stop = true;
     }
     return tc;
 }

@@ -17,6 +17,7 @@ typedef struct {
     uint32_t *rows;
     uint16_t *meta;
     uint2 *body_lo, *body_hi;       /* record bodies: bits 0..63, bits 64..127 */
+    uint4 *body_w;                  /* below QP_MIN: levels 8..15 (int16) of > 128-bit blocks */
     unsigned long long *tcx;        /* k_dyn_row: per (frame, rect row, MB) bottom TotalCoeffs */
     uint32_t *rowstage;             /* per (frame, row group): its bits from bit 0 (rs_frame_words) */
     uint32_t *gbits;                /* per (frame, row group): its bit count */

@@ -313,7 +313,7 @@ __global__ __launch_bounds__(256) void k_dyn_rows(const DevStream *__restrict__ 
         }
         rw[i] = e;
     }
-    if (my_gen) gen = 1;
+    if (my_gen || S->dyn_qp < QP_MIN) gen = 1;            /* half-pel chroma chains; 16-bit levels */
     __syncthreads();
     if (t == 0) {
         /* a general-path NAL takes a record slot (index in rbsp_bytes until
@@ -366,9 +366,11 @@ __device__ inline void code_frame(const DevStream *__restrict__ st,
                                                      const uint8_t *__restrict__ src,
                                                      const uint8_t *__restrict__ refs,
                                                      uint16_t *__restrict__ meta, uint2 *__restrict__ blo,
-                                                     uint2 *__restrict__ bhi, int s, int f, int bx)
+                                                     uint2 *__restrict__ bhi, uint4 *__restrict__ bwd, int s,
+                                                     int f, int bx)
 {
     __shared__ uint4 lv[CODE_T];
+    __shared__ int16_t lw[CODE_T][16];              /* below QP_MIN: the levels as int16 */
     __shared__ uint16_t wc[CODE_NW][SORT_KEYS];    /* per wave: blocks per TotalCoeff class */
     __shared__ uint16_t order[CODE_T];
     __shared__ PTabs ptabs;
@@ -386,6 +388,10 @@ __device__ inline void code_frame(const DevStream *__restrict__ st,
 
     const int ndt = g.w * g.h, ntask = 24 * ndt;
     const int task = bx * CODE_T + t;
+    /* the stream's rect QP; below QP_MIN the levels need 16 bits (wide) */
+    const int qpy = __builtin_amdgcn_readfirstlane(st[s].dyn_qp);
+    const QParams ql = qparams_rt(qpy), qc = qparams_rt(qp_chroma(qpy));
+    const bool wide = qpy < QP_MIN;
     const size_t nb = (size_t)s * ld_fr + f;
     const uint32_t *rw = rows + nb * (size_t)(32 * g.h);
     const int w = st[s].w, h = st[s].h;
@@ -398,6 +404,7 @@ __device__ inline void code_frame(const DevStream *__restrict__ st,
     const size_t gs = df.rbsp_bytes;                    /* its record slot (k_dyn_rows) */
     uint16_t *M = meta + gs * (size_t)(NPC * ndt);
     uint2 *BL = blo + gs * (size_t)(NPC * ndt), *BH = bhi + gs * (size_t)(NPC * ndt);
+    uint4 *BW = bwd + gs * (size_t)(NPC * ndt);
 
     const bool luma = task < 16 * ndt;
     const bool act = task < ntask;
@@ -435,8 +442,9 @@ __device__ inline void code_frame(const DevStream *__restrict__ st,
         fwd4x4(res, W);
 #pragma unroll
         for (int k2 = 0; k2 < 16; ++k2) {
-            const int v = quant(W[ZZ[k2]], ZZ[k2], g.ql);    /* |v| <= 127 (QP >= 22): int8 */
+            const int v = quant(W[ZZ[k2]], ZZ[k2], ql);      /* |v| <= 127 at QP >= 22: int8 */
             pk[k2 >> 2] |= ((uint32_t)v & 255u) << (8 * (k2 & 3));
+            if (wide) lw[t][k2] = (int16_t)v;
             n += v != 0;
         }
     } else if (act) {
@@ -496,10 +504,12 @@ __device__ inline void code_frame(const DevStream *__restrict__ st,
         w0 = W[0];
 #pragma unroll
         for (int k2 = 1; k2 < 16; ++k2) {
-            const int v = quant(W[ZZ[k2]], ZZ[k2], g.qc);
+            const int v = quant(W[ZZ[k2]], ZZ[k2], qc);
             pk[(k2 - 1) >> 2] |= ((uint32_t)v & 255u) << (8 * ((k2 - 1) & 3));
+            if (wide) lw[t][k2 - 1] = (int16_t)v;
             n += v != 0;
         }
+        if (wide) lw[t][15] = 0;
     }
     /* chroma DC: the quad's four DC coefficients -> 2x2 Hadamard, quant; the
      * whole CAVLC block (nC = -1) is coded by the quad's first lane after the
@@ -511,10 +521,10 @@ __device__ inline void code_frame(const DevStream *__restrict__ st,
         const int d0 = __shfl(w0, qb, 64), d1 = __shfl(w0, qb + 1, 64);
         const int d2 = __shfl(w0, qb + 2, 64), d3 = __shfl(w0, qb + 3, 64);
         if (dc_lane) {
-            dq[0] = quant_dc(d0 + d1 + d2 + d3, g.qc);
-            dq[1] = quant_dc(d0 - d1 + d2 - d3, g.qc);
-            dq[2] = quant_dc(d0 + d1 - d2 - d3, g.qc);
-            dq[3] = quant_dc(d0 - d1 - d2 + d3, g.qc);
+            dq[0] = quant_dc(d0 + d1 + d2 + d3, qc);
+            dq[1] = quant_dc(d0 - d1 + d2 - d3, qc);
+            dq[2] = quant_dc(d0 + d1 - d2 - d3, qc);
+            dq[3] = quant_dc(d0 - d1 - d2 + d3, qc);
         }
     }
     /* encode order: by TotalCoeff, largest first (a counting sort over the
@@ -577,8 +587,20 @@ __device__ inline void code_frame(const DevStream *__restrict__ st,
     int t1 = 0;
     bool ok = true;
     int tc = 0;
-    if (tk < ntask) {
+    if (tk < ntask && !wide) {
         tc = cavlc_body(cap, ptabs, v4, ul ? 16 : 15, t1, ok);
+    } else if (tk < ntask) {
+        /* 16-bit levels: the whole block through the coder's tables, its
+         * coeff_token (at nC 0) skipped; over 128 bits the record keeps the
+         * levels (32 bytes: BL, BH, BW) */
+        const int max = ul ? 16 : 15;
+        tc = tc_t1_of(lw[u], max, t1);
+        uint32_t tv;
+        int tl;
+        coeff_token(g_tabs, tc, t1, 0, tv, tl);
+        SkipSink<CapSink> sk{cap, (uint32_t)tl};
+        cavlc_block(sk, g_tabs, lw[u], max, 0);
+        ok = cap.n <= 128;
     }
     /* each lane stores its own block's record (task order, so a workgroup's
      * records are one contiguous range; un-sorting through LDS first was
@@ -587,11 +609,17 @@ __device__ inline void code_frame(const DevStream *__restrict__ st,
         const uint16_t mm = ok ? (uint16_t)(cap.n | (uint32_t)tc << 8 | (uint32_t)t1 << 13)
                                : (uint16_t)((uint32_t)tc << 8 | (uint32_t)t1 << 13 | M_OVF);
         M[tk] = mm;
+        uint4 ov = v4;                                  /* the levels of a > 128-bit body */
+        if (wide && !ok) {
+            const uint4 *l2 = reinterpret_cast<const uint4 *>(lw[u]);
+            ov = l2[0];
+            BW[tk] = l2[1];
+        }
         if ((mm & 255u) || (mm & M_OVF))
             put_body(BL, BH, tk,
                      ok ? make_uint4((uint32_t)cap.lo, (uint32_t)(cap.lo >> 32), (uint32_t)cap.hi,
                                      (uint32_t)(cap.hi >> 32))
-                        : v4,
+                        : ov,
                      (mm & 255u) > 64u || (mm & M_OVF));
     }
 }
@@ -609,13 +637,13 @@ __global__ __launch_bounds__(CODE_T) void k_dyn_code_general(const DevStream *__
                                                              const uint8_t *__restrict__ refs,
                                                              uint16_t *__restrict__ meta,
                                                              uint2 *__restrict__ blo, uint2 *__restrict__ bhi,
-                                                             const uint32_t *__restrict__ ctr)
+                                                             uint4 *__restrict__ bwd, const uint32_t *__restrict__ ctr)
 {
     const uint32_t n = min(__builtin_amdgcn_readfirstlane(ctr[1]), g.gen_cap);
     for (uint32_t j = blockIdx.y; j < n; j += gridDim.y) {
         const uint32_t q = __builtin_amdgcn_readfirstlane(ctr[DYN_CTR_LIST + j]);
         const int s = (int)(q / (uint32_t)ld_fr), f = (int)(q - (uint32_t)s * (uint32_t)ld_fr);
-        code_frame(st, dfr, ld_fr, pend, nal, ld_nal, g, rows, src, refs, meta, blo, bhi, s, f, blockIdx.x);
+        code_frame(st, dfr, ld_fr, pend, nal, ld_nal, g, rows, src, refs, meta, blo, bhi, bwd, s, f, blockIdx.x);
         __syncthreads();
     }
 }
@@ -756,36 +784,49 @@ __device__ inline void wave_sync()
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-/* a > 128-bit block from its levels (rare): measure / write */
-__device__ __attribute__((noinline)) uint32_t ovf_bits(const PTabs &PT, const Tabs &TB, uint4 bd, int pc, int nC)
+/* a > 128-bit block from its levels (rare): measure / write.  bd: 16 int8
+ * levels (chroma DC: 4 int16); bw != nullptr: the 16-bit form of the
+ * general path below QP_MIN -- bd levels 0-7, *bw levels 8-15, int16 */
+template <class S>
+__device__ inline void ovf_code(S &sk, const PTabs &PT, const Tabs &TB, uint4 bd, const uint4 *bw, int pc, int nC)
 {
-    CountSink cn{0};
     if (nC == -1) {
         const int dq[4] = {(int)(int16_t)(bd.x & 0xffffu), (int)(int16_t)(bd.x >> 16),
                            (int)(int16_t)(bd.y & 0xffffu), (int)(int16_t)(bd.y >> 16)};
-        cavlc_dc4(cn, PT, dq);
+        cavlc_dc4(sk, PT, dq);
+    } else if (bw) {
+        const uint4 hi = *bw;
+        const uint32_t w8[8] = {bd.x, bd.y, bd.z, bd.w, hi.x, hi.y, hi.z, hi.w};
+        int16_t l16[16];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            l16[2 * i] = (int16_t)(w8[i] & 0xffffu);
+            l16[2 * i + 1] = (int16_t)(w8[i] >> 16);
+        }
+        cavlc_block(sk, TB, l16, pc < 16 ? 16 : 15, nC);
     } else {
         const int8_t *lvp = reinterpret_cast<const int8_t *>(&bd);
-        cavlc_block(cn, TB, lvp, pc < 16 ? 16 : 15, nC);
+        cavlc_block(sk, TB, lvp, pc < 16 ? 16 : 15, nC);
     }
+}
+
+__device__ __attribute__((noinline)) uint32_t ovf_bits(const PTabs &PT, const Tabs &TB, uint4 bd, const uint4 *bw,
+                                                       int pc, int nC)
+{
+    CountSink cn{0};
+    ovf_code(cn, PT, TB, bd, bw, pc, nC);
     return cn.n;
 }
 
 /* the sink lives in the callee: a sink passed by reference would be kept in
  * scratch memory by the caller on its every put */
 __device__ __attribute__((noinline)) void ovf_put(uint32_t *buf, uint32_t lo, uint32_t n, uint32_t pos,
-                                                  const PTabs &PT, const Tabs &TB, uint4 bd, int pc, int nC)
+                                                  const PTabs &PT, const Tabs &TB, uint4 bd, const uint4 *bw, int pc,
+                                                  int nC)
 {
     WSink sk{LdsOrWin{buf, lo, n}, 0, 0, 0};
     sk.start(pos);
-    if (nC == -1) {
-        const int dq[4] = {(int)(int16_t)(bd.x & 0xffffu), (int)(int16_t)(bd.x >> 16),
-                           (int)(int16_t)(bd.y & 0xffffu), (int)(int16_t)(bd.y >> 16)};
-        cavlc_dc4(sk, PT, dq);
-    } else {
-        const int8_t *lvp = reinterpret_cast<const int8_t *>(&bd);
-        cavlc_block(sk, TB, lvp, pc < 16 ? 16 : 15, nC);
-    }
+    ovf_code(sk, PT, TB, bd, bw, pc, nC);
     sk.finish();
 }
 
@@ -868,7 +909,7 @@ __global__ __launch_bounds__(GW) void k_dyn_static(const DevStream *__restrict__
     const NalDesc d = nal[(size_t)s * ld_nal + j];
     wave_sync();
     NalCtx c = nal_ctx(S, d, L.wo, L.wl, L.wv);
-    c.qpd = g.qp - QP_DEFAULT;                          /* the rect's QP: slice_qp_delta */
+    c.qpd = S->dyn_qp - QP_DEFAULT;                     /* the stream's rect QP: slice_qp_delta */
     const HeadCtx H = head_ctx(c);
     const int mbw = H.mbw, mbh = c.h / 16;
     int ra, rb;
@@ -1360,6 +1401,7 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
                                                      const uint8_t *__restrict__ refs,
                                                      const uint16_t *__restrict__ meta,
                                                      const uint2 *__restrict__ blo, const uint2 *__restrict__ bhi,
+                                                     const uint4 *__restrict__ bwd,
                                                      unsigned long long *__restrict__ tcx, uint32_t epoch,
                                                      uint32_t *__restrict__ rowstage, uint32_t *__restrict__ gbits,
                                                      uint32_t *__restrict__ spill, uint32_t *__restrict__ ctr,
@@ -1457,6 +1499,9 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
          * one mv): 0 or 4 here (k_dyn_rows sends half-pel chains to the
          * general path) */
         const uint32_t frc = __builtin_amdgcn_readfirstlane((L.rt[16] >> 28) & 7u);
+        /* the stream's rect QP (QP_MIN and up here: int8 levels) */
+        const int qpy = __builtin_amdgcn_readfirstlane(S->dyn_qp);
+        const QParams ql = qparams_rt(qpy), qc = qparams_rt(qp_chroma(qpy));
         auto issue = [&](int q, BlkPix &px) {
             const int kd = kind_of(q);
             if (kd == 2) return;
@@ -1480,7 +1525,7 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
             uint32_t pk[4];
             int w0 = 0;
             if (kd == 0) {
-                levels_pk<true>(px.a, px.b, pk, w0, g.ql);
+                levels_pk<true>(px.a, px.b, pk, w0, ql);
             } else {
                 uint32_t pr[4];
                 if (frc == 4u) {
@@ -1493,7 +1538,7 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
 #pragma unroll
                     for (int i = 0; i < 4; ++i) pr[i] = bilin4(px.b[i], i < 3 ? px.b[i + 1] : px.c, frc);
                 }
-                levels_pk<false>(px.a, pr, pk, w0, g.qc);
+                levels_pk<false>(px.a, pr, pk, w0, qc);
             }
             const int e = v - L0;                           /* chroma task index */
             const bool ok = kd == 0 ? v < nl : e < 8 * w;
@@ -1515,8 +1560,8 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
                 const int d2 = __shfl(w0, qb + 2, 64), d3 = __shfl(w0, qb + 3, 64);
                 if (ok && (e & 3) == 0) {
                     const int k = e >> 3, p = (e >> 2) & 1;
-                    const int q0 = quant_dc(d0 + d1 + d2 + d3, g.qc), q1 = quant_dc(d0 - d1 + d2 - d3, g.qc);
-                    const int q2 = quant_dc(d0 + d1 - d2 - d3, g.qc), q3 = quant_dc(d0 - d1 - d2 + d3, g.qc);
+                    const int q0 = quant_dc(d0 + d1 + d2 + d3, qc), q1 = quant_dc(d0 - d1 + d2 - d3, qc);
+                    const int q2 = quant_dc(d0 + d1 - d2 - d3, qc), q3 = quant_dc(d0 - d1 - d2 + d3, qc);
                     lv[k * NPC + 16 + p] = make_uint4(((uint32_t)q0 & 0xffffu) | (uint32_t)q1 << 16,
                                                       ((uint32_t)q2 & 0xffffu) | (uint32_t)q3 << 16, 0u, 0u);
                     mt[k * NPC + 16 + p] =
@@ -1660,6 +1705,13 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
     }
     const NalCtx c = nal_ctx(S, d, L.wo, L.wl, L.wv);
     const HeadCtx H = head_ctx(c);
+    /* a piece's levels past 8 (16-bit records of the general path below
+     * QP_MIN), nullptr for the int8 forms */
+    const bool wide = GEN && __builtin_amdgcn_readfirstlane(S->dyn_qp) < QP_MIN;
+    auto ovf_wide = [&](int k, int pc) -> const uint4 * {
+        if (!wide) return nullptr;
+        return bwd + (size_t)df.rbsp_bytes * (size_t)(NPC * ndt) + rec_of(r * w + k, pc, ndt);
+    };
     __syncthreads();                                    /* records, top TotalCoeffs, waypoint table */
     if (stamps) stv[2] = __builtin_amdgcn_s_memrealtime();
     ROW_CUT(2);
@@ -1694,7 +1746,7 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
         /* chroma DC: its body holds the whole block, token included */
         const uint32_t tl = nC < 0 ? 0u : (nC >= 8 ? 6u : ce >> 8);
         uint32_t len = tl + (mv & 255u);
-        if (mv & M_OVF) len = ovf_bits(PT, TB, lv[i], pc, nC);            /* rare */
+        if (mv & M_OVF) len = ovf_bits(PT, TB, lv[i], ovf_wide(k, pc), pc, nC);   /* rare */
         uint32_t nc1 = (uint32_t)(nC + 1);
         if (!(mv & M_OVF) && nC >= 0 && len <= 128u) {
             /* the token goes in front of the body here, where its code is
@@ -1886,7 +1938,7 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
                     else put_piece(L.buf, p0, n, pos, tv, tl, bd, mv & 255u);
                 }
             } else {
-                ovf_put(L.buf, p0, n, pos, PT, TB, bd, pc, nC);
+                ovf_put(L.buf, p0, n, pos, PT, TB, bd, ovf_wide(k, pc), pc, nC);
             }
         }
         __syncthreads();
@@ -3298,19 +3350,20 @@ int dyn_launch_code(hipStream_t hs, int nframes, int S, DevStream *st, const Nal
     if (hipGetLastError() != hipSuccess) return -1;
     const int nchunk = (24 * g->w * g->h + CODE_T - 1) / CODE_T;
     hipLaunchKernelGGL(k_dyn_code_general, dim3(nchunk, CODE_GEN_Y), dim3(CODE_T), 0, hs, st, dfr, ld_fr,
-                       pend, nal, ld_nal, *g, x->rows, src, refs, x->meta, x->body_lo, x->body_hi, x->ctr);
+                       pend, nal, ld_nal, *g, x->rows, src, refs, x->meta, x->body_lo, x->body_hi, x->body_w,
+                       x->ctr);
     if (hipGetLastError() != hipSuccess) return -1;
     hipLaunchKernelGGL(k_dyn_row<false>, dim3(g->h, nframes, S), dim3(row_threads(g->w)),
                        row_lds_bytes(g->w, mbw), hs, st, nal, ld_nal, pend, dfr, ld_fr, *g, x->rows, src, refs,
-                       x->meta, x->body_lo, x->body_hi, x->tcx, epoch, x->rowstage, x->gbits, x->spill, x->ctr,
-                       stamps);
+                       x->meta, x->body_lo, x->body_hi, x->body_w, x->tcx, epoch, x->rowstage, x->gbits, x->spill,
+                       x->ctr, stamps);
     if (hipGetLastError() != hipSuccess) return -1;
     /* the general path: one row workgroup per record slot that may be taken */
     hipLaunchKernelGGL(k_dyn_row<true>, dim3(g->h, std::min<uint32_t>(g->gen_cap, (uint32_t)(nframes * S)), 1),
                        dim3(row_threads(g->w)),
                        row_lds_bytes(g->w, mbw), hs, st, nal, ld_nal, pend, dfr, ld_fr, *g, x->rows, src, refs,
-                       x->meta, x->body_lo, x->body_hi, x->tcx, epoch, x->rowstage, x->gbits, x->spill, x->ctr,
-                       stamps);
+                       x->meta, x->body_lo, x->body_hi, x->body_w, x->tcx, epoch, x->rowstage, x->gbits, x->spill,
+                       x->ctr, stamps);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -38,7 +38,8 @@ typedef struct {
     int32_t n_slow;               /* NALs routed to the serial device path      */
     uint64_t batch_bytes;         /* bytes appended by this batch               */
     uint64_t undelivered;         /* arena bytes not yet packed to the host (output_to_host) */
-    uint32_t pad[18];
+    int32_t dyn_qp;               /* the dynamic rect's QP, 0..51 (scroll_batch_set_dyn_qp) */
+    uint32_t pad[17];
 } DevStream;
 
 /* One planned NAL unit (32 bytes). */

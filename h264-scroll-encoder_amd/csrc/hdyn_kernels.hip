@@ -42,7 +42,6 @@ using namespace scroll::hint;
 
 namespace {
 
-constexpr QParams HQ = qparams(QP_DEFAULT);   /* the rect under hints codes at QP 26 */
 
 __constant__ Tabs h_tabs = SCROLL_DYN_TABS;
 
@@ -64,27 +63,6 @@ __device__ inline void lds_wave_sync()
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
-
-/* drops the first `skip` bits (the coeff_token) of what is put */
-template <class S>
-struct SkipSink {
-    S &in;
-    uint32_t skip;
-    __device__ inline void put(uint32_t v, int n)
-    {
-        if (n <= 0) return;
-        if (skip >= (uint32_t)n) {
-            skip -= (uint32_t)n;
-            return;
-        }
-        if (skip) {
-            n -= (int)skip;
-            v &= low_mask(n);
-            skip = 0;
-        }
-        in.put(v, n);
-    }
-};
 
 struct LdsOrW {
     uint32_t *b;
@@ -166,6 +144,9 @@ __global__ __launch_bounds__(HD_T) void k_hdyn_code(const DevStream *__restrict_
         }
         return;
     }
+    /* the frame's rect QP (scroll_batch_set_dyn_qp / _stream / _at) */
+    const int qpy = __builtin_amdgcn_readfirstlane(SF.hd_qp);
+    const QParams HQ = qparams_rt(qpy), HQC = qparams_rt(qp_chroma(qpy));
     const int mvx = me.mx / 4, mvy = me.my / 4, W = c.w, Hh = c.h;
     const uint32_t ysz = (uint32_t)W * (uint32_t)Hh;
     const uint8_t *rp = refs + (size_t)s * g.ref_ld;
@@ -222,7 +203,7 @@ __global__ __launch_bounds__(HD_T) void k_hdyn_code(const DevStream *__restrict_
         } else {
             const int p = (t - 16) >> 2, k = (t - 16) & 3, pc = 18 + 4 * p + k;
             L.wdc[p][k] = Wc[0];
-            for (int k2 = 1; k2 < 16; ++k2) L.lev[pc][k2 - 1] = quant(Wc[ZZ[k2]], ZZ[k2], HQ);
+            for (int k2 = 1; k2 < 16; ++k2) L.lev[pc][k2 - 1] = quant(Wc[ZZ[k2]], ZZ[k2], HQC);
             L.lev[pc][15] = 0;
         }
     }
@@ -230,10 +211,10 @@ __global__ __launch_bounds__(HD_T) void k_hdyn_code(const DevStream *__restrict_
     if (t == 24 || t == 25) {                               /* chroma DC 2x2 Hadamard */
         const int p = t - 24;
         const int d0 = L.wdc[p][0], d1 = L.wdc[p][1], d2 = L.wdc[p][2], d3 = L.wdc[p][3];
-        L.lev[16 + p][0] = quant_dc(d0 + d1 + d2 + d3, HQ);
-        L.lev[16 + p][1] = quant_dc(d0 - d1 + d2 - d3, HQ);
-        L.lev[16 + p][2] = quant_dc(d0 + d1 - d2 - d3, HQ);
-        L.lev[16 + p][3] = quant_dc(d0 - d1 - d2 + d3, HQ);
+        L.lev[16 + p][0] = quant_dc(d0 + d1 + d2 + d3, HQC);
+        L.lev[16 + p][1] = quant_dc(d0 - d1 + d2 - d3, HQC);
+        L.lev[16 + p][2] = quant_dc(d0 + d1 - d2 - d3, HQC);
+        L.lev[16 + p][3] = quant_dc(d0 - d1 - d2 + d3, HQC);
     }
     lds_wave_sync();
 
@@ -296,6 +277,7 @@ __global__ __launch_bounds__(HD_T) void k_hdyn_code(const DevStream *__restrict_
         dcn = L.tc[16] + L.tc[17];
         for (int k = 18; k < 26; ++k) acn += L.tc[k];
         r.cbp = (uint8_t)(cbp_l | (acn ? 2 : (dcn ? 1 : 0)) << 4);
+        if (r.cbp) atomicMin(&spf[fi].hd_first, (uint32_t)q);    /* the mb_qp_delta chain's first MB */
         uint32_t body = 0;
         for (int k = 0; k < 26; ++k) {
             r.tc[k] = L.tc[k];
@@ -313,7 +295,10 @@ __global__ __launch_bounds__(HD_T) void k_hdyn_code(const DevStream *__restrict_
 __global__ void k_hdyn_reset(SpliceFrame *__restrict__ spf, int ld_fr)
 {
     SpliceFrame &F = spf[(size_t)blockIdx.y * ld_fr + blockIdx.x];
-    if (F.w > 0) F.status = SCROLL_SPLICE_OK;
+    if (F.w > 0) {
+        F.status = SCROLL_SPLICE_OK;
+        F.hd_first = ~0u;
+    }
 }
 
 }  // namespace

@@ -77,9 +77,12 @@ enum { IP_COUNT = 0, IP_WRITE = 1, IP_WRITE_STAGED = 2 };
 template <int MODE>
 __global__ __launch_bounds__(IT) void k_ipcm(IpcmGeom G, const uint8_t *__restrict__ pics,
                                              uint32_t *__restrict__ counts, uint8_t *__restrict__ out,
-                                             uint8_t *__restrict__ stg, uint64_t stg_stride)
+                                             uint8_t *__restrict__ stg, uint64_t stg_stride,
+                                             uint32_t *__restrict__ over)
 {
     constexpr bool WRITE = MODE != IP_COUNT;
+    if (!WRITE && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) *over = 0u;   /* k_ipcm_size sets it */
+    if (WRITE && __builtin_amdgcn_readfirstlane(*over)) return;    /* a file past out_stride: none written */
     __shared__ alignas(16) uint8_t rb[LB + CH];
     __shared__ alignas(16) uint8_t ob[16 + CH + CH / 2 + 16];
     __shared__ int32_t wsm[IT / 64];
@@ -317,20 +320,42 @@ __global__ __launch_bounds__(IT) void k_ipcm(IpcmGeom G, const uint8_t *__restri
     }
 }
 
+/* grid (n): file n's size = prefix + RBSP + its chunks' EP bytes; any file
+ * past out_stride sets *over (the write pass then writes nothing) */
+__global__ __launch_bounds__(IT) void k_ipcm_size(IpcmGeom G, const uint32_t *__restrict__ counts,
+                                                  uint64_t *__restrict__ sizes, uint32_t *__restrict__ over)
+{
+    __shared__ uint32_t wss[IT / 64];
+    const int t = threadIdx.x;
+    const uint32_t n = blockIdx.x;
+    uint32_t ep = 0;
+    for (uint32_t k = (uint32_t)t; k < G.nchunk; k += IT) ep += counts[(size_t)n * G.nchunk + k];
+    uint32_t ex, tot;
+    block_excl_sum(ep, wss, ex, tot);
+    if (t == 0) {
+        const uint64_t sz = (uint64_t)G.npre + G.rbsp_len + tot;
+        sizes[n] = sz;
+        if (sz > G.out_stride) atomicOr(over, 1u);
+    }
+}
+
 }  // namespace
 
 int ipcm_launch(hipStream_t hs, int pass, int n, const IpcmGeom *g, const uint8_t *pics,
-                uint32_t *counts, uint8_t *out, uint8_t *stg, uint64_t stg_stride)
+                uint32_t *counts, uint8_t *out, uint8_t *stg, uint64_t stg_stride, uint64_t *sizes, uint32_t *over)
 {
     if (n <= 0) return 0;
-    if (pass == 0)
+    if (pass == 0) {
         hipLaunchKernelGGL(k_ipcm<IP_COUNT>, dim3(g->nchunk, n), dim3(IT), 0, hs, *g, pics, counts, out, stg,
-                           stg_stride);
-    else if (stg)
+                           stg_stride, over);
+        if (hipGetLastError() != hipSuccess) return -1;
+        hipLaunchKernelGGL(k_ipcm_size, dim3(n), dim3(IT), 0, hs, *g, counts, sizes, over);
+    } else if (stg) {
         hipLaunchKernelGGL(k_ipcm<IP_WRITE_STAGED>, dim3(g->nchunk, n), dim3(IT), 0, hs, *g, pics, counts, out,
-                           stg, stg_stride);
-    else
+                           stg, stg_stride, over);
+    } else {
         hipLaunchKernelGGL(k_ipcm<IP_WRITE>, dim3(g->nchunk, n), dim3(IT), 0, hs, *g, pics, counts, out, stg,
-                           stg_stride);
+                           stg_stride, over);
+    }
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -945,6 +945,7 @@ struct ScrollBatch {
      * every frame's rect MBs are coded by k_hdyn_code into splice records
      * (d_sp_rec, word pool d_sp_rbsp) and composed by k_splice_stage */
     std::vector<int32_t> h_dyn_pos;    /* [2 (s * max_frames + f)]: rect origin, x0 < 0: none */
+    std::vector<int32_t> h_dyn_qp;     /* [s * max_frames + f]: the frame's rect QP under hints, -1: the stream's */
     int dyn_pos_custom = 0;            /* some frame's origin differs from the batch rect */
     int dyn_qp = 26;                   /* the rect's QP (scroll_batch_set_dyn_qp)          */
     int hd_dirty = 0;                  /* d_spf / HintFrame of the combined frames out of date */
@@ -1186,8 +1187,15 @@ int scroll_batch_add_stream(ScrollBatch *b, const ComposerConfig *cfg)
     if (rc) return rc;
     int s = b->nstreams;
     DevStream *d = &b->h_st[s];
+    if (b->dyn_qp != 26 && !cfg->deblocking_filter_control_present_flag) {
+        set_err("scroll_batch_add_stream: a stream with the deblocking filter on (no "
+                "deblocking_filter_control_present_flag) needs the rect at QP 26, the batch's is %d",
+                b->dyn_qp);
+        return SCROLL_ERR_CONFIG;
+    }
     memset(d, 0, sizeof(*d));
     cfg_to_dev(cfg, d);
+    d->dyn_qp = b->dyn_qp;
     d->out_pos = 0;
     d->out_cap = b->arena_bytes;
     HIPCHK(hipSetDevice(b->device));
@@ -1817,6 +1825,7 @@ static void dyn_release(ScrollBatch *b)
     (void)hipFree(b->dx.meta);
     (void)hipFree(b->dx.body_lo);
     (void)hipFree(b->dx.body_hi);
+    (void)hipFree(b->dx.body_w);
     (void)hipFree(b->dx.tcx);
     (void)hipFree(b->dx.rowstage);
     (void)hipFree(b->dx.ctr);
@@ -1826,6 +1835,7 @@ static void dyn_release(ScrollBatch *b)
     b->dyn_on = 0;
     b->dyn_refs = 0;
     b->h_dyn_pos.clear();
+    b->h_dyn_qp.clear();
     b->dyn_pos_custom = 0;
     if (b->hint_on) {                  /* the combined frames become plain hint frames */
         b->geo.x0 = b->geo.y0 = b->geo.w = b->geo.h = 0;
@@ -1927,6 +1937,7 @@ int scroll_batch_set_dyn_rect(ScrollBatch *b, int x0, int y0, int w, int h, size
     if (e == hipSuccess) e = hipMalloc(&b->dx.meta, nrec * sizeof(uint16_t));
     if (e == hipSuccess) e = hipMalloc(&b->dx.body_lo, nrec * sizeof(uint2));
     if (e == hipSuccess) e = hipMalloc(&b->dx.body_hi, nrec * sizeof(uint2));
+    if (e == hipSuccess) e = hipMalloc(&b->dx.body_w, nrec * sizeof(uint4));
     const size_t ng = (size_t)g.ngroups;
     if (e == hipSuccess) e = hipMalloc(&b->dx.tcx, S * F * w * h * sizeof(unsigned long long));
     if (e == hipSuccess) e = hipMemset(b->dx.tcx, 0, S * F * w * h * sizeof(unsigned long long));
@@ -1950,6 +1961,7 @@ int scroll_batch_set_dyn_rect(ScrollBatch *b, int x0, int y0, int w, int h, size
     b->geo = g;
     b->dyn_on = 1;
     b->h_dyn_pos.assign(2 * S * F, 0);
+    b->h_dyn_qp.assign(S * F, -1);
     for (size_t i = 0; i < S * F; ++i) {
         b->h_dyn_pos[2 * i] = x0;
         b->h_dyn_pos[2 * i + 1] = y0;
@@ -1999,15 +2011,18 @@ static int dyn_grow_pools(ScrollBatch *b)
     const size_t rs_words = S * F * g.rs_frame_words + (size_t)g.rs_spill_cap * g.rs_spill_words;
     uint16_t *meta = nullptr;
     uint2 *lo = nullptr, *hi = nullptr;
+    uint4 *wd = nullptr;
     uint32_t *rs = nullptr;
     hipError_t e = hipMalloc(&meta, nrec * sizeof(uint16_t));
     if (e == hipSuccess) e = hipMalloc(&lo, nrec * sizeof(uint2));
     if (e == hipSuccess) e = hipMalloc(&hi, nrec * sizeof(uint2));
+    if (e == hipSuccess) e = hipMalloc(&wd, nrec * sizeof(uint4));
     if (e == hipSuccess) e = hipMalloc(&rs, rs_words * sizeof(uint32_t));
     if (e != hipSuccess) {
         (void)hipFree(meta);
         (void)hipFree(lo);
         (void)hipFree(hi);
+        (void)hipFree(wd);
         (void)hipFree(rs);
         (void)hipGetLastError();
         return e == hipErrorOutOfMemory ? SCROLL_ERR_OOM : SCROLL_ERR_HIP;
@@ -2015,10 +2030,12 @@ static int dyn_grow_pools(ScrollBatch *b)
     (void)hipFree(b->dx.meta);
     (void)hipFree(b->dx.body_lo);
     (void)hipFree(b->dx.body_hi);
+    (void)hipFree(b->dx.body_w);
     (void)hipFree(b->dx.rowstage);
     b->dx.meta = meta;
     b->dx.body_lo = lo;
     b->dx.body_hi = hi;
+    b->dx.body_w = wd;
     b->dx.rowstage = rs;
     b->dx.spill = rs + S * F * g.rs_frame_words;
     b->geo.gen_cap = g.gen_cap;
@@ -2245,28 +2262,80 @@ static int hd_upload(ScrollBatch *b)
         o.h = b->geo.h;
         o.rbsp_word = i * nmb * b->hd_mb_words;
         o.rec_first = (uint32_t)(i * nmb);
+        const int fq = i < b->h_dyn_qp.size() ? b->h_dyn_qp[i] : -1;
+        const size_t st = i / F;
+        o.hd_qp = fq >= 0 ? fq : (st < (size_t)b->nstreams ? b->h_st[st].dyn_qp : b->dyn_qp);
     }
     HIPCHK(hipMemcpy(b->d_spf, spf.data(), S * F * sizeof(SpliceFrame), hipMemcpyHostToDevice));
     b->hd_dirty = 0;
     return SCROLL_OK;
 }
 
-int scroll_batch_set_dyn_qp(ScrollBatch *b, int qp)
+/* the rect's QP of stream s (every stream: s < 0); with the deblocking
+ * filter on (no deblocking_filter_control_present_flag: ingested streams may
+ * have it) a QP other than 26 would change the filtering of the scroll
+ * region's MBs (their QP follows the slice / the coded MBs before them), so
+ * it is refused for such streams */
+static int set_stream_qp(ScrollBatch *b, int s, int qp, const char *who)
 {
-    if (!b || qp < SCROLL_DYN_QP_MIN || qp > SCROLL_DYN_QP_MAX) {
-        set_err("scroll_batch_set_dyn_qp: QP %d outside %d..%d", qp, SCROLL_DYN_QP_MIN, SCROLL_DYN_QP_MAX);
+    if (!b || qp < SCROLL_DYN_QP_MIN || qp > SCROLL_DYN_QP_MAX || s >= b->nstreams) {
+        set_err("%s: QP %d outside %d..%d or stream %d out of range", who, qp, SCROLL_DYN_QP_MIN,
+                SCROLL_DYN_QP_MAX, s);
         return SCROLL_ERR_ARG;
     }
-    if (b->hint_on && qp != 26) {
-        set_err("scroll_batch_set_dyn_qp: the rect under UI hints codes at QP 26");
+    const int s0 = s < 0 ? 0 : s, s1 = s < 0 ? b->nstreams : s + 1;
+    for (int k = s0; k < s1; ++k)
+        if (qp != 26 && !b->h_st[k].deblock) {
+            set_err("%s: stream %d has the deblocking filter on (no "
+                    "deblocking_filter_control_present_flag): its rect codes at QP 26", who, k);
+            return SCROLL_ERR_CONFIG;
+        }
+    int rc = batch_host_sync(b);
+    if (rc) return rc;
+    HIPCHK(hipSetDevice(b->device));
+    for (int k = s0; k < s1; ++k) {
+        b->h_st[k].dyn_qp = qp;
+        HIPCHK(hipMemcpy(&b->d_st[k].dyn_qp, &qp, sizeof(int32_t), hipMemcpyHostToDevice));
+    }
+    if (s < 0) b->dyn_qp = qp;         /* streams added later */
+    b->hd_dirty = 1;                   /* under hints: frames without their own QP follow the stream */
+    return SCROLL_OK;
+}
+
+int scroll_batch_set_dyn_qp(ScrollBatch *b, int qp)
+{
+    return set_stream_qp(b, -1, qp, "scroll_batch_set_dyn_qp");
+}
+
+int scroll_batch_set_dyn_qp_stream(ScrollBatch *b, int s, int qp)
+{
+    if (!b || s < 0) {
+        set_err("scroll_batch_set_dyn_qp_stream: bad stream");
+        return SCROLL_ERR_ARG;
+    }
+    return set_stream_qp(b, s, qp, "scroll_batch_set_dyn_qp_stream");
+}
+
+int scroll_batch_set_dyn_qp_at(ScrollBatch *b, int s, int f, int qp)
+{
+    if (!b || !b->hint_on || !b->dyn_on || s < 0 || s >= b->nstreams || f < 0 || f >= b->max_frames ||
+        qp < -1 || qp > SCROLL_DYN_QP_MAX) {
+        set_err("scroll_batch_set_dyn_qp_at: needs UI hints and the dynamic rect; stream / frame / QP "
+                "(-1, 0..%d) out of range", SCROLL_DYN_QP_MAX);
+        return SCROLL_ERR_ARG;
+    }
+    if (qp >= 0 && qp != 26 && !b->h_st[s].deblock) {
+        set_err("scroll_batch_set_dyn_qp_at: stream %d has the deblocking filter on: its rect codes at QP 26",
+                s);
         return SCROLL_ERR_CONFIG;
     }
     int rc = batch_host_sync(b);
     if (rc) return rc;
-    b->dyn_qp = qp;
-    b->geo.qp = qp;                    /* kernels take the geometry by value at launch */
-    b->geo.ql = scroll::dyn::qparams(qp);
-    b->geo.qc = scroll::dyn::qparams(scroll::dyn::qp_chroma(qp));
+    const size_t i = (size_t)s * b->max_frames + f;
+    if (b->h_dyn_qp.size() < (size_t)b->max_streams * b->max_frames)
+        b->h_dyn_qp.assign((size_t)b->max_streams * b->max_frames, -1);
+    b->h_dyn_qp[i] = qp;
+    b->hd_dirty = 1;
     return SCROLL_OK;
 }
 
@@ -2288,10 +2357,6 @@ int scroll_batch_set_hints(ScrollBatch *b, int s, int f, const ScrollHintRect *r
                     r.ref, r.mv_x, r.mv_y);
             return SCROLL_ERR_ARG;
         }
-    }
-    if (!b->hint_on && b->dyn_qp != 26) {
-        set_err("scroll_batch_set_hints: the dynamic rect's QP is %d; under UI hints it codes at 26", b->dyn_qp);
-        return SCROLL_ERR_CONFIG;
     }
     int rc = batch_host_sync(b);
     if (rc) return rc;
@@ -2404,6 +2469,7 @@ static int splice_upload(ScrollBatch *b)
 {
     const size_t S = (size_t)b->max_streams, F = (size_t)b->max_frames;
     std::vector<SpliceFrame> spf(S * F);
+    for (SpliceFrame &o : spf) o.hd_qp = -1;             /* spliced slices keep their own QP chain */
     std::vector<int32_t> list;
     std::vector<uint8_t> pool;
     size_t words = 0, recs = 0, nunits = 0, slot = b->geo.slot_bytes;
@@ -2413,6 +2479,7 @@ static int splice_upload(ScrollBatch *b)
         const ScrollBatch::SpliceHost &h = b->h_sp[i];
         SpliceFrame &o = spf[i];
         o = SpliceFrame{};
+        o.hd_qp = -1;
         if (h.w <= 0) continue;
         o.x0 = h.x0;
         o.y0 = h.y0;
@@ -2827,7 +2894,9 @@ int scroll_batch_ipcm_files_device(ScrollBatch *b, int n, int w, int h, const ui
     }
     g.rbsp_len = (uint32_t)(g.nh - 2 + 386 * nmb + 1);
     g.nchunk = (g.rbsp_len + IPCM_CHUNK - 1) / IPCM_CHUNK;
-    const size_t need = (size_t)n * g.nchunk * sizeof(uint32_t);
+    /* counts [n][nchunk] u32, then sizes [n] u64, then the over flag */
+    const size_t cnt_bytes = ((size_t)n * g.nchunk * sizeof(uint32_t) + 7) & ~(size_t)7;
+    const size_t need = cnt_bytes + (size_t)n * sizeof(uint64_t) + sizeof(uint64_t);
     if (need > b->ipcm_cap) {
         (void)hipFree(b->d_ipcm_cnt);
         b->d_ipcm_cnt = nullptr;
@@ -2860,43 +2929,32 @@ int scroll_batch_ipcm_files_device(ScrollBatch *b, int n, int w, int h, const ui
             if (!e) HIPCHK(timing_event(&e));
         HIPCHK(hipEventRecord(b->ing_ev[0], hs));
     }
-    if (ipcm_launch(hs, 0, n, &g, d_pics, b->d_ipcm_cnt, d_out, stg, stg_stride)) {
-        set_err("ipcm launch: %s", hipGetErrorString(hipGetLastError()));
-        return SCROLL_ERR_HIP;
-    }
-    std::vector<uint32_t> cnt((size_t)n * g.nchunk);
-    HIPCHK(hipMemcpyAsync(cnt.data(), b->d_ipcm_cnt, need, hipMemcpyDeviceToHost, hs));
-    HIPCHK(hipStreamSynchronize(hs));
-    float ms0 = 0.0f;
-    if (b->timing) {
-        HIPCHK(hipEventRecord(b->ing_ev[1], hs));
-        HIPCHK(hipEventSynchronize(b->ing_ev[1]));
-        HIPCHK(hipEventElapsedTime(&ms0, b->ing_ev[0], b->ing_ev[1]));
-    }
-    int over = -1;
-    for (int k = 0; k < n; ++k) {
-        uint64_t ep = 0;
-        for (uint32_t c = 0; c < g.nchunk; ++c) ep += cnt[(size_t)k * g.nchunk + c];
-        sizes[k] = g.npre + (uint64_t)g.rbsp_len + ep;
-        if (sizes[k] > out_stride && over < 0) over = k;
-    }
-    if (over >= 0) {
-        set_err("scroll_batch_ipcm_files: file %d needs %llu bytes, out_stride is %zu", over,
-                (unsigned long long)sizes[over], out_stride);
-        return SCROLL_ERR_OVERFLOW;
-    }
-    if (b->timing) HIPCHK(hipEventRecord(b->ing_ev[0], hs));
-    if (ipcm_launch(hs, 1, n, &g, d_pics, b->d_ipcm_cnt, d_out, stg, stg_stride)) {
+    uint64_t *d_sizes = reinterpret_cast<uint64_t *>(reinterpret_cast<uint8_t *>(b->d_ipcm_cnt) + cnt_bytes);
+    uint32_t *d_over = reinterpret_cast<uint32_t *>(d_sizes + n);
+    /* count pass, sizes and the overflow check, write pass: no host step in
+     * between (the write pass writes nothing when a file is over) */
+    if (ipcm_launch(hs, 0, n, &g, d_pics, b->d_ipcm_cnt, d_out, stg, stg_stride, d_sizes, d_over) ||
+        ipcm_launch(hs, 1, n, &g, d_pics, b->d_ipcm_cnt, d_out, stg, stg_stride, d_sizes, d_over)) {
         set_err("ipcm launch: %s", hipGetErrorString(hipGetLastError()));
         return SCROLL_ERR_HIP;
     }
     if (b->timing) HIPCHK(hipEventRecord(b->ing_ev[1], hs));
+    uint32_t over_flag = 0;
+    HIPCHK(hipMemcpyAsync(sizes, d_sizes, (size_t)n * sizeof(uint64_t), hipMemcpyDeviceToHost, hs));
+    HIPCHK(hipMemcpyAsync(&over_flag, d_over, sizeof(uint32_t), hipMemcpyDeviceToHost, hs));
     HIPCHK(hipStreamSynchronize(hs));
     if (b->timing) {
-        float ms1 = 0.0f;
-        HIPCHK(hipEventElapsedTime(&ms1, b->ing_ev[0], b->ing_ev[1]));
-        b->ipcm_ms += (double)ms0 + ms1;
+        float ms = 0.0f;
+        HIPCHK(hipEventElapsedTime(&ms, b->ing_ev[0], b->ing_ev[1]));
+        b->ipcm_ms += ms;
         b->ipcm_n++;
+    }
+    if (over_flag) {
+        int over = 0;
+        while (over < n && sizes[over] <= out_stride) ++over;
+        set_err("scroll_batch_ipcm_files: file %d needs %llu bytes, out_stride is %zu", over,
+                (unsigned long long)sizes[over < n ? over : 0], out_stride);
+        return SCROLL_ERR_OVERFLOW;
     }
     return SCROLL_OK;
 }
@@ -3131,8 +3189,15 @@ int scroll_engine_write_nals(const ComposerConfig *cfg, const NalDesc *nals, int
     rc = temp_batch(1, n, round_arena(cap), SCROLL_MODE_COMPOSER, &b);
     if (rc) return rc;
     DevStream *d = &b->h_st[0];
+    if (b->dyn_qp != 26 && !cfg->deblocking_filter_control_present_flag) {
+        set_err("scroll_batch_add_stream: a stream with the deblocking filter on (no "
+                "deblocking_filter_control_present_flag) needs the rect at QP 26, the batch's is %d",
+                b->dyn_qp);
+        return SCROLL_ERR_CONFIG;
+    }
     memset(d, 0, sizeof(*d));
     cfg_to_dev(cfg, d);
+    d->dyn_qp = b->dyn_qp;
     d->out_pos = 0;
     d->out_cap = cap;
     d->nnal = n;

@@ -41,6 +41,12 @@ typedef struct {
     int32_t stage_status;           /* k_splice_stage of the last compose         */
     uint32_t unit_first;            /* first unit slot                            */
     int32_t nunits;                 /* NAL units found (k_splice_units; may exceed the slots) */
+    /* the dynamic rect under hints (k_hdyn_code's frames; -1 for spliced
+     * slices): its MBs' QP; the first of its MBs (raster) with a residual
+     * (k_hdyn_reset: ~0, then atomicMin) carries mb_qp_delta hd_qp - 26, the
+     * others 0 (the chain from the slice QP 26) */
+    int32_t hd_qp;
+    uint32_t hd_first;
 } SpliceFrame;
 
 /* one NAL unit (slice) of a spliced picture: its bytes [b, e) of the

@@ -609,7 +609,7 @@ __global__ __launch_bounds__(64) void k_splice_unesc(int n, const int32_t *__res
         const uint32_t h0 = len ? U(p[0]) : 0u;
         const uint32_t w0 = (ub + 3u) >> 2;
         uint32_t nb = 0, end = 0;
-        const bool ok = len >= 2 && !(h0 & 0x80) && (h0 & 31) == 1;
+        const bool ok = len >= 2 && !(h0 & 0x80) && ((h0 & 31) == 1 || (h0 & 31) == 5);   /* non-IDR / IDR slice */
         if (ok) {
             uint32_t *o = rbsp + F->rbsp_word + w0;
             const uint32_t nwmax = (len + 2u) / 4u;
@@ -887,30 +887,34 @@ __global__ __launch_bounds__(64 * LANE_WAVES) void k_splice_lanes(const int32_t 
         const int mbw_c = S.w / 16, x0c = F->x0, y0c = F->y0;
         SpliceMbRec *rec = recs + F->rec_first;
         const uint32_t w0 = UN->w0, nbytes = UN->nbytes, end = UN->end, base = 32u * w0;
-        const int ref_idc = (int)(F->nal[UN->b] >> 5) & 3;
+        const uint32_t h0 = F->nal[UN->b];
+        const int ref_idc = (int)(h0 >> 5) & 3;
+        const bool idr = (h0 & 31u) == 5u;
         LRd r;
         r.init(rbsp + F->rbsp_word + w0, (nbytes + 3u) >> 2, 8u * nbytes);
         int status = SCROLL_SPLICE_ERR_HEADER, first = -1, m = 0;
         int fq_mb = -1, fq_qp = 0, last_qp = 0;
         int nrefs = 2;
         int qp = 0;
-        bool go = true;
+        bool go = true, islice = false;
         first = (int)r.ue();
         {
             const uint32_t stype = r.ue();
-            if (stype != 0 && stype != 5) go = false;
+            islice = stype == 2 || stype == 7;
+            if ((stype != 0 && stype != 5 && !islice) || (idr && !islice)) go = false;   /* P / I (IDR: I) */
         }
         if (go && r.ue() != 0) go = false;
         if (go) {
             r.skip(S.log2_mfn);
+            if (idr) r.ue();                                   /* idr_pic_id */
             if (S.poc_type == 0) r.skip(S.log2_poc);
-            if (r.u(1)) {
+            if (!islice && r.u(1)) {
                 const uint32_t k = r.ue();
                 if (k > 31) go = false;
                 nrefs = (int)k + 1;
             }
         }
-        if (go && r.u(1)) {
+        if (go && !islice && r.u(1)) {
             for (int k = 0;; ++k) {
                 const uint32_t idc = r.ue();
                 if (r.bad || r.over() || k > 32) {
@@ -925,7 +929,9 @@ __global__ __launch_bounds__(64 * LANE_WAVES) void k_splice_lanes(const int32_t 
                 }
             }
         }
-        if (go && ref_idc && r.u(1)) {
+        if (go && ref_idc && idr) {
+            r.skip(2);                                         /* no_output_of_prior_pics, long_term_reference */
+        } else if (go && ref_idc && r.u(1)) {
             for (int k = 0;; ++k) {
                 const uint32_t op = r.ue();
                 if (r.bad || r.over() || k > 64 || op > 6) {
@@ -996,7 +1002,7 @@ __global__ __launch_bounds__(64 * LANE_WAVES) void k_splice_lanes(const int32_t 
             bool fail = false;
             for (bool first_mb = true; !fail; first_mb = false) {
                 if (r.p >= end && !first_mb) break;
-                const uint32_t run = r.ue();
+                const uint32_t run = islice ? 0u : r.ue();            /* I slices: no mb_skip_run */
                 if (r.bad || r.over() || run > (uint32_t)(nmb - m)) {
                     fail = true;
                     break;
@@ -1052,7 +1058,7 @@ __global__ __launch_bounds__(64 * LANE_WAVES) void k_splice_lanes(const int32_t 
                     break;
                 }
                 const bool aA = x > 0 && m - 1 >= m0, aC = y > 0 && x + 1 < W && m - W + 1 >= m0;
-                const uint32_t mbt = r.ue();
+                const uint32_t mbt = r.ue() + (islice ? 5u : 0u);    /* an I slice's k: the P slice's 5 + k */
                 if (r.bad || r.over() || mbt > 30u) {
                     fail = true;
                     break;
@@ -1412,23 +1418,27 @@ __global__ __launch_bounds__(64) void k_splice_parse(int n, const int32_t *__res
     if (W > PARSE_MAXW) goto done;
     {
     const int ref_idc = (int)(h0 >> 5) & 3;
+    const bool idr = (h0 & 31u) == 5u;
     r.init(rbsp + F->rbsp_word + w0, (nb + 3u) >> 2, 8u * nb);
 
     int nrefs = 2;                         /* the composer's PPS (h264_writer.c:114) */
     first = (int)r.ue();                                           /* first_mb_in_slice */
+    bool islice;
     {
         const uint32_t stype = r.ue();
-        if (stype != 0 && stype != 5) goto done;
+        islice = stype == 2 || stype == 7;
+        if ((stype != 0 && stype != 5 && !islice) || (idr && !islice)) goto done;   /* P / I (IDR: I) */
     }
     if (r.ue() != 0) goto done;                                    /* pps id */
     r.skip(S.log2_mfn);
+    if (idr) r.ue();                                               /* idr_pic_id */
     if (S.poc_type == 0) r.skip(S.log2_poc);
-    if (r.u(1)) {
+    if (!islice && r.u(1)) {
         const uint32_t k = r.ue();
         if (k > 31) goto done;
         nrefs = (int)k + 1;
     }
-    if (r.u(1)) {                          /* list modification: the composed list only */
+    if (!islice && r.u(1)) {               /* list modification: the composed list only */
         for (int k = 0;; ++k) {
             const uint32_t idc = r.ue();
             if (r.bad || r.over() || k > 32) {
@@ -1439,7 +1449,9 @@ __global__ __launch_bounds__(64) void k_splice_parse(int n, const int32_t *__res
             if (idc != 2 || r.ue() != (uint32_t)k) goto done;
         }
     }
-    if (ref_idc && r.u(1)) {                                       /* MMCO */
+    if (ref_idc && idr) {
+        r.skip(2);                                                 /* no_output_of_prior_pics, long_term_reference */
+    } else if (ref_idc && r.u(1)) {                                /* MMCO */
         for (int k = 0;; ++k) {
             const uint32_t op = r.ue();
             if (r.bad || r.over() || k > 64 || op > 6) {
@@ -1525,7 +1537,7 @@ __global__ __launch_bounds__(64) void k_splice_parse(int n, const int32_t *__res
         const int ts = tc_slot(lane);
         for (bool first_mb = true;; first_mb = false) {
             if (r.pos() >= end && !first_mb) break;
-            const uint32_t run = r.ue();
+            const uint32_t run = islice ? 0u : r.ue();                  /* I slices: no mb_skip_run */
             if (r.bad || r.over() || run > (uint32_t)(nmb - m)) goto done;
             for (uint32_t k = 0; k < run; ++k, next()) {          /* P_Skip */
                 avail();
@@ -1564,7 +1576,7 @@ __global__ __launch_bounds__(64) void k_splice_parse(int n, const int32_t *__res
             }
             if (m == nmb) goto done;
             avail();
-            const uint32_t mbt = r.ue();                               /* mb_type (Tables 7-13, 7-11) */
+            const uint32_t mbt = r.ue() + (islice ? 5u : 0u);          /* mb_type (Tables 7-13, 7-11) */
             if (r.bad || r.over() || mbt > 30) goto done;
             SpliceMbRec *R = rec + m;
             const uint8_t nbsame = (uint8_t)((aA ? 1 : 0) | (aB ? 2 : 0));
@@ -2142,6 +2154,8 @@ __global__ __launch_bounds__(DT) __attribute__((amdgpu_waves_per_eu(SCROLL_STAGE
 #pragma unroll
                     for (int q = 0; q < SPLICE_REC_HEAD / 16; ++q) hv[q] = hp[q];
                     __builtin_memcpy(&hd, hv, SPLICE_REC_HEAD);
+                    if (SF.hd_qp >= 0)                             /* the dynamic rect under hints: its QP chain */
+                        hd.qpd = (int8_t)((uint32_t)k == SF.hd_first ? SF.hd_qp - 26 : 0);
                     et = edge_tc(hd);
                     const SpliceMbRec &mb = hd;
                     me = Mv{mb.ref, mb.mx, mb.my};

@@ -178,6 +178,9 @@ def _load():
                                       [ctypes.c_size_t]),
         "scroll_batch_set_dyn_refs": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, u8p, u8p]),
         "scroll_batch_set_dyn_qp": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+        "scroll_batch_set_dyn_qp_stream": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]),
+        "scroll_batch_set_dyn_qp_at": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                                      ctypes.c_int]),
         "scroll_batch_set_dyn_source": (ctypes.c_int, [ctypes.c_void_p, u8p, ctypes.c_int]),
         "scroll_batch_set_dyn_rect_at": (ctypes.c_int, [ctypes.c_void_p] + [ctypes.c_int] * 4),
         "scroll_batch_dyn_source_device": (ctypes.c_void_p, [ctypes.c_void_p, P(ctypes.c_size_t),
@@ -585,10 +588,18 @@ class Batch:
     def set_dyn_rect(self, x0, y0, w, h, slot_bytes=0):
         self._chk(lib.scroll_batch_set_dyn_rect(self.h, x0, y0, w, h, slot_bytes), "set_dyn_rect")
 
-    def set_dyn_qp(self, qp):
-        """the rect's QP (22..51, default 26) for the following composes:
-        slice_qp_delta qp - 26 in the dynamic scroll NALs"""
-        self._chk(lib.scroll_batch_set_dyn_qp(self.h, qp), "set_dyn_qp")
+    def set_dyn_qp(self, qp, stream=None):
+        """the dynamic rect's QP (0..51) of every stream, or of one: its
+        scroll NALs carry slice_qp_delta qp - 26 (scroll_batch_set_dyn_qp /
+        _stream)"""
+        if stream is None:
+            self._chk(lib.scroll_batch_set_dyn_qp(self.h, qp), "set_dyn_qp")
+        else:
+            self._chk(lib.scroll_batch_set_dyn_qp_stream(self.h, stream, qp), "set_dyn_qp_stream")
+
+    def set_dyn_qp_at(self, s, f, qp):
+        """under UI hints: frame f of stream s at QP qp (-1: the stream's)"""
+        self._chk(lib.scroll_batch_set_dyn_qp_at(self.h, s, f, qp), "set_dyn_qp_at")
 
     def set_dyn_refs(self, ref_a, ref_b, stream=-1):
         """ref_a / ref_b: I420 bytes (w*h*3/2) of reference pictures A and B"""

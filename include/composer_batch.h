@@ -184,16 +184,27 @@ long long scroll_batch_last_nals(ScrollBatch *b);
  *       global stream ids stream_base + s and frame numbers t0 + f). */
 int scroll_batch_set_dyn_rect(ScrollBatch *b, int x0, int y0, int w, int h, size_t slot_bytes);
 int scroll_batch_set_dyn_refs(ScrollBatch *b, int s, const uint8_t *ref_a, const uint8_t *ref_b);
-/*   scroll_batch_set_dyn_qp(b, qp)   the rect's QP, 22..51 (default 26), for
- *       the following composes: the dynamic scroll NALs then carry
- *       slice_qp_delta = qp - 26 (chroma at QPc, Table 8-15) and their MBs
- *       mb_qp_delta 0; waypoint NALs and the P-only path are unchanged.  Not
- *       combinable with UI hints (their rect codes at 26): SCROLL_ERR_CONFIG.
- *       Below 22 a level of a +-255 residual would not fit the coder's packed
- *       8-bit levels (SCROLL_ERR_ARG). */
-#define SCROLL_DYN_QP_MIN 22
+/*   scroll_batch_set_dyn_qp(b, qp)   the rect's QP, 0..51 (default 26), of
+ *       every stream (and of streams added later), for the following
+ *       composes: a stream's dynamic scroll NALs then carry slice_qp_delta =
+ *       qp - 26 (chroma at QPc, Table 8-15) and their MBs mb_qp_delta 0;
+ *       waypoint NALs and the P-only path are unchanged.  Below 22 a NAL's
+ *       levels need 16 bits and it is coded on the general path (records in
+ *       HBM); levels are clamped to +-2063, the largest every CAVLC context
+ *       codes with level_prefix <= 15 (reached only by chroma DC below QPc 6).
+ *   scroll_batch_set_dyn_qp_stream(b, s, qp)   the same for stream s.
+ *   scroll_batch_set_dyn_qp_at(b, s, f, qp)    under UI hints (the rect in the
+ *       frame's hint record): frame f of stream s at QP qp, -1 = the
+ *       stream's.  There the slice QP stays 26 and the rect's first MB with a
+ *       residual carries mb_qp_delta qp - 26, the others 0.
+ *   A stream with the deblocking filter on (no
+ *   deblocking_filter_control_present_flag, e.g. an ingested one) keeps QP 26:
+ *   another QP would change the filtering of its scroll MBs (SCROLL_ERR_CONFIG). */
+#define SCROLL_DYN_QP_MIN 0
 #define SCROLL_DYN_QP_MAX 51
 int scroll_batch_set_dyn_qp(ScrollBatch *b, int qp);
+int scroll_batch_set_dyn_qp_stream(ScrollBatch *b, int s, int qp);
+int scroll_batch_set_dyn_qp_at(ScrollBatch *b, int s, int f, int qp);
 int scroll_batch_set_dyn_source(ScrollBatch *b, const uint8_t *src, int nframes);
 /* Under UI hints (scroll_batch_set_hints) the rect's MBs keep the hint
  * field's (ref, mv) -- full-pel luma, 2-D 1/8-pel chroma prediction at that

@@ -149,7 +149,13 @@ int or_qp_chroma(int qp)
     return qp < 30 ? qp : T[qp - 30];
 }
 
-/* pos = raster position in the 4x4 block; dc_chroma: 2x2 chroma DC */
+int or_dyn_qp(const or_dyn_rect *r)
+{
+    return r->qp == OR_DYN_QP0 ? 0 : (r->qp ? r->qp : OR_QP);
+}
+
+/* pos = raster position in the 4x4 block; dc_chroma: 2x2 chroma DC; the
+ * level clamped to +-OR_LEVEL_MAX (a bound only QP < 6 reaches) */
 int or_quant(int w, int qp, int pos, int dc_chroma)
 {
     const int i = pos / 4, j = pos % 4;
@@ -157,8 +163,9 @@ int or_quant(int w, int qp, int pos, int dc_chroma)
     const int qbits = 15 + qp / 6, f = (1 << qbits) / 6;
     const int mf = OR_MF[qp % 6][dc_chroma ? 0 : cls];
     const int a = w < 0 ? -w : w;
-    const int z = dc_chroma ? (int)(((int64_t)a * mf + 2 * f) >> (qbits + 1))
-                            : (int)(((int64_t)a * mf + f) >> qbits);
+    int z = dc_chroma ? (int)(((int64_t)a * mf + 2 * f) >> (qbits + 1))
+                      : (int)(((int64_t)a * mf + f) >> qbits);
+    if (z > OR_LEVEL_MAX) z = OR_LEVEL_MAX;
     return w < 0 ? -z : z;
 }
 
@@ -427,7 +434,7 @@ static void or_mb_levels(const or_cfg *c, const or_refs *R, const or_dyn_rect *r
     const int lw = 16 * rc->w, cw = 8 * rc->w;
     const uint8_t *sy = src, *su = src + (size_t)lw * 16 * rc->h, *sv = su + (size_t)cw * 8 * rc->h;
     const int lx0 = 16 * (mbx - rc->x0), ly0 = 16 * (mby - rc->y0);
-    const int qp = rc->qp ? rc->qp : OR_QP, qpc = or_qp_chroma(qp);
+    const int qp = or_dyn_qp(rc), qpc = or_qp_chroma(qp);
     for (int r = 0; r < 16; ++r) {
         const int bx = 4 * (r % 4), by = 4 * (r / 4);
         int res[16], W[16];
@@ -539,7 +546,7 @@ size_t or_scroll_nal_dyn(uint8_t *dst, size_t cap, or_cfg *c, int off, const or_
     uint8_t *rbsp = tl_rbsp;
     or_bits b;
     or_bits_init(&b, rbsp, rcap);
-    or_scroll_header_qpd(&b, c, rc->qp ? rc->qp - OR_QP : 0);   /* :549-553; the rect's QP */
+    or_scroll_header_qpd(&b, c, or_dyn_qp(rc) - OR_QP);   /* :549-553; the rect's QP */
 
     /* regions (:555-588) */
     int a_end = (c->h - off) / 16, wa = -1, woa = 0, wb = -1, wob = 0;

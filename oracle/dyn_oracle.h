@@ -51,9 +51,21 @@ extern "C" {
 
 typedef struct or_dyn_rect_s {
     int x0, y0, w, h;             /* MB units */
-    int qp;                       /* the rect's QP, 0 = 26 (slice_qp_delta qp - 26;
-                                   * chroma at QPc, Table 8-15); or_scroll_nal_dyn only */
+    int qp;                       /* the rect's QP: 0 = 26 (the default), 1..51, or
+                                   * OR_DYN_QP0 (-1) = QP 0.  Slice QP 26 + (QP - 26)
+                                   * (slice_qp_delta) in or_scroll_nal_dyn, the MBs'
+                                   * mb_qp_delta chain under hints; chroma at QPc
+                                   * (Table 8-15).  Levels are clamped to
+                                   * +-OR_LEVEL_MAX (only chroma DC below QPc 6
+                                   * reaches it; luma levels stay <= 1632) */
 } or_dyn_rect;
+#define OR_DYN_QP0 (-1)
+/* the largest |level| every CAVLC context codes with level_prefix <= 15
+ * (9.2.2.1: levelCode (15 << suffixLength) + 4095, suffixLength 0: 30 + 4095,
+ * so |level| <= 2063 always fits; baseline-profile streams allow no larger
+ * prefix) */
+#define OR_LEVEL_MAX 2063
+int or_dyn_qp(const or_dyn_rect *r);             /* the rect's QP, 0..51 */
 
 typedef struct {
     int w, h;                     /* luma size; chroma w/2 x h/2 */

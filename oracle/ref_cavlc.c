@@ -33,6 +33,33 @@ int ref_cavlc_parse(const uint8_t *rbsp, size_t n, size_t start_bit, int num_ref
     return rc;
 }
 
+/* the same for an I slice's MB layer (process_i_slice :1063-1360: a whole
+ * 20x20-MB picture, mb_type / prediction modes / cbp / residuals), its
+ * debug output silenced */
+static int quiet_begin(void);
+static void quiet_end(int saved);
+int ref_cavlc_parse_i(const uint8_t *rbsp, size_t n, size_t start_bit, size_t *end_bit)
+{
+    BitReader br;
+    bitreader_init(&br, rbsp, n);
+    for (size_t i = 0; i < start_bit; ++i) bitreader_read_bit(&br);
+    size_t cap = n * 4 + ((size_t)16 << 20);     /* + the walker's I_PCM padding MBs per row */
+    uint8_t *out = (uint8_t *)malloc(cap);
+    BitWriter bw;
+    bitwriter_init(&bw, out, cap);
+    free(top_mb_ctx);
+    top_mb_ctx = NULL;
+    top_mb_ctx_size = 0;
+    fflush(stdout);
+    const int saved = quiet_begin();
+    const int rc = process_i_slice(&br, &bw);
+    fflush(stdout);
+    quiet_end(saved);
+    *end_bit = bitreader_get_bit_position(&br);
+    free(out);
+    return rc;
+}
+
 /* ------------------------------------------------------------------------ */
 /* value-level check of one inter MB's residual (cbp me(v), mb_qp_delta,      */
 /* blocks), every decode step a reference function                          */

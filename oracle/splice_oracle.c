@@ -441,11 +441,12 @@ int or_splice_parse(const or_cfg *c, const or_splice *sp, or_splice_mb *mbs, uin
     for (int u = 0; u < nu && !err; ++u) {
         const uint8_t *p = sp->nal + ub[u];
         const size_t n = ue[u] - ub[u];
-        if (n < 2 || (p[0] & 0x80) || (p[0] & 31) != 1) {
+        const int nut = p[0] & 31;
+        if (n < 2 || (p[0] & 0x80) || (nut != 1 && nut != 5)) {  /* non-IDR or IDR slice */
             err = OR_SPLICE_ERR_NAL;
             break;
         }
-        const int ref_idc = (p[0] >> 5) & 3;
+        const int ref_idc = (p[0] >> 5) & 3, idr = nut == 5;
         const size_t rn = sp_unescape(rbsp + rb0, p + 1, n - 1);
         /* bit positions are kept relative to the whole rbsp[] (all slices) */
         rd_t r = {rbsp, (rb0 + rn) * 8, rb0 * 8, 0};
@@ -460,14 +461,16 @@ int or_splice_parse(const or_cfg *c, const or_splice *sp, or_splice_mb *mbs, uin
             break;
         }
         const uint32_t st = rd_ue(&r);
-        if ((st != 0 && st != 5) || rd_ue(&r) != 0) {             /* P, pic_parameter_set_id 0 */
-            err = OR_SPLICE_ERR_HEADER;
+        const int islice = st == 2 || st == 7;
+        if ((st != 0 && st != 5 && !islice) || (idr && !islice) || rd_ue(&r) != 0) {
+            err = OR_SPLICE_ERR_HEADER;                           /* P / I, pic_parameter_set_id 0 */
             break;
         }
         rd_u(&r, c->log2_mfn);                                    /* frame_num */
+        if (idr) rd_ue(&r);                                       /* idr_pic_id */
         if (c->poc_type == 0) rd_u(&r, c->log2_poc);              /* pic_order_cnt_lsb */
         int nrefs = c->num_ref_default_m1 + 1;
-        if (rd_u(&r, 1)) {                                        /* num_ref_idx_active_override */
+        if (!islice && rd_u(&r, 1)) {                             /* num_ref_idx_active_override */
             const uint32_t k = rd_ue(&r);
             if (k > 31) {
                 err = OR_SPLICE_ERR_HEADER;
@@ -475,7 +478,7 @@ int or_splice_parse(const or_cfg *c, const or_splice *sp, or_splice_mb *mbs, uin
             }
             nrefs = (int)k + 1;
         }
-        if (rd_u(&r, 1)) {                                        /* ref_pic_list_modification */
+        if (!islice && rd_u(&r, 1)) {                             /* ref_pic_list_modification */
             /* only the composer's own list (h264_writer.c:455-539): op k puts
              * long_term_pic_num k at index k -- the composed list itself */
             for (int k = 0;; ++k) {
@@ -492,7 +495,9 @@ int or_splice_parse(const or_cfg *c, const or_splice *sp, or_splice_mb *mbs, uin
             }
             if (err) break;
         }
-        if (ref_idc && rd_u(&r, 1)) {                             /* adaptive_ref_pic_marking */
+        if (ref_idc && idr) {
+            rd_u(&r, 2);                                          /* no_output_of_prior_pics, long_term_reference */
+        } else if (ref_idc && rd_u(&r, 1)) {                      /* adaptive_ref_pic_marking */
             for (int k = 0;; ++k) {
                 const uint32_t op = rd_ue(&r);
                 if (r.bad || k > 64 || op > 6) {
@@ -526,7 +531,7 @@ int or_splice_parse(const or_cfg *c, const or_splice *sp, or_splice_mb *mbs, uin
         while (!err) {
             if (r.p >= end && !first_mb) break;
             first_mb = 0;
-            const uint32_t run = rd_ue(&r);
+            const uint32_t run = islice ? 0u : rd_ue(&r);         /* I slices: no mb_skip_run */
             if (r.bad || run > (uint32_t)(nmb - m)) {
                 err = OR_SPLICE_ERR_SYNTAX;
                 break;
@@ -564,8 +569,9 @@ int or_splice_parse(const or_cfg *c, const or_splice *sp, or_splice_mb *mbs, uin
             or_splice_mb *mb = &mbs[m];
             const uint8_t *L = x && sid[m - 1] == u ? mbs[m - 1].tc : NULL;
             const uint8_t *T = y && sid[m - W] == u ? mbs[m - W].tc : NULL;
-            const uint32_t mbt = rd_ue(&r);                       /* mb_type (Table 7-13, 7-11) */
-            if (r.bad || mbt > 30) {
+            /* mb_type (Table 7-13, 7-11; an I slice's k is the P slice's 5 + k) */
+            const uint32_t mbt = rd_ue(&r) + (islice ? 5u : 0u);
+            if (r.bad || mbt > 30 || (islice && mbt < 5)) {
                 err = OR_SPLICE_ERR_SYNTAX;
                 break;
             }
@@ -1072,6 +1078,7 @@ static void hd_mb(const or_cfg *c, const or_refs *R, const or_dyn_rect *rc, cons
     const int lw = 16 * rc->w, cw = 8 * rc->w;
     const uint8_t *sy = src, *su = src + (size_t)lw * 16 * rc->h, *sv = su + (size_t)cw * 8 * rc->h;
     const int lx0 = 16 * (x - rc->x0), ly0 = 16 * (y - rc->y0);
+    const int qp = or_dyn_qp(rc), qpc = or_qp_chroma(qp);
     int luma[16][16], cdc[2][4], cac[2][4][15];
     for (int r = 0; r < 16; ++r) {
         const int bx = 4 * (r % 4), by = 4 * (r / 4);
@@ -1081,7 +1088,7 @@ static void hd_mb(const or_cfg *c, const or_refs *R, const or_dyn_rect *rc, cons
                 res[4 * i + j] = sy[(size_t)(ly0 + by + i) * lw + lx0 + bx + j] -
                                  hd_pred(c, R, ref, 0, 16 * x + bx + j, 16 * y + by + i, mvx, mvy);
         or_fwd4x4(res, W);
-        for (int k = 0; k < 16; ++k) luma[r][k] = or_quant(W[HD_ZZ[k]], 26, HD_ZZ[k], 0);
+        for (int k = 0; k < 16; ++k) luma[r][k] = or_quant(W[HD_ZZ[k]], qp, HD_ZZ[k], 0);
     }
     const int cx0 = 8 * (x - rc->x0), cy0 = 8 * (y - rc->y0);
     for (int p = 0; p < 2; ++p) {
@@ -1096,18 +1103,18 @@ static void hd_mb(const or_cfg *c, const or_refs *R, const or_dyn_rect *rc, cons
                                      hd_pred(c, R, ref, 1 + p, 8 * x + bx + j, 8 * y + by + i, mvx, mvy);
             or_fwd4x4(res, W);
             dc[k] = W[0];
-            for (int i = 1; i < 16; ++i) cac[p][k][i - 1] = or_quant(W[HD_ZZ[i]], 26, HD_ZZ[i], 0);
+            for (int i = 1; i < 16; ++i) cac[p][k][i - 1] = or_quant(W[HD_ZZ[i]], qpc, HD_ZZ[i], 0);
         }
-        cdc[p][0] = or_quant(dc[0] + dc[1] + dc[2] + dc[3], 26, 0, 1);
-        cdc[p][1] = or_quant(dc[0] - dc[1] + dc[2] - dc[3], 26, 0, 1);
-        cdc[p][2] = or_quant(dc[0] + dc[1] - dc[2] - dc[3], 26, 0, 1);
-        cdc[p][3] = or_quant(dc[0] - dc[1] - dc[2] + dc[3], 26, 0, 1);
+        cdc[p][0] = or_quant(dc[0] + dc[1] + dc[2] + dc[3], qpc, 0, 1);
+        cdc[p][1] = or_quant(dc[0] - dc[1] + dc[2] - dc[3], qpc, 0, 1);
+        cdc[p][2] = or_quant(dc[0] + dc[1] - dc[2] - dc[3], qpc, 0, 1);
+        cdc[p][3] = or_quant(dc[0] - dc[1] - dc[2] + dc[3], qpc, 0, 1);
     }
     memset(mb, 0, sizeof(*mb));
     mb->ref = ref;
     mb->mx = 4 * mvx;
     mb->my = 4 * mvy;
-    mb->qp = 26;
+    mb->qp = qp;
     int cbp_l = 0, dcn = 0, acn = 0;
     for (int r = 0; r < 16; ++r) {
         hd_piece(erb, mb, r, luma[r], 16);
@@ -1157,6 +1164,15 @@ size_t or_hint_dyn_scroll_nal(uint8_t *dst, size_t cap, or_cfg *c, int off, cons
             }
             hd_mb(c, R, rc, src, x, y, ref, mvx, mvy, mb, &eb);
         }
+    /* mb_qp_delta: the chain of the coded MBs (raster order) from the slice
+     * QP 26 -- the first one carries QP - 26, the rest 0 */
+    for (size_t i = 0, qp_c = 26; i < nmb; ++i) {
+        or_splice_mb *mb = &mbs[i];
+        if (!mb->cbp) continue;
+        mb->qpd = mb->qp - (int)qp_c;
+        mb->hasqpd = 1;
+        qp_c = (size_t)mb->qp;
+    }
     const size_t nb = sp_compose(dst, cap, c, off, r, n, mode, rc->x0, rc->y0, rc->w, rc->h, mbs, erb,
                                  or_bytes(&eb), err);
     free(mbs);
@@ -1209,6 +1225,18 @@ static void sp_rand_block(uint32_t *s, const or_ext_params *p, int *coef, int ma
 static void ext_header(or_bits *b, const or_cfg *c, const or_ext_params *p, int first, int nrefs, int nrefs_def)
 {
     or_ue(b, (uint32_t)first);                                    /* first_mb_in_slice */
+    if (p->islice) {                                              /* I (7: all of the picture) */
+        or_ue(b, 7);
+        or_ue(b, 0);                                              /* pps id */
+        or_put(b, 0, c->log2_mfn);
+        if (p->islice == 2) or_ue(b, 1);                          /* idr_pic_id */
+        if (c->poc_type == 0) or_put(b, 0, c->log2_poc);
+        if (p->islice == 2) or_put(b, 0, 2);                      /* no_output_of_prior_pics, long_term_reference */
+        else if (p->ref_idc) or_put(b, 0, 1);                     /* sliding window */
+        or_se(b, p->slice_qp_delta);
+        if (c->deblock) or_ue(b, 1);
+        return;
+    }
     or_ue(b, 0);                                                  /* P */
     or_ue(b, 0);                                                  /* pps id */
     or_put(b, 0, c->log2_mfn);
@@ -1245,8 +1273,9 @@ static void ext_intra(or_bits *b, uint32_t *s, const or_ext_params *p, int type,
     memset(t, 0, OR_SPLICE_PIECES);
     memset(im[m], -1, 16);
     if (mbt_force) type = mbt_force == 5 ? 1 : (mbt_force == 30 ? 3 : 2);
+    const uint32_t mo = p->islice ? 5u : 0u;                      /* I slice: mb_type k = P's 5 + k */
     if (type == 3) {
-        or_ue(b, 30);
+        or_ue(b, 30 - mo);
         while (b->nbits & 7) or_put(b, 0, 1);
         for (int k = 0; k < 384; ++k) or_put(b, p->pcm_zero ? 0u : (sp_rng(s) & 255u), 8);
         memset(t, 16, OR_SPLICE_PIECES);
@@ -1254,7 +1283,7 @@ static void ext_intra(or_bits *b, uint32_t *s, const or_ext_params *p, int type,
     }
     int coef[16];
     if (type == 1) {
-        or_ue(b, 5);
+        or_ue(b, 5 - mo);
         for (int blk = 0; blk < 16; ++blk) {
             const int ri = sp_blk_raster(blk), bx = ri & 3, by = ri >> 2;
             int mA = -2, mB = -2;
@@ -1306,7 +1335,7 @@ static void ext_intra(or_bits *b, uint32_t *s, const or_ext_params *p, int type,
     /* I_16x16: prediction mode, chroma cbp, luma cbp in the mb_type */
     const int it = mbt_force ? mbt_force - 6 : (int)(sp_rng(s) % 24);
     const int cbl = it >= 12 ? 15 : 0, cbc = (it >> 2) % 3;
-    or_ue(b, (uint32_t)(6 + it));
+    or_ue(b, (uint32_t)(6 + it) - mo);
     or_ue(b, sp_rng(s) % 4);                                      /* intra_chroma_pred_mode */
     const int j = p->qp_jitter;
     int nq = *qp + (j ? (int)(sp_rng(s) % (uint32_t)(2 * j + 1)) - j : 0);
@@ -1333,6 +1362,11 @@ static void ext_intra(or_bits *b, uint32_t *s, const or_ext_params *p, int type,
             }
     }
 }
+
+/* the stand-in encoder's NAL header: IDR pictures are nal_unit_type 5, a
+ * reference (nal_ref_idc 3 unless given) */
+static int ext_nut(const or_ext_params *p) { return p->islice == 2 ? 5 : 1; }
+static int ext_ref_idc(const or_ext_params *p) { return p->islice == 2 && !p->ref_idc ? 3 : p->ref_idc; }
 
 size_t or_ext_slice(uint8_t *dst, size_t cap, const or_cfg *c, int W, int H, uint32_t seed,
                     const or_ext_params *p)
@@ -1361,7 +1395,7 @@ size_t or_ext_slice(uint8_t *dst, size_t cap, const or_cfg *c, int W, int H, uin
             if (run > 0) or_ue(&b, (uint32_t)run);
             run = 0;
             or_trailing(&b);
-            nb += or_nal(dst + nb, cap - nb, p->ref_idc, 1, rbsp, or_bytes(&b));
+            nb += or_nal(dst + nb, cap - nb, ext_ref_idc(p), ext_nut(p), rbsp, or_bytes(&b));
             or_bits_init(&b, rbsp, rcap);
             ext_header(&b, c, p, m, nrefs, nrefs_def);
             qp = 26 + p->slice_qp_delta;
@@ -1380,6 +1414,19 @@ size_t or_ext_slice(uint8_t *dst, size_t cap, const or_cfg *c, int W, int H, uin
             break;
         }
         const int forced = m == p->bad_mb ? p->bad_type : 0;     /* a valid intra MB of that type here */
+        if (p->islice) {                                          /* every MB intra, no mb_skip_run */
+            const int interior = x > 0 && x < W - 1 && y > top;
+            const int k = (int)(sp_rng(&s) % 5);
+            const int ty = p->intra_types ? p->intra_types : 7;
+            int type = forced ? 0 : 3;                            /* the edge ring: I_PCM */
+            if (!forced && (interior || p->islice == 3)) {
+                type = k < 2 ? 1 : (k < 4 ? 2 : 3);
+                if (!(ty >> (type - 1) & 1)) type = (ty & 2) ? 2 : ((ty & 1) ? 1 : 3);
+            }
+            ext_intra(&b, &s, p, type, forced, x, y, W, sid, im, tcs, &qp);
+            for (int q = 0; q < 16; ++q) *sp_at(&F, x, y, q & 3, q >> 2) = (or_mvi){0, 0, -1, 1};
+            continue;
+        }
         if (!forced && (int)(sp_rng(&s) % 1000) < p->skip_pm) {
             int px, py;
             sp_pskip(&A, &B, &C, &px, &py);
@@ -1490,7 +1537,7 @@ size_t or_ext_slice(uint8_t *dst, size_t cap, const or_cfg *c, int W, int H, uin
     }
     if (run > 0) or_ue(&b, (uint32_t)run);
     or_trailing(&b);
-    nb += or_nal(dst + nb, cap - nb, p->ref_idc, 1, rbsp, or_bytes(&b));
+    nb += or_nal(dst + nb, cap - nb, ext_ref_idc(p), ext_nut(p), rbsp, or_bytes(&b));
     free(rbsp);
     free(F.f);
     free(tcs);

@@ -13,7 +13,9 @@
  * the composed NAL from the standard and checks that every spliced MB
  * decodes to the same (ref, mv, cbp, QP, coefficient levels).
  *
- * Input: one external P slice NAL (nal_unit_type 1, CAVLC) coded for a
+ * Input: one external P or I slice NAL (nal_unit_type 1, or 5 for an IDR
+ * picture: a conventional encoder's first frame and scene cuts,
+ * MASTER_DESIGN.md:39-40,85-90; CAVLC) coded for a
  * picture of w x h MBs with the composed stream's SPS/PPS fields
  * (log2_max_frame_num, POC type, num_ref_idx default, deblocking flag); the
  * rect [x0, x0 + w) x [y0, y0 + h) of the composed picture receives its MBs.
@@ -49,6 +51,10 @@
  * waypoint i) and its motion vectors are displacements in composed-picture
  * coordinates.
  *
+ * An I slice (slice_type 2 / 7; IDR: idr_pic_id, the IDR dec_ref_pic_marking)
+ * has no mb_skip_run and its MBs' mb_type k (Table 7-11: 0 I_4x4, 1-24
+ * I_16x16, 25 I_PCM) is the P slice's intra mb_type 5 + k, under the same
+ * availability rule (trans_resizer.c:1063 process_i_slice, :887-1058).
  * Transplant, per spliced MB (composed slice QP 26):
  *   - P_Skip becomes P_L0_16x16 with ref 0 and its P_Skip motion (8.4.1.1,
  *     evaluated in the external picture), cbp 0;
@@ -91,7 +97,7 @@ extern "C" {
 
 /* error codes (same values as SCROLL_SPLICE_ERR_* in include/composer_batch.h) */
 #define OR_SPLICE_OK 0
-#define OR_SPLICE_ERR_NAL 1      /* not a coded slice of a non-IDR picture        */
+#define OR_SPLICE_ERR_NAL 1      /* not a coded slice (nal_unit_type 1 or 5)      */
 #define OR_SPLICE_ERR_HEADER 2   /* slice header outside the supported syntax     */
 #define OR_SPLICE_ERR_MBTYPE 3   /* an intra MB whose prediction would change     */
 #define OR_SPLICE_ERR_SYNTAX 4   /* malformed / truncated slice data              */
@@ -191,6 +197,12 @@ typedef struct {
     int slice_rows;              /* 0: one slice; k: a slice per k MB rows       */
     int pcm_zero;                /* I_PCM samples all 0 (emulation prevention)   */
     int intra_types;             /* 0: all; else bit 0 I_4x4, 1 I_16x16, 2 I_PCM  */
+    int islice;                  /* 0: P slices; 1: I slices (every MB intra: I_4x4 /
+                                  * I_16x16 where any rect placement splices them,
+                                  * else I_PCM -- the edge ring); 2: the same as an
+                                  * IDR picture (nal_unit_type 5); 3: I slices of
+                                  * intra_types everywhere, edge ring included (a
+                                  * syntax check for the reference's I-slice walker) */
 } or_ext_params;
 size_t or_ext_slice(uint8_t *dst, size_t cap, const or_cfg *c, int w, int h, uint32_t seed,
                     const or_ext_params *p);

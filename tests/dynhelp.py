@@ -10,7 +10,12 @@ class OrCfg(ctypes.Structure):
 
 
 class Rect(ctypes.Structure):
-    _fields_ = [(n, ctypes.c_int) for n in ("x0", "y0", "w", "h", "qp")]   # qp 0 = 26
+    _fields_ = [(n, ctypes.c_int) for n in ("x0", "y0", "w", "h", "qp")]   # qp 0 = 26, -1 = QP 0
+
+
+def qp_field(qp):
+    """or_dyn_rect.qp for a QP 0..51 (0 = 26 there, OR_DYN_QP0 = -1 is QP 0)"""
+    return -1 if qp == 0 else qp
 
 
 class Pic(ctypes.Structure):
@@ -37,6 +42,25 @@ class StripedRefs:
         self.refs = Refs()
         self.refs.ab[0] = ctypes.pointer(self.pics[0])
         self.refs.ab[1] = ctypes.pointer(self.pics[1])
+
+
+class FlatRefs:
+    """pictures A, B of one sample value everywhere"""
+
+    def __init__(self, w, h, value=0):
+        self.planes, self.pics = [], []
+        for _ in (0, 1):
+            y = (ctypes.c_uint8 * (w * h))(*([value] * (w * h)))
+            u = (ctypes.c_uint8 * (w * h // 4))(*([value] * (w * h // 4)))
+            v = (ctypes.c_uint8 * (w * h // 4))(*([value] * (w * h // 4)))
+            self.planes.append((y, u, v))
+            self.pics.append(Pic(w, h, ctypes.addressof(y), ctypes.addressof(u), ctypes.addressof(v)))
+        self.refs = Refs()
+        self.refs.ab[0] = ctypes.pointer(self.pics[0])
+        self.refs.ab[1] = ctypes.pointer(self.pics[1])
+
+    def i420(self, which):
+        return b"".join(bytes(p) for p in self.planes[which])
 
 
 def rect_source(lib, s, t, rect):
@@ -131,12 +155,12 @@ class ExtParams(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int) for n in
                 ("nrefs", "max_ref", "skip_pm", "cbp_pm", "big_pm", "mv_range",
                  "slice_qp_delta", "qp_jitter", "ref_idc", "bad_mb", "bad_type", "list_mod",
-                 "part_pm", "intra_pm", "slice_rows", "pcm_zero", "intra_types")]
+                 "part_pm", "intra_pm", "slice_rows", "pcm_zero", "intra_types", "islice")]
 
 
 EXT_DEFAULT = dict(nrefs=0, max_ref=1, skip_pm=250, cbp_pm=600, big_pm=20, mv_range=64,
                    slice_qp_delta=0, qp_jitter=3, ref_idc=0, bad_mb=-1, bad_type=0,
-                   list_mod=0, part_pm=0, intra_pm=0, slice_rows=0, pcm_zero=0, intra_types=0)
+                   list_mod=0, part_pm=0, intra_pm=0, slice_rows=0, pcm_zero=0, intra_types=0, islice=0)
 
 
 def ext_slice(oracle, cfg, w, h, seed, **kw):

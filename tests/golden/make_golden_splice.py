@@ -10,7 +10,8 @@ compiled from the reference sources by `make -C oracle ref`
 at 20x20 MBs).  This script writes, through the CPU oracle
 (oracle/splice_oracle.c):
   * external slices of the oracle's stand-in encoder for 20x20-MB pictures
-    (P_Skip runs, several references, QP changes, escape-coded levels);
+    (P_Skip runs, several references, QP changes, escape-coded levels), and
+    I pictures through the reference's I-slice walker (process_i_slice);
   * composed 320x320 scroll NALs with a spliced rect (both modes, through
     the 496 waypoint so the composed list has 3 references);
 and records, per NAL, the reference parser's verdict on its MB layer (status,
@@ -48,6 +49,16 @@ EXT = [  # stand-in encoder parameters for 20x20-MB external slices
     dict(intra_pm=400, intra_types=3, cbp_pm=800),
     dict(intra_pm=250, intra_types=3, skip_pm=300, part_pm=300, qp_jitter=6),
 ]
+# I pictures for the reference's I-slice walker (process_i_slice :1063-1360;
+# a whole 20x20-MB picture, one slice; I_4x4 / I_16x16 everywhere -- the
+# walker counts an I_PCM MB's TotalCoeffs as 0, see above): a conventional
+# encoder's first frame / scene cut, spliced as P-slice intra MBs (islice 3:
+# the stand-in encoder's I-slice mode with the edge ring of intra_types)
+EXT_I = [
+    dict(islice=3, intra_types=3, cbp_pm=800),
+    dict(islice=3, intra_types=1, cbp_pm=1000, big_pm=100, qp_jitter=8),
+    dict(islice=3, intra_types=2, slice_qp_delta=-5),
+]
 # composed frames: (offset, mode, rect) on a 320x320 stream scrolling 490..500
 SPLICED = [(490 + i, i % 2, rect) for i, rect in enumerate(
     [(3, 4, 8, 6), (0, 0, 20, 20), (19, 19, 1, 1), (5, 0, 10, 3), (0, 12, 7, 8), (12, 5, 8, 9),
@@ -79,6 +90,11 @@ def cases(oracle):
         nal = ext_slice(oracle, c, 20, 20, 7000 + k, **kw)
         H, b, rbsp = hp.slice_header(nal, nrefs_default=2)      # the composer's PPS
         yield dict(kind="external", case=k, nrefs=H["nrefs"], sha256=hashlib.sha256(nal).hexdigest(),
+                   nal_bytes=len(nal), mb_start_bit=b.p, stop_bit=_stop_bit(rbsp)), nal, rbsp
+    for k, kw in enumerate(EXT_I):
+        nal = ext_slice(oracle, c, 20, 20, 7500 + k, **kw)
+        H, b, rbsp = hp.slice_header(nal, nrefs_default=2)
+        yield dict(kind="external-i", case=k, nrefs=H["nrefs"], sha256=hashlib.sha256(nal).hexdigest(),
                    nal_bytes=len(nal), mb_start_bit=b.p, stop_bit=_stop_bit(rbsp)), nal, rbsp
     buf = (ctypes.c_uint8 * (1 << 21))()
     err = ctypes.c_int()
@@ -123,7 +139,10 @@ def main():
     out = []
     for c, nal, rbsp in cases(oracle):
         end = ctypes.c_size_t()
-        rc = ref.ref_cavlc_parse(rbsp, len(rbsp), c["mb_start_bit"], c["nrefs"], ctypes.byref(end))
+        if c["kind"] == "external-i":
+            rc = ref.ref_cavlc_parse_i(rbsp, len(rbsp), c["mb_start_bit"], ctypes.byref(end))
+        else:
+            rc = ref.ref_cavlc_parse(rbsp, len(rbsp), c["mb_start_bit"], c["nrefs"], ctypes.byref(end))
         c["ref_status"], c["ref_end_bit"] = rc, end.value
         out.append(c)
     json.dump(out, open(os.path.join(HERE, "splice_ref.json"), "w"), indent=1)

@@ -260,22 +260,27 @@ def slice_header(nal, log2_mfn=4, poc_type=2, log2_poc=4, deblock=1, nrefs_defau
     nrefs_default: num_ref_idx_l0_active without an override (the composer's
     PPS: 2)"""
     assert nal[:4] == b"\x00\x00\x00\x01"
-    ref_idc = nal[4] >> 5
+    ref_idc, nut = nal[4] >> 5, nal[4] & 31
     b = Bits(ebsp_to_rbsp(nal[5:]))
     H = {"first_mb": b.ue(), "slice_type": b.ue(), "pps": b.ue(), "frame_num": b.u(log2_mfn)}
+    islice = H["slice_type"] in (2, 7)
+    if nut == 5:
+        H["idr_pic_id"] = b.ue()
     if poc_type == 0:
         H["poc"] = b.u(log2_poc)
     nrefs = nrefs_default
-    if b.u(1):
+    if not islice and b.u(1):
         nrefs = b.ue() + 1
     H["nrefs"] = nrefs
-    if b.u(1):
+    if not islice and b.u(1):
         while True:
             idc = b.ue()
             if idc == 3:
                 break
             b.ue()
-    if ref_idc:
+    if ref_idc and nut == 5:
+        b.u(2)                                   # no_output_of_prior_pics, long_term_reference
+    elif ref_idc:
         if b.u(1):
             while True:
                 op = b.ue()
@@ -666,26 +671,33 @@ def decode_p_slice(nal, w, h, predictor="spec", log2_mfn=4, poc_type=2, log2_poc
     m, nmb, H0 = 0, mbw * mbh, None
     for si, unit in enumerate(nal_units(nal)):
         ref_idc, nut = unit[0] >> 5, unit[0] & 31
-        assert nut == 1, "coded slice of a non-IDR picture"
+        assert nut in (1, 5), "coded slice of a non-IDR or IDR picture"
         rb = ebsp_to_rbsp(unit[1:])
         stop = _rbsp_stop(rb)
         b = Bits(rb)
         H = {"first_mb": b.ue(), "slice_type": b.ue(), "pps": b.ue(), "frame_num": b.u(log2_mfn)}
         assert H["first_mb"] == m, "slices in MB order"
+        islice = H["slice_type"] in (2, 7)
+        assert islice or H["slice_type"] in (0, 5), "a P or I slice"
+        assert nut == 1 or islice, "an IDR picture has I slices"
+        if nut == 5:
+            H["idr_pic_id"] = b.ue()
         if poc_type == 0:
             H["poc"] = b.u(log2_poc)
         nrefs = nrefs_default
-        if b.u(1):
+        if not islice and b.u(1):
             nrefs = b.ue() + 1
         H["nrefs"] = nrefs
-        H["list_mod"] = b.u(1)
+        H["list_mod"] = 0 if islice else b.u(1)
         if H["list_mod"]:                        # ref_pic_list_modification (waypoints)
             while True:
                 idc = b.ue()
                 if idc == 3:
                     break
                 b.ue()
-        if ref_idc and b.u(1):
+        if ref_idc and nut == 5:
+            b.u(2)                               # no_output_of_prior_pics, long_term_reference
+        elif ref_idc and b.u(1):
             while True:
                 op = b.ue()
                 if op == 0:
@@ -712,7 +724,7 @@ def decode_p_slice(nal, w, h, predictor="spec", log2_mfn=4, poc_type=2, log2_poc
         first = True
         while first or b.p < stop:
             first = False
-            run = b.ue()
+            run = 0 if islice else b.ue()        # I slices: no mb_skip_run
             for _ in range(run):
                 y, x = divmod(m, mbw)
                 assert y < mbh, "mb_skip_run past the picture"
@@ -737,7 +749,7 @@ def decode_p_slice(nal, w, h, predictor="spec", log2_mfn=4, poc_type=2, log2_poc
                 trace.append((m, b.p))
             left = tcs[y][x - 1] if F.avail(x - 1, y) else None
             top = tcs[y - 1][x] if F.avail(x, y - 1) else None
-            mbt = b.ue()
+            mbt = b.ue() + (5 if islice else 0)  # an I slice's mb_type k is the P slice's 5 + k
             assert mbt <= 30, "a P-slice mb_type"
             t = [0] * 24
             luma = [[0] * 16 for _ in range(16)]

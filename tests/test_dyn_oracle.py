@@ -15,7 +15,7 @@ import pytest
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 import h264_pslice as hp  # noqa: E402
-from dynhelp import OrCfg, Rect, StripedRefs, rect_source, split_nals  # noqa: E402
+from dynhelp import FlatRefs, OrCfg, Rect, StripedRefs, qp_field, rect_source, split_nals  # noqa: E402
 
 
 def _pred(lib, cfg, R, ref, mv, mbx, mby):
@@ -235,8 +235,9 @@ def test_dyn_rect_qp_decodes(oracle):
     R = StripedRefs(lib, w, h)
     buf = (ctypes.c_uint8 * (1 << 21))()
     psnrs = []
-    for qp in (22, 26, 30, 39, 51):
-        rc = Rect(1, 1, 4, 4, qp)
+    qps = (0, 5, 12, 18, 22, 26, 30, 39, 51)
+    for qp in qps:
+        rc = Rect(1, 1, 4, 4, qp_field(qp))
         cfg = OrCfg()
         lib.or_cfg_init(ctypes.byref(cfg), w, h)
         cfg.frame_num = 2
@@ -277,7 +278,7 @@ def test_dyn_rect_qp_decodes(oracle):
                             org.append(src[base + (8 * (y - rc.y0) + i) * cw + 8 * (x - rc.x0) + j])
             assert len(got) == rc.w * rc.h
         psnrs.append(_psnr(rec, org))
-    assert psnrs[0] > 38.0 and psnrs[1] > 34.0, psnrs
+    assert psnrs[qps.index(22)] > 38.0 and psnrs[qps.index(26)] > 34.0 and psnrs[0] > 50.0, psnrs
     assert all(a > b for a, b in zip(psnrs, psnrs[1:])), psnrs
     # qp 26 written out is the default's bytes
     c1, c2 = OrCfg(), OrCfg()
@@ -290,3 +291,37 @@ def test_dyn_rect_qp_decodes(oracle):
     n2 = lib.or_compose_dyn(b2, len(b2), ctypes.byref(c2), 40, 0, ctypes.byref(Rect(1, 1, 4, 4, 26)), src,
                             ctypes.byref(R.refs), None)
     assert bytes(buf[:n1]) == bytes(b2[:n2])
+
+
+def test_dyn_rect_low_qp_levels_clamped_and_parsed(oracle):
+    """QP 0 on saturated residuals (black references, white chroma, +-255
+    luma noise): the chroma DC levels reach OR_LEVEL_MAX (2063, the clamp;
+    luma levels stay <= 1632 at any QP) and are coded with level_prefix 15
+    (the escape every context accepts); the NAL parses in the test decoder
+    to exactly those levels"""
+    lib = oracle
+    w, h = 64, 64
+    R = FlatRefs(w, h, 0)
+    rc = Rect(1, 1, 2, 2, qp_field(0))
+    n = 384 * rc.w * rc.h
+    rng = __import__("random").Random(5)
+    src = (ctypes.c_uint8 * n)(*([rng.choice((0, 255)) for _ in range(256 * rc.w * rc.h)] +
+                                 [255] * (128 * rc.w * rc.h)))
+    cfg = OrCfg()
+    lib.or_cfg_init(ctypes.byref(cfg), w, h)
+    cfg.frame_num = 2
+    buf = (ctypes.c_uint8 * (1 << 20))()
+    nb = lib.or_compose_dyn(buf, len(buf), ctypes.byref(cfg), 3, 0, ctypes.byref(rc), src,
+                            ctypes.byref(R.refs), None)
+    scroll = split_nals(bytes(buf[:nb]))[-1]
+    big = []
+
+    def on_mb(x, y, ref, mvd, cbp, luma, cdc, cac):
+        for b in luma:
+            big.extend(abs(v) for v in b)
+        for b in cdc:
+            big.extend(abs(v) for v in b)
+
+    H, nmb = hp.parse_p_slice(scroll, w, h, on_mb=on_mb)
+    assert H["qp_delta"] == -26 and nmb == (w // 16) * (h // 16)
+    assert max(big) == 2063                     # the clamp was reached and coded

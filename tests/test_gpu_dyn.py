@@ -13,7 +13,7 @@ import numpy as np
 import pytest
 
 from conftest import synthetic_offsets
-from dynhelp import OrCfg, Pic, Rect, Refs, StripedRefs, rect_source, split_nals
+from dynhelp import qp_field, OrCfg, Pic, Rect, Refs, StripedRefs, rect_source, split_nals
 
 pytestmark = pytest.mark.gpu
 
@@ -94,7 +94,8 @@ def oracle_streams(oracle, w, h, offsets, rect, src, R, mode=0, frame_num=2, way
 
 
 def gpu_streams(gpu, w, h, offsets, rect, R, src=None, synth=False, mode=0, chunks=None,
-                arena=None, slot=0, waypoints=(), shared_refs=True, per_stream_refs=None, debug=0):
+                arena=None, slot=0, waypoints=(), shared_refs=True, per_stream_refs=None, debug=0,
+                stream_qp=None):
     S, F = offsets.shape
     b = gpu.Batch(S, F, arena or (8 << 20), mode=mode)
     if debug:
@@ -103,7 +104,9 @@ def gpu_streams(gpu, w, h, offsets, rect, R, src=None, synth=False, mode=0, chun
         b.add_stream(gpu.make_config(w, h, waypoints=waypoints))
     b.set_dyn_rect(rect.x0, rect.y0, rect.w, rect.h, slot)
     if rect.qp:
-        b.set_dyn_qp(rect.qp)
+        b.set_dyn_qp(0 if rect.qp == -1 else rect.qp)
+    for s, q in (stream_qp or {}).items():
+        b.set_dyn_qp(q, stream=s)
     if shared_refs:
         b.set_dyn_refs(R.i420(0), R.i420(1))
     for s, Rs in (per_stream_refs or {}).items():
@@ -405,14 +408,15 @@ def test_dyn_round3_gather_still_exact(gpu, oracle, geom):
     check_equal(b, want)
 
 
-@pytest.mark.parametrize("qp", [22, 30, 37, 51])
+@pytest.mark.parametrize("qp", [0, 12, 18, 22, 30, 37, 51])
 def test_dyn_rect_qp(gpu, oracle, scroll, qp):
     """scroll_batch_set_dyn_qp: luma at qp, chroma at QPc, slice_qp_delta qp -
     26 in the dynamic NALs (waypoints on the way stay the reference's), at
     the config-3 geometry with random references (the largest levels) and
-    through the general path's half-pel chroma waypoints"""
+    through the general path's half-pel chroma waypoints; below 22 every NAL
+    takes the general path with 16-bit levels"""
     w, h = 1280, 720
-    rect = Rect(28, 10, 25, 25, qp)
+    rect = Rect(28, 10, 25, 25, qp_field(qp))
     S, F = 2, 8
     offs = synthetic_offsets(S, F, h, first_stream=3)
     offs[1] = np.arange(490, 498)
@@ -423,21 +427,48 @@ def test_dyn_rect_qp(gpu, oracle, scroll, qp):
     assert rc == 0, gpu.last_error()
     check_equal(b, want)
     with pytest.raises(Exception):
-        b.set_dyn_qp(21)
+        b.set_dyn_qp(52)
     b.close()
 
 
-def test_dyn_qp_not_with_hints(gpu, scroll):
-    b = gpu.Batch(1, 2, 1 << 20)
+def test_dyn_rect_qp_per_stream(gpu, oracle, scroll):
+    """scroll_batch_set_dyn_qp_stream: one batch, each stream at its own QP
+    (16-bit general path and int8 k_dyn_row path side by side), each equal
+    to the oracle at that QP; a later batch-wide QP overrides them all"""
+    w, h = 1280, 720
+    S, F = 5, 6
+    qps = [12, 40, 18, 26, 0]
+    base = Rect(28, 10, 25, 25)
+    offs = synthetic_offsets(S, F, h, first_stream=1)
+    R = striped_refs(oracle, w, h)
+    src = synth_source(oracle, S, F, base)
+    want = []
+    for s, q in enumerate(qps):
+        rs = Rect(28, 10, 25, 25, qp_field(q))
+        want += oracle_streams(oracle, w, h, offs[s:s + 1], rs, src[s:s + 1], R)
+    b, rc = gpu_streams(gpu, w, h, offs, base, R, src, stream_qp=dict(enumerate(qps)))
+    assert rc == 0, gpu.last_error()
+    check_equal(b, want)
+    b.close()
+
+
+def test_dyn_qp_with_hints_and_deblocking(gpu, scroll):
+    """QP is accepted under hints (per frame too); a stream with the
+    deblocking filter on keeps QP 26"""
+    b = gpu.Batch(2, 2, 1 << 20)
     b.add_stream(gpu.make_config(320, 320))
+    b.add_stream(gpu.make_config(320, 320, deblock=0))
     b.set_dyn_rect(1, 1, 2, 2)
-    b.set_dyn_qp(30)
+    b.set_dyn_qp(30, stream=0)
     with pytest.raises(Exception):
-        b.set_hints(0, 0, [], 1)
-    b.set_dyn_qp(26)
-    b.set_hints(0, 0, [], 1)
+        b.set_dyn_qp(30, stream=1)
     with pytest.raises(Exception):
         b.set_dyn_qp(30)
+    b.set_hints(0, 0, [], 1)
+    b.set_dyn_qp_at(0, 1, 12)
+    with pytest.raises(Exception):
+        b.set_dyn_qp_at(1, 1, 12)
+    b.set_dyn_qp_at(1, 1, 26)
     b.close()
 
 

@@ -15,7 +15,7 @@ import numpy as np
 import pytest
 
 from conftest import synthetic_offsets
-from dynhelp import OrCfg, Rect, hint_array, random_hints, split_nals
+from dynhelp import OrCfg, Rect, hint_array, qp_field, random_hints, split_nals
 from test_gpu_dyn import oracle_streams, random_refs, striped_refs, synth_source
 
 pytestmark = pytest.mark.gpu
@@ -49,7 +49,7 @@ def plan(oracle, w, h, offsets, rw, rh, seed, p_hint=0.8, p_none=0.15, modes=(EX
 
 
 def oracle_hintdyn(oracle, w, h, offsets, rw, rh, plan_, src, R, compose_mode=0, waypoints=(),
-                   t0=0):
+                   t0=0, qp_of=None):
     S, F = offsets.shape
     oracle.or_compose_hint_dyn.restype = ctypes.c_size_t
     buf = (ctypes.c_uint8 * (16 << 20))()
@@ -66,7 +66,7 @@ def oracle_hintdyn(oracle, w, h, offsets, rw, rh, plan_, src, R, compose_mode=0,
         for f in range(F):
             rects, hm, pos = plan_[(s, f)]
             arr, n = hint_array(rects)
-            rc = Rect(pos[0], pos[1], rw, rh) if pos else None
+            rc = Rect(pos[0], pos[1], rw, rh, qp_field(qp_of(s, f)) if qp_of else 0) if pos else None
             sp = np.ascontiguousarray(src[s, t0 + f])
             k = oracle.or_compose_hint_dyn(buf, len(buf), ctypes.byref(c), int(offsets[s, f]),
                                            compose_mode, arr, n, hm,
@@ -250,4 +250,34 @@ def test_arguments(gpu, oracle, scroll):
         b.set_splice(0, 0, 0, 0, 1, 1, b"\x00\x00\x00\x01\x21\x00")
     b.compose(2)
     assert b.sync() == 0, gpu.last_error()
+    b.close()
+
+
+def test_hinted_rect_qp_per_stream_and_frame(gpu, oracle):
+    """the rect under hints at per-stream QPs (scroll_batch_set_dyn_qp_stream)
+    with per-frame overrides (scroll_batch_set_dyn_qp_at), QP 0 included:
+    k_hdyn_code quantises at the frame's QP, the rect's first coded MB
+    carries mb_qp_delta QP - 26 (k_splice_stage), equal to the oracle"""
+    w, h = 640, 480
+    rw, rh = 9, 7
+    S, F = 3, 5
+    offs = synthetic_offsets(S, F, h)
+    plan_ = plan(oracle, w, h, offs, rw, rh, seed=41)
+    R = random_refs(w, h, 13)
+    src = synth_source(oracle, S, F, Rect(0, 0, rw, rh))
+    sq = [12, 40, 26]
+    fq = {(0, 1): 0, (1, 3): 18, (2, 2): 51}
+    qp_of = lambda s_, f_: fq.get((s_, f_), sq[s_])   # noqa: E731
+    want = oracle_hintdyn(oracle, w, h, offs, rw, rh, plan_, src, R, qp_of=qp_of)
+    b = gpu_batch(gpu, w, h, S, F, (0, 0, rw, rh), R, slot=2048 * rw * rh)   # QP 0: larger MB regions
+    apply_plan(b, plan_, F)
+    for s_, q in enumerate(sq):
+        b.set_dyn_qp(q, stream=s_)
+    for (s_, f_), q in fq.items():
+        b.set_dyn_qp_at(s_, f_, q)
+    b.set_offsets(np.ascontiguousarray(offs))
+    b.set_dyn_source(np.ascontiguousarray(src).tobytes(), F)
+    b.compose(F)
+    assert b.sync() == 0, gpu.last_error()
+    check_equal(b, want)
     b.close()

@@ -436,3 +436,43 @@ def test_multislice_rules(gpu, oracle, scroll):
     for i, s in enumerate(ok):
         assert b.output(s) == want[i], s
     b.close()
+
+
+@pytest.mark.parametrize("islice,rows", [(1, 0), (2, 0), (1, 1), (2, 2)])
+def test_i_and_idr_pictures(gpu, oracle, islice, rows):
+    """a conventional encoder's first frame / scene cut: I slices (islice 1)
+    and IDR pictures (islice 2, nal_unit_type 5), one slice or one per 1-2
+    MB rows, every MB intra with an I_PCM edge ring, spliced at random
+    places in all three modes: k_splice_lanes / k_splice_parse read the I /
+    IDR header and the MBs without mb_skip_run, equal to the oracle"""
+    w, h = 640, 480
+    offs = synthetic_offsets(3, 8, h, first_stream=7)
+    frames, want = plan(oracle, w, h, offs, 60 + 3 * islice + rows, p_splice=0.9, p_hint=0.3,
+                        max_rect=(14, 10), ext_kw=dict(islice=islice, slice_rows=rows, cbp_pm=800,
+                                                       big_pm=20, qp_jitter=4))
+    b, rc = gpu_streams(gpu, w, h, offs, frames)
+    assert rc == 0, gpu.last_error()
+    check_equal(b, want)
+    for (s, f), (_, _, sp) in frames.items():
+        assert b.splice_status(s, f) == 0
+    b.close()
+
+
+def test_all_intra_25x25_in_the_rect_interior(gpu, oracle):
+    """the verdict's case: a 25x25-MB all-intra picture (I_4x4 / I_16x16
+    inside, I_PCM edge ring), as an I and as an IDR picture, spliced at the
+    config-3 rect (28, 10) of a 1280x720 stream"""
+    w, h = 1280, 720
+    offs = synthetic_offsets(2, 4, h, first_stream=3)
+    c = _cfg(oracle, w, h)
+    frames = {}
+    for s in range(2):
+        for f in range(4):
+            nal = ext_slice(oracle, c, 25, 25, 90 + 4 * s + f, islice=1 + (f & 1), cbp_pm=900, big_pm=10,
+                            qp_jitter=2, intra_types=3 if s else 0)
+            frames[(s, f)] = ([], SPEC if f % 3 else EXACT, (28, 10, 25, 25, nal))
+    _, want = plan_from(oracle, w, h, offs, frames)
+    b, rc = gpu_streams(gpu, w, h, offs, frames)
+    assert rc == 0, gpu.last_error()
+    check_equal(b, want)
+    b.close()

@@ -321,7 +321,9 @@ def test_errors(oracle):
     bad = ext_slice(oracle, c, 4, 3, 1, bad_mb=5, bad_type=31)
     assert compose(splice_of(2, 2, 4, 3, bad)) == ERR_SYNTAX
     # not a non-IDR slice: an IDR NAL header, an SPS
-    assert compose(splice_of(2, 2, 4, 3, good[:4] + bytes([0x65]) + good[5:])) == ERR_NAL
+    # an IDR NAL header on a P slice: IDR pictures are I slices only
+    assert compose(splice_of(2, 2, 4, 3, good[:4] + bytes([0x65]) + good[5:])) == ERR_HEADER
+    assert compose(splice_of(2, 2, 4, 3, good[:4] + bytes([0x66]) + good[5:])) == ERR_NAL      # SEI
     assert compose(splice_of(2, 2, 4, 3, good[:4] + bytes([0x67]) + good[5:])) == ERR_NAL
     # a rect whose MB count differs from the slice's: too many MBs / too few
     assert compose(splice_of(2, 2, 4, 2, good)) == ERR_SYNTAX
@@ -346,7 +348,8 @@ def test_reference_parser_accepts_spliced_nals(oracle):
     (trans_resizer process_p_slice, built from /root/reference by
     oracle/Makefile `ref`) consumed the MB layer of every fixture NAL --
     external slices of the stand-in encoder and composed 320x320 NALs with a
-    spliced rect, both modes, 2 and 3 references -- exactly up to its
+    spliced rect, both modes, 2 and 3 references -- and its I-slice walker
+    (process_i_slice) the stand-in encoder's I pictures, exactly up to the
     rbsp_stop_one_bit.  The oracle must still produce those NALs bit for bit;
     where the reference build exists the parse is repeated live."""
     import json
@@ -357,7 +360,7 @@ def test_reference_parser_accepts_spliced_nals(oracle):
     import make_golden_splice as mg
     fx = json.load(open(os.path.join(here, "golden", "splice_ref.json")))
     assert all(c["ref_status"] == 0 and c["ref_end_bit"] == c["stop_bit"] for c in fx)
-    assert {c["kind"] for c in fx} == {"external", "composed", "composed-intra"}
+    assert {c["kind"] for c in fx} == {"external", "external-i", "composed", "composed-intra"}
     refso = os.path.join(os.path.dirname(here), "oracle", "_ref", "libref_cavlc.so")
     ref = ctypes.CDLL(refso) if os.path.exists(refso) else None
     got = list(mg.cases(oracle))
@@ -366,6 +369,50 @@ def test_reference_parser_accepts_spliced_nals(oracle):
         assert c["sha256"] == f["sha256"] and c["mb_start_bit"] == f["mb_start_bit"]
         if ref is not None:
             end = ctypes.c_size_t()
-            assert ref.ref_cavlc_parse(rbsp, len(rbsp), c["mb_start_bit"], c["nrefs"],
-                                       ctypes.byref(end)) == 0
+            if c["kind"] == "external-i":                 # the reference's I-slice walker
+                assert ref.ref_cavlc_parse_i(rbsp, len(rbsp), c["mb_start_bit"], ctypes.byref(end)) == 0
+            else:
+                assert ref.ref_cavlc_parse(rbsp, len(rbsp), c["mb_start_bit"], c["nrefs"],
+                                           ctypes.byref(end)) == 0
             assert end.value == c["stop_bit"]
+
+
+def test_i_and_idr_slices_splice(oracle):
+    """a conventional encoder's first frame and scene cuts are I / IDR
+    pictures (MASTER_DESIGN.md:39-40,85-90): I slices (nal_unit_type 1) and
+    IDR slices (5), one slice or one per MB row, every MB intra with an
+    I_PCM edge ring (I_4x4 / I_16x16 inside), spliced into the rect's
+    interior: they parse (no mb_skip_run, mb_type k = the P slice's 5 + k),
+    compose as P-slice intra MBs and decode to the external MBs in all three
+    modes; the same picture on the rect's left edge inside the composed
+    picture keeps the edge ring's I_PCM and still splices; an all-I_4x4
+    picture there is refused (SCROLL_SPLICE_ERR_MBTYPE)"""
+    rng = random.Random(5)
+    buf = (ctypes.c_uint8 * (1 << 21))()
+    w, h = 640, 480
+    c = _cfg(oracle, w, h)
+    cov = dict(i4=0, i16=0, pcm=0)
+    for i, (islice, rows) in enumerate([(1, 0), (2, 0), (1, 1), (2, 2), (2, 0), (1, 0)]):
+        sw, sh = 25 if i == 0 else rng.randint(4, 12), 25 if i == 0 else rng.randint(4, 9)
+        sw, sh = min(sw, w // 16 - 2), min(sh, h // 16 - 2)
+        x0, y0 = rng.randint(1, w // 16 - sw - 1), rng.randint(1, h // 16 - sh - 1)
+        nal = ext_slice(oracle, c, sw, sh, 700 + i, islice=islice, slice_rows=rows, cbp_pm=800,
+                        big_pm=30, qp_jitter=3, intra_types=3 if i % 2 else 0, slice_qp_delta=rng.randint(-4, 4))
+        nu = nal[4] & 31
+        assert nu == (5 if islice == 2 else 1)
+        sp = splice_of(x0, y0, sw, sh, nal)
+        e, mbs = _parse(oracle, c, sp)
+        assert e == 0, (i, e)
+        for mode in (EXACT, PSKIP, SPEC):
+            got, ext = _check_frame(oracle, c, 100 + i, [], mode, sp, buf)
+        assert all(m["intra"] for row in ext for m in row)
+        cov["i4"] += sum(m["intra"] == 1 for row in ext for m in row)
+        cov["i16"] += sum(m["intra"] == 2 for row in ext for m in row)
+        cov["pcm"] += sum(m["intra"] == 3 for row in ext for m in row)
+        e2, _ = _parse(oracle, c, splice_of(0, y0, sw, sh, nal))          # the picture's left edge
+        assert e2 == 0
+    assert all(v > 0 for v in cov.values()), cov
+    # an I_4x4 on the rect's top-left corner, inside the composed picture
+    nal = ext_slice(oracle, c, 4, 4, 9, islice=1, bad_mb=0, bad_type=5)
+    e, _ = _parse(oracle, c, splice_of(3, 3, 4, 4, nal))
+    assert e == 3

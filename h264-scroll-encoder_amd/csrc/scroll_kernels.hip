@@ -2677,10 +2677,37 @@ int scroll_batch_splice_status(ScrollBatch *b, int s, int f, int *status)
     return splice_frame_status(b, (size_t)s * b->max_frames + f, status);
 }
 
+int scroll_batch_splice_refusal(ScrollBatch *b, int s, int f, int *status, int *mb_x, int *mb_y, int *mb_type)
+{
+    if (!b || !status || s < 0 || s >= b->nstreams || f < 0 || f >= b->max_frames)
+        return SCROLL_ERR_ARG;
+    int rc = batch_host_sync(b);
+    if (rc) return rc;
+    HIPCHK(hipSetDevice(b->device));
+    const size_t i = (size_t)s * b->max_frames + f;
+    rc = splice_frame_status(b, i, status);
+    if (rc) return rc;
+    int x = -1, y = -1, t = -1;
+    if (*status == SCROLL_SPLICE_ERR_MBTYPE && b->d_spf) {
+        SpliceFrame sf;
+        HIPCHK(hipMemcpy(&sf, b->d_spf + i, sizeof(sf), hipMemcpyDeviceToHost));
+        if (sf.bad_mb >= 0 && sf.w > 0) {
+            const int m = sf.bad_mb & 0xffff;
+            x = m % sf.w;
+            y = m / sf.w;
+            t = sf.bad_mb >> 16;
+        }
+    }
+    if (mb_x) *mb_x = x;
+    if (mb_y) *mb_y = y;
+    if (mb_type) *mb_type = t;
+    return SCROLL_OK;
+}
+
 static const char *splice_msg(int e)
 {
     switch (e) {
-    case SCROLL_SPLICE_ERR_NAL: return "not a coded slice of a non-IDR picture (or more than 1,024 slices)";
+    case SCROLL_SPLICE_ERR_NAL: return "not a coded slice of an IDR or non-IDR picture (or more than 1,024 slices)";
     case SCROLL_SPLICE_ERR_HEADER: return "slice header outside the supported syntax, or slices out of order";
     case SCROLL_SPLICE_ERR_MBTYPE: return "an intra MB whose prediction reads other samples in the composed picture";
     case SCROLL_SPLICE_ERR_SYNTAX: return "malformed or truncated slice data, or slices not covering the rect's MBs";

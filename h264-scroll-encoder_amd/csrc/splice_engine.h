@@ -47,6 +47,8 @@ typedef struct {
      * others 0 (the chain from the slice QP 26) */
     int32_t hd_qp;
     uint32_t hd_first;
+    int32_t bad_mb;                 /* k_splice_fix: the first failing slice's SpliceUnit.bad */
+    int32_t pad;
 } SpliceFrame;
 
 /* one NAL unit (slice) of a spliced picture: its bytes [b, e) of the
@@ -61,7 +63,7 @@ typedef struct {
     uint32_t w0, nbytes, end;
     int32_t first, nmb, status;
     int32_t fq_mb, fq_qp, last_qp;
-    int32_t pad;
+    int32_t bad;                    /* SCROLL_SPLICE_ERR_MBTYPE: the refused MB (rect raster) | mb_type << 16; -1 */
 } SpliceUnit;
 
 /* frames of at least this many slices are parsed one slice per lane

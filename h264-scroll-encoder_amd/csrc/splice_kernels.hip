@@ -658,6 +658,7 @@ __global__ __launch_bounds__(64) void k_splice_unesc(int n, const int32_t *__res
             UN->nbytes = nb;
             UN->end = end;
             UN->status = ok ? SCROLL_SPLICE_OK : SCROLL_SPLICE_ERR_NAL;
+            UN->bad = -1;
             UN->first = -1;
             UN->nmb = 0;
         }
@@ -892,7 +893,7 @@ __global__ __launch_bounds__(64 * LANE_WAVES) void k_splice_lanes(const int32_t 
         const bool idr = (h0 & 31u) == 5u;
         LRd r;
         r.init(rbsp + F->rbsp_word + w0, (nbytes + 3u) >> 2, 8u * nbytes);
-        int status = SCROLL_SPLICE_ERR_HEADER, first = -1, m = 0;
+        int status = SCROLL_SPLICE_ERR_HEADER, first = -1, m = 0, bad = -1;
         int fq_mb = -1, fq_qp = 0, last_qp = 0;
         int nrefs = 2;
         int qp = 0;
@@ -1134,6 +1135,7 @@ __global__ __launch_bounds__(64 * LANE_WAVES) void k_splice_lanes(const int32_t 
                         if ((na && !same(-1, 0, aA)) || (nbb && !same(0, -1, false)) || (nd && !same(-1, -1, false)) ||
                             (nc && !same(1, -1, aC))) {
                             status = SCROLL_SPLICE_ERR_MBTYPE;
+                            bad = m | (int)mbt << 16;
                             fail = true;
                             break;
                         }
@@ -1357,6 +1359,7 @@ __global__ __launch_bounds__(64 * LANE_WAVES) void k_splice_lanes(const int32_t 
         UN->first = first;
         UN->nmb = m - (first < 0 ? 0 : first);
         UN->status = status;
+        UN->bad = bad;
         UN->fq_mb = fq_mb;
         UN->fq_qp = fq_qp;
         UN->last_qp = last_qp;
@@ -1411,7 +1414,7 @@ __global__ __launch_bounds__(64) void k_splice_parse(int n, const int32_t *__res
      * per-lane values: the header byte goes through readfirstlane, or every
      * branch on it -- and the whole bit reader after it -- turns divergent */
     const uint32_t h0 = U(F->nal[U(UN->b)]);
-    int status = SCROLL_SPLICE_ERR_HEADER, first = -1, m = 0;
+    int status = SCROLL_SPLICE_ERR_HEADER, first = -1, m = 0, bad = -1;
     int fq_mb = -1, fq_qp = 0, last_qp = 0;
     SRd r;
     const uint32_t w0 = U(UN->w0), nb = U(UN->nbytes), end = U(UN->end), base = 32u * w0;
@@ -1645,6 +1648,7 @@ __global__ __launch_bounds__(64) void k_splice_parse(int n, const int32_t *__res
                     if ((na && !same(-1, 0, aA)) || (nbb && !same(0, -1, aB)) || (nd && !same(-1, -1, aD)) ||
                         (nc && !same(1, -1, aC))) {
                         status = SCROLL_SPLICE_ERR_MBTYPE;
+                        bad = m | (int)mbt << 16;
                         goto done;
                     }
                     if (intra == 1) {
@@ -1819,6 +1823,7 @@ done:
         UN->first = first;
         UN->nmb = m - (first < 0 ? 0 : first);
         UN->status = status;
+        UN->bad = bad;
         UN->fq_mb = fq_mb;
         UN->fq_qp = fq_qp;
         UN->last_qp = last_qp;
@@ -1844,7 +1849,7 @@ __global__ __launch_bounds__(64) void k_splice_fix(int n, const int32_t *__restr
     const int nu = min(nall, (int)splice_unit_cap(nmb));
     const SpliceUnit *UN = units + F->unit_first;
     SpliceMbRec *rec = recs + F->rec_first;
-    int status = SCROLL_SPLICE_OK;
+    int status = SCROLL_SPLICE_OK, bad = -1;
     if (nall > SPLICE_MAXU || nall < 1) {
         status = SCROLL_SPLICE_ERR_NAL;
     } else {
@@ -1861,6 +1866,7 @@ __global__ __launch_bounds__(64) void k_splice_fix(int n, const int32_t *__restr
             }
             if (un.status != SCROLL_SPLICE_OK) {
                 status = un.status;
+                bad = un.status == SCROLL_SPLICE_ERR_MBTYPE ? un.bad : -1;
                 break;
             }
             if (un.fq_mb >= 0) {
@@ -1875,6 +1881,7 @@ __global__ __launch_bounds__(64) void k_splice_fix(int n, const int32_t *__restr
         if (status == SCROLL_SPLICE_OK && (nall > nu || expect != nmb)) status = SCROLL_SPLICE_ERR_SYNTAX;
     }
     F->status = status;
+    F->bad_mb = bad;
 }
 
 /* ------------------------------------------------------------------------ */

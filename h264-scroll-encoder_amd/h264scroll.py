@@ -204,6 +204,9 @@ def _load():
                                                            P(ScrollSpliceDesc)]),
         "scroll_batch_splice_status": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
                                                       P(ctypes.c_int)]),
+        "scroll_batch_splice_refusal": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                                       P(ctypes.c_int), P(ctypes.c_int), P(ctypes.c_int),
+                                                       P(ctypes.c_int)]),
         "scroll_batch_ingest": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, P(u8p),
                                                P(ctypes.c_size_t), P(u8p), P(ctypes.c_size_t),
                                                P(ctypes.c_int)]),
@@ -583,6 +586,14 @@ class Batch:
         st = ctypes.c_int()
         self._chk(lib.scroll_batch_splice_status(self.h, s, f, ctypes.byref(st)), "splice_status")
         return st.value
+
+    def splice_refusal(self, s, f):
+        """(status, mb_x, mb_y, mb_type): for SCROLL_SPLICE_ERR_MBTYPE the
+        refused MB of the external picture and its P-slice mb_type"""
+        v = [ctypes.c_int() for _ in range(4)]
+        self._chk(lib.scroll_batch_splice_refusal(self.h, s, f, *[ctypes.byref(x) for x in v]),
+                  "splice_refusal")
+        return tuple(x.value for x in v)
 
     # ---- dynamic rect (configs 3-5) ----
     def set_dyn_rect(self, x0, y0, w, h, slot_bytes=0):

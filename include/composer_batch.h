@@ -299,8 +299,10 @@ int scroll_batch_clear_hints(ScrollBatch *b);
  * The external picture: one NAL (Annex-B start code optional), or several
  * Annex-B NAL units -- its slices, in MB order, each starting at the MB after
  * the previous one's last (first_mb_in_slice), together covering the w*h MBs
- * (at most 1,024 slices; each is parsed by its own wave); nal_unit_type 1,
- * CAVLC, parsed with the composed stream's SPS/PPS (log2_max_frame_num, POC
+ * (at most 1,024 slices; each is parsed by its own wave); P slices or I
+ * slices (nal_unit_type 1, or 5 for an IDR picture: a conventional encoder's
+ * first frame and scene cuts; an I slice's MBs are the P slice's intra types,
+ * without mb_skip_run), CAVLC, parsed with the composed stream's SPS/PPS (log2_max_frame_num, POC
  * type, 2 default references, disable_deblocking_filter_idc 1 when the
  * stream signals deblocking control); no ref_pic_list_modification, or one
  * that restates the composed list (op k: long_term_pic_num k, as the
@@ -327,7 +329,7 @@ int scroll_batch_clear_hints(ScrollBatch *b);
  * external slice plus 16 bytes per picture MB) for every (stream, frame). */
 #define SCROLL_SPLICE_MAX_BYTES   ((uint64_t)1 << 29)   /* n < 512 MiB: 32-bit bit offsets */
 #define SCROLL_SPLICE_OK          0
-#define SCROLL_SPLICE_ERR_NAL     1   /* not a coded slice of a non-IDR picture, or
+#define SCROLL_SPLICE_ERR_NAL     1   /* not a coded slice (nal_unit_type 1 / 5), or
                                        * more than 1,024 slices                      */
 #define SCROLL_SPLICE_ERR_HEADER  2   /* slice header outside the supported syntax  */
 #define SCROLL_SPLICE_ERR_MBTYPE  3   /* an intra MB whose prediction would change   */
@@ -352,6 +354,12 @@ int scroll_batch_clear_splices(ScrollBatch *b);
 /* after sync: SCROLL_SPLICE_* of frame f of stream s in the last compose
  * (SCROLL_SPLICE_OK also when the frame has no splice) */
 int scroll_batch_splice_status(ScrollBatch *b, int s, int f, int *status);
+/* the same, and for SCROLL_SPLICE_ERR_MBTYPE the refused MB: its position in
+ * the external picture (MB units) and its mb_type in P-slice numbering (5
+ * I_4x4, 6..29 I_16x16; an I slice's k is 5 + k) -- the MB a caller can
+ * re-code as I_PCM or with a mode that reads no neighbour across the rect's
+ * edge (the margin ring, docs/MASTER_DESIGN.md:54-56); -1 otherwise */
+int scroll_batch_splice_refusal(ScrollBatch *b, int s, int f, int *status, int *mb_x, int *mb_y, int *mb_type);
 
 /* ---- stream ingest on the GPU ----
  * Batched composer_init + composer_write_header (reference src/composer.c:

@@ -422,12 +422,18 @@ static void sp_pskip(const or_mvi *A, const or_mvi *B, const or_mvi *C, int *px,
     or_spec_predict(A, B, C, 0, px, py);
 }
 
+/* the MB the last parse refused with OR_SPLICE_ERR_MBTYPE: its index in the
+ * external picture | its (P-slice) mb_type << 16, or -1 */
+static __thread int sp_refused = -1;
+int or_splice_refused(void) { return sp_refused; }
+
 int or_splice_parse(const or_cfg *c, const or_splice *sp, or_splice_mb *mbs, uint8_t *rbsp,
                     size_t *rbsp_n)
 {
     enum { MAXU = 1024 };
     size_t ub[MAXU], ue[MAXU];
     *rbsp_n = 0;
+    sp_refused = -1;
     const int nu = sp_units(sp->nal, sp->n, ub, ue, MAXU);
     if (nu <= 0) return OR_SPLICE_ERR_NAL;
     const int W = sp->w, H = sp->h, nmb = W * H;
@@ -630,6 +636,7 @@ int or_splice_parse(const or_cfg *c, const or_splice *sp, or_splice_mb *mbs, uin
                 }
                 if (!sp_intra_ok(c, sp, sid, x, y, mb->intra, modes, cm)) {
                     err = OR_SPLICE_ERR_MBTYPE;
+                    sp_refused = m | (int)mbt << 16;
                     break;
                 }
                 int cbp;

@@ -171,6 +171,11 @@ size_t or_compose_hint_dyn(uint8_t *dst, size_t cap, or_cfg *c, int off, int com
                            const or_hint_rect *r, int n, int mode, const or_dyn_rect *rc,
                            const uint8_t *src, const or_refs *R, int *err);
 
+/* after or_splice_parse (or a compose) failed with OR_SPLICE_ERR_MBTYPE: the
+ * refused MB's index in the external picture | its P-slice mb_type << 16;
+ * -1 otherwise (scroll_batch_splice_refusal's oracle) */
+int or_splice_refused(void);
+
 /* ---- test-input generator: a stand-in "dynamic encoder" (MASTER_DESIGN
  * §4.2) writing standard CAVLC P slices of a w x h MB picture with random
  * MBs, so the tests have external slices to splice ---- */

@@ -397,11 +397,22 @@ def test_intra_on_rect_edges(gpu, oracle, scroll):
         frames[(i, 2)] = ([], SPEC, (2, 2, 4, 3, nal))
     b, rc = gpu_streams(gpu, w, h, offs, frames)
     assert rc == scroll.SCROLL_ERR_CONFIG
+    oracle.or_splice_refused.restype = ctypes.c_int
     for i, (mb, t) in enumerate(((0, 5), (1, 12), (4, 30), (0, 30))):
         want = 0 if t == 30 else scroll.SCROLL_SPLICE_ERR_MBTYPE
         assert b.splice_status(i, 2) == want, (i, b.splice_status(i, 2))
         if want == 0:
             assert b.splice_status(i, 0) == 0
+        else:
+            # the refused MB, as the oracle's parse names it (scroll_batch_splice_refusal)
+            rb = (ctypes.c_uint8 * (len(frames[(i, 2)][2][4]) + 8))()
+            mbs = (ctypes.c_uint8 * (4 * 12 * 2048))()
+            rn = ctypes.c_size_t()
+            sp = splice_of(*frames[(i, 2)][2])
+            assert oracle.or_splice_parse(ctypes.byref(c), ctypes.byref(sp), mbs, rb, ctypes.byref(rn)) == want
+            ref = oracle.or_splice_refused()
+            assert b.splice_refusal(i, 2) == (want, (ref & 0xffff) % 4, (ref & 0xffff) // 4, ref >> 16)
+            assert (ref & 0xffff, ref >> 16) == (mb, t)
     good = {k: v for k, v in frames.items() if k[0] >= 2}
     _, want = plan_from(oracle, w, h, offs[2:], {(s - 2, f): v for (s, f), v in good.items()})
     check_equal(b, [None, None] + want, streams=[2, 3])

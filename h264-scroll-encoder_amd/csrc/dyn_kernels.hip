@@ -1366,8 +1366,8 @@ __device__ inline uint32_t bilin4(uint32_t b, uint32_t c, uint32_t f)
 /* i / NPC for a piece index of a rect row (i < NPC DYN_MAX_W): a 24-bit
  * multiply by the rounded-up reciprocal instead of the compiler's
  * quarter-rate high multiply */
-static_assert(NPC == 26 && NPC * DYN_MAX_W < 6577, "div_npc's reciprocal (2521 / 2^16) is exact below 6577");
-__device__ inline int div_npc(int i) { return (int)(__umul24((uint32_t)i, 2521u) >> 16); }
+static_assert(NPC == 26 && NPC * DYN_MAX_W < 18724, "div_npc's reciprocal (10083 / 2^18) is exact below 18724");
+__device__ inline int div_npc(int i) { return (int)(__umul24((uint32_t)i, 10083u) >> 18); }
 
 __device__ inline int row_slot(int task, int w)
 {
@@ -1975,8 +1975,29 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
 #endif
 constexpr int EPS_T = SCROLL_EPS_T, EPS_NW = EPS_T / 64, EPS_KW = SCROLL_EPS_KW, EPS_CHUNK = EPS_T * 4 * EPS_KW;
 static_assert(EPS_KW % 4 == 0, "the EP scan reads 16-byte LDS vectors");
-static_assert(DYN_MAX_H + 2 * ((DYN_MAX_MBH + DYN_STATIC_ROWS - 1) / DYN_STATIC_ROWS) <= 64,
-              "rs_table scans the row groups with one wave");
+/* row groups per NAL at most (rect rows + static groups above / below) */
+constexpr int RS_GMAX = DYN_MAX_H + 2 * ((DYN_MAX_MBH + DYN_STATIC_ROWS - 1) / DYN_STATIC_ROWS);
+/* the group tables live in dynamic LDS sized by the NAL's group count
+ * (goff [ng + 1], gb / gw [ng], then cw [ng] and cbase [ng + 1] where a
+ * kernel has them): the benched rects' few groups take little LDS, a whole
+ * 4K frame's 137 fit too */
+__host__ __device__ inline size_t gtab_bytes(int ng, bool epfix)
+{
+    return (size_t)4 * (epfix ? 5 * (size_t)ng + 2 : 3 * (size_t)ng + 1);
+}
+struct GTab {
+    uint32_t *goff, *gb, *gw, *cw, *cbase;
+};
+__device__ inline GTab gtab_of(uint32_t *p, int ng)
+{
+    GTab T;
+    T.goff = p;
+    T.gb = p + ng + 1;
+    T.gw = T.gb + ng;
+    T.cw = T.gw + ng;
+    T.cbase = T.cw + ng;
+    return T;
+}
 
 /* the RBSP word (MSB first) at bit P (a multiple of 32) of a NAL whose row
  * groups have offsets goff, bit counts gb and row-stage words at fr + gw;
@@ -2048,28 +2069,33 @@ __device__ inline void scan_load(ScanLoads &L, uint32_t c0, int t, int ng, uint3
     gcarry = gg;
 }
 
-/* the row-group table of NAL nb in LDS (wave 0): goff = bit offsets (goff[ng]
- * = RBSP bits incl. the stop bit), gb = bit counts, gw = first row-stage
- * words in the frame's region, cw = the groups' EP-candidate records.
- * count (k_dyn_epfix): lane t's group's candidate count, read with the
- * table (the record word is the count unless it names a spill slot) */
+/* the row-group table of NAL nb in LDS (wave 0, 64 groups per step with
+ * the offset carried): goff = bit offsets (goff[ng] = RBSP bits incl. the
+ * stop bit), gb = bit counts, gw = first row-stage words in the frame's
+ * region, cw = the groups' EP-candidate records.  cnt (k_dyn_epfix): each
+ * group's candidate count, read with the table (the record word is the
+ * count unless it names a spill slot) */
 __device__ inline void rs_table(const uint32_t *gbits, size_t nb, const DynGeom &g, const uint32_t *fr,
                                 uint32_t *goff, uint32_t *gb, uint32_t *gw, uint32_t *cw, int t,
-                                uint32_t *bad = nullptr, uint32_t *count = nullptr)
+                                uint32_t *bad = nullptr, uint32_t *cnt = nullptr)
 {
     const int ng = g.ngroups;
     constexpr int SR = DYN_STATIC_ROWS;
     const int nA = max(1, (g.y0 + SR - 1) / SR);
-    if (t < 64) {
-        const bool row = t >= nA && t < nA + g.h;
-        uint32_t w = (uint32_t)rs_group_words(g, nA, t), c = (uint32_t)rs_runs_words(g, nA, t);
+    if (t >= 64) return;
+    uint32_t carry = 0;
+    for (int g0 = 0; g0 < ng; g0 += 64) {
+        const int gi = g0 + t;
+        const bool in = gi < ng;
+        const bool row = gi >= nA && gi < nA + g.h;
+        uint32_t w = (uint32_t)rs_group_words(g, nA, gi), c = (uint32_t)rs_runs_words(g, nA, gi);
         /* both loads in flight together */
-        const uint32_t b = t < ng ? gbits[nb * (size_t)ng + t] : 0u;
-        uint32_t m = t < ng && (row || count) ? fr[c] : 0u;
+        const uint32_t b = in ? gbits[nb * (size_t)ng + gi] : 0u;
+        uint32_t m = in && (row || cnt) ? fr[c] : 0u;
         const uint32_t incl = wave_incl_sum(b, t);
-        if (t < ng) {
-            gb[t] = b;
-            goff[t] = incl - b;
+        if (in) {
+            gb[gi] = b;
+            goff[gi] = carry + incl - b;
             /* a rect row that outgrew its slot: its record word names the
              * spill slot (relative to fr) holding its bits and record */
             if (row && (m & 0x80000000u)) {
@@ -2084,18 +2110,19 @@ __device__ inline void rs_table(const uint32_t *gbits, size_t nb, const DynGeom 
                     rel / g.rs_spill_words < g.rs_spill_cap) {
                     w = m & 0x7fffffffu;
                     c = w + g.rs_spill_words - EPC_ROW;
-                    if (count) m = fr[c];
+                    if (cnt) m = fr[c];
                 } else {
                     if (bad) *bad = 1u;
                     m = 0u;
                 }
             }
-            gw[t] = w;
-            if (cw) cw[t] = c;
+            gw[gi] = w;
+            if (cw) cw[gi] = c;
+            if (cnt) cnt[gi] = m;
         }
-        if (count) *count = t < ng ? m : 0u;
-        if (t == 63) goff[ng] = incl;
+        carry += __shfl(incl, 63, 64);
     }
+    if (t == 0) goff[ng] = carry;
 }
 
 /* the RBSP word (MSB first) at bit P, a multiple of 32 (0 past the end) */
@@ -2216,7 +2243,9 @@ __global__ __launch_bounds__(EPS_T) void k_dyn_epscan(DevStream *__restrict__ st
                                                      const uint32_t *__restrict__ slow_n,
                                                      const uint32_t *__restrict__ slow)
 {
-    __shared__ uint32_t goff[65], gb[64], gw[64];
+    extern __shared__ uint32_t gdyn[];                  /* the group tables (gtab_bytes) */
+    const GTab GT = gtab_of(gdyn, g.ngroups);
+    uint32_t *goff = GT.goff, *gb = GT.gb, *gw = GT.gw;
     __shared__ int32_t wmax[EPS_NW];
     __shared__ uint32_t ep_n, ep_base;
     __shared__ uint4 cbuf4[EPS_CHUNK / 16];              /* the chunk's bytes */
@@ -2525,15 +2554,24 @@ __device__ inline void ep_fix(DevStream *st, DynFrame *DF, size_t nb, int s, con
         reinterpret_cast<uint4 *>(lst)[i] = make_uint4(0u, 0u, 0u, 0u);
     if (t < 64) {
         if (t == 0) bad = 0u;
-        uint32_t c;                                     /* the group's candidate count */
-        rs_table(gbits, nb, g, fr, goff, gb, gw, cw, t, &bad, &c);
-        const uint32_t cmax = (t >= nA && t < nA + g.h) ? EPC_ROW - 1u : EPC_STATIC - 1u;
-        const uint32_t cc = min(c, cmax);
-        const uint32_t incl = wave_incl_sum(cc, t);
-        if (t < ng) cbase[t] = incl - cc;
-        if (t == 63) cbase[ng] = incl;
-        const bool ov = __builtin_amdgcn_ballot_w64(c > cmax) != 0;
+        wave_sync();
+        /* the groups' candidate counts (into cbase), then their bases */
+        rs_table(gbits, nb, g, fr, goff, gb, gw, cw, t, &bad, cbase);
+        wave_sync();
+        uint32_t carry = 0;
+        bool ov = false;
+        for (int g0 = 0; g0 < ng; g0 += 64) {
+            const int gi = g0 + t;
+            const uint32_t c = gi < ng ? cbase[gi] : 0u;
+            const uint32_t cmax = (gi >= nA && gi < nA + g.h) ? EPC_ROW - 1u : EPC_STATIC - 1u;
+            const uint32_t cc = min(c, cmax);
+            const uint32_t incl = wave_incl_sum(cc, t);
+            if (gi < ng) cbase[gi] = carry + incl - cc;
+            ov |= __builtin_amdgcn_ballot_w64(c > cmax) != 0;
+            carry += __shfl(incl, 63, 64);
+        }
         if (t == 0) {
+            cbase[ng] = carry;
             slow = ov ? 1u : 0u;
             nlst = 0;
         }
@@ -2741,9 +2779,10 @@ __global__ __launch_bounds__(EPF_T) void k_dyn_epfix(DevStream *__restrict__ st,
                                                      uint32_t *__restrict__ slow_n, uint32_t *__restrict__ slow,
                                                      uint64_t *__restrict__ stamps)
 {
-    __shared__ uint32_t goff[65], gb[64], gw[64], cw[64];
-    __shared__ uint32_t cbase[65];                      /* runs before group g */
     __shared__ __attribute__((aligned(16))) uint32_t lst[EPF_LIST];   /* the position bitmap / list */
+    extern __shared__ uint32_t gdyn[];                  /* the group tables (gtab_bytes); cbase: runs before group g */
+    const GTab GT = gtab_of(gdyn, g.ngroups);
+    uint32_t *goff = GT.goff, *gb = GT.gb, *gw = GT.gw, *cw = GT.cw, *cbase = GT.cbase;
     __shared__ uint32_t cnt[4], ws[EPF_T / 64];
     const int f = blockIdx.x, s = blockIdx.y, t = threadIdx.x;
     if (f >= nframes) return;
@@ -2780,7 +2819,9 @@ __global__ __launch_bounds__(DT) void k_dyn_emit(const DevStream *__restrict__ s
     __shared__ alignas(16) uint8_t ob[OBUF];
     __shared__ int32_t wmax[NW];
     __shared__ uint32_t wsum[NW];
-    __shared__ uint32_t goff[65], gb[64], gw[64];
+    extern __shared__ uint32_t gdyn[];                  /* the group tables (gtab_bytes) */
+    const GTab GT = gtab_of(gdyn, g.ngroups);
+    uint32_t *goff = GT.goff, *gb = GT.gb, *gw = GT.gw;
     const int f = blockIdx.x, s = blockIdx.y, t = threadIdx.x;
     const size_t nb = (size_t)s * ld_fr + f;
     const DynFrame df = dfr[nb];
@@ -2899,7 +2940,9 @@ __global__ __launch_bounds__(DT) void k_dyn_emit_gather(const DevStream *__restr
                                                         uint64_t *__restrict__ stamps)
 {
     __shared__ uint32_t raw[EPLIST_MAX], sp[EPLIST_MAX];
-    __shared__ uint32_t goff[RS ? 65 : 1], gb[RS ? 64 : 1], gw[RS ? 64 : 1];
+    extern __shared__ uint32_t gdyn[];                  /* RS: the group tables (gtab_bytes) */
+    const GTab GT = gtab_of(gdyn, RS ? g.ngroups : 0);
+    uint32_t *goff = GT.goff, *gb = GT.gb, *gw = GT.gw;
     const int s = blockIdx.y, f = dyn_frame_of(blockIdx.x, s), t = threadIdx.x;
     /* debug: realtime at entry / after the sort / at exit, EP count, HW_ID */
     uint64_t *stp = stamps && t == 0 && blockIdx.z == 0 ? stamps + ((size_t)s * gridDim.x + f) * 8 : nullptr;
@@ -3136,7 +3179,9 @@ __global__ __launch_bounds__(DT) void k_dyn_gather(const DevStream *__restrict__
                                                   uint64_t *__restrict__ stamps)
 {
     __shared__ uint32_t raw[EPLIST_MAX], sp[EPLIST_MAX + 1];
-    __shared__ uint32_t goff[65], gb[64], gw[64];
+    extern __shared__ uint32_t gdyn[];                  /* the group tables (gtab_bytes) */
+    const GTab GT = gtab_of(gdyn, g.ngroups);
+    uint32_t *goff = GT.goff, *gb = GT.gb, *gw = GT.gw;
     const int s = blockIdx.y, f = dyn_frame_of(blockIdx.x, s), t = threadIdx.x;
     const DynFrame df = dfr[(size_t)s * ld_fr + f];
     const int j = df.nal;
@@ -3353,6 +3398,16 @@ int dyn_launch_code(hipStream_t hs, int nframes, int S, DevStream *st, const Nal
                        pend, nal, ld_nal, *g, x->rows, src, refs, x->meta, x->body_lo, x->body_hi, x->body_w,
                        x->ctr);
     if (hipGetLastError() != hipSuccess) return -1;
+    if (row_lds_bytes(g->w, mbw) > 65536) {
+        /* wide rects (a whole 1280- or 4096-px row): dynamic LDS past the
+         * 64 KB default, up to the CU's 160 KB (set_dyn_rect's bound) */
+        const int rl = (int)row_lds_bytes(g->w, mbw);
+        if (hipFuncSetAttribute(reinterpret_cast<const void *>(&k_dyn_row<false>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, rl) != hipSuccess ||
+            hipFuncSetAttribute(reinterpret_cast<const void *>(&k_dyn_row<true>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, rl) != hipSuccess)
+            return -1;
+    }
     hipLaunchKernelGGL(k_dyn_row<false>, dim3(g->h, nframes, S), dim3(row_threads(g->w)),
                        row_lds_bytes(g->w, mbw), hs, st, nal, ld_nal, pend, dfr, ld_fr, *g, x->rows, src, refs,
                        x->meta, x->body_lo, x->body_hi, x->body_w, x->tcx, epoch, x->rowstage, x->gbits, x->spill,
@@ -3383,10 +3438,12 @@ int dyn_launch_pack(hipStream_t hs, int nframes, int S, DevStream *st, const Nal
     if (nframes <= 0 || S <= 0) return 0;
     if (dyn_launch_static(hs, nframes, S, st, nal, ld_nal, pend, dfr, ld_fr, g, x)) return -1;
     uint32_t *slow_n = x->ctr + DYN_CTR_SLOW, *slow = x->ctr + DYN_CTR_LIST + x->ctr_frames;
-    hipLaunchKernelGGL(k_dyn_epfix, dim3(nframes, S), dim3(EPF_T), 0, hs, st, dfr, ld_fr, nframes, *g,
+    hipLaunchKernelGGL(k_dyn_epfix, dim3(nframes, S), dim3(EPF_T), gtab_bytes(g->ngroups, true), hs, st, dfr,
+                       ld_fr, nframes, *g,
                        x->rowstage, x->gbits, eps, slow_n, slow, stamps);
     if (hipGetLastError() != hipSuccess) return -1;
-    hipLaunchKernelGGL(k_dyn_epscan, dim3(EPS_Z, EPS_SLOTS), dim3(EPS_T), 0, hs, st, dfr, ld_fr, *g,
+    hipLaunchKernelGGL(k_dyn_epscan, dim3(EPS_Z, EPS_SLOTS), dim3(EPS_T), gtab_bytes(g->ngroups, false), hs, st,
+                       dfr, ld_fr, *g,
                        x->rowstage, x->gbits, eps, slow_n, slow);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
@@ -3404,14 +3461,15 @@ int dyn_launch_emit(hipStream_t hs, int nframes, int S, const DevStream *st, con
     const bool big = (int64_t)g->w * g->h > 1024;
     const uint32_t *rs = x ? x->rowstage : nullptr, *gbits = x ? x->gbits : nullptr;
     const dim3 grid(nframes, S, GATHER_Z);
+    const size_t gl = x ? gtab_bytes(g->ngroups, false) : 0;     /* the group tables (RS) */
     if (x && !(g->debug & SCROLL_DEBUG_DYN_GATHER1))
-        hipLaunchKernelGGL(k_dyn_gather, dim3(nframes, S, SCROLL_GATHER2_Z), dim3(DT), 0, hs, st, nal, ld_nal, dfr,
+        hipLaunchKernelGGL(k_dyn_gather, dim3(nframes, S, SCROLL_GATHER2_Z), dim3(DT), gl, hs, st, nal, ld_nal, dfr,
                            ld_fr, *g, stage, rs, gbits, arena, ld_arena, stamps);
     else if (x && big)
-        hipLaunchKernelGGL((k_dyn_emit_gather<4, true>), grid, dim3(DT), 0, hs, st, nal, ld_nal, dfr, ld_fr, *g,
+        hipLaunchKernelGGL((k_dyn_emit_gather<4, true>), grid, dim3(DT), gl, hs, st, nal, ld_nal, dfr, ld_fr, *g,
                            stage, rs, gbits, arena, ld_arena, stamps);
     else if (x)
-        hipLaunchKernelGGL((k_dyn_emit_gather<1, true>), grid, dim3(DT), 0, hs, st, nal, ld_nal, dfr, ld_fr, *g,
+        hipLaunchKernelGGL((k_dyn_emit_gather<1, true>), grid, dim3(DT), gl, hs, st, nal, ld_nal, dfr, ld_fr, *g,
                            stage, rs, gbits, arena, ld_arena, stamps);
     else if (big)
         hipLaunchKernelGGL((k_dyn_emit_gather<4, false>), grid, dim3(DT), 0, hs, st, nal, ld_nal, dfr, ld_fr,
@@ -3420,7 +3478,7 @@ int dyn_launch_emit(hipStream_t hs, int nframes, int S, const DevStream *st, con
         hipLaunchKernelGGL((k_dyn_emit_gather<1, false>), grid, dim3(DT), 0, hs, st, nal, ld_nal, dfr, ld_fr,
                            *g, stage, rs, gbits, arena, ld_arena, stamps);
     if (hipGetLastError() != hipSuccess) return -1;
-    hipLaunchKernelGGL(k_dyn_emit, dim3(nframes, S), dim3(DT), 0, hs, st, nal, ld_nal, dfr, ld_fr,
+    hipLaunchKernelGGL(k_dyn_emit, dim3(nframes, S), dim3(DT), gl, hs, st, nal, ld_nal, dfr, ld_fr,
                        *g, stage, rs, gbits, arena, ld_arena);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

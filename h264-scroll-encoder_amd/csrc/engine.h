@@ -84,8 +84,8 @@ typedef struct {
 } DynFrame;
 
 /* dynamic rect geometry and buffer strides (one per batch) */
-#define DYN_MAX_W 64                /* rect width limit (MBs)                     */
-#define DYN_MAX_H 48                /* rect height limit (MBs)                    */
+#define DYN_MAX_W 256               /* rect width limit (MBs): a whole 4096-px row */
+#define DYN_MAX_H 256               /* rect height limit (MBs): a whole 4K frame   */
 #define DYN_MAX_MBW 512             /* picture width limit with the rect (MBs)   */
 #define DYN_MAX_MBH 512             /* picture height limit with the rect (MBs)  */
 #define DYN_STATIC_ROWS 64          /* MB rows per static k_dyn_group row group (4 measured slower) */

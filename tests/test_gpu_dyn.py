@@ -508,3 +508,25 @@ def test_dyn_lite_timing_bytes_and_pairs(gpu, oracle):
             else:
                 assert plan > 0 and demit > 0
         b.close()
+
+
+@pytest.mark.parametrize("w,h,rect,S,F,refs", [
+    (1280, 720, (0, 0, 80, 45), 3, 6, "striped"),     # a whole 720p frame (ngroups 47)
+    (1280, 720, (0, 0, 80, 45), 2, 3, "random"),      # noise: spill slots, multi-pass bit windows
+    (3840, 2160, (0, 0, 240, 135), 1, 3, "striped"),  # a whole 4K frame: 137 row groups, 142 KB LDS rows
+])
+def test_dyn_rect_whole_frame(gpu, oracle, scroll, w, h, rect, S, F, refs):
+    """the rect cap lifted to the whole frame (MASTER_DESIGN.md:220's full
+    conventional encode as the hint fallback): every MB dynamic, rows of 80
+    / 240 MBs through k_dyn_row (several bit-window passes, dynamic LDS past
+    64 KB), more than 64 row groups through k_dyn_epfix / k_dyn_gather,
+    equal to oracle/dyn_oracle.c"""
+    rc = Rect(*rect)
+    offs = synthetic_offsets(S, F, h, first_stream=2)
+    R = striped_refs(oracle, w, h) if refs == "striped" else random_refs(w, h, 5)
+    src = synth_source(oracle, S, F, rc)
+    want = oracle_streams(oracle, w, h, offs, rc, src, R)
+    b, rcode = gpu_streams(gpu, w, h, offs, rc, R, src, arena=(64 << 20) * F)
+    assert rcode == 0, gpu.last_error()
+    check_equal(b, want)
+    b.close()

@@ -18,18 +18,18 @@ typedef struct {
     uint16_t *meta;
     uint2 *body_lo, *body_hi;       /* record bodies: bits 0..63, bits 64..127 */
     uint4 *body_w;                  /* below QP_MIN: levels 8..15 (int16) of > 128-bit blocks */
+    uint4 *heads;                   /* per frame: the 12 MB-head classes (k_dyn_rows -> k_dyn_row), HEAD_WORDS */
     unsigned long long *tcx;        /* k_dyn_row: per (frame, rect row, MB) bottom TotalCoeffs */
     uint32_t *rowstage;             /* per (frame, row group): its bits from bit 0 (rs_frame_words) */
     uint32_t *gbits;                /* per (frame, row group): its bit count */
     uint32_t *spill;                /* rs_spill_cap spill slots (rect rows over their slot) */
     uint32_t *ctr;                  /* per compose: [0] spill slots taken, [1] general records taken,
-                                     * [2] NALs k_dyn_epfix left to k_dyn_epscan, [DYN_CTR_LIST + k]
-                                     * the frame (s ld_fr + f) holding general record k,
-                                     * [DYN_CTR_LIST + ctr_frames + q] the q-th NAL for k_dyn_epscan */
+                                     * [2], [3] unused, [DYN_CTR_LIST + k] the frame (s ld_fr + f)
+                                     * holding general record k */
     uint32_t ctr_frames;            /* frames the lists hold (S ld_fr) */
     uint32_t epoch;                 /* look-back epoch of the last compose (24 bits, never 0) */
 } DynScratch;
-#define DYN_CTR_SLOW 2               /* ctr[]: the k_dyn_epscan count           */
+#define DYN_HEAD_VECS 16             /* heads[] per frame: 12 classes MSB first, then their lengths */
 #define DYN_CTR_LIST 4               /* ctr[]: the lists (the counters zeroed per compose: 4 words) */
 
 /* k_dyn_rows + k_dyn_code_general (records of the general-path NALs) +
@@ -38,9 +38,8 @@ int dyn_launch_code(hipStream_t hs, int nframes, int S, DevStream *st, const Nal
                     int ld_nal, const PlanPending *pend, DynFrame *dfr, int ld_fr,
                     const DynGeom *g, const uint8_t *src, const uint8_t *refs, const DynScratch *x,
                     uint32_t epoch, int mbw, uint64_t *stamps);
-/* k_dyn_static (static row groups) + k_dyn_epfix (+ k_dyn_epscan for the
- * NALs it flags): RBSP sizes and sorted EP positions (eps: DYN_OVF_BYTES per
- * frame) straight from the row groups */
+/* k_dyn_static (static row groups) + k_dyn_epfix: RBSP sizes and EP
+ * positions (eps: DYN_OVF_BYTES per frame) straight from the row groups */
 /* k_dyn_static alone (the static row groups: header, rows above / below the
  * rect).  (Measured in round 4: on a second HIP stream beside the block
  * coder, 1.69 against 1.67 ms per step -- no gain) */
@@ -49,7 +48,7 @@ int dyn_launch_static(hipStream_t hs, int nframes, int S, DevStream *st, const N
 int dyn_launch_pack(hipStream_t hs, int nframes, int S, DevStream *st, const NalDesc *nal,
                     int ld_nal, const PlanPending *pend, DynFrame *dfr, int ld_fr,
                     const DynGeom *g, const DynScratch *x, uint8_t *eps, uint64_t *stamps);
-/* k_dyn_emit_gather + k_dyn_emit: x != NULL -- the dynamic rect (RBSP from
+/* k_dyn_gather (k_dyn_emit_gather on the hint / splice path): x != NULL -- the dynamic rect (RBSP from
  * the row groups, EP lists in stage = eps); x == NULL -- the staged RBSP of
  * the hint / splice path (slot_bytes per frame, EP list in the slot tail) */
 int dyn_launch_emit(hipStream_t hs, int nframes, int S, const DevStream *st, const NalDesc *nal,

@@ -15,12 +15,13 @@
  *                         above / below the rect, stop bit) -> row-stage words
  *   k_dyn_epfix           per NAL: row-group offsets, emulation-prevention
  *                         positions from the groups' EP-candidate words
- *                         (k_dyn_epscan rescans the NALs it flags)
+ *                         (or, past what those settle, a scan of the NAL)
  *   k_plan (size pass)    NAL sizes (dynamic: 5 + RBSP + EP), arena offsets
  *   k_emit                every other NAL (dynamic NALs are "external")
- *   k_dyn_emit_gather     row-stage groups -> arena: start code, NAL header,
- *                         EP bytes, 16-byte chunks (k_dyn_emit: > 2048 EP
- *                         bytes); the RBSP is never staged
+ *   k_dyn_gather          row-stage groups -> arena: start code, NAL header,
+ *                         EP bytes, 16-byte chunks (emit_serial in the same
+ *                         workgroup past 2048 EP bytes); the RBSP is never
+ *                         staged
  *
  * The bits are those of oracle/dyn_oracle.c (or_scroll_nal_dyn); parity is
  * checked bit-exact by tests/test_gpu_dyn.py.  Roofline: HBM (source pixels
@@ -86,7 +87,7 @@ __device__ inline void load_rowtabs(RowTabs &dst, int t, int nthr)
 
 constexpr int HEAD_MAX = 160;           /* bits of one MB head (huge mvd: 2 x 63 + ref) */
 constexpr int HDR_MAX = 1024;           /* slice header bits (8 waypoints + MMCO ~ 250) */
-constexpr int OBUF = 6400;              /* k_dyn_emit: 127 carry + 5 + 4096 x 1.5 */
+constexpr int OBUF = 6400;              /* emit_serial: 127 carry + 5 + 4096 x 1.5 */
 
 /* DynFrame.err bits: a pool ran out (the batch grows it, the compose is
  * repeated); the general chroma path; k_dyn_row's wait for the row above
@@ -98,7 +99,8 @@ constexpr uint32_t DF_OVER = 1u, DF_GENERAL = 2u, DF_HANDOFF = 4u;
 constexpr uint64_t HANDOFF_TICKS = 5000000ull;
 constexpr uint64_t HANDOFF_GAP = 100000ull;     /* 1 ms: a longer gap between two polls is a preemption */
 /* k_dyn_epfix could not settle the NAL's EP positions from the candidates
- * (too many): k_dyn_epscan scans it whole; not an error for the emit */
+ * (too many): it scanned the NAL whole (ep_scan, list unsorted); not an
+ * error for the emit */
 constexpr uint32_t DF_EPSLOW = 0x100u;
 /* the NAL's size and EP list are final (ep_fix ran; the list is sorted
  * unless DF_EPSLOW) */
@@ -119,7 +121,7 @@ constexpr uint32_t DF_FIXED = 0x200u;
  * non-zero).  Runs starting at the group's first bit, and the bytes reaching
  * past the group's end, are the group seam's (k_dyn_epfix reads those
  * bytes).  At most EPC_ROW - 1 / EPC_STATIC - 1 words per group (more: the
- * NAL takes the whole scan, k_dyn_epscan). */
+ * NAL takes the whole scan, ep_scan). */
 /* record words per group (count, then word indices): rect rows, static
  * groups (64 MB rows of scroll heads: large-mv codewords can repeat a run
  * in every MB) */
@@ -247,93 +249,6 @@ __device__ inline int rec_of(int q, int pc, int ndt)
 }
 constexpr uint32_t M_OVF = 1u << 15;
 constexpr uint32_t ROW_GEN = 1u << 31, ROW_OFF = 0x0fffffffu;
-
-/* ---------------------------------------------------------------------- */
-/* k_dyn_rows                                                              */
-/* ---------------------------------------------------------------------- */
-/* rows[n][i], i < 32 h (h = rect MB rows):
- *   i < 16 h        luma row 16 y0 + i: byte offset of its prediction row in
- *                   the stream's reference pair (picture * pic + row * w)
- *   16 h .. 24 h    chroma row 8 y0 + i': the upper bilinear row
- *                   (picture * pic + ysz + row * w / 2), the 1/8-pel
- *                   fraction in bits 28..30, ROW_GEN if the waypoint chain
- *                   has a half-pel step (the general path)
- *   24 h .. 32 h    the lower bilinear row (used when the fraction != 0)
- * Sets DynFrame.err = DF_GENERAL when some row of the NAL needs the general
- * path (never for waypoints the composer creates), else 0. */
-__global__ __launch_bounds__(256) void k_dyn_rows(const DevStream *__restrict__ st,
-                                                  const NalDesc *__restrict__ nal, int ld_nal,
-                                                  const PlanPending *__restrict__ pend,
-                                                  DynFrame *__restrict__ dfr, int ld_fr, DynGeom g,
-                                                  uint32_t *__restrict__ rows, uint32_t *__restrict__ ctr)
-{
-    __shared__ int32_t wo[8], wl[8], wv[8];
-    __shared__ int32_t gen;
-    const int s = blockIdx.y, f = blockIdx.x, t = threadIdx.x;
-    DynFrame *DF = dfr + (size_t)s * ld_fr + f;
-    const int j = DF->nal;
-    if (j < 0) return;
-    if (t < 8) {
-        wo[t] = pend[s].wo[t];
-        wl[t] = pend[s].wl[t];
-        wv[t] = pend[s].wv[t];
-    }
-    if (t == 0) gen = 0;
-    __syncthreads();
-    const DevStream *S = st + s;
-    const NalDesc d = nal[(size_t)s * ld_nal + j];
-    const NalCtx c = nal_ctx(S, d, wo, wl, wv);
-    const Regions rg = regions(c);
-    const int w = c.w, h = c.h, a_end = (h - c.off) / 16;
-    const uint32_t ysz = (uint32_t)w * (uint32_t)h, pic = ysz + ysz / 2;
-    const WpTab T{wo, wv, h};
-    uint32_t *rw = rows + ((size_t)s * ld_fr + f) * (size_t)(32 * g.h);
-    bool my_gen = false;
-    for (int i = t; i < 32 * g.h; i += 256) {
-        uint32_t e;
-        if (i < 16 * g.h) {
-            const int Y = 16 * g.y0 + i, row = Y >> 4;
-            const bool cA = row < a_end;
-            int yo;
-            const int b = luma_row(T, cA ? rg.ra : rg.rb, Y + (cA ? rg.mva : rg.mvb), yo);
-            e = (uint32_t)b * pic + (uint32_t)yo * (uint32_t)w;
-        } else {
-            const int i2 = i - 16 * g.h, bot = i2 >= 8 * g.h;
-            const int Y = 8 * g.y0 + (bot ? i2 - 8 * g.h : i2), row = Y >> 3;
-            const bool cA = row < a_end;
-            const int q = 4 * (cA ? rg.mva : rg.mvb), o = q >> 3, fr = q & 7;
-            int yo;
-            const int b = chroma_row(T, cA ? rg.ra : rg.rb, Y + o + bot, yo);
-            if (b < 0) {
-                e = ROW_GEN;
-                if (!bot || fr) my_gen = true;
-            } else {
-                e = ((uint32_t)b * pic + ysz + (uint32_t)yo * (uint32_t)(w / 2)) | (uint32_t)fr << 28;
-            }
-        }
-        rw[i] = e;
-    }
-    if (my_gen || S->dyn_qp < QP_MIN) gen = 1;            /* half-pel chroma chains; 16-bit levels */
-    __syncthreads();
-    if (t == 0) {
-        /* a general-path NAL takes a record slot (index in rbsp_bytes until
-         * k_dyn_epfix); none left: the frame fails (DF_OVER, the batch
-         * grows the pool for the next compose) */
-        uint32_t e = 0u;
-        if (gen) {
-            const uint32_t k = atomicAdd(&ctr[1], 1u);
-            if (k < g.gen_cap) {
-                DF->rbsp_bytes = k;
-                ctr[DYN_CTR_LIST + k] = (uint32_t)((size_t)s * ld_fr + f);   /* k_dyn_row<true>'s list */
-                e = DF_GENERAL;
-            } else {
-                e = DF_OVER;
-            }
-        }
-        DF->err = e;
-        DF->ep = 0u;                                    /* k_dyn_epscan adds to it */
-    }
-}
 
 /* ---------------------------------------------------------------------- */
 /* k_dyn_code_general: block records of the general-path NALs              */
@@ -849,6 +764,106 @@ __device__ inline uint4 body_msb(uint64_t hi, uint64_t lo, uint32_t n)
 
 /* ---------------------------------------------------------------------- */
 /* k_dyn_static: the static row groups of a dynamic NAL                    */
+/* ---------------------------------------------------------------------- */
+/* k_dyn_rows                                                              */
+/* ---------------------------------------------------------------------- */
+/* rows[n][i], i < 32 h (h = rect MB rows):
+ *   i < 16 h        luma row 16 y0 + i: byte offset of its prediction row in
+ *                   the stream's reference pair (picture * pic + row * w)
+ *   16 h .. 24 h    chroma row 8 y0 + i': the upper bilinear row
+ *                   (picture * pic + ysz + row * w / 2), the 1/8-pel
+ *                   fraction in bits 28..30, ROW_GEN if the waypoint chain
+ *                   has a half-pel step (the general path)
+ *   24 h .. 32 h    the lower bilinear row (used when the fraction != 0)
+ * Sets DynFrame.err = DF_GENERAL when some row of the NAL needs the general
+ * path (never for waypoints the composer creates), else 0. */
+__global__ __launch_bounds__(256) void k_dyn_rows(const DevStream *__restrict__ st,
+                                                  const NalDesc *__restrict__ nal, int ld_nal,
+                                                  const PlanPending *__restrict__ pend,
+                                                  DynFrame *__restrict__ dfr, int ld_fr, DynGeom g,
+                                                  uint32_t *__restrict__ rows, uint32_t *__restrict__ ctr,
+                                                  uint4 *__restrict__ heads)
+{
+    __shared__ int32_t wo[8], wl[8], wv[8];
+    __shared__ int32_t gen;
+    const int s = blockIdx.y, f = blockIdx.x, t = threadIdx.x;
+    DynFrame *DF = dfr + (size_t)s * ld_fr + f;
+    const int j = DF->nal;
+    if (j < 0) return;
+    if (t < 8) {
+        wo[t] = pend[s].wo[t];
+        wl[t] = pend[s].wl[t];
+        wv[t] = pend[s].wv[t];
+    }
+    if (t == 0) gen = 0;
+    __syncthreads();
+    const DevStream *S = st + s;
+    const NalDesc d = nal[(size_t)s * ld_nal + j];
+    const NalCtx c = nal_ctx(S, d, wo, wl, wv);
+    if (t < 12) {
+        /* the NAL's 12 MB-head classes, MSB first, for every
+         * rect row of k_dyn_row (which computed them once per row before):
+         * vectors 0-11 the bits, 12-14 the lengths (bit 31: over 128 bits,
+         * the row then writes its heads through the bit sink) */
+        const HeadCtx H = head_ctx(c);
+        CapSink hc{0, 0, 0};
+        H.put_class(hc, t);
+        uint4 *hv = heads + ((size_t)s * ld_fr + f) * DYN_HEAD_VECS;
+        hv[t] = body_msb(hc.hi, hc.lo, min(hc.n, 128u));
+        reinterpret_cast<uint32_t *>(hv + 12)[t] = hc.n | (hc.over() ? 0x80000000u : 0u);
+    }
+    const Regions rg = regions(c);
+    const int w = c.w, h = c.h, a_end = (h - c.off) / 16;
+    const uint32_t ysz = (uint32_t)w * (uint32_t)h, pic = ysz + ysz / 2;
+    const WpTab T{wo, wv, h};
+    uint32_t *rw = rows + ((size_t)s * ld_fr + f) * (size_t)(32 * g.h);
+    bool my_gen = false;
+    for (int i = t; i < 32 * g.h; i += 256) {
+        uint32_t e;
+        if (i < 16 * g.h) {
+            const int Y = 16 * g.y0 + i, row = Y >> 4;
+            const bool cA = row < a_end;
+            int yo;
+            const int b = luma_row(T, cA ? rg.ra : rg.rb, Y + (cA ? rg.mva : rg.mvb), yo);
+            e = (uint32_t)b * pic + (uint32_t)yo * (uint32_t)w;
+        } else {
+            const int i2 = i - 16 * g.h, bot = i2 >= 8 * g.h;
+            const int Y = 8 * g.y0 + (bot ? i2 - 8 * g.h : i2), row = Y >> 3;
+            const bool cA = row < a_end;
+            const int q = 4 * (cA ? rg.mva : rg.mvb), o = q >> 3, fr = q & 7;
+            int yo;
+            const int b = chroma_row(T, cA ? rg.ra : rg.rb, Y + o + bot, yo);
+            if (b < 0) {
+                e = ROW_GEN;
+                if (!bot || fr) my_gen = true;
+            } else {
+                e = ((uint32_t)b * pic + ysz + (uint32_t)yo * (uint32_t)(w / 2)) | (uint32_t)fr << 28;
+            }
+        }
+        rw[i] = e;
+    }
+    if (my_gen || S->dyn_qp < QP_MIN) gen = 1;            /* half-pel chroma chains; 16-bit levels */
+    __syncthreads();
+    if (t == 0) {
+        /* a general-path NAL takes a record slot (index in rbsp_bytes until
+         * k_dyn_epfix); none left: the frame fails (DF_OVER, the batch
+         * grows the pool for the next compose) */
+        uint32_t e = 0u;
+        if (gen) {
+            const uint32_t k = atomicAdd(&ctr[1], 1u);
+            if (k < g.gen_cap) {
+                DF->rbsp_bytes = k;
+                ctr[DYN_CTR_LIST + k] = (uint32_t)((size_t)s * ld_fr + f);   /* k_dyn_row<true>'s list */
+                e = DF_GENERAL;
+            } else {
+                e = DF_OVER;
+            }
+        }
+        DF->err = e;
+        DF->ep = 0u;                                    /* k_dyn_epfix sets it */
+    }
+}
+
 /* ---------------------------------------------------------------------- */
 /* A NAL's bits are: slice header, then per MB row the MB heads (one of 12
  * codeword classes) and, for dynamic MBs, coded_block_pattern,
@@ -1405,7 +1420,7 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
                                                      unsigned long long *__restrict__ tcx, uint32_t epoch,
                                                      uint32_t *__restrict__ rowstage, uint32_t *__restrict__ gbits,
                                                      uint32_t *__restrict__ spill, uint32_t *__restrict__ ctr,
-                                                     uint64_t *__restrict__ stamps)
+                                                     const uint4 *__restrict__ heads, uint64_t *__restrict__ stamps)
 {
     __shared__ RowFixed L;
     extern __shared__ uint4 rdyn[];
@@ -1481,6 +1496,15 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
     if (t == 0) {
         L.head_over = 0;
         L.ncand = 0;
+    }
+    if (t < 12) {                       /* the NAL's MB-head classes (k_dyn_rows) */
+        const uint4 *hv = heads + nb * DYN_HEAD_VECS;
+        const uint4 m = hv[t];
+        const uint32_t hl = reinterpret_cast<const uint32_t *>(hv + 12)[t];
+        L.hhi[t] = (uint64_t)m.x << 32 | m.y;
+        L.hlo[t] = (uint64_t)m.z << 32 | m.w;
+        L.hlen[t] = hl & 0x7fffffffu;
+        if (hl >> 31) L.head_over = 1;                  /* after lane 0's 0 (same wave, same word) */
     }
     if (t < SORT_KEYS) L.kc[0][t] = 0u;
     if (t < NPC) L.pcd[t] = pc_desc(t);
@@ -1656,12 +1680,17 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
             const int rec = rec_of(q0 + k, pc, ndt);
             const uint16_t mv = M[rec];
             mt[i] = mv;
+            /* an empty body stored as zeros: phases 3 and 5 OR a piece's
+             * first words whatever its length (stale LDS there was ORed into
+             * the row's bits) */
+            uint4 bv = make_uint4(0u, 0u, 0u, 0u);
             if ((mv & 255u) || (mv & M_OVF)) {
                 const uint4 bd = get_body(BL, BH, rec, (mv & 255u) > 64u || (mv & M_OVF));
-                lv[i] = (mv & M_OVF) ? bd
-                                     : body_msb((uint64_t)bd.z | (uint64_t)bd.w << 32,
-                                                (uint64_t)bd.x | (uint64_t)bd.y << 32, mv & 255u);
+                bv = (mv & M_OVF) ? bd
+                                  : body_msb((uint64_t)bd.z | (uint64_t)bd.w << 32,
+                                             (uint64_t)bd.x | (uint64_t)bd.y << 32, mv & 255u);
             }
+            lv[i] = bv;
         }
         for (int i = t; i < 8 * w; i += T) {
             const int k = i >> 3, e = i & 7;
@@ -1717,15 +1746,6 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
     ROW_CUT(2);
 
     /* ---- 3: coeff_token, piece lengths ----------------------------------- */
-    if (t < 12) {                                       /* the MB-head classes, MSB first (put_piece1's form) */
-        CapSink hc{0, 0, 0};
-        H.put_class(hc, t);
-        const uint4 m = body_msb(hc.hi, hc.lo, min(hc.n, 128u));
-        L.hhi[t] = (uint64_t)m.x << 32 | m.y;
-        L.hlo[t] = (uint64_t)m.z << 32 | m.w;
-        L.hlen[t] = hc.n;
-        if (hc.over()) L.head_over = 1;
-    }
     const Tabs &TB = g_tabs;
     const PTabs &PT = *reinterpret_cast<const PTabs *>(&g_ptabs);       /* the rare overflow paths */
     const uint16_t(*ctab)[68] = L.ptabs.ct;
@@ -1962,21 +1982,16 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
  * from bit 0 of its row-stage slot); the row groups' bit counts give their
  * offsets (one wave scan; ngroups <= 64).  An RBSP word is assembled from
  * the (one, at group seams two or more) row-stage words it spans -- a
- * funnel shift.  k_dyn_epscan reads EPS_CHUNK bytes at a time, EPS_KW words
- * per thread, word w of a chunk thread w % EPS_T's (neighbouring lanes read
+ * funnel shift.  ep_scan reads 4 EPS_KW NT bytes at a time, EPS_KW words
+ * per thread, word w of a chunk thread w % NT's (neighbouring lanes read
  * neighbouring row-stage words, the next chunk's loads in flight while this
  * one is scanned). */
 #ifndef SCROLL_EPS_KW
 #define SCROLL_EPS_KW 4
 #endif
 /* EPS_KW words per thread and chunk (4 or 8) */
-#ifndef SCROLL_EPS_T
-#define SCROLL_EPS_T 256
-#endif
-constexpr int EPS_T = SCROLL_EPS_T, EPS_NW = EPS_T / 64, EPS_KW = SCROLL_EPS_KW, EPS_CHUNK = EPS_T * 4 * EPS_KW;
+constexpr int EPS_KW = SCROLL_EPS_KW;
 static_assert(EPS_KW % 4 == 0, "the EP scan reads 16-byte LDS vectors");
-/* row groups per NAL at most (rect rows + static groups above / below) */
-constexpr int RS_GMAX = DYN_MAX_H + 2 * ((DYN_MAX_MBH + DYN_STATIC_ROWS - 1) / DYN_STATIC_ROWS);
 /* the group tables live in dynamic LDS sized by the NAL's group count
  * (goff [ng + 1], gb / gw [ng], then cw [ng] and cbase [ng + 1] where a
  * kernel has them): the benched rects' few groups take little LDS, a whole
@@ -2039,13 +2054,14 @@ __device__ inline int rs_group_at(uint32_t P, int ng, const uint32_t *goff)
     return lo;
 }
 
-/* the first source words of the EPS_KW words thread t assembles for the
- * chunk at byte c0 (x1: the next word, where the shift needs it) */
+/* the first source words of the EPS_KW words thread t (of NT) assembles
+ * for the chunk at byte c0 (x1: the next word, where the shift needs it) */
 struct ScanLoads {
     uint32_t x0[EPS_KW], x1[EPS_KW], y[EPS_KW];           /* y: the next group's first word (seam words) */
     int g[EPS_KW];
 };
 
+template <int NT>
 __device__ inline void scan_load(ScanLoads &L, uint32_t c0, int t, int ng, uint32_t T, const uint32_t *goff,
                                    const uint32_t *gb, const uint32_t *gw, const uint32_t *fr, int &gcarry)
 {
@@ -2056,7 +2072,7 @@ __device__ inline void scan_load(ScanLoads &L, uint32_t c0, int t, int ng, uint3
     while (gg + 1 < ng && goff[gg + 1] <= P0) ++gg;
 #pragma unroll
     for (int k = 0; k < EPS_KW; ++k) {
-        const uint32_t P = P0 + 32u * EPS_T * (uint32_t)k;
+        const uint32_t P = P0 + 32u * NT * (uint32_t)k;
         while (gg + 1 < ng && goff[gg + 1] <= P) ++gg;
         L.g[k] = gg;
         const uint32_t lp = P - goff[gg], i = lp >> 5;
@@ -2212,72 +2228,44 @@ __device__ inline void rs_load8(uint32_t P, int &gg, int ng, uint32_t T, const u
 }
 
 /* ---------------------------------------------------------------------- */
-/* k_dyn_epscan: a NAL's RBSP size and emulation-prevention positions, read  */
-/* straight from its row groups -- no staged copy of the RBSP               */
+/* ep_scan: a NAL's emulation-prevention positions, read straight from its  */
+/* row groups -- no staged copy of the RBSP                                 */
 /* ---------------------------------------------------------------------- */
-/* Only for the NALs k_dyn_epfix flagged DF_EPSLOW (more candidates or EP
- * bytes than it keeps; never in the benches).
- * EPS_Z workgroups per NAL; workgroup z takes the 4 KB chunks z, z + EPS_Z,
- * ... (the RBSP is never written anywhere: k_dyn_emit_gather assembles the
- * arena bytes from the row groups again).  Per chunk: every staged word from
- * the row-stage word(s) it spans (a funnel shift), the chunk's bytes in LDS,
- * then the closed-form EP rule per byte.  The zero run before the chunk comes
- * from a look-back over the RBSP before it, and only when the chunk's first
- * byte is <= 3 (otherwise no byte of the chunk can depend on it).  EP
- * positions gather in LDS and go to the frame's EP list (k_dyn_emit_gather
- * sorts them) at a base reserved by one global atomic per workgroup; DF->ep
- * ends as the NAL's total (k_dyn_epfix zeroed it and set rbsp_bytes). */
-#ifndef SCROLL_EPS_Z
-#define SCROLL_EPS_Z 4
-#endif
-constexpr int EPS_Z = SCROLL_EPS_Z;
-
-/* grid (EPS_Z, EPS_SLOTS): workgroup (z, j) takes the NALs j, j +
- * EPS_SLOTS, ... of the list k_dyn_epfix filled (*slow_n of them, slow[q] =
- * s ld_fr + f): an empty list costs EPS_Z EPS_SLOTS workgroups that read one
- * word, not one per frame */
-constexpr int EPS_SLOTS = 64;
-__global__ __launch_bounds__(EPS_T) void k_dyn_epscan(DevStream *__restrict__ st, DynFrame *__restrict__ dfr,
-                                                     int ld_fr, DynGeom g, const uint32_t *__restrict__ rowstage,
-                                                     const uint32_t *__restrict__ gbits, uint8_t *__restrict__ eps,
-                                                     const uint32_t *__restrict__ slow_n,
-                                                     const uint32_t *__restrict__ slow)
+/* Per chunk: every word from the row-stage word(s) it spans (a funnel
+ * shift), the chunk's bytes in LDS, then the closed-form EP rule per byte.
+ * The zero run before the chunk comes from a look-back over the RBSP before
+ * it, and only when the chunk's first byte is <= 3 (otherwise no byte of the
+ * chunk can depend on it). */
+/* A NAL whose EP sites the candidate records cannot give (DF_EPSLOW: a
+ * group over its record's candidate slots, or more positions than ep_fix's
+ * set holds) is scanned whole by its own k_dyn_epfix workgroup (NT
+ * threads), chunk after chunk, the next chunk's loads in flight; cbuf: NT
+ * EPS_KW words of LDS, wmax: NT / 64 words, ep_n: an LDS counter.  The
+ * positions go straight to the frame's EP list in any order (the gather
+ * sorts a DF_EPSLOW list); returns the NAL's EP byte count.  (Round 4 had
+ * this in a launch of its own over a device-side list, k_dyn_epscan: one
+ * launch per compose for NALs that config 3 never has) */
+template <int NT>
+__device__ uint32_t ep_scan(const uint32_t *fr, int ng, uint32_t T, const uint32_t *goff, const uint32_t *gb,
+                            const uint32_t *gw, uint32_t *cbuf, int *wmax, uint32_t &ep_n, uint32_t *eplist, int t)
 {
-    extern __shared__ uint32_t gdyn[];                  /* the group tables (gtab_bytes) */
-    const GTab GT = gtab_of(gdyn, g.ngroups);
-    uint32_t *goff = GT.goff, *gb = GT.gb, *gw = GT.gw;
-    __shared__ int32_t wmax[EPS_NW];
-    __shared__ uint32_t ep_n, ep_base;
-    __shared__ uint4 cbuf4[EPS_CHUNK / 16];              /* the chunk's bytes */
-    __shared__ uint32_t epl[EPLIST_MAX];                /* this workgroup's EP positions */
-    uint32_t *cbuf = reinterpret_cast<uint32_t *>(cbuf4);
-    (void)st;
-    const int z = blockIdx.x, t = threadIdx.x;
-    const uint32_t nslow = __builtin_amdgcn_readfirstlane(*slow_n);
-    for (uint32_t q = blockIdx.y; q < nslow; q += EPS_SLOTS) {
-    const size_t nb = __builtin_amdgcn_readfirstlane(slow[q]);
-    DynFrame *DF = dfr + nb;
-    __syncthreads();                                    /* the previous NAL's LDS reads are done */
-    const int ng = g.ngroups;
-    const uint32_t *fr = rowstage + nb * g.rs_frame_words;
-    rs_table(gbits, nb, g, fr, goff, gb, gw, nullptr, t);
+    constexpr int CH = NT * 4 * EPS_KW;                 /* bytes per chunk */
+    const uint32_t nin = (T + 7) >> 3;                  /* bitwriter.c:103-111 */
+    uint4 *cbuf4 = reinterpret_cast<uint4 *>(cbuf);
     if (t == 0) ep_n = 0;
     __syncthreads();
-    const uint32_t T = goff[ng];                        /* NAL RBSP bits incl. the stop bit */
-    const uint32_t nin = (T + 7) >> 3;                  /* bitwriter.c:103-111 */
     ScanLoads ld;
-    uint32_t c0 = (uint32_t)z * EPS_CHUNK;
     int gcarry = 0;
-    if (c0 < nin) {
-        gcarry = rs_group_at(c0 * 8u + 32u * (uint32_t)t, ng, goff);
-        scan_load(ld, c0, t, ng, T, goff, gb, gw, fr, gcarry);
+    if (nin > 0) {
+        gcarry = rs_group_at(32u * (uint32_t)t, ng, goff);
+        scan_load<NT>(ld, 0u, t, ng, T, goff, gb, gw, fr, gcarry);
     }
-    for (; c0 < nin; c0 += EPS_Z * EPS_CHUNK) {
+    for (uint32_t c0 = 0; c0 < nin; c0 += CH) {
         {
             const uint32_t P0 = c0 * 8u + 32u * (uint32_t)t;
 #pragma unroll
             for (int k = 0; k < EPS_KW; ++k) {
-                const uint32_t P = P0 + 32u * EPS_T * (uint32_t)k;
+                const uint32_t P = P0 + 32u * NT * (uint32_t)k;
                 const int g0 = ld.g[k];
                 const uint32_t lp = P - goff[g0], sh = lp & 31u;
                 uint32_t v = 0;
@@ -2296,11 +2284,11 @@ __global__ __launch_bounds__(EPS_T) void k_dyn_epscan(DevStream *__restrict__ st
                         }
                     }
                 }
-                cbuf[t + EPS_T * k] = __builtin_bswap32(v);   /* memory order */
+                cbuf[t + NT * k] = __builtin_bswap32(v);    /* memory order */
             }
         }
-        const uint32_t cn = c0 + EPS_Z * EPS_CHUNK;
-        if (cn < nin) scan_load(ld, cn, t, ng, T, goff, gb, gw, fr, gcarry);
+        const uint32_t cn = c0 + CH;
+        if (cn < nin) scan_load<NT>(ld, cn, t, ng, T, goff, gb, gw, fr, gcarry);
         lds_barrier();                                  /* the next chunk's loads stay in flight */
         /* the last non-zero RBSP byte before the chunk: needed only when its
          * first byte is <= 3 (else that byte is non-zero and no EP decision
@@ -2331,7 +2319,7 @@ __global__ __launch_bounds__(EPS_T) void k_dyn_epscan(DevStream *__restrict__ st
         }
         if (t == 0 && lnz < 0) lnz = lz;                /* the run reaching back past the chunk */
         int ex, tot;
-        block_excl_max<EPS_NW, true>(lnz, wmax, ex, tot);   /* its barriers also free cbuf */
+        block_excl_max<NT / 64, true>(lnz, wmax, ex, tot);   /* its barriers also free cbuf */
         int prev = t == 0 ? lz : ex;
         uint32_t ins = 0;
 #pragma unroll
@@ -2346,21 +2334,13 @@ __global__ __launch_bounds__(EPS_T) void k_dyn_epscan(DevStream *__restrict__ st
             while (ins) {
                 const int i = __builtin_ctz(ins);
                 ins &= ins - 1u;
-                if (k < (uint32_t)EPLIST_MAX) epl[k] = ib + (uint32_t)i;   /* RBSP index the 03 precedes */
+                if (k < (uint32_t)EPLIST_MAX) eplist[k] = ib + (uint32_t)i;   /* RBSP index the 03 precedes */
                 k++;
             }
         }
     }
     __syncthreads();
-    const uint32_t n = ep_n;
-    if (n == 0) continue;
-    if (t == 0) ep_base = atomicAdd(&DF->ep, n);
-    __syncthreads();
-    uint32_t *eplist = reinterpret_cast<uint32_t *>(eps + nb * DYN_OVF_BYTES);
-    const uint32_t base = ep_base;
-    for (uint32_t i = (uint32_t)t; i < n && i < (uint32_t)EPLIST_MAX; i += EPS_T)
-        if (base + i < (uint32_t)EPLIST_MAX) eplist[base + i] = epl[i];
-    }
+    return ep_n;
 }
 
 /* ---------------------------------------------------------------------- */
@@ -2378,7 +2358,7 @@ __global__ __launch_bounds__(EPS_T) void k_dyn_epscan(DevStream *__restrict__ st
  * Every other byte is preceded by a non-zero byte within fewer than 22 zero
  * bits.  A byte can be decided twice (a run's last byte at a seam): kept
  * once.  More candidates in a group than its record holds, or more than EPF_LIST
- * positions: DF_EPSLOW (k_dyn_epscan scans the NAL). */
+ * positions: DF_EPSLOW (the workgroup scans the NAL, ep_scan). */
 #ifndef SCROLL_EPF_T
 #define SCROLL_EPF_T 128
 #endif
@@ -2520,7 +2500,7 @@ __device__ __attribute__((always_inline)) inline uint32_t ep_list_windows(uint32
 template <int NT, int LCAP>
 __device__ inline void ep_fix(DevStream *st, DynFrame *DF, size_t nb, int s, const DynGeom &g,
                               const uint32_t *rowstage, const uint32_t *gbits, uint8_t *eps, const EpfLds &E,
-                              int t, uint32_t *slow_n, uint32_t *slow_list, uint64_t *stp)
+                              int t, uint64_t *stp)
 {
     static_assert(NT >= 128 && NT % 64 == 0, "ep_fix: one seam wave and at least one candidate wave");
     static_assert(LCAP % (4 * NT) == 0 && LCAP >= 8 * NT, "ep_fix: the bitmap in whole 16-byte chunks per thread");
@@ -2614,6 +2594,7 @@ __device__ inline void ep_fix(DevStream *st, DynFrame *DF, size_t nb, int s, con
                 const uint32_t S = goff[k];
                 if (S < T) ep_eval_bytes(S >> 3, (S + 7) >> 3, nin, ng, T, goff, gb, gw, fr, bm, lst, &nlst, lcap);
             }
+            if (stp && lane == 0) stp[7] = __builtin_amdgcn_s_memrealtime();   /* the seam wave's end */
         }
         /* candidate words, CB per thread and pass: the index loads, then
          * the three data words of each, then the runs */
@@ -2665,20 +2646,23 @@ __device__ inline void ep_fix(DevStream *st, DynFrame *DF, size_t nb, int s, con
                 }
             }
         }
+        stamp(4);                                       /* wave 0's candidates done */
     }
     __syncthreads();
     stamp(2);
     const uint32_t n = nlst;
-    if (slow || (!bm && n > lcap)) {
+    uint32_t *eplist = reinterpret_cast<uint32_t *>(eps + nb * DYN_OVF_BYTES);
+    if (slow || (!bm && n > lcap)) {                    /* the whole NAL scanned here */
+        static_assert(NT * EPS_KW <= LCAP, "ep_scan's chunk buffer is the position set's LDS");
+        __syncthreads();                                /* every thread is past the set */
+        const uint32_t ne = ep_scan<NT>(fr, ng, T, goff, gb, gw, lst, reinterpret_cast<int *>(E.ws), nlst, eplist, t);
         if (t == 0) {
-            DF->err = DF_EPSLOW | DF_FIXED;             /* k_dyn_epscan finds them */
+            DF->err = DF_EPSLOW | DF_FIXED;             /* the list unsorted: the gather sorts it */
             DF->rbsp_bytes = nin;
-            DF->ep = 0;
-            slow_list[atomicAdd(slow_n, 1u)] = (uint32_t)nb;   /* at most once per frame */
+            DF->ep = ne;
         }
         return;
     }
-    uint32_t *eplist = reinterpret_cast<uint32_t *>(eps + nb * DYN_OVF_BYTES);
     constexpr int CW = LCAP / NT;                       /* bitmap words per thread (whole bitmap) */
     if (!bm && n <= lcap - 4u * NT) {
         const uint32_t base = ep_list_windows<NT, LCAP>(lst, n, nin, eplist, E.ws, t, lane, wave);
@@ -2764,7 +2748,6 @@ __device__ inline void ep_fix(DevStream *st, DynFrame *DF, size_t nb, int s, con
         DF->ep = nu;
         if (stp) stp[6] = (uint64_t)nc | (uint64_t)nu << 32;
     }
-    stamp(4);
     stamp(5);
 }
 
@@ -2776,7 +2759,6 @@ __global__ __launch_bounds__(EPF_T) void k_dyn_epfix(DevStream *__restrict__ st,
                                                      int ld_fr, int nframes, DynGeom g,
                                                      const uint32_t *__restrict__ rowstage,
                                                      const uint32_t *__restrict__ gbits, uint8_t *__restrict__ eps,
-                                                     uint32_t *__restrict__ slow_n, uint32_t *__restrict__ slow,
                                                      uint64_t *__restrict__ stamps)
 {
     __shared__ __attribute__((aligned(16))) uint32_t lst[EPF_LIST];   /* the position bitmap / list */
@@ -2790,11 +2772,11 @@ __global__ __launch_bounds__(EPF_T) void k_dyn_epfix(DevStream *__restrict__ st,
     DynFrame *DF = dfr + nb;
     if (DF->nal < 0) return;
     const EpfLds E{goff, gb, gw, cw, cbase, lst, cnt, ws};
-    ep_fix<EPF_T, EPF_LIST>(st, DF, nb, s, g, rowstage, gbits, eps, E, t, slow_n, slow, stamps ? stamps + ((size_t)s * nframes + f) * 8 : nullptr);
+    ep_fix<EPF_T, EPF_LIST>(st, DF, nb, s, g, rowstage, gbits, eps, E, t, stamps ? stamps + ((size_t)s * nframes + f) * 8 : nullptr);
 }
 
 /* ---------------------------------------------------------------------- */
-/* k_dyn_emit: staged RBSP -> arena with start code, header, EP bytes       */
+/* emit_serial: RBSP -> arena with start code, header, EP bytes            */
 /* ---------------------------------------------------------------------- */
 __device__ inline void store16(uint8_t *A, uint64_t p, const uint8_t *src, uint64_t lo, uint64_t hi)
 {
@@ -2806,30 +2788,22 @@ __device__ inline void store16(uint8_t *A, uint64_t p, const uint8_t *src, uint6
         if (p + i >= lo && p + i < hi) A[p + i] = src[i];
 }
 
-/* rowstage != nullptr: the dynamic rect's NALs, whose RBSP lives only in
- * their row groups (gbits); else the staged RBSP of the hint / splice path */
-__global__ __launch_bounds__(DT) void k_dyn_emit(const DevStream *__restrict__ st,
-                                                 const NalDesc *__restrict__ nal, int ld_nal,
-                                                 const DynFrame *__restrict__ dfr, int ld_fr,
-                                                 DynGeom g, const uint8_t *__restrict__ stage,
-                                                 const uint32_t *__restrict__ rowstage,
-                                                 const uint32_t *__restrict__ gbits,
-                                                 uint8_t *__restrict__ arena, uint64_t ld_arena)
+/* The NALs with more EP bytes than the gathers keep positions for
+ * (ep_cap: past 2,048, or 4 under SCROLL_DEBUG_DYN_EPCAP4): one workgroup
+ * streams the NAL through an LDS byte buffer, finding the EP sites on the
+ * way.  Called by the gather workgroup of the NAL (z = 0) in place of its
+ * chunk loop -- no launch of its own.  rowstage != nullptr: the dynamic
+ * rect's NALs, whose RBSP lives only in their row groups (gbits, tables in
+ * goff / gb / gw); else the staged RBSP of the hint / splice path.  ob: OBUF
+ * bytes (16-byte aligned), wmax / wsum: NW words each, of the caller's LDS */
+__device__ __attribute__((always_inline)) inline void emit_serial(const NalDesc &d, const DynFrame &df, size_t nb, int s,
+                                                      const DynGeom &g, const uint8_t *__restrict__ stage,
+                                                      const uint32_t *__restrict__ rowstage,
+                                                      const uint32_t *__restrict__ gbits,
+                                                      uint8_t *__restrict__ arena, uint64_t ld_arena,
+                                                      uint32_t *goff, uint32_t *gb, uint32_t *gw, uint8_t *ob,
+                                                      int32_t *wmax, uint32_t *wsum, int t)
 {
-    __shared__ alignas(16) uint8_t ob[OBUF];
-    __shared__ int32_t wmax[NW];
-    __shared__ uint32_t wsum[NW];
-    extern __shared__ uint32_t gdyn[];                  /* the group tables (gtab_bytes) */
-    const GTab GT = gtab_of(gdyn, g.ngroups);
-    uint32_t *goff = GT.goff, *gb = GT.gb, *gw = GT.gw;
-    const int f = blockIdx.x, s = blockIdx.y, t = threadIdx.x;
-    const size_t nb = (size_t)s * ld_fr + f;
-    const DynFrame df = dfr[nb];
-    const int j = df.nal;
-    if (j < 0 || j >= st[s].nnal || (df.err & ~(DF_EPSLOW | DF_FIXED))) return;   /* nnal = 0: nothing committed */
-    if (df.ep <= ep_cap(g)) return;                          /* k_dyn_emit_gather's NAL */
-    const NalDesc d = nal[(size_t)s * ld_nal + j];
-    if (d.slow != 2) return;
     uint8_t *A = arena + (size_t)s * ld_arena;
     const uint64_t o0 = d.out_off, o1 = o0 + d.size;
     const bool RS = rowstage != nullptr;
@@ -2905,6 +2879,7 @@ __global__ __launch_bounds__(DT) void k_dyn_emit(const DevStream *__restrict__ s
     }
     for (uint32_t c = (uint32_t)t; 16u * c < fill; c += DT) store16(A, lb + 16u * c, ob + 16u * c, o0, o1);
 }
+static_assert(OBUF <= 4 * EPLIST_MAX && NW <= EPLIST_MAX, "emit_serial's buffers fit the gathers' LDS lists");
 
 /* ---------------------------------------------------------------------- */
 /* k_dyn_emit_gather: the same output for NALs with <= EPLIST_MAX EP bytes  */
@@ -2927,7 +2902,7 @@ __device__ inline uint32_t pick4(const uint32_t w[8], int i)     /* w[i], i in 0
 constexpr int GATHER_Z = SCROLL_GATHER_Z;             /* workgroups per NAL (2 and 4 measured slower) */
 
 /* RS: the dynamic rect's NALs -- RBSP bytes assembled from the row groups
- * (rs_load8), EP lists at stage + DYN_OVF_BYTES per frame (k_dyn_epscan);
+ * (rs_load8), EP lists at stage + DYN_OVF_BYTES per frame (k_dyn_epfix);
  * else the staged RBSP + slot-tail EP list of the hint / splice path */
 template <int U, bool RS>
 __global__ __launch_bounds__(DT) void k_dyn_emit_gather(const DevStream *__restrict__ st,
@@ -2939,7 +2914,8 @@ __global__ __launch_bounds__(DT) void k_dyn_emit_gather(const DevStream *__restr
                                                         uint8_t *__restrict__ arena, uint64_t ld_arena,
                                                         uint64_t *__restrict__ stamps)
 {
-    __shared__ uint32_t raw[EPLIST_MAX], sp[EPLIST_MAX];
+    __shared__ alignas(16) uint32_t raw[EPLIST_MAX];
+    __shared__ uint32_t sp[EPLIST_MAX];
     extern __shared__ uint32_t gdyn[];                  /* RS: the group tables (gtab_bytes) */
     const GTab GT = gtab_of(gdyn, RS ? g.ngroups : 0);
     uint32_t *goff = GT.goff, *gb = GT.gb, *gw = GT.gw;
@@ -2951,16 +2927,21 @@ __global__ __launch_bounds__(DT) void k_dyn_emit_gather(const DevStream *__restr
     const int j = df.nal;
     if (j < 0 || j >= st[s].nnal || (df.err & ~(DF_EPSLOW | DF_FIXED))) return;   /* nnal = 0: nothing committed */
     const uint32_t n = df.ep;
-    if (n > ep_cap(g)) return;                               /* k_dyn_emit's NAL */
     const NalDesc d = nal[(size_t)s * ld_nal + j];
     if (d.slow != 2) return;
     const size_t nb = (size_t)s * ld_fr + f;
+    if (n > ep_cap(g)) {                                     /* past the position list: streamed */
+        if (blockIdx.z == 0)
+            emit_serial(d, df, nb, s, g, stage, rowstage, gbits, arena, ld_arena, goff, gb, gw,
+                        reinterpret_cast<uint8_t *>(raw), reinterpret_cast<int32_t *>(sp), sp + NW, t);
+        return;
+    }
     const uint8_t *in = RS ? nullptr : stage + nb * g.slot_bytes;
     const uint32_t *el = reinterpret_cast<const uint32_t *>(RS ? stage + nb * DYN_OVF_BYTES
                                                                : in + g.slot_bytes - DYN_OVF_BYTES);
     const uint32_t *fr = RS ? rowstage + nb * g.rs_frame_words : nullptr;
     if (RS) rs_table(gbits, nb, g, fr, goff, gb, gw, nullptr, t);
-    /* ep_fix leaves the list sorted (not k_dyn_epscan, nor the hint / splice path) */
+    /* ep_fix leaves the list sorted (not ep_scan, nor the hint / splice path) */
     const bool sorted = RS && !(df.err & DF_EPSLOW);
     for (uint32_t i = t; i < n; i += DT) (sorted ? sp : raw)[i] = el[i];
     __syncthreads();
@@ -3169,7 +3150,7 @@ __device__ inline W4 shr128(const W4 &x, uint32_t s)
     return W4{{a[0], a[1], a[2], a[3]}};
 }
 
-__global__ __launch_bounds__(DT) void k_dyn_gather(const DevStream *__restrict__ st,
+__global__ __launch_bounds__(DT) __attribute__((amdgpu_waves_per_eu(8))) void k_dyn_gather(const DevStream *__restrict__ st,
                                                   const NalDesc *__restrict__ nal, int ld_nal,
                                                   const DynFrame *__restrict__ dfr, int ld_fr, DynGeom g,
                                                   const uint8_t *__restrict__ eps,
@@ -3178,7 +3159,8 @@ __global__ __launch_bounds__(DT) void k_dyn_gather(const DevStream *__restrict__
                                                   uint8_t *__restrict__ arena, uint64_t ld_arena,
                                                   uint64_t *__restrict__ stamps)
 {
-    __shared__ uint32_t raw[EPLIST_MAX], sp[EPLIST_MAX + 1];
+    __shared__ alignas(16) uint32_t raw[EPLIST_MAX];
+    __shared__ uint32_t sp[EPLIST_MAX + 1];
     extern __shared__ uint32_t gdyn[];                  /* the group tables (gtab_bytes) */
     const GTab GT = gtab_of(gdyn, g.ngroups);
     uint32_t *goff = GT.goff, *gb = GT.gb, *gw = GT.gw;
@@ -3187,9 +3169,14 @@ __global__ __launch_bounds__(DT) void k_dyn_gather(const DevStream *__restrict__
     const int j = df.nal;
     if (j < 0 || j >= st[s].nnal || (df.err & ~(DF_EPSLOW | DF_FIXED))) return;   /* nnal = 0: nothing committed */
     const uint32_t n = df.ep;
-    if (n > ep_cap(g)) return;                               /* k_dyn_emit's NAL */
     const NalDesc d = nal[(size_t)s * ld_nal + j];
     if (d.slow != 2) return;
+    if (n > ep_cap(g)) {                                     /* past the position list: streamed */
+        if (blockIdx.z == 0)
+            emit_serial(d, df, (size_t)s * ld_fr + f, s, g, nullptr, rowstage, gbits, arena, ld_arena, goff, gb,
+                        gw, reinterpret_cast<uint8_t *>(raw), reinterpret_cast<int32_t *>(sp), sp + NW, t);
+        return;
+    }
     /* debug (SCROLL_DEBUG_DYN_STAMPS): realtime at entry, after the prologue, at the end */
     uint64_t *stp = stamps && blockIdx.z == 0 && t == 0 ? stamps + ((size_t)s * gridDim.x + blockIdx.x) * 8 : nullptr;
     if (stp) stp[0] = __builtin_amdgcn_s_memrealtime();
@@ -3201,7 +3188,7 @@ __global__ __launch_bounds__(DT) void k_dyn_gather(const DevStream *__restrict__
     for (uint32_t i = t; i < n; i += DT) (sorted ? sp : raw)[i] = el[i];
     if (t == 0) sp[n] = 0x3fffffffu;                         /* sentinel: sp[n] + n never before a chunk */
     __syncthreads();
-    for (uint32_t i = t; i < (sorted ? 0u : n); i += DT) {   /* k_dyn_epscan's lists: by rank */
+    for (uint32_t i = t; i < (sorted ? 0u : n); i += DT) {   /* ep_scan's lists: by rank */
         const uint32_t v = raw[i];
         uint32_t r = 0;
         for (uint32_t k = 0; k < n; ++k) r += raw[k] < v ? 1u : 0u;
@@ -3391,7 +3378,7 @@ int dyn_launch_code(hipStream_t hs, int nframes, int S, DevStream *st, const Nal
         }
     }
     hipLaunchKernelGGL(k_dyn_rows, dim3(nframes, S), dim3(256), 0, hs, st, nal, ld_nal, pend, dfr, ld_fr,
-                       *g, x->rows, x->ctr);
+                       *g, x->rows, x->ctr, x->heads);
     if (hipGetLastError() != hipSuccess) return -1;
     const int nchunk = (24 * g->w * g->h + CODE_T - 1) / CODE_T;
     hipLaunchKernelGGL(k_dyn_code_general, dim3(nchunk, CODE_GEN_Y), dim3(CODE_T), 0, hs, st, dfr, ld_fr,
@@ -3411,14 +3398,14 @@ int dyn_launch_code(hipStream_t hs, int nframes, int S, DevStream *st, const Nal
     hipLaunchKernelGGL(k_dyn_row<false>, dim3(g->h, nframes, S), dim3(row_threads(g->w)),
                        row_lds_bytes(g->w, mbw), hs, st, nal, ld_nal, pend, dfr, ld_fr, *g, x->rows, src, refs,
                        x->meta, x->body_lo, x->body_hi, x->body_w, x->tcx, epoch, x->rowstage, x->gbits, x->spill,
-                       x->ctr, stamps);
+                       x->ctr, x->heads, stamps);
     if (hipGetLastError() != hipSuccess) return -1;
     /* the general path: one row workgroup per record slot that may be taken */
     hipLaunchKernelGGL(k_dyn_row<true>, dim3(g->h, std::min<uint32_t>(g->gen_cap, (uint32_t)(nframes * S)), 1),
                        dim3(row_threads(g->w)),
                        row_lds_bytes(g->w, mbw), hs, st, nal, ld_nal, pend, dfr, ld_fr, *g, x->rows, src, refs,
                        x->meta, x->body_lo, x->body_hi, x->body_w, x->tcx, epoch, x->rowstage, x->gbits, x->spill,
-                       x->ctr, stamps);
+                       x->ctr, x->heads, stamps);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -3437,14 +3424,8 @@ int dyn_launch_pack(hipStream_t hs, int nframes, int S, DevStream *st, const Nal
 {
     if (nframes <= 0 || S <= 0) return 0;
     if (dyn_launch_static(hs, nframes, S, st, nal, ld_nal, pend, dfr, ld_fr, g, x)) return -1;
-    uint32_t *slow_n = x->ctr + DYN_CTR_SLOW, *slow = x->ctr + DYN_CTR_LIST + x->ctr_frames;
     hipLaunchKernelGGL(k_dyn_epfix, dim3(nframes, S), dim3(EPF_T), gtab_bytes(g->ngroups, true), hs, st, dfr,
-                       ld_fr, nframes, *g,
-                       x->rowstage, x->gbits, eps, slow_n, slow, stamps);
-    if (hipGetLastError() != hipSuccess) return -1;
-    hipLaunchKernelGGL(k_dyn_epscan, dim3(EPS_Z, EPS_SLOTS), dim3(EPS_T), gtab_bytes(g->ngroups, false), hs, st,
-                       dfr, ld_fr, *g,
-                       x->rowstage, x->gbits, eps, slow_n, slow);
+                       ld_fr, nframes, *g, x->rowstage, x->gbits, eps, stamps);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -3477,9 +3458,6 @@ int dyn_launch_emit(hipStream_t hs, int nframes, int S, const DevStream *st, con
     else
         hipLaunchKernelGGL((k_dyn_emit_gather<1, false>), grid, dim3(DT), 0, hs, st, nal, ld_nal, dfr, ld_fr,
                            *g, stage, rs, gbits, arena, ld_arena, stamps);
-    if (hipGetLastError() != hipSuccess) return -1;
-    hipLaunchKernelGGL(k_dyn_emit, dim3(nframes, S), dim3(DT), gl, hs, st, nal, ld_nal, dfr, ld_fr,
-                       *g, stage, rs, gbits, arena, ld_arena);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

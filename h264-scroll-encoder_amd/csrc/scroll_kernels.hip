@@ -121,7 +121,8 @@ __global__ __launch_bounds__(PLAN_THREADS) void k_plan(DevStream *__restrict__ s
                                                        int flags, PlanPending *__restrict__ pend,
                                                        DynFrame *__restrict__ dfr, int ld_fr,
                                                        const uint32_t *__restrict__ pool_ctr = nullptr,
-                                                       uint32_t spill_cap = 0, uint32_t gen_cap = 0)
+                                                       uint32_t spill_cap = 0, uint32_t gen_cap = 0,
+                                                       uint32_t *__restrict__ ctr_zero = nullptr)
 {
     const int s = blockIdx.x;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -138,6 +139,9 @@ __global__ __launch_bounds__(PLAN_THREADS) void k_plan(DevStream *__restrict__ s
         s_wl[tid] = S->wp_lt[tid];
         s_wv[tid] = S->wp_valid[tid];
     }
+    /* the dynamic rect's per-compose counters (spill / record slots),
+     * zeroed here rather than by a fill launch of their own */
+    if (ctr_zero && s == 0 && tid < DYN_CTR_LIST) ctr_zero[tid] = 0u;
     if (tid == 0) {
         s_cfg[0] = S->w; s_cfg[1] = S->h; s_cfg[2] = S->log2_mfn; s_cfg[3] = S->poc_type;
         s_cfg[4] = S->log2_poc; s_cfg[5] = S->deblock; s_cfg[6] = S->frame_num; s_cfg[7] = S->nwp;
@@ -384,7 +388,7 @@ __global__ __launch_bounds__(PLAN_THREADS) void k_plan(DevStream *__restrict__ s
 /* head from memory (the previous compose's bytes); its last tile zero-     */
 /* fills its line tail (arena slack).  Tiles holding a serial-path NAL use  */
 /* the generic byte path and the owning lane writes that NAL serially;     */
-/* dynamic-rect NALs (slow = 2) are written by k_dyn_emit.                  */
+/* dynamic-rect NALs (slow = 2) are written by k_dyn_gather.                */
 /* ---------------------------------------------------------------------- */
 constexpr int PURE_U = 4;         /* 64-chunk groups per stream iteration      */
 constexpr int XB = SEAM_XB, XA = SEAM_XA;   /* neighbour layouts before / after the tile */
@@ -771,7 +775,7 @@ __global__ __launch_bounds__(EMIT_WAVES * 64) void k_emit(const DevStream *__res
     } else {
         /* generic byte path: the bytes of every own run-layout NAL, one
          * byte per lane; serial-path and dynamic-rect NALs are written by
-         * their own writers (below / k_dyn_emit) */
+         * their own writers (below / k_dyn_gather) */
         const Lay *Lo = L + XB;
         const int32_t *no = noff + XB;
         for (int jn = 0; jn < cnt; ++jn) {
@@ -1314,10 +1318,11 @@ static int launch(ScrollBatch *b, int nframes, int plan_mode, int nal_max, hipSt
         HIPCHK(hipGetLastError());
         if ((rc = mark(1)) || (rc = mark(2)) || (rc = mark(3))) return rc;
     } else {
+        const bool dyn_rect = b->dyn_on && !hint;
         hipLaunchKernelGGL(k_plan, dim3(S), dim3(PLAN_THREADS), 0, hs, b->d_st, b->d_off,
                            b->max_frames, b->d_nal, b->ld_nal, nframes, plan_mode,
                            b->debug | plan_flags | PLAN_STATE | PLAN_DYN, b->d_pend, b->d_dfr,
-                           ld_fr);
+                           ld_fr, nullptr, 0u, 0u, dyn_rect ? b->dx.ctr : nullptr);
         HIPCHK(hipGetLastError());
         if ((rc = mark(1))) return rc;
         uint64_t *stamps = nullptr;
@@ -1370,7 +1375,6 @@ static int launch(ScrollBatch *b, int nframes, int plan_mode, int nal_max, hipSt
              * at 2 / 4 / 8 chunks: DESIGN.md §6; the device-side frame lists
              * are batch-wide, so the launches below cover the whole batch) */
             const DynGeom &G = b->geo;
-            HIPCHK(hipMemsetAsync(b->dx.ctr, 0, DYN_CTR_LIST * sizeof(uint32_t), hs));   /* spill / record slots, epscan list */
             if (dyn_launch_code(hs, nframes, S, b->d_st, b->d_nal, b->ld_nal, b->d_pend, b->d_dfr, ld_fr, &G,
                                 b->d_src, b->d_refs, &b->dx, b->dx.epoch, b->dyn_pw / 16, stamps)) {
                 set_err("k_dyn_code launch: %s", hipGetErrorString(hipGetLastError()));
@@ -1379,7 +1383,7 @@ static int launch(ScrollBatch *b, int nframes, int plan_mode, int nal_max, hipSt
             if ((rc = mark(6))) return rc;
             if (dyn_launch_pack(hs, nframes, S, b->d_st, b->d_nal, b->ld_nal, b->d_pend, b->d_dfr, ld_fr, &G,
                                 &b->dx, b->d_stage, stamps ? b->d_dbg : nullptr)) {
-                set_err("k_dyn_static / k_dyn_epscan launch: %s", hipGetErrorString(hipGetLastError()));
+                set_err("k_dyn_static / k_dyn_epfix launch: %s", hipGetErrorString(hipGetLastError()));
                 return SCROLL_ERR_HIP;
             }
         }
@@ -1414,7 +1418,7 @@ static int launch(ScrollBatch *b, int nframes, int plan_mode, int nal_max, hipSt
                                (uint64_t)b->ld_arena,
                                (b->debug & SCROLL_DEBUG_DYN_STAMPS) && b->d_dbg
                                    ? b->d_dbg + (size_t)nframes * S * 8 : nullptr)) {
-        set_err("k_dyn_emit launch: %s", hipGetErrorString(hipGetLastError()));
+        set_err("k_dyn_gather launch: %s", hipGetErrorString(hipGetLastError()));
         return SCROLL_ERR_HIP;
     }
     if ((rc = mark(5))) return rc;
@@ -1826,6 +1830,7 @@ static void dyn_release(ScrollBatch *b)
     (void)hipFree(b->dx.body_lo);
     (void)hipFree(b->dx.body_hi);
     (void)hipFree(b->dx.body_w);
+    (void)hipFree(b->dx.heads);
     (void)hipFree(b->dx.tcx);
     (void)hipFree(b->dx.rowstage);
     (void)hipFree(b->dx.ctr);
@@ -1939,13 +1944,14 @@ int scroll_batch_set_dyn_rect(ScrollBatch *b, int x0, int y0, int w, int h, size
     if (e == hipSuccess) e = hipMalloc(&b->dx.body_hi, nrec * sizeof(uint2));
     if (e == hipSuccess) e = hipMalloc(&b->dx.body_w, nrec * sizeof(uint4));
     const size_t ng = (size_t)g.ngroups;
+    if (e == hipSuccess) e = hipMalloc(&b->dx.heads, S * F * DYN_HEAD_VECS * sizeof(uint4));
     if (e == hipSuccess) e = hipMalloc(&b->dx.tcx, S * F * w * h * sizeof(unsigned long long));
     if (e == hipSuccess) e = hipMemset(b->dx.tcx, 0, S * F * w * h * sizeof(unsigned long long));
     const size_t rs_words = S * F * g.rs_frame_words + (size_t)g.rs_spill_cap * g.rs_spill_words;
     if (e == hipSuccess) e = hipMalloc(&b->dx.rowstage, rs_words * sizeof(uint32_t));
     if (e == hipSuccess) b->dx.spill = b->dx.rowstage + S * F * g.rs_frame_words;
-    /* counters, the general-record list and the k_dyn_epscan list (dyn_engine.h) */
-    if (e == hipSuccess) e = hipMalloc(&b->dx.ctr, (DYN_CTR_LIST + 2 * S * F) * sizeof(uint32_t));
+    /* counters and the general-record list (dyn_engine.h) */
+    if (e == hipSuccess) e = hipMalloc(&b->dx.ctr, (DYN_CTR_LIST + S * F) * sizeof(uint32_t));
     b->dx.ctr_frames = (uint32_t)(S * F);
     if (e == hipSuccess) e = hipMalloc(&b->dx.gbits, S * F * ng * sizeof(uint32_t));
     b->dx.epoch = 0;

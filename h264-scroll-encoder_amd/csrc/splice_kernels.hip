@@ -680,6 +680,15 @@ __global__ __launch_bounds__(64) void k_splice_unesc(int n, const int32_t *__res
  * k_splice_parse's. */
 constexpr int SPLICE_REDO = 99;
 constexpr int LANE_WAVES = 1;
+/* slices per wave: the lanes past it only build the tables.  The parse is a
+ * chain of dependent loads per slice, and a frame batch has few slices per
+ * SIMD (config-3 rows: 102,400 slices = 1.6 full waves per SIMD), so fewer
+ * slices per wave put more waves on each SIMD to overlap their chains */
+#ifndef SCROLL_SPLICE_LPW
+#define SCROLL_SPLICE_LPW 64
+#endif
+constexpr int LANE_ACTIVE = SCROLL_SPLICE_LPW;
+static_assert(LANE_ACTIVE >= 1 && LANE_ACTIVE <= 64 && LANE_WAVES == 1, "k_splice_lanes: one wave, 1-64 slices");
 
 struct LaneLds {
     uint16_t ct[4][128];                 /* coeff_token: lz 8 + 3 bits -> len << 8 | tc << 2 | t1 */
@@ -874,11 +883,11 @@ __global__ __launch_bounds__(64 * LANE_WAVES) void k_splice_lanes(const int32_t 
     __shared__ LaneLds L;
     const int t = threadIdx.x, lane = t & 63;
     const int nl = lanes[0];
-    const int stride = (int)gridDim.x * (int)blockDim.x;
-    if ((int)blockIdx.x * (int)blockDim.x >= nl) return;
+    const int stride = (int)gridDim.x * LANE_ACTIVE;
+    if ((int)blockIdx.x * LANE_ACTIVE >= nl) return;
     lane_tables(L, t, (int)blockDim.x);
     __syncthreads();
-    for (int q = (int)blockIdx.x * (int)blockDim.x + t; q < nl; q += stride) {
+    for (int q = t < LANE_ACTIVE ? (int)blockIdx.x * LANE_ACTIVE + t : nl; q < nl; q += stride) {
         const int idx = list[lanes[1 + 2 * q]], u = lanes[2 + 2 * q];
         const SpliceFrame *F = spf + idx;
         SpliceUnit *UN = units + F->unit_first + u;
@@ -2431,7 +2440,7 @@ int splice_launch_parse(hipStream_t hs, int n, int ymax, const int32_t *list, Sp
     const dim3 gy(n, (unsigned)std::max(1, std::min(ymax, 64)));
     hipLaunchKernelGGL(k_splice_units, dim3(n), dim3(DT), 0, hs, n, list, spf, units, lanes);
     hipLaunchKernelGGL(k_splice_unesc, gy, dim3(64), 0, hs, n, list, spf, units, rbsp);
-    const unsigned lw = (unsigned)std::min<size_t>((nslots + 64 * LANE_WAVES - 1) / (64 * LANE_WAVES), 4096);
+    const unsigned lw = (unsigned)std::min<size_t>((nslots + LANE_ACTIVE - 1) / LANE_ACTIVE, 16384);
     hipLaunchKernelGGL(k_splice_lanes, dim3(std::max(lw, 1u)), dim3(64 * LANE_WAVES), 0, hs, list, spf, units, lanes, st,
                        ld_fr, rbsp, rec);
     hipLaunchKernelGGL(k_splice_parse, gy, dim3(64), 0, hs, n, list, spf, units, st, ld_fr, rbsp, rec);

@@ -21,7 +21,7 @@ using dyn::OrSink;
 constexpr int DT = 256;                         /* threads per staging workgroup */
 constexpr int NW = DT / 64;
 constexpr int EPLIST_MAX = DYN_OVF_BYTES / 4;   /* EP positions kept per NAL (slot tail) */
-/* NALs with more EP bytes than this go to k_dyn_emit (SCROLL_DEBUG_DYN_EPCAP4
+/* NALs with more EP bytes than this go to emit_serial (SCROLL_DEBUG_DYN_EPCAP4
  * lowers it so the tests reach that path) */
 __device__ inline uint32_t ep_cap(const DynGeom &g)
 {

@@ -95,11 +95,21 @@ def main():
         print(f"k_dyn_epfix: {len(x)} WGs, span {(x[:, 5].max() - t0) / 100.0:.1f} us, WG duration mean "
               f"{((x[:, 5] - x[:, 0]) / 100.0).mean():.1f} us, candidate words mean {(x[:, 6] & 0xffffffff).mean():.1f}, "
               f"EP positions mean {(x[:, 6] >> 32).mean():.1f}")
-        prev = x[:, 0]
-        for k, nm in enumerate(["table+counts", "seams+cands", "sort", "compact+out"]):
-            d = (x[:, k + 1] - prev) / 100.0
-            print(f"  {nm:12s} mean {d.mean():7.2f} us  p99 {np.percentile(d, 99):7.2f}")
-            prev = x[:, k + 1]
+        # slots: 0 entry, 1 table+counts, 2 seams+cands (barrier), 3 sort, 4 wave 0's
+        # candidates, 5 end, 6 counts, 7 the seam wave's end
+        for nm, a, b_ in (("table+counts", 0, 1), ("seams+cands", 1, 2), ("  seam wave", 1, 7),
+                          ("  cand wave0", 1, 4), ("sort", 2, 3), ("compact+out", 3, 5)):
+            ok = x[:, b_] > 0
+            d = (x[ok, b_] - x[ok, a]) / 100.0
+            if len(d):
+                print(f"  {nm:12s} mean {d.mean():7.2f} us  p99 {np.percentile(d, 99):7.2f}")
+        nc = (x[:, 6] & 0xffffffff).astype(np.float64)
+        dur = (x[:, 5] - x[:, 0]) / 100.0
+        q = np.percentile(nc, [25, 50, 75])
+        for lo, hi in ((0, q[0]), (q[0], q[1]), (q[1], q[2]), (q[2], np.inf)):
+            m = (nc >= lo) & (nc < hi)
+            if m.any():
+                print(f"  candidates [{lo:.0f}, {hi:.0f}): {int(m.sum())} WGs, duration mean {dur[m].mean():.1f} us")
         conc = [int(np.sum((x[:, 0] <= v) & (x[:, 5] > v))) for v in np.linspace(t0, x[:, 5].max(), 12)]
         print("  resident WGs over time:", conc)
     e = allst[S * F:2 * S * F].astype(np.int64)  # k_dyn_gather: realtime (100 MHz)

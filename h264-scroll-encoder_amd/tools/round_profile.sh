@@ -28,6 +28,9 @@ if [ "$PART" = prof ] || [ "$PART" = all ]; then
     done
     $T 120 rocprofv3 --output-format csv --pmc FETCH_SIZE -d "$O/pmc_fetch" -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu --no-host > "$O/pmc_fetch.log" 2>&1
     $T 120 rocprofv3 --output-format csv --pmc WRITE_SIZE -d "$O/pmc_write" -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu --no-host > "$O/pmc_write.log" 2>&1
+    for c in FETCH_SIZE WRITE_SIZE; do          # the splice launches' traffic (tools/traffic.py)
+        $T 120 rocprofv3 --output-format csv --pmc $c -d "$O/pmc_splice_$c" -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu --no-verify --workload p720splicerows > "$O/pmc_splice_$c.log" 2>&1
+    done
     bash h264-scroll-encoder_amd/tools/sq_pass.sh "$O/sq"
     $T 120 python3 h264-scroll-encoder_amd/tools/dyn_stamps.py > "$O/dyn_stamps.txt" 2>&1
 fi

@@ -181,22 +181,24 @@ def test_experiment_mode(gpu, oracle):
 
 def test_errors_fail_only_their_stream(gpu, oracle, scroll):
     w, h = 256, 256
-    offs = synthetic_offsets(5, 6, h)
+    offs = synthetic_offsets(6, 6, h)
     c = _cfg(oracle, w, h)
     good = ext_slice(oracle, c, 4, 3, 1)
+    G = 5                                                   # the stream without an error
     cases = {
         0: (scroll.SCROLL_SPLICE_ERR_MBTYPE, ext_slice(oracle, c, 4, 3, 1, bad_mb=0, bad_type=5)),
-        1: (scroll.SCROLL_SPLICE_ERR_NAL, good[:4] + bytes([0x65]) + good[5:]),
+        1: (scroll.SCROLL_SPLICE_ERR_NAL, good[:4] + bytes([0x66]) + good[5:]),      # an SEI
         2: (scroll.SCROLL_SPLICE_ERR_SYNTAX, good[:len(good) // 2]),
         3: (scroll.SCROLL_SPLICE_ERR_REF, ext_slice(oracle, c, 4, 3, 2, nrefs=4, max_ref=3,
                                                     skip_pm=0)),
+        4: (scroll.SCROLL_SPLICE_ERR_HEADER, good[:4] + bytes([0x65]) + good[5:]),   # IDR, P slice
     }
-    b = gpu.Batch(5, 6, 8 << 20)
-    for _ in range(5):
+    b = gpu.Batch(6, 6, 8 << 20)
+    for _ in range(6):
         b.add_stream(gpu.make_config(w, h))
     for s, (_, nal) in cases.items():
         b.set_splice(s, 2, 2, 2, 4, 3, nal)
-    b.set_splice(4, 1, 2, 2, 4, 3, good)
+    b.set_splice(G, 1, 2, 2, 4, 3, good)
     b.set_offsets(offs)
     b.compose(6)
     assert b.sync() == scroll.SCROLL_ERR_CONFIG
@@ -210,10 +212,10 @@ def test_errors_fail_only_their_stream(gpu, oracle, scroll):
     o = bytearray()
     for t in range(6):
         sp = splice_of(2, 2, 4, 3, good) if t == 1 else None
-        k = oracle.or_compose_splice(buf, len(buf), ctypes.byref(c4), int(offs[4, t]), 0, None, 0,
+        k = oracle.or_compose_splice(buf, len(buf), ctypes.byref(c4), int(offs[G, t]), 0, None, 0,
                                      SPEC, ctypes.byref(sp) if sp else None, ctypes.byref(err))
         o += bytes(buf[:k])
-    assert b.output(4) == bytes(o)
+    assert b.output(G) == bytes(o)
     b.close()
 
 

@@ -683,9 +683,11 @@ constexpr int LANE_WAVES = 1;
 /* slices per wave: the lanes past it only build the tables.  The parse is a
  * chain of dependent loads per slice, and a frame batch has few slices per
  * SIMD (config-3 rows: 102,400 slices = 1.6 full waves per SIMD), so fewer
- * slices per wave put more waves on each SIMD to overlap their chains */
+ * slices per wave put more waves on each SIMD to overlap their chains
+ * (p720splicerows, rocprofv3: k_splice_lanes 4.40 / 4.08 / 4.34 ms at 64 /
+ * 32 / 16 slices per wave) */
 #ifndef SCROLL_SPLICE_LPW
-#define SCROLL_SPLICE_LPW 64
+#define SCROLL_SPLICE_LPW 32
 #endif
 constexpr int LANE_ACTIVE = SCROLL_SPLICE_LPW;
 static_assert(LANE_ACTIVE >= 1 && LANE_ACTIVE <= 64 && LANE_WAVES == 1, "k_splice_lanes: one wave, 1-64 slices");

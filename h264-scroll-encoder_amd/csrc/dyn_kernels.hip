@@ -3128,6 +3128,13 @@ __global__ __launch_bounds__(DT) void k_dyn_emit_gather(const DevStream *__restr
 #ifndef SCROLL_GATHER2_Z
 #define SCROLL_GATHER2_Z 1
 #endif
+/* 1: two chunk sets per thread in turn, the next chunk's loads in flight
+ * while one is assembled (0.142 against 0.146 ms per config-3 launch).
+ * Measured and not kept: non-temporal arena stores (0.143), non-temporal
+ * row-stage loads (0.153) */
+#ifndef SCROLL_GATHER_PIPE
+#define SCROLL_GATHER_PIPE 1
+#endif
 
 /* 128-bit helpers on four words, word 0 most significant */
 struct W4 {
@@ -3227,66 +3234,9 @@ __global__ __launch_bounds__(DT) __attribute__((amdgpu_waves_per_eu(8))) void k_
     const int32_t d0 = (int32_t)(o0 - (cfirst << 4)) + 5;
     const int32_t nebsp = (int32_t)(d.size - 5);
     int gg = 0;                                              /* the thread's group, carried */
-    for (uint32_t c = cbeg + (uint32_t)t; c < cend; c += DT) {
-        const int32_t u0 = 16 * (int32_t)c - d0;
+    /* the NAL edges and three-group chunks: byte by byte */
+    auto slow_chunk = [&](uint32_t c, uint32_t K) {
         uint8_t *q = A + ((cfirst + c) << 4);
-        uint32_t K = raw[u0 > 0 ? min(u0 >> cs, nblk - 1) : 0];
-        if (u0 >= 0 && u0 + 16 <= nebsp) {
-            while ((int32_t)(sp[K] + K) < u0) K++;               /* sentinel stops it */
-            const uint32_t i0 = (uint32_t)u0 - K, P = 8u * i0;
-            while (gg + 1 < ng && goff[gg + 1] <= P) ++gg;
-            while (gg > 0 && goff[gg] > P) --gg;                 /* never for increasing P */
-            const uint32_t lp = P - goff[gg], rem = gb[gg] - lp;  /* bits left in the group */
-            const bool two = rem < 128u;
-            if (!two || gg + 1 >= ng || gb[gg + 1] >= 128u - rem) {
-                /* 160 bits of the group from word lp >> 5 */
-                const uint32_t wo = 4u * (gw[gg] + (lp >> 5));
-                const auto xa = __builtin_amdgcn_raw_buffer_load_b128(rr, wo, 0, 0);
-                const uint32_t x4 = __builtin_amdgcn_raw_buffer_load_b32(rr, wo + 16u, 0, 0);
-                uint32_t yb[4] = {0u, 0u, 0u, 0u};
-                if (two && gg + 1 < ng) {
-                    const auto y = __builtin_amdgcn_raw_buffer_load_b128(rr, 4u * gw[gg + 1], 0, 0);
-                    yb[0] = (uint32_t)y[0]; yb[1] = (uint32_t)y[1]; yb[2] = (uint32_t)y[2]; yb[3] = (uint32_t)y[3];
-                }
-                const uint32_t x[5] = {(uint32_t)xa[0], (uint32_t)xa[1], (uint32_t)xa[2], (uint32_t)xa[3], x4};
-                const uint32_t sh = lp & 31u;
-                W4 R;
-#pragma unroll
-                for (int k = 0; k < 4; ++k) R.w[k] = sh ? __builtin_amdgcn_alignbit(x[k], x[k + 1], 32u - sh) : x[k];
-                if (two) {                                       /* rem bits of this group, then the next */
-                    const W4 B = shr128(W4{{yb[0], yb[1], yb[2], yb[3]}}, rem);
-#pragma unroll
-                    for (int k = 0; k < 4; ++k) {
-                        const uint32_t kb = 32u * (uint32_t)k;  /* bits of word k kept from this group */
-                        const uint32_t keep = rem <= kb ? 0u : (rem >= kb + 32u ? 32u : rem - kb);
-                        const uint32_t m = keep == 0u ? 0u : (keep == 32u ? 0xffffffffu : ~(0xffffffffu >> keep));
-                        R.w[k] = (R.w[k] & m) | B.w[k];
-                    }
-                }
-                /* the EP bytes inside the chunk: byte e becomes 03, the
-                 * bytes from e on move one byte later */
-                for (uint32_t m = K;; ++m) {
-                    const int32_t e = (int32_t)(sp[m] + m) - u0;
-                    if (e >= 16) break;
-                    const W4 S = shr128(R, 8u);
-                    const uint32_t eb = 8u * (uint32_t)e;
-#pragma unroll
-                    for (int k = 0; k < 4; ++k) {
-                        const uint32_t kb = 32u * (uint32_t)k;
-                        const uint32_t keep = eb <= kb ? 0u : (eb >= kb + 32u ? 32u : eb - kb);
-                        const uint32_t mk = keep == 0u ? 0u : (keep == 32u ? 0xffffffffu : ~(0xffffffffu >> keep));
-                        /* the 03 byte: bits [eb, eb + 8) */
-                        const uint32_t three = (eb >= kb && eb < kb + 32u) ? (3u << (24u - (eb - kb))) : 0u;
-                        const uint32_t mk2 = (eb >= kb && eb < kb + 32u) ? (0xff000000u >> (eb - kb)) : 0u;
-                        R.w[k] = (R.w[k] & mk) | (S.w[k] & ~mk & ~mk2) | three;
-                    }
-                }
-                *reinterpret_cast<uint4 *>(q) = make_uint4(__builtin_bswap32(R.w[0]), __builtin_bswap32(R.w[1]),
-                                                           __builtin_bswap32(R.w[2]), __builtin_bswap32(R.w[3]));
-                continue;
-            }
-        }
-        /* NAL edges and three-group chunks: byte by byte */
         for (int b = 0; b < 16; ++b) {
             const uint64_t qa = ((cfirst + c) << 4) + (uint64_t)b;
             if (qa < o0 || qa >= o1) continue;
@@ -3306,7 +3256,142 @@ __global__ __launch_bounds__(DT) __attribute__((amdgpu_waves_per_eu(8))) void k_
             }
             q[b] = v;
         }
+    };
+    /* chunk c's 128 RBSP bits from its loads (x: 160 bits of the group from
+     * word lp >> 5, y: the next group's first 128 when the chunk runs past
+     * rem bits), the EP bytes inside it, stored */
+    auto fast_chunk = [&](uint32_t c, int32_t u0, uint32_t K, uint32_t lp, uint32_t rem, bool two, const uint32_t x[5],
+                          const uint32_t yb[4]) {
+        const uint32_t sh = lp & 31u;
+        W4 R;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) R.w[k] = sh ? __builtin_amdgcn_alignbit(x[k], x[k + 1], 32u - sh) : x[k];
+        if (two) {                                           /* rem bits of this group, then the next */
+            const W4 B = shr128(W4{{yb[0], yb[1], yb[2], yb[3]}}, rem);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint32_t kb = 32u * (uint32_t)k;      /* bits of word k kept from this group */
+                const uint32_t keep = rem <= kb ? 0u : (rem >= kb + 32u ? 32u : rem - kb);
+                const uint32_t m = keep == 0u ? 0u : (keep == 32u ? 0xffffffffu : ~(0xffffffffu >> keep));
+                R.w[k] = (R.w[k] & m) | B.w[k];
+            }
+        }
+        /* the EP bytes inside the chunk: byte e becomes 03, the bytes from
+         * e on move one byte later */
+        for (uint32_t m = K;; ++m) {
+            const int32_t e = (int32_t)(sp[m] + m) - u0;
+            if (e >= 16) break;
+            const W4 S = shr128(R, 8u);
+            const uint32_t eb = 8u * (uint32_t)e;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint32_t kb = 32u * (uint32_t)k;
+                const uint32_t keep = eb <= kb ? 0u : (eb >= kb + 32u ? 32u : eb - kb);
+                const uint32_t mk = keep == 0u ? 0u : (keep == 32u ? 0xffffffffu : ~(0xffffffffu >> keep));
+                /* the 03 byte: bits [eb, eb + 8) */
+                const uint32_t three = (eb >= kb && eb < kb + 32u) ? (3u << (24u - (eb - kb))) : 0u;
+                const uint32_t mk2 = (eb >= kb && eb < kb + 32u) ? (0xff000000u >> (eb - kb)) : 0u;
+                R.w[k] = (R.w[k] & mk) | (S.w[k] & ~mk & ~mk2) | three;
+            }
+        }
+        *reinterpret_cast<uint4 *>(A + ((cfirst + c) << 4)) =
+            make_uint4(__builtin_bswap32(R.w[0]), __builtin_bswap32(R.w[1]), __builtin_bswap32(R.w[2]),
+                       __builtin_bswap32(R.w[3]));
+    };
+#if SCROLL_GATHER_PIPE
+    /* two chunk sets in turn (no register copies between them): chunk c +
+     * DT's search and loads go out before chunk c is assembled and stored.
+     * Every chunk loads (the edge / past-the-end ones at word 0, unused), so
+     * the number of loads in flight is fixed and the waits count them */
+    struct GSet {
+        uint32_t c, K, lp, rem;
+        int32_t u0;
+        bool fast, two, yv;                                  /* yv: y holds the next group's words */
+        uint32_t x[5], y[4];
+    };
+    auto prep = [&](uint32_t c, GSet &S) {
+        const int32_t u0 = 16 * (int32_t)c - d0;
+        uint32_t K = raw[u0 > 0 ? min(u0 >> cs, nblk - 1) : 0];
+        uint32_t wo = 0u, yo = 0u;
+        S.c = c;
+        S.u0 = u0;
+        S.fast = false;
+        S.two = false;
+        S.yv = false;
+        S.lp = S.rem = 0u;
+        if (c < cend && u0 >= 0 && u0 + 16 <= nebsp) {
+            while ((int32_t)(sp[K] + K) < u0) K++;           /* sentinel stops it */
+            const uint32_t i0 = (uint32_t)u0 - K, P = 8u * i0;
+            while (gg + 1 < ng && goff[gg + 1] <= P) ++gg;
+            const uint32_t lp = P - goff[gg], rem = gb[gg] - lp;
+            const bool two = rem < 128u;
+            if (!two || gg + 1 >= ng || gb[gg + 1] >= 128u - rem) {
+                S.fast = true;
+                S.two = two;
+                S.lp = lp;
+                S.rem = rem;
+                S.yv = two && gg + 1 < ng;
+                wo = 4u * (gw[gg] + (lp >> 5));
+                yo = S.yv ? 4u * gw[gg + 1] : wo;
+            }
+        }
+        S.K = K;
+        const auto xa = __builtin_amdgcn_raw_buffer_load_b128(rr, wo, 0, 0);
+        const uint32_t x4 = __builtin_amdgcn_raw_buffer_load_b32(rr, wo + 16u, 0, 0);
+        const auto y = __builtin_amdgcn_raw_buffer_load_b128(rr, yo, 0, 0);
+        S.x[0] = (uint32_t)xa[0]; S.x[1] = (uint32_t)xa[1]; S.x[2] = (uint32_t)xa[2]; S.x[3] = (uint32_t)xa[3];
+        S.x[4] = x4;
+        S.y[0] = (uint32_t)y[0]; S.y[1] = (uint32_t)y[1]; S.y[2] = (uint32_t)y[2]; S.y[3] = (uint32_t)y[3];
+    };
+    auto finish = [&](GSet &S) {
+        if (S.fast) {
+            const uint32_t yb[4] = {S.yv ? S.y[0] : 0u, S.yv ? S.y[1] : 0u, S.yv ? S.y[2] : 0u, S.yv ? S.y[3] : 0u};
+            fast_chunk(S.c, S.u0, S.K, S.lp, S.rem, S.two, S.x, yb);
+        } else {
+            slow_chunk(S.c, S.K);
+        }
+    };
+    GSet sa, sb;
+    uint32_t c = cbeg + (uint32_t)t;
+    if (c < cend) prep(c, sa);
+    while (c < cend) {
+        prep(c + DT, sb);
+        finish(sa);
+        c += DT;
+        if (c >= cend) break;
+        prep(c + DT, sa);
+        finish(sb);
+        c += DT;
     }
+#else
+    for (uint32_t c = cbeg + (uint32_t)t; c < cend; c += DT) {
+        const int32_t u0 = 16 * (int32_t)c - d0;
+        uint32_t K = raw[u0 > 0 ? min(u0 >> cs, nblk - 1) : 0];
+        if (u0 >= 0 && u0 + 16 <= nebsp) {
+            while ((int32_t)(sp[K] + K) < u0) K++;               /* sentinel stops it */
+            const uint32_t i0 = (uint32_t)u0 - K, P = 8u * i0;
+            while (gg + 1 < ng && goff[gg + 1] <= P) ++gg;
+            while (gg > 0 && goff[gg] > P) --gg;                 /* never for increasing P */
+            const uint32_t lp = P - goff[gg], rem = gb[gg] - lp;  /* bits left in the group */
+            const bool two = rem < 128u;
+            if (!two || gg + 1 >= ng || gb[gg + 1] >= 128u - rem) {
+                /* 160 bits of the group from word lp >> 5 */
+                const uint32_t wo = 4u * (gw[gg] + (lp >> 5));
+                const auto xa = __builtin_amdgcn_raw_buffer_load_b128(rr, wo, 0, 0);
+                const uint32_t x4 = __builtin_amdgcn_raw_buffer_load_b32(rr, wo + 16u, 0, 0);
+                uint32_t yb[4] = {0u, 0u, 0u, 0u};
+                if (two && gg + 1 < ng) {
+                    const auto y = __builtin_amdgcn_raw_buffer_load_b128(rr, 4u * gw[gg + 1], 0, 0);
+                    yb[0] = (uint32_t)y[0]; yb[1] = (uint32_t)y[1]; yb[2] = (uint32_t)y[2]; yb[3] = (uint32_t)y[3];
+                }
+                const uint32_t x[5] = {(uint32_t)xa[0], (uint32_t)xa[1], (uint32_t)xa[2], (uint32_t)xa[3], x4};
+                fast_chunk(c, u0, K, lp, rem, two, x, yb);
+                continue;
+            }
+        }
+        slow_chunk(c, K);
+    }
+#endif
     if (stamps) {                                            /* uniform */
         __syncthreads();
         if (stp) stp[2] = __builtin_amdgcn_s_memrealtime();

@@ -1233,13 +1233,16 @@ static_assert(2 * SORT_KEYS <= 32 && 32 + LVT_N <= ROW_GB, "the sort counts and 
 static_assert(ROW_PAD == 4, "RowFixed::buf holds ROW_PAD spare words");
 static_assert(offsetof(RowFixed, lvt) % 8 == 0, "the level table is copied in 8-byte words");
 
-/* dynamic LDS of k_dyn_row: lv [NPC w] uint4 (levels, then bodies), mbits
- * [w] u32, moff [mbw + 1] u32, mt / lo / off16 [NPC w] u16 (the sort's
- * order [24 w] u16 lives in off16 until phase 4), ta [8 w] u8 (top TotalCoeffs), cbp / code [w] u8 */
-__host__ __device__ inline size_t row_lds_bytes(int w, int mbw)
+/* dynamic LDS of k_dyn_row: lv [NPC w] uint4 (levels, then bodies), moff
+ * [w + 1] u32 (the rect columns' bit offsets in the row; the static
+ * columns' are closed forms of their three head classes), mt / lo / off16
+ * [NPC w] u16 (the sort's order [24 w] u16 lives in off16 until phase 4), ta
+ * [8 w] u8 (top TotalCoeffs; from phase 4 on the MBs' bit counts, u32 [w]),
+ * cbp / code [w] u8.  (Round 4 kept moff for every column of the picture:
+ * 964 bytes more at 4K, config 5's row workgroups needed 33.5 KB) */
+__host__ __device__ inline size_t row_lds_bytes(int w)
 {
-    return (size_t)16 * NPC * w + (size_t)4 * (w + mbw + 1) + (size_t)2 * (3 * NPC * w) +
-           (size_t)10 * w + 16;
+    return (size_t)16 * NPC * w + (size_t)4 * (w + 1) + (size_t)2 * (3 * NPC * w) + (size_t)10 * w + 16;
 }
 
 /* The nC neighbours of piece class pc (0-15 luma raster, 16 / 17 chroma DC,
@@ -1483,10 +1486,11 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
     if (df.nal < 0 || ((df.err & DF_GENERAL) != 0) != GEN) return;
 
     uint4 *lv = rdyn;
-    uint32_t *mbits = reinterpret_cast<uint32_t *>(lv + npc), *moff = mbits + w;
-    uint16_t *mt = reinterpret_cast<uint16_t *>(moff + mbw + 1), *lo = mt + npc, *off16 = lo + npc;
+    uint32_t *moff = reinterpret_cast<uint32_t *>(lv + npc);
+    uint16_t *mt = reinterpret_cast<uint16_t *>(moff + w + 1), *lo = mt + npc, *off16 = lo + npc;
     uint16_t *order = off16;                          /* CAVLC phase only; off16 is phase 4's */
     uint8_t *ta = reinterpret_cast<uint8_t *>(off16 + npc), *cbpa = ta + 8 * w, *codea = cbpa + w;
+    uint32_t *mbits = reinterpret_cast<uint32_t *>(ta);   /* phase 4 on: ta is dead after phase 3 */
 
     if (t < 8) {
         L.wo[t] = pend[s].wo[t];
@@ -1831,30 +1835,37 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
         cbpa[k] = (uint8_t)cbp;
         codea[k] = (uint8_t)code;
     }
+    /* the bit offset of column col in the row: a static column's head (+ its
+     * coded_block_pattern '1') is the row's first / middle / last class, so
+     * the static columns before the rect and after it are closed forms; the
+     * rect's columns come from the scan below (moff) */
+    const int x1 = R.x0 + w;
+    const uint32_t h0 = head_bits(row, 0) + 1u;
+    const uint32_t h1 = mbw >= 3 ? head_bits(row, 1) + 1u : 0u;
+    const uint32_t h2 = mbw >= 2 ? head_bits(row, mbw - 1) + 1u : 0u;
+    auto colpos = [&](int col) -> uint32_t {
+        if (col <= R.x0) return col == 0 ? 0u : h0 + (uint32_t)(col - 1) * h1;
+        if (col < x1) return moff[col - R.x0];
+        return moff[w] + (uint32_t)(col - x1) * h1 + (col == mbw && x1 <= mbw - 1 ? h2 - h1 : 0u);
+    };
     __syncthreads();
     const int gi = nA + r;
     if (wave == 0) {
-        uint32_t carry = 0;
-        for (int c0 = 0; c0 < mbw; c0 += 64) {
-            const int col = c0 + lane;
-            uint32_t len = 0;
-            if (col < mbw) {
-                const int k = col - R.x0;
-                len = (k >= 0 && k < w) ? mbits[k] : head_bits(row, col) + 1u;
-            }
+        uint32_t carry = R.x0 == 0 ? 0u : h0 + (uint32_t)(R.x0 - 1) * h1;
+        for (int k0 = 0; k0 < w; k0 += 64) {
+            const int k = k0 + lane;
+            const uint32_t len = k < w ? mbits[k] : 0u;
             const uint32_t incl = wave_incl_sum(len, lane);
-            if (col < mbw) moff[col] = carry + incl - len;
+            if (k < w) moff[k] = carry + incl - len;
             carry += __shfl(incl, 63, 64);
         }
-        if (lane == 0) {
-            moff[mbw] = carry;
-            gbits[nb * (size_t)ng + gi] = carry;
-        }
+        if (lane == 0) moff[w] = carry;
     }
     __syncthreads();
     if (stamps) stv[4] = __builtin_amdgcn_s_memrealtime();
     ROW_CUT(4);
-    const uint32_t bits = moff[mbw];
+    const uint32_t bits = colpos(mbw);
+    if (t == 0) gbits[nb * (size_t)ng + gi] = bits;
 
     /* ---- 5: bits -> the row's own row-stage words ------------------------ */
     uint32_t *out = rowstage + nb * g.rs_frame_words + rs_group_words(g, nA, gi);
@@ -1892,8 +1903,8 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
          * in, written as one piece */
         const bool one = npass == 1;
         for (int col = t; col < mbw; col += T) {
-            const uint32_t pos = moff[col];
-            if (!one && (pos >= 32u * (p0 + n) || moff[col + 1] <= 32u * p0)) continue;
+            const uint32_t pos = colpos(col);
+            if (!one && (pos >= 32u * (p0 + n) || colpos(col + 1) <= 32u * p0)) continue;
             const int k = col - R.x0;
             const bool in = k >= 0 && k < w;
             if (one && !head_over) {
@@ -1943,7 +1954,7 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
             if (o == 0xffffu) continue;
             const int k = div_npc(i), pc = i - k * NPC;
             const uint32_t e = lo[i], mv = mt[i];
-            const uint32_t pos = moff[R.x0 + k] + o;
+            const uint32_t pos = moff[k] + o;
             if (!one && (pos >= 32u * (p0 + n) || pos + (e & LO_LEN) <= 32u * p0)) continue;
             const int nC = (int)(e >> 11) - 1;
             const uint4 bd = lv[i];
@@ -3470,10 +3481,10 @@ int dyn_launch_code(hipStream_t hs, int nframes, int S, DevStream *st, const Nal
                        pend, nal, ld_nal, *g, x->rows, src, refs, x->meta, x->body_lo, x->body_hi, x->body_w,
                        x->ctr);
     if (hipGetLastError() != hipSuccess) return -1;
-    if (row_lds_bytes(g->w, mbw) > 65536) {
+    if (row_lds_bytes(g->w) > 65536) {
         /* wide rects (a whole 1280- or 4096-px row): dynamic LDS past the
          * 64 KB default, up to the CU's 160 KB (set_dyn_rect's bound) */
-        const int rl = (int)row_lds_bytes(g->w, mbw);
+        const int rl = (int)row_lds_bytes(g->w);
         if (hipFuncSetAttribute(reinterpret_cast<const void *>(&k_dyn_row<false>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, rl) != hipSuccess ||
             hipFuncSetAttribute(reinterpret_cast<const void *>(&k_dyn_row<true>),
@@ -3481,14 +3492,14 @@ int dyn_launch_code(hipStream_t hs, int nframes, int S, DevStream *st, const Nal
             return -1;
     }
     hipLaunchKernelGGL(k_dyn_row<false>, dim3(g->h, nframes, S), dim3(row_threads(g->w)),
-                       row_lds_bytes(g->w, mbw), hs, st, nal, ld_nal, pend, dfr, ld_fr, *g, x->rows, src, refs,
+                       row_lds_bytes(g->w), hs, st, nal, ld_nal, pend, dfr, ld_fr, *g, x->rows, src, refs,
                        x->meta, x->body_lo, x->body_hi, x->body_w, x->tcx, epoch, x->rowstage, x->gbits, x->spill,
                        x->ctr, x->heads, stamps);
     if (hipGetLastError() != hipSuccess) return -1;
     /* the general path: one row workgroup per record slot that may be taken */
     hipLaunchKernelGGL(k_dyn_row<true>, dim3(g->h, std::min<uint32_t>(g->gen_cap, (uint32_t)(nframes * S)), 1),
                        dim3(row_threads(g->w)),
-                       row_lds_bytes(g->w, mbw), hs, st, nal, ld_nal, pend, dfr, ld_fr, *g, x->rows, src, refs,
+                       row_lds_bytes(g->w), hs, st, nal, ld_nal, pend, dfr, ld_fr, *g, x->rows, src, refs,
                        x->meta, x->body_lo, x->body_hi, x->body_w, x->tcx, epoch, x->rowstage, x->gbits, x->spill,
                        x->ctr, x->heads, stamps);
     return hipGetLastError() == hipSuccess ? 0 : -1;
@@ -3581,4 +3592,19 @@ size_t dyn_slot_bound(int mbw, int mbh, int rw, int rh)
     const size_t bits = (size_t)HDR_MAX + (size_t)mbw * mbh * (HEAD_MAX + 1) +
                         (size_t)rw * rh * MB_BITS_MAX + 64;
     return ((bits / 8 + 32 + DYN_OVF_BYTES) + 255) & ~(size_t)255;
+}
+
+/* profiling aid (tools/row_occupancy.py): resident k_dyn_row<false>
+ * workgroups per CU for a w-MB rect row in an mbw-MB picture, with extra
+ * bytes of dynamic LDS added (negative: removed) -- the HIP occupancy
+ * calculator's answer for this very kernel (registers, static LDS) */
+extern "C" int scroll_debug_row_occupancy(int w, int mbw, int extra_lds)
+{
+    int n = -1;
+    (void)mbw;                              /* (round 4's LDS grew with the picture width) */
+    const size_t lds = (size_t)((long)row_lds_bytes(w) + extra_lds);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, reinterpret_cast<const void *>(&k_dyn_row<false>),
+                                                     row_threads(w), lds) != hipSuccess)
+        return -1;
+    return n;
 }

@@ -1926,6 +1926,7 @@ struct SpliceLds {
     uint8_t cbpc[48];                       /* inter coded_block_pattern -> codeNum */
     uint32_t ep_n;
     int32_t bad;
+    uint32_t carry;                         /* the partial word at the bit position (MSB first) */
 };
 static_assert(offsetof(SpliceMbRec, blen) == SPLICE_REC_HEAD && sizeof(SpliceMbRec) == 352,
               "the stage copies a record's first SPLICE_REC_HEAD bytes in 16-byte loads");
@@ -2097,6 +2098,7 @@ __global__ __launch_bounds__(DT) __attribute__((amdgpu_waves_per_eu(SCROLL_STAGE
     if (t == 0) {
         L.ep_n = 0;
         L.bad = 0;
+        L.carry = 0u;
     }
     if (t < 8) {
         L.wo[t] = pend[s].wo[t];
@@ -2140,268 +2142,263 @@ __global__ __launch_bounds__(DT) __attribute__((amdgpu_waves_per_eu(SCROLL_STAGE
     uint32_t *eplist = reinterpret_cast<uint32_t *>(slot + slot_bytes - DYN_OVF_BYTES);
 
     bool my_bad = false, my_ref_bad = false;
-    uint32_t total = 0;            /* bits: header + MBs (uniform) */
-    int last_end = -1;
-    /* sweep 0 counts, sweep 1 writes at the counted offsets */
-    for (int sweep = 0; sweep < 2; ++sweep) {
-        uint32_t pos = F0;
-        int last = -1;             /* last coded MB before the window (uniform) */
-        if (sweep == 1 && t == 0) {
-            GSink hs{{out}, 0, 0, 0};
-            hs.start(0);
-            emit_slice_header(hs, c);
-            hs.finish();
-        }
-        for (int m0 = 0; m0 < nmb; m0 += DT) {
-            /* the previous window's writing sweep still reads the ring (the
-             * neighbour blocks of its partitioned MBs): wait before refilling */
-            lds_barrier();
-            const int m = m0 + t;
-            int x = 0, y = 0, k = -1;
-            Mv me{0, 0, 0};
-            bool parted = false;
-            SpliceMbRec hd;                                        /* a spliced MB's record head */
-            uint4 et = make_uint4(0u, 0u, 0u, 0u);
-            if (m < nmb) {
-                y = (int)div_m((uint32_t)m, m_mbw);
-                x = m - y * mbw;
-                if (x >= SF.x0 && x < SF.x0 + SF.w && y >= SF.y0 && y < SF.y0 + SF.h) {
-                    k = (y - SF.y0) * SF.w + (x - SF.x0);
-                    const uint4 *hp = reinterpret_cast<const uint4 *>(rec + k);
-                    uint4 hv[SPLICE_REC_HEAD / 16];
+    /* one sweep (round 5; round 4 counted the whole picture first, then
+     * coded it again to write): each window's bits go out as soon as they
+     * are placed, the word they share with the previous window carried in
+     * LDS (L.carry), so no word is written twice concurrently and the slot
+     * needs no zeroing; the slot's capacity is checked per window before
+     * any store, and a frame that fails (capacity, hint, reference) has
+     * written only inside its own slot and commits nothing */
+    uint32_t pos = F0;             /* bits: header + MBs so far (uniform) */
+    int last = -1;                 /* last coded MB before the window (uniform) */
+    bool over = false;
+    for (int m0 = 0; m0 < nmb; m0 += DT) {
+        /* the previous window's writing sweep still reads the ring (the
+         * neighbour blocks of its partitioned MBs): wait before refilling */
+        lds_barrier();
+        const int m = m0 + t;
+        int x = 0, y = 0, k = -1;
+        Mv me{0, 0, 0};
+        bool parted = false;
+        SpliceMbRec hd;                                        /* a spliced MB's record head */
+        uint4 et = make_uint4(0u, 0u, 0u, 0u);
+        if (m < nmb) {
+            y = (int)div_m((uint32_t)m, m_mbw);
+            x = m - y * mbw;
+            if (x >= SF.x0 && x < SF.x0 + SF.w && y >= SF.y0 && y < SF.y0 + SF.h) {
+                k = (y - SF.y0) * SF.w + (x - SF.x0);
+                const uint4 *hp = reinterpret_cast<const uint4 *>(rec + k);
+                uint4 hv[SPLICE_REC_HEAD / 16];
 #pragma unroll
-                    for (int q = 0; q < SPLICE_REC_HEAD / 16; ++q) hv[q] = hp[q];
-                    __builtin_memcpy(&hd, hv, SPLICE_REC_HEAD);
-                    if (SF.hd_qp >= 0)                             /* the dynamic rect under hints: its QP chain */
-                        hd.qpd = (int8_t)((uint32_t)k == SF.hd_first ? SF.hd_qp - 26 : 0);
-                    et = edge_tc(hd);
-                    const SpliceMbRec &mb = hd;
-                    me = Mv{mb.ref, mb.mx, mb.my};
-                    parted = mb.part != 0;
-                    auto valid = [&](int rf) {
-                        const int wk = rf - 2;
-                        return rf == 0 || rf == 1 || (wk >= 0 && wk < c.nwp && L.wv[wk]);
-                    };
-                    my_ref_bad |= !mb.intra && !valid(mb.ref);
-                    if (parted)
-                        for (int q = 1; q < 16; ++q) my_ref_bad |= !valid(rec[k].bref[q]);   /* past the head */
-                } else {
-                    bool bad;
-                    me = field(L.rc, L.wv, nr, x, y, lay, c.nwp, bad);
-                    my_bad |= bad;
-                }
-                L.fr[m & (RING - 1)] = me.ref;
-                L.fx[m & (RING - 1)] = me.mx;
-                L.fy[m & (RING - 1)] = me.my;
-                L.fk[m & (RING - 1)] = parted ? k : -1;
-                L.etc[m & (RING - 1)] = et;
+                for (int q = 0; q < SPLICE_REC_HEAD / 16; ++q) hv[q] = hp[q];
+                __builtin_memcpy(&hd, hv, SPLICE_REC_HEAD);
+                if (SF.hd_qp >= 0)                             /* the dynamic rect under hints: its QP chain */
+                    hd.qpd = (int8_t)((uint32_t)k == SF.hd_first ? SF.hd_qp - 26 : 0);
+                et = edge_tc(hd);
+                const SpliceMbRec &mb = hd;
+                me = Mv{mb.ref, mb.mx, mb.my};
+                parted = mb.part != 0;
+                auto valid = [&](int rf) {
+                    const int wk = rf - 2;
+                    return rf == 0 || rf == 1 || (wk >= 0 && wk < c.nwp && L.wv[wk]);
+                };
+                my_ref_bad |= !mb.intra && !valid(mb.ref);
+                if (parted)
+                    for (int q = 1; q < 16; ++q) my_ref_bad |= !valid(rec[k].bref[q]);   /* past the head */
+            } else {
+                bool bad;
+                me = field(L.rc, L.wv, nr, x, y, lay, c.nwp, bad);
+                my_bad |= bad;
             }
-            __syncthreads();
-            bool coded = false;
-            int px = 0, py = 0;
-            const Mv none{-1, 0, 0};
-            /* 4x4 block (bx, by) of MB q (partitioned spliced MBs from their record) */
-            auto blk = [&](int q, int bx, int by) {
-                const int kk = L.fk[q & (RING - 1)];
-                if (kk >= 0) return unpk_mv(rec[kk].bref[4 * by + bx], rec[kk].bmv[4 * by + bx]);
-                return Mv{L.fr[q & (RING - 1)], L.fx[q & (RING - 1)], L.fy[q & (RING - 1)]};
-            };
-            if (m < nmb && !parted) {
-                const Mv A = x > 0 ? blk(m - 1, 3, 0) : none;
-                const Mv B = y > 0 ? blk(m - mbw, 0, 3) : none;
-                const Mv C = y == 0 ? none
-                                    : (x + 1 < mbw ? blk(m - mbw + 1, 0, 3) : (x > 0 ? blk(m - mbw - 1, 3, 3) : none));
-                if (spec) {
-                    int sx, sy;
-                    pskip_mv(x > 0, y > 0, A, B, C, sx, sy);
-                    coded = !pskip ||
-                            !(me.ref == 0 && me.mx == sx && me.my == sy && (k < 0 || hd.cbp == 0));
-                    predict_spec(A, B, C, me.ref, px, py);
-                } else {
-                    coded = true;
-                    predict_ref(A, B, C, me.ref, px, py);
-                }
-            }
-            coded |= m < nmb && parted;                            /* predicted per partition */
-            int excl, cmax;
-            block_excl_max(coded ? m : -1, L.wmax, excl, cmax);
-            /* the MB's bits: head, then (spliced) cbp / qp / pieces */
-            /* the left / top MBs' edge TotalCoeffs (0 outside the rect) */
-            const uint4 el = x > 0 ? L.etc[(m - 1) & (RING - 1)] : make_uint4(0u, 0u, 0u, 0u);
-            const uint4 eu = y > 0 ? L.etc[(m - mbw) & (RING - 1)] : make_uint4(0u, 0u, 0u, 0u);
-            /* a partitioned spliced MB's neighbour block (cx, cy) (6.4.11.7) */
-            auto pnb = [&](int cx, int cy, uint32_t dn) {
-                if (cy >= 0) {
-                    if (cx >= 4) return none;
-                    if (cx >= 0)
-                        return (dn >> (4 * cy + cx)) & 1u ? unpk_mv(rec[k].bref[4 * cy + cx], rec[k].bmv[4 * cy + cx])
-                                                          : none;
-                    return x > 0 ? blk(m - 1, 3, cy) : none;
-                }
-                if (y == 0) return none;
-                if (cx < 0) return x > 0 ? blk(m - mbw - 1, 3, 3) : none;
-                if (cx < 4) return blk(m - mbw, cx, 3);
-                return x + 1 < mbw ? blk(m - mbw + 1, 0, 3) : none;
-            };
-            const bool intra = k >= 0 && hd.intra;
-            uint32_t pcm_pad = 0;
-            auto code_mb = [&](auto &sk) {
-                put_ue(sk, (uint32_t)(m - max(excl, last) - 1));  /* mb_skip_run */
-                if (intra) {
-                    put_ue(sk, hd.mbt);                            /* verbatim, like its prediction syntax */
-                    splice_tail(sk, hd, rec + k, el, eu, x > 0, y > 0, L, rb, pcm_pad);
-                    return;
-                }
-                if (parted) {
-                    const SpliceMbRec &mb = rec[k];
-                    const int part = mb.part;
-                    const uint32_t sub = mb.sub;
-                    put_ue(sk, (uint32_t)part);                    /* P_L0_L0_16x8 / 8x16, P_8x8 */
-                    if (part == 3)
-                        for (int i = 0; i < 4; ++i) put_ue(sk, (sub >> (2 * i)) & 3u);
-                    for (int i = 0; i < (part == 3 ? 4 : 2); ++i) {  /* ref_idx per mbPartIdx */
-                        const int q = part == 1 ? 8 * i : (part == 2 ? 2 * i : 2 * (i & 1) + 8 * (i >> 1));
-                        const int rf = mb.bref[q];
-                        if (nrefs == 2) sk.put((uint32_t)(1 - (rf & 1)), 1);
-                        else put_ue(sk, (uint32_t)rf);
-                    }
-                    uint32_t dn = 0;
-                    for_parts(part, sub, [&](int bx, int by, int bw, int bh, int mp) {
-                        const int q = 4 * by + bx;
-                        const Mv v = unpk_mv(mb.bref[q], mb.bmv[q]);
-                        int qx, qy;
-                        predict_part(part, mp, bx, by, bw, v.ref, [&](int cx, int cy) { return pnb(cx, cy, dn); },
-                                     qx, qy);
-                        put_se(sk, v.mx - qx);
-                        put_se(sk, v.my - qy);
-                        dn |= part_mask(bx, by, bw, bh);
-                    });
-                } else {
-                    sk.put(1, 1);                                  /* P_L0_16x16 */
-                    if (nrefs == 2) sk.put((uint32_t)(1 - (me.ref & 1)), 1);
-                    else if (nrefs > 2) put_ue(sk, (uint32_t)me.ref);
-                    put_se(sk, me.mx - px);
-                    put_se(sk, me.my - py);
-                }
-                if (k >= 0) splice_tail(sk, hd, rec + k, el, eu, x > 0, y > 0, L, rb, 0u);
-                else sk.put(1, 1);                                 /* coded_block_pattern 0 */
-            };
-            CountSink cs{0};
-            if (coded) code_mb(cs);
-            /* I_PCM: pcm_alignment_zero_bits for its composed position.  Sizes
-             * without them, scanned: the n-th I_PCM of the window starts its
-             * samples at key_n + (pads before it) mod 8 with key_n = its
-             * unpadded position mod 8, so pad_n = key_(n-1) - key_n mod 8
-             * (key_0 = 0) */
-            const bool pcm = coded && intra && hd.intra == 3;
-            if (__syncthreads_or(pcm)) {
-                uint32_t o0, t0;
-                block_excl_sum(cs.n, L.wsum, o0, t0);
-                CountSink hc{0};
-                put_ue(hc, (uint32_t)(m - max(excl, last) - 1));
-                put_ue(hc, 30u);
-                const int lane = t & 63, wv = t >> 6;
-                const uint64_t bl = __ballot(pcm);
-                if (lane == 0) L.pcm_mask[wv] = bl;
-                L.pcm_key[t] = (uint8_t)((pos + o0 + hc.n) & 7u);
-                __syncthreads();
-                if (pcm) {
-                    int prev = -1;
-                    const uint64_t below = bl & ((1ull << lane) - 1ull);
-                    if (below) {
-                        prev = 64 * wv + 63 - __builtin_clzll(below);
-                    } else {
-                        for (int w2 = wv - 1; w2 >= 0 && prev < 0; --w2)
-                            if (L.pcm_mask[w2]) prev = 64 * w2 + 63 - __builtin_clzll(L.pcm_mask[w2]);
-                    }
-                    const uint32_t kp = prev >= 0 ? L.pcm_key[prev] : 0u;
-                    pcm_pad = (kp - L.pcm_key[t]) & 7u;
-                    cs.n += pcm_pad;
-                }
-                __syncthreads();
-            }
-            uint32_t off, T;
-            block_excl_sum(cs.n, L.wsum, off, T);
-            if (sweep == 1) {
-                /* the window's bits through an LDS word window (passes of
-                 * SPL_WB words), then out with plain stores -- global
-                 * atomics per word would each hold the lane's next loads
-                 * (one in-order vector-memory counter); only the window's
-                 * first and last words, shared with its neighbours, are ORed */
-                const uint32_t wlo = pos >> 5, whi = (pos + T + 31u) >> 5;
-                for (uint32_t b0 = wlo; b0 < whi; b0 += SPL_WB) {
-                    const uint32_t n = min((uint32_t)SPL_WB, whi - b0);
-                    for (uint32_t i = (uint32_t)t; i < n; i += DT) L.wbuf[i] = 0u;
-                    __syncthreads();
-                    const uint32_t a0 = pos + off;
-                    if (coded && a0 < 32u * (b0 + n) && a0 + cs.n > 32u * b0) {
-                        OrSink<LdsWin> sk{LdsWin{L.wbuf, b0, n}, 0, 0, 0};
-                        sk.start(a0);
-                        code_mb(sk);
-                        sk.finish();
-                    }
-                    __syncthreads();
-                    for (uint32_t i = (uint32_t)t; i < n; i += DT) {
-                        const uint32_t v = L.wbuf[i], gi = b0 + i;
-                        if (gi == wlo || gi + 1 == whi) {
-                            if (v) atomicOr(&out[gi], __builtin_bswap32(v));
-                        } else {
-                            out[gi] = __builtin_bswap32(v);
-                        }
-                    }
-                    __syncthreads();
-                }
-            }
-            pos += T;
-            last = max(last, cmax);
+            L.fr[m & (RING - 1)] = me.ref;
+            L.fx[m & (RING - 1)] = me.mx;
+            L.fy[m & (RING - 1)] = me.my;
+            L.fk[m & (RING - 1)] = parted ? k : -1;
+            L.etc[m & (RING - 1)] = et;
         }
-        if (sweep == 0) {
-            /* trailing skipped MBs, rbsp_stop_one_bit, alignment */
-            uint32_t nb = pos + 1u;
-            if (last < nmb - 1) {
-                CountSink cc{0};
-                put_ue(cc, (uint32_t)(nmb - 1 - last));
-                nb += cc.n;
+        __syncthreads();
+        bool coded = false;
+        int px = 0, py = 0;
+        const Mv none{-1, 0, 0};
+        /* 4x4 block (bx, by) of MB q (partitioned spliced MBs from their record) */
+        auto blk = [&](int q, int bx, int by) {
+            const int kk = L.fk[q & (RING - 1)];
+            if (kk >= 0) return unpk_mv(rec[kk].bref[4 * by + bx], rec[kk].bmv[4 * by + bx]);
+            return Mv{L.fr[q & (RING - 1)], L.fx[q & (RING - 1)], L.fy[q & (RING - 1)]};
+        };
+        if (m < nmb && !parted) {
+            const Mv A = x > 0 ? blk(m - 1, 3, 0) : none;
+            const Mv B = y > 0 ? blk(m - mbw, 0, 3) : none;
+            const Mv C = y == 0 ? none
+                                : (x + 1 < mbw ? blk(m - mbw + 1, 0, 3) : (x > 0 ? blk(m - mbw - 1, 3, 3) : none));
+            if (spec) {
+                int sx, sy;
+                pskip_mv(x > 0, y > 0, A, B, C, sx, sy);
+                coded = !pskip ||
+                        !(me.ref == 0 && me.mx == sx && me.my == sy && (k < 0 || hd.cbp == 0));
+                predict_spec(A, B, C, me.ref, px, py);
+            } else {
+                coded = true;
+                predict_ref(A, B, C, me.ref, px, py);
             }
-            total = nb;
-            last_end = last;
-            const uint32_t nw = (nb + 31u) >> 5;
-            const bool over = nw + 2u > cap_words;
-            if (my_bad) atomicOr(&L.bad, 1);
-            if (my_ref_bad) atomicOr(&L.bad, 2);
-            __syncthreads();
-            const int bad = L.bad;
-            if (over || bad) {
-                if (t == 0) {
-                    DF->ep = 0;
-                    DF->err = over ? 1u : (bad & 1 ? 4u : 8u);
-                    if (over) atomicOr((unsigned int *)&S->err, SCROLL_DEVERR_DYN);
-                    else if (bad & 1) atomicOr((unsigned int *)&S->err, SCROLL_DEVERR_HINT);
-                    else {
-                        atomicOr((unsigned int *)&S->err, SCROLL_DEVERR_SPLICE);
-                        spf[fi].stage_status = SCROLL_SPLICE_ERR_REF;
-                    }
-                }
+        }
+        coded |= m < nmb && parted;                            /* predicted per partition */
+        int excl, cmax;
+        block_excl_max(coded ? m : -1, L.wmax, excl, cmax);
+        /* the MB's bits: head, then (spliced) cbp / qp / pieces */
+        /* the left / top MBs' edge TotalCoeffs (0 outside the rect) */
+        const uint4 el = x > 0 ? L.etc[(m - 1) & (RING - 1)] : make_uint4(0u, 0u, 0u, 0u);
+        const uint4 eu = y > 0 ? L.etc[(m - mbw) & (RING - 1)] : make_uint4(0u, 0u, 0u, 0u);
+        /* a partitioned spliced MB's neighbour block (cx, cy) (6.4.11.7) */
+        auto pnb = [&](int cx, int cy, uint32_t dn) {
+            if (cy >= 0) {
+                if (cx >= 4) return none;
+                if (cx >= 0)
+                    return (dn >> (4 * cy + cx)) & 1u ? unpk_mv(rec[k].bref[4 * cy + cx], rec[k].bmv[4 * cy + cx])
+                                                      : none;
+                return x > 0 ? blk(m - 1, 3, cy) : none;
+            }
+            if (y == 0) return none;
+            if (cx < 0) return x > 0 ? blk(m - mbw - 1, 3, 3) : none;
+            if (cx < 4) return blk(m - mbw, cx, 3);
+            return x + 1 < mbw ? blk(m - mbw + 1, 0, 3) : none;
+        };
+        const bool intra = k >= 0 && hd.intra;
+        uint32_t pcm_pad = 0;
+        auto code_mb = [&](auto &sk) {
+            put_ue(sk, (uint32_t)(m - max(excl, last) - 1));  /* mb_skip_run */
+            if (intra) {
+                put_ue(sk, hd.mbt);                            /* verbatim, like its prediction syntax */
+                splice_tail(sk, hd, rec + k, el, eu, x > 0, y > 0, L, rb, pcm_pad);
                 return;
             }
-            for (uint32_t q = (uint32_t)t; q < nw + 1u; q += DT) out[q] = 0u;
-            __threadfence();
+            if (parted) {
+                const SpliceMbRec &mb = rec[k];
+                const int part = mb.part;
+                const uint32_t sub = mb.sub;
+                put_ue(sk, (uint32_t)part);                    /* P_L0_L0_16x8 / 8x16, P_8x8 */
+                if (part == 3)
+                    for (int i = 0; i < 4; ++i) put_ue(sk, (sub >> (2 * i)) & 3u);
+                for (int i = 0; i < (part == 3 ? 4 : 2); ++i) {  /* ref_idx per mbPartIdx */
+                    const int q = part == 1 ? 8 * i : (part == 2 ? 2 * i : 2 * (i & 1) + 8 * (i >> 1));
+                    const int rf = mb.bref[q];
+                    if (nrefs == 2) sk.put((uint32_t)(1 - (rf & 1)), 1);
+                    else put_ue(sk, (uint32_t)rf);
+                }
+                uint32_t dn = 0;
+                for_parts(part, sub, [&](int bx, int by, int bw, int bh, int mp) {
+                    const int q = 4 * by + bx;
+                    const Mv v = unpk_mv(mb.bref[q], mb.bmv[q]);
+                    int qx, qy;
+                    predict_part(part, mp, bx, by, bw, v.ref, [&](int cx, int cy) { return pnb(cx, cy, dn); },
+                                 qx, qy);
+                    put_se(sk, v.mx - qx);
+                    put_se(sk, v.my - qy);
+                    dn |= part_mask(bx, by, bw, bh);
+                });
+            } else {
+                sk.put(1, 1);                                  /* P_L0_16x16 */
+                if (nrefs == 2) sk.put((uint32_t)(1 - (me.ref & 1)), 1);
+                else if (nrefs > 2) put_ue(sk, (uint32_t)me.ref);
+                put_se(sk, me.mx - px);
+                put_se(sk, me.my - py);
+            }
+            if (k >= 0) splice_tail(sk, hd, rec + k, el, eu, x > 0, y > 0, L, rb, 0u);
+            else sk.put(1, 1);                                 /* coded_block_pattern 0 */
+        };
+        CountSink cs{0};
+        if (coded) code_mb(cs);
+        /* I_PCM: pcm_alignment_zero_bits for its composed position.  Sizes
+         * without them, scanned: the n-th I_PCM of the window starts its
+         * samples at key_n + (pads before it) mod 8 with key_n = its
+         * unpadded position mod 8, so pad_n = key_(n-1) - key_n mod 8
+         * (key_0 = 0) */
+        const bool pcm = coded && intra && hd.intra == 3;
+        if (__syncthreads_or(pcm)) {
+            uint32_t o0, t0;
+            block_excl_sum(cs.n, L.wsum, o0, t0);
+            CountSink hc{0};
+            put_ue(hc, (uint32_t)(m - max(excl, last) - 1));
+            put_ue(hc, 30u);
+            const int lane = t & 63, wv = t >> 6;
+            const uint64_t bl = __ballot(pcm);
+            if (lane == 0) L.pcm_mask[wv] = bl;
+            L.pcm_key[t] = (uint8_t)((pos + o0 + hc.n) & 7u);
+            __syncthreads();
+            if (pcm) {
+                int prev = -1;
+                const uint64_t below = bl & ((1ull << lane) - 1ull);
+                if (below) {
+                    prev = 64 * wv + 63 - __builtin_clzll(below);
+                } else {
+                    for (int w2 = wv - 1; w2 >= 0 && prev < 0; --w2)
+                        if (L.pcm_mask[w2]) prev = 64 * w2 + 63 - __builtin_clzll(L.pcm_mask[w2]);
+                }
+                const uint32_t kp = prev >= 0 ? L.pcm_key[prev] : 0u;
+                pcm_pad = (kp - L.pcm_key[t]) & 7u;
+                cs.n += pcm_pad;
+            }
             __syncthreads();
         }
-    }
-    /* trailing run + stop bit (thread 0; positions from the count) */
-    if (t == 0) {
-        uint32_t run_bits = 0;
-        if (last_end < nmb - 1) {
-            CountSink cc{0};
-            put_ue(cc, (uint32_t)(nmb - 1 - last_end));
-            run_bits = cc.n;
+        uint32_t off, T;
+        block_excl_sum(cs.n, L.wsum, off, T);
+            {
+            /* the window's bits [pos, pos + T) -- window 0 from bit 0,
+             * with the slice header -- through the LDS word window
+             * (passes of SPL_WB words), then out with plain stores */
+            const uint32_t wlo = m0 == 0 ? 0u : pos >> 5, whi = (pos + T + 31u) >> 5;
+            if (whi + 2u > cap_words) over = true;             /* uniform */
+            for (uint32_t b0 = wlo; b0 < whi && !over; b0 += SPL_WB) {
+                const uint32_t n = min((uint32_t)SPL_WB, whi - b0);
+                for (uint32_t i = (uint32_t)t; i < n; i += DT)
+                    L.wbuf[i] = (b0 == wlo && i == 0 && m0 > 0) ? L.carry : 0u;
+                __syncthreads();
+                if (m0 == 0 && b0 == 0 && t == 0) {
+                    OrSink<LdsWin> hs{LdsWin{L.wbuf, 0u, n}, 0, 0, 0};
+                    hs.start(0);
+                    emit_slice_header(hs, c);
+                    hs.finish();
+                }
+                const uint32_t a0 = pos + off;
+                if (coded && a0 < 32u * (b0 + n) && a0 + cs.n > 32u * b0) {
+                    OrSink<LdsWin> sk{LdsWin{L.wbuf, b0, n}, 0, 0, 0};
+                    sk.start(a0);
+                    code_mb(sk);
+                    sk.finish();
+                }
+                __syncthreads();
+                for (uint32_t i = (uint32_t)t; i < n; i += DT) out[b0 + i] = __builtin_bswap32(L.wbuf[i]);
+                if (b0 + n == whi && t == 0) L.carry = ((pos + T) & 31u) ? L.wbuf[n - 1] : 0u;
+                __syncthreads();
+            }
         }
-        GSink sk{{out}, 0, 0, 0};
-        sk.start(total - 1u - run_bits);
+        pos += T;
+        last = max(last, cmax);
+        if (over) break;
+    }
+    uint32_t run_bits = 0;
+    if (last < nmb - 1) {
+        CountSink cc{0};
+        put_ue(cc, (uint32_t)(nmb - 1 - last));
+        run_bits = cc.n;
+    }
+    const uint32_t total = pos + run_bits + 1u;     /* + rbsp_stop_one_bit */
+    const int last_end = last;
+    {
+        const uint32_t nw = (total + 31u) >> 5;
+        over |= nw + 2u > cap_words;
+        if (my_bad) atomicOr(&L.bad, 1);
+        if (my_ref_bad) atomicOr(&L.bad, 2);
+        __syncthreads();
+        const int bad = L.bad;
+        if (over || bad) {
+            if (t == 0) {
+                DF->ep = 0;
+                DF->err = over ? 1u : (bad & 1 ? 4u : 8u);
+                if (over) atomicOr((unsigned int *)&S->err, SCROLL_DEVERR_DYN);
+                else if (bad & 1) atomicOr((unsigned int *)&S->err, SCROLL_DEVERR_HINT);
+                else {
+                    atomicOr((unsigned int *)&S->err, SCROLL_DEVERR_SPLICE);
+                    spf[fi].stage_status = SCROLL_SPLICE_ERR_REF;
+                }
+            }
+            return;
+        }
+    }
+    /* trailing skipped MBs, rbsp_stop_one_bit, alignment zeros, after the
+     * carried word; the word after the last (the EP scan's look-ahead) 0 */
+    if (t == 0) {                                   /* the window buffer is free */
+        const uint32_t w0 = pos >> 5;
+        L.wbuf[0] = L.carry;
+        L.wbuf[1] = 0u;
+        OrSink<LdsWin> sk{LdsWin{L.wbuf, w0, 2u}, 0, 0, 0};
+        sk.start(pos);
         if (run_bits) put_ue(sk, (uint32_t)(nmb - 1 - last_end));
         sk.put(1, 1);
         sk.finish();
+        out[w0] = __builtin_bswap32(L.wbuf[0]);
+        out[w0 + 1] = __builtin_bswap32(L.wbuf[1]);
+        if (w0 + 2u <= ((total + 31u) >> 5)) out[w0 + 2] = 0u;
     }
     __threadfence();
     __syncthreads();

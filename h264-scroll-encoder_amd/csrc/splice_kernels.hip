@@ -1040,11 +1040,11 @@ __global__ __launch_bounds__(64 * LANE_WAVES) void k_splice_lanes(const int32_t 
                     R->nbsame = (uint8_t)(aA ? 1 : 0);
                     R->res_len = 0;
                     R->body = 0;
-                    for (int j = 0; j < SPLICE_PIECES; ++j) {
-                        R->tc[j] = 0;
-                        R->t1[j] = 0;
-                        R->blen[j] = 0;
-                    }
+                    /* the TotalCoeffs (its neighbours' nC) as 7 dword stores;
+                     * t1 / blen / boff are read only for cbp's pieces */
+                    uint32_t *tw = reinterpret_cast<uint32_t *>(R->tc);
+#pragma unroll
+                    for (int q = 0; q < (SPLICE_PIECES + 1) / 4; ++q) tw[q] = 0u;
                     const uint32_t v = pk_mv(px, py);
                     if (m == m0) {
                         fmv = v;
@@ -1328,11 +1328,18 @@ __global__ __launch_bounds__(64 * LANE_WAVES) void k_splice_lanes(const int32_t 
                 R->body = (uint16_t)body;
                 R->res_off = base + rs0;
                 R->res_len = rsn;
-                for (int j = 0; j < SPLICE_PIECES; ++j) {
-                    R->tc[j] = L.tcc[j][lane];
-                    if (!((coded >> j) & 1u)) {
-                        R->t1[j] = 0;
-                        R->blen[j] = 0;
+                {
+                    /* the TotalCoeffs as 7 dword stores (one byte store per
+                     * piece had each wave store to 64 records 27 times); t1 /
+                     * blen / boff are read only for cbp's pieces, all parsed */
+                    uint32_t *tw = reinterpret_cast<uint32_t *>(R->tc);
+#pragma unroll
+                    for (int q = 0; q < (SPLICE_PIECES + 1) / 4; ++q) {
+                        uint32_t v = 0;
+#pragma unroll
+                        for (int b2 = 0; b2 < 4; ++b2)
+                            if (4 * q + b2 < SPLICE_PIECES) v |= (uint32_t)L.tcc[4 * q + b2][lane] << (8 * b2);
+                        tw[q] = v;
                     }
                 }
                 /* hand the context on */
@@ -1930,6 +1937,8 @@ struct SpliceLds {
 };
 static_assert(offsetof(SpliceMbRec, blen) == SPLICE_REC_HEAD && sizeof(SpliceMbRec) == 352,
               "the stage copies a record's first SPLICE_REC_HEAD bytes in 16-byte loads");
+static_assert(offsetof(SpliceMbRec, tc) % 4 == 0 && (SPLICE_PIECES + 1) % 4 == 0,
+              "k_splice_lanes stores the TotalCoeffs as whole dwords");
 
 /* an MB's TotalCoeffs its right / lower neighbour reads for nC: x = pieces 3
  * 7 11 15, y = 19 21 23 25 (right column), z = 12 13 14 15, w = 20 21 24 25

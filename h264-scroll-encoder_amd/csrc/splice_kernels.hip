@@ -874,6 +874,22 @@ __device__ inline bool lane_block(LRd &r, const LaneLds &L, int nC, int maxc, in
     return true;
 }
 
+/* an MB record's fixed fields in three wide stores (one lane per slice:
+ * each store of the wave goes to 64 records, so field-by-field byte stores
+ * had cost one store instruction per field) */
+__device__ inline void store_mb_head(SpliceMbRec *R, int ref, int cbp, int qpd, int mx, int my, int skip, int part,
+                                     uint32_t sub, int intra, uint32_t res_off, uint32_t res_len, uint32_t poff,
+                                     uint32_t plen, uint32_t mbt, int cbp_code, int nbsame, int hasqpd, uint32_t body)
+{
+    uint4 *h = reinterpret_cast<uint4 *>(R);
+    h[0] = make_uint4((uint32_t)(uint16_t)ref | (uint32_t)(cbp & 255) << 16 | (uint32_t)(qpd & 255) << 24, (uint32_t)mx,
+                      (uint32_t)my,
+                      (uint32_t)skip | (uint32_t)part << 8 | (sub & 255u) << 16 | (uint32_t)intra << 24);
+    reinterpret_cast<uint2 *>(R)[9] = make_uint2(res_off, res_len);
+    h[5] = make_uint4(poff, (plen & 0xffffu) | (mbt & 255u) << 16 | (uint32_t)(cbp_code & 255) << 24,
+                      (uint32_t)(nbsame & 255) | (uint32_t)(hasqpd & 255) << 8 | (body & 0xffffu) << 16, 0u);
+}
+
 __global__ __launch_bounds__(64 * LANE_WAVES) void k_splice_lanes(const int32_t *__restrict__ list,
                                                                   const SpliceFrame *__restrict__ spf,
                                                                   SpliceUnit *__restrict__ units,
@@ -1028,18 +1044,7 @@ __global__ __launch_bounds__(64 * LANE_WAVES) void k_splice_lanes(const int32_t 
                     const bool aA = x > 0 && m - 1 >= m0;
                     const int px = 0, py = 0;                          /* 8.4.1.1: the MB above unavailable */
                     SpliceMbRec *R = rec + m;
-                    R->ref = 0;
-                    R->cbp = 0;
-                    R->qpd = 0;
-                    R->mx = px;
-                    R->my = py;
-                    R->skip = 1;
-                    R->part = 0;
-                    R->intra = 0;
-                    R->hasqpd = 0;
-                    R->nbsame = (uint8_t)(aA ? 1 : 0);
-                    R->res_len = 0;
-                    R->body = 0;
+                    store_mb_head(R, 0, 0, 0, px, py, 1, 0, 0u, 0, 0u, 0u, 0u, 0u, 0u, 0, aA ? 1 : 0, 0, 0u);
                     /* the TotalCoeffs (its neighbours' nC) as 7 dword stores;
                      * t1 / blen / boff are read only for cbp's pieces */
                     uint32_t *tw = reinterpret_cast<uint32_t *>(R->tc);
@@ -1083,6 +1088,7 @@ __global__ __launch_bounds__(64 * LANE_WAVES) void k_splice_lanes(const int32_t 
                 uint32_t nim = 0xffffffffu;                             /* this MB's modes 3 7 11 15 */
                 Mv me{0, 0, 0};
                 int part = 0;
+                uint32_t subv = 0;                                      /* P_8x8 sub_mb_types */
                 if (mbt >= 5u) {
                     const int it = (int)mbt - 5;
                     intra = it == 0 ? 1 : (it == 25 ? 3 : 2);
@@ -1246,7 +1252,7 @@ __global__ __launch_bounds__(64 * LANE_WAVES) void k_splice_lanes(const int32_t 
                             R->bmv[q2] = L.cmv[q2][lane];
                         }
                     }
-                    R->sub = (uint8_t)sub;
+                    subv = sub;
                     const uint32_t code = r.ue();
                     cbp = code < 48u ? (int)L.cbpi[code] : -1;
                     if (r.bad || r.over() || cbp < 0) {
@@ -1255,12 +1261,6 @@ __global__ __launch_bounds__(64 * LANE_WAVES) void k_splice_lanes(const int32_t 
                     }
                     hasqpd = cbp != 0;
                 }
-                R->ref = (int16_t)me.ref;
-                R->mx = me.mx;
-                R->my = me.my;
-                R->skip = 0;
-                R->part = (uint8_t)part;
-                if (intra) R->sub = 0;
                 if (hasqpd) {
                     const int dq = r.se();
                     if (dq < -26 || dq > 25) {
@@ -1316,18 +1316,8 @@ __global__ __launch_bounds__(64 * LANE_WAVES) void k_splice_lanes(const int32_t 
                     }
                     rsn = r.p - rs0;
                 }
-                R->cbp = (uint8_t)cbp;
-                R->qpd = (int8_t)qpd;
-                R->hasqpd = (uint8_t)hasqpd;
-                R->intra = (uint8_t)intra;
-                R->mbt = (uint8_t)mbt;
-                R->cbp_code = (uint8_t)cbp_code;
-                R->poff = base + poff;
-                R->plen = (uint16_t)plen;
-                R->nbsame = (uint8_t)(aA ? 1 : 0);
-                R->body = (uint16_t)body;
-                R->res_off = base + rs0;
-                R->res_len = rsn;
+                store_mb_head(R, me.ref, cbp, qpd, me.mx, me.my, 0, part, intra ? 0u : subv, intra, base + rs0, rsn,
+                              base + poff, plen, mbt, cbp_code, aA ? 1 : 0, hasqpd, body);
                 {
                     /* the TotalCoeffs as 7 dword stores (one byte store per
                      * piece had each wave store to 64 records 27 times); t1 /
@@ -1939,6 +1929,11 @@ static_assert(offsetof(SpliceMbRec, blen) == SPLICE_REC_HEAD && sizeof(SpliceMbR
               "the stage copies a record's first SPLICE_REC_HEAD bytes in 16-byte loads");
 static_assert(offsetof(SpliceMbRec, tc) % 4 == 0 && (SPLICE_PIECES + 1) % 4 == 0,
               "k_splice_lanes stores the TotalCoeffs as whole dwords");
+static_assert(offsetof(SpliceMbRec, mx) == 4 && offsetof(SpliceMbRec, skip) == 12 && offsetof(SpliceMbRec, intra) == 15 &&
+                  offsetof(SpliceMbRec, res_off) == 72 && offsetof(SpliceMbRec, poff) == 80 &&
+                  offsetof(SpliceMbRec, mbt) == 86 && offsetof(SpliceMbRec, nbsame) == 88 &&
+                  offsetof(SpliceMbRec, body) == 90,
+              "store_mb_head's packing");
 
 /* an MB's TotalCoeffs its right / lower neighbour reads for nC: x = pieces 3
  * 7 11 15, y = 19 21 23 25 (right column), z = 12 13 14 15, w = 20 21 24 25

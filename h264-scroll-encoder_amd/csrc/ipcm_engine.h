@@ -36,9 +36,10 @@ typedef struct {
 /* pass 0: emulation-prevention bytes per chunk -> counts[n][nchunk] (and,
  * with stg, each file's RBSP -> stg + n * stg_stride, stg_stride >=
  * nchunk * IPCM_CHUNK, a multiple of 16), then each file's size -> sizes[n]
- * and *over = 1 if one exceeds out_stride; pass 1: files -> out (prefix,
- * EBSP), from stg when given, nothing when *over.  No host step between the
- * passes.  0, or -1 when a launch failed. */
+ * and *over = 1 if one exceeds out_stride (also *sticky, when given: never
+ * cleared by the kernels); pass 1: files -> out (prefix, EBSP), from stg
+ * when given, nothing when *over.  No host step between the passes.  0, or
+ * -1 when a launch failed. */
 int ipcm_launch(hipStream_t hs, int pass, int n, const IpcmGeom *g, const uint8_t *pics,
                 uint32_t *counts, uint8_t *out, uint8_t *stg, uint64_t stg_stride, uint64_t *sizes,
-                uint32_t *over);
+                uint32_t *over, uint32_t *sticky);

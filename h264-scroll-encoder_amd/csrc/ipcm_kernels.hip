@@ -321,9 +321,11 @@ __global__ __launch_bounds__(IT) void k_ipcm(IpcmGeom G, const uint8_t *__restri
 }
 
 /* grid (n): file n's size = prefix + RBSP + its chunks' EP bytes; any file
- * past out_stride sets *over (the write pass then writes nothing) */
+ * past out_stride sets *over (the write pass then writes nothing) and, for
+ * the asynchronous calls, *sticky (read at the batch's next sync) */
 __global__ __launch_bounds__(IT) void k_ipcm_size(IpcmGeom G, const uint32_t *__restrict__ counts,
-                                                  uint64_t *__restrict__ sizes, uint32_t *__restrict__ over)
+                                                  uint64_t *__restrict__ sizes, uint32_t *__restrict__ over,
+                                                  uint32_t *__restrict__ sticky)
 {
     __shared__ uint32_t wss[IT / 64];
     const int t = threadIdx.x;
@@ -335,21 +337,25 @@ __global__ __launch_bounds__(IT) void k_ipcm_size(IpcmGeom G, const uint32_t *__
     if (t == 0) {
         const uint64_t sz = (uint64_t)G.npre + G.rbsp_len + tot;
         sizes[n] = sz;
-        if (sz > G.out_stride) atomicOr(over, 1u);
+        if (sz > G.out_stride) {
+            atomicOr(over, 1u);
+            if (sticky) atomicOr(sticky, 1u);
+        }
     }
 }
 
 }  // namespace
 
 int ipcm_launch(hipStream_t hs, int pass, int n, const IpcmGeom *g, const uint8_t *pics,
-                uint32_t *counts, uint8_t *out, uint8_t *stg, uint64_t stg_stride, uint64_t *sizes, uint32_t *over)
+                uint32_t *counts, uint8_t *out, uint8_t *stg, uint64_t stg_stride, uint64_t *sizes, uint32_t *over,
+                uint32_t *sticky)
 {
     if (n <= 0) return 0;
     if (pass == 0) {
         hipLaunchKernelGGL(k_ipcm<IP_COUNT>, dim3(g->nchunk, n), dim3(IT), 0, hs, *g, pics, counts, out, stg,
                            stg_stride, over);
         if (hipGetLastError() != hipSuccess) return -1;
-        hipLaunchKernelGGL(k_ipcm_size, dim3(n), dim3(IT), 0, hs, *g, counts, sizes, over);
+        hipLaunchKernelGGL(k_ipcm_size, dim3(n), dim3(IT), 0, hs, *g, counts, sizes, over, sticky);
     } else if (stg) {
         hipLaunchKernelGGL(k_ipcm<IP_WRITE_STAGED>, dim3(g->nchunk, n), dim3(IT), 0, hs, *g, pics, counts, out,
                            stg, stg_stride, over);

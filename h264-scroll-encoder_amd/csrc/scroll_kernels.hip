@@ -985,6 +985,13 @@ struct ScrollBatch {
     size_t ipcm_stg_cap = 0;
     double ipcm_ms = 0.0;
     int ipcm_n = 0;
+    /* the asynchronous I_PCM calls since the last sync: their overflow flag
+     * (checked at the sync) and, with timing, their event pairs */
+    uint32_t *ipcm_over = nullptr;      /* = d_ipcm_sticky while calls are pending */
+    uint32_t *d_ipcm_sticky = nullptr;
+    size_t ipcm_over_stride = 0;
+    std::vector<hipEvent_t> ipcm_ev;    /* pairs, reused */
+    size_t ipcm_ev_used = 0;
     double ing_ms = 0.0;
     int ing_n = 0;
     /* host delivery: per-stream (offset, bytes) table of the last packing */
@@ -1141,6 +1148,9 @@ void scroll_batch_destroy(ScrollBatch *b)
     (void)hipFree(b->d_ing_work);
     for (hipEvent_t e : b->ing_ev)
         if (e) (void)hipEventDestroy(e);
+    for (hipEvent_t e : b->ipcm_ev)
+        if (e) (void)hipEventDestroy(e);
+    (void)hipFree(b->d_ipcm_sticky);
     if (b->d_dbg) (void)hipFree(b->d_dbg);
     delete b;
 }
@@ -1155,6 +1165,8 @@ int scroll_batch_set_debug(ScrollBatch *b, int flags)
 }
 
 static int dyn_grow_pools(ScrollBatch *b);
+
+static int ipcm_async_check(ScrollBatch *b);
 
 static int batch_host_sync(ScrollBatch *b)
 {
@@ -1485,6 +1497,7 @@ int scroll_batch_sync(ScrollBatch *b)
     {
         int rc0 = batch_host_sync(b);
         if (rc0) return rc0;
+        if ((rc0 = ipcm_async_check(b))) return rc0;
     }
     if (b->timed_pending) {
         event_ms(b->ev, b->ev_dyn != 0, false, b->ms);
@@ -2867,11 +2880,13 @@ int scroll_batch_ingest_stats(ScrollBatch *b, double *ms, int *count)
 }
 
 /* ------------------- reference files from pictures (I_PCM) ------------------ */
-int scroll_batch_ipcm_files_device(ScrollBatch *b, int n, int w, int h, const uint8_t *d_pics,
-                                   size_t pic_stride, uint8_t *d_out, size_t out_stride,
-                                   uint64_t *sizes)
+/* the I_PCM files of n pictures; sizes: host (synchronous call) or device
+ * (d_sizes, asynchronous: the overflow check waits for the next sync) */
+static int ipcm_files(ScrollBatch *b, int n, int w, int h, const uint8_t *d_pics, size_t pic_stride, uint8_t *d_out,
+                      size_t out_stride, uint64_t *sizes, uint64_t *d_sizes_out)
 {
-    if (!b || n < 0 || (n > 0 && (!d_pics || !d_out || !sizes))) return SCROLL_ERR_ARG;
+    const bool async = d_sizes_out != nullptr;
+    if (!b || n < 0 || (n > 0 && (!d_pics || !d_out || !(sizes || d_sizes_out)))) return SCROLL_ERR_ARG;
     if (n == 0) return SCROLL_OK;
     const size_t nmb = (size_t)(w / 16) * (size_t)(h / 16);
     if (w <= 0 || h <= 0 || (w & 15) || (h & 15) || nmb >= 65536 ||
@@ -2879,9 +2894,15 @@ int scroll_batch_ipcm_files_device(ScrollBatch *b, int n, int w, int h, const ui
         set_err("scroll_batch_ipcm_files: %dx%d pictures (stride %zu) not supported", w, h, pic_stride);
         return SCROLL_ERR_ARG;
     }
-    int rc = batch_host_sync(b);
-    if (rc) return rc;
+    if (!async) {
+        int rc = batch_host_sync(b);
+        if (rc) return rc;
+    }
     HIPCHK(hipSetDevice(b->device));
+    if (async && !b->ipcm_over) {                   /* the sticky overflow flag (read at the next sync) */
+        if (!b->d_ipcm_sticky) HIPCHK(hipMalloc(&b->d_ipcm_sticky, sizeof(uint32_t)));
+        HIPCHK(hipMemsetAsync(b->d_ipcm_sticky, 0, sizeof(uint32_t), b->own));
+    }
     IpcmGeom g{};
     g.w = w;
     g.h = h;
@@ -2930,6 +2951,10 @@ int scroll_batch_ipcm_files_device(ScrollBatch *b, int n, int w, int h, const ui
     /* counts [n][nchunk] u32, then sizes [n] u64, then the over flag */
     const size_t cnt_bytes = ((size_t)n * g.nchunk * sizeof(uint32_t) + 7) & ~(size_t)7;
     const size_t need = cnt_bytes + (size_t)n * sizeof(uint64_t) + sizeof(uint64_t);
+    if (need > b->ipcm_cap && async && b->ipcm_over) {
+        /* an earlier asynchronous call may still use the scratch */
+        HIPCHK(hipStreamSynchronize(b->own));
+    }
     if (need > b->ipcm_cap) {
         (void)hipFree(b->d_ipcm_cnt);
         b->d_ipcm_cnt = nullptr;
@@ -2957,28 +2982,53 @@ int scroll_batch_ipcm_files_device(ScrollBatch *b, int n, int w, int h, const ui
         if (b->d_ipcm_stg) stg = b->d_ipcm_stg;
     }
     hipStream_t hs = b->own;
-    if (b->timing) {
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (b->timing && !async) {
         for (hipEvent_t &e : b->ing_ev)                  /* created lazily, shared with ingest */
             if (!e) HIPCHK(timing_event(&e));
-        HIPCHK(hipEventRecord(b->ing_ev[0], hs));
+        e0 = b->ing_ev[0];
+        e1 = b->ing_ev[1];
+    } else if (b->timing) {                             /* a pair per call, read at the stats */
+        if (b->ipcm_ev.size() < b->ipcm_ev_used + 2) {
+            for (int k = 0; k < 2; ++k) {
+                hipEvent_t e;
+                HIPCHK(timing_event(&e));
+                b->ipcm_ev.push_back(e);
+            }
+        }
+        e0 = b->ipcm_ev[b->ipcm_ev_used];
+        e1 = b->ipcm_ev[b->ipcm_ev_used + 1];
+        b->ipcm_ev_used += 2;
     }
-    uint64_t *d_sizes = reinterpret_cast<uint64_t *>(reinterpret_cast<uint8_t *>(b->d_ipcm_cnt) + cnt_bytes);
-    uint32_t *d_over = reinterpret_cast<uint32_t *>(d_sizes + n);
+    if (e0) HIPCHK(hipEventRecord(e0, hs));
+    uint64_t *d_sizes = async ? d_sizes_out
+                              : reinterpret_cast<uint64_t *>(reinterpret_cast<uint8_t *>(b->d_ipcm_cnt) + cnt_bytes);
+    uint32_t *d_over = reinterpret_cast<uint32_t *>(reinterpret_cast<uint8_t *>(b->d_ipcm_cnt) + cnt_bytes +
+                                                    (size_t)n * sizeof(uint64_t));
     /* count pass, sizes and the overflow check, write pass: no host step in
      * between (the write pass writes nothing when a file is over) */
-    if (ipcm_launch(hs, 0, n, &g, d_pics, b->d_ipcm_cnt, d_out, stg, stg_stride, d_sizes, d_over) ||
-        ipcm_launch(hs, 1, n, &g, d_pics, b->d_ipcm_cnt, d_out, stg, stg_stride, d_sizes, d_over)) {
+    uint32_t *sticky = async ? b->d_ipcm_sticky : nullptr;
+    if (ipcm_launch(hs, 0, n, &g, d_pics, b->d_ipcm_cnt, d_out, stg, stg_stride, d_sizes, d_over, sticky) ||
+        ipcm_launch(hs, 1, n, &g, d_pics, b->d_ipcm_cnt, d_out, stg, stg_stride, d_sizes, d_over, sticky)) {
         set_err("ipcm launch: %s", hipGetErrorString(hipGetLastError()));
         return SCROLL_ERR_HIP;
     }
-    if (b->timing) HIPCHK(hipEventRecord(b->ing_ev[1], hs));
+    if (e1) HIPCHK(hipEventRecord(e1, hs));
+    if (async) {
+        /* nothing comes back now: the overflow flag is read at the next sync */
+        b->ipcm_over = b->d_ipcm_sticky;
+        b->ipcm_over_stride = out_stride;
+        b->last = hs;
+        b->host_valid = 0;
+        return SCROLL_OK;
+    }
     uint32_t over_flag = 0;
     HIPCHK(hipMemcpyAsync(sizes, d_sizes, (size_t)n * sizeof(uint64_t), hipMemcpyDeviceToHost, hs));
     HIPCHK(hipMemcpyAsync(&over_flag, d_over, sizeof(uint32_t), hipMemcpyDeviceToHost, hs));
     HIPCHK(hipStreamSynchronize(hs));
-    if (b->timing) {
+    if (e0) {
         float ms = 0.0f;
-        HIPCHK(hipEventElapsedTime(&ms, b->ing_ev[0], b->ing_ev[1]));
+        HIPCHK(hipEventElapsedTime(&ms, e0, e1));
         b->ipcm_ms += ms;
         b->ipcm_n++;
     }
@@ -2992,9 +3042,51 @@ int scroll_batch_ipcm_files_device(ScrollBatch *b, int n, int w, int h, const ui
     return SCROLL_OK;
 }
 
+int scroll_batch_ipcm_files_device(ScrollBatch *b, int n, int w, int h, const uint8_t *d_pics,
+                                   size_t pic_stride, uint8_t *d_out, size_t out_stride,
+                                   uint64_t *sizes)
+{
+    return ipcm_files(b, n, w, h, d_pics, pic_stride, d_out, out_stride, sizes, nullptr);
+}
+
+int scroll_batch_ipcm_files_device_async(ScrollBatch *b, int n, int w, int h, const uint8_t *d_pics,
+                                         size_t pic_stride, uint8_t *d_out, size_t out_stride,
+                                         uint64_t *d_sizes)
+{
+    if (!b || (n > 0 && !d_sizes)) return SCROLL_ERR_ARG;
+    return ipcm_files(b, n, w, h, d_pics, pic_stride, d_out, out_stride, nullptr, d_sizes);
+}
+
+/* the asynchronous I_PCM calls' outcome (scroll_batch_sync): their overflow
+ * flag, after the stream is idle */
+static int ipcm_async_check(ScrollBatch *b)
+{
+    if (!b->ipcm_over) return SCROLL_OK;
+    uint32_t over = 0;
+    HIPCHK(hipStreamSynchronize(b->own));
+    HIPCHK(hipMemcpy(&over, b->ipcm_over, sizeof(over), hipMemcpyDeviceToHost));
+    b->ipcm_over = nullptr;
+    if (over) {
+        set_err("scroll_batch_ipcm_files_device_async: a file exceeded out_stride (%zu bytes): "
+                "its call wrote no file", b->ipcm_over_stride);
+        return SCROLL_ERR_OVERFLOW;
+    }
+    return SCROLL_OK;
+}
+
 int scroll_batch_ipcm_stats(ScrollBatch *b, double *ms, int *count)
 {
     if (!b) return SCROLL_ERR_ARG;
+    if (b->ipcm_ev_used) {                              /* the asynchronous calls' pairs */
+        HIPCHK(hipStreamSynchronize(b->own));
+        for (size_t k = 0; k + 1 < b->ipcm_ev_used; k += 2) {
+            float v = 0.0f;
+            HIPCHK(hipEventElapsedTime(&v, b->ipcm_ev[k], b->ipcm_ev[k + 1]));
+            b->ipcm_ms += v;
+            b->ipcm_n++;
+        }
+        b->ipcm_ev_used = 0;
+    }
     if (ms) *ms = b->ipcm_ms;
     if (count) *count = b->ipcm_n;
     b->ipcm_ms = 0.0;

@@ -225,6 +225,10 @@ def _load():
                                                           ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t,
                                                           ctypes.c_void_p, ctypes.c_size_t,
                                                           P(ctypes.c_uint64)]),
+        "scroll_batch_ipcm_files_device_async": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                                                ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t,
+                                                                ctypes.c_void_p, ctypes.c_size_t,
+                                                                ctypes.c_void_p]),
         "scroll_batch_ipcm_stats": (ctypes.c_int, [ctypes.c_void_p, P(ctypes.c_double),
                                                    P(ctypes.c_int)]),
         "composer_batch_write_scroll_frames": (ctypes.c_int, [P(P(Composer)), P(ctypes.c_int),
@@ -545,6 +549,13 @@ class Batch:
                                                      pic_stride, ctypes.c_void_p(d_out),
                                                      out_stride, sizes), "ipcm_files_device")
         return [int(sizes[i]) for i in range(n)]
+
+    def ipcm_files_device_async(self, n, w, h, d_pics, pic_stride, d_out, out_stride, d_sizes):
+        """the same, sizes to d_sizes (device, n u64), no host step: an
+        overflow surfaces at the next sync()"""
+        self._chk(lib.scroll_batch_ipcm_files_device_async(self.h, n, w, h, ctypes.c_void_p(d_pics), pic_stride,
+                                                           ctypes.c_void_p(d_out), out_stride,
+                                                           ctypes.c_void_p(d_sizes)), "ipcm_files_device_async")
 
     def ipcm_stats(self):
         ms, n = ctypes.c_double(), ctypes.c_int()

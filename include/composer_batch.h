@@ -429,6 +429,15 @@ int scroll_batch_ingest_stats(ScrollBatch *b, double *ms, int *count);
 int scroll_batch_ipcm_files_device(ScrollBatch *b, int n, int w, int h, const uint8_t *d_pics,
                                    size_t pic_stride, uint8_t *d_out, size_t out_stride,
                                    uint64_t *sizes);
+/* the same without the host step: the sizes go to d_sizes (device, n u64)
+ * and the call returns once its launches are queued on the batch's stream;
+ * a file past out_stride (that call then writes no file) is reported by the
+ * next scroll_batch_sync as SCROLL_ERR_OVERFLOW.  For pipelines that feed
+ * the files straight to scroll_batch_ingest_device; the scratch is the
+ * batch's, so calls of one batch run in stream order. */
+int scroll_batch_ipcm_files_device_async(ScrollBatch *b, int n, int w, int h, const uint8_t *d_pics,
+                                         size_t pic_stride, uint8_t *d_out, size_t out_stride,
+                                         uint64_t *d_sizes);
 /* with timing enabled: summed kernel ms of the calls above since the last
  * call (both passes) and the number of calls */
 int scroll_batch_ipcm_stats(ScrollBatch *b, double *ms, int *count);

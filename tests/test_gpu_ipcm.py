@@ -210,3 +210,43 @@ def test_files_feed_ingest_and_compose(gpu, hip, oracle):
         b.close()
         dev.free()
         out.free()
+
+
+def test_async_entry_matches_and_reports_overflow_at_sync(gpu, hip, oracle, scroll):
+    """scroll_batch_ipcm_files_device_async: sizes to a device array, no host
+    step per call; back-to-back calls give the oracle's files, and a call
+    past out_stride surfaces at the next sync as SCROLL_ERR_OVERFLOW (that
+    call writes no file), the following calls unaffected once synced"""
+    w, h = 176, 144
+    pics = pictures(w, h, ["rand", "zero", "sparse", "a"], seed=11)
+    n, psz = len(pics), w * h * 3 // 2
+    stride = (psz + 255) // 256 * 256
+    want = [ipcm_file(oracle, w, h, p) for p in pics]
+    ostride = (max(len(f) for f in want) + 255) // 256 * 256
+    dev, out, dsz = hip.buf(n * stride), hip.buf(n * ostride, 0xAB), hip.buf(8 * n)
+    b = gpu.Batch(1, 1, 1 << 20, device=0)
+    try:
+        for i, p in enumerate(pics):
+            dev.write(i * stride, p)
+        for _ in range(3):                               # stream-ordered reuse of the batch scratch
+            b.ipcm_files_device_async(n, w, h, dev.p, stride, out.p, ostride, dsz.p)
+        assert b.sync() == 0, gpu.last_error()
+        sizes = np.frombuffer(dsz.read().tobytes(), np.uint64)
+        host = out.read()
+        for i in range(n):
+            assert int(sizes[i]) == len(want[i])
+            assert host[i * ostride:i * ostride + len(want[i])].tobytes() == want[i]
+        small = min(len(f) for f in want) - 1              # every file over
+        out2 = hip.buf(n * ostride, 0xAB)
+        b.ipcm_files_device_async(n, w, h, dev.p, stride, out2.p, small, dsz.p)
+        assert b.sync() == scroll.SCROLL_ERR_OVERFLOW
+        assert "out_stride" in gpu.last_error()
+        assert (out2.read() == 0xAB).all(), "an over-size call wrote bytes"
+        out2.free()
+        b.ipcm_files_device_async(n, w, h, dev.p, stride, out.p, ostride, dsz.p)
+        assert b.sync() == 0, gpu.last_error()
+    finally:
+        b.close()
+        dev.free()
+        out.free()
+        dsz.free()

@@ -1428,8 +1428,9 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
     __shared__ RowFixed L;
     extern __shared__ uint4 rdyn[];
     /* debug: realtime at entry and after each phase (tools/dyn_stamps.py) */
-    uint64_t stv[6] = {0, 0, 0, 0, 0, 0};
-    if (stamps) stv[0] = __builtin_amdgcn_s_memrealtime();
+    /* (straight to the slot: an array of the six stamps was kept in scratch
+     * memory, zeroed by every thread) */
+    const uint64_t t_entry = stamps ? __builtin_amdgcn_s_memrealtime() : 0ull;
     const int r = blockIdx.x, t = threadIdx.x, T = blockDim.x, lane = t & 63, wave = t >> 6, nwv = T >> 6;
     int f = blockIdx.y, s = blockIdx.z;
     if (GEN) {                          /* grid (h, record slots): the frames k_dyn_rows listed */
@@ -1441,6 +1442,11 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
     }
     const size_t nb = (size_t)s * ld_fr + f;
     constexpr bool general = GEN;
+    uint64_t *const stp = stamps && t == 0
+                              ? stamps + (((size_t)s * gridDim.y + f) * g.ngroups + (max(1, (g.y0 + DYN_STATIC_ROWS - 1) /
+                                                                                        DYN_STATIC_ROWS) + r)) * 8
+                              : nullptr;
+    if (stp) stp[0] = t_entry;
     const Rect R{g.x0, g.y0, g.w, g.h};
     const int w = R.w, ndt = R.w * R.h, row = R.y0 + r, npc = NPC * w, ntask = 24 * w;
     const int ng = g.ngroups;
@@ -1605,7 +1611,7 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
             compute(pa, cur);
         }
         __syncthreads();                                /* levels, TotalCoeffs, ptabs, counts */
-        if (stamps) stv[1] = __builtin_amdgcn_s_memrealtime();
+        if (stp) stp[1] = __builtin_amdgcn_s_memrealtime();
         /* the row's bottom TotalCoeffs (luma 12-15, chroma AC raster 2, 3 of
          * each plane) for the row below: one granule per MB */
         const bool nopub = (g.debug & SCROLL_DEBUG_DYN_NOPUBLISH) && s == 0 && f == 0 && r == 0;   /* tests */
@@ -1746,7 +1752,7 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
         return bwd + (size_t)df.rbsp_bytes * (size_t)(NPC * ndt) + rec_of(r * w + k, pc, ndt);
     };
     __syncthreads();                                    /* records, top TotalCoeffs, waypoint table */
-    if (stamps) stv[2] = __builtin_amdgcn_s_memrealtime();
+    if (stp) stp[2] = __builtin_amdgcn_s_memrealtime();
     ROW_CUT(2);
 
     /* ---- 3: coeff_token, piece lengths ----------------------------------- */
@@ -1788,7 +1794,7 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
         lo[i] = (uint16_t)(len | nc1 << 11);
     }
     __syncthreads();
-    if (stamps) stv[3] = __builtin_amdgcn_s_memrealtime();
+    if (stp) stp[3] = __builtin_amdgcn_s_memrealtime();
     ROW_CUT(3);
     const bool head_over = L.head_over;
     auto head_bits = [&](int rr, int col) -> uint32_t {
@@ -1862,7 +1868,7 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
         if (lane == 0) moff[w] = carry;
     }
     __syncthreads();
-    if (stamps) stv[4] = __builtin_amdgcn_s_memrealtime();
+    if (stp) stp[4] = __builtin_amdgcn_s_memrealtime();
     ROW_CUT(4);
     const uint32_t bits = colpos(mbw);
     if (t == 0) gbits[nb * (size_t)ng + gi] = bits;
@@ -1977,12 +1983,10 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
         __syncthreads();
     }
     if (t == 0 && !lost) out[epc] = L.ncand;
-    if (stamps && t == 0) {
-        stv[5] = __builtin_amdgcn_s_memrealtime();
-        uint64_t *o = stamps + (((size_t)s * gridDim.y + f) * ng + gi) * 8;
-        for (int k2 = 0; k2 < 6; ++k2) o[k2] = stv[k2];
-        o[6] = bits;
-        o[7] = (uint64_t)(uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 4);     /* HW_ID */
+    if (stp) {
+        stp[5] = __builtin_amdgcn_s_memrealtime();
+        stp[6] = bits;
+        stp[7] = (uint64_t)(uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 4);     /* HW_ID */
     }
 }
 

@@ -775,7 +775,7 @@ def verify_splice_step(b, ext_host, wl, first, passes, nstreams=None):
     return ok, d
 
 
-ING_KERNEL = "ingest call: k_ing_scan, k_ing_head, k_ing_seg<SUMMARY>, k_ing_fix, k_ing_seg<WRITE_STAGED>"
+ING_KERNEL = "ingest call: k_ing_scan, k_ing_head, k_ing_seg<FUSED>"
 IPCM_KERNEL = "k_ipcm (count + write passes)"
 # the splice workloads' timed launches (one HIP event pair: parse, then stage)
 SPLICE_KERNEL = ("k_splice_units+k_splice_unesc+k_splice_lanes+k_splice_parse+k_splice_fix"

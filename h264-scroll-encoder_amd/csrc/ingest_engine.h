@@ -19,6 +19,7 @@ enum {
     ING_ERR_DIMS = 3,               /* A and B differ in size (composer.c:177)   */
     ING_ERR_NALS = 4,               /* more than ING_SC_MAX NAL units in a file  */
     ING_ERR_OVERFLOW = 5,           /* the header does not fit the arena         */
+    ING_ERR_WAIT = 6,               /* a segment waited too long for an earlier one (k_ing_seg) */
 };
 
 typedef struct {
@@ -40,11 +41,15 @@ typedef struct {
  * header bytes at the start of its arena.  0, or -1 when a launch failed. */
 int ingest_launch(hipStream_t hs, const uint8_t *in, const IngestFile *files, int nstreams,
                   uint64_t max_file, IngestScan *scan, IngestOut *outs, uint8_t *arena,
-                  uint64_t ld_arena, uint64_t cap, int first_stream, void *work, size_t work_bytes);
+                  uint64_t ld_arena, uint64_t cap, int first_stream, void *work, size_t work_bytes, int mode);
+/* the segmented path's passes: one (summary, placement and write in one
+ * workgroup per segment, the default), or round 4's three -- summary, serial
+ * placement per stream, write -- whose write pass reads the summary pass's
+ * output bytes back (staged) or decodes the segment again */
+enum { ING_ONEPASS = 0, ING_STAGED = 1, ING_RECOMPUTE = 2 };
 /* device scratch of the segmented path (work; nullptr: one workgroup per
- * stream); staged: room for the summary pass's output bytes, which the write
- * pass then reads instead of decoding the segment again */
-size_t ingest_work_bytes(int nstreams, uint64_t max_file, bool staged);
+ * stream) for mode ING_* */
+size_t ingest_work_bytes(int nstreams, uint64_t max_file, int mode);
 
 /* mid-stream long-term reference updates (k_ing_update): files[k] -> a
  * non-IDR I frame of stream ups[2 k] marked long-term ups[2 k + 1],

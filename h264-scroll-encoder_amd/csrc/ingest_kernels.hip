@@ -24,8 +24,10 @@
  *                 16 MB and SCROLL_INGEST_SERIAL.
  *   segmented     (the default, below k_ing_stream) the same parse in
  *                 k_ing_head, each slice body cut into 16 KB segments
- *                 over many workgroups: k_ing_seg<SUMMARY>, k_ing_fix,
- *                 k_ing_seg<WRITE_STAGED>.
+ *                 over many workgroups: k_ing_seg<FUSED> (summary,
+ *                 look-back placement and write in one pass; round 4's
+ *                 k_ing_seg<SUMMARY>, k_ing_fix, k_ing_seg<WRITE_STAGED>
+ *                 stay for comparison, SCROLL_INGEST_THREEPASS).
  * Bits: byte-identical to the reference's composer_write_header output
  * (tests/test_gpu_ingest.py against oracle/scroll_oracle.c, pinned by the
  * reference's golden header files).  Roofline: HBM (files in, header NALs
@@ -786,12 +788,92 @@ struct IngSeg {
     uint32_t cafter;                     /* EP insertions after the first non-zero byte */
     int64_t lnz;                         /* last non-zero output byte before it, relative (k_ing_fix) */
     uint64_t at;                         /* arena offset of its first output byte (k_ing_fix) */
+    /* the one-pass path's hand-off (k_ing_seg<SEG_FUSED>): the summary
+     * (hw[0..1]) and the chain state after the segment (hw[2..3]) as words
+     * with a valid bit (63), written and polled with relaxed agent-scope
+     * atomics -- no fence: an agent-scope release / acquire writes back /
+     * invalidates the XCD's L2 (a first version that published a flag that
+     * way, looking back one segment at a time from lane 0, took 3.1 ms per
+     * call against 0.96 ms now).  Zeroed by k_ing_head. */
+    unsigned long long hw[4];
 };
+
+/* the hand-off words: summary kept / nout / cafter (< 2^17 each), f + 1 /
+ * last + 1 (< 2^17) / vf; state: bad, arena position; RBSP bytes (< 2^32)
+ * and last non-zero output byte + 1 (< 2^31) of the slice so far */
+__device__ inline uint64_t hw_s0(uint32_t kept, uint32_t nout, uint32_t cafter)
+{
+    return 1ull << 63 | (uint64_t)kept << 34 | (uint64_t)nout << 17 | cafter;
+}
+__device__ inline uint64_t hw_s1(int32_t f, int32_t last, int32_t vf)
+{
+    return 1ull << 63 | (uint64_t)(uint32_t)(f + 1) << 25 | (uint64_t)(uint32_t)(last + 1) << 8 | (uint32_t)vf;
+}
+__device__ inline uint64_t hw_p0(uint64_t pos, uint32_t bad) { return 1ull << 63 | (uint64_t)(bad != 0) << 62 | pos; }
+__device__ inline uint64_t hw_p1(uint64_t R0, int64_t lnz) { return 1ull << 63 | R0 << 31 | (uint64_t)(lnz + 1); }
+__device__ inline bool hw_valid(uint64_t a, uint64_t b) { return (a & b) >> 63; }
+__device__ inline uint64_t hw_load(unsigned long long *p)
+{
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ inline void hw_store(unsigned long long *p, uint64_t v)
+{
+    __hip_atomic_store(p, (unsigned long long)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+/* the chain state over a new stream's segments, A's then B's (k_ing_fix's
+ * serial loop as a step per segment): arena position, RBSP bytes and last
+ * non-zero output byte of the slice so far, a header-longer-than-a-segment
+ * flag */
+struct IngChain {
+    uint64_t pos, R0;
+    int64_t lnz;
+    uint32_t bad;
+};
+
+/* even numbers >= 2 in [a, b] */
+__device__ inline int64_t evens_ge2(int64_t a, int64_t b)
+{
+    if (a < 2) a = 2;
+    const int64_t f = a + (a & 1);
+    return b < f ? 0 : (b - f) / 2 + 1;
+}
+
+/* segment c of slice P (summary kept / nout / f / vf / last / cafter) on
+ * the chain: its arena offset and incoming last non-zero byte (relative to
+ * its first output byte), then the state after it.  nal_at: the slice's NAL
+ * offset (segment 0; A's from k_ing_head, B's where A ends) */
+__device__ inline void ing_chain_step(IngChain &st, const IngPlan &P, uint32_t c, uint64_t nal_at, uint32_t kept,
+                                      uint32_t nout, int32_t f, int32_t vf, int32_t last, uint32_t cafter,
+                                      uint64_t &at, int64_t &lnz_rel)
+{
+    const int64_t D = (int64_t)P.hlen - (int64_t)P.mb_start, cd = (D + 7) >> 3;
+    if (c == 0) {
+        st.pos = nal_at + 5;
+        st.R0 = 0;
+        st.lnz = -1;
+    }
+    const int64_t o0 = c == 0 ? 0 : (int64_t)st.R0 + cd;
+    if (c > 0 && o0 < (int64_t)P.npre) st.bad = 1;         /* a header longer than a segment's body */
+    at = st.pos;
+    lnz_rel = st.lnz - o0;
+    const int64_t of = f >= 0 ? o0 + f : o0 + (int64_t)nout;   /* first non-zero (or the end) */
+    int64_t ins = nout ? evens_ge2(o0 - 1 - st.lnz, of - 2 - st.lnz) : 0;   /* zero bytes o0 .. of - 1 */
+    if (f >= 0) {
+        const int64_t run = of - 1 - st.lnz;
+        if (vf <= 3 && run >= 2 && !(run & 1)) ins++;
+        ins += cafter;
+        st.lnz = o0 + last;
+    }
+    st.pos += nout + (uint64_t)ins;
+    st.R0 += kept;
+}
 
 __global__ __launch_bounds__(DT) void k_ing_head(const uint8_t *__restrict__ in,
                                                  const IngestFile *__restrict__ files,
                                                  const IngestScan *__restrict__ scan,
                                                  IngestOut *__restrict__ outs, IngPlan *__restrict__ plans,
+                                                 IngSeg *__restrict__ segs, uint32_t *__restrict__ ticket,
                                                  uint32_t maxseg, uint8_t *__restrict__ arena,
                                                  uint64_t ld_arena, uint64_t cap, int first_stream)
 {
@@ -800,6 +882,12 @@ __global__ __launch_bounds__(DT) void k_ing_head(const uint8_t *__restrict__ in,
     uint8_t *A = arena + (size_t)(first_stream + k) * ld_arena;
     const uint8_t *d[2] = {in + files[2 * k].off, in + files[2 * k + 1].off};
     const uint64_t n[2] = {files[2 * k].size, files[2 * k + 1].size};
+    /* the one-pass segments' hand-off flags and ticket (k_ing_seg<SEG_FUSED>) */
+    for (uint32_t q = (uint32_t)t; q < 2 * maxseg; q += DT) {
+        IngSeg &Q = segs[(size_t)2 * k * maxseg + q];
+        Q.hw[0] = Q.hw[1] = Q.hw[2] = Q.hw[3] = 0ull;
+    }
+    if (k == 0 && t == 0 && ticket) *ticket = 0u;
     if (t != 0) return;
     int err = ING_OK;
     for (int f = 0; f < 2 && err == ING_OK; ++f) {
@@ -950,19 +1038,57 @@ struct SegLds {
  * puts it.  Emulation prevention needs the last non-zero byte before each
  * byte: inside the segment a max-scan, from the segments before k_ing_fix's
  * lnz.  All windows of a phase share one workgroup scan. */
-enum { SEG_SUMMARY = 0, SEG_WRITE = 1, SEG_WRITE_STAGED = 2 };
+enum { SEG_SUMMARY = 0, SEG_WRITE = 1, SEG_WRITE_STAGED = 2, SEG_FUSED = 3 };
+
+/* SEG_FUSED (round 5, the default): summary, place and write in one
+ * workgroup, the output bytes never leaving registers.  Workgroups take
+ * their segment from a ticket, in the order (stream's segment index over A
+ * then B, stream), so every segment before it in its stream holds an earlier
+ * ticket: it has started and publishes its summary without waiting for
+ * anything.  A segment publishes its summary, looks back (decoupled
+ * look-back) for the nearest earlier segment that has published its chain
+ * state, steps the chain over the summaries in between (k_ing_fix's loop),
+ * publishes its own state and writes.  The stream's last segment reports the
+ * header's bytes.  Traffic: the file once here (and once in k_ing_scan), the
+ * arena once -- 1.60x the algorithmic bytes; round 4's summary / fix /
+ * staged-write passes also wrote and read back the output bytes (2.52x).
+ * The look-back (wave 0, 64 segments per load) costs the workgroup about
+ * two agent-scope round trips: 0.96 ms per ingest720 call against the three
+ * passes' 0.90 ms. */
+constexpr uint64_t ING_WAIT_TICKS = 5000000ull;      /* 50 ms of waiting for an earlier segment: the stream fails */
+constexpr uint64_t ING_WAIT_GAP = 100000ull;         /* a longer gap between two polls is a preemption, not counted */
 
 template <int MODE>
 __global__ __launch_bounds__(DT) void k_ing_seg(const uint8_t *__restrict__ in,
                                                 const IngPlan *__restrict__ plans,
                                                 IngSeg *__restrict__ segs, uint32_t maxseg,
                                                 uint8_t *__restrict__ arena, uint64_t ld_arena,
-                                                int first_stream, uint8_t *__restrict__ stg)
+                                                int first_stream, uint8_t *__restrict__ stg,
+                                                uint32_t *__restrict__ ticket, IngestOut *__restrict__ outs,
+                                                uint64_t cap)
 {
     constexpr bool WRITE = MODE != SEG_SUMMARY;
+    constexpr bool FUSED = MODE == SEG_FUSED;
     __shared__ SegLds L;
-    const uint32_t c = blockIdx.x, p = blockIdx.y;
+    __shared__ uint32_t s_tk;
+    __shared__ uint64_t s_at, s_nal;
+    __shared__ int64_t s_lnz;
+    __shared__ uint32_t s_skip;
+    __shared__ int32_t s_vf;
+    uint32_t c = blockIdx.x, p = blockIdx.y, v = 0, ntot = 0;
     const int t = threadIdx.x;
+    if (FUSED) {                                            /* grid (2 maxseg, streams) */
+        if (t == 0) s_tk = atomicAdd(ticket, 1u);
+        __syncthreads();
+        const uint32_t tk = s_tk, k = tk % gridDim.y;
+        v = tk / gridDim.y;
+        const IngPlan &PA = plans[2 * k];
+        if (!PA.ok) return;
+        ntot = PA.nseg + plans[2 * k + 1].nseg;
+        if (v >= ntot) return;
+        p = v < PA.nseg ? 2 * k : 2 * k + 1;
+        c = v < PA.nseg ? v : v - PA.nseg;
+    }
     const IngPlan &P = plans[p];
     if (!P.ok || c >= P.nseg) return;
     IngSeg &G = segs[(size_t)p * maxseg + c];
@@ -1118,16 +1244,16 @@ __global__ __launch_bounds__(DT) void k_ing_seg(const uint8_t *__restrict__ in,
      * the zero run since the last non-zero byte is even and >= 2 */
     int lx[NJ], lt[NJ];
     block_excl_max_v<NJ>(my_l, L.wmax, lx, lt);
-    /* positions relative to the segment, int32; a last non-zero byte
-     * further back than 4 bytes only matters through its parity */
-    int32_t before;
-    {
-        const int64_t b = WRITE ? G.lnz : -((int64_t)1 << 40);
-        before = b >= -4 ? (int32_t)b : -4 - (int32_t)(b & 1);
-    }
     const int32_t nout32 = (int32_t)nout;
     uint32_t nb[NJ + 1], insm[NJ];
     uint32_t naft = 0;
+    int32_t before;
+    /* lnz_in: the last non-zero output byte before the segment, relative */
+    auto ep_pass = [&](int64_t lnz_in) {
+    /* positions relative to the segment, int32; a last non-zero byte
+     * further back than 4 bytes only matters through its parity */
+    before = lnz_in >= -4 ? (int32_t)lnz_in : -4 - (int32_t)(lnz_in & 1);
+    naft = 0;
     nb[NJ] = 0;
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
@@ -1164,12 +1290,19 @@ __global__ __launch_bounds__(DT) void k_ing_seg(const uint8_t *__restrict__ in,
         }
         if (lt[j] >= 0) before = OCH * j + lt[j];
     }
-    if (!WRITE) {
+    };
+    ep_pass(WRITE && !FUSED ? G.lnz : -((int64_t)1 << 40));
+    int32_t my_first = -1, my_last = -1;
+    uint32_t my_cafter = 0;
+    if (!WRITE || FUSED) {
         uint32_t v1[1] = {naft}, e1v[1], t1v[1];
         int fv[1] = {my_f == INT32_MAX ? -1 : INT32_MAX - my_f}, fe[1], ft[1];
         block_excl_max_v<1>(fv, L.wmin, fe, ft);
         block_excl_sum_v<1>(v1, L.wsum, e1v, t1v);
         const int32_t first = ft[0] >= 0 ? INT32_MAX - ft[0] : -1;
+        my_first = first;
+        my_last = before >= 0 ? before : -1;
+        my_cafter = t1v[0];
         if (t == 0) {
             G.kept = kept;
             G.nout = (uint32_t)nout;
@@ -1186,9 +1319,118 @@ __global__ __launch_bounds__(DT) void k_ing_seg(const uint8_t *__restrict__ in,
 #pragma unroll
                 for (int k = 0; k < 4; ++k)
                     if (jj == j && k == (q >> 2)) x = (ow[jj][k] >> (8 * (q & 3))) & 255u;
-            G.vf = (int32_t)x;
+            if (FUSED) s_vf = (int32_t)x;           /* published by lane 0 with the rest */
+            else G.vf = (int32_t)x;
         }
-        return;
+        if (!FUSED) return;
+    }
+    uint64_t at = G.at;
+    int64_t lnz_in = G.lnz;
+    if (FUSED) {
+        __syncthreads();                                    /* s_vf */
+        if (t < 64) {                                       /* wave 0: publish, look back, place */
+            const int lane = t, k = (int)(p >> 1);
+            const IngPlan &PA = plans[2 * k];
+            IngSeg *SA = segs + (size_t)(2 * k) * maxseg, *SB = SA + maxseg;
+            auto seg_at = [&](int64_t u) -> IngSeg & {
+                return (uint32_t)u < PA.nseg ? SA[u] : SB[(uint32_t)u - PA.nseg];
+            };
+            const int32_t vf = my_first >= 0 ? s_vf : 0;
+            if (lane == 0) {
+                hw_store(&G.hw[0], hw_s0(kept, (uint32_t)nout, my_cafter));
+                hw_store(&G.hw[1], hw_s1(my_first, my_last, vf));
+            }
+            /* the nearest earlier segment of the stream with its state (64
+             * at a time; none: the chain starts at A's segment 0) */
+            int64_t base = -1;
+            uint64_t b0 = 0, b1 = 0;
+            for (int64_t hi = (int64_t)v - 1; hi >= 0; hi -= 64) {
+                const int64_t u = hi - lane;
+                uint64_t q0 = 0, q1 = 0;
+                if (u >= 0) {
+                    q0 = hw_load(&seg_at(u).hw[2]);
+                    q1 = hw_load(&seg_at(u).hw[3]);
+                }
+                const uint64_t m = __builtin_amdgcn_ballot_w64(u >= 0 && hw_valid(q0, q1));
+                if (m) {
+                    const int L = __builtin_ctzll(m);
+                    base = hi - L;
+                    b0 = __shfl(q0, L, 64);
+                    b1 = __shfl(q1, L, 64);
+                    break;
+                }
+            }
+            IngChain st{0, 0, -1, 0};
+            if (base >= 0) st = IngChain{b0 & ((1ull << 62) - 1), (b1 >> 31) & 0xffffffffull,
+                                         (int64_t)(b1 & 0x7fffffffull) - 1, (uint32_t)((b0 >> 62) & 1u)};
+            /* the summaries after it, 64 at a time (each published without
+             * waiting for anything: the poll is bounded only against a
+             * broken dispatch), stepped through in order */
+            uint64_t prev = __builtin_amdgcn_s_memrealtime(), waited = 0, nal = 0;
+            bool late = false;
+            auto step_over = [&](int64_t w, uint64_t a0, uint64_t a1, uint64_t &at_o, int64_t &lr_o) {
+                const bool inB = (uint32_t)w >= PA.nseg;
+                const uint32_t cw = inB ? (uint32_t)w - PA.nseg : (uint32_t)w;
+                if (cw == 0) nal = inB ? st.pos : PA.at;
+                ing_chain_step(st, plans[2 * k + (inB ? 1 : 0)], cw, nal, (uint32_t)(a0 >> 34) & 0x1ffffu,
+                               (uint32_t)(a0 >> 17) & 0x1ffffu, (int32_t)((a1 >> 25) & 0x1ffffu) - 1,
+                               (int32_t)(a1 & 255u), (int32_t)((a1 >> 8) & 0x1ffffu) - 1, (uint32_t)a0 & 0x1ffffu,
+                               at_o, lr_o);
+            };
+            uint64_t xat = 0;
+            int64_t xl = -1;
+            for (int64_t lo = base + 1; lo < (int64_t)v && !late; lo += 64) {
+                const int64_t u = lo + lane;
+                bool need = u < (int64_t)v;
+                uint64_t q0 = 0, q1 = 0;
+                for (;;) {
+                    if (need) {
+                        q0 = hw_load(&seg_at(u).hw[0]);
+                        q1 = hw_load(&seg_at(u).hw[1]);
+                        need = !hw_valid(q0, q1);
+                    }
+                    if (__builtin_amdgcn_ballot_w64(need) == 0) break;
+                    const uint64_t now = __builtin_amdgcn_s_memrealtime(), gap = now - prev;
+                    prev = now;
+                    if (gap < ING_WAIT_GAP) waited += gap;
+                    if (waited > ING_WAIT_TICKS) {
+                        late = true;
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                }
+                if (late) break;
+                const int n = (int)min((int64_t)64, (int64_t)v - lo);
+                for (int j = 0; j < n; ++j) {
+                    uint64_t dat;
+                    int64_t dl;
+                    step_over(lo + j, __shfl(q0, j, 64), __shfl(q1, j, 64), dat, dl);
+                }
+            }
+            step_over((int64_t)v, hw_s0(kept, (uint32_t)nout, my_cafter), hw_s1(my_first, my_last, vf), xat, xl);
+            if (lane == 0) {
+                if (!late) {
+                    hw_store(&G.hw[2], hw_p0(st.pos, st.bad));
+                    hw_store(&G.hw[3], hw_p1(st.R0, st.lnz));
+                }
+                s_nal = nal;
+                s_at = xat;
+                s_lnz = xl;
+                /* nothing of a stream that fails is written past its arena */
+                s_skip = late || st.bad || st.pos > cap;
+                if (v + 1 == ntot || late) {                /* the stream's outcome */
+                    if (late) outs[k].err = ING_ERR_WAIT;
+                    else if (st.bad) outs[k].err = ING_ERR_PARSE;
+                    else if (st.pos > cap) outs[k].err = ING_ERR_OVERFLOW;
+                    if (!late && !st.bad && st.pos <= cap) outs[k].bytes = st.pos;
+                }
+            }
+        }
+        __syncthreads();
+        if (s_skip) return;
+        at = s_at;
+        lnz_in = s_lnz;
+        ep_pass(lnz_in);
     }
     /* 4. write, window by window, staged at the arena address's phase in
      * 16-byte lines: whole lines go out as one 16-byte store, the two end
@@ -1196,9 +1438,8 @@ __global__ __launch_bounds__(DT) void k_ing_seg(const uint8_t *__restrict__ in,
     uint32_t ex[NJ + 1], tot[NJ + 1];
     block_excl_sum_v<NJ + 1>(nb, L.wsum, ex, tot);
     uint8_t *A = arena + (size_t)(first_stream + (int)(p >> 1)) * ld_arena;
-    uint64_t at = G.at;
     if (c == 0 && t == 0) {
-        const uint64_t a5 = P.at;
+        const uint64_t a5 = FUSED ? s_nal : P.at;
         A[a5] = 0;
         A[a5 + 1] = 0;
         A[a5 + 2] = 0;
@@ -1253,14 +1494,6 @@ __global__ __launch_bounds__(DT) void k_ing_seg(const uint8_t *__restrict__ in,
         at += tot[j];
         __syncthreads();
     }
-}
-
-/* even numbers >= 2 in [a, b] */
-__device__ inline int64_t evens_ge2(int64_t a, int64_t b)
-{
-    if (a < 2) a = 2;
-    const int64_t f = a + (a & 1);
-    return b < f ? 0 : (b - f) / 2 + 1;
 }
 
 /* per stream, serial over the segments of A then B: RBSP prefix, output
@@ -1481,7 +1714,7 @@ int update_launch(hipStream_t hs, const uint8_t *in, const IngestFile *files, in
 
 int ingest_launch(hipStream_t hs, const uint8_t *in, const IngestFile *files, int nstreams,
                   uint64_t max_file, IngestScan *scan, IngestOut *outs, uint8_t *arena,
-                  uint64_t ld_arena, uint64_t cap, int first_stream, void *work, size_t work_bytes)
+                  uint64_t ld_arena, uint64_t cap, int first_stream, void *work, size_t work_bytes, int mode)
 {
     if (nstreams <= 0) return 0;
     if (hipMemsetAsync(scan, 0, sizeof(IngestScan) * 2 * (size_t)nstreams, hs) != hipSuccess)
@@ -1499,30 +1732,37 @@ int ingest_launch(hipStream_t hs, const uint8_t *in, const IngestFile *files, in
     }
     IngPlan *plans = reinterpret_cast<IngPlan *>(work);
     IngSeg *segs = reinterpret_cast<IngSeg *>(plans + 2 * (size_t)nstreams);
-    hipLaunchKernelGGL(k_ing_head, dim3(nstreams), dim3(DT), 0, hs, in, files, scan, outs, plans, maxseg, arena,
-                       ld_arena, cap, first_stream);
-    uint8_t *stg = nullptr;                 /* the summary pass's output bytes, when the scratch holds them */
     const size_t base = 2 * (size_t)nstreams * (sizeof(IngPlan) + maxseg * sizeof(IngSeg));
-    if (work_bytes >= base + 2 * (size_t)nstreams * maxseg * (size_t)(NJ * OCH) + 16)
+    uint32_t *ticket = reinterpret_cast<uint32_t *>(reinterpret_cast<uint8_t *>(work) + base);
+    if (work_bytes < base + 16) return -1;
+    hipLaunchKernelGGL(k_ing_head, dim3(nstreams), dim3(DT), 0, hs, in, files, scan, outs, plans, segs,
+                       mode == ING_ONEPASS ? ticket : nullptr, maxseg, arena, ld_arena, cap, first_stream);
+    if (mode == ING_ONEPASS) {
+        hipLaunchKernelGGL(k_ing_seg<SEG_FUSED>, dim3(2 * maxseg, nstreams), dim3(DT), 0, hs, in, plans, segs,
+                           maxseg, arena, ld_arena, first_stream, nullptr, ticket, outs, cap);
+        return hipGetLastError() == hipSuccess ? 0 : -1;
+    }
+    uint8_t *stg = nullptr;                 /* the summary pass's output bytes, when the scratch holds them */
+    if (mode == ING_STAGED && work_bytes >= base + 2 * (size_t)nstreams * maxseg * (size_t)(NJ * OCH) + 16)
         stg = reinterpret_cast<uint8_t *>(((uintptr_t)work + base + 15) & ~(uintptr_t)15);
     hipLaunchKernelGGL(k_ing_seg<SEG_SUMMARY>, dim3(maxseg, 2 * nstreams), dim3(DT), 0, hs, in, plans, segs,
-                       maxseg, arena, ld_arena, first_stream, stg);
+                       maxseg, arena, ld_arena, first_stream, stg, nullptr, nullptr, 0ull);
     hipLaunchKernelGGL(k_ing_fix, dim3(nstreams), dim3(64), 0, hs, plans, segs, maxseg, outs, cap);
     if (stg)
         hipLaunchKernelGGL(k_ing_seg<SEG_WRITE_STAGED>, dim3(maxseg, 2 * nstreams), dim3(DT), 0, hs, in, plans,
-                           segs, maxseg, arena, ld_arena, first_stream, stg);
+                           segs, maxseg, arena, ld_arena, first_stream, stg, nullptr, nullptr, 0ull);
     else
         hipLaunchKernelGGL(k_ing_seg<SEG_WRITE>, dim3(maxseg, 2 * nstreams), dim3(DT), 0, hs, in, plans, segs,
-                           maxseg, arena, ld_arena, first_stream, stg);
+                           maxseg, arena, ld_arena, first_stream, stg, nullptr, nullptr, 0ull);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 /* scratch of the segmented path; 0 when ingest_launch takes the one-workgroup
  * path anyway (a slice over FIX_MAXSEG segments), which needs none */
-size_t ingest_work_bytes(int nstreams, uint64_t max_file, bool staged)
+size_t ingest_work_bytes(int nstreams, uint64_t max_file, int mode)
 {
     const size_t maxseg = (size_t)((max_file + SEG - 1) / SEG) + 1u;
     if (maxseg > (size_t)FIX_MAXSEG) return 0;
     const size_t base = 2 * (size_t)nstreams * (sizeof(IngPlan) + maxseg * sizeof(IngSeg));
-    return staged ? base + 2 * (size_t)nstreams * maxseg * (size_t)(NJ * OCH) + 16 : base;
+    return mode == ING_STAGED ? base + 2 * (size_t)nstreams * maxseg * (size_t)(NJ * OCH) + 16 : base + 16;
 }

@@ -2744,6 +2744,7 @@ static const char *ing_msg(int e)
     case ING_ERR_DIMS: return "reference frame dimensions don't match";
     case ING_ERR_NALS: return "too many NAL units in a reference file";
     case ING_ERR_OVERFLOW: return "header larger than the stream arena";
+    case ING_ERR_WAIT: return "a segment of the header waited too long for the one before it";
     default: return "ingest failed";
     }
 }
@@ -2788,14 +2789,20 @@ int scroll_batch_ingest_device(ScrollBatch *b, int n, const uint8_t *d_files, co
         totf += files[k].size;
     }
     const bool serial = getenv("SCROLL_INGEST_SERIAL") != nullptr;
-    /* the staged write pass while its scratch (every file sized like the
-     * largest, ~1.25x per segment) stays within 4x the input plus 256 MB and
-     * under 8 GB -- a batch of small files with one huge one takes the
-     * recomputing pass instead of a scratch sized by the huge one */
-    const size_t stg_bytes = ingest_work_bytes(n, maxf, true);
-    const bool staged = getenv("SCROLL_INGEST_RECOMPUTE") == nullptr && stg_bytes <= ((size_t)8 << 30) &&
-                        stg_bytes <= 4 * (size_t)totf + ((size_t)256 << 20);
-    const size_t wb = serial ? 0 : ingest_work_bytes(n, maxf, staged);
+    /* the one-pass segments (default); round 4's three passes for
+     * comparison (tests): SCROLL_INGEST_THREEPASS=1 stages the output bytes
+     * while that scratch (every file sized like the largest, ~1.25x per
+     * segment) stays within 4x the input plus 256 MB and under 8 GB, and
+     * otherwise -- or with SCROLL_INGEST_RECOMPUTE=1 -- decodes again */
+    int mode = ING_ONEPASS;
+    if (getenv("SCROLL_INGEST_THREEPASS") || getenv("SCROLL_INGEST_RECOMPUTE")) {
+        const size_t stg_bytes = ingest_work_bytes(n, maxf, ING_STAGED);
+        mode = getenv("SCROLL_INGEST_RECOMPUTE") == nullptr && stg_bytes <= ((size_t)8 << 30) &&
+                       stg_bytes <= 4 * (size_t)totf + ((size_t)256 << 20)
+                   ? ING_STAGED
+                   : ING_RECOMPUTE;
+    }
+    const size_t wb = serial ? 0 : ingest_work_bytes(n, maxf, mode);
     if (wb > b->ing_work_bytes) {
         (void)hipFree(b->d_ing_work);
         b->d_ing_work = nullptr;
@@ -2817,7 +2824,7 @@ int scroll_batch_ingest_device(ScrollBatch *b, int n, const uint8_t *d_files, co
     }
     if (ingest_launch(hs, d_files, b->d_ing_files, n, maxf, b->d_ing_scan, b->d_ing_out,
                       b->d_arena, (uint64_t)b->ld_arena, (uint64_t)b->arena_bytes, b->nstreams,
-                      serial ? nullptr : b->d_ing_work, wb)) {
+                      serial ? nullptr : b->d_ing_work, wb, mode)) {
         set_err("ingest launch: %s", hipGetErrorString(hipGetLastError()));
         return SCROLL_ERR_HIP;
     }

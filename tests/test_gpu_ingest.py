@@ -213,19 +213,32 @@ def test_ingest_errors_add_no_stream(gpu, oracle, scroll):
 
 
 def test_ingest_segmented_matches_one_workgroup_path(gpu, oracle, monkeypatch):
-    """the segmented path (default: slices cut into 16 KB EBSP segments over
-    many workgroups, the write pass reading the summary pass's bytes), its
-    recomputing write pass (SCROLL_INGEST_RECOMPUTE) and the
-    one-workgroup-per-stream path (SCROLL_INGEST_SERIAL) write the same bytes;
-    EP-heavy 1280x720 files put zero runs of both parities across segment
-    boundaries"""
+    """the segmented path -- by default one pass (each 16 KB EBSP segment
+    summarised, placed by look-back over the segments before it and written
+    by one workgroup), or round 4's three passes with the write pass reading
+    the summary pass's bytes (SCROLL_INGEST_THREEPASS) or decoding again
+    (SCROLL_INGEST_RECOMPUTE) -- and the one-workgroup-per-stream path
+    (SCROLL_INGEST_SERIAL) write the same bytes; EP-heavy 1280x720 files put
+    zero runs of both parities across segment boundaries"""
     w, h = 1280, 720
     pairs = [variant_files(oracle, w, h, k) for k in (1, 2, 3, 6, 7)]
     outs = []
-    for env in (None, "SCROLL_INGEST_RECOMPUTE", "SCROLL_INGEST_SERIAL"):
+    for env in (None, "SCROLL_INGEST_THREEPASS", "SCROLL_INGEST_RECOMPUTE", "SCROLL_INGEST_SERIAL"):
+        for e in ("SCROLL_INGEST_THREEPASS", "SCROLL_INGEST_RECOMPUTE", "SCROLL_INGEST_SERIAL"):
+            monkeypatch.delenv(e, raising=False)
         if env:
             monkeypatch.setenv(env, "1")
         b = check_ingest(gpu, oracle, pairs, nframes=0, arena=8 << 20)
         outs.append([b.output(s) for s in range(len(pairs))])
         b.close()
-    assert outs[0] == outs[1] == outs[2]
+    assert outs[0] == outs[1] == outs[2] == outs[3]
+
+
+def test_ingest_one_pass_many_streams(gpu, oracle):
+    """the one-pass path's look-back under load: 48 new streams of 1280x720
+    files (about 90 segments each, A's chain continuing into B's), every
+    header byte-identical to the oracle's"""
+    w, h = 1280, 720
+    pairs = [variant_files(oracle, w, h, k % 8) for k in range(48)]
+    b = check_ingest(gpu, oracle, pairs, nframes=0, arena=8 << 20)
+    b.close()

@@ -794,7 +794,7 @@ struct IngSeg {
      * atomics -- no fence: an agent-scope release / acquire writes back /
      * invalidates the XCD's L2 (a first version that published a flag that
      * way, looking back one segment at a time from lane 0, took 3.1 ms per
-     * call against 0.96 ms now).  Zeroed by k_ing_head. */
+     * call against 0.80 ms now).  Zeroed by k_ing_head. */
     unsigned long long hw[4];
 };
 
@@ -1040,6 +1040,12 @@ struct SegLds {
  * lnz.  All windows of a phase share one workgroup scan. */
 enum { SEG_SUMMARY = 0, SEG_WRITE = 1, SEG_WRITE_STAGED = 2, SEG_FUSED = 3 };
 
+/* waves per SIMD k_ing_seg is compiled for: the fused pass held 128 VGPRs
+ * (4 workgroups per CU) unbounded, while its LDS allows 6 */
+#ifndef SCROLL_ING_WAVES
+#define SCROLL_ING_WAVES 6
+#endif
+
 /* SEG_FUSED (round 5, the default): summary, place and write in one
  * workgroup, the output bytes never leaving registers.  Workgroups take
  * their segment from a ticket, in the order (stream's segment index over A
@@ -1053,13 +1059,14 @@ enum { SEG_SUMMARY = 0, SEG_WRITE = 1, SEG_WRITE_STAGED = 2, SEG_FUSED = 3 };
  * arena once -- 1.60x the algorithmic bytes; round 4's summary / fix /
  * staged-write passes also wrote and read back the output bytes (2.52x).
  * The look-back (wave 0, 64 segments per load) costs the workgroup about
- * two agent-scope round trips: 0.96 ms per ingest720 call against the three
- * passes' 0.90 ms. */
+ * two agent-scope round trips, hidden by 6 workgroups per CU (the output
+ * bytes parked in LDS meanwhile): 0.80 ms per ingest720 call against the
+ * three passes' 0.90 ms. */
 constexpr uint64_t ING_WAIT_TICKS = 5000000ull;      /* 50 ms of waiting for an earlier segment: the stream fails */
 constexpr uint64_t ING_WAIT_GAP = 100000ull;         /* a longer gap between two polls is a preemption, not counted */
 
 template <int MODE>
-__global__ __launch_bounds__(DT) void k_ing_seg(const uint8_t *__restrict__ in,
+__global__ __launch_bounds__(DT) __attribute__((amdgpu_waves_per_eu(SCROLL_ING_WAVES))) void k_ing_seg(const uint8_t *__restrict__ in,
                                                 const IngPlan *__restrict__ plans,
                                                 IngSeg *__restrict__ segs, uint32_t maxseg,
                                                 uint8_t *__restrict__ arena, uint64_t ld_arena,
@@ -1327,6 +1334,13 @@ __global__ __launch_bounds__(DT) void k_ing_seg(const uint8_t *__restrict__ in,
     uint64_t at = G.at;
     int64_t lnz_in = G.lnz;
     if (FUSED) {
+        /* the output bytes wait in LDS (free: the RBSP bytes are consumed)
+         * while wave 0 looks back -- kept in registers across it the pass
+         * needed 128 VGPRs, 4 waves per SIMD */
+        static_assert(NJ * DT * 16 <= SEG_LDS_BYTES, "the parked output bytes fit the LDS buffer");
+        uint4 *park = reinterpret_cast<uint4 *>(L.rb);
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) park[j * DT + t] = make_uint4(ow[j][0], ow[j][1], ow[j][2], ow[j][3]);
         __syncthreads();                                    /* s_vf */
         if (t < 64) {                                       /* wave 0: publish, look back, place */
             const int lane = t, k = (int)(p >> 1);
@@ -1428,6 +1442,15 @@ __global__ __launch_bounds__(DT) void k_ing_seg(const uint8_t *__restrict__ in,
         }
         __syncthreads();
         if (s_skip) return;
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            const uint4 q = park[j * DT + t];
+            ow[j][0] = q.x;
+            ow[j][1] = q.y;
+            ow[j][2] = q.z;
+            ow[j][3] = q.w;
+        }
+        __syncthreads();                                    /* the staging below reuses the buffer */
         at = s_at;
         lnz_in = s_lnz;
         ep_pass(lnz_in);

@@ -2156,6 +2156,12 @@ __global__ __launch_bounds__(DT) __attribute__((amdgpu_waves_per_eu(SCROLL_STAGE
     uint32_t pos = F0;             /* bits: header + MBs so far (uniform) */
     int last = -1;                 /* last coded MB before the window (uniform) */
     bool over = false;
+    /* emulation prevention as the words go out (round 5; round 4 read the
+     * slot back word by word after a fence, looking back for the last
+     * non-zero byte through agent-scope loads): the last non-zero byte of
+     * the words written so far (uniform) and this thread's insertions */
+    int lnzb = -1;
+    uint32_t my_ep = 0;
     for (int m0 = 0; m0 < nmb; m0 += DT) {
         /* the previous window's writing sweep still reads the ring (the
          * neighbour blocks of its partitioned MBs): wait before refilling */
@@ -2351,6 +2357,19 @@ __global__ __launch_bounds__(DT) __attribute__((amdgpu_waves_per_eu(SCROLL_STAGE
                     sk.finish();
                 }
                 __syncthreads();
+                /* the words final here (all but a last one the next window
+                 * still ORs into): their 03 insertions, the last non-zero byte
+                 * before each from a block max-scan and lnzb */
+                const uint32_t nfin = (b0 + n == whi && ((pos + T) & 31u)) ? n - 1u : n;
+                for (uint32_t c0 = 0; c0 < nfin; c0 += DT) {
+                    const uint32_t i = c0 + (uint32_t)t;
+                    const uint32_t wv = i < nfin ? L.wbuf[i] : 0u;
+                    int ex, tot;
+                    block_excl_max(wv ? (int)(4u * (b0 + i)) + last_nz_byte(wv) : -1, L.wmax, ex, tot);
+                    int prev = max(ex, lnzb);
+                    if (i < nfin) my_ep += ep_word(wv, 4u * (b0 + i), 0xffffffffu, prev, eplist, &L.ep_n);
+                    lnzb = max(lnzb, tot);
+                }
                 for (uint32_t i = (uint32_t)t; i < n; i += DT) out[b0 + i] = __builtin_bswap32(L.wbuf[i]);
                 if (b0 + n == whi && t == 0) L.carry = ((pos + T) & 31u) ? L.wbuf[n - 1] : 0u;
                 __syncthreads();
@@ -2391,6 +2410,7 @@ __global__ __launch_bounds__(DT) __attribute__((amdgpu_waves_per_eu(SCROLL_STAGE
     }
     /* trailing skipped MBs, rbsp_stop_one_bit, alignment zeros, after the
      * carried word; the word after the last (the EP scan's look-ahead) 0 */
+    const uint32_t nbytes = (total + 7u) >> 3;
     if (t == 0) {                                   /* the window buffer is free */
         const uint32_t w0 = pos >> 5;
         L.wbuf[0] = L.carry;
@@ -2403,26 +2423,9 @@ __global__ __launch_bounds__(DT) __attribute__((amdgpu_waves_per_eu(SCROLL_STAGE
         out[w0] = __builtin_bswap32(L.wbuf[0]);
         out[w0 + 1] = __builtin_bswap32(L.wbuf[1]);
         if (w0 + 2u <= ((total + 31u) >> 5)) out[w0 + 2] = 0u;
-    }
-    __threadfence();
-    __syncthreads();
-    /* emulation prevention: per word, the zero run before it from the last
-     * non-zero byte (looked up backwards) */
-    const uint32_t nbytes = (total + 7u) >> 3, nw = (nbytes + 3u) >> 2;
-    uint32_t my_ep = 0;
-    for (uint32_t jw = (uint32_t)t; jw < nw; jw += DT) {
-        const uint32_t wv = __builtin_bswap32(__hip_atomic_load(&out[jw], __ATOMIC_RELAXED,
-                                                                __HIP_MEMORY_SCOPE_AGENT));
-        int prev = -1;
-        for (int jj = (int)jw - 1; jj >= 0; --jj) {
-            const uint32_t pv = __builtin_bswap32(
-                __hip_atomic_load(&out[jj], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-            if (pv) {
-                prev = 4 * jj + last_nz_byte(pv);
-                break;
-            }
-        }
-        my_ep += ep_word(wv, 4u * jw, nbytes, prev, eplist, &L.ep_n);
+        int prev = lnzb;                            /* the last words' insertions (bytes < nbytes) */
+        my_ep += ep_word(L.wbuf[0], 4u * w0, nbytes, prev, eplist, &L.ep_n);
+        my_ep += ep_word(L.wbuf[1], 4u * (w0 + 1u), nbytes, prev, eplist, &L.ep_n);
     }
     uint32_t ex, tot;
     block_excl_sum(my_ep, L.wsum, ex, tot);

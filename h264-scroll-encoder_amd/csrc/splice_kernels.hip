@@ -698,10 +698,19 @@ struct LaneLds {
     uint8_t tzd[3 * 16];                 /* chroma DC total_zeros */
     uint8_t rb[7 * 48];                  /* run_before: (min(zl, 7) - 1) 48 + min(lz, 11) 4 + 2 bits */
     uint8_t cbpi[48];                    /* inter codeNum -> coded_block_pattern */
-    uint8_t tcc[SPLICE_PIECES][64];      /* per lane: the current MB's TotalCoeffs */
-    uint32_t cmv[16][64];                /* per lane: the current MB's blocks as they decode */
-    int8_t crf[16][64];
-    int8_t im[16][64];                   /* per lane: the current MB's Intra4x4PredModes */
+    /* per active lane (LANE_ACTIVE; round 4 sized them for all 64) */
+    uint8_t tcc[SPLICE_PIECES][LANE_ACTIVE];   /* the current MB's TotalCoeffs */
+    uint32_t cmv[16][LANE_ACTIVE];             /* the current MB's blocks as they decode */
+    int8_t crf[16][LANE_ACTIVE];
+    int8_t im[16][LANE_ACTIVE];                /* the current MB's Intra4x4PredModes */
+    /* the current MB's pieces -- TrailingOnes, body length and offset --
+     * written to its record in whole lines when the MB is done: stored
+     * field by field as parsed, 102 K lanes' open records (4.5 MB per XCD)
+     * outgrew the L2 and reached HBM as partial lines, 5.5 GB of writes per
+     * p720splicerows step for 0.9 GB of records */
+    uint8_t t1s[SPLICE_PIECES + 1][LANE_ACTIVE];
+    uint16_t bls[SPLICE_PIECES + 1][LANE_ACTIVE];
+    uint32_t bos[SPLICE_PIECES + 1][LANE_ACTIVE];
 };
 
 /* a lane's own bit reader: the next 33..64 bits in a 64-bit register, a
@@ -1247,10 +1256,21 @@ __global__ __launch_bounds__(64 * LANE_WAVES) void k_splice_lanes(const int32_t 
                             break;
                         }
                         me = unpk_mv(L.crf[0][lane], L.cmv[0][lane]);
-                        for (int q2 = 0; q2 < 16; ++q2) {
-                            R->bref[q2] = L.crf[q2][lane];
-                            R->bmv[q2] = L.cmv[q2][lane];
+                        /* the blocks' refs and motion in 8-byte stores */
+                        uint2 *bw = reinterpret_cast<uint2 *>(R->bref);
+#pragma unroll
+                        for (int h2 = 0; h2 < 2; ++h2) {
+                            uint32_t v0 = 0, v1 = 0;
+#pragma unroll
+                            for (int b2 = 0; b2 < 4; ++b2) {
+                                v0 |= (uint32_t)(uint8_t)L.crf[8 * h2 + b2][lane] << (8 * b2);
+                                v1 |= (uint32_t)(uint8_t)L.crf[8 * h2 + 4 + b2][lane] << (8 * b2);
+                            }
+                            bw[h2] = make_uint2(v0, v1);
                         }
+                        uint2 *mw = reinterpret_cast<uint2 *>(R->bmv);
+#pragma unroll
+                        for (int h2 = 0; h2 < 8; ++h2) mw[h2] = make_uint2(L.cmv[2 * h2][lane], L.cmv[2 * h2 + 1][lane]);
                     }
                     subv = sub;
                     const uint32_t code = r.ue();
@@ -1292,9 +1312,9 @@ __global__ __launch_bounds__(64 * LANE_WAVES) void k_splice_lanes(const int32_t 
                             return;
                         }
                         L.tcc[pi][lane] = (uint8_t)tc;
-                        R->t1[pi] = (uint8_t)t1;
-                        R->boff[pi] = base + bo;
-                        R->blen[pi] = (uint16_t)bl;
+                        L.t1s[pi][lane] = (uint8_t)t1;
+                        L.bos[pi][lane] = base + bo;
+                        L.bls[pi][lane] = (uint16_t)bl;
                         coded |= 1u << pi;
                         body += bl;
                     };
@@ -1330,6 +1350,29 @@ __global__ __launch_bounds__(64 * LANE_WAVES) void k_splice_lanes(const int32_t 
                         for (int b2 = 0; b2 < 4; ++b2)
                             if (4 * q + b2 < SPLICE_PIECES) v |= (uint32_t)L.tcc[4 * q + b2][lane] << (8 * b2);
                         tw[q] = v;
+                    }
+                    if (hasqpd) {
+                        /* the pieces' TrailingOnes (7 dwords), then blen [28] u16 +
+                         * boff [28] u32 -- record bytes 96 .. 264 -- as 10 16-byte
+                         * stores and an 8-byte one; a piece the cbp leaves out
+                         * carries a stale value, which no reader looks at */
+                        uint32_t *t1w = reinterpret_cast<uint32_t *>(R->t1);
+#pragma unroll
+                        for (int q = 0; q < (SPLICE_PIECES + 1) / 4; ++q) {
+                            uint32_t v = 0;
+#pragma unroll
+                            for (int b2 = 0; b2 < 4; ++b2) v |= (uint32_t)L.t1s[4 * q + b2][lane] << (8 * b2);
+                            t1w[q] = v;
+                        }
+                        auto dw = [&](int d) -> uint32_t {          /* dword d of bytes 96 .. 264 */
+                            if (d < (SPLICE_PIECES + 1) / 2)
+                                return (uint32_t)L.bls[2 * d][lane] | (uint32_t)L.bls[2 * d + 1][lane] << 16;
+                            return L.bos[d - (SPLICE_PIECES + 1) / 2][lane];
+                        };
+                        uint4 *bq = reinterpret_cast<uint4 *>(R->blen);
+#pragma unroll
+                        for (int q = 0; q < 10; ++q) bq[q] = make_uint4(dw(4 * q), dw(4 * q + 1), dw(4 * q + 2), dw(4 * q + 3));
+                        reinterpret_cast<uint2 *>(R->blen)[20] = make_uint2(dw(40), dw(41));
                     }
                 }
                 /* hand the context on */
@@ -1929,6 +1972,9 @@ static_assert(offsetof(SpliceMbRec, blen) == SPLICE_REC_HEAD && sizeof(SpliceMbR
               "the stage copies a record's first SPLICE_REC_HEAD bytes in 16-byte loads");
 static_assert(offsetof(SpliceMbRec, tc) % 4 == 0 && (SPLICE_PIECES + 1) % 4 == 0,
               "k_splice_lanes stores the TotalCoeffs as whole dwords");
+static_assert(offsetof(SpliceMbRec, t1) % 4 == 0 && offsetof(SpliceMbRec, blen) == 96 && offsetof(SpliceMbRec, boff) == 152 &&
+                  offsetof(SpliceMbRec, bref) == 264 && offsetof(SpliceMbRec, bmv) == 280 && (SPLICE_PIECES + 1) == 28,
+              "k_splice_lanes' record stores: t1 in dwords, blen + boff as 168 bytes from 96, bref / bmv in 8-byte stores");
 static_assert(offsetof(SpliceMbRec, mx) == 4 && offsetof(SpliceMbRec, skip) == 12 && offsetof(SpliceMbRec, intra) == 15 &&
                   offsetof(SpliceMbRec, res_off) == 72 && offsetof(SpliceMbRec, poff) == 80 &&
                   offsetof(SpliceMbRec, mbt) == 86 && offsetof(SpliceMbRec, nbsame) == 88 &&

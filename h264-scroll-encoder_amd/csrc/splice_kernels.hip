@@ -1939,6 +1939,9 @@ __global__ __launch_bounds__(64) void k_splice_fix(int n, const int32_t *__restr
 /* k_splice_stage                                                            */
 /* ------------------------------------------------------------------------ */
 constexpr int SPL_WB = 2048;                 /* writing sweep: LDS words per pass (64 Kbit) */
+#ifndef SCROLL_STAGE_HEAD_LDS
+#define SCROLL_STAGE_HEAD_LDS 1
+#endif
 
 /* ORs MSB-first words into LDS words [lo, lo + n) (others dropped: another pass) */
 struct LdsWin {
@@ -1967,6 +1970,11 @@ struct SpliceLds {
     uint32_t ep_n;
     int32_t bad;
     uint32_t carry;                         /* the partial word at the bit position (MSB first) */
+#if SCROLL_STAGE_HEAD_LDS
+    /* each lane's spliced MB record head (SPLICE_REC_HEAD bytes): held in
+     * registers across the window it took the kernel to 252 VGPRs */
+    alignas(16) uint8_t hdb[DT][SPLICE_REC_HEAD];
+#endif
 };
 static_assert(offsetof(SpliceMbRec, blen) == SPLICE_REC_HEAD && sizeof(SpliceMbRec) == 352,
               "the stage copies a record's first SPLICE_REC_HEAD bytes in 16-byte loads");
@@ -2216,7 +2224,11 @@ __global__ __launch_bounds__(DT) __attribute__((amdgpu_waves_per_eu(SCROLL_STAGE
         int x = 0, y = 0, k = -1;
         Mv me{0, 0, 0};
         bool parted = false;
+#if SCROLL_STAGE_HEAD_LDS
+        SpliceMbRec &hd = *reinterpret_cast<SpliceMbRec *>(L.hdb[t]);   /* its head only */
+#else
         SpliceMbRec hd;                                        /* a spliced MB's record head */
+#endif
         uint4 et = make_uint4(0u, 0u, 0u, 0u);
         if (m < nmb) {
             y = (int)div_m((uint32_t)m, m_mbw);
@@ -2224,10 +2236,15 @@ __global__ __launch_bounds__(DT) __attribute__((amdgpu_waves_per_eu(SCROLL_STAGE
             if (x >= SF.x0 && x < SF.x0 + SF.w && y >= SF.y0 && y < SF.y0 + SF.h) {
                 k = (y - SF.y0) * SF.w + (x - SF.x0);
                 const uint4 *hp = reinterpret_cast<const uint4 *>(rec + k);
+#if SCROLL_STAGE_HEAD_LDS
+#pragma unroll
+                for (int q = 0; q < SPLICE_REC_HEAD / 16; ++q) reinterpret_cast<uint4 *>(L.hdb[t])[q] = hp[q];
+#else
                 uint4 hv[SPLICE_REC_HEAD / 16];
 #pragma unroll
                 for (int q = 0; q < SPLICE_REC_HEAD / 16; ++q) hv[q] = hp[q];
                 __builtin_memcpy(&hd, hv, SPLICE_REC_HEAD);
+#endif
                 if (SF.hd_qp >= 0)                             /* the dynamic rect under hints: its QP chain */
                     hd.qpd = (int8_t)((uint32_t)k == SF.hd_first ? SF.hd_qp - 26 : 0);
                 et = edge_tc(hd);

@@ -5,7 +5,7 @@
 #   bench: bench lines of every workload (+ config 3 at 1024 streams);
 #   prof:  rocprofv3 kernel stats of p720dyn / p4kdyn / p720splicerows /
 #          ingest720 / ipcm720, FETCH_SIZE and WRITE_SIZE passes (separate
-#          runs) over k_dyn_row, one SQ counter pass over the dynamic-rect
+#          runs) over k_dyn_row (and the splice / ingest launches), one SQ counter pass over the dynamic-rect
 #          kernels, and the per-workgroup stamps (dyn_stamps.py).
 # Every GPU step has its own time limit; the first failing step ends the script.
 set -e -o pipefail
@@ -28,8 +28,9 @@ if [ "$PART" = prof ] || [ "$PART" = all ]; then
     done
     $T 120 rocprofv3 --output-format csv --pmc FETCH_SIZE -d "$O/pmc_fetch" -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu --no-host > "$O/pmc_fetch.log" 2>&1
     $T 120 rocprofv3 --output-format csv --pmc WRITE_SIZE -d "$O/pmc_write" -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu --no-host > "$O/pmc_write.log" 2>&1
-    for c in FETCH_SIZE WRITE_SIZE; do          # the splice launches' traffic (tools/traffic.py)
+    for c in FETCH_SIZE WRITE_SIZE; do          # the splice and ingest launches' traffic (tools/traffic.py)
         $T 120 rocprofv3 --output-format csv --pmc $c -d "$O/pmc_splice_$c" -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu --no-verify --workload p720splicerows > "$O/pmc_splice_$c.log" 2>&1
+        $T 120 rocprofv3 --output-format csv --pmc $c -d "$O/pmc_ingest_$c" -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu --no-verify --workload ingest720 > "$O/pmc_ingest_$c.log" 2>&1
     done
     bash h264-scroll-encoder_amd/tools/sq_pass.sh "$O/sq"
     $T 120 python3 h264-scroll-encoder_amd/tools/dyn_stamps.py > "$O/dyn_stamps.txt" 2>&1

@@ -682,12 +682,14 @@ constexpr int SPLICE_REDO = 99;
 constexpr int LANE_WAVES = 1;
 /* slices per wave: the lanes past it only build the tables.  The parse is a
  * chain of dependent loads per slice, and a frame batch has few slices per
- * SIMD (config-3 rows: 102,400 slices = 1.6 full waves per SIMD), so fewer
- * slices per wave put more waves on each SIMD to overlap their chains
- * (p720splicerows, rocprofv3: k_splice_lanes 4.40 / 4.08 / 4.34 ms at 64 /
- * 32 / 16 slices per wave) */
+ * SIMD (config-3 rows: 102,400 slices = 1.6 full waves per SIMD).  With the
+ * records written field by field, fewer slices per wave had paid (4.40 /
+ * 4.08 / 4.34 ms at 64 / 32 / 16 slices per wave): each bit-reader wait
+ * also waited for the wave's scattered stores.  With the records staged in
+ * LDS and written whole, 64 is best (p720splicerows, rocprofv3: 2.62-2.65 /
+ * 3.33 / 3.62 ms at 64 / 32 / 16) */
 #ifndef SCROLL_SPLICE_LPW
-#define SCROLL_SPLICE_LPW 32
+#define SCROLL_SPLICE_LPW 64
 #endif
 constexpr int LANE_ACTIVE = SCROLL_SPLICE_LPW;
 static_assert(LANE_ACTIVE >= 1 && LANE_ACTIVE <= 64 && LANE_WAVES == 1, "k_splice_lanes: one wave, 1-64 slices");

@@ -541,24 +541,42 @@ __global__ __launch_bounds__(DT) void k_splice_units(int n, const int32_t *__res
         return;
     }
     uint32_t k = 0;                                   /* units so far (uniform) */
-    for (uint32_t c0 = 0; c0 + 3 <= len; c0 += 4 * DT) {
-        uint32_t hit = 0, cnt = 0;
+    /* aligned 16-byte lines, one per thread and pass (round 5; round 4 made
+     * three byte loads per position): byte j of a line is the 01 of a start
+     * code at position k - 2 when it is 01 after two zero bytes (SWAR tests
+     * on whole dwords, the dword before the line loaded too) -- positions 0
+     * .. len - 3 as before.  A line never leaves the pages of the bytes it
+     * holds. */
+    const uintptr_t pb = reinterpret_cast<uintptr_t>(p), a0 = pb & ~(uintptr_t)15, ae = pb + len;
+    for (uintptr_t c = a0; c < ae; c += 16u * DT) {
+        const uintptr_t A = c + 16u * (uintptr_t)t;
+        uint4 v = make_uint4(0u, 0u, 0u, 0u);
+        uint32_t pw = 0;
+        if (A < ae) {
+            v = *reinterpret_cast<const uint4 *>(A);
+            if (A > a0) pw = *reinterpret_cast<const uint32_t *>(A - 4);
+        }
+        const uint32_t W[4] = {v.x, v.y, v.z, v.w};
+        const int64_t k0 = (int64_t)A - (int64_t)pb;
+        uint32_t hit = 0, zp = zero_hi(pw);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const uint32_t pos = c0 + 4u * (uint32_t)t + (uint32_t)q;
-            if (pos + 3 <= len && !p[pos] && !p[pos + 1] && p[pos + 2] == 1) {
-                hit |= 1u << q;
-                cnt++;
+        for (int d = 0; d < 4; ++d) {
+            const uint32_t z = zero_hi(W[d]), e1 = zero_hi(W[d] ^ 0x01010101u);
+            const uint32_t sc4 = e1 & __builtin_amdgcn_alignbyte(z, zp, 3u) & __builtin_amdgcn_alignbyte(z, zp, 2u);
+            zp = z;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int64_t kk = k0 + 4 * d + j;
+                hit |= (((sc4 >> (8 * j + 7)) & 1u) && kk >= 2 && kk < (int64_t)len) ? 1u << (4 * d + j) : 0u;
             }
         }
         uint32_t ex, tot;
-        block_excl_sum(cnt, ws, ex, tot);
-        for (int q = 0; q < 4; ++q)
-            if (hit & (1u << q)) {
-                const uint32_t pos = c0 + 4u * (uint32_t)t + (uint32_t)q, u = k + ex++;
-                if (u < cap) UN[u].b = pos + 3u;
-                if (u >= 1 && u - 1 < cap) UN[u - 1].e = pos;
-            }
+        block_excl_sum((uint32_t)__builtin_popcount(hit), ws, ex, tot);
+        for (uint32_t m = hit; m; m &= m - 1u) {
+            const uint32_t pos = (uint32_t)(k0 + __builtin_ctz(m) - 2), u = k + ex++;
+            if (u < cap) UN[u].b = pos + 3u;
+            if (u >= 1 && u - 1 < cap) UN[u - 1].e = pos;
+        }
         k += tot;
     }
     if (t == 0 && k >= 1 && k - 1 < cap) UN[k - 1].e = len;
@@ -585,22 +603,30 @@ __global__ __launch_bounds__(DT) void k_splice_units(int n, const int32_t *__res
 
 /* k_splice_unesc: one wave per slice (a frame's slices dealt over the grid's
  * y waves): the NAL header checked, emulation prevention bytes out (7.4.1:
- * byte i of the payload goes unless it is 03 after two zero bytes; 4 bytes
- * per lane per pass, the output index by a wave prefix count; bytes land
- * MSB-first in words -- byte k at byte address k ^ 3 -- from word ceil(b / 4)
- * of the frame's region on: (len + 2) / 4 words, which never reach the next
- * unit's), and its rbsp_stop_one_bit found by a ballot over the words from
- * the end.  status: SCROLL_SPLICE_ERR_NAL (a bad header), else 0 until the
- * parse. */
+ * payload byte k >= 3 goes when it is 03 after two zero bytes), the bytes
+ * MSB-first in words from word ceil(b / 4) of the frame's region on (b = the
+ * unit's byte offset: a unit's RBSP never reaches the next unit's words), and
+ * the position of its rbsp_stop_one_bit.  Round 5: each lane takes an aligned
+ * 16-byte line of the payload per pass (one load; the two bytes before it
+ * from the lane below), the removal test on whole dwords (SWAR), the kept
+ * bytes through an LDS word window by a wave prefix count, whole words out;
+ * the last non-zero byte comes from the pass, not from reading the words
+ * back.  (Round 4: four byte loads and up to four byte stores per byte, the
+ * region zeroed first: 0.34 ms per p720splicerows step.)  status:
+ * SCROLL_SPLICE_ERR_NAL (a bad header), else 0 until the parse. */
 __global__ __launch_bounds__(64) void k_splice_unesc(int n, const int32_t *__restrict__ list,
                                                      const SpliceFrame *__restrict__ spf,
                                                      SpliceUnit *__restrict__ units,
                                                      uint32_t *__restrict__ rbsp)
 {
+    /* the pass's output bytes at their MSB-first places (byte i at i ^ 3),
+     * word 0 = the word carried from the pass before */
+    __shared__ uint32_t ow[64 * 4 + 2];
     const int i = blockIdx.x, lane = threadIdx.x;
     if (i >= n) return;
     const SpliceFrame *F = spf + list[i];
     const int nu = min(F->nunits, (int)splice_unit_cap(F->w * F->h));
+    uint8_t *ob = reinterpret_cast<uint8_t *>(ow);
     for (int u = (int)blockIdx.y; u < nu; u += (int)gridDim.y) {
         SpliceUnit *UN = units + F->unit_first + u;
         const uint32_t ub = U(UN->b);
@@ -612,46 +638,81 @@ __global__ __launch_bounds__(64) void k_splice_unesc(int n, const int32_t *__res
         const bool ok = len >= 2 && !(h0 & 0x80) && ((h0 & 31) == 1 || (h0 & 31) == 5);   /* non-IDR / IDR slice */
         if (ok) {
             uint32_t *o = rbsp + F->rbsp_word + w0;
-            const uint32_t nwmax = (len + 2u) / 4u;
-            for (uint32_t k = (uint32_t)lane; k < nwmax; k += 64) o[k] = 0u;
-            __syncthreads();
-            uint8_t *ob = reinterpret_cast<uint8_t *>(o);
-            for (uint32_t c0 = 1; c0 < len; c0 += 256) {
-                uint32_t keep = 0, cnt = 0;
-                uint8_t by[4];
+            /* aligned lines over payload bytes [1, len): a line never leaves
+             * the pages of the bytes it holds */
+            const uintptr_t pb = reinterpret_cast<uintptr_t>(p);
+            const uintptr_t a0 = (pb + 1u) & ~(uintptr_t)15, ae = pb + len;
+            uint32_t prevw = 0;                              /* lane 63's last dword of the pass before */
+            uint32_t wout = 0, carry = 0;                    /* words written; bytes in the carried word */
+            int64_t lastnz = -1;                             /* output index of the last non-zero byte */
+            uint32_t lastv = 0;
+            for (uintptr_t c = a0; c < ae; c += 64u * 16u) {
+                const uintptr_t A = c + 16u * (uintptr_t)lane;
+                uint4 v = make_uint4(0u, 0u, 0u, 0u);
+                if (A < ae) v = *reinterpret_cast<const uint4 *>(A);
+                const uint32_t W[4] = {v.x, v.y, v.z, v.w};
+                uint32_t pw = __shfl_up(v.w, 1, 64);
+                if (lane == 0) pw = prevw;
+                prevw = __shfl(v.w, 63, 64);
+                /* k = A + b - pb: kept iff 1 <= k < len and not (k >= 3, 03 after 00 00) */
+                const int64_t k0 = (int64_t)A - (int64_t)pb;
+                uint32_t keep = 0;
+                uint32_t zp = zero_hi(pw);
 #pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const uint32_t k = c0 + 4u * (uint32_t)lane + (uint32_t)q;
-                    by[q] = k < len ? p[k] : 0;
-                    const bool ep = k < len && k >= 3 && by[q] == 3 && p[k - 1] == 0 && p[k - 2] == 0;
-                    const bool kp = k < len && !ep;
-                    keep |= kp ? 1u << q : 0u;
-                    cnt += kp ? 1u : 0u;
+                for (int d = 0; d < 4; ++d) {
+                    const uint32_t z = zero_hi(W[d]), e3 = zero_hi(W[d] ^ 0x03030303u);
+                    const uint32_t rm = e3 & __builtin_amdgcn_alignbyte(z, zp, 3u) & __builtin_amdgcn_alignbyte(z, zp, 2u);
+                    zp = z;
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const int64_t k = k0 + 4 * d + j;
+                        const bool in = k >= 1 && k < (int64_t)len;
+                        const bool gone = k >= 3 && ((rm >> (8 * j + 7)) & 1u);
+                        keep |= (in && !gone) ? 1u << (4 * d + j) : 0u;
+                    }
                 }
+                const uint32_t cnt = (uint32_t)__builtin_popcount(keep);
                 const uint32_t incl = wave_incl_sum(cnt, lane);
-                uint32_t at = nb + incl - cnt;
+                const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane(incl, 63);
+                /* the window: the carried word, then this pass's bytes */
+                for (int q = lane; q < 64 * 4 + 2; q += 64)
+                    if (q > 0) ow[q] = 0u;
+                __syncthreads();
+                uint32_t at = carry + incl - cnt;
+                int64_t mylast = -1;
+                uint32_t mylv = 0;
 #pragma unroll
-                for (int q = 0; q < 4; ++q)
-                    if (keep & (1u << q)) {
-                        ob[at ^ 3u] = by[q];
+                for (int q = 0; q < 16; ++q)
+                    if ((keep >> q) & 1u) {
+                        const uint32_t bv = (W[q >> 2] >> (8 * (q & 3))) & 255u;
+                        ob[at ^ 3u] = (uint8_t)bv;
+                        if (bv) {
+                            mylast = (int64_t)(4u * wout + at);
+                            mylv = bv;
+                        }
                         at++;
                     }
-                nb += __builtin_amdgcn_readlane(incl, 63);
-            }
-            __syncthreads();
-            nb = U(nb);
-            const uint32_t nw = (nb + 3u) >> 2;
-            for (int c = (int)nw - 1; c >= 0; c -= 64) {
-                const int k = c - lane;
-                const uint32_t v = k >= 0 ? o[k] : 0u;
-                const uint64_t bl = __ballot(v != 0u);
+                __syncthreads();
+                const uint32_t nbw = carry + tot, full = nbw >> 2;
+                for (uint32_t q = (uint32_t)lane; q < full; q += 64) o[wout + q] = ow[q];
+                /* the last non-zero byte so far: the highest lane that has one */
+                const uint64_t bl = __ballot(mylast >= 0);
                 if (bl) {
-                    const int l = __builtin_ctzll(bl);
-                    const uint32_t vv = U((uint32_t)__builtin_amdgcn_readlane(v, l));
-                    end = 32u * (uint32_t)(c - l) + 31u - (uint32_t)__builtin_ctz(vv);
-                    break;
+                    const int l = 63 - __builtin_clzll(bl);
+                    lastnz = (int64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)mylast, l);
+                    lastv = (uint32_t)__builtin_amdgcn_readlane(mylv, l);
                 }
+                const uint32_t cw = ow[full];                /* the partial word, carried */
+                __syncthreads();
+                if (lane == 0) ow[0] = cw;
+                wout += full;
+                carry = nbw & 3u;
+                nb += tot;
+                __syncthreads();
             }
+            if (carry && lane == 0) o[wout] = ow[0];         /* the last word, zero-padded */
+            nb = U(nb);
+            if (lastnz >= 0) end = 8u * (uint32_t)lastnz + 7u - (uint32_t)__builtin_ctz(lastv);
         }
         if (lane == 0) {
             UN->w0 = w0;

@@ -301,8 +301,8 @@ def test_dynamic_coder_output_spliced_from_device(gpu, oracle):
 def test_startcode_less_odd_length_adjacent_frames(gpu, oracle):
     """NALs handed over without an Annex-B start code (optional in the API)
     whose lengths are not multiples of 4, in adjacent frames of a stream: the
-    RBSP pool regions of neighbouring frames must not overlap (the parse
-    zeroes (len + 3) / 4 + 2 words of its frame's region)"""
+    RBSP pool regions of neighbouring frames must not overlap (k_splice_unesc
+    writes whole words, the last one zero-padded)"""
     w, h = 320, 256
     S, F = 2, 8
     offs = synthetic_offsets(S, F, h, first_stream=3)
@@ -325,6 +325,43 @@ def test_startcode_less_odd_length_adjacent_frames(gpu, oracle):
     check_equal(b, want)
     assert lens <= {1, 2, 3}
     b.close()
+
+
+def test_device_slices_at_every_alignment(gpu, oracle):
+    """slices handed over by device pointer at every byte offset modulo 16
+    (k_splice_units / k_splice_unesc read the aligned 16-byte lines around
+    them, the bytes outside the slice masked): the oracle's bytes"""
+    from test_gpu_ipcm import Hip             # device memory through libh264scroll's own HIP runtime
+    w, h = 320, 256
+    S, F = 2, 8
+    offs = synthetic_offsets(S, F, h, first_stream=5)
+    c = _cfg(oracle, w, h)
+    frames = {}
+    for s in range(S):
+        for t in range(F):
+            nal = ext_slice(oracle, c, 5, 4, 5000 + 31 * s + t, cbp_pm=800, skip_pm=100)
+            frames[(s, t)] = ([], SPEC, (3, 2, 5, 4, nal))
+    _, want = plan_from(oracle, w, h, offs, frames)
+    total = sum(len(sp[4]) + 32 for (_, _, sp) in frames.values())
+    dev = Hip().buf(total + 64, fill=0xA5)                   # non-zero bytes around the slices
+    pos, specs = 0, []
+    for k, ((s, t), (_, _, sp)) in enumerate(sorted(frames.items())):
+        nal = bytes(sp[4])
+        pos = ((pos + 15) & ~15) + k % 16
+        dev.write(pos, nal)
+        specs.append((s, t, 3, 2, 5, 4, dev.p + pos, len(nal)))
+        pos += len(nal)
+    b = gpu.Batch(S, F, 16 << 20)
+    for _ in range(S):
+        b.add_stream(gpu.make_config(w, h))
+    b.set_splices_device(specs)
+    b.set_offsets(offs)
+    b.compose(F)
+    assert b.sync() == 0, gpu.last_error()
+    check_equal(b, want)
+    assert {sp[6] % 16 for sp in specs} == set(range(16))
+    b.close()
+    dev.free()
 
 
 def plan_from(oracle, w, h, offsets, frames, compose_mode=0):

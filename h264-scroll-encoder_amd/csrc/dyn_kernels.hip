@@ -1199,9 +1199,18 @@ constexpr int ROW_MAXT = 1024;
 #ifndef SCROLL_ROW_WAVES
 #define SCROLL_ROW_WAVES 8
 #endif
-/* block tasks per thread (about: threads = 24 w / NP rounded up to waves) */
+/* block tasks per thread (about: threads = 24 w / NP rounded up to waves):
+ * 3 for rows up to SCROLL_ROW_WIDE MBs, SCROLL_ROW_NP_WIDE past it.  Config
+ * 3's 25-MB rows: 1.29 ms at 3 against 1.41 at 4 or 5; config 5's 47-MB
+ * rows: 2.72 ms at 4 against 2.86 at 3 and 2.81 at 5 (round 5) */
 #ifndef SCROLL_ROW_NP
 #define SCROLL_ROW_NP 3
+#endif
+#ifndef SCROLL_ROW_NP_WIDE
+#define SCROLL_ROW_NP_WIDE 4
+#endif
+#ifndef SCROLL_ROW_WIDE
+#define SCROLL_ROW_WIDE 40
 #endif
 constexpr int ROW_NPMAX = 8;                    /* tasks per thread at most (1536 tasks / 192) */
 #ifndef SCROLL_ROW_GB
@@ -1291,8 +1300,8 @@ __host__ __device__ inline int row_vtasks(int w) { return row_chroma0(w) + 8 * w
 /* threads of a k_dyn_row workgroup: about SCROLL_ROW_NP block tasks each */
 __host__ __device__ inline int row_threads(int w)
 {
-    const int nt = row_vtasks(w);
-    const int a = (((nt + SCROLL_ROW_NP - 1) / SCROLL_ROW_NP) + 63) & ~63;
+    const int nt = row_vtasks(w), np = w > SCROLL_ROW_WIDE ? SCROLL_ROW_NP_WIDE : SCROLL_ROW_NP;
+    const int a = (((nt + np - 1) / np) + 63) & ~63;
     const int b = (((nt + ROW_NPMAX - 1) / ROW_NPMAX) + 63) & ~63;      /* np <= ROW_NPMAX */
     const int t = a > b ? a : b;
     return t < ROW_MAXT ? t : ROW_MAXT;

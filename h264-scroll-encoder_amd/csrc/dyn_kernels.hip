@@ -1249,9 +1249,27 @@ static_assert(offsetof(RowFixed, lvt) % 8 == 0, "the level table is copied in 8-
  * [8 w] u8 (top TotalCoeffs; from phase 4 on the MBs' bit counts, u32 [w]),
  * cbp / code [w] u8.  (Round 4 kept moff for every column of the picture:
  * 964 bytes more at 4K, config 5's row workgroups needed 33.5 KB) */
-__host__ __device__ inline size_t row_lds_bytes(int w)
+__host__ __device__ inline size_t row_lds_base(int w)
 {
     return (size_t)16 * NPC * w + (size_t)4 * (w + 1) + (size_t)2 * (3 * NPC * w) + (size_t)10 * w + 16;
+}
+/* rows over SCROLL_ROW_WIDE MBs write through a wider bit window of
+ * ROW_GB_WIDE words at the end of the dynamic LDS (when the workgroup still
+ * fits the CU's 160 KB): config 5's 47-MB rows (about 37 Kbit) in one pass
+ * instead of two, 2.70 -> 2.49 ms per launch; config 3 keeps the static
+ * window (its 8 workgroups per CU have no LDS to spare) */
+#ifndef SCROLL_ROW_GB_WIDE
+#define SCROLL_ROW_GB_WIDE 1248
+#endif
+constexpr int ROW_GB_WIDE = SCROLL_ROW_GB_WIDE;
+__host__ __device__ inline size_t row_wide_off(int w) { return (row_lds_base(w) + 15) & ~(size_t)15; }
+__host__ __device__ inline bool row_wide_win(int w)
+{
+    return w > SCROLL_ROW_WIDE && row_wide_off(w) + 4 * (size_t)(ROW_GB_WIDE + ROW_PAD) + sizeof(RowFixed) <= 163840;
+}
+__host__ __device__ inline size_t row_lds_bytes(int w)
+{
+    return row_wide_win(w) ? row_wide_off(w) + 4 * (size_t)(ROW_GB_WIDE + ROW_PAD) : row_lds_base(w);
 }
 
 /* The nC neighbours of piece class pc (0-15 luma raster, 16 / 17 chroma DC,
@@ -1883,6 +1901,9 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
     if (t == 0) gbits[nb * (size_t)ng + gi] = bits;
 
     /* ---- 5: bits -> the row's own row-stage words ------------------------ */
+    const bool wwin = row_wide_win(w);
+    uint32_t *const wb = wwin ? reinterpret_cast<uint32_t *>(reinterpret_cast<uint8_t *>(rdyn) + row_wide_off(w)) : L.buf;
+    const uint32_t GBW = wwin ? (uint32_t)ROW_GB_WIDE : (uint32_t)ROW_GB;
     uint32_t *out = rowstage + nb * g.rs_frame_words + rs_group_words(g, nA, gi);
     uint32_t epc = g.rs_row_words - EPC_ROW;            /* the EP-candidate record in the slot */
     bool lost = false;                                  /* no spill slot: the frame fails (DF_OVER) */
@@ -1906,13 +1927,13 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
         }
     }
     const uint32_t nw = lost ? 0u : min((bits + 31u) >> 5, epc);     /* provable bound: never clipped */
-    const int npass = (int)((nw + ROW_GB - 1) / ROW_GB);
+    const int npass = (int)((nw + GBW - 1) / GBW);
     for (int pi = 0; pi < npass; ++pi) {
-        const uint32_t p0 = (uint32_t)pi * ROW_GB;
-        const uint32_t n = min((uint32_t)ROW_GB, nw - p0);
-        for (uint32_t i = (uint32_t)t; i < n; i += (uint32_t)T) L.buf[i] = 0u;
+        const uint32_t p0 = (uint32_t)pi * GBW;
+        const uint32_t n = min((uint32_t)GBW, nw - p0);
+        for (uint32_t i = (uint32_t)t; i < n; i += (uint32_t)T) wb[i] = 0u;
         __syncthreads();
-        const LdsOrWin win{L.buf, p0, n};
+        const LdsOrWin win{wb, p0, n};
         /* MB heads (+ coded_block_pattern / mb_qp_delta) of every column:
          * in a one-pass row the class's MSB-first bits with the tail ORed
          * in, written as one piece */
@@ -1942,7 +1963,7 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
 #pragma unroll
                     for (uint32_t j = 0; j < 4; ++j)
                         wv[j] |= (j == q ? t32 >> r : 0u) | (j == q + 1u && r ? t32 << (32u - r) : 0u);
-                    put_piece1(L.buf, pos, 0u, 0u, make_uint4(wv[0], wv[1], wv[2], wv[3]), hl + tn);
+                    put_piece1(wb, pos, 0u, 0u, make_uint4(wv[0], wv[1], wv[2], wv[3]), hl + tn);
                     continue;
                 }
             }
@@ -1975,20 +1996,20 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
             const uint4 bd = lv[i];
             if (!(mv & M_OVF)) {
                 if (nC == -1) {                         /* a bare body (token in front since phase 3) */
-                    if (one) put_piece1(L.buf, pos, 0u, 0u, bd, mv & 255u);
-                    else put_piece(L.buf, p0, n, pos, 0u, 0u, bd, mv & 255u);
+                    if (one) put_piece1(wb, pos, 0u, 0u, bd, mv & 255u);
+                    else put_piece(wb, p0, n, pos, 0u, 0u, bd, mv & 255u);
                 } else {                                /* bodies over 128 - tl bits */
                     uint32_t tv = 0, tl = 0;
                     piece_token(ctab, mv, nC, tv, tl);
-                    if (one) put_piece1(L.buf, pos, tv, tl, bd, mv & 255u);
-                    else put_piece(L.buf, p0, n, pos, tv, tl, bd, mv & 255u);
+                    if (one) put_piece1(wb, pos, tv, tl, bd, mv & 255u);
+                    else put_piece(wb, p0, n, pos, tv, tl, bd, mv & 255u);
                 }
             } else {
-                ovf_put(L.buf, p0, n, pos, PT, TB, bd, ovf_wide(k, pc), pc, nC);
+                ovf_put(wb, p0, n, pos, PT, TB, bd, ovf_wide(k, pc), pc, nC);
             }
         }
         __syncthreads();
-        flush_window(L.buf, n, p0, p0 + n >= nw, out, &L.ncand, out + epc, EPC_ROW - 1, t, T);
+        flush_window(wb, n, p0, p0 + n >= nw, out, &L.ncand, out + epc, EPC_ROW - 1, t, T);
         __syncthreads();
     }
     if (t == 0 && !lost) out[epc] = L.ncand;

@@ -68,6 +68,12 @@ WORKLOADS = {
                    desc="BASELINE config 5 per GPU: 128 concurrent 3840x2160 streams (1024 over 8 "
                         "GPUs) + 720x720 dynamic rect (47x47 MBs, +16 px margin); the scroll passes "
                         "496/992/1488/1984 -> up to 6 reference pictures"),
+    "p720full": dict(w=1280, h=720, streams=256, frames=4, rect=(0, 0, 80, 45), rect_px="1280x720",
+                     metric="composed frames/sec (1280x720, whole-frame residual: the conventional-encode "
+                            "fallback); bit-exact vs CPU",
+                     desc="the conventional-encode fallback (docs/MASTER_DESIGN.md:220): 256 concurrent "
+                          "1280x720 streams, every scroll frame's whole picture (80x45 MBs) through the "
+                          "residual coder (4x4 int transform + quant + CAVLC) over the scroll motion"),
     "p720": dict(w=1280, h=720, streams=256, frames=1024, rect=None,
                  desc="BASELINE config 2: 256 concurrent 1280x720 streams, P-only "
                       "(no dynamic rect), composer_write_scroll_frame semantics"),
@@ -434,6 +440,12 @@ def max_over_ranks(x, dist):
     return float(t.item())
 
 
+def rect_label(wl):
+    """'360x360' for a square rect of rect_px pixels, else rect_px itself"""
+    r = wl.get("rect_px")
+    return f"{r}x{r}" if isinstance(r, int) else str(r)
+
+
 def cpu_baseline(wl, threads):
     """Oracle (C restatement, bit-exact to the reference) on host cores."""
     repo_oracle = os.path.join(HERE, "oracle")
@@ -454,7 +466,7 @@ def cpu_baseline(wl, threads):
                                         ctypes.byref(nbytes))
         return dict(value=round(fps, 1), unit="frames/s", cores=threads, kind="port",
                     sample=f"{nstreams} streams x {nframes} frames {wl['w']}x{wl['h']} + "
-                           f"{wl['rect_px']}x{wl['rect_px']} dynamic rect ({rw}x{rh} MBs; same synthetic offsets, 4 source "
+                           f"{rect_label(wl)} dynamic rect ({rw}x{rh} MBs; same synthetic offsets, 4 source "
                            f"frames cycled per stream), {threads} pthreads, "
                            f"oracle/dyn_oracle.c -O2",
                     single_core_fps=round(fps1, 1))
@@ -822,17 +834,27 @@ def usable_cores():
 
 
 def revision():
-    """the source revision of this tree (.revision written before a GPU run,
-    else git)"""
+    """the source revision of this tree: git's HEAD (+ "-dirty" with
+    uncommitted changes to tracked files) where the tree has its .git, else
+    the .revision file written on the build host before a GPU run (the
+    snapshot on the GPU box has no .git).  A stale .revision never shadows
+    git."""
+    if os.path.isdir(os.path.join(HERE, ".git")):
+        try:
+            import subprocess
+            head = subprocess.run(["git", "-C", HERE, "rev-parse", "HEAD"], capture_output=True,
+                                  text=True, timeout=10).stdout.strip()
+            dirty = subprocess.run(["git", "-C", HERE, "status", "--porcelain", "--untracked-files=no"],
+                                   capture_output=True, text=True, timeout=10).stdout.strip()
+            if head:
+                return head + ("-dirty" if dirty else "")
+        except Exception:
+            pass
     p = os.path.join(HERE, ".revision")
     if os.path.exists(p):
-        return open(p).read().split()[0]
-    try:
-        import subprocess
-        return subprocess.run(["git", "-C", HERE, "rev-parse", "HEAD"], capture_output=True,
-                              text=True, timeout=10).stdout.strip() or None
-    except Exception:
-        return None
+        w = open(p).read().split()
+        return (w[0] + ("-dirty" if "dirty" in w[1:] else "")) if w else None
+    return None
 
 
 def launch_ranks(n):
@@ -987,7 +1009,7 @@ def main():
         achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
         traffic = load_traffic(args.workload, kern, alg_bytes)
         out = {
-            "metric": METRIC,
+            "metric": wl.get("metric", METRIC),
             "value": round(value, 1),
             "unit": "frames/s",
             "n_gpus": world,

@@ -1243,6 +1243,21 @@ int scroll_batch_set_config(ScrollBatch *b, int s, const ComposerConfig *cfg)
     rc = batch_host_sync(b);
     if (rc) return rc;
     DevStream *d = &b->h_st[s];
+    if (!cfg->deblocking_filter_control_present_flag) {
+        /* the guard of add_stream / set_dyn_qp*: the loop filter on keeps the
+         * stream's rect, and every per-frame rect QP of it, at 26 */
+        bool bad = d->dyn_qp != 26;
+        const size_t F = (size_t)b->max_frames, i0 = (size_t)s * F;
+        for (size_t f = 0; !bad && f < F && i0 + f < b->h_dyn_qp.size(); ++f) {
+            const int q = b->h_dyn_qp[i0 + f];
+            bad = q >= 0 && q != 26;
+        }
+        if (bad) {
+            set_err("scroll_batch_set_config: stream %d's rect QP is not 26: it cannot turn the deblocking "
+                    "filter on (no deblocking_filter_control_present_flag)", s);
+            return SCROLL_ERR_CONFIG;
+        }
+    }
     cfg_to_dev(cfg, d);
     HIPCHK(hipSetDevice(b->device));
     HIPCHK(hipMemcpy(b->d_st + s, d, sizeof(DevStream), hipMemcpyHostToDevice));
@@ -2843,7 +2858,11 @@ int scroll_batch_ingest_device(ScrollBatch *b, int n, const uint8_t *d_files, co
     for (int k = 0; k < n; ++k) {
         if (outs[k].err != ING_OK) {
             set_err("scroll_batch_ingest: new stream %d: %s", k, ing_msg(outs[k].err));
-            return outs[k].err == ING_ERR_OVERFLOW ? SCROLL_ERR_OVERFLOW : SCROLL_ERR_CONFIG;
+            /* a segment's bounded look-back wait is a device hand-off failure,
+             * not a bad file (as k_dyn_row's DF_HANDOFF) */
+            return outs[k].err == ING_ERR_OVERFLOW ? SCROLL_ERR_OVERFLOW
+                   : outs[k].err == ING_ERR_WAIT   ? SCROLL_ERR_DEVICE
+                                                   : SCROLL_ERR_CONFIG;
         }
         if ((b->dyn_on && (outs[k].w != b->dyn_pw || outs[k].h != b->dyn_ph)) ||
             (b->hint_on && ((outs[k].w / 16) * (outs[k].h / 16) > b->hint_max_mb ||
@@ -2857,6 +2876,15 @@ int scroll_batch_ingest_device(ScrollBatch *b, int n, const uint8_t *d_files, co
      * after composer_write_header */
     const int s0 = b->nstreams;
     for (int k = 0; k < n; ++k) {
+        /* the rule add_stream enforces: the loop filter on (no
+         * deblocking_filter_control_present_flag) keeps the rect at QP 26 */
+        if (b->dyn_qp != 26 && !outs[k].deblock) {
+            set_err("scroll_batch_ingest: new stream %d has the deblocking filter on (no "
+                    "deblocking_filter_control_present_flag); the batch's rect QP is %d, not 26", k, b->dyn_qp);
+            return SCROLL_ERR_CONFIG;
+        }
+    }
+    for (int k = 0; k < n; ++k) {
         ComposerConfig cfg;
         composer_config_init(&cfg, outs[k].w, outs[k].h);
         composer_config_set_sps_params(&cfg, 4, 2, 4);
@@ -2866,6 +2894,7 @@ int scroll_batch_ingest_device(ScrollBatch *b, int n, const uint8_t *d_files, co
         DevStream *d = &b->h_st[s0 + k];
         memset(d, 0, sizeof(*d));
         cfg_to_dev(&cfg, d);
+        d->dyn_qp = b->dyn_qp;              /* the batch's rect QP, as add_stream sets it */
         d->out_pos = outs[k].bytes;
         d->undelivered = outs[k].bytes;     /* SPS + PPS + A + B go out with the first delivery */
         d->out_cap = b->arena_bytes;
@@ -3006,6 +3035,14 @@ static int ipcm_files(ScrollBatch *b, int n, int w, int h, const uint8_t *d_pics
         e0 = b->ipcm_ev[b->ipcm_ev_used];
         e1 = b->ipcm_ev[b->ipcm_ev_used + 1];
         b->ipcm_ev_used += 2;
+    }
+    if (async && b->last && b->last != hs) {
+        /* a compose queued on a caller's stream: own waits for it, so that
+         * b->last = own below still covers it (the next sync must not copy
+         * d_st back while that compose runs) */
+        if (!b->out_ev) HIPCHK(hipEventCreateWithFlags(&b->out_ev, hipEventDisableTiming));
+        HIPCHK(hipEventRecord(b->out_ev, b->last));
+        HIPCHK(hipStreamWaitEvent(hs, b->out_ev, 0));
     }
     if (e0) HIPCHK(hipEventRecord(e0, hs));
     uint64_t *d_sizes = async ? d_sizes_out

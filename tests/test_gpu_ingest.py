@@ -242,3 +242,75 @@ def test_ingest_one_pass_many_streams(gpu, oracle):
     pairs = [variant_files(oracle, w, h, k % 8) for k in range(48)]
     b = check_ingest(gpu, oracle, pairs, nframes=0, arena=8 << 20)
     b.close()
+
+
+def _striped_i420(oracle, w, h, which):
+    from dynhelp import StripedRefs
+    sr = StripedRefs(oracle, w, h)
+    return b"".join(bytes(p) for p in sr.planes[which]), sr
+
+
+def test_ingest_then_dynamic_rect_at_default_qp(gpu, oracle):
+    """ingested streams carry the batch's rect QP (26 by default): composed
+    with the dynamic rect -- ingested before and after scroll_batch_set_dyn_rect
+    -- their bytes are the header the oracle's composer_init +
+    composer_write_header writes, then the oracle's dynamic-rect NALs
+    (oracle/dyn_oracle.c) at QP 26.  (Round 5 left an ingested stream's QP
+    at 0: slice_qp_delta -26 on the general path.)"""
+    from dynhelp import Rect, rect_source
+    from test_gpu_dyn import oracle_streams, synth_source
+    w, h, F = 320, 240, 6
+    rect = Rect(3, 2, 6, 5)
+    a, bb = ref_file(oracle, w, h, 0), ref_file(oracle, w, h, 1)
+    ia, sr = _striped_i420(oracle, w, h, 0)
+    ib, _ = _striped_i420(oracle, w, h, 1)
+    b = gpu.Batch(4, F, 8 << 20)
+    try:
+        assert b.ingest([(a, bb)]) == 0                  # before the rect exists
+        b.set_dyn_rect(rect.x0, rect.y0, rect.w, rect.h)
+        b.set_dyn_refs(ia, ib)
+        assert b.ingest([(a, bb), (a, bb)]) == 1          # after it
+        S = b.num_streams
+        offs = np.array([[oracle.or_tri(i * 4 + 13 * s, h) for i in range(F)] for s in range(S)], np.int32)
+        src = synth_source(oracle, S, F, rect)
+        b.set_offsets(offs)
+        b.set_dyn_source(np.ascontiguousarray(src).tobytes(), F)
+        b.compose(F)
+        assert b.sync() == 0, gpu.last_error()
+        head = expected(oracle, a, bb, 0)
+        want = oracle_streams(oracle, w, h, offs, rect, src, sr)
+        for s in range(S):
+            got = b.output(s)
+            assert got[:len(head)] == head, s
+            assert got[len(head):] == want[s], (s, len(got) - len(head), len(want[s]))
+    finally:
+        b.close()
+
+
+def test_ingest_deblocking_stream_keeps_rect_qp_26(gpu, oracle, scroll):
+    """a file whose PPS lacks deblocking_filter_control_present_flag (the
+    loop filter on) cannot join a batch whose rect QP is not 26 (the rule
+    add_stream enforces); nothing is added.  scroll_batch_set_config cannot
+    turn the filter on for a stream whose rect QP is not 26."""
+    w, h = 320, 240
+    good = (ref_file(oracle, w, h, 0), ref_file(oracle, w, h, 1))
+    nodb = variant_files(oracle, w, h, 1)                # deblock 0 in its PPS
+    b = gpu.Batch(4, 2, 8 << 20)
+    try:
+        assert b.ingest([good]) == 0
+        b.set_dyn_rect(1, 1, 2, 2)
+        b.set_dyn_qp(30)
+        with pytest.raises(RuntimeError):
+            b.ingest([good, nodb])
+        assert "deblocking" in gpu.last_error() and b.num_streams == 1
+        assert b.ingest([good]) == 1                      # a file with the flag joins at QP 30
+        c = b.config(1)
+        c.deblocking_filter_control_present_flag = 0
+        with pytest.raises(RuntimeError):
+            b.set_config(1, c)
+        assert "deblocking" in gpu.last_error()
+        b.set_dyn_qp(26)
+        b.set_config(1, c)                                # at QP 26 it may
+        assert b.config(1).deblocking_filter_control_present_flag == 0
+    finally:
+        b.close()

@@ -250,3 +250,51 @@ def test_async_entry_matches_and_reports_overflow_at_sync(gpu, hip, oracle, scro
         dev.free()
         out.free()
         dsz.free()
+
+
+def test_async_after_compose_on_caller_stream(gpu, hip, oracle):
+    """a compose queued on the caller's (non-blocking) HIP stream, then the
+    asynchronous I_PCM entry on the batch's own stream, then one sync: the
+    sync covers the compose too (own waits for it), so every stream's output
+    is the oracle's whole, and the files are the oracle's"""
+    import random
+    from test_gpu_parity import _oracle_stream
+    L = hip.lib
+    L.hipStreamCreateWithFlags.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint]
+    L.hipStreamCreateWithFlags.restype = ctypes.c_int
+    L.hipStreamDestroy.argtypes = [ctypes.c_void_p]
+    cs = ctypes.c_void_p()
+    assert L.hipStreamCreateWithFlags(ctypes.byref(cs), 1) == 0        # hipStreamNonBlocking
+    w, h, S, F = 1280, 720, 64, 256
+    rng = random.Random(5)
+    offs = np.array([[rng.randint(0, h) for _ in range(F)] for _ in range(S)], np.int32)
+    pw, ph = 176, 144
+    pics = pictures(pw, ph, ["rand", "sparse"], seed=2)
+    n, psz = len(pics), pw * ph * 3 // 2
+    stride = (psz + 255) // 256 * 256
+    want_f = [ipcm_file(oracle, pw, ph, p) for p in pics]
+    ostride = (max(len(f) for f in want_f) + 255) // 256 * 256
+    dev, out, dsz = hip.buf(n * stride), hip.buf(n * ostride, 0xAB), hip.buf(8 * n)
+    b = gpu.Batch(S, F, 4 << 20, device=0)
+    try:
+        for i, p in enumerate(pics):
+            dev.write(i * stride, p)
+        for _ in range(S):
+            b.add_stream(gpu.make_config(w, h))
+        b.set_offsets(offs)
+        b.compose(F, stream=cs.value)
+        b.ipcm_files_device_async(n, pw, ph, dev.p, stride, out.p, ostride, dsz.p)
+        assert b.sync() == 0, gpu.last_error()
+        for s in range(S):
+            assert b.output_size(s) == len(_oracle_stream(oracle, w, h, offs[s])[0]), s
+        for s in (0, S // 2, S - 1):
+            assert b.output(s) == _oracle_stream(oracle, w, h, offs[s])[0], s
+        host = out.read()
+        for i in range(n):
+            assert host[i * ostride:i * ostride + len(want_f[i])].tobytes() == want_f[i]
+    finally:
+        b.close()
+        dev.free()
+        out.free()
+        dsz.free()
+        L.hipStreamDestroy(cs)

@@ -53,6 +53,23 @@ __device__ uint32_t g_tzrb[TZRB_N];
  * CAVLC phase */
 __constant__ LvTab g_lvt = make_lvt();
 
+/* the quantiser at every rect QP, luma and chroma (QPc, Table 8-15): one
+ * uniform index -> scalar loads (qparams_rt's six-way selects compiled to a
+ * branch maze per workgroup) */
+struct QpPair {
+    QParams l, c;
+};
+struct QpTab {
+    QpPair q[QP_MAX + 1];
+};
+constexpr QpTab make_qptab()
+{
+    QpTab T{};
+    for (int i = 0; i <= QP_MAX; ++i) T.q[i] = QpPair{qparams(i), qparams(qp_chroma(i))};
+    return T;
+}
+__constant__ QpTab g_qptab = make_qptab();
+
 __global__ __launch_bounds__(256) void k_tzrb_init()
 {
     const int i = blockIdx.x * 256 + threadIdx.x;
@@ -1392,6 +1409,18 @@ __device__ inline void fetch_pass(const FetchOff &o, bool luma, uint32_t adv, ui
     }
     px.c = luma ? 0u : __builtin_amdgcn_raw_buffer_load_b32(rb, o.c, adv, 0);
 }
+/* the same with the ninth load for luma too (o.c = o.b[3]; its value unused):
+ * every pass issues nine loads (k_dyn_row's counted waits) */
+__device__ inline void fetch_pass9(const FetchOff &o, uint32_t adv, uint32_t stride, __amdgpu_buffer_rsrc_t fs,
+                                   __amdgpu_buffer_rsrc_t rb, BlkPix &px)
+{
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        px.a[i] = __builtin_amdgcn_raw_buffer_load_b32(fs, o.s, adv + (uint32_t)i * stride, 0);
+        px.b[i] = __builtin_amdgcn_raw_buffer_load_b32(rb, o.b[i], adv, 0);
+    }
+    px.c = __builtin_amdgcn_raw_buffer_load_b32(rb, o.c, adv, 0);
+}
 
 /* ((8 - f) b + f c + 4) >> 3 for the four bytes of b, c: even and odd bytes
  * as two 16-bit halves each (at most 2,044: no carry between halves), two
@@ -1507,12 +1536,12 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
         if (k0 == 0) {
             fetch_luma(fo, t, r, g, rtg + 16 * r);
             fo.pb = 0;
-            fetch_pass(fo, true, 0u, (uint32_t)(16 * w), fs, rb, nx);
+            fetch_pass9(fo, 0u, (uint32_t)(16 * w), fs, rb, nx);
         } else if (k0 == 1) {
             fetch_chroma(fo, t - L0, r, g, csz, rtg + 16 * g.h + 8 * r, rtg + 24 * g.h + 8 * r);
             fo.pb = 0;
             fo_chroma = true;
-            fetch_pass(fo, false, 0u, (uint32_t)(8 * w), fs, rb, nx);
+            fetch_pass9(fo, 0u, (uint32_t)(8 * w), fs, rb, nx);
         }
     }
     const DynFrame df = dfr[nb];
@@ -1562,7 +1591,8 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
         const uint32_t frc = __builtin_amdgcn_readfirstlane((L.rt[16] >> 28) & 7u);
         /* the stream's rect QP (QP_MIN and up here: int8 levels) */
         const int qpy = __builtin_amdgcn_readfirstlane(S->dyn_qp);
-        const QParams ql = qparams_rt(qpy), qc = qparams_rt(qp_chroma(qpy));
+        const QParams ql = g_qptab.q[qpy].l, qc = g_qptab.q[qpy].c;
+#ifdef SCROLL_ROW_LVOLD
         auto issue = [&](int q, BlkPix &px) {
             const int kd = kind_of(q);
             if (kd == 2) return;
@@ -1637,6 +1667,106 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
             if (pa + 1 < np) issue(pa + 1, nx);
             compute(pa, cur);
         }
+#else
+        /* round 6: a wave's passes are luma ones, then chroma ones, then
+         * none (L0 and T are multiples of 64), so two loops whose kind is
+         * known at compile time: no per-pass kind tests, and the compiler
+         * schedules the next pass's loads and this pass's coding as one
+         * straight block.  The next pass's loads are in flight while this
+         * one is coded; qL / qC: this wave's luma / luma + chroma passes */
+        const int qL = nl > wv0 ? (nl - wv0 + T - 1) / T : 0;
+        const int qC = ntv > wv0 ? (ntv - wv0 + T - 1) / T : 0;
+        auto issue_l = [&](int q, BlkPix &px) {
+            fetch_pass9(fo, (uint32_t)((q - fo.pb) * T), (uint32_t)(16 * w), fs, rb, px);
+        };
+        auto issue_c = [&](int q, BlkPix &px) {
+            if (!fo_chroma) {
+                fetch_chroma(fo, q * T + t - L0, r, g, csz, L.rt + 16, L.rt + 24);
+                fo.pb = q;
+                fo_chroma = true;
+            }
+            fetch_pass9(fo, (uint32_t)((q - fo.pb) * T), (uint32_t)(8 * w), fs, rb, px);
+        };
+        /* the loads of pass q: luma, else chroma -- past the wave's tasks
+         * too (offsets in the descriptors' ranges or read as 0 past them,
+         * never used): every path issues the same nine loads, so the wait
+         * for the other set before its coding counts nine, not zero */
+        auto issue_any = [&](int q, BlkPix &px) {
+            if (q < qL) issue_l(q, px);
+            else issue_c(q, px);
+        };
+        /* a level record: packed levels, TotalCoeff, its rank in its class
+         * (counting sort: the order inside a class does not matter) */
+        auto put_rec = [&](int slot, const uint32_t pk[4]) {
+            const int n = nz_bytes(pk[0]) + nz_bytes(pk[1]) + nz_bytes(pk[2]) + nz_bytes(pk[3]);
+            lv[slot] = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+            mt[slot] = (uint16_t)((uint32_t)min(n, 16) << 8);
+            lo[slot] = (uint16_t)atomicAdd(&L.kc[0][SORT_KEYS - 1 - min(n, SORT_KEYS - 1)], 1u);
+        };
+        auto code_l = [&](int q, const BlkPix &px) {
+            const int v = q * T + t;
+            uint32_t pk[4];
+            int w0 = 0;
+            levels_pk<true>(px.a, px.b, pk, w0, ql);
+            if (v < nl) put_rec((int)__umul24((uint32_t)(v >> 4), (uint32_t)NPC) + (v & 15), pk);
+        };
+        auto code_c = [&](int q, const BlkPix &px) {
+            const int e = q * T + t - L0;                   /* chroma task index */
+            uint32_t pr[4], pk[4];
+            int w0 = 0;
+            if (frc == 4u) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) pr[i] = __builtin_amdgcn_lerp(px.b[i], i < 3 ? px.b[i + 1] : px.c, 0x01010101u);
+            } else if (frc == 0u) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) pr[i] = px.b[i];
+            } else {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) pr[i] = bilin4(px.b[i], i < 3 ? px.b[i + 1] : px.c, frc);
+            }
+            levels_pk<false>(px.a, pr, pk, w0, qc);
+            const bool ok = e < 8 * w;
+            if (ok) put_rec((int)__umul24((uint32_t)(e >> 3), (uint32_t)NPC) + 18 + (e & 7), pk);
+            /* chroma DC: the quad's four DC coefficients -> 2x2 Hadamard,
+             * quant -> levels as int16 in the DC slot (quads are lane-aligned) */
+            const int qb = lane & ~3;
+            const int d0 = __shfl(w0, qb, 64), d1 = __shfl(w0, qb + 1, 64);
+            const int d2 = __shfl(w0, qb + 2, 64), d3 = __shfl(w0, qb + 3, 64);
+            if (ok && (e & 3) == 0) {
+                const int k = e >> 3, p = (e >> 2) & 1;
+                const int q0 = quant_dc(d0 + d1 + d2 + d3, qc), q1 = quant_dc(d0 - d1 + d2 - d3, qc);
+                const int q2 = quant_dc(d0 + d1 - d2 - d3, qc), q3 = quant_dc(d0 - d1 - d2 + d3, qc);
+                lv[k * NPC + 16 + p] = make_uint4(((uint32_t)q0 & 0xffffu) | (uint32_t)q1 << 16,
+                                                  ((uint32_t)q2 & 0xffffu) | (uint32_t)q3 << 16, 0u, 0u);
+                mt[k * NPC + 16 + p] = (uint16_t)((uint32_t)((q0 != 0) + (q1 != 0) + (q2 != 0) + (q3 != 0)) << 8);
+            }
+        };
+        /* two pixel sets in fixed roles (the passes unrolled by two): pass
+         * q + 1's loads go into one while pass q is coded from the other --
+         * no register copies between passes.  pass 0's loads are in flight */
+        BlkPix A = nx, B;
+        int q = 0;
+        for (; q + 1 < qL; q += 2) {
+            issue_l(q + 1, B);
+            code_l(q, A);
+            issue_any(q + 2, A);
+            code_l(q + 1, B);
+        }
+        if (q < qL) {                                       /* an odd luma pass left */
+            issue_any(q + 1, B);
+            code_l(q, A);
+            A = B;                                          /* once: the first chroma pass */
+            ++q;
+        }
+        for (; q + 1 < qC; q += 2) {
+            issue_c(q + 1, B);
+            code_c(q, A);
+            issue_c(q + 2, A);                              /* past the tasks: nine unused loads */
+            code_c(q + 1, B);
+        }
+        if (q < qC) code_c(q, A);
+        (void)np;
+#endif
         __syncthreads();                                /* levels, TotalCoeffs, ptabs, counts */
         if (stp) stp[1] = __builtin_amdgcn_s_memrealtime();
         /* the row's bottom TotalCoeffs (luma 12-15, chroma AC raster 2, 3 of

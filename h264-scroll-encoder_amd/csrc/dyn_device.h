@@ -1155,10 +1155,23 @@ __device__ __host__ inline int cavlc_body_t(CAP &cap, const int8_t *lb, uint32_t
     /* the level class (lvt_entry): suffixLength, +7 for the first level
      * after fewer than three trailing ones */
     int cls = ((tc > 10 && t1 < 3) ? 1 : 0) + (t1 < 3 ? 7 : 0);
+    /* the next level's byte is read one iteration ahead, so each level
+     * waits for one LDS round trip (its codeword) instead of two; past the
+     * last level m is 0 and the read is the guard byte lb[-1] (unused) */
+#ifndef SCROLL_CAVLC_NOPF
+    int pn = top_bit(m);
+    int vn = (int)lb[pn];
     for (int k = t1; k < tc; ++k) {                        /* levels below the trailing ones */
+        const int v = vn;
+        m &= ~(1u << pn);
+        pn = top_bit(m);
+        vn = (int)lb[pn];
+#else
+    for (int k = t1; k < tc; ++k) {
         const int p = top_bit(m);
         m &= ~(1u << p);
         const int v = (int)lb[p];
+#endif
         uint32_t e;
         if (v >= -LVT_V && v <= LVT_V) {
             e = lvt[cls * LVT_W + v + LVT_V + 1];

@@ -1414,6 +1414,17 @@ __device__ inline void fetch_pass(const FetchOff &o, bool luma, uint32_t adv, ui
 __device__ inline void fetch_pass9(const FetchOff &o, uint32_t adv, uint32_t stride, __amdgpu_buffer_rsrc_t fs,
                                    __amdgpu_buffer_rsrc_t rb, BlkPix &px)
 {
+#ifdef SCROLL_ABL_NOLOAD
+    /* profiling variant only: no pixel loads (values from the offsets), the
+     * ceiling of any change to how the pixels are fetched */
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        px.a[i] = (o.s + adv + (uint32_t)i * stride) * 0x9e3779b1u;
+        px.b[i] = (o.b[i] + adv) * 0x85ebca6bu;
+    }
+    px.c = o.c + adv;
+    return;
+#endif
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         px.a[i] = __builtin_amdgcn_raw_buffer_load_b32(fs, o.s, adv + (uint32_t)i * stride, 0);

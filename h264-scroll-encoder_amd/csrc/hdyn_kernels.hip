@@ -103,7 +103,11 @@ __global__ __launch_bounds__(HD_T) void k_hdyn_code(const DevStream *__restrict_
     const SpliceFrame SF = spf[fi];
     if (SF.w <= 0) return;                                  /* no rect in this frame */
     const HintFrame H = hf[fi];
-    const int nr = min((int)H.n, SCROLL_HINT_MAX_RECTS);
+    /* the fallback (k_hint_fb): a dormant whole-picture region (SF.pad 1)
+     * codes only in a frame that falls back, whose hint rects are dropped */
+    const bool fb = (H.mode & HINT_MODE_FB) != 0;
+    if ((SF.pad & 1) && !fb) return;
+    const int nr = fb ? 0 : min((int)H.n, SCROLL_HINT_MAX_RECTS);
     if (t < 8) {
         L.wo[t] = pend[s].wo[t];
         L.wl[t] = pend[s].wl[t];

@@ -18,5 +18,10 @@ int hint_launch_stage(hipStream_t hs, int nframes, int S, DevStream *st, const N
                       int ld_nal, const PlanPending *pend, DynFrame *dfr, int ld_fr,
                       const HintFrame *hf, const ScrollHintRect *pool, uint8_t *stage,
                       uint64_t slot_bytes);
+/* the conventional-encode fallback: frames whose hints name a reference the
+ * frame lacks get HintFrame.mode |= HINT_MODE_FB (the others have it cleared) */
+int hint_launch_fb(hipStream_t hs, int nframes, int S, const DevStream *st, const NalDesc *nal, int ld_nal,
+                   const PlanPending *pend, const DynFrame *dfr, int ld_fr, HintFrame *hf,
+                   const ScrollHintRect *pool);
 /* staging bytes per frame that no hinted NAL of an mbw x mbh picture exceeds */
 size_t hint_slot_bound(int mbw, int mbh);

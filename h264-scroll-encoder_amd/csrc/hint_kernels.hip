@@ -74,7 +74,7 @@ __global__ __launch_bounds__(DT) void k_hint_stage(DevStream *__restrict__ st,
     const int j = DF->nal;
     if (j < 0) return;                                     /* experiment mode: no scroll NAL */
     const HintFrame H = hf[(size_t)s * ld_fr + f];
-    if (H.mode & HINT_MODE_SPLICED) return;                /* k_splice_stage's frame */
+    if (H.mode & (HINT_MODE_SPLICED | HINT_MODE_FB)) return;   /* k_splice_stage's frame */
     const int nr = min((int)H.n, SCROLL_HINT_MAX_RECTS);
     const int hmode = H.mode & 0xff;
     const bool pskip = hmode == SCROLL_HINT_PSKIP;
@@ -261,7 +261,78 @@ __global__ __launch_bounds__(DT) void k_hint_stage(DevStream *__restrict__ st,
     }
 }
 
+/* The conventional-encode fallback (docs/MASTER_DESIGN.md:220, "hints
+ * missing/inconsistent -> full conventional encode"; scroll_batch_set_fallback):
+ * one workgroup per scroll NAL, before the stage kernels.  A frame whose hint
+ * record has an MB on a rect naming a reference the frame lacks -- the frames
+ * that fail their stream with SCROLL_ERR_CONFIG otherwise -- is marked
+ * HINT_MODE_FB: k_hint_stage leaves it, k_hdyn_code codes its whole picture
+ * (the batch's rect is the picture) over the scroll frame's own motion (its
+ * hint rects dropped) and k_splice_stage composes it in the frame's hint
+ * mode.  The bit is the device's: set or cleared here every compose. */
+__global__ __launch_bounds__(DT) void k_hint_fb(const DevStream *__restrict__ st,
+                                                const NalDesc *__restrict__ nal, int ld_nal,
+                                                const PlanPending *__restrict__ pend,
+                                                const DynFrame *__restrict__ dfr, int ld_fr,
+                                                HintFrame *__restrict__ hf,
+                                                const ScrollHintRect *__restrict__ pool)
+{
+    __shared__ ScrollHintRect rc[SCROLL_HINT_MAX_RECTS];
+    __shared__ int32_t wv[8];
+    __shared__ int32_t any;
+    const int s = blockIdx.y, f = blockIdx.x, t = threadIdx.x;
+    const size_t fi = (size_t)s * ld_fr + f;
+    const HintFrame H = hf[fi];
+    const int j = dfr[fi].nal;
+    const int nr = min((int)H.n, SCROLL_HINT_MAX_RECTS);
+    bool bad = false;
+    if (j >= 0 && nr > 0) {                                /* uniform */
+        if (t < nr) rc[t] = pool[H.first + t];
+        if (t < 8) wv[t] = pend[s].wv[t];
+        if (t == 0) any = 0;
+        __syncthreads();
+        const DevStream *S = st + s;
+        const NalDesc d = nal[(size_t)s * ld_nal + j];
+        NalCtx c;
+        c.w = S->w;
+        c.h = S->h;
+        c.log2_mfn = S->log2_mfn;
+        c.poc_type = S->poc_type;
+        c.log2_poc = S->log2_poc;
+        c.deblock = S->deblock;
+        c.kind = d.kind;
+        c.off = d.off;
+        c.frame_num = d.frame_num;
+        c.nwp = d.nwp;
+        const Regions rg = regions(c);
+        const Layout lay{(c.h - c.off) / 16, rg.ra, 4 * rg.mva, rg.rb, 4 * rg.mvb};
+        const int mbw = c.w / 16, nmb = mbw * (c.h / 16);
+        bool my = false;
+        for (int m = t; m < nmb; m += DT) {
+            bool b1;
+            (void)field(rc, wv, nr, m % mbw, m / mbw, lay, c.nwp, b1);
+            my |= b1;
+        }
+        if (my) any = 1;
+        __syncthreads();
+        bad = any != 0;
+    }
+    if (t == 0) {
+        const int32_t mode = bad ? (H.mode | HINT_MODE_FB) : (H.mode & ~HINT_MODE_FB);
+        if (mode != H.mode) hf[fi].mode = (int16_t)mode;
+    }
+}
+
 }  // namespace
+
+int hint_launch_fb(hipStream_t hs, int nframes, int S, const DevStream *st, const NalDesc *nal, int ld_nal,
+                   const PlanPending *pend, const DynFrame *dfr, int ld_fr, HintFrame *hf,
+                   const ScrollHintRect *pool)
+{
+    if (nframes <= 0 || S <= 0) return 0;
+    hipLaunchKernelGGL(k_hint_fb, dim3(nframes, S), dim3(DT), 0, hs, st, nal, ld_nal, pend, dfr, ld_fr, hf, pool);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
 
 int hint_launch_stage(hipStream_t hs, int nframes, int S, DevStream *st, const NalDesc *nal,
                       int ld_nal, const PlanPending *pend, DynFrame *dfr, int ld_fr,

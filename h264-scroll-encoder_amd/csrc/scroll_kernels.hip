@@ -949,6 +949,7 @@ struct ScrollBatch {
      * every frame's rect MBs are coded by k_hdyn_code into splice records
      * (d_sp_rec, word pool d_sp_rbsp) and composed by k_splice_stage */
     std::vector<int32_t> h_dyn_pos;    /* [2 (s * max_frames + f)]: rect origin, x0 < 0: none */
+    int fallback = 0;                  /* scroll_batch_set_fallback: k_hint_fb before the stage kernels */
     std::vector<int32_t> h_dyn_qp;     /* [s * max_frames + f]: the frame's rect QP under hints, -1: the stream's */
     int dyn_pos_custom = 0;            /* some frame's origin differs from the batch rect */
     int dyn_qp = 26;                   /* the rect's QP (scroll_batch_set_dyn_qp)          */
@@ -1372,6 +1373,12 @@ static int launch(ScrollBatch *b, int nframes, int plan_mode, int nal_max, hipSt
                     return SCROLL_ERR_HIP;
                 }
                 b->sp_parse = 0;
+            }
+            if (b->fallback && b->dyn_on &&
+                hint_launch_fb(hs, nframes, S, b->d_st, b->d_nal, b->ld_nal, b->d_pend, b->d_dfr, ld_fr,
+                               b->d_hf, b->d_pool)) {
+                set_err("k_hint_fb launch: %s", hipGetErrorString(hipGetLastError()));
+                return SCROLL_ERR_HIP;
             }
             if (hint_launch_stage(hs, nframes, S, b->d_st, b->d_nal, b->ld_nal, b->d_pend,
                                   b->d_dfr, ld_fr, b->d_hf, b->d_pool, b->d_stage,
@@ -2031,6 +2038,38 @@ int scroll_batch_set_dyn_rect_at(ScrollBatch *b, int s, int f, int x0, int y0)
     return SCROLL_OK;
 }
 
+/* the conventional-encode fallback (docs/MASTER_DESIGN.md:220): needs the
+ * dynamic rect to be the whole picture, so that every frame's source is a
+ * whole picture a conventional encoder would have */
+int scroll_batch_set_fallback(ScrollBatch *b, int on)
+{
+    if (!b) return SCROLL_ERR_ARG;
+    if (on && (!b->dyn_on || b->geo.x0 != 0 || b->geo.y0 != 0 || b->geo.w != b->dyn_pw / 16 ||
+               b->geo.h != b->dyn_ph / 16)) {
+        set_err("scroll_batch_set_fallback: needs the dynamic rect to be the whole picture "
+                "(scroll_batch_set_dyn_rect(b, 0, 0, width / 16, height / 16, ...))");
+        return SCROLL_ERR_CONFIG;
+    }
+    int rc = batch_host_sync(b);
+    if (rc) return rc;
+    b->fallback = on ? 1 : 0;
+    b->hd_dirty = 1;
+    return SCROLL_OK;
+}
+
+int scroll_batch_fallback_frame(ScrollBatch *b, int s, int f, int *fell_back)
+{
+    if (!b || !fell_back || s < 0 || s >= b->nstreams || f < 0 || f >= b->max_frames) return SCROLL_ERR_ARG;
+    *fell_back = 0;
+    if (!b->hint_on || !b->d_hf) return SCROLL_OK;
+    int rc = batch_host_sync(b);
+    if (rc) return rc;
+    HintFrame H;
+    HIPCHK(hipMemcpy(&H, b->d_hf + (size_t)s * b->max_frames + f, sizeof(H), hipMemcpyDeviceToHost));
+    *fell_back = (H.mode & HINT_MODE_FB) ? 1 : 0;
+    return SCROLL_OK;
+}
+
 /* the general-path record pool and the row-stage spill pool at their
  * bounds (a slot for every NAL / rect row), keeping source and references */
 static int dyn_grow_pools(ScrollBatch *b)
@@ -2289,9 +2328,13 @@ static int hd_upload(ScrollBatch *b)
     for (size_t i = 0; i < S * F; ++i) {
         SpliceFrame &o = spf[i];
         o = SpliceFrame{};
-        if (b->h_dyn_pos[2 * i] < 0) continue;
-        o.x0 = b->h_dyn_pos[2 * i];
-        o.y0 = b->h_dyn_pos[2 * i + 1];
+        const bool dormant = b->h_dyn_pos[2 * i] < 0;
+        if (dormant && !b->fallback) continue;
+        /* the fallback: a frame without the rect keeps a dormant whole-picture
+         * region (pad 1) that k_hdyn_code codes only if k_hint_fb marks it */
+        o.x0 = dormant ? 0 : b->h_dyn_pos[2 * i];
+        o.y0 = dormant ? 0 : b->h_dyn_pos[2 * i + 1];
+        o.pad = dormant ? 1 : 0;
         o.w = b->geo.w;
         o.h = b->geo.h;
         o.rbsp_word = i * nmb * b->hd_mb_words;

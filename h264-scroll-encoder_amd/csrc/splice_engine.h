@@ -19,6 +19,8 @@
 #define SPLICE_REF_INTRA (-2)       /* ref of an intra MB in the motion field:
                                      * available, never matching (8.4.1.3.1)      */
 #define HINT_MODE_SPLICED 0x100     /* HintFrame.mode bit: k_splice_stage stages it */
+#define HINT_MODE_FB 0x200          /* HintFrame.mode bit (device, k_hint_fb): the frame falls back to a
+                                       whole-picture residual coding, its hint rects dropped */
 
 /* unit slots of a spliced picture of nmb MBs: every slice holds an MB, so
  * slice nmb (if any) is the first one that cannot fit and fails the frame */

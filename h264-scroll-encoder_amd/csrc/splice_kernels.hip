@@ -2195,7 +2195,7 @@ __global__ __launch_bounds__(DT) __attribute__((amdgpu_waves_per_eu(SCROLL_STAGE
     const int s = blockIdx.y, f = dyn_frame_of(blockIdx.x, s), t = threadIdx.x;
     const size_t fi = (size_t)s * ld_fr + f;
     const HintFrame H = hf[fi];
-    if (!(H.mode & HINT_MODE_SPLICED)) return;                 /* k_hint_stage's frame */
+    if (!(H.mode & (HINT_MODE_SPLICED | HINT_MODE_FB))) return;   /* k_hint_stage's frame */
     DevStream *S = st + s;
     DynFrame *DF = dfr + fi;
     const int j = DF->nal;
@@ -2212,7 +2212,7 @@ __global__ __launch_bounds__(DT) __attribute__((amdgpu_waves_per_eu(SCROLL_STAGE
     if (t == 0) spf[fi].stage_status = SCROLL_SPLICE_OK;
     const SpliceMbRec *rec = recs + SF.rec_first;
     const uint32_t *rb = rbsp + SF.rbsp_word;
-    const int nr = min((int)H.n, SCROLL_HINT_MAX_RECTS);
+    const int nr = (H.mode & HINT_MODE_FB) ? 0 : min((int)H.n, SCROLL_HINT_MAX_RECTS);   /* fallback: no rects */
     const int hmode = H.mode & 0xff;
     const bool pskip = hmode == SCROLL_HINT_PSKIP;
     const bool spec = hmode != SCROLL_HINT_EXACT;

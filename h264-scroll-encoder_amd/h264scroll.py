@@ -183,6 +183,9 @@ def _load():
                                                       ctypes.c_int]),
         "scroll_batch_set_dyn_source": (ctypes.c_int, [ctypes.c_void_p, u8p, ctypes.c_int]),
         "scroll_batch_set_dyn_rect_at": (ctypes.c_int, [ctypes.c_void_p] + [ctypes.c_int] * 4),
+        "scroll_batch_set_fallback": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+        "scroll_batch_fallback_frame": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                                       ctypes.POINTER(ctypes.c_int)]),
         "scroll_batch_dyn_source_device": (ctypes.c_void_p, [ctypes.c_void_p, P(ctypes.c_size_t),
                                                              P(ctypes.c_size_t)]),
         "scroll_batch_dyn_source_synth": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int,
@@ -633,6 +636,17 @@ class Batch:
         no rect in that frame.  Positions other than set_dyn_rect's need UI
         hints (set_hints) at compose time."""
         self._chk(lib.scroll_batch_set_dyn_rect_at(self.h, s, f, x0, y0), "set_dyn_rect_at")
+
+    def set_fallback(self, on=True):
+        """the conventional-encode fallback (scroll_batch_set_fallback): frames
+        whose hints name a reference they lack are coded as whole P frames"""
+        self._chk(lib.scroll_batch_set_fallback(self.h, 1 if on else 0), "set_fallback")
+
+    def fallback_frame(self, s, f):
+        """1 when frame f of stream s fell back in the last compose"""
+        v = ctypes.c_int()
+        self._chk(lib.scroll_batch_fallback_frame(self.h, s, f, ctypes.byref(v)), "fallback_frame")
+        return v.value
 
     def set_dyn_source(self, src, nframes):
         """src: bytes of [num_streams][nframes][384*w*h]"""

@@ -219,6 +219,25 @@ int scroll_batch_set_dyn_source(ScrollBatch *b, const uint8_t *src, int nframes)
  * Bit-exact definition: oracle/splice_oracle.h or_hint_dyn_scroll_nal.
  * Not combinable with spliced slices (one rect per frame). */
 int scroll_batch_set_dyn_rect_at(ScrollBatch *b, int s, int f, int x0, int y0);
+/* The conventional-encode fallback (docs/MASTER_DESIGN.md:220: "if hints
+ * missing/inconsistent -> full conventional encode"), opt-in:
+ *   scroll_batch_set_fallback(b, 1)   with UI hints and a dynamic rect that
+ *       is the whole picture (set_dyn_rect(b, 0, 0, width / 16, height / 16,
+ *       ...): every frame's source is then a whole picture, as a conventional
+ *       encoder's).  A frame whose hints put an MB on a rect naming a
+ *       reference the frame lacks -- a frame that fails its stream with
+ *       SCROLL_ERR_CONFIG without the flag -- is coded instead as a full
+ *       P frame: its hint rects dropped, every MB on the scroll frame's own
+ *       motion with the residual of the frame's source (the rect at (0, 0),
+ *       whether or not set_dyn_rect_at placed it), in the frame's hint mode
+ *       and rect QP.  Other frames are unchanged.  SCROLL_ERR_CONFIG when the
+ *       rect is not the whole picture.
+ *   scroll_batch_fallback_frame(b, s, f, &on)   after a compose: 1 when
+ *       frame f of stream s fell back.
+ * Bit-exact definition: oracle/splice_oracle.h or_compose_hint_dyn with no
+ * hint rects and the whole-picture rect. */
+int scroll_batch_set_fallback(ScrollBatch *b, int on);
+int scroll_batch_fallback_frame(ScrollBatch *b, int s, int f, int *fell_back);
 uint8_t *scroll_batch_dyn_source_device(ScrollBatch *b, size_t *stream_stride,
                                         size_t *frame_stride);
 int scroll_batch_dyn_source_synth(ScrollBatch *b, int nframes, int stream_base, int t0);

@@ -281,3 +281,83 @@ def test_hinted_rect_qp_per_stream_and_frame(gpu, oracle):
     assert b.sync() == 0, gpu.last_error()
     check_equal(b, want)
     b.close()
+
+
+def test_fallback_whole_frame_on_inconsistent_hints(gpu, oracle, scroll):
+    """scroll_batch_set_fallback (docs/MASTER_DESIGN.md:220: hints
+    inconsistent -> full conventional encode): the rect is the whole picture;
+    streams 1 and 3 get frames whose topmost hint rect names a waypoint the
+    frame lacks.  Those frames -- the ones that fail the stream without the
+    flag -- come out as or_compose_hint_dyn with no hint rects and the
+    whole-picture rect; every other frame (with or without the rect placed,
+    all three hint modes) is the oracle's hinted frame; streams 0 and 2 are
+    untouched.  Without the flag the same batch fails."""
+    w, h, S, F = 320, 240, 4, 8
+    mbw, mbh = w // 16, h // 16
+    offs = synthetic_offsets(S, F, h, first_stream=2)
+    offs[1] = np.clip(np.arange(490, 490 + F), 0, h)        # through the 496 waypoint
+    rc = Rect(0, 0, mbw, mbh)
+    R = striped_refs(oracle, w, h)
+    src = synth_source(oracle, S, F, rc)
+    rng = random.Random(9)
+    pl, bad = {}, set()
+    for s in range(S):
+        for f in range(F):
+            rects = random_hints(rng, mbw, mbh, [0, 1], 4)
+            if s in (1, 3) and f % 3 != 1:
+                rects = rects + [(2, 2, 9, 7, 2 + 6, 16, -32)]   # waypoint 6: never valid here
+                bad.add((s, f))
+            pl[(s, f)] = (rects, rng.choice((EXACT, PSKIP, SPEC)), (0, 0) if rng.random() < 0.35 else None)
+    oracle.or_compose_hint_dyn.restype = ctypes.c_size_t
+    buf = (ctypes.c_uint8 * (16 << 20))()
+    err = ctypes.c_int()
+    want, fell = [], set()
+    for s in range(S):
+        c = OrCfg()
+        oracle.or_cfg_init(ctypes.byref(c), w, h)
+        c.frame_num = 2
+        o = bytearray()
+        for f in range(F):
+            rects, hm, pos = pl[(s, f)]
+            sp = np.ascontiguousarray(src[s, f])
+            arr, n = hint_array(rects)
+            c2 = OrCfg.from_buffer_copy(c)
+            r1 = Rect(0, 0, mbw, mbh) if pos else None
+            k = oracle.or_compose_hint_dyn(buf, len(buf), ctypes.byref(c2), int(offs[s, f]), 0, arr, n, hm,
+                                           ctypes.byref(r1) if r1 else None, sp.ctypes.data_as(ctypes.c_void_p),
+                                           ctypes.byref(R.refs), ctypes.byref(err))
+            if err.value != 0:                                 # inconsistent: the whole frame instead
+                fell.add((s, f))
+                c2 = OrCfg.from_buffer_copy(c)
+                k = oracle.or_compose_hint_dyn(buf, len(buf), ctypes.byref(c2), int(offs[s, f]), 0, None, 0,
+                                               hm, ctypes.byref(Rect(0, 0, mbw, mbh)),
+                                               sp.ctypes.data_as(ctypes.c_void_p), ctypes.byref(R.refs),
+                                               ctypes.byref(err))
+            assert err.value == 0 and k > 0, (s, f)
+            o += bytes(buf[:k])
+            c = c2
+        want.append(bytes(o))
+    assert fell == bad, "the test's invalid rects must be the ones the oracle refuses"
+    b = gpu_batch(gpu, w, h, S, F, (0, 0, mbw, mbh), R)
+    b.set_fallback(True)
+    apply_plan(b, pl, F)
+    b.set_offsets(offs)
+    b.set_dyn_source(src.tobytes(), F)
+    b.compose(F)
+    assert b.sync() == 0, gpu.last_error()
+    check_equal(b, want)
+    for s in range(S):
+        for f in range(F):
+            assert b.fallback_frame(s, f) == ((s, f) in fell), (s, f)
+    b.close()
+    b = gpu_batch(gpu, w, h, S, F, (0, 0, mbw, mbh), R)        # without the flag: the stream fails
+    apply_plan(b, pl, F)
+    b.set_offsets(offs)
+    b.set_dyn_source(src.tobytes(), F)
+    b.compose(F)
+    assert b.sync() == scroll.SCROLL_ERR_CONFIG
+    b.close()
+    b = gpu_batch(gpu, w, h, S, F, (2, 2, 5, 4), R)             # not the whole picture
+    with pytest.raises(RuntimeError):
+        b.set_fallback(True)
+    b.close()

@@ -1155,10 +1155,35 @@ __device__ __host__ inline int cavlc_body_t(CAP &cap, const int8_t *lb, uint32_t
     /* the level class (lvt_entry): suffixLength, +7 for the first level
      * after fewer than three trailing ones */
     int cls = ((tc > 10 && t1 < 3) ? 1 : 0) + (t1 < 3 ? 7 : 0);
-    /* the next level's byte is read one iteration ahead, so each level
-     * waits for one LDS round trip (its codeword) instead of two; past the
-     * last level m is 0 and the read is the guard byte lb[-1] (unused) */
+    /* the level codeword from the table, or (|v| > LVT_V) the arithmetic form */
+    auto level_code = [&](int v, int cl) -> uint32_t {
+        if (v >= -LVT_V && v <= LVT_V) return lvt[cl * LVT_W + v + LVT_V + 1];
+        const int sl = cl >= 7 ? cl - 7 : cl, adj = cl >= 7 ? 2 : 0;
+        const int a = v < 0 ? -v : v;
+        const int code = 2 * a - 2 + (v < 0 ? 1 : 0) - adj;
+        const int lim = sl ? (15 << sl) : 30;
+        const uint32_t mk = (1u << sl) - 1u;
+        uint32_t fv = ((uint32_t)code & mk) | (mk + 1u);
+        uint32_t fl = (uint32_t)((code >> sl) + 1 + sl);
+        const bool e15 = code >= lim, e14 = sl == 0 && code >= 14;
+        fv = e15 ? (uint32_t)(4096 + code - lim) : (e14 ? (uint32_t)(code + 2) : fv);
+        fl = e15 ? 28u : (e14 ? 19u : fl);
+        const int s1 = sl == 0 ? 1 : sl;
+        return fv | fl << 13 | (uint32_t)(s1 + ((a > (3 << (s1 - 1)) && s1 < 6) ? 1 : 0)) << 18;
+    };
 #ifndef SCROLL_CAVLC_NOPF
+    /* round 6: the loop holds the table path only (levels clamped into the
+     * table, a lane whose block has a level past LVT_V flagged), so the rare
+     * arithmetic form costs no exec-mask branch per level; a flagged lane
+     * codes its block again below with it.  The next level's byte is read
+     * one iteration ahead, so each level waits for one LDS round trip (its
+     * codeword) instead of two; past the last level m is 0 and the read is
+     * the guard byte lb[-1] (unused) */
+    const uint32_t m0 = m, an0 = an;
+    const uint64_t acc0 = acc;
+    const int cls0 = cls;
+    const CAP cap0 = cap;
+    bool big = false;
     int pn = top_bit(m);
     int vn = (int)lb[pn];
     for (int k = t1; k < tc; ++k) {                        /* levels below the trailing ones */
@@ -1166,32 +1191,35 @@ __device__ __host__ inline int cavlc_body_t(CAP &cap, const int8_t *lb, uint32_t
         m &= ~(1u << pn);
         pn = top_bit(m);
         vn = (int)lb[pn];
+        const int vc = v < -LVT_V ? -LVT_V : (v > LVT_V ? LVT_V : v);
+        big |= vc != v;
+        const uint32_t e = lvt[cls * LVT_W + vc + LVT_V + 1];
+        push(acc, an, e & 0x1fffu, (e >> 13) & 31u, cap);
+        cls = (int)(e >> 18);
+    }
+    if (big) {                                             /* rare: the block again, exact */
+        m = m0;
+        an = an0;
+        acc = acc0;
+        cls = cls0;
+        cap = cap0;
+        for (int k = t1; k < tc; ++k) {
+            const int p = top_bit(m);
+            m &= ~(1u << p);
+            const uint32_t e = level_code((int)lb[p], cls);
+            push(acc, an, e & 0x1fffu, (e >> 13) & 31u, cap);
+            cls = (int)(e >> 18);
+        }
+    }
 #else
     for (int k = t1; k < tc; ++k) {
         const int p = top_bit(m);
         m &= ~(1u << p);
-        const int v = (int)lb[p];
-#endif
-        uint32_t e;
-        if (v >= -LVT_V && v <= LVT_V) {
-            e = lvt[cls * LVT_W + v + LVT_V + 1];
-        } else {                                           /* rare: the arithmetic form */
-            const int sl = cls >= 7 ? cls - 7 : cls, adj = cls >= 7 ? 2 : 0;
-            const int a = v < 0 ? -v : v;
-            const int code = 2 * a - 2 + (v < 0 ? 1 : 0) - adj;
-            const int lim = sl ? (15 << sl) : 30;
-            const uint32_t mk = (1u << sl) - 1u;
-            uint32_t fv = ((uint32_t)code & mk) | (mk + 1u);
-            uint32_t fl = (uint32_t)((code >> sl) + 1 + sl);
-            const bool e15 = code >= lim, e14 = sl == 0 && code >= 14;
-            fv = e15 ? (uint32_t)(4096 + code - lim) : (e14 ? (uint32_t)(code + 2) : fv);
-            fl = e15 ? 28u : (e14 ? 19u : fl);
-            const int s1 = sl == 0 ? 1 : sl;
-            e = fv | fl << 13 | (uint32_t)(s1 + ((a > (3 << (s1 - 1)) && s1 < 6) ? 1 : 0)) << 18;
-        }
+        const uint32_t e = level_code((int)lb[p], cls);
         push(acc, an, e & 0x1fffu, (e >> 13) & 31u, cap);
         cls = (int)(e >> 18);
     }
+#endif
     /* total_zeros + run_before: the entry's code, len = 31 - ctz */
     const uint32_t tzl = 31u - (uint32_t)__builtin_ctz(tzrb);
     push(acc, an, (tzrb >> 1) >> (31u - tzl), tzl, cap);

@@ -38,8 +38,9 @@ def main():
     ap.add_argument("--alg-bytes", type=float, default=0.0)
     ap.add_argument("--label", default="")
     ap.add_argument("--fetch-scale", type=float, default=2.0,
-                    help="gfx950 FETCH_SIZE correction (2 = wide coalesced reads, the guide's "
-                         "calibrated case; other access widths are uncalibrated)")
+                    help="gfx950 FETCH_SIZE correction: 2, calibrated for 1-, 4-, 8- and 16-byte "
+                         "lanes over whole lines (tools/fetch_calib.cpp, profiles/r06_fetch_calib.json)")
+    ap.add_argument("--revision", default="", help="the source revision measured")
     a = ap.parse_args()
     raw = write = 0.0
     nd = []
@@ -55,7 +56,10 @@ def main():
            "fetch_bytes_per_launch": round(fetch), "write_bytes_per_launch": round(write),
            "hbm_bytes_per_launch": round(fetch + write),
            "method": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes); "
-                     f"FETCH_SIZE x {a.fetch_scale} (gfx950 correction)"}
+                     f"FETCH_SIZE x {a.fetch_scale} (gfx950 correction, calibrated per access width: "
+                     "profiles/r06_fetch_calib.json)"}
+    if a.revision:
+        out["revision"] = a.revision
     if a.alg_bytes:
         out["alg_bytes_per_launch"] = a.alg_bytes
         out["traffic_over_alg"] = round((fetch + write) / a.alg_bytes, 4)

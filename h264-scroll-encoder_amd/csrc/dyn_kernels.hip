@@ -1708,12 +1708,26 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
         };
         /* a level record: packed levels, TotalCoeff, its rank in its class
          * (counting sort: the order inside a class does not matter) */
+#ifdef SCROLL_ROW_OLDREC
         auto put_rec = [&](int slot, const uint32_t pk[4]) {
             const int n = nz_bytes(pk[0]) + nz_bytes(pk[1]) + nz_bytes(pk[2]) + nz_bytes(pk[3]);
             lv[slot] = make_uint4(pk[0], pk[1], pk[2], pk[3]);
             mt[slot] = (uint16_t)((uint32_t)min(n, 16) << 8);
             lo[slot] = (uint16_t)atomicAdd(&L.kc[0][SORT_KEYS - 1 - min(n, SORT_KEYS - 1)], 1u);
         };
+#else
+        /* round 6: mt holds the block's non-zero mask until its CAVLC body
+         * (TotalCoeff = its popcount), so the body phase reads it instead of
+         * deriving it from the levels again */
+        auto put_rec = [&](int slot, const uint32_t pk[4]) {
+            const uint4 p4 = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+            const uint32_t nz = nz_mask16(p4);
+            const int n = __builtin_popcount(nz);
+            lv[slot] = p4;
+            mt[slot] = (uint16_t)nz;
+            lo[slot] = (uint16_t)atomicAdd(&L.kc[0][SORT_KEYS - 1 - min(n, SORT_KEYS - 1)], 1u);
+        };
+#endif
         auto code_l = [&](int q, const BlkPix &px) {
             const int v = q * T + t;
             uint32_t pk[4];
@@ -1738,6 +1752,13 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
             levels_pk<false>(px.a, pr, pk, w0, qc);
             const bool ok = e < 8 * w;
             if (ok) put_rec((int)__umul24((uint32_t)(e >> 3), (uint32_t)NPC) + 18 + (e & 7), pk);
+#ifndef SCROLL_ROW_OLDREC
+            /* chroma DC: the block's DC coefficient (|W0| <= 4080) as int16 i
+             * of its plane's DC slot; the 2x2 Hadamard and quant follow the
+             * loop, once per DC block (round 6: in the loop every chroma lane
+             * ran them, masked to one lane of four) */
+            if (ok) reinterpret_cast<int16_t *>(lv + (e >> 3) * NPC + 16 + ((e >> 2) & 1))[e & 3] = (int16_t)w0;
+#else
             /* chroma DC: the quad's four DC coefficients -> 2x2 Hadamard,
              * quant -> levels as int16 in the DC slot (quads are lane-aligned) */
             const int qb = lane & ~3;
@@ -1751,6 +1772,7 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
                                                   ((uint32_t)q2 & 0xffffu) | (uint32_t)q3 << 16, 0u, 0u);
                 mt[k * NPC + 16 + p] = (uint16_t)((uint32_t)((q0 != 0) + (q1 != 0) + (q2 != 0) + (q3 != 0)) << 8);
             }
+#endif
         };
         /* two pixel sets in fixed roles (the passes unrolled by two): pass
          * q + 1's loads go into one while pass q is coded from the other --
@@ -1789,7 +1811,11 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
 #pragma unroll
             for (int e = 0; e < 8; ++e) {
                 const int pcA = e < 4 ? 12 + e : (e < 6 ? 16 + e : 18 + e);
+#ifdef SCROLL_ROW_OLDREC
                 v |= (uint64_t)(tc_of(mk[pcA]) & 31) << (5 * e);
+#else
+                v |= (uint64_t)__builtin_popcount(mk[pcA]) << (5 * e);    /* the block's non-zero mask */
+#endif
             }
             lb_store(tcx + (nb * R.h + r) * (size_t)w + t, (uint64_t)(epoch & 0xffffffu) << 40 | v);
         }
@@ -1797,15 +1823,28 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
         if (t >= T - 2 * w) {
             const int i = t - (T - 2 * w), k = i >> 1, p = i & 1, sl = k * NPC + 16 + p;
             const uint4 q = lv[sl];
+#ifdef SCROLL_ROW_OLDREC
             const int dq[4] = {(int)(int16_t)(q.x & 0xffffu), (int)(int16_t)(q.x >> 16),
                                (int)(int16_t)(q.y & 0xffffu), (int)(int16_t)(q.y >> 16)};
+#else
+            /* the four DC coefficients of the plane's 4x4 blocks (raster) ->
+             * 2x2 Hadamard, quant (qbits + 1) */
+            const int d0 = (int)(int16_t)(q.x & 0xffffu), d1 = (int)(int16_t)(q.x >> 16);
+            const int d2 = (int)(int16_t)(q.y & 0xffffu), d3 = (int)(int16_t)(q.y >> 16);
+            const int dq[4] = {quant_dc(d0 + d1 + d2 + d3, qc), quant_dc(d0 - d1 + d2 - d3, qc),
+                               quant_dc(d0 + d1 - d2 - d3, qc), quant_dc(d0 - d1 - d2 + d3, qc)};
+#endif
             CapSink cap{0, 0, 0};
             const int tc = cavlc_dc4(cap, L.ptabs, dq);
             if (cap.n <= 128) {
                 mt[sl] = (uint16_t)(cap.n | (uint32_t)tc << 8);
                 lv[sl] = body_msb(cap.hi, cap.lo, cap.n);
             } else {
-                mt[sl] = (uint16_t)((uint32_t)tc << 8 | M_OVF);       /* levels stay in lv */
+                mt[sl] = (uint16_t)((uint32_t)tc << 8 | M_OVF);       /* the levels in lv */
+#ifndef SCROLL_ROW_OLDREC
+                lv[sl] = make_uint4(((uint32_t)dq[0] & 0xffffu) | (uint32_t)dq[1] << 16,
+                                    ((uint32_t)dq[2] & 0xffffu) | (uint32_t)dq[3] << 16, 0u, 0u);
+#endif
             }
         }
         if (t < SORT_KEYS) {                            /* class k = t: its base */
@@ -1821,7 +1860,12 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
         __syncthreads();
         for (int task = t; task < ntask; task += T) {       /* the slot, chroma flagged in bit 15 */
             const int slot = row_slot(task, w);
-            order[L.kc[1][SORT_KEYS - 1 - min(tc_of(mt[slot]), SORT_KEYS - 1)] + lo[slot]] =
+#ifdef SCROLL_ROW_OLDREC
+            const int tcs = tc_of(mt[slot]);
+#else
+            const int tcs = __builtin_popcount(mt[slot]);
+#endif
+            order[L.kc[1][SORT_KEYS - 1 - min(tcs, SORT_KEYS - 1)] + lo[slot]] =
                 (uint16_t)(slot | (task < 16 * w ? 0 : 0x8000));
         }
         __syncthreads();
@@ -1834,13 +1878,16 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
             const uint32_t oe = order[pos];
             const int slot = (int)(oe & 0x7fffu);
             const bool luma = !(oe & 0x8000u);
-            const uint4 v4 = lv[slot];
             CapSink cap{0, 0, 0};
             int t1 = 0;
             bool ok = true;
             /* total_zeros + run_before from the table: the load is in flight
              * during the trailing ones and the level loop */
-            const uint32_t nz = nz_mask16(v4);
+#ifdef SCROLL_ROW_OLDREC
+            const uint32_t nz = nz_mask16(lv[slot]);
+#else
+            const uint32_t nz = mt[slot];                   /* the non-zero mask (levels phase) */
+#endif
             const uint32_t tzrb = g_tzrb[luma ? nz : 65536u + nz];
             const int tc = cavlc_body_t(cap, reinterpret_cast<const int8_t *>(lv + slot), nz, tzrb, t1, ok, L.lvt);
             mt[slot] = ok ? (uint16_t)(cap.n | (uint32_t)tc << 8 | (uint32_t)t1 << 13)
@@ -2941,7 +2988,17 @@ __device__ inline void ep_fix(DevStream *st, DynFrame *DF, size_t nb, int s, con
  * NAL, four NALs per workgroup, 0.138 against 0.086 ms -- each NAL's
  * candidate and seam loops then take several passes of 64 lanes.) */
 constexpr int EPF_LIST = SCROLL_EPF_LIST;
-__global__ __launch_bounds__(EPF_T) void k_dyn_epfix(DevStream *__restrict__ st, DynFrame *__restrict__ dfr,
+/* waves per SIMD the epfix registers target (SCROLL_EPF_WAVES; 0: the
+ * compiler's choice) */
+#ifndef SCROLL_EPF_WAVES
+#define SCROLL_EPF_WAVES 0
+#endif
+#if SCROLL_EPF_WAVES
+#define EPF_ATTR __attribute__((amdgpu_waves_per_eu(SCROLL_EPF_WAVES)))
+#else
+#define EPF_ATTR
+#endif
+__global__ __launch_bounds__(EPF_T) EPF_ATTR void k_dyn_epfix(DevStream *__restrict__ st, DynFrame *__restrict__ dfr,
                                                      int ld_fr, int nframes, DynGeom g,
                                                      const uint32_t *__restrict__ rowstage,
                                                      const uint32_t *__restrict__ gbits, uint8_t *__restrict__ eps,

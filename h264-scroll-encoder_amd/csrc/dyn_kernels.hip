@@ -1977,14 +1977,17 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
     /* one straight path for every piece class: its neighbours from pc_desc
      * (the per-class branches had made every wave run all of them) */
     const int nAe = R.x0 > 0 ? 0 : -1, nBe = row > 0 ? 0 : -1;
-    for (int i = t; i < npc; i += T) {
-        const int k = div_npc(i), pc = i - k * NPC;
-        const uint32_t mv = mt[i], D = L.pcd[pc];
+    /* piece i = k NPC + pc, D = its class's neighbour descriptor */
+    auto token = [&](int i, int k, int pc, uint32_t D) {
+        const uint32_t mv = mt[i];
         const int ia = max(i + (int)(D & 63u) - 32, 0), ib = max(i + (int)((D >> 7) & 63u) - 32, 0);
         const int tA = tc_of(mt[ia]), tB = tc_of(mt[ib]), tT = (int)ta[8 * k + (int)((D >> 14) & 7u)];
         const int nA = ((D & 64u) && k == 0) ? nAe : tA;
         const int nB = (D & 8192u) ? (r > 0 ? tT : nBe) : tB;
-        const int nC0 = (nA >= 0 && nB >= 0) ? (nA + nB + 1) >> 1 : max(max(nA, nB), 0);
+        /* both available: their rounded mean, else the available one (9.2.1);
+         * as selects, no divergent branch */
+        const int mean = (nA + nB + 1) >> 1, one = max(max(nA, nB), 0);
+        const int nC0 = (nA | nB) >= 0 ? mean : one;
         const int nC = (D >> 17) ? -1 : nC0;
         const int tc = tc_of(mv), t1 = (int)((mv >> 13) & 3u);
         const uint32_t ce = ctab[nC < 0 ? 3 : (nC < 2 ? 0 : (nC < 4 ? 1 : 2))][4 * tc + t1];
@@ -2007,6 +2010,10 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
             nc1 = 0u;
         }
         lo[i] = (uint16_t)(len | nc1 << 11);
+    };
+    for (int i = t; i < npc; i += T) {
+        const int k = div_npc(i), pc = i - k * NPC;
+        token(i, k, pc, L.pcd[pc]);
     }
     __syncthreads();
     if (stp) stp[3] = __builtin_amdgcn_s_memrealtime();

@@ -296,8 +296,17 @@ def _load():
         "bitreader_get_remaining_bytes": (ctypes.c_size_t, [P(BitReader)]),
         "bitreader_get_pointer": (u8p, [P(BitReader)]),
     }
+    # an A/B variant library from an earlier revision (H264SCROLL_LIB) may
+    # lack the newest entry points: those stay unbound there (a call fails
+    # loudly); the tree's own library must export every one
+    variant = bool(os.environ.get("H264SCROLL_LIB"))
     for name, (res, args) in sig.items():
-        f = getattr(lib, name)
+        try:
+            f = getattr(lib, name)
+        except AttributeError:
+            if variant:
+                continue
+            raise
         f.restype = res
         f.argtypes = args
     return lib

@@ -32,12 +32,20 @@ typedef struct {
 #define DYN_HEAD_VECS 16             /* heads[] per frame: 12 classes MSB first, then their lengths */
 #define DYN_CTR_LIST 4               /* ctr[]: the lists (the counters zeroed per compose: 4 words) */
 
+/* a second HIP stream beside the block coder: after k_dyn_rows it takes the
+ * general path (k_dyn_code_general, k_dyn_row<true>) and k_dyn_static, which
+ * k_dyn_row<false> does not wait for; k_dyn_epfix waits for both (e1) */
+typedef struct {
+    hipStream_t side;
+    hipEvent_t e0, e1;
+} DynFork;
 /* k_dyn_rows + k_dyn_code_general (records of the general-path NALs) +
- * k_dyn_row (every rect row: block coding + packing -> its row-stage bits) */
+ * k_dyn_row (every rect row: block coding + packing -> its row-stage bits);
+ * fk != NULL: the fork above (k_dyn_static then runs on the side stream) */
 int dyn_launch_code(hipStream_t hs, int nframes, int S, DevStream *st, const NalDesc *nal,
                     int ld_nal, const PlanPending *pend, DynFrame *dfr, int ld_fr,
                     const DynGeom *g, const uint8_t *src, const uint8_t *refs, const DynScratch *x,
-                    uint32_t epoch, int mbw, uint64_t *stamps);
+                    uint32_t epoch, int mbw, uint64_t *stamps, const DynFork *fk);
 /* k_dyn_static (static row groups) + k_dyn_epfix: RBSP sizes and EP
  * positions (eps: DYN_OVF_BYTES per frame) straight from the row groups */
 /* k_dyn_static alone (the static row groups: header, rows above / below the
@@ -47,7 +55,7 @@ int dyn_launch_static(hipStream_t hs, int nframes, int S, DevStream *st, const N
                       const PlanPending *pend, DynFrame *dfr, int ld_fr, const DynGeom *g, const DynScratch *x);
 int dyn_launch_pack(hipStream_t hs, int nframes, int S, DevStream *st, const NalDesc *nal,
                     int ld_nal, const PlanPending *pend, DynFrame *dfr, int ld_fr,
-                    const DynGeom *g, const DynScratch *x, uint8_t *eps, uint64_t *stamps);
+                    const DynGeom *g, const DynScratch *x, uint8_t *eps, uint64_t *stamps, const DynFork *fk);
 /* k_dyn_gather (k_dyn_emit_gather on the hint / splice path): x != NULL -- the dynamic rect (RBSP from
  * the row groups, EP lists in stage = eps); x == NULL -- the staged RBSP of
  * the hint / splice path (slot_bytes per frame, EP list in the slot tail) */

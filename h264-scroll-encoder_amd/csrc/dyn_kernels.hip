@@ -3697,7 +3697,7 @@ __global__ __launch_bounds__(256) void k_dyn_synth(uint8_t *__restrict__ src, Dy
 int dyn_launch_code(hipStream_t hs, int nframes, int S, DevStream *st, const NalDesc *nal,
                     int ld_nal, const PlanPending *pend, DynFrame *dfr, int ld_fr,
                     const DynGeom *g, const uint8_t *src, const uint8_t *refs, const DynScratch *x,
-                    uint32_t epoch, int mbw, uint64_t *stamps)
+                    uint32_t epoch, int mbw, uint64_t *stamps, const DynFork *fk)
 {
     if (nframes <= 0 || S <= 0) return 0;
     {                                   /* the tzrb table, once per device (and process) */
@@ -3715,8 +3715,14 @@ int dyn_launch_code(hipStream_t hs, int nframes, int S, DevStream *st, const Nal
     hipLaunchKernelGGL(k_dyn_rows, dim3(nframes, S), dim3(256), 0, hs, st, nal, ld_nal, pend, dfr, ld_fr,
                        *g, x->rows, x->ctr, x->heads);
     if (hipGetLastError() != hipSuccess) return -1;
+    hipStream_t hg = hs;                /* the general path's stream */
+    if (fk) {
+        if (hipEventRecord(fk->e0, hs) != hipSuccess || hipStreamWaitEvent(fk->side, fk->e0, 0) != hipSuccess)
+            return -1;
+        hg = fk->side;
+    }
     const int nchunk = (24 * g->w * g->h + CODE_T - 1) / CODE_T;
-    hipLaunchKernelGGL(k_dyn_code_general, dim3(nchunk, CODE_GEN_Y), dim3(CODE_T), 0, hs, st, dfr, ld_fr,
+    hipLaunchKernelGGL(k_dyn_code_general, dim3(nchunk, CODE_GEN_Y), dim3(CODE_T), 0, hg, st, dfr, ld_fr,
                        pend, nal, ld_nal, *g, x->rows, src, refs, x->meta, x->body_lo, x->body_hi, x->body_w,
                        x->ctr);
     if (hipGetLastError() != hipSuccess) return -1;
@@ -3738,10 +3744,16 @@ int dyn_launch_code(hipStream_t hs, int nframes, int S, DevStream *st, const Nal
     /* the general path: one row workgroup per record slot that may be taken */
     hipLaunchKernelGGL(k_dyn_row<true>, dim3(g->h, std::min<uint32_t>(g->gen_cap, (uint32_t)(nframes * S)), 1),
                        dim3(row_threads(g->w)),
-                       row_lds_bytes(g->w), hs, st, nal, ld_nal, pend, dfr, ld_fr, *g, x->rows, src, refs,
+                       row_lds_bytes(g->w), hg, st, nal, ld_nal, pend, dfr, ld_fr, *g, x->rows, src, refs,
                        x->meta, x->body_lo, x->body_hi, x->body_w, x->tcx, epoch, x->rowstage, x->gbits, x->spill,
                        x->ctr, x->heads, stamps);
-    return hipGetLastError() == hipSuccess ? 0 : -1;
+    if (hipGetLastError() != hipSuccess) return -1;
+    if (fk) {                           /* the static row groups beside the block coder too */
+        if (dyn_launch_static(hg, nframes, S, st, nal, ld_nal, pend, dfr, ld_fr, g, x) ||
+            hipEventRecord(fk->e1, hg) != hipSuccess)
+            return -1;
+    }
+    return 0;
 }
 
 int dyn_launch_static(hipStream_t hs, int nframes, int S, DevStream *st, const NalDesc *nal, int ld_nal,
@@ -3755,10 +3767,14 @@ int dyn_launch_static(hipStream_t hs, int nframes, int S, DevStream *st, const N
 
 int dyn_launch_pack(hipStream_t hs, int nframes, int S, DevStream *st, const NalDesc *nal,
                     int ld_nal, const PlanPending *pend, DynFrame *dfr, int ld_fr,
-                    const DynGeom *g, const DynScratch *x, uint8_t *eps, uint64_t *stamps)
+                    const DynGeom *g, const DynScratch *x, uint8_t *eps, uint64_t *stamps, const DynFork *fk)
 {
     if (nframes <= 0 || S <= 0) return 0;
-    if (dyn_launch_static(hs, nframes, S, st, nal, ld_nal, pend, dfr, ld_fr, g, x)) return -1;
+    if (fk) {                           /* k_dyn_static and the general path ran beside k_dyn_row */
+        if (hipStreamWaitEvent(hs, fk->e1, 0) != hipSuccess) return -1;
+    } else if (dyn_launch_static(hs, nframes, S, st, nal, ld_nal, pend, dfr, ld_fr, g, x)) {
+        return -1;
+    }
     hipLaunchKernelGGL(k_dyn_epfix, dim3(nframes, S), dim3(EPF_T), gtab_bytes(g->ngroups, true), hs, st, dfr,
                        ld_fr, nframes, *g, x->rowstage, x->gbits, eps, stamps);
     return hipGetLastError() == hipSuccess ? 0 : -1;

@@ -950,6 +950,7 @@ struct ScrollBatch {
      * (d_sp_rec, word pool d_sp_rbsp) and composed by k_splice_stage */
     std::vector<int32_t> h_dyn_pos;    /* [2 (s * max_frames + f)]: rect origin, x0 < 0: none */
     int fallback = 0;                  /* scroll_batch_set_fallback: k_hint_fb before the stage kernels */
+    DynFork fork{};                    /* SCROLL_DYN_FORK=1: the general path + static groups beside k_dyn_row */
     std::vector<int32_t> h_dyn_qp;     /* [s * max_frames + f]: the frame's rect QP under hints, -1: the stream's */
     int dyn_pos_custom = 0;            /* some frame's origin differs from the batch rect */
     int dyn_qp = 26;                   /* the rect's QP (scroll_batch_set_dyn_qp)          */
@@ -1117,6 +1118,12 @@ void scroll_batch_destroy(ScrollBatch *b)
     for (int i = 0; i < NEV; ++i)
         if (b->ev[i]) (void)hipEventDestroy(b->ev[i]);
     for (hipEvent_t e : b->ring) (void)hipEventDestroy(e);
+    if (b->fork.side) {
+        (void)hipStreamSynchronize(b->fork.side);
+        (void)hipStreamDestroy(b->fork.side);
+        (void)hipEventDestroy(b->fork.e0);
+        (void)hipEventDestroy(b->fork.e1);
+    }
     if (b->own) (void)hipStreamDestroy(b->own);
     (void)hipFree(b->d_st);
     (void)hipHostFree(b->h_st);
@@ -1409,14 +1416,29 @@ static int launch(ScrollBatch *b, int nframes, int plan_mode, int nal_max, hipSt
              * at 2 / 4 / 8 chunks: DESIGN.md §6; the device-side frame lists
              * are batch-wide, so the launches below cover the whole batch) */
             const DynGeom &G = b->geo;
+            /* SCROLL_DYN_FORK=1: the general path and the static groups on a
+             * second stream beside k_dyn_row (created on first use) */
+            const DynFork *fk = nullptr;
+            static const bool fork_on = [] {
+                const char *e = getenv("SCROLL_DYN_FORK");
+                return e && e[0] == '1';
+            }();
+            if (fork_on) {
+                if (!b->fork.side) {
+                    HIPCHK(hipStreamCreateWithFlags(&b->fork.side, hipStreamNonBlocking));
+                    HIPCHK(hipEventCreateWithFlags(&b->fork.e0, hipEventDisableTiming));
+                    HIPCHK(hipEventCreateWithFlags(&b->fork.e1, hipEventDisableTiming));
+                }
+                fk = &b->fork;
+            }
             if (dyn_launch_code(hs, nframes, S, b->d_st, b->d_nal, b->ld_nal, b->d_pend, b->d_dfr, ld_fr, &G,
-                                b->d_src, b->d_refs, &b->dx, b->dx.epoch, b->dyn_pw / 16, stamps)) {
+                                b->d_src, b->d_refs, &b->dx, b->dx.epoch, b->dyn_pw / 16, stamps, fk)) {
                 set_err("k_dyn_code launch: %s", hipGetErrorString(hipGetLastError()));
                 return SCROLL_ERR_HIP;
             }
             if ((rc = mark(6))) return rc;
             if (dyn_launch_pack(hs, nframes, S, b->d_st, b->d_nal, b->ld_nal, b->d_pend, b->d_dfr, ld_fr, &G,
-                                &b->dx, b->d_stage, stamps ? b->d_dbg : nullptr)) {
+                                &b->dx, b->d_stage, stamps ? b->d_dbg : nullptr, fk)) {
                 set_err("k_dyn_static / k_dyn_epfix launch: %s", hipGetErrorString(hipGetLastError()));
                 return SCROLL_ERR_HIP;
             }

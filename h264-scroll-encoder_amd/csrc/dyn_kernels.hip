@@ -34,6 +34,7 @@
 
 #include "dyn_device.h"
 #include "dyn_engine.h"
+#include "row_mfma.h"
 #include "stage_util.h"
 
 using namespace scroll;
@@ -1371,7 +1372,7 @@ struct FetchOff {
 
 /* luma task v (MB k = v / 16, raster block v % 16) of rect row ry; rt = the
  * row's 16 luma prediction rows (LDS, or k_dyn_rows' table in global memory) */
-__device__ inline void fetch_luma(FetchOff &o, int v, int ry, const DynGeom &g, const uint32_t *rt)
+[[maybe_unused]] __device__ inline void fetch_luma(FetchOff &o, int v, int ry, const DynGeom &g, const uint32_t *rt)
 {
     const int k = v >> 4, r = v & 15, bx = r & 3, by = r >> 2;
     o.s = (uint32_t)((16 * ry + 4 * by) * (16 * g.w) + 16 * k + 4 * bx);
@@ -1383,7 +1384,7 @@ __device__ inline void fetch_luma(FetchOff &o, int v, int ry, const DynGeom &g, 
 
 /* chroma AC task e (MB e / 8, plane (e / 4) % 2, raster block e % 4); ru /
  * rd = the row's 8 upper / lower bilinear rows */
-__device__ inline void fetch_chroma(FetchOff &o, int e, int ry, const DynGeom &g, uint32_t csz, const uint32_t *ru,
+[[maybe_unused]] __device__ inline void fetch_chroma(FetchOff &o, int e, int ry, const DynGeom &g, uint32_t csz, const uint32_t *ru,
                                     const uint32_t *rd)
 {
     const int ndt = g.w * g.h, k = e >> 3, p = (e >> 2) & 1, r = e & 3, bx = r & 1, by = r >> 1;
@@ -1399,7 +1400,7 @@ __device__ inline void fetch_chroma(FetchOff &o, int e, int ry, const DynGeom &g
  * source / the reference pair or read 0 past the descriptor (raw buffer
  * range check), and their results are never stored.  Chroma always loads
  * its lower row (used only with a fraction): no wait for the fraction */
-__device__ inline void fetch_pass(const FetchOff &o, bool luma, uint32_t adv, uint32_t stride,
+[[maybe_unused]] __device__ inline void fetch_pass(const FetchOff &o, bool luma, uint32_t adv, uint32_t stride,
                                   __amdgpu_buffer_rsrc_t fs, __amdgpu_buffer_rsrc_t rb, BlkPix &px)
 {
 #pragma unroll
@@ -1411,7 +1412,7 @@ __device__ inline void fetch_pass(const FetchOff &o, bool luma, uint32_t adv, ui
 }
 /* the same with the ninth load for luma too (o.c = o.b[3]; its value unused):
  * every pass issues nine loads (k_dyn_row's counted waits) */
-__device__ inline void fetch_pass9(const FetchOff &o, uint32_t adv, uint32_t stride, __amdgpu_buffer_rsrc_t fs,
+[[maybe_unused]] __device__ inline void fetch_pass9(const FetchOff &o, uint32_t adv, uint32_t stride, __amdgpu_buffer_rsrc_t fs,
                                    __amdgpu_buffer_rsrc_t rb, BlkPix &px)
 {
 #ifdef SCROLL_ABL_NOLOAD
@@ -1432,6 +1433,55 @@ __device__ inline void fetch_pass9(const FetchOff &o, uint32_t adv, uint32_t str
     }
     px.c = __builtin_amdgcn_raw_buffer_load_b32(rb, o.c, adv, 0);
 }
+
+/* round 6: the matrix-core levels (row_mfma.h).  A wave's pass = 64 tasks
+ * = 4 tiles; lane (g = lane / 16, n = lane % 16) loads 16 bytes of one
+ * source row, of its prediction row and (chroma) of the lower bilinear row:
+ *   luma:   n = (MB m = n / 4 of the wave's four, block row n % 4), pixel
+ *           row g of the block row; tile j = block column j;
+ *   chroma: n = (plane n / 8, block row (n / 4) % 2, MB pair n % 4), pixel
+ *           row g; tile j = (MB j / 2 of the pair, block column j % 2).
+ * The offsets advance by T bytes per pass as FetchOff's (16 or 8 bytes per
+ * MB, T / 16 or T / 8 MBs per pass) */
+struct MFetch {
+    uint32_t s, p, q;           /* source row; prediction row; its lower bilinear row (chroma) */
+    int pb;
+};
+struct MPix {
+    uint4 s, p, q;
+};
+__device__ inline void mfetch_luma(MFetch &o, int v0, int ry, const DynGeom &g, const uint32_t *rt, int lane)
+{
+    const int gq = lane >> 4, n = lane & 15, k = (v0 >> 4) + (n >> 2), y = 4 * (n & 3) + gq;
+    o.s = (uint32_t)((16 * ry + y) * (16 * g.w) + 16 * k);
+    o.p = (uint32_t)(16 * (g.x0 + k)) + rt[y];
+    o.q = o.p;
+}
+__device__ inline void mfetch_chroma(MFetch &o, int e0, int ry, const DynGeom &g, uint32_t csz, const uint32_t *ru,
+                                     const uint32_t *rd, int lane)
+{
+    const int ndt = g.w * g.h, gq = lane >> 4, n = lane & 15, p = n >> 3, by = (n >> 2) & 1;
+    const int k = (e0 >> 3) + 2 * (n & 3), y = 4 * by + gq;
+    o.s = (uint32_t)(256 * ndt + (p ? 64 * ndt : 0) + (8 * ry + y) * (8 * g.w) + 8 * k);
+    const uint32_t co = (uint32_t)p * csz + (uint32_t)(8 * (g.x0 + k));
+    o.p = co + (ru[y] & ROW_OFF);
+    o.q = co + ((gq < 3 ? ru[y + 1] : rd[y]) & ROW_OFF);
+}
+__device__ inline void mfetch_pass(const MFetch &o, bool chroma, uint32_t adv, __amdgpu_buffer_rsrc_t fs,
+                                   __amdgpu_buffer_rsrc_t rb, MPix &px)
+{
+    const auto a = __builtin_amdgcn_raw_buffer_load_b128(fs, o.s, adv, 0);
+    const auto b = __builtin_amdgcn_raw_buffer_load_b128(rb, o.p, adv, 0);
+    px.s = make_uint4(a[0], a[1], a[2], a[3]);
+    px.p = make_uint4(b[0], b[1], b[2], b[3]);
+    if (chroma) {
+        const auto c = __builtin_amdgcn_raw_buffer_load_b128(rb, o.q, adv, 0);
+        px.q = make_uint4(c[0], c[1], c[2], c[3]);
+    } else {
+        px.q = px.p;            /* every field written: the sets stay in registers */
+    }
+}
+__constant__ KMat g_kmat = make_kmat();
 
 /* ((8 - f) b + f c + 4) >> 3 for the four bytes of b, c: even and odd bytes
  * as two 16-bit halves each (at most 2,044: no carry between halves), two
@@ -1537,6 +1587,26 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
      * LDS copy of the table (a frame this instantiation does not code reads
      * a table k_dyn_rows did not write: offsets into the descriptors' ranges
      * or past them, which read 0; nothing is stored) */
+#ifndef SCROLL_ROW_VALU
+    MFetch mo;
+    mo.pb = -1;
+    bool mo_chroma = false;
+    MPix mx;
+    if (!general) {
+        const uint32_t *rtg = rows + nb * (size_t)(32 * g.h);
+        const int k0 = kind_of(0);
+        if (k0 == 0) {
+            mfetch_luma(mo, wv0, r, g, rtg + 16 * r, lane);
+            mo.pb = 0;
+            mfetch_pass(mo, false, 0u, fs, rb, mx);
+        } else if (k0 == 1) {
+            mfetch_chroma(mo, wv0 - L0, r, g, csz, rtg + 16 * g.h + 8 * r, rtg + 24 * g.h + 8 * r, lane);
+            mo.pb = 0;
+            mo_chroma = true;
+            mfetch_pass(mo, true, 0u, fs, rb, mx);
+        }
+    }
+#else
     FetchOff fo;
     fo.pb = -1;
     bool fo_chroma = false;
@@ -1555,6 +1625,7 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
             fetch_pass9(fo, 0u, (uint32_t)(8 * w), fs, rb, nx);
         }
     }
+#endif
     const DynFrame df = dfr[nb];
     if (df.nal < 0 || ((df.err & DF_GENERAL) != 0) != GEN) return;
 
@@ -1603,7 +1674,7 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
         /* the stream's rect QP (QP_MIN and up here: int8 levels) */
         const int qpy = __builtin_amdgcn_readfirstlane(S->dyn_qp);
         const QParams ql = g_qptab.q[qpy].l, qc = g_qptab.q[qpy].c;
-#ifdef SCROLL_ROW_LVOLD
+#if defined(SCROLL_ROW_LVOLD) && defined(SCROLL_ROW_VALU)
         auto issue = [&](int q, BlkPix &px) {
             const int kd = kind_of(q);
             if (kd == 2) return;
@@ -1678,7 +1749,7 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
             if (pa + 1 < np) issue(pa + 1, nx);
             compute(pa, cur);
         }
-#else
+#elif defined(SCROLL_ROW_VALU)
         /* round 6: a wave's passes are luma ones, then chroma ones, then
          * none (L0 and T are multiples of 64), so two loops whose kind is
          * known at compile time: no per-pass kind tests, and the compiler
@@ -1798,6 +1869,115 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
             code_c(q + 1, B);
         }
         if (q < qC) code_c(q, A);
+        (void)np;
+#else
+        /* round 6: the levels on the matrix cores (row_mfma.h, MFetch): per
+         * pass and wave 4 tiles of 16 blocks, each one MFMA, the quant of two
+         * tiles per asm block, a lane-group transpose, then one block per
+         * lane as before (put_rec).  The pass structure is the vector
+         * form's: luma passes, then chroma ones, the next pass's loads in
+         * flight while one is coded */
+        const int qL = nl > wv0 ? (nl - wv0 + T - 1) / T : 0;
+        const int qC = ntv > wv0 ? (ntv - wv0 + T - 1) / T : 0;
+        const int gq = lane >> 4, ln = lane & 15;
+        auto issue_l = [&](int q, MPix &px) { mfetch_pass(mo, false, (uint32_t)((q - mo.pb) * T), fs, rb, px); };
+        auto issue_c = [&](int q, MPix &px) {
+            if (!mo_chroma) {
+                mfetch_chroma(mo, q * T + wv0 - L0, r, g, csz, L.rt + 16, L.rt + 24, lane);
+                mo.pb = q;
+                mo_chroma = true;
+            }
+            mfetch_pass(mo, true, (uint32_t)((q - mo.pb) * T), fs, rb, px);
+        };
+        auto issue_any = [&](int q, MPix &px) {
+            if (q < qL) issue_l(q, px);
+            else issue_c(q, px);
+        };
+        auto put_rec = [&](int slot, const uint32_t pk[4]) {
+            const uint4 p4 = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+            const uint32_t nz = nz_mask16(p4);
+            const int n = __builtin_popcount(nz);
+            lv[slot] = p4;
+            mt[slot] = (uint16_t)nz;
+            lo[slot] = (uint16_t)atomicAdd(&L.kc[0][SORT_KEYS - 1 - min(n, SORT_KEYS - 1)], 1u);
+        };
+        const uint64_t aL = g_kmat.a[0][lane];
+        const MQuant QL = mquant_of(gq, true, ql);
+        auto code_l = [&](int q, const MPix &px) {
+            uint32_t wd[4];
+            {
+                const mfma_v4i d0 = mtile(aL, px.s.x, px.p.x), d1 = mtile(aL, px.s.y, px.p.y);
+                mquant2(d0, d1, QL, wd[0], wd[1]);
+            }
+            {
+                const mfma_v4i d2 = mtile(aL, px.s.z, px.p.z), d3 = mtile(aL, px.s.w, px.p.w);
+                mquant2(d2, d3, QL, wd[2], wd[3]);
+            }
+            mtranspose(wd);
+            /* lane (gq, ln): block (MB ln / 4 of the pass's four, row ln % 4, column gq) */
+            const int k = ((q * T + wv0) >> 4) + (ln >> 2);
+            if (k < w) put_rec((int)__umul24((uint32_t)k, (uint32_t)NPC) + 4 * (ln & 3) + gq, wd);
+        };
+        auto code_c = [&](int q, const MPix &px, uint64_t aC, const MQuant &QC) {
+            uint32_t pr[4];
+            const uint32_t up[4] = {px.p.x, px.p.y, px.p.z, px.p.w}, dn[4] = {px.q.x, px.q.y, px.q.z, px.q.w};
+            if (frc == 4u) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) pr[j] = __builtin_amdgcn_lerp(up[j], dn[j], 0x01010101u);
+            } else if (frc == 0u) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) pr[j] = up[j];
+            } else {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) pr[j] = bilin4(up[j], dn[j], frc);
+            }
+            const mfma_v4i d0 = mtile(aC, px.s.x, pr[0]), d1 = mtile(aC, px.s.y, pr[1]);
+            const mfma_v4i d2 = mtile(aC, px.s.z, pr[2]), d3 = mtile(aC, px.s.w, pr[3]);
+            const int kb = ((q * T + wv0 - L0) >> 3) + 2 * (ln & 3), pl = ln >> 3, by = (ln >> 2) & 1;
+            /* the DC coefficients (row 15, lane group 3) as int16 into their
+             * plane's DC slot: tile j = MB kb + j / 2, block column j % 2 */
+            if (gq == 3) {
+                const int dcv[4] = {d0[3], d1[3], d2[3], d3[3]};
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int k = kb + (j >> 1);
+                    if (k < w)
+                        reinterpret_cast<int16_t *>(lv + (int)__umul24((uint32_t)k, (uint32_t)NPC) + 16 + pl)[2 * by + (j & 1)] =
+                            (int16_t)dcv[j];
+                }
+            }
+            uint32_t wd[4];
+            mquant2(d0, d1, QC, wd[0], wd[1]);
+            mquant2(d2, d3, QC, wd[2], wd[3]);
+            mtranspose(wd);
+            const int k = kb + (gq >> 1);
+            if (k < w) put_rec((int)__umul24((uint32_t)k, (uint32_t)NPC) + 18 + 4 * pl + 2 * by + (gq & 1), wd);
+        };
+        MPix A = mx, B;
+        int q = 0;
+        for (; q + 1 < qL; q += 2) {
+            issue_l(q + 1, B);
+            code_l(q, A);
+            issue_any(q + 2, A);
+            code_l(q + 1, B);
+        }
+        if (q < qL) {                                       /* an odd luma pass left */
+            issue_any(q + 1, B);
+            code_l(q, A);
+            A = B;                                          /* once: the first chroma pass */
+            ++q;
+        }
+        if (q < qC) {
+            const uint64_t aC = g_kmat.a[1][lane];
+            const MQuant QC = mquant_of(gq, false, qc);
+            for (; q + 1 < qC; q += 2) {
+                issue_c(q + 1, B);
+                code_c(q, A, aC, QC);
+                issue_c(q + 2, A);                          /* past the tasks: unused loads */
+                code_c(q + 1, B, aC, QC);
+            }
+            if (q < qC) code_c(q, A, aC, QC);
+        }
         (void)np;
 #endif
         __syncthreads();                                /* levels, TotalCoeffs, ptabs, counts */

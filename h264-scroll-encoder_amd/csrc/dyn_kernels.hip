@@ -3555,9 +3555,20 @@ __global__ __launch_bounds__(DT) void k_dyn_emit_gather(const DevStream *__restr
  * chunks meeting three groups (groups under 128 bits: tiny rects) take a
  * byte loop.  Grid (frames, streams, Z): workgroup z owns 1/Z of the NAL's
  * chunks. */
-#ifndef SCROLL_GATHER2_Z
-#define SCROLL_GATHER2_Z 1
-#endif
+/* workgroups per NAL (grid z): one per ~640 rect MBs -- a config-3 NAL
+ * (25 x 25 MBs, ~116 KB) keeps one (Z = 2 measured equal), the whole-picture
+ * rects of the fallback (80 x 45: ~350 KB per NAL, 1,024 NALs = 4 workgroups
+ * per CU at Z = 1) take 5, at most 16.  SCROLL_GATHER_Z overrides it */
+inline int gather_z(const DynGeom &g)
+{
+    static const int env = [] {
+        const char *e = getenv("SCROLL_GATHER_Z");
+        return e ? atoi(e) : 0;
+    }();
+    if (env > 0) return env < 64 ? env : 64;
+    const int64_t mbs = (int64_t)g.w * g.h / 640;
+    return (int)(mbs < 1 ? 1 : (mbs > 16 ? 16 : mbs));
+}
 /* 1: two chunk sets per thread in turn, the next chunk's loads in flight
  * while one is assembled (0.142 against 0.146 ms per config-3 launch).
  * Measured and not kept: non-temporal arena stores (0.143), non-temporal
@@ -3975,7 +3986,7 @@ int dyn_launch_emit(hipStream_t hs, int nframes, int S, const DevStream *st, con
     const dim3 grid(nframes, S, GATHER_Z);
     const size_t gl = x ? gtab_bytes(g->ngroups, false) : 0;     /* the group tables (RS) */
     if (x && !(g->debug & SCROLL_DEBUG_DYN_GATHER1))
-        hipLaunchKernelGGL(k_dyn_gather, dim3(nframes, S, SCROLL_GATHER2_Z), dim3(DT), gl, hs, st, nal, ld_nal, dfr,
+        hipLaunchKernelGGL(k_dyn_gather, dim3(nframes, S, gather_z(*g)), dim3(DT), gl, hs, st, nal, ld_nal, dfr,
                            ld_fr, *g, stage, rs, gbits, arena, ld_arena, stamps);
     else if (x && big)
         hipLaunchKernelGGL((k_dyn_emit_gather<4, true>), grid, dim3(DT), gl, hs, st, nal, ld_nal, dfr, ld_fr, *g,

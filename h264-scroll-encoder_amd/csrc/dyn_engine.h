@@ -70,5 +70,9 @@ int dyn_launch_synth(hipStream_t hs, int nframes, int S, uint8_t *src, const Dyn
 void dyn_rowstage_geom(DynGeom *g, int mbw, int mbh);
 /* staging bytes per frame that no dynamic NAL can exceed */
 size_t dyn_slot_bound(int mbw, int mbh, int rw, int rh);
+/* EP positions kept per frame for an rw x rh MB rect on the rows' path
+ * (DynGeom.ep_cap; the list buffer holds 4 ep_cap bytes per frame;
+ * SCROLL_DEBUG_DYN_EPWIN: the large form on any rect) */
+uint32_t dyn_ep_cap(int rw, int rh, int debug);
 
 #endif

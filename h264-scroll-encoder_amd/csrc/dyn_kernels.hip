@@ -2667,7 +2667,7 @@ __device__ inline void rs_load8(uint32_t P, int &gg, int ng, uint32_t T, const u
  * launch per compose for NALs that config 3 never has) */
 template <int NT>
 __device__ uint32_t ep_scan(const uint32_t *fr, int ng, uint32_t T, const uint32_t *goff, const uint32_t *gb,
-                            const uint32_t *gw, uint32_t *cbuf, int *wmax, uint32_t &ep_n, uint32_t *eplist, int t)
+                            const uint32_t *gw, uint32_t *cbuf, int *wmax, uint32_t &ep_n, uint32_t *eplist, int t, uint32_t ecap)
 {
     constexpr int CH = NT * 4 * EPS_KW;                 /* bytes per chunk */
     const uint32_t nin = (T + 7) >> 3;                  /* bitwriter.c:103-111 */
@@ -2754,7 +2754,7 @@ __device__ uint32_t ep_scan(const uint32_t *fr, int ng, uint32_t T, const uint32
             while (ins) {
                 const int i = __builtin_ctz(ins);
                 ins &= ins - 1u;
-                if (k < (uint32_t)EPLIST_MAX) eplist[k] = ib + (uint32_t)i;   /* RBSP index the 03 precedes */
+                if (k < ecap) eplist[k] = ib + (uint32_t)i;   /* RBSP index the 03 precedes */
                 k++;
             }
         }
@@ -2855,7 +2855,7 @@ __device__ inline int cand_group(uint32_t i, int ng, const uint32_t *cbase)
 template <int NT, int LCAP>
 __device__ __attribute__((always_inline)) inline uint32_t ep_list_windows(uint32_t *lst, uint32_t n, uint32_t nin,
                                                                           uint32_t *eplist, uint32_t *ws, int t,
-                                                                          int lane, int wave)
+                                                                          int lane, int wave, uint32_t ecap)
 {
     const uint32_t ws0 = (n + 4u * NT - 1u) / (4u * NT) * (4u * NT);
     const uint32_t HW = (uint32_t)LCAP - ws0, CH = HW / (uint32_t)NT;   /* multiples of 4 NT / 4 */
@@ -2892,7 +2892,7 @@ __device__ __attribute__((always_inline)) inline uint32_t ep_list_windows(uint32
 #pragma unroll
             for (int e = 0; e < 4; ++e)
                 for (uint32_t m = wv4[e]; m; m &= m - 1u) {
-                    if (ex < (uint32_t)EPLIST_MAX)
+                    if (ex < ecap)
                         eplist[ex] = w0 + 32u * ((uint32_t)t * CH + 4u * k + (uint32_t)e) + (uint32_t)__builtin_ctz(m);
                     ++ex;
                 }
@@ -2905,7 +2905,7 @@ __device__ __attribute__((always_inline)) inline uint32_t ep_list_windows(uint32
 
 /* k_dyn_epfix's work for NAL nb (stream s), every thread of the workgroup
  * (NT of them, at least two waves) calling: size, EP positions sorted and
- * each once into the frame's EP list (EPLIST_MAX kept), DF_FIXED set.  The
+ * each once into the frame's EP list (g.ep_cap kept), DF_FIXED set.  The
  * step is a chain of dependent loads per NAL (the measured round-4 split:
  * table 2.3 us, counts 1.2, seams + candidates 14.6, sort 4.7 per
  * workgroup), so the work is laid out for few round trips: the candidate
@@ -3071,11 +3071,11 @@ __device__ inline void ep_fix(DevStream *st, DynFrame *DF, size_t nb, int s, con
     __syncthreads();
     stamp(2);
     const uint32_t n = nlst;
-    uint32_t *eplist = reinterpret_cast<uint32_t *>(eps + nb * DYN_OVF_BYTES);
+    uint32_t *eplist = reinterpret_cast<uint32_t *>(eps + nb * eps_stride(g));
     if (slow || (!bm && n > lcap)) {                    /* the whole NAL scanned here */
         static_assert(NT * EPS_KW <= LCAP, "ep_scan's chunk buffer is the position set's LDS");
         __syncthreads();                                /* every thread is past the set */
-        const uint32_t ne = ep_scan<NT>(fr, ng, T, goff, gb, gw, lst, reinterpret_cast<int *>(E.ws), nlst, eplist, t);
+        const uint32_t ne = ep_scan<NT>(fr, ng, T, goff, gb, gw, lst, reinterpret_cast<int *>(E.ws), nlst, eplist, t, g.ep_cap);
         if (t == 0) {
             DF->err = DF_EPSLOW | DF_FIXED;             /* the list unsorted: the gather sorts it */
             DF->rbsp_bytes = nin;
@@ -3085,7 +3085,7 @@ __device__ inline void ep_fix(DevStream *st, DynFrame *DF, size_t nb, int s, con
     }
     constexpr int CW = LCAP / NT;                       /* bitmap words per thread (whole bitmap) */
     if (!bm && n <= lcap - 4u * NT) {
-        const uint32_t base = ep_list_windows<NT, LCAP>(lst, n, nin, eplist, E.ws, t, lane, wave);
+        const uint32_t base = ep_list_windows<NT, LCAP>(lst, n, nin, eplist, E.ws, t, lane, wave, g.ep_cap);
         stamp(3);
         if (t == 0) nu = base;
     } else if (!bm) {
@@ -3123,7 +3123,7 @@ __device__ inline void ep_fix(DevStream *st, DynFrame *DF, size_t nb, int s, con
         if (t == NT - 1) nu = ex + mine;
         for (uint32_t i = c0; i < c1; ++i)
             if (i == 0u || lst[i] != lst[i - 1u]) {
-                if (ex < (uint32_t)EPLIST_MAX) eplist[ex] = lst[i];
+                if (ex < g.ep_cap) eplist[ex] = lst[i];
                 ++ex;
             }
     } else {
@@ -3154,7 +3154,7 @@ __device__ inline void ep_fix(DevStream *st, DynFrame *DF, size_t nb, int s, con
 #pragma unroll
                 for (int e = 0; e < 4; ++e)
                     for (uint32_t m = wv4[e]; m; m &= m - 1u) {
-                        if (ex < (uint32_t)EPLIST_MAX)
+                        if (ex < g.ep_cap)
                             eplist[ex] = 32u * (uint32_t)(t * CW + 4 * k + e) + (uint32_t)__builtin_ctz(m);
                         ++ex;
                     }
@@ -3185,24 +3185,43 @@ constexpr int EPF_LIST = SCROLL_EPF_LIST;
 #else
 #define EPF_ATTR
 #endif
-__global__ __launch_bounds__(EPF_T) EPF_ATTR void k_dyn_epfix(DevStream *__restrict__ st, DynFrame *__restrict__ dfr,
+template <int NT, int LCAP>
+__global__ __launch_bounds__(NT) EPF_ATTR void k_dyn_epfix(DevStream *__restrict__ st, DynFrame *__restrict__ dfr,
                                                      int ld_fr, int nframes, DynGeom g,
                                                      const uint32_t *__restrict__ rowstage,
                                                      const uint32_t *__restrict__ gbits, uint8_t *__restrict__ eps,
                                                      uint64_t *__restrict__ stamps)
 {
-    __shared__ __attribute__((aligned(16))) uint32_t lst[EPF_LIST];   /* the position bitmap / list */
+    __shared__ __attribute__((aligned(16))) uint32_t lst[LCAP];   /* the position bitmap / list */
     extern __shared__ uint32_t gdyn[];                  /* the group tables (gtab_bytes); cbase: runs before group g */
     const GTab GT = gtab_of(gdyn, g.ngroups);
     uint32_t *goff = GT.goff, *gb = GT.gb, *gw = GT.gw, *cw = GT.cw, *cbase = GT.cbase;
-    __shared__ uint32_t cnt[4], ws[EPF_T / 64];
+    __shared__ uint32_t cnt[4], ws[NT / 64];
     const int f = blockIdx.x, s = blockIdx.y, t = threadIdx.x;
     if (f >= nframes) return;
     const size_t nb = (size_t)s * ld_fr + f;
     DynFrame *DF = dfr + nb;
     if (DF->nal < 0) return;
     const EpfLds E{goff, gb, gw, cw, cbase, lst, cnt, ws};
-    ep_fix<EPF_T, EPF_LIST>(st, DF, nb, s, g, rowstage, gbits, eps, E, t, stamps ? stamps + ((size_t)s * nframes + f) * 8 : nullptr);
+    ep_fix<NT, LCAP>(st, DF, nb, s, g, rowstage, gbits, eps, E, t, stamps ? stamps + ((size_t)s * nframes + f) * 8 : nullptr);
+}
+/* the whole-picture rects' NALs (~300 KB at 720p) hold more EP bytes than
+ * the 2,048-entry set (a quarter of p720full's frames had ~2,200: the whole
+ * NAL then went through ep_scan and emit_serial, one workgroup each: gather
+ * 1.17 + epfix 0.76 ms per step, now 0.18 + 0.10): an 8,192-entry set for
+ * rects over EPF_BIG_MBS MBs.  Config 5 (2,209 MBs, 221 KB NALs: the bitmap
+ * covers them) 2.93 -> 2.86 ms per step with it; config 3 (625 MBs) 1.47
+ * -> 1.56 (fewer resident workgroups), so it keeps the small one.
+ * SCROLL_EPF_BIG=0 / 1 forces the small / big form */
+constexpr int EPF_BIG_LIST = 8192;
+constexpr int EPF_BIG_MBS = 1024;
+inline bool epf_big_rect(int64_t mbs)
+{
+    static const int env = [] {
+        const char *e = getenv("SCROLL_EPF_BIG");
+        return e ? atoi(e) : -1;
+    }();
+    return env >= 0 ? env != 0 : mbs > EPF_BIG_MBS;
 }
 
 /* ---------------------------------------------------------------------- */
@@ -3360,14 +3379,14 @@ __global__ __launch_bounds__(DT) void k_dyn_emit_gather(const DevStream *__restr
     const NalDesc d = nal[(size_t)s * ld_nal + j];
     if (d.slow != 2) return;
     const size_t nb = (size_t)s * ld_fr + f;
-    if (n > ep_cap(g)) {                                     /* past the position list: streamed */
+    if (n > min(ep_cap(g, RS), (uint32_t)EPLIST_MAX)) {     /* past the position list: streamed */
         if (blockIdx.z == 0)
             emit_serial(d, df, nb, s, g, stage, rowstage, gbits, arena, ld_arena, goff, gb, gw,
                         reinterpret_cast<uint8_t *>(raw), reinterpret_cast<int32_t *>(sp), sp + NW, t);
         return;
     }
     const uint8_t *in = RS ? nullptr : stage + nb * g.slot_bytes;
-    const uint32_t *el = reinterpret_cast<const uint32_t *>(RS ? stage + nb * DYN_OVF_BYTES
+    const uint32_t *el = reinterpret_cast<const uint32_t *>(RS ? stage + nb * eps_stride(g)
                                                                : in + g.slot_bytes - DYN_OVF_BYTES);
     const uint32_t *fr = RS ? rowstage + nb * g.rs_frame_words : nullptr;
     if (RS) rs_table(gbits, nb, g, fr, goff, gb, gw, nullptr, t);
@@ -3569,13 +3588,10 @@ inline int gather_z(const DynGeom &g)
     const int64_t mbs = (int64_t)g.w * g.h / 640;
     return (int)(mbs < 1 ? 1 : (mbs > 16 ? 16 : mbs));
 }
-/* 1: two chunk sets per thread in turn, the next chunk's loads in flight
- * while one is assembled (0.142 against 0.146 ms per config-3 launch).
- * Measured and not kept: non-temporal arena stores (0.143), non-temporal
- * row-stage loads (0.153) */
-#ifndef SCROLL_GATHER_PIPE
-#define SCROLL_GATHER_PIPE 1
-#endif
+/* Two chunk sets per thread in turn, the next chunk's loads in flight while
+ * one is assembled (round 5: 0.142 against 0.146 ms per config-3 launch for
+ * one chunk at a time, that form since removed).  Measured and not kept:
+ * non-temporal arena stores (0.143), non-temporal row-stage loads (0.153) */
 
 /* 128-bit helpers on four words, word 0 most significant */
 struct W4 {
@@ -3619,7 +3635,13 @@ __global__ __launch_bounds__(DT) __attribute__((amdgpu_waves_per_eu(8))) void k_
     const uint32_t n = df.ep;
     const NalDesc d = nal[(size_t)s * ld_nal + j];
     if (d.slow != 2) return;
-    if (n > ep_cap(g)) {                                     /* past the position list: streamed */
+    const bool sorted = !(df.err & DF_EPSLOW);
+    /* past the position list, or an unsorted list (ep_scan's) longer than
+     * the LDS holds: streamed */
+    /* positions per LDS window (SCROLL_DEBUG_DYN_EPWIN: 7, so the tests'
+     * NALs take the window path) */
+    const uint32_t wcap = (g.debug & SCROLL_DEBUG_DYN_EPWIN) ? 7u : (uint32_t)EPLIST_MAX - 1u;
+    if (n > ep_cap(g, true) || (!sorted && n > wcap)) {
         if (blockIdx.z == 0)
             emit_serial(d, df, (size_t)s * ld_fr + f, s, g, nullptr, rowstage, gbits, arena, ld_arena, goff, gb,
                         gw, reinterpret_cast<uint8_t *>(raw), reinterpret_cast<int32_t *>(sp), sp + NW, t);
@@ -3629,43 +3651,13 @@ __global__ __launch_bounds__(DT) __attribute__((amdgpu_waves_per_eu(8))) void k_
     uint64_t *stp = stamps && blockIdx.z == 0 && t == 0 ? stamps + ((size_t)s * gridDim.x + blockIdx.x) * 8 : nullptr;
     if (stp) stp[0] = __builtin_amdgcn_s_memrealtime();
     const size_t nb = (size_t)s * ld_fr + f;
-    const uint32_t *el = reinterpret_cast<const uint32_t *>(eps + nb * DYN_OVF_BYTES);
+    const uint32_t *el = reinterpret_cast<const uint32_t *>(eps + nb * eps_stride(g));
     const uint32_t *fr = rowstage + nb * g.rs_frame_words;
     rs_table(gbits, nb, g, fr, goff, gb, gw, nullptr, t);
-    const bool sorted = !(df.err & DF_EPSLOW);
-    for (uint32_t i = t; i < n; i += DT) (sorted ? sp : raw)[i] = el[i];
-    if (t == 0) sp[n] = 0x3fffffffu;                         /* sentinel: sp[n] + n never before a chunk */
-    __syncthreads();
-    for (uint32_t i = t; i < (sorted ? 0u : n); i += DT) {   /* ep_scan's lists: by rank */
-        const uint32_t v = raw[i];
-        uint32_t r = 0;
-        for (uint32_t k = 0; k < n; ++k) r += raw[k] < v ? 1u : 0u;
-        sp[r] = v;
-    }
-    __syncthreads();
     const int ng = g.ngroups;
-    const uint32_t T = goff[ng];
     const __amdgpu_buffer_rsrc_t rr = buf_rsrc(fr, 0xfffffffcu);   /* the frame's groups + spill slots */
     uint8_t *A = arena + (size_t)s * ld_arena;
     const uint64_t o0 = d.out_off, o1 = o0 + d.size;
-    /* coarse index: raw[b] = EP bytes before EBSP index b << cs (the j-th EP
-     * byte sits at EBSP index sp[j] + j, strictly increasing) */
-    int lg = 0;
-    while ((1u << lg) <= n) lg++;
-    int cs = 8;
-    while ((d.size >> cs) >= (uint32_t)EPLIST_MAX) cs++;
-    const int nblk = (int)(d.size >> cs) + 1;
-    for (int bi = t; bi < nblk; bi += DT) {
-        const uint32_t e0 = (uint32_t)bi << cs;
-        uint32_t K = 0;
-        for (int b = lg - 1; b >= 0; --b) {
-            const uint32_t k2 = K + (1u << b);
-            K = k2 <= n && sp[k2 - 1] + (k2 - 1) < e0 ? k2 : K;
-        }
-        raw[bi] = K;
-    }
-    __syncthreads();
-    if (stp) stp[1] = __builtin_amdgcn_s_memrealtime();
     const uint8_t hdr[5] = {0, 0, 0, 1, nal_header_byte(0)};           /* nal.c:59-64 */
     const uint64_t cfirst = o0 >> 4;
     const uint32_t cnal = (uint32_t)(((o1 + 15) >> 4) - cfirst);
@@ -3675,6 +3667,18 @@ __global__ __launch_bounds__(DT) __attribute__((amdgpu_waves_per_eu(8))) void k_
     const int32_t d0 = (int32_t)(o0 - (cfirst << 4)) + 5;
     const int32_t nebsp = (int32_t)(d.size - 5);
     int gg = 0;                                              /* the thread's group, carried */
+    /* The EP positions in LDS: the whole sorted list when it fits (every
+     * benched NAL but the whole-picture rect's heaviest), else windows of the
+     * workgroup's chunks whose EP bytes fit (round 6).  The j-th EP byte sits
+     * at EBSP index el[j] + j; the LDS copy holds window positions j = kb + k
+     * as sp[k] = el[kb + k] + kb, so sp[k] + k is that index and K (a local
+     * count) + kb the EP bytes before a chunk.  raw: the window's coarse index
+     * (EP bytes before EBSP index ub + (b << cs)) */
+    const bool whole = n <= wcap;
+    __shared__ uint32_t win[3];                              /* kb, m, ce of the next window */
+    uint32_t kb = 0, T = 0;
+    int32_t ub = 0;
+    int cs = 8, nblk = 1;
     /* the NAL edges and three-group chunks: byte by byte */
     auto slow_chunk = [&](uint32_t c, uint32_t K) {
         uint8_t *q = A + ((cfirst + c) << 4);
@@ -3690,7 +3694,7 @@ __global__ __launch_bounds__(DT) __attribute__((amdgpu_waves_per_eu(8))) void k_
                 if ((int32_t)(sp[K] + K) == uu) {
                     v = 3;
                 } else {
-                    const uint32_t ri = (uint32_t)uu - K;
+                    const uint32_t ri = (uint32_t)uu - K - kb;
                     const uint32_t wd = rs_word(32u * (ri >> 2), ng, T, goff, gb, gw, fr);
                     v = (uint8_t)(wd >> (8u * (3u - (ri & 3u))));
                 }
@@ -3739,7 +3743,6 @@ __global__ __launch_bounds__(DT) __attribute__((amdgpu_waves_per_eu(8))) void k_
             make_uint4(__builtin_bswap32(R.w[0]), __builtin_bswap32(R.w[1]), __builtin_bswap32(R.w[2]),
                        __builtin_bswap32(R.w[3]));
     };
-#if SCROLL_GATHER_PIPE
     /* two chunk sets in turn (no register copies between them): chunk c +
      * DT's search and loads go out before chunk c is assembled and stored.
      * Every chunk loads (the edge / past-the-end ones at word 0, unused), so
@@ -3750,9 +3753,10 @@ __global__ __launch_bounds__(DT) __attribute__((amdgpu_waves_per_eu(8))) void k_
         bool fast, two, yv;                                  /* yv: y holds the next group's words */
         uint32_t x[5], y[4];
     };
+    uint32_t wend = cend;                                    /* the window's chunk end */
     auto prep = [&](uint32_t c, GSet &S) {
-        const int32_t u0 = 16 * (int32_t)c - d0;
-        uint32_t K = raw[u0 > 0 ? min(u0 >> cs, nblk - 1) : 0];
+        const int32_t u0 = 16 * (int32_t)c - d0, du = u0 - ub;
+        uint32_t K = raw[du > 0 ? min(du >> cs, nblk - 1) : 0];
         uint32_t wo = 0u, yo = 0u;
         S.c = c;
         S.u0 = u0;
@@ -3760,9 +3764,9 @@ __global__ __launch_bounds__(DT) __attribute__((amdgpu_waves_per_eu(8))) void k_
         S.two = false;
         S.yv = false;
         S.lp = S.rem = 0u;
-        if (c < cend && u0 >= 0 && u0 + 16 <= nebsp) {
+        if (c < wend && u0 >= 0 && u0 + 16 <= nebsp) {
             while ((int32_t)(sp[K] + K) < u0) K++;           /* sentinel stops it */
-            const uint32_t i0 = (uint32_t)u0 - K, P = 8u * i0;
+            const uint32_t i0 = (uint32_t)u0 - K - kb, P = 8u * i0;
             while (gg + 1 < ng && goff[gg + 1] <= P) ++gg;
             const uint32_t lp = P - goff[gg], rem = gb[gg] - lp;
             const bool two = rem < 128u;
@@ -3792,47 +3796,80 @@ __global__ __launch_bounds__(DT) __attribute__((amdgpu_waves_per_eu(8))) void k_
             slow_chunk(S.c, S.K);
         }
     };
-    GSet sa, sb;
-    uint32_t c = cbeg + (uint32_t)t;
-    if (c < cend) prep(c, sa);
-    while (c < cend) {
-        prep(c + DT, sb);
-        finish(sa);
-        c += DT;
-        if (c >= cend) break;
-        prep(c + DT, sa);
-        finish(sb);
-        c += DT;
-    }
-#else
-    for (uint32_t c = cbeg + (uint32_t)t; c < cend; c += DT) {
-        const int32_t u0 = 16 * (int32_t)c - d0;
-        uint32_t K = raw[u0 > 0 ? min(u0 >> cs, nblk - 1) : 0];
-        if (u0 >= 0 && u0 + 16 <= nebsp) {
-            while ((int32_t)(sp[K] + K) < u0) K++;               /* sentinel stops it */
-            const uint32_t i0 = (uint32_t)u0 - K, P = 8u * i0;
-            while (gg + 1 < ng && goff[gg + 1] <= P) ++gg;
-            while (gg > 0 && goff[gg] > P) --gg;                 /* never for increasing P */
-            const uint32_t lp = P - goff[gg], rem = gb[gg] - lp;  /* bits left in the group */
-            const bool two = rem < 128u;
-            if (!two || gg + 1 >= ng || gb[gg + 1] >= 128u - rem) {
-                /* 160 bits of the group from word lp >> 5 */
-                const uint32_t wo = 4u * (gw[gg] + (lp >> 5));
-                const auto xa = __builtin_amdgcn_raw_buffer_load_b128(rr, wo, 0, 0);
-                const uint32_t x4 = __builtin_amdgcn_raw_buffer_load_b32(rr, wo + 16u, 0, 0);
-                uint32_t yb[4] = {0u, 0u, 0u, 0u};
-                if (two && gg + 1 < ng) {
-                    const auto y = __builtin_amdgcn_raw_buffer_load_b128(rr, 4u * gw[gg + 1], 0, 0);
-                    yb[0] = (uint32_t)y[0]; yb[1] = (uint32_t)y[1]; yb[2] = (uint32_t)y[2]; yb[3] = (uint32_t)y[3];
+    for (uint32_t cb = cbeg; cb < cend; cb = wend) {
+        uint32_t m = n;
+        if (whole) {
+            kb = 0;
+            wend = cend;
+        } else {
+            /* the window from chunk cb: its first EP byte kb (a binary search
+             * in the sorted list), as many as the LDS holds, ending at the
+             * chunk of the first one that does not fit (a chunk holds at most
+             * 16 EP bytes, so a window is never empty) */
+            __syncthreads();                                 /* the last window's sp / raw are done */
+            if (t == 0) {
+                const int32_t ulo = 16 * (int32_t)cb - d0;
+                uint32_t lo = 0, hi = n;
+                while (lo < hi) {
+                    const uint32_t mid = (lo + hi) >> 1;
+                    if ((int32_t)(el[mid] + mid) < ulo) lo = mid + 1;
+                    else hi = mid;
                 }
-                const uint32_t x[5] = {(uint32_t)xa[0], (uint32_t)xa[1], (uint32_t)xa[2], (uint32_t)xa[3], x4};
-                fast_chunk(c, u0, K, lp, rem, two, x, yb);
-                continue;
+                const uint32_t mm = min(n - lo, wcap);
+                uint32_t ce = cend;
+                if (lo + mm < n) ce = min(cend, max(cb + 1u, (uint32_t)((int32_t)(el[lo + mm] + lo + mm) + d0) >> 4));
+                win[0] = lo;
+                win[1] = mm;
+                win[2] = ce;
             }
+            __syncthreads();
+            kb = win[0];
+            m = win[1];
+            wend = win[2];
         }
-        slow_chunk(c, K);
+        for (uint32_t i = t; i < m; i += DT) (sorted ? sp : raw)[i] = el[kb + i] + kb;
+        if (t == 0) sp[m] = 0x3fffffffu;                     /* sentinel: sp[m] + m never before a chunk */
+        __syncthreads();
+        for (uint32_t i = t; i < (sorted ? 0u : m); i += DT) {   /* ep_scan's lists (whole only): by rank */
+            const uint32_t v = raw[i];
+            uint32_t r = 0;
+            for (uint32_t k = 0; k < m; ++k) r += raw[k] < v ? 1u : 0u;
+            sp[r] = v;
+        }
+        __syncthreads();
+        T = goff[ng];
+        /* coarse index over the window's EBSP bytes from ub */
+        ub = whole ? 0 : max(0, 16 * (int32_t)cb - d0);
+        const uint32_t span = whole ? d.size : (uint32_t)(16 * (int32_t)wend - d0 - ub + 16);
+        int lg = 0;
+        while ((1u << lg) <= m) lg++;
+        cs = 8;
+        while ((span >> cs) >= (uint32_t)EPLIST_MAX) cs++;
+        nblk = (int)(span >> cs) + 1;
+        for (int bi = t; bi < nblk; bi += DT) {
+            const uint32_t e0 = (uint32_t)ub + ((uint32_t)bi << cs);
+            uint32_t K = 0;
+            for (int b = lg - 1; b >= 0; --b) {
+                const uint32_t k2 = K + (1u << b);
+                K = k2 <= m && sp[k2 - 1] + (k2 - 1) < e0 ? k2 : K;
+            }
+            raw[bi] = K;
+        }
+        __syncthreads();
+        if (stp && cb == cbeg) stp[1] = __builtin_amdgcn_s_memrealtime();
+        GSet sa, sb;
+        uint32_t c = cb + (uint32_t)t;
+        if (c < wend) prep(c, sa);
+        while (c < wend) {
+            prep(c + DT, sb);
+            finish(sa);
+            c += DT;
+            if (c >= wend) break;
+            prep(c + DT, sa);
+            finish(sb);
+            c += DT;
+        }
     }
-#endif
     if (stamps) {                                            /* uniform */
         __syncthreads();
         if (stp) stp[2] = __builtin_amdgcn_s_memrealtime();
@@ -3966,8 +4003,12 @@ int dyn_launch_pack(hipStream_t hs, int nframes, int S, DevStream *st, const Nal
     } else if (dyn_launch_static(hs, nframes, S, st, nal, ld_nal, pend, dfr, ld_fr, g, x)) {
         return -1;
     }
-    hipLaunchKernelGGL(k_dyn_epfix, dim3(nframes, S), dim3(EPF_T), gtab_bytes(g->ngroups, true), hs, st, dfr,
-                       ld_fr, nframes, *g, x->rowstage, x->gbits, eps, stamps);
+    if (g->ep_cap >= (uint32_t)EPF_BIG_LIST)
+        hipLaunchKernelGGL((k_dyn_epfix<EPF_T, EPF_BIG_LIST>), dim3(nframes, S), dim3(EPF_T), gtab_bytes(g->ngroups, true),
+                           hs, st, dfr, ld_fr, nframes, *g, x->rowstage, x->gbits, eps, stamps);
+    else
+        hipLaunchKernelGGL((k_dyn_epfix<EPF_T, EPF_LIST>), dim3(nframes, S), dim3(EPF_T), gtab_bytes(g->ngroups, true),
+                           hs, st, dfr, ld_fr, nframes, *g, x->rowstage, x->gbits, eps, stamps);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -4029,6 +4070,13 @@ void dyn_rowstage_geom(DynGeom *g, int mbw, int mbh)
     g->rs_row_words = words((uint64_t)mbw * (HEAD_MAX + 1) + (uint64_t)g->w * SCROLL_DYN_ROW_KBITS + 64) + EPC_ROW;
     if (g->rs_row_words > g->rs_spill_words) g->rs_row_words = g->rs_spill_words;
     g->rs_frame_words = (uint64_t)(g->ngroups - g->h) * g->rs_static_words + (uint64_t)g->h * g->rs_row_words;
+}
+
+/* EP positions kept per frame by the rows' path (the list buffer's stride / 4) */
+uint32_t dyn_ep_cap(int rw, int rh, int debug)
+{
+    return (debug & SCROLL_DEBUG_DYN_EPWIN) || epf_big_rect((int64_t)rw * rh) ? (uint32_t)EPF_BIG_LIST
+                                                                            : (uint32_t)EPLIST_MAX;
 }
 
 size_t dyn_slot_bound(int mbw, int mbh, int rw, int rh)

@@ -111,6 +111,7 @@ typedef struct {
     uint32_t rs_spill_cap;          /* spill slots after the frames' regions       */
     uint32_t gen_cap;               /* general-path record slots (NALs)           */
     uint32_t rs_frames;             /* frame regions before the spill slots (S F)  */
+    uint32_t ep_cap;                /* EP positions kept per frame (the dyn path's list; 4 ep_cap bytes a frame) */
 } DynGeom;
 
 /* hints of one composed frame: rects [first, first + n) of the batch's rect

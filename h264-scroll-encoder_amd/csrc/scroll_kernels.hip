@@ -1966,6 +1966,7 @@ int scroll_batch_set_dyn_rect(ScrollBatch *b, int x0, int y0, int w, int h, size
     g.src_ld = round256((size_t)b->max_frames * g.src_fr);
     g.ref_ld = 0;
     g.slot_bytes = slot_bytes ? round256(slot_bytes + DYN_OVF_BYTES) : dyn_slot_bound(mbw, mbh, w, h);
+    g.ep_cap = dyn_ep_cap(w, h, b->debug);
     dyn_rowstage_geom(&g, mbw, mbh);
     b->dyn_pw = pw;
     b->dyn_ph = ph;
@@ -1975,7 +1976,7 @@ int scroll_batch_set_dyn_rect(ScrollBatch *b, int x0, int y0, int w, int h, size
         e = hipMalloc(&b->d_dfr, S * F * sizeof(DynFrame));
         /* the RBSP is never staged (k_dyn_epfix / k_dyn_emit_gather read the
          * row groups): per frame only its EP list; slot_bytes stays the cap */
-        if (e == hipSuccess) e = hipMalloc(&b->d_stage, S * F * DYN_OVF_BYTES);
+        if (e == hipSuccess) e = hipMalloc(&b->d_stage, S * F * (size_t)4 * g.ep_cap);
         if (e == hipSuccess) e = hipMemset(b->d_dfr, 0, S * F * sizeof(DynFrame));
     }
     if (e == hipSuccess) e = hipMalloc(&b->d_src, S * g.src_ld);
@@ -2525,7 +2526,7 @@ int scroll_batch_clear_hints(ScrollBatch *b)
     if (b->dyn_on) {                   /* the dynamic rect alone again: its DynFrames + EP lists */
         const size_t S = (size_t)b->max_streams, F = (size_t)b->max_frames;
         hipError_t e = hipMalloc(&b->d_dfr, S * F * sizeof(DynFrame));
-        if (e == hipSuccess) e = hipMalloc(&b->d_stage, S * F * DYN_OVF_BYTES);
+        if (e == hipSuccess) e = hipMalloc(&b->d_stage, S * F * (size_t)4 * b->geo.ep_cap);
         if (e == hipSuccess) e = hipMemset(b->d_dfr, 0, S * F * sizeof(DynFrame));
         if (e != hipSuccess) {
             set_err("scroll_batch_clear_hints: %s", hipGetErrorString(e));

@@ -23,10 +23,13 @@ constexpr int NW = DT / 64;
 constexpr int EPLIST_MAX = DYN_OVF_BYTES / 4;   /* EP positions kept per NAL (slot tail) */
 /* NALs with more EP bytes than this go to emit_serial (SCROLL_DEBUG_DYN_EPCAP4
  * lowers it so the tests reach that path) */
-__device__ inline uint32_t ep_cap(const DynGeom &g)
+__device__ inline uint32_t ep_cap(const DynGeom &g, bool rs)
 {
-    return (g.debug & SCROLL_DEBUG_DYN_EPCAP4) ? 4u : (uint32_t)EPLIST_MAX;
+    return (g.debug & SCROLL_DEBUG_DYN_EPCAP4) ? 4u : (rs ? g.ep_cap : (uint32_t)EPLIST_MAX);
 }
+/* bytes of a frame's EP list in the dynamic rect's list buffer (the rows'
+ * path: k_dyn_epfix writes it, k_dyn_gather reads it) */
+__host__ __device__ inline size_t eps_stride(const DynGeom &g) { return (size_t)4 * g.ep_cap; }
 
 __device__ inline int wave_incl_max(int v, int lane)
 {

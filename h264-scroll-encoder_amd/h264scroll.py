@@ -40,6 +40,7 @@ SCROLL_DEBUG_DYN_NOWRITE = 4096
 SCROLL_DEBUG_DYN_EPCAP4 = 8192
 SCROLL_DEBUG_DYN_NOPUBLISH = 16384
 SCROLL_DEBUG_DYN_GATHER1 = 32768
+SCROLL_DEBUG_DYN_EPWIN = 65536
 SCROLL_COMPOSE_REWIND = 1
 MAX_WAYPOINTS = 8
 MV_LIMIT_PX = 496

@@ -80,6 +80,11 @@ extern "C" {
 /* tests: the dynamic rect's NALs go to the arena through the round-3 gather
  * (k_dyn_emit_gather) instead of k_dyn_gather; output unchanged */
 #define SCROLL_DEBUG_DYN_GATHER1 32768
+/* tests: the dynamic rect's EP-position machinery of the whole-picture rects
+ * on any rect -- the 8,192-entry epfix set and list, and k_dyn_gather's LDS
+ * windows at 7 positions each (every NAL with more EP bytes is gathered
+ * window by window); output unchanged.  Set before scroll_batch_set_dyn_rect */
+#define SCROLL_DEBUG_DYN_EPWIN 65536
 
 typedef struct ScrollBatch ScrollBatch;
 

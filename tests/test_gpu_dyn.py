@@ -325,6 +325,41 @@ def test_dyn_large_nal_emit_path(gpu, oracle):
     check_equal(b, want)
 
 
+def test_dyn_ep_windows(gpu, oracle):
+    """the EP-position path of the whole-picture rects (round 6: their
+    heaviest NALs hold more EP bytes than 2,048 -- a third of p720full's
+    frames, ~2,200): k_dyn_epfix's 8,192-entry set and list, and
+    k_dyn_gather taking the sorted list window by window into LDS.
+    SCROLL_DEBUG_DYN_EPWIN puts any rect on that path with 7 positions per
+    window, so every NAL with more EP bytes is gathered in several windows
+    (and split over several workgroups the windows cross); bytes unchanged"""
+    w, h = 1280, 720
+    rect = Rect(28, 10, 25, 25)
+    S, F = 2, 6
+    offs = synthetic_offsets(S, F, h)
+    R = striped_refs(oracle, w, h)
+    src = synth_source(oracle, S, F, rect)
+    want = oracle_streams(oracle, w, h, offs, rect, src, R)
+    b, rc = gpu_streams(gpu, w, h, offs, rect, R, synth=True, debug=gpu.SCROLL_DEBUG_DYN_EPWIN)
+    assert rc == 0, gpu.last_error()
+    check_equal(b, want)
+    eps = [b.dyn_frame_info(s, t)[1] for s in range(S) for t in range(F)]
+    assert sum(e > 7 for e in eps) >= 2, eps          # the window path ran
+
+    w, h = 96, 96
+    rect = Rect(0, 0, 6, 6)
+    rng = np.random.default_rng(23)
+    S, F = 2, 10
+    offs = rng.integers(-200, 300, (S, F)).astype(np.int32)
+    R = random_refs(w, h, 4)
+    src = rng.integers(0, 256, (S, F, 384 * 36)).astype(np.uint8)
+    src[:, ::3] = 0                                   # zero pictures: long zero-bit runs
+    want = oracle_streams(oracle, w, h, offs, rect, src, R)
+    b, rc = gpu_streams(gpu, w, h, offs, rect, R, src, debug=gpu.SCROLL_DEBUG_DYN_EPWIN)
+    assert rc == 0, gpu.last_error()
+    check_equal(b, want)
+
+
 def test_dyn_spill_pool_runs_out_and_grows(gpu, oracle):
     """the row stage is sized for typical rows (SCROLL_DYN_ROW_KBITS per MB);
     a row past its slot takes a spill slot (k_dyn_row), and the pool holds

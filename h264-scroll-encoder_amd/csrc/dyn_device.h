@@ -397,14 +397,14 @@ __device__ __host__ inline int half(uint32_t x, int h) { return (int)(int16_t)(u
     "v_ashrrev_i32 %[t5], 31, %[ye0]\n\t" \
     "v_ashrrev_i32 %[t6], 31, %[yo0]\n\t" \
     "v_ashrrev_i32 %[t7], 31, %[ye1]\n\t" \
-    "v_bfi_b32 %[t0], %[t0], %[k1], %[k0]\n\t" \
-    "v_bfi_b32 %[t1], %[t1], %[k1], %[k0]\n\t" \
-    "v_bfi_b32 %[t2], %[t2], %[k1], %[k0]\n\t" \
-    "v_bfi_b32 %[t3], %[t3], %[k1], %[k0]\n\t" \
-    "v_bfi_b32 %[t4], %[t4], %[k1], %[k0]\n\t" \
-    "v_bfi_b32 %[t5], %[t5], %[k1], %[k0]\n\t" \
-    "v_bfi_b32 %[t6], %[t6], %[k1], %[k0]\n\t" \
-    "v_bfi_b32 %[t7], %[t7], %[k1], %[k0]\n\t" \
+    "v_bitop3_b32 %[t0], %[t0], %[k1], %[k0] bitop3:0xca\n\t" \
+    "v_bitop3_b32 %[t1], %[t1], %[k1], %[k0] bitop3:0xca\n\t" \
+    "v_bitop3_b32 %[t2], %[t2], %[k1], %[k0] bitop3:0xca\n\t" \
+    "v_bitop3_b32 %[t3], %[t3], %[k1], %[k0] bitop3:0xca\n\t" \
+    "v_bitop3_b32 %[t4], %[t4], %[k1], %[k0] bitop3:0xca\n\t" \
+    "v_bitop3_b32 %[t5], %[t5], %[k1], %[k0] bitop3:0xca\n\t" \
+    "v_bitop3_b32 %[t6], %[t6], %[k1], %[k0] bitop3:0xca\n\t" \
+    "v_bitop3_b32 %[t7], %[t7], %[k1], %[k0] bitop3:0xca\n\t" \
     "v_mad_i32_i16 %[t0], %[ye0], %[mf0], %[t0]\n\t" \
     "v_mad_i32_i16 %[t1], %[yo0], %[mf2], %[t1]\n\t" \
     "v_mad_i32_i16 %[t2], %[ye1], %[mf2], %[t2]\n\t" \
@@ -431,14 +431,14 @@ __device__ __host__ inline int half(uint32_t x, int h) { return (int)(int16_t)(u
     "v_ashrrev_i32 %[t5], 31, %[yo2]\n\t" \
     "v_ashrrev_i32 %[t6], 31, %[ye3]\n\t" \
     "v_ashrrev_i32 %[t7], 31, %[yo3]\n\t" \
-    "v_bfi_b32 %[t0], %[t0], %[k1], %[k0]\n\t" \
-    "v_bfi_b32 %[t1], %[t1], %[k1], %[k0]\n\t" \
-    "v_bfi_b32 %[t2], %[t2], %[k1], %[k0]\n\t" \
-    "v_bfi_b32 %[t3], %[t3], %[k1], %[k0]\n\t" \
-    "v_bfi_b32 %[t4], %[t4], %[k1], %[k0]\n\t" \
-    "v_bfi_b32 %[t5], %[t5], %[k1], %[k0]\n\t" \
-    "v_bfi_b32 %[t6], %[t6], %[k1], %[k0]\n\t" \
-    "v_bfi_b32 %[t7], %[t7], %[k1], %[k0]\n\t" \
+    "v_bitop3_b32 %[t0], %[t0], %[k1], %[k0] bitop3:0xca\n\t" \
+    "v_bitop3_b32 %[t1], %[t1], %[k1], %[k0] bitop3:0xca\n\t" \
+    "v_bitop3_b32 %[t2], %[t2], %[k1], %[k0] bitop3:0xca\n\t" \
+    "v_bitop3_b32 %[t3], %[t3], %[k1], %[k0] bitop3:0xca\n\t" \
+    "v_bitop3_b32 %[t4], %[t4], %[k1], %[k0] bitop3:0xca\n\t" \
+    "v_bitop3_b32 %[t5], %[t5], %[k1], %[k0] bitop3:0xca\n\t" \
+    "v_bitop3_b32 %[t6], %[t6], %[k1], %[k0] bitop3:0xca\n\t" \
+    "v_bitop3_b32 %[t7], %[t7], %[k1], %[k0] bitop3:0xca\n\t" \
     "v_mad_i32_i16 %[t0], %[yo2], %[mf2], %[t0]\n\t" \
     "v_mad_i32_i16 %[t1], %[ye3], %[mf2], %[t1]\n\t" \
     "v_mad_i32_i16 %[t2], %[yo3], %[mf1], %[t2]\n\t" \
@@ -465,14 +465,14 @@ __device__ __host__ inline int half(uint32_t x, int h) { return (int)(int16_t)(u
     "v_ashrrev_i32 %[t5], 31, %[yo0]\n\t" \
     "v_ashrrev_i32 %[t6], 31, %[ye1]\n\t" \
     "v_bfe_i32 %[t7], %[yo2], 15, 1\n\t" \
-    "v_bfi_b32 %[t0], %[t0], %[k1], %[k0]\n\t" \
-    "v_bfi_b32 %[t1], %[t1], %[k1], %[k0]\n\t" \
-    "v_bfi_b32 %[t2], %[t2], %[k1], %[k0]\n\t" \
-    "v_bfi_b32 %[t3], %[t3], %[k1], %[k0]\n\t" \
-    "v_bfi_b32 %[t4], %[t4], %[k1], %[k0]\n\t" \
-    "v_bfi_b32 %[t5], %[t5], %[k1], %[k0]\n\t" \
-    "v_bfi_b32 %[t6], %[t6], %[k1], %[k0]\n\t" \
-    "v_bfi_b32 %[t7], %[t7], %[k1], %[k0]\n\t" \
+    "v_bitop3_b32 %[t0], %[t0], %[k1], %[k0] bitop3:0xca\n\t" \
+    "v_bitop3_b32 %[t1], %[t1], %[k1], %[k0] bitop3:0xca\n\t" \
+    "v_bitop3_b32 %[t2], %[t2], %[k1], %[k0] bitop3:0xca\n\t" \
+    "v_bitop3_b32 %[t3], %[t3], %[k1], %[k0] bitop3:0xca\n\t" \
+    "v_bitop3_b32 %[t4], %[t4], %[k1], %[k0] bitop3:0xca\n\t" \
+    "v_bitop3_b32 %[t5], %[t5], %[k1], %[k0] bitop3:0xca\n\t" \
+    "v_bitop3_b32 %[t6], %[t6], %[k1], %[k0] bitop3:0xca\n\t" \
+    "v_bitop3_b32 %[t7], %[t7], %[k1], %[k0] bitop3:0xca\n\t" \
     "v_mad_i32_i16 %[t0], %[yo0], %[mf2], %[t0]\n\t" \
     "v_mad_i32_i16 %[t1], %[ye1], %[mf2], %[t1]\n\t" \
     "v_mad_i32_i16 %[t2], %[ye2], %[mf0], %[t2]\n\t" \
@@ -498,13 +498,13 @@ __device__ __host__ inline int half(uint32_t x, int h) { return (int)(int16_t)(u
     "v_ashrrev_i32 %[t4], 31, %[yo2]\n\t" \
     "v_ashrrev_i32 %[t5], 31, %[ye3]\n\t" \
     "v_ashrrev_i32 %[t6], 31, %[yo3]\n\t" \
-    "v_bfi_b32 %[t0], %[t0], %[k1], %[k0]\n\t" \
-    "v_bfi_b32 %[t1], %[t1], %[k1], %[k0]\n\t" \
-    "v_bfi_b32 %[t2], %[t2], %[k1], %[k0]\n\t" \
-    "v_bfi_b32 %[t3], %[t3], %[k1], %[k0]\n\t" \
-    "v_bfi_b32 %[t4], %[t4], %[k1], %[k0]\n\t" \
-    "v_bfi_b32 %[t5], %[t5], %[k1], %[k0]\n\t" \
-    "v_bfi_b32 %[t6], %[t6], %[k1], %[k0]\n\t" \
+    "v_bitop3_b32 %[t0], %[t0], %[k1], %[k0] bitop3:0xca\n\t" \
+    "v_bitop3_b32 %[t1], %[t1], %[k1], %[k0] bitop3:0xca\n\t" \
+    "v_bitop3_b32 %[t2], %[t2], %[k1], %[k0] bitop3:0xca\n\t" \
+    "v_bitop3_b32 %[t3], %[t3], %[k1], %[k0] bitop3:0xca\n\t" \
+    "v_bitop3_b32 %[t4], %[t4], %[k1], %[k0] bitop3:0xca\n\t" \
+    "v_bitop3_b32 %[t5], %[t5], %[k1], %[k0] bitop3:0xca\n\t" \
+    "v_bitop3_b32 %[t6], %[t6], %[k1], %[k0] bitop3:0xca\n\t" \
     "v_mad_i32_i16 %[t0], %[ye3], %[mf2], %[t0]\n\t" \
     "v_mad_i32_i16 %[t1], %[yo3], %[mf1], %[t1]\n\t" \
     "v_mad_i32_i16 %[t2], %[ye2], %[mf0], %[t2] op_sel:[1,0,0,0]\n\t" \
@@ -526,7 +526,7 @@ __device__ __host__ inline int half(uint32_t x, int h) { return (int)(int16_t)(u
  * W[0] (chroma DC, unquantised); the same values as fwd4x4 + quant of a - pr */
 template <bool LUMA>
 __device__ __host__ inline void levels_pk(const uint32_t a[4], const uint32_t pr[4], uint32_t pk4[4], int &w0,
-                                          const QParams &q)
+                                          const QParams &q, uint32_t k1v, uint32_t k0v)
 {
 #ifdef __HIP_DEVICE_COMPILE__
     typedef short s2 __attribute__((ext_vector_type(2)));
@@ -581,7 +581,7 @@ __device__ __host__ inline void levels_pk(const uint32_t a[4], const uint32_t pr
       [t4] "=&v"(t4), [t5] "=&v"(t5), [t6] "=&v"(t6), [t7] "=&v"(t7)                                     \
     : [ye0] "v"(ye[0]), [ye1] "v"(ye[1]), [ye2] "v"(ye[2]), [ye3] "v"(ye[3]), [yo0] "v"(yo[0]),          \
       [yo1] "v"(yo[1]), [yo2] "v"(yo[2]), [yo3] "v"(yo[3]),                                              \
-      [k1] "s"((uint32_t)((1 << q.qbits) - 1 - q.qf)), [k0] "v"((uint32_t)q.qf), [sh] "v"(q.qbits), [mf0] "s"(q.mf0), \
+      [k1] "v"(k1v), [k0] "v"(k0v), [sh] "v"(q.qbits), [mf0] "s"(q.mf0), \
       [mf1] "s"(q.mf1), [mf2] "s"(q.mf2)
     if constexpr (LUMA) {
         asm(SCROLL_QLUMA0 SCROLL_QOPS(pk4[0], pk4[1]));
@@ -592,6 +592,8 @@ __device__ __host__ inline void levels_pk(const uint32_t a[4], const uint32_t pr
     }
 #undef SCROLL_QOPS
 #else
+    (void)k1v;
+    (void)k0v;
     using pk::half;
     using pk::pack2;
     uint32_t E[4], O[4];
@@ -630,6 +632,28 @@ __device__ __host__ inline void levels_pk(const uint32_t a[4], const uint32_t pr
 #endif
 }
 
+/* the same with the bias pair (k1 = 2^qbits - 1 - qf, k0 = qf) from the
+ * QParams; callers in a loop pass them pinned in VGPRs (levels_bias), so
+ * the bias select is a full-rate v_bitop3 (with an SGPR operand it issues
+ * at half rate: profiles/r06_valu_rate2.json) */
+template <bool LUMA>
+__device__ __host__ inline void levels_pk(const uint32_t a[4], const uint32_t pr[4], uint32_t pk4[4], int &w0,
+                                          const QParams &q)
+{
+    levels_pk<LUMA>(a, pr, pk4, w0, q, (uint32_t)((1 << q.qbits) - 1 - q.qf), (uint32_t)q.qf);
+}
+struct LevelsBias {
+    uint32_t k1, k0;
+};
+__device__ __host__ inline LevelsBias levels_bias(const QParams &q)
+{
+    LevelsBias b{(uint32_t)((1 << q.qbits) - 1 - q.qf), (uint32_t)q.qf};
+#ifdef __HIP_DEVICE_COMPILE__
+    asm("" : "+v"(b.k1), "+v"(b.k0));
+#endif
+    return b;
+}
+
 /* non-zero bytes of a word (levels packed as int8) */
 __device__ __host__ inline int nz_bytes(uint32_t x)
 {
@@ -647,6 +671,33 @@ __device__ __host__ inline uint32_t nz_nibble(uint32_t x)
 __device__ __host__ inline uint32_t nz_mask16(uint4 pk)
 {
     return nz_nibble(pk.x) | nz_nibble(pk.y) << 4 | nz_nibble(pk.z) << 8 | nz_nibble(pk.w) << 12;
+}
+/* the same with the two byte masks passed in (k_dyn_row pins them in VGPRs:
+ * the add and the v_bitop3 then issue at full rate, not half as with SGPR
+ * operands) */
+struct NzConst {
+    uint32_t c7f, c80;
+};
+__device__ __host__ inline NzConst nz_const()
+{
+    NzConst c{0x7f7f7f7fu, 0x80808080u};
+#ifdef __HIP_DEVICE_COMPILE__
+    asm("" : "+v"(c.c7f), "+v"(c.c80));
+#endif
+    return c;
+}
+__device__ __host__ inline uint32_t nz_nibble_c(uint32_t x, const NzConst &c)
+{
+#ifdef __HIP_DEVICE_COMPILE__
+    const uint32_t hb = __builtin_amdgcn_bitop3_b32((x & c.c7f) + c.c7f, c.c80, x, 0xc8);   /* ((x & 7f) + 7f | x) & 80 */
+#else
+    const uint32_t hb = (((x & c.c7f) + c.c7f) | x) & c.c80;
+#endif
+    return (hb * 0x00204081u) >> 28;
+}
+__device__ __host__ inline uint32_t nz_mask16_c(uint4 pk, const NzConst &c)
+{
+    return nz_nibble_c(pk.x, c) | nz_nibble_c(pk.y, c) << 4 | nz_nibble_c(pk.z, c) << 8 | nz_nibble_c(pk.w, c) << 12;
 }
 
 /* chroma DC (2x2): qbits + 1, f doubled (|w| <= 16320; q: the chroma QP's) */

@@ -1434,7 +1434,10 @@ struct FetchOff {
     px.c = __builtin_amdgcn_raw_buffer_load_b32(rb, o.c, adv, 0);
 }
 
-/* round 6: the matrix-core levels (row_mfma.h).  A wave's pass = 64 tasks
+/* round 6, an opt-in build (-DSCROLL_ROW_MFMA; the product path is the
+ * vector form: the north star prescribes no MFMA for this integer path, and
+ * the matrix-core form measured only 2.5 % faster): the
+ * matrix-core levels (row_mfma.h).  A wave's pass = 64 tasks
  * = 4 tiles; lane (g = lane / 16, n = lane % 16) loads 16 bytes of one
  * source row, of its prediction row and (chroma) of the lower bilinear row:
  *   luma:   n = (MB m = n / 4 of the wave's four, block row n % 4), pixel
@@ -1450,14 +1453,14 @@ struct MFetch {
 struct MPix {
     uint4 s, p, q;
 };
-__device__ inline void mfetch_luma(MFetch &o, int v0, int ry, const DynGeom &g, const uint32_t *rt, int lane)
+[[maybe_unused]] __device__ inline void mfetch_luma(MFetch &o, int v0, int ry, const DynGeom &g, const uint32_t *rt, int lane)
 {
     const int gq = lane >> 4, n = lane & 15, k = (v0 >> 4) + (n >> 2), y = 4 * (n & 3) + gq;
     o.s = (uint32_t)((16 * ry + y) * (16 * g.w) + 16 * k);
     o.p = (uint32_t)(16 * (g.x0 + k)) + rt[y];
     o.q = o.p;
 }
-__device__ inline void mfetch_chroma(MFetch &o, int e0, int ry, const DynGeom &g, uint32_t csz, const uint32_t *ru,
+[[maybe_unused]] __device__ inline void mfetch_chroma(MFetch &o, int e0, int ry, const DynGeom &g, uint32_t csz, const uint32_t *ru,
                                      const uint32_t *rd, int lane)
 {
     const int ndt = g.w * g.h, gq = lane >> 4, n = lane & 15, p = n >> 3, by = (n >> 2) & 1;
@@ -1467,7 +1470,7 @@ __device__ inline void mfetch_chroma(MFetch &o, int e0, int ry, const DynGeom &g
     o.p = co + (ru[y] & ROW_OFF);
     o.q = co + ((gq < 3 ? ru[y + 1] : rd[y]) & ROW_OFF);
 }
-__device__ inline void mfetch_pass(const MFetch &o, bool chroma, uint32_t adv, __amdgpu_buffer_rsrc_t fs,
+[[maybe_unused]] __device__ inline void mfetch_pass(const MFetch &o, bool chroma, uint32_t adv, __amdgpu_buffer_rsrc_t fs,
                                    __amdgpu_buffer_rsrc_t rb, MPix &px)
 {
     const auto a = __builtin_amdgcn_raw_buffer_load_b128(fs, o.s, adv, 0);
@@ -1481,7 +1484,9 @@ __device__ inline void mfetch_pass(const MFetch &o, bool chroma, uint32_t adv, _
         px.q = px.p;            /* every field written: the sets stay in registers */
     }
 }
+#ifdef SCROLL_ROW_MFMA
 __constant__ KMat g_kmat = make_kmat();
+#endif
 
 /* ((8 - f) b + f c + 4) >> 3 for the four bytes of b, c: even and odd bytes
  * as two 16-bit halves each (at most 2,044: no carry between halves), two
@@ -1587,7 +1592,7 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
      * LDS copy of the table (a frame this instantiation does not code reads
      * a table k_dyn_rows did not write: offsets into the descriptors' ranges
      * or past them, which read 0; nothing is stored) */
-#ifndef SCROLL_ROW_VALU
+#ifdef SCROLL_ROW_MFMA
     MFetch mo;
     mo.pb = -1;
     bool mo_chroma = false;
@@ -1674,7 +1679,7 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
         /* the stream's rect QP (QP_MIN and up here: int8 levels) */
         const int qpy = __builtin_amdgcn_readfirstlane(S->dyn_qp);
         const QParams ql = g_qptab.q[qpy].l, qc = g_qptab.q[qpy].c;
-#if defined(SCROLL_ROW_LVOLD) && defined(SCROLL_ROW_VALU)
+#if defined(SCROLL_ROW_LVOLD) && !defined(SCROLL_ROW_MFMA)
         auto issue = [&](int q, BlkPix &px) {
             const int kd = kind_of(q);
             if (kd == 2) return;
@@ -1749,7 +1754,7 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
             if (pa + 1 < np) issue(pa + 1, nx);
             compute(pa, cur);
         }
-#elif defined(SCROLL_ROW_VALU)
+#elif !defined(SCROLL_ROW_MFMA)
         /* round 6: a wave's passes are luma ones, then chroma ones, then
          * none (L0 and T are multiples of 64), so two loops whose kind is
          * known at compile time: no per-pass kind tests, and the compiler
@@ -1790,20 +1795,23 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
         /* round 6: mt holds the block's non-zero mask until its CAVLC body
          * (TotalCoeff = its popcount), so the body phase reads it instead of
          * deriving it from the levels again */
+        const NzConst nzc = nz_const();
         auto put_rec = [&](int slot, const uint32_t pk[4]) {
             const uint4 p4 = make_uint4(pk[0], pk[1], pk[2], pk[3]);
-            const uint32_t nz = nz_mask16(p4);
+            const uint32_t nz = nz_mask16_c(p4, nzc);
             const int n = __builtin_popcount(nz);
             lv[slot] = p4;
             mt[slot] = (uint16_t)nz;
             lo[slot] = (uint16_t)atomicAdd(&L.kc[0][SORT_KEYS - 1 - min(n, SORT_KEYS - 1)], 1u);
         };
 #endif
+        /* the quantisers' bias pairs pinned in VGPRs (full-rate v_bitop3) */
+        const LevelsBias bl = levels_bias(ql), bc = levels_bias(qc);
         auto code_l = [&](int q, const BlkPix &px) {
             const int v = q * T + t;
             uint32_t pk[4];
             int w0 = 0;
-            levels_pk<true>(px.a, px.b, pk, w0, ql);
+            levels_pk<true>(px.a, px.b, pk, w0, ql, bl.k1, bl.k0);
             if (v < nl) put_rec((int)__umul24((uint32_t)(v >> 4), (uint32_t)NPC) + (v & 15), pk);
         };
         auto code_c = [&](int q, const BlkPix &px) {
@@ -1820,7 +1828,7 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
 #pragma unroll
                 for (int i = 0; i < 4; ++i) pr[i] = bilin4(px.b[i], i < 3 ? px.b[i + 1] : px.c, frc);
             }
-            levels_pk<false>(px.a, pr, pk, w0, qc);
+            levels_pk<false>(px.a, pr, pk, w0, qc, bc.k1, bc.k0);
             const bool ok = e < 8 * w;
             if (ok) put_rec((int)__umul24((uint32_t)(e >> 3), (uint32_t)NPC) + 18 + (e & 7), pk);
 #ifndef SCROLL_ROW_OLDREC

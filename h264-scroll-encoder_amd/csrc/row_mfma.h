@@ -1,5 +1,9 @@
 /*
- * row_mfma.h -- k_dyn_row's levels on the matrix cores (round 6).
+ * row_mfma.h -- k_dyn_row's levels on the matrix cores (round 6): an
+ * opt-in build (-DSCROLL_ROW_MFMA) kept as a measured experiment; the
+ * product path is the vector form (levels_pk), as the north star
+ * prescribes no MFMA for this integer path (DESIGN.md §5 round 6 has the
+ * numbers: 2.5 % on k_dyn_row).
  *
  * The residual transform of a 4x4 block is linear in its pixels: with X the
  * source rows and P the prediction rows, W = C (X - P) C^T, i.e. one 16 x 32

@@ -1802,7 +1802,13 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
             const int n = __builtin_popcount(nz);
             lv[slot] = p4;
             mt[slot] = (uint16_t)nz;
-            lo[slot] = (uint16_t)atomicAdd(&L.kc[0][SORT_KEYS - 1 - min(n, SORT_KEYS - 1)], 1u);
+            /* a block without levels has no CAVLC body: no rank (its class
+             * sorts last and is never read), and no same-address LDS atomic
+             * of the many such lanes of a wave */
+#ifndef SCROLL_ROW_RANK_ALL
+            if (n)
+#endif
+                lo[slot] = (uint16_t)atomicAdd(&L.kc[0][SORT_KEYS - 1 - min(n, SORT_KEYS - 1)], 1u);
         };
 #endif
         /* the quantisers' bias pairs pinned in VGPRs (full-rate v_bitop3) */
@@ -1907,7 +1913,13 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
             const int n = __builtin_popcount(nz);
             lv[slot] = p4;
             mt[slot] = (uint16_t)nz;
-            lo[slot] = (uint16_t)atomicAdd(&L.kc[0][SORT_KEYS - 1 - min(n, SORT_KEYS - 1)], 1u);
+            /* a block without levels has no CAVLC body: no rank (its class
+             * sorts last and is never read), and no same-address LDS atomic
+             * of the many such lanes of a wave */
+#ifndef SCROLL_ROW_RANK_ALL
+            if (n)
+#endif
+                lo[slot] = (uint16_t)atomicAdd(&L.kc[0][SORT_KEYS - 1 - min(n, SORT_KEYS - 1)], 1u);
         };
         const uint64_t aL = g_kmat.a[0][lane];
         const MQuant QL = mquant_of(gq, true, ql);
@@ -2053,8 +2065,9 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
 #else
             const int tcs = __builtin_popcount(mt[slot]);
 #endif
-            order[L.kc[1][SORT_KEYS - 1 - min(tcs, SORT_KEYS - 1)] + lo[slot]] =
-                (uint16_t)(slot | (task < 16 * w ? 0 : 0x8000));
+            if (tcs)
+                order[L.kc[1][SORT_KEYS - 1 - min(tcs, SORT_KEYS - 1)] + lo[slot]] =
+                    (uint16_t)(slot | (task < 16 * w ? 0 : 0x8000));
         }
         __syncthreads();
     ROW_CUT(1);

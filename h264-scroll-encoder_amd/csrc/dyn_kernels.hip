@@ -1162,10 +1162,12 @@ __device__ inline void put_piece(uint32_t *buf, uint32_t p0, uint32_t n, uint32_
 }
 
 /* put_piece for a row written in one pass (the window is the row's words
- * from 0, with ROW_PAD spare words after it): the first three words ORed
- * whatever the piece's length (zero words past its end change nothing), the
- * rest only for pieces that reach them -- no window tests, no per-word
- * branches for the common pieces of <= 3 words */
+ * from 0, with ROW_PAD spare words after it): the first SCROLL_PUT_FIRST
+ * words ORed whatever the piece's length (zero words past its end change
+ * nothing), the rest only for pieces that reach them -- no window tests.
+ * Round 6: 1 instead of 3 -- a zero OR into the word the next lane's piece
+ * starts in is a same-address LDS conflict (k_dyn_row's conflicts 112 ->
+ * 91 M per config-3 launch, its time equal within noise) */
 constexpr uint32_t ROW_PAD = 4;
 __device__ inline void put_piece1(uint32_t *buf, uint32_t pos, uint32_t tv, uint32_t tl, uint4 b, uint32_t bl)
 {
@@ -1175,9 +1177,12 @@ __device__ inline void put_piece1(uint32_t *buf, uint32_t pos, uint32_t tv, uint
     const uint32_t c4 = __builtin_amdgcn_alignbit(b.w, 0u, tl);
     const uint32_t sh = pos & 31u, nw = (sh + tl + bl + 31u) >> 5;
     uint32_t *d = buf + (pos >> 5);
+#ifndef SCROLL_PUT_FIRST
+#define SCROLL_PUT_FIRST 1       /* words ORed whatever the length (round 6: 3 -> 1, fewer same-address ORs) */
+#endif
     atomicOr(d, c0 >> sh);
-    atomicOr(d + 1, __builtin_amdgcn_alignbit(c0, c1, sh));
-    atomicOr(d + 2, __builtin_amdgcn_alignbit(c1, c2, sh));
+    if (SCROLL_PUT_FIRST >= 2 || nw > 1u) atomicOr(d + 1, __builtin_amdgcn_alignbit(c0, c1, sh));
+    if (SCROLL_PUT_FIRST >= 3 || nw > 2u) atomicOr(d + 2, __builtin_amdgcn_alignbit(c1, c2, sh));
     if (nw > 3u) {
         atomicOr(d + 3, __builtin_amdgcn_alignbit(c2, c3, sh));
         if (nw > 4u) {

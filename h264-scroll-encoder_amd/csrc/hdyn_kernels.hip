@@ -283,11 +283,12 @@ __global__ __launch_bounds__(HD_T) void k_hdyn_code(const DevStream *__restrict_
         r.cbp = (uint8_t)(cbp_l | (acn ? 2 : (dcn ? 1 : 0)) << 4);
         if (r.cbp) atomicMin(&spf[fi].hd_first, (uint32_t)q);    /* the mb_qp_delta chain's first MB */
         uint32_t body = 0;
+        r.res_off = 32u * (uint32_t)q * mb_words;      /* the pieces' base (res_len 0: no whole run) */
+        static_assert(32 * HDYN_MB_WORDS_MAX <= 0xffff, "a piece's offset from res_off in 16 bits");
         for (int k = 0; k < 26; ++k) {
             r.tc[k] = L.tc[k];
             r.t1[k] = L.t1[k];
-            r.blen[k] = (uint16_t)L.len[k];
-            r.boff[k] = 32u * (uint32_t)q * mb_words + L.off[k];
+            r.bo[k] = L.len[k] | L.off[k] << 16;       /* off <= 32 mb_words, checked above */
             body += L.len[k];
         }
         r.body = (uint16_t)body;

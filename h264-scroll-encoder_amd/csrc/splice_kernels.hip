@@ -772,8 +772,7 @@ struct LaneLds {
      * outgrew the L2 and reached HBM as partial lines, 5.5 GB of writes per
      * p720splicerows step for 0.9 GB of records */
     uint8_t t1s[SPLICE_PIECES + 1][LANE_ACTIVE];
-    uint16_t bls[SPLICE_PIECES + 1][LANE_ACTIVE];
-    uint32_t bos[SPLICE_PIECES + 1][LANE_ACTIVE];
+    uint32_t bos[SPLICE_PIECES + 1][LANE_ACTIVE];   /* the record's bo words */
 };
 
 /* a lane's own bit reader: the next 33..64 bits in a 64-bit register, a
@@ -1376,8 +1375,7 @@ __global__ __launch_bounds__(64 * LANE_WAVES) void k_splice_lanes(const int32_t 
                         }
                         L.tcc[pi][lane] = (uint8_t)tc;
                         L.t1s[pi][lane] = (uint8_t)t1;
-                        L.bos[pi][lane] = base + bo;
-                        L.bls[pi][lane] = (uint16_t)bl;
+                        L.bos[pi][lane] = bl | (bo - rs0) << 16;
                         coded |= 1u << pi;
                         body += bl;
                     };
@@ -1415,10 +1413,10 @@ __global__ __launch_bounds__(64 * LANE_WAVES) void k_splice_lanes(const int32_t 
                         tw[q] = v;
                     }
                     if (hasqpd) {
-                        /* the pieces' TrailingOnes (7 dwords), then blen [28] u16 +
-                         * boff [28] u32 -- record bytes 96 .. 264 -- as 10 16-byte
-                         * stores and an 8-byte one; a piece the cbp leaves out
-                         * carries a stale value, which no reader looks at */
+                        /* the pieces' TrailingOnes (7 dwords), then bo [28] --
+                         * record bytes 96 .. 208 -- as 7 16-byte stores; a piece
+                         * the cbp leaves out carries a stale value, which no
+                         * reader looks at */
                         uint32_t *t1w = reinterpret_cast<uint32_t *>(R->t1);
 #pragma unroll
                         for (int q = 0; q < (SPLICE_PIECES + 1) / 4; ++q) {
@@ -1427,15 +1425,11 @@ __global__ __launch_bounds__(64 * LANE_WAVES) void k_splice_lanes(const int32_t 
                             for (int b2 = 0; b2 < 4; ++b2) v |= (uint32_t)L.t1s[4 * q + b2][lane] << (8 * b2);
                             t1w[q] = v;
                         }
-                        auto dw = [&](int d) -> uint32_t {          /* dword d of bytes 96 .. 264 */
-                            if (d < (SPLICE_PIECES + 1) / 2)
-                                return (uint32_t)L.bls[2 * d][lane] | (uint32_t)L.bls[2 * d + 1][lane] << 16;
-                            return L.bos[d - (SPLICE_PIECES + 1) / 2][lane];
-                        };
-                        uint4 *bq = reinterpret_cast<uint4 *>(R->blen);
+                        uint4 *bq = reinterpret_cast<uint4 *>(R->bo);
 #pragma unroll
-                        for (int q = 0; q < 10; ++q) bq[q] = make_uint4(dw(4 * q), dw(4 * q + 1), dw(4 * q + 2), dw(4 * q + 3));
-                        reinterpret_cast<uint2 *>(R->blen)[20] = make_uint2(dw(40), dw(41));
+                        for (int q = 0; q < (SPLICE_PIECES + 1) / 4; ++q)
+                            bq[q] = make_uint4(L.bos[4 * q][lane], L.bos[4 * q + 1][lane], L.bos[4 * q + 2][lane],
+                                               L.bos[4 * q + 3][lane]);
                     }
                 }
                 /* hand the context on */
@@ -1680,8 +1674,7 @@ __global__ __launch_bounds__(64) void k_splice_parse(int n, const int32_t *__res
                 if (lane < SPLICE_PIECES) {
                     R->tc[lane] = 0;
                     R->t1[lane] = 0;
-                    R->blen[lane] = 0;
-                    R->boff[lane] = 0;
+                    R->bo[lane] = 0;
                 }
                 if (ts >= 0) L.tcrow[x][ts] = 0;
                 tc_left = 0;
@@ -1914,8 +1907,7 @@ __global__ __launch_bounds__(64) void k_splice_parse(int n, const int32_t *__res
             if (lane < SPLICE_PIECES) {
                 R->tc[lane] = (uint8_t)po.tc;
                 R->t1[lane] = (uint8_t)po.t1;
-                R->blen[lane] = (uint16_t)po.len;
-                R->boff[lane] = base + po.off;
+                R->bo[lane] = po.len ? po.len | (po.off - rs0) << 16 : 0u;
             }
             if (ts >= 0) L.tcrow[x][ts] = (uint8_t)po.tc;
             tc_left = po.tc;
@@ -2039,13 +2031,13 @@ struct SpliceLds {
     alignas(16) uint8_t hdb[DT][SPLICE_REC_HEAD];
 #endif
 };
-static_assert(offsetof(SpliceMbRec, blen) == SPLICE_REC_HEAD && sizeof(SpliceMbRec) == 352,
+static_assert(offsetof(SpliceMbRec, bo) == SPLICE_REC_HEAD && sizeof(SpliceMbRec) == 288,
               "the stage copies a record's first SPLICE_REC_HEAD bytes in 16-byte loads");
 static_assert(offsetof(SpliceMbRec, tc) % 4 == 0 && (SPLICE_PIECES + 1) % 4 == 0,
               "k_splice_lanes stores the TotalCoeffs as whole dwords");
-static_assert(offsetof(SpliceMbRec, t1) % 4 == 0 && offsetof(SpliceMbRec, blen) == 96 && offsetof(SpliceMbRec, boff) == 152 &&
-                  offsetof(SpliceMbRec, bref) == 264 && offsetof(SpliceMbRec, bmv) == 280 && (SPLICE_PIECES + 1) == 28,
-              "k_splice_lanes' record stores: t1 in dwords, blen + boff as 168 bytes from 96, bref / bmv in 8-byte stores");
+static_assert(offsetof(SpliceMbRec, t1) % 4 == 0 && offsetof(SpliceMbRec, bo) == 96 &&
+                  offsetof(SpliceMbRec, bref) == 208 && offsetof(SpliceMbRec, bmv) == 224 && (SPLICE_PIECES + 1) == 28,
+              "k_splice_lanes' record stores: t1 in dwords, bo as 112 bytes from 96, bref / bmv in 8-byte stores");
 static_assert(offsetof(SpliceMbRec, mx) == 4 && offsetof(SpliceMbRec, skip) == 12 && offsetof(SpliceMbRec, intra) == 15 &&
                   offsetof(SpliceMbRec, res_off) == 72 && offsetof(SpliceMbRec, poff) == 80 &&
                   offsetof(SpliceMbRec, mbt) == 86 && offsetof(SpliceMbRec, nbsame) == 88 &&
@@ -2158,7 +2150,10 @@ __device__ inline void splice_tail(SK &sk, const SpliceMbRec &h, const SpliceMbR
             len = e >> 8;
         }
         sk.put(v, (int)len);
-        if constexpr (!count) put_rbsp(sk, rb, R->boff[i], R->blen[i]);
+        if constexpr (!count) {
+            const uint32_t bo = R->bo[i];
+            put_rbsp(sk, rb, h.res_off + (bo >> 16), bo & 0xffffu);
+        }
     };
     if (h.intra == 2) piece(26, nc_edge(0, h, l, t, al, at));
 #pragma unroll

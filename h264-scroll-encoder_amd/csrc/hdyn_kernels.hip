@@ -242,8 +242,12 @@ __global__ __launch_bounds__(HD_T) void k_hdyn_code(const DevStream *__restrict_
     }
     lds_wave_sync();
     if (t == 0) {
+        /* the bodies in syntax order (luma4x4BlkIdx, then chroma), as the
+         * stage walks them from res_off (no coeff_tokens between them here) */
         uint32_t o = 0;
-        for (int k = 0; k < 26; ++k) {
+        for (int j = 0; j < 26; ++j) {
+            const int q8 = j >> 2, q4 = j & 3;
+            const int k = j < 16 ? 4 * ((q8 >> 1) * 2 + (q4 >> 1)) + (q8 & 1) * 2 + (q4 & 1) : j;
             L.off[k] = o;
             o += L.len[k];
         }
@@ -283,12 +287,11 @@ __global__ __launch_bounds__(HD_T) void k_hdyn_code(const DevStream *__restrict_
         r.cbp = (uint8_t)(cbp_l | (acn ? 2 : (dcn ? 1 : 0)) << 4);
         if (r.cbp) atomicMin(&spf[fi].hd_first, (uint32_t)q);    /* the mb_qp_delta chain's first MB */
         uint32_t body = 0;
-        r.res_off = 32u * (uint32_t)q * mb_words;      /* the pieces' base (res_len 0: no whole run) */
-        static_assert(32 * HDYN_MB_WORDS_MAX <= 0xffff, "a piece's offset from res_off in 16 bits");
+        r.res_off = 32u * (uint32_t)q * mb_words;      /* the bodies from here (res_len 0: no whole run) */
         for (int k = 0; k < 26; ++k) {
             r.tc[k] = L.tc[k];
             r.t1[k] = L.t1[k];
-            r.bo[k] = L.len[k] | L.off[k] << 16;       /* off <= 32 mb_words, checked above */
+            r.bl[k] = (uint16_t)L.len[k];                /* no token bits before it */
             body += L.len[k];
         }
         r.body = (uint16_t)body;

@@ -82,13 +82,14 @@ typedef struct {
  * / mx / my are then block 0's.  An intra MB (intra 1 I_4x4, 2 I_16x16, 3
  * I_PCM) keeps its mb_type, its prediction syntax's bits (poff, plen; I_PCM:
  * poff = its samples), I_4x4's cbp codeNum.  nbsame: bit 0 / 1 the left /
- * top MB is in the rect and the same slice.  288 bytes; the first 96 (motion,
+ * top MB is in the rect and the same slice.  232 bytes; the first 96 (motion,
  * cbp, TotalCoeffs, TrailingOnes, the intra / residual fields) are what the
- * stage's counting sweep reads; per piece one word bo: its body's length in
- * bits | its offset from res_off << 16 (an MB's residual is < 18 Kbit with
- * level_prefix <= 15; round 6: u16 length + u32 absolute offset, 352-byte
- * records), read by the writing sweep in one load; the blocks' motion only
- * for partitioned MBs. */
+ * stage's counting sweep reads; per piece a u16: its body's length in bits
+ * (<= 625 with level_prefix <= 15) | the bits of its coeff_token in the
+ * external slice (<= 16) << 11 -- the pieces are contiguous from res_off in
+ * syntax order, so the writing sweep finds each body by a running sum (round
+ * 6: a u16 length and a u32 offset per piece, 352-byte records); the blocks'
+ * motion only for partitioned MBs. */
 typedef struct {
     int16_t ref;
     uint8_t cbp;
@@ -96,14 +97,14 @@ typedef struct {
     int32_t mx, my;
     uint8_t skip, part, sub, intra;
     uint8_t tc[SPLICE_PIECES + 1], t1[SPLICE_PIECES + 1];
-    uint32_t res_off, res_len;      /* the residual after mb_qp_delta (len 0: none / not parsed); the pieces' base */
+    uint32_t res_off, res_len;      /* the residual after mb_qp_delta (len 0: none / not parsed); the pieces start there */
     uint32_t poff;
     uint16_t plen;
     uint8_t mbt, cbp_code;
     uint8_t nbsame, hasqpd;
     uint16_t body;                  /* bits of its pieces' bodies (after coeff_token) */
     uint32_t pad;                   /* -- the stage reads the 96 bytes up to here at once -- */
-    uint32_t bo[SPLICE_PIECES + 1];
+    uint16_t bl[SPLICE_PIECES + 1];
     int8_t bref[16];
     uint32_t bmv[16];
 } SpliceMbRec;

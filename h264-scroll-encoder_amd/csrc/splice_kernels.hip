@@ -442,7 +442,7 @@ __device__ __attribute__((always_inline)) inline bool wrd_body(SRd &r, const Lan
 
 /* lane j: piece j of the MB being parsed */
 struct PieceOut {
-    uint32_t tc, t1, off, len;
+    uint32_t tc, t1, tl, len;                   /* tl: the coeff_token's bits */
 };
 
 /* one residual block: coeff_token, then the body; lane pi keeps the fields */
@@ -450,13 +450,14 @@ __device__ __attribute__((always_inline)) inline bool wrd_piece(SRd &r, const La
                                                                 int nC, int maxc, PieceOut &po)
 {
     int tc, t1;
+    const uint32_t ps = r.p;
     if (!wrd_token(r, T, nC, tc, t1) || tc > maxc) return false;
     const uint32_t p0 = r.p;
     if (!wrd_body(r, T, tc, t1, maxc)) return false;
     if ((int)(threadIdx.x & 63) == pi) {
         po.tc = (uint32_t)tc;
         po.t1 = (uint32_t)t1;
-        po.off = p0;
+        po.tl = p0 - ps;
         po.len = r.p - p0;
     }
     return true;
@@ -772,7 +773,7 @@ struct LaneLds {
      * outgrew the L2 and reached HBM as partial lines, 5.5 GB of writes per
      * p720splicerows step for 0.9 GB of records */
     uint8_t t1s[SPLICE_PIECES + 1][LANE_ACTIVE];
-    uint32_t bos[SPLICE_PIECES + 1][LANE_ACTIVE];   /* the record's bo words */
+    uint16_t bls[SPLICE_PIECES + 1][LANE_ACTIVE];   /* the record's bl words */
 };
 
 /* a lane's own bit reader: the next 33..64 bits in a 64-bit register, a
@@ -1369,13 +1370,14 @@ __global__ __launch_bounds__(64 * LANE_WAVES) void k_splice_lanes(const int32_t 
                         if (!okr) return;
                         int tc, t1;
                         uint32_t bo, bl;
+                        const uint32_t ps = r.p;
                         if (!lane_block(r, L, nC, maxc, tc, t1, bo, bl)) {
                             okr = false;
                             return;
                         }
                         L.tcc[pi][lane] = (uint8_t)tc;
                         L.t1s[pi][lane] = (uint8_t)t1;
-                        L.bos[pi][lane] = bl | (bo - rs0) << 16;
+                        L.bls[pi][lane] = (uint16_t)(bl | (bo - ps) << 11);
                         coded |= 1u << pi;
                         body += bl;
                     };
@@ -1413,10 +1415,10 @@ __global__ __launch_bounds__(64 * LANE_WAVES) void k_splice_lanes(const int32_t 
                         tw[q] = v;
                     }
                     if (hasqpd) {
-                        /* the pieces' TrailingOnes (7 dwords), then bo [28] --
-                         * record bytes 96 .. 208 -- as 7 16-byte stores; a piece
-                         * the cbp leaves out carries a stale value, which no
-                         * reader looks at */
+                        /* the pieces' TrailingOnes (7 dwords), then bl [28] --
+                         * record bytes 96 .. 152 -- as 3 16-byte stores and an
+                         * 8-byte one; a piece the cbp leaves out carries a stale
+                         * value, which no reader looks at */
                         uint32_t *t1w = reinterpret_cast<uint32_t *>(R->t1);
 #pragma unroll
                         for (int q = 0; q < (SPLICE_PIECES + 1) / 4; ++q) {
@@ -1425,11 +1427,13 @@ __global__ __launch_bounds__(64 * LANE_WAVES) void k_splice_lanes(const int32_t 
                             for (int b2 = 0; b2 < 4; ++b2) v |= (uint32_t)L.t1s[4 * q + b2][lane] << (8 * b2);
                             t1w[q] = v;
                         }
-                        uint4 *bq = reinterpret_cast<uint4 *>(R->bo);
+                        auto dw = [&](int d) -> uint32_t {          /* dword d of bytes 96 .. 152 */
+                            return (uint32_t)L.bls[2 * d][lane] | (uint32_t)L.bls[2 * d + 1][lane] << 16;
+                        };
+                        uint4 *bq = reinterpret_cast<uint4 *>(R->bl);
 #pragma unroll
-                        for (int q = 0; q < (SPLICE_PIECES + 1) / 4; ++q)
-                            bq[q] = make_uint4(L.bos[4 * q][lane], L.bos[4 * q + 1][lane], L.bos[4 * q + 2][lane],
-                                               L.bos[4 * q + 3][lane]);
+                        for (int q = 0; q < 3; ++q) bq[q] = make_uint4(dw(4 * q), dw(4 * q + 1), dw(4 * q + 2), dw(4 * q + 3));
+                        reinterpret_cast<uint2 *>(R->bl)[6] = make_uint2(dw(12), dw(13));
                     }
                 }
                 /* hand the context on */
@@ -1674,7 +1678,7 @@ __global__ __launch_bounds__(64) void k_splice_parse(int n, const int32_t *__res
                 if (lane < SPLICE_PIECES) {
                     R->tc[lane] = 0;
                     R->t1[lane] = 0;
-                    R->bo[lane] = 0;
+                    R->bl[lane] = 0;
                 }
                 if (ts >= 0) L.tcrow[x][ts] = 0;
                 tc_left = 0;
@@ -1907,7 +1911,7 @@ __global__ __launch_bounds__(64) void k_splice_parse(int n, const int32_t *__res
             if (lane < SPLICE_PIECES) {
                 R->tc[lane] = (uint8_t)po.tc;
                 R->t1[lane] = (uint8_t)po.t1;
-                R->bo[lane] = po.len ? po.len | (po.off - rs0) << 16 : 0u;
+                R->bl[lane] = (uint16_t)(po.len | po.tl << 11);
             }
             if (ts >= 0) L.tcrow[x][ts] = (uint8_t)po.tc;
             tc_left = po.tc;
@@ -2031,13 +2035,13 @@ struct SpliceLds {
     alignas(16) uint8_t hdb[DT][SPLICE_REC_HEAD];
 #endif
 };
-static_assert(offsetof(SpliceMbRec, bo) == SPLICE_REC_HEAD && sizeof(SpliceMbRec) == 288,
+static_assert(offsetof(SpliceMbRec, bl) == SPLICE_REC_HEAD && sizeof(SpliceMbRec) == 232,
               "the stage copies a record's first SPLICE_REC_HEAD bytes in 16-byte loads");
 static_assert(offsetof(SpliceMbRec, tc) % 4 == 0 && (SPLICE_PIECES + 1) % 4 == 0,
               "k_splice_lanes stores the TotalCoeffs as whole dwords");
-static_assert(offsetof(SpliceMbRec, t1) % 4 == 0 && offsetof(SpliceMbRec, bo) == 96 &&
-                  offsetof(SpliceMbRec, bref) == 208 && offsetof(SpliceMbRec, bmv) == 224 && (SPLICE_PIECES + 1) == 28,
-              "k_splice_lanes' record stores: t1 in dwords, bo as 112 bytes from 96, bref / bmv in 8-byte stores");
+static_assert(offsetof(SpliceMbRec, t1) % 4 == 0 && offsetof(SpliceMbRec, bl) == 96 &&
+                  offsetof(SpliceMbRec, bref) == 152 && offsetof(SpliceMbRec, bmv) == 168 && (SPLICE_PIECES + 1) == 28,
+              "k_splice_lanes' record stores: t1 in dwords, bl as 56 bytes from 96, bref / bmv in 8-byte stores");
 static_assert(offsetof(SpliceMbRec, mx) == 4 && offsetof(SpliceMbRec, skip) == 12 && offsetof(SpliceMbRec, intra) == 15 &&
                   offsetof(SpliceMbRec, res_off) == 72 && offsetof(SpliceMbRec, poff) == 80 &&
                   offsetof(SpliceMbRec, mbt) == 86 && offsetof(SpliceMbRec, nbsame) == 88 &&
@@ -2138,6 +2142,7 @@ __device__ inline void splice_tail(SK &sk, const SpliceMbRec &h, const SpliceMbR
         return;
     }
     if constexpr (count) sk.n += h.body;
+    uint32_t rp = h.res_off;                    /* the external bits: pieces contiguous in syntax order */
     auto piece = [&](int i, int nC) {
         const int tc = h.tc[i], t1 = h.t1[i];
         uint32_t v, len;
@@ -2151,8 +2156,10 @@ __device__ inline void splice_tail(SK &sk, const SpliceMbRec &h, const SpliceMbR
         }
         sk.put(v, (int)len);
         if constexpr (!count) {
-            const uint32_t bo = R->bo[i];
-            put_rbsp(sk, rb, h.res_off + (bo >> 16), bo & 0xffffu);
+            const uint32_t e = R->bl[i];
+            rp += e >> 11;                      /* past its external coeff_token */
+            put_rbsp(sk, rb, rp, e & 2047u);
+            rp += e & 2047u;
         }
     };
     if (h.intra == 2) piece(26, nc_edge(0, h, l, t, al, at));

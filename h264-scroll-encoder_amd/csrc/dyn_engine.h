@@ -41,11 +41,14 @@ typedef struct {
 } DynFork;
 /* k_dyn_rows + k_dyn_code_general (records of the general-path NALs) +
  * k_dyn_row (every rect row: block coding + packing -> its row-stage bits);
- * fk != NULL: the fork above (k_dyn_static then runs on the side stream) */
+ * fk != NULL: the fork above (k_dyn_static then runs on the side stream);
+ * ev0 / ev1 != NULL: recorded right before / after k_dyn_row (the bench's
+ * lite timing: that kernel alone) */
 int dyn_launch_code(hipStream_t hs, int nframes, int S, DevStream *st, const NalDesc *nal,
                     int ld_nal, const PlanPending *pend, DynFrame *dfr, int ld_fr,
                     const DynGeom *g, const uint8_t *src, const uint8_t *refs, const DynScratch *x,
-                    uint32_t epoch, int mbw, uint64_t *stamps, const DynFork *fk);
+                    uint32_t epoch, int mbw, uint64_t *stamps, const DynFork *fk, hipEvent_t ev0 = nullptr,
+                    hipEvent_t ev1 = nullptr);
 /* k_dyn_static (static row groups) + k_dyn_epfix: RBSP sizes and EP
  * positions (eps: DYN_OVF_BYTES per frame) straight from the row groups */
 /* k_dyn_static alone (the static row groups: header, rows above / below the

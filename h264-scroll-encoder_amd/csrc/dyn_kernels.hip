@@ -3241,6 +3241,8 @@ __global__ __launch_bounds__(NT) EPF_ATTR void k_dyn_epfix(DevStream *__restrict
  * SCROLL_EPF_BIG=0 / 1 forces the small / big form */
 constexpr int EPF_BIG_LIST = 8192;
 constexpr int EPF_BIG_MBS = 1024;
+/* (measured, round 6: 256 threads per workgroup for launches of few NALs --
+ * one frame per stream, 256 NALs, a workgroup per CU -- no change) */
 inline bool epf_big_rect(int64_t mbs)
 {
     static const int env = [] {
@@ -3603,16 +3605,21 @@ __global__ __launch_bounds__(DT) void k_dyn_emit_gather(const DevStream *__restr
 /* workgroups per NAL (grid z): one per ~640 rect MBs -- a config-3 NAL
  * (25 x 25 MBs, ~116 KB) keeps one (Z = 2 measured equal), the whole-picture
  * rects of the fallback (80 x 45: ~350 KB per NAL, 1,024 NALs = 4 workgroups
- * per CU at Z = 1) take 5, at most 16.  SCROLL_GATHER_Z overrides it */
-inline int gather_z(const DynGeom &g)
+ * per CU at Z = 1) take 5, at most 16 -- and at least GATHER_MIN_WG
+ * workgroups in all (round 6: a compose of one frame per stream, 256 NALs,
+ * had one workgroup per CU, 46 us of latency-bound gather).  nnal: the NAL
+ * slots launched.  SCROLL_GATHER_Z overrides it */
+constexpr int64_t GATHER_MIN_WG = 2048;
+inline int gather_z(const DynGeom &g, int64_t nnal)
 {
     static const int env = [] {
         const char *e = getenv("SCROLL_GATHER_Z");
         return e ? atoi(e) : 0;
     }();
     if (env > 0) return env < 64 ? env : 64;
-    const int64_t mbs = (int64_t)g.w * g.h / 640;
-    return (int)(mbs < 1 ? 1 : (mbs > 16 ? 16 : mbs));
+    int64_t z = (int64_t)g.w * g.h / 640;
+    if (nnal > 0 && z * nnal < GATHER_MIN_WG) z = (GATHER_MIN_WG + nnal - 1) / nnal;
+    return (int)(z < 1 ? 1 : (z > 16 ? 16 : z));
 }
 /* Two chunk sets per thread in turn, the next chunk's loads in flight while
  * one is assembled (round 5: 0.142 against 0.146 ms per config-3 launch for
@@ -3951,7 +3958,7 @@ __global__ __launch_bounds__(256) void k_dyn_synth(uint8_t *__restrict__ src, Dy
 int dyn_launch_code(hipStream_t hs, int nframes, int S, DevStream *st, const NalDesc *nal,
                     int ld_nal, const PlanPending *pend, DynFrame *dfr, int ld_fr,
                     const DynGeom *g, const uint8_t *src, const uint8_t *refs, const DynScratch *x,
-                    uint32_t epoch, int mbw, uint64_t *stamps, const DynFork *fk)
+                    uint32_t epoch, int mbw, uint64_t *stamps, const DynFork *fk, hipEvent_t ev0, hipEvent_t ev1)
 {
     if (nframes <= 0 || S <= 0) return 0;
     {                                   /* the tzrb table, once per device (and process) */
@@ -3990,11 +3997,13 @@ int dyn_launch_code(hipStream_t hs, int nframes, int S, DevStream *st, const Nal
                                 hipFuncAttributeMaxDynamicSharedMemorySize, rl) != hipSuccess)
             return -1;
     }
+    if (ev0 && hipEventRecord(ev0, hs) != hipSuccess) return -1;
     hipLaunchKernelGGL(k_dyn_row<false>, dim3(g->h, nframes, S), dim3(row_threads(g->w)),
                        row_lds_bytes(g->w), hs, st, nal, ld_nal, pend, dfr, ld_fr, *g, x->rows, src, refs,
                        x->meta, x->body_lo, x->body_hi, x->body_w, x->tcx, epoch, x->rowstage, x->gbits, x->spill,
                        x->ctr, x->heads, stamps);
     if (hipGetLastError() != hipSuccess) return -1;
+    if (ev1 && hipEventRecord(ev1, hs) != hipSuccess) return -1;
     /* the general path: one row workgroup per record slot that may be taken */
     hipLaunchKernelGGL(k_dyn_row<true>, dim3(g->h, std::min<uint32_t>(g->gen_cap, (uint32_t)(nframes * S)), 1),
                        dim3(row_threads(g->w)),
@@ -4053,7 +4062,7 @@ int dyn_launch_emit(hipStream_t hs, int nframes, int S, const DevStream *st, con
     const dim3 grid(nframes, S, GATHER_Z);
     const size_t gl = x ? gtab_bytes(g->ngroups, false) : 0;     /* the group tables (RS) */
     if (x && !(g->debug & SCROLL_DEBUG_DYN_GATHER1))
-        hipLaunchKernelGGL(k_dyn_gather, dim3(nframes, S, gather_z(*g)), dim3(DT), gl, hs, st, nal, ld_nal, dfr,
+        hipLaunchKernelGGL(k_dyn_gather, dim3(nframes, S, gather_z(*g, (int64_t)nframes * S)), dim3(DT), gl, hs, st, nal, ld_nal, dfr,
                            ld_fr, *g, stage, rs, gbits, arena, ld_arena, stamps);
     else if (x && big)
         hipLaunchKernelGGL((k_dyn_emit_gather<4, true>), grid, dim3(DT), gl, hs, st, nal, ld_nal, dfr, ld_fr, *g,

@@ -1329,10 +1329,13 @@ static int launch(ScrollBatch *b, int nframes, int plan_mode, int nal_max, hipSt
     const bool hint = b->hint_on && plan_mode != SCROLL_PLAN_EXPLICIT;
     const bool dyn = (b->dyn_on || hint) && plan_mode != SCROLL_PLAN_EXPLICIT;   /* staged NALs */
     const bool lite = b->timing == 2;
+    /* lite with the row coder: its pair goes right around k_dyn_row
+     * (dyn_launch_code), not around the whole code step */
+    const bool lite_row = lite && dyn && !hint;
     auto mark = [&](int k) -> int {
         if (!b->timing || (!dyn && k != 0 && k != 1 && k != 4)) return SCROLL_OK;
         if (lite) {                     /* the dominant kernel's pair, ring only */
-            if (k == 1 || k == (dyn ? 6 : 4)) HIPCHK(hipEventRecord(rev[k], hs));
+            if ((k == 1 || k == (dyn ? 6 : 4)) && !lite_row) HIPCHK(hipEventRecord(rev[k], hs));
             return SCROLL_OK;
         }
         HIPCHK(hipEventRecord(b->ev[k], hs));
@@ -1432,7 +1435,8 @@ static int launch(ScrollBatch *b, int nframes, int plan_mode, int nal_max, hipSt
                 fk = &b->fork;
             }
             if (dyn_launch_code(hs, nframes, S, b->d_st, b->d_nal, b->ld_nal, b->d_pend, b->d_dfr, ld_fr, &G,
-                                b->d_src, b->d_refs, &b->dx, b->dx.epoch, b->dyn_pw / 16, stamps, fk)) {
+                                b->d_src, b->d_refs, &b->dx, b->dx.epoch, b->dyn_pw / 16, stamps, fk,
+                                lite_row ? rev[1] : nullptr, lite_row ? rev[6] : nullptr)) {
                 set_err("k_dyn_code launch: %s", hipGetErrorString(hipGetLastError()));
                 return SCROLL_ERR_HIP;
             }

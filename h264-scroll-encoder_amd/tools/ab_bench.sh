@@ -8,10 +8,11 @@ O=$1; shift
 mkdir -p "$O"
 export TMPDIR=/tmp
 W=${AB_WORKLOAD:-p720dyn}
+A=${AB_ARGS:-}          # extra bench.py arguments, e.g. "--frames 1 --steps 50"
 for rep in 1 2; do
     for v in "$@" cur; do
         if [ "$v" = cur ]; then L=""; else L=variants/$v/libh264scroll.so; fi
-        H264SCROLL_LIB=$L timeout -k 10 200 python3 bench.py --steps 20 --warmup 3 --no-cpu --no-host --workload $W > "$O/bench_${v}_$rep.json" 2> "$O/bench_${v}_$rep.err"
+        H264SCROLL_LIB=$L timeout -k 10 200 python3 bench.py --steps 20 --warmup 3 --no-cpu --no-host --workload $W $A > "$O/bench_${v}_$rep.json" 2> "$O/bench_${v}_$rep.err"
     done
 done
 echo done > "$O/DONE"

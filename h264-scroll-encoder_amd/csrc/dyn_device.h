@@ -1166,10 +1166,12 @@ constexpr LvTab make_lvt()
  *     from them;
  *   - the level loop as in cavlc_body;
  *   - total_zeros + run_before as one field from the entry.
- * Same bits, TotalCoeff, TrailingOnes and ok as cavlc_body<CAP, true>. */
+ * Same bits, TotalCoeff, TrailingOnes and ok as cavlc_body<CAP, true>.
+ * bx: level i is byte i ^ bx of lb (k_dyn_row's records with their dwords
+ * swizzled per slot, so lanes on consecutive slots read different banks) */
 template <class CAP>
 __device__ __host__ inline int cavlc_body_t(CAP &cap, const int8_t *lb, uint32_t nz, uint32_t tzrb, int &t1o,
-                                            bool &ok, const uint32_t *lvt)
+                                            bool &ok, const uint32_t *lvt, uint32_t bx = 0)
 {
     const int tc = __builtin_popcount(nz);
     /* g: the mask shifted up one with a guard bit 0 -- clz(g) <= 31, and
@@ -1181,7 +1183,7 @@ __device__ __host__ inline int cavlc_body_t(CAP &cap, const int8_t *lb, uint32_t
     const uint32_t g2 = g1 & ~((0x80000000u >> c1) & ~1u);
     const int c2 = __builtin_clz(g2);
     const uint32_t g3 = g2 & ~((0x80000000u >> c2) & ~1u);
-    const int v0 = lb[30 - c0], v1 = lb[30 - c1], v2 = lb[30 - c2];
+    const int v0 = lb[(30 - c0) ^ (int)bx], v1 = lb[(30 - c1) ^ (int)bx], v2 = lb[(30 - c2) ^ (int)bx];
     /* a level is a trailing one iff it exists (not the guard) and is +-1 */
     const bool o0 = c0 < 31 && v0 * v0 == 1, o1 = o0 && c1 < 31 && v1 * v1 == 1;
     const bool o2 = o1 && c2 < 31 && v2 * v2 == 1;
@@ -1236,12 +1238,12 @@ __device__ __host__ inline int cavlc_body_t(CAP &cap, const int8_t *lb, uint32_t
     const CAP cap0 = cap;
     bool big = false;
     int pn = top_bit(m);
-    int vn = (int)lb[pn];
+    int vn = (int)lb[pn ^ (int)bx];
     for (int k = t1; k < tc; ++k) {                        /* levels below the trailing ones */
         const int v = vn;
         m &= ~(1u << pn);
         pn = top_bit(m);
-        vn = (int)lb[pn];
+        vn = (int)lb[pn ^ (int)bx];
         const int vc = v < -LVT_V ? -LVT_V : (v > LVT_V ? LVT_V : v);
         big |= vc != v;
         const uint32_t e = lvt[cls * LVT_W + vc + LVT_V + 1];
@@ -1257,7 +1259,7 @@ __device__ __host__ inline int cavlc_body_t(CAP &cap, const int8_t *lb, uint32_t
         for (int k = t1; k < tc; ++k) {
             const int p = top_bit(m);
             m &= ~(1u << p);
-            const uint32_t e = level_code((int)lb[p], cls);
+            const uint32_t e = level_code((int)lb[p ^ (int)bx], cls);
             push(acc, an, e & 0x1fffu, (e >> 13) & 31u, cap);
             cls = (int)(e >> 18);
         }
@@ -1266,7 +1268,7 @@ __device__ __host__ inline int cavlc_body_t(CAP &cap, const int8_t *lb, uint32_t
     for (int k = t1; k < tc; ++k) {
         const int p = top_bit(m);
         m &= ~(1u << p);
-        const uint32_t e = level_code((int)lb[p], cls);
+        const uint32_t e = level_code((int)lb[p ^ (int)bx], cls);
         push(acc, an, e & 0x1fffu, (e >> 13) & 31u, cap);
         cls = (int)(e >> 18);
     }

@@ -1169,6 +1169,23 @@ __device__ inline void put_piece(uint32_t *buf, uint32_t p0, uint32_t n, uint32_
  * starts in is a same-address LDS conflict (k_dyn_row's conflicts 112 ->
  * 91 M per config-3 launch, its time equal within noise) */
 constexpr uint32_t ROW_PAD = 4;
+
+/* SCROLL_LV_SWZ=1 (measured, not kept): k_dyn_row's level records between
+ * the sort and the CAVLC bodies with dword d of the record in slot s at
+ * d ^ lv_key(s) (an involution), swizzled in the sort's pass -- LDS bank
+ * conflicts 91 -> 68 M per config-3 launch, but k_dyn_row 1.206 -> 1.232 ms
+ * (the extra record read / permute / write per block costs more than the
+ * conflicts did; profiles/r06j_lds_swizzle_p720dyn.txt) */
+#ifndef SCROLL_LV_SWZ
+#define SCROLL_LV_SWZ 0
+#endif
+__device__ inline uint32_t lv_key(int slot) { return ((uint32_t)slot >> 4) & 3u; }
+__device__ inline uint4 lv_swz(uint4 v, uint32_t key)
+{
+    if (key & 1u) v = make_uint4(v.y, v.x, v.w, v.z);
+    if (key & 2u) v = make_uint4(v.z, v.w, v.x, v.y);
+    return v;
+}
 __device__ inline void put_piece1(uint32_t *buf, uint32_t pos, uint32_t tv, uint32_t tl, uint4 b, uint32_t bl)
 {
     const uint32_t tw = tv & low_mask((int)tl);
@@ -2070,9 +2087,19 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
 #else
             const int tcs = __builtin_popcount(mt[slot]);
 #endif
-            if (tcs)
+            if (tcs) {
                 order[L.kc[1][SORT_KEYS - 1 - min(tcs, SORT_KEYS - 1)] + lo[slot]] =
                     (uint16_t)(slot | (task < 16 * w ? 0 : 0x8000));
+#if SCROLL_LV_SWZ
+                /* the record's dwords swizzled by its slot (lv_key): the
+                 * CAVLC lanes read one level byte each from records on
+                 * about consecutive slots (the sort's ranks follow the
+                 * lanes), 16 bytes apart -- four banks -- so lanes 16 slots
+                 * apart met in one bank; with dword d at d ^ key they don't */
+                const uint32_t key = lv_key(slot);
+                if (key) lv[slot] = lv_swz(lv[slot], key);
+#endif
+            }
         }
         __syncthreads();
     ROW_CUT(1);
@@ -2095,10 +2122,13 @@ __global__ __launch_bounds__(ROW_MAXT) __attribute__((amdgpu_waves_per_eu(SCROLL
             const uint32_t nz = mt[slot];                   /* the non-zero mask (levels phase) */
 #endif
             const uint32_t tzrb = g_tzrb[luma ? nz : 65536u + nz];
-            const int tc = cavlc_body_t(cap, reinterpret_cast<const int8_t *>(lv + slot), nz, tzrb, t1, ok, L.lvt);
+            const uint32_t key = SCROLL_LV_SWZ ? lv_key(slot) : 0u;
+            const int tc = cavlc_body_t(cap, reinterpret_cast<const int8_t *>(lv + slot), nz, tzrb, t1, ok, L.lvt,
+                                        key << 2);
             mt[slot] = ok ? (uint16_t)(cap.n | (uint32_t)tc << 8 | (uint32_t)t1 << 13)
                           : (uint16_t)((uint32_t)tc << 8 | (uint32_t)t1 << 13 | M_OVF);
             if (ok) lv[slot] = body_msb(cap.hi, cap.lo, cap.n);
+            else if (key) lv[slot] = lv_swz(lv[slot], key);     /* rare: the levels stay, in plain order */
         }
     } else {
         /* general path: records of k_dyn_code_general */

@@ -88,7 +88,12 @@ typedef struct {
 #define DYN_MAX_H 256               /* rect height limit (MBs): a whole 4K frame   */
 #define DYN_MAX_MBW 512             /* picture width limit with the rect (MBs)   */
 #define DYN_MAX_MBH 512             /* picture height limit with the rect (MBs)  */
-#define DYN_STATIC_ROWS 64          /* MB rows per static k_dyn_group row group (4 measured slower) */
+#ifndef DYN_STATIC_ROWS
+/* MB rows per static row group (k_dyn_static, one wave each): round 6 64 ->
+ * 16, config 5's 88 static rows in 6 groups instead of 2 (2.872 -> 2.833 ms
+ * per step; 8: the same, 32: 2.891; 4 measured slower in round 3) */
+#define DYN_STATIC_ROWS 16
+#endif
 #define DYN_PIECES 26               /* coded pieces per dynamic MB: 16 luma, 2 DC, 8 AC */
 #define DYN_OVF_BYTES 8192          /* staging-slot tail: levels of > 128-bit blocks */
 #ifndef SCROLL_DYN_ROW_KBITS

@@ -17,7 +17,9 @@
 #include <stddef.h>
 #include <stdint.h>
 
-#define IPCM_CHUNK 4096              /* RBSP bytes per workgroup              */
+#ifndef IPCM_CHUNK
+#define IPCM_CHUNK 4096              /* RBSP bytes per workgroup (16 per thread) */
+#endif
 #define IPCM_PRE_MAX 96              /* SPS + PPS NAL units + IDR start code   */
 
 typedef struct {
@@ -43,3 +45,21 @@ typedef struct {
 int ipcm_launch(hipStream_t hs, int pass, int n, const IpcmGeom *g, const uint8_t *pics,
                 uint32_t *counts, uint8_t *out, uint8_t *stg, uint64_t stg_stride, uint64_t *sizes,
                 uint32_t *over, uint32_t *sticky);
+
+/* the one pass (round 6): usable when out_stride >= ipcm_worst(g), so that no
+ * file can overflow.  hw: n x nchunk hand-off words, tagged with epoch (24
+ * bits, never 0, a new one per call; the words start zeroed); sizes: n u64;
+ * *over (and *sticky) set only if a look-back wait expired (a broken
+ * dispatch; no file of the call is then complete) */
+typedef struct {
+    unsigned long long *hw;
+    uint32_t epoch;
+    uint64_t *sizes;
+    uint32_t *sticky;
+} IpcmOnePass;
+static inline uint64_t ipcm_worst(const IpcmGeom *g)
+{
+    return (uint64_t)g->npre + g->rbsp_len + (g->rbsp_len + 1u) / 2u;   /* an EP byte per two RBSP bytes at most */
+}
+int ipcm_launch_onepass(hipStream_t hs, int n, const IpcmGeom *g, const uint8_t *pics, uint8_t *out,
+                        uint32_t *over, const IpcmOnePass *op);

@@ -13,6 +13,15 @@
  *   pass 1  the same bytes + the EP bytes at the chunk's output offset
  *           (prefix + RBSP offset + EP bytes of the earlier chunks);
  *           whole 16-byte lines stored aligned, edge lines byte by byte
+ *   one pass (round 6, IP_ONEPASS, opt-in: SCROLL_IPCM_ONEPASS=1, when
+ *           out_stride holds the worst case so no file can overflow; less
+ *           traffic, more time -- scroll_kernels.hip): both in one workgroup -- the chunk's EP
+ *           count published, the counts of the earlier chunks of its file
+ *           found by a decoupled look-back (workgroups start in grid order,
+ *           so every earlier chunk has started or will), the bytes written
+ *           from registers.  The pictures are read once and nothing is
+ *           staged: the count pass's RBSP copy (written, then read back) and
+ *           its second reading of the pictures are gone
  *
  * The bits are those of oracle/scroll_oracle.c or_ipcm_picture_file
  * (tests/test_gpu_ipcm.py), which for the striped pictures is pinned to the
@@ -29,7 +38,8 @@ using namespace scroll::stage;
 
 namespace {
 
-constexpr int IT = 256;                     /* threads per workgroup            */
+constexpr int IT = IPCM_CHUNK / 16;         /* threads per workgroup            */
+constexpr int IP_WAVES = IT / 64;
 constexpr int LB = 64;                      /* look-back bytes staged before it */
 constexpr uint32_t CH = IPCM_CHUNK;
 static_assert(CH == 16 * IT, "16 RBSP bytes per thread");
@@ -72,24 +82,48 @@ __device__ inline uint32_t rbsp_at(const IpcmGeom &G, const uint8_t *pic, uint32
     return pic[a];
 }
 
-enum { IP_COUNT = 0, IP_WRITE = 1, IP_WRITE_STAGED = 2 };
+enum { IP_COUNT = 0, IP_WRITE = 1, IP_WRITE_STAGED = 2, IP_ONEPASS = 3 };
+
+/* the one-pass hand-off word of a chunk: the call's epoch (24 bits) << 40 |
+ * inclusive flag << 39 | EP bytes (of the chunk alone, or of the file up to
+ * and including it); relaxed agent-scope atomics, no fence (ingest's note:
+ * an agent-scope release / acquire writes back / invalidates the XCD's L2) */
+constexpr uint64_t IP_INCL = 1ull << 39, IP_VAL = IP_INCL - 1ull;
+constexpr uint64_t IP_WAIT_TICKS = 5000000ull;        /* 50 ms of waiting for an earlier chunk: the call fails */
+constexpr uint64_t IP_WAIT_GAP = 100000ull;           /* a longer gap between two polls is a preemption */
+__device__ inline uint64_t ip_load(unsigned long long *p)
+{
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ inline void ip_store(unsigned long long *p, uint64_t v)
+{
+    __hip_atomic_store(p, (unsigned long long)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
 template <int MODE>
 __global__ __launch_bounds__(IT) void k_ipcm(IpcmGeom G, const uint8_t *__restrict__ pics,
                                              uint32_t *__restrict__ counts, uint8_t *__restrict__ out,
                                              uint8_t *__restrict__ stg, uint64_t stg_stride,
-                                             uint32_t *__restrict__ over)
+                                             uint32_t *__restrict__ over, IpcmOnePass op)
 {
     constexpr bool WRITE = MODE != IP_COUNT;
+    constexpr bool ONE = MODE == IP_ONEPASS;
     if (!WRITE && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) *over = 0u;   /* k_ipcm_size sets it */
-    if (WRITE && __builtin_amdgcn_readfirstlane(*over)) return;    /* a file past out_stride: none written */
+    if (WRITE && !ONE && __builtin_amdgcn_readfirstlane(*over)) return;    /* a file past out_stride: none written */
     __shared__ alignas(16) uint8_t rb[LB + CH];
     __shared__ alignas(16) uint8_t ob[16 + CH + CH / 2 + 16];
-    __shared__ int32_t wsm[IT / 64];
-    __shared__ uint32_t wss[IT / 64];
+    __shared__ int32_t wsm[IP_WAVES];
+    __shared__ uint32_t wss[IP_WAVES];
     __shared__ int32_t deep;
+    __shared__ uint32_t s_pre, s_late;
     const int t = threadIdx.x;
     const uint32_t c = blockIdx.x, n = blockIdx.y;
+    /* one pass: the workgroups start in grid order (x fastest, in order on
+     * each XCD), so every earlier chunk of the file has started or will start
+     * without waiting for this one; the wait is bounded all the same.  (A
+     * ticket from one global counter instead, as ingest takes its segments:
+     * 86 K same-address atomics per call, 1.10 against 0.58 ms.) */
+    if (ONE && c == 0 && n == 0 && t == 0) *over = 0u;   /* set only by a wait that expired */
     const uint8_t *pic = pics + (size_t)n * G.pic_stride;
     const uint32_t c0 = c * CH, c1 = min(c0 + CH, G.rbsp_len);
     uint8_t *S = stg ? stg + (size_t)n * stg_stride : nullptr;       /* the file's RBSP (count pass) */
@@ -222,7 +256,7 @@ __global__ __launch_bounds__(IT) void k_ipcm(IpcmGeom G, const uint8_t *__restri
     for (int k = 0; k < 4; ++k)
         if (qw[k]) mylast = (int)g0 + 4 * k + 3 - (__builtin_clz(qw[k]) >> 3);
     int pm, tmax;
-    block_excl_max(mylast, wsm, pm, tmax);                /* its barriers publish deep */
+    block_excl_max<IP_WAVES>(mylast, wsm, pm, tmax);                /* its barriers publish deep */
     int carry = -1;
     if (c0 > 0) {
         carry = deep;
@@ -279,16 +313,71 @@ __global__ __launch_bounds__(IT) void k_ipcm(IpcmGeom G, const uint8_t *__restri
         }
     }
     uint32_t ex, tot;
-    block_excl_sum(cnt, wss, ex, tot);
+    block_excl_sum<IP_WAVES>(cnt, wss, ex, tot);
     if (!WRITE) {
         if (t == 0) counts[(size_t)n * G.nchunk + c] = tot;
         return;
     }
     /* EP bytes of the earlier chunks of this file */
-    uint32_t pre = 0;
-    for (uint32_t k = (uint32_t)t; k < c; k += IT) pre += counts[(size_t)n * G.nchunk + k];
-    uint32_t pex, ptot;
-    block_excl_sum(pre, wss, pex, ptot);
+    uint32_t ptot;
+    if (ONE) {
+        if (t < 64) {                                   /* wave 0: publish, look back, publish */
+            const int lane = t;
+            const uint64_t tag = (uint64_t)op.epoch << 40;
+            unsigned long long *H = op.hw + (size_t)n * G.nchunk;
+            if (lane == 0) ip_store(&H[c], tag | (c == 0 ? IP_INCL : 0ull) | tot);
+            uint64_t excl = 0, prevt = __builtin_amdgcn_s_memrealtime(), waited = 0;
+            bool late = false;
+            /* the earlier chunks 64 at a time, nearest first: the sum of
+             * their counts down to the nearest one with its file prefix */
+            for (int64_t hi = (int64_t)c - 1; hi >= 0 && !late;) {
+                const int64_t u = hi - lane;
+                uint64_t q = 0;
+                bool val = u < 0;                       /* before chunk 0: nothing (never reached) */
+                for (;;) {
+                    if (!val) {
+                        q = ip_load(&H[u]);
+                        val = (q >> 40) == (uint64_t)op.epoch;
+                    }
+                    const uint64_t mi = __builtin_amdgcn_ballot_w64(u >= 0 && val && (q & IP_INCL));
+                    const int li = mi ? __builtin_ctzll(mi) : 63;
+                    const uint64_t needm = li == 63 ? ~0ull : ((2ull << li) - 1ull);
+                    if ((__builtin_amdgcn_ballot_w64(val) & needm) == needm) {
+                        const uint32_t v = (u >= 0 && lane <= li) ? (uint32_t)(q & IP_VAL) : 0u;
+                        excl += __shfl(wave_incl_sum(v, lane), 63, 64);
+                        hi = mi ? -1 : hi - 64;
+                        break;
+                    }
+                    const uint64_t now = __builtin_amdgcn_s_memrealtime(), gap = now - prevt;
+                    prevt = now;
+                    if (gap < IP_WAIT_GAP) waited += gap;
+                    if (waited > IP_WAIT_TICKS) {
+                        late = true;
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                }
+            }
+            if (lane == 0) {
+                if (c > 0 && !late) ip_store(&H[c], tag | IP_INCL | (excl + tot));
+                s_pre = (uint32_t)excl;
+                s_late = late;
+                if (late) {                             /* a broken dispatch: the call fails */
+                    atomicOr(over, 1u);
+                    if (op.sticky) atomicOr(op.sticky, 1u);
+                }
+                if (!late && c + 1 == G.nchunk) op.sizes[n] = (uint64_t)G.npre + G.rbsp_len + excl + tot;
+            }
+        }
+        __syncthreads();
+        if (s_late) return;
+        ptot = s_pre;
+    } else {
+        uint32_t pre = 0;
+        for (uint32_t k = (uint32_t)t; k < c; k += IT) pre += counts[(size_t)n * G.nchunk + k];
+        uint32_t pex;
+        block_excl_sum<IP_WAVES>(pre, wss, pex, ptot);
+    }
     uint8_t *F = out + (size_t)n * G.out_stride;
     const uint64_t O = (uint64_t)G.npre + c0 + ptot;            /* file offset of RBSP byte c0 */
     const uint32_t sh = (uint32_t)(reinterpret_cast<uintptr_t>(F + O) & 15u);
@@ -333,7 +422,7 @@ __global__ __launch_bounds__(IT) void k_ipcm_size(IpcmGeom G, const uint32_t *__
     uint32_t ep = 0;
     for (uint32_t k = (uint32_t)t; k < G.nchunk; k += IT) ep += counts[(size_t)n * G.nchunk + k];
     uint32_t ex, tot;
-    block_excl_sum(ep, wss, ex, tot);
+    block_excl_sum<IP_WAVES>(ep, wss, ex, tot);
     if (t == 0) {
         const uint64_t sz = (uint64_t)G.npre + G.rbsp_len + tot;
         sizes[n] = sz;
@@ -351,17 +440,27 @@ int ipcm_launch(hipStream_t hs, int pass, int n, const IpcmGeom *g, const uint8_
                 uint32_t *sticky)
 {
     if (n <= 0) return 0;
+    const IpcmOnePass none{};
     if (pass == 0) {
         hipLaunchKernelGGL(k_ipcm<IP_COUNT>, dim3(g->nchunk, n), dim3(IT), 0, hs, *g, pics, counts, out, stg,
-                           stg_stride, over);
+                           stg_stride, over, none);
         if (hipGetLastError() != hipSuccess) return -1;
         hipLaunchKernelGGL(k_ipcm_size, dim3(n), dim3(IT), 0, hs, *g, counts, sizes, over, sticky);
     } else if (stg) {
         hipLaunchKernelGGL(k_ipcm<IP_WRITE_STAGED>, dim3(g->nchunk, n), dim3(IT), 0, hs, *g, pics, counts, out,
-                           stg, stg_stride, over);
+                           stg, stg_stride, over, none);
     } else {
         hipLaunchKernelGGL(k_ipcm<IP_WRITE>, dim3(g->nchunk, n), dim3(IT), 0, hs, *g, pics, counts, out, stg,
-                           stg_stride, over);
+                           stg_stride, over, none);
     }
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int ipcm_launch_onepass(hipStream_t hs, int n, const IpcmGeom *g, const uint8_t *pics, uint8_t *out,
+                        uint32_t *over, const IpcmOnePass *op)
+{
+    if (n <= 0) return 0;
+    hipLaunchKernelGGL(k_ipcm<IP_ONEPASS>, dim3(g->nchunk, n), dim3(IT), 0, hs, *g, pics, nullptr, out, nullptr,
+                       0ull, over, *op);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

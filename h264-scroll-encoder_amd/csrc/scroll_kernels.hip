@@ -985,6 +985,10 @@ struct ScrollBatch {
     size_t ipcm_cap = 0;
     uint8_t *d_ipcm_stg = nullptr;              /* count pass RBSP for the write pass */
     size_t ipcm_stg_cap = 0;
+    /* the one pass: the chunks' hand-off words */
+    unsigned long long *d_ipcm_hw = nullptr;
+    size_t ipcm_hw_cap = 0;
+    uint32_t ipcm_epoch = 0;
     double ipcm_ms = 0.0;
     int ipcm_n = 0;
     /* the asynchronous I_PCM calls since the last sync: their overflow flag
@@ -1150,6 +1154,7 @@ void scroll_batch_destroy(ScrollBatch *b)
     (void)hipFree(b->d_ing_in);
     (void)hipFree(b->d_ipcm_cnt);
     (void)hipFree(b->d_ipcm_stg);
+    (void)hipFree(b->d_ipcm_hw);
     (void)hipFree(b->d_ing_files);
     (void)hipFree(b->d_ing_scan);
     (void)hipFree(b->d_ing_out);
@@ -3072,12 +3077,31 @@ static int ipcm_files(ScrollBatch *b, int n, int w, int h, const uint8_t *d_pics
         }
         b->ipcm_cap = need;
     }
+    /* SCROLL_IPCM_ONEPASS=1: the one pass when no file can overflow
+     * out_stride -- 1.54x the algorithmic bytes instead of 2.50x, but 0.67
+     * against 0.57 ms per ipcm720 call (its look-back holds each workgroup
+     * for a round trip; profiles/r06o_ipcm_onepass.txt), so not the default */
+    const bool one = getenv("SCROLL_IPCM_ONEPASS") != nullptr && out_stride >= ipcm_worst(&g);
+    if (one && (size_t)n * g.nchunk > b->ipcm_hw_cap) {
+        if (async && b->ipcm_over) HIPCHK(hipStreamSynchronize(b->own));
+        (void)hipFree(b->d_ipcm_hw);
+        b->d_ipcm_hw = nullptr;
+        b->ipcm_hw_cap = 0;
+        const size_t words = (size_t)n * g.nchunk;
+        hipError_t e = hipMalloc(&b->d_ipcm_hw, words * sizeof(unsigned long long));
+        if (e != hipSuccess) {
+            set_err("scroll_batch_ipcm_files: %s", hipGetErrorString(e));
+            return e == hipErrorOutOfMemory ? SCROLL_ERR_OOM : SCROLL_ERR_HIP;
+        }
+        HIPCHK(hipMemsetAsync(b->d_ipcm_hw, 0, words * sizeof(unsigned long long), b->own));
+        b->ipcm_hw_cap = words;
+    }
     /* the write pass reads the count pass's RBSP while that scratch stays
      * under 4 GB, else it generates the bytes again */
     const uint64_t stg_stride = (uint64_t)g.nchunk * IPCM_CHUNK;
     const size_t stg_need = (size_t)n * stg_stride;
     uint8_t *stg = nullptr;
-    if (getenv("SCROLL_IPCM_RECOMPUTE") == nullptr && stg_need <= ((size_t)4 << 30)) {
+    if (!one && getenv("SCROLL_IPCM_RECOMPUTE") == nullptr && stg_need <= ((size_t)4 << 30)) {
         if (stg_need > b->ipcm_stg_cap) {
             (void)hipFree(b->d_ipcm_stg);
             b->d_ipcm_stg = nullptr;
@@ -3122,8 +3146,15 @@ static int ipcm_files(ScrollBatch *b, int n, int w, int h, const uint8_t *d_pics
     /* count pass, sizes and the overflow check, write pass: no host step in
      * between (the write pass writes nothing when a file is over) */
     uint32_t *sticky = async ? b->d_ipcm_sticky : nullptr;
-    if (ipcm_launch(hs, 0, n, &g, d_pics, b->d_ipcm_cnt, d_out, stg, stg_stride, d_sizes, d_over, sticky) ||
-        ipcm_launch(hs, 1, n, &g, d_pics, b->d_ipcm_cnt, d_out, stg, stg_stride, d_sizes, d_over, sticky)) {
+    if (one) {
+        b->ipcm_epoch = b->ipcm_epoch % 0xffffffu + 1u;          /* 24 bits, never 0 */
+        const IpcmOnePass op{b->d_ipcm_hw, b->ipcm_epoch, d_sizes, sticky};
+        if (ipcm_launch_onepass(hs, n, &g, d_pics, d_out, d_over, &op)) {
+            set_err("ipcm launch: %s", hipGetErrorString(hipGetLastError()));
+            return SCROLL_ERR_HIP;
+        }
+    } else if (ipcm_launch(hs, 0, n, &g, d_pics, b->d_ipcm_cnt, d_out, stg, stg_stride, d_sizes, d_over, sticky) ||
+               ipcm_launch(hs, 1, n, &g, d_pics, b->d_ipcm_cnt, d_out, stg, stg_stride, d_sizes, d_over, sticky)) {
         set_err("ipcm launch: %s", hipGetErrorString(hipGetLastError()));
         return SCROLL_ERR_HIP;
     }

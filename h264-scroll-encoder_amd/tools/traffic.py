@@ -47,6 +47,8 @@ def main():
     for k in a.kernel.split(","):
         fk = per_dispatch(a.fetch_dir, "FETCH_SIZE", k)
         wk = per_dispatch(a.write_dir, "WRITE_SIZE", k)
+        if not fk or not wk:                        # a kernel this build does not launch
+            continue
         raw += 1024 * sum(fk) / len(fk)             # KB -> bytes
         write += 1024 * sum(wk) / len(wk)
         nd.append([k, len(fk), len(wk)])

@@ -153,6 +153,26 @@ def test_generating_write_pass_matches(gpu, hip, oracle, monkeypatch, w, h):
         assert (t == 0xAB).all(), "bytes written past the file"
 
 
+@pytest.mark.parametrize("w,h", [(16, 16), (176, 144), (1280, 720)])
+def test_onepass_matches(gpu, hip, oracle, monkeypatch, w, h):
+    """SCROLL_IPCM_ONEPASS (round 6, opt-in): count and write in one
+    workgroup, the file offsets by a decoupled look-back over the chunks'
+    hand-off words; same files, nothing past them -- twice on one batch, so
+    the second call's words carry a new epoch over the first's"""
+    kinds = ["rand", "zero", "low", "sparse", "a"]
+    pics = pictures(w, h, kinds, seed=5 * w + h)
+    monkeypatch.setenv("SCROLL_IPCM_ONEPASS", "1")
+    b = gpu.Batch(1, 1, 1 << 20, device=0)
+    try:
+        for rep in range(2):
+            files, tails = gpu_files(gpu, hip, w, h, pics[rep:] + pics[:rep], b=b)
+            for k, (p, f, t) in enumerate(zip(pics[rep:] + pics[:rep], files, tails)):
+                assert f == ipcm_file(oracle, w, h, p), f"{k} {w}x{h} call {rep}"
+                assert (t == 0xAB).all(), "bytes written past the file"
+    finally:
+        b.close()
+
+
 def test_4k_pictures(gpu, hip, oracle, golden_md5):
     w, h = 3840, 2160
     pics = pictures(w, h, ["a", "zero"])

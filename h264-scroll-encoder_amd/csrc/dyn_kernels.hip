@@ -560,7 +560,10 @@ __device__ inline void code_frame(const DevStream *__restrict__ st,
 /* grid (chunks, CODE_GEN_Y): workgroup (c, y) codes chunk c of the flagged
  * NALs y, y + CODE_GEN_Y, ... of k_dyn_rows' list (ctr[1] of them, as
  * k_dyn_row<true> reads it): with none flagged a launch reads one word */
-constexpr int CODE_GEN_Y = 64;
+#ifndef SCROLL_CODE_GEN_Y
+#define SCROLL_CODE_GEN_Y 64        /* 16 measured: the no-op launch 4.3 us, the step the same */
+#endif
+constexpr int CODE_GEN_Y = SCROLL_CODE_GEN_Y;
 __global__ __launch_bounds__(CODE_T) void k_dyn_code_general(const DevStream *__restrict__ st,
                                                              const DynFrame *__restrict__ dfr, int ld_fr,
                                                              const PlanPending *__restrict__ pend,

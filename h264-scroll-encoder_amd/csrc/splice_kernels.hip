@@ -2093,6 +2093,10 @@ __device__ inline uint32_t bits_at(const uint32_t *w, uint32_t q)
     return o ? (w[k] << o) | (w[k + 1] >> (32u - o)) : w[k];
 }
 
+#ifndef SCROLL_STAGE_BL_PRELOAD
+#define SCROLL_STAGE_BL_PRELOAD 1
+#endif
+
 /* n bits at bit q of the RBSP words, put */
 template <class SK>
 __device__ inline void put_rbsp(SK &sk, const uint32_t *rb, uint32_t q0, uint32_t n)
@@ -2143,6 +2147,20 @@ __device__ inline void splice_tail(SK &sk, const SpliceMbRec &h, const SpliceMbR
     }
     if constexpr (count) sk.n += h.body;
     uint32_t rp = h.res_off;                    /* the external bits: pieces contiguous in syntax order */
+    /* the pieces' u16 words, all at once (7 8-byte loads; records are 8-byte
+     * aligned): per piece only its body's bit loads remain on the chain */
+    uint32_t blw[(SPLICE_PIECES + 1) / 2] = {};
+#if SCROLL_STAGE_BL_PRELOAD
+    if constexpr (!count) {
+        const uint2 *bq = reinterpret_cast<const uint2 *>(R->bl);
+#pragma unroll
+        for (int q = 0; q < (SPLICE_PIECES + 1) / 4; ++q) {
+            const uint2 v = bq[q];
+            blw[2 * q] = v.x;
+            blw[2 * q + 1] = v.y;
+        }
+    }
+#endif
     auto piece = [&](int i, int nC) {
         const int tc = h.tc[i], t1 = h.t1[i];
         uint32_t v, len;
@@ -2156,7 +2174,7 @@ __device__ inline void splice_tail(SK &sk, const SpliceMbRec &h, const SpliceMbR
         }
         sk.put(v, (int)len);
         if constexpr (!count) {
-            const uint32_t e = R->bl[i];
+            const uint32_t e = SCROLL_STAGE_BL_PRELOAD ? (blw[i >> 1] >> (16 * (i & 1))) & 0xffffu : R->bl[i];
             rp += e >> 11;                      /* past its external coeff_token */
             put_rbsp(sk, rb, rp, e & 2047u);
             rp += e & 2047u;

@@ -2322,7 +2322,7 @@ static int hd_setup(ScrollBatch *b)
 {
     const size_t S = (size_t)b->max_streams, F = (size_t)b->max_frames;
     const size_t nmb = (size_t)b->geo.w * b->geo.h;
-    const size_t words = S * F * nmb * b->hd_mb_words + 2;   /* + bits_at's look-ahead */
+    const size_t words = S * F * nmb * b->hd_mb_words + 2 + RWIN_SLACK_WORDS;   /* + the stage's look-ahead */
     int rc;
     if (!b->d_spf) {
         HIPCHK(hipMalloc(&b->d_spf, S * F * sizeof(SpliceFrame)));
@@ -2616,7 +2616,7 @@ static int splice_upload(ScrollBatch *b)
         HIPCHK(hipMalloc(&b->d_spf, S * F * sizeof(SpliceFrame)));
     }
     if ((rc = sp_grow((void **)&b->d_sp_nal, &b->sp_nal_cap, pool.size(), 1)) ||
-        (rc = sp_grow((void **)&b->d_sp_rbsp, &b->sp_rbsp_cap, words, sizeof(uint32_t))) ||
+        (rc = sp_grow((void **)&b->d_sp_rbsp, &b->sp_rbsp_cap, words + RWIN_SLACK_WORDS, sizeof(uint32_t))) ||
         (rc = sp_grow((void **)&b->d_sp_rec, &b->sp_rec_cap, recs, sizeof(SpliceMbRec))) ||
         (rc = sp_grow((void **)&b->d_sp_list, &b->sp_list_cap, list.size(), sizeof(int32_t))) ||
         (rc = sp_grow((void **)&b->d_sp_units, &b->sp_units_cap, nunits, sizeof(SpliceUnit))))

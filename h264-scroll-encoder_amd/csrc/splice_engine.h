@@ -109,6 +109,9 @@ typedef struct {
     uint32_t bmv[16];
 } SpliceMbRec;
 #define SPLICE_REC_HEAD 96
+/* RBSP word pools: words past the last unit that k_splice_stage's body
+ * reader may load (splice_kernels.hip RWin) */
+#define RWIN_SLACK_WORDS 8
 
 
 /* 0, or -1 when the launch failed */

@@ -2096,6 +2096,50 @@ __device__ inline uint32_t bits_at(const uint32_t *w, uint32_t q)
 #ifndef SCROLL_STAGE_BL_PRELOAD
 #define SCROLL_STAGE_BL_PRELOAD 1
 #endif
+/* SCROLL_STAGE_RWIN=1 (measured, not kept): the body reader below --
+ * p720splicerows 5.09 -> 5.16 ms per step (profiles/r06s_stage_rwin.txt) */
+#ifndef SCROLL_STAGE_RWIN
+#define SCROLL_STAGE_RWIN 0
+#endif
+
+/* the writing sweep's reader of an MB's piece bodies: six RBSP words from
+ * word wb in registers, moved on one word as a read passes word wb, the
+ * word loaded then five words ahead -- the loads run ahead of the bits
+ * instead of one load round trip per body, and a read always takes w0 / w1
+ * (no selects: a select chain over the six became a scratch copy indexed
+ * per lane).  Reads up to 6 words past the MB's last bit: the word pools
+ * keep RWIN_SLACK_WORDS after their last unit */
+static_assert(RWIN_SLACK_WORDS >= 6, "RWin reads up to 6 words past an MB's last bit");
+struct RWin {
+    const uint32_t *rb;
+    uint32_t wb, w0, w1, w2, w3, w4, w5;
+    __device__ inline void init(const uint32_t *r, uint32_t q)
+    {
+        rb = r;
+        wb = q >> 5;
+        w0 = rb[wb];
+        w1 = rb[wb + 1];
+        w2 = rb[wb + 2];
+        w3 = rb[wb + 3];
+        w4 = rb[wb + 4];
+        w5 = rb[wb + 5];
+    }
+    /* the 32 bits from bit q (q >= 32 wb), MSB first */
+    __device__ inline uint32_t at(uint32_t q)
+    {
+        while ((q >> 5) > wb) {
+            w0 = w1;
+            w1 = w2;
+            w2 = w3;
+            w3 = w4;
+            w4 = w5;
+            w5 = rb[wb + 6];
+            ++wb;
+        }
+        const uint32_t o = q & 31u;
+        return o ? __builtin_amdgcn_alignbit(w0, w1, 32u - o) : w0;
+    }
+};
 
 /* n bits at bit q of the RBSP words, put */
 template <class SK>
@@ -2161,6 +2205,10 @@ __device__ inline void splice_tail(SK &sk, const SpliceMbRec &h, const SpliceMbR
         }
     }
 #endif
+    RWin win;
+    if constexpr (!count) {
+        if (SCROLL_STAGE_RWIN) win.init(rb, rp);
+    }
     auto piece = [&](int i, int nC) {
         const int tc = h.tc[i], t1 = h.t1[i];
         uint32_t v, len;
@@ -2176,8 +2224,16 @@ __device__ inline void splice_tail(SK &sk, const SpliceMbRec &h, const SpliceMbR
         if constexpr (!count) {
             const uint32_t e = SCROLL_STAGE_BL_PRELOAD ? (blw[i >> 1] >> (16 * (i & 1))) & 0xffffu : R->bl[i];
             rp += e >> 11;                      /* past its external coeff_token */
-            put_rbsp(sk, rb, rp, e & 2047u);
-            rp += e & 2047u;
+            const uint32_t n = e & 2047u;
+            if (SCROLL_STAGE_RWIN) {
+                for (uint32_t k = 0; k < n; k += 32) {
+                    const int c = (int)min(32u, n - k);
+                    sk.put(win.at(rp + k) >> (32 - c), c);
+                }
+            } else {
+                put_rbsp(sk, rb, rp, n);
+            }
+            rp += n;
         }
     };
     if (h.intra == 2) piece(26, nc_edge(0, h, l, t, al, at));

@@ -748,10 +748,13 @@ constexpr int LANE_WAVES = 1;
  * records written field by field, fewer slices per wave had paid (4.40 /
  * 4.08 / 4.34 ms at 64 / 32 / 16 slices per wave): each bit-reader wait
  * also waited for the wave's scattered stores.  With the records staged in
- * LDS and written whole, 64 is best (p720splicerows, rocprofv3: 2.62-2.65 /
- * 3.33 / 3.62 ms at 64 / 32 / 16) */
+ * LDS and written whole, 64 was best (p720splicerows, rocprofv3: 2.62-2.65 /
+ * 3.33 / 3.62 ms at 64 / 32 / 16).  Round 6, with the 232-byte records (the
+ * lane arrays a third smaller): 32 again, the whole step 5.06 -> 4.94 and
+ * 5.07 -> 5.01 ms in two alternating A/Bs (24: 5.88, 16: 6.14, 48: 5.01;
+ * profiles/r06v_splice_lpw.txt) */
 #ifndef SCROLL_SPLICE_LPW
-#define SCROLL_SPLICE_LPW 64
+#define SCROLL_SPLICE_LPW 32
 #endif
 constexpr int LANE_ACTIVE = SCROLL_SPLICE_LPW;
 static_assert(LANE_ACTIVE >= 1 && LANE_ACTIVE <= 64 && LANE_WAVES == 1, "k_splice_lanes: one wave, 1-64 slices");
